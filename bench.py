@@ -1,0 +1,146 @@
+#!/usr/bin/env python3
+"""Headline benchmark: PPO optimizer samples/s (whole node), 1v1-mid LSTM-512 policy, synthetic data.
+
+Metric (BASELINE.json): "PPO optimizer samples/sec (whole node) + actor steps/sec, 1v1-mid LSTM policy". A *sample*
+is one timestep of one sequence consumed by an optimizer step — the reference's ``steps per s``
+(optimizer.py:485-486: n_steps = sequences × seq_len). The baseline is the reference's published ~1000 steps/s
+(README.md:35).
+
+One timed *step* = one synchronous data-parallel PPO minibatch update on every rank: on-device minibatch gather from
+the HBM replay pool → forward (entity encoder, LSTM over seq_len, heads) → PPO clipped-surrogate + value + entropy
+loss → backward → RCCL all-reduce of the flat gradient → fused clip + Adam. Per-GPU work is fixed (weak scaling):
+each rank trains on ``--batch-size`` sequences of ``--seq-len`` steps.
+
+    python bench.py                                   # 1 GPU
+    python -m torch.distributed.run --nproc-per-node 8 ... bench.py --gpus 8
+
+Rank 0 prints ONE JSON line. The actor number (batched many-game inference steps/s) is measured *outside* the timed
+learner region and reported as an extra field.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+BASELINE_STEPS_PER_S = 1000.0   # reference README.md:35 (one optimizer)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=int(os.environ.get('WORLD_SIZE', 1)))
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--batch-size', type=int, default=8, help='sequences per GPU per step (reference deploy: 8)')
+    ap.add_argument('--seq-len', type=int, default=1400, help='steps per sequence (reference deploy: 1400)')
+    ap.add_argument('--model', default='lstm512')
+    ap.add_argument('--backend', default='auto', choices=['auto', 'fused', 'torch'])
+    ap.add_argument('--algo', default='ppo', choices=['ppo', 'vpg'])
+    ap.add_argument('--replay', type=int, default=0, help='sequences in the on-HBM replay pool (0 = 4x batch)')
+    ap.add_argument('--graph', type=int, default=-1, help='capture the step in a hipGraph (-1 = auto)')
+    ap.add_argument('--actor', type=int, default=1, help='also measure batched actor steps/s (untimed region)')
+    ap.add_argument('--actor-games', type=int, default=1024)
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    use_cuda = torch.cuda.is_available()
+    device = torch.device(f'cuda:{local}' if use_cuda else 'cpu')
+    if use_cuda:
+        torch.cuda.set_device(device)
+    if world > 1:
+        from dotaclient_amd.parallel.dist import init_distribution
+        init_distribution(device=device)
+
+    from dotaclient_amd.learner.engine import Learner, LossConfig
+    from dotaclient_amd.learner.synthetic import DeviceReplay
+    from dotaclient_amd.models.policy import Policy, get_config
+
+    torch.manual_seed(7 + rank)
+    cfg = get_config(args.model)
+    policy = Policy(cfg)
+    backend = args.backend
+    if backend == 'auto':
+        backend = 'fused' if use_cuda else 'torch'
+    learner = Learner(policy, LossConfig(algo=args.algo), device=device, backend=backend)
+    n_pool = args.replay or 4 * args.batch_size
+    replay = DeviceReplay(n_pool, args.seq_len, cfg.layout, cfg.hidden if cfg.rnn == 'lstm' else None, device,
+                          seed=1000 * rank)
+
+    def step():
+        batch = replay.sample(args.batch_size)
+        return learner.train_step(batch)
+
+    for _ in range(args.warmup):
+        m = step()
+    if use_cuda:
+        torch.cuda.synchronize()
+    loss_val = float(m['loss']) if args.warmup else float('nan')
+
+    if world > 1:
+        dist.barrier()
+    if use_cuda:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m = step()
+    if use_cuda:
+        torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    final_loss = float(m['loss'])
+
+    samples = args.batch_size * args.seq_len * world * args.steps
+    value = samples / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+
+    actor = None
+    if args.actor and rank == 0 and use_cuda:
+        try:
+            from dotaclient_amd.actor.batched import measure_actor_throughput
+            actor = measure_actor_throughput(policy, device, n_games=args.actor_games)
+        except Exception as e:  # the learner metric stands on its own
+            actor = {'error': repr(e)}
+
+    if rank == 0:
+        out = {
+            'metric': 'PPO optimizer samples/sec (whole node) + actor steps/sec, 1v1-mid LSTM policy',
+            'value': value,
+            'unit': 'samples/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': ms_per_step,
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': value / BASELINE_STEPS_PER_S,
+            'dtype': 'bf16',
+            'data': 'synthetic (on-HBM replay of synthetic 1v1-mid experience, random-init weights)',
+            'config': {'model': f'{args.model} ({cfg.rnn}-{cfg.hidden}, 1v1-mid entity encoder)',
+                       'global_batch': args.batch_size * world, 'seq_len': args.seq_len,
+                       'parallelism': f'dp{world}', 'algo': args.algo, 'backend': backend},
+            'loss_first': loss_val, 'loss_last': final_loss,
+            'actor': actor,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,95 @@
+"""Fused global-norm clip + Adam over the flat parameter buffer.
+
+Replaces the reference's ``clip_grad_norm_(0.5)`` + ``torch.optim.Adam(lr)`` (optimizer.py:281, 680-681) with one
+optimizer over :class:`~dotaclient_amd.parallel.dp.FlatParams`:
+
+* global L2 norm of the (already DP-averaged) flat gradient, clip coefficient ``min(1, max_norm / (norm + 1e-6))``
+  (torch's ``clip_grad_norm_`` formula);
+* Adam with torch's default betas/eps and *per-parameter* step counts;
+* parameters whose DP has-grad count is 0 are skipped entirely (no moment decay, no step increment) — the
+  sparse-parameter semantics of the reference's DP wrapper (distributed.py:40-42).
+
+On GPU this runs as two HIP kernels (``ops.adam_norm`` partial sums + ``ops.adam_update`` fused update, see
+ops/csrc/adam.hip); :meth:`FlatAdam.step_reference` is the torch implementation used on CPU and as the oracle.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ..parallel.dp import FlatParams
+
+
+class FlatAdam:
+    def __init__(self, flat: FlatParams, lr: float = 1e-4, betas=(0.9, 0.999), eps: float = 1e-8,
+                 max_grad_norm: Optional[float] = 0.5, use_kernels: Optional[bool] = None):
+        self.flat = flat
+        self.lr, self.betas, self.eps = lr, betas, eps
+        self.max_grad_norm = max_grad_norm
+        dev = flat.flat.device
+        self.exp_avg = torch.zeros_like(flat.flat)
+        self.exp_avg_sq = torch.zeros_like(flat.flat)
+        self.steps = torch.zeros(len(flat.params), device=dev, dtype=torch.float32)
+        self.last_grad_norm = torch.zeros((), device=dev, dtype=torch.float32)
+        if use_kernels is None:
+            use_kernels = dev.type == 'cuda'
+        self.use_kernels = use_kernels
+        if use_kernels:
+            from .. import ops
+            self._ops = ops.require()
+
+    # ------------------------------------------------------------------------------------------------
+    def step(self, counts: Optional[torch.Tensor] = None):
+        if counts is None:
+            counts = torch.ones(len(self.flat.params), device=self.flat.flat.device)
+        if self.use_kernels:
+            return self._step_kernels(counts)
+        return self.step_reference(counts)
+
+    def _step_kernels(self, counts):
+        b1, b2 = self.betas
+        max_norm = self.max_grad_norm if self.max_grad_norm is not None else -1.0
+        self._ops.adam_step(self.flat.flat, self.flat.grad, self.exp_avg, self.exp_avg_sq, self.flat.segment_ids,
+                            counts, self.steps, self.last_grad_norm, float(self.lr), float(b1), float(b2),
+                            float(self.eps), float(max_norm))
+        return self.last_grad_norm
+
+    @torch.no_grad()
+    def step_reference(self, counts):
+        b1, b2 = self.betas
+        g = self.flat.grad
+        norm = torch.linalg.vector_norm(g)
+        self.last_grad_norm.copy_(norm)
+        if self.max_grad_norm is not None:
+            coef = (self.max_grad_norm / (norm + 1e-6)).clamp(max=1.0)
+            g = g * coef
+        active_p = counts > 0
+        self.steps += active_p.to(self.steps.dtype)
+        seg = self.flat.segment_ids.long()
+        valid = seg >= 0
+        segc = seg.clamp_min(0)
+        active = active_p[segc] & valid
+        step = self.steps[segc]
+        m = torch.where(active, b1 * self.exp_avg + (1 - b1) * g, self.exp_avg)
+        v = torch.where(active, b2 * self.exp_avg_sq + (1 - b2) * g * g, self.exp_avg_sq)
+        self.exp_avg.copy_(m)
+        self.exp_avg_sq.copy_(v)
+        bc1 = 1 - torch.pow(torch.full_like(step, b1), step)
+        bc2 = 1 - torch.pow(torch.full_like(step, b2), step)
+        denom = (v.sqrt() / bc2.clamp_min(1e-30).sqrt()) + self.eps
+        upd = (self.lr / bc1.clamp_min(1e-30)) * m / denom
+        self.flat.flat.sub_(torch.where(active, upd, torch.zeros_like(upd)))
+        return norm
+
+    # ------------------------------------------------------------------------------------------------
+    def state_dict(self):
+        return {'exp_avg': self.exp_avg.cpu(), 'exp_avg_sq': self.exp_avg_sq.cpu(), 'steps': self.steps.cpu(),
+                'lr': self.lr, 'betas': self.betas, 'eps': self.eps, 'max_grad_norm': self.max_grad_norm}
+
+    def load_state_dict(self, d):
+        self.exp_avg.copy_(d['exp_avg'])
+        self.exp_avg_sq.copy_(d['exp_avg_sq'])
+        self.steps.copy_(d['steps'])
+        self.lr, self.betas, self.eps = d['lr'], tuple(d['betas']), d['eps']
+        self.max_grad_norm = d['max_grad_norm']

@@ -1,0 +1,109 @@
+// Fused global-norm gradient clip + Adam over one flat fp32 parameter buffer (gfx950).
+//
+// Replaces clip_grad_norm_(0.5) + torch.optim.Adam (reference optimizer.py:281, 680-681) with two launches over the
+// flat buffers of dotaclient_amd.parallel.dp.FlatParams:
+//   1. adam_norm_kernel   : per-block partial sums of g^2 (float4 loads, grid-stride), written to partials[blk];
+//                           block 0 also advances the per-parameter step counters for parameters with count > 0.
+//   2. adam_update_kernel : every block re-reduces the (<=1024) partials itself — no third launch, no cross-block
+//                           hand-off — then applies clip + Adam to its float4 groups. Parameters with DP has-grad
+//                           count 0 are skipped (sparse-param semantics, reference distributed.py:40-42).
+// Memory-bound: ~28 B/element moved. Offsets are 64-element aligned so a float4 group never straddles parameters.
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxBlocks = 1024;
+
+__global__ __launch_bounds__(kThreads) void adam_norm_kernel(const float4* __restrict__ g, int n4,
+                                                             float* __restrict__ partials,
+                                                             const float* __restrict__ counts,
+                                                             float* __restrict__ steps, int n_params) {
+  float acc = 0.f;
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < n4; i += gridDim.x * kThreads) {
+    float4 v = g[i];
+    acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+  }
+  __shared__ float red[kThreads / dca::kWave];
+  acc = dca::wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < kThreads / dca::kWave; ++w) s += red[w];
+    partials[blockIdx.x] = s;
+  }
+  if (blockIdx.x == 0) {
+    for (int p = threadIdx.x; p < n_params; p += kThreads)
+      if (counts[p] > 0.f) steps[p] += 1.f;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void adam_update_kernel(
+    float4* __restrict__ param, const float4* __restrict__ grad, float4* __restrict__ m, float4* __restrict__ v,
+    const int* __restrict__ seg, int n4, const float* __restrict__ partials, int nparts,
+    const float* __restrict__ counts, const float* __restrict__ steps, float* __restrict__ norm_out, float lr,
+    float b1, float b2, float eps, float max_norm) {
+  __shared__ float red[kThreads / dca::kWave];
+  __shared__ float s_coef;
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += kThreads) acc += partials[i];
+  acc = dca::wave_sum(acc);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < kThreads / dca::kWave; ++w) s += red[w];
+    const float norm = sqrtf(s);
+    float coef = 1.f;
+    if (max_norm > 0.f) coef = fminf(1.f, max_norm / (norm + 1e-6f));
+    s_coef = coef;
+    if (blockIdx.x == 0) *norm_out = norm;
+  }
+  __syncthreads();
+  const float coef = s_coef;
+  for (int i = blockIdx.x * kThreads + threadIdx.x; i < n4; i += gridDim.x * kThreads) {
+    const int s = seg[i * 4];
+    if (s < 0) continue;
+    if (!(counts[s] > 0.f)) continue;
+    const float t = steps[s];
+    const float bc1 = 1.f - powf(b1, t);
+    const float bc2s = sqrtf(1.f - powf(b2, t));
+    const float step_size = lr / bc1;
+    float4 gg = grad[i], mm = m[i], vv = v[i], pp = param[i];
+#define DCA_ADAM_LANE(c)                                          \
+    {                                                             \
+      const float gc = gg.c * coef;                               \
+      mm.c = b1 * mm.c + (1.f - b1) * gc;                         \
+      vv.c = b2 * vv.c + (1.f - b2) * gc * gc;                    \
+      pp.c -= step_size * mm.c / (sqrtf(vv.c) / bc2s + eps);      \
+    }
+    DCA_ADAM_LANE(x) DCA_ADAM_LANE(y) DCA_ADAM_LANE(z) DCA_ADAM_LANE(w)
+#undef DCA_ADAM_LANE
+    m[i] = mm;
+    v[i] = vv;
+    param[i] = pp;
+  }
+}
+
+}  // namespace
+
+// n must be a multiple of 4 (FlatParams pads every parameter to 64 elements). `partials` holds >= kMaxBlocks floats.
+extern "C" hipError_t dca_adam_step(float* param, const float* grad, float* m, float* v, const int* seg, int64_t n,
+                                    const float* counts, float* steps, int n_params, float* partials,
+                                    float* norm_out, float lr, float b1, float b2, float eps, float max_norm,
+                                    hipStream_t stream) {
+  const int n4 = (int)(n / 4);
+  int blocks = (n4 + kThreads - 1) / kThreads;
+  blocks = blocks < 1 ? 1 : (blocks > kMaxBlocks ? kMaxBlocks : blocks);
+  adam_norm_kernel<<<blocks, kThreads, 0, stream>>>(reinterpret_cast<const float4*>(grad), n4, partials, counts,
+                                                    steps, n_params);
+  DCA_CHECK_LAUNCH();
+  adam_update_kernel<<<blocks, kThreads, 0, stream>>>(
+      reinterpret_cast<float4*>(param), reinterpret_cast<const float4*>(grad), reinterpret_cast<float4*>(m),
+      reinterpret_cast<float4*>(v), seg, n4, partials, blocks, counts, steps, norm_out, lr, b1, b2, eps, max_norm);
+  DCA_CHECK_LAUNCH();
+  return hipSuccess;
+}

@@ -1,0 +1,65 @@
+"""FlatAdam (fused clip + Adam over the flat buffer) vs torch.optim.Adam + clip_grad_norm_ (reference
+optimizer.py:281, 680-681)."""
+import pytest
+import torch
+
+from dotaclient_amd.learner.optim import FlatAdam
+from dotaclient_amd.models.policy import Policy
+from dotaclient_amd.parallel.dp import FlatParams
+
+
+def _grads(model, seed):
+    g = torch.Generator().manual_seed(seed)
+    return [torch.randn(p.shape, generator=g) * (0.5 + i % 3) for i, p in enumerate(model.parameters())]
+
+
+def _run_reference(model, grads_seq, lr, max_norm, skip=()):
+    opt = torch.optim.Adam(model.parameters(), lr=lr)
+    params = list(model.parameters())
+    for grads in grads_seq:
+        for i, (p, g) in enumerate(zip(params, grads)):
+            p.grad = None if i in skip else g.clone()
+        torch.nn.utils.clip_grad_norm_([p for p in params if p.grad is not None], max_norm)
+        opt.step()
+
+
+def _run_flat(model, grads_seq, lr, max_norm, skip=(), device='cpu', kernels=False):
+    model = model.to(device)
+    flat = FlatParams(model, device=device)
+    opt = FlatAdam(flat, lr=lr, max_grad_norm=max_norm, use_kernels=kernels)
+    counts = torch.ones(len(flat.params), device=device)
+    for i in skip:
+        counts[i] = 0
+    for grads in grads_seq:
+        flat.zero_grad()
+        for i, (p, g) in enumerate(zip(flat.params, grads)):
+            if i not in skip:
+                p.grad.copy_(g.to(device))
+        opt.step(counts)
+    return model
+
+
+@pytest.mark.parametrize('skip', [(), (3, 28)])
+def test_flat_adam_matches_torch(skip):
+    torch.manual_seed(0)
+    a = Policy('compat')
+    b = Policy('compat')
+    b.load_state_dict(a.state_dict())
+    seq = [_grads(a, s) for s in range(4)]
+    _run_reference(a, seq, 1e-3, 0.5, skip)
+    _run_flat(b, seq, 1e-3, 0.5, skip)
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6, msg=n)
+
+
+@pytest.mark.gpu
+def test_adam_kernel_matches_reference(gpu_ops):
+    torch.manual_seed(0)
+    a = Policy('lstm512')
+    b = Policy('lstm512')
+    b.load_state_dict(a.state_dict())
+    seq = [_grads(a, s) for s in range(3)]
+    _run_flat(a, seq, 1e-3, 0.5, skip=(5,))
+    b = _run_flat(b, seq, 1e-3, 0.5, skip=(5,), device='cuda', kernels=True)
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb.cpu(), rtol=1e-5, atol=2e-6, msg=n)
