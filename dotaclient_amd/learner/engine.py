@@ -64,7 +64,7 @@ class Learner:
 
     # ------------------------------------------------------------------------------------------------
     def _autocast(self):
-        if self.backend == 'torch' and self.device.type == 'cuda':
+        if self.backend == 'torch' and self.device.type == 'cuda':   # 'torch-fp32' = fp32 oracle
             return torch.autocast('cuda', dtype=torch.bfloat16)
         return contextlib.nullcontext()
 

@@ -97,11 +97,42 @@ std::vector<torch::Tensor> lstm_bwd(torch::Tensor dhs, torch::Tensor gates, torc
   return {dgates, dh0, dc0};
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// Fused heads + loss. Returns (dz (N,ldz) f32, dtl (N,U) f32, partials (nblk,16) f32, logp (N) f32).
+std::vector<torch::Tensor> heads_loss(torch::Tensor z, torch::Tensor emb, torch::Tensor act, torch::Tensor msk,
+                                      torch::Tensor adv, torch::Tensor ret, torch::Tensor logp_old,
+                                      torch::Tensor nret, torch::Tensor norms, int64_t algo, bool compat_value_bug,
+                                      int64_t S_bug, int64_t B_bug, double clip_eps, double ent_coef,
+                                      double vf_coef) {
+  CHECK_F32(z); CHECK_BF16(emb); CHECK_U8(act); CHECK_U8(msk); CHECK_F32(adv); CHECK_F32(ret);
+  CHECK_F32(logp_old); CHECK_F32(nret); CHECK_F32(norms);
+  TORCH_CHECK(z.dim() == 2 && emb.dim() == 3 && emb.size(2) == 128, "z (N,ldz), emb (N,U,128)");
+  const int N = z.size(0), ldz = z.size(1), U = emb.size(1);
+  TORCH_CHECK(emb.size(0) == N && act.size(0) == N && msk.size(0) == N, "row count mismatch");
+  TORCH_CHECK(act.size(1) == 21 + U && msk.size(1) == 21 + U, "actions/masks must be (N, 21+U)");
+  TORCH_CHECK(adv.numel() == N && ret.numel() == N && logp_old.numel() == N && nret.numel() == N, "per-row inputs");
+  TORCH_CHECK(norms.numel() >= 8, "norms must hold 8 floats");
+  TORCH_CHECK(ldz % 4 == 0 && ldz >= 150 && U <= 64, "ldz must be a multiple of 4 and >= 150; U <= 64");
+  auto dz = torch::empty_like(z);
+  auto dtl = torch::empty({N, U}, z.options());
+  const int nb = dca_heads_loss_nblocks(N);
+  auto part = torch::empty({nb, 16}, z.options());
+  auto logp = torch::empty({N}, z.options());
+  hip_check(dca_heads_loss(ptr<float>(z), ldz, ptr<short>(emb), ptr<unsigned char>(act), ptr<unsigned char>(msk),
+                           21 + U, ptr<float>(adv), ptr<float>(ret), ptr<float>(logp_old), ptr<float>(nret),
+                           ptr<float>(norms), ptr<float>(dz), ptr<float>(dtl), ptr<float>(part), ptr<float>(logp), N,
+                           U, (int)algo, compat_value_bug ? 1 : 0, (int)S_bug, (int)B_bug, (float)clip_eps,
+                           (float)ent_coef, (float)vf_coef, cur_stream()),
+            "dca_heads_loss");
+  return {dz, dtl, part, logp};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "dotaclient_amd gfx950 HIP kernels";
   m.def("adam_step", &adam_step, "fused global-norm clip + Adam over a flat fp32 buffer");
   m.def("lstm_fwd", &lstm_fwd, "persistent LSTM forward recurrence (granule all-gather)");
+  m.def("heads_loss", &heads_loss, "fused heads + pointer + masked log-softmax + PPO/VPG loss + gradients");
   m.def("lstm_bwd", &lstm_bwd, "persistent LSTM backward recurrence (granule reduce-scatter)");
 }

@@ -1,0 +1,228 @@
+// Fused action heads + pointer attention + masked log-softmax + PPO/VPG loss + analytic gradients (gfx950).
+//
+// One wave per timestep row. Replaces, for every row, the reference's chain (policy.py:148-158, 171-180;
+// optimizer.py:602-672): pointer logits q·embᵀ, four masked log-softmaxes, selection by the one-hot action,
+// clipped surrogate / VPG term, per-head masked entropy and the value loss — and writes the gradient of the
+// batch loss w.r.t. every head input in the same pass (no autograd graph, no masked_select, no host sync):
+//
+//   z   (N, ldz) f32 : [ q (128) | enum (3) | x (9) | y (9) | value (1) | pad ]  (output of ONE heads GEMM)
+//   emb (N, U, 128) bf16 : unit embeddings (pointer keys)
+//   dz  (N, ldz) f32 : ∂L/∂z   (dq in cols 0..127, d logits, dV)  → feeds the heads GEMM backward
+//   dtl (N, U)  f32  : ∂L/∂(target logits)                         → ∂L/∂emb = dtl ⊗ q (encoder backward)
+//   part(nblk, 16)   : per-block partial sums of the loss terms / metrics (reduced on the host side)
+//
+// The batch normalisers (valid steps, selections per head) depend only on the experience, so they are computed
+// before this kernel and passed in `norms`; every row's gradient is then final in one pass.
+//   norms[0] = 1/n_valid  norms[1] = 1/total_selections  norms[2..5] = 1/n_sel[head] (0 if none)
+//   norms[6] = Σ G_last (VPG compat value-bug term)
+#include "common.h"
+
+namespace {
+
+constexpr int kRowsPerBlock = 4;
+constexpr int kQ = 128;
+constexpr int kNPart = 16;
+
+struct Params {
+  const float* z; int ldz;
+  const short* emb;
+  const unsigned char* act; const unsigned char* msk; int A;
+  const float* adv; const float* ret; const float* logp_old; const float* nret;
+  const float* norms;
+  float* dz; float* dtl; float* part; float* logp_out;
+  int N, U, algo, compat_value_bug, S_bug, B_bug;
+  float clip_eps, ent_coef, vf_coef;
+};
+
+// masked log-softmax of one head held one entry per lane (lane < W); returns logp for the lane's entry.
+__device__ __forceinline__ void head_lsm(float logit, bool m, int lane, int W, float& logp, float& p) {
+  const bool in = lane < W;
+  const float v = (in && m) ? logit : -INFINITY;
+  float mx = dca::wave_max(v);
+  const bool any = mx > -INFINITY;
+  if (!any) mx = 0.f;
+  const float e = (in && m) ? __expf(logit - mx) : 0.f;
+  float s = dca::wave_sum(e);
+  if (!(s > 0.f)) s = 1.f;
+  logp = logit - mx - __logf(s);
+  p = (in && m) ? __expf(logp) : 0.f;
+}
+
+__global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int n = blockIdx.x * kRowsPerBlock + wv;
+  __shared__ float s_tl[kRowsPerBlock][64];
+  __shared__ float s_dtl[kRowsPerBlock][64];
+  __shared__ float s_part[kRowsPerBlock][kNPart];
+  float acc[kNPart];
+#pragma unroll
+  for (int i = 0; i < kNPart; ++i) acc[i] = 0.f;
+
+  if (n < P.N) {
+    const int U = P.U;
+    const float* zr = P.z + (size_t)n * P.ldz;
+    // ---- q slice for this lane (8 consecutive features) and pointer logits, 4 units per wave-instruction
+    const int ks = lane & 15, ug = lane >> 4;
+    float q8[8];
+    {
+      const float4 a = *reinterpret_cast<const float4*>(zr + 8 * ks);
+      const float4 b = *reinterpret_cast<const float4*>(zr + 8 * ks + 4);
+      q8[0] = a.x; q8[1] = a.y; q8[2] = a.z; q8[3] = a.w; q8[4] = b.x; q8[5] = b.y; q8[6] = b.z; q8[7] = b.w;
+    }
+    constexpr int kMaxIt = 16;   // U ≤ 64
+    dca::bf16x8 e8[kMaxIt];
+    const int nit = (U + 3) >> 2;
+    const short* er = P.emb + (size_t)n * U * kQ;
+#pragma unroll
+    for (int it = 0; it < kMaxIt; ++it) {
+      if (it < nit) {
+        const int u = it * 4 + ug;
+        dca::bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (u < U) v = *reinterpret_cast<const dca::bf16x8*>(er + (size_t)u * kQ + 8 * ks);
+        e8[it] = v;
+        float d = 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) d += q8[j] * dca::bf2f(v[j]);
+        d = dca::group_sum<16>(d);
+        if (ks == 0 && u < U) s_tl[wv][u] = d;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // ---- the four heads: (offset in flat action vector, width, source)
+    const unsigned char* ar = P.act + (size_t)n * P.A;
+    const unsigned char* mr = P.msk + (size_t)n * P.A;
+    const int hoff[4] = {0, 3, 12, 21};
+    const int hw[4] = {3, 9, 9, U};
+    float logp[4], pr[4], a[4];
+    bool mk[4];
+    float sel = 0.f;
+    int nsel = 0;
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const bool in = lane < hw[h];
+      float lg = 0.f;
+      if (in) lg = (h == 3) ? s_tl[wv][lane] : zr[kQ + hoff[h] + lane];
+      mk[h] = in && mr[hoff[h] + lane];
+      a[h] = (in && ar[hoff[h] + lane]) ? 1.f : 0.f;
+      head_lsm(lg, mk[h], lane, hw[h], logp[h], pr[h]);
+      if (!in) logp[h] = 0.f;
+      const float sh = dca::wave_sum(a[h] * logp[h]);
+      sel += sh;
+      const int ns = __popcll(__ballot(a[h] > 0.f));
+      nsel += ns;
+      // entropy of this head over valid entries: -Σ m p logp
+      acc[2 + h] += -dca::wave_sum(mk[h] ? pr[h] * logp[h] : 0.f);
+    }
+    const float valid = nsel > 0 ? 1.f : 0.f;
+    const float V = zr[kQ + 21];
+    const float R = P.ret[n];
+    float g_sel = 0.f, dV = 0.f;
+    if (P.algo == 0) {   // PPO
+      const float A = P.adv[n];
+      const float lr = sel - P.logp_old[n];
+      const float r = __expf(lr);
+      const float s1 = r * A;
+      const float rc = fminf(fmaxf(r, 1.f - P.clip_eps), 1.f + P.clip_eps);
+      const float s2 = rc * A;
+      acc[0] += valid * fminf(s1, s2);
+      const bool clipped = (A > 0.f && r > 1.f + P.clip_eps) || (A < 0.f && r < 1.f - P.clip_eps);
+      g_sel = clipped ? 0.f : -valid * A * r * P.norms[0];
+      acc[1] += valid * (V - R) * (V - R);
+      dV = P.vf_coef * 2.f * (V - R) * valid * P.norms[0];
+      acc[6] += valid * (-lr);
+      acc[7] += valid * (fabsf(r - 1.f) > P.clip_eps ? 1.f : 0.f);
+      acc[8] += valid * A;
+    } else {             // VPG (reference objective)
+      const float nr = P.nret[n];
+      acc[0] += -sel * nr;
+      g_sel = -nr * P.norms[1];
+      acc[1] += (V - R) * (V - R);
+      acc[9] += V;
+      acc[10] += V * V;
+      acc[8] += V - R;
+      if (P.vf_coef > 0.f) {
+        if (P.compat_value_bug) {
+          const float S = (float)P.S_bug, Bq = (float)P.B_bug;
+          dV = P.vf_coef * 2.f * (S * V - P.norms[6]) / (Bq * S * S);
+        } else {
+          dV = P.vf_coef * 2.f * (V - R) / (float)P.N;
+        }
+      }
+    }
+    acc[11] += valid;
+    if (P.logp_out) if (lane == 0) P.logp_out[n] = sel;
+    // ---- gradients through the four log-softmaxes
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const bool in = lane < hw[h];
+      float dlp = g_sel * a[h];
+      if (P.ent_coef > 0.f) dlp += P.ent_coef * P.norms[2 + h] * (mk[h] ? pr[h] * (1.f + logp[h]) : 0.f);
+      if (!in) dlp = 0.f;
+      const float sd = dca::wave_sum(dlp);
+      const float dl = dlp - (mk[h] ? pr[h] : 0.f) * sd;
+      if (in) {
+        if (h == 3) {
+          s_dtl[wv][lane] = dl;
+          P.dtl[(size_t)n * U + lane] = dl;
+        } else {
+          P.dz[(size_t)n * P.ldz + kQ + hoff[h] + lane] = dl;
+        }
+      }
+    }
+    if (lane == 0) P.dz[(size_t)n * P.ldz + kQ + 21] = dV;
+    if (lane < P.ldz - kQ - 22) P.dz[(size_t)n * P.ldz + kQ + 22 + lane] = 0.f;
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    // ---- dq = Σ_u dtl[u] · emb[u]
+    float dq[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int it = 0; it < kMaxIt; ++it) {
+      if (it < nit) {
+        const int u = it * 4 + ug;
+        const float g = (u < U) ? s_dtl[wv][u] : 0.f;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) dq[j] += g * dca::bf2f(e8[it][j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      dq[j] += __shfl_xor(dq[j], 16, 64);
+      dq[j] += __shfl_xor(dq[j], 32, 64);
+    }
+    if (ug == 0) {
+      float4* o = reinterpret_cast<float4*>(P.dz + (size_t)n * P.ldz + 8 * ks);
+      o[0] = make_float4(dq[0], dq[1], dq[2], dq[3]);
+      o[1] = make_float4(dq[4], dq[5], dq[6], dq[7]);
+    }
+  }
+  // ---- block partials
+  if (lane == 0) {
+#pragma unroll
+    for (int i = 0; i < kNPart; ++i) s_part[wv][i] = acc[i];
+  }
+  __syncthreads();
+  if (tid < kNPart) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < kRowsPerBlock; ++w) s += s_part[w][tid];
+    P.part[(size_t)blockIdx.x * kNPart + tid] = s;
+  }
+}
+
+}  // namespace
+
+extern "C" int dca_heads_loss_nblocks(int N) { return (N + kRowsPerBlock - 1) / kRowsPerBlock; }
+
+extern "C" hipError_t dca_heads_loss(const float* z, int ldz, const short* emb, const unsigned char* act,
+                                     const unsigned char* msk, int A, const float* adv, const float* ret,
+                                     const float* logp_old, const float* nret, const float* norms, float* dz,
+                                     float* dtl, float* part, float* logp_out, int N, int U, int algo,
+                                     int compat_value_bug, int S_bug, int B_bug, float clip_eps, float ent_coef,
+                                     float vf_coef, hipStream_t st) {
+  if (U > 64 || U < 1 || ldz < kQ + 22 || A != 21 + U) return hipErrorInvalidValue;
+  Params P{z, ldz, emb, act, msk, A, adv, ret, logp_old, nret, norms, dz, dtl, part, logp_out, N, U, algo,
+           compat_value_bug, S_bug, B_bug, clip_eps, ent_coef, vf_coef};
+  heads_loss_kernel<<<dca_heads_loss_nblocks(N), 256, 0, st>>>(P);
+  return hipGetLastError();
+}

@@ -17,4 +17,11 @@ hipError_t dca_lstm_bwd(const float* dhs, const float* gates, const float* cs, c
                         const float* dcn, const short* whh, float* dgates, float* dh0, float* dc0,
                         unsigned long long* ring, unsigned* err, int B, int S, int H, hipStream_t st);
 
+int dca_heads_loss_nblocks(int N);
+hipError_t dca_heads_loss(const float* z, int ldz, const short* emb, const unsigned char* act, const unsigned char* msk,
+                          int A, const float* adv, const float* ret, const float* logp_old, const float* nret,
+                          const float* norms, float* dz, float* dtl, float* part, float* logp_out, int N, int U,
+                          int algo, int compat_value_bug, int S_bug, int B_bug, float clip_eps, float ent_coef,
+                          float vf_coef, hipStream_t st);
+
 }  // extern "C"
