@@ -1,0 +1,154 @@
+"""Experience record and its wire codecs.
+
+The reference ships each rollout as ``pickle.dumps(dict)`` on the ``experience`` queue (agent.py:387-409) with keys
+``game_id, team_id, player_id, states{7}, actions{4}, masks{4}, rewards (T,9) f64, weight_version, canvas``
+(SURVEY §2.8.4). :class:`Rollout` holds the same content in packed form (one ``(T,U,10)`` unit tensor, flat
+``(T, 21+U)`` action/mask vectors) plus the north-star extensions the PPO/LSTM learner needs:
+
+* ``logp`` (T,) — joint log-prob of the sampled action under the behaviour policy (PPO ratio),
+* ``values`` (T,) — V(s_t) of the behaviour policy (GAE),
+* ``hidden0`` (2, H) — LSTM (h, c) at the first step of the rollout (R2D2-style stored state),
+* ``bootstrap_value`` / ``done`` — how the rollout ended (truncated by ``rollout_size`` or terminal).
+
+Codecs:
+
+* :func:`encode` / :func:`decode` — a compact binary format (``DCX1`` magic, JSON header, raw little-endian arrays);
+  zero-copy ``np.frombuffer`` on decode. ~4× smaller/faster than pickling torch tensors.
+* :meth:`Rollout.to_reference_dict` / :meth:`Rollout.from_reference_dict` — exact reference message layout, so a
+  reference agent's pickled message can be ingested and ours can be read by the reference optimizer.
+  Only trusted in-cluster producers are unpickled (:func:`decode_any`), mirroring the reference's trust model.
+"""
+from __future__ import annotations
+
+import io
+import json
+import pickle
+import struct
+from dataclasses import dataclass, field
+from typing import Dict, Optional, Tuple
+
+import numpy as np
+
+from ..constants import INPUT_KEYS, LAYOUT_1V1, N_MOVE_ENUMS, REWARD_KEYS, UNIT_KEYS, UnitLayout
+
+MAGIC = b'DCX1'
+
+
+@dataclass
+class Rollout:
+    game_id: str
+    team_id: int
+    player_id: int
+    env: np.ndarray                      # (T, 3) f32
+    units: np.ndarray                    # (T, U, 10) f32
+    actions: np.ndarray                  # (T, 21+U) u8 one-hot per sampled head
+    masks: np.ndarray                    # (T, 21+U) u8 selected-heads mask
+    rewards: np.ndarray                  # (T, 9) f64 in REWARD_KEYS order
+    weight_version: int
+    canvas: Optional[np.ndarray] = None  # (256, 256, 3) u8
+    logp: Optional[np.ndarray] = None
+    values: Optional[np.ndarray] = None
+    hidden0: Optional[np.ndarray] = None
+    bootstrap_value: float = 0.0
+    done: bool = True
+    layout: Tuple[int, ...] = field(default_factory=lambda: LAYOUT_1V1.counts)
+
+    @property
+    def length(self) -> int:
+        return int(self.rewards.shape[0])
+
+    def unit_layout(self) -> UnitLayout:
+        return UnitLayout(*self.layout)
+
+    # -------------------------------------------------------------------------------------------------
+    def to_reference_dict(self) -> Dict:
+        """Reference message layout (agent.py:397-407), torch tensors as the reference's pickles carry."""
+        import torch
+        lay = self.unit_layout()
+        states = {'env': torch.from_numpy(np.ascontiguousarray(self.env))}
+        for k, sl in lay.slices().items():
+            states[k] = torch.from_numpy(np.ascontiguousarray(self.units[:, sl]))
+        heads = {}
+        acc = 0
+        for k, n in lay.action_counts().items():
+            heads[k] = (acc, n)
+            acc += n
+        actions = {k: torch.from_numpy(np.ascontiguousarray(self.actions[:, o:o + n])) for k, (o, n) in heads.items()}
+        masks = {k: torch.from_numpy(np.ascontiguousarray(self.masks[:, o:o + n])) for k, (o, n) in heads.items()}
+        return {'game_id': self.game_id, 'team_id': self.team_id, 'player_id': self.player_id, 'states': states,
+                'actions': actions, 'masks': masks, 'rewards': self.rewards, 'weight_version': self.weight_version,
+                'canvas': self.canvas}
+
+    @classmethod
+    def from_reference_dict(cls, d: Dict) -> 'Rollout':
+        def npy(x):
+            return x.numpy() if hasattr(x, 'numpy') else np.asarray(x)
+        states = d['states']
+        counts = tuple(int(npy(states[k]).shape[1]) for k in UNIT_KEYS)
+        units = np.concatenate([npy(states[k]) for k in UNIT_KEYS], axis=1).astype(np.float32)
+        order = ['enum', 'x', 'y', 'target_unit']
+        actions = np.concatenate([npy(d['actions'][k]) for k in order], axis=1).astype(np.uint8)
+        masks = np.concatenate([npy(d['masks'][k]) for k in order], axis=1).astype(np.uint8)
+        return cls(game_id=str(d['game_id']), team_id=int(d['team_id']), player_id=int(d['player_id']),
+                   env=npy(states['env']).astype(np.float32), units=units, actions=actions, masks=masks,
+                   rewards=np.asarray(d['rewards'], dtype=np.float64), weight_version=int(d['weight_version']),
+                   canvas=None if d.get('canvas') is None else np.asarray(d['canvas'], dtype=np.uint8),
+                   layout=counts)
+
+
+_ARRAYS = ['env', 'units', 'actions', 'masks', 'rewards', 'canvas', 'logp', 'values', 'hidden0']
+
+
+def encode(r: Rollout) -> bytes:
+    header = {'game_id': r.game_id, 'team_id': r.team_id, 'player_id': r.player_id,
+              'weight_version': r.weight_version, 'bootstrap_value': float(r.bootstrap_value), 'done': bool(r.done),
+              'layout': list(r.layout), 'arrays': []}
+    blobs = []
+    off = 0
+    for name in _ARRAYS:
+        a = getattr(r, name)
+        if a is None:
+            continue
+        a = np.ascontiguousarray(a)
+        b = a.tobytes()
+        header['arrays'].append([name, a.dtype.str, list(a.shape), off, len(b)])
+        blobs.append(b)
+        off += len(b)
+    h = json.dumps(header, separators=(',', ':')).encode()
+    return b''.join([MAGIC, struct.pack('<I', len(h)), h] + blobs)
+
+
+def decode(buf: bytes) -> Rollout:
+    if buf[:4] != MAGIC:
+        raise ValueError('not a DCX1 experience message')
+    (hl,) = struct.unpack_from('<I', buf, 4)
+    header = json.loads(bytes(buf[8:8 + hl]))
+    base = 8 + hl
+    arrays = {}
+    mv = memoryview(buf)
+    for name, dt, shape, off, n in header['arrays']:
+        arrays[name] = np.frombuffer(mv[base + off: base + off + n], dtype=np.dtype(dt)).reshape(shape)
+    return Rollout(game_id=header['game_id'], team_id=header['team_id'], player_id=header['player_id'],
+                   weight_version=header['weight_version'], bootstrap_value=header['bootstrap_value'],
+                   done=header['done'], layout=tuple(header['layout']), **{k: arrays.get(k) for k in _ARRAYS})
+
+
+def decode_any(buf: bytes) -> Rollout:
+    """DCX1 binary, or a reference agent's pickled dict (trusted in-cluster producer only)."""
+    if buf[:4] == MAGIC:
+        return decode(buf)
+    return Rollout.from_reference_dict(pickle.loads(buf))
+
+
+# ---- model messages -------------------------------------------------------------------------------------------
+def encode_state_dict(state_dict) -> bytes:
+    """``torch.save(state_dict)`` bytes — the reference's model message / checkpoint format (optimizer.py:699-703)."""
+    import torch
+    buf = io.BytesIO()
+    torch.save(state_dict, buf)
+    return buf.getvalue()
+
+
+def decode_state_dict(b: bytes):
+    import torch
+    return torch.load(io.BytesIO(b), map_location='cpu', weights_only=True)

