@@ -49,7 +49,7 @@ void adam_step(torch::Tensor param, torch::Tensor grad, torch::Tensor m, torch::
 // ------------------------------------------------------------------------------------------------------------
 // Persistent LSTM recurrence. xp (B,S,4H) f32, whh (4H,H) bf16, h0/c0 (B,H) f32, err (1) int32 device flag.
 std::vector<torch::Tensor> lstm_fwd(torch::Tensor xp, torch::Tensor whh, torch::Tensor h0, torch::Tensor c0,
-                                    torch::Tensor err, bool want_f32_h) {
+                                    torch::Tensor err, bool want_f32_h, int64_t local) {
   CHECK_F32(xp); CHECK_BF16(whh); CHECK_F32(h0); CHECK_F32(c0); CHECK_I32(err);
   TORCH_CHECK(xp.dim() == 3, "xp must be (B,S,4H)");
   const int B = xp.size(0), S = xp.size(1), G4 = xp.size(2), H = G4 / 4;
@@ -67,7 +67,8 @@ std::vector<torch::Tensor> lstm_fwd(torch::Tensor xp, torch::Tensor whh, torch::
   auto ring = torch::empty({(int64_t)dca_lstm_ring_elems(B, H, 0)}, f32.dtype(at::kLong));
   hip_check(dca_lstm_fwd(ptr<float>(xp), ptr<short>(whh), ptr<float>(h0), ptr<float>(c0), ptr<short>(hs),
                          want_f32_h ? ptr<float>(hsf) : nullptr, ptr<float>(cs), ptr<float>(gates), ptr<float>(hn),
-                         ptr<float>(cn), ptr<unsigned long long>(ring), ptr<unsigned>(err), B, S, H, cur_stream()),
+                         ptr<float>(cn), ptr<unsigned long long>(ring), ptr<unsigned>(err), B, S, H, (int)local,
+                         cur_stream()),
             "dca_lstm_fwd");
   return {hs, want_f32_h ? hsf : hs, cs, gates, hn, cn};
 }

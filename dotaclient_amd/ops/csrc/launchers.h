@@ -12,7 +12,7 @@ hipError_t dca_adam_step(float* param, const float* grad, float* m, float* v, co
 size_t dca_lstm_ring_elems(int B, int H, int backward);
 hipError_t dca_lstm_fwd(const float* xp, const short* whh, const float* h0, const float* c0, short* hs, float* hsf,
                         float* cs, float* gates, float* hn, float* cn, unsigned long long* ring, unsigned* err, int B,
-                        int S, int H, hipStream_t st);
+                        int S, int H, int local, hipStream_t st);
 hipError_t dca_lstm_bwd(const float* dhs, const float* gates, const float* cs, const float* c0, const float* dhn,
                         const float* dcn, const short* whh, float* dgates, float* dh0, float* dc0,
                         unsigned long long* ring, unsigned* err, int B, int S, int H, hipStream_t st);

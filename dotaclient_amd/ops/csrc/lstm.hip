@@ -43,6 +43,11 @@ __device__ __forceinline__ unsigned long long ld_granule(const unsigned long lon
 __device__ __forceinline__ void st_granule(unsigned long long* p, unsigned long long v) {
   __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// XCD-local hand-off: a plain store keeps the line in the producer XCD's L2, where same-XCD consumers' L1-bypassing
+// (agent-scope) loads hit it. Only valid when every workgroup of the launch sits on ONE XCD (see LOCAL below).
+__device__ __forceinline__ void st_granule_local(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
 __device__ __forceinline__ unsigned ld_err(const unsigned* p) {
   return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -60,7 +65,7 @@ __device__ __forceinline__ bool spin_fail(unsigned& spins, unsigned* err, unsign
       return true;
     }
   }
-  __builtin_amdgcn_s_sleep(1);
+  if (spins > 64) __builtin_amdgcn_s_sleep(1);
   return false;
 }
 
@@ -76,7 +81,7 @@ __device__ __forceinline__ bool spin_fail(unsigned& spins, unsigned* err, unsign
 // gates  (B, S, 4H) f32  out: activated i, f, g, o
 // hn,cn  (B, H)     f32  out: final state
 // ring   (2, B, H/2) u64 granules (zeroed)
-template <int MT, int KS>
+template <int MT, int KS, bool LOCAL>
 __global__ __launch_bounds__(kThreads) void lstm_fwd_kernel(const float* __restrict__ xp, const short* __restrict__ whh,
                                                             const float* __restrict__ h0, const float* __restrict__ c0,
                                                             short* __restrict__ hs, float* __restrict__ hsf,
@@ -86,7 +91,9 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_kernel(const float* __restr
   constexpr int H = 128 * KS;           // each of the 4 waves owns K/4 = 32·KS of the reduction
   constexpr int G4 = 4 * H;
   constexpr int HP = H / 2;             // granules per batch row
-  const int w = blockIdx.x;
+  // LOCAL: the grid is 8× oversized and only blocks ≡ 0 (mod 8) — which the dispatcher deals to one XCD — work.
+  if (LOCAL && (blockIdx.x & 7) != 0) return;
+  const int w = LOCAL ? (blockIdx.x >> 3) : blockIdx.x;
   const int j0 = w * kUw;
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int lrow = lane & 15, lkg = lane >> 4;
@@ -234,8 +241,9 @@ __global__ __launch_bounds__(kThreads) void lstm_fwd_kernel(const float* __restr
         const int b = p >> 3, jj = p & 7;
         const unsigned pl = (unsigned)(unsigned short)dca::f2bf(hv) |
                             ((unsigned)(unsigned short)dca::f2bf(hnext) << 16);
-        st_granule(ring + (size_t)(t & 1) * B * HP + (size_t)b * HP + ((j0 + jj) >> 1),
-                   ((unsigned long long)(unsigned)(t + 1) << 32) | pl);
+        unsigned long long* gptr = ring + (size_t)(t & 1) * B * HP + (size_t)b * HP + ((j0 + jj) >> 1);
+        const unsigned long long gv = ((unsigned long long)(unsigned)(t + 1) << 32) | pl;
+        if (LOCAL) st_granule_local(gptr, gv); else st_granule(gptr, gv);
       }
     }
     __syncthreads();   // red[] is rewritten next step
@@ -421,11 +429,16 @@ __global__ __launch_bounds__(kThreads) void lstm_bwd_kernel(const float* __restr
 template <int MT, int KS>
 hipError_t launch_fwd(const float* xp, const short* whh, const float* h0, const float* c0, short* hs, float* hsf,
                       float* cs, float* gates, float* hn, float* cn, unsigned long long* ring, unsigned* err, int B,
-                      int S, hipStream_t st) {
+                      int S, int local, hipStream_t st) {
   constexpr int H = 128 * KS;
   hipError_t e = hipMemsetAsync(ring, 0, sizeof(unsigned long long) * 2 * B * (H / 2), st);
   if (e != hipSuccess) return e;
-  lstm_fwd_kernel<MT, KS><<<H / kUw, kThreads, 0, st>>>(xp, whh, h0, c0, hs, hsf, cs, gates, hn, cn, ring, err, B, S);
+  if (local)
+    lstm_fwd_kernel<MT, KS, true><<<8 * (H / kUw), kThreads, 0, st>>>(xp, whh, h0, c0, hs, hsf, cs, gates, hn, cn,
+                                                                      ring, err, B, S);
+  else
+    lstm_fwd_kernel<MT, KS, false><<<H / kUw, kThreads, 0, st>>>(xp, whh, h0, c0, hs, hsf, cs, gates, hn, cn, ring,
+                                                                 err, B, S);
   return hipGetLastError();
 }
 
@@ -462,10 +475,11 @@ extern "C" size_t dca_lstm_ring_elems(int B, int H, int backward) {
 
 extern "C" hipError_t dca_lstm_fwd(const float* xp, const short* whh, const float* h0, const float* c0, short* hs,
                                    float* hsf, float* cs, float* gates, float* hn, float* cn,
-                                   unsigned long long* ring, unsigned* err, int B, int S, int H, hipStream_t st) {
+                                   unsigned long long* ring, unsigned* err, int B, int S, int H, int local,
+                                   hipStream_t st) {
   if (B < 1 || B > 64 || S < 1 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
   const int MT = mt_for(B), KS = H / 128;
-#define DCA_F(mt, ks) launch_fwd<mt, ks>(xp, whh, h0, c0, hs, hsf, cs, gates, hn, cn, ring, err, B, S, st)
+#define DCA_F(mt, ks) launch_fwd<mt, ks>(xp, whh, h0, c0, hs, hsf, cs, gates, hn, cn, ring, err, B, S, local, st)
   DCA_DISPATCH_MT_KS(MT, KS, DCA_F)
 #undef DCA_F
 }

@@ -16,6 +16,9 @@ import torch
 from . import require
 
 MAX_B = 64
+# Hand-off mode of the forward recurrence: 0 = agent-scope write-through granules (placement independent),
+# 1 = XCD-local (all workgroups dealt to one XCD, L2-resident granules; validated before use, see tests).
+FWD_LOCAL = 0
 
 
 def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -33,7 +36,7 @@ class _Recurrence(torch.autograd.Function):
         for s in range(0, B, MAX_B):
             e = min(B, s + MAX_B)
             outs.append(C.lstm_fwd(xp[s:e].contiguous(), whh16, h0[s:e].contiguous(), c0[s:e].contiguous(), err,
-                                   True))
+                                   True, FWD_LOCAL))
         hs16, hsf, cs, gates, hn, cn = (torch.cat([o[i] for o in outs]) if len(outs) > 1 else outs[0][i]
                                         for i in range(6))
         ctx.save_for_backward(gates, cs, c0, whh16, hs16, h0)
