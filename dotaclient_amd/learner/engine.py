@@ -58,7 +58,7 @@ class Learner:
         self.model = self.policy
         if backend == 'fused':
             from ..models.fused import FusedPolicy
-            self.model = FusedPolicy(self.policy)
+            self.model = FusedPolicy(self.policy, loss_cfg)
         self.counts = self.policy.layout.action_counts()
         self.n_steps = 0
 

@@ -1,63 +1,257 @@
 """MI355X execution of :class:`~dotaclient_amd.models.policy.Policy` on hand-written gfx950 kernels.
 
 Same parameters (it wraps the reference module and reads its ``nn.Parameter``s, which live in the learner's flat
-buffer), different execution:
+buffer), different execution. The whole learner forward *and* backward is ONE ``autograd.Function`` with an explicit,
+hand-ordered backward (no per-op autograd graph):
 
-=================  =====================================================================================
-stage              MI355X path
-=================  =====================================================================================
-entity encoder     ``ops.encoder``: fused unit-MLP + per-type GEMM + max-pool (+argmax) HIP kernel
-                   (falls back to bf16 torch ops only for configurations the kernel does not cover)
-pre-RNN            bf16 GEMM (fp32 out) + ReLU
-LSTM               ``ops.lstm``: input projection GEMM + ONE persistent recurrence launch (fwd and bwd)
-heads + loss       ``ops.heads``: one heads GEMM + the fused pointer/log-softmax/PPO/entropy/value kernel
-optimizer          ``learner.optim.FlatAdam``: fused clip + Adam kernels over the flat buffer
-=================  =====================================================================================
+=================  ======================================================================================
+stage              forward / backward
+=================  ======================================================================================
+entity encoder     ``_C.encoder_fwd``: unit MLP + per-type GEMM + max-pool/argmax (MFMA, one kernel) /
+                   ``_C.encoder_bwd`` (∂W1 in-kernel) + one large-K hipBLASLt GEMM per unit type for ∂W_τ
+pre-RNN            bf16 GEMM (fp32 out) + ReLU / two GEMMs
+LSTM               input-projection GEMM + ONE persistent ``_C.lstm_fwd`` launch /
+                   ONE persistent ``_C.lstm_bwd`` launch + weight-gradient GEMMs over all B·S rows
+heads + loss       one heads GEMM + ``_C.heads_loss`` (pointer logits, 4 masked log-softmaxes, PPO/VPG,
+                   entropy, value, and ∂L/∂(every head input) in the same pass) / two GEMMs
+=================  ======================================================================================
+
+The 5v5 entity-attention variant keeps the encoder on bf16 torch ops (the attention block has no fused kernel yet)
+and uses the same LSTM and heads kernels through per-stage autograd wrappers.
 """
 from __future__ import annotations
 
-from typing import Dict
+from typing import Dict, List
 
 import torch
 import torch.nn.functional as F
 
-from .policy import Policy
+from .policy import TYPE_SUFFIX, Policy
+
+LDZ = 160
+
+
+def _mm(a, b):
+    return torch.mm(a, b, out_dtype=torch.float32)
+
+
+def _bf(t):
+    return t.detach().to(torch.bfloat16)
+
+
+class _PolicyLoss(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, fp: 'FusedPolicy', units, env, actions, masks, adv, ret, logp_old, nret, norms, h0, c0, *params):
+        C = fp.C
+        cfg, lc = fp.cfg, fp.loss_cfg
+        P = dict(zip(fp.param_names, params))
+        B, S, U, _ = units.shape
+        N = B * S
+        counts = list(cfg.layout.counts)
+        units2 = units.reshape(N, U, 10).contiguous()
+        env2 = env.reshape(N, 3).contiguous()
+        wt16 = torch.stack([_bf(P[f'affine_unit_{s}.weight']) for s in TYPE_SUFFIX])
+        bt = torch.stack([P[f'affine_unit_{s}.bias'].detach() for s in TYPE_SUFFIX])
+        x896, emb, arg = C.encoder_fwd(units2, env2, P['affine_unit_basic_stats.weight'].detach(),
+                                       P['affine_unit_basic_stats.bias'].detach(), wt16, bt,
+                                       P['affine_env.weight'].detach(), P['affine_env.bias'].detach(), counts,
+                                       bool(cfg.compat_bugs))
+        if cfg.compat_bugs:   # reference policy.py:127: enemy-tower pool = enemy-nonhero pool
+            x896[:, 640:768] = x896[:, 512:640]
+            arg[:, 5] = arg[:, 3]
+        wpre16 = _bf(P['affine_pre_rnn.weight'])
+        x = torch.relu(_mm(x896, wpre16.t()) + P['affine_pre_rnn.bias'].detach())
+        x16 = x.to(torch.bfloat16)
+        if cfg.rnn == 'lstm':
+            H = cfg.hidden
+            wih16, whh16 = _bf(P['rnn.weight_ih_l0']), _bf(P['rnn.weight_hh_l0'])
+            xp = (_mm(x16, wih16.t()) + (P['rnn.bias_ih_l0'].detach() + P['rnn.bias_hh_l0'].detach())).view(B, S, 4 * H)
+            hs, cs, gates = [], [], []
+            for s0 in range(0, B, 64):
+                s1 = min(B, s0 + 64)
+                o = C.lstm_fwd(xp[s0:s1], whh16, h0[s0:s1].contiguous(), c0[s0:s1].contiguous(), fp.err, False, 0)
+                hs.append(o[0]); cs.append(o[2]); gates.append(o[3])
+            cat = (lambda L: torch.cat(L) if len(L) > 1 else L[0])
+            hs16, cs, gates = cat(hs), cat(cs), cat(gates)
+            xh16 = hs16.view(N, H)
+            rnn_saved = (hs16, cs, gates, wih16, whh16)
+        else:
+            wf16 = _bf(P['fake_rnn.weight'])
+            xh16 = (_mm(x16, wf16.t()) + P['fake_rnn.bias'].detach()).to(torch.bfloat16)
+            rnn_saved = (wf16,)
+        wcat, bcat = fp.head_cat(P)
+        wcat16 = wcat.to(torch.bfloat16)
+        z = _mm(xh16, wcat16.t()) + bcat
+        dz, dtl, part, logp = C.heads_loss(z, emb.view(N, U, 128), actions, masks, adv, ret, logp_old, nret, norms,
+                                           0 if lc.algo == 'ppo' else 1, bool(lc.compat_value_bug), S, B,
+                                           float(lc.clip_eps), float(lc.entropy_coef), float(lc.vf_coef))
+        ctx.fp = fp
+        ctx.dims = (B, S, U, N)
+        ctx.save_for_backward(units2, env2, x896, arg, x, x16, xh16, h0, c0, dz, dtl, z, wt16, wpre16, wcat16,
+                              *rnn_saved)
+        ctx.mark_non_differentiable(logp)
+        return part.sum(0), logp
+
+    @staticmethod
+    def backward(ctx, gpart, _glogp):
+        fp = ctx.fp
+        C, cfg = fp.C, fp.cfg
+        B, S, U, N = ctx.dims
+        (units2, env2, x896, arg, x, x16, xh16, h0, c0, dz, dtl, z, wt16, wpre16, wcat16, *rnn_saved) = \
+            ctx.saved_tensors
+        P = {n: p for n, p in zip(fp.param_names, fp.params)}
+        g = gpart[15]
+        grads: Dict[str, torch.Tensor] = {}
+        # ---- heads
+        dZ = dz * g
+        dZ16 = dZ.to(torch.bfloat16)
+        dWcat = _mm(dZ16.t(), xh16)
+        dbcat = dZ.sum(0)
+        fp.split_head_grads(dWcat, dbcat, grads)
+        dxh = _mm(dZ16, wcat16)
+        # ---- recurrence
+        if cfg.rnn == 'lstm':
+            hs16, cs, gates, wih16, whh16 = rnn_saved
+            H = cfg.hidden
+            dxh3 = dxh.view(B, S, H)
+            dg, dh0s, dc0s = [], [], []
+            for s0 in range(0, B, 64):
+                s1 = min(B, s0 + 64)
+                o = C.lstm_bwd(dxh3[s0:s1], gates[s0:s1], cs[s0:s1], c0[s0:s1].contiguous(), None, None, whh16,
+                               fp.err)
+                dg.append(o[0])
+            dgates = (torch.cat(dg) if len(dg) > 1 else dg[0]).view(N, 4 * H)
+            dG16 = dgates.to(torch.bfloat16)
+            hprev = torch.cat([h0.to(torch.bfloat16).unsqueeze(1), hs16[:, :-1]], dim=1).view(N, H)
+            grads['rnn.weight_hh_l0'] = _mm(dG16.t(), hprev)
+            grads['rnn.weight_ih_l0'] = _mm(dG16.t(), x16)
+            db = dgates.sum(0)
+            grads['rnn.bias_ih_l0'] = db
+            grads['rnn.bias_hh_l0'] = db
+            dx = _mm(dG16, wih16)
+        else:
+            (wf16,) = rnn_saved
+            dxh16 = dxh.to(torch.bfloat16)
+            grads['fake_rnn.weight'] = _mm(dxh16.t(), x16)
+            grads['fake_rnn.bias'] = dxh.sum(0)
+            dx = _mm(dxh16, wf16)
+        # ---- pre-RNN
+        dpre = dx * (x > 0)
+        dpre16 = dpre.to(torch.bfloat16)
+        grads['affine_pre_rnn.weight'] = _mm(dpre16.t(), x896)
+        grads['affine_pre_rnn.bias'] = dpre.sum(0)
+        dx896 = _mm(dpre16, wpre16)
+        # ---- entity encoder
+        dtl_g = (dtl * g).contiguous()
+        wtT16 = wt16.transpose(1, 2).contiguous()
+        counts = list(cfg.layout.counts)
+        demb, basic, dw1, db1 = C.encoder_bwd(units2, P['affine_unit_basic_stats.weight'].detach(),
+                                              P['affine_unit_basic_stats.bias'].detach(), wtT16, dtl_g, z, dx896, arg,
+                                              counts, bool(cfg.compat_bugs))
+        grads['affine_unit_basic_stats.weight'] = dw1
+        grads['affine_unit_basic_stats.bias'] = db1
+        q = z[:, :128]
+        off = 0
+        for t, (s, cnt) in enumerate(zip(TYPE_SUFFIX, counts)):
+            lo, hi = off * N, (off + cnt) * N
+            grads[f'affine_unit_{s}.weight'] = _mm(demb[lo:hi].t(), basic[lo:hi])
+            db = q.t() @ dtl_g[:, off:off + cnt].sum(1)
+            if not (cfg.compat_bugs and t == 5):
+                db = db + dx896[:, 128 + 128 * t:256 + 128 * t].sum(0)
+            if cfg.compat_bugs and t == 3:
+                db = db + dx896[:, 128 + 128 * 5:256 + 128 * 5].sum(0)
+            grads[f'affine_unit_{s}.bias'] = db
+            off += cnt
+        # env embedding (3 → 128): tiny, fp32 torch
+        we, be = P['affine_env.weight'].detach(), P['affine_env.bias'].detach()
+        de = dx896[:, :128] * ((env2 @ we.t() + be) > 0)
+        grads['affine_env.weight'] = de.t() @ env2
+        grads['affine_env.bias'] = de.sum(0)
+        out = [grads.get(n) for n in fp.param_names]
+        return (None,) * 12 + tuple(out)
 
 
 class FusedPolicy:
-    def __init__(self, policy: Policy):
+    def __init__(self, policy: Policy, loss_cfg=None):
         from .. import ops
-        ops.require()
+        self.C = ops.require()
         self.policy = policy
         self.cfg = policy.config
+        self.loss_cfg = loss_cfg
         dev = next(policy.parameters()).device
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
-        self._zero_v = None
+        self.param_names: List[str] = [n for n, _ in policy.named_parameters()]
+        self.params = [p for _, p in policy.named_parameters()]
+        self.fully_fused = not self.cfg.entity_attention and self.cfg.unit_dim == 128 and self.cfg.env_dim == 128
 
     def refresh(self):
-        pass
+        self.params = [p for _, p in self.policy.named_parameters()]
 
     # ------------------------------------------------------------------------------------------------
-    def _wcat(self, with_value: bool):
-        p = self.policy
+    def head_cat(self, P):
+        """Concatenate the five head Linear layers into one (LDZ, H) matrix: [q | enum | x | y | value | pad]."""
         H = self.cfg.hidden
-        dev = p.affine_value.weight.device
-        wv, bv = p.affine_value.weight, p.affine_value.bias
-        if not with_value:
-            wv, bv = torch.zeros(1, H, device=dev), torch.zeros(1, device=dev)
-        from ..ops.heads import LDZ
-        pad = LDZ - (128 + 3 + 9 + 9 + 1)
-        w = torch.cat([p.affine_unit_attention.weight, p.affine_head_enum.weight, p.affine_move_x.weight,
-                       p.affine_move_y.weight, wv, torch.zeros(pad, H, device=dev)], 0)
-        b = torch.cat([p.affine_unit_attention.bias, p.affine_head_enum.bias, p.affine_move_x.bias,
-                       p.affine_move_y.bias, bv, torch.zeros(pad, device=dev)], 0)
+        dev = P['affine_value.weight'].device
+        with_value = self.loss_cfg is None or self.loss_cfg.vf_coef > 0
+        wv = P['affine_value.weight'].detach() if with_value else torch.zeros(1, H, device=dev)
+        bv = P['affine_value.bias'].detach() if with_value else torch.zeros(1, device=dev)
+        pad = LDZ - 150
+        w = torch.cat([P['affine_unit_attention.weight'].detach(), P['affine_head_enum.weight'].detach(),
+                       P['affine_move_x.weight'].detach(), P['affine_move_y.weight'].detach(), wv,
+                       torch.zeros(pad, H, device=dev)], 0)
+        b = torch.cat([P['affine_unit_attention.bias'].detach(), P['affine_head_enum.bias'].detach(),
+                       P['affine_move_x.bias'].detach(), P['affine_move_y.bias'].detach(), bv,
+                       torch.zeros(pad, device=dev)], 0)
         return w, b
 
-    def trunk(self, env: torch.Tensor, units: torch.Tensor, h0=None, c0=None):
-        """Encoder + pre-RNN + recurrence. Returns (xh (B,S,H) f32, emb (B,S,U,128) bf16, hn, cn)."""
-        from ..ops.encoder import encode
+    def split_head_grads(self, dW, db, grads):
+        spans = [('affine_unit_attention', 0, 128), ('affine_head_enum', 128, 131), ('affine_move_x', 131, 140),
+                 ('affine_move_y', 140, 149)]
+        if self.loss_cfg is None or self.loss_cfg.vf_coef > 0:
+            spans.append(('affine_value', 149, 150))
+        for name, lo, hi in spans:
+            grads[f'{name}.weight'] = dW[lo:hi]
+            grads[f'{name}.bias'] = db[lo:hi]
+
+    # ------------------------------------------------------------------------------------------------
+    def loss(self, batch: Dict[str, torch.Tensor], cfg):
+        from ..ops.heads import assemble_loss, batch_norms, heads_loss
+        self.loss_cfg = cfg
+        B, S = batch['env'].shape[:2]
+        N = B * S
+        dev = batch['env'].device
+        actions = batch['actions'].reshape(N, -1).contiguous()
+        masks = batch['masks'].reshape(N, -1).contiguous()
+        ret = batch['ret'].reshape(N).float().contiguous()
+        algo = 0 if cfg.algo == 'ppo' else 1
+        norms = batch_norms(actions, ret, cfg.compat_value_bug and algo == 1, S)
+        zeros = torch.zeros(N, device=dev)
+        adv = batch['adv'].reshape(N).contiguous() if 'adv' in batch else zeros
+        lpo = batch['logp_old'].reshape(N).contiguous() if 'logp_old' in batch else zeros
+        nret = batch['norm_ret'].reshape(N).contiguous() if 'norm_ret' in batch else zeros
+        if not self.fully_fused:
+            xh, emb, _, _ = self.trunk(batch['env'], batch['units'], batch.get('h0'), batch.get('c0'))
+            w, b = self.head_cat(dict(zip(self.param_names, self.params)))
+            U = emb.shape[2]
+            return heads_loss(xh.reshape(N, -1), w, b, emb.reshape(N, U, -1), batch, cfg, S)[:2]
+        H = self.cfg.hidden
+        h0 = batch.get('h0')
+        c0 = batch.get('c0')
+        if h0 is None:
+            h0 = torch.zeros(B, H, device=dev)
+            c0 = torch.zeros(B, H, device=dev)
+        self.refresh()
+        part, logp = _PolicyLoss.apply(self, batch['units'].contiguous(), batch['env'].contiguous(), actions, masks,
+                                       adv, ret, lpo, nret, norms, h0.contiguous(), c0.contiguous(), *self.params)
+        loss, metrics = assemble_loss(part, norms, cfg, ret, N, S)
+        return loss, metrics
+
+    # ---- per-stage path (entity-attention configs) --------------------------------------------------
+    def trunk(self, env, units, h0=None, c0=None):
         p = self.policy
-        x, emb = encode(p, env, units)                 # x (B,S,pre_rnn) f32, emb bf16
+        with torch.autocast('cuda', dtype=torch.bfloat16):
+            x, emb = p.encode(env, units)
+        x, emb = x.float(), emb.to(torch.bfloat16)
         B, S, _ = x.shape
         if self.cfg.rnn == 'lstm':
             from ..ops.lstm import lstm_sequence
@@ -72,16 +266,6 @@ class FusedPolicy:
             xh = F.linear(x, p.fake_rnn.weight, p.fake_rnn.bias)
             hn = cn = None
         return xh, emb, hn, cn
-
-    def loss(self, batch: Dict[str, torch.Tensor], cfg):
-        from ..ops.heads import heads_loss
-        B, S = batch['env'].shape[:2]
-        xh, emb, _, _ = self.trunk(batch['env'], batch['units'], batch.get('h0'), batch.get('c0'))
-        with_value = cfg.vf_coef > 0
-        w, b = self._wcat(with_value)
-        U = emb.shape[2]
-        loss, metrics, _ = heads_loss(xh.reshape(B * S, -1), w, b, emb.reshape(B * S, U, -1), batch, cfg, S)
-        return loss, metrics
 
     def check_error(self):
         """Raise if a persistent kernel timed out (host sync — call at iteration boundaries, not per step)."""

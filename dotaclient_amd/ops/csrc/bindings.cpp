@@ -128,6 +128,64 @@ std::vector<torch::Tensor> heads_loss(torch::Tensor z, torch::Tensor emb, torch:
   return {dz, dtl, part, logp};
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// Fused entity encoder. units (N,U,10) f32, env (N,3) f32, w1 (128,10), b1 (128), wt (6,128,128) bf16,
+// bt (6,128), we (128,3), be (128); counts = 6 unit counts. Returns (x896 bf16 (N,896), emb bf16 (N,U,128),
+// argmax u8 (N,6,128)).
+std::vector<torch::Tensor> encoder_fwd(torch::Tensor units, torch::Tensor env, torch::Tensor w1, torch::Tensor b1,
+                                       torch::Tensor wt, torch::Tensor bt, torch::Tensor we, torch::Tensor be,
+                                       std::vector<int64_t> counts, bool compat) {
+  CHECK_F32(units); CHECK_F32(env); CHECK_F32(w1); CHECK_F32(b1); CHECK_BF16(wt); CHECK_F32(bt); CHECK_F32(we);
+  CHECK_F32(be);
+  TORCH_CHECK(units.dim() == 3 && units.size(2) == 10, "units must be (N,U,10)");
+  const int N = units.size(0), U = units.size(1);
+  TORCH_CHECK(env.size(0) == N && env.size(1) == 3, "env must be (N,3)");
+  TORCH_CHECK(w1.size(0) == 128 && w1.size(1) == 10 && wt.size(0) == 6 && wt.size(1) == 128 && wt.size(2) == 128,
+              "weight shapes");
+  TORCH_CHECK(counts.size() == 6, "counts must have 6 entries");
+  int c[6];
+  int64_t tot = 0;
+  for (int i = 0; i < 6; ++i) { c[i] = (int)counts[i]; tot += counts[i]; }
+  TORCH_CHECK(tot == U && U <= 64, "counts must sum to U <= 64");
+  auto o = units.options();
+  auto x896 = torch::empty({N, 896}, o.dtype(at::kBFloat16));
+  auto emb = torch::empty({N, U, 128}, o.dtype(at::kBFloat16));
+  auto arg = torch::empty({N, 6, 128}, o.dtype(at::kByte));
+  hip_check(dca_encoder_fwd(ptr<float>(units), ptr<float>(env), ptr<float>(w1), ptr<float>(b1), ptr<short>(wt),
+                            ptr<float>(bt), ptr<float>(we), ptr<float>(be), ptr<short>(x896), ptr<short>(emb),
+                            ptr<unsigned char>(arg), N, U, c, compat ? 1 : 0, cur_stream()),
+            "dca_encoder_fwd");
+  return {x896, emb, arg};
+}
+
+// Returns (demb bf16 (U*N,128) type-major, basic bf16 (U*N,128) type-major, dw1 (128,10) f32, db1 (128) f32).
+std::vector<torch::Tensor> encoder_bwd(torch::Tensor units, torch::Tensor w1, torch::Tensor b1, torch::Tensor wtT,
+                                       torch::Tensor dtl, torch::Tensor q, torch::Tensor dx, torch::Tensor arg,
+                                       std::vector<int64_t> counts, bool compat) {
+  CHECK_F32(units); CHECK_F32(w1); CHECK_F32(b1); CHECK_BF16(wtT); CHECK_F32(dtl); CHECK_F32(dx); CHECK_U8(arg);
+  CHECK_DEV(q); CHECK_DT(q, at::kFloat);
+  const int N = units.size(0), U = units.size(1);
+  TORCH_CHECK(q.dim() == 2 && q.size(0) == N && q.size(1) >= 128 && q.stride(1) == 1 && q.stride(0) % 4 == 0,
+              "q must be (N, >=128) with unit column stride and 16-B aligned rows");
+  TORCH_CHECK(dtl.size(0) == N && dtl.size(1) == U && dx.size(0) == N && dx.size(1) == 896, "dtl/dx shapes");
+  TORCH_CHECK(arg.size(0) == N && arg.size(1) == 6 && arg.size(2) == 128, "arg shape");
+  int c[6];
+  int64_t tot = 0;
+  for (int i = 0; i < 6; ++i) { c[i] = (int)counts[i]; tot += counts[i]; }
+  TORCH_CHECK(tot == U && U <= 64, "counts must sum to U <= 64");
+  auto o = units.options();
+  auto demb = torch::empty({(int64_t)U * N, 128}, o.dtype(at::kBFloat16));
+  auto basic = torch::empty({(int64_t)U * N, 128}, o.dtype(at::kBFloat16));
+  auto dw1 = torch::zeros({128, 10}, o);
+  auto db1 = torch::zeros({128}, o);
+  hip_check(dca_encoder_bwd(ptr<float>(units), ptr<float>(w1), ptr<float>(b1), ptr<short>(wtT), ptr<float>(dtl),
+                            ptr<float>(q), (int)q.stride(0), ptr<float>(dx), ptr<unsigned char>(arg),
+                            ptr<short>(demb), ptr<short>(basic), ptr<float>(dw1), ptr<float>(db1), N, U, c,
+                            compat ? 1 : 0, cur_stream()),
+            "dca_encoder_bwd");
+  return {demb, basic, dw1, db1};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -135,5 +193,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adam_step", &adam_step, "fused global-norm clip + Adam over a flat fp32 buffer");
   m.def("lstm_fwd", &lstm_fwd, "persistent LSTM forward recurrence (granule all-gather)");
   m.def("heads_loss", &heads_loss, "fused heads + pointer + masked log-softmax + PPO/VPG loss + gradients");
+  m.def("encoder_fwd", &encoder_fwd, "fused entity encoder forward (unit MLP, per-type GEMM, max-pool+argmax)");
+  m.def("encoder_bwd", &encoder_bwd, "fused entity encoder backward (dW1 in-kernel; demb/basic for dW_type GEMMs)");
   m.def("lstm_bwd", &lstm_bwd, "persistent LSTM backward recurrence (granule reduce-scatter)");
 }
