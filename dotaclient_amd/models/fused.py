@@ -57,7 +57,7 @@ class _PolicyLoss(torch.autograd.Function):
                                        P['affine_env.weight'].detach(), P['affine_env.bias'].detach(), counts,
                                        bool(cfg.compat_bugs))
         if cfg.compat_bugs:   # reference policy.py:127: enemy-tower pool = enemy-nonhero pool
-            x896[:, 640:768] = x896[:, 512:640]
+            x896[:, 768:896] = x896[:, 512:640]
             arg[:, 5] = arg[:, 3]
         wpre16 = _bf(P['affine_pre_rnn.weight'])
         x = torch.relu(_mm(x896, wpre16.t()) + P['affine_pre_rnn.bias'].detach())
