@@ -1,0 +1,319 @@
+"""Learner runtime: ingest rollouts → returns/advantages → sequences → DP optimizer steps → checkpoint + publish.
+
+Capability parity with the reference's ``DotaOptimizer`` (optimizer.py:209-715):
+
+* consume rollouts from the experience queue until ≥ ``seq_per_epoch`` sequences (optimizer.py:441-453);
+* pad each rollout to a multiple of ``seq_len``, compute returns over the WHOLE rollout before slicing (so returns
+  carry across chunks), per-team EMA(0.99) reward normalisation, slice into ``Sequence`` chunks (345-422);
+* ``epochs`` passes of shuffled minibatches of ``batch_size`` sequences (458-471); ``seq_per_epoch % batch_size == 0``;
+* metrics with the reference's tag names (476-561), checkpoint ``model_%09d.pt`` + model publish every iteration
+  (563, 691-715), resume from the latest checkpoint (244-272), optional pretrained weights (strict=False, 271-272).
+
+Beyond the reference: PPO + GAE (``algo='ppo'``, the north star), LSTM chunks start from the actor's stored hidden
+state, on-device minibatching (one H2D upload per iteration, then index_select on HBM), full trainer state in the
+checkpoint, NaN guard without a per-step host sync (checked once per iteration), per-stage timers, and every rank
+resumes from the same iteration (reference quirk §2.10-7).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import random
+import socket
+import time
+from dataclasses import asdict, dataclass, field
+from datetime import datetime
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..constants import EPS, OBSERVATIONS_PER_SECOND, REWARD_KEYS
+from ..models.policy import Policy, get_config
+from ..parallel import dist as pdist
+from ..transport.codec import Rollout, decode_any
+from ..utils import checkpoint as ckpt
+from ..utils.metrics import MetricsWriter, StageTimer
+from .engine import Learner, LossConfig
+from .returns import RunningMeanStd, discount, gae
+
+logger = logging.getLogger(__name__)
+
+
+def default_log_dir():
+    return '{}_{}'.format(datetime.now().strftime('%b%d_%H-%M-%S'), socket.gethostname())
+
+
+@dataclass
+class OptimizerConfig:
+    log_dir: str = field(default_factory=default_log_dir)
+    epochs: int = 4                    # optimizer.py:774
+    seq_per_epoch: int = 16            # optimizer.py:775
+    batch_size: int = 4                # optimizer.py:776
+    seq_len: int = 256                 # optimizer.py:777
+    learning_rate: float = 1e-4
+    entropy_coef: float = 0.01
+    vf_coef: float = 0.5
+    pretrained_model: Optional[str] = None
+    mq_prefetch_count: int = 4
+    run_local: bool = True
+    iterations: int = 10000            # optimizer.py:238
+    algo: str = 'ppo'
+    model: str = 'lstm512'
+    gamma: float = 0.98
+    gae_lambda: float = 0.95
+    clip_eps: float = 0.1
+    max_grad_norm: float = 0.5
+    compat_value_bug: bool = False
+    normalize_advantages: bool = True
+    device: str = 'auto'
+    backend: str = 'auto'
+    checkpoint_keep: int = 0
+    histogram_freq: int = 128          # optimizer.py:214
+    xp_timeout: Optional[float] = None
+    seed: int = 7
+
+
+class Sequence:
+    """One ``seq_len`` chunk of a rollout (optimizer.py:165-200), plus PPO/LSTM extras."""
+
+    def __init__(self, game_id, env, units, actions, masks, rewards, returns, norm_returns, adv, logp, values,
+                 weight_version, team_id, hidden, valid):
+        self.game_id = game_id
+        self.env, self.units, self.actions, self.masks = env, units, actions, masks
+        self.rewards = rewards
+        self.discounted_rewards = returns
+        self.norm_discounted_rewards = norm_returns
+        self.adv, self.logp, self.values = adv, logp, values
+        self.weight_version = weight_version
+        self.team_id = team_id
+        self.hidden = hidden
+        self.valid = valid
+
+
+class DotaOptimizer:
+    SPEED_KEY = 'steps per s'
+
+    def __init__(self, cfg: OptimizerConfig, broker, checkpoint: Optional[bool] = None):
+        self.cfg = cfg
+        assert cfg.seq_per_epoch >= cfg.batch_size and cfg.seq_per_epoch % cfg.batch_size == 0
+        self.broker = broker
+        self.checkpoint = pdist.is_master() if checkpoint is None else checkpoint
+        dev = cfg.device
+        if dev == 'auto':
+            dev = f'cuda:{pdist.local_rank()}' if torch.cuda.is_available() else 'cpu'
+        self.device = torch.device(dev)
+        random.seed(cfg.seed)
+        np.random.seed(cfg.seed)
+        torch.manual_seed(cfg.seed)
+        self.policy_cfg = get_config(cfg.model)
+        self.policy = Policy(self.policy_cfg)
+        self.running = RunningMeanStd(0.99)
+        self.iteration_start = 1
+        self.writer = MetricsWriter(cfg.log_dir if self.checkpoint else None)
+        self.timer = StageTimer()
+        pretrained = cfg.pretrained_model
+        trainer_state = None
+        latest = ckpt.latest_model(cfg.log_dir)
+        if latest is not None:
+            logger.info('resuming from %s', latest)
+            self.iteration_start = ckpt.iteration_from_model_filename(latest) + 1
+            pretrained = latest
+            trainer_state = ckpt.load_trainer_state(cfg.log_dir, self.iteration_start - 1)
+        if pretrained is not None:
+            self.policy.load_state_dict(ckpt.load_model_file(pretrained), strict=False)
+        lc = LossConfig(algo=cfg.algo, learning_rate=cfg.learning_rate, entropy_coef=cfg.entropy_coef,
+                        vf_coef=cfg.vf_coef, clip_eps=cfg.clip_eps, gamma=cfg.gamma, gae_lambda=cfg.gae_lambda,
+                        max_grad_norm=cfg.max_grad_norm, compat_value_bug=cfg.compat_value_bug)
+        self.learner = Learner(self.policy, lc, device=self.device, backend=cfg.backend)
+        if trainer_state is not None:
+            self.learner.load_state_dict(trainer_state['learner'])
+            self.running.load_state_dict(trainer_state['running'])
+        # every rank starts from rank 0's iteration (reference workers restart at 1, §2.10-7)
+        if pdist.is_distributed():
+            t = torch.tensor([self.iteration_start], device=self.device if self.device.type == 'cuda' else 'cpu')
+            torch.distributed.broadcast(t, 0)
+            self.iteration_start = int(t.item())
+        self.time_last_step = time.time()
+        if self.iteration_start == 1:
+            self.upload_model(version=0)
+
+    # ------------------------------------------------------------------------------------------------
+    def get_rollout(self) -> Rollout:
+        body = self.broker.consume_experience(timeout=self.cfg.xp_timeout)
+        if body is None:
+            raise TimeoutError('no experience received')
+        return decode_any(body)
+
+    def experiences_from_rollout(self, r: Rollout) -> List[Sequence]:
+        S = self.cfg.seq_len
+        T = r.length
+        pad = (S - T % S) % S
+        n_seq = (T + pad) // S
+
+        def padt(a, fill=0):
+            if a is None or pad == 0:
+                return a
+            w = [(0, pad)] + [(0, 0)] * (a.ndim - 1)
+            return np.pad(a, w, mode='constant', constant_values=fill)
+        rewards = padt(r.rewards)
+        summed = rewards.sum(axis=1)
+        valid = np.concatenate([np.ones(T, np.float32), np.zeros(pad, np.float32)])
+        if self.cfg.algo == 'ppo' and r.values is not None:
+            values = padt(r.values.astype(np.float32))
+            adv, ret = gae(summed[:T], r.values, r.bootstrap_value, self.cfg.gamma, self.cfg.gae_lambda, done=r.done)
+            adv, ret = padt(adv), padt(ret)
+            self.running.update(ret[:T], r.team_id)
+            norm = adv
+        else:
+            # reference: discounted return over the full (padded) rollout, γ = 0.98 (optimizer.py:382)
+            ret = discount(summed, self.cfg.gamma)
+            self.running.update(ret, r.team_id)
+            norm = self.running.normalize(ret, r.team_id)
+            adv = norm
+            values = np.zeros(T + pad, np.float32)
+        logp = padt(r.logp.astype(np.float32)) if r.logp is not None else np.zeros(T + pad, np.float32)
+        env, units = padt(r.env), padt(r.units)
+        actions, masks = padt(r.actions), padt(r.masks)
+        seqs = []
+        H = self.policy_cfg.hidden
+        for s in range(n_seq):
+            a, b = s * S, (s + 1) * S
+            hidden = None
+            if self.policy.is_recurrent:
+                hidden = np.zeros((2, H), np.float32)
+                if r.hiddens is not None and r.hidden_stride and a % r.hidden_stride == 0 \
+                        and a // r.hidden_stride < len(r.hiddens):
+                    hidden = r.hiddens[a // r.hidden_stride]
+            seqs.append(Sequence(r.game_id, env[a:b], units[a:b], actions[a:b], masks[a:b], rewards[a:b], ret[a:b],
+                                 norm[a:b], adv[a:b], logp[a:b], values[a:b], r.weight_version, r.team_id, hidden,
+                                 valid[a:b]))
+        return seqs
+
+    def _to_device(self, seqs: List[Sequence]) -> Dict[str, torch.Tensor]:
+        def st(name, dtype):
+            a = np.stack([getattr(s, name) for s in seqs])
+            t = torch.from_numpy(np.ascontiguousarray(a)).to(dtype)
+            if self.device.type == 'cuda':
+                t = t.pin_memory()
+            return t.to(self.device, non_blocking=True)
+        d = {'env': st('env', torch.float32), 'units': st('units', torch.float32),
+             'actions': st('actions', torch.uint8), 'masks': st('masks', torch.uint8),
+             'ret': st('discounted_rewards', torch.float32), 'norm_ret': st('norm_discounted_rewards', torch.float32),
+             'adv': st('adv', torch.float32), 'logp_old': st('logp', torch.float32), 'valid': st('valid', torch.float32)}
+        if self.policy.is_recurrent:
+            h = st('hidden', torch.float32)
+            d['h0'], d['c0'] = h[:, 0].contiguous(), h[:, 1].contiguous()
+        if self.cfg.algo == 'ppo' and self.cfg.normalize_advantages:
+            v = d['valid']
+            n = v.sum().clamp_min(1.0)
+            mu = (d['adv'] * v).sum() / n
+            sd = (((d['adv'] - mu) ** 2 * v).sum() / n).sqrt()
+            d['adv'] = ((d['adv'] - mu) / (sd + EPS)) * v
+        return d
+
+    # ------------------------------------------------------------------------------------------------
+    def run(self, iterations: Optional[int] = None):
+        cfg = self.cfg
+        end = self.iteration_start + iterations if iterations is not None else cfg.iterations
+        for it in range(self.iteration_start, end):
+            self.run_iteration(it)
+        return end
+
+    def run_iteration(self, it: int):
+        cfg = self.cfg
+        self.timer.start('ingest')
+        experiences: List[Sequence] = []
+        subrewards, rollout_lens, weight_ages = [], [], []
+        canvas = None
+        while len(experiences) < cfg.seq_per_epoch:
+            r = self.get_rollout()
+            experiences.extend(self.experiences_from_rollout(r))
+            subrewards.append(r.rewards.sum(axis=0))
+            rollout_lens.append(r.length)
+            weight_ages.append(it - r.weight_version)
+            canvas = r.canvas
+        self.timer.stop('ingest')
+        # all sequences of this iteration go to the device once; minibatches are gathered on-device
+        self.timer.start('h2d')
+        n = len(experiences) - len(experiences) % cfg.batch_size
+        data = self._to_device(experiences[:n])
+        self.timer.stop('h2d')
+        self.timer.start('train')
+        losses, metrics_acc = [], {}
+        g = torch.Generator().manual_seed(cfg.seed * 1000003 + it)
+        for ep in range(cfg.epochs):
+            perm = torch.randperm(n, generator=g)
+            for b0 in range(0, n, cfg.batch_size):
+                idx = perm[b0:b0 + cfg.batch_size].to(self.device)
+                batch = {k: v.index_select(0, idx) for k, v in data.items()}
+                m = self.learner.train_step(batch)
+                losses.append(m['loss'])
+                for k, v in m.items():
+                    metrics_acc.setdefault(k, []).append(v)
+        if self.device.type == 'cuda':
+            torch.cuda.synchronize(self.device)
+        self.timer.stop('train')
+        loss_t = torch.stack(losses).float().cpu()
+        if torch.isnan(loss_t).any():
+            raise ValueError(f'NaN loss at iteration {it}: {loss_t.tolist()}')
+        if self.learner.backend == 'fused':
+            self.learner.model.check_error()
+        n_steps = len(experiences) * cfg.seq_len
+        now = time.time()
+        steps_per_s = n_steps / max(now - self.time_last_step, 1e-9)
+        self.time_last_step = now
+        sub = np.stack(subrewards) / n_steps * OBSERVATIONS_PER_SECOND
+        rollout_rewards = sub.sum(axis=1)
+        reward_dict = dict(zip(REWARD_KEYS, sub.sum(axis=0)))
+        mean = {k: torch.stack(v).float().mean().item() for k, v in metrics_acc.items()}
+        metrics = {
+            self.SPEED_KEY: steps_per_s,
+            'samples per s per gpu': steps_per_s * cfg.epochs,
+            'reward_per_sec/sum': float(rollout_rewards.sum()),
+            'loss/sum': mean['loss'], 'loss/policy': mean['policy_loss'], 'loss/entropy': mean['entropy_loss'],
+            'loss/advantage': mean['advantage_loss'], 'entropy': mean['entropy'], 'advantage': mean['advantage'],
+            'avg_rollout_len': float(np.mean(rollout_lens)), 'avg_weight_age': float(np.mean(weight_ages)),
+            'grad_norm': mean['grad_norm'],
+        }
+        for k in ('approx_kl', 'clipfrac'):
+            if k in mean:
+                metrics[k] = mean[k]
+        for team, v in self.running.mean.items():
+            metrics[f'rewards/running_mean_{team}'] = v
+        for team, v in self.running.std.items():
+            metrics[f'rewards/running_std_{team}'] = v
+        for k in ('enum', 'x', 'y', 'target_unit'):
+            metrics[f'entropy/{k}'] = mean[f'entropy/{k}']
+        for k, v in reward_dict.items():
+            metrics[f'reward_per_sec/{k}'] = float(v)
+        metrics.update(self.timer.pop())
+        logger.info('it=%d steps_per_s=%.1f avg_weight_age=%.1f reward_per_sec=%.4f loss=%.4f entropy=%.3f', it,
+                    steps_per_s, metrics['avg_weight_age'], metrics['reward_per_sec/sum'], metrics['loss/sum'],
+                    metrics['entropy'])
+        self.last_metrics = metrics
+        if self.checkpoint:
+            w = self.writer
+            w.add_scalars(metrics, it)
+            w.add_histogram('losses', loss_t.numpy(), it)
+            w.add_histogram('rollout_lens', np.asarray(rollout_lens), it)
+            w.add_histogram('weight_age', np.asarray(weight_ages), it)
+            w.add_histogram('rewards_per_sec_per_rollout', rollout_rewards, it)
+            if it % cfg.histogram_freq == 1:
+                for name, p in self.policy.named_parameters():
+                    w.add_histogram('param/' + name, p.detach().float().cpu().numpy(), it)
+                w.add_image('canvas', canvas, it)
+            qs = getattr(self.broker, 'xp_queue_size', None)
+            if qs is not None:
+                w.add_scalar('mq_size', qs, it)
+            w.flush()
+            self.upload_model(version=it)
+
+    def upload_model(self, version: int):
+        if not self.checkpoint:
+            return
+        path, data = ckpt.save_model(self.policy.state_dict(), self.cfg.log_dir, version)
+        ckpt.save_trainer_state({'learner': self.learner.state_dict(), 'running': self.running.state_dict(),
+                                 'iteration': version, 'config': asdict(self.cfg)}, self.cfg.log_dir, version)
+        ckpt.prune(self.cfg.log_dir, self.cfg.checkpoint_keep)
+        self.broker.publish_model(data, version)

@@ -7,7 +7,9 @@ The reference ships each rollout as ``pickle.dumps(dict)`` on the ``experience``
 
 * ``logp`` (T,) — joint log-prob of the sampled action under the behaviour policy (PPO ratio),
 * ``values`` (T,) — V(s_t) of the behaviour policy (GAE),
-* ``hidden0`` (2, H) — LSTM (h, c) at the first step of the rollout (R2D2-style stored state),
+* ``hiddens`` (K, 2, H) — LSTM (h, c) *before* steps 0, stride, 2·stride, … of the rollout (``hidden_stride``), so
+  the learner can start every ``seq_len`` chunk from the state the actor actually had (R2D2-style stored state,
+  SURVEY §5);
 * ``bootstrap_value`` / ``done`` — how the rollout ended (truncated by ``rollout_size`` or terminal).
 
 Codecs:
@@ -48,7 +50,8 @@ class Rollout:
     canvas: Optional[np.ndarray] = None  # (256, 256, 3) u8
     logp: Optional[np.ndarray] = None
     values: Optional[np.ndarray] = None
-    hidden0: Optional[np.ndarray] = None
+    hiddens: Optional[np.ndarray] = None
+    hidden_stride: int = 0
     bootstrap_value: float = 0.0
     done: bool = True
     layout: Tuple[int, ...] = field(default_factory=lambda: LAYOUT_1V1.counts)
@@ -96,12 +99,13 @@ class Rollout:
                    layout=counts)
 
 
-_ARRAYS = ['env', 'units', 'actions', 'masks', 'rewards', 'canvas', 'logp', 'values', 'hidden0']
+_ARRAYS = ['env', 'units', 'actions', 'masks', 'rewards', 'canvas', 'logp', 'values', 'hiddens']
 
 
 def encode(r: Rollout) -> bytes:
     header = {'game_id': r.game_id, 'team_id': r.team_id, 'player_id': r.player_id,
               'weight_version': r.weight_version, 'bootstrap_value': float(r.bootstrap_value), 'done': bool(r.done),
+              'hidden_stride': int(r.hidden_stride),
               'layout': list(r.layout), 'arrays': []}
     blobs = []
     off = 0
@@ -130,6 +134,7 @@ def decode(buf: bytes) -> Rollout:
         arrays[name] = np.frombuffer(mv[base + off: base + off + n], dtype=np.dtype(dt)).reshape(shape)
     return Rollout(game_id=header['game_id'], team_id=header['team_id'], player_id=header['player_id'],
                    weight_version=header['weight_version'], bootstrap_value=header['bootstrap_value'],
+                   hidden_stride=header.get('hidden_stride', 0),
                    done=header['done'], layout=tuple(header['layout']), **{k: arrays.get(k) for k in _ARRAYS})
 
 
