@@ -94,7 +94,10 @@ def ppo_loss(logits: Dict[str, torch.Tensor], values: torch.Tensor, actions: Dic
     surr2 = torch.clamp(ratio, 1.0 - clip_eps, 1.0 + clip_eps) * advantages
     policy_loss = -(torch.minimum(surr1, surr2) * valid).sum() / n_valid
     v = values.squeeze(-1)
-    value_loss = vf_coef * ((v - returns).pow(2) * valid).sum() / n_valid
+    if vf_coef > 0:
+        value_loss = vf_coef * ((v - returns).pow(2) * valid).sum() / n_valid
+    else:   # keep the value head out of the graph (reference sparse-param semantics, optimizer.py:667-670)
+        value_loss = torch.zeros((), device=v.device, dtype=v.dtype)
     ents = _entropies(terms)
     entropy = torch.stack(list(ents.values())).sum()
     entropy_loss = -entropy_coef * entropy

@@ -1,0 +1,136 @@
+"""Multi-process data parallelism on CPU (gloo): the flat-bucket DP wrapper reproduces the reference's
+``DistributedDataParallelSparseParamCPU`` semantics (distributed.py:16-79) and single-process large-batch math."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+
+
+class Toy(torch.nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.a = torch.nn.Linear(4, 4)
+        self.b = torch.nn.Linear(4, 4)
+        self.c = torch.nn.Linear(4, 4)   # never used: must stay untouched
+
+
+def _toy_worker(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        from dotaclient_amd.parallel.dp import DataParallel
+        torch.manual_seed(100 + rank)          # different init per rank → broadcast must equalise
+        m = Toy()
+        dp = DataParallel(m, bucket_cap_mb=0.0001, overlap=False)
+        x = torch.full((2, 4), float(rank + 1))
+        out = m.a(x).sum()
+        if rank == 0:
+            out = out + m.b(x).sum()           # only rank 0 produces a gradient for b
+        dp.zero_grad()
+        out.backward()
+        dp.sync()
+        q.put((rank, {k: v.detach().clone() for k, v in m.state_dict().items()},
+               {n: p.grad.clone() for n, p in m.named_parameters()}, dp.counts.clone()))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e), None, None))
+
+
+def test_sparse_param_semantics_two_ranks():
+    world, port = 2, _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_toy_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, sd, grads, counts = q.get(timeout=120)
+        assert grads is not None, sd
+        res[r] = (sd, grads, counts)
+    for p in ps:
+        p.join(timeout=60)
+    sd0, g0, c0 = res[0]
+    sd1, g1, c1 = res[1]
+    for k in sd0:
+        assert torch.equal(sd0[k], sd1[k]), k          # rank-0 broadcast at construction
+    for k in g0:
+        assert torch.equal(g0[k], g1[k]), k            # identical reduced grads on every rank (fixes §2.10-8)
+    names = list(g0)
+    counts = dict(zip(names, c0.tolist()))
+    assert counts['a.weight'] == 2 and counts['b.weight'] == 1 and counts['c.weight'] == 0
+    # a: mean over ranks of per-rank grads (x = 1 and x = 2) → column sums (2·1 + 2·2)/2 = 3
+    assert torch.allclose(g0['a.weight'], torch.full((4, 4), 3.0))
+    # b: only rank 0 had it → divided by its count 1
+    assert torch.allclose(g0['b.weight'], torch.full((4, 4), 2.0))
+    assert torch.count_nonzero(g0['c.weight']) == 0
+
+
+def _learner_worker(rank, world, port, q, batch_seed):
+    try:
+        _init(rank, world, port)
+        from dotaclient_amd.learner.engine import Learner, LossConfig
+        from dotaclient_amd.learner.synthetic import make_batch
+        from dotaclient_amd.models.policy import Policy, get_config
+        torch.manual_seed(0)
+        cfg = get_config('lstm128')
+        L = Learner(Policy(cfg), LossConfig(algo='ppo', vf_coef=0.0), device='cpu', backend='torch', overlap=False)
+        b = make_batch(4, 16, cfg.layout, cfg.hidden, seed=batch_seed + rank)
+        L.train_step(b)
+        q.put((rank, L.flat.flat.clone(), L.dp.counts.clone()))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e), None))
+
+
+def test_dp_step_equals_single_process_average():
+    from dotaclient_amd.learner.engine import Learner, LossConfig
+    from dotaclient_amd.learner.synthetic import make_batch
+    from dotaclient_amd.models.policy import Policy, get_config
+    world, port, seed = 2, _free_port(), 11
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_learner_worker, args=(r, world, port, q, seed)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = {}
+    for _ in range(world):
+        r, flat, counts = q.get(timeout=180)
+        assert counts is not None, flat
+        out[r] = (flat, counts)
+    for p in ps:
+        p.join(timeout=60)
+    assert torch.equal(out[0][0], out[1][0])
+    # single-process oracle: average of the two per-rank gradients, same optimizer step
+    torch.manual_seed(0)
+    cfg = get_config('lstm128')
+    L = Learner(Policy(cfg), LossConfig(algo='ppo', vf_coef=0.0), device='cpu', backend='torch', dp=False)
+    grads = []
+    for r in range(world):
+        L.dp.zero_grad()
+        loss, _ = L.loss(make_batch(4, 16, cfg.layout, cfg.hidden, seed=seed + r))
+        loss.backward()
+        grads.append(L.flat.grad.clone())
+    L.flat.grad.copy_(sum(grads) / world)
+    counts = out[0][1]
+    names = L.flat.names
+    assert counts[names.index('affine_value.weight')] == 0      # vf_coef = 0: value head has no grad anywhere
+    L.opt.step(counts)
+    torch.testing.assert_close(L.flat.flat, out[0][0], rtol=1e-5, atol=1e-6)
