@@ -39,6 +39,28 @@ def _bf(t):
     return t.detach().to(torch.bfloat16)
 
 
+def tn_splitk(a: torch.Tensor, b: torch.Tensor, chunk: int = 2048) -> torch.Tensor:
+    """aᵀ·b for tall-skinny operands (K ≫ M, N: weight gradients reduced over B·S·units rows) as a batched GEMM over
+    K-chunks + a sum. A plain GEMM of this shape gets only (M/64)·(N/128) workgroups and no split-K on hipBLASLt
+    (measured 25 TF for 128×128×179200); chunking gives K/chunk× more parallelism."""
+    K, M = a.shape
+    N = b.shape[1]
+    nc = K // chunk
+    if nc < 2:
+        return torch.mm(a.t(), b, out_dtype=torch.float32) if a.dtype == torch.bfloat16 else a.t() @ b
+    main = nc * chunk
+    if a.dtype == torch.bfloat16:
+        part = torch.bmm(a[:main].view(nc, chunk, M).transpose(1, 2), b[:main].view(nc, chunk, N),
+                         out_dtype=torch.float32)
+    else:
+        part = torch.bmm(a[:main].view(nc, chunk, M).transpose(1, 2), b[:main].view(nc, chunk, N))
+    out = part.sum(0)
+    if main < K:
+        out += (torch.mm(a[main:].t(), b[main:], out_dtype=torch.float32) if a.dtype == torch.bfloat16
+                else a[main:].t() @ b[main:])
+    return out
+
+
 class _PolicyLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, fp: 'FusedPolicy', units, env, actions, masks, adv, ret, logp_old, nret, norms, h0, c0, *params):
@@ -67,9 +89,10 @@ class _PolicyLoss(torch.autograd.Function):
             wih16, whh16 = _bf(P['rnn.weight_ih_l0']), _bf(P['rnn.weight_hh_l0'])
             xp = (_mm(x16, wih16.t()) + (P['rnn.bias_ih_l0'].detach() + P['rnn.bias_hh_l0'].detach())).view(B, S, 4 * H)
             hs, cs, gates = [], [], []
-            for s0 in range(0, B, 64):
-                s1 = min(B, s0 + 64)
-                o = C.lstm_fwd(xp[s0:s1], whh16, h0[s0:s1].contiguous(), c0[s0:s1].contiguous(), fp.err, False, 0)
+            mb = C.lstm_max_batch(H)
+            for s0 in range(0, B, mb):
+                s1 = min(B, s0 + mb)
+                o = C.lstm_fwd(xp[s0:s1], whh16, h0[s0:s1].contiguous(), c0[s0:s1].contiguous(), fp.err, False)
                 hs.append(o[0]); cs.append(o[2]); gates.append(o[3])
             cat = (lambda L: torch.cat(L) if len(L) > 1 else L[0])
             hs16, cs, gates = cat(hs), cat(cs), cat(gates)
@@ -114,9 +137,10 @@ class _PolicyLoss(torch.autograd.Function):
             hs16, cs, gates, wih16, whh16 = rnn_saved
             H = cfg.hidden
             dxh3 = dxh.view(B, S, H)
-            dg, dh0s, dc0s = [], [], []
-            for s0 in range(0, B, 64):
-                s1 = min(B, s0 + 64)
+            dg = []
+            mb = C.lstm_max_batch(H)
+            for s0 in range(0, B, mb):
+                s1 = min(B, s0 + mb)
                 o = C.lstm_bwd(dxh3[s0:s1], gates[s0:s1], cs[s0:s1], c0[s0:s1].contiguous(), None, None, whh16,
                                fp.err)
                 dg.append(o[0])
@@ -151,16 +175,24 @@ class _PolicyLoss(torch.autograd.Function):
         grads['affine_unit_basic_stats.weight'] = dw1
         grads['affine_unit_basic_stats.bias'] = db1
         q = z[:, :128]
+        # ∂b_τ = Σ_n q[n]·Σ_{u∈τ} dtl[n,u] + Σ_n ∂pool_τ[n]  (each pooled column routes to exactly one unit)
+        seg = torch.zeros(U, 6, device=q.device)
+        off = 0
+        for t, cnt in enumerate(counts):
+            seg[off:off + cnt, t] = 1.0
+            off += cnt
+        dbt = tn_splitk((dtl_g @ seg).contiguous(), q.contiguous())          # (6, 128)
+        dpool = dx896[:, 128:].reshape(N, 6, 128).sum(0)
+        if cfg.compat_bugs:
+            dpool = dpool.clone()
+            dpool[3] += dpool[5]
+            dpool[5] = 0
+        dbt = dbt + dpool
         off = 0
         for t, (s, cnt) in enumerate(zip(TYPE_SUFFIX, counts)):
             lo, hi = off * N, (off + cnt) * N
-            grads[f'affine_unit_{s}.weight'] = _mm(demb[lo:hi].t(), basic[lo:hi])
-            db = q.t() @ dtl_g[:, off:off + cnt].sum(1)
-            if not (cfg.compat_bugs and t == 5):
-                db = db + dx896[:, 128 + 128 * t:256 + 128 * t].sum(0)
-            if cfg.compat_bugs and t == 3:
-                db = db + dx896[:, 128 + 128 * 5:256 + 128 * 5].sum(0)
-            grads[f'affine_unit_{s}.bias'] = db
+            grads[f'affine_unit_{s}.weight'] = tn_splitk(demb[lo:hi], basic[lo:hi])
+            grads[f'affine_unit_{s}.bias'] = dbt[t]
             off += cnt
         # env embedding (3 → 128): tiny, fp32 torch
         we, be = P['affine_env.weight'].detach(), P['affine_env.bias'].detach()

@@ -49,14 +49,14 @@ void adam_step(torch::Tensor param, torch::Tensor grad, torch::Tensor m, torch::
 // ------------------------------------------------------------------------------------------------------------
 // Persistent LSTM recurrence. xp (B,S,4H) f32, whh (4H,H) bf16, h0/c0 (B,H) f32, err (1) int32 device flag.
 std::vector<torch::Tensor> lstm_fwd(torch::Tensor xp, torch::Tensor whh, torch::Tensor h0, torch::Tensor c0,
-                                    torch::Tensor err, bool want_f32_h, int64_t local) {
+                                    torch::Tensor err, bool want_f32_h) {
   CHECK_F32(xp); CHECK_BF16(whh); CHECK_F32(h0); CHECK_F32(c0); CHECK_I32(err);
   TORCH_CHECK(xp.dim() == 3, "xp must be (B,S,4H)");
   const int B = xp.size(0), S = xp.size(1), G4 = xp.size(2), H = G4 / 4;
   TORCH_CHECK(whh.size(0) == G4 && whh.size(1) == H, "whh must be (4H,H)");
   TORCH_CHECK(h0.size(0) == B && h0.size(1) == H && c0.size(0) == B && c0.size(1) == H, "h0/c0 must be (B,H)");
-  TORCH_CHECK(B >= 1 && B <= 64, "lstm_fwd: 1 <= B <= 64 per launch");
   TORCH_CHECK(H == 128 || H == 256 || H == 512, "lstm_fwd: H in {128,256,512}");
+  TORCH_CHECK(B >= 1 && B <= dca_lstm_max_batch(H), "lstm_fwd: batch exceeds the per-launch maximum");
   auto f32 = xp.options();
   auto hs = torch::empty({B, S, H}, f32.dtype(at::kBFloat16));
   torch::Tensor hsf = want_f32_h ? torch::empty({B, S, H}, f32) : torch::Tensor();
@@ -67,8 +67,7 @@ std::vector<torch::Tensor> lstm_fwd(torch::Tensor xp, torch::Tensor whh, torch::
   auto ring = torch::empty({(int64_t)dca_lstm_ring_elems(B, H, 0)}, f32.dtype(at::kLong));
   hip_check(dca_lstm_fwd(ptr<float>(xp), ptr<short>(whh), ptr<float>(h0), ptr<float>(c0), ptr<short>(hs),
                          want_f32_h ? ptr<float>(hsf) : nullptr, ptr<float>(cs), ptr<float>(gates), ptr<float>(hn),
-                         ptr<float>(cn), ptr<unsigned long long>(ring), ptr<unsigned>(err), B, S, H, (int)local,
-                         cur_stream()),
+                         ptr<float>(cn), ptr<unsigned long long>(ring), ptr<unsigned>(err), B, S, H, cur_stream()),
             "dca_lstm_fwd");
   return {hs, want_f32_h ? hsf : hs, cs, gates, hn, cn};
 }
@@ -81,7 +80,8 @@ std::vector<torch::Tensor> lstm_bwd(torch::Tensor dhs, torch::Tensor gates, torc
   TORCH_CHECK(gates.size(0) == B && gates.size(1) == S && gates.size(2) == 4 * H, "gates must be (B,S,4H)");
   TORCH_CHECK(cs.sizes() == dhs.sizes(), "cs must be (B,S,H)");
   TORCH_CHECK(whh.size(0) == 4 * H && whh.size(1) == H, "whh must be (4H,H)");
-  TORCH_CHECK(B >= 1 && B <= 64, "lstm_bwd: 1 <= B <= 64 per launch");
+  TORCH_CHECK(H == 128 || H == 256 || H == 512, "lstm_bwd: H in {128,256,512}");
+  TORCH_CHECK(B >= 1 && B <= dca_lstm_max_batch(H), "lstm_bwd: batch exceeds the per-launch maximum");
   const float* dhn_p = nullptr;
   const float* dcn_p = nullptr;
   if (dhn.has_value() && dhn->defined()) { CHECK_F32((*dhn)); dhn_p = ptr<float>(*dhn); }
@@ -191,6 +191,7 @@ std::vector<torch::Tensor> encoder_bwd(torch::Tensor units, torch::Tensor w1, to
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "dotaclient_amd gfx950 HIP kernels";
   m.def("adam_step", &adam_step, "fused global-norm clip + Adam over a flat fp32 buffer");
+  m.def("lstm_max_batch", &dca_lstm_max_batch, "max sequences per persistent LSTM launch for hidden size H");
   m.def("lstm_fwd", &lstm_fwd, "persistent LSTM forward recurrence (granule all-gather)");
   m.def("heads_loss", &heads_loss, "fused heads + pointer + masked log-softmax + PPO/VPG loss + gradients");
   m.def("encoder_fwd", &encoder_fwd, "fused entity encoder forward (unit MLP, per-type GEMM, max-pool+argmax)");

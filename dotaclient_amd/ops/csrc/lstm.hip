@@ -33,7 +33,6 @@ using dca::bf16x8;
 using gu64 = __attribute__((address_space(1))) unsigned long long;
 using gu32 = __attribute__((address_space(1))) unsigned int;
 
-constexpr int kThreads = 256;
 constexpr int kUw = 8;                  // hidden units per workgroup
 constexpr unsigned kSpinLimit = 1u << 21;
 
@@ -42,11 +41,6 @@ __device__ __forceinline__ unsigned long long ld_granule(const unsigned long lon
 }
 __device__ __forceinline__ void st_granule(unsigned long long* p, unsigned long long v) {
   __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-// XCD-local hand-off: a plain store keeps the line in the producer XCD's L2, where same-XCD consumers' L1-bypassing
-// (agent-scope) loads hit it. Only valid when every workgroup of the launch sits on ONE XCD (see LOCAL below).
-__device__ __forceinline__ void st_granule_local(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 __device__ __forceinline__ unsigned ld_err(const unsigned* p) {
   return __hip_atomic_load((gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -69,388 +63,460 @@ __device__ __forceinline__ bool spin_fail(unsigned& spins, unsigned* err, unsign
   return false;
 }
 
+// One workgroup-wide rendezvous that orders LDS traffic only. Unlike __syncthreads() it does NOT wait for
+// outstanding global stores/loads (no vmcnt(0)), so a wave's in-flight granule or output stores never stall the
+// others (cdna_hip_programming.md §5 "Pipelining across barriers"). The "memory" clobber stops the compiler from
+// moving LDS accesses across it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 // =============================================================================================================
-// Forward
+// Forward — 5 waves: waves 0-3 are POLLERS (gather h_{t-1} for their K quarter, prefetch x·W_ihᵀ, MFMA, write
+// partial gates to LDS; they never store to global memory, so their polls never wait behind store completion),
+// wave 4 is the PUBLISHER (sums the partials, cell update, publishes h_t granules + outputs; it never loads
+// global memory inside the loop, so its stores never stall it). One LDS-only barrier per step.
 // =============================================================================================================
 // xp     (B, S, 4H) f32  input projection incl. both biases
 // whh    (4H, H)    bf16 recurrent weights (PyTorch layout, gate order i,f,g,o)
 // h0,c0  (B, H)     f32
-// hs     (B, S, H)  bf16 out: h_t
-// hsf    (B, S, H)  f32  out: h_t (optional, may be null)
-// cs     (B, S, H)  f32  out: c_t
-// gates  (B, S, 4H) f32  out: activated i, f, g, o
+// hs     (B, S, H)  bf16 out: h_t          hsf (B,S,H) f32 out (optional)
+// cs     (B, S, H)  f32  out: c_t          gates (B,S,4H) f32 out: activated i, f, g, o
 // hn,cn  (B, H)     f32  out: final state
-// ring   (2, B, H/2) u64 granules (zeroed)
-template <int MT, int KS, bool LOCAL>
-__global__ __launch_bounds__(kThreads) void lstm_fwd_kernel(const float* __restrict__ xp, const short* __restrict__ whh,
-                                                            const float* __restrict__ h0, const float* __restrict__ c0,
-                                                            short* __restrict__ hs, float* __restrict__ hsf,
-                                                            float* __restrict__ cs, float* __restrict__ gates,
-                                                            float* __restrict__ hn, float* __restrict__ cn,
-                                                            unsigned long long* ring, unsigned* err, int B, int S) {
-  constexpr int H = 128 * KS;           // each of the 4 waves owns K/4 = 32·KS of the reduction
+// ring   (2, B, H/2) u64 granules {tag = t+1, 2×bf16 h} (zeroed before launch)
+constexpr int kFwdThreads = 320;
+constexpr int kBwdThreads = 512;
+constexpr int kMaxPairs = 512;   // B·8 ≤ 512
+
+template <int MT, int KS>
+__global__ __launch_bounds__(kFwdThreads) void lstm_fwd_kernel(const float* __restrict__ xp,
+                                                               const short* __restrict__ whh,
+                                                               const float* __restrict__ h0,
+                                                               const float* __restrict__ c0, short* __restrict__ hs,
+                                                               float* __restrict__ hsf, float* __restrict__ cs,
+                                                               float* __restrict__ gates, float* __restrict__ hn,
+                                                               float* __restrict__ cn, unsigned long long* ring,
+                                                               unsigned* err, int Btot, int Bc, int S) {
+  constexpr int H = 128 * KS;
   constexpr int G4 = 4 * H;
-  constexpr int HP = H / 2;             // granules per batch row
-  // LOCAL: the grid is 8× oversized and only blocks ≡ 0 (mod 8) — which the dispatcher deals to one XCD — work.
-  if (LOCAL && (blockIdx.x & 7) != 0) return;
-  const int w = LOCAL ? (blockIdx.x >> 3) : blockIdx.x;
+  constexpr int HP = H / 2;
+  // independent chains of ≤ 16·MT sequences run side by side in one launch (blockIdx = chain·NWG + w)
+  const int chain = blockIdx.x / (H / kUw);
+  const int b0 = chain * Bc;
+  const int B = min(Bc, Btot - b0);
+  xp += (size_t)b0 * S * G4; h0 += (size_t)b0 * H; c0 += (size_t)b0 * H; hs += (size_t)b0 * S * H;
+  if (hsf) hsf += (size_t)b0 * S * H;
+  cs += (size_t)b0 * S * H; gates += (size_t)b0 * S * G4; hn += (size_t)b0 * H; cn += (size_t)b0 * H;
+  ring += (size_t)chain * 2 * Bc * HP;
+  const int w = blockIdx.x % (H / kUw);
   const int j0 = w * kUw;
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int lrow = lane & 15, lkg = lane >> 4;
+  const int P = B * kUw;
 
-  __shared__ float red[4][MT][2][16][17];
+  constexpr int PMAX = 128 * MT;        // pairs (B·8) this instantiation supports
+  __shared__ float red[2][4][MT][2][16][17];
+  __shared__ float xpl[2][4][PMAX];
+  __shared__ int abort_flag;
+  if (tid == 0) abort_flag = 0;
+  __syncthreads();
 
-  // ---- W_hh slice as MFMA B fragments: B[k][c] = W[row(c)][k]; lane holds c = lane&15 (+16·nt), k = 8·lkg + j.
+  const bool poller = wv < 4;
   bf16x8 wf[2][KS];
+  if (poller) {
 #pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    const int c = nt * 16 + lrow;                  // local gate column 0..31
-    const int row = (c >> 3) * H + j0 + (c & 7);   // gate q = c/8, unit c%8
+    for (int nt = 0; nt < 2; ++nt) {
+      const int c = nt * 16 + lrow;
+      const int row = (c >> 3) * H + j0 + (c & 7);
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const int k = wv * (32 * KS) + ks * 32 + 8 * lkg;
-      wf[nt][ks] = *reinterpret_cast<const bf16x8*>(whh + (size_t)row * H + k);
+      for (int ks = 0; ks < KS; ++ks) {
+        const int k = wv * (32 * KS) + ks * 32 + 8 * lkg;
+        wf[nt][ks] = *reinterpret_cast<const bf16x8*>(whh + (size_t)row * H + k);
+      }
     }
   }
-
-  // ---- elementwise ownership: pairs p = b*8 + jj; up to 2 per thread (B ≤ 64)
-  const int P = B * kUw;
-  float creg[2];
-  float hreg[2];
+  // publisher state: pairs p = lane + 64·r
+  constexpr int NPR = PMAX / 64;
+  float creg[NPR], hreg[NPR];
+  if (!poller) {
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int p = tid + r * kThreads;
-    creg[r] = 0.f;
-    hreg[r] = 0.f;
-    if (p < P) {
-      const int b = p >> 3, jj = p & 7;
-      creg[r] = c0[b * H + j0 + jj];
-      hreg[r] = h0[b * H + j0 + jj];
+    for (int r = 0; r < NPR; ++r) {
+      const int p = lane + 64 * r;
+      creg[r] = hreg[r] = 0.f;
+      if (p < P) {
+        creg[r] = c0[(p >> 3) * H + j0 + (p & 7)];
+        hreg[r] = h0[(p >> 3) * H + j0 + (p & 7)];
+      }
     }
   }
 
   unsigned spins = 0;
-  bool dead = false;
   for (int t = 0; t < S; ++t) {
-    // -------- prefetch this step's input projection (plain loads; written before launch)
-    float xv[2][4];
+    const int par = t & 1;
+    if (poller) {
+      // -------- prefetch this step's x·W_ihᵀ values (4 per pair) — issued before the poll, consumed after it
+      constexpr int NXV = (4 * PMAX) / 256;
+      float xv[NXV];
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int p = tid + r * kThreads;
-      if (p < P) {
-        const int b = p >> 3, jj = p & 7;
-        const float* x = xp + ((size_t)b * S + t) * G4 + j0 + jj;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) xv[r][q] = x[q * H];
-      }
-    }
-    // -------- gather h_{t-1} A-fragments (rows = batch, k = hidden) for this wave's K quarter
-    bf16x8 af[MT][KS];
-    if (t == 0) {
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          const int b = mt * 16 + lrow;
-          const int k = wv * (32 * KS) + ks * 32 + 8 * lkg;
-          bf16x8 v;
-#pragma unroll
-          for (int j = 0; j < 8; ++j) v[j] = (b < B) ? dca::f2bf(h0[b * H + k + j]) : (short)0;
-          af[mt][ks] = v;
+      for (int i = 0; i < NXV; ++i) {
+        const int idx = tid + 256 * i;
+        xv[i] = 0.f;
+        if (idx < 4 * P) {
+          const int p = idx >> 2, q = idx & 3;
+          xv[i] = xp[((size_t)(p >> 3) * S + t) * G4 + q * H + j0 + (p & 7)];
         }
-    } else {
-      const unsigned long long* slot = ring + (size_t)((t - 1) & 1) * B * HP;
-      const unsigned tag = (unsigned)t;     // h_{t-1} carries tag t
-      while (true) {
-        bool ok = true;
+      }
+      // -------- A fragments of h_{t-1} for this wave's K quarter
+      bf16x8 af[MT][KS];
+      bool dead = false;
+      if (t == 0) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) {
             const int b = mt * 16 + lrow;
             const int k = wv * (32 * KS) + ks * 32 + 8 * lkg;
-            bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (b < B) {
-              const unsigned long long* g = slot + (size_t)b * HP + (k >> 1);
+            bf16x8 v;
 #pragma unroll
-              for (int q = 0; q < 4; ++q) {
-                const unsigned long long x = ld_granule(g + q);
-                ok &= (unsigned)(x >> 32) == tag;
-                const unsigned pl = (unsigned)x;
-                v[2 * q] = (short)(pl & 0xffffu);
-                v[2 * q + 1] = (short)(pl >> 16);
-              }
-            }
+            for (int j = 0; j < 8; ++j) v[j] = (b < B) ? dca::f2bf(h0[b * H + k + j]) : (short)0;
             af[mt][ks] = v;
           }
-        if (__all(ok)) break;
-        if (spin_fail(spins, err, 1u)) { dead = true; break; }
-      }
-    }
-    // -------- partial gates over this wave's K quarter
+      } else {
+        const unsigned long long* slot = ring + (size_t)((t - 1) & 1) * B * HP;
+        const unsigned tag = (unsigned)t;
+        while (true) {
+          bool ok = true;
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt)
+          for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        dca::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            for (int ks = 0; ks < KS; ++ks) {
+              const int b = mt * 16 + lrow;
+              const int k = wv * (32 * KS) + ks * 32 + 8 * lkg;
+              bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+              if (b < B) {
+                const unsigned long long* g = slot + (size_t)b * HP + (k >> 1);
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt][ks], wf[nt][ks], acc, 0, 0, 0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[wv][mt][nt][lkg * 4 + r][lrow] = acc[r];
-      }
-    __syncthreads();
-    if (__syncthreads_or(dead)) break;
-    // -------- cell update for owned (b, unit) pairs, publish h_t granules
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int p = tid + r * kThreads;
-      float hv = 0.f;
-      if (p < P) {
-        const int b = p >> 3, jj = p & 7;
-        const int mt = b >> 4, row = b & 15;
-        float pre[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const int c = q * kUw + jj;
-          const int nt = c >> 4, cc = c & 15;
-          pre[q] = red[0][mt][nt][row][cc] + red[1][mt][nt][row][cc] + red[2][mt][nt][row][cc] +
-                   red[3][mt][nt][row][cc] + xv[r][q];
+                for (int q = 0; q < 4; ++q) {
+                  const unsigned long long x = ld_granule(g + q);
+                  ok &= (unsigned)(x >> 32) == tag;
+                  const unsigned pl = (unsigned)x;
+                  v[2 * q] = (short)(pl & 0xffffu);
+                  v[2 * q + 1] = (short)(pl >> 16);
+                }
+              }
+              af[mt][ks] = v;
+            }
+          if (__all(ok)) break;
+          if (spin_fail(spins, err, 1u)) { dead = true; break; }
         }
-        const float ig = dca::sigmoidf_(pre[0]);
-        const float fg = dca::sigmoidf_(pre[1]);
-        const float gg = dca::tanhf_(pre[2]);
-        const float og = dca::sigmoidf_(pre[3]);
-        const float c = fg * creg[r] + ig * gg;
-        hv = og * dca::tanhf_(c);
-        creg[r] = c;
-        hreg[r] = hv;
-        const size_t bt = (size_t)b * S + t;
-        hs[bt * H + j0 + jj] = dca::f2bf(hv);
-        if (hsf) hsf[bt * H + j0 + jj] = hv;
-        cs[bt * H + j0 + jj] = c;
-        float* gp = gates + bt * G4 + j0 + jj;
-        gp[0] = ig;
-        gp[H] = fg;
-        gp[2 * H] = gg;
-        gp[3 * H] = og;
       }
-      // pair units (jj, jj+1) into one granule: lanes p and p+1 are adjacent in the wave
-      const float hnext = __shfl_down(hv, 1, 64);
-      if (p < P && (p & 1) == 0) {
-        const int b = p >> 3, jj = p & 7;
-        const unsigned pl = (unsigned)(unsigned short)dca::f2bf(hv) |
-                            ((unsigned)(unsigned short)dca::f2bf(hnext) << 16);
-        unsigned long long* gptr = ring + (size_t)(t & 1) * B * HP + (size_t)b * HP + ((j0 + jj) >> 1);
-        const unsigned long long gv = ((unsigned long long)(unsigned)(t + 1) << 32) | pl;
-        if (LOCAL) st_granule_local(gptr, gv); else st_granule(gptr, gv);
+      if (dead && lane == 0) abort_flag = 1;
+      // -------- partial gates over this wave's K quarter → LDS
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          dca::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[mt][ks], wf[nt][ks], acc, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[par][wv][mt][nt][lkg * 4 + r][lrow] = acc[r];
+        }
+#pragma unroll
+      for (int i = 0; i < NXV; ++i) {
+        const int idx = tid + 256 * i;
+        if (idx < 4 * P) xpl[par][idx & 3][idx >> 2] = xv[i];
       }
     }
-    __syncthreads();   // red[] is rewritten next step
-  }
+    lds_barrier();
+    if (abort_flag) break;
+    if (!poller) {
+      // -------- cell update for every owned pair, publish h_t
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int p = tid + r * kThreads;
-    if (p < P) {
-      const int b = p >> 3, jj = p & 7;
-      hn[b * H + j0 + jj] = hreg[r];
-      cn[b * H + j0 + jj] = creg[r];
+      for (int r = 0; r < NPR; ++r) {
+        const int p = lane + 64 * r;
+        if (64 * r >= P) break;                     // wave-uniform
+        float hv = 0.f;
+        if (p < P) {
+          const int b = p >> 3, jj = p & 7;
+          const int mt = b >> 4, row = b & 15;
+          float pre[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const int c = q * kUw + jj;
+            const int nt = c >> 4, cc = c & 15;
+            pre[q] = red[par][0][mt][nt][row][cc] + red[par][1][mt][nt][row][cc] + red[par][2][mt][nt][row][cc] +
+                     red[par][3][mt][nt][row][cc] + xpl[par][q][p];
+          }
+          const float ig = dca::sigmoidf_(pre[0]);
+          const float fg = dca::sigmoidf_(pre[1]);
+          const float gg = dca::tanhf_(pre[2]);
+          const float og = dca::sigmoidf_(pre[3]);
+          const float c = fg * creg[r] + ig * gg;
+          hv = og * dca::tanhf_(c);
+          creg[r] = c;
+          hreg[r] = hv;
+          const size_t bt = (size_t)b * S + t;
+          hs[bt * H + j0 + jj] = dca::f2bf(hv);
+          if (hsf) hsf[bt * H + j0 + jj] = hv;
+          cs[bt * H + j0 + jj] = c;
+          float* gp = gates + bt * G4 + j0 + jj;
+          gp[0] = ig;
+          gp[H] = fg;
+          gp[2 * H] = gg;
+          gp[3 * H] = og;
+        }
+        const float hnext = __shfl_down(hv, 1, 64);
+        if (p < P && (p & 1) == 0) {
+          const int b = p >> 3, jj = p & 7;
+          const unsigned pl = (unsigned)(unsigned short)dca::f2bf(hv) |
+                              ((unsigned)(unsigned short)dca::f2bf(hnext) << 16);
+          st_granule(ring + (size_t)par * B * HP + (size_t)b * HP + ((j0 + jj) >> 1),
+                     ((unsigned long long)(unsigned)(t + 1) << 32) | pl);
+        }
+      }
+    }
+  }
+  if (!poller && !abort_flag) {
+#pragma unroll
+    for (int r = 0; r < NPR; ++r) {
+      const int p = lane + 64 * r;
+      if (p < P) {
+        hn[(p >> 3) * H + j0 + (p & 7)] = hreg[r];
+        cn[(p >> 3) * H + j0 + (p & 7)] = creg[r];
+      }
     }
   }
 }
 
 // =============================================================================================================
-// Backward
+// Backward — 8 waves: waves 0-3 are POLLERS (gather Σ partials of step t+1 for the owned units and prefetch the
+// step's saved activations into LDS; no global stores), waves 4-7 are PUBLISHERS (each recomputes the owned units'
+// gate gradients from LDS — redundantly, so no publisher-side barrier is needed — then multiplies its own quarter
+// of the W slice and publishes the B×H/4 partial as {tag, f32} granules; wave 4 also writes ∂gates).
 // =============================================================================================================
-// dhs    (B, S, H)  f32  ∂L/∂h_t from everything above the LSTM (not including the recurrence)
-// gates  (B, S, 4H) f32  activated gates from the forward
-// cs     (B, S, H)  f32  c_t from the forward; c0 (B, H)
+// dhs    (B, S, H)  f32  ∂L/∂h_t from everything above the LSTM
+// gates  (B, S, 4H) f32  activated gates;  cs (B,S,H) f32 c_t;  c0 (B,H)
 // dhn,dcn(B, H)     f32  ∂L/∂(h_S, c_S) (may be null)
-// dgates (B, S, 4H) f32  out: ∂L/∂(gate pre-activations) (input to the weight-gradient GEMMs)
-// dh0,dc0(B, H)     f32  out
-// ring   (2, NWG, B, H) u64 granules {tag, f32} (zeroed)
+// dgates (B, S, 4H) f32  out: ∂L/∂(gate pre-activations);  dh0, dc0 (B,H) out
+// ring   (2, NWG, B, H) u64 granules {tag = t+1, f32} (zeroed)
 template <int MT, int KS>
-__global__ __launch_bounds__(kThreads) void lstm_bwd_kernel(const float* __restrict__ dhs, const float* __restrict__ gates,
-                                                            const float* __restrict__ cs, const float* __restrict__ c0,
-                                                            const float* __restrict__ dhn, const float* __restrict__ dcn,
-                                                            const short* __restrict__ whh, float* __restrict__ dgates,
-                                                            float* __restrict__ dh0, float* __restrict__ dc0,
-                                                            unsigned long long* ring, unsigned* err, int B, int S) {
+__global__ __launch_bounds__(kBwdThreads) void lstm_bwd_kernel(const float* __restrict__ dhs,
+                                                               const float* __restrict__ gates,
+                                                               const float* __restrict__ cs,
+                                                               const float* __restrict__ c0,
+                                                               const float* __restrict__ dhn,
+                                                               const float* __restrict__ dcn,
+                                                               const short* __restrict__ whh,
+                                                               float* __restrict__ dgates, float* __restrict__ dh0,
+                                                               float* __restrict__ dc0, unsigned long long* ring,
+                                                               unsigned* err, int Btot, int Bc, int S) {
   constexpr int H = 128 * KS;
   constexpr int G4 = 4 * H;
   constexpr int NWG = H / kUw;
-  constexpr int NT_W = H / 64;          // N tiles (16 columns) per wave: H/16 tiles over 4 waves
-  const int w = blockIdx.x;
+  constexpr int NT_W = H / 64;          // 16-column N tiles per publisher wave
+  const int chain = blockIdx.x / NWG;
+  const int b0 = chain * Bc;
+  const int B = min(Bc, Btot - b0);
+  dhs += (size_t)b0 * S * H; gates += (size_t)b0 * S * G4; cs += (size_t)b0 * S * H; c0 += (size_t)b0 * H;
+  if (dhn) dhn += (size_t)b0 * H;
+  if (dcn) dcn += (size_t)b0 * H;
+  dgates += (size_t)b0 * S * G4; dh0 += (size_t)b0 * H; dc0 += (size_t)b0 * H;
+  ring += (size_t)chain * 2 * NWG * Bc * H;
+  const int w = blockIdx.x % NWG;
   const int j0 = w * kUw;
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int lrow = lane & 15, lkg = lane >> 4;
-
-  __shared__ short dgl[MT * 16][40];            // dG_blk (bf16) as the MFMA A operand, padded rows
-  __shared__ float dpart[4][512];               // per-wave partial sums of dh_rec (pairs ≤ 512)
-
-  // ---- W slice as B fragments: B[k][col] = W[row(k)][col], row(k) = (k/8)·H + j0 + k%8, k = 8·lkg + j.
-  bf16x8 wf[NT_W];
-#pragma unroll
-  for (int n = 0; n < NT_W; ++n) {
-    const int col = (wv * NT_W + n) * 16 + lrow;
-    bf16x8 v;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = whh[(size_t)(lkg * H + j0 + j) * H + col];
-    wf[n] = v;
-  }
-  // zero the padding rows of the A operand once
-  for (int i = tid; i < MT * 16 * 40; i += kThreads) (&dgl[0][0])[i] = 0;
-
   const int P = B * kUw;
-  float dcreg[2];
-#pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int p = tid + r * kThreads;
-    dcreg[r] = 0.f;
-    if (p < P && dcn) dcreg[r] = dcn[(p >> 3) * H + j0 + (p & 7)];
-  }
+  const bool poller = wv < 4;
+  const int pw = wv - 4;
+
+  constexpr int PMAX = 128 * MT;
+  __shared__ float dpart[2][4][PMAX];
+  __shared__ float inp[2][7][PMAX];        // i, f, g, o, c_t, c_{t-1}, dhs_t
+  __shared__ short dgl[4][MT * 16][40];
+  __shared__ int abort_flag;
+  if (tid == 0) abort_flag = 0;
+  for (int i = tid; i < 4 * MT * 16 * 40; i += kBwdThreads) (&dgl[0][0][0])[i] = 0;
   __syncthreads();
 
-  unsigned spins = 0;
-  bool dead = false, bdead = false;
-  // Gather Σ_w' partial_{w'}[b][J_w] of step `ts` (tag ts+1) for every owned pair. Wave pg sums producers
-  // [pg·NWG/4, (pg+1)·NWG/4) for 64 pairs per pass; the 4 partial sums meet in LDS (one barrier).
-  auto gather = [&](int ts, float (&dh)[2]) {
-    const unsigned long long* slot = ring + (size_t)(ts & 1) * NWG * B * H;
-    const unsigned tag = (unsigned)(ts + 1);
-    const int pg = wv;
-    const int npass = (P + 63) >> 6;
-    for (int pass = 0; pass < npass; ++pass) {
-      const int p = pass * 64 + lane;
-      if (p < P) {
-        const int b = p >> 3, jj = p & 7;
-        float s = 0.f;
-        while (true) {
-          bool ok = true;
-          s = 0.f;
-#pragma unroll 4
-          for (int i = 0; i < NWG / 4; ++i) {
-            const int wp = pg * (NWG / 4) + i;
-            const unsigned long long x = ld_granule(slot + ((size_t)wp * B + b) * H + j0 + jj);
-            ok &= (unsigned)(x >> 32) == tag;
-            s += __uint_as_float((unsigned)x);
-          }
-          if (__all(ok)) break;
-          if (spin_fail(spins, err, 2u)) { dead = true; break; }
-        }
-        dpart[pg][p] = s;
-      }
-    }
-    __syncthreads();
+  bf16x8 wf[NT_W];
+  constexpr int NPR = PMAX / 64;
+  float dcreg[NPR];
+  if (!poller) {
 #pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int p = tid + r * kThreads;
-      dh[r] = (p < P) ? dpart[0][p] + dpart[1][p] + dpart[2][p] + dpart[3][p] : 0.f;
+    for (int n = 0; n < NT_W; ++n) {
+      const int col = (pw * NT_W + n) * 16 + lrow;
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = whh[(size_t)(lkg * H + j0 + j) * H + col];
+      wf[n] = v;
     }
-  };
+#pragma unroll
+    for (int r = 0; r < NPR; ++r) {
+      const int p = lane + 64 * r;
+      dcreg[r] = (p < P && dcn) ? dcn[(p >> 3) * H + j0 + (p & 7)] : 0.f;
+    }
+  }
 
-  for (int t = S - 1; t >= 0; --t) {
-    float dh[2] = {0.f, 0.f};
-    if (t == S - 1) {
+  unsigned spins = 0;
+  for (int k = 0; k <= S; ++k) {
+    const int t = S - 1 - k;            // step handled by the publishers this iteration (-1: final gather)
+    const int par = k & 1;
+    if (poller) {
+      // -------- prefetch the saved activations of step t (7 values per pair)
+      constexpr int NIN = (7 * PMAX + 255) / 256;
+      float iv[NIN];
+      if (t >= 0) {
 #pragma unroll
-      for (int r = 0; r < 2; ++r) {
-        const int p = tid + r * kThreads;
-        if (p < P && dhn) dh[r] = dhn[(p >> 3) * H + j0 + (p & 7)];
+        for (int i = 0; i < NIN; ++i) {
+          const int idx = tid + 256 * i;
+          iv[i] = 0.f;
+          if (idx < 7 * P) {
+            const int p = idx % P, f = idx / P;
+            const int b = p >> 3, jj = p & 7;
+            const size_t bt = (size_t)b * S + t;
+            if (f < 4) iv[i] = gates[bt * G4 + f * H + j0 + jj];
+            else if (f == 4) iv[i] = cs[bt * H + j0 + jj];
+            else if (f == 5) iv[i] = (t > 0) ? cs[(bt - 1) * H + j0 + jj] : c0[b * H + j0 + jj];
+            else iv[i] = dhs[bt * H + j0 + jj];
+          }
+        }
       }
-    } else {
-      gather(t + 1, dh);
-      if (__syncthreads_or(dead)) { bdead = true; break; }
-    }
-    // -------- elementwise: dG_t for owned pairs
-#pragma unroll
-    for (int r = 0; r < 2; ++r) {
-      const int p = tid + r * kThreads;
-      if (p < P) {
-        const int b = p >> 3, jj = p & 7;
-        const size_t bt = (size_t)b * S + t;
-        const float* gp = gates + bt * G4 + j0 + jj;
-        const float ig = gp[0], fg = gp[H], gg = gp[2 * H], og = gp[3 * H];
-        const float c = cs[bt * H + j0 + jj];
-        const float cprev = (t > 0) ? cs[(bt - 1) * H + j0 + jj] : c0[b * H + j0 + jj];
-        const float tc = dca::tanhf_(c);
-        const float dht = dhs[bt * H + j0 + jj] + dh[r];
-        const float dc = dcreg[r] + dht * og * (1.f - tc * tc);
-        const float d_o = dht * tc * og * (1.f - og);
-        const float d_i = dc * gg * ig * (1.f - ig);
-        const float d_f = dc * cprev * fg * (1.f - fg);
-        const float d_g = dc * ig * (1.f - gg * gg);
-        dcreg[r] = dc * fg;
-        float* dg = dgates + bt * G4 + j0 + jj;
-        dg[0] = d_i;
-        dg[H] = d_f;
-        dg[2 * H] = d_g;
-        dg[3 * H] = d_o;
-        dgl[b][0 * 8 + jj] = dca::f2bf(d_i);
-        dgl[b][1 * 8 + jj] = dca::f2bf(d_f);
-        dgl[b][2 * 8 + jj] = dca::f2bf(d_g);
-        dgl[b][3 * 8 + jj] = dca::f2bf(d_o);
+      // -------- recurrent gradient for h_t: Σ_w' partial_{w'} of step t+1 (k = 0: the given ∂L/∂h_S)
+      bool dead = false;
+      const int pg = wv;
+      for (int pass = 0; pass * 64 < P; ++pass) {
+        const int p = pass * 64 + lane;
+        float s = 0.f;
+        if (k == 0) {
+          if (pg == 0 && p < P && dhn) s = dhn[(p >> 3) * H + j0 + (p & 7)];
+        } else if (p < P) {
+          const unsigned long long* slot = ring + (size_t)((t + 1) & 1) * NWG * B * H;
+          const unsigned tag = (unsigned)(t + 2);
+          const int b = p >> 3, jj = p & 7;
+          while (true) {
+            bool ok = true;
+            s = 0.f;
+#pragma unroll 4
+            for (int i = 0; i < NWG / 4; ++i) {
+              const int wp = pg * (NWG / 4) + i;
+              const unsigned long long x = ld_granule(slot + ((size_t)wp * B + b) * H + j0 + jj);
+              ok &= (unsigned)(x >> 32) == tag;
+              s += __uint_as_float((unsigned)x);
+            }
+            if (__all(ok)) break;
+            if (spin_fail(spins, err, 2u)) { dead = true; break; }
+          }
+        }
+        if (p < P) dpart[par][pg][p] = s;
       }
-    }
-    __syncthreads();
-    // -------- partial_w = dG_blk (B×32) · W_blk (32×H), publish as {tag=t+1, f32} granules
-    unsigned long long* slot = ring + (size_t)(t & 1) * NWG * B * H + (size_t)w * B * H;
+      if (dead && lane == 0) abort_flag = 1;
+      if (t >= 0) {
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(&dgl[mt * 16 + lrow][8 * lkg]);
-#pragma unroll
-      for (int n = 0; n < NT_W; ++n) {
-        dca::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[n], acc, 0, 0, 0);
-        const int col = (wv * NT_W + n) * 16 + lrow;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int b = mt * 16 + lkg * 4 + r;
-          if (b < B)
-            st_granule(slot + (size_t)b * H + col,
-                       ((unsigned long long)(unsigned)(t + 1) << 32) | __float_as_uint(acc[r]));
+        for (int i = 0; i < NIN; ++i) {
+          const int idx = tid + 256 * i;
+          if (idx < 7 * P) inp[par][idx / P][idx % P] = iv[i];
         }
       }
     }
-    __syncthreads();   // dgl[] is rewritten next step
-  }
-  // -------- dh0 = Σ partials of step 0, dc0 = carried dc
-  float dh[2] = {0.f, 0.f};
-  if (!bdead) gather(0, dh);
+    lds_barrier();
+    if (abort_flag) break;
+    if (t < 0) {
+      // final gather done: ∂L/∂h0
+      if (poller) {
+        for (int p = tid; p < P; p += 256)
+          dh0[(p >> 3) * H + j0 + (p & 7)] = dpart[par][0][p] + dpart[par][1][p] + dpart[par][2][p] + dpart[par][3][p];
+      }
+      break;
+    }
+    if (!poller) {
+      // -------- gate gradients of the owned units (every publisher wave computes all pairs)
 #pragma unroll
-  for (int r = 0; r < 2; ++r) {
-    const int p = tid + r * kThreads;
-    if (p < P) {
-      dh0[(p >> 3) * H + j0 + (p & 7)] = dh[r];
-      dc0[(p >> 3) * H + j0 + (p & 7)] = dcreg[r];
+      for (int r = 0; r < NPR; ++r) {
+        const int p = lane + 64 * r;
+        if (64 * r >= P) break;
+        if (p < P) {
+          const int b = p >> 3, jj = p & 7;
+          const float ig = inp[par][0][p], fg = inp[par][1][p], gg = inp[par][2][p], og = inp[par][3][p];
+          const float c = inp[par][4][p], cprev = inp[par][5][p];
+          const float dht = inp[par][6][p] + dpart[par][0][p] + dpart[par][1][p] + dpart[par][2][p] +
+                            dpart[par][3][p];
+          const float tc = dca::tanhf_(c);
+          const float dc = dcreg[r] + dht * og * (1.f - tc * tc);
+          const float d_o = dht * tc * og * (1.f - og);
+          const float d_i = dc * gg * ig * (1.f - ig);
+          const float d_f = dc * cprev * fg * (1.f - fg);
+          const float d_g = dc * ig * (1.f - gg * gg);
+          dcreg[r] = dc * fg;
+          dgl[pw][b][0 * 8 + jj] = dca::f2bf(d_i);
+          dgl[pw][b][1 * 8 + jj] = dca::f2bf(d_f);
+          dgl[pw][b][2 * 8 + jj] = dca::f2bf(d_g);
+          dgl[pw][b][3 * 8 + jj] = dca::f2bf(d_o);
+          if (pw == 0) {
+            float* dg = dgates + ((size_t)b * S + t) * G4 + j0 + jj;
+            dg[0] = d_i;
+            dg[H] = d_f;
+            dg[2 * H] = d_g;
+            dg[3 * H] = d_o;
+            if (t == 0) dc0[b * H + j0 + jj] = dcreg[r];
+          }
+        }
+      }
+      // -------- partial = dG_blk (B×32) · W_blk (32 × this wave's H/4 columns) → granules of step t
+      unsigned long long* slot = ring + (size_t)(t & 1) * NWG * B * H + (size_t)w * B * H;
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(&dgl[pw][mt * 16 + lrow][8 * lkg]);
+#pragma unroll
+        for (int n = 0; n < NT_W; ++n) {
+          dca::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+          acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[n], acc, 0, 0, 0);
+          const int col = (pw * NT_W + n) * 16 + lrow;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int b = mt * 16 + lkg * 4 + r;
+            if (b < B)
+              st_granule(slot + (size_t)b * H + col,
+                         ((unsigned long long)(unsigned)(t + 1) << 32) | __float_as_uint(acc[r]));
+          }
+        }
+      }
     }
   }
+}
+
+// Chains: sequences are split into independent groups of Bc ≤ 16·MT (MT ≤ 2 keeps every variant spill-free), all
+// run concurrently. Total workgroups = chains·H/8 ≤ 256 so every chain is co-resident.
+inline void plan_chains(int B, int H, int& nch, int& Bc, int& MT) {
+  const int nwg = H / kUw;
+  const int max_ch = 256 / nwg;
+  nch = (B + 31) / 32;
+  if (nch > max_ch) nch = max_ch;
+  Bc = (B + nch - 1) / nch;
+  MT = Bc <= 16 ? 1 : 2;
 }
 
 template <int MT, int KS>
 hipError_t launch_fwd(const float* xp, const short* whh, const float* h0, const float* c0, short* hs, float* hsf,
                       float* cs, float* gates, float* hn, float* cn, unsigned long long* ring, unsigned* err, int B,
-                      int S, int local, hipStream_t st) {
+                      int Bc, int nch, int S, hipStream_t st) {
   constexpr int H = 128 * KS;
-  hipError_t e = hipMemsetAsync(ring, 0, sizeof(unsigned long long) * 2 * B * (H / 2), st);
+  hipError_t e = hipMemsetAsync(ring, 0, sizeof(unsigned long long) * (size_t)nch * 2 * Bc * (H / 2), st);
   if (e != hipSuccess) return e;
-  if (local)
-    lstm_fwd_kernel<MT, KS, true><<<8 * (H / kUw), kThreads, 0, st>>>(xp, whh, h0, c0, hs, hsf, cs, gates, hn, cn,
-                                                                      ring, err, B, S);
-  else
-    lstm_fwd_kernel<MT, KS, false><<<H / kUw, kThreads, 0, st>>>(xp, whh, h0, c0, hs, hsf, cs, gates, hn, cn, ring,
-                                                                 err, B, S);
+  lstm_fwd_kernel<MT, KS><<<nch * (H / kUw), kFwdThreads, 0, st>>>(xp, whh, h0, c0, hs, hsf, cs, gates, hn, cn,
+                                                                   ring, err, B, Bc, S);
   return hipGetLastError();
 }
 
 template <int MT, int KS>
 hipError_t launch_bwd(const float* dhs, const float* gates, const float* cs, const float* c0, const float* dhn,
                       const float* dcn, const short* whh, float* dgates, float* dh0, float* dc0,
-                      unsigned long long* ring, unsigned* err, int B, int S, hipStream_t st) {
+                      unsigned long long* ring, unsigned* err, int B, int Bc, int nch, int S, hipStream_t st) {
   constexpr int H = 128 * KS;
-  hipError_t e = hipMemsetAsync(ring, 0, sizeof(unsigned long long) * 2 * (H / kUw) * B * H, st);
+  hipError_t e = hipMemsetAsync(ring, 0, sizeof(unsigned long long) * (size_t)nch * 2 * (H / kUw) * Bc * H, st);
   if (e != hipSuccess) return e;
-  lstm_bwd_kernel<MT, KS><<<H / kUw, kThreads, 0, st>>>(dhs, gates, cs, c0, dhn, dcn, whh, dgates, dh0, dc0, ring, err,
-                                                        B, S);
+  lstm_bwd_kernel<MT, KS><<<nch * (H / kUw), kBwdThreads, 0, st>>>(dhs, gates, cs, c0, dhn, dcn, whh, dgates, dh0,
+                                                                   dc0, ring, err, B, Bc, S);
   return hipGetLastError();
 }
 
@@ -461,25 +527,32 @@ hipError_t launch_bwd(const float* dhs, const float* gates, const float* cs, con
     case 0x11: return __VA_ARGS__(1, 1); case 0x12: return __VA_ARGS__(1, 2);      \
     case 0x14: return __VA_ARGS__(1, 4); case 0x21: return __VA_ARGS__(2, 1);      \
     case 0x22: return __VA_ARGS__(2, 2); case 0x24: return __VA_ARGS__(2, 4);      \
-    case 0x41: return __VA_ARGS__(4, 1); case 0x42: return __VA_ARGS__(4, 2);      \
-    case 0x44: return __VA_ARGS__(4, 4);                                           \
     default: return hipErrorInvalidValue;                                          \
   }
 
-static int mt_for(int B) { return B <= 16 ? 1 : (B <= 32 ? 2 : 4); }
+static bool lstm_shape_ok(int B, int H) {
+  if (B < 1 || (H != 128 && H != 256 && H != 512)) return false;
+  return B <= 32 * (256 / (H / kUw));
+}
 
-// Ring sizes (u64 elements): forward 2·B·H/2, backward 2·(H/8)·B·H.
+// Max batch per launch for hidden size H (chains of ≤ 32 sequences, ≤ 256 workgroups).
+extern "C" int dca_lstm_max_batch(int H) { return 32 * (256 / (H / kUw)); }
+
+// Ring sizes (u64 elements) for the chain plan of (B, H).
 extern "C" size_t dca_lstm_ring_elems(int B, int H, int backward) {
-  return backward ? (size_t)2 * (H / kUw) * B * H : (size_t)2 * B * (H / 2);
+  int nch, Bc, MT;
+  plan_chains(B, H, nch, Bc, MT);
+  return backward ? (size_t)nch * 2 * (H / kUw) * Bc * H : (size_t)nch * 2 * Bc * (H / 2);
 }
 
 extern "C" hipError_t dca_lstm_fwd(const float* xp, const short* whh, const float* h0, const float* c0, short* hs,
                                    float* hsf, float* cs, float* gates, float* hn, float* cn,
-                                   unsigned long long* ring, unsigned* err, int B, int S, int H, int local,
-                                   hipStream_t st) {
-  if (B < 1 || B > 64 || S < 1 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
-  const int MT = mt_for(B), KS = H / 128;
-#define DCA_F(mt, ks) launch_fwd<mt, ks>(xp, whh, h0, c0, hs, hsf, cs, gates, hn, cn, ring, err, B, S, local, st)
+                                   unsigned long long* ring, unsigned* err, int B, int S, int H, hipStream_t st) {
+  if (!lstm_shape_ok(B, H) || S < 1) return hipErrorInvalidValue;
+  int nch, Bc, MT;
+  plan_chains(B, H, nch, Bc, MT);
+  const int KS = H / 128;
+#define DCA_F(mt, ks) launch_fwd<mt, ks>(xp, whh, h0, c0, hs, hsf, cs, gates, hn, cn, ring, err, B, Bc, nch, S, st)
   DCA_DISPATCH_MT_KS(MT, KS, DCA_F)
 #undef DCA_F
 }
@@ -488,9 +561,11 @@ extern "C" hipError_t dca_lstm_bwd(const float* dhs, const float* gates, const f
                                    const float* dhn, const float* dcn, const short* whh, float* dgates, float* dh0,
                                    float* dc0, unsigned long long* ring, unsigned* err, int B, int S, int H,
                                    hipStream_t st) {
-  if (B < 1 || B > 64 || S < 1 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
-  const int MT = mt_for(B), KS = H / 128;
-#define DCA_B(mt, ks) launch_bwd<mt, ks>(dhs, gates, cs, c0, dhn, dcn, whh, dgates, dh0, dc0, ring, err, B, S, st)
+  if (!lstm_shape_ok(B, H) || S < 1) return hipErrorInvalidValue;
+  int nch, Bc, MT;
+  plan_chains(B, H, nch, Bc, MT);
+  const int KS = H / 128;
+#define DCA_B(mt, ks) launch_bwd<mt, ks>(dhs, gates, cs, c0, dhn, dcn, whh, dgates, dh0, dc0, ring, err, B, Bc, nch, S, st)
   DCA_DISPATCH_MT_KS(MT, KS, DCA_B)
 #undef DCA_B
 }

@@ -15,10 +15,6 @@ import torch
 
 from . import require
 
-MAX_B = 64
-# Hand-off mode of the forward recurrence: 0 = agent-scope write-through granules (placement independent),
-# 1 = XCD-local (all workgroups dealt to one XCD, L2-resident granules; validated before use, see tests).
-FWD_LOCAL = 0
 
 
 def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
@@ -32,11 +28,12 @@ class _Recurrence(torch.autograd.Function):
         C = require()
         whh16 = w_hh.detach().to(torch.bfloat16).contiguous()
         B = xp.shape[0]
+        MAX_B = C.lstm_max_batch(w_hh.shape[1])
         outs = []
         for s in range(0, B, MAX_B):
             e = min(B, s + MAX_B)
             outs.append(C.lstm_fwd(xp[s:e].contiguous(), whh16, h0[s:e].contiguous(), c0[s:e].contiguous(), err,
-                                   True, FWD_LOCAL))
+                                   True))
         hs16, hsf, cs, gates, hn, cn = (torch.cat([o[i] for o in outs]) if len(outs) > 1 else outs[0][i]
                                         for i in range(6))
         ctx.save_for_backward(gates, cs, c0, whh16, hs16, h0)
@@ -50,6 +47,7 @@ class _Recurrence(torch.autograd.Function):
         gates, cs, c0, whh16, hs16, h0 = ctx.saved_tensors
         B, S, H = cs.shape
         dhs = dhs.contiguous() if dhs is not None else torch.zeros_like(cs)
+        MAX_B = C.lstm_max_batch(H)
         outs = []
         for s in range(0, B, MAX_B):
             e = min(B, s + MAX_B)

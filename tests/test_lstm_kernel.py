@@ -9,7 +9,7 @@ def _rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
-@pytest.mark.parametrize('B,S,H', [(5, 37, 128), (8, 64, 512), (24, 20, 256), (40, 16, 512), (64, 8, 128)])
+@pytest.mark.parametrize('B,S,H', [(5, 37, 128), (8, 64, 512), (24, 20, 256), (40, 16, 512), (64, 8, 128), (100, 9, 512), (300, 5, 128)])
 def test_lstm_fwd_bwd_matches_torch(gpu_ops, B, S, H):
     from dotaclient_amd.ops.lstm import lstm_sequence
     torch.manual_seed(B * 1000 + S)
