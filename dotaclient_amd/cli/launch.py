@@ -1,0 +1,105 @@
+"""Single-node job launcher: broker + learner rank(s) + actor processes (+ optional validation actor).
+
+The reference deploys this as k8s objects (ks-app/components/{rmq,optimizer,agent,agent-val}.jsonnet); this launcher
+runs the same topology on one machine (and is what ``deploy/`` manifests call per pod):
+
+    python -m dotaclient_amd.cli.launch --actors 4 --games-per-actor 16 --optimizers 1 --log-dir runs/exp1
+
+Children are supervised: an actor that exits is restarted (the reference relies on k8s restarting agent pods,
+agent.py:896-900); the learner is restarted with resume-from-checkpoint (``restartPolicy: OnFailure``,
+optimizer.jsonnet:82). Ctrl-C / SIGTERM stops the whole job.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import os
+import signal
+import subprocess
+import sys
+import time
+
+logger = logging.getLogger('dotaclient_amd.launch')
+
+
+def build_parser():
+    ap = argparse.ArgumentParser(formatter_class=argparse.ArgumentDefaultsHelpFormatter)
+    ap.add_argument('--port', type=int, default=5672)
+    ap.add_argument('--actors', type=int, default=2)
+    ap.add_argument('--games-per-actor', type=int, default=4)
+    ap.add_argument('--optimizers', type=int, default=1, help='learner ranks (one per GPU)')
+    ap.add_argument('--validation', type=int, default=0, help='number of validation actors')
+    ap.add_argument('--log-dir', type=str, default='runs/local')
+    ap.add_argument('--model-preset', type=str, default='lstm512')
+    ap.add_argument('--actor-device', type=str, default='cpu')
+    ap.add_argument('--max-restarts', type=int, default=5)
+    ap.add_argument('--duration', type=float, default=0.0, help='stop after N seconds (0 = run forever)')
+    ap.add_argument('optimizer_args', nargs=argparse.REMAINDER, help='extra args after -- go to the optimizer')
+    return ap
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    logging.basicConfig(format='%(asctime)s %(levelname)-8s %(message)s', level='INFO')
+    from ..transport.broker import TcpBrokerServer
+    srv = TcpBrokerServer('127.0.0.1', args.port).start()
+    logger.info('broker on 127.0.0.1:%d', srv.port)
+    py = sys.executable
+    extra = [a for a in args.optimizer_args if a != '--']
+    specs = {}
+    if args.optimizers > 1:
+        specs['optimizer'] = [py, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={args.optimizers}',
+                              '--master-addr', '127.0.0.1', '-m', 'dotaclient_amd.cli.optimizer']
+    else:
+        specs['optimizer'] = [py, '-m', 'dotaclient_amd.cli.optimizer']
+    specs['optimizer'] += ['--port', str(srv.port), '--log-dir', args.log_dir, '--model-preset', args.model_preset] + extra
+    for i in range(args.actors):
+        specs[f'actor{i}'] = [py, '-m', 'dotaclient_amd.cli.agent', '--port', str(srv.port), '--games',
+                              str(args.games_per_actor), '--device', args.actor_device, '--model-preset',
+                              args.model_preset, '--seed', str(1000 + i)]
+    for i in range(args.validation):
+        specs[f'val{i}'] = [py, '-m', 'dotaclient_amd.cli.agent', '--port', str(srv.port), '--validation', 'true',
+                            '--log-dir', os.path.join(args.log_dir, 'val'), '--model-preset', args.model_preset]
+    procs, restarts = {}, {k: 0 for k in specs}
+    for k, cmd in specs.items():
+        procs[k] = subprocess.Popen(cmd)
+    stop = {'flag': False}
+
+    def handler(*_):
+        stop['flag'] = True
+    signal.signal(signal.SIGINT, handler)
+    signal.signal(signal.SIGTERM, handler)
+    t0 = time.time()
+    rc = 0
+    try:
+        while not stop['flag']:
+            if args.duration and time.time() - t0 > args.duration:
+                break
+            for k, p in list(procs.items()):
+                code = p.poll()
+                if code is None:
+                    continue
+                if restarts[k] >= args.max_restarts:
+                    logger.error('%s exited with %s; restart budget exhausted', k, code)
+                    stop['flag'] = True
+                    rc = code or 1
+                    break
+                restarts[k] += 1
+                logger.warning('%s exited with %s; restarting (%d/%d)', k, code, restarts[k], args.max_restarts)
+                procs[k] = subprocess.Popen(specs[k])
+            time.sleep(1.0)
+    finally:
+        for p in procs.values():
+            if p.poll() is None:
+                p.terminate()
+        for p in procs.values():
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+        srv.stop()
+    return rc
+
+
+if __name__ == '__main__':
+    sys.exit(main())

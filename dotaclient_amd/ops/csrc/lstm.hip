@@ -382,33 +382,49 @@ __global__ __launch_bounds__(kBwdThreads) void lstm_bwd_kernel(const float* __re
           }
         }
       }
-      // -------- recurrent gradient for h_t: Σ_w' partial_{w'} of step t+1 (k = 0: the given ∂L/∂h_S)
+      // -------- recurrent gradient for h_t: Σ_w' partial_{w'} of step t+1 (k = 0: the given ∂L/∂h_S).
+      // All of this wave's granules (every pass of 64 pairs × its NWG/4 producers) are loaded in ONE poll round, so
+      // a step costs one hand-off round trip whatever the batch.
       bool dead = false;
       const int pg = wv;
-      for (int pass = 0; pass * 64 < P; ++pass) {
-        const int p = pass * 64 + lane;
-        float s = 0.f;
-        if (k == 0) {
-          if (pg == 0 && p < P && dhn) s = dhn[(p >> 3) * H + j0 + (p & 7)];
-        } else if (p < P) {
-          const unsigned long long* slot = ring + (size_t)((t + 1) & 1) * NWG * B * H;
-          const unsigned tag = (unsigned)(t + 2);
-          const int b = p >> 3, jj = p & 7;
-          while (true) {
-            bool ok = true;
-            s = 0.f;
-#pragma unroll 4
-            for (int i = 0; i < NWG / 4; ++i) {
-              const int wp = pg * (NWG / 4) + i;
-              const unsigned long long x = ld_granule(slot + ((size_t)wp * B + b) * H + j0 + jj);
-              ok &= (unsigned)(x >> 32) == tag;
-              s += __uint_as_float((unsigned)x);
-            }
-            if (__all(ok)) break;
-            if (spin_fail(spins, err, 2u)) { dead = true; break; }
-          }
+      constexpr int NPASS = PMAX / 64;
+      const int npass = (P + 63) >> 6;
+      float ssum[NPASS];
+      if (k == 0) {
+#pragma unroll
+        for (int ps = 0; ps < NPASS; ++ps) {
+          const int p = ps * 64 + lane;
+          ssum[ps] = (pg == 0 && p < P && dhn) ? dhn[(p >> 3) * H + j0 + (p & 7)] : 0.f;
         }
-        if (p < P) dpart[par][pg][p] = s;
+      } else {
+        const unsigned long long* slot = ring + (size_t)((t + 1) & 1) * NWG * B * H;
+        const unsigned tag = (unsigned)(t + 2);
+        while (true) {
+          bool ok = true;
+#pragma unroll
+          for (int ps = 0; ps < NPASS; ++ps) {
+            const int p = ps * 64 + lane;
+            float s = 0.f;
+            if (ps < npass && p < P) {
+              const int b = p >> 3, jj = p & 7;
+#pragma unroll 4
+              for (int i = 0; i < NWG / 4; ++i) {
+                const int wp = pg * (NWG / 4) + i;
+                const unsigned long long x = ld_granule(slot + ((size_t)wp * B + b) * H + j0 + jj);
+                ok &= (unsigned)(x >> 32) == tag;
+                s += __uint_as_float((unsigned)x);
+              }
+            }
+            ssum[ps] = s;
+          }
+          if (__all(ok)) break;
+          if (spin_fail(spins, err, 2u)) { dead = true; break; }
+        }
+      }
+#pragma unroll
+      for (int ps = 0; ps < NPASS; ++ps) {
+        const int p = ps * 64 + lane;
+        if (p < P) dpart[par][pg][p] = ssum[ps];
       }
       if (dead && lane == 0) abort_flag = 1;
       if (t >= 0) {
