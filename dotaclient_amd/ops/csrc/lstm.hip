@@ -182,31 +182,45 @@ __global__ __launch_bounds__(kFwdThreads) void lstm_fwd_kernel(const float* __re
       } else {
         const unsigned long long* slot = ring + (size_t)((t - 1) & 1) * B * HP;
         const unsigned tag = (unsigned)t;
+        // Issue EVERY granule load of the poll round before looking at any result: relaxed atomic loads are
+        // ordered memory operations for the scheduler, so interleaving load/use would serialise them into one
+        // round trip each. Rows ≥ B load row 0 (always valid memory) and are ignored.
+        unsigned long long gr[MT][KS][4];
         while (true) {
-          bool ok = true;
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
               const int b = mt * 16 + lrow;
               const int k = wv * (32 * KS) + ks * 32 + 8 * lkg;
-              bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-              if (b < B) {
-                const unsigned long long* g = slot + (size_t)b * HP + (k >> 1);
+              const unsigned long long* g = slot + (size_t)(b < B ? b : 0) * HP + (k >> 1);
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                  const unsigned long long x = ld_granule(g + q);
-                  ok &= (unsigned)(x >> 32) == tag;
-                  const unsigned pl = (unsigned)x;
-                  v[2 * q] = (short)(pl & 0xffffu);
-                  v[2 * q + 1] = (short)(pl >> 16);
-                }
-              }
-              af[mt][ks] = v;
+              for (int q = 0; q < 4; ++q) gr[mt][ks][q] = ld_granule(g + q);
             }
+          bool ok = true;
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+              for (int q = 0; q < 4; ++q) ok &= (unsigned)(gr[mt][ks][q] >> 32) == tag;
           if (__all(ok)) break;
           if (spin_fail(spins, err, 1u)) { dead = true; break; }
         }
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+            const bool valid = mt * 16 + lrow < B;
+            bf16x8 v;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const unsigned pl = valid ? (unsigned)gr[mt][ks][q] : 0u;
+              v[2 * q] = (short)(pl & 0xffffu);
+              v[2 * q + 1] = (short)(pl >> 16);
+            }
+            af[mt][ks] = v;
+          }
       }
       if (dead && lane == 0) abort_flag = 1;
       // -------- partial gates over this wave's K quarter → LDS
@@ -367,19 +381,19 @@ __global__ __launch_bounds__(kBwdThreads) void lstm_bwd_kernel(const float* __re
       constexpr int NIN = (7 * PMAX + 255) / 256;
       float iv[NIN];
       if (t >= 0) {
+        // branch-free address selection so every load of the prefetch is in flight together
 #pragma unroll
         for (int i = 0; i < NIN; ++i) {
-          const int idx = tid + 256 * i;
-          iv[i] = 0.f;
-          if (idx < 7 * P) {
-            const int p = idx % P, f = idx / P;
-            const int b = p >> 3, jj = p & 7;
-            const size_t bt = (size_t)b * S + t;
-            if (f < 4) iv[i] = gates[bt * G4 + f * H + j0 + jj];
-            else if (f == 4) iv[i] = cs[bt * H + j0 + jj];
-            else if (f == 5) iv[i] = (t > 0) ? cs[(bt - 1) * H + j0 + jj] : c0[b * H + j0 + jj];
-            else iv[i] = dhs[bt * H + j0 + jj];
-          }
+          const int idx0 = tid + 256 * i;
+          const int idx = idx0 < 7 * P ? idx0 : 0;
+          const int p = idx % P, f = idx / P;
+          const int b = p >> 3, jj = p & 7;
+          const size_t bt = (size_t)b * S + t;
+          const float* src = gates + bt * G4 + (f & 3) * H + j0 + jj;
+          src = (f == 4) ? cs + bt * H + j0 + jj : src;
+          src = (f == 5) ? ((t > 0) ? cs + (bt - 1) * H + j0 + jj : c0 + b * H + j0 + jj) : src;
+          src = (f == 6) ? dhs + bt * H + j0 + jj : src;
+          iv[i] = *src;
         }
       }
       // -------- recurrent gradient for h_t: Σ_w' partial_{w'} of step t+1 (k = 0: the given ∂L/∂h_S).
@@ -399,26 +413,32 @@ __global__ __launch_bounds__(kBwdThreads) void lstm_bwd_kernel(const float* __re
       } else {
         const unsigned long long* slot = ring + (size_t)((t + 1) & 1) * NWG * B * H;
         const unsigned tag = (unsigned)(t + 2);
+        constexpr int NPG = NWG / 4;                 // producers per poller wave
+        unsigned long long gr[NPASS][NPG];           // all loads of a round issued before any use (see forward)
         while (true) {
-          bool ok = true;
 #pragma unroll
           for (int ps = 0; ps < NPASS; ++ps) {
             const int p = ps * 64 + lane;
-            float s = 0.f;
-            if (ps < npass && p < P) {
-              const int b = p >> 3, jj = p & 7;
-#pragma unroll 4
-              for (int i = 0; i < NWG / 4; ++i) {
-                const int wp = pg * (NWG / 4) + i;
-                const unsigned long long x = ld_granule(slot + ((size_t)wp * B + b) * H + j0 + jj);
-                ok &= (unsigned)(x >> 32) == tag;
-                s += __uint_as_float((unsigned)x);
-              }
-            }
-            ssum[ps] = s;
+            const int pc = (ps < npass && p < P) ? p : 0;
+            const int b = pc >> 3, jj = pc & 7;
+#pragma unroll
+            for (int i = 0; i < NPG; ++i)
+              gr[ps][i] = ld_granule(slot + ((size_t)(pg * NPG + i) * B + b) * H + j0 + jj);
           }
+          bool ok = true;
+#pragma unroll
+          for (int ps = 0; ps < NPASS; ++ps)
+#pragma unroll
+            for (int i = 0; i < NPG; ++i) ok &= (unsigned)(gr[ps][i] >> 32) == tag;
           if (__all(ok)) break;
           if (spin_fail(spins, err, 2u)) { dead = true; break; }
+        }
+#pragma unroll
+        for (int ps = 0; ps < NPASS; ++ps) {
+          float s = 0.f;
+#pragma unroll
+          for (int i = 0; i < NPG; ++i) s += __uint_as_float((unsigned)gr[ps][i]);
+          ssum[ps] = (ps < npass && ps * 64 + lane < P) ? s : 0.f;
         }
       }
 #pragma unroll
