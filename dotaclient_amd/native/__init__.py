@@ -1,0 +1,9 @@
+"""Native host-side runtime (C++): protobuf featurizer, shared-memory ring, crc32c. Built by ``native/build.py``."""
+from __future__ import annotations
+
+try:
+    from ._native import ShmRing, crc32c, featurize_batch  # noqa: F401
+    AVAILABLE = True
+except ImportError:  # pragma: no cover - not built yet
+    AVAILABLE = False
+    ShmRing = crc32c = featurize_batch = None

@@ -182,28 +182,51 @@ __global__ __launch_bounds__(kFwdThreads) void lstm_fwd_kernel(const float* __re
       } else {
         const unsigned long long* slot = ring + (size_t)((t - 1) & 1) * B * HP;
         const unsigned tag = (unsigned)t;
-        // Issue EVERY granule load of the poll round before looking at any result: relaxed atomic loads are
-        // ordered memory operations for the scheduler, so interleaving load/use would serialise them into one
-        // round trip each. Rows ≥ B load row 0 (always valid memory) and are ignored.
+        // Two-phase poll. (1) PROBE: one granule per fragment (each 8-value fragment comes from exactly one
+        // producer workgroup) until every probed tag matches — cheap, so spinning does not flood the memory
+        // system. (2) FETCH: issue every granule load before looking at any result (relaxed atomic loads are
+        // ordered for the scheduler: interleaved load/use would serialise them), verify, refetch if needed.
         unsigned long long gr[MT][KS][4];
         while (true) {
+          bool ok = true;
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
               const int b = mt * 16 + lrow;
               const int k = wv * (32 * KS) + ks * 32 + 8 * lkg;
-              const unsigned long long* g = slot + (size_t)(b < B ? b : 0) * HP + (k >> 1);
+              if (b < B) gr[mt][ks][3] = ld_granule(slot + (size_t)b * HP + (k >> 1) + 3);
+            }
 #pragma unroll
-              for (int q = 0; q < 4; ++q) gr[mt][ks][q] = ld_granule(g + q);
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks)
+              if (mt * 16 + lrow < B) ok &= (unsigned)(gr[mt][ks][3] >> 32) == tag;
+          if (__all(ok)) break;
+          if (spin_fail(spins, err, 1u)) { dead = true; break; }
+        }
+        while (!dead) {
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+            for (int ks = 0; ks < KS; ++ks) {
+              const int b = mt * 16 + lrow;
+              const int k = wv * (32 * KS) + ks * 32 + 8 * lkg;
+              if (b < B) {
+                const unsigned long long* g = slot + (size_t)b * HP + (k >> 1);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) gr[mt][ks][q] = ld_granule(g + q);
+              }
             }
           bool ok = true;
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
+              if (mt * 16 + lrow < B) {
 #pragma unroll
-              for (int q = 0; q < 4; ++q) ok &= (unsigned)(gr[mt][ks][q] >> 32) == tag;
+                for (int q = 0; q < 4; ++q) ok &= (unsigned)(gr[mt][ks][q] >> 32) == tag;
+              }
           if (__all(ok)) break;
           if (spin_fail(spins, err, 1u)) { dead = true; break; }
         }
@@ -414,22 +437,44 @@ __global__ __launch_bounds__(kBwdThreads) void lstm_bwd_kernel(const float* __re
         const unsigned long long* slot = ring + (size_t)((t + 1) & 1) * NWG * B * H;
         const unsigned tag = (unsigned)(t + 2);
         constexpr int NPG = NWG / 4;                 // producers per poller wave
-        unsigned long long gr[NPASS][NPG];           // all loads of a round issued before any use (see forward)
+        unsigned long long gr[NPASS][NPG];
+        // (1) PROBE: each lane checks ONE producer of its pair (lanes rotate over the producers), so the wave
+        //     as a whole samples every producer with a single load per lane per round.
         while (true) {
+          bool ok = true;
 #pragma unroll
           for (int ps = 0; ps < NPASS; ++ps) {
             const int p = ps * 64 + lane;
-            const int pc = (ps < npass && p < P) ? p : 0;
-            const int b = pc >> 3, jj = pc & 7;
+            if (ps < npass && p < P) {
+              const int wp = pg * NPG + (lane % NPG);
+              gr[ps][0] = ld_granule(slot + ((size_t)wp * B + (p >> 3)) * H + j0 + (p & 7));
+            }
+          }
 #pragma unroll
-            for (int i = 0; i < NPG; ++i)
-              gr[ps][i] = ld_granule(slot + ((size_t)(pg * NPG + i) * B + b) * H + j0 + jj);
+          for (int ps = 0; ps < NPASS; ++ps)
+            if (ps < npass && ps * 64 + lane < P) ok &= (unsigned)(gr[ps][0] >> 32) == tag;
+          if (__all(ok)) break;
+          if (spin_fail(spins, err, 2u)) { dead = true; break; }
+        }
+        // (2) FETCH every granule of the round, all loads in flight before any use; verify, refetch if needed.
+        while (!dead) {
+#pragma unroll
+          for (int ps = 0; ps < NPASS; ++ps) {
+            const int p = ps * 64 + lane;
+            if (ps < npass && p < P) {
+              const int b = p >> 3, jj = p & 7;
+#pragma unroll
+              for (int i = 0; i < NPG; ++i)
+                gr[ps][i] = ld_granule(slot + ((size_t)(pg * NPG + i) * B + b) * H + j0 + jj);
+            }
           }
           bool ok = true;
 #pragma unroll
           for (int ps = 0; ps < NPASS; ++ps)
+            if (ps < npass && ps * 64 + lane < P) {
 #pragma unroll
-            for (int i = 0; i < NPG; ++i) ok &= (unsigned)(gr[ps][i] >> 32) == tag;
+              for (int i = 0; i < NPG; ++i) ok &= (unsigned)(gr[ps][i] >> 32) == tag;
+            }
           if (__all(ok)) break;
           if (spin_fail(spins, err, 2u)) { dead = true; break; }
         }
