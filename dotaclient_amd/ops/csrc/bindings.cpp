@@ -49,7 +49,7 @@ void adam_step(torch::Tensor param, torch::Tensor grad, torch::Tensor m, torch::
 // ------------------------------------------------------------------------------------------------------------
 // Persistent LSTM recurrence. xp (B,S,4H) f32, whh (4H,H) bf16, h0/c0 (B,H) f32, err (1) int32 device flag.
 std::vector<torch::Tensor> lstm_fwd(torch::Tensor xp, torch::Tensor whh, torch::Tensor h0, torch::Tensor c0,
-                                    torch::Tensor err, bool want_f32_h) {
+                                    torch::Tensor err, bool want_f32_h, c10::optional<torch::Tensor> trace) {
   CHECK_F32(xp); CHECK_BF16(whh); CHECK_F32(h0); CHECK_F32(c0); CHECK_I32(err);
   TORCH_CHECK(xp.dim() == 3, "xp must be (B,S,4H)");
   const int B = xp.size(0), S = xp.size(1), G4 = xp.size(2), H = G4 / 4;
@@ -67,7 +67,8 @@ std::vector<torch::Tensor> lstm_fwd(torch::Tensor xp, torch::Tensor whh, torch::
   auto ring = torch::empty({(int64_t)dca_lstm_ring_elems(B, H, 0)}, f32.dtype(at::kLong));
   hip_check(dca_lstm_fwd(ptr<float>(xp), ptr<short>(whh), ptr<float>(h0), ptr<float>(c0), ptr<short>(hs),
                          want_f32_h ? ptr<float>(hsf) : nullptr, ptr<float>(cs), ptr<float>(gates), ptr<float>(hn),
-                         ptr<float>(cn), ptr<unsigned long long>(ring), ptr<unsigned>(err), B, S, H, cur_stream()),
+                         ptr<float>(cn), ptr<unsigned long long>(ring), ptr<unsigned>(err), B, S, H, cur_stream(),
+                         (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr),
             "dca_lstm_fwd");
   return {hs, want_f32_h ? hsf : hs, cs, gates, hn, cn};
 }
@@ -192,7 +193,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "dotaclient_amd gfx950 HIP kernels";
   m.def("adam_step", &adam_step, "fused global-norm clip + Adam over a flat fp32 buffer");
   m.def("lstm_max_batch", &dca_lstm_max_batch, "max sequences per persistent LSTM launch for hidden size H");
-  m.def("lstm_fwd", &lstm_fwd, "persistent LSTM forward recurrence (granule all-gather)");
+  m.def("lstm_fwd", &lstm_fwd, "persistent LSTM forward recurrence (granule all-gather)", py::arg("xp"),
+        py::arg("whh"), py::arg("h0"), py::arg("c0"), py::arg("err"), py::arg("want_f32_h"),
+        py::arg("trace") = py::none());
   m.def("heads_loss", &heads_loss, "fused heads + pointer + masked log-softmax + PPO/VPG loss + gradients");
   m.def("encoder_fwd", &encoder_fwd, "fused entity encoder forward (unit MLP, per-type GEMM, max-pool+argmax)");
   m.def("encoder_bwd", &encoder_bwd, "fused entity encoder backward (dW1 in-kernel; demb/basic for dW_type GEMMs)");

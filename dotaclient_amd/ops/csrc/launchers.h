@@ -13,7 +13,7 @@ size_t dca_lstm_ring_elems(int B, int H, int backward);
 int dca_lstm_max_batch(int H);
 hipError_t dca_lstm_fwd(const float* xp, const short* whh, const float* h0, const float* c0, short* hs, float* hsf,
                         float* cs, float* gates, float* hn, float* cn, unsigned long long* ring, unsigned* err, int B,
-                        int S, int H, hipStream_t st);
+                        int S, int H, hipStream_t st, unsigned long long* trace = nullptr);
 hipError_t dca_lstm_bwd(const float* dhs, const float* gates, const float* cs, const float* c0, const float* dhn,
                         const float* dcn, const short* whh, float* dgates, float* dh0, float* dc0,
                         unsigned long long* ring, unsigned* err, int B, int S, int H, hipStream_t st);

@@ -94,10 +94,15 @@ __global__ __launch_bounds__(kFwdThreads) void lstm_fwd_kernel(const float* __re
                                                                float* __restrict__ hsf, float* __restrict__ cs,
                                                                float* __restrict__ gates, float* __restrict__ hn,
                                                                float* __restrict__ cn, unsigned long long* ring,
-                                                               unsigned* err, int Btot, int Bc, int S) {
+                                                               unsigned* err, int Btot, int Bc, int S,
+                                                               unsigned long long* trace) {
   constexpr int H = 128 * KS;
   constexpr int G4 = 4 * H;
   constexpr int HP = H / 2;
+  // optional in-kernel timestamps (s_memrealtime, 100 MHz, chip-wide) for the first 64 steps: trace[wg][wave][t][ev]
+#define DCA_TSTAMP(ev)                                                                                   \
+  if (trace && lane == 0 && t < 64)                                                                       \
+    trace[(((size_t)blockIdx.x * 8 + wv) * 64 + t) * 8 + (ev)] = __builtin_amdgcn_s_memrealtime()
   // independent chains of ≤ 16·MT sequences run side by side in one launch (blockIdx = chain·NWG + w)
   const int chain = blockIdx.x / (H / kUw);
   const int b0 = chain * Bc;
@@ -152,6 +157,7 @@ __global__ __launch_bounds__(kFwdThreads) void lstm_fwd_kernel(const float* __re
   for (int t = 0; t < S; ++t) {
     const int par = t & 1;
     if (poller) {
+      DCA_TSTAMP(0);
       // -------- prefetch this step's x·W_ihᵀ values (4 per pair) — issued before the poll, consumed after it
       constexpr int NXV = (4 * PMAX) / 256;
       float xv[NXV];
@@ -205,6 +211,7 @@ __global__ __launch_bounds__(kFwdThreads) void lstm_fwd_kernel(const float* __re
           if (__all(ok)) break;
           if (spin_fail(spins, err, 1u)) { dead = true; break; }
         }
+        DCA_TSTAMP(1);
         while (!dead) {
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
@@ -245,6 +252,7 @@ __global__ __launch_bounds__(kFwdThreads) void lstm_fwd_kernel(const float* __re
             af[mt][ks] = v;
           }
       }
+      DCA_TSTAMP(2);
       if (dead && lane == 0) abort_flag = 1;
       // -------- partial gates over this wave's K quarter → LDS
 #pragma unroll
@@ -263,10 +271,12 @@ __global__ __launch_bounds__(kFwdThreads) void lstm_fwd_kernel(const float* __re
         const int idx = tid + 256 * i;
         if (idx < 4 * P) xpl[par][idx & 3][idx >> 2] = xv[i];
       }
+      DCA_TSTAMP(3);
     }
     lds_barrier();
     if (abort_flag) break;
     if (!poller) {
+      DCA_TSTAMP(4);
       // -------- cell update for every owned pair, publish h_t
 #pragma unroll
       for (int r = 0; r < NPR; ++r) {
@@ -311,8 +321,10 @@ __global__ __launch_bounds__(kFwdThreads) void lstm_fwd_kernel(const float* __re
                      ((unsigned long long)(unsigned)(t + 1) << 32) | pl);
         }
       }
+      DCA_TSTAMP(5);
     }
   }
+#undef DCA_TSTAMP
   if (!poller && !abort_flag) {
 #pragma unroll
     for (int r = 0; r < NPR; ++r) {
@@ -580,12 +592,12 @@ inline void plan_chains(int B, int H, int& nch, int& Bc, int& MT) {
 template <int MT, int KS>
 hipError_t launch_fwd(const float* xp, const short* whh, const float* h0, const float* c0, short* hs, float* hsf,
                       float* cs, float* gates, float* hn, float* cn, unsigned long long* ring, unsigned* err, int B,
-                      int Bc, int nch, int S, hipStream_t st) {
+                      int Bc, int nch, int S, unsigned long long* trace, hipStream_t st) {
   constexpr int H = 128 * KS;
   hipError_t e = hipMemsetAsync(ring, 0, sizeof(unsigned long long) * (size_t)nch * 2 * Bc * (H / 2), st);
   if (e != hipSuccess) return e;
   lstm_fwd_kernel<MT, KS><<<nch * (H / kUw), kFwdThreads, 0, st>>>(xp, whh, h0, c0, hs, hsf, cs, gates, hn, cn,
-                                                                   ring, err, B, Bc, S);
+                                                                   ring, err, B, Bc, S, trace);
   return hipGetLastError();
 }
 
@@ -628,12 +640,13 @@ extern "C" size_t dca_lstm_ring_elems(int B, int H, int backward) {
 
 extern "C" hipError_t dca_lstm_fwd(const float* xp, const short* whh, const float* h0, const float* c0, short* hs,
                                    float* hsf, float* cs, float* gates, float* hn, float* cn,
-                                   unsigned long long* ring, unsigned* err, int B, int S, int H, hipStream_t st) {
+                                   unsigned long long* ring, unsigned* err, int B, int S, int H, hipStream_t st,
+                                   unsigned long long* trace) {
   if (!lstm_shape_ok(B, H) || S < 1) return hipErrorInvalidValue;
   int nch, Bc, MT;
   plan_chains(B, H, nch, Bc, MT);
   const int KS = H / 128;
-#define DCA_F(mt, ks) launch_fwd<mt, ks>(xp, whh, h0, c0, hs, hsf, cs, gates, hn, cn, ring, err, B, Bc, nch, S, st)
+#define DCA_F(mt, ks) launch_fwd<mt, ks>(xp, whh, h0, c0, hs, hsf, cs, gates, hn, cn, ring, err, B, Bc, nch, S, trace, st)
   DCA_DISPATCH_MT_KS(MT, KS, DCA_F)
 #undef DCA_F
 }

@@ -1,0 +1,85 @@
+"""Node-local broker on shared memory: the experience queue is a native MPMC ring in POSIX shm
+(``native.ShmRing``: robust process-shared mutex + condvars, bounded, blocking with timeouts); the latest model is
+an atomically-replaced file in /dev/shm (x-recent-history length 1 semantics). Actors and learner ranks on one node
+exchange experience without a broker process or TCP."""
+from __future__ import annotations
+
+import os
+import struct
+import threading
+import time
+from typing import Callable, Optional
+
+from .. import native
+
+
+class ShmBroker:
+    def __init__(self, name: str, capacity: int = 1 << 28, create: Optional[bool] = None, drop_oldest: bool = False):
+        if not native.AVAILABLE:
+            raise RuntimeError('native module not built (python -m dotaclient_amd.native.build)')
+        self.name = name.strip('/')
+        path = f'/dev/shm/{self.name}_xp'
+        if create is None:
+            create = not os.path.exists(path)
+        self.ring = native.ShmRing(f'/{self.name}_xp', capacity, create)
+        self.model_path = f'/dev/shm/{self.name}_model'
+        self.drop_oldest = drop_oldest
+        self._subs = []
+        self._stop = threading.Event()
+        self._thread = None
+
+    def publish_experience(self, body: bytes, timeout: Optional[float] = None):
+        ok = self.ring.push(body, -1.0 if timeout is None else timeout, self.drop_oldest)
+        if not ok:
+            raise TimeoutError('experience ring full')
+
+    def consume_experience(self, timeout: Optional[float] = None) -> Optional[bytes]:
+        return self.ring.pop(-1.0 if timeout is None else float(timeout))
+
+    @property
+    def xp_queue_size(self) -> int:
+        return int(self.ring.size())
+
+    def publish_model(self, body: bytes, version: int):
+        tmp = f'{self.model_path}.{os.getpid()}.tmp'
+        with open(tmp, 'wb') as f:
+            f.write(struct.pack('<q', int(version)) + body)
+        os.replace(tmp, self.model_path)
+
+    def latest_model(self, newer_than: int = -(1 << 62), timeout: Optional[float] = 0.0):
+        t0 = time.time()
+        while True:
+            try:
+                with open(self.model_path, 'rb') as f:
+                    data = f.read()
+                v = struct.unpack_from('<q', data)[0]
+                if v > newer_than:
+                    return v, data[8:]
+            except (FileNotFoundError, struct.error):
+                pass
+            if not timeout or time.time() - t0 > timeout:
+                return None
+            time.sleep(0.01)
+
+    def subscribe_model(self, callback: Callable[[int, bytes], None], poll: float = 0.2):
+        self._subs.append(callback)
+        if self._thread is None:
+            def run():
+                have = -(1 << 62)
+                while not self._stop.is_set():
+                    m = self.latest_model(newer_than=have, timeout=poll)
+                    if m is not None:
+                        have = m[0]
+                        for cb in list(self._subs):
+                            cb(*m)
+            self._thread = threading.Thread(target=run, daemon=True)
+            self._thread.start()
+
+    def close(self, unlink: bool = False):
+        self._stop.set()
+        if unlink:
+            native.ShmRing.unlink(f'/{self.name}_xp')
+            try:
+                os.remove(self.model_path)
+            except FileNotFoundError:
+                pass

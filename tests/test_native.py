@@ -1,0 +1,122 @@
+"""Native host runtime: C++ protobuf featurizer vs the python featurizer, shm ring (incl. multi-process), crc32c."""
+import multiprocessing as mp
+import os
+import uuid
+
+import numpy as np
+import pytest
+
+from dotaclient_amd import native
+from dotaclient_amd.constants import LAYOUT_1V1, LAYOUT_5V5, TEAM_DIRE, TEAM_RADIANT
+from dotaclient_amd.env import SyntheticDotaService, get_1v1_selfplay_config, get_5v5_selfplay_config
+from dotaclient_amd.features.featurizer import featurize
+from dotaclient_amd.protos import FIELD_NUMBERS, pb
+
+pytestmark = pytest.mark.skipif(not native.AVAILABLE, reason='native module not built')
+
+
+def _states(cfg_fn, n_steps=300, seed=0):
+    svc = SyntheticDotaService(seed=seed)
+    svc.reset_sync(cfg_fn())
+    out = []
+    for i in range(n_steps):
+        for team in (TEAM_RADIANT, TEAM_DIRE):
+            o = svc.observe_sync(pb.ObserveConfig(team_id=team))
+            if o.status != 0:
+                return out
+            if i % 7 == 0:
+                out.append((o.world_state.SerializeToString(), team))
+            svc.act_sync(pb.Actions(actions=pb.CMsgBotWorldState.Actions(), team_id=team))
+    return out
+
+
+def test_field_numbers_match_cpp_decoder():
+    # the C++ decoder hard-codes these numbers (native/featurizer.cpp parse_unit / parse_world)
+    assert FIELD_NUMBERS['WorldState']['dota_time'] == 3 and FIELD_NUMBERS['WorldState']['units'] == 11
+    u = FIELD_NUMBERS['Unit']
+    assert (u['handle'], u['unit_type'], u['name'], u['team_id'], u['location'], u['is_alive'], u['player_id']) == \
+        (1, 2, 3, 4, 6, 7, 8)
+    assert (u['facing'], u['health'], u['health_max'], u['attack_range'], u['attack_target_handle'],
+            u['anim_activity'], u['is_invulnerable'], u['is_attack_immune'],
+            u['incoming_tracking_projectiles']) == (11, 20, 21, 30, 35, 40, 50, 51, 70)
+    assert FIELD_NUMBERS['Projectile'] == {'caster_handle': 1, 'location': 2, 'is_attack': 4}
+
+
+@pytest.mark.parametrize('cfg_fn,layout,players', [(get_1v1_selfplay_config, LAYOUT_1V1, {TEAM_RADIANT: [0], TEAM_DIRE: [5]}),
+                                                    (get_5v5_selfplay_config, LAYOUT_5V5,
+                                                     {TEAM_RADIANT: [0, 2], TEAM_DIRE: [5, 9]})])
+def test_native_featurizer_matches_python(cfg_fn, layout, players):
+    states = _states(cfg_fn)
+    blobs, pids, tids = [], [], []
+    for b, team in states:
+        for p in players[team]:
+            blobs.append(b)
+            pids.append(p)
+            tids.append(team)
+    env, units, handles, ncreep = native.featurize_batch(blobs, pids, tids, list(layout.counts), 4)
+    for i, (b, p, t) in enumerate(zip(blobs, pids, tids)):
+        f = featurize(pb.CMsgBotWorldState.FromString(b), p, t, layout=layout)
+        np.testing.assert_allclose(env[i], f.env, rtol=1e-5, atol=1e-6)
+        np.testing.assert_allclose(units[i], f.units, rtol=1e-5, atol=1e-5)
+        np.testing.assert_array_equal(handles[i], f.handles)
+        assert ncreep[i] == f.n_allied_creep
+
+
+def test_native_featurizer_rejects_garbage():
+    with pytest.raises(RuntimeError):
+        native.featurize_batch([b'\xff\xff\xff'], [0], [2], list(LAYOUT_1V1.counts), 1)
+
+
+def test_crc32c():
+    assert native.crc32c(b'123456789') == 0xE3069283
+    from dotaclient_amd.utils.tfevents import _TABLE
+    data = os.urandom(1000)
+    crc = 0xFFFFFFFF
+    for x in data:
+        crc = _TABLE[(crc ^ x) & 0xFF] ^ (crc >> 8)
+    assert native.crc32c(data) == crc ^ 0xFFFFFFFF
+
+
+def _producer(name, n, k):
+    r = native.ShmRing(name, 1 << 16, False)
+    for i in range(n):
+        assert r.push(f'{k}:{i}:'.encode() + os.urandom(300 + i % 200), 10.0, False)
+
+
+def test_shm_ring_mpmc():
+    name = f'/dca_test_{uuid.uuid4().hex[:8]}'
+    ring = native.ShmRing(name, 1 << 16, True)
+    try:
+        assert ring.pop(0.0) is None
+        ctx = mp.get_context('spawn')
+        ps = [ctx.Process(target=_producer, args=(name, 500, k)) for k in range(3)]
+        for p in ps:
+            p.start()
+        got = {}
+        for _ in range(1500):
+            m = ring.pop(20.0)
+            assert m is not None
+            k, i = m.split(b':')[:2]
+            got.setdefault(int(k), []).append(int(i))
+        for p in ps:
+            p.join(timeout=30)
+            assert p.exitcode == 0
+        for k in range(3):
+            assert got[k] == list(range(500))    # per-producer FIFO, nothing lost across wrap-arounds
+        assert ring.size() == 0
+    finally:
+        native.ShmRing.unlink(name)
+
+
+def test_shm_broker_roundtrip():
+    from dotaclient_amd.transport.shm import ShmBroker
+    name = f'dca_b_{uuid.uuid4().hex[:8]}'
+    b = ShmBroker(name, capacity=1 << 20, create=True)
+    try:
+        b.publish_experience(b'abc')
+        assert b.xp_queue_size == 1 and b.consume_experience(1.0) == b'abc'
+        b.publish_model(b'w1', 4)
+        assert b.latest_model(newer_than=3) == (4, b'w1')
+        assert b.latest_model(newer_than=4) is None
+    finally:
+        b.close(unlink=True)
