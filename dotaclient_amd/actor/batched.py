@@ -1,0 +1,310 @@
+"""GPU-resident batched actor inference: one hipGraph replay steps thousands of players at once.
+
+The reference actor runs one player per process on the CPU: featurize → ``policy.single`` → ``select_actions`` →
+``action_to_pb`` every 200 ms of game time (agent.py:641-660, policy.py:171-283). Here the per-player state (LSTM
+h/c) lives on the GPU in fixed slots and one step of *all* slots is a captured graph:
+
+    H2D(env, units, handles, keep)           pinned → static device buffers (one copy each)
+    h, c *= keep                             episode resets without host round trips
+    encoder_fwd                              fused entity encoder kernel (shared with the learner)
+    relu(x896·W_preᵀ + b)                    hipBLASLt
+    gates = x·W_ihᵀ + h·W_hhᵀ + b            hipBLASLt (fp32 out) → lstm_cell kernel (or fake_rnn Linear)
+    z = h·W_headsᵀ + b                       one GEMM for all 5 heads (q | enum | x | y | value)
+    sample_actions                           fused masked log-softmax + Gumbel-max + hierarchical selection
+    D2H(idx, logp, value[, act, msk])
+
+so the host only featurizes (native C++, :mod:`dotaclient_amd.native`) and turns indices into protobuf actions.
+Sampling uses a counter-based hash RNG (seed, step counter, row, head, entry) kept in device memory, so replays
+draw fresh noise without re-capture.
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+from ..models.policy import Policy
+
+LDZ = 160
+TYPE_SUFFIX = ('allied_heroes', 'enemy_heroes', 'allied_nonheroes', 'enemy_nonheroes', 'allied_towers',
+               'enemy_towers')
+
+
+class GpuActorPolicy:
+    """Fixed-slot batched policy step on one GPU (fully-fused policies: no entity attention)."""
+
+    def __init__(self, policy: Policy, n_slots: int, device='cuda', seed: int = 0, use_graph: bool = True,
+                 record: bool = True):
+        from .. import ops
+        self.C = ops.require()
+        cfg = policy.config
+        if cfg.entity_attention or cfg.unit_dim != 128 or cfg.env_dim != 128:
+            raise ValueError('GpuActorPolicy needs a fully-fused policy (no entity attention, 128-wide embeddings)')
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.n = n_slots
+        self.U = cfg.layout.max_units
+        self.A = 21 + self.U
+        self.seed = int(seed)
+        self.use_graph = use_graph
+        self.record = record
+        self.policy = policy
+        self._alloc()
+        self.load_weights(policy)
+        self.graph: Optional[torch.cuda.CUDAGraph] = None
+
+    # ------------------------------------------------------------------------------------------------
+    def _alloc(self):
+        n, U, A, dev = self.n, self.U, self.A, self.device
+        H = self.cfg.hidden
+        pin = dict(pin_memory=True)
+        self.h_env = torch.zeros(n, 3, **pin)
+        self.h_units = torch.zeros(n, U, 10, **pin)
+        self.h_handles = torch.full((n, U), -1, dtype=torch.long, **pin)
+        self.h_keep = torch.ones(n, 1, **pin)
+        self.d_env = torch.zeros(n, 3, device=dev)
+        self.d_units = torch.zeros(n, U, 10, device=dev)
+        self.d_handles = torch.full((n, U), -1, dtype=torch.long, device=dev)
+        self.d_keep = torch.ones(n, 1, device=dev)
+        self.h = torch.zeros(n, H, device=dev)
+        self.c = torch.zeros(n, H, device=dev)
+        self.h16 = torch.zeros(n, H, dtype=torch.bfloat16, device=dev)
+        self.ctr = torch.zeros(1, dtype=torch.long, device=dev)
+        self.idx = torch.zeros(n, 4, dtype=torch.int32, device=dev)
+        self.act = torch.zeros(n, A, dtype=torch.uint8, device=dev)
+        self.msk = torch.zeros(n, A, dtype=torch.uint8, device=dev)
+        self.logp = torch.zeros(n, device=dev)
+        self.value = torch.zeros(n, device=dev)
+        self.o_idx = torch.zeros(n, 4, dtype=torch.int32, **pin)
+        self.o_logp = torch.zeros(n, **pin)
+        self.o_value = torch.zeros(n, **pin)
+        self.o_act = torch.zeros(n, A, dtype=torch.uint8, **pin)
+        self.o_msk = torch.zeros(n, A, dtype=torch.uint8, **pin)
+        self.stream = torch.cuda.Stream(device=dev)
+
+    @torch.no_grad()
+    def load_weights(self, policy_or_state):
+        """(Re)load weights in place — buffers keep their addresses, so a captured graph stays valid."""
+        sd = policy_or_state.state_dict() if isinstance(policy_or_state, torch.nn.Module) else policy_or_state
+        dev = self.device
+        g = (lambda k: sd[k].detach().to(dev, torch.float32))
+        bf = (lambda k: sd[k].detach().to(dev, torch.bfloat16))
+        w = {
+            'w1': g('affine_unit_basic_stats.weight').contiguous(), 'b1': g('affine_unit_basic_stats.bias'),
+            'wt16': torch.stack([bf(f'affine_unit_{s}.weight') for s in TYPE_SUFFIX]).contiguous(),
+            'bt': torch.stack([g(f'affine_unit_{s}.bias') for s in TYPE_SUFFIX]).contiguous(),
+            'we': g('affine_env.weight').contiguous(), 'be': g('affine_env.bias'),
+            'wpreT': bf('affine_pre_rnn.weight').t().contiguous(), 'bpre': g('affine_pre_rnn.bias'),
+        }
+        H = self.cfg.hidden
+        if self.cfg.rnn == 'lstm':
+            w['wihT'] = bf('rnn.weight_ih_l0').t().contiguous()
+            w['whhT'] = bf('rnn.weight_hh_l0').t().contiguous()
+            w['brnn'] = g('rnn.bias_ih_l0') + g('rnn.bias_hh_l0')
+        else:
+            w['wfT'] = bf('fake_rnn.weight').t().contiguous()
+            w['bf'] = g('fake_rnn.bias')
+        heads = ['affine_unit_attention', 'affine_head_enum', 'affine_move_x', 'affine_move_y', 'affine_value']
+        wh = torch.cat([g(f'{k}.weight') for k in heads] + [torch.zeros(LDZ - 150, H, device=dev)], 0)
+        bh = torch.cat([g(f'{k}.bias') for k in heads] + [torch.zeros(LDZ - 150, device=dev)], 0)
+        w['whT'] = wh.to(torch.bfloat16).t().contiguous()
+        w['bh'] = bh.contiguous()
+        if not hasattr(self, 'w'):
+            self.w = w
+        else:
+            for k, v in w.items():
+                self.w[k].copy_(v)
+
+    # ------------------------------------------------------------------------------------------------
+    def _forward(self):
+        """The captured body: reads d_* / h / c, writes idx/act/msk/logp/value and the new h / c."""
+        C, w, cfg = self.C, self.w, self.cfg
+        mm = (lambda a, b: torch.mm(a, b, out_dtype=torch.float32))
+        self.h.mul_(self.d_keep)
+        self.c.mul_(self.d_keep)
+        self.h16.copy_(self.h)
+        x896, emb, _ = C.encoder_fwd(self.d_units, self.d_env, w['w1'], w['b1'], w['wt16'], w['bt'], w['we'],
+                                     w['be'], list(cfg.layout.counts), bool(cfg.compat_bugs))
+        if cfg.compat_bugs:
+            x896[:, 768:896] = x896[:, 512:640]
+        x = torch.relu(mm(x896, w['wpreT']) + w['bpre']).to(torch.bfloat16)
+        if cfg.rnn == 'lstm':
+            gates = mm(x, w['wihT'])
+            gates += w['brnn']
+            gates += mm(self.h16, w['whhT'])
+            C.lstm_cell(gates, self.h, self.c, self.h16)
+            xh = self.h16
+        else:
+            self.h.copy_(mm(x, w['wfT']) + w['bf'])
+            xh = self.h.to(torch.bfloat16)
+        z = mm(xh, w['whT']) + w['bh']
+        C.sample_actions(z, emb, self.d_handles, self.seed, self.ctr, self.idx, self.act, self.msk, self.logp,
+                         self.value)
+        self.ctr.add_(1)
+
+    def _h2d(self):
+        self.d_env.copy_(self.h_env, non_blocking=True)
+        self.d_units.copy_(self.h_units, non_blocking=True)
+        self.d_handles.copy_(self.h_handles, non_blocking=True)
+        self.d_keep.copy_(self.h_keep, non_blocking=True)
+
+    def _d2h(self):
+        self.o_idx.copy_(self.idx, non_blocking=True)
+        self.o_logp.copy_(self.logp, non_blocking=True)
+        self.o_value.copy_(self.value, non_blocking=True)
+        if self.record:
+            self.o_act.copy_(self.act, non_blocking=True)
+            self.o_msk.copy_(self.msk, non_blocking=True)
+
+    def capture(self):
+        """Warm up (hipBLASLt heuristics, allocator) on a side stream and capture the step body in a hipGraph."""
+        s = self.stream
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        ctr0 = self.ctr.clone()
+        with torch.cuda.stream(s):
+            for _ in range(3):
+                self._forward()
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            self._forward()
+        torch.cuda.synchronize(self.device)
+        # warm-up steps advanced the recurrent state and the RNG counter: start from a clean slate
+        self.ctr.copy_(ctr0)
+        self.h.zero_(); self.c.zero_(); self.h16.zero_()
+        self.graph = g
+
+    # ------------------------------------------------------------------------------------------------
+    def step_async(self):
+        """Launch one step for all slots using the host staging buffers; call :meth:`wait` for the outputs."""
+        if self.use_graph and self.graph is None:
+            self.capture()
+        with torch.cuda.stream(self.stream):
+            self._h2d()
+            if self.graph is not None:
+                self.graph.replay()
+            else:
+                self._forward()
+            self._d2h()
+            self._done = torch.cuda.Event()
+            self._done.record(self.stream)
+
+    def wait(self) -> Dict[str, np.ndarray]:
+        self._done.synchronize()
+        self.h_keep.fill_(1.0)
+        out = {'idx': self.o_idx.numpy(), 'logp': self.o_logp.numpy(), 'value': self.o_value.numpy()}
+        if self.record:
+            out['actions'] = self.o_act.numpy()
+            out['masks'] = self.o_msk.numpy()
+        return out
+
+    def step(self, env: np.ndarray, units: np.ndarray, handles: np.ndarray, reset: Optional[np.ndarray] = None):
+        """Synchronous step: (n,3), (n,U,10), (n,U) arrays for all slots; ``reset`` (n,) bool zeroes h/c first."""
+        self.h_env.numpy()[:] = env
+        self.h_units.numpy()[:] = units
+        self.h_handles.numpy()[:] = handles
+        if reset is not None:
+            self.h_keep.numpy()[:, 0] = 1.0 - np.asarray(reset, dtype=np.float32)
+        self.step_async()
+        return self.wait()
+
+    def hidden(self):
+        return self.h, self.c
+
+
+# ----------------------------------------------------------------------------------------------------
+def _synthetic_states(n_states: int, seed: int = 0):
+    """Serialized CMsgBotWorldState snapshots from the synthetic engine (both teams' views, varied game times)."""
+    from ..env import SyntheticDotaService
+    from ..env.configs import get_1v1_selfplay_config
+    from ..features.actions import action_to_pb
+    from ..features.featurizer import get_unit
+    from ..protos import pb
+    svc = SyntheticDotaService(seed=seed)
+    svc.reset_sync(get_1v1_selfplay_config())
+    rng = np.random.default_rng(seed)
+    states = []
+    t = 0
+    while len(states) < n_states:
+        t += 1
+        for team, pid in ((2, 0), (3, 5)):
+            ws = svc.observe_sync(pb.ObserveConfig(team_id=team)).world_state
+            if t > 100 and t % 3 == 0:   # skip the pre-horn start; decorrelate a little
+                states.append(ws.SerializeToString())
+            hero = get_unit(ws, player_id=pid)
+            if hero is None:
+                act = action_to_pb({'enum': 0}, None, None, pid)
+            else:
+                act = action_to_pb({'enum': 1, 'x': int(rng.integers(9)), 'y': int(rng.integers(9))},
+                                   hero.location, None, pid)
+            svc.act_sync(pb.Actions(actions=pb.CMsgBotWorldState.Actions(actions=[act]), team_id=team))
+    return states[:n_states]
+
+
+def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048, steps: int = 50,
+                             warmup: int = 5, featurize: bool = True, threads: int = 8) -> Dict[str, float]:
+    """Actor steps/s (player-observations → sampled actions per second) of one GPU-resident batched actor.
+
+    ``n_games`` 1v1 games = 2·n_games player slots stepped per launch. With ``featurize`` the host side decodes
+    and featurizes serialized world states through the native featurizer every step (the reference actor's
+    per-step work, agent.py:611-660) overlapped with the previous GPU step; otherwise only the GPU step + copies
+    are timed. Returns ``{'steps_per_s', 'gpu_steps_per_s', 'ms_per_step', 'slots'}``.
+    """
+    n = 2 * n_games
+    dev = torch.device(device)
+    layout = policy.config.layout
+    gp = GpuActorPolicy(policy, n, device=dev, seed=1234, record=True)
+    feat = None
+    if featurize:
+        from .. import native
+        if not native.AVAILABLE:
+            featurize = False
+        else:
+            pool = _synthetic_states(256)
+            pids = [0 if i % 2 == 0 else 5 for i in range(n)]
+            teams = [2 if i % 2 == 0 else 3 for i in range(n)]
+            batch = [pool[i % len(pool)] for i in range(n)]
+            counts = list(layout.counts)
+
+            def feat():
+                return native.featurize_batch(batch, pids, teams, counts, threads)
+    if not featurize:
+        rng = np.random.default_rng(0)
+        env = rng.standard_normal((n, 3)).astype(np.float32)
+        units = rng.standard_normal((n, layout.max_units, 10)).astype(np.float32)
+        handles = np.where(rng.random((n, layout.max_units)) < 0.5, rng.integers(1, 1000, (n, layout.max_units)),
+                           -1).astype(np.int64)
+
+        def feat():
+            return env, units, handles, None
+
+    def fill(f):
+        gp.h_env.numpy()[:] = f[0]
+        gp.h_units.numpy()[:] = f[1]
+        gp.h_handles.numpy()[:] = f[2]
+
+    fill(feat())
+    gp.step_async(); gp.wait()
+    for _ in range(warmup):
+        gp.step_async()
+        f = feat()
+        gp.wait()
+        fill(f)
+    # GPU-only rate (no featurize in the loop)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        gp.step_async()
+        gp.wait()
+    gpu_dt = (time.perf_counter() - t0) / steps
+    # pipelined: featurize step t+1 on the host while the GPU runs step t
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        gp.step_async()
+        f = feat()
+        gp.wait()
+        fill(f)
+    dt = (time.perf_counter() - t0) / steps
+    return {'steps_per_s': n / dt, 'gpu_steps_per_s': n / gpu_dt, 'ms_per_step': dt * 1e3, 'slots': n}

@@ -1,0 +1,163 @@
+// Actor-side inference kernels (gfx950): fused LSTM cell and fused masked hierarchical action sampling.
+//
+// Reference actor step (agent.py:641-660, policy.py:171-283): policy.single → action_masks → select_actions
+// (enum first, then x,y for MOVE or target_unit for ATTACK, each a masked categorical) → head_masks ∧ action masks.
+// Here one launch does it for a whole batch of players, one wave per player row:
+//   * pointer logits q·embᵀ over the unit slots, validity from unit handles (self slot 0 never targetable; ATTACK
+//     disabled when no unit is targetable — policy.py:272-283);
+//   * masked log-softmax of the 4 heads, Gumbel-max sampling with a counter-based hash RNG (seed, step counter,
+//     row, head, entry) — deterministic for a given seed/counter, graph-capturable (the counter lives in device
+//     memory and is bumped by the caller);
+//   * hierarchical selection, joint log-prob of the sampled action, one-hot actions and selected-heads masks
+//     (the experience record), and V(s).
+#include "common.h"
+
+namespace {
+
+constexpr int kQ = 128;
+
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ float gumbel(unsigned long long seed, unsigned long long ctr, int row, int head, int e) {
+  const unsigned long long h =
+      mix64(seed ^ mix64(ctr ^ mix64(((unsigned long long)row << 24) ^ ((unsigned long long)head << 16) ^ e)));
+  const float u = ((float)(h >> 40) + 0.5f) * (1.0f / 16777216.0f);   // (0,1)
+  return -__logf(-__logf(u));
+}
+
+// arg-max over lanes of (v); ties → lowest lane
+__device__ __forceinline__ int wave_argmax(float v, int lane) {
+  int idx = lane;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const float ov = __shfl_xor(v, o, 64);
+    const int oi = __shfl_xor(idx, o, 64);
+    if (ov > v || (ov == v && oi < idx)) { v = ov; idx = oi; }
+  }
+  return idx;
+}
+
+__global__ __launch_bounds__(256) void sample_kernel(const float* __restrict__ z, int ldz,
+                                                     const short* __restrict__ emb,
+                                                     const long long* __restrict__ handles, int N, int U,
+                                                     unsigned long long seed, const long long* __restrict__ ctr,
+                                                     int* __restrict__ idx_out, unsigned char* __restrict__ act_out,
+                                                     unsigned char* __restrict__ msk_out, float* __restrict__ logp_out,
+                                                     float* __restrict__ value_out) {
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int n = blockIdx.x * 4 + wv;
+  if (n >= N) return;
+  const int A = 21 + U;
+  const float* zr = z + (size_t)n * ldz;
+  // ---- pointer logits (4 units per wave instruction, 16 lanes per unit)
+  const int ks = lane & 15, ug = lane >> 4;
+  float q8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) q8[j] = zr[8 * ks + j];
+  float tl = -INFINITY;   // lane u holds target logit u
+  for (int it = 0; it * 4 < U; ++it) {
+    const int u = it * 4 + ug;
+    float d = 0.f;
+    if (u < U) {
+      const dca::bf16x8 v = *reinterpret_cast<const dca::bf16x8*>(emb + ((size_t)n * U + u) * kQ + 8 * ks);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d += q8[j] * dca::bf2f(v[j]);
+    }
+    d = dca::group_sum<16>(d);
+    // lane (16·g) holds unit it*4+g; move it to lane u
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const float dv = __shfl(d, 16 * g, 64);
+      if (lane == it * 4 + g) tl = dv;
+    }
+  }
+  // ---- validity
+  const bool tvalid = lane < U && lane != 0 && handles[(size_t)n * U + lane] != -1;
+  const bool any_target = __any(tvalid);
+  const unsigned long long c = *ctr;
+  const int hoff[4] = {0, 3, 12, 21};
+  const int hw[4] = {3, 9, 9, U};
+  int pick[4];
+  float plogp[4];
+#pragma unroll
+  for (int h = 0; h < 4; ++h) {
+    const bool in = lane < hw[h];
+    float lg = 0.f;
+    bool m = false;
+    if (h == 3) { lg = tl; m = tvalid; }
+    else if (in) { lg = zr[kQ + hoff[h] + lane]; m = (h == 0 && lane == 2) ? any_target : true; }
+    const float v = m ? lg : -INFINITY;
+    float mx = dca::wave_max(v);
+    const bool any = mx > -INFINITY;
+    if (!any) mx = 0.f;
+    float s = dca::wave_sum(m ? __expf(lg - mx) : 0.f);
+    if (!(s > 0.f)) s = 1.f;
+    const float lp = lg - mx - __logf(s);
+    const float key = m ? lp + gumbel(seed, c, n, h, lane) : -INFINITY;
+    int k = wave_argmax(key, lane);
+    if (!any) k = 0;
+    pick[h] = k;
+    plogp[h] = __shfl(lp, k, 64);
+    // selected-heads mask (head sampled ∧ valid) and one-hot action, written after the enum is known
+    if (h == 3) {
+      const int e = pick[0];
+      const bool mv = e == 1, at = e == 2;
+      for (int hh = 0; hh < 4; ++hh) {
+        const bool head_on = hh == 0 || ((hh == 1 || hh == 2) && mv) || (hh == 3 && at);
+        for (int j = lane; j < hw[hh]; j += 64) {
+          bool valid = true;
+          if (hh == 3) valid = j != 0 && handles[(size_t)n * U + j] != -1;
+          if (hh == 0 && j == 2) valid = any_target;
+          msk_out[(size_t)n * A + hoff[hh] + j] = (head_on && valid) ? 1 : 0;
+          act_out[(size_t)n * A + hoff[hh] + j] = (head_on && j == pick[hh]) ? 1 : 0;
+        }
+      }
+      if (lane == 0) {
+        idx_out[n * 4 + 0] = pick[0];
+        idx_out[n * 4 + 1] = pick[1];
+        idx_out[n * 4 + 2] = pick[2];
+        idx_out[n * 4 + 3] = pick[3];
+        logp_out[n] = plogp[0] + (mv ? plogp[1] + plogp[2] : 0.f) + (at ? plogp[3] : 0.f);
+        value_out[n] = zr[kQ + 21];
+      }
+    }
+  }
+}
+
+// gates (N, 4H) pre-activations (x·W_ihᵀ + h·W_hhᵀ + b, fp32) → h, c (fp32) in place + h bf16 copy
+__global__ __launch_bounds__(256) void lstm_cell_kernel(const float* __restrict__ g, float* __restrict__ h,
+                                                        float* __restrict__ c, short* __restrict__ h16, int N,
+                                                        int H) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= N * H) return;
+  const int n = i / H, j = i % H;
+  const float* gr = g + (size_t)n * 4 * H;
+  const float ig = dca::sigmoidf_(gr[j]), fg = dca::sigmoidf_(gr[H + j]), gg = dca::tanhf_(gr[2 * H + j]),
+              og = dca::sigmoidf_(gr[3 * H + j]);
+  const float cn = fg * c[i] + ig * gg;
+  const float hn = og * dca::tanhf_(cn);
+  c[i] = cn;
+  h[i] = hn;
+  h16[i] = dca::f2bf(hn);
+}
+
+}  // namespace
+
+extern "C" hipError_t dca_sample_actions(const float* z, int ldz, const short* emb, const long long* handles, int N,
+                                         int U, unsigned long long seed, const long long* ctr, int* idx,
+                                         unsigned char* act, unsigned char* msk, float* logp, float* value,
+                                         hipStream_t st) {
+  if (U < 1 || U > 64 || ldz < kQ + 22) return hipErrorInvalidValue;
+  sample_kernel<<<(N + 3) / 4, 256, 0, st>>>(z, ldz, emb, handles, N, U, seed, ctr, idx, act, msk, logp, value);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t dca_lstm_cell(const float* gates, float* h, float* c, short* h16, int N, int H, hipStream_t st) {
+  lstm_cell_kernel<<<(N * H + 255) / 256, 256, 0, st>>>(gates, h, c, h16, N, H);
+  return hipGetLastError();
+}

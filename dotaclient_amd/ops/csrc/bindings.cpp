@@ -187,6 +187,37 @@ std::vector<torch::Tensor> encoder_bwd(torch::Tensor units, torch::Tensor w1, to
   return {demb, basic, dw1, db1};
 }
 
+// ------------------------------------------------------------------------------------------------------------
+// Actor inference. Fused masked hierarchical sampling: z (N,ldz) f32 head logits [q|enum|x|y|v|pad], emb (N,U,128)
+// bf16, handles (N,U) int64, ctr (1) int64 device step counter; writes idx (N,4) i32, act/msk (N,21+U) u8,
+// logp (N) f32, value (N) f32 (all preallocated so the op is hipGraph-capturable).
+void sample_actions(torch::Tensor z, torch::Tensor emb, torch::Tensor handles, int64_t seed, torch::Tensor ctr,
+                    torch::Tensor idx, torch::Tensor act, torch::Tensor msk, torch::Tensor logp, torch::Tensor value) {
+  CHECK_F32(z); CHECK_BF16(emb); CHECK_DEV(handles); CHECK_CONTIG(handles); CHECK_DT(handles, at::kLong);
+  CHECK_DEV(ctr); CHECK_DT(ctr, at::kLong); CHECK_I32(idx); CHECK_U8(act); CHECK_U8(msk); CHECK_F32(logp);
+  CHECK_F32(value);
+  TORCH_CHECK(z.dim() == 2 && emb.dim() == 3 && emb.size(2) == 128, "z (N,ldz), emb (N,U,128)");
+  const int N = z.size(0), ldz = z.size(1), U = emb.size(1);
+  TORCH_CHECK(emb.size(0) == N && handles.size(0) == N && handles.size(1) == U, "row/unit count mismatch");
+  TORCH_CHECK(idx.size(0) == N && idx.size(1) == 4 && logp.numel() == N && value.numel() == N, "output shapes");
+  TORCH_CHECK(act.size(0) == N && act.size(1) == 21 + U && msk.sizes() == act.sizes(), "act/msk (N,21+U)");
+  TORCH_CHECK(U <= 64 && ldz >= 150, "U <= 64, ldz >= 150");
+  hip_check(dca_sample_actions(ptr<float>(z), ldz, ptr<short>(emb), ptr<long long>(handles), N, U,
+                               (unsigned long long)seed, ptr<long long>(ctr), ptr<int>(idx), ptr<unsigned char>(act),
+                               ptr<unsigned char>(msk), ptr<float>(logp), ptr<float>(value), cur_stream()),
+            "dca_sample_actions");
+}
+
+// LSTM cell from fp32 pre-activation gates (N,4H): updates h, c (N,H) f32 in place, writes h16 (N,H) bf16.
+void lstm_cell(torch::Tensor gates, torch::Tensor h, torch::Tensor c, torch::Tensor h16) {
+  CHECK_F32(gates); CHECK_F32(h); CHECK_F32(c); CHECK_BF16(h16);
+  const int N = h.size(0), H = h.size(1);
+  TORCH_CHECK(gates.size(0) == N && gates.size(1) == 4 * H && c.sizes() == h.sizes() && h16.sizes() == h.sizes(),
+              "lstm_cell shapes");
+  hip_check(dca_lstm_cell(ptr<float>(gates), ptr<float>(h), ptr<float>(c), ptr<short>(h16), N, H, cur_stream()),
+            "dca_lstm_cell");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -200,4 +231,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("encoder_fwd", &encoder_fwd, "fused entity encoder forward (unit MLP, per-type GEMM, max-pool+argmax)");
   m.def("encoder_bwd", &encoder_bwd, "fused entity encoder backward (dW1 in-kernel; demb/basic for dW_type GEMMs)");
   m.def("lstm_bwd", &lstm_bwd, "persistent LSTM backward recurrence (granule reduce-scatter)");
+  m.def("sample_actions", &sample_actions, "fused masked hierarchical Gumbel-max action sampling (actor)");
+  m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)");
 }

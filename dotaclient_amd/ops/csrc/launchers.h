@@ -33,4 +33,9 @@ hipError_t dca_encoder_bwd(const float* units, const float* w1, const float* b1,
                            short* basic, float* dw1, float* db1, int N, int U, const int* counts, int compat,
                            hipStream_t st);
 
+hipError_t dca_sample_actions(const float* z, int ldz, const short* emb, const long long* handles, int N, int U,
+                              unsigned long long seed, const long long* ctr, int* idx, unsigned char* act,
+                              unsigned char* msk, float* logp, float* value, hipStream_t st);
+hipError_t dca_lstm_cell(const float* gates, float* h, float* c, short* h16, int N, int H, hipStream_t st);
+
 }  // extern "C"
