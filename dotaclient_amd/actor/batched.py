@@ -25,11 +25,9 @@ from typing import Dict, Optional
 import numpy as np
 import torch
 
-from ..models.policy import Policy
+from ..models.policy import TYPE_SUFFIX, Policy
 
 LDZ = 160
-TYPE_SUFFIX = ('allied_heroes', 'enemy_heroes', 'allied_nonheroes', 'enemy_nonheroes', 'allied_towers',
-               'enemy_towers')
 
 
 class GpuActorPolicy:

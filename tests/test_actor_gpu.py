@@ -80,10 +80,10 @@ def test_sample_actions_distribution(gpu_ops):
     h1[0, 1:6] = torch.arange(10, 15, device='cuda')
     z, emb, handles = z1.expand(N, -1).contiguous(), e1.expand(N, -1, -1).contiguous(), h1.expand(N, -1).contiguous()
     idx, *_ = _run_sample(gpu_ops, z, emb, handles, seed=11, ctr=3)
-    lps, _ = _torch_logps(z1, e1, h1)
-    for col, k, w in ((0, 'enum', 3), (1, 'x', 9), (3, 'target', U)):
+    lps, valid = _torch_logps(z1, e1, h1)
+    for col, k, o, w in ((0, 'enum', 0, 3), (1, 'x', 3, 9), (3, 'target', 21, U)):
         freq = torch.bincount(idx[:, col], minlength=w).float() / N
-        p = lps[k][0].exp()
+        p = lps[k][0].exp() * valid[0, o:o + w]
         assert (freq - p).abs().max() < 0.015, (k, freq, p)
     # a different counter gives different draws; the same counter reproduces them
     idx2, *_ = _run_sample(gpu_ops, z, emb, handles, seed=11, ctr=4)
