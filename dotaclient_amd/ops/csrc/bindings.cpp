@@ -75,7 +75,7 @@ std::vector<torch::Tensor> lstm_fwd(torch::Tensor xp, torch::Tensor whh, torch::
 
 std::vector<torch::Tensor> lstm_bwd(torch::Tensor dhs, torch::Tensor gates, torch::Tensor cs, torch::Tensor c0,
                                     c10::optional<torch::Tensor> dhn, c10::optional<torch::Tensor> dcn,
-                                    torch::Tensor whh, torch::Tensor err) {
+                                    torch::Tensor whh, torch::Tensor err, c10::optional<torch::Tensor> trace) {
   CHECK_F32(dhs); CHECK_F32(gates); CHECK_F32(cs); CHECK_F32(c0); CHECK_BF16(whh); CHECK_I32(err);
   const int B = dhs.size(0), S = dhs.size(1), H = dhs.size(2);
   TORCH_CHECK(gates.size(0) == B && gates.size(1) == S && gates.size(2) == 4 * H, "gates must be (B,S,4H)");
@@ -94,7 +94,8 @@ std::vector<torch::Tensor> lstm_bwd(torch::Tensor dhs, torch::Tensor gates, torc
   auto ring = torch::empty({(int64_t)dca_lstm_ring_elems(B, H, 1)}, f32.dtype(at::kLong));
   hip_check(dca_lstm_bwd(ptr<float>(dhs), ptr<float>(gates), ptr<float>(cs), ptr<float>(c0), dhn_p, dcn_p,
                          ptr<short>(whh), ptr<float>(dgates), ptr<float>(dh0), ptr<float>(dc0),
-                         ptr<unsigned long long>(ring), ptr<unsigned>(err), B, S, H, cur_stream()),
+                         ptr<unsigned long long>(ring), ptr<unsigned>(err), B, S, H, cur_stream(),
+                         (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr),
             "dca_lstm_bwd");
   return {dgates, dh0, dc0};
 }
@@ -230,7 +231,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("heads_loss", &heads_loss, "fused heads + pointer + masked log-softmax + PPO/VPG loss + gradients");
   m.def("encoder_fwd", &encoder_fwd, "fused entity encoder forward (unit MLP, per-type GEMM, max-pool+argmax)");
   m.def("encoder_bwd", &encoder_bwd, "fused entity encoder backward (dW1 in-kernel; demb/basic for dW_type GEMMs)");
-  m.def("lstm_bwd", &lstm_bwd, "persistent LSTM backward recurrence (granule reduce-scatter)");
+  m.def("lstm_bwd", &lstm_bwd, "persistent LSTM backward recurrence (granule reduce-scatter)", py::arg("dhs"),
+        py::arg("gates"), py::arg("cs"), py::arg("c0"), py::arg("dhn"), py::arg("dcn"), py::arg("whh"), py::arg("err"),
+        py::arg("trace") = py::none());
   m.def("sample_actions", &sample_actions, "fused masked hierarchical Gumbel-max action sampling (actor)");
   m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)");
 }

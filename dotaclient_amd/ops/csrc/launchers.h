@@ -16,7 +16,8 @@ hipError_t dca_lstm_fwd(const float* xp, const short* whh, const float* h0, cons
                         int S, int H, hipStream_t st, unsigned long long* trace = nullptr);
 hipError_t dca_lstm_bwd(const float* dhs, const float* gates, const float* cs, const float* c0, const float* dhn,
                         const float* dcn, const short* whh, float* dgates, float* dh0, float* dc0,
-                        unsigned long long* ring, unsigned* err, int B, int S, int H, hipStream_t st);
+                        unsigned long long* ring, unsigned* err, int B, int S, int H, hipStream_t st,
+                        unsigned long long* trace = nullptr);
 
 int dca_heads_loss_nblocks(int N);
 hipError_t dca_heads_loss(const float* z, int ldz, const short* emb, const unsigned char* act, const unsigned char* msk,

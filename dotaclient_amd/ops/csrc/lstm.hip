@@ -26,6 +26,8 @@
 //     can never hang the GPU. The grid (≤ 64·chains workgroups of 256 threads) is always co-resident.
 // MFMA: v_mfma_f32_16x16x32_bf16, batch rows in M (B ≤ 16·MT), gate columns / hidden units in N.
 #include "common.h"
+#include <cstdio>
+#include <cstdlib>
 
 namespace {
 
@@ -34,6 +36,9 @@ using gu64 = __attribute__((address_space(1))) unsigned long long;
 using gu32 = __attribute__((address_space(1))) unsigned int;
 
 constexpr int kUw = 8;                  // hidden units per workgroup
+constexpr int kSc1 = 16;                // buffer-op cache policy: sc1 = agent-coherent (bypasses the per-XCD L2)
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 constexpr unsigned kSpinLimit = 1u << 21;
 
 __device__ __forceinline__ unsigned long long ld_granule(const unsigned long long* p) {
@@ -61,6 +66,21 @@ __device__ __forceinline__ bool spin_fail(unsigned& spins, unsigned* err, unsign
   }
   if (spins > 64) __builtin_amdgcn_s_sleep(1);
   return false;
+}
+
+__device__ __forceinline__ void sleep_n(int n) {
+  for (int i = 0; i < n; ++i) __builtin_amdgcn_s_sleep(1);
+}
+
+// Buffer resource for a wave-uniform base pointer. readfirstlane makes the uniformity explicit: code inside
+// role branches (poller / publisher) is divergent to the compiler, which would otherwise keep the descriptor in
+// VGPRs and wrap every buffer load in a waterfall loop.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, int bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0,
+                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
 // One workgroup-wide rendezvous that orders LDS traffic only. Unlike __syncthreads() it does NOT wait for
@@ -95,7 +115,8 @@ __global__ __launch_bounds__(kFwdThreads) void lstm_fwd_kernel(const float* __re
                                                                float* __restrict__ gates, float* __restrict__ hn,
                                                                float* __restrict__ cn, unsigned long long* ring,
                                                                unsigned* err, int Btot, int Bc, int S,
-                                                               unsigned long long* trace) {
+                                                               unsigned long long* trace, int pre_sleep,
+                                                               int spin_sleep) {
   constexpr int H = 128 * KS;
   constexpr int G4 = 4 * H;
   constexpr int HP = H / 2;
@@ -121,7 +142,8 @@ __global__ __launch_bounds__(kFwdThreads) void lstm_fwd_kernel(const float* __re
   __shared__ float red[2][4][MT][2][16][17];
   __shared__ float xpl[2][4][PMAX];
   __shared__ int abort_flag;
-  if (tid == 0) abort_flag = 0;
+  __shared__ int pub_issued;               // last step whose h granules this workgroup's publisher has issued
+  if (tid == 0) { abort_flag = 0; pub_issued = 0; }
   __syncthreads();
 
   const bool poller = wv < 4;
@@ -188,66 +210,57 @@ __global__ __launch_bounds__(kFwdThreads) void lstm_fwd_kernel(const float* __re
       } else {
         const unsigned long long* slot = ring + (size_t)((t - 1) & 1) * B * HP;
         const unsigned tag = (unsigned)t;
-        // Two-phase poll. (1) PROBE: one granule per fragment (each 8-value fragment comes from exactly one
-        // producer workgroup) until every probed tag matches — cheap, so spinning does not flood the memory
-        // system. (2) FETCH: issue every granule load before looking at any result (relaxed atomic loads are
-        // ordered for the scheduler: interleaved load/use would serialise them), verify, refetch if needed.
-        unsigned long long gr[MT][KS][4];
+        // Data-carrying poll: each fragment (8 h values of one batch row = 4 granules = 32 contiguous bytes, all
+        // written by ONE producer store instruction) is read with two 16-byte agent-coherent (sc1) buffer loads —
+        // the poll IS the fetch, so a step costs one hand-off round trip, and every load of a round is in flight
+        // before any tag is inspected. Buffer loads (unlike atomic/volatile loads) are not serialised by the
+        // compiler; the spin loop's side effects keep them inside the loop.
+        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(slot, B * HP * 8);
+        i32x4 g2[MT][KS][2];
+        // Do not poll before this workgroup's own publisher has ISSUED its step t-1 granule stores: polls queue in
+        // the same per-CU vector-memory path and would delay that store — and no other workgroup's data can be
+        // expected much earlier, all of them run in lockstep. The wait is LDS-only.
+        while (*(volatile int*)&pub_issued < t) __builtin_amdgcn_s_sleep(0);
+        sleep_n(pre_sleep);
         while (true) {
-          bool ok = true;
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks) {
               const int b = mt * 16 + lrow;
               const int k = wv * (32 * KS) + ks * 32 + 8 * lkg;
-              if (b < B) gr[mt][ks][3] = ld_granule(slot + (size_t)b * HP + (k >> 1) + 3);
+              const int off = (b * HP + (k >> 1)) * 8;
+              if (b < B) {
+                g2[mt][ks][0] = __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, kSc1);
+                g2[mt][ks][1] = __builtin_amdgcn_raw_buffer_load_b128(rs, off + 16, 0, kSc1);
+              }
             }
+          bool ok = true;
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
             for (int ks = 0; ks < KS; ++ks)
-              if (mt * 16 + lrow < B) ok &= (unsigned)(gr[mt][ks][3] >> 32) == tag;
+              if (mt * 16 + lrow < B)
+                ok &= ((unsigned)g2[mt][ks][0].y == tag) & ((unsigned)g2[mt][ks][0].w == tag) &
+                      ((unsigned)g2[mt][ks][1].y == tag) & ((unsigned)g2[mt][ks][1].w == tag);
           if (__all(ok)) break;
           if (spin_fail(spins, err, 1u)) { dead = true; break; }
+          sleep_n(spin_sleep);
         }
         DCA_TSTAMP(1);
-        while (!dead) {
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks) {
-              const int b = mt * 16 + lrow;
-              const int k = wv * (32 * KS) + ks * 32 + 8 * lkg;
-              if (b < B) {
-                const unsigned long long* g = slot + (size_t)b * HP + (k >> 1);
-#pragma unroll
-                for (int q = 0; q < 4; ++q) gr[mt][ks][q] = ld_granule(g + q);
-              }
-            }
-          bool ok = true;
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-            for (int ks = 0; ks < KS; ++ks)
-              if (mt * 16 + lrow < B) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) ok &= (unsigned)(gr[mt][ks][q] >> 32) == tag;
-              }
-          if (__all(ok)) break;
-          if (spin_fail(spins, err, 1u)) { dead = true; break; }
-        }
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks) {
             const bool valid = mt * 16 + lrow < B;
+            const unsigned pl[4] = {(unsigned)g2[mt][ks][0].x, (unsigned)g2[mt][ks][0].z, (unsigned)g2[mt][ks][1].x,
+                                    (unsigned)g2[mt][ks][1].z};
             bf16x8 v;
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-              const unsigned pl = valid ? (unsigned)gr[mt][ks][q] : 0u;
-              v[2 * q] = (short)(pl & 0xffffu);
-              v[2 * q + 1] = (short)(pl >> 16);
+              const unsigned u = valid ? pl[q] : 0u;
+              v[2 * q] = (short)(u & 0xffffu);
+              v[2 * q + 1] = (short)(u >> 16);
             }
             af[mt][ks] = v;
           }
@@ -277,11 +290,14 @@ __global__ __launch_bounds__(kFwdThreads) void lstm_fwd_kernel(const float* __re
     if (abort_flag) break;
     if (!poller) {
       DCA_TSTAMP(4);
-      // -------- cell update for every owned pair, publish h_t
+      // -------- cell update for every owned pair; publish the h_t granules FIRST (the next step's critical path),
+      // then the bulky per-step outputs, so the hand-off stores are never queued behind them.
+      float gi[NPR], gf[NPR], gg_[NPR], go[NPR];
 #pragma unroll
       for (int r = 0; r < NPR; ++r) {
         const int p = lane + 64 * r;
-        if (64 * r >= P) break;                     // wave-uniform
+        gi[r] = gf[r] = gg_[r] = go[r] = 0.f;
+        if (64 * r >= P) continue;                  // wave-uniform
         float hv = 0.f;
         if (p < P) {
           const int b = p >> 3, jj = p & 7;
@@ -294,23 +310,14 @@ __global__ __launch_bounds__(kFwdThreads) void lstm_fwd_kernel(const float* __re
             pre[q] = red[par][0][mt][nt][row][cc] + red[par][1][mt][nt][row][cc] + red[par][2][mt][nt][row][cc] +
                      red[par][3][mt][nt][row][cc] + xpl[par][q][p];
           }
-          const float ig = dca::sigmoidf_(pre[0]);
-          const float fg = dca::sigmoidf_(pre[1]);
-          const float gg = dca::tanhf_(pre[2]);
-          const float og = dca::sigmoidf_(pre[3]);
-          const float c = fg * creg[r] + ig * gg;
-          hv = og * dca::tanhf_(c);
+          gi[r] = dca::sigmoidf_(pre[0]);
+          gf[r] = dca::sigmoidf_(pre[1]);
+          gg_[r] = dca::tanhf_(pre[2]);
+          go[r] = dca::sigmoidf_(pre[3]);
+          const float c = gf[r] * creg[r] + gi[r] * gg_[r];
+          hv = go[r] * dca::tanhf_(c);
           creg[r] = c;
           hreg[r] = hv;
-          const size_t bt = (size_t)b * S + t;
-          hs[bt * H + j0 + jj] = dca::f2bf(hv);
-          if (hsf) hsf[bt * H + j0 + jj] = hv;
-          cs[bt * H + j0 + jj] = c;
-          float* gp = gates + bt * G4 + j0 + jj;
-          gp[0] = ig;
-          gp[H] = fg;
-          gp[2 * H] = gg;
-          gp[3 * H] = og;
         }
         const float hnext = __shfl_down(hv, 1, 64);
         if (p < P && (p & 1) == 0) {
@@ -319,6 +326,25 @@ __global__ __launch_bounds__(kFwdThreads) void lstm_fwd_kernel(const float* __re
                               ((unsigned)(unsigned short)dca::f2bf(hnext) << 16);
           st_granule(ring + (size_t)par * B * HP + (size_t)b * HP + ((j0 + jj) >> 1),
                      ((unsigned long long)(unsigned)(t + 1) << 32) | pl);
+        }
+      }
+      if (lane == 0) *(volatile int*)&pub_issued = t + 1;
+      DCA_TSTAMP(6);
+#pragma unroll
+      for (int r = 0; r < NPR; ++r) {
+        const int p = lane + 64 * r;
+        if (64 * r >= P) break;                     // wave-uniform
+        if (p < P) {
+          const int b = p >> 3, jj = p & 7;
+          const size_t bt = (size_t)b * S + t;
+          hs[bt * H + j0 + jj] = dca::f2bf(hreg[r]);
+          if (hsf) hsf[bt * H + j0 + jj] = hreg[r];
+          cs[bt * H + j0 + jj] = creg[r];
+          float* gp = gates + bt * G4 + j0 + jj;
+          gp[0] = gi[r];
+          gp[H] = gf[r];
+          gp[2 * H] = gg_[r];
+          gp[3 * H] = go[r];
         }
       }
       DCA_TSTAMP(5);
@@ -347,7 +373,7 @@ __global__ __launch_bounds__(kFwdThreads) void lstm_fwd_kernel(const float* __re
 // gates  (B, S, 4H) f32  activated gates;  cs (B,S,H) f32 c_t;  c0 (B,H)
 // dhn,dcn(B, H)     f32  ∂L/∂(h_S, c_S) (may be null)
 // dgates (B, S, 4H) f32  out: ∂L/∂(gate pre-activations);  dh0, dc0 (B,H) out
-// ring   (2, NWG, B, H) u64 granules {tag = t+1, f32} (zeroed)
+// ring   (2, B, NWG consumers, NWG producers, 2 quads) 16-byte chunks {2×bf16, tag, 2×bf16, tag} (zeroed)
 template <int MT, int KS>
 __global__ __launch_bounds__(kBwdThreads) void lstm_bwd_kernel(const float* __restrict__ dhs,
                                                                const float* __restrict__ gates,
@@ -358,7 +384,12 @@ __global__ __launch_bounds__(kBwdThreads) void lstm_bwd_kernel(const float* __re
                                                                const short* __restrict__ whh,
                                                                float* __restrict__ dgates, float* __restrict__ dh0,
                                                                float* __restrict__ dc0, unsigned long long* ring,
-                                                               unsigned* err, int Btot, int Bc, int S) {
+                                                               unsigned* err, int Btot, int Bc, int S,
+                                                               int pre_sleep, int spin_sleep,
+                                                               unsigned long long* trace) {
+#define DCA_TSTAMPB(ev)                                                                                  \
+  if (trace && lane == 0 && k < 64)                                                                       \
+    trace[(((size_t)blockIdx.x * 8 + wv) * 64 + k) * 8 + (ev)] = __builtin_amdgcn_s_memrealtime()
   constexpr int H = 128 * KS;
   constexpr int G4 = 4 * H;
   constexpr int NWG = H / kUw;
@@ -380,11 +411,15 @@ __global__ __launch_bounds__(kBwdThreads) void lstm_bwd_kernel(const float* __re
   const int pw = wv - 4;
 
   constexpr int PMAX = 128 * MT;
-  __shared__ float dpart[2][4][PMAX];
+  constexpr int NSLOT = (NWG * 2) / 64 > 0 ? (NWG * 2) / 64 : 1;   // LDS partial slots (producer groups per row)
+  __shared__ float dpart[2][NSLOT][PMAX];
   __shared__ float inp[2][7][PMAX];        // i, f, g, o, c_t, c_{t-1}, dhs_t
   __shared__ short dgl[4][MT * 16][40];
+  constexpr int SC = NT_W * 16 + 8;        // staging row pitch (bf16), padded
+  __shared__ unsigned short stg[4][MT * 16][SC];
   __shared__ int abort_flag;
-  if (tid == 0) abort_flag = 0;
+  __shared__ int pub_cnt;                  // publisher waves that issued their partial stores (4 per step)
+  if (tid == 0) { abort_flag = 0; pub_cnt = 0; }
   for (int i = tid; i < 4 * MT * 16 * 40; i += kBwdThreads) (&dgl[0][0][0])[i] = 0;
   __syncthreads();
 
@@ -432,77 +467,68 @@ __global__ __launch_bounds__(kBwdThreads) void lstm_bwd_kernel(const float* __re
         }
       }
       // -------- recurrent gradient for h_t: Σ_w' partial_{w'} of step t+1 (k = 0: the given ∂L/∂h_S).
-      // All of this wave's granules (every pass of 64 pairs × its NWG/4 producers) are loaded in ONE poll round, so
-      // a step costs one hand-off round trip whatever the batch.
+      // Ring layout (parity, b, consumer, producer, unit): the NWG×8 partials this workgroup needs for one batch row
+      // are one contiguous block, read as 16-byte chunks {2 units of one producer} by all 256 poller lanes with
+      // sc1 buffer loads — data-carrying polls, every load of a group of 8 rows in flight at once. The sum over
+      // producers is a lane-shuffle tree (producers differ in lane bits 2..5) plus the per-wave LDS slots
+      // (dpart[.][pslot]) that the publishers add up.
+      DCA_TSTAMPB(0);
       bool dead = false;
-      const int pg = wv;
-      constexpr int NPASS = PMAX / 64;
-      const int npass = (P + 63) >> 6;
-      float ssum[NPASS];
+      constexpr int CPR = NWG * 2;                    // 16-byte chunks {2 granules, 4 units} per batch row block
+      constexpr int RPP = 256 / CPR;                  // rows covered per load slot (2, 4 or 8)
+      constexpr int NLD = 8 / RPP;                    // loads per lane per group of 8 rows
+      constexpr int LSPAN = CPR < 64 ? CPR : 64;      // lanes of one row inside a wave
+      const int chunk = tid % CPR, ro = tid / CPR;
+      const int pslot = (tid >> 6) % NSLOT;
       if (k == 0) {
+        for (int p = tid; p < P; p += 256) {
+          const float v = dhn ? dhn[(p >> 3) * H + j0 + (p & 7)] : 0.f;
 #pragma unroll
-        for (int ps = 0; ps < NPASS; ++ps) {
-          const int p = ps * 64 + lane;
-          ssum[ps] = (pg == 0 && p < P && dhn) ? dhn[(p >> 3) * H + j0 + (p & 7)] : 0.f;
+          for (int sl = 0; sl < NSLOT; ++sl) dpart[par][sl][p] = sl == 0 ? v : 0.f;
         }
       } else {
-        const unsigned long long* slot = ring + (size_t)((t + 1) & 1) * NWG * B * H;
+        const unsigned long long* slot = ring + (size_t)((t + 1) & 1) * B * NWG * NWG * 4 + (size_t)w * NWG * 4;
+        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(slot, ((B - 1) * NWG * NWG * 4 + NWG * 4) * 8);
         const unsigned tag = (unsigned)(t + 2);
-        constexpr int NPG = NWG / 4;                 // producers per poller wave
-        unsigned long long gr[NPASS][NPG];
-        // (1) PROBE: each lane checks ONE producer of its pair (lanes rotate over the producers), so the wave
-        //     as a whole samples every producer with a single load per lane per round.
-        while (true) {
-          bool ok = true;
+        for (int g0 = 0; g0 < B && !dead; g0 += 8) {
+          i32x4 g2[NLD];
+          if (g0 == 0) {
+            while (*(volatile int*)&pub_cnt < 4 * k) __builtin_amdgcn_s_sleep(0);   // see the forward
+            sleep_n(pre_sleep);
+          }
+          while (true) {
 #pragma unroll
-          for (int ps = 0; ps < NPASS; ++ps) {
-            const int p = ps * 64 + lane;
-            if (ps < npass && p < P) {
-              const int wp = pg * NPG + (lane % NPG);
-              gr[ps][0] = ld_granule(slot + ((size_t)wp * B + (p >> 3)) * H + j0 + (p & 7));
+            for (int i = 0; i < NLD; ++i) {
+              const int b = g0 + i * RPP + ro;
+              if (b < B) g2[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (b * NWG * NWG * 2 + chunk) * 16, 0, kSc1);
             }
+            bool ok = true;
+#pragma unroll
+            for (int i = 0; i < NLD; ++i)
+              if (g0 + i * RPP + ro < B) ok &= ((unsigned)g2[i].y == tag) & ((unsigned)g2[i].w == tag);
+            if (__all(ok)) break;
+            if (spin_fail(spins, err, 2u)) { dead = true; break; }
+            sleep_n(spin_sleep);
           }
 #pragma unroll
-          for (int ps = 0; ps < NPASS; ++ps)
-            if (ps < npass && ps * 64 + lane < P) ok &= (unsigned)(gr[ps][0] >> 32) == tag;
-          if (__all(ok)) break;
-          if (spin_fail(spins, err, 2u)) { dead = true; break; }
-        }
-        // (2) FETCH every granule of the round, all loads in flight before any use; verify, refetch if needed.
-        while (!dead) {
+          for (int i = 0; i < NLD; ++i) {
+            float sv[4];
+            const unsigned x = (unsigned)g2[i].x, z = (unsigned)g2[i].z;
+            sv[0] = __uint_as_float(x << 16); sv[1] = __uint_as_float(x & 0xffff0000u);
+            sv[2] = __uint_as_float(z << 16); sv[3] = __uint_as_float(z & 0xffff0000u);
 #pragma unroll
-          for (int ps = 0; ps < NPASS; ++ps) {
-            const int p = ps * 64 + lane;
-            if (ps < npass && p < P) {
-              const int b = p >> 3, jj = p & 7;
+            for (int o = 2; o < LSPAN; o <<= 1)
 #pragma unroll
-              for (int i = 0; i < NPG; ++i)
-                gr[ps][i] = ld_granule(slot + ((size_t)(pg * NPG + i) * B + b) * H + j0 + jj);
+              for (int q = 0; q < 4; ++q) sv[q] += __shfl_xor(sv[q], o, 64);
+            const int b = g0 + i * RPP + ro;
+            if ((lane % LSPAN) < 2 && b < B) {
+#pragma unroll
+              for (int q = 0; q < 4; ++q) dpart[par][pslot][b * kUw + (lane & 1) * 4 + q] = sv[q];
             }
           }
-          bool ok = true;
-#pragma unroll
-          for (int ps = 0; ps < NPASS; ++ps)
-            if (ps < npass && ps * 64 + lane < P) {
-#pragma unroll
-              for (int i = 0; i < NPG; ++i) ok &= (unsigned)(gr[ps][i] >> 32) == tag;
-            }
-          if (__all(ok)) break;
-          if (spin_fail(spins, err, 2u)) { dead = true; break; }
-        }
-#pragma unroll
-        for (int ps = 0; ps < NPASS; ++ps) {
-          float s = 0.f;
-#pragma unroll
-          for (int i = 0; i < NPG; ++i) s += __uint_as_float((unsigned)gr[ps][i]);
-          ssum[ps] = (ps < npass && ps * 64 + lane < P) ? s : 0.f;
         }
       }
-#pragma unroll
-      for (int ps = 0; ps < NPASS; ++ps) {
-        const int p = ps * 64 + lane;
-        if (p < P) dpart[par][pg][p] = ssum[ps];
-      }
+      DCA_TSTAMPB(1);
       if (dead && lane == 0) abort_flag = 1;
       if (t >= 0) {
 #pragma unroll
@@ -511,6 +537,7 @@ __global__ __launch_bounds__(kBwdThreads) void lstm_bwd_kernel(const float* __re
           if (idx < 7 * P) inp[par][idx / P][idx % P] = iv[i];
         }
       }
+      DCA_TSTAMPB(2);
     }
     lds_barrier();
     if (abort_flag) break;
@@ -518,12 +545,19 @@ __global__ __launch_bounds__(kBwdThreads) void lstm_bwd_kernel(const float* __re
       // final gather done: ∂L/∂h0
       if (poller) {
         for (int p = tid; p < P; p += 256)
-          dh0[(p >> 3) * H + j0 + (p & 7)] = dpart[par][0][p] + dpart[par][1][p] + dpart[par][2][p] + dpart[par][3][p];
+        {
+          float v = 0.f;
+#pragma unroll
+          for (int sl = 0; sl < NSLOT; ++sl) v += dpart[par][sl][p];
+          dh0[(p >> 3) * H + j0 + (p & 7)] = v;
+        }
       }
       break;
     }
     if (!poller) {
+      DCA_TSTAMPB(3);
       // -------- gate gradients of the owned units (every publisher wave computes all pairs)
+      float dgr[NPR][4];
 #pragma unroll
       for (int r = 0; r < NPR; ++r) {
         const int p = lane + 64 * r;
@@ -532,31 +566,26 @@ __global__ __launch_bounds__(kBwdThreads) void lstm_bwd_kernel(const float* __re
           const int b = p >> 3, jj = p & 7;
           const float ig = inp[par][0][p], fg = inp[par][1][p], gg = inp[par][2][p], og = inp[par][3][p];
           const float c = inp[par][4][p], cprev = inp[par][5][p];
-          const float dht = inp[par][6][p] + dpart[par][0][p] + dpart[par][1][p] + dpart[par][2][p] +
-                            dpart[par][3][p];
+          float dht = inp[par][6][p];
+#pragma unroll
+          for (int sl = 0; sl < NSLOT; ++sl) dht += dpart[par][sl][p];
           const float tc = dca::tanhf_(c);
           const float dc = dcreg[r] + dht * og * (1.f - tc * tc);
-          const float d_o = dht * tc * og * (1.f - og);
-          const float d_i = dc * gg * ig * (1.f - ig);
-          const float d_f = dc * cprev * fg * (1.f - fg);
-          const float d_g = dc * ig * (1.f - gg * gg);
+          dgr[r][3] = dht * tc * og * (1.f - og);
+          dgr[r][0] = dc * gg * ig * (1.f - ig);
+          dgr[r][1] = dc * cprev * fg * (1.f - fg);
+          dgr[r][2] = dc * ig * (1.f - gg * gg);
           dcreg[r] = dc * fg;
-          dgl[pw][b][0 * 8 + jj] = dca::f2bf(d_i);
-          dgl[pw][b][1 * 8 + jj] = dca::f2bf(d_f);
-          dgl[pw][b][2 * 8 + jj] = dca::f2bf(d_g);
-          dgl[pw][b][3 * 8 + jj] = dca::f2bf(d_o);
-          if (pw == 0) {
-            float* dg = dgates + ((size_t)b * S + t) * G4 + j0 + jj;
-            dg[0] = d_i;
-            dg[H] = d_f;
-            dg[2 * H] = d_g;
-            dg[3 * H] = d_o;
-            if (t == 0) dc0[b * H + j0 + jj] = dcreg[r];
-          }
+#pragma unroll
+          for (int q = 0; q < 4; ++q) dgl[pw][b][q * 8 + jj] = dca::f2bf(dgr[r][q]);
         }
       }
-      // -------- partial = dG_blk (B×32) · W_blk (32 × this wave's H/4 columns) → granules of step t
-      unsigned long long* slot = ring + (size_t)(t & 1) * NWG * B * H + (size_t)w * B * H;
+      DCA_TSTAMPB(4);
+      // -------- partial = dG_blk (B×32) · W_blk (32 × this wave's H/4 columns) → hand-off chunks of step t.
+      // Chunk = 16 bytes {bf16 u0,u1 | tag | bf16 u2,u3 | tag} per (row, consumer, producer, unit quad). Store
+      // instructions, not bytes, are what a CU's memory path pays for, so the accumulator tiles are transposed
+      // through LDS (bf16) and every lane then stores whole chunks: B·H/64/64 full-wave stores instead of 4 per
+      // 16-column tile.
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) {
         const bf16x8 a = *reinterpret_cast<const bf16x8*>(&dgl[pw][mt * 16 + lrow][8 * lkg]);
@@ -564,18 +593,57 @@ __global__ __launch_bounds__(kBwdThreads) void lstm_bwd_kernel(const float* __re
         for (int n = 0; n < NT_W; ++n) {
           dca::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
           acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[n], acc, 0, 0, 0);
-          const int col = (pw * NT_W + n) * 16 + lrow;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int b = mt * 16 + lkg * 4 + r;
-            if (b < B)
-              st_granule(slot + (size_t)b * H + col,
-                         ((unsigned long long)(unsigned)(t + 1) << 32) | __float_as_uint(acc[r]));
+          for (int r = 0; r < 4; ++r) stg[pw][mt * 16 + lkg * 4 + r][n * 16 + lrow] = (unsigned short)dca::f2bf(acc[r]);
+        }
+      }
+      {
+        const __amdgpu_buffer_rsrc_t ws = uniform_rsrc(ring + (size_t)(t & 1) * B * NWG * NWG * 4, B * NWG * NWG * 32);
+        const int tg = t + 1;
+        constexpr int QPR = NT_W * 4;                 // unit quads per row in this wave's columns
+        const int nq = B * QPR;
+        for (int qi = lane; qi < nq; qi += 64) {
+          const int b = qi / QPR, cq = qi % QPR;
+          const uint2 v = *reinterpret_cast<const uint2*>(&stg[pw][b][cq * 4]);
+          const int col = pw * NT_W * 16 + cq * 4;
+          const i32x4 cv = {(int)v.x, tg, (int)v.y, tg};
+          __builtin_amdgcn_raw_buffer_store_b128(cv, ws, (((b * NWG + (col >> 3)) * NWG + w) * 2 + ((col & 7) >> 2)) * 16,
+                                                 0, kSc1);
+        }
+      }
+      if (lane == 0) atomicAdd(&pub_cnt, 1);
+      DCA_TSTAMPB(5);
+      // -------- ∂gates outputs (off the hand-off critical path)
+      if (pw == 0) {
+#pragma unroll
+        for (int r = 0; r < NPR; ++r) {
+          const int p = lane + 64 * r;
+          if (64 * r >= P) break;
+          if (p < P) {
+            const int b = p >> 3, jj = p & 7;
+            float* dg = dgates + ((size_t)b * S + t) * G4 + j0 + jj;
+            dg[0] = dgr[r][0];
+            dg[H] = dgr[r][1];
+            dg[2 * H] = dgr[r][2];
+            dg[3 * H] = dgr[r][3];
+            if (t == 0) dc0[b * H + j0 + jj] = dcreg[r];
           }
         }
       }
+      DCA_TSTAMPB(6);
     }
   }
+#undef DCA_TSTAMPB
+}
+
+// Tuning knobs (s_sleep counts before the first poll / after a failed poll round) for fwd and bwd, read from
+// DCA_LSTM_KNOBS="fpre,fspin,bpre,bspin" on every launch (default 0 0 0 0) — for latency experiments only.
+inline int knob(int i) {
+  const char* e = getenv("DCA_LSTM_KNOBS");
+  if (!e) return 0;
+  int v[4] = {0, 0, 0, 0};
+  sscanf(e, "%d,%d,%d,%d", &v[0], &v[1], &v[2], &v[3]);
+  return v[i];
 }
 
 // Chains: sequences are split into independent groups of Bc ≤ 16·MT (MT ≤ 2 keeps every variant spill-free), all
@@ -597,19 +665,20 @@ hipError_t launch_fwd(const float* xp, const short* whh, const float* h0, const 
   hipError_t e = hipMemsetAsync(ring, 0, sizeof(unsigned long long) * (size_t)nch * 2 * Bc * (H / 2), st);
   if (e != hipSuccess) return e;
   lstm_fwd_kernel<MT, KS><<<nch * (H / kUw), kFwdThreads, 0, st>>>(xp, whh, h0, c0, hs, hsf, cs, gates, hn, cn,
-                                                                   ring, err, B, Bc, S, trace);
+                                                                   ring, err, B, Bc, S, trace, knob(0), knob(1));
   return hipGetLastError();
 }
 
 template <int MT, int KS>
 hipError_t launch_bwd(const float* dhs, const float* gates, const float* cs, const float* c0, const float* dhn,
                       const float* dcn, const short* whh, float* dgates, float* dh0, float* dc0,
-                      unsigned long long* ring, unsigned* err, int B, int Bc, int nch, int S, hipStream_t st) {
+                      unsigned long long* ring, unsigned* err, int B, int Bc, int nch, int S,
+                      unsigned long long* trace, hipStream_t st) {
   constexpr int H = 128 * KS;
   hipError_t e = hipMemsetAsync(ring, 0, sizeof(unsigned long long) * (size_t)nch * 2 * (H / kUw) * Bc * H, st);
   if (e != hipSuccess) return e;
   lstm_bwd_kernel<MT, KS><<<nch * (H / kUw), kBwdThreads, 0, st>>>(dhs, gates, cs, c0, dhn, dcn, whh, dgates, dh0,
-                                                                   dc0, ring, err, B, Bc, S);
+                                                                   dc0, ring, err, B, Bc, S, knob(2), knob(3), trace);
   return hipGetLastError();
 }
 
@@ -654,12 +723,12 @@ extern "C" hipError_t dca_lstm_fwd(const float* xp, const short* whh, const floa
 extern "C" hipError_t dca_lstm_bwd(const float* dhs, const float* gates, const float* cs, const float* c0,
                                    const float* dhn, const float* dcn, const short* whh, float* dgates, float* dh0,
                                    float* dc0, unsigned long long* ring, unsigned* err, int B, int S, int H,
-                                   hipStream_t st) {
+                                   hipStream_t st, unsigned long long* trace) {
   if (!lstm_shape_ok(B, H) || S < 1) return hipErrorInvalidValue;
   int nch, Bc, MT;
   plan_chains(B, H, nch, Bc, MT);
   const int KS = H / 128;
-#define DCA_B(mt, ks) launch_bwd<mt, ks>(dhs, gates, cs, c0, dhn, dcn, whh, dgates, dh0, dc0, ring, err, B, Bc, nch, S, st)
+#define DCA_B(mt, ks) launch_bwd<mt, ks>(dhs, gates, cs, c0, dhn, dcn, whh, dgates, dh0, dc0, ring, err, B, Bc, nch, S, trace, st)
   DCA_DISPATCH_MT_KS(MT, KS, DCA_B)
 #undef DCA_B
 }
