@@ -28,6 +28,8 @@ import torch.nn.functional as F
 
 from .policy import TYPE_SUFFIX, Policy
 
+from ..ops.lstm import impl as lstm_impl  # noqa: E402
+
 LDZ = 160
 
 
@@ -87,16 +89,26 @@ class _PolicyLoss(torch.autograd.Function):
         if cfg.rnn == 'lstm':
             H = cfg.hidden
             wih16, whh16 = _bf(P['rnn.weight_ih_l0']), _bf(P['rnn.weight_hh_l0'])
-            xp = (_mm(x16, wih16.t()) + (P['rnn.bias_ih_l0'].detach() + P['rnn.bias_hh_l0'].detach())).view(B, S, 4 * H)
-            hs, cs, gates = [], [], []
-            mb = C.lstm_max_batch(H)
-            for s0 in range(0, B, mb):
-                s1 = min(B, s0 + mb)
-                o = C.lstm_fwd(xp[s0:s1], whh16, h0[s0:s1].contiguous(), c0[s0:s1].contiguous(), fp.err, False)
-                hs.append(o[0]); cs.append(o[2]); gates.append(o[3])
-            cat = (lambda L: torch.cat(L) if len(L) > 1 else L[0])
-            hs16, cs, gates = cat(hs), cat(cs), cat(gates)
+            bias = P['rnn.bias_ih_l0'].detach() + P['rnn.bias_hh_l0'].detach()
+            if lstm_impl() == 'team':
+                # unit-major gate order: W_ih rows permuted so x·W_ihᵀ lands directly in the (B,S,H,4) layout
+                perm = fp.gate_perm(H, wih16.device)
+                wih16 = wih16[perm].contiguous()
+                xp4 = (_mm(x16, wih16.t()) + bias[perm]).view(B, S, H, 4)
+                hs16, _, cs, gates, _, _ = C.lstm_team_fwd(xp4, whh16, h0, c0, fp.err, False)
+            else:
+                perm = None
+                xp = (_mm(x16, wih16.t()) + bias).view(B, S, 4 * H)
+                hs, cs, gates = [], [], []
+                mb = C.lstm_max_batch(H)
+                for s0 in range(0, B, mb):
+                    s1 = min(B, s0 + mb)
+                    o = C.lstm_fwd(xp[s0:s1], whh16, h0[s0:s1].contiguous(), c0[s0:s1].contiguous(), fp.err, False)
+                    hs.append(o[0]); cs.append(o[2]); gates.append(o[3])
+                cat = (lambda L: torch.cat(L) if len(L) > 1 else L[0])
+                hs16, cs, gates = cat(hs), cat(cs), cat(gates)
             xh16 = hs16.view(N, H)
+            ctx.perm = perm
             rnn_saved = (hs16, cs, gates, wih16, whh16)
         else:
             wf16 = _bf(P['fake_rnn.weight'])
@@ -137,19 +149,29 @@ class _PolicyLoss(torch.autograd.Function):
             hs16, cs, gates, wih16, whh16 = rnn_saved
             H = cfg.hidden
             dxh3 = dxh.view(B, S, H)
-            dg = []
-            mb = C.lstm_max_batch(H)
-            for s0 in range(0, B, mb):
-                s1 = min(B, s0 + mb)
-                o = C.lstm_bwd(dxh3[s0:s1], gates[s0:s1], cs[s0:s1], c0[s0:s1].contiguous(), None, None, whh16,
-                               fp.err)
-                dg.append(o[0])
-            dgates = (torch.cat(dg) if len(dg) > 1 else dg[0]).view(N, 4 * H)
+            perm = ctx.perm
+            if perm is not None:
+                dgates = C.lstm_team_bwd(dxh3, gates, cs, c0, None, None, whh16, fp.err)[0].view(N, 4 * H)
+            else:
+                dg = []
+                mb = C.lstm_max_batch(H)
+                for s0 in range(0, B, mb):
+                    s1 = min(B, s0 + mb)
+                    o = C.lstm_bwd(dxh3[s0:s1], gates[s0:s1], cs[s0:s1], c0[s0:s1].contiguous(), None, None, whh16,
+                                   fp.err)
+                    dg.append(o[0])
+                dgates = (torch.cat(dg) if len(dg) > 1 else dg[0]).view(N, 4 * H)
             dG16 = dgates.to(torch.bfloat16)
             hprev = torch.cat([h0.to(torch.bfloat16).unsqueeze(1), hs16[:, :-1]], dim=1).view(N, H)
-            grads['rnn.weight_hh_l0'] = _mm(dG16.t(), hprev)
-            grads['rnn.weight_ih_l0'] = _mm(dG16.t(), x16)
+            dwhh = _mm(dG16.t(), hprev)
+            dwih = _mm(dG16.t(), x16)
             db = dgates.sum(0)
+            if perm is not None:           # back to PyTorch's gate-major row order
+                inv = torch.empty_like(perm)
+                inv[perm] = torch.arange(perm.numel(), device=perm.device)
+                dwhh, dwih, db = dwhh[inv], dwih[inv], db[inv]
+            grads['rnn.weight_hh_l0'] = dwhh
+            grads['rnn.weight_ih_l0'] = dwih
             grads['rnn.bias_ih_l0'] = db
             grads['rnn.bias_hh_l0'] = db
             dx = _mm(dG16, wih16)
@@ -215,6 +237,13 @@ class FusedPolicy:
         self.param_names: List[str] = [n for n, _ in policy.named_parameters()]
         self.params = [p for _, p in policy.named_parameters()]
         self.fully_fused = not self.cfg.entity_attention and self.cfg.unit_dim == 128 and self.cfg.env_dim == 128
+
+    def gate_perm(self, H, device):
+        key = (H, str(device))
+        if getattr(self, '_perm_key', None) != key:
+            from ..ops.lstm import gate_perm
+            self._perm, self._perm_key = gate_perm(H, device), key
+        return self._perm
 
     def refresh(self):
         self.params = [p for _, p in self.policy.named_parameters()]

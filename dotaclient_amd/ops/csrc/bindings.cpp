@@ -101,6 +101,61 @@ std::vector<torch::Tensor> lstm_bwd(torch::Tensor dhs, torch::Tensor gates, torc
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// XCD-team LSTM recurrence (lstm_team.hip). Gates in unit-major (B,S,H,4) layout; see the kernel header.
+std::vector<torch::Tensor> lstm_team_fwd(torch::Tensor xp4, torch::Tensor whh, torch::Tensor h0, torch::Tensor c0,
+                                         torch::Tensor err, bool want_f32_h, c10::optional<torch::Tensor> trace) {
+  CHECK_F32(xp4); CHECK_BF16(whh); CHECK_F32(h0); CHECK_F32(c0); CHECK_I32(err);
+  TORCH_CHECK(xp4.dim() == 4 && xp4.size(3) == 4, "xp4 must be (B,S,H,4)");
+  const int B = xp4.size(0), S = xp4.size(1), H = xp4.size(2);
+  TORCH_CHECK(whh.size(0) == 4 * H && whh.size(1) == H, "whh must be (4H,H)");
+  TORCH_CHECK(h0.size(0) == B && h0.size(1) == H && c0.size(0) == B && c0.size(1) == H, "h0/c0 must be (B,H)");
+  TORCH_CHECK(H == 128 || H == 256 || H == 512, "lstm_team_fwd: H in {128,256,512}");
+  auto f32 = xp4.options();
+  auto hs = torch::empty({B, S, H}, f32.dtype(at::kBFloat16));
+  torch::Tensor hsf = want_f32_h ? torch::empty({B, S, H}, f32) : torch::Tensor();
+  auto cs = torch::empty({B, S, H}, f32);
+  auto gates4 = torch::empty({B, S, H, 4}, f32);
+  auto hn = torch::empty({B, H}, f32);
+  auto cn = torch::empty({B, H}, f32);
+  const size_t wsb = dca_lstm_team_workspace(B, H, 0);
+  auto ws = torch::empty({(int64_t)wsb}, f32.dtype(at::kByte));
+  hip_check(dca_lstm_team_fwd(ptr<float>(xp4), ptr<short>(whh), ptr<float>(h0), ptr<float>(c0), ptr<short>(hs),
+                              want_f32_h ? ptr<float>(hsf) : nullptr, ptr<float>(cs), ptr<float>(gates4),
+                              ptr<float>(hn), ptr<float>(cn), ws.data_ptr(), wsb, ptr<unsigned>(err), B, S, H,
+                              cur_stream(),
+                              (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr),
+            "dca_lstm_team_fwd");
+  return {hs, want_f32_h ? hsf : hs, cs, gates4, hn, cn};
+}
+
+std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4, torch::Tensor cs,
+                                         torch::Tensor c0, c10::optional<torch::Tensor> dhn,
+                                         c10::optional<torch::Tensor> dcn, torch::Tensor whh, torch::Tensor err) {
+  CHECK_F32(dhs); CHECK_F32(gates4); CHECK_F32(cs); CHECK_F32(c0); CHECK_BF16(whh); CHECK_I32(err);
+  const int B = dhs.size(0), S = dhs.size(1), H = dhs.size(2);
+  TORCH_CHECK(gates4.dim() == 4 && gates4.size(0) == B && gates4.size(1) == S && gates4.size(2) == H &&
+                  gates4.size(3) == 4, "gates4 must be (B,S,H,4)");
+  TORCH_CHECK(cs.sizes() == dhs.sizes(), "cs must be (B,S,H)");
+  TORCH_CHECK(whh.size(0) == 4 * H && whh.size(1) == H, "whh must be (4H,H)");
+  TORCH_CHECK(H == 128 || H == 256 || H == 512, "lstm_team_bwd: H in {128,256,512}");
+  const float* dhn_p = nullptr;
+  const float* dcn_p = nullptr;
+  if (dhn.has_value() && dhn->defined()) { CHECK_F32((*dhn)); dhn_p = ptr<float>(*dhn); }
+  if (dcn.has_value() && dcn->defined()) { CHECK_F32((*dcn)); dcn_p = ptr<float>(*dcn); }
+  auto f32 = dhs.options();
+  auto dgates4 = torch::empty({B, S, H, 4}, f32);
+  auto dh0 = torch::empty({B, H}, f32);
+  auto dc0 = torch::empty({B, H}, f32);
+  const size_t wsb = dca_lstm_team_workspace(B, H, 1);
+  auto ws = torch::empty({(int64_t)wsb}, f32.dtype(at::kByte));
+  hip_check(dca_lstm_team_bwd(ptr<float>(dhs), ptr<float>(gates4), ptr<float>(cs), ptr<float>(c0), dhn_p, dcn_p,
+                              ptr<short>(whh), ptr<float>(dgates4), ptr<float>(dh0), ptr<float>(dc0), ws.data_ptr(),
+                              wsb, ptr<unsigned>(err), B, S, H, cur_stream()),
+            "dca_lstm_team_bwd");
+  return {dgates4, dh0, dc0};
+}
+
+// ------------------------------------------------------------------------------------------------------------
 // Fused heads + loss. Returns (dz (N,ldz) f32, dtl (N,U) f32, partials (nblk,16) f32, logp (N) f32).
 std::vector<torch::Tensor> heads_loss(torch::Tensor z, torch::Tensor emb, torch::Tensor act, torch::Tensor msk,
                                       torch::Tensor adv, torch::Tensor ret, torch::Tensor logp_old,
@@ -234,6 +289,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_bwd", &lstm_bwd, "persistent LSTM backward recurrence (granule reduce-scatter)", py::arg("dhs"),
         py::arg("gates"), py::arg("cs"), py::arg("c0"), py::arg("dhn"), py::arg("dcn"), py::arg("whh"), py::arg("err"),
         py::arg("trace") = py::none());
+  m.def("lstm_team_fwd", &lstm_team_fwd, "XCD-team persistent LSTM forward (L2-local hand-off), (B,S,H,4) gates",
+        py::arg("xp4"), py::arg("whh"), py::arg("h0"), py::arg("c0"), py::arg("err"), py::arg("want_f32_h"),
+        py::arg("trace") = py::none());
+  m.def("lstm_team_bwd", &lstm_team_bwd, "XCD-team persistent LSTM backward (L2-local reduce-scatter)",
+        py::arg("dhs"), py::arg("gates4"), py::arg("cs"), py::arg("c0"), py::arg("dhn"), py::arg("dcn"),
+        py::arg("whh"), py::arg("err"));
   m.def("sample_actions", &sample_actions, "fused masked hierarchical Gumbel-max action sampling (actor)");
   m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)");
 }

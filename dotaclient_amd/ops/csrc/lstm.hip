@@ -56,6 +56,7 @@ __device__ __forceinline__ void raise_err(unsigned* p, unsigned code) {
 
 // Bounded-spin bookkeeping shared by all polls of a wave. Returns true when the wave must give up.
 __device__ __forceinline__ bool spin_fail(unsigned& spins, unsigned* err, unsigned code) {
+  asm volatile("" ::: "memory");   // compiler barrier: the next poll round's buffer loads must be re-issued
   ++spins;
   if ((spins & 255u) == 0) {
     if (ld_err(err) != 0) return true;

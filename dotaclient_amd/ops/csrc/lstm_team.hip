@@ -1,0 +1,646 @@
+// XCD-team persistent LSTM recurrence (forward / backward) for gfx950 — the default learner recurrence.
+//
+// Same math as lstm.hip (reference north star: policy.py:67-68, 143-145 sketch an LSTM; BASELINE.json names the
+// LSTM policy), different machine mapping. A recurrence step is latency-bound: its critical path is one
+// all-to-all hand-off of the step's state between the workgroups that own slices of W_hh. lstm.hip spreads 64
+// workgroups over all 8 XCDs, so every hand-off crosses the Infinity Fabric (write-through + L2-bypassing polls,
+// ≈2.5-3 µs per all-gather under load). Here a TEAM of 32 workgroups — one per CU of a single XCD — runs a whole
+// sequence chain and exchanges through that XCD's shared L2: plain stores keep the lines in L2 and sc1 polls (L1
+// bypass, L2-served) see them ≈0.2 µs later (scripts/ubench/xcd_pingpong.hip: 451 ns round trip same-XCD vs
+// 768 ns cross-XCD, idle). Up to 8 teams (one per XCD) run independent chains of ≤ 32 sequences concurrently.
+//
+// Team formation is placement-robust: every workgroup reads HW_REG_XCC_ID and takes a ticket on its XCC's
+// counter; the first 32 of an XCC form its team, a leader commits the team only when all 32 arrived (bounded
+// wait), and committed teams pull chains from a shared queue — so any dispatch that lands ≥ 32 workgroups on at
+// least one XCD finishes every chain (if none does, *err = 3 and the caller falls back to lstm.hip).
+//
+// Layouts (unit-major gates "(H,4)" so a hidden unit's 4 gates are one 16-byte vector):
+//   xp4    (B, S, H, 4) f32  x·W_ihᵀ + b_ih + b_hh with W_ih rows permuted to (unit, gate) order
+//   whh    (4H, H)      bf16 PyTorch layout (gate-major rows i,f,g,o)
+//   gates4 (B, S, H, 4) f32  activated i, f, g, o          dgates4 (B, S, H, 4) f32 ∂L/∂pre-activations
+//   hs (B,S,H) bf16, hsf (B,S,H) f32 (optional), cs (B,S,H) f32, h0/c0/hn/cn/dh0/dc0 (B,H) f32
+// Each workgroup (member m of 32) owns U = H/32 hidden units J_m = [mU, mU+U) and their 4U gate rows.
+//
+// Forward step t:  gather h_{t-1} (B×H bf16, tagged granules, all 256 threads) → LDS → barrier → waves w < U/4
+//   each own one 16-column MFMA tile = 4 units × 4 gates over the full K = H, W slice in VGPRs → 4×4 lane
+//   transpose puts (i,f,g,o) of one (row, unit) in one lane → cell update (c in registers) → publish h_t granules.
+// Backward step t (reduce-scatter, partials in bf16): gather Σ_producers partial dh for own units (xor-shuffle
+//   reduction over the 32 producers) → barrier → gate gradients per (row, unit) → dG (bf16) to LDS → barrier →
+//   partial dh_{t-1} (B×H) = dG_own (B×4U) · W_own (4U×H) on MFMA, W slice in VGPRs → LDS transpose → full-wave
+//   16-byte chunk stores {2×bf16, tag, 2×bf16, tag} to each consumer's block.
+#include "common.h"
+#include <cstdlib>
+
+namespace {
+
+using dca::bf16x8;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+constexpr int kT = 32;                  // workgroups per team (CUs per XCD)
+constexpr int kMaxTeams = 8;
+constexpr int kThreads = 256;
+constexpr int kSc1 = 16;                // buffer cache policy: sc1 (bypass the CU's L1, served by the XCD L2)
+constexpr int kPlain = 0;               // plain store: write-through L1, line stays in the XCD L2
+constexpr unsigned kSpinLimit = 1u << 22;
+
+struct TeamCtl {                         // zeroed before every launch
+  unsigned xcnt[16];                     // tickets per XCC
+  unsigned state[kMaxTeams];             // 0 pending, 1 committed, 2 aborted
+  unsigned chain[kMaxTeams];             // (announce iter << 16) | chain id
+  unsigned done[kMaxTeams];              // members that finished their current chain
+  unsigned next_chain;
+  unsigned abort;
+};
+
+__device__ __forceinline__ unsigned xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xf; }
+__device__ __forceinline__ unsigned ld_acq(const unsigned* p) {
+  return __hip_atomic_load((__attribute__((address_space(1))) unsigned*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_rel(unsigned* p, unsigned v) {
+  __hip_atomic_store((__attribute__((address_space(1))) unsigned*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned add_agent(unsigned* p, unsigned v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, int bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0,
+                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// Bounded spin bookkeeping; true when this wave must give up (timeout or another workgroup raised an error).
+__device__ __forceinline__ bool spin_fail(unsigned& spins, TeamCtl* ctl, unsigned* err, unsigned code) {
+  asm volatile("" ::: "memory");        // compiler barrier: re-issue the poll loads every round
+  ++spins;
+  if ((spins & 255u) == 0) {
+    if (ld_acq(&ctl->abort) != 0) return true;
+    if (spins > kSpinLimit) {
+      st_rel(err, code);
+      st_rel(&ctl->abort, 1u);
+      return true;
+    }
+  }
+  if (spins > 32) __builtin_amdgcn_s_sleep(1);
+  return false;
+}
+
+// Team formation + chain queue. Returns the team id (≥ 0) or -1 if this workgroup must exit. Called by all
+// threads; thread 0 does the global traffic, the result is broadcast through LDS.
+__device__ int join_team(TeamCtl* ctl, unsigned* err, int* sh) {
+  if (threadIdx.x == 0) {
+    int res = -1;
+    const unsigned x = xcc_id();
+    if (x < kMaxTeams) {
+      const unsigned r = add_agent(&ctl->xcnt[x], 1u);
+      if (r < (unsigned)kT) {
+        res = (int)x * 64 + (int)r;        // team x, member r
+        unsigned spins = 0;
+        if (r == 0) {
+          bool ok = false;
+          while (true) {
+            if (ld_acq(&ctl->xcnt[x]) >= (unsigned)kT) { ok = true; break; }
+            if (++spins > (1u << 16)) break;
+            __builtin_amdgcn_s_sleep(2);
+          }
+          st_rel(&ctl->state[x], ok ? 1u : 2u);
+          if (!ok) {
+            res = -1;
+            st_rel(err, 3u);                 // team formation failed on this XCD (placement/residency)
+          }
+        } else {
+          unsigned s;
+          while ((s = ld_acq(&ctl->state[x])) == 0) {
+            if (++spins > (1u << 18)) break;
+            __builtin_amdgcn_s_sleep(2);
+          }
+          if (s != 1) res = -1;
+        }
+      }
+    }
+    *sh = res;
+  }
+  __syncthreads();
+  return *sh;
+}
+
+// Next chain for this team (all members agree). Returns chain id or -1 when the queue is drained / aborted.
+__device__ int next_chain(TeamCtl* ctl, int team, int member, unsigned iter, int nch, int* sh) {
+  if (threadIdx.x == 0) {
+    int res = -1;
+    unsigned spins = 0;
+    if (member == 0) {
+      // every member finished the previous chain (its exchange buffers are free again)
+      while (ld_acq(&ctl->done[team]) < (unsigned)kT * iter) {
+        if (ld_acq(&ctl->abort) || ++spins > (1u << 24)) { spins = ~0u; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      unsigned c = spins == ~0u ? 0xffffu : add_agent(&ctl->next_chain, 1u);
+      if (c > 0xffffu) c = 0xffffu;
+      st_rel(&ctl->chain[team], ((iter + 1) << 16) | c);
+      res = (c < (unsigned)nch) ? (int)c : -1;
+    } else {
+      unsigned v;
+      while (((v = ld_acq(&ctl->chain[team])) >> 16) != iter + 1) {
+        if (ld_acq(&ctl->abort) || ++spins > (1u << 24)) { v = 0xffffu; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      const unsigned c = v & 0xffffu;
+      res = (c < (unsigned)nch) ? (int)c : -1;
+    }
+    *sh = res;
+  }
+  __syncthreads();
+  return *sh;
+}
+
+// =============================================================================================================
+// Forward. MT = 16-row batch tiles per chain (Bc ≤ 16·MT), KS = H/128.
+// xg (per team): [2 parity][Bc][H/2] u64 granules {lo: 2×bf16 h, hi: tag}
+// =============================================================================================================
+template <int MT, int KS>
+__global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
+    const float* __restrict__ xp4, const short* __restrict__ whh, const float* __restrict__ h0,
+    const float* __restrict__ c0, short* __restrict__ hs, float* __restrict__ hsf, float* __restrict__ cs,
+    float* __restrict__ gates4, float* __restrict__ hn, float* __restrict__ cn, unsigned long long* xg_all,
+    TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, unsigned long long* trace,
+    int knobs) {
+  constexpr int H = 128 * KS;
+  constexpr int U = H / kT;             // units per workgroup (4·KS)
+  constexpr int NTILE = U / 4;          // 16-column MFMA tiles per workgroup (= KS)
+  constexpr int KSTEP = H / 32;         // k-steps of the full K
+  constexpr int HP = H + 8;             // LDS row pitch (bf16)
+  constexpr int RB = MT * 16;
+  __shared__ short hl[2][RB][HP];
+  __shared__ int sh_int;
+
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int me = join_team(ctl, err, &sh_int);
+  if (me < 0) return;
+  const int team = me >> 6, m = me & 63;
+  const int j0 = m * U;
+#define TSTAMP(ev)                                                                                        \
+  if (trace && lane == 0 && team == 0 && t < 64)                                                          \
+    trace[(((size_t)m * 4 + wv) * 64 + t) * 8 + (ev)] = __builtin_amdgcn_s_memrealtime()
+  unsigned long long* xg = xg_all + (size_t)team * 2 * Bc * (H / 2);
+
+  // zero the padding rows of both h buffers once
+  for (int i = tid; i < 2 * RB * HP; i += kThreads) (&hl[0][0][0])[i] = 0;
+
+  // W_hh slice for this wave's tile: columns c = 4·ul + q ↔ gate row q·H + j0 + 4·wv + ul, full K, in VGPRs
+  const bool mfma_wave = wv < NTILE;
+  const int col = lane & 15, kg = lane >> 4;
+  bf16x8 wf[KSTEP];
+  if (mfma_wave) {
+    const int row = (col & 3) * H + j0 + 4 * wv + (col >> 2);
+#pragma unroll
+    for (int ks = 0; ks < KSTEP; ++ks)
+      wf[ks] = *reinterpret_cast<const bf16x8*>(whh + (size_t)row * H + ks * 32 + 8 * kg);
+  }
+  // elementwise mapping after the 4×4 transpose: lane → (row 4·kg + (col&3) [+16·mt], unit j0 + 4·wv + col/4)
+  const int erow = 4 * kg + (col & 3);
+  const int eunit = j0 + 4 * wv + (col >> 2);
+
+  unsigned spins = 0;
+  for (unsigned iter = 0;; ++iter) {
+    const int chain = next_chain(ctl, team, m, iter, nch, &sh_int);
+    if (chain < 0) break;
+    const int b0 = chain * Bc;
+    const int B = min(Bc, Btot - b0);
+    const unsigned tagbase = (iter + 1) << 16;
+    const float* xpc = xp4 + (size_t)b0 * S * H * 4;
+    float creg[MT], hreg[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int b = mt * 16 + erow;
+      creg[mt] = (mfma_wave && b < B) ? c0[(size_t)(b0 + b) * H + eunit] : 0.f;
+      hreg[mt] = 0.f;
+    }
+    bool dead = false;
+    for (int t = 0; t < S; ++t) {
+      const int par = t & 1;
+      TSTAMP(0);
+      // ---- prefetch this step's input projection (one 16-B vector per owned (row, unit))
+      dca::f32x4 xv[MT];
+      if (mfma_wave) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const int b = mt * 16 + erow;
+          xv[mt] = (b < B) ? *reinterpret_cast<const dca::f32x4*>(xpc + (((size_t)b * S + t) * H + eunit) * 4)
+                           : dca::f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      // ---- gather h_{t-1} into hl[par]
+      if (t == 0) {
+        for (int i = tid; i < B * H; i += kThreads) {
+          const int b = i / H, k = i % H;
+          hl[par][b][k] = dca::f2bf(h0[(size_t)(b0 + b) * H + k]);
+        }
+      } else {
+        const unsigned tag = tagbase | (unsigned)t;          // h_{t-1} carries tag t
+        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(xg + (size_t)((t - 1) & 1) * Bc * (H / 2), Bc * (H / 2) * 8);
+        constexpr int CPR = H / 4;                            // 16-B chunks (4 h values) per row
+        constexpr int NL = (RB * CPR + kThreads - 1) / kThreads;
+        // every chunk is re-polled only until it has arrived, so later rounds move only the missing bytes
+        i32x4 g[NL];
+        bool okc[NL];
+#pragma unroll
+        for (int i = 0; i < NL; ++i) okc[i] = tid + kThreads * i >= B * CPR;
+        for (int i = 0; i < (knobs & 0xff); ++i) __builtin_amdgcn_s_sleep(1);
+        if ((knobs >> 9) & 1) {
+          while (!okc[0]) {
+            g[0] = __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16, 0, kSc1);
+            okc[0] = ((unsigned)g[0].y == tag) & ((unsigned)g[0].w == tag);
+            if (__all(okc[0])) break;
+            if (spin_fail(spins, ctl, err, 1u)) { dead = true; break; }
+          }
+        }
+        while (!dead) {
+#pragma unroll
+          for (int i = 0; i < NL; ++i)
+            if (!okc[i]) g[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + kThreads * i) * 16, 0, kSc1);
+          bool ok = true;
+#pragma unroll
+          for (int i = 0; i < NL; ++i) {
+            okc[i] = okc[i] || (((unsigned)g[i].y == tag) & ((unsigned)g[i].w == tag));
+            ok &= okc[i];
+          }
+          if (__all(ok)) break;
+          if (spin_fail(spins, ctl, err, 1u)) { dead = true; break; }
+        }
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+          const int ci = tid + kThreads * i;
+          if (ci < B * CPR) {
+            const int b = ci / CPR, k = (ci % CPR) * 4;
+            *reinterpret_cast<u32x2*>(&hl[par][b][k]) = u32x2{(unsigned)g[i].x, (unsigned)g[i].z};
+          }
+        }
+      }
+      TSTAMP(1);
+      if (dead) sh_int = -2;
+      lds_barrier();
+      if (sh_int == -2) break;
+      TSTAMP(2);
+      if (mfma_wave) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          if (mt * 16 >= B) break;                            // wave-uniform
+          // ---- gates pre-activation tile: rows = batch, columns = (unit, gate)
+          dca::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < KSTEP; ++ks) {
+            const bf16x8 a = *reinterpret_cast<const bf16x8*>(&hl[par][mt * 16 + col][ks * 32 + 8 * kg]);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[ks], acc, 0, 0, 0);
+          }
+          // ---- 4×4 transpose inside each group of 4 lanes: lane (q' = col&3) gets gate q of row 4kg+q'
+          float gq0 = 0.f, gq1 = 0.f, gq2 = 0.f, gq3 = 0.f;
+          const int q0 = col & 3;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int sel = (q0 - j) & 3;                       // what this lane sends in round j
+            const float send = sel == 0 ? acc[0] : sel == 1 ? acc[1] : sel == 2 ? acc[2] : acc[3];
+            const int qs = (q0 + j) & 3;                        // gate carried by the received value
+            const float got = __shfl(send, (lane & ~3) | qs, 64);
+            gq0 = qs == 0 ? got : gq0;
+            gq1 = qs == 1 ? got : gq1;
+            gq2 = qs == 2 ? got : gq2;
+            gq3 = qs == 3 ? got : gq3;
+          }
+          const int b = mt * 16 + erow;
+          const float pi = gq0 + xv[mt][0], pf = gq1 + xv[mt][1], pg = gq2 + xv[mt][2], po = gq3 + xv[mt][3];
+          const float ig = dca::sigmoidf_(pi), fg = dca::sigmoidf_(pf), gg = dca::tanhf_(pg), og = dca::sigmoidf_(po);
+          const float c = fg * creg[mt] + ig * gg;
+          const float hv = og * dca::tanhf_(c);
+          if (b < B) { creg[mt] = c; hreg[mt] = hv; }
+          TSTAMP(3);
+          // ---- publish h_t: granule {h(u), h(u+1)} by the even-unit lane (partner unit is 4 lanes up)
+          const float hnb = __shfl_down(hv, 4, 64);
+          if (b < B && ((col >> 2) & 1) == 0) {
+            const unsigned pl = (unsigned)(unsigned short)dca::f2bf(hv) | ((unsigned)(unsigned short)dca::f2bf(hnb) << 16);
+            const u32x2 gv = {pl, tagbase | (unsigned)(t + 1)};
+            const __amdgpu_buffer_rsrc_t ws = uniform_rsrc(xg + (size_t)par * Bc * (H / 2), Bc * (H / 2) * 8);
+            __builtin_amdgcn_raw_buffer_store_b64(gv, ws, (b * (H / 2) + (eunit >> 1)) * 8, 0, kPlain);
+          }
+          TSTAMP(4);
+          // ---- outputs
+          if (b < B && !((knobs >> 8) & 1)) {
+            const size_t bt = (size_t)(b0 + b) * S + t;
+            hs[bt * H + eunit] = dca::f2bf(hv);
+            if (hsf) hsf[bt * H + eunit] = hv;
+            cs[bt * H + eunit] = c;
+            *reinterpret_cast<dca::f32x4*>(gates4 + (bt * H + eunit) * 4) = dca::f32x4{ig, fg, gg, og};
+          }
+          TSTAMP(5);
+        }
+      }
+    }
+#undef TSTAMP
+    if (sh_int == -2) return;
+    if (mfma_wave) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const int b = mt * 16 + erow;
+        if (b < B) {
+          hn[(size_t)(b0 + b) * H + eunit] = hreg[mt];
+          cn[(size_t)(b0 + b) * H + eunit] = creg[mt];
+        }
+      }
+    }
+    __syncthreads();
+    if (tid == 0) add_agent(&ctl->done[team], 1u);
+  }
+}
+
+// =============================================================================================================
+// Backward. xb (per team): [2 parity][kT consumers][Bc][NQ quads][kT producers] 16-B chunks
+// {bf16 u0,u1 | tag | bf16 u2,u3 | tag}, NQ = U/4.
+// =============================================================================================================
+template <int MT, int KS>
+__global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
+    const float* __restrict__ dhs, const float* __restrict__ gates4, const float* __restrict__ cs,
+    const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
+    const short* __restrict__ whh, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
+    i32x4* xb_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S) {
+  constexpr int H = 128 * KS;
+  constexpr int U = H / kT;             // 4·KS units per workgroup
+  constexpr int NQ = U / 4;             // unit quads per (consumer, row)
+  constexpr int G = 4 * U;              // gate columns per workgroup (MFMA K)
+  constexpr int KSTEP = (G + 31) / 32;  // K padded to a multiple of 32
+  constexpr int TPW = (H / 16) / 4;     // output n-tiles per wave (2·KS)
+  constexpr int RB = MT * 16;
+  constexpr int NPAIR = (RB * U + kThreads - 1) / kThreads;
+  constexpr int SC = TPW * 16 + 8;      // staging pitch (bf16)
+  __shared__ short dgl[RB][KSTEP * 32 + 8];
+  __shared__ unsigned short stg[4][RB][SC];
+  __shared__ float dhrec[RB][U];
+  __shared__ int sh_int;
+
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int me = join_team(ctl, err, &sh_int);
+  if (me < 0) return;
+  const int team = me >> 6, m = me & 63;
+  const int j0 = m * U;
+  const size_t xb_team = (size_t)2 * kT * Bc * NQ * kT;
+  i32x4* xb = xb_all + (size_t)team * xb_team;
+
+  for (int i = tid; i < RB * (KSTEP * 32 + 8); i += kThreads) (&dgl[0][0])[i] = 0;
+
+  // W slice for this wave: B[k][n] = W[row(k)][n], k = gate column (unit-major u·4+q) of this workgroup,
+  // n ∈ this wave's TPW output tiles
+  const int col = lane & 15, kg = lane >> 4;
+  bf16x8 wf[TPW][KSTEP];
+#pragma unroll
+  for (int tt = 0; tt < TPW; ++tt) {
+    const int n = (wv * TPW + tt) * 16 + col;
+#pragma unroll
+    for (int ks = 0; ks < KSTEP; ++ks) {
+      bf16x8 v;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = ks * 32 + 8 * kg + j;
+        v[j] = (k < G) ? whh[(size_t)((k & 3) * H + j0 + (k >> 2)) * H + n] : (short)0;
+      }
+      wf[tt][ks] = v;
+    }
+  }
+
+  unsigned spins = 0;
+  for (unsigned iter = 0;; ++iter) {
+    const int chain = next_chain(ctl, team, m, iter, nch, &sh_int);
+    if (chain < 0) break;
+    const int b0 = chain * Bc;
+    const int B = min(Bc, Btot - b0);
+    const unsigned tagbase = (iter + 1) << 16;
+    float dcarry[NPAIR];
+#pragma unroll
+    for (int i = 0; i < NPAIR; ++i) {
+      const int pi = tid + kThreads * i;
+      const int b = pi / U, u = pi % U;
+      dcarry[i] = (pi < B * U && dcn) ? dcn[(size_t)(b0 + b) * H + j0 + u] : 0.f;
+    }
+    bool dead = false;
+    for (int k = 0; k <= S; ++k) {
+      const int t = S - 1 - k;          // step whose gate gradients are produced this iteration (-1: final)
+      // ---- prefetch the saved activations of step t for the owned pairs
+      dca::f32x4 gv[NPAIR];
+      float cv[NPAIR], cpv[NPAIR], dv[NPAIR];
+      if (t >= 0) {
+#pragma unroll
+        for (int i = 0; i < NPAIR; ++i) {
+          const int pi = tid + kThreads * i;
+          if (pi < B * U) {
+            const int b = pi / U, u = pi % U;
+            const size_t bt = (size_t)(b0 + b) * S + t;
+            gv[i] = *reinterpret_cast<const dca::f32x4*>(gates4 + (bt * H + j0 + u) * 4);
+            cv[i] = cs[bt * H + j0 + u];
+            cpv[i] = t > 0 ? cs[(bt - 1) * H + j0 + u] : c0[(size_t)(b0 + b) * H + j0 + u];
+            dv[i] = dhs[bt * H + j0 + u];
+          }
+        }
+      }
+      // ---- recurrent gradient Σ_p partial_p (of step t+1) for the owned units → dhrec
+      if (k == 0) {
+        for (int i = tid; i < B * U; i += kThreads) {
+          const int b = i / U, u = i % U;
+          dhrec[b][u] = dhn ? dhn[(size_t)(b0 + b) * H + j0 + u] : 0.f;
+        }
+      } else {
+        const unsigned tag = tagbase | (unsigned)(t + 2);
+        const __amdgpu_buffer_rsrc_t rs =
+            uniform_rsrc(xb + ((size_t)((t + 1) & 1) * kT + m) * Bc * NQ * kT, Bc * NQ * kT * 16);
+        constexpr int NL = (RB * NQ * kT + kThreads - 1) / kThreads;
+        i32x4 g[NL];
+        bool okc[NL];
+#pragma unroll
+        for (int i = 0; i < NL; ++i) okc[i] = tid + kThreads * i >= B * NQ * kT;
+        while (true) {
+#pragma unroll
+          for (int i = 0; i < NL; ++i)
+            if (!okc[i]) g[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + kThreads * i) * 16, 0, kSc1);
+          bool ok = true;
+#pragma unroll
+          for (int i = 0; i < NL; ++i) {
+            okc[i] = okc[i] || (((unsigned)g[i].y == tag) & ((unsigned)g[i].w == tag));
+            ok &= okc[i];
+          }
+          if (__all(ok)) break;
+          if (spin_fail(spins, ctl, err, 2u)) { dead = true; break; }
+        }
+#pragma unroll
+        for (int i = 0; i < NL; ++i) {
+          const int ci = tid + kThreads * i;
+          const bool valid = ci < B * NQ * kT;
+          const unsigned x = valid ? (unsigned)g[i].x : 0u, z = valid ? (unsigned)g[i].z : 0u;
+          float s0 = __uint_as_float(x << 16), s1 = __uint_as_float(x & 0xffff0000u);
+          float s2 = __uint_as_float(z << 16), s3 = __uint_as_float(z & 0xffff0000u);
+#pragma unroll
+          for (int o = 1; o < kT; o <<= 1) {           // producers are the 32 lowest lane bits' index
+            s0 += __shfl_xor(s0, o, 64);
+            s1 += __shfl_xor(s1, o, 64);
+            s2 += __shfl_xor(s2, o, 64);
+            s3 += __shfl_xor(s3, o, 64);
+          }
+          if (valid && (ci % kT) == 0) {
+            const int rest = ci / kT, quad = rest % NQ, b = rest / NQ;
+            dhrec[b][quad * 4 + 0] = s0;
+            dhrec[b][quad * 4 + 1] = s1;
+            dhrec[b][quad * 4 + 2] = s2;
+            dhrec[b][quad * 4 + 3] = s3;
+          }
+        }
+      }
+      if (dead) sh_int = -2;
+      lds_barrier();
+      if (sh_int == -2) break;
+      if (t < 0) {
+        for (int i = tid; i < B * U; i += kThreads) {
+          const int b = i / U, u = i % U;
+          dh0[(size_t)(b0 + b) * H + j0 + u] = dhrec[b][u];
+        }
+        break;
+      }
+      // ---- gate gradients for the owned (row, unit) pairs
+#pragma unroll
+      for (int i = 0; i < NPAIR; ++i) {
+        const int pi = tid + kThreads * i;
+        if (pi < B * U) {
+          const int b = pi / U, u = pi % U;
+          const float ig = gv[i][0], fg = gv[i][1], gg = gv[i][2], og = gv[i][3];
+          const float dht = dv[i] + dhrec[b][u];
+          const float tc = dca::tanhf_(cv[i]);
+          const float dc = dcarry[i] + dht * og * (1.f - tc * tc);
+          const float d_i = dc * gg * ig * (1.f - ig);
+          const float d_f = dc * cpv[i] * fg * (1.f - fg);
+          const float d_g = dc * ig * (1.f - gg * gg);
+          const float d_o = dht * tc * og * (1.f - og);
+          dcarry[i] = dc * fg;
+          dgl[b][u * 4 + 0] = dca::f2bf(d_i);
+          dgl[b][u * 4 + 1] = dca::f2bf(d_f);
+          dgl[b][u * 4 + 2] = dca::f2bf(d_g);
+          dgl[b][u * 4 + 3] = dca::f2bf(d_o);
+          const size_t bt = (size_t)(b0 + b) * S + t;
+          *reinterpret_cast<dca::f32x4*>(dgates4 + (bt * H + j0 + u) * 4) = dca::f32x4{d_i, d_f, d_g, d_o};
+          if (t == 0) dc0[(size_t)(b0 + b) * H + j0 + u] = dcarry[i];
+        }
+      }
+      lds_barrier();
+      // ---- partial dh_{t-1}[b, n] = Σ_k dG[b, k] · W[row(k), n] for this wave's n tiles → LDS (bf16)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        if (mt * 16 >= B) break;
+        bf16x8 a[KSTEP];
+#pragma unroll
+        for (int ks = 0; ks < KSTEP; ++ks) a[ks] = *reinterpret_cast<const bf16x8*>(&dgl[mt * 16 + col][ks * 32 + 8 * kg]);
+#pragma unroll
+        for (int tt = 0; tt < TPW; ++tt) {
+          dca::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < KSTEP; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], wf[tt][ks], acc, 0, 0, 0);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) stg[wv][mt * 16 + kg * 4 + r][tt * 16 + col] = (unsigned short)dca::f2bf(acc[r]);
+        }
+      }
+      // ---- publish: every lane stores whole 16-B chunks (one consumer quad of one row)
+      {
+        const __amdgpu_buffer_rsrc_t ws = uniform_rsrc(xb + (size_t)(t & 1) * kT * Bc * NQ * kT, kT * Bc * NQ * kT * 16);
+        const int tg = (int)(tagbase | (unsigned)(t + 1));
+        constexpr int QPR = TPW * 4;                    // quads per row in this wave's columns
+        for (int qi = lane; qi < B * QPR; qi += 64) {
+          const int b = qi / QPR, cq = qi % QPR;
+          const u32x2 v = *reinterpret_cast<const u32x2*>(&stg[wv][b][cq * 4]);
+          const int n = (wv * TPW) * 16 + cq * 4;       // first unit of the quad
+          const int cons = n / U, quad = (n % U) / 4;
+          const i32x4 cv = {(int)v.x, tg, (int)v.y, tg};
+          __builtin_amdgcn_raw_buffer_store_b128(cv, ws, (((cons * Bc + b) * NQ + quad) * kT + m) * 16, 0, kPlain);
+        }
+      }
+    }
+    if (sh_int == -2) return;
+    __syncthreads();
+    if (tid == 0) add_agent(&ctl->done[team], 1u);
+  }
+}
+
+// DCA_TEAM_KNOBS = pre_sleep | skip_outputs << 8 | probe_first << 9 (latency experiments only; default 0)
+inline int team_knobs() {
+  const char* e = getenv("DCA_TEAM_KNOBS");
+  return e ? atoi(e) : 0;
+}
+
+inline void plan(int B, int& nch, int& Bc, int& MT) {
+  // chains of ≤ 32 sequences; as many concurrent chains as teams (8), more chains queue behind them
+  nch = (B + 31) / 32;
+  if (nch < kMaxTeams && B > 16) {
+    // prefer more, smaller chains while teams are idle (≤ 16 rows keeps MT = 1)
+    const int n16 = (B + 15) / 16;
+    nch = n16 <= kMaxTeams ? n16 : nch;
+  }
+  Bc = (B + nch - 1) / nch;
+  MT = Bc <= 16 ? 1 : 2;
+}
+
+}  // namespace
+
+#define DCA_TEAM_DISPATCH(MT_, KS_, ...)                                            \
+  switch (((MT_) << 4) | (KS_)) {                                                  \
+    case 0x11: return __VA_ARGS__(1, 1); case 0x12: return __VA_ARGS__(1, 2);      \
+    case 0x14: return __VA_ARGS__(1, 4); case 0x21: return __VA_ARGS__(2, 1);      \
+    case 0x22: return __VA_ARGS__(2, 2); case 0x24: return __VA_ARGS__(2, 4);      \
+    default: return hipErrorInvalidValue;                                          \
+  }
+
+// Workspace bytes (control block + per-team exchange buffers) for a launch of (B, H).
+extern "C" size_t dca_lstm_team_workspace(int B, int H, int backward) {
+  int nch, Bc, MT;
+  plan(B, nch, Bc, MT);
+  const size_t ctl = 256;
+  if (!backward) return ctl + (size_t)kMaxTeams * 2 * Bc * (H / 2) * 8;
+  return ctl + (size_t)kMaxTeams * 2 * kT * Bc * ((H / kT) / 4) * kT * 16;
+}
+
+extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const short* whh, const float* h0, const float* c0,
+                                        short* hs, float* hsf, float* cs, float* gates4, float* hn, float* cn,
+                                        void* ws, size_t ws_bytes, unsigned* err, int B, int S, int H,
+                                        hipStream_t st, unsigned long long* trace) {
+  if (B < 1 || S < 1 || S >= 65535 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
+  if (ws_bytes < dca_lstm_team_workspace(B, H, 0)) return hipErrorInvalidValue;
+  int nch, Bc, MT;
+  plan(B, nch, Bc, MT);
+  hipError_t e = hipMemsetAsync(ws, 0, dca_lstm_team_workspace(B, H, 0), st);
+  if (e != hipSuccess) return e;
+  TeamCtl* ctl = reinterpret_cast<TeamCtl*>(ws);
+  unsigned long long* xg = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws) + 256);
+  const int KS = H / 128;
+#define DCA_F(mt, ks)                                                                                           \
+  (lstm_team_fwd_kernel<mt, ks><<<kMaxTeams * kT, kThreads, 0, st>>>(xp4, whh, h0, c0, hs, hsf, cs, gates4, hn, \
+                                                                      cn, xg, ctl, err, B, Bc, nch, S, trace, team_knobs()), \
+   hipGetLastError())
+  DCA_TEAM_DISPATCH(MT, KS, DCA_F)
+#undef DCA_F
+}
+
+extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, const float* cs, const float* c0,
+                                        const float* dhn, const float* dcn, const short* whh, float* dgates4,
+                                        float* dh0, float* dc0, void* ws, size_t ws_bytes, unsigned* err, int B,
+                                        int S, int H, hipStream_t st) {
+  if (B < 1 || S < 1 || S >= 65534 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
+  if (ws_bytes < dca_lstm_team_workspace(B, H, 1)) return hipErrorInvalidValue;
+  int nch, Bc, MT;
+  plan(B, nch, Bc, MT);
+  hipError_t e = hipMemsetAsync(ws, 0, dca_lstm_team_workspace(B, H, 1), st);
+  if (e != hipSuccess) return e;
+  TeamCtl* ctl = reinterpret_cast<TeamCtl*>(ws);
+  i32x4* xb = reinterpret_cast<i32x4*>(reinterpret_cast<char*>(ws) + 256);
+  const int KS = H / 128;
+#define DCA_B(mt, ks)                                                                                              \
+  (lstm_team_bwd_kernel<mt, ks><<<kMaxTeams * kT, kThreads, 0, st>>>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, \
+                                                                      dh0, dc0, xb, ctl, err, B, Bc, nch, S),      \
+   hipGetLastError())
+  DCA_TEAM_DISPATCH(MT, KS, DCA_B)
+#undef DCA_B
+}

@@ -8,12 +8,41 @@ PyTorch gate order i, f, g, o) returning ``(out (B,S,H) f32, h_n, c_n)``:
   and cell states for backward;
 * backward runs the reverse recurrence in one launch (``_C.lstm_bwd``) producing ∂L/∂gates for every step, then the
   weight gradients are plain GEMMs over all B·S rows: dW_ih = dGᵀx, dW_hh = dGᵀh_{t-1}, db = ΣdG, dx = dG·W_ih.
+
+Two kernel families implement the recurrence (``impl()``, env ``DCA_LSTM_IMPL``):
+
+* ``team`` (default, ops/csrc/lstm_team.hip): 32 workgroups of ONE XCD per sequence chain, exchanging the step
+  state through that XCD's L2; gates in unit-major (B,S,H,4) layout;
+* ``ring`` (ops/csrc/lstm.hip): 64+ workgroups across all XCDs, cross-fabric granule hand-off (fallback).
 """
 from __future__ import annotations
+
+import os
 
 import torch
 
 from . import require
+
+
+def impl() -> str:
+    v = os.environ.get('DCA_LSTM_IMPL', 'team')
+    if v not in ('team', 'ring'):
+        raise ValueError(f'DCA_LSTM_IMPL must be team or ring, got {v!r}')
+    return v
+
+
+def gate_perm(H: int, device) -> torch.Tensor:
+    """Row permutation gate-major (q·H + j) → unit-major (4·j + q): W[perm] puts a unit's 4 gates together."""
+    j = torch.arange(H, device=device)
+    return (torch.arange(4, device=device)[None, :] * H + j[:, None]).reshape(-1)
+
+
+def team_fwd(C, xp4, whh16, h0, c0, err, want_f32_h):
+    return C.lstm_team_fwd(xp4, whh16, h0.contiguous(), c0.contiguous(), err, want_f32_h)
+
+
+def team_bwd(C, dhs, gates4, cs, c0, dhn, dcn, whh16, err):
+    return C.lstm_team_bwd(dhs, gates4, cs, c0.contiguous(), dhn, dcn, whh16, err)
 
 
 
@@ -27,7 +56,16 @@ class _Recurrence(torch.autograd.Function):
     def forward(ctx, xp, w_hh, h0, c0, err):
         C = require()
         whh16 = w_hh.detach().to(torch.bfloat16).contiguous()
-        B = xp.shape[0]
+        B, S, G4 = xp.shape
+        H = G4 // 4
+        ctx.team = impl() == 'team'
+        ctx.err = err
+        if ctx.team:
+            xp4 = xp.view(B, S, 4, H).transpose(2, 3).contiguous()
+            hs16, hsf, cs, gates4, hn, cn = team_fwd(C, xp4, whh16, h0, c0, err, True)
+            ctx.save_for_backward(gates4, cs, c0, whh16, hs16, h0)
+            ctx.mark_non_differentiable(hs16)
+            return hsf, hn, cn, hs16
         MAX_B = C.lstm_max_batch(w_hh.shape[1])
         outs = []
         for s in range(0, B, MAX_B):
@@ -47,6 +85,14 @@ class _Recurrence(torch.autograd.Function):
         gates, cs, c0, whh16, hs16, h0 = ctx.saved_tensors
         B, S, H = cs.shape
         dhs = dhs.contiguous() if dhs is not None else torch.zeros_like(cs)
+        dhn = None if dhn is None else dhn.contiguous()
+        dcn = None if dcn is None else dcn.contiguous()
+        if ctx.team:
+            dg4, dh0, dc0 = team_bwd(C, dhs, gates, cs, c0, dhn, dcn, whh16, ctx.err)
+            dgates = dg4.permute(0, 1, 3, 2).reshape(B, S, 4 * H)
+            hprev = torch.cat([h0.to(torch.bfloat16).unsqueeze(1), hs16[:, :-1]], dim=1).reshape(B * S, H)
+            dw_hh = _mm_f32(dgates.reshape(B * S, 4 * H).t(), hprev)
+            return dgates, dw_hh, dh0, dc0, None
         MAX_B = C.lstm_max_batch(H)
         outs = []
         for s in range(0, B, MAX_B):

@@ -1,0 +1,51 @@
+#!/usr/bin/env python3
+"""In-kernel timestamps (s_memrealtime, 10 ns) of the XCD-team LSTM forward: per-step phase breakdown.
+Events per (member workgroup, wave, step): 0 step start, 1 h_{t-1} gathered, 2 after barrier, 3 gates/transposed,
+4 h_t published, 5 outputs stored."""
+import json
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, '.')
+from dotaclient_amd import ops  # noqa: E402
+
+med = (lambda a: float(np.median(a)))
+
+
+def fwd(B=8, H=512, S=200):
+    C = ops.require()
+    torch.manual_seed(0)
+    xp = torch.randn(B, S, H, 4, device='cuda') * 0.5
+    whh = (torch.randn(4 * H, H, device='cuda') * 0.05).to(torch.bfloat16)
+    h0 = torch.zeros(B, H, device='cuda')
+    err = torch.zeros(1, dtype=torch.int32, device='cuda')
+    tr = torch.zeros(32 * 4 * 64 * 8, dtype=torch.int64, device='cuda')
+    for _ in range(3):
+        tr.zero_()
+        C.lstm_team_fwd(xp, whh, h0, h0, err, False, tr)
+    torch.cuda.synchronize()
+    t = tr.view(32, 4, 64, 8).cpu().numpy().astype(np.float64) * 10.0
+    nt = H // 128
+    w = t[:, :nt, 8:60]                     # MFMA waves
+    o = {'kernel': 'team_fwd', 'B': B, 'H': H}
+    o['step_ns'] = med(np.diff(w[..., 0], axis=2))
+    o['gather_ns'] = med(w[..., 1] - w[..., 0])
+    o['barrier_ns'] = med(w[..., 2] - w[..., 1])
+    o['mfma_cell_ns'] = med(w[..., 3] - w[..., 2])
+    o['publish_ns'] = med(w[..., 4] - w[..., 3])
+    o['outputs_ns'] = med(w[..., 5] - w[..., 4])
+    last_pub = w[..., 4].max(axis=(0, 1))
+    o['publish_to_first_gather_ns'] = med(w[..., 1].min(axis=(0, 1))[1:] - last_pub[:-1])
+    o['publish_to_last_gather_ns'] = med(w[..., 1].max(axis=(0, 1))[1:] - last_pub[:-1])
+    first_pub = w[..., 4].min(axis=(0, 1))
+    o['publish_skew_ns'] = med(last_pub - first_pub)
+    o['err'] = int(err.item())
+    print(json.dumps(o), flush=True)
+
+
+if __name__ == '__main__':
+    fwd(8, 512)
+    fwd(8, 128)
+    fwd(32, 512)

@@ -9,8 +9,10 @@ def _rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
+@pytest.mark.parametrize('impl', ['team', 'ring'])
 @pytest.mark.parametrize('B,S,H', [(5, 37, 128), (8, 64, 512), (24, 20, 256), (40, 16, 512), (64, 8, 128), (100, 9, 512), (300, 5, 128)])
-def test_lstm_fwd_bwd_matches_torch(gpu_ops, B, S, H):
+def test_lstm_fwd_bwd_matches_torch(gpu_ops, monkeypatch, impl, B, S, H):
+    monkeypatch.setenv('DCA_LSTM_IMPL', impl)
     from dotaclient_amd.ops.lstm import lstm_sequence
     torch.manual_seed(B * 1000 + S)
     dev = 'cuda'
@@ -40,8 +42,10 @@ def test_lstm_fwd_bwd_matches_torch(gpu_ops, B, S, H):
         assert _rel(a, b) < 3e-2, (name, _rel(a, b))
 
 
-def test_lstm_repeat_launch_consistent(gpu_ops):
-    """Ring re-initialisation: back-to-back launches on the same stream give identical results."""
+@pytest.mark.parametrize('impl', ['team', 'ring'])
+def test_lstm_repeat_launch_consistent(gpu_ops, monkeypatch, impl):
+    """Exchange-buffer re-initialisation: back-to-back launches on the same stream give identical results."""
+    monkeypatch.setenv('DCA_LSTM_IMPL', impl)
     from dotaclient_amd.ops.lstm import lstm_sequence
     torch.manual_seed(0)
     B, S, H = 8, 100, 512
@@ -55,3 +59,23 @@ def test_lstm_repeat_launch_consistent(gpu_ops):
     torch.cuda.synchronize()
     assert int(err.item()) == 0
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[1], outs[2])
+
+
+def test_team_many_chains_queue(gpu_ops, monkeypatch):
+    """More chains than XCD teams (B=600 → 19 chains of 32): teams pull chains from the queue; result == ring."""
+    from dotaclient_amd.ops.lstm import lstm_sequence
+    torch.manual_seed(1)
+    B, S, H, I = 600, 12, 128, 64
+    w_ih = torch.randn(4 * H, I, device='cuda') * 0.1
+    w_hh = torch.randn(4 * H, H, device='cuda') * 0.1
+    b = torch.randn(4 * H, device='cuda') * 0.1
+    x = torch.randn(B, S, I, device='cuda')
+    h0 = torch.randn(B, H, device='cuda') * 0.1
+    err = torch.zeros(1, dtype=torch.int32, device='cuda')
+    monkeypatch.setenv('DCA_LSTM_IMPL', 'team')
+    out_t = lstm_sequence(x, w_ih, w_hh, b, b, h0, h0, err)[0]
+    monkeypatch.setenv('DCA_LSTM_IMPL', 'ring')
+    out_r = lstm_sequence(x, w_ih, w_hh, b, b, h0, h0, err)[0]
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    assert _rel(out_t, out_r) < 1e-2
