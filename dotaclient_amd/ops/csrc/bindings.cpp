@@ -130,7 +130,8 @@ std::vector<torch::Tensor> lstm_team_fwd(torch::Tensor xp4, torch::Tensor whh, t
 
 std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4, torch::Tensor cs,
                                          torch::Tensor c0, c10::optional<torch::Tensor> dhn,
-                                         c10::optional<torch::Tensor> dcn, torch::Tensor whh, torch::Tensor err) {
+                                         c10::optional<torch::Tensor> dcn, torch::Tensor whh, torch::Tensor err,
+                                         c10::optional<torch::Tensor> trace) {
   CHECK_F32(dhs); CHECK_F32(gates4); CHECK_F32(cs); CHECK_F32(c0); CHECK_BF16(whh); CHECK_I32(err);
   const int B = dhs.size(0), S = dhs.size(1), H = dhs.size(2);
   TORCH_CHECK(gates4.dim() == 4 && gates4.size(0) == B && gates4.size(1) == S && gates4.size(2) == H &&
@@ -150,7 +151,8 @@ std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4
   auto ws = torch::empty({(int64_t)wsb}, f32.dtype(at::kByte));
   hip_check(dca_lstm_team_bwd(ptr<float>(dhs), ptr<float>(gates4), ptr<float>(cs), ptr<float>(c0), dhn_p, dcn_p,
                               ptr<short>(whh), ptr<float>(dgates4), ptr<float>(dh0), ptr<float>(dc0), ws.data_ptr(),
-                              wsb, ptr<unsigned>(err), B, S, H, cur_stream()),
+                              wsb, ptr<unsigned>(err), B, S, H, cur_stream(),
+                              (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr),
             "dca_lstm_team_bwd");
   return {dgates4, dh0, dc0};
 }
@@ -294,7 +296,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("trace") = py::none());
   m.def("lstm_team_bwd", &lstm_team_bwd, "XCD-team persistent LSTM backward (L2-local reduce-scatter)",
         py::arg("dhs"), py::arg("gates4"), py::arg("cs"), py::arg("c0"), py::arg("dhn"), py::arg("dcn"),
-        py::arg("whh"), py::arg("err"));
+        py::arg("whh"), py::arg("err"), py::arg("trace") = py::none());
   m.def("sample_actions", &sample_actions, "fused masked hierarchical Gumbel-max action sampling (actor)");
   m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)");
 }

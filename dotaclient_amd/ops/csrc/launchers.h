@@ -42,7 +42,7 @@ hipError_t dca_lstm_team_fwd(const float* xp4, const short* whh, const float* h0
 hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, const float* cs, const float* c0,
                              const float* dhn, const float* dcn, const short* whh, float* dgates4, float* dh0,
                              float* dc0, void* ws, size_t ws_bytes, unsigned* err, int B, int S, int H,
-                             hipStream_t st);
+                             hipStream_t st, unsigned long long* trace = nullptr);
 
 hipError_t dca_sample_actions(const float* z, int ldz, const short* emb, const long long* handles, int N, int U,
                               unsigned long long seed, const long long* ctr, int* idx, unsigned char* act,

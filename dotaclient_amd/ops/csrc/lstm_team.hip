@@ -184,7 +184,7 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
   const int team = me >> 6, m = me & 63;
   const int j0 = m * U;
 #define TSTAMP(ev)                                                                                        \
-  if (trace && lane == 0 && team == 0 && t < 64)                                                          \
+  if (trace && lane == 0 && chain == 0 && t < 64)                                                          \
     trace[(((size_t)m * 4 + wv) * 64 + t) * 8 + (ev)] = __builtin_amdgcn_s_memrealtime()
   unsigned long long* xg = xg_all + (size_t)team * 2 * Bc * (H / 2);
 
@@ -357,27 +357,29 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
 }
 
 // =============================================================================================================
-// Backward. xb (per team): [2 parity][kT consumers][Bc][NQ quads][kT producers] 16-B chunks
-// {bf16 u0,u1 | tag | bf16 u2,u3 | tag}, NQ = U/4.
+// Backward (all-gather of dG). Measured: what limits an in-XCD hand-off is the bytes WRITTEN per step (they also
+// leave the XCD), not the bytes read from L2 — a reduce-scatter of B×H partials per workgroup (512 KB per step per
+// team at B=8, H=512) took 2.7 µs per hand-off, so the backward gathers the B×4H gate gradients instead (32 KB
+// written per step) and every workgroup computes its own units' recurrent gradient over the full K = 4H:
+//   dh_{t}[b, J_m] = Σ_gc dG_{t+1}[b, gc] · W_hh[row(gc), J_m]      (gc = 4·j + q unit-major, row = q·H + j)
+// xg (per team): [2 parity][Bc][H] 16-B chunks {bf16 d_i,d_f | tag | bf16 d_g,d_o | tag} (one per (row, unit)).
+// Waves split K = 4H in quarters (W_hhᵀ slice of the owned units in VGPRs); partial tiles are summed via LDS.
 // =============================================================================================================
 template <int MT, int KS>
 __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
     const float* __restrict__ dhs, const float* __restrict__ gates4, const float* __restrict__ cs,
     const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
     const short* __restrict__ whh, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
-    i32x4* xb_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S) {
+    i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, unsigned long long* trace) {
   constexpr int H = 128 * KS;
-  constexpr int U = H / kT;             // 4·KS units per workgroup
-  constexpr int NQ = U / 4;             // unit quads per (consumer, row)
-  constexpr int G = 4 * U;              // gate columns per workgroup (MFMA K)
-  constexpr int KSTEP = (G + 31) / 32;  // K padded to a multiple of 32
-  constexpr int TPW = (H / 16) / 4;     // output n-tiles per wave (2·KS)
+  constexpr int U = H / kT;             // 4·KS units per workgroup (MFMA N, zero-padded to 16)
+  constexpr int KW = H;                 // K (= 4H gate columns) per wave
+  constexpr int KSTEP = KW / 32;
   constexpr int RB = MT * 16;
+  constexpr int GP = 4 * H + 8;         // LDS pitch (bf16) of the gathered dG rows
   constexpr int NPAIR = (RB * U + kThreads - 1) / kThreads;
-  constexpr int SC = TPW * 16 + 8;      // staging pitch (bf16)
-  __shared__ short dgl[RB][KSTEP * 32 + 8];
-  __shared__ unsigned short stg[4][RB][SC];
-  __shared__ float dhrec[RB][U];
+  __shared__ short dgl[RB][GP];
+  __shared__ float red[4][RB][17];
   __shared__ int sh_int;
 
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
@@ -385,28 +387,25 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
   if (me < 0) return;
   const int team = me >> 6, m = me & 63;
   const int j0 = m * U;
-  const size_t xb_team = (size_t)2 * kT * Bc * NQ * kT;
-  i32x4* xb = xb_all + (size_t)team * xb_team;
+  i32x4* xg = xg_all + (size_t)team * 2 * Bc * H;
+#define TSTAMPB(ev)                                                                                       \
+  if (trace && lane == 0 && chain == 0 && k < 64)                                                         \
+    trace[(((size_t)m * 4 + wv) * 64 + k) * 8 + (ev)] = __builtin_amdgcn_s_memrealtime()
 
-  for (int i = tid; i < RB * (KSTEP * 32 + 8); i += kThreads) (&dgl[0][0])[i] = 0;
+  for (int i = tid; i < RB * GP; i += kThreads) (&dgl[0][0])[i] = 0;
 
-  // W slice for this wave: B[k][n] = W[row(k)][n], k = gate column (unit-major u·4+q) of this workgroup,
-  // n ∈ this wave's TPW output tiles
+  // B operand: lane holds Wᵀ[gc][u] for gc = wv·H + ks·32 + 8·kg + j, u = lane & 15 (zero for u ≥ U)
   const int col = lane & 15, kg = lane >> 4;
-  bf16x8 wf[TPW][KSTEP];
+  bf16x8 wf[KSTEP];
 #pragma unroll
-  for (int tt = 0; tt < TPW; ++tt) {
-    const int n = (wv * TPW + tt) * 16 + col;
+  for (int ks = 0; ks < KSTEP; ++ks) {
+    bf16x8 v;
 #pragma unroll
-    for (int ks = 0; ks < KSTEP; ++ks) {
-      bf16x8 v;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int k = ks * 32 + 8 * kg + j;
-        v[j] = (k < G) ? whh[(size_t)((k & 3) * H + j0 + (k >> 2)) * H + n] : (short)0;
-      }
-      wf[tt][ks] = v;
+    for (int j = 0; j < 8; ++j) {
+      const int gc = wv * KW + ks * 32 + 8 * kg + j;
+      v[j] = (col < U) ? whh[(size_t)((gc & 3) * H + (gc >> 2)) * H + j0 + col] : (short)0;
     }
+    wf[ks] = v;
   }
 
   unsigned spins = 0;
@@ -420,12 +419,12 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
 #pragma unroll
     for (int i = 0; i < NPAIR; ++i) {
       const int pi = tid + kThreads * i;
-      const int b = pi / U, u = pi % U;
-      dcarry[i] = (pi < B * U && dcn) ? dcn[(size_t)(b0 + b) * H + j0 + u] : 0.f;
+      dcarry[i] = (pi < B * U && dcn) ? dcn[(size_t)(b0 + pi / U) * H + j0 + pi % U] : 0.f;
     }
     bool dead = false;
     for (int k = 0; k <= S; ++k) {
       const int t = S - 1 - k;          // step whose gate gradients are produced this iteration (-1: final)
+      TSTAMPB(0);
       // ---- prefetch the saved activations of step t for the owned pairs
       dca::f32x4 gv[NPAIR];
       float cv[NPAIR], cpv[NPAIR], dv[NPAIR];
@@ -443,75 +442,82 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
           }
         }
       }
-      // ---- recurrent gradient Σ_p partial_p (of step t+1) for the owned units → dhrec
-      if (k == 0) {
-        for (int i = tid; i < B * U; i += kThreads) {
-          const int b = i / U, u = i % U;
-          dhrec[b][u] = dhn ? dhn[(size_t)(b0 + b) * H + j0 + u] : 0.f;
-        }
-      } else {
+      // ---- gather dG_{t+1} (B × 4H bf16) into LDS, all loads of a group of 8 rows in flight
+      if (k > 0) {
         const unsigned tag = tagbase | (unsigned)(t + 2);
-        const __amdgpu_buffer_rsrc_t rs =
-            uniform_rsrc(xb + ((size_t)((t + 1) & 1) * kT + m) * Bc * NQ * kT, Bc * NQ * kT * 16);
-        constexpr int NL = (RB * NQ * kT + kThreads - 1) / kThreads;
-        i32x4 g[NL];
-        bool okc[NL];
+        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(xg + (size_t)((t + 1) & 1) * Bc * H, Bc * H * 16);
+        constexpr int NL = 8 * H / kThreads;          // chunks per thread per group of 8 rows
+        for (int g0 = 0; g0 < B && !dead; g0 += 8) {
+          const int nck = min(8, B - g0) * H;
+          i32x4 g[NL];
+          bool okc[NL];
 #pragma unroll
-        for (int i = 0; i < NL; ++i) okc[i] = tid + kThreads * i >= B * NQ * kT;
-        while (true) {
+          for (int i = 0; i < NL; ++i) okc[i] = tid + kThreads * i >= nck;
+          while (true) {
 #pragma unroll
-          for (int i = 0; i < NL; ++i)
-            if (!okc[i]) g[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + kThreads * i) * 16, 0, kSc1);
-          bool ok = true;
+            for (int i = 0; i < NL; ++i)
+              if (!okc[i]) g[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (g0 * H + tid + kThreads * i) * 16, 0, kSc1);
+            bool ok = true;
+#pragma unroll
+            for (int i = 0; i < NL; ++i) {
+              okc[i] = okc[i] || (((unsigned)g[i].y == tag) & ((unsigned)g[i].w == tag));
+              ok &= okc[i];
+            }
+            if (__all(ok)) break;
+            if (spin_fail(spins, ctl, err, 2u)) { dead = true; break; }
+          }
 #pragma unroll
           for (int i = 0; i < NL; ++i) {
-            okc[i] = okc[i] || (((unsigned)g[i].y == tag) & ((unsigned)g[i].w == tag));
-            ok &= okc[i];
-          }
-          if (__all(ok)) break;
-          if (spin_fail(spins, ctl, err, 2u)) { dead = true; break; }
-        }
-#pragma unroll
-        for (int i = 0; i < NL; ++i) {
-          const int ci = tid + kThreads * i;
-          const bool valid = ci < B * NQ * kT;
-          const unsigned x = valid ? (unsigned)g[i].x : 0u, z = valid ? (unsigned)g[i].z : 0u;
-          float s0 = __uint_as_float(x << 16), s1 = __uint_as_float(x & 0xffff0000u);
-          float s2 = __uint_as_float(z << 16), s3 = __uint_as_float(z & 0xffff0000u);
-#pragma unroll
-          for (int o = 1; o < kT; o <<= 1) {           // producers are the 32 lowest lane bits' index
-            s0 += __shfl_xor(s0, o, 64);
-            s1 += __shfl_xor(s1, o, 64);
-            s2 += __shfl_xor(s2, o, 64);
-            s3 += __shfl_xor(s3, o, 64);
-          }
-          if (valid && (ci % kT) == 0) {
-            const int rest = ci / kT, quad = rest % NQ, b = rest / NQ;
-            dhrec[b][quad * 4 + 0] = s0;
-            dhrec[b][quad * 4 + 1] = s1;
-            dhrec[b][quad * 4 + 2] = s2;
-            dhrec[b][quad * 4 + 3] = s3;
+            const int ci = tid + kThreads * i;
+            if (ci < nck) {
+              const int b = g0 + ci / H, j = ci % H;
+              *reinterpret_cast<u32x2*>(&dgl[b][4 * j]) = u32x2{(unsigned)g[i].x, (unsigned)g[i].z};
+            }
           }
         }
       }
+      TSTAMPB(1);
       if (dead) sh_int = -2;
       lds_barrier();
       if (sh_int == -2) break;
+      TSTAMPB(2);
+      // ---- partial recurrent gradient over this wave's K quarter → red[wv]
+      if (k > 0) {
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          if (mt * 16 >= B) break;
+          dca::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int ks = 0; ks < KSTEP; ++ks) {
+            const bf16x8 a = *reinterpret_cast<const bf16x8*>(&dgl[mt * 16 + col][wv * KW + ks * 32 + 8 * kg]);
+            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[ks], acc, 0, 0, 0);
+          }
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[wv][mt * 16 + kg * 4 + r][col] = acc[r];
+        }
+      }
+      TSTAMPB(3);
+      lds_barrier();
+      TSTAMPB(4);
       if (t < 0) {
         for (int i = tid; i < B * U; i += kThreads) {
           const int b = i / U, u = i % U;
-          dh0[(size_t)(b0 + b) * H + j0 + u] = dhrec[b][u];
+          dh0[(size_t)(b0 + b) * H + j0 + u] = red[0][b][u] + red[1][b][u] + red[2][b][u] + red[3][b][u];
         }
         break;
       }
-      // ---- gate gradients for the owned (row, unit) pairs
+      // ---- gate gradients for the owned (row, unit) pairs; publish dG_t, write ∂gates
+      const __amdgpu_buffer_rsrc_t ws = uniform_rsrc(xg + (size_t)(t & 1) * Bc * H, Bc * H * 16);
+      const int tg = (int)(tagbase | (unsigned)(t + 1));
 #pragma unroll
       for (int i = 0; i < NPAIR; ++i) {
         const int pi = tid + kThreads * i;
         if (pi < B * U) {
           const int b = pi / U, u = pi % U;
+          const float rec = k == 0 ? (dhn ? dhn[(size_t)(b0 + b) * H + j0 + u] : 0.f)
+                                   : red[0][b][u] + red[1][b][u] + red[2][b][u] + red[3][b][u];
           const float ig = gv[i][0], fg = gv[i][1], gg = gv[i][2], og = gv[i][3];
-          const float dht = dv[i] + dhrec[b][u];
+          const float dht = dv[i] + rec;
           const float tc = dca::tanhf_(cv[i]);
           const float dc = dcarry[i] + dht * og * (1.f - tc * tc);
           const float d_i = dc * gg * ig * (1.f - ig);
@@ -519,51 +525,21 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
           const float d_g = dc * ig * (1.f - gg * gg);
           const float d_o = dht * tc * og * (1.f - og);
           dcarry[i] = dc * fg;
-          dgl[b][u * 4 + 0] = dca::f2bf(d_i);
-          dgl[b][u * 4 + 1] = dca::f2bf(d_f);
-          dgl[b][u * 4 + 2] = dca::f2bf(d_g);
-          dgl[b][u * 4 + 3] = dca::f2bf(d_o);
+          const unsigned p01 = (unsigned)(unsigned short)dca::f2bf(d_i) | ((unsigned)(unsigned short)dca::f2bf(d_f) << 16);
+          const unsigned p23 = (unsigned)(unsigned short)dca::f2bf(d_g) | ((unsigned)(unsigned short)dca::f2bf(d_o) << 16);
+          __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)p01, tg, (int)p23, tg}, ws, (b * H + j0 + u) * 16, 0, kPlain);
           const size_t bt = (size_t)(b0 + b) * S + t;
           *reinterpret_cast<dca::f32x4*>(dgates4 + (bt * H + j0 + u) * 4) = dca::f32x4{d_i, d_f, d_g, d_o};
           if (t == 0) dc0[(size_t)(b0 + b) * H + j0 + u] = dcarry[i];
         }
       }
-      lds_barrier();
-      // ---- partial dh_{t-1}[b, n] = Σ_k dG[b, k] · W[row(k), n] for this wave's n tiles → LDS (bf16)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        if (mt * 16 >= B) break;
-        bf16x8 a[KSTEP];
-#pragma unroll
-        for (int ks = 0; ks < KSTEP; ++ks) a[ks] = *reinterpret_cast<const bf16x8*>(&dgl[mt * 16 + col][ks * 32 + 8 * kg]);
-#pragma unroll
-        for (int tt = 0; tt < TPW; ++tt) {
-          dca::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-          for (int ks = 0; ks < KSTEP; ++ks) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[ks], wf[tt][ks], acc, 0, 0, 0);
-#pragma unroll
-          for (int r = 0; r < 4; ++r) stg[wv][mt * 16 + kg * 4 + r][tt * 16 + col] = (unsigned short)dca::f2bf(acc[r]);
-        }
-      }
-      // ---- publish: every lane stores whole 16-B chunks (one consumer quad of one row)
-      {
-        const __amdgpu_buffer_rsrc_t ws = uniform_rsrc(xb + (size_t)(t & 1) * kT * Bc * NQ * kT, kT * Bc * NQ * kT * 16);
-        const int tg = (int)(tagbase | (unsigned)(t + 1));
-        constexpr int QPR = TPW * 4;                    // quads per row in this wave's columns
-        for (int qi = lane; qi < B * QPR; qi += 64) {
-          const int b = qi / QPR, cq = qi % QPR;
-          const u32x2 v = *reinterpret_cast<const u32x2*>(&stg[wv][b][cq * 4]);
-          const int n = (wv * TPW) * 16 + cq * 4;       // first unit of the quad
-          const int cons = n / U, quad = (n % U) / 4;
-          const i32x4 cv = {(int)v.x, tg, (int)v.y, tg};
-          __builtin_amdgcn_raw_buffer_store_b128(cv, ws, (((cons * Bc + b) * NQ + quad) * kT + m) * 16, 0, kPlain);
-        }
-      }
+      TSTAMPB(6);
     }
     if (sh_int == -2) return;
     __syncthreads();
     if (tid == 0) add_agent(&ctl->done[team], 1u);
   }
+#undef TSTAMPB
 }
 
 // DCA_TEAM_KNOBS = pre_sleep | skip_outputs << 8 | probe_first << 9 (latency experiments only; default 0)
@@ -600,7 +576,7 @@ extern "C" size_t dca_lstm_team_workspace(int B, int H, int backward) {
   plan(B, nch, Bc, MT);
   const size_t ctl = 256;
   if (!backward) return ctl + (size_t)kMaxTeams * 2 * Bc * (H / 2) * 8;
-  return ctl + (size_t)kMaxTeams * 2 * kT * Bc * ((H / kT) / 4) * kT * 16;
+  return ctl + (size_t)kMaxTeams * 2 * Bc * H * 16;
 }
 
 extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const short* whh, const float* h0, const float* c0,
@@ -627,7 +603,7 @@ extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const short* whh, cons
 extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, const float* cs, const float* c0,
                                         const float* dhn, const float* dcn, const short* whh, float* dgates4,
                                         float* dh0, float* dc0, void* ws, size_t ws_bytes, unsigned* err, int B,
-                                        int S, int H, hipStream_t st) {
+                                        int S, int H, hipStream_t st, unsigned long long* trace) {
   if (B < 1 || S < 1 || S >= 65534 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
   if (ws_bytes < dca_lstm_team_workspace(B, H, 1)) return hipErrorInvalidValue;
   int nch, Bc, MT;
@@ -639,7 +615,7 @@ extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, c
   const int KS = H / 128;
 #define DCA_B(mt, ks)                                                                                              \
   (lstm_team_bwd_kernel<mt, ks><<<kMaxTeams * kT, kThreads, 0, st>>>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, \
-                                                                      dh0, dc0, xb, ctl, err, B, Bc, nch, S),      \
+                                                                      dh0, dc0, xb, ctl, err, B, Bc, nch, S, trace), \
    hipGetLastError())
   DCA_TEAM_DISPATCH(MT, KS, DCA_B)
 #undef DCA_B

@@ -45,7 +45,42 @@ def fwd(B=8, H=512, S=200):
     print(json.dumps(o), flush=True)
 
 
-if __name__ == '__main__':
+if __name__ == '__main__' and 'bwd' not in sys.argv:
     fwd(8, 512)
     fwd(8, 128)
     fwd(32, 512)
+
+
+def bwd(B=8, H=512, S=200):
+    C = ops.require()
+    torch.manual_seed(0)
+    xp = torch.randn(B, S, H, 4, device='cuda') * 0.5
+    whh = (torch.randn(4 * H, H, device='cuda') * 0.05).to(torch.bfloat16)
+    h0 = torch.zeros(B, H, device='cuda')
+    err = torch.zeros(1, dtype=torch.int32, device='cuda')
+    out = C.lstm_team_fwd(xp, whh, h0, h0, err, False)
+    dh = torch.randn(B, S, H, device='cuda')
+    tr = torch.zeros(32 * 4 * 64 * 8, dtype=torch.int64, device='cuda')
+    for _ in range(3):
+        tr.zero_()
+        C.lstm_team_bwd(dh, out[3], out[2], h0, None, None, whh, err, tr)
+    torch.cuda.synchronize()
+    t = tr.view(32, 4, 64, 8).cpu().numpy().astype(np.float64) * 10.0
+    w = t[:, :, 8:60]
+    o = {'kernel': 'team_bwd', 'B': B, 'H': H}
+    o['step_ns'] = med(np.diff(w[..., 0], axis=2))
+    o['gather_ns'] = med(w[..., 1] - w[..., 0])
+    o['barrier1_ns'] = med(w[..., 2] - w[..., 1])
+    o['elementwise_ns'] = med(w[..., 3] - w[..., 2])
+    o['barrier2_ns'] = med(w[..., 4] - w[..., 3])
+    o['mfma_stage_ns'] = med(w[..., 5] - w[..., 4])
+    o['stores_ns'] = med(w[..., 6] - w[..., 5])
+    last_pub = w[..., 6].max(axis=(0, 1))
+    o['publish_to_first_gather_ns'] = med(w[..., 1].min(axis=(0, 1))[1:] - last_pub[:-1])
+    o['publish_to_last_gather_ns'] = med(w[..., 1].max(axis=(0, 1))[1:] - last_pub[:-1])
+    o['err'] = int(err.item())
+    print(json.dumps(o), flush=True)
+
+
+if __name__ == '__main__' and 'bwd' in sys.argv:
+    bwd(8, 512)
