@@ -131,6 +131,7 @@ class _GameSlot:
         self.prev_obs = {}
         self.done = False
         self.end_state = None
+        self.opponent_version = None  # snapshot version the non-latest team played (league games)
         self.dota_time = -float('inf')
         self.drawing = Drawing()
         self.n_steps = 0
@@ -149,7 +150,7 @@ class Actor:
                  config_fn: Callable, rollout_size: int = 10 ** 9, max_dota_time: float = 600.0,
                  latest_weights_prob: float = 1.0, validation: bool = False, layout: UnitLayout = LAYOUT_1V1,
                  hidden_size: Optional[int] = None, hidden_stride: int = 0, wire: str = 'dcx1',
-                 metrics=None, rng: Optional[random.Random] = None):
+                 metrics=None, rng: Optional[random.Random] = None, league=None):
         self.services = list(services)
         self.weight_store = weight_store
         self.runner_for = runner_for
@@ -165,6 +166,7 @@ class Actor:
         self.wire = wire
         self.metrics = metrics
         self.rng = rng or random.Random()
+        self.league = league          # actor/league.py; None = the reference's oldest-snapshot opponent
         self.slots: List[Optional[_GameSlot]] = [None] * len(self.services)
         self.games_finished = 0
         self.steps_taken = 0
@@ -190,7 +192,13 @@ class Actor:
                     policy = self.weight_store.policy_for(self.weight_store.latest_weights())
                 else:
                     if old_policy is None:
-                        old_policy = self.weight_store.policy_for(self.weight_store.oldest_weights())
+                        if self.league is not None:
+                            vs = self.league.sample()
+                            old_policy = self.league.policy(vs)
+                        else:
+                            vs = self.weight_store.oldest_weights()
+                            old_policy = self.weight_store.policy_for(vs)
+                        slot.opponent_version = int(vs[0])
                     policy = old_policy
                 slot.players[p_res.team_id].append(Player(
                     game_id, p_res.id, p_res.team_id, p_res.hero, policy, latest, slot.drawing, self.validation,
@@ -216,6 +224,12 @@ class Actor:
             player.pending = r     # published once the next step's value (bootstrap) is known
 
     def _finish(self, slot: _GameSlot):
+        if self.league is not None and slot.opponent_version is not None:
+            latest_team = next((t for t in (TEAM_RADIANT, TEAM_DIRE)
+                                if any(p.use_latest_weights for p in slot.players[t])), None)
+            if latest_team is not None:
+                won = {Status.RADIANT_WIN: TEAM_RADIANT, Status.DIRE_WIN: TEAM_DIRE}.get(slot.end_state)
+                self.league.record(slot.opponent_version, 0.5 if won is None else float(won == latest_team))
         for team in (TEAM_RADIANT, TEAM_DIRE):
             for p in slot.players[team]:
                 p.process_endstate(slot.end_state)

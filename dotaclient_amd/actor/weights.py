@@ -5,8 +5,8 @@
   mid-game, exactly like the reference's synced players (agent.py:293-297).
 * ``oldest_weights`` / ``latest_weights`` back the reference's mini-league: with probability
   ``1 − latest_weights_prob`` one team plays the oldest stored weights and does not roll out (agent.py:760-765).
-* ``sample_league`` extends that into a configurable league (BASELINE config 5): uniform over history, or
-  prioritised towards recent / winning snapshots (see ``actor/league.py``).
+* :class:`~dotaclient_amd.actor.league.League` extends that into a configurable league (BASELINE config 5):
+  uniform over history, recency-weighted, or prioritised fictitious self-play from recorded results.
 """
 from __future__ import annotations
 

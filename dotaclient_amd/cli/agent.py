@@ -46,6 +46,8 @@ def build_parser():
     ap.add_argument('--wire', type=str, default='dcx1', choices=['dcx1', 'pickle'])
     ap.add_argument('--seed', type=int, default=None)
     ap.add_argument('--hidden-stride', type=int, default=256, help='store LSTM state every N steps')
+    ap.add_argument('--league', type=str, default='oldest', choices=['oldest', 'uniform', 'recent', 'pfsp'],
+                    help='opponent sampling over the weight history when not playing the latest weights')
     return ap
 
 
@@ -94,12 +96,14 @@ def main(argv=None):
         return r
     metrics = MetricsWriter(args.log_dir) if (args.validation and args.log_dir) else None
     config_fn = (lambda: get_1v1_bot_vs_default_config(rng=rng)) if args.validation else get_1v1_selfplay_config
+    from ..actor.league import League
+    league = None if args.league == 'oldest' else League(ws, mode=args.league, rng=rng)
     actor = Actor(make_services(args.env, args.games, seed), ws, runner_for,
                   None if args.validation else broker.publish_experience, config_fn,
                   rollout_size=args.rollout_size, max_dota_time=args.max_dota_time,
                   latest_weights_prob=args.use_latest_weights_prob, validation=args.validation, layout=cfg.layout,
                   hidden_size=cfg.hidden if cfg.rnn == 'lstm' else None, hidden_stride=args.hidden_stride,
-                  wire=args.wire, metrics=metrics, rng=rng)
+                  wire=args.wire, metrics=metrics, rng=rng, league=league)
     t0 = time.time()
     last = 0
     try:
