@@ -1,0 +1,42 @@
+"""bench.py contract on the multi-process path (gloo on CPU, world_size 2): one JSON line from rank 0 with the
+whole-job aggregate, weak-scaling fields and the BASELINE metric name."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize('world', [1, 2])
+def test_bench_json_contract_cpu(world):
+    env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS='2', CUDA_VISIBLE_DEVICES='', HIP_VISIBLE_DEVICES='')
+    args = ['bench.py', '--gpus', str(world), '--steps', '2', '--warmup', '1', '--batch-size', '2', '--seq-len', '16',
+            '--model', 'lstm128', '--actor', '0']
+    if world > 1:
+        cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={world}',
+               '--master-addr', '127.0.0.1', '--master-port', str(_port())] + args
+    else:
+        cmd = [sys.executable] + args
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, out.stdout
+    r = json.loads(lines[0])
+    assert r['metric'] == 'PPO optimizer samples/sec (whole node) + actor steps/sec, 1v1-mid LSTM policy'
+    assert r['n_gpus'] == world and r['steps'] == 2 and r['warmup'] == 1 and r['scaling'] == 'weak'
+    assert r['higher_is_better'] is True and r['config']['parallelism'] == f'dp{world}'
+    assert r['config']['global_batch'] == 2 * world and r['config']['seq_len'] == 16
+    assert abs(r['value'] - 2 * world * 16 * 2 / (r['ms_per_step'] * 2 / 1e3)) / r['value'] < 1e-6
+    assert r['vs_baseline'] == pytest.approx(r['value'] / 1000.0)
