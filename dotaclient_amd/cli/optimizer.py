@@ -53,6 +53,9 @@ def build_parser():
     ap.add_argument('--max-grad-norm', type=float, default=0.5)
     ap.add_argument('--compat-value-bug', type=str2bool, default=False)
     ap.add_argument('--checkpoint-keep', type=int, default=0)
+    ap.add_argument('--replay-gb', type=float, default=0.0, help='on-HBM replay buffer budget in GB (0 = off)')
+    ap.add_argument('--replay-capacity', type=int, default=0, help='replay capacity in sequences (overrides GB)')
+    ap.add_argument('--replay-recent', type=int, default=0, help='sample from the newest N sequences (0 = all)')
     return ap
 
 
@@ -76,7 +79,8 @@ def main(argv=None):
                           iterations=args.iterations, algo=args.algo, model=args.model_preset, gamma=args.gamma,
                           gae_lambda=args.gae_lambda, clip_eps=args.clip_eps, max_grad_norm=args.max_grad_norm,
                           compat_value_bug=args.compat_value_bug, device=device, backend=args.backend,
-                          checkpoint_keep=args.checkpoint_keep)
+                          checkpoint_keep=args.checkpoint_keep, replay_gb=args.replay_gb,
+                          replay_capacity=args.replay_capacity, replay_recent=args.replay_recent)
     broker = make_broker(args.broker or f'tcp://{args.ip}:{args.port}')
     try:
         DotaOptimizer(cfg, broker).run()

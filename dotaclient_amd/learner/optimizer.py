@@ -72,6 +72,9 @@ class OptimizerConfig:
     histogram_freq: int = 128          # optimizer.py:214
     xp_timeout: Optional[float] = None
     seed: int = 7
+    replay_gb: float = 0.0             # on-HBM replay budget (GB); 0 with replay_capacity 0 = reference behaviour
+    replay_capacity: int = 0           # sequences (overrides replay_gb)
+    replay_recent: int = 0             # sample from the newest N sequences (0 = whole buffer)
 
 
 class Sequence:
@@ -134,6 +137,14 @@ class DotaOptimizer:
             t = torch.tensor([self.iteration_start], device=self.device if self.device.type == 'cuda' else 'cpu')
             torch.distributed.broadcast(t, 0)
             self.iteration_start = int(t.item())
+        self.replay = None
+        if cfg.replay_capacity or cfg.replay_gb:
+            from .replay import HbmReplay
+            hid = self.policy_cfg.hidden if self.policy.is_recurrent else None
+            cap = cfg.replay_capacity or HbmReplay.capacity_for_bytes(cfg.replay_gb * 1e9, cfg.seq_len,
+                                                                       self.policy_cfg.layout, hid)
+            self.replay = HbmReplay(cap, cfg.seq_len, self.policy_cfg.layout, hid, self.device, seed=cfg.seed)
+            logger.info('on-device replay: %d sequences, %.2f GB', cap, self.replay.nbytes / 1e9)
         self.time_last_step = time.time()
         if self.iteration_start == 1:
             self.upload_model(version=0)
@@ -242,7 +253,15 @@ class DotaOptimizer:
         self.timer.start('train')
         losses, metrics_acc = [], {}
         g = torch.Generator().manual_seed(cfg.seed * 1000003 + it)
-        for ep in range(cfg.epochs):
+        if self.replay is not None:
+            # fresh sequences go into the on-HBM ring; minibatches are sampled from it on-device
+            self.replay.add(data, version=it)
+            for _ in range(cfg.epochs * (n // cfg.batch_size)):
+                m = self.learner.train_step(self.replay.sample(cfg.batch_size, cfg.replay_recent or None))
+                losses.append(m['loss'])
+                for k, v in m.items():
+                    metrics_acc.setdefault(k, []).append(v)
+        for ep in range(cfg.epochs if self.replay is None else 0):
             perm = torch.randperm(n, generator=g)
             for b0 in range(0, n, cfg.batch_size):
                 idx = perm[b0:b0 + cfg.batch_size].to(self.device)
@@ -279,6 +298,8 @@ class DotaOptimizer:
         for k in ('approx_kl', 'clipfrac'):
             if k in mean:
                 metrics[k] = mean[k]
+        if self.replay is not None:
+            metrics['replay/size'] = float(len(self.replay))
         for team, v in self.running.mean.items():
             metrics[f'rewards/running_mean_{team}'] = v
         for team, v in self.running.std.items():

@@ -1,0 +1,118 @@
+"""On-HBM experience replay: a preallocated device ring buffer of training sequences.
+
+BASELINE.json config 5 asks for a replay buffer sized for the MI355X's 288 GB of HBM3E. The reference has no
+replay at all — every iteration trains on exactly the ``seq_per_epoch`` freshly consumed sequences, on the CPU
+(optimizer.py:433-483). :class:`HbmReplay` keeps every field the learner step reads as one preallocated tensor
+per field on the GPU (``(capacity, seq_len, …)``), so
+
+* ingest is one pinned host→device copy per field per iteration (``add``), written at the ring cursor;
+* a minibatch is an on-device ``index_select`` of ``B`` rows (``sample``) — no host round trip, no allocation;
+* capacity is chosen from a byte budget (``capacity_for_bytes``): one LSTM-512 1v1 sequence of 1400 steps is
+  ≈2.4 MB, so 200 GB holds ≈80k sequences (≈115 M timesteps).
+
+Sampling is uniform over the filled part, optionally restricted to the ``recent`` newest sequences (on-policy-ish
+PPO typically samples the newest window; off-policy correction is the PPO ratio against the stored ``logp_old``).
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+import torch
+
+from ..constants import UnitLayout
+
+_F32 = torch.float32
+
+
+def field_specs(S: int, layout: UnitLayout, hidden: Optional[int]):
+    U = layout.max_units
+    A = 21 + U
+    spec = {
+        'env': ((S, 3), _F32), 'units': ((S, U, 10), _F32), 'actions': ((S, A), torch.uint8),
+        'masks': ((S, A), torch.uint8), 'ret': ((S,), _F32), 'norm_ret': ((S,), _F32), 'adv': ((S,), _F32),
+        'logp_old': ((S,), _F32), 'valid': ((S,), _F32),
+    }
+    if hidden:
+        spec['h0'] = ((hidden,), _F32)
+        spec['c0'] = ((hidden,), _F32)
+    return spec
+
+
+def bytes_per_sequence(S: int, layout: UnitLayout, hidden: Optional[int]) -> int:
+    n = 0
+    for shape, dt in field_specs(S, layout, hidden).values():
+        k = 1
+        for d in shape:
+            k *= d
+        n += k * torch.tensor([], dtype=dt).element_size()
+    return n + 8     # version
+
+
+class HbmReplay:
+    def __init__(self, capacity: int, S: int, layout: UnitLayout, hidden: Optional[int], device, seed: int = 0):
+        if capacity < 1:
+            raise ValueError('replay capacity must be >= 1')
+        self.capacity = int(capacity)
+        self.S = S
+        self.device = torch.device(device)
+        self.specs = field_specs(S, layout, hidden)
+        self.data = {k: torch.zeros((self.capacity,) + shape, dtype=dt, device=self.device)
+                     for k, (shape, dt) in self.specs.items()}
+        self.version = torch.full((self.capacity,), -1, dtype=torch.long, device=self.device)
+        self.cursor = 0
+        self.size = 0
+        self.inserted = 0
+        self._g = torch.Generator(device=self.device).manual_seed(seed)
+
+    @staticmethod
+    def capacity_for_bytes(budget: float, S: int, layout: UnitLayout, hidden: Optional[int]) -> int:
+        return max(1, int(budget // bytes_per_sequence(S, layout, hidden)))
+
+    @property
+    def nbytes(self) -> int:
+        return sum(t.numel() * t.element_size() for t in self.data.values()) + self.version.numel() * 8
+
+    def __len__(self):
+        return self.size
+
+    # ------------------------------------------------------------------------------------------------
+    def add(self, batch: Dict[str, torch.Tensor], version: int = 0):
+        """Append ``n`` sequences (host or device tensors, leading dim n) at the ring cursor (wrapping)."""
+        n = int(next(iter(batch.values())).shape[0])
+        if n > self.capacity:
+            batch = {k: v[-self.capacity:] for k, v in batch.items()}
+            n = self.capacity
+        first = min(n, self.capacity - self.cursor)
+        spans = [(self.cursor, 0, first)]
+        if first < n:
+            spans.append((0, first, n - first))
+        for k, dst in self.data.items():
+            src = batch[k]
+            if src.device != self.device and self.device.type == 'cuda' and not src.is_pinned():
+                src = src.pin_memory()
+            for d0, s0, cnt in spans:
+                dst[d0:d0 + cnt].copy_(src[s0:s0 + cnt], non_blocking=True)
+        for d0, _, cnt in spans:
+            self.version[d0:d0 + cnt] = int(version)
+        self.cursor = (self.cursor + n) % self.capacity
+        self.size = min(self.capacity, self.size + n)
+        self.inserted += n
+        return n
+
+    def _window(self, recent: Optional[int]):
+        m = self.size if not recent else min(self.size, int(recent))
+        return m
+
+    def sample_indices(self, B: int, recent: Optional[int] = None) -> torch.Tensor:
+        if self.size == 0:
+            raise RuntimeError('replay is empty')
+        m = self._window(recent)
+        r = torch.randint(0, m, (B,), device=self.device, generator=self._g)
+        # newest-first window ending at the cursor: position (cursor - 1 - r) mod capacity
+        return (self.cursor - 1 - r) % self.capacity
+
+    def gather(self, idx: torch.Tensor) -> Dict[str, torch.Tensor]:
+        return {k: v.index_select(0, idx) for k, v in self.data.items()}
+
+    def sample(self, B: int, recent: Optional[int] = None) -> Dict[str, torch.Tensor]:
+        return self.gather(self.sample_indices(B, recent))

@@ -115,18 +115,18 @@ def make_batch(B: int, S: int, layout: UnitLayout, hidden: Optional[int], device
 
 
 class DeviceReplay:
-    """A pool of synthetic sequences resident in device memory; :meth:`sample` gathers a minibatch on-device
-    (the learner's on-HBM replay source for benchmarking)."""
+    """A pool of synthetic sequences resident in device memory (an :class:`~.replay.HbmReplay` filled with
+    :func:`make_batch` data); :meth:`sample` gathers a minibatch on-device — the bench's on-HBM replay source."""
 
     def __init__(self, n_seq: int, S: int, layout: UnitLayout, hidden: Optional[int], device, seed: int = 0,
                  chunk: int = 16):
-        parts = [make_batch(min(chunk, n_seq - i), S, layout, hidden, device=device, seed=seed + i)
-                 for i in range(0, n_seq, chunk)]
-        self.data = {k: torch.cat([p[k] for p in parts]) for k in parts[0]}
+        from .replay import HbmReplay
+        self.buf = HbmReplay(n_seq, S, layout, hidden, device, seed=seed)
+        for i in range(0, n_seq, chunk):
+            self.buf.add(make_batch(min(chunk, n_seq - i), S, layout, hidden, device=device, seed=seed + i))
+        self.data = self.buf.data
         self.n = n_seq
         self.device = torch.device(device)
-        self._g = torch.Generator(device=self.device).manual_seed(seed)
 
     def sample(self, B: int) -> Dict[str, torch.Tensor]:
-        idx = torch.randint(0, self.n, (B,), device=self.device, generator=self._g)
-        return {k: v.index_select(0, idx) for k, v in self.data.items()}
+        return self.buf.sample(B)

@@ -1,0 +1,85 @@
+"""On-HBM replay ring buffer (learner/replay.py): ring semantics, newest-window sampling, byte budgeting, and the
+optimizer training from it."""
+import pytest
+import torch
+
+from dotaclient_amd.constants import LAYOUT_1V1
+from dotaclient_amd.learner.replay import HbmReplay, bytes_per_sequence
+from dotaclient_amd.learner.synthetic import make_batch
+
+
+def _batch(n, S, seed, hidden=128):
+    b = make_batch(n, S, LAYOUT_1V1, hidden, device='cpu', seed=seed)
+    b['ret'] = torch.full((n, S), float(seed))        # tag rows by their batch seed
+    return b
+
+
+def test_ring_wraps_and_keeps_newest():
+    r = HbmReplay(5, 8, LAYOUT_1V1, 128, 'cpu')
+    for seed in range(3):                              # 3 adds of 2 → 6 rows into capacity 5
+        r.add(_batch(2, 8, seed), version=seed)
+    assert len(r) == 5 and r.inserted == 6 and r.cursor == 1
+    tags = r.data['ret'][:, 0].tolist()
+    assert sorted(tags) == [0.0, 1.0, 1.0, 2.0, 2.0]  # the oldest row was overwritten
+    assert r.version.tolist().count(2) == 2
+
+
+def test_recent_window_sampling_only_returns_newest():
+    r = HbmReplay(16, 4, LAYOUT_1V1, None, 'cpu', seed=1)
+    for seed in range(8):
+        r.add(_batch(2, 4, seed, hidden=None), version=seed)
+    s = r.sample(64, recent=2)
+    assert set(s['ret'][:, 0].tolist()) == {7.0}
+    s = r.sample(256)
+    assert set(s['ret'][:, 0].tolist()) == set(float(i) for i in range(8))
+    assert s['units'].shape == (256, 4, LAYOUT_1V1.max_units, 10) and s['actions'].dtype == torch.uint8
+
+
+def test_capacity_for_bytes_matches_allocation():
+    S, H = 1400, 512
+    per = bytes_per_sequence(S, LAYOUT_1V1, H)
+    assert 2.0e6 < per < 3.0e6                        # ≈2.4 MB per 1400-step LSTM-512 sequence
+    cap = HbmReplay.capacity_for_bytes(10 * per + 5, S, LAYOUT_1V1, H)
+    assert cap == 10
+    r = HbmReplay(3, 16, LAYOUT_1V1, 64, 'cpu')
+    assert r.nbytes == 3 * bytes_per_sequence(16, LAYOUT_1V1, 64)
+
+
+def test_optimizer_trains_from_replay(tmp_path):
+    import numpy as np
+    from dotaclient_amd.learner.optimizer import DotaOptimizer, OptimizerConfig
+    from dotaclient_amd.transport.broker import InProcBroker
+    from dotaclient_amd.transport.codec import Rollout, encode
+    br = InProcBroker()
+    cfg = OptimizerConfig(log_dir=str(tmp_path), model='lstm128', epochs=2, seq_per_epoch=4, batch_size=2,
+                          seq_len=16, device='cpu', replay_capacity=6, xp_timeout=30)
+    opt = DotaOptimizer(cfg, br)
+    rng = np.random.default_rng(0)
+    U, A = LAYOUT_1V1.max_units, 21 + LAYOUT_1V1.max_units
+    for i in range(8):
+        T = 16
+        act = np.zeros((T, A), np.uint8)
+        act[:, 0] = 1
+        msk = np.zeros((T, A), np.uint8)
+        msk[:, :3] = 1
+        br.publish_experience(encode(Rollout(
+            game_id=f'g{i}', team_id=2 + i % 2, player_id=0, weight_version=0, env=rng.standard_normal((T, 3)).astype(np.float32),
+            units=rng.standard_normal((T, U, 10)).astype(np.float32), actions=act, masks=msk,
+            rewards=rng.standard_normal((T, 9)), logp=np.full(T, -1.0, np.float32),
+            values=np.zeros(T, np.float32), done=True)))
+    opt.run(iterations=2)
+    assert len(opt.replay) == 6 and opt.replay.inserted == 8
+    assert np.isfinite(opt.last_metrics['loss/sum']) and opt.last_metrics['replay/size'] == 6.0
+
+
+@pytest.mark.gpu
+def test_replay_on_hbm_large(gpu_ops):
+    """A multi-GB on-device buffer: add/sample stay on the GPU and return the right rows."""
+    S, H = 1400, 512
+    cap = HbmReplay.capacity_for_bytes(8e9, S, LAYOUT_1V1, H)
+    r = HbmReplay(cap, S, LAYOUT_1V1, H, 'cuda')
+    assert r.nbytes > 7e9
+    b = {k: v.cuda() for k, v in _batch(4, S, 3, hidden=H).items()}
+    r.add(b, version=1)
+    s = r.sample(8)
+    assert s['units'].is_cuda and torch.equal(s['ret'][:, 0].cpu(), torch.full((8,), 3.0))
