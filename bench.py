@@ -113,6 +113,9 @@ def main():
         try:
             from dotaclient_amd.actor.batched import measure_actor_throughput
             actor = measure_actor_throughput(policy, device, n_games=args.actor_games)
+            f8 = measure_actor_throughput(policy, device, n_games=args.actor_games, fp8=True)
+            actor['fp8_gpu_steps_per_s'] = f8['gpu_steps_per_s']
+            actor['fp8_steps_per_s'] = f8['steps_per_s']
         except Exception as e:  # the learner metric stands on its own
             actor = {'error': repr(e)}
 

@@ -34,7 +34,7 @@ class GpuActorPolicy:
     """Fixed-slot batched policy step on one GPU (fully-fused policies: no entity attention)."""
 
     def __init__(self, policy: Policy, n_slots: int, device='cuda', seed: int = 0, use_graph: bool = True,
-                 record: bool = True):
+                 record: bool = True, fp8: bool = False):
         from .. import ops
         self.C = ops.require()
         cfg = policy.config
@@ -48,6 +48,7 @@ class GpuActorPolicy:
         self.seed = int(seed)
         self.use_graph = use_graph
         self.record = record
+        self.fp8 = fp8                   # e4m3 MFMA GEMMs (ops/fp8.py) for the pre-RNN, LSTM and heads projections
         self.policy = policy
         self._alloc()
         self.load_weights(policy)
@@ -109,17 +110,36 @@ class GpuActorPolicy:
         bh = torch.cat([g(f'{k}.bias') for k in heads] + [torch.zeros(LDZ - 150, device=dev)], 0)
         w['whT'] = wh.to(torch.bfloat16).t().contiguous()
         w['bh'] = bh.contiguous()
+        if self.fp8:
+            from ..ops import fp8 as F8
+            src = {'wpreT': g('affine_pre_rnn.weight'), 'whT': wh}
+            if self.cfg.rnn == 'lstm':
+                src['wihT'] = g('rnn.weight_ih_l0')
+                src['whhT'] = g('rnn.weight_hh_l0')
+            else:
+                src['wfT'] = g('fake_rnn.weight')
+            for k, v in src.items():
+                if hasattr(self, 'w') and isinstance(self.w.get(k), F8.Fp8Weight):
+                    self.w[k].load_(v)
+                    w[k] = self.w[k]
+                else:
+                    w[k] = F8.Fp8Weight(v)
         if not hasattr(self, 'w'):
             self.w = w
         else:
             for k, v in w.items():
-                self.w[k].copy_(v)
+                if isinstance(v, torch.Tensor):
+                    self.w[k].copy_(v)
 
     # ------------------------------------------------------------------------------------------------
     def _forward(self):
         """The captured body: reads d_* / h / c, writes idx/act/msk/logp/value and the new h / c."""
         C, w, cfg = self.C, self.w, self.cfg
-        mm = (lambda a, b: torch.mm(a, b, out_dtype=torch.float32))
+        if self.fp8:
+            from ..ops import fp8 as F8
+            mm = (lambda a, b: F8.linear(a, b))
+        else:
+            mm = (lambda a, b: torch.mm(a, b, out_dtype=torch.float32))
         self.h.mul_(self.d_keep)
         self.c.mul_(self.d_keep)
         self.h16.copy_(self.h)
@@ -242,7 +262,8 @@ def _synthetic_states(n_states: int, seed: int = 0):
 
 
 def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048, steps: int = 50,
-                             warmup: int = 5, featurize: bool = True, threads: int = 8) -> Dict[str, float]:
+                             warmup: int = 5, featurize: bool = True, threads: int = 8,
+                             fp8: bool = False) -> Dict[str, float]:
     """Actor steps/s (player-observations → sampled actions per second) of one GPU-resident batched actor.
 
     ``n_games`` 1v1 games = 2·n_games player slots stepped per launch. With ``featurize`` the host side decodes
@@ -253,7 +274,7 @@ def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048,
     n = 2 * n_games
     dev = torch.device(device)
     layout = policy.config.layout
-    gp = GpuActorPolicy(policy, n, device=dev, seed=1234, record=True)
+    gp = GpuActorPolicy(policy, n, device=dev, seed=1234, record=True, fp8=fp8)
     feat = None
     if featurize:
         from .. import native

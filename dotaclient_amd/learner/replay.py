@@ -88,7 +88,7 @@ class HbmReplay:
             spans.append((0, first, n - first))
         for k, dst in self.data.items():
             src = batch[k]
-            if src.device != self.device and self.device.type == 'cuda' and not src.is_pinned():
+            if src.device.type == 'cpu' and self.device.type == 'cuda' and not src.is_pinned():
                 src = src.pin_memory()
             for d0, s0, cnt in spans:
                 dst[d0:d0 + cnt].copy_(src[s0:s0 + cnt], non_blocking=True)
