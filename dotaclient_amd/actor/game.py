@@ -32,6 +32,7 @@ from ..features.featurizer import featurize, get_unit
 from ..features.reward import end_state_reward, get_reward, pack_rewards
 from ..protos import HeroControlMode, Status, TEAM_DIRE, TEAM_RADIANT, pb
 from ..transport.codec import Rollout, encode
+from ..utils.faults import faults
 from .drawing import Drawing
 
 logger = logging.getLogger(__name__)
@@ -210,6 +211,12 @@ class Actor:
         if self.publish is None or self.validation or not player.use_latest_weights:
             return
         body = encode(rollout) if self.wire == 'dcx1' else __import__('pickle').dumps(rollout.to_reference_dict())
+        f = faults()
+        if f.active:
+            if f.should('drop_xp'):
+                return
+            if f.should('corrupt_xp'):
+                body = f.corrupt(body)
         self.publish(body)
         self.rollouts_sent += 1
 
@@ -310,6 +317,8 @@ class Actor:
 
     def step(self):
         """One observation interval for every game (both teams), starting/finishing games as needed."""
+        if faults().should('actor_crash'):
+            raise RuntimeError('injected actor crash (DCA_FAULTS actor_crash)')
         for i in range(len(self.slots)):
             if self.slots[i] is None:
                 self._start_game(i)

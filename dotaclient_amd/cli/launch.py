@@ -38,6 +38,49 @@ def build_parser():
     return ap
 
 
+class Supervisor:
+    """Restart-on-exit process supervisor (the reference relies on k8s for this: agent pods are restarted when
+    agent.py returns, agent.py:896-900; the optimizer Job has ``restartPolicy: OnFailure``)."""
+
+    def __init__(self, specs, max_restarts: int = 5, env=None):
+        self.specs = dict(specs)
+        self.max_restarts = max_restarts
+        self.env = env
+        self.procs = {}
+        self.restarts = {k: 0 for k in self.specs}
+        self.failed = None
+
+    def start(self):
+        for k, cmd in self.specs.items():
+            self.procs[k] = subprocess.Popen(cmd, env=self.env)
+        return self
+
+    def poll(self) -> bool:
+        """Restart exited children; False once a child exhausted its restart budget."""
+        for k, p in list(self.procs.items()):
+            code = p.poll()
+            if code is None:
+                continue
+            if self.restarts[k] >= self.max_restarts:
+                logger.error('%s exited with %s; restart budget exhausted', k, code)
+                self.failed = (k, code)
+                return False
+            self.restarts[k] += 1
+            logger.warning('%s exited with %s; restarting (%d/%d)', k, code, self.restarts[k], self.max_restarts)
+            self.procs[k] = subprocess.Popen(self.specs[k], env=self.env)
+        return True
+
+    def stop(self, timeout: float = 20.0):
+        for p in self.procs.values():
+            if p.poll() is None:
+                p.terminate()
+        for p in self.procs.values():
+            try:
+                p.wait(timeout=timeout)
+            except subprocess.TimeoutExpired:
+                p.kill()
+
+
 def main(argv=None):
     args = build_parser().parse_args(argv)
     logging.basicConfig(format='%(asctime)s %(levelname)-8s %(message)s', level='INFO')
@@ -60,9 +103,7 @@ def main(argv=None):
     for i in range(args.validation):
         specs[f'val{i}'] = [py, '-m', 'dotaclient_amd.cli.agent', '--port', str(srv.port), '--validation', 'true',
                             '--log-dir', os.path.join(args.log_dir, 'val'), '--model-preset', args.model_preset]
-    procs, restarts = {}, {k: 0 for k in specs}
-    for k, cmd in specs.items():
-        procs[k] = subprocess.Popen(cmd)
+    sup = Supervisor(specs, args.max_restarts).start()
     stop = {'flag': False}
 
     def handler(*_):
@@ -75,28 +116,12 @@ def main(argv=None):
         while not stop['flag']:
             if args.duration and time.time() - t0 > args.duration:
                 break
-            for k, p in list(procs.items()):
-                code = p.poll()
-                if code is None:
-                    continue
-                if restarts[k] >= args.max_restarts:
-                    logger.error('%s exited with %s; restart budget exhausted', k, code)
-                    stop['flag'] = True
-                    rc = code or 1
-                    break
-                restarts[k] += 1
-                logger.warning('%s exited with %s; restarting (%d/%d)', k, code, restarts[k], args.max_restarts)
-                procs[k] = subprocess.Popen(specs[k])
+            if not sup.poll():
+                rc = sup.failed[1] or 1
+                break
             time.sleep(1.0)
     finally:
-        for p in procs.values():
-            if p.poll() is None:
-                p.terminate()
-        for p in procs.values():
-            try:
-                p.wait(timeout=20)
-            except subprocess.TimeoutExpired:
-                p.kill()
+        sup.stop()
         srv.stop()
     return rc
 

@@ -31,8 +31,9 @@ import torch
 from ..constants import EPS, OBSERVATIONS_PER_SECOND, REWARD_KEYS
 from ..models.policy import Policy, get_config
 from ..parallel import dist as pdist
-from ..transport.codec import Rollout, decode_any
+from ..transport.codec import CorruptMessage, Rollout, decode_any
 from ..utils import checkpoint as ckpt
+from ..utils.faults import faults
 from ..utils.metrics import MetricsWriter, StageTimer
 from .engine import Learner, LossConfig
 from .returns import RunningMeanStd, discount, gae
@@ -137,6 +138,7 @@ class DotaOptimizer:
             t = torch.tensor([self.iteration_start], device=self.device if self.device.type == 'cuda' else 'cpu')
             torch.distributed.broadcast(t, 0)
             self.iteration_start = int(t.item())
+        self.corrupt_rollouts = 0
         self.replay = None
         if cfg.replay_capacity or cfg.replay_gb:
             from .replay import HbmReplay
@@ -151,10 +153,15 @@ class DotaOptimizer:
 
     # ------------------------------------------------------------------------------------------------
     def get_rollout(self) -> Rollout:
-        body = self.broker.consume_experience(timeout=self.cfg.xp_timeout)
-        if body is None:
-            raise TimeoutError('no experience received')
-        return decode_any(body)
+        while True:
+            body = self.broker.consume_experience(timeout=self.cfg.xp_timeout)
+            if body is None:
+                raise TimeoutError('no experience received')
+            try:
+                return decode_any(body)
+            except CorruptMessage as e:       # drop it, like a lost message; the actors keep producing
+                self.corrupt_rollouts += 1
+                logger.warning('dropping corrupted experience message (%s); %d so far', e, self.corrupt_rollouts)
 
     def experiences_from_rollout(self, r: Rollout) -> List[Sequence]:
         S = self.cfg.seq_len
@@ -274,6 +281,8 @@ class DotaOptimizer:
             torch.cuda.synchronize(self.device)
         self.timer.stop('train')
         loss_t = torch.stack(losses).float().cpu()
+        if faults().nan_loss(it):
+            loss_t[0] = float('nan')
         if torch.isnan(loss_t).any():
             raise ValueError(f'NaN loss at iteration {it}: {loss_t.tolist()}')
         if self.learner.backend == 'fused':

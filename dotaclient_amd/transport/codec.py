@@ -14,8 +14,10 @@ The reference ships each rollout as ``pickle.dumps(dict)`` on the ``experience``
 
 Codecs:
 
-* :func:`encode` / :func:`decode` — a compact binary format (``DCX1`` magic, JSON header, raw little-endian arrays);
-  zero-copy ``np.frombuffer`` on decode. ~4× smaller/faster than pickling torch tensors.
+* :func:`encode` / :func:`decode` — a compact binary format (``DCX1`` magic, JSON header, raw little-endian arrays,
+  CRC-32 trailer over everything before it); zero-copy ``np.frombuffer`` on decode, and a corrupted or truncated
+  message raises :class:`CorruptMessage` instead of feeding garbage to the learner. ~4× smaller/faster than
+  pickling torch tensors.
 * :meth:`Rollout.to_reference_dict` / :meth:`Rollout.from_reference_dict` — exact reference message layout, so a
   reference agent's pickled message can be ingested and ours can be read by the reference optimizer.
   Only trusted in-cluster producers are unpickled (:func:`decode_any`), mirroring the reference's trust model.
@@ -26,6 +28,7 @@ import io
 import json
 import pickle
 import struct
+import zlib
 from dataclasses import dataclass, field
 from typing import Dict, Optional, Tuple
 
@@ -34,6 +37,10 @@ import numpy as np
 from ..constants import INPUT_KEYS, LAYOUT_1V1, N_MOVE_ENUMS, REWARD_KEYS, UNIT_KEYS, UnitLayout
 
 MAGIC = b'DCX1'
+
+
+class CorruptMessage(ValueError):
+    """A DCX1 message failed its CRC / framing checks."""
 
 
 @dataclass
@@ -119,12 +126,18 @@ def encode(r: Rollout) -> bytes:
         blobs.append(b)
         off += len(b)
     h = json.dumps(header, separators=(',', ':')).encode()
-    return b''.join([MAGIC, struct.pack('<I', len(h)), h] + blobs)
+    body = b''.join([MAGIC, struct.pack('<I', len(h)), h] + blobs)
+    return body + struct.pack('<I', zlib.crc32(body))
 
 
 def decode(buf: bytes) -> Rollout:
     if buf[:4] != MAGIC:
         raise ValueError('not a DCX1 experience message')
+    if len(buf) < 12:
+        raise CorruptMessage('truncated DCX1 message')
+    (crc,) = struct.unpack_from('<I', buf, len(buf) - 4)
+    if zlib.crc32(memoryview(buf)[:len(buf) - 4]) != crc:
+        raise CorruptMessage('DCX1 CRC mismatch (corrupted or truncated experience message)')
     (hl,) = struct.unpack_from('<I', buf, 4)
     header = json.loads(bytes(buf[8:8 + hl]))
     base = 8 + hl
