@@ -249,19 +249,22 @@ class FusedPolicy:
         self.params = [p for _, p in self.policy.named_parameters()]
 
     # ------------------------------------------------------------------------------------------------
-    def head_cat(self, P):
-        """Concatenate the five head Linear layers into one (LDZ, H) matrix: [q | enum | x | y | value | pad]."""
+    def head_cat(self, P, differentiable: bool = False):
+        """Concatenate the five head Linear layers into one (LDZ, H) matrix: [q | enum | x | y | value | pad].
+        ``differentiable`` keeps the autograd link to the parameters (per-stage path); the fully fused Function
+        computes the head gradients itself and uses detached copies."""
         H = self.cfg.hidden
         dev = P['affine_value.weight'].device
+        d = (lambda t: t) if differentiable else (lambda t: t.detach())
         with_value = self.loss_cfg is None or self.loss_cfg.vf_coef > 0
-        wv = P['affine_value.weight'].detach() if with_value else torch.zeros(1, H, device=dev)
-        bv = P['affine_value.bias'].detach() if with_value else torch.zeros(1, device=dev)
+        wv = d(P['affine_value.weight']) if with_value else torch.zeros(1, H, device=dev)
+        bv = d(P['affine_value.bias']) if with_value else torch.zeros(1, device=dev)
         pad = LDZ - 150
-        w = torch.cat([P['affine_unit_attention.weight'].detach(), P['affine_head_enum.weight'].detach(),
-                       P['affine_move_x.weight'].detach(), P['affine_move_y.weight'].detach(), wv,
+        w = torch.cat([d(P['affine_unit_attention.weight']), d(P['affine_head_enum.weight']),
+                       d(P['affine_move_x.weight']), d(P['affine_move_y.weight']), wv,
                        torch.zeros(pad, H, device=dev)], 0)
-        b = torch.cat([P['affine_unit_attention.bias'].detach(), P['affine_head_enum.bias'].detach(),
-                       P['affine_move_x.bias'].detach(), P['affine_move_y.bias'].detach(), bv,
+        b = torch.cat([d(P['affine_unit_attention.bias']), d(P['affine_head_enum.bias']),
+                       d(P['affine_move_x.bias']), d(P['affine_move_y.bias']), bv,
                        torch.zeros(pad, device=dev)], 0)
         return w, b
 
@@ -292,7 +295,7 @@ class FusedPolicy:
         nret = batch['norm_ret'].reshape(N).contiguous() if 'norm_ret' in batch else zeros
         if not self.fully_fused:
             xh, emb, _, _ = self.trunk(batch['env'], batch['units'], batch.get('h0'), batch.get('c0'))
-            w, b = self.head_cat(dict(zip(self.param_names, self.params)))
+            w, b = self.head_cat(dict(zip(self.param_names, self.params)), differentiable=True)
             U = emb.shape[2]
             return heads_loss(xh.reshape(N, -1), w, b, emb.reshape(N, U, -1), batch, cfg, S)[:2]
         H = self.cfg.hidden

@@ -16,7 +16,8 @@ def _rel(a, b):
 
 
 @pytest.mark.parametrize('preset,algo,B,S', [('lstm512', 'ppo', 4, 48), ('lstm128', 'ppo', 7, 33),
-                                             ('compat', 'vpg', 3, 40), ('lstm512', 'vpg', 2, 30)])
+                                             ('compat', 'vpg', 3, 40), ('lstm512', 'vpg', 2, 30),
+                                             ('5v5', 'ppo', 3, 24)])
 def test_fused_loss_and_grads_match_reference(gpu_ops, preset, algo, B, S):
     torch.manual_seed(0)
     cfg = get_config(preset)
