@@ -72,13 +72,27 @@ def main():
     if backend == 'auto':
         backend = 'fused' if use_cuda else 'torch'
     learner = Learner(policy, LossConfig(algo=args.algo), device=device, backend=backend)
+    if args.graph == 1 or (args.graph == -1 and backend == 'fused'):
+        learner.enable_graph(warmup=1)
     n_pool = args.replay or 4 * args.batch_size
     replay = DeviceReplay(n_pool, args.seq_len, cfg.layout, cfg.hidden if cfg.rnn == 'lstm' else None, device,
                           seed=1000 * rank)
 
+    trace = os.environ.get('DCA_BENCH_TRACE') == '1'
+
     def step():
         batch = replay.sample(args.batch_size)
-        return learner.train_step(batch)
+        t = time.perf_counter()
+        out = learner.train_step(batch)
+        if trace:
+            torch.cuda.synchronize()
+            print(f'[bench] step {learner.n_steps} {1e3 * (time.perf_counter() - t):.2f} ms loss '
+                  f'{float(out["loss"]):.5f} gnorm {float(out["grad_norm"]):.5f} '
+                  f'params_finite {bool(torch.isfinite(learner.flat.flat).all())} '
+                  f'grad_finite {bool(torch.isfinite(learner.flat.grad).all())} '
+                  f'err {int(learner.model.err.item()) if backend == "fused" else 0}',
+                  file=sys.stderr, flush=True)
+        return out
 
     for _ in range(args.warmup):
         m = step()
@@ -103,6 +117,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     final_loss = float(m['loss'])
+    if backend == 'fused':
+        learner.model.check_error()       # a persistent-kernel timeout would invalidate the measurement
 
     samples = args.batch_size * args.seq_len * world * args.steps
     value = samples / elapsed

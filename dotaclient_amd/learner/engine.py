@@ -61,6 +61,23 @@ class Learner:
             self.model = FusedPolicy(self.policy, loss_cfg)
         self.counts = self.policy.layout.action_counts()
         self.n_steps = 0
+        self.graph = None                 # captured forward+backward (see enable_graph)
+        self._graph_warmup = 0
+
+    def enable_graph(self, warmup: int = 2):
+        """Capture forward + loss + backward of the fused step in a hipGraph after ``warmup`` eager steps. The
+        step launches a few hundred kernels (per-chunk GEMMs, the persistent recurrence, fused kernels); eager
+        Python + hipBLASLt launch cost is several ms per step, a graph replay is one launch. The DP all-reduce and
+        the fused Adam stay outside the graph (RCCL collectives are not captured). Inputs are copied into
+        static buffers before each replay; the batch shapes must not change."""
+        if self.backend != 'fused' or self.device.type != 'cuda':
+            return False
+        # only the forward-computed step (models/pipelined.py) is captured: it has no work in an autograd
+        # backward thread (capturing _PolicyLoss's autograd backward gave wrong gradients on replay)
+        if not self.model.use_pipeline():
+            return False
+        self._graph_warmup = max(1, int(warmup))
+        return True
 
     # ------------------------------------------------------------------------------------------------
     def _autocast(self):
@@ -90,13 +107,45 @@ class Learner:
         return vpg_loss(logits, values, actions, masks, batch['norm_ret'], batch['ret'], cfg.entropy_coef,
                         cfg.vf_coef, compat_value_bug=cfg.compat_value_bug, stable=stable)
 
-    def train_step(self, batch: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
-        """One synchronous DP optimizer step. Returns device-resident metric tensors (no host sync)."""
+    def _fwd_bwd(self, batch):
         self.dp.zero_grad()
         loss, metrics = self.loss(batch)
         loss.backward()
+        if self.backend == 'fused' and getattr(self.model, 'direct_used', False):
+            # the fused Functions accumulate straight into the flat gradient buffer (no per-parameter autograd
+            # hooks fire); tell the DP layer which parameters received a gradient
+            self.dp.has_grad.copy_(self.model.grad_mask)
+        return {k: v.detach() for k, v in metrics.items()}
+
+    def _graphed_fwd_bwd(self, batch):
+        if self.graph is None:
+            self._static_in = {k: v.clone() for k, v in batch.items()}
+            # the capture stream must outlive the graph: hipBLASLt's per-stream workspace that the captured GEMM
+            # nodes point at belongs to it
+            s = self._graph_stream = torch.cuda.Stream(device=self.device)
+            s.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(s):          # one more eager run on the capture stream (allocator warm-up)
+                self._fwd_bwd(self._static_in)
+            torch.cuda.current_stream(self.device).wait_stream(s)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph, stream=s):
+                self._static_out = self._fwd_bwd(self._static_in)
+            self._graph_mask_used = getattr(self.model, 'direct_used', False)
+        for k, v in batch.items():
+            self._static_in[k].copy_(v, non_blocking=True)
+        self.dp.zero_grad()
+        self.graph.replay()
+        if self._graph_mask_used:
+            self.dp.has_grad.copy_(self.model.grad_mask)
+        return {k: v.clone() for k, v in self._static_out.items()}
+
+    def train_step(self, batch: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
+        """One synchronous DP optimizer step. Returns device-resident metric tensors (no host sync)."""
+        if self._graph_warmup and self.n_steps >= self._graph_warmup:
+            metrics = self._graphed_fwd_bwd(batch)
+        else:
+            metrics = self._fwd_bwd(batch)
         self.dp.sync()
-        metrics = {k: v.detach() for k, v in metrics.items()}
         metrics['grad_norm'] = self.opt.step(self.dp.counts)
         self.n_steps += 1
         return metrics

@@ -29,6 +29,7 @@ import torch.nn.functional as F
 from .policy import TYPE_SUFFIX, Policy
 
 from ..ops.lstm import impl as lstm_impl  # noqa: E402
+from ..ops.lstm import team_bwd, team_fwd  # noqa: E402
 
 LDZ = 160
 
@@ -95,7 +96,7 @@ class _PolicyLoss(torch.autograd.Function):
                 perm = fp.gate_perm(H, wih16.device)
                 wih16 = wih16[perm].contiguous()
                 xp4 = (_mm(x16, wih16.t()) + bias[perm]).view(B, S, H, 4)
-                hs16, _, cs, gates, _, _ = C.lstm_team_fwd(xp4, whh16, h0, c0, fp.err, False)
+                hs16, _, cs, gates, _, _ = team_fwd(C, xp4, whh16, h0, c0, fp.err, False)
             else:
                 perm = None
                 xp = (_mm(x16, wih16.t()) + bias).view(B, S, 4 * H)
@@ -151,7 +152,7 @@ class _PolicyLoss(torch.autograd.Function):
             dxh3 = dxh.view(B, S, H)
             perm = ctx.perm
             if perm is not None:
-                dgates = C.lstm_team_bwd(dxh3, gates, cs, c0, None, None, whh16, fp.err)[0].view(N, 4 * H)
+                dgates = team_bwd(C, dxh3, gates, cs, c0, None, None, whh16, fp.err)[0].view(N, 4 * H)
             else:
                 dg = []
                 mb = C.lstm_max_batch(H)
@@ -221,8 +222,8 @@ class _PolicyLoss(torch.autograd.Function):
         de = dx896[:, :128] * ((env2 @ we.t() + be) > 0)
         grads['affine_env.weight'] = de.t() @ env2
         grads['affine_env.bias'] = de.sum(0)
-        out = [grads.get(n) for n in fp.param_names]
-        return (None,) * 12 + tuple(out)
+        fp.apply_direct_grads([grads.get(n) for n in fp.param_names], None)
+        return (None,) * (12 + len(fp.param_names))
 
 
 class FusedPolicy:
@@ -237,6 +238,48 @@ class FusedPolicy:
         self.param_names: List[str] = [n for n, _ in policy.named_parameters()]
         self.params = [p for _, p in policy.named_parameters()]
         self.fully_fused = not self.cfg.entity_attention and self.cfg.unit_dim == 128 and self.cfg.env_dim == 128
+
+    def apply_direct_grads(self, grads, g):
+        """Accumulate precomputed gradients straight into the parameters' ``.grad`` (views of the learner's flat
+        buffer) with two multi-tensor kernels, instead of returning 30 tensors to autograd (which launches one
+        accumulation copy per parameter, ≈1 ms of host-bound launches per step). ``g`` = upstream gradient
+        (None = 1). Records which parameters received a gradient in ``grad_mask`` for the DP has-grad counts."""
+        gl, views, mask = [], [], []
+        for p, t in zip(self.params, grads):
+            mask.append(t is not None)
+            if t is None:
+                continue
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+            gl.append((t if t.dtype == torch.float32 else t.float()).contiguous())
+            views.append(p.grad)
+        # one launch with the tensor table in the kernel arguments — torch's foreach kernels stage their tensor
+        # lists through a host buffer, which a replayed hipGraph would read stale
+        self.C.multi_axpy(views, gl, None if g is None else g.reshape(1).float().contiguous())
+        if getattr(self, '_mask_list', None) != mask:
+            self._mask_list = mask
+            self.grad_mask = torch.tensor(mask, dtype=torch.float32, device=self.err.device)
+        self.direct_used = True
+
+    def side_stream(self):
+        if getattr(self, '_side', None) is None:
+            self._side = torch.cuda.Stream(device=self.err.device)
+        return self._side
+
+    def use_pipeline(self) -> bool:
+        """Time-chunked two-stream step (models/pipelined.py): team LSTM, fully fused LSTM policy, no compat value
+        bug (its value loss couples all rows of a sequence). ``DCA_PIPELINE=0`` disables it."""
+        import os
+        lc = self.loss_cfg
+        return (self.fully_fused and self.cfg.rnn == 'lstm' and lstm_impl() == 'team'
+                and not (lc is not None and lc.compat_value_bug) and os.environ.get('DCA_PIPELINE', '1') != '0')
+
+    @property
+    def chunks(self) -> int:
+        import os
+        # 1 = no time-chunk overlap: measured on MI355X, GEMMs running concurrently on the other XCDs slow the
+        # L2-bound team recurrence by more than they save (bench 10.25 / 10.6 / 11.0 ms at 1 / 2 / 4 chunks)
+        return int(os.environ.get('DCA_PIPELINE_CHUNKS', '1'))
 
     def gate_perm(self, H, device):
         key = (H, str(device))
@@ -281,6 +324,7 @@ class FusedPolicy:
     def loss(self, batch: Dict[str, torch.Tensor], cfg):
         from ..ops.heads import assemble_loss, batch_norms, heads_loss
         self.loss_cfg = cfg
+        self.direct_used = False
         B, S = batch['env'].shape[:2]
         N = B * S
         dev = batch['env'].device
@@ -305,8 +349,12 @@ class FusedPolicy:
             h0 = torch.zeros(B, H, device=dev)
             c0 = torch.zeros(B, H, device=dev)
         self.refresh()
-        part, logp = _PolicyLoss.apply(self, batch['units'].contiguous(), batch['env'].contiguous(), actions, masks,
-                                       adv, ret, lpo, nret, norms, h0.contiguous(), c0.contiguous(), *self.params)
+        fn = _PolicyLoss
+        if self.use_pipeline():
+            from .pipelined import PipelinedPolicyLoss
+            fn = PipelinedPolicyLoss
+        part, logp = fn.apply(self, batch['units'].contiguous(), batch['env'].contiguous(), actions, masks,
+                              adv, ret, lpo, nret, norms, h0.contiguous(), c0.contiguous(), *self.params)
         loss, metrics = assemble_loss(part, norms, cfg, ret, N, S)
         return loss, metrics
 

@@ -107,3 +107,50 @@ extern "C" hipError_t dca_adam_step(float* param, const float* grad, float* m, f
   DCA_CHECK_LAUNCH();
   return hipSuccess;
 }
+
+// ------------------------------------------------------------------------------------------------------------
+// Multi-tensor "dst_i += s · src_i" for up to kMaxAxpy tensors in ONE launch. The tensor table travels by value in
+// the kernel arguments (no host-side metadata buffer), so the launch is safe to capture in a hipGraph and replay
+// (the fused learner step adds its 30 precomputed parameter gradients into the flat gradient buffer with it).
+namespace {
+constexpr int kMaxAxpy = 64;
+struct AxpyTable {
+  float* dst[kMaxAxpy];
+  const float* src[kMaxAxpy];
+  long long start[kMaxAxpy + 1];   // prefix sum of element counts
+  int n;
+};
+
+__global__ __launch_bounds__(256) void multi_axpy_kernel(AxpyTable tab, const float* __restrict__ scale) {
+  const float s = scale ? *scale : 1.f;
+  const long long total = tab.start[tab.n];
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    int lo = 0, hi = tab.n - 1;                    // tensor containing element e (binary search, ≤ 6 steps)
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tab.start[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    const long long k = e - tab.start[lo];
+    tab.dst[lo][k] += s * tab.src[lo][k];
+  }
+}
+}  // namespace
+
+extern "C" hipError_t dca_multi_axpy(float* const* dst, const float* const* src, const long long* numel, int n,
+                                     const float* scale, hipStream_t st) {
+  if (n < 0 || n > kMaxAxpy) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  AxpyTable tab;
+  tab.n = n;
+  tab.start[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    tab.dst[i] = dst[i];
+    tab.src[i] = src[i];
+    tab.start[i + 1] = tab.start[i] + numel[i];
+  }
+  const long long total = tab.start[n];
+  int blocks = (int)((total + 255) / 256);
+  if (blocks > 2048) blocks = 2048;
+  multi_axpy_kernel<<<blocks, 256, 0, st>>>(tab, scale);
+  return hipGetLastError();
+}

@@ -46,6 +46,26 @@ void adam_step(torch::Tensor param, torch::Tensor grad, torch::Tensor m, torch::
             "dca_adam_step");
 }
 
+// dst_i += scale · src_i over a list of fp32 tensors in one graph-capturable launch (scale: 1-element device
+// tensor or None = 1).
+void multi_axpy(std::vector<torch::Tensor> dst, std::vector<torch::Tensor> src, c10::optional<torch::Tensor> scale) {
+  TORCH_CHECK(dst.size() == src.size(), "multi_axpy: list length mismatch");
+  TORCH_CHECK(dst.size() <= 64, "multi_axpy: at most 64 tensors");
+  std::vector<float*> d;
+  std::vector<const float*> s;
+  std::vector<long long> n;
+  for (size_t i = 0; i < dst.size(); ++i) {
+    CHECK_F32(dst[i]); CHECK_F32(src[i]);
+    TORCH_CHECK(dst[i].numel() == src[i].numel(), "multi_axpy: numel mismatch at ", i);
+    d.push_back(ptr<float>(dst[i]));
+    s.push_back(ptr<float>(src[i]));
+    n.push_back(dst[i].numel());
+  }
+  const float* sp = nullptr;
+  if (scale.has_value() && scale->defined()) { CHECK_F32((*scale)); sp = ptr<float>(*scale); }
+  hip_check(dca_multi_axpy(d.data(), s.data(), n.data(), (int)d.size(), sp, cur_stream()), "dca_multi_axpy");
+}
+
 // ------------------------------------------------------------------------------------------------------------
 // Persistent LSTM recurrence. xp (B,S,4H) f32, whh (4H,H) bf16, h0/c0 (B,H) f32, err (1) int32 device flag.
 std::vector<torch::Tensor> lstm_fwd(torch::Tensor xp, torch::Tensor whh, torch::Tensor h0, torch::Tensor c0,
@@ -101,28 +121,54 @@ std::vector<torch::Tensor> lstm_bwd(torch::Tensor dhs, torch::Tensor gates, torc
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// XCD-team LSTM recurrence (lstm_team.hip). Gates in unit-major (B,S,H,4) layout; see the kernel header.
+// XCD-team LSTM recurrence (lstm_team.hip). Gates in unit-major (·,·,H,4) layout; see the kernel header.
+// time_major=false: xp4 (B,S,H,4) and outputs (B,S,…); time_major=true: xp4 (S,B,H,4) and outputs (S,B,…) — a
+// time chunk [t0,t1) of a time-major tensor is then a contiguous slice, which the pipelined learner step uses.
+// Outputs may be passed in (e.g. slices of a whole-sequence tensor) to avoid copies.
+namespace {
+inline torch::Tensor out_or_new(const c10::optional<torch::Tensor>& o, at::IntArrayRef shape,
+                                const at::TensorOptions& opt, const char* name) {
+  if (o.has_value() && o->defined()) {
+    TORCH_CHECK(o->is_cuda() && o->is_contiguous() && o->sizes() == shape && o->scalar_type() == opt.dtype(),
+                name, ": preallocated output has the wrong shape/dtype/layout");
+    return *o;
+  }
+  return torch::empty(shape, opt);
+}
+}  // namespace
+
+inline void check_ctl(const torch::Tensor& ctl) {
+  CHECK_DEV(ctl); CHECK_CONTIG(ctl);
+  TORCH_CHECK(ctl.numel() * ctl.element_size() >= (int64_t)dca_lstm_team_ctl_bytes(),
+              "team control block too small (use ops.lstm.team_ctl())");
+}
+
 std::vector<torch::Tensor> lstm_team_fwd(torch::Tensor xp4, torch::Tensor whh, torch::Tensor h0, torch::Tensor c0,
-                                         torch::Tensor err, bool want_f32_h, c10::optional<torch::Tensor> trace) {
-  CHECK_F32(xp4); CHECK_BF16(whh); CHECK_F32(h0); CHECK_F32(c0); CHECK_I32(err);
-  TORCH_CHECK(xp4.dim() == 4 && xp4.size(3) == 4, "xp4 must be (B,S,H,4)");
-  const int B = xp4.size(0), S = xp4.size(1), H = xp4.size(2);
+                                         torch::Tensor err, torch::Tensor ctl, bool want_f32_h,
+                                         c10::optional<torch::Tensor> trace,
+                                         bool time_major, c10::optional<torch::Tensor> hs_out,
+                                         c10::optional<torch::Tensor> cs_out, c10::optional<torch::Tensor> gates_out) {
+  CHECK_F32(xp4); CHECK_BF16(whh); CHECK_F32(h0); CHECK_F32(c0); CHECK_I32(err); check_ctl(ctl);
+  TORCH_CHECK(xp4.dim() == 4 && xp4.size(3) == 4, "xp4 must be (B,S,H,4) or (S,B,H,4)");
+  const int B = time_major ? xp4.size(1) : xp4.size(0), S = time_major ? xp4.size(0) : xp4.size(1);
+  const int H = xp4.size(2);
   TORCH_CHECK(whh.size(0) == 4 * H && whh.size(1) == H, "whh must be (4H,H)");
   TORCH_CHECK(h0.size(0) == B && h0.size(1) == H && c0.size(0) == B && c0.size(1) == H, "h0/c0 must be (B,H)");
   TORCH_CHECK(H == 128 || H == 256 || H == 512, "lstm_team_fwd: H in {128,256,512}");
   auto f32 = xp4.options();
-  auto hs = torch::empty({B, S, H}, f32.dtype(at::kBFloat16));
-  torch::Tensor hsf = want_f32_h ? torch::empty({B, S, H}, f32) : torch::Tensor();
-  auto cs = torch::empty({B, S, H}, f32);
-  auto gates4 = torch::empty({B, S, H, 4}, f32);
+  const int64_t d0 = time_major ? S : B, d1 = time_major ? B : S;
+  auto hs = out_or_new(hs_out, {d0, d1, H}, f32.dtype(at::kBFloat16), "hs_out");
+  torch::Tensor hsf = want_f32_h ? torch::empty({d0, d1, H}, f32) : torch::Tensor();
+  auto cs = out_or_new(cs_out, {d0, d1, H}, f32, "cs_out");
+  auto gates4 = out_or_new(gates_out, {d0, d1, H, 4}, f32, "gates_out");
   auto hn = torch::empty({B, H}, f32);
   auto cn = torch::empty({B, H}, f32);
   const size_t wsb = dca_lstm_team_workspace(B, H, 0);
   auto ws = torch::empty({(int64_t)wsb}, f32.dtype(at::kByte));
   hip_check(dca_lstm_team_fwd(ptr<float>(xp4), ptr<short>(whh), ptr<float>(h0), ptr<float>(c0), ptr<short>(hs),
                               want_f32_h ? ptr<float>(hsf) : nullptr, ptr<float>(cs), ptr<float>(gates4),
-                              ptr<float>(hn), ptr<float>(cn), ws.data_ptr(), wsb, ptr<unsigned>(err), B, S, H,
-                              cur_stream(),
+                              ptr<float>(hn), ptr<float>(cn), ctl.data_ptr(), ws.data_ptr(), wsb,
+                              ptr<unsigned>(err), B, S, H, time_major ? 1 : 0, cur_stream(),
                               (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr),
             "dca_lstm_team_fwd");
   return {hs, want_f32_h ? hsf : hs, cs, gates4, hn, cn};
@@ -131,12 +177,16 @@ std::vector<torch::Tensor> lstm_team_fwd(torch::Tensor xp4, torch::Tensor whh, t
 std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4, torch::Tensor cs,
                                          torch::Tensor c0, c10::optional<torch::Tensor> dhn,
                                          c10::optional<torch::Tensor> dcn, torch::Tensor whh, torch::Tensor err,
-                                         c10::optional<torch::Tensor> trace) {
+                                         torch::Tensor ctl, c10::optional<torch::Tensor> trace, bool time_major,
+                                         c10::optional<torch::Tensor> dg_out) {
   CHECK_F32(dhs); CHECK_F32(gates4); CHECK_F32(cs); CHECK_F32(c0); CHECK_BF16(whh); CHECK_I32(err);
-  const int B = dhs.size(0), S = dhs.size(1), H = dhs.size(2);
-  TORCH_CHECK(gates4.dim() == 4 && gates4.size(0) == B && gates4.size(1) == S && gates4.size(2) == H &&
-                  gates4.size(3) == 4, "gates4 must be (B,S,H,4)");
-  TORCH_CHECK(cs.sizes() == dhs.sizes(), "cs must be (B,S,H)");
+  check_ctl(ctl);
+  const int B = time_major ? dhs.size(1) : dhs.size(0), S = time_major ? dhs.size(0) : dhs.size(1);
+  const int H = dhs.size(2);
+  TORCH_CHECK(gates4.dim() == 4 && gates4.size(0) == dhs.size(0) && gates4.size(1) == dhs.size(1) &&
+                  gates4.size(2) == H && gates4.size(3) == 4, "gates4 must match dhs with a trailing 4");
+  TORCH_CHECK(cs.sizes() == dhs.sizes(), "cs must match dhs");
+  TORCH_CHECK(c0.size(0) == B && c0.size(1) == H, "c0 must be (B,H)");
   TORCH_CHECK(whh.size(0) == 4 * H && whh.size(1) == H, "whh must be (4H,H)");
   TORCH_CHECK(H == 128 || H == 256 || H == 512, "lstm_team_bwd: H in {128,256,512}");
   const float* dhn_p = nullptr;
@@ -144,14 +194,14 @@ std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4
   if (dhn.has_value() && dhn->defined()) { CHECK_F32((*dhn)); dhn_p = ptr<float>(*dhn); }
   if (dcn.has_value() && dcn->defined()) { CHECK_F32((*dcn)); dcn_p = ptr<float>(*dcn); }
   auto f32 = dhs.options();
-  auto dgates4 = torch::empty({B, S, H, 4}, f32);
+  auto dgates4 = out_or_new(dg_out, {dhs.size(0), dhs.size(1), H, 4}, f32, "dg_out");
   auto dh0 = torch::empty({B, H}, f32);
   auto dc0 = torch::empty({B, H}, f32);
   const size_t wsb = dca_lstm_team_workspace(B, H, 1);
   auto ws = torch::empty({(int64_t)wsb}, f32.dtype(at::kByte));
   hip_check(dca_lstm_team_bwd(ptr<float>(dhs), ptr<float>(gates4), ptr<float>(cs), ptr<float>(c0), dhn_p, dcn_p,
-                              ptr<short>(whh), ptr<float>(dgates4), ptr<float>(dh0), ptr<float>(dc0), ws.data_ptr(),
-                              wsb, ptr<unsigned>(err), B, S, H, cur_stream(),
+                              ptr<short>(whh), ptr<float>(dgates4), ptr<float>(dh0), ptr<float>(dc0), ctl.data_ptr(),
+                              ws.data_ptr(), wsb, ptr<unsigned>(err), B, S, H, time_major ? 1 : 0, cur_stream(),
                               (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr),
             "dca_lstm_team_bwd");
   return {dgates4, dh0, dc0};
@@ -281,6 +331,9 @@ void lstm_cell(torch::Tensor gates, torch::Tensor h, torch::Tensor c, torch::Ten
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "dotaclient_amd gfx950 HIP kernels";
   m.def("adam_step", &adam_step, "fused global-norm clip + Adam over a flat fp32 buffer");
+  m.def("multi_axpy", &multi_axpy, "dst_i += scale * src_i for a list of fp32 tensors (one graph-safe launch)",
+        py::arg("dst"), py::arg("src"), py::arg("scale") = py::none());
+  m.def("lstm_team_ctl_bytes", &dca_lstm_team_ctl_bytes, "bytes of a persistent team-LSTM control block");
   m.def("lstm_max_batch", &dca_lstm_max_batch, "max sequences per persistent LSTM launch for hidden size H");
   m.def("lstm_fwd", &lstm_fwd, "persistent LSTM forward recurrence (granule all-gather)", py::arg("xp"),
         py::arg("whh"), py::arg("h0"), py::arg("c0"), py::arg("err"), py::arg("want_f32_h"),
@@ -291,12 +344,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_bwd", &lstm_bwd, "persistent LSTM backward recurrence (granule reduce-scatter)", py::arg("dhs"),
         py::arg("gates"), py::arg("cs"), py::arg("c0"), py::arg("dhn"), py::arg("dcn"), py::arg("whh"), py::arg("err"),
         py::arg("trace") = py::none());
-  m.def("lstm_team_fwd", &lstm_team_fwd, "XCD-team persistent LSTM forward (L2-local hand-off), (B,S,H,4) gates",
-        py::arg("xp4"), py::arg("whh"), py::arg("h0"), py::arg("c0"), py::arg("err"), py::arg("want_f32_h"),
-        py::arg("trace") = py::none());
+  m.def("lstm_team_fwd", &lstm_team_fwd, "XCD-team persistent LSTM forward (L2-local hand-off), unit-major gates",
+        py::arg("xp4"), py::arg("whh"), py::arg("h0"), py::arg("c0"), py::arg("err"), py::arg("ctl"),
+        py::arg("want_f32_h"), py::arg("trace") = py::none(), py::arg("time_major") = false, py::arg("hs_out") = py::none(),
+        py::arg("cs_out") = py::none(), py::arg("gates_out") = py::none());
   m.def("lstm_team_bwd", &lstm_team_bwd, "XCD-team persistent LSTM backward (L2-local reduce-scatter)",
         py::arg("dhs"), py::arg("gates4"), py::arg("cs"), py::arg("c0"), py::arg("dhn"), py::arg("dcn"),
-        py::arg("whh"), py::arg("err"), py::arg("trace") = py::none());
+        py::arg("whh"), py::arg("err"), py::arg("ctl"), py::arg("trace") = py::none(),
+        py::arg("time_major") = false, py::arg("dg_out") = py::none());
   m.def("sample_actions", &sample_actions, "fused masked hierarchical Gumbel-max action sampling (actor)");
   m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)");
 }

@@ -146,7 +146,7 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
           const float S = (float)P.S_bug, Bq = (float)P.B_bug;
           dV = P.vf_coef * 2.f * (S * V - P.norms[6]) / (Bq * S * S);
         } else {
-          dV = P.vf_coef * 2.f * (V - R) / (float)P.N;
+          dV = P.vf_coef * 2.f * (V - R) / ((float)P.S_bug * (float)P.B_bug);   // mean over ALL B·S rows (chunk-safe)
         }
       }
     }

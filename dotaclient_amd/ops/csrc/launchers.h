@@ -9,6 +9,9 @@ hipError_t dca_adam_step(float* param, const float* grad, float* m, float* v, co
                          const float* counts, float* steps, int n_params, float* partials, float* norm_out, float lr,
                          float b1, float b2, float eps, float max_norm, hipStream_t stream);
 
+hipError_t dca_multi_axpy(float* const* dst, const float* const* src, const long long* numel, int n,
+                          const float* scale, hipStream_t st);
+
 size_t dca_lstm_ring_elems(int B, int H, int backward);
 int dca_lstm_max_batch(int H);
 hipError_t dca_lstm_fwd(const float* xp, const short* whh, const float* h0, const float* c0, short* hs, float* hsf,
@@ -34,15 +37,16 @@ hipError_t dca_encoder_bwd(const float* units, const float* w1, const float* b1,
                            short* basic, float* dw1, float* db1, int N, int U, const int* counts, int compat,
                            hipStream_t st);
 
+size_t dca_lstm_team_ctl_bytes();
 size_t dca_lstm_team_workspace(int B, int H, int backward);
 hipError_t dca_lstm_team_fwd(const float* xp4, const short* whh, const float* h0, const float* c0, short* hs,
-                             float* hsf, float* cs, float* gates4, float* hn, float* cn, void* ws, size_t ws_bytes,
-                             unsigned* err, int B, int S, int H, hipStream_t st,
+                             float* hsf, float* cs, float* gates4, float* hn, float* cn, void* ctl, void* ws,
+                             size_t ws_bytes, unsigned* err, int B, int S, int H, int time_major, hipStream_t st,
                              unsigned long long* trace = nullptr);
 hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, const float* cs, const float* c0,
                              const float* dhn, const float* dcn, const short* whh, float* dgates4, float* dh0,
-                             float* dc0, void* ws, size_t ws_bytes, unsigned* err, int B, int S, int H,
-                             hipStream_t st, unsigned long long* trace = nullptr);
+                             float* dc0, void* ctl, void* ws, size_t ws_bytes, unsigned* err, int B, int S, int H,
+                             int time_major, hipStream_t st, unsigned long long* trace = nullptr);
 
 hipError_t dca_sample_actions(const float* z, int ldz, const short* emb, const long long* handles, int N, int U,
                               unsigned long long seed, const long long* ctr, int* idx, unsigned char* act,

@@ -44,14 +44,21 @@ constexpr int kSc1 = 16;                // buffer cache policy: sc1 (bypass the 
 constexpr int kPlain = 0;               // plain store: write-through L1, line stays in the XCD L2
 constexpr unsigned kSpinLimit = 1u << 22;
 
-struct TeamCtl {                         // zeroed before every launch
+// Persistent control block (one per stream, zero-initialised once, caller-owned). It is SELF-CLEANING: the last
+// workgroup of a launch to exit resets every field and bumps ``epoch``, so a launch never depends on a memset —
+// which also makes the kernels safe to replay from a hipGraph. ``epoch`` is folded into every hand-off tag, so
+// exchange buffers need no zeroing either: data left by an earlier launch can never match.
+struct TeamCtl {
   unsigned xcnt[16];                     // tickets per XCC
   unsigned state[kMaxTeams];             // 0 pending, 1 committed, 2 aborted
   unsigned chain[kMaxTeams];             // (announce iter << 16) | chain id
   unsigned done[kMaxTeams];              // members that finished their current chain
   unsigned next_chain;
   unsigned abort;
+  unsigned exits;                        // workgroups that have left the launch
+  unsigned epoch;                        // launches completed on this control block
 };
+static_assert(sizeof(TeamCtl) <= 256, "TeamCtl must fit the 256-byte control tensor");
 
 __device__ __forceinline__ unsigned xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xf; }
 __device__ __forceinline__ unsigned ld_acq(const unsigned* p) {
@@ -91,8 +98,9 @@ __device__ __forceinline__ bool spin_fail(unsigned& spins, TeamCtl* ctl, unsigne
 
 // Team formation + chain queue. Returns the team id (≥ 0) or -1 if this workgroup must exit. Called by all
 // threads; thread 0 does the global traffic, the result is broadcast through LDS.
-__device__ int join_team(TeamCtl* ctl, unsigned* err, int* sh) {
+__device__ int join_team(TeamCtl* ctl, unsigned* err, int* sh, unsigned* sh_epoch) {
   if (threadIdx.x == 0) {
+    *sh_epoch = ld_acq(&ctl->epoch);
     int res = -1;
     const unsigned x = xcc_id();
     if (x < kMaxTeams) {
@@ -158,16 +166,41 @@ __device__ int next_chain(TeamCtl* ctl, int team, int member, unsigned iter, int
   return *sh;
 }
 
+// Every workgroup calls this last (all threads). The last one to leave resets the control block for the next
+// launch on the same stream and advances the epoch.
+__device__ void team_exit(TeamCtl* ctl) {
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned e = add_agent(&ctl->exits, 1u);
+    if (e == gridDim.x - 1) {
+      for (int i = 0; i < 16; ++i) st_rel(&ctl->xcnt[i], 0u);
+      for (int i = 0; i < kMaxTeams; ++i) {
+        st_rel(&ctl->state[i], 0u);
+        st_rel(&ctl->chain[i], 0u);
+        st_rel(&ctl->done[i], 0u);
+      }
+      st_rel(&ctl->next_chain, 0u);
+      st_rel(&ctl->abort, 0u);
+      st_rel(&ctl->exits, 0u);
+      st_rel(&ctl->epoch, ld_acq(&ctl->epoch) + 1u);
+    }
+  }
+}
+
+__device__ __forceinline__ unsigned make_tagbase(unsigned epoch, unsigned iter) {
+  return ((epoch & 0x7ffu) << 21) | (((iter + 1u) & 0x1fu) << 16);   // | (t + 1): 16 bits
+}
+
 // =============================================================================================================
 // Forward. MT = 16-row batch tiles per chain (Bc ≤ 16·MT), KS = H/128.
 // xg (per team): [2 parity][Bc][H/2] u64 granules {lo: 2×bf16 h, hi: tag}
 // =============================================================================================================
 template <int MT, int KS>
-__global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
+__device__ __forceinline__ void lstm_team_fwd_body(
     const float* __restrict__ xp4, const short* __restrict__ whh, const float* __restrict__ h0,
     const float* __restrict__ c0, short* __restrict__ hs, float* __restrict__ hsf, float* __restrict__ cs,
     float* __restrict__ gates4, float* __restrict__ hn, float* __restrict__ cn, unsigned long long* xg_all,
-    TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, unsigned long long* trace,
+    TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st, unsigned long long* trace,
     int knobs) {
   constexpr int H = 128 * KS;
   constexpr int U = H / kT;             // units per workgroup (4·KS)
@@ -177,9 +210,11 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
   constexpr int RB = MT * 16;
   __shared__ short hl[2][RB][HP];
   __shared__ int sh_int;
+  __shared__ unsigned sh_epoch;
 
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-  const int me = join_team(ctl, err, &sh_int);
+  const int me = join_team(ctl, err, &sh_int, &sh_epoch);
+  const unsigned epoch = sh_epoch;
   if (me < 0) return;
   const int team = me >> 6, m = me & 63;
   const int j0 = m * U;
@@ -211,8 +246,7 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
     if (chain < 0) break;
     const int b0 = chain * Bc;
     const int B = min(Bc, Btot - b0);
-    const unsigned tagbase = (iter + 1) << 16;
-    const float* xpc = xp4 + (size_t)b0 * S * H * 4;
+    const unsigned tagbase = make_tagbase(epoch, iter);
     float creg[MT], hreg[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
@@ -230,7 +264,7 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const int b = mt * 16 + erow;
-          xv[mt] = (b < B) ? *reinterpret_cast<const dca::f32x4*>(xpc + (((size_t)b * S + t) * H + eunit) * 4)
+          xv[mt] = (b < B) ? *reinterpret_cast<const dca::f32x4*>(xp4 + (((size_t)(b0 + b) * sb + (size_t)t * st) * H + eunit) * 4)
                            : dca::f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
@@ -329,7 +363,7 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
           TSTAMP(4);
           // ---- outputs
           if (b < B && !((knobs >> 8) & 1)) {
-            const size_t bt = (size_t)(b0 + b) * S + t;
+            const size_t bt = (size_t)(b0 + b) * sb + (size_t)t * st;
             hs[bt * H + eunit] = dca::f2bf(hv);
             if (hsf) hsf[bt * H + eunit] = hv;
             cs[bt * H + eunit] = c;
@@ -366,11 +400,12 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
 // Waves split K = 4H in quarters (W_hhᵀ slice of the owned units in VGPRs); partial tiles are summed via LDS.
 // =============================================================================================================
 template <int MT, int KS>
-__global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
+__device__ __forceinline__ void lstm_team_bwd_body(
     const float* __restrict__ dhs, const float* __restrict__ gates4, const float* __restrict__ cs,
     const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
     const short* __restrict__ whh, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
-    i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, unsigned long long* trace) {
+    i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
+    unsigned long long* trace) {
   constexpr int H = 128 * KS;
   constexpr int U = H / kT;             // 4·KS units per workgroup (MFMA N, zero-padded to 16)
   constexpr int KW = H;                 // K (= 4H gate columns) per wave
@@ -381,9 +416,11 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
   __shared__ short dgl[RB][GP];
   __shared__ float red[4][RB][17];
   __shared__ int sh_int;
+  __shared__ unsigned sh_epoch;
 
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-  const int me = join_team(ctl, err, &sh_int);
+  const int me = join_team(ctl, err, &sh_int, &sh_epoch);
+  const unsigned epoch = sh_epoch;
   if (me < 0) return;
   const int team = me >> 6, m = me & 63;
   const int j0 = m * U;
@@ -414,7 +451,7 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
     if (chain < 0) break;
     const int b0 = chain * Bc;
     const int B = min(Bc, Btot - b0);
-    const unsigned tagbase = (iter + 1) << 16;
+    const unsigned tagbase = make_tagbase(epoch, iter);
     float dcarry[NPAIR];
 #pragma unroll
     for (int i = 0; i < NPAIR; ++i) {
@@ -434,10 +471,10 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
           const int pi = tid + kThreads * i;
           if (pi < B * U) {
             const int b = pi / U, u = pi % U;
-            const size_t bt = (size_t)(b0 + b) * S + t;
+            const size_t bt = (size_t)(b0 + b) * sb + (size_t)t * st;
             gv[i] = *reinterpret_cast<const dca::f32x4*>(gates4 + (bt * H + j0 + u) * 4);
             cv[i] = cs[bt * H + j0 + u];
-            cpv[i] = t > 0 ? cs[(bt - 1) * H + j0 + u] : c0[(size_t)(b0 + b) * H + j0 + u];
+            cpv[i] = t > 0 ? cs[(bt - st) * H + j0 + u] : c0[(size_t)(b0 + b) * H + j0 + u];
             dv[i] = dhs[bt * H + j0 + u];
           }
         }
@@ -528,7 +565,7 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
           const unsigned p01 = (unsigned)(unsigned short)dca::f2bf(d_i) | ((unsigned)(unsigned short)dca::f2bf(d_f) << 16);
           const unsigned p23 = (unsigned)(unsigned short)dca::f2bf(d_g) | ((unsigned)(unsigned short)dca::f2bf(d_o) << 16);
           __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)p01, tg, (int)p23, tg}, ws, (b * H + j0 + u) * 16, 0, kPlain);
-          const size_t bt = (size_t)(b0 + b) * S + t;
+          const size_t bt = (size_t)(b0 + b) * sb + (size_t)t * st;
           *reinterpret_cast<dca::f32x4*>(dgates4 + (bt * H + j0 + u) * 4) = dca::f32x4{d_i, d_f, d_g, d_o};
           if (t == 0) dc0[(size_t)(b0 + b) * H + j0 + u] = dcarry[i];
         }
@@ -540,6 +577,30 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
     if (tid == 0) add_agent(&ctl->done[team], 1u);
   }
 #undef TSTAMPB
+}
+
+template <int MT, int KS>
+__global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
+    const float* __restrict__ xp4, const short* __restrict__ whh, const float* __restrict__ h0,
+    const float* __restrict__ c0, short* __restrict__ hs, float* __restrict__ hsf, float* __restrict__ cs,
+    float* __restrict__ gates4, float* __restrict__ hn, float* __restrict__ cn, unsigned long long* xg_all,
+    TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st, unsigned long long* trace,
+    int knobs) {
+  lstm_team_fwd_body<MT, KS>(xp4, whh, h0, c0, hs, hsf, cs, gates4, hn, cn, xg_all, ctl, err, Btot, Bc, nch, S, sb,
+                             st, trace, knobs);
+  team_exit(ctl);
+}
+
+template <int MT, int KS>
+__global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
+    const float* __restrict__ dhs, const float* __restrict__ gates4, const float* __restrict__ cs,
+    const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
+    const short* __restrict__ whh, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
+    i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
+    unsigned long long* trace) {
+  lstm_team_bwd_body<MT, KS>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, dh0, dc0, xg_all, ctl, err, Btot, Bc, nch,
+                             S, sb, st, trace);
+  team_exit(ctl);
 }
 
 // DCA_TEAM_KNOBS = pre_sleep | skip_outputs << 8 | probe_first << 9 (latency experiments only; default 0)
@@ -571,30 +632,32 @@ inline void plan(int B, int& nch, int& Bc, int& MT) {
   }
 
 // Workspace bytes (control block + per-team exchange buffers) for a launch of (B, H).
+extern "C" size_t dca_lstm_team_ctl_bytes() { return 256; }
+
+// Exchange-buffer bytes (per-team hand-off rings) for a launch of (B, H). Not zeroed: tags carry the epoch.
 extern "C" size_t dca_lstm_team_workspace(int B, int H, int backward) {
   int nch, Bc, MT;
   plan(B, nch, Bc, MT);
-  const size_t ctl = 256;
-  if (!backward) return ctl + (size_t)kMaxTeams * 2 * Bc * (H / 2) * 8;
-  return ctl + (size_t)kMaxTeams * 2 * Bc * H * 16;
+  if (!backward) return (size_t)kMaxTeams * 2 * Bc * (H / 2) * 8;
+  return (size_t)kMaxTeams * 2 * Bc * H * 16;
 }
 
 extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const short* whh, const float* h0, const float* c0,
                                         short* hs, float* hsf, float* cs, float* gates4, float* hn, float* cn,
-                                        void* ws, size_t ws_bytes, unsigned* err, int B, int S, int H,
-                                        hipStream_t st, unsigned long long* trace) {
+                                        void* ctl_mem, void* ws, size_t ws_bytes, unsigned* err, int B, int S, int H,
+                                        int time_major, hipStream_t stream, unsigned long long* trace) {
   if (B < 1 || S < 1 || S >= 65535 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
-  if (ws_bytes < dca_lstm_team_workspace(B, H, 0)) return hipErrorInvalidValue;
+  if (ws_bytes < dca_lstm_team_workspace(B, H, 0) || ctl_mem == nullptr) return hipErrorInvalidValue;
   int nch, Bc, MT;
   plan(B, nch, Bc, MT);
-  hipError_t e = hipMemsetAsync(ws, 0, dca_lstm_team_workspace(B, H, 0), st);
-  if (e != hipSuccess) return e;
-  TeamCtl* ctl = reinterpret_cast<TeamCtl*>(ws);
-  unsigned long long* xg = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws) + 256);
+  const int sb = time_major ? 1 : S, st = time_major ? B : 1;   // row(b, t) = b·sb + t·st
+  TeamCtl* ctl = reinterpret_cast<TeamCtl*>(ctl_mem);
+  unsigned long long* xg = reinterpret_cast<unsigned long long*>(ws);
   const int KS = H / 128;
 #define DCA_F(mt, ks)                                                                                           \
-  (lstm_team_fwd_kernel<mt, ks><<<kMaxTeams * kT, kThreads, 0, st>>>(xp4, whh, h0, c0, hs, hsf, cs, gates4, hn, \
-                                                                      cn, xg, ctl, err, B, Bc, nch, S, trace, team_knobs()), \
+  (lstm_team_fwd_kernel<mt, ks><<<kMaxTeams * kT, kThreads, 0, stream>>>(xp4, whh, h0, c0, hs, hsf, cs, gates4, \
+                                                                          hn, cn, xg, ctl, err, B, Bc, nch, S, sb, \
+                                                                          st, trace, team_knobs()),                \
    hipGetLastError())
   DCA_TEAM_DISPATCH(MT, KS, DCA_F)
 #undef DCA_F
@@ -602,20 +665,21 @@ extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const short* whh, cons
 
 extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, const float* cs, const float* c0,
                                         const float* dhn, const float* dcn, const short* whh, float* dgates4,
-                                        float* dh0, float* dc0, void* ws, size_t ws_bytes, unsigned* err, int B,
-                                        int S, int H, hipStream_t st, unsigned long long* trace) {
+                                        float* dh0, float* dc0, void* ctl_mem, void* ws, size_t ws_bytes,
+                                        unsigned* err, int B, int S, int H, int time_major, hipStream_t stream,
+                                        unsigned long long* trace) {
   if (B < 1 || S < 1 || S >= 65534 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
-  if (ws_bytes < dca_lstm_team_workspace(B, H, 1)) return hipErrorInvalidValue;
+  if (ws_bytes < dca_lstm_team_workspace(B, H, 1) || ctl_mem == nullptr) return hipErrorInvalidValue;
   int nch, Bc, MT;
   plan(B, nch, Bc, MT);
-  hipError_t e = hipMemsetAsync(ws, 0, dca_lstm_team_workspace(B, H, 1), st);
-  if (e != hipSuccess) return e;
-  TeamCtl* ctl = reinterpret_cast<TeamCtl*>(ws);
-  i32x4* xb = reinterpret_cast<i32x4*>(reinterpret_cast<char*>(ws) + 256);
+  const int sb = time_major ? 1 : S, st = time_major ? B : 1;
+  TeamCtl* ctl = reinterpret_cast<TeamCtl*>(ctl_mem);
+  i32x4* xb = reinterpret_cast<i32x4*>(ws);
   const int KS = H / 128;
 #define DCA_B(mt, ks)                                                                                              \
-  (lstm_team_bwd_kernel<mt, ks><<<kMaxTeams * kT, kThreads, 0, st>>>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, \
-                                                                      dh0, dc0, xb, ctl, err, B, Bc, nch, S, trace), \
+  (lstm_team_bwd_kernel<mt, ks><<<kMaxTeams * kT, kThreads, 0, stream>>>(dhs, gates4, cs, c0, dhn, dcn, whh,      \
+                                                                          dgates4, dh0, dc0, xb, ctl, err, B, Bc,  \
+                                                                          nch, S, sb, st, trace),                  \
    hipGetLastError())
   DCA_TEAM_DISPATCH(MT, KS, DCA_B)
 #undef DCA_B

@@ -37,12 +37,31 @@ def gate_perm(H: int, device) -> torch.Tensor:
     return (torch.arange(4, device=device)[None, :] * H + j[:, None]).reshape(-1)
 
 
-def team_fwd(C, xp4, whh16, h0, c0, err, want_f32_h):
-    return C.lstm_team_fwd(xp4, whh16, h0.contiguous(), c0.contiguous(), err, want_f32_h)
+_CTL = {}
 
 
-def team_bwd(C, dhs, gates4, cs, c0, dhn, dcn, whh16, err):
-    return C.lstm_team_bwd(dhs, gates4, cs, c0.contiguous(), dhn, dcn, whh16, err)
+def team_ctl(device=None, stream=None) -> torch.Tensor:
+    """The persistent, self-cleaning control block for team-LSTM launches on (device, stream): zero-initialised
+    once; each launch leaves it clean for the next one and advances its epoch (lstm_team.hip ``TeamCtl``). Team
+    kernels on different streams must not share a block, kernels on one stream are serialised anyway."""
+    dev = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+    if dev.index is None:
+        dev = torch.device('cuda', torch.cuda.current_device())
+    s = stream if stream is not None else torch.cuda.current_stream(dev)
+    key = (dev.index, s.cuda_stream)
+    t = _CTL.get(key)
+    if t is None:
+        t = _CTL[key] = torch.zeros(64, dtype=torch.int32, device=dev)
+    return t
+
+
+def team_fwd(C, xp4, whh16, h0, c0, err, want_f32_h, **kw):
+    return C.lstm_team_fwd(xp4, whh16, h0.contiguous(), c0.contiguous(), err, team_ctl(xp4.device), want_f32_h,
+                           **kw)
+
+
+def team_bwd(C, dhs, gates4, cs, c0, dhn, dcn, whh16, err, **kw):
+    return C.lstm_team_bwd(dhs, gates4, cs, c0.contiguous(), dhn, dcn, whh16, err, team_ctl(dhs.device), **kw)
 
 
 

@@ -143,8 +143,8 @@ class DataParallel:
 
     def _make_hook(self, i: int):
         def hook(p):
-            self.has_grad[i] = 1.0
-            if self.overlap:
+            self.has_grad[i:i + 1].fill_(1.0)          # kernel fill (capturable), no host→device scalar copy
+            if self.overlap and not torch.cuda.is_current_stream_capturing():
                 b = self.param_bucket[i]
                 self._pending[b] = self._pending.get(b, 0) + 1
                 # Launch strictly in bucket-index order so every rank issues the same collective sequence

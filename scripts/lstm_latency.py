@@ -9,6 +9,7 @@ import torch
 
 sys.path.insert(0, '.')
 from dotaclient_amd import ops  # noqa: E402
+from dotaclient_amd.ops.lstm import team_ctl  # noqa: E402
 
 
 def _time(fn, reps):
@@ -31,9 +32,9 @@ def bench(B, S, H, reps=5, impl='team'):
     dh = torch.randn(B, S, H, device=dev)
     if impl == 'team':
         xp = torch.randn(B, S, H, 4, device=dev) * 0.5
-        out = C.lstm_team_fwd(xp, whh, h0, h0, err, True)
-        tf = _time(lambda: C.lstm_team_fwd(xp, whh, h0, h0, err, True), reps)
-        tb = _time(lambda: C.lstm_team_bwd(dh, out[3], out[2], h0, None, None, whh, err), reps)
+        out = C.lstm_team_fwd(xp, whh, h0, h0, err, team_ctl(), True)
+        tf = _time(lambda: C.lstm_team_fwd(xp, whh, h0, h0, err, team_ctl(), True), reps)
+        tb = _time(lambda: C.lstm_team_bwd(dh, out[3], out[2], h0, None, None, whh, err, team_ctl()), reps)
     else:
         xp = torch.randn(B, S, 4 * H, device=dev) * 0.5
         out = C.lstm_fwd(xp, whh, h0, h0, err, True)

@@ -10,6 +10,7 @@ import torch
 
 sys.path.insert(0, '.')
 from dotaclient_amd import ops  # noqa: E402
+from dotaclient_amd.ops.lstm import team_ctl  # noqa: E402
 
 med = (lambda a: float(np.median(a)))
 
@@ -24,7 +25,7 @@ def fwd(B=8, H=512, S=200):
     tr = torch.zeros(32 * 4 * 64 * 8, dtype=torch.int64, device='cuda')
     for _ in range(3):
         tr.zero_()
-        C.lstm_team_fwd(xp, whh, h0, h0, err, False, tr)
+        C.lstm_team_fwd(xp, whh, h0, h0, err, team_ctl(), False, tr)
     torch.cuda.synchronize()
     t = tr.view(32, 4, 64, 8).cpu().numpy().astype(np.float64) * 10.0
     nt = H // 128
@@ -58,12 +59,12 @@ def bwd(B=8, H=512, S=200):
     whh = (torch.randn(4 * H, H, device='cuda') * 0.05).to(torch.bfloat16)
     h0 = torch.zeros(B, H, device='cuda')
     err = torch.zeros(1, dtype=torch.int32, device='cuda')
-    out = C.lstm_team_fwd(xp, whh, h0, h0, err, False)
+    out = C.lstm_team_fwd(xp, whh, h0, h0, err, team_ctl(), False)
     dh = torch.randn(B, S, H, device='cuda')
     tr = torch.zeros(32 * 4 * 64 * 8, dtype=torch.int64, device='cuda')
     for _ in range(3):
         tr.zero_()
-        C.lstm_team_bwd(dh, out[3], out[2], h0, None, None, whh, err, tr)
+        C.lstm_team_bwd(dh, out[3], out[2], h0, None, None, whh, err, team_ctl(), tr)
     torch.cuda.synchronize()
     t = tr.view(32, 4, 64, 8).cpu().numpy().astype(np.float64) * 10.0
     w = t[:, :, 8:60]

@@ -15,10 +15,13 @@ def _rel(a, b):
     return ((a - b).norm() / (b.norm() + 1e-12)).item()
 
 
+@pytest.mark.parametrize('pipeline', ['1', '0'])
 @pytest.mark.parametrize('preset,algo,B,S', [('lstm512', 'ppo', 4, 48), ('lstm128', 'ppo', 7, 33),
                                              ('compat', 'vpg', 3, 40), ('lstm512', 'vpg', 2, 30),
                                              ('5v5', 'ppo', 3, 24)])
-def test_fused_loss_and_grads_match_reference(gpu_ops, preset, algo, B, S):
+def test_fused_loss_and_grads_match_reference(gpu_ops, monkeypatch, pipeline, preset, algo, B, S):
+    monkeypatch.setenv('DCA_PIPELINE', pipeline)
+    monkeypatch.setenv('DCA_PIPELINE_CHUNKS', '3')
     torch.manual_seed(0)
     cfg = get_config(preset)
     pol = Policy(cfg)
@@ -56,3 +59,28 @@ def test_fused_train_step_decreases_loss(gpu_ops):
     losses = [float(L.train_step(batch)['loss']) for _ in range(8)]
     L.model.check_error()
     assert losses[-1] < losses[0]
+
+
+@pytest.mark.parametrize('chunks', ['1', '3'])
+def test_graph_captured_step_matches_eager(gpu_ops, monkeypatch, chunks):
+    """hipGraph-captured forward+backward (Learner.enable_graph) gives the same parameters as eager steps, also
+    across host synchronisations between replays (a stale host-staged buffer in the graph would show up there)."""
+    monkeypatch.setenv('DCA_PIPELINE_CHUNKS', chunks)
+    torch.manual_seed(0)
+    cfg = get_config('lstm512')
+    pol = Policy(cfg)
+    ref = copy.deepcopy(pol)
+    lc = LossConfig(algo='ppo')
+    a = Learner(pol, lc, device='cuda', backend='fused', dp=False)
+    b = Learner(ref, lc, device='cuda', backend='fused', dp=False)
+    assert b.enable_graph(warmup=1)
+    batches = [make_batch(4, 40, cfg.layout, cfg.hidden, device='cuda', seed=s) for s in range(4)]
+    for bt in batches:
+        ma = a.train_step(bt)
+        mb = b.train_step(bt)
+        torch.cuda.synchronize()
+        torch.cuda.synchronize()
+        torch.testing.assert_close(mb['grad_norm'], ma['grad_norm'], rtol=1e-4, atol=1e-7)
+    assert b.graph is not None
+    torch.testing.assert_close(b.flat.flat, a.flat.flat, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(mb['loss'], ma['loss'], rtol=1e-5, atol=1e-6)
