@@ -63,10 +63,12 @@ class GpuActorPolicy:
         self.h_units = torch.zeros(n, U, 10, **pin)
         self.h_handles = torch.full((n, U), -1, dtype=torch.long, **pin)
         self.h_keep = torch.ones(n, 1, **pin)
+        self.h_active = torch.ones(n, **pin)
         self.d_env = torch.zeros(n, 3, device=dev)
         self.d_units = torch.zeros(n, U, 10, device=dev)
         self.d_handles = torch.full((n, U), -1, dtype=torch.long, device=dev)
         self.d_keep = torch.ones(n, 1, device=dev)
+        self.d_active = torch.ones(n, device=dev)     # 0 → slot not stepped: LSTM state left untouched
         self.h = torch.zeros(n, H, device=dev)
         self.c = torch.zeros(n, H, device=dev)
         self.h16 = torch.zeros(n, H, dtype=torch.bfloat16, device=dev)
@@ -152,7 +154,7 @@ class GpuActorPolicy:
             gates = mm(x, w['wihT'])
             gates += w['brnn']
             gates += mm(self.h16, w['whhT'])
-            C.lstm_cell(gates, self.h, self.c, self.h16)
+            C.lstm_cell(gates, self.h, self.c, self.h16, self.d_active)
             xh = self.h16
         else:
             self.h.copy_(mm(x, w['wfT']) + w['bf'])
@@ -167,6 +169,7 @@ class GpuActorPolicy:
         self.d_units.copy_(self.h_units, non_blocking=True)
         self.d_handles.copy_(self.h_handles, non_blocking=True)
         self.d_keep.copy_(self.h_keep, non_blocking=True)
+        self.d_active.copy_(self.h_active, non_blocking=True)
 
     def _d2h(self):
         self.o_idx.copy_(self.idx, non_blocking=True)
@@ -218,13 +221,16 @@ class GpuActorPolicy:
             out['masks'] = self.o_msk.numpy()
         return out
 
-    def step(self, env: np.ndarray, units: np.ndarray, handles: np.ndarray, reset: Optional[np.ndarray] = None):
-        """Synchronous step: (n,3), (n,U,10), (n,U) arrays for all slots; ``reset`` (n,) bool zeroes h/c first."""
+    def step(self, env: np.ndarray, units: np.ndarray, handles: np.ndarray, reset: Optional[np.ndarray] = None,
+             active: Optional[np.ndarray] = None):
+        """Synchronous step: (n,3), (n,U,10), (n,U) arrays for all slots; ``reset`` (n,) bool zeroes h/c first;
+        ``active`` (n,) bool: only these slots advance their LSTM state (outputs of the others are don't-care)."""
         self.h_env.numpy()[:] = env
         self.h_units.numpy()[:] = units
         self.h_handles.numpy()[:] = handles
         if reset is not None:
             self.h_keep.numpy()[:, 0] = 1.0 - np.asarray(reset, dtype=np.float32)
+        self.h_active.numpy()[:] = 1.0 if active is None else np.asarray(active, dtype=np.float32)
         self.step_async()
         return self.wait()
 

@@ -59,6 +59,7 @@ class Player:
         self.total_steps = 0
         self.pending: Optional[Rollout] = None   # rollout waiting for its bootstrap value
         self.rewarded = False
+        self.runner = None                       # stateful (GPU-slot) runner holding this player's LSTM state
         self._reset_buffers()
 
     def _reset_buffers(self):
@@ -239,6 +240,9 @@ class Actor:
                 self.league.record(slot.opponent_version, 0.5 if won is None else float(won == latest_team))
         for team in (TEAM_RADIANT, TEAM_DIRE):
             for p in slot.players[team]:
+                if p.runner is not None:
+                    p.runner.release(id(p))
+                    p.runner = None
                 p.process_endstate(slot.end_state)
                 if p.pending is not None:
                     p.pending.bootstrap_value = 0.0
@@ -281,20 +285,33 @@ class Actor:
                 f, hero = p.featurize(obs)
                 batch.append((slot, p, f, hero))
         # one batched policy step per distinct policy object
+        # (a player bound to a stateful runner stays with it: its recurrent state lives there)
         groups: Dict[int, List[int]] = {}
         for k, (_, p, _, _) in enumerate(batch):
-            groups.setdefault(id(p.policy), []).append(k)
+            groups.setdefault(id(p.runner) if p.runner is not None else id(p.policy), []).append(k)
         actions_by_slot: Dict[int, list] = {}
         for _, idxs in groups.items():
             pol = batch[idxs[0]][1].policy
-            runner = self.runner_for(pol)
+            runner = batch[idxs[0]][1].runner or self.runner_for(pol)
             env = np.stack([batch[k][2].env for k in idxs])
             units = np.stack([batch[k][2].units for k in idxs])
             handles = np.stack([batch[k][2].handles for k in idxs])
-            hidden = None
-            if pol.is_recurrent:
-                hidden = (np.stack([batch[k][1].hidden[0] for k in idxs]), np.stack([batch[k][1].hidden[1] for k in idxs]))
-            out, new_hidden = runner.step(env, units, handles, hidden)
+            hidden = new_hidden = None
+            if getattr(runner, 'stateful', False):
+                # LSTM state stays in the runner's device slots; fetch it only where the record stores it
+                players = [batch[k][1] for k in idxs]
+                need = [p.hidden is not None and bool(p.hidden_stride) and len(p.env) % p.hidden_stride == 0
+                        for p in players]
+                out, prev = runner.step_players(env, units, handles, [id(p) for p in players], need)
+                for j, p in enumerate(players):
+                    p.runner = runner
+                    if prev is not None and j in prev:
+                        p.hidden = prev[j]
+            else:
+                if pol.is_recurrent:
+                    hidden = (np.stack([batch[k][1].hidden[0] for k in idxs]),
+                              np.stack([batch[k][1].hidden[1] for k in idxs]))
+                out, new_hidden = runner.step(env, units, handles, hidden)
             for j, k in enumerate(idxs):
                 slot, p, f, hero = batch[k]
                 if p.pending is not None:          # truncated rollout: bootstrap from this step's value

@@ -12,8 +12,9 @@ kernels) and captures the step in a hipGraph; on CPU it runs the torch reference
 """
 from __future__ import annotations
 
+from collections import OrderedDict
 from dataclasses import dataclass
-from typing import List, Optional
+from typing import Callable, List, Optional
 
 import numpy as np
 import torch
@@ -110,3 +111,36 @@ class PolicyRunner:
         if hn is not None:
             new_hidden = (hn[0][0].cpu().numpy(), hn[1][0].cpu().numpy())
         return out, new_hidden
+
+
+class RunnerCache:
+    """``runner_for(policy)`` for the Actor: one runner for the synced latest policy and one per stored weight
+    version (LRU of ``max_snapshots``), so games against the same snapshot share a runner — on the GPU, one
+    captured graph and one slot table — instead of one per Policy object (the WeightStore builds a fresh object per
+    opponent game, actor/weights.py). Players already bound to an evicted stateful runner keep using it."""
+
+    def __init__(self, make: Callable, latest_policy=None, max_snapshots: int = 8):
+        self.make = make
+        self.latest_policy = latest_policy
+        self.max_snapshots = max(1, int(max_snapshots))
+        self.latest = None
+        self.snapshots: "OrderedDict[int, object]" = OrderedDict()
+
+    def __call__(self, policy):
+        if policy is self.latest_policy:
+            if self.latest is None:
+                self.latest = self.make(policy)
+            return self.latest
+        key = getattr(policy, 'weight_version', None)
+        key = ('obj', id(policy)) if key is None else key
+        r = self.snapshots.get(key)
+        if r is None:
+            r = self.snapshots[key] = self.make(policy)
+            while len(self.snapshots) > self.max_snapshots:
+                self.snapshots.popitem(last=False)
+        else:
+            self.snapshots.move_to_end(key)
+        return r
+
+    def runners(self):
+        return ([self.latest] if self.latest is not None else []) + list(self.snapshots.values())

@@ -46,6 +46,8 @@ def build_parser():
     ap.add_argument('--wire', type=str, default='dcx1', choices=['dcx1', 'pickle'])
     ap.add_argument('--seed', type=int, default=None)
     ap.add_argument('--hidden-stride', type=int, default=256, help='store LSTM state every N steps')
+    ap.add_argument('--fp8', type=str2bool, default=False,
+                    help='GPU actor: e4m3 FP8 policy GEMMs (pre-RNN, LSTM input/recurrent, heads)')
     ap.add_argument('--league', type=str, default='oldest', choices=['oldest', 'uniform', 'recent', 'pfsp'],
                     help='opponent sampling over the weight history when not playing the latest weights')
     return ap
@@ -66,7 +68,8 @@ def main(argv=None):
     args = build_parser().parse_args(argv)
     logging.basicConfig(format='%(asctime)s %(levelname)-8s %(message)s', level=args.log_level)
     from ..actor.game import Actor
-    from ..actor.runner import PolicyRunner
+    from ..actor.gpu_runner import GpuRunner, gpu_runner_supported
+    from ..actor.runner import PolicyRunner, RunnerCache
     from ..actor.weights import WeightStore
     from ..env import get_1v1_bot_vs_default_config, get_1v1_selfplay_config
     from ..models.policy import get_config
@@ -87,13 +90,15 @@ def main(argv=None):
     device = args.device
     if device.startswith('cuda') and not torch.cuda.is_available():
         device = 'cpu'
-    runners = {}
 
-    def runner_for(policy):
-        r = runners.get(id(policy))
-        if r is None:
-            r = runners[id(policy)] = PolicyRunner(policy, device=device, seed=rng.randrange(1 << 30))
-        return r
+    def make_runner(policy):
+        seed_r = rng.randrange(1 << 30)
+        if device.startswith('cuda') and gpu_runner_supported(policy):
+            # graph-captured batched GPU step; players' LSTM state lives in device slots
+            return GpuRunner(policy.to(device), device=device, seed=seed_r, capacity=max(8, 2 * args.games),
+                             fp8=args.fp8)
+        return PolicyRunner(policy, device=device, seed=seed_r)
+    runner_for = RunnerCache(make_runner, latest_policy=ws.latest_policy)
     metrics = MetricsWriter(args.log_dir) if (args.validation and args.log_dir) else None
     config_fn = (lambda: get_1v1_bot_vs_default_config(rng=rng)) if args.validation else get_1v1_selfplay_config
     from ..actor.league import League

@@ -131,11 +131,12 @@ __global__ __launch_bounds__(256) void sample_kernel(const float* __restrict__ z
 
 // gates (N, 4H) pre-activations (x·W_ihᵀ + h·W_hhᵀ + b, fp32) → h, c (fp32) in place + h bf16 copy
 __global__ __launch_bounds__(256) void lstm_cell_kernel(const float* __restrict__ g, float* __restrict__ h,
-                                                        float* __restrict__ c, short* __restrict__ h16, int N,
-                                                        int H) {
+                                                        float* __restrict__ c, short* __restrict__ h16,
+                                                        const float* __restrict__ active, int N, int H) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= N * H) return;
   const int n = i / H, j = i % H;
+  if (active && active[n] == 0.f) return;   // slot not stepped this call: its state is left untouched
   const float* gr = g + (size_t)n * 4 * H;
   const float ig = dca::sigmoidf_(gr[j]), fg = dca::sigmoidf_(gr[H + j]), gg = dca::tanhf_(gr[2 * H + j]),
               og = dca::sigmoidf_(gr[3 * H + j]);
@@ -157,7 +158,8 @@ extern "C" hipError_t dca_sample_actions(const float* z, int ldz, const short* e
   return hipGetLastError();
 }
 
-extern "C" hipError_t dca_lstm_cell(const float* gates, float* h, float* c, short* h16, int N, int H, hipStream_t st) {
-  lstm_cell_kernel<<<(N * H + 255) / 256, 256, 0, st>>>(gates, h, c, h16, N, H);
+extern "C" hipError_t dca_lstm_cell(const float* gates, float* h, float* c, short* h16, const float* active, int N,
+                                    int H, hipStream_t st) {
+  lstm_cell_kernel<<<(N * H + 255) / 256, 256, 0, st>>>(gates, h, c, h16, active, N, H);
   return hipGetLastError();
 }

@@ -317,12 +317,20 @@ void sample_actions(torch::Tensor z, torch::Tensor emb, torch::Tensor handles, i
 }
 
 // LSTM cell from fp32 pre-activation gates (N,4H): updates h, c (N,H) f32 in place, writes h16 (N,H) bf16.
-void lstm_cell(torch::Tensor gates, torch::Tensor h, torch::Tensor c, torch::Tensor h16) {
+// Optional ``active`` (N) f32: rows with active == 0 keep their h / c / h16 (slots not stepped this call).
+void lstm_cell(torch::Tensor gates, torch::Tensor h, torch::Tensor c, torch::Tensor h16,
+               c10::optional<torch::Tensor> active) {
   CHECK_F32(gates); CHECK_F32(h); CHECK_F32(c); CHECK_BF16(h16);
   const int N = h.size(0), H = h.size(1);
   TORCH_CHECK(gates.size(0) == N && gates.size(1) == 4 * H && c.sizes() == h.sizes() && h16.sizes() == h.sizes(),
               "lstm_cell shapes");
-  hip_check(dca_lstm_cell(ptr<float>(gates), ptr<float>(h), ptr<float>(c), ptr<short>(h16), N, H, cur_stream()),
+  const float* act = nullptr;
+  if (active && active->defined()) {
+    CHECK_F32(*active);
+    TORCH_CHECK(active->numel() == N, "lstm_cell: active must have one entry per row");
+    act = ptr<float>(*active);
+  }
+  hip_check(dca_lstm_cell(ptr<float>(gates), ptr<float>(h), ptr<float>(c), ptr<short>(h16), act, N, H, cur_stream()),
             "dca_lstm_cell");
 }
 
@@ -353,5 +361,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("whh"), py::arg("err"), py::arg("ctl"), py::arg("trace") = py::none(),
         py::arg("time_major") = false, py::arg("dg_out") = py::none());
   m.def("sample_actions", &sample_actions, "fused masked hierarchical Gumbel-max action sampling (actor)");
-  m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)");
+  m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)", py::arg("gates"),
+        py::arg("h"), py::arg("c"), py::arg("h16"), py::arg("active") = py::none());
 }
