@@ -610,13 +610,14 @@ inline int team_knobs() {
 }
 
 inline void plan(int B, int& nch, int& Bc, int& MT) {
-  // chains of ≤ 32 sequences; as many concurrent chains as teams (8), more chains queue behind them
-  nch = (B + 31) / 32;
-  if (nch < kMaxTeams && B > 16) {
-    // prefer more, smaller chains while teams are idle (≤ 16 rows keeps MT = 1)
-    const int n16 = (B + 15) / 16;
-    nch = n16 <= kMaxTeams ? n16 : nch;
-  }
+  // Spread the sequences over all 8 teams (one chain per XCD) before packing rows into a chain: per-step latency
+  // grows with rows per chain (more granules to gather and publish), measured B=8, H=512 fwd/bwd µs per step:
+  // 1 chain × 8 rows 2.21/2.82, 2 × 4 2.09/2.57, 4 × 2 2.08/2.41, 8 × 1 2.08/2.26. Chains hold ≤ 32 rows; beyond
+  // 8·32 sequences further chains queue behind the running ones.
+  nch = B <= kMaxTeams * 32 ? (B < kMaxTeams ? B : kMaxTeams) : (B + 31) / 32;
+  // DCA_TEAM_ROWS = sequences per chain (latency experiments: e.g. 1 → B independent chains on B teams)
+  static const int forced = [] { const char* e = getenv("DCA_TEAM_ROWS"); return e ? atoi(e) : 0; }();
+  if (forced > 0 && forced <= 32) nch = (B + forced - 1) / forced;
   Bc = (B + nch - 1) / nch;
   MT = Bc <= 16 ? 1 : 2;
 }
