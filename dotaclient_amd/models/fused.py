@@ -8,7 +8,7 @@ hand-ordered backward (no per-op autograd graph):
 stage              forward / backward
 =================  ======================================================================================
 entity encoder     ``_C.encoder_fwd``: unit MLP + per-type GEMM + max-pool/argmax (MFMA, one kernel) /
-                   ``_C.encoder_bwd`` (∂W1 in-kernel) + one large-K hipBLASLt GEMM per unit type for ∂W_τ
+                   ``_C.encoder_bwd``: ∂W1 in-kernel, ∂emb/basic as K-blocked images → split-K MFMA GEMM for ∂W_τ
 pre-RNN            bf16 GEMM (fp32 out) + ReLU / two GEMMs
 LSTM               input-projection GEMM + ONE persistent ``_C.lstm_fwd`` launch /
                    ONE persistent ``_C.lstm_bwd`` launch + weight-gradient GEMMs over all B·S rows
@@ -192,7 +192,7 @@ class _PolicyLoss(torch.autograd.Function):
         dtl_g = (dtl * g).contiguous()
         wtT16 = wt16.transpose(1, 2).contiguous()
         counts = list(cfg.layout.counts)
-        demb, basic, dw1, db1 = C.encoder_bwd(units2, P['affine_unit_basic_stats.weight'].detach(),
+        dwt, dw1, db1 = C.encoder_bwd(units2, P['affine_unit_basic_stats.weight'].detach(),
                                               P['affine_unit_basic_stats.bias'].detach(), wtT16, dtl_g, z, dx896, arg,
                                               counts, bool(cfg.compat_bugs))
         grads['affine_unit_basic_stats.weight'] = dw1
@@ -211,12 +211,9 @@ class _PolicyLoss(torch.autograd.Function):
             dpool[3] += dpool[5]
             dpool[5] = 0
         dbt = dbt + dpool
-        off = 0
-        for t, (s, cnt) in enumerate(zip(TYPE_SUFFIX, counts)):
-            lo, hi = off * N, (off + cnt) * N
-            grads[f'affine_unit_{s}.weight'] = tn_splitk(demb[lo:hi], basic[lo:hi])
+        for t, s in enumerate(TYPE_SUFFIX):
+            grads[f'affine_unit_{s}.weight'] = dwt[t]
             grads[f'affine_unit_{s}.bias'] = dbt[t]
-            off += cnt
         # env embedding (3 → 128): tiny, fp32 torch
         we, be = P['affine_env.weight'].detach(), P['affine_env.bias'].detach()
         de = dx896[:, :128] * ((env2 @ we.t() + be) > 0)

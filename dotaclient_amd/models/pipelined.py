@@ -184,16 +184,12 @@ class PipelinedPolicyLoss(torch.autograd.Function):
             dbpre += dpre.sum(0)
             dx896 = _mm(dpre16, wpre16)
             q = z[r0:r1, :128]
-            demb, basic, dw1_c, db1_c = C.encoder_bwd(units_t[r0:r1], w1, b1, wtT16, dtl[r0:r1], z[r0:r1],
+            dwt_c, dw1_c, db1_c = C.encoder_bwd(units_t[r0:r1], w1, b1, wtT16, dtl[r0:r1], z[r0:r1],
                                                       dx896, arg[r0:r1], counts, bool(cfg.compat_bugs))
             dw1 += dw1_c
             db1 += db1_c
             dbt += tn_splitk((dtl[r0:r1] @ seg).contiguous(), q.contiguous()) + dx896[:, 128:].reshape(n, 6, 128).sum(0)
-            off = 0
-            for t, cnt in enumerate(counts):
-                lo, hi = off * n, (off + cnt) * n
-                dWt[t] += tn_splitk(demb[lo:hi], basic[lo:hi])
-                off += cnt
+            dWt += dwt_c
             env_c = env_t[r0:r1]
             de = dx896[:, :128] * ((env_c @ we.t() + be) > 0)
             dWe += de.t() @ env_c

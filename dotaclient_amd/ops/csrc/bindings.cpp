@@ -283,16 +283,17 @@ std::vector<torch::Tensor> encoder_bwd(torch::Tensor units, torch::Tensor w1, to
   for (int i = 0; i < 6; ++i) { c[i] = (int)counts[i]; tot += counts[i]; }
   TORCH_CHECK(tot == U && U <= 64, "counts must sum to U <= 64");
   auto o = units.options();
-  auto demb = torch::empty({(int64_t)U * N, 128}, o.dtype(at::kBFloat16));
-  auto basic = torch::empty({(int64_t)U * N, 128}, o.dtype(at::kBFloat16));
-  auto dw1 = torch::zeros({128, 10}, o);
-  auto db1 = torch::zeros({128}, o);
+  auto dwt = torch::empty({6, 128, 128}, o);
+  auto dw1 = torch::empty({128, 10}, o);
+  auto db1 = torch::empty({128}, o);
+  const size_t wsb = dca_encoder_bwd_workspace(N, U, c);
+  auto ws = torch::empty({(int64_t)((wsb + 3) / 4)}, o);
   hip_check(dca_encoder_bwd(ptr<float>(units), ptr<float>(w1), ptr<float>(b1), ptr<short>(wtT), ptr<float>(dtl),
-                            ptr<float>(q), (int)q.stride(0), ptr<float>(dx), ptr<unsigned char>(arg),
-                            ptr<short>(demb), ptr<short>(basic), ptr<float>(dw1), ptr<float>(db1), N, U, c,
-                            compat ? 1 : 0, cur_stream()),
+                            ptr<float>(q), (int)q.stride(0), ptr<float>(dx), ptr<unsigned char>(arg), ptr<float>(dwt),
+                            ptr<float>(dw1), ptr<float>(db1), ws.data_ptr(), wsb, N, U, c, compat ? 1 : 0,
+                            cur_stream()),
             "dca_encoder_bwd");
-  return {demb, basic, dw1, db1};
+  return {dwt, dw1, db1};
 }
 
 // ------------------------------------------------------------------------------------------------------------
@@ -348,7 +349,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("trace") = py::none());
   m.def("heads_loss", &heads_loss, "fused heads + pointer + masked log-softmax + PPO/VPG loss + gradients");
   m.def("encoder_fwd", &encoder_fwd, "fused entity encoder forward (unit MLP, per-type GEMM, max-pool+argmax)");
-  m.def("encoder_bwd", &encoder_bwd, "fused entity encoder backward (dW1 in-kernel; demb/basic for dW_type GEMMs)");
+  m.def("encoder_bwd", &encoder_bwd, "fused entity encoder backward: dW_type (K-blocked split-K MFMA GEMM), dW1, db1");
   m.def("lstm_bwd", &lstm_bwd, "persistent LSTM backward recurrence (granule reduce-scatter)", py::arg("dhs"),
         py::arg("gates"), py::arg("cs"), py::arg("c0"), py::arg("dhn"), py::arg("dcn"), py::arg("whh"), py::arg("err"),
         py::arg("trace") = py::none());

@@ -43,10 +43,8 @@ __device__ __forceinline__ float group_max(float v) {
 
 // bf16 <-> f32 (round-to-nearest-even), as raw 16-bit patterns.
 __device__ __forceinline__ short f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x7fffffu)) return (short)((u >> 16) | 0x40);  // NaN stays NaN
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (short)(u >> 16);
+  // round-to-nearest-even in one v_cvt_pk_bf16_f32 (gfx950); NaN stays NaN
+  return __builtin_bit_cast(short, (__bf16)f);
 }
 __device__ __forceinline__ float bf2f(short h) { return __uint_as_float(((uint32_t)(uint16_t)h) << 16); }
 

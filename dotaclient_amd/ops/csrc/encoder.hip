@@ -62,14 +62,14 @@ struct BwdParams {
   int ldq;
   const float* dx;      // (N, 896) f32 ∂L/∂x896
   const unsigned char* arg;
-  short* demb;          // type-major bf16: type τ block at rowbase[τ], row m = u·N + n
+  short* demb;          // K-blocked bf16 (see kBlk): block (τ, u, 16-row block rb) at blkbase[τ] + u·NB + rb
   short* basic;         // same layout
-  float* dw1;           // (128, 10) f32 accumulated with atomics
-  float* db1;           // (128)
+  float* w1part;        // (gridDim.x, 128·10 + 128) f32 per-workgroup ∂W1 ‖ ∂b1 partials
   int N;
   int compat;
   Layout L;
-  long long rowbase[6];
+  long long blkbase[6];
+  int NB;               // 16-row blocks per unit slot = ⌈N/16⌉
 };
 
 __device__ __forceinline__ void type_job(int wv, int j, int& tau, int& g) {
@@ -77,27 +77,6 @@ __device__ __forceinline__ void type_job(int wv, int j, int& tau, int& g) {
   const int lists[2][3] = {{2, 1, 4}, {3, 0, 5}};
   g = wv & 1;
   tau = (j < 3) ? lists[wv >> 1][j] : -1;
-}
-
-// ------------------------------------------------------------------------------------------------------------
-// Layer 1 for a 16-row tile on fp32 MFMA. Returns C-layout (rows (lane>>4)*4+r, col 16n + lane&15) pre-activations.
-__device__ __forceinline__ void layer1(const float* __restrict__ units, int U, int N, int row0, int uslot,
-                                      const float (&w1f)[8][3], f32x4 (&acc)[8], int lane) {
-  const int i = lane & 15, kq = lane >> 4;
-  const int row = row0 + i;
-  float a[3];
-#pragma unroll
-  for (int s = 0; s < 3; ++s) {
-    const int k = 4 * s + kq;
-    a[s] = (row < N && k < kF) ? units[((size_t)row * U + uslot) * kF + k] : 0.f;
-  }
-#pragma unroll
-  for (int n = 0; n < 8; ++n) {
-    f32x4 c = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 3; ++s) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], w1f[n][s], c, 0, 0, 0);
-    acc[n] = c;
-  }
 }
 
 __device__ __forceinline__ void load_w1(const float* __restrict__ w1, float (&w1f)[8][3], int lane) {
@@ -121,12 +100,57 @@ __device__ __forceinline__ void load_bfrags(const short* __restrict__ m, bf16x8 
       bf[n][s] = *reinterpret_cast<const bf16x8*>(m + (size_t)(16 * n + j) * kD + 32 * s + 8 * kg);
 }
 
+// LDS staging of a type job's unit features (shared by forward and backward, see the backward's notes).
+constexpr int kStage = 24;                  // units staged per chunk (1v1 max 16, 5v5 max 24 per type)
+constexpr int kUP = kStage * kF + 4;        // LDS pitch (floats) of a staged row
+constexpr int kW1 = kD * kF + kD;           // ∂W1 (128×10) ‖ ∂b1 (128) floats per partial
+
+__device__ __forceinline__ void layer1_lds(const float* __restrict__ ur, int u, const float (&w1f)[8][3],
+                                          f32x4 (&acc)[8], int lane) {
+  // ur: staged rows [16][kUP]; row i = lane&15, k = 4s + lane>>4
+  const int i = lane & 15, kq = lane >> 4;
+  float a[3];
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const int k = 4 * s + kq;
+    a[s] = k < kF ? ur[i * kUP + u * kF + k] : 0.f;
+  }
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int s = 0; s < 3; ++s) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], w1f[n][s], c, 0, 0, 0);
+    acc[n] = c;
+  }
+}
+
+// Stage units[row0 .. row0+15][uoff+c0 .. +cc][0..9] and dtl for the same (row, unit) block into LDS (one wave).
+__device__ __forceinline__ void stage_units(const float* __restrict__ units, const float* __restrict__ dtl, int U,
+                                            int N, int row0, int ubase, int cc, float* ur, float* dr, int lane) {
+  const int per = cc * kF;
+  const int tot = 16 * per;
+#pragma unroll 4
+  for (int idx = lane; idx < tot; idx += 64) {
+    const int r = idx / per, e = idx - r * per;
+    const int row = row0 + r;
+    ur[r * kUP + e] = row < N ? units[((size_t)row * U + ubase) * kF + e] : 0.f;
+  }
+  if (dtl) {
+    for (int idx = lane; idx < 16 * cc; idx += 64) {
+      const int r = idx / cc, e = idx - r * cc;
+      const int row = row0 + r;
+      dr[r * kStage + e] = row < N ? dtl[(size_t)row * U + ubase + e] : 0.f;
+    }
+  }
+}
+
 // ============================================================================================================
 __global__ __launch_bounds__(256, 1) void encoder_fwd_kernel(FwdParams P) {
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int rbase = blockIdx.x * kRows;
   const int U = P.L.U, N = P.N;
   __shared__ __attribute__((aligned(16))) short scr[4][16][kLd];
+  __shared__ __attribute__((aligned(16))) float ust[4][16 * kUP];
 
   // ---- env embedding: relu(We·env + be) → x896[:, 0:128] (32 rows × 128 cols over 256 threads)
   {
@@ -167,9 +191,16 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_kernel(FwdParams P) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) parg[n][r] = 0;
     }
+    float* ur = &ust[wv][0];
     for (int u = 0; u < cnt; ++u) {
+      const int uc = u % kStage;
+      if (uc == 0) {   // stage the next ≤ kStage units of this job (all loads in flight at once)
+        __builtin_amdgcn_wave_barrier();
+        stage_units(P.units, nullptr, U, N, row0, uoff + u, min(kStage, cnt - u), ur, nullptr, lane);
+        __builtin_amdgcn_wave_barrier();
+      }
       f32x4 acc[8];
-      layer1(P.units, U, N, row0, uoff + u, w1f, acc, lane);
+      layer1_lds(ur, uc, w1f, acc, lane);
       // basic = relu(acc + b1) → bf16 → scratch [row][col]
 #pragma unroll
       for (int n = 0; n < 8; ++n)
@@ -224,12 +255,37 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_kernel(FwdParams P) {
 }
 
 // ============================================================================================================
+// Backward. Latency structure: one wave per SIMD (W_τ lives in 128 VGPRs), so every global load a unit iteration
+// waits on is exposed. Per type job the wave therefore (1) stages the job's unit features and pointer-logit
+// gradients for its 16 rows in LDS with all loads in flight at once, and (2) hoists the per-(row, type) operands —
+// pointer query q, pool gradient ∂pool and the argmax bytes — into registers; a unit iteration then touches
+// global memory only for its output stores. ∂W1/∂b1 are reduced over the workgroup's waves in LDS and written as
+// one partial per workgroup; encoder_w1_reduce sums the partials in a fixed order (deterministic, no atomics).
+// K-blocked layout of ∂emb and basic for the weight-gradient GEMM (∂W_τ = Σ ∂embᵀ·basic over all rows and units):
+// element (row r of 16-row block blk, column e) at (blk·128 + e)·16 + r. A 16x16x32 MFMA fragment (8 consecutive k
+// of one column) is then one 16-byte load, and a (τ, u, row block) tile is 4 KB contiguous.
+// The tile is transposed through a padded per-wave LDS image: column e at element e·16 + (e/8)·16 (32-B pad every
+// 8 columns spreads the four 8-column groups of a store over different banks).
+constexpr int kTile = 128 * 16 + 16 * 16;
+__device__ __forceinline__ int toff(int e, int r) { return e * 16 + (e >> 3) * 16 + r; }
+__device__ __forceinline__ void store_tile(const short* tw, short* dst, int lane) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int c = lane + 64 * q;                  // 16-byte chunk: column c/2, rows 8·(c&1) …
+    *reinterpret_cast<bf16x8*>(dst + c * 8) = *reinterpret_cast<const bf16x8*>(tw + toff(c >> 1, 8 * (c & 1)));
+  }
+}
+
 __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int rbase = blockIdx.x * kRows;
   const int U = P.L.U, N = P.N;
   const int i = lane & 15, kg = lane >> 4;
-  __shared__ __attribute__((aligned(16))) short scr[4][16][kLd];
+  __shared__ __attribute__((aligned(16))) short tsc[4][kTile];
+  __shared__ __attribute__((aligned(16))) float ust[4][16 * kUP];
+  __shared__ float dst_[4][16 * kStage];
+  __shared__ float wred[kW1];
+  short* tw = &tsc[wv][0];
 
   float w1f[8][3];
   load_w1(P.w1, w1f, lane);
@@ -243,6 +299,7 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
     dw1acc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
     db1acc[n] = 0.f;
   }
+  for (int e = tid; e < kW1; e += 256) wred[e] = 0.f;
 
   for (int j = 0; j < 3; ++j) {
     int tau, g;
@@ -250,120 +307,234 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
     const int cnt = P.L.cnt[tau], uoff = P.L.off[tau];
     if (cnt == 0) continue;
     const int row0 = rbase + 16 * g;
+    if (row0 >= N) continue;                      // wave-uniform: no rows in this group
+    const int rb = row0 / 16;
     bf16x8 wf[8][4];   // B[k=e][n=j] = W_τ[e][j] = W_τᵀ[j][e]
     load_bfrags(P.wtT + (size_t)tau * kD * kD, wf, lane);
-    // per-lane A-layout row data reused across the type's units: q and ∂pool (8 cols × 4 k-steps)
     const int arow = row0 + i;
     const bool rok = arow < N;
     const bool eth_dead = P.compat && tau == 5;   // reference bug: eth pool unused → no pool gradient
-    for (int u = 0; u < cnt; ++u) {
-      // ---- recompute layer 1 (C layout) → basic f32 + bf16 staged for the type-major store
-      f32x4 acc[8];
-      layer1(P.units, U, N, row0, uoff + u, w1f, acc, lane);
-      f32x4 bas[8];
+    // ---- per-(row, type) operands in A layout (row i, cols 32s + 8kg + jj), loaded once per type job
+    float qv[4][8], dpv[4][8];
+    unsigned agv[4][2];
 #pragma unroll
-      for (int n = 0; n < 8; ++n)
+    for (int s = 0; s < 4; ++s) {
+      const int e0 = 32 * s + 8 * kg;
+      if (rok) {
+        const float4 qa = *reinterpret_cast<const float4*>(P.q + (size_t)arow * P.ldq + e0);
+        const float4 qb = *reinterpret_cast<const float4*>(P.q + (size_t)arow * P.ldq + e0 + 4);
+        qv[s][0] = qa.x; qv[s][1] = qa.y; qv[s][2] = qa.z; qv[s][3] = qa.w;
+        qv[s][4] = qb.x; qv[s][5] = qb.y; qv[s][6] = qb.z; qv[s][7] = qb.w;
+        const float* dp = P.dx + (size_t)arow * 896 + kD + tau * kD + e0;
+        const float4 da = *reinterpret_cast<const float4*>(dp);
+        const float4 db = *reinterpret_cast<const float4*>(dp + 4);
+        dpv[s][0] = da.x; dpv[s][1] = da.y; dpv[s][2] = da.z; dpv[s][3] = da.w;
+        dpv[s][4] = db.x; dpv[s][5] = db.y; dpv[s][6] = db.z; dpv[s][7] = db.w;
+        const uint2 ag = *reinterpret_cast<const uint2*>(P.arg + ((size_t)arow * 6 + tau) * kD + e0);
+        agv[s][0] = eth_dead ? 0xffffffffu : ag.x;
+        agv[s][1] = eth_dead ? 0xffffffffu : ag.y;
+      } else {
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bas[n][r] = fmaxf(acc[n][r] + b1v[n], 0.f);
-      // ---- ∂emb in A layout: lane (row i, cols 32s + 8kg + jj)
-      const float dtl = rok ? P.dtl[(size_t)arow * U + uoff + u] : 0.f;
-      bf16x8 de[4];
-      const size_t mrow = (size_t)u * N + arow;   // row within the type-major block of τ
+        for (int jj = 0; jj < 8; ++jj) { qv[s][jj] = 0.f; dpv[s][jj] = 0.f; }
+        agv[s][0] = agv[s][1] = 0xffffffffu;
+      }
+    }
+    float* ur = &ust[wv][0];
+    float* dr = &dst_[wv][0];
+    for (int c0 = 0; c0 < cnt; c0 += kStage) {
+      const int cc = min(kStage, cnt - c0);
+      __builtin_amdgcn_wave_barrier();
+      stage_units(P.units, P.dtl, U, N, row0, uoff + c0, cc, ur, dr, lane);
+      __builtin_amdgcn_wave_barrier();
+      for (int uc = 0; uc < cc; ++uc) {
+        const int u = c0 + uc;
+        // ---- recompute layer 1 (C layout) → basic f32
+        f32x4 acc[8];
+        layer1_lds(ur, uc, w1f, acc, lane);
+        f32x4 bas[8];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int e0 = 32 * s + 8 * kg;
-        float v[8];
-        if (rok) {
-          const float4 qa = *reinterpret_cast<const float4*>(P.q + (size_t)arow * P.ldq + e0);
-          const float4 qb = *reinterpret_cast<const float4*>(P.q + (size_t)arow * P.ldq + e0 + 4);
-          v[0] = dtl * qa.x; v[1] = dtl * qa.y; v[2] = dtl * qa.z; v[3] = dtl * qa.w;
-          v[4] = dtl * qb.x; v[5] = dtl * qb.y; v[6] = dtl * qb.z; v[7] = dtl * qb.w;
-          if (!eth_dead) {
-            const float* dp = P.dx + (size_t)arow * 896 + kD + tau * kD + e0;
-            const unsigned char* ag = P.arg + ((size_t)arow * 6 + tau) * kD + e0;
+        for (int n = 0; n < 8; ++n)
 #pragma unroll
-            for (int jj = 0; jj < 8; ++jj) v[jj] += (ag[jj] == u) ? dp[jj] : 0.f;
+          for (int r = 0; r < 4; ++r) bas[n][r] = fmaxf(acc[n][r] + b1v[n], 0.f);
+        // ---- ∂emb in A layout: dtl·q + ∂pool where this unit is the argmax
+        const float dtl = dr[i * kStage + uc];
+        bf16x8 de[4];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          float v[8];
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) {
+            const unsigned ab = (agv[s][jj >> 2] >> (8 * (jj & 3))) & 0xffu;
+            v[jj] = dtl * qv[s][jj] + (ab == (unsigned)u ? dpv[s][jj] : 0.f);
           }
-          if (P.compat && tau == 3) {   // eth pool = enh pool: its gradient lands on enh argmax units
+          if (P.compat && tau == 3 && rok) {   // eth pool = enh pool: its gradient lands on enh argmax units
+            const int e0 = 32 * s + 8 * kg;
             const float* dp = P.dx + (size_t)arow * 896 + kD + 5 * kD + e0;
             const unsigned char* ag = P.arg + ((size_t)arow * 6 + 3) * kD + e0;
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) v[jj] += (ag[jj] == u) ? dp[jj] : 0.f;
           }
-        } else {
+          bf16x8 h;
 #pragma unroll
-          for (int jj = 0; jj < 8; ++jj) v[jj] = 0.f;
+          for (int jj = 0; jj < 8; ++jj) h[jj] = dca::f2bf(v[jj]);
+          de[s] = h;
+#pragma unroll
+          for (int jj = 0; jj < 8; ++jj) tw[toff(32 * s + 8 * kg + jj, i)] = h[jj];
         }
-        bf16x8 h;
+        // ---- ∂emb tile → K-blocked image (4 KB contiguous per (τ, u, row block))
+        const size_t blk = (size_t)(P.blkbase[tau] + (long long)u * P.NB + rb) * (kD * 16);
+        __builtin_amdgcn_wave_barrier();
+        store_tile(tw, P.demb + blk, lane);
+        __builtin_amdgcn_wave_barrier();
+        // ---- ∂basic = ∂emb · W_τ, ReLU' → C layout
+        f32x4 dbp[8];
 #pragma unroll
-        for (int jj = 0; jj < 8; ++jj) h[jj] = dca::f2bf(v[jj]);
-        de[s] = h;
-        if (rok) *reinterpret_cast<bf16x8*>(P.demb + P.rowbase[tau] * kD + mrow * kD + e0) = h;
-      }
-      // ---- ∂basic = ∂emb · W_τ, ReLU' → C layout
-      f32x4 dbp[8];
+        for (int n = 0; n < 8; ++n) {
+          f32x4 c = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int n = 0; n < 8; ++n) {
-        f32x4 c = {0.f, 0.f, 0.f, 0.f};
+          for (int s = 0; s < 4; ++s) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(de[s], wf[n][s], c, 0, 0, 0);
 #pragma unroll
-        for (int s = 0; s < 4; ++s) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(de[s], wf[n][s], c, 0, 0, 0);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) c[r] = bas[n][r] > 0.f ? c[r] : 0.f;
-        dbp[n] = c;
-      }
-      // ---- ∂W1 += ∂basicᵀ · units  (16x16x16 bf16: A[j][m] = ∂basic C-tile, B[m][k] = units)
-      bf16x4 ub;
-      {
-        const int kk = lane & 15;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = row0 + 4 * kg + r;
-          const float x = (row < N && kk < kF) ? P.units[((size_t)row * U + uoff + u) * kF + kk] : 0.f;
-          ub[r] = dca::f2bf(x);
+          for (int r = 0; r < 4; ++r) c[r] = bas[n][r] > 0.f ? c[r] : 0.f;
+          dbp[n] = c;
         }
-      }
+        // ---- ∂W1 += ∂basicᵀ · units  (16x16x16 bf16: A[j][m] = ∂basic C-tile, B[m][k] = units from LDS)
+        bf16x4 ub;
+        {
+          const int kk = lane & 15;
 #pragma unroll
-      for (int n = 0; n < 8; ++n) {
-        bf16x4 a;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          a[r] = dca::f2bf(dbp[n][r]);
-          db1acc[n] += dbp[n][r];
+          for (int r = 0; r < 4; ++r) ub[r] = dca::f2bf(kk < kF ? ur[(4 * kg + r) * kUP + uc * kF + kk] : 0.f);
         }
-        dw1acc[n] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, ub, dw1acc[n], 0, 0, 0);
-      }
-      // ---- store basic (bf16, type-major) via the LDS scratch for coalescing
 #pragma unroll
-      for (int n = 0; n < 8; ++n)
+        for (int n = 0; n < 8; ++n) {
+          bf16x4 a;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) scr[wv][kg * 4 + r][16 * n + i] = dca::f2bf(bas[n][r]);
-      __builtin_amdgcn_wave_barrier();
-      {
-        const int rr = lane >> 2, ch = lane & 3;
-        const int row = row0 + rr;
-        if (row < N) {
-          const bf16x8* src = reinterpret_cast<const bf16x8*>(&scr[wv][rr][32 * ch]);
-          bf16x8* dst = reinterpret_cast<bf16x8*>(P.basic + P.rowbase[tau] * kD + ((size_t)u * N + row) * kD + 32 * ch);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) dst[q] = src[q];
+          for (int r = 0; r < 4; ++r) {
+            a[r] = dca::f2bf(dbp[n][r]);
+            db1acc[n] += dbp[n][r];
+          }
+          dw1acc[n] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, ub, dw1acc[n], 0, 0, 0);
         }
+        // ---- basic tile (C layout: rows 4kg + r, column 16n + i) → K-blocked image
+#pragma unroll
+        for (int n = 0; n < 8; ++n) {
+          bf16x4 v4;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v4[r] = dca::f2bf(bas[n][r]);
+          *reinterpret_cast<bf16x4*>(&tw[toff(16 * n + i, 4 * kg)]) = v4;
+        }
+        __builtin_amdgcn_wave_barrier();
+        store_tile(tw, P.basic + blk, lane);
+        __builtin_amdgcn_wave_barrier();
       }
-      __builtin_amdgcn_wave_barrier();
     }
   }
-  // ---- flush ∂W1 (rows j = 16n + 4kg + r, col k = lane&15 < 10) and ∂b1
+  // ---- ∂W1 (rows j = 16n + 4kg + r, col k = lane&15 < 10) and ∂b1: waves → LDS (fixed order) → one partial
+  for (int w = 0; w < 4; ++w) {
+    __syncthreads();
+    if (wv == w) {
 #pragma unroll
-  for (int n = 0; n < 8; ++n) {
-    const int k = lane & 15;
-    if (k < kF) {
+      for (int n = 0; n < 8; ++n) {
+        const int k = lane & 15;
+        if (k < kF) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) atomicAdd(&P.dw1[(16 * n + 4 * kg + r) * kF + k], dw1acc[n][r]);
+          for (int r = 0; r < 4; ++r) wred[(16 * n + 4 * kg + r) * kF + k] += dw1acc[n][r];
+        }
+        float s = db1acc[n];
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        if (kg == 0) wred[kD * kF + 16 * n + i] += s;
+      }
     }
-    float s = db1acc[n];
-    s += __shfl_xor(s, 16, 64);
-    s += __shfl_xor(s, 32, 64);
-    if (kg == 0) atomicAdd(&P.db1[16 * n + i], s);
   }
+  __syncthreads();
+  for (int e = tid; e < kW1; e += 256) P.w1part[(size_t)blockIdx.x * kW1 + e] = wred[e];
+}
+
+// Fixed-order sum of the per-workgroup ∂W1‖∂b1 partials: block of 256 = 64 columns × 4 row phases.
+__global__ __launch_bounds__(256) void encoder_w1_reduce(const float* __restrict__ part, int nblk,
+                                                          float* __restrict__ dw1, float* __restrict__ db1) {
+  __shared__ float red[4][64];
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < kW1)
+    for (int b = ph; b < nblk; b += 4) s += part[(size_t)b * kW1 + c];
+  red[ph][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (ph == 0 && c < kW1) {
+    const float v = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+    if (c < kD * kF) dw1[c] = v;
+    else db1[c - kD * kF] = v;
+  }
+}
+
+
+// ============================================================================================================
+// ∂W_τ = Σ_k ∂emb[k]ᵀ · basic[k] over the K-blocked images (K = units of τ × rows): split-K over jobs of kJobBlk
+// 16-row blocks; a workgroup's 4 waves own the four 64×64 quadrants of the 128×128 output (16 MFMA tiles each,
+// operands straight from HBM/L2 as 16-B fragments, next k-step prefetched into registers). Each job writes its
+// partial tile-linearly; dwt_reduce sums a type's partials in job order (deterministic).
+constexpr int kJobBlk = 64;
+struct DwtJobs {
+  long long blkbase[6];
+  int nblk[6];
+  int jbase[7];
+};
+
+__device__ __forceinline__ void dwt_load(const short* __restrict__ A, const short* __restrict__ Bm, long long b,
+                                         long long bend, int mq, int nq, int lane, bf16x8 (&a)[4], bf16x8 (&bb)[4]) {
+  const long long blk = b + (lane >> 5);
+  const bool ok = blk < bend;
+  const int kh = 8 * ((lane >> 4) & 1);
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const size_t oa = ((size_t)blk * kD + 64 * mq + 16 * t + (lane & 15)) * 16 + kh;
+    const size_t ob = ((size_t)blk * kD + 64 * nq + 16 * t + (lane & 15)) * 16 + kh;
+    a[t] = ok ? *reinterpret_cast<const bf16x8*>(A + oa) : bf16x8{};
+    bb[t] = ok ? *reinterpret_cast<const bf16x8*>(Bm + ob) : bf16x8{};
+  }
+}
+
+__global__ __launch_bounds__(256, 2) void dwt_blocked_kernel(const short* __restrict__ A, const short* __restrict__ Bm,
+                                                             DwtJobs J, float* __restrict__ part) {
+  const int job = blockIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  int tau = 0;
+  while (tau < 5 && job >= J.jbase[tau + 1]) ++tau;
+  const long long b0 = J.blkbase[tau] + (long long)(job - J.jbase[tau]) * kJobBlk;
+  const long long bend = min(b0 + kJobBlk, J.blkbase[tau] + J.nblk[tau]);
+  const int mq = wv >> 1, nq = wv & 1;
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 a[4], bb[4], an[4], bn[4];
+  dwt_load(A, Bm, b0, bend, mq, nq, lane, a, bb);
+  for (long long b = b0; b < bend; b += 2) {
+    if (b + 2 < bend) dwt_load(A, Bm, b + 2, bend, mq, nq, lane, an, bn);
+#pragma unroll
+    for (int x = 0; x < 4; ++x)
+#pragma unroll
+      for (int y = 0; y < 4; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[x], bb[y], acc[x][y], 0, 0, 0);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) { a[t] = an[t]; bb[t] = bn[t]; }
+  }
+  // tile-linear partial: ((wave·16 + 4x + y)·64 + lane)·4 + r
+  float* dst = part + (size_t)job * (kD * kD) + (size_t)wv * 16 * 256;
+#pragma unroll
+  for (int x = 0; x < 4; ++x)
+#pragma unroll
+    for (int y = 0; y < 4; ++y) *reinterpret_cast<f32x4*>(dst + ((4 * x + y) * 64 + lane) * 4) = acc[x][y];
+}
+
+__global__ __launch_bounds__(256) void dwt_reduce(const float* __restrict__ part, DwtJobs J, float* __restrict__ dwt) {
+  const int tau = blockIdx.y;
+  const int xi = blockIdx.x * 256 + threadIdx.x;        // tile-linear element
+  float s = 0.f;
+  for (int j = J.jbase[tau]; j < J.jbase[tau + 1]; ++j) s += part[(size_t)j * (kD * kD) + xi];
+  const int r = xi & 3, lane = (xi >> 2) & 63, tile = (xi >> 8) & 15, wv = xi >> 12;
+  const int m = 64 * (wv >> 1) + 16 * (tile >> 2) + 4 * (lane >> 4) + r;
+  const int n = 64 * (wv & 1) + 16 * (tile & 3) + (lane & 15);
+  dwt[(size_t)tau * kD * kD + m * kD + n] = s;
 }
 
 }  // namespace
@@ -381,20 +552,62 @@ extern "C" hipError_t dca_encoder_fwd(const float* units, const float* env, cons
   return hipGetLastError();
 }
 
+namespace {
+void dwt_plan(int N, const int* counts, DwtJobs& J, int& NB) {
+  NB = (N + 15) / 16;
+  long long acc = 0;
+  int jobs = 0;
+  for (int t = 0; t < 6; ++t) {
+    J.blkbase[t] = acc;
+    J.nblk[t] = counts[t] * NB;
+    J.jbase[t] = jobs;
+    acc += J.nblk[t];
+    jobs += (J.nblk[t] + kJobBlk - 1) / kJobBlk;
+  }
+  J.jbase[6] = jobs;
+}
+}  // namespace
+
+// Workspace: ∂W1 partials ‖ K-blocked ∂emb and basic images (bf16) ‖ ∂W_τ split-K partials.
+extern "C" size_t dca_encoder_bwd_workspace(int N, int U, const int* counts) {
+  DwtJobs J;
+  int NB;
+  dwt_plan(N, counts, J, NB);
+  const size_t w1 = (size_t)((N + kRows - 1) / kRows) * kW1 * sizeof(float);
+  const size_t img = (size_t)U * NB * kD * 16 * sizeof(short);
+  const size_t parts = (size_t)J.jbase[6] * kD * kD * sizeof(float);
+  return w1 + 2 * img + parts;
+}
+
 extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const float* b1, const short* wtT,
                                       const float* dtl, const float* q, int ldq, const float* dx,
-                                      const unsigned char* arg, short* demb, short* basic, float* dw1, float* db1,
-                                      int N, int U, const int* counts, int compat, hipStream_t st) {
-  BwdParams P{units, w1, b1, wtT, dtl, q, ldq, dx, arg, demb, basic, dw1, db1, N, compat, {}, {}};
+                                      const unsigned char* arg, float* dwt, float* dw1, float* db1, void* ws,
+                                      size_t ws_bytes, int N, int U, const int* counts, int compat, hipStream_t st) {
+  if (ws_bytes < dca_encoder_bwd_workspace(N, U, counts)) return hipErrorInvalidValue;
+  DwtJobs J;
+  int NB;
+  dwt_plan(N, counts, J, NB);
+  const int nblk = (N + kRows - 1) / kRows;
+  char* p = static_cast<char*>(ws);
+  float* w1part = reinterpret_cast<float*>(p);
+  p += (size_t)nblk * kW1 * sizeof(float);
+  const size_t img = (size_t)U * NB * kD * 16;
+  short* demb = reinterpret_cast<short*>(p);
+  short* basic = demb + img;
+  float* parts = reinterpret_cast<float*>(basic + img);
+  BwdParams P{units, w1, b1, wtT, dtl, q, ldq, dx, arg, demb, basic, w1part, N, compat, {}, {}, NB};
   P.L.U = U;
   int acc = 0;
   for (int t = 0; t < 6; ++t) {
     P.L.cnt[t] = counts[t];
     P.L.off[t] = acc;
-    P.rowbase[t] = (long long)acc * N;
+    P.blkbase[t] = J.blkbase[t];
     acc += counts[t];
   }
   if (acc != U || U > 64) return hipErrorInvalidValue;
-  encoder_bwd_kernel<<<(N + kRows - 1) / kRows, 256, 0, st>>>(P);
+  encoder_bwd_kernel<<<nblk, 256, 0, st>>>(P);
+  encoder_w1_reduce<<<(kW1 + 63) / 64, 256, 0, st>>>(w1part, nblk, dw1, db1);
+  if (J.jbase[6] > 0) dwt_blocked_kernel<<<J.jbase[6], 256, 0, st>>>(demb, basic, J, parts);
+  dwt_reduce<<<dim3(kD * kD / 256, 6), 256, 0, st>>>(parts, J, dwt);
   return hipGetLastError();
 }

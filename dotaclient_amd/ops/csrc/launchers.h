@@ -32,9 +32,10 @@ hipError_t dca_heads_loss(const float* z, int ldz, const short* emb, const unsig
 hipError_t dca_encoder_fwd(const float* units, const float* env, const float* w1, const float* b1, const short* wt,
                            const float* bt, const float* we, const float* be, short* x896, short* emb,
                            unsigned char* arg, int N, int U, const int* counts, int compat, hipStream_t st);
+size_t dca_encoder_bwd_workspace(int N, int U, const int* counts);
 hipError_t dca_encoder_bwd(const float* units, const float* w1, const float* b1, const short* wtT, const float* dtl,
-                           const float* q, int ldq, const float* dx, const unsigned char* arg, short* demb,
-                           short* basic, float* dw1, float* db1, int N, int U, const int* counts, int compat,
+                           const float* q, int ldq, const float* dx, const unsigned char* arg, float* dwt, float* dw1,
+                           float* db1, void* ws, size_t ws_bytes, int N, int U, const int* counts, int compat,
                            hipStream_t st);
 
 size_t dca_lstm_team_ctl_bytes();
