@@ -283,7 +283,27 @@ class FusedPolicy:
         if getattr(self, '_perm_key', None) != key:
             from ..ops.lstm import gate_perm
             self._perm, self._perm_key = gate_perm(H, device), key
+            self._inv = torch.empty_like(self._perm)
+            self._inv[self._perm] = torch.arange(self._perm.numel(), device=self._perm.device)
         return self._perm
+
+    def gate_inv(self, H, device):
+        """Inverse of :meth:`gate_perm` (unit-major gate rows → PyTorch gate-major rows), cached."""
+        self.gate_perm(H, device)
+        return self._inv
+
+    def type_segments(self, device):
+        """(U, 6) 0/1 matrix mapping unit slots to their unit type (sums pointer gradients per type), cached."""
+        key = str(device)
+        if getattr(self, '_seg_key', None) != key:
+            counts = list(self.cfg.layout.counts)
+            seg = torch.zeros(sum(counts), 6, device=device)
+            off = 0
+            for t, cnt in enumerate(counts):
+                seg[off:off + cnt, t] = 1.0
+                off += cnt
+            self._seg, self._seg_key = seg, key
+        return self._seg
 
     def refresh(self):
         self.params = [p for _, p in self.policy.named_parameters()]

@@ -44,6 +44,11 @@ def _bf(t):
     return t.detach().to(torch.bfloat16)
 
 
+def _acc(a, b):
+    """Accumulate a per-chunk gradient: the first chunk's tensor is used as is (no zero fill + add)."""
+    return b if a is None else a.add_(b)
+
+
 def chunk_bounds(S: int, chunks: int):
     c = max(1, min(chunks, S))
     edges = [round(i * S / c) for i in range(c + 1)]
@@ -79,25 +84,26 @@ class PipelinedPolicyLoss(torch.autograd.Function):
         perm = fp.gate_perm(H, dev)
         wih16 = _bf(P['rnn.weight_ih_l0'])[perm].contiguous()
         whh16 = _bf(P['rnn.weight_hh_l0'])
-        bias_p = (P['rnn.bias_ih_l0'].detach() + P['rnn.bias_hh_l0'].detach())[perm]
+        bias_p = (P['rnn.bias_ih_l0'].detach() + P['rnn.bias_hh_l0'].detach())[perm].contiguous()
         wcat, bcat = fp.head_cat(P)
         wcat16 = wcat.to(torch.bfloat16)
         # ---- encoder, pre-RNN, input projection over all rows (row-parallel, fast)
         x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs))
         x = torch.relu(_mm(x896, wpre16.t()) + P['affine_pre_rnn.bias'].detach())
         x16 = x.to(torch.bfloat16)
-        xp4 = (_mm(x16, wih16.t()) + bias_p).view(S, B, H, 4)
+        xp4 = _mm(x16, wih16.t()).view(S, B, H, 4)          # the recurrence kernel adds the bias (bias4)
         hs16 = torch.empty(S, B, H, dtype=torch.bfloat16, device=dev)
         cs = torch.empty(S, B, H, device=dev)
         gates4 = torch.empty(S, B, H, 4, device=dev)
-        dxh = torch.empty(S, B, H, device=dev)
-        z = torch.empty(N, LDZ, device=dev)
-        dtl = torch.empty(N, U, device=dev)
-        logp = torch.empty(N, device=dev)
-        dWcat = torch.zeros(LDZ, H, device=dev)
-        dbcat = torch.zeros(LDZ, device=dev)
-        parts = []
         spans = chunk_bounds(S, fp.chunks)
+        one = len(spans) == 1            # single chunk: outputs are used as produced (no staging copies)
+        if not one:
+            dxh = torch.empty(S, B, H, device=dev)
+            z = torch.empty(N, LDZ, device=dev)
+            dtl = torch.empty(N, U, device=dev)
+            logp = torch.empty(N, device=dev)
+        dWcat = dbcat = None
+        parts = []
         algo = 0 if lc.algo == 'ppo' else 1
         # ---- forward recurrence on stream L, heads (+ heads backward) per chunk on the main stream
         ready = torch.cuda.Event()
@@ -110,7 +116,7 @@ class PipelinedPolicyLoss(torch.autograd.Function):
         with torch.cuda.stream(sL):
             for t0, t1 in spans:
                 o = team_fwd(C, xp4[t0:t1], whh16, h_c, c_c, fp.err, False, time_major=True,
-                             hs_out=hs16[t0:t1], cs_out=cs[t0:t1], gates_out=gates4[t0:t1])
+                             hs_out=hs16[t0:t1], cs_out=cs[t0:t1], gates_out=gates4[t0:t1], bias4=bias_p)
                 h_c, c_c = o[4], o[5]
                 e = torch.cuda.Event()
                 e.record(sL)
@@ -120,40 +126,30 @@ class PipelinedPolicyLoss(torch.autograd.Function):
             r0, r1 = t0 * B, t1 * B
             xh = hs16[t0:t1].view(-1, H)
             zc = _mm(xh, wcat16.t()) + bcat
-            z[r0:r1].copy_(zc)
             dz, dtl_c, part, lp = C.heads_loss(zc, emb[r0:r1], act_t[r0:r1], msk_t[r0:r1], adv_t[r0:r1],
                                                ret_t[r0:r1], lpo_t[r0:r1], nret_t[r0:r1], norms, algo, False,
                                                S, B, float(lc.clip_eps), float(lc.entropy_coef), float(lc.vf_coef))
-            dtl[r0:r1].copy_(dtl_c)
-            logp[r0:r1].copy_(lp)
             parts.append(part.sum(0))
             dz16 = dz.to(torch.bfloat16)
-            dWcat += _mm(dz16.t(), xh)
-            dbcat += dz.sum(0)
-            dxh[t0:t1].copy_(_mm(dz16, wcat16).view(t1 - t0, B, H))
+            dWcat = _acc(dWcat, _mm(dz16.t(), xh))
+            dbcat = _acc(dbcat, dz.sum(0))
+            if one:
+                z, dtl, logp = zc, dtl_c, lp
+                dxh = _mm(dz16, wcat16).view(S, B, H)
+            else:
+                z[r0:r1].copy_(zc)
+                dtl[r0:r1].copy_(dtl_c)
+                logp[r0:r1].copy_(lp)
+                dxh[t0:t1].copy_(_mm(dz16, wcat16).view(t1 - t0, B, H))
         heads_done = torch.cuda.Event()
         heads_done.record(main)
         # ---- backward recurrence on stream L (reverse chunks), weight gradients per chunk on the main stream
         grads: Dict[str, torch.Tensor] = {}
         fp.split_head_grads(dWcat, dbcat, grads)
-        dgates4 = torch.empty(S, B, H, 4, device=dev)
-        dWhh = torch.zeros(4 * H, H, device=dev)
-        dWih = torch.zeros(4 * H, x16.shape[1], device=dev)
-        db = torch.zeros(4 * H, device=dev)
-        dWpre = torch.zeros_like(P['affine_pre_rnn.weight'], dtype=torch.float32)
-        dbpre = torch.zeros(dWpre.shape[0], device=dev)
-        dw1 = torch.zeros(128, 10, device=dev)
-        db1 = torch.zeros(128, device=dev)
-        dWt = torch.zeros(6, 128, 128, device=dev)
-        dbt = torch.zeros(6, 128, device=dev)
-        dWe = torch.zeros_like(we, dtype=torch.float32)
-        dbe = torch.zeros_like(be, dtype=torch.float32)
+        dgates16 = torch.empty(S, B, H, 4, dtype=torch.bfloat16, device=dev)   # ∂gates straight from the kernel
+        dWhh = dWih = db = dWpre = dbpre = dw1 = db1 = dWt = dbt = dWe = dbe = None
         wtT16 = wt16.transpose(1, 2).contiguous()
-        seg = torch.zeros(U, 6, device=dev)
-        off = 0
-        for t, cnt in enumerate(counts):
-            seg[off:off + cnt, t] = 1.0
-            off += cnt
+        seg = fp.type_segments(dev)
         h016 = h0.to(torch.bfloat16)
         sL.wait_event(heads_done)
         dh_n = dc_n = None
@@ -162,8 +158,9 @@ class PipelinedPolicyLoss(torch.autograd.Function):
             for t0, t1 in reversed(spans):
                 cinit = c0.contiguous() if t0 == 0 else cs[t0 - 1]
                 o = team_bwd(C, dxh[t0:t1], gates4[t0:t1], cs[t0:t1], cinit, dh_n, dc_n, whh16, fp.err,
-                             time_major=True, dg_out=dgates4[t0:t1])
+                             time_major=True, dg_out=dgates16[t0:t1], dg_bf16=True, want_dbias=True)
                 dh_n, dc_n = o[1], o[2]
+                db = _acc(db, o[3])
                 e = torch.cuda.Event()
                 e.record(sL)
                 bwd_done.append(e)
@@ -171,31 +168,29 @@ class PipelinedPolicyLoss(torch.autograd.Function):
             main.wait_event(done)
             r0, r1 = t0 * B, t1 * B
             n = r1 - r0
-            dg = dgates4[t0:t1].view(n, 4 * H)
-            dG16 = dg.to(torch.bfloat16)
+            dG16 = dgates16[t0:t1].view(n, 4 * H)
             hprev = hs16[t0 - 1:t1 - 1].view(n, H) if t0 > 0 else torch.cat(
                 [h016.unsqueeze(0), hs16[0:t1 - 1]], 0).view(n, H)
-            dWhh += _mm(dG16.t(), hprev)
-            dWih += _mm(dG16.t(), x16[r0:r1])
-            db += dg.sum(0)
+            dWhh = _acc(dWhh, _mm(dG16.t(), hprev))
+            dWih = _acc(dWih, _mm(dG16.t(), x16[r0:r1]))
             dpre = _mm(dG16, wih16) * (x[r0:r1] > 0)
             dpre16 = dpre.to(torch.bfloat16)
-            dWpre += _mm(dpre16.t(), x896[r0:r1])
-            dbpre += dpre.sum(0)
+            dWpre = _acc(dWpre, _mm(dpre16.t(), x896[r0:r1]))
+            dbpre = _acc(dbpre, dpre.sum(0))
             dx896 = _mm(dpre16, wpre16)
             q = z[r0:r1, :128]
             dwt_c, dw1_c, db1_c = C.encoder_bwd(units_t[r0:r1], w1, b1, wtT16, dtl[r0:r1], z[r0:r1],
                                                       dx896, arg[r0:r1], counts, bool(cfg.compat_bugs))
-            dw1 += dw1_c
-            db1 += db1_c
-            dbt += tn_splitk((dtl[r0:r1] @ seg).contiguous(), q.contiguous()) + dx896[:, 128:].reshape(n, 6, 128).sum(0)
-            dWt += dwt_c
+            dw1 = _acc(dw1, dw1_c)
+            db1 = _acc(db1, db1_c)
+            dbt = _acc(dbt, tn_splitk((dtl[r0:r1] @ seg).contiguous(), q.contiguous())
+                       + dx896[:, 128:].reshape(n, 6, 128).sum(0))
+            dWt = _acc(dWt, dwt_c)
             env_c = env_t[r0:r1]
             de = dx896[:, :128] * ((env_c @ we.t() + be) > 0)
-            dWe += de.t() @ env_c
-            dbe += de.sum(0)
-        inv = torch.empty_like(perm)
-        inv[perm] = torch.arange(perm.numel(), device=dev)
+            dWe = _acc(dWe, de.t() @ env_c)
+            dbe = _acc(dbe, de.sum(0))
+        inv = fp.gate_inv(H, dev)
         grads['rnn.weight_hh_l0'] = dWhh[inv]
         grads['rnn.weight_ih_l0'] = dWih[inv]
         grads['rnn.bias_ih_l0'] = db[inv]

@@ -147,7 +147,8 @@ std::vector<torch::Tensor> lstm_team_fwd(torch::Tensor xp4, torch::Tensor whh, t
                                          torch::Tensor err, torch::Tensor ctl, bool want_f32_h,
                                          c10::optional<torch::Tensor> trace,
                                          bool time_major, c10::optional<torch::Tensor> hs_out,
-                                         c10::optional<torch::Tensor> cs_out, c10::optional<torch::Tensor> gates_out) {
+                                         c10::optional<torch::Tensor> cs_out, c10::optional<torch::Tensor> gates_out,
+                                         c10::optional<torch::Tensor> bias4) {
   CHECK_F32(xp4); CHECK_BF16(whh); CHECK_F32(h0); CHECK_F32(c0); CHECK_I32(err); check_ctl(ctl);
   TORCH_CHECK(xp4.dim() == 4 && xp4.size(3) == 4, "xp4 must be (B,S,H,4) or (S,B,H,4)");
   const int B = time_major ? xp4.size(1) : xp4.size(0), S = time_major ? xp4.size(0) : xp4.size(1);
@@ -163,13 +164,20 @@ std::vector<torch::Tensor> lstm_team_fwd(torch::Tensor xp4, torch::Tensor whh, t
   auto gates4 = out_or_new(gates_out, {d0, d1, H, 4}, f32, "gates_out");
   auto hn = torch::empty({B, H}, f32);
   auto cn = torch::empty({B, H}, f32);
+  const float* bias_p = nullptr;
+  if (bias4.has_value() && bias4->defined()) {
+    CHECK_F32((*bias4));
+    TORCH_CHECK(bias4->numel() == 4 * H, "bias4 must hold 4H floats (unit-major)");
+    bias_p = ptr<float>(*bias4);
+  }
   const size_t wsb = dca_lstm_team_workspace(B, H, 0);
   auto ws = torch::empty({(int64_t)wsb}, f32.dtype(at::kByte));
   hip_check(dca_lstm_team_fwd(ptr<float>(xp4), ptr<short>(whh), ptr<float>(h0), ptr<float>(c0), ptr<short>(hs),
                               want_f32_h ? ptr<float>(hsf) : nullptr, ptr<float>(cs), ptr<float>(gates4),
                               ptr<float>(hn), ptr<float>(cn), ctl.data_ptr(), ws.data_ptr(), wsb,
                               ptr<unsigned>(err), B, S, H, time_major ? 1 : 0, cur_stream(),
-                              (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr),
+                              (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr,
+                              bias_p),
             "dca_lstm_team_fwd");
   return {hs, want_f32_h ? hsf : hs, cs, gates4, hn, cn};
 }
@@ -178,7 +186,7 @@ std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4
                                          torch::Tensor c0, c10::optional<torch::Tensor> dhn,
                                          c10::optional<torch::Tensor> dcn, torch::Tensor whh, torch::Tensor err,
                                          torch::Tensor ctl, c10::optional<torch::Tensor> trace, bool time_major,
-                                         c10::optional<torch::Tensor> dg_out) {
+                                         c10::optional<torch::Tensor> dg_out, bool dg_bf16, bool want_dbias) {
   CHECK_F32(dhs); CHECK_F32(gates4); CHECK_F32(cs); CHECK_F32(c0); CHECK_BF16(whh); CHECK_I32(err);
   check_ctl(ctl);
   const int B = time_major ? dhs.size(1) : dhs.size(0), S = time_major ? dhs.size(0) : dhs.size(1);
@@ -194,16 +202,23 @@ std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4
   if (dhn.has_value() && dhn->defined()) { CHECK_F32((*dhn)); dhn_p = ptr<float>(*dhn); }
   if (dcn.has_value() && dcn->defined()) { CHECK_F32((*dcn)); dcn_p = ptr<float>(*dcn); }
   auto f32 = dhs.options();
-  auto dgates4 = out_or_new(dg_out, {dhs.size(0), dhs.size(1), H, 4}, f32, "dg_out");
+  // ∂gates in f32, or in bf16 (half the bytes; what the weight-gradient GEMMs consume)
+  auto dgates4 = out_or_new(dg_out, {dhs.size(0), dhs.size(1), H, 4}, dg_bf16 ? f32.dtype(at::kBFloat16) : f32,
+                            "dg_out");
   auto dh0 = torch::empty({B, H}, f32);
   auto dc0 = torch::empty({B, H}, f32);
+  // per-chain bias-gradient partials (Σ over the chain's rows and steps), summed in chain order below
+  torch::Tensor dbp = want_dbias ? torch::empty({dca_lstm_team_chains(B), 4 * H}, f32) : torch::Tensor();
   const size_t wsb = dca_lstm_team_workspace(B, H, 1);
   auto ws = torch::empty({(int64_t)wsb}, f32.dtype(at::kByte));
   hip_check(dca_lstm_team_bwd(ptr<float>(dhs), ptr<float>(gates4), ptr<float>(cs), ptr<float>(c0), dhn_p, dcn_p,
-                              ptr<short>(whh), ptr<float>(dgates4), ptr<float>(dh0), ptr<float>(dc0), ctl.data_ptr(),
-                              ws.data_ptr(), wsb, ptr<unsigned>(err), B, S, H, time_major ? 1 : 0, cur_stream(),
-                              (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr),
+                              ptr<short>(whh), dg_bf16 ? nullptr : ptr<float>(dgates4), ptr<float>(dh0),
+                              ptr<float>(dc0), ctl.data_ptr(), ws.data_ptr(), wsb, ptr<unsigned>(err), B, S, H,
+                              time_major ? 1 : 0, cur_stream(),
+                              (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr,
+                              dg_bf16 ? ptr<short>(dgates4) : nullptr, want_dbias ? ptr<float>(dbp) : nullptr),
             "dca_lstm_team_bwd");
+  if (want_dbias) return {dgates4, dh0, dc0, dbp.sum(0)};
   return {dgates4, dh0, dc0};
 }
 
@@ -356,11 +371,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_team_fwd", &lstm_team_fwd, "XCD-team persistent LSTM forward (L2-local hand-off), unit-major gates",
         py::arg("xp4"), py::arg("whh"), py::arg("h0"), py::arg("c0"), py::arg("err"), py::arg("ctl"),
         py::arg("want_f32_h"), py::arg("trace") = py::none(), py::arg("time_major") = false, py::arg("hs_out") = py::none(),
-        py::arg("cs_out") = py::none(), py::arg("gates_out") = py::none());
+        py::arg("cs_out") = py::none(), py::arg("gates_out") = py::none(), py::arg("bias4") = py::none());
   m.def("lstm_team_bwd", &lstm_team_bwd, "XCD-team persistent LSTM backward (L2-local reduce-scatter)",
         py::arg("dhs"), py::arg("gates4"), py::arg("cs"), py::arg("c0"), py::arg("dhn"), py::arg("dcn"),
         py::arg("whh"), py::arg("err"), py::arg("ctl"), py::arg("trace") = py::none(),
-        py::arg("time_major") = false, py::arg("dg_out") = py::none());
+        py::arg("time_major") = false, py::arg("dg_out") = py::none(), py::arg("dg_bf16") = false,
+        py::arg("want_dbias") = false);
   m.def("sample_actions", &sample_actions, "fused masked hierarchical Gumbel-max action sampling (actor)");
   m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)", py::arg("gates"),
         py::arg("h"), py::arg("c"), py::arg("h16"), py::arg("active") = py::none());

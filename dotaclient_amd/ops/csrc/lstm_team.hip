@@ -201,7 +201,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
     const float* __restrict__ c0, short* __restrict__ hs, float* __restrict__ hsf, float* __restrict__ cs,
     float* __restrict__ gates4, float* __restrict__ hn, float* __restrict__ cn, unsigned long long* xg_all,
     TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st, unsigned long long* trace,
-    int knobs) {
+    int knobs, const float* __restrict__ bias4) {
   constexpr int H = 128 * KS;
   constexpr int U = H / kT;             // units per workgroup (4·KS)
   constexpr int NTILE = U / 4;          // 16-column MFMA tiles per workgroup (= KS)
@@ -239,6 +239,9 @@ __device__ __forceinline__ void lstm_team_fwd_body(
   // elementwise mapping after the 4×4 transpose: lane → (row 4·kg + (col&3) [+16·mt], unit j0 + 4·wv + col/4)
   const int erow = 4 * kg + (col & 3);
   const int eunit = j0 + 4 * wv + (col >> 2);
+  // folded LSTM bias (b_ih + b_hh, unit-major): xp4 may then be the bare input projection
+  const dca::f32x4 bv = (bias4 && mfma_wave) ? *reinterpret_cast<const dca::f32x4*>(bias4 + eunit * 4)
+                                             : dca::f32x4{0.f, 0.f, 0.f, 0.f};
 
   unsigned spins = 0;
   for (unsigned iter = 0;; ++iter) {
@@ -258,7 +261,8 @@ __device__ __forceinline__ void lstm_team_fwd_body(
     for (int t = 0; t < S; ++t) {
       const int par = t & 1;
       TSTAMP(0);
-      // ---- prefetch this step's input projection (one 16-B vector per owned (row, unit))
+      // ---- prefetch this step's input projection (one 16-B vector per owned (row, unit)). Loading it one step
+      // ahead instead measured slower (2.11 vs 1.94 µs per step at B=8, H=512).
       dca::f32x4 xv[MT];
       if (mfma_wave) {
 #pragma unroll
@@ -346,7 +350,9 @@ __device__ __forceinline__ void lstm_team_fwd_body(
             gq3 = qs == 3 ? got : gq3;
           }
           const int b = mt * 16 + erow;
-          const float pi = gq0 + xv[mt][0], pf = gq1 + xv[mt][1], pg = gq2 + xv[mt][2], po = gq3 + xv[mt][3];
+          // (bias added here, at the use: an add right after the prefetch would wait out the load before the gather)
+          const float pi = gq0 + (xv[mt][0] + bv[0]), pf = gq1 + (xv[mt][1] + bv[1]), pg = gq2 + (xv[mt][2] + bv[2]),
+                      po = gq3 + (xv[mt][3] + bv[3]);
           const float ig = dca::sigmoidf_(pi), fg = dca::sigmoidf_(pf), gg = dca::tanhf_(pg), og = dca::sigmoidf_(po);
           const float c = fg * creg[mt] + ig * gg;
           const float hv = og * dca::tanhf_(c);
@@ -405,7 +411,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
     const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
     const short* __restrict__ whh, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
     i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
-    unsigned long long* trace) {
+    unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart) {
   constexpr int H = 128 * KS;
   constexpr int U = H / kT;             // 4·KS units per workgroup (MFMA N, zero-padded to 16)
   constexpr int KW = H;                 // K (= 4H gate columns) per wave
@@ -415,6 +421,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
   constexpr int NPAIR = (RB * U + kThreads - 1) / kThreads;
   __shared__ short dgl[RB][GP];
   __shared__ float red[4][RB][17];
+  __shared__ float dbs[RB * U * 4];     // per-(row, unit, gate) bias-gradient sums of a chain
   __shared__ int sh_int;
   __shared__ unsigned sh_epoch;
 
@@ -453,6 +460,9 @@ __device__ __forceinline__ void lstm_team_bwd_body(
     const int B = min(Bc, Btot - b0);
     const unsigned tagbase = make_tagbase(epoch, iter);
     float dcarry[NPAIR];
+    dca::f32x4 dsum[NPAIR];               // Σ_t ∂gates of the owned pairs (bias gradient)
+#pragma unroll
+    for (int i = 0; i < NPAIR; ++i) dsum[i] = dca::f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < NPAIR; ++i) {
       const int pi = tid + kThreads * i;
@@ -566,13 +576,29 @@ __device__ __forceinline__ void lstm_team_bwd_body(
           const unsigned p23 = (unsigned)(unsigned short)dca::f2bf(d_g) | ((unsigned)(unsigned short)dca::f2bf(d_o) << 16);
           __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)p01, tg, (int)p23, tg}, ws, (b * H + j0 + u) * 16, 0, kPlain);
           const size_t bt = (size_t)(b0 + b) * sb + (size_t)t * st;
-          *reinterpret_cast<dca::f32x4*>(dgates4 + (bt * H + j0 + u) * 4) = dca::f32x4{d_i, d_f, d_g, d_o};
+          if (dg16) *reinterpret_cast<u32x2*>(dg16 + (bt * H + j0 + u) * 4) = u32x2{p01, p23};
+          else *reinterpret_cast<dca::f32x4*>(dgates4 + (bt * H + j0 + u) * 4) = dca::f32x4{d_i, d_f, d_g, d_o};
+          dsum[i] += dca::f32x4{d_i, d_f, d_g, d_o};
           if (t == 0) dc0[(size_t)(b0 + b) * H + j0 + u] = dcarry[i];
         }
       }
       TSTAMPB(6);
     }
     if (sh_int == -2) return;
+    if (dbpart) {
+      // bias gradient of this chain for the owned units: Σ over rows (fixed order) of the per-pair sums
+#pragma unroll
+      for (int i = 0; i < NPAIR; ++i) {
+        const int pi = tid + kThreads * i;
+        if (pi < B * U) *reinterpret_cast<dca::f32x4*>(&dbs[pi * 4]) = dsum[i];
+      }
+      __syncthreads();
+      for (int o = tid; o < U * 4; o += kThreads) {
+        float acc = 0.f;
+        for (int b = 0; b < B; ++b) acc += dbs[b * U * 4 + o];
+        dbpart[(size_t)chain * 4 * H + 4 * j0 + o] = acc;
+      }
+    }
     __syncthreads();
     if (tid == 0) add_agent(&ctl->done[team], 1u);
   }
@@ -585,9 +611,9 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
     const float* __restrict__ c0, short* __restrict__ hs, float* __restrict__ hsf, float* __restrict__ cs,
     float* __restrict__ gates4, float* __restrict__ hn, float* __restrict__ cn, unsigned long long* xg_all,
     TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st, unsigned long long* trace,
-    int knobs) {
+    int knobs, const float* __restrict__ bias4) {
   lstm_team_fwd_body<MT, KS>(xp4, whh, h0, c0, hs, hsf, cs, gates4, hn, cn, xg_all, ctl, err, Btot, Bc, nch, S, sb,
-                             st, trace, knobs);
+                             st, trace, knobs, bias4);
   team_exit(ctl);
 }
 
@@ -597,9 +623,9 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
     const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
     const short* __restrict__ whh, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
     i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
-    unsigned long long* trace) {
+    unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart) {
   lstm_team_bwd_body<MT, KS>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, dh0, dc0, xg_all, ctl, err, Btot, Bc, nch,
-                             S, sb, st, trace);
+                             S, sb, st, trace, dg16, dbpart);
   team_exit(ctl);
 }
 
@@ -635,6 +661,13 @@ inline void plan(int B, int& nch, int& Bc, int& MT) {
 // Workspace bytes (control block + per-team exchange buffers) for a launch of (B, H).
 extern "C" size_t dca_lstm_team_ctl_bytes() { return 256; }
 
+// Sequence chains a launch of B sequences is split into (rows of the backward's bias-gradient partials).
+extern "C" int dca_lstm_team_chains(int B) {
+  int nch, Bc, MT;
+  plan(B, nch, Bc, MT);
+  return nch;
+}
+
 // Exchange-buffer bytes (per-team hand-off rings) for a launch of (B, H). Not zeroed: tags carry the epoch.
 extern "C" size_t dca_lstm_team_workspace(int B, int H, int backward) {
   int nch, Bc, MT;
@@ -646,7 +679,8 @@ extern "C" size_t dca_lstm_team_workspace(int B, int H, int backward) {
 extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const short* whh, const float* h0, const float* c0,
                                         short* hs, float* hsf, float* cs, float* gates4, float* hn, float* cn,
                                         void* ctl_mem, void* ws, size_t ws_bytes, unsigned* err, int B, int S, int H,
-                                        int time_major, hipStream_t stream, unsigned long long* trace) {
+                                        int time_major, hipStream_t stream, unsigned long long* trace,
+                                        const float* bias4) {
   if (B < 1 || S < 1 || S >= 65535 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
   if (ws_bytes < dca_lstm_team_workspace(B, H, 0) || ctl_mem == nullptr) return hipErrorInvalidValue;
   int nch, Bc, MT;
@@ -658,7 +692,7 @@ extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const short* whh, cons
 #define DCA_F(mt, ks)                                                                                           \
   (lstm_team_fwd_kernel<mt, ks><<<kMaxTeams * kT, kThreads, 0, stream>>>(xp4, whh, h0, c0, hs, hsf, cs, gates4, \
                                                                           hn, cn, xg, ctl, err, B, Bc, nch, S, sb, \
-                                                                          st, trace, team_knobs()),                \
+                                                                          st, trace, team_knobs(), bias4),         \
    hipGetLastError())
   DCA_TEAM_DISPATCH(MT, KS, DCA_F)
 #undef DCA_F
@@ -668,8 +702,9 @@ extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, c
                                         const float* dhn, const float* dcn, const short* whh, float* dgates4,
                                         float* dh0, float* dc0, void* ctl_mem, void* ws, size_t ws_bytes,
                                         unsigned* err, int B, int S, int H, int time_major, hipStream_t stream,
-                                        unsigned long long* trace) {
+                                        unsigned long long* trace, short* dg16, float* dbpart) {
   if (B < 1 || S < 1 || S >= 65534 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
+  if (dgates4 == nullptr && dg16 == nullptr) return hipErrorInvalidValue;
   if (ws_bytes < dca_lstm_team_workspace(B, H, 1) || ctl_mem == nullptr) return hipErrorInvalidValue;
   int nch, Bc, MT;
   plan(B, nch, Bc, MT);
@@ -680,7 +715,7 @@ extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, c
 #define DCA_B(mt, ks)                                                                                              \
   (lstm_team_bwd_kernel<mt, ks><<<kMaxTeams * kT, kThreads, 0, stream>>>(dhs, gates4, cs, c0, dhn, dcn, whh,      \
                                                                           dgates4, dh0, dc0, xb, ctl, err, B, Bc,  \
-                                                                          nch, S, sb, st, trace),                  \
+                                                                          nch, S, sb, st, trace, dg16, dbpart),    \
    hipGetLastError())
   DCA_TEAM_DISPATCH(MT, KS, DCA_B)
 #undef DCA_B

@@ -79,3 +79,32 @@ def test_team_many_chains_queue(gpu_ops, monkeypatch):
     torch.cuda.synchronize()
     assert int(err.item()) == 0
     assert _rel(out_t, out_r) < 1e-2
+
+
+@pytest.mark.parametrize('B,S,H,tm', [(8, 40, 512, True), (20, 17, 256, False), (3, 25, 128, True)])
+def test_team_folded_bias_bf16_dgates_and_bias_grad(gpu_ops, B, S, H, tm):
+    """Folded bias (bias4) == bias added to xp4; bf16 ∂gates == f32 ∂gates rounded; the in-kernel bias gradient
+    == Σ over rows and steps of the f32 ∂gates."""
+    from dotaclient_amd.ops.lstm import team_bwd, team_fwd
+    C = gpu_ops
+    torch.manual_seed(7)
+    shp = (S, B, H, 4) if tm else (B, S, H, 4)
+    xp = torch.randn(*shp, device='cuda') * 0.5
+    bias = torch.randn(4 * H, device='cuda') * 0.3
+    whh = (torch.randn(4 * H, H, device='cuda') * 0.05).to(torch.bfloat16)
+    h0 = torch.randn(B, H, device='cuda') * 0.1
+    c0 = torch.randn(B, H, device='cuda') * 0.1
+    err = torch.zeros(1, dtype=torch.int32, device='cuda')
+    ref = team_fwd(C, xp + bias.view(H, 4), whh, h0, c0, err, True, time_major=tm)
+    got = team_fwd(C, xp, whh, h0, c0, err, True, time_major=tm, bias4=bias)
+    torch.testing.assert_close(got[1], ref[1], atol=1e-5, rtol=1e-5)
+    torch.testing.assert_close(got[3], ref[3], atol=1e-5, rtol=1e-5)
+    dh = torch.randn(*shp[:3], device='cuda')
+    g32 = team_bwd(C, dh, ref[3], ref[2], c0, None, None, whh, err, time_major=tm)
+    g16 = team_bwd(C, dh, ref[3], ref[2], c0, None, None, whh, err, time_major=tm, dg_bf16=True, want_dbias=True)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0
+    assert g16[0].dtype == torch.bfloat16
+    torch.testing.assert_close(g16[0].float(), g32[0].to(torch.bfloat16).float(), atol=1e-6, rtol=0)
+    torch.testing.assert_close(g16[1], g32[1], atol=1e-6, rtol=1e-6)
+    torch.testing.assert_close(g16[3], g32[0].sum((0, 1)).reshape(-1), atol=1e-3, rtol=1e-4)
