@@ -76,6 +76,7 @@ class OptimizerConfig:
     replay_gb: float = 0.0             # on-HBM replay budget (GB); 0 with replay_capacity 0 = reference behaviour
     replay_capacity: int = 0           # sequences (overrides replay_gb)
     replay_recent: int = 0             # sample from the newest N sequences (0 = whole buffer)
+    ingest: str = 'auto'               # 'device' (HIP return/GAE scan over the uploaded rollouts) | 'host' | 'auto'
 
 
 class Sequence:
@@ -97,6 +98,7 @@ class Sequence:
 
 class DotaOptimizer:
     SPEED_KEY = 'steps per s'
+    MAX_TEAMS = 16
 
     def __init__(self, cfg: OptimizerConfig, broker, checkpoint: Optional[bool] = None):
         self.cfg = cfg
@@ -113,6 +115,7 @@ class DotaOptimizer:
         self.policy_cfg = get_config(cfg.model)
         self.policy = Policy(self.policy_cfg)
         self.running = RunningMeanStd(0.99)
+        self.team_keys: Dict[int, int] = {}     # team_id -> row of the device EMA state
         self.iteration_start = 1
         self.writer = MetricsWriter(cfg.log_dir if self.checkpoint else None)
         self.timer = StageTimer()
@@ -133,6 +136,13 @@ class DotaOptimizer:
         if trainer_state is not None:
             self.learner.load_state_dict(trainer_state['learner'])
             self.running.load_state_dict(trainer_state['running'])
+        self.ingest = cfg.ingest if cfg.ingest != 'auto' else ('device' if self.device.type == 'cuda' else 'host')
+        # per-team EMA(0.99) reward statistics as device state (mean, std, initialised) for the device ingest path
+        self.ema = torch.zeros(self.MAX_TEAMS, 3, device=self.device)
+        for team in self.running.mean:
+            if self.running.mean[team] is not None:
+                k = self._team_key(team)
+                self.ema[k] = torch.tensor([self.running.mean[team], self.running.std[team], 1.0])
         # every rank starts from rank 0's iteration (reference workers restart at 1, §2.10-7)
         if pdist.is_distributed():
             t = torch.tensor([self.iteration_start], device=self.device if self.device.type == 'cuda' else 'cpu')
@@ -208,6 +218,94 @@ class DotaOptimizer:
                                  valid[a:b]))
         return seqs
 
+    def _team_key(self, team: int) -> int:
+        k = self.team_keys.get(team)
+        if k is None:
+            if len(self.team_keys) >= self.MAX_TEAMS:
+                raise ValueError(f'more than {self.MAX_TEAMS} distinct team ids')
+            k = self.team_keys[team] = len(self.team_keys)
+        return k
+
+    def _ingest_device(self, rollouts: List[Rollout], n_keep: int) -> Dict[str, torch.Tensor]:
+        """Device ingest: every rollout of the iteration is padded to a multiple of ``seq_len`` and concatenated on
+        the host into one pinned buffer per field (a single upload each); returns / GAE and the per-team EMA
+        normalisation run as the HIP segmented reverse scan (``ops/csrc/scan.hip``) over all rollouts at once; the
+        learner's sequences are a reshape of the result. Same numbers as :meth:`experiences_from_rollout` +
+        :meth:`_to_device` (the host path), without per-rollout numpy work or per-sequence stacking."""
+        from ..ops.scan import compute_returns
+        cfg = self.cfg
+        S = cfg.seq_len
+        dev = self.device
+        lens = [r.length for r in rollouts]
+        off = np.zeros(len(rollouts) + 1, np.int64)
+        off[1:] = np.cumsum([-(-T // S) * S for T in lens])
+        L = int(off[-1])
+        pin = dev.type == 'cuda'
+
+        def cat(name, tail, dtype, conv=None):
+            buf = torch.zeros((L,) + tuple(tail), dtype=dtype, pin_memory=pin)
+            bn = buf.numpy()
+            for r, a in zip(rollouts, off[:-1]):
+                x = getattr(r, name)
+                if x is not None:
+                    bn[a:a + len(x)] = x if conv is None else conv(x)
+            return buf.to(dev, non_blocking=True)
+        r0 = rollouts[0]
+        A = r0.actions.shape[1]
+        U = r0.units.shape[1]
+        d = {'env': cat('env', (3,), torch.float32), 'units': cat('units', (U, 10), torch.float32),
+             'actions': cat('actions', (A,), torch.uint8), 'masks': cat('masks', (A,), torch.uint8),
+             'logp_old': cat('logp', (), torch.float32)}
+        rew = cat('rewards', (r0.rewards.shape[1],), torch.float32)
+        gae_mode = cfg.algo == 'ppo' and all(r.values is not None for r in rollouts)
+        vals = cat('values', (), torch.float32) if gae_mode else None
+        valid = torch.zeros(L, dtype=torch.float32, pin_memory=pin)
+        for T, a in zip(lens, off[:-1]):
+            valid[a:a + T] = 1.0
+        d['valid'] = valid.to(dev, non_blocking=True)
+        keys = [self._team_key(r.team_id) for r in rollouts]
+        out = compute_returns(rew, vals, off.astype(np.int32), lens, [r.bootstrap_value for r in rollouts],
+                              [bool(r.done) for r in rollouts], keys, self.ema, 'gae' if gae_mode else 'discount',
+                              gamma=cfg.gamma, lam=cfg.gae_lambda, factor=self.running.factor)
+        d['ret'], d['adv'] = out['ret'], out['adv']
+        d['norm_ret'] = out['norm'] if not gae_mode else out['adv']
+        n_rows = n_keep * S
+        d = {k: v[:n_rows].reshape((n_keep, S) + tuple(v.shape[1:])) for k, v in d.items()}
+        if self.policy.is_recurrent:
+            H = self.policy_cfg.hidden
+            hid = np.zeros((n_keep, 2, H), np.float32)
+            i = 0
+            for r, T in zip(rollouts, lens):
+                for s in range(-(-T // S)):
+                    if i >= n_keep:
+                        break
+                    a = s * S
+                    if r.hiddens is not None and r.hidden_stride and a % r.hidden_stride == 0 \
+                            and a // r.hidden_stride < len(r.hiddens):
+                        hid[i] = r.hiddens[a // r.hidden_stride]
+                    i += 1
+            h = torch.from_numpy(hid)
+            h = (h.pin_memory() if pin else h).to(dev, non_blocking=True)
+            d['h0'], d['c0'] = h[:, 0].contiguous(), h[:, 1].contiguous()
+        self._normalize_advantages(d)
+        return d
+
+    def _sync_running(self):
+        """Mirror the device EMA state into the host RunningMeanStd (metrics + checkpoint)."""
+        e = self.ema.cpu()
+        for team, k in self.team_keys.items():
+            if e[k, 2] != 0:
+                self.running.mean[team] = float(e[k, 0])
+                self.running.std[team] = float(e[k, 1])
+
+    def _normalize_advantages(self, d):
+        if self.cfg.algo == 'ppo' and self.cfg.normalize_advantages:
+            v = d['valid']
+            n = v.sum().clamp_min(1.0)
+            mu = (d['adv'] * v).sum() / n
+            sd = (((d['adv'] - mu) ** 2 * v).sum() / n).sqrt()
+            d['adv'] = ((d['adv'] - mu) / (sd + EPS)) * v
+
     def _to_device(self, seqs: List[Sequence]) -> Dict[str, torch.Tensor]:
         def st(name, dtype):
             a = np.stack([getattr(s, name) for s in seqs])
@@ -222,12 +320,7 @@ class DotaOptimizer:
         if self.policy.is_recurrent:
             h = st('hidden', torch.float32)
             d['h0'], d['c0'] = h[:, 0].contiguous(), h[:, 1].contiguous()
-        if self.cfg.algo == 'ppo' and self.cfg.normalize_advantages:
-            v = d['valid']
-            n = v.sum().clamp_min(1.0)
-            mu = (d['adv'] * v).sum() / n
-            sd = (((d['adv'] - mu) ** 2 * v).sum() / n).sqrt()
-            d['adv'] = ((d['adv'] - mu) / (sd + EPS)) * v
+        self._normalize_advantages(d)
         return d
 
     # ------------------------------------------------------------------------------------------------
@@ -242,11 +335,18 @@ class DotaOptimizer:
         cfg = self.cfg
         self.timer.start('ingest')
         experiences: List[Sequence] = []
+        rollouts: List[Rollout] = []
+        n_seq = 0
         subrewards, rollout_lens, weight_ages = [], [], []
         canvas = None
-        while len(experiences) < cfg.seq_per_epoch:
+        while n_seq < cfg.seq_per_epoch:
             r = self.get_rollout()
-            experiences.extend(self.experiences_from_rollout(r))
+            if self.ingest == 'device':
+                rollouts.append(r)
+                n_seq += -(-r.length // cfg.seq_len)
+            else:
+                experiences.extend(self.experiences_from_rollout(r))
+                n_seq = len(experiences)
             subrewards.append(r.rewards.sum(axis=0))
             rollout_lens.append(r.length)
             weight_ages.append(it - r.weight_version)
@@ -254,8 +354,11 @@ class DotaOptimizer:
         self.timer.stop('ingest')
         # all sequences of this iteration go to the device once; minibatches are gathered on-device
         self.timer.start('h2d')
-        n = len(experiences) - len(experiences) % cfg.batch_size
-        data = self._to_device(experiences[:n])
+        n = n_seq - n_seq % cfg.batch_size
+        if self.ingest == 'device':
+            data = self._ingest_device(rollouts, n)
+        else:
+            data = self._to_device(experiences[:n])
         self.timer.stop('h2d')
         self.timer.start('train')
         losses, metrics_acc = [], {}
@@ -287,7 +390,9 @@ class DotaOptimizer:
             raise ValueError(f'NaN loss at iteration {it}: {loss_t.tolist()}')
         if self.learner.backend == 'fused':
             self.learner.model.check_error()
-        n_steps = len(experiences) * cfg.seq_len
+        n_steps = n_seq * cfg.seq_len
+        if self.ingest == 'device':
+            self._sync_running()
         now = time.time()
         steps_per_s = n_steps / max(now - self.time_last_step, 1e-9)
         self.time_last_step = now

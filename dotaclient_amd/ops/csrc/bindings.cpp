@@ -7,6 +7,9 @@
 #include <ATen/hip/HIPContext.h>
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstring>
+
 #include "launchers.h"
 
 namespace {
@@ -350,6 +353,67 @@ void lstm_cell(torch::Tensor gates, torch::Tensor h, torch::Tensor c, torch::Ten
             "dca_lstm_cell");
 }
 
+// Returns / advantages over concatenated padded rollouts. rew (L,K) f32 and val (L) f32 (GAE; ignored for mode 0)
+// live on the GPU; the per-segment metadata is host data — off (nseg+1) i32 row offsets, seglen (nseg) i32 valid
+// steps, keys (nseg) i32 team key, boot (nseg) f32 bootstrap values, done (nseg) u8 — validated here and uploaded in
+// one copy. ema (n_keys,3) f32 [mean, std, initialised] is read and replaced by the state after this batch.
+// mode 0 = discounted return + EMA normalisation (reference VPG), 1 = GAE(γ, λ). Writes ret/adv/norm (L) and
+// stats (nseg,2) [mean, std of the returns].
+void returns_scan(torch::Tensor rew, torch::Tensor val, torch::Tensor off, torch::Tensor seglen, torch::Tensor boot,
+                  torch::Tensor done, torch::Tensor keys, torch::Tensor ema, torch::Tensor ret, torch::Tensor adv,
+                  torch::Tensor norm, torch::Tensor stats, int64_t mode, bool normalize, double gamma, double lam,
+                  double factor, double eps) {
+  CHECK_F32(rew); CHECK_F32(ema); CHECK_F32(ret); CHECK_F32(adv); CHECK_F32(norm); CHECK_F32(stats);
+  TORCH_CHECK(rew.dim() == 2, "rew must be (L, K)");
+  const int64_t L = rew.size(0);
+  const int nseg = seglen.numel();
+  for (auto* t : {&off, &seglen, &keys, &boot, &done})
+    TORCH_CHECK(!t->is_cuda() && t->is_contiguous(), "returns_scan: segment metadata must be contiguous host tensors");
+  TORCH_CHECK(off.scalar_type() == at::kInt && seglen.scalar_type() == at::kInt && keys.scalar_type() == at::kInt &&
+              boot.scalar_type() == at::kFloat && done.scalar_type() == at::kByte, "returns_scan: metadata dtypes");
+  TORCH_CHECK(off.numel() == nseg + 1 && boot.numel() == nseg && done.numel() == nseg && keys.numel() == nseg,
+              "returns_scan: per-segment tensor lengths");
+  TORCH_CHECK(ret.numel() == L && adv.numel() == L && norm.numel() == L && stats.numel() == 2 * nseg,
+              "returns_scan: output lengths");
+  TORCH_CHECK(ema.dim() == 2 && ema.size(1) == 3, "ema must be (n_keys, 3)");
+  TORCH_CHECK(mode == 0 || mode == 1, "mode must be 0 (discount) or 1 (gae)");
+  TORCH_CHECK(rew.size(1) <= 64, "returns_scan: at most 64 sub-rewards");
+  const float* vp = nullptr;
+  if (mode == 1) {
+    CHECK_F32(val);
+    TORCH_CHECK(val.numel() == L, "returns_scan: values must have one entry per row");
+    vp = ptr<float>(val);
+  }
+  if (nseg == 0) return;
+  const int* o = off.data_ptr<int>();
+  const int* k = keys.data_ptr<int>();
+  TORCH_CHECK(o[0] == 0 && o[nseg] == L, "returns_scan: offsets must span [0, L]");
+  int max_len = 0;
+  for (int i = 0; i < nseg; ++i) {
+    TORCH_CHECK(o[i + 1] >= o[i], "returns_scan: decreasing offsets at segment ", i);
+    TORCH_CHECK(k[i] >= 0 && k[i] < ema.size(0), "returns_scan: key out of range at segment ", i);
+    max_len = std::max(max_len, o[i + 1] - o[i]);
+  }
+  // one upload of the packed metadata: [off | seglen | keys | boot | done]
+  auto meta = torch::empty({(int64_t)(4 * nseg + 1 + (nseg + 3) / 4)}, torch::dtype(at::kInt));
+  int* mp = meta.data_ptr<int>();
+  std::memcpy(mp, o, sizeof(int) * (nseg + 1));
+  std::memcpy(mp + nseg + 1, seglen.data_ptr<int>(), sizeof(int) * nseg);
+  std::memcpy(mp + 2 * nseg + 1, k, sizeof(int) * nseg);
+  std::memcpy(mp + 3 * nseg + 1, boot.data_ptr<float>(), sizeof(float) * nseg);
+  std::memcpy(mp + 4 * nseg + 1, done.data_ptr<uint8_t>(), nseg);
+  auto md = meta.to(rew.device());
+  int* d = md.data_ptr<int>();
+  auto ema_out = ema.clone();
+  hip_check(dca_returns(ptr<float>(rew), (int)rew.size(1), vp, d, d + nseg + 1, reinterpret_cast<float*>(d + 3 * nseg + 1),
+                        reinterpret_cast<unsigned char*>(d + 4 * nseg + 1), d + 2 * nseg + 1, nseg, max_len,
+                        ptr<float>(ret), ptr<float>(adv), ptr<float>(norm), ptr<float>(stats), ptr<float>(ema),
+                        ptr<float>(ema_out), (int)mode, normalize ? 1 : 0, (float)gamma, (float)lam, (float)factor,
+                        (float)eps, cur_stream()),
+            "dca_returns");
+  ema.copy_(ema_out);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -380,4 +444,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sample_actions", &sample_actions, "fused masked hierarchical Gumbel-max action sampling (actor)");
   m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)", py::arg("gates"),
         py::arg("h"), py::arg("c"), py::arg("h16"), py::arg("active") = py::none());
+  m.def("returns_scan", &returns_scan, "segmented reverse scan: discounted returns / GAE + per-team EMA normalisation");
 }

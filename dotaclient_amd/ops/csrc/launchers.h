@@ -57,4 +57,9 @@ hipError_t dca_sample_actions(const float* z, int ldz, const short* emb, const l
 hipError_t dca_lstm_cell(const float* gates, float* h, float* c, short* h16, const float* active, int N, int H,
                          hipStream_t st);
 
+hipError_t dca_returns(const float* rew, int K, const float* val, const int* off, const int* seglen,
+                       const float* boot, const unsigned char* done, const int* keys, int nseg, int max_len,
+                       float* ret, float* adv, float* norm, float* stats, const float* ema_in, float* ema_out,
+                       int mode, int normalize, float gamma, float lam, float factor, float eps, hipStream_t st);
+
 }  // extern "C"

@@ -1,0 +1,189 @@
+// Device return / advantage computation over a batch of rollouts (gfx950): segmented reverse linear scan +
+// per-segment statistics + per-team EMA reward normalisation.
+//
+// Reference semantics (SURVEY §2.3 K-return / K-norm):
+//   * discounted return over the whole padded rollout, G_t = r_t + γ·G_{t+1}, r_t = Σ_k subreward_k
+//     (optimizer.py:52-53, 382 — scipy lfilter);
+//   * per-team EMA(0.99) of the batch mean / std of those returns, updated once per rollout in arrival order, and the
+//     normalised return (G − μ)/(σ + eps) (optimizer.py:335-343, 185-186);
+//   * the PPO path (north star): GAE(γ, λ) over the valid prefix, A_t = δ_t + γλ·A_{t+1},
+//     δ_t = r_t + γ·V_{t+1} − V_t (bootstrapped with the actor's V at the cut, 0 at a terminal), returns = A + V.
+//
+// Layout: all rollouts of an iteration are concatenated, each padded to a multiple of seq_len (segment s spans
+// [off[s], off[s+1]) with T_s valid steps), so the learner's sequences are a plain reshape of the outputs.
+//
+//   1. returns_scan_kernel   — one 256-thread workgroup per rollout. Each thread owns a contiguous chunk, reduces it
+//      to an affine map y ↦ X + p·y (the chunk's recurrence with the carry y coming from later steps), the 256 maps
+//      are composed by a wave-level suffix scan (DPP shuffles) and a 4-entry LDS scan across waves, then every
+//      thread replays its chunk from its exact carry. The forcing terms are computed once (pass 1) and parked in the
+//      output buffer, which the same thread reads back in pass 2 (no cross-thread hazards). A third pass over the
+//      thread's own outputs gives the two-pass mean / population std of the returns.
+//   2. ema_normalize_kernel  — grid (segments × blocks-per-segment). Thread 0 of each block folds the statistics of
+//      every earlier segment of the same team into the EMA state (rollouts are few, the fold is O(n_seg)), the block
+//      normalises its slice, and the block that owns a team's last segment writes that team's final EMA state.
+#include "common.h"
+
+namespace {
+
+constexpr int kT = 256;
+constexpr int kWaves = kT / dca::kWave;
+
+__device__ __forceinline__ float forcing(const float* __restrict__ rew, int K, const float* __restrict__ val,
+                                         size_t row, int t, int T, float vboot, float gamma, int mode) {
+  const float* rr = rew + row * K;
+  float r = 0.f;
+  for (int k = 0; k < K; ++k) r += rr[k];
+  if (mode == 1) {
+    const float vn = (t + 1 < T) ? val[row + 1] : vboot;
+    return r + gamma * vn - val[row];
+  }
+  return r;
+}
+
+__global__ __launch_bounds__(kT) void returns_scan_kernel(
+    const float* __restrict__ rew, int K, const float* __restrict__ val, const int* __restrict__ off,
+    const int* __restrict__ seglen, const float* __restrict__ boot, const unsigned char* __restrict__ done,
+    float* __restrict__ ret, float* __restrict__ adv, float* __restrict__ stats, int mode, float gamma, float lam) {
+  const int s = blockIdx.x;
+  const int base = off[s];
+  const int P = off[s + 1] - base;
+  const int T = min(seglen[s], P);
+  const int n = (mode == 1) ? T : P;                 // GAE: the padded tail is zero
+  const float c = (mode == 1) ? gamma * lam : gamma;
+  const float vboot = (mode == 1 && !done[s]) ? boot[s] : 0.f;
+  float* acc_out = (mode == 1) ? adv : ret;          // the scanned quantity
+  const int per = (n + kT - 1) / kT;
+  const int lo = min((int)threadIdx.x * per, n), hi = min(lo + per, n);
+
+  // pass 1: forcing terms (parked in acc_out) and this chunk's map y -> X + p*y
+  float X = 0.f, p = 1.f;
+  for (int t = hi - 1; t >= lo; --t) {
+    const float d = forcing(rew, K, val, (size_t)base + t, t, T, vboot, gamma, mode);
+    acc_out[base + t] = d;
+    X = d + c * X;
+    p *= c;
+  }
+
+  // suffix scan of the maps: lane l ends with the composition of lanes l..63 of its wave
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float xo = __shfl_down(X, o, 64), po = __shfl_down(p, o, 64);
+    if (lane + o < 64) {
+      X = X + p * xo;
+      p = p * po;
+    }
+  }
+  __shared__ float wx[kWaves], wp[kWaves], red[kWaves];
+  if (lane == 0) {
+    wx[w] = X;
+    wp[w] = p;
+  }
+  __syncthreads();
+  float y = 0.f;                                      // carry entering this wave from later waves
+  for (int k = kWaves - 1; k > w; --k) y = wx[k] + wp[k] * y;
+  const float x1 = __shfl_down(X, 1, 64), p1 = __shfl_down(p, 1, 64);
+  float carry = (lane == 63) ? y : x1 + p1 * y;     // value of the recurrence just after this chunk
+
+  // pass 2: replay the chunk from its carry; returns and the running sum for the statistics
+  float sum = 0.f;
+  for (int t = hi - 1; t >= lo; --t) {
+    const size_t i = (size_t)base + t;
+    carry = acc_out[i] + c * carry;
+    acc_out[i] = carry;
+    float g = carry;
+    if (mode == 1) {
+      g = carry + val[i];
+      ret[i] = g;
+    }
+    sum += g;
+  }
+  if (mode == 1) {                                    // zero tail of a GAE segment
+    for (int t = T + threadIdx.x; t < P; t += kT) {
+      ret[base + t] = 0.f;
+      adv[base + t] = 0.f;
+    }
+  }
+
+  // two-pass mean / population std of the returns over the scanned range
+  sum = dca::wave_sum(sum);
+  if (lane == 0) red[w] = sum;
+  __syncthreads();
+  float tot = 0.f;
+#pragma unroll
+  for (int k = 0; k < kWaves; ++k) tot += red[k];
+  const float mean = tot / (float)max(n, 1);
+  __syncthreads();
+  float sq = 0.f;
+  for (int t = lo; t < hi; ++t) {
+    const float dlt = ret[base + t] - mean;
+    sq += dlt * dlt;
+  }
+  sq = dca::wave_sum(sq);
+  if (lane == 0) red[w] = sq;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) v += red[k];
+    stats[2 * s] = mean;
+    stats[2 * s + 1] = sqrtf(v / (float)max(n, 1));
+  }
+}
+
+__global__ __launch_bounds__(kT) void ema_normalize_kernel(
+    const float* __restrict__ ret, const int* __restrict__ off, const int* __restrict__ keys,
+    const float* __restrict__ stats, int nseg, const float* __restrict__ ema_in, float* __restrict__ ema_out,
+    float* __restrict__ norm, int normalize, float factor, float eps) {
+  const int s = blockIdx.x;
+  const int key = keys[s];
+  __shared__ float sm, ss;
+  if (threadIdx.x == 0) {
+    float m = ema_in[3 * key], sd = ema_in[3 * key + 1];
+    bool init = ema_in[3 * key + 2] != 0.f;
+    for (int j = 0; j <= s; ++j) {
+      if (keys[j] != key) continue;
+      const float bm = stats[2 * j], bs = stats[2 * j + 1];
+      if (!init) {
+        m = bm;
+        sd = bs;
+        init = true;
+      } else {
+        m = m * factor + bm * (1.f - factor);
+        sd = sd * factor + bs * (1.f - factor);
+      }
+    }
+    sm = m;
+    ss = sd;
+    bool last = true;
+    for (int j = s + 1; j < nseg && last; ++j) last = keys[j] != key;
+    if (last && blockIdx.y == 0) {
+      ema_out[3 * key] = m;
+      ema_out[3 * key + 1] = sd;
+      ema_out[3 * key + 2] = 1.f;
+    }
+  }
+  if (!normalize) return;
+  __syncthreads();
+  const float m = sm, inv = 1.f / (ss + eps);
+  const int base = off[s], P = off[s + 1] - base;
+  for (int t = blockIdx.y * kT + threadIdx.x; t < P; t += gridDim.y * kT) norm[base + t] = (ret[base + t] - m) * inv;
+}
+
+}  // namespace
+
+extern "C" hipError_t dca_returns(const float* rew, int K, const float* val, const int* off, const int* seglen,
+                                  const float* boot, const unsigned char* done, const int* keys, int nseg, int max_len,
+                                  float* ret, float* adv, float* norm, float* stats, const float* ema_in,
+                                  float* ema_out, int mode, int normalize, float gamma, float lam, float factor,
+                                  float eps, hipStream_t st) {
+  if (nseg <= 0) return hipSuccess;
+  hipLaunchKernelGGL(returns_scan_kernel, dim3(nseg), dim3(kT), 0, st, rew, K, val, off, seglen, boot, done, ret, adv,
+                     stats, mode, gamma, lam);
+  DCA_CHECK_LAUNCH();
+  const int by = normalize ? max(1, min(64, (max_len + 4 * kT - 1) / (4 * kT))) : 1;
+  hipLaunchKernelGGL(ema_normalize_kernel, dim3(nseg, by), dim3(kT), 0, st, ret, off, keys, stats, nseg, ema_in,
+                     ema_out, norm, normalize, factor, eps);
+  DCA_CHECK_LAUNCH();
+  return hipSuccess;
+}

@@ -1,0 +1,105 @@
+"""Returns / advantages over a batch of rollouts on the device (``csrc/scan.hip``) plus its CPU reference.
+
+All rollouts of a learner iteration are concatenated, each padded to a multiple of ``seq_len``; segment ``s`` spans
+rows ``off[s]:off[s+1]`` of which the first ``seglen[s]`` are real steps. ``compute_returns`` returns per-row
+``ret`` / ``adv`` / ``norm`` and per-segment ``stats`` (mean, population std of the returns), and advances the
+per-team EMA state ``ema`` (``(n_keys, 3)`` = mean, std, initialised) in rollout order:
+
+* ``mode='discount'`` — reference VPG path: ``G_t = r_t + γ G_{t+1}`` over the whole padded segment
+  (optimizer.py:52-53, 382), EMA(0.99) update with the segment's (mean, std) (optimizer.py:335-343) and the normalised
+  return ``(G − μ)/(σ + eps)`` (optimizer.py:185-186) in ``norm`` (= ``adv``).
+* ``mode='gae'`` — PPO path: GAE(γ, λ) over the valid prefix, ``ret = adv + V``, zeros in the padded tail; the EMA is
+  updated with the statistics of ``ret[:T]`` (metrics only); ``norm`` = ``adv``.
+
+On a GPU tensor the HIP kernel runs (and the extension is required); on CPU the torch reference below runs — it is
+also the oracle of the GPU tests.
+"""
+from __future__ import annotations
+
+from typing import Dict
+
+import torch
+
+from ..constants import EPS
+
+MODES = {'discount': 0, 'gae': 1}
+
+
+def _reference(rew, val, off, seglen, boot, done, keys, ema, mode, gamma, lam, factor, eps, normalize):
+    L = rew.shape[0]
+    r = rew.double().sum(1)
+    v = val.double() if mode == 1 else None
+    ret = torch.zeros(L, dtype=torch.float64)
+    adv = torch.zeros(L, dtype=torch.float64)
+    nseg = seglen.numel()
+    stats = torch.zeros(nseg, 2, dtype=torch.float64)
+    for s in range(nseg):
+        a, b = int(off[s]), int(off[s + 1])
+        T = min(int(seglen[s]), b - a)
+        if mode == 1:
+            acc, nv = 0.0, (0.0 if bool(done[s]) else float(boot[s]))
+            for t in range(T - 1, -1, -1):
+                delta = float(r[a + t]) + gamma * nv - float(v[a + t])
+                acc = delta + gamma * lam * acc
+                adv[a + t] = acc
+                nv = float(v[a + t])
+            ret[a:a + T] = adv[a:a + T] + v[a:a + T]
+            seg = ret[a:a + T]
+        else:
+            acc = 0.0
+            for t in range(b - a - 1, -1, -1):
+                acc = float(r[a + t]) + gamma * acc
+                ret[a + t] = acc
+            seg = ret[a:b]
+        if seg.numel():
+            stats[s, 0] = seg.mean()
+            stats[s, 1] = seg.std(unbiased=False)
+    ema_new = ema.clone().double()
+    norm = adv.clone() if mode == 1 else torch.zeros(L, dtype=torch.float64)
+    for s in range(nseg):
+        k = int(keys[s])
+        if ema_new[k, 2] == 0:
+            ema_new[k, 0], ema_new[k, 1], ema_new[k, 2] = stats[s, 0], stats[s, 1], 1.0
+        else:
+            ema_new[k, 0] = ema_new[k, 0] * factor + stats[s, 0] * (1 - factor)
+            ema_new[k, 1] = ema_new[k, 1] * factor + stats[s, 1] * (1 - factor)
+        if mode == 0 and normalize:
+            a, b = int(off[s]), int(off[s + 1])
+            norm[a:b] = (ret[a:b] - ema_new[k, 0]) / (ema_new[k, 1] + eps)
+    if mode == 0:
+        adv = norm if normalize else ret.clone()
+    ema.copy_(ema_new.to(ema.dtype))
+    f = torch.float32
+    return {'ret': ret.to(f), 'adv': adv.to(f), 'norm': norm.to(f), 'stats': stats.to(f)}
+
+
+def compute_returns(rew: torch.Tensor, val, off, seglen, boot, done, keys, ema: torch.Tensor, mode: str = 'gae',
+                    gamma: float = 0.98, lam: float = 0.95, factor: float = 0.99, eps: float = EPS,
+                    normalize: bool = True) -> Dict[str, torch.Tensor]:
+    """``rew`` (L, K) f32 sub-rewards (summed per row), ``val`` (L,) f32 or None; per-segment metadata as host
+    int32/float32/uint8 tensors or sequences; ``ema`` (n_keys, 3) f32 on the same device as ``rew`` (updated in
+    place)."""
+    m = MODES[mode]
+    off = torch.as_tensor(off, dtype=torch.int32).contiguous()
+    seglen = torch.as_tensor(seglen, dtype=torch.int32).contiguous()
+    keys = torch.as_tensor(keys, dtype=torch.int32).contiguous()
+    boot = torch.as_tensor(boot, dtype=torch.float32).contiguous()
+    done = torch.as_tensor(done, dtype=torch.uint8).contiguous()
+    if m == 1 and val is None:
+        raise ValueError('gae needs values')
+    if rew.device.type != 'cuda':
+        return _reference(rew, val, off, seglen, boot, done, keys, ema, m, gamma, lam, factor, eps, normalize)
+    from . import require
+    C = require()
+    L = rew.shape[0]
+    rew = rew.float().contiguous()
+    v = val.float().contiguous() if m == 1 else rew.new_empty(0)
+    ret = torch.empty(L, device=rew.device)
+    adv = torch.empty(L, device=rew.device) if m == 1 else ret.new_empty(L)
+    norm = torch.empty(L, device=rew.device) if m == 0 else adv
+    stats = torch.empty(seglen.numel(), 2, device=rew.device)
+    C.returns_scan(rew, v, off, seglen, boot, done, keys, ema, ret, adv, norm, stats, m, bool(normalize and m == 0),
+                   float(gamma), float(lam), float(factor), float(eps))
+    if m == 0:
+        adv = norm if normalize else ret
+    return {'ret': ret, 'adv': adv, 'norm': norm, 'stats': stats}

@@ -1,0 +1,123 @@
+"""Device return / GAE scan (ops/csrc/scan.hip) and the device ingest path of the learner.
+
+* CPU: the torch reference of ``compute_returns`` equals the host numpy path (``discount`` / ``gae`` /
+  ``RunningMeanStd``, themselves pinned to scipy.lfilter and the reference formula in test_runtime.py), and the
+  learner's device-ingest batch equals the host ``experiences_from_rollout`` + ``_to_device`` batch.
+* GPU: the HIP kernel equals the fp64 torch reference over ragged segments, both modes, incl. long rollouts.
+"""
+import numpy as np
+import pytest
+import torch
+
+from dotaclient_amd.learner.returns import RunningMeanStd, discount, gae
+from dotaclient_amd.ops.scan import compute_returns
+from dotaclient_amd.transport.codec import Rollout
+
+
+def _segments(rng, lens, S, K=9):
+    padded = [-(-T // S) * S for T in lens]
+    off = np.concatenate([[0], np.cumsum(padded)]).astype(np.int32)
+    L = int(off[-1])
+    rew = np.zeros((L, K), np.float32)
+    val = np.zeros(L, np.float32)
+    for T, a in zip(lens, off[:-1]):
+        rew[a:a + T] = rng.randn(T, K) * 0.1
+        val[a:a + T] = rng.randn(T)
+    return off, rew, val
+
+
+@pytest.mark.parametrize('mode', ['discount', 'gae'])
+def test_reference_matches_host_numpy(mode):
+    rng = np.random.RandomState(3)
+    S = 64
+    lens = [50, 64, 130, 7, 200]
+    keys = [0, 1, 0, 0, 1]
+    boot = rng.randn(len(lens)).astype(np.float32)
+    done = [True, False, False, True, False]
+    off, rew, val = _segments(rng, lens, S)
+    ema = torch.zeros(4, 3)
+    out = compute_returns(torch.from_numpy(rew), torch.from_numpy(val), off, lens, boot, done, keys, ema, mode)
+    rms = RunningMeanStd(0.99)
+    for i, (T, a, b) in enumerate(zip(lens, off[:-1], off[1:])):
+        summed = rew[a:b].astype(np.float64).sum(1)
+        if mode == 'gae':
+            adv, ret = gae(summed[:T], val[a:a + T], boot[i], 0.98, 0.95, done=done[i])
+            np.testing.assert_allclose(out['adv'][a:a + T].numpy(), adv, rtol=1e-5, atol=1e-5)
+            np.testing.assert_allclose(out['ret'][a:a + T].numpy(), ret, rtol=1e-5, atol=1e-5)
+            assert (out['ret'][a + T:b] == 0).all() and (out['adv'][a + T:b] == 0).all()
+            rms.update(ret, keys[i])
+        else:
+            ret = discount(summed, 0.98)
+            np.testing.assert_allclose(out['ret'][a:b].numpy(), ret, rtol=1e-5, atol=1e-5)
+            rms.update(ret, keys[i])
+            np.testing.assert_allclose(out['norm'][a:b].numpy(), rms.normalize(ret, keys[i]), rtol=1e-4, atol=1e-4)
+    for k in (0, 1):
+        assert float(ema[k, 0]) == pytest.approx(rms.mean[k], rel=1e-5, abs=1e-6)
+        assert float(ema[k, 1]) == pytest.approx(rms.std[k], rel=1e-5, abs=1e-6)
+        assert float(ema[k, 2]) == 1.0
+    assert float(ema[2, 2]) == 0.0
+
+
+def _rollouts(n, U=40, H=16, seed=0):
+    rng = np.random.RandomState(seed)
+    out = []
+    for i in range(n):
+        T = int(rng.randint(20, 150))
+        out.append(Rollout(game_id=f'g{i}', team_id=2 + i % 2, player_id=0, env=rng.randn(T, 3).astype(np.float32),
+                           units=rng.randn(T, U, 10).astype(np.float32),
+                           actions=(rng.rand(T, 21 + U) > 0.9).astype(np.uint8),
+                           masks=(rng.rand(T, 21 + U) > 0.5).astype(np.uint8), rewards=rng.randn(T, 9) * 0.1,
+                           weight_version=1, logp=rng.randn(T).astype(np.float32),
+                           values=rng.randn(T).astype(np.float32), hiddens=rng.randn(8, 2, H).astype(np.float32),
+                           hidden_stride=32, bootstrap_value=float(rng.randn()), done=bool(i % 3 == 0)))
+    return out
+
+
+@pytest.mark.parametrize('algo', ['ppo', 'vpg'])
+def test_device_ingest_equals_host_ingest(tmp_path, algo):
+    from dotaclient_amd.learner.optimizer import DotaOptimizer, OptimizerConfig
+    from dotaclient_amd.transport.broker import InProcBroker
+
+    def make(ingest, sub):
+        cfg = OptimizerConfig(log_dir=str(tmp_path / sub), batch_size=2, seq_len=32, seq_per_epoch=8, epochs=1,
+                              algo=algo, model='lstm128', device='cpu', backend='torch', ingest=ingest)
+        return DotaOptimizer(cfg, InProcBroker())
+    host, dev = make('host', 'h'), make('device', 'd')
+    for it in range(2):                                  # two rounds: the EMA state carries over
+        rs = _rollouts(5, H=host.policy_cfg.hidden, seed=it)
+        seqs = []
+        for r in rs:
+            seqs.extend(host.experiences_from_rollout(r))
+        n = len(seqs) - len(seqs) % 2
+        a = host._to_device(seqs[:n])
+        b = dev._ingest_device(rs, n)
+        assert set(a) == set(b)
+        for k in a:
+            assert a[k].shape == b[k].shape, k
+            torch.testing.assert_close(b[k].float(), a[k].float(), rtol=1e-4, atol=1e-4, msg=k)
+        dev._sync_running()
+        for team in (2, 3):
+            assert dev.running.mean[team] == pytest.approx(host.running.mean[team], rel=1e-5, abs=1e-6)
+            assert dev.running.std[team] == pytest.approx(host.running.std[team], rel=1e-5, abs=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('mode', ['discount', 'gae'])
+def test_scan_kernel_matches_reference(gpu_ops, mode):
+    rng = np.random.RandomState(11)
+    S = 1400
+    lens = [1380, 1400, 2900, 1, 700, 9999, 3000, 64]
+    keys = [0, 1, 0, 1, 1, 0, 2, 0]
+    boot = rng.randn(len(lens)).astype(np.float32)
+    done = [True, False, False, True, False, True, False, False]
+    off, rew, val = _segments(rng, lens, S)
+    ema_c = torch.zeros(3, 3)
+    ema_c[1] = torch.tensor([0.3, 1.5, 1.0])            # a resumed team state
+    ema_g = ema_c.clone().cuda()
+    ref = compute_returns(torch.from_numpy(rew), torch.from_numpy(val), off, lens, boot, done, keys, ema_c, mode)
+    got = compute_returns(torch.from_numpy(rew).cuda(), torch.from_numpy(val).cuda(), off, lens, boot, done, keys,
+                          ema_g, mode)
+    torch.cuda.synchronize()
+    for k in ('ret', 'adv', 'norm', 'stats'):
+        torch.testing.assert_close(got[k].cpu(), ref[k], rtol=2e-4, atol=2e-4, msg=k)
+    torch.testing.assert_close(ema_g.cpu(), ema_c, rtol=1e-5, atol=1e-5)
