@@ -81,9 +81,9 @@ def main():
     trace = os.environ.get('DCA_BENCH_TRACE') == '1'
 
     def step():
-        batch = replay.sample(args.batch_size)
         t = time.perf_counter()
-        out = learner.train_step(batch)
+        # on-device minibatch gather from the HBM replay pool (part of the captured step on the fused path)
+        out = learner.train_step_replay(replay.buf, args.batch_size)
         if trace:
             torch.cuda.synchronize()
             print(f'[bench] step {learner.n_steps} {1e3 * (time.perf_counter() - t):.2f} ms loss '

@@ -59,6 +59,7 @@ class Learner:
         if backend == 'fused':
             from ..models.fused import FusedPolicy
             self.model = FusedPolicy(self.policy, loss_cfg)
+            self.model.attach_flat(self.flat.flat)
         self.counts = self.policy.layout.action_counts()
         self.n_steps = 0
         self.graph = None                 # captured forward+backward (see enable_graph)
@@ -117,34 +118,132 @@ class Learner:
             self.dp.has_grad.copy_(self.model.grad_mask)
         return {k: v.detach() for k, v in metrics.items()}
 
-    def _graphed_fwd_bwd(self, batch):
-        if self.graph is None:
-            self._static_in = {k: v.clone() for k, v in batch.items()}
+    # ---- direct (autograd-free) fused LSTM step ------------------------------------------------------
+    def direct(self) -> bool:
+        """The fused LSTM policy runs the autograd-free step (models/pipelined.py:train_direct)."""
+        return self.backend == 'fused' and self.device.type == 'cuda' and self.model.use_pipeline()
+
+    STEP_FIELDS = ('units', 'env', 'actions', 'masks', 'adv', 'ret', 'logp_old', 'norm_ret')
+
+    @staticmethod
+    def batch_to_time_major(batch):
+        """Batch-major ``(B,S,…)`` fields → time-major rows ``(S·B,…)`` (row = t·B + b)."""
+        B, S = batch['env'].shape[:2]
+        out = {}
+        for k in Learner.STEP_FIELDS:
+            v = batch.get(k)
+            if v is None:
+                v = torch.zeros(B, S, device=batch['env'].device)
+            out[k] = v.transpose(0, 1).reshape(S * B, *v.shape[2:]).contiguous()
+        for k in ('h0', 'c0'):
+            if k in batch:
+                out[k] = batch[k].contiguous()
+        return out, B, S
+
+    def gather_time_major(self, replay, idx, S: int):
+        """Minibatch of replay rows ``idx`` gathered straight into time-major rows: one index_select per field
+        over the pool viewed as (capacity·S, …) — no batch-major copy, no transpose."""
+        B = idx.numel()
+        ar = getattr(self, '_arange', None)
+        if ar is None or ar.numel() < S or ar.device != idx.device:
+            ar = self._arange = torch.arange(max(S, 1), device=idx.device, dtype=torch.long)
+        rows = (idx.view(1, B) * S + ar[:S].view(S, 1)).reshape(-1)
+        out = {}
+        for k in self.STEP_FIELDS:
+            pool = replay.data[k]
+            out[k] = pool.view(-1, *pool.shape[2:]).index_select(0, rows)
+        for k in ('h0', 'c0'):
+            if k in replay.data:
+                out[k] = replay.data[k].index_select(0, idx)
+        return out
+
+    def _direct_body(self, batch_tm, B, S):
+        self.flat.grad.zero_()
+        vec = self.model.train_direct(batch_tm, B, S, self.cfg)
+        self.dp.has_grad.copy_(self.model.grad_mask)
+        return vec
+
+    def _metrics_from_vec(self, vec):
+        from ..models.pipelined import METRIC_NAMES
+        names = METRIC_NAMES if self.cfg.algo == 'ppo' else [n for n in METRIC_NAMES
+                                                              if n not in ('approx_kl', 'clipfrac')]
+        return {n: vec[METRIC_NAMES.index(n)] for n in names}
+
+    def _graph_ready(self) -> bool:
+        return bool(self._graph_warmup) and self.n_steps >= self._graph_warmup
+
+    def _replay_graph(self, key, body):
+        """Capture ``body`` (a function of the static inputs) once per key, then replay it."""
+        graphs = self.__dict__.setdefault('_graphs', {})
+        if key not in graphs:
             # the capture stream must outlive the graph: hipBLASLt's per-stream workspace that the captured GEMM
             # nodes point at belongs to it
-            s = self._graph_stream = torch.cuda.Stream(device=self.device)
-            s.wait_stream(torch.cuda.current_stream(self.device))
+            if getattr(self, '_graph_stream', None) is None:
+                self._graph_stream = torch.cuda.Stream(device=self.device)
+            s = self._graph_stream
+            cur = torch.cuda.current_stream(self.device)
+            s.wait_stream(cur)
             with torch.cuda.stream(s):          # one more eager run on the capture stream (allocator warm-up)
-                self._fwd_bwd(self._static_in)
-            torch.cuda.current_stream(self.device).wait_stream(s)
-            self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph, stream=s):
-                self._static_out = self._fwd_bwd(self._static_in)
-            self._graph_mask_used = getattr(self.model, 'direct_used', False)
-        for k, v in batch.items():
-            self._static_in[k].copy_(v, non_blocking=True)
-        self.dp.zero_grad()
-        self.graph.replay()
-        if self._graph_mask_used:
-            self.dp.has_grad.copy_(self.model.grad_mask)
-        return {k: v.clone() for k, v in self._static_out.items()}
+                body()
+            cur.wait_stream(s)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                out = body()
+            graphs[key] = (g, out)
+            self.graph = g
+        g, out = graphs[key]
+        g.replay()
+        return out
+
+    def _step_direct_batch(self, batch):
+        if not self._graph_ready():
+            bt, B, S = self.batch_to_time_major(batch)
+            return self._direct_body(bt, B, S)
+        B, S = batch['env'].shape[:2]
+        key = ('batch', B, S, tuple(sorted(batch)))
+        if key not in self.__dict__.get('_graphs', {}):
+            self._static_in = {k: v.clone() for k, v in batch.items()}
+        else:
+            for k, v in batch.items():
+                self._static_in[k].copy_(v, non_blocking=True)
+
+        def body():
+            bt, B_, S_ = self.batch_to_time_major(self._static_in)
+            return self._direct_body(bt, B_, S_)
+        return self._replay_graph(key, body)
+
+    def train_step_replay(self, replay, B: int, recent: Optional[int] = None) -> Dict[str, torch.Tensor]:
+        """One DP optimizer step on a minibatch sampled from an on-device replay (``learner.replay.HbmReplay``).
+        On the direct fused path the gather itself is part of the captured graph (only the sampled indices are
+        copied in)."""
+        idx = replay.sample_indices(B, recent)
+        if not self.direct():
+            return self.train_step(replay.gather(idx))
+        S = replay.S
+        if self._graph_ready():
+            key = ('replay', id(replay), B, S)
+            if key not in self.__dict__.get('_graphs', {}):
+                self._static_idx = idx.clone()
+            else:
+                self._static_idx.copy_(idx)
+            vec = self._replay_graph(key, lambda: self._direct_body(
+                self.gather_time_major(replay, self._static_idx, S), B, S))
+        else:
+            vec = self._direct_body(self.gather_time_major(replay, idx, S), B, S)
+        return self._finish(vec)
+
+    def _finish(self, vec):
+        metrics = self._metrics_from_vec(vec.clone())
+        self.dp.sync()
+        metrics['grad_norm'] = self.opt.step(self.dp.counts)
+        self.n_steps += 1
+        return metrics
 
     def train_step(self, batch: Dict[str, torch.Tensor]) -> Dict[str, torch.Tensor]:
         """One synchronous DP optimizer step. Returns device-resident metric tensors (no host sync)."""
-        if self._graph_warmup and self.n_steps >= self._graph_warmup:
-            metrics = self._graphed_fwd_bwd(batch)
-        else:
-            metrics = self._fwd_bwd(batch)
+        if self.direct():
+            return self._finish(self._step_direct_batch(batch))
+        metrics = self._fwd_bwd(batch)
         self.dp.sync()
         metrics['grad_norm'] = self.opt.step(self.dp.counts)
         self.n_steps += 1

@@ -367,7 +367,7 @@ class DotaOptimizer:
             # fresh sequences go into the on-HBM ring; minibatches are sampled from it on-device
             self.replay.add(data, version=it)
             for _ in range(cfg.epochs * (n // cfg.batch_size)):
-                m = self.learner.train_step(self.replay.sample(cfg.batch_size, cfg.replay_recent or None))
+                m = self.learner.train_step_replay(self.replay, cfg.batch_size, cfg.replay_recent or None)
                 losses.append(m['loss'])
                 for k, v in m.items():
                     metrics_acc.setdefault(k, []).append(v)

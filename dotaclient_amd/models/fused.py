@@ -236,14 +236,14 @@ class FusedPolicy:
         self.params = [p for _, p in policy.named_parameters()]
         self.fully_fused = not self.cfg.entity_attention and self.cfg.unit_dim == 128 and self.cfg.env_dim == 128
 
-    def apply_direct_grads(self, grads, g):
+    def apply_direct_grads(self, grads, g, written=()):
         """Accumulate precomputed gradients straight into the parameters' ``.grad`` (views of the learner's flat
         buffer) with two multi-tensor kernels, instead of returning 30 tensors to autograd (which launches one
         accumulation copy per parameter, ≈1 ms of host-bound launches per step). ``g`` = upstream gradient
         (None = 1). Records which parameters received a gradient in ``grad_mask`` for the DP has-grad counts."""
         gl, views, mask = [], [], []
-        for p, t in zip(self.params, grads):
-            mask.append(t is not None)
+        for name, p, t in zip(self.param_names, self.params, grads):
+            mask.append(t is not None or name in written)
             if t is None:
                 continue
             if p.grad is None:
@@ -257,6 +257,45 @@ class FusedPolicy:
             self._mask_list = mask
             self.grad_mask = torch.tensor(mask, dtype=torch.float32, device=self.err.device)
         self.direct_used = True
+
+    # ---- direct (autograd-free) learner step support ---------------------------------------------
+    def attach_flat(self, flat: torch.Tensor):
+        """The learner's flat fp32 parameter buffer (every parameter is a view of it): the per-step weight images
+        are gathered from it by one kernel (models/pipelined.py:WeightImages)."""
+        self.flat_buffer = flat
+        self._wimg = None
+
+    def weight_images(self):
+        from .pipelined import WeightImages
+        with_value = self.loss_cfg is None or self.loss_cfg.vf_coef > 0
+        key = (with_value, self.flat_buffer.data_ptr() if getattr(self, 'flat_buffer', None) is not None else None,
+               tuple(p.data_ptr() for p in self.params))
+        if getattr(self, '_wimg', None) is None or self._wimg_key != key:
+            if getattr(self, 'flat_buffer', None) is None:
+                raise RuntimeError('FusedPolicy.attach_flat(flat) must be called before the fused LSTM step')
+            self._wimg = WeightImages(self, self.flat_buffer, with_value)
+            self._wimg_key = key
+        return self._wimg
+
+    def scratch(self, name, shape, dtype, device):
+        d = self.__dict__.setdefault('_scratch', {})
+        t = d.get(name)
+        if t is None or tuple(t.shape) != tuple(shape) or t.dtype != dtype or t.device != torch.device(device):
+            t = d[name] = torch.zeros(shape, dtype=dtype, device=device)
+        return t
+
+    def loss_prep_ws(self, device):
+        return self.scratch('loss_prep_ws', (int(self.C.loss_prep_ws_elems()),), torch.int32, device)
+
+    def train_direct(self, batch_tm, B: int, S: int, cfg=None) -> torch.Tensor:
+        """Autograd-free step over time-major rows (see models/pipelined.py:train_direct); returns the metrics
+        vector. Only for :meth:`use_pipeline` configurations."""
+        from .pipelined import train_direct
+        if cfg is not None:
+            self.loss_cfg = cfg
+        self.refresh()
+        self.direct_used = False
+        return train_direct(self, batch_tm, B, S)
 
     def side_stream(self):
         if getattr(self, '_side', None) is None:
@@ -287,6 +326,13 @@ class FusedPolicy:
             self._inv[self._perm] = torch.arange(self._perm.numel(), device=self._perm.device)
         return self._perm
 
+    def gate_perm_i32(self, H, device):
+        """:meth:`gate_perm` as int32 (the TN GEMM's output row map: unit-major result row m → gate-major row)."""
+        key = (H, str(device))
+        if getattr(self, '_perm32_key', None) != key:
+            self._perm32, self._perm32_key = self.gate_perm(H, device).to(torch.int32).contiguous(), key
+        return self._perm32
+
     def gate_inv(self, H, device):
         """Inverse of :meth:`gate_perm` (unit-major gate rows → PyTorch gate-major rows), cached."""
         self.gate_perm(H, device)
@@ -304,6 +350,15 @@ class FusedPolicy:
                 off += cnt
             self._seg, self._seg_key = seg, key
         return self._seg
+
+    def type_offsets(self, device):
+        """(7,) int32 device tensor: first unit slot of each unit type (+ total), cached."""
+        key = str(device)
+        if getattr(self, '_toff_key', None) != key:
+            import itertools
+            offs = [0] + list(itertools.accumulate(self.cfg.layout.counts))
+            self._toff, self._toff_key = torch.tensor(offs, dtype=torch.int32, device=device), key
+        return self._toff
 
     def refresh(self):
         self.params = [p for _, p in self.policy.named_parameters()]

@@ -1,32 +1,31 @@
-"""Time-chunked, two-stream learner step: everything that is not the LSTM recurrence runs UNDER it.
+"""The fused LSTM learner step: time-major core, weight images, and the autograd-free direct step.
 
-With the XCD-team recurrence (ops/csrc/lstm_team.hip) a batch of 8 sequences occupies one XCD (32 of 256 CUs)
-for the whole forward and backward recurrence — ≈8 ms of a ≈12 ms step — while every other stage (heads GEMMs and
-the fused heads+loss kernel, the weight-gradient GEMMs, the pre-RNN backward, the entity-encoder backward) waits
-for it. Those stages are all row-parallel, so the sequence is cut into ``C`` time chunks and software-pipelined:
+Rows are processed TIME-MAJOR (row = t·B + b) so a time chunk is a contiguous slice of every activation. The
+loss and every gradient are computed in ONE forward pass of explicit kernels (no autograd graph); two ways in:
+
+* :class:`PipelinedPolicyLoss` — an ``autograd.Function`` over batch-major inputs (transposed once on entry) whose
+  ``backward`` only scales the precomputed gradients by the upstream gradient (used by ``Learner.loss`` callers
+  that backprop themselves, and by tests);
+* :func:`train_direct` — the learner's hot path: time-major inputs (gathered straight from the HBM replay,
+  ``learner.engine.Learner.train_step_replay``), loss normalisers from one kernel (``loss_prep``), the per-step
+  working copies of all weights from one gather kernel (``weight_prep``, :class:`WeightImages`), gradients written
+  into the flat gradient buffer by one multi-tensor kernel and the loss + metrics by one kernel
+  (``loss_assemble``) — about 120 fewer launches per step than the autograd route, and the whole step is
+  capturable in one hipGraph.
+
+Time chunks (``DCA_PIPELINE_CHUNKS`` > 1) software-pipeline the step over two streams:
 
     stream L (recurrence):  F0 F1 F2 F3 ............ B3 B2 B1 B0
     stream A (everything):     H0 H1 H2 H3            G3 G2 G1 G0
 
-* ``F_c`` = team-LSTM forward over chunk c (carrying h, c between chunks); ``H_c`` = heads GEMM + heads/loss kernel
-  + the heads backward GEMMs of chunk c (produces ∂L/∂h for chunk c) — overlapped with ``F_{c+1}``;
-* ``B_c`` = team-LSTM backward over chunk c (carrying ∂h, ∂c backwards); ``G_c`` = all weight gradients that
-  depend on chunk c's ∂gates (W_hh, W_ih, biases, pre-RNN, entity encoder incl. ∂W_τ) — overlapped with
-  ``B_{c-1}``.
-
-Measured: overlapping does not pay on MI355X today — GEMMs running on the other XCDs slow the L2-bound team
-recurrence more than they save (10.25 / 10.6 / 11.0 ms per bench step at 1 / 2 / 4 chunks), so the default is one
-chunk; what this Function buys in that setting is a step with NO work in the autograd backward, which is what makes
-the whole forward+backward capturable in one hipGraph (Learner.enable_graph).
-
-Rows are processed TIME-MAJOR (row = t·B + b) so a chunk is a contiguous slice of every activation; the inputs
-are transposed once on entry. The loss and every gradient are computed in the Function's forward (for an upstream
-gradient of 1); ``backward`` only scales them by the actual upstream gradient — the math is identical to
-:class:`~dotaclient_amd.models.fused._PolicyLoss` up to summation order.
+``F_c``/``B_c`` = team-LSTM forward/backward over chunk c, ``H_c`` = heads GEMM + heads/loss kernel + heads backward
+of chunk c, ``G_c`` = the weight gradients that depend on chunk c. Measured on MI355X it does not pay (GEMMs on the
+other XCDs slow the L2-bound recurrence more than they save: 10.25 / 10.6 / 11.0 ms per bench step at 1 / 2 / 4
+chunks), so the default is one chunk.
 """
 from __future__ import annotations
 
-from typing import Dict
+from typing import Dict, List, Optional
 
 import torch
 
@@ -35,13 +34,15 @@ from .policy import TYPE_SUFFIX
 
 LDZ = 160
 
+# parameters whose gradient the direct step accumulates in place (split-K GEMM straight into the flat grad buffer)
+DIRECT_GEMM_GRADS = ('rnn.weight_hh_l0', 'rnn.weight_ih_l0', 'affine_pre_rnn.weight')
+
+METRIC_NAMES = ['loss', 'policy_loss', 'entropy_loss', 'advantage_loss', 'entropy', 'advantage', 'approx_kl',
+                'clipfrac', 'entropy/enum', 'entropy/x', 'entropy/y', 'entropy/target_unit']
+
 
 def _mm(a, b):
     return torch.mm(a, b, out_dtype=torch.float32)
-
-
-def _bf(t):
-    return t.detach().to(torch.bfloat16)
 
 
 def _acc(a, b):
@@ -55,164 +56,274 @@ def chunk_bounds(S: int, chunks: int):
     return [(edges[i], edges[i + 1]) for i in range(c) if edges[i + 1] > edges[i]]
 
 
+class WeightImages:
+    """Per-step working copies of the weights, produced by ONE ``weight_prep`` gather launch from the flat fp32
+    parameter buffer (instead of ≈25 cast / stack / permute / cat launches):
+
+    bf16: ``wt16`` (6,128,128) type weights, ``wtT16`` their transposes, ``wpre16`` (256,896), ``wih16`` (4H,256)
+    rows in unit-major gate order, ``whh16`` (4H,H), ``wcat16`` (LDZ,H) = [attention|enum|x|y|value|0-pad];
+    fp32: ``bt`` (6,128), ``bias4`` (4H) = (b_ih + b_hh) in unit-major gate order, ``bcat`` (LDZ).
+    The index maps are built once from the parameters' offsets in the flat buffer."""
+
+    def __init__(self, fp, flat: torch.Tensor, with_value: bool):
+        cfg = fp.cfg
+        H = cfg.hidden
+        dev = flat.device
+        base = flat.data_ptr()
+        P = dict(zip(fp.param_names, fp.params))
+
+        def idx(name):
+            p = P[name]
+            assert p.is_contiguous() and p.dtype == torch.float32
+            off = (p.data_ptr() - base) // 4
+            assert 0 <= off and off + p.numel() <= flat.numel(), f'{name} is not a view of the flat buffer'
+            return torch.arange(p.numel(), dtype=torch.int64).view(p.shape) + off
+
+        perm = fp.gate_perm(H, 'cpu')
+        neg = lambda *shape: torch.full(shape, -1, dtype=torch.int64)  # noqa: E731
+        wt = torch.stack([idx(f'affine_unit_{s}.weight') for s in TYPE_SUFFIX])
+        head_rows = [idx('affine_unit_attention.weight'), idx('affine_head_enum.weight'),
+                     idx('affine_move_x.weight'), idx('affine_move_y.weight'),
+                     idx('affine_value.weight') if with_value else neg(1, H)]
+        wcat = torch.cat(head_rows + [neg(LDZ - 150, H)], 0)
+        parts16 = {'wt16': wt, 'wtT16': wt.transpose(1, 2).contiguous(), 'wpre16': idx('affine_pre_rnn.weight'),
+                   'wih16': idx('rnn.weight_ih_l0')[perm], 'whh16': idx('rnn.weight_hh_l0'), 'wcat16': wcat}
+        head_b = [idx('affine_unit_attention.bias'), idx('affine_head_enum.bias'), idx('affine_move_x.bias'),
+                  idx('affine_move_y.bias'), idx('affine_value.bias') if with_value else neg(1)]
+        bcat = torch.cat(head_b + [neg(LDZ - 150)])
+        parts32 = {'bt': (torch.stack([idx(f'affine_unit_{s}.bias') for s in TYPE_SUFFIX]), None),
+                   'bias4': (idx('rnn.bias_ih_l0')[perm], idx('rnn.bias_hh_l0')[perm]),
+                   'bcat': (bcat, None)}
+        self.shapes16 = {k: tuple(v.shape) for k, v in parts16.items()}
+        self.shapes32 = {k: tuple(v[0].shape) for k, v in parts32.items()}
+        m16 = torch.cat([v.reshape(-1) for v in parts16.values()])
+        m32 = torch.cat([torch.stack([a.reshape(-1), (b.reshape(-1) if b is not None else neg(a.numel()))], 1)
+                         for a, b in parts32.values()])
+        self.map16 = m16.to(torch.int32).to(dev)
+        self.map32 = m32.to(torch.int32).contiguous().to(dev)
+        self.buf16 = torch.empty(m16.numel(), dtype=torch.bfloat16, device=dev)
+        self.buf32 = torch.empty(m32.shape[0], dtype=torch.float32, device=dev)
+        self.views: Dict[str, torch.Tensor] = {}
+        o = 0
+        for k, shp in self.shapes16.items():
+            n = 1
+            for d in shp:
+                n *= d
+            self.views[k] = self.buf16[o:o + n].view(shp)
+            o += n
+        o = 0
+        for k, shp in self.shapes32.items():
+            n = 1
+            for d in shp:
+                n *= d
+            self.views[k] = self.buf32[o:o + n].view(shp)
+            o += n
+        self.flat = flat
+
+    def refresh(self, C) -> Dict[str, torch.Tensor]:
+        C.weight_prep(self.flat, self.map16, self.buf16, self.map32, self.buf32)
+        return self.views
+
+
+def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], units_t, env_t, act_t, msk_t, adv_t,
+                  ret_t, lpo_t, nret_t, norms, h0, c0, B: int, S: int, gout: Optional[Dict[str, torch.Tensor]] = None):
+    """Loss partials and all parameter gradients of one minibatch, from TIME-MAJOR rows (row = t·B + b).
+
+    ``W`` = :class:`WeightImages` views, ``P`` = fp32 parameters (for the small fp32 weights used directly).
+    ``gout`` (direct mode): parameter name → gradient tensor (a view of the flat gradient buffer); the big
+    weight-gradient GEMMs (W_hh, W_ih, pre-RNN) ACCUMULATE straight into those and are left out of ``grads``.
+    Returns (partials (R,16) f32, logp (N) f32 time-major, grads {param name → tensor})."""
+    from ..ops.gemm import gemm_tn
+    C = fp.C
+    cfg, lc = fp.cfg, fp.loss_cfg
+    N = B * S
+    U = units_t.shape[1]
+    H = cfg.hidden
+    dev = units_t.device
+    counts = list(cfg.layout.counts)
+    main = torch.cuda.current_stream(dev)
+    sL = fp.side_stream()
+    w1, b1 = P['affine_unit_basic_stats.weight'].detach(), P['affine_unit_basic_stats.bias'].detach()
+    we, be = P['affine_env.weight'].detach(), P['affine_env.bias'].detach()
+    wt16, wtT16, wpre16 = W['wt16'], W['wtT16'], W['wpre16']
+    wih16, whh16, wcat16 = W['wih16'], W['whh16'], W['wcat16']
+    bt, bias_p, bcat = W['bt'], W['bias4'], W['bcat']
+    # ---- encoder, pre-RNN, input projection over all rows (row-parallel, fast)
+    x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs))
+    x = torch.relu(_mm(x896, wpre16.t()) + P['affine_pre_rnn.bias'].detach())
+    x16 = x.to(torch.bfloat16)
+    xp4 = _mm(x16, wih16.t()).view(S, B, H, 4)          # the recurrence kernel adds the bias (bias4)
+    hs16 = torch.empty(S, B, H, dtype=torch.bfloat16, device=dev)
+    cs = torch.empty(S, B, H, device=dev)
+    gates4 = torch.empty(S, B, H, 4, device=dev)
+    spans = chunk_bounds(S, fp.chunks)
+    one = len(spans) == 1            # single chunk: outputs are used as produced (no staging copies)
+    if not one:
+        dxh = torch.empty(S, B, H, device=dev)
+        z = torch.empty(N, LDZ, device=dev)
+        dtl = torch.empty(N, U, device=dev)
+        logp = torch.empty(N, device=dev)
+    dWcat = dbcat = None
+    parts: List[torch.Tensor] = []
+    algo = 0 if lc.algo == 'ppo' else 1
+    # ---- forward recurrence on stream L, heads (+ heads backward) per chunk on the main stream
+    ready = torch.cuda.Event()
+    ready.record(main)
+    sL.wait_event(ready)
+    # every recurrence chunk is enqueued up front (the host must never hold the recurrence stream back while it
+    # is busy launching the per-chunk work of the main stream)
+    h_c, c_c = h0.contiguous(), c0.contiguous()
+    fwd_done = []
+    with torch.cuda.stream(sL):
+        for t0, t1 in spans:
+            o = team_fwd(C, xp4[t0:t1], whh16, h_c, c_c, fp.err, False, time_major=True,
+                         hs_out=hs16[t0:t1], cs_out=cs[t0:t1], gates_out=gates4[t0:t1], bias4=bias_p)
+            h_c, c_c = o[4], o[5]
+            e = torch.cuda.Event()
+            e.record(sL)
+            fwd_done.append(e)
+    for (t0, t1), done in zip(spans, fwd_done):
+        main.wait_event(done)
+        r0, r1 = t0 * B, t1 * B
+        xh = hs16[t0:t1].view(-1, H)
+        zc = _mm(xh, wcat16.t()) + bcat
+        dz, dtl_c, part, lp = C.heads_loss(zc, emb[r0:r1], act_t[r0:r1], msk_t[r0:r1], adv_t[r0:r1],
+                                           ret_t[r0:r1], lpo_t[r0:r1], nret_t[r0:r1], norms, algo, False,
+                                           S, B, float(lc.clip_eps), float(lc.entropy_coef), float(lc.vf_coef))
+        parts.append(part)
+        dz16 = dz.to(torch.bfloat16)
+        dWcat = gemm_tn(dz16, xh, out=dWcat, accumulate=dWcat is not None)
+        dbcat = _acc(dbcat, dz.sum(0))
+        if one:
+            z, dtl, logp = zc, dtl_c, lp
+            dxh = _mm(dz16, wcat16).view(S, B, H)
+        else:
+            z[r0:r1].copy_(zc)
+            dtl[r0:r1].copy_(dtl_c)
+            logp[r0:r1].copy_(lp)
+            dxh[t0:t1].copy_(_mm(dz16, wcat16).view(t1 - t0, B, H))
+    heads_done = torch.cuda.Event()
+    heads_done.record(main)
+    # ---- backward recurrence on stream L (reverse chunks), weight gradients per chunk on the main stream
+    grads: Dict[str, torch.Tensor] = {}
+    fp.split_head_grads(dWcat, dbcat, grads)
+    dgates16 = torch.empty(S, B, H, 4, dtype=torch.bfloat16, device=dev)   # ∂gates straight from the kernel
+    db = dbpre = dw1 = db1 = dWt = dbt = dWe = dbe = None
+    gperm = fp.gate_perm_i32(H, dev)
+    # weight-gradient GEMMs: split-K MFMA over the B·S rows (ops/csrc/gemm_tn.hip), written in PyTorch's gate-major
+    # row order through the gate permutation; in direct mode accumulated straight into the flat gradient buffer
+    direct = gout is not None
+    dWhh = gout['rnn.weight_hh_l0'] if direct else torch.zeros(4 * H, H, device=dev)
+    dWih = gout['rnn.weight_ih_l0'] if direct else torch.zeros(4 * H, x16.shape[1], device=dev)
+    dWpre = gout['affine_pre_rnn.weight'] if direct else torch.zeros(wpre16.shape[0], wpre16.shape[1], device=dev)
+    h016 = h0.to(torch.bfloat16)
+    sL.wait_event(heads_done)
+    dh_n = dc_n = None
+    bwd_done = []
+    with torch.cuda.stream(sL):
+        for t0, t1 in reversed(spans):
+            cinit = c0.contiguous() if t0 == 0 else cs[t0 - 1]
+            o = team_bwd(C, dxh[t0:t1], gates4[t0:t1], cs[t0:t1], cinit, dh_n, dc_n, whh16, fp.err,
+                         time_major=True, dg_out=dgates16[t0:t1], dg_bf16=True, want_dbias=True)
+            dh_n, dc_n = o[1], o[2]
+            db = _acc(db, o[3])
+            e = torch.cuda.Event()
+            e.record(sL)
+            bwd_done.append(e)
+    for (t0, t1), done in zip(reversed(spans), bwd_done):
+        main.wait_event(done)
+        r0, r1 = t0 * B, t1 * B
+        n = r1 - r0
+        dG16 = dgates16[t0:t1].view(n, 4 * H)
+        if t0 > 0:
+            gemm_tn(dG16, hs16[t0 - 1:t1 - 1].view(n, H), out=dWhh, perm=gperm, accumulate=True)
+        else:       # h_{t-1} rows: h0 for t = 0, then hs[0 : t1-1] — no concatenation materialised
+            gemm_tn(dG16, hs16[0:t1 - 1].view(n - B, H), out=dWhh, perm=gperm, accumulate=True, b0=h016)
+        gemm_tn(dG16, x16[r0:r1], out=dWih, perm=gperm, accumulate=True)
+        dpre = _mm(dG16, wih16) * (x[r0:r1] > 0)
+        dpre16 = dpre.to(torch.bfloat16)
+        gemm_tn(dpre16, x896[r0:r1], out=dWpre, accumulate=True)
+        dbpre = _acc(dbpre, dpre.sum(0))
+        dx896 = _mm(dpre16, wpre16)
+        dwt_c, dw1_c, db1_c = C.encoder_bwd(units_t[r0:r1], w1, b1, wtT16, dtl[r0:r1], z[r0:r1],
+                                            dx896, arg[r0:r1], counts, bool(cfg.compat_bugs))
+        dw1 = _acc(dw1, dw1_c)
+        db1 = _acc(db1, db1_c)
+        dWt = _acc(dWt, dwt_c)
+        # ∂b_τ, ∂W_env, ∂b_env: one pass over the rows (ops/csrc/glue.hip enc_small_grads)
+        dbt_c, dWe_c, dbe_c = C.enc_small_grads(z[r0:r1], dtl[r0:r1], fp.type_offsets(dev), dx896, env_t[r0:r1],
+                                                we, be, bool(cfg.compat_bugs))
+        dbt = _acc(dbt, dbt_c)
+        dWe = _acc(dWe, dWe_c)
+        dbe = _acc(dbe, dbe_c)
+    inv = fp.gate_inv(H, dev)
+    if not direct:
+        grads['rnn.weight_hh_l0'] = dWhh
+        grads['rnn.weight_ih_l0'] = dWih
+        grads['affine_pre_rnn.weight'] = dWpre
+    grads['rnn.bias_ih_l0'] = db[inv]
+    grads['rnn.bias_hh_l0'] = grads['rnn.bias_ih_l0']
+    grads['affine_pre_rnn.bias'] = dbpre
+    grads['affine_unit_basic_stats.weight'] = dw1
+    grads['affine_unit_basic_stats.bias'] = db1
+    for t, s in enumerate(TYPE_SUFFIX):
+        grads[f'affine_unit_{s}.weight'] = dWt[t]
+        grads[f'affine_unit_{s}.bias'] = dbt[t]
+    grads['affine_env.weight'] = dWe
+    grads['affine_env.bias'] = dbe
+    part = parts[0] if len(parts) == 1 else torch.cat(parts, 0)
+    return part, logp, grads
+
+
 class PipelinedPolicyLoss(torch.autograd.Function):
     @staticmethod
     def forward(ctx, fp, units, env, actions, masks, adv, ret, logp_old, nret, norms, h0, c0, *params):
-        from .fused import tn_splitk
-        C = fp.C
-        cfg, lc = fp.cfg, fp.loss_cfg
         P = dict(zip(fp.param_names, params))
         B, S, U, _ = units.shape
         N = B * S
-        H = cfg.hidden
-        dev = units.device
-        counts = list(cfg.layout.counts)
-        main = torch.cuda.current_stream(dev)
-        sL = fp.side_stream()
         tm = (lambda x: x.reshape(B, S, *x.shape[1:]).transpose(0, 1).reshape(N, *x.shape[1:]).contiguous())
-        # ---- time-major inputs
         units_t = units.transpose(0, 1).reshape(N, U, 10).contiguous()
         env_t = env.transpose(0, 1).reshape(N, 3).contiguous()
-        act_t, msk_t = tm(actions), tm(masks)
-        adv_t, ret_t, lpo_t, nret_t = tm(adv), tm(ret), tm(logp_old), tm(nret)
-        # ---- weights
-        w1, b1 = P['affine_unit_basic_stats.weight'].detach(), P['affine_unit_basic_stats.bias'].detach()
-        wt16 = torch.stack([_bf(P[f'affine_unit_{s}.weight']) for s in TYPE_SUFFIX])
-        bt = torch.stack([P[f'affine_unit_{s}.bias'].detach() for s in TYPE_SUFFIX])
-        we, be = P['affine_env.weight'].detach(), P['affine_env.bias'].detach()
-        wpre16 = _bf(P['affine_pre_rnn.weight'])
-        perm = fp.gate_perm(H, dev)
-        wih16 = _bf(P['rnn.weight_ih_l0'])[perm].contiguous()
-        whh16 = _bf(P['rnn.weight_hh_l0'])
-        bias_p = (P['rnn.bias_ih_l0'].detach() + P['rnn.bias_hh_l0'].detach())[perm].contiguous()
-        wcat, bcat = fp.head_cat(P)
-        wcat16 = wcat.to(torch.bfloat16)
-        # ---- encoder, pre-RNN, input projection over all rows (row-parallel, fast)
-        x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs))
-        x = torch.relu(_mm(x896, wpre16.t()) + P['affine_pre_rnn.bias'].detach())
-        x16 = x.to(torch.bfloat16)
-        xp4 = _mm(x16, wih16.t()).view(S, B, H, 4)          # the recurrence kernel adds the bias (bias4)
-        hs16 = torch.empty(S, B, H, dtype=torch.bfloat16, device=dev)
-        cs = torch.empty(S, B, H, device=dev)
-        gates4 = torch.empty(S, B, H, 4, device=dev)
-        spans = chunk_bounds(S, fp.chunks)
-        one = len(spans) == 1            # single chunk: outputs are used as produced (no staging copies)
-        if not one:
-            dxh = torch.empty(S, B, H, device=dev)
-            z = torch.empty(N, LDZ, device=dev)
-            dtl = torch.empty(N, U, device=dev)
-            logp = torch.empty(N, device=dev)
-        dWcat = dbcat = None
-        parts = []
-        algo = 0 if lc.algo == 'ppo' else 1
-        # ---- forward recurrence on stream L, heads (+ heads backward) per chunk on the main stream
-        ready = torch.cuda.Event()
-        ready.record(main)
-        sL.wait_event(ready)
-        # every recurrence chunk is enqueued up front (the host must never hold the recurrence stream back while it
-        # is busy launching the per-chunk work of the main stream)
-        h_c, c_c = h0.contiguous(), c0.contiguous()
-        fwd_done = []
-        with torch.cuda.stream(sL):
-            for t0, t1 in spans:
-                o = team_fwd(C, xp4[t0:t1], whh16, h_c, c_c, fp.err, False, time_major=True,
-                             hs_out=hs16[t0:t1], cs_out=cs[t0:t1], gates_out=gates4[t0:t1], bias4=bias_p)
-                h_c, c_c = o[4], o[5]
-                e = torch.cuda.Event()
-                e.record(sL)
-                fwd_done.append(e)
-        for (t0, t1), done in zip(spans, fwd_done):
-            main.wait_event(done)
-            r0, r1 = t0 * B, t1 * B
-            xh = hs16[t0:t1].view(-1, H)
-            zc = _mm(xh, wcat16.t()) + bcat
-            dz, dtl_c, part, lp = C.heads_loss(zc, emb[r0:r1], act_t[r0:r1], msk_t[r0:r1], adv_t[r0:r1],
-                                               ret_t[r0:r1], lpo_t[r0:r1], nret_t[r0:r1], norms, algo, False,
-                                               S, B, float(lc.clip_eps), float(lc.entropy_coef), float(lc.vf_coef))
-            parts.append(part.sum(0))
-            dz16 = dz.to(torch.bfloat16)
-            dWcat = _acc(dWcat, _mm(dz16.t(), xh))
-            dbcat = _acc(dbcat, dz.sum(0))
-            if one:
-                z, dtl, logp = zc, dtl_c, lp
-                dxh = _mm(dz16, wcat16).view(S, B, H)
-            else:
-                z[r0:r1].copy_(zc)
-                dtl[r0:r1].copy_(dtl_c)
-                logp[r0:r1].copy_(lp)
-                dxh[t0:t1].copy_(_mm(dz16, wcat16).view(t1 - t0, B, H))
-        heads_done = torch.cuda.Event()
-        heads_done.record(main)
-        # ---- backward recurrence on stream L (reverse chunks), weight gradients per chunk on the main stream
-        grads: Dict[str, torch.Tensor] = {}
-        fp.split_head_grads(dWcat, dbcat, grads)
-        dgates16 = torch.empty(S, B, H, 4, dtype=torch.bfloat16, device=dev)   # ∂gates straight from the kernel
-        dWhh = dWih = db = dWpre = dbpre = dw1 = db1 = dWt = dbt = dWe = dbe = None
-        wtT16 = wt16.transpose(1, 2).contiguous()
-        seg = fp.type_segments(dev)
-        h016 = h0.to(torch.bfloat16)
-        sL.wait_event(heads_done)
-        dh_n = dc_n = None
-        bwd_done = []
-        with torch.cuda.stream(sL):
-            for t0, t1 in reversed(spans):
-                cinit = c0.contiguous() if t0 == 0 else cs[t0 - 1]
-                o = team_bwd(C, dxh[t0:t1], gates4[t0:t1], cs[t0:t1], cinit, dh_n, dc_n, whh16, fp.err,
-                             time_major=True, dg_out=dgates16[t0:t1], dg_bf16=True, want_dbias=True)
-                dh_n, dc_n = o[1], o[2]
-                db = _acc(db, o[3])
-                e = torch.cuda.Event()
-                e.record(sL)
-                bwd_done.append(e)
-        for (t0, t1), done in zip(reversed(spans), bwd_done):
-            main.wait_event(done)
-            r0, r1 = t0 * B, t1 * B
-            n = r1 - r0
-            dG16 = dgates16[t0:t1].view(n, 4 * H)
-            hprev = hs16[t0 - 1:t1 - 1].view(n, H) if t0 > 0 else torch.cat(
-                [h016.unsqueeze(0), hs16[0:t1 - 1]], 0).view(n, H)
-            dWhh = _acc(dWhh, _mm(dG16.t(), hprev))
-            dWih = _acc(dWih, _mm(dG16.t(), x16[r0:r1]))
-            dpre = _mm(dG16, wih16) * (x[r0:r1] > 0)
-            dpre16 = dpre.to(torch.bfloat16)
-            dWpre = _acc(dWpre, _mm(dpre16.t(), x896[r0:r1]))
-            dbpre = _acc(dbpre, dpre.sum(0))
-            dx896 = _mm(dpre16, wpre16)
-            q = z[r0:r1, :128]
-            dwt_c, dw1_c, db1_c = C.encoder_bwd(units_t[r0:r1], w1, b1, wtT16, dtl[r0:r1], z[r0:r1],
-                                                      dx896, arg[r0:r1], counts, bool(cfg.compat_bugs))
-            dw1 = _acc(dw1, dw1_c)
-            db1 = _acc(db1, db1_c)
-            dbt = _acc(dbt, tn_splitk((dtl[r0:r1] @ seg).contiguous(), q.contiguous())
-                       + dx896[:, 128:].reshape(n, 6, 128).sum(0))
-            dWt = _acc(dWt, dwt_c)
-            env_c = env_t[r0:r1]
-            de = dx896[:, :128] * ((env_c @ we.t() + be) > 0)
-            dWe = _acc(dWe, de.t() @ env_c)
-            dbe = _acc(dbe, de.sum(0))
-        inv = fp.gate_inv(H, dev)
-        grads['rnn.weight_hh_l0'] = dWhh[inv]
-        grads['rnn.weight_ih_l0'] = dWih[inv]
-        grads['rnn.bias_ih_l0'] = db[inv]
-        grads['rnn.bias_hh_l0'] = grads['rnn.bias_ih_l0']
-        grads['affine_pre_rnn.weight'] = dWpre
-        grads['affine_pre_rnn.bias'] = dbpre
-        grads['affine_unit_basic_stats.weight'] = dw1
-        grads['affine_unit_basic_stats.bias'] = db1
-        for t, s in enumerate(TYPE_SUFFIX):
-            grads[f'affine_unit_{s}.weight'] = dWt[t]
-            grads[f'affine_unit_{s}.bias'] = dbt[t]
-        grads['affine_env.weight'] = dWe
-        grads['affine_env.bias'] = dbe
+        W = fp.weight_images().refresh(fp.C)
+        part, logp, grads = fused_step_tm(fp, W, P, units_t, env_t, tm(actions), tm(masks), tm(adv), tm(ret),
+                                          tm(logp_old), tm(nret), norms, h0, c0, B, S)
         ctx.grads = [grads.get(nm) for nm in fp.param_names]
         ctx.fp = fp
-        # logp back to batch-major (B·S) row order
-        logp_b = logp.view(S, B).t().reshape(N)
+        logp_b = logp.view(S, B).t().reshape(N)        # back to batch-major (B·S) row order
         ctx.mark_non_differentiable(logp_b)
-        return torch.stack(parts).sum(0), logp_b
+        return part.sum(0), logp_b
 
     @staticmethod
     def backward(ctx, gpart, _glogp):
         ctx.fp.apply_direct_grads(ctx.grads, gpart[15])
         ctx.grads = None
         return (None,) * (12 + len(ctx.fp.param_names))
+
+
+def train_direct(fp, batch_tm: Dict[str, torch.Tensor], B: int, S: int) -> torch.Tensor:
+    """One learner step without autograd: gradients are ADDED into the parameters' ``.grad`` (views of the flat
+    gradient buffer), ``fp.grad_mask`` marks which parameters got one. ``batch_tm`` holds time-major rows
+    (``units (N,U,10)``, ``env (N,3)``, ``actions``/``masks (N,A)`` u8, ``adv``/``ret``/``logp_old``/``norm_ret``
+    (N,)) plus ``h0``/``c0 (B,H)``. Returns the metrics vector (16,) laid out as :data:`METRIC_NAMES`."""
+    C = fp.C
+    lc = fp.loss_cfg
+    N = B * S
+    dev = batch_tm['units'].device
+    norms = fp.scratch('norms', (8,), torch.float32, dev)
+    C.loss_prep(batch_tm['actions'], fp.loss_prep_ws(dev), norms)
+    W = fp.weight_images().refresh(C)
+    P = dict(zip(fp.param_names, fp.params))
+    H = fp.cfg.hidden
+    h0 = batch_tm.get('h0')
+    c0 = batch_tm.get('c0')
+    if h0 is None:
+        h0 = torch.zeros(B, H, device=dev)
+        c0 = torch.zeros(B, H, device=dev)
+    gout = {nm: P[nm].grad for nm in DIRECT_GEMM_GRADS}
+    part, _, grads = fused_step_tm(fp, W, P, batch_tm['units'], batch_tm['env'], batch_tm['actions'],
+                                   batch_tm['masks'], batch_tm['adv'], batch_tm['ret'], batch_tm['logp_old'],
+                                   batch_tm['norm_ret'], norms, h0, c0, B, S, gout=gout)
+    fp.apply_direct_grads([grads.get(nm) for nm in fp.param_names], None, written=set(DIRECT_GEMM_GRADS))
+    out = torch.empty(16, device=dev)
+    C.loss_assemble(part, norms, N, 0 if lc.algo == 'ppo' else 1, float(lc.entropy_coef), float(lc.vf_coef), out)
+    return out

@@ -414,6 +414,111 @@ void returns_scan(torch::Tensor rew, torch::Tensor val, torch::Tensor off, torch
   ema.copy_(ema_out);
 }
 
+// Loss normalisers from the one-hot action rows act (N,A) u8 → norms (8) f32. ws: int32 workspace of
+// 5·loss_prep_blocks() + 1 elements whose last element (the arrival counter) must be zero before the first call
+// (the kernel leaves it zero again, so the op is hipGraph-replayable).
+void loss_prep(torch::Tensor act, torch::Tensor ws, torch::Tensor norms) {
+  CHECK_U8(act); CHECK_I32(ws); CHECK_F32(norms);
+  TORCH_CHECK(act.dim() == 2 && act.size(1) >= 22 && act.size(1) <= 128, "act must be (N, 21+U), U <= 107");
+  const int nb = dca_loss_prep_blocks();
+  TORCH_CHECK(ws.numel() >= 5 * nb + 1 && norms.numel() >= 8, "loss_prep: workspace / norms too small");
+  int* w = ptr<int>(ws);
+  hip_check(dca_loss_prep(ptr<unsigned char>(act), (int)act.size(0), (int)act.size(1), w,
+                          reinterpret_cast<unsigned*>(w + 5 * nb), ptr<float>(norms), cur_stream()),
+            "dca_loss_prep");
+}
+
+int64_t loss_prep_ws_elems() { return 5 * dca_loss_prep_blocks() + 1; }
+
+// Loss scalar + metrics (out (16) f32) from the heads/loss partials part (R,16).
+void loss_assemble(torch::Tensor part, torch::Tensor norms, int64_t N, int64_t algo, double ent_coef, double vf_coef,
+                   torch::Tensor out) {
+  CHECK_F32(part); CHECK_F32(norms); CHECK_F32(out);
+  TORCH_CHECK(part.dim() == 2 && part.size(1) == 16 && out.numel() >= 16 && norms.numel() >= 8,
+              "loss_assemble shapes");
+  hip_check(dca_loss_assemble(ptr<float>(part), (int)part.size(0), ptr<float>(norms), (int)N, (int)algo,
+                              (float)ent_coef, (float)vf_coef, ptr<float>(out), cur_stream()),
+            "dca_loss_assemble");
+}
+
+// Working copies of the weights: dst16[i] = bf16(src[map16[i]]) (0 where map16 < 0),
+// dst32[i] = src[map32[i,0]] + src[map32[i,1]] (negative index = 0 term).
+void weight_prep(torch::Tensor src, torch::Tensor map16, torch::Tensor dst16, torch::Tensor map32,
+                 torch::Tensor dst32) {
+  CHECK_F32(src); CHECK_I32(map16); CHECK_BF16(dst16); CHECK_I32(map32); CHECK_F32(dst32);
+  TORCH_CHECK(map16.numel() == dst16.numel() && map32.numel() == 2 * dst32.numel(), "weight_prep: map sizes");
+  hip_check(dca_weight_prep(ptr<float>(src), ptr<int>(map16), ptr<short>(dst16), (int)dst16.numel(), ptr<int>(map32),
+                            ptr<float>(dst32), (int)dst32.numel(), cur_stream()),
+            "dca_weight_prep");
+}
+
+// C (+)= Aᵀ·B for K-outer bf16 operands (split-K MFMA, ops/csrc/gemm_tn.hip). A (K,M) and B (K-split_rows,N) are
+// row-major with unit column stride (any row stride); optional B0 (split_rows,N) supplies rows k < split_rows of
+// the B operand. C (M',N) f32 with unit column stride; optional perm (M) i32 maps result row m → C row perm[m].
+void gemm_tn(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torch::Tensor> perm, bool accumulate,
+             c10::optional<torch::Tensor> B0) {
+  CHECK_DEV(A); CHECK_DEV(B); CHECK_DEV(C);
+  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 && C.scalar_type() == at::kFloat,
+              "gemm_tn: A, B bf16, C f32");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1 &&
+              C.stride(1) == 1, "gemm_tn: 2-D operands with unit column stride");
+  const int K = A.size(0), M = A.size(1), N = B.size(1);
+  int split_rows = 0;
+  const short* b0 = nullptr;
+  if (B0 && B0->defined()) {
+    CHECK_DEV(*B0);
+    TORCH_CHECK(B0->scalar_type() == at::kBFloat16 && B0->dim() == 2 && B0->size(1) == N && B0->stride(1) == 1 &&
+                B0->stride(0) == B.stride(0), "gemm_tn: B0 must match B's columns and row stride");
+    split_rows = B0->size(0);
+    b0 = ptr<short>(*B0);
+  }
+  TORCH_CHECK(B.size(0) + split_rows == K, "gemm_tn: K mismatch between A and [B0; B]");
+  TORCH_CHECK(M % 8 == 0 && N % 8 == 0 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0,
+              "gemm_tn: M, N and row strides must be multiples of 8 (16-B loads)");
+  const int* pp = nullptr;
+  int64_t crow = M;
+  if (perm && perm->defined()) {
+    CHECK_I32(*perm);
+    TORCH_CHECK(perm->numel() == M, "gemm_tn: perm must have M entries");
+    pp = ptr<int>(*perm);
+    crow = C.size(0);
+  }
+  TORCH_CHECK(C.size(0) >= crow && C.size(1) == N, "gemm_tn: C shape");
+  if (K == 0) {
+    if (!accumulate) C.zero_();
+    return;
+  }
+  int splits, kc, tiles;
+  dca_gemm_tn_plan(M, N, K, &splits, &kc, &tiles);
+  torch::Tensor slab;
+  if (splits > 1) slab = torch::empty({(int64_t)splits * M * N}, C.options());
+  hip_check(dca_gemm_tn(ptr<short>(A), (int)A.stride(0), ptr<short>(B), (int)B.stride(0), b0, split_rows,
+                        ptr<float>(C), (int)C.stride(0), pp, accumulate ? 1 : 0, M, N, K,
+                        splits > 1 ? ptr<float>(slab) : nullptr, cur_stream()),
+            "dca_gemm_tn");
+}
+
+// Entity-encoder small gradients in one pass: returns (dbt (6,128), dWe (128,3), dbe (128)). z (N,ldz) f32 with the
+// pointer query in columns 0..127, dtl (N,U) f32, type_off (7) i32 device unit-slot offsets per type, dx (N,896) f32
+// (∂ of the encoder output x896), env (N,3) f32, we (128,3), be (128) f32.
+std::vector<torch::Tensor> enc_small_grads(torch::Tensor z, torch::Tensor dtl, torch::Tensor type_off, torch::Tensor dx,
+                                           torch::Tensor env, torch::Tensor we, torch::Tensor be, bool compat) {
+  CHECK_DEV(z); CHECK_DT(z, at::kFloat); TORCH_CHECK(z.stride(1) == 1 && z.size(1) >= 128, "z (N, ldz>=128)");
+  CHECK_F32(dtl); CHECK_I32(type_off); CHECK_F32(dx); CHECK_F32(env); CHECK_F32(we); CHECK_F32(be);
+  const int N = z.size(0), U = dtl.size(1);
+  TORCH_CHECK(dtl.size(0) == N && dx.size(0) == N && dx.size(1) == 896 && env.size(0) == N && env.size(1) == 3 &&
+              we.size(0) == 128 && we.size(1) == 3 && be.numel() == 128 && type_off.numel() == 7,
+              "enc_small_grads shapes");
+  auto o = z.options();
+  auto part = torch::empty({(int64_t)dca_enc_small_blocks() * dca_enc_small_out()}, o);
+  auto out = torch::empty({(int64_t)dca_enc_small_out()}, o);
+  hip_check(dca_enc_small_grads(ptr<float>(z), (int)z.stride(0), ptr<float>(dtl), U, ptr<int>(type_off),
+                                ptr<float>(dx), ptr<float>(env), ptr<float>(we), ptr<float>(be), N, compat ? 1 : 0,
+                                ptr<float>(part), ptr<float>(out), cur_stream()),
+            "dca_enc_small_grads");
+  return {out.narrow(0, 0, 768).view({6, 128}), out.narrow(0, 768, 384).view({128, 3}), out.narrow(0, 1152, 128)};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -444,5 +549,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sample_actions", &sample_actions, "fused masked hierarchical Gumbel-max action sampling (actor)");
   m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)", py::arg("gates"),
         py::arg("h"), py::arg("c"), py::arg("h16"), py::arg("active") = py::none());
+  m.def("loss_prep", &loss_prep, "loss normalisers from one-hot action rows (graph-replayable)");
+  m.def("loss_prep_ws_elems", &loss_prep_ws_elems, "int32 workspace elements of loss_prep");
+  m.def("loss_assemble", &loss_assemble, "loss scalar + metrics from heads/loss partials");
+  m.def("weight_prep", &weight_prep, "gather the flat fp32 params into bf16 / fp32 working weight images");
+  m.def("gemm_tn", &gemm_tn, "C (+)= A^T B for K-outer bf16 operands (split-K MFMA, LDS transposed reads)",
+        py::arg("A"), py::arg("B"), py::arg("C"), py::arg("perm") = py::none(), py::arg("accumulate") = false,
+        py::arg("B0") = py::none());
+  m.def("enc_small_grads", &enc_small_grads, "entity-encoder type-bias and env-layer gradients in one pass");
   m.def("returns_scan", &returns_scan, "segmented reverse scan: discounted returns / GAE + per-team EMA normalisation");
 }

@@ -1,0 +1,238 @@
+// Split-K bf16 "TN" GEMM for the learner's weight gradients (gfx950 MFMA): C[M×N] (+)= Aᵀ·B with
+//   A (K×M) bf16 row-major (row stride lda) — e.g. ∂gates (B·S rows × 4H),
+//   B (K×N) bf16 row-major (row stride ldb) — e.g. h_{t-1} / x (B·S rows × H),
+// i.e. both operands are K-OUTER: the reduction runs over the B·S = 11 200 rows of a minibatch. hipBLASLt picks a
+// 64×64 tile with no split-K for these (24-256 workgroups, 23-280 TF/s, ≈80 µs each); here:
+//
+// * 128×128 output tile per 256-thread workgroup (4 waves as 2×2, each 64×64 = 4×4 v_mfma_f32_16x16x32_bf16 tiles);
+// * the K range is split over workgroups (≈256-512 workgroups in flight), each stages 64-row K slabs of A and B
+//   through LDS (double-buffered, coalesced 16-B global loads of whole 256-B rows) and feeds the MFMAs with
+//   ds_read_b64_tr_b16 transposed reads — the operands are stored [k][m] / [k][n] and the MFMA wants k-contiguous
+//   fragments, the hardware transpose read gives exactly that (cdna_hip_programming.md T10);
+// * LDS image swizzle off(row, ch) = 256·row + 16·(ch ^ (((row&3)<<2) | ((row>>2)&3))) (T10 layout (b)): the two
+//   16-lane groups of a half read rows 8 apart in the same columns — conflict-free;
+// * split-K partials go to an fp32 slab; a second, fully parallel launch sums the slabs in fixed order
+//   (deterministic) and writes C, optionally through a row permutation (unit-major → PyTorch gate-major rows) and
+//   optionally accumulating into C (the flat grad). (Summing in the last-arriving workgroup of each tile was 5-10×
+//   slower: one workgroup's serial, latency-bound pass over all slabs of its tile.)
+// * B may be "row-split": rows k < split come from B0 (e.g. h0), rows ≥ split from B shifted by `split` rows —
+//   the LSTM's h_{t-1} operand without materialising the concatenation.
+#include "common.h"
+
+namespace {
+
+using dca::bf16x8;
+using dca::f32x4;
+typedef short bf16x4v __attribute__((ext_vector_type(4)));
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int kThreads = 256;
+constexpr int kTileBytes = BK * 128 * 2;             // one operand stage: 64 rows × 256 B = 16 KB
+
+__device__ __forceinline__ int lds_off(int row, int ch) {   // byte offset of 16-B chunk ch of row
+  return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
+}
+
+struct Args {
+  const short* A; int lda;
+  const short* B; int ldb;
+  const short* B0; int split;
+  float* C; int ldc;
+  const int* perm;      // optional output row map (C row perm[m] receives result row m)
+  float* slab;          // [splits][M][N] fp32 partials (splits > 1)
+  int M, N, K, kc, splits, tiles_n, accumulate;
+};
+
+__device__ __forceinline__ void load_stage(const Args& a, int kbase, int kend, int m_base, int n_base,
+                                           uint4 (&ra)[4], uint4 (&rb)[4]) {
+  const int t = threadIdx.x, ch = t & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (t >> 4) + 16 * i;
+    const int k = kbase + r;
+    uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
+    if (k < kend) {
+      const int m = m_base + ch * 8;
+      if (m < a.M) va = *reinterpret_cast<const uint4*>(a.A + (size_t)k * a.lda + m);
+      const int n = n_base + ch * 8;
+      if (n < a.N) {
+        const short* bp = (k < a.split) ? a.B0 + (size_t)k * a.ldb : a.B + (size_t)(k - a.split) * a.ldb;
+        vb = *reinterpret_cast<const uint4*>(bp + n);
+      }
+    }
+    ra[i] = va;
+    rb[i] = vb;
+  }
+}
+
+__device__ __forceinline__ void store_stage(char* As, char* Bs, const uint4 (&ra)[4], const uint4 (&rb)[4]) {
+  const int t = threadIdx.x, ch = t & 15;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = (t >> 4) + 16 * i;
+    *reinterpret_cast<uint4*>(As + lds_off(r, ch)) = ra[i];
+    *reinterpret_cast<uint4*>(Bs + lds_off(r, ch)) = rb[i];
+  }
+}
+
+// 16x16x32 operand fragment (k = 8·(lane>>4) + j, column c0 + (lane&15)) from a [k][128] swizzled image via two
+// transposed reads (rows k0 + 8g + 4r + q, columns c0 + 4p … 4p+3).
+__device__ __forceinline__ bf16x8 frag_tr(const char* img, int k0, int c0) {
+  const int l = threadIdx.x & 63, g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+  const int ch = (c0 >> 3) + (p >> 1);
+  const int row0 = k0 + 8 * g + q;
+  typedef __attribute__((address_space(3))) bf16x4v lds_v4;
+  const bf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4*)(img + lds_off(row0, ch) + 8 * (p & 1)));
+  const bf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+      (lds_v4*)(img + lds_off(row0 + 4, ch) + 8 * (p & 1)));
+  bf16x8 f;
+  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+  return f;
+}
+
+__global__ __launch_bounds__(kThreads) void gemm_tn_kernel(Args a) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+#define AS(b) (smem + (b) * kTileBytes)
+#define BS(b) (smem + (2 + (b)) * kTileBytes)
+  const int tile = blockIdx.x, split = blockIdx.y;
+  const int tm = tile / a.tiles_n, tn = tile % a.tiles_n;
+  const int m_base = tm * BM, n_base = tn * BN;
+  const int k_lo = split * a.kc, k_hi = min(a.K, k_lo + a.kc);
+  const int w = threadIdx.x >> 6, wm = w & 1, wn = w >> 1;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  uint4 ra[4], rb[4];
+  int buf = 0;
+  if (k_lo < k_hi) {
+    load_stage(a, k_lo, k_hi, m_base, n_base, ra, rb);
+    store_stage(AS(0), BS(0), ra, rb);
+  }
+  __syncthreads();
+  for (int kb = k_lo; kb < k_hi; kb += BK) {
+    const bool more = kb + BK < k_hi;
+    if (more) load_stage(a, kb + BK, k_hi, m_base, n_base, ra, rb);   // in flight during the MFMAs
+#pragma unroll
+    for (int ks = 0; ks < BK / 32; ++ks) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = frag_tr(AS(buf), ks * 32, wm * 64 + i * 16);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = frag_tr(BS(buf), ks * 32, wn * 64 + j * 16);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) store_stage(AS(buf ^ 1), BS(buf ^ 1), ra, rb);
+    __syncthreads();
+    buf ^= 1;
+  }
+
+  // accumulator element (i, j, e): row m = wm*64 + 16i + 4(l>>4) + e, column n = wn*64 + 16j + (l&15)
+  const int l = threadIdx.x & 63;
+  if (a.splits == 1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int m = m_base + wm * 64 + 16 * i + 4 * (l >> 4) + e;
+        if (m >= a.M) continue;
+        float* crow = a.C + (size_t)(a.perm ? a.perm[m] : m) * a.ldc;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = n_base + wn * 64 + 16 * j + (l & 15);
+          if (n < a.N) crow[n] = a.accumulate ? crow[n] + acc[i][j][e] : acc[i][j][e];
+        }
+      }
+    return;
+  }
+  float* slab = a.slab + (size_t)split * a.M * a.N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m_base + wm * 64 + 16 * i + 4 * (l >> 4) + e;
+      if (m >= a.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = n_base + wn * 64 + 16 * j + (l & 15);
+        if (n < a.N) slab[(size_t)m * a.N + n] = acc[i][j][e];
+      }
+    }
+#undef AS
+#undef BS
+}
+
+// Fixed-order (deterministic) sum of the split-K slabs, one float4 of C per thread, optional row map / accumulate.
+__global__ __launch_bounds__(256) void gemm_tn_reduce(const float* __restrict__ slab, int splits, int M, int N,
+                                                      float* __restrict__ C, int ldc, const int* __restrict__ perm,
+                                                      int accumulate) {
+  const int n4 = N >> 2;
+  const size_t plane = (size_t)M * N;
+  for (int idx = blockIdx.x * 256 + threadIdx.x; idx < M * n4; idx += gridDim.x * 256) {
+    const int m = idx / n4, n = (idx % n4) * 4;
+    const f32x4* src = reinterpret_cast<const f32x4*>(slab + (size_t)m * N + n);
+    f32x4 s = __builtin_nontemporal_load(src);
+    int sp = 1;
+    for (; sp + 3 < splits; sp += 4) {
+      const f32x4 v0 = __builtin_nontemporal_load(src + (sp + 0) * (plane / 4));
+      const f32x4 v1 = __builtin_nontemporal_load(src + (sp + 1) * (plane / 4));
+      const f32x4 v2 = __builtin_nontemporal_load(src + (sp + 2) * (plane / 4));
+      const f32x4 v3 = __builtin_nontemporal_load(src + (sp + 3) * (plane / 4));
+      s += v0;
+      s += v1;
+      s += v2;
+      s += v3;
+    }
+    for (; sp < splits; ++sp) s += __builtin_nontemporal_load(src + sp * (plane / 4));
+    float* cp = C + (size_t)(perm ? perm[m] : m) * ldc + n;
+    if (accumulate) {
+      s[0] += cp[0]; s[1] += cp[1]; s[2] += cp[2]; s[3] += cp[3];
+    }
+    cp[0] = s[0]; cp[1] = s[1]; cp[2] = s[2]; cp[3] = s[3];
+  }
+}
+
+}  // namespace
+
+extern "C" void dca_gemm_tn_plan(int M, int N, int K, int* splits, int* kc, int* tiles) {
+  const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
+  const int t = tm * tn;
+  int s = (384 + t - 1) / t;                              // aim at ≈1.5 workgroups per CU
+  const int kmax = (K + BK - 1) / BK;                     // at least one 64-row slab per split
+  if (s > kmax) s = kmax;
+  if (s < 1) s = 1;
+  int c = (K + s - 1) / s;
+  c = (c + BK - 1) / BK * BK;
+  s = (K + c - 1) / c;
+  *splits = s;
+  *kc = c;
+  *tiles = t;
+}
+
+extern "C" hipError_t dca_gemm_tn(const short* A, int lda, const short* B, int ldb, const short* B0, int split_rows,
+                                  float* C, int ldc, const int* perm, int accumulate, int M, int N, int K, float* slab,
+                                  hipStream_t st) {
+  int splits, kc, tiles;
+  dca_gemm_tn_plan(M, N, K, &splits, &kc, &tiles);
+  Args a{A, lda, B, ldb, B0 ? B0 : B, B0 ? split_rows : 0, C, ldc, perm, slab, M, N, K, kc, splits,
+         (N + BN - 1) / BN, accumulate};
+  hipLaunchKernelGGL(gemm_tn_kernel, dim3(tiles, splits), dim3(kThreads), 4 * kTileBytes, st, a);
+  DCA_CHECK_LAUNCH();
+  if (splits > 1) {
+    const int n = M * (N / 4);
+    int blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(gemm_tn_reduce, dim3(blocks), dim3(256), 0, st, slab, splits, M, N, C, ldc, perm, accumulate);
+    DCA_CHECK_LAUNCH();
+  }
+  return hipSuccess;
+}

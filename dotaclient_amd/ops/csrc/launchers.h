@@ -62,4 +62,23 @@ hipError_t dca_returns(const float* rew, int K, const float* val, const int* off
                        float* ret, float* adv, float* norm, float* stats, const float* ema_in, float* ema_out,
                        int mode, int normalize, float gamma, float lam, float factor, float eps, hipStream_t st);
 
+int dca_loss_prep_blocks();
+hipError_t dca_loss_prep(const unsigned char* act, int N, int A, int* partial, unsigned* counter, float* norms,
+                         hipStream_t st);
+hipError_t dca_loss_assemble(const float* part, int nrows, const float* norms, int N, int algo, float ent_coef,
+                             float vf_coef, float* out, hipStream_t st);
+hipError_t dca_weight_prep(const float* src, const int* map16, short* dst16, int n16, const int* map32, float* dst32,
+                           int n32, hipStream_t st);
+
+void dca_gemm_tn_plan(int M, int N, int K, int* splits, int* kc, int* tiles);
+hipError_t dca_gemm_tn(const short* A, int lda, const short* B, int ldb, const short* B0, int split_rows, float* C,
+                       int ldc, const int* perm, int accumulate, int M, int N, int K, float* slab,
+                       hipStream_t st);
+
+int dca_enc_small_out();
+int dca_enc_small_blocks();
+hipError_t dca_enc_small_grads(const float* z, int ldz, const float* dtl, int U, const int* type_off, const float* dx,
+                               const float* env, const float* we, const float* be, int N, int compat, float* part,
+                               float* out, hipStream_t st);
+
 }  // extern "C"

@@ -1,0 +1,20 @@
+"""Python face of the split-K bf16 TN GEMM (``csrc/gemm_tn.hip``): ``C (+)= Aᵀ·B`` for K-outer operands — the
+learner's weight gradients, reduced over the B·S rows of a minibatch."""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from . import require
+
+def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, perm: Optional[torch.Tensor] = None,
+            accumulate: bool = False, b0: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``a`` (K, M) bf16, ``b`` (K - b0_rows, N) bf16 (``b0`` supplies the first rows of the B operand), result
+    (M, N) f32 written to ``out`` (through row map ``perm`` if given; added to it if ``accumulate``)."""
+    C = require()
+    M, N = a.shape[1], b.shape[1]
+    if out is None:
+        out = torch.empty(M if perm is None else int(perm.numel()), N, device=a.device, dtype=torch.float32)
+    C.gemm_tn(a, b, out, perm, bool(accumulate), b0)
+    return out

@@ -84,3 +84,51 @@ def test_graph_captured_step_matches_eager(gpu_ops, monkeypatch, chunks):
     assert b.graph is not None
     torch.testing.assert_close(b.flat.flat, a.flat.flat, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(mb['loss'], ma['loss'], rtol=1e-5, atol=1e-6)
+
+
+def test_direct_replay_step_matches_autograd_step(gpu_ops):
+    """The autograd-free direct step fed from the HBM replay (time-major gather inside the captured graph) updates
+    the parameters exactly like the autograd Function path on the same minibatch."""
+    from dotaclient_amd.learner.replay import HbmReplay
+    torch.manual_seed(0)
+    cfg = get_config('lstm512')
+    pol = Policy(cfg)
+    ref = copy.deepcopy(pol)
+    lc = LossConfig(algo='ppo')
+    a = Learner(pol, lc, device='cuda', backend='fused', dp=False)
+    b = Learner(ref, lc, device='cuda', backend='fused', dp=False)
+    assert b.direct() and b.enable_graph(warmup=1)
+    rep = HbmReplay(6, 40, cfg.layout, cfg.hidden, 'cuda', seed=5)
+    rep.add(make_batch(6, 40, cfg.layout, cfg.hidden, device='cuda', seed=9))
+    for step in range(3):
+        g_state = rep._g.get_state()
+        idx = rep.sample_indices(4)
+        rep._g.set_state(g_state)
+        batch = rep.gather(idx)
+        # a: autograd Function path (loss + backward), b: direct replay path (graph from step 1 on)
+        a.dp.zero_grad()
+        la, ma = a.loss(batch)
+        la.backward()
+        a.dp.has_grad.copy_(a.model.grad_mask)
+        a.dp.sync()
+        ma['grad_norm'] = a.opt.step(a.dp.counts)
+        mb = b.train_step_replay(rep, 4)
+        torch.cuda.synchronize()
+        for k in ('loss', 'policy_loss', 'entropy', 'advantage_loss', 'approx_kl', 'clipfrac', 'grad_norm'):
+            torch.testing.assert_close(mb[k], ma[k].detach(), rtol=2e-4, atol=2e-6, msg=f'step {step} {k}')
+    torch.testing.assert_close(b.flat.flat, a.flat.flat, rtol=1e-5, atol=1e-6)
+
+
+def test_loss_prep_kernel_matches_batch_norms(gpu_ops):
+    from dotaclient_amd.ops.heads import batch_norms
+    cfg = get_config('lstm512')
+    batch = make_batch(5, 301, cfg.layout, cfg.hidden, device='cuda', seed=2)
+    act = batch['actions'].reshape(-1, batch['actions'].shape[-1]).contiguous()
+    ret = batch['ret'].reshape(-1)
+    ref = batch_norms(act, ret, False, 301)
+    ws = torch.zeros(int(gpu_ops.loss_prep_ws_elems()), dtype=torch.int32, device='cuda')
+    out = torch.full((8,), 7.0, device='cuda')
+    for _ in range(3):                           # the self-resetting counter must allow repeated launches
+        gpu_ops.loss_prep(act, ws, out)
+        torch.testing.assert_close(out, ref, rtol=1e-6, atol=0)
+    assert int(ws[-1]) == 0
