@@ -35,7 +35,7 @@ from .policy import TYPE_SUFFIX
 LDZ = 160
 
 # parameters whose gradient the direct step accumulates in place (split-K GEMM straight into the flat grad buffer)
-DIRECT_GEMM_GRADS = ('rnn.weight_hh_l0', 'rnn.weight_ih_l0', 'affine_pre_rnn.weight')
+DIRECT_GEMM_GRADS = ('rnn.weight_hh_l0', 'rnn.weight_ih_l0', 'affine_pre_rnn.weight', 'affine_pre_rnn.bias')
 
 METRIC_NAMES = ['loss', 'policy_loss', 'entropy_loss', 'advantage_loss', 'entropy', 'advantage', 'approx_kl',
                 'clipfrac', 'entropy/enum', 'entropy/x', 'entropy/y', 'entropy/target_unit']
@@ -60,7 +60,8 @@ class WeightImages:
     """Per-step working copies of the weights, produced by ONE ``weight_prep`` gather launch from the flat fp32
     parameter buffer (instead of ≈25 cast / stack / permute / cat launches):
 
-    bf16: ``wt16`` (6,128,128) type weights, ``wtT16`` their transposes, ``wpre16`` (256,896), ``wih16`` (4H,256)
+    bf16: ``wt16`` (6,128,128) type weights, ``wtT16`` their transposes, ``wpre16`` (256,896) + ``bpre16``,
+    ``wih16`` (4H,256)
     rows in unit-major gate order, ``whh16`` (4H,H), ``wcat16`` (LDZ,H) = [attention|enum|x|y|value|0-pad];
     fp32: ``bt`` (6,128), ``bias4`` (4H) = (b_ih + b_hh) in unit-major gate order, ``bcat`` (LDZ).
     The index maps are built once from the parameters' offsets in the flat buffer."""
@@ -87,6 +88,7 @@ class WeightImages:
                      idx('affine_value.weight') if with_value else neg(1, H)]
         wcat = torch.cat(head_rows + [neg(LDZ - 150, H)], 0)
         parts16 = {'wt16': wt, 'wtT16': wt.transpose(1, 2).contiguous(), 'wpre16': idx('affine_pre_rnn.weight'),
+                   'bpre16': idx('affine_pre_rnn.bias'),
                    'wih16': idx('rnn.weight_ih_l0')[perm], 'whh16': idx('rnn.weight_hh_l0'), 'wcat16': wcat}
         head_b = [idx('affine_unit_attention.bias'), idx('affine_head_enum.bias'), idx('affine_move_x.bias'),
                   idx('affine_move_y.bias'), idx('affine_value.bias') if with_value else neg(1)]
@@ -150,8 +152,8 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
     bt, bias_p, bcat = W['bt'], W['bias4'], W['bcat']
     # ---- encoder, pre-RNN, input projection over all rows (row-parallel, fast)
     x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs))
-    x = torch.relu(_mm(x896, wpre16.t()) + P['affine_pre_rnn.bias'].detach())
-    x16 = x.to(torch.bfloat16)
+    # relu(x896·W_preᵀ + b) as ONE hipBLASLt GEMM with a bias+ReLU epilogue, bf16 out (x16 > 0 ⟺ x > 0)
+    x16 = torch._addmm_activation(W['bpre16'], x896, wpre16.t())
     xp4 = _mm(x16, wih16.t()).view(S, B, H, 4)          # the recurrence kernel adds the bias (bias4)
     hs16 = torch.empty(S, B, H, dtype=torch.bfloat16, device=dev)
     cs = torch.empty(S, B, H, device=dev)
@@ -192,8 +194,10 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
                                            S, B, float(lc.clip_eps), float(lc.entropy_coef), float(lc.vf_coef))
         parts.append(part)
         dz16 = dz.to(torch.bfloat16)
-        dWcat = gemm_tn(dz16, xh, out=dWcat, accumulate=dWcat is not None)
-        dbcat = _acc(dbcat, dz.sum(0))
+        first = dWcat is None
+        if first:
+            dbcat = torch.empty(LDZ, device=dev)
+        dWcat = gemm_tn(dz16, xh, out=dWcat, accumulate=not first, colsum=dbcat)
         if one:
             z, dtl, logp = zc, dtl_c, lp
             dxh = _mm(dz16, wcat16).view(S, B, H)
@@ -208,7 +212,7 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
     grads: Dict[str, torch.Tensor] = {}
     fp.split_head_grads(dWcat, dbcat, grads)
     dgates16 = torch.empty(S, B, H, 4, dtype=torch.bfloat16, device=dev)   # ∂gates straight from the kernel
-    db = dbpre = dw1 = db1 = dWt = dbt = dWe = dbe = None
+    db = dw1 = db1 = dWt = dbt = dWe = dbe = None
     gperm = fp.gate_perm_i32(H, dev)
     # weight-gradient GEMMs: split-K MFMA over the B·S rows (ops/csrc/gemm_tn.hip), written in PyTorch's gate-major
     # row order through the gate permutation; in direct mode accumulated straight into the flat gradient buffer
@@ -216,6 +220,7 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
     dWhh = gout['rnn.weight_hh_l0'] if direct else torch.zeros(4 * H, H, device=dev)
     dWih = gout['rnn.weight_ih_l0'] if direct else torch.zeros(4 * H, x16.shape[1], device=dev)
     dWpre = gout['affine_pre_rnn.weight'] if direct else torch.zeros(wpre16.shape[0], wpre16.shape[1], device=dev)
+    dbpre = gout['affine_pre_rnn.bias'] if direct else torch.zeros(wpre16.shape[0], device=dev)
     h016 = h0.to(torch.bfloat16)
     sL.wait_event(heads_done)
     dh_n = dc_n = None
@@ -240,10 +245,9 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
         else:       # h_{t-1} rows: h0 for t = 0, then hs[0 : t1-1] — no concatenation materialised
             gemm_tn(dG16, hs16[0:t1 - 1].view(n - B, H), out=dWhh, perm=gperm, accumulate=True, b0=h016)
         gemm_tn(dG16, x16[r0:r1], out=dWih, perm=gperm, accumulate=True)
-        dpre = _mm(dG16, wih16) * (x[r0:r1] > 0)
-        dpre16 = dpre.to(torch.bfloat16)
-        gemm_tn(dpre16, x896[r0:r1], out=dWpre, accumulate=True)
-        dbpre = _acc(dbpre, dpre.sum(0))
+        # ∂pre-activation of the pre-RNN layer: bf16 GEMM, ReLU mask in one threshold_backward kernel
+        dpre16 = torch.ops.aten.threshold_backward(torch.mm(dG16, wih16), x16[r0:r1], 0)
+        gemm_tn(dpre16, x896[r0:r1], out=dWpre, accumulate=True, colsum=dbpre)
         dx896 = _mm(dpre16, wpre16)
         dwt_c, dw1_c, db1_c = C.encoder_bwd(units_t[r0:r1], w1, b1, wtT16, dtl[r0:r1], z[r0:r1],
                                             dx896, arg[r0:r1], counts, bool(cfg.compat_bugs))
@@ -261,9 +265,9 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
         grads['rnn.weight_hh_l0'] = dWhh
         grads['rnn.weight_ih_l0'] = dWih
         grads['affine_pre_rnn.weight'] = dWpre
+        grads['affine_pre_rnn.bias'] = dbpre
     grads['rnn.bias_ih_l0'] = db[inv]
     grads['rnn.bias_hh_l0'] = grads['rnn.bias_ih_l0']
-    grads['affine_pre_rnn.bias'] = dbpre
     grads['affine_unit_basic_stats.weight'] = dw1
     grads['affine_unit_basic_stats.bias'] = db1
     for t, s in enumerate(TYPE_SUFFIX):

@@ -456,7 +456,7 @@ void weight_prep(torch::Tensor src, torch::Tensor map16, torch::Tensor dst16, to
 // row-major with unit column stride (any row stride); optional B0 (split_rows,N) supplies rows k < split_rows of
 // the B operand. C (M',N) f32 with unit column stride; optional perm (M) i32 maps result row m → C row perm[m].
 void gemm_tn(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torch::Tensor> perm, bool accumulate,
-             c10::optional<torch::Tensor> B0) {
+             c10::optional<torch::Tensor> B0, c10::optional<torch::Tensor> colsum) {
   CHECK_DEV(A); CHECK_DEV(B); CHECK_DEV(C);
   TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 && C.scalar_type() == at::kFloat,
               "gemm_tn: A, B bf16, C f32");
@@ -484,17 +484,26 @@ void gemm_tn(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<to
     crow = C.size(0);
   }
   TORCH_CHECK(C.size(0) >= crow && C.size(1) == N, "gemm_tn: C shape");
+  float* csp = nullptr;
+  if (colsum && colsum->defined()) {
+    CHECK_F32(*colsum);
+    TORCH_CHECK(colsum->numel() >= crow, "gemm_tn: colsum must have one entry per C row");
+    csp = ptr<float>(*colsum);
+  }
   if (K == 0) {
-    if (!accumulate) C.zero_();
+    if (!accumulate) {
+      C.zero_();
+      if (csp) colsum->zero_();
+    }
     return;
   }
   int splits, kc, tiles;
   dca_gemm_tn_plan(M, N, K, &splits, &kc, &tiles);
   torch::Tensor slab;
-  if (splits > 1) slab = torch::empty({(int64_t)splits * M * N}, C.options());
+  if (splits > 1) slab = torch::empty({(int64_t)splits * M * N + (csp ? (int64_t)splits * M : 0)}, C.options());
   hip_check(dca_gemm_tn(ptr<short>(A), (int)A.stride(0), ptr<short>(B), (int)B.stride(0), b0, split_rows,
                         ptr<float>(C), (int)C.stride(0), pp, accumulate ? 1 : 0, M, N, K,
-                        splits > 1 ? ptr<float>(slab) : nullptr, cur_stream()),
+                        splits > 1 ? ptr<float>(slab) : nullptr, csp, cur_stream()),
             "dca_gemm_tn");
 }
 
@@ -555,7 +564,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("weight_prep", &weight_prep, "gather the flat fp32 params into bf16 / fp32 working weight images");
   m.def("gemm_tn", &gemm_tn, "C (+)= A^T B for K-outer bf16 operands (split-K MFMA, LDS transposed reads)",
         py::arg("A"), py::arg("B"), py::arg("C"), py::arg("perm") = py::none(), py::arg("accumulate") = false,
-        py::arg("B0") = py::none());
+        py::arg("B0") = py::none(), py::arg("colsum") = py::none());
   m.def("enc_small_grads", &enc_small_grads, "entity-encoder type-bias and env-layer gradients in one pass");
   m.def("returns_scan", &returns_scan, "segmented reverse scan: discounted returns / GAE + per-team EMA normalisation");
 }

@@ -39,7 +39,8 @@ struct Args {
   const short* B0; int split;
   float* C; int ldc;
   const int* perm;      // optional output row map (C row perm[m] receives result row m)
-  float* slab;          // [splits][M][N] fp32 partials (splits > 1)
+  float* slab;          // [splits][M][N] fp32 partials (splits > 1), then [splits][M] column-sum partials
+  float* colsum;        // optional: colsum[m] (+)= Σ_k A[k][m] (a bias gradient), computed by the tn == 0 tiles
   int M, N, K, kc, splits, tiles_n, accumulate;
 };
 
@@ -72,6 +73,19 @@ __device__ __forceinline__ void store_stage(char* As, char* Bs, const uint4 (&ra
     const int r = (t >> 4) + 16 * i;
     *reinterpret_cast<uint4*>(As + lds_off(r, ch)) = ra[i];
     *reinterpret_cast<uint4*>(Bs + lds_off(r, ch)) = rb[i];
+  }
+}
+
+// running per-thread sums of the 8 A columns this thread stages (ch·8 … ch·8+7), for the optional column sum
+__device__ __forceinline__ void colsum_acc(float (&cs)[8], const uint4 (&ra)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const unsigned w[4] = {ra[i].x, ra[i].y, ra[i].z, ra[i].w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      cs[2 * j] += __uint_as_float(w[j] << 16);
+      cs[2 * j + 1] += __uint_as_float(w[j] & 0xffff0000u);
+    }
   }
 }
 
@@ -109,10 +123,13 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_kernel(Args a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   uint4 ra[4], rb[4];
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  const bool do_cs = a.colsum != nullptr && tn == 0;
   int buf = 0;
   if (k_lo < k_hi) {
     load_stage(a, k_lo, k_hi, m_base, n_base, ra, rb);
     store_stage(AS(0), BS(0), ra, rb);
+    if (do_cs) colsum_acc(cs, ra);
   }
   __syncthreads();
   for (int kb = k_lo; kb < k_hi; kb += BK) {
@@ -131,9 +148,32 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_kernel(Args a) {
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
-    if (more) store_stage(AS(buf ^ 1), BS(buf ^ 1), ra, rb);
+    if (more) {
+      store_stage(AS(buf ^ 1), BS(buf ^ 1), ra, rb);
+      if (do_cs) colsum_acc(cs, ra);
+    }
     __syncthreads();
     buf ^= 1;
+  }
+  if (do_cs) {       // 16 row groups share each column chunk: fixed-order LDS fold, then one value per column
+    float* red = reinterpret_cast<float*>(smem);       // [16][128] (the LDS images are dead after the barrier)
+    const int t = threadIdx.x, ch = t & 15, rg = t >> 4;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) red[rg * 128 + ch * 8 + j] = cs[j];
+    __syncthreads();
+    if (t < 128) {
+      float v = 0.f;
+      for (int g = 0; g < 16; ++g) v += red[g * 128 + t];
+      const int m = m_base + t;
+      if (m < a.M) {
+        if (a.splits == 1) {
+          float* cp = a.colsum + (a.perm ? a.perm[m] : m);
+          *cp = a.accumulate ? *cp + v : v;
+        } else {
+          a.slab[(size_t)a.splits * a.M * a.N + (size_t)split * a.M + m] = v;
+        }
+      }
+    }
   }
 
   // accumulator element (i, j, e): row m = wm*64 + 16i + 4(l>>4) + e, column n = wn*64 + 16j + (l&15)
@@ -174,9 +214,18 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_kernel(Args a) {
 // Fixed-order (deterministic) sum of the split-K slabs, one float4 of C per thread, optional row map / accumulate.
 __global__ __launch_bounds__(256) void gemm_tn_reduce(const float* __restrict__ slab, int splits, int M, int N,
                                                       float* __restrict__ C, int ldc, const int* __restrict__ perm,
-                                                      int accumulate) {
+                                                      int accumulate, float* __restrict__ colsum) {
   const int n4 = N >> 2;
   const size_t plane = (size_t)M * N;
+  if (colsum != nullptr) {
+    const float* cs = slab + (size_t)splits * plane;
+    for (int m = blockIdx.x * 256 + threadIdx.x; m < M; m += gridDim.x * 256) {
+      float v = 0.f;
+      for (int sp = 0; sp < splits; ++sp) v += cs[(size_t)sp * M + m];
+      float* cp = colsum + (perm ? perm[m] : m);
+      *cp = accumulate ? *cp + v : v;
+    }
+  }
   for (int idx = blockIdx.x * 256 + threadIdx.x; idx < M * n4; idx += gridDim.x * 256) {
     const int m = idx / n4, n = (idx % n4) * 4;
     const f32x4* src = reinterpret_cast<const f32x4*>(slab + (size_t)m * N + n);
@@ -220,10 +269,10 @@ extern "C" void dca_gemm_tn_plan(int M, int N, int K, int* splits, int* kc, int*
 
 extern "C" hipError_t dca_gemm_tn(const short* A, int lda, const short* B, int ldb, const short* B0, int split_rows,
                                   float* C, int ldc, const int* perm, int accumulate, int M, int N, int K, float* slab,
-                                  hipStream_t st) {
+                                  float* colsum, hipStream_t st) {
   int splits, kc, tiles;
   dca_gemm_tn_plan(M, N, K, &splits, &kc, &tiles);
-  Args a{A, lda, B, ldb, B0 ? B0 : B, B0 ? split_rows : 0, C, ldc, perm, slab, M, N, K, kc, splits,
+  Args a{A, lda, B, ldb, B0 ? B0 : B, B0 ? split_rows : 0, C, ldc, perm, slab, colsum, M, N, K, kc, splits,
          (N + BN - 1) / BN, accumulate};
   hipLaunchKernelGGL(gemm_tn_kernel, dim3(tiles, splits), dim3(kThreads), 4 * kTileBytes, st, a);
   DCA_CHECK_LAUNCH();
@@ -231,7 +280,8 @@ extern "C" hipError_t dca_gemm_tn(const short* A, int lda, const short* B, int l
     const int n = M * (N / 4);
     int blocks = (n + 255) / 256;
     if (blocks > 4096) blocks = 4096;
-    hipLaunchKernelGGL(gemm_tn_reduce, dim3(blocks), dim3(256), 0, st, slab, splits, M, N, C, ldc, perm, accumulate);
+    hipLaunchKernelGGL(gemm_tn_reduce, dim3(blocks), dim3(256), 0, st, slab, splits, M, N, C, ldc, perm, accumulate,
+                       colsum);
     DCA_CHECK_LAUNCH();
   }
   return hipSuccess;

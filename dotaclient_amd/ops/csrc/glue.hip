@@ -65,12 +65,19 @@ __global__ __launch_bounds__(kPrepThreads) void loss_prep_kernel(const unsigned 
   __syncthreads();
   if (!last) return;
   __threadfence();                                               // acquire every block's partials
-  if (threadIdx.x < 5) {
-    long long tot = 0;
-    for (int b = 0; b < (int)gridDim.x; ++b)
-      tot += __hip_atomic_load(partial + b * 5 + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    red[0][threadIdx.x] = (int)tot;
+  // parallel fold: thread b loads block b's five counts (all loads in flight at once), then a fixed LDS tree
+  __shared__ int fold[kPrepBlocks][5];
+  for (int b = threadIdx.x; b < kPrepBlocks; b += kPrepThreads)
+    for (int i = 0; i < 5; ++i)
+      fold[b][i] = b < (int)gridDim.x
+                       ? __hip_atomic_load(partial + b * 5 + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+  __syncthreads();
+  for (int o = kPrepBlocks / 2; o > 0; o >>= 1) {
+    for (int b = threadIdx.x; b < o; b += kPrepThreads)
+      for (int i = 0; i < 5; ++i) fold[b][i] += fold[b + o][i];
+    __syncthreads();
   }
+  if (threadIdx.x < 5) red[0][threadIdx.x] = fold[0][threadIdx.x];
   __syncthreads();
   if (threadIdx.x == 0) {
     auto inv = [](long long x) { return x > 0 ? 1.f / (float)x : 0.f; };
@@ -164,14 +171,15 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restric
   }
 }
 
-constexpr int kSgBlocks = 128;
+constexpr int kSgBlocks = 256;
+constexpr int kSgPhases = 4;                  // row phases per block (128 columns each)
 constexpr int kSgRows = 32;                       // rows per LDS tile
 constexpr int kSgOut = 6 * 128 + 128 * 3 + 128;   // [dbt | dWe | dbe] per partial
 
-// Thread (phase ph = tid >> 7, column d = tid & 127). Per row n:
+// Thread (row phase ph = tid >> 7, column d = tid & 127). Per row n:
 //   ∂b_τ[d] += q[n,d]·Σ_{u∈τ} dtl[n,u] + dx[n, 128 + 128τ' + d]   (τ' = pool column routed to τ; compat: 5 → 3)
 //   de = dx[n,d]·[env[n]·W_env[d] + b_env[d] > 0];  ∂W_env[d,c] += de·env[n,c];  ∂b_env[d] += de
-__global__ __launch_bounds__(256) void enc_small_grads_kernel(const float* __restrict__ z, int ldz,
+__global__ __launch_bounds__(128 * kSgPhases) void enc_small_grads_kernel(const float* __restrict__ z, int ldz,
                                                               const float* __restrict__ dtl, int U,
                                                               const int* __restrict__ type_off,
                                                               const float* __restrict__ dx, const float* __restrict__ env,
@@ -180,7 +188,7 @@ __global__ __launch_bounds__(256) void enc_small_grads_kernel(const float* __res
   const int d = threadIdx.x & 127, ph = threadIdx.x >> 7;
   __shared__ float s_seg[kSgRows][6];
   __shared__ float s_env[kSgRows][3];
-  __shared__ float red[kSgOut];
+  __shared__ float red[kSgPhases - 1][kSgOut];
   float adbt[6] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, adwe[3] = {0.f, 0.f, 0.f}, adbe = 0.f;
   const float w0 = we[d * 3 + 0], w1 = we[d * 3 + 1], w2 = we[d * 3 + 2], bd = be[d];
   const int rows_per = (N + gridDim.x - 1) / gridDim.x;
@@ -188,16 +196,17 @@ __global__ __launch_bounds__(256) void enc_small_grads_kernel(const float* __res
   for (int t0 = r_lo; t0 < r_hi; t0 += kSgRows) {
     const int nt = min(kSgRows, r_hi - t0);
     __syncthreads();
-    for (int i = threadIdx.x; i < nt * 6; i += 256) {          // per-(row, type) pointer-gradient sums
+    for (int i = threadIdx.x; i < nt * 6; i += 128 * kSgPhases) {   // per-(row, type) pointer-gradient sums
       const int r = i / 6, ty = i % 6;
       const float* dr = dtl + (size_t)(t0 + r) * U;
       float sacc = 0.f;
       for (int u = type_off[ty]; u < type_off[ty + 1]; ++u) sacc += dr[u];
       s_seg[r][ty] = sacc;
     }
-    for (int i = threadIdx.x; i < nt * 3; i += 256) s_env[i / 3][i % 3] = env[(size_t)(t0 + i / 3) * 3 + i % 3];
+    for (int i = threadIdx.x; i < nt * 3; i += 128 * kSgPhases)
+      s_env[i / 3][i % 3] = env[(size_t)(t0 + i / 3) * 3 + i % 3];
     __syncthreads();
-    for (int r = ph; r < nt; r += 2) {
+    for (int r = ph; r < nt; r += kSgPhases) {
       const size_t n = t0 + r;
       const float q = z[n * ldz + d];
       const float* dxr = dx + n * 896;
@@ -219,19 +228,30 @@ __global__ __launch_bounds__(256) void enc_small_grads_kernel(const float* __res
       adbe += de;
     }
   }
-  // combine the two row phases in a fixed order, one partial per block
+  // combine the row phases in a fixed order, one partial per block
   __syncthreads();
-  if (ph == 1) {
-    for (int ty = 0; ty < 6; ++ty) red[ty * 128 + d] = adbt[ty];
-    for (int c = 0; c < 3; ++c) red[768 + d * 3 + c] = adwe[c];
-    red[1152 + d] = adbe;
+  if (ph > 0) {
+    float* rr = red[ph - 1];
+    for (int ty = 0; ty < 6; ++ty) rr[ty * 128 + d] = adbt[ty];
+    for (int c = 0; c < 3; ++c) rr[768 + d * 3 + c] = adwe[c];
+    rr[1152 + d] = adbe;
   }
   __syncthreads();
   if (ph == 0) {
     float* o = part + (size_t)blockIdx.x * kSgOut;
-    for (int ty = 0; ty < 6; ++ty) o[ty * 128 + d] = adbt[ty] + red[ty * 128 + d];
-    for (int c = 0; c < 3; ++c) o[768 + d * 3 + c] = adwe[c] + red[768 + d * 3 + c];
-    o[1152 + d] = adbe + red[1152 + d];
+    for (int ty = 0; ty < 6; ++ty) {
+      float v = adbt[ty];
+      for (int k = 0; k < kSgPhases - 1; ++k) v += red[k][ty * 128 + d];
+      o[ty * 128 + d] = v;
+    }
+    for (int c = 0; c < 3; ++c) {
+      float v = adwe[c];
+      for (int k = 0; k < kSgPhases - 1; ++k) v += red[k][768 + d * 3 + c];
+      o[768 + d * 3 + c] = v;
+    }
+    float v = adbe;
+    for (int k = 0; k < kSgPhases - 1; ++k) v += red[k][1152 + d];
+    o[1152 + d] = v;
   }
 }
 
@@ -267,7 +287,7 @@ extern "C" int dca_enc_small_blocks() { return kSgBlocks; }
 extern "C" hipError_t dca_enc_small_grads(const float* z, int ldz, const float* dtl, int U, const int* type_off,
                                           const float* dx, const float* env, const float* we, const float* be, int N,
                                           int compat, float* part, float* out, hipStream_t st) {
-  hipLaunchKernelGGL(enc_small_grads_kernel, dim3(kSgBlocks), dim3(256), 0, st, z, ldz, dtl, U, type_off, dx, env, we,
+  hipLaunchKernelGGL(enc_small_grads_kernel, dim3(kSgBlocks), dim3(128 * kSgPhases), 0, st, z, ldz, dtl, U, type_off, dx, env, we,
                      be, N, compat, part);
   DCA_CHECK_LAUNCH();
   hipLaunchKernelGGL(enc_small_reduce, dim3((kSgOut + 63) / 64), dim3(256), 0, st, part, kSgBlocks, out);

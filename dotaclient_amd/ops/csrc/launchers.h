@@ -72,7 +72,7 @@ hipError_t dca_weight_prep(const float* src, const int* map16, short* dst16, int
 
 void dca_gemm_tn_plan(int M, int N, int K, int* splits, int* kc, int* tiles);
 hipError_t dca_gemm_tn(const short* A, int lda, const short* B, int ldb, const short* B0, int split_rows, float* C,
-                       int ldc, const int* perm, int accumulate, int M, int N, int K, float* slab,
+                       int ldc, const int* perm, int accumulate, int M, int N, int K, float* slab, float* colsum,
                        hipStream_t st);
 
 int dca_enc_small_out();

@@ -9,12 +9,14 @@ import torch
 from . import require
 
 def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, perm: Optional[torch.Tensor] = None,
-            accumulate: bool = False, b0: Optional[torch.Tensor] = None) -> torch.Tensor:
+            accumulate: bool = False, b0: Optional[torch.Tensor] = None,
+            colsum: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``a`` (K, M) bf16, ``b`` (K - b0_rows, N) bf16 (``b0`` supplies the first rows of the B operand), result
-    (M, N) f32 written to ``out`` (through row map ``perm`` if given; added to it if ``accumulate``)."""
+    (M, N) f32 written to ``out`` (through row map ``perm`` if given; added to it if ``accumulate``). ``colsum``
+    (M,) f32, if given, receives Σ_k a[k, m] the same way (a bias gradient, from the staged bf16 A tiles)."""
     C = require()
     M, N = a.shape[1], b.shape[1]
     if out is None:
         out = torch.empty(M if perm is None else int(perm.numel()), N, device=a.device, dtype=torch.float32)
-    C.gemm_tn(a, b, out, perm, bool(accumulate), b0)
+    C.gemm_tn(a, b, out, perm, bool(accumulate), b0, colsum)
     return out

@@ -35,3 +35,20 @@ def test_gemm_tn_perm_accumulate_rowsplit_strided(gpu_ops):
     ref[perm.long()] += a.float().t() @ b_all.float()
     torch.cuda.synchronize()
     torch.testing.assert_close(out, ref, rtol=1e-4, atol=0.1)
+
+
+@pytest.mark.parametrize('M,N,K', [(160, 512, 11200), (256, 896, 300)])
+def test_gemm_tn_colsum(gpu_ops, M, N, K):
+    """Optional Σ_k A[k, m] (bias gradient) alongside the product, split-K and single-split plans, accumulate."""
+    from dotaclient_amd.ops.gemm import gemm_tn
+    g = torch.Generator(device='cuda').manual_seed(K)
+    a = torch.randn(K, M, device='cuda', generator=g).to(torch.bfloat16)
+    b = torch.randn(K, N, device='cuda', generator=g).to(torch.bfloat16)
+    cs = torch.full((M,), 0.5, device='cuda')
+    out = gemm_tn(a, b, colsum=cs)
+    cs2 = torch.full((M,), 0.5, device='cuda')
+    gemm_tn(a, b, out=out.clone(), accumulate=True, colsum=cs2)
+    torch.cuda.synchronize()
+    ref = a.float().sum(0)
+    torch.testing.assert_close(cs, ref, rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(cs2, ref + 0.5, rtol=1e-4, atol=1e-2)
