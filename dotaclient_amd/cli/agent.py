@@ -33,7 +33,10 @@ def build_parser():
     ap.add_argument('--max-dota-time', type=int, default=600, help='maximum in-game time before restarting')
     ap.add_argument('-l', '--log', dest='log_level', default='INFO',
                     choices=['DEBUG', 'INFO', 'WARNING', 'ERROR', 'CRITICAL'])
-    ap.add_argument('--model', type=str, default=None, help='initial model file (state_dict)')
+    ap.add_argument('--model', type=str, default=None,
+                    help='initial model: a state_dict file or a store URL (<url>#<key>, gs://bucket/path.pt)')
+    ap.add_argument('--artifact-url', type=str, default=None,
+                    help='validation: mirror the tensorboard events file here (reference: GCS)')
     ap.add_argument('--use-latest-weights-prob', type=float, default=1.0)
     # reference: type=bool (any non-empty string is True, quirk §2.9); we parse booleans properly
     ap.add_argument('--validation', type=str2bool, default=False)
@@ -82,7 +85,8 @@ def main(argv=None):
     broker = make_broker(args.broker or f'tcp://{args.ip}:{args.port}')
     ws = WeightStore(cfg, device='cpu')
     if args.model:
-        ws.load_file(args.model)
+        from ..utils.artifacts import resolve_model_path
+        ws.load_file(resolve_model_path(args.model))
     broker.subscribe_model(ws.add_bytes)
     logger.info('waiting for the first model...')
     while not ws.wait_ready(timeout=5.0):
@@ -100,6 +104,12 @@ def main(argv=None):
         return PolicyRunner(policy, device=device, seed=seed_r)
     runner_for = RunnerCache(make_runner, latest_policy=ws.latest_policy)
     metrics = MetricsWriter(args.log_dir) if (args.validation and args.log_dir) else None
+    uploader = None
+    if metrics is not None and args.artifact_url:
+        import os
+        from ..utils.artifacts import Uploader, mirror_events, open_store
+        uploader = Uploader(open_store(args.artifact_url))
+        metrics.on_flush.append(mirror_events(uploader, os.path.basename(os.path.normpath(args.log_dir))))
     config_fn = (lambda: get_1v1_bot_vs_default_config(rng=rng)) if args.validation else get_1v1_selfplay_config
     from ..actor.league import League
     league = None if args.league == 'oldest' else League(ws, mode=args.league, rng=rng)
@@ -121,6 +131,9 @@ def main(argv=None):
     except Exception:   # reference: any exception ends the agent; the supervisor restarts it (agent.py:896-900)
         logger.exception('actor failed')
         return 1
+    finally:
+        if uploader is not None:
+            uploader.flush()
     return 0
 
 

@@ -41,7 +41,10 @@ def build_parser():
     ap.add_argument('--mq-prefetch-count', type=int, default=4)
     ap.add_argument('-l', '--log', dest='log_level', default='INFO',
                     choices=['DEBUG', 'INFO', 'WARNING', 'ERROR', 'CRITICAL'])
-    ap.add_argument('--run-local', type=str2bool, default=True)
+    ap.add_argument('--run-local', type=str2bool, default=None,
+                    help='disable the artifact store (default: on when --artifact-url is not given)')
+    ap.add_argument('--artifact-url', type=str, default=None,
+                    help='mirror checkpoints + events here (dir, file://, or an fsspec URL such as gs://bucket)')
     ap.add_argument('--algo', type=str, default='ppo', choices=['ppo', 'vpg'])
     ap.add_argument('--model-preset', type=str, default='lstm512')
     ap.add_argument('--iterations', type=int, default=10000)
@@ -75,7 +78,9 @@ def main(argv=None):
     cfg = OptimizerConfig(log_dir=args.log_dir, epochs=args.epochs, seq_per_epoch=args.seq_per_epoch,
                           batch_size=args.batch_size, seq_len=args.seq_len, learning_rate=args.learning_rate,
                           entropy_coef=args.entropy_coef, vf_coef=args.vf_coef, pretrained_model=args.pretrained_model,
-                          mq_prefetch_count=args.mq_prefetch_count, run_local=args.run_local,
+                          mq_prefetch_count=args.mq_prefetch_count,
+                          run_local=(args.artifact_url is None) if args.run_local is None else args.run_local,
+                          artifact_url=args.artifact_url,
                           iterations=args.iterations, algo=args.algo, model=args.model_preset, gamma=args.gamma,
                           gae_lambda=args.gae_lambda, clip_eps=args.clip_eps, max_grad_norm=args.max_grad_norm,
                           compat_value_bug=args.compat_value_bug, device=device, backend=args.backend,

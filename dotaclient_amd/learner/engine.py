@@ -253,6 +253,15 @@ class Learner:
     def state_dict(self):
         return {'optimizer': self.opt.state_dict(), 'n_steps': self.n_steps}
 
+    def broadcast_state(self, src: int = 0):
+        """Make every rank's optimizer state (Adam moments, per-parameter step counts) equal to rank ``src``'s."""
+        import torch.distributed as dist
+        for t in (self.opt.exp_avg, self.opt.exp_avg_sq, self.opt.steps):
+            dist.broadcast(t, src)
+        n = torch.tensor([self.n_steps], dtype=torch.int64, device=self.opt.steps.device)
+        dist.broadcast(n, src)
+        self.n_steps = int(n.item())
+
     def load_state_dict(self, d):
         self.opt.load_state_dict(d['optimizer'])
         self.n_steps = d.get('n_steps', 0)

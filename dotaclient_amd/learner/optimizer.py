@@ -77,6 +77,7 @@ class OptimizerConfig:
     replay_capacity: int = 0           # sequences (overrides replay_gb)
     replay_recent: int = 0             # sample from the newest N sequences (0 = whole buffer)
     ingest: str = 'auto'               # 'device' (HIP return/GAE scan over the uploaded rollouts) | 'host' | 'auto'
+    artifact_url: Optional[str] = None  # off-node mirror of checkpoints + events (reference: GCS bucket, §utils.artifacts)
 
 
 class Sequence:
@@ -120,8 +121,19 @@ class DotaOptimizer:
         self.writer = MetricsWriter(cfg.log_dir if self.checkpoint else None)
         self.timer = StageTimer()
         pretrained = cfg.pretrained_model
+        if pretrained:
+            from ..utils.artifacts import resolve_model_path
+            pretrained = resolve_model_path(pretrained)
+        # artifact store (reference: GCS bucket 'dotaservice', disabled by --run-local)
+        from ..utils.artifacts import Uploader, fetch_latest_checkpoint, open_store
+        self.store = open_store(cfg.artifact_url) if (cfg.artifact_url and not cfg.run_local) else None
+        self.store_prefix = os.path.basename(os.path.normpath(cfg.log_dir))
+        self.uploader = Uploader(self.store) if (self.store is not None and self.checkpoint) else None
         trainer_state = None
         latest = ckpt.latest_model(cfg.log_dir)
+        if latest is None and self.store is not None and self.checkpoint:
+            os.makedirs(cfg.log_dir, exist_ok=True)
+            latest = fetch_latest_checkpoint(self.store, self.store_prefix, cfg.log_dir)
         if latest is not None:
             logger.info('resuming from %s', latest)
             self.iteration_start = ckpt.iteration_from_model_filename(latest) + 1
@@ -143,11 +155,14 @@ class DotaOptimizer:
             if self.running.mean[team] is not None:
                 k = self._team_key(team)
                 self.ema[k] = torch.tensor([self.running.mean[team], self.running.std[team], 1.0])
-        # every rank starts from rank 0's iteration (reference workers restart at 1, §2.10-7)
+        # every rank starts from rank 0's iteration (reference workers restart at 1, §2.10-7) and with rank 0's
+        # optimizer state (Adam moments / step counts): identical averaged gradients only keep the replicas in sync
+        # if every replica applies them with the same optimizer state
         if pdist.is_distributed():
             t = torch.tensor([self.iteration_start], device=self.device if self.device.type == 'cuda' else 'cpu')
             torch.distributed.broadcast(t, 0)
             self.iteration_start = int(t.item())
+            self.learner.broadcast_state(0)
         self.corrupt_rollouts = 0
         self.replay = None
         if cfg.replay_capacity or cfg.replay_gb:
@@ -327,8 +342,12 @@ class DotaOptimizer:
     def run(self, iterations: Optional[int] = None):
         cfg = self.cfg
         end = self.iteration_start + iterations if iterations is not None else cfg.iterations
-        for it in range(self.iteration_start, end):
-            self.run_iteration(it)
+        try:
+            for it in range(self.iteration_start, end):
+                self.run_iteration(it)
+        finally:
+            if self.uploader is not None:
+                self.uploader.flush()
         return end
 
     def run_iteration(self, it: int):
@@ -443,12 +462,22 @@ class DotaOptimizer:
                 w.add_scalar('mq_size', qs, it)
             w.flush()
             self.upload_model(version=it)
+            if self.uploader is not None and w.events_filename:
+                # upload a snapshot: the live events file keeps growing while the uploader copies
+                import shutil
+                snap = w.events_filename + '.snapshot'
+                shutil.copyfile(w.events_filename, snap)
+                self.uploader.submit(snap, f'{self.store_prefix}/{os.path.basename(w.events_filename)}')
 
     def upload_model(self, version: int):
         if not self.checkpoint:
             return
         path, data = ckpt.save_model(self.policy.state_dict(), self.cfg.log_dir, version)
-        ckpt.save_trainer_state({'learner': self.learner.state_dict(), 'running': self.running.state_dict(),
-                                 'iteration': version, 'config': asdict(self.cfg)}, self.cfg.log_dir, version)
+        spath = ckpt.save_trainer_state({'learner': self.learner.state_dict(), 'running': self.running.state_dict(),
+                                         'iteration': version, 'config': asdict(self.cfg)}, self.cfg.log_dir, version)
+        if self.uploader is not None:   # reference optimizer.py:713-715 (GCS upload of the model file)
+            self.uploader.submit(path, f'{self.store_prefix}/{os.path.basename(path)}')
+            self.uploader.submit(spath, f'{self.store_prefix}/{os.path.basename(spath)}')
+            self.uploader.flush()       # a pruned file must not vanish before its upload
         ckpt.prune(self.cfg.log_dir, self.cfg.checkpoint_keep)
         self.broker.publish_model(data, version)

@@ -34,6 +34,7 @@ class MetricsWriter:
         self.log_dir = log_dir
         self._jsonl = None
         self.tb = None
+        self.on_flush = []          # callbacks after every flush (e.g. mirror the events file to an artifact store)
         if log_dir:
             os.makedirs(log_dir, exist_ok=True)
             self._jsonl = open(os.path.join(log_dir, jsonl_name), 'a')
@@ -70,6 +71,8 @@ class MetricsWriter:
             self._jsonl.flush()
         if self.tb:
             self.tb.flush()
+        for cb in self.on_flush:
+            cb(self)
 
     def close(self):
         self.flush()

@@ -1,4 +1,6 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_gemm_tn.py -x -v --timeout 120 --timeout-method thread > gpurun_out/gemm_test.log 2>&1 && \
-timeout -k 10 300 python -u scripts/gemm_layouts.py > gpurun_out/gemm_layouts.log 2>&1
+timeout -k 10 300 python -u -m pytest tests/test_lstm_kernel.py tests/test_fused_policy.py -x -v --timeout 120 --timeout-method thread > gpurun_out/lstm_test.log 2>&1 && \
+DCA_TEAM_IOWAVE=0 timeout -k 10 120 python -u scripts/lstm_latency.py team > gpurun_out/lat_old.log 2>&1 && \
+timeout -k 10 120 python -u scripts/lstm_latency.py team > gpurun_out/lat_new.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --actor 0 > gpurun_out/bench.log 2>&1
