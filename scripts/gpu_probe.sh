@@ -1,6 +1,3 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest tests/test_lstm_kernel.py tests/test_fused_policy.py -x -v --timeout 120 --timeout-method thread > gpurun_out/lstm_test.log 2>&1 && \
-DCA_TEAM_IOWAVE=0 timeout -k 10 120 python -u scripts/lstm_latency.py team > gpurun_out/lat_old.log 2>&1 && \
-timeout -k 10 120 python -u scripts/lstm_latency.py team > gpurun_out/lat_new.log 2>&1 && \
-timeout -k 10 300 python -u bench.py --actor 0 > gpurun_out/bench.log 2>&1
+cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof5 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --model 5v5 --steps 3 --warmup 2 --actor 0 > $GRAFT_REPO_ROOT/gpurun_out/prof5.log 2>&1
