@@ -149,7 +149,9 @@ def main():
             'vs_baseline': value / BASELINE_STEPS_PER_S,
             'dtype': 'bf16',
             'data': 'synthetic (on-HBM replay of synthetic 1v1-mid experience, random-init weights)',
-            'config': {'model': f'{args.model} ({cfg.rnn}-{cfg.hidden}, 1v1-mid entity encoder)',
+            'config': {'model': f'{args.model} ({cfg.rnn}-{cfg.hidden}, '
+                                f'{"5v5 entity-attention" if cfg.entity_attention else "1v1-mid entity"} encoder, '
+                                f'{cfg.layout.max_units} units)',
                        'global_batch': args.batch_size * world, 'seq_len': args.seq_len,
                        'parallelism': f'dp{world}', 'algo': args.algo, 'backend': backend},
             'loss_first': loss_val, 'loss_last': final_loss,

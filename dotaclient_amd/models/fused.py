@@ -235,6 +235,9 @@ class FusedPolicy:
         self.param_names: List[str] = [n for n, _ in policy.named_parameters()]
         self.params = [p for _, p in policy.named_parameters()]
         self.fully_fused = not self.cfg.entity_attention and self.cfg.unit_dim == 128 and self.cfg.env_dim == 128
+        # the 5v5 entity-attention encoder has fused kernels on the pipelined (time-major) step only
+        self.attention_fused = (self.cfg.entity_attention and self.cfg.unit_dim == 128 and self.cfg.env_dim == 128
+                                and self.cfg.attention_heads == 4 and self.cfg.layout.max_units == 64)
 
     def apply_direct_grads(self, grads, g, written=()):
         """Accumulate precomputed gradients straight into the parameters' ``.grad`` (views of the learner's flat
@@ -307,7 +310,7 @@ class FusedPolicy:
         bug (its value loss couples all rows of a sequence). ``DCA_PIPELINE=0`` disables it."""
         import os
         lc = self.loss_cfg
-        return (self.fully_fused and self.cfg.rnn == 'lstm' and lstm_impl() == 'team'
+        return ((self.fully_fused or self.attention_fused) and self.cfg.rnn == 'lstm' and lstm_impl() == 'team'
                 and not (lc is not None and lc.compat_value_bug) and os.environ.get('DCA_PIPELINE', '1') != '0')
 
     @property
@@ -351,6 +354,10 @@ class FusedPolicy:
             self._seg, self._seg_key = seg, key
         return self._seg
 
+    def type_offset_list(self):
+        import itertools
+        return [0] + list(itertools.accumulate(self.cfg.layout.counts))
+
     def type_offsets(self, device):
         """(7,) int32 device tensor: first unit slot of each unit type (+ total), cached."""
         key = str(device)
@@ -359,6 +366,14 @@ class FusedPolicy:
             offs = [0] + list(itertools.accumulate(self.cfg.layout.counts))
             self._toff, self._toff_key = torch.tensor(offs, dtype=torch.int32, device=device), key
         return self._toff
+
+    def unit_types(self, device):
+        """(U,) uint8 device tensor: unit slot → unit type index, cached."""
+        key = str(device)
+        if getattr(self, '_utype_key', None) != key:
+            ty = sum([[t] * c for t, c in enumerate(self.cfg.layout.counts)], [])
+            self._utype, self._utype_key = torch.tensor(ty, dtype=torch.uint8, device=device), key
+        return self._utype
 
     def refresh(self):
         self.params = [p for _, p in self.policy.named_parameters()]
@@ -409,7 +424,7 @@ class FusedPolicy:
         adv = batch['adv'].reshape(N).contiguous() if 'adv' in batch else zeros
         lpo = batch['logp_old'].reshape(N).contiguous() if 'logp_old' in batch else zeros
         nret = batch['norm_ret'].reshape(N).contiguous() if 'norm_ret' in batch else zeros
-        if not self.fully_fused:
+        if not self.fully_fused and not self.use_pipeline():
             xh, emb, _, _ = self.trunk(batch['env'], batch['units'], batch.get('h0'), batch.get('c0'))
             w, b = self.head_cat(dict(zip(self.param_names, self.params)), differentiable=True)
             U = emb.shape[2]

@@ -96,11 +96,22 @@ class WeightImages:
         parts32 = {'bt': (torch.stack([idx(f'affine_unit_{s}.bias') for s in TYPE_SUFFIX]), None),
                    'bias4': (idx('rnn.bias_ih_l0')[perm], idx('rnn.bias_hh_l0')[perm]),
                    'bcat': (bcat, None)}
+        if cfg.entity_attention:
+            # 5v5 attention block; the encoder adds b_τ + b_out (residual bias folded into E0, see attn.hip)
+            parts16['wqkv16'] = idx('entity_attn.qkv.weight')
+            parts16['bqkv16'] = idx('entity_attn.qkv.bias')
+            parts16['wout16'] = idx('entity_attn.out.weight')
+            bo = idx('entity_attn.out.bias')
+            parts32['bt'] = (parts32['bt'][0], bo.unsqueeze(0).expand(6, -1))
+            parts32['bout'] = (bo, None)
+            parts32['ln_g'] = (idx('entity_attn.ln.weight'), None)
+            parts32['ln_b'] = (idx('entity_attn.ln.bias'), None)
         self.shapes16 = {k: tuple(v.shape) for k, v in parts16.items()}
         self.shapes32 = {k: tuple(v[0].shape) for k, v in parts32.items()}
         m16 = torch.cat([v.reshape(-1) for v in parts16.values()])
         m32 = torch.cat([torch.stack([a.reshape(-1), (b.reshape(-1) if b is not None else neg(a.numel()))], 1)
                          for a, b in parts32.values()])
+        # (expand() above is a broadcast view; reshape copies it)
         self.map16 = m16.to(torch.int32).to(dev)
         self.map32 = m32.to(torch.int32).contiguous().to(dev)
         self.buf16 = torch.empty(m16.numel(), dtype=torch.bfloat16, device=dev)
@@ -151,7 +162,21 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
     wih16, whh16, wcat16 = W['wih16'], W['whh16'], W['wcat16']
     bt, bias_p, bcat = W['bt'], W['bias4'], W['bcat']
     # ---- encoder, pre-RNN, input projection over all rows (row-parallel, fast)
+    attn = cfg.entity_attention
     x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs))
+    if attn:
+        # 5v5 entity attention (ops/csrc/attn.hip): emb = E0 + b_out here (bias folded into bt)
+        toff = fp.type_offset_list()
+        E0p = emb.view(N * U, 128)
+        Xn, ln_mu, ln_rs = C.ln_fwd(E0p, W['bout'], W['ln_g'], W['ln_b'], 1e-5)
+        QKV = torch.addmm(W['bqkv16'], Xn, W['wqkv16'].t())
+        Oat, lse = C.attn_fwd(QKV)
+        E1 = torch.addmm(E0p, Oat, W['wout16'].t())                 # residual + out-projection, bf16
+        arg = C.attn_pool(E1, toff, x896, bool(cfg.compat_bugs))    # pools of the attended embeddings
+        emb = E1.view(N, U, 128)
+    elif cfg.compat_bugs:   # reference policy.py:127: enemy-tower pool = enemy-nonhero pool
+        x896[:, 768:896] = x896[:, 512:640]
+        arg[:, 5] = arg[:, 3]
     # relu(x896·W_preᵀ + b) as ONE hipBLASLt GEMM with a bias+ReLU epilogue, bf16 out (x16 > 0 ⟺ x > 0)
     x16 = torch._addmm_activation(W['bpre16'], x896, wpre16.t())
     xp4 = _mm(x16, wih16.t()).view(S, B, H, 4)          # the recurrence kernel adds the bias (bias4)
@@ -213,6 +238,13 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
     fp.split_head_grads(dWcat, dbcat, grads)
     dgates16 = torch.empty(S, B, H, 4, dtype=torch.bfloat16, device=dev)   # ∂gates straight from the kernel
     db = dw1 = db1 = dWt = dbt = dWe = dbe = None
+    dgam = dbet = None
+    first_attn = True
+    if attn:
+        dWout = torch.empty(128, 128, device=dev)
+        dbout = torch.empty(128, device=dev)
+        dWqkv = torch.empty(384, 128, device=dev)
+        dbqkv = torch.empty(384, device=dev)
     gperm = fp.gate_perm_i32(H, dev)
     # weight-gradient GEMMs: split-K MFMA over the B·S rows (ops/csrc/gemm_tn.hip), written in PyTorch's gate-major
     # row order through the gate permutation; in direct mode accumulated straight into the flat gradient buffer
@@ -249,15 +281,30 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
         dpre16 = torch.ops.aten.threshold_backward(torch.mm(dG16, wih16), x16[r0:r1], 0)
         gemm_tn(dpre16, x896[r0:r1], out=dWpre, accumulate=True, colsum=dbpre)
         dx896 = _mm(dpre16, wpre16)
+        demb_in = None
+        if attn:
+            # attention block backward over this chunk's rows (unit rows r0·U … r1·U)
+            a0, a1 = r0 * U, r1 * U
+            dE1 = C.attn_demb(dtl[r0:r1], z[r0:r1], dx896, arg[r0:r1], toff, bool(cfg.compat_bugs))
+            gemm_tn(dE1, Oat[a0:a1], out=dWout, accumulate=not first_attn, colsum=dbout)
+            dO = torch.mm(dE1, W['wout16'])
+            dQKV = C.attn_bwd(QKV[a0:a1], Oat[a0:a1], dO, lse[r0:r1])
+            gemm_tn(dQKV, Xn[a0:a1], out=dWqkv, accumulate=not first_attn, colsum=dbqkv)
+            dXn = torch.mm(dQKV, W['wqkv16'])
+            demb_in, dg_c, dbe_c_, dbt_attn = C.ln_bwd(dXn, E0p[a0:a1], W['bout'], W['ln_g'], ln_mu[a0:a1],
+                                                       ln_rs[a0:a1], dE1, fp.unit_types(dev))
+            dgam = _acc(dgam, dg_c)
+            dbet = _acc(dbet, dbe_c_)
+            first_attn = False
         dwt_c, dw1_c, db1_c = C.encoder_bwd(units_t[r0:r1], w1, b1, wtT16, dtl[r0:r1], z[r0:r1],
-                                            dx896, arg[r0:r1], counts, bool(cfg.compat_bugs))
+                                            dx896, arg[r0:r1], counts, bool(cfg.compat_bugs), demb_in=demb_in)
         dw1 = _acc(dw1, dw1_c)
         db1 = _acc(db1, db1_c)
         dWt = _acc(dWt, dwt_c)
         # ∂b_τ, ∂W_env, ∂b_env: one pass over the rows (ops/csrc/glue.hip enc_small_grads)
         dbt_c, dWe_c, dbe_c = C.enc_small_grads(z[r0:r1], dtl[r0:r1], fp.type_offsets(dev), dx896, env_t[r0:r1],
                                                 we, be, bool(cfg.compat_bugs))
-        dbt = _acc(dbt, dbt_c)
+        dbt = _acc(dbt, dbt_attn if attn else dbt_c)
         dWe = _acc(dWe, dWe_c)
         dbe = _acc(dbe, dbe_c)
     inv = fp.gate_inv(H, dev)
@@ -275,6 +322,13 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
         grads[f'affine_unit_{s}.bias'] = dbt[t]
     grads['affine_env.weight'] = dWe
     grads['affine_env.bias'] = dbe
+    if attn:
+        grads['entity_attn.ln.weight'] = dgam
+        grads['entity_attn.ln.bias'] = dbet
+        grads['entity_attn.qkv.weight'] = dWqkv
+        grads['entity_attn.qkv.bias'] = dbqkv
+        grads['entity_attn.out.weight'] = dWout
+        grads['entity_attn.out.bias'] = dbout
     part = parts[0] if len(parts) == 1 else torch.cat(parts, 0)
     return part, logp, grads
 

@@ -1,0 +1,475 @@
+// Entity-attention block of the 5v5 policy (gfx950): pre-LN multi-head self-attention over the unit axis of every
+// timestep row, then max-pool per unit type. PyTorch module: models/policy.py EntityAttention (BASELINE config 4);
+// the 1v1 reference has no attention (policy.py:97-138), the pooling is the reference's K-maxpool.
+//
+//   E0  = W_τ·basic + b_τ                       (encoder_fwd; the kernel adds b_τ + b_out, see ln_fwd)
+//   Xn  = LN(E0)·γ + β                          ln_fwd_kernel   (16 lanes per unit row, stats saved)
+//   QKV = Xn·W_qkvᵀ + b_qkv                     hipBLASLt (bias epilogue)
+//   O   = softmax(Q Kᵀ/√d) V   per (row, head)  attn_fwd_kernel (one wave per (row, head): 64×64 scores in
+//                                               registers, MFMA 16x16x32, P through LDS, log-sum-exp saved)
+//   E1  = E0 + O·W_outᵀ + b_out                 hipBLASLt (residual via beta = 1 on E0 + b_out)
+//   pools, argmax per type of E1                pool_kernel
+// Backward: demb_kernel (∂E1 = dtl⊗q + ∂pool routed to the argmax unit), attn_bwd_kernel (recomputes P from the
+// saved log-sum-exp; dQ, dK, dV), ln_bwd_kernel (∂E0 = ∂E1 + LN'ᵀ∂Xn; ∂γ, ∂β and the per-type ∂b_τ as per-block
+// partials), colsum_kernel (fixed-order partial sums: deterministic). The weight-gradient GEMMs over the N·U
+// unit rows run on gemm_tn (split-K) with their bias column sums.
+//
+// MFMA operand images live in per-wave LDS; fragments that need a column of an image come from
+// ds_read_b64_tr_b16 transposed reads (cdna_hip_programming.md T10), the others from 16-B row reads.
+#include "common.h"
+
+namespace {
+
+using dca::bf16x8;
+using dca::f32x4;
+typedef short bf16x4v __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) bf16x4v lds_v4;
+
+constexpr int kU = 64;        // unit slots per row (5v5 layout)
+constexpr int kD = 128;       // embedding width
+constexpr int kHd = 32;       // head width (4 heads)
+constexpr int kP32 = 40;      // LDS pitch (bf16) of a 64×32 image
+constexpr int kP64 = 72;      // LDS pitch (bf16) of a 64×64 image
+
+// A[m][k] (m = m0 + lane&15, k = k0 + 8·(lane>>4) … +7) from an image stored [m][k]: one 16-B read
+__device__ __forceinline__ bf16x8 frag_row(const short* img, int pitch, int m0, int k0) {
+  const int l = threadIdx.x & 63;
+  return *reinterpret_cast<const bf16x8*>(img + (m0 + (l & 15)) * pitch + k0 + 8 * (l >> 4));
+}
+
+// Fragment whose lane index runs along the image's COLUMNS: element jj of lane l = img[k0 + 8(l>>4) + jj][c0 + (l&15)]
+// (two transposed reads: rows k0 + 8g + q and +4, columns c0 + 4p … 4p+3 supplied by lane 4q+p of each group)
+__device__ __forceinline__ bf16x8 frag_tr(const short* img, int pitch, int k0, int c0) {
+  const int l = threadIdx.x & 63, g = l >> 4, i = l & 15, q = i >> 2, p = i & 3;
+  const short* a = img + (k0 + 8 * g + q) * pitch + c0 + 4 * p;
+  const bf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)a);
+  const bf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a + 4 * pitch));
+  bf16x8 f;
+  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+  return f;
+}
+
+__device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// stage a 64×32 head slice (row stride `stride` elements) into an LDS image [64][kP32]
+__device__ __forceinline__ void stage64x32(short* img, const short* __restrict__ src, int stride) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int idx = l + 64 * it, u = idx >> 2, c = idx & 3;
+    *reinterpret_cast<bf16x8*>(img + u * kP32 + 8 * c) =
+        *reinterpret_cast<const bf16x8*>(src + (size_t)u * stride + 8 * c);
+  }
+}
+
+// ============================================================================================================
+// LayerNorm forward: x = E0' − b_sub (E0' carries b_out, folded into the encoder's type bias), 16 lanes × 8 columns.
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const short* __restrict__ e0, const float* __restrict__ bsub,
+                                                     const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                     short* __restrict__ xn, float* __restrict__ mean,
+                                                     float* __restrict__ rstd, int R, float eps) {
+  const int row = blockIdx.x * 16 + (threadIdx.x >> 4), c0 = (threadIdx.x & 15) * 8;
+  if (row >= R) return;
+  const bf16x8 v = *reinterpret_cast<const bf16x8*>(e0 + (size_t)row * kD + c0);
+  float x[8], s = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    x[j] = dca::bf2f(v[j]) - bsub[c0 + j];
+    s += x[j];
+  }
+  s = dca::group_sum<16>(s);
+  const float mu = s * (1.f / kD);
+  float q = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    x[j] -= mu;
+    q += x[j] * x[j];
+  }
+  q = dca::group_sum<16>(q);
+  const float rs = rsqrtf(q * (1.f / kD) + eps);
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = dca::f2bf(x[j] * rs * gamma[c0 + j] + beta[c0 + j]);
+  *reinterpret_cast<bf16x8*>(xn + (size_t)row * kD + c0) = o;
+  if ((threadIdx.x & 15) == 0) {
+    mean[row] = mu;
+    rstd[row] = rs;
+  }
+}
+
+// ============================================================================================================
+// Attention forward, one wave per (row n, head h) (blockIdx.x = n·4 + h). qkv (N·64, 384) bf16 = [q | k | v],
+// each 4 heads × 32. Writes o (N·64, 128) bf16 and lse (N, 4, 64) f32 (natural-log, scaled scores).
+__global__ __launch_bounds__(64) void attn_fwd_kernel(const short* __restrict__ qkv, short* __restrict__ o,
+                                                      float* __restrict__ lse, float scale) {
+  __shared__ __attribute__((aligned(16))) short Qs[kU * kP32], Ks[kU * kP32], Vs[kU * kP32];
+  __shared__ __attribute__((aligned(16))) short PT[kU * kP64];   // P transposed: [key j][query i]
+  const int n = blockIdx.x >> 2, h = blockIdx.x & 3;
+  const int l = threadIdx.x, kg = l >> 4, li = l & 15;
+  const short* base = qkv + (size_t)n * kU * 384 + h * kHd;
+  stage64x32(Qs, base, 384);
+  stage64x32(Ks, base + 128, 384);
+  stage64x32(Vs, base + 256, 384);
+  __syncthreads();
+  // S = Q Kᵀ: tile (a, b) = queries 16a…, keys 16b…; lane holds rows 16a + 4kg + r, column 16b + li
+  f32x4 s[4][4];
+  bf16x8 qa[4], kb[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) qa[a] = frag_row(Qs, kP32, 16 * a, 0);
+#pragma unroll
+  for (int b = 0; b < 4; ++b) kb[b] = frag_row(Ks, kP32, 16 * b, 0);
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) s[a][b] = mfma(qa[a], kb[b], f32x4{0.f, 0.f, 0.f, 0.f});
+  // row softmax over the 64 keys (4 tiles × 16 lanes)
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float m = fmaxf(fmaxf(s[a][0][r], s[a][1][r]), fmaxf(s[a][2][r], s[a][3][r]));
+      m = dca::group_max<16>(m) * scale;
+      float e[4], sum = 0.f;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        e[b] = __expf(s[a][b][r] * scale - m);
+        sum += e[b];
+      }
+      sum = dca::group_sum<16>(sum);
+      const float inv = 1.f / sum;
+#pragma unroll
+      for (int b = 0; b < 4; ++b) s[a][b][r] = e[b] * inv;
+      if (li == 0) lse[((size_t)n * 4 + h) * kU + 16 * a + 4 * kg + r] = m + __logf(sum);
+    }
+  // P → PT[j][i]: the lane's 4 consecutive queries of one key are one 8-byte write
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      bf16x4v v;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = dca::f2bf(s[a][b][r]);
+      *reinterpret_cast<bf16x4v*>(PT + (16 * b + li) * kP64 + 16 * a + 4 * kg) = v;
+    }
+  __syncthreads();
+  // O = P V: A[i][k=j] = PT[j][i] (transposed read), B[k=j][n=d] = V[j][d] (transposed read)
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) acc = mfma(frag_tr(PT, kP64, 32 * ks, 16 * a), frag_tr(Vs, kP32, 32 * ks, 16 * c), acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        o[((size_t)n * kU + 16 * a + 4 * kg + r) * kD + h * kHd + 16 * c + li] = dca::f2bf(acc[r]);
+    }
+}
+
+// ============================================================================================================
+// Attention backward, one wave per (row, head). do_ (N·64, 128) bf16 = ∂O; writes dqkv (N·64, 384) bf16.
+__global__ __launch_bounds__(64) void attn_bwd_kernel(const short* __restrict__ qkv, const short* __restrict__ o,
+                                                      const short* __restrict__ do_, const float* __restrict__ lse,
+                                                      short* __restrict__ dqkv, float scale) {
+  __shared__ __attribute__((aligned(16))) short Qs[kU * kP32], Ks[kU * kP32], Vs[kU * kP32], Ds[kU * kP32];
+  __shared__ __attribute__((aligned(16))) short PT[kU * kP64], ST[kU * kP64];   // Pᵀ and (scale·dS)ᵀ, [j][i]
+  __shared__ float Dl[kU], Ll[kU];
+  const int n = blockIdx.x >> 2, h = blockIdx.x & 3;
+  const int l = threadIdx.x, kg = l >> 4, li = l & 15;
+  const short* base = qkv + (size_t)n * kU * 384 + h * kHd;
+  stage64x32(Qs, base, 384);
+  stage64x32(Ks, base + 128, 384);
+  stage64x32(Vs, base + 256, 384);
+  stage64x32(Ds, do_ + (size_t)n * kU * kD + h * kHd, kD);
+  {  // D_i = Σ_d ∂O[i][d]·O[i][d] (lane = query i), LSE
+    const short* orow = o + ((size_t)n * kU + l) * kD + h * kHd;
+    const short* drow = do_ + ((size_t)n * kU + l) * kD + h * kHd;
+    float d = 0.f;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const bf16x8 ov = *reinterpret_cast<const bf16x8*>(orow + 8 * c);
+      const bf16x8 dv = *reinterpret_cast<const bf16x8*>(drow + 8 * c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) d += dca::bf2f(ov[j]) * dca::bf2f(dv[j]);
+    }
+    Dl[l] = d;
+    Ll[l] = lse[((size_t)n * 4 + h) * kU + l];
+  }
+  __syncthreads();
+  f32x4 p[4][4], dp[4][4];
+  {
+    bf16x8 qa[4], kb[4], da[4], vb[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      qa[a] = frag_row(Qs, kP32, 16 * a, 0);
+      da[a] = frag_row(Ds, kP32, 16 * a, 0);
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      kb[b] = frag_row(Ks, kP32, 16 * b, 0);
+      vb[b] = frag_row(Vs, kP32, 16 * b, 0);
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        p[a][b] = mfma(qa[a], kb[b], f32x4{0.f, 0.f, 0.f, 0.f});
+        dp[a][b] = mfma(da[a], vb[b], f32x4{0.f, 0.f, 0.f, 0.f});
+      }
+  }
+  // P = exp(scale·S − LSE); scale·dS = scale·P∘(dP − D); both stored transposed
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      bf16x4v pv, sv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * a + 4 * kg + r;
+        const float pr = __expf(p[a][b][r] * scale - Ll[i]);
+        pv[r] = dca::f2bf(pr);
+        sv[r] = dca::f2bf(scale * pr * (dp[a][b][r] - Dl[i]));
+      }
+      *reinterpret_cast<bf16x4v*>(PT + (16 * b + li) * kP64 + 16 * a + 4 * kg) = pv;
+      *reinterpret_cast<bf16x4v*>(ST + (16 * b + li) * kP64 + 16 * a + 4 * kg) = sv;
+    }
+  __syncthreads();
+  short* out = dqkv + (size_t)n * kU * 384 + h * kHd;
+  // dV = Pᵀ ∂O and dK = dSᵀ Q: C[j][d]; A[j][k=i] row reads of PT / ST, B[k=i][n=d] transposed reads of ∂O / Q
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 av = {0.f, 0.f, 0.f, 0.f}, ak = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        av = mfma(frag_row(PT, kP64, 16 * b, 32 * ks), frag_tr(Ds, kP32, 32 * ks, 16 * c), av);
+        ak = mfma(frag_row(ST, kP64, 16 * b, 32 * ks), frag_tr(Qs, kP32, 32 * ks, 16 * c), ak);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const size_t j = 16 * b + 4 * kg + r;
+        out[j * 384 + 256 + 16 * c + li] = dca::f2bf(av[r]);
+        out[j * 384 + 128 + 16 * c + li] = dca::f2bf(ak[r]);
+      }
+    }
+  // dQ = dS K: C[i][d]; A[i][k=j] = STᵀ (transposed read), B[k=j][n=d] = K (transposed read)
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 aq = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) aq = mfma(frag_tr(ST, kP64, 32 * ks, 16 * a), frag_tr(Ks, kP32, 32 * ks, 16 * c), aq);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(size_t)(16 * a + 4 * kg + r) * 384 + 16 * c + li] = dca::f2bf(aq[r]);
+    }
+}
+
+// ============================================================================================================
+// Max-pool + argmax per unit type over the attended embeddings E1 (N·64, 128) bf16 → x896[:, 128 + 128τ + c] and
+// arg (N, 6, 128) u8 (first maximum, like the fused 1v1 encoder). compat: the enemy-tower pool reuses the
+// enemy-nonhero pool (reference policy.py:127). One block of 128 threads (= columns) per row.
+struct TypeOff {
+  int off[7];
+};
+
+__global__ __launch_bounds__(128) void pool_kernel(const short* __restrict__ e1, TypeOff T, short* __restrict__ x896,
+                                                   unsigned char* __restrict__ arg, int compat) {
+  const int n = blockIdx.x, c = threadIdx.x;
+  const short* rowp = e1 + (size_t)n * kU * kD + c;
+#pragma unroll
+  for (int t = 0; t < 6; ++t) {
+    const int src = (compat && t == 5) ? 3 : t;
+    float m = -INFINITY;
+    int am = 0;
+    for (int u = T.off[src]; u < T.off[src + 1]; ++u) {
+      const float v = dca::bf2f(rowp[(size_t)u * kD]);
+      if (v > m) {
+        m = v;
+        am = u - T.off[src];
+      }
+    }
+    x896[(size_t)n * 896 + kD + t * kD + c] = dca::f2bf(m);
+    arg[((size_t)n * 6 + t) * kD + c] = (unsigned char)am;
+  }
+}
+
+// ∂E1[n,u,c] = dtl[n,u]·q[n,c] + Σ_τ [u = off_τ + arg[n,τ,c]]·∂pool_τ[n,c] (compat: the eth pool's gradient goes to
+// the enh argmax). One block of 128 threads per row; the row's 64 dtl values via LDS.
+__global__ __launch_bounds__(128) void demb_kernel(const float* __restrict__ dtl, const float* __restrict__ q, int ldq,
+                                                   const float* __restrict__ dx, const unsigned char* __restrict__ arg,
+                                                   TypeOff T, short* __restrict__ de1, int compat) {
+  const int n = blockIdx.x, c = threadIdx.x;
+  __shared__ float sd[kU];
+  if (c < kU) sd[c] = dtl[(size_t)n * kU + c];
+  __syncthreads();
+  const float qc = q[(size_t)n * ldq + c];
+  int au[6];
+  float dp[6];
+#pragma unroll
+  for (int t = 0; t < 6; ++t) {
+    const int src = (compat && t == 5) ? 3 : t;
+    au[t] = T.off[src] + arg[((size_t)n * 6 + t) * kD + c];
+    dp[t] = dx[(size_t)n * 896 + kD + t * kD + c];
+  }
+  short* out = de1 + (size_t)n * kU * kD + c;
+  for (int u = 0; u < kU; ++u) {
+    float v = sd[u] * qc;
+#pragma unroll
+    for (int t = 0; t < 6; ++t) v += (au[t] == u) ? dp[t] : 0.f;
+    out[(size_t)u * kD] = dca::f2bf(v);
+  }
+}
+
+// ============================================================================================================
+// LayerNorm backward + residual: ∂E0 = ∂E1 + rstd·(g − mean(g) − x̂·mean(g∘x̂)), g = ∂Xn∘γ. Per-block partials
+// [∂γ (128) | ∂β (128) | ∂b_τ (6×128)]; the type of unit row r is type_of[r % 64]. 16 lanes × 8 columns per row,
+// 16 rows per pass, grid-stride over the rows.
+constexpr int kLnPart = 2 * kD + 6 * kD;
+
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const short* __restrict__ dxn, const short* __restrict__ e0,
+                                                     const float* __restrict__ bsub, const float* __restrict__ gamma,
+                                                     const float* __restrict__ mean, const float* __restrict__ rstd,
+                                                     const short* __restrict__ de1, const unsigned char* type_of,
+                                                     short* __restrict__ de0, float* __restrict__ part, int R) {
+  const int lr = threadIdx.x >> 4, c0 = (threadIdx.x & 15) * 8;
+  float gacc[8], bacc[8], tacc[6][8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    gacc[j] = bacc[j] = 0.f;
+#pragma unroll
+    for (int t = 0; t < 6; ++t) tacc[t][j] = 0.f;
+  }
+  float gm[8], bs[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    gm[j] = gamma[c0 + j];
+    bs[j] = bsub[c0 + j];
+  }
+  for (int row = blockIdx.x * 16 + lr; row < R; row += gridDim.x * 16) {
+    const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dxn + (size_t)row * kD + c0);
+    const bf16x8 ev = *reinterpret_cast<const bf16x8*>(e0 + (size_t)row * kD + c0);
+    const bf16x8 rv = *reinterpret_cast<const bf16x8*>(de1 + (size_t)row * kD + c0);
+    const float mu = mean[row], rs = rstd[row];
+    float xh[8], g[8], s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      xh[j] = (dca::bf2f(ev[j]) - bs[j] - mu) * rs;
+      const float d = dca::bf2f(dv[j]);
+      g[j] = d * gm[j];
+      s1 += g[j];
+      s2 += g[j] * xh[j];
+      gacc[j] += d * xh[j];
+      bacc[j] += d;
+    }
+    s1 = dca::group_sum<16>(s1) * (1.f / kD);
+    s2 = dca::group_sum<16>(s2) * (1.f / kD);
+    const int t = type_of[row % kU];
+    bf16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v = dca::bf2f(rv[j]) + rs * (g[j] - s1 - xh[j] * s2);
+      o[j] = dca::f2bf(v);
+#pragma unroll
+      for (int tt = 0; tt < 6; ++tt) tacc[tt][j] += (tt == t) ? v : 0.f;
+    }
+    *reinterpret_cast<bf16x8*>(de0 + (size_t)row * kD + c0) = o;
+  }
+  // fixed-order block reduction over the 16 row lanes → one partial per block
+  __shared__ float red[16][kLnPart];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    red[lr][c0 + j] = gacc[j];
+    red[lr][kD + c0 + j] = bacc[j];
+#pragma unroll
+    for (int t = 0; t < 6; ++t) red[lr][2 * kD + t * kD + c0 + j] = tacc[t][j];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < kLnPart; e += 256) {
+    float v = 0.f;
+    for (int k = 0; k < 16; ++k) v += red[k][e];
+    part[(size_t)blockIdx.x * kLnPart + e] = v;
+  }
+}
+
+// out[c] = Σ_b part[b][c] in block order (deterministic); 64 columns × 4 row phases per block.
+__global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ part, int nblk, int W,
+                                                     float* __restrict__ out) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
+  float s = 0.f;
+  if (c < W) {
+    int b = ph;
+    for (; b + 12 < nblk; b += 16) {
+      const float v0 = part[(size_t)b * W + c], v1 = part[(size_t)(b + 4) * W + c];
+      const float v2 = part[(size_t)(b + 8) * W + c], v3 = part[(size_t)(b + 12) * W + c];
+      s += v0;
+      s += v1;
+      s += v2;
+      s += v3;
+    }
+    for (; b < nblk; b += 4) s += part[(size_t)b * W + c];
+  }
+  __shared__ float red[4][64];
+  red[ph][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (ph == 0 && c < W) out[c] = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+
+}  // namespace
+
+extern "C" int dca_ln_part_width() { return kLnPart; }
+
+extern "C" hipError_t dca_ln_fwd(const short* e0, const float* bsub, const float* gamma, const float* beta, short* xn,
+                                 float* mean, float* rstd, int R, float eps, hipStream_t st) {
+  hipLaunchKernelGGL(ln_fwd_kernel, dim3((R + 15) / 16), dim3(256), 0, st, e0, bsub, gamma, beta, xn, mean, rstd, R,
+                     eps);
+  DCA_CHECK_LAUNCH();
+  return hipSuccess;
+}
+
+extern "C" hipError_t dca_attn_fwd(const short* qkv, short* o, float* lse, int N, float scale, hipStream_t st) {
+  hipLaunchKernelGGL(attn_fwd_kernel, dim3(N * 4), dim3(64), 0, st, qkv, o, lse, scale);
+  DCA_CHECK_LAUNCH();
+  return hipSuccess;
+}
+
+extern "C" hipError_t dca_attn_bwd(const short* qkv, const short* o, const short* dout, const float* lse, short* dqkv,
+                                   int N, float scale, hipStream_t st) {
+  hipLaunchKernelGGL(attn_bwd_kernel, dim3(N * 4), dim3(64), 0, st, qkv, o, dout, lse, dqkv, scale);
+  DCA_CHECK_LAUNCH();
+  return hipSuccess;
+}
+
+extern "C" hipError_t dca_attn_pool(const short* e1, const int* type_off, short* x896, unsigned char* arg, int N,
+                                    int compat, hipStream_t st) {
+  TypeOff T;
+  for (int i = 0; i < 7; ++i) T.off[i] = type_off[i];
+  hipLaunchKernelGGL(pool_kernel, dim3(N), dim3(128), 0, st, e1, T, x896, arg, compat);
+  DCA_CHECK_LAUNCH();
+  return hipSuccess;
+}
+
+extern "C" hipError_t dca_attn_demb(const float* dtl, const float* q, int ldq, const float* dx,
+                                    const unsigned char* arg, const int* type_off, short* de1, int N, int compat,
+                                    hipStream_t st) {
+  TypeOff T;
+  for (int i = 0; i < 7; ++i) T.off[i] = type_off[i];
+  hipLaunchKernelGGL(demb_kernel, dim3(N), dim3(128), 0, st, dtl, q, ldq, dx, arg, T, de1, compat);
+  DCA_CHECK_LAUNCH();
+  return hipSuccess;
+}
+
+extern "C" hipError_t dca_ln_bwd(const short* dxn, const short* e0, const float* bsub, const float* gamma,
+                                 const float* mean, const float* rstd, const short* de1, const unsigned char* type_of,
+                                 short* de0, float* part, int nblk, float* out, int R, hipStream_t st) {
+  hipLaunchKernelGGL(ln_bwd_kernel, dim3(nblk), dim3(256), 0, st, dxn, e0, bsub, gamma, mean, rstd, de1, type_of, de0,
+                     part, R);
+  DCA_CHECK_LAUNCH();
+  hipLaunchKernelGGL(colsum_kernel, dim3((kLnPart + 63) / 64), dim3(256), 0, st, part, nblk, kLnPart, out);
+  DCA_CHECK_LAUNCH();
+  return hipSuccess;
+}

@@ -288,7 +288,8 @@ std::vector<torch::Tensor> encoder_fwd(torch::Tensor units, torch::Tensor env, t
 // Returns (demb bf16 (U*N,128) type-major, basic bf16 (U*N,128) type-major, dw1 (128,10) f32, db1 (128) f32).
 std::vector<torch::Tensor> encoder_bwd(torch::Tensor units, torch::Tensor w1, torch::Tensor b1, torch::Tensor wtT,
                                        torch::Tensor dtl, torch::Tensor q, torch::Tensor dx, torch::Tensor arg,
-                                       std::vector<int64_t> counts, bool compat) {
+                                       std::vector<int64_t> counts, bool compat,
+                                       c10::optional<torch::Tensor> demb_in) {
   CHECK_F32(units); CHECK_F32(w1); CHECK_F32(b1); CHECK_BF16(wtT); CHECK_F32(dtl); CHECK_F32(dx); CHECK_U8(arg);
   CHECK_DEV(q); CHECK_DT(q, at::kFloat);
   const int N = units.size(0), U = units.size(1);
@@ -306,10 +307,16 @@ std::vector<torch::Tensor> encoder_bwd(torch::Tensor units, torch::Tensor w1, to
   auto db1 = torch::empty({128}, o);
   const size_t wsb = dca_encoder_bwd_workspace(N, U, c);
   auto ws = torch::empty({(int64_t)((wsb + 3) / 4)}, o);
+  const short* dein = nullptr;
+  if (demb_in && demb_in->defined()) {
+    CHECK_BF16(*demb_in);
+    TORCH_CHECK(demb_in->numel() == (int64_t)N * U * 128, "demb_in must be (N, U, 128)");
+    dein = ptr<short>(*demb_in);
+  }
   hip_check(dca_encoder_bwd(ptr<float>(units), ptr<float>(w1), ptr<float>(b1), ptr<short>(wtT), ptr<float>(dtl),
                             ptr<float>(q), (int)q.stride(0), ptr<float>(dx), ptr<unsigned char>(arg), ptr<float>(dwt),
                             ptr<float>(dw1), ptr<float>(db1), ws.data_ptr(), wsb, N, U, c, compat ? 1 : 0,
-                            cur_stream()),
+                            cur_stream(), dein),
             "dca_encoder_bwd");
   return {dwt, dw1, db1};
 }
@@ -528,6 +535,101 @@ std::vector<torch::Tensor> enc_small_grads(torch::Tensor z, torch::Tensor dtl, t
   return {out.narrow(0, 0, 768).view({6, 128}), out.narrow(0, 768, 384).view({128, 3}), out.narrow(0, 1152, 128)};
 }
 
+// ---- 5v5 entity-attention block (ops/csrc/attn.hip); 64 unit slots, width 128, 4 heads × 32 -------------------
+std::vector<torch::Tensor> ln_fwd(torch::Tensor e0, torch::Tensor bsub, torch::Tensor gamma, torch::Tensor beta,
+                                  double eps) {
+  CHECK_BF16(e0); CHECK_F32(bsub); CHECK_F32(gamma); CHECK_F32(beta);
+  TORCH_CHECK(e0.size(-1) == 128 && bsub.numel() == 128 && gamma.numel() == 128 && beta.numel() == 128, "ln_fwd");
+  const int64_t R = e0.numel() / 128;
+  auto xn = torch::empty({R, 128}, e0.options());
+  auto mean = torch::empty({R}, gamma.options());
+  auto rstd = torch::empty({R}, gamma.options());
+  hip_check(dca_ln_fwd(ptr<short>(e0), ptr<float>(bsub), ptr<float>(gamma), ptr<float>(beta), ptr<short>(xn),
+                       ptr<float>(mean), ptr<float>(rstd), (int)R, (float)eps, cur_stream()),
+            "dca_ln_fwd");
+  return {xn, mean, rstd};
+}
+
+std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv) {
+  CHECK_BF16(qkv);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) == 384 && qkv.size(0) % 64 == 0, "qkv must be (N*64, 384)");
+  const int N = qkv.size(0) / 64;
+  auto o = torch::empty({(int64_t)N * 64, 128}, qkv.options());
+  auto lse = torch::empty({(int64_t)N, 4, 64}, qkv.options().dtype(at::kFloat));
+  hip_check(dca_attn_fwd(ptr<short>(qkv), ptr<short>(o), ptr<float>(lse), N, 1.f / sqrtf(32.f), cur_stream()),
+            "dca_attn_fwd");
+  return {o, lse};
+}
+
+torch::Tensor attn_bwd(torch::Tensor qkv, torch::Tensor o, torch::Tensor dout, torch::Tensor lse) {
+  CHECK_BF16(qkv); CHECK_BF16(o); CHECK_BF16(dout); CHECK_F32(lse);
+  TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) == 384 && qkv.size(0) % 64 == 0, "qkv must be (N*64, 384)");
+  const int N = qkv.size(0) / 64;
+  TORCH_CHECK(o.numel() == (int64_t)N * 64 * 128 && dout.numel() == o.numel() && lse.numel() == (int64_t)N * 256,
+              "attn_bwd shapes");
+  auto dqkv = torch::empty_like(qkv);
+  hip_check(dca_attn_bwd(ptr<short>(qkv), ptr<short>(o), ptr<short>(dout), ptr<float>(lse), ptr<short>(dqkv), N,
+                         1.f / sqrtf(32.f), cur_stream()),
+            "dca_attn_bwd");
+  return dqkv;
+}
+
+static void check_type_off(const std::vector<int64_t>& t) {
+  TORCH_CHECK(t.size() == 7 && t[0] == 0 && t[6] == 64, "type offsets must be 7 values from 0 to 64");
+  for (int i = 0; i < 6; ++i) TORCH_CHECK(t[i + 1] >= t[i], "type offsets must be non-decreasing");
+}
+
+// pools of E1 (N*64,128) bf16 into x896[:, 128:] (bf16, in place) and arg (N,6,128) u8 (returned)
+torch::Tensor attn_pool(torch::Tensor e1, std::vector<int64_t> type_off, torch::Tensor x896, bool compat) {
+  CHECK_BF16(e1); CHECK_BF16(x896);
+  check_type_off(type_off);
+  const int N = e1.numel() / (64 * 128);
+  TORCH_CHECK(x896.numel() == (int64_t)N * 896, "x896 must be (N, 896)");
+  auto arg = torch::empty({(int64_t)N, 6, 128}, e1.options().dtype(at::kByte));
+  int off[7];
+  for (int i = 0; i < 7; ++i) off[i] = (int)type_off[i];
+  hip_check(dca_attn_pool(ptr<short>(e1), off, ptr<short>(x896), ptr<unsigned char>(arg), N, compat ? 1 : 0,
+                          cur_stream()),
+            "dca_attn_pool");
+  return arg;
+}
+
+torch::Tensor attn_demb(torch::Tensor dtl, torch::Tensor q, torch::Tensor dx, torch::Tensor arg,
+                        std::vector<int64_t> type_off, bool compat) {
+  CHECK_F32(dtl); CHECK_DEV(q); CHECK_DT(q, at::kFloat); CHECK_F32(dx); CHECK_U8(arg);
+  check_type_off(type_off);
+  const int N = dtl.size(0);
+  TORCH_CHECK(dtl.size(1) == 64 && q.size(0) == N && q.stride(1) == 1 && dx.size(0) == N && dx.size(1) == 896 &&
+              arg.numel() == (int64_t)N * 6 * 128, "attn_demb shapes");
+  auto de1 = torch::empty({(int64_t)N * 64, 128}, dx.options().dtype(at::kBFloat16));
+  int off[7];
+  for (int i = 0; i < 7; ++i) off[i] = (int)type_off[i];
+  hip_check(dca_attn_demb(ptr<float>(dtl), ptr<float>(q), (int)q.stride(0), ptr<float>(dx), ptr<unsigned char>(arg),
+                          off, ptr<short>(de1), N, compat ? 1 : 0, cur_stream()),
+            "dca_attn_demb");
+  return de1;
+}
+
+// returns (dE0 bf16 (R,128), dgamma (128), dbeta (128), dbt (6,128)); type_of: (64) u8 device, unit slot → type
+std::vector<torch::Tensor> ln_bwd(torch::Tensor dxn, torch::Tensor e0, torch::Tensor bsub, torch::Tensor gamma,
+                                  torch::Tensor mean, torch::Tensor rstd, torch::Tensor de1, torch::Tensor type_of) {
+  CHECK_BF16(dxn); CHECK_BF16(e0); CHECK_F32(bsub); CHECK_F32(gamma); CHECK_F32(mean); CHECK_F32(rstd);
+  CHECK_BF16(de1); CHECK_U8(type_of);
+  const int64_t R = e0.numel() / 128;
+  TORCH_CHECK(dxn.numel() == R * 128 && de1.numel() == R * 128 && mean.numel() == R && rstd.numel() == R &&
+              type_of.numel() == 64 && R % 64 == 0, "ln_bwd shapes");
+  auto de0 = torch::empty({R, 128}, e0.options());
+  const int W = dca_ln_part_width();
+  const int nblk = (int)std::min<int64_t>(1024, (R + 15) / 16);
+  auto part = torch::empty({(int64_t)nblk * W}, gamma.options());
+  auto out = torch::empty({W}, gamma.options());
+  hip_check(dca_ln_bwd(ptr<short>(dxn), ptr<short>(e0), ptr<float>(bsub), ptr<float>(gamma), ptr<float>(mean),
+                       ptr<float>(rstd), ptr<short>(de1), ptr<unsigned char>(type_of), ptr<short>(de0),
+                       ptr<float>(part), nblk, ptr<float>(out), (int)R, cur_stream()),
+            "dca_ln_bwd");
+  return {de0, out.narrow(0, 0, 128), out.narrow(0, 128, 128), out.narrow(0, 256, 768).view({6, 128})};
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -542,7 +644,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("trace") = py::none());
   m.def("heads_loss", &heads_loss, "fused heads + pointer + masked log-softmax + PPO/VPG loss + gradients");
   m.def("encoder_fwd", &encoder_fwd, "fused entity encoder forward (unit MLP, per-type GEMM, max-pool+argmax)");
-  m.def("encoder_bwd", &encoder_bwd, "fused entity encoder backward: dW_type (K-blocked split-K MFMA GEMM), dW1, db1");
+  m.def("encoder_bwd", &encoder_bwd, "fused entity encoder backward: dW_type (K-blocked split-K MFMA GEMM), dW1, db1",
+        py::arg("units"), py::arg("w1"), py::arg("b1"), py::arg("wtT"), py::arg("dtl"), py::arg("q"), py::arg("dx"),
+        py::arg("arg"), py::arg("counts"), py::arg("compat"), py::arg("demb_in") = py::none());
   m.def("lstm_bwd", &lstm_bwd, "persistent LSTM backward recurrence (granule reduce-scatter)", py::arg("dhs"),
         py::arg("gates"), py::arg("cs"), py::arg("c0"), py::arg("dhn"), py::arg("dcn"), py::arg("whh"), py::arg("err"),
         py::arg("trace") = py::none());
@@ -566,5 +670,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("A"), py::arg("B"), py::arg("C"), py::arg("perm") = py::none(), py::arg("accumulate") = false,
         py::arg("B0") = py::none(), py::arg("colsum") = py::none());
   m.def("enc_small_grads", &enc_small_grads, "entity-encoder type-bias and env-layer gradients in one pass");
+  m.def("ln_fwd", &ln_fwd, "LayerNorm(E0 - bsub) -> (xn bf16, mean, rstd)");
+  m.def("attn_fwd", &attn_fwd, "entity self-attention per (row, head): (o bf16, lse)");
+  m.def("attn_bwd", &attn_bwd, "entity self-attention backward: dqkv");
+  m.def("attn_pool", &attn_pool, "per-type max-pool + argmax of attended embeddings into x896");
+  m.def("attn_demb", &attn_demb, "dE1 = dtl*q + pool gradient at the argmax unit");
+  m.def("ln_bwd", &ln_bwd, "LayerNorm backward + residual: (dE0, dgamma, dbeta, dbt)");
   m.def("returns_scan", &returns_scan, "segmented reverse scan: discounted returns / GAE + per-team EMA normalisation");
 }

@@ -70,6 +70,7 @@ struct BwdParams {
   Layout L;
   long long blkbase[6];
   int NB;               // 16-row blocks per unit slot = ⌈N/16⌉
+  const short* demb_in; // optional (N, U, 128) bf16: ∂emb given (entity-attention path) — dtl/q/dx/arg unused
 };
 
 __device__ __forceinline__ void type_job(int wv, int j, int& tau, int& g) {
@@ -314,13 +315,14 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
     const int arow = row0 + i;
     const bool rok = arow < N;
     const bool eth_dead = P.compat && tau == 5;   // reference bug: eth pool unused → no pool gradient
+    const bool given = P.demb_in != nullptr;       // wave-uniform
     // ---- per-(row, type) operands in A layout (row i, cols 32s + 8kg + jj), loaded once per type job
     float qv[4][8], dpv[4][8];
     unsigned agv[4][2];
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
       const int e0 = 32 * s + 8 * kg;
-      if (rok) {
+      if (rok && !given) {
         const float4 qa = *reinterpret_cast<const float4*>(P.q + (size_t)arow * P.ldq + e0);
         const float4 qb = *reinterpret_cast<const float4*>(P.q + (size_t)arow * P.ldq + e0 + 4);
         qv[s][0] = qa.x; qv[s][1] = qa.y; qv[s][2] = qa.z; qv[s][3] = qa.w;
@@ -344,7 +346,7 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
     for (int c0 = 0; c0 < cnt; c0 += kStage) {
       const int cc = min(kStage, cnt - c0);
       __builtin_amdgcn_wave_barrier();
-      stage_units(P.units, P.dtl, U, N, row0, uoff + c0, cc, ur, dr, lane);
+      stage_units(P.units, given ? nullptr : P.dtl, U, N, row0, uoff + c0, cc, ur, dr, lane);
       __builtin_amdgcn_wave_barrier();
       for (int uc = 0; uc < cc; ++uc) {
         const int u = c0 + uc;
@@ -356,11 +358,21 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
         for (int n = 0; n < 8; ++n)
 #pragma unroll
           for (int r = 0; r < 4; ++r) bas[n][r] = fmaxf(acc[n][r] + b1v[n], 0.f);
-        // ---- ∂emb in A layout: dtl·q + ∂pool where this unit is the argmax
-        const float dtl = dr[i * kStage + uc];
+        // ---- ∂emb in A layout: dtl·q + ∂pool where this unit is the argmax (or given)
+        const float dtl = given ? 0.f : dr[i * kStage + uc];
         bf16x8 de[4];
+        if (given) {
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
+          for (int s = 0; s < 4; ++s) {
+            bf16x8 h = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (rok) h = *reinterpret_cast<const bf16x8*>(P.demb_in + ((size_t)arow * U + uoff + u) * kD + 32 * s + 8 * kg);
+            de[s] = h;
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) tw[toff(32 * s + 8 * kg + jj, i)] = h[jj];
+          }
+        }
+#pragma unroll
+        for (int s = 0; s < 4 && !given; ++s) {
           float v[8];
 #pragma unroll
           for (int jj = 0; jj < 8; ++jj) {
@@ -582,7 +594,8 @@ extern "C" size_t dca_encoder_bwd_workspace(int N, int U, const int* counts) {
 extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const float* b1, const short* wtT,
                                       const float* dtl, const float* q, int ldq, const float* dx,
                                       const unsigned char* arg, float* dwt, float* dw1, float* db1, void* ws,
-                                      size_t ws_bytes, int N, int U, const int* counts, int compat, hipStream_t st) {
+                                      size_t ws_bytes, int N, int U, const int* counts, int compat, hipStream_t st,
+                                      const short* demb_in) {
   if (ws_bytes < dca_encoder_bwd_workspace(N, U, counts)) return hipErrorInvalidValue;
   DwtJobs J;
   int NB;
@@ -595,7 +608,7 @@ extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const
   short* demb = reinterpret_cast<short*>(p);
   short* basic = demb + img;
   float* parts = reinterpret_cast<float*>(basic + img);
-  BwdParams P{units, w1, b1, wtT, dtl, q, ldq, dx, arg, demb, basic, w1part, N, compat, {}, {}, NB};
+  BwdParams P{units, w1, b1, wtT, dtl, q, ldq, dx, arg, demb, basic, w1part, N, compat, {}, {}, NB, demb_in};
   P.L.U = U;
   int acc = 0;
   for (int t = 0; t < 6; ++t) {

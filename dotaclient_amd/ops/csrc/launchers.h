@@ -36,7 +36,7 @@ size_t dca_encoder_bwd_workspace(int N, int U, const int* counts);
 hipError_t dca_encoder_bwd(const float* units, const float* w1, const float* b1, const short* wtT, const float* dtl,
                            const float* q, int ldq, const float* dx, const unsigned char* arg, float* dwt, float* dw1,
                            float* db1, void* ws, size_t ws_bytes, int N, int U, const int* counts, int compat,
-                           hipStream_t st);
+                           hipStream_t st, const short* demb_in = nullptr);
 
 size_t dca_lstm_team_ctl_bytes();
 size_t dca_lstm_team_workspace(int B, int H, int backward);
@@ -80,5 +80,19 @@ int dca_enc_small_blocks();
 hipError_t dca_enc_small_grads(const float* z, int ldz, const float* dtl, int U, const int* type_off, const float* dx,
                                const float* env, const float* we, const float* be, int N, int compat, float* part,
                                float* out, hipStream_t st);
+
+int dca_ln_part_width();
+hipError_t dca_ln_fwd(const short* e0, const float* bsub, const float* gamma, const float* beta, short* xn, float* mean,
+                      float* rstd, int R, float eps, hipStream_t st);
+hipError_t dca_attn_fwd(const short* qkv, short* o, float* lse, int N, float scale, hipStream_t st);
+hipError_t dca_attn_bwd(const short* qkv, const short* o, const short* dout, const float* lse, short* dqkv, int N,
+                        float scale, hipStream_t st);
+hipError_t dca_attn_pool(const short* e1, const int* type_off, short* x896, unsigned char* arg, int N, int compat,
+                         hipStream_t st);
+hipError_t dca_attn_demb(const float* dtl, const float* q, int ldq, const float* dx, const unsigned char* arg,
+                         const int* type_off, short* de1, int N, int compat, hipStream_t st);
+hipError_t dca_ln_bwd(const short* dxn, const short* e0, const float* bsub, const float* gamma, const float* mean,
+                      const float* rstd, const short* de1, const unsigned char* type_of, short* de0, float* part,
+                      int nblk, float* out, int R, hipStream_t st);
 
 }  // extern "C"

@@ -1,0 +1,135 @@
+"""5v5 entity-attention block kernels (ops/csrc/attn.hip) vs plain PyTorch fp32 references of the same ops."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+N = 37                       # timestep rows (not a multiple of anything on purpose)
+U, D, NH, HD = 64, 128, 4, 32
+TYPE_OFF = [0, 5, 10, 34, 58, 61, 64]   # 5v5 layout (5, 5, 24, 24, 3, 3)
+
+
+def _bf(t):
+    return t.to(torch.bfloat16)
+
+
+def _g(seed):
+    return torch.Generator(device='cuda').manual_seed(seed)
+
+
+def test_ln_fwd(gpu_ops):
+    g = _g(0)
+    e0 = _bf(torch.randn(N * U, D, device='cuda', generator=g) * 2 + 0.5)
+    bsub = torch.randn(D, device='cuda', generator=g) * 0.1
+    gamma = 1 + 0.1 * torch.randn(D, device='cuda', generator=g)
+    beta = 0.1 * torch.randn(D, device='cuda', generator=g)
+    xn, mean, rstd = gpu_ops.ln_fwd(e0, bsub, gamma, beta, 1e-5)
+    x = e0.float() - bsub
+    ref = F.layer_norm(x, (D,), gamma, beta, 1e-5)
+    torch.testing.assert_close(xn.float(), ref, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(mean, x.mean(-1), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(rstd, 1 / torch.sqrt(x.var(-1, unbiased=False) + 1e-5), rtol=1e-3, atol=1e-3)
+
+
+def _attn_ref(qkv):
+    q, k, v = qkv.float().view(N, U, 3, NH, HD).unbind(2)
+    q, k, v = (t.transpose(1, 2) for t in (q, k, v))            # (N, h, U, d)
+    s = q @ k.transpose(-1, -2) / HD ** 0.5
+    o = torch.softmax(s, -1) @ v
+    return o.transpose(1, 2).reshape(N * U, D), torch.logsumexp(s, -1)
+
+
+def test_attn_fwd_bwd(gpu_ops):
+    g = _g(1)
+    qkv = _bf(torch.randn(N * U, 3 * D, device='cuda', generator=g))
+    o, lse = gpu_ops.attn_fwd(qkv)
+    o_ref, lse_ref = _attn_ref(qkv)
+    torch.testing.assert_close(o.float(), o_ref, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(lse, lse_ref, rtol=1e-3, atol=1e-3)
+    dout = _bf(torch.randn(N * U, D, device='cuda', generator=g))
+    dqkv = gpu_ops.attn_bwd(qkv, o, dout, lse)
+    x = qkv.float().requires_grad_(True)
+    _attn_ref(x)[0].backward(dout.float())
+    ref = x.grad
+    err = (dqkv.float() - ref).norm() / ref.norm()
+    assert err < 2e-2, float(err)
+    for part in range(3):   # q, k, v blocks each
+        a, b = dqkv.float()[:, part * D:(part + 1) * D], ref[:, part * D:(part + 1) * D]
+        assert (a - b).norm() / b.norm() < 3e-2, part
+
+
+@pytest.mark.parametrize('compat', [False, True])
+def test_pool_and_demb(gpu_ops, compat):
+    g = _g(2)
+    e1 = _bf(torch.randn(N * U, D, device='cuda', generator=g))
+    x896 = torch.zeros(N, 896, device='cuda', dtype=torch.bfloat16)
+    arg = gpu_ops.attn_pool(e1, TYPE_OFF, x896, compat)
+    e = e1.float().view(N, U, D)
+    for t in range(6):
+        src = 3 if (compat and t == 5) else t
+        seg = e[:, TYPE_OFF[src]:TYPE_OFF[src + 1]]
+        mx, am = seg.max(1)
+        torch.testing.assert_close(x896[:, D + t * D:D + (t + 1) * D].float(), mx)
+        got = seg.gather(1, arg[:, t].long().unsqueeze(1)).squeeze(1)
+        torch.testing.assert_close(got, mx)
+    # ∂E1 = dtl ⊗ q + pool gradient routed to the argmax unit
+    dtl = torch.randn(N, U, device='cuda', generator=g)
+    z = torch.randn(N, 160, device='cuda', generator=g)
+    dx = torch.randn(N, 896, device='cuda', generator=g)
+    de1 = gpu_ops.attn_demb(dtl, z, dx, arg, TYPE_OFF, compat)
+    ref = dtl.unsqueeze(-1) * z[:, None, :D]
+    for t in range(6):
+        src = 3 if (compat and t == 5) else t
+        u = TYPE_OFF[src] + arg[:, t].long()                    # (N, D)
+        ref.scatter_add_(1, u.unsqueeze(1), dx[:, D + t * D:D + (t + 1) * D].unsqueeze(1))
+    torch.testing.assert_close(de1.float().view(N, U, D), ref, rtol=1e-2, atol=2e-2)
+
+
+def test_ln_bwd(gpu_ops):
+    g = _g(3)
+    R = N * U
+    e0 = _bf(torch.randn(R, D, device='cuda', generator=g))
+    bsub = torch.randn(D, device='cuda', generator=g) * 0.1
+    gamma = 1 + 0.1 * torch.randn(D, device='cuda', generator=g)
+    beta = 0.1 * torch.randn(D, device='cuda', generator=g)
+    _, mean, rstd = gpu_ops.ln_fwd(e0, bsub, gamma, beta, 1e-5)
+    dxn = _bf(torch.randn(R, D, device='cuda', generator=g))
+    de1 = _bf(torch.randn(R, D, device='cuda', generator=g))
+    type_of = torch.tensor(sum([[t] * (TYPE_OFF[t + 1] - TYPE_OFF[t]) for t in range(6)], []), dtype=torch.uint8,
+                           device='cuda')
+    de0, dgam, dbet, dbt = gpu_ops.ln_bwd(dxn, e0, bsub, gamma, mean, rstd, de1, type_of)
+    x = (e0.float() - bsub).requires_grad_(True)
+    gm, bt = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
+    F.layer_norm(x, (D,), gm, bt, 1e-5).backward(dxn.float())
+    ref_de0 = x.grad + de1.float()
+    torch.testing.assert_close(de0.float(), ref_de0, rtol=2e-2, atol=3e-2)
+    torch.testing.assert_close(dgam, gm.grad, rtol=1e-3, atol=1e-2)
+    torch.testing.assert_close(dbet, bt.grad, rtol=1e-3, atol=1e-2)
+    ref_dbt = torch.stack([ref_de0.view(N, U, D)[:, TYPE_OFF[t]:TYPE_OFF[t + 1]].sum((0, 1)) for t in range(6)])
+    torch.testing.assert_close(dbt, ref_dbt, rtol=2e-2, atol=0.5)
+
+
+def test_encoder_bwd_with_given_demb(gpu_ops):
+    """encoder_bwd(demb_in=∂E0): ∂W_τ, ∂W1, ∂b1 of the unit MLP + per-type linear for an arbitrary ∂E0."""
+    g = _g(4)
+    units = torch.randn(N, U, 10, device='cuda', generator=g)
+    w1 = torch.randn(D, 10, device='cuda', generator=g) * 0.3
+    b1 = torch.randn(D, device='cuda', generator=g) * 0.1
+    wt = torch.randn(6, D, D, device='cuda', generator=g) * 0.1
+    demb = _bf(torch.randn(N, U, D, device='cuda', generator=g))
+    counts = [TYPE_OFF[t + 1] - TYPE_OFF[t] for t in range(6)]
+    wtT16 = _bf(wt).transpose(1, 2).contiguous()
+    dummy_q = torch.zeros(N, 160, device='cuda')
+    dwt, dw1, db1 = gpu_ops.encoder_bwd(units, w1, b1, wtT16, torch.zeros(N, U, device='cuda'), dummy_q,
+                                        torch.zeros(N, 896, device='cuda'),
+                                        torch.zeros(N, 6, 128, dtype=torch.uint8, device='cuda'), counts, False,
+                                        demb_in=demb)
+    W1 = w1.clone().requires_grad_(True)
+    B1 = b1.clone().requires_grad_(True)
+    WT = wt.clone().requires_grad_(True)
+    basic = F.relu(units @ W1.t() + B1)
+    embs = [basic[:, TYPE_OFF[t]:TYPE_OFF[t + 1]] @ _bf(WT[t]).float().t() for t in range(6)]
+    torch.cat(embs, 1).backward(demb.float())
+    for got, ref, name in ((dwt, WT.grad, 'dwt'), (dw1, W1.grad, 'dw1'), (db1, B1.grad, 'db1')):
+        assert (got - ref).norm() / ref.norm() < 3e-2, name

@@ -134,3 +134,53 @@ def test_dp_step_equals_single_process_average():
     assert counts[names.index('affine_value.weight')] == 0      # vf_coef = 0: value head has no grad anywhere
     L.opt.step(counts)
     torch.testing.assert_close(L.flat.flat, out[0][0], rtol=1e-5, atol=1e-6)
+
+
+def _resume_worker(rank, world, port, root, q):
+    try:
+        _init(rank, world, port)
+        from dotaclient_amd.learner.optimizer import DotaOptimizer, OptimizerConfig
+        from dotaclient_amd.transport.broker import InProcBroker
+        # rank 0 sees the run's checkpoint directory, rank 1 a fresh, empty node-local directory
+        ld = os.path.join(root, 'run') if rank == 0 else os.path.join(root, f'empty{rank}')
+        cfg = OptimizerConfig(log_dir=ld, batch_size=2, seq_len=16, seq_per_epoch=2, epochs=1, model='lstm128',
+                              device='cpu', backend='torch')
+        opt = DotaOptimizer(cfg, InProcBroker(), checkpoint=rank == 0)
+        q.put((rank, opt.iteration_start, opt.learner.opt.exp_avg.clone(), opt.learner.opt.steps.clone(),
+               opt.learner.flat.flat.clone()))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e), None, None, None))
+
+
+def test_resume_equalises_iteration_and_optimizer_state(tmp_path):
+    """Only rank 0 can read the checkpoint (reference workers restart at iteration 1 with fresh Adam state,
+    §2.10-7): every rank must resume at rank 0's iteration with rank 0's weights AND optimizer moments."""
+    from dotaclient_amd.learner.engine import Learner, LossConfig
+    from dotaclient_amd.models.policy import Policy, get_config
+    from dotaclient_amd.utils import checkpoint as ckpt
+    torch.manual_seed(3)
+    pol = Policy(get_config('lstm128'))
+    L = Learner(pol, LossConfig(), device='cpu', backend='torch', dp=False)
+    L.opt.exp_avg.normal_()
+    L.opt.steps.fill_(41)
+    run = tmp_path / 'run'
+    ckpt.save_model(pol.state_dict(), str(run), 41)
+    ckpt.save_trainer_state({'learner': L.state_dict(), 'running': {'factor': 0.99, 'mean': {}, 'std': {}},
+                             'iteration': 41}, str(run), 41)
+    world, port = 2, _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_resume_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = dict((r[0], r[1:]) for r in (q.get(timeout=300) for _ in range(world)))
+    for p in ps:
+        p.join(timeout=60)
+    assert all(isinstance(v[0], int) for v in res.values()), res
+    assert res[0][0] == res[1][0] == 42
+    torch.testing.assert_close(res[1][1], res[0][1])
+    torch.testing.assert_close(res[0][1], L.opt.exp_avg)
+    assert (res[1][2] == 41).all()
+    torch.testing.assert_close(res[1][3], res[0][3])
