@@ -211,42 +211,78 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_kernel(Args a) {
 #undef BS
 }
 
-// Fixed-order (deterministic) sum of the split-K slabs, one float4 of C per thread, optional row map / accumulate.
+// Fixed-order (deterministic) sum of the split-K slabs, optional row map / accumulate. A block owns 16 float4 outputs
+// × 16 split phases: thread (phase p, output o) sums splits p, p+16, … with 4 loads in flight, then a fixed LDS
+// fold over the phases — many threads per output, so a long split list (K = 716 800 unit rows of the 5v5 attention
+// weight gradients → ≈380 splits of a single tile) is not one latency-bound serial chain per output.
+constexpr int kRedPh = 16;
 __global__ __launch_bounds__(256) void gemm_tn_reduce(const float* __restrict__ slab, int splits, int M, int N,
                                                       float* __restrict__ C, int ldc, const int* __restrict__ perm,
                                                       int accumulate, float* __restrict__ colsum) {
   const int n4 = N >> 2;
   const size_t plane = (size_t)M * N;
-  if (colsum != nullptr) {
-    const float* cs = slab + (size_t)splits * plane;
-    for (int m = blockIdx.x * 256 + threadIdx.x; m < M; m += gridDim.x * 256) {
-      float v = 0.f;
-      for (int sp = 0; sp < splits; ++sp) v += cs[(size_t)sp * M + m];
-      float* cp = colsum + (perm ? perm[m] : m);
-      *cp = accumulate ? *cp + v : v;
+  const int ph = threadIdx.x >> 4, oi = threadIdx.x & 15;
+  __shared__ f32x4 red[kRedPh][16];
+  const int nout = M * n4;
+  for (int base = blockIdx.x * 16; base < nout; base += gridDim.x * 16) {
+    const int idx = base + oi;
+    f32x4 s = {0.f, 0.f, 0.f, 0.f};
+    if (idx < nout) {
+      const int m = idx / n4, n = (idx % n4) * 4;
+      const f32x4* src = reinterpret_cast<const f32x4*>(slab + (size_t)m * N + n);
+      int sp = ph;
+      for (; sp + 3 * kRedPh < splits; sp += 4 * kRedPh) {
+        const f32x4 v0 = __builtin_nontemporal_load(src + (size_t)(sp + 0 * kRedPh) * (plane / 4));
+        const f32x4 v1 = __builtin_nontemporal_load(src + (size_t)(sp + 1 * kRedPh) * (plane / 4));
+        const f32x4 v2 = __builtin_nontemporal_load(src + (size_t)(sp + 2 * kRedPh) * (plane / 4));
+        const f32x4 v3 = __builtin_nontemporal_load(src + (size_t)(sp + 3 * kRedPh) * (plane / 4));
+        s += v0;
+        s += v1;
+        s += v2;
+        s += v3;
+      }
+      for (; sp < splits; sp += kRedPh) s += __builtin_nontemporal_load(src + (size_t)sp * (plane / 4));
     }
+    red[ph][oi] = s;
+    __syncthreads();
+    if (ph == 0 && idx < nout) {
+      for (int k = 1; k < kRedPh; ++k) s += red[k][oi];
+      const int m = idx / n4, n = (idx % n4) * 4;
+      float* cp = C + (size_t)(perm ? perm[m] : m) * ldc + n;
+      if (accumulate) {
+        s[0] += cp[0]; s[1] += cp[1]; s[2] += cp[2]; s[3] += cp[3];
+      }
+      cp[0] = s[0]; cp[1] = s[1]; cp[2] = s[2]; cp[3] = s[3];
+    }
+    __syncthreads();
   }
-  for (int idx = blockIdx.x * 256 + threadIdx.x; idx < M * n4; idx += gridDim.x * 256) {
-    const int m = idx / n4, n = (idx % n4) * 4;
-    const f32x4* src = reinterpret_cast<const f32x4*>(slab + (size_t)m * N + n);
-    f32x4 s = __builtin_nontemporal_load(src);
-    int sp = 1;
-    for (; sp + 3 < splits; sp += 4) {
-      const f32x4 v0 = __builtin_nontemporal_load(src + (sp + 0) * (plane / 4));
-      const f32x4 v1 = __builtin_nontemporal_load(src + (sp + 1) * (plane / 4));
-      const f32x4 v2 = __builtin_nontemporal_load(src + (sp + 2) * (plane / 4));
-      const f32x4 v3 = __builtin_nontemporal_load(src + (sp + 3) * (plane / 4));
-      s += v0;
-      s += v1;
-      s += v2;
-      s += v3;
+  if (colsum != nullptr) {       // same phase split for the column sums: 16 columns × 16 split phases per pass
+    const float* cs = slab + (size_t)splits * plane;
+    __shared__ float cred[kRedPh][16];
+    for (int base = blockIdx.x * 16; base < M; base += gridDim.x * 16) {
+      const int m = base + oi;
+      float v = 0.f;
+      if (m < M) {
+        int sp = ph;
+        for (; sp + 3 * kRedPh < splits; sp += 4 * kRedPh) {
+          const float v0 = cs[(size_t)(sp + 0 * kRedPh) * M + m], v1 = cs[(size_t)(sp + 1 * kRedPh) * M + m];
+          const float v2 = cs[(size_t)(sp + 2 * kRedPh) * M + m], v3 = cs[(size_t)(sp + 3 * kRedPh) * M + m];
+          v += v0;
+          v += v1;
+          v += v2;
+          v += v3;
+        }
+        for (; sp < splits; sp += kRedPh) v += cs[(size_t)sp * M + m];
+      }
+      cred[ph][oi] = v;
+      __syncthreads();
+      if (ph == 0 && m < M) {
+        for (int k = 1; k < kRedPh; ++k) v += cred[k][oi];
+        float* cp = colsum + (perm ? perm[m] : m);
+        *cp = accumulate ? *cp + v : v;
+      }
+      __syncthreads();
     }
-    for (; sp < splits; ++sp) s += __builtin_nontemporal_load(src + sp * (plane / 4));
-    float* cp = C + (size_t)(perm ? perm[m] : m) * ldc + n;
-    if (accumulate) {
-      s[0] += cp[0]; s[1] += cp[1]; s[2] += cp[2]; s[3] += cp[3];
-    }
-    cp[0] = s[0]; cp[1] = s[1]; cp[2] = s[2]; cp[3] = s[3];
   }
 }
 
@@ -278,7 +314,7 @@ extern "C" hipError_t dca_gemm_tn(const short* A, int lda, const short* B, int l
   DCA_CHECK_LAUNCH();
   if (splits > 1) {
     const int n = M * (N / 4);
-    int blocks = (n + 255) / 256;
+    int blocks = (n + 15) / 16;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(gemm_tn_reduce, dim3(blocks), dim3(256), 0, st, slab, splits, M, N, C, ldc, perm, accumulate,
                        colsum);
