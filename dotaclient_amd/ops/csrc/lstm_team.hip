@@ -31,7 +31,10 @@
 //
 // Tried and measured slower (kept out): a role-separated forward whose 5th "IO" wave owns every HBM access of a step
 // (x·W_ih prefetch 1-2 steps ahead into an LDS ring, h/c/gate outputs from an LDS staging ring) so the MFMA waves'
-// in-order vmcnt waits see only polls and publishes: 2.17-2.22 vs 1.92 µs per forward step at B=8, H=512.
+// in-order vmcnt waits see only polls and publishes: 2.17-2.22 vs 1.92 µs per forward step at B=8, H=512. Also
+// slower: storing a step's outputs after the NEXT step's gather barrier instead of right after the publish (2.08 vs
+// 1.96 µs forward, 2.33 vs 2.28 backward — stores queued ahead of the publish delay it), although skipping the
+// output stores altogether (knob) saves 0.14 µs per forward step; the x·W_ih load's placement does not matter.
 #include "common.h"
 #include <cstdlib>
 
@@ -272,7 +275,8 @@ __device__ __forceinline__ void lstm_team_fwd_body(
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const int b = mt * 16 + erow;
-          xv[mt] = (b < B) ? *reinterpret_cast<const dca::f32x4*>(xp4 + (((size_t)(b0 + b) * sb + (size_t)t * st) * H + eunit) * 4)
+          const size_t tx = ((knobs >> 10) & 1) ? 0 : (size_t)t;   // knob: every step reads step 0 (L2-resident)
+          xv[mt] = (b < B) ? *reinterpret_cast<const dca::f32x4*>(xp4 + (((size_t)(b0 + b) * sb + tx * st) * H + eunit) * 4)
                            : dca::f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
@@ -633,7 +637,7 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
   team_exit(ctl);
 }
 
-// DCA_TEAM_KNOBS = pre_sleep | skip_outputs << 8 | probe_first << 9 (latency experiments only; default 0)
+// DCA_TEAM_KNOBS = pre_sleep | skip_outputs << 8 | probe_first << 9 | xp_step0 << 10 (latency experiments only)
 inline int team_knobs() {
   const char* e = getenv("DCA_TEAM_KNOBS");
   return e ? atoi(e) : 0;
