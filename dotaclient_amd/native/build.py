@@ -1,5 +1,8 @@
 """Build the native host-side module ``dotaclient_amd/native/_native*.so`` (C++17, pybind11, no torch):
-protobuf wire decoder + featurizer, shared-memory experience ring, crc32c. ``python -m dotaclient_amd.native.build``."""
+protobuf wire decoder + featurizer, shared-memory experience ring, crc32c. ``python -m dotaclient_amd.native.build``.
+
+``build_sanitizer('asan' | 'tsan')`` builds the standalone sanitizer driver (``sanitize_main.cpp`` over ``core.h``)
+under AddressSanitizer + UndefinedBehaviorSanitizer or ThreadSanitizer (host code only)."""
 from __future__ import annotations
 
 import os
@@ -9,20 +12,18 @@ import sysconfig
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 SRC = os.path.join(HERE, 'featurizer.cpp')
+CORE = os.path.join(HERE, 'core.h')
 TARGET = os.path.join(HERE, '_native' + (sysconfig.get_config_var('EXT_SUFFIX') or '.so'))
 
 
-def build(verbose: bool = True, force: bool = False, debug_asan: bool = False) -> str:
-    if not force and os.path.exists(TARGET) and os.path.getmtime(TARGET) > os.path.getmtime(SRC) and not debug_asan:
+def build(verbose: bool = True, force: bool = False) -> str:
+    if (not force and os.path.exists(TARGET)
+            and os.path.getmtime(TARGET) > max(os.path.getmtime(SRC), os.path.getmtime(CORE))):
         return TARGET
     import pybind11
     cxx = os.environ.get('CXX', 'g++')
     flags = ['-O3', '-std=c++17', '-fPIC', '-shared', '-msse4.2', '-pthread', '-Wall', '-Wno-unused-function']
     target = TARGET
-    if debug_asan:   # host-side sanitizer build (race / memory checks of the ring + decoder)
-        flags = ['-O1', '-g', '-std=c++17', '-fPIC', '-shared', '-msse4.2', '-pthread', '-fsanitize=address,undefined',
-                 '-fno-omit-frame-pointer']
-        target = os.path.join(HERE, '_native_asan' + (sysconfig.get_config_var('EXT_SUFFIX') or '.so'))
     cmd = [cxx, *flags, '-I', pybind11.get_include(), '-I', sysconfig.get_paths()['include'], SRC, '-o', target, '-lrt']
     if verbose:
         print('[dotaclient_amd.native] ' + ' '.join(cmd[:3]) + ' ...', flush=True)
@@ -30,5 +31,31 @@ def build(verbose: bool = True, force: bool = False, debug_asan: bool = False) -
     return target
 
 
+SANITIZE_FLAGS = {
+    'asan': ['-fsanitize=address,undefined', '-fno-sanitize-recover=undefined', '-fno-omit-frame-pointer'],
+    'tsan': ['-fsanitize=thread'],
+}
+
+
+def build_sanitizer(kind: str = 'asan', verbose: bool = False) -> str:
+    """Compile the sanitizer driver for ``kind`` into ``native/_build/sanitize_<kind>``; returns its path."""
+    out_dir = os.path.join(HERE, '_build')
+    os.makedirs(out_dir, exist_ok=True)
+    target = os.path.join(out_dir, f'sanitize_{kind}')
+    src = os.path.join(HERE, 'sanitize_main.cpp')
+    if os.path.exists(target) and os.path.getmtime(target) > max(os.path.getmtime(src), os.path.getmtime(CORE)):
+        return target
+    cxx = os.environ.get('CXX', 'g++')
+    cmd = [cxx, '-O1', '-g', '-std=c++17', '-msse4.2', '-pthread', *SANITIZE_FLAGS[kind], src, '-o', target, '-lrt']
+    if verbose:
+        print('[dotaclient_amd.native] ' + ' '.join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+    return target
+
+
 if __name__ == '__main__':
-    build(force='--force' in sys.argv, debug_asan='--asan' in sys.argv)
+    if '--sanitize' in sys.argv:
+        for k in ('asan', 'tsan'):
+            print(build_sanitizer(k, verbose=True))
+    else:
+        build(force='--force' in sys.argv)

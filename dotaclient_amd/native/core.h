@@ -1,0 +1,440 @@
+// Native actor-side runtime core (no Python): proto2 wire decoder + featurizer, shared-memory MPMC ring, crc32c.
+// Included by the pybind11 module (featurizer.cpp) and by the sanitizer driver (sanitize_main.cpp), which runs it
+// under AddressSanitizer / UndefinedBehaviorSanitizer / ThreadSanitizer: decoder fuzzing on malformed bytes, the
+// ring under concurrent producers and consumers. See featurizer.cpp for the reference semantics.
+#pragma once
+#include <errno.h>
+#include <fcntl.h>
+#include <nmmintrin.h>
+#include <pthread.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <vector>
+
+namespace dca_native {
+
+
+// ============================================================================================================
+// proto2 wire decoding
+// ============================================================================================================
+struct Reader {
+  const uint8_t* p;
+  const uint8_t* e;
+  bool ok() const { return p < e; }
+  uint64_t varint() {
+    uint64_t v = 0;
+    int s = 0;
+    while (p < e) {
+      const uint8_t b = *p++;
+      v |= (uint64_t)(b & 0x7f) << s;
+      if (!(b & 0x80)) return v;
+      s += 7;
+      if (s > 63) break;
+    }
+    throw std::runtime_error("malformed varint");
+  }
+  float f32() {
+    if (e - p < 4) throw std::runtime_error("truncated fixed32");
+    float f;
+    std::memcpy(&f, p, 4);
+    p += 4;
+    return f;
+  }
+  std::string_view bytes() {
+    const uint64_t n = varint();
+    if ((uint64_t)(e - p) < n) throw std::runtime_error("truncated length-delimited field");
+    std::string_view s((const char*)p, n);
+    p += n;
+    return s;
+  }
+  void skip(int wt) {
+    switch (wt) {
+      case 0: varint(); break;
+      case 1: p += 8; break;
+      case 2: bytes(); break;
+      case 5: p += 4; break;
+      default: throw std::runtime_error("unsupported wire type");
+    }
+    if (p > e) throw std::runtime_error("truncated field");
+  }
+};
+
+enum UnitTypeE { HERO = 1, CREEP_HERO = 2, LANE_CREEP = 3, TOWER = 6 };
+
+struct Unit {
+  uint32_t handle = 0;
+  int unit_type = 0;
+  std::string_view name;
+  uint32_t team_id = 0;
+  float x = 0, y = 0, z = 0;
+  bool is_alive = false;
+  int32_t player_id = 0;
+  float facing = 0;
+  int32_t health = 0, health_max = 0;
+  int32_t attack_range = 0;
+  uint32_t attack_target = 0;
+  int32_t anim = 0;
+  bool invuln = false, attack_immune = false;
+  std::vector<uint32_t> attack_casters;   // incoming tracking projectiles with is_attack
+};
+
+struct World {
+  float dota_time = 0;
+  std::vector<Unit> units;
+};
+
+void parse_vector(std::string_view s, Unit& u) {
+  Reader r{(const uint8_t*)s.data(), (const uint8_t*)s.data() + s.size()};
+  while (r.ok()) {
+    const uint64_t k = r.varint();
+    const int f = (int)(k >> 3), wt = (int)(k & 7);
+    if (wt == 5 && f == 1) u.x = r.f32();
+    else if (wt == 5 && f == 2) u.y = r.f32();
+    else if (wt == 5 && f == 3) u.z = r.f32();
+    else r.skip(wt);
+  }
+}
+
+void parse_projectile(std::string_view s, Unit& u) {
+  Reader r{(const uint8_t*)s.data(), (const uint8_t*)s.data() + s.size()};
+  uint32_t caster = 0;
+  bool is_attack = false;
+  while (r.ok()) {
+    const uint64_t k = r.varint();
+    const int f = (int)(k >> 3), wt = (int)(k & 7);
+    if (wt == 0 && f == 1) caster = (uint32_t)r.varint();
+    else if (wt == 0 && f == 4) is_attack = r.varint() != 0;
+    else r.skip(wt);
+  }
+  if (is_attack) u.attack_casters.push_back(caster);
+}
+
+void parse_unit(std::string_view s, Unit& u) {
+  Reader r{(const uint8_t*)s.data(), (const uint8_t*)s.data() + s.size()};
+  while (r.ok()) {
+    const uint64_t k = r.varint();
+    const int f = (int)(k >> 3), wt = (int)(k & 7);
+    if (wt == 0) {
+      const uint64_t v = r.varint();
+      switch (f) {
+        case 1: u.handle = (uint32_t)v; break;
+        case 2: u.unit_type = (int)v; break;
+        case 4: u.team_id = (uint32_t)v; break;
+        case 7: u.is_alive = v != 0; break;
+        case 8: u.player_id = (int32_t)v; break;
+        case 20: u.health = (int32_t)v; break;
+        case 21: u.health_max = (int32_t)v; break;
+        case 30: u.attack_range = (int32_t)v; break;
+        case 35: u.attack_target = (uint32_t)v; break;
+        case 40: u.anim = (int32_t)v; break;
+        case 50: u.invuln = v != 0; break;
+        case 51: u.attack_immune = v != 0; break;
+        default: break;
+      }
+    } else if (wt == 5) {
+      const float v = r.f32();
+      if (f == 11) u.facing = v;
+    } else if (wt == 2) {
+      const std::string_view b = r.bytes();
+      if (f == 3) u.name = b;
+      else if (f == 6) parse_vector(b, u);
+      else if (f == 70) parse_projectile(b, u);
+    } else {
+      r.skip(wt);
+    }
+  }
+}
+
+void parse_world(const uint8_t* data, size_t n, World& w) {
+  Reader r{data, data + n};
+  while (r.ok()) {
+    const uint64_t k = r.varint();
+    const int f = (int)(k >> 3), wt = (int)(k & 7);
+    if (wt == 5 && f == 3) {
+      w.dota_time = r.f32();
+    } else if (wt == 2 && f == 11) {
+      w.units.emplace_back();
+      parse_unit(r.bytes(), w.units.back());
+    } else {
+      r.skip(wt);
+    }
+  }
+}
+
+// ============================================================================================================
+// featurizer (reference agent.py:496-637)
+// ============================================================================================================
+constexpr float kMapHalf = 7000.f;
+constexpr float kPi = 3.14159265358979323846f;
+
+bool ends_with(std::string_view s, std::string_view suf) {
+  return s.size() >= suf.size() && s.substr(s.size() - suf.size()) == suf;
+}
+
+float attacking(const Unit& a, const Unit& t) {
+  if (a.attack_target == t.handle) return 1.f;
+  for (uint32_t c : t.attack_casters)
+    if (c == a.handle) return 1.f;
+  return 0.f;
+}
+
+void unit_rows(const std::vector<const Unit*>& list, const Unit& hero, bool only_self, int max_units, float* m,
+               int64_t* handles) {
+  for (int i = 0; i < max_units; ++i) {
+    handles[i] = -1;
+    for (int k = 0; k < 10; ++k) m[i * 10 + k] = 0.f;
+  }
+  int i = 0;
+  const uint32_t opp = hero.team_id == 2 ? 3 : (hero.team_id == 3 ? 2 : 0);
+  for (const Unit* up : list) {
+    const Unit& u = *up;
+    if (!u.is_alive) continue;
+    if (only_self && u.handle != hero.handle) continue;
+    if (i >= max_units) break;
+    const float hp = u.health_max ? (float)u.health / (float)u.health_max : 0.f;
+    const double dx = (double)hero.x - (double)u.x, dy = (double)hero.y - (double)u.y;
+    const float dist = (float)std::sqrt(dx * dx + dy * dy);
+    float* r = m + i * 10;
+    r[0] = 1.f - hp;
+    r[1] = u.x / kMapHalf;
+    r[2] = u.y / kMapHalf;
+    r[3] = u.z / 512.f - 0.5f;
+    r[4] = dist / kMapHalf - 0.5f;
+    r[5] = std::sin(u.facing * 2.f * kPi / 360.f);
+    r[6] = std::cos(u.facing * 2.f * kPi / 360.f);
+    r[7] = (dist <= (float)hero.attack_range ? 1.f : 0.f) - 0.5f;
+    r[8] = attacking(u, hero) - 0.5f;
+    r[9] = attacking(hero, u) - 0.5f;
+    int64_t h = (int64_t)u.handle;
+    if (u.invuln || u.attack_immune) h = -1;
+    else if (u.team_id == opp && u.unit_type == TOWER && u.anim == 1500) h = -1;
+    else if (u.team_id == hero.team_id && u.unit_type == TOWER) h = -1;
+    else if (u.team_id == hero.team_id && hp > 0.5f) h = -1;
+    handles[i] = h;
+    ++i;
+  }
+}
+
+// returns number of allied lane creeps (for the creep-spawn sanity check), or -1 when the hero is missing
+int featurize_one(const World& w, int player_id, int team_id, const int* counts, int U, float* env, float* units,
+                  int64_t* handles) {
+  const Unit* hero = nullptr;
+  for (const Unit& u : w.units)
+    if (u.unit_type == HERO && u.player_id == player_id) { hero = &u; break; }
+  if (!hero) return -1;
+  env[0] = w.dota_time / 1200.f;
+  env[1] = std::sin(w.dota_time * 2.f * kPi / 60.f);
+  env[2] = team_id == 3 ? -0.2f : 0.2f;
+  std::vector<const Unit*> ah, eh, anh, enh, ac, ec, at, et;
+  for (const Unit& u : w.units) {
+    const bool ally = u.team_id == hero->team_id;
+    switch (u.unit_type) {
+      case HERO: (ally ? ah : eh).push_back(&u); break;
+      case CREEP_HERO: (ally ? anh : enh).push_back(&u); break;
+      case LANE_CREEP: (ally ? ac : ec).push_back(&u); break;
+      case TOWER:
+        if (ends_with(u.name, "1_mid")) (ally ? at : et).push_back(&u);
+        break;
+      default: break;
+    }
+  }
+  std::vector<const Unit*> anhc(anh), enhc(enh);
+  anhc.insert(anhc.end(), ac.begin(), ac.end());
+  enhc.insert(enhc.end(), ec.begin(), ec.end());
+  if (counts[0] > 1) {   // 5v5: self first, then teammates
+    std::vector<const Unit*> s{hero};
+    for (const Unit* u : ah)
+      if (u->player_id != player_id) s.push_back(u);
+    ah.swap(s);
+  }
+  const std::vector<const Unit*>* lists[6] = {&ah, &eh, &anhc, &enhc, &at, &et};
+  int off = 0;
+  for (int t = 0; t < 6; ++t) {
+    unit_rows(*lists[t], *hero, t == 0 && counts[0] == 1, counts[t], units + off * 10, handles + off);
+    off += counts[t];
+  }
+  (void)U;
+  return (int)ac.size();
+}
+
+// ============================================================================================================
+// Shared-memory MPMC ring
+// ============================================================================================================
+struct RingHeader {
+  uint64_t magic;
+  uint64_t capacity;   // bytes of the data area
+  uint64_t head;       // read offset (monotonic)
+  uint64_t tail;       // write offset (monotonic)
+  uint64_t count;      // messages queued
+  uint64_t dropped;
+  pthread_mutex_t mu;
+  pthread_cond_t not_empty;
+  pthread_cond_t not_full;
+};
+constexpr uint64_t kMagic = 0x444341524e473031ull;   // "DCARNG01"
+
+void deadline_in(double seconds, timespec& ts) {
+  clock_gettime(CLOCK_REALTIME, &ts);
+  const double s = std::max(0.0, seconds);
+  const long sec = (long)s;
+  long nsec = ts.tv_nsec + (long)((s - sec) * 1e9);
+  ts.tv_sec += sec + nsec / 1000000000L;
+  ts.tv_nsec = nsec % 1000000000L;
+}
+
+class RingCore {
+ public:
+  RingCore(const std::string& name, uint64_t capacity, bool create) : name_(name) {
+    const int flags = create ? (O_CREAT | O_RDWR) : O_RDWR;
+    fd_ = shm_open(name.c_str(), flags, 0600);
+    if (fd_ < 0) throw std::runtime_error("shm_open failed: " + std::string(strerror(errno)));
+    size_ = sizeof(RingHeader) + capacity;
+    if (create && ftruncate(fd_, (off_t)size_) != 0) throw std::runtime_error("ftruncate failed");
+    if (!create) {
+      struct stat st;
+      fstat(fd_, &st);
+      size_ = (size_t)st.st_size;
+    }
+    base_ = (uint8_t*)mmap(nullptr, size_, PROT_READ | PROT_WRITE, MAP_SHARED, fd_, 0);
+    if (base_ == MAP_FAILED) throw std::runtime_error("mmap failed");
+    hdr_ = (RingHeader*)base_;
+    data_ = base_ + sizeof(RingHeader);
+    if (create) {
+      std::memset(hdr_, 0, sizeof(RingHeader));
+      hdr_->capacity = capacity;
+      pthread_mutexattr_t ma;
+      pthread_mutexattr_init(&ma);
+      pthread_mutexattr_setpshared(&ma, PTHREAD_PROCESS_SHARED);
+      pthread_mutexattr_setrobust(&ma, PTHREAD_MUTEX_ROBUST);
+      pthread_mutex_init(&hdr_->mu, &ma);
+      pthread_condattr_t ca;
+      pthread_condattr_init(&ca);
+      pthread_condattr_setpshared(&ca, PTHREAD_PROCESS_SHARED);
+      pthread_cond_init(&hdr_->not_empty, &ca);
+      pthread_cond_init(&hdr_->not_full, &ca);
+      hdr_->magic = kMagic;
+    } else if (hdr_->magic != kMagic) {
+      throw std::runtime_error("not a dotaclient_amd shm ring");
+    }
+  }
+  ~RingCore() {
+    if (base_ && base_ != MAP_FAILED) munmap(base_, size_);
+    if (fd_ >= 0) close(fd_);
+  }
+
+  void lock() {
+    const int r = pthread_mutex_lock(&hdr_->mu);
+    if (r == EOWNERDEAD) pthread_mutex_consistent(&hdr_->mu);   // a producer died holding the lock
+  }
+  void unlock() { pthread_mutex_unlock(&hdr_->mu); }
+
+  // message = u64 length + payload, padded to 8 bytes; a length of ~0 marks "wrap to start"
+  bool push(const char* msg_data, size_t msg_size, double timeout, bool drop_oldest) {
+    const uint64_t need = 8 + ((msg_size + 7) & ~7ull);
+    if (need + 8 > hdr_->capacity) throw std::invalid_argument("message larger than ring");
+    lock();
+    while (true) {
+      const uint64_t used = hdr_->tail - hdr_->head;
+      const uint64_t pos = hdr_->tail % hdr_->capacity;
+      const uint64_t to_end = hdr_->capacity - pos;
+      const uint64_t want = (to_end < need) ? to_end + need : need;
+      if (used + want <= hdr_->capacity) {
+        if (to_end < need) {
+          if (to_end >= 8) { const uint64_t wrap = ~0ull; std::memcpy(data_ + pos, &wrap, 8); }
+          hdr_->tail += to_end;
+        }
+        const uint64_t p2 = hdr_->tail % hdr_->capacity;
+        const uint64_t len = msg_size;
+        std::memcpy(data_ + p2, &len, 8);
+        std::memcpy(data_ + p2 + 8, msg_data, msg_size);
+        hdr_->tail += need;
+        hdr_->count += 1;
+        pthread_cond_signal(&hdr_->not_empty);
+        unlock();
+        return true;
+      }
+      if (drop_oldest && hdr_->count > 0) {
+        pop_locked(nullptr);
+        hdr_->dropped += 1;
+        continue;
+      }
+      if (timeout == 0.0) { unlock(); return false; }
+      if (timeout < 0) {
+        pthread_cond_wait(&hdr_->not_full, &hdr_->mu);
+      } else {
+        timespec ts;
+        deadline_in(timeout, ts);
+        if (pthread_cond_timedwait(&hdr_->not_full, &hdr_->mu, &ts) == ETIMEDOUT) { unlock(); return false; }
+      }
+    }
+  }
+
+  bool pop_locked(std::string* out) {
+    if (hdr_->count == 0) return false;
+    uint64_t pos = hdr_->head % hdr_->capacity;
+    uint64_t len;
+    if (hdr_->capacity - pos < 8) { hdr_->head += hdr_->capacity - pos; pos = 0; }
+    std::memcpy(&len, data_ + pos, 8);
+    if (len == ~0ull) {
+      hdr_->head += hdr_->capacity - pos;
+      pos = 0;
+      std::memcpy(&len, data_, 8);
+    }
+    if (out) out->assign((const char*)data_ + pos + 8, len);
+    hdr_->head += 8 + ((len + 7) & ~7ull);
+    hdr_->count -= 1;
+    pthread_cond_signal(&hdr_->not_full);
+    return true;
+  }
+
+  bool pop(std::string* out, double timeout) {
+    bool got = false;
+    lock();
+    while (!(got = pop_locked(out))) {
+      if (timeout == 0.0) break;
+      if (timeout < 0) {
+        pthread_cond_wait(&hdr_->not_empty, &hdr_->mu);
+      } else {
+        timespec ts;
+        deadline_in(timeout, ts);
+        if (pthread_cond_timedwait(&hdr_->not_empty, &hdr_->mu, &ts) == ETIMEDOUT) { got = pop_locked(out); break; }
+      }
+    }
+    unlock();
+    return got;
+  }
+
+  uint64_t size() { lock(); const uint64_t c = hdr_->count; unlock(); return c; }
+  uint64_t dropped() { return hdr_->dropped; }
+  static void unlink(const std::string& name) { shm_unlink(name.c_str()); }
+
+ private:
+  std::string name_;
+  int fd_ = -1;
+  size_t size_ = 0;
+  uint8_t* base_ = nullptr;
+  RingHeader* hdr_ = nullptr;
+  uint8_t* data_ = nullptr;
+};
+
+// ============================================================================================================
+inline uint32_t crc32c_raw(const uint8_t* p, size_t n) {
+  uint64_t crc = 0xFFFFFFFFu;
+  while (n >= 8) { uint64_t v; std::memcpy(&v, p, 8); crc = _mm_crc32_u64(crc, v); p += 8; n -= 8; }
+  while (n--) crc = _mm_crc32_u8((uint32_t)crc, *p++);
+  return (uint32_t)crc ^ 0xFFFFFFFFu;
+}
+
+}  // namespace dca_native

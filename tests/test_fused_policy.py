@@ -132,3 +132,26 @@ def test_loss_prep_kernel_matches_batch_norms(gpu_ops):
         gpu_ops.loss_prep(act, ws, out)
         torch.testing.assert_close(out, ref, rtol=1e-6, atol=0)
     assert int(ws[-1]) == 0
+
+
+@pytest.mark.parametrize('preset', ['lstm512', '5v5'])
+def test_fused_step_is_bitwise_deterministic(gpu_ops, preset):
+    """Deterministic-mode check: every reduction on the fused step runs in a fixed order (no float
+    atomics), so two learners fed the same replay minibatches end bit-identical."""
+    from dotaclient_amd.learner.replay import HbmReplay
+    cfg = get_config(preset)
+    torch.manual_seed(0)
+    pol = Policy(cfg)
+    ref = copy.deepcopy(pol)
+    learners = [Learner(p, LossConfig(algo='ppo'), device='cuda', backend='fused', dp=False) for p in (pol, ref)]
+    reps = []
+    for L in learners:
+        assert L.enable_graph(warmup=1)
+        rep = HbmReplay(6, 48, cfg.layout, cfg.hidden, 'cuda', seed=11)
+        rep.add(make_batch(6, 48, cfg.layout, cfg.hidden, device='cuda', seed=4))
+        reps.append(rep)
+    for _ in range(3):
+        ms = [L.train_step_replay(rep, 4) for L, rep in zip(learners, reps)]
+    torch.cuda.synchronize()
+    assert torch.equal(learners[0].flat.flat, learners[1].flat.flat)
+    assert torch.equal(ms[0]['loss'], ms[1]['loss']) and torch.equal(ms[0]['grad_norm'], ms[1]['grad_norm'])
