@@ -144,6 +144,13 @@ class Learner:
         """Minibatch of replay rows ``idx`` gathered straight into time-major rows: one index_select per field
         over the pool viewed as (capacity·S, …) — no batch-major copy, no transpose."""
         B = idx.numel()
+        if idx.is_cuda:                 # one HIP launch for every field (ops/csrc/glue.hip replay_gather)
+            from .. import ops
+            seq = [k for k in ('h0', 'c0') if k in replay.data]
+            outs = ops.require().replay_gather([replay.data[k] for k in self.STEP_FIELDS] +
+                                               [replay.data[k] for k in seq], len(self.STEP_FIELDS),
+                                               idx.contiguous())
+            return dict(zip(list(self.STEP_FIELDS) + seq, outs))
         ar = getattr(self, '_arange', None)
         if ar is None or ar.numel() < S or ar.device != idx.device:
             ar = self._arange = torch.arange(max(S, 1), device=idx.device, dtype=torch.long)

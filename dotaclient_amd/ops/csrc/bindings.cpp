@@ -630,6 +630,46 @@ std::vector<torch::Tensor> ln_bwd(torch::Tensor dxn, torch::Tensor e0, torch::Te
   return {de0, out.narrow(0, 0, 128), out.narrow(0, 128, 128), out.narrow(0, 256, 768).view({6, 128})};
 }
 
+// Minibatch gather from an HBM replay pool into time-major rows (one launch for all fields). pools: per-step
+// fields (capacity, S, …) then per-sequence fields (capacity, …) (n_step of them are per-step); idx (B) int64 device.
+// Returns the gathered tensors: per-step fields as (S·B, …), per-sequence fields as (B, …).
+std::vector<torch::Tensor> replay_gather(std::vector<torch::Tensor> pools, int64_t n_step, torch::Tensor idx) {
+  CHECK_DEV(idx); CHECK_CONTIG(idx); CHECK_DT(idx, at::kLong);
+  TORCH_CHECK(!pools.empty() && pools.size() <= 12, "replay_gather: 1..12 fields");
+  const int B = idx.numel();
+  const int S = n_step > 0 ? pools[0].size(1) : 1;
+  std::vector<torch::Tensor> out;
+  std::vector<const void*> src;
+  std::vector<void*> dst;
+  std::vector<long long> rb;
+  std::vector<int> ps;
+  for (size_t i = 0; i < pools.size(); ++i) {
+    const torch::Tensor& p = pools[i];
+    CHECK_DEV(p); CHECK_CONTIG(p);
+    const bool step = (int64_t)i < n_step;
+    TORCH_CHECK(!step || (p.dim() >= 2 && p.size(1) == S), "replay_gather: per-step pools must be (capacity, S, ...)");
+    std::vector<int64_t> shape;
+    if (step) {
+      shape.push_back((int64_t)S * B);
+      for (int d = 2; d < p.dim(); ++d) shape.push_back(p.size(d));
+    } else {
+      shape.push_back(B);
+      for (int d = 1; d < p.dim(); ++d) shape.push_back(p.size(d));
+    }
+    auto o = torch::empty(shape, p.options());
+    const int64_t per = step ? p.numel() / (p.size(0) * S) : p.numel() / p.size(0);
+    src.push_back(p.data_ptr());
+    dst.push_back(o.data_ptr());
+    rb.push_back((long long)(per * p.element_size()));
+    ps.push_back(step ? 1 : 0);
+    out.push_back(o);
+  }
+  hip_check(dca_replay_gather(src.data(), dst.data(), rb.data(), ps.data(), (int)pools.size(), ptr<long long>(idx), S,
+                              B, cur_stream()),
+            "dca_replay_gather");
+  return out;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -676,5 +716,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_pool", &attn_pool, "per-type max-pool + argmax of attended embeddings into x896");
   m.def("attn_demb", &attn_demb, "dE1 = dtl*q + pool gradient at the argmax unit");
   m.def("ln_bwd", &ln_bwd, "LayerNorm backward + residual: (dE0, dgamma, dbeta, dbt)");
+  m.def("replay_gather", &replay_gather, "minibatch gather from an HBM replay pool into time-major rows (one launch)");
   m.def("returns_scan", &returns_scan, "segmented reverse scan: discounted returns / GAE + per-team EMA normalisation");
 }

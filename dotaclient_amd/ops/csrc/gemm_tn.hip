@@ -211,42 +211,45 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_kernel(Args a) {
 #undef BS
 }
 
-// Fixed-order (deterministic) sum of the split-K slabs, optional row map / accumulate. A block owns 16 float4 outputs
-// × 16 split phases: thread (phase p, output o) sums splits p, p+16, … with 4 loads in flight, then a fixed LDS
-// fold over the phases — many threads per output, so a long split list (K = 716 800 unit rows of the 5v5 attention
-// weight gradients → ≈380 splits of a single tile) is not one latency-bound serial chain per output.
-constexpr int kRedPh = 16;
+// Fixed-order (deterministic) sum of the split-K slabs, optional row map / accumulate. A block of 256 threads owns
+// 256/P float4 outputs × P split phases (P = power of two ≤ min(16, splits)): thread (phase p, output o) sums splits
+// p, p+P, … with 4 loads in flight, then a fixed LDS fold over the phases — a long split list (K = 716 800 unit rows
+// of the 5v5 attention weight gradients → ≈380 splits of one tile) is not one latency-bound chain per output, and
+// a short one (6-25 splits of the 1v1 gradients) keeps every thread busy.
 __global__ __launch_bounds__(256) void gemm_tn_reduce(const float* __restrict__ slab, int splits, int M, int N,
                                                       float* __restrict__ C, int ldc, const int* __restrict__ perm,
-                                                      int accumulate, float* __restrict__ colsum) {
+                                                      int accumulate, float* __restrict__ colsum, int lp) {
+  const int P = 1 << lp, OPB = 256 >> lp;
   const int n4 = N >> 2;
-  const size_t plane = (size_t)M * N;
-  const int ph = threadIdx.x >> 4, oi = threadIdx.x & 15;
-  __shared__ f32x4 red[kRedPh][16];
+  const size_t plane4 = (size_t)M * N / 4;
+  const int ph = threadIdx.x >> (8 - lp), oi = threadIdx.x & (OPB - 1);
+  __shared__ f32x4 red[256];
   const int nout = M * n4;
-  for (int base = blockIdx.x * 16; base < nout; base += gridDim.x * 16) {
+  for (int base = blockIdx.x * OPB; base < nout; base += gridDim.x * OPB) {
     const int idx = base + oi;
     f32x4 s = {0.f, 0.f, 0.f, 0.f};
     if (idx < nout) {
       const int m = idx / n4, n = (idx % n4) * 4;
       const f32x4* src = reinterpret_cast<const f32x4*>(slab + (size_t)m * N + n);
       int sp = ph;
-      for (; sp + 3 * kRedPh < splits; sp += 4 * kRedPh) {
-        const f32x4 v0 = __builtin_nontemporal_load(src + (size_t)(sp + 0 * kRedPh) * (plane / 4));
-        const f32x4 v1 = __builtin_nontemporal_load(src + (size_t)(sp + 1 * kRedPh) * (plane / 4));
-        const f32x4 v2 = __builtin_nontemporal_load(src + (size_t)(sp + 2 * kRedPh) * (plane / 4));
-        const f32x4 v3 = __builtin_nontemporal_load(src + (size_t)(sp + 3 * kRedPh) * (plane / 4));
+      for (; sp + 3 * P < splits; sp += 4 * P) {
+        const f32x4 v0 = __builtin_nontemporal_load(src + (size_t)(sp + 0 * P) * plane4);
+        const f32x4 v1 = __builtin_nontemporal_load(src + (size_t)(sp + 1 * P) * plane4);
+        const f32x4 v2 = __builtin_nontemporal_load(src + (size_t)(sp + 2 * P) * plane4);
+        const f32x4 v3 = __builtin_nontemporal_load(src + (size_t)(sp + 3 * P) * plane4);
         s += v0;
         s += v1;
         s += v2;
         s += v3;
       }
-      for (; sp < splits; sp += kRedPh) s += __builtin_nontemporal_load(src + (size_t)sp * (plane / 4));
+      for (; sp < splits; sp += P) s += __builtin_nontemporal_load(src + (size_t)sp * plane4);
     }
-    red[ph][oi] = s;
-    __syncthreads();
+    if (P > 1) {
+      red[threadIdx.x] = s;
+      __syncthreads();
+    }
     if (ph == 0 && idx < nout) {
-      for (int k = 1; k < kRedPh; ++k) s += red[k][oi];
+      for (int k = 1; k < P; ++k) s += red[k * OPB + oi];
       const int m = idx / n4, n = (idx % n4) * 4;
       float* cp = C + (size_t)(perm ? perm[m] : m) * ldc + n;
       if (accumulate) {
@@ -254,30 +257,30 @@ __global__ __launch_bounds__(256) void gemm_tn_reduce(const float* __restrict__ 
       }
       cp[0] = s[0]; cp[1] = s[1]; cp[2] = s[2]; cp[3] = s[3];
     }
-    __syncthreads();
+    if (P > 1) __syncthreads();
   }
-  if (colsum != nullptr) {       // same phase split for the column sums: 16 columns × 16 split phases per pass
-    const float* cs = slab + (size_t)splits * plane;
-    __shared__ float cred[kRedPh][16];
-    for (int base = blockIdx.x * 16; base < M; base += gridDim.x * 16) {
+  if (colsum != nullptr) {       // same phase split for the column sums
+    const float* cs = slab + (size_t)splits * plane4 * 4;
+    __shared__ float cred[256];
+    for (int base = blockIdx.x * OPB; base < M; base += gridDim.x * OPB) {
       const int m = base + oi;
       float v = 0.f;
       if (m < M) {
         int sp = ph;
-        for (; sp + 3 * kRedPh < splits; sp += 4 * kRedPh) {
-          const float v0 = cs[(size_t)(sp + 0 * kRedPh) * M + m], v1 = cs[(size_t)(sp + 1 * kRedPh) * M + m];
-          const float v2 = cs[(size_t)(sp + 2 * kRedPh) * M + m], v3 = cs[(size_t)(sp + 3 * kRedPh) * M + m];
+        for (; sp + 3 * P < splits; sp += 4 * P) {
+          const float v0 = cs[(size_t)(sp + 0 * P) * M + m], v1 = cs[(size_t)(sp + 1 * P) * M + m];
+          const float v2 = cs[(size_t)(sp + 2 * P) * M + m], v3 = cs[(size_t)(sp + 3 * P) * M + m];
           v += v0;
           v += v1;
           v += v2;
           v += v3;
         }
-        for (; sp < splits; sp += kRedPh) v += cs[(size_t)sp * M + m];
+        for (; sp < splits; sp += P) v += cs[(size_t)sp * M + m];
       }
-      cred[ph][oi] = v;
+      cred[threadIdx.x] = v;
       __syncthreads();
       if (ph == 0 && m < M) {
-        for (int k = 1; k < kRedPh; ++k) v += cred[k][oi];
+        for (int k = 1; k < P; ++k) v += cred[k * OPB + oi];
         float* cp = colsum + (perm ? perm[m] : m);
         *cp = accumulate ? *cp + v : v;
       }
@@ -313,11 +316,13 @@ extern "C" hipError_t dca_gemm_tn(const short* A, int lda, const short* B, int l
   hipLaunchKernelGGL(gemm_tn_kernel, dim3(tiles, splits), dim3(kThreads), 4 * kTileBytes, st, a);
   DCA_CHECK_LAUNCH();
   if (splits > 1) {
-    const int n = M * (N / 4);
-    int blocks = (n + 15) / 16;
+    int lp = 0;
+    while (lp < 4 && (2 << lp) <= splits) ++lp;            // P = 2^lp ≤ min(16, splits)
+    const int n = M * (N / 4), opb = 256 >> lp;
+    int blocks = (n + opb - 1) / opb;
     if (blocks > 4096) blocks = 4096;
     hipLaunchKernelGGL(gemm_tn_reduce, dim3(blocks), dim3(256), 0, st, slab, splits, M, N, C, ldc, perm, accumulate,
-                       colsum);
+                       colsum, lp);
     DCA_CHECK_LAUNCH();
   }
   return hipSuccess;

@@ -11,6 +11,8 @@
 //                        (was ≈15 launches: dtl·seg GEMM, a split-K bmm, column sums, the env ReLU mask and a
 //                        128×3 fp32 GEMM that hipBLASLt ran at 55 µs), deterministic per-block partials +
 //                        enc_small_reduce.
+//   replay_gather_kernel the learner minibatch straight from the HBM replay pool in TIME-MAJOR row order, every
+//                        field in one launch (was a row-index computation + one index_select per field).
 //   weight_prep_kernel   every per-step working copy of the weights in one gather pass over the flat fp32 buffer:
 //                        bf16 images (stacked / permuted / transposed / zero-padded, via an int32 source map) and
 //                        fp32 images (optionally the sum of two sources: b_ih + b_hh).
@@ -279,7 +281,68 @@ __global__ __launch_bounds__(256) void enc_small_reduce(const float* __restrict_
                                        red[3][threadIdx.x];
 }
 
+constexpr int kMaxGather = 12;
+struct GatherField {
+  const char* src;      // pool base: (capacity, S, …) per-step field or (capacity, …) per-sequence field
+  char* dst;            // (S·B, …) time-major rows, or (B, …)
+  long long row_bytes;  // bytes per time step (per-step) or per sequence
+  int per_step;
+  int unit;             // copy granule: 16, 4 or 1 bytes (divides row_bytes and the alignment)
+};
+struct GatherArgs {
+  GatherField f[kMaxGather];
+  const long long* idx;
+  int S, B;
+};
+
+template <typename T>
+__device__ __forceinline__ void gather_rows(const GatherField& F, const long long* __restrict__ idx, int S, int B) {
+  const long long wpr = F.row_bytes / (long long)sizeof(T);
+  const long long rows = F.per_step ? (long long)S * B : B;
+  const long long total = rows * wpr;
+  const T* src = reinterpret_cast<const T*>(F.src);
+  T* dst = reinterpret_cast<T*>(F.dst);
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const long long r = i / wpr, w = i - r * wpr;
+    long long srow;
+    if (F.per_step) {
+      const long long t = r / B, b = r - t * B;
+      srow = idx[b] * S + t;
+    } else {
+      srow = idx[r];
+    }
+    dst[r * wpr + w] = src[srow * wpr + w];
+  }
+}
+
+__global__ __launch_bounds__(256) void replay_gather_kernel(GatherArgs a) {
+  const GatherField& F = a.f[blockIdx.y];
+  if (F.unit == 16) gather_rows<uint4>(F, a.idx, a.S, a.B);
+  else if (F.unit == 4) gather_rows<unsigned>(F, a.idx, a.S, a.B);
+  else gather_rows<unsigned char>(F, a.idx, a.S, a.B);
+}
+
 }  // namespace
+
+extern "C" hipError_t dca_replay_gather(const void* const* src, void* const* dst, const long long* row_bytes,
+                                        const int* per_step, int nf, const long long* idx, int S, int B,
+                                        hipStream_t st) {
+  if (nf < 1 || nf > kMaxGather) return hipErrorInvalidValue;
+  GatherArgs a{};
+  for (int i = 0; i < nf; ++i) {
+    const unsigned long long align = (unsigned long long)src[i] | (unsigned long long)dst[i];
+    int unit = 1;
+    if (row_bytes[i] % 16 == 0 && align % 16 == 0) unit = 16;
+    else if (row_bytes[i] % 4 == 0 && align % 4 == 0) unit = 4;
+    a.f[i] = GatherField{static_cast<const char*>(src[i]), static_cast<char*>(dst[i]), row_bytes[i], per_step[i], unit};
+  }
+  a.idx = idx;
+  a.S = S;
+  a.B = B;
+  hipLaunchKernelGGL(replay_gather_kernel, dim3(256, nf), dim3(256), 0, st, a);
+  DCA_CHECK_LAUNCH();
+  return hipSuccess;
+}
 
 extern "C" int dca_enc_small_out() { return kSgOut; }
 extern "C" int dca_enc_small_blocks() { return kSgBlocks; }

@@ -95,4 +95,7 @@ hipError_t dca_ln_bwd(const short* dxn, const short* e0, const float* bsub, cons
                       const float* rstd, const short* de1, const unsigned char* type_of, short* de0, float* part,
                       int nblk, float* out, int R, hipStream_t st);
 
+hipError_t dca_replay_gather(const void* const* src, void* const* dst, const long long* row_bytes, const int* per_step,
+                             int nf, const long long* idx, int S, int B, hipStream_t st);
+
 }  // extern "C"

@@ -1,5 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
-for c in 1 2 4 7; do
-  DCA_PIPELINE_CHUNKS=$c timeout -k 10 300 python -u bench.py --actor 0 --steps 10 --warmup 3 > gpurun_out/bench_c$c.log 2>&1 || exit 1
-done
+timeout -k 10 300 python -u -m pytest tests/test_gemm_tn.py tests/test_fused_policy.py -x -q --timeout 120 --timeout-method thread > gpurun_out/fused_test.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --actor 0 > gpurun_out/bench.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --model 5v5 --steps 10 --warmup 3 --actor 0 > gpurun_out/bench_5v5.log 2>&1
