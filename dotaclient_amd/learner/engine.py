@@ -194,7 +194,11 @@ class Learner:
                 body()
             cur.wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s):
+            # with a process group up, RCCL's watchdog thread queries events while we capture: only this thread's
+            # calls are capture-checked ('thread_local'), the watchdog's are not (they touch no captured stream)
+            import torch.distributed as dist
+            mode = 'thread_local' if (dist.is_available() and dist.is_initialized()) else 'global'
+            with torch.cuda.graph(g, stream=s, capture_error_mode=mode):
                 out = body()
             graphs[key] = (g, out)
             self.graph = g

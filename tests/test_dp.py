@@ -44,8 +44,10 @@ def _toy_worker(rank, world, port, q):
         dp.zero_grad()
         out.backward()
         dp.sync()
-        q.put((rank, {k: v.detach().clone() for k, v in m.state_dict().items()},
-               {n: p.grad.clone() for n, p in m.named_parameters()}, dp.counts.clone()))
+        # numpy, not torch tensors: torch.multiprocessing shares tensors by fd through the child's resource sharer,
+        # which is gone once the child exits — the parent may unpickle later (flaky FileNotFoundError)
+        q.put((rank, {k: v.detach().numpy().copy() for k, v in m.state_dict().items()},
+               {n: p.grad.numpy().copy() for n, p in m.named_parameters()}, dp.counts.numpy().copy()))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover
@@ -63,7 +65,8 @@ def test_sparse_param_semantics_two_ranks():
     for _ in range(world):
         r, sd, grads, counts = q.get(timeout=120)
         assert grads is not None, sd
-        res[r] = (sd, grads, counts)
+        res[r] = ({k: torch.from_numpy(v) for k, v in sd.items()}, {k: torch.from_numpy(v) for k, v in grads.items()},
+                  torch.from_numpy(counts))
     for p in ps:
         p.join(timeout=60)
     sd0, g0, c0 = res[0]
@@ -93,7 +96,7 @@ def _learner_worker(rank, world, port, q, batch_seed):
         L = Learner(Policy(cfg), LossConfig(algo='ppo', vf_coef=0.0), device='cpu', backend='torch', overlap=False)
         b = make_batch(4, 16, cfg.layout, cfg.hidden, seed=batch_seed + rank)
         L.train_step(b)
-        q.put((rank, L.flat.flat.clone(), L.dp.counts.clone()))
+        q.put((rank, L.flat.flat.numpy().copy(), L.dp.counts.numpy().copy()))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover
@@ -114,7 +117,7 @@ def test_dp_step_equals_single_process_average():
     for _ in range(world):
         r, flat, counts = q.get(timeout=180)
         assert counts is not None, flat
-        out[r] = (flat, counts)
+        out[r] = (torch.from_numpy(flat), torch.from_numpy(counts))
     for p in ps:
         p.join(timeout=60)
     assert torch.equal(out[0][0], out[1][0])
@@ -146,8 +149,8 @@ def _resume_worker(rank, world, port, root, q):
         cfg = OptimizerConfig(log_dir=ld, batch_size=2, seq_len=16, seq_per_epoch=2, epochs=1, model='lstm128',
                               device='cpu', backend='torch')
         opt = DotaOptimizer(cfg, InProcBroker(), checkpoint=rank == 0)
-        q.put((rank, opt.iteration_start, opt.learner.opt.exp_avg.clone(), opt.learner.opt.steps.clone(),
-               opt.learner.flat.flat.clone()))
+        q.put((rank, opt.iteration_start, opt.learner.opt.exp_avg.numpy().copy(),
+               opt.learner.opt.steps.numpy().copy(), opt.learner.flat.flat.numpy().copy()))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover
@@ -175,7 +178,8 @@ def test_resume_equalises_iteration_and_optimizer_state(tmp_path):
     ps = [ctx.Process(target=_resume_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
     for p in ps:
         p.start()
-    res = dict((r[0], r[1:]) for r in (q.get(timeout=300) for _ in range(world)))
+    res = dict((r[0], tuple(torch.from_numpy(x) if hasattr(x, 'dtype') else x for x in r[1:]))
+               for r in (q.get(timeout=300) for _ in range(world)))
     for p in ps:
         p.join(timeout=60)
     assert all(isinstance(v[0], int) for v in res.values()), res

@@ -155,3 +155,47 @@ def test_fused_step_is_bitwise_deterministic(gpu_ops, preset):
     torch.cuda.synchronize()
     assert torch.equal(learners[0].flat.flat, learners[1].flat.flat)
     assert torch.equal(ms[0]['loss'], ms[1]['loss']) and torch.equal(ms[0]['grad_norm'], ms[1]['grad_norm'])
+
+
+def _pg_worker(port, q):
+    import os
+    import torch.distributed as dist
+    try:
+        os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK='0', WORLD_SIZE='1')
+        torch.cuda.set_device(0)
+        dist.init_process_group('nccl', rank=0, world_size=1, device_id=torch.device('cuda:0'))
+        t = torch.ones(4, device='cuda')
+        dist.all_reduce(t)                      # the RCCL watchdog now tracks work while we capture below
+        from dotaclient_amd.learner.replay import HbmReplay
+        cfg = get_config('lstm128')
+        L = Learner(Policy(cfg), LossConfig(algo='ppo'), device='cuda', backend='fused')
+        assert L.enable_graph(warmup=1)
+        rep = HbmReplay(4, 32, cfg.layout, cfg.hidden, 'cuda', seed=1)
+        rep.add(make_batch(4, 32, cfg.layout, cfg.hidden, device='cuda', seed=2))
+        for _ in range(4):
+            m = L.train_step_replay(rep, 2)
+            dist.all_reduce(t)
+        torch.cuda.synchronize()
+        q.put(('ok', float(m['loss']), L.graph is not None))
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put(('err', repr(e), False))
+
+
+def test_graph_capture_with_rccl_process_group(gpu_ops):
+    """The captured learner step coexists with an initialised RCCL process group (its watchdog thread runs during
+    capture) — the multi-GPU bench path, rehearsed with one rank on the one available GPU."""
+    import socket
+    import torch.multiprocessing as mp
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    p = ctx.Process(target=_pg_worker, args=(port, q))
+    p.start()
+    res = q.get(timeout=240)
+    p.join(timeout=60)
+    assert res[0] == 'ok', res
+    assert res[2] and res[1] == res[1]
