@@ -343,7 +343,9 @@ __device__ __forceinline__ void lstm_team_fwd_body(
             const bf16x8 a = *reinterpret_cast<const bf16x8*>(&hl[par][mt * 16 + col][ks * 32 + 8 * kg]);
             acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[ks], acc, 0, 0, 0);
           }
-          // ---- 4×4 transpose inside each group of 4 lanes: lane (q' = col&3) gets gate q of row 4kg+q'
+          // ---- 4×4 transpose inside each group of 4 lanes: lane (q' = col&3) gets gate q of row 4kg+q'. Round j:
+          // lane a sends its value for row (a-j)&3 and receives from lane (a+j)&3 of its quad — a DPP quad_perm
+          // (register-to-register, a few cycles) instead of an LDS-routed ds_bpermute
           float gq0 = 0.f, gq1 = 0.f, gq2 = 0.f, gq3 = 0.f;
           const int q0 = col & 3;
 #pragma unroll
@@ -351,7 +353,11 @@ __device__ __forceinline__ void lstm_team_fwd_body(
             const int sel = (q0 - j) & 3;                       // what this lane sends in round j
             const float send = sel == 0 ? acc[0] : sel == 1 ? acc[1] : sel == 2 ? acc[2] : acc[3];
             const int qs = (q0 + j) & 3;                        // gate carried by the received value
-            const float got = __shfl(send, (lane & ~3) | qs, 64);
+            // quad_perm [(0+j)&3, (1+j)&3, (2+j)&3, (3+j)&3]: 0xE4 (identity), 0x39, 0x4E, 0x93
+            float got = send;
+            if (j == 1) got = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), 0x39, 0xF, 0xF, false));
+            if (j == 2) got = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), 0x4E, 0xF, 0xF, false));
+            if (j == 3) got = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send), 0x93, 0xF, 0xF, false));
             gq0 = qs == 0 ? got : gq0;
             gq1 = qs == 1 ? got : gq1;
             gq2 = qs == 2 ? got : gq2;
