@@ -373,7 +373,8 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           if (b < B) { creg[mt] = c; hreg[mt] = hv; }
           TSTAMP(3);
           // ---- publish h_t: granule {h(u), h(u+1)} by the even-unit lane (partner unit is 4 lanes up)
-          const float hnb = __shfl_down(hv, 4, 64);
+          // partner unit's h from 4 lanes up, same 16-lane row: DPP row_shl:4 (register-to-register)
+          const float hnb = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(hv), 0x104, 0xF, 0xF, false));
           if (b < B && ((col >> 2) & 1) == 0) {
             const unsigned pl = (unsigned)(unsigned short)dca::f2bf(hv) | ((unsigned)(unsigned short)dca::f2bf(hnb) << 16);
             const u32x2 gv = {pl, tagbase | (unsigned)(t + 1)};
