@@ -50,6 +50,12 @@ __device__ __forceinline__ bf16x8 frag_tr(const short* img, int pitch, int k0, i
   return f;
 }
 
+// same fragment as frag_row, straight from global memory (row stride `stride` elements)
+__device__ __forceinline__ bf16x8 frag_row_g(const short* __restrict__ src, int stride, int m0, int k0) {
+  const int l = threadIdx.x & 63;
+  return *reinterpret_cast<const bf16x8*>(src + (size_t)(m0 + (l & 15)) * stride + k0 + 8 * (l >> 4));
+}
+
 __device__ __forceinline__ f32x4 mfma(bf16x8 a, bf16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -105,22 +111,21 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const short* __restrict__ e
 // each 4 heads × 32. Writes o (N·64, 128) bf16 and lse (N, 4, 64) f32 (natural-log, scaled scores).
 __global__ __launch_bounds__(64) void attn_fwd_kernel(const short* __restrict__ qkv, short* __restrict__ o,
                                                       float* __restrict__ lse, float scale) {
-  __shared__ __attribute__((aligned(16))) short Qs[kU * kP32], Ks[kU * kP32], Vs[kU * kP32];
+  // Q and K fragments are row reads straight from global memory; only V (read by columns) and Pᵀ go through LDS
+  // (14 KB per wave → ≈11 waves per CU instead of 6)
+  __shared__ __attribute__((aligned(16))) short Vs[kU * kP32];
   __shared__ __attribute__((aligned(16))) short PT[kU * kP64];   // P transposed: [key j][query i]
   const int n = blockIdx.x >> 2, h = blockIdx.x & 3;
   const int l = threadIdx.x, kg = l >> 4, li = l & 15;
   const short* base = qkv + (size_t)n * kU * 384 + h * kHd;
-  stage64x32(Qs, base, 384);
-  stage64x32(Ks, base + 128, 384);
-  stage64x32(Vs, base + 256, 384);
-  __syncthreads();
-  // S = Q Kᵀ: tile (a, b) = queries 16a…, keys 16b…; lane holds rows 16a + 4kg + r, column 16b + li
-  f32x4 s[4][4];
   bf16x8 qa[4], kb[4];
 #pragma unroll
-  for (int a = 0; a < 4; ++a) qa[a] = frag_row(Qs, kP32, 16 * a, 0);
+  for (int a = 0; a < 4; ++a) qa[a] = frag_row_g(base, 384, 16 * a, 0);
 #pragma unroll
-  for (int b = 0; b < 4; ++b) kb[b] = frag_row(Ks, kP32, 16 * b, 0);
+  for (int b = 0; b < 4; ++b) kb[b] = frag_row_g(base + 128, 384, 16 * b, 0);
+  stage64x32(Vs, base + 256, 384);
+  // S = Q Kᵀ: tile (a, b) = queries 16a…, keys 16b…; lane holds rows 16a + 4kg + r, column 16b + li
+  f32x4 s[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -174,7 +179,8 @@ __global__ __launch_bounds__(64) void attn_fwd_kernel(const short* __restrict__ 
 __global__ __launch_bounds__(64) void attn_bwd_kernel(const short* __restrict__ qkv, const short* __restrict__ o,
                                                       const short* __restrict__ do_, const float* __restrict__ lse,
                                                       short* __restrict__ dqkv, float scale) {
-  __shared__ __attribute__((aligned(16))) short Qs[kU * kP32], Ks[kU * kP32], Vs[kU * kP32], Ds[kU * kP32];
+  // V is only read by rows (from global); Q, K and ∂O are also read by columns (transposed reads) → LDS
+  __shared__ __attribute__((aligned(16))) short Qs[kU * kP32], Ks[kU * kP32], Ds[kU * kP32];
   __shared__ __attribute__((aligned(16))) short PT[kU * kP64], ST[kU * kP64];   // Pᵀ and (scale·dS)ᵀ, [j][i]
   __shared__ float Dl[kU], Ll[kU];
   const int n = blockIdx.x >> 2, h = blockIdx.x & 3;
@@ -182,7 +188,6 @@ __global__ __launch_bounds__(64) void attn_bwd_kernel(const short* __restrict__ 
   const short* base = qkv + (size_t)n * kU * 384 + h * kHd;
   stage64x32(Qs, base, 384);
   stage64x32(Ks, base + 128, 384);
-  stage64x32(Vs, base + 256, 384);
   stage64x32(Ds, do_ + (size_t)n * kU * kD + h * kHd, kD);
   {  // D_i = Σ_d ∂O[i][d]·O[i][d] (lane = query i), LSE
     const short* orow = o + ((size_t)n * kU + l) * kD + h * kHd;
@@ -210,7 +215,7 @@ __global__ __launch_bounds__(64) void attn_bwd_kernel(const short* __restrict__ 
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       kb[b] = frag_row(Ks, kP32, 16 * b, 0);
-      vb[b] = frag_row(Vs, kP32, 16 * b, 0);
+      vb[b] = frag_row_g(base + 256, 384, 16 * b, 0);
     }
 #pragma unroll
     for (int a = 0; a < 4; ++a)
