@@ -103,7 +103,8 @@ __device__ __forceinline__ void load_bfrags(const short* __restrict__ m, bf16x8 
 
 // LDS staging of a type job's unit features (shared by forward and backward, see the backward's notes).
 constexpr int kStage = 24;                  // units staged per chunk (1v1 max 16, 5v5 max 24 per type)
-constexpr int kUP = kStage * kF + 4;        // LDS pitch (floats) of a staged row
+constexpr int kUP = 4 * 64 + 1;            // LDS pitch (floats) of a staged row (see stage_units)
+constexpr int kDP = 64;                    // LDS pitch (floats) of a staged dtl row
 constexpr int kW1 = kD * kF + kD;           // ∂W1 (128×10) ‖ ∂b1 (128) floats per partial
 
 __device__ __forceinline__ void layer1_lds(const float* __restrict__ ur, int u, const float (&w1f)[8][3],
@@ -125,24 +126,110 @@ __device__ __forceinline__ void layer1_lds(const float* __restrict__ ur, int u, 
   }
 }
 
-// Stage units[row0 .. row0+15][uoff+c0 .. +cc][0..9] and dtl for the same (row, unit) block into LDS (one wave).
-__device__ __forceinline__ void stage_units(const float* __restrict__ units, const float* __restrict__ dtl, int U,
-                                            int N, int row0, int ubase, int cc, float* ur, float* dr, int lane) {
-  const int per = cc * kF;
-  const int tot = 16 * per;
-#pragma unroll 4
-  for (int idx = lane; idx < tot; idx += 64) {
-    const int r = idx / per, e = idx - r * per;
-    const int row = row0 + r;
-    ur[r * kUP + e] = row < N ? units[((size_t)row * U + ubase) * kF + e] : 0.f;
-  }
-  if (dtl) {
-    for (int idx = lane; idx < 16 * cc; idx += 64) {
-      const int r = idx / cc, e = idx - r * cc;
-      const int row = row0 + r;
-      dr[r * kStage + e] = row < N ? dtl[(size_t)row * U + ubase + e] : 0.f;
+// Layer 1 on ONE v_mfma_f32_16x16x32_bf16 per 16-column tile (16 cycles) instead of three exact-f32 16x16x4 MFMAs
+// (96 cycles): split x = x_hi + x_lo and W1 = W_hi + W_lo into bf16 pairs and lay the K = 32 slots out as
+//   k 0-9: x_hi·W_hi   k 10-19: x_lo·W_hi   k 20-29: x_hi·W_lo   k 30: 1·b_hi   k 31: 1·b_lo
+// which is x·W1ᵀ + b1 up to the dropped x_lo·W_lo and the bf16 rounding of the lo parts (≈2⁻¹⁶ relative; the
+// result is rounded to bf16 for layer 2 anyway). Slot → (feature, part) depends on the lane's k-group only.
+__device__ __forceinline__ int l1_feat(int slot) { return slot < 30 ? slot % 10 : -1; }
+__device__ __forceinline__ bool l1_xlo(int slot) { return slot >= 10 && slot < 20; }
+__device__ __forceinline__ bool l1_wlo(int slot) { return slot >= 20; }   // slot 31 = b_lo (30 = b_hi)
+
+__device__ __forceinline__ void load_w1_split(const float* __restrict__ w1, const float* __restrict__ b1,
+                                              bf16x8 (&wb)[8], int lane) {
+  const int j = lane & 15, kg = lane >> 4;
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    const int col = 16 * n + j;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int slot = 8 * kg + jj, f = l1_feat(slot);
+      const float w = f >= 0 ? w1[col * kF + f] : b1[col];
+      const short hi = dca::f2bf(w);
+      const short lo = dca::f2bf(w - dca::bf2f(hi));
+      wb[n][jj] = (slot == 31 || (f >= 0 && l1_wlo(slot))) ? lo : hi;
     }
   }
+}
+
+// A fragment of one unit for the 16 staged rows (row = lane & 15), slots 8·kg … 8·kg + 7.
+__device__ __forceinline__ bf16x8 l1_afrag(const float* __restrict__ ur, int u, int lane) {
+  const int i = lane & 15, kg = lane >> 4;
+  const float* x = ur + i * kUP + u * kF;
+  bf16x8 a;
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) {
+    const int slot = 8 * kg + jj, f = l1_feat(slot);
+    const float v = x[f < 0 ? 0 : f];
+    const short hi = dca::f2bf(v);
+    const short lo = dca::f2bf(v - dca::bf2f(hi));
+    a[jj] = f < 0 ? (short)0x3F80 : (l1_xlo(slot) ? lo : hi);   // 0x3F80 = bf16 1.0 (bias slots)
+  }
+  return a;
+}
+
+__device__ __forceinline__ void layer1_split(const float* __restrict__ ur, int u, const bf16x8 (&wb)[8],
+                                             f32x4 (&acc)[8], int lane) {
+  const bf16x8 a = l1_afrag(ur, u, lane);
+#pragma unroll
+  for (int n = 0; n < 8; ++n)
+    acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wb[n], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+}
+
+// 16×128 bf16 tile image in LDS, TRANSPOSED ([column][row], 32-B image rows): a C-layout fragment (rows 4kg … 4kg+3
+// of one column) is one ds_write_b64, and tile_frag reads it back as A fragments / row-major 16-B chunks with
+// ds_read_b64_tr_b16. Image row R sits at R·16 + (R/8)·64 shorts (a 128-B skew between 8-row groups) with its four
+// 8-B chunks XOR-swizzled by 2·((R/8)&1): both the writes (16 rows × 2 chunks per half-wave) and the transposed reads
+// (rows 8g + q and 8g + q + 4, 4 chunks) then hit 32 distinct bank pairs per half-wave.
+constexpr int kImg = 128 * 16 + 16 * 64;   // shorts per tile image
+__device__ __forceinline__ int img_off(int R, int c) { return R * 16 + (R >> 3) * 64 + 4 * (c ^ (2 * ((R >> 3) & 1))); }
+typedef short lds_bf16x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void tile_put(short* img, int n, const f32x4& v, int lane) {
+  const int i = lane & 15, kg = lane >> 4;
+  bf16x4 h;
+  h[0] = dca::f2bf(v[0]); h[1] = dca::f2bf(v[1]); h[2] = dca::f2bf(v[2]); h[3] = dca::f2bf(v[3]);
+  *reinterpret_cast<bf16x4*>(img + img_off(16 * n + i, kg)) = h;
+}
+// element jj of lane l = image[k0 + 8(l>>4) + jj][l & 15] (= tile row l&15, columns k0 + 8(l>>4) … +7); k0 % 16 == 0
+__device__ __forceinline__ bf16x8 tile_frag(const short* img, int k0, int lane) {
+  typedef __attribute__((address_space(3))) lds_bf16x4 lds_v4;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const short* a = img + img_off(k0 + 8 * g + q, p);
+  const lds_bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)a);
+  const lds_bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a + 4 * 16));   // row + 4: same group
+  bf16x8 f;
+  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+  return f;
+}
+
+// Stage units[row0 .. row0+15][uoff+c0 .. +cc][0..9] and dtl for the same (row, unit) block into LDS (one wave) with
+// LDS-DMA (global_load_lds_dword: no VGPRs, every load of the job in flight at once, one drain). Each instruction moves
+// 64 consecutive floats of one row, so rows sit kUP = 4·64 + 1 floats apart (the +1 skews the banks of the 16 rows a
+// fragment read touches). Rows past N load row N-1: their results are never stored and their gradients are zero.
+// (Register-staged conditional loads made the compiler wait out each load before the next: ≈40 serialised round
+// trips per 16-unit job, then most of the encoder's time.)
+__device__ __forceinline__ void stage_units(const float* __restrict__ units, const float* __restrict__ dtl, int U,
+                                            int N, int row0, int ubase, int cc, float* ur, float* dr, int lane) {
+  typedef __attribute__((address_space(1))) void gvoid;
+  typedef __attribute__((address_space(3))) void lvoid;
+  const int per = cc * kF;                       // floats per row (contiguous in global memory)
+  const int nk = (per + 63) >> 6;
+#pragma unroll 4
+  for (int r = 0; r < 16; ++r) {
+    const float* src = units + ((size_t)min(row0 + r, N - 1) * U + ubase) * kF;
+    for (int k = 0; k < nk; ++k)
+      __builtin_amdgcn_global_load_lds((gvoid*)(src + min(64 * k + lane, per - 1)), (lvoid*)(ur + r * kUP + 64 * k),
+                                       4, 0, 0);
+  }
+  if (dtl) {
+#pragma unroll 4
+    for (int r = 0; r < 16; ++r)
+      __builtin_amdgcn_global_load_lds((gvoid*)(dtl + (size_t)min(row0 + r, N - 1) * U + ubase + min(lane, cc - 1)),
+                                       (lvoid*)(dr + r * kDP), 4, 0, 0);
+  }
+  // drain here, once: later unit iterations then carry no vmcnt waits (which would also wait out their own stores)
+  __builtin_amdgcn_s_waitcnt(0);
 }
 
 // ============================================================================================================
@@ -150,7 +237,7 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_kernel(FwdParams P) {
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int rbase = blockIdx.x * kRows;
   const int U = P.L.U, N = P.N;
-  __shared__ __attribute__((aligned(16))) short scr[4][16][kLd];
+  __shared__ __attribute__((aligned(16))) short scr[4][kImg];
   __shared__ __attribute__((aligned(16))) float ust[4][16 * kUP];
 
   // ---- env embedding: relu(We·env + be) → x896[:, 0:128] (32 rows × 128 cols over 256 threads)
@@ -166,11 +253,9 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_kernel(FwdParams P) {
     }
   }
 
-  float w1f[8][3];
-  load_w1(P.w1, w1f, lane);
-  float b1v[8];
-#pragma unroll
-  for (int n = 0; n < 8; ++n) b1v[n] = P.b1[16 * n + (lane & 15)];
+  bf16x8 wb[8];
+  load_w1_split(P.w1, P.b1, wb, lane);
+  short* img = &scr[wv][0];
 
   const int i = lane & 15, kg = lane >> 4;
   for (int j = 0; j < 3; ++j) {
@@ -193,27 +278,29 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_kernel(FwdParams P) {
       for (int r = 0; r < 4; ++r) parg[n][r] = 0;
     }
     float* ur = &ust[wv][0];
-    for (int u = 0; u < cnt; ++u) {
-      const int uc = u % kStage;
-      if (uc == 0) {   // stage the next ≤ kStage units of this job (all loads in flight at once)
-        __builtin_amdgcn_wave_barrier();
-        stage_units(P.units, nullptr, U, N, row0, uoff + u, min(kStage, cnt - u), ur, nullptr, lane);
-        __builtin_amdgcn_wave_barrier();
-      }
+    for (int c0 = 0; c0 < cnt; c0 += kStage) {
+     const int cc = min(kStage, cnt - c0);
+     // stage the next ≤ kStage units of this job (all loads in flight at once; also drains the W_τ loads)
+     __builtin_amdgcn_wave_barrier();
+     stage_units(P.units, nullptr, U, N, row0, uoff + c0, cc, ur, nullptr, lane);
+     __builtin_amdgcn_wave_barrier();
+     for (int uc = 0; uc < cc; ++uc) {
+      const int u = c0 + uc;
+      // layer 1 (bias folded into the MFMA) → ReLU → bf16 transposed tile image → layer-2 A fragments
       f32x4 acc[8];
-      layer1_lds(ur, uc, w1f, acc, lane);
-      // basic = relu(acc + b1) → bf16 → scratch [row][col]
+      layer1_split(ur, uc, wb, acc, lane);
 #pragma unroll
-      for (int n = 0; n < 8; ++n)
+      for (int n = 0; n < 8; ++n) {
+        f32x4 b;
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          scr[wv][kg * 4 + r][16 * n + i] = dca::f2bf(fmaxf(acc[n][r] + b1v[n], 0.f));
+        for (int r = 0; r < 4; ++r) b[r] = fmaxf(acc[n][r], 0.f);
+        tile_put(img, n, b, lane);
+      }
       __builtin_amdgcn_wave_barrier();
       bf16x8 af[4];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) af[s] = *reinterpret_cast<const bf16x8*>(&scr[wv][i][32 * s + 8 * kg]);
-      __builtin_amdgcn_wave_barrier();
-      // layer 2
+      for (int s = 0; s < 4; ++s) af[s] = tile_frag(img, 32 * s, lane);
+      // layer 2 (LDS ops of a wave execute in order: the writes below cannot overtake the reads above)
 #pragma unroll
       for (int n = 0; n < 8; ++n) {
         f32x4 c = {0.f, 0.f, 0.f, 0.f};
@@ -223,22 +310,22 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_kernel(FwdParams P) {
         for (int r = 0; r < 4; ++r) {
           const float v = c[r] + btv[n];
           if (v > pmax[n][r]) { pmax[n][r] = v; parg[n][r] = u; }
-          scr[wv][kg * 4 + r][16 * n + i] = dca::f2bf(v);
+          c[r] = v;
         }
+        tile_put(img, n, c, lane);
       }
       __builtin_amdgcn_wave_barrier();
-      // coalesced store of the 16×128 bf16 embedding tile: lane → (row lane>>2, 64-B chunk lane&3)
+      // embedding tile → row-major: lane → row i, columns 32s + 8kg … +7 (16-B stores, 64 B contiguous per row)
       {
-        const int rr = lane >> 2, ch = lane & 3;
-        const int row = row0 + rr;
-        if (row < N) {
-          const bf16x8* src = reinterpret_cast<const bf16x8*>(&scr[wv][rr][32 * ch]);
-          bf16x8* dst = reinterpret_cast<bf16x8*>(P.emb + ((size_t)row * U + uoff + u) * kD + 32 * ch);
+        const int row = row0 + i;
 #pragma unroll
-          for (int q = 0; q < 4; ++q) dst[q] = src[q];
+        for (int s = 0; s < 4; ++s) {
+          const bf16x8 f = tile_frag(img, 32 * s, lane);
+          if (row < N) *reinterpret_cast<bf16x8*>(P.emb + ((size_t)row * U + uoff + u) * kD + 32 * s + 8 * kg) = f;
         }
       }
       __builtin_amdgcn_wave_barrier();
+     }
     }
     // ---- flush pool + argmax for this (type, group); compat: eth pool is overwritten by enh (host side)
 #pragma unroll
@@ -284,7 +371,7 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
   const int i = lane & 15, kg = lane >> 4;
   __shared__ __attribute__((aligned(16))) short tsc[4][kTile];
   __shared__ __attribute__((aligned(16))) float ust[4][16 * kUP];
-  __shared__ float dst_[4][16 * kStage];
+  __shared__ float dst_[4][16 * kDP];
   __shared__ float wred[kW1];
   short* tw = &tsc[wv][0];
 
@@ -359,7 +446,7 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) bas[n][r] = fmaxf(acc[n][r] + b1v[n], 0.f);
         // ---- ∂emb in A layout: dtl·q + ∂pool where this unit is the argmax (or given)
-        const float dtl = given ? 0.f : dr[i * kStage + uc];
+        const float dtl = given ? 0.f : dr[i * kDP + uc];
         bf16x8 de[4];
         if (given) {
 #pragma unroll

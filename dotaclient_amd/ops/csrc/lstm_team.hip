@@ -627,6 +627,7 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
     float* __restrict__ gates4, float* __restrict__ hn, float* __restrict__ cn, unsigned long long* xg_all,
     TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st, unsigned long long* trace,
     int knobs, const float* __restrict__ bias4) {
+  __builtin_amdgcn_s_setprio(3);   // issue priority over co-resident waves of kernels overlapped on other streams
   lstm_team_fwd_body<MT, KS>(xp4, whh, h0, c0, hs, hsf, cs, gates4, hn, cn, xg_all, ctl, err, Btot, Bc, nch, S, sb,
                              st, trace, knobs, bias4);
   team_exit(ctl);
@@ -639,6 +640,7 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
     const short* __restrict__ whh, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
     i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
     unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart) {
+  __builtin_amdgcn_s_setprio(3);
   lstm_team_bwd_body<MT, KS>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, dh0, dc0, xg_all, ctl, err, Btot, Bc, nch,
                              S, sb, st, trace, dg16, dbpart);
   team_exit(ctl);

@@ -1,0 +1,7 @@
+#!/bin/bash
+# rocprofv3 counter passes over the standalone entity-encoder probe (scripts/enc_probe.py); results under gpurun_out/
+set -e
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT -d gpurun_out/encpmc1 -o run -- python scripts/enc_probe.py 2 > gpurun_out/encpmc.log 2>&1
+timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR GRBM_GUI_ACTIVE -d gpurun_out/encpmc2 -o run -- python scripts/enc_probe.py 2 >> gpurun_out/encpmc.log 2>&1

@@ -1,25 +1,19 @@
 #!/usr/bin/env python3
-"""Summarise a rocprofv3 PMC database (rocpd sqlite): mean counter value per kernel (name filter optional).
-usage: pmc_summary.py <run_results.db> [substring ...]"""
+"""Per-kernel mean counter values from rocprofv3 --pmc sqlite output:  pmc_summary.py <db> [kernel-substring ...]"""
 import sqlite3
 import sys
 from collections import defaultdict
 
-
-def main(path, subs):
-    db = sqlite3.connect(path)
-    acc = defaultdict(lambda: defaultdict(list))
-    for name, cn, v in db.execute('select kernel_name, counter_name, value from counters_collection'):
-        short = name.replace('(anonymous namespace)::', '').split('(')[0].replace('void ', '')[:60]
-        if subs and not any(s in name for s in subs):
-            continue
-        acc[short][cn].append(v)
-    for k, d in acc.items():
-        print(k)
-        for cn in sorted(d):
-            vals = d[cn]
-            print(f'    {cn:28s} {sum(vals) / len(vals):16.1f}   (n={len(vals)})')
-
-
-if __name__ == '__main__':
-    main(sys.argv[1], sys.argv[2:])
+db = sys.argv[1]
+keys = sys.argv[2:]
+c = sqlite3.connect(db)
+acc = defaultdict(lambda: defaultdict(list))
+for name, ctr, val, disp in c.execute('select kernel_name, counter_name, value, dispatch_id from counters_collection'):
+    short = name.replace('(anonymous namespace)::', '').replace('void ', '').split('(')[0][:60]
+    if keys and not any(k in short for k in keys):
+        continue
+    acc[short][ctr].append(val)
+for k, d in acc.items():
+    print(k)
+    for ctr, v in sorted(d.items()):
+        print(f'   {ctr:28s} {sum(v) / len(v):16.0f}  (n={len(v)})')
