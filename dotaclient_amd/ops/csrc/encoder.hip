@@ -8,11 +8,14 @@
 // Wave jobs (balanced for both 1v1 (1,5,16,16,1,1) and 5v5 (5,5,24,24,3,3) layouts):
 //   waves 0,1: types {anh, eh, ath} for groups 0,1     waves 2,3: types {enh, ah, eth} for groups 0,1
 // Per tile:
-//   layer 1 : 16×10 units · W1ᵀ on v_mfma_f32_16x16x4_f32 (exact fp32, K padded to 12), +b1, ReLU
-//   → bf16 C-tile transposed through a per-wave LDS scratch into A-fragments
+//   layer 1 : 16×10 units · W1ᵀ + b1 on ONE v_mfma_f32_16x16x32_bf16 per column tile (bf16 hi/lo split of x, W1
+//             and b1, ≈2⁻¹⁶ relative; layer1_split), ReLU
+//   → bf16 C-tile written transposed into a per-wave LDS image (ds_write_b64), read back as A fragments with
+//     ds_read_b64_tr_b16
 //   layer 2 : 16×128 · W_τᵀ on v_mfma_f32_16x16x32_bf16 with W_τ held in 128 VGPRs for the whole type job
-//   → +b_τ, running max/argmax per (row, column), bf16 embedding tile staged through LDS for 16-B coalesced stores.
-// Backward recomputes layer 1, builds ∂emb = dtl⊗q + scatter(∂pool at argmax) in A-fragment layout, computes
+//   → +b_τ, running max/argmax per (row, column), bf16 embedding tile through the same image for 16-B row stores.
+// Unit features reach LDS by LDS-DMA (stage_units), so a type job has one memory round trip before its tiles.
+// Backward recomputes layer 1 (same split form), builds ∂emb = dtl⊗q + scatter(∂pool at argmax) in A-fragment layout, computes
 // ∂basic = ∂emb·W_τ (MFMA, W_τᵀ in VGPRs), applies ReLU', accumulates ∂W1 in-register on
 // v_mfma_f32_16x16x16_bf16 (the C-layout ∂basic tile IS the A operand), and writes ∂emb and basic activations
 // (bf16, type-major) so ∂W_τ = ∂emb_τᵀ·basic_τ runs as one large-K hipBLASLt GEMM per type.
@@ -80,17 +83,6 @@ __device__ __forceinline__ void type_job(int wv, int j, int& tau, int& g) {
   tau = (j < 3) ? lists[wv >> 1][j] : -1;
 }
 
-__device__ __forceinline__ void load_w1(const float* __restrict__ w1, float (&w1f)[8][3], int lane) {
-  const int kq = lane >> 4, j = lane & 15;
-#pragma unroll
-  for (int n = 0; n < 8; ++n)
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const int k = 4 * s + kq;
-      w1f[n][s] = (k < kF) ? w1[(16 * n + j) * kF + k] : 0.f;
-    }
-}
-
 // B fragments of a 128×128 bf16 matrix M stored row-major [col][k] (i.e. B[k][col] = M[col][k]).
 __device__ __forceinline__ void load_bfrags(const short* __restrict__ m, bf16x8 (&bf)[8][4], int lane) {
   const int j = lane & 15, kg = lane >> 4;
@@ -106,25 +98,6 @@ constexpr int kStage = 24;                  // units staged per chunk (1v1 max 1
 constexpr int kUP = 4 * 64 + 1;            // LDS pitch (floats) of a staged row (see stage_units)
 constexpr int kDP = 64;                    // LDS pitch (floats) of a staged dtl row
 constexpr int kW1 = kD * kF + kD;           // ∂W1 (128×10) ‖ ∂b1 (128) floats per partial
-
-__device__ __forceinline__ void layer1_lds(const float* __restrict__ ur, int u, const float (&w1f)[8][3],
-                                          f32x4 (&acc)[8], int lane) {
-  // ur: staged rows [16][kUP]; row i = lane&15, k = 4s + lane>>4
-  const int i = lane & 15, kq = lane >> 4;
-  float a[3];
-#pragma unroll
-  for (int s = 0; s < 3; ++s) {
-    const int k = 4 * s + kq;
-    a[s] = k < kF ? ur[i * kUP + u * kF + k] : 0.f;
-  }
-#pragma unroll
-  for (int n = 0; n < 8; ++n) {
-    f32x4 c = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int s = 0; s < 3; ++s) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a[s], w1f[n][s], c, 0, 0, 0);
-    acc[n] = c;
-  }
-}
 
 // Layer 1 on ONE v_mfma_f32_16x16x32_bf16 per 16-column tile (16 cycles) instead of three exact-f32 16x16x4 MFMAs
 // (96 cycles): split x = x_hi + x_lo and W1 = W_hi + W_lo into bf16 pairs and lay the K = 32 slots out as
@@ -375,11 +348,8 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
   __shared__ float wred[kW1];
   short* tw = &tsc[wv][0];
 
-  float w1f[8][3];
-  load_w1(P.w1, w1f, lane);
-  float b1v[8];
-#pragma unroll
-  for (int n = 0; n < 8; ++n) b1v[n] = P.b1[16 * n + i];
+  bf16x8 wb[8];                                   // layer 1 exactly as the forward computed it (layer1_split)
+  load_w1_split(P.w1, P.b1, wb, lane);
   f32x4 dw1acc[8];
   float db1acc[8];
 #pragma unroll
@@ -439,12 +409,12 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
         const int u = c0 + uc;
         // ---- recompute layer 1 (C layout) → basic f32
         f32x4 acc[8];
-        layer1_lds(ur, uc, w1f, acc, lane);
+        layer1_split(ur, uc, wb, acc, lane);
         f32x4 bas[8];
 #pragma unroll
         for (int n = 0; n < 8; ++n)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) bas[n][r] = fmaxf(acc[n][r] + b1v[n], 0.f);
+          for (int r = 0; r < 4; ++r) bas[n][r] = fmaxf(acc[n][r], 0.f);
         // ---- ∂emb in A layout: dtl·q + ∂pool where this unit is the argmax (or given)
         const float dtl = given ? 0.f : dr[i * kDP + uc];
         bf16x8 de[4];
@@ -625,11 +595,19 @@ __global__ __launch_bounds__(256, 2) void dwt_blocked_kernel(const short* __rest
     for (int y = 0; y < 4; ++y) *reinterpret_cast<f32x4*>(dst + ((4 * x + y) * 64 + lane) * 4) = acc[x][y];
 }
 
+// 64 elements × 4 job phases per block (a phase sums every 4th job, the phases combine in a fixed order through LDS):
+// 4× the parallelism of one thread per element over up to 175 jobs, still deterministic.
 __global__ __launch_bounds__(256) void dwt_reduce(const float* __restrict__ part, DwtJobs J, float* __restrict__ dwt) {
-  const int tau = blockIdx.y;
-  const int xi = blockIdx.x * 256 + threadIdx.x;        // tile-linear element
+  __shared__ float red[4][64];
+  const int tau = blockIdx.y, ph = threadIdx.x >> 6;
+  const int xi = blockIdx.x * 64 + (threadIdx.x & 63);  // tile-linear element
   float s = 0.f;
-  for (int j = J.jbase[tau]; j < J.jbase[tau + 1]; ++j) s += part[(size_t)j * (kD * kD) + xi];
+#pragma unroll 4
+  for (int j = J.jbase[tau] + ph; j < J.jbase[tau + 1]; j += 4) s += part[(size_t)j * (kD * kD) + xi];
+  red[ph][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (ph) return;
+  s = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
   const int r = xi & 3, lane = (xi >> 2) & 63, tile = (xi >> 8) & 15, wv = xi >> 12;
   const int m = 64 * (wv >> 1) + 16 * (tile >> 2) + 4 * (lane >> 4) + r;
   const int n = 64 * (wv & 1) + 16 * (tile & 3) + (lane & 15);
@@ -708,6 +686,6 @@ extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const
   encoder_bwd_kernel<<<nblk, 256, 0, st>>>(P);
   encoder_w1_reduce<<<(kW1 + 63) / 64, 256, 0, st>>>(w1part, nblk, dw1, db1);
   if (J.jbase[6] > 0) dwt_blocked_kernel<<<J.jbase[6], 256, 0, st>>>(demb, basic, J, parts);
-  dwt_reduce<<<dim3(kD * kD / 256, 6), 256, 0, st>>>(parts, J, dwt);
+  dwt_reduce<<<dim3(kD * kD / 64, 6), 256, 0, st>>>(parts, J, dwt);
   return hipGetLastError();
 }
