@@ -35,6 +35,10 @@
 // slower: storing a step's outputs after the NEXT step's gather barrier instead of right after the publish (2.08 vs
 // 1.96 µs forward, 2.33 vs 2.28 backward — stores queued ahead of the publish delay it), although skipping the
 // output stores altogether (knob) saves 0.14 µs per forward step; the x·W_ih load's placement does not matter.
+// Two ways of getting those stores out of the pollers' vmcnt queue that measured no better: (1) a "ring" forward that
+// publishes every step into its own slot (the slots then ARE the h output; gates recomputed by one GEMM, c kept):
+// 1.99 vs 1.98 µs — a fresh slot misses the XCD L2 where the reused parity buffers hit; (2) polling waves 0,1
+// staging their outputs in LDS for the non-polling waves 2,3 to store: 2.05-2.12 vs 1.94 µs.
 #include "common.h"
 #include <cstdlib>
 
