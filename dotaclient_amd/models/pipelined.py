@@ -213,12 +213,13 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
         main.wait_event(done)
         r0, r1 = t0 * B, t1 * B
         xh = hs16[t0:t1].view(-1, H)
-        zc = _mm(xh, wcat16.t()) + bcat
-        dz, dtl_c, part, lp = C.heads_loss(zc, emb[r0:r1], act_t[r0:r1], msk_t[r0:r1], adv_t[r0:r1],
-                                           ret_t[r0:r1], lpo_t[r0:r1], nret_t[r0:r1], norms, algo, False,
-                                           S, B, float(lc.clip_eps), float(lc.entropy_coef), float(lc.vf_coef))
+        zc = torch.addmm(bcat, xh, wcat16.t(), out_dtype=torch.float32)     # bias in the GEMM epilogue
+        # ∂L/∂z straight in bf16: only the backward GEMMs read it
+        dz16, dtl_c, part, lp = C.heads_loss(zc, emb[r0:r1], act_t[r0:r1], msk_t[r0:r1], adv_t[r0:r1],
+                                             ret_t[r0:r1], lpo_t[r0:r1], nret_t[r0:r1], norms, algo, False,
+                                             S, B, float(lc.clip_eps), float(lc.entropy_coef), float(lc.vf_coef),
+                                             dz_bf16=True)
         parts.append(part)
-        dz16 = dz.to(torch.bfloat16)
         first = dWcat is None
         if first:
             dbcat = torch.empty(LDZ, device=dev)

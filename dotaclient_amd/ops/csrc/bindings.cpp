@@ -226,12 +226,12 @@ std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Fused heads + loss. Returns (dz (N,ldz) f32, dtl (N,U) f32, partials (nblk,16) f32, logp (N) f32).
+// Fused heads + loss. Returns (dz (N,ldz) f32 — bf16 with dz_bf16 —, dtl (N,U) f32, partials (nblk,16) f32, logp (N) f32).
 std::vector<torch::Tensor> heads_loss(torch::Tensor z, torch::Tensor emb, torch::Tensor act, torch::Tensor msk,
                                       torch::Tensor adv, torch::Tensor ret, torch::Tensor logp_old,
                                       torch::Tensor nret, torch::Tensor norms, int64_t algo, bool compat_value_bug,
                                       int64_t S_bug, int64_t B_bug, double clip_eps, double ent_coef,
-                                      double vf_coef) {
+                                      double vf_coef, bool dz_bf16) {
   CHECK_F32(z); CHECK_BF16(emb); CHECK_U8(act); CHECK_U8(msk); CHECK_F32(adv); CHECK_F32(ret);
   CHECK_F32(logp_old); CHECK_F32(nret); CHECK_F32(norms);
   TORCH_CHECK(z.dim() == 2 && emb.dim() == 3 && emb.size(2) == 128, "z (N,ldz), emb (N,U,128)");
@@ -241,16 +241,17 @@ std::vector<torch::Tensor> heads_loss(torch::Tensor z, torch::Tensor emb, torch:
   TORCH_CHECK(adv.numel() == N && ret.numel() == N && logp_old.numel() == N && nret.numel() == N, "per-row inputs");
   TORCH_CHECK(norms.numel() >= 8, "norms must hold 8 floats");
   TORCH_CHECK(ldz % 4 == 0 && ldz >= 150 && U <= 64, "ldz must be a multiple of 4 and >= 150; U <= 64");
-  auto dz = torch::empty_like(z);
+  auto dz = dz_bf16 ? torch::empty_like(z, z.options().dtype(at::kBFloat16)) : torch::empty_like(z);
   auto dtl = torch::empty({N, U}, z.options());
   const int nb = dca_heads_loss_nblocks(N);
   auto part = torch::empty({nb, 16}, z.options());
   auto logp = torch::empty({N}, z.options());
   hip_check(dca_heads_loss(ptr<float>(z), ldz, ptr<short>(emb), ptr<unsigned char>(act), ptr<unsigned char>(msk),
                            21 + U, ptr<float>(adv), ptr<float>(ret), ptr<float>(logp_old), ptr<float>(nret),
-                           ptr<float>(norms), ptr<float>(dz), ptr<float>(dtl), ptr<float>(part), ptr<float>(logp), N,
-                           U, (int)algo, compat_value_bug ? 1 : 0, (int)S_bug, (int)B_bug, (float)clip_eps,
-                           (float)ent_coef, (float)vf_coef, cur_stream()),
+                           ptr<float>(norms), dz_bf16 ? nullptr : ptr<float>(dz), ptr<float>(dtl), ptr<float>(part),
+                           ptr<float>(logp), N, U, (int)algo, compat_value_bug ? 1 : 0, (int)S_bug, (int)B_bug,
+                           (float)clip_eps, (float)ent_coef, (float)vf_coef, cur_stream(),
+                           dz_bf16 ? ptr<short>(dz) : nullptr),
             "dca_heads_loss");
   return {dz, dtl, part, logp};
 }
@@ -682,7 +683,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("lstm_fwd", &lstm_fwd, "persistent LSTM forward recurrence (granule all-gather)", py::arg("xp"),
         py::arg("whh"), py::arg("h0"), py::arg("c0"), py::arg("err"), py::arg("want_f32_h"),
         py::arg("trace") = py::none());
-  m.def("heads_loss", &heads_loss, "fused heads + pointer + masked log-softmax + PPO/VPG loss + gradients");
+  m.def("heads_loss", &heads_loss, "fused heads + pointer + masked log-softmax + PPO/VPG loss + gradients",
+        py::arg("z"), py::arg("emb"), py::arg("act"), py::arg("msk"), py::arg("adv"), py::arg("ret"),
+        py::arg("logp_old"), py::arg("nret"), py::arg("norms"), py::arg("algo"), py::arg("compat_value_bug"),
+        py::arg("S_bug"), py::arg("B_bug"), py::arg("clip_eps"), py::arg("ent_coef"), py::arg("vf_coef"),
+        py::arg("dz_bf16") = false);
   m.def("encoder_fwd", &encoder_fwd, "fused entity encoder forward (unit MLP, per-type GEMM, max-pool+argmax)");
   m.def("encoder_bwd", &encoder_bwd, "fused entity encoder backward: dW_type (K-blocked split-K MFMA GEMM), dW1, db1",
         py::arg("units"), py::arg("w1"), py::arg("b1"), py::arg("wtT"), py::arg("dtl"), py::arg("q"), py::arg("dx"),

@@ -30,9 +30,15 @@ struct Params {
   const float* adv; const float* ret; const float* logp_old; const float* nret;
   const float* norms;
   float* dz; float* dtl; float* part; float* logp_out;
+  short* dz16;   // if set: ∂L/∂z written in bf16 here instead of f32 to dz (what the backward GEMMs consume)
   int N, U, algo, compat_value_bug, S_bug, B_bug;
   float clip_eps, ent_coef, vf_coef;
 };
+
+__device__ __forceinline__ void put_dz(const Params& P, size_t i, float v) {
+  if (P.dz16) P.dz16[i] = dca::f2bf(v);
+  else P.dz[i] = v;
+}
 
 // masked log-softmax of one head held one entry per lane (lane < W); returns logp for the lane's entry.
 __device__ __forceinline__ void head_lsm(float logit, bool m, int lane, int W, float& logp, float& p) {
@@ -166,12 +172,12 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
           s_dtl[wv][lane] = dl;
           P.dtl[(size_t)n * U + lane] = dl;
         } else {
-          P.dz[(size_t)n * P.ldz + kQ + hoff[h] + lane] = dl;
+          put_dz(P, (size_t)n * P.ldz + kQ + hoff[h] + lane, dl);
         }
       }
     }
-    if (lane == 0) P.dz[(size_t)n * P.ldz + kQ + 21] = dV;
-    if (lane < P.ldz - kQ - 22) P.dz[(size_t)n * P.ldz + kQ + 22 + lane] = 0.f;
+    if (lane == 0) put_dz(P, (size_t)n * P.ldz + kQ + 21, dV);
+    if (lane < P.ldz - kQ - 22) put_dz(P, (size_t)n * P.ldz + kQ + 22 + lane, 0.f);
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     // ---- dq = Σ_u dtl[u] · emb[u]
@@ -191,9 +197,16 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
       dq[j] += __shfl_xor(dq[j], 32, 64);
     }
     if (ug == 0) {
-      float4* o = reinterpret_cast<float4*>(P.dz + (size_t)n * P.ldz + 8 * ks);
-      o[0] = make_float4(dq[0], dq[1], dq[2], dq[3]);
-      o[1] = make_float4(dq[4], dq[5], dq[6], dq[7]);
+      if (P.dz16) {
+        dca::bf16x8 h;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) h[j] = dca::f2bf(dq[j]);
+        *reinterpret_cast<dca::bf16x8*>(P.dz16 + (size_t)n * P.ldz + 8 * ks) = h;
+      } else {
+        float4* o = reinterpret_cast<float4*>(P.dz + (size_t)n * P.ldz + 8 * ks);
+        o[0] = make_float4(dq[0], dq[1], dq[2], dq[3]);
+        o[1] = make_float4(dq[4], dq[5], dq[6], dq[7]);
+      }
     }
   }
   // ---- block partials
@@ -219,9 +232,9 @@ extern "C" hipError_t dca_heads_loss(const float* z, int ldz, const short* emb, 
                                      const float* logp_old, const float* nret, const float* norms, float* dz,
                                      float* dtl, float* part, float* logp_out, int N, int U, int algo,
                                      int compat_value_bug, int S_bug, int B_bug, float clip_eps, float ent_coef,
-                                     float vf_coef, hipStream_t st) {
+                                     float vf_coef, hipStream_t st, short* dz16) {
   if (U > 64 || U < 1 || ldz < kQ + 22 || A != 21 + U) return hipErrorInvalidValue;
-  Params P{z, ldz, emb, act, msk, A, adv, ret, logp_old, nret, norms, dz, dtl, part, logp_out, N, U, algo,
+  Params P{z, ldz, emb, act, msk, A, adv, ret, logp_old, nret, norms, dz, dtl, part, logp_out, dz16, N, U, algo,
            compat_value_bug, S_bug, B_bug, clip_eps, ent_coef, vf_coef};
   heads_loss_kernel<<<dca_heads_loss_nblocks(N), 256, 0, st>>>(P);
   return hipGetLastError();

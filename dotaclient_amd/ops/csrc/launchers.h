@@ -27,7 +27,7 @@ hipError_t dca_heads_loss(const float* z, int ldz, const short* emb, const unsig
                           int A, const float* adv, const float* ret, const float* logp_old, const float* nret,
                           const float* norms, float* dz, float* dtl, float* part, float* logp_out, int N, int U,
                           int algo, int compat_value_bug, int S_bug, int B_bug, float clip_eps, float ent_coef,
-                          float vf_coef, hipStream_t st);
+                          float vf_coef, hipStream_t st, short* dz16 = nullptr);
 
 hipError_t dca_encoder_fwd(const float* units, const float* env, const float* w1, const float* b1, const short* wt,
                            const float* bt, const float* we, const float* be, short* x896, short* emb,
