@@ -164,9 +164,32 @@ class Learner:
                 out[k] = replay.data[k].index_select(0, idx)
         return out
 
-    def _direct_body(self, batch_tm, B, S):
+    def _split_mode(self) -> bool:
+        """Data-parallel direct step in two phases: the recurrence / pre-RNN / heads gradients are all-reduced on
+        the comm stream while the encoder backward still runs (RCCL over xGMI overlapped with backward). The split
+        needs the single-chunk step and a contiguous early-parameter range (DataParallel.split_buckets).
+        ``DCA_DP_SPLIT=1`` forces it without a process group (single-GPU tests of the two-graph mechanics)."""
+        import os
+        if getattr(self, '_split', None) is None:
+            force = os.environ.get('DCA_DP_SPLIT') == '1'
+            ok = (self.direct() and (self.dp.enabled or force) and self.model.chunks == 1
+                  and os.environ.get('DCA_DP_SPLIT', '') != '0')
+            if ok:
+                early = self.model.early_param_names()
+                idx = [i for i, n in enumerate(self.model.param_names) if n in early]
+                ok = self.dp.split_buckets(idx) if self.dp.enabled else bool(idx)
+            self._split = bool(ok)
+        return self._split
+
+    def _direct_body(self, batch_tm, B, S, hook=None):
         self.flat.grad.zero_()
-        vec = self.model.train_direct(batch_tm, B, S, self.cfg)
+        if hook is None and self._split_mode():
+            hook = self.dp.launch_early                   # eager step: launch the early buckets right away
+        self.model.split_hook = hook
+        try:
+            vec = self.model.train_direct(batch_tm, B, S, self.cfg)
+        finally:
+            self.model.split_hook = None
         self.dp.has_grad.copy_(self.model.grad_mask)
         return vec
 
@@ -178,6 +201,46 @@ class Learner:
 
     def _graph_ready(self) -> bool:
         return bool(self._graph_warmup) and self.n_steps >= self._graph_warmup
+
+    def _replay_split(self, key, body):
+        """Split-mode capture/replay: ``body(hook)`` is captured as TWO graphs — the hook, called once by the step
+        at its split point, ends the first capture and begins the second (same memory pool). Replay: graph 1, then
+        the early buckets' all-reduce on the comm stream, then graph 2 overlapping it."""
+        graphs = self.__dict__.setdefault('_graphs', {})
+        if key not in graphs:
+            if getattr(self, '_graph_stream', None) is None:
+                self._graph_stream = torch.cuda.Stream(device=self.device)
+            s = self._graph_stream
+            cur = torch.cuda.current_stream(self.device)
+            s.wait_stream(cur)
+            with torch.cuda.stream(s):              # eager warm-up on the capture stream, no collectives
+                body(lambda: None)
+            cur.wait_stream(s)
+            import torch.distributed as dist
+            mode = 'thread_local' if (dist.is_available() and dist.is_initialized()) else 'global'
+            g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            switched = []
+
+            def switch():
+                g1.capture_end()
+                g2.capture_begin(pool=g1.pool(), capture_error_mode=mode)
+                switched.append(True)
+
+            torch.cuda.synchronize(self.device)
+            with torch.cuda.stream(s):
+                g1.capture_begin(capture_error_mode=mode)
+                out = body(switch)
+                if not switched:
+                    raise RuntimeError('direct step never reached its DP split point')
+                g2.capture_end()
+            cur.wait_stream(s)
+            graphs[key] = ((g1, g2), out)
+            self.graph = g1
+        (g1, g2), out = graphs[key]
+        g1.replay()
+        self.dp.launch_early()
+        g2.replay()
+        return out
 
     def _replay_graph(self, key, body):
         """Capture ``body`` (a function of the static inputs) once per key, then replay it."""
@@ -218,6 +281,12 @@ class Learner:
             for k, v in batch.items():
                 self._static_in[k].copy_(v, non_blocking=True)
 
+        if self._split_mode():
+            def body_split(hook):
+                bt, B_, S_ = self.batch_to_time_major(self._static_in)
+                return self._direct_body(bt, B_, S_, hook=hook)
+            return self._replay_split(key, body_split)
+
         def body():
             bt, B_, S_ = self.batch_to_time_major(self._static_in)
             return self._direct_body(bt, B_, S_)
@@ -237,8 +306,12 @@ class Learner:
                 self._static_idx = idx.clone()
             else:
                 self._static_idx.copy_(idx)
-            vec = self._replay_graph(key, lambda: self._direct_body(
-                self.gather_time_major(replay, self._static_idx, S), B, S))
+            if self._split_mode():
+                vec = self._replay_split(key, lambda hook: self._direct_body(
+                    self.gather_time_major(replay, self._static_idx, S), B, S, hook=hook))
+            else:
+                vec = self._replay_graph(key, lambda: self._direct_body(
+                    self.gather_time_major(replay, self._static_idx, S), B, S))
         else:
             vec = self._direct_body(self.gather_time_major(replay, idx, S), B, S)
         return self._finish(vec)

@@ -239,7 +239,7 @@ class FusedPolicy:
         self.attention_fused = (self.cfg.entity_attention and self.cfg.unit_dim == 128 and self.cfg.env_dim == 128
                                 and self.cfg.attention_heads == 4 and self.cfg.layout.max_units == 64)
 
-    def apply_direct_grads(self, grads, g, written=()):
+    def apply_direct_grads(self, grads, g, written=(), set_mask: bool = True):
         """Accumulate precomputed gradients straight into the parameters' ``.grad`` (views of the learner's flat
         buffer) with two multi-tensor kernels, instead of returning 30 tensors to autograd (which launches one
         accumulation copy per parameter, ≈1 ms of host-bound launches per step). ``g`` = upstream gradient
@@ -256,7 +256,7 @@ class FusedPolicy:
         # one launch with the tensor table in the kernel arguments — torch's foreach kernels stage their tensor
         # lists through a host buffer, which a replayed hipGraph would read stale
         self.C.multi_axpy(views, gl, None if g is None else g.reshape(1).float().contiguous())
-        if getattr(self, '_mask_list', None) != mask:
+        if set_mask and getattr(self, '_mask_list', None) != mask:
             self._mask_list = mask
             self.grad_mask = torch.tensor(mask, dtype=torch.float32, device=self.err.device)
         self.direct_used = True
@@ -312,6 +312,18 @@ class FusedPolicy:
         lc = self.loss_cfg
         return ((self.fully_fused or self.attention_fused) and self.cfg.rnn == 'lstm' and lstm_impl() == 'team'
                 and not (lc is not None and lc.compat_value_bug) and os.environ.get('DCA_PIPELINE', '1') != '0')
+
+    # Data-parallel split of the direct step (learner/engine.py): the learner sets ``split_hook`` to a callable
+    # that the step calls once, at the point where every gradient of :meth:`early_param_names` is final.
+    split_hook = None
+    early_applied = frozenset()
+
+    def early_param_names(self) -> frozenset:
+        """Parameters whose gradients are final before the encoder backward (pre-RNN, recurrence, heads): a
+        contiguous suffix of the registration order, so their flat-buffer range is one all-reduce bucket."""
+        pre = ('affine_pre_rnn.', 'rnn.', 'affine_head_enum.', 'affine_move_', 'affine_unit_attention.',
+               'affine_value.')
+        return frozenset(n for n in self.param_names if n.startswith(pre))
 
     @property
     def chunks(self) -> int:

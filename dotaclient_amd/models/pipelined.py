@@ -237,6 +237,10 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
     # ---- backward recurrence on stream L (reverse chunks), weight gradients per chunk on the main stream
     grads: Dict[str, torch.Tensor] = {}
     fp.split_head_grads(dWcat, dbcat, grads)
+    # data-parallel split (direct mode, single chunk): see the split point in the backward loop below
+    split = fp.split_hook if (gout is not None and one) else None
+    early_names = fp.early_param_names() if split is not None else frozenset()
+    fp.early_applied = frozenset()
     dgates16 = torch.empty(S, B, H, 4, dtype=torch.bfloat16, device=dev)   # ∂gates straight from the kernel
     db = dw1 = db1 = dWt = dbt = dWe = dbe = None
     dgam = dbet = None
@@ -282,6 +286,17 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
         dpre16 = torch.ops.aten.threshold_backward(torch.mm(dG16, wih16), x16[r0:r1], 0)
         gemm_tn(dpre16, x896[r0:r1], out=dWpre, accumulate=True, colsum=dbpre)
         dx896 = _mm(dpre16, wpre16)
+        if split is not None:
+            # DP split point: every gradient of the recurrence, pre-RNN and heads is final here (the big ones are
+            # already in the flat buffer); apply the small ones and let the learner all-reduce those buckets while
+            # the encoder backward below runs (see Learner._replay_split)
+            grads['rnn.bias_ih_l0'] = db[fp.gate_inv(H, dev)]
+            grads['rnn.bias_hh_l0'] = grads['rnn.bias_ih_l0']
+            early = [grads.pop(nm, None) if nm in early_names else None for nm in fp.param_names]
+            fp.apply_direct_grads(early, None, set_mask=False)    # the final call records the full mask
+            fp.early_applied = early_names
+            split()
+            split = None
         demb_in = None
         if attn:
             # attention block backward over this chunk's rows (unit rows r0·U … r1·U)
@@ -314,8 +329,9 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
         grads['rnn.weight_ih_l0'] = dWih
         grads['affine_pre_rnn.weight'] = dWpre
         grads['affine_pre_rnn.bias'] = dbpre
-    grads['rnn.bias_ih_l0'] = db[inv]
-    grads['rnn.bias_hh_l0'] = grads['rnn.bias_ih_l0']
+    if 'rnn.bias_ih_l0' not in fp.early_applied:
+        grads['rnn.bias_ih_l0'] = db[inv]
+        grads['rnn.bias_hh_l0'] = grads['rnn.bias_ih_l0']
     grads['affine_unit_basic_stats.weight'] = dw1
     grads['affine_unit_basic_stats.bias'] = db1
     for t, s in enumerate(TYPE_SUFFIX):
@@ -382,7 +398,8 @@ def train_direct(fp, batch_tm: Dict[str, torch.Tensor], B: int, S: int) -> torch
     part, _, grads = fused_step_tm(fp, W, P, batch_tm['units'], batch_tm['env'], batch_tm['actions'],
                                    batch_tm['masks'], batch_tm['adv'], batch_tm['ret'], batch_tm['logp_old'],
                                    batch_tm['norm_ret'], norms, h0, c0, B, S, gout=gout)
-    fp.apply_direct_grads([grads.get(nm) for nm in fp.param_names], None, written=set(DIRECT_GEMM_GRADS))
+    fp.apply_direct_grads([grads.get(nm) for nm in fp.param_names], None,
+                          written=set(DIRECT_GEMM_GRADS) | set(fp.early_applied))
     out = torch.empty(16, device=dev)
     C.loss_assemble(part, norms, N, 0 if lc.algo == 'ppo' else 1, float(lc.entropy_coef), float(lc.vf_coef), out)
     return out

@@ -141,6 +141,44 @@ class DataParallel:
             hi = max(self.flat.offsets[i] + self.flat.numel[i] for i in idxs)
             self.bucket_ranges.append((lo, hi))
 
+    def split_buckets(self, early: Sequence[int], cap_mb: float = 8.0) -> bool:
+        """Bucket layout for a step whose gradients finish in two phases (the learner's direct step): the EARLY
+        parameters (a contiguous index range) get their own buckets, launched by :meth:`launch_early` while the
+        second phase still runs; the rest form the last bucket, which carries the has-grad counts. Returns False
+        (layout unchanged) if ``early`` is not a contiguous proper sub-range."""
+        early = sorted(set(early))
+        if not early or len(early) >= self.n_params or early != list(range(early[0], early[-1] + 1)):
+            return False
+        late = [i for i in range(self.n_params) if i not in set(early)]
+        lo = [self.flat.offsets[i] for i in late]
+        hi = [self.flat.offsets[i] + self.flat.numel[i] for i in late]
+        if max(hi) - min(lo) != sum(self.flat.numel[i] for i in late):
+            return False                                     # late params not contiguous in the flat buffer
+        cap = max(1, int(cap_mb * 1024 * 1024 / self.flat.grad.element_size()))
+        buckets, cur, size = [], [], 0
+        for i in early[::-1]:
+            if cur and size + self.flat.numel[i] > cap:
+                buckets.append(cur)
+                cur, size = [], 0
+            cur.append(i)
+            size += self.flat.numel[i]
+        buckets.append(cur)
+        buckets.append(late[::-1])
+        self.buckets = buckets
+        self.param_bucket = {i: b for b, idxs in enumerate(buckets) for i in idxs}
+        self.bucket_ranges = [(min(self.flat.offsets[i] for i in idxs),
+                               max(self.flat.offsets[i] + self.flat.numel[i] for i in idxs)) for idxs in buckets]
+        return True
+
+    def launch_early(self):
+        """All-reduce every bucket but the last (the early-phase gradients) now, asynchronously on the comm
+        stream, overlapping whatever the current stream runs next; :meth:`sync` finishes the step."""
+        if not self.enabled:
+            return
+        for b in range(self._next, len(self.buckets) - 1):
+            self._launch(b)
+        self._next = len(self.buckets) - 1
+
     def _make_hook(self, i: int):
         def hook(p):
             self.has_grad[i:i + 1].fill_(1.0)          # kernel fill (capturable), no host→device scalar copy

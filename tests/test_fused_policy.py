@@ -157,11 +157,38 @@ def test_fused_step_is_bitwise_deterministic(gpu_ops, preset):
     assert torch.equal(ms[0]['loss'], ms[1]['loss']) and torch.equal(ms[0]['grad_norm'], ms[1]['grad_norm'])
 
 
+@pytest.mark.parametrize('preset', ['lstm512', '5v5'])
+def test_dp_split_step_matches_single_graph(gpu_ops, monkeypatch, preset):
+    """The data-parallel split step (two captured graphs around the point where the recurrence / pre-RNN / heads
+    gradients are final, early buckets all-reduced in between) computes exactly what the single-graph step does."""
+    from dotaclient_amd.learner.replay import HbmReplay
+    cfg = get_config(preset)
+    torch.manual_seed(0)
+    pol = Policy(cfg)
+    ref = copy.deepcopy(pol)
+    flats, losses = [], []
+    for p, split in ((pol, '1'), (ref, '0')):
+        monkeypatch.setenv('DCA_DP_SPLIT', split)
+        L = Learner(p, LossConfig(algo='ppo'), device='cuda', backend='fused', dp=False)
+        assert L.enable_graph(warmup=1)
+        rep = HbmReplay(6, 48, cfg.layout, cfg.hidden, 'cuda', seed=11)
+        rep.add(make_batch(6, 48, cfg.layout, cfg.hidden, device='cuda', seed=4))
+        for _ in range(3):
+            m = L.train_step_replay(rep, 4)
+        torch.cuda.synchronize()
+        assert L._split == (split == '1')
+        flats.append(L.flat.flat.clone())
+        losses.append(m['loss'].clone())
+    assert torch.equal(flats[0], flats[1])
+    assert torch.equal(losses[0], losses[1])
+
+
 def _pg_worker(port, q):
     import os
     import torch.distributed as dist
     try:
-        os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK='0', WORLD_SIZE='1')
+        # DCA_DP_SPLIT=1: the two-graph split capture (thread_local mode under the live process group) too
+        os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK='0', WORLD_SIZE='1', DCA_DP_SPLIT='1')
         torch.cuda.set_device(0)
         dist.init_process_group('nccl', rank=0, world_size=1, device_id=torch.device('cuda:0'))
         t = torch.ones(4, device='cuda')
@@ -176,7 +203,7 @@ def _pg_worker(port, q):
             m = L.train_step_replay(rep, 2)
             dist.all_reduce(t)
         torch.cuda.synchronize()
-        q.put(('ok', float(m['loss']), L.graph is not None))
+        q.put(('ok', float(m['loss']), L.graph is not None and L._split))
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover
         q.put(('err', repr(e), False))
