@@ -149,11 +149,9 @@ class DataParallel:
         early = sorted(set(early))
         if not early or len(early) >= self.n_params or early != list(range(early[0], early[-1] + 1)):
             return False
+        if early[0] != 0 and early[-1] != self.n_params - 1:
+            return False                     # early must be a prefix or suffix: both bucket ranges then contiguous
         late = [i for i in range(self.n_params) if i not in set(early)]
-        lo = [self.flat.offsets[i] for i in late]
-        hi = [self.flat.offsets[i] + self.flat.numel[i] for i in late]
-        if max(hi) - min(lo) != sum(self.flat.numel[i] for i in late):
-            return False                                     # late params not contiguous in the flat buffer
         cap = max(1, int(cap_mb * 1024 * 1024 / self.flat.grad.element_size()))
         buckets, cur, size = [], [], 0
         for i in early[::-1]:

@@ -30,19 +30,24 @@ class Toy(torch.nn.Module):
         self.c = torch.nn.Linear(4, 4)   # never used: must stay untouched
 
 
-def _toy_worker(rank, world, port, q):
+def _toy_worker(rank, world, port, q, split=False):
     try:
         _init(rank, world, port)
         from dotaclient_amd.parallel.dp import DataParallel
         torch.manual_seed(100 + rank)          # different init per rank → broadcast must equalise
         m = Toy()
         dp = DataParallel(m, bucket_cap_mb=0.0001, overlap=False)
+        if split:     # the learner's two-phase layout: b, c early (own buckets), a last with the counts
+            assert dp.split_buckets([2, 3, 4, 5], cap_mb=0.0001)
+            assert dp.buckets[-1] == [1, 0]
         x = torch.full((2, 4), float(rank + 1))
         out = m.a(x).sum()
         if rank == 0:
             out = out + m.b(x).sum()           # only rank 0 produces a gradient for b
         dp.zero_grad()
         out.backward()
+        if split:
+            dp.launch_early()
         dp.sync()
         # numpy, not torch tensors: torch.multiprocessing shares tensors by fd through the child's resource sharer,
         # which is gone once the child exits — the parent may unpickle later (flaky FileNotFoundError)
@@ -54,11 +59,12 @@ def _toy_worker(rank, world, port, q):
         q.put((rank, repr(e), None, None))
 
 
-def test_sparse_param_semantics_two_ranks():
+@pytest.mark.parametrize('split', [False, True])
+def test_sparse_param_semantics_two_ranks(split):
     world, port = 2, _free_port()
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
-    ps = [ctx.Process(target=_toy_worker, args=(r, world, port, q)) for r in range(world)]
+    ps = [ctx.Process(target=_toy_worker, args=(r, world, port, q, split)) for r in range(world)]
     for p in ps:
         p.start()
     res = {}
@@ -188,3 +194,24 @@ def test_resume_equalises_iteration_and_optimizer_state(tmp_path):
     torch.testing.assert_close(res[0][1], L.opt.exp_avg)
     assert (res[1][2] == 41).all()
     torch.testing.assert_close(res[1][3], res[0][3])
+
+
+@pytest.mark.parametrize('preset', ['lstm512', '5v5'])
+def test_split_buckets_on_policy_layout(preset):
+    """The learner's DP split (recurrence / pre-RNN / heads early, encoder last with the counts) is a valid bucket
+    layout on the real policy's flat buffer (64-element aligned offsets): two disjoint contiguous ranges."""
+    from dotaclient_amd.models.policy import Policy, get_config
+    from dotaclient_amd.parallel.dp import DataParallel
+    pol = Policy(get_config(preset))
+    dp = DataParallel(pol, overlap=False, broadcast=False)
+    names = [n for n, _ in pol.named_parameters()]
+    pre = ('affine_pre_rnn.', 'rnn.', 'affine_head_enum.', 'affine_move_', 'affine_unit_attention.', 'affine_value.')
+    early = [i for i, n in enumerate(names) if n.startswith(pre)]
+    assert dp.split_buckets(early)
+    late = sorted(dp.buckets[-1])
+    assert set(late) == set(range(len(names))) - set(early)
+    assert all(n.startswith(('affine_env', 'affine_unit_basic', 'entity_attn')) or
+               (n.startswith('affine_unit_') and 'attention' not in n) for n in (names[i] for i in late))
+    (llo, lhi) = dp.bucket_ranges[-1]
+    for lo, hi in dp.bucket_ranges[:-1]:
+        assert hi <= llo or lo >= lhi
