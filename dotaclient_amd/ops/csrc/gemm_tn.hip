@@ -15,6 +15,9 @@
 //   (deterministic) and writes C, optionally through a row permutation (unit-major → PyTorch gate-major rows) and
 //   optionally accumulating into C (the flat grad). (Summing in the last-arriving workgroup of each tile was 5-10×
 //   slower: one workgroup's serial, latency-bound pass over all slabs of its tile.)
+// * Staging the slabs by LDS-DMA (global_load_lds_dwordx4 with the swizzle applied on the source side, the bias
+//   column sum as an extra MFMA against ones) measured SLOWER here: 57 / 33 / 23 / 18 µs vs 47 / 29 / 21 / 15 µs for
+//   the four 1v1 weight gradients (the register-staged loads overlap the MFMAs better at this K-slab depth).
 // * B may be "row-split": rows k < split come from B0 (e.g. h0), rows ≥ split from B shifted by `split` rows —
 //   the LSTM's h_{t-1} operand without materialising the concatenation.
 #include "common.h"
