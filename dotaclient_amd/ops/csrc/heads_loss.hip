@@ -60,6 +60,9 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
   __shared__ float s_tl[kRowsPerBlock][64];
   __shared__ float s_dtl[kRowsPerBlock][64];
   __shared__ float s_part[kRowsPerBlock][kNPart];
+  __shared__ float s_zl[kRowsPerBlock][32];
+  __shared__ unsigned char s_act[kRowsPerBlock][128];
+  __shared__ unsigned char s_msk[kRowsPerBlock][128];
   float acc[kNPart];
 #pragma unroll
   for (int i = 0; i < kNPart; ++i) acc[i] = 0.f;
@@ -67,7 +70,8 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
   if (n < P.N) {
     const int U = P.U;
     const float* zr = P.z + (size_t)n * P.ldz;
-    // ---- q slice for this lane (8 consecutive features) and pointer logits, 4 units per wave-instruction
+    // ---- every global load of the row first, addresses clamped in range (a conditional load per element made the
+    //      compiler wait out each one before issuing the next: ≈20 serialised round trips per row)
     const int ks = lane & 15, ug = lane >> 4;
     float q8[8];
     {
@@ -75,20 +79,33 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
       const float4 b = *reinterpret_cast<const float4*>(zr + 8 * ks + 4);
       q8[0] = a.x; q8[1] = a.y; q8[2] = a.z; q8[3] = a.w; q8[4] = b.x; q8[5] = b.y; q8[6] = b.z; q8[7] = b.w;
     }
+    const float zl = zr[kQ + min(lane, 21)];                 // enum | x | y logits and the value
+    const float A_n = P.adv[n], R_n = P.ret[n], lpo_n = P.logp_old[n], nret_n = P.nret[n];
+    float nm[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) nm[i] = P.norms[i];
+    const unsigned char* ar = P.act + (size_t)n * P.A;
+    const unsigned char* mr = P.msk + (size_t)n * P.A;
+    const unsigned char a0 = ar[min(lane, P.A - 1)], a1 = ar[min(lane + 64, P.A - 1)];
+    const unsigned char m0 = mr[min(lane, P.A - 1)], m1 = mr[min(lane + 64, P.A - 1)];
     constexpr int kMaxIt = 16;   // U ≤ 64
     dca::bf16x8 e8[kMaxIt];
     const int nit = (U + 3) >> 2;
     const short* er = P.emb + (size_t)n * U * kQ;
 #pragma unroll
+    for (int it = 0; it < kMaxIt; ++it)
+      if (it < nit) e8[it] = *reinterpret_cast<const dca::bf16x8*>(er + (size_t)min(it * 4 + ug, U - 1) * kQ + 8 * ks);
+    if (lane < 32) s_zl[wv][lane] = zl;
+    s_act[wv][lane] = a0; s_act[wv][lane + 64] = a1;
+    s_msk[wv][lane] = m0; s_msk[wv][lane + 64] = m1;
+    // ---- pointer logits q·emb_u, 4 units per wave-instruction (16 lanes × 8 features each)
+#pragma unroll
     for (int it = 0; it < kMaxIt; ++it) {
       if (it < nit) {
         const int u = it * 4 + ug;
-        dca::bf16x8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (u < U) v = *reinterpret_cast<const dca::bf16x8*>(er + (size_t)u * kQ + 8 * ks);
-        e8[it] = v;
         float d = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d += q8[j] * dca::bf2f(v[j]);
+        for (int j = 0; j < 8; ++j) d += q8[j] * dca::bf2f(e8[it][j]);
         d = dca::group_sum<16>(d);
         if (ks == 0 && u < U) s_tl[wv][u] = d;
       }
@@ -96,8 +113,6 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     // ---- the four heads: (offset in flat action vector, width, source)
-    const unsigned char* ar = P.act + (size_t)n * P.A;
-    const unsigned char* mr = P.msk + (size_t)n * P.A;
     const int hoff[4] = {0, 3, 12, 21};
     const int hw[4] = {3, 9, 9, U};
     float logp[4], pr[4], a[4];
@@ -108,9 +123,9 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
     for (int h = 0; h < 4; ++h) {
       const bool in = lane < hw[h];
       float lg = 0.f;
-      if (in) lg = (h == 3) ? s_tl[wv][lane] : zr[kQ + hoff[h] + lane];
-      mk[h] = in && mr[hoff[h] + lane];
-      a[h] = (in && ar[hoff[h] + lane]) ? 1.f : 0.f;
+      if (in) lg = (h == 3) ? s_tl[wv][lane] : s_zl[wv][hoff[h] + lane];
+      mk[h] = in && s_msk[wv][hoff[h] + lane];
+      a[h] = (in && s_act[wv][hoff[h] + lane]) ? 1.f : 0.f;
       head_lsm(lg, mk[h], lane, hw[h], logp[h], pr[h]);
       if (!in) logp[h] = 0.f;
       const float sh = dca::wave_sum(a[h] * logp[h]);
@@ -121,28 +136,28 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
       acc[2 + h] += -dca::wave_sum(mk[h] ? pr[h] * logp[h] : 0.f);
     }
     const float valid = nsel > 0 ? 1.f : 0.f;
-    const float V = zr[kQ + 21];
-    const float R = P.ret[n];
+    const float V = s_zl[wv][21];
+    const float R = R_n;
     float g_sel = 0.f, dV = 0.f;
     if (P.algo == 0) {   // PPO
-      const float A = P.adv[n];
-      const float lr = sel - P.logp_old[n];
+      const float A = A_n;
+      const float lr = sel - lpo_n;
       const float r = __expf(lr);
       const float s1 = r * A;
       const float rc = fminf(fmaxf(r, 1.f - P.clip_eps), 1.f + P.clip_eps);
       const float s2 = rc * A;
       acc[0] += valid * fminf(s1, s2);
       const bool clipped = (A > 0.f && r > 1.f + P.clip_eps) || (A < 0.f && r < 1.f - P.clip_eps);
-      g_sel = clipped ? 0.f : -valid * A * r * P.norms[0];
+      g_sel = clipped ? 0.f : -valid * A * r * nm[0];
       acc[1] += valid * (V - R) * (V - R);
-      dV = P.vf_coef * 2.f * (V - R) * valid * P.norms[0];
+      dV = P.vf_coef * 2.f * (V - R) * valid * nm[0];
       acc[6] += valid * (-lr);
       acc[7] += valid * (fabsf(r - 1.f) > P.clip_eps ? 1.f : 0.f);
       acc[8] += valid * A;
     } else {             // VPG (reference objective)
-      const float nr = P.nret[n];
+      const float nr = nret_n;
       acc[0] += -sel * nr;
-      g_sel = -nr * P.norms[1];
+      g_sel = -nr * nm[1];
       acc[1] += (V - R) * (V - R);
       acc[9] += V;
       acc[10] += V * V;
@@ -150,7 +165,7 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
       if (P.vf_coef > 0.f) {
         if (P.compat_value_bug) {
           const float S = (float)P.S_bug, Bq = (float)P.B_bug;
-          dV = P.vf_coef * 2.f * (S * V - P.norms[6]) / (Bq * S * S);
+          dV = P.vf_coef * 2.f * (S * V - nm[6]) / (Bq * S * S);
         } else {
           dV = P.vf_coef * 2.f * (V - R) / ((float)P.S_bug * (float)P.B_bug);   // mean over ALL B·S rows (chunk-safe)
         }
@@ -163,7 +178,7 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
     for (int h = 0; h < 4; ++h) {
       const bool in = lane < hw[h];
       float dlp = g_sel * a[h];
-      if (P.ent_coef > 0.f) dlp += P.ent_coef * P.norms[2 + h] * (mk[h] ? pr[h] * (1.f + logp[h]) : 0.f);
+      if (P.ent_coef > 0.f) dlp += P.ent_coef * nm[2 + h] * (mk[h] ? pr[h] * (1.f + logp[h]) : 0.f);
       if (!in) dlp = 0.f;
       const float sd = dca::wave_sum(dlp);
       const float dl = dlp - (mk[h] ? pr[h] : 0.f) * sd;

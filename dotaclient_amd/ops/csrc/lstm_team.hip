@@ -38,7 +38,10 @@
 // Two ways of getting those stores out of the pollers' vmcnt queue that measured no better: (1) a "ring" forward that
 // publishes every step into its own slot (the slots then ARE the h output; gates recomputed by one GEMM, c kept):
 // 1.99 vs 1.98 µs — a fresh slot misses the XCD L2 where the reused parity buffers hit; (2) polling waves 0,1
-// staging their outputs in LDS for the non-polling waves 2,3 to store: 2.05-2.12 vs 1.94 µs.
+// staging their outputs in LDS for the non-polling waves 2,3 to store: 2.05-2.12 vs 1.94 µs. (Working hypothesis for
+// a later round: the cost is the acknowledgement latency of partial writes to lines not resident in the XCD L2 —
+// the ring's fresh slots and the output rows alike — so warming those lines ahead of the writes, from a queue no
+// poll or barrier waits on, is the lever still untried.)
 #include "common.h"
 #include <cstdlib>
 
