@@ -133,3 +133,39 @@ def test_encoder_bwd_with_given_demb(gpu_ops):
     torch.cat(embs, 1).backward(demb.float())
     for got, ref, name in ((dwt, WT.grad, 'dwt'), (dw1, W1.grad, 'dw1'), (db1, B1.grad, 'db1')):
         assert (got - ref).norm() / ref.norm() < 3e-2, name
+
+
+@pytest.mark.parametrize('layout', ['1v1', '5v5'])
+def test_encoder_fwd_matches_fp32(gpu_ops, layout):
+    """encoder_fwd (LDS-DMA staging, split-bf16 layer 1, per-type MFMA GEMMs, running max/argmax) vs a plain fp32
+    PyTorch reference of the same ops (policy.py:97-138): unit embeddings, pools, env embedding, argmax."""
+    g = _g(5)
+    counts = [1, 5, 16, 16, 1, 1] if layout == '1v1' else [5, 5, 24, 24, 3, 3]
+    Uc = sum(counts)
+    off = [0]
+    for c in counts:
+        off.append(off[-1] + c)
+    Nr = 75                                          # not a multiple of the 16-row groups on purpose
+    units = torch.randn(Nr, Uc, 10, device='cuda', generator=g)
+    env = torch.randn(Nr, 3, device='cuda', generator=g)
+    w1 = torch.randn(D, 10, device='cuda', generator=g) * 0.3
+    b1 = torch.randn(D, device='cuda', generator=g) * 0.1
+    wt = torch.randn(6, D, D, device='cuda', generator=g) * 0.1
+    bt = torch.randn(6, D, device='cuda', generator=g) * 0.1
+    we = torch.randn(D, 3, device='cuda', generator=g)
+    be = torch.randn(D, device='cuda', generator=g)
+    x896, emb, arg = gpu_ops.encoder_fwd(units, env, w1, b1, _bf(wt), bt, we, be, counts, False)
+    basic = torch.relu(units @ w1.t() + b1)                                   # fp32 reference
+    ref = torch.cat([basic[:, off[t]:off[t + 1]] @ _bf(wt[t]).float().t() + bt[t] for t in range(6)], 1)
+    err = (emb.float() - ref).norm() / ref.norm()
+    assert err < 1e-2, float(err)                    # bf16 storage + bf16 layer-2 operand
+    torch.testing.assert_close(x896[:, :D].float(), torch.relu(env @ we.t() + be), rtol=1e-2, atol=1e-2)
+    for t in range(6):
+        seg = ref[:, off[t]:off[t + 1]]
+        mx, am = seg.max(1)
+        torch.testing.assert_close(x896[:, D + t * D:D + (t + 1) * D].float(), mx, rtol=1e-2, atol=2e-2)
+        # argmax must agree wherever the reference maximum is separated from the runner-up by more than rounding
+        if seg.shape[1] > 1:
+            top2 = seg.topk(2, dim=1).values
+            clear = (top2[:, 0] - top2[:, 1]) > 2e-2
+            assert torch.equal(arg[:, t].long()[clear], am[clear])
