@@ -42,7 +42,8 @@
 // a later round: the cost is the acknowledgement latency of partial writes to lines not resident in the XCD L2 —
 // the ring's fresh slots and the output rows alike — so warming those lines ahead of the writes, from a queue no
 // poll or barrier waits on, is the lever still untried; non-temporal output stores measured no different, 1.891 vs
-// 1.895 µs.)
+// 1.895 µs.) Backward: its gate-gradient store costs 0.05-0.07 µs per step (2.27-2.30 vs 2.23 µs without it), but
+// taking wave 0 (whose lanes store) off the poll, with waves 1-3 gathering 3 chunks per thread, was slower: 2.34-2.36.
 #include "common.h"
 #include <cstdlib>
 
