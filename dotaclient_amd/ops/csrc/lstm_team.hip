@@ -44,6 +44,9 @@
 // poll or barrier waits on, is the lever still untried; non-temporal output stores measured no different, 1.891 vs
 // 1.895 µs.) Backward: its gate-gradient store costs 0.05-0.07 µs per step (2.27-2.30 vs 2.23 µs without it), but
 // taking wave 0 (whose lanes store) off the poll, with waves 1-3 gathering 3 chunks per thread, was slower: 2.34-2.36.
+// Forward store COUNT matters more than bytes: one packed 16-B record {bf16 gates, f32 c, bf16 h} per (row, unit)
+// instead of the three stores ran 1.84 vs 1.895 µs — left out (bf16 saved gates for the backward, and an h unpack
+// pass would eat half the gain).
 #include "common.h"
 #include <cstdlib>
 
