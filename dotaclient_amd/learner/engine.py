@@ -316,10 +316,16 @@ class Learner:
             vec = self._direct_body(self.gather_time_major(replay, idx, S), B, S)
         return self._finish(vec)
 
+    def _sync_and_step(self):
+        """DP reduction + optimizer step. With the fused Adam on a multi-rank job the has-grad average is taken
+        inside the optimizer kernels (no separate pass over the gradient buffer after the all-reduce)."""
+        fold = self.dp.enabled and self.opt.use_kernels
+        self.dp.sync(scale=not fold)
+        return self.opt.step(self.dp.counts, divide=fold)
+
     def _finish(self, vec):
         metrics = self._metrics_from_vec(vec.clone())
-        self.dp.sync()
-        metrics['grad_norm'] = self.opt.step(self.dp.counts)
+        metrics['grad_norm'] = self._sync_and_step()
         self.n_steps += 1
         return metrics
 
@@ -328,8 +334,7 @@ class Learner:
         if self.direct():
             return self._finish(self._step_direct_batch(batch))
         metrics = self._fwd_bwd(batch)
-        self.dp.sync()
-        metrics['grad_norm'] = self.opt.step(self.dp.counts)
+        metrics['grad_norm'] = self._sync_and_step()
         self.n_steps += 1
         return metrics
 

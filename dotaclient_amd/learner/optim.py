@@ -40,25 +40,31 @@ class FlatAdam:
             self._ops = ops.require()
 
     # ------------------------------------------------------------------------------------------------
-    def step(self, counts: Optional[torch.Tensor] = None):
+    def step(self, counts: Optional[torch.Tensor] = None, divide: bool = False):
+        """``divide``: ``flat.grad`` holds the DP all-reduce SUMS (DataParallel.sync(scale=False)); the has-grad
+        average grad / counts[param] is taken inside the optimizer instead of by a separate pass."""
         if counts is None:
             counts = torch.ones(len(self.flat.params), device=self.flat.flat.device)
         if self.use_kernels:
-            return self._step_kernels(counts)
-        return self.step_reference(counts)
+            return self._step_kernels(counts, divide)
+        return self.step_reference(counts, divide)
 
-    def _step_kernels(self, counts):
+    def _step_kernels(self, counts, divide=False):
         b1, b2 = self.betas
         max_norm = self.max_grad_norm if self.max_grad_norm is not None else -1.0
         self._ops.adam_step(self.flat.flat, self.flat.grad, self.exp_avg, self.exp_avg_sq, self.flat.segment_ids,
                             counts, self.steps, self.last_grad_norm, float(self.lr), float(b1), float(b2),
-                            float(self.eps), float(max_norm))
+                            float(self.eps), float(max_norm), divide=bool(divide))
         return self.last_grad_norm
 
     @torch.no_grad()
-    def step_reference(self, counts):
+    def step_reference(self, counts, divide=False):
         b1, b2 = self.betas
         g = self.flat.grad
+        if divide:
+            segc = self.flat.segment_ids.long().clamp_min(0)
+            inv = torch.where(counts > 0, 1.0 / counts.clamp_min(1.0), torch.zeros_like(counts))
+            g = g * torch.where(self.flat.segment_ids >= 0, inv[segc], torch.zeros_like(g))
         norm = torch.linalg.vector_norm(g)
         self.last_grad_norm.copy_(norm)
         if self.max_grad_norm is not None:

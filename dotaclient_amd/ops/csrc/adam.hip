@@ -15,14 +15,24 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kMaxBlocks = 1024;
 
+// divide: the gradient buffer holds DP SUMS; the has-grad average g / count[param] is taken here (count 0 → 0)
+// instead of by a separate pass over the buffer after the all-reduce.
+__device__ __forceinline__ float grad_scale(const int* seg, const float* counts, int i, int divide) {
+  if (!divide) return 1.f;
+  const int s = seg[i * 4];
+  return (s >= 0 && counts[s] > 0.f) ? 1.f / counts[s] : 0.f;
+}
+
 __global__ __launch_bounds__(kThreads) void adam_norm_kernel(const float4* __restrict__ g, int n4,
                                                              float* __restrict__ partials,
                                                              const float* __restrict__ counts,
-                                                             float* __restrict__ steps, int n_params) {
+                                                             float* __restrict__ steps, int n_params,
+                                                             const int* __restrict__ seg, int divide) {
   float acc = 0.f;
   for (int i = blockIdx.x * kThreads + threadIdx.x; i < n4; i += gridDim.x * kThreads) {
     float4 v = g[i];
-    acc += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    const float sc = grad_scale(seg, counts, i, divide);
+    acc += sc * sc * (v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w);
   }
   __shared__ float red[kThreads / dca::kWave];
   acc = dca::wave_sum(acc);
@@ -44,7 +54,7 @@ __global__ __launch_bounds__(kThreads) void adam_update_kernel(
     float4* __restrict__ param, const float4* __restrict__ grad, float4* __restrict__ m, float4* __restrict__ v,
     const int* __restrict__ seg, int n4, const float* __restrict__ partials, int nparts,
     const float* __restrict__ counts, const float* __restrict__ steps, float* __restrict__ norm_out, float lr,
-    float b1, float b2, float eps, float max_norm) {
+    float b1, float b2, float eps, float max_norm, int divide) {
   __shared__ float red[kThreads / dca::kWave];
   __shared__ float s_coef;
   float acc = 0.f;
@@ -69,13 +79,14 @@ __global__ __launch_bounds__(kThreads) void adam_update_kernel(
     if (s < 0) continue;
     if (!(counts[s] > 0.f)) continue;
     const float t = steps[s];
+    const float gcoef = divide ? coef / counts[s] : coef;
     const float bc1 = 1.f - powf(b1, t);
     const float bc2s = sqrtf(1.f - powf(b2, t));
     const float step_size = lr / bc1;
     float4 gg = grad[i], mm = m[i], vv = v[i], pp = param[i];
 #define DCA_ADAM_LANE(c)                                          \
     {                                                             \
-      const float gc = gg.c * coef;                               \
+      const float gc = gg.c * gcoef;                              \
       mm.c = b1 * mm.c + (1.f - b1) * gc;                         \
       vv.c = b2 * vv.c + (1.f - b2) * gc * gc;                    \
       pp.c -= step_size * mm.c / (sqrtf(vv.c) / bc2s + eps);      \
@@ -94,16 +105,17 @@ __global__ __launch_bounds__(kThreads) void adam_update_kernel(
 extern "C" hipError_t dca_adam_step(float* param, const float* grad, float* m, float* v, const int* seg, int64_t n,
                                     const float* counts, float* steps, int n_params, float* partials,
                                     float* norm_out, float lr, float b1, float b2, float eps, float max_norm,
-                                    hipStream_t stream) {
+                                    hipStream_t stream, int divide) {
   const int n4 = (int)(n / 4);
   int blocks = (n4 + kThreads - 1) / kThreads;
   blocks = blocks < 1 ? 1 : (blocks > kMaxBlocks ? kMaxBlocks : blocks);
   adam_norm_kernel<<<blocks, kThreads, 0, stream>>>(reinterpret_cast<const float4*>(grad), n4, partials, counts,
-                                                    steps, n_params);
+                                                    steps, n_params, seg, divide);
   DCA_CHECK_LAUNCH();
   adam_update_kernel<<<blocks, kThreads, 0, stream>>>(
       reinterpret_cast<float4*>(param), reinterpret_cast<const float4*>(grad), reinterpret_cast<float4*>(m),
-      reinterpret_cast<float4*>(v), seg, n4, partials, blocks, counts, steps, norm_out, lr, b1, b2, eps, max_norm);
+      reinterpret_cast<float4*>(v), seg, n4, partials, blocks, counts, steps, norm_out, lr, b1, b2, eps, max_norm,
+      divide);
   DCA_CHECK_LAUNCH();
   return hipSuccess;
 }

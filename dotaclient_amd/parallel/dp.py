@@ -211,9 +211,10 @@ class DataParallel:
         self._next = 0
         self._works = []
 
-    def sync(self):
+    def sync(self, scale: bool = True):
         """Finish the gradient reduction. Afterwards ``flat.grad`` holds the has-grad-averaged gradient and
-        ``counts`` the number of ranks that had a gradient for each parameter."""
+        ``counts`` the number of ranks that had a gradient for each parameter. ``scale=False`` leaves the SUMS in
+        ``flat.grad`` for an optimizer that divides by the counts itself (FlatAdam.step(divide=True))."""
         if not self.enabled:
             self.counts.copy_(self.has_grad)
             return
@@ -238,6 +239,8 @@ class DataParallel:
         self._works = []
         self._pending = {}
         self._next = 0
+        if not scale:
+            return
         # grad /= count  (count 0 → gradient stays 0 and the optimizer skips the parameter)
         inv = torch.where(self.counts > 0, 1.0 / self.counts.clamp_min(1.0), torch.zeros_like(self.counts))
         seg = self.flat.segment_ids

@@ -23,19 +23,21 @@ def _run_reference(model, grads_seq, lr, max_norm, skip=()):
         opt.step()
 
 
-def _run_flat(model, grads_seq, lr, max_norm, skip=(), device='cpu', kernels=False):
+def _run_flat(model, grads_seq, lr, max_norm, skip=(), device='cpu', kernels=False, ranks=1):
+    """ranks > 1: the gradient buffer holds the SUM over that many identical ranks (what DataParallel.sync(
+    scale=False) leaves) and the optimizer takes the has-grad average itself (step(divide=True))."""
     model = model.to(device)
     flat = FlatParams(model, device=device)
     opt = FlatAdam(flat, lr=lr, max_grad_norm=max_norm, use_kernels=kernels)
-    counts = torch.ones(len(flat.params), device=device)
+    counts = torch.full((len(flat.params),), float(ranks), device=device)
     for i in skip:
         counts[i] = 0
     for grads in grads_seq:
         flat.zero_grad()
         for i, (p, g) in enumerate(zip(flat.params, grads)):
             if i not in skip:
-                p.grad.copy_(g.to(device))
-        opt.step(counts)
+                p.grad.copy_(g.to(device) * ranks)
+        opt.step(counts, divide=ranks > 1)
     return model
 
 
@@ -61,5 +63,32 @@ def test_adam_kernel_matches_reference(gpu_ops):
     seq = [_grads(a, s) for s in range(3)]
     _run_flat(a, seq, 1e-3, 0.5, skip=(5,))
     b = _run_flat(b, seq, 1e-3, 0.5, skip=(5,), device='cuda', kernels=True)
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb.cpu(), rtol=1e-5, atol=2e-6, msg=n)
+
+
+@pytest.mark.parametrize('skip', [(), (3, 28)])
+def test_flat_adam_divide_equals_presummed_average(skip):
+    """step(divide=True) on rank SUMS == step() on the already averaged gradients (the DP fold)."""
+    torch.manual_seed(0)
+    a = Policy('compat')
+    b = Policy('compat')
+    b.load_state_dict(a.state_dict())
+    seq = [_grads(a, s) for s in range(3)]
+    _run_flat(a, seq, 1e-3, 0.5, skip)
+    _run_flat(b, seq, 1e-3, 0.5, skip, ranks=3)
+    for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
+        torch.testing.assert_close(pa, pb, rtol=1e-5, atol=1e-6, msg=n)
+
+
+@pytest.mark.gpu
+def test_adam_kernel_divide_mode(gpu_ops):
+    torch.manual_seed(0)
+    a = Policy('lstm512')
+    b = Policy('lstm512')
+    b.load_state_dict(a.state_dict())
+    seq = [_grads(a, s) for s in range(3)]
+    _run_flat(a, seq, 1e-3, 0.5, skip=(5,))
+    b = _run_flat(b, seq, 1e-3, 0.5, skip=(5,), device='cuda', kernels=True, ranks=4)
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         torch.testing.assert_close(pa, pb.cpu(), rtol=1e-5, atol=2e-6, msg=n)
