@@ -519,18 +519,23 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
   for (int e = tid; e < kW1; e += 256) P.w1part[(size_t)blockIdx.x * kW1 + e] = wred[e];
 }
 
-// Fixed-order sum of the per-workgroup ∂W1‖∂b1 partials: block of 256 = 64 columns × 4 row phases.
+// Fixed-order sum of the per-workgroup ∂W1‖∂b1 partials: block of 256 = 16 columns × 16 row phases (88 blocks;
+// 64 × 4 gave 22 blocks whose threads each walked ~90 partials: 23 µs, latency-bound).
 __global__ __launch_bounds__(256) void encoder_w1_reduce(const float* __restrict__ part, int nblk,
                                                           float* __restrict__ dw1, float* __restrict__ db1) {
-  __shared__ float red[4][64];
-  const int c = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6;
+  __shared__ float red[16][16];
+  const int c = blockIdx.x * 16 + (threadIdx.x & 15), ph = threadIdx.x >> 4;
   float s = 0.f;
-  if (c < kW1)
-    for (int b = ph; b < nblk; b += 4) s += part[(size_t)b * kW1 + c];
-  red[ph][threadIdx.x & 63] = s;
+  if (c < kW1) {
+#pragma unroll 4
+    for (int b = ph; b < nblk; b += 16) s += part[(size_t)b * kW1 + c];
+  }
+  red[ph][threadIdx.x & 15] = s;
   __syncthreads();
   if (ph == 0 && c < kW1) {
-    const float v = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v += red[k][threadIdx.x];
     if (c < kD * kF) dw1[c] = v;
     else db1[c - kD * kF] = v;
   }
@@ -684,7 +689,7 @@ extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const
   }
   if (acc != U || U > 64) return hipErrorInvalidValue;
   encoder_bwd_kernel<<<nblk, 256, 0, st>>>(P);
-  encoder_w1_reduce<<<(kW1 + 63) / 64, 256, 0, st>>>(w1part, nblk, dw1, db1);
+  encoder_w1_reduce<<<(kW1 + 15) / 16, 256, 0, st>>>(w1part, nblk, dw1, db1);
   if (J.jbase[6] > 0) dwt_blocked_kernel<<<J.jbase[6], 256, 0, st>>>(demb, basic, J, parts);
   dwt_reduce<<<dim3(kD * kD / 64, 6), 256, 0, st>>>(parts, J, dwt);
   return hipGetLastError();
