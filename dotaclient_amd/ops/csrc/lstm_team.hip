@@ -38,11 +38,9 @@
 // Two ways of getting those stores out of the pollers' vmcnt queue that measured no better: (1) a "ring" forward that
 // publishes every step into its own slot (the slots then ARE the h output; gates recomputed by one GEMM, c kept):
 // 1.99 vs 1.98 µs — a fresh slot misses the XCD L2 where the reused parity buffers hit; (2) polling waves 0,1
-// staging their outputs in LDS for the non-polling waves 2,3 to store: 2.05-2.12 vs 1.94 µs. (Working hypothesis for
-// a later round: the cost is the acknowledgement latency of partial writes to lines not resident in the XCD L2 —
-// the ring's fresh slots and the output rows alike — so warming those lines ahead of the writes, from a queue no
-// poll or barrier waits on, is the lever still untried; non-temporal output stores measured no different, 1.891 vs
-// 1.895 µs.) Backward: its gate-gradient store costs 0.05-0.07 µs per step (2.27-2.30 vs 2.23 µs without it), but
+// staging their outputs in LDS for the non-polling waves 2,3 to store: 2.05-2.12 vs 1.94 µs. Not the residency of the
+// written lines: outputs redirected into an 8-step L2-resident window ran 1.93-1.95 µs (no change), non-temporal
+// stores 1.891 vs 1.895 — the cost follows the NUMBER of store instructions ahead of the next poll. Backward: its gate-gradient store costs 0.05-0.07 µs per step (2.27-2.30 vs 2.23 µs without it), but
 // taking wave 0 (whose lanes store) off the poll, with waves 1-3 gathering 3 chunks per thread, was slower: 2.34-2.36.
 // Forward store COUNT matters more than bytes: one packed 16-B record {bf16 gates, f32 c, bf16 h} per (row, unit)
 // instead of the three stores ran 1.84 vs 1.895 µs — left out (bf16 saved gates for the backward, and an h unpack
