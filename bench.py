@@ -41,6 +41,10 @@ def parse():
     ap.add_argument('--model', default='lstm512')
     ap.add_argument('--backend', default='auto', choices=['auto', 'fused', 'torch'])
     ap.add_argument('--algo', default='ppo', choices=['ppo', 'vpg'])
+    ap.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'],
+                    help='fp32 = the reference\'s training precision (headline); bf16 = bf16 GEMM operands')
+    ap.add_argument('--bf16-extra', type=int, default=1,
+                    help='also time the bf16 learner (reported as an extra field, not the headline)')
     ap.add_argument('--replay', type=int, default=0, help='sequences in the on-HBM replay pool (0 = 4x batch)')
     ap.add_argument('--graph', type=int, default=-1, help='capture the step in a hipGraph (-1 = auto)')
     ap.add_argument('--actor', type=int, default=1, help='also measure batched actor steps/s (untimed region)')
@@ -65,64 +69,75 @@ def main():
     from dotaclient_amd.learner.synthetic import DeviceReplay
     from dotaclient_amd.models.policy import Policy, get_config
 
-    torch.manual_seed(7 + rank)
     cfg = get_config(args.model)
-    policy = Policy(cfg)
-    backend = args.backend
-    if backend == 'auto':
-        backend = 'fused' if use_cuda else 'torch'
-    learner = Learner(policy, LossConfig(algo=args.algo), device=device, backend=backend)
-    if args.graph == 1 or (args.graph == -1 and backend == 'fused'):
-        learner.enable_graph(warmup=1)
-    n_pool = args.replay or 4 * args.batch_size
-    replay = DeviceReplay(n_pool, args.seq_len, cfg.layout, cfg.hidden if cfg.rnn == 'lstm' else None, device,
-                          seed=1000 * rank)
-
     trace = os.environ.get('DCA_BENCH_TRACE') == '1'
 
-    def step():
-        t = time.perf_counter()
-        # on-device minibatch gather from the HBM replay pool (part of the captured step on the fused path)
-        out = learner.train_step_replay(replay.buf, args.batch_size)
-        if trace:
+    def run(precision):
+        """Build a learner of this precision and time ``args.steps`` DP PPO steps after ``args.warmup``; returns
+        (elapsed s (max over ranks), loss_first, loss_last, learner, policy)."""
+        torch.manual_seed(7 + rank)
+        policy = Policy(cfg)
+        backend = args.backend
+        if backend == 'auto':
+            backend = 'fused' if use_cuda else 'torch'
+        learner = Learner(policy, LossConfig(algo=args.algo), device=device, backend=backend, precision=precision)
+        if args.graph == 1 or (args.graph == -1 and learner.backend == 'fused'):
+            learner.enable_graph(warmup=1)
+        n_pool = args.replay or 4 * args.batch_size
+        replay = DeviceReplay(n_pool, args.seq_len, cfg.layout, cfg.hidden if cfg.rnn == 'lstm' else None, device,
+                              seed=1000 * rank)
+
+        def step():
+            t = time.perf_counter()
+            # on-device minibatch gather from the HBM replay pool (part of the captured step on the fused path)
+            out = learner.train_step_replay(replay.buf, args.batch_size)
+            if trace:
+                torch.cuda.synchronize()
+                print(f'[bench] {precision} step {learner.n_steps} {1e3 * (time.perf_counter() - t):.2f} ms loss '
+                      f'{float(out["loss"]):.5f} gnorm {float(out["grad_norm"]):.5f} '
+                      f'params_finite {bool(torch.isfinite(learner.flat.flat).all())} '
+                      f'grad_finite {bool(torch.isfinite(learner.flat.grad).all())} '
+                      f'err {int(learner.model.err.item()) if learner.backend == "fused" else 0}',
+                      file=sys.stderr, flush=True)
+            return out
+
+        m = None
+        for _ in range(args.warmup):
+            m = step()
+        if use_cuda:
             torch.cuda.synchronize()
-            print(f'[bench] step {learner.n_steps} {1e3 * (time.perf_counter() - t):.2f} ms loss '
-                  f'{float(out["loss"]):.5f} gnorm {float(out["grad_norm"]):.5f} '
-                  f'params_finite {bool(torch.isfinite(learner.flat.flat).all())} '
-                  f'grad_finite {bool(torch.isfinite(learner.flat.grad).all())} '
-                  f'err {int(learner.model.err.item()) if backend == "fused" else 0}',
-                  file=sys.stderr, flush=True)
-        return out
+        loss_first = float(m['loss']) if m is not None else float('nan')
+        if world > 1:
+            dist.barrier()
+        if use_cuda:
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            m = step()
+        if use_cuda:
+            torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+        loss_last = float(m['loss'])
+        if learner.backend == 'fused':
+            learner.model.check_error()       # a persistent-kernel timeout would invalidate the measurement
+        return elapsed, loss_first, loss_last, learner, policy
 
-    for _ in range(args.warmup):
-        m = step()
-    if use_cuda:
-        torch.cuda.synchronize()
-    loss_val = float(m['loss']) if args.warmup else float('nan')
-
-    if world > 1:
-        dist.barrier()
-    if use_cuda:
-        torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        m = step()
-    if use_cuda:
-        torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    final_loss = float(m['loss'])
-    if backend == 'fused':
-        learner.model.check_error()       # a persistent-kernel timeout would invalidate the measurement
-
+    elapsed, loss_val, final_loss, learner, policy = run(args.precision)
+    backend = learner.backend
     samples = args.batch_size * args.seq_len * world * args.steps
     value = samples / elapsed
     ms_per_step = elapsed / args.steps * 1e3
+    extra = None
+    if args.bf16_extra and args.precision == 'fp32' and use_cuda:
+        del learner
+        e16, _, _, _, _ = run('bf16')
+        extra = {'precision': 'bf16', 'value': samples / e16, 'ms_per_step': e16 / args.steps * 1e3}
 
     actor = None
     if args.actor and rank == 0 and use_cuda:
@@ -147,7 +162,11 @@ def main():
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': value / BASELINE_STEPS_PER_S,
-            'dtype': 'bf16',
+            'dtype': args.precision,
+            'precision_note': ('fp32 activations, gradients, accumulation and optimizer; hand-written MFMA kernels '
+                               'use bf16x3 split operands (x = hi + lo, ~2^-16 relative per product), plain GEMMs '
+                               'exact fp32 (hipBLASLt)') if args.precision == 'fp32' else
+                              'bf16 GEMM operands and saved activations, fp32 accumulation / recurrence / optimizer',
             'data': 'synthetic (on-HBM replay of synthetic 1v1-mid experience, random-init weights)',
             'config': {'model': f'{args.model} ({cfg.rnn}-{cfg.hidden}, '
                                 f'{"5v5 entity-attention" if cfg.entity_attention else "1v1-mid entity"} encoder, '
@@ -155,6 +174,7 @@ def main():
                        'global_batch': args.batch_size * world, 'seq_len': args.seq_len,
                        'parallelism': f'dp{world}', 'algo': args.algo, 'backend': backend},
             'loss_first': loss_val, 'loss_last': final_loss,
+            'bf16_learner': extra,
             'actor': actor,
         }
         print(json.dumps(out), flush=True)

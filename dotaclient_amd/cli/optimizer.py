@@ -3,6 +3,7 @@
 Reference-compatible flags: ``--log-dir --ip --port --epochs --seq-per-epoch --batch-size --seq-len --learning-rate
 --entropy-coef --vf-coef --pretrained-model --mq-prefetch-count -l/--log --run-local``. Additional: ``--broker``,
 ``--algo`` (ppo | vpg), ``--model-preset``, ``--iterations``, ``--device``, ``--backend`` (fused | torch),
+``--precision`` (fp32 | bf16),
 ``--gamma --gae-lambda --clip-eps --max-grad-norm --compat-value-bug --checkpoint-keep``.
 
 Data parallel: launch one process per GPU with ``torch.distributed.run`` (RCCL over xGMI); every rank consumes
@@ -50,6 +51,8 @@ def build_parser():
     ap.add_argument('--iterations', type=int, default=10000)
     ap.add_argument('--device', type=str, default='auto')
     ap.add_argument('--backend', type=str, default='auto', choices=['auto', 'fused', 'torch'])
+    ap.add_argument('--precision', type=str, default='fp32', choices=['fp32', 'bf16'],
+                    help='fp32 = reference training precision (bf16x3 split-MFMA kernels); bf16 = bf16 GEMM operands')
     ap.add_argument('--gamma', type=float, default=0.98)
     ap.add_argument('--gae-lambda', type=float, default=0.95)
     ap.add_argument('--clip-eps', type=float, default=0.1)
@@ -84,6 +87,7 @@ def main(argv=None):
                           iterations=args.iterations, algo=args.algo, model=args.model_preset, gamma=args.gamma,
                           gae_lambda=args.gae_lambda, clip_eps=args.clip_eps, max_grad_norm=args.max_grad_norm,
                           compat_value_bug=args.compat_value_bug, device=device, backend=args.backend,
+                          precision=args.precision,
                           checkpoint_keep=args.checkpoint_keep, replay_gb=args.replay_gb,
                           replay_capacity=args.replay_capacity, replay_recent=args.replay_recent)
     broker = make_broker(args.broker or f'tcp://{args.ip}:{args.port}')

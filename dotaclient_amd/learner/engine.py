@@ -8,7 +8,12 @@ Backends for the model math:
 
 * ``'fused'`` (default on GPU): :class:`~dotaclient_amd.models.fused.FusedPolicy` — hand-written gfx950 HIP kernels
   for the entity encoder, LSTM recurrence and heads+loss; plain GEMMs through hipBLASLt.
-* ``'torch'``: the eager reference model (``models.policy.Policy``) under bf16 autocast on GPU, fp32 on CPU.
+* ``'torch'``: the eager reference model (``models.policy.Policy``): fp32, or under bf16 autocast on GPU with
+  ``precision='bf16'``.
+
+``precision`` (default ``'fp32'``, the reference's training precision — optimizer.py:281 trains the fp32 module):
+``'fp32'`` keeps activations, gradients and accumulation in fp32 (the fused kernels run bf16x3 split MFMA, see
+``models/fused.py``); ``'bf16'`` uses bf16 GEMM operands / saved activations with fp32 accumulation and optimizer.
 
 Batches are dicts of device tensors (see :func:`dotaclient_amd.learner.synthetic.make_batch` for the schema):
 ``env (B,S,3) f32``, ``units (B,S,U,10) f32``, ``actions``/``masks (B,S,A) u8`` (flat ``enum|x|y|target_unit``),
@@ -43,12 +48,20 @@ class LossConfig:
 
 class Learner:
     def __init__(self, policy: Policy, loss_cfg: LossConfig, device='cpu', backend: str = 'auto',
-                 bucket_cap_mb: float = 8.0, overlap: bool = True, dp: bool = True):
+                 bucket_cap_mb: float = 8.0, overlap: bool = True, dp: bool = True, precision: str = 'fp32'):
+        if precision not in ('fp32', 'bf16'):
+            raise ValueError(f'precision must be fp32 or bf16, got {precision!r}')
         self.device = torch.device(device)
         self.cfg = loss_cfg
+        self.precision = precision
         self.policy = policy.to(self.device)
         if backend == 'auto':
             backend = 'fused' if self.device.type == 'cuda' else 'torch'
+        if backend == 'fused' and precision == 'fp32' and self.policy.config.entity_attention:
+            import logging
+            logging.getLogger(__name__).warning('fp32 learner: the 5v5 entity-attention policy runs on the eager fp32 '
+                                                'path (its fused kernels are bf16: precision="bf16")')
+            backend = 'torch'
         self.backend = backend
         self.flat = FlatParams(self.policy, device=self.device)
         self.dp = DataParallel(self.policy, flat=self.flat, bucket_cap_mb=bucket_cap_mb, overlap=overlap,
@@ -58,7 +71,7 @@ class Learner:
         self.model = self.policy
         if backend == 'fused':
             from ..models.fused import FusedPolicy
-            self.model = FusedPolicy(self.policy, loss_cfg)
+            self.model = FusedPolicy(self.policy, loss_cfg, precision=precision)
             self.model.attach_flat(self.flat.flat)
         self.counts = self.policy.layout.action_counts()
         self.n_steps = 0
@@ -82,7 +95,7 @@ class Learner:
 
     # ------------------------------------------------------------------------------------------------
     def _autocast(self):
-        if self.backend == 'torch' and self.device.type == 'cuda':   # 'torch-fp32' = fp32 oracle
+        if self.backend == 'torch' and self.device.type == 'cuda' and self.precision == 'bf16':
             return torch.autocast('cuda', dtype=torch.bfloat16)
         return contextlib.nullcontext()
 

@@ -69,6 +69,7 @@ class OptimizerConfig:
     normalize_advantages: bool = True
     device: str = 'auto'
     backend: str = 'auto'
+    precision: str = 'fp32'            # 'fp32' (reference precision) | 'bf16' (bf16 GEMM operands, fp32 accumulation)
     checkpoint_keep: int = 0
     histogram_freq: int = 128          # optimizer.py:214
     xp_timeout: Optional[float] = None
@@ -144,7 +145,7 @@ class DotaOptimizer:
         lc = LossConfig(algo=cfg.algo, learning_rate=cfg.learning_rate, entropy_coef=cfg.entropy_coef,
                         vf_coef=cfg.vf_coef, clip_eps=cfg.clip_eps, gamma=cfg.gamma, gae_lambda=cfg.gae_lambda,
                         max_grad_norm=cfg.max_grad_norm, compat_value_bug=cfg.compat_value_bug)
-        self.learner = Learner(self.policy, lc, device=self.device, backend=cfg.backend)
+        self.learner = Learner(self.policy, lc, device=self.device, backend=cfg.backend, precision=cfg.precision)
         if trainer_state is not None:
             self.learner.load_state_dict(trainer_state['learner'])
             self.running.load_state_dict(trainer_state['running'])

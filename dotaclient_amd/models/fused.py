@@ -16,8 +16,16 @@ heads + loss       one heads GEMM + ``_C.heads_loss`` (pointer logits, 4 masked 
                    entropy, value, and ∂L/∂(every head input) in the same pass) / two GEMMs
 =================  ======================================================================================
 
-The 5v5 entity-attention variant keeps the encoder on bf16 torch ops (the attention block has no fused kernel yet)
-and uses the same LSTM and heads kernels through per-stage autograd wrappers.
+Precision (``FusedPolicy(precision=...)``):
+
+* ``'fp32'`` (default; the reference trains in fp32, optimizer.py:281, policy.py:52-78): fp32 activations,
+  gradients and accumulation end to end. The hand-written kernels run "bf16x3" — each fp32 MFMA operand split once
+  into a hi and a lo bf16, products as hi·hi + lo·hi + hi·lo (≈2⁻¹⁶ relative per product) — and the plain GEMMs
+  run on hipBLASLt's exact-f32 path. The LSTM hidden state is exchanged and stored in fp32.
+* ``'bf16'``: bf16 GEMM operands / saved activations, fp32 accumulation, recurrence state and optimizer.
+
+The 5v5 entity-attention policy has fused kernels on the bf16 pipelined step; in fp32 the learner runs it on the
+eager fp32 reference path (``learner/engine.py``).
 """
 from __future__ import annotations
 
@@ -35,7 +43,8 @@ LDZ = 160
 
 
 def _mm(a, b):
-    return torch.mm(a, b, out_dtype=torch.float32)
+    """fp32-output GEMM: bf16 operands on hipBLASLt's bf16 path, fp32 operands on its exact-f32 path."""
+    return a @ b if a.dtype == torch.float32 else torch.mm(a, b, out_dtype=torch.float32)
 
 
 def _bf(t):
@@ -70,6 +79,8 @@ class _PolicyLoss(torch.autograd.Function):
         C = fp.C
         cfg, lc = fp.cfg, fp.loss_cfg
         P = dict(zip(fp.param_names, params))
+        _bf = fp.wcast                        # GEMM operand dtype of this learner: bf16, or fp32 (bf16x3 kernels)
+        adt = torch.float32 if fp.fp32 else torch.bfloat16
         B, S, U, _ = units.shape
         N = B * S
         counts = list(cfg.layout.counts)
@@ -86,7 +97,7 @@ class _PolicyLoss(torch.autograd.Function):
             arg[:, 5] = arg[:, 3]
         wpre16 = _bf(P['affine_pre_rnn.weight'])
         x = torch.relu(_mm(x896, wpre16.t()) + P['affine_pre_rnn.bias'].detach())
-        x16 = x.to(torch.bfloat16)
+        x16 = x.to(adt)
         if cfg.rnn == 'lstm':
             H = cfg.hidden
             wih16, whh16 = _bf(P['rnn.weight_ih_l0']), _bf(P['rnn.weight_hh_l0'])
@@ -98,6 +109,7 @@ class _PolicyLoss(torch.autograd.Function):
                 xp4 = (_mm(x16, wih16.t()) + bias[perm]).view(B, S, H, 4)
                 hs16, _, cs, gates, _, _ = team_fwd(C, xp4, whh16, h0, c0, fp.err, False)
             else:
+                assert not fp.fp32, 'the fp32 learner runs the team recurrence (DCA_LSTM_IMPL=team)'
                 perm = None
                 xp = (_mm(x16, wih16.t()) + bias).view(B, S, 4 * H)
                 hs, cs, gates = [], [], []
@@ -113,10 +125,10 @@ class _PolicyLoss(torch.autograd.Function):
             rnn_saved = (hs16, cs, gates, wih16, whh16)
         else:
             wf16 = _bf(P['fake_rnn.weight'])
-            xh16 = (_mm(x16, wf16.t()) + P['fake_rnn.bias'].detach()).to(torch.bfloat16)
+            xh16 = (_mm(x16, wf16.t()) + P['fake_rnn.bias'].detach()).to(adt)
             rnn_saved = (wf16,)
         wcat, bcat = fp.head_cat(P)
-        wcat16 = wcat.to(torch.bfloat16)
+        wcat16 = wcat.to(adt)
         z = _mm(xh16, wcat16.t()) + bcat
         dz, dtl, part, logp = C.heads_loss(z, emb.view(N, U, 128), actions, masks, adv, ret, logp_old, nret, norms,
                                            0 if lc.algo == 'ppo' else 1, bool(lc.compat_value_bug), S, B,
@@ -138,9 +150,10 @@ class _PolicyLoss(torch.autograd.Function):
         P = {n: p for n, p in zip(fp.param_names, fp.params)}
         g = gpart[15]
         grads: Dict[str, torch.Tensor] = {}
+        adt = torch.float32 if fp.fp32 else torch.bfloat16
         # ---- heads
         dZ = dz * g
-        dZ16 = dZ.to(torch.bfloat16)
+        dZ16 = dZ.to(adt)
         dWcat = _mm(dZ16.t(), xh16)
         dbcat = dZ.sum(0)
         fp.split_head_grads(dWcat, dbcat, grads)
@@ -162,8 +175,8 @@ class _PolicyLoss(torch.autograd.Function):
                                    fp.err)
                     dg.append(o[0])
                 dgates = (torch.cat(dg) if len(dg) > 1 else dg[0]).view(N, 4 * H)
-            dG16 = dgates.to(torch.bfloat16)
-            hprev = torch.cat([h0.to(torch.bfloat16).unsqueeze(1), hs16[:, :-1]], dim=1).view(N, H)
+            dG16 = dgates.to(adt)
+            hprev = torch.cat([h0.to(adt).unsqueeze(1), hs16[:, :-1]], dim=1).view(N, H)
             dwhh = _mm(dG16.t(), hprev)
             dwih = _mm(dG16.t(), x16)
             db = dgates.sum(0)
@@ -178,13 +191,13 @@ class _PolicyLoss(torch.autograd.Function):
             dx = _mm(dG16, wih16)
         else:
             (wf16,) = rnn_saved
-            dxh16 = dxh.to(torch.bfloat16)
+            dxh16 = dxh.to(adt)
             grads['fake_rnn.weight'] = _mm(dxh16.t(), x16)
             grads['fake_rnn.bias'] = dxh.sum(0)
             dx = _mm(dxh16, wf16)
         # ---- pre-RNN
         dpre = dx * (x > 0)
-        dpre16 = dpre.to(torch.bfloat16)
+        dpre16 = dpre.to(adt)
         grads['affine_pre_rnn.weight'] = _mm(dpre16.t(), x896)
         grads['affine_pre_rnn.bias'] = dpre.sum(0)
         dx896 = _mm(dpre16, wpre16)
@@ -224,12 +237,19 @@ class _PolicyLoss(torch.autograd.Function):
 
 
 class FusedPolicy:
-    def __init__(self, policy: Policy, loss_cfg=None):
+    def __init__(self, policy: Policy, loss_cfg=None, precision: str = 'fp32'):
         from .. import ops
+        if precision not in ('fp32', 'bf16'):
+            raise ValueError(f'precision must be fp32 or bf16, got {precision!r}')
         self.C = ops.require()
         self.policy = policy
         self.cfg = policy.config
         self.loss_cfg = loss_cfg
+        self.precision = precision
+        self.fp32 = precision == 'fp32'
+        if self.fp32 and self.cfg.entity_attention:
+            raise ValueError('the fp32 fused learner has no entity-attention kernels: use backend="torch" (fp32 '
+                             'eager) or precision="bf16" for the 5v5 policy')
         dev = next(policy.parameters()).device
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.param_names: List[str] = [n for n, _ in policy.named_parameters()]
@@ -238,6 +258,11 @@ class FusedPolicy:
         # the 5v5 entity-attention encoder has fused kernels on the pipelined (time-major) step only
         self.attention_fused = (self.cfg.entity_attention and self.cfg.unit_dim == 128 and self.cfg.env_dim == 128
                                 and self.cfg.attention_heads == 4 and self.cfg.layout.max_units == 64)
+
+    def wcast(self, t: torch.Tensor) -> torch.Tensor:
+        """A detached working copy of a weight in this learner's GEMM operand dtype (fp32 or bf16)."""
+        t = t.detach()
+        return t if self.fp32 else t.to(torch.bfloat16)
 
     def apply_direct_grads(self, grads, g, written=(), set_mask: bool = True):
         """Accumulate precomputed gradients straight into the parameters' ``.grad`` (views of the learner's flat

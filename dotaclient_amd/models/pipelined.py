@@ -42,7 +42,12 @@ METRIC_NAMES = ['loss', 'policy_loss', 'entropy_loss', 'advantage_loss', 'entrop
 
 
 def _mm(a, b):
-    return torch.mm(a, b, out_dtype=torch.float32)
+    """GEMM with fp32 output: bf16 operands on hipBLASLt's bf16 path, fp32 operands on its exact-f32 path."""
+    return a @ b if a.dtype == torch.float32 else torch.mm(a, b, out_dtype=torch.float32)
+
+
+def _addmm(bias, a, b):
+    return torch.addmm(bias, a, b) if a.dtype == torch.float32 else torch.addmm(bias, a, b, out_dtype=torch.float32)
 
 
 def _acc(a, b):
@@ -60,10 +65,10 @@ class WeightImages:
     """Per-step working copies of the weights, produced by ONE ``weight_prep`` gather launch from the flat fp32
     parameter buffer (instead of ≈25 cast / stack / permute / cat launches):
 
-    bf16: ``wt16`` (6,128,128) type weights, ``wtT16`` their transposes, ``wpre16`` (256,896) + ``bpre16``,
-    ``wih16`` (4H,256)
-    rows in unit-major gate order, ``whh16`` (4H,H), ``wcat16`` (LDZ,H) = [attention|enum|x|y|value|0-pad];
-    fp32: ``bt`` (6,128), ``bias4`` (4H) = (b_ih + b_hh) in unit-major gate order, ``bcat`` (LDZ).
+    GEMM operands (bf16 in the bf16 learner, fp32 in the fp32 learner — same keys): ``wt16`` (6,128,128) type
+    weights, ``wtT16`` their transposes, ``wpre16`` (256,896) + ``bpre16``, ``wih16`` (4H,256) rows in unit-major
+    gate order, ``whh16`` (4H,H), ``wcat16`` (LDZ,H) = [attention|enum|x|y|value|0-pad];
+    always fp32: ``bt`` (6,128), ``bias4`` (4H) = (b_ih + b_hh) in unit-major gate order, ``bcat`` (LDZ).
     The index maps are built once from the parameters' offsets in the flat buffer."""
 
     def __init__(self, fp, flat: torch.Tensor, with_value: bool):
@@ -106,9 +111,14 @@ class WeightImages:
             parts32['bout'] = (bo, None)
             parts32['ln_g'] = (idx('entity_attn.ln.weight'), None)
             parts32['ln_b'] = (idx('entity_attn.ln.bias'), None)
+        if getattr(fp, 'fp32', False):
+            # fp32 learner: the GEMM operand images are fp32 gathers too (the HIP kernels split them into bf16 hi/lo
+            # pairs themselves, hipBLASLt runs exact f32)
+            parts32.update({k: (v, None) for k, v in parts16.items()})
+            parts16 = {}
         self.shapes16 = {k: tuple(v.shape) for k, v in parts16.items()}
         self.shapes32 = {k: tuple(v[0].shape) for k, v in parts32.items()}
-        m16 = torch.cat([v.reshape(-1) for v in parts16.values()])
+        m16 = torch.cat([v.reshape(-1) for v in parts16.values()]) if parts16 else torch.zeros(0, dtype=torch.int64)
         m32 = torch.cat([torch.stack([a.reshape(-1), (b.reshape(-1) if b is not None else neg(a.numel()))], 1)
                          for a, b in parts32.values()])
         # (expand() above is a broadcast view; reshape copies it)
@@ -163,6 +173,10 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
     bt, bias_p, bcat = W['bt'], W['bias4'], W['bcat']
     # ---- encoder, pre-RNN, input projection over all rows (row-parallel, fast)
     attn = cfg.entity_attention
+    f32 = bool(getattr(fp, 'fp32', False))    # fp32-accurate learner: fp32 activations, bf16x3 MFMA, exact-f32 GEMMs
+    adt = torch.float32 if f32 else torch.bfloat16
+    assert not (f32 and attn), 'the fp32 learner has no fused entity-attention kernels (FusedPolicy.use_pipeline)'
+    # (x896 / emb come back in the weights' dtype: bf16, or fp32 from the bf16x3 encoder)
     x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs))
     if attn:
         # 5v5 entity attention (ops/csrc/attn.hip): emb = E0 + b_out here (bias folded into bt)
@@ -177,10 +191,10 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
     elif cfg.compat_bugs:   # reference policy.py:127: enemy-tower pool = enemy-nonhero pool
         x896[:, 768:896] = x896[:, 512:640]
         arg[:, 5] = arg[:, 3]
-    # relu(x896·W_preᵀ + b) as ONE hipBLASLt GEMM with a bias+ReLU epilogue, bf16 out (x16 > 0 ⟺ x > 0)
+    # relu(x896·W_preᵀ + b) as ONE hipBLASLt GEMM with a bias+ReLU epilogue, bf16 (fp32) out (x16 > 0 ⟺ x > 0)
     x16 = torch._addmm_activation(W['bpre16'], x896, wpre16.t())
     xp4 = _mm(x16, wih16.t()).view(S, B, H, 4)          # the recurrence kernel adds the bias (bias4)
-    hs16 = torch.empty(S, B, H, dtype=torch.bfloat16, device=dev)
+    hs16 = torch.empty(S, B, H, dtype=adt, device=dev)
     cs = torch.empty(S, B, H, device=dev)
     gates4 = torch.empty(S, B, H, 4, device=dev)
     spans = chunk_bounds(S, fp.chunks)
@@ -213,12 +227,12 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
         main.wait_event(done)
         r0, r1 = t0 * B, t1 * B
         xh = hs16[t0:t1].view(-1, H)
-        zc = torch.addmm(bcat, xh, wcat16.t(), out_dtype=torch.float32)     # bias in the GEMM epilogue
-        # ∂L/∂z straight in bf16: only the backward GEMMs read it
+        zc = _addmm(bcat, xh, wcat16.t())     # bias in the GEMM epilogue
+        # ∂L/∂z straight in the GEMM operand dtype: only the backward GEMMs read it
         dz16, dtl_c, part, lp = C.heads_loss(zc, emb[r0:r1], act_t[r0:r1], msk_t[r0:r1], adv_t[r0:r1],
                                              ret_t[r0:r1], lpo_t[r0:r1], nret_t[r0:r1], norms, algo, False,
                                              S, B, float(lc.clip_eps), float(lc.entropy_coef), float(lc.vf_coef),
-                                             dz_bf16=True)
+                                             dz_bf16=not f32)
         parts.append(part)
         first = dWcat is None
         if first:
@@ -241,7 +255,7 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
     split = fp.split_hook if (gout is not None and one) else None
     early_names = fp.early_param_names() if split is not None else frozenset()
     fp.early_applied = frozenset()
-    dgates16 = torch.empty(S, B, H, 4, dtype=torch.bfloat16, device=dev)   # ∂gates straight from the kernel
+    dgates16 = torch.empty(S, B, H, 4, dtype=adt, device=dev)   # ∂gates straight from the kernel
     db = dw1 = db1 = dWt = dbt = dWe = dbe = None
     dgam = dbet = None
     first_attn = True
@@ -258,7 +272,7 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
     dWih = gout['rnn.weight_ih_l0'] if direct else torch.zeros(4 * H, x16.shape[1], device=dev)
     dWpre = gout['affine_pre_rnn.weight'] if direct else torch.zeros(wpre16.shape[0], wpre16.shape[1], device=dev)
     dbpre = gout['affine_pre_rnn.bias'] if direct else torch.zeros(wpre16.shape[0], device=dev)
-    h016 = h0.to(torch.bfloat16)
+    h016 = h0.to(adt).contiguous()
     sL.wait_event(heads_done)
     dh_n = dc_n = None
     bwd_done = []
@@ -266,7 +280,8 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
         for t0, t1 in reversed(spans):
             cinit = c0.contiguous() if t0 == 0 else cs[t0 - 1]
             o = team_bwd(C, dxh[t0:t1], gates4[t0:t1], cs[t0:t1], cinit, dh_n, dc_n, whh16, fp.err,
-                         time_major=True, dg_out=dgates16[t0:t1], dg_bf16=True, want_dbias=True)
+                         time_major=True, dg_out=dgates16[t0:t1], dg_bf16=not f32,
+                         want_dbias=True)
             dh_n, dc_n = o[1], o[2]
             db = _acc(db, o[3])
             e = torch.cuda.Event()
@@ -282,7 +297,7 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
         else:       # h_{t-1} rows: h0 for t = 0, then hs[0 : t1-1] — no concatenation materialised
             gemm_tn(dG16, hs16[0:t1 - 1].view(n - B, H), out=dWhh, perm=gperm, accumulate=True, b0=h016)
         gemm_tn(dG16, x16[r0:r1], out=dWih, perm=gperm, accumulate=True)
-        # ∂pre-activation of the pre-RNN layer: bf16 GEMM, ReLU mask in one threshold_backward kernel
+        # ∂pre-activation of the pre-RNN layer: one GEMM (bf16 or exact f32), ReLU mask in one threshold_backward
         dpre16 = torch.ops.aten.threshold_backward(torch.mm(dG16, wih16), x16[r0:r1], 0)
         gemm_tn(dpre16, x896[r0:r1], out=dWpre, accumulate=True, colsum=dbpre)
         dx896 = _mm(dpre16, wpre16)

@@ -125,6 +125,8 @@ std::vector<torch::Tensor> lstm_bwd(torch::Tensor dhs, torch::Tensor gates, torc
 
 // ------------------------------------------------------------------------------------------------------------
 // XCD-team LSTM recurrence (lstm_team.hip). Gates in unit-major (·,·,H,4) layout; see the kernel header.
+// whh bf16: bf16 MFMA, h exchanged in bf16 (hs bf16, optional f32 copy); whh fp32: the fp32-accurate variant
+// (bf16x3 split MFMA, h exchanged in fp32; returns hs f32 in both hs slots).
 // time_major=false: xp4 (B,S,H,4) and outputs (B,S,…); time_major=true: xp4 (S,B,H,4) and outputs (S,B,…) — a
 // time chunk [t0,t1) of a time-major tensor is then a contiguous slice, which the pipelined learner step uses.
 // Outputs may be passed in (e.g. slices of a whole-sequence tensor) to avoid copies.
@@ -152,7 +154,9 @@ std::vector<torch::Tensor> lstm_team_fwd(torch::Tensor xp4, torch::Tensor whh, t
                                          bool time_major, c10::optional<torch::Tensor> hs_out,
                                          c10::optional<torch::Tensor> cs_out, c10::optional<torch::Tensor> gates_out,
                                          c10::optional<torch::Tensor> bias4) {
-  CHECK_F32(xp4); CHECK_BF16(whh); CHECK_F32(h0); CHECK_F32(c0); CHECK_I32(err); check_ctl(ctl);
+  CHECK_F32(xp4); CHECK_DEV(whh); CHECK_CONTIG(whh); CHECK_F32(h0); CHECK_F32(c0); CHECK_I32(err); check_ctl(ctl);
+  const bool f32w = whh.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32w || whh.scalar_type() == at::kBFloat16, "whh must be bf16 or f32");
   TORCH_CHECK(xp4.dim() == 4 && xp4.size(3) == 4, "xp4 must be (B,S,H,4) or (S,B,H,4)");
   const int B = time_major ? xp4.size(1) : xp4.size(0), S = time_major ? xp4.size(0) : xp4.size(1);
   const int H = xp4.size(2);
@@ -161,8 +165,8 @@ std::vector<torch::Tensor> lstm_team_fwd(torch::Tensor xp4, torch::Tensor whh, t
   TORCH_CHECK(H == 128 || H == 256 || H == 512, "lstm_team_fwd: H in {128,256,512}");
   auto f32 = xp4.options();
   const int64_t d0 = time_major ? S : B, d1 = time_major ? B : S;
-  auto hs = out_or_new(hs_out, {d0, d1, H}, f32.dtype(at::kBFloat16), "hs_out");
-  torch::Tensor hsf = want_f32_h ? torch::empty({d0, d1, H}, f32) : torch::Tensor();
+  auto hs = out_or_new(hs_out, {d0, d1, H}, f32w ? f32 : f32.dtype(at::kBFloat16), "hs_out");
+  torch::Tensor hsf = (want_f32_h && !f32w) ? torch::empty({d0, d1, H}, f32) : torch::Tensor();
   auto cs = out_or_new(cs_out, {d0, d1, H}, f32, "cs_out");
   auto gates4 = out_or_new(gates_out, {d0, d1, H, 4}, f32, "gates_out");
   auto hn = torch::empty({B, H}, f32);
@@ -173,15 +177,17 @@ std::vector<torch::Tensor> lstm_team_fwd(torch::Tensor xp4, torch::Tensor whh, t
     TORCH_CHECK(bias4->numel() == 4 * H, "bias4 must hold 4H floats (unit-major)");
     bias_p = ptr<float>(*bias4);
   }
-  const size_t wsb = dca_lstm_team_workspace(B, H, 0);
+  const size_t wsb = dca_lstm_team_workspace(B, H, 0, f32w ? 1 : 0);
   auto ws = torch::empty({(int64_t)wsb}, f32.dtype(at::kByte));
-  hip_check(dca_lstm_team_fwd(ptr<float>(xp4), ptr<short>(whh), ptr<float>(h0), ptr<float>(c0), ptr<short>(hs),
-                              want_f32_h ? ptr<float>(hsf) : nullptr, ptr<float>(cs), ptr<float>(gates4),
-                              ptr<float>(hn), ptr<float>(cn), ctl.data_ptr(), ws.data_ptr(), wsb,
+  hip_check(dca_lstm_team_fwd(ptr<float>(xp4), whh.data_ptr(), ptr<float>(h0), ptr<float>(c0),
+                              f32w ? nullptr : ptr<short>(hs),
+                              f32w ? ptr<float>(hs) : (want_f32_h ? ptr<float>(hsf) : nullptr), ptr<float>(cs),
+                              ptr<float>(gates4), ptr<float>(hn), ptr<float>(cn), ctl.data_ptr(), ws.data_ptr(), wsb,
                               ptr<unsigned>(err), B, S, H, time_major ? 1 : 0, cur_stream(),
                               (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr,
-                              bias_p),
+                              bias_p, f32w ? 1 : 0),
             "dca_lstm_team_fwd");
+  if (f32w) return {hs, hs, cs, gates4, hn, cn};
   return {hs, want_f32_h ? hsf : hs, cs, gates4, hn, cn};
 }
 
@@ -190,8 +196,11 @@ std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4
                                          c10::optional<torch::Tensor> dcn, torch::Tensor whh, torch::Tensor err,
                                          torch::Tensor ctl, c10::optional<torch::Tensor> trace, bool time_major,
                                          c10::optional<torch::Tensor> dg_out, bool dg_bf16, bool want_dbias) {
-  CHECK_F32(dhs); CHECK_F32(gates4); CHECK_F32(cs); CHECK_F32(c0); CHECK_BF16(whh); CHECK_I32(err);
+  CHECK_F32(dhs); CHECK_F32(gates4); CHECK_F32(cs); CHECK_F32(c0); CHECK_DEV(whh); CHECK_CONTIG(whh); CHECK_I32(err);
   check_ctl(ctl);
+  const bool f32w = whh.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32w || whh.scalar_type() == at::kBFloat16, "whh must be bf16 or f32");
+  TORCH_CHECK(!(f32w && dg_bf16), "lstm_team_bwd: the fp32 variant writes fp32 gate gradients");
   const int B = time_major ? dhs.size(1) : dhs.size(0), S = time_major ? dhs.size(0) : dhs.size(1);
   const int H = dhs.size(2);
   TORCH_CHECK(gates4.dim() == 4 && gates4.size(0) == dhs.size(0) && gates4.size(1) == dhs.size(1) &&
@@ -211,15 +220,16 @@ std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4
   auto dh0 = torch::empty({B, H}, f32);
   auto dc0 = torch::empty({B, H}, f32);
   // per-chain bias-gradient partials (Σ over the chain's rows and steps), summed in chain order below
-  torch::Tensor dbp = want_dbias ? torch::empty({dca_lstm_team_chains(B), 4 * H}, f32) : torch::Tensor();
-  const size_t wsb = dca_lstm_team_workspace(B, H, 1);
+  torch::Tensor dbp = want_dbias ? torch::empty({dca_lstm_team_chains(B, f32w ? 1 : 0), 4 * H}, f32) : torch::Tensor();
+  const size_t wsb = dca_lstm_team_workspace(B, H, 1, f32w ? 1 : 0);
   auto ws = torch::empty({(int64_t)wsb}, f32.dtype(at::kByte));
   hip_check(dca_lstm_team_bwd(ptr<float>(dhs), ptr<float>(gates4), ptr<float>(cs), ptr<float>(c0), dhn_p, dcn_p,
-                              ptr<short>(whh), dg_bf16 ? nullptr : ptr<float>(dgates4), ptr<float>(dh0),
+                              whh.data_ptr(), dg_bf16 ? nullptr : ptr<float>(dgates4), ptr<float>(dh0),
                               ptr<float>(dc0), ctl.data_ptr(), ws.data_ptr(), wsb, ptr<unsigned>(err), B, S, H,
                               time_major ? 1 : 0, cur_stream(),
                               (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr,
-                              dg_bf16 ? ptr<short>(dgates4) : nullptr, want_dbias ? ptr<float>(dbp) : nullptr),
+                              dg_bf16 ? ptr<short>(dgates4) : nullptr, want_dbias ? ptr<float>(dbp) : nullptr,
+                              f32w ? 1 : 0),
             "dca_lstm_team_bwd");
   if (want_dbias) return {dgates4, dh0, dc0, dbp.sum(0)};
   return {dgates4, dh0, dc0};
@@ -232,8 +242,10 @@ std::vector<torch::Tensor> heads_loss(torch::Tensor z, torch::Tensor emb, torch:
                                       torch::Tensor nret, torch::Tensor norms, int64_t algo, bool compat_value_bug,
                                       int64_t S_bug, int64_t B_bug, double clip_eps, double ent_coef,
                                       double vf_coef, bool dz_bf16) {
-  CHECK_F32(z); CHECK_BF16(emb); CHECK_U8(act); CHECK_U8(msk); CHECK_F32(adv); CHECK_F32(ret);
+  CHECK_F32(z); CHECK_DEV(emb); CHECK_CONTIG(emb); CHECK_U8(act); CHECK_U8(msk); CHECK_F32(adv); CHECK_F32(ret);
   CHECK_F32(logp_old); CHECK_F32(nret); CHECK_F32(norms);
+  const bool ef32 = emb.scalar_type() == at::kFloat;
+  TORCH_CHECK(ef32 || emb.scalar_type() == at::kBFloat16, "emb must be bf16 or f32");
   TORCH_CHECK(z.dim() == 2 && emb.dim() == 3 && emb.size(2) == 128, "z (N,ldz), emb (N,U,128)");
   const int N = z.size(0), ldz = z.size(1), U = emb.size(1);
   TORCH_CHECK(emb.size(0) == N && act.size(0) == N && msk.size(0) == N, "row count mismatch");
@@ -246,25 +258,27 @@ std::vector<torch::Tensor> heads_loss(torch::Tensor z, torch::Tensor emb, torch:
   const int nb = dca_heads_loss_nblocks(N);
   auto part = torch::empty({nb, 16}, z.options());
   auto logp = torch::empty({N}, z.options());
-  hip_check(dca_heads_loss(ptr<float>(z), ldz, ptr<short>(emb), ptr<unsigned char>(act), ptr<unsigned char>(msk),
+  hip_check(dca_heads_loss(ptr<float>(z), ldz, emb.data_ptr(), ptr<unsigned char>(act), ptr<unsigned char>(msk),
                            21 + U, ptr<float>(adv), ptr<float>(ret), ptr<float>(logp_old), ptr<float>(nret),
                            ptr<float>(norms), dz_bf16 ? nullptr : ptr<float>(dz), ptr<float>(dtl), ptr<float>(part),
                            ptr<float>(logp), N, U, (int)algo, compat_value_bug ? 1 : 0, (int)S_bug, (int)B_bug,
                            (float)clip_eps, (float)ent_coef, (float)vf_coef, cur_stream(),
-                           dz_bf16 ? ptr<short>(dz) : nullptr),
+                           dz_bf16 ? ptr<short>(dz) : nullptr, ef32 ? 1 : 0),
             "dca_heads_loss");
   return {dz, dtl, part, logp};
 }
 
 // ------------------------------------------------------------------------------------------------------------
-// Fused entity encoder. units (N,U,10) f32, env (N,3) f32, w1 (128,10), b1 (128), wt (6,128,128) bf16,
-// bt (6,128), we (128,3), be (128); counts = 6 unit counts. Returns (x896 bf16 (N,896), emb bf16 (N,U,128),
-// argmax u8 (N,6,128)).
+// Fused entity encoder. units (N,U,10) f32, env (N,3) f32, w1 (128,10), b1 (128), wt (6,128,128) bf16 or f32,
+// bt (6,128), we (128,3), be (128); counts = 6 unit counts. Returns (x896 (N,896), emb (N,U,128), argmax u8
+// (N,6,128)); x896 / emb have wt's dtype (f32: the fp32-accurate bf16x3 variant).
 std::vector<torch::Tensor> encoder_fwd(torch::Tensor units, torch::Tensor env, torch::Tensor w1, torch::Tensor b1,
                                        torch::Tensor wt, torch::Tensor bt, torch::Tensor we, torch::Tensor be,
                                        std::vector<int64_t> counts, bool compat) {
-  CHECK_F32(units); CHECK_F32(env); CHECK_F32(w1); CHECK_F32(b1); CHECK_BF16(wt); CHECK_F32(bt); CHECK_F32(we);
-  CHECK_F32(be);
+  CHECK_F32(units); CHECK_F32(env); CHECK_F32(w1); CHECK_F32(b1); CHECK_DEV(wt); CHECK_CONTIG(wt); CHECK_F32(bt);
+  CHECK_F32(we); CHECK_F32(be);
+  const bool f32w = wt.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32w || wt.scalar_type() == at::kBFloat16, "wt must be bf16 or f32");
   TORCH_CHECK(units.dim() == 3 && units.size(2) == 10, "units must be (N,U,10)");
   const int N = units.size(0), U = units.size(1);
   TORCH_CHECK(env.size(0) == N && env.size(1) == 3, "env must be (N,3)");
@@ -276,12 +290,13 @@ std::vector<torch::Tensor> encoder_fwd(torch::Tensor units, torch::Tensor env, t
   for (int i = 0; i < 6; ++i) { c[i] = (int)counts[i]; tot += counts[i]; }
   TORCH_CHECK(tot == U && U <= 64, "counts must sum to U <= 64");
   auto o = units.options();
-  auto x896 = torch::empty({N, 896}, o.dtype(at::kBFloat16));
-  auto emb = torch::empty({N, U, 128}, o.dtype(at::kBFloat16));
+  const auto adt = f32w ? at::kFloat : at::kBFloat16;
+  auto x896 = torch::empty({N, 896}, o.dtype(adt));
+  auto emb = torch::empty({N, U, 128}, o.dtype(adt));
   auto arg = torch::empty({N, 6, 128}, o.dtype(at::kByte));
-  hip_check(dca_encoder_fwd(ptr<float>(units), ptr<float>(env), ptr<float>(w1), ptr<float>(b1), ptr<short>(wt),
-                            ptr<float>(bt), ptr<float>(we), ptr<float>(be), ptr<short>(x896), ptr<short>(emb),
-                            ptr<unsigned char>(arg), N, U, c, compat ? 1 : 0, cur_stream()),
+  hip_check(dca_encoder_fwd(ptr<float>(units), ptr<float>(env), ptr<float>(w1), ptr<float>(b1), wt.data_ptr(),
+                            ptr<float>(bt), ptr<float>(we), ptr<float>(be), x896.data_ptr(), emb.data_ptr(),
+                            ptr<unsigned char>(arg), N, U, c, compat ? 1 : 0, cur_stream(), f32w ? 1 : 0),
             "dca_encoder_fwd");
   return {x896, emb, arg};
 }
@@ -291,8 +306,10 @@ std::vector<torch::Tensor> encoder_bwd(torch::Tensor units, torch::Tensor w1, to
                                        torch::Tensor dtl, torch::Tensor q, torch::Tensor dx, torch::Tensor arg,
                                        std::vector<int64_t> counts, bool compat,
                                        c10::optional<torch::Tensor> demb_in) {
-  CHECK_F32(units); CHECK_F32(w1); CHECK_F32(b1); CHECK_BF16(wtT); CHECK_F32(dtl); CHECK_F32(dx); CHECK_U8(arg);
-  CHECK_DEV(q); CHECK_DT(q, at::kFloat);
+  CHECK_F32(units); CHECK_F32(w1); CHECK_F32(b1); CHECK_DEV(wtT); CHECK_CONTIG(wtT); CHECK_F32(dtl); CHECK_F32(dx);
+  CHECK_U8(arg); CHECK_DEV(q); CHECK_DT(q, at::kFloat);
+  const bool f32w = wtT.scalar_type() == at::kFloat;
+  TORCH_CHECK(f32w || wtT.scalar_type() == at::kBFloat16, "wtT must be bf16 or f32");
   const int N = units.size(0), U = units.size(1);
   TORCH_CHECK(q.dim() == 2 && q.size(0) == N && q.size(1) >= 128 && q.stride(1) == 1 && q.stride(0) % 4 == 0,
               "q must be (N, >=128) with unit column stride and 16-B aligned rows");
@@ -306,18 +323,19 @@ std::vector<torch::Tensor> encoder_bwd(torch::Tensor units, torch::Tensor w1, to
   auto dwt = torch::empty({6, 128, 128}, o);
   auto dw1 = torch::empty({128, 10}, o);
   auto db1 = torch::empty({128}, o);
-  const size_t wsb = dca_encoder_bwd_workspace(N, U, c);
+  const size_t wsb = dca_encoder_bwd_workspace(N, U, c, f32w ? 1 : 0);
   auto ws = torch::empty({(int64_t)((wsb + 3) / 4)}, o);
   const short* dein = nullptr;
   if (demb_in && demb_in->defined()) {
     CHECK_BF16(*demb_in);
+    TORCH_CHECK(!f32w, "encoder_bwd: demb_in is a bf16-variant input");
     TORCH_CHECK(demb_in->numel() == (int64_t)N * U * 128, "demb_in must be (N, U, 128)");
     dein = ptr<short>(*demb_in);
   }
-  hip_check(dca_encoder_bwd(ptr<float>(units), ptr<float>(w1), ptr<float>(b1), ptr<short>(wtT), ptr<float>(dtl),
+  hip_check(dca_encoder_bwd(ptr<float>(units), ptr<float>(w1), ptr<float>(b1), wtT.data_ptr(), ptr<float>(dtl),
                             ptr<float>(q), (int)q.stride(0), ptr<float>(dx), ptr<unsigned char>(arg), ptr<float>(dwt),
                             ptr<float>(dw1), ptr<float>(db1), ws.data_ptr(), wsb, N, U, c, compat ? 1 : 0,
-                            cur_stream(), dein),
+                            cur_stream(), dein, f32w ? 1 : 0),
             "dca_encoder_bwd");
   return {dwt, dw1, db1};
 }
@@ -460,29 +478,34 @@ void weight_prep(torch::Tensor src, torch::Tensor map16, torch::Tensor dst16, to
             "dca_weight_prep");
 }
 
-// C (+)= Aᵀ·B for K-outer bf16 operands (split-K MFMA, ops/csrc/gemm_tn.hip). A (K,M) and B (K-split_rows,N) are
-// row-major with unit column stride (any row stride); optional B0 (split_rows,N) supplies rows k < split_rows of
-// the B operand. C (M',N) f32 with unit column stride; optional perm (M) i32 maps result row m → C row perm[m].
+// C (+)= Aᵀ·B for K-outer operands (split-K MFMA, ops/csrc/gemm_tn.hip). A (K,M) and B (K-split_rows,N) are
+// row-major with unit column stride (any row stride), both bf16 or both fp32 (fp32: bf16x3 split MFMA, ≈fp32
+// accuracy); optional B0 (split_rows,N) supplies rows k < split_rows of the B operand. C (M',N) f32 with unit column
+// stride; optional perm (M) i32 maps result row m → C row perm[m].
 void gemm_tn(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torch::Tensor> perm, bool accumulate,
              c10::optional<torch::Tensor> B0, c10::optional<torch::Tensor> colsum) {
   CHECK_DEV(A); CHECK_DEV(B); CHECK_DEV(C);
-  TORCH_CHECK(A.scalar_type() == at::kBFloat16 && B.scalar_type() == at::kBFloat16 && C.scalar_type() == at::kFloat,
-              "gemm_tn: A, B bf16, C f32");
+  const bool f32 = A.scalar_type() == at::kFloat;
+  TORCH_CHECK((A.scalar_type() == at::kBFloat16 || f32) && B.scalar_type() == A.scalar_type() &&
+                  C.scalar_type() == at::kFloat, "gemm_tn: A, B both bf16 or both f32; C f32");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2 && A.stride(1) == 1 && B.stride(1) == 1 &&
               C.stride(1) == 1, "gemm_tn: 2-D operands with unit column stride");
   const int K = A.size(0), M = A.size(1), N = B.size(1);
   int split_rows = 0;
-  const short* b0 = nullptr;
+  const void* b0 = nullptr;
   if (B0 && B0->defined()) {
     CHECK_DEV(*B0);
-    TORCH_CHECK(B0->scalar_type() == at::kBFloat16 && B0->dim() == 2 && B0->size(1) == N && B0->stride(1) == 1 &&
-                B0->stride(0) == B.stride(0), "gemm_tn: B0 must match B's columns and row stride");
+    TORCH_CHECK(B0->scalar_type() == A.scalar_type() && B0->dim() == 2 && B0->size(1) == N && B0->stride(1) == 1 &&
+                B0->stride(0) == B.stride(0), "gemm_tn: B0 must match B's dtype, columns and row stride");
     split_rows = B0->size(0);
-    b0 = ptr<short>(*B0);
+    b0 = B0->data_ptr();
   }
   TORCH_CHECK(B.size(0) + split_rows == K, "gemm_tn: K mismatch between A and [B0; B]");
-  TORCH_CHECK(M % 8 == 0 && N % 8 == 0 && A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0,
-              "gemm_tn: M, N and row strides must be multiples of 8 (16-B loads)");
+  const int al = f32 ? 4 : 8;   // elements per 16-B load
+  TORCH_CHECK(M % 8 == 0 && N % 8 == 0 && A.stride(0) % al == 0 && B.stride(0) % al == 0,
+              "gemm_tn: M, N multiples of 8 and row strides 16-B aligned");
+  TORCH_CHECK((reinterpret_cast<uintptr_t>(A.data_ptr()) & 15) == 0 && (reinterpret_cast<uintptr_t>(B.data_ptr()) & 15) == 0 &&
+              (b0 == nullptr || (reinterpret_cast<uintptr_t>(b0) & 15) == 0), "gemm_tn: operands must be 16-B aligned");
   const int* pp = nullptr;
   int64_t crow = M;
   if (perm && perm->defined()) {
@@ -506,12 +529,12 @@ void gemm_tn(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<to
     return;
   }
   int splits, kc, tiles;
-  dca_gemm_tn_plan(M, N, K, &splits, &kc, &tiles);
+  dca_gemm_tn_plan(M, N, K, &splits, &kc, &tiles, f32 ? 1 : 0);
   torch::Tensor slab;
   if (splits > 1) slab = torch::empty({(int64_t)splits * M * N + (csp ? (int64_t)splits * M : 0)}, C.options());
-  hip_check(dca_gemm_tn(ptr<short>(A), (int)A.stride(0), ptr<short>(B), (int)B.stride(0), b0, split_rows,
+  hip_check(dca_gemm_tn(A.data_ptr(), (int)A.stride(0), B.data_ptr(), (int)B.stride(0), b0, split_rows,
                         ptr<float>(C), (int)C.stride(0), pp, accumulate ? 1 : 0, M, N, K,
-                        splits > 1 ? ptr<float>(slab) : nullptr, csp, cur_stream()),
+                        splits > 1 ? ptr<float>(slab) : nullptr, csp, cur_stream(), f32 ? 1 : 0),
             "dca_gemm_tn");
 }
 
@@ -714,7 +737,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("loss_prep_ws_elems", &loss_prep_ws_elems, "int32 workspace elements of loss_prep");
   m.def("loss_assemble", &loss_assemble, "loss scalar + metrics from heads/loss partials");
   m.def("weight_prep", &weight_prep, "gather the flat fp32 params into bf16 / fp32 working weight images");
-  m.def("gemm_tn", &gemm_tn, "C (+)= A^T B for K-outer bf16 operands (split-K MFMA, LDS transposed reads)",
+  m.def("gemm_tn", &gemm_tn, "C (+)= A^T B for K-outer bf16 or fp32 (bf16x3) operands (split-K MFMA, LDS transposed reads)",
         py::arg("A"), py::arg("B"), py::arg("C"), py::arg("perm") = py::none(), py::arg("accumulate") = false,
         py::arg("B0") = py::none(), py::arg("colsum") = py::none());
   m.def("enc_small_grads", &enc_small_grads, "entity-encoder type-bias and env-layer gradients in one pass");

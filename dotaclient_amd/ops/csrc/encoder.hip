@@ -43,12 +43,12 @@ struct FwdParams {
   const float* env;     // (N, 3)
   const float* w1;      // (128, 10)
   const float* b1;      // (128)
-  const short* wt;      // (6, 128, 128) bf16  W_τ (out, in)
+  const void* wt;       // (6, 128, 128) W_τ (out, in): bf16, or fp32 in the F32 variant
   const float* bt;      // (6, 128)
   const float* we;      // (128, 3)
   const float* be;      // (128)
-  short* x896;          // (N, 896) bf16 out: [env | pool_ah | pool_eh | pool_anh | pool_enh | pool_ath | pool_eth]
-  short* emb;           // (N, U, 128) bf16 out
+  void* x896;           // (N, 896) out (bf16 / F32: fp32): [env | pool_ah | pool_eh | pool_anh | pool_enh | pool_ath | pool_eth]
+  void* emb;            // (N, U, 128) out (bf16 / F32: fp32)
   unsigned char* arg;   // (N, 6, 128) u8 out
   int N;
   int compat;           // reference bug: eth pool = enh pool (policy.py:127)
@@ -59,7 +59,7 @@ struct BwdParams {
   const float* units;
   const float* w1;
   const float* b1;
-  const short* wtT;     // (6, 128, 128) bf16  W_τᵀ (in, out)
+  const void* wtT;      // (6, 128, 128) W_τᵀ (in, out): bf16, or fp32 in the F32 variant
   const float* dtl;     // (N, U) ∂L/∂pointer-logit
   const float* q;       // pointer query, row stride ldq
   int ldq;
@@ -67,6 +67,8 @@ struct BwdParams {
   const unsigned char* arg;
   short* demb;          // K-blocked bf16 (see kBlk): block (τ, u, 16-row block rb) at blkbase[τ] + u·NB + rb
   short* basic;         // same layout
+  short* demb_lo;       // F32 only: lo bf16 halves of ∂emb / basic (value = hi + lo), same layout
+  short* basic_lo;
   float* w1part;        // (gridDim.x, 128·10 + 128) f32 per-workgroup ∂W1 ‖ ∂b1 partials
   int N;
   int compat;
@@ -92,6 +94,8 @@ __device__ __forceinline__ void load_bfrags(const short* __restrict__ m, bf16x8 
     for (int s = 0; s < 4; ++s)
       bf[n][s] = *reinterpret_cast<const bf16x8*>(m + (size_t)(16 * n + j) * kD + 32 * s + 8 * kg);
 }
+
+__device__ __forceinline__ short bf_lo(float v) { return dca::f2bf(v - dca::bf2f(dca::f2bf(v))); }
 
 // LDS staging of a type job's unit features (shared by forward and backward, see the backward's notes).
 constexpr int kStage = 24;                  // units staged per chunk (1v1 max 16, 5v5 max 24 per type)
@@ -163,6 +167,13 @@ __device__ __forceinline__ void tile_put(short* img, int n, const f32x4& v, int 
   h[0] = dca::f2bf(v[0]); h[1] = dca::f2bf(v[1]); h[2] = dca::f2bf(v[2]); h[3] = dca::f2bf(v[3]);
   *reinterpret_cast<bf16x4*>(img + img_off(16 * n + i, kg)) = h;
 }
+// the lo bf16 halves (v - bf16(v)) of a C-layout fragment, same image layout (F32 variant)
+__device__ __forceinline__ void tile_put_lo(short* img, int n, const f32x4& v, int lane) {
+  const int i = lane & 15, kg = lane >> 4;
+  bf16x4 h;
+  h[0] = bf_lo(v[0]); h[1] = bf_lo(v[1]); h[2] = bf_lo(v[2]); h[3] = bf_lo(v[3]);
+  *reinterpret_cast<bf16x4*>(img + img_off(16 * n + i, kg)) = h;
+}
 // element jj of lane l = image[k0 + 8(l>>4) + jj][l & 15] (= tile row l&15, columns k0 + 8(l>>4) … +7); k0 % 16 == 0
 __device__ __forceinline__ bf16x8 tile_frag(const short* img, int k0, int lane) {
   typedef __attribute__((address_space(3))) lds_bf16x4 lds_v4;
@@ -210,6 +221,8 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_kernel(FwdParams P) {
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int rbase = blockIdx.x * kRows;
   const int U = P.L.U, N = P.N;
+  short* const x896 = static_cast<short*>(P.x896);
+  short* const embo = static_cast<short*>(P.emb);
   __shared__ __attribute__((aligned(16))) short scr[4][kImg];
   __shared__ __attribute__((aligned(16))) float ust[4][16 * kUP];
 
@@ -221,7 +234,7 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_kernel(FwdParams P) {
       const float e0 = P.env[row * 3], e1 = P.env[row * 3 + 1], e2 = P.env[row * 3 + 2];
       for (int c = c0; c < c0 + 16; ++c) {
         const float v = P.be[c] + P.we[c * 3] * e0 + P.we[c * 3 + 1] * e1 + P.we[c * 3 + 2] * e2;
-        P.x896[(size_t)row * 896 + c] = dca::f2bf(fmaxf(v, 0.f));
+        x896[(size_t)row * 896 + c] = dca::f2bf(fmaxf(v, 0.f));
       }
     }
   }
@@ -238,7 +251,7 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_kernel(FwdParams P) {
     if (cnt == 0) continue;
     const int row0 = rbase + 16 * g;
     bf16x8 wf[8][4];
-    load_bfrags(P.wt + (size_t)tau * kD * kD, wf, lane);
+    load_bfrags(static_cast<const short*>(P.wt) + (size_t)tau * kD * kD, wf, lane);
     float btv[8];
 #pragma unroll
     for (int n = 0; n < 8; ++n) btv[n] = P.bt[tau * kD + 16 * n + i];
@@ -294,7 +307,7 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_kernel(FwdParams P) {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
           const bf16x8 f = tile_frag(img, 32 * s, lane);
-          if (row < N) *reinterpret_cast<bf16x8*>(P.emb + ((size_t)row * U + uoff + u) * kD + 32 * s + 8 * kg) = f;
+          if (row < N) *reinterpret_cast<bf16x8*>(embo + ((size_t)row * U + uoff + u) * kD + 32 * s + 8 * kg) = f;
         }
       }
       __builtin_amdgcn_wave_barrier();
@@ -308,7 +321,7 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_kernel(FwdParams P) {
         const int row = row0 + kg * 4 + r;
         if (row < N) {
           const int col = 16 * n + i;
-          P.x896[(size_t)row * 896 + kD + tau * kD + col] = dca::f2bf(pmax[n][r]);
+          x896[(size_t)row * 896 + kD + tau * kD + col] = dca::f2bf(pmax[n][r]);
           P.arg[((size_t)row * 6 + tau) * kD + col] = (unsigned char)parg[n][r];
         }
       }
@@ -368,7 +381,7 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
     if (row0 >= N) continue;                      // wave-uniform: no rows in this group
     const int rb = row0 / 16;
     bf16x8 wf[8][4];   // B[k=e][n=j] = W_τ[e][j] = W_τᵀ[j][e]
-    load_bfrags(P.wtT + (size_t)tau * kD * kD, wf, lane);
+    load_bfrags(static_cast<const short*>(P.wtT) + (size_t)tau * kD * kD, wf, lane);
     const int arow = row0 + i;
     const bool rok = arow < N;
     const bool eth_dead = P.compat && tau == 5;   // reference bug: eth pool unused → no pool gradient
@@ -519,6 +532,352 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
   for (int e = tid; e < kW1; e += 256) P.w1part[(size_t)blockIdx.x * kW1 + e] = wred[e];
 }
 
+// ============================================================================================================
+// F32 variants (the learner's fp32-accurate mode, "bf16x3"): every MFMA operand x is split once into two bf16,
+// x = hi + lo, and a product is hi·hi + lo·hi + hi·lo on three independent accumulation chains (the dropped lo·lo
+// term and the rounding of lo are ≈2⁻¹⁶ relative; f32 accumulation). Outputs are fp32. The hi + lo weight
+// fragments of a whole 128×128 W_τ would take 256 VGPRs on top of the job's state (spills), so a type job runs in
+// two passes over its units, each pass owning one 64-column half of the output (W half = 128 VGPRs); the cheap
+// layer 1 (one 16x16x32 MFMA per 16 columns) is recomputed per pass, the staged units are reused when they fit.
+constexpr int kHalfN = 4;   // 16-column MFMA tiles per half
+
+__device__ __forceinline__ void load_bfrags_split_half(const float* __restrict__ m, int h, bf16x8 (&bf)[kHalfN][4],
+                                                       bf16x8 (&bl)[kHalfN][4], int lane) {
+  const int j = lane & 15, kg = lane >> 4;
+#pragma unroll
+  for (int nn = 0; nn < kHalfN; ++nn)
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float* p = m + (size_t)(16 * (kHalfN * h + nn) + j) * kD + 32 * s + 8 * kg;
+      const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+      const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        bf[nn][s][jj] = dca::f2bf(v[jj]);
+        bl[nn][s][jj] = dca::f2bf(v[jj] - dca::bf2f(bf[nn][s][jj]));
+      }
+    }
+}
+
+// bf16x3 16×16 tile over K = 128: Σ_s a·w + al·w + a·wl (three chains)
+__device__ __forceinline__ f32x4 mfma3_k128(const bf16x8 (&a)[4], const bf16x8 (&al)[4], const bf16x8 (&w)[4],
+                                            const bf16x8 (&wl)[4]) {
+  f32x4 c = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f}, c2 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], w[s], c, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[s], w[s], c1, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[s], wl[s], c2, 0, 0, 0);
+  }
+  return c + (c1 + c2);
+}
+
+__global__ __launch_bounds__(256, 1) void encoder_fwd_f32_kernel(FwdParams P) {
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int rbase = blockIdx.x * kRows;
+  const int U = P.L.U, N = P.N;
+  float* const x896 = static_cast<float*>(P.x896);
+  float* const embo = static_cast<float*>(P.emb);
+  __shared__ __attribute__((aligned(16))) short scr[4][kImg];
+  __shared__ __attribute__((aligned(16))) short scl[4][kImg];
+  __shared__ __attribute__((aligned(16))) float ust[4][16 * kUP];
+
+  {   // env embedding (fp32 VALU)
+    const int r = tid >> 3, c0 = (tid & 7) * 16;
+    const int row = rbase + r;
+    if (row < N) {
+      const float e0 = P.env[row * 3], e1 = P.env[row * 3 + 1], e2 = P.env[row * 3 + 2];
+      for (int c = c0; c < c0 + 16; ++c) {
+        const float v = P.be[c] + P.we[c * 3] * e0 + P.we[c * 3 + 1] * e1 + P.we[c * 3 + 2] * e2;
+        x896[(size_t)row * 896 + c] = fmaxf(v, 0.f);
+      }
+    }
+  }
+
+  bf16x8 wb[8];
+  load_w1_split(P.w1, P.b1, wb, lane);
+  short* img = &scr[wv][0];
+  short* imgl = &scl[wv][0];
+  const int i = lane & 15, kg = lane >> 4;
+  for (int j = 0; j < 3; ++j) {
+    int tau, g;
+    type_job(wv, j, tau, g);
+    const int cnt = P.L.cnt[tau], uoff = P.L.off[tau];
+    if (cnt == 0) continue;
+    const int row0 = rbase + 16 * g;
+    float* ur = &ust[wv][0];
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 wf[kHalfN][4], wfl[kHalfN][4];
+      load_bfrags_split_half(static_cast<const float*>(P.wt) + (size_t)tau * kD * kD, h, wf, wfl, lane);
+      float btv[kHalfN];
+#pragma unroll
+      for (int nn = 0; nn < kHalfN; ++nn) btv[nn] = P.bt[tau * kD + 16 * (kHalfN * h + nn) + i];
+      f32x4 pmax[kHalfN];
+      int parg[kHalfN][4];
+#pragma unroll
+      for (int nn = 0; nn < kHalfN; ++nn) {
+        pmax[nn] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) parg[nn][r] = 0;
+      }
+      for (int c0 = 0; c0 < cnt; c0 += kStage) {
+        const int cc = min(kStage, cnt - c0);
+        if (h == 0 || cnt > kStage) {   // one chunk: the staged units of the first pass serve the second
+          __builtin_amdgcn_wave_barrier();
+          stage_units(P.units, nullptr, U, N, row0, uoff + c0, cc, ur, nullptr, lane);
+          __builtin_amdgcn_wave_barrier();
+        }
+        for (int uc = 0; uc < cc; ++uc) {
+          const int u = c0 + uc;
+          f32x4 acc[8];
+          layer1_split(ur, uc, wb, acc, lane);
+#pragma unroll
+          for (int n = 0; n < 8; ++n) {
+            f32x4 b;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) b[r] = fmaxf(acc[n][r], 0.f);
+            tile_put(img, n, b, lane);
+            tile_put_lo(imgl, n, b, lane);
+          }
+          __builtin_amdgcn_wave_barrier();
+          bf16x8 af[4], afl[4];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            af[s] = tile_frag(img, 32 * s, lane);
+            afl[s] = tile_frag(imgl, 32 * s, lane);
+          }
+#pragma unroll
+          for (int nn = 0; nn < kHalfN; ++nn) {
+            f32x4 c = mfma3_k128(af, afl, wf[nn], wfl[nn]);
+            const int n = kHalfN * h + nn;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float v = c[r] + btv[nn];
+              if (v > pmax[nn][r]) { pmax[nn][r] = v; parg[nn][r] = u; }
+              const int row = row0 + 4 * kg + r;
+              if (row < N) embo[((size_t)row * U + uoff + u) * kD + 16 * n + i] = v;
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+#pragma unroll
+      for (int nn = 0; nn < kHalfN; ++nn)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = row0 + kg * 4 + r;
+          if (row < N) {
+            const int col = 16 * (kHalfN * h + nn) + i;
+            x896[(size_t)row * 896 + kD + tau * kD + col] = pmax[nn][r];
+            P.arg[((size_t)row * 6 + tau) * kD + col] = (unsigned char)parg[nn][r];
+          }
+        }
+    }
+  }
+}
+
+// half of a K-blocked tile image (columns 64h … 64h+63 = chunks 128h … 128h+127)
+__device__ __forceinline__ void store_tile_half(const short* tw, short* dst, int h, int lane) {
+#pragma unroll
+  for (int q = 2 * h; q < 2 * h + 2; ++q) {
+    const int c = lane + 64 * q;
+    *reinterpret_cast<bf16x8*>(dst + c * 8) = *reinterpret_cast<const bf16x8*>(tw + toff(c >> 1, 8 * (c & 1)));
+  }
+}
+
+__global__ __launch_bounds__(256, 1) void encoder_bwd_f32_kernel(BwdParams P) {
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int rbase = blockIdx.x * kRows;
+  const int U = P.L.U, N = P.N;
+  const int i = lane & 15, kg = lane >> 4;
+  __shared__ __attribute__((aligned(16))) short tsc[4][kTile];
+  __shared__ __attribute__((aligned(16))) float ust[4][16 * kUP];
+  __shared__ float dst_[4][16 * kDP];
+  __shared__ float wred[kW1];
+  short* tw = &tsc[wv][0];
+
+  bf16x8 wb[8];
+  load_w1_split(P.w1, P.b1, wb, lane);
+  f32x4 dw1acc[8];
+  float db1acc[8];
+#pragma unroll
+  for (int n = 0; n < 8; ++n) {
+    dw1acc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    db1acc[n] = 0.f;
+  }
+  for (int e = tid; e < kW1; e += 256) wred[e] = 0.f;
+
+  for (int j = 0; j < 3; ++j) {
+    int tau, g;
+    type_job(wv, j, tau, g);
+    const int cnt = P.L.cnt[tau], uoff = P.L.off[tau];
+    if (cnt == 0) continue;
+    const int row0 = rbase + 16 * g;
+    if (row0 >= N) continue;
+    const int rb = row0 / 16;
+    const int arow = row0 + i;
+    const bool rok = arow < N;
+    const bool eth_dead = P.compat && tau == 5;
+    float* ur = &ust[wv][0];
+    float* dr = &dst_[wv][0];
+    for (int h = 0; h < 2; ++h) {
+      bf16x8 wf[kHalfN][4], wfl[kHalfN][4];   // B[k=e][n=j] = W_τ[e][j] for basic columns j of this half
+      load_bfrags_split_half(static_cast<const float*>(P.wtT) + (size_t)tau * kD * kD, h, wf, wfl, lane);
+      for (int c0 = 0; c0 < cnt; c0 += kStage) {
+        const int cc = min(kStage, cnt - c0);
+        if (h == 0 || cnt > kStage) {
+          __builtin_amdgcn_wave_barrier();
+          stage_units(P.units, P.dtl, U, N, row0, uoff + c0, cc, ur, dr, lane);
+          __builtin_amdgcn_wave_barrier();
+        }
+        for (int uc = 0; uc < cc; ++uc) {
+          const int u = c0 + uc;
+          const size_t blk = (size_t)(P.blkbase[tau] + (long long)u * P.NB + rb) * (kD * 16);
+          // ---- ∂emb (all 128 columns: the K of this half's ∂basic) = dtl·q + ∂pool at the argmax, split hi / lo
+          const float dtl = dr[i * kDP + uc];
+          bf16x8 de[4], del[4];
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const int e0 = 32 * s + 8 * kg;
+            float v[8];
+            if (rok) {
+              const float* qp = P.q + (size_t)arow * P.ldq + e0;
+              const float* dp = P.dx + (size_t)arow * 896 + kD + tau * kD + e0;
+              const unsigned char* ag = P.arg + ((size_t)arow * 6 + tau) * kD + e0;
+              const float4 qa = *reinterpret_cast<const float4*>(qp), qb = *reinterpret_cast<const float4*>(qp + 4);
+              const float4 da = *reinterpret_cast<const float4*>(dp), db = *reinterpret_cast<const float4*>(dp + 4);
+              const uint2 a8 = *reinterpret_cast<const uint2*>(ag);
+              const float qv[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
+              const float dv[8] = {da.x, da.y, da.z, da.w, db.x, db.y, db.z, db.w};
+#pragma unroll
+              for (int jj = 0; jj < 8; ++jj) {
+                const unsigned ab = ((jj < 4 ? a8.x : a8.y) >> (8 * (jj & 3))) & 0xffu;
+                v[jj] = dtl * qv[jj] + ((!eth_dead && ab == (unsigned)u) ? dv[jj] : 0.f);
+              }
+              if (P.compat && tau == 3) {   // eth pool = enh pool: its gradient lands on enh argmax units
+                const float* dp5 = P.dx + (size_t)arow * 896 + kD + 5 * kD + e0;
+#pragma unroll
+                for (int jj = 0; jj < 8; ++jj) {
+                  const unsigned ab = ((jj < 4 ? a8.x : a8.y) >> (8 * (jj & 3))) & 0xffu;
+                  v[jj] += (ab == (unsigned)u) ? dp5[jj] : 0.f;
+                }
+              }
+            } else {
+#pragma unroll
+              for (int jj = 0; jj < 8; ++jj) v[jj] = 0.f;
+            }
+#pragma unroll
+            for (int jj = 0; jj < 8; ++jj) {
+              de[s][jj] = dca::f2bf(v[jj]);
+              del[s][jj] = dca::f2bf(v[jj] - dca::bf2f(de[s][jj]));
+            }
+          }
+          if (h == 0) {   // ∂emb hi / lo images (whole tile) for the ∂W_τ GEMM
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+              for (int jj = 0; jj < 8; ++jj) tw[toff(32 * s + 8 * kg + jj, i)] = de[s][jj];
+            __builtin_amdgcn_wave_barrier();
+            store_tile(tw, P.demb + blk, lane);
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int s = 0; s < 4; ++s)
+#pragma unroll
+              for (int jj = 0; jj < 8; ++jj) tw[toff(32 * s + 8 * kg + jj, i)] = del[s][jj];
+            __builtin_amdgcn_wave_barrier();
+            store_tile(tw, P.demb_lo + blk, lane);
+            __builtin_amdgcn_wave_barrier();
+          }
+          // ---- layer 1 of this half's columns (recomputed, C layout) and ∂basic = ∂emb · W_τ, ReLU'
+          f32x4 bas[kHalfN], dbp[kHalfN];
+          {
+            const bf16x8 a = l1_afrag(ur, uc, lane);
+#pragma unroll
+            for (int nn = 0; nn < kHalfN; ++nn) {
+              const f32x4 l1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wb[kHalfN * h + nn],
+                                                                       f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+              for (int r = 0; r < 4; ++r) bas[nn][r] = fmaxf(l1[r], 0.f);
+            }
+          }
+#pragma unroll
+          for (int nn = 0; nn < kHalfN; ++nn) {
+            f32x4 c = mfma3_k128(de, del, wf[nn], wfl[nn]);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) c[r] = bas[nn][r] > 0.f ? c[r] : 0.f;
+            dbp[nn] = c;
+          }
+          // ---- ∂W1 rows of this half += ∂basicᵀ · units (16x16x16, bf16x3)
+          bf16x4 ub, ubl;
+          {
+            const int kk = lane & 15;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const float x = kk < kF ? ur[(4 * kg + r) * kUP + uc * kF + kk] : 0.f;
+              ub[r] = dca::f2bf(x);
+              ubl[r] = dca::f2bf(x - dca::bf2f(ub[r]));
+            }
+          }
+#pragma unroll
+          for (int nn = 0; nn < kHalfN; ++nn) {
+            const int n = kHalfN * h + nn;
+            bf16x4 a, al;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              a[r] = dca::f2bf(dbp[nn][r]);
+              al[r] = dca::f2bf(dbp[nn][r] - dca::bf2f(a[r]));
+              db1acc[n] += dbp[nn][r];
+            }
+            dw1acc[n] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, ub, dw1acc[n], 0, 0, 0);
+            dw1acc[n] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, ubl, dw1acc[n], 0, 0, 0);
+            dw1acc[n] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, ub, dw1acc[n], 0, 0, 0);
+          }
+          // ---- this half of the basic tile → hi / lo K-blocked images
+#pragma unroll
+          for (int nn = 0; nn < kHalfN; ++nn) {
+            bf16x4 v4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v4[r] = dca::f2bf(bas[nn][r]);
+            *reinterpret_cast<bf16x4*>(&tw[toff(16 * (kHalfN * h + nn) + i, 4 * kg)]) = v4;
+          }
+          __builtin_amdgcn_wave_barrier();
+          store_tile_half(tw, P.basic + blk, h, lane);
+          __builtin_amdgcn_wave_barrier();
+#pragma unroll
+          for (int nn = 0; nn < kHalfN; ++nn) {
+            bf16x4 v4;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v4[r] = bf_lo(bas[nn][r]);
+            *reinterpret_cast<bf16x4*>(&tw[toff(16 * (kHalfN * h + nn) + i, 4 * kg)]) = v4;
+          }
+          __builtin_amdgcn_wave_barrier();
+          store_tile_half(tw, P.basic_lo + blk, h, lane);
+          __builtin_amdgcn_wave_barrier();
+        }
+      }
+    }
+  }
+  for (int w = 0; w < 4; ++w) {
+    __syncthreads();
+    if (wv == w) {
+#pragma unroll
+      for (int n = 0; n < 8; ++n) {
+        const int k = lane & 15;
+        if (k < kF) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) wred[(16 * n + 4 * kg + r) * kF + k] += dw1acc[n][r];
+        }
+        float s = db1acc[n];
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        if (kg == 0) wred[kD * kF + 16 * n + i] += s;
+      }
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < kW1; e += 256) P.w1part[(size_t)blockIdx.x * kW1 + e] = wred[e];
+}
+
 // Fixed-order sum of the per-workgroup ∂W1‖∂b1 partials: block of 256 = 16 columns × 16 row phases (88 blocks;
 // 64 × 4 gave 22 blocks whose threads each walked ~90 partials: 23 µs, latency-bound).
 __global__ __launch_bounds__(256) void encoder_w1_reduce(const float* __restrict__ part, int nblk,
@@ -568,7 +927,10 @@ __device__ __forceinline__ void dwt_load(const short* __restrict__ A, const shor
   }
 }
 
+// F32: Al / Bl are the lo-half images; acc += a·b + al·b + a·bl (bf16x3)
+template <bool F32>
 __global__ __launch_bounds__(256, 2) void dwt_blocked_kernel(const short* __restrict__ A, const short* __restrict__ Bm,
+                                                             const short* __restrict__ Al, const short* __restrict__ Bl,
                                                              DwtJobs J, float* __restrict__ part) {
   const int job = blockIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int tau = 0;
@@ -582,15 +944,33 @@ __global__ __launch_bounds__(256, 2) void dwt_blocked_kernel(const short* __rest
 #pragma unroll
     for (int y = 0; y < 4; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 a[4], bb[4], an[4], bn[4];
+  bf16x8 al[4], bl[4], aln[4], bln[4];
   dwt_load(A, Bm, b0, bend, mq, nq, lane, a, bb);
+  if constexpr (F32) dwt_load(Al, Bl, b0, bend, mq, nq, lane, al, bl);
   for (long long b = b0; b < bend; b += 2) {
-    if (b + 2 < bend) dwt_load(A, Bm, b + 2, bend, mq, nq, lane, an, bn);
+    if (b + 2 < bend) {
+      dwt_load(A, Bm, b + 2, bend, mq, nq, lane, an, bn);
+      if constexpr (F32) dwt_load(Al, Bl, b + 2, bend, mq, nq, lane, aln, bln);
+    }
+    if constexpr (F32) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[x], bb[y], acc[x][y], 0, 0, 0);
+#pragma unroll
+      for (int x = 0; x < 4; ++x)
+#pragma unroll
+        for (int y = 0; y < 4; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[x], bl[y], acc[x][y], 0, 0, 0);
+    }
 #pragma unroll
     for (int x = 0; x < 4; ++x)
 #pragma unroll
       for (int y = 0; y < 4; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[x], bb[y], acc[x][y], 0, 0, 0);
 #pragma unroll
-    for (int t = 0; t < 4; ++t) { a[t] = an[t]; bb[t] = bn[t]; }
+    for (int t = 0; t < 4; ++t) {
+      a[t] = an[t]; bb[t] = bn[t];
+      if constexpr (F32) { al[t] = aln[t]; bl[t] = bln[t]; }
+    }
   }
   // tile-linear partial: ((wave·16 + 4x + y)·64 + lane)·4 + r
   float* dst = part + (size_t)job * (kD * kD) + (size_t)wv * 16 * 256;
@@ -621,16 +1001,18 @@ __global__ __launch_bounds__(256) void dwt_reduce(const float* __restrict__ part
 
 }  // namespace
 
+// f32 = 1: wt fp32, x896 / emb fp32 (bf16x3 layer 2); f32 = 0: wt, x896, emb bf16
 extern "C" hipError_t dca_encoder_fwd(const float* units, const float* env, const float* w1, const float* b1,
-                                      const short* wt, const float* bt, const float* we, const float* be, short* x896,
-                                      short* emb, unsigned char* arg, int N, int U, const int* counts, int compat,
-                                      hipStream_t st) {
+                                      const void* wt, const float* bt, const float* we, const float* be, void* x896,
+                                      void* emb, unsigned char* arg, int N, int U, const int* counts, int compat,
+                                      hipStream_t st, int f32) {
   FwdParams P{units, env, w1, b1, wt, bt, we, be, x896, emb, arg, N, compat, {}};
   P.L.U = U;
   int acc = 0;
   for (int t = 0; t < 6; ++t) { P.L.cnt[t] = counts[t]; P.L.off[t] = acc; acc += counts[t]; }
   if (acc != U || U > 64) return hipErrorInvalidValue;
-  encoder_fwd_kernel<<<(N + kRows - 1) / kRows, 256, 0, st>>>(P);
+  if (f32) encoder_fwd_f32_kernel<<<(N + kRows - 1) / kRows, 256, 0, st>>>(P);
+  else encoder_fwd_kernel<<<(N + kRows - 1) / kRows, 256, 0, st>>>(P);
   return hipGetLastError();
 }
 
@@ -650,23 +1032,24 @@ void dwt_plan(int N, const int* counts, DwtJobs& J, int& NB) {
 }
 }  // namespace
 
-// Workspace: ∂W1 partials ‖ K-blocked ∂emb and basic images (bf16) ‖ ∂W_τ split-K partials.
-extern "C" size_t dca_encoder_bwd_workspace(int N, int U, const int* counts) {
+// Workspace: ∂W1 partials ‖ K-blocked ∂emb and basic images (bf16; F32: hi and lo of each) ‖ ∂W_τ split-K partials.
+extern "C" size_t dca_encoder_bwd_workspace(int N, int U, const int* counts, int f32) {
   DwtJobs J;
   int NB;
   dwt_plan(N, counts, J, NB);
   const size_t w1 = (size_t)((N + kRows - 1) / kRows) * kW1 * sizeof(float);
   const size_t img = (size_t)U * NB * kD * 16 * sizeof(short);
   const size_t parts = (size_t)J.jbase[6] * kD * kD * sizeof(float);
-  return w1 + 2 * img + parts;
+  return w1 + (f32 ? 4 : 2) * img + parts;
 }
 
-extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const float* b1, const short* wtT,
+extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const float* b1, const void* wtT,
                                       const float* dtl, const float* q, int ldq, const float* dx,
                                       const unsigned char* arg, float* dwt, float* dw1, float* db1, void* ws,
                                       size_t ws_bytes, int N, int U, const int* counts, int compat, hipStream_t st,
-                                      const short* demb_in) {
-  if (ws_bytes < dca_encoder_bwd_workspace(N, U, counts)) return hipErrorInvalidValue;
+                                      const short* demb_in, int f32) {
+  if (ws_bytes < dca_encoder_bwd_workspace(N, U, counts, f32)) return hipErrorInvalidValue;
+  if (f32 && demb_in) return hipErrorInvalidValue;
   DwtJobs J;
   int NB;
   dwt_plan(N, counts, J, NB);
@@ -677,8 +1060,11 @@ extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const
   const size_t img = (size_t)U * NB * kD * 16;
   short* demb = reinterpret_cast<short*>(p);
   short* basic = demb + img;
-  float* parts = reinterpret_cast<float*>(basic + img);
-  BwdParams P{units, w1, b1, wtT, dtl, q, ldq, dx, arg, demb, basic, w1part, N, compat, {}, {}, NB, demb_in};
+  short* demb_lo = f32 ? basic + img : nullptr;
+  short* basic_lo = f32 ? demb_lo + img : nullptr;
+  float* parts = reinterpret_cast<float*>(basic + (f32 ? 3 : 1) * img);
+  BwdParams P{units, w1, b1, wtT, dtl, q, ldq, dx, arg, demb, basic, demb_lo, basic_lo, w1part, N, compat, {}, {},
+              NB, demb_in};
   P.L.U = U;
   int acc = 0;
   for (int t = 0; t < 6; ++t) {
@@ -688,9 +1074,13 @@ extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const
     acc += counts[t];
   }
   if (acc != U || U > 64) return hipErrorInvalidValue;
-  encoder_bwd_kernel<<<nblk, 256, 0, st>>>(P);
+  if (f32) encoder_bwd_f32_kernel<<<nblk, 256, 0, st>>>(P);
+  else encoder_bwd_kernel<<<nblk, 256, 0, st>>>(P);
   encoder_w1_reduce<<<(kW1 + 15) / 16, 256, 0, st>>>(w1part, nblk, dw1, db1);
-  if (J.jbase[6] > 0) dwt_blocked_kernel<<<J.jbase[6], 256, 0, st>>>(demb, basic, J, parts);
+  if (J.jbase[6] > 0) {
+    if (f32) dwt_blocked_kernel<true><<<J.jbase[6], 256, 0, st>>>(demb, basic, demb_lo, basic_lo, J, parts);
+    else dwt_blocked_kernel<false><<<J.jbase[6], 256, 0, st>>>(demb, basic, nullptr, nullptr, J, parts);
+  }
   dwt_reduce<<<dim3(kD * kD / 64, 6), 256, 0, st>>>(parts, J, dwt);
   return hipGetLastError();
 }

@@ -1,4 +1,4 @@
-// Split-K bf16 "TN" GEMM for the learner's weight gradients (gfx950 MFMA): C[M×N] (+)= Aᵀ·B with
+// Split-K "TN" GEMM for the learner's weight gradients (gfx950 MFMA): C[M×N] (+)= Aᵀ·B with
 //   A (K×M) bf16 row-major (row stride lda) — e.g. ∂gates (B·S rows × 4H),
 //   B (K×N) bf16 row-major (row stride ldb) — e.g. h_{t-1} / x (B·S rows × H),
 // i.e. both operands are K-OUTER: the reduction runs over the B·S = 11 200 rows of a minibatch. hipBLASLt picks a
@@ -20,6 +20,11 @@
 //   the four 1v1 weight gradients (the register-staged loads overlap the MFMAs better at this K-slab depth).
 // * B may be "row-split": rows k < split come from B0 (e.g. h0), rows ≥ split from B shifted by `split` rows —
 //   the LSTM's h_{t-1} operand without materialising the concatenation.
+// * fp32 operands (the learner's fp32-accurate mode): "bf16x3" — every value is split once while staging, x = hi +
+//   lo (two bf16), into a hi and a lo LDS image, and Aᵀ·B ≈ hiᵀ·hi + loᵀ·hi + hiᵀ·lo on the bf16 MFMA (the dropped
+//   lo·lo term and the lo rounding are ≈2⁻¹⁶ relative per product; fp32 accumulation). 3× the bf16 MFMA work is
+//   still ≈5× the exact-f32 MFMA rate (v_mfma_f32_16x16x4_f32 runs at 1/16 of bf16). 32-row K slabs keep the four
+//   images of a stage within the bf16 kernel's 64 KB of LDS.
 #include "common.h"
 
 namespace {
@@ -37,9 +42,9 @@ __device__ __forceinline__ int lds_off(int row, int ch) {   // byte offset of 16
 }
 
 struct Args {
-  const short* A; int lda;
-  const short* B; int ldb;
-  const short* B0; int split;
+  const void* A; int lda;
+  const void* B; int ldb;
+  const void* B0; int split;
   float* C; int ldc;
   const int* perm;      // optional output row map (C row perm[m] receives result row m)
   float* slab;          // [splits][M][N] fp32 partials (splits > 1), then [splits][M] column-sum partials
@@ -47,9 +52,11 @@ struct Args {
   int M, N, K, kc, splits, tiles_n, accumulate;
 };
 
+// ---- bf16 operands: 64-row K slabs, one image per operand -------------------------------------------------------
 __device__ __forceinline__ void load_stage(const Args& a, int kbase, int kend, int m_base, int n_base,
                                            uint4 (&ra)[4], uint4 (&rb)[4]) {
   const int t = threadIdx.x, ch = t & 15;
+  const short* A = static_cast<const short*>(a.A);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int r = (t >> 4) + 16 * i;
@@ -57,10 +64,11 @@ __device__ __forceinline__ void load_stage(const Args& a, int kbase, int kend, i
     uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
     if (k < kend) {
       const int m = m_base + ch * 8;
-      if (m < a.M) va = *reinterpret_cast<const uint4*>(a.A + (size_t)k * a.lda + m);
+      if (m < a.M) va = *reinterpret_cast<const uint4*>(A + (size_t)k * a.lda + m);
       const int n = n_base + ch * 8;
       if (n < a.N) {
-        const short* bp = (k < a.split) ? a.B0 + (size_t)k * a.ldb : a.B + (size_t)(k - a.split) * a.ldb;
+        const short* bp = (k < a.split) ? static_cast<const short*>(a.B0) + (size_t)k * a.ldb
+                                        : static_cast<const short*>(a.B) + (size_t)(k - a.split) * a.ldb;
         vb = *reinterpret_cast<const uint4*>(bp + n);
       }
     }
@@ -92,6 +100,79 @@ __device__ __forceinline__ void colsum_acc(float (&cs)[8], const uint4 (&ra)[4])
   }
 }
 
+// ---- fp32 operands ("bf16x3": x = hi + lo, Aᵀ·B ≈ hiᵀhi + loᵀhi + hiᵀlo, ≈2⁻¹⁶ relative per product, f32
+// accumulation): 32-row K slabs, every fp32 value split once while staging into a hi and a lo image ---------------
+struct F32Stage {
+  float4 a[2][2], b[2][2];   // [row i][half]: 8 consecutive columns of one K row
+};
+
+__device__ __forceinline__ void load_stage_f32(const Args& a, int kbase, int kend, int m_base, int n_base,
+                                               F32Stage& r) {
+  const int t = threadIdx.x, ch = t & 15;
+  const float* A = static_cast<const float*>(a.A);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int k = kbase + (t >> 4) + 16 * i;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    r.a[i][0] = r.a[i][1] = r.b[i][0] = r.b[i][1] = z;
+    if (k < kend) {
+      const int m = m_base + ch * 8;
+      if (m < a.M) {
+        const float4* p = reinterpret_cast<const float4*>(A + (size_t)k * a.lda + m);
+        r.a[i][0] = p[0];
+        r.a[i][1] = p[1];
+      }
+      const int n = n_base + ch * 8;
+      if (n < a.N) {
+        const float* bp = (k < a.split) ? static_cast<const float*>(a.B0) + (size_t)k * a.ldb
+                                        : static_cast<const float*>(a.B) + (size_t)(k - a.split) * a.ldb;
+        const float4* p = reinterpret_cast<const float4*>(bp + n);
+        r.b[i][0] = p[0];
+        r.b[i][1] = p[1];
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ unsigned pack_bf2(float x, float y) {
+  return (unsigned)(unsigned short)dca::f2bf(x) | ((unsigned)(unsigned short)dca::f2bf(y) << 16);
+}
+
+// 8 floats → (hi, lo) bf16 chunks
+__device__ __forceinline__ void split8(const float4& p, const float4& q, uint4& hi, uint4& lo) {
+  const float v[8] = {p.x, p.y, p.z, p.w, q.x, q.y, q.z, q.w};
+  float l[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) l[j] = v[j] - dca::bf2f(dca::f2bf(v[j]));
+  hi = make_uint4(pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7]));
+  lo = make_uint4(pack_bf2(l[0], l[1]), pack_bf2(l[2], l[3]), pack_bf2(l[4], l[5]), pack_bf2(l[6], l[7]));
+}
+
+// images of one stage: A hi | A lo | B hi | B lo, 32 rows × 256 B each
+constexpr int kImgF32 = 32 * 256;
+__device__ __forceinline__ void store_stage_f32(char* S, const F32Stage& r) {
+  const int t = threadIdx.x, ch = t & 15;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = (t >> 4) + 16 * i;
+    uint4 hi, lo;
+    split8(r.a[i][0], r.a[i][1], hi, lo);
+    *reinterpret_cast<uint4*>(S + lds_off(row, ch)) = hi;
+    *reinterpret_cast<uint4*>(S + kImgF32 + lds_off(row, ch)) = lo;
+    split8(r.b[i][0], r.b[i][1], hi, lo);
+    *reinterpret_cast<uint4*>(S + 2 * kImgF32 + lds_off(row, ch)) = hi;
+    *reinterpret_cast<uint4*>(S + 3 * kImgF32 + lds_off(row, ch)) = lo;
+  }
+}
+
+__device__ __forceinline__ void colsum_acc_f32(float (&cs)[8], const F32Stage& r) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    cs[0] += r.a[i][0].x; cs[1] += r.a[i][0].y; cs[2] += r.a[i][0].z; cs[3] += r.a[i][0].w;
+    cs[4] += r.a[i][1].x; cs[5] += r.a[i][1].y; cs[6] += r.a[i][1].z; cs[7] += r.a[i][1].w;
+  }
+}
+
 // 16x16x32 operand fragment (k = 8·(lane>>4) + j, column c0 + (lane&15)) from a [k][128] swizzled image via two
 // transposed reads (rows k0 + 8g + 4r + q, columns c0 + 4p … 4p+3).
 __device__ __forceinline__ bf16x8 frag_tr(const char* img, int k0, int c0) {
@@ -109,10 +190,14 @@ __device__ __forceinline__ bf16x8 frag_tr(const char* img, int k0, int c0) {
   return f;
 }
 
+template <bool F32>
 __global__ __launch_bounds__(kThreads) void gemm_tn_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  constexpr int BKx = F32 ? 32 : BK;
+  // bf16: [A0 | A1 | B0 | B1] 16 KB images; F32: [stage0: Ahi Alo Bhi Blo | stage1: …] 8 KB images
 #define AS(b) (smem + (b) * kTileBytes)
 #define BS(b) (smem + (2 + (b)) * kTileBytes)
+#define SF(b) (smem + (b) * 4 * kImgF32)
   const int tile = blockIdx.x, split = blockIdx.y;
   const int tm = tile / a.tiles_n, tn = tile % a.tiles_n;
   const int m_base = tm * BM, n_base = tn * BN;
@@ -126,34 +211,74 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_kernel(Args a) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   uint4 ra[4], rb[4];
+  F32Stage rf;
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const bool do_cs = a.colsum != nullptr && tn == 0;
   int buf = 0;
   if (k_lo < k_hi) {
-    load_stage(a, k_lo, k_hi, m_base, n_base, ra, rb);
-    store_stage(AS(0), BS(0), ra, rb);
-    if (do_cs) colsum_acc(cs, ra);
+    if constexpr (F32) {
+      load_stage_f32(a, k_lo, k_hi, m_base, n_base, rf);
+      store_stage_f32(SF(0), rf);
+      if (do_cs) colsum_acc_f32(cs, rf);
+    } else {
+      load_stage(a, k_lo, k_hi, m_base, n_base, ra, rb);
+      store_stage(AS(0), BS(0), ra, rb);
+      if (do_cs) colsum_acc(cs, ra);
+    }
   }
   __syncthreads();
-  for (int kb = k_lo; kb < k_hi; kb += BK) {
-    const bool more = kb + BK < k_hi;
-    if (more) load_stage(a, kb + BK, k_hi, m_base, n_base, ra, rb);   // in flight during the MFMAs
+  for (int kb = k_lo; kb < k_hi; kb += BKx) {
+    const bool more = kb + BKx < k_hi;
+    if constexpr (F32) {
+      if (more) load_stage_f32(a, kb + BKx, k_hi, m_base, n_base, rf);   // in flight during the MFMAs
+      const char* S = SF(buf);
+      bf16x8 fah[4], fal[4], fbh[4], fbl[4];
 #pragma unroll
-    for (int ks = 0; ks < BK / 32; ++ks) {
-      bf16x8 fa[4], fb[4];
+      for (int i = 0; i < 4; ++i) {
+        fah[i] = frag_tr(S, 0, wm * 64 + i * 16);
+        fal[i] = frag_tr(S + kImgF32, 0, wm * 64 + i * 16);
+      }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = frag_tr(AS(buf), ks * 32, wm * 64 + i * 16);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = frag_tr(BS(buf), ks * 32, wn * 64 + j * 16);
+      for (int j = 0; j < 4; ++j) {
+        fbh[j] = frag_tr(S + 2 * kImgF32, 0, wn * 64 + j * 16);
+        fbl[j] = frag_tr(S + 3 * kImgF32, 0, wn * 64 + j * 16);
+      }
+      // small terms first, the hi·hi product last (16 independent accumulators interleave the chains)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-    }
-    if (more) {
-      store_stage(AS(buf ^ 1), BS(buf ^ 1), ra, rb);
-      if (do_cs) colsum_acc(cs, ra);
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fal[i], fbh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fah[i], fbl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fah[i], fbh[j], acc[i][j], 0, 0, 0);
+      if (more) {
+        store_stage_f32(SF(buf ^ 1), rf);
+        if (do_cs) colsum_acc_f32(cs, rf);
+      }
+    } else {
+      if (more) load_stage(a, kb + BK, k_hi, m_base, n_base, ra, rb);   // in flight during the MFMAs
+#pragma unroll
+      for (int ks = 0; ks < BK / 32; ++ks) {
+        bf16x8 fa[4], fb[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[i] = frag_tr(AS(buf), ks * 32, wm * 64 + i * 16);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb[j] = frag_tr(BS(buf), ks * 32, wn * 64 + j * 16);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+      if (more) {
+        store_stage(AS(buf ^ 1), BS(buf ^ 1), ra, rb);
+        if (do_cs) colsum_acc(cs, ra);
+      }
     }
     __syncthreads();
     buf ^= 1;
@@ -212,6 +337,7 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_kernel(Args a) {
     }
 #undef AS
 #undef BS
+#undef SF
 }
 
 // Fixed-order (deterministic) sum of the split-K slabs, optional row map / accumulate. A block of 256 threads owns
@@ -294,29 +420,32 @@ __global__ __launch_bounds__(256) void gemm_tn_reduce(const float* __restrict__ 
 
 }  // namespace
 
-extern "C" void dca_gemm_tn_plan(int M, int N, int K, int* splits, int* kc, int* tiles) {
+extern "C" void dca_gemm_tn_plan(int M, int N, int K, int* splits, int* kc, int* tiles, int f32) {
+  const int bk = f32 ? 32 : BK;
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   const int t = tm * tn;
   int s = (384 + t - 1) / t;                              // aim at ≈1.5 workgroups per CU
-  const int kmax = (K + BK - 1) / BK;                     // at least one 64-row slab per split
+  const int kmax = (K + bk - 1) / bk;                     // at least one K slab per split
   if (s > kmax) s = kmax;
   if (s < 1) s = 1;
   int c = (K + s - 1) / s;
-  c = (c + BK - 1) / BK * BK;
+  c = (c + bk - 1) / bk * bk;
   s = (K + c - 1) / c;
   *splits = s;
   *kc = c;
   *tiles = t;
 }
 
-extern "C" hipError_t dca_gemm_tn(const short* A, int lda, const short* B, int ldb, const short* B0, int split_rows,
+// f32 = 0: A, B, B0 bf16; f32 = 1: fp32 operands (bf16x3 split MFMA)
+extern "C" hipError_t dca_gemm_tn(const void* A, int lda, const void* B, int ldb, const void* B0, int split_rows,
                                   float* C, int ldc, const int* perm, int accumulate, int M, int N, int K, float* slab,
-                                  float* colsum, hipStream_t st) {
+                                  float* colsum, hipStream_t st, int f32) {
   int splits, kc, tiles;
-  dca_gemm_tn_plan(M, N, K, &splits, &kc, &tiles);
+  dca_gemm_tn_plan(M, N, K, &splits, &kc, &tiles, f32);
   Args a{A, lda, B, ldb, B0 ? B0 : B, B0 ? split_rows : 0, C, ldc, perm, slab, colsum, M, N, K, kc, splits,
          (N + BN - 1) / BN, accumulate};
-  hipLaunchKernelGGL(gemm_tn_kernel, dim3(tiles, splits), dim3(kThreads), 4 * kTileBytes, st, a);
+  if (f32) hipLaunchKernelGGL(gemm_tn_kernel<true>, dim3(tiles, splits), dim3(kThreads), 8 * kImgF32, st, a);
+  else hipLaunchKernelGGL(gemm_tn_kernel<false>, dim3(tiles, splits), dim3(kThreads), 4 * kTileBytes, st, a);
   DCA_CHECK_LAUNCH();
   if (splits > 1) {
     int lp = 0;

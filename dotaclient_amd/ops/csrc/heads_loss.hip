@@ -6,7 +6,7 @@
 // batch loss w.r.t. every head input in the same pass (no autograd graph, no masked_select, no host sync):
 //
 //   z   (N, ldz) f32 : [ q (128) | enum (3) | x (9) | y (9) | value (1) | pad ]  (output of ONE heads GEMM)
-//   emb (N, U, 128) bf16 : unit embeddings (pointer keys)
+//   emb (N, U, 128) bf16 : unit embeddings (pointer keys); fp32 in the F32 variant (the learner's fp32 mode)
 //   dz  (N, ldz) f32 : ∂L/∂z   (dq in cols 0..127, d logits, dV)  → feeds the heads GEMM backward
 //   dtl (N, U)  f32  : ∂L/∂(target logits)                         → ∂L/∂emb = dtl ⊗ q (encoder backward)
 //   part(nblk, 16)   : per-block partial sums of the loss terms / metrics (reduced on the host side)
@@ -25,7 +25,7 @@ constexpr int kNPart = 16;
 
 struct Params {
   const float* z; int ldz;
-  const short* emb;
+  const void* emb;
   const unsigned char* act; const unsigned char* msk; int A;
   const float* adv; const float* ret; const float* logp_old; const float* nret;
   const float* norms;
@@ -54,6 +54,7 @@ __device__ __forceinline__ void head_lsm(float logit, bool m, int lane, int W, f
   p = (in && m) ? __expf(logp) : 0.f;
 }
 
+template <bool F32>
 __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int n = blockIdx.x * kRowsPerBlock + wv;
@@ -89,12 +90,24 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
     const unsigned char a0 = ar[min(lane, P.A - 1)], a1 = ar[min(lane + 64, P.A - 1)];
     const unsigned char m0 = mr[min(lane, P.A - 1)], m1 = mr[min(lane + 64, P.A - 1)];
     constexpr int kMaxIt = 16;   // U ≤ 64
-    dca::bf16x8 e8[kMaxIt];
+    // the row's unit embeddings, 8 features per lane and 4 units per wave-instruction, all loads issued up front
+    float e8[kMaxIt][8];
     const int nit = (U + 3) >> 2;
-    const short* er = P.emb + (size_t)n * U * kQ;
 #pragma unroll
     for (int it = 0; it < kMaxIt; ++it)
-      if (it < nit) e8[it] = *reinterpret_cast<const dca::bf16x8*>(er + (size_t)min(it * 4 + ug, U - 1) * kQ + 8 * ks);
+      if (it < nit) {
+        const size_t o = ((size_t)n * U + min(it * 4 + ug, U - 1)) * kQ + 8 * ks;
+        if constexpr (F32) {
+          const float4 a = *reinterpret_cast<const float4*>(static_cast<const float*>(P.emb) + o);
+          const float4 b = *reinterpret_cast<const float4*>(static_cast<const float*>(P.emb) + o + 4);
+          e8[it][0] = a.x; e8[it][1] = a.y; e8[it][2] = a.z; e8[it][3] = a.w;
+          e8[it][4] = b.x; e8[it][5] = b.y; e8[it][6] = b.z; e8[it][7] = b.w;
+        } else {
+          const dca::bf16x8 h = *reinterpret_cast<const dca::bf16x8*>(static_cast<const short*>(P.emb) + o);
+#pragma unroll
+          for (int j = 0; j < 8; ++j) e8[it][j] = dca::bf2f(h[j]);
+        }
+      }
     if (lane < 32) s_zl[wv][lane] = zl;
     s_act[wv][lane] = a0; s_act[wv][lane + 64] = a1;
     s_msk[wv][lane] = m0; s_msk[wv][lane + 64] = m1;
@@ -105,7 +118,7 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
         const int u = it * 4 + ug;
         float d = 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) d += q8[j] * dca::bf2f(e8[it][j]);
+        for (int j = 0; j < 8; ++j) d += q8[j] * e8[it][j];
         d = dca::group_sum<16>(d);
         if (ks == 0 && u < U) s_tl[wv][u] = d;
       }
@@ -203,7 +216,7 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
         const int u = it * 4 + ug;
         const float g = (u < U) ? s_dtl[wv][u] : 0.f;
 #pragma unroll
-        for (int j = 0; j < 8; ++j) dq[j] += g * dca::bf2f(e8[it][j]);
+        for (int j = 0; j < 8; ++j) dq[j] += g * e8[it][j];
       }
     }
 #pragma unroll
@@ -242,15 +255,17 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
 
 extern "C" int dca_heads_loss_nblocks(int N) { return (N + kRowsPerBlock - 1) / kRowsPerBlock; }
 
-extern "C" hipError_t dca_heads_loss(const float* z, int ldz, const short* emb, const unsigned char* act,
+// emb_f32 = 1: emb is (N, U, 128) fp32, else bf16
+extern "C" hipError_t dca_heads_loss(const float* z, int ldz, const void* emb, const unsigned char* act,
                                      const unsigned char* msk, int A, const float* adv, const float* ret,
                                      const float* logp_old, const float* nret, const float* norms, float* dz,
                                      float* dtl, float* part, float* logp_out, int N, int U, int algo,
                                      int compat_value_bug, int S_bug, int B_bug, float clip_eps, float ent_coef,
-                                     float vf_coef, hipStream_t st, short* dz16) {
+                                     float vf_coef, hipStream_t st, short* dz16, int emb_f32) {
   if (U > 64 || U < 1 || ldz < kQ + 22 || A != 21 + U) return hipErrorInvalidValue;
   Params P{z, ldz, emb, act, msk, A, adv, ret, logp_old, nret, norms, dz, dtl, part, logp_out, dz16, N, U, algo,
            compat_value_bug, S_bug, B_bug, clip_eps, ent_coef, vf_coef};
-  heads_loss_kernel<<<dca_heads_loss_nblocks(N), 256, 0, st>>>(P);
+  if (emb_f32) heads_loss_kernel<true><<<dca_heads_loss_nblocks(N), 256, 0, st>>>(P);
+  else heads_loss_kernel<false><<<dca_heads_loss_nblocks(N), 256, 0, st>>>(P);
   return hipGetLastError();
 }

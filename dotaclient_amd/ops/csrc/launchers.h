@@ -23,33 +23,33 @@ hipError_t dca_lstm_bwd(const float* dhs, const float* gates, const float* cs, c
                         unsigned long long* trace = nullptr);
 
 int dca_heads_loss_nblocks(int N);
-hipError_t dca_heads_loss(const float* z, int ldz, const short* emb, const unsigned char* act, const unsigned char* msk,
+hipError_t dca_heads_loss(const float* z, int ldz, const void* emb, const unsigned char* act, const unsigned char* msk,
                           int A, const float* adv, const float* ret, const float* logp_old, const float* nret,
                           const float* norms, float* dz, float* dtl, float* part, float* logp_out, int N, int U,
                           int algo, int compat_value_bug, int S_bug, int B_bug, float clip_eps, float ent_coef,
-                          float vf_coef, hipStream_t st, short* dz16 = nullptr);
+                          float vf_coef, hipStream_t st, short* dz16, int emb_f32);
 
-hipError_t dca_encoder_fwd(const float* units, const float* env, const float* w1, const float* b1, const short* wt,
-                           const float* bt, const float* we, const float* be, short* x896, short* emb,
-                           unsigned char* arg, int N, int U, const int* counts, int compat, hipStream_t st);
-size_t dca_encoder_bwd_workspace(int N, int U, const int* counts);
-hipError_t dca_encoder_bwd(const float* units, const float* w1, const float* b1, const short* wtT, const float* dtl,
+hipError_t dca_encoder_fwd(const float* units, const float* env, const float* w1, const float* b1, const void* wt,
+                           const float* bt, const float* we, const float* be, void* x896, void* emb,
+                           unsigned char* arg, int N, int U, const int* counts, int compat, hipStream_t st, int f32);
+size_t dca_encoder_bwd_workspace(int N, int U, const int* counts, int f32);
+hipError_t dca_encoder_bwd(const float* units, const float* w1, const float* b1, const void* wtT, const float* dtl,
                            const float* q, int ldq, const float* dx, const unsigned char* arg, float* dwt, float* dw1,
                            float* db1, void* ws, size_t ws_bytes, int N, int U, const int* counts, int compat,
-                           hipStream_t st, const short* demb_in = nullptr);
+                           hipStream_t st, const short* demb_in, int f32);
 
 size_t dca_lstm_team_ctl_bytes();
-size_t dca_lstm_team_workspace(int B, int H, int backward);
-hipError_t dca_lstm_team_fwd(const float* xp4, const short* whh, const float* h0, const float* c0, short* hs,
+size_t dca_lstm_team_workspace(int B, int H, int backward, int f32);
+hipError_t dca_lstm_team_fwd(const float* xp4, const void* whh, const float* h0, const float* c0, short* hs,
                              float* hsf, float* cs, float* gates4, float* hn, float* cn, void* ctl, void* ws,
                              size_t ws_bytes, unsigned* err, int B, int S, int H, int time_major, hipStream_t st,
-                             unsigned long long* trace = nullptr, const float* bias4 = nullptr);
-int dca_lstm_team_chains(int B);
+                             unsigned long long* trace, const float* bias4, int f32);
+int dca_lstm_team_chains(int B, int f32);
 hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, const float* cs, const float* c0,
-                             const float* dhn, const float* dcn, const short* whh, float* dgates4, float* dh0,
+                             const float* dhn, const float* dcn, const void* whh, float* dgates4, float* dh0,
                              float* dc0, void* ctl, void* ws, size_t ws_bytes, unsigned* err, int B, int S, int H,
-                             int time_major, hipStream_t st, unsigned long long* trace = nullptr,
-                             short* dg16 = nullptr, float* dbpart = nullptr);
+                             int time_major, hipStream_t st, unsigned long long* trace, short* dg16, float* dbpart,
+                             int f32);
 
 hipError_t dca_sample_actions(const float* z, int ldz, const short* emb, const long long* handles, int N, int U,
                               unsigned long long seed, const long long* ctr, int* idx, unsigned char* act,
@@ -70,10 +70,10 @@ hipError_t dca_loss_assemble(const float* part, int nrows, const float* norms, i
 hipError_t dca_weight_prep(const float* src, const int* map16, short* dst16, int n16, const int* map32, float* dst32,
                            int n32, hipStream_t st);
 
-void dca_gemm_tn_plan(int M, int N, int K, int* splits, int* kc, int* tiles);
-hipError_t dca_gemm_tn(const short* A, int lda, const short* B, int ldb, const short* B0, int split_rows, float* C,
+void dca_gemm_tn_plan(int M, int N, int K, int* splits, int* kc, int* tiles, int f32);
+hipError_t dca_gemm_tn(const void* A, int lda, const void* B, int ldb, const void* B0, int split_rows, float* C,
                        int ldc, const int* perm, int accumulate, int M, int N, int K, float* slab, float* colsum,
-                       hipStream_t st);
+                       hipStream_t st, int f32);
 
 int dca_enc_small_out();
 int dca_enc_small_blocks();

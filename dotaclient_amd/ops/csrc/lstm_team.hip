@@ -89,6 +89,17 @@ __device__ __forceinline__ unsigned add_agent(unsigned* p, unsigned v) {
 }
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// 8 consecutive fp32 values → hi / lo bf16 fragments (x = hi + lo up to ≈2⁻¹⁷ relative)
+__device__ __forceinline__ void split_frag(const float* __restrict__ p, bf16x8& hi, bf16x8& lo) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    hi[j] = dca::f2bf(v[j]);
+    lo[j] = dca::f2bf(v[j] - dca::bf2f(hi[j]));
+  }
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, int bytes) {
   const unsigned long long a = (unsigned long long)p;
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
@@ -212,9 +223,9 @@ __device__ __forceinline__ unsigned make_tagbase(unsigned epoch, unsigned iter) 
 // Forward. MT = 16-row batch tiles per chain (Bc ≤ 16·MT), KS = H/128.
 // xg (per team): [2 parity][Bc][H/2] u64 granules {lo: 2×bf16 h, hi: tag}
 // =============================================================================================================
-template <int MT, int KS>
+template <int MT, int KS, bool F32>
 __device__ __forceinline__ void lstm_team_fwd_body(
-    const float* __restrict__ xp4, const short* __restrict__ whh, const float* __restrict__ h0,
+    const float* __restrict__ xp4, const void* __restrict__ whh_, const float* __restrict__ h0,
     const float* __restrict__ c0, short* __restrict__ hs, float* __restrict__ hsf, float* __restrict__ cs,
     float* __restrict__ gates4, float* __restrict__ hn, float* __restrict__ cn, unsigned long long* xg_all,
     TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st, unsigned long long* trace,
@@ -226,6 +237,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
   constexpr int HP = H + 8;             // LDS row pitch (bf16)
   constexpr int RB = MT * 16;
   __shared__ short hl[2][RB][HP];
+  __shared__ short hlo[F32 ? 2 : 1][F32 ? RB : 1][F32 ? HP : 1];   // F32: lo bf16 half of h (h = hi + lo)
   __shared__ int sh_int;
   __shared__ unsigned sh_epoch;
 
@@ -238,20 +250,33 @@ __device__ __forceinline__ void lstm_team_fwd_body(
 #define TSTAMP(ev)                                                                                        \
   if (trace && lane == 0 && chain == 0 && t < 64)                                                          \
     trace[(((size_t)m * 4 + wv) * 64 + t) * 8 + (ev)] = __builtin_amdgcn_s_memrealtime()
-  unsigned long long* xg = xg_all + (size_t)team * 2 * Bc * (H / 2);
+  // granules per row: bf16 h → H/2 (2 units each), F32 h → H (one unit each)
+  constexpr int GPR = F32 ? H : H / 2;
+  unsigned long long* xg = xg_all + (size_t)team * 2 * Bc * GPR;
 
   // zero the padding rows of both h buffers once
   for (int i = tid; i < 2 * RB * HP; i += kThreads) (&hl[0][0][0])[i] = 0;
+  if constexpr (F32)
+    for (int i = tid; i < 2 * RB * HP; i += kThreads) (&hlo[0][0][0])[i] = 0;
 
   // W_hh slice for this wave's tile: columns c = 4·ul + q ↔ gate row q·H + j0 + 4·wv + ul, full K, in VGPRs
+  // (F32: fp32 W_hh split into hi/lo bf16 fragments once, here)
   const bool mfma_wave = wv < NTILE;
   const int col = lane & 15, kg = lane >> 4;
   bf16x8 wf[KSTEP];
+  bf16x8 wfl[F32 ? KSTEP : 1];
   if (mfma_wave) {
     const int row = (col & 3) * H + j0 + 4 * wv + (col >> 2);
+    if constexpr (F32) {
+      const float* whh = static_cast<const float*>(whh_);
 #pragma unroll
-    for (int ks = 0; ks < KSTEP; ++ks)
-      wf[ks] = *reinterpret_cast<const bf16x8*>(whh + (size_t)row * H + ks * 32 + 8 * kg);
+      for (int ks = 0; ks < KSTEP; ++ks) split_frag(whh + (size_t)row * H + ks * 32 + 8 * kg, wf[ks], wfl[ks]);
+    } else {
+      const short* whh = static_cast<const short*>(whh_);
+#pragma unroll
+      for (int ks = 0; ks < KSTEP; ++ks)
+        wf[ks] = *reinterpret_cast<const bf16x8*>(whh + (size_t)row * H + ks * 32 + 8 * kg);
+    }
   }
   // elementwise mapping after the 4×4 transpose: lane → (row 4·kg + (col&3) [+16·mt], unit j0 + 4·wv + col/4)
   const int erow = 4 * kg + (col & 3);
@@ -294,12 +319,14 @@ __device__ __forceinline__ void lstm_team_fwd_body(
       if (t == 0) {
         for (int i = tid; i < B * H; i += kThreads) {
           const int b = i / H, k = i % H;
-          hl[par][b][k] = dca::f2bf(h0[(size_t)(b0 + b) * H + k]);
+          const float v = h0[(size_t)(b0 + b) * H + k];
+          hl[par][b][k] = dca::f2bf(v);
+          if constexpr (F32) hlo[par][b][k] = dca::f2bf(v - dca::bf2f(dca::f2bf(v)));
         }
       } else {
         const unsigned tag = tagbase | (unsigned)t;          // h_{t-1} carries tag t
-        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(xg + (size_t)((t - 1) & 1) * Bc * (H / 2), Bc * (H / 2) * 8);
-        constexpr int CPR = H / 4;                            // 16-B chunks (4 h values) per row
+        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(xg + (size_t)((t - 1) & 1) * Bc * GPR, Bc * GPR * 8);
+        constexpr int CPR = F32 ? H / 2 : H / 4;              // 16-B chunks (2 f32 / 4 bf16 h values) per row
         constexpr int NL = (RB * CPR + kThreads - 1) / kThreads;
         // every chunk is re-polled only until it has arrived, so later rounds move only the missing bytes
         i32x4 g[NL];
@@ -332,8 +359,18 @@ __device__ __forceinline__ void lstm_team_fwd_body(
         for (int i = 0; i < NL; ++i) {
           const int ci = tid + kThreads * i;
           if (ci < B * CPR) {
-            const int b = ci / CPR, k = (ci % CPR) * 4;
-            *reinterpret_cast<u32x2*>(&hl[par][b][k]) = u32x2{(unsigned)g[i].x, (unsigned)g[i].z};
+            if constexpr (F32) {
+              const int b = ci / CPR, k = (ci % CPR) * 2;
+              const float x = __int_as_float(g[i].x), z = __int_as_float(g[i].z);
+              const short xh = dca::f2bf(x), zh = dca::f2bf(z);
+              *reinterpret_cast<unsigned*>(&hl[par][b][k]) = (unsigned)(unsigned short)xh | ((unsigned)(unsigned short)zh << 16);
+              *reinterpret_cast<unsigned*>(&hlo[par][b][k]) =
+                  (unsigned)(unsigned short)dca::f2bf(x - dca::bf2f(xh)) |
+                  ((unsigned)(unsigned short)dca::f2bf(z - dca::bf2f(zh)) << 16);
+            } else {
+              const int b = ci / CPR, k = (ci % CPR) * 4;
+              *reinterpret_cast<u32x2*>(&hl[par][b][k]) = u32x2{(unsigned)g[i].x, (unsigned)g[i].z};
+            }
           }
         }
       }
@@ -348,10 +385,24 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           if (mt * 16 >= B) break;                            // wave-uniform
           // ---- gates pre-activation tile: rows = batch, columns = (unit, gate)
           dca::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (F32) {
+            // three independent accumulation chains (hi·hi, lo·hi, hi·lo) keep the MFMA pipe full
+            dca::f32x4 a1 = {0.f, 0.f, 0.f, 0.f}, a2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int ks = 0; ks < KSTEP; ++ks) {
-            const bf16x8 a = *reinterpret_cast<const bf16x8*>(&hl[par][mt * 16 + col][ks * 32 + 8 * kg]);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[ks], acc, 0, 0, 0);
+            for (int ks = 0; ks < KSTEP; ++ks) {
+              const bf16x8 a = *reinterpret_cast<const bf16x8*>(&hl[par][mt * 16 + col][ks * 32 + 8 * kg]);
+              const bf16x8 al = *reinterpret_cast<const bf16x8*>(&hlo[par][mt * 16 + col][ks * 32 + 8 * kg]);
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[ks], acc, 0, 0, 0);
+              a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wf[ks], a1, 0, 0, 0);
+              a2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wfl[ks], a2, 0, 0, 0);
+            }
+            acc += a1 + a2;
+          } else {
+#pragma unroll
+            for (int ks = 0; ks < KSTEP; ++ks) {
+              const bf16x8 a = *reinterpret_cast<const bf16x8*>(&hl[par][mt * 16 + col][ks * 32 + 8 * kg]);
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[ks], acc, 0, 0, 0);
+            }
           }
           // ---- 4×4 transpose inside each group of 4 lanes: lane (q' = col&3) gets gate q of row 4kg+q'. Round j:
           // lane a sends its value for row (a-j)&3 and receives from lane (a+j)&3 of its quad — a DPP quad_perm
@@ -382,20 +433,29 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           const float hv = og * dca::tanhf_(c);
           if (b < B) { creg[mt] = c; hreg[mt] = hv; }
           TSTAMP(3);
-          // ---- publish h_t: granule {h(u), h(u+1)} by the even-unit lane (partner unit is 4 lanes up)
-          // partner unit's h from 4 lanes up, same 16-lane row: DPP row_shl:4 (register-to-register)
-          const float hnb = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(hv), 0x104, 0xF, 0xF, false));
-          if (b < B && ((col >> 2) & 1) == 0) {
-            const unsigned pl = (unsigned)(unsigned short)dca::f2bf(hv) | ((unsigned)(unsigned short)dca::f2bf(hnb) << 16);
-            const u32x2 gv = {pl, tagbase | (unsigned)(t + 1)};
-            const __amdgpu_buffer_rsrc_t ws = uniform_rsrc(xg + (size_t)par * Bc * (H / 2), Bc * (H / 2) * 8);
-            __builtin_amdgcn_raw_buffer_store_b64(gv, ws, (b * (H / 2) + (eunit >> 1)) * 8, 0, kPlain);
+          if constexpr (F32) {
+            // ---- publish h_t: granule {f32 h(u), tag} by every lane of a live row
+            if (b < B) {
+              const u32x2 gv = {(unsigned)__float_as_int(hv), tagbase | (unsigned)(t + 1)};
+              const __amdgpu_buffer_rsrc_t ws = uniform_rsrc(xg + (size_t)par * Bc * GPR, Bc * GPR * 8);
+              __builtin_amdgcn_raw_buffer_store_b64(gv, ws, (b * H + eunit) * 8, 0, kPlain);
+            }
+          } else {
+            // ---- publish h_t: granule {h(u), h(u+1)} by the even-unit lane (partner unit is 4 lanes up)
+            // partner unit's h from 4 lanes up, same 16-lane row: DPP row_shl:4 (register-to-register)
+            const float hnb = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(hv), 0x104, 0xF, 0xF, false));
+            if (b < B && ((col >> 2) & 1) == 0) {
+              const unsigned pl = (unsigned)(unsigned short)dca::f2bf(hv) | ((unsigned)(unsigned short)dca::f2bf(hnb) << 16);
+              const u32x2 gv = {pl, tagbase | (unsigned)(t + 1)};
+              const __amdgpu_buffer_rsrc_t ws = uniform_rsrc(xg + (size_t)par * Bc * GPR, Bc * GPR * 8);
+              __builtin_amdgcn_raw_buffer_store_b64(gv, ws, (b * (H / 2) + (eunit >> 1)) * 8, 0, kPlain);
+            }
           }
           TSTAMP(4);
           // ---- outputs
           if (b < B && !((knobs >> 8) & 1)) {
             const size_t bt = (size_t)(b0 + b) * sb + (size_t)t * st;
-            hs[bt * H + eunit] = dca::f2bf(hv);
+            if (hs) hs[bt * H + eunit] = dca::f2bf(hv);
             if (hsf) hsf[bt * H + eunit] = hv;
             cs[bt * H + eunit] = c;
             *reinterpret_cast<dca::f32x4*>(gates4 + (bt * H + eunit) * 4) = dca::f32x4{ig, fg, gg, og};
@@ -430,11 +490,11 @@ __device__ __forceinline__ void lstm_team_fwd_body(
 // xg (per team): [2 parity][Bc][H] 16-B chunks {bf16 d_i,d_f | tag | bf16 d_g,d_o | tag} (one per (row, unit)).
 // Waves split K = 4H in quarters (W_hhᵀ slice of the owned units in VGPRs); partial tiles are summed via LDS.
 // =============================================================================================================
-template <int MT, int KS>
+template <int MT, int KS, bool F32>
 __device__ __forceinline__ void lstm_team_bwd_body(
     const float* __restrict__ dhs, const float* __restrict__ gates4, const float* __restrict__ cs,
     const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
-    const short* __restrict__ whh, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
+    const void* __restrict__ whh_, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
     i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
     unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart) {
   constexpr int H = 128 * KS;
@@ -445,6 +505,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
   constexpr int GP = 4 * H + 8;         // LDS pitch (bf16) of the gathered dG rows
   constexpr int NPAIR = (RB * U + kThreads - 1) / kThreads;
   __shared__ short dgl[RB][GP];
+  __shared__ short dglo[F32 ? RB : 1][F32 ? GP : 1];   // F32: lo bf16 half of the gathered gate gradients
   __shared__ float red[4][RB][17];
   __shared__ float dbs[RB * U * 4];     // per-(row, unit, gate) bias-gradient sums of a chain
   __shared__ int sh_int;
@@ -456,25 +517,38 @@ __device__ __forceinline__ void lstm_team_bwd_body(
   if (me < 0) return;
   const int team = me >> 6, m = me & 63;
   const int j0 = m * U;
-  i32x4* xg = xg_all + (size_t)team * 2 * Bc * H;
+  // 16-B chunks per (row, unit): bf16 {d_i,d_f | tag | d_g,d_o | tag}; F32 {d_i, tag, d_f, tag} {d_g, tag, d_o, tag}
+  constexpr int CPU_ = F32 ? 2 : 1;
+  i32x4* xg = xg_all + (size_t)team * 2 * Bc * H * CPU_;
 #define TSTAMPB(ev)                                                                                       \
   if (trace && lane == 0 && chain == 0 && k < 64)                                                         \
     trace[(((size_t)m * 4 + wv) * 64 + k) * 8 + (ev)] = __builtin_amdgcn_s_memrealtime()
 
   for (int i = tid; i < RB * GP; i += kThreads) (&dgl[0][0])[i] = 0;
+  if constexpr (F32)
+    for (int i = tid; i < RB * GP; i += kThreads) (&dglo[0][0])[i] = 0;
 
   // B operand: lane holds Wᵀ[gc][u] for gc = wv·H + ks·32 + 8·kg + j, u = lane & 15 (zero for u ≥ U)
   const int col = lane & 15, kg = lane >> 4;
   bf16x8 wf[KSTEP];
+  bf16x8 wfl[F32 ? KSTEP : 1];
 #pragma unroll
   for (int ks = 0; ks < KSTEP; ++ks) {
-    bf16x8 v;
+    bf16x8 v, vl;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int gc = wv * KW + ks * 32 + 8 * kg + j;
-      v[j] = (col < U) ? whh[(size_t)((gc & 3) * H + (gc >> 2)) * H + j0 + col] : (short)0;
+      const size_t wi = (size_t)((gc & 3) * H + (gc >> 2)) * H + j0 + col;
+      if constexpr (F32) {
+        const float w = (col < U) ? static_cast<const float*>(whh_)[wi] : 0.f;
+        v[j] = dca::f2bf(w);
+        vl[j] = dca::f2bf(w - dca::bf2f(v[j]));
+      } else {
+        v[j] = (col < U) ? static_cast<const short*>(whh_)[wi] : (short)0;
+      }
     }
     wf[ks] = v;
+    if constexpr (F32) wfl[ks] = vl;
   }
 
   unsigned spins = 0;
@@ -517,10 +591,11 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       // ---- gather dG_{t+1} (B × 4H bf16) into LDS, all loads of a group of 8 rows in flight
       if (k > 0) {
         const unsigned tag = tagbase | (unsigned)(t + 2);
-        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(xg + (size_t)((t + 1) & 1) * Bc * H, Bc * H * 16);
-        constexpr int NL = 8 * H / kThreads;          // chunks per thread per group of 8 rows
-        for (int g0 = 0; g0 < B && !dead; g0 += 8) {
-          const int nck = min(8, B - g0) * H;
+        const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(xg + (size_t)((t + 1) & 1) * Bc * H * CPU_, Bc * H * CPU_ * 16);
+        constexpr int RG = F32 ? 4 : 8;                    // rows per gather group
+        constexpr int NL = RG * H * CPU_ / kThreads;       // chunks per thread per group
+        for (int g0 = 0; g0 < B && !dead; g0 += RG) {
+          const int nck = min(RG, B - g0) * H * CPU_;
           i32x4 g[NL];
           bool okc[NL];
 #pragma unroll
@@ -528,7 +603,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
           while (true) {
 #pragma unroll
             for (int i = 0; i < NL; ++i)
-              if (!okc[i]) g[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (g0 * H + tid + kThreads * i) * 16, 0, kSc1);
+              if (!okc[i]) g[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (g0 * H * CPU_ + tid + kThreads * i) * 16, 0, kSc1);
             bool ok = true;
 #pragma unroll
             for (int i = 0; i < NL; ++i) {
@@ -542,8 +617,18 @@ __device__ __forceinline__ void lstm_team_bwd_body(
           for (int i = 0; i < NL; ++i) {
             const int ci = tid + kThreads * i;
             if (ci < nck) {
-              const int b = g0 + ci / H, j = ci % H;
-              *reinterpret_cast<u32x2*>(&dgl[b][4 * j]) = u32x2{(unsigned)g[i].x, (unsigned)g[i].z};
+              if constexpr (F32) {
+                const int b = g0 + ci / (2 * H), r = ci % (2 * H), gc = 4 * (r >> 1) + 2 * (r & 1);
+                const float x = __int_as_float(g[i].x), z = __int_as_float(g[i].z);
+                const short xh = dca::f2bf(x), zh = dca::f2bf(z);
+                *reinterpret_cast<unsigned*>(&dgl[b][gc]) = (unsigned)(unsigned short)xh | ((unsigned)(unsigned short)zh << 16);
+                *reinterpret_cast<unsigned*>(&dglo[b][gc]) =
+                    (unsigned)(unsigned short)dca::f2bf(x - dca::bf2f(xh)) |
+                    ((unsigned)(unsigned short)dca::f2bf(z - dca::bf2f(zh)) << 16);
+              } else {
+                const int b = g0 + ci / H, j = ci % H;
+                *reinterpret_cast<u32x2*>(&dgl[b][4 * j]) = u32x2{(unsigned)g[i].x, (unsigned)g[i].z};
+              }
             }
           }
         }
@@ -559,10 +644,23 @@ __device__ __forceinline__ void lstm_team_bwd_body(
         for (int mt = 0; mt < MT; ++mt) {
           if (mt * 16 >= B) break;
           dca::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (F32) {
+            dca::f32x4 a1 = {0.f, 0.f, 0.f, 0.f}, a2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int ks = 0; ks < KSTEP; ++ks) {
-            const bf16x8 a = *reinterpret_cast<const bf16x8*>(&dgl[mt * 16 + col][wv * KW + ks * 32 + 8 * kg]);
-            acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[ks], acc, 0, 0, 0);
+            for (int ks = 0; ks < KSTEP; ++ks) {
+              const bf16x8 a = *reinterpret_cast<const bf16x8*>(&dgl[mt * 16 + col][wv * KW + ks * 32 + 8 * kg]);
+              const bf16x8 al = *reinterpret_cast<const bf16x8*>(&dglo[mt * 16 + col][wv * KW + ks * 32 + 8 * kg]);
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[ks], acc, 0, 0, 0);
+              a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, wf[ks], a1, 0, 0, 0);
+              a2 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wfl[ks], a2, 0, 0, 0);
+            }
+            acc += a1 + a2;
+          } else {
+#pragma unroll
+            for (int ks = 0; ks < KSTEP; ++ks) {
+              const bf16x8 a = *reinterpret_cast<const bf16x8*>(&dgl[mt * 16 + col][wv * KW + ks * 32 + 8 * kg]);
+              acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wf[ks], acc, 0, 0, 0);
+            }
           }
 #pragma unroll
           for (int r = 0; r < 4; ++r) red[wv][mt * 16 + kg * 4 + r][col] = acc[r];
@@ -579,7 +677,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
         break;
       }
       // ---- gate gradients for the owned (row, unit) pairs; publish dG_t, write ∂gates
-      const __amdgpu_buffer_rsrc_t ws = uniform_rsrc(xg + (size_t)(t & 1) * Bc * H, Bc * H * 16);
+      const __amdgpu_buffer_rsrc_t ws = uniform_rsrc(xg + (size_t)(t & 1) * Bc * H * CPU_, Bc * H * CPU_ * 16);
       const int tg = (int)(tagbase | (unsigned)(t + 1));
 #pragma unroll
       for (int i = 0; i < NPAIR; ++i) {
@@ -597,12 +695,21 @@ __device__ __forceinline__ void lstm_team_bwd_body(
           const float d_g = dc * ig * (1.f - gg * gg);
           const float d_o = dht * tc * og * (1.f - og);
           dcarry[i] = dc * fg;
-          const unsigned p01 = (unsigned)(unsigned short)dca::f2bf(d_i) | ((unsigned)(unsigned short)dca::f2bf(d_f) << 16);
-          const unsigned p23 = (unsigned)(unsigned short)dca::f2bf(d_g) | ((unsigned)(unsigned short)dca::f2bf(d_o) << 16);
-          __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)p01, tg, (int)p23, tg}, ws, (b * H + j0 + u) * 16, 0, kPlain);
           const size_t bt = (size_t)(b0 + b) * sb + (size_t)t * st;
-          if (dg16) *reinterpret_cast<u32x2*>(dg16 + (bt * H + j0 + u) * 4) = u32x2{p01, p23};
-          else *reinterpret_cast<dca::f32x4*>(dgates4 + (bt * H + j0 + u) * 4) = dca::f32x4{d_i, d_f, d_g, d_o};
+          if constexpr (F32) {
+            const int o = (b * H + j0 + u) * 2 * 16;
+            __builtin_amdgcn_raw_buffer_store_b128(i32x4{__float_as_int(d_i), tg, __float_as_int(d_f), tg}, ws, o, 0,
+                                                   kPlain);
+            __builtin_amdgcn_raw_buffer_store_b128(i32x4{__float_as_int(d_g), tg, __float_as_int(d_o), tg}, ws, o + 16,
+                                                   0, kPlain);
+            *reinterpret_cast<dca::f32x4*>(dgates4 + (bt * H + j0 + u) * 4) = dca::f32x4{d_i, d_f, d_g, d_o};
+          } else {
+            const unsigned p01 = (unsigned)(unsigned short)dca::f2bf(d_i) | ((unsigned)(unsigned short)dca::f2bf(d_f) << 16);
+            const unsigned p23 = (unsigned)(unsigned short)dca::f2bf(d_g) | ((unsigned)(unsigned short)dca::f2bf(d_o) << 16);
+            __builtin_amdgcn_raw_buffer_store_b128(i32x4{(int)p01, tg, (int)p23, tg}, ws, (b * H + j0 + u) * 16, 0, kPlain);
+            if (dg16) *reinterpret_cast<u32x2*>(dg16 + (bt * H + j0 + u) * 4) = u32x2{p01, p23};
+            else *reinterpret_cast<dca::f32x4*>(dgates4 + (bt * H + j0 + u) * 4) = dca::f32x4{d_i, d_f, d_g, d_o};
+          }
           dsum[i] += dca::f32x4{d_i, d_f, d_g, d_o};
           if (t == 0) dc0[(size_t)(b0 + b) * H + j0 + u] = dcarry[i];
         }
@@ -630,28 +737,28 @@ __device__ __forceinline__ void lstm_team_bwd_body(
 #undef TSTAMPB
 }
 
-template <int MT, int KS>
+template <int MT, int KS, bool F32>
 __global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
-    const float* __restrict__ xp4, const short* __restrict__ whh, const float* __restrict__ h0,
+    const float* __restrict__ xp4, const void* __restrict__ whh, const float* __restrict__ h0,
     const float* __restrict__ c0, short* __restrict__ hs, float* __restrict__ hsf, float* __restrict__ cs,
     float* __restrict__ gates4, float* __restrict__ hn, float* __restrict__ cn, unsigned long long* xg_all,
     TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st, unsigned long long* trace,
     int knobs, const float* __restrict__ bias4) {
   __builtin_amdgcn_s_setprio(3);   // issue priority over co-resident waves of kernels overlapped on other streams
-  lstm_team_fwd_body<MT, KS>(xp4, whh, h0, c0, hs, hsf, cs, gates4, hn, cn, xg_all, ctl, err, Btot, Bc, nch, S, sb,
+  lstm_team_fwd_body<MT, KS, F32>(xp4, whh, h0, c0, hs, hsf, cs, gates4, hn, cn, xg_all, ctl, err, Btot, Bc, nch, S, sb,
                              st, trace, knobs, bias4);
   team_exit(ctl);
 }
 
-template <int MT, int KS>
+template <int MT, int KS, bool F32>
 __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
     const float* __restrict__ dhs, const float* __restrict__ gates4, const float* __restrict__ cs,
     const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
-    const short* __restrict__ whh, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
+    const void* __restrict__ whh, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
     i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
     unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart) {
   __builtin_amdgcn_s_setprio(3);
-  lstm_team_bwd_body<MT, KS>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, dh0, dc0, xg_all, ctl, err, Btot, Bc, nch,
+  lstm_team_bwd_body<MT, KS, F32>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, dh0, dc0, xg_all, ctl, err, Btot, Bc, nch,
                              S, sb, st, trace, dg16, dbpart);
   team_exit(ctl);
 }
@@ -662,7 +769,7 @@ inline int team_knobs() {
   return e ? atoi(e) : 0;
 }
 
-inline void plan(int B, int& nch, int& Bc, int& MT) {
+inline void plan(int B, int& nch, int& Bc, int& MT, int f32 = 0) {
   // Spread the sequences over all 8 teams (one chain per XCD) before packing rows into a chain: per-step latency
   // grows with rows per chain (more granules to gather and publish), measured B=8, H=512 fwd/bwd µs per step:
   // 1 chain × 8 rows 2.21/2.82, 2 × 4 2.09/2.57, 4 × 2 2.08/2.41, 8 × 1 2.08/2.26. Chains hold ≤ 32 rows; beyond
@@ -671,79 +778,87 @@ inline void plan(int B, int& nch, int& Bc, int& MT) {
   // DCA_TEAM_ROWS = sequences per chain (latency experiments: e.g. 1 → B independent chains on B teams)
   static const int forced = [] { const char* e = getenv("DCA_TEAM_ROWS"); return e ? atoi(e) : 0; }();
   if (forced > 0 && forced <= 32) nch = (B + forced - 1) / forced;
+  // F32 chains hold ≤ 16 rows (the backward's hi + lo gate-gradient images of 16 rows take 132 KB of LDS)
+  if (f32 && (B + nch - 1) / nch > 16) nch = (B + 15) / 16;
   Bc = (B + nch - 1) / nch;
   MT = Bc <= 16 ? 1 : 2;
 }
 
 }  // namespace
 
-#define DCA_TEAM_DISPATCH(MT_, KS_, ...)                                            \
-  switch (((MT_) << 4) | (KS_)) {                                                  \
-    case 0x11: return __VA_ARGS__(1, 1); case 0x12: return __VA_ARGS__(1, 2);      \
-    case 0x14: return __VA_ARGS__(1, 4); case 0x21: return __VA_ARGS__(2, 1);      \
-    case 0x22: return __VA_ARGS__(2, 2); case 0x24: return __VA_ARGS__(2, 4);      \
-    default: return hipErrorInvalidValue;                                          \
+#define DCA_TEAM_DISPATCH(MT_, KS_, F32_, ...)                                               \
+  switch (((F32_) << 8) | ((MT_) << 4) | (KS_)) {                                           \
+    case 0x011: return __VA_ARGS__(1, 1, false); case 0x012: return __VA_ARGS__(1, 2, false); \
+    case 0x014: return __VA_ARGS__(1, 4, false); case 0x021: return __VA_ARGS__(2, 1, false); \
+    case 0x022: return __VA_ARGS__(2, 2, false); case 0x024: return __VA_ARGS__(2, 4, false); \
+    case 0x111: return __VA_ARGS__(1, 1, true);  case 0x112: return __VA_ARGS__(1, 2, true);  \
+    case 0x114: return __VA_ARGS__(1, 4, true);                                               \
+    default: return hipErrorInvalidValue;                                                     \
   }
 
 // Workspace bytes (control block + per-team exchange buffers) for a launch of (B, H).
 extern "C" size_t dca_lstm_team_ctl_bytes() { return 256; }
 
 // Sequence chains a launch of B sequences is split into (rows of the backward's bias-gradient partials).
-extern "C" int dca_lstm_team_chains(int B) {
+extern "C" int dca_lstm_team_chains(int B, int f32) {
   int nch, Bc, MT;
-  plan(B, nch, Bc, MT);
+  plan(B, nch, Bc, MT, f32);
   return nch;
 }
 
 // Exchange-buffer bytes (per-team hand-off rings) for a launch of (B, H). Not zeroed: tags carry the epoch.
-extern "C" size_t dca_lstm_team_workspace(int B, int H, int backward) {
+extern "C" size_t dca_lstm_team_workspace(int B, int H, int backward, int f32) {
   int nch, Bc, MT;
-  plan(B, nch, Bc, MT);
-  if (!backward) return (size_t)kMaxTeams * 2 * Bc * (H / 2) * 8;
-  return (size_t)kMaxTeams * 2 * Bc * H * 16;
+  plan(B, nch, Bc, MT, f32);
+  if (!backward) return (size_t)kMaxTeams * 2 * Bc * (f32 ? H : H / 2) * 8;
+  return (size_t)kMaxTeams * 2 * Bc * H * (f32 ? 2 : 1) * 16;
 }
 
-extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const short* whh, const float* h0, const float* c0,
+// whh: (4H,H) bf16 (f32 = 0) or fp32 (f32 = 1: bf16x3 split MFMA, h exchanged and stored in fp32, hs unused)
+extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const void* whh, const float* h0, const float* c0,
                                         short* hs, float* hsf, float* cs, float* gates4, float* hn, float* cn,
                                         void* ctl_mem, void* ws, size_t ws_bytes, unsigned* err, int B, int S, int H,
                                         int time_major, hipStream_t stream, unsigned long long* trace,
-                                        const float* bias4) {
+                                        const float* bias4, int f32) {
   if (B < 1 || S < 1 || S >= 65535 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
-  if (ws_bytes < dca_lstm_team_workspace(B, H, 0) || ctl_mem == nullptr) return hipErrorInvalidValue;
+  if (ws_bytes < dca_lstm_team_workspace(B, H, 0, f32) || ctl_mem == nullptr) return hipErrorInvalidValue;
+  if (f32 && hsf == nullptr) return hipErrorInvalidValue;
+  if (!f32 && hs == nullptr) return hipErrorInvalidValue;
   int nch, Bc, MT;
-  plan(B, nch, Bc, MT);
+  plan(B, nch, Bc, MT, f32);
   const int sb = time_major ? 1 : S, st = time_major ? B : 1;   // row(b, t) = b·sb + t·st
   TeamCtl* ctl = reinterpret_cast<TeamCtl*>(ctl_mem);
   unsigned long long* xg = reinterpret_cast<unsigned long long*>(ws);
   const int KS = H / 128;
-#define DCA_F(mt, ks)                                                                                           \
-  (lstm_team_fwd_kernel<mt, ks><<<kMaxTeams * kT, kThreads, 0, stream>>>(xp4, whh, h0, c0, hs, hsf, cs, gates4, \
+#define DCA_F(mt, ks, f)                                                                                        \
+  (lstm_team_fwd_kernel<mt, ks, f><<<kMaxTeams * kT, kThreads, 0, stream>>>(xp4, whh, h0, c0, hs, hsf, cs, gates4, \
                                                                           hn, cn, xg, ctl, err, B, Bc, nch, S, sb, \
                                                                           st, trace, team_knobs(), bias4),         \
    hipGetLastError())
-  DCA_TEAM_DISPATCH(MT, KS, DCA_F)
+  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, DCA_F)
 #undef DCA_F
 }
 
 extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, const float* cs, const float* c0,
-                                        const float* dhn, const float* dcn, const short* whh, float* dgates4,
+                                        const float* dhn, const float* dcn, const void* whh, float* dgates4,
                                         float* dh0, float* dc0, void* ctl_mem, void* ws, size_t ws_bytes,
                                         unsigned* err, int B, int S, int H, int time_major, hipStream_t stream,
-                                        unsigned long long* trace, short* dg16, float* dbpart) {
+                                        unsigned long long* trace, short* dg16, float* dbpart, int f32) {
   if (B < 1 || S < 1 || S >= 65534 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
   if (dgates4 == nullptr && dg16 == nullptr) return hipErrorInvalidValue;
-  if (ws_bytes < dca_lstm_team_workspace(B, H, 1) || ctl_mem == nullptr) return hipErrorInvalidValue;
+  if (f32 && dgates4 == nullptr) return hipErrorInvalidValue;
+  if (ws_bytes < dca_lstm_team_workspace(B, H, 1, f32) || ctl_mem == nullptr) return hipErrorInvalidValue;
   int nch, Bc, MT;
-  plan(B, nch, Bc, MT);
+  plan(B, nch, Bc, MT, f32);
   const int sb = time_major ? 1 : S, st = time_major ? B : 1;
   TeamCtl* ctl = reinterpret_cast<TeamCtl*>(ctl_mem);
   i32x4* xb = reinterpret_cast<i32x4*>(ws);
   const int KS = H / 128;
-#define DCA_B(mt, ks)                                                                                              \
-  (lstm_team_bwd_kernel<mt, ks><<<kMaxTeams * kT, kThreads, 0, stream>>>(dhs, gates4, cs, c0, dhn, dcn, whh,      \
+#define DCA_B(mt, ks, f)                                                                                           \
+  (lstm_team_bwd_kernel<mt, ks, f><<<kMaxTeams * kT, kThreads, 0, stream>>>(dhs, gates4, cs, c0, dhn, dcn, whh,      \
                                                                           dgates4, dh0, dc0, xb, ctl, err, B, Bc,  \
                                                                           nch, S, sb, st, trace, dg16, dbpart),    \
    hipGetLastError())
-  DCA_TEAM_DISPATCH(MT, KS, DCA_B)
+  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, DCA_B)
 #undef DCA_B
 }

@@ -1,4 +1,4 @@
-"""Python face of the split-K bf16 TN GEMM (``csrc/gemm_tn.hip``): ``C (+)= Aᵀ·B`` for K-outer operands — the
+"""Python face of the split-K TN GEMM (``csrc/gemm_tn.hip``): ``C (+)= Aᵀ·B`` for K-outer operands — the
 learner's weight gradients, reduced over the B·S rows of a minibatch."""
 from __future__ import annotations
 
@@ -11,9 +11,10 @@ from . import require
 def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, perm: Optional[torch.Tensor] = None,
             accumulate: bool = False, b0: Optional[torch.Tensor] = None,
             colsum: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """``a`` (K, M) bf16, ``b`` (K - b0_rows, N) bf16 (``b0`` supplies the first rows of the B operand), result
+    """``a`` (K, M), ``b`` (K - b0_rows, N) — both bf16, or both fp32 (bf16x3 split MFMA: ≈2⁻¹⁶ relative per
+    product, fp32 accumulation) — (``b0`` supplies the first rows of the B operand), result
     (M, N) f32 written to ``out`` (through row map ``perm`` if given; added to it if ``accumulate``). ``colsum``
-    (M,) f32, if given, receives Σ_k a[k, m] the same way (a bias gradient, from the staged bf16 A tiles)."""
+    (M,) f32, if given, receives Σ_k a[k, m] the same way (a bias gradient, from the staged A tiles)."""
     C = require()
     M, N = a.shape[1], b.shape[1]
     if out is None:

@@ -1,4 +1,7 @@
-"""Fused MI355X learner path (HIP kernels) vs the fp32 torch reference: loss and every parameter gradient."""
+"""Fused MI355X learner path (HIP kernels) vs the fp32 torch reference: loss and every parameter gradient.
+
+The bf16 learner is checked here at short horizons with bf16 tolerances; the fp32 (bf16x3) learner and the deploy
+horizon (S=1400) are pinned in test_fp32_kernels.py."""
 import copy
 
 import pytest
@@ -27,9 +30,8 @@ def test_fused_loss_and_grads_match_reference(gpu_ops, monkeypatch, pipeline, pr
     pol = Policy(cfg)
     ref = copy.deepcopy(pol)
     lc = LossConfig(algo=algo, vf_coef=0.5, entropy_coef=0.01)
-    fused = Learner(pol, lc, device='cuda', backend='fused', dp=False)
-    torch_l = Learner(ref, lc, device='cuda', backend='torch', dp=False)
-    torch_l.backend = 'torch-fp32'      # no autocast: fp32 oracle
+    fused = Learner(pol, lc, device='cuda', backend='fused', dp=False, precision='bf16')
+    torch_l = Learner(ref, lc, device='cuda', backend='torch', dp=False, precision='fp32')   # fp32 oracle
     batch = make_batch(B, S, cfg.layout, cfg.hidden if cfg.rnn == 'lstm' else None, device='cuda', seed=3)
     for L in (fused, torch_l):
         L.dp.zero_grad()
@@ -51,18 +53,20 @@ def test_fused_loss_and_grads_match_reference(gpu_ops, monkeypatch, pipeline, pr
         assert _rel(gf, gr) < 1.2e-1, (name, _rel(gf, gr))
 
 
-def test_fused_train_step_decreases_loss(gpu_ops):
+@pytest.mark.parametrize('precision', ['fp32', 'bf16'])
+def test_fused_train_step_decreases_loss(gpu_ops, precision):
     torch.manual_seed(0)
     cfg = get_config('lstm512')
-    L = Learner(Policy(cfg), LossConfig(algo='ppo', learning_rate=3e-4), device='cuda', backend='fused', dp=False)
+    L = Learner(Policy(cfg), LossConfig(algo='ppo', learning_rate=3e-4), device='cuda', backend='fused', dp=False,
+                precision=precision)
     batch = make_batch(4, 64, cfg.layout, cfg.hidden, device='cuda', seed=1)
     losses = [float(L.train_step(batch)['loss']) for _ in range(8)]
     L.model.check_error()
     assert losses[-1] < losses[0]
 
 
-@pytest.mark.parametrize('chunks', ['1', '3'])
-def test_graph_captured_step_matches_eager(gpu_ops, monkeypatch, chunks):
+@pytest.mark.parametrize('chunks,precision', [('1', 'fp32'), ('3', 'fp32'), ('1', 'bf16')])
+def test_graph_captured_step_matches_eager(gpu_ops, monkeypatch, chunks, precision):
     """hipGraph-captured forward+backward (Learner.enable_graph) gives the same parameters as eager steps, also
     across host synchronisations between replays (a stale host-staged buffer in the graph would show up there)."""
     monkeypatch.setenv('DCA_PIPELINE_CHUNKS', chunks)
@@ -71,8 +75,8 @@ def test_graph_captured_step_matches_eager(gpu_ops, monkeypatch, chunks):
     pol = Policy(cfg)
     ref = copy.deepcopy(pol)
     lc = LossConfig(algo='ppo')
-    a = Learner(pol, lc, device='cuda', backend='fused', dp=False)
-    b = Learner(ref, lc, device='cuda', backend='fused', dp=False)
+    a = Learner(pol, lc, device='cuda', backend='fused', dp=False, precision=precision)
+    b = Learner(ref, lc, device='cuda', backend='fused', dp=False, precision=precision)
     assert b.enable_graph(warmup=1)
     batches = [make_batch(4, 40, cfg.layout, cfg.hidden, device='cuda', seed=s) for s in range(4)]
     for bt in batches:
@@ -86,7 +90,8 @@ def test_graph_captured_step_matches_eager(gpu_ops, monkeypatch, chunks):
     torch.testing.assert_close(mb['loss'], ma['loss'], rtol=1e-5, atol=1e-6)
 
 
-def test_direct_replay_step_matches_autograd_step(gpu_ops):
+@pytest.mark.parametrize('precision', ['fp32', 'bf16'])
+def test_direct_replay_step_matches_autograd_step(gpu_ops, precision):
     """The autograd-free direct step fed from the HBM replay (time-major gather inside the captured graph) updates
     the parameters exactly like the autograd Function path on the same minibatch."""
     from dotaclient_amd.learner.replay import HbmReplay
@@ -95,8 +100,8 @@ def test_direct_replay_step_matches_autograd_step(gpu_ops):
     pol = Policy(cfg)
     ref = copy.deepcopy(pol)
     lc = LossConfig(algo='ppo')
-    a = Learner(pol, lc, device='cuda', backend='fused', dp=False)
-    b = Learner(ref, lc, device='cuda', backend='fused', dp=False)
+    a = Learner(pol, lc, device='cuda', backend='fused', dp=False, precision=precision)
+    b = Learner(ref, lc, device='cuda', backend='fused', dp=False, precision=precision)
     assert b.direct() and b.enable_graph(warmup=1)
     rep = HbmReplay(6, 40, cfg.layout, cfg.hidden, 'cuda', seed=5)
     rep.add(make_batch(6, 40, cfg.layout, cfg.hidden, device='cuda', seed=9))
@@ -134,8 +139,8 @@ def test_loss_prep_kernel_matches_batch_norms(gpu_ops):
     assert int(ws[-1]) == 0
 
 
-@pytest.mark.parametrize('preset', ['lstm512', '5v5'])
-def test_fused_step_is_bitwise_deterministic(gpu_ops, preset):
+@pytest.mark.parametrize('preset,precision', [('lstm512', 'fp32'), ('lstm512', 'bf16'), ('5v5', 'bf16')])
+def test_fused_step_is_bitwise_deterministic(gpu_ops, preset, precision):
     """Deterministic-mode check: every reduction on the fused step runs in a fixed order (no float
     atomics), so two learners fed the same replay minibatches end bit-identical."""
     from dotaclient_amd.learner.replay import HbmReplay
@@ -143,7 +148,8 @@ def test_fused_step_is_bitwise_deterministic(gpu_ops, preset):
     torch.manual_seed(0)
     pol = Policy(cfg)
     ref = copy.deepcopy(pol)
-    learners = [Learner(p, LossConfig(algo='ppo'), device='cuda', backend='fused', dp=False) for p in (pol, ref)]
+    learners = [Learner(p, LossConfig(algo='ppo'), device='cuda', backend='fused', dp=False, precision=precision)
+                for p in (pol, ref)]
     reps = []
     for L in learners:
         assert L.enable_graph(warmup=1)
@@ -157,8 +163,8 @@ def test_fused_step_is_bitwise_deterministic(gpu_ops, preset):
     assert torch.equal(ms[0]['loss'], ms[1]['loss']) and torch.equal(ms[0]['grad_norm'], ms[1]['grad_norm'])
 
 
-@pytest.mark.parametrize('preset', ['lstm512', '5v5'])
-def test_dp_split_step_matches_single_graph(gpu_ops, monkeypatch, preset):
+@pytest.mark.parametrize('preset,precision', [('lstm512', 'fp32'), ('5v5', 'bf16')])
+def test_dp_split_step_matches_single_graph(gpu_ops, monkeypatch, preset, precision):
     """The data-parallel split step (two captured graphs around the point where the recurrence / pre-RNN / heads
     gradients are final, early buckets all-reduced in between) computes exactly what the single-graph step does."""
     from dotaclient_amd.learner.replay import HbmReplay
@@ -169,7 +175,7 @@ def test_dp_split_step_matches_single_graph(gpu_ops, monkeypatch, preset):
     flats, losses = [], []
     for p, split in ((pol, '1'), (ref, '0')):
         monkeypatch.setenv('DCA_DP_SPLIT', split)
-        L = Learner(p, LossConfig(algo='ppo'), device='cuda', backend='fused', dp=False)
+        L = Learner(p, LossConfig(algo='ppo'), device='cuda', backend='fused', dp=False, precision=precision)
         assert L.enable_graph(warmup=1)
         rep = HbmReplay(6, 48, cfg.layout, cfg.hidden, 'cuda', seed=11)
         rep.add(make_batch(6, 48, cfg.layout, cfg.hidden, device='cuda', seed=4))
