@@ -223,7 +223,12 @@ __device__ __forceinline__ unsigned make_tagbase(unsigned epoch, unsigned iter) 
 // Forward. MT = 16-row batch tiles per chain (Bc ≤ 16·MT), KS = H/128.
 // xg (per team): [2 parity][Bc][H/2] u64 granules {lo: 2×bf16 h, hi: tag}
 // =============================================================================================================
-template <int MT, int KS, bool F32>
+// V1 (F32 only, one sequence row per chain — every launch of B ≤ 8 sequences): the recurrent product runs as exact
+// fp32 VALU dot products instead of MFMA tiles whose 16 rows would be 15/16 padding. Lane (col, kg) of a wave keeps
+// W_hh[row(col)][kg·H/4 … kg·H/4 + H/4) as fp32 VGPRs (128 at H = 512), reads h_{t-1} (fp32, LDS) with broadcast
+// 16-B loads, and the four k-quarters are summed with two cross-lane adds; a quad broadcast then hands each lane
+// of the (row 0, unit) quad all four gates — the lane mapping of the MFMA path after its 4×4 transpose.
+template <int MT, int KS, bool F32, bool V1>
 __device__ __forceinline__ void lstm_team_fwd_body(
     const float* __restrict__ xp4, const void* __restrict__ whh_, const float* __restrict__ h0,
     const float* __restrict__ c0, short* __restrict__ hs, float* __restrict__ hsf, float* __restrict__ cs,
@@ -236,8 +241,14 @@ __device__ __forceinline__ void lstm_team_fwd_body(
   constexpr int KSTEP = H / 32;         // k-steps of the full K
   constexpr int HP = H + 8;             // LDS row pitch (bf16)
   constexpr int RB = MT * 16;
-  __shared__ short hl[2][RB][HP];
-  __shared__ short hlo[F32 ? 2 : 1][F32 ? RB : 1][F32 ? HP : 1];   // F32: lo bf16 half of h (h = hi + lo)
+  constexpr int KQ = H / 4;             // V1: k-quarter per lane group
+  static_assert(!V1 || (F32 && MT == 1), "V1 is the fp32 one-row variant");
+  __shared__ short hl[V1 ? 1 : 2][V1 ? 1 : RB][V1 ? 1 : HP];
+  __shared__ short hlo[F32 && !V1 ? 2 : 1][F32 && !V1 ? RB : 1][F32 && !V1 ? HP : 1];   // F32: lo bf16 half of h
+  // V1: h_{t-1} of row 0; each k-quarter padded by 4 floats so the four lane groups' broadcast reads of one
+  // ds_read_b128 hit different banks (quarters 512 B apart would all map to the same 4 banks: 2 cycles per group)
+  constexpr int QP = KQ + 4;
+  __shared__ __attribute__((aligned(16))) float hf[V1 ? 2 : 1][V1 ? 4 * QP : 4];
   __shared__ int sh_int;
   __shared__ unsigned sh_epoch;
 
@@ -255,19 +266,28 @@ __device__ __forceinline__ void lstm_team_fwd_body(
   unsigned long long* xg = xg_all + (size_t)team * 2 * Bc * GPR;
 
   // zero the padding rows of both h buffers once
-  for (int i = tid; i < 2 * RB * HP; i += kThreads) (&hl[0][0][0])[i] = 0;
-  if constexpr (F32)
+  if constexpr (!V1)
+    for (int i = tid; i < 2 * RB * HP; i += kThreads) (&hl[0][0][0])[i] = 0;
+  if constexpr (F32 && !V1)
     for (int i = tid; i < 2 * RB * HP; i += kThreads) (&hlo[0][0][0])[i] = 0;
 
   // W_hh slice for this wave's tile: columns c = 4·ul + q ↔ gate row q·H + j0 + 4·wv + ul, full K, in VGPRs
   // (F32: fp32 W_hh split into hi/lo bf16 fragments once, here)
   const bool mfma_wave = wv < NTILE;
   const int col = lane & 15, kg = lane >> 4;
-  bf16x8 wf[KSTEP];
-  bf16x8 wfl[F32 ? KSTEP : 1];
+  bf16x8 wf[V1 ? 1 : KSTEP];
+  bf16x8 wfl[F32 && !V1 ? KSTEP : 1];
+  float wq[V1 ? KQ : 1];
   if (mfma_wave) {
     const int row = (col & 3) * H + j0 + 4 * wv + (col >> 2);
-    if constexpr (F32) {
+    if constexpr (V1) {
+      const float* wr = static_cast<const float*>(whh_) + (size_t)row * H + kg * KQ;
+#pragma unroll
+      for (int j = 0; j < KQ; j += 4) {
+        const float4 v = *reinterpret_cast<const float4*>(wr + j);
+        wq[j] = v.x; wq[j + 1] = v.y; wq[j + 2] = v.z; wq[j + 3] = v.w;
+      }
+    } else if constexpr (F32) {
       const float* whh = static_cast<const float*>(whh_);
 #pragma unroll
       for (int ks = 0; ks < KSTEP; ++ks) split_frag(whh + (size_t)row * H + ks * 32 + 8 * kg, wf[ks], wfl[ks]);
@@ -320,14 +340,18 @@ __device__ __forceinline__ void lstm_team_fwd_body(
         for (int i = tid; i < B * H; i += kThreads) {
           const int b = i / H, k = i % H;
           const float v = h0[(size_t)(b0 + b) * H + k];
-          hl[par][b][k] = dca::f2bf(v);
-          if constexpr (F32) hlo[par][b][k] = dca::f2bf(v - dca::bf2f(dca::f2bf(v)));
+          if constexpr (V1) {
+            hf[par][k + (k / KQ) * 4] = v;
+          } else {
+            hl[par][b][k] = dca::f2bf(v);
+            if constexpr (F32) hlo[par][b][k] = dca::f2bf(v - dca::bf2f(dca::f2bf(v)));
+          }
         }
       } else {
         const unsigned tag = tagbase | (unsigned)t;          // h_{t-1} carries tag t
         const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(xg + (size_t)((t - 1) & 1) * Bc * GPR, Bc * GPR * 8);
         constexpr int CPR = F32 ? H / 2 : H / 4;              // 16-B chunks (2 f32 / 4 bf16 h values) per row
-        constexpr int NL = (RB * CPR + kThreads - 1) / kThreads;
+        constexpr int NL = ((V1 ? 1 : RB) * CPR + kThreads - 1) / kThreads;   // (V1: one row)
         // every chunk is re-polled only until it has arrived, so later rounds move only the missing bytes
         i32x4 g[NL];
         bool okc[NL];
@@ -359,7 +383,11 @@ __device__ __forceinline__ void lstm_team_fwd_body(
         for (int i = 0; i < NL; ++i) {
           const int ci = tid + kThreads * i;
           if (ci < B * CPR) {
-            if constexpr (F32) {
+            if constexpr (V1) {
+              const int k = 2 * ci;
+              *reinterpret_cast<float2*>(&hf[par][k + (k / KQ) * 4]) =
+                  make_float2(__int_as_float(g[i].x), __int_as_float(g[i].z));
+            } else if constexpr (F32) {
               const int b = ci / CPR, k = (ci % CPR) * 2;
               const float x = __int_as_float(g[i].x), z = __int_as_float(g[i].z);
               const short xh = dca::f2bf(x), zh = dca::f2bf(z);
@@ -383,6 +411,28 @@ __device__ __forceinline__ void lstm_team_fwd_body(
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           if (mt * 16 >= B) break;                            // wave-uniform
+          float gq0 = 0.f, gq1 = 0.f, gq2 = 0.f, gq3 = 0.f;
+          if constexpr (V1) {
+            // ---- exact fp32 dot products over this lane's k-quarter, 4 partial chains
+            const float* hp = &hf[par][kg * QP];
+            float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+            for (int j = 0; j < KQ; j += 4) {
+              const float4 hv = *reinterpret_cast<const float4*>(hp + j);
+              s0 = fmaf(wq[j], hv.x, s0);
+              s1 = fmaf(wq[j + 1], hv.y, s1);
+              s2 = fmaf(wq[j + 2], hv.z, s2);
+              s3 = fmaf(wq[j + 3], hv.w, s3);
+            }
+            float sum = (s0 + s1) + (s2 + s3);
+            sum += __shfl_xor(sum, 16, 64);
+            sum += __shfl_xor(sum, 32, 64);
+            // column col = 4·unit + gate: every lane of a quad receives the quad's four gates (quad_perm broadcast)
+            gq0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sum), 0x00, 0xF, 0xF, false));
+            gq1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sum), 0x55, 0xF, 0xF, false));
+            gq2 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sum), 0xAA, 0xF, 0xF, false));
+            gq3 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sum), 0xFF, 0xF, 0xF, false));
+          } else {
           // ---- gates pre-activation tile: rows = batch, columns = (unit, gate)
           dca::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
           if constexpr (F32) {
@@ -407,7 +457,6 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           // ---- 4×4 transpose inside each group of 4 lanes: lane (q' = col&3) gets gate q of row 4kg+q'. Round j:
           // lane a sends its value for row (a-j)&3 and receives from lane (a+j)&3 of its quad — a DPP quad_perm
           // (register-to-register, a few cycles) instead of an LDS-routed ds_bpermute
-          float gq0 = 0.f, gq1 = 0.f, gq2 = 0.f, gq3 = 0.f;
           const int q0 = col & 3;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
@@ -424,6 +473,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
             gq2 = qs == 2 ? got : gq2;
             gq3 = qs == 3 ? got : gq3;
           }
+          }   // !V1
           const int b = mt * 16 + erow;
           // (bias added here, at the use: an add right after the prefetch would wait out the load before the gather)
           const float pi = gq0 + (xv[mt][0] + bv[0]), pf = gq1 + (xv[mt][1] + bv[1]), pg = gq2 + (xv[mt][2] + bv[2]),
@@ -490,7 +540,9 @@ __device__ __forceinline__ void lstm_team_fwd_body(
 // xg (per team): [2 parity][Bc][H] 16-B chunks {bf16 d_i,d_f | tag | bf16 d_g,d_o | tag} (one per (row, unit)).
 // Waves split K = 4H in quarters (W_hhᵀ slice of the owned units in VGPRs); partial tiles are summed via LDS.
 // =============================================================================================================
-template <int MT, int KS, bool F32>
+// V1 (F32, one row per chain): the partial recurrent gradient as exact fp32 VALU dot products — lane (u, kg) keeps
+// W_hhᵀ[gc][j0 + u] for its wave's K quarter and k-group as fp32 VGPRs, dG_{t+1} of row 0 sits in LDS in fp32.
+template <int MT, int KS, bool F32, bool V1>
 __device__ __forceinline__ void lstm_team_bwd_body(
     const float* __restrict__ dhs, const float* __restrict__ gates4, const float* __restrict__ cs,
     const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
@@ -504,8 +556,13 @@ __device__ __forceinline__ void lstm_team_bwd_body(
   constexpr int RB = MT * 16;
   constexpr int GP = 4 * H + 8;         // LDS pitch (bf16) of the gathered dG rows
   constexpr int NPAIR = (RB * U + kThreads - 1) / kThreads;
-  __shared__ short dgl[RB][GP];
-  __shared__ short dglo[F32 ? RB : 1][F32 ? GP : 1];   // F32: lo bf16 half of the gathered gate gradients
+  constexpr int KQ = KW / 4;            // V1: k-group slice of a wave's K quarter
+  static_assert(!V1 || (F32 && MT == 1), "V1 is the fp32 one-row variant");
+  __shared__ short dgl[V1 ? 1 : RB][V1 ? 1 : GP];
+  __shared__ short dglo[F32 && !V1 ? RB : 1][F32 && !V1 ? GP : 1];   // F32: lo bf16 half of the gathered dG
+  // V1: dG_{t+1} of row 0, fp32; every KQ-slice padded by 4 floats (bank spread of the broadcast reads, as forward)
+  constexpr int QP = KQ + 4;
+  __shared__ __attribute__((aligned(16))) float dgf[V1 ? 16 * QP : 4];
   __shared__ float red[4][RB][17];
   __shared__ float dbs[RB * U * 4];     // per-(row, unit, gate) bias-gradient sums of a chain
   __shared__ int sh_int;
@@ -524,16 +581,25 @@ __device__ __forceinline__ void lstm_team_bwd_body(
   if (trace && lane == 0 && chain == 0 && k < 64)                                                         \
     trace[(((size_t)m * 4 + wv) * 64 + k) * 8 + (ev)] = __builtin_amdgcn_s_memrealtime()
 
-  for (int i = tid; i < RB * GP; i += kThreads) (&dgl[0][0])[i] = 0;
-  if constexpr (F32)
+  if constexpr (!V1)
+    for (int i = tid; i < RB * GP; i += kThreads) (&dgl[0][0])[i] = 0;
+  if constexpr (F32 && !V1)
     for (int i = tid; i < RB * GP; i += kThreads) (&dglo[0][0])[i] = 0;
 
   // B operand: lane holds Wᵀ[gc][u] for gc = wv·H + ks·32 + 8·kg + j, u = lane & 15 (zero for u ≥ U)
   const int col = lane & 15, kg = lane >> 4;
-  bf16x8 wf[KSTEP];
-  bf16x8 wfl[F32 ? KSTEP : 1];
+  bf16x8 wf[V1 ? 1 : KSTEP];
+  bf16x8 wfl[F32 && !V1 ? KSTEP : 1];
+  float wq[V1 ? KQ : 1];
+  if constexpr (V1) {
 #pragma unroll
-  for (int ks = 0; ks < KSTEP; ++ks) {
+    for (int j = 0; j < KQ; ++j) {
+      const int gc = wv * KW + kg * KQ + j;
+      wq[j] = (col < U) ? static_cast<const float*>(whh_)[(size_t)((gc & 3) * H + (gc >> 2)) * H + j0 + col] : 0.f;
+    }
+  }
+#pragma unroll
+  for (int ks = 0; ks < (V1 ? 0 : KSTEP); ++ks) {
     bf16x8 v, vl;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -548,7 +614,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       }
     }
     wf[ks] = v;
-    if constexpr (F32) wfl[ks] = vl;
+    if constexpr (F32 && !V1) wfl[ks] = vl;
   }
 
   unsigned spins = 0;
@@ -592,7 +658,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       if (k > 0) {
         const unsigned tag = tagbase | (unsigned)(t + 2);
         const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(xg + (size_t)((t + 1) & 1) * Bc * H * CPU_, Bc * H * CPU_ * 16);
-        constexpr int RG = F32 ? 4 : 8;                    // rows per gather group
+        constexpr int RG = V1 ? 1 : (F32 ? 4 : 8);         // rows per gather group
         constexpr int NL = RG * H * CPU_ / kThreads;       // chunks per thread per group
         for (int g0 = 0; g0 < B && !dead; g0 += RG) {
           const int nck = min(RG, B - g0) * H * CPU_;
@@ -617,7 +683,11 @@ __device__ __forceinline__ void lstm_team_bwd_body(
           for (int i = 0; i < NL; ++i) {
             const int ci = tid + kThreads * i;
             if (ci < nck) {
-              if constexpr (F32) {
+              if constexpr (V1) {
+                const int gc = 4 * (ci >> 1) + 2 * (ci & 1);
+                *reinterpret_cast<float2*>(&dgf[gc + (gc / KQ) * 4]) =
+                    make_float2(__int_as_float(g[i].x), __int_as_float(g[i].z));
+              } else if constexpr (F32) {
                 const int b = g0 + ci / (2 * H), r = ci % (2 * H), gc = 4 * (r >> 1) + 2 * (r & 1);
                 const float x = __int_as_float(g[i].x), z = __int_as_float(g[i].z);
                 const short xh = dca::f2bf(x), zh = dca::f2bf(z);
@@ -639,7 +709,22 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       if (sh_int == -2) break;
       TSTAMPB(2);
       // ---- partial recurrent gradient over this wave's K quarter → red[wv]
-      if (k > 0) {
+      if (V1 && k > 0) {
+        const float* gp = &dgf[(wv * 4 + kg) * QP];
+        float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+#pragma unroll
+        for (int j = 0; j < KQ; j += 4) {
+          const float4 d4 = *reinterpret_cast<const float4*>(gp + j);
+          s0 = fmaf(wq[j], d4.x, s0);
+          s1 = fmaf(wq[j + 1], d4.y, s1);
+          s2 = fmaf(wq[j + 2], d4.z, s2);
+          s3 = fmaf(wq[j + 3], d4.w, s3);
+        }
+        float sum = (s0 + s1) + (s2 + s3);
+        sum += __shfl_xor(sum, 16, 64);
+        sum += __shfl_xor(sum, 32, 64);
+        if (kg == 0) red[wv][0][col] = sum;
+      } else if (k > 0) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           if (mt * 16 >= B) break;
@@ -737,7 +822,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
 #undef TSTAMPB
 }
 
-template <int MT, int KS, bool F32>
+template <int MT, int KS, bool F32, bool V1>
 __global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
     const float* __restrict__ xp4, const void* __restrict__ whh, const float* __restrict__ h0,
     const float* __restrict__ c0, short* __restrict__ hs, float* __restrict__ hsf, float* __restrict__ cs,
@@ -745,12 +830,12 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
     TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st, unsigned long long* trace,
     int knobs, const float* __restrict__ bias4) {
   __builtin_amdgcn_s_setprio(3);   // issue priority over co-resident waves of kernels overlapped on other streams
-  lstm_team_fwd_body<MT, KS, F32>(xp4, whh, h0, c0, hs, hsf, cs, gates4, hn, cn, xg_all, ctl, err, Btot, Bc, nch, S, sb,
+  lstm_team_fwd_body<MT, KS, F32, V1>(xp4, whh, h0, c0, hs, hsf, cs, gates4, hn, cn, xg_all, ctl, err, Btot, Bc, nch, S, sb,
                              st, trace, knobs, bias4);
   team_exit(ctl);
 }
 
-template <int MT, int KS, bool F32>
+template <int MT, int KS, bool F32, bool V1>
 __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
     const float* __restrict__ dhs, const float* __restrict__ gates4, const float* __restrict__ cs,
     const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
@@ -758,7 +843,7 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
     i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
     unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart) {
   __builtin_amdgcn_s_setprio(3);
-  lstm_team_bwd_body<MT, KS, F32>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, dh0, dc0, xg_all, ctl, err, Btot, Bc, nch,
+  lstm_team_bwd_body<MT, KS, F32, V1>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, dh0, dc0, xg_all, ctl, err, Btot, Bc, nch,
                              S, sb, st, trace, dg16, dbpart);
   team_exit(ctl);
 }
@@ -786,15 +871,24 @@ inline void plan(int B, int& nch, int& Bc, int& MT, int f32 = 0) {
 
 }  // namespace
 
-#define DCA_TEAM_DISPATCH(MT_, KS_, F32_, ...)                                               \
-  switch (((F32_) << 8) | ((MT_) << 4) | (KS_)) {                                           \
-    case 0x011: return __VA_ARGS__(1, 1, false); case 0x012: return __VA_ARGS__(1, 2, false); \
-    case 0x014: return __VA_ARGS__(1, 4, false); case 0x021: return __VA_ARGS__(2, 1, false); \
-    case 0x022: return __VA_ARGS__(2, 2, false); case 0x024: return __VA_ARGS__(2, 4, false); \
-    case 0x111: return __VA_ARGS__(1, 1, true);  case 0x112: return __VA_ARGS__(1, 2, true);  \
-    case 0x114: return __VA_ARGS__(1, 4, true);                                               \
-    default: return hipErrorInvalidValue;                                                     \
+// (F32_, V1_) = (0, 0) bf16 MFMA, (1, 0) bf16x3 MFMA, (1, 1) exact-fp32 VALU for one-row chains
+#define DCA_TEAM_DISPATCH(MT_, KS_, F32_, V1_, ...)                                                        \
+  switch (((V1_) << 12) | ((F32_) << 8) | ((MT_) << 4) | (KS_)) {                                          \
+    case 0x0011: return __VA_ARGS__(1, 1, false, false); case 0x0012: return __VA_ARGS__(1, 2, false, false); \
+    case 0x0014: return __VA_ARGS__(1, 4, false, false); case 0x0021: return __VA_ARGS__(2, 1, false, false); \
+    case 0x0022: return __VA_ARGS__(2, 2, false, false); case 0x0024: return __VA_ARGS__(2, 4, false, false); \
+    case 0x0111: return __VA_ARGS__(1, 1, true, false);  case 0x0112: return __VA_ARGS__(1, 2, true, false);  \
+    case 0x0114: return __VA_ARGS__(1, 4, true, false);                                                      \
+    case 0x1111: return __VA_ARGS__(1, 1, true, true);   case 0x1112: return __VA_ARGS__(1, 2, true, true);   \
+    case 0x1114: return __VA_ARGS__(1, 4, true, true);                                                       \
+    default: return hipErrorInvalidValue;                                                                    \
   }
+
+// one-row fp32 chains take the exact VALU variant (DCA_TEAM_V1=0 forces the bf16x3 MFMA one, for comparison)
+inline int use_v1(int f32, int Bc) {
+  static const int off = [] { const char* e = getenv("DCA_TEAM_V1"); return e && e[0] == '0'; }();
+  return (f32 && Bc == 1 && !off) ? 1 : 0;
+}
 
 // Workspace bytes (control block + per-team exchange buffers) for a launch of (B, H).
 extern "C" size_t dca_lstm_team_ctl_bytes() { return 256; }
@@ -830,12 +924,12 @@ extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const void* whh, const
   TeamCtl* ctl = reinterpret_cast<TeamCtl*>(ctl_mem);
   unsigned long long* xg = reinterpret_cast<unsigned long long*>(ws);
   const int KS = H / 128;
-#define DCA_F(mt, ks, f)                                                                                        \
-  (lstm_team_fwd_kernel<mt, ks, f><<<kMaxTeams * kT, kThreads, 0, stream>>>(xp4, whh, h0, c0, hs, hsf, cs, gates4, \
+#define DCA_F(mt, ks, f, v)                                                                                     \
+  (lstm_team_fwd_kernel<mt, ks, f, v><<<kMaxTeams * kT, kThreads, 0, stream>>>(xp4, whh, h0, c0, hs, hsf, cs, gates4, \
                                                                           hn, cn, xg, ctl, err, B, Bc, nch, S, sb, \
                                                                           st, trace, team_knobs(), bias4),         \
    hipGetLastError())
-  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, DCA_F)
+  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc), DCA_F)
 #undef DCA_F
 }
 
@@ -854,11 +948,11 @@ extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, c
   TeamCtl* ctl = reinterpret_cast<TeamCtl*>(ctl_mem);
   i32x4* xb = reinterpret_cast<i32x4*>(ws);
   const int KS = H / 128;
-#define DCA_B(mt, ks, f)                                                                                           \
-  (lstm_team_bwd_kernel<mt, ks, f><<<kMaxTeams * kT, kThreads, 0, stream>>>(dhs, gates4, cs, c0, dhn, dcn, whh,      \
+#define DCA_B(mt, ks, f, v)                                                                                        \
+  (lstm_team_bwd_kernel<mt, ks, f, v><<<kMaxTeams * kT, kThreads, 0, stream>>>(dhs, gates4, cs, c0, dhn, dcn, whh,      \
                                                                           dgates4, dh0, dc0, xb, ctl, err, B, Bc,  \
                                                                           nch, S, sb, st, trace, dg16, dbpart),    \
    hipGetLastError())
-  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, DCA_B)
+  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc), DCA_B)
 #undef DCA_B
 }
