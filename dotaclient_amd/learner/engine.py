@@ -331,10 +331,15 @@ class Learner:
 
     def _sync_and_step(self):
         """DP reduction + optimizer step. With the fused Adam on a multi-rank job the has-grad average is taken
-        inside the optimizer kernels (no separate pass over the gradient buffer after the all-reduce)."""
+        inside the optimizer kernels (no separate pass over the gradient buffer after the all-reduce). The fused
+        model's persistent-kernel error flag rides in the count-carrying bucket: if the recurrence failed on ANY
+        rank, every rank's Adam skips this step on the device (FusedPolicy.check_error raises at the iteration
+        boundary) — the reference raises before optimizer.step() (optimizer.py:674-676)."""
+        if self.backend == 'fused':
+            self.dp.err_flag.copy_(self.model.err)
         fold = self.dp.enabled and self.opt.use_kernels
         self.dp.sync(scale=not fold)
-        return self.opt.step(self.dp.counts, divide=fold)
+        return self.opt.step(self.dp.counts, divide=fold, skip=self.dp.err_flag)
 
     def _finish(self, vec):
         metrics = self._metrics_from_vec(vec.clone())

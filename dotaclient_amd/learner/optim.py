@@ -40,33 +40,38 @@ class FlatAdam:
             self._ops = ops.require()
 
     # ------------------------------------------------------------------------------------------------
-    def step(self, counts: Optional[torch.Tensor] = None, divide: bool = False):
+    def step(self, counts: Optional[torch.Tensor] = None, divide: bool = False,
+             skip: Optional[torch.Tensor] = None):
         """``divide``: ``flat.grad`` holds the DP all-reduce SUMS (DataParallel.sync(scale=False)); the has-grad
-        average grad / counts[param] is taken inside the optimizer instead of by a separate pass."""
+        average grad / counts[param] is taken inside the optimizer instead of by a separate pass. ``skip``: 1-element
+        f32 device flag; nonzero → nothing is applied this step (decided on the device, no host sync)."""
         if counts is None:
             counts = torch.ones(len(self.flat.params), device=self.flat.flat.device)
         if self.use_kernels:
-            return self._step_kernels(counts, divide)
-        return self.step_reference(counts, divide)
+            return self._step_kernels(counts, divide, skip)
+        return self.step_reference(counts, divide, skip)
 
-    def _step_kernels(self, counts, divide=False):
+    def _step_kernels(self, counts, divide=False, skip=None):
         b1, b2 = self.betas
         max_norm = self.max_grad_norm if self.max_grad_norm is not None else -1.0
         self._ops.adam_step(self.flat.flat, self.flat.grad, self.exp_avg, self.exp_avg_sq, self.flat.segment_ids,
                             counts, self.steps, self.last_grad_norm, float(self.lr), float(b1), float(b2),
-                            float(self.eps), float(max_norm), divide=bool(divide))
+                            float(self.eps), float(max_norm), divide=bool(divide), header=int(self.flat.header),
+                            skip=skip)
         return self.last_grad_norm
 
     @torch.no_grad()
-    def step_reference(self, counts, divide=False):
+    def step_reference(self, counts, divide=False, skip=None):
         b1, b2 = self.betas
-        g = self.flat.grad
+        g = torch.where(self.flat.segment_ids >= 0, self.flat.grad, torch.zeros_like(self.flat.grad))   # no header
         if divide:
             segc = self.flat.segment_ids.long().clamp_min(0)
             inv = torch.where(counts > 0, 1.0 / counts.clamp_min(1.0), torch.zeros_like(counts))
             g = g * torch.where(self.flat.segment_ids >= 0, inv[segc], torch.zeros_like(g))
         norm = torch.linalg.vector_norm(g)
         self.last_grad_norm.copy_(norm)
+        if skip is not None and float(skip.reshape(-1)[0]) != 0.0:
+            return norm
         if self.max_grad_norm is not None:
             coef = (self.max_grad_norm / (norm + 1e-6)).clamp(max=1.0)
             g = g * coef
@@ -93,9 +98,20 @@ class FlatAdam:
         return {'exp_avg': self.exp_avg.cpu(), 'exp_avg_sq': self.exp_avg_sq.cpu(), 'steps': self.steps.cpu(),
                 'lr': self.lr, 'betas': self.betas, 'eps': self.eps, 'max_grad_norm': self.max_grad_norm}
 
-    def load_state_dict(self, d):
+    def load_state_dict(self, d, keep_hparams: bool = True):
+        """Restore the moments and step counts. The hyperparameters this optimizer was built with (from the CLI)
+        win over the checkpointed ones unless ``keep_hparams`` is False; a difference is logged."""
         self.exp_avg.copy_(d['exp_avg'])
         self.exp_avg_sq.copy_(d['exp_avg_sq'])
         self.steps.copy_(d['steps'])
-        self.lr, self.betas, self.eps = d['lr'], tuple(d['betas']), d['eps']
-        self.max_grad_norm = d['max_grad_norm']
+        saved = {'lr': d['lr'], 'betas': tuple(d['betas']), 'eps': d['eps'], 'max_grad_norm': d['max_grad_norm']}
+        if not keep_hparams:
+            self.lr, self.betas, self.eps, self.max_grad_norm = (saved['lr'], saved['betas'], saved['eps'],
+                                                                 saved['max_grad_norm'])
+            return
+        cur = {'lr': self.lr, 'betas': tuple(self.betas), 'eps': self.eps, 'max_grad_norm': self.max_grad_norm}
+        diff = {k: (saved[k], cur[k]) for k in cur if saved[k] != cur[k]}
+        if diff:
+            import logging
+            logging.getLogger(__name__).warning('resume: keeping the configured optimizer hyperparameters over the '
+                                                'checkpointed ones (checkpoint, configured): %s', diff)

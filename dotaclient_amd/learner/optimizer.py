@@ -79,6 +79,7 @@ class OptimizerConfig:
     replay_recent: int = 0             # sample from the newest N sequences (0 = whole buffer)
     ingest: str = 'auto'               # 'device' (HIP return/GAE scan over the uploaded rollouts) | 'host' | 'auto'
     artifact_url: Optional[str] = None  # off-node mirror of checkpoints + events (reference: GCS bucket, §utils.artifacts)
+    allow_pickle_experience: bool = False  # accept reference-agent pickles (restricted unpickler); off: DCX1 only
 
 
 class Sequence:
@@ -164,6 +165,7 @@ class DotaOptimizer:
             torch.distributed.broadcast(t, 0)
             self.iteration_start = int(t.item())
             self.learner.broadcast_state(0)
+            self._broadcast_reward_stats(0)
         self.corrupt_rollouts = 0
         self.replay = None
         if cfg.replay_capacity or cfg.replay_gb:
@@ -177,6 +179,30 @@ class DotaOptimizer:
         if self.iteration_start == 1:
             self.upload_model(version=0)
 
+    def _broadcast_reward_stats(self, src: int = 0):
+        """Every rank normalises returns with rank ``src``'s per-team EMA(0.99) statistics after a resume (only rank
+        0 reads the trainer state): the team→row map, the device EMA rows and the host RunningMeanStd."""
+        import torch.distributed as tdist
+        keys = [sorted(self.team_keys.items())]
+        tdist.broadcast_object_list(keys, src)
+        self.team_keys = dict(keys[0])
+        run = [self.running.state_dict()]
+        tdist.broadcast_object_list(run, src)
+        self.running.load_state_dict(run[0])
+        ema = self.ema if self.device.type == 'cuda' else self.ema.contiguous()
+        tdist.broadcast(ema, src)
+        self.ema.copy_(ema)
+
+    def _agree_steps(self, n: int) -> int:
+        """Sequences this rank trains on this iteration: its full minibatches, reduced to the MINIMUM over the DP
+        ranks — ranks receive rollouts of different lengths, and a rank running one more train_step than the others
+        would pair its gradient all-reduce with the next iteration's (or hang on the last one)."""
+        if not pdist.is_distributed():
+            return n
+        t = torch.tensor([n], dtype=torch.int64, device=self.device if self.device.type == 'cuda' else 'cpu')
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
+        return int(t.item())
+
     # ------------------------------------------------------------------------------------------------
     def get_rollout(self) -> Rollout:
         while True:
@@ -184,7 +210,7 @@ class DotaOptimizer:
             if body is None:
                 raise TimeoutError('no experience received')
             try:
-                return decode_any(body)
+                return decode_any(body, allow_pickle=self.cfg.allow_pickle_experience)
             except CorruptMessage as e:       # drop it, like a lost message; the actors keep producing
                 self.corrupt_rollouts += 1
                 logger.warning('dropping corrupted experience message (%s); %d so far', e, self.corrupt_rollouts)
@@ -374,7 +400,7 @@ class DotaOptimizer:
         self.timer.stop('ingest')
         # all sequences of this iteration go to the device once; minibatches are gathered on-device
         self.timer.start('h2d')
-        n = n_seq - n_seq % cfg.batch_size
+        n = self._agree_steps(n_seq - n_seq % cfg.batch_size)
         if self.ingest == 'device':
             data = self._ingest_device(rollouts, n)
         else:

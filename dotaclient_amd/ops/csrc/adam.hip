@@ -8,6 +8,10 @@
 //                           hand-off — then applies clip + Adam to its float4 groups. Parameters with DP has-grad
 //                           count 0 are skipped (sparse-param semantics, reference distributed.py:40-42).
 // Memory-bound: ~28 B/element moved. Offsets are 64-element aligned so a float4 group never straddles parameters.
+// The first h4 float4 groups are the flat buffer's header (has-grad counts + the kernel-error flag, see
+// parallel/dp.py), never part of the gradient norm. `skip` (optional, device): when *skip != 0 — a persistent
+// recurrence kernel failed on some rank this step — neither the step counters nor any parameter / moment changes
+// (the reference raises before optimizer.step(), optimizer.py:674-676; here the decision stays on the device).
 #include "common.h"
 
 namespace {
@@ -27,9 +31,10 @@ __global__ __launch_bounds__(kThreads) void adam_norm_kernel(const float4* __res
                                                              float* __restrict__ partials,
                                                              const float* __restrict__ counts,
                                                              float* __restrict__ steps, int n_params,
-                                                             const int* __restrict__ seg, int divide) {
+                                                             const int* __restrict__ seg, int divide, int h4,
+                                                             const float* __restrict__ skip) {
   float acc = 0.f;
-  for (int i = blockIdx.x * kThreads + threadIdx.x; i < n4; i += gridDim.x * kThreads) {
+  for (int i = h4 + blockIdx.x * kThreads + threadIdx.x; i < n4; i += gridDim.x * kThreads) {
     float4 v = g[i];
     const float sc = grad_scale(seg, counts, i, divide);
     acc += sc * sc * (v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w);
@@ -44,7 +49,7 @@ __global__ __launch_bounds__(kThreads) void adam_norm_kernel(const float4* __res
     for (int w = 0; w < kThreads / dca::kWave; ++w) s += red[w];
     partials[blockIdx.x] = s;
   }
-  if (blockIdx.x == 0) {
+  if (blockIdx.x == 0 && !(skip && *skip != 0.f)) {
     for (int p = threadIdx.x; p < n_params; p += kThreads)
       if (counts[p] > 0.f) steps[p] += 1.f;
   }
@@ -54,7 +59,7 @@ __global__ __launch_bounds__(kThreads) void adam_update_kernel(
     float4* __restrict__ param, const float4* __restrict__ grad, float4* __restrict__ m, float4* __restrict__ v,
     const int* __restrict__ seg, int n4, const float* __restrict__ partials, int nparts,
     const float* __restrict__ counts, const float* __restrict__ steps, float* __restrict__ norm_out, float lr,
-    float b1, float b2, float eps, float max_norm, int divide) {
+    float b1, float b2, float eps, float max_norm, int divide, const float* __restrict__ skip) {
   __shared__ float red[kThreads / dca::kWave];
   __shared__ float s_coef;
   float acc = 0.f;
@@ -73,6 +78,7 @@ __global__ __launch_bounds__(kThreads) void adam_update_kernel(
     if (blockIdx.x == 0) *norm_out = norm;
   }
   __syncthreads();
+  if (skip && *skip != 0.f) return;          // failed step: the norm is reported, nothing is applied
   const float coef = s_coef;
   for (int i = blockIdx.x * kThreads + threadIdx.x; i < n4; i += gridDim.x * kThreads) {
     const int s = seg[i * 4];
@@ -105,17 +111,18 @@ __global__ __launch_bounds__(kThreads) void adam_update_kernel(
 extern "C" hipError_t dca_adam_step(float* param, const float* grad, float* m, float* v, const int* seg, int64_t n,
                                     const float* counts, float* steps, int n_params, float* partials,
                                     float* norm_out, float lr, float b1, float b2, float eps, float max_norm,
-                                    hipStream_t stream, int divide) {
+                                    hipStream_t stream, int divide, int64_t header, const float* skip) {
+  if (header < 0 || header % 4 != 0 || header > n) return hipErrorInvalidValue;
   const int n4 = (int)(n / 4);
   int blocks = (n4 + kThreads - 1) / kThreads;
   blocks = blocks < 1 ? 1 : (blocks > kMaxBlocks ? kMaxBlocks : blocks);
   adam_norm_kernel<<<blocks, kThreads, 0, stream>>>(reinterpret_cast<const float4*>(grad), n4, partials, counts,
-                                                    steps, n_params, seg, divide);
+                                                    steps, n_params, seg, divide, (int)(header / 4), skip);
   DCA_CHECK_LAUNCH();
   adam_update_kernel<<<blocks, kThreads, 0, stream>>>(
       reinterpret_cast<float4*>(param), reinterpret_cast<const float4*>(grad), reinterpret_cast<float4*>(m),
       reinterpret_cast<float4*>(v), seg, n4, partials, blocks, counts, steps, norm_out, lr, b1, b2, eps, max_norm,
-      divide);
+      divide, skip);
   DCA_CHECK_LAUNCH();
   return hipSuccess;
 }

@@ -7,7 +7,8 @@ extern "C" {
 
 hipError_t dca_adam_step(float* param, const float* grad, float* m, float* v, const int* seg, int64_t n,
                          const float* counts, float* steps, int n_params, float* partials, float* norm_out, float lr,
-                         float b1, float b2, float eps, float max_norm, hipStream_t st, int divide = 0);
+                         float b1, float b2, float eps, float max_norm, hipStream_t st, int divide, int64_t header,
+                         const float* skip);
 
 hipError_t dca_multi_axpy(float* const* dst, const float* const* src, const long long* numel, int n,
                           const float* scale, hipStream_t st);

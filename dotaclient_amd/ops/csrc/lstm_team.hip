@@ -12,7 +12,13 @@
 // Team formation is placement-robust: every workgroup reads HW_REG_XCC_ID and takes a ticket on its XCC's
 // counter; the first 32 of an XCC form its team, a leader commits the team only when all 32 arrived (bounded
 // wait), and committed teams pull chains from a shared queue — so any dispatch that lands ≥ 32 workgroups on at
-// least one XCD finishes every chain (if none does, *err = 3 and the caller falls back to lstm.hip).
+// least one XCD finishes every chain. An XCD whose team cannot form is not an error by itself (the other teams
+// drain the queue); only chains left UNPROCESSED are: the last workgroup to exit checks the queue and sets
+// *err = 3. Error codes (1 forward hand-off timeout, 2 backward timeout, 3 unprocessed chains) are sticky; the
+// learner reduces the flag across DP ranks with the has-grad counts and the fused Adam skips the update when it
+// is set (learner/engine.py), so a failed recurrence never reaches the weights; FusedPolicy.check_error raises at
+// the iteration boundary (before checkpoint / publish). DCA_TEAM_FAIL=1 makes every workgroup refuse to form a
+// team (fault-injection tests).
 //
 // Layouts (unit-major gates "(H,4)" so a hidden unit's 4 gates are one 16-byte vector):
 //   xp4    (B, S, H, 4) f32  x·W_ihᵀ + b_ih + b_hh with W_ih rows permuted to (unit, gate) order
@@ -126,12 +132,12 @@ __device__ __forceinline__ bool spin_fail(unsigned& spins, TeamCtl* ctl, unsigne
 
 // Team formation + chain queue. Returns the team id (≥ 0) or -1 if this workgroup must exit. Called by all
 // threads; thread 0 does the global traffic, the result is broadcast through LDS.
-__device__ int join_team(TeamCtl* ctl, unsigned* err, int* sh, unsigned* sh_epoch) {
+__device__ int join_team(TeamCtl* ctl, unsigned* err, int* sh, unsigned* sh_epoch, bool refuse = false) {
   if (threadIdx.x == 0) {
     *sh_epoch = ld_acq(&ctl->epoch);
     int res = -1;
     const unsigned x = xcc_id();
-    if (x < kMaxTeams) {
+    if (x < kMaxTeams && !refuse) {
       const unsigned r = add_agent(&ctl->xcnt[x], 1u);
       if (r < (unsigned)kT) {
         res = (int)x * 64 + (int)r;        // team x, member r
@@ -144,10 +150,7 @@ __device__ int join_team(TeamCtl* ctl, unsigned* err, int* sh, unsigned* sh_epoc
             __builtin_amdgcn_s_sleep(2);
           }
           st_rel(&ctl->state[x], ok ? 1u : 2u);
-          if (!ok) {
-            res = -1;
-            st_rel(err, 3u);                 // team formation failed on this XCD (placement/residency)
-          }
+          if (!ok) res = -1;                 // no team on this XCD (placement/residency); others may drain the queue
         } else {
           unsigned s;
           while ((s = ld_acq(&ctl->state[x])) == 0) {
@@ -194,13 +197,14 @@ __device__ int next_chain(TeamCtl* ctl, int team, int member, unsigned iter, int
   return *sh;
 }
 
-// Every workgroup calls this last (all threads). The last one to leave resets the control block for the next
-// launch on the same stream and advances the epoch.
-__device__ void team_exit(TeamCtl* ctl) {
+// Every workgroup calls this last (all threads). The last one to leave flags chains that no team processed
+// (*err = 3), then resets the control block for the next launch on the same stream and advances the epoch.
+__device__ void team_exit(TeamCtl* ctl, unsigned* err, int nch) {
   __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned e = add_agent(&ctl->exits, 1u);
     if (e == gridDim.x - 1) {
+      if (ld_acq(&ctl->next_chain) < (unsigned)nch) st_rel(err, 3u);
       for (int i = 0; i < 16; ++i) st_rel(&ctl->xcnt[i], 0u);
       for (int i = 0; i < kMaxTeams; ++i) {
         st_rel(&ctl->state[i], 0u);
@@ -253,7 +257,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
   __shared__ unsigned sh_epoch;
 
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-  const int me = join_team(ctl, err, &sh_int, &sh_epoch);
+  const int me = join_team(ctl, err, &sh_int, &sh_epoch, (knobs >> 11) & 1);
   const unsigned epoch = sh_epoch;
   if (me < 0) return;
   const int team = me >> 6, m = me & 63;
@@ -832,7 +836,7 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
   __builtin_amdgcn_s_setprio(3);   // issue priority over co-resident waves of kernels overlapped on other streams
   lstm_team_fwd_body<MT, KS, F32, V1>(xp4, whh, h0, c0, hs, hsf, cs, gates4, hn, cn, xg_all, ctl, err, Btot, Bc, nch, S, sb,
                              st, trace, knobs, bias4);
-  team_exit(ctl);
+  team_exit(ctl, err, nch);
 }
 
 template <int MT, int KS, bool F32, bool V1>
@@ -845,13 +849,15 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
   __builtin_amdgcn_s_setprio(3);
   lstm_team_bwd_body<MT, KS, F32, V1>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, dh0, dc0, xg_all, ctl, err, Btot, Bc, nch,
                              S, sb, st, trace, dg16, dbpart);
-  team_exit(ctl);
+  team_exit(ctl, err, nch);
 }
 
-// DCA_TEAM_KNOBS = pre_sleep | skip_outputs << 8 | probe_first << 9 | xp_step0 << 10 (latency experiments only)
+// DCA_TEAM_KNOBS = pre_sleep | skip_outputs << 8 | probe_first << 9 | xp_step0 << 10 (latency experiments only);
+// DCA_TEAM_FAIL=1 sets bit 11: no workgroup joins a team (fault injection: every chain left unprocessed → err 3)
 inline int team_knobs() {
   const char* e = getenv("DCA_TEAM_KNOBS");
-  return e ? atoi(e) : 0;
+  const char* f = getenv("DCA_TEAM_FAIL");
+  return (e ? atoi(e) : 0) | ((f && f[0] == '1') ? (1 << 11) : 0);
 }
 
 inline void plan(int B, int& nch, int& Bc, int& MT, int f32 = 0) {

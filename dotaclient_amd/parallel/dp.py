@@ -13,8 +13,9 @@ Re-designed for MI355X / RCCL over xGMI rather than translated:
 * all parameters live as views of ONE flat fp32 buffer and all gradients as views of ONE flat gradient buffer,
   so the reference's 60 sequential per-parameter gloo calls become a handful of large bucketed collectives (a
   ring all-reduce over xGMI is per-link bandwidth bound; few large messages amortise RCCL launch latency);
-* the per-parameter has-grad counts travel as an extra float segment *inside* the last bucket — no separate
-  collective;
+* the per-parameter has-grad counts — and the persistent kernels' error flag — travel in a header segment at the
+  START of the flat gradient buffer, inside the last bucket (which always holds the first-registered parameters):
+  one contiguous all-reduce, no separate collective and no per-step concatenation / copy;
 * with ``overlap=True`` a bucket's all-reduce is issued on a dedicated comm stream from a post-accumulate-grad hook
   as soon as every parameter in it has its gradient, so communication overlaps the rest of backward (buckets are
   formed in reverse registration order ≈ backward order);
@@ -37,6 +38,8 @@ class FlatParams:
     ``flat[offsets[i]:offsets[i]+numel[i]]`` is parameter i; autograd accumulates in place into the matching
     view of ``grad`` because ``.grad`` is pre-set (zero it with :meth:`zero_grad`, never set it to None).
     Offsets are 64-element aligned so each parameter starts on a 256-B boundary (16-B vector loads in kernels).
+    The first ``header`` elements (``n_params + 1`` rounded up to 64) hold no parameter: in ``grad`` they carry the
+    DP has-grad flags / counts and the kernel-error flag (:class:`DataParallel`); segment id -1, never stepped.
     """
 
     ALIGN = 64
@@ -50,8 +53,9 @@ class FlatParams:
                 self.params.append(p)
         device = torch.device(device) if device is not None else self.params[0].device
         self.numel = [p.numel() for p in self.params]
+        self.header = (len(self.params) + 1 + self.ALIGN - 1) // self.ALIGN * self.ALIGN
         self.offsets = []
-        off = 0
+        off = self.header
         for n in self.numel:
             self.offsets.append(off)
             off += (n + self.ALIGN - 1) // self.ALIGN * self.ALIGN
@@ -99,9 +103,12 @@ class DataParallel:
         self.enabled = self.world > 1
         self.n_params = len(self.flat.params)
         dev = self.flat.grad.device
-        # has-grad flags, one float per parameter (1 = this rank produced a gradient this step)
-        self.has_grad = torch.zeros(self.n_params, device=dev, dtype=self.flat.grad.dtype)
-        self.counts = torch.ones(self.n_params, device=dev, dtype=self.flat.grad.dtype)
+        # has-grad flags, one float per parameter (1 = this rank produced a gradient this step), and the error flag
+        # of the persistent kernels: views of the gradient buffer's header, all-reduced with the last bucket —
+        # afterwards the same memory holds the has-grad COUNTS and the number of ranks whose step failed
+        self.has_grad = self.flat.grad[:self.n_params]
+        self.err_flag = self.flat.grad[self.n_params:self.n_params + 1]
+        self.counts = self.has_grad
         self.overlap = overlap and self.enabled and dev.type == 'cuda'
         self._build_buckets(bucket_cap_mb)
         self._comm_stream = torch.cuda.Stream(device=dev) if self.overlap else None
@@ -140,6 +147,14 @@ class DataParallel:
             lo = min(self.flat.offsets[i] for i in idxs)
             hi = max(self.flat.offsets[i] + self.flat.numel[i] for i in idxs)
             self.bucket_ranges.append((lo, hi))
+        self._extend_last()
+
+    def _extend_last(self):
+        """The last bucket holds parameter 0, so its range starts right after the header: extend it over the header
+        (has-grad flags + error flag ride along in the same all-reduce)."""
+        lo, hi = self.bucket_ranges[-1]
+        assert 0 in self.buckets[-1] and lo == self.flat.header, 'the count-carrying bucket must hold parameter 0'
+        self.bucket_ranges[-1] = (0, hi)
 
     def split_buckets(self, early: Sequence[int], cap_mb: float = 8.0) -> bool:
         """Bucket layout for a step whose gradients finish in two phases (the learner's direct step): the EARLY
@@ -149,8 +164,8 @@ class DataParallel:
         early = sorted(set(early))
         if not early or len(early) >= self.n_params or early != list(range(early[0], early[-1] + 1)):
             return False
-        if early[0] != 0 and early[-1] != self.n_params - 1:
-            return False                     # early must be a prefix or suffix: both bucket ranges then contiguous
+        if early[-1] != self.n_params - 1:
+            return False                     # early must be a suffix: the late bucket then starts at the header
         late = [i for i in range(self.n_params) if i not in set(early)]
         cap = max(1, int(cap_mb * 1024 * 1024 / self.flat.grad.element_size()))
         buckets, cur, size = [], [], 0
@@ -166,6 +181,7 @@ class DataParallel:
         self.param_bucket = {i: b for b, idxs in enumerate(buckets) for i in idxs}
         self.bucket_ranges = [(min(self.flat.offsets[i] for i in idxs),
                                max(self.flat.offsets[i] + self.flat.numel[i] for i in idxs)) for idxs in buckets]
+        self._extend_last()
         return True
 
     def launch_early(self):
@@ -215,15 +231,14 @@ class DataParallel:
         """Finish the gradient reduction. Afterwards ``flat.grad`` holds the has-grad-averaged gradient and
         ``counts`` the number of ranks that had a gradient for each parameter. ``scale=False`` leaves the SUMS in
         ``flat.grad`` for an optimizer that divides by the counts itself (FlatAdam.step(divide=True))."""
-        if not self.enabled:
-            self.counts.copy_(self.has_grad)
+        if not self.enabled:                  # counts IS has_grad (same header view)
             return
         # Launch whatever the hooks did not (params without grad on this rank, the count-carrying last bucket).
         for b in range(self._next, len(self.buckets) - 1):
             self._launch(b)
-        # The last bucket carries the has-grad flags appended as an extra segment.
+        # The last bucket starts at 0: header (has-grad flags, error flag) + the first parameters, one view.
         lo, hi = self.bucket_ranges[-1]
-        last = torch.cat([self.flat.grad[lo:hi], self.has_grad])
+        last = self.flat.grad[lo:hi]
         if self.overlap:
             cur = torch.cuda.current_stream(last.device)
             self._comm_stream.wait_stream(cur)
@@ -234,18 +249,17 @@ class DataParallel:
             cur.wait_stream(self._comm_stream)
         else:
             dist.all_reduce(last, op=dist.ReduceOp.SUM, group=self.group)
-        self.flat.grad[lo:hi].copy_(last[: hi - lo])
-        self.counts.copy_(last[hi - lo:])
         self._works = []
         self._pending = {}
         self._next = 0
         if not scale:
             return
-        # grad /= count  (count 0 → gradient stays 0 and the optimizer skips the parameter)
+        # grad /= count  (count 0 → gradient stays 0 and the optimizer skips the parameter); the header keeps the counts
+        h = self.flat.header
         inv = torch.where(self.counts > 0, 1.0 / self.counts.clamp_min(1.0), torch.zeros_like(self.counts))
-        seg = self.flat.segment_ids
-        scale = torch.where(seg >= 0, inv[seg.clamp_min(0).long()], torch.zeros_like(self.flat.grad))
-        self.flat.grad.mul_(scale)
+        seg = self.flat.segment_ids[h:]
+        scale = torch.where(seg >= 0, inv[seg.clamp_min(0).long()], torch.zeros_like(self.flat.grad[h:]))
+        self.flat.grad[h:].mul_(scale)
 
     def remove_hooks(self):
         for h in self._hooks:

@@ -20,7 +20,10 @@ Codecs:
   pickling torch tensors.
 * :meth:`Rollout.to_reference_dict` / :meth:`Rollout.from_reference_dict` — exact reference message layout, so a
   reference agent's pickled message can be ingested and ours can be read by the reference optimizer.
-  Only trusted in-cluster producers are unpickled (:func:`decode_any`), mirroring the reference's trust model.
+  Reference pickles are decoded only when explicitly allowed (``decode_any(allow_pickle=True)``, the learner's
+  ``--allow-pickle-experience``), and then by a restricted unpickler that can build nothing but dicts, lists,
+  strings, numbers and numpy arrays — an unauthenticated broker port must not be a code-execution endpoint.
+  Any message that fails to decode (either format) raises :class:`CorruptMessage`.
 """
 from __future__ import annotations
 
@@ -151,11 +154,44 @@ def decode(buf: bytes) -> Rollout:
                    done=header['done'], layout=tuple(header['layout']), **{k: arrays.get(k) for k in _ARRAYS})
 
 
-def decode_any(buf: bytes) -> Rollout:
-    """DCX1 binary, or a reference agent's pickled dict (trusted in-cluster producer only)."""
-    if buf[:4] == MAGIC:
-        return decode(buf)
-    return Rollout.from_reference_dict(pickle.loads(buf))
+def _storage_from_bytes(b):
+    # torch.storage._load_from_bytes would torch.load(weights_only=False) attacker-controlled bytes
+    import torch
+    return torch.load(io.BytesIO(b), weights_only=True)
+
+
+class _ArrayUnpickler(pickle.Unpickler):
+    """Unpickler for the reference's experience dicts (numpy arrays and torch tensors in plain containers): only
+    array / tensor reconstruction can be resolved — tensor storages through a weights-only ``torch.load`` — so a
+    crafted message cannot run code."""
+    _ALLOWED = {('numpy.core.multiarray', '_reconstruct'), ('numpy._core.multiarray', '_reconstruct'),
+                ('numpy.core.multiarray', 'scalar'), ('numpy._core.multiarray', 'scalar'),
+                ('numpy', 'ndarray'), ('numpy', 'dtype'), ('collections', 'OrderedDict'),
+                ('torch._utils', '_rebuild_tensor_v2')}
+
+    def find_class(self, module, name):
+        if (module, name) == ('torch.storage', '_load_from_bytes'):
+            return _storage_from_bytes
+        if (module, name) in self._ALLOWED:
+            return super().find_class(module, name)
+        raise pickle.UnpicklingError(f'global {module}.{name} is not allowed in an experience message')
+
+
+def decode_any(buf: bytes, allow_pickle: bool = False) -> Rollout:
+    """DCX1 binary, or (``allow_pickle``) a reference agent's pickled dict through :class:`_ArrayUnpickler`. Every
+    decode failure surfaces as :class:`CorruptMessage` (the learner drops the message and carries on)."""
+    try:
+        if buf[:4] == MAGIC:
+            return decode(buf)
+        if not allow_pickle:
+            raise CorruptMessage('not a DCX1 message (reference pickles need allow_pickle / '
+                                 '--allow-pickle-experience)')
+        return Rollout.from_reference_dict(_ArrayUnpickler(io.BytesIO(buf)).load())
+    except CorruptMessage:
+        raise
+    except (pickle.UnpicklingError, ValueError, KeyError, TypeError, IndexError, AttributeError, EOFError,
+            struct.error, UnicodeDecodeError) as e:
+        raise CorruptMessage(f'undecodable experience message: {e!r}') from e
 
 
 # ---- model messages -------------------------------------------------------------------------------------------

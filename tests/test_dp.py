@@ -215,3 +215,53 @@ def test_split_buckets_on_policy_layout(preset):
     (llo, lhi) = dp.bucket_ranges[-1]
     for lo, hi in dp.bucket_ranges[:-1]:
         assert hi <= llo or lo >= lhi
+
+
+def _uneven_worker(rank, world, port, root, q):
+    """Every rank gets rollouts of different lengths: 5 and 7 sequences of 16 steps → 4 and 6 full minibatch rows
+    of 2. Without the MIN agreement rank 1 would run a third train_step (and all-reduce) that rank 0 never joins."""
+    try:
+        _init(rank, world, port)
+        import numpy as np
+        from dotaclient_amd.learner.optimizer import DotaOptimizer, OptimizerConfig
+        from dotaclient_amd.transport.broker import InProcBroker
+        from dotaclient_amd.transport.codec import Rollout, encode
+        cfg = OptimizerConfig(log_dir=os.path.join(root, f'r{rank}'), batch_size=2, seq_len=16, seq_per_epoch=4,
+                              epochs=1, model='lstm128', device='cpu', backend='torch', xp_timeout=30)
+        br = InProcBroker()
+        opt = DotaOptimizer(cfg, br, checkpoint=rank == 0)
+        rng = np.random.default_rng(rank)
+        U = opt.policy_cfg.layout.max_units
+        for T in ((16 * 5 - 3,) if rank == 0 else (16 * 7 - 1,)):
+            act = np.zeros((T, 21 + U), np.uint8)
+            act[:, 0] = 1
+            br.publish_experience(encode(Rollout(
+                game_id=f'g{rank}', team_id=2, player_id=0, weight_version=0,
+                env=rng.standard_normal((T, 3)).astype(np.float32),
+                units=rng.standard_normal((T, U, 10)).astype(np.float32), actions=act,
+                masks=np.ones((T, 21 + U), np.uint8), rewards=rng.standard_normal((T, 9)),
+                logp=np.full(T, -1.0, np.float32), values=np.zeros(T, np.float32), done=True)))
+        opt.run(iterations=1)
+        q.put((rank, opt.learner.flat.flat.numpy().copy(), opt.learner.n_steps))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e), None))
+
+
+def test_ranks_with_uneven_rollouts_run_the_same_steps(tmp_path):
+    world, port = 2, _free_port()
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_uneven_worker, args=(r, world, port, str(tmp_path), q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    for _ in range(world):
+        r, flat, steps = q.get(timeout=300)
+        assert steps is not None, flat
+        res[r] = (flat, steps)
+    for p in ps:
+        p.join(timeout=60)
+    assert res[0][1] == res[1][1] == 2            # min(5, 7) sequences → 4 rows → 2 minibatches on both ranks
+    assert (res[0][0] == res[1][0]).all()

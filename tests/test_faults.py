@@ -41,6 +41,21 @@ def test_crc_rejects_every_single_byte_flip():
     assert decode(body).game_id == 'g0'
 
 
+def test_corrupted_magic_bytes_are_dropped_not_unpickled(tmp_path):
+    """A flipped byte inside the 4 magic bytes used to route the message to pickle.loads (UnpicklingError crashed
+    the learner): it must be dropped like any other corrupted message."""
+    br = InProcBroker()
+    opt = _optimizer(tmp_path, br)
+    for i in range(4):
+        body = bytearray(encode(_rollout(i)))
+        if i == 0:
+            body[0] ^= 0x5A                  # byte 0 of the DCX1 magic
+        br.publish_experience(bytes(body))
+    opt.run(iterations=1)
+    assert opt.corrupt_rollouts == 1
+    assert np.isfinite(opt.last_metrics['loss/sum'])
+
+
 def _optimizer(tmp_path, br, **kw):
     from dotaclient_amd.learner.optimizer import DotaOptimizer, OptimizerConfig
     cfg = OptimizerConfig(log_dir=str(tmp_path), model='lstm128', epochs=1, seq_per_epoch=2, batch_size=2,

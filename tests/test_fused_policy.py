@@ -232,3 +232,27 @@ def test_graph_capture_with_rccl_process_group(gpu_ops):
     p.join(timeout=60)
     assert res[0] == 'ok', res
     assert res[2] and res[1] == res[1]
+
+
+@pytest.mark.parametrize('precision', ['fp32', 'bf16'])
+def test_team_formation_failure_never_reaches_the_weights(gpu_ops, monkeypatch, precision):
+    """DCA_TEAM_FAIL=1: no workgroup joins a recurrence team, so every chain is left unprocessed. The kernel flags
+    err = 3 (checked by its last workgroup), the flag rides in the count-carrying all-reduce bucket, and the fused
+    Adam skips the step on the device — parameters, moments and step counts unchanged — before check_error raises
+    at the host boundary (reference: NaN check raises before optimizer.step(), optimizer.py:674-676)."""
+    cfg = get_config('lstm128')
+    torch.manual_seed(0)
+    L = Learner(Policy(cfg), LossConfig(algo='ppo'), device='cuda', backend='fused', dp=False, precision=precision)
+    batch = make_batch(4, 24, cfg.layout, cfg.hidden, device='cuda', seed=1)
+    L.train_step(batch)                                   # a healthy step first
+    torch.cuda.synchronize()
+    L.model.check_error()
+    before = (L.flat.flat.clone(), L.opt.exp_avg.clone(), L.opt.steps.clone())
+    monkeypatch.setenv('DCA_TEAM_FAIL', '1')
+    L.train_step(batch)
+    torch.cuda.synchronize()
+    assert int(L.model.err.item()) == 3
+    assert torch.equal(L.flat.flat, before[0]) and torch.equal(L.opt.exp_avg, before[1])
+    assert torch.equal(L.opt.steps, before[2])
+    with pytest.raises(RuntimeError, match='error code 3'):
+        L.model.check_error()

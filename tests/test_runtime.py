@@ -64,9 +64,27 @@ def test_codec_roundtrip_binary_and_reference_pickle():
     assert set(ref['states']) == {'env', 'allied_heroes', 'enemy_heroes', 'allied_nonheroes', 'enemy_nonheroes',
                                   'allied_towers', 'enemy_towers'}
     assert ref['states']['enemy_heroes'].shape == (30, 5, 10) and ref['actions']['target_unit'].shape == (30, 40)
-    back = decode_any(pickle.dumps(ref))
+    back = decode_any(pickle.dumps(ref), allow_pickle=True)
     np.testing.assert_array_equal(back.units, r.units)
     np.testing.assert_array_equal(back.actions, r.actions)
+
+
+def test_pickle_experience_is_opt_in_and_restricted():
+    """Reference pickles are refused unless allowed, and even then only arrays / containers can be built: a
+    message that would run code on unpickling is a CorruptMessage, not an exploit."""
+    import os
+    from dotaclient_amd.transport.codec import CorruptMessage
+    ref = _rollout().to_reference_dict()
+    with pytest.raises(CorruptMessage):
+        decode_any(pickle.dumps(ref))                  # default: DCX1 only
+
+    class Evil:
+        def __reduce__(self):
+            return (os.system, ('echo pwned > /dev/null',))
+    with pytest.raises(CorruptMessage):
+        decode_any(pickle.dumps({'game_id': Evil()}), allow_pickle=True)
+    with pytest.raises(CorruptMessage):
+        decode_any(b'\x80\x04garbage', allow_pickle=True)
 
 
 def test_inproc_broker_recent_history_and_backpressure():
