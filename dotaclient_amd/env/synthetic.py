@@ -14,6 +14,11 @@ that produces ``CMsgBotWorldState`` protobufs with every field the featurizer / 
 
 The service is advanced after *both* teams have acted (the reference loop is observe(R) → act(R) →
 observe(D) → act(D), agent.py:802-827). One observation = ``ticks_per_observation`` ticks at 30 tps.
+
+This module is also the ORACLE of the native vectorised engine (``native/vecenv.h``, :mod:`dotaclient_amd.env.vec`),
+which reproduces it bit for bit: CPython's MT19937 seeding and ``random()``, dict-ordered unit iteration, and
+geometry written with operations that are correctly rounded in both languages (``_dist`` is sqrt(dx²+dy²), not
+``math.hypot``, whose CPython algorithm differs from libm's).
 """
 from __future__ import annotations
 
@@ -32,6 +37,10 @@ CREEP_SPAWN = {TEAM_RADIANT: (-4700.0, -4300.0), TEAM_DIRE: (4000.0, 3600.0)}
 T1_MID = {TEAM_RADIANT: (-1544.0, -1408.0), TEAM_DIRE: (524.0, 652.0)}
 ANCIENT = {TEAM_RADIANT: (-5400.0, -5000.0), TEAM_DIRE: (5200.0, 4700.0)}
 OPP = {TEAM_RADIANT: TEAM_DIRE, TEAM_DIRE: TEAM_RADIANT}
+
+def _hypot(dx: float, dy: float) -> float:
+    return math.sqrt(dx * dx + dy * dy)
+
 
 ANIM_TOWER_IDLE = 1500
 ANIM_TOWER_ATTACK = 1503
@@ -156,11 +165,11 @@ class SyntheticGame:
     # -------------------------------------------------------------------------------------------------
     @staticmethod
     def _dist(a: SimUnit, b: SimUnit) -> float:
-        return math.hypot(a.x - b.x, a.y - b.y)
+        return _hypot(a.x - b.x, a.y - b.y)
 
     def _move_towards(self, u: SimUnit, tx: float, ty: float, dt: float):
         dx, dy = tx - u.x, ty - u.y
-        d = math.hypot(dx, dy)
+        d = _hypot(dx, dy)
         if d < 1e-3:
             return
         step = min(d, u.speed * dt)
@@ -357,7 +366,7 @@ class SyntheticGame:
         allies = [u for u in self.units.values() if u.team_id == team_id and u.alive]
         for u in self.units.values():
             if self.fog and u.team_id != team_id and u.unit_type != UnitType.TOWER:
-                if not any(math.hypot(a.x - u.x, a.y - u.y) <= VISION_RADIUS for a in allies):
+                if not any(_hypot(a.x - u.x, a.y - u.y) <= VISION_RADIUS for a in allies):
                     continue
             m = ws.units.add(handle=u.handle, unit_type=u.unit_type, name=u.name, team_id=u.team_id,
                              level=u.level, is_alive=u.alive, player_id=u.player_id, facing=u.facing,

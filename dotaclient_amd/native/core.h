@@ -176,8 +176,7 @@ void parse_world(const uint8_t* data, size_t n, World& w) {
 // ============================================================================================================
 // featurizer (reference agent.py:496-637)
 // ============================================================================================================
-constexpr float kMapHalf = 7000.f;
-constexpr float kPi = 3.14159265358979323846f;
+constexpr double kMapHalf = 7000.0;
 
 bool ends_with(std::string_view s, std::string_view suf) {
   return s.size() >= suf.size() && s.substr(s.size() - suf.size()) == suf;
@@ -203,25 +202,28 @@ void unit_rows(const std::vector<const Unit*>& list, const Unit& hero, bool only
     if (!u.is_alive) continue;
     if (only_self && u.handle != hero.handle) continue;
     if (i >= max_units) break;
-    const float hp = u.health_max ? (float)u.health / (float)u.health_max : 0.f;
+    // every feature in double, cast once (the python featurizer's arithmetic, agent.py:521-532), so the native
+    // path is bit-identical to featurizer.py rather than merely close
+    const double hp = u.health_max ? (double)u.health / (double)u.health_max : 0.0;
     const double dx = (double)hero.x - (double)u.x, dy = (double)hero.y - (double)u.y;
-    const float dist = (float)std::sqrt(dx * dx + dy * dy);
+    const double dist = std::sqrt(dx * dx + dy * dy);
+    const double tau = 2.0 * 3.14159265358979323846;
     float* r = m + i * 10;
-    r[0] = 1.f - hp;
-    r[1] = u.x / kMapHalf;
-    r[2] = u.y / kMapHalf;
-    r[3] = u.z / 512.f - 0.5f;
-    r[4] = dist / kMapHalf - 0.5f;
-    r[5] = std::sin(u.facing * 2.f * kPi / 360.f);
-    r[6] = std::cos(u.facing * 2.f * kPi / 360.f);
-    r[7] = (dist <= (float)hero.attack_range ? 1.f : 0.f) - 0.5f;
+    r[0] = (float)(1.0 - hp);
+    r[1] = (float)((double)u.x / kMapHalf);
+    r[2] = (float)((double)u.y / kMapHalf);
+    r[3] = (float)((double)u.z / 512.0 - 0.5);
+    r[4] = (float)(dist / kMapHalf - 0.5);
+    r[5] = (float)std::sin((double)u.facing * tau / 360.0);
+    r[6] = (float)std::cos((double)u.facing * tau / 360.0);
+    r[7] = (dist <= (double)hero.attack_range ? 1.f : 0.f) - 0.5f;
     r[8] = attacking(u, hero) - 0.5f;
     r[9] = attacking(hero, u) - 0.5f;
     int64_t h = (int64_t)u.handle;
     if (u.invuln || u.attack_immune) h = -1;
     else if (u.team_id == opp && u.unit_type == TOWER && u.anim == 1500) h = -1;
     else if (u.team_id == hero.team_id && u.unit_type == TOWER) h = -1;
-    else if (u.team_id == hero.team_id && hp > 0.5f) h = -1;
+    else if (u.team_id == hero.team_id && hp > 0.5) h = -1;
     handles[i] = h;
     ++i;
   }
@@ -234,8 +236,8 @@ int featurize_one(const World& w, int player_id, int team_id, const int* counts,
   for (const Unit& u : w.units)
     if (u.unit_type == HERO && u.player_id == player_id) { hero = &u; break; }
   if (!hero) return -1;
-  env[0] = w.dota_time / 1200.f;
-  env[1] = std::sin(w.dota_time * 2.f * kPi / 60.f);
+  env[0] = (float)((double)w.dota_time / 1200.0);
+  env[1] = (float)std::sin((double)w.dota_time * (2.0 * 3.14159265358979323846) / 60.0);
   env[2] = team_id == 3 ? -0.2f : 0.2f;
   std::vector<const Unit*> ah, eh, anh, enh, ac, ec, at, et;
   for (const Unit& u : w.units) {

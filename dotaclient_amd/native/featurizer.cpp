@@ -13,7 +13,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <map>
+
 #include "core.h"
+#include "vecenv.h"
 
 namespace py = pybind11;
 
@@ -99,6 +102,186 @@ class ShmRing {
   RingCore r_;
 };
 
+// ---- vectorised self-play runtime (vecenv.h) -----------------------------------------------------------------
+template <typename T>
+T* checked(py::array a, std::vector<py::ssize_t> shape, const char* what, bool writeable) {
+  if (!a.dtype().is(py::dtype::of<T>())) throw std::invalid_argument(std::string(what) + ": wrong dtype");
+  if (!(a.flags() & py::array::c_style)) throw std::invalid_argument(std::string(what) + ": must be C-contiguous");
+  if (a.ndim() != (py::ssize_t)shape.size()) throw std::invalid_argument(std::string(what) + ": wrong rank");
+  for (size_t i = 0; i < shape.size(); ++i)
+    if (shape[i] >= 0 && a.shape(i) != shape[i]) throw std::invalid_argument(std::string(what) + ": wrong shape");
+  if (writeable && !a.writeable()) throw std::invalid_argument(std::string(what) + ": must be writeable");
+  return static_cast<T*>(a.mutable_data());
+}
+
+class PyVecEnv {
+ public:
+  PyVecEnv(int n_games, int mode, uint64_t seed, double max_dota_time, long rollout_size, int hidden_stride,
+           int hidden_size, std::vector<int> counts, int threads, double latest_weights_prob, bool validation,
+           bool fog, double start_time, std::string tag)
+      : env_(make(n_games, mode, seed, max_dota_time, rollout_size, hidden_stride, hidden_size, counts, threads,
+                  latest_weights_prob, validation, fog, start_time, tag)) {
+    S_ = env_.slots();
+    U_ = env_.units();
+    H_ = hidden_size;
+  }
+  py::array_t<int32_t> begin_step() {
+    std::vector<int> r;
+    {
+      py::gil_scoped_release rel;
+      r = env_.begin_step();
+    }
+    return py::array_t<int32_t>((py::ssize_t)r.size(), r.data());
+  }
+  py::array_t<int32_t> observe(py::array env, py::array units, py::array handles, py::array active) {
+    float* e = checked<float>(env, {S_, 3}, "env", true);
+    float* u = checked<float>(units, {S_, U_, 10}, "units", true);
+    int64_t* h = checked<int64_t>(handles, {S_, U_}, "handles", true);
+    uint8_t* a = checked<uint8_t>(active, {S_}, "active", true);
+    std::vector<int> need;
+    {
+      py::gil_scoped_release rel;
+      need = env_.observe(e, u, h, a);
+    }
+    return py::array_t<int32_t>((py::ssize_t)need.size(), need.data());
+  }
+  void act(py::array idx, py::array act, py::array msk, py::array logp, py::array value, py::object hidden,
+           py::object hidden_slots, py::array handles, long weight_version) {
+    const int A = 21 + U_;
+    const int32_t* ix = checked<int32_t>(idx, {S_, 4}, "idx", false);
+    const uint8_t* ac = checked<uint8_t>(act, {S_, A}, "act", false);
+    const uint8_t* mk = checked<uint8_t>(msk, {S_, A}, "msk", false);
+    const float* lp = checked<float>(logp, {S_}, "logp", false);
+    const float* vl = checked<float>(value, {S_}, "value", false);
+    const int64_t* hd = checked<int64_t>(handles, {S_, U_}, "handles", false);
+    const float* hid = nullptr;
+    const int* hs = nullptr;
+    int nh = 0;
+    if (!hidden.is_none()) {
+      py::array ha = hidden.cast<py::array>(), sa = hidden_slots.cast<py::array>();
+      nh = (int)sa.shape(0);
+      hid = checked<float>(ha, {nh, 2, H_}, "hidden", false);
+      hs = checked<int32_t>(sa, {nh}, "hidden_slots", false);
+      for (int i = 0; i < nh; ++i)
+        if (hs[i] < 0 || hs[i] >= S_) throw std::invalid_argument("hidden_slots out of range");
+    }
+    for (py::ssize_t i = 0; i < (py::ssize_t)S_ * 4; ++i)
+      if ((i % 4 == 0 && (ix[i] < 0 || ix[i] > 2)) || ((i % 4 == 1 || i % 4 == 2) && (ix[i] < 0 || ix[i] > 8)))
+        throw std::invalid_argument("idx: action index out of range");
+    py::gil_scoped_release rel;
+    env_.act(ix, ac, mk, lp, vl, hid, hs, nh, hd, weight_version);
+  }
+  py::list pop_rollouts() {
+    std::vector<std::string> r = env_.pop_rollouts();
+    py::list out;
+    for (auto& b : r) out.append(py::bytes(b));
+    return out;
+  }
+  py::list pop_results() {
+    py::list out;
+    for (auto& r : env_.pop_results()) out.append(py::make_tuple(r.first, r.second));
+    return out;
+  }
+  py::array_t<int32_t> opponent_slots() {
+    std::vector<int> s = env_.opponent_slots();
+    return py::array_t<int32_t>((py::ssize_t)s.size(), s.data());
+  }
+  int slots() const { return S_; }
+  int players_per_game() const { return env_.players_per_game(); }
+  long games_finished() const { return env_.games_finished(); }
+  long steps_taken() const { return env_.steps_taken(); }
+  long rollouts_sent() const { return env_.rollouts_sent(); }
+  double dota_time(int g) const { return env_.dota_time(g); }
+  int status(int g) const { return env_.status(g); }
+
+ private:
+  static VecConfig make(int n_games, int mode, uint64_t seed, double max_dota_time, long rollout_size,
+                        int hidden_stride, int hidden_size, const std::vector<int>& counts, int threads,
+                        double latest_weights_prob, bool validation, bool fog, double start_time,
+                        const std::string& tag) {
+    if (n_games < 1 || mode < 0 || mode > 2 || counts.size() != 6 || rollout_size < 1 || hidden_size < 0)
+      throw std::invalid_argument("VecEnv: bad configuration");
+    VecConfig c;
+    c.n_games = n_games;
+    c.mode = mode;
+    c.seed = seed;
+    c.max_dota_time = max_dota_time;
+    c.rollout_size = rollout_size;
+    c.hidden_stride = hidden_stride;
+    c.hidden_size = hidden_size;
+    for (int i = 0; i < 6; ++i) c.counts[i] = counts[i];
+    c.threads = threads;
+    c.latest_weights_prob = latest_weights_prob;
+    c.validation = validation;
+    c.fog = fog;
+    c.start_time = start_time;
+    c.tag = tag;
+    return c;
+  }
+  VecEnv env_;
+  int S_ = 0, U_ = 0, H_ = 0;
+};
+
+// one SimGame driven step by step with explicit orders (parity tests against env/synthetic.py)
+class PySimGame {
+ public:
+  PySimGame(std::vector<std::tuple<int, int, int>> picks, uint64_t seed, double start_time, bool fog, double dt) {
+    std::vector<Pick> p;
+    for (auto& t : picks) p.push_back(Pick{std::get<0>(t), std::get<1>(t), std::get<2>(t)});
+    g_.init(p, seed, start_time, fog, dt);
+  }
+  // orders: (player, type 0/1/2, mx, my, target handle)
+  void step(std::vector<std::tuple<int, int, double, double, int64_t>> orders) {
+    std::vector<SimGame::Order> o;
+    for (auto& t : orders) {
+      SimGame::Order x;
+      x.player = std::get<0>(t);
+      x.type = std::get<1>(t);
+      x.mx = std::get<2>(t);
+      x.my = std::get<3>(t);
+      x.target = std::get<4>(t);
+      o.push_back(x);
+    }
+    g_.step(o);
+  }
+  py::tuple featurize(int team, int player_id, std::vector<int> counts) {
+    World w;
+    g_.world(team, w);
+    int U = 0;
+    for (int c : counts) U += c;
+    py::array_t<float> env({(py::ssize_t)3});
+    py::array_t<float> units({(py::ssize_t)U, (py::ssize_t)10});
+    py::array_t<int64_t> handles({(py::ssize_t)U});
+    featurize_one(w, player_id, team, counts.data(), U, env.mutable_data(), units.mutable_data(),
+                  handles.mutable_data());
+    return py::make_tuple(env, units, handles);
+  }
+  py::array_t<double> reward(int player_id, int team) {   // reward vs the previous call's view
+    RewardView cur = reward_view(g_, player_id, team);
+    py::array_t<double> r((py::ssize_t)9);
+    auto it = prev_.find(player_id);
+    if (it == prev_.end()) {
+      std::fill(r.mutable_data(), r.mutable_data() + 9, 0.0);
+    } else {
+      shaped_reward(it->second, cur, r.mutable_data());
+    }
+    prev_[player_id] = cur;
+    return r;
+  }
+  // (handle, unit_type, team, x, y, hp, alive, target) per unit, python dict order
+  std::vector<std::tuple<int, int, int, double, double, double, bool, int>> units() const {
+    std::vector<std::tuple<int, int, int, double, double, double, bool, int>> o;
+    for (const SUnit& u : g_.units) o.emplace_back(u.handle, u.unit_type, u.team, u.x, u.y, u.hp, u.alive, u.target);
+    return o;
+  }
+  double dota_time() const { return g_.dota_time; }
+  int status() const { return g_.status; }
+
+ private:
+  SimGame g_;
+  std::map<int, RewardView> prev_;
+};
+
 uint32_t crc32c(py::bytes b) {
   char* buf;
   py::ssize_t len;
@@ -114,6 +297,37 @@ PYBIND11_MODULE(_native, m) {
         py::arg("counts"), py::arg("threads") = 4,
         "Decode CMsgBotWorldState bytes and featurize for (player, team): returns env, units, handles, n_allied_creep");
   m.def("crc32c", &crc32c);
+  py::class_<PyVecEnv>(m, "VecEnv")
+      .def(py::init<int, int, uint64_t, double, long, int, int, std::vector<int>, int, double, bool, bool, double,
+                    std::string>(),
+           py::arg("n_games"), py::arg("mode") = 0, py::arg("seed") = 0, py::arg("max_dota_time") = 600.0,
+           py::arg("rollout_size") = (long)1 << 40, py::arg("hidden_stride") = 0, py::arg("hidden_size") = 0,
+           py::arg("counts") = std::vector<int>{1, 5, 16, 16, 1, 1}, py::arg("threads") = 8,
+           py::arg("latest_weights_prob") = 1.0, py::arg("validation") = false, py::arg("fog") = true,
+           py::arg("start_time") = -10.0, py::arg("tag") = std::string("vec"))
+      .def("begin_step", &PyVecEnv::begin_step)
+      .def("observe", &PyVecEnv::observe, py::arg("env"), py::arg("units"), py::arg("handles"), py::arg("active"))
+      .def("act", &PyVecEnv::act, py::arg("idx"), py::arg("act"), py::arg("msk"), py::arg("logp"), py::arg("value"),
+           py::arg("hidden"), py::arg("hidden_slots"), py::arg("handles"), py::arg("weight_version"))
+      .def("pop_rollouts", &PyVecEnv::pop_rollouts)
+      .def("pop_results", &PyVecEnv::pop_results)
+      .def("opponent_slots", &PyVecEnv::opponent_slots)
+      .def_property_readonly("slots", &PyVecEnv::slots)
+      .def_property_readonly("players_per_game", &PyVecEnv::players_per_game)
+      .def_property_readonly("games_finished", &PyVecEnv::games_finished)
+      .def_property_readonly("steps_taken", &PyVecEnv::steps_taken)
+      .def_property_readonly("rollouts_sent", &PyVecEnv::rollouts_sent)
+      .def("dota_time", &PyVecEnv::dota_time)
+      .def("status", &PyVecEnv::status);
+  py::class_<PySimGame>(m, "SimGame")
+      .def(py::init<std::vector<std::tuple<int, int, int>>, uint64_t, double, bool, double>(), py::arg("picks"),
+           py::arg("seed"), py::arg("start_time") = -10.0, py::arg("fog") = true, py::arg("dt") = 0.5)
+      .def("step", &PySimGame::step)
+      .def("featurize", &PySimGame::featurize)
+      .def("reward", &PySimGame::reward)
+      .def("units", &PySimGame::units)
+      .def_property_readonly("dota_time", &PySimGame::dota_time)
+      .def_property_readonly("status", &PySimGame::status);
   py::class_<ShmRing>(m, "ShmRing")
       .def(py::init<const std::string&, uint64_t, bool>(), py::arg("name"), py::arg("capacity") = 1 << 26,
            py::arg("create") = true)
