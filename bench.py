@@ -14,8 +14,9 @@ each rank trains on ``--batch-size`` sequences of ``--seq-len`` steps.
     python bench.py                                   # 1 GPU
     python -m torch.distributed.run --nproc-per-node 8 ... bench.py --gpus 8
 
-Rank 0 prints ONE JSON line. The actor number (batched many-game inference steps/s) is measured *outside* the timed
-learner region and reported as an extra field.
+Rank 0 prints ONE JSON line. The actor numbers are measured *outside* the timed learner region and reported as
+extra fields: ``actor.steps_per_s`` = player-steps/s of the whole self-play runtime (actor/vec.py), and
+``actor.policy_step_per_s`` = the batched GPU policy step alone.
 """
 from __future__ import annotations
 
@@ -47,8 +48,9 @@ def parse():
                     help='also time the bf16 learner (reported as an extra field, not the headline)')
     ap.add_argument('--replay', type=int, default=0, help='sequences in the on-HBM replay pool (0 = 4x batch)')
     ap.add_argument('--graph', type=int, default=-1, help='capture the step in a hipGraph (-1 = auto)')
-    ap.add_argument('--actor', type=int, default=1, help='also measure batched actor steps/s (untimed region)')
-    ap.add_argument('--actor-games', type=int, default=1024)
+    ap.add_argument('--actor', type=int, default=1, help='also measure actor steps/s (untimed region)')
+    ap.add_argument('--actor-games', type=int, default=2048, help='concurrent 1v1 games of the actor runtime')
+    ap.add_argument('--actor-threads', type=int, default=14, help='host threads of the native actor runtime')
     return ap.parse_args()
 
 
@@ -141,14 +143,26 @@ def main():
 
     actor = None
     if args.actor and rank == 0 and use_cuda:
+        # actor.steps_per_s: the whole self-play runtime (actor/vec.py: native engine + featurize + reward +
+        # trajectory/rollout encoding on host threads, one hipGraph policy step for every player) in player-steps/s;
+        # actor.policy_step_per_s: the batched GPU policy step alone (observations pre-staged)
+        actor = {}
+        try:
+            from dotaclient_amd.actor.vec import measure_vec_actor
+            rt = measure_vec_actor(policy, device, n_games=args.actor_games, threads=args.actor_threads)
+            actor.update(steps_per_s=rt['steps_per_s'], runtime=rt)
+        except Exception as e:  # the learner metric stands on its own
+            actor['runtime_error'] = repr(e)
         try:
             from dotaclient_amd.actor.batched import measure_actor_throughput
-            actor = measure_actor_throughput(policy, device, n_games=args.actor_games)
-            f8 = measure_actor_throughput(policy, device, n_games=args.actor_games, fp8=True)
-            actor['fp8_gpu_steps_per_s'] = f8['gpu_steps_per_s']
-            actor['fp8_steps_per_s'] = f8['steps_per_s']
-        except Exception as e:  # the learner metric stands on its own
-            actor = {'error': repr(e)}
+            mb = measure_actor_throughput(policy, device, n_games=args.actor_games, threads=args.actor_threads)
+            actor['policy_step_per_s'] = mb['gpu_steps_per_s']
+            actor['policy_step_protobuf_featurize_per_s'] = mb['steps_per_s']
+            f8 = measure_actor_throughput(policy, device, n_games=args.actor_games, fp8=True,
+                                          threads=args.actor_threads)
+            actor['fp8_policy_step_per_s'] = f8['gpu_steps_per_s']
+        except Exception as e:
+            actor['policy_step_error'] = repr(e)
 
     if rank == 0:
         out = {

@@ -34,7 +34,7 @@ class GpuActorPolicy:
     """Fixed-slot batched policy step on one GPU (fully-fused policies: no entity attention)."""
 
     def __init__(self, policy: Policy, n_slots: int, device='cuda', seed: int = 0, use_graph: bool = True,
-                 record: bool = True, fp8: bool = False):
+                 record: bool = True, fp8: bool = False, inputs_from: Optional['GpuActorPolicy'] = None):
         from .. import ops
         self.C = ops.require()
         cfg = policy.config
@@ -50,18 +50,25 @@ class GpuActorPolicy:
         self.record = record
         self.fp8 = fp8                   # e4m3 MFMA GEMMs (ops/fp8.py) for the pre-RNN, LSTM and heads projections
         self.policy = policy
-        self._alloc()
+        self._alloc(inputs_from)
         self.load_weights(policy)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
 
     # ------------------------------------------------------------------------------------------------
-    def _alloc(self):
+    def _alloc(self, inputs_from=None):
         n, U, A, dev = self.n, self.U, self.A, self.device
         H = self.cfg.hidden
         pin = dict(pin_memory=True)
-        self.h_env = torch.zeros(n, 3, **pin)
-        self.h_units = torch.zeros(n, U, 10, **pin)
-        self.h_handles = torch.full((n, U), -1, dtype=torch.long, **pin)
+        if inputs_from is not None:
+            # a second policy over the same observations (league opponents): share the staged inputs; keep/active
+            # stay per policy
+            if (inputs_from.n, inputs_from.U) != (n, U):
+                raise ValueError('inputs_from: slot count / layout mismatch')
+            self.h_env, self.h_units, self.h_handles = inputs_from.h_env, inputs_from.h_units, inputs_from.h_handles
+        else:
+            self.h_env = torch.zeros(n, 3, **pin)
+            self.h_units = torch.zeros(n, U, 10, **pin)
+            self.h_handles = torch.full((n, U), -1, dtype=torch.long, **pin)
         self.h_keep = torch.ones(n, 1, **pin)
         self.h_active = torch.ones(n, **pin)
         self.d_env = torch.zeros(n, 3, device=dev)
@@ -83,11 +90,24 @@ class GpuActorPolicy:
         self.o_value = torch.zeros(n, **pin)
         self.o_act = torch.zeros(n, A, dtype=torch.uint8, **pin)
         self.o_msk = torch.zeros(n, A, dtype=torch.uint8, **pin)
+        # LSTM state snapshots (h, c before the step, after resets) of selected rows — trajectory hidden states
+        self.h_rows = torch.zeros(n, dtype=torch.long, **pin)
+        self.d_rows = torch.zeros(n, dtype=torch.long, device=dev)
+        self.d_snap = torch.zeros(n, 2, H, device=dev)
+        self.o_snap = torch.zeros(n, 2, H, **pin)
+        self._snap_n = 0
         self.stream = torch.cuda.Stream(device=dev)
 
     @torch.no_grad()
     def load_weights(self, policy_or_state):
-        """(Re)load weights in place — buffers keep their addresses, so a captured graph stays valid."""
+        """(Re)load weights in place — buffers keep their addresses, so a captured graph stays valid. The copies
+        run on the step stream, so they are ordered after the previous replay and before the next one."""
+        if hasattr(self, 'stream'):
+            with torch.cuda.stream(self.stream):
+                return self._load_weights(policy_or_state)
+        return self._load_weights(policy_or_state)
+
+    def _load_weights(self, policy_or_state):
         sd = policy_or_state.state_dict() if isinstance(policy_or_state, torch.nn.Module) else policy_or_state
         dev = self.device
         g = (lambda k: sd[k].detach().to(dev, torch.float32))
@@ -198,12 +218,28 @@ class GpuActorPolicy:
         self.graph = g
 
     # ------------------------------------------------------------------------------------------------
-    def step_async(self):
-        """Launch one step for all slots using the host staging buffers; call :meth:`wait` for the outputs."""
+    def _snapshot(self, rows: np.ndarray):
+        k = len(rows)
+        self.h_rows.numpy()[:k] = rows
+        d = self.d_rows[:k]
+        d.copy_(self.h_rows[:k], non_blocking=True)
+        keep = self.d_keep.index_select(0, d)
+        torch.mul(self.h.index_select(0, d), keep, out=self.d_snap[:k, 0])
+        torch.mul(self.c.index_select(0, d), keep, out=self.d_snap[:k, 1])
+        self.o_snap[:k].copy_(self.d_snap[:k], non_blocking=True)
+        self._snap_n = k
+
+    def step_async(self, snapshot_rows: Optional[np.ndarray] = None):
+        """Launch one step for all slots using the host staging buffers; call :meth:`wait` for the outputs.
+        ``snapshot_rows``: slots whose LSTM state *entering* this step (after resets) :meth:`wait` returns as
+        ``out['hidden']`` (k, 2, H) — the trajectory's stored states (codec ``hiddens``)."""
         if self.use_graph and self.graph is None:
             self.capture()
         with torch.cuda.stream(self.stream):
             self._h2d()
+            self._snap_n = 0
+            if snapshot_rows is not None and len(snapshot_rows) and self.cfg.rnn == 'lstm':
+                self._snapshot(np.asarray(snapshot_rows))
             if self.graph is not None:
                 self.graph.replay()
             else:
@@ -219,6 +255,8 @@ class GpuActorPolicy:
         if self.record:
             out['actions'] = self.o_act.numpy()
             out['masks'] = self.o_msk.numpy()
+        if self._snap_n:
+            out['hidden'] = self.o_snap.numpy()[:self._snap_n]
         return out
 
     def step(self, env: np.ndarray, units: np.ndarray, handles: np.ndarray, reset: Optional[np.ndarray] = None,
@@ -236,6 +274,83 @@ class GpuActorPolicy:
 
     def hidden(self):
         return self.h, self.c
+
+
+class TorchSlotPolicy:
+    """:class:`GpuActorPolicy`'s host interface (staged ``h_*`` inputs, per-slot LSTM state, ``keep``/``active``,
+    :meth:`step_async`/:meth:`wait`, hidden snapshots) over the eager torch policy on any device — the CPU actor
+    (BASELINE config 1: no GPU) and policies the fused graph does not cover (5v5 entity attention)."""
+
+    def __init__(self, policy: Policy, n_slots: int, device='cpu', seed: int = 0, record: bool = True,
+                 inputs_from: Optional['TorchSlotPolicy'] = None, **_):
+        from .runner import PolicyRunner
+        self.cfg = policy.config
+        self.n = n_slots
+        self.U = self.cfg.layout.max_units
+        self.A = 21 + self.U
+        self.device = torch.device(device)
+        self.policy = type(policy)(self.cfg).to(self.device).eval()
+        self.load_weights(policy)
+        self.runner = PolicyRunner(self.policy, device=self.device, seed=seed)
+        n, U = n_slots, self.U
+        if inputs_from is not None:
+            if (inputs_from.n, inputs_from.U) != (n, U):
+                raise ValueError('inputs_from: slot count / layout mismatch')
+            self.h_env, self.h_units, self.h_handles = inputs_from.h_env, inputs_from.h_units, inputs_from.h_handles
+        else:
+            self.h_env = torch.zeros(n, 3)
+            self.h_units = torch.zeros(n, U, 10)
+            self.h_handles = torch.full((n, U), -1, dtype=torch.long)
+        self.h_keep = torch.ones(n, 1)
+        self.h_active = torch.ones(n)
+        H = self.cfg.hidden
+        self.recurrent = self.cfg.rnn == 'lstm'
+        self.h = np.zeros((n, H), np.float32)
+        self.c = np.zeros((n, H), np.float32)
+        self._out = None
+
+    @torch.no_grad()
+    def load_weights(self, policy_or_state):
+        sd = policy_or_state.state_dict() if isinstance(policy_or_state, torch.nn.Module) else policy_or_state
+        self.policy.load_state_dict({k: v.detach().to(self.device) for k, v in sd.items()}, strict=True)
+
+    def step_async(self, snapshot_rows: Optional[np.ndarray] = None):
+        keep = self.h_keep.numpy()
+        self.h *= keep
+        self.c *= keep
+        out = {}
+        if snapshot_rows is not None and len(snapshot_rows) and self.recurrent:
+            rows = np.asarray(snapshot_rows)
+            out['hidden'] = np.stack([self.h[rows], self.c[rows]], 1)
+        act = np.flatnonzero(self.h_active.numpy() > 0)
+        n, A = self.n, self.A
+        out.update(idx=np.zeros((n, 4), np.int32), logp=np.zeros(n, np.float32), value=np.zeros(n, np.float32),
+                   actions=np.zeros((n, A), np.uint8), masks=np.zeros((n, A), np.uint8))
+        if len(act):
+            hid = (self.h[act], self.c[act]) if self.recurrent else None
+            o, nh = self.runner.step(self.h_env.numpy()[act], self.h_units.numpy()[act], self.h_handles.numpy()[act],
+                                     hid)
+            out['idx'][act] = np.stack([o.enum, o.x, o.y, o.target], 1)
+            out['logp'][act], out['value'][act] = o.logp, o.value
+            out['actions'][act], out['masks'][act] = o.actions, o.masks
+            if nh is not None:
+                self.h[act], self.c[act] = nh
+        self._out = out
+
+    def wait(self) -> Dict[str, np.ndarray]:
+        self.h_keep.fill_(1.0)
+        return self._out
+
+
+def make_slot_policy(policy: Policy, n_slots: int, device='cuda', **kw):
+    """The fused graph-captured :class:`GpuActorPolicy` where it applies, else :class:`TorchSlotPolicy`."""
+    dev = torch.device(device)
+    cfg = policy.config
+    if dev.type == 'cuda' and not cfg.entity_attention and cfg.unit_dim == 128 and cfg.env_dim == 128:
+        return GpuActorPolicy(policy, n_slots, device=dev, **kw)
+    kw.pop('fp8', None)
+    kw.pop('use_graph', None)
+    return TorchSlotPolicy(policy, n_slots, device=dev, **kw)
 
 
 # ----------------------------------------------------------------------------------------------------

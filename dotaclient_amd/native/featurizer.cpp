@@ -179,7 +179,7 @@ class PyVecEnv {
   }
   py::list pop_results() {
     py::list out;
-    for (auto& r : env_.pop_results()) out.append(py::make_tuple(r.first, r.second));
+    for (auto& r : env_.pop_results()) out.append(py::make_tuple(r[0], r[1], r[2]));
     return out;
   }
   py::array_t<int32_t> opponent_slots() {

@@ -16,6 +16,7 @@
 // Both teams are observed at once: the reference's observe(D) happens before the engine advances, so it does not
 // depend on R's action — one batched policy step serves both teams of every game.
 #pragma once
+#include <array>
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
@@ -836,10 +837,11 @@ class VecEnv {
   double dota_time(int gi) const { return games_[gi].sim.dota_time; }
   int status(int gi) const { return games_[gi].sim.status; }
   const std::vector<uint8_t>& canvas(int gi) const { return games_[gi].canvas; }
-  // per-game results of finished games since the last call: (team of the latest-weights side, end_state)
-  std::vector<std::pair<int, int>> pop_results() {
+  // per-game results of finished games since the last call:
+  // (game index, team of the latest-weights side or 0 when both sides played the latest weights, end_state)
+  std::vector<std::array<int, 3>> pop_results() {
     std::lock_guard<std::mutex> l(out_m_);
-    std::vector<std::pair<int, int>> r;
+    std::vector<std::array<int, 3>> r;
     r.swap(results_);
     return r;
   }
@@ -1061,7 +1063,7 @@ class VecEnv {
     }
     {
       std::lock_guard<std::mutex> l(out_m_);
-      results_.push_back({g.opponent_team ? latest_team : 0, g.end_state});
+      results_.push_back({(int)(&g - games_.data()), g.opponent_team ? latest_team : 0, g.end_state});
     }
     g.running = false;
   }
@@ -1077,7 +1079,7 @@ class VecEnv {
   std::atomic<long> steps_taken_{0}, rollouts_sent_{0};
   std::mutex out_m_;
   std::vector<std::string> out_;
-  std::vector<std::pair<int, int>> results_;
+  std::vector<std::array<int, 3>> results_;
 };
 
 }  // namespace dca_native

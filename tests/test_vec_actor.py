@@ -1,0 +1,149 @@
+"""VecActor orchestration (actor/vec.py) on CPU: the native VecEnv + TorchSlotPolicy (GpuActorPolicy's interface).
+
+The decisive check is *replay consistency*: every published rollout is re-run through the eager policy from its
+first stored LSTM state — the stored states at every ``hidden_stride`` step, the recorded ``values`` and the
+``logp`` of the recorded actions under the recorded masks must all match what the actor had. That pins the slot
+bookkeeping (resets, active masks, group pipelining, hidden snapshots, truncated rollouts) end to end.
+"""
+import numpy as np
+import pytest
+import torch
+
+from dotaclient_amd import native
+from dotaclient_amd.actor.weights import WeightStore
+from dotaclient_amd.models.policy import Policy, get_config, masked_log_softmax
+from dotaclient_amd.transport.codec import decode
+
+pytestmark = pytest.mark.skipif(not native.AVAILABLE, reason='native module not built')
+
+HEADS = [('enum', 0, 3), ('x', 3, 9), ('y', 12, 9)]
+
+
+def _store(cfg, versions=(0,), seed=0):
+    ws = WeightStore(cfg, device='cpu')
+    for v in versions:
+        torch.manual_seed(seed + v)
+        ws.add(v, {k: t.detach().clone() for k, t in Policy(cfg).state_dict().items()})
+    return ws
+
+
+def _replay(policy, r, stride):
+    """Re-run a rollout; returns (hidden states at the stride points, values, logp of the recorded actions)."""
+    U = r.units.shape[1]
+    heads = HEADS + [('target_unit', 21, U)]
+    h = (torch.from_numpy(r.hiddens[0, 0].copy())[None, None], torch.from_numpy(r.hiddens[0, 1].copy())[None, None])
+    hs, vals, lps = [], [], []
+    with torch.no_grad():
+        for t in range(r.length):
+            if t % stride == 0:
+                hs.append(np.stack([h[0][0, 0].numpy(), h[1][0, 0].numpy()]))
+            logits, value, h = policy.forward_packed(torch.from_numpy(r.env[t:t + 1].copy())[None],
+                                                     torch.from_numpy(r.units[t:t + 1].copy())[None], h)
+            vals.append(float(value[0, 0, 0]))
+            lp = 0.0
+            for k, o, w in heads:
+                m = torch.from_numpy(r.masks[t, o:o + w].astype(bool))
+                if not m.any():
+                    continue
+                a = int(np.argmax(r.actions[t, o:o + w]))
+                lp += float(masked_log_softmax(logits[k].reshape(1, w).float(), m[None], dim=-1)[0, a])
+            lps.append(lp)
+    return np.stack(hs), np.array(vals, np.float32), np.array(lps, np.float32)
+
+
+@pytest.mark.parametrize('groups', [1, 2])
+def test_vec_actor_rollouts_replay_consistent(groups):
+    from dotaclient_amd.actor.vec import VecActor
+    cfg = get_config('lstm128')
+    ws = _store(cfg)
+    sent = []
+    stride = 8
+    va = VecActor(ws, 3, sent.append, device='cpu', seed=5, rollout_size=24, max_dota_time=25.0,
+                  hidden_stride=stride, threads=2, groups=groups)
+    while va.games_finished < 4:
+        va.step()
+    assert va.rollouts_sent == len(sent) > 0
+    rs = [decode(b) for b in sent]
+    pol = ws.policy_for(ws.latest_weights())
+    per_player = {}
+    for r in rs:
+        assert r.hiddens.shape == (-(-r.length // stride), 2, 128)
+        assert r.weight_version == 0 and r.hidden_stride == stride
+        hs, vals, lps = _replay(pol, r, stride)
+        np.testing.assert_allclose(hs, r.hiddens, atol=2e-5)
+        np.testing.assert_allclose(vals, r.values, atol=2e-5)
+        np.testing.assert_allclose(lps, r.logp, atol=5e-4)
+        per_player.setdefault((r.game_id, r.team_id, r.player_id), []).append(r)
+    for key, lst in per_player.items():
+        assert lst[-1].done and not any(r.done for r in lst[:-1]), key
+        assert not np.any(lst[0].hiddens[0]), key                  # a game starts from the zero state
+        assert all(r.length == 24 for r in lst[:-1]), key
+    assert va.steps_taken >= sum(r.length for r in rs)
+
+
+def test_vec_actor_league_opponents_and_hot_swap():
+    from dotaclient_amd.actor.league import League
+    from dotaclient_amd.actor.vec import VecActor
+    import random
+    cfg = get_config('lstm128')
+    ws = _store(cfg, versions=(0, 1, 2))
+    league = League(ws, mode='uniform', rng=random.Random(0))
+    sent = []
+    va = VecActor(ws, 4, sent.append, device='cpu', seed=9, max_dota_time=15.0, hidden_stride=8, threads=2,
+                  groups=2, latest_weights_prob=0.0, league=league, opponent_refresh=2)
+    while va.games_finished < 6:
+        va.step()
+    # every game had an opponent team: exactly one (team, player) per game rolls out
+    teams = {}
+    for b in sent:
+        r = decode(b)
+        teams.setdefault(r.game_id, set()).add(r.team_id)
+    assert teams and all(len(t) == 1 for t in teams.values())
+    assert sum(g for _, g in league.stats().values()) == va.opp_games_finished == va.games_finished
+    # the opponents played stored snapshots and never more than two at once per group
+    assert all(len(g.opp) <= 2 for g in va.groups)
+    # hot swap: a new latest version reaches the games started after it, which replay exactly under it
+    torch.manual_seed(99)
+    ws.add(7, {k: t.detach().clone() for k, t in Policy(cfg).state_dict().items()})
+    n0 = va.games_finished
+    while va.games_finished < n0 + 4:      # drain the games in flight at the swap
+        va.step()
+    sent.clear()
+    while va.games_finished < n0 + 8:
+        va.step()
+    rs = [decode(b) for b in sent]
+    assert rs and all(r.weight_version == 7 for r in rs)
+    pol = ws.policy_for(ws.latest_weights())
+    for r in rs:
+        _, vals, lps = _replay(pol, r, 8)
+        np.testing.assert_allclose(vals, r.values, atol=2e-5)
+        np.testing.assert_allclose(lps, r.logp, atol=5e-4)
+
+
+@pytest.mark.gpu
+def test_vec_actor_gpu_graph_policy_replay_consistent():
+    """The hipGraph GpuActorPolicy path (bf16 GEMMs, fused LSTM cell + sampling kernels) with league opponents:
+    rollouts replay under the fp32 eager policy within bf16 tolerance (slot/state mix-ups would be O(1))."""
+    import random
+    from dotaclient_amd.actor.batched import GpuActorPolicy
+    from dotaclient_amd.actor.league import League
+    from dotaclient_amd.actor.vec import VecActor
+    cfg = get_config('lstm512')
+    ws = _store(cfg, versions=(0, 1))
+    sent = []
+    va = VecActor(ws, 16, sent.append, device='cuda', seed=3, rollout_size=32, max_dota_time=20.0,
+                  hidden_stride=16, threads=4, groups=2, latest_weights_prob=0.5,
+                  league=League(ws, mode='uniform', rng=random.Random(1)))
+    assert all(isinstance(g.gp, GpuActorPolicy) for g in va.groups)
+    while va.games_finished < 24:
+        va.step()
+    va.close()
+    assert va.opp_games_finished > 0
+    pol = ws.policy_for(ws.latest_weights())
+    rs = [decode(b) for b in sent]
+    assert len(rs) > 16
+    for r in rs:
+        hs, vals, lps = _replay(pol, r, 16)
+        np.testing.assert_allclose(hs, r.hiddens, atol=5e-2)
+        np.testing.assert_allclose(vals, r.values, atol=5e-2)
+        np.testing.assert_allclose(lps, r.logp, atol=1e-1)
