@@ -51,6 +51,9 @@ def parse():
     ap.add_argument('--actor', type=int, default=1, help='also measure actor steps/s (untimed region)')
     ap.add_argument('--actor-games', type=int, default=2048, help='concurrent 1v1 games of the actor runtime')
     ap.add_argument('--actor-threads', type=int, default=14, help='host threads of the native actor runtime')
+    ap.add_argument('--e2e', type=float, default=20.0,
+                    help='seconds of the end-to-end actors→queue→learner loop on GPU 0 (1-GPU runs; 0 = off)')
+    ap.add_argument('--e2e-games', type=int, default=1024)
     return ap.parse_args()
 
 
@@ -137,7 +140,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     extra = None
     if args.bf16_extra and args.precision == 'fp32' and use_cuda:
-        del learner
+        learner = None
         e16, _, _, _, _ = run('bf16')
         extra = {'precision': 'bf16', 'value': samples / e16, 'ms_per_step': e16 / args.steps * 1e3}
 
@@ -163,6 +166,18 @@ def main():
             actor['fp8_policy_step_per_s'] = f8['gpu_steps_per_s']
         except Exception as e:
             actor['policy_step_error'] = repr(e)
+
+    e2e = None
+    if args.e2e > 0 and world == 1 and use_cuda:
+        # the reference's own metric ('steps per s' incl. the wait for experience, optimizer.py:485-486) from the
+        # real loop: VecActor → queue → DotaOptimizer (deploy shape 8×1400, 16 seq/iteration) → model → VecActor
+        learner = None
+        try:
+            from dotaclient_amd.learner.e2e import measure_e2e
+            e2e = measure_e2e(model=args.model, device=device, duration=args.e2e, games=args.e2e_games,
+                              threads=args.actor_threads, seq_len=args.seq_len, precision=args.precision)
+        except Exception as e:
+            e2e = {'error': repr(e)}
 
     if rank == 0:
         out = {
@@ -190,6 +205,7 @@ def main():
             'loss_first': loss_val, 'loss_last': final_loss,
             'bf16_learner': extra,
             'actor': actor,
+            'e2e': e2e,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

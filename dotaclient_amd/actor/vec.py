@@ -51,7 +51,7 @@ class _Group:
                                    rollout_size=a.rollout_size, hidden_stride=a.hidden_stride if a.H else 0,
                                    hidden_size=a.H, counts=list(a.cfg.layout.counts), threads=a.threads,
                                    latest_weights_prob=a.latest_weights_prob, start_time=a.start_time, fog=a.fog,
-                                   tag=f'{a.tag}{index}')
+                                   tag=f'{a.tag}{index}', stagger=a.stagger)
         self.S = self.ve.slots
         self.ppg = self.ve.players_per_game
         self.gp = make_slot_policy(a.policy, self.S, device=a.device, seed=seed, fp8=a.fp8)
@@ -80,7 +80,7 @@ class VecActor:
                  mode: str = '1v1', seed: int = 0, rollout_size: int = 10 ** 9, max_dota_time: float = 600.0,
                  latest_weights_prob: float = 1.0, hidden_stride: int = 256, threads: int = 8, groups: int = 2,
                  league=None, fp8: bool = False, opponent_refresh: int = 64, start_time: float = -10.0,
-                 fog: bool = True, tag: str = 'vec'):
+                 fog: bool = True, tag: str = 'vec', stagger: bool = False):
         from .. import native
         if not native.AVAILABLE:
             raise RuntimeError('VecActor needs the native module (python -m dotaclient_amd.native.build)')
@@ -107,6 +107,7 @@ class VecActor:
         self.start_time = float(start_time)
         self.fog = bool(fog)
         self.tag = tag
+        self.stagger = bool(stagger)     # staggered first games (no lockstep bursts of whole-game rollouts)
         groups = max(1, min(int(groups), n_games))
         sizes = [n_games // groups + (1 if i < n_games % groups else 0) for i in range(groups)]
         self.groups = [_Group(self, i, sizes[i], seed * 7919 + i) for i in range(groups)]
@@ -281,14 +282,15 @@ def measure_vec_actor(policy, device='cuda', n_games: int = 2048, steps: int = 1
     sink = []
     va = VecActor(ws, n_games, lambda b: sink.append(len(b)), device=device, seed=1, threads=threads,
                   groups=groups, hidden_stride=hidden_stride, rollout_size=rollout_size, fp8=fp8)
+    sync = (lambda: torch.cuda.synchronize(va.device)) if va.device.type == 'cuda' else (lambda: None)
     for _ in range(warmup):
         va.step()
-    torch.cuda.synchronize(va.device)
+    sync()
     s0, r0, k0 = va.steps_taken, va.rollouts_sent, len(sink)
     t0 = time.perf_counter()
     for _ in range(steps):
         va.step()
-    torch.cuda.synchronize(va.device)
+    sync()
     dt = time.perf_counter() - t0
     n = va.steps_taken - s0
     return {'steps_per_s': n / dt, 'ms_per_step': dt / steps * 1e3, 'games': n_games,

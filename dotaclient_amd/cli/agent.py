@@ -51,6 +51,10 @@ def build_parser():
     ap.add_argument('--hidden-stride', type=int, default=256, help='store LSTM state every N steps')
     ap.add_argument('--fp8', type=str2bool, default=False,
                     help='GPU actor: e4m3 FP8 policy GEMMs (pre-RNN, LSTM input/recurrent, heads)')
+    ap.add_argument('--runtime', type=str, default='auto', choices=['auto', 'vec', 'service'],
+                    help='vec: native vectorised self-play (actor/vec.py, synthetic env only); service: the '
+                         'protobuf Actor over DotaService games; auto: vec for synthetic self-play')
+    ap.add_argument('--threads', type=int, default=8, help='host threads of the vec runtime')
     ap.add_argument('--league', type=str, default='oldest', choices=['oldest', 'uniform', 'recent', 'pfsp'],
                     help='opponent sampling over the weight history when not playing the latest weights')
     return ap
@@ -113,6 +117,14 @@ def main(argv=None):
     config_fn = (lambda: get_1v1_bot_vs_default_config(rng=rng)) if args.validation else get_1v1_selfplay_config
     from ..actor.league import League
     league = None if args.league == 'oldest' else League(ws, mode=args.league, rng=rng)
+    runtime = args.runtime
+    if runtime == 'auto':
+        from .. import native
+        runtime = 'vec' if (args.env == 'synthetic' and not args.validation and native.AVAILABLE) else 'service'
+    if runtime == 'vec':
+        if args.env != 'synthetic' or args.validation:
+            raise SystemExit('--runtime vec drives the synthetic engine in self-play only')
+        return _run_vec(args, ws, broker, league, device, seed, cfg)
     actor = Actor(make_services(args.env, args.games, seed), ws, runner_for,
                   None if args.validation else broker.publish_experience, config_fn,
                   rollout_size=args.rollout_size, max_dota_time=args.max_dota_time,
@@ -134,6 +146,22 @@ def main(argv=None):
     finally:
         if uploader is not None:
             uploader.flush()
+    return 0
+
+
+def _run_vec(args, ws, broker, league, device, seed, cfg):
+    from ..actor.vec import VecActor
+    va = VecActor(ws, args.games, broker.publish_experience, device=device,
+                  mode='5v5' if cfg.layout.counts[0] > 1 else '1v1', seed=seed, rollout_size=args.rollout_size,
+                  max_dota_time=args.max_dota_time, latest_weights_prob=args.use_latest_weights_prob,
+                  hidden_stride=args.hidden_stride, threads=args.threads, league=league, fp8=args.fp8, stagger=True)
+    try:
+        va.run(n_games=args.n_games)
+    except Exception:
+        logger.exception('actor failed')
+        return 1
+    finally:
+        va.close()
     return 0
 
 

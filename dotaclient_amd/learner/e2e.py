@@ -1,0 +1,116 @@
+"""End-to-end node measurement: actors → experience queue → learner → model broadcast → actors, on one GPU.
+
+The reference's only published number is the optimizer's ``steps per s`` — sequence steps consumed per wall second
+*including the wait for experience* (optimizer.py:485-486, README.md:35: ~1000 with 40 agents per optimizer). This
+runs that loop for real, in one process:
+
+* a :class:`~dotaclient_amd.actor.vec.VecActor` thread (native vectorised self-play + hipGraph batched policy)
+  publishes whole-game DCX1 rollouts (the deploy's ``--rollout-size 9999``, params.libsonnet:19) into a bounded
+  :class:`~dotaclient_amd.transport.broker.InProcBroker` (oldest dropped when full), with staggered first games so
+  the lockstep games do not all publish on the same step;
+* :class:`~dotaclient_amd.learner.optimizer.DotaOptimizer` (the learner runtime, unchanged: decode, device ingest
+  with the return / GAE scan, hipGraph PPO steps, checkpoint + model publish every iteration) consumes them with
+  the deploy's shape — batch 8 × seq_len 1400, 16 sequences per iteration, 1 epoch (params.libsonnet:7-24);
+* every published model reaches the actor's :class:`~dotaclient_amd.actor.weights.WeightStore` and is hot-swapped
+  into the actor graphs between steps, so ``avg_weight_age`` is real.
+
+Both run on the same GPU (their kernels share the CUs). Reported: the reference metric (``steps per s``, padded
+sequences as the reference counts them), the unpadded experience steps/s actually trained on, ``avg_weight_age``,
+the actor's player-steps/s during the window and the queue drops.
+"""
+from __future__ import annotations
+
+import logging
+import shutil
+import tempfile
+import threading
+import time
+from typing import Dict, Optional
+
+import numpy as np
+import torch
+
+logger = logging.getLogger(__name__)
+
+
+def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, games: int = 1024,
+                threads: int = 14, seq_len: int = 1400, batch_size: int = 8, seq_per_epoch: int = 16,
+                epochs: int = 1, precision: str = 'fp32', max_dota_time: float = 600.0, rollout_size: int = 9999,
+                queue_size: int = 64, warmup_iterations: int = 2, max_iterations: Optional[int] = None,
+                log_dir: Optional[str] = None) -> Dict[str, float]:
+    from ..actor.vec import VecActor
+    from ..actor.weights import WeightStore
+    from ..transport.broker import InProcBroker
+    from .optimizer import DotaOptimizer, OptimizerConfig
+
+    tmp = log_dir or tempfile.mkdtemp(prefix='dca_e2e_')
+    broker = InProcBroker(maxsize=queue_size, drop_oldest=True)
+    cfg = OptimizerConfig(log_dir=tmp, epochs=epochs, seq_per_epoch=seq_per_epoch, batch_size=batch_size,
+                          seq_len=seq_len, model=model, precision=precision, device=str(device), checkpoint_keep=2,
+                          run_local=True, xp_timeout=300.0, histogram_freq=10 ** 9)
+    opt = DotaOptimizer(cfg, broker)                       # publishes model version 0
+    ws = WeightStore(model, device='cpu')
+    broker.subscribe_model(ws.add_bytes)
+    va = VecActor(ws, games, broker.publish_experience, device=device, seed=11, rollout_size=rollout_size,
+                  max_dota_time=max_dota_time, hidden_stride=seq_len, threads=threads, stagger=True)
+    for _ in range(3):                                     # capture the actor graphs before the learner's
+        va.step()
+    stop = threading.Event()
+    err = []
+
+    def actor_loop():
+        try:
+            while not stop.is_set():
+                va.step()
+        except BaseException as e:                         # surfaced on the main thread
+            err.append(e)
+
+    th = threading.Thread(target=actor_loop, name='vec-actor', daemon=True)
+    th.start()
+    rows = []
+    try:
+        it = opt.iteration_start
+        for _ in range(warmup_iterations):
+            opt.run_iteration(it)
+            it += 1
+            if err:
+                raise err[0]
+        t0 = time.perf_counter()
+        s0, d0 = va.steps_taken, broker.n_dropped
+        opt.time_last_step = time.time()
+        while time.perf_counter() - t0 < duration and (max_iterations is None or len(rows) < max_iterations):
+            opt.run_iteration(it)
+            it += 1
+            m = opt.last_metrics
+            rows.append((m[DotaOptimizer.SPEED_KEY], m['avg_weight_age'], m['avg_rollout_len'],
+                         m.get('time/train', float('nan')), m.get('time/ingest', float('nan')), m['experience_steps']))
+            if err:
+                raise err[0]
+        if opt.device.type == 'cuda':
+            torch.cuda.synchronize(opt.device)
+        wall = time.perf_counter() - t0
+        actor_steps = va.steps_taken - s0
+        dropped = broker.n_dropped - d0
+    finally:
+        stop.set()
+        th.join(timeout=60)
+        va.close()
+        if log_dir is None:
+            shutil.rmtree(tmp, ignore_errors=True)
+    a = np.asarray(rows, dtype=np.float64)
+    n_it = len(rows)
+    padded = n_it * seq_per_epoch * seq_len
+    valid = float(a[:, 5].sum()) if n_it else 0.0         # unpadded experience steps consumed
+    return {
+        'steps_per_s': padded / wall if n_it else 0.0,          # the reference's 'steps per s' (padded, incl. wait)
+        'valid_steps_per_s': valid / wall if n_it else 0.0,
+        'iterations': n_it, 'wall_s': wall,
+        'avg_weight_age': float(a[:, 1].mean()) if n_it else float('nan'),
+        'avg_rollout_len': float(a[:, 2].mean()) if n_it else float('nan'),
+        'train_ms_per_iteration': 1e3 * float(a[:, 3].mean()) if n_it else float('nan'),
+        'ingest_ms_per_iteration': 1e3 * float(a[:, 4].mean()) if n_it else float('nan'),
+        'actor_steps_per_s': actor_steps / wall,
+        'queue_dropped': int(dropped), 'games': games,
+        'config': {'batch_size': batch_size, 'seq_len': seq_len, 'seq_per_epoch': seq_per_epoch, 'epochs': epochs,
+                   'rollout_size': rollout_size, 'max_dota_time': max_dota_time, 'precision': precision},
+    }

@@ -215,6 +215,13 @@ class Learner:
     def _graph_ready(self) -> bool:
         return bool(self._graph_warmup) and self.n_steps >= self._graph_warmup
 
+    @staticmethod
+    def _capture_mode() -> str:
+        """Only this thread's HIP calls are capture-checked ('thread_local'): other threads of the process keep
+        running while the learner captures — RCCL's watchdog querying events, or an in-process actor stepping its
+        own graphs on its own streams (learner/e2e.py). Neither touches the capturing stream."""
+        return 'thread_local'
+
     def _replay_split(self, key, body):
         """Split-mode capture/replay: ``body(hook)`` is captured as TWO graphs — the hook, called once by the step
         at its split point, ends the first capture and begins the second (same memory pool). Replay: graph 1, then
@@ -229,8 +236,7 @@ class Learner:
             with torch.cuda.stream(s):              # eager warm-up on the capture stream, no collectives
                 body(lambda: None)
             cur.wait_stream(s)
-            import torch.distributed as dist
-            mode = 'thread_local' if (dist.is_available() and dist.is_initialized()) else 'global'
+            mode = self._capture_mode()
             g1, g2 = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             switched = []
 
@@ -270,11 +276,7 @@ class Learner:
                 body()
             cur.wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            # with a process group up, RCCL's watchdog thread queries events while we capture: only this thread's
-            # calls are capture-checked ('thread_local'), the watchdog's are not (they touch no captured stream)
-            import torch.distributed as dist
-            mode = 'thread_local' if (dist.is_available() and dist.is_initialized()) else 'global'
-            with torch.cuda.graph(g, stream=s, capture_error_mode=mode):
+            with torch.cuda.graph(g, stream=s, capture_error_mode=self._capture_mode()):
                 out = body()
             graphs[key] = (g, out)
             self.graph = g

@@ -80,6 +80,7 @@ class OptimizerConfig:
     ingest: str = 'auto'               # 'device' (HIP return/GAE scan over the uploaded rollouts) | 'host' | 'auto'
     artifact_url: Optional[str] = None  # off-node mirror of checkpoints + events (reference: GCS bucket, §utils.artifacts)
     allow_pickle_experience: bool = False  # accept reference-agent pickles (restricted unpickler); off: DCX1 only
+    graph: bool = True                 # capture the fused train step in a hipGraph (learner/engine.py enable_graph)
 
 
 class Sequence:
@@ -147,6 +148,8 @@ class DotaOptimizer:
                         vf_coef=cfg.vf_coef, clip_eps=cfg.clip_eps, gamma=cfg.gamma, gae_lambda=cfg.gae_lambda,
                         max_grad_norm=cfg.max_grad_norm, compat_value_bug=cfg.compat_value_bug)
         self.learner = Learner(self.policy, lc, device=self.device, backend=cfg.backend, precision=cfg.precision)
+        if cfg.graph:
+            self.learner.enable_graph(warmup=1)
         if trainer_state is not None:
             self.learner.load_state_dict(trainer_state['learner'])
             self.running.load_state_dict(trainer_state['running'])
@@ -453,6 +456,7 @@ class DotaOptimizer:
             'loss/sum': mean['loss'], 'loss/policy': mean['policy_loss'], 'loss/entropy': mean['entropy_loss'],
             'loss/advantage': mean['advantage_loss'], 'entropy': mean['entropy'], 'advantage': mean['advantage'],
             'avg_rollout_len': float(np.mean(rollout_lens)), 'avg_weight_age': float(np.mean(weight_ages)),
+            'experience_steps': float(np.sum(rollout_lens)),
             'grad_norm': mean['grad_norm'],
         }
         for k in ('approx_kl', 'clipfrac'):

@@ -118,9 +118,9 @@ class PyVecEnv {
  public:
   PyVecEnv(int n_games, int mode, uint64_t seed, double max_dota_time, long rollout_size, int hidden_stride,
            int hidden_size, std::vector<int> counts, int threads, double latest_weights_prob, bool validation,
-           bool fog, double start_time, std::string tag)
+           bool fog, double start_time, std::string tag, bool stagger)
       : env_(make(n_games, mode, seed, max_dota_time, rollout_size, hidden_stride, hidden_size, counts, threads,
-                  latest_weights_prob, validation, fog, start_time, tag)) {
+                  latest_weights_prob, validation, fog, start_time, tag, stagger)) {
     S_ = env_.slots();
     U_ = env_.units();
     H_ = hidden_size;
@@ -198,7 +198,7 @@ class PyVecEnv {
   static VecConfig make(int n_games, int mode, uint64_t seed, double max_dota_time, long rollout_size,
                         int hidden_stride, int hidden_size, const std::vector<int>& counts, int threads,
                         double latest_weights_prob, bool validation, bool fog, double start_time,
-                        const std::string& tag) {
+                        const std::string& tag, bool stagger) {
     if (n_games < 1 || mode < 0 || mode > 2 || counts.size() != 6 || rollout_size < 1 || hidden_size < 0)
       throw std::invalid_argument("VecEnv: bad configuration");
     VecConfig c;
@@ -216,6 +216,7 @@ class PyVecEnv {
     c.fog = fog;
     c.start_time = start_time;
     c.tag = tag;
+    c.stagger = stagger;
     return c;
   }
   VecEnv env_;
@@ -299,12 +300,12 @@ PYBIND11_MODULE(_native, m) {
   m.def("crc32c", &crc32c);
   py::class_<PyVecEnv>(m, "VecEnv")
       .def(py::init<int, int, uint64_t, double, long, int, int, std::vector<int>, int, double, bool, bool, double,
-                    std::string>(),
+                    std::string, bool>(),
            py::arg("n_games"), py::arg("mode") = 0, py::arg("seed") = 0, py::arg("max_dota_time") = 600.0,
            py::arg("rollout_size") = (long)1 << 40, py::arg("hidden_stride") = 0, py::arg("hidden_size") = 0,
            py::arg("counts") = std::vector<int>{1, 5, 16, 16, 1, 1}, py::arg("threads") = 8,
            py::arg("latest_weights_prob") = 1.0, py::arg("validation") = false, py::arg("fog") = true,
-           py::arg("start_time") = -10.0, py::arg("tag") = std::string("vec"))
+           py::arg("start_time") = -10.0, py::arg("tag") = std::string("vec"), py::arg("stagger") = false)
       .def("begin_step", &PyVecEnv::begin_step)
       .def("observe", &PyVecEnv::observe, py::arg("env"), py::arg("units"), py::arg("handles"), py::arg("active"))
       .def("act", &PyVecEnv::act, py::arg("idx"), py::arg("act"), py::arg("msk"), py::arg("logp"), py::arg("value"),

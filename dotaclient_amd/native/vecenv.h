@@ -721,6 +721,9 @@ struct VecConfig {
   int counts[6] = {1, 5, 16, 16, 1, 1};
   int threads = 8;
   bool validation = false;
+  // staggered resets: the FIRST game of slot gi ends at start + (max - start)·(gi+1)/n_games instead of max, so
+  // lockstep games do not all finish (and publish whole-game rollouts) on the same step
+  bool stagger = false;
   std::string tag = "vec";
 };
 
@@ -757,6 +760,7 @@ struct VGame {
   bool running = false, done = false, fresh = false;
   int end_state = -1;            // Status, -1 = none (time limit)
   float obs_time = 0;
+  double limit = 0;              // dota time at which this game ends (max_dota_time, or staggered)
   int opponent_team = 0;         // 0: both latest; else the team playing the opponent (old) weights
   uint64_t serial = 0;
   std::vector<SimGame::Order> orders;
@@ -875,6 +879,9 @@ class VecEnv {
     g.sim.init(pk, seed, cfg_.start_time, cfg_.fog, cfg_.dt);
     g.game_id = cfg_.tag + "_" + std::to_string(serial);
     g.serial = serial;
+    g.limit = cfg_.max_dota_time;
+    if (cfg_.stagger && serial <= (uint64_t)cfg_.n_games)
+      g.limit = cfg_.start_time + (cfg_.max_dota_time - cfg_.start_time) * (double)(gi + 1) / (double)cfg_.n_games;
     g.running = true;
     g.done = false;
     g.fresh = true;
@@ -1039,7 +1046,7 @@ class VecEnv {
         }
     }
     steps_taken_ += stepped;
-    if (g.done || (double)g.obs_time >= cfg_.max_dota_time) finish(g, version);
+    if (g.done || (double)g.obs_time >= g.limit) finish(g, version);
   }
 
   void finish(VGame& g, long version) {
