@@ -19,6 +19,7 @@ def _free_port():
 
 def _init(rank, world, port):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    torch.set_num_threads(1)               # up to 8 ranks share the 8 CPUs of the test box
     dist.init_process_group('gloo', rank=rank, world_size=world)
 
 
@@ -59,9 +60,9 @@ def _toy_worker(rank, world, port, q, split=False):
         q.put((rank, repr(e), None, None))
 
 
-@pytest.mark.parametrize('split', [False, True])
-def test_sparse_param_semantics_two_ranks(split):
-    world, port = 2, _free_port()
+@pytest.mark.parametrize('world,split', [(2, False), (2, True), (4, True), (8, False), (8, True)])
+def test_sparse_param_semantics(world, split):
+    port = _free_port()
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     ps = [ctx.Process(target=_toy_worker, args=(r, world, port, q, split)) for r in range(world)]
@@ -76,16 +77,17 @@ def test_sparse_param_semantics_two_ranks(split):
     for p in ps:
         p.join(timeout=60)
     sd0, g0, c0 = res[0]
-    sd1, g1, c1 = res[1]
-    for k in sd0:
-        assert torch.equal(sd0[k], sd1[k]), k          # rank-0 broadcast at construction
-    for k in g0:
-        assert torch.equal(g0[k], g1[k]), k            # identical reduced grads on every rank (fixes §2.10-8)
+    for r in range(1, world):
+        sdr, gr, _ = res[r]
+        for k in sd0:
+            assert torch.equal(sd0[k], sdr[k]), k      # rank-0 broadcast at construction
+        for k in g0:
+            assert torch.equal(g0[k], gr[k]), k        # identical reduced grads on every rank (fixes §2.10-8)
     names = list(g0)
     counts = dict(zip(names, c0.tolist()))
-    assert counts['a.weight'] == 2 and counts['b.weight'] == 1 and counts['c.weight'] == 0
-    # a: mean over ranks of per-rank grads (x = 1 and x = 2) → column sums (2·1 + 2·2)/2 = 3
-    assert torch.allclose(g0['a.weight'], torch.full((4, 4), 3.0))
+    assert counts['a.weight'] == world and counts['b.weight'] == 1 and counts['c.weight'] == 0
+    # a: mean over ranks of per-rank grads (x = rank + 1) → column sums 2·mean(1..world) = world + 1
+    assert torch.allclose(g0['a.weight'], torch.full((4, 4), float(world + 1)))
     # b: only rank 0 had it → divided by its count 1
     assert torch.allclose(g0['b.weight'], torch.full((4, 4), 2.0))
     assert torch.count_nonzero(g0['c.weight']) == 0
@@ -109,11 +111,12 @@ def _learner_worker(rank, world, port, q, batch_seed):
         q.put((rank, repr(e), None))
 
 
-def test_dp_step_equals_single_process_average():
+@pytest.mark.parametrize('world', [2, 4, 8])
+def test_dp_step_equals_single_process_average(world):
     from dotaclient_amd.learner.engine import Learner, LossConfig
     from dotaclient_amd.learner.synthetic import make_batch
     from dotaclient_amd.models.policy import Policy, get_config
-    world, port, seed = 2, _free_port(), 11
+    port, seed = _free_port(), 11
     ctx = mp.get_context('spawn')
     q = ctx.Queue()
     ps = [ctx.Process(target=_learner_worker, args=(r, world, port, q, seed)) for r in range(world)]
@@ -126,7 +129,8 @@ def test_dp_step_equals_single_process_average():
         out[r] = (torch.from_numpy(flat), torch.from_numpy(counts))
     for p in ps:
         p.join(timeout=60)
-    assert torch.equal(out[0][0], out[1][0])
+    for r in range(1, world):
+        assert torch.equal(out[0][0], out[r][0])
     # single-process oracle: average of the two per-rank gradients, same optimizer step
     torch.manual_seed(0)
     cfg = get_config('lstm128')
