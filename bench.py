@@ -34,6 +34,8 @@ BASELINE_STEPS_PER_S = 1000.0   # reference README.md:35 (one optimizer)
 
 def parse():
     ap = argparse.ArgumentParser()
+    from dotaclient_amd.presets import add_preset_arg
+    add_preset_arg(ap)
     ap.add_argument('--gpus', type=int, default=int(os.environ.get('WORLD_SIZE', 1)))
     ap.add_argument('--steps', type=int, default=20)
     ap.add_argument('--warmup', type=int, default=5)
@@ -54,7 +56,8 @@ def parse():
     ap.add_argument('--e2e', type=float, default=20.0,
                     help='seconds of the end-to-end actors→queue→learner loop on GPU 0 (1-GPU runs; 0 = off)')
     ap.add_argument('--e2e-games', type=int, default=1024)
-    return ap.parse_args()
+    from dotaclient_amd.presets import parse_with_preset
+    return parse_with_preset(ap, 'bench')
 
 
 def main():

@@ -26,6 +26,8 @@ def str2bool(v):
 
 def build_parser():
     ap = argparse.ArgumentParser(formatter_class=argparse.ArgumentDefaultsHelpFormatter)
+    from ..presets import add_preset_arg
+    add_preset_arg(ap)
     ap.add_argument('--ip', type=str, default='127.0.0.1', help='broker ip')
     ap.add_argument('--port', type=int, default=5672, help='broker port')
     ap.add_argument('--broker', type=str, default=None, help='broker url (overrides --ip/--port)')
@@ -72,7 +74,8 @@ def make_services(env: str, n: int, seed: int):
 
 
 def main(argv=None):
-    args = build_parser().parse_args(argv)
+    from ..presets import parse_with_preset
+    args = parse_with_preset(build_parser(), 'agent', argv)
     logging.basicConfig(format='%(asctime)s %(levelname)-8s %(message)s', level=args.log_level)
     from ..actor.game import Actor
     from ..actor.gpu_runner import GpuRunner, gpu_runner_supported

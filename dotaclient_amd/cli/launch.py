@@ -24,6 +24,8 @@ logger = logging.getLogger('dotaclient_amd.launch')
 
 def build_parser():
     ap = argparse.ArgumentParser(formatter_class=argparse.ArgumentDefaultsHelpFormatter)
+    from ..presets import add_preset_arg
+    add_preset_arg(ap)
     ap.add_argument('--port', type=int, default=5672)
     ap.add_argument('--actors', type=int, default=2)
     ap.add_argument('--games-per-actor', type=int, default=4)
@@ -82,7 +84,8 @@ class Supervisor:
 
 
 def main(argv=None):
-    args = build_parser().parse_args(argv)
+    from ..presets import parse_with_preset
+    args = parse_with_preset(build_parser(), 'launch', argv)
     logging.basicConfig(format='%(asctime)s %(levelname)-8s %(message)s', level='INFO')
     from ..transport.broker import TcpBrokerServer
     srv = TcpBrokerServer('127.0.0.1', args.port).start()
@@ -95,11 +98,16 @@ def main(argv=None):
                               '--master-addr', '127.0.0.1', '-m', 'dotaclient_amd.cli.optimizer']
     else:
         specs['optimizer'] = [py, '-m', 'dotaclient_amd.cli.optimizer']
-    specs['optimizer'] += ['--port', str(srv.port), '--log-dir', args.log_dir, '--model-preset', args.model_preset] + extra
+    pre = ['--preset', args.preset] if args.preset else []
+    specs['optimizer'] += (pre + ['--port', str(srv.port), '--log-dir', args.log_dir, '--model-preset',
+                                  args.model_preset] + extra)
     for i in range(args.actors):
-        specs[f'actor{i}'] = [py, '-m', 'dotaclient_amd.cli.agent', '--port', str(srv.port), '--games',
-                              str(args.games_per_actor), '--device', args.actor_device, '--model-preset',
-                              args.model_preset, '--seed', str(1000 + i)]
+        dev = args.actor_device
+        if dev == 'cuda' and args.optimizers > 1:
+            dev = f'cuda:{i % args.optimizers}'          # one actor process per GPU next to its learner rank
+        specs[f'actor{i}'] = [py, '-m', 'dotaclient_amd.cli.agent'] + pre + [
+            '--port', str(srv.port), '--games', str(args.games_per_actor), '--device', dev, '--model-preset',
+            args.model_preset, '--seed', str(1000 + i)]
     for i in range(args.validation):
         specs[f'val{i}'] = [py, '-m', 'dotaclient_amd.cli.agent', '--port', str(srv.port), '--validation', 'true',
                             '--log-dir', os.path.join(args.log_dir, 'val'), '--model-preset', args.model_preset]

@@ -27,6 +27,8 @@ def str2bool(v):
 def build_parser():
     from ..learner.optimizer import default_log_dir
     ap = argparse.ArgumentParser(formatter_class=argparse.ArgumentDefaultsHelpFormatter)
+    from ..presets import add_preset_arg
+    add_preset_arg(ap)
     ap.add_argument('--log-dir', type=str, default=default_log_dir())
     ap.add_argument('--ip', type=str, default='127.0.0.1')
     ap.add_argument('--port', type=int, default=5672)
@@ -69,7 +71,8 @@ def build_parser():
 
 
 def main(argv=None):
-    args = build_parser().parse_args(argv)
+    from ..presets import parse_with_preset
+    args = parse_with_preset(build_parser(), 'optimizer', argv)
     logging.basicConfig(format='%(asctime)s %(levelname)-8s %(message)s', level=args.log_level)
     import torch
     from ..learner.optimizer import DotaOptimizer, OptimizerConfig
