@@ -106,22 +106,39 @@ __device__ __forceinline__ void split_frag(const float* __restrict__ p, bf16x8& 
   }
 }
 
-// ---- V1 (exact fp32 VALU) dot product over one lane's K quarter: Σ_j wq[j]·x[j], x read from LDS with 16-B
-// broadcast loads (the 16 lanes of a row share the quarter). Four accumulators (j mod 4), issued as two packed
-// fp32 FMAs (v_pk_fma_f32: two lanes' worth of FMA per 4-cycle wave64 issue) — the step's dot products are VALU-issue
-// bound, not LDS bound: moving the operand into registers with DPP row broadcasts (one v_mov_dpp per FMA) measured
-// slower, 0.84 vs 0.76 µs for the compute phase at H = 512. Same per-accumulator order as scalar FMAs.
+// ---- V1 (exact fp32 VALU) dot products. Lane (r = lane/16, s = lane%16) of a wave owns FOUR outputs (the 4 gates
+// of one unit forward, 4 units backward) over ONE K slice of KSL = K/16 elements: the slice's operand is read from LDS
+// once (KSL/4 ds_read_b128, shared by the 4 rows through the LDS broadcast) and feeds 4 outputs, then a DPP row
+// reduction sums the 16 slices. The step is bound by LDS return bandwidth and VALU issue, not by the FMAs: the first
+// layout (lane = one output over a K quarter) read 4× the bytes — 32 × 1 KB per wave per step, 0.64 µs of compute
+// phase at H = 512 — and a register/DPP-broadcast operand (one v_mov_dpp per FMA) was slower still (0.84 µs). FMAs
+// issue as packed fp32 (v_pk_fma_f32, two outputs per instruction), two chains (even / odd k) per output pair.
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-template <int KQ>
-__device__ __forceinline__ float pk_dot(const float* wq, const float* x) {
-  f32x2 a = {0.f, 0.f}, b = {0.f, 0.f};
+template <int KSL>
+__device__ __forceinline__ void pk_dot4(const float* wq, const float* x, float& o0, float& o1, float& o2, float& o3) {
+  f32x2 a01e = {0.f, 0.f}, a01o = {0.f, 0.f}, a23e = {0.f, 0.f}, a23o = {0.f, 0.f};
 #pragma unroll
-  for (int j = 0; j < KQ; j += 4) {
+  for (int j = 0; j < KSL; j += 4) {
     const float4 v = *reinterpret_cast<const float4*>(x + j);
-    a = __builtin_elementwise_fma(f32x2{wq[j], wq[j + 1]}, f32x2{v.x, v.y}, a);
-    b = __builtin_elementwise_fma(f32x2{wq[j + 2], wq[j + 3]}, f32x2{v.z, v.w}, b);
+    a01e = __builtin_elementwise_fma(f32x2{wq[j], wq[KSL + j]}, f32x2{v.x, v.x}, a01e);
+    a23e = __builtin_elementwise_fma(f32x2{wq[2 * KSL + j], wq[3 * KSL + j]}, f32x2{v.x, v.x}, a23e);
+    a01o = __builtin_elementwise_fma(f32x2{wq[j + 1], wq[KSL + j + 1]}, f32x2{v.y, v.y}, a01o);
+    a23o = __builtin_elementwise_fma(f32x2{wq[2 * KSL + j + 1], wq[3 * KSL + j + 1]}, f32x2{v.y, v.y}, a23o);
+    a01e = __builtin_elementwise_fma(f32x2{wq[j + 2], wq[KSL + j + 2]}, f32x2{v.z, v.z}, a01e);
+    a23e = __builtin_elementwise_fma(f32x2{wq[2 * KSL + j + 2], wq[3 * KSL + j + 2]}, f32x2{v.z, v.z}, a23e);
+    a01o = __builtin_elementwise_fma(f32x2{wq[j + 3], wq[KSL + j + 3]}, f32x2{v.w, v.w}, a01o);
+    a23o = __builtin_elementwise_fma(f32x2{wq[2 * KSL + j + 3], wq[3 * KSL + j + 3]}, f32x2{v.w, v.w}, a23o);
   }
-  return (a.x + a.y) + (b.x + b.y);
+  const f32x2 a01 = a01e + a01o, a23 = a23e + a23o;
+  o0 = a01.x; o1 = a01.y; o2 = a23.x; o3 = a23.y;
+}
+// Σ over the 16 lanes of this lane's DPP row, result in every lane: xor 1, xor 2 (quad_perm), half-row and row mirrors
+__device__ __forceinline__ float row_sum16(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false));
+  return v;
 }
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, int bytes) {
@@ -263,14 +280,14 @@ __device__ __forceinline__ void lstm_team_fwd_body(
   constexpr int KSTEP = H / 32;         // k-steps of the full K
   constexpr int HP = H + 8;             // LDS row pitch (bf16)
   constexpr int RB = MT * 16;
-  constexpr int KQ = H / 4;             // V1: k-quarter per lane group
+  constexpr int KSL = H / 16;           // V1: K slice per lane
   static_assert(!V1 || (F32 && MT == 1), "V1 is the fp32 one-row variant");
   __shared__ short hl[V1 ? 1 : 2][V1 ? 1 : RB][V1 ? 1 : HP];
   __shared__ short hlo[F32 && !V1 ? 2 : 1][F32 && !V1 ? RB : 1][F32 && !V1 ? HP : 1];   // F32: lo bf16 half of h
-  // V1: h_{t-1} of row 0; each k-quarter padded by 4 floats so the four lane groups' broadcast reads of one
-  // ds_read_b128 hit different banks (quarters 512 B apart would all map to the same 4 banks: 2 cycles per group)
-  constexpr int QP = KQ + 4;
-  __shared__ __attribute__((aligned(16))) float hf[V1 ? 2 : 1][V1 ? 4 * QP : 4];
+  // V1: h_{t-1} of row 0 as 16 K slices, each padded by 4 floats (the 16 lanes of a row read 16 different slices
+  // with one ds_read_b128: unpadded 128-B strides would put pairs of lanes on the same banks)
+  constexpr int SP = KSL + 4;
+  __shared__ __attribute__((aligned(16))) float hf[V1 ? 2 : 1][V1 ? 16 * SP : 4];
   __shared__ int sh_int;
   __shared__ unsigned sh_epoch;
 
@@ -299,15 +316,20 @@ __device__ __forceinline__ void lstm_team_fwd_body(
   const int col = lane & 15, kg = lane >> 4;
   bf16x8 wf[V1 ? 1 : KSTEP];
   bf16x8 wfl[F32 && !V1 ? KSTEP : 1];
-  float wq[V1 ? KQ : 1];
+  float wq[V1 ? 4 * KSL : 1];
   if (mfma_wave) {
     const int row = (col & 3) * H + j0 + 4 * wv + (col >> 2);
     if constexpr (V1) {
-      const float* wr = static_cast<const float*>(whh_) + (size_t)row * H + kg * KQ;
+      // lane (u = lane/16, slice = lane%16): W_hh rows of the 4 gates of unit j0 + 4·wv + u over the slice
 #pragma unroll
-      for (int j = 0; j < KQ; j += 4) {
-        const float4 v = *reinterpret_cast<const float4*>(wr + j);
-        wq[j] = v.x; wq[j + 1] = v.y; wq[j + 2] = v.z; wq[j + 3] = v.w;
+      for (int g = 0; g < 4; ++g) {
+        const float* wr = static_cast<const float*>(whh_) + (size_t)(g * H + j0 + 4 * wv + (lane >> 4)) * H +
+                          (lane & 15) * KSL;
+#pragma unroll
+        for (int j = 0; j < KSL; j += 4) {
+          const float4 v = *reinterpret_cast<const float4*>(wr + j);
+          wq[g * KSL + j] = v.x; wq[g * KSL + j + 1] = v.y; wq[g * KSL + j + 2] = v.z; wq[g * KSL + j + 3] = v.w;
+        }
       }
     } else if constexpr (F32) {
       const float* whh = static_cast<const float*>(whh_);
@@ -321,8 +343,9 @@ __device__ __forceinline__ void lstm_team_fwd_body(
     }
   }
   // elementwise mapping after the 4×4 transpose: lane → (row 4·kg + (col&3) [+16·mt], unit j0 + 4·wv + col/4)
-  const int erow = 4 * kg + (col & 3);
-  const int eunit = j0 + 4 * wv + (col >> 2);
+  // (V1: lane (u, slice) → row = slice — only slice 0 is a live row —, unit j0 + 4·wv + u)
+  const int erow = V1 ? (lane & 15) : 4 * kg + (col & 3);
+  const int eunit = j0 + 4 * wv + (V1 ? (lane >> 4) : (col >> 2));
   // folded LSTM bias (b_ih + b_hh, unit-major): xp4 may then be the bare input projection
   const dca::f32x4 bv = (bias4 && mfma_wave) ? *reinterpret_cast<const dca::f32x4*>(bias4 + eunit * 4)
                                              : dca::f32x4{0.f, 0.f, 0.f, 0.f};
@@ -363,7 +386,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           const int b = i / H, k = i % H;
           const float v = h0[(size_t)(b0 + b) * H + k];
           if constexpr (V1) {
-            hf[par][k + (k / KQ) * 4] = v;
+            hf[par][(k / KSL) * SP + k % KSL] = v;
           } else {
             hl[par][b][k] = dca::f2bf(v);
             if constexpr (F32) hlo[par][b][k] = dca::f2bf(v - dca::bf2f(dca::f2bf(v)));
@@ -407,7 +430,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           if (ci < B * CPR) {
             if constexpr (V1) {
               const int k = 2 * ci;
-              *reinterpret_cast<float2*>(&hf[par][k + (k / KQ) * 4]) =
+              *reinterpret_cast<float2*>(&hf[par][(k / KSL) * SP + k % KSL]) =
                   make_float2(__int_as_float(g[i].x), __int_as_float(g[i].z));
             } else if constexpr (F32) {
               const int b = ci / CPR, k = (ci % CPR) * 2;
@@ -435,15 +458,12 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           if (mt * 16 >= B) break;                            // wave-uniform
           float gq0 = 0.f, gq1 = 0.f, gq2 = 0.f, gq3 = 0.f;
           if constexpr (V1) {
-            // ---- exact fp32 dot products over this lane's k-quarter, 4 partial chains (packed FMA)
-            float sum = pk_dot<KQ>(wq, &hf[par][kg * QP]);
-            sum += __shfl_xor(sum, 16, 64);
-            sum += __shfl_xor(sum, 32, 64);
-            // column col = 4·unit + gate: every lane of a quad receives the quad's four gates (quad_perm broadcast)
-            gq0 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sum), 0x00, 0xF, 0xF, false));
-            gq1 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sum), 0x55, 0xF, 0xF, false));
-            gq2 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sum), 0xAA, 0xF, 0xF, false));
-            gq3 = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(sum), 0xFF, 0xF, 0xF, false));
+            // ---- exact fp32: 4 gates of this lane's unit over its K slice, summed over the row's 16 slices
+            pk_dot4<KSL>(wq, &hf[par][(lane & 15) * SP], gq0, gq1, gq2, gq3);
+            gq0 = row_sum16(gq0);
+            gq1 = row_sum16(gq1);
+            gq2 = row_sum16(gq2);
+            gq3 = row_sum16(gq3);
           } else {
           // ---- gates pre-activation tile: rows = batch, columns = (unit, gate)
           dca::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -568,13 +588,13 @@ __device__ __forceinline__ void lstm_team_bwd_body(
   constexpr int RB = MT * 16;
   constexpr int GP = 4 * H + 8;         // LDS pitch (bf16) of the gathered dG rows
   constexpr int NPAIR = (RB * U + kThreads - 1) / kThreads;
-  constexpr int KQ = KW / 4;            // V1: k-group slice of a wave's K quarter
+  constexpr int KSL = KW / 16;          // V1: K slice per lane of a wave's K quarter
   static_assert(!V1 || (F32 && MT == 1), "V1 is the fp32 one-row variant");
   __shared__ short dgl[V1 ? 1 : RB][V1 ? 1 : GP];
   __shared__ short dglo[F32 && !V1 ? RB : 1][F32 && !V1 ? GP : 1];   // F32: lo bf16 half of the gathered dG
-  // V1: dG_{t+1} of row 0, fp32; every KQ-slice padded by 4 floats (bank spread of the broadcast reads, as forward)
-  constexpr int QP = KQ + 4;
-  __shared__ __attribute__((aligned(16))) float dgf[V1 ? 16 * QP : 4];
+  // V1: dG_{t+1} of row 0, fp32, as 64 K slices each padded by 4 floats (bank spread, as forward)
+  constexpr int SP = KSL + 4;
+  __shared__ __attribute__((aligned(16))) float dgf[V1 ? (4 * H / KSL) * SP : 4];
   __shared__ float red[4][RB][17];
   __shared__ float dbs[RB * U * 4];     // per-(row, unit, gate) bias-gradient sums of a chain
   __shared__ int sh_int;
@@ -602,12 +622,18 @@ __device__ __forceinline__ void lstm_team_bwd_body(
   const int col = lane & 15, kg = lane >> 4;
   bf16x8 wf[V1 ? 1 : KSTEP];
   bf16x8 wfl[F32 && !V1 ? KSTEP : 1];
-  float wq[V1 ? KQ : 1];
+  float wq[V1 ? 4 * KSL : 1];
   if constexpr (V1) {
+    // lane (ug = lane/16, slice = lane%16): W_hhᵀ of units j0 + 4·ug + uu (uu < 4) over the slice's gate columns
 #pragma unroll
-    for (int j = 0; j < KQ; ++j) {
-      const int gc = wv * KW + kg * KQ + j;
-      wq[j] = (col < U) ? static_cast<const float*>(whh_)[(size_t)((gc & 3) * H + (gc >> 2)) * H + j0 + col] : 0.f;
+    for (int uu = 0; uu < 4; ++uu) {
+      const int unit = 4 * (lane >> 4) + uu;
+#pragma unroll
+      for (int j = 0; j < KSL; ++j) {
+        const int gc = wv * KW + (lane & 15) * KSL + j;
+        wq[uu * KSL + j] =
+            (unit < U) ? static_cast<const float*>(whh_)[(size_t)((gc & 3) * H + (gc >> 2)) * H + j0 + unit] : 0.f;
+      }
     }
   }
 #pragma unroll
@@ -697,7 +723,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
             if (ci < nck) {
               if constexpr (V1) {
                 const int gc = 4 * (ci >> 1) + 2 * (ci & 1);
-                *reinterpret_cast<float2*>(&dgf[gc + (gc / KQ) * 4]) =
+                *reinterpret_cast<float2*>(&dgf[(gc / KSL) * SP + gc % KSL]) =
                     make_float2(__int_as_float(g[i].x), __int_as_float(g[i].z));
               } else if constexpr (F32) {
                 const int b = g0 + ci / (2 * H), r = ci % (2 * H), gc = 4 * (r >> 1) + 2 * (r & 1);
@@ -722,10 +748,19 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       TSTAMPB(2);
       // ---- partial recurrent gradient over this wave's K quarter → red[wv]
       if (V1 && k > 0) {
-        float sum = pk_dot<KQ>(wq, &dgf[(wv * 4 + kg) * QP]);
-        sum += __shfl_xor(sum, 16, 64);
-        sum += __shfl_xor(sum, 32, 64);
-        if (kg == 0) red[wv][0][col] = sum;
+        float o0, o1, o2, o3;
+        pk_dot4<KSL>(wq, &dgf[(wv * 16 + (lane & 15)) * SP], o0, o1, o2, o3);
+        o0 = row_sum16(o0);
+        o1 = row_sum16(o1);
+        o2 = row_sum16(o2);
+        o3 = row_sum16(o3);
+        const int u0 = 4 * (lane >> 4);
+        if ((lane & 15) == 0 && u0 < U) {
+          red[wv][0][u0] = o0;
+          red[wv][0][u0 + 1] = o1;
+          red[wv][0][u0 + 2] = o2;
+          red[wv][0][u0 + 3] = o3;
+        }
       } else if (k > 0) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
