@@ -31,6 +31,7 @@ constexpr int kD = 128;          // embedding width
 constexpr int kF = 10;           // unit features
 constexpr int kRows = 32;        // rows per workgroup
 constexpr int kLd = kD + 8;      // LDS scratch row stride (bf16): 272 B breaks the 256-B bank period
+constexpr int kJobs = 3;         // type jobs per wave; grid.y splits them over workgroups
 
 struct Layout {
   int U;
@@ -69,7 +70,7 @@ struct BwdParams {
   short* basic;         // same layout
   short* demb_lo;       // F32 only: lo bf16 halves of ∂emb / basic (value = hi + lo), same layout
   short* basic_lo;
-  float* w1part;        // (gridDim.x, 128·10 + 128) f32 per-workgroup ∂W1 ‖ ∂b1 partials
+  float* w1part;        // (gridDim.y·gridDim.x, 128·10 + 128) f32 per-workgroup ∂W1 ‖ ∂b1 partials
   int N;
   int compat;
   Layout L;
@@ -226,8 +227,8 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_kernel(FwdParams P) {
   __shared__ __attribute__((aligned(16))) short scr[4][kImg];
   __shared__ __attribute__((aligned(16))) float ust[4][16 * kUP];
 
-  // ---- env embedding: relu(We·env + be) → x896[:, 0:128] (32 rows × 128 cols over 256 threads)
-  {
+  // ---- env embedding: relu(We·env + be) → x896[:, 0:128] (32 rows × 128 cols over 256 threads; job 0's workgroups)
+  if (blockIdx.y == 0) {
     const int r = tid >> 3, c0 = (tid & 7) * 16;
     const int row = rbase + r;
     if (row < N) {
@@ -244,7 +245,9 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_kernel(FwdParams P) {
   short* img = &scr[wv][0];
 
   const int i = lane & 15, kg = lane >> 4;
-  for (int j = 0; j < 3; ++j) {
+  // job split over blockIdx.y (gridDim.y == 3: one type job per wave per workgroup; 1: all three)
+  const int jlo = gridDim.y == 3 ? (int)blockIdx.y : 0, jhi = gridDim.y == 3 ? jlo + 1 : 3;
+  for (int j = jlo; j < jhi; ++j) {
     int tau, g;
     type_job(wv, j, tau, g);
     const int cnt = P.L.cnt[tau], uoff = P.L.off[tau];
@@ -372,7 +375,9 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
   }
   for (int e = tid; e < kW1; e += 256) wred[e] = 0.f;
 
-  for (int j = 0; j < 3; ++j) {
+  // job split over blockIdx.y (gridDim.y == 3: one type job per wave per workgroup; 1: all three)
+  const int jlo = gridDim.y == 3 ? (int)blockIdx.y : 0, jhi = gridDim.y == 3 ? jlo + 1 : 3;
+  for (int j = jlo; j < jhi; ++j) {
     int tau, g;
     type_job(wv, j, tau, g);
     const int cnt = P.L.cnt[tau], uoff = P.L.off[tau];
@@ -529,7 +534,7 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
     }
   }
   __syncthreads();
-  for (int e = tid; e < kW1; e += 256) P.w1part[(size_t)blockIdx.x * kW1 + e] = wred[e];
+  for (int e = tid; e < kW1; e += 256) P.w1part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kW1 + e] = wred[e];
 }
 
 // ============================================================================================================
@@ -582,7 +587,7 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_f32_kernel(FwdParams P) {
   __shared__ __attribute__((aligned(16))) short scl[4][kImg];
   __shared__ __attribute__((aligned(16))) float ust[4][16 * kUP];
 
-  {   // env embedding (fp32 VALU)
+  if (blockIdx.y == 0) {   // env embedding (fp32 VALU; job 0's workgroups)
     const int r = tid >> 3, c0 = (tid & 7) * 16;
     const int row = rbase + r;
     if (row < N) {
@@ -599,7 +604,9 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_f32_kernel(FwdParams P) {
   short* img = &scr[wv][0];
   short* imgl = &scl[wv][0];
   const int i = lane & 15, kg = lane >> 4;
-  for (int j = 0; j < 3; ++j) {
+  // job split over blockIdx.y (gridDim.y == 3: one type job per wave per workgroup; 1: all three)
+  const int jlo = gridDim.y == 3 ? (int)blockIdx.y : 0, jhi = gridDim.y == 3 ? jlo + 1 : 3;
+  for (int j = jlo; j < jhi; ++j) {
     int tau, g;
     type_job(wv, j, tau, g);
     const int cnt = P.L.cnt[tau], uoff = P.L.off[tau];
@@ -707,7 +714,9 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_f32_kernel(BwdParams P) {
   }
   for (int e = tid; e < kW1; e += 256) wred[e] = 0.f;
 
-  for (int j = 0; j < 3; ++j) {
+  // job split over blockIdx.y (gridDim.y == 3: one type job per wave per workgroup; 1: all three)
+  const int jlo = gridDim.y == 3 ? (int)blockIdx.y : 0, jhi = gridDim.y == 3 ? jlo + 1 : 3;
+  for (int j = jlo; j < jhi; ++j) {
     int tau, g;
     type_job(wv, j, tau, g);
     const int cnt = P.L.cnt[tau], uoff = P.L.off[tau];
@@ -875,7 +884,7 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_f32_kernel(BwdParams P) {
     }
   }
   __syncthreads();
-  for (int e = tid; e < kW1; e += 256) P.w1part[(size_t)blockIdx.x * kW1 + e] = wred[e];
+  for (int e = tid; e < kW1; e += 256) P.w1part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kW1 + e] = wred[e];
 }
 
 // Fixed-order sum of the per-workgroup ∂W1‖∂b1 partials: block of 256 = 16 columns × 16 row phases (88 blocks;
@@ -1011,8 +1020,11 @@ extern "C" hipError_t dca_encoder_fwd(const float* units, const float* env, cons
   int acc = 0;
   for (int t = 0; t < 6; ++t) { P.L.cnt[t] = counts[t]; P.L.off[t] = acc; acc += counts[t]; }
   if (acc != U || U > 64) return hipErrorInvalidValue;
-  if (f32) encoder_fwd_f32_kernel<<<(N + kRows - 1) / kRows, 256, 0, st>>>(P);
-  else encoder_fwd_kernel<<<(N + kRows - 1) / kRows, 256, 0, st>>>(P);
+  // (row block, type job) grid: 3× the workgroups of a row-block grid, so small batches (the actor's few thousand
+  // rows) still fill the 256 CUs, and heavy jobs (16-unit types, dispatched first) are balanced by the light ones
+  const dim3 grid((N + kRows - 1) / kRows, kJobs);
+  if (f32) encoder_fwd_f32_kernel<<<grid, 256, 0, st>>>(P);
+  else encoder_fwd_kernel<<<grid, 256, 0, st>>>(P);
   return hipGetLastError();
 }
 
@@ -1037,7 +1049,7 @@ extern "C" size_t dca_encoder_bwd_workspace(int N, int U, const int* counts, int
   DwtJobs J;
   int NB;
   dwt_plan(N, counts, J, NB);
-  const size_t w1 = (size_t)((N + kRows - 1) / kRows) * kW1 * sizeof(float);
+  const size_t w1 = (size_t)((N + kRows - 1) / kRows) * kJobs * kW1 * sizeof(float);
   const size_t img = (size_t)U * NB * kD * 16 * sizeof(short);
   const size_t parts = (size_t)J.jbase[6] * kD * kD * sizeof(float);
   return w1 + (f32 ? 4 : 2) * img + parts;
@@ -1056,7 +1068,7 @@ extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const
   const int nblk = (N + kRows - 1) / kRows;
   char* p = static_cast<char*>(ws);
   float* w1part = reinterpret_cast<float*>(p);
-  p += (size_t)nblk * kW1 * sizeof(float);
+  p += (size_t)nblk * kJobs * kW1 * sizeof(float);
   const size_t img = (size_t)U * NB * kD * 16;
   short* demb = reinterpret_cast<short*>(p);
   short* basic = demb + img;
@@ -1074,9 +1086,10 @@ extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const
     acc += counts[t];
   }
   if (acc != U || U > 64) return hipErrorInvalidValue;
-  if (f32) encoder_bwd_f32_kernel<<<nblk, 256, 0, st>>>(P);
-  else encoder_bwd_kernel<<<nblk, 256, 0, st>>>(P);
-  encoder_w1_reduce<<<(kW1 + 15) / 16, 256, 0, st>>>(w1part, nblk, dw1, db1);
+  const dim3 grid(nblk, kJobs);
+  if (f32) encoder_bwd_f32_kernel<<<grid, 256, 0, st>>>(P);
+  else encoder_bwd_kernel<<<grid, 256, 0, st>>>(P);
+  encoder_w1_reduce<<<(kW1 + 15) / 16, 256, 0, st>>>(w1part, nblk * kJobs, dw1, db1);
   if (J.jbase[6] > 0) {
     if (f32) dwt_blocked_kernel<true><<<J.jbase[6], 256, 0, st>>>(demb, basic, demb_lo, basic_lo, J, parts);
     else dwt_blocked_kernel<false><<<J.jbase[6], 256, 0, st>>>(demb, basic, nullptr, nullptr, J, parts);
