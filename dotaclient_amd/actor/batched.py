@@ -79,6 +79,7 @@ class GpuActorPolicy:
         self.h = torch.zeros(n, H, device=dev)
         self.c = torch.zeros(n, H, device=dev)
         self.h16 = torch.zeros(n, H, dtype=torch.bfloat16, device=dev)
+        self.xh = torch.zeros(n, self.cfg.pre_rnn_dim + H, dtype=torch.bfloat16, device=dev)   # [x | bf16(h)]
         self.ctr = torch.zeros(1, dtype=torch.long, device=dev)
         self.idx = torch.zeros(n, 4, dtype=torch.int32, device=dev)
         self.act = torch.zeros(n, A, dtype=torch.uint8, device=dev)
@@ -118,11 +119,13 @@ class GpuActorPolicy:
             'bt': torch.stack([g(f'affine_unit_{s}.bias') for s in TYPE_SUFFIX]).contiguous(),
             'we': g('affine_env.weight').contiguous(), 'be': g('affine_env.bias'),
             'wpreT': bf('affine_pre_rnn.weight').t().contiguous(), 'bpre': g('affine_pre_rnn.bias'),
+            'bpre16': bf('affine_pre_rnn.bias').contiguous(),
         }
         H = self.cfg.hidden
         if self.cfg.rnn == 'lstm':
             w['wihT'] = bf('rnn.weight_ih_l0').t().contiguous()
             w['whhT'] = bf('rnn.weight_hh_l0').t().contiguous()
+            w['wcatT'] = torch.cat([bf('rnn.weight_ih_l0'), bf('rnn.weight_hh_l0')], 1).t().contiguous()
             w['brnn'] = g('rnn.bias_ih_l0') + g('rnn.bias_hh_l0')
         else:
             w['wfT'] = bf('fake_rnn.weight').t().contiguous()
@@ -155,31 +158,44 @@ class GpuActorPolicy:
 
     # ------------------------------------------------------------------------------------------------
     def _forward(self):
-        """The captured body: reads d_* / h / c, writes idx/act/msk/logp/value and the new h / c."""
+        """The captured body: reads d_* / h / c, writes idx/act/msk/logp/value and the new h / c.
+
+        bf16 path, 8 launches: encoder kernel → pre-RNN GEMM (bias + ReLU epilogue, bf16 out) → ``actor_state_prep``
+        (episode resets + the [x | bf16(h)] operand) → ONE gate GEMM (K = P + H, bias epilogue) → LSTM cell → heads
+        GEMM (bias epilogue) → sampling kernel → RNG counter."""
         C, w, cfg = self.C, self.w, self.cfg
-        if self.fp8:
-            from ..ops import fp8 as F8
-            mm = (lambda a, b: F8.linear(a, b))
-        else:
-            mm = (lambda a, b: torch.mm(a, b, out_dtype=torch.float32))
-        self.h.mul_(self.d_keep)
-        self.c.mul_(self.d_keep)
-        self.h16.copy_(self.h)
         x896, emb, _ = C.encoder_fwd(self.d_units, self.d_env, w['w1'], w['b1'], w['wt16'], w['bt'], w['we'],
                                      w['be'], list(cfg.layout.counts), bool(cfg.compat_bugs))
         if cfg.compat_bugs:
             x896[:, 768:896] = x896[:, 512:640]
-        x = torch.relu(mm(x896, w['wpreT']) + w['bpre']).to(torch.bfloat16)
-        if cfg.rnn == 'lstm':
-            gates = mm(x, w['wihT'])
-            gates += w['brnn']
-            gates += mm(self.h16, w['whhT'])
-            C.lstm_cell(gates, self.h, self.c, self.h16, self.d_active)
-            xh = self.h16
+        if self.fp8:
+            from ..ops import fp8 as F8
+            mm = (lambda a, b: F8.linear(a, b))
+            self.h.mul_(self.d_keep)
+            self.c.mul_(self.d_keep)
+            self.h16.copy_(self.h)
+            x = torch.relu(mm(x896, w['wpreT']) + w['bpre']).to(torch.bfloat16)
+            if cfg.rnn == 'lstm':
+                gates = mm(x, w['wihT'])
+                gates += w['brnn']
+                gates += mm(self.h16, w['whhT'])
+                C.lstm_cell(gates, self.h, self.c, self.h16, self.d_active)
+                xh = self.h16
+            else:
+                self.h.copy_(mm(x, w['wfT']) + w['bf'])
+                xh = self.h.to(torch.bfloat16)
+            z = mm(xh, w['whT']) + w['bh']
         else:
-            self.h.copy_(mm(x, w['wfT']) + w['bf'])
-            xh = self.h.to(torch.bfloat16)
-        z = mm(xh, w['whT']) + w['bh']
+            x = torch._addmm_activation(w['bpre16'], x896, w['wpreT'])
+            if cfg.rnn == 'lstm':
+                C.actor_state_prep(x, self.h, self.c, self.d_keep.view(-1), self.xh)
+                gates = torch.addmm(w['brnn'], self.xh, w['wcatT'], out_dtype=torch.float32)
+                C.lstm_cell(gates, self.h, self.c, self.h16, self.d_active)
+                xh = self.h16
+            else:
+                self.h.copy_(torch.addmm(w['bf'], x, w['wfT'], out_dtype=torch.float32))
+                xh = self.h.to(torch.bfloat16)
+            z = torch.addmm(w['bh'], xh, w['whT'], out_dtype=torch.float32)
         C.sample_actions(z, emb, self.d_handles, self.seed, self.ctr, self.idx, self.act, self.msk, self.logp,
                          self.value)
         self.ctr.add_(1)
@@ -200,17 +216,22 @@ class GpuActorPolicy:
             self.o_msk.copy_(self.msk, non_blocking=True)
 
     def capture(self):
-        """Warm up (hipBLASLt heuristics, allocator) on a side stream and capture the step body in a hipGraph."""
+        """Warm up (hipBLASLt heuristics, allocator) on a side stream and capture the WHOLE step — input copies from
+        the pinned staging buffers, the policy step, output copies back — in one hipGraph: a step is one launch."""
         s = self.stream
         s.wait_stream(torch.cuda.current_stream(self.device))
         ctr0 = self.ctr.clone()
         with torch.cuda.stream(s):
             for _ in range(3):
+                self._h2d()
                 self._forward()
+                self._d2h()
         torch.cuda.current_stream(self.device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
+        with torch.cuda.graph(g, stream=s, capture_error_mode='thread_local'):
+            self._h2d()
             self._forward()
+            self._d2h()
         torch.cuda.synchronize(self.device)
         # warm-up steps advanced the recurrent state and the RNG counter: start from a clean slate
         self.ctr.copy_(ctr0)
@@ -219,13 +240,15 @@ class GpuActorPolicy:
 
     # ------------------------------------------------------------------------------------------------
     def _snapshot(self, rows: np.ndarray):
+        """Gather the selected rows' (h, c) as they ENTER this step (before its resets, which the host applies from
+        the staged keep flags in :meth:`wait`), on the step stream ahead of the step."""
         k = len(rows)
         self.h_rows.numpy()[:k] = rows
+        self._snap_keep = self.h_keep.numpy()[rows, 0].copy()
         d = self.d_rows[:k]
         d.copy_(self.h_rows[:k], non_blocking=True)
-        keep = self.d_keep.index_select(0, d)
-        torch.mul(self.h.index_select(0, d), keep, out=self.d_snap[:k, 0])
-        torch.mul(self.c.index_select(0, d), keep, out=self.d_snap[:k, 1])
+        torch.index_select(self.h, 0, d, out=self.d_snap[:k, 0])
+        torch.index_select(self.c, 0, d, out=self.d_snap[:k, 1])
         self.o_snap[:k].copy_(self.d_snap[:k], non_blocking=True)
         self._snap_n = k
 
@@ -236,15 +259,15 @@ class GpuActorPolicy:
         if self.use_graph and self.graph is None:
             self.capture()
         with torch.cuda.stream(self.stream):
-            self._h2d()
             self._snap_n = 0
             if snapshot_rows is not None and len(snapshot_rows) and self.cfg.rnn == 'lstm':
                 self._snapshot(np.asarray(snapshot_rows))
             if self.graph is not None:
                 self.graph.replay()
             else:
+                self._h2d()
                 self._forward()
-            self._d2h()
+                self._d2h()
             self._done = torch.cuda.Event()
             self._done.record(self.stream)
 
@@ -256,7 +279,9 @@ class GpuActorPolicy:
             out['actions'] = self.o_act.numpy()
             out['masks'] = self.o_msk.numpy()
         if self._snap_n:
-            out['hidden'] = self.o_snap.numpy()[:self._snap_n]
+            hid = self.o_snap.numpy()[:self._snap_n]
+            hid *= self._snap_keep[:, None, None]        # resets of this step (keep = 0) → zero state
+            out['hidden'] = hid
         return out
 
     def step(self, env: np.ndarray, units: np.ndarray, handles: np.ndarray, reset: Optional[np.ndarray] = None,

@@ -147,7 +147,43 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const float* __restrict_
   h16[i] = dca::f2bf(hn);
 }
 
+// Actor step input staging: episode resets (h, c *= keep) and the combined gate-GEMM operand xh = [x | bf16(h)]
+// (N, P + H) bf16, so x·W_ihᵀ + h·W_hhᵀ + b is ONE GEMM (K = P + H, bias in its epilogue). pre: the pre-RNN
+// activations (N, P) bf16 (hipBLASLt ReLU epilogue). Replaces three elementwise passes, a cast and two GEMM-output adds.
+__global__ __launch_bounds__(256) void actor_state_prep_kernel(const short* __restrict__ pre, float* __restrict__ h,
+                                                               float* __restrict__ c, const float* __restrict__ keep,
+                                                               short* __restrict__ xh, int N, int P, int H) {
+  const int per = (P > H ? P : H) / 4;            // one 4-column quad of the row per thread
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= N * per) return;
+  const int n = i / per, j = (i % per) * 4;
+  short* xr = xh + (size_t)n * (P + H);
+  if (j < P) *reinterpret_cast<uint2*>(xr + j) = *reinterpret_cast<const uint2*>(pre + (size_t)n * P + j);
+  if (j < H) {
+    const float k = keep[n];
+    float4 hv = *reinterpret_cast<const float4*>(h + (size_t)n * H + j);
+    if (k != 1.f) {
+      float4 cv = *reinterpret_cast<const float4*>(c + (size_t)n * H + j);
+      hv.x *= k; hv.y *= k; hv.z *= k; hv.w *= k;
+      cv.x *= k; cv.y *= k; cv.z *= k; cv.w *= k;
+      *reinterpret_cast<float4*>(h + (size_t)n * H + j) = hv;
+      *reinterpret_cast<float4*>(c + (size_t)n * H + j) = cv;
+    }
+    const unsigned lo = (unsigned)(unsigned short)dca::f2bf(hv.x) | ((unsigned)(unsigned short)dca::f2bf(hv.y) << 16);
+    const unsigned hi = (unsigned)(unsigned short)dca::f2bf(hv.z) | ((unsigned)(unsigned short)dca::f2bf(hv.w) << 16);
+    *reinterpret_cast<uint2*>(xr + P + j) = make_uint2(lo, hi);
+  }
+}
+
 }  // namespace
+
+extern "C" hipError_t dca_actor_state_prep(const short* pre, float* h, float* c, const float* keep, short* xh, int N,
+                                           int P, int H, hipStream_t st) {
+  if (H % 4 || P % 4) return hipErrorInvalidValue;
+  const int per = (P > H ? P : H) / 4;
+  actor_state_prep_kernel<<<(N * per + 255) / 256, 256, 0, st>>>(pre, h, c, keep, xh, N, P, H);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t dca_sample_actions(const float* z, int ldz, const short* emb, const long long* handles, int N,
                                          int U, unsigned long long seed, const long long* ctr, int* idx,

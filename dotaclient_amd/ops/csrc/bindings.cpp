@@ -369,6 +369,16 @@ void sample_actions(torch::Tensor z, torch::Tensor emb, torch::Tensor handles, i
             "dca_sample_actions");
 }
 
+// Actor step staging: h, c *= keep (N) in place; xh (N, P + H) bf16 = [pre | bf16(h)] for the one-GEMM gates.
+void actor_state_prep(torch::Tensor pre, torch::Tensor h, torch::Tensor c, torch::Tensor keep, torch::Tensor xh) {
+  CHECK_BF16(pre); CHECK_F32(h); CHECK_F32(c); CHECK_F32(keep); CHECK_BF16(xh);
+  const int N = h.size(0), H = h.size(1), P = pre.size(1);
+  TORCH_CHECK(pre.dim() == 2 && pre.size(0) == N && c.sizes() == h.sizes() && keep.numel() == N && xh.dim() == 2 &&
+              xh.size(0) == N && xh.size(1) == P + H && H % 4 == 0 && P % 4 == 0, "actor_state_prep shapes");
+  hip_check(dca_actor_state_prep(ptr<short>(pre), ptr<float>(h), ptr<float>(c), ptr<float>(keep), ptr<short>(xh), N, P,
+                                 H, cur_stream()), "dca_actor_state_prep");
+}
+
 // LSTM cell from fp32 pre-activation gates (N,4H): updates h, c (N,H) f32 in place, writes h16 (N,H) bf16.
 // Optional ``active`` (N) f32: rows with active == 0 keep their h / c / h16 (slots not stepped this call).
 void lstm_cell(torch::Tensor gates, torch::Tensor h, torch::Tensor c, torch::Tensor h16,
@@ -740,6 +750,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("time_major") = false, py::arg("dg_out") = py::none(), py::arg("dg_bf16") = false,
         py::arg("want_dbias") = false);
   m.def("sample_actions", &sample_actions, "fused masked hierarchical Gumbel-max action sampling (actor)");
+  m.def("actor_state_prep", &actor_state_prep, "actor step: state resets + [x | bf16(h)] gate-GEMM operand");
   m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)", py::arg("gates"),
         py::arg("h"), py::arg("c"), py::arg("h16"), py::arg("active") = py::none());
   m.def("loss_prep", &loss_prep, "loss normalisers from one-hot action rows (graph-replayable)");
