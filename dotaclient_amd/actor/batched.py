@@ -31,15 +31,17 @@ LDZ = 160
 
 
 class GpuActorPolicy:
-    """Fixed-slot batched policy step on one GPU (fully-fused policies: no entity attention)."""
+    """Fixed-slot batched policy step on one GPU: LSTM / linear-RNN policies, 1v1 or 5v5 (entity attention)."""
 
     def __init__(self, policy: Policy, n_slots: int, device='cuda', seed: int = 0, use_graph: bool = True,
                  record: bool = True, fp8: bool = False, inputs_from: Optional['GpuActorPolicy'] = None):
         from .. import ops
         self.C = ops.require()
         cfg = policy.config
-        if cfg.entity_attention or cfg.unit_dim != 128 or cfg.env_dim != 128:
-            raise ValueError('GpuActorPolicy needs a fully-fused policy (no entity attention, 128-wide embeddings)')
+        if cfg.unit_dim != 128 or cfg.env_dim != 128:
+            raise ValueError('GpuActorPolicy needs 128-wide unit / env embeddings (the fused encoder kernel)')
+        if cfg.entity_attention and (cfg.layout.max_units != 64 or cfg.attention_heads != 4):
+            raise ValueError('GpuActorPolicy: the attention kernels cover 64 unit slots × 4 heads (the 5v5 preset)')
         self.cfg = cfg
         self.device = torch.device(device)
         self.n = n_slots
@@ -50,6 +52,8 @@ class GpuActorPolicy:
         self.record = record
         self.fp8 = fp8                   # e4m3 MFMA GEMMs (ops/fp8.py) for the pre-RNN, LSTM and heads projections
         self.policy = policy
+        import itertools
+        self.toff = [0] + list(itertools.accumulate(cfg.layout.counts))     # first slot of each unit type
         self._alloc(inputs_from)
         self.load_weights(policy)
         self.graph: Optional[torch.cuda.CUDAGraph] = None
@@ -115,12 +119,21 @@ class GpuActorPolicy:
         bf = (lambda k: sd[k].detach().to(dev, torch.bfloat16))
         w = {
             'w1': g('affine_unit_basic_stats.weight').contiguous(), 'b1': g('affine_unit_basic_stats.bias'),
+            # (entity attention: the encoder adds b_τ + b_out — the residual's bias folded into E0, as the learner)
             'wt16': torch.stack([bf(f'affine_unit_{s}.weight') for s in TYPE_SUFFIX]).contiguous(),
             'bt': torch.stack([g(f'affine_unit_{s}.bias') for s in TYPE_SUFFIX]).contiguous(),
             'we': g('affine_env.weight').contiguous(), 'be': g('affine_env.bias'),
             'wpreT': bf('affine_pre_rnn.weight').t().contiguous(), 'bpre': g('affine_pre_rnn.bias'),
             'bpre16': bf('affine_pre_rnn.bias').contiguous(),
         }
+        if self.cfg.entity_attention:
+            w['bt'] = (w['bt'] + g('entity_attn.out.bias')[None]).contiguous()
+            w['bout'] = g('entity_attn.out.bias').contiguous()
+            w['ln_g'] = g('entity_attn.ln.weight').contiguous()
+            w['ln_b'] = g('entity_attn.ln.bias').contiguous()
+            w['wqkv16'] = bf('entity_attn.qkv.weight').contiguous()
+            w['bqkv16'] = bf('entity_attn.qkv.bias').contiguous()
+            w['wout16'] = bf('entity_attn.out.weight').contiguous()
         H = self.cfg.hidden
         if self.cfg.rnn == 'lstm':
             w['wihT'] = bf('rnn.weight_ih_l0').t().contiguous()
@@ -166,7 +179,16 @@ class GpuActorPolicy:
         C, w, cfg = self.C, self.w, self.cfg
         x896, emb, _ = C.encoder_fwd(self.d_units, self.d_env, w['w1'], w['b1'], w['wt16'], w['bt'], w['we'],
                                      w['be'], list(cfg.layout.counts), bool(cfg.compat_bugs))
-        if cfg.compat_bugs:
+        if cfg.entity_attention:
+            # 5v5 pre-LN self-attention over the 64 unit slots (ops/csrc/attn.hip), pools of the attended embeddings
+            E0p = emb.view(self.n * self.U, 128)
+            Xn, _, _ = C.ln_fwd(E0p, w['bout'], w['ln_g'], w['ln_b'], 1e-5)
+            QKV = torch.addmm(w['bqkv16'], Xn, w['wqkv16'].t())
+            Oat, _ = C.attn_fwd(QKV)
+            E1 = torch.addmm(E0p, Oat, w['wout16'].t())                # residual + out-projection
+            C.attn_pool(E1, self.toff, x896, bool(cfg.compat_bugs))
+            emb = E1.view(self.n, self.U, 128)
+        elif cfg.compat_bugs:
             x896[:, 768:896] = x896[:, 512:640]
         if self.fp8:
             from ..ops import fp8 as F8
@@ -371,7 +393,8 @@ def make_slot_policy(policy: Policy, n_slots: int, device='cuda', **kw):
     """The fused graph-captured :class:`GpuActorPolicy` where it applies, else :class:`TorchSlotPolicy`."""
     dev = torch.device(device)
     cfg = policy.config
-    if dev.type == 'cuda' and not cfg.entity_attention and cfg.unit_dim == 128 and cfg.env_dim == 128:
+    if dev.type == 'cuda' and cfg.unit_dim == 128 and cfg.env_dim == 128 and (
+            not cfg.entity_attention or (cfg.layout.max_units == 64 and cfg.attention_heads == 4)):
         return GpuActorPolicy(policy, n_slots, device=dev, **kw)
     kw.pop('fp8', None)
     kw.pop('use_graph', None)

@@ -30,9 +30,11 @@ from .runner import StepOutput
 
 
 def gpu_runner_supported(policy: Policy) -> bool:
-    """Fully-fused policies (the batched GPU actor path) — no entity attention, 128-wide embeddings."""
+    """Policies the batched GPU actor path covers: 128-wide embeddings; entity attention over 64 slots × 4 heads."""
     cfg = policy.config
-    return (not cfg.entity_attention) and cfg.unit_dim == 128 and cfg.env_dim == 128
+    if cfg.entity_attention and (cfg.layout.max_units != 64 or cfg.attention_heads != 4):
+        return False
+    return cfg.unit_dim == 128 and cfg.env_dim == 128
 
 
 class GpuRunner:
@@ -41,7 +43,7 @@ class GpuRunner:
     def __init__(self, policy: Policy, device='cuda', seed: int = 0, capacity: int = 64, fp8: bool = False,
                  use_graph: bool = True):
         if not gpu_runner_supported(policy):
-            raise ValueError('GpuRunner needs a fully-fused policy (see gpu_runner_supported)')
+            raise ValueError('GpuRunner: policy not covered by the batched GPU actor (see gpu_runner_supported)')
         self.policy = policy
         self.device = torch.device(device)
         self.seed = int(seed)

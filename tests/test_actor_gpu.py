@@ -107,7 +107,7 @@ def test_lstm_cell_kernel(gpu_ops):
     torch.testing.assert_close(h16.float(), hr, atol=1e-2, rtol=1e-2)
 
 
-@pytest.mark.parametrize('preset', ['lstm512', 'lstm128', 'compat'])
+@pytest.mark.parametrize('preset', ['lstm512', 'lstm128', 'compat', '5v5'])
 @pytest.mark.parametrize('graph', [True, False])
 def test_gpu_actor_matches_policy(gpu_ops, preset, graph):
     """Graph-captured batched actor: values and log-probs of the sampled actions match the torch policy, with the

@@ -121,29 +121,30 @@ def test_vec_actor_league_opponents_and_hot_swap():
 
 
 @pytest.mark.gpu
-def test_vec_actor_gpu_graph_policy_replay_consistent():
+@pytest.mark.parametrize('preset,mode', [('lstm512', '1v1'), ('5v5', '5v5')])
+def test_vec_actor_gpu_graph_policy_replay_consistent(preset, mode):
     """The hipGraph GpuActorPolicy path (bf16 GEMMs, fused LSTM cell + sampling kernels) with league opponents:
     rollouts replay under the fp32 eager policy within bf16 tolerance (slot/state mix-ups would be O(1))."""
     import random
     from dotaclient_amd.actor.batched import GpuActorPolicy
     from dotaclient_amd.actor.league import League
     from dotaclient_amd.actor.vec import VecActor
-    cfg = get_config('lstm512')
+    cfg = get_config(preset)
     ws = _store(cfg, versions=(0, 1))
     sent = []
-    va = VecActor(ws, 16, sent.append, device='cuda', seed=3, rollout_size=32, max_dota_time=20.0,
-                  hidden_stride=16, threads=4, groups=2, latest_weights_prob=0.5,
+    va = VecActor(ws, 16 if mode == '1v1' else 4, sent.append, device='cuda', seed=3, rollout_size=32,
+                  max_dota_time=20.0, mode=mode, hidden_stride=16, threads=4, groups=2, latest_weights_prob=0.5,
                   league=League(ws, mode='uniform', rng=random.Random(1)))
     assert all(isinstance(g.gp, GpuActorPolicy) for g in va.groups)
-    while va.games_finished < 24:
+    while va.games_finished < (24 if mode == '1v1' else 6):
         va.step()
     va.close()
     assert va.opp_games_finished > 0
     pol = ws.policy_for(ws.latest_weights())
     rs = [decode(b) for b in sent]
     assert len(rs) > 16
-    for r in rs:
+    for r in rs[:60]:
         hs, vals, lps = _replay(pol, r, 16)
-        np.testing.assert_allclose(hs, r.hiddens, atol=5e-2)
+        np.testing.assert_allclose(hs, r.hiddens, atol=5e-2 if mode == '1v1' else 1e-1)
         np.testing.assert_allclose(vals, r.values, atol=5e-2)
         np.testing.assert_allclose(lps, r.logp, atol=1e-1)
