@@ -164,9 +164,6 @@ def main():
             mb = measure_actor_throughput(policy, device, n_games=args.actor_games, threads=args.actor_threads)
             actor['policy_step_per_s'] = mb['gpu_steps_per_s']
             actor['policy_step_protobuf_featurize_per_s'] = mb['steps_per_s']
-            f8 = measure_actor_throughput(policy, device, n_games=args.actor_games, fp8=True,
-                                          threads=args.actor_threads)
-            actor['fp8_policy_step_per_s'] = f8['gpu_steps_per_s']
         except Exception as e:
             actor['policy_step_error'] = repr(e)
 

@@ -8,7 +8,7 @@ h/c) lives on the GPU in fixed slots and one step of *all* slots is a captured g
     h, c *= keep                             episode resets without host round trips
     encoder_fwd                              fused entity encoder kernel (shared with the learner)
     relu(x896·W_preᵀ + b)                    hipBLASLt
-    gates = x·W_ihᵀ + h·W_hhᵀ + b            hipBLASLt (fp32 out) → lstm_cell kernel (or fake_rnn Linear)
+    gates = [x | h]·[W_ih | W_hh]ᵀ + b        ONE hipBLASLt GEMM (fp32 out) → lstm_cell kernel (or fake_rnn Linear)
     z = h·W_headsᵀ + b                       one GEMM for all 5 heads (q | enum | x | y | value)
     sample_actions                           fused masked log-softmax + Gumbel-max + hierarchical selection
     D2H(idx, logp, value[, act, msk])
@@ -34,7 +34,7 @@ class GpuActorPolicy:
     """Fixed-slot batched policy step on one GPU: LSTM / linear-RNN policies, 1v1 or 5v5 (entity attention)."""
 
     def __init__(self, policy: Policy, n_slots: int, device='cuda', seed: int = 0, use_graph: bool = True,
-                 record: bool = True, fp8: bool = False, inputs_from: Optional['GpuActorPolicy'] = None):
+                 record: bool = True, inputs_from: Optional['GpuActorPolicy'] = None):
         from .. import ops
         self.C = ops.require()
         cfg = policy.config
@@ -50,7 +50,6 @@ class GpuActorPolicy:
         self.seed = int(seed)
         self.use_graph = use_graph
         self.record = record
-        self.fp8 = fp8                   # e4m3 MFMA GEMMs (ops/fp8.py) for the pre-RNN, LSTM and heads projections
         self.policy = policy
         import itertools
         self.toff = [0] + list(itertools.accumulate(cfg.layout.counts))     # first slot of each unit type
@@ -136,8 +135,6 @@ class GpuActorPolicy:
             w['wout16'] = bf('entity_attn.out.weight').contiguous()
         H = self.cfg.hidden
         if self.cfg.rnn == 'lstm':
-            w['wihT'] = bf('rnn.weight_ih_l0').t().contiguous()
-            w['whhT'] = bf('rnn.weight_hh_l0').t().contiguous()
             w['wcatT'] = torch.cat([bf('rnn.weight_ih_l0'), bf('rnn.weight_hh_l0')], 1).t().contiguous()
             w['brnn'] = g('rnn.bias_ih_l0') + g('rnn.bias_hh_l0')
         else:
@@ -148,20 +145,6 @@ class GpuActorPolicy:
         bh = torch.cat([g(f'{k}.bias') for k in heads] + [torch.zeros(LDZ - 150, device=dev)], 0)
         w['whT'] = wh.to(torch.bfloat16).t().contiguous()
         w['bh'] = bh.contiguous()
-        if self.fp8:
-            from ..ops import fp8 as F8
-            src = {'wpreT': g('affine_pre_rnn.weight'), 'whT': wh}
-            if self.cfg.rnn == 'lstm':
-                src['wihT'] = g('rnn.weight_ih_l0')
-                src['whhT'] = g('rnn.weight_hh_l0')
-            else:
-                src['wfT'] = g('fake_rnn.weight')
-            for k, v in src.items():
-                if hasattr(self, 'w') and isinstance(self.w.get(k), F8.Fp8Weight):
-                    self.w[k].load_(v)
-                    w[k] = self.w[k]
-                else:
-                    w[k] = F8.Fp8Weight(v)
         if not hasattr(self, 'w'):
             self.w = w
         else:
@@ -190,34 +173,16 @@ class GpuActorPolicy:
             emb = E1.view(self.n, self.U, 128)
         elif cfg.compat_bugs:
             x896[:, 768:896] = x896[:, 512:640]
-        if self.fp8:
-            from ..ops import fp8 as F8
-            mm = (lambda a, b: F8.linear(a, b))
-            self.h.mul_(self.d_keep)
-            self.c.mul_(self.d_keep)
-            self.h16.copy_(self.h)
-            x = torch.relu(mm(x896, w['wpreT']) + w['bpre']).to(torch.bfloat16)
-            if cfg.rnn == 'lstm':
-                gates = mm(x, w['wihT'])
-                gates += w['brnn']
-                gates += mm(self.h16, w['whhT'])
-                C.lstm_cell(gates, self.h, self.c, self.h16, self.d_active)
-                xh = self.h16
-            else:
-                self.h.copy_(mm(x, w['wfT']) + w['bf'])
-                xh = self.h.to(torch.bfloat16)
-            z = mm(xh, w['whT']) + w['bh']
+        x = torch._addmm_activation(w['bpre16'], x896, w['wpreT'])
+        if cfg.rnn == 'lstm':
+            C.actor_state_prep(x, self.h, self.c, self.d_keep.view(-1), self.xh)
+            gates = torch.addmm(w['brnn'], self.xh, w['wcatT'], out_dtype=torch.float32)
+            C.lstm_cell(gates, self.h, self.c, self.h16, self.d_active)
+            xh = self.h16
         else:
-            x = torch._addmm_activation(w['bpre16'], x896, w['wpreT'])
-            if cfg.rnn == 'lstm':
-                C.actor_state_prep(x, self.h, self.c, self.d_keep.view(-1), self.xh)
-                gates = torch.addmm(w['brnn'], self.xh, w['wcatT'], out_dtype=torch.float32)
-                C.lstm_cell(gates, self.h, self.c, self.h16, self.d_active)
-                xh = self.h16
-            else:
-                self.h.copy_(torch.addmm(w['bf'], x, w['wfT'], out_dtype=torch.float32))
-                xh = self.h.to(torch.bfloat16)
-            z = torch.addmm(w['bh'], xh, w['whT'], out_dtype=torch.float32)
+            self.h.copy_(torch.addmm(w['bf'], x, w['wfT'], out_dtype=torch.float32))
+            xh = self.h.to(torch.bfloat16)
+        z = torch.addmm(w['bh'], xh, w['whT'], out_dtype=torch.float32)
         C.sample_actions(z, emb, self.d_handles, self.seed, self.ctr, self.idx, self.act, self.msk, self.logp,
                          self.value)
         self.ctr.add_(1)
@@ -396,7 +361,6 @@ def make_slot_policy(policy: Policy, n_slots: int, device='cuda', **kw):
     if dev.type == 'cuda' and cfg.unit_dim == 128 and cfg.env_dim == 128 and (
             not cfg.entity_attention or (cfg.layout.max_units == 64 and cfg.attention_heads == 4)):
         return GpuActorPolicy(policy, n_slots, device=dev, **kw)
-    kw.pop('fp8', None)
     kw.pop('use_graph', None)
     return TorchSlotPolicy(policy, n_slots, device=dev, **kw)
 
@@ -431,8 +395,7 @@ def _synthetic_states(n_states: int, seed: int = 0):
 
 
 def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048, steps: int = 50,
-                             warmup: int = 5, featurize: bool = True, threads: int = 8,
-                             fp8: bool = False) -> Dict[str, float]:
+                             warmup: int = 5, featurize: bool = True, threads: int = 8) -> Dict[str, float]:
     """Actor steps/s (player-observations → sampled actions per second) of one GPU-resident batched actor.
 
     ``n_games`` 1v1 games = 2·n_games player slots stepped per launch. With ``featurize`` the host side decodes
@@ -443,7 +406,7 @@ def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048,
     n = 2 * n_games
     dev = torch.device(device)
     layout = policy.config.layout
-    gp = GpuActorPolicy(policy, n, device=dev, seed=1234, record=True, fp8=fp8)
+    gp = GpuActorPolicy(policy, n, device=dev, seed=1234, record=True)
     feat = None
     if featurize:
         from .. import native

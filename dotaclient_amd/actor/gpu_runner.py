@@ -40,14 +40,13 @@ def gpu_runner_supported(policy: Policy) -> bool:
 class GpuRunner:
     stateful = True
 
-    def __init__(self, policy: Policy, device='cuda', seed: int = 0, capacity: int = 64, fp8: bool = False,
+    def __init__(self, policy: Policy, device='cuda', seed: int = 0, capacity: int = 64,
                  use_graph: bool = True):
         if not gpu_runner_supported(policy):
             raise ValueError('GpuRunner: policy not covered by the batched GPU actor (see gpu_runner_supported)')
         self.policy = policy
         self.device = torch.device(device)
         self.seed = int(seed)
-        self.fp8 = fp8
         self.use_graph = use_graph
         self.recurrent = policy.config.rnn == 'lstm'
         self.H = policy.config.hidden
@@ -68,7 +67,7 @@ class GpuRunner:
     def _grow(self, cap: int):
         old = self.gp
         gp = GpuActorPolicy(self.policy, cap, device=self.device, seed=self.seed, use_graph=self.use_graph,
-                            record=True, fp8=self.fp8)
+                            record=True)
         if self.use_graph:
             gp.capture()                 # capture zeroes the slot state: do it before carrying the old state over
         if old is not None:

@@ -54,7 +54,7 @@ class _Group:
                                    tag=f'{a.tag}{index}', stagger=a.stagger)
         self.S = self.ve.slots
         self.ppg = self.ve.players_per_game
-        self.gp = make_slot_policy(a.policy, self.S, device=a.device, seed=seed, fp8=a.fp8)
+        self.gp = make_slot_policy(a.policy, self.S, device=a.device, seed=seed)
         self.env = self.gp.h_env.numpy()
         self.units = self.gp.h_units.numpy()
         self.handles = self.gp.h_handles.numpy()
@@ -79,7 +79,7 @@ class VecActor:
     def __init__(self, weight_store, n_games: int, publish: Optional[Callable[[bytes], None]], device='cuda',
                  mode: str = '1v1', seed: int = 0, rollout_size: int = 10 ** 9, max_dota_time: float = 600.0,
                  latest_weights_prob: float = 1.0, hidden_stride: int = 256, threads: int = 8, groups: int = 2,
-                 league=None, fp8: bool = False, opponent_refresh: int = 64, start_time: float = -10.0,
+                 league=None, opponent_refresh: int = 64, start_time: float = -10.0,
                  fog: bool = True, tag: str = 'vec', stagger: bool = False):
         from .. import native
         if not native.AVAILABLE:
@@ -102,7 +102,6 @@ class VecActor:
         self.H = self.cfg.hidden if self.cfg.rnn == 'lstm' else 0
         self.threads = int(threads)
         self.league = league
-        self.fp8 = fp8
         self.opponent_refresh = int(opponent_refresh)
         self.start_time = float(start_time)
         self.fog = bool(fog)
@@ -141,7 +140,7 @@ class VecActor:
     def _opponent(self, g: _Group, k: int) -> _Opponent:
         while len(g.opp) <= k:
             gp = make_slot_policy(self.policy, g.S, device=self.device, seed=g.seed + 104729 * (len(g.opp) + 1),
-                                  fp8=self.fp8, inputs_from=g.gp)
+                                  inputs_from=g.gp)
             g.opp.append(_Opponent(gp))
         return g.opp[k]
 
@@ -272,8 +271,7 @@ class VecActor:
 
 
 def measure_vec_actor(policy, device='cuda', n_games: int = 2048, steps: int = 100, warmup: int = 10,
-                      threads: int = 8, groups: int = 2, hidden_stride: int = 256, rollout_size: int = 64,
-                      fp8: bool = False) -> Dict[str, float]:
+                      threads: int = 8, groups: int = 2, hidden_stride: int = 256, rollout_size: int = 64) -> Dict[str, float]:
     """Whole-runtime actor throughput: player-steps/s of :class:`VecActor` self-play (engine + featurize + reward +
     GPU policy + trajectory recording + rollout encoding), rollouts counted (published into a sink)."""
     from .weights import WeightStore
@@ -281,7 +279,7 @@ def measure_vec_actor(policy, device='cuda', n_games: int = 2048, steps: int = 1
     ws.add(0, {k: v.detach().cpu() for k, v in policy.state_dict().items()})
     sink = []
     va = VecActor(ws, n_games, lambda b: sink.append(len(b)), device=device, seed=1, threads=threads,
-                  groups=groups, hidden_stride=hidden_stride, rollout_size=rollout_size, fp8=fp8)
+                  groups=groups, hidden_stride=hidden_stride, rollout_size=rollout_size)
     sync = (lambda: torch.cuda.synchronize(va.device)) if va.device.type == 'cuda' else (lambda: None)
     for _ in range(warmup):
         va.step()

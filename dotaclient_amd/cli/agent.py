@@ -51,8 +51,6 @@ def build_parser():
     ap.add_argument('--wire', type=str, default='dcx1', choices=['dcx1', 'pickle'])
     ap.add_argument('--seed', type=int, default=None)
     ap.add_argument('--hidden-stride', type=int, default=256, help='store LSTM state every N steps')
-    ap.add_argument('--fp8', type=str2bool, default=False,
-                    help='GPU actor: e4m3 FP8 policy GEMMs (pre-RNN, LSTM input/recurrent, heads)')
     ap.add_argument('--runtime', type=str, default='auto', choices=['auto', 'vec', 'service'],
                     help='vec: native vectorised self-play (actor/vec.py, synthetic env only); service: the '
                          'protobuf Actor over DotaService games; auto: vec for synthetic self-play')
@@ -107,7 +105,7 @@ def main(argv=None):
         if device.startswith('cuda') and gpu_runner_supported(policy):
             # graph-captured batched GPU step; players' LSTM state lives in device slots
             return GpuRunner(policy.to(device), device=device, seed=seed_r, capacity=max(8, 2 * args.games),
-                             fp8=args.fp8)
+                             )
         return PolicyRunner(policy, device=device, seed=seed_r)
     runner_for = RunnerCache(make_runner, latest_policy=ws.latest_policy)
     metrics = MetricsWriter(args.log_dir) if (args.validation and args.log_dir) else None
@@ -157,7 +155,7 @@ def _run_vec(args, ws, broker, league, device, seed, cfg):
     va = VecActor(ws, args.games, broker.publish_experience, device=device,
                   mode='5v5' if cfg.layout.counts[0] > 1 else '1v1', seed=seed, rollout_size=args.rollout_size,
                   max_dota_time=args.max_dota_time, latest_weights_prob=args.use_latest_weights_prob,
-                  hidden_stride=args.hidden_stride, threads=args.threads, league=league, fp8=args.fp8, stagger=True)
+                  hidden_stride=args.hidden_stride, threads=args.threads, league=league, stagger=True)
     try:
         va.run(n_games=args.n_games)
     except Exception:

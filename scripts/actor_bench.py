@@ -1,4 +1,4 @@
-"""Batched GPU actor throughput alone (for rocprofv3): python3 scripts/actor_bench.py [n_games] [fp8]"""
+"""Batched GPU actor throughput alone (for rocprofv3): python3 scripts/actor_bench.py [n_games]"""
 import json
 import os
 import sys
@@ -10,7 +10,6 @@ from dotaclient_amd.actor.batched import measure_actor_throughput  # noqa: E402
 from dotaclient_amd.models.policy import Policy, get_config  # noqa: E402
 
 n_games = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
-fp8 = len(sys.argv) > 2 and sys.argv[2] == 'fp8'
 torch.manual_seed(0)
 policy = Policy(get_config('lstm512'))
-print(json.dumps(measure_actor_throughput(policy, torch.device('cuda:0'), n_games=n_games, fp8=fp8)))
+print(json.dumps(measure_actor_throughput(policy, torch.device('cuda:0'), n_games=n_games)))

@@ -163,39 +163,3 @@ def test_gpu_actor_matches_policy(gpu_ops, preset, graph):
             hg, _ = gp.hidden()
             assert ((hg - hidden[0][0]).norm() / hidden[0][0].norm()) < 2e-2
 
-
-def test_fp8_linear_matches_fp32(gpu_ops):
-    from dotaclient_amd.ops import fp8 as F8
-    torch.manual_seed(4)
-    x = torch.randn(256, 896, device='cuda')
-    w = torch.randn(512, 896, device='cuda') * 0.05
-    b = torch.randn(512, device='cuda')
-    y = F8.linear(x, F8.Fp8Weight(w), b)
-    ref = x @ w.t() + b
-    assert y.dtype == torch.float32
-    assert ((y - ref).norm() / ref.norm()).item() < 5e-2
-
-
-@pytest.mark.parametrize('preset', ['lstm512', 'compat'])
-def test_gpu_actor_fp8_close_to_bf16(gpu_ops, preset):
-    """e4m3 policy GEMMs: values and joint log-probs of the same sampled actions stay close to the bf16 actor."""
-    from dotaclient_amd.actor.batched import GpuActorPolicy
-    torch.manual_seed(5)
-    cfg = get_config(preset)
-    pol = Policy(cfg).cuda().eval()
-    n, U = 128, cfg.layout.max_units
-    rng = np.random.default_rng(0)
-    env = rng.standard_normal((n, 3)).astype(np.float32)
-    units = rng.standard_normal((n, U, 10)).astype(np.float32)
-    handles = np.where(rng.random((n, U)) < 0.5, rng.integers(1, 999, (n, U)), -1).astype(np.int64)
-    a = GpuActorPolicy(pol, n, device='cuda', seed=9, use_graph=True)
-    b = GpuActorPolicy(pol, n, device='cuda', seed=9, use_graph=True, fp8=True)
-    for _ in range(3):
-        oa = a.step(env, units, handles)
-        ob = b.step(env, units, handles)
-    va, vb = torch.tensor(oa['value']), torch.tensor(ob['value'])
-    assert (va - vb).abs().max() < 0.1 * va.abs().max() + 0.05
-    same = (oa['idx'] == ob['idx']).all(1)
-    assert same.mean() > 0.5          # same Gumbel noise → mostly identical draws
-    la, lb = torch.tensor(oa['logp'])[same], torch.tensor(ob['logp'])[same]
-    assert (la - lb).abs().mean() < 0.1
