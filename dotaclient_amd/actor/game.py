@@ -22,7 +22,7 @@ import time
 import uuid
 from collections import Counter
 from datetime import datetime
-from typing import Callable, Dict, List, Optional
+from typing import Callable, Dict, List, NamedTuple, Optional
 
 import numpy as np
 
@@ -88,11 +88,15 @@ class Player:
     def featurize(self, obs):
         hero = get_unit(obs, player_id=self.player_id)
         f = featurize(obs, self.player_id, self.team_id, layout=self.layout, hero_unit=hero)
-        if not self.creeps_had_spawned and obs.dota_time > 0.:
-            self.creeps_had_spawned = f.n_allied_creep > 0
-            if not self.creeps_had_spawned:
-                raise ValueError(f'Creeps have not spawned at timestep {obs.dota_time}')
+        self.check_creeps(f.n_allied_creep, obs.dota_time)
         return f, hero
+
+    def check_creeps(self, n_allied_creep: int, dota_time: float):
+        """Creep-spawn sanity check (agent.py:621-627)."""
+        if not self.creeps_had_spawned and dota_time > 0.:
+            self.creeps_had_spawned = n_allied_creep > 0
+            if not self.creeps_had_spawned:
+                raise ValueError(f'Creeps have not spawned at timestep {dota_time}')
 
     def record(self, f, out, i: int):
         """Store the step's policy input / sampled action / masks / behaviour data (agent.py:702-704)."""
@@ -125,6 +129,14 @@ class Player:
                        done=done, layout=self.layout.counts)
 
 
+class _NativeFeat(NamedTuple):
+    """Rows of one native ``featurize_batch`` call (same fields the actor reads from ``Featurized``)."""
+    env: np.ndarray
+    units: np.ndarray
+    handles: np.ndarray
+    n_allied_creep: int
+
+
 class _GameSlot:
     def __init__(self, service, game_id: str):
         self.service = service
@@ -152,7 +164,8 @@ class Actor:
                  config_fn: Callable, rollout_size: int = 10 ** 9, max_dota_time: float = 600.0,
                  latest_weights_prob: float = 1.0, validation: bool = False, layout: UnitLayout = LAYOUT_1V1,
                  hidden_size: Optional[int] = None, hidden_stride: int = 0, wire: str = 'dcx1',
-                 metrics=None, rng: Optional[random.Random] = None, league=None):
+                 metrics=None, rng: Optional[random.Random] = None, league=None,
+                 native_featurize: Optional[bool] = None, featurize_threads: int = 4):
         self.services = list(services)
         self.weight_store = weight_store
         self.runner_for = runner_for
@@ -169,6 +182,13 @@ class Actor:
         self.metrics = metrics
         self.rng = rng or random.Random()
         self.league = league          # actor/league.py; None = the reference's oldest-snapshot opponent
+        # featurize every player of a team-turn in ONE native call (C++ protobuf decode + featurizer, threads,
+        # GIL released; bit-identical to features/featurizer.py) instead of a python featurize per player
+        from .. import native
+        self.native_featurize = native.AVAILABLE if native_featurize is None else bool(native_featurize)
+        if self.native_featurize and not native.AVAILABLE:
+            raise RuntimeError('native_featurize=True but the native module is not built')
+        self.featurize_threads = int(featurize_threads)
         self.slots: List[Optional[_GameSlot]] = [None] * len(self.services)
         self.games_finished = 0
         self.steps_taken = 0
@@ -282,8 +302,13 @@ class Actor:
                 p.compute_reward(prev_obs=slot.prev_obs[team], obs=obs)
                 slot.reward_sum[team] += sum(p.rewards[-1].values())
                 p.rewarded = True
-                f, hero = p.featurize(obs)
-                batch.append((slot, p, f, hero))
+                if self.native_featurize:
+                    batch.append((slot, p, obs, None))
+                else:
+                    f, hero = p.featurize(obs)
+                    batch.append((slot, p, f, hero))
+        if self.native_featurize and batch:
+            batch = self._featurize_native(batch)
         # one batched policy step per distinct policy object
         # (a player bound to a stateful runner stays with it: its recurrent state lives there)
         groups: Dict[int, List[int]] = {}
@@ -331,6 +356,26 @@ class Actor:
             acts.dota_time = slot.cur_obs.dota_time
             slot.service.act_sync(pb.Actions(actions=acts, team_id=team))
             slot.prev_obs[team] = slot.cur_obs
+
+    def _featurize_native(self, batch):
+        """(slot, player, obs, None) → (slot, player, features, hero unit): one serialisation per observation, one
+        native call for all players of the team-turn."""
+        from .. import native
+        wire, states = {}, []
+        for _, _, obs, _ in batch:
+            b = wire.get(id(obs))
+            if b is None:
+                b = wire[id(obs)] = obs.SerializeToString()
+            states.append(b)
+        env, units, handles, ncreep = native.featurize_batch(
+            states, [p.player_id for _, p, _, _ in batch], [p.team_id for _, p, _, _ in batch],
+            list(self.layout.counts), self.featurize_threads)
+        out = []
+        for k, (slot, p, obs, _) in enumerate(batch):
+            hero = get_unit(obs, player_id=p.player_id)
+            p.check_creeps(int(ncreep[k]), obs.dota_time)
+            out.append((slot, p, _NativeFeat(env[k], units[k], handles[k], int(ncreep[k])), hero))
+        return out
 
     def step(self):
         """One observation interval for every game (both teams), starting/finishing games as needed."""

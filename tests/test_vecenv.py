@@ -178,3 +178,23 @@ def test_vecenv_rollouts_equal_python_actor(seed, rollout_size):
             for k in ('env', 'units', 'actions', 'masks', 'rewards', 'logp', 'values', 'canvas'):
                 np.testing.assert_array_equal(getattr(rg, k), getattr(rw, k), err_msg=f'{key} {k}')
             assert (rg.done, rg.weight_version, rg.bootstrap_value) == (rw.done, rw.weight_version, rw.bootstrap_value)
+
+
+@pytest.mark.parametrize('seed', [5, 29])
+def test_actor_native_featurize_rollouts_identical(seed):
+    """The protobuf Actor with the native batched featurizer (one C++ call per team-turn) publishes exactly the
+    rollouts of the python-featurizer Actor."""
+    from dotaclient_amd.actor.game import Actor
+    out = {}
+    for nat in (False, True):
+        sent = []
+        actor = Actor([SyntheticDotaService(seed=seed + i) for i in range(3)], _Store(), lambda pol: _Runner(),
+                      sent.append, get_1v1_selfplay_config, rollout_size=40, max_dota_time=60.0, layout=LAYOUT_1V1,
+                      native_featurize=nat)
+        while actor.games_finished < 3:
+            actor.step()
+        out[nat] = [decode(b) for b in sent]
+    assert len(out[True]) == len(out[False]) > 0
+    for a, b in zip(out[False], out[True]):
+        for k in ('env', 'units', 'actions', 'masks', 'rewards', 'logp', 'values', 'canvas'):
+            np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
