@@ -54,6 +54,8 @@ def build_parser():
     ap.add_argument('--device', type=str, default='auto')
     ap.add_argument('--backend', type=str, default='auto', choices=['auto', 'fused', 'torch'])
     ap.add_argument('--graph', type=int, default=1, help='capture the fused train step in a hipGraph')
+    ap.add_argument('--async-checkpoint', type=int, default=1,
+                    help='publish the model first, write checkpoint files on a background thread')
     ap.add_argument('--precision', type=str, default='fp32', choices=['fp32', 'bf16'],
                     help='fp32 = reference training precision (bf16x3 split-MFMA kernels); bf16 = bf16 GEMM operands')
     ap.add_argument('--gamma', type=float, default=0.98)
@@ -93,7 +95,7 @@ def main(argv=None):
                           iterations=args.iterations, algo=args.algo, model=args.model_preset, gamma=args.gamma,
                           gae_lambda=args.gae_lambda, clip_eps=args.clip_eps, max_grad_norm=args.max_grad_norm,
                           compat_value_bug=args.compat_value_bug, device=device, backend=args.backend,
-                          precision=args.precision, graph=bool(args.graph),
+                          precision=args.precision, graph=bool(args.graph), async_checkpoint=bool(args.async_checkpoint),
                           checkpoint_keep=args.checkpoint_keep, replay_gb=args.replay_gb,
                           replay_capacity=args.replay_capacity, replay_recent=args.replay_recent,
                           allow_pickle_experience=args.allow_pickle_experience)

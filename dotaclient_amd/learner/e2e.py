@@ -47,10 +47,14 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
     broker = InProcBroker(maxsize=queue_size, drop_oldest=True)
     cfg = OptimizerConfig(log_dir=tmp, epochs=epochs, seq_per_epoch=seq_per_epoch, batch_size=batch_size,
                           seq_len=seq_len, model=model, precision=precision, device=str(device), checkpoint_keep=2,
-                          run_local=True, xp_timeout=300.0, histogram_freq=10 ** 9)
+                          run_local=True, xp_timeout=300.0, histogram_freq=10 ** 9, async_checkpoint=True)
     opt = DotaOptimizer(cfg, broker)                       # publishes model version 0
     ws = WeightStore(model, device='cpu')
-    broker.subscribe_model(ws.add_bytes)
+    from concurrent.futures import ThreadPoolExecutor
+    loader = ThreadPoolExecutor(1, thread_name_prefix='weights')
+    # decode + load of a published model on its own thread (the in-proc broker calls subscribers synchronously)
+    broker.subscribe_model(lambda v, b: loader.submit(ws.add_bytes, v, b))
+    loader.submit(lambda: None).result()
     va = VecActor(ws, games, broker.publish_experience, device=device, seed=11, rollout_size=rollout_size,
                   max_dota_time=max_dota_time, hidden_stride=seq_len, threads=threads, stagger=True)
     for _ in range(3):                                     # capture the actor graphs before the learner's
@@ -95,6 +99,8 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
         stop.set()
         th.join(timeout=60)
         va.close()
+        opt.flush_checkpoints()
+        loader.shutdown(wait=True)
         if log_dir is None:
             shutil.rmtree(tmp, ignore_errors=True)
     a = np.asarray(rows, dtype=np.float64)

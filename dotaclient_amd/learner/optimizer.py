@@ -81,6 +81,7 @@ class OptimizerConfig:
     artifact_url: Optional[str] = None  # off-node mirror of checkpoints + events (reference: GCS bucket, §utils.artifacts)
     allow_pickle_experience: bool = False  # accept reference-agent pickles (restricted unpickler); off: DCX1 only
     graph: bool = True                 # capture the fused train step in a hipGraph (learner/engine.py enable_graph)
+    async_checkpoint: bool = False     # write checkpoint files on a background thread (the model is published first)
 
 
 class Sequence:
@@ -376,9 +377,16 @@ class DotaOptimizer:
             for it in range(self.iteration_start, end):
                 self.run_iteration(it)
         finally:
+            self.flush_checkpoints()
             if self.uploader is not None:
                 self.uploader.flush()
         return end
+
+    def flush_checkpoints(self):
+        """Wait for the background checkpoint writes (``async_checkpoint``)."""
+        ex = getattr(self, '_ckpt_pool', None)
+        if ex is not None:
+            ex.submit(lambda: None).result()
 
     def run_iteration(self, it: int):
         cfg = self.cfg
@@ -448,7 +456,10 @@ class DotaOptimizer:
         sub = np.stack(subrewards) / n_steps * OBSERVATIONS_PER_SECOND
         rollout_rewards = sub.sum(axis=1)
         reward_dict = dict(zip(REWARD_KEYS, sub.sum(axis=0)))
-        mean = {k: torch.stack(v).float().mean().item() for k, v in metrics_acc.items()}
+        # every metric's iteration mean in ONE device→host copy (not one synchronising .item() per metric)
+        keys = list(metrics_acc)
+        means = torch.stack([torch.stack(metrics_acc[k]).float().mean() for k in keys]).cpu().tolist()
+        mean = dict(zip(keys, means))
         metrics = {
             self.SPEED_KEY: steps_per_s,
             'samples per s per gpu': steps_per_s * cfg.epochs,
@@ -503,12 +514,40 @@ class DotaOptimizer:
     def upload_model(self, version: int):
         if not self.checkpoint:
             return
-        path, data = ckpt.save_model(self.policy.state_dict(), self.cfg.log_dir, version)
-        spath = ckpt.save_trainer_state({'learner': self.learner.state_dict(), 'running': self.running.state_dict(),
-                                         'iteration': version, 'config': asdict(self.cfg)}, self.cfg.log_dir, version)
+        import io
+        sd = {k: v.detach().cpu() for k, v in self.policy.state_dict().items()}
+        buf = io.BytesIO()
+        torch.save(sd, buf)
+        data = buf.getvalue()
+        trainer = {'learner': _to_cpu(self.learner.state_dict()), 'running': self.running.state_dict(),
+                   'iteration': version, 'config': asdict(self.cfg)}
+        if not self.cfg.async_checkpoint:
+            self._write_checkpoint(data, trainer, version)
+            self.broker.publish_model(data, version)
+            return
+        # publish first (actors see the new weights now); the files follow on one ordered background writer
+        self.broker.publish_model(data, version)
+        if getattr(self, '_ckpt_pool', None) is None:
+            from concurrent.futures import ThreadPoolExecutor
+            self._ckpt_pool = ThreadPoolExecutor(1, thread_name_prefix='ckpt')
+        self._ckpt_pool.submit(self._write_checkpoint, data, trainer, version)
+
+    def _write_checkpoint(self, data: bytes, trainer, version: int):
+        path = ckpt.write_model_bytes(data, self.cfg.log_dir, version)
+        spath = ckpt.save_trainer_state(trainer, self.cfg.log_dir, version)
         if self.uploader is not None:   # reference optimizer.py:713-715 (GCS upload of the model file)
             self.uploader.submit(path, f'{self.store_prefix}/{os.path.basename(path)}')
             self.uploader.submit(spath, f'{self.store_prefix}/{os.path.basename(spath)}')
             self.uploader.flush()       # a pruned file must not vanish before its upload
         ckpt.prune(self.cfg.log_dir, self.cfg.checkpoint_keep)
-        self.broker.publish_model(data, version)
+
+
+def _to_cpu(x):
+    """Host snapshot of a (nested) state dict: device tensors copied now, so a background writer sees this step."""
+    if isinstance(x, torch.Tensor):
+        return x.detach().cpu()
+    if isinstance(x, dict):
+        return {k: _to_cpu(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_to_cpu(v) for v in x)
+    return x

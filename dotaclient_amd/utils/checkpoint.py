@@ -34,16 +34,21 @@ def _atomic_save(obj, path: str):
 def save_model(state_dict, log_dir: str, version: int) -> Tuple[str, bytes]:
     """Write ``model_%09d.pt``; returns (path, serialized bytes) so the caller can also publish the bytes."""
     import io
-    os.makedirs(log_dir, exist_ok=True)
     buf = io.BytesIO()
     torch.save({k: v.detach().cpu() for k, v in state_dict.items()}, buf)
     data = buf.getvalue()
+    return write_model_bytes(data, log_dir, version), data
+
+
+def write_model_bytes(data: bytes, log_dir: str, version: int) -> str:
+    """Atomically write already-serialised ``model_%09d.pt`` bytes (tmp file + rename)."""
+    os.makedirs(log_dir, exist_ok=True)
     path = os.path.join(log_dir, MODEL_FILENAME_FMT % version)
     tmp = path + '.tmp'
     with open(tmp, 'wb') as f:
         f.write(data)
     os.replace(tmp, path)
-    return path, data
+    return path
 
 
 def save_trainer_state(state, log_dir: str, version: int) -> str:
