@@ -57,11 +57,6 @@ class Learner:
         self.policy = policy.to(self.device)
         if backend == 'auto':
             backend = 'fused' if self.device.type == 'cuda' else 'torch'
-        if backend == 'fused' and precision == 'fp32' and self.policy.config.entity_attention:
-            import logging
-            logging.getLogger(__name__).warning('fp32 learner: the 5v5 entity-attention policy runs on the eager fp32 '
-                                                'path (its fused kernels are bf16: precision="bf16")')
-            backend = 'torch'
         self.backend = backend
         self.flat = FlatParams(self.policy, device=self.device)
         self.dp = DataParallel(self.policy, flat=self.flat, bucket_cap_mb=bucket_cap_mb, overlap=overlap,

@@ -24,8 +24,9 @@ Precision (``FusedPolicy(precision=...)``):
   run on hipBLASLt's exact-f32 path. The LSTM hidden state is exchanged and stored in fp32.
 * ``'bf16'``: bf16 GEMM operands / saved activations, fp32 accumulation, recurrence state and optimizer.
 
-The 5v5 entity-attention policy has fused kernels on the bf16 pipelined step; in fp32 the learner runs it on the
-eager fp32 reference path (``learner/engine.py``).
+The 5v5 entity-attention block runs on its bf16 kernels (ops/csrc/attn.hip) in the bf16 learner and as explicit
+fp32 torch ops with a hand-written backward in the fp32 learner (``models/pipelined.py:_attn_fwd_f32``); the rest
+of the 5v5 step is the same fused pipeline.
 """
 from __future__ import annotations
 
@@ -247,9 +248,6 @@ class FusedPolicy:
         self.loss_cfg = loss_cfg
         self.precision = precision
         self.fp32 = precision == 'fp32'
-        if self.fp32 and self.cfg.entity_attention:
-            raise ValueError('the fp32 fused learner has no entity-attention kernels: use backend="torch" (fp32 '
-                             'eager) or precision="bf16" for the 5v5 policy')
         dev = next(policy.parameters()).device
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.param_names: List[str] = [n for n, _ in policy.named_parameters()]

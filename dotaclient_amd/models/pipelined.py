@@ -101,7 +101,7 @@ class WeightImages:
         parts32 = {'bt': (torch.stack([idx(f'affine_unit_{s}.bias') for s in TYPE_SUFFIX]), None),
                    'bias4': (idx('rnn.bias_ih_l0')[perm], idx('rnn.bias_hh_l0')[perm]),
                    'bcat': (bcat, None)}
-        if cfg.entity_attention:
+        if cfg.entity_attention and not getattr(fp, 'fp32', False):
             # 5v5 attention block; the encoder adds b_τ + b_out (residual bias folded into E0, see attn.hip)
             parts16['wqkv16'] = idx('entity_attn.qkv.weight')
             parts16['bqkv16'] = idx('entity_attn.qkv.bias')
@@ -148,6 +148,82 @@ class WeightImages:
         return self.views
 
 
+# ---- fp32 entity-attention block (5v5 at the reference precision) ------------------------------------------------
+# The bf16 learner runs the block on ops/csrc/attn.hip; the fp32 learner runs it as explicit fp32 torch ops with a
+# hand-written backward (no autograd graph: the step stays capturable), between the bf16x3 encoder kernels and the
+# rest of the fused step. Same math as models/policy.py:EntityAttention + the per-type max-pools (pool gradients
+# routed to the first maximal unit — the encoder kernels' convention).
+def _attn_fwd_f32(E0, P, heads: int, eps: float = 1e-5):
+    N, U, D = E0.shape
+    d = D // heads
+    mu = E0.mean(-1, keepdim=True)
+    xc = E0 - mu
+    rstd = torch.rsqrt((xc * xc).mean(-1, keepdim=True) + eps)
+    xhat = xc * rstd
+    Xn = xhat * P['entity_attn.ln.weight'] + P['entity_attn.ln.bias']
+    qkv = torch.addmm(P['entity_attn.qkv.bias'], Xn.view(N * U, D), P['entity_attn.qkv.weight'].t())
+    q, k, v = qkv.view(N, U, 3, heads, d).permute(2, 0, 3, 1, 4).unbind(0)          # (N, h, U, d)
+    att = torch.softmax(torch.matmul(q, k.transpose(-1, -2)) * (1.0 / float(d) ** 0.5), dim=-1)
+    o = torch.matmul(att, v).transpose(1, 2).reshape(N * U, D)
+    E1 = torch.addmm(P['entity_attn.out.bias'], o, P['entity_attn.out.weight'].t()).view(N, U, D) + E0
+    return E1, (xhat, rstd, Xn, q, k, v, att, o)
+
+
+def _attn_bwd_f32(saved, dE1, P, heads: int):
+    xhat, rstd, Xn, q, k, v, att, o = saved
+    N, U, D = dE1.shape
+    d = D // heads
+    g = {}
+    dE1f = dE1.reshape(N * U, D)
+    g['entity_attn.out.weight'] = dE1f.t() @ o
+    g['entity_attn.out.bias'] = dE1f.sum(0)
+    do = (dE1f @ P['entity_attn.out.weight']).view(N, U, heads, d).transpose(1, 2)   # (N, h, U, d)
+    dv = torch.matmul(att.transpose(-1, -2), do)
+    dp = torch.matmul(do, v.transpose(-1, -2))
+    ds = att * (dp - (dp * att).sum(-1, keepdim=True)) * (1.0 / float(d) ** 0.5)
+    dq = torch.matmul(ds, k)
+    dk = torch.matmul(ds.transpose(-1, -2), q)
+    dqkv = torch.stack([dq, dk, dv], 0).permute(1, 3, 0, 2, 4).reshape(N * U, 3 * D)
+    g['entity_attn.qkv.weight'] = dqkv.t() @ Xn.view(N * U, D)
+    g['entity_attn.qkv.bias'] = dqkv.sum(0)
+    dXn = (dqkv @ P['entity_attn.qkv.weight']).view(N, U, D)
+    g['entity_attn.ln.weight'] = (dXn * xhat).sum((0, 1))
+    g['entity_attn.ln.bias'] = dXn.sum((0, 1))
+    dxh = dXn * P['entity_attn.ln.weight']
+    dE0 = dE1 + rstd * (dxh - dxh.mean(-1, keepdim=True) - xhat * (dxh * xhat).mean(-1, keepdim=True))
+    return dE0, g
+
+
+def _attn_pools_f32(E1, toff, x896, compat: bool):
+    """x896[:, 128:] = per-type max over the attended embeddings; returns each type's argmax (N, 128)."""
+    idx = []
+    for t in range(6):
+        o0, o1 = toff[t], toff[t + 1]
+        if compat and t == 5:      # reference policy.py:127: the enemy-tower pool is the enemy-nonhero pool
+            o0, o1 = toff[3], toff[4]
+        if o1 > o0:
+            seg = E1[:, o0:o1]
+            a = seg.argmax(1)
+            x896[:, 128 * (t + 1):128 * (t + 2)] = seg.gather(1, a.unsqueeze(1)).squeeze(1)
+        else:
+            a = None
+            x896[:, 128 * (t + 1):128 * (t + 2)] = 0.
+        idx.append(a)
+    return idx
+
+
+def _attn_demb_f32(dtl, q, dx896, idx, toff, compat: bool):
+    """∂E1 = dtl ⊗ q (pointer logits) + each type's pool gradient at its argmax unit."""
+    dE1 = dtl.unsqueeze(-1) * q.unsqueeze(1)
+    for t in range(6):
+        a = idx[t]
+        if a is None:
+            continue
+        o0, o1 = (toff[3], toff[4]) if (compat and t == 5) else (toff[t], toff[t + 1])
+        dE1[:, o0:o1].scatter_add_(1, a.unsqueeze(1), dx896[:, 128 * (t + 1):128 * (t + 2)].unsqueeze(1))
+    return dE1
+
+
 def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], units_t, env_t, act_t, msk_t, adv_t,
                   ret_t, lpo_t, nret_t, norms, h0, c0, B: int, S: int, gout: Optional[Dict[str, torch.Tensor]] = None):
     """Loss partials and all parameter gradients of one minibatch, from TIME-MAJOR rows (row = t·B + b).
@@ -175,10 +251,16 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
     attn = cfg.entity_attention
     f32 = bool(getattr(fp, 'fp32', False))    # fp32-accurate learner: fp32 activations, bf16x3 MFMA, exact-f32 GEMMs
     adt = torch.float32 if f32 else torch.bfloat16
-    assert not (f32 and attn), 'the fp32 learner has no fused entity-attention kernels (FusedPolicy.use_pipeline)'
     # (x896 / emb come back in the weights' dtype: bf16, or fp32 from the bf16x3 encoder)
     x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs))
-    if attn:
+    attn32 = attn and f32
+    if attn32:
+        # fp32 entity attention as explicit torch ops (bt is NOT folded with b_out in the fp32 images)
+        toff = fp.type_offset_list()
+        E1, attn_saved = _attn_fwd_f32(emb.view(N, U, 128), P, cfg.attention_heads)
+        pool_idx = _attn_pools_f32(E1, toff, x896, bool(cfg.compat_bugs))
+        emb = E1
+    elif attn:
         # 5v5 entity attention (ops/csrc/attn.hip): emb = E0 + b_out here (bias folded into bt)
         toff = fp.type_offset_list()
         E0p = emb.view(N * U, 128)
@@ -199,6 +281,7 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
     gates4 = torch.empty(S, B, H, 4, device=dev)
     spans = chunk_bounds(S, fp.chunks)
     one = len(spans) == 1            # single chunk: outputs are used as produced (no staging copies)
+    assert one or not attn32, "the fp32 entity-attention step runs as one time chunk"
     if not one:
         dxh = torch.empty(S, B, H, device=dev)
         z = torch.empty(N, LDZ, device=dev)
@@ -313,7 +396,15 @@ def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], un
             split()
             split = None
         demb_in = None
-        if attn:
+        if attn32:
+            dE1 = _attn_demb_f32(dtl, z[:, :128], dx896, pool_idx, toff, bool(cfg.compat_bugs))
+            dE0, agr = _attn_bwd_f32(attn_saved, dE1, P, cfg.attention_heads)
+            demb_in = dE0.contiguous()
+            dbt_attn = torch.stack([dE0[:, toff[t]:toff[t + 1]].sum((0, 1)) for t in range(6)])
+            dgam, dbet = agr['entity_attn.ln.weight'], agr['entity_attn.ln.bias']
+            dWqkv, dbqkv = agr['entity_attn.qkv.weight'], agr['entity_attn.qkv.bias']
+            dWout, dbout = agr['entity_attn.out.weight'], agr['entity_attn.out.bias']
+        elif attn:
             # attention block backward over this chunk's rows (unit rows r0·U … r1·U)
             a0, a1 = r0 * U, r1 * U
             dE1 = C.attn_demb(dtl[r0:r1], z[r0:r1], dx896, arg[r0:r1], toff, bool(cfg.compat_bugs))

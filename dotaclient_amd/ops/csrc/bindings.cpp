@@ -333,12 +333,13 @@ std::vector<torch::Tensor> encoder_bwd(torch::Tensor units, torch::Tensor w1, to
   auto db1 = torch::empty({128}, o);
   const size_t wsb = dca_encoder_bwd_workspace(N, U, c, f32w ? 1 : 0);
   auto ws = torch::empty({(int64_t)((wsb + 3) / 4)}, o);
-  const short* dein = nullptr;
+  const void* dein = nullptr;
   if (demb_in && demb_in->defined()) {
-    CHECK_BF16(*demb_in);
-    TORCH_CHECK(!f32w, "encoder_bwd: demb_in is a bf16-variant input");
+    CHECK_DEV(*demb_in); CHECK_CONTIG(*demb_in);
+    // the given ∂emb has the variant's activation dtype: bf16, or fp32 with fp32 weights (bf16x3 variant)
+    TORCH_CHECK(demb_in->scalar_type() == (f32w ? at::kFloat : at::kBFloat16), "encoder_bwd: demb_in dtype");
     TORCH_CHECK(demb_in->numel() == (int64_t)N * U * 128, "demb_in must be (N, U, 128)");
-    dein = ptr<short>(*demb_in);
+    dein = demb_in->data_ptr();
   }
   hip_check(dca_encoder_bwd(ptr<float>(units), ptr<float>(w1), ptr<float>(b1), wtT.data_ptr(), ptr<float>(dtl),
                             ptr<float>(q), (int)q.stride(0), ptr<float>(dx), ptr<unsigned char>(arg), ptr<float>(dwt),

@@ -76,7 +76,8 @@ struct BwdParams {
   Layout L;
   long long blkbase[6];
   int NB;               // 16-row blocks per unit slot = ⌈N/16⌉
-  const short* demb_in; // optional (N, U, 128) bf16: ∂emb given (entity-attention path) — dtl/q/dx/arg unused
+  const void* demb_in;  // optional (N, U, 128) ∂emb given (entity-attention path; bf16, or fp32 in the F32 variant) —
+                        // dtl/q/dx/arg unused
 };
 
 __device__ __forceinline__ void type_job(int wv, int j, int& tau, int& g) {
@@ -440,7 +441,9 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
             bf16x8 h = {0, 0, 0, 0, 0, 0, 0, 0};
-            if (rok) h = *reinterpret_cast<const bf16x8*>(P.demb_in + ((size_t)arow * U + uoff + u) * kD + 32 * s + 8 * kg);
+            if (rok)
+              h = *reinterpret_cast<const bf16x8*>(static_cast<const short*>(P.demb_in) +
+                                                   ((size_t)arow * U + uoff + u) * kD + 32 * s + 8 * kg);
             de[s] = h;
 #pragma unroll
             for (int jj = 0; jj < 8; ++jj) tw[toff(32 * s + 8 * kg + jj, i)] = h[jj];
@@ -727,6 +730,7 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_f32_kernel(BwdParams P) {
     const int arow = row0 + i;
     const bool rok = arow < N;
     const bool eth_dead = P.compat && tau == 5;
+    const bool given = P.demb_in != nullptr;       // wave-uniform
     float* ur = &ust[wv][0];
     float* dr = &dst_[wv][0];
     for (int h = 0; h < 2; ++h) {
@@ -736,20 +740,25 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_f32_kernel(BwdParams P) {
         const int cc = min(kStage, cnt - c0);
         if (h == 0 || cnt > kStage) {
           __builtin_amdgcn_wave_barrier();
-          stage_units(P.units, P.dtl, U, N, row0, uoff + c0, cc, ur, dr, lane);
+          stage_units(P.units, given ? nullptr : P.dtl, U, N, row0, uoff + c0, cc, ur, dr, lane);
           __builtin_amdgcn_wave_barrier();
         }
         for (int uc = 0; uc < cc; ++uc) {
           const int u = c0 + uc;
           const size_t blk = (size_t)(P.blkbase[tau] + (long long)u * P.NB + rb) * (kD * 16);
-          // ---- ∂emb (all 128 columns: the K of this half's ∂basic) = dtl·q + ∂pool at the argmax, split hi / lo
-          const float dtl = dr[i * kDP + uc];
+          // ---- ∂emb (all 128 columns: the K of this half's ∂basic) = dtl·q + ∂pool at the argmax (or given, fp32),
+          // split hi / lo
+          const float dtl = given ? 0.f : dr[i * kDP + uc];
           bf16x8 de[4], del[4];
 #pragma unroll
           for (int s = 0; s < 4; ++s) {
             const int e0 = 32 * s + 8 * kg;
             float v[8];
-            if (rok) {
+            if (rok && given) {
+              const float* gp = static_cast<const float*>(P.demb_in) + ((size_t)arow * U + uoff + u) * kD + e0;
+              const float4 ga = *reinterpret_cast<const float4*>(gp), gb = *reinterpret_cast<const float4*>(gp + 4);
+              v[0] = ga.x; v[1] = ga.y; v[2] = ga.z; v[3] = ga.w; v[4] = gb.x; v[5] = gb.y; v[6] = gb.z; v[7] = gb.w;
+            } else if (rok) {
               const float* qp = P.q + (size_t)arow * P.ldq + e0;
               const float* dp = P.dx + (size_t)arow * 896 + kD + tau * kD + e0;
               const unsigned char* ag = P.arg + ((size_t)arow * 6 + tau) * kD + e0;
@@ -1059,9 +1068,8 @@ extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const
                                       const float* dtl, const float* q, int ldq, const float* dx,
                                       const unsigned char* arg, float* dwt, float* dw1, float* db1, void* ws,
                                       size_t ws_bytes, int N, int U, const int* counts, int compat, hipStream_t st,
-                                      const short* demb_in, int f32) {
+                                      const void* demb_in, int f32) {
   if (ws_bytes < dca_encoder_bwd_workspace(N, U, counts, f32)) return hipErrorInvalidValue;
-  if (f32 && demb_in) return hipErrorInvalidValue;
   DwtJobs J;
   int NB;
   dwt_plan(N, counts, J, NB);

@@ -37,7 +37,7 @@ size_t dca_encoder_bwd_workspace(int N, int U, const int* counts, int f32);
 hipError_t dca_encoder_bwd(const float* units, const float* w1, const float* b1, const void* wtT, const float* dtl,
                            const float* q, int ldq, const float* dx, const unsigned char* arg, float* dwt, float* dw1,
                            float* db1, void* ws, size_t ws_bytes, int N, int U, const int* counts, int compat,
-                           hipStream_t st, const short* demb_in, int f32);
+                           hipStream_t st, const void* demb_in, int f32);
 
 size_t dca_lstm_team_ctl_bytes();
 size_t dca_lstm_team_workspace(int B, int H, int backward, int f32);

@@ -272,7 +272,7 @@ def test_fused_step_deploy_shape_matches_fp32_oracle(gpu_ops, precision):
     assert worst[0][0] < tol, worst[:5]
 
 
-@pytest.mark.parametrize('preset,algo', [('lstm128', 'ppo'), ('compat', 'vpg'), ('lstm512', 'vpg')])
+@pytest.mark.parametrize('preset,algo', [('lstm128', 'ppo'), ('compat', 'vpg'), ('lstm512', 'vpg'), ('5v5', 'ppo')])
 def test_fused_fp32_presets_match_fp64(gpu_ops, preset, algo):
     """fp32 mode on the other presets (lstm128, the reference network in compat mode through the autograd Function
     path, VPG) at the deploy shape B=8, S=1400: the fused learner and the fp32 torch oracle both measured against a
