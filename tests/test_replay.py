@@ -83,3 +83,40 @@ def test_replay_on_hbm_large(gpu_ops):
     r.add(b, version=1)
     s = r.sample(8)
     assert s['units'].is_cuda and torch.equal(s['ret'][:, 0].cpu(), torch.full((8,), 3.0))
+
+
+@pytest.mark.gpu
+def test_replay_200gb_on_hbm_accounting_and_training(gpu_ops):
+    """BASELINE config 5's on-HBM replay at scale: a 200 GB buffer of 1400-step LSTM-512 sequences. The bytes the
+    driver reports as taken match ``nbytes`` (and ``bytes_per_sequence`` × capacity), writes across the ring's wrap
+    point land where expected, and the fused learner trains from it."""
+    from dotaclient_amd.learner.engine import Learner, LossConfig
+    from dotaclient_amd.learner.replay import bytes_per_sequence
+    from dotaclient_amd.models.policy import Policy, get_config
+    S, H, budget = 1400, 512, 200e9
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()                       # earlier tests' cached blocks must not be reused here
+    free0, total = torch.cuda.mem_get_info()
+    alloc0 = torch.cuda.memory_allocated()
+    if free0 < budget + 20e9:
+        pytest.skip(f'needs {budget / 1e9 + 20:.0f} GB free HBM, have {free0 / 1e9:.0f}')
+    cap = HbmReplay.capacity_for_bytes(budget, S, LAYOUT_1V1, H)
+    r = HbmReplay(cap, S, LAYOUT_1V1, H, 'cuda')
+    torch.cuda.synchronize()
+    free1, _ = torch.cuda.mem_get_info()
+    assert 0.995 * budget <= r.nbytes <= budget
+    assert abs(r.nbytes - (cap * bytes_per_sequence(S, LAYOUT_1V1, H) + cap * 8)) < 1e6
+    # the allocator's and the driver's view: the buffer really is resident HBM of that size
+    assert abs((torch.cuda.memory_allocated() - alloc0) - r.nbytes) < 1e-3 * r.nbytes
+    assert free0 - free1 >= 0.99 * r.nbytes, (free0 - free1, r.nbytes)
+    # fill up to the wrap point, then write across it
+    r.cursor = cap - 2
+    b = {k: v.cuda() for k, v in _batch(4, S, 7, hidden=H).items()}
+    r.add(b, version=5)
+    assert r.cursor == 2 and int(r.version[cap - 1]) == 5 and int(r.version[1]) == 5
+    assert torch.equal(r.data['ret'][cap - 2, 0].cpu(), torch.tensor(7.0)) and float(r.data['ret'][1, 0]) == 7.0
+    L = Learner(Policy(get_config('lstm512')), LossConfig(algo='ppo'), device='cuda', backend='fused', dp=False)
+    m = L.train_step_replay(r, 4, recent=4)
+    torch.cuda.synchronize()
+    assert torch.isfinite(m['loss'])
+    del r
