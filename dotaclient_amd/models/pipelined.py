@@ -156,42 +156,40 @@ class WeightImages:
 def _attn_fwd_f32(E0, P, heads: int, eps: float = 1e-5):
     N, U, D = E0.shape
     d = D // heads
-    mu = E0.mean(-1, keepdim=True)
-    xc = E0 - mu
-    rstd = torch.rsqrt((xc * xc).mean(-1, keepdim=True) + eps)
-    xhat = xc * rstd
-    Xn = xhat * P['entity_attn.ln.weight'] + P['entity_attn.ln.bias']
+    Xn, mu, rstd = torch.native_layer_norm(E0, (D,), P['entity_attn.ln.weight'], P['entity_attn.ln.bias'], eps)
     qkv = torch.addmm(P['entity_attn.qkv.bias'], Xn.view(N * U, D), P['entity_attn.qkv.weight'].t())
     q, k, v = qkv.view(N, U, 3, heads, d).permute(2, 0, 3, 1, 4).unbind(0)          # (N, h, U, d)
-    att = torch.softmax(torch.matmul(q, k.transpose(-1, -2)) * (1.0 / float(d) ** 0.5), dim=-1)
+    qs = q * (1.0 / float(d) ** 0.5)                  # scale the (small) queries, not the (N, h, U, U) scores
+    att = torch.softmax(torch.matmul(qs, k.transpose(-1, -2)), dim=-1)
     o = torch.matmul(att, v).transpose(1, 2).reshape(N * U, D)
     E1 = torch.addmm(P['entity_attn.out.bias'], o, P['entity_attn.out.weight'].t()).view(N, U, D) + E0
-    return E1, (xhat, rstd, Xn, q, k, v, att, o)
+    return E1, (E0, mu, rstd, Xn, qs, k, v, att, o)
 
 
 def _attn_bwd_f32(saved, dE1, P, heads: int):
-    xhat, rstd, Xn, q, k, v, att, o = saved
+    """Explicit backward: LayerNorm and softmax through their ATen backward kernels (one pass each), the weight
+    gradients over the N·U unit rows on the split-K TN GEMM (K-outer operands, bias column sums on the way)."""
+    from ..ops.gemm import gemm_tn
+    E0, mu, rstd, Xn, qs, k, v, att, o = saved
     N, U, D = dE1.shape
     d = D // heads
     g = {}
     dE1f = dE1.reshape(N * U, D)
-    g['entity_attn.out.weight'] = dE1f.t() @ o
-    g['entity_attn.out.bias'] = dE1f.sum(0)
+    g['entity_attn.out.bias'] = torch.empty(D, device=dE1.device)
+    g['entity_attn.out.weight'] = gemm_tn(dE1f, o, colsum=g['entity_attn.out.bias'])
     do = (dE1f @ P['entity_attn.out.weight']).view(N, U, heads, d).transpose(1, 2)   # (N, h, U, d)
     dv = torch.matmul(att.transpose(-1, -2), do)
     dp = torch.matmul(do, v.transpose(-1, -2))
-    ds = att * (dp - (dp * att).sum(-1, keepdim=True)) * (1.0 / float(d) ** 0.5)
-    dq = torch.matmul(ds, k)
-    dk = torch.matmul(ds.transpose(-1, -2), q)
+    ds = torch._softmax_backward_data(dp, att, -1, torch.float32)
+    dq = torch.matmul(ds, k) * (1.0 / float(d) ** 0.5)
+    dk = torch.matmul(ds.transpose(-1, -2), qs)
     dqkv = torch.stack([dq, dk, dv], 0).permute(1, 3, 0, 2, 4).reshape(N * U, 3 * D)
-    g['entity_attn.qkv.weight'] = dqkv.t() @ Xn.view(N * U, D)
-    g['entity_attn.qkv.bias'] = dqkv.sum(0)
+    g['entity_attn.qkv.bias'] = torch.empty(3 * D, device=dE1.device)
+    g['entity_attn.qkv.weight'] = gemm_tn(dqkv, Xn.view(N * U, D), colsum=g['entity_attn.qkv.bias'])
     dXn = (dqkv @ P['entity_attn.qkv.weight']).view(N, U, D)
-    g['entity_attn.ln.weight'] = (dXn * xhat).sum((0, 1))
-    g['entity_attn.ln.bias'] = dXn.sum((0, 1))
-    dxh = dXn * P['entity_attn.ln.weight']
-    dE0 = dE1 + rstd * (dxh - dxh.mean(-1, keepdim=True) - xhat * (dxh * xhat).mean(-1, keepdim=True))
-    return dE0, g
+    dE0_ln, g['entity_attn.ln.weight'], g['entity_attn.ln.bias'] = torch.ops.aten.native_layer_norm_backward(
+        dXn, E0, (D,), mu, rstd, P['entity_attn.ln.weight'], P['entity_attn.ln.bias'], [True, True, True])
+    return dE1 + dE0_ln, g
 
 
 def _attn_pools_f32(E1, toff, x896, compat: bool):
