@@ -239,12 +239,14 @@ int featurize_one(const World& w, int player_id, int team_id, const int* counts,
   env[0] = (float)((double)w.dota_time / 1200.0);
   env[1] = (float)std::sin((double)w.dota_time * (2.0 * 3.14159265358979323846) / 60.0);
   env[2] = team_id == 3 ? -0.2f : 0.2f;
-  std::vector<const Unit*> ah, eh, anh, enh, ac, ec, at, et;
+  // per-thread scratch lists (capacity reused across calls: no allocation per observation)
+  thread_local std::vector<const Unit*> ah, eh, anhc, enhc, ac, ec, at, et, s5;
+  ah.clear(); eh.clear(); anhc.clear(); enhc.clear(); ac.clear(); ec.clear(); at.clear(); et.clear();
   for (const Unit& u : w.units) {
     const bool ally = u.team_id == hero->team_id;
     switch (u.unit_type) {
       case HERO: (ally ? ah : eh).push_back(&u); break;
-      case CREEP_HERO: (ally ? anh : enh).push_back(&u); break;
+      case CREEP_HERO: (ally ? anhc : enhc).push_back(&u); break;   // non-hero creeps first, lane creeps after
       case LANE_CREEP: (ally ? ac : ec).push_back(&u); break;
       case TOWER:
         if (ends_with(u.name, "1_mid")) (ally ? at : et).push_back(&u);
@@ -252,14 +254,14 @@ int featurize_one(const World& w, int player_id, int team_id, const int* counts,
       default: break;
     }
   }
-  std::vector<const Unit*> anhc(anh), enhc(enh);
   anhc.insert(anhc.end(), ac.begin(), ac.end());
   enhc.insert(enhc.end(), ec.begin(), ec.end());
   if (counts[0] > 1) {   // 5v5: self first, then teammates
-    std::vector<const Unit*> s{hero};
+    s5.clear();
+    s5.push_back(hero);
     for (const Unit* u : ah)
-      if (u->player_id != player_id) s.push_back(u);
-    ah.swap(s);
+      if (u->player_id != player_id) s5.push_back(u);
+    ah.swap(s5);
   }
   const std::vector<const Unit*>* lists[6] = {&ah, &eh, &anhc, &enhc, &at, &et};
   int off = 0;

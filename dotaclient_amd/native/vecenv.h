@@ -173,6 +173,7 @@ struct Pick {
 class SimGame {
  public:
   std::vector<SUnit> units;       // python dict insertion order
+  std::vector<SUnit> keep_;       // step() scratch (reused capacity)
   std::vector<PStats> players;    // dict keyed by player_id, insertion order
   PyRandom rng;
   double dt = 0.5, dota_time = -10.0;
@@ -281,13 +282,17 @@ class SimGame {
   }
 
   // nearest alive non-invulnerable enemy of `team` within max_range (python: last candidate wins ties)
+  // (the squared-distance pre-test only skips units whose correctly rounded sqrt must exceed bd — the kept
+  // comparison is the python one, so the choice is bit-identical; it saves the sqrt of every far unit)
   SUnit* nearest(const SUnit& u, int team, double max_range, bool non_hero_only) {
     SUnit* best = nullptr;
     double bd = max_range;
     for (SUnit& v : units) {
       if (!v.alive || v.team == team || v.invulnerable) continue;
       if (non_hero_only && v.unit_type == HERO) continue;
-      const double d = dist(u, v);
+      const double dx = u.x - v.x, dy = u.y - v.y, d2 = dx * dx + dy * dy;
+      if (d2 > bd * bd * (1.0 + 1e-14)) continue;
+      const double d = std::sqrt(d2);
       if (d <= bd) { best = &v; bd = d; }
     }
     return best;
@@ -475,11 +480,11 @@ class SimGame {
       }
     }
     // creeps that died before this step are removed; the ones that died in it linger one observation
-    std::vector<SUnit> keep;
-    keep.reserve(units.size());
+    keep_.clear();
+    keep_.reserve(units.size());
     for (SUnit& u : units)
-      if (!(!u.alive && u.unit_type == LANE_CREEP && u.respawn_at == -1.0)) keep.push_back(std::move(u));
-    units.swap(keep);
+      if (!(!u.alive && u.unit_type == LANE_CREEP && u.respawn_at == -1.0)) keep_.push_back(std::move(u));
+    units.swap(keep_);
     for (SUnit& u : units)
       if (!u.alive && u.unit_type == LANE_CREEP) u.respawn_at = -1.0;
     for (const PStats& p : players)
@@ -491,15 +496,20 @@ class SimGame {
   // CMsgBotWorldState(team) as the featurizer sees it after the protobuf round trip
   void world(int team, World& w) const {
     w.dota_time = (float)dota_time;
-    w.units.clear();
+    size_t k = 0;                   // overwrite w's units in place: their attack_casters keep their capacity
     for (const SUnit& u : units) {
       if (fog && u.team != team && u.unit_type != TOWER) {
         bool seen = false;
-        for (const SUnit& a : units)
-          if (a.team == team && a.alive && hyp(a.x - u.x, a.y - u.y) <= kVision) { seen = true; break; }
+        for (const SUnit& a : units) {
+          if (a.team != team || !a.alive) continue;
+          const double dx = a.x - u.x, dy = a.y - u.y, d2 = dx * dx + dy * dy;
+          if (d2 > kVision * kVision * (1.0 + 1e-14)) continue;       // sqrt(d2) > kVision for sure
+          if (std::sqrt(d2) <= kVision) { seen = true; break; }
+        }
         if (!seen) continue;
       }
-      Unit m;
+      if (k == w.units.size()) w.units.emplace_back();
+      Unit& m = w.units[k++];
       m.handle = (uint32_t)u.handle;
       m.unit_type = u.unit_type;
       m.name = u.kind == K_TOWER1 ? std::string_view("tower1_mid") : (u.kind == K_TOWER2 ? std::string_view("tower2_mid")
@@ -518,9 +528,10 @@ class SimGame {
       m.anim = u.unit_type == TOWER ? (u.target ? 1503 : 1500) : 0;
       m.invuln = u.invulnerable;
       m.attack_immune = false;
+      m.attack_casters.clear();
       for (int c : u.projectiles) m.attack_casters.push_back((uint32_t)c);
-      w.units.push_back(std::move(m));
     }
+    w.units.resize(k);
   }
 };
 
@@ -765,6 +776,7 @@ struct VGame {
   uint64_t serial = 0;
   std::vector<SimGame::Order> orders;
   double last_reward_sum[2] = {0, 0};   // per-team Σ of this step's shaped rewards (zero-sum ``enemy`` term)
+  World world_buf[2];
 };
 
 class VecEnv {
@@ -919,7 +931,7 @@ class VecEnv {
       return;
     }
     g.obs_time = (float)g.sim.dota_time;
-    World w[2];
+    World* w = g.world_buf;        // per-game scratch: the unit vectors keep their capacity across steps
     g.sim.world(TEAM_R, w[0]);
     g.sim.world(TEAM_D, w[1]);
     double reward_sum[2] = {0, 0};
