@@ -271,15 +271,19 @@ class VecActor:
 
 
 def measure_vec_actor(policy, device='cuda', n_games: int = 2048, steps: int = 100, warmup: int = 10,
-                      threads: int = 8, groups: int = 2, hidden_stride: int = 256, rollout_size: int = 64) -> Dict[str, float]:
+                      threads: int = 8, groups: int = 2, hidden_stride: int = 1400, rollout_size: int = 9999,
+                      max_dota_time: float = 600.0) -> Dict[str, float]:
     """Whole-runtime actor throughput: player-steps/s of :class:`VecActor` self-play (engine + featurize + reward +
-    GPU policy + trajectory recording + rollout encoding), rollouts counted (published into a sink)."""
+    GPU policy + trajectory recording + rollout encoding), rollouts counted (published into a sink). Deploy shape
+    (params.libsonnet:16-19): whole-game rollouts (``rollout_size`` 9999) of 600 s games, with staggered first
+    games so the measured window sees the steady-state rate of finished games (and their DCX1 encoding)."""
     from .weights import WeightStore
     ws = WeightStore(policy.config, device='cpu')
     ws.add(0, {k: v.detach().cpu() for k, v in policy.state_dict().items()})
     sink = []
     va = VecActor(ws, n_games, lambda b: sink.append(len(b)), device=device, seed=1, threads=threads,
-                  groups=groups, hidden_stride=hidden_stride, rollout_size=rollout_size)
+                  groups=groups, hidden_stride=hidden_stride, rollout_size=rollout_size,
+                  max_dota_time=max_dota_time, stagger=True)
     sync = (lambda: torch.cuda.synchronize(va.device)) if va.device.type == 'cuda' else (lambda: None)
     for _ in range(warmup):
         va.step()
@@ -293,4 +297,5 @@ def measure_vec_actor(policy, device='cuda', n_games: int = 2048, steps: int = 1
     n = va.steps_taken - s0
     return {'steps_per_s': n / dt, 'ms_per_step': dt / steps * 1e3, 'games': n_games,
             'player_steps': n, 'rollouts_per_s': (va.rollouts_sent - r0) / dt,
-            'rollout_mb_per_s': sum(sink[k0:]) / dt / 1e6, 'threads': threads, 'groups': groups}
+            'rollout_mb_per_s': sum(sink[k0:]) / dt / 1e6, 'threads': threads, 'groups': groups,
+            'rollout_size': rollout_size}

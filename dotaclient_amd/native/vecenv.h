@@ -585,18 +585,31 @@ inline void shaped_reward(const RewardView& a, const RewardView& b, double* r) {
 // ============================================================================================================
 // DCX1 encoding (transport/codec.py encode): JSON header + raw little-endian arrays + zlib CRC-32 trailer
 // ============================================================================================================
+// slice-by-8 (8 bytes per step through 8 derived tables, ≈4× the byte-wise loop): a whole-game rollout is ≈2 MB
 inline uint32_t crc32_zlib(const uint8_t* p, size_t n, uint32_t crc = 0) {
-  static uint32_t table[256];
+  static uint32_t T[8][256];
   static std::once_flag once;
   std::call_once(once, [] {
     for (uint32_t i = 0; i < 256; ++i) {
       uint32_t c = i;
       for (int k = 0; k < 8; ++k) c = (c & 1) ? 0xEDB88320U ^ (c >> 1) : c >> 1;
-      table[i] = c;
+      T[0][i] = c;
     }
+    for (uint32_t i = 0; i < 256; ++i)
+      for (int t = 1; t < 8; ++t) T[t][i] = (T[t - 1][i] >> 8) ^ T[0][T[t - 1][i] & 0xff];
   });
   crc = ~crc;
-  for (size_t i = 0; i < n; ++i) crc = table[(crc ^ p[i]) & 0xff] ^ (crc >> 8);
+  while (n >= 8) {
+    uint32_t lo, hi;
+    std::memcpy(&lo, p, 4);
+    std::memcpy(&hi, p + 4, 4);
+    lo ^= crc;
+    crc = T[7][lo & 0xff] ^ T[6][(lo >> 8) & 0xff] ^ T[5][(lo >> 16) & 0xff] ^ T[4][lo >> 24] ^
+          T[3][hi & 0xff] ^ T[2][(hi >> 8) & 0xff] ^ T[1][(hi >> 16) & 0xff] ^ T[0][hi >> 24];
+    p += 8;
+    n -= 8;
+  }
+  while (n--) crc = T[0][(crc ^ *p++) & 0xff] ^ (crc >> 8);
   return ~crc;
 }
 
