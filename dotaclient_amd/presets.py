@@ -64,7 +64,7 @@ PRESETS: Dict[str, RunPreset] = {p.name: p for p in [
                          max_dota_time=600),
               bench=dict(model='5v5', batch_size=8, seq_len=1400, precision='fp32'),
               launch=dict(model_preset='5v5', actors=8, games_per_actor=256, actor_device='cuda', optimizers=8)),
-    RunPreset('league-replay', 'Self-play league, fp8 MFMA policy GEMMs + 288 GB on-HBM replay buffer', 1,
+    RunPreset('league-replay', 'Self-play league (PFSP opponents) + 200 GB on-HBM replay buffer', 1,
               optimizer=dict(model_preset='lstm512', precision='fp32', replay_gb=200.0, **_DEPLOY),
               agent=dict(model_preset='lstm512', device='cuda', games=1024, runtime='vec', rollout_size=9999,
                          max_dota_time=600, league='pfsp', use_latest_weights_prob=0.8),
