@@ -60,7 +60,7 @@ struct BwdParams {
   const float* units;
   const float* w1;
   const float* b1;
-  const void* wtT;      // (6, 128, 128) W_τᵀ (in, out): bf16, or fp32 in the F32 variant
+  const void* wtT;      // (6, 128, 128) bf16 W_τᵀ (in, out)
   const float* dtl;     // (N, U) ∂L/∂pointer-logit
   const float* q;       // pointer query, row stride ldq
   int ldq;
@@ -68,15 +68,13 @@ struct BwdParams {
   const unsigned char* arg;
   short* demb;          // K-blocked bf16 (see kBlk): block (τ, u, 16-row block rb) at blkbase[τ] + u·NB + rb
   short* basic;         // same layout
-  short* demb_lo;       // F32 only: lo bf16 halves of ∂emb / basic (value = hi + lo), same layout
-  short* basic_lo;
   float* w1part;        // (gridDim.y·gridDim.x, 128·10 + 128) f32 per-workgroup ∂W1 ‖ ∂b1 partials
   int N;
   int compat;
   Layout L;
   long long blkbase[6];
   int NB;               // 16-row blocks per unit slot = ⌈N/16⌉
-  const void* demb_in;  // optional (N, U, 128) ∂emb given (entity-attention path; bf16, or fp32 in the F32 variant) —
+  const void* demb_in;  // optional (N, U, 128) bf16 ∂emb given (entity-attention path) —
                         // dtl/q/dx/arg unused
 };
 
@@ -95,6 +93,17 @@ __device__ __forceinline__ void load_bfrags(const short* __restrict__ m, bf16x8 
 #pragma unroll
     for (int s = 0; s < 4; ++s)
       bf[n][s] = *reinterpret_cast<const bf16x8*>(m + (size_t)(16 * n + j) * kD + 32 * s + 8 * kg);
+}
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// buffer resource over [p, p + bytes) from wave-uniform values (no waterfall loops around the buffer loads)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, int bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0,
+                                           __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
 __device__ __forceinline__ short bf_lo(float v) { return dca::f2bf(v - dca::bf2f(dca::f2bf(v))); }
@@ -686,214 +695,282 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_f32_kernel(FwdParams P) {
   }
 }
 
-// half of a K-blocked tile image (columns 64h … 64h+63 = chunks 128h … 128h+127)
-__device__ __forceinline__ void store_tile_half(const short* tw, short* dst, int h, int lane) {
+// F32 backward, fused ∂W_τ. The bf16 path writes ∂emb and basic as K-blocked images for a separate GEMM; at bf16x3
+// that is four bf16 images (≈460 MB at the 1v1 learner shape) written and read back. Here a workgroup of 8 waves
+// owns a contiguous range of (16-row group, unit) items of ONE type τ and keeps ∂W_τ in registers across the range:
+//   * wave w builds e-tile w of the item's ∂emb (C layout, fp32 → hi / lo bf16) into a double-buffered transposed
+//     LDS image (tile_put layout), one item ahead, between its MFMAs of the current item; one LDS-only barrier per
+//     item;
+//   * wave w owns basic columns j ∈ tile w: layer 1 (recomputed), ∂basic = ∂emb·W_τ[:, j] (bf16x3, A fragments
+//     by ds_read_b64_tr_b16), ReLU', ∂W1 rows j, and ∂W_τᵀ[j][e] += basicᵀ·∂emb on 16x16x16 MFMAs whose A operand
+//     is the C-layout basic tile and whose B operand is the C-layout ∂emb tile read back as written;
+//   * an item's unit features and dtl (identical for all 8 waves) are staged once into LDS by LDS-DMA two items
+//     ahead; the per-row q / ∂pool / argmax of the wave's e-tile are raw buffer loads (hardware bounds check: rows
+//     past N read 0), issued one item ahead and only when the row group changes.
+// 2 waves per SIMD (≤ 256 VGPRs) overlap one wave's loads / VALU with the other's MFMAs.
+// Each workgroup writes one tile-linear 128×128 ∂W_τ partial and one ∂W1‖∂b1 partial; fixed-order reduces follow.
+struct FbParams {
+  const float* units;
+  const float* w1;
+  const float* b1;
+  const float* wtT;      // (6, 128, 128) fp32 W_τᵀ (in, out)
+  const float* dtl;
+  const float* q;
+  int ldq;
+  const float* dx;
+  const unsigned char* arg;
+  const float* demb_in;  // optional fp32 (N, U, 128)
+  float* w1part;         // (jobs, kW1)
+  float* dwtpart;        // (jobs, 128·128) tile-linear
+  int N;
+  int compat;
+  int items;             // items per job
+  Layout L;
+  int jbase[7];
+};
+
+struct FbBuild {   // per-row-group data the ∂emb build needs (e = 16·wv + i, rows 4kg + r); GIVEN: the item's ∂emb
+  float q[4];      // q[row][e]                              (GIVEN: ∂emb[row][u][e])
+  float ds[4];     // ∂pool[row][e] routed to this type (compat: + the eth slot for enh; none for a dead eth)
+  unsigned ab[4];  // argmax byte of each row (unpacked: packing would wait for the loads where they are issued)
+};
+
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0));
+}
+
+struct FbRsrc {
+  __amdgpu_buffer_rsrc_t q, x, a, g;
+};
+
+// Build loads of item k (raw buffer loads: 32-bit offsets, rows past N read 0). rg: item k starts a new row group —
+// q / ∂pool / argmax are per row, shared by the type's units, so they are re-read only then.
+template <bool GIVEN, bool COMPAT>
+__device__ __forceinline__ void fb_load_build(FbBuild& p, const FbRsrc& R, int ldq, int k, bool rg, int cnt, int uoff,
+                                              int U, int tau, int wv, int i, int kg) {
+  const int rb = k / cnt, u = k - rb * cnt, row0 = 16 * rb;
+  const int e = 16 * wv + i;
+  if constexpr (GIVEN) {
 #pragma unroll
-  for (int q = 2 * h; q < 2 * h + 2; ++q) {
-    const int c = lane + 64 * q;
-    *reinterpret_cast<bf16x8*>(dst + c * 8) = *reinterpret_cast<const bf16x8*>(tw + toff(c >> 1, 8 * (c & 1)));
+    for (int r = 0; r < 4; ++r) p.q[r] = bload(R.g, (((row0 + 4 * kg + r) * U + uoff + u) * kD + e) * 4);
+  } else if (rg) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int row = row0 + 4 * kg + r;
+      p.q[r] = bload(R.q, (row * ldq + e) * 4);
+      const int xo = (row * 896 + kD + tau * kD + e) * 4;
+      p.ds[r] = tau == 5 && COMPAT ? 0.f : bload(R.x, xo);
+      if constexpr (COMPAT) p.ds[r] += tau == 3 ? bload(R.x, xo + 2 * kD * 4) : 0.f;
+      p.ab[r] = __builtin_amdgcn_raw_buffer_load_b8(R.a, (row * 6 + tau) * kD + e, 0, 0);
+    }
   }
 }
 
-__global__ __launch_bounds__(256, 1) void encoder_bwd_f32_kernel(BwdParams P) {
-  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-  const int rbase = blockIdx.x * kRows;
+// Per-item staging (LDS, 3 slots): units[row0 .. row0+15][u][0..9] (160 floats) ‖ dtl[row0 .. row0+15][u] (16) —
+// the same for all 8 waves, so it is moved once by LDS-DMA (waves 0-2, one global_load_lds_dword each; rows past N
+// read row N-1, whose ∂emb is zero) instead of being loaded by every wave into registers.
+constexpr int kStg = 192;
+__device__ __forceinline__ void fb_stage(const FbParams& P, float* slot, int k, int cnt, int uoff, int wv, int lane) {
+  if (wv >= 3) return;
+  typedef __attribute__((address_space(1))) void gvoid;
+  typedef __attribute__((address_space(3))) void lvoid;
   const int U = P.L.U, N = P.N;
+  const int rb = k / cnt, u = k - rb * cnt, row0 = 16 * rb;
+  const int idx = 64 * wv + lane;
+  const float* src;
+  if (idx < 16 * kF) {
+    const int row = min(row0 + idx / kF, N - 1);
+    src = P.units + ((size_t)row * U + uoff + u) * kF + idx % kF;
+  } else {
+    const int row = min(row0 + min(idx - 16 * kF, 15), N - 1);
+    src = P.dtl ? P.dtl + (size_t)row * U + uoff + u : P.units;
+  }
+  __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(slot + 64 * wv), 4, 0, 0);
+}
+
+// all of this wave's loads (incl. its LDS-DMA) done, then the workgroup barrier
+__device__ __forceinline__ void fb_sync() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// ∂emb e-tile wv of item k (C layout) → hi / lo image
+template <bool GIVEN>
+__device__ __forceinline__ void fb_build(const FbBuild& b, const float* slot, int u, short* ih, short* il, int wv,
+                                         int lane) {
+  const int kg = lane >> 4;
+  f32x4 v;
+  if constexpr (GIVEN) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = b.q[r];
+  } else {
+    const f32x4 d4 = *reinterpret_cast<const f32x4*>(slot + 16 * kF + 4 * kg);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = d4[r] * b.q[r] + (b.ab[r] == (unsigned)u ? b.ds[r] : 0.f);
+  }
+  tile_put(ih, wv, v, lane);
+  tile_put_lo(il, wv, v, lane);
+}
+
+template <bool GIVEN, bool COMPAT>
+__global__ __launch_bounds__(512, 1) void encoder_bwd_f32_fused_kernel(FbParams P) {
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int i = lane & 15, kg = lane >> 4;
-  __shared__ __attribute__((aligned(16))) short tsc[4][kTile];
-  __shared__ __attribute__((aligned(16))) float ust[4][16 * kUP];
-  __shared__ float dst_[4][16 * kDP];
-  __shared__ float wred[kW1];
-  short* tw = &tsc[wv][0];
-
-  bf16x8 wb[8];
-  load_w1_split(P.w1, P.b1, wb, lane);
-  f32x4 dw1acc[8];
-  float db1acc[8];
+  const int job = blockIdx.x;
+  int tau = 0;
 #pragma unroll
-  for (int n = 0; n < 8; ++n) {
-    dw1acc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
-    db1acc[n] = 0.f;
+  for (int t = 1; t < 6; ++t) tau += job >= P.jbase[t] ? 1 : 0;
+  const int cnt = P.L.cnt[tau], uoff = P.L.off[tau], N = P.N, U = P.L.U;
+  const int NB = (N + 15) >> 4;
+  const int k0 = (job - P.jbase[tau]) * P.items, k1 = min(k0 + P.items, cnt * NB);
+  __shared__ __attribute__((aligned(16))) short img[2][2][kImg];   // [buffer][hi, lo]
+  __shared__ __attribute__((aligned(16))) float stg[3][kStg];
+  FbRsrc R;
+  if constexpr (GIVEN) {
+    R.g = uniform_rsrc(P.demb_in, N * U * kD * 4);
+  } else {
+    R.q = uniform_rsrc(P.q, N * P.ldq * 4);
+    R.x = uniform_rsrc(P.dx, N * 896 * 4);
+    R.a = uniform_rsrc(P.arg, N * 6 * kD);
   }
-  for (int e = tid; e < kW1; e += 256) wred[e] = 0.f;
 
-  // job split over blockIdx.y (gridDim.y == 3: one type job per wave per workgroup; 1: all three)
-  const int jlo = gridDim.y == 3 ? (int)blockIdx.y : 0, jhi = gridDim.y == 3 ? jlo + 1 : 3;
-  for (int j = jlo; j < jhi; ++j) {
-    int tau, g;
-    type_job(wv, j, tau, g);
-    const int cnt = P.L.cnt[tau], uoff = P.L.off[tau];
-    if (cnt == 0) continue;
-    const int row0 = rbase + 16 * g;
-    if (row0 >= N) continue;
-    const int rb = row0 / 16;
-    const int arow = row0 + i;
-    const bool rok = arow < N;
-    const bool eth_dead = P.compat && tau == 5;
-    const bool given = P.demb_in != nullptr;       // wave-uniform
-    float* ur = &ust[wv][0];
-    float* dr = &dst_[wv][0];
-    for (int h = 0; h < 2; ++h) {
-      bf16x8 wf[kHalfN][4], wfl[kHalfN][4];   // B[k=e][n=j] = W_τ[e][j] for basic columns j of this half
-      load_bfrags_split_half(static_cast<const float*>(P.wtT) + (size_t)tau * kD * kD, h, wf, wfl, lane);
-      for (int c0 = 0; c0 < cnt; c0 += kStage) {
-        const int cc = min(kStage, cnt - c0);
-        if (h == 0 || cnt > kStage) {
-          __builtin_amdgcn_wave_barrier();
-          stage_units(P.units, given ? nullptr : P.dtl, U, N, row0, uoff + c0, cc, ur, dr, lane);
-          __builtin_amdgcn_wave_barrier();
-        }
-        for (int uc = 0; uc < cc; ++uc) {
-          const int u = c0 + uc;
-          const size_t blk = (size_t)(P.blkbase[tau] + (long long)u * P.NB + rb) * (kD * 16);
-          // ---- ∂emb (all 128 columns: the K of this half's ∂basic) = dtl·q + ∂pool at the argmax (or given, fp32),
-          // split hi / lo
-          const float dtl = given ? 0.f : dr[i * kDP + uc];
-          bf16x8 de[4], del[4];
+  // ---- weights of this wave's basic-column tile: B[k = e][n = j] = W_τ[e][j] (bf16x3 halves) and the split W1 row
+  const int col = 16 * wv + i;
+  bf16x8 wf[4], wfl[4], wb;
 #pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            const int e0 = 32 * s + 8 * kg;
-            float v[8];
-            if (rok && given) {
-              const float* gp = static_cast<const float*>(P.demb_in) + ((size_t)arow * U + uoff + u) * kD + e0;
-              const float4 ga = *reinterpret_cast<const float4*>(gp), gb = *reinterpret_cast<const float4*>(gp + 4);
-              v[0] = ga.x; v[1] = ga.y; v[2] = ga.z; v[3] = ga.w; v[4] = gb.x; v[5] = gb.y; v[6] = gb.z; v[7] = gb.w;
-            } else if (rok) {
-              const float* qp = P.q + (size_t)arow * P.ldq + e0;
-              const float* dp = P.dx + (size_t)arow * 896 + kD + tau * kD + e0;
-              const unsigned char* ag = P.arg + ((size_t)arow * 6 + tau) * kD + e0;
-              const float4 qa = *reinterpret_cast<const float4*>(qp), qb = *reinterpret_cast<const float4*>(qp + 4);
-              const float4 da = *reinterpret_cast<const float4*>(dp), db = *reinterpret_cast<const float4*>(dp + 4);
-              const uint2 a8 = *reinterpret_cast<const uint2*>(ag);
-              const float qv[8] = {qa.x, qa.y, qa.z, qa.w, qb.x, qb.y, qb.z, qb.w};
-              const float dv[8] = {da.x, da.y, da.z, da.w, db.x, db.y, db.z, db.w};
+  for (int s = 0; s < 4; ++s) {
+    const float* p = P.wtT + ((size_t)tau * kD + col) * kD + 32 * s + 8 * kg;
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
-              for (int jj = 0; jj < 8; ++jj) {
-                const unsigned ab = ((jj < 4 ? a8.x : a8.y) >> (8 * (jj & 3))) & 0xffu;
-                v[jj] = dtl * qv[jj] + ((!eth_dead && ab == (unsigned)u) ? dv[jj] : 0.f);
-              }
-              if (P.compat && tau == 3) {   // eth pool = enh pool: its gradient lands on enh argmax units
-                const float* dp5 = P.dx + (size_t)arow * 896 + kD + 5 * kD + e0;
-#pragma unroll
-                for (int jj = 0; jj < 8; ++jj) {
-                  const unsigned ab = ((jj < 4 ? a8.x : a8.y) >> (8 * (jj & 3))) & 0xffu;
-                  v[jj] += (ab == (unsigned)u) ? dp5[jj] : 0.f;
-                }
-              }
-            } else {
-#pragma unroll
-              for (int jj = 0; jj < 8; ++jj) v[jj] = 0.f;
-            }
-#pragma unroll
-            for (int jj = 0; jj < 8; ++jj) {
-              de[s][jj] = dca::f2bf(v[jj]);
-              del[s][jj] = dca::f2bf(v[jj] - dca::bf2f(de[s][jj]));
-            }
-          }
-          if (h == 0) {   // ∂emb hi / lo images (whole tile) for the ∂W_τ GEMM
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-              for (int jj = 0; jj < 8; ++jj) tw[toff(32 * s + 8 * kg + jj, i)] = de[s][jj];
-            __builtin_amdgcn_wave_barrier();
-            store_tile(tw, P.demb + blk, lane);
-            __builtin_amdgcn_wave_barrier();
-#pragma unroll
-            for (int s = 0; s < 4; ++s)
-#pragma unroll
-              for (int jj = 0; jj < 8; ++jj) tw[toff(32 * s + 8 * kg + jj, i)] = del[s][jj];
-            __builtin_amdgcn_wave_barrier();
-            store_tile(tw, P.demb_lo + blk, lane);
-            __builtin_amdgcn_wave_barrier();
-          }
-          // ---- layer 1 of this half's columns (recomputed, C layout) and ∂basic = ∂emb · W_τ, ReLU'
-          f32x4 bas[kHalfN], dbp[kHalfN];
-          {
-            const bf16x8 a = l1_afrag(ur, uc, lane);
-#pragma unroll
-            for (int nn = 0; nn < kHalfN; ++nn) {
-              const f32x4 l1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, wb[kHalfN * h + nn],
-                                                                       f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-#pragma unroll
-              for (int r = 0; r < 4; ++r) bas[nn][r] = fmaxf(l1[r], 0.f);
-            }
-          }
-#pragma unroll
-          for (int nn = 0; nn < kHalfN; ++nn) {
-            f32x4 c = mfma3_k128(de, del, wf[nn], wfl[nn]);
-#pragma unroll
-            for (int r = 0; r < 4; ++r) c[r] = bas[nn][r] > 0.f ? c[r] : 0.f;
-            dbp[nn] = c;
-          }
-          // ---- ∂W1 rows of this half += ∂basicᵀ · units (16x16x16, bf16x3)
-          bf16x4 ub, ubl;
-          {
-            const int kk = lane & 15;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float x = kk < kF ? ur[(4 * kg + r) * kUP + uc * kF + kk] : 0.f;
-              ub[r] = dca::f2bf(x);
-              ubl[r] = dca::f2bf(x - dca::bf2f(ub[r]));
-            }
-          }
-#pragma unroll
-          for (int nn = 0; nn < kHalfN; ++nn) {
-            const int n = kHalfN * h + nn;
-            bf16x4 a, al;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              a[r] = dca::f2bf(dbp[nn][r]);
-              al[r] = dca::f2bf(dbp[nn][r] - dca::bf2f(a[r]));
-              db1acc[n] += dbp[nn][r];
-            }
-            dw1acc[n] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, ub, dw1acc[n], 0, 0, 0);
-            dw1acc[n] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, ubl, dw1acc[n], 0, 0, 0);
-            dw1acc[n] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, ub, dw1acc[n], 0, 0, 0);
-          }
-          // ---- this half of the basic tile → hi / lo K-blocked images
-#pragma unroll
-          for (int nn = 0; nn < kHalfN; ++nn) {
-            bf16x4 v4;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v4[r] = dca::f2bf(bas[nn][r]);
-            *reinterpret_cast<bf16x4*>(&tw[toff(16 * (kHalfN * h + nn) + i, 4 * kg)]) = v4;
-          }
-          __builtin_amdgcn_wave_barrier();
-          store_tile_half(tw, P.basic + blk, h, lane);
-          __builtin_amdgcn_wave_barrier();
-#pragma unroll
-          for (int nn = 0; nn < kHalfN; ++nn) {
-            bf16x4 v4;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v4[r] = bf_lo(bas[nn][r]);
-            *reinterpret_cast<bf16x4*>(&tw[toff(16 * (kHalfN * h + nn) + i, 4 * kg)]) = v4;
-          }
-          __builtin_amdgcn_wave_barrier();
-          store_tile_half(tw, P.basic_lo + blk, h, lane);
-          __builtin_amdgcn_wave_barrier();
-        }
-      }
+    for (int jj = 0; jj < 8; ++jj) {
+      wf[s][jj] = dca::f2bf(v[jj]);
+      wfl[s][jj] = dca::f2bf(v[jj] - dca::bf2f(wf[s][jj]));
     }
   }
-  for (int w = 0; w < 4; ++w) {
-    __syncthreads();
-    if (wv == w) {
 #pragma unroll
-      for (int n = 0; n < 8; ++n) {
-        const int k = lane & 15;
-        if (k < kF) {
-#pragma unroll
-          for (int r = 0; r < 4; ++r) wred[(16 * n + 4 * kg + r) * kF + k] += dw1acc[n][r];
-        }
-        float s = db1acc[n];
-        s += __shfl_xor(s, 16, 64);
-        s += __shfl_xor(s, 32, 64);
-        if (kg == 0) wred[kD * kF + 16 * n + i] += s;
-      }
-    }
+  for (int jj = 0; jj < 8; ++jj) {
+    const int slot = 8 * kg + jj, f = l1_feat(slot);
+    const float w = f >= 0 ? P.w1[col * kF + f] : P.b1[col];
+    const short hi = dca::f2bf(w);
+    const short lo = dca::f2bf(w - dca::bf2f(hi));
+    wb[jj] = (slot == 31 || (f >= 0 && l1_wlo(slot))) ? lo : hi;
   }
+  f32x4 acc[8], dw1acc = {0.f, 0.f, 0.f, 0.f};
+  float db1acc = 0.f;
+#pragma unroll
+  for (int et = 0; et < 8; ++et) acc[et] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // Software pipeline, per item k: [sync: image k built, staging of k+1 landed] → stage k+2 → item k's MFMAs with
+  // the ∂emb of k+1 built in between (its row data were loaded one item earlier) → build loads of k+2.
+  FbBuild bn;
+  const int kl = max(k1 - 1, 0);
+  fb_stage(P, stg[k0 % 3], min(k0, kl), cnt, uoff, wv, lane);
+  fb_stage(P, stg[(k0 + 1) % 3], min(k0 + 1, kl), cnt, uoff, wv, lane);
+  fb_load_build<GIVEN, COMPAT>(bn, R, P.ldq, min(k0, kl), true, cnt, uoff, U, tau, wv, i, kg);
+  fb_sync();
+  fb_build<GIVEN>(bn, stg[k0 % 3], k0 % cnt, &img[0][0][0], &img[0][1][0], wv, lane);
+  fb_load_build<GIVEN, COMPAT>(bn, R, P.ldq, min(k0 + 1, kl), min(k0 + 1, kl) % cnt == 0, cnt, uoff, U, tau, wv, i,
+                               kg);
+  int buf = 0;
+  for (int k = k0; k < k1; ++k) {
+    fb_sync();
+    fb_stage(P, stg[(k + 2) % 3], min(k + 2, kl), cnt, uoff, wv, lane);
+    const float* sl = stg[k % 3];
+    bf16x8 a1;
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      const int slot = 8 * kg + jj;
+      const float x = sl[i * kF + max(l1_feat(slot), 0)];
+      const short hi = dca::f2bf(x);
+      const short lo = dca::f2bf(x - dca::bf2f(hi));
+      a1[jj] = l1_feat(slot) < 0 ? (short)0x3F80 : (l1_xlo(slot) ? lo : hi);
+    }
+    bf16x4 ub, ubl;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float x = i < kF ? sl[(4 * kg + r) * kF + i] : 0.f;
+      ub[r] = dca::f2bf(x);
+      ubl[r] = dca::f2bf(x - dca::bf2f(ub[r]));
+    }
+    const short* ih = &img[buf][0][0];
+    const short* il = &img[buf][1][0];
+    bf16x8 de[4], del[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      de[s] = tile_frag(ih, 32 * s, lane);
+      del[s] = tile_frag(il, 32 * s, lane);
+    }
+    bf16x4 eh[8], el[8];
+#pragma unroll
+    for (int et = 0; et < 8; ++et) {
+      eh[et] = *reinterpret_cast<const bf16x4*>(ih + img_off(16 * et + i, kg));
+      el[et] = *reinterpret_cast<const bf16x4*>(il + img_off(16 * et + i, kg));
+    }
+    const f32x4 l1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, wb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+    f32x4 c = mfma3_k128(de, del, wf, wfl);
+    // item k + 1's ∂emb into the other image (every wave has passed this item's barrier, so none still reads it;
+    // past the range's end this rewrites the last item, which nobody reads)
+    fb_build<GIVEN>(bn, stg[(k + 1) % 3], min(k + 1, kl) % cnt, &img[buf ^ 1][0][0], &img[buf ^ 1][1][0], wv, lane);
+    fb_load_build<GIVEN, COMPAT>(bn, R, P.ldq, min(k + 2, kl), k + 2 <= kl && (k + 2) % cnt == 0, cnt, uoff, U, tau,
+                                 wv, i, kg);
+    bf16x4 bh, bl;
+    f32x4 bas;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      bas[r] = fmaxf(l1[r], 0.f);
+      bh[r] = dca::f2bf(bas[r]);
+      bl[r] = dca::f2bf(bas[r] - dca::bf2f(bh[r]));
+    }
+    // ∂W_τᵀ[j][e] += Σ_rows basic[row][j] · ∂emb[row][e]
+#pragma unroll
+    for (int et = 0; et < 8; ++et) {
+      acc[et] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(bl, eh[et], acc[et], 0, 0, 0);
+      acc[et] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(bh, el[et], acc[et], 0, 0, 0);
+      acc[et] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(bh, eh[et], acc[et], 0, 0, 0);
+    }
+    bf16x4 a, al;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      c[r] = bas[r] > 0.f ? c[r] : 0.f;
+      a[r] = dca::f2bf(c[r]);
+      al[r] = dca::f2bf(c[r] - dca::bf2f(a[r]));
+      db1acc += c[r];
+    }
+    // ∂W1[j][f] += Σ_rows ∂basic[row][j] · units[row][f]
+    dw1acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, ub, dw1acc, 0, 0, 0);
+    dw1acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, ubl, dw1acc, 0, 0, 0);
+    dw1acc = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a, ub, dw1acc, 0, 0, 0);
+    buf ^= 1;
+  }
+  // ---- partials: ∂W_τ tile-linear ((wv·8 + et)·64 + lane)·4 + r; ∂W1 rows j of this wave's tile, ∂b1
+  float* dst = P.dwtpart + (size_t)job * (kD * kD);
+#pragma unroll
+  for (int et = 0; et < 8; ++et) *reinterpret_cast<f32x4*>(dst + ((8 * wv + et) * 64 + lane) * 4) = acc[et];
+  float* wp = P.w1part + (size_t)job * kW1;
+  if (i < kF) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) wp[(16 * wv + 4 * kg + r) * kF + i] = dw1acc[r];
+  }
+  float s = db1acc;
+  s += __shfl_xor(s, 16, 64);
+  s += __shfl_xor(s, 32, 64);
+  if (kg == 0) wp[kD * kF + 16 * wv + i] = s;
+}
+
+// Fixed-order sum of a type's fused-backward partials (tile-linear → ∂W_τ[e][j]); 4 job phases per block as dwt_reduce.
+__global__ __launch_bounds__(256) void fb_dwt_reduce(const float* __restrict__ part, FbParams P, float* __restrict__ dwt) {
+  __shared__ float red[4][64];
+  const int tau = blockIdx.y, ph = threadIdx.x >> 6;
+  const int xi = blockIdx.x * 64 + (threadIdx.x & 63);
+  float s = 0.f;
+#pragma unroll 4
+  for (int j = P.jbase[tau] + ph; j < P.jbase[tau + 1]; j += 4) s += part[(size_t)j * (kD * kD) + xi];
+  red[ph][threadIdx.x & 63] = s;
   __syncthreads();
-  for (int e = tid; e < kW1; e += 256) P.w1part[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * kW1 + e] = wred[e];
+  if (ph) return;
+  s = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+  const int r = xi & 3, lane = (xi >> 2) & 63, tile = xi >> 8;
+  const int j = 16 * (tile >> 3) + 4 * (lane >> 4) + r;
+  const int e = 16 * (tile & 7) + (lane & 15);
+  dwt[(size_t)tau * kD * kD + e * kD + j] = s;
 }
 
 // Fixed-order sum of the per-workgroup ∂W1‖∂b1 partials: block of 256 = 16 columns × 16 row phases (88 blocks;
@@ -945,10 +1022,7 @@ __device__ __forceinline__ void dwt_load(const short* __restrict__ A, const shor
   }
 }
 
-// F32: Al / Bl are the lo-half images; acc += a·b + al·b + a·bl (bf16x3)
-template <bool F32>
 __global__ __launch_bounds__(256, 2) void dwt_blocked_kernel(const short* __restrict__ A, const short* __restrict__ Bm,
-                                                             const short* __restrict__ Al, const short* __restrict__ Bl,
                                                              DwtJobs J, float* __restrict__ part) {
   const int job = blockIdx.x, wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   int tau = 0;
@@ -962,32 +1036,17 @@ __global__ __launch_bounds__(256, 2) void dwt_blocked_kernel(const short* __rest
 #pragma unroll
     for (int y = 0; y < 4; ++y) acc[x][y] = f32x4{0.f, 0.f, 0.f, 0.f};
   bf16x8 a[4], bb[4], an[4], bn[4];
-  bf16x8 al[4], bl[4], aln[4], bln[4];
   dwt_load(A, Bm, b0, bend, mq, nq, lane, a, bb);
-  if constexpr (F32) dwt_load(Al, Bl, b0, bend, mq, nq, lane, al, bl);
   for (long long b = b0; b < bend; b += 2) {
-    if (b + 2 < bend) {
-      dwt_load(A, Bm, b + 2, bend, mq, nq, lane, an, bn);
-      if constexpr (F32) dwt_load(Al, Bl, b + 2, bend, mq, nq, lane, aln, bln);
-    }
-    if constexpr (F32) {
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[x], bb[y], acc[x][y], 0, 0, 0);
-#pragma unroll
-      for (int x = 0; x < 4; ++x)
-#pragma unroll
-        for (int y = 0; y < 4; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[x], bl[y], acc[x][y], 0, 0, 0);
-    }
+    if (b + 2 < bend) dwt_load(A, Bm, b + 2, bend, mq, nq, lane, an, bn);
 #pragma unroll
     for (int x = 0; x < 4; ++x)
 #pragma unroll
       for (int y = 0; y < 4; ++y) acc[x][y] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[x], bb[y], acc[x][y], 0, 0, 0);
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
-      a[t] = an[t]; bb[t] = bn[t];
-      if constexpr (F32) { al[t] = aln[t]; bl[t] = bln[t]; }
+      a[t] = an[t];
+      bb[t] = bn[t];
     }
   }
   // tile-linear partial: ((wave·16 + 4x + y)·64 + lane)·4 + r
@@ -1051,17 +1110,37 @@ void dwt_plan(int N, const int* counts, DwtJobs& J, int& NB) {
   }
   J.jbase[6] = jobs;
 }
+
+void fb_plan(int N, const int* counts, FbParams& P) {
+  const long long NB = (N + 15) / 16;
+  long long total = 0;
+  for (int t = 0; t < 6; ++t) total += counts[t] * NB;
+  // ≈500 equal jobs: two rounds of one workgroup per CU (VGPR-bound occupancy), + at most one tail job per type
+  P.items = (int)std::max<long long>(1, (total + 499) / 500);
+  int jobs = 0;
+  for (int t = 0; t < 6; ++t) {
+    P.jbase[t] = jobs;
+    jobs += (int)((counts[t] * NB + P.items - 1) / P.items);
+  }
+  P.jbase[6] = jobs;
+}
 }  // namespace
 
-// Workspace: ∂W1 partials ‖ K-blocked ∂emb and basic images (bf16; F32: hi and lo of each) ‖ ∂W_τ split-K partials.
+// Workspace. bf16: ∂W1 partials ‖ K-blocked ∂emb and basic images ‖ ∂W_τ split-K partials. F32 (fused ∂W_τ):
+// per job one ∂W1‖∂b1 partial and one 128×128 ∂W_τ partial.
 extern "C" size_t dca_encoder_bwd_workspace(int N, int U, const int* counts, int f32) {
+  if (f32) {
+    FbParams F{};
+    fb_plan(N, counts, F);
+    return (size_t)F.jbase[6] * (kW1 + kD * kD) * sizeof(float);
+  }
   DwtJobs J;
   int NB;
   dwt_plan(N, counts, J, NB);
   const size_t w1 = (size_t)((N + kRows - 1) / kRows) * kJobs * kW1 * sizeof(float);
   const size_t img = (size_t)U * NB * kD * 16 * sizeof(short);
   const size_t parts = (size_t)J.jbase[6] * kD * kD * sizeof(float);
-  return w1 + (f32 ? 4 : 2) * img + parts;
+  return w1 + 2 * img + parts;
 }
 
 extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const float* b1, const void* wtT,
@@ -1070,6 +1149,27 @@ extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const
                                       size_t ws_bytes, int N, int U, const int* counts, int compat, hipStream_t st,
                                       const void* demb_in, int f32) {
   if (ws_bytes < dca_encoder_bwd_workspace(N, U, counts, f32)) return hipErrorInvalidValue;
+  int acc = 0;
+  for (int t = 0; t < 6; ++t) acc += counts[t];
+  if (acc != U || U > 64) return hipErrorInvalidValue;
+  if (f32) {
+    FbParams F{units, w1, b1, static_cast<const float*>(wtT), dtl, q, ldq, dx, arg,
+               static_cast<const float*>(demb_in), nullptr, nullptr, N, compat, 0, {}, {}};
+    fb_plan(N, counts, F);
+    F.L.U = U;
+    for (int t = 0, o = 0; t < 6; ++t) { F.L.cnt[t] = counts[t]; F.L.off[t] = o; o += counts[t]; }
+    const int jobs = F.jbase[6];
+    F.w1part = static_cast<float*>(ws);
+    F.dwtpart = F.w1part + (size_t)jobs * kW1;
+    if (jobs > 0) {
+      if (demb_in) encoder_bwd_f32_fused_kernel<true, false><<<jobs, 512, 0, st>>>(F);
+      else if (compat) encoder_bwd_f32_fused_kernel<false, true><<<jobs, 512, 0, st>>>(F);
+      else encoder_bwd_f32_fused_kernel<false, false><<<jobs, 512, 0, st>>>(F);
+    }
+    encoder_w1_reduce<<<(kW1 + 15) / 16, 256, 0, st>>>(F.w1part, jobs, dw1, db1);
+    fb_dwt_reduce<<<dim3(kD * kD / 64, 6), 256, 0, st>>>(F.dwtpart, F, dwt);
+    return hipGetLastError();
+  }
   DwtJobs J;
   int NB;
   dwt_plan(N, counts, J, NB);
@@ -1080,28 +1180,19 @@ extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const
   const size_t img = (size_t)U * NB * kD * 16;
   short* demb = reinterpret_cast<short*>(p);
   short* basic = demb + img;
-  short* demb_lo = f32 ? basic + img : nullptr;
-  short* basic_lo = f32 ? demb_lo + img : nullptr;
-  float* parts = reinterpret_cast<float*>(basic + (f32 ? 3 : 1) * img);
-  BwdParams P{units, w1, b1, wtT, dtl, q, ldq, dx, arg, demb, basic, demb_lo, basic_lo, w1part, N, compat, {}, {},
-              NB, demb_in};
+  float* parts = reinterpret_cast<float*>(basic + img);
+  BwdParams P{units, w1, b1, wtT, dtl, q, ldq, dx, arg, demb, basic, w1part, N, compat, {}, {}, NB, demb_in};
   P.L.U = U;
-  int acc = 0;
+  acc = 0;
   for (int t = 0; t < 6; ++t) {
     P.L.cnt[t] = counts[t];
     P.L.off[t] = acc;
     P.blkbase[t] = J.blkbase[t];
     acc += counts[t];
   }
-  if (acc != U || U > 64) return hipErrorInvalidValue;
-  const dim3 grid(nblk, kJobs);
-  if (f32) encoder_bwd_f32_kernel<<<grid, 256, 0, st>>>(P);
-  else encoder_bwd_kernel<<<grid, 256, 0, st>>>(P);
+  encoder_bwd_kernel<<<dim3(nblk, kJobs), 256, 0, st>>>(P);
   encoder_w1_reduce<<<(kW1 + 15) / 16, 256, 0, st>>>(w1part, nblk * kJobs, dw1, db1);
-  if (J.jbase[6] > 0) {
-    if (f32) dwt_blocked_kernel<true><<<J.jbase[6], 256, 0, st>>>(demb, basic, demb_lo, basic_lo, J, parts);
-    else dwt_blocked_kernel<false><<<J.jbase[6], 256, 0, st>>>(demb, basic, nullptr, nullptr, J, parts);
-  }
+  if (J.jbase[6] > 0) dwt_blocked_kernel<<<J.jbase[6], 256, 0, st>>>(demb, basic, J, parts);
   dwt_reduce<<<dim3(kD * kD / 64, 6), 256, 0, st>>>(parts, J, dwt);
   return hipGetLastError();
 }

@@ -136,8 +136,8 @@ def test_team_lstm_fp32_more_rows_than_a_chain(gpu_ops):
 
 
 # ------------------------------------------------------------------------------------------------ entity encoder
-@pytest.mark.parametrize('layout', ['1v1', '5v5'])
-def test_encoder_fp32_fwd_bwd(gpu_ops, layout):
+@pytest.mark.parametrize('layout,N', [('1v1', 75), ('5v5', 75), ('1v1', 3000), ('5v5', 1111)])
+def test_encoder_fp32_fwd_bwd(gpu_ops, layout, N):
     """encoder_fwd/encoder_bwd with fp32 weights (bf16x3 kernels) vs float64 autograd of the same ops
     (policy.py:97-138): embeddings, pools, argmax, and ∂W_τ / ∂W1 / ∂b1 through the pointer logits and the pools."""
     g = _g(5)
@@ -146,7 +146,8 @@ def test_encoder_fp32_fwd_bwd(gpu_ops, layout):
     off = [0]
     for c in counts:
         off.append(off[-1] + c)
-    N = 75                                           # not a multiple of the 16-row groups on purpose
+    # N not a multiple of the 16-row groups on purpose; the larger N give the fused backward multi-item jobs that
+    # start and end inside a row group
     units = torch.randn(N, U, 10, device='cuda', generator=g)
     env = torch.randn(N, 3, device='cuda', generator=g)
     w1 = torch.randn(D, 10, device='cuda', generator=g) * 0.3
@@ -160,7 +161,8 @@ def test_encoder_fp32_fwd_bwd(gpu_ops, layout):
     W1 = w1.double().requires_grad_(True)
     B1 = b1.double().requires_grad_(True)
     WT = wt.double().requires_grad_(True)
-    basic = torch.relu(units.double() @ W1.t() + B1)
+    pre = units.double() @ W1.t() + B1
+    basic = torch.relu(pre)
     ref = torch.cat([basic[:, off[t]:off[t + 1]] @ WT[t].t() + bt[t].double() for t in range(6)], 1)
     assert _rel(emb, ref) < 2e-5, _rel(emb, ref)
     assert _rel(x896[:, :D], torch.relu(env.double() @ we.double().t() + be.double())) < 1e-6
@@ -181,12 +183,20 @@ def test_encoder_fp32_fwd_bwd(gpu_ops, layout):
     tl = torch.einsum('nud,nd->nu', ref, q[:, :D].double())
     kpools = [ref[:, off[t]:off[t + 1]].gather(1, arg[:, t].long().unsqueeze(1)).squeeze(1) for t in range(6)]
     loss = (tl * dtl.double()).sum() + (torch.cat(kpools, 1) * dx[:, D:].double()).sum()
-    gw1, gb1, gwt = torch.autograd.grad(loss, [W1, B1, WT])
+    gw1, gb1, gwt, gbasic = torch.autograd.grad(loss, [W1, B1, WT, basic])
     dwt, dw1, db1 = gpu_ops.encoder_bwd(units, w1, b1, wt.transpose(1, 2).contiguous(), dtl, q, dx, arg, counts,
                                         False)
     torch.cuda.synchronize()
-    for got, want, name in ((dwt, gwt, 'dwt'), (dw1, gw1, 'dw1'), (db1, gb1, 'db1')):
-        assert _rel(got, want) < 1e-4, (name, _rel(got, want))
+    # ReLU' at a pre-activation within the kernel's layer-1 rounding (bf16 split, ≈2⁻¹⁶ of Σ|x·w|) of zero may go
+    # either way: those (row, unit, column) terms of ∂W1 / ∂b1 form an allowed band (a handful at N = 3000)
+    amb = (pre.detach().abs() < 1e-4 * (units.double().abs() @ w1.double().abs().t() + b1.double().abs())).double()
+    gb = gbasic.detach() * amb
+    band_w1 = torch.einsum('nuj,nuf->jf', gb.abs(), units.double().abs())
+    band_b1 = gb.abs().sum((0, 1))
+    assert _rel(dwt, gwt) < 1e-4, ('dwt', _rel(dwt, gwt))
+    for got, want, band, name in ((dw1, gw1, band_w1, 'dw1'), (db1, gb1, band_b1, 'db1')):
+        excess = ((got.double() - want).abs() - band).clamp(min=0)
+        assert float(excess.norm() / want.norm()) < 1e-4, (name, _rel(got, want), int(amb.sum()))
 
 
 # --------------------------------------------------------------------- whole step at the deploy horizon (S=1400)
