@@ -552,30 +552,9 @@ __global__ __launch_bounds__(256, 1) void encoder_bwd_kernel(BwdParams P) {
 // ============================================================================================================
 // F32 variants (the learner's fp32-accurate mode, "bf16x3"): every MFMA operand x is split once into two bf16,
 // x = hi + lo, and a product is hi·hi + lo·hi + hi·lo on three independent accumulation chains (the dropped lo·lo
-// term and the rounding of lo are ≈2⁻¹⁶ relative; f32 accumulation). Outputs are fp32. The hi + lo weight
-// fragments of a whole 128×128 W_τ would take 256 VGPRs on top of the job's state (spills), so a type job runs in
-// two passes over its units, each pass owning one 64-column half of the output (W half = 128 VGPRs); the cheap
-// layer 1 (one 16x16x32 MFMA per 16 columns) is recomputed per pass, the staged units are reused when they fit.
-constexpr int kHalfN = 4;   // 16-column MFMA tiles per half
-
-__device__ __forceinline__ void load_bfrags_split_half(const float* __restrict__ m, int h, bf16x8 (&bf)[kHalfN][4],
-                                                       bf16x8 (&bl)[kHalfN][4], int lane) {
-  const int j = lane & 15, kg = lane >> 4;
-#pragma unroll
-  for (int nn = 0; nn < kHalfN; ++nn)
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const float* p = m + (size_t)(16 * (kHalfN * h + nn) + j) * kD + 32 * s + 8 * kg;
-      const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-      const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        bf[nn][s][jj] = dca::f2bf(v[jj]);
-        bl[nn][s][jj] = dca::f2bf(v[jj] - dca::bf2f(bf[nn][s][jj]));
-      }
-    }
-}
-
+// term and the rounding of lo are ≈2⁻¹⁶ relative; f32 accumulation). Outputs are fp32. Both F32 kernels run
+// 8-wave workgroups over ranges of (16-row group, unit) items of one type, wave w owning 16 output columns (its
+// hi + lo weight fragments: 32 VGPRs), so that two waves share a SIMD.
 // bf16x3 16×16 tile over K = 128: Σ_s a·w + al·w + a·wl (three chains)
 __device__ __forceinline__ f32x4 mfma3_k128(const bf16x8 (&a)[4], const bf16x8 (&al)[4], const bf16x8 (&w)[4],
                                             const bf16x8 (&wl)[4]) {
@@ -589,112 +568,6 @@ __device__ __forceinline__ f32x4 mfma3_k128(const bf16x8 (&a)[4], const bf16x8 (
   return c + (c1 + c2);
 }
 
-__global__ __launch_bounds__(256, 1) void encoder_fwd_f32_kernel(FwdParams P) {
-  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-  const int rbase = blockIdx.x * kRows;
-  const int U = P.L.U, N = P.N;
-  float* const x896 = static_cast<float*>(P.x896);
-  float* const embo = static_cast<float*>(P.emb);
-  __shared__ __attribute__((aligned(16))) short scr[4][kImg];
-  __shared__ __attribute__((aligned(16))) short scl[4][kImg];
-  __shared__ __attribute__((aligned(16))) float ust[4][16 * kUP];
-
-  if (blockIdx.y == 0) {   // env embedding (fp32 VALU; job 0's workgroups)
-    const int r = tid >> 3, c0 = (tid & 7) * 16;
-    const int row = rbase + r;
-    if (row < N) {
-      const float e0 = P.env[row * 3], e1 = P.env[row * 3 + 1], e2 = P.env[row * 3 + 2];
-      for (int c = c0; c < c0 + 16; ++c) {
-        const float v = P.be[c] + P.we[c * 3] * e0 + P.we[c * 3 + 1] * e1 + P.we[c * 3 + 2] * e2;
-        x896[(size_t)row * 896 + c] = fmaxf(v, 0.f);
-      }
-    }
-  }
-
-  bf16x8 wb[8];
-  load_w1_split(P.w1, P.b1, wb, lane);
-  short* img = &scr[wv][0];
-  short* imgl = &scl[wv][0];
-  const int i = lane & 15, kg = lane >> 4;
-  // job split over blockIdx.y (gridDim.y == 3: one type job per wave per workgroup; 1: all three)
-  const int jlo = gridDim.y == 3 ? (int)blockIdx.y : 0, jhi = gridDim.y == 3 ? jlo + 1 : 3;
-  for (int j = jlo; j < jhi; ++j) {
-    int tau, g;
-    type_job(wv, j, tau, g);
-    const int cnt = P.L.cnt[tau], uoff = P.L.off[tau];
-    if (cnt == 0) continue;
-    const int row0 = rbase + 16 * g;
-    float* ur = &ust[wv][0];
-    for (int h = 0; h < 2; ++h) {
-      bf16x8 wf[kHalfN][4], wfl[kHalfN][4];
-      load_bfrags_split_half(static_cast<const float*>(P.wt) + (size_t)tau * kD * kD, h, wf, wfl, lane);
-      float btv[kHalfN];
-#pragma unroll
-      for (int nn = 0; nn < kHalfN; ++nn) btv[nn] = P.bt[tau * kD + 16 * (kHalfN * h + nn) + i];
-      f32x4 pmax[kHalfN];
-      int parg[kHalfN][4];
-#pragma unroll
-      for (int nn = 0; nn < kHalfN; ++nn) {
-        pmax[nn] = (f32x4){-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-#pragma unroll
-        for (int r = 0; r < 4; ++r) parg[nn][r] = 0;
-      }
-      for (int c0 = 0; c0 < cnt; c0 += kStage) {
-        const int cc = min(kStage, cnt - c0);
-        if (h == 0 || cnt > kStage) {   // one chunk: the staged units of the first pass serve the second
-          __builtin_amdgcn_wave_barrier();
-          stage_units(P.units, nullptr, U, N, row0, uoff + c0, cc, ur, nullptr, lane);
-          __builtin_amdgcn_wave_barrier();
-        }
-        for (int uc = 0; uc < cc; ++uc) {
-          const int u = c0 + uc;
-          f32x4 acc[8];
-          layer1_split(ur, uc, wb, acc, lane);
-#pragma unroll
-          for (int n = 0; n < 8; ++n) {
-            f32x4 b;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) b[r] = fmaxf(acc[n][r], 0.f);
-            tile_put(img, n, b, lane);
-            tile_put_lo(imgl, n, b, lane);
-          }
-          __builtin_amdgcn_wave_barrier();
-          bf16x8 af[4], afl[4];
-#pragma unroll
-          for (int s = 0; s < 4; ++s) {
-            af[s] = tile_frag(img, 32 * s, lane);
-            afl[s] = tile_frag(imgl, 32 * s, lane);
-          }
-#pragma unroll
-          for (int nn = 0; nn < kHalfN; ++nn) {
-            f32x4 c = mfma3_k128(af, afl, wf[nn], wfl[nn]);
-            const int n = kHalfN * h + nn;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const float v = c[r] + btv[nn];
-              if (v > pmax[nn][r]) { pmax[nn][r] = v; parg[nn][r] = u; }
-              const int row = row0 + 4 * kg + r;
-              if (row < N) embo[((size_t)row * U + uoff + u) * kD + 16 * n + i] = v;
-            }
-          }
-          __builtin_amdgcn_wave_barrier();
-        }
-      }
-#pragma unroll
-      for (int nn = 0; nn < kHalfN; ++nn)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int row = row0 + kg * 4 + r;
-          if (row < N) {
-            const int col = 16 * (kHalfN * h + nn) + i;
-            x896[(size_t)row * 896 + kD + tau * kD + col] = pmax[nn][r];
-            P.arg[((size_t)row * 6 + tau) * kD + col] = (unsigned char)parg[nn][r];
-          }
-        }
-    }
-  }
-}
-
 // F32 backward, fused ∂W_τ. The bf16 path writes ∂emb and basic as K-blocked images for a separate GEMM; at bf16x3
 // that is four bf16 images (≈460 MB at the 1v1 learner shape) written and read back. Here a workgroup of 8 waves
 // owns a contiguous range of (16-row group, unit) items of ONE type τ and keeps ∂W_τ in registers across the range:
@@ -704,8 +577,7 @@ __global__ __launch_bounds__(256, 1) void encoder_fwd_f32_kernel(FwdParams P) {
 //   * wave w owns basic columns j ∈ tile w: layer 1 (recomputed), ∂basic = ∂emb·W_τ[:, j] (bf16x3, A fragments
 //     by ds_read_b64_tr_b16), ReLU', ∂W1 rows j, and ∂W_τᵀ[j][e] += basicᵀ·∂emb on 16x16x16 MFMAs whose A operand
 //     is the C-layout basic tile and whose B operand is the C-layout ∂emb tile read back as written;
-//   * an item's unit features and dtl (identical for all 8 waves) are staged once into LDS by LDS-DMA two items
-//     ahead; the per-row q / ∂pool / argmax of the wave's e-tile are raw buffer loads (hardware bounds check: rows
+//   * an item's unit features and dtl (identical for all 8 waves) are staged once into LDS two items ahead; the per-row q / ∂pool / argmax of the wave's e-tile are raw buffer loads (hardware bounds check: rows
 //     past N read 0), issued one item ahead and only when the row group changes.
 // 2 waves per SIMD (≤ 256 VGPRs) overlap one wave's loads / VALU with the other's MFMAs.
 // Each workgroup writes one tile-linear 128×128 ∂W_τ partial and one ∂W1‖∂b1 partial; fixed-order reduces follow.
@@ -766,30 +638,19 @@ __device__ __forceinline__ void fb_load_build(FbBuild& p, const FbRsrc& R, int l
   }
 }
 
-// Per-item staging (LDS, 3 slots): units[row0 .. row0+15][u][0..9] (160 floats) ‖ dtl[row0 .. row0+15][u] (16) —
-// the same for all 8 waves, so it is moved once by LDS-DMA (waves 0-2, one global_load_lds_dword each; rows past N
-// read row N-1, whose ∂emb is zero) instead of being loaded by every wave into registers.
+// Per-item staging (LDS, 3 slots): units[row0 .. row0+15][u][0..9] (160 floats) ‖ dtl[row0 .. row0+15][u] (16) — the
+// same for all 8 waves, so waves 0-2 load it once (one dword per lane, rows past N read row N-1, whose ∂emb is zero),
+// hold it in a register for an item and write it to the slot two items ahead of its use. (An LDS-DMA load instead
+// made the compiler wait for it before every later read of the staging array: one exposed round trip per item.)
 constexpr int kStg = 192;
-__device__ __forceinline__ void fb_stage(const FbParams& P, float* slot, int k, int cnt, int uoff, int wv, int lane) {
-  if (wv >= 3) return;
-  typedef __attribute__((address_space(1))) void gvoid;
-  typedef __attribute__((address_space(3))) void lvoid;
+__device__ __forceinline__ float fb_stage_load(const FbParams& P, int k, int cnt, int uoff, int wv, int lane) {
   const int U = P.L.U, N = P.N;
   const int rb = k / cnt, u = k - rb * cnt, row0 = 16 * rb;
-  const int idx = 64 * wv + lane;
-  const float* src;
-  if (idx < 16 * kF) {
-    const int row = min(row0 + idx / kF, N - 1);
-    src = P.units + ((size_t)row * U + uoff + u) * kF + idx % kF;
-  } else {
-    const int row = min(row0 + min(idx - 16 * kF, 15), N - 1);
-    src = P.dtl ? P.dtl + (size_t)row * U + uoff + u : P.units;
-  }
-  __builtin_amdgcn_global_load_lds((gvoid*)src, (lvoid*)(slot + 64 * wv), 4, 0, 0);
+  const int idx = 64 * min(wv, 2) + lane;
+  if (idx < 16 * kF) return P.units[((size_t)min(row0 + idx / kF, N - 1) * U + uoff + u) * kF + idx % kF];
+  const int row = min(row0 + min(idx - 16 * kF, 15), N - 1);
+  return P.dtl ? P.dtl[(size_t)row * U + uoff + u] : 0.f;
 }
-
-// all of this wave's loads (incl. its LDS-DMA) done, then the workgroup barrier
-__device__ __forceinline__ void fb_sync() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ∂emb e-tile wv of item k (C layout) → hi / lo image
 template <bool GIVEN>
@@ -801,7 +662,7 @@ __device__ __forceinline__ void fb_build(const FbBuild& b, const float* slot, in
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = b.q[r];
   } else {
-    const f32x4 d4 = *reinterpret_cast<const f32x4*>(slot + 16 * kF + 4 * kg);
+    const f32x4 d4 = *reinterpret_cast<const f32x4*>(slot + 16 * kF + 4 * kg);   // dtl of rows 4kg … 4kg + 3
 #pragma unroll
     for (int r = 0; r < 4; ++r) v[r] = d4[r] * b.q[r] + (b.ab[r] == (unsigned)u ? b.ds[r] : 0.f);
   }
@@ -858,21 +719,29 @@ __global__ __launch_bounds__(512, 1) void encoder_bwd_f32_fused_kernel(FbParams 
 #pragma unroll
   for (int et = 0; et < 8; ++et) acc[et] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // Software pipeline, per item k: [sync: image k built, staging of k+1 landed] → stage k+2 → item k's MFMAs with
-  // the ∂emb of k+1 built in between (its row data were loaded one item earlier) → build loads of k+2.
+  // Software pipeline, per item k: [barrier: image k built, staging slot of k+1 written] → waves 0-2 write the
+  // staging of k+2 (loaded one item earlier) and load k+3 → item k's MFMAs with the ∂emb of k+1 built in between
+  // (its row data were loaded one item earlier) → build loads of k+2. No barrier waits on global memory.
   FbBuild bn;
   const int kl = max(k1 - 1, 0);
-  fb_stage(P, stg[k0 % 3], min(k0, kl), cnt, uoff, wv, lane);
-  fb_stage(P, stg[(k0 + 1) % 3], min(k0 + 1, kl), cnt, uoff, wv, lane);
+  float pre = 0.f;
+  if (wv < 3) {
+    stg[k0 % 3][64 * wv + lane] = fb_stage_load(P, min(k0, kl), cnt, uoff, wv, lane);
+    stg[(k0 + 1) % 3][64 * wv + lane] = fb_stage_load(P, min(k0 + 1, kl), cnt, uoff, wv, lane);
+    pre = fb_stage_load(P, min(k0 + 2, kl), cnt, uoff, wv, lane);
+  }
   fb_load_build<GIVEN, COMPAT>(bn, R, P.ldq, min(k0, kl), true, cnt, uoff, U, tau, wv, i, kg);
-  fb_sync();
+  lds_barrier();
   fb_build<GIVEN>(bn, stg[k0 % 3], k0 % cnt, &img[0][0][0], &img[0][1][0], wv, lane);
   fb_load_build<GIVEN, COMPAT>(bn, R, P.ldq, min(k0 + 1, kl), min(k0 + 1, kl) % cnt == 0, cnt, uoff, U, tau, wv, i,
                                kg);
   int buf = 0;
   for (int k = k0; k < k1; ++k) {
-    fb_sync();
-    fb_stage(P, stg[(k + 2) % 3], min(k + 2, kl), cnt, uoff, wv, lane);
+    lds_barrier();
+    if (wv < 3) {
+      stg[(k + 2) % 3][64 * wv + lane] = pre;
+      pre = fb_stage_load(P, min(k + 3, kl), cnt, uoff, wv, lane);
+    }
     const float* sl = stg[k % 3];
     bf16x8 a1;
 #pragma unroll
@@ -953,6 +822,164 @@ __global__ __launch_bounds__(512, 1) void encoder_bwd_f32_fused_kernel(FbParams 
   s += __shfl_xor(s, 16, 64);
   s += __shfl_xor(s, 32, 64);
   if (kg == 0) wp[kD * kF + 16 * wv + i] = s;
+}
+
+// F32 forward over item ranges (same organisation as the fused backward): a workgroup of 8 waves owns whole 16-row
+// groups of ONE type τ and walks its (row group, unit) items; per item
+//   * wave w computes basic tile w (layer 1, one 16x16x32 MFMA on the bf16-split unit features staged in LDS two
+//     items ahead) → ReLU → hi / lo transposed image (double-buffered, one item ahead);
+//   * wave w computes output columns 16w … 16w+15 of emb = basic·W_τᵀ + b_τ (bf16x3 over K = 128, A fragments by
+//     ds_read_b64_tr_b16), stores them (fp32) and keeps the running max / argmax over the group's units in
+//     registers, flushed to x896 / arg after the group's last unit.
+struct FfParams {
+  const float* units;
+  const float* env;
+  const float* w1;
+  const float* b1;
+  const float* wt;       // (6, 128, 128) fp32 W_τ (out, in)
+  const float* bt;
+  const float* we;
+  const float* be;
+  float* x896;
+  float* emb;
+  unsigned char* arg;
+  int N;
+  Layout L;
+  int gpj[6];            // row groups per job of each type
+  int jbase[7];
+};
+
+__device__ __forceinline__ float ff_stage_load(const FfParams& P, __amdgpu_buffer_rsrc_t Ru, int k, int cnt, int uoff,
+                                              int wv, int lane) {
+  const int idx = min(64 * min(wv, 2) + lane, 16 * kF - 1);
+  const int rb = k / cnt, u = k - rb * cnt;
+  const int row = min(16 * rb + idx / kF, P.N - 1);
+  return bload(Ru, ((row * P.L.U + uoff + u) * kF + idx % kF) * 4);
+}
+
+// layer 1 of basic tile wv for the staged item → ReLU → hi / lo image
+__device__ __forceinline__ void ff_layer1(const float* sl, const bf16x8& wb, short* ih, short* il, int wv, int lane) {
+  const int i = lane & 15, kg = lane >> 4;
+  bf16x8 a1;
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) {
+    const int slot = 8 * kg + jj;
+    const float x = sl[i * kF + max(l1_feat(slot), 0)];
+    const short hi = dca::f2bf(x);
+    const short lo = dca::f2bf(x - dca::bf2f(hi));
+    a1[jj] = l1_feat(slot) < 0 ? (short)0x3F80 : (l1_xlo(slot) ? lo : hi);
+  }
+  const f32x4 l1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, wb, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+  f32x4 b;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) b[r] = fmaxf(l1[r], 0.f);
+  tile_put(ih, wv, b, lane);
+  tile_put_lo(il, wv, b, lane);
+}
+
+__global__ __launch_bounds__(512, 1) void encoder_fwd_f32_items_kernel(FfParams P) {
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int i = lane & 15, kg = lane >> 4;
+  const int job = blockIdx.x, N = P.N, U = P.L.U;
+  // env embedding (fp32 VALU): 32-row blocks strided over the jobs
+  for (int rbase = 32 * job; rbase < N; rbase += 32 * (int)gridDim.x) {
+    const int row = rbase + (tid >> 4), c0 = (tid & 15) * 8;
+    if (row < N) {
+      const float e0 = P.env[row * 3], e1 = P.env[row * 3 + 1], e2 = P.env[row * 3 + 2];
+#pragma unroll
+      for (int c = c0; c < c0 + 8; ++c)
+        P.x896[(size_t)row * 896 + c] = fmaxf(P.be[c] + P.we[c * 3] * e0 + P.we[c * 3 + 1] * e1 + P.we[c * 3 + 2] * e2, 0.f);
+    }
+  }
+  int tau = 0;
+#pragma unroll
+  for (int t = 1; t < 6; ++t) tau += job >= P.jbase[t] ? 1 : 0;
+  if (job >= P.jbase[6]) return;
+  const int cnt = P.L.cnt[tau], uoff = P.L.off[tau];
+  const int NB = (N + 15) >> 4;
+  const int g0 = (job - P.jbase[tau]) * P.gpj[tau], g1 = min(g0 + P.gpj[tau], NB);
+  const int k0 = g0 * cnt, k1 = g1 * cnt, kl = k1 - 1;
+  __shared__ __attribute__((aligned(16))) short img[2][2][kImg];
+  __shared__ __attribute__((aligned(16))) float stg[3][kStg];
+
+  const int col = 16 * wv + i;
+  bf16x8 wf[4], wfl[4], wb;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {   // B[k = j][n = out] = W_τ[out][j]
+    const float* p = P.wt + ((size_t)tau * kD + col) * kD + 32 * s + 8 * kg;
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) {
+      wf[s][jj] = dca::f2bf(v[jj]);
+      wfl[s][jj] = dca::f2bf(v[jj] - dca::bf2f(wf[s][jj]));
+    }
+  }
+#pragma unroll
+  for (int jj = 0; jj < 8; ++jj) {
+    const int slot = 8 * kg + jj, f = l1_feat(slot);
+    const float w = f >= 0 ? P.w1[col * kF + f] : P.b1[col];
+    const short hi = dca::f2bf(w);
+    const short lo = dca::f2bf(w - dca::bf2f(hi));
+    wb[jj] = (slot == 31 || (f >= 0 && l1_wlo(slot))) ? lo : hi;
+  }
+  const float btv = P.bt[tau * kD + col];
+  const __amdgpu_buffer_rsrc_t Ru = uniform_rsrc(P.units, N * U * kF * 4),
+                               Re = uniform_rsrc(P.emb, N * U * kD * 4);
+  f32x4 pmax = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  int parg[4] = {0, 0, 0, 0};
+
+  // staging as in the fused backward: waves 0-2 write item k+2's unit rows at item k, loaded one item earlier
+  float pre = 0.f;
+  if (wv < 3) {
+    stg[k0 % 3][64 * wv + lane] = ff_stage_load(P, Ru, k0, cnt, uoff, wv, lane);
+    stg[(k0 + 1) % 3][64 * wv + lane] = ff_stage_load(P, Ru, min(k0 + 1, kl), cnt, uoff, wv, lane);
+    pre = ff_stage_load(P, Ru, min(k0 + 2, kl), cnt, uoff, wv, lane);
+  }
+  lds_barrier();
+  ff_layer1(stg[k0 % 3], wb, &img[0][0][0], &img[0][1][0], wv, lane);
+  int buf = 0;
+  for (int k = k0; k < k1; ++k) {
+    lds_barrier();   // image k complete; staging slot of k + 1 written
+    if (wv < 3) {
+      stg[(k + 2) % 3][64 * wv + lane] = pre;
+      pre = ff_stage_load(P, Ru, min(k + 3, kl), cnt, uoff, wv, lane);
+    }
+    const int rb = k / cnt, u = k - rb * cnt, row0 = 16 * rb;
+    const short* ih = &img[buf][0][0];
+    const short* il = &img[buf][1][0];
+    bf16x8 af[4], afl[4];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      af[s] = tile_frag(ih, 32 * s, lane);
+      afl[s] = tile_frag(il, 32 * s, lane);
+    }
+    const f32x4 c = mfma3_k128(af, afl, wf, wfl);
+    // next item's basic tile into the other image (past the range's end: a rewrite nobody reads)
+    ff_layer1(stg[(k + 1) % 3], wb, &img[buf ^ 1][0][0], &img[buf ^ 1][1][0], wv, lane);
+    // emb stores are bounds-checked buffer stores (rows past N are dropped): no per-row branches
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = c[r] + btv;
+      if (v > pmax[r]) { pmax[r] = v; parg[r] = u; }
+      const int row = row0 + 4 * kg + r;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), Re, ((row * U + uoff + u) * kD + col) * 4,
+                                            0, 0);
+    }
+    if (u == cnt - 1) {   // the group's last unit: pools + argmax
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + 4 * kg + r;
+        if (row < N) {
+          P.x896[(size_t)row * 896 + kD + tau * kD + col] = pmax[r];
+          P.arg[((size_t)row * 6 + tau) * kD + col] = (unsigned char)parg[r];
+        }
+        pmax[r] = -INFINITY;
+        parg[r] = 0;
+      }
+    }
+    buf ^= 1;
+  }
 }
 
 // Fixed-order sum of a type's fused-backward partials (tile-linear → ∂W_τ[e][j]); 4 job phases per block as dwt_reduce.
@@ -1090,9 +1117,26 @@ extern "C" hipError_t dca_encoder_fwd(const float* units, const float* env, cons
   if (acc != U || U > 64) return hipErrorInvalidValue;
   // (row block, type job) grid: 3× the workgroups of a row-block grid, so small batches (the actor's few thousand
   // rows) still fill the 256 CUs, and heavy jobs (16-unit types, dispatched first) are balanced by the light ones
+  if (f32) {
+    FfParams F{units, env, w1, b1, static_cast<const float*>(wt), bt, we, be, static_cast<float*>(x896),
+               static_cast<float*>(emb), arg, N, P.L, {}, {}};
+    const long long NB = (N + 15) / 16;
+    long long total = 0;
+    for (int t = 0; t < 6; ++t) total += counts[t] * NB;
+    const long long target = std::max<long long>(1, (total + 499) / 500);   // ≈500 equal jobs (cf. fb_plan)
+    int jobs = 0;
+    for (int t = 0; t < 6; ++t) {
+      F.jbase[t] = jobs;
+      F.gpj[t] = (int)((target + std::max(1, counts[t]) - 1) / std::max(1, counts[t]));
+      if (counts[t] > 0) jobs += (int)((NB + F.gpj[t] - 1) / F.gpj[t]);
+    }
+    F.jbase[6] = jobs;
+    // every launch also covers the env embedding (32-row blocks strided over the grid)
+    encoder_fwd_f32_items_kernel<<<std::max(jobs, 1), 512, 0, st>>>(F);
+    return hipGetLastError();
+  }
   const dim3 grid((N + kRows - 1) / kRows, kJobs);
-  if (f32) encoder_fwd_f32_kernel<<<grid, 256, 0, st>>>(P);
-  else encoder_fwd_kernel<<<grid, 256, 0, st>>>(P);
+  encoder_fwd_kernel<<<grid, 256, 0, st>>>(P);
   return hipGetLastError();
 }
 
