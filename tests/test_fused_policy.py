@@ -86,8 +86,12 @@ def test_graph_captured_step_matches_eager(gpu_ops, monkeypatch, chunks, precisi
         torch.cuda.synchronize()
         torch.testing.assert_close(mb['grad_norm'], ma['grad_norm'], rtol=1e-4, atol=1e-7)
     assert b.graph is not None
-    torch.testing.assert_close(b.flat.flat, a.flat.flat, rtol=1e-5, atol=1e-6)
-    torch.testing.assert_close(mb['loss'], ma['loss'], rtol=1e-5, atol=1e-6)
+    # the chunked two-stream fp32 step is not bitwise reproducible run to run (two EAGER learners differed by 4e-8 in
+    # a parameter at step 4 on MI355X; cause not isolated — the chunked mode is off by default); Adam's m/√v turns
+    # that into ≈5e-6 on near-zero-gradient elements. A stale graph buffer shows up as O(1e-2+) errors.
+    rtol, atol = (1e-3, 1e-5) if chunks != '1' else (1e-5, 1e-6)
+    torch.testing.assert_close(b.flat.flat, a.flat.flat, rtol=rtol, atol=atol)
+    torch.testing.assert_close(mb['loss'], ma['loss'], rtol=rtol, atol=atol)
 
 
 @pytest.mark.parametrize('precision', ['fp32', 'bf16'])
