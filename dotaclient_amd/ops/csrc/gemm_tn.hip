@@ -41,6 +41,24 @@ __device__ __forceinline__ int lds_off(int row, int ch) {   // byte offset of 16
   return 256 * row + 16 * (ch ^ (((row & 3) << 2) | ((row >> 2) & 3)));
 }
 
+// Buffer resource over [p, p + bytes) from wave-uniform values. The staging loads are raw buffer loads with the
+// hardware bounds check standing in for the K / M / N edge tests: an out-of-range chunk gets an offset past the end and
+// reads 0. (With if-guarded loads the compiler merged each guarded value with its zero default right after the
+// load, i.e. waited for every slab load where it was issued instead of behind the MFMAs.)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, long long bytes) {
+  const unsigned long long a = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+  const int nb = (int)(bytes < 0 ? 0 : (bytes > 0x7fff0000LL ? 0x7fff0000LL : bytes));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0,
+                                           __builtin_amdgcn_readfirstlane(nb), 0x00020000);
+}
+constexpr int kOob = 0x7fff8000;   // byte offset past every operand (≤ 0x7fff0000 bytes)
+
+__device__ __forceinline__ uint4 bload16(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+
 struct Args {
   const void* A; int lda;
   const void* B; int ldb;
@@ -52,28 +70,39 @@ struct Args {
   int M, N, K, kc, splits, tiles_n, accumulate;
 };
 
+struct Rsrc {
+  __amdgpu_buffer_rsrc_t A, B, B0;
+};
+
+// operand byte counts: A has K rows, B K - split rows, B0 split rows (row strides lda / ldb, es-byte elements)
+__device__ __forceinline__ Rsrc make_rsrc(const Args& a, int es) {
+  Rsrc r;
+  r.A = uniform_rsrc(a.A, ((long long)(a.K - 1) * a.lda + a.M) * es);
+  r.B = uniform_rsrc(a.B, a.K > a.split ? ((long long)(a.K - a.split - 1) * a.ldb + a.N) * es : 0);
+  r.B0 = uniform_rsrc(a.B0 ? a.B0 : a.B, a.split > 0 ? ((long long)(a.split - 1) * a.ldb + a.N) * es : 0);
+  return r;
+}
+
 // ---- bf16 operands: 64-row K slabs, one image per operand -------------------------------------------------------
-__device__ __forceinline__ void load_stage(const Args& a, int kbase, int kend, int m_base, int n_base,
+template <bool WITH_B0>
+__device__ __forceinline__ void load_stage(const Args& a, const Rsrc& R, int kbase, int kend, int m_base, int n_base,
                                            uint4 (&ra)[4], uint4 (&rb)[4]) {
   const int t = threadIdx.x, ch = t & 15;
-  const short* A = static_cast<const short*>(a.A);
+  const int m = m_base + ch * 8, n = n_base + ch * 8;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int r = (t >> 4) + 16 * i;
-    const int k = kbase + r;
-    uint4 va = make_uint4(0, 0, 0, 0), vb = make_uint4(0, 0, 0, 0);
-    if (k < kend) {
-      const int m = m_base + ch * 8;
-      if (m < a.M) va = *reinterpret_cast<const uint4*>(A + (size_t)k * a.lda + m);
-      const int n = n_base + ch * 8;
-      if (n < a.N) {
-        const short* bp = (k < a.split) ? static_cast<const short*>(a.B0) + (size_t)k * a.ldb
-                                        : static_cast<const short*>(a.B) + (size_t)(k - a.split) * a.ldb;
-        vb = *reinterpret_cast<const uint4*>(bp + n);
-      }
+    const int k = kbase + (t >> 4) + 16 * i;
+    const bool kin = k < kend;
+    ra[i] = bload16(R.A, kin && m < a.M ? (k * a.lda + m) * 2 : kOob);
+    rb[i] = bload16(R.B, kin && n < a.N && k >= a.split ? ((k - a.split) * a.ldb + n) * 2 : kOob);
+  }
+  if (WITH_B0 && kbase < a.split) {   // the slab holding B0's rows (the LSTM's h0): a split-K chunk's first slab
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = kbase + (t >> 4) + 16 * i;
+      const uint4 v = bload16(R.B0, k < kend && n < a.N && k < a.split ? (k * a.ldb + n) * 2 : kOob);
+      rb[i] = make_uint4(rb[i].x | v.x, rb[i].y | v.y, rb[i].z | v.z, rb[i].w | v.w);
     }
-    ra[i] = va;
-    rb[i] = vb;
   }
 }
 
@@ -106,30 +135,33 @@ struct F32Stage {
   float4 a[2][2], b[2][2];   // [row i][half]: 8 consecutive columns of one K row
 };
 
-__device__ __forceinline__ void load_stage_f32(const Args& a, int kbase, int kend, int m_base, int n_base,
-                                               F32Stage& r) {
+template <bool WITH_B0>
+__device__ __forceinline__ void load_stage_f32(const Args& a, const Rsrc& R, int kbase, int kend, int m_base,
+                                               int n_base, F32Stage& r) {
   const int t = threadIdx.x, ch = t & 15;
-  const float* A = static_cast<const float*>(a.A);
+  const int m = m_base + ch * 8, n = n_base + ch * 8;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int k = kbase + (t >> 4) + 16 * i;
-    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-    r.a[i][0] = r.a[i][1] = r.b[i][0] = r.b[i][1] = z;
-    if (k < kend) {
-      const int m = m_base + ch * 8;
-      if (m < a.M) {
-        const float4* p = reinterpret_cast<const float4*>(A + (size_t)k * a.lda + m);
-        r.a[i][0] = p[0];
-        r.a[i][1] = p[1];
-      }
-      const int n = n_base + ch * 8;
-      if (n < a.N) {
-        const float* bp = (k < a.split) ? static_cast<const float*>(a.B0) + (size_t)k * a.ldb
-                                        : static_cast<const float*>(a.B) + (size_t)(k - a.split) * a.ldb;
-        const float4* p = reinterpret_cast<const float4*>(bp + n);
-        r.b[i][0] = p[0];
-        r.b[i][1] = p[1];
-      }
+    const bool kin = k < kend;
+    const int oa = kin && m < a.M ? (k * a.lda + m) * 4 : kOob;
+    const int ob = kin && n < a.N && k >= a.split ? ((k - a.split) * a.ldb + n) * 4 : kOob;
+    r.a[i][0] = __builtin_bit_cast(float4, bload16(R.A, oa));
+    r.a[i][1] = __builtin_bit_cast(float4, bload16(R.A, oa + 16));
+    r.b[i][0] = __builtin_bit_cast(float4, bload16(R.B, ob));
+    r.b[i][1] = __builtin_bit_cast(float4, bload16(R.B, ob + 16));
+  }
+  // the slab holding B0's rows: only a split-K chunk's first slab (the host keeps split ≤ the slab depth), loaded
+  // in the prologue; the main-loop loads never take this branch, so their results need no merge (which would wait)
+  if (WITH_B0 && kbase < a.split) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int k = kbase + (t >> 4) + 16 * i;
+      const int o0 = k < kend && n < a.N && k < a.split ? (k * a.ldb + n) * 4 : kOob;
+      const float4 p = __builtin_bit_cast(float4, bload16(R.B0, o0));
+      const float4 q = __builtin_bit_cast(float4, bload16(R.B0, o0 + 16));
+      r.b[i][0] = make_float4(r.b[i][0].x + p.x, r.b[i][0].y + p.y, r.b[i][0].z + p.z, r.b[i][0].w + p.w);
+      r.b[i][1] = make_float4(r.b[i][1].x + q.x, r.b[i][1].y + q.y, r.b[i][1].z + q.z, r.b[i][1].w + q.w);
     }
   }
 }
@@ -215,13 +247,14 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_kernel(Args a) {
   float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   const bool do_cs = a.colsum != nullptr && tn == 0;
   int buf = 0;
+  const Rsrc R = make_rsrc(a, F32 ? 4 : 2);
   if (k_lo < k_hi) {
     if constexpr (F32) {
-      load_stage_f32(a, k_lo, k_hi, m_base, n_base, rf);
+      load_stage_f32<true>(a, R, k_lo, k_hi, m_base, n_base, rf);
       store_stage_f32(SF(0), rf);
       if (do_cs) colsum_acc_f32(cs, rf);
     } else {
-      load_stage(a, k_lo, k_hi, m_base, n_base, ra, rb);
+      load_stage<true>(a, R, k_lo, k_hi, m_base, n_base, ra, rb);
       store_stage(AS(0), BS(0), ra, rb);
       if (do_cs) colsum_acc(cs, ra);
     }
@@ -230,7 +263,7 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_kernel(Args a) {
   for (int kb = k_lo; kb < k_hi; kb += BKx) {
     const bool more = kb + BKx < k_hi;
     if constexpr (F32) {
-      if (more) load_stage_f32(a, kb + BKx, k_hi, m_base, n_base, rf);   // in flight during the MFMAs
+      if (more) load_stage_f32<false>(a, R, kb + BKx, k_hi, m_base, n_base, rf);   // in flight during the MFMAs
       const char* S = SF(buf);
       bf16x8 fah[4], fal[4], fbh[4], fbl[4];
 #pragma unroll
@@ -261,7 +294,7 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_kernel(Args a) {
         if (do_cs) colsum_acc_f32(cs, rf);
       }
     } else {
-      if (more) load_stage(a, kb + BK, k_hi, m_base, n_base, ra, rb);   // in flight during the MFMAs
+      if (more) load_stage<false>(a, R, kb + BK, k_hi, m_base, n_base, ra, rb);   // in flight during the MFMAs
 #pragma unroll
       for (int ks = 0; ks < BK / 32; ++ks) {
         bf16x8 fa[4], fb[4];
@@ -440,6 +473,7 @@ extern "C" void dca_gemm_tn_plan(int M, int N, int K, int* splits, int* kc, int*
 extern "C" hipError_t dca_gemm_tn(const void* A, int lda, const void* B, int ldb, const void* B0, int split_rows,
                                   float* C, int ldc, const int* perm, int accumulate, int M, int N, int K, float* slab,
                                   float* colsum, hipStream_t st, int f32) {
+  if (B0 && split_rows > (f32 ? 32 : BK)) return hipErrorInvalidValue;   // B0 is read by a chunk's first slab only
   int splits, kc, tiles;
   dca_gemm_tn_plan(M, N, K, &splits, &kc, &tiles, f32);
   Args a{A, lda, B, ldb, B0 ? B0 : B, B0 ? split_rows : 0, C, ldc, perm, slab, colsum, M, N, K, kc, splits,

@@ -19,5 +19,11 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None
     M, N = a.shape[1], b.shape[1]
     if out is None:
         out = torch.empty(M if perm is None else int(perm.numel()), N, device=a.device, dtype=torch.float32)
+    if b0 is not None and b0.shape[0] > _B0_MAX_ROWS:
+        # the kernel reads b0 only in a split-K chunk's first K slab (32 rows at fp32); deeper b0: concatenate
+        b, b0 = torch.cat([b0, b]), None
     C.gemm_tn(a, b, out, perm, bool(accumulate), b0, colsum)
     return out
+
+
+_B0_MAX_ROWS = 32   # ops/csrc/gemm_tn.hip: the fp32 K slab depth (bf16: 64)
