@@ -193,8 +193,8 @@ def main():
             'vs_baseline': value / BASELINE_STEPS_PER_S,
             'dtype': args.precision,
             'precision_note': ('fp32 activations, gradients, accumulation and optimizer; hand-written MFMA kernels '
-                               'use bf16x3 split operands (x = hi + lo, ~2^-16 relative per product), plain GEMMs '
-                               'exact fp32 (hipBLASLt)') if args.precision == 'fp32' else
+                               'use bf16x3 split operands (x = hi + lo, ~2^-16 relative per product), plain GEMMs on '
+                               "hipBLASLt's fast fp32 mode (same bf16x3 accuracy class; DCA_F32_GEMM=exact for exact)") if args.precision == 'fp32' else
                               'bf16 GEMM operands and saved activations, fp32 accumulation / recurrence / optimizer',
             'data': 'synthetic (on-HBM replay of synthetic 1v1-mid experience, random-init weights)',
             'config': {'model': f'{args.model} ({cfg.rnn}-{cfg.hidden}, '

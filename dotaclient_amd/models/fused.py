@@ -21,7 +21,8 @@ Precision (``FusedPolicy(precision=...)``):
 * ``'fp32'`` (default; the reference trains in fp32, optimizer.py:281, policy.py:52-78): fp32 activations,
   gradients and accumulation end to end. The hand-written kernels run "bf16x3" — each fp32 MFMA operand split once
   into a hi and a lo bf16, products as hi·hi + lo·hi + hi·lo (≈2⁻¹⁶ relative per product) — and the plain GEMMs
-  run on hipBLASLt's exact-f32 path. The LSTM hidden state is exchanged and stored in fp32.
+  run on hipBLASLt's fast fp32 mode, the same accuracy class (``DCA_F32_GEMM=exact``: its exact-f32 path). The LSTM
+  hidden state is exchanged and stored in fp32.
 * ``'bf16'``: bf16 GEMM operands / saved activations, fp32 accumulation, recurrence state and optimizer.
 
 The 5v5 entity-attention block runs on its bf16 kernels (ops/csrc/attn.hip) in the bf16 learner and as explicit

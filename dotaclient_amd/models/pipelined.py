@@ -25,6 +25,7 @@ chunks), so the default is one chunk.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, List, Optional
 
 import torch
@@ -42,7 +43,8 @@ METRIC_NAMES = ['loss', 'policy_loss', 'entropy_loss', 'advantage_loss', 'entrop
 
 
 def _mm(a, b):
-    """GEMM with fp32 output: bf16 operands on hipBLASLt's bf16 path, fp32 operands on its exact-f32 path."""
+    """GEMM with fp32 output: bf16 operands on hipBLASLt's bf16 path, fp32 operands on its fp32 path (fast bf16x3-class
+    mode inside :func:`fused_step_tm` unless DCA_F32_GEMM=exact)."""
     return a @ b if a.dtype == torch.float32 else torch.mm(a, b, out_dtype=torch.float32)
 
 
@@ -222,8 +224,26 @@ def _attn_demb_f32(dtl, q, dx896, idx, toff, compat: bool):
     return dE1
 
 
-def fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], units_t, env_t, act_t, msk_t, adv_t,
-                  ret_t, lpo_t, nret_t, norms, h0, c0, B: int, S: int, gout: Optional[Dict[str, torch.Tensor]] = None):
+# fp32 learner: hipBLASLt's plain GEMMs (pre-RNN, input projection, heads, the ∂X products) in its fast fp32 mode
+# (``allow_tf32``; on gfx950 a bf16x3-class split product: 4.4e-6 relative error on an 11200×256×2048 product vs
+# 2.9e-7 exact, 58 vs 127 µs), the same accuracy class as the hand-written bf16x3 kernels. DCA_F32_GEMM=exact keeps
+# hipBLASLt's exact-f32 path.
+_F32_GEMM_FAST = os.environ.get('DCA_F32_GEMM', 'fast') != 'exact'
+
+
+def fused_step_tm(fp, *args, **kw):
+    if not (_F32_GEMM_FAST and getattr(fp, 'fp32', False)):
+        return _fused_step_tm(fp, *args, **kw)
+    prev = torch.backends.cuda.matmul.allow_tf32
+    torch.backends.cuda.matmul.allow_tf32 = True
+    try:
+        return _fused_step_tm(fp, *args, **kw)
+    finally:
+        torch.backends.cuda.matmul.allow_tf32 = prev
+
+
+def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], units_t, env_t, act_t, msk_t, adv_t,
+                   ret_t, lpo_t, nret_t, norms, h0, c0, B: int, S: int, gout: Optional[Dict[str, torch.Tensor]] = None):
     """Loss partials and all parameter gradients of one minibatch, from TIME-MAJOR rows (row = t·B + b).
 
     ``W`` = :class:`WeightImages` views, ``P`` = fp32 parameters (for the small fp32 weights used directly).
