@@ -96,7 +96,10 @@ class WeightImages:
         wcat = torch.cat(head_rows + [neg(LDZ - 150, H)], 0)
         parts16 = {'wt16': wt, 'wtT16': wt.transpose(1, 2).contiguous(), 'wpre16': idx('affine_pre_rnn.weight'),
                    'bpre16': idx('affine_pre_rnn.bias'),
-                   'wih16': idx('rnn.weight_ih_l0')[perm], 'whh16': idx('rnn.weight_hh_l0'), 'wcat16': wcat}
+                   'wih16': idx('rnn.weight_ih_l0')[perm], 'whh16': idx('rnn.weight_hh_l0'), 'wcat16': wcat,
+                   # (in, 4H) copy for ∂pre = ∂G·W_ih: hipBLASLt is 1.7x faster with this operand K-contiguous
+                   # (85 vs 141 µs at 11200×2048×256, fast fp32)
+                   'wihT16': idx('rnn.weight_ih_l0')[perm].t().contiguous()}
         head_b = [idx('affine_unit_attention.bias'), idx('affine_head_enum.bias'), idx('affine_move_x.bias'),
                   idx('affine_move_y.bias'), idx('affine_value.bias') if with_value else neg(1)]
         bcat = torch.cat(head_b + [neg(LDZ - 150)])
@@ -399,7 +402,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             gemm_tn(dG16, hs16[0:t1 - 1].view(n - B, H), out=dWhh, perm=gperm, accumulate=True, b0=h016)
         gemm_tn(dG16, x16[r0:r1], out=dWih, perm=gperm, accumulate=True)
         # ∂pre-activation of the pre-RNN layer: one GEMM (bf16 or exact f32), ReLU mask in one threshold_backward
-        dpre16 = torch.ops.aten.threshold_backward(torch.mm(dG16, wih16), x16[r0:r1], 0)
+        dpre16 = torch.ops.aten.threshold_backward(torch.mm(dG16, W['wihT16'].t()), x16[r0:r1], 0)
         gemm_tn(dpre16, x896[r0:r1], out=dWpre, accumulate=True, colsum=dbpre)
         dx896 = _mm(dpre16, wpre16)
         if split is not None:
