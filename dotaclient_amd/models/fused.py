@@ -25,9 +25,9 @@ Precision (``FusedPolicy(precision=...)``):
   hidden state is exchanged and stored in fp32.
 * ``'bf16'``: bf16 GEMM operands / saved activations, fp32 accumulation, recurrence state and optimizer.
 
-The 5v5 entity-attention block runs on its bf16 kernels (ops/csrc/attn.hip) in the bf16 learner and as explicit
-fp32 torch ops with a hand-written backward in the fp32 learner (``models/pipelined.py:_attn_fwd_f32``); the rest
-of the 5v5 step is the same fused pipeline.
+The 5v5 entity-attention block runs on its bf16 kernels (ops/csrc/attn.hip) in the bf16 learner and on its fp32
+(bf16x3 split-MFMA) attention kernels + fp32 GEMMs with a hand-written backward in the fp32 learner
+(``models/pipelined.py:_attn_fwd_f32``); the rest of the 5v5 step is the same fused pipeline.
 """
 from __future__ import annotations
 

@@ -154,41 +154,35 @@ class WeightImages:
 
 
 # ---- fp32 entity-attention block (5v5 at the reference precision) ------------------------------------------------
-# The bf16 learner runs the block on ops/csrc/attn.hip; the fp32 learner runs it as explicit fp32 torch ops with a
-# hand-written backward (no autograd graph: the step stays capturable), between the bf16x3 encoder kernels and the
-# rest of the fused step. Same math as models/policy.py:EntityAttention + the per-type max-pools (pool gradients
-# routed to the first maximal unit — the encoder kernels' convention).
-def _attn_fwd_f32(E0, P, heads: int, eps: float = 1e-5):
+# The bf16 learner runs the block on ops/csrc/attn.hip's bf16 kernels; the fp32 learner runs LayerNorm (ATen), the
+# QKV / out-projection GEMMs (hipBLASLt fp32) and the attention core on attn.hip's fp32 kernels (bf16x3 split MFMA,
+# softmax / LSE in fp32, P never leaves registers), with a hand-written backward (no autograd graph: the step stays
+# capturable), between the bf16x3 encoder kernels and the rest of the fused step. Same math as
+# models/policy.py:EntityAttention + the per-type max-pools (pool gradients routed to the first maximal unit — the
+# encoder kernels' convention).
+def _attn_fwd_f32(E0, P, heads: int, C, eps: float = 1e-5):
     N, U, D = E0.shape
-    d = D // heads
+    assert (U, D, heads) == (64, 128, 4), 'the attention kernels are built for 64 unit slots × 128 wide, 4 heads'
     Xn, mu, rstd = torch.native_layer_norm(E0, (D,), P['entity_attn.ln.weight'], P['entity_attn.ln.bias'], eps)
     qkv = torch.addmm(P['entity_attn.qkv.bias'], Xn.view(N * U, D), P['entity_attn.qkv.weight'].t())
-    q, k, v = qkv.view(N, U, 3, heads, d).permute(2, 0, 3, 1, 4).unbind(0)          # (N, h, U, d)
-    qs = q * (1.0 / float(d) ** 0.5)                  # scale the (small) queries, not the (N, h, U, U) scores
-    att = torch.softmax(torch.matmul(qs, k.transpose(-1, -2)), dim=-1)
-    o = torch.matmul(att, v).transpose(1, 2).reshape(N * U, D)
-    E1 = torch.addmm(P['entity_attn.out.bias'], o, P['entity_attn.out.weight'].t()).view(N, U, D) + E0
-    return E1, (E0, mu, rstd, Xn, qs, k, v, att, o)
+    o, lse = C.attn_fwd(qkv)
+    E1 = torch.addmm(E0.view(N * U, D), o, P['entity_attn.out.weight'].t()).view(N, U, D)
+    E1 += P['entity_attn.out.bias']
+    return E1, (E0, mu, rstd, Xn, qkv, o, lse)
 
 
-def _attn_bwd_f32(saved, dE1, P, heads: int):
-    """Explicit backward: LayerNorm and softmax through their ATen backward kernels (one pass each), the weight
+def _attn_bwd_f32(saved, dE1, P, heads: int, C):
+    """Explicit backward: attention core on the fp32 kernel, LayerNorm through its ATen backward kernel, the weight
     gradients over the N·U unit rows on the split-K TN GEMM (K-outer operands, bias column sums on the way)."""
     from ..ops.gemm import gemm_tn
-    E0, mu, rstd, Xn, qs, k, v, att, o = saved
+    E0, mu, rstd, Xn, qkv, o, lse = saved
     N, U, D = dE1.shape
-    d = D // heads
     g = {}
     dE1f = dE1.reshape(N * U, D)
     g['entity_attn.out.bias'] = torch.empty(D, device=dE1.device)
     g['entity_attn.out.weight'] = gemm_tn(dE1f, o, colsum=g['entity_attn.out.bias'])
-    do = (dE1f @ P['entity_attn.out.weight']).view(N, U, heads, d).transpose(1, 2)   # (N, h, U, d)
-    dv = torch.matmul(att.transpose(-1, -2), do)
-    dp = torch.matmul(do, v.transpose(-1, -2))
-    ds = torch._softmax_backward_data(dp, att, -1, torch.float32)
-    dq = torch.matmul(ds, k) * (1.0 / float(d) ** 0.5)
-    dk = torch.matmul(ds.transpose(-1, -2), qs)
-    dqkv = torch.stack([dq, dk, dv], 0).permute(1, 3, 0, 2, 4).reshape(N * U, 3 * D)
+    do = dE1f @ P['entity_attn.out.weight']
+    dqkv = C.attn_bwd(qkv, o, do, lse)
     g['entity_attn.qkv.bias'] = torch.empty(3 * D, device=dE1.device)
     g['entity_attn.qkv.weight'] = gemm_tn(dqkv, Xn.view(N * U, D), colsum=g['entity_attn.qkv.bias'])
     dXn = (dqkv @ P['entity_attn.qkv.weight']).view(N, U, D)
@@ -276,9 +270,9 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs))
     attn32 = attn and f32
     if attn32:
-        # fp32 entity attention as explicit torch ops (bt is NOT folded with b_out in the fp32 images)
+        # fp32 entity attention: fp32 attention kernels + hipBLASLt fp32 GEMMs (bt is NOT folded with b_out here)
         toff = fp.type_offset_list()
-        E1, attn_saved = _attn_fwd_f32(emb.view(N, U, 128), P, cfg.attention_heads)
+        E1, attn_saved = _attn_fwd_f32(emb.view(N, U, 128), P, cfg.attention_heads, C)
         pool_idx = _attn_pools_f32(E1, toff, x896, bool(cfg.compat_bugs))
         emb = E1
     elif attn:
@@ -419,7 +413,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         demb_in = None
         if attn32:
             dE1 = _attn_demb_f32(dtl, z[:, :128], dx896, pool_idx, toff, bool(cfg.compat_bugs))
-            dE0, agr = _attn_bwd_f32(attn_saved, dE1, P, cfg.attention_heads)
+            dE0, agr = _attn_bwd_f32(attn_saved, dE1, P, cfg.attention_heads, C)
             demb_in = dE0.contiguous()
             dbt_attn = torch.stack([dE0[:, toff[t]:toff[t + 1]].sum((0, 1)) for t in range(6)])
             dgam, dbet = agr['entity_attn.ln.weight'], agr['entity_attn.ln.bias']

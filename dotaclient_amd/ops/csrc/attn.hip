@@ -424,7 +424,271 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
   if (ph == 0 && c < W) out[c] = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
 }
 
+// ============================================================================================================
+// fp32 (reference-precision) attention core for the fp32 learner: same math as attn_fwd/bwd_kernel over fp32
+// qkv / o / ∂O, every product a bf16x3 split MFMA (x = hi + lo, hi·hi + hi·lo + lo·hi, fp32 accumulation; ≈2⁻¹⁶
+// relative per product), softmax and LSE in fp32. Replaces the explicit torch ops whose (N, 4, 64, 64) fp32
+// probability tensor (0.73 GB at N = 11 200) was written once and re-read three times per step.
+//
+// Register-resident layout (no LDS in the forward): Sᵀ = K·Qᵀ comes out of the 16x16x32 MFMA with lane
+// (j = 16b + 4kg + r, i = 16a + li), which is EXACTLY the A-operand layout of a 16x16x16 MFMA contracting over j
+// (A[m = i][k = j]: m = lane&15, k = 4(lane>>4) + r) — so O = P·V takes P straight from the score registers. The
+// backward keeps the i-major S = Q·Kᵀ layout instead (lane (i = 16a + 4kg + r, j = 16b + li) = A[m = j][k = i]) for
+// ∂V = Pᵀ∂O and ∂K = ∂Sᵀ Q, and passes ∂S through LDS (hi / lo images, transposed reads) only for ∂Q = ∂S K.
+__device__ __forceinline__ void split8(const float* __restrict__ p, bf16x8& hi, bf16x8& lo) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    hi[j] = dca::f2bf(v[j]);
+    lo[j] = dca::f2bf(v[j] - dca::bf2f(hi[j]));
+  }
+}
+__device__ __forceinline__ void split4(const float v0, const float v1, const float v2, const float v3, bf16x4v& hi,
+                                       bf16x4v& lo) {
+  const float v[4] = {v0, v1, v2, v3};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    hi[j] = dca::f2bf(v[j]);
+    lo[j] = dca::f2bf(v[j] - dca::bf2f(hi[j]));
+  }
+}
+// bf16x3 products: 16x16x32 (A, B = 8-element fragments) and 16x16x16 (4-element fragments)
+__device__ __forceinline__ f32x4 mfma3(const bf16x8& ah, const bf16x8& al, const bf16x8& bh, const bf16x8& bl,
+                                       f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bl, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bh, c, 0, 0, 0);
+}
+__device__ __forceinline__ f32x4 mfma3k16(const bf16x4v& ah, const bf16x4v& al, const bf16x4v& bh,
+                                          const bf16x4v& bl, f32x4 c) {
+  c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(al, bh, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bl, c, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(ah, bh, c, 0, 0, 0);
+}
+
+// Forward, one wave per (row n, head h) = blockIdx.x · 4 + h. qkv (N·64, 384) f32 → o (N·64, 128) f32, lse (N,4,64).
+__global__ __launch_bounds__(64) void attn_fwd_f32_kernel(const float* __restrict__ qkv, float* __restrict__ o,
+                                                          float* __restrict__ lse, float scale) {
+  const int n = blockIdx.x >> 2, h = blockIdx.x & 3;
+  const int l = threadIdx.x, kg = l >> 4, li = l & 15;
+  const float* base = qkv + (size_t)n * kU * 384 + h * kHd;
+  // V operand of O = P·V (B[k = j][n = d]): lane needs V[16b + 4kg + r][16c + li] — issued first, used last
+  float vr[4][2][4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) vr[b][c][r] = base[(size_t)(16 * b + 4 * kg + r) * 384 + 256 + 16 * c + li];
+  bf16x8 qh[4], ql[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) split8(base + (size_t)(16 * a + li) * 384 + 8 * kg, qh[a], ql[a]);
+  // Sᵀ tiles: s[b][a] lane (key j = 16b + 4kg + r, query i = 16a + li)
+  f32x4 s[4][4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) {
+    bf16x8 kh, kl;
+    split8(base + 128 + (size_t)(16 * b + li) * 384 + 8 * kg, kh, kl);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) s[b][a] = mfma3(kh, kl, qh[a], ql[a], f32x4{0.f, 0.f, 0.f, 0.f});
+  }
+  // softmax over the keys of query i = 16a + li: in-lane over (b, r), then across the 4 lane groups (xor 16, 32)
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) m = fmaxf(m, s[b][a][r]);
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    m *= scale;
+    float sum = 0.f;
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = __expf(s[b][a][r] * scale - m);
+        s[b][a][r] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = 1.f / sum;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) s[b][a] *= inv;
+    if (kg == 0) lse[((size_t)n * 4 + h) * kU + 16 * a + li] = m + __logf(sum);
+  }
+  // O = P·V on 16x16x16: A[m = i][k = j] = s[b][a] as is, B[k = j][n = d] = vr[b][c]
+  bf16x4v vh[4][2], vl[4][2];
+#pragma unroll
+  for (int b = 0; b < 4; ++b)
+#pragma unroll
+    for (int c = 0; c < 2; ++c) split4(vr[b][c][0], vr[b][c][1], vr[b][c][2], vr[b][c][3], vh[b][c], vl[b][c]);
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    bf16x4v ph[4], pl[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) split4(s[b][a][0], s[b][a][1], s[b][a][2], s[b][a][3], ph[b], pl[b]);
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int b = 0; b < 4; ++b) acc = mfma3k16(ph[b], pl[b], vh[b][c], vl[b][c], acc);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[((size_t)n * kU + 16 * a + 4 * kg + r) * kD + h * kHd + 16 * c + li] = acc[r];
+    }
+  }
+}
+
+// Backward, one wave per (row, head). do_ (N·64, 128) f32 = ∂O; writes dqkv (N·64, 384) f32.
+__global__ __launch_bounds__(64) void attn_bwd_f32_kernel(const float* __restrict__ qkv, const float* __restrict__ o,
+                                                          const float* __restrict__ do_, const float* __restrict__ lse,
+                                                          float* __restrict__ dqkv, float scale) {
+  __shared__ __attribute__((aligned(16))) short STh[kU * kP64], STl[kU * kP64];   // (scale·∂S)ᵀ hi / lo, [j][i]
+  __shared__ float Dl[kU], Ll[kU];
+  const int n = blockIdx.x >> 2, h = blockIdx.x & 3;
+  const int l = threadIdx.x, kg = l >> 4, li = l & 15;
+  const float* base = qkv + (size_t)n * kU * 384 + h * kHd;
+  const float* dob = do_ + (size_t)n * kU * kD + h * kHd;
+  const float* ob = o + (size_t)n * kU * kD + h * kHd;
+  // D_i = Σ_d ∂O[i][d]·O[i][d] for i = 16a + li (lane group kg sums d = 8kg … 8kg + 7), LSE
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const float* orow = ob + (size_t)(16 * a + li) * kD + 8 * kg;
+    const float* drow = dob + (size_t)(16 * a + li) * kD + 8 * kg;
+    const float4 o0 = *reinterpret_cast<const float4*>(orow), o1 = *reinterpret_cast<const float4*>(orow + 4);
+    const float4 d0 = *reinterpret_cast<const float4*>(drow), d1 = *reinterpret_cast<const float4*>(drow + 4);
+    float d = o0.x * d0.x + o0.y * d0.y + o0.z * d0.z + o0.w * d0.w + o1.x * d1.x + o1.y * d1.y + o1.z * d1.z +
+              o1.w * d1.w;
+    d += __shfl_xor(d, 16, 64);
+    d += __shfl_xor(d, 32, 64);
+    if (kg == 0) Dl[16 * a + li] = d;
+  }
+  Ll[l] = lse[((size_t)n * 4 + h) * kU + l];
+  // S = Q Kᵀ and dP = ∂O Vᵀ, i-major: p[a][b] lane (query i = 16a + 4kg + r, key j = 16b + li)
+  f32x4 p[4][4], dp[4][4];
+  {
+    bf16x8 qh[4], ql[4], dh[4], dl[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      split8(base + (size_t)(16 * a + li) * 384 + 8 * kg, qh[a], ql[a]);
+      split8(dob + (size_t)(16 * a + li) * kD + 8 * kg, dh[a], dl[a]);
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      bf16x8 kh, kl, vh, vl;
+      split8(base + 128 + (size_t)(16 * b + li) * 384 + 8 * kg, kh, kl);
+      split8(base + 256 + (size_t)(16 * b + li) * 384 + 8 * kg, vh, vl);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        p[a][b] = mfma3(qh[a], ql[a], kh, kl, f32x4{0.f, 0.f, 0.f, 0.f});
+        dp[a][b] = mfma3(dh[a], dl[a], vh, vl, f32x4{0.f, 0.f, 0.f, 0.f});
+      }
+    }
+  }
+  __syncthreads();
+  // P = exp(scale·S − LSE); dp ← scale·P∘(dP − D) (= ∂L/∂S_raw); (scale·∂S)ᵀ hi/lo images for ∂Q
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int i = 16 * a + 4 * kg + r;
+      const float L = Ll[i], D = Dl[i];
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const float pr = __expf(p[a][b][r] * scale - L);
+        p[a][b][r] = pr;
+        dp[a][b][r] = scale * pr * (dp[a][b][r] - D);
+      }
+    }
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      bf16x4v sh, sl;
+      split4(dp[a][b][0], dp[a][b][1], dp[a][b][2], dp[a][b][3], sh, sl);
+      *reinterpret_cast<bf16x4v*>(STh + (16 * b + li) * kP64 + 16 * a + 4 * kg) = sh;
+      *reinterpret_cast<bf16x4v*>(STl + (16 * b + li) * kP64 + 16 * a + 4 * kg) = sl;
+    }
+  float* out = dqkv + (size_t)n * kU * 384 + h * kHd;
+  // ∂V = Pᵀ∂O and ∂K = ∂Sᵀ Q on 16x16x16: A[m = j][k = i] = p / dp registers (k-chunk a), B[k = i][n = d] = rows
+  // 16a + 4kg + r of ∂O / Q at column 16c + li
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    bf16x4v doh[4], dol[4], qh[4], ql[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      float dv[4], qv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        dv[r] = dob[(size_t)(16 * a + 4 * kg + r) * kD + 16 * c + li];
+        qv[r] = base[(size_t)(16 * a + 4 * kg + r) * 384 + 16 * c + li];
+      }
+      split4(dv[0], dv[1], dv[2], dv[3], doh[a], dol[a]);
+      split4(qv[0], qv[1], qv[2], qv[3], qh[a], ql[a]);
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      f32x4 av = {0.f, 0.f, 0.f, 0.f}, ak = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        bf16x4v ph, pl, sh, sl;
+        split4(p[a][b][0], p[a][b][1], p[a][b][2], p[a][b][3], ph, pl);
+        split4(dp[a][b][0], dp[a][b][1], dp[a][b][2], dp[a][b][3], sh, sl);
+        av = mfma3k16(ph, pl, doh[a], dol[a], av);
+        ak = mfma3k16(sh, sl, qh[a], ql[a], ak);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const size_t j = 16 * b + 4 * kg + r;
+        out[j * 384 + 256 + 16 * c + li] = av[r];
+        out[j * 384 + 128 + 16 * c + li] = ak[r];
+      }
+    }
+  }
+  __syncthreads();
+  // ∂Q = ∂S K on 16x16x32: A[m = i][k = j] = transposed reads of the ∂Sᵀ images, B[k = j][n = d] = K rows
+  // 32ks + 8kg … +7 at column 16c + li
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    bf16x8 kh[2], kl[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const float v = base[(size_t)(32 * ks + 8 * kg + jj) * 384 + 128 + 16 * c + li];
+        kh[ks][jj] = dca::f2bf(v);
+        kl[ks][jj] = dca::f2bf(v - dca::bf2f(kh[ks][jj]));
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      f32x4 aq = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        aq = mfma3(frag_tr(STh, kP64, 32 * ks, 16 * a), frag_tr(STl, kP64, 32 * ks, 16 * a), kh[ks], kl[ks], aq);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) out[(size_t)(16 * a + 4 * kg + r) * 384 + 16 * c + li] = aq[r];
+    }
+  }
+}
+
 }  // namespace
+
+extern "C" hipError_t dca_attn_fwd_f32(const float* qkv, float* o, float* lse, int N, float scale, hipStream_t st) {
+  hipLaunchKernelGGL(attn_fwd_f32_kernel, dim3(N * 4), dim3(64), 0, st, qkv, o, lse, scale);
+  DCA_CHECK_LAUNCH();
+  return hipSuccess;
+}
+
+extern "C" hipError_t dca_attn_bwd_f32(const float* qkv, const float* o, const float* dout, const float* lse,
+                                       float* dqkv, int N, float scale, hipStream_t st) {
+  hipLaunchKernelGGL(attn_bwd_f32_kernel, dim3(N * 4), dim3(64), 0, st, qkv, o, dout, lse, dqkv, scale);
+  DCA_CHECK_LAUNCH();
+  return hipSuccess;
+}
 
 extern "C" int dca_ln_part_width() { return kLnPart; }
 

@@ -594,23 +594,37 @@ std::vector<torch::Tensor> ln_fwd(torch::Tensor e0, torch::Tensor bsub, torch::T
 }
 
 std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv) {
-  CHECK_BF16(qkv);
   TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) == 384 && qkv.size(0) % 64 == 0, "qkv must be (N*64, 384)");
   const int N = qkv.size(0) / 64;
   auto o = torch::empty({(int64_t)N * 64, 128}, qkv.options());
   auto lse = torch::empty({(int64_t)N, 4, 64}, qkv.options().dtype(at::kFloat));
+  if (qkv.scalar_type() == at::kFloat) {   // fp32 learner: bf16x3 split-MFMA kernel
+    CHECK_F32(qkv);
+    hip_check(dca_attn_fwd_f32(ptr<float>(qkv), ptr<float>(o), ptr<float>(lse), N, 1.f / sqrtf(32.f), cur_stream()),
+              "dca_attn_fwd_f32");
+    return {o, lse};
+  }
+  CHECK_BF16(qkv);
   hip_check(dca_attn_fwd(ptr<short>(qkv), ptr<short>(o), ptr<float>(lse), N, 1.f / sqrtf(32.f), cur_stream()),
             "dca_attn_fwd");
   return {o, lse};
 }
 
 torch::Tensor attn_bwd(torch::Tensor qkv, torch::Tensor o, torch::Tensor dout, torch::Tensor lse) {
-  CHECK_BF16(qkv); CHECK_BF16(o); CHECK_BF16(dout); CHECK_F32(lse);
+  CHECK_F32(lse);
   TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) == 384 && qkv.size(0) % 64 == 0, "qkv must be (N*64, 384)");
   const int N = qkv.size(0) / 64;
   TORCH_CHECK(o.numel() == (int64_t)N * 64 * 128 && dout.numel() == o.numel() && lse.numel() == (int64_t)N * 256,
               "attn_bwd shapes");
   auto dqkv = torch::empty_like(qkv);
+  if (qkv.scalar_type() == at::kFloat) {
+    CHECK_F32(qkv); CHECK_F32(o); CHECK_F32(dout);
+    hip_check(dca_attn_bwd_f32(ptr<float>(qkv), ptr<float>(o), ptr<float>(dout), ptr<float>(lse), ptr<float>(dqkv), N,
+                               1.f / sqrtf(32.f), cur_stream()),
+              "dca_attn_bwd_f32");
+    return dqkv;
+  }
+  CHECK_BF16(qkv); CHECK_BF16(o); CHECK_BF16(dout);
   hip_check(dca_attn_bwd(ptr<short>(qkv), ptr<short>(o), ptr<short>(dout), ptr<float>(lse), ptr<short>(dqkv), N,
                          1.f / sqrtf(32.f), cur_stream()),
             "dca_attn_bwd");
@@ -763,7 +777,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("B0") = py::none(), py::arg("colsum") = py::none());
   m.def("enc_small_grads", &enc_small_grads, "entity-encoder type-bias and env-layer gradients in one pass");
   m.def("ln_fwd", &ln_fwd, "LayerNorm(E0 - bsub) -> (xn bf16, mean, rstd)");
-  m.def("attn_fwd", &attn_fwd, "entity self-attention per (row, head): (o bf16, lse)");
+  m.def("attn_fwd", &attn_fwd, "entity self-attention per (row, head): (o, lse); bf16, or fp32 (bf16x3 MFMA)");
   m.def("attn_bwd", &attn_bwd, "entity self-attention backward: dqkv");
   m.def("attn_pool", &attn_pool, "per-type max-pool + argmax of attended embeddings into x896");
   m.def("attn_demb", &attn_demb, "dE1 = dtl*q + pool gradient at the argmax unit");

@@ -88,6 +88,9 @@ int dca_ln_part_width();
 hipError_t dca_ln_fwd(const short* e0, const float* bsub, const float* gamma, const float* beta, short* xn, float* mean,
                       float* rstd, int R, float eps, hipStream_t st);
 hipError_t dca_attn_fwd(const short* qkv, short* o, float* lse, int N, float scale, hipStream_t st);
+hipError_t dca_attn_fwd_f32(const float* qkv, float* o, float* lse, int N, float scale, hipStream_t st);
+hipError_t dca_attn_bwd_f32(const float* qkv, const float* o, const float* dout, const float* lse, float* dqkv, int N,
+                            float scale, hipStream_t st);
 hipError_t dca_attn_bwd(const short* qkv, const short* o, const short* dout, const float* lse, short* dqkv, int N,
                         float scale, hipStream_t st);
 hipError_t dca_attn_pool(const short* e1, const int* type_off, short* x896, unsigned char* arg, int N, int compat,

@@ -59,6 +59,28 @@ def test_attn_fwd_bwd(gpu_ops):
         assert (a - b).norm() / b.norm() < 3e-2, part
 
 
+def test_attn_fwd_bwd_f32(gpu_ops):
+    """fp32 attention core (bf16x3 split MFMA, fp32 softmax) vs an fp64 reference: fp32-class accuracy."""
+    g = _g(2)
+    qkv = torch.randn(N * U, 3 * D, device='cuda', generator=g) * 1.5       # peaky rows as well as flat ones
+    o, lse = gpu_ops.attn_fwd(qkv)
+    assert o.dtype == torch.float32
+    x = qkv.double().requires_grad_(True)
+    q, k, v = x.view(N, U, 3, NH, HD).unbind(2)
+    q, k, v = (t.transpose(1, 2) for t in (q, k, v))
+    s = q @ k.transpose(-1, -2) / HD ** 0.5
+    o_ref = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(N * U, D)
+    rel = lambda a, b: float((a.double() - b).norm() / b.norm())   # noqa: E731
+    assert rel(o, o_ref.detach()) < 2e-5
+    torch.testing.assert_close(lse.double(), torch.logsumexp(s, -1).detach(), rtol=1e-5, atol=1e-5)
+    dout = torch.randn(N * U, D, device='cuda', generator=g)
+    dqkv = gpu_ops.attn_bwd(qkv, o, dout, lse)
+    o_ref.backward(dout.double())
+    for part in range(3):   # q, k, v blocks each
+        a, b = dqkv[:, part * D:(part + 1) * D], x.grad[:, part * D:(part + 1) * D]
+        assert rel(a, b) < 5e-5, (part, rel(a, b))
+
+
 @pytest.mark.parametrize('compat', [False, True])
 def test_pool_and_demb(gpu_ops, compat):
     g = _g(2)
