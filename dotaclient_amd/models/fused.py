@@ -26,8 +26,8 @@ Precision (``FusedPolicy(precision=...)``):
 * ``'bf16'``: bf16 GEMM operands / saved activations, fp32 accumulation, recurrence state and optimizer.
 
 The 5v5 entity-attention block runs on its bf16 kernels (ops/csrc/attn.hip) in the bf16 learner and on its fp32
-(bf16x3 split-MFMA) attention kernels + fp32 GEMMs with a hand-written backward in the fp32 learner
-(``models/pipelined.py:_attn_fwd_f32``); the rest of the 5v5 step is the same fused pipeline.
+(bf16x3 split-MFMA) attention core, fp32 LayerNorm / pool kernels and hipBLASLt fp32 GEMMs in the fp32 learner
+(``models/pipelined.py:_fused_step_tm``); the rest of the 5v5 step is the same fused pipeline.
 """
 from __future__ import annotations
 
@@ -402,6 +402,13 @@ class FusedPolicy:
             offs = [0] + list(itertools.accumulate(self.cfg.layout.counts))
             self._toff, self._toff_key = torch.tensor(offs, dtype=torch.int32, device=device), key
         return self._toff
+
+    def no_bias(self, device):
+        """Empty f32 device tensor: "no b_sub" for the fp32 LayerNorm kernels (bt is not folded with b_out there)."""
+        key = str(device)
+        if getattr(self, '_nob_key', None) != key:
+            self._nob, self._nob_key = torch.empty(0, device=device), key
+        return self._nob
 
     def unit_types(self, device):
         """(U,) uint8 device tensor: unit slot → unit type index, cached."""

@@ -153,74 +153,6 @@ class WeightImages:
         return self.views
 
 
-# ---- fp32 entity-attention block (5v5 at the reference precision) ------------------------------------------------
-# The bf16 learner runs the block on ops/csrc/attn.hip's bf16 kernels; the fp32 learner runs LayerNorm (ATen), the
-# QKV / out-projection GEMMs (hipBLASLt fp32) and the attention core on attn.hip's fp32 kernels (bf16x3 split MFMA,
-# softmax / LSE in fp32, P never leaves registers), with a hand-written backward (no autograd graph: the step stays
-# capturable), between the bf16x3 encoder kernels and the rest of the fused step. Same math as
-# models/policy.py:EntityAttention + the per-type max-pools (pool gradients routed to the first maximal unit — the
-# encoder kernels' convention).
-def _attn_fwd_f32(E0, P, heads: int, C, eps: float = 1e-5):
-    N, U, D = E0.shape
-    assert (U, D, heads) == (64, 128, 4), 'the attention kernels are built for 64 unit slots × 128 wide, 4 heads'
-    Xn, mu, rstd = torch.native_layer_norm(E0, (D,), P['entity_attn.ln.weight'], P['entity_attn.ln.bias'], eps)
-    qkv = torch.addmm(P['entity_attn.qkv.bias'], Xn.view(N * U, D), P['entity_attn.qkv.weight'].t())
-    o, lse = C.attn_fwd(qkv)
-    E1 = torch.addmm(E0.view(N * U, D), o, P['entity_attn.out.weight'].t()).view(N, U, D)
-    E1 += P['entity_attn.out.bias']
-    return E1, (E0, mu, rstd, Xn, qkv, o, lse)
-
-
-def _attn_bwd_f32(saved, dE1, P, heads: int, C):
-    """Explicit backward: attention core on the fp32 kernel, LayerNorm through its ATen backward kernel, the weight
-    gradients over the N·U unit rows on the split-K TN GEMM (K-outer operands, bias column sums on the way)."""
-    from ..ops.gemm import gemm_tn
-    E0, mu, rstd, Xn, qkv, o, lse = saved
-    N, U, D = dE1.shape
-    g = {}
-    dE1f = dE1.reshape(N * U, D)
-    g['entity_attn.out.bias'] = torch.empty(D, device=dE1.device)
-    g['entity_attn.out.weight'] = gemm_tn(dE1f, o, colsum=g['entity_attn.out.bias'])
-    do = dE1f @ P['entity_attn.out.weight']
-    dqkv = C.attn_bwd(qkv, o, do, lse)
-    g['entity_attn.qkv.bias'] = torch.empty(3 * D, device=dE1.device)
-    g['entity_attn.qkv.weight'] = gemm_tn(dqkv, Xn.view(N * U, D), colsum=g['entity_attn.qkv.bias'])
-    dXn = (dqkv @ P['entity_attn.qkv.weight']).view(N, U, D)
-    dE0_ln, g['entity_attn.ln.weight'], g['entity_attn.ln.bias'] = torch.ops.aten.native_layer_norm_backward(
-        dXn, E0, (D,), mu, rstd, P['entity_attn.ln.weight'], P['entity_attn.ln.bias'], [True, True, True])
-    return dE1 + dE0_ln, g
-
-
-def _attn_pools_f32(E1, toff, x896, compat: bool):
-    """x896[:, 128:] = per-type max over the attended embeddings; returns each type's argmax (N, 128)."""
-    idx = []
-    for t in range(6):
-        o0, o1 = toff[t], toff[t + 1]
-        if compat and t == 5:      # reference policy.py:127: the enemy-tower pool is the enemy-nonhero pool
-            o0, o1 = toff[3], toff[4]
-        if o1 > o0:
-            seg = E1[:, o0:o1]
-            a = seg.argmax(1)
-            x896[:, 128 * (t + 1):128 * (t + 2)] = seg.gather(1, a.unsqueeze(1)).squeeze(1)
-        else:
-            a = None
-            x896[:, 128 * (t + 1):128 * (t + 2)] = 0.
-        idx.append(a)
-    return idx
-
-
-def _attn_demb_f32(dtl, q, dx896, idx, toff, compat: bool):
-    """∂E1 = dtl ⊗ q (pointer logits) + each type's pool gradient at its argmax unit."""
-    dE1 = dtl.unsqueeze(-1) * q.unsqueeze(1)
-    for t in range(6):
-        a = idx[t]
-        if a is None:
-            continue
-        o0, o1 = (toff[3], toff[4]) if (compat and t == 5) else (toff[t], toff[t + 1])
-        dE1[:, o0:o1].scatter_add_(1, a.unsqueeze(1), dx896[:, 128 * (t + 1):128 * (t + 2)].unsqueeze(1))
-    return dE1
-
-
 # fp32 learner: hipBLASLt's plain GEMMs (pre-RNN, input projection, heads, the ∂X products) in its fast fp32 mode
 # (``allow_tf32``; on gfx950 a bf16x3-class split product: 4.4e-6 relative error on an 11200×256×2048 product vs
 # 2.9e-7 exact, 58 vs 127 µs), the same accuracy class as the hand-written bf16x3 kernels. DCA_F32_GEMM=exact keeps
@@ -270,11 +202,17 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs))
     attn32 = attn and f32
     if attn32:
-        # fp32 entity attention: fp32 attention kernels + hipBLASLt fp32 GEMMs (bt is NOT folded with b_out here)
+        # 5v5 entity attention at fp32 (ops/csrc/attn.hip fp32 kernels: LayerNorm, bf16x3 attention core, pools; the
+        # QKV / out-projection GEMMs on hipBLASLt fp32). bt is NOT folded with b_out in the fp32 images: b_sub = none
         toff = fp.type_offset_list()
-        E1, attn_saved = _attn_fwd_f32(emb.view(N, U, 128), P, cfg.attention_heads, C)
-        pool_idx = _attn_pools_f32(E1, toff, x896, bool(cfg.compat_bugs))
-        emb = E1
+        E0p = emb.view(N * U, 128)
+        Xn, ln_mu, ln_rs = C.ln_fwd(E0p, fp.no_bias(dev), P['entity_attn.ln.weight'], P['entity_attn.ln.bias'], 1e-5)
+        QKV = torch.addmm(P['entity_attn.qkv.bias'], Xn, P['entity_attn.qkv.weight'].t())
+        Oat, lse = C.attn_fwd(QKV)
+        E1 = torch.addmm(E0p, Oat, P['entity_attn.out.weight'].t())        # residual + out-projection
+        E1 += P['entity_attn.out.bias']
+        arg = C.attn_pool(E1, toff, x896, bool(cfg.compat_bugs))            # pools of the attended embeddings
+        emb = E1.view(N, U, 128)
     elif attn:
         # 5v5 entity attention (ops/csrc/attn.hip): emb = E0 + b_out here (bias folded into bt)
         toff = fp.type_offset_list()
@@ -412,17 +350,20 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             split = None
         demb_in = None
         if attn32:
-            dE1 = _attn_demb_f32(dtl, z[:, :128], dx896, pool_idx, toff, bool(cfg.compat_bugs))
-            dE0, agr = _attn_bwd_f32(attn_saved, dE1, P, cfg.attention_heads, C)
-            demb_in = dE0.contiguous()
-            dbt_attn = torch.stack([dE0[:, toff[t]:toff[t + 1]].sum((0, 1)) for t in range(6)])
-            dgam, dbet = agr['entity_attn.ln.weight'], agr['entity_attn.ln.bias']
-            dWqkv, dbqkv = agr['entity_attn.qkv.weight'], agr['entity_attn.qkv.bias']
-            dWout, dbout = agr['entity_attn.out.weight'], agr['entity_attn.out.bias']
+            dE1 = C.attn_demb(dtl, z, dx896, arg, toff, bool(cfg.compat_bugs), True)
+            dbout = torch.empty(128, device=dev)
+            dWout = gemm_tn(dE1, Oat, colsum=dbout)
+            dO = dE1 @ P['entity_attn.out.weight']
+            dQKV = C.attn_bwd(QKV, Oat, dO, lse)
+            dbqkv = torch.empty(384, device=dev)
+            dWqkv = gemm_tn(dQKV, Xn, colsum=dbqkv)
+            dXn = dQKV @ P['entity_attn.qkv.weight']
+            demb_in, dgam, dbet, dbt_attn = C.ln_bwd(dXn, E0p, fp.no_bias(dev), P['entity_attn.ln.weight'], ln_mu,
+                                                     ln_rs, dE1, fp.unit_types(dev))
         elif attn:
             # attention block backward over this chunk's rows (unit rows r0·U … r1·U)
             a0, a1 = r0 * U, r1 * U
-            dE1 = C.attn_demb(dtl[r0:r1], z[r0:r1], dx896, arg[r0:r1], toff, bool(cfg.compat_bugs))
+            dE1 = C.attn_demb(dtl[r0:r1], z[r0:r1], dx896, arg[r0:r1], toff, bool(cfg.compat_bugs), False)
             gemm_tn(dE1, Oat[a0:a1], out=dWout, accumulate=not first_attn, colsum=dbout)
             dO = torch.mm(dE1, W['wout16'])
             dQKV = C.attn_bwd(QKV[a0:a1], Oat[a0:a1], dO, lse[r0:r1])

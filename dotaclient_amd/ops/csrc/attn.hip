@@ -71,19 +71,46 @@ __device__ __forceinline__ void stage64x32(short* img, const short* __restrict__
   }
 }
 
+// element access for the kernels templated on the activation type (bf16 learner: short, fp32 learner: float)
+__device__ __forceinline__ float ldf(short v) { return dca::bf2f(v); }
+__device__ __forceinline__ float ldf(float v) { return v; }
+__device__ __forceinline__ void stf(short* p, float v) { *p = dca::f2bf(v); }
+__device__ __forceinline__ void stf(float* p, float v) { *p = v; }
+__device__ __forceinline__ void ld8(const short* p, float* x) {
+  const bf16x8 v = *reinterpret_cast<const bf16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) x[j] = dca::bf2f(v[j]);
+}
+__device__ __forceinline__ void ld8(const float* p, float* x) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  x[0] = a.x; x[1] = a.y; x[2] = a.z; x[3] = a.w; x[4] = b.x; x[5] = b.y; x[6] = b.z; x[7] = b.w;
+}
+__device__ __forceinline__ void st8(short* p, const float* x) {
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = dca::f2bf(x[j]);
+  *reinterpret_cast<bf16x8*>(p) = o;
+}
+__device__ __forceinline__ void st8(float* p, const float* x) {
+  *reinterpret_cast<float4*>(p) = make_float4(x[0], x[1], x[2], x[3]);
+  *reinterpret_cast<float4*>(p + 4) = make_float4(x[4], x[5], x[6], x[7]);
+}
+
 // ============================================================================================================
-// LayerNorm forward: x = E0' − b_sub (E0' carries b_out, folded into the encoder's type bias), 16 lanes × 8 columns.
-__global__ __launch_bounds__(256) void ln_fwd_kernel(const short* __restrict__ e0, const float* __restrict__ bsub,
+// LayerNorm forward: x = E0' − b_sub (bf16 learner: E0' carries b_out, folded into the encoder's type bias; fp32
+// learner: b_sub = null), 16 lanes × 8 columns.
+template <typename T>
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ e0, const float* __restrict__ bsub,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
-                                                     short* __restrict__ xn, float* __restrict__ mean,
+                                                     T* __restrict__ xn, float* __restrict__ mean,
                                                      float* __restrict__ rstd, int R, float eps) {
   const int row = blockIdx.x * 16 + (threadIdx.x >> 4), c0 = (threadIdx.x & 15) * 8;
   if (row >= R) return;
-  const bf16x8 v = *reinterpret_cast<const bf16x8*>(e0 + (size_t)row * kD + c0);
   float x[8], s = 0.f;
+  ld8(e0 + (size_t)row * kD + c0, x);
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    x[j] = dca::bf2f(v[j]) - bsub[c0 + j];
+    if (bsub) x[j] -= bsub[c0 + j];
     s += x[j];
   }
   s = dca::group_sum<16>(s);
@@ -96,10 +123,9 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const short* __restrict__ e
   }
   q = dca::group_sum<16>(q);
   const float rs = rsqrtf(q * (1.f / kD) + eps);
-  bf16x8 o;
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = dca::f2bf(x[j] * rs * gamma[c0 + j] + beta[c0 + j]);
-  *reinterpret_cast<bf16x8*>(xn + (size_t)row * kD + c0) = o;
+  for (int j = 0; j < 8; ++j) x[j] = x[j] * rs * gamma[c0 + j] + beta[c0 + j];
+  st8(xn + (size_t)row * kD + c0, x);
   if ((threadIdx.x & 15) == 0) {
     mean[row] = mu;
     rstd[row] = rs;
@@ -282,32 +308,34 @@ struct TypeOff {
   int off[7];
 };
 
-__global__ __launch_bounds__(128) void pool_kernel(const short* __restrict__ e1, TypeOff T, short* __restrict__ x896,
+template <typename E>
+__global__ __launch_bounds__(128) void pool_kernel(const E* __restrict__ e1, TypeOff T, E* __restrict__ x896,
                                                    unsigned char* __restrict__ arg, int compat) {
   const int n = blockIdx.x, c = threadIdx.x;
-  const short* rowp = e1 + (size_t)n * kU * kD + c;
+  const E* rowp = e1 + (size_t)n * kU * kD + c;
 #pragma unroll
   for (int t = 0; t < 6; ++t) {
     const int src = (compat && t == 5) ? 3 : t;
     float m = -INFINITY;
     int am = 0;
     for (int u = T.off[src]; u < T.off[src + 1]; ++u) {
-      const float v = dca::bf2f(rowp[(size_t)u * kD]);
+      const float v = ldf(rowp[(size_t)u * kD]);
       if (v > m) {
         m = v;
         am = u - T.off[src];
       }
     }
-    x896[(size_t)n * 896 + kD + t * kD + c] = dca::f2bf(m);
+    stf(x896 + (size_t)n * 896 + kD + t * kD + c, m);
     arg[((size_t)n * 6 + t) * kD + c] = (unsigned char)am;
   }
 }
 
 // ∂E1[n,u,c] = dtl[n,u]·q[n,c] + Σ_τ [u = off_τ + arg[n,τ,c]]·∂pool_τ[n,c] (compat: the eth pool's gradient goes to
 // the enh argmax). One block of 128 threads per row; the row's 64 dtl values via LDS.
+template <typename E>
 __global__ __launch_bounds__(128) void demb_kernel(const float* __restrict__ dtl, const float* __restrict__ q, int ldq,
                                                    const float* __restrict__ dx, const unsigned char* __restrict__ arg,
-                                                   TypeOff T, short* __restrict__ de1, int compat) {
+                                                   TypeOff T, E* __restrict__ de1, int compat) {
   const int n = blockIdx.x, c = threadIdx.x;
   __shared__ float sd[kU];
   if (c < kU) sd[c] = dtl[(size_t)n * kU + c];
@@ -321,12 +349,12 @@ __global__ __launch_bounds__(128) void demb_kernel(const float* __restrict__ dtl
     au[t] = T.off[src] + arg[((size_t)n * 6 + t) * kD + c];
     dp[t] = dx[(size_t)n * 896 + kD + t * kD + c];
   }
-  short* out = de1 + (size_t)n * kU * kD + c;
+  E* out = de1 + (size_t)n * kU * kD + c;
   for (int u = 0; u < kU; ++u) {
     float v = sd[u] * qc;
 #pragma unroll
     for (int t = 0; t < 6; ++t) v += (au[t] == u) ? dp[t] : 0.f;
-    out[(size_t)u * kD] = dca::f2bf(v);
+    stf(out + (size_t)u * kD, v);
   }
 }
 
@@ -336,11 +364,12 @@ __global__ __launch_bounds__(128) void demb_kernel(const float* __restrict__ dtl
 // 16 rows per pass, grid-stride over the rows.
 constexpr int kLnPart = 2 * kD + 6 * kD;
 
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const short* __restrict__ dxn, const short* __restrict__ e0,
+template <typename E>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const E* __restrict__ dxn, const E* __restrict__ e0,
                                                      const float* __restrict__ bsub, const float* __restrict__ gamma,
                                                      const float* __restrict__ mean, const float* __restrict__ rstd,
-                                                     const short* __restrict__ de1, const unsigned char* type_of,
-                                                     short* __restrict__ de0, float* __restrict__ part, int R) {
+                                                     const E* __restrict__ de1, const unsigned char* type_of,
+                                                     E* __restrict__ de0, float* __restrict__ part, int R) {
   const int lr = threadIdx.x >> 4, c0 = (threadIdx.x & 15) * 8;
   float gacc[8], bacc[8], tacc[6][8];
 #pragma unroll
@@ -353,18 +382,19 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const short* __restrict__ d
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     gm[j] = gamma[c0 + j];
-    bs[j] = bsub[c0 + j];
+    bs[j] = bsub ? bsub[c0 + j] : 0.f;
   }
   for (int row = blockIdx.x * 16 + lr; row < R; row += gridDim.x * 16) {
-    const bf16x8 dv = *reinterpret_cast<const bf16x8*>(dxn + (size_t)row * kD + c0);
-    const bf16x8 ev = *reinterpret_cast<const bf16x8*>(e0 + (size_t)row * kD + c0);
-    const bf16x8 rv = *reinterpret_cast<const bf16x8*>(de1 + (size_t)row * kD + c0);
+    float dv[8], ev[8], rv[8];
+    ld8(dxn + (size_t)row * kD + c0, dv);
+    ld8(e0 + (size_t)row * kD + c0, ev);
+    ld8(de1 + (size_t)row * kD + c0, rv);
     const float mu = mean[row], rs = rstd[row];
     float xh[8], g[8], s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      xh[j] = (dca::bf2f(ev[j]) - bs[j] - mu) * rs;
-      const float d = dca::bf2f(dv[j]);
+      xh[j] = (ev[j] - bs[j] - mu) * rs;
+      const float d = dv[j];
       g[j] = d * gm[j];
       s1 += g[j];
       s2 += g[j] * xh[j];
@@ -374,15 +404,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const short* __restrict__ d
     s1 = dca::group_sum<16>(s1) * (1.f / kD);
     s2 = dca::group_sum<16>(s2) * (1.f / kD);
     const int t = type_of[row % kU];
-    bf16x8 o;
+    float o[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const float v = dca::bf2f(rv[j]) + rs * (g[j] - s1 - xh[j] * s2);
-      o[j] = dca::f2bf(v);
+      const float v = rv[j] + rs * (g[j] - s1 - xh[j] * s2);
+      o[j] = v;
 #pragma unroll
       for (int tt = 0; tt < 6; ++tt) tacc[tt][j] += (tt == t) ? v : 0.f;
     }
-    *reinterpret_cast<bf16x8*>(de0 + (size_t)row * kD + c0) = o;
+    st8(de0 + (size_t)row * kD + c0, o);
   }
   // fixed-order block reduction over the 16 row lanes → one partial per block
   __shared__ float red[16][kLnPart];
@@ -692,10 +722,14 @@ extern "C" hipError_t dca_attn_bwd_f32(const float* qkv, const float* o, const f
 
 extern "C" int dca_ln_part_width() { return kLnPart; }
 
-extern "C" hipError_t dca_ln_fwd(const short* e0, const float* bsub, const float* gamma, const float* beta, short* xn,
-                                 float* mean, float* rstd, int R, float eps, hipStream_t st) {
-  hipLaunchKernelGGL(ln_fwd_kernel, dim3((R + 15) / 16), dim3(256), 0, st, e0, bsub, gamma, beta, xn, mean, rstd, R,
-                     eps);
+extern "C" hipError_t dca_ln_fwd(const void* e0, const float* bsub, const float* gamma, const float* beta, void* xn,
+                                 float* mean, float* rstd, int R, float eps, int f32, hipStream_t st) {
+  if (f32)
+    hipLaunchKernelGGL(ln_fwd_kernel<float>, dim3((R + 15) / 16), dim3(256), 0, st, (const float*)e0, bsub, gamma,
+                       beta, (float*)xn, mean, rstd, R, eps);
+  else
+    hipLaunchKernelGGL(ln_fwd_kernel<short>, dim3((R + 15) / 16), dim3(256), 0, st, (const short*)e0, bsub, gamma,
+                       beta, (short*)xn, mean, rstd, R, eps);
   DCA_CHECK_LAUNCH();
   return hipSuccess;
 }
@@ -713,30 +747,40 @@ extern "C" hipError_t dca_attn_bwd(const short* qkv, const short* o, const short
   return hipSuccess;
 }
 
-extern "C" hipError_t dca_attn_pool(const short* e1, const int* type_off, short* x896, unsigned char* arg, int N,
-                                    int compat, hipStream_t st) {
+extern "C" hipError_t dca_attn_pool(const void* e1, const int* type_off, void* x896, unsigned char* arg, int N,
+                                    int compat, int f32, hipStream_t st) {
   TypeOff T;
   for (int i = 0; i < 7; ++i) T.off[i] = type_off[i];
-  hipLaunchKernelGGL(pool_kernel, dim3(N), dim3(128), 0, st, e1, T, x896, arg, compat);
+  if (f32)
+    hipLaunchKernelGGL(pool_kernel<float>, dim3(N), dim3(128), 0, st, (const float*)e1, T, (float*)x896, arg, compat);
+  else
+    hipLaunchKernelGGL(pool_kernel<short>, dim3(N), dim3(128), 0, st, (const short*)e1, T, (short*)x896, arg, compat);
   DCA_CHECK_LAUNCH();
   return hipSuccess;
 }
 
 extern "C" hipError_t dca_attn_demb(const float* dtl, const float* q, int ldq, const float* dx,
-                                    const unsigned char* arg, const int* type_off, short* de1, int N, int compat,
-                                    hipStream_t st) {
+                                    const unsigned char* arg, const int* type_off, void* de1, int N, int compat,
+                                    int f32, hipStream_t st) {
   TypeOff T;
   for (int i = 0; i < 7; ++i) T.off[i] = type_off[i];
-  hipLaunchKernelGGL(demb_kernel, dim3(N), dim3(128), 0, st, dtl, q, ldq, dx, arg, T, de1, compat);
+  if (f32)
+    hipLaunchKernelGGL(demb_kernel<float>, dim3(N), dim3(128), 0, st, dtl, q, ldq, dx, arg, T, (float*)de1, compat);
+  else
+    hipLaunchKernelGGL(demb_kernel<short>, dim3(N), dim3(128), 0, st, dtl, q, ldq, dx, arg, T, (short*)de1, compat);
   DCA_CHECK_LAUNCH();
   return hipSuccess;
 }
 
-extern "C" hipError_t dca_ln_bwd(const short* dxn, const short* e0, const float* bsub, const float* gamma,
-                                 const float* mean, const float* rstd, const short* de1, const unsigned char* type_of,
-                                 short* de0, float* part, int nblk, float* out, int R, hipStream_t st) {
-  hipLaunchKernelGGL(ln_bwd_kernel, dim3(nblk), dim3(256), 0, st, dxn, e0, bsub, gamma, mean, rstd, de1, type_of, de0,
-                     part, R);
+extern "C" hipError_t dca_ln_bwd(const void* dxn, const void* e0, const float* bsub, const float* gamma,
+                                 const float* mean, const float* rstd, const void* de1, const unsigned char* type_of,
+                                 void* de0, float* part, int nblk, float* out, int R, int f32, hipStream_t st) {
+  if (f32)
+    hipLaunchKernelGGL(ln_bwd_kernel<float>, dim3(nblk), dim3(256), 0, st, (const float*)dxn, (const float*)e0, bsub,
+                       gamma, mean, rstd, (const float*)de1, type_of, (float*)de0, part, R);
+  else
+    hipLaunchKernelGGL(ln_bwd_kernel<short>, dim3(nblk), dim3(256), 0, st, (const short*)dxn, (const short*)e0, bsub,
+                       gamma, mean, rstd, (const short*)de1, type_of, (short*)de0, part, R);
   DCA_CHECK_LAUNCH();
   hipLaunchKernelGGL(colsum_kernel, dim3((kLnPart + 63) / 64), dim3(256), 0, st, part, nblk, kLnPart, out);
   DCA_CHECK_LAUNCH();

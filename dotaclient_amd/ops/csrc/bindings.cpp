@@ -581,14 +581,20 @@ std::vector<torch::Tensor> enc_small_grads(torch::Tensor z, torch::Tensor dtl, t
 // ---- 5v5 entity-attention block (ops/csrc/attn.hip); 64 unit slots, width 128, 4 heads × 32 -------------------
 std::vector<torch::Tensor> ln_fwd(torch::Tensor e0, torch::Tensor bsub, torch::Tensor gamma, torch::Tensor beta,
                                   double eps) {
-  CHECK_BF16(e0); CHECK_F32(bsub); CHECK_F32(gamma); CHECK_F32(beta);
-  TORCH_CHECK(e0.size(-1) == 128 && bsub.numel() == 128 && gamma.numel() == 128 && beta.numel() == 128, "ln_fwd");
+  // bf16 learner: bf16 E0' with b_sub; fp32 learner: fp32 E0, b_sub an empty tensor (no subtraction)
+  const bool f32 = e0.scalar_type() == at::kFloat;
+  if (f32) { CHECK_F32(e0); } else { CHECK_BF16(e0); }
+  CHECK_F32(gamma); CHECK_F32(beta);
+  if (bsub.numel()) { CHECK_F32(bsub); }
+  TORCH_CHECK(e0.size(-1) == 128 && (bsub.numel() == 128 || (f32 && bsub.numel() == 0)) && gamma.numel() == 128 &&
+              beta.numel() == 128, "ln_fwd");
   const int64_t R = e0.numel() / 128;
   auto xn = torch::empty({R, 128}, e0.options());
   auto mean = torch::empty({R}, gamma.options());
   auto rstd = torch::empty({R}, gamma.options());
-  hip_check(dca_ln_fwd(ptr<short>(e0), ptr<float>(bsub), ptr<float>(gamma), ptr<float>(beta), ptr<short>(xn),
-                       ptr<float>(mean), ptr<float>(rstd), (int)R, (float)eps, cur_stream()),
+  hip_check(dca_ln_fwd(e0.data_ptr(), bsub.numel() ? ptr<float>(bsub) : nullptr, ptr<float>(gamma), ptr<float>(beta),
+                       xn.data_ptr(), ptr<float>(mean), ptr<float>(rstd), (int)R, (float)eps, f32 ? 1 : 0,
+                       cur_stream()),
             "dca_ln_fwd");
   return {xn, mean, rstd};
 }
@@ -638,31 +644,32 @@ static void check_type_off(const std::vector<int64_t>& t) {
 
 // pools of E1 (N*64,128) bf16 into x896[:, 128:] (bf16, in place) and arg (N,6,128) u8 (returned)
 torch::Tensor attn_pool(torch::Tensor e1, std::vector<int64_t> type_off, torch::Tensor x896, bool compat) {
-  CHECK_BF16(e1); CHECK_BF16(x896);
+  const bool f32 = e1.scalar_type() == at::kFloat;
+  if (f32) { CHECK_F32(e1); CHECK_F32(x896); } else { CHECK_BF16(e1); CHECK_BF16(x896); }
   check_type_off(type_off);
   const int N = e1.numel() / (64 * 128);
   TORCH_CHECK(x896.numel() == (int64_t)N * 896, "x896 must be (N, 896)");
   auto arg = torch::empty({(int64_t)N, 6, 128}, e1.options().dtype(at::kByte));
   int off[7];
   for (int i = 0; i < 7; ++i) off[i] = (int)type_off[i];
-  hip_check(dca_attn_pool(ptr<short>(e1), off, ptr<short>(x896), ptr<unsigned char>(arg), N, compat ? 1 : 0,
-                          cur_stream()),
+  hip_check(dca_attn_pool(e1.data_ptr(), off, x896.data_ptr(), ptr<unsigned char>(arg), N, compat ? 1 : 0,
+                          f32 ? 1 : 0, cur_stream()),
             "dca_attn_pool");
   return arg;
 }
 
 torch::Tensor attn_demb(torch::Tensor dtl, torch::Tensor q, torch::Tensor dx, torch::Tensor arg,
-                        std::vector<int64_t> type_off, bool compat) {
+                        std::vector<int64_t> type_off, bool compat, bool f32) {
   CHECK_F32(dtl); CHECK_DEV(q); CHECK_DT(q, at::kFloat); CHECK_F32(dx); CHECK_U8(arg);
   check_type_off(type_off);
   const int N = dtl.size(0);
   TORCH_CHECK(dtl.size(1) == 64 && q.size(0) == N && q.stride(1) == 1 && dx.size(0) == N && dx.size(1) == 896 &&
               arg.numel() == (int64_t)N * 6 * 128, "attn_demb shapes");
-  auto de1 = torch::empty({(int64_t)N * 64, 128}, dx.options().dtype(at::kBFloat16));
+  auto de1 = torch::empty({(int64_t)N * 64, 128}, dx.options().dtype(f32 ? at::kFloat : at::kBFloat16));
   int off[7];
   for (int i = 0; i < 7; ++i) off[i] = (int)type_off[i];
   hip_check(dca_attn_demb(ptr<float>(dtl), ptr<float>(q), (int)q.stride(0), ptr<float>(dx), ptr<unsigned char>(arg),
-                          off, ptr<short>(de1), N, compat ? 1 : 0, cur_stream()),
+                          off, de1.data_ptr(), N, compat ? 1 : 0, f32 ? 1 : 0, cur_stream()),
             "dca_attn_demb");
   return de1;
 }
@@ -670,8 +677,11 @@ torch::Tensor attn_demb(torch::Tensor dtl, torch::Tensor q, torch::Tensor dx, to
 // returns (dE0 bf16 (R,128), dgamma (128), dbeta (128), dbt (6,128)); type_of: (64) u8 device, unit slot → type
 std::vector<torch::Tensor> ln_bwd(torch::Tensor dxn, torch::Tensor e0, torch::Tensor bsub, torch::Tensor gamma,
                                   torch::Tensor mean, torch::Tensor rstd, torch::Tensor de1, torch::Tensor type_of) {
-  CHECK_BF16(dxn); CHECK_BF16(e0); CHECK_F32(bsub); CHECK_F32(gamma); CHECK_F32(mean); CHECK_F32(rstd);
-  CHECK_BF16(de1); CHECK_U8(type_of);
+  const bool f32 = e0.scalar_type() == at::kFloat;
+  if (f32) { CHECK_F32(dxn); CHECK_F32(e0); CHECK_F32(de1); } else { CHECK_BF16(dxn); CHECK_BF16(e0); CHECK_BF16(de1); }
+  CHECK_F32(gamma); CHECK_F32(mean); CHECK_F32(rstd); CHECK_U8(type_of);
+  if (bsub.numel()) { CHECK_F32(bsub); }
+  TORCH_CHECK(bsub.numel() == 128 || (f32 && bsub.numel() == 0), "ln_bwd: b_sub must be (128) (or empty in fp32)");
   const int64_t R = e0.numel() / 128;
   TORCH_CHECK(dxn.numel() == R * 128 && de1.numel() == R * 128 && mean.numel() == R && rstd.numel() == R &&
               type_of.numel() == 64 && R % 64 == 0, "ln_bwd shapes");
@@ -680,9 +690,9 @@ std::vector<torch::Tensor> ln_bwd(torch::Tensor dxn, torch::Tensor e0, torch::Te
   const int nblk = (int)std::min<int64_t>(1024, (R + 15) / 16);
   auto part = torch::empty({(int64_t)nblk * W}, gamma.options());
   auto out = torch::empty({W}, gamma.options());
-  hip_check(dca_ln_bwd(ptr<short>(dxn), ptr<short>(e0), ptr<float>(bsub), ptr<float>(gamma), ptr<float>(mean),
-                       ptr<float>(rstd), ptr<short>(de1), ptr<unsigned char>(type_of), ptr<short>(de0),
-                       ptr<float>(part), nblk, ptr<float>(out), (int)R, cur_stream()),
+  hip_check(dca_ln_bwd(dxn.data_ptr(), e0.data_ptr(), bsub.numel() ? ptr<float>(bsub) : nullptr, ptr<float>(gamma),
+                       ptr<float>(mean), ptr<float>(rstd), de1.data_ptr(), ptr<unsigned char>(type_of),
+                       de0.data_ptr(), ptr<float>(part), nblk, ptr<float>(out), (int)R, f32 ? 1 : 0, cur_stream()),
             "dca_ln_bwd");
   return {de0, out.narrow(0, 0, 128), out.narrow(0, 128, 128), out.narrow(0, 256, 768).view({6, 128})};
 }
@@ -776,11 +786,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("A"), py::arg("B"), py::arg("C"), py::arg("perm") = py::none(), py::arg("accumulate") = false,
         py::arg("B0") = py::none(), py::arg("colsum") = py::none());
   m.def("enc_small_grads", &enc_small_grads, "entity-encoder type-bias and env-layer gradients in one pass");
-  m.def("ln_fwd", &ln_fwd, "LayerNorm(E0 - bsub) -> (xn bf16, mean, rstd)");
+  m.def("ln_fwd", &ln_fwd, "LayerNorm(E0 - bsub) -> (xn, mean, rstd); bf16, or fp32 (bsub may be empty)");
   m.def("attn_fwd", &attn_fwd, "entity self-attention per (row, head): (o, lse); bf16, or fp32 (bf16x3 MFMA)");
   m.def("attn_bwd", &attn_bwd, "entity self-attention backward: dqkv");
   m.def("attn_pool", &attn_pool, "per-type max-pool + argmax of attended embeddings into x896");
-  m.def("attn_demb", &attn_demb, "dE1 = dtl*q + pool gradient at the argmax unit");
+  m.def("attn_demb", &attn_demb, "dE1 = dtl*q + pool gradient at the argmax unit (bf16 or f32 out)");
   m.def("ln_bwd", &ln_bwd, "LayerNorm backward + residual: (dE0, dgamma, dbeta, dbt)");
   m.def("replay_gather", &replay_gather, "minibatch gather from an HBM replay pool into time-major rows (one launch)");
   m.def("returns_scan", &returns_scan, "segmented reverse scan: discounted returns / GAE + per-team EMA normalisation");

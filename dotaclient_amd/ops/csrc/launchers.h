@@ -85,21 +85,21 @@ hipError_t dca_enc_small_grads(const float* z, int ldz, const float* dtl, int U,
                                float* out, hipStream_t st);
 
 int dca_ln_part_width();
-hipError_t dca_ln_fwd(const short* e0, const float* bsub, const float* gamma, const float* beta, short* xn, float* mean,
-                      float* rstd, int R, float eps, hipStream_t st);
+hipError_t dca_ln_fwd(const void* e0, const float* bsub, const float* gamma, const float* beta, void* xn, float* mean,
+                      float* rstd, int R, float eps, int f32, hipStream_t st);
 hipError_t dca_attn_fwd(const short* qkv, short* o, float* lse, int N, float scale, hipStream_t st);
 hipError_t dca_attn_fwd_f32(const float* qkv, float* o, float* lse, int N, float scale, hipStream_t st);
 hipError_t dca_attn_bwd_f32(const float* qkv, const float* o, const float* dout, const float* lse, float* dqkv, int N,
                             float scale, hipStream_t st);
 hipError_t dca_attn_bwd(const short* qkv, const short* o, const short* dout, const float* lse, short* dqkv, int N,
                         float scale, hipStream_t st);
-hipError_t dca_attn_pool(const short* e1, const int* type_off, short* x896, unsigned char* arg, int N, int compat,
-                         hipStream_t st);
+hipError_t dca_attn_pool(const void* e1, const int* type_off, void* x896, unsigned char* arg, int N, int compat,
+                         int f32, hipStream_t st);
 hipError_t dca_attn_demb(const float* dtl, const float* q, int ldq, const float* dx, const unsigned char* arg,
-                         const int* type_off, short* de1, int N, int compat, hipStream_t st);
-hipError_t dca_ln_bwd(const short* dxn, const short* e0, const float* bsub, const float* gamma, const float* mean,
-                      const float* rstd, const short* de1, const unsigned char* type_of, short* de0, float* part,
-                      int nblk, float* out, int R, hipStream_t st);
+                         const int* type_off, void* de1, int N, int compat, int f32, hipStream_t st);
+hipError_t dca_ln_bwd(const void* dxn, const void* e0, const float* bsub, const float* gamma, const float* mean,
+                      const float* rstd, const void* de1, const unsigned char* type_of, void* de0, float* part,
+                      int nblk, float* out, int R, int f32, hipStream_t st);
 
 hipError_t dca_replay_gather(const void* const* src, void* const* dst, const long long* row_bytes, const int* per_step,
                              int nf, const long long* idx, int S, int B, hipStream_t st);

@@ -99,7 +99,7 @@ def test_pool_and_demb(gpu_ops, compat):
     dtl = torch.randn(N, U, device='cuda', generator=g)
     z = torch.randn(N, 160, device='cuda', generator=g)
     dx = torch.randn(N, 896, device='cuda', generator=g)
-    de1 = gpu_ops.attn_demb(dtl, z, dx, arg, TYPE_OFF, compat)
+    de1 = gpu_ops.attn_demb(dtl, z, dx, arg, TYPE_OFF, compat, False)
     ref = dtl.unsqueeze(-1) * z[:, None, :D]
     for t in range(6):
         src = 3 if (compat and t == 5) else t
@@ -130,6 +130,57 @@ def test_ln_bwd(gpu_ops):
     torch.testing.assert_close(dbet, bt.grad, rtol=1e-3, atol=1e-2)
     ref_dbt = torch.stack([ref_de0.view(N, U, D)[:, TYPE_OFF[t]:TYPE_OFF[t + 1]].sum((0, 1)) for t in range(6)])
     torch.testing.assert_close(dbt, ref_dbt, rtol=2e-2, atol=0.5)
+
+
+@pytest.mark.parametrize('compat', [False, True])
+def test_block_kernels_f32(gpu_ops, compat):
+    """fp32 learner's block kernels: LayerNorm fwd/bwd without b_sub (+ residual, ∂γ, ∂β, per-type ∂b_τ), pools and
+    ∂E1 routing, against float64 references."""
+    g = _g(5)
+    R = N * U
+    rel = lambda a, b: float((a.double() - b).norm() / b.norm())   # noqa: E731
+    e0 = torch.randn(R, D, device='cuda', generator=g) * 2 + 0.5
+    gamma = 1 + 0.1 * torch.randn(D, device='cuda', generator=g)
+    beta = 0.1 * torch.randn(D, device='cuda', generator=g)
+    nob = torch.empty(0, device='cuda')
+    xn, mean, rstd = gpu_ops.ln_fwd(e0, nob, gamma, beta, 1e-5)
+    assert xn.dtype == torch.float32
+    x = e0.double().requires_grad_(True)
+    gm, bt = gamma.double().requires_grad_(True), beta.double().requires_grad_(True)
+    y = F.layer_norm(x, (D,), gm, bt, 1e-5)
+    assert rel(xn, y.detach()) < 1e-6
+    dxn = torch.randn(R, D, device='cuda', generator=g)
+    de1 = torch.randn(R, D, device='cuda', generator=g)
+    type_of = torch.tensor(sum([[t] * (TYPE_OFF[t + 1] - TYPE_OFF[t]) for t in range(6)], []), dtype=torch.uint8,
+                           device='cuda')
+    de0, dgam, dbet, dbt = gpu_ops.ln_bwd(dxn, e0, nob, gamma, mean, rstd, de1, type_of)
+    y.backward(dxn.double())
+    ref_de0 = x.grad + de1.double()
+    assert rel(de0, ref_de0) < 1e-5
+    assert rel(dgam, gm.grad) < 1e-5 and rel(dbet, bt.grad) < 1e-5
+    ref_dbt = torch.stack([ref_de0.view(N, U, D)[:, TYPE_OFF[t]:TYPE_OFF[t + 1]].sum((0, 1)) for t in range(6)])
+    assert rel(dbt, ref_dbt) < 1e-5
+    # pools (exact: max is a selection) and the routed ∂E1
+    x896 = torch.zeros(N, 896, device='cuda')
+    arg = gpu_ops.attn_pool(e0, TYPE_OFF, x896, compat)
+    e = e0.view(N, U, D)
+    for t in range(6):
+        src = 3 if (compat and t == 5) else t
+        seg = e[:, TYPE_OFF[src]:TYPE_OFF[src + 1]]
+        mx, am = seg.max(1)
+        assert torch.equal(x896[:, D + t * D:D + (t + 1) * D], mx)
+        assert torch.equal(seg.gather(1, arg[:, t].long().unsqueeze(1)).squeeze(1), mx)
+    dtl = torch.randn(N, U, device='cuda', generator=g)
+    z = torch.randn(N, 160, device='cuda', generator=g)
+    dx = torch.randn(N, 896, device='cuda', generator=g)
+    got = gpu_ops.attn_demb(dtl, z, dx, arg, TYPE_OFF, compat, True)
+    assert got.dtype == torch.float32
+    ref = dtl.double().unsqueeze(-1) * z.double()[:, None, :D]
+    for t in range(6):
+        src = 3 if (compat and t == 5) else t
+        u = TYPE_OFF[src] + arg[:, t].long()
+        ref.scatter_add_(1, u.unsqueeze(1), dx.double()[:, D + t * D:D + (t + 1) * D].unsqueeze(1))
+    assert rel(got.view(N, U, D), ref) < 1e-6
 
 
 def test_encoder_bwd_with_given_demb(gpu_ops):
