@@ -158,6 +158,9 @@ class WeightImages:
 # 2.9e-7 exact, 58 vs 127 µs), the same accuracy class as the hand-written bf16x3 kernels. DCA_F32_GEMM=exact keeps
 # hipBLASLt's exact-f32 path.
 _F32_GEMM_FAST = os.environ.get('DCA_F32_GEMM', 'fast') != 'exact'
+# weight-gradient GEMMs of the recurrence and pre-RNN layer on the (then idle) recurrence stream, overlapped with the
+# ∂X chain of the main stream (DCA_WG_OVERLAP=0: everything on the main stream)
+_WG_OVERLAP = os.environ.get('DCA_WG_OVERLAP', '1') != '0'
 
 
 def fused_step_tm(fp, *args, **kw):
@@ -323,21 +326,37 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             e = torch.cuda.Event()
             e.record(sL)
             bwd_done.append(e)
+    # single chunk: the recurrence stream (idle once the backward recurrence is done) takes the weight-gradient GEMMs
+    # of W_hh, W_ih and the pre-RNN layer, off the critical ∂X chain (∂pre → ∂x896 → encoder backward) on the main
+    # stream; the main stream joins it before the DP split point and before returning
+    wg_side = one and _WG_OVERLAP
+    wg_done = None
     for (t0, t1), done in zip(reversed(spans), bwd_done):
         main.wait_event(done)
         r0, r1 = t0 * B, t1 * B
         n = r1 - r0
         dG16 = dgates16[t0:t1].view(n, 4 * H)
-        if t0 > 0:
-            gemm_tn(dG16, hs16[t0 - 1:t1 - 1].view(n, H), out=dWhh, perm=gperm, accumulate=True)
-        else:       # h_{t-1} rows: h0 for t = 0, then hs[0 : t1-1] — no concatenation materialised
-            gemm_tn(dG16, hs16[0:t1 - 1].view(n - B, H), out=dWhh, perm=gperm, accumulate=True, b0=h016)
-        gemm_tn(dG16, x16[r0:r1], out=dWih, perm=gperm, accumulate=True)
+        with torch.cuda.stream(sL if wg_side else main):
+            if t0 > 0:
+                gemm_tn(dG16, hs16[t0 - 1:t1 - 1].view(n, H), out=dWhh, perm=gperm, accumulate=True)
+            else:       # h_{t-1} rows: h0 for t = 0, then hs[0 : t1-1] — no concatenation materialised
+                gemm_tn(dG16, hs16[0:t1 - 1].view(n - B, H), out=dWhh, perm=gperm, accumulate=True, b0=h016)
+            gemm_tn(dG16, x16[r0:r1], out=dWih, perm=gperm, accumulate=True)
         # ∂pre-activation of the pre-RNN layer: one GEMM (bf16 or exact f32), ReLU mask in one threshold_backward
         dpre16 = torch.ops.aten.threshold_backward(torch.mm(dG16, W['wihT16'].t()), x16[r0:r1], 0)
-        gemm_tn(dpre16, x896[r0:r1], out=dWpre, accumulate=True, colsum=dbpre)
+        if wg_side:
+            sL.wait_stream(main)
+            with torch.cuda.stream(sL):
+                gemm_tn(dpre16, x896[r0:r1], out=dWpre, accumulate=True, colsum=dbpre)
+                wg_done = torch.cuda.Event()
+                wg_done.record(sL)
+        else:
+            gemm_tn(dpre16, x896[r0:r1], out=dWpre, accumulate=True, colsum=dbpre)
         dx896 = _mm(dpre16, wpre16)
         if split is not None:
+            if wg_done is not None:
+                main.wait_event(wg_done)
+                wg_done = None
             # DP split point: every gradient of the recurrence, pre-RNN and heads is final here (the big ones are
             # already in the flat buffer); apply the small ones and let the learner all-reduce those buckets while
             # the encoder backward below runs (see Learner._replay_split)
@@ -385,6 +404,8 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         dbt = _acc(dbt, dbt_attn if attn else dbt_c)
         dWe = _acc(dWe, dWe_c)
         dbe = _acc(dbe, dbe_c)
+    if wg_done is not None:
+        main.wait_event(wg_done)
     inv = fp.gate_inv(H, dev)
     if not direct:
         grads['rnn.weight_hh_l0'] = dWhh

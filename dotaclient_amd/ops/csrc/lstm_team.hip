@@ -150,7 +150,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, in
 }
 
 // Bounded spin bookkeeping; true when this wave must give up (timeout or another workgroup raised an error).
-__device__ __forceinline__ bool spin_fail(unsigned& spins, TeamCtl* ctl, unsigned* err, unsigned code) {
+__device__ __forceinline__ bool spin_fail(unsigned& spins, TeamCtl* ctl, unsigned* err, unsigned code, int knobs) {
   asm volatile("" ::: "memory");        // compiler barrier: re-issue the poll loads every round
   ++spins;
   if ((spins & 255u) == 0) {
@@ -161,7 +161,7 @@ __device__ __forceinline__ bool spin_fail(unsigned& spins, TeamCtl* ctl, unsigne
       return true;
     }
   }
-  if (spins > 32) __builtin_amdgcn_s_sleep(1);
+  if (spins > 32 && !((knobs >> 13) & 1)) __builtin_amdgcn_s_sleep(1);
   return false;
 }
 
@@ -367,6 +367,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
     bool dead = false;
     for (int t = 0; t < S; ++t) {
       const int par = t & 1;
+      if ((knobs >> 12) & 1) spins = 0;
       TSTAMP(0);
       // ---- prefetch this step's input projection (one 16-B vector per owned (row, unit)). Loading it one step
       // ahead instead measured slower (2.11 vs 1.94 µs per step at B=8, H=512).
@@ -408,7 +409,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
             g[0] = __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16, 0, kSc1);
             okc[0] = ((unsigned)g[0].y == tag) & ((unsigned)g[0].w == tag);
             if (__all(okc[0])) break;
-            if (spin_fail(spins, ctl, err, 1u)) { dead = true; break; }
+            if (spin_fail(spins, ctl, err, 1u, knobs)) { dead = true; break; }
           }
         }
         while (!dead) {
@@ -422,7 +423,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
             ok &= okc[i];
           }
           if (__all(ok)) break;
-          if (spin_fail(spins, ctl, err, 1u)) { dead = true; break; }
+          if (spin_fail(spins, ctl, err, 1u, knobs)) { dead = true; break; }
         }
 #pragma unroll
         for (int i = 0; i < NL; ++i) {
@@ -580,7 +581,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
     const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
     const void* __restrict__ whh_, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
     i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
-    unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart) {
+    unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart, int knobs) {
   constexpr int H = 128 * KS;
   constexpr int U = H / kT;             // 4·KS units per workgroup (MFMA N, zero-padded to 16)
   constexpr int KW = H;                 // K (= 4H gate columns) per wave
@@ -674,6 +675,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
     bool dead = false;
     for (int k = 0; k <= S; ++k) {
       const int t = S - 1 - k;          // step whose gate gradients are produced this iteration (-1: final)
+      if ((knobs >> 12) & 1) spins = 0;
       TSTAMPB(0);
       // ---- prefetch the saved activations of step t for the owned pairs
       dca::f32x4 gv[NPAIR];
@@ -715,7 +717,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
               ok &= okc[i];
             }
             if (__all(ok)) break;
-            if (spin_fail(spins, ctl, err, 2u)) { dead = true; break; }
+            if (spin_fail(spins, ctl, err, 2u, knobs)) { dead = true; break; }
           }
 #pragma unroll
           for (int i = 0; i < NL; ++i) {
@@ -878,14 +880,15 @@ __global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
     const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
     const void* __restrict__ whh, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
     i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
-    unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart) {
+    unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart, int knobs) {
   __builtin_amdgcn_s_setprio(3);
   lstm_team_bwd_body<MT, KS, F32, V1>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, dh0, dc0, xg_all, ctl, err, Btot, Bc, nch,
-                             S, sb, st, trace, dg16, dbpart);
+                             S, sb, st, trace, dg16, dbpart, knobs);
   team_exit(ctl, err, nch);
 }
 
-// DCA_TEAM_KNOBS = pre_sleep | skip_outputs << 8 | probe_first << 9 | xp_step0 << 10 (latency experiments only);
+// DCA_TEAM_KNOBS = pre_sleep | skip_outputs << 8 | probe_first << 9 | xp_step0 << 10 | spin count reset per step << 12
+// | no poll back-off sleep << 13 (latency experiments only);
 // DCA_TEAM_FAIL=1 sets bit 11: no workgroup joins a team (fault injection: every chain left unprocessed → err 3)
 inline int team_knobs() {
   const char* e = getenv("DCA_TEAM_KNOBS");
@@ -990,7 +993,8 @@ extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, c
 #define DCA_B(mt, ks, f, v)                                                                                        \
   (lstm_team_bwd_kernel<mt, ks, f, v><<<kMaxTeams * kT, kThreads, 0, stream>>>(dhs, gates4, cs, c0, dhn, dcn, whh,      \
                                                                           dgates4, dh0, dc0, xb, ctl, err, B, Bc,  \
-                                                                          nch, S, sb, st, trace, dg16, dbpart),    \
+                                                                          nch, S, sb, st, trace, dg16, dbpart,      \
+                                                                          team_knobs()),                           \
    hipGetLastError())
   DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc), DCA_B)
 #undef DCA_B
