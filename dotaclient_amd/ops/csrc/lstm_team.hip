@@ -48,6 +48,10 @@
 // written lines: outputs redirected into an 8-step L2-resident window ran 1.93-1.95 µs (no change), non-temporal
 // stores 1.891 vs 1.895 — the cost follows the NUMBER of store instructions ahead of the next poll. Backward: its gate-gradient store costs 0.05-0.07 µs per step (2.27-2.30 vs 2.23 µs without it), but
 // taking wave 0 (whose lanes store) off the poll, with waves 1-3 gathering 3 chunks per thread, was slower: 2.34-2.36.
+// Round 2, fp32 V1 path (B=8, H=512): a double-buffered poll (second unpredicated round issued 0-4 sleeps after the
+// first, so a late granule is seen up to half a round trip sooner) ran 1.435 vs 1.287 µs per forward step — the
+// extra L2 reads slow the publishers more than the finer granularity gains; the poll back-off sleep (reset per step
+// or removed, knob bits 12/13) measured within ±0.01 µs.
 // Forward store COUNT matters more than bytes: one packed 16-B record {bf16 gates, f32 c, bf16 h} per (row, unit)
 // instead of the three stores ran 1.84 vs 1.895 µs — left out (bf16 saved gates for the backward, and an h unpack
 // pass would eat half the gain).
