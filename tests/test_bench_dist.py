@@ -1,4 +1,4 @@
-"""bench.py contract on the multi-process path (gloo on CPU, world_size 2): one JSON line from rank 0 with the
+"""bench.py contract on the multi-process path (gloo on CPU, world_size 2 and 4): one JSON line from rank 0 with the
 whole-job aggregate, weak-scaling fields and the BASELINE metric name."""
 import json
 import os
@@ -19,7 +19,7 @@ def _port():
     return p
 
 
-@pytest.mark.parametrize('world', [1, 2])
+@pytest.mark.parametrize('world', [1, 2, 4])
 def test_bench_json_contract_cpu(world):
     env = dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS='2', CUDA_VISIBLE_DEVICES='', HIP_VISIBLE_DEVICES='')
     args = ['bench.py', '--gpus', str(world), '--steps', '2', '--warmup', '1', '--batch-size', '2', '--seq-len', '16',
