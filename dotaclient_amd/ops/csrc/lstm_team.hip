@@ -51,7 +51,8 @@
 // Round 2, fp32 V1 path (B=8, H=512): a double-buffered poll (second unpredicated round issued 0-4 sleeps after the
 // first, so a late granule is seen up to half a round trip sooner) ran 1.435 vs 1.287 µs per forward step — the
 // extra L2 reads slow the publishers more than the finer granularity gains; the poll back-off sleep (reset per step
-// or removed, knob bits 12/13) measured within ±0.01 µs.
+// or removed, knob bits 12/13) measured within ±0.01 µs; a backward whose activation prefetch always hits L2 (step
+// S-1 every step) ran 1.379 vs 1.385 µs — the saved-activation loads are not on the critical path either.
 // Forward store COUNT matters more than bytes: one packed 16-B record {bf16 gates, f32 c, bf16 h} per (row, unit)
 // instead of the three stores ran 1.84 vs 1.895 µs — left out (bf16 saved gates for the backward, and an h unpack
 // pass would eat half the gain).
