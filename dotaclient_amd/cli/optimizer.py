@@ -67,6 +67,8 @@ def build_parser():
     ap.add_argument('--replay-gb', type=float, default=0.0, help='on-HBM replay buffer budget in GB (0 = off)')
     ap.add_argument('--replay-capacity', type=int, default=0, help='replay capacity in sequences (overrides GB)')
     ap.add_argument('--replay-recent', type=int, default=0, help='sample from the newest N sequences (0 = all)')
+    ap.add_argument('--prefetch-rollouts', type=int, default=0,
+                    help='decode up to N experience messages ahead on a background thread (0 = inline)')
     ap.add_argument('--allow-pickle-experience', type=str2bool, default=False,
                     help='also accept reference agents\' pickled experience (restricted unpickler: arrays only)')
     return ap
@@ -98,7 +100,8 @@ def main(argv=None):
                           precision=args.precision, graph=bool(args.graph), async_checkpoint=bool(args.async_checkpoint),
                           checkpoint_keep=args.checkpoint_keep, replay_gb=args.replay_gb,
                           replay_capacity=args.replay_capacity, replay_recent=args.replay_recent,
-                          allow_pickle_experience=args.allow_pickle_experience)
+                          allow_pickle_experience=args.allow_pickle_experience,
+                          prefetch_rollouts=args.prefetch_rollouts)
     broker = make_broker(args.broker or f'tcp://{args.ip}:{args.port}')
     try:
         DotaOptimizer(cfg, broker).run()

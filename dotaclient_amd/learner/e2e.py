@@ -10,7 +10,9 @@ runs that loop for real, in one process:
   the lockstep games do not all publish on the same step;
 * :class:`~dotaclient_amd.learner.optimizer.DotaOptimizer` (the learner runtime, unchanged: decode, device ingest
   with the return / GAE scan, hipGraph PPO steps, checkpoint + model publish every iteration) consumes them with
-  the deploy's shape — batch 8 × seq_len 1400, 16 sequences per iteration, 1 epoch (params.libsonnet:7-24);
+  the deploy's shape — batch 8 × seq_len 1400, 16 sequences per iteration, 1 epoch (params.libsonnet:7-24), with
+  experience decoded ``prefetch`` messages ahead on a background thread (``prefetch_rollouts``) so the next
+  iteration's decode overlaps this one's GPU training;
 * every published model reaches the actor's :class:`~dotaclient_amd.actor.weights.WeightStore` and is hot-swapped
   into the actor graphs between steps, so ``avg_weight_age`` is real.
 
@@ -37,7 +39,7 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
                 threads: int = 14, seq_len: int = 1400, batch_size: int = 8, seq_per_epoch: int = 16,
                 epochs: int = 1, precision: str = 'fp32', max_dota_time: float = 600.0, rollout_size: int = 9999,
                 queue_size: int = 64, warmup_iterations: int = 2, max_iterations: Optional[int] = None,
-                log_dir: Optional[str] = None) -> Dict[str, float]:
+                log_dir: Optional[str] = None, prefetch: int = 32) -> Dict[str, float]:
     from ..actor.vec import VecActor
     from ..actor.weights import WeightStore
     from ..transport.broker import InProcBroker
@@ -47,7 +49,8 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
     broker = InProcBroker(maxsize=queue_size, drop_oldest=True)
     cfg = OptimizerConfig(log_dir=tmp, epochs=epochs, seq_per_epoch=seq_per_epoch, batch_size=batch_size,
                           seq_len=seq_len, model=model, precision=precision, device=str(device), checkpoint_keep=2,
-                          run_local=True, xp_timeout=300.0, histogram_freq=10 ** 9, async_checkpoint=True)
+                          run_local=True, xp_timeout=300.0, histogram_freq=10 ** 9, async_checkpoint=True,
+                          prefetch_rollouts=prefetch)
     opt = DotaOptimizer(cfg, broker)                       # publishes model version 0
     ws = WeightStore(model, device='cpu')
     from concurrent.futures import ThreadPoolExecutor
@@ -87,7 +90,9 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
             it += 1
             m = opt.last_metrics
             rows.append((m[DotaOptimizer.SPEED_KEY], m['avg_weight_age'], m['avg_rollout_len'],
-                         m.get('time/train', float('nan')), m.get('time/ingest', float('nan')), m['experience_steps']))
+                         m.get('time/train', float('nan')), m.get('time/ingest', float('nan')), m['experience_steps'],
+                         m.get('time/h2d', float('nan')), m.get('time/log', float('nan')),
+                         m.get('time/publish', float('nan'))))
             if err:
                 raise err[0]
         if opt.device.type == 'cuda':
@@ -97,6 +102,7 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
         dropped = broker.n_dropped - d0
     finally:
         stop.set()
+        opt.close()
         th.join(timeout=60)
         va.close()
         opt.flush_checkpoints()
@@ -115,8 +121,12 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
         'avg_rollout_len': float(a[:, 2].mean()) if n_it else float('nan'),
         'train_ms_per_iteration': 1e3 * float(a[:, 3].mean()) if n_it else float('nan'),
         'ingest_ms_per_iteration': 1e3 * float(a[:, 4].mean()) if n_it else float('nan'),
+        'h2d_ms_per_iteration': 1e3 * float(a[:, 6].mean()) if n_it else float('nan'),
+        'log_ms_per_iteration': 1e3 * float(a[:, 7].mean()) if n_it else float('nan'),
+        'publish_ms_per_iteration': 1e3 * float(a[:, 8].mean()) if n_it else float('nan'),
         'actor_steps_per_s': actor_steps / wall,
         'queue_dropped': int(dropped), 'games': games,
         'config': {'batch_size': batch_size, 'seq_len': seq_len, 'seq_per_epoch': seq_per_epoch, 'epochs': epochs,
-                   'rollout_size': rollout_size, 'max_dota_time': max_dota_time, 'precision': precision},
+                   'rollout_size': rollout_size, 'max_dota_time': max_dota_time, 'precision': precision,
+                   'prefetch_rollouts': prefetch},
     }

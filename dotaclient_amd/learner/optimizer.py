@@ -16,6 +16,7 @@ resumes from the same iteration (reference quirk §2.10-7).
 """
 from __future__ import annotations
 
+import copy
 import logging
 import os
 import random
@@ -82,6 +83,8 @@ class OptimizerConfig:
     allow_pickle_experience: bool = False  # accept reference-agent pickles (restricted unpickler); off: DCX1 only
     graph: bool = True                 # capture the fused train step in a hipGraph (learner/engine.py enable_graph)
     async_checkpoint: bool = False     # write checkpoint files on a background thread (the model is published first)
+    prefetch_rollouts: int = 0         # >0: consume + decode up to N rollouts ahead on a background thread (overlaps
+                                       #     the next iteration's decode with this one's training); 0: inline
 
 
 class Sequence:
@@ -209,8 +212,33 @@ class DotaOptimizer:
 
     # ------------------------------------------------------------------------------------------------
     def get_rollout(self) -> Rollout:
+        """Next decoded rollout: from the decode-ahead thread when ``prefetch_rollouts`` > 0, else inline."""
+        if self.cfg.prefetch_rollouts > 0:
+            pf = getattr(self, '_prefetcher', None)
+            if pf is None:
+                # a blocking client of its own when the broker has one (TCP): the main thread's broker calls
+                # (queue size, model publish) must not wait behind the thread's long polls
+                mk = getattr(self.broker, 'consumer', None)
+                self._xp_broker = mk() if mk is not None else self.broker
+                pf = self._prefetcher = _RolloutPrefetcher(self._consume_decode, self.cfg.prefetch_rollouts)
+            return pf.get()
+        return self._consume_decode()
+
+    def close(self):
+        """Stop the decode-ahead thread (if any); rollouts it already took from the queue are dropped."""
+        pf = getattr(self, '_prefetcher', None)
+        if pf is not None:
+            pf.close()
+            self._prefetcher = None
+            xb = getattr(self, '_xp_broker', None)
+            if xb is not None and xb is not self.broker and hasattr(xb, 'close'):
+                xb.close()
+            self._xp_broker = None
+
+    def _consume_decode(self) -> Rollout:
+        broker = getattr(self, '_xp_broker', None) or self.broker
         while True:
-            body = self.broker.consume_experience(timeout=self.cfg.xp_timeout)
+            body = broker.consume_experience(timeout=self.cfg.xp_timeout)
             if body is None:
                 raise TimeoutError('no experience received')
             try:
@@ -289,12 +317,14 @@ class DotaOptimizer:
         pin = dev.type == 'cuda'
 
         def cat(name, tail, dtype, conv=None):
-            buf = torch.zeros((L,) + tuple(tail), dtype=dtype, pin_memory=pin)
+            buf = self._staging(name, (L,) + tuple(tail), dtype, pin)
             bn = buf.numpy()
-            for r, a in zip(rollouts, off[:-1]):
+            for r, a, b in zip(rollouts, off[:-1], off[1:]):
                 x = getattr(r, name)
-                if x is not None:
-                    bn[a:a + len(x)] = x if conv is None else conv(x)
+                n = 0 if x is None else len(x)
+                if n:
+                    bn[a:a + n] = x if conv is None else conv(x)
+                bn[a + n:b] = 0                     # sequence padding (the staging buffer is reused, not zeroed)
             return buf.to(dev, non_blocking=True)
         r0 = rollouts[0]
         A = r0.actions.shape[1]
@@ -305,9 +335,11 @@ class DotaOptimizer:
         rew = cat('rewards', (r0.rewards.shape[1],), torch.float32)
         gae_mode = cfg.algo == 'ppo' and all(r.values is not None for r in rollouts)
         vals = cat('values', (), torch.float32) if gae_mode else None
-        valid = torch.zeros(L, dtype=torch.float32, pin_memory=pin)
-        for T, a in zip(lens, off[:-1]):
-            valid[a:a + T] = 1.0
+        valid = self._staging('valid', (L,), torch.float32, pin)
+        vn = valid.numpy()
+        for T, a, b in zip(lens, off[:-1], off[1:]):
+            vn[a:a + T] = 1.0
+            vn[a + T:b] = 0.0
         d['valid'] = valid.to(dev, non_blocking=True)
         keys = [self._team_key(r.team_id) for r in rollouts]
         out = compute_returns(rew, vals, off.astype(np.int32), lens, [r.bootstrap_value for r in rollouts],
@@ -335,6 +367,20 @@ class DotaOptimizer:
             d['h0'], d['c0'] = h[:, 0].contiguous(), h[:, 1].contiguous()
         self._normalize_advantages(d)
         return d
+
+    def _staging(self, name: str, shape, dtype, pin: bool) -> torch.Tensor:
+        """Host staging buffer for one ingest field (contents undefined: the caller writes every row), reused across
+        iterations (pinned allocations cost milliseconds each). Safe to overwrite: the previous iteration's uploads
+        were consumed before its training finished (the iteration ends with a device synchronise)."""
+        if not pin:                 # CPU learner: .to(cpu) would alias the buffer into the iteration's data
+            return torch.empty(shape, dtype=dtype)
+        cache = self.__dict__.setdefault('_stage_bufs', {})
+        n = int(np.prod(shape))
+        buf = cache.get(name)
+        if buf is None or buf.dtype != dtype or buf.numel() < n:
+            buf = cache[name] = torch.empty(max(n, 2 * (buf.numel() if buf is not None else 0)), dtype=dtype,
+                                            pin_memory=pin)
+        return buf[:n].view(shape)
 
     def _sync_running(self):
         """Mirror the device EMA state into the host RunningMeanStd (metrics + checkpoint)."""
@@ -377,6 +423,7 @@ class DotaOptimizer:
             for it in range(self.iteration_start, end):
                 self.run_iteration(it)
         finally:
+            self.close()
             self.flush_checkpoints()
             if self.uploader is not None:
                 self.uploader.flush()
@@ -489,6 +536,7 @@ class DotaOptimizer:
                     metrics['entropy'])
         self.last_metrics = metrics
         if self.checkpoint:
+            self.timer.start('log')
             w = self.writer
             w.add_scalars(metrics, it)
             w.add_histogram('losses', loss_t.numpy(), it)
@@ -503,7 +551,10 @@ class DotaOptimizer:
             if qs is not None:
                 w.add_scalar('mq_size', qs, it)
             w.flush()
+            self.timer.stop('log')
+            self.timer.start('publish')
             self.upload_model(version=it)
+            self.timer.stop('publish')
             if self.uploader is not None and w.events_filename:
                 # upload a snapshot: the live events file keeps growing while the uploader copies
                 import shutil
@@ -514,6 +565,8 @@ class DotaOptimizer:
     def upload_model(self, version: int):
         if not self.checkpoint:
             return
+        if self.cfg.async_checkpoint and self.device.type == 'cuda' and version > 0:
+            return self._upload_model_async(version)
         import io
         sd = {k: v.detach().cpu() for k, v in self.policy.state_dict().items()}
         buf = io.BytesIO()
@@ -527,10 +580,39 @@ class DotaOptimizer:
             return
         # publish first (actors see the new weights now); the files follow on one ordered background writer
         self.broker.publish_model(data, version)
+        self._ckpt_pool_get().submit(self._write_checkpoint, data, trainer, version)
+
+    def _ckpt_pool_get(self):
         if getattr(self, '_ckpt_pool', None) is None:
             from concurrent.futures import ThreadPoolExecutor
             self._ckpt_pool = ThreadPoolExecutor(1, thread_name_prefix='ckpt')
-        self._ckpt_pool.submit(self._write_checkpoint, data, trainer, version)
+        return self._ckpt_pool
+
+    def _upload_model_async(self, version: int):
+        """GPU learner with ``async_checkpoint``: the main thread only snapshots the weights and trainer state ON THE
+        DEVICE (clones queued behind this iteration's steps + an event); host copies on a stream of the writer's own,
+        serialisation, the model publish and the files run on the ordered background writer, overlapping the next
+        iteration's ingest and training."""
+        sd = {k: v.detach().clone() for k, v in self.policy.state_dict().items()}
+        trainer = {'learner': _clone_dev(self.learner.state_dict()), 'running': copy.deepcopy(self.running.state_dict()),
+                   'iteration': version, 'config': asdict(self.cfg)}
+        ev = torch.cuda.Event()
+        ev.record()
+        self._ckpt_pool_get().submit(self._publish_snapshot, sd, trainer, ev, version)
+
+    def _publish_snapshot(self, sd, trainer, ev, version: int):
+        import io
+        st = getattr(self, '_pub_stream', None)
+        if st is None:
+            st = self._pub_stream = torch.cuda.Stream(device=self.device)
+        with torch.cuda.stream(st):
+            st.wait_event(ev)
+            sd, trainer = _to_cpu(sd), _to_cpu(trainer)
+        buf = io.BytesIO()
+        torch.save(sd, buf)
+        data = buf.getvalue()
+        self.broker.publish_model(data, version)
+        self._write_checkpoint(data, trainer, version)
 
     def _write_checkpoint(self, data: bytes, trainer, version: int):
         path = ckpt.write_model_bytes(data, self.cfg.log_dir, version)
@@ -540,6 +622,61 @@ class DotaOptimizer:
             self.uploader.submit(spath, f'{self.store_prefix}/{os.path.basename(spath)}')
             self.uploader.flush()       # a pruned file must not vanish before its upload
         ckpt.prune(self.cfg.log_dir, self.cfg.checkpoint_keep)
+
+
+class _RolloutPrefetcher:
+    """Background consume + decode of experience messages into a bounded queue. The learner's main thread then only
+    waits when the actors are behind; DCX1 decode (CRC, array views) and broker waits overlap the GPU training of the
+    previous iteration. An exception in the thread (e.g. the experience timeout) is re-raised by :meth:`get`."""
+
+    def __init__(self, fetch, depth: int):
+        import queue
+        import threading
+        self._queue_mod = queue
+        self.q = queue.Queue(maxsize=max(1, depth))
+        self.fetch = fetch
+        self.err: Optional[BaseException] = None
+        self.stop = threading.Event()
+        self.th = threading.Thread(target=self._run, name='xp-prefetch', daemon=True)
+        self.th.start()
+
+    def _run(self):
+        try:
+            while not self.stop.is_set():
+                r = self.fetch()
+                while not self.stop.is_set():
+                    try:
+                        self.q.put(r, timeout=0.1)
+                        break
+                    except self._queue_mod.Full:
+                        continue
+        except BaseException as e:       # surfaced on the consumer's thread
+            self.err = e
+
+    def get(self) -> Rollout:
+        while True:
+            try:
+                return self.q.get(timeout=0.05)
+            except self._queue_mod.Empty:
+                if self.err is not None:
+                    raise self.err
+                if not self.th.is_alive():
+                    raise RuntimeError('experience prefetch thread exited')
+
+    def close(self):
+        self.stop.set()
+        self.th.join(timeout=5.0)
+
+
+def _clone_dev(x):
+    """Device-side snapshot of a (nested) state dict: tensors cloned on the current stream, the rest as is."""
+    if isinstance(x, torch.Tensor):
+        return x.detach().clone()
+    if isinstance(x, dict):
+        return {k: _clone_dev(v) for k, v in x.items()}
+    if isinstance(x, (list, tuple)):
+        return type(x)(_clone_dev(v) for v in x)
+    return x
 
 
 def _to_cpu(x):

@@ -216,6 +216,11 @@ class TcpBroker:
                 time.sleep(self.retry_delay)
         raise ConnectionError(f'cannot reach broker {self.host}:{self.port}: {last}')
 
+    def consumer(self) -> 'TcpBroker':
+        """A second client on its own connection for a thread that blocks in ``consume_experience`` (the learner's
+        decode-ahead thread), so its long polls never hold this client's lock."""
+        return TcpBroker(self.host, self.port, self.max_retries, self.retry_delay)
+
     def _call(self, op, payload=b''):
         with self._lock:
             for attempt in range(2):

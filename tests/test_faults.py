@@ -63,9 +63,10 @@ def _optimizer(tmp_path, br, **kw):
     return DotaOptimizer(cfg, br)
 
 
-def test_learner_drops_corrupted_messages_and_keeps_training(tmp_path):
+@pytest.mark.parametrize('prefetch', [0, 3])
+def test_learner_drops_corrupted_messages_and_keeps_training(tmp_path, prefetch):
     br = InProcBroker()
-    opt = _optimizer(tmp_path, br)
+    opt = _optimizer(tmp_path, br, prefetch_rollouts=prefetch)
     f = Faults('seed=1')
     for i in range(6):
         body = encode(_rollout(i))
@@ -147,3 +148,14 @@ def test_nan_loss_raises_then_resume_from_checkpoint(tmp_path, monkeypatch):
             assert torch.isfinite(b).all()
     opt2.run(iterations=1)
     assert np.isfinite(opt2.last_metrics['loss/sum'])
+
+
+def test_prefetch_thread_surfaces_the_experience_timeout(tmp_path):
+    """Decode-ahead thread: the broker's experience timeout raised on the thread reaches the learner's caller, and
+    close() stops the thread."""
+    br = InProcBroker()
+    opt = _optimizer(tmp_path, br, prefetch_rollouts=2)
+    opt.cfg.xp_timeout = 0.2
+    with pytest.raises(TimeoutError):
+        opt.run(iterations=1)
+    assert getattr(opt, '_prefetcher', None) is None

@@ -1,0 +1,55 @@
+"""Learner runtime on the GPU with the overlapped host work: decode-ahead thread (``prefetch_rollouts``) and the
+device-snapshot model publish + checkpoint writer (``async_checkpoint``). The published model, the checkpoint file
+and the resumed trainer state must all be the weights of the iteration they are labelled with."""
+import io
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from dotaclient_amd.constants import LAYOUT_1V1
+from dotaclient_amd.transport.broker import InProcBroker
+from dotaclient_amd.transport.codec import Rollout, encode
+
+pytestmark = pytest.mark.gpu
+
+
+def _rollout(i, T=48):
+    rng = np.random.default_rng(i)
+    U, A = LAYOUT_1V1.max_units, 21 + LAYOUT_1V1.max_units
+    act = np.zeros((T, A), np.uint8)
+    act[:, 0] = 1
+    msk = np.zeros((T, A), np.uint8)
+    msk[:, :3] = 1
+    return Rollout(game_id=f'g{i}', team_id=2 + i % 2, player_id=0, weight_version=0,
+                   env=rng.standard_normal((T, 3)).astype(np.float32),
+                   units=rng.standard_normal((T, U, 10)).astype(np.float32), actions=act, masks=msk,
+                   rewards=rng.standard_normal((T, 9)), logp=np.full(T, -1.0, np.float32),
+                   values=np.zeros(T, np.float32), done=True)
+
+
+def test_prefetch_and_async_publish_on_gpu(tmp_path):
+    from dotaclient_amd.learner.optimizer import DotaOptimizer, OptimizerConfig
+    from dotaclient_amd.utils import checkpoint as ckpt
+    br = InProcBroker()
+    for i in range(12):
+        br.publish_experience(encode(_rollout(i)))
+    cfg = OptimizerConfig(log_dir=str(tmp_path), model='lstm128', epochs=1, seq_per_epoch=4, batch_size=2,
+                          seq_len=48, device='cuda', xp_timeout=30, async_checkpoint=True, prefetch_rollouts=3)
+    opt = DotaOptimizer(cfg, br)
+    opt.run(iterations=2)                       # run() joins the writer and stops the decode-ahead thread
+    assert getattr(opt, '_prefetcher', None) is None
+    assert np.isfinite(opt.last_metrics['loss/sum'])
+    live = {k: v.detach().cpu() for k, v in opt.policy.state_dict().items()}
+    version, body = br.latest_model()
+    assert version == 2
+    pub = torch.load(io.BytesIO(body), weights_only=True)
+    disk = ckpt.load_model_file(os.path.join(str(tmp_path), 'model_000000002.pt'))
+    for k, v in live.items():
+        assert torch.equal(pub[k], v), k
+        assert torch.equal(disk[k], v), k
+    opt2 = DotaOptimizer(cfg, InProcBroker())
+    assert opt2.iteration_start == 3
+    torch.testing.assert_close(opt2.learner.opt.exp_avg, opt.learner.opt.exp_avg)
+    torch.testing.assert_close(opt2.learner.opt.exp_avg_sq, opt.learner.opt.exp_avg_sq)
