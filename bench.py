@@ -56,6 +56,8 @@ def parse():
     ap.add_argument('--e2e', type=float, default=20.0,
                     help='seconds of the end-to-end actors→queue→learner loop on GPU 0 (1-GPU runs; 0 = off)')
     ap.add_argument('--e2e-games', type=int, default=1024)
+    ap.add_argument('--e2e-mode', default='process', choices=['process', 'thread'],
+                    help='e2e actor as a spawned process over the shm broker (deploy split) or as a thread')
     from dotaclient_amd.presets import parse_with_preset
     return parse_with_preset(ap, 'bench')
 
@@ -173,9 +175,10 @@ def main():
         # real loop: VecActor → queue → DotaOptimizer (deploy shape 8×1400, 16 seq/iteration) → model → VecActor
         learner = None
         try:
-            from dotaclient_amd.learner.e2e import measure_e2e
-            e2e = measure_e2e(model=args.model, device=device, duration=args.e2e, games=args.e2e_games,
-                              threads=args.actor_threads, seq_len=args.seq_len, precision=args.precision)
+            from dotaclient_amd.learner.e2e import measure_e2e, measure_e2e_procs
+            fn = measure_e2e_procs if args.e2e_mode == 'process' else measure_e2e
+            e2e = fn(model=args.model, device=device, duration=args.e2e, games=args.e2e_games,
+                     threads=args.actor_threads, seq_len=args.seq_len, precision=args.precision)
         except Exception as e:
             e2e = {'error': repr(e)}
 

@@ -74,32 +74,10 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
 
     th = threading.Thread(target=actor_loop, name='vec-actor', daemon=True)
     th.start()
-    rows = []
     try:
-        it = opt.iteration_start
-        for _ in range(warmup_iterations):
-            opt.run_iteration(it)
-            it += 1
-            if err:
-                raise err[0]
-        t0 = time.perf_counter()
-        s0, d0 = va.steps_taken, broker.n_dropped
-        opt.time_last_step = time.time()
-        while time.perf_counter() - t0 < duration and (max_iterations is None or len(rows) < max_iterations):
-            opt.run_iteration(it)
-            it += 1
-            m = opt.last_metrics
-            rows.append((m[DotaOptimizer.SPEED_KEY], m['avg_weight_age'], m['avg_rollout_len'],
-                         m.get('time/train', float('nan')), m.get('time/ingest', float('nan')), m['experience_steps'],
-                         m.get('time/h2d', float('nan')), m.get('time/log', float('nan')),
-                         m.get('time/publish', float('nan'))))
-            if err:
-                raise err[0]
-        if opt.device.type == 'cuda':
-            torch.cuda.synchronize(opt.device)
-        wall = time.perf_counter() - t0
-        actor_steps = va.steps_taken - s0
-        dropped = broker.n_dropped - d0
+        rows, wall, (actor_steps, dropped) = _learner_loop(
+            opt, duration, warmup_iterations, max_iterations,
+            counters=lambda: (va.steps_taken, broker.n_dropped), check=lambda: err and err[0])
     finally:
         stop.set()
         opt.close()
@@ -109,6 +87,46 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
         loader.shutdown(wait=True)
         if log_dir is None:
             shutil.rmtree(tmp, ignore_errors=True)
+    return _summary(rows, wall, actor_steps, dropped, games, dict(
+        batch_size=batch_size, seq_len=seq_len, seq_per_epoch=seq_per_epoch, epochs=epochs, rollout_size=rollout_size,
+        max_dota_time=max_dota_time, precision=precision, prefetch_rollouts=prefetch, actor='thread'))
+
+
+def _learner_loop(opt, duration, warmup_iterations, max_iterations, counters, check):
+    """Run learner iterations for ``duration`` seconds after ``warmup_iterations``; per-iteration metric rows, the
+    wall time and the (actor steps, dropped rollouts) deltas of the window."""
+    from .optimizer import DotaOptimizer
+    rows = []
+    it = opt.iteration_start
+    for _ in range(warmup_iterations):
+        opt.run_iteration(it)
+        it += 1
+        e = check()
+        if e:
+            raise e
+    t0 = time.perf_counter()
+    c0 = counters()
+    opt.time_last_step = time.time()
+    while time.perf_counter() - t0 < duration and (max_iterations is None or len(rows) < max_iterations):
+        opt.run_iteration(it)
+        it += 1
+        m = opt.last_metrics
+        rows.append((m[DotaOptimizer.SPEED_KEY], m['avg_weight_age'], m['avg_rollout_len'],
+                     m.get('time/train', float('nan')), m.get('time/ingest', float('nan')), m['experience_steps'],
+                     m.get('time/h2d', float('nan')), m.get('time/log', float('nan')),
+                     m.get('time/publish', float('nan'))))
+        e = check()
+        if e:
+            raise e
+    if opt.device.type == 'cuda':
+        torch.cuda.synchronize(opt.device)
+    wall = time.perf_counter() - t0
+    c1 = counters()
+    return rows, wall, (c1[0] - c0[0], c1[1] - c0[1])
+
+
+def _summary(rows, wall, actor_steps, dropped, games, config):
+    seq_per_epoch, seq_len = config['seq_per_epoch'], config['seq_len']
     a = np.asarray(rows, dtype=np.float64)
     n_it = len(rows)
     padded = n_it * seq_per_epoch * seq_len
@@ -125,8 +143,101 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
         'log_ms_per_iteration': 1e3 * float(a[:, 7].mean()) if n_it else float('nan'),
         'publish_ms_per_iteration': 1e3 * float(a[:, 8].mean()) if n_it else float('nan'),
         'actor_steps_per_s': actor_steps / wall,
-        'queue_dropped': int(dropped), 'games': games,
-        'config': {'batch_size': batch_size, 'seq_len': seq_len, 'seq_per_epoch': seq_per_epoch, 'epochs': epochs,
-                   'rollout_size': rollout_size, 'max_dota_time': max_dota_time, 'precision': precision,
-                   'prefetch_rollouts': prefetch},
+        'queue_dropped': int(dropped), 'games': games, 'config': config,
     }
+
+
+def _actor_process_main(name: str, model: str, games: int, threads: int, seq_len: int, rollout_size: int,
+                        max_dota_time: float, device: str, seed: int, stop, ready, steps, failed):
+    """Actor role of :func:`measure_e2e_procs`: a process of its own (own interpreter and GIL) that plays ``games``
+    VecActor games on the GPU, pushes whole-game rollouts into the node's shared-memory experience ring and hot-swaps
+    every model the learner publishes into that broker's model slot."""
+    try:
+        from ..actor.vec import VecActor
+        from ..actor.weights import WeightStore
+        from ..transport.shm import ShmBroker
+        br = ShmBroker(name, create=False, drop_oldest=True)
+        ws = WeightStore(model, device='cpu')
+        m = br.latest_model(timeout=120.0)
+        if m is None:
+            raise TimeoutError('no model published by the learner')
+        ws.add_bytes(*m)
+        br.subscribe_model(lambda v, b: ws.add_bytes(v, b), poll=0.005)
+        va = VecActor(ws, games, br.publish_experience, device=device, seed=seed, rollout_size=rollout_size,
+                      max_dota_time=max_dota_time, hidden_stride=seq_len, threads=threads, stagger=True)
+        for _ in range(3):
+            va.step()
+        ready.set()
+        while not stop.is_set():
+            va.step()
+            steps.value = va.steps_taken
+        va.close()
+        br.close()
+    except BaseException:
+        import traceback
+        traceback.print_exc()
+        failed.set()
+        ready.set()
+
+
+def measure_e2e_procs(model: str = 'lstm512', device='cuda', duration: float = 20.0, games: int = 1024,
+                      threads: int = 14, seq_len: int = 1400, batch_size: int = 8, seq_per_epoch: int = 16,
+                      epochs: int = 1, precision: str = 'fp32', max_dota_time: float = 600.0,
+                      rollout_size: int = 9999, warmup_iterations: int = 2, max_iterations: Optional[int] = None,
+                      log_dir: Optional[str] = None, prefetch: int = 32, ring_bytes: int = 1 << 26
+                      ) -> Dict[str, float]:
+    """:func:`measure_e2e` with the deploy's process split: the actor in a process of its own (spawned, same GPU)
+    and the learner here, exchanging rollouts and models through the node-local shared-memory broker
+    (``transport/shm.py``: native MPMC ring + model slot) instead of in-process queues — no GIL shared between the
+    actor's host loop and the learner's ingest / publish threads. The ring holds ``ring_bytes`` (64 MB ≈ the thread
+    variant's 64-rollout queue at the deploy's mean rollout size; the oldest rollouts are dropped when it is full),
+    which bounds the experience's weight age."""
+    import multiprocessing as mp
+    import os
+    from ..transport.shm import ShmBroker
+    from .optimizer import DotaOptimizer, OptimizerConfig
+
+    tmp = log_dir or tempfile.mkdtemp(prefix='dca_e2e_')
+    name = f'dca_e2e_{os.getpid()}_{int(time.time() * 1e3) % 10 ** 9}'
+    broker = ShmBroker(name, capacity=ring_bytes, create=True, drop_oldest=True)
+    ctx = mp.get_context('spawn')
+    stop, ready, failed = ctx.Event(), ctx.Event(), ctx.Event()
+    steps = ctx.Value('q', 0)
+    proc = None
+    try:
+        cfg = OptimizerConfig(log_dir=tmp, epochs=epochs, seq_per_epoch=seq_per_epoch, batch_size=batch_size,
+                              seq_len=seq_len, model=model, precision=precision, device=str(device),
+                              checkpoint_keep=2, run_local=True, xp_timeout=300.0, histogram_freq=10 ** 9,
+                              async_checkpoint=True, prefetch_rollouts=prefetch)
+        opt = DotaOptimizer(cfg, broker)                   # publishes model version 0 into the shm model slot
+        proc = ctx.Process(target=_actor_process_main, name='e2e-actor', daemon=True,
+                           args=(name, model, games, threads, seq_len, rollout_size, max_dota_time, str(device), 11,
+                                 stop, ready, steps, failed))
+        proc.start()
+        if not ready.wait(timeout=600) or failed.is_set():
+            raise RuntimeError('e2e actor process failed to start')
+
+        def check():
+            if failed.is_set() or not proc.is_alive():
+                return RuntimeError('e2e actor process died')
+            return None
+        try:
+            rows, wall, (actor_steps, _) = _learner_loop(opt, duration, warmup_iterations, max_iterations,
+                                                         counters=lambda: (steps.value, 0), check=check)
+        finally:
+            opt.close()
+            opt.flush_checkpoints()
+    finally:
+        stop.set()
+        if proc is not None:
+            proc.join(timeout=60)
+            if proc.is_alive():
+                proc.kill()
+                proc.join(timeout=10)
+        broker.close(unlink=True)
+        if log_dir is None:
+            shutil.rmtree(tmp, ignore_errors=True)
+    out = _summary(rows, wall, actor_steps, -1, games, dict(
+        batch_size=batch_size, seq_len=seq_len, seq_per_epoch=seq_per_epoch, epochs=epochs, rollout_size=rollout_size,
+        max_dota_time=max_dota_time, precision=precision, prefetch_rollouts=prefetch, actor='process (shm broker)'))
+    return out

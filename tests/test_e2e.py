@@ -15,3 +15,17 @@ def test_e2e_actor_learner_loop_cpu():
     # models flow back to the actor: rollouts are at most a few versions old
     assert 0 <= r['avg_weight_age'] < 4
     assert r['actor_steps_per_s'] > 0
+
+
+def test_e2e_actor_process_over_shm_cpu():
+    """The deploy's process split: VecActor in a spawned process, rollouts and models through the shared-memory
+    broker (native ring + model slot), the learner here."""
+    import glob
+    from dotaclient_amd.learner.e2e import measure_e2e_procs
+    before = set(glob.glob('/dev/shm/dca_e2e_*'))
+    r = measure_e2e_procs(model='lstm128', device='cpu', duration=60.0, max_iterations=3, games=8, threads=2,
+                          seq_len=64, batch_size=4, seq_per_epoch=8, max_dota_time=20.0, warmup_iterations=1)
+    assert r['iterations'] == 3
+    assert r['steps_per_s'] > 0 and r['actor_steps_per_s'] > 0
+    assert 0 <= r['avg_weight_age'] < 8
+    assert set(glob.glob('/dev/shm/dca_e2e_*')) == before          # ring and model slot unlinked
