@@ -403,13 +403,6 @@ class FusedPolicy:
             self._toff, self._toff_key = torch.tensor(offs, dtype=torch.int32, device=device), key
         return self._toff
 
-    def no_bias(self, device):
-        """Empty f32 device tensor: "no b_sub" for the fp32 LayerNorm kernels (bt is not folded with b_out there)."""
-        key = str(device)
-        if getattr(self, '_nob_key', None) != key:
-            self._nob, self._nob_key = torch.empty(0, device=device), key
-        return self._nob
-
     def unit_types(self, device):
         """(U,) uint8 device tensor: unit slot → unit type index, cached."""
         key = str(device)

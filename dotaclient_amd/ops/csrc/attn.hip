@@ -103,11 +103,13 @@ template <typename T>
 __global__ __launch_bounds__(256) void ln_fwd_kernel(const T* __restrict__ e0, const float* __restrict__ bsub,
                                                      const float* __restrict__ gamma, const float* __restrict__ beta,
                                                      T* __restrict__ xn, float* __restrict__ mean,
-                                                     float* __restrict__ rstd, int R, float eps) {
+                                                     float* __restrict__ rstd, int R, float eps,
+                                                     T* __restrict__ e0_copy) {
   const int row = blockIdx.x * 16 + (threadIdx.x >> 4), c0 = (threadIdx.x & 15) * 8;
   if (row >= R) return;
   float x[8], s = 0.f;
   ld8(e0 + (size_t)row * kD + c0, x);
+  if (e0_copy) st8(e0_copy + (size_t)row * kD + c0, x);   // optional copy of the input (saved for the backward)
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     if (bsub) x[j] -= bsub[c0 + j];
@@ -465,9 +467,14 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
 // (A[m = i][k = j]: m = lane&15, k = 4(lane>>4) + r) — so O = P·V takes P straight from the score registers. The
 // backward keeps the i-major S = Q·Kᵀ layout instead (lane (i = 16a + 4kg + r, j = 16b + li) = A[m = j][k = i]) for
 // ∂V = Pᵀ∂O and ∂K = ∂Sᵀ Q, and passes ∂S through LDS (hi / lo images, transposed reads) only for ∂Q = ∂S K.
-__device__ __forceinline__ void split8(const float* __restrict__ p, bf16x8& hi, bf16x8& lo) {
+__device__ __forceinline__ void split8(const float* __restrict__ p, bf16x8& hi, bf16x8& lo,
+                                       const float* bias8 = nullptr) {
   const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-  const float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  if (bias8) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] += bias8[j];
+  }
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
     hi[j] = dca::f2bf(v[j]);
@@ -498,11 +505,20 @@ __device__ __forceinline__ f32x4 mfma3k16(const bf16x4v& ah, const bf16x4v& al, 
 }
 
 // Forward, one wave per (row n, head h) = blockIdx.x · 4 + h. qkv (N·64, 384) f32 → o (N·64, 128) f32, lse (N,4,64).
-__global__ __launch_bounds__(64) void attn_fwd_f32_kernel(const float* __restrict__ qkv, float* __restrict__ o,
-                                                          float* __restrict__ lse, float scale) {
+__global__ __launch_bounds__(64) void attn_fwd_f32_kernel(const float* __restrict__ qkv, const float* __restrict__ bq,
+                                                          float* __restrict__ o, float* __restrict__ lse, float scale) {
   const int n = blockIdx.x >> 2, h = blockIdx.x & 3;
   const int l = threadIdx.x, kg = l >> 4, li = l & 15;
   const float* base = qkv + (size_t)n * kU * 384 + h * kHd;
+  // QKV projection bias (384, added here: hipBLASLt's bias-epilogue GEMM is 1.7x slower than the plain one)
+  float qb[8], kb8[8], vb[2];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    qb[j] = bq[h * kHd + 8 * kg + j];
+    kb8[j] = bq[128 + h * kHd + 8 * kg + j];
+  }
+  vb[0] = bq[256 + h * kHd + li];
+  vb[1] = bq[256 + h * kHd + 16 + li];
   // V operand of O = P·V (B[k = j][n = d]): lane needs V[16b + 4kg + r][16c + li] — issued first, used last
   float vr[4][2][4];
 #pragma unroll
@@ -510,16 +526,16 @@ __global__ __launch_bounds__(64) void attn_fwd_f32_kernel(const float* __restric
 #pragma unroll
     for (int c = 0; c < 2; ++c)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) vr[b][c][r] = base[(size_t)(16 * b + 4 * kg + r) * 384 + 256 + 16 * c + li];
+      for (int r = 0; r < 4; ++r) vr[b][c][r] = base[(size_t)(16 * b + 4 * kg + r) * 384 + 256 + 16 * c + li] + vb[c];
   bf16x8 qh[4], ql[4];
 #pragma unroll
-  for (int a = 0; a < 4; ++a) split8(base + (size_t)(16 * a + li) * 384 + 8 * kg, qh[a], ql[a]);
+  for (int a = 0; a < 4; ++a) split8(base + (size_t)(16 * a + li) * 384 + 8 * kg, qh[a], ql[a], qb);
   // Sᵀ tiles: s[b][a] lane (key j = 16b + 4kg + r, query i = 16a + li)
   f32x4 s[4][4];
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
     bf16x8 kh, kl;
-    split8(base + 128 + (size_t)(16 * b + li) * 384 + 8 * kg, kh, kl);
+    split8(base + 128 + (size_t)(16 * b + li) * 384 + 8 * kg, kh, kl, kb8);
 #pragma unroll
     for (int a = 0; a < 4; ++a) s[b][a] = mfma3(kh, kl, qh[a], ql[a], f32x4{0.f, 0.f, 0.f, 0.f});
   }
@@ -573,7 +589,8 @@ __global__ __launch_bounds__(64) void attn_fwd_f32_kernel(const float* __restric
 }
 
 // Backward, one wave per (row, head). do_ (N·64, 128) f32 = ∂O; writes dqkv (N·64, 384) f32.
-__global__ __launch_bounds__(64) void attn_bwd_f32_kernel(const float* __restrict__ qkv, const float* __restrict__ o,
+__global__ __launch_bounds__(64) void attn_bwd_f32_kernel(const float* __restrict__ qkv, const float* __restrict__ bq,
+                                                          const float* __restrict__ o,
                                                           const float* __restrict__ do_, const float* __restrict__ lse,
                                                           float* __restrict__ dqkv, float scale) {
   __shared__ __attribute__((aligned(16))) short STh[kU * kP64], STl[kU * kP64];   // (scale·∂S)ᵀ hi / lo, [j][i]
@@ -583,6 +600,13 @@ __global__ __launch_bounds__(64) void attn_bwd_f32_kernel(const float* __restric
   const float* base = qkv + (size_t)n * kU * 384 + h * kHd;
   const float* dob = do_ + (size_t)n * kU * kD + h * kHd;
   const float* ob = o + (size_t)n * kU * kD + h * kHd;
+  float qb[8], kb8[8], vb8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    qb[j] = bq[h * kHd + 8 * kg + j];
+    kb8[j] = bq[128 + h * kHd + 8 * kg + j];
+    vb8[j] = bq[256 + h * kHd + 8 * kg + j];
+  }
   // D_i = Σ_d ∂O[i][d]·O[i][d] for i = 16a + li (lane group kg sums d = 8kg … 8kg + 7), LSE
 #pragma unroll
   for (int a = 0; a < 4; ++a) {
@@ -603,14 +627,14 @@ __global__ __launch_bounds__(64) void attn_bwd_f32_kernel(const float* __restric
     bf16x8 qh[4], ql[4], dh[4], dl[4];
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
-      split8(base + (size_t)(16 * a + li) * 384 + 8 * kg, qh[a], ql[a]);
+      split8(base + (size_t)(16 * a + li) * 384 + 8 * kg, qh[a], ql[a], qb);
       split8(dob + (size_t)(16 * a + li) * kD + 8 * kg, dh[a], dl[a]);
     }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       bf16x8 kh, kl, vh, vl;
-      split8(base + 128 + (size_t)(16 * b + li) * 384 + 8 * kg, kh, kl);
-      split8(base + 256 + (size_t)(16 * b + li) * 384 + 8 * kg, vh, vl);
+      split8(base + 128 + (size_t)(16 * b + li) * 384 + 8 * kg, kh, kl, kb8);
+      split8(base + 256 + (size_t)(16 * b + li) * 384 + 8 * kg, vh, vl, vb8);
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
         p[a][b] = mfma3(qh[a], ql[a], kh, kl, f32x4{0.f, 0.f, 0.f, 0.f});
@@ -647,6 +671,7 @@ __global__ __launch_bounds__(64) void attn_bwd_f32_kernel(const float* __restric
   // 16a + 4kg + r of ∂O / Q at column 16c + li
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
+    const float qbc = bq[h * kHd + 16 * c + li];
     bf16x4v doh[4], dol[4], qh[4], ql[4];
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
@@ -654,7 +679,7 @@ __global__ __launch_bounds__(64) void attn_bwd_f32_kernel(const float* __restric
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         dv[r] = dob[(size_t)(16 * a + 4 * kg + r) * kD + 16 * c + li];
-        qv[r] = base[(size_t)(16 * a + 4 * kg + r) * 384 + 16 * c + li];
+        qv[r] = base[(size_t)(16 * a + 4 * kg + r) * 384 + 16 * c + li] + qbc;
       }
       split4(dv[0], dv[1], dv[2], dv[3], doh[a], dol[a]);
       split4(qv[0], qv[1], qv[2], qv[3], qh[a], ql[a]);
@@ -683,12 +708,13 @@ __global__ __launch_bounds__(64) void attn_bwd_f32_kernel(const float* __restric
   // 32ks + 8kg … +7 at column 16c + li
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
+    const float kbc = bq[128 + h * kHd + 16 * c + li];
     bf16x8 kh[2], kl[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
-        const float v = base[(size_t)(32 * ks + 8 * kg + jj) * 384 + 128 + 16 * c + li];
+        const float v = base[(size_t)(32 * ks + 8 * kg + jj) * 384 + 128 + 16 * c + li] + kbc;
         kh[ks][jj] = dca::f2bf(v);
         kl[ks][jj] = dca::f2bf(v - dca::bf2f(kh[ks][jj]));
       }
@@ -707,15 +733,16 @@ __global__ __launch_bounds__(64) void attn_bwd_f32_kernel(const float* __restric
 
 }  // namespace
 
-extern "C" hipError_t dca_attn_fwd_f32(const float* qkv, float* o, float* lse, int N, float scale, hipStream_t st) {
-  hipLaunchKernelGGL(attn_fwd_f32_kernel, dim3(N * 4), dim3(64), 0, st, qkv, o, lse, scale);
+extern "C" hipError_t dca_attn_fwd_f32(const float* qkv, const float* bq, float* o, float* lse, int N, float scale,
+                                       hipStream_t st) {
+  hipLaunchKernelGGL(attn_fwd_f32_kernel, dim3(N * 4), dim3(64), 0, st, qkv, bq, o, lse, scale);
   DCA_CHECK_LAUNCH();
   return hipSuccess;
 }
 
-extern "C" hipError_t dca_attn_bwd_f32(const float* qkv, const float* o, const float* dout, const float* lse,
-                                       float* dqkv, int N, float scale, hipStream_t st) {
-  hipLaunchKernelGGL(attn_bwd_f32_kernel, dim3(N * 4), dim3(64), 0, st, qkv, o, dout, lse, dqkv, scale);
+extern "C" hipError_t dca_attn_bwd_f32(const float* qkv, const float* bq, const float* o, const float* dout,
+                                       const float* lse, float* dqkv, int N, float scale, hipStream_t st) {
+  hipLaunchKernelGGL(attn_bwd_f32_kernel, dim3(N * 4), dim3(64), 0, st, qkv, bq, o, dout, lse, dqkv, scale);
   DCA_CHECK_LAUNCH();
   return hipSuccess;
 }
@@ -723,13 +750,13 @@ extern "C" hipError_t dca_attn_bwd_f32(const float* qkv, const float* o, const f
 extern "C" int dca_ln_part_width() { return kLnPart; }
 
 extern "C" hipError_t dca_ln_fwd(const void* e0, const float* bsub, const float* gamma, const float* beta, void* xn,
-                                 float* mean, float* rstd, int R, float eps, int f32, hipStream_t st) {
+                                 float* mean, float* rstd, int R, float eps, int f32, void* e0_copy, hipStream_t st) {
   if (f32)
     hipLaunchKernelGGL(ln_fwd_kernel<float>, dim3((R + 15) / 16), dim3(256), 0, st, (const float*)e0, bsub, gamma,
-                       beta, (float*)xn, mean, rstd, R, eps);
+                       beta, (float*)xn, mean, rstd, R, eps, (float*)e0_copy);
   else
     hipLaunchKernelGGL(ln_fwd_kernel<short>, dim3((R + 15) / 16), dim3(256), 0, st, (const short*)e0, bsub, gamma,
-                       beta, (short*)xn, mean, rstd, R, eps);
+                       beta, (short*)xn, mean, rstd, R, eps, (short*)e0_copy);
   DCA_CHECK_LAUNCH();
   return hipSuccess;
 }

@@ -580,7 +580,7 @@ std::vector<torch::Tensor> enc_small_grads(torch::Tensor z, torch::Tensor dtl, t
 
 // ---- 5v5 entity-attention block (ops/csrc/attn.hip); 64 unit slots, width 128, 4 heads × 32 -------------------
 std::vector<torch::Tensor> ln_fwd(torch::Tensor e0, torch::Tensor bsub, torch::Tensor gamma, torch::Tensor beta,
-                                  double eps) {
+                                  double eps, c10::optional<torch::Tensor> e0_copy) {
   // bf16 learner: bf16 E0' with b_sub; fp32 learner: fp32 E0, b_sub an empty tensor (no subtraction)
   const bool f32 = e0.scalar_type() == at::kFloat;
   if (f32) { CHECK_F32(e0); } else { CHECK_BF16(e0); }
@@ -592,31 +592,51 @@ std::vector<torch::Tensor> ln_fwd(torch::Tensor e0, torch::Tensor bsub, torch::T
   auto xn = torch::empty({R, 128}, e0.options());
   auto mean = torch::empty({R}, gamma.options());
   auto rstd = torch::empty({R}, gamma.options());
+  void* cp = nullptr;
+  if (e0_copy.has_value() && e0_copy->defined()) {
+    TORCH_CHECK(e0_copy->scalar_type() == e0.scalar_type() && e0_copy->is_contiguous() && e0_copy->numel() == R * 128,
+                "e0_copy must be a contiguous tensor like e0");
+    cp = e0_copy->data_ptr();
+  }
   hip_check(dca_ln_fwd(e0.data_ptr(), bsub.numel() ? ptr<float>(bsub) : nullptr, ptr<float>(gamma), ptr<float>(beta),
-                       xn.data_ptr(), ptr<float>(mean), ptr<float>(rstd), (int)R, (float)eps, f32 ? 1 : 0,
+                       xn.data_ptr(), ptr<float>(mean), ptr<float>(rstd), (int)R, (float)eps, f32 ? 1 : 0, cp,
                        cur_stream()),
             "dca_ln_fwd");
   return {xn, mean, rstd};
 }
 
-std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv) {
+// fp32 variants: qkv WITHOUT its bias (the kernels add bqkv on load; zeros when absent)
+static torch::Tensor qkv_bias(const torch::Tensor& qkv, const c10::optional<torch::Tensor>& bqkv) {
+  if (bqkv.has_value() && bqkv->defined()) {
+    CHECK_F32((*bqkv));
+    TORCH_CHECK(bqkv->numel() == 384, "bqkv must hold 384 floats");
+    return *bqkv;
+  }
+  return torch::zeros({384}, qkv.options().dtype(at::kFloat));
+}
+
+std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, c10::optional<torch::Tensor> bqkv) {
   TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) == 384 && qkv.size(0) % 64 == 0, "qkv must be (N*64, 384)");
   const int N = qkv.size(0) / 64;
   auto o = torch::empty({(int64_t)N * 64, 128}, qkv.options());
   auto lse = torch::empty({(int64_t)N, 4, 64}, qkv.options().dtype(at::kFloat));
   if (qkv.scalar_type() == at::kFloat) {   // fp32 learner: bf16x3 split-MFMA kernel
     CHECK_F32(qkv);
-    hip_check(dca_attn_fwd_f32(ptr<float>(qkv), ptr<float>(o), ptr<float>(lse), N, 1.f / sqrtf(32.f), cur_stream()),
+    auto b = qkv_bias(qkv, bqkv);
+    hip_check(dca_attn_fwd_f32(ptr<float>(qkv), ptr<float>(b), ptr<float>(o), ptr<float>(lse), N, 1.f / sqrtf(32.f),
+                               cur_stream()),
               "dca_attn_fwd_f32");
     return {o, lse};
   }
+  TORCH_CHECK(!(bqkv.has_value() && bqkv->defined()), "attn_fwd: the bf16 kernel takes qkv with its bias");
   CHECK_BF16(qkv);
   hip_check(dca_attn_fwd(ptr<short>(qkv), ptr<short>(o), ptr<float>(lse), N, 1.f / sqrtf(32.f), cur_stream()),
             "dca_attn_fwd");
   return {o, lse};
 }
 
-torch::Tensor attn_bwd(torch::Tensor qkv, torch::Tensor o, torch::Tensor dout, torch::Tensor lse) {
+torch::Tensor attn_bwd(torch::Tensor qkv, torch::Tensor o, torch::Tensor dout, torch::Tensor lse,
+                       c10::optional<torch::Tensor> bqkv) {
   CHECK_F32(lse);
   TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) == 384 && qkv.size(0) % 64 == 0, "qkv must be (N*64, 384)");
   const int N = qkv.size(0) / 64;
@@ -625,8 +645,9 @@ torch::Tensor attn_bwd(torch::Tensor qkv, torch::Tensor o, torch::Tensor dout, t
   auto dqkv = torch::empty_like(qkv);
   if (qkv.scalar_type() == at::kFloat) {
     CHECK_F32(qkv); CHECK_F32(o); CHECK_F32(dout);
-    hip_check(dca_attn_bwd_f32(ptr<float>(qkv), ptr<float>(o), ptr<float>(dout), ptr<float>(lse), ptr<float>(dqkv), N,
-                               1.f / sqrtf(32.f), cur_stream()),
+    auto b = qkv_bias(qkv, bqkv);
+    hip_check(dca_attn_bwd_f32(ptr<float>(qkv), ptr<float>(b), ptr<float>(o), ptr<float>(dout), ptr<float>(lse),
+                               ptr<float>(dqkv), N, 1.f / sqrtf(32.f), cur_stream()),
               "dca_attn_bwd_f32");
     return dqkv;
   }
@@ -786,9 +807,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("A"), py::arg("B"), py::arg("C"), py::arg("perm") = py::none(), py::arg("accumulate") = false,
         py::arg("B0") = py::none(), py::arg("colsum") = py::none());
   m.def("enc_small_grads", &enc_small_grads, "entity-encoder type-bias and env-layer gradients in one pass");
-  m.def("ln_fwd", &ln_fwd, "LayerNorm(E0 - bsub) -> (xn, mean, rstd); bf16, or fp32 (bsub may be empty)");
-  m.def("attn_fwd", &attn_fwd, "entity self-attention per (row, head): (o, lse); bf16, or fp32 (bf16x3 MFMA)");
-  m.def("attn_bwd", &attn_bwd, "entity self-attention backward: dqkv");
+  m.def("ln_fwd", &ln_fwd, "LayerNorm(E0 - bsub) -> (xn, mean, rstd); bf16, or fp32 (bsub may be empty); optional copy of E0",
+        py::arg("e0"), py::arg("bsub"), py::arg("gamma"), py::arg("beta"), py::arg("eps"),
+        py::arg("e0_copy") = py::none());
+  m.def("attn_fwd", &attn_fwd, "entity self-attention per (row, head): (o, lse); bf16, or fp32 (bf16x3 MFMA, qkv bias "
+        "added on load)", py::arg("qkv"), py::arg("bqkv") = py::none());
+  m.def("attn_bwd", &attn_bwd, "entity self-attention backward: dqkv", py::arg("qkv"), py::arg("o"), py::arg("dout"),
+        py::arg("lse"), py::arg("bqkv") = py::none());
   m.def("attn_pool", &attn_pool, "per-type max-pool + argmax of attended embeddings into x896");
   m.def("attn_demb", &attn_demb, "dE1 = dtl*q + pool gradient at the argmax unit (bf16 or f32 out)");
   m.def("ln_bwd", &ln_bwd, "LayerNorm backward + residual: (dE0, dgamma, dbeta, dbt)");

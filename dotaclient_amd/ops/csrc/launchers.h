@@ -86,11 +86,11 @@ hipError_t dca_enc_small_grads(const float* z, int ldz, const float* dtl, int U,
 
 int dca_ln_part_width();
 hipError_t dca_ln_fwd(const void* e0, const float* bsub, const float* gamma, const float* beta, void* xn, float* mean,
-                      float* rstd, int R, float eps, int f32, hipStream_t st);
+                      float* rstd, int R, float eps, int f32, void* e0_copy, hipStream_t st);
 hipError_t dca_attn_fwd(const short* qkv, short* o, float* lse, int N, float scale, hipStream_t st);
-hipError_t dca_attn_fwd_f32(const float* qkv, float* o, float* lse, int N, float scale, hipStream_t st);
-hipError_t dca_attn_bwd_f32(const float* qkv, const float* o, const float* dout, const float* lse, float* dqkv, int N,
-                            float scale, hipStream_t st);
+hipError_t dca_attn_fwd_f32(const float* qkv, const float* bq, float* o, float* lse, int N, float scale, hipStream_t st);
+hipError_t dca_attn_bwd_f32(const float* qkv, const float* bq, const float* o, const float* dout, const float* lse,
+                            float* dqkv, int N, float scale, hipStream_t st);
 hipError_t dca_attn_bwd(const short* qkv, const short* o, const short* dout, const float* lse, short* dqkv, int N,
                         float scale, hipStream_t st);
 hipError_t dca_attn_pool(const void* e1, const int* type_off, void* x896, unsigned char* arg, int N, int compat,

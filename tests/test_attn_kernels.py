@@ -63,9 +63,10 @@ def test_attn_fwd_bwd_f32(gpu_ops):
     """fp32 attention core (bf16x3 split MFMA, fp32 softmax) vs an fp64 reference: fp32-class accuracy."""
     g = _g(2)
     qkv = torch.randn(N * U, 3 * D, device='cuda', generator=g) * 1.5       # peaky rows as well as flat ones
-    o, lse = gpu_ops.attn_fwd(qkv)
+    bq = torch.randn(3 * D, device='cuda', generator=g) * 0.5                # added by the kernels on load
+    o, lse = gpu_ops.attn_fwd(qkv, bq)
     assert o.dtype == torch.float32
-    x = qkv.double().requires_grad_(True)
+    x = (qkv + bq).double().requires_grad_(True)
     q, k, v = x.view(N, U, 3, NH, HD).unbind(2)
     q, k, v = (t.transpose(1, 2) for t in (q, k, v))
     s = q @ k.transpose(-1, -2) / HD ** 0.5
@@ -74,7 +75,7 @@ def test_attn_fwd_bwd_f32(gpu_ops):
     assert rel(o, o_ref.detach()) < 2e-5
     torch.testing.assert_close(lse.double(), torch.logsumexp(s, -1).detach(), rtol=1e-5, atol=1e-5)
     dout = torch.randn(N * U, D, device='cuda', generator=g)
-    dqkv = gpu_ops.attn_bwd(qkv, o, dout, lse)
+    dqkv = gpu_ops.attn_bwd(qkv, o, dout, lse, bq)
     o_ref.backward(dout.double())
     for part in range(3):   # q, k, v blocks each
         a, b = dqkv[:, part * D:(part + 1) * D], x.grad[:, part * D:(part + 1) * D]
@@ -143,8 +144,12 @@ def test_block_kernels_f32(gpu_ops, compat):
     gamma = 1 + 0.1 * torch.randn(D, device='cuda', generator=g)
     beta = 0.1 * torch.randn(D, device='cuda', generator=g)
     nob = torch.empty(0, device='cuda')
-    xn, mean, rstd = gpu_ops.ln_fwd(e0, nob, gamma, beta, 1e-5)
-    assert xn.dtype == torch.float32
+    cp = torch.empty_like(e0)
+    xn, mean, rstd = gpu_ops.ln_fwd(e0, nob, gamma, beta, 1e-5, e0_copy=cp)
+    assert xn.dtype == torch.float32 and torch.equal(cp, e0)
+    bsub = torch.randn(D, device='cuda', generator=g) * 0.1               # b_sub path: LN(e0 + b − b) == LN(e0)
+    xn2, mean2, rstd2 = gpu_ops.ln_fwd(e0 + bsub, bsub, gamma, beta, 1e-5)
+    torch.testing.assert_close(xn2, xn, rtol=1e-5, atol=1e-5)
     x = e0.double().requires_grad_(True)
     gm, bt = gamma.double().requires_grad_(True), beta.double().requires_grad_(True)
     y = F.layer_norm(x, (D,), gm, bt, 1e-5)
