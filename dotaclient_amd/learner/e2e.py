@@ -207,8 +207,8 @@ def measure_e2e_procs(model: str = 'lstm512', device='cuda', duration: float = 2
     try:
         cfg = OptimizerConfig(log_dir=tmp, epochs=epochs, seq_per_epoch=seq_per_epoch, batch_size=batch_size,
                               seq_len=seq_len, model=model, precision=precision, device=str(device),
-                              checkpoint_keep=2, run_local=True, xp_timeout=300.0, histogram_freq=10 ** 9,
-                              async_checkpoint=True, prefetch_rollouts=prefetch)
+                              checkpoint_keep=2, run_local=True, xp_timeout=60.0, histogram_freq=10 ** 9,
+                              async_checkpoint=True, prefetch_rollouts=prefetch)   # (a live actor sends ~1000/s)
         opt = DotaOptimizer(cfg, broker)                   # publishes model version 0 into the shm model slot
         proc = ctx.Process(target=_actor_process_main, name='e2e-actor', daemon=True,
                            args=(name, model, games, threads, seq_len, rollout_size, max_dota_time, str(device), 11,
