@@ -404,14 +404,24 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             dgam = _acc(dgam, dg_c)
             dbet = _acc(dbet, dbe_c_)
             first_attn = False
+        # ∂b_τ, ∂W_env, ∂b_env: one pass over the rows (ops/csrc/glue.hip enc_small_grads); single chunk: on the
+        # recurrence stream, concurrent with the encoder backward
+        def small_grads():
+            return C.enc_small_grads(z[r0:r1], dtl[r0:r1], fp.type_offsets(dev), dx896, env_t[r0:r1], we, be,
+                                     bool(cfg.compat_bugs))
+        small = None
+        if wg_side:
+            sL.wait_stream(main)
+            with torch.cuda.stream(sL):
+                small = small_grads()
+                wg_done = torch.cuda.Event()
+                wg_done.record(sL)
         dwt_c, dw1_c, db1_c = C.encoder_bwd(units_t[r0:r1], w1, b1, wtT16, dtl[r0:r1], z[r0:r1],
                                             dx896, arg[r0:r1], counts, bool(cfg.compat_bugs), demb_in=demb_in)
         dw1 = _acc(dw1, dw1_c)
         db1 = _acc(db1, db1_c)
         dWt = _acc(dWt, dwt_c)
-        # ∂b_τ, ∂W_env, ∂b_env: one pass over the rows (ops/csrc/glue.hip enc_small_grads)
-        dbt_c, dWe_c, dbe_c = C.enc_small_grads(z[r0:r1], dtl[r0:r1], fp.type_offsets(dev), dx896, env_t[r0:r1],
-                                                we, be, bool(cfg.compat_bugs))
+        dbt_c, dWe_c, dbe_c = small if small is not None else small_grads()
         dbt = _acc(dbt, dbt_attn if attn else dbt_c)
         dWe = _acc(dWe, dWe_c)
         dbe = _acc(dbe, dbe_c)
