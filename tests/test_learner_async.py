@@ -53,3 +53,17 @@ def test_prefetch_and_async_publish_on_gpu(tmp_path):
     assert opt2.iteration_start == 3
     torch.testing.assert_close(opt2.learner.opt.exp_avg, opt.learner.opt.exp_avg)
     torch.testing.assert_close(opt2.learner.opt.exp_avg_sq, opt.learner.opt.exp_avg_sq)
+
+
+def test_e2e_actor_process_on_gpu():
+    """bench.py's default e2e mode on the GPU: VecActor in a spawned process (its own HIP context on the same GPU)
+    over the shared-memory broker, the learner here; rollouts flow, models flow back, the ring is unlinked."""
+    import glob
+    from dotaclient_amd.learner.e2e import measure_e2e_procs
+    before = set(glob.glob('/dev/shm/dca_e2e_*'))
+    r = measure_e2e_procs(model='lstm128', device='cuda', duration=30.0, max_iterations=3, games=64, threads=4,
+                          seq_len=128, batch_size=4, seq_per_epoch=8, max_dota_time=30.0, warmup_iterations=1)
+    assert r['iterations'] == 3
+    assert r['steps_per_s'] > 0 and r['actor_steps_per_s'] > 0
+    assert 0 <= r['avg_weight_age'] < 16
+    assert set(glob.glob('/dev/shm/dca_e2e_*')) == before
