@@ -255,6 +255,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         dtl = torch.empty(N, U, device=dev)
         logp = torch.empty(N, device=dev)
     dWcat = dbcat = None
+    heads_wg = None
     parts: List[torch.Tensor] = []
     algo = 0 if lc.algo == 'ppo' else 1
     # ---- forward recurrence on stream L, heads (+ heads backward) per chunk on the main stream
@@ -287,7 +288,13 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         first = dWcat is None
         if first:
             dbcat = torch.empty(LDZ, device=dev)
-        dWcat = gemm_tn(dz16, xh, out=dWcat, accumulate=not first, colsum=dbcat)
+        if one and _WG_OVERLAP:
+            # single chunk: the heads' weight gradient waits on the recurrence stream behind the backward
+            # recurrence (off the path between the two recurrences; joined with the other weight gradients)
+            dWcat = torch.empty(LDZ, H, device=dev)
+            heads_wg = (dz16, xh)
+        else:
+            dWcat = gemm_tn(dz16, xh, out=dWcat, accumulate=not first, colsum=dbcat)
         if one:
             z, dtl, logp = zc, dtl_c, lp
             dxh = _mm(dz16, wcat16).view(S, B, H)
@@ -337,6 +344,8 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             e = torch.cuda.Event()
             e.record(sL)
             bwd_done.append(e)
+        if heads_wg is not None:
+            gemm_tn(heads_wg[0], heads_wg[1], out=dWcat, colsum=dbcat)
     # single chunk: the recurrence stream (idle once the backward recurrence is done) takes the weight-gradient GEMMs
     # of W_hh, W_ih and the pre-RNN layer, off the critical ∂X chain (∂pre → ∂x896 → encoder backward) on the main
     # stream; the main stream joins it before the DP split point and before returning
