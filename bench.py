@@ -14,13 +14,24 @@ each rank trains on ``--batch-size`` sequences of ``--seq-len`` steps.
     python bench.py                                   # 1 GPU
     python -m torch.distributed.run --nproc-per-node 8 ... bench.py --gpus 8
 
-Rank 0 prints ONE JSON line. The actor numbers are measured *outside* the timed learner region and reported as
-extra fields: ``actor.steps_per_s`` = player-steps/s of the whole self-play runtime (actor/vec.py), and
-``actor.policy_step_per_s`` = the batched GPU policy step alone.
+Rank 0 prints ONE JSON line. The actor and end-to-end numbers are measured *outside* the timed learner region, on
+EVERY rank (one actor runtime per GPU), and reported as node aggregates (sums over ranks) with per-rank lists:
+
+* ``actor.steps_per_s`` — player-steps/s of the whole self-play runtime (actor/vec.py), ``actor.policy_step_per_s``
+  the batched GPU policy step alone;
+* ``e2e`` — the reference's node topology run for real (learner/e2e.py ``measure_e2e_node``): one experience queue
+  per node fed by one actor process per GPU, WORLD_SIZE learner ranks consuming disjoint rollouts (DDP over RCCL),
+  rank 0 alone publishing the model. ``e2e.steps_per_s`` is the reference's own metric (optimizer.py:485-486, padded
+  sequence steps incl. the wait for experience) summed over ranks; ``vs_baseline_e2e`` compares THAT with the
+  reference's ≈1000 steps/s, the like-for-like node-level comparison (``vs_baseline`` is the compute-only learner).
+
+Knobs for rehearsing the multi-rank path on one GPU: ``DCA_DIST_BACKEND=gloo`` and ``DCA_SHARED_GPU=1`` (every rank
+on cuda:0).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -52,12 +63,16 @@ def parse():
     ap.add_argument('--graph', type=int, default=-1, help='capture the step in a hipGraph (-1 = auto)')
     ap.add_argument('--actor', type=int, default=1, help='also measure actor steps/s (untimed region)')
     ap.add_argument('--actor-games', type=int, default=2048, help='concurrent 1v1 games of the actor runtime')
-    ap.add_argument('--actor-threads', type=int, default=14, help='host threads of the native actor runtime')
+    ap.add_argument('--actor-threads', type=int, default=14,
+                    help='host threads of the native actor runtime per GPU (16-CPU share per GPU)')
     ap.add_argument('--e2e', type=float, default=20.0,
-                    help='seconds of the end-to-end actors→queue→learner loop on GPU 0 (1-GPU runs; 0 = off)')
+                    help='seconds of the end-to-end actors→queue→learners loop on every rank (0 = off)')
     ap.add_argument('--e2e-games', type=int, default=1024)
     ap.add_argument('--e2e-mode', default='process', choices=['process', 'thread'],
-                    help='e2e actor as a spawned process over the shm broker (deploy split) or as a thread')
+                    help='e2e actors as one spawned process per rank over the node broker (deploy split) or as a '
+                         'thread (1 GPU only)')
+    ap.add_argument('--e2e-transport', default='auto', choices=['auto', 'shm', 'tcp'],
+                    help='node experience queue: shared-memory ring (auto on one node) or a TCP broker on rank 0')
     from dotaclient_amd.presets import parse_with_preset
     return parse_with_preset(ap, 'bench')
 
@@ -68,12 +83,13 @@ def main():
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
     use_cuda = torch.cuda.is_available()
-    device = torch.device(f'cuda:{local}' if use_cuda else 'cpu')
+    shared = os.environ.get('DCA_SHARED_GPU') == '1'          # rehearsal: every rank on GPU 0
+    device = torch.device(f'cuda:{0 if shared else local}' if use_cuda else 'cpu')
     if use_cuda:
         torch.cuda.set_device(device)
     if world > 1:
         from dotaclient_amd.parallel.dist import init_distribution
-        init_distribution(device=device)
+        init_distribution(backend=os.environ.get('DCA_DIST_BACKEND') or None, device=device)
 
     from dotaclient_amd.learner.engine import Learner, LossConfig
     from dotaclient_amd.learner.synthetic import DeviceReplay
@@ -134,12 +150,15 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
         loss_last = float(m['loss'])
-        if learner.backend == 'fused':
-            learner.model.check_error()       # a persistent-kernel timeout would invalidate the measurement
+        learner.check_error()       # a persistent-kernel timeout would invalidate the measurement
         return elapsed, loss_first, loss_last, learner, policy
 
     elapsed, loss_val, final_loss, learner, policy = run(args.precision)
     backend = learner.backend
+    step_mode = {'hipgraph': learner.graph is not None, 'dp_split_overlap': bool(getattr(learner, '_split', False)),
+                 'dist_backend': dist.get_backend() if world > 1 else None}
+    # DP replicas must hold bit-identical weights after the timed steps (checked across ranks below)
+    weights_sha = hashlib.sha256(learner.flat.flat.detach().cpu().numpy().tobytes()).hexdigest()[:16]
     samples = args.batch_size * args.seq_len * world * args.steps
     value = samples / elapsed
     ms_per_step = elapsed / args.steps * 1e3
@@ -149,39 +168,68 @@ def main():
         e16, _, _, _, _ = run('bf16')
         extra = {'precision': 'bf16', 'value': samples / e16, 'ms_per_step': e16 / args.steps * 1e3}
 
+    def gather(x):
+        """Every rank's value of ``x`` on every rank (rank order)."""
+        if world == 1:
+            return [x]
+        out = [None] * world
+        dist.all_gather_object(out, x)
+        return out
+
     actor = None
-    if args.actor and rank == 0 and use_cuda:
-        # actor.steps_per_s: the whole self-play runtime (actor/vec.py: native engine + featurize + reward +
-        # trajectory/rollout encoding on host threads, one hipGraph policy step for every player) in player-steps/s;
-        # actor.policy_step_per_s: the batched GPU policy step alone (observations pre-staged)
-        actor = {}
+    if args.actor and use_cuda:
+        # one actor runtime per GPU, all ranks at once (node aggregate = sum): actor.steps_per_s is the whole
+        # self-play runtime (actor/vec.py: native engine + featurize + reward + trajectory/rollout encoding on host
+        # threads, one hipGraph policy step for every player) in player-steps/s; actor.policy_step_per_s is the
+        # batched GPU policy step alone (observations pre-staged)
+        mine = {}
+        if world > 1:
+            dist.barrier()
         try:
             from dotaclient_amd.actor.vec import measure_vec_actor
             rt = measure_vec_actor(policy, device, n_games=args.actor_games, threads=args.actor_threads)
-            actor.update(steps_per_s=rt['steps_per_s'], runtime=rt)
+            mine.update(steps_per_s=rt['steps_per_s'], runtime=rt)
         except Exception as e:  # the learner metric stands on its own
-            actor['runtime_error'] = repr(e)
+            mine['runtime_error'] = repr(e)
+        if world > 1:
+            dist.barrier()
         try:
             from dotaclient_amd.actor.batched import measure_actor_throughput
             mb = measure_actor_throughput(policy, device, n_games=args.actor_games, threads=args.actor_threads)
-            actor['policy_step_per_s'] = mb['gpu_steps_per_s']
-            actor['policy_step_protobuf_featurize_per_s'] = mb['steps_per_s']
+            mine['policy_step_per_s'] = mb['gpu_steps_per_s']
+            mine['policy_step_protobuf_featurize_per_s'] = mb['steps_per_s']
         except Exception as e:
-            actor['policy_step_error'] = repr(e)
+            mine['policy_step_error'] = repr(e)
+        ranks = gather(mine)
+        actor = dict(ranks[0])
+        for k in ('steps_per_s', 'policy_step_per_s', 'policy_step_protobuf_featurize_per_s'):
+            vals = [r.get(k) for r in ranks]
+            if all(v is not None for v in vals):
+                actor[k] = float(sum(vals))
+                actor[k + '_per_rank'] = vals
+        actor['ranks'] = world
 
     e2e = None
-    if args.e2e > 0 and world == 1 and use_cuda:
+    if args.e2e > 0 and use_cuda and (args.e2e_mode == 'process' or world == 1):
         # the reference's own metric ('steps per s' incl. the wait for experience, optimizer.py:485-486) from the
-        # real loop: VecActor → queue → DotaOptimizer (deploy shape 8×1400, 16 seq/iteration) → model → VecActor
+        # real node loop: actor process per GPU → ONE node queue → WORLD_SIZE DotaOptimizer ranks (deploy shape
+        # 8×1400, 16 seq/iteration, DDP) → rank 0 publishes the model → actors
         learner = None
         try:
-            from dotaclient_amd.learner.e2e import measure_e2e, measure_e2e_procs
-            fn = measure_e2e_procs if args.e2e_mode == 'process' else measure_e2e
-            e2e = fn(model=args.model, device=device, duration=args.e2e, games=args.e2e_games,
-                     threads=args.actor_threads, seq_len=args.seq_len, precision=args.precision)
+            from dotaclient_amd.learner.e2e import measure_e2e, measure_e2e_node
+            kw = dict(model=args.model, device=device, duration=args.e2e, games=args.e2e_games,
+                      threads=args.actor_threads, seq_len=args.seq_len, precision=args.precision)
+            if args.e2e_mode == 'process':
+                e2e = measure_e2e_node(transport=args.e2e_transport, **kw)
+            else:
+                e2e = measure_e2e(**kw)
         except Exception as e:
             e2e = {'error': repr(e)}
+        errs = gather('error' in e2e)
+        if any(errs) and 'error' not in e2e:
+            e2e = {'error': f'failed on rank(s) {[i for i, x in enumerate(errs) if x]}'}
 
+    shas = gather(weights_sha)
     if rank == 0:
         out = {
             'metric': 'PPO optimizer samples/sec (whole node) + actor steps/sec, 1v1-mid LSTM policy',
@@ -194,7 +242,9 @@ def main():
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': value / BASELINE_STEPS_PER_S,
-            'dtype': args.precision,
+            'vs_baseline_e2e': (e2e['steps_per_s'] / BASELINE_STEPS_PER_S
+                                if e2e and 'steps_per_s' in e2e else None),
+            'dtype': 'fp32 (bf16x3 MFMA operands)' if args.precision == 'fp32' else args.precision,
             'precision_note': ('fp32 activations, gradients, accumulation and optimizer; hand-written MFMA kernels '
                                'use bf16x3 split operands (x = hi + lo, ~2^-16 relative per product), plain GEMMs on '
                                "hipBLASLt's fast fp32 mode (same bf16x3 accuracy class; DCA_F32_GEMM=exact for exact)") if args.precision == 'fp32' else
@@ -204,9 +254,11 @@ def main():
                                 f'{"5v5 entity-attention" if cfg.entity_attention else "1v1-mid entity"} encoder, '
                                 f'{cfg.layout.max_units} units)',
                        'global_batch': args.batch_size * world, 'seq_len': args.seq_len,
-                       'parallelism': f'dp{world}', 'algo': args.algo, 'backend': backend},
+                       'parallelism': f'dp{world}', 'algo': args.algo, 'backend': backend, 'step': step_mode},
             'loss_first': loss_val, 'loss_last': final_loss,
             'bf16_learner': extra,
+            'dp_replicas_identical': len(set(shas)) == 1,
+            'weights_sha16_per_rank': shas,
             'actor': actor,
             'e2e': e2e,
         }

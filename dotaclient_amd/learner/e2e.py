@@ -92,9 +92,10 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
         max_dota_time=max_dota_time, precision=precision, prefetch_rollouts=prefetch, actor='thread'))
 
 
-def _learner_loop(opt, duration, warmup_iterations, max_iterations, counters, check):
+def _learner_loop(opt, duration, warmup_iterations, max_iterations, counters, check, agree=None):
     """Run learner iterations for ``duration`` seconds after ``warmup_iterations``; per-iteration metric rows, the
-    wall time and the (actor steps, dropped rollouts) deltas of the window."""
+    wall time and the (actor steps, dropped rollouts) deltas of the window. ``agree(local_continue) -> bool``
+    makes data-parallel ranks stop on the same iteration (every rank runs the same number of DP steps)."""
     from .optimizer import DotaOptimizer
     rows = []
     it = opt.iteration_start
@@ -107,7 +108,12 @@ def _learner_loop(opt, duration, warmup_iterations, max_iterations, counters, ch
     t0 = time.perf_counter()
     c0 = counters()
     opt.time_last_step = time.time()
-    while time.perf_counter() - t0 < duration and (max_iterations is None or len(rows) < max_iterations):
+    while True:
+        cont = time.perf_counter() - t0 < duration and (max_iterations is None or len(rows) < max_iterations)
+        if agree is not None:
+            cont = agree(cont)
+        if not cont:
+            break
         opt.run_iteration(it)
         it += 1
         m = opt.last_metrics
@@ -147,24 +153,38 @@ def _summary(rows, wall, actor_steps, dropped, games, config):
     }
 
 
-def _actor_process_main(name: str, model: str, games: int, threads: int, seq_len: int, rollout_size: int,
-                        max_dota_time: float, device: str, seed: int, stop, ready, steps, failed):
-    """Actor role of :func:`measure_e2e_procs`: a process of its own (own interpreter and GIL) that plays ``games``
-    VecActor games on the GPU, pushes whole-game rollouts into the node's shared-memory experience ring and hot-swaps
-    every model the learner publishes into that broker's model slot."""
+def open_node_broker(addr: str, drop_oldest: bool = True):
+    """Client of the node's experience / model broker: ``shm://name`` (native ring + model slot in /dev/shm) or
+    ``tcp://host:port`` (TcpBrokerServer)."""
+    if addr.startswith('shm://'):
+        from ..transport.shm import ShmBroker
+        return ShmBroker(addr[6:], create=False, drop_oldest=drop_oldest)
+    from ..transport.broker import make_broker
+    return make_broker(addr)
+
+
+def _actor_process_main(addr: str, model: str, games: int, threads: int, seq_len: int, rollout_size: int,
+                        max_dota_time: float, device: str, seed: int, stop, ready, steps, failed, tag: str = 'a0'):
+    """Actor role of :func:`measure_e2e_node`: a process of its own (own interpreter and GIL) that plays ``games``
+    VecActor games on its GPU, pushes whole-game rollouts into the node's experience queue and hot-swaps every model
+    the learner's rank 0 publishes (reference agent.py:855-902 with the model subscription of 198-223). It tears its
+    threads down before returning, so the process exits with status 0."""
+    br = None
     try:
         from ..actor.vec import VecActor
         from ..actor.weights import WeightStore
-        from ..transport.shm import ShmBroker
-        br = ShmBroker(name, create=False, drop_oldest=True)
+        if device.startswith('cuda') and torch.device(device).index is not None:
+            torch.cuda.set_device(torch.device(device))
+        br = open_node_broker(addr, drop_oldest=True)
         ws = WeightStore(model, device='cpu')
-        m = br.latest_model(timeout=120.0)
+        m = br.latest_model(timeout=600.0)
         if m is None:
             raise TimeoutError('no model published by the learner')
         ws.add_bytes(*m)
-        br.subscribe_model(lambda v, b: ws.add_bytes(v, b), poll=0.005)
+        br.subscribe_model(lambda v, b: ws.add_bytes(v, b), poll=0.005 if addr.startswith('shm://') else 0.25)
         va = VecActor(ws, games, br.publish_experience, device=device, seed=seed, rollout_size=rollout_size,
-                      max_dota_time=max_dota_time, hidden_stride=seq_len, threads=threads, stagger=True)
+                      max_dota_time=max_dota_time, hidden_stride=seq_len, threads=threads, stagger=True,
+                      tag=f'{tag}.vec')         # game ids unique across the node's actor processes
         for _ in range(3):
             va.step()
         ready.set()
@@ -172,72 +192,177 @@ def _actor_process_main(name: str, model: str, games: int, threads: int, seq_len
             va.step()
             steps.value = va.steps_taken
         va.close()
-        br.close()
     except BaseException:
         import traceback
         traceback.print_exc()
         failed.set()
         ready.set()
+    finally:
+        if br is not None:
+            br.close()                  # joins the model subscriber thread
 
 
-def measure_e2e_procs(model: str = 'lstm512', device='cuda', duration: float = 20.0, games: int = 1024,
-                      threads: int = 14, seq_len: int = 1400, batch_size: int = 8, seq_per_epoch: int = 16,
-                      epochs: int = 1, precision: str = 'fp32', max_dota_time: float = 600.0,
-                      rollout_size: int = 9999, warmup_iterations: int = 2, max_iterations: Optional[int] = None,
-                      log_dir: Optional[str] = None, prefetch: int = 32, ring_bytes: int = 1 << 26
-                      ) -> Dict[str, float]:
-    """:func:`measure_e2e` with the deploy's process split: the actor in a process of its own (spawned, same GPU)
-    and the learner here, exchanging rollouts and models through the node-local shared-memory broker
-    (``transport/shm.py``: native MPMC ring + model slot) instead of in-process queues — no GIL shared between the
-    actor's host loop and the learner's ingest / publish threads. The ring holds ``ring_bytes`` (64 MB ≈ the thread
-    variant's 64-rollout queue at the deploy's mean rollout size; the oldest rollouts are dropped when it is full),
-    which bounds the experience's weight age."""
+def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20.0, games: int = 1024,
+                     threads: int = 14, seq_len: int = 1400, batch_size: int = 8, seq_per_epoch: int = 16,
+                     epochs: int = 1, precision: str = 'fp32', max_dota_time: float = 600.0,
+                     rollout_size: int = 9999, warmup_iterations: int = 2, max_iterations: Optional[int] = None,
+                     log_dir: Optional[str] = None, prefetch: int = 32, ring_bytes: int = 1 << 26,
+                     transport: str = 'auto', backend: str = 'auto', idle_probe: float = 3.0,
+                     report=None, record_consumed: int = 0) -> Dict[str, float]:
+    """The reference's node topology end to end (optimizer.py:144-150, 274-287; ks-app/components/optimizer.jsonnet:
+    79-174): ONE experience queue per node fed by actor processes, ``WORLD_SIZE`` learner ranks (one per GPU, DDP
+    over RCCL) consuming disjoint rollouts from it as competing consumers, and rank 0 alone checkpointing and
+    publishing the model every iteration, which every actor hot-swaps. Works at any world size (1 = one GPU).
+
+    Rank 0 creates the node's broker — the shared-memory ring (``transport='shm'``, the default when every rank is
+    on this node) or a TCP broker served from rank 0's process (``'tcp'``) — and broadcasts its address. Every rank
+    spawns one actor process on its own device. Ranks agree every iteration on whether to go on, so all of them run
+    the same DP steps. Before the timed window, ``idle_probe`` seconds of actor throughput are measured with the
+    learners idle (CPU sharing vs. the persistent recurrence holding the CUs).
+
+    Returns, on every rank, the node aggregate: ``steps_per_s`` (the reference's ``steps per s``, padded, summed
+    over ranks), ``valid_steps_per_s``, ``actor_steps_per_s`` (sum), their per-rank lists, ``queue_dropped`` (ring
+    drops during the window) and the per-rank stage times. ``report(opt) -> dict`` (tests) runs on every rank after
+    the window; the results are returned in rank order under ``reports``."""
     import multiprocessing as mp
     import os
-    from ..transport.shm import ShmBroker
+    import torch.distributed as tdist
+    from ..parallel import dist as pdist
     from .optimizer import DotaOptimizer, OptimizerConfig
 
+    world, rank = pdist.get_world_size(), pdist.get_rank()
+    local_world = int(os.environ.get('LOCAL_WORLD_SIZE', world))
+    if transport == 'auto':
+        from .. import native
+        transport = 'shm' if (local_world == world and native.AVAILABLE) else 'tcp'
+    dev = torch.device(device)
+    coll_dev = dev if (dev.type == 'cuda' and pdist.is_distributed() and tdist.get_backend() == 'nccl') else 'cpu'
+
+    owner = None                    # rank 0's ShmBroker (creator) or TcpBrokerServer
+    addr = None
+    if rank == 0:
+        if transport == 'shm':
+            from ..transport.shm import ShmBroker
+            name = f'dca_e2e_{os.getpid()}_{int(time.time() * 1e3) % 10 ** 9}'
+            owner = ShmBroker(name, capacity=ring_bytes * world, create=True, drop_oldest=True)
+            addr = f'shm://{name}'
+        else:
+            from ..transport.broker import TcpBrokerServer
+            host = os.environ.get('MASTER_ADDR', '127.0.0.1') if world > 1 else '127.0.0.1'
+            owner = TcpBrokerServer(host, 0, maxsize=64 * world, drop_oldest=True).start()
+            addr = f'tcp://{owner.host}:{owner.port}'
+    if pdist.is_distributed():
+        box = [addr]
+        tdist.broadcast_object_list(box, 0)
+        addr = box[0]
+    broker = owner if (rank == 0 and transport == 'shm') else open_node_broker(addr, drop_oldest=True)
+
     tmp = log_dir or tempfile.mkdtemp(prefix='dca_e2e_')
-    name = f'dca_e2e_{os.getpid()}_{int(time.time() * 1e3) % 10 ** 9}'
-    broker = ShmBroker(name, capacity=ring_bytes, create=True, drop_oldest=True)
     ctx = mp.get_context('spawn')
     stop, ready, failed = ctx.Event(), ctx.Event(), ctx.Event()
     steps = ctx.Value('q', 0)
-    proc = None
+    proc = opt = None
+    rows, wall, actor_steps, idle = [], 0.0, 0, float('nan')
+    err = None
+
+    def dropped_total():
+        return int(owner.ring.dropped()) if transport == 'shm' and rank == 0 else \
+            (int(owner.broker.n_dropped) if rank == 0 else 0)
     try:
+        # the actor starts first (interpreter + engine + graph capture overlap the learner's construction) and
+        # waits for rank 0's model version 0
+        proc = ctx.Process(target=_actor_process_main, name=f'e2e-actor-{rank}', daemon=True,
+                           args=(addr, model, games, threads, seq_len, rollout_size, max_dota_time, str(device),
+                                 11 + 7919 * rank, stop, ready, steps, failed, f'a{rank}'))
+        proc.start()
         cfg = OptimizerConfig(log_dir=tmp, epochs=epochs, seq_per_epoch=seq_per_epoch, batch_size=batch_size,
                               seq_len=seq_len, model=model, precision=precision, device=str(device),
-                              checkpoint_keep=2, run_local=True, xp_timeout=60.0, histogram_freq=10 ** 9,
-                              async_checkpoint=True, prefetch_rollouts=prefetch)   # (a live actor sends ~1000/s)
-        opt = DotaOptimizer(cfg, broker)                   # publishes model version 0 into the shm model slot
-        proc = ctx.Process(target=_actor_process_main, name='e2e-actor', daemon=True,
-                           args=(name, model, games, threads, seq_len, rollout_size, max_dota_time, str(device), 11,
-                                 stop, ready, steps, failed))
-        proc.start()
-        if not ready.wait(timeout=600) or failed.is_set():
+                              backend=backend, checkpoint_keep=2, run_local=True, xp_timeout=120.0,
+                              histogram_freq=10 ** 9, async_checkpoint=dev.type == 'cuda',
+                              prefetch_rollouts=prefetch, record_consumed=record_consumed)
+        opt = DotaOptimizer(cfg, broker, checkpoint=rank == 0)     # rank 0 publishes model version 0
+        if not ready.wait(timeout=900) or failed.is_set():
             raise RuntimeError('e2e actor process failed to start')
+        if pdist.is_distributed():
+            tdist.barrier()
+        if idle_probe > 0:
+            s0, t0 = steps.value, time.perf_counter()
+            time.sleep(idle_probe)
+            idle = (steps.value - s0) / (time.perf_counter() - t0)
 
         def check():
             if failed.is_set() or not proc.is_alive():
-                return RuntimeError('e2e actor process died')
+                return RuntimeError(f'e2e actor process died (exit code {proc.exitcode})')
             return None
+
+        def agree(cont: bool) -> bool:
+            if not pdist.is_distributed():
+                return cont
+            t = torch.tensor([1 if cont else 0], dtype=torch.int32, device=coll_dev)
+            tdist.all_reduce(t, op=tdist.ReduceOp.MIN)
+            return bool(t.item())
+        d0 = dropped_total()
         try:
             rows, wall, (actor_steps, _) = _learner_loop(opt, duration, warmup_iterations, max_iterations,
-                                                         counters=lambda: (steps.value, 0), check=check)
+                                                         counters=lambda: (steps.value, 0), check=check, agree=agree)
         finally:
             opt.close()
             opt.flush_checkpoints()
+        queue_dropped = dropped_total() - d0
+        extra = report(opt) if report is not None else None
+    except BaseException as e:
+        err = e
+        raise
     finally:
         stop.set()
         if proc is not None:
-            proc.join(timeout=60)
+            proc.join(timeout=120)
             if proc.is_alive():
                 proc.kill()
                 proc.join(timeout=10)
-        broker.close(unlink=True)
+                if err is None:
+                    err = RuntimeError('e2e actor process did not exit')
+            elif proc.exitcode != 0 and err is None:
+                err = RuntimeError(f'e2e actor process exited with status {proc.exitcode}')
+        if broker is not owner and hasattr(broker, 'close'):
+            broker.close()
+        if pdist.is_distributed() and err is None:
+            tdist.barrier()             # every rank's actor is done with the broker before rank 0 removes it
+        if owner is not None:
+            if transport == 'shm':
+                owner.close(unlink=True)
+            else:
+                owner.stop()
         if log_dir is None:
             shutil.rmtree(tmp, ignore_errors=True)
-    out = _summary(rows, wall, actor_steps, -1, games, dict(
-        batch_size=batch_size, seq_len=seq_len, seq_per_epoch=seq_per_epoch, epochs=epochs, rollout_size=rollout_size,
-        max_dota_time=max_dota_time, precision=precision, prefetch_rollouts=prefetch, actor='process (shm broker)'))
+    if err is not None:
+        raise err
+    mine = _summary(rows, wall, actor_steps, queue_dropped, games, dict(seq_per_epoch=seq_per_epoch, seq_len=seq_len))
+    mine['actor_idle_steps_per_s'] = idle
+    mine['report'] = extra
+    per_rank = [mine]
+    if pdist.is_distributed():
+        per_rank = [None] * world
+        tdist.all_gather_object(per_rank, mine)
+    out = dict(per_rank[0])
+    for k in ('steps_per_s', 'valid_steps_per_s', 'actor_steps_per_s', 'actor_idle_steps_per_s'):
+        out[k] = float(sum(r[k] for r in per_rank))
+        out[k + '_per_rank'] = [r[k] for r in per_rank]
+    out['queue_dropped'] = int(per_rank[0]['queue_dropped'])
+    reports = [r.pop('report') for r in per_rank]
+    out.pop('report', None)
+    if report is not None:
+        out['reports'] = reports
+    out['iterations'] = int(per_rank[0]['iterations'])
+    out['games'] = games * world
+    out['ranks'] = world
+    out['config'] = dict(batch_size=batch_size, seq_len=seq_len, seq_per_epoch=seq_per_epoch, epochs=epochs,
+                         rollout_size=rollout_size, max_dota_time=max_dota_time, precision=precision,
+                         prefetch_rollouts=prefetch, games_per_rank=games,
+                         actor=f'one process per rank over the node {transport} broker', learners=world)
     return out
+
+
+def measure_e2e_procs(**kw) -> Dict[str, float]:
+    """One-GPU form of :func:`measure_e2e_node` (the actor in a process of its own over the shm broker)."""
+    return measure_e2e_node(**kw)

@@ -336,7 +336,27 @@ class Learner:
             self.dp.err_flag.copy_(self.model.err)
         fold = self.dp.enabled and self.opt.use_kernels
         self.dp.sync(scale=not fold)
+        if self.backend == 'fused' and self.dp.enabled:
+            # the reduced flag is non-zero on EVERY rank when any rank's recurrence failed: keep it sticky so that
+            # all ranks raise together at the iteration boundary (check_error), not only the failing one
+            sticky = getattr(self, '_err_any', None)
+            if sticky is None:
+                sticky = self._err_any = torch.zeros_like(self.dp.err_flag)
+            torch.maximum(sticky, self.dp.err_flag, out=sticky)
         return self.opt.step(self.dp.counts, divide=fold, skip=self.dp.err_flag)
+
+    def check_error(self):
+        """Raise (on every DP rank alike) if a persistent kernel failed on any rank since the last call; host sync,
+        call at iteration boundaries."""
+        if self.backend != 'fused':
+            return
+        sticky = getattr(self, '_err_any', None)
+        if sticky is not None and float(sticky.item()) != 0.0:
+            own = int(self.model.err.item())
+            sticky.zero_()
+            raise RuntimeError(f'persistent kernel error on a data-parallel rank (own code {own}): the step was '
+                               'skipped by every rank\'s Adam')
+        self.model.check_error()
 
     def _finish(self, vec):
         metrics = self._metrics_from_vec(vec.clone())

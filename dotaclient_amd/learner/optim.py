@@ -94,24 +94,54 @@ class FlatAdam:
         return norm
 
     # ------------------------------------------------------------------------------------------------
+    def layout(self):
+        """The flat buffer's layout (header length, per-parameter offsets and sizes): the moments are only meaningful
+        against the layout they were written with."""
+        return {'header': int(self.flat.header), 'offsets': [int(o) for o in self.flat.offsets],
+                'numel': [int(n) for n in self.flat.numel]}
+
     def state_dict(self):
         return {'exp_avg': self.exp_avg.cpu(), 'exp_avg_sq': self.exp_avg_sq.cpu(), 'steps': self.steps.cpu(),
-                'lr': self.lr, 'betas': self.betas, 'eps': self.eps, 'max_grad_norm': self.max_grad_norm}
+                'lr': self.lr, 'betas': self.betas, 'eps': self.eps, 'max_grad_norm': self.max_grad_norm,
+                'layout': self.layout()}
 
     def load_state_dict(self, d, keep_hparams: bool = True):
         """Restore the moments and step counts. The hyperparameters this optimizer was built with (from the CLI)
-        win over the checkpointed ones unless ``keep_hparams`` is False; a difference is logged."""
-        self.exp_avg.copy_(d['exp_avg'])
-        self.exp_avg_sq.copy_(d['exp_avg_sq'])
+        win over the checkpointed ones unless ``keep_hparams`` is False; a difference is logged. Moments saved
+        under another flat layout are remapped parameter by parameter (same parameters, same sizes); a state without
+        a recorded layout (written before layouts were versioned) is accepted only if its length matches the
+        current buffer exactly, otherwise it is rejected with ValueError."""
+        import logging
+        log = logging.getLogger(__name__)
+        cur = self.layout()
+        saved = d.get('layout')
+        if saved is None:
+            if d['exp_avg'].numel() != self.exp_avg.numel():
+                raise ValueError(f'optimizer state of {d["exp_avg"].numel()} elements has no recorded flat layout '
+                                 f'and does not match this buffer ({self.exp_avg.numel()} elements): it was '
+                                 'written by an older layout; resume the weights only (drop the trainer state)')
+            self.exp_avg.copy_(d['exp_avg'])
+            self.exp_avg_sq.copy_(d['exp_avg_sq'])
+        elif saved == cur:
+            self.exp_avg.copy_(d['exp_avg'])
+            self.exp_avg_sq.copy_(d['exp_avg_sq'])
+        else:
+            if saved['numel'] != cur['numel']:
+                raise ValueError('optimizer state was written for different parameters (sizes '
+                                 f'{saved["numel"]} vs {cur["numel"]})')
+            log.info('resume: remapping Adam moments from flat layout (header %d) to (header %d)', saved['header'],
+                     cur['header'])
+            for key in ('exp_avg', 'exp_avg_sq'):
+                src, dst = d[key], getattr(self, key)
+                for so, do, n in zip(saved['offsets'], cur['offsets'], cur['numel']):
+                    dst[do:do + n].copy_(src[so:so + n])
         self.steps.copy_(d['steps'])
-        saved = {'lr': d['lr'], 'betas': tuple(d['betas']), 'eps': d['eps'], 'max_grad_norm': d['max_grad_norm']}
+        hp = {'lr': d['lr'], 'betas': tuple(d['betas']), 'eps': d['eps'], 'max_grad_norm': d['max_grad_norm']}
         if not keep_hparams:
-            self.lr, self.betas, self.eps, self.max_grad_norm = (saved['lr'], saved['betas'], saved['eps'],
-                                                                 saved['max_grad_norm'])
+            self.lr, self.betas, self.eps, self.max_grad_norm = hp['lr'], hp['betas'], hp['eps'], hp['max_grad_norm']
             return
-        cur = {'lr': self.lr, 'betas': tuple(self.betas), 'eps': self.eps, 'max_grad_norm': self.max_grad_norm}
-        diff = {k: (saved[k], cur[k]) for k in cur if saved[k] != cur[k]}
+        mine = {'lr': self.lr, 'betas': tuple(self.betas), 'eps': self.eps, 'max_grad_norm': self.max_grad_norm}
+        diff = {k: (hp[k], mine[k]) for k in mine if hp[k] != mine[k]}
         if diff:
-            import logging
-            logging.getLogger(__name__).warning('resume: keeping the configured optimizer hyperparameters over the '
-                                                'checkpointed ones (checkpoint, configured): %s', diff)
+            log.warning('resume: keeping the configured optimizer hyperparameters over the checkpointed ones '
+                        '(checkpoint, configured): %s', diff)

@@ -85,6 +85,8 @@ class OptimizerConfig:
     async_checkpoint: bool = False     # write checkpoint files on a background thread (the model is published first)
     prefetch_rollouts: int = 0         # >0: consume + decode up to N rollouts ahead on a background thread (overlaps
                                        #     the next iteration's decode with this one's training); 0: inline
+    record_consumed: int = 0           # keep the keys (game, team, player, version, length) of the last N rollouts
+                                       #     consumed (competing-consumer tests; 0 = off)
 
 
 class Sequence:
@@ -174,6 +176,11 @@ class DotaOptimizer:
             self.learner.broadcast_state(0)
             self._broadcast_reward_stats(0)
         self.corrupt_rollouts = 0
+        self.n_published = 0               # model messages this rank published (rank 0 only, reference :284-287)
+        self.consumed = None
+        if cfg.record_consumed:
+            import collections
+            self.consumed = collections.deque(maxlen=cfg.record_consumed)
         self.replay = None
         if cfg.replay_capacity or cfg.replay_gb:
             from .replay import HbmReplay
@@ -213,6 +220,12 @@ class DotaOptimizer:
     # ------------------------------------------------------------------------------------------------
     def get_rollout(self) -> Rollout:
         """Next decoded rollout: from the decode-ahead thread when ``prefetch_rollouts`` > 0, else inline."""
+        r = self._next_rollout()
+        if self.consumed is not None:
+            self.consumed.append((r.game_id, int(r.team_id), int(r.player_id), int(r.weight_version), r.length))
+        return r
+
+    def _next_rollout(self) -> Rollout:
         if self.cfg.prefetch_rollouts > 0:
             pf = getattr(self, '_prefetcher', None)
             if pf is None:
@@ -221,24 +234,41 @@ class DotaOptimizer:
                 mk = getattr(self.broker, 'consumer', None)
                 self._xp_broker = mk() if mk is not None else self.broker
                 pf = self._prefetcher = _RolloutPrefetcher(self._consume_decode, self.cfg.prefetch_rollouts)
+                self.prefetch_dropped = 0
             return pf.get()
         return self._consume_decode()
 
     def close(self):
-        """Stop the decode-ahead thread (if any); rollouts it already took from the queue are dropped."""
+        """Stop the decode-ahead thread (if any) and join it; rollouts it had already taken from the queue are
+        dropped and counted in ``prefetch_dropped``."""
         pf = getattr(self, '_prefetcher', None)
         if pf is not None:
-            pf.close()
+            self.prefetch_dropped = pf.close()
             self._prefetcher = None
             xb = getattr(self, '_xp_broker', None)
             if xb is not None and xb is not self.broker and hasattr(xb, 'close'):
                 xb.close()
             self._xp_broker = None
 
-    def _consume_decode(self) -> Rollout:
+    def _consume_decode(self, stop=None) -> Rollout:
+        """Next decodable rollout from the queue. With ``stop`` (the decode-ahead thread's event) the queue is polled
+        in bounded slices so that :meth:`close` ends the thread promptly instead of leaving it blocked inside the
+        broker; returns None once ``stop`` is set."""
         broker = getattr(self, '_xp_broker', None) or self.broker
+        total = self.cfg.xp_timeout
         while True:
-            body = broker.consume_experience(timeout=self.cfg.xp_timeout)
+            if stop is None:
+                body = broker.consume_experience(timeout=total)
+            else:
+                t0 = time.monotonic()
+                body = None
+                while body is None and not stop.is_set():
+                    left = None if total is None else total - (time.monotonic() - t0)
+                    if left is not None and left <= 0:
+                        break
+                    body = broker.consume_experience(timeout=0.25 if left is None else min(0.25, left))
+                if body is None and stop.is_set():
+                    return None
             if body is None:
                 raise TimeoutError('no experience received')
             try:
@@ -430,10 +460,25 @@ class DotaOptimizer:
         return end
 
     def flush_checkpoints(self):
-        """Wait for the background checkpoint writes (``async_checkpoint``)."""
-        ex = getattr(self, '_ckpt_pool', None)
-        if ex is not None:
-            ex.submit(lambda: None).result()
+        """Wait for the background publishes / checkpoint writes (``async_checkpoint``); re-raises the first failure
+        on this thread, as the synchronous path would have."""
+        self._check_background(wait=True)
+
+    def _check_background(self, wait: bool = False):
+        """Surface failures of the ordered background writer: a failed model publish or checkpoint write must stop
+        the learner (actors would otherwise keep playing stale weights with nothing reported)."""
+        pending = self.__dict__.setdefault('_bg_futures', [])
+        keep = []
+        for f in pending:
+            if wait or f.done():
+                f.result()                  # raises the writer's exception here
+            else:
+                keep.append(f)
+        self._bg_futures = keep
+
+    def _submit_background(self, fn, *args):
+        self._check_background()
+        self.__dict__.setdefault('_bg_futures', []).append(self._ckpt_pool_get().submit(fn, *args))
 
     def run_iteration(self, it: int):
         cfg = self.cfg
@@ -492,8 +537,7 @@ class DotaOptimizer:
             loss_t[0] = float('nan')
         if torch.isnan(loss_t).any():
             raise ValueError(f'NaN loss at iteration {it}: {loss_t.tolist()}')
-        if self.learner.backend == 'fused':
-            self.learner.model.check_error()
+        self.learner.check_error()
         n_steps = n_seq * cfg.seq_len
         if self.ingest == 'device':
             self._sync_running()
@@ -577,10 +621,12 @@ class DotaOptimizer:
         if not self.cfg.async_checkpoint:
             self._write_checkpoint(data, trainer, version)
             self.broker.publish_model(data, version)
+            self.n_published += 1
             return
         # publish first (actors see the new weights now); the files follow on one ordered background writer
         self.broker.publish_model(data, version)
-        self._ckpt_pool_get().submit(self._write_checkpoint, data, trainer, version)
+        self.n_published += 1
+        self._submit_background(self._write_checkpoint, data, trainer, version)
 
     def _ckpt_pool_get(self):
         if getattr(self, '_ckpt_pool', None) is None:
@@ -598,7 +644,7 @@ class DotaOptimizer:
                    'iteration': version, 'config': asdict(self.cfg)}
         ev = torch.cuda.Event()
         ev.record()
-        self._ckpt_pool_get().submit(self._publish_snapshot, sd, trainer, ev, version)
+        self._submit_background(self._publish_snapshot, sd, trainer, ev, version)
 
     def _publish_snapshot(self, sd, trainer, ev, version: int):
         import io
@@ -612,6 +658,7 @@ class DotaOptimizer:
         torch.save(sd, buf)
         data = buf.getvalue()
         self.broker.publish_model(data, version)
+        self.n_published += 1
         self._write_checkpoint(data, trainer, version)
 
     def _write_checkpoint(self, data: bytes, trainer, version: int):
@@ -636,6 +683,7 @@ class _RolloutPrefetcher:
         self.q = queue.Queue(maxsize=max(1, depth))
         self.fetch = fetch
         self.err: Optional[BaseException] = None
+        self.lost = 0
         self.stop = threading.Event()
         self.th = threading.Thread(target=self._run, name='xp-prefetch', daemon=True)
         self.th.start()
@@ -643,13 +691,17 @@ class _RolloutPrefetcher:
     def _run(self):
         try:
             while not self.stop.is_set():
-                r = self.fetch()
-                while not self.stop.is_set():
+                r = self.fetch(self.stop)
+                if r is None:
+                    break
+                while True:
                     try:
                         self.q.put(r, timeout=0.1)
                         break
                     except self._queue_mod.Full:
-                        continue
+                        if self.stop.is_set():
+                            self.lost += 1
+                            return
         except BaseException as e:       # surfaced on the consumer's thread
             self.err = e
 
@@ -663,9 +715,13 @@ class _RolloutPrefetcher:
                 if not self.th.is_alive():
                     raise RuntimeError('experience prefetch thread exited')
 
-    def close(self):
+    def close(self) -> int:
+        """Stop and join the thread (it polls the queue in bounded slices); returns the decoded rollouts dropped."""
         self.stop.set()
-        self.th.join(timeout=5.0)
+        self.th.join(timeout=30.0)
+        if self.th.is_alive():
+            raise RuntimeError('experience prefetch thread did not stop')
+        return self.lost + self.q.qsize()
 
 
 def _clone_dev(x):

@@ -280,6 +280,9 @@ class TcpBroker:
 
     def close(self):
         self._stop.set()
+        th, self._sub_thread = self._sub_thread, None
+        if th is not None and th is not threading.current_thread():
+            th.join(timeout=30.0)           # its long poll ends within ``poll`` seconds
         if self._sock is not None:
             try:
                 self._sock.close()

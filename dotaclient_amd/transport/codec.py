@@ -160,18 +160,42 @@ def _storage_from_bytes(b):
     return torch.load(io.BytesIO(b), weights_only=True)
 
 
+def _storage_elements(storage) -> int:
+    import torch
+    if isinstance(storage, torch.storage.TypedStorage):
+        return int(storage._untyped_storage.nbytes()) // torch.empty((), dtype=storage.dtype).element_size()
+    return int(storage.nbytes())
+
+
+def _rebuild_tensor_checked(storage, storage_offset, size, stride, *args, **kwargs):
+    """``torch._utils._rebuild_tensor_v2`` restricted to views INSIDE the loaded storage. The stock rebuild calls
+    ``set_``, which grows the storage to whatever size/stride the message claims — a crafted message could force an
+    allocation of any size. Out-of-range views are rejected as corrupt instead."""
+    import torch._utils as tu
+    size, stride = tuple(int(x) for x in size), tuple(int(x) for x in stride)
+    off = int(storage_offset)
+    if len(size) != len(stride) or off < 0 or any(x < 0 for x in size) or any(x < 0 for x in stride):
+        raise CorruptMessage(f'invalid tensor view: size={size} stride={stride} offset={off}')
+    if all(x > 0 for x in size):
+        last = off + sum((n - 1) * st for n, st in zip(size, stride))
+        if last >= _storage_elements(storage):
+            raise CorruptMessage(f'tensor view size={size} stride={stride} offset={off} exceeds its storage')
+    return tu._rebuild_tensor_v2(storage, off, size, stride, *args, **kwargs)
+
+
 class _ArrayUnpickler(pickle.Unpickler):
     """Unpickler for the reference's experience dicts (numpy arrays and torch tensors in plain containers): only
-    array / tensor reconstruction can be resolved — tensor storages through a weights-only ``torch.load`` — so a
-    crafted message cannot run code."""
+    array / tensor reconstruction can be resolved — tensor storages through a weights-only ``torch.load``, tensor
+    views bounds-checked against their storage — so a crafted message cannot run code or force huge allocations."""
     _ALLOWED = {('numpy.core.multiarray', '_reconstruct'), ('numpy._core.multiarray', '_reconstruct'),
                 ('numpy.core.multiarray', 'scalar'), ('numpy._core.multiarray', 'scalar'),
-                ('numpy', 'ndarray'), ('numpy', 'dtype'), ('collections', 'OrderedDict'),
-                ('torch._utils', '_rebuild_tensor_v2')}
+                ('numpy', 'ndarray'), ('numpy', 'dtype'), ('collections', 'OrderedDict')}
 
     def find_class(self, module, name):
         if (module, name) == ('torch.storage', '_load_from_bytes'):
             return _storage_from_bytes
+        if (module, name) == ('torch._utils', '_rebuild_tensor_v2'):
+            return _rebuild_tensor_checked
         if (module, name) in self._ALLOWED:
             return super().find_class(module, name)
         raise pickle.UnpicklingError(f'global {module}.{name} is not allowed in an experience message')
@@ -190,7 +214,7 @@ def decode_any(buf: bytes, allow_pickle: bool = False) -> Rollout:
     except CorruptMessage:
         raise
     except (pickle.UnpicklingError, ValueError, KeyError, TypeError, IndexError, AttributeError, EOFError,
-            struct.error, UnicodeDecodeError) as e:
+            struct.error, UnicodeDecodeError, RuntimeError, MemoryError, OverflowError) as e:
         raise CorruptMessage(f'undecodable experience message: {e!r}') from e
 
 

@@ -76,7 +76,13 @@ class ShmBroker:
             self._thread.start()
 
     def close(self, unlink: bool = False):
+        """Stop and JOIN the model subscriber thread before returning: a daemon thread still running the callback
+        (weight decode inside torch C++ code) when the interpreter finalises is torn down by a forced unwind, which
+        aborts the process with ``terminate called without an active exception``."""
         self._stop.set()
+        th, self._thread = self._thread, None
+        if th is not None and th is not threading.current_thread():
+            th.join(timeout=30.0)
         if unlink:
             native.ShmRing.unlink(f'/{self.name}_xp')
             try:

@@ -40,3 +40,4 @@ def test_bench_json_contract_cpu(world):
     assert r['config']['global_batch'] == 2 * world and r['config']['seq_len'] == 16
     assert abs(r['value'] - 2 * world * 16 * 2 / (r['ms_per_step'] * 2 / 1e3)) / r['value'] < 1e-6
     assert r['vs_baseline'] == pytest.approx(r['value'] / 1000.0)
+    assert r['dp_replicas_identical'] is True and len(r['weights_sha16_per_rank']) == world

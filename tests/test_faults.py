@@ -58,8 +58,9 @@ def test_corrupted_magic_bytes_are_dropped_not_unpickled(tmp_path):
 
 def _optimizer(tmp_path, br, **kw):
     from dotaclient_amd.learner.optimizer import DotaOptimizer, OptimizerConfig
+    kw.setdefault('xp_timeout', 10)
     cfg = OptimizerConfig(log_dir=str(tmp_path), model='lstm128', epochs=1, seq_per_epoch=2, batch_size=2,
-                          seq_len=16, device='cpu', xp_timeout=10, **kw)
+                          seq_len=16, device='cpu', **kw)
     return DotaOptimizer(cfg, br)
 
 
@@ -159,3 +160,70 @@ def test_prefetch_thread_surfaces_the_experience_timeout(tmp_path):
     with pytest.raises(TimeoutError):
         opt.run(iterations=1)
     assert getattr(opt, '_prefetcher', None) is None
+
+
+class _HugeView:
+    """Pickles as a tensor whose claimed size far exceeds its 4-element storage (``set_`` used to grow
+    the storage to fit, so such a message could force an allocation of any size)."""
+
+    def __init__(self, size, stride, offset=0):
+        self.size, self.stride, self.offset = size, stride, offset
+
+    def __reduce__(self):
+        import collections
+        import torch._utils
+        st = torch.zeros(4).untyped_storage()
+        return (torch._utils._rebuild_tensor_v2,
+                (torch.storage.TypedStorage(wrap_storage=st, dtype=torch.float32, _internal=True), self.offset,
+                 self.size, self.stride, False, collections.OrderedDict()))
+
+
+@pytest.mark.parametrize('size,stride,offset', [((1 << 45,), (1,), 0), ((1 << 26, 1, 10), (10, 10, 1), 0),
+                                                ((2,), (1,), 3), ((2,), (-1,), 1)])
+def test_pickled_tensor_views_beyond_their_storage_are_corrupt(size, stride, offset):
+    import pickle
+    from dotaclient_amd.transport.codec import decode_any
+    body = pickle.dumps({'states': {'env': _HugeView(size, stride, offset)}})
+    with pytest.raises(CorruptMessage):
+        decode_any(body, allow_pickle=True)
+
+
+def test_pickled_tensor_views_inside_their_storage_still_decode():
+    import pickle
+    from dotaclient_amd.transport.codec import _ArrayUnpickler
+    import io
+    t = torch.arange(12, dtype=torch.float32).view(3, 4)[1:, 1:3]
+    out = _ArrayUnpickler(io.BytesIO(pickle.dumps({'x': t}))).load()
+    torch.testing.assert_close(out['x'], t)
+
+
+def test_background_publish_failure_surfaces_on_the_main_thread(tmp_path):
+    """with async checkpoints the model publish / file writes run on a writer thread; a failure there must
+    raise on the learner's thread (at the next publish or at flush), not vanish."""
+    br = InProcBroker()
+    opt = _optimizer(tmp_path, br, async_checkpoint=True)
+    calls = []
+
+    def broken_publish(body, version):
+        calls.append(version)
+        raise OSError('publish failed')
+    br.publish_model = broken_publish
+    for i in range(4):
+        br.publish_experience(encode(_rollout(i)))
+    with pytest.raises(OSError, match='publish failed'):
+        opt.run(iterations=1)                 # run() flushes the writer on the way out
+    assert calls == [1]
+
+
+def test_prefetch_thread_stops_promptly_and_counts_drops(tmp_path):
+    """close() must end the decode-ahead thread even when it is waiting on an empty queue (the default
+    experience timeout is None), and report decoded rollouts it had to drop."""
+    br = InProcBroker()
+    opt = _optimizer(tmp_path, br, prefetch_rollouts=8, xp_timeout=None)
+    for i in range(5):
+        br.publish_experience(encode(_rollout(i)))
+    opt.run(iterations=1)                     # consumes 2 of 5; the thread decodes ahead and then blocks
+    t0 = time.time()
+    opt.close()
+    assert time.time() - t0 < 5.0
+    assert opt.prefetch_dropped == 3

@@ -92,3 +92,33 @@ def test_adam_kernel_divide_mode(gpu_ops):
     b = _run_flat(b, seq, 1e-3, 0.5, skip=(5,), device='cuda', kernels=True, ranks=4)
     for (n, pa), pb in zip(a.named_parameters(), b.parameters()):
         torch.testing.assert_close(pa, pb.cpu(), rtol=1e-5, atol=2e-6, msg=n)
+
+
+def test_adam_state_remaps_across_flat_layouts():
+    """the flat layout (header + offsets) is recorded with the moments; a state written under another
+    layout is remapped parameter by parameter, and an unversioned state of the wrong length is rejected."""
+    from dotaclient_amd.models.policy import get_config
+    torch.manual_seed(0)
+    model = Policy(get_config('lstm128'))
+    flat = FlatParams(model)
+    opt = FlatAdam(flat, use_kernels=False)
+    for i in range(len(flat.params)):
+        o, n = flat.offsets[i], flat.numel[i]
+        opt.exp_avg[o:o + n] = float(i + 1)
+        opt.exp_avg_sq[o:o + n] = float(10 * (i + 1))
+    sd = opt.state_dict()
+    # the same moments under a different layout (header 0, parameters packed): remapped by parameter
+    old = {'header': 0, 'offsets': [], 'numel': list(sd['layout']['numel'])}
+    off = 0
+    for n in old['numel']:
+        old['offsets'].append(off)
+        off += n
+    legacy = dict(sd, layout=old, exp_avg=torch.cat([torch.full((n,), float(i + 1)) for i, n in enumerate(old['numel'])]),
+                  exp_avg_sq=torch.cat([torch.full((n,), float(10 * (i + 1))) for i, n in enumerate(old['numel'])]))
+    opt2 = FlatAdam(FlatParams(Policy(get_config('lstm128'))), use_kernels=False)
+    opt2.load_state_dict(legacy)
+    torch.testing.assert_close(opt2.exp_avg, opt.exp_avg)
+    torch.testing.assert_close(opt2.exp_avg_sq, opt.exp_avg_sq)
+    unversioned = {k: v for k, v in legacy.items() if k != 'layout'}
+    with pytest.raises(ValueError, match='older layout'):
+        opt2.load_state_dict(unversioned)
