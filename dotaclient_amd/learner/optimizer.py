@@ -239,12 +239,17 @@ class DotaOptimizer:
         return self._consume_decode()
 
     def close(self):
-        """Stop the decode-ahead thread (if any) and join it; rollouts it had already taken from the queue are
-        dropped and counted in ``prefetch_dropped``."""
+        """Stop the decode-ahead / stager thread (if any) and join it; rollouts it had already taken from the queue
+        are dropped and counted in ``prefetch_dropped``."""
         pf = getattr(self, '_prefetcher', None)
-        if pf is not None:
-            self.prefetch_dropped = pf.close()
-            self._prefetcher = None
+        pl = getattr(self, '_pipeline', None)
+        if pl is not None:
+            self.prefetch_dropped = pl.close()
+            self._pipeline = None
+        if pf is not None or pl is not None:
+            if pf is not None:
+                self.prefetch_dropped = pf.close()
+                self._prefetcher = None
             xb = getattr(self, '_xp_broker', None)
             if xb is not None and xb is not self.broker and hasattr(xb, 'close'):
                 xb.close()
@@ -331,69 +336,49 @@ class DotaOptimizer:
         return k
 
     def _ingest_device(self, rollouts: List[Rollout], n_keep: int) -> Dict[str, torch.Tensor]:
-        """Device ingest: every rollout of the iteration is padded to a multiple of ``seq_len`` and concatenated on
-        the host into one pinned buffer per field (a single upload each); returns / GAE and the per-team EMA
-        normalisation run as the HIP segmented reverse scan (``ops/csrc/scan.hip``) over all rollouts at once; the
-        learner's sequences are a reshape of the result. Same numbers as :meth:`experiences_from_rollout` +
-        :meth:`_to_device` (the host path), without per-rollout numpy work or per-sequence stacking."""
+        """Device ingest, inline: stage + upload this iteration's rollouts (valid rows only) and expand them on the
+        device (:mod:`learner.ingest`), then the return / GAE scan. The pipelined form runs the staging on the
+        stager thread one iteration ahead (``prefetch_rollouts`` > 0 on a GPU learner)."""
+        return self._finish_ingest(self._ingest_pipeline(thread=False).stage(rollouts), n_keep)
+
+    def _ingest_pipeline(self, thread: bool):
+        pl = getattr(self, '_pipeline', None)
+        if pl is None:
+            from .ingest import IngestPipeline
+            H = self.policy_cfg.hidden if self.policy.is_recurrent else 0
+            if thread:
+                # a blocking client of its own when the broker has one (TCP): the main thread's broker calls
+                # (queue size, model publish) must not wait behind the stager's long polls
+                mk = getattr(self.broker, 'consumer', None)
+                self._xp_broker = mk() if mk is not None else self.broker
+            pl = self._pipeline = IngestPipeline(self._consume_decode if thread else None, self.cfg.seq_len,
+                                                 self.cfg.seq_per_epoch, self.cfg.algo, H, self.device)
+        return pl
+
+    def _finish_ingest(self, st, n_keep: int) -> Dict[str, torch.Tensor]:
+        """Expand a staged iteration into the padded layout and run the HIP segmented reverse scan (returns / GAE +
+        per-team EMA(0.99) normalisation, ``ops/csrc/scan.hip``) over all its rollouts at once; the learner's
+        sequences are a reshape of the result. Same numbers as :meth:`experiences_from_rollout` + :meth:`_to_device`
+        (the host path)."""
         from ..ops.scan import compute_returns
         cfg = self.cfg
         S = cfg.seq_len
-        dev = self.device
-        lens = [r.length for r in rollouts]
-        off = np.zeros(len(rollouts) + 1, np.int64)
-        off[1:] = np.cumsum([-(-T // S) * S for T in lens])
-        L = int(off[-1])
-        pin = dev.type == 'cuda'
-
-        def cat(name, tail, dtype, conv=None):
-            buf = self._staging(name, (L,) + tuple(tail), dtype, pin)
-            bn = buf.numpy()
-            for r, a, b in zip(rollouts, off[:-1], off[1:]):
-                x = getattr(r, name)
-                n = 0 if x is None else len(x)
-                if n:
-                    bn[a:a + n] = x if conv is None else conv(x)
-                bn[a + n:b] = 0                     # sequence padding (the staging buffer is reused, not zeroed)
-            return buf.to(dev, non_blocking=True)
-        r0 = rollouts[0]
-        A = r0.actions.shape[1]
-        U = r0.units.shape[1]
-        d = {'env': cat('env', (3,), torch.float32), 'units': cat('units', (U, 10), torch.float32),
-             'actions': cat('actions', (A,), torch.uint8), 'masks': cat('masks', (A,), torch.uint8),
-             'logp_old': cat('logp', (), torch.float32)}
-        rew = cat('rewards', (r0.rewards.shape[1],), torch.float32)
-        gae_mode = cfg.algo == 'ppo' and all(r.values is not None for r in rollouts)
-        vals = cat('values', (), torch.float32) if gae_mode else None
-        valid = self._staging('valid', (L,), torch.float32, pin)
-        vn = valid.numpy()
-        for T, a, b in zip(lens, off[:-1], off[1:]):
-            vn[a:a + T] = 1.0
-            vn[a + T:b] = 0.0
-        d['valid'] = valid.to(dev, non_blocking=True)
+        pad = self.__dict__.setdefault('_pad_bufs', {})
+        x = self._pipeline.expand(st, pad)
+        d = {'env': x['env'], 'units': x['units'], 'actions': x['actions'], 'masks': x['masks'],
+             'logp_old': x['logp'], 'valid': x['valid']}
+        rollouts = st.rollouts
         keys = [self._team_key(r.team_id) for r in rollouts]
-        out = compute_returns(rew, vals, off.astype(np.int32), lens, [r.bootstrap_value for r in rollouts],
-                              [bool(r.done) for r in rollouts], keys, self.ema, 'gae' if gae_mode else 'discount',
-                              gamma=cfg.gamma, lam=cfg.gae_lambda, factor=self.running.factor)
+        out = compute_returns(x['rewards'], x.get('values') if st.gae_mode else None, st.off.astype(np.int32),
+                              st.lens, [r.bootstrap_value for r in rollouts], [bool(r.done) for r in rollouts], keys,
+                              self.ema, 'gae' if st.gae_mode else 'discount', gamma=cfg.gamma, lam=cfg.gae_lambda,
+                              factor=self.running.factor)
         d['ret'], d['adv'] = out['ret'], out['adv']
-        d['norm_ret'] = out['norm'] if not gae_mode else out['adv']
+        d['norm_ret'] = out['norm'] if not st.gae_mode else out['adv']
         n_rows = n_keep * S
         d = {k: v[:n_rows].reshape((n_keep, S) + tuple(v.shape[1:])) for k, v in d.items()}
         if self.policy.is_recurrent:
-            H = self.policy_cfg.hidden
-            hid = np.zeros((n_keep, 2, H), np.float32)
-            i = 0
-            for r, T in zip(rollouts, lens):
-                for s in range(-(-T // S)):
-                    if i >= n_keep:
-                        break
-                    a = s * S
-                    if r.hiddens is not None and r.hidden_stride and a % r.hidden_stride == 0 \
-                            and a // r.hidden_stride < len(r.hiddens):
-                        hid[i] = r.hiddens[a // r.hidden_stride]
-                    i += 1
-            h = torch.from_numpy(hid)
-            h = (h.pin_memory() if pin else h).to(dev, non_blocking=True)
+            h = x['hid'][:n_keep]
             d['h0'], d['c0'] = h[:, 0].contiguous(), h[:, 1].contiguous()
         self._normalize_advantages(d)
         return d
@@ -480,31 +465,45 @@ class DotaOptimizer:
         self._check_background()
         self.__dict__.setdefault('_bg_futures', []).append(self._ckpt_pool_get().submit(fn, *args))
 
+    def _pipelined(self) -> bool:
+        return self.ingest == 'device' and self.device.type == 'cuda' and self.cfg.prefetch_rollouts > 0
+
     def run_iteration(self, it: int):
         cfg = self.cfg
         self.timer.start('ingest')
         experiences: List[Sequence] = []
         rollouts: List[Rollout] = []
         n_seq = 0
-        subrewards, rollout_lens, weight_ages = [], [], []
-        canvas = None
-        while n_seq < cfg.seq_per_epoch:
-            r = self.get_rollout()
-            if self.ingest == 'device':
-                rollouts.append(r)
-                n_seq += -(-r.length // cfg.seq_len)
-            else:
-                experiences.extend(self.experiences_from_rollout(r))
-                n_seq = len(experiences)
-            subrewards.append(r.rewards.sum(axis=0))
-            rollout_lens.append(r.length)
-            weight_ages.append(it - r.weight_version)
-            canvas = r.canvas
+        staged = None
+        if self._pipelined():
+            # staged (decoded, packed, uploaded) by the stager thread while the previous iteration trained
+            staged = self._ingest_pipeline(thread=True).get()
+            rollouts, n_seq = staged.rollouts, staged.n_seq
+            if self.consumed is not None:
+                self.consumed.extend((r.game_id, int(r.team_id), int(r.player_id), int(r.weight_version), r.length)
+                                     for r in rollouts)
+        else:
+            while n_seq < cfg.seq_per_epoch:
+                r = self.get_rollout()
+                if self.ingest == 'device':
+                    rollouts.append(r)
+                    n_seq += -(-r.length // cfg.seq_len)
+                else:
+                    experiences.extend(self.experiences_from_rollout(r))
+                    n_seq = len(experiences)
+                if self.ingest != 'device':
+                    rollouts.append(r)
+        subrewards = [r.rewards.sum(axis=0) for r in rollouts]
+        rollout_lens = [r.length for r in rollouts]
+        weight_ages = [it - r.weight_version for r in rollouts]
+        canvas = rollouts[-1].canvas
         self.timer.stop('ingest')
         # all sequences of this iteration go to the device once; minibatches are gathered on-device
         self.timer.start('h2d')
         n = self._agree_steps(n_seq - n_seq % cfg.batch_size)
-        if self.ingest == 'device':
+        if staged is not None:
+            data = self._finish_ingest(staged, n)
+        elif self.ingest == 'device':
             data = self._ingest_device(rollouts, n)
         else:
             data = self._to_device(experiences[:n])
@@ -581,30 +580,43 @@ class DotaOptimizer:
         self.last_metrics = metrics
         if self.checkpoint:
             self.timer.start('log')
-            w = self.writer
-            w.add_scalars(metrics, it)
-            w.add_histogram('losses', loss_t.numpy(), it)
-            w.add_histogram('rollout_lens', np.asarray(rollout_lens), it)
-            w.add_histogram('weight_age', np.asarray(weight_ages), it)
-            w.add_histogram('rewards_per_sec_per_rollout', rollout_rewards, it)
+            hist = None
             if it % cfg.histogram_freq == 1:
-                for name, p in self.policy.named_parameters():
-                    w.add_histogram('param/' + name, p.detach().float().cpu().numpy(), it)
-                w.add_image('canvas', canvas, it)
+                hist = {name: p.detach().float().cpu().numpy() for name, p in self.policy.named_parameters()}
             qs = getattr(self.broker, 'xp_queue_size', None)
-            if qs is not None:
-                w.add_scalar('mq_size', qs, it)
-            w.flush()
+            job = (self._write_logs, it, metrics, loss_t.numpy(), np.asarray(rollout_lens), np.asarray(weight_ages),
+                   rollout_rewards, hist, canvas, qs)
+            if cfg.async_checkpoint and self.device.type == 'cuda':
+                self._submit_background(*job)         # tensorboard events + their upload on the ordered writer
+            else:
+                job[0](*job[1:])
             self.timer.stop('log')
             self.timer.start('publish')
             self.upload_model(version=it)
             self.timer.stop('publish')
-            if self.uploader is not None and w.events_filename:
-                # upload a snapshot: the live events file keeps growing while the uploader copies
-                import shutil
-                snap = w.events_filename + '.snapshot'
-                shutil.copyfile(w.events_filename, snap)
-                self.uploader.submit(snap, f'{self.store_prefix}/{os.path.basename(w.events_filename)}')
+
+    def _write_logs(self, it, metrics, losses, rollout_lens, weight_ages, rollout_rewards, hist, canvas, qs):
+        """The reference's tensorboard scalars / histograms / canvas image (optimizer.py:500-561) and the events
+        file upload (GCS role, :559-561)."""
+        w = self.writer
+        w.add_scalars(metrics, it)
+        w.add_histogram('losses', losses, it)
+        w.add_histogram('rollout_lens', rollout_lens, it)
+        w.add_histogram('weight_age', weight_ages, it)
+        w.add_histogram('rewards_per_sec_per_rollout', rollout_rewards, it)
+        if hist is not None:
+            for name, v in hist.items():
+                w.add_histogram('param/' + name, v, it)
+            w.add_image('canvas', canvas, it)
+        if qs is not None:
+            w.add_scalar('mq_size', qs, it)
+        w.flush()
+        if self.uploader is not None and w.events_filename:
+            # upload a snapshot: the live events file keeps growing while the uploader copies
+            import shutil
+            snap = w.events_filename + '.snapshot'
+            shutil.copyfile(w.events_filename, snap)
+            self.uploader.submit(snap, f'{self.store_prefix}/{os.path.basename(w.events_filename)}')
 
     def upload_model(self, version: int):
         if not self.checkpoint:
@@ -635,25 +647,39 @@ class DotaOptimizer:
         return self._ckpt_pool
 
     def _upload_model_async(self, version: int):
-        """GPU learner with ``async_checkpoint``: the main thread only snapshots the weights and trainer state ON THE
-        DEVICE (clones queued behind this iteration's steps + an event); host copies on a stream of the writer's own,
-        serialisation, the model publish and the files run on the ordered background writer, overlapping the next
-        iteration's ingest and training."""
-        sd = {k: v.detach().clone() for k, v in self.policy.state_dict().items()}
-        trainer = {'learner': _clone_dev(self.learner.state_dict()), 'running': copy.deepcopy(self.running.state_dict()),
-                   'iteration': version, 'config': asdict(self.cfg)}
+        """GPU learner with ``async_checkpoint``: the main thread only snapshots the weights and optimizer state ON
+        THE DEVICE — four flat clones (parameters, Adam moments, step counts) queued behind this iteration's steps
+        plus an event, no per-tensor launches, no host sync; host copies on a stream of the writer's own,
+        state-dict assembly, serialisation, the model publish and the files run on the ordered background writer,
+        overlapping the next iteration's ingest and training."""
+        fl, opt = self.learner.flat, self.learner.opt
+        snap = {'flat': fl.flat.detach().clone(), 'exp_avg': opt.exp_avg.clone(), 'exp_avg_sq': opt.exp_avg_sq.clone(),
+                'steps': opt.steps.clone()}
+        meta = {'n_steps': self.learner.n_steps, 'running': copy.deepcopy(self.running.state_dict()),
+                'hparams': {'lr': opt.lr, 'betas': opt.betas, 'eps': opt.eps, 'max_grad_norm': opt.max_grad_norm},
+                'layout': opt.layout()}
         ev = torch.cuda.Event()
         ev.record()
-        self._submit_background(self._publish_snapshot, sd, trainer, ev, version)
+        self._submit_background(self._publish_snapshot, snap, meta, ev, version)
 
-    def _publish_snapshot(self, sd, trainer, ev, version: int):
+    def _publish_snapshot(self, snap, meta, ev, version: int):
         import io
         st = getattr(self, '_pub_stream', None)
         if st is None:
             st = self._pub_stream = torch.cuda.Stream(device=self.device)
         with torch.cuda.stream(st):
             st.wait_event(ev)
-            sd, trainer = _to_cpu(sd), _to_cpu(trainer)
+            snap = _to_cpu(snap)
+        fl = self.learner.flat
+        flat = snap['flat']
+        # own storage per tensor: the message / checkpoint holds exactly the reference's 30 state_dict tensors
+        params = {n: flat[o:o + k].view(p.shape).clone() for n, p, o, k in zip(fl.names, fl.params, fl.offsets,
+                                                                               fl.numel)}
+        sd = {k: params[k] for k in self.policy.state_dict().keys()}
+        optim = {'exp_avg': snap['exp_avg'], 'exp_avg_sq': snap['exp_avg_sq'], 'steps': snap['steps'],
+                 'layout': meta['layout'], **meta['hparams']}
+        trainer = {'learner': {'optimizer': optim, 'n_steps': meta['n_steps']}, 'running': meta['running'],
+                   'iteration': version, 'config': asdict(self.cfg)}
         buf = io.BytesIO()
         torch.save(sd, buf)
         data = buf.getvalue()
@@ -722,17 +748,6 @@ class _RolloutPrefetcher:
         if self.th.is_alive():
             raise RuntimeError('experience prefetch thread did not stop')
         return self.lost + self.q.qsize()
-
-
-def _clone_dev(x):
-    """Device-side snapshot of a (nested) state dict: tensors cloned on the current stream, the rest as is."""
-    if isinstance(x, torch.Tensor):
-        return x.detach().clone()
-    if isinstance(x, dict):
-        return {k: _clone_dev(v) for k, v in x.items()}
-    if isinstance(x, (list, tuple)):
-        return type(x)(_clone_dev(v) for v in x)
-    return x
 
 
 def _to_cpu(x):

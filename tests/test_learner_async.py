@@ -68,3 +68,24 @@ def test_e2e_actor_process_on_gpu():
     assert 0 <= r['avg_weight_age'] < 16
     assert r['queue_dropped'] >= 0 and r['actor_idle_steps_per_s'] > 0
     assert glob.glob(mine) == []
+
+
+def test_pipelined_ingest_matches_inline_on_gpu(tmp_path):
+    """The stager thread (valid rows packed into a pinned slot, uploaded on a copy stream one iteration ahead,
+    expanded to the padded layout on the device) trains on exactly what the inline ingest builds: same rollouts in
+    the same order → bitwise-identical weights and reward statistics after three iterations (slots reused)."""
+    from dotaclient_amd.learner.optimizer import DotaOptimizer, OptimizerConfig
+    outs = []
+    for prefetch in (0, 4):
+        br = InProcBroker()
+        for i in range(24):
+            br.publish_experience(encode(_rollout(i, T=17 + 13 * i)))
+        cfg = OptimizerConfig(log_dir=str(tmp_path / f'p{prefetch}'), model='lstm128', epochs=1, seq_per_epoch=4,
+                              batch_size=2, seq_len=48, device='cuda', xp_timeout=30, prefetch_rollouts=prefetch,
+                              graph=False)
+        opt = DotaOptimizer(cfg, br)
+        opt.run(iterations=3)
+        assert opt._pipelined() == (prefetch > 0)
+        outs.append((opt.learner.flat.flat.detach().cpu().clone(), opt.ema.detach().cpu().clone()))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
