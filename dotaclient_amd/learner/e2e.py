@@ -262,7 +262,7 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
     stop, ready, failed = ctx.Event(), ctx.Event(), ctx.Event()
     steps = ctx.Value('q', 0)
     proc = opt = None
-    rows, wall, actor_steps, idle = [], 0.0, 0, float('nan')
+    rows, wall, actor_steps, idle, gpu_busy = [], 0.0, 0, float('nan'), float('nan')
     err = None
 
     def dropped_total():
@@ -289,6 +289,8 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
             s0, t0 = steps.value, time.perf_counter()
             time.sleep(idle_probe)
             idle = (steps.value - s0) / (time.perf_counter() - t0)
+            if dev.type == 'cuda':
+                gpu_busy = _gpu_busy_probe(opt, steps, idle_probe, batch_size, seq_len)
 
         def check():
             if failed.is_set() or not proc.is_alive():
@@ -339,13 +341,15 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
         raise err
     mine = _summary(rows, wall, actor_steps, queue_dropped, games, dict(seq_per_epoch=seq_per_epoch, seq_len=seq_len))
     mine['actor_idle_steps_per_s'] = idle
+    mine['actor_gpu_busy_steps_per_s'] = gpu_busy
     mine['report'] = extra
     per_rank = [mine]
     if pdist.is_distributed():
         per_rank = [None] * world
         tdist.all_gather_object(per_rank, mine)
     out = dict(per_rank[0])
-    for k in ('steps_per_s', 'valid_steps_per_s', 'actor_steps_per_s', 'actor_idle_steps_per_s'):
+    for k in ('steps_per_s', 'valid_steps_per_s', 'actor_steps_per_s', 'actor_idle_steps_per_s',
+              'actor_gpu_busy_steps_per_s'):
         out[k] = float(sum(r[k] for r in per_rank))
         out[k + '_per_rank'] = [r[k] for r in per_rank]
     out['queue_dropped'] = int(per_rank[0]['queue_dropped'])
@@ -361,6 +365,35 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                          prefetch_rollouts=prefetch, games_per_rank=games,
                          actor=f'one process per rank over the node {transport} broker', learners=world)
     return out
+
+
+def _gpu_busy_probe(opt, steps, seconds: float, batch_size: int, seq_len: int) -> float:
+    """Actor player-steps/s while this rank's learner runs back-to-back training steps on synthetic on-device data
+    and NO host work (no ingest, decode, publish): against the idle-learner rate and the full-loop rate it separates
+    GPU contention (the persistent recurrence holds every CU for ≈1.7-2 ms per launch) from CPU sharing. The
+    learner's weights and optimizer state are restored afterwards."""
+    from .synthetic import DeviceReplay
+    lrn = opt.learner
+    if getattr(lrn, 'backend', None) != 'fused':
+        return float('nan')
+    cfg = opt.policy_cfg
+    rep = DeviceReplay(2 * batch_size, seq_len, cfg.layout, cfg.hidden if cfg.rnn == 'lstm' else None, opt.device,
+                       seed=5)
+    saved = [t.clone() for t in (lrn.flat.flat, lrn.opt.exp_avg, lrn.opt.exp_avg_sq, lrn.opt.steps)]
+    n_steps = lrn.n_steps
+    lrn.train_step_replay(rep.buf, batch_size)
+    torch.cuda.synchronize(opt.device)
+    s0, t0 = steps.value, time.perf_counter()
+    for _ in range(max(1, int(seconds * 200))):    # a fixed count (~5 ms steps): DP ranks run the same all-reduces
+        lrn.train_step_replay(rep.buf, batch_size)
+    torch.cuda.synchronize(opt.device)
+    rate = (steps.value - s0) / (time.perf_counter() - t0)
+    for dst, src in zip((lrn.flat.flat, lrn.opt.exp_avg, lrn.opt.exp_avg_sq, lrn.opt.steps), saved):
+        dst.copy_(src)
+    lrn.n_steps = n_steps
+    lrn.check_error()
+    torch.cuda.synchronize(opt.device)
+    return rate
 
 
 def measure_e2e_procs(**kw) -> Dict[str, float]:
