@@ -71,10 +71,17 @@ def parse():
     ap.add_argument('--e2e-mode', default='process', choices=['process', 'thread'],
                     help='e2e actors as one spawned process per rank over the node broker (deploy split) or as a '
                          'thread (1 GPU only)')
+    ap.add_argument('--e2e-probe', type=float, default=3.0,
+                    help='seconds of each actor probe before the e2e window (learner idle / GPU-only learner)')
     ap.add_argument('--e2e-transport', default='auto', choices=['auto', 'shm', 'tcp'],
                     help='node experience queue: shared-memory ring (auto on one node) or a TCP broker on rank 0')
     from dotaclient_amd.presets import parse_with_preset
     return parse_with_preset(ap, 'bench')
+
+
+def progress(msg: str):
+    """Phase markers on stderr (one line each, flushed) so a long multi-rank run shows where it is."""
+    print(f'[bench r{os.environ.get("RANK", "0")} {time.strftime("%H:%M:%S")}] {msg}', file=sys.stderr, flush=True)
 
 
 def main():
@@ -153,7 +160,9 @@ def main():
         learner.check_error()       # a persistent-kernel timeout would invalidate the measurement
         return elapsed, loss_first, loss_last, learner, policy
 
+    progress(f'learner {args.precision}: world {world}, device {device}')
     elapsed, loss_val, final_loss, learner, policy = run(args.precision)
+    progress(f'learner {args.precision} done: {elapsed / args.steps * 1e3:.3f} ms/step')
     backend = learner.backend
     step_mode = {'hipgraph': learner.graph is not None, 'dp_split_overlap': bool(getattr(learner, '_split', False)),
                  'dist_backend': dist.get_backend() if world > 1 else None}
@@ -166,6 +175,7 @@ def main():
     if args.bf16_extra and args.precision == 'fp32' and use_cuda:
         learner = None
         e16, _, _, _, _ = run('bf16')
+        progress(f'learner bf16 done: {e16 / args.steps * 1e3:.3f} ms/step')
         extra = {'precision': 'bf16', 'value': samples / e16, 'ms_per_step': e16 / args.steps * 1e3}
 
     def gather(x):
@@ -201,6 +211,7 @@ def main():
         except Exception as e:
             mine['policy_step_error'] = repr(e)
         ranks = gather(mine)
+        progress('actor measurements done')
         actor = dict(ranks[0])
         for k in ('steps_per_s', 'policy_step_per_s', 'policy_step_protobuf_featurize_per_s'):
             vals = [r.get(k) for r in ranks]
@@ -219,12 +230,15 @@ def main():
             from dotaclient_amd.learner.e2e import measure_e2e, measure_e2e_node
             kw = dict(model=args.model, device=device, duration=args.e2e, games=args.e2e_games,
                       threads=args.actor_threads, seq_len=args.seq_len, precision=args.precision)
+            progress('e2e start')
             if args.e2e_mode == 'process':
-                e2e = measure_e2e_node(transport=args.e2e_transport, **kw)
+                e2e = measure_e2e_node(transport=args.e2e_transport, progress=progress, idle_probe=args.e2e_probe,
+                                       **kw)
             else:
                 e2e = measure_e2e(**kw)
         except Exception as e:
             e2e = {'error': repr(e)}
+        progress(f'e2e done: {e2e.get("error", "ok")}')
         errs = gather('error' in e2e)
         if any(errs) and 'error' not in e2e:
             e2e = {'error': f'failed on rank(s) {[i for i, x in enumerate(errs) if x]}'}

@@ -208,7 +208,7 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                      rollout_size: int = 9999, warmup_iterations: int = 2, max_iterations: Optional[int] = None,
                      log_dir: Optional[str] = None, prefetch: int = 32, ring_bytes: int = 1 << 26,
                      transport: str = 'auto', backend: str = 'auto', idle_probe: float = 3.0,
-                     report=None, record_consumed: int = 0) -> Dict[str, float]:
+                     report=None, record_consumed: int = 0, progress=None) -> Dict[str, float]:
     """The reference's node topology end to end (optimizer.py:144-150, 274-287; ks-app/components/optimizer.jsonnet:
     79-174): ONE experience queue per node fed by actor processes, ``WORLD_SIZE`` learner ranks (one per GPU, DDP
     over RCCL) consuming disjoint rollouts from it as competing consumers, and rank 0 alone checkpointing and
@@ -229,6 +229,7 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
     import torch.distributed as tdist
     from ..parallel import dist as pdist
     from .optimizer import DotaOptimizer, OptimizerConfig
+    say = progress or (lambda msg: logger.info(msg))
 
     world, rank = pdist.get_world_size(), pdist.get_rank()
     local_world = int(os.environ.get('LOCAL_WORLD_SIZE', world))
@@ -281,21 +282,12 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                               histogram_freq=10 ** 9, async_checkpoint=dev.type == 'cuda',
                               prefetch_rollouts=prefetch, record_consumed=record_consumed)
         opt = DotaOptimizer(cfg, broker, checkpoint=rank == 0)     # rank 0 publishes model version 0
+        say(f'e2e: learner ready ({transport} broker {addr}); waiting for the actor process')
         if not ready.wait(timeout=900) or failed.is_set():
             raise RuntimeError('e2e actor process failed to start')
         if pdist.is_distributed():
             tdist.barrier()
-        if idle_probe > 0:
-            s0, t0 = steps.value, time.perf_counter()
-            time.sleep(idle_probe)
-            idle = (steps.value - s0) / (time.perf_counter() - t0)
-            if dev.type == 'cuda':
-                gpu_busy = _gpu_busy_probe(opt, steps, idle_probe, batch_size, seq_len)
-
-        def check():
-            if failed.is_set() or not proc.is_alive():
-                return RuntimeError(f'e2e actor process died (exit code {proc.exitcode})')
-            return None
+        say('e2e: actor ready')
 
         def agree(cont: bool) -> bool:
             if not pdist.is_distributed():
@@ -303,7 +295,22 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
             t = torch.tensor([1 if cont else 0], dtype=torch.int32, device=coll_dev)
             tdist.all_reduce(t, op=tdist.ReduceOp.MIN)
             return bool(t.item())
+        if idle_probe > 0:
+            s0, t0 = steps.value, time.perf_counter()
+            time.sleep(idle_probe)
+            idle = (steps.value - s0) / (time.perf_counter() - t0)
+            say(f'e2e: idle-learner actor probe {idle:.0f} player-steps/s')
+            if dev.type == 'cuda':
+                gpu_busy = _gpu_busy_probe(opt, steps, idle_probe, batch_size, seq_len, agree)
+                say(f'e2e: busy-GPU actor probe {gpu_busy:.0f} player-steps/s')
+
+        def check():
+            if failed.is_set() or not proc.is_alive():
+                return RuntimeError(f'e2e actor process died (exit code {proc.exitcode})')
+            return None
+
         d0 = dropped_total()
+        say('e2e: learner loop')
         try:
             rows, wall, (actor_steps, _) = _learner_loop(opt, duration, warmup_iterations, max_iterations,
                                                          counters=lambda: (steps.value, 0), check=check, agree=agree)
@@ -367,7 +374,7 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
     return out
 
 
-def _gpu_busy_probe(opt, steps, seconds: float, batch_size: int, seq_len: int) -> float:
+def _gpu_busy_probe(opt, steps, seconds: float, batch_size: int, seq_len: int, agree) -> float:
     """Actor player-steps/s while this rank's learner runs back-to-back training steps on synthetic on-device data
     and NO host work (no ingest, decode, publish): against the idle-learner rate and the full-loop rate it separates
     GPU contention (the persistent recurrence holds every CU for ≈1.7-2 ms per launch) from CPU sharing. The
@@ -384,9 +391,11 @@ def _gpu_busy_probe(opt, steps, seconds: float, batch_size: int, seq_len: int) -
     lrn.train_step_replay(rep.buf, batch_size)
     torch.cuda.synchronize(opt.device)
     s0, t0 = steps.value, time.perf_counter()
-    for _ in range(max(1, int(seconds * 200))):    # a fixed count (~5 ms steps): DP ranks run the same all-reduces
+    for _ in range(400):
         lrn.train_step_replay(rep.buf, batch_size)
-    torch.cuda.synchronize(opt.device)
+        torch.cuda.synchronize(opt.device)
+        if not agree(time.perf_counter() - t0 < seconds):  # DP ranks stop on the same step (same all-reduces)
+            break
     rate = (steps.value - s0) / (time.perf_counter() - t0)
     for dst, src in zip((lrn.flat.flat, lrn.opt.exp_avg, lrn.opt.exp_avg_sq, lrn.opt.steps), saved):
         dst.copy_(src)

@@ -31,9 +31,13 @@ def test_bench_two_ranks_on_one_gpu_deploy_shape():
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=2',
            '--master-addr', '127.0.0.1', '--master-port', str(_port()), 'bench.py', '--gpus', '2', '--steps', '3',
            '--warmup', '2', '--bf16-extra', '0', '--actor-games', '256', '--actor-threads', '4', '--e2e', '6',
-           '--e2e-games', '128']
-    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
-    assert out.returncode == 0, out.stderr[-4000:]
+           '--e2e-games', '128', '--e2e-probe', '1']
+    # the ranks' progress goes to a file under gpurun_out/ as it happens (a long run stays visibly alive)
+    os.makedirs(os.path.join(ROOT, 'gpurun_out'), exist_ok=True)
+    log = os.path.join(ROOT, 'gpurun_out', 'bench_2rank_shared_gpu.err')
+    with open(log, 'w') as err:
+        out = subprocess.run(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=err, text=True, timeout=600)
+    assert out.returncode == 0, open(log).read()[-4000:]
     lines = [ln for ln in out.stdout.splitlines() if ln.startswith('{')]
     assert len(lines) == 1, out.stdout[-4000:]
     r = json.loads(lines[0])
