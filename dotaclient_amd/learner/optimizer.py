@@ -529,7 +529,11 @@ class DotaOptimizer:
                 for k, v in m.items():
                     metrics_acc.setdefault(k, []).append(v)
         if self.device.type == 'cuda':
-            torch.cuda.synchronize(self.device)
+            # a blocking-sync event: the host thread sleeps until the GPU is done instead of spinning a core that
+            # the node's actor threads (same CPU share) can use
+            ev = torch.cuda.Event(blocking=True)
+            ev.record()
+            ev.synchronize()
         self.timer.stop('train')
         loss_t = torch.stack(losses).float().cpu()
         if faults().nan_loss(it):
