@@ -204,6 +204,15 @@ def main():
         if world > 1:
             dist.barrier()
         try:
+            # the same runtime on the reference actor's wire path: every observation a serialised CMsgBotWorldState
+            # decoded + featurized natively, every team's orders an Actions protobuf (agent.py:564-637, 805-825)
+            rt = measure_vec_actor(policy, device, n_games=args.actor_games, threads=args.actor_threads, wire=True)
+            mine.update(protobuf_runtime_steps_per_s=rt['steps_per_s'], protobuf_runtime=rt)
+        except Exception as e:
+            mine['protobuf_runtime_error'] = repr(e)
+        if world > 1:
+            dist.barrier()
+        try:
             from dotaclient_amd.actor.batched import measure_actor_throughput
             mb = measure_actor_throughput(policy, device, n_games=args.actor_games, threads=args.actor_threads)
             mine['policy_step_per_s'] = mb['gpu_steps_per_s']
@@ -213,7 +222,8 @@ def main():
         ranks = gather(mine)
         progress('actor measurements done')
         actor = dict(ranks[0])
-        for k in ('steps_per_s', 'policy_step_per_s', 'policy_step_protobuf_featurize_per_s'):
+        for k in ('steps_per_s', 'protobuf_runtime_steps_per_s', 'policy_step_per_s',
+                  'policy_step_protobuf_featurize_per_s'):
             vals = [r.get(k) for r in ranks]
             if all(v is not None for v in vals):
                 actor[k] = float(sum(vals))

@@ -51,7 +51,7 @@ class _Group:
                                    rollout_size=a.rollout_size, hidden_stride=a.hidden_stride if a.H else 0,
                                    hidden_size=a.H, counts=list(a.cfg.layout.counts), threads=a.threads,
                                    latest_weights_prob=a.latest_weights_prob, start_time=a.start_time, fog=a.fog,
-                                   tag=f'{a.tag}{index}', stagger=a.stagger)
+                                   tag=f'{a.tag}{index}', stagger=a.stagger, wire=a.wire)
         self.S = self.ve.slots
         self.ppg = self.ve.players_per_game
         self.gp = make_slot_policy(a.policy, self.S, device=a.device, seed=seed)
@@ -80,7 +80,7 @@ class VecActor:
                  mode: str = '1v1', seed: int = 0, rollout_size: int = 10 ** 9, max_dota_time: float = 600.0,
                  latest_weights_prob: float = 1.0, hidden_stride: int = 256, threads: int = 8, groups: int = 2,
                  league=None, opponent_refresh: int = 64, start_time: float = -10.0,
-                 fog: bool = True, tag: str = 'vec', stagger: bool = False):
+                 fog: bool = True, tag: str = 'vec', stagger: bool = False, wire: bool = False):
         from .. import native
         if not native.AVAILABLE:
             raise RuntimeError('VecActor needs the native module (python -m dotaclient_amd.native.build)')
@@ -107,6 +107,9 @@ class VecActor:
         self.fog = bool(fog)
         self.tag = tag
         self.stagger = bool(stagger)     # staggered first games (no lockstep bursts of whole-game rollouts)
+        # observations as serialised CMsgBotWorldState protobufs through the native wire decoder + featurizer, and
+        # orders as Actions protobufs (the reference actor's observe / act path, agent.py:805-825)
+        self.wire = bool(wire)
         groups = max(1, min(int(groups), n_games))
         sizes = [n_games // groups + (1 if i < n_games % groups else 0) for i in range(groups)]
         self.groups = [_Group(self, i, sizes[i], seed * 7919 + i) for i in range(groups)]
@@ -237,6 +240,11 @@ class VecActor:
     def steps_taken(self) -> int:
         return sum(int(g.ve.steps_taken) for g in self.groups)
 
+    @property
+    def wire_bytes(self) -> int:
+        """Protobuf bytes serialised and decoded so far (wire mode)."""
+        return sum(int(g.ve.wire_bytes) for g in self.groups)
+
     def step(self):
         """One observation interval of every game. Groups are software-pipelined: the host observes group i+1
         while the GPU steps group i, then acts on group i's outputs while the GPU steps group i+1. Between calls
@@ -272,7 +280,7 @@ class VecActor:
 
 def measure_vec_actor(policy, device='cuda', n_games: int = 2048, steps: int = 100, warmup: int = 10,
                       threads: int = 8, groups: int = 2, hidden_stride: int = 1400, rollout_size: int = 9999,
-                      max_dota_time: float = 600.0) -> Dict[str, float]:
+                      max_dota_time: float = 600.0, wire: bool = False) -> Dict[str, float]:
     """Whole-runtime actor throughput: player-steps/s of :class:`VecActor` self-play (engine + featurize + reward +
     GPU policy + trajectory recording + rollout encoding), rollouts counted (published into a sink). Deploy shape
     (params.libsonnet:16-19): whole-game rollouts (``rollout_size`` 9999) of 600 s games, with staggered first
@@ -283,12 +291,12 @@ def measure_vec_actor(policy, device='cuda', n_games: int = 2048, steps: int = 1
     sink = []
     va = VecActor(ws, n_games, lambda b: sink.append(len(b)), device=device, seed=1, threads=threads,
                   groups=groups, hidden_stride=hidden_stride, rollout_size=rollout_size,
-                  max_dota_time=max_dota_time, stagger=True)
+                  max_dota_time=max_dota_time, stagger=True, wire=wire)
     sync = (lambda: torch.cuda.synchronize(va.device)) if va.device.type == 'cuda' else (lambda: None)
     for _ in range(warmup):
         va.step()
     sync()
-    s0, r0, k0 = va.steps_taken, va.rollouts_sent, len(sink)
+    s0, r0, k0, w0 = va.steps_taken, va.rollouts_sent, len(sink), va.wire_bytes
     t0 = time.perf_counter()
     for _ in range(steps):
         va.step()
@@ -298,4 +306,4 @@ def measure_vec_actor(policy, device='cuda', n_games: int = 2048, steps: int = 1
     return {'steps_per_s': n / dt, 'ms_per_step': dt / steps * 1e3, 'games': n_games,
             'player_steps': n, 'rollouts_per_s': (va.rollouts_sent - r0) / dt,
             'rollout_mb_per_s': sum(sink[k0:]) / dt / 1e6, 'threads': threads, 'groups': groups,
-            'rollout_size': rollout_size}
+            'rollout_size': rollout_size, 'wire': wire, 'protobuf_mb_per_s': (va.wire_bytes - w0) / dt / 1e6}

@@ -71,6 +71,23 @@ struct Reader {
   }
 };
 
+// proto2 wire encoding (the synthetic engine's CMsgBotWorldState on the wire, vecenv.h SimGame::world_bytes):
+// fields are appended in field-number order, so the bytes equal python protobuf's SerializeToString of the same
+// message with the same fields set
+struct Writer {
+  std::string* o;
+  void varint(uint64_t v) {
+    while (v >= 0x80) { o->push_back((char)(uint8_t)(v | 0x80)); v >>= 7; }
+    o->push_back((char)(uint8_t)v);
+  }
+  void tag(int f, int wt) { varint(((uint64_t)f << 3) | (uint64_t)wt); }
+  void u64(int f, uint64_t v) { tag(f, 0); varint(v); }
+  void i32(int f, int32_t v) { tag(f, 0); varint((uint64_t)(int64_t)v); }   // negative: 10-byte sign extension
+  void boolean(int f, bool v) { tag(f, 0); o->push_back(v ? 1 : 0); }
+  void f32(int f, float v) { tag(f, 5); char b[4]; std::memcpy(b, &v, 4); o->append(b, 4); }
+  void bytes(int f, std::string_view s) { tag(f, 2); varint(s.size()); o->append(s.data(), s.size()); }
+};
+
 enum UnitTypeE { HERO = 1, CREEP_HERO = 2, LANE_CREEP = 3, TOWER = 6 };
 
 struct Unit {

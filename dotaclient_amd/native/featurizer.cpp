@@ -118,9 +118,9 @@ class PyVecEnv {
  public:
   PyVecEnv(int n_games, int mode, uint64_t seed, double max_dota_time, long rollout_size, int hidden_stride,
            int hidden_size, std::vector<int> counts, int threads, double latest_weights_prob, bool validation,
-           bool fog, double start_time, std::string tag, bool stagger)
+           bool fog, double start_time, std::string tag, bool stagger, bool wire)
       : env_(make(n_games, mode, seed, max_dota_time, rollout_size, hidden_stride, hidden_size, counts, threads,
-                  latest_weights_prob, validation, fog, start_time, tag, stagger)) {
+                  latest_weights_prob, validation, fog, start_time, tag, stagger, wire)) {
     S_ = env_.slots();
     U_ = env_.units();
     H_ = hidden_size;
@@ -191,6 +191,7 @@ class PyVecEnv {
   long games_finished() const { return env_.games_finished(); }
   long steps_taken() const { return env_.steps_taken(); }
   long rollouts_sent() const { return env_.rollouts_sent(); }
+  long wire_bytes() const { return env_.wire_bytes(); }
   double dota_time(int g) const { return env_.dota_time(g); }
   int status(int g) const { return env_.status(g); }
 
@@ -198,7 +199,7 @@ class PyVecEnv {
   static VecConfig make(int n_games, int mode, uint64_t seed, double max_dota_time, long rollout_size,
                         int hidden_stride, int hidden_size, const std::vector<int>& counts, int threads,
                         double latest_weights_prob, bool validation, bool fog, double start_time,
-                        const std::string& tag, bool stagger) {
+                        const std::string& tag, bool stagger, bool wire) {
     if (n_games < 1 || mode < 0 || mode > 2 || counts.size() != 6 || rollout_size < 1 || hidden_size < 0)
       throw std::invalid_argument("VecEnv: bad configuration");
     VecConfig c;
@@ -217,6 +218,7 @@ class PyVecEnv {
     c.start_time = start_time;
     c.tag = tag;
     c.stagger = stagger;
+    c.wire = wire;
     return c;
   }
   VecEnv env_;
@@ -244,6 +246,11 @@ class PySimGame {
       o.push_back(x);
     }
     g_.step(o);
+  }
+  py::bytes world_bytes(int team) {
+    std::string b;
+    g_.world_bytes(team, b);
+    return py::bytes(b);
   }
   py::tuple featurize(int team, int player_id, std::vector<int> counts) {
     World w;
@@ -300,12 +307,13 @@ PYBIND11_MODULE(_native, m) {
   m.def("crc32c", &crc32c);
   py::class_<PyVecEnv>(m, "VecEnv")
       .def(py::init<int, int, uint64_t, double, long, int, int, std::vector<int>, int, double, bool, bool, double,
-                    std::string, bool>(),
+                    std::string, bool, bool>(),
            py::arg("n_games"), py::arg("mode") = 0, py::arg("seed") = 0, py::arg("max_dota_time") = 600.0,
            py::arg("rollout_size") = (long)1 << 40, py::arg("hidden_stride") = 0, py::arg("hidden_size") = 0,
            py::arg("counts") = std::vector<int>{1, 5, 16, 16, 1, 1}, py::arg("threads") = 8,
            py::arg("latest_weights_prob") = 1.0, py::arg("validation") = false, py::arg("fog") = true,
-           py::arg("start_time") = -10.0, py::arg("tag") = std::string("vec"), py::arg("stagger") = false)
+           py::arg("start_time") = -10.0, py::arg("tag") = std::string("vec"), py::arg("stagger") = false,
+           py::arg("wire") = false)
       .def("begin_step", &PyVecEnv::begin_step)
       .def("observe", &PyVecEnv::observe, py::arg("env"), py::arg("units"), py::arg("handles"), py::arg("active"))
       .def("act", &PyVecEnv::act, py::arg("idx"), py::arg("act"), py::arg("msk"), py::arg("logp"), py::arg("value"),
@@ -318,6 +326,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("games_finished", &PyVecEnv::games_finished)
       .def_property_readonly("steps_taken", &PyVecEnv::steps_taken)
       .def_property_readonly("rollouts_sent", &PyVecEnv::rollouts_sent)
+      .def_property_readonly("wire_bytes", &PyVecEnv::wire_bytes)
       .def("dota_time", &PyVecEnv::dota_time)
       .def("status", &PyVecEnv::status);
   py::class_<PySimGame>(m, "SimGame")
@@ -325,6 +334,7 @@ PYBIND11_MODULE(_native, m) {
            py::arg("seed"), py::arg("start_time") = -10.0, py::arg("fog") = true, py::arg("dt") = 0.5)
       .def("step", &PySimGame::step)
       .def("featurize", &PySimGame::featurize)
+      .def("world_bytes", &PySimGame::world_bytes)
       .def("reward", &PySimGame::reward)
       .def("units", &PySimGame::units)
       .def_property_readonly("dota_time", &PySimGame::dota_time)

@@ -493,6 +493,97 @@ class SimGame {
     n_steps += 1;
   }
 
+  bool visible(const SUnit& u, int team) const {
+    if (!fog || u.team == team || u.unit_type == TOWER) return true;
+    for (const SUnit& a : units) {
+      if (a.team != team || !a.alive) continue;
+      const double dx = a.x - u.x, dy = a.y - u.y, d2 = dx * dx + dy * dy;
+      if (d2 > kVision * kVision * (1.0 + 1e-14)) continue;       // sqrt(d2) > kVision for sure
+      if (std::sqrt(d2) <= kVision) return true;
+    }
+    return false;
+  }
+
+  // CMsgBotWorldState(team) serialised on the wire, field for field what env/synthetic.py world_state() sets (so
+  // the bytes equal its SerializeToString): the protobuf observation the reference's actor receives from
+  // DotaService.observe (agent.py:805-810) and featurizes from (agent.py:564-637).
+  void world_bytes(int team, std::string& out) const {
+    out.clear();
+    Writer w{&out};
+    w.u64(1, (uint64_t)team);
+    w.f32(2, (float)(dota_time + 90.0));
+    w.f32(3, (float)dota_time);
+    thread_local std::string sub, unit;
+    for (const PStats& p : players) {
+      sub.clear();
+      Writer s{&sub};
+      s.i32(1, p.player_id);
+      s.u64(2, (uint64_t)p.hero_id);
+      s.u64(5, (uint64_t)p.kills);
+      s.u64(6, (uint64_t)p.deaths);
+      s.u64(8, (uint64_t)p.team_id);
+      w.bytes(10, sub);
+    }
+    for (const SUnit& u : units) {
+      if (!visible(u, team)) continue;
+      unit.clear();
+      Writer s{&unit};
+      s.u64(1, (uint64_t)(uint32_t)u.handle);
+      s.u64(2, (uint64_t)u.unit_type);
+      s.bytes(3, unit_name(u));
+      s.u64(4, (uint64_t)u.team);
+      s.u64(5, (uint64_t)(uint32_t)u.level);
+      sub.clear();
+      Writer l{&sub};
+      l.f32(1, (float)u.x);
+      l.f32(2, (float)u.y);
+      l.f32(3, 128.0f);
+      s.bytes(6, sub);
+      s.boolean(7, u.alive);
+      s.i32(8, u.player_id);
+      s.f32(11, (float)u.facing);
+      s.i32(20, (int32_t)std::max(0.0, u.hp));
+      s.i32(21, (int32_t)u.hp_max);
+      s.f32(23, (float)u.mana);
+      s.f32(24, (float)u.mana_max);
+      s.i32(30, (int32_t)u.attack_range);
+      s.i32(31, (int32_t)u.damage);
+      s.u64(35, (uint64_t)(uint32_t)u.target);
+      if (u.unit_type == TOWER) s.i32(40, u.target ? 1503 : 1500);
+      s.boolean(50, u.invulnerable);
+      if (u.unit_type == HERO) {
+        int lvl, need;
+        level_from_total_xp(u.total_xp, lvl, need);
+        s.u64(60, (uint64_t)(uint32_t)need);
+      }
+      s.u64(61, (uint64_t)(uint32_t)u.last_hits);
+      s.u64(62, (uint64_t)(uint32_t)u.denies);
+      for (int c : u.projectiles) {
+        sub.clear();
+        Writer q{&sub};
+        q.u64(1, (uint64_t)(uint32_t)c);
+        q.boolean(4, true);
+        s.bytes(70, sub);
+      }
+      w.bytes(11, unit);
+    }
+  }
+
+  std::string_view unit_name(const SUnit& u) const {
+    const bool r = u.team == TEAM_R;
+    switch (u.kind) {
+      case K_HERO:
+        for (const PStats& p : players)
+          if (p.player_id == u.player_id)
+            return p.hero_id == HERO_NEVERMORE ? "npc_dota_hero_nevermore" : "npc_dota_hero_sniper";
+        return "npc_dota_hero_sniper";
+      case K_TOWER1: return r ? "npc_dota_goodguys_tower1_mid" : "npc_dota_badguys_tower1_mid";
+      case K_TOWER2: return r ? "npc_dota_goodguys_tower2_mid" : "npc_dota_badguys_tower2_mid";
+      case K_MELEE: return r ? "npc_dota_creep_goodguys_melee" : "npc_dota_creep_badguys_melee";
+      default: return r ? "npc_dota_creep_goodguys_ranged" : "npc_dota_creep_badguys_ranged";
+    }
+  }
+
   // CMsgBotWorldState(team) as the featurizer sees it after the protobuf round trip
   void world(int team, World& w) const {
     w.dota_time = (float)dota_time;
@@ -749,6 +840,9 @@ struct VecConfig {
   // lockstep games do not all finish (and publish whole-game rollouts) on the same step
   bool stagger = false;
   std::string tag = "vec";
+  // observations as serialised CMsgBotWorldState protobufs decoded by the wire featurizer (the reference actor's
+  // observe → featurize path) instead of straight from the engine's state
+  bool wire = false;
 };
 
 struct Traj {
@@ -790,6 +884,7 @@ struct VGame {
   std::vector<SimGame::Order> orders;
   double last_reward_sum[2] = {0, 0};   // per-team Σ of this step's shaped rewards (zero-sum ``enemy`` term)
   World world_buf[2];
+  std::string wire_buf[2];       // wire mode: this step's serialised observations (World names point into them)
 };
 
 class VecEnv {
@@ -863,6 +958,7 @@ class VecEnv {
   long games_finished() const { return games_finished_; }
   long steps_taken() const { return steps_taken_.load(); }
   long rollouts_sent() const { return rollouts_sent_.load(); }
+  long wire_bytes() const { return wire_bytes_.load(); }
   double dota_time(int gi) const { return games_[gi].sim.dota_time; }
   int status(int gi) const { return games_[gi].sim.status; }
   const std::vector<uint8_t>& canvas(int gi) const { return games_[gi].canvas; }
@@ -945,8 +1041,18 @@ class VecEnv {
     }
     g.obs_time = (float)g.sim.dota_time;
     World* w = g.world_buf;        // per-game scratch: the unit vectors keep their capacity across steps
-    g.sim.world(TEAM_R, w[0]);
-    g.sim.world(TEAM_D, w[1]);
+    if (cfg_.wire) {
+      // the reference actor's path: serialised CMsgBotWorldState per team → wire decode → featurize
+      for (int ti = 0; ti < 2; ++ti) {
+        g.sim.world_bytes(ti == 0 ? TEAM_R : TEAM_D, g.wire_buf[ti]);
+        w[ti].units.clear();
+        parse_world((const uint8_t*)g.wire_buf[ti].data(), g.wire_buf[ti].size(), w[ti]);
+        wire_bytes_ += (long)g.wire_buf[ti].size();
+      }
+    } else {
+      g.sim.world(TEAM_R, w[0]);
+      g.sim.world(TEAM_D, w[1]);
+    }
     double reward_sum[2] = {0, 0};
     for (VPlayer& p : g.players) {
       const int ti = p.team == TEAM_R ? 0 : 1;
@@ -1057,6 +1163,7 @@ class VecEnv {
         }
         g.orders.push_back(o);
       }
+      if (cfg_.wire) wire_orders(g);
       g.sim.step(g.orders);
       // zero-sum shaping: subtract the opponent team's summed step reward (agent.py:829-833)
       if (!cfg_.validation)
@@ -1072,6 +1179,96 @@ class VecEnv {
     }
     steps_taken_ += stepped;
     if (g.done || (double)g.obs_time >= g.limit) finish(g, version);
+  }
+
+  // wire mode: each team's orders travel as the reference's Actions protobuf (CMsgBotWorldState.Actions{dota_time,
+  // actions[]}, features/actions.py action_to_pb ↔ agent.py:665-695, 822-825) and are decoded back into the engine's
+  // orders — the act() half of the DotaService round trip
+  void wire_orders(VGame& g) {
+    std::string& buf = g.wire_buf[0];          // observations of this step are featurized already
+    std::vector<SimGame::Order> decoded;
+    for (int team : {TEAM_R, TEAM_D}) {
+      buf.clear();
+      Writer w{&buf};
+      w.f32(1, (float)g.obs_time);
+      thread_local std::string a, sub, loc;
+      for (const SimGame::Order& o : g.orders) {
+        if (team_of(g, o.player) != team) continue;
+        a.clear();
+        Writer x{&a};
+        x.u64(1, o.type == 1 ? 37u : (o.type == 2 ? 4u : 0u));   // MOVE_DIRECTLY / ATTACK_TARGET / NONE
+        x.i32(2, o.player);
+        x.i32(3, 0);                                             // actionDelay
+        if (o.type == 1) {
+          loc.clear();
+          Writer l{&loc};
+          l.f32(1, (float)o.mx);
+          l.f32(2, (float)o.my);
+          l.f32(3, 0.f);
+          sub.clear();
+          Writer m{&sub};
+          m.bytes(2, loc);
+          x.bytes(10, sub);
+        } else if (o.type == 2) {
+          sub.clear();
+          Writer m{&sub};
+          m.i32(2, (int32_t)o.target);
+          m.boolean(3, true);
+          x.bytes(12, sub);
+        }
+        w.bytes(2, a);
+      }
+      wire_bytes_ += (long)buf.size();
+      parse_actions((const uint8_t*)buf.data(), buf.size(), decoded);
+    }
+    g.orders.swap(decoded);
+  }
+
+  static int team_of(const VGame& g, int player) {
+    for (const VPlayer& p : g.players)
+      if (p.player_id == player) return p.team;
+    return 0;
+  }
+
+  static void parse_actions(const uint8_t* data, size_t n, std::vector<SimGame::Order>& out) {
+    Reader r{data, data + n};
+    while (r.ok()) {
+      const uint64_t k = r.varint();
+      const int f = (int)(k >> 3), wt = (int)(k & 7);
+      if (!(wt == 2 && f == 2)) { r.skip(wt); continue; }
+      const std::string_view a = r.bytes();
+      Reader ar{(const uint8_t*)a.data(), (const uint8_t*)a.data() + a.size()};
+      SimGame::Order o;
+      uint64_t type = 0;
+      while (ar.ok()) {
+        const uint64_t ak = ar.varint();
+        const int af = (int)(ak >> 3), awt = (int)(ak & 7);
+        if (awt == 0 && af == 1) type = ar.varint();
+        else if (awt == 0 && af == 2) o.player = (int)(int32_t)ar.varint();
+        else if (awt == 2 && (af == 10 || af == 12)) {
+          const std::string_view m = ar.bytes();
+          Reader mr{(const uint8_t*)m.data(), (const uint8_t*)m.data() + m.size()};
+          while (mr.ok()) {
+            const uint64_t mk = mr.varint();
+            const int mf = (int)(mk >> 3), mwt = (int)(mk & 7);
+            if (af == 10 && mwt == 2 && mf == 2) {
+              Unit tmp;
+              parse_vector(mr.bytes(), tmp);
+              o.mx = (double)tmp.x;
+              o.my = (double)tmp.y;
+            } else if (af == 12 && mwt == 0 && mf == 2) {
+              o.target = (int64_t)(int32_t)mr.varint();
+            } else {
+              mr.skip(mwt);
+            }
+          }
+        } else {
+          ar.skip(awt);
+        }
+      }
+      o.type = type == 37 ? 1 : (type == 4 ? 2 : 0);
+      out.push_back(o);
+    }
   }
 
   void finish(VGame& g, long version) {
@@ -1108,7 +1305,7 @@ class VecEnv {
   PyRandom rng_;
   uint64_t started_ = 0;
   long games_finished_ = 0;
-  std::atomic<long> steps_taken_{0}, rollouts_sent_{0};
+  std::atomic<long> steps_taken_{0}, rollouts_sent_{0}, wire_bytes_{0};
   std::mutex out_m_;
   std::vector<std::string> out_;
   std::vector<std::array<int, 3>> results_;

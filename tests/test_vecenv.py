@@ -198,3 +198,74 @@ def test_actor_native_featurize_rollouts_identical(seed):
     for a, b in zip(out[False], out[True]):
         for k in ('env', 'units', 'actions', 'masks', 'rewards', 'logp', 'values', 'canvas'):
             np.testing.assert_array_equal(getattr(a, k), getattr(b, k), err_msg=k)
+
+
+@pytest.mark.parametrize('seed', [3, 2 ** 33 + 5])
+def test_simgame_world_bytes_equal_python_protobuf(seed):
+    """The engine's serialised CMsgBotWorldState (the observation the reference actor receives from
+    DotaService.observe, agent.py:805-810) is byte-identical to python protobuf's SerializeToString of the oracle's
+    world_state, for both teams' views (fog included), every step."""
+    cfg = get_1v1_selfplay_config()
+    py = SyntheticGame(cfg, seed=seed)
+    cc = N.SimGame(_picks(cfg), seed)
+    rng = np.random.default_rng(seed)
+    for step in range(400):
+        for team in (TEAM_RADIANT, TEAM_DIRE):
+            want = py.world_state(team).SerializeToString()
+            got = cc.world_bytes(team)
+            assert got == want, (step, team)
+        acts, orders = {}, []
+        for team, pid in ((TEAM_RADIANT, 0), (TEAM_DIRE, 5)):
+            hero = get_unit(py.world_state(team), pid)
+            mx, my = hero.location.x + 68.75 * int(rng.integers(-4, 5)), hero.location.y + 68.75 * int(rng.integers(-4, 5))
+            a = pb.CMsgBotWorldState.Action(actionType=pb.CMsgBotWorldState.Action.DOTA_UNIT_ORDER_MOVE_DIRECTLY,
+                                            player=pid)
+            a.moveDirectly.location.x, a.moveDirectly.location.y = mx, my
+            acts[team] = [a]
+            orders.append((pid, 1, a.moveDirectly.location.x, a.moveDirectly.location.y, -1))
+        py.step(acts)
+        cc.step(orders)
+        if py.status != 0:
+            break
+
+
+@pytest.mark.parametrize('mode', ['1v1', '5v5'])
+def test_vecenv_wire_observations_identical(mode):
+    """VecEnv(wire=True) — observations serialised to protobuf and featurized by the wire decoder, the reference
+    actor's path — yields exactly the struct path's observations and rollouts."""
+    from dotaclient_amd.constants import LAYOUT_5V5
+    lay = LAYOUT_1V1 if mode == '1v1' else LAYOUT_5V5
+    m = 0 if mode == '1v1' else 1
+    envs = [N.VecEnv(6, mode=m, seed=9, max_dota_time=40.0, counts=list(lay.counts), threads=2, wire=w,
+                     rollout_size=37) for w in (False, True)]
+    S, U = envs[0].slots, lay.max_units
+    rng = np.random.default_rng(0)
+    out = []
+    for ve in envs:
+        out.append([])
+        r = np.random.default_rng(0)
+        for step in range(120):
+            ve.begin_step()
+            env = np.zeros((S, 3), np.float32)
+            units = np.zeros((S, U, 10), np.float32)
+            handles = np.zeros((S, U), np.int64)
+            active = np.zeros(S, np.uint8)
+            ve.observe(env, units, handles, active)
+            out[-1].append((env.copy(), units.copy(), handles.copy(), active.copy()))
+            idx = np.zeros((S, 4), np.int32)
+            idx[:, 0] = r.integers(0, 3, S)                   # none / move / attack (orders via Actions protobufs)
+            idx[:, 1] = r.integers(0, 9, S)
+            idx[:, 2] = r.integers(0, 9, S)
+            idx[:, 3] = r.integers(0, U, S)
+            A = 21 + U
+            ve.act(idx, np.zeros((S, A), np.uint8), np.zeros((S, A), np.uint8), np.zeros(S, np.float32),
+                   np.zeros(S, np.float32), None, None, handles, 0)
+            out[-1].append(tuple(sorted(ve.pop_rollouts())))      # (pool threads emit in any order)
+    assert envs[1].wire_bytes > 0 and envs[0].wire_bytes == 0
+    for a, b in zip(out[0], out[1]):
+        for x, y in zip(a, b):
+            if isinstance(x, np.ndarray):
+                np.testing.assert_array_equal(x, y)
+            else:
+                assert x == y
+    del rng
