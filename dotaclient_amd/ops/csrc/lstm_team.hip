@@ -146,6 +146,13 @@ __device__ __forceinline__ float row_sum16(float v) {
   return v;
 }
 
+// Σ over the 32 lanes of this lane's half-wave (two DPP rows), result in every lane: row sum, then xor 16 by
+// ds_swizzle (bit mode, and 0x1f / xor 0x10 inside each 32-lane group)
+__device__ __forceinline__ float row_sum32(float v) {
+  v = row_sum16(v);
+  return v + __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), 0x401F));
+}
+
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, int bytes) {
   const unsigned long long a = (unsigned long long)p;
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)a);
@@ -272,7 +279,10 @@ __device__ __forceinline__ unsigned make_tagbase(unsigned epoch, unsigned iter) 
 // W_hh[row(col)][kg·H/4 … kg·H/4 + H/4) as fp32 VGPRs (128 at H = 512), reads h_{t-1} (fp32, LDS) with broadcast
 // 16-B loads, and the four k-quarters are summed with two cross-lane adds; a quad broadcast then hands each lane
 // of the (row 0, unit) quad all four gates — the lane mapping of the MFMA path after its 4×4 transpose.
-template <int MT, int KS, bool F32, bool V1>
+// VAR: 0 = MFMA tiles, 1 = V1 (exact fp32 VALU, 4 waves: lane = (unit, one of 16 K slices)), 2 = V2 (V1 on 8
+// waves — two per SIMD — at H = 512: lane = (unit, one of 32 K slices of 16), so a SIMD interleaves two waves' FMA
+// streams instead of issuing one wave's every other cycle; each wave owns 2 units, a lane half the K slice)
+template <int MT, int KS, bool F32, int VAR>
 __device__ __forceinline__ void lstm_team_fwd_body(
     const float* __restrict__ xp4, const void* __restrict__ whh_, const float* __restrict__ h0,
     const float* __restrict__ c0, short* __restrict__ hs, float* __restrict__ hsf, float* __restrict__ cs,
@@ -285,14 +295,19 @@ __device__ __forceinline__ void lstm_team_fwd_body(
   constexpr int KSTEP = H / 32;         // k-steps of the full K
   constexpr int HP = H + 8;             // LDS row pitch (bf16)
   constexpr int RB = MT * 16;
-  constexpr int KSL = H / 16;           // V1: K slice per lane
+  constexpr bool V1 = VAR >= 1;
+  constexpr int NT = VAR == 2 ? 512 : kThreads;   // threads per workgroup
+  constexpr int LPU = VAR == 2 ? 32 : 16;         // V1/V2: lanes (K slices) per unit
+  constexpr int UPW = 64 / LPU;                   // V1/V2: units per wave
+  constexpr int KSL = H / LPU;                    // V1/V2: K slice per lane
   static_assert(!V1 || (F32 && MT == 1), "V1 is the fp32 one-row variant");
+  static_assert(VAR != 2 || H == 512, "V2 maps 8 waves x 2 units onto the 16 units of H = 512");
   __shared__ short hl[V1 ? 1 : 2][V1 ? 1 : RB][V1 ? 1 : HP];
   __shared__ short hlo[F32 && !V1 ? 2 : 1][F32 && !V1 ? RB : 1][F32 && !V1 ? HP : 1];   // F32: lo bf16 half of h
   // V1: h_{t-1} of row 0 as 16 K slices, each padded by 4 floats (the 16 lanes of a row read 16 different slices
   // with one ds_read_b128: unpadded 128-B strides would put pairs of lanes on the same banks)
   constexpr int SP = KSL + 4;
-  __shared__ __attribute__((aligned(16))) float hf[V1 ? 2 : 1][V1 ? 16 * SP : 4];
+  __shared__ __attribute__((aligned(16))) float hf[V1 ? 2 : 1][V1 ? LPU * SP : 4];
   __shared__ int sh_int;
   __shared__ unsigned sh_epoch;
 
@@ -303,7 +318,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
   const int team = me >> 6, m = me & 63;
   const int j0 = m * U;
 #define TSTAMP(ev)                                                                                        \
-  if (trace && lane == 0 && chain == 0 && t < 64)                                                          \
+  if (trace && lane == 0 && wv < 4 && chain == 0 && t < 64)                                                \
     trace[(((size_t)m * 4 + wv) * 64 + t) * 8 + (ev)] = __builtin_amdgcn_s_memrealtime()
   // granules per row: bf16 h → H/2 (2 units each), F32 h → H (one unit each)
   constexpr int GPR = F32 ? H : H / 2;
@@ -311,13 +326,13 @@ __device__ __forceinline__ void lstm_team_fwd_body(
 
   // zero the padding rows of both h buffers once
   if constexpr (!V1)
-    for (int i = tid; i < 2 * RB * HP; i += kThreads) (&hl[0][0][0])[i] = 0;
+    for (int i = tid; i < 2 * RB * HP; i += NT) (&hl[0][0][0])[i] = 0;
   if constexpr (F32 && !V1)
-    for (int i = tid; i < 2 * RB * HP; i += kThreads) (&hlo[0][0][0])[i] = 0;
+    for (int i = tid; i < 2 * RB * HP; i += NT) (&hlo[0][0][0])[i] = 0;
 
   // W_hh slice for this wave's tile: columns c = 4·ul + q ↔ gate row q·H + j0 + 4·wv + ul, full K, in VGPRs
   // (F32: fp32 W_hh split into hi/lo bf16 fragments once, here)
-  const bool mfma_wave = wv < NTILE;
+  const bool mfma_wave = VAR == 2 || wv < NTILE;
   const int col = lane & 15, kg = lane >> 4;
   bf16x8 wf[V1 ? 1 : KSTEP];
   bf16x8 wfl[F32 && !V1 ? KSTEP : 1];
@@ -325,11 +340,11 @@ __device__ __forceinline__ void lstm_team_fwd_body(
   if (mfma_wave) {
     const int row = (col & 3) * H + j0 + 4 * wv + (col >> 2);
     if constexpr (V1) {
-      // lane (u = lane/16, slice = lane%16): W_hh rows of the 4 gates of unit j0 + 4·wv + u over the slice
+      // lane (u = lane/LPU, slice = lane%LPU): W_hh rows of the 4 gates of unit j0 + UPW·wv + u over the slice
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const float* wr = static_cast<const float*>(whh_) + (size_t)(g * H + j0 + 4 * wv + (lane >> 4)) * H +
-                          (lane & 15) * KSL;
+        const float* wr = static_cast<const float*>(whh_) + (size_t)(g * H + j0 + UPW * wv + lane / LPU) * H +
+                          (lane % LPU) * KSL;
 #pragma unroll
         for (int j = 0; j < KSL; j += 4) {
           const float4 v = *reinterpret_cast<const float4*>(wr + j);
@@ -349,8 +364,8 @@ __device__ __forceinline__ void lstm_team_fwd_body(
   }
   // elementwise mapping after the 4×4 transpose: lane → (row 4·kg + (col&3) [+16·mt], unit j0 + 4·wv + col/4)
   // (V1: lane (u, slice) → row = slice — only slice 0 is a live row —, unit j0 + 4·wv + u)
-  const int erow = V1 ? (lane & 15) : 4 * kg + (col & 3);
-  const int eunit = j0 + 4 * wv + (V1 ? (lane >> 4) : (col >> 2));
+  const int erow = V1 ? (lane % LPU) : 4 * kg + (col & 3);
+  const int eunit = j0 + (V1 ? UPW * wv + lane / LPU : 4 * wv + (col >> 2));
   // folded LSTM bias (b_ih + b_hh, unit-major): xp4 may then be the bare input projection
   const dca::f32x4 bv = (bias4 && mfma_wave) ? *reinterpret_cast<const dca::f32x4*>(bias4 + eunit * 4)
                                              : dca::f32x4{0.f, 0.f, 0.f, 0.f};
@@ -388,7 +403,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
       }
       // ---- gather h_{t-1} into hl[par]
       if (t == 0) {
-        for (int i = tid; i < B * H; i += kThreads) {
+        for (int i = tid; i < B * H; i += NT) {
           const int b = i / H, k = i % H;
           const float v = h0[(size_t)(b0 + b) * H + k];
           if constexpr (V1) {
@@ -402,12 +417,12 @@ __device__ __forceinline__ void lstm_team_fwd_body(
         const unsigned tag = tagbase | (unsigned)t;          // h_{t-1} carries tag t
         const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(xg + (size_t)((t - 1) & 1) * Bc * GPR, Bc * GPR * 8);
         constexpr int CPR = F32 ? H / 2 : H / 4;              // 16-B chunks (2 f32 / 4 bf16 h values) per row
-        constexpr int NL = ((V1 ? 1 : RB) * CPR + kThreads - 1) / kThreads;   // (V1: one row)
+        constexpr int NL = ((V1 ? 1 : RB) * CPR + NT - 1) / NT;   // (V1: one row)
         // every chunk is re-polled only until it has arrived, so later rounds move only the missing bytes
         i32x4 g[NL];
         bool okc[NL];
 #pragma unroll
-        for (int i = 0; i < NL; ++i) okc[i] = tid + kThreads * i >= B * CPR;
+        for (int i = 0; i < NL; ++i) okc[i] = tid + NT * i >= B * CPR;
         for (int i = 0; i < (knobs & 0xff); ++i) __builtin_amdgcn_s_sleep(1);
         if ((knobs >> 9) & 1) {
           while (!okc[0]) {
@@ -420,7 +435,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
         while (!dead) {
 #pragma unroll
           for (int i = 0; i < NL; ++i)
-            if (!okc[i]) g[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + kThreads * i) * 16, 0, kSc1);
+            if (!okc[i]) g[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (tid + NT * i) * 16, 0, kSc1);
           bool ok = true;
 #pragma unroll
           for (int i = 0; i < NL; ++i) {
@@ -432,7 +447,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
         }
 #pragma unroll
         for (int i = 0; i < NL; ++i) {
-          const int ci = tid + kThreads * i;
+          const int ci = tid + NT * i;
           if (ci < B * CPR) {
             if constexpr (V1) {
               const int k = 2 * ci;
@@ -464,12 +479,19 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           if (mt * 16 >= B) break;                            // wave-uniform
           float gq0 = 0.f, gq1 = 0.f, gq2 = 0.f, gq3 = 0.f;
           if constexpr (V1) {
-            // ---- exact fp32: 4 gates of this lane's unit over its K slice, summed over the row's 16 slices
-            pk_dot4<KSL>(wq, &hf[par][(lane & 15) * SP], gq0, gq1, gq2, gq3);
-            gq0 = row_sum16(gq0);
-            gq1 = row_sum16(gq1);
-            gq2 = row_sum16(gq2);
-            gq3 = row_sum16(gq3);
+            // ---- exact fp32: 4 gates of this lane's unit over its K slice, summed over the unit's LPU slices
+            pk_dot4<KSL>(wq, &hf[par][(lane % LPU) * SP], gq0, gq1, gq2, gq3);
+            if constexpr (LPU == 32) {
+              gq0 = row_sum32(gq0);
+              gq1 = row_sum32(gq1);
+              gq2 = row_sum32(gq2);
+              gq3 = row_sum32(gq3);
+            } else {
+              gq0 = row_sum16(gq0);
+              gq1 = row_sum16(gq1);
+              gq2 = row_sum16(gq2);
+              gq3 = row_sum16(gq3);
+            }
           } else {
           // ---- gates pre-activation tile: rows = batch, columns = (unit, gate)
           dca::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
@@ -580,7 +602,8 @@ __device__ __forceinline__ void lstm_team_fwd_body(
 // =============================================================================================================
 // V1 (F32, one row per chain): the partial recurrent gradient as exact fp32 VALU dot products — lane (u, kg) keeps
 // W_hhᵀ[gc][j0 + u] for its wave's K quarter and k-group as fp32 VGPRs, dG_{t+1} of row 0 sits in LDS in fp32.
-template <int MT, int KS, bool F32, bool V1>
+// VAR 2 (V2, H = 512): 8 waves, each over one eighth of K = 4H (lane = (4 units, one of 16 slices of 16 gate columns))
+template <int MT, int KS, bool F32, int VAR>
 __device__ __forceinline__ void lstm_team_bwd_body(
     const float* __restrict__ dhs, const float* __restrict__ gates4, const float* __restrict__ cs,
     const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
@@ -589,19 +612,23 @@ __device__ __forceinline__ void lstm_team_bwd_body(
     unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart, int knobs) {
   constexpr int H = 128 * KS;
   constexpr int U = H / kT;             // 4·KS units per workgroup (MFMA N, zero-padded to 16)
-  constexpr int KW = H;                 // K (= 4H gate columns) per wave
+  constexpr bool V1 = VAR >= 1;
+  constexpr int NW = VAR == 2 ? 8 : 4;  // waves (K parts)
+  constexpr int NT = 64 * NW;
+  constexpr int KW = 4 * H / NW;        // K (= 4H gate columns) per wave
   constexpr int KSTEP = KW / 32;
   constexpr int RB = MT * 16;
   constexpr int GP = 4 * H + 8;         // LDS pitch (bf16) of the gathered dG rows
-  constexpr int NPAIR = (RB * U + kThreads - 1) / kThreads;
-  constexpr int KSL = KW / 16;          // V1: K slice per lane of a wave's K quarter
+  constexpr int NPAIR = (RB * U + NT - 1) / NT;
+  constexpr int KSL = KW / 16;          // V1: K slice per lane of a wave's K part
   static_assert(!V1 || (F32 && MT == 1), "V1 is the fp32 one-row variant");
+  static_assert(VAR != 2 || H == 512, "V2 is the H = 512 variant");
   __shared__ short dgl[V1 ? 1 : RB][V1 ? 1 : GP];
   __shared__ short dglo[F32 && !V1 ? RB : 1][F32 && !V1 ? GP : 1];   // F32: lo bf16 half of the gathered dG
   // V1: dG_{t+1} of row 0, fp32, as 64 K slices each padded by 4 floats (bank spread, as forward)
   constexpr int SP = KSL + 4;
   __shared__ __attribute__((aligned(16))) float dgf[V1 ? (4 * H / KSL) * SP : 4];
-  __shared__ float red[4][RB][17];
+  __shared__ float red[NW][RB][17];
   __shared__ float dbs[RB * U * 4];     // per-(row, unit, gate) bias-gradient sums of a chain
   __shared__ int sh_int;
   __shared__ unsigned sh_epoch;
@@ -616,13 +643,13 @@ __device__ __forceinline__ void lstm_team_bwd_body(
   constexpr int CPU_ = F32 ? 2 : 1;
   i32x4* xg = xg_all + (size_t)team * 2 * Bc * H * CPU_;
 #define TSTAMPB(ev)                                                                                       \
-  if (trace && lane == 0 && chain == 0 && k < 64)                                                         \
+  if (trace && lane == 0 && wv < 4 && chain == 0 && k < 64)                                               \
     trace[(((size_t)m * 4 + wv) * 64 + k) * 8 + (ev)] = __builtin_amdgcn_s_memrealtime()
 
   if constexpr (!V1)
-    for (int i = tid; i < RB * GP; i += kThreads) (&dgl[0][0])[i] = 0;
+    for (int i = tid; i < RB * GP; i += NT) (&dgl[0][0])[i] = 0;
   if constexpr (F32 && !V1)
-    for (int i = tid; i < RB * GP; i += kThreads) (&dglo[0][0])[i] = 0;
+    for (int i = tid; i < RB * GP; i += NT) (&dglo[0][0])[i] = 0;
 
   // B operand: lane holds Wᵀ[gc][u] for gc = wv·H + ks·32 + 8·kg + j, u = lane & 15 (zero for u ≥ U)
   const int col = lane & 15, kg = lane >> 4;
@@ -674,7 +701,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
     for (int i = 0; i < NPAIR; ++i) dsum[i] = dca::f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < NPAIR; ++i) {
-      const int pi = tid + kThreads * i;
+      const int pi = tid + NT * i;
       dcarry[i] = (pi < B * U && dcn) ? dcn[(size_t)(b0 + pi / U) * H + j0 + pi % U] : 0.f;
     }
     bool dead = false;
@@ -688,7 +715,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       if (t >= 0) {
 #pragma unroll
         for (int i = 0; i < NPAIR; ++i) {
-          const int pi = tid + kThreads * i;
+          const int pi = tid + NT * i;
           if (pi < B * U) {
             const int b = pi / U, u = pi % U;
             const size_t bt = (size_t)(b0 + b) * sb + (size_t)t * st;
@@ -704,17 +731,17 @@ __device__ __forceinline__ void lstm_team_bwd_body(
         const unsigned tag = tagbase | (unsigned)(t + 2);
         const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(xg + (size_t)((t + 1) & 1) * Bc * H * CPU_, Bc * H * CPU_ * 16);
         constexpr int RG = V1 ? 1 : (F32 ? 4 : 8);         // rows per gather group
-        constexpr int NL = RG * H * CPU_ / kThreads;       // chunks per thread per group
+        constexpr int NL = RG * H * CPU_ / NT;             // chunks per thread per group
         for (int g0 = 0; g0 < B && !dead; g0 += RG) {
           const int nck = min(RG, B - g0) * H * CPU_;
           i32x4 g[NL];
           bool okc[NL];
 #pragma unroll
-          for (int i = 0; i < NL; ++i) okc[i] = tid + kThreads * i >= nck;
+          for (int i = 0; i < NL; ++i) okc[i] = tid + NT * i >= nck;
           while (true) {
 #pragma unroll
             for (int i = 0; i < NL; ++i)
-              if (!okc[i]) g[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (g0 * H * CPU_ + tid + kThreads * i) * 16, 0, kSc1);
+              if (!okc[i]) g[i] = __builtin_amdgcn_raw_buffer_load_b128(rs, (g0 * H * CPU_ + tid + NT * i) * 16, 0, kSc1);
             bool ok = true;
 #pragma unroll
             for (int i = 0; i < NL; ++i) {
@@ -726,7 +753,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
           }
 #pragma unroll
           for (int i = 0; i < NL; ++i) {
-            const int ci = tid + kThreads * i;
+            const int ci = tid + NT * i;
             if (ci < nck) {
               if constexpr (V1) {
                 const int gc = 4 * (ci >> 1) + 2 * (ci & 1);
@@ -799,9 +826,12 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       lds_barrier();
       TSTAMPB(4);
       if (t < 0) {
-        for (int i = tid; i < B * U; i += kThreads) {
+        for (int i = tid; i < B * U; i += NT) {
           const int b = i / U, u = i % U;
-          dh0[(size_t)(b0 + b) * H + j0 + u] = red[0][b][u] + red[1][b][u] + red[2][b][u] + red[3][b][u];
+          float acc = 0.f;
+#pragma unroll
+          for (int w = 0; w < NW; ++w) acc += red[w][b][u];
+          dh0[(size_t)(b0 + b) * H + j0 + u] = acc;
         }
         break;
       }
@@ -810,11 +840,16 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       const int tg = (int)(tagbase | (unsigned)(t + 1));
 #pragma unroll
       for (int i = 0; i < NPAIR; ++i) {
-        const int pi = tid + kThreads * i;
+        const int pi = tid + NT * i;
         if (pi < B * U) {
           const int b = pi / U, u = pi % U;
-          const float rec = k == 0 ? (dhn ? dhn[(size_t)(b0 + b) * H + j0 + u] : 0.f)
-                                   : red[0][b][u] + red[1][b][u] + red[2][b][u] + red[3][b][u];
+          float rec = 0.f;
+          if (k == 0) {
+            rec = dhn ? dhn[(size_t)(b0 + b) * H + j0 + u] : 0.f;
+          } else {
+#pragma unroll
+            for (int w = 0; w < NW; ++w) rec += red[w][b][u];
+          }
           const float ig = gv[i][0], fg = gv[i][1], gg = gv[i][2], og = gv[i][3];
           const float dht = dv[i] + rec;
           const float tc = dca::tanhf_(cv[i]);
@@ -850,11 +885,11 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       // bias gradient of this chain for the owned units: Σ over rows (fixed order) of the per-pair sums
 #pragma unroll
       for (int i = 0; i < NPAIR; ++i) {
-        const int pi = tid + kThreads * i;
+        const int pi = tid + NT * i;
         if (pi < B * U) *reinterpret_cast<dca::f32x4*>(&dbs[pi * 4]) = dsum[i];
       }
       __syncthreads();
-      for (int o = tid; o < U * 4; o += kThreads) {
+      for (int o = tid; o < U * 4; o += NT) {
         float acc = 0.f;
         for (int b = 0; b < B; ++b) acc += dbs[b * U * 4 + o];
         dbpart[(size_t)chain * 4 * H + 4 * j0 + o] = acc;
@@ -866,28 +901,28 @@ __device__ __forceinline__ void lstm_team_bwd_body(
 #undef TSTAMPB
 }
 
-template <int MT, int KS, bool F32, bool V1>
-__global__ __launch_bounds__(kThreads, 1) void lstm_team_fwd_kernel(
+template <int MT, int KS, bool F32, int VAR>
+__global__ __launch_bounds__(VAR == 2 ? 512 : kThreads, 1) void lstm_team_fwd_kernel(
     const float* __restrict__ xp4, const void* __restrict__ whh, const float* __restrict__ h0,
     const float* __restrict__ c0, short* __restrict__ hs, float* __restrict__ hsf, float* __restrict__ cs,
     float* __restrict__ gates4, float* __restrict__ hn, float* __restrict__ cn, unsigned long long* xg_all,
     TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st, unsigned long long* trace,
     int knobs, const float* __restrict__ bias4) {
   __builtin_amdgcn_s_setprio(3);   // issue priority over co-resident waves of kernels overlapped on other streams
-  lstm_team_fwd_body<MT, KS, F32, V1>(xp4, whh, h0, c0, hs, hsf, cs, gates4, hn, cn, xg_all, ctl, err, Btot, Bc, nch, S, sb,
+  lstm_team_fwd_body<MT, KS, F32, VAR>(xp4, whh, h0, c0, hs, hsf, cs, gates4, hn, cn, xg_all, ctl, err, Btot, Bc, nch, S, sb,
                              st, trace, knobs, bias4);
   team_exit(ctl, err, nch);
 }
 
-template <int MT, int KS, bool F32, bool V1>
-__global__ __launch_bounds__(kThreads, 1) void lstm_team_bwd_kernel(
+template <int MT, int KS, bool F32, int VAR>
+__global__ __launch_bounds__(VAR == 2 ? 512 : kThreads, 1) void lstm_team_bwd_kernel(
     const float* __restrict__ dhs, const float* __restrict__ gates4, const float* __restrict__ cs,
     const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
     const void* __restrict__ whh, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
     i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
     unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart, int knobs) {
   __builtin_amdgcn_s_setprio(3);
-  lstm_team_bwd_body<MT, KS, F32, V1>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, dh0, dc0, xg_all, ctl, err, Btot, Bc, nch,
+  lstm_team_bwd_body<MT, KS, F32, VAR>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, dh0, dc0, xg_all, ctl, err, Btot, Bc, nch,
                              S, sb, st, trace, dg16, dbpart, knobs);
   team_exit(ctl, err, nch);
 }
@@ -921,21 +956,25 @@ inline void plan(int B, int& nch, int& Bc, int& MT, int f32 = 0) {
 // (F32_, V1_) = (0, 0) bf16 MFMA, (1, 0) bf16x3 MFMA, (1, 1) exact-fp32 VALU for one-row chains
 #define DCA_TEAM_DISPATCH(MT_, KS_, F32_, V1_, ...)                                                        \
   switch (((V1_) << 12) | ((F32_) << 8) | ((MT_) << 4) | (KS_)) {                                          \
-    case 0x0011: return __VA_ARGS__(1, 1, false, false); case 0x0012: return __VA_ARGS__(1, 2, false, false); \
-    case 0x0014: return __VA_ARGS__(1, 4, false, false); case 0x0021: return __VA_ARGS__(2, 1, false, false); \
-    case 0x0022: return __VA_ARGS__(2, 2, false, false); case 0x0024: return __VA_ARGS__(2, 4, false, false); \
-    case 0x0111: return __VA_ARGS__(1, 1, true, false);  case 0x0112: return __VA_ARGS__(1, 2, true, false);  \
-    case 0x0114: return __VA_ARGS__(1, 4, true, false);                                                      \
-    case 0x1111: return __VA_ARGS__(1, 1, true, true);   case 0x1112: return __VA_ARGS__(1, 2, true, true);   \
-    case 0x1114: return __VA_ARGS__(1, 4, true, true);                                                       \
+    case 0x0011: return __VA_ARGS__(1, 1, false, 0); case 0x0012: return __VA_ARGS__(1, 2, false, 0); \
+    case 0x0014: return __VA_ARGS__(1, 4, false, 0); case 0x0021: return __VA_ARGS__(2, 1, false, 0); \
+    case 0x0022: return __VA_ARGS__(2, 2, false, 0); case 0x0024: return __VA_ARGS__(2, 4, false, 0); \
+    case 0x0111: return __VA_ARGS__(1, 1, true, 0);  case 0x0112: return __VA_ARGS__(1, 2, true, 0);  \
+    case 0x0114: return __VA_ARGS__(1, 4, true, 0);                                                      \
+    case 0x1111: return __VA_ARGS__(1, 1, true, 1);      case 0x1112: return __VA_ARGS__(1, 2, true, 1);      \
+    case 0x1114: return __VA_ARGS__(1, 4, true, 1);      case 0x2114: return __VA_ARGS__(1, 4, true, 2);      \
     default: return hipErrorInvalidValue;                                                                    \
   }
 
-// one-row fp32 chains take the exact VALU variant (DCA_TEAM_V1=0 forces the bf16x3 MFMA one, for comparison)
-inline int use_v1(int f32, int Bc) {
+// one-row fp32 chains take the exact VALU variant (DCA_TEAM_V1=0 forces the bf16x3 MFMA one, for comparison); at
+// H = 512 its 8-wave form V2 unless DCA_TEAM_V2=0
+inline int use_v1(int f32, int Bc, int H) {
   static const int off = [] { const char* e = getenv("DCA_TEAM_V1"); return e && e[0] == '0'; }();
-  return (f32 && Bc == 1 && !off) ? 1 : 0;
+  static const int v2off = [] { const char* e = getenv("DCA_TEAM_V2"); return e && e[0] == '0'; }();
+  if (!(f32 && Bc == 1 && !off)) return 0;
+  return (H == 512 && !v2off) ? 2 : 1;
 }
+inline int team_threads(int var) { return var == 2 ? 512 : kThreads; }
 
 // Workspace bytes (control block + per-team exchange buffers) for a launch of (B, H).
 extern "C" size_t dca_lstm_team_ctl_bytes() { return 256; }
@@ -972,11 +1011,11 @@ extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const void* whh, const
   unsigned long long* xg = reinterpret_cast<unsigned long long*>(ws);
   const int KS = H / 128;
 #define DCA_F(mt, ks, f, v)                                                                                     \
-  (lstm_team_fwd_kernel<mt, ks, f, v><<<kMaxTeams * kT, kThreads, 0, stream>>>(xp4, whh, h0, c0, hs, hsf, cs, gates4, \
+  (lstm_team_fwd_kernel<mt, ks, f, v><<<kMaxTeams * kT, team_threads(v), 0, stream>>>(xp4, whh, h0, c0, hs, hsf, cs, gates4, \
                                                                           hn, cn, xg, ctl, err, B, Bc, nch, S, sb, \
                                                                           st, trace, team_knobs(), bias4),         \
    hipGetLastError())
-  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc), DCA_F)
+  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc, H), DCA_F)
 #undef DCA_F
 }
 
@@ -996,11 +1035,11 @@ extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, c
   i32x4* xb = reinterpret_cast<i32x4*>(ws);
   const int KS = H / 128;
 #define DCA_B(mt, ks, f, v)                                                                                        \
-  (lstm_team_bwd_kernel<mt, ks, f, v><<<kMaxTeams * kT, kThreads, 0, stream>>>(dhs, gates4, cs, c0, dhn, dcn, whh,      \
+  (lstm_team_bwd_kernel<mt, ks, f, v><<<kMaxTeams * kT, team_threads(v), 0, stream>>>(dhs, gates4, cs, c0, dhn, dcn, whh,      \
                                                                           dgates4, dh0, dc0, xb, ctl, err, B, Bc,  \
                                                                           nch, S, sb, st, trace, dg16, dbpart,      \
                                                                           team_knobs()),                           \
    hipGetLastError())
-  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc), DCA_B)
+  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc, H), DCA_B)
 #undef DCA_B
 }
