@@ -100,6 +100,9 @@ class WeightImages:
                    # (in, 4H) copy for ∂pre = ∂G·W_ih: hipBLASLt is 1.7x faster with this operand K-contiguous
                    # (85 vs 141 µs at 11200×2048×256, fast fp32)
                    'wihT16': idx('rnn.weight_ih_l0')[perm].t().contiguous()}
+        if getattr(fp, 'fp32', False):
+            # (out, in)-transposed pre-RNN weight: the fused ∂X chain's second operand, K-contiguous per column
+            parts16['wpreT'] = idx('affine_pre_rnn.weight').t().contiguous()
         head_b = [idx('affine_unit_attention.bias'), idx('affine_head_enum.bias'), idx('affine_move_x.bias'),
                   idx('affine_move_y.bias'), idx('affine_value.bias') if with_value else neg(1)]
         bcat = torch.cat(head_b + [neg(LDZ - 150)])
@@ -167,6 +170,9 @@ _F32_GEMM_FAST = os.environ.get('DCA_F32_GEMM', 'fast') != 'exact'
 # weight-gradient GEMMs of the recurrence and pre-RNN layer on the (then idle) recurrence stream, overlapped with the
 # ∂X chain of the main stream (DCA_WG_OVERLAP=0: everything on the main stream)
 _WG_OVERLAP = os.environ.get('DCA_WG_OVERLAP', '1') != '0'
+# fp32 learner: the ∂X chain ∂pre = (∂G·W_ih)⊙[x>0], ∂x896 = ∂pre·W_pre as ONE hand-written MFMA kernel
+# (ops/csrc/dx_chain.hip) instead of two hipBLASLt GEMMs + a threshold_backward (DCA_DX_FUSED=0: the library path)
+_DX_FUSED = os.environ.get('DCA_DX_FUSED', '1') != '0'
 
 
 def fused_step_tm(fp, *args, **kw):
@@ -362,8 +368,13 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             else:       # h_{t-1} rows: h0 for t = 0, then hs[0 : t1-1] — no concatenation materialised
                 gemm_tn(dG16, hs16[0:t1 - 1].view(n - B, H), out=dWhh, perm=gperm, accumulate=True, b0=h016)
             gemm_tn(dG16, x16[r0:r1], out=dWih, perm=gperm, accumulate=True)
-        # ∂pre-activation of the pre-RNN layer: one GEMM (bf16 or exact f32), ReLU mask in one threshold_backward
-        dpre16 = torch.ops.aten.threshold_backward(torch.mm(dG16, W['wihT16'].t()), x16[r0:r1], 0)
+        fused_dx = f32 and _DX_FUSED and 'wpreT' in W
+        if fused_dx:
+            # ∂pre = (∂G·W_ih)⊙[x16 > 0] and ∂x896 = ∂pre·W_pre in one launch (the ∂pre tile stays in LDS)
+            dpre16, dx896 = C.dpre_dx(dG16, W['wihT16'], x16[r0:r1], W['wpreT'], exact=not _F32_GEMM_FAST)
+        else:
+            # ∂pre-activation of the pre-RNN layer: one GEMM (bf16 or exact f32), ReLU mask in one threshold_backward
+            dpre16 = torch.ops.aten.threshold_backward(torch.mm(dG16, W['wihT16'].t()), x16[r0:r1], 0)
         if wg_side:
             sL.wait_stream(main)
             with torch.cuda.stream(sL):
@@ -372,7 +383,8 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
                 wg_done.record(sL)
         else:
             gemm_tn(dpre16, x896[r0:r1], out=dWpre, accumulate=True, colsum=dbpre)
-        dx896 = _mm(dpre16, wpre16)
+        if not fused_dx:
+            dx896 = _mm(dpre16, wpre16)
         if split is not None:
             if wg_done is not None:
                 main.wait_event(wg_done)

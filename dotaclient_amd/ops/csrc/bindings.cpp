@@ -578,6 +578,27 @@ std::vector<torch::Tensor> enc_small_grads(torch::Tensor z, torch::Tensor dtl, t
   return {out.narrow(0, 0, 768).view({6, 128}), out.narrow(0, 768, 384).view({128, 3}), out.narrow(0, 1152, 128)};
 }
 
+// Fused ∂X chain of the fp32 pre-RNN layer (ops/csrc/dx_chain.hip): dpre = (dG · W_ih) ⊙ [x > 0], dx = dpre · W_pre.
+// dG (N, K1) f32, wihT (256, K1) f32 (K-contiguous image of W_ih, gate rows in dG's column order), x (N, 256) f32
+// ReLU outputs, wpreT (X, 256) f32. Returns (dpre (N, 256), dx (N, X)). exact: exact-f32 MFMA instead of bf16x3.
+std::vector<torch::Tensor> dpre_dx(torch::Tensor dG, torch::Tensor wihT, torch::Tensor x, torch::Tensor wpreT,
+                                   bool exact) {
+  CHECK_F32(dG); CHECK_F32(wihT); CHECK_F32(x); CHECK_F32(wpreT);
+  const int N = dG.size(0), K1 = dG.size(1), X = wpreT.size(0);
+  TORCH_CHECK(dG.dim() == 2 && wihT.dim() == 2 && x.dim() == 2 && wpreT.dim() == 2, "dpre_dx: 2-D operands");
+  TORCH_CHECK(wihT.size(0) == 256 && wihT.size(1) == K1 && x.size(0) == N && x.size(1) == 256 &&
+              wpreT.size(1) == 256, "dpre_dx: shapes (N,K1) (256,K1) (N,256) (X,256)");
+  TORCH_CHECK(K1 % 32 == 0 && X % 128 == 0, "dpre_dx: K1 % 32 == 0 and X % 128 == 0");
+  TORCH_CHECK((long long)N * K1 * 4 <= 0x7fff0000LL, "dpre_dx: dG too large for one launch");
+  auto o = dG.options();
+  auto dpre = torch::empty({N, 256}, o);
+  auto dx = torch::empty({N, X}, o);
+  hip_check(dca_dpre_dx(ptr<float>(dG), ptr<float>(wihT), ptr<float>(x), ptr<float>(wpreT), ptr<float>(dpre),
+                        ptr<float>(dx), N, K1, X, exact ? 1 : 0, cur_stream()),
+            "dca_dpre_dx");
+  return {dpre, dx};
+}
+
 // ---- 5v5 entity-attention block (ops/csrc/attn.hip); 64 unit slots, width 128, 4 heads × 32 -------------------
 std::vector<torch::Tensor> ln_fwd(torch::Tensor e0, torch::Tensor bsub, torch::Tensor gamma, torch::Tensor beta,
                                   double eps, c10::optional<torch::Tensor> e0_copy) {
@@ -806,6 +827,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_tn", &gemm_tn, "C (+)= A^T B for K-outer bf16 or fp32 (bf16x3) operands (split-K MFMA, LDS transposed reads)",
         py::arg("A"), py::arg("B"), py::arg("C"), py::arg("perm") = py::none(), py::arg("accumulate") = false,
         py::arg("B0") = py::none(), py::arg("colsum") = py::none());
+  m.def("dpre_dx", &dpre_dx, "fused pre-RNN dX chain: (dG·W_ih)*[x>0] -> dpre, dpre·W_pre -> dx (bf16x3 or exact MFMA)",
+        py::arg("dG"), py::arg("wihT"), py::arg("x"), py::arg("wpreT"), py::arg("exact") = false);
   m.def("enc_small_grads", &enc_small_grads, "entity-encoder type-bias and env-layer gradients in one pass");
   m.def("ln_fwd", &ln_fwd, "LayerNorm(E0 - bsub) -> (xn, mean, rstd); bf16, or fp32 (bsub may be empty); optional copy of E0",
         py::arg("e0"), py::arg("bsub"), py::arg("gamma"), py::arg("beta"), py::arg("eps"),

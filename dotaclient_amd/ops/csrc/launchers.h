@@ -5,6 +5,10 @@
 
 extern "C" {
 
+size_t dca_dpre_dx_lds(int exact);
+hipError_t dca_dpre_dx(const float* dG, const float* wihT, const float* x, const float* wpreT, float* dpre, float* dx,
+                       int N, int K1, int X, int exact, hipStream_t stream);
+
 hipError_t dca_adam_step(float* param, const float* grad, float* m, float* v, const int* seg, int64_t n,
                          const float* counts, float* steps, int n_params, float* partials, float* norm_out, float lr,
                          float b1, float b2, float eps, float max_norm, hipStream_t st, int divide, int64_t header,

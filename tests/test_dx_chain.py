@@ -1,0 +1,28 @@
+"""Fused pre-RNN ∂X chain (ops/csrc/dx_chain.hip) vs a float64 torch reference of the same two products + ReLU mask:
+dpre = (dG·W_ih)⊙[x>0], dx = dpre·W_pre. bf16x3 mode at the fp32 learner's accuracy class, exact mode at fp32
+rounding. Shapes: the deploy step (N = 8·1400, 4H = 2048, 256, 896) and a ragged row count."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize('N', [11200, 1000])
+@pytest.mark.parametrize('exact', [False, True])
+def test_dpre_dx_matches_fp64(gpu_ops, N, exact):
+    g = torch.Generator(device='cuda').manual_seed(N)
+    K1, P, X = 2048, 256, 896
+    dG = torch.randn(N, K1, device='cuda', generator=g) * 1e-3
+    wihT = torch.randn(P, K1, device='cuda', generator=g) * 0.05
+    x = torch.relu(torch.randn(N, P, device='cuda', generator=g))
+    wpreT = torch.randn(X, P, device='cuda', generator=g) * 0.05
+    for _ in range(2):
+        dpre, dx = gpu_ops.dpre_dx(dG, wihT, x, wpreT, exact)
+        torch.cuda.synchronize()
+    ref_pre = (dG.double() @ wihT.double().t()) * (x > 0)
+    ref_dx = ref_pre @ wpreT.double()
+    tol = 2e-6 if exact else 3e-5
+    for got, ref in ((dpre, ref_pre), (dx, ref_dx)):
+        err = (got.double() - ref).abs().max() / ref.abs().max()
+        assert err < tol, (float(err), exact)
+    assert torch.equal(dpre == 0, ref_pre == 0) or exact is False
