@@ -588,7 +588,7 @@ std::vector<torch::Tensor> dpre_dx(torch::Tensor dG, torch::Tensor wihT, torch::
   TORCH_CHECK(dG.dim() == 2 && wihT.dim() == 2 && x.dim() == 2 && wpreT.dim() == 2, "dpre_dx: 2-D operands");
   TORCH_CHECK(wihT.size(0) == 256 && wihT.size(1) == K1 && x.size(0) == N && x.size(1) == 256 &&
               wpreT.size(1) == 256, "dpre_dx: shapes (N,K1) (256,K1) (N,256) (X,256)");
-  TORCH_CHECK(K1 % 32 == 0 && X % 128 == 0, "dpre_dx: K1 % 32 == 0 and X % 128 == 0");
+  TORCH_CHECK(K1 % 128 == 0 && X % 128 == 0, "dpre_dx: K1 % 128 == 0 and X % 128 == 0");
   TORCH_CHECK((long long)N * K1 * 4 <= 0x7fff0000LL, "dpre_dx: dG too large for one launch");
   auto o = dG.options();
   auto dpre = torch::empty({N, 256}, o);

@@ -30,7 +30,7 @@ namespace {
 using dca::bf16x8;
 using dca::f32x4;
 
-constexpr int BM = 64, BK = 32, NT = 512, P = 256, XC = 128;
+constexpr int BM = 64, BK = 32, NT = 512, P = 256, XC = 128, RD = 4;
 
 template <bool EXACT>
 struct Lay {
@@ -129,18 +129,21 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
   const int arow = r0 + ar;
   const int a_off0 = arow < N ? (arow * K1 + ak) * 4 : kOob;
   const int b_off0 = (bc * K1 + bk) * 4;
-  float4 sa, sb[4];
-  auto load1 = [&](int k0) {
-    sa = ld4(rA, a_off0 == kOob ? kOob : a_off0 + k0 * 4);
+  // register ring of RD slabs in flight: the slab stored into LDS at iteration ks was loaded at ks + 1 - RD, so
+  // RD - 1 slabs of MFMA work cover each load's latency (one slab of lead was 4x slower: every store waited out a
+  // full memory round trip)
+  float4 sa[RD], sb[RD][4];
+  auto load1 = [&](int slot, int k0) {
+    sa[slot] = ld4(rA, a_off0 == kOob ? kOob : a_off0 + k0 * 4);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sb[i] = ld4(rW1, b_off0 + (k0 + 4 * i) * 4);
+    for (int i = 0; i < 4; ++i) sb[slot][i] = ld4(rW1, b_off0 + (k0 + 4 * i) * 4);
   };
-  auto store1 = [&](int buf) {
+  auto store1 = [&](int slot, int buf) {
     char* base = lds + buf * L::S1;
-    put4<EXACT>(base, L::A1, ar, ak, sa);
+    put4<EXACT>(base, L::A1, ar, ak, sa[slot]);
     char* bb = base + L::IMG * L::A1;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) put4<EXACT>(bb, L::B1, bc, bk + 4 * i, sb[i]);
+    for (int i = 0; i < 4; ++i) put4<EXACT>(bb, L::B1, bc, bk + 4 * i, sb[slot][i]);
   };
   const int wr = w >> 2, wc = w & 3;             // 2 × 4 waves: rows 32·wr, cols 64·wc
   f32x4 acc[2][4];
@@ -148,25 +151,30 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nk = K1 / BK;
-  load1(0);
-  store1(0);
+  const int nk = K1 / BK;                         // multiple of RD (host check)
+#pragma unroll
+  for (int d = 0; d < RD; ++d) load1(d, d * BK);
+  store1(0, 0);
   __syncthreads();
-  for (int ks = 0; ks < nk; ++ks) {
-    if (ks + 1 < nk) load1((ks + 1) * BK);
-    const char* base = lds + (ks & 1) * L::S1;
-    const char* bb = base + L::IMG * L::A1;
-    Frag fa[2], fb[4];
+  for (int ks0 = 0; ks0 < nk; ks0 += RD) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) get_frag<EXACT>(base, L::A1, (wr * 32 + i * 16 + r16) * L::RP, q, fa[i]);
+    for (int d = 0; d < RD; ++d) {
+      const int ks = ks0 + d;
+      const char* base = lds + (d & 1) * L::S1;   // (RD even: slab ks sits in buffer ks & 1 = d & 1)
+      const char* bb = base + L::IMG * L::A1;
+      Frag fa[2], fb[4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) get_frag<EXACT>(bb, L::B1, (wc * 64 + j * 16 + r16) * L::RP, q, fb[j]);
+      for (int i = 0; i < 2; ++i) get_frag<EXACT>(base, L::A1, (wr * 32 + i * 16 + r16) * L::RP, q, fa[i]);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int j = 0; j < 4; ++j) get_frag<EXACT>(bb, L::B1, (wc * 64 + j * 16 + r16) * L::RP, q, fb[j]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = mma<EXACT>(fa[i], fb[j], acc[i][j]);
-    if (ks + 1 < nk) store1((ks + 1) & 1);
-    __syncthreads();
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = mma<EXACT>(fa[i], fb[j], acc[i][j]);
+      if (ks + 1 < nk) store1((d + 1) % RD, (d + 1) & 1);
+      if (ks + RD < nk) load1(d, (ks + RD) * BK);  // slot d held slab ks, stored at the previous iteration
+      __syncthreads();
+    }
   }
 
   // ================= ReLU mask, dpre → HBM and → LDS (stage-2 A operand) =================
@@ -198,53 +206,59 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
   // staging map: B slab 128 cols × 32 k = 1024 float4 (two per thread: col t/4, k 8·(t%4) + 4·i)
   char* s2 = lds + L::D;
   const int cc = tid >> 2, ck = (tid & 3) * 8;
-  float4 sw[2];
-  auto load2 = [&](int c0, int k0) {
+  constexpr int nk2 = P / BK;
+  float4 sw[RD][2];
+  auto load2 = [&](int slot, int it) {
+    const int c0 = (it / nk2) * XC, k0 = (it % nk2) * BK;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) sw[i] = ld4(rW2, ((c0 + cc) * P + k0 + ck + 4 * i) * 4);
+    for (int i = 0; i < 2; ++i) sw[slot][i] = ld4(rW2, ((c0 + cc) * P + k0 + ck + 4 * i) * 4);
   };
-  auto store2 = [&](int buf) {
+  auto store2 = [&](int slot, int buf) {
     char* bb = s2 + buf * L::S2;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) put4<EXACT>(bb, L::B2, cc, ck + 4 * i, sw[i]);
+    for (int i = 0; i < 2; ++i) put4<EXACT>(bb, L::B2, cc, ck + 4 * i, sw[slot][i]);
   };
   const int vr = w >> 1, vc = w & 1;             // 4 × 2 waves: rows 16·vr, cols 64·vc of the chunk
-  constexpr int nk2 = P / BK;
-  const int nchunk = X / XC, total = nchunk * nk2;
+  const int nchunk = X / XC, total = nchunk * nk2;   // multiple of RD (nk2 = 8)
   f32x4 acc2[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  load2(0, 0);
-  store2(0);
+#pragma unroll
+  for (int d = 0; d < RD; ++d) load2(d, d);
+  store2(0, 0);
   __syncthreads();                                // dpre tile and the first W_pre slab are in LDS
-  for (int it = 0; it < total; ++it) {
-    const int chunk = it / nk2, ks = it % nk2;
-    if (it + 1 < total) load2(((it + 1) / nk2) * XC, ((it + 1) % nk2) * BK);
-    const char* bb = s2 + (it & 1) * L::S2;
-    Frag fa, fb[4];
-    // A fragment: dpre row 16·vr + r16, k = 32·ks + 8·q … (the dpre image holds the full K = P per row)
-    if constexpr (EXACT) {
-      get_frag<true>(dimg, 0, (vr * 16 + r16) * L::DP + ks * BK * 4, q, fa);
-    } else {
-      get_frag<false>(dimg, BM * L::DP, (vr * 16 + r16) * L::DP + ks * BK * 2, q, fa);
-    }
+  for (int it0 = 0; it0 < total; it0 += RD) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) get_frag<EXACT>(bb, L::B2, (vc * 64 + j * 16 + r16) * L::RP, q, fb[j]);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc2[j] = mma<EXACT>(fa, fb[j], acc2[j]);
-    if (it + 1 < total) store2((it + 1) & 1);
-    if (ks == nk2 - 1) {                          // chunk done: store its 64 × 128 output tile
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int grow = r0 + vr * 16 + 4 * q + e;
-          if (grow < N) dx[(size_t)grow * X + chunk * XC + vc * 64 + j * 16 + r16] = acc2[j][e];
-        }
-        acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int d = 0; d < RD; ++d) {
+      const int it = it0 + d;
+      const int chunk = it / nk2, ks = it % nk2;
+      const char* bb = s2 + (d & 1) * L::S2;
+      Frag fa, fb[4];
+      // A fragment: dpre row 16·vr + r16, k = 32·ks + 8·q … (the dpre image holds the full K = P per row)
+      if constexpr (EXACT) {
+        get_frag<true>(dimg, 0, (vr * 16 + r16) * L::DP + ks * BK * 4, q, fa);
+      } else {
+        get_frag<false>(dimg, BM * L::DP, (vr * 16 + r16) * L::DP + ks * BK * 2, q, fa);
       }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) get_frag<EXACT>(bb, L::B2, (vc * 64 + j * 16 + r16) * L::RP, q, fb[j]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc2[j] = mma<EXACT>(fa, fb[j], acc2[j]);
+      if (it + 1 < total) store2((d + 1) % RD, (d + 1) & 1);
+      if (it + RD < total) load2(d, it + RD);
+      if (ks == nk2 - 1) {                        // chunk done: store its 64 × 128 output tile
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int grow = r0 + vr * 16 + 4 * q + e;
+            if (grow < N) dx[(size_t)grow * X + chunk * XC + vc * 64 + j * 16 + r16] = acc2[j][e];
+          }
+          acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      }
+      __syncthreads();
     }
-    __syncthreads();
   }
 }
 
@@ -256,7 +270,8 @@ extern "C" size_t dca_dpre_dx_lds(int exact) { return exact ? Lay<true>::BYTES :
 // wpreT (X, P) f32; outputs dpre (N, P), dx (N, X) f32. K1 % 32 == 0, X % 128 == 0.
 extern "C" hipError_t dca_dpre_dx(const float* dG, const float* wihT, const float* x, const float* wpreT, float* dpre,
                                   float* dx, int N, int K1, int X, int exact, hipStream_t stream) {
-  if (N < 1 || K1 < 32 || K1 % BK != 0 || X < XC || X % XC != 0) return hipErrorInvalidValue;
+  if (N < 1 || K1 < RD * BK || K1 % (RD * BK) != 0 || X < XC || X % XC != 0 || ((X / XC) * (P / BK)) % RD != 0)
+    return hipErrorInvalidValue;
   if ((long long)N * K1 * 4 > 0x7fff0000LL) return hipErrorInvalidValue;      // buffer-resource range
   const int grid = (N + BM - 1) / BM;
   if (exact) {

@@ -967,12 +967,13 @@ inline void plan(int B, int& nch, int& Bc, int& MT, int f32 = 0) {
   }
 
 // one-row fp32 chains take the exact VALU variant (DCA_TEAM_V1=0 forces the bf16x3 MFMA one, for comparison); at
-// H = 512 its 8-wave form V2 unless DCA_TEAM_V2=0
-inline int use_v1(int f32, int Bc, int H) {
+// H = 512 the backward takes its 8-wave form V2 (measured B=8, S=1400: backward 2069 vs 2137 µs, while the 8-wave
+// forward was SLOWER, 2056 vs 1778 µs). DCA_TEAM_V2 = 0 (neither), 1 (both directions), default: backward only.
+inline int use_v1(int f32, int Bc, int H, int backward) {
   static const int off = [] { const char* e = getenv("DCA_TEAM_V1"); return e && e[0] == '0'; }();
-  static const int v2off = [] { const char* e = getenv("DCA_TEAM_V2"); return e && e[0] == '0'; }();
+  static const int v2 = [] { const char* e = getenv("DCA_TEAM_V2"); return e ? (e[0] == '0' ? 0 : 3) : 2; }();
   if (!(f32 && Bc == 1 && !off)) return 0;
-  return (H == 512 && !v2off) ? 2 : 1;
+  return (H == 512 && (v2 & (backward ? 2 : 1))) ? 2 : 1;
 }
 inline int team_threads(int var) { return var == 2 ? 512 : kThreads; }
 
@@ -1015,7 +1016,7 @@ extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const void* whh, const
                                                                           hn, cn, xg, ctl, err, B, Bc, nch, S, sb, \
                                                                           st, trace, team_knobs(), bias4),         \
    hipGetLastError())
-  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc, H), DCA_F)
+  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc, H, 0), DCA_F)
 #undef DCA_F
 }
 
@@ -1040,6 +1041,6 @@ extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, c
                                                                           nch, S, sb, st, trace, dg16, dbpart,      \
                                                                           team_knobs()),                           \
    hipGetLastError())
-  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc, H), DCA_B)
+  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc, H, 1), DCA_B)
 #undef DCA_B
 }
