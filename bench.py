@@ -59,6 +59,8 @@ def parse():
                     help='fp32 = the reference\'s training precision (headline); bf16 = bf16 GEMM operands')
     ap.add_argument('--bf16-extra', type=int, default=1,
                     help='also time the bf16 learner (reported as an extra field, not the headline)')
+    ap.add_argument('--exact-extra', type=int, default=1,
+                    help='also time the fp32-exact learner (IEEE fp32 products, no bf16x3 split; extra field)')
     ap.add_argument('--replay', type=int, default=0, help='sequences in the on-HBM replay pool (0 = 4x batch)')
     ap.add_argument('--graph', type=int, default=-1, help='capture the step in a hipGraph (-1 = auto)')
     ap.add_argument('--actor', type=int, default=1, help='also measure actor steps/s (untimed region)')
@@ -177,6 +179,16 @@ def main():
         e16, _, _, _, _ = run('bf16')
         progress(f'learner bf16 done: {e16 / args.steps * 1e3:.3f} ms/step')
         extra = {'precision': 'bf16', 'value': samples / e16, 'ms_per_step': e16 / args.steps * 1e3}
+    exact = None
+    if args.exact_extra and args.precision == 'fp32' and use_cuda and not cfg.entity_attention:
+        learner = None
+        try:
+            ex, lx0, lx1, _, _ = run('fp32-exact')
+            progress(f'learner fp32-exact done: {ex / args.steps * 1e3:.3f} ms/step')
+            exact = {'precision': 'fp32-exact (IEEE fp32 products: exact-f32 MFMA / VALU / hipBLASLt)',
+                     'value': samples / ex, 'ms_per_step': ex / args.steps * 1e3, 'loss_first': lx0, 'loss_last': lx1}
+        except Exception as e:
+            exact = {'error': repr(e)}
 
     def gather(x):
         """Every rank's value of ``x`` on every rank (rank order)."""
@@ -269,9 +281,10 @@ def main():
             'vs_baseline_e2e': (e2e['steps_per_s'] / BASELINE_STEPS_PER_S
                                 if e2e and 'steps_per_s' in e2e else None),
             'dtype': 'fp32 (bf16x3 MFMA operands)' if args.precision == 'fp32' else args.precision,
-            'precision_note': ('fp32 activations, gradients, accumulation and optimizer; hand-written MFMA kernels '
-                               'use bf16x3 split operands (x = hi + lo, ~2^-16 relative per product), plain GEMMs on '
-                               "hipBLASLt's fast fp32 mode (same bf16x3 accuracy class; DCA_F32_GEMM=exact for exact)") if args.precision == 'fp32' else
+            'precision_note': ('fp32 activations, gradients, accumulation and optimizer; GEMM operands bf16x3-split '
+                               '(x = hi + lo, ~2^-16 relative per product) in the hand-written MFMA kernels and '
+                               "hipBLASLt's fast fp32 mode; the LSTM recurrence and heads/loss are exact fp32 VALU. "
+                               'exact_fp32_learner = the same step with IEEE fp32 products everywhere') if args.precision == 'fp32' else
                               'bf16 GEMM operands and saved activations, fp32 accumulation / recurrence / optimizer',
             'data': 'synthetic (on-HBM replay of synthetic 1v1-mid experience, random-init weights)',
             'config': {'model': f'{args.model} ({cfg.rnn}-{cfg.hidden}, '
@@ -281,6 +294,7 @@ def main():
                        'parallelism': f'dp{world}', 'algo': args.algo, 'backend': backend, 'step': step_mode},
             'loss_first': loss_val, 'loss_last': final_loss,
             'bf16_learner': extra,
+            'exact_fp32_learner': exact,
             'dp_replicas_identical': len(set(shas)) == 1,
             'weights_sha16_per_rank': shas,
             'actor': actor,

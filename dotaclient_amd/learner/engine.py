@@ -49,8 +49,8 @@ class LossConfig:
 class Learner:
     def __init__(self, policy: Policy, loss_cfg: LossConfig, device='cpu', backend: str = 'auto',
                  bucket_cap_mb: float = 8.0, overlap: bool = True, dp: bool = True, precision: str = 'fp32'):
-        if precision not in ('fp32', 'bf16'):
-            raise ValueError(f'precision must be fp32 or bf16, got {precision!r}')
+        if precision not in ('fp32', 'bf16', 'fp32-exact'):
+            raise ValueError(f'precision must be fp32, fp32-exact or bf16, got {precision!r}')
         self.device = torch.device(device)
         self.cfg = loss_cfg
         self.precision = precision

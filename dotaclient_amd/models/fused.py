@@ -241,14 +241,20 @@ class _PolicyLoss(torch.autograd.Function):
 class FusedPolicy:
     def __init__(self, policy: Policy, loss_cfg=None, precision: str = 'fp32'):
         from .. import ops
-        if precision not in ('fp32', 'bf16'):
-            raise ValueError(f'precision must be fp32 or bf16, got {precision!r}')
+        if precision not in ('fp32', 'bf16', 'fp32-exact'):
+            raise ValueError(f'precision must be fp32, fp32-exact or bf16, got {precision!r}')
         self.C = ops.require()
         self.policy = policy
         self.cfg = policy.config
         self.loss_cfg = loss_cfg
         self.precision = precision
-        self.fp32 = precision == 'fp32'
+        self.fp32 = precision in ('fp32', 'fp32-exact')
+        # 'fp32-exact': IEEE fp32 products everywhere (no bf16x3 split): hipBLASLt's exact-f32 GEMMs, the exact-f32
+        # MFMA template of the fused ∂X kernel, the exact VALU recurrence and heads/loss kernels, and the encoder /
+        # weight-gradient products as exact-f32 torch ops (models/pipelined.py) — the accuracy reference mode
+        self.exact = precision == 'fp32-exact'
+        if self.exact and policy.config.entity_attention:
+            raise ValueError('fp32-exact covers the 1v1 policies (the entity-attention kernels are bf16x3 only)')
         dev = next(policy.parameters()).device
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.param_names: List[str] = [n for n, _ in policy.named_parameters()]

@@ -176,14 +176,95 @@ _DX_FUSED = os.environ.get('DCA_DX_FUSED', '1') != '0'
 
 
 def fused_step_tm(fp, *args, **kw):
-    if not (_F32_GEMM_FAST and getattr(fp, 'fp32', False)):
+    exact = getattr(fp, 'exact', False)
+    if not (getattr(fp, 'fp32', False) and (exact or _F32_GEMM_FAST)):
         return _fused_step_tm(fp, *args, **kw)
     prev = torch.backends.cuda.matmul.allow_tf32
-    torch.backends.cuda.matmul.allow_tf32 = True
+    torch.backends.cuda.matmul.allow_tf32 = not exact
     try:
         return _fused_step_tm(fp, *args, **kw)
     finally:
         torch.backends.cuda.matmul.allow_tf32 = prev
+
+
+def _gemm_tn_exact(a, b, out=None, perm=None, accumulate=False, b0=None, colsum=None):
+    """``ops.gemm.gemm_tn`` semantics (C (+)= Aᵀ·B through row map ``perm``, optional B0 rows, optional column sums
+    of A) as exact-f32 hipBLASLt products: the fp32-exact learner's weight gradients."""
+    if b0 is not None:
+        b = torch.cat([b0, b])
+    c = a.t() @ b
+    cs = a.sum(0) if colsum is not None else None
+    if perm is not None:
+        idx = perm.long()
+        if out is None:
+            out = torch.zeros(int(perm.numel()), c.shape[1], device=c.device)
+        (out.index_add_ if accumulate else out.index_copy_)(0, idx, c)
+    elif out is None:
+        out = c
+    elif accumulate:
+        out.add_(c)
+    else:
+        out.copy_(c)
+    if cs is not None:
+        colsum.copy_(cs)
+    return out
+
+
+def _encoder_exact(fp, P, units_t, env_t):
+    """The entity encoder (policy.py:97-132 / Policy.encode up to the pre-RNN layer) as exact-f32 torch ops — plain
+    ops, no autograd graph, so the step stays capturable in a hipGraph; pools remember their argmax unit (torch
+    ``max``, the reference's op) for :func:`_encoder_exact_bwd`. Returns x896 (N, 896), emb (N, U, 128), saved."""
+    from ..constants import UNIT_KEYS
+    cfg = fp.cfg
+    sl = cfg.layout.slices()
+    g = lambda n: P[n].detach()    # noqa: E731
+    N, U = units_t.shape[:2]
+    env_e = torch.relu(torch.addmm(g('affine_env.bias'), env_t, g('affine_env.weight').t()))
+    basic = torch.relu(torch.addmm(g('affine_unit_basic_stats.bias'), units_t.reshape(N * U, 10),
+                                   g('affine_unit_basic_stats.weight').t())).view(N, U, -1)
+    emb = torch.empty(N, U, cfg.unit_dim, device=units_t.device, dtype=units_t.dtype)
+    for key, s_ in zip(UNIT_KEYS, TYPE_SUFFIX):
+        a = sl[key]
+        n_u = a.stop - a.start
+        emb[:, a] = torch.addmm(g(f'affine_unit_{s_}.bias'), basic[:, a].reshape(N * n_u, -1),
+                                g(f'affine_unit_{s_}.weight').t()).view(N, n_u, -1)
+    pools, idx = [], []
+    for key in UNIT_KEYS:
+        k = 'enemy_nonheroes' if (cfg.compat_bugs and key == 'enemy_towers') else key
+        m = emb[:, sl[k]].max(dim=1)
+        pools.append(m.values)
+        idx.append((sl[k].start, m.indices))
+    x896 = torch.cat([env_e] + pools, 1)
+    return x896, emb, (env_e, basic, emb, idx, units_t, env_t)
+
+
+def _encoder_exact_bwd(fp, P, saved, dx896, dtl, z):
+    """Encoder parameter gradients (exact-f32 torch ops) from ∂x896 and the pointer head's ∂emb = dtl ⊗ q
+    (q = z[:, :128]); each pooled column routes its gradient to its argmax unit. Returns (dWt (6,128,128),
+    dw1, db1, (dbt (6,128), dWe, dbe))."""
+    from ..constants import UNIT_KEYS
+    env_e, basic, emb, idx, units_t, env_t = saved
+    cfg = fp.cfg
+    sl = cfg.layout.slices()
+    D = emb.shape[2]
+    N, U = units_t.shape[:2]
+    demb = dtl.unsqueeze(2) * z[:, None, :D]
+    for t, (start, ind) in enumerate(idx):
+        dpool = dx896[:, 128 + D * t:128 + D * (t + 1)]
+        demb.scatter_add_(1, (ind + start).unsqueeze(1), dpool.unsqueeze(1))
+    dWt, dbt, dbasic = [], [], torch.empty_like(basic)
+    for key, s_ in zip(UNIT_KEYS, TYPE_SUFFIX):
+        a = sl[key]
+        n_u = a.stop - a.start
+        de = demb[:, a].reshape(N * n_u, D)
+        dWt.append(de.t() @ basic[:, a].reshape(N * n_u, -1))
+        dbt.append(de.sum(0))
+        dbasic[:, a] = (de @ P[f'affine_unit_{s_}.weight'].detach()).view(N, n_u, -1)
+    dpre1 = (dbasic * (basic > 0)).view(N * U, -1)
+    dw1 = dpre1.t() @ units_t.reshape(N * U, 10)
+    db1 = dpre1.sum(0)
+    de_env = dx896[:, :128] * (env_e > 0)
+    return torch.stack(dWt), dw1, db1, (torch.stack(dbt), de_env.t() @ env_t, de_env.sum(0))
 
 
 def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], units_t, env_t, act_t, msk_t, adv_t,
@@ -195,6 +276,9 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     weight-gradient GEMMs (W_hh, W_ih, pre-RNN) ACCUMULATE straight into those and are left out of ``grads``.
     Returns (partials (R,16) f32, logp (N) f32 time-major, grads {param name → tensor})."""
     from ..ops.gemm import gemm_tn
+    exact = bool(getattr(fp, 'exact', False))
+    if exact:
+        gemm_tn = _gemm_tn_exact          # noqa: F811 — exact-f32 weight gradients
     C = fp.C
     cfg, lc = fp.cfg, fp.loss_cfg
     N = B * S
@@ -214,7 +298,12 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     f32 = bool(getattr(fp, 'fp32', False))    # fp32-accurate learner: fp32 activations, bf16x3 MFMA, exact-f32 GEMMs
     adt = torch.float32 if f32 else torch.bfloat16
     # (x896 / emb come back in the weights' dtype: bf16, or fp32 from the bf16x3 encoder)
-    x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs))
+    enc_graph = None
+    if exact:
+        x896, emb, enc_graph = _encoder_exact(fp, P, units_t, env_t)
+        arg = None
+    else:
+        x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs))
     attn32 = attn and f32
     if attn32:
         # 5v5 entity attention at fp32 (ops/csrc/attn.hip fp32 kernels: LayerNorm, bf16x3 attention core, pools; the
@@ -243,7 +332,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         E1 = torch.addmm(E0p, Oat, W['wout16'].t())                 # residual + out-projection, bf16
         arg = C.attn_pool(E1, toff, x896, bool(cfg.compat_bugs))    # pools of the attended embeddings
         emb = E1.view(N, U, 128)
-    elif cfg.compat_bugs:   # reference policy.py:127: enemy-tower pool = enemy-nonhero pool
+    elif cfg.compat_bugs and not exact:   # reference policy.py:127: enemy-tower pool = enemy-nonhero pool
         x896[:, 768:896] = x896[:, 512:640]
         arg[:, 5] = arg[:, 3]
     # relu(x896·W_preᵀ + b) as ONE hipBLASLt GEMM with a bias+ReLU epilogue, bf16 (fp32) out (x16 > 0 ⟺ x > 0)
@@ -371,7 +460,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         fused_dx = f32 and _DX_FUSED and 'wpreT' in W
         if fused_dx:
             # ∂pre = (∂G·W_ih)⊙[x16 > 0] and ∂x896 = ∂pre·W_pre in one launch (the ∂pre tile stays in LDS)
-            dpre16, dx896 = C.dpre_dx(dG16, W['wihT16'], x16[r0:r1], W['wpreT'], exact=not _F32_GEMM_FAST)
+            dpre16, dx896 = C.dpre_dx(dG16, W['wihT16'], x16[r0:r1], W['wpreT'], exact=exact or not _F32_GEMM_FAST)
         else:
             # ∂pre-activation of the pre-RNN layer: one GEMM (bf16 or exact f32), ReLU mask in one threshold_backward
             dpre16 = torch.ops.aten.threshold_backward(torch.mm(dG16, W['wihT16'].t()), x16[r0:r1], 0)
@@ -431,14 +520,17 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             return C.enc_small_grads(z[r0:r1], dtl[r0:r1], fp.type_offsets(dev), dx896, env_t[r0:r1], we, be,
                                      bool(cfg.compat_bugs))
         small = None
-        if wg_side:
+        if exact:
+            dwt_c, dw1_c, db1_c, small = _encoder_exact_bwd(fp, P, enc_graph, dx896, dtl[r0:r1], z[r0:r1])
+        elif wg_side:
             sL.wait_stream(main)
             with torch.cuda.stream(sL):
                 small = small_grads()
                 wg_done = torch.cuda.Event()
                 wg_done.record(sL)
-        dwt_c, dw1_c, db1_c = C.encoder_bwd(units_t[r0:r1], w1, b1, wtT16, dtl[r0:r1], z[r0:r1],
-                                            dx896, arg[r0:r1], counts, bool(cfg.compat_bugs), demb_in=demb_in)
+        if not exact:
+            dwt_c, dw1_c, db1_c = C.encoder_bwd(units_t[r0:r1], w1, b1, wtT16, dtl[r0:r1], z[r0:r1],
+                                                dx896, arg[r0:r1], counts, bool(cfg.compat_bugs), demb_in=demb_in)
         dw1 = _acc(dw1, dw1_c)
         db1 = _acc(db1, db1_c)
         dWt = _acc(dWt, dwt_c)

@@ -1,0 +1,79 @@
+"""The fp32-exact learner mode (FusedPolicy(precision='fp32-exact')): IEEE-fp32 products end to end.
+
+CPU: the exact encoder forward/backward of models/pipelined.py (plain torch ops with argmax pool routing, no autograd
+graph so the step stays hipGraph-capturable) equals autograd through the reference encoder (Policy.encode, with the
+reference's ``max`` pooling) in float64.
+GPU: the whole fused step at the deploy shape (lstm512, B=8, S=1400) against a float64 evaluation, per tensor."""
+import copy
+
+import pytest
+import torch
+
+from dotaclient_amd.models.pipelined import _encoder_exact, _encoder_exact_bwd
+from dotaclient_amd.models.policy import TYPE_SUFFIX, Policy, get_config
+
+
+class _FP:
+    def __init__(self, cfg):
+        self.cfg = cfg
+
+
+def _ref_encoder(pol, units, env):
+    """Policy.encode up to x896, with max (argmax-routed gradient) pooling like the reference (policy.py:102-127)."""
+    import torch.nn.functional as F
+    from dotaclient_amd.constants import UNIT_KEYS
+    cfg = pol.config
+    env_e = F.relu(pol.affine_env(env))
+    basic = F.relu(pol.affine_unit_basic_stats(units))
+    sl = pol.layout.slices()
+    emb = torch.cat([getattr(pol, f'affine_unit_{s}')(basic[:, sl[k]]) for k, s in zip(UNIT_KEYS, TYPE_SUFFIX)], 1)
+    pools = []
+    for k in UNIT_KEYS:
+        kk = 'enemy_nonheroes' if (cfg.compat_bugs and k == 'enemy_towers') else k
+        pools.append(emb[:, sl[kk]].max(dim=1).values)
+    return torch.cat([env_e] + pools, 1), emb
+
+
+@pytest.mark.parametrize('preset', ['lstm512', 'compat'])
+def test_exact_encoder_matches_autograd_fp64(preset):
+    torch.manual_seed(0)
+    pol = Policy(get_config(preset)).double()
+    N, U = 64, pol.layout.max_units
+    units = torch.randn(N, U, 10, dtype=torch.float64)
+    env = torch.randn(N, 3, dtype=torch.float64)
+    dx = torch.randn(N, 896, dtype=torch.float64)
+    dtl = torch.randn(N, U, dtype=torch.float64)
+    z = torch.randn(N, 160, dtype=torch.float64)
+    P = dict(pol.named_parameters())
+    x896, emb, saved = _encoder_exact(_FP(pol.config), P, units, env)
+    xr, er = _ref_encoder(pol, units, env)
+    torch.testing.assert_close(x896, xr.detach())
+    torch.testing.assert_close(emb, er.detach())
+    dwt, dw1, db1, (dbt, dwe, dbe) = _encoder_exact_bwd(_FP(pol.config), P, saved, dx, dtl, z)
+    demb = dtl.unsqueeze(2) * z[:, None, :128]
+    names = ['affine_unit_basic_stats.weight', 'affine_unit_basic_stats.bias', 'affine_env.weight',
+             'affine_env.bias'] + [f'affine_unit_{s}.{k}' for s in TYPE_SUFFIX for k in ('weight', 'bias')]
+    g = dict(zip(names, torch.autograd.grad([xr, er], [P[n] for n in names], grad_outputs=[dx, demb],
+                                            allow_unused=True)))
+    torch.testing.assert_close(dw1, g['affine_unit_basic_stats.weight'])
+    torch.testing.assert_close(db1, g['affine_unit_basic_stats.bias'])
+    torch.testing.assert_close(dwe, g['affine_env.weight'])
+    torch.testing.assert_close(dbe, g['affine_env.bias'])
+    for t, s in enumerate(TYPE_SUFFIX):
+        want_w = g[f'affine_unit_{s}.weight']
+        torch.testing.assert_close(dwt[t], want_w if want_w is not None else torch.zeros_like(dwt[t]))
+        want_b = g[f'affine_unit_{s}.bias']
+        torch.testing.assert_close(dbt[t], want_b if want_b is not None else torch.zeros_like(dbt[t]))
+
+
+@pytest.mark.gpu
+def test_exact_fused_step_deploy_shape_matches_fp64(gpu_ops):
+    """fp32-exact at B=8, S=1400: every gradient tensor within 1e-5 (relative) of float64 — the bf16x3 headline mode
+    is pinned at 1e-3 (tests/test_fp32_kernels.py)."""
+    from tests.test_fp32_kernels import _rel, _step_grads
+    (lf, _, gf), (lo, _, go), (l64, g64) = _step_grads('fp32-exact', 'lstm512', 'ppo', 8, 1400, fp64=True)
+    rows = sorted(((_rel(gf[n], g64[n]), _rel(go[n], g64[n]), n) for n in g64
+                   if g64[n] is not None and g64[n].norm() > 0), reverse=True)
+    print('fp32-exact: worst (fused vs fp64, torch-fp32 vs fp64):', rows[:5], 'loss', lf, lo, l64)
+    assert abs(lf - l64) <= 1e-6 * max(1e-2, abs(l64)), (lf, l64)
+    assert rows[0][0] < 1e-5, rows[:5]
