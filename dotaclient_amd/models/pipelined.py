@@ -369,6 +369,14 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             e = torch.cuda.Event()
             e.record(sL)
             fwd_done.append(e)
+    dx_w = None
+    if f32 and _DX_FUSED and 'wpreT' in W:
+        # weight operands of the fused ∂X kernel, split once per step into bf16 hi/lo images (exact: fp32 as is);
+        # enqueued before the main stream waits on the forward recurrence, so they run beside it
+        if exact:
+            dx_w = (W['wihT16'], W['wihT16'].new_empty(0), W['wpreT'], W['wpreT'].new_empty(0))
+        else:
+            dx_w = tuple(C.split_bf16x2(W['wihT16'])) + tuple(C.split_bf16x2(W['wpreT']))
     for (t0, t1), done in zip(spans, fwd_done):
         main.wait_event(done)
         r0, r1 = t0 * B, t1 * B
@@ -378,7 +386,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         dz16, dtl_c, part, lp = C.heads_loss(zc, emb[r0:r1], act_t[r0:r1], msk_t[r0:r1], adv_t[r0:r1],
                                              ret_t[r0:r1], lpo_t[r0:r1], nret_t[r0:r1], norms, algo, False,
                                              S, B, float(lc.clip_eps), float(lc.entropy_coef), float(lc.vf_coef),
-                                             dz_bf16=not f32)
+                                             dz_bf16=not f32, precise=exact)
         parts.append(part)
         first = dWcat is None
         if first:
@@ -457,10 +465,10 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             else:       # h_{t-1} rows: h0 for t = 0, then hs[0 : t1-1] — no concatenation materialised
                 gemm_tn(dG16, hs16[0:t1 - 1].view(n - B, H), out=dWhh, perm=gperm, accumulate=True, b0=h016)
             gemm_tn(dG16, x16[r0:r1], out=dWih, perm=gperm, accumulate=True)
-        fused_dx = f32 and _DX_FUSED and 'wpreT' in W
+        fused_dx = dx_w is not None
         if fused_dx:
             # ∂pre = (∂G·W_ih)⊙[x16 > 0] and ∂x896 = ∂pre·W_pre in one launch (the ∂pre tile stays in LDS)
-            dpre16, dx896 = C.dpre_dx(dG16, W['wihT16'], x16[r0:r1], W['wpreT'], exact=exact or not _F32_GEMM_FAST)
+            dpre16, dx896 = C.dpre_dx(dG16, dx_w[0], dx_w[1], x16[r0:r1], dx_w[2], dx_w[3])
         else:
             # ∂pre-activation of the pre-RNN layer: one GEMM (bf16 or exact f32), ReLU mask in one threshold_backward
             dpre16 = torch.ops.aten.threshold_backward(torch.mm(dG16, W['wihT16'].t()), x16[r0:r1], 0)

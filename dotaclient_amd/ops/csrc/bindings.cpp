@@ -249,7 +249,7 @@ std::vector<torch::Tensor> heads_loss(torch::Tensor z, torch::Tensor emb, torch:
                                       torch::Tensor adv, torch::Tensor ret, torch::Tensor logp_old,
                                       torch::Tensor nret, torch::Tensor norms, int64_t algo, bool compat_value_bug,
                                       int64_t S_bug, int64_t B_bug, double clip_eps, double ent_coef,
-                                      double vf_coef, bool dz_bf16) {
+                                      double vf_coef, bool dz_bf16, bool precise) {
   CHECK_F32(z); CHECK_DEV(emb); CHECK_CONTIG(emb); CHECK_U8(act); CHECK_U8(msk); CHECK_F32(adv); CHECK_F32(ret);
   CHECK_F32(logp_old); CHECK_F32(nret); CHECK_F32(norms);
   const bool ef32 = emb.scalar_type() == at::kFloat;
@@ -271,7 +271,7 @@ std::vector<torch::Tensor> heads_loss(torch::Tensor z, torch::Tensor emb, torch:
                            ptr<float>(norms), dz_bf16 ? nullptr : ptr<float>(dz), ptr<float>(dtl), ptr<float>(part),
                            ptr<float>(logp), N, U, (int)algo, compat_value_bug ? 1 : 0, (int)S_bug, (int)B_bug,
                            (float)clip_eps, (float)ent_coef, (float)vf_coef, cur_stream(),
-                           dz_bf16 ? ptr<short>(dz) : nullptr, ef32 ? 1 : 0),
+                           dz_bf16 ? ptr<short>(dz) : nullptr, ef32 ? 1 : 0, precise && ef32 ? 1 : 0),
             "dca_heads_loss");
   return {dz, dtl, part, logp};
 }
@@ -578,23 +578,44 @@ std::vector<torch::Tensor> enc_small_grads(torch::Tensor z, torch::Tensor dtl, t
   return {out.narrow(0, 0, 768).view({6, 128}), out.narrow(0, 768, 384).view({128, 3}), out.narrow(0, 1152, 128)};
 }
 
+// fp32 → (hi, lo) bf16 images, x = hi + lo (the bf16x3 operand split, done once per step for a weight image)
+std::vector<torch::Tensor> split_bf16x2(torch::Tensor src) {
+  CHECK_F32(src);
+  TORCH_CHECK(src.numel() % 4 == 0, "split_bf16x2: numel % 4 == 0");
+  auto hi = torch::empty(src.sizes(), src.options().dtype(at::kBFloat16));
+  auto lo = torch::empty(src.sizes(), src.options().dtype(at::kBFloat16));
+  hip_check(dca_split_bf16x2(ptr<float>(src), ptr<short>(hi), ptr<short>(lo), src.numel(), cur_stream()),
+            "dca_split_bf16x2");
+  return {hi, lo};
+}
+
 // Fused ∂X chain of the fp32 pre-RNN layer (ops/csrc/dx_chain.hip): dpre = (dG · W_ih) ⊙ [x > 0], dx = dpre · W_pre.
-// dG (N, K1) f32, wihT (256, K1) f32 (K-contiguous image of W_ih, gate rows in dG's column order), x (N, 256) f32
-// ReLU outputs, wpreT (X, 256) f32. Returns (dpre (N, 256), dx (N, X)). exact: exact-f32 MFMA instead of bf16x3.
-std::vector<torch::Tensor> dpre_dx(torch::Tensor dG, torch::Tensor wihT, torch::Tensor x, torch::Tensor wpreT,
-                                   bool exact) {
-  CHECK_F32(dG); CHECK_F32(wihT); CHECK_F32(x); CHECK_F32(wpreT);
-  const int N = dG.size(0), K1 = dG.size(1), X = wpreT.size(0);
-  TORCH_CHECK(dG.dim() == 2 && wihT.dim() == 2 && x.dim() == 2 && wpreT.dim() == 2, "dpre_dx: 2-D operands");
-  TORCH_CHECK(wihT.size(0) == 256 && wihT.size(1) == K1 && x.size(0) == N && x.size(1) == 256 &&
-              wpreT.size(1) == 256, "dpre_dx: shapes (N,K1) (256,K1) (N,256) (X,256)");
+// dG (N, K1) f32, x (N, 256) f32 ReLU outputs; weights K-contiguous per output column: w1 = W_ihᵀ image (256, K1),
+// w2 = W_preᵀ image (X, 256) — bf16 hi / lo images (bf16x3), or fp32 with w1l / w2l empty (exact).
+// Returns (dpre (N, 256), dx (N, X)).
+std::vector<torch::Tensor> dpre_dx(torch::Tensor dG, torch::Tensor w1h, torch::Tensor w1l, torch::Tensor x,
+                                   torch::Tensor w2h, torch::Tensor w2l) {
+  CHECK_F32(dG); CHECK_F32(x); CHECK_DEV(w1h); CHECK_CONTIG(w1h); CHECK_DEV(w2h); CHECK_CONTIG(w2h);
+  const bool exact = w1h.scalar_type() == at::kFloat;
+  if (exact) {
+    TORCH_CHECK(w2h.scalar_type() == at::kFloat, "dpre_dx: both weights fp32 (exact) or bf16 hi/lo pairs");
+  } else {
+    CHECK_DT(w1h, at::kBFloat16); CHECK_DT(w2h, at::kBFloat16); CHECK_DEV(w1l); CHECK_CONTIG(w1l);
+    CHECK_DEV(w2l); CHECK_CONTIG(w2l); CHECK_DT(w1l, at::kBFloat16); CHECK_DT(w2l, at::kBFloat16);
+    TORCH_CHECK(w1l.sizes() == w1h.sizes() && w2l.sizes() == w2h.sizes(), "dpre_dx: hi / lo image shapes");
+  }
+  const int N = dG.size(0), K1 = dG.size(1), X = w2h.size(0);
+  TORCH_CHECK(dG.dim() == 2 && w1h.dim() == 2 && x.dim() == 2 && w2h.dim() == 2, "dpre_dx: 2-D operands");
+  TORCH_CHECK(w1h.size(0) == 256 && w1h.size(1) == K1 && x.size(0) == N && x.size(1) == 256 && w2h.size(1) == 256,
+              "dpre_dx: shapes (N,K1) (256,K1) (N,256) (X,256)");
   TORCH_CHECK(K1 % 128 == 0 && X % 128 == 0, "dpre_dx: K1 % 128 == 0 and X % 128 == 0");
   TORCH_CHECK((long long)N * K1 * 4 <= 0x7fff0000LL, "dpre_dx: dG too large for one launch");
   auto o = dG.options();
   auto dpre = torch::empty({N, 256}, o);
   auto dx = torch::empty({N, X}, o);
-  hip_check(dca_dpre_dx(ptr<float>(dG), ptr<float>(wihT), ptr<float>(x), ptr<float>(wpreT), ptr<float>(dpre),
-                        ptr<float>(dx), N, K1, X, exact ? 1 : 0, cur_stream()),
+  hip_check(dca_dpre_dx(ptr<float>(dG), w1h.data_ptr(), exact ? nullptr : w1l.data_ptr(), ptr<float>(x),
+                        w2h.data_ptr(), exact ? nullptr : w2l.data_ptr(), ptr<float>(dpre), ptr<float>(dx), N, K1, X,
+                        exact ? 1 : 0, cur_stream()),
             "dca_dpre_dx");
   return {dpre, dx};
 }
@@ -799,7 +820,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("z"), py::arg("emb"), py::arg("act"), py::arg("msk"), py::arg("adv"), py::arg("ret"),
         py::arg("logp_old"), py::arg("nret"), py::arg("norms"), py::arg("algo"), py::arg("compat_value_bug"),
         py::arg("S_bug"), py::arg("B_bug"), py::arg("clip_eps"), py::arg("ent_coef"), py::arg("vf_coef"),
-        py::arg("dz_bf16") = false);
+        py::arg("dz_bf16") = false, py::arg("precise") = false);
   m.def("encoder_fwd", &encoder_fwd, "fused entity encoder forward (unit MLP, per-type GEMM, max-pool+argmax)");
   m.def("encoder_bwd", &encoder_bwd, "fused entity encoder backward: dW_type (K-blocked split-K MFMA GEMM), dW1, db1",
         py::arg("units"), py::arg("w1"), py::arg("b1"), py::arg("wtT"), py::arg("dtl"), py::arg("q"), py::arg("dx"),
@@ -827,8 +848,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_tn", &gemm_tn, "C (+)= A^T B for K-outer bf16 or fp32 (bf16x3) operands (split-K MFMA, LDS transposed reads)",
         py::arg("A"), py::arg("B"), py::arg("C"), py::arg("perm") = py::none(), py::arg("accumulate") = false,
         py::arg("B0") = py::none(), py::arg("colsum") = py::none());
-  m.def("dpre_dx", &dpre_dx, "fused pre-RNN dX chain: (dG·W_ih)*[x>0] -> dpre, dpre·W_pre -> dx (bf16x3 or exact MFMA)",
-        py::arg("dG"), py::arg("wihT"), py::arg("x"), py::arg("wpreT"), py::arg("exact") = false);
+  m.def("dpre_dx", &dpre_dx, "fused pre-RNN dX chain: (dG·W_ih)*[x>0] -> dpre, dpre·W_pre -> dx (bf16x3 with pre-split "
+        "bf16 hi/lo weights, or exact-f32 MFMA with fp32 weights)", py::arg("dG"), py::arg("w1h"), py::arg("w1l"),
+        py::arg("x"), py::arg("w2h"), py::arg("w2l"));
+  m.def("split_bf16x2", &split_bf16x2, "fp32 -> (hi, lo) bf16 images with x = hi + lo");
   m.def("enc_small_grads", &enc_small_grads, "entity-encoder type-bias and env-layer gradients in one pass");
   m.def("ln_fwd", &ln_fwd, "LayerNorm(E0 - bsub) -> (xn, mean, rstd); bf16, or fp32 (bsub may be empty); optional copy of E0",
         py::arg("e0"), py::arg("bsub"), py::arg("gamma"), py::arg("beta"), py::arg("eps"),

@@ -11,18 +11,23 @@
 // One 512-thread workgroup (8 waves) per 64-row tile; the 64 × P dpre tile never leaves the workgroup between the
 // two products (it is written once to HBM for the pre-RNN weight gradient, and kept in LDS as the second product's
 // A operand):
-// * stage 1, K = 4H in 32-deep slabs, double-buffered through LDS (register-staged 16-B loads of the next slab
-//   issued before the current slab's MFMAs, one barrier per slab); waves as 2 (32 rows) × 4 (64 columns), each
-//   2 × 4 v_mfma_f32_16x16x32_bf16 tiles;
-// * ReLU mask + dpre store in the accumulator layout, dpre written into LDS;
-// * stage 2, X in 128-column chunks × K = P in 32-deep slabs (same double-buffered pipeline), waves as 4 (16 rows) ×
-//   2 (64 columns).
-// Operands are fp32; both weight operands come K-contiguous per output column (W_ihᵀ image (P × 4H) and W_preᵀ
-// image (X × P), models/pipelined.py WeightImages), so every MFMA fragment is a plain 16-B LDS read.
-// EXACT = false: bf16x3 — every fp32 value is split ONCE while staging into hi + lo bf16 LDS images and each product
-// is hi·hi + lo·hi + hi·lo on the bf16 MFMA (≈2⁻¹⁶ relative per product, the fp32 learner's accuracy class);
-// EXACT = true: exact fp32 on v_mfma_f32_16x16x4_f32 — the 16x16x32 fragment's 8 k values of a lane feed 8 chained
-// 16x16x4 MFMAs (call j takes element j: lane l contributes k = 8·(l/16) + j, so the 8 calls cover all 32 k).
+// * stage 1, K = 4H in 32-deep slabs, double-buffered through LDS, loads issued RD slabs ahead into a register ring
+//   (one slab of lead left every LDS store waiting out a full memory round trip), one barrier per slab; waves as
+//   2 (32 rows) × 4 (64 columns), each 2 × 4 v_mfma_f32_16x16x32_bf16 tiles;
+// * ReLU mask + dpre store in the accumulator layout, dpre written into LDS in the stage-1 A layout (8 slabs);
+// * stage 2, X in 128-column chunks × K = P in 32-deep slabs (same pipeline), waves as 4 (16 rows) × 2 (64 columns).
+// Both weight operands come K-contiguous per output column (W_ihᵀ image (P × 4H), W_preᵀ image (X × P)).
+//
+// EXACT = false: bf16x3 — x = hi + lo (two bf16), products hi·hi + lo·hi + hi·lo on the bf16 MFMA (≈2⁻¹⁶ relative per
+// product, the fp32 learner's accuracy class). The weights arrive PRE-SPLIT (hi / lo bf16 images, split once per
+// step by dca_split_bf16x2), so only the dG slab is split while staging. LDS images: 64-B rows (32 bf16) with the
+// 16-B chunk index XOR (row>>1)&3 — conflict-free for the fragment reads (ds_read_b128 lane groups), the dG b64
+// stores and the weight b128 stores (exhaustive check over the lane→address maps; the first version, 80-B padded
+// rows without swizzle and the weights split in-kernel, measured 4.8 bank-conflict cycles per LDS instruction,
+// 5 VALU per MFMA and 205 µs at the deploy shape).
+// EXACT = true: exact fp32 on v_mfma_f32_16x16x4_f32 — a 16x16x32 fragment's 8 k values per lane feed 8 chained
+// 16x16x4 MFMAs (call j takes element j: lane l contributes k = 8·(l/16) + j, so the 8 calls cover all 32 k);
+// fp32 LDS rows (144-B pitch), fp32 weights.
 #include "common.h"
 
 namespace {
@@ -34,18 +39,23 @@ constexpr int BM = 64, BK = 32, NT = 512, P = 256, XC = 128, RD = 4;
 
 template <bool EXACT>
 struct Lay {
-  // bytes per operand row of one 32-deep slab: hi/lo bf16 (64 B + 16 pad) or fp32 (128 B + 16 pad)
-  static constexpr int RP = EXACT ? 144 : 80;
-  static constexpr int IMG = EXACT ? 1 : 2;              // images per operand (hi, lo)
-  static constexpr int A1 = BM * RP;                      // stage-1 A image bytes
-  static constexpr int B1 = P * RP;                       // stage-1 B image bytes
-  static constexpr int S1 = IMG * (A1 + B1);              // one stage-1 buffer
-  static constexpr int DP = EXACT ? (P * 4 + 16) : (P * 2 + 16);   // dpre row pitch
-  static constexpr int D = IMG * BM * DP;                 // dpre tile (A operand of stage 2)
-  static constexpr int B2 = XC * RP;                      // stage-2 B image bytes
+  static constexpr int RP = EXACT ? 144 : 64;             // bytes per operand row of one 32-deep slab
+  static constexpr int IMG = EXACT ? 1 : 2;               // images per operand (hi, lo)
+  static constexpr int A1 = BM * RP;                       // stage-1 A image bytes
+  static constexpr int B1 = P * RP;                        // stage-1 B image bytes
+  static constexpr int S1 = IMG * (A1 + B1);               // one stage-1 buffer
+  static constexpr int D = IMG * (P / BK) * A1;            // dpre tile: 8 slabs in the A layout
+  static constexpr int B2 = XC * RP;                       // stage-2 B image bytes
   static constexpr int S2 = IMG * B2;
   static constexpr int BYTES = (2 * S1 > D + 2 * S2) ? 2 * S1 : D + 2 * S2;
 };
+
+// byte offset of 16-B chunk c of row r in a slab image (bf16: 4 chunks per row, swizzled; fp32: 8, padded rows)
+template <bool EXACT>
+__device__ __forceinline__ int coff(int r, int c) {
+  if constexpr (EXACT) return r * Lay<true>::RP + 16 * c;
+  else return r * 64 + 16 * (c ^ ((r >> 1) & 3));
+}
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, long long bytes) {
   const unsigned long long a = (unsigned long long)p;
@@ -55,43 +65,38 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p, long long 
   return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0,
                                            __builtin_amdgcn_readfirstlane(nb), 0x00020000);
 }
-__device__ __forceinline__ float4 ld4(__amdgpu_buffer_rsrc_t r, int off) {   // out of range → zeros
-  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+__device__ __forceinline__ uint4 ld16(__amdgpu_buffer_rsrc_t r, int off) {   // out of range → zeros
+  return __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0));
+}
+constexpr int kOob = 0x7fff8000;
+
+__device__ __forceinline__ unsigned pack2(short a, short b) {
+  return (unsigned)(unsigned short)a | ((unsigned)(unsigned short)b << 16);
+}
+// 4 fp32 → hi / lo bf16 quads
+__device__ __forceinline__ void split4(const float4 v, uint2& hi, uint2& lo) {
+  const short h0 = dca::f2bf(v.x), h1 = dca::f2bf(v.y), h2 = dca::f2bf(v.z), h3 = dca::f2bf(v.w);
+  hi = make_uint2(pack2(h0, h1), pack2(h2, h3));
+  lo = make_uint2(pack2(dca::f2bf(v.x - dca::bf2f(h0)), dca::f2bf(v.y - dca::bf2f(h1))),
+                  pack2(dca::f2bf(v.z - dca::bf2f(h2)), dca::f2bf(v.w - dca::bf2f(h3))));
 }
 
-// ---- staging: 4 consecutive fp32 values of one operand row → LDS (hi / lo bf16 images, or fp32)
-template <bool EXACT>
-__device__ __forceinline__ void put4(char* img, int img_bytes, int row, int k, float4 v) {
-  const int off = row * Lay<EXACT>::RP + k * (EXACT ? 4 : 2);
-  if constexpr (EXACT) {
-    *reinterpret_cast<float4*>(img + off) = v;
-  } else {
-    const short h0 = dca::f2bf(v.x), h1 = dca::f2bf(v.y), h2 = dca::f2bf(v.z), h3 = dca::f2bf(v.w);
-    const short l0 = dca::f2bf(v.x - dca::bf2f(h0)), l1 = dca::f2bf(v.y - dca::bf2f(h1)),
-                l2 = dca::f2bf(v.z - dca::bf2f(h2)), l3 = dca::f2bf(v.w - dca::bf2f(h3));
-    *reinterpret_cast<uint2*>(img + off) = make_uint2((unsigned)(unsigned short)h0 | ((unsigned)(unsigned short)h1 << 16),
-                                                      (unsigned)(unsigned short)h2 | ((unsigned)(unsigned short)h3 << 16));
-    *reinterpret_cast<uint2*>(img + img_bytes + off) =
-        make_uint2((unsigned)(unsigned short)l0 | ((unsigned)(unsigned short)l1 << 16),
-                   (unsigned)(unsigned short)l2 | ((unsigned)(unsigned short)l3 << 16));
-  }
-}
-
-// one MFMA fragment (row `row` of an image, k chunk q = lane/16 of the 32-deep slab)
 struct Frag {
   bf16x8 hi, lo;        // bf16x3
   float f[8];           // exact
 };
+// fragment of row r (chunk q = lane/16 of the 32-deep slab) from a slab image
 template <bool EXACT>
-__device__ __forceinline__ void get_frag(const char* img, int img_bytes, int row_off, int q, Frag& fr) {
+__device__ __forceinline__ void get_frag(const char* img, int img_bytes, int r, int q, Frag& fr) {
   if constexpr (EXACT) {
-    const float4 a = *reinterpret_cast<const float4*>(img + row_off + q * 32);
-    const float4 b = *reinterpret_cast<const float4*>(img + row_off + q * 32 + 16);
+    const float4 a = *reinterpret_cast<const float4*>(img + coff<true>(r, 2 * q));
+    const float4 b = *reinterpret_cast<const float4*>(img + coff<true>(r, 2 * q + 1));
     fr.f[0] = a.x; fr.f[1] = a.y; fr.f[2] = a.z; fr.f[3] = a.w;
     fr.f[4] = b.x; fr.f[5] = b.y; fr.f[6] = b.z; fr.f[7] = b.w;
   } else {
-    fr.hi = *reinterpret_cast<const bf16x8*>(img + row_off + q * 16);
-    fr.lo = *reinterpret_cast<const bf16x8*>(img + img_bytes + row_off + q * 16);
+    const int o = coff<false>(r, q);
+    fr.hi = *reinterpret_cast<const bf16x8*>(img + o);
+    fr.lo = *reinterpret_cast<const bf16x8*>(img + img_bytes + o);
   }
 }
 template <bool EXACT>
@@ -108,42 +113,63 @@ __device__ __forceinline__ f32x4 mma(const Frag& a, const Frag& b, f32x4 c) {
 }
 
 template <bool EXACT>
-__global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict__ dG, const float* __restrict__ wihT,
-                                                        const float* __restrict__ x, const float* __restrict__ wpreT,
+__global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict__ dG, const void* __restrict__ w1h,
+                                                        const void* __restrict__ w1l, const float* __restrict__ x,
+                                                        const void* __restrict__ w2h, const void* __restrict__ w2l,
                                                         float* __restrict__ dpre, float* __restrict__ dx, int N,
                                                         int K1, int X) {
   using L = Lay<EXACT>;
+  constexpr int ES = EXACT ? 4 : 2;                 // bytes per weight element in HBM
   __shared__ __attribute__((aligned(16))) char lds[L::BYTES];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, r16 = lane & 15, q = lane >> 4;
   const int r0 = blockIdx.x * BM;
   const __amdgpu_buffer_rsrc_t rA = rsrc(dG, (long long)N * K1 * 4);
-  const __amdgpu_buffer_rsrc_t rW1 = rsrc(wihT, (long long)P * K1 * 4);
-  const __amdgpu_buffer_rsrc_t rW2 = rsrc(wpreT, (long long)X * P * 4);
-  constexpr int kOob = 0x7fff8000;
+  const __amdgpu_buffer_rsrc_t rW1h = rsrc(w1h, (long long)P * K1 * ES);
+  const __amdgpu_buffer_rsrc_t rW1l = rsrc(EXACT ? w1h : w1l, (long long)P * K1 * ES);
+  const __amdgpu_buffer_rsrc_t rW2h = rsrc(w2h, (long long)X * P * ES);
+  const __amdgpu_buffer_rsrc_t rW2l = rsrc(EXACT ? w2h : w2l, (long long)X * P * ES);
 
   // ================= stage 1: C1 (64 × P) = dG[r0:r0+64] · W_ih =================
-  // staging map: A slab 64 rows × 32 k = 512 float4 (one per thread: row t/8, k 4·(t%8));
-  //              B slab P cols × 32 k = 2048 float4 (four per thread: col t/2, k 16·(t%2) + 4·i)
-  const int ar = tid >> 3, ak = (tid & 7) * 4;
-  const int bc = tid >> 1, bk = (tid & 1) * 16;
+  const int ar = tid >> 3, ak = (tid & 7) * 4;              // dG slab: one fp32 quad per thread
   const int arow = r0 + ar;
   const int a_off0 = arow < N ? (arow * K1 + ak) * 4 : kOob;
-  const int b_off0 = (bc * K1 + bk) * 4;
-  // register ring of RD slabs in flight: the slab stored into LDS at iteration ks was loaded at ks + 1 - RD, so
-  // RD - 1 slabs of MFMA work cover each load's latency (one slab of lead was 4x slower: every store waited out a
-  // full memory round trip)
-  float4 sa[RD], sb[RD][4];
+  const int br = tid & 255, bh = tid >> 8;                   // W1 slab: 16 k per thread
+  const int b_off0 = (br * K1 + 16 * bh) * ES;
+  float4 sa[RD];
+  uint4 sb[RD][4];
   auto load1 = [&](int slot, int k0) {
-    sa[slot] = ld4(rA, a_off0 == kOob ? kOob : a_off0 + k0 * 4);
+    sa[slot] = __builtin_bit_cast(float4, ld16(rA, a_off0 == kOob ? kOob : a_off0 + k0 * 4));
+    if constexpr (EXACT) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sb[slot][i] = ld4(rW1, b_off0 + (k0 + 4 * i) * 4);
+      for (int i = 0; i < 4; ++i) sb[slot][i] = ld16(rW1h, b_off0 + (k0 + 4 * i) * 4);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        sb[slot][j] = ld16(rW1h, b_off0 + (k0 + 8 * j) * 2);
+        sb[slot][2 + j] = ld16(rW1l, b_off0 + (k0 + 8 * j) * 2);
+      }
+    }
   };
   auto store1 = [&](int slot, int buf) {
     char* base = lds + buf * L::S1;
-    put4<EXACT>(base, L::A1, ar, ak, sa[slot]);
     char* bb = base + L::IMG * L::A1;
+    if constexpr (EXACT) {
+      *reinterpret_cast<float4*>(base + ar * L::RP + ak * 4) = sa[slot];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) put4<EXACT>(bb, L::B1, bc, bk + 4 * i, sb[slot][i]);
+      for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(bb + br * L::RP + (16 * bh + 4 * i) * 4) = sb[slot][i];
+    } else {
+      uint2 hi, lo;
+      split4(sa[slot], hi, lo);
+      const int o = coff<false>(ar, ak >> 3) + 8 * ((ak >> 2) & 1);
+      *reinterpret_cast<uint2*>(base + o) = hi;
+      *reinterpret_cast<uint2*>(base + L::A1 + o) = lo;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int ob = coff<false>(br, 2 * bh + j);
+        *reinterpret_cast<uint4*>(bb + ob) = sb[slot][j];
+        *reinterpret_cast<uint4*>(bb + L::B1 + ob) = sb[slot][2 + j];
+      }
+    }
   };
   const int wr = w >> 2, wc = w & 3;             // 2 × 4 waves: rows 32·wr, cols 64·wc
   f32x4 acc[2][4];
@@ -164,9 +190,9 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
       const char* bb = base + L::IMG * L::A1;
       Frag fa[2], fb[4];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) get_frag<EXACT>(base, L::A1, (wr * 32 + i * 16 + r16) * L::RP, q, fa[i]);
+      for (int i = 0; i < 2; ++i) get_frag<EXACT>(base, L::A1, wr * 32 + i * 16 + r16, q, fa[i]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) get_frag<EXACT>(bb, L::B1, (wc * 64 + j * 16 + r16) * L::RP, q, fb[j]);
+      for (int j = 0; j < 4; ++j) get_frag<EXACT>(bb, L::B1, wc * 64 + j * 16 + r16, q, fb[j]);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -177,9 +203,10 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
     }
   }
 
-  // ================= ReLU mask, dpre → HBM and → LDS (stage-2 A operand) =================
+  // ================= ReLU mask, dpre → HBM and → LDS (stage-2 A operand, 8 slabs in the A layout) =============
   // accumulator layout: acc[i][j][e] = C[row 32·wr + 16·i + 4·q + e][col 64·wc + 16·j + r16]
   char* dimg = lds;                               // aliases the stage-1 buffers (all reads done: barrier above)
+  constexpr int DIMG = (P / BK) * L::A1;          // one image (hi, or fp32) of the dpre tile
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -193,30 +220,44 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
           v = x[(size_t)grow * P + col] > 0.f ? acc[i][j][e] : 0.f;
           dpre[(size_t)grow * P + col] = v;
         }
+        const int kk = col & (BK - 1);
+        char* slab = dimg + (col / BK) * L::A1;
         if constexpr (EXACT) {
-          *reinterpret_cast<float*>(dimg + row * L::DP + col * 4) = v;
+          *reinterpret_cast<float*>(slab + coff<true>(row, kk >> 2) + 4 * (kk & 3)) = v;
         } else {
+          const int o = coff<false>(row, kk >> 3) + 2 * (kk & 7);
           const short h = dca::f2bf(v);
-          *reinterpret_cast<short*>(dimg + row * L::DP + col * 2) = h;
-          *reinterpret_cast<short*>(dimg + BM * L::DP + row * L::DP + col * 2) = dca::f2bf(v - dca::bf2f(h));
+          *reinterpret_cast<short*>(slab + o) = h;
+          *reinterpret_cast<short*>(slab + DIMG + o) = dca::f2bf(v - dca::bf2f(h));
         }
       }
 
   // ================= stage 2: dx (64 × X) = dpre · W_pre, 128-column chunks =================
-  // staging map: B slab 128 cols × 32 k = 1024 float4 (two per thread: col t/4, k 8·(t%4) + 4·i)
   char* s2 = lds + L::D;
-  const int cc = tid >> 2, ck = (tid & 3) * 8;
   constexpr int nk2 = P / BK;
-  float4 sw[RD][2];
+  const int cr = tid & 127, cq = tid >> 7;        // W2 slab: row, chunk (8 k)
+  uint4 sw[RD][2];
   auto load2 = [&](int slot, int it) {
     const int c0 = (it / nk2) * XC, k0 = (it % nk2) * BK;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) sw[slot][i] = ld4(rW2, ((c0 + cc) * P + k0 + ck + 4 * i) * 4);
+    const int o = ((c0 + cr) * P + k0 + 8 * cq) * ES;
+    if constexpr (EXACT) {
+      sw[slot][0] = ld16(rW2h, o);
+      sw[slot][1] = ld16(rW2h, o + 16);
+    } else {
+      sw[slot][0] = ld16(rW2h, o);
+      sw[slot][1] = ld16(rW2l, o);
+    }
   };
   auto store2 = [&](int slot, int buf) {
     char* bb = s2 + buf * L::S2;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) put4<EXACT>(bb, L::B2, cc, ck + 4 * i, sw[slot][i]);
+    if constexpr (EXACT) {
+      *reinterpret_cast<uint4*>(bb + coff<true>(cr, 2 * cq)) = sw[slot][0];
+      *reinterpret_cast<uint4*>(bb + coff<true>(cr, 2 * cq + 1)) = sw[slot][1];
+    } else {
+      const int o = coff<false>(cr, cq);
+      *reinterpret_cast<uint4*>(bb + o) = sw[slot][0];
+      *reinterpret_cast<uint4*>(bb + L::B2 + o) = sw[slot][1];
+    }
   };
   const int vr = w >> 1, vc = w & 1;             // 4 × 2 waves: rows 16·vr, cols 64·vc of the chunk
   const int nchunk = X / XC, total = nchunk * nk2;   // multiple of RD (nk2 = 8)
@@ -234,14 +275,9 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
       const int chunk = it / nk2, ks = it % nk2;
       const char* bb = s2 + (d & 1) * L::S2;
       Frag fa, fb[4];
-      // A fragment: dpre row 16·vr + r16, k = 32·ks + 8·q … (the dpre image holds the full K = P per row)
-      if constexpr (EXACT) {
-        get_frag<true>(dimg, 0, (vr * 16 + r16) * L::DP + ks * BK * 4, q, fa);
-      } else {
-        get_frag<false>(dimg, BM * L::DP, (vr * 16 + r16) * L::DP + ks * BK * 2, q, fa);
-      }
+      get_frag<EXACT>(dimg + ks * L::A1, DIMG, vr * 16 + r16, q, fa);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) get_frag<EXACT>(bb, L::B2, (vc * 64 + j * 16 + r16) * L::RP, q, fb[j]);
+      for (int j = 0; j < 4; ++j) get_frag<EXACT>(bb, L::B2, vc * 64 + j * 16 + r16, q, fb[j]);
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc2[j] = mma<EXACT>(fa, fb[j], acc2[j]);
       if (it + 1 < total) store2((d + 1) % RD, (d + 1) & 1);
@@ -262,22 +298,42 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
   }
 }
 
+// fp32 → hi / lo bf16 images (x = hi + lo), 4 elements per thread
+__global__ __launch_bounds__(256) void split_bf16x2_kernel(const float4* __restrict__ src, uint2* __restrict__ hi,
+                                                           uint2* __restrict__ lo, int n4) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n4) split4(src[i], hi[i], lo[i]);
+}
+
 }  // namespace
 
-extern "C" size_t dca_dpre_dx_lds(int exact) { return exact ? Lay<true>::BYTES : Lay<false>::BYTES; }
+// src (n fp32, n % 4 == 0) → hi, lo (n bf16 each)
+extern "C" hipError_t dca_split_bf16x2(const float* src, short* hi, short* lo, long long n, hipStream_t stream) {
+  if (n % 4 != 0) return hipErrorInvalidValue;
+  const int n4 = (int)(n / 4);
+  if (n4 == 0) return hipSuccess;
+  hipLaunchKernelGGL(split_bf16x2_kernel, dim3((n4 + 255) / 256), dim3(256), 0, stream,
+                     reinterpret_cast<const float4*>(src), reinterpret_cast<uint2*>(hi), reinterpret_cast<uint2*>(lo),
+                     n4);
+  return hipGetLastError();
+}
 
-// dG (N, K1) f32 row-major; wihT (P=256, K1) f32 (K-contiguous per output column); x (N, P) f32 (ReLU outputs);
-// wpreT (X, P) f32; outputs dpre (N, P), dx (N, X) f32. K1 % 32 == 0, X % 128 == 0.
-extern "C" hipError_t dca_dpre_dx(const float* dG, const float* wihT, const float* x, const float* wpreT, float* dpre,
-                                  float* dx, int N, int K1, int X, int exact, hipStream_t stream) {
+// dG (N, K1) f32 row-major; x (N, P) f32 (ReLU outputs). Weights K-contiguous per output column:
+// bf16x3 (exact = 0): w1h / w1l (P, K1) and w2h / w2l (X, P) bf16 hi / lo images; exact: w1h (P, K1), w2h (X, P)
+// fp32 (w1l / w2l unused). Outputs dpre (N, P), dx (N, X) f32. K1 % 128 == 0, X % 128 == 0.
+extern "C" hipError_t dca_dpre_dx(const float* dG, const void* w1h, const void* w1l, const float* x, const void* w2h,
+                                  const void* w2l, float* dpre, float* dx, int N, int K1, int X, int exact,
+                                  hipStream_t stream) {
   if (N < 1 || K1 < RD * BK || K1 % (RD * BK) != 0 || X < XC || X % XC != 0 || ((X / XC) * (P / BK)) % RD != 0)
     return hipErrorInvalidValue;
   if ((long long)N * K1 * 4 > 0x7fff0000LL) return hipErrorInvalidValue;      // buffer-resource range
   const int grid = (N + BM - 1) / BM;
   if (exact) {
-    hipLaunchKernelGGL(dpre_dx_kernel<true>, dim3(grid), dim3(NT), 0, stream, dG, wihT, x, wpreT, dpre, dx, N, K1, X);
+    hipLaunchKernelGGL(dpre_dx_kernel<true>, dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre, dx, N,
+                       K1, X);
   } else {
-    hipLaunchKernelGGL(dpre_dx_kernel<false>, dim3(grid), dim3(NT), 0, stream, dG, wihT, x, wpreT, dpre, dx, N, K1, X);
+    hipLaunchKernelGGL(dpre_dx_kernel<false>, dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre, dx,
+                       N, K1, X);
   }
   return hipGetLastError();
 }

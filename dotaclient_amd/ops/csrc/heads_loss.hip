@@ -40,21 +40,29 @@ __device__ __forceinline__ void put_dz(const Params& P, size_t i, float v) {
   else P.dz[i] = v;
 }
 
+// exp / log: the hardware approximations (v_exp_f32 / v_log_f32 based) by default; libm's correctly-rounded-class
+// expf / logf in the fp32-exact learner (PRECISE), whose ∂L/∂z feeds gradients summed over 11 200 rows
+template <bool PRECISE>
+__device__ __forceinline__ float xexp(float x) { return PRECISE ? expf(x) : __expf(x); }
+template <bool PRECISE>
+__device__ __forceinline__ float xlog(float x) { return PRECISE ? logf(x) : __logf(x); }
+
 // masked log-softmax of one head held one entry per lane (lane < W); returns logp for the lane's entry.
+template <bool PRECISE>
 __device__ __forceinline__ void head_lsm(float logit, bool m, int lane, int W, float& logp, float& p) {
   const bool in = lane < W;
   const float v = (in && m) ? logit : -INFINITY;
   float mx = dca::wave_max(v);
   const bool any = mx > -INFINITY;
   if (!any) mx = 0.f;
-  const float e = (in && m) ? __expf(logit - mx) : 0.f;
+  const float e = (in && m) ? xexp<PRECISE>(logit - mx) : 0.f;
   float s = dca::wave_sum(e);
   if (!(s > 0.f)) s = 1.f;
-  logp = logit - mx - __logf(s);
-  p = (in && m) ? __expf(logp) : 0.f;
+  logp = logit - mx - xlog<PRECISE>(s);
+  p = (in && m) ? xexp<PRECISE>(logp) : 0.f;
 }
 
-template <bool F32>
+template <bool F32, bool PRECISE>
 __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int n = blockIdx.x * kRowsPerBlock + wv;
@@ -139,7 +147,7 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
       if (in) lg = (h == 3) ? s_tl[wv][lane] : s_zl[wv][hoff[h] + lane];
       mk[h] = in && s_msk[wv][hoff[h] + lane];
       a[h] = (in && s_act[wv][hoff[h] + lane]) ? 1.f : 0.f;
-      head_lsm(lg, mk[h], lane, hw[h], logp[h], pr[h]);
+      head_lsm<PRECISE>(lg, mk[h], lane, hw[h], logp[h], pr[h]);
       if (!in) logp[h] = 0.f;
       const float sh = dca::wave_sum(a[h] * logp[h]);
       sel += sh;
@@ -155,7 +163,7 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
     if (P.algo == 0) {   // PPO
       const float A = A_n;
       const float lr = sel - lpo_n;
-      const float r = __expf(lr);
+      const float r = xexp<PRECISE>(lr);
       const float s1 = r * A;
       const float rc = fminf(fmaxf(r, 1.f - P.clip_eps), 1.f + P.clip_eps);
       const float s2 = rc * A;
@@ -261,11 +269,12 @@ extern "C" hipError_t dca_heads_loss(const float* z, int ldz, const void* emb, c
                                      const float* logp_old, const float* nret, const float* norms, float* dz,
                                      float* dtl, float* part, float* logp_out, int N, int U, int algo,
                                      int compat_value_bug, int S_bug, int B_bug, float clip_eps, float ent_coef,
-                                     float vf_coef, hipStream_t st, short* dz16, int emb_f32) {
+                                     float vf_coef, hipStream_t st, short* dz16, int emb_f32, int precise) {
   if (U > 64 || U < 1 || ldz < kQ + 22 || A != 21 + U) return hipErrorInvalidValue;
   Params P{z, ldz, emb, act, msk, A, adv, ret, logp_old, nret, norms, dz, dtl, part, logp_out, dz16, N, U, algo,
            compat_value_bug, S_bug, B_bug, clip_eps, ent_coef, vf_coef};
-  if (emb_f32) heads_loss_kernel<true><<<dca_heads_loss_nblocks(N), 256, 0, st>>>(P);
-  else heads_loss_kernel<false><<<dca_heads_loss_nblocks(N), 256, 0, st>>>(P);
+  if (emb_f32 && precise) heads_loss_kernel<true, true><<<dca_heads_loss_nblocks(N), 256, 0, st>>>(P);
+  else if (emb_f32) heads_loss_kernel<true, false><<<dca_heads_loss_nblocks(N), 256, 0, st>>>(P);
+  else heads_loss_kernel<false, false><<<dca_heads_loss_nblocks(N), 256, 0, st>>>(P);
   return hipGetLastError();
 }

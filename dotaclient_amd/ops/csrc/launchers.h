@@ -5,9 +5,9 @@
 
 extern "C" {
 
-size_t dca_dpre_dx_lds(int exact);
-hipError_t dca_dpre_dx(const float* dG, const float* wihT, const float* x, const float* wpreT, float* dpre, float* dx,
-                       int N, int K1, int X, int exact, hipStream_t stream);
+hipError_t dca_split_bf16x2(const float* src, short* hi, short* lo, long long n, hipStream_t stream);
+hipError_t dca_dpre_dx(const float* dG, const void* w1h, const void* w1l, const float* x, const void* w2h,
+                       const void* w2l, float* dpre, float* dx, int N, int K1, int X, int exact, hipStream_t stream);
 
 hipError_t dca_adam_step(float* param, const float* grad, float* m, float* v, const int* seg, int64_t n,
                          const float* counts, float* steps, int n_params, float* partials, float* norm_out, float lr,
@@ -32,7 +32,7 @@ hipError_t dca_heads_loss(const float* z, int ldz, const void* emb, const unsign
                           int A, const float* adv, const float* ret, const float* logp_old, const float* nret,
                           const float* norms, float* dz, float* dtl, float* part, float* logp_out, int N, int U,
                           int algo, int compat_value_bug, int S_bug, int B_bug, float clip_eps, float ent_coef,
-                          float vf_coef, hipStream_t st, short* dz16, int emb_f32);
+                          float vf_coef, hipStream_t st, short* dz16, int emb_f32, int precise = 0);
 
 hipError_t dca_encoder_fwd(const float* units, const float* env, const float* w1, const float* b1, const void* wt,
                            const float* bt, const float* we, const float* be, void* x896, void* emb,

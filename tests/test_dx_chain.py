@@ -17,7 +17,14 @@ def test_dpre_dx_matches_fp64(gpu_ops, N, exact):
     x = torch.relu(torch.randn(N, P, device='cuda', generator=g))
     wpreT = torch.randn(X, P, device='cuda', generator=g) * 0.05
     for _ in range(2):
-        dpre, dx = gpu_ops.dpre_dx(dG, wihT, x, wpreT, exact)
+        if exact:
+            e = wihT.new_empty(0)
+            dpre, dx = gpu_ops.dpre_dx(dG, wihT, e, x, wpreT, e)
+        else:
+            w1h, w1l = gpu_ops.split_bf16x2(wihT)
+            w2h, w2l = gpu_ops.split_bf16x2(wpreT)
+            torch.testing.assert_close(w1h.float() + w1l.float(), wihT, rtol=2e-5, atol=0)
+            dpre, dx = gpu_ops.dpre_dx(dG, w1h, w1l, x, w2h, w2l)
         torch.cuda.synchronize()
     ref_pre = (dG.double() @ wihT.double().t()) * (x > 0)
     ref_dx = ref_pre @ wpreT.double().t()
