@@ -364,7 +364,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     with torch.cuda.stream(sL):
         for t0, t1 in spans:
             o = team_fwd(C, xp4[t0:t1], whh16, h_c, c_c, fp.err, False, time_major=True,
-                         hs_out=hs16[t0:t1], cs_out=cs[t0:t1], gates_out=gates4[t0:t1], bias4=bias_p)
+                         hs_out=hs16[t0:t1], cs_out=cs[t0:t1], gates_out=gates4[t0:t1], bias4=bias_p, precise=exact)
             h_c, c_c = o[4], o[5]
             e = torch.cuda.Event()
             e.record(sL)
@@ -441,7 +441,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             cinit = c0.contiguous() if t0 == 0 else cs[t0 - 1]
             o = team_bwd(C, dxh[t0:t1], gates4[t0:t1], cs[t0:t1], cinit, dh_n, dc_n, whh16, fp.err,
                          time_major=True, dg_out=dgates16[t0:t1], dg_bf16=not f32,
-                         want_dbias=True)
+                         want_dbias=True, precise=exact)
             dh_n, dc_n = o[1], o[2]
             db = _acc(db, o[3])
             e = torch.cuda.Event()

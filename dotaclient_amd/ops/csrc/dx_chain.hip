@@ -99,16 +99,32 @@ __device__ __forceinline__ void get_frag(const char* img, int img_bytes, int r, 
     fr.lo = *reinterpret_cast<const bf16x8*>(img + img_bytes + o);
   }
 }
-template <bool EXACT>
-__device__ __forceinline__ f32x4 mma(const Frag& a, const Frag& b, f32x4 c) {
+// all NI × NJ tiles of one slab, one product pass at a time over every tile (the three bf16x3 passes of a tile
+// are dependent on its accumulator; interleaving the tiles keeps the MFMA pipe fed instead of waiting out each
+// accumulator's latency twice per tile)
+template <bool EXACT, int NI, int NJ>
+__device__ __forceinline__ void mma_tiles(const Frag (&fa)[NI], const Frag (&fb)[NJ], f32x4 (&acc)[NI][NJ]) {
   if constexpr (EXACT) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.f[j], b.f[j], c, 0, 0, 0);
-    return c;
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int i = 0; i < NI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i].f[e], fb[j].f[e], acc[i][j], 0, 0, 0);
   } else {
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.lo, b.hi, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.lo, c, 0, 0, 0);
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.hi, b.hi, c, 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].lo, fb[j].hi, acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].hi, fb[j].lo, acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].hi, fb[j].hi, acc[i][j], 0, 0, 0);
   }
 }
 
@@ -193,10 +209,7 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
       for (int i = 0; i < 2; ++i) get_frag<EXACT>(base, L::A1, wr * 32 + i * 16 + r16, q, fa[i]);
 #pragma unroll
       for (int j = 0; j < 4; ++j) get_frag<EXACT>(bb, L::B1, wc * 64 + j * 16 + r16, q, fb[j]);
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = mma<EXACT>(fa[i], fb[j], acc[i][j]);
+      mma_tiles<EXACT, 2, 4>(fa, fb, acc);
       if (ks + 1 < nk) store1((d + 1) % RD, (d + 1) & 1);
       if (ks + RD < nk) load1(d, (ks + RD) * BK);  // slot d held slab ks, stored at the previous iteration
       __syncthreads();
@@ -261,9 +274,9 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
   };
   const int vr = w >> 1, vc = w & 1;             // 4 × 2 waves: rows 16·vr, cols 64·vc of the chunk
   const int nchunk = X / XC, total = nchunk * nk2;   // multiple of RD (nk2 = 8)
-  f32x4 acc2[4];
+  f32x4 acc2[1][4];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int j = 0; j < 4; ++j) acc2[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int d = 0; d < RD; ++d) load2(d, d);
   store2(0, 0);
@@ -274,12 +287,11 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
       const int it = it0 + d;
       const int chunk = it / nk2, ks = it % nk2;
       const char* bb = s2 + (d & 1) * L::S2;
-      Frag fa, fb[4];
-      get_frag<EXACT>(dimg + ks * L::A1, DIMG, vr * 16 + r16, q, fa);
+      Frag fa[1], fb[4];
+      get_frag<EXACT>(dimg + ks * L::A1, DIMG, vr * 16 + r16, q, fa[0]);
 #pragma unroll
       for (int j = 0; j < 4; ++j) get_frag<EXACT>(bb, L::B2, vc * 64 + j * 16 + r16, q, fb[j]);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc2[j] = mma<EXACT>(fa, fb[j], acc2[j]);
+      mma_tiles<EXACT, 1, 4>(fa, fb, acc2);
       if (it + 1 < total) store2((d + 1) % RD, (d + 1) & 1);
       if (it + RD < total) load2(d, it + RD);
       if (ks == nk2 - 1) {                        // chunk done: store its 64 × 128 output tile
@@ -288,9 +300,9 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int grow = r0 + vr * 16 + 4 * q + e;
-            if (grow < N) dx[(size_t)grow * X + chunk * XC + vc * 64 + j * 16 + r16] = acc2[j][e];
+            if (grow < N) dx[(size_t)grow * X + chunk * XC + vc * 64 + j * 16 + r16] = acc2[0][j][e];
           }
-          acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          acc2[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
       __syncthreads();

@@ -146,6 +146,13 @@ __device__ __forceinline__ float row_sum16(float v) {
   return v;
 }
 
+// activations: the fast forms (v_exp_f32 + v_rcp_f32, ≈1e-7 relative) or, in the fp32-exact learner, libm expf /
+// tanhf with IEEE division
+template <bool PREC>
+__device__ __forceinline__ float sigm(float x) { return PREC ? 1.f / (1.f + expf(-x)) : dca::sigmoidf_(x); }
+template <bool PREC>
+__device__ __forceinline__ float tanh_(float x) { return PREC ? tanhf(x) : dca::tanhf_(x); }
+
 // Σ over the 32 lanes of this lane's half-wave (two DPP rows), result in every lane: row sum, then xor 16 by
 // ds_swizzle (bit mode, and 0x1f / xor 0x10 inside each 32-lane group)
 __device__ __forceinline__ float row_sum32(float v) {
@@ -295,13 +302,15 @@ __device__ __forceinline__ void lstm_team_fwd_body(
   constexpr int KSTEP = H / 32;         // k-steps of the full K
   constexpr int HP = H + 8;             // LDS row pitch (bf16)
   constexpr int RB = MT * 16;
-  constexpr bool V1 = VAR >= 1;
-  constexpr int NT = VAR == 2 ? 512 : kThreads;   // threads per workgroup
-  constexpr int LPU = VAR == 2 ? 32 : 16;         // V1/V2: lanes (K slices) per unit
+  constexpr int VV = VAR & 3;                     // variant; VAR & 4: precise (libm-class) activations
+  constexpr bool PREC = (VAR & 4) != 0;
+  constexpr bool V1 = VV >= 1;
+  constexpr int NT = VV == 2 ? 512 : kThreads;    // threads per workgroup
+  constexpr int LPU = VV == 2 ? 32 : 16;          // V1/V2: lanes (K slices) per unit
   constexpr int UPW = 64 / LPU;                   // V1/V2: units per wave
   constexpr int KSL = H / LPU;                    // V1/V2: K slice per lane
   static_assert(!V1 || (F32 && MT == 1), "V1 is the fp32 one-row variant");
-  static_assert(VAR != 2 || H == 512, "V2 maps 8 waves x 2 units onto the 16 units of H = 512");
+  static_assert(VV != 2 || H == 512, "V2 maps 8 waves x 2 units onto the 16 units of H = 512");
   __shared__ short hl[V1 ? 1 : 2][V1 ? 1 : RB][V1 ? 1 : HP];
   __shared__ short hlo[F32 && !V1 ? 2 : 1][F32 && !V1 ? RB : 1][F32 && !V1 ? HP : 1];   // F32: lo bf16 half of h
   // V1: h_{t-1} of row 0 as 16 K slices, each padded by 4 floats (the 16 lanes of a row read 16 different slices
@@ -332,7 +341,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
 
   // W_hh slice for this wave's tile: columns c = 4·ul + q ↔ gate row q·H + j0 + 4·wv + ul, full K, in VGPRs
   // (F32: fp32 W_hh split into hi/lo bf16 fragments once, here)
-  const bool mfma_wave = VAR == 2 || wv < NTILE;
+  const bool mfma_wave = VV == 2 || wv < NTILE;
   const int col = lane & 15, kg = lane >> 4;
   bf16x8 wf[V1 ? 1 : KSTEP];
   bf16x8 wfl[F32 && !V1 ? KSTEP : 1];
@@ -538,9 +547,9 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           // (bias added here, at the use: an add right after the prefetch would wait out the load before the gather)
           const float pi = gq0 + (xv[mt][0] + bv[0]), pf = gq1 + (xv[mt][1] + bv[1]), pg = gq2 + (xv[mt][2] + bv[2]),
                       po = gq3 + (xv[mt][3] + bv[3]);
-          const float ig = dca::sigmoidf_(pi), fg = dca::sigmoidf_(pf), gg = dca::tanhf_(pg), og = dca::sigmoidf_(po);
+          const float ig = sigm<PREC>(pi), fg = sigm<PREC>(pf), gg = tanh_<PREC>(pg), og = sigm<PREC>(po);
           const float c = fg * creg[mt] + ig * gg;
-          const float hv = og * dca::tanhf_(c);
+          const float hv = og * tanh_<PREC>(c);
           if (b < B) { creg[mt] = c; hreg[mt] = hv; }
           TSTAMP(3);
           if constexpr (F32) {
@@ -612,8 +621,10 @@ __device__ __forceinline__ void lstm_team_bwd_body(
     unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart, int knobs) {
   constexpr int H = 128 * KS;
   constexpr int U = H / kT;             // 4·KS units per workgroup (MFMA N, zero-padded to 16)
-  constexpr bool V1 = VAR >= 1;
-  constexpr int NW = VAR == 2 ? 8 : 4;  // waves (K parts)
+  constexpr int VV = VAR & 3;
+  constexpr bool PREC = (VAR & 4) != 0;
+  constexpr bool V1 = VV >= 1;
+  constexpr int NW = VV == 2 ? 8 : 4;   // waves (K parts)
   constexpr int NT = 64 * NW;
   constexpr int KW = 4 * H / NW;        // K (= 4H gate columns) per wave
   constexpr int KSTEP = KW / 32;
@@ -622,7 +633,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
   constexpr int NPAIR = (RB * U + NT - 1) / NT;
   constexpr int KSL = KW / 16;          // V1: K slice per lane of a wave's K part
   static_assert(!V1 || (F32 && MT == 1), "V1 is the fp32 one-row variant");
-  static_assert(VAR != 2 || H == 512, "V2 is the H = 512 variant");
+  static_assert(VV != 2 || H == 512, "V2 is the H = 512 variant");
   __shared__ short dgl[V1 ? 1 : RB][V1 ? 1 : GP];
   __shared__ short dglo[F32 && !V1 ? RB : 1][F32 && !V1 ? GP : 1];   // F32: lo bf16 half of the gathered dG
   // V1: dG_{t+1} of row 0, fp32, as 64 K slices each padded by 4 floats (bank spread, as forward)
@@ -852,7 +863,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
           }
           const float ig = gv[i][0], fg = gv[i][1], gg = gv[i][2], og = gv[i][3];
           const float dht = dv[i] + rec;
-          const float tc = dca::tanhf_(cv[i]);
+          const float tc = tanh_<PREC>(cv[i]);
           const float dc = dcarry[i] + dht * og * (1.f - tc * tc);
           const float d_i = dc * gg * ig * (1.f - ig);
           const float d_f = dc * cpv[i] * fg * (1.f - fg);
@@ -902,7 +913,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
 }
 
 template <int MT, int KS, bool F32, int VAR>
-__global__ __launch_bounds__(VAR == 2 ? 512 : kThreads, 1) void lstm_team_fwd_kernel(
+__global__ __launch_bounds__((VAR & 3) == 2 ? 512 : kThreads, 1) void lstm_team_fwd_kernel(
     const float* __restrict__ xp4, const void* __restrict__ whh, const float* __restrict__ h0,
     const float* __restrict__ c0, short* __restrict__ hs, float* __restrict__ hsf, float* __restrict__ cs,
     float* __restrict__ gates4, float* __restrict__ hn, float* __restrict__ cn, unsigned long long* xg_all,
@@ -915,7 +926,7 @@ __global__ __launch_bounds__(VAR == 2 ? 512 : kThreads, 1) void lstm_team_fwd_ke
 }
 
 template <int MT, int KS, bool F32, int VAR>
-__global__ __launch_bounds__(VAR == 2 ? 512 : kThreads, 1) void lstm_team_bwd_kernel(
+__global__ __launch_bounds__((VAR & 3) == 2 ? 512 : kThreads, 1) void lstm_team_bwd_kernel(
     const float* __restrict__ dhs, const float* __restrict__ gates4, const float* __restrict__ cs,
     const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
     const void* __restrict__ whh, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
@@ -963,19 +974,21 @@ inline void plan(int B, int& nch, int& Bc, int& MT, int f32 = 0) {
     case 0x0114: return __VA_ARGS__(1, 4, true, 0);                                                      \
     case 0x1111: return __VA_ARGS__(1, 1, true, 1);      case 0x1112: return __VA_ARGS__(1, 2, true, 1);      \
     case 0x1114: return __VA_ARGS__(1, 4, true, 1);      case 0x2114: return __VA_ARGS__(1, 4, true, 2);      \
+    case 0x5111: return __VA_ARGS__(1, 1, true, 5);      case 0x5112: return __VA_ARGS__(1, 2, true, 5);      \
+    case 0x5114: return __VA_ARGS__(1, 4, true, 5);      case 0x6114: return __VA_ARGS__(1, 4, true, 6);      \
     default: return hipErrorInvalidValue;                                                                    \
   }
 
 // one-row fp32 chains take the exact VALU variant (DCA_TEAM_V1=0 forces the bf16x3 MFMA one, for comparison); at
 // H = 512 the backward takes its 8-wave form V2 (measured B=8, S=1400: backward 2069 vs 2137 µs, while the 8-wave
 // forward was SLOWER, 2056 vs 1778 µs). DCA_TEAM_V2 = 0 (neither), 1 (both directions), default: backward only.
-inline int use_v1(int f32, int Bc, int H, int backward) {
+inline int use_v1(int f32, int Bc, int H, int backward, int precise) {
   static const int off = [] { const char* e = getenv("DCA_TEAM_V1"); return e && e[0] == '0'; }();
   static const int v2 = [] { const char* e = getenv("DCA_TEAM_V2"); return e ? (e[0] == '0' ? 0 : 3) : 2; }();
   if (!(f32 && Bc == 1 && !off)) return 0;
-  return (H == 512 && (v2 & (backward ? 2 : 1))) ? 2 : 1;
+  return ((H == 512 && (v2 & (backward ? 2 : 1))) ? 2 : 1) | (precise ? 4 : 0);
 }
-inline int team_threads(int var) { return var == 2 ? 512 : kThreads; }
+inline int team_threads(int var) { return (var & 3) == 2 ? 512 : kThreads; }
 
 // Workspace bytes (control block + per-team exchange buffers) for a launch of (B, H).
 extern "C" size_t dca_lstm_team_ctl_bytes() { return 256; }
@@ -1000,7 +1013,7 @@ extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const void* whh, const
                                         short* hs, float* hsf, float* cs, float* gates4, float* hn, float* cn,
                                         void* ctl_mem, void* ws, size_t ws_bytes, unsigned* err, int B, int S, int H,
                                         int time_major, hipStream_t stream, unsigned long long* trace,
-                                        const float* bias4, int f32) {
+                                        const float* bias4, int f32, int precise) {
   if (B < 1 || S < 1 || S >= 65535 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
   if (ws_bytes < dca_lstm_team_workspace(B, H, 0, f32) || ctl_mem == nullptr) return hipErrorInvalidValue;
   if (f32 && hsf == nullptr) return hipErrorInvalidValue;
@@ -1016,7 +1029,7 @@ extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const void* whh, const
                                                                           hn, cn, xg, ctl, err, B, Bc, nch, S, sb, \
                                                                           st, trace, team_knobs(), bias4),         \
    hipGetLastError())
-  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc, H, 0), DCA_F)
+  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc, H, 0, precise), DCA_F)
 #undef DCA_F
 }
 
@@ -1024,7 +1037,7 @@ extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, c
                                         const float* dhn, const float* dcn, const void* whh, float* dgates4,
                                         float* dh0, float* dc0, void* ctl_mem, void* ws, size_t ws_bytes,
                                         unsigned* err, int B, int S, int H, int time_major, hipStream_t stream,
-                                        unsigned long long* trace, short* dg16, float* dbpart, int f32) {
+                                        unsigned long long* trace, short* dg16, float* dbpart, int f32, int precise) {
   if (B < 1 || S < 1 || S >= 65534 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
   if (dgates4 == nullptr && dg16 == nullptr) return hipErrorInvalidValue;
   if (f32 && dgates4 == nullptr) return hipErrorInvalidValue;
@@ -1041,6 +1054,6 @@ extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, c
                                                                           nch, S, sb, st, trace, dg16, dbpart,      \
                                                                           team_knobs()),                           \
    hipGetLastError())
-  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc, H, 1), DCA_B)
+  DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc, H, 1, precise), DCA_B)
 #undef DCA_B
 }
