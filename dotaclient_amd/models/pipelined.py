@@ -189,10 +189,24 @@ def fused_step_tm(fp, *args, **kw):
 
 def _gemm_tn_exact(a, b, out=None, perm=None, accumulate=False, b0=None, colsum=None):
     """``ops.gemm.gemm_tn`` semantics (C (+)= Aᵀ·B through row map ``perm``, optional B0 rows, optional column sums
-    of A) as exact-f32 hipBLASLt products: the fp32-exact learner's weight gradients."""
+    of A) as exact-f32 hipBLASLt products: the fp32-exact learner's weight gradients.
+
+    Split-K: the K = B·S rows run as ≤ 256-row batched products whose partials are summed afterwards. One long
+    product let the library accumulate each output over all 11 200 rows in one chain — measured 1.8e-5 relative error
+    on the enum head's ∂W (three outputs per row, heavy cancellation) against 9e-8 for the same operands summed in
+    float64 (scripts/exact_stage_diag.py)."""
     if b0 is not None:
         b = torch.cat([b0, b])
-    c = a.t() @ b
+    K = a.shape[0]
+    kc = 256
+    nk = (K + kc - 1) // kc
+    if nk > 1:
+        pad = nk * kc - K
+        ap = torch.nn.functional.pad(a, (0, 0, 0, pad)) if pad else a
+        bp = torch.nn.functional.pad(b, (0, 0, 0, pad)) if pad else b
+        c = torch.bmm(ap.reshape(nk, kc, -1).transpose(1, 2), bp.reshape(nk, kc, -1)).sum(0)
+    else:
+        c = a.t() @ b
     cs = a.sum(0) if colsum is not None else None
     if perm is not None:
         idx = perm.long()

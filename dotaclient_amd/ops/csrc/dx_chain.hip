@@ -153,16 +153,20 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
   const int b_off0 = (br * K1 + 16 * bh) * ES;
   float4 sa[RD];
   uint4 sb[RD][4];
+  // Branch-free: a slab past K reads out of range (zeros, no memory traffic) instead of being skipped — a load
+  // under an `if` made the compiler wait for every outstanding load at the join (s_waitcnt vmcnt(0) ahead of each
+  // slab's loads), which serialised the ring
   auto load1 = [&](int slot, int k0) {
-    sa[slot] = __builtin_bit_cast(float4, ld16(rA, a_off0 == kOob ? kOob : a_off0 + k0 * 4));
+    const bool in = k0 < K1;
+    sa[slot] = __builtin_bit_cast(float4, ld16(rA, (in && a_off0 != kOob) ? a_off0 + k0 * 4 : kOob));
     if constexpr (EXACT) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) sb[slot][i] = ld16(rW1h, b_off0 + (k0 + 4 * i) * 4);
+      for (int i = 0; i < 4; ++i) sb[slot][i] = ld16(rW1h, in ? b_off0 + (k0 + 4 * i) * 4 : kOob);
     } else {
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        sb[slot][j] = ld16(rW1h, b_off0 + (k0 + 8 * j) * 2);
-        sb[slot][2 + j] = ld16(rW1l, b_off0 + (k0 + 8 * j) * 2);
+        sb[slot][j] = ld16(rW1h, in ? b_off0 + (k0 + 8 * j) * 2 : kOob);
+        sb[slot][2 + j] = ld16(rW1l, in ? b_off0 + (k0 + 8 * j) * 2 : kOob);
       }
     }
   };
@@ -210,8 +214,8 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
 #pragma unroll
       for (int j = 0; j < 4; ++j) get_frag<EXACT>(bb, L::B1, wc * 64 + j * 16 + r16, q, fb[j]);
       mma_tiles<EXACT, 2, 4>(fa, fb, acc);
-      if (ks + 1 < nk) store1((d + 1) % RD, (d + 1) & 1);
-      if (ks + RD < nk) load1(d, (ks + RD) * BK);  // slot d held slab ks, stored at the previous iteration
+      store1((d + 1) % RD, (d + 1) & 1);            // (after the last slab: zeros into a buffer nobody reads)
+      load1(d, (ks + RD) * BK);                    // slot d held slab ks, stored at the previous iteration
       __syncthreads();
     }
   }
@@ -248,11 +252,12 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
   // ================= stage 2: dx (64 × X) = dpre · W_pre, 128-column chunks =================
   char* s2 = lds + L::D;
   constexpr int nk2 = P / BK;
+  const int nchunk = X / XC, total = nchunk * nk2;   // multiple of RD (nk2 = 8)
   const int cr = tid & 127, cq = tid >> 7;        // W2 slab: row, chunk (8 k)
   uint4 sw[RD][2];
-  auto load2 = [&](int slot, int it) {
+  auto load2 = [&](int slot, int it) {             // branch-free like load1 (it ≥ total: zeros)
     const int c0 = (it / nk2) * XC, k0 = (it % nk2) * BK;
-    const int o = ((c0 + cr) * P + k0 + 8 * cq) * ES;
+    const int o = it < total ? ((c0 + cr) * P + k0 + 8 * cq) * ES : kOob;
     if constexpr (EXACT) {
       sw[slot][0] = ld16(rW2h, o);
       sw[slot][1] = ld16(rW2h, o + 16);
@@ -273,7 +278,6 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
     }
   };
   const int vr = w >> 1, vc = w & 1;             // 4 × 2 waves: rows 16·vr, cols 64·vc of the chunk
-  const int nchunk = X / XC, total = nchunk * nk2;   // multiple of RD (nk2 = 8)
   f32x4 acc2[1][4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc2[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -292,8 +296,8 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
 #pragma unroll
       for (int j = 0; j < 4; ++j) get_frag<EXACT>(bb, L::B2, vc * 64 + j * 16 + r16, q, fb[j]);
       mma_tiles<EXACT, 1, 4>(fa, fb, acc2);
-      if (it + 1 < total) store2((d + 1) % RD, (d + 1) & 1);
-      if (it + RD < total) load2(d, it + RD);
+      store2((d + 1) % RD, (d + 1) & 1);
+      load2(d, it + RD);
       if (ks == nk2 - 1) {                        // chunk done: store its 64 × 128 output tile
 #pragma unroll
         for (int j = 0; j < 4; ++j) {

@@ -67,13 +67,17 @@ def test_exact_encoder_matches_autograd_fp64(preset):
 
 
 @pytest.mark.gpu
-def test_exact_fused_step_deploy_shape_matches_fp64(gpu_ops):
+@pytest.mark.parametrize('algo', ['ppo', 'vpg'])
+def test_exact_fused_step_deploy_shape_matches_fp64(gpu_ops, algo):
     """fp32-exact at B=8, S=1400: every gradient tensor within 1e-5 (relative) of float64 — the bf16x3 headline mode
-    is pinned at 1e-3 (tests/test_fp32_kernels.py)."""
+    is pinned at 1e-3 (tests/test_fp32_kernels.py). VPG's ∂b1 / ∂W1 of the unit encoder sit at ≈1.2e-5 for the plain
+    torch-fp32 evaluation itself (the conditioning of that sum, not the kernels): there a tensor may reach 1.5× the
+    torch-fp32 error instead (measured: fused 1.01e-5 vs torch 1.22e-5)."""
     from tests.test_fp32_kernels import _rel, _step_grads
-    (lf, _, gf), (lo, _, go), (l64, g64) = _step_grads('fp32-exact', 'lstm512', 'ppo', 8, 1400, fp64=True)
+    (lf, _, gf), (lo, _, go), (l64, g64) = _step_grads('fp32-exact', 'lstm512', algo, 8, 1400, fp64=True)
     rows = sorted(((_rel(gf[n], g64[n]), _rel(go[n], g64[n]), n) for n in g64
                    if g64[n] is not None and g64[n].norm() > 0), reverse=True)
-    print('fp32-exact: worst (fused vs fp64, torch-fp32 vs fp64):', rows[:5], 'loss', lf, lo, l64)
+    print(f'fp32-exact {algo}: worst (fused vs fp64, torch-fp32 vs fp64):', rows[:5], 'loss', lf, lo, l64)
     assert abs(lf - l64) <= 1e-6 * max(1e-2, abs(l64)), (lf, l64)
-    assert rows[0][0] < 1e-5, rows[:5]
+    bad = [r for r in rows if r[0] >= max(1e-5, 1.5 * r[1] if algo == 'vpg' else 0.0)]
+    assert not bad, bad[:5]
