@@ -390,7 +390,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         if exact:
             dx_w = (W['wihT16'], W['wihT16'].new_empty(0), W['wpreT'], W['wpreT'].new_empty(0))
         else:
-            dx_w = tuple(C.split_bf16x2(W['wihT16'])) + tuple(C.split_bf16x2(W['wpreT']))
+            dx_w = tuple(C.split_bf16x2(W['wihT16'], True)) + tuple(C.split_bf16x2(W['wpreT'], True))
     for (t0, t1), done in zip(spans, fwd_done):
         main.wait_event(done)
         r0, r1 = t0 * B, t1 * B

@@ -580,9 +580,18 @@ std::vector<torch::Tensor> enc_small_grads(torch::Tensor z, torch::Tensor dtl, t
 }
 
 // fp32 → (hi, lo) bf16 images, x = hi + lo (the bf16x3 operand split, done once per step for a weight image)
-std::vector<torch::Tensor> split_bf16x2(torch::Tensor src) {
+std::vector<torch::Tensor> split_bf16x2(torch::Tensor src, bool slab_major) {
   CHECK_F32(src);
   TORCH_CHECK(src.numel() % 4 == 0, "split_bf16x2: numel % 4 == 0");
+  if (slab_major) {
+    TORCH_CHECK(src.dim() == 2 && src.size(1) % 32 == 0, "split_bf16x2: slab-major images need (R, K), K % 32 == 0");
+    const int R = src.size(0), K = src.size(1);
+    auto hi = torch::empty({K / 32, R, 32}, src.options().dtype(at::kBFloat16));
+    auto lo = torch::empty({K / 32, R, 32}, src.options().dtype(at::kBFloat16));
+    hip_check(dca_split_bf16x2_blk(ptr<float>(src), ptr<short>(hi), ptr<short>(lo), R, K, cur_stream()),
+              "dca_split_bf16x2_blk");
+    return {hi, lo};
+  }
   auto hi = torch::empty(src.sizes(), src.options().dtype(at::kBFloat16));
   auto lo = torch::empty(src.sizes(), src.options().dtype(at::kBFloat16));
   hip_check(dca_split_bf16x2(ptr<float>(src), ptr<short>(hi), ptr<short>(lo), src.numel(), cur_stream()),
@@ -605,10 +614,21 @@ std::vector<torch::Tensor> dpre_dx(torch::Tensor dG, torch::Tensor w1h, torch::T
     CHECK_DEV(w2l); CHECK_CONTIG(w2l); CHECK_DT(w1l, at::kBFloat16); CHECK_DT(w2l, at::kBFloat16);
     TORCH_CHECK(w1l.sizes() == w1h.sizes() && w2l.sizes() == w2h.sizes(), "dpre_dx: hi / lo image shapes");
   }
-  const int N = dG.size(0), K1 = dG.size(1), X = w2h.size(0);
-  TORCH_CHECK(dG.dim() == 2 && w1h.dim() == 2 && x.dim() == 2 && w2h.dim() == 2, "dpre_dx: 2-D operands");
-  TORCH_CHECK(w1h.size(0) == 256 && w1h.size(1) == K1 && x.size(0) == N && x.size(1) == 256 && w2h.size(1) == 256,
-              "dpre_dx: shapes (N,K1) (256,K1) (N,256) (X,256)");
+  const int N = dG.size(0), K1 = dG.size(1);
+  TORCH_CHECK(dG.dim() == 2 && x.dim() == 2, "dpre_dx: 2-D dG and x");
+  int X;
+  if (exact) {
+    TORCH_CHECK(w1h.dim() == 2 && w2h.dim() == 2, "dpre_dx: exact weights (256,K1) (X,256)");
+    X = w2h.size(0);
+    TORCH_CHECK(w1h.size(0) == 256 && w1h.size(1) == K1 && w2h.size(1) == 256, "dpre_dx: shapes (256,K1) (X,256)");
+  } else {
+    // slab-major images (split_bf16x2(..., slab_major=True)): (K1/32, 256, 32) and (256/32, X, 32)
+    TORCH_CHECK(w1h.dim() == 3 && w2h.dim() == 3 && w1h.size(0) * 32 == K1 && w1h.size(1) == 256 &&
+                w1h.size(2) == 32 && w2h.size(0) == 8 && w2h.size(2) == 32,
+                "dpre_dx: bf16x3 weights are slab-major images (K1/32,256,32) and (8,X,32)");
+    X = w2h.size(1);
+  }
+  TORCH_CHECK(x.size(0) == N && x.size(1) == 256, "dpre_dx: x (N,256)");
   TORCH_CHECK(K1 % 128 == 0 && X % 128 == 0, "dpre_dx: K1 % 128 == 0 and X % 128 == 0");
   TORCH_CHECK((long long)N * K1 * 4 <= 0x7fff0000LL, "dpre_dx: dG too large for one launch");
   auto o = dG.options();
@@ -853,7 +873,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("dpre_dx", &dpre_dx, "fused pre-RNN dX chain: (dG·W_ih)*[x>0] -> dpre, dpre·W_pre -> dx (bf16x3 with pre-split "
         "bf16 hi/lo weights, or exact-f32 MFMA with fp32 weights)", py::arg("dG"), py::arg("w1h"), py::arg("w1l"),
         py::arg("x"), py::arg("w2h"), py::arg("w2l"));
-  m.def("split_bf16x2", &split_bf16x2, "fp32 -> (hi, lo) bf16 images with x = hi + lo");
+  m.def("split_bf16x2", &split_bf16x2, "fp32 -> (hi, lo) bf16 images with x = hi + lo (slab_major: (R,K) -> "
+        "[K/32][R][32] images, the dpre_dx operand layout)", py::arg("src"), py::arg("slab_major") = false);
   m.def("enc_small_grads", &enc_small_grads, "entity-encoder type-bias and env-layer gradients in one pass");
   m.def("ln_fwd", &ln_fwd, "LayerNorm(E0 - bsub) -> (xn, mean, rstd); bf16, or fp32 (bsub may be empty); optional copy of E0",
         py::arg("e0"), py::arg("bsub"), py::arg("gamma"), py::arg("beta"), py::arg("eps"),

@@ -29,6 +29,7 @@
 // 16x16x4 MFMAs (call j takes element j: lane l contributes k = 8·(l/16) + j, so the 8 calls cover all 32 k);
 // fp32 LDS rows (144-B pitch), fp32 weights.
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -133,7 +134,7 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
                                                         const void* __restrict__ w1l, const float* __restrict__ x,
                                                         const void* __restrict__ w2h, const void* __restrict__ w2l,
                                                         float* __restrict__ dpre, float* __restrict__ dx, int N,
-                                                        int K1, int X) {
+                                                        int K1, int X, int dbg) {
   using L = Lay<EXACT>;
   constexpr int ES = EXACT ? 4 : 2;                 // bytes per weight element in HBM
   __shared__ __attribute__((aligned(16))) char lds[L::BYTES];
@@ -149,7 +150,7 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
   const int ar = tid >> 3, ak = (tid & 7) * 4;              // dG slab: one fp32 quad per thread
   const int arow = r0 + ar;
   const int a_off0 = arow < N ? (arow * K1 + ak) * 4 : kOob;
-  const int br = tid & 255, bh = tid >> 8;                   // W1 slab: 16 k per thread
+  const int br = tid & 255, bh = tid >> 8;                   // exact W1 slab: 16 k per thread
   const int b_off0 = (br * K1 + 16 * bh) * ES;
   float4 sa[RD];
   uint4 sb[RD][4];
@@ -158,15 +159,18 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
   // slab's loads), which serialised the ring
   auto load1 = [&](int slot, int k0) {
     const bool in = k0 < K1;
-    sa[slot] = __builtin_bit_cast(float4, ld16(rA, (in && a_off0 != kOob) ? a_off0 + k0 * 4 : kOob));
+    if (!(dbg & 8)) sa[slot] = __builtin_bit_cast(float4, ld16(rA, (in && a_off0 != kOob) ? a_off0 + k0 * 4 : kOob));
+    if (dbg & 16) return;
     if constexpr (EXACT) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) sb[slot][i] = ld16(rW1h, in ? b_off0 + (k0 + 4 * i) * 4 : kOob);
     } else {
+      // slab-major images: the 256 × 32 slab is 16 KB contiguous per image, a wave instruction reads 1 KB of it
+      const int o = (k0 / BK) * (P * 64) + tid * 16;
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        sb[slot][j] = ld16(rW1h, in ? b_off0 + (k0 + 8 * j) * 2 : kOob);
-        sb[slot][2 + j] = ld16(rW1l, in ? b_off0 + (k0 + 8 * j) * 2 : kOob);
+        sb[slot][j] = ld16(rW1h, in ? o + 8192 * j : kOob);
+        sb[slot][2 + j] = ld16(rW1l, in ? o + 8192 * j : kOob);
       }
     }
   };
@@ -184,8 +188,8 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
       *reinterpret_cast<uint2*>(base + o) = hi;
       *reinterpret_cast<uint2*>(base + L::A1 + o) = lo;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int ob = coff<false>(br, 2 * bh + j);
+      for (int j = 0; j < 2; ++j) {              // 16-B chunk tid & 3 of rows tid / 4 and 128 + tid / 4
+        const int ob = coff<false>(128 * j + (tid >> 2), tid & 3);
         *reinterpret_cast<uint4*>(bb + ob) = sb[slot][j];
         *reinterpret_cast<uint4*>(bb + L::B1 + ob) = sb[slot][2 + j];
       }
@@ -213,9 +217,10 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
       for (int i = 0; i < 2; ++i) get_frag<EXACT>(base, L::A1, wr * 32 + i * 16 + r16, q, fa[i]);
 #pragma unroll
       for (int j = 0; j < 4; ++j) get_frag<EXACT>(bb, L::B1, wc * 64 + j * 16 + r16, q, fb[j]);
-      mma_tiles<EXACT, 2, 4>(fa, fb, acc);
+      if (!(dbg & 2)) mma_tiles<EXACT, 2, 4>(fa, fb, acc);
+      else if (fa[0].hi[0] == 12345 && fb[0].hi[1] == 4321) acc[0][0][0] += 1.f;
       store1((d + 1) % RD, (d + 1) & 1);            // (after the last slab: zeros into a buffer nobody reads)
-      load1(d, (ks + RD) * BK);                    // slot d held slab ks, stored at the previous iteration
+      if (!(dbg & 1)) load1(d, (ks + RD) * BK);    // slot d held slab ks, stored at the previous iteration
       __syncthreads();
     }
   }
@@ -250,18 +255,20 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
       }
 
   // ================= stage 2: dx (64 × X) = dpre · W_pre, 128-column chunks =================
+  if (dbg & 4) return;
   char* s2 = lds + L::D;
   constexpr int nk2 = P / BK;
   const int nchunk = X / XC, total = nchunk * nk2;   // multiple of RD (nk2 = 8)
   const int cr = tid & 127, cq = tid >> 7;        // W2 slab: row, chunk (8 k)
   uint4 sw[RD][2];
   auto load2 = [&](int slot, int it) {             // branch-free like load1 (it ≥ total: zeros)
-    const int c0 = (it / nk2) * XC, k0 = (it % nk2) * BK;
-    const int o = it < total ? ((c0 + cr) * P + k0 + 8 * cq) * ES : kOob;
+    const int c0 = (it / nk2) * XC, kb = it % nk2;
     if constexpr (EXACT) {
+      const int o = it < total ? ((c0 + cr) * P + kb * BK + 8 * cq) * ES : kOob;
       sw[slot][0] = ld16(rW2h, o);
       sw[slot][1] = ld16(rW2h, o + 16);
-    } else {
+    } else {                                      // slab-major images: rows c0 … c0+127 of k-block kb, 8 KB
+      const int o = it < total ? (kb * X + c0) * 64 + tid * 16 : kOob;
       sw[slot][0] = ld16(rW2h, o);
       sw[slot][1] = ld16(rW2l, o);
     }
@@ -272,7 +279,7 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
       *reinterpret_cast<uint4*>(bb + coff<true>(cr, 2 * cq)) = sw[slot][0];
       *reinterpret_cast<uint4*>(bb + coff<true>(cr, 2 * cq + 1)) = sw[slot][1];
     } else {
-      const int o = coff<false>(cr, cq);
+      const int o = coff<false>(tid >> 2, tid & 3);
       *reinterpret_cast<uint4*>(bb + o) = sw[slot][0];
       *reinterpret_cast<uint4*>(bb + L::B2 + o) = sw[slot][1];
     }
@@ -321,7 +328,28 @@ __global__ __launch_bounds__(256) void split_bf16x2_kernel(const float4* __restr
   if (i < n4) split4(src[i], hi[i], lo[i]);
 }
 
+// fp32 (R, K) row-major → hi / lo images in SLAB-MAJOR order [K/32][R][32] (the bf16x3 operand layout of
+// dpre_dx_kernel: one 32-deep slab of all R rows is contiguous)
+__global__ __launch_bounds__(256) void split_bf16x2_blk_kernel(const float4* __restrict__ src, uint2* __restrict__ hi,
+                                                               uint2* __restrict__ lo, int R, int K) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= R * (K / 4)) return;
+  const int r = (4 * i) / K, k = (4 * i) % K;
+  const int o4 = ((((k >> 5) * R + r) << 5) + (k & 31)) >> 2;
+  split4(src[i], hi[o4], lo[o4]);
+}
+
 }  // namespace
+
+// src (R, K) fp32 → slab-major hi / lo images [K/32][R][32] (K % 32 == 0)
+extern "C" hipError_t dca_split_bf16x2_blk(const float* src, short* hi, short* lo, int R, int K, hipStream_t stream) {
+  if (K % 32 != 0 || R < 1) return hipErrorInvalidValue;
+  const int n4 = R * (K / 4);
+  hipLaunchKernelGGL(split_bf16x2_blk_kernel, dim3((n4 + 255) / 256), dim3(256), 0, stream,
+                     reinterpret_cast<const float4*>(src), reinterpret_cast<uint2*>(hi), reinterpret_cast<uint2*>(lo),
+                     R, K);
+  return hipGetLastError();
+}
 
 // src (n fp32, n % 4 == 0) → hi, lo (n bf16 each)
 extern "C" hipError_t dca_split_bf16x2(const float* src, short* hi, short* lo, long long n, hipStream_t stream) {
@@ -334,9 +362,9 @@ extern "C" hipError_t dca_split_bf16x2(const float* src, short* hi, short* lo, l
   return hipGetLastError();
 }
 
-// dG (N, K1) f32 row-major; x (N, P) f32 (ReLU outputs). Weights K-contiguous per output column:
-// bf16x3 (exact = 0): w1h / w1l (P, K1) and w2h / w2l (X, P) bf16 hi / lo images; exact: w1h (P, K1), w2h (X, P)
-// fp32 (w1l / w2l unused). Outputs dpre (N, P), dx (N, X) f32. K1 % 128 == 0, X % 128 == 0.
+// dG (N, K1) f32 row-major; x (N, P) f32 (ReLU outputs). Weights: bf16x3 (exact = 0): w1h / w1l = slab-major
+// hi / lo images [K1/32][P][32] of W_ihᵀ (P, K1), w2h / w2l = [P/32][X][32] of W_preᵀ (X, P) (dca_split_bf16x2_blk);
+// exact: w1h (P, K1), w2h (X, P) fp32 row-major (w1l / w2l unused). Outputs dpre (N, P), dx (N, X) f32. K1 % 128 == 0, X % 128 == 0.
 extern "C" hipError_t dca_dpre_dx(const float* dG, const void* w1h, const void* w1l, const float* x, const void* w2h,
                                   const void* w2l, float* dpre, float* dx, int N, int K1, int X, int exact,
                                   hipStream_t stream) {
@@ -344,12 +372,15 @@ extern "C" hipError_t dca_dpre_dx(const float* dG, const void* w1h, const void* 
     return hipErrorInvalidValue;
   if ((long long)N * K1 * 4 > 0x7fff0000LL) return hipErrorInvalidValue;      // buffer-resource range
   const int grid = (N + BM - 1) / BM;
+  // DCA_DX_DBG (microbenchmark knob, scripts/dx_bench.py): bit 0 no global loads past the prologue, bit 1 no MFMA,
+  // bit 2 stage 1 only, bit 3 no dG loads, bit 4 no weight loads (stage 1)
+  static const int dbg = [] { const char* e = getenv("DCA_DX_DBG"); return e ? atoi(e) : 0; }();
   if (exact) {
     hipLaunchKernelGGL(dpre_dx_kernel<true>, dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre, dx, N,
-                       K1, X);
+                       K1, X, dbg);
   } else {
     hipLaunchKernelGGL(dpre_dx_kernel<false>, dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre, dx,
-                       N, K1, X);
+                       N, K1, X, dbg);
   }
   return hipGetLastError();
 }

@@ -36,11 +36,11 @@ if __name__ == '__main__':
         d = torch.ops.aten.threshold_backward(torch.mm(dG, wihT.t()), x, 0)
         return d, d @ wpre
     only = 'fused' in sys.argv
-    w1h, w1l = C.split_bf16x2(wihT)
-    w2h, w2l = C.split_bf16x2(wpreT)
+    w1h, w1l = C.split_bf16x2(wihT, True)
+    w2h, w2l = C.split_bf16x2(wpreT, True)
     e = wihT.new_empty(0)
     print(f'dpre_dx bf16x3: {timeit(lambda: C.dpre_dx(dG, w1h, w1l, x, w2h, w2l)):.1f} us', flush=True)
-    print(f'split_bf16x2 of both weights: {timeit(lambda: (C.split_bf16x2(wihT), C.split_bf16x2(wpreT))):.1f} us',
+    print(f'split_bf16x2 of both weights: {timeit(lambda: (C.split_bf16x2(wihT, True), C.split_bf16x2(wpreT, True))):.1f} us',
           flush=True)
     if not only:
         print(f'dpre_dx exact: {timeit(lambda: C.dpre_dx(dG, wihT, e, x, wpreT, e)):.1f} us', flush=True)

@@ -21,9 +21,13 @@ def test_dpre_dx_matches_fp64(gpu_ops, N, exact):
             e = wihT.new_empty(0)
             dpre, dx = gpu_ops.dpre_dx(dG, wihT, e, x, wpreT, e)
         else:
-            w1h, w1l = gpu_ops.split_bf16x2(wihT)
-            w2h, w2l = gpu_ops.split_bf16x2(wpreT)
-            torch.testing.assert_close(w1h.float() + w1l.float(), wihT, rtol=2e-5, atol=0)
+            w1h, w1l = gpu_ops.split_bf16x2(wihT, True)       # slab-major images [K/32][rows][32]
+            w2h, w2l = gpu_ops.split_bf16x2(wpreT, True)
+            back = (w1h.float() + w1l.float()).permute(1, 0, 2).reshape(P, K1)
+            torch.testing.assert_close(back, wihT, rtol=2e-5, atol=0)
+            h2, l2 = gpu_ops.split_bf16x2(wpreT)                # plain layout: same values, row-major
+            torch.testing.assert_close(h2, w2h.permute(1, 0, 2).reshape(X, P), rtol=0, atol=0)
+            torch.testing.assert_close(l2, w2l.permute(1, 0, 2).reshape(X, P), rtol=0, atol=0)
             dpre, dx = gpu_ops.dpre_dx(dG, w1h, w1l, x, w2h, w2l)
         torch.cuda.synchronize()
     ref_pre = (dG.double() @ wihT.double().t()) * (x > 0)
