@@ -18,7 +18,8 @@ Rank 0 prints ONE JSON line. The actor and end-to-end numbers are measured *outs
 EVERY rank (one actor runtime per GPU), and reported as node aggregates (sums over ranks) with per-rank lists:
 
 * ``actor.steps_per_s`` — player-steps/s of the whole self-play runtime (actor/vec.py), ``actor.policy_step_per_s``
-  the batched GPU policy step alone;
+  the batched GPU policy step alone; ``actor.policy_step_fp8_per_s`` the same step on the e4m3 MFMA kernel
+  (BASELINE config 5, actor/batched.py Fp8ActorPolicy) and ``actor.fp8_vs_bf16_policy_step`` their ratio;
 * ``e2e`` — the reference's node topology run for real (learner/e2e.py ``measure_e2e_node``): one experience queue
   per node fed by one actor process per GPU, WORLD_SIZE learner ranks consuming disjoint rollouts (DDP over RCCL),
   rank 0 alone publishing the model. ``e2e.steps_per_s`` is the reference's own metric (optimizer.py:485-486, padded
@@ -231,11 +232,24 @@ def main():
             mine['policy_step_protobuf_featurize_per_s'] = mb['steps_per_s']
         except Exception as e:
             mine['policy_step_error'] = repr(e)
+        try:
+            # BASELINE config 5: the same step with the pre-RNN layer, LSTM step and heads on the hand-written e4m3
+            # MFMA kernel (ops/csrc/actor_fp8.hip; per-channel weight / per-row activation scales) and fp16 / int32
+            # observation staging
+            mb = measure_actor_throughput(policy, device, n_games=args.actor_games, threads=args.actor_threads,
+                                          precision='fp8')
+            mine['policy_step_fp8_per_s'] = mb['gpu_steps_per_s']
+            mine['policy_step_fp8_protobuf_featurize_per_s'] = mb['steps_per_s']
+            if mine.get('policy_step_per_s'):
+                mine['fp8_vs_bf16_policy_step'] = mb['gpu_steps_per_s'] / mine['policy_step_per_s']
+        except Exception as e:
+            mine['policy_step_fp8_error'] = repr(e)
         ranks = gather(mine)
         progress('actor measurements done')
         actor = dict(ranks[0])
         for k in ('steps_per_s', 'protobuf_runtime_steps_per_s', 'policy_step_per_s',
-                  'policy_step_protobuf_featurize_per_s'):
+                  'policy_step_protobuf_featurize_per_s', 'policy_step_fp8_per_s',
+                  'policy_step_fp8_protobuf_featurize_per_s'):
             vals = [r.get(k) for r in ranks]
             if all(v is not None for v in vals):
                 actor[k] = float(sum(vals))

@@ -113,6 +113,15 @@ class GpuActorPolicy:
 
     def _load_weights(self, policy_or_state):
         sd = policy_or_state.state_dict() if isinstance(policy_or_state, torch.nn.Module) else policy_or_state
+        w = self._weight_dict(sd)
+        if not hasattr(self, 'w'):
+            self.w = w
+        else:
+            for k, v in w.items():
+                if isinstance(v, torch.Tensor):
+                    self.w[k].copy_(v)
+
+    def _weight_dict(self, sd) -> Dict[str, torch.Tensor]:
         dev = self.device
         g = (lambda k: sd[k].detach().to(dev, torch.float32))
         bf = (lambda k: sd[k].detach().to(dev, torch.bfloat16))
@@ -145,12 +154,8 @@ class GpuActorPolicy:
         bh = torch.cat([g(f'{k}.bias') for k in heads] + [torch.zeros(LDZ - 150, device=dev)], 0)
         w['whT'] = wh.to(torch.bfloat16).t().contiguous()
         w['bh'] = bh.contiguous()
-        if not hasattr(self, 'w'):
-            self.w = w
-        else:
-            for k, v in w.items():
-                if isinstance(v, torch.Tensor):
-                    self.w[k].copy_(v)
+        w['wh32'] = wh.contiguous()
+        return w
 
     # ------------------------------------------------------------------------------------------------
     def _forward(self):
@@ -275,17 +280,105 @@ class GpuActorPolicy:
              active: Optional[np.ndarray] = None):
         """Synchronous step: (n,3), (n,U,10), (n,U) arrays for all slots; ``reset`` (n,) bool zeroes h/c first;
         ``active`` (n,) bool: only these slots advance their LSTM state (outputs of the others are don't-care)."""
-        self.h_env.numpy()[:] = env
-        self.h_units.numpy()[:] = units
-        self.h_handles.numpy()[:] = handles
+        self.stage(env, units, handles)
         if reset is not None:
             self.h_keep.numpy()[:, 0] = 1.0 - np.asarray(reset, dtype=np.float32)
         self.h_active.numpy()[:] = 1.0 if active is None else np.asarray(active, dtype=np.float32)
         self.step_async()
         return self.wait()
 
+    def stage(self, env: np.ndarray, units: np.ndarray, handles: np.ndarray):
+        """Copy (n,3), (n,U,10), (n,U) host arrays into the pinned staging buffers (torch's vectorised casts: the
+        fp8 step stages fp16 / int32, and numpy's fp32→fp16 cast is several times slower)."""
+        self.h_env.copy_(torch.from_numpy(np.ascontiguousarray(env)))
+        self.h_units.copy_(torch.from_numpy(np.ascontiguousarray(units)))
+        self.h_handles.copy_(torch.from_numpy(np.ascontiguousarray(handles)))
+
     def hidden(self):
         return self.h, self.c
+
+
+def fp8_weight(w: torch.Tensor):
+    """(N, K) fp32 weight → (e4m3fn bytes in MFMA fragment order, (N,) fp32 per-channel dequant scales) for
+    ops/csrc/actor_fp8.hip: each output channel's max |w| maps to 448 (the largest finite e4m3fn); byte order
+    [N/16 column tile][K/64 k-step pair][lane = 16·(k%32 // 8) + n%16][k-step of the pair][k % 8] — one tile's two
+    k-steps are one coalesced 1 KB load of a wave."""
+    N, K = w.shape
+    if N % 16 or K % 64:
+        raise ValueError(f'fp8_weight: ({N}, {K}) must be multiples of (16, 64)')
+    amax = w.abs().amax(1)
+    s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    q = (w / s[:, None]).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).view(torch.uint8)
+    frag = q.view(N // 16, 16, K // 64, 2, 4, 8).permute(0, 2, 4, 1, 3, 5).contiguous()
+    return frag.view(-1), s.float().contiguous()
+
+
+class Fp8ActorPolicy(GpuActorPolicy):
+    """:class:`GpuActorPolicy` with the pre-RNN layer, the LSTM step and the heads as ONE hand-written e4m3 MFMA
+    kernel (ops/csrc/actor_fp8.hip; BASELINE config 5, fp8 actor inference): weights quantised per output channel
+    at (hot-)load time, activations per row inside the kernel. The entity encoder (bf16 MFMA kernel) and the
+    sampling kernel are shared with the bf16 step.
+
+    Compact staging: unit features cross PCIe as fp16 and unit handles as int32 (3.3 + 0.7 MB per 4096-slot step
+    instead of 6.6 + 1.3 MB — the copies were 57 % of the bf16 step), widened on the GPU inside the captured graph.
+    The host-side buffers keep the :class:`GpuActorPolicy` API (``h_units`` / ``h_handles`` numpy views assign with
+    a cast). 1v1 LSTM policies with hidden 512 / pre-RNN 256 (the kernel's shape)."""
+
+    def __init__(self, policy: Policy, n_slots: int, device='cuda', **kw):
+        cfg = policy.config
+        if cfg.rnn != 'lstm' or cfg.hidden != 512 or cfg.pre_rnn_dim != 256 or cfg.entity_attention:
+            raise ValueError('Fp8ActorPolicy: 1v1 LSTM policy with hidden 512, pre-RNN 256')
+        super().__init__(policy, n_slots, device=device, **kw)
+
+    def _alloc(self, inputs_from=None):
+        super()._alloc(inputs_from)
+        n, U, dev = self.n, self.U, self.device
+        if inputs_from is None:
+            self.h_units = torch.zeros(n, U, 10, dtype=torch.float16, pin_memory=True)
+            self.h_handles = torch.full((n, U), -1, dtype=torch.int32, pin_memory=True)
+        elif self.h_units.dtype != torch.float16:
+            raise ValueError('Fp8ActorPolicy: inputs_from must be another Fp8ActorPolicy (compact staging)')
+        self.d_units16 = torch.zeros(n, U, 10, dtype=torch.float16, device=dev)
+        self.d_handles32 = torch.full((n, U), -1, dtype=torch.int32, device=dev)
+        self.z = torch.zeros(n, LDZ, device=dev)
+
+    def _weight_dict(self, sd):
+        w = super()._weight_dict(sd)
+        dev = self.device
+        g = (lambda k: sd[k].detach().to(dev, torch.float32))
+        from ..ops.lstm import gate_perm
+        perm = gate_perm(self.cfg.hidden, dev)
+        w['wpre8'], w['spre'] = fp8_weight(g('affine_pre_rnn.weight'))
+        w['bpre32'] = g('affine_pre_rnn.bias').contiguous()
+        wcat = torch.cat([g('rnn.weight_ih_l0'), g('rnn.weight_hh_l0')], 1)[perm]
+        w['wg8'], w['sg'] = fp8_weight(wcat.contiguous())
+        w['bg'] = (g('rnn.bias_ih_l0') + g('rnn.bias_hh_l0'))[perm].contiguous()
+        w['wh8'], w['sh8'] = fp8_weight(w['wh32'])
+        for k in ('wcatT', 'brnn', 'whT', 'wpreT', 'bpre16'):   # the bf16 step's operands are not used here
+            w.pop(k, None)
+        return w
+
+    def _h2d(self):
+        self.d_env.copy_(self.h_env, non_blocking=True)
+        self.d_units16.copy_(self.h_units, non_blocking=True)
+        self.d_handles32.copy_(self.h_handles, non_blocking=True)
+        self.d_keep.copy_(self.h_keep, non_blocking=True)
+        self.d_active.copy_(self.h_active, non_blocking=True)
+        self.d_units.copy_(self.d_units16)          # widen on the GPU (one elementwise pass each)
+        self.d_handles.copy_(self.d_handles32)
+
+    def _forward(self):
+        """Captured body, 4 launches: encoder → fp8 core (pre-RNN, gates + cell, heads) → sampling → RNG counter."""
+        C, w, cfg = self.C, self.w, self.cfg
+        x896, emb, _ = C.encoder_fwd(self.d_units, self.d_env, w['w1'], w['b1'], w['wt16'], w['bt'], w['we'],
+                                     w['be'], list(cfg.layout.counts), bool(cfg.compat_bugs))
+        if cfg.compat_bugs:
+            x896[:, 768:896] = x896[:, 512:640]
+        C.actor_fp8(x896, w['wpre8'], w['spre'], w['bpre32'], w['wg8'], w['sg'], w['bg'], w['wh8'], w['sh8'],
+                    w['bh'], self.h, self.c, self.d_keep.view(-1), self.z, self.d_active)
+        C.sample_actions(self.z, emb, self.d_handles, self.seed, self.ctr, self.idx, self.act, self.msk, self.logp,
+                         self.value)
+        self.ctr.add_(1)
 
 
 class TorchSlotPolicy:
@@ -354,10 +447,13 @@ class TorchSlotPolicy:
         return self._out
 
 
-def make_slot_policy(policy: Policy, n_slots: int, device='cuda', **kw):
-    """The fused graph-captured :class:`GpuActorPolicy` where it applies, else :class:`TorchSlotPolicy`."""
+def make_slot_policy(policy: Policy, n_slots: int, device='cuda', precision: str = 'bf16', **kw):
+    """The fused graph-captured :class:`GpuActorPolicy` where it applies (``precision='fp8'``:
+    :class:`Fp8ActorPolicy`), else :class:`TorchSlotPolicy`."""
     dev = torch.device(device)
     cfg = policy.config
+    if precision == 'fp8':
+        return Fp8ActorPolicy(policy, n_slots, device=dev, **kw)
     if dev.type == 'cuda' and cfg.unit_dim == 128 and cfg.env_dim == 128 and (
             not cfg.entity_attention or (cfg.layout.max_units == 64 and cfg.attention_heads == 4)):
         return GpuActorPolicy(policy, n_slots, device=dev, **kw)
@@ -395,18 +491,20 @@ def _synthetic_states(n_states: int, seed: int = 0):
 
 
 def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048, steps: int = 50,
-                             warmup: int = 5, featurize: bool = True, threads: int = 8) -> Dict[str, float]:
+                             warmup: int = 5, featurize: bool = True, threads: int = 8,
+                             precision: str = 'bf16') -> Dict[str, float]:
     """Actor steps/s (player-observations → sampled actions per second) of one GPU-resident batched actor.
 
     ``n_games`` 1v1 games = 2·n_games player slots stepped per launch. With ``featurize`` the host side decodes
     and featurizes serialized world states through the native featurizer every step (the reference actor's
     per-step work, agent.py:611-660) overlapped with the previous GPU step; otherwise only the GPU step + copies
-    are timed. Returns ``{'steps_per_s', 'gpu_steps_per_s', 'ms_per_step', 'slots'}``.
+    are timed. ``precision='fp8'``: :class:`Fp8ActorPolicy`. Returns ``{'steps_per_s', 'gpu_steps_per_s',
+    'ms_per_step', 'slots'}``.
     """
     n = 2 * n_games
     dev = torch.device(device)
     layout = policy.config.layout
-    gp = GpuActorPolicy(policy, n, device=dev, seed=1234, record=True)
+    gp = (Fp8ActorPolicy if precision == 'fp8' else GpuActorPolicy)(policy, n, device=dev, seed=1234, record=True)
     feat = None
     if featurize:
         from .. import native
@@ -432,9 +530,7 @@ def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048,
             return env, units, handles, None
 
     def fill(f):
-        gp.h_env.numpy()[:] = f[0]
-        gp.h_units.numpy()[:] = f[1]
-        gp.h_handles.numpy()[:] = f[2]
+        gp.stage(f[0], f[1], f[2])
 
     fill(feat())
     gp.step_async(); gp.wait()

@@ -1,0 +1,362 @@
+// fp8 actor policy core (gfx950, OCP e4m3fn MFMA): one launch from the encoder's pooled features to the head logits
+// of a batch of player slots — the reference actor's per-step policy evaluation (agent.py:641-660 →
+// policy.py:135-158: pre-RNN layer, LSTM step, the five heads), BASELINE config 5 (fp8 actor inference).
+//
+//   x896 (n, 896) bf16  ──►  pre = relu(x·W_preᵀ + b)                       (16 × 256 per workgroup)
+//                      ──►  gates = [pre | h]·[W_ih | W_hh]ᵀ + b_ih + b_hh   (16 × 2048, unit-major gate columns)
+//                      ──►  LSTM cell (c, h fp32 state in place, resets / inactive slots)
+//                      ──►  z = h·W_headsᵀ + b                               (16 × 160 → the sampling kernel)
+//
+// Quantisation. Weights: per output channel, scaled at hot-swap time (actor/batched.py Fp8ActorPolicy) so the
+// channel's max |w| maps to 448, converted by torch to float8_e4m3fn and laid out in MFMA FRAGMENT ORDER
+// [col tile][k-step pair][lane][16 B]: a wave reads one tile's two k-steps as one coalesced 1 KB load and the
+// weights stream from L2 straight into registers (no LDS staging, no reuse inside a workgroup to stage for).
+// Activations: per row, inside the kernel — the row's max |v| over the GEMM's whole K maps to 448 (x896 for the
+// pre-RNN layer; [pre | h] jointly for the gates, fp8 keeps 3 mantissa bits at every exponent so the smaller h
+// values do not need a scale of their own; h for the heads), converted by v_cvt_pk_fp8_f32 (RNE) into an LDS A
+// image. Products run on v_mfma_f32_16x16x32_fp8_fp8 (fp32 accumulation); the epilogue applies
+// scale_row · scale_col + bias. The cell's four gates of a (row, unit) sit in four adjacent lanes of the C layout
+// (unit-major columns); a quad transpose by DPP broadcasts hands each lane one (row, unit).
+//
+// One 512-thread workgroup (8 waves) per 16 slots (n = 4096 slots → 256 workgroups, one per CU). Every workgroup streams all
+// weights (1.8 MB of fp8) from L2 once, half the bytes of the bf16 path's operands, through a 4-deep register ring
+// per wave that runs across the gate stage's chunk boundaries (1 pair of lookahead measured 61 µs for 4096 slots:
+// the stream was latency-bound); the LSTM cell works on c staged in LDS so no global access sits inside the
+// stream, and h / c leave in one coalesced pass.
+#include "common.h"
+
+namespace {
+
+using dca::f32x4;
+
+constexpr int BM = 16, NT = 512, NW = NT / 64, TPR = NT / BM;   // 8 waves; 32 staging threads per row
+constexpr int XD = 896, PD = 256, HD = 512, GD = 4 * HD, KG = PD + HD, ZD = 160;
+constexpr int LDX = XD + 16, LDG = KG + 16, LDF = PD + 4, LDH = HD + 4;   // LDS row pitches (bytes / floats)
+constexpr float kQmax = 448.f;                                          // largest finite e4m3fn
+
+// 8 fp32 → 8 e4m3fn bytes (round to nearest even), element j in byte j: one 16x16x32 fp8 MFMA operand
+__device__ __forceinline__ long long pack8(const float* v) {
+  int lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
+  lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], lo, true);
+  int hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[4], v[5], 0, false);
+  hi = __builtin_amdgcn_cvt_pk_fp8_f32(v[6], v[7], hi, true);
+  return (long long)(unsigned)lo | ((long long)(unsigned)hi << 32);
+}
+
+__device__ __forceinline__ f32x4 mma8(long long a, long long b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, c, 0, 0, 0);
+}
+
+// A fragment of k-step s from a row-major fp8 LDS image: lane l holds A[row l&15][k = 32s + 8(l>>4) + j]
+__device__ __forceinline__ long long afrag(const unsigned char* img, int ld, int s, int lane) {
+  return *reinterpret_cast<const long long*>(img + (lane & 15) * ld + 32 * s + 8 * (lane >> 4));
+}
+
+// one fragment-ordered weight pair (k-steps 2p, 2p+1) of column tile `tile`: 16 B per lane
+__device__ __forceinline__ uint4 bpair(const uint4* __restrict__ w, int ksteps, int tile, int p, int lane) {
+  return w[((size_t)tile * (ksteps / 2) + p) * 64 + lane];
+}
+__device__ __forceinline__ long long lo64(uint4 v) { return (long long)v.x | ((long long)v.y << 32); }
+__device__ __forceinline__ long long hi64(uint4 v) { return (long long)v.z | ((long long)v.w << 32); }
+
+// Streamed weight GEMM: NCH chunks of NTL column tiles (tile of chunk ch, slot i = tile0 + NTL·ch + i, or tile0 +
+// i + 4·ch... via `tile(ch, i)`), each over K = 64·KP (KP k-step pairs). The (chunk, pair) sequence is ONE stream
+// with a D-deep register ring of weight pairs, so the loads of the next chunk are in flight during the epilogue of
+// the current one; the epilogue `epi(ch, acc)` runs after a chunk's last pair (it must not touch global memory:
+// every vector memory op counts in the same in-order vmcnt as the ring's loads).
+template <int NTL, int KP, int NCH, int D, class TileFn, class Epi>
+__device__ __forceinline__ void stream_gemm(const unsigned char* aimg, int lda, const uint4* __restrict__ w,
+                                            TileFn tile, int lane, Epi epi) {
+  static_assert((NCH * KP) % D == 0, "stream length must be a multiple of the ring depth");
+  constexpr int T = NCH * KP;
+  uint4 ring[D][NTL];
+  f32x4 acc[NTL];
+#pragma unroll
+  for (int i = 0; i < NTL; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto issue = [&](int slot, int t) {
+    t = t < T ? t : T - 1;                         // past the end: reload the last pair (never consumed)
+    const int ch = t / KP, p = t - ch * KP;
+#pragma unroll
+    for (int i = 0; i < NTL; ++i) ring[slot][i] = bpair(w, 2 * KP, tile(ch, i), p, lane);
+  };
+#pragma unroll
+  for (int d = 0; d < D; ++d) issue(d, d);
+  for (int t0 = 0; t0 < T; t0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int t = t0 + d, ch = t / KP, p = t - ch * KP;
+      const long long a0 = afrag(aimg, lda, 2 * p, lane), a1 = afrag(aimg, lda, 2 * p + 1, lane);
+#pragma unroll
+      for (int i = 0; i < NTL; ++i) acc[i] = mma8(a0, lo64(ring[d][i]), acc[i]);
+#pragma unroll
+      for (int i = 0; i < NTL; ++i) acc[i] = mma8(a1, hi64(ring[d][i]), acc[i]);
+      issue(d, t + D);
+      if (p == KP - 1) {
+        epi(ch, acc);
+#pragma unroll
+        for (int i = 0; i < NTL; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ float dpp_quad_bcast(float v, int k) {   // lane (lane & ~3) + k of this lane's quad
+  switch (k) {
+    case 0: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x00, 0xF, 0xF, false));
+    case 1: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x55, 0xF, 0xF, false));
+    case 2: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xAA, 0xF, 0xF, false));
+    default: return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xFF, 0xF, 0xF, false));
+  }
+}
+
+struct Fp8Args {
+  const short* x896;                     // (n, 896) bf16
+  const uint4* wpre; const float* spre; const float* bpre;     // 256 × 896, fragment order
+  const uint4* wg; const float* sg; const float* bg;           // 2048 × 768 unit-major rows ([W_ih | W_hh])
+  const uint4* wh; const float* sh; const float* bh;           // 160 × 512 heads
+  float* h; float* c;                    // (n, 512) fp32 state, in place
+  const float* keep; const float* active;
+  float* z;                              // (n, 160) fp32
+  int n;
+};
+
+__global__ __launch_bounds__(NT) void actor_fp8_kernel(Fp8Args A) {
+  __shared__ __attribute__((aligned(16))) unsigned char a8x[BM * LDX];   // x896 fp8, later h fp8 (heads)
+  __shared__ __attribute__((aligned(16))) unsigned char a8g[BM * LDG];   // [pre | h] fp8
+  __shared__ __attribute__((aligned(16))) float xf[BM * LDF];            // pre-RNN output fp32
+  __shared__ __attribute__((aligned(16))) float hn[BM * LDH];            // new h fp32
+  __shared__ __attribute__((aligned(16))) float cs[BM * LDH];            // c·keep, then the new c (active rows)
+  __shared__ float s_row[3][BM];                                         // dequant scales per row
+  __shared__ float s_keep[BM], s_act[BM];
+  // per-column dequant scales and biases (read in the streamed GEMMs' epilogues, which must stay off global memory)
+  __shared__ float col_s[PD + GD + ZD], col_b[PD + GD + ZD];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int q = lane >> 4, cl = lane & 15;
+  const int row0 = blockIdx.x * BM;
+  const int n = A.n;
+  const int r = tid / TPR, sub = tid % TPR;            // staging: TPR threads per row
+  const int grow_r = min(row0 + r, n - 1);
+  const bool row_ok = row0 + r < n;
+
+  // ---- stage 0: x896 row → fp8 (per-row scale); keep / active flags; column scales / biases
+  for (int i = tid; i < PD + GD + ZD; i += NT) {
+    const bool p = i < PD, g = !p && i < PD + GD;
+    const int k = p ? i : (g ? i - PD : i - PD - GD);
+    col_s[i] = p ? A.spre[k] : (g ? A.sg[k] : A.sh[k]);
+    col_b[i] = p ? A.bpre[k] : (g ? A.bg[k] : A.bh[k]);
+  }
+  {
+    if (sub == 0) {
+      s_keep[r] = A.keep[grow_r];
+      s_act[r] = (A.active == nullptr || A.active[grow_r] != 0.f) ? 1.f : 0.f;
+    }
+    constexpr int NCX = (XD / 8 + TPR - 1) / TPR;      // 8-element chunks per thread (the last one partial)
+    float v[NCX][8];
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < NCX; ++i) {
+      const int chk = min(sub + TPR * i, XD / 8 - 1);   // (a duplicate of the last chunk past the row's end)
+      const dca::bf16x8 b = *reinterpret_cast<const dca::bf16x8*>(A.x896 + (size_t)grow_r * XD + 8 * chk);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        v[i][j] = dca::bf2f(b[j]);
+        amax = fmaxf(amax, fabsf(v[i][j]));
+      }
+    }
+    amax = dca::group_max<TPR>(amax);
+    const float qs = amax > 0.f ? kQmax / amax : 1.f;
+    if (sub == 0) s_row[0][r] = amax > 0.f ? amax / kQmax : 1.f;
+#pragma unroll
+    for (int i = 0; i < NCX; ++i) {
+      if (sub + TPR * i >= XD / 8) continue;
+      float t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = v[i][j] * qs;
+      *reinterpret_cast<long long*>(a8x + r * LDX + 8 * (sub + TPR * i)) = pack8(t);
+    }
+  }
+  __syncthreads();
+
+  // ---- stage 1: pre = relu(x·W_preᵀ·scales + b): wave w owns column tiles 2w, 2w+1
+  stream_gemm<2, XD / 64, 1, 2>(
+      a8x, LDX, A.wpre, [&](int, int i) { return 2 * w + i; }, lane, [&](int, const f32x4 (&acc)[2]) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int col = 16 * (2 * w + i) + cl;
+          const float sc = col_s[col], b = col_b[col];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = 4 * q + e;
+            xf[row * LDF + col] = fmaxf(acc[i][e] * s_row[0][row] * sc + b, 0.f);
+          }
+        }
+      });
+  __syncthreads();
+
+  // ---- stage 2: [pre | keep·h_prev] → fp8 with one per-row scale; keep·c_prev → LDS
+  {
+    const float kp = s_keep[r];
+    constexpr int NCP = PD / 8 / TPR, NCH = HD / 8 / TPR;   // 8-element chunks per thread of pre / h
+    float xv[NCP][8], hv[NCH][8];
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < NCP; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        xv[i][j] = xf[r * LDF + 8 * (sub + TPR * i) + j];
+        amax = fmaxf(amax, fabsf(xv[i][j]));
+      }
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      const size_t o = (size_t)grow_r * HD + 8 * (sub + TPR * i);
+      const float4 a = *reinterpret_cast<const float4*>(A.h + o), b = *reinterpret_cast<const float4*>(A.h + o + 4);
+      const float4 ca = *reinterpret_cast<const float4*>(A.c + o), cb = *reinterpret_cast<const float4*>(A.c + o + 4);
+      const float t[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        hv[i][j] = t[j] * kp;
+        amax = fmaxf(amax, fabsf(hv[i][j]));
+      }
+      float* cp = cs + r * LDH + 8 * (sub + TPR * i);
+      *reinterpret_cast<float4*>(cp) = make_float4(ca.x * kp, ca.y * kp, ca.z * kp, ca.w * kp);
+      *reinterpret_cast<float4*>(cp + 4) = make_float4(cb.x * kp, cb.y * kp, cb.z * kp, cb.w * kp);
+    }
+    amax = dca::group_max<TPR>(amax);
+    const float qs = amax > 0.f ? kQmax / amax : 1.f;
+    if (sub == 0) s_row[1][r] = amax > 0.f ? amax / kQmax : 1.f;
+#pragma unroll
+    for (int i = 0; i < NCP; ++i) {
+      float t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = xv[i][j] * qs;
+      *reinterpret_cast<long long*>(a8g + r * LDG + 8 * (sub + TPR * i)) = pack8(t);
+    }
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      float t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = hv[i][j] * qs;
+      *reinterpret_cast<long long*>(a8g + r * LDG + PD + 8 * (sub + TPR * i)) = pack8(t);
+    }
+  }
+  __syncthreads();
+
+  // ---- stage 3: gates (wave w: units 64w … 64w+63 = tiles 16w … 16w+15, 4 chunks of 4) + LSTM cell in LDS
+  stream_gemm<4, KG / 64, 4, 4>(
+      a8g, LDG, A.wg, [&](int ch, int i) { return 16 * w + 4 * ch + i; }, lane,
+      [&](int ch, const f32x4 (&acc)[4]) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int col = 16 * (16 * w + 4 * ch + i) + cl;   // unit-major gate column: unit col/4, gate col%4
+          const float sc = col_s[PD + col], b = col_b[PD + col];
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = acc[i][e] * s_row[1][4 * q + e] * sc + b;
+          // quad transpose: this lane takes row 4q + g (g = its gate index), the 4 gates of its unit at that row
+          const int g = cl & 3;
+          float G[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float sel = 0.f;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const float t = dpp_quad_bcast(v[e], k);
+              sel = g == e ? t : sel;
+            }
+            G[k] = sel;
+          }
+          const int row = 4 * q + g, unit = col >> 2;
+          float* cp = cs + row * LDH + unit;
+          const float ig = dca::sigmoidf_(G[0]), fg = dca::sigmoidf_(G[1]), gg = dca::tanhf_(G[2]),
+                      og = dca::sigmoidf_(G[3]);
+          const float cn = fg * *cp + ig * gg;
+          hn[row * LDH + unit] = og * dca::tanhf_(cn);
+          if (s_act[row] != 0.f) *cp = cn;
+        }
+      });
+  __syncthreads();
+
+  // ---- stage 3b: state out (coalesced rows): active → new h, c; inactive → only this step's reset
+  if (row_ok) {
+    const bool act = s_act[r] != 0.f;
+    const float kp = s_keep[r];
+    if (act || kp != 1.f) {
+#pragma unroll
+      for (int i = 0; i < HD / 8 / TPR; ++i) {
+        const size_t o = (size_t)grow_r * HD + 8 * (sub + TPR * i);
+        const float* cp = cs + r * LDH + 8 * (sub + TPR * i);
+        *reinterpret_cast<float4*>(A.c + o) = *reinterpret_cast<const float4*>(cp);
+        *reinterpret_cast<float4*>(A.c + o + 4) = *reinterpret_cast<const float4*>(cp + 4);
+        if (act) {
+          const float* hp = hn + r * LDH + 8 * (sub + TPR * i);
+          *reinterpret_cast<float4*>(A.h + o) = *reinterpret_cast<const float4*>(hp);
+          *reinterpret_cast<float4*>(A.h + o + 4) = *reinterpret_cast<const float4*>(hp + 4);
+        } else {
+          float4 a = *reinterpret_cast<const float4*>(A.h + o), b = *reinterpret_cast<const float4*>(A.h + o + 4);
+          a.x *= kp; a.y *= kp; a.z *= kp; a.w *= kp; b.x *= kp; b.y *= kp; b.z *= kp; b.w *= kp;
+          *reinterpret_cast<float4*>(A.h + o) = a;
+          *reinterpret_cast<float4*>(A.h + o + 4) = b;
+        }
+      }
+    }
+  }
+
+  // ---- stage 4: new h → fp8 (per-row scale) into the x image's space
+  {
+    constexpr int NCH = HD / 8 / TPR;
+    float hv[NCH][8];
+    float amax = 0.f;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        hv[i][j] = hn[r * LDH + 8 * (sub + TPR * i) + j];
+        amax = fmaxf(amax, fabsf(hv[i][j]));
+      }
+    amax = dca::group_max<TPR>(amax);
+    const float qs = amax > 0.f ? kQmax / amax : 1.f;
+    if (sub == 0) s_row[2][r] = amax > 0.f ? amax / kQmax : 1.f;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      float t[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) t[j] = hv[i][j] * qs;
+      *reinterpret_cast<long long*>(a8x + r * LDX + 8 * (sub + TPR * i)) = pack8(t);
+    }
+  }
+  __syncthreads();
+
+  // ---- stage 5: heads z = h·W_headsᵀ·scales + b (10 column tiles: wave w takes w and w + 8 — waves 2-7 a
+  //      duplicate of their first tile as the second, whose result is dropped)
+  stream_gemm<2, HD / 64, 1, 4>(
+      a8x, LDX, A.wh, [&](int, int i) { return min(w + NW * i, ZD / 16 - 1); }, lane,
+      [&](int, const f32x4 (&acc)[2]) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          if (w + NW * i >= ZD / 16) continue;
+          const int col = 16 * (w + NW * i) + cl;
+          const float sc = col_s[PD + GD + col], b = col_b[PD + GD + col];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int row = 4 * q + e, grow = row0 + row;
+            if (grow < n) A.z[(size_t)grow * ZD + col] = acc[i][e] * s_row[2][row] * sc + b;
+          }
+        }
+      });
+}
+
+}  // namespace
+
+// x896 (n,896) bf16; weights fragment-ordered fp8 (see actor/batched.py fp8_weight) with fp32 per-channel scales and
+// biases: wpre (256×896), wg (2048×768, unit-major rows, [W_ih | W_hh]), wh (160×512); h, c (n,512) fp32 in place;
+// keep (n), active (n or null); z (n,160) fp32.
+extern "C" hipError_t dca_actor_fp8(const short* x896, const void* wpre, const float* spre, const float* bpre,
+                                    const void* wg, const float* sg, const float* bg, const void* wh, const float* sh,
+                                    const float* bh, float* h, float* c, const float* keep, const float* active,
+                                    float* z, int n, hipStream_t stream) {
+  if (n < 1) return hipSuccess;
+  Fp8Args a{x896, reinterpret_cast<const uint4*>(wpre), spre, bpre, reinterpret_cast<const uint4*>(wg), sg, bg,
+            reinterpret_cast<const uint4*>(wh), sh, bh, h, c, keep, active, z, n};
+  hipLaunchKernelGGL(actor_fp8_kernel, dim3((n + BM - 1) / BM), dim3(NT), 0, stream, a);
+  return hipGetLastError();
+}

@@ -399,6 +399,35 @@ void lstm_cell(torch::Tensor gates, torch::Tensor h, torch::Tensor c, torch::Ten
             "dca_lstm_cell");
 }
 
+// fp8 actor policy core (actor_fp8.hip): x896 (n,896) bf16 → pre-RNN → gates + LSTM cell (h, c in place) → z (n,160).
+// Weights are fragment-ordered e4m3fn bytes (uint8) with fp32 per-channel scales (actor/batched.py fp8_weight).
+void actor_fp8(torch::Tensor x896, torch::Tensor wpre, torch::Tensor spre, torch::Tensor bpre, torch::Tensor wg,
+               torch::Tensor sg, torch::Tensor bg, torch::Tensor wh, torch::Tensor sh, torch::Tensor bh,
+               torch::Tensor h, torch::Tensor c, torch::Tensor keep, torch::Tensor z,
+               c10::optional<torch::Tensor> active) {
+  CHECK_BF16(x896); CHECK_U8(wpre); CHECK_U8(wg); CHECK_U8(wh);
+  CHECK_F32(spre); CHECK_F32(bpre); CHECK_F32(sg); CHECK_F32(bg); CHECK_F32(sh); CHECK_F32(bh);
+  CHECK_F32(h); CHECK_F32(c); CHECK_F32(keep); CHECK_F32(z);
+  const int n = x896.size(0);
+  TORCH_CHECK(x896.dim() == 2 && x896.size(1) == 896, "actor_fp8: x896 (n, 896)");
+  TORCH_CHECK(wpre.numel() == 256 * 896 && spre.numel() == 256 && bpre.numel() == 256, "actor_fp8: pre-RNN 256x896");
+  TORCH_CHECK(wg.numel() == 2048 * 768 && sg.numel() == 2048 && bg.numel() == 2048, "actor_fp8: gates 2048x768");
+  TORCH_CHECK(wh.numel() == 160 * 512 && sh.numel() == 160 && bh.numel() == 160, "actor_fp8: heads 160x512");
+  TORCH_CHECK(h.dim() == 2 && h.size(0) == n && h.size(1) == 512 && c.sizes() == h.sizes() && keep.numel() == n,
+              "actor_fp8: h, c (n, 512), keep (n)");
+  TORCH_CHECK(z.dim() == 2 && z.size(0) == n && z.size(1) == 160, "actor_fp8: z (n, 160)");
+  const float* act = nullptr;
+  if (active && active->defined()) {
+    CHECK_F32(*active);
+    TORCH_CHECK(active->numel() == n, "actor_fp8: active (n)");
+    act = ptr<float>(*active);
+  }
+  hip_check(dca_actor_fp8(ptr<short>(x896), wpre.data_ptr(), ptr<float>(spre), ptr<float>(bpre), wg.data_ptr(),
+                          ptr<float>(sg), ptr<float>(bg), wh.data_ptr(), ptr<float>(sh), ptr<float>(bh), ptr<float>(h),
+                          ptr<float>(c), ptr<float>(keep), act, ptr<float>(z), n, cur_stream()),
+            "dca_actor_fp8");
+}
+
 // Returns / advantages over concatenated padded rollouts. rew (L,K) f32 and val (L) f32 (GAE; ignored for mode 0)
 // live on the GPU; the per-segment metadata is host data — off (nseg+1) i32 row offsets, seglen (nseg) i32 valid
 // steps, keys (nseg) i32 team key, boot (nseg) f32 bootstrap values, done (nseg) u8 — validated here and uploaded in
@@ -863,6 +892,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("actor_state_prep", &actor_state_prep, "actor step: state resets + [x | bf16(h)] gate-GEMM operand");
   m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)", py::arg("gates"),
         py::arg("h"), py::arg("c"), py::arg("h16"), py::arg("active") = py::none());
+  m.def("actor_fp8", &actor_fp8, "fp8 (e4m3) actor policy core: pre-RNN + LSTM step + heads from x896",
+        py::arg("x896"), py::arg("wpre"), py::arg("spre"), py::arg("bpre"), py::arg("wg"), py::arg("sg"), py::arg("bg"),
+        py::arg("wh"), py::arg("sh"), py::arg("bh"), py::arg("h"), py::arg("c"), py::arg("keep"), py::arg("z"),
+        py::arg("active") = py::none());
   m.def("loss_prep", &loss_prep, "loss normalisers from one-hot action rows (graph-replayable)");
   m.def("loss_prep_ws_elems", &loss_prep_ws_elems, "int32 workspace elements of loss_prep");
   m.def("loss_assemble", &loss_assemble, "loss scalar + metrics from heads/loss partials");

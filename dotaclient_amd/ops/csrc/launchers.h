@@ -7,6 +7,11 @@ extern "C" {
 
 hipError_t dca_split_bf16x2(const float* src, short* hi, short* lo, long long n, hipStream_t stream);
 hipError_t dca_split_bf16x2_blk(const float* src, short* hi, short* lo, int R, int K, hipStream_t stream);
+// actor_fp8.hip
+hipError_t dca_actor_fp8(const short* x896, const void* wpre, const float* spre, const float* bpre, const void* wg,
+                         const float* sg, const float* bg, const void* wh, const float* sh, const float* bh, float* h,
+                         float* c, const float* keep, const float* active, float* z, int n, hipStream_t stream);
+
 hipError_t dca_dpre_dx(const float* dG, const void* w1h, const void* w1l, const float* x, const void* w2h,
                        const void* w2l, float* dpre, float* dx, int N, int K1, int X, int exact, hipStream_t stream);
 

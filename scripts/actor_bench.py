@@ -1,4 +1,4 @@
-"""Batched GPU actor throughput alone (for rocprofv3): python3 scripts/actor_bench.py [n_games]"""
+"""Batched GPU actor throughput alone (for rocprofv3): python3 scripts/actor_bench.py [n_games] [bf16|fp8]"""
 import json
 import os
 import sys
@@ -12,4 +12,5 @@ from dotaclient_amd.models.policy import Policy, get_config  # noqa: E402
 n_games = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 torch.manual_seed(0)
 policy = Policy(get_config('lstm512'))
-print(json.dumps(measure_actor_throughput(policy, torch.device('cuda:0'), n_games=n_games)))
+prec = sys.argv[2] if len(sys.argv) > 2 else 'bf16'
+print(json.dumps(measure_actor_throughput(policy, torch.device('cuda:0'), n_games=n_games, precision=prec)))

@@ -1,0 +1,104 @@
+"""fp8 actor policy step (ops/csrc/actor_fp8.hip, actor/batched.py Fp8ActorPolicy; BASELINE config 5).
+
+* the e4m3 MFMA core against a torch emulation of the same quantisation (per-channel weight scales, per-row
+  activation scales, fp8 round trip) in fp32 — a wrong fragment map or quad transpose shows as O(1) errors, the
+  tolerance only covers accumulation order and an occasional rounding tie of an intermediate;
+* resets (keep = 0) and inactive slots (state untouched) like the bf16 step;
+* enum-action agreement of the whole graph-captured fp8 step with the bf16 step on the same observations and
+  sampling noise ≥ 99 %.
+The fragment-order weight layout round-trips on the CPU."""
+import numpy as np
+import pytest
+import torch
+
+from dotaclient_amd.actor.batched import fp8_weight
+from dotaclient_amd.models.policy import Policy, get_config
+
+
+def _unfrag(f, s, N, K):
+    q = f.view(N // 16, K // 64, 4, 16, 2, 8).permute(0, 3, 1, 4, 2, 5).reshape(N, K)
+    return q.view(torch.float8_e4m3fn).float() * s[:, None]
+
+
+def test_fp8_weight_fragment_order_roundtrip():
+    torch.manual_seed(0)
+    w = torch.randn(48, 192)
+    f, s = fp8_weight(w)
+    back = _unfrag(f, s, 48, 192)
+    assert float((back - w).abs().max() / w.abs().max()) < 0.07         # e4m3: 3 mantissa bits
+    # exact for values that are e4m3 numbers times the channel scale
+    w2 = torch.tensor([[1.0, -2.0, 0.5, 448.0] * 16] * 16)
+    f2, s2 = fp8_weight(w2)
+    torch.testing.assert_close(_unfrag(f2, s2, 16, 64), w2, rtol=0, atol=0)
+
+
+def _qrows(x):
+    amax = x.abs().amax(1, keepdim=True)
+    s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    return (x / s).to(torch.float8_e4m3fn).float() * s
+
+
+@pytest.mark.gpu
+def test_fp8_core_matches_quantised_emulation(gpu_ops):
+    from dotaclient_amd.actor.batched import Fp8ActorPolicy
+    torch.manual_seed(0)
+    pol = Policy(get_config('lstm512'))
+    n = 100                                          # 7 workgroups, the last one partial
+    gp = Fp8ActorPolicy(pol, n, device='cuda', use_graph=False)
+    w = gp.w
+    g = torch.Generator(device='cuda').manual_seed(1)
+    x896 = torch.relu(torch.randn(n, 896, device='cuda', generator=g)).to(torch.bfloat16)
+    h = torch.randn(n, 512, device='cuda', generator=g) * 0.3
+    c = torch.randn(n, 512, device='cuda', generator=g)
+    keep = torch.ones(n, device='cuda')
+    keep[::7] = 0.0
+    active = torch.ones(n, device='cuda')
+    active[3::11] = 0.0
+    z = torch.empty(n, 160, device='cuda')
+    h1, c1 = h.clone(), c.clone()
+    gpu_ops.actor_fp8(x896, w['wpre8'], w['spre'], w['bpre32'], w['wg8'], w['sg'], w['bg'], w['wh8'], w['sh8'],
+                      w['bh'], h1, c1, keep, z, active)
+    torch.cuda.synchronize()
+    # emulation
+    Wp = _unfrag(w['wpre8'], w['spre'], 256, 896)
+    Wg = _unfrag(w['wg8'], w['sg'], 2048, 768)
+    Wh = _unfrag(w['wh8'], w['sh8'], 160, 512)
+    pre = torch.relu(_qrows(x896.float()) @ Wp.t() + w['bpre32'])
+    hk, ck = h * keep[:, None], c * keep[:, None]
+    a = _qrows(torch.cat([pre, hk], 1))
+    G = (a @ Wg.t() + w['bg']).view(n, 512, 4)              # unit-major gate columns
+    cn = torch.sigmoid(G[..., 1]) * ck + torch.sigmoid(G[..., 0]) * torch.tanh(G[..., 2])
+    hn = torch.sigmoid(G[..., 3]) * torch.tanh(cn)
+    zr = _qrows(hn) @ Wh.t() + w['bh']
+    on = active > 0
+    rel = lambda a_, b_: float((a_ - b_).norm() / b_.norm())   # noqa: E731
+    assert rel(h1[on], hn[on]) < 2e-2, rel(h1[on], hn[on])
+    assert rel(c1[on], cn[on]) < 2e-2, rel(c1[on], cn[on])
+    assert rel(z[:, :150], zr[:, :150]) < 3e-2, rel(z[:, :150], zr[:, :150])
+    # inactive slots: state untouched, except the reset (keep = 0 → zero state) of this step
+    off = ~on
+    torch.testing.assert_close(h1[off], hk[off], rtol=0, atol=0)
+    torch.testing.assert_close(c1[off], ck[off], rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+def test_fp8_policy_enum_agreement_with_bf16(gpu_ops):
+    from dotaclient_amd.actor.batched import Fp8ActorPolicy, GpuActorPolicy
+    torch.manual_seed(0)
+    pol = Policy(get_config('lstm512'))
+    n = 4096
+    U = pol.layout.max_units
+    rng = np.random.default_rng(0)
+    bf = GpuActorPolicy(pol, n, device='cuda', seed=7)
+    f8 = Fp8ActorPolicy(pol, n, device='cuda', seed=7)
+    agree, moves = [], []
+    for _ in range(3):
+        env = rng.standard_normal((n, 3)).astype(np.float32)
+        units = rng.standard_normal((n, U, 10)).astype(np.float32)
+        handles = np.where(rng.random((n, U)) < 0.5, rng.integers(1, 1000, (n, U)), -1).astype(np.int64)
+        o16 = bf.step(env, units, handles)
+        o8 = f8.step(env, units, handles)
+        agree.append(float((o16['idx'][:, 0] == o8['idx'][:, 0]).mean()))
+        moves.append(float((o16['idx'][:, 0] == 1).mean()))
+    print('fp8 vs bf16 enum agreement per step', agree, 'move share', moves)
+    assert min(agree) >= 0.99, agree
