@@ -60,6 +60,8 @@ def parse():
                     help='fp32 = the reference\'s training precision (headline); bf16 = bf16 GEMM operands')
     ap.add_argument('--bf16-extra', type=int, default=1,
                     help='also time the bf16 learner (reported as an extra field, not the headline)')
+    ap.add_argument('--model-5v5-extra', type=int, default=1,
+                    help='also time the 5v5 entity-attention policy (BASELINE config 4) at the same B, S, precision')
     ap.add_argument('--exact-extra', type=int, default=1,
                     help='also time the fp32-exact learner (IEEE fp32 products, no bf16x3 split; extra field)')
     ap.add_argument('--replay', type=int, default=0, help='sequences in the on-HBM replay pool (0 = 4x batch)')
@@ -108,7 +110,7 @@ def main():
     cfg = get_config(args.model)
     trace = os.environ.get('DCA_BENCH_TRACE') == '1'
 
-    def run(precision):
+    def run(precision, cfg=cfg):
         """Build a learner of this precision and time ``args.steps`` DP PPO steps after ``args.warmup``; returns
         (elapsed s (max over ranks), loss_first, loss_last, learner, policy)."""
         torch.manual_seed(7 + rank)
@@ -190,6 +192,19 @@ def main():
                      'value': samples / ex, 'ms_per_step': ex / args.steps * 1e3, 'loss_first': lx0, 'loss_last': lx1}
         except Exception as e:
             exact = {'error': repr(e)}
+
+    model_5v5 = None
+    if args.model_5v5_extra and use_cuda and not cfg.entity_attention:
+        # BASELINE config 4: the 5v5 policy (64 unit slots, pre-LN entity self-attention) through the same fused
+        # learner step, same B, S, precision and DP layout
+        learner = None
+        try:
+            e5, l50, l51, _, _ = run(args.precision, get_config('5v5'))
+            progress(f'learner 5v5 done: {e5 / args.steps * 1e3:.3f} ms/step')
+            model_5v5 = {'model': '5v5', 'precision': args.precision, 'value': samples / e5,
+                         'ms_per_step': e5 / args.steps * 1e3, 'loss_first': l50, 'loss_last': l51}
+        except Exception as e:
+            model_5v5 = {'error': repr(e)}
 
     def gather(x):
         """Every rank's value of ``x`` on every rank (rank order)."""
@@ -309,6 +324,7 @@ def main():
             'loss_first': loss_val, 'loss_last': final_loss,
             'bf16_learner': extra,
             'exact_fp32_learner': exact,
+            'model_5v5': model_5v5,
             'dp_replicas_identical': len(set(shas)) == 1,
             'weights_sha16_per_rank': shas,
             'actor': actor,

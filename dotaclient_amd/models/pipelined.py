@@ -173,6 +173,9 @@ _WG_OVERLAP = os.environ.get('DCA_WG_OVERLAP', '1') != '0'
 # fp32 learner: the ∂X chain ∂pre = (∂G·W_ih)⊙[x>0], ∂x896 = ∂pre·W_pre as ONE hand-written MFMA kernel
 # (ops/csrc/dx_chain.hip) instead of two hipBLASLt GEMMs + a threshold_backward (DCA_DX_FUSED=0: the library path)
 _DX_FUSED = os.environ.get('DCA_DX_FUSED', '1') != '0'
+# fp32 5v5: the entity-attention block forward (LN, QKV, attention, out-projection + residual, pools) as ONE kernel
+# (ops/csrc/attn_block.hip) instead of ln_fwd + hipBLASLt + attn_fwd + hipBLASLt + pool (DCA_ATTN_FUSED=0)
+_ATTN_FUSED = os.environ.get('DCA_ATTN_FUSED', '1') != '0'
 
 
 def fused_step_tm(fp, *args, **kw):
@@ -326,15 +329,25 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         # (E1 = E0' + O·W_outᵀ) and the QKV GEMM runs without its bias epilogue (added by the attention kernels):
         # 213 + 480 µs instead of 359 + 116 (copy, GEMM, bias pass) + 795 µs at N·U = 716 800 rows
         toff = fp.type_offset_list()
-        E0b = emb.view(N * U, 128)
-        E0p = torch.empty_like(E0b)
-        Xn, ln_mu, ln_rs = C.ln_fwd(E0b, W['bout'], P['entity_attn.ln.weight'], P['entity_attn.ln.bias'], 1e-5,
-                                    e0_copy=E0p)
-        QKV = torch.mm(Xn, P['entity_attn.qkv.weight'].detach().t())
         bqkv = P['entity_attn.qkv.bias'].detach()
-        Oat, lse = C.attn_fwd(QKV, bqkv)
-        E1 = E0b.addmm_(Oat, P['entity_attn.out.weight'].detach().t())     # residual + out-projection, in place
-        arg = C.attn_pool(E1, toff, x896, bool(cfg.compat_bugs))            # pools of the attended embeddings
+        if _ATTN_FUSED:
+            # one kernel per step; E0' stays untouched (the LayerNorm backward's input), E1 is a new tensor
+            E0p = emb.view(N * U, 128)
+            wq = C.split_bf16x2(P['entity_attn.qkv.weight'].detach())
+            wo = C.split_bf16x2(P['entity_attn.out.weight'].detach())
+            arg = torch.empty(N, 6, 128, dtype=torch.uint8, device=dev)
+            Xn, ln_mu, ln_rs, QKV, Oat, lse, E1 = C.attn_block_fwd(
+                E0p, W['bout'], P['entity_attn.ln.weight'].detach(), P['entity_attn.ln.bias'].detach(), wq[0], wq[1],
+                bqkv, wo[0], wo[1], toff, x896, arg, bool(cfg.compat_bugs), 1e-5)
+        else:
+            E0b = emb.view(N * U, 128)
+            E0p = torch.empty_like(E0b)
+            Xn, ln_mu, ln_rs = C.ln_fwd(E0b, W['bout'], P['entity_attn.ln.weight'], P['entity_attn.ln.bias'], 1e-5,
+                                        e0_copy=E0p)
+            QKV = torch.mm(Xn, P['entity_attn.qkv.weight'].detach().t())
+            Oat, lse = C.attn_fwd(QKV, bqkv)
+            E1 = E0b.addmm_(Oat, P['entity_attn.out.weight'].detach().t())     # residual + out-projection, in place
+            arg = C.attn_pool(E1, toff, x896, bool(cfg.compat_bugs))            # pools of the attended embeddings
         emb = E1.view(N, U, 128)
     elif attn:
         # 5v5 entity attention (ops/csrc/attn.hip): emb = E0 + b_out here (bias folded into bt)

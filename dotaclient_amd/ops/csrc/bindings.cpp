@@ -428,6 +428,42 @@ void actor_fp8(torch::Tensor x896, torch::Tensor wpre, torch::Tensor spre, torch
             "dca_actor_fp8");
 }
 
+// Fused fp32 entity-attention block forward (attn_block.hip): e0 = E0' (N·64, 128) → xn, mean, rstd, qkv (no bias), o,
+// lse, e1 (all for the backward / heads), and the pools into x896[:, 128:896] + arg (N, 6, 128). Weights: bf16 hi / lo
+// images of W_qkv (384, 128) and W_out (128, 128) (split_bf16x2), bq (384).
+std::vector<torch::Tensor> attn_block_fwd(torch::Tensor e0, torch::Tensor bout, torch::Tensor gamma, torch::Tensor beta,
+                                          torch::Tensor wqh, torch::Tensor wql, torch::Tensor bq, torch::Tensor woh,
+                                          torch::Tensor wol, std::vector<int64_t> type_off, torch::Tensor x896,
+                                          torch::Tensor arg, bool compat, double eps) {
+  CHECK_F32(e0); CHECK_F32(bout); CHECK_F32(gamma); CHECK_F32(beta); CHECK_F32(bq); CHECK_F32(x896); CHECK_U8(arg);
+  CHECK_BF16(wqh); CHECK_BF16(wql); CHECK_BF16(woh); CHECK_BF16(wol);
+  TORCH_CHECK(e0.numel() % (64 * 128) == 0 && e0.size(-1) == 128, "attn_block_fwd: e0 (N·64, 128)");
+  const int64_t N = e0.numel() / (64 * 128);
+  TORCH_CHECK(wqh.numel() == 384 * 128 && wql.numel() == 384 * 128 && woh.numel() == 128 * 128 &&
+              wol.numel() == 128 * 128 && bq.numel() == 384 && bout.numel() == 128 && gamma.numel() == 128 &&
+              beta.numel() == 128, "attn_block_fwd: weight shapes");
+  TORCH_CHECK(x896.dim() == 2 && x896.size(0) == N && x896.size(1) == 896, "attn_block_fwd: x896 (N, 896)");
+  TORCH_CHECK(arg.numel() == N * 6 * 128, "attn_block_fwd: arg (N, 6, 128)");
+  TORCH_CHECK(type_off.size() == 7 && type_off[0] == 0 && type_off[6] == 64, "attn_block_fwd: 7 type offsets 0 … 64");
+  int off[7];
+  for (int i = 0; i < 7; ++i) off[i] = (int)type_off[i];
+  auto o32 = e0.options();
+  auto xn = torch::empty({N * 64, 128}, o32);
+  auto mu = torch::empty({N * 64}, o32);
+  auto rs = torch::empty({N * 64}, o32);
+  auto qkv = torch::empty({N * 64, 384}, o32);
+  auto o = torch::empty({N * 64, 128}, o32);
+  auto lse = torch::empty({N, 4, 64}, o32);
+  auto e1 = torch::empty({N * 64, 128}, o32);
+  hip_check(dca_attn_block_fwd_f32(ptr<float>(e0), ptr<float>(bout), ptr<float>(gamma), ptr<float>(beta),
+                                   ptr<short>(wqh), ptr<short>(wql), ptr<float>(bq), ptr<short>(woh), ptr<short>(wol),
+                                   ptr<float>(xn), ptr<float>(mu), ptr<float>(rs), ptr<float>(qkv), ptr<float>(o),
+                                   ptr<float>(lse), ptr<float>(e1), ptr<float>(x896), ptr<unsigned char>(arg), off,
+                                   compat ? 1 : 0, (int)N, (float)eps, cur_stream()),
+            "dca_attn_block_fwd_f32");
+  return {xn, mu, rs, qkv, o, lse, e1};
+}
+
 // Returns / advantages over concatenated padded rollouts. rew (L,K) f32 and val (L) f32 (GAE; ignored for mode 0)
 // live on the GPU; the per-segment metadata is host data — off (nseg+1) i32 row offsets, seglen (nseg) i32 valid
 // steps, keys (nseg) i32 team key, boot (nseg) f32 bootstrap values, done (nseg) u8 — validated here and uploaded in
@@ -896,6 +932,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x896"), py::arg("wpre"), py::arg("spre"), py::arg("bpre"), py::arg("wg"), py::arg("sg"), py::arg("bg"),
         py::arg("wh"), py::arg("sh"), py::arg("bh"), py::arg("h"), py::arg("c"), py::arg("keep"), py::arg("z"),
         py::arg("active") = py::none());
+  m.def("attn_block_fwd", &attn_block_fwd, "fused fp32 entity-attention block forward: LN + QKV + attention + "
+        "out-projection + residual + pools (-> xn, mean, rstd, qkv, o, lse, e1)");
   m.def("loss_prep", &loss_prep, "loss normalisers from one-hot action rows (graph-replayable)");
   m.def("loss_prep_ws_elems", &loss_prep_ws_elems, "int32 workspace elements of loss_prep");
   m.def("loss_assemble", &loss_assemble, "loss scalar + metrics from heads/loss partials");

@@ -7,6 +7,12 @@ extern "C" {
 
 hipError_t dca_split_bf16x2(const float* src, short* hi, short* lo, long long n, hipStream_t stream);
 hipError_t dca_split_bf16x2_blk(const float* src, short* hi, short* lo, int R, int K, hipStream_t stream);
+// attn_block.hip
+hipError_t dca_attn_block_fwd_f32(const float* e0, const float* bout, const float* gamma, const float* beta,
+                                  const short* wqh, const short* wql, const float* bq, const short* woh,
+                                  const short* wol, float* xn, float* mu, float* rs, float* qkv, float* o, float* lse,
+                                  float* e1, float* x896, unsigned char* arg, const int* off, int compat, int N,
+                                  float eps, hipStream_t stream);
 // actor_fp8.hip
 hipError_t dca_actor_fp8(const short* x896, const void* wpre, const float* spre, const float* bpre, const void* wg,
                          const float* sg, const float* bg, const void* wh, const float* sh, const float* bh, float* h,

@@ -247,3 +247,49 @@ def test_encoder_fwd_matches_fp32(gpu_ops, layout):
             top2 = seg.topk(2, dim=1).values
             clear = (top2[:, 0] - top2[:, 1]) > 2e-2
             assert torch.equal(arg[:, t].long()[clear], am[clear])
+
+
+@pytest.mark.parametrize('compat', [False, True])
+def test_attn_block_fwd_f32_matches_fp64(gpu_ops, compat):
+    """Fused fp32 block forward (ops/csrc/attn_block.hip: LN → QKV → attention → out-projection + residual → pools)
+    against float64 torch ops of the same block, every saved tensor (Xn, stats, QKV without bias, O, LSE, E1) and
+    the pools / argmax."""
+    g = _g(5)
+    e0 = torch.randn(N * U, D, device='cuda', generator=g) * 1.5 + 0.3
+    bout = torch.randn(D, device='cuda', generator=g) * 0.1
+    gamma = 1 + 0.1 * torch.randn(D, device='cuda', generator=g)
+    beta = 0.1 * torch.randn(D, device='cuda', generator=g)
+    wq = torch.randn(3 * D, D, device='cuda', generator=g) * D ** -0.5
+    bq = torch.randn(3 * D, device='cuda', generator=g) * 0.2
+    wo = torch.randn(D, D, device='cuda', generator=g) * D ** -0.5
+    x896 = torch.zeros(N, 896, device='cuda')
+    arg = torch.empty(N, 6, 128, dtype=torch.uint8, device='cuda')
+    qh, ql = gpu_ops.split_bf16x2(wq)
+    oh, ol = gpu_ops.split_bf16x2(wo)
+    xn, mu, rs, qkv, o, lse, e1 = gpu_ops.attn_block_fwd(e0, bout, gamma, beta, qh, ql, bq, oh, ol, TYPE_OFF, x896,
+                                                         arg, compat, 1e-5)
+    torch.cuda.synchronize()
+    d = lambda t: t.double()   # noqa: E731
+    x = d(e0) - d(bout)
+    xr = F.layer_norm(x, (D,), d(gamma), d(beta), 1e-5)
+    qkv_r = xr @ d(wq).t()
+    q, k, v = (qkv_r + d(bq)).view(N, U, 3, NH, HD).unbind(2)
+    q, k, v = (t.transpose(1, 2) for t in (q, k, v))
+    s = q @ k.transpose(-1, -2) / HD ** 0.5
+    o_r = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(N * U, D)
+    e1_r = d(e0) + o_r @ d(wo).t()
+    rel = lambda a, b: float((a.double() - b).norm() / b.norm())   # noqa: E731
+    assert rel(xn, xr) < 1e-6
+    torch.testing.assert_close(mu.double(), x.mean(-1), rtol=1e-5, atol=1e-5)
+    assert rel(qkv, qkv_r) < 2e-5
+    assert rel(o, o_r) < 3e-5
+    torch.testing.assert_close(lse.double(), torch.logsumexp(s, -1), rtol=1e-5, atol=1e-5)
+    assert rel(e1, e1_r) < 2e-5
+    e = e1_r.view(N, U, D)
+    for t in range(6):
+        src = 3 if (compat and t == 5) else t
+        seg = e[:, TYPE_OFF[src]:TYPE_OFF[src + 1]]
+        mx = seg.max(1).values
+        torch.testing.assert_close(x896[:, D + t * D:D + (t + 1) * D].double(), mx, rtol=1e-4, atol=1e-4)
+        got = e1.view(N, U, D)[:, TYPE_OFF[src]:TYPE_OFF[src + 1]].gather(1, arg[:, t].long().unsqueeze(1)).squeeze(1)
+        torch.testing.assert_close(got, x896[:, D + t * D:D + (t + 1) * D], rtol=0, atol=0)   # arg = the kernel's max

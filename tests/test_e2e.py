@@ -24,7 +24,7 @@ def test_e2e_actor_process_over_shm_cpu():
     import glob
     from dotaclient_amd.learner.e2e import measure_e2e_procs
     mine = f'/dev/shm/dca_e2e_{os.getpid()}_*'
-    r = measure_e2e_procs(model='lstm128', device='cpu', duration=60.0, max_iterations=3, games=8, threads=2,
+    r = measure_e2e_procs(model='lstm128', device='cpu', duration=180.0, max_iterations=3, games=8, threads=2,
                           seq_len=64, batch_size=4, seq_per_epoch=8, max_dota_time=20.0, warmup_iterations=1)
     assert r['iterations'] == 3
     assert r['steps_per_s'] > 0 and r['actor_steps_per_s'] > 0
