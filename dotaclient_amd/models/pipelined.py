@@ -125,11 +125,21 @@ class WeightImages:
             parts32['bout'] = (bo, None)
             parts32['ln_g'] = (idx('entity_attn.ln.weight'), None)
             parts32['ln_b'] = (idx('entity_attn.ln.bias'), None)
+        partsS = {}
         if getattr(fp, 'fp32', False):
             # fp32 learner: the GEMM operand images are fp32 gathers too (the HIP kernels split them into bf16 hi/lo
             # pairs themselves, hipBLASLt runs exact f32)
             parts32.update({k: (v, None) for k, v in parts16.items()})
             parts16 = {}
+            # bf16 hi / lo SLAB-MAJOR images [K/32][rows][32] of the chain kernels' weights (ops/csrc/dx_chain.hip):
+            # forward W_pre (256, 896) and W_ih (4H, 256, unit-major rows); ∂X W_ihᵀ (256, 4H) and W_preᵀ (896, 256)
+            def slab(t):
+                return t.reshape(t.shape[0], t.shape[1] // 32, 32).permute(1, 0, 2).contiguous()
+            wpre_i = idx('affine_pre_rnn.weight')
+            wih_i = idx('rnn.weight_ih_l0')[perm]
+            if wpre_i.shape[1] % 128 == 0 and wih_i.shape[0] % 128 == 0:
+                partsS = {'pre_s': slab(wpre_i), 'ih_s': slab(wih_i), 'dx1_s': slab(wih_i.t()),
+                          'dx2_s': slab(wpre_i.t())}
         self.shapes16 = {k: tuple(v.shape) for k, v in parts16.items()}
         self.shapes32 = {k: tuple(v[0].shape) for k, v in parts32.items()}
         m16 = torch.cat([v.reshape(-1) for v in parts16.values()]) if parts16 else torch.zeros(0, dtype=torch.int64)
@@ -141,6 +151,15 @@ class WeightImages:
         self.buf16 = torch.empty(m16.numel(), dtype=torch.bfloat16, device=dev)
         self.buf32 = torch.empty(m32.shape[0], dtype=torch.float32, device=dev)
         self.views: Dict[str, torch.Tensor] = {}
+        self.mapS = self.bufH = self.bufL = None
+        if partsS:
+            self.mapS = torch.cat([v.reshape(-1) for v in partsS.values()]).to(torch.int32).to(dev)
+            self.bufH = torch.empty(self.mapS.numel(), dtype=torch.bfloat16, device=dev)
+            self.bufL = torch.empty_like(self.bufH)
+            o = 0
+            for k, v in partsS.items():
+                self.views[k] = (self.bufH[o:o + v.numel()].view(v.shape), self.bufL[o:o + v.numel()].view(v.shape))
+                o += v.numel()
         o = 0
         for k, shp in self.shapes16.items():
             n = 1
@@ -158,7 +177,10 @@ class WeightImages:
         self.flat = flat
 
     def refresh(self, C) -> Dict[str, torch.Tensor]:
-        C.weight_prep(self.flat, self.map16, self.buf16, self.map32, self.buf32)
+        if self.mapS is not None:
+            C.weight_prep(self.flat, self.map16, self.buf16, self.map32, self.buf32, self.mapS, self.bufH, self.bufL)
+        else:
+            C.weight_prep(self.flat, self.map16, self.buf16, self.map32, self.buf32)
         return self.views
 
 
@@ -176,6 +198,9 @@ _DX_FUSED = os.environ.get('DCA_DX_FUSED', '1') != '0'
 # fp32 5v5: the entity-attention block forward (LN, QKV, attention, out-projection + residual, pools) as ONE kernel
 # (ops/csrc/attn_block.hip) instead of ln_fwd + hipBLASLt + attn_fwd + hipBLASLt + pool (DCA_ATTN_FUSED=0)
 _ATTN_FUSED = os.environ.get('DCA_ATTN_FUSED', '1') != '0'
+# fp32 learner: the forward chain x = relu(x896·W_preᵀ + b), xp = x·W_ihᵀ as ONE hand-written kernel (the ∂X
+# kernel's forward twin, ops/csrc/dx_chain.hip) instead of two hipBLASLt GEMMs (DCA_FWD_CHAIN=0)
+_FWD_CHAIN = os.environ.get('DCA_FWD_CHAIN', '1') != '0'
 
 
 def fused_step_tm(fp, *args, **kw):
@@ -363,8 +388,16 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         x896[:, 768:896] = x896[:, 512:640]
         arg[:, 5] = arg[:, 3]
     # relu(x896·W_preᵀ + b) as ONE hipBLASLt GEMM with a bias+ReLU epilogue, bf16 (fp32) out (x16 > 0 ⟺ x > 0)
-    x16 = torch._addmm_activation(W['bpre16'], x896, wpre16.t())
-    xp4 = _mm(x16, wih16.t()).view(S, B, H, 4)          # the recurrence kernel adds the bias (bias4)
+    if f32 and not exact and _FWD_CHAIN:
+        if 'pre_s' in W:                 # hi / lo images from the step's weight_prep launch
+            fw1, fw2 = W['pre_s'], W['ih_s']
+        else:
+            fw1, fw2 = C.split_bf16x2(wpre16, True), C.split_bf16x2(wih16, True)   # slab-major bf16 hi / lo images
+        x16, xp = C.pre_rnn_chain(x896, fw1[0], fw1[1], W['bpre16'], fw2[0], fw2[1])
+        xp4 = xp.view(S, B, H, 4)
+    else:
+        x16 = torch._addmm_activation(W['bpre16'], x896, wpre16.t())
+        xp4 = _mm(x16, wih16.t()).view(S, B, H, 4)      # the recurrence kernel adds the bias (bias4)
     hs16 = torch.empty(S, B, H, dtype=adt, device=dev)
     cs = torch.empty(S, B, H, device=dev)
     gates4 = torch.empty(S, B, H, 4, device=dev)
@@ -402,6 +435,8 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         # enqueued before the main stream waits on the forward recurrence, so they run beside it
         if exact:
             dx_w = (W['wihT16'], W['wihT16'].new_empty(0), W['wpreT'], W['wpreT'].new_empty(0))
+        elif 'dx1_s' in W:
+            dx_w = tuple(W['dx1_s']) + tuple(W['dx2_s'])
         else:
             dx_w = tuple(C.split_bf16x2(W['wihT16'], True)) + tuple(C.split_bf16x2(W['wpreT'], True))
     for (t0, t1), done in zip(spans, fwd_done):

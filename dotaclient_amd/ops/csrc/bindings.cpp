@@ -555,11 +555,21 @@ void loss_assemble(torch::Tensor part, torch::Tensor norms, int64_t N, int64_t a
 // Working copies of the weights: dst16[i] = bf16(src[map16[i]]) (0 where map16 < 0),
 // dst32[i] = src[map32[i,0]] + src[map32[i,1]] (negative index = 0 term).
 void weight_prep(torch::Tensor src, torch::Tensor map16, torch::Tensor dst16, torch::Tensor map32,
-                 torch::Tensor dst32) {
+                 torch::Tensor dst32, c10::optional<torch::Tensor> maps, c10::optional<torch::Tensor> dsth,
+                 c10::optional<torch::Tensor> dstl) {
   CHECK_F32(src); CHECK_I32(map16); CHECK_BF16(dst16); CHECK_I32(map32); CHECK_F32(dst32);
   TORCH_CHECK(map16.numel() == dst16.numel() && map32.numel() == 2 * dst32.numel(), "weight_prep: map sizes");
+  const int* ms = nullptr;
+  short *dh = nullptr, *dl = nullptr;
+  int ns = 0;
+  if (maps && maps->defined()) {
+    TORCH_CHECK(dsth && dsth->defined() && dstl && dstl->defined(), "weight_prep: split map needs both hi / lo outputs");
+    CHECK_I32(*maps); CHECK_BF16(*dsth); CHECK_BF16(*dstl);
+    TORCH_CHECK(maps->numel() == dsth->numel() && dstl->numel() == dsth->numel(), "weight_prep: split map sizes");
+    ms = ptr<int>(*maps); dh = ptr<short>(*dsth); dl = ptr<short>(*dstl); ns = (int)maps->numel();
+  }
   hip_check(dca_weight_prep(ptr<float>(src), ptr<int>(map16), ptr<short>(dst16), (int)dst16.numel(), ptr<int>(map32),
-                            ptr<float>(dst32), (int)dst32.numel(), cur_stream()),
+                            ptr<float>(dst32), (int)dst32.numel(), ms, dh, dl, ns, cur_stream()),
             "dca_weight_prep");
 }
 
@@ -701,9 +711,33 @@ std::vector<torch::Tensor> dpre_dx(torch::Tensor dG, torch::Tensor w1h, torch::T
   auto dx = torch::empty({N, X}, o);
   hip_check(dca_dpre_dx(ptr<float>(dG), w1h.data_ptr(), exact ? nullptr : w1l.data_ptr(), ptr<float>(x),
                         w2h.data_ptr(), exact ? nullptr : w2l.data_ptr(), ptr<float>(dpre), ptr<float>(dx), N, K1, X,
-                        exact ? 1 : 0, cur_stream()),
+                        exact ? 1 : 0, 0, cur_stream()),
             "dca_dpre_dx");
   return {dpre, dx};
+}
+
+// The forward twin of dpre_dx (same kernel, bias + ReLU epilogue): x = relu(x896·W_preᵀ + b) (N, 256) and
+// xp = x·W_ihᵀ (N, X) in one launch, bf16x3 with slab-major hi / lo weight images (split_bf16x2(w, True) of W_pre
+// (256, K1) and of W_ih (X, 256)).
+std::vector<torch::Tensor> pre_rnn_chain(torch::Tensor x896, torch::Tensor w1h, torch::Tensor w1l, torch::Tensor bias,
+                                         torch::Tensor w2h, torch::Tensor w2l) {
+  CHECK_F32(x896); CHECK_F32(bias);
+  CHECK_BF16(w1h); CHECK_BF16(w1l); CHECK_BF16(w2h); CHECK_BF16(w2l);
+  const int N = x896.size(0), K1 = x896.size(1);
+  TORCH_CHECK(x896.dim() == 2 && bias.numel() == 256, "pre_rnn_chain: x896 (N, K1), bias (256)");
+  TORCH_CHECK(w1h.dim() == 3 && w1h.size(0) * 32 == K1 && w1h.size(1) == 256 && w1h.size(2) == 32 &&
+              w1l.sizes() == w1h.sizes() && w2h.dim() == 3 && w2h.size(0) == 8 && w2h.size(2) == 32 &&
+              w2l.sizes() == w2h.sizes(), "pre_rnn_chain: slab-major images (K1/32,256,32) and (8,X,32)");
+  const int X = w2h.size(1);
+  TORCH_CHECK(K1 % 128 == 0 && X % 128 == 0, "pre_rnn_chain: K1 % 128 == 0 and X % 128 == 0");
+  TORCH_CHECK((long long)N * K1 * 4 <= 0x7fff0000LL, "pre_rnn_chain: x896 too large for one launch");
+  auto o = x896.options();
+  auto x = torch::empty({N, 256}, o);
+  auto xp = torch::empty({N, X}, o);
+  hip_check(dca_dpre_dx(ptr<float>(x896), w1h.data_ptr(), w1l.data_ptr(), ptr<float>(bias), w2h.data_ptr(),
+                        w2l.data_ptr(), ptr<float>(x), ptr<float>(xp), N, K1, X, 0, 1, cur_stream()),
+            "dca_dpre_dx(forward)");
+  return {x, xp};
 }
 
 // ---- 5v5 entity-attention block (ops/csrc/attn.hip); 64 unit slots, width 128, 4 heads × 32 -------------------
@@ -937,13 +971,17 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("loss_prep", &loss_prep, "loss normalisers from one-hot action rows (graph-replayable)");
   m.def("loss_prep_ws_elems", &loss_prep_ws_elems, "int32 workspace elements of loss_prep");
   m.def("loss_assemble", &loss_assemble, "loss scalar + metrics from heads/loss partials");
-  m.def("weight_prep", &weight_prep, "gather the flat fp32 params into bf16 / fp32 working weight images");
+  m.def("weight_prep", &weight_prep, "gather the flat fp32 params into bf16 / fp32 working weight images (+ bf16 "
+        "hi / lo split images)", py::arg("src"), py::arg("map16"), py::arg("dst16"), py::arg("map32"), py::arg("dst32"),
+        py::arg("maps") = py::none(), py::arg("dsth") = py::none(), py::arg("dstl") = py::none());
   m.def("gemm_tn", &gemm_tn, "C (+)= A^T B for K-outer bf16 or fp32 (bf16x3) operands (split-K MFMA, LDS transposed reads)",
         py::arg("A"), py::arg("B"), py::arg("C"), py::arg("perm") = py::none(), py::arg("accumulate") = false,
         py::arg("B0") = py::none(), py::arg("colsum") = py::none());
   m.def("dpre_dx", &dpre_dx, "fused pre-RNN dX chain: (dG·W_ih)*[x>0] -> dpre, dpre·W_pre -> dx (bf16x3 with pre-split "
         "bf16 hi/lo weights, or exact-f32 MFMA with fp32 weights)", py::arg("dG"), py::arg("w1h"), py::arg("w1l"),
         py::arg("x"), py::arg("w2h"), py::arg("w2l"));
+  m.def("pre_rnn_chain", &pre_rnn_chain, "fused forward chain x = relu(x896·W_pre^T + b), xp = x·W_ih^T (bf16x3)",
+        py::arg("x896"), py::arg("w1h"), py::arg("w1l"), py::arg("bias"), py::arg("w2h"), py::arg("w2l"));
   m.def("split_bf16x2", &split_bf16x2, "fp32 -> (hi, lo) bf16 images with x = hi + lo (slab_major: (R,K) -> "
         "[K/32][R][32] images, the dpre_dx operand layout)", py::arg("src"), py::arg("slab_major") = false);
   m.def("enc_small_grads", &enc_small_grads, "entity-encoder type-bias and env-layer gradients in one pass");

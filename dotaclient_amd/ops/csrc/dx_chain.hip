@@ -129,7 +129,9 @@ __device__ __forceinline__ void mma_tiles(const Frag (&fa)[NI], const Frag (&fb)
   }
 }
 
-template <bool EXACT>
+// EPI 0: the ∂X chain's ReLU backward (v = [x > 0]·acc, x the layer's output); EPI 1: the forward chain's bias + ReLU
+// (v = max(acc + b, 0), `x` = the bias (P)) — pre-RNN layer then input projection, x896 → x → x·W_ihᵀ
+template <bool EXACT, int EPI>
 __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict__ dG, const void* __restrict__ w1h,
                                                         const void* __restrict__ w1l, const float* __restrict__ x,
                                                         const void* __restrict__ w2h, const void* __restrict__ w2l,
@@ -239,7 +241,8 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
         const int grow = r0 + row;
         float v = 0.f;
         if (grow < N) {
-          v = x[(size_t)grow * P + col] > 0.f ? acc[i][j][e] : 0.f;
+          if constexpr (EPI == 0) v = x[(size_t)grow * P + col] > 0.f ? acc[i][j][e] : 0.f;
+          else v = fmaxf(acc[i][j][e] + x[col], 0.f);
           dpre[(size_t)grow * P + col] = v;
         }
         const int kk = col & (BK - 1);
@@ -365,9 +368,10 @@ extern "C" hipError_t dca_split_bf16x2(const float* src, short* hi, short* lo, l
 // dG (N, K1) f32 row-major; x (N, P) f32 (ReLU outputs). Weights: bf16x3 (exact = 0): w1h / w1l = slab-major
 // hi / lo images [K1/32][P][32] of W_ihᵀ (P, K1), w2h / w2l = [P/32][X][32] of W_preᵀ (X, P) (dca_split_bf16x2_blk);
 // exact: w1h (P, K1), w2h (X, P) fp32 row-major (w1l / w2l unused). Outputs dpre (N, P), dx (N, X) f32. K1 % 128 == 0, X % 128 == 0.
+// epi = 1: the forward chain (dG = x896, x = the pre-RNN bias (P), dpre = relu(x896·W_preᵀ + b), dx = that · W_ihᵀ).
 extern "C" hipError_t dca_dpre_dx(const float* dG, const void* w1h, const void* w1l, const float* x, const void* w2h,
                                   const void* w2l, float* dpre, float* dx, int N, int K1, int X, int exact,
-                                  hipStream_t stream) {
+                                  int epi, hipStream_t stream) {
   if (N < 1 || K1 < RD * BK || K1 % (RD * BK) != 0 || X < XC || X % XC != 0 || ((X / XC) * (P / BK)) % RD != 0)
     return hipErrorInvalidValue;
   if ((long long)N * K1 * 4 > 0x7fff0000LL) return hipErrorInvalidValue;      // buffer-resource range
@@ -375,12 +379,18 @@ extern "C" hipError_t dca_dpre_dx(const float* dG, const void* w1h, const void* 
   // DCA_DX_DBG (microbenchmark knob, scripts/dx_bench.py): bit 0 no global loads past the prologue, bit 1 no MFMA,
   // bit 2 stage 1 only, bit 3 no dG loads, bit 4 no weight loads (stage 1)
   static const int dbg = [] { const char* e = getenv("DCA_DX_DBG"); return e ? atoi(e) : 0; }();
-  if (exact) {
-    hipLaunchKernelGGL(dpre_dx_kernel<true>, dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre, dx, N,
-                       K1, X, dbg);
-  } else {
-    hipLaunchKernelGGL(dpre_dx_kernel<false>, dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre, dx,
+  if (exact && epi == 0) {
+    hipLaunchKernelGGL((dpre_dx_kernel<true, 0>), dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre, dx,
                        N, K1, X, dbg);
+  } else if (exact) {
+    hipLaunchKernelGGL((dpre_dx_kernel<true, 1>), dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre, dx,
+                       N, K1, X, dbg);
+  } else if (epi == 0) {
+    hipLaunchKernelGGL((dpre_dx_kernel<false, 0>), dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre,
+                       dx, N, K1, X, dbg);
+  } else {
+    hipLaunchKernelGGL((dpre_dx_kernel<false, 1>), dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre,
+                       dx, N, K1, X, dbg);
   }
   return hipGetLastError();
 }

@@ -15,7 +15,8 @@
 //                        field in one launch (was a row-index computation + one index_select per field).
 //   weight_prep_kernel   every per-step working copy of the weights in one gather pass over the flat fp32 buffer:
 //                        bf16 images (stacked / permuted / transposed / zero-padded, via an int32 source map) and
-//                        fp32 images (optionally the sum of two sources: b_ih + b_hh).
+//                        fp32 images (optionally the sum of two sources: b_ih + b_hh), and bf16 hi / lo split images
+//                        (x = hi + lo) for the bf16x3 operands of the fp32 learner's chain kernels.
 #include "common.h"
 
 namespace {
@@ -161,8 +162,16 @@ __global__ __launch_bounds__(kAsmThreads) void loss_assemble_kernel(const float*
 __global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restrict__ src, const int* __restrict__ map16,
                                                           short* __restrict__ dst16, int n16,
                                                           const int2* __restrict__ map32, float* __restrict__ dst32,
-                                                          int n32) {
+                                                          int n32, const int* __restrict__ maps,
+                                                          short* __restrict__ dsth, short* __restrict__ dstl, int ns) {
   const int stride = gridDim.x * blockDim.x;
+  // bf16x3 operand images: x = hi + lo (the slab-major weight images of the fp32 learner's hand-written chains)
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
+    const float v = src[maps[i]];
+    const short h = dca::f2bf(v);
+    dsth[i] = h;
+    dstl[i] = dca::f2bf(v - dca::bf2f(h));
+  }
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += stride) {
     const int m = map16[i];
     dst16[i] = dca::f2bf(m >= 0 ? src[m] : 0.f);
@@ -377,13 +386,15 @@ extern "C" hipError_t dca_loss_assemble(const float* part, int nrows, const floa
 }
 
 extern "C" hipError_t dca_weight_prep(const float* src, const int* map16, short* dst16, int n16, const int* map32,
-                                      float* dst32, int n32, hipStream_t st) {
-  const int n = n16 > n32 ? n16 : n32;
+                                      float* dst32, int n32, const int* maps, short* dsth, short* dstl, int ns,
+                                      hipStream_t st) {
+  int n = n16 > n32 ? n16 : n32;
+  if (ns > n) n = ns;
   int blocks = (n + 255) / 256;
   if (blocks > 2048) blocks = 2048;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(weight_prep_kernel, dim3(blocks), dim3(256), 0, st, src, map16, dst16, n16,
-                     reinterpret_cast<const int2*>(map32), dst32, n32);
+                     reinterpret_cast<const int2*>(map32), dst32, n32, maps, dsth, dstl, ns);
   DCA_CHECK_LAUNCH();
   return hipSuccess;
 }

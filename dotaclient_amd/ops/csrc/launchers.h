@@ -19,7 +19,7 @@ hipError_t dca_actor_fp8(const short* x896, const void* wpre, const float* spre,
                          float* c, const float* keep, const float* active, float* z, int n, hipStream_t stream);
 
 hipError_t dca_dpre_dx(const float* dG, const void* w1h, const void* w1l, const float* x, const void* w2h,
-                       const void* w2l, float* dpre, float* dx, int N, int K1, int X, int exact, hipStream_t stream);
+                       const void* w2l, float* dpre, float* dx, int N, int K1, int X, int exact, int epi, hipStream_t stream);
 
 hipError_t dca_adam_step(float* param, const float* grad, float* m, float* v, const int* seg, int64_t n,
                          const float* counts, float* steps, int n_params, float* partials, float* norm_out, float lr,
@@ -87,7 +87,7 @@ hipError_t dca_loss_prep(const unsigned char* act, int N, int A, int* partial, u
 hipError_t dca_loss_assemble(const float* part, int nrows, const float* norms, int N, int algo, float ent_coef,
                              float vf_coef, float* out, hipStream_t st);
 hipError_t dca_weight_prep(const float* src, const int* map16, short* dst16, int n16, const int* map32, float* dst32,
-                           int n32, hipStream_t st);
+                           int n32, const int* maps, short* dsth, short* dstl, int ns, hipStream_t st);
 
 void dca_gemm_tn_plan(int M, int N, int K, int* splits, int* kc, int* tiles, int f32);
 hipError_t dca_gemm_tn(const void* A, int lda, const void* B, int ldb, const void* B0, int split_rows, float* C,

@@ -37,3 +37,24 @@ def test_dpre_dx_matches_fp64(gpu_ops, N, exact):
         err = (got.double() - ref).abs().max() / ref.abs().max()
         assert err < tol, (float(err), exact)
     assert bool((dpre[x <= 0] == 0).all())                 # the ReLU mask is exact
+
+
+@pytest.mark.parametrize('N', [11200, 1000])
+def test_pre_rnn_chain_matches_fp64(gpu_ops, N):
+    """Forward twin (bias + ReLU epilogue): x = relu(x896·W_preᵀ + b), xp = x·W_ihᵀ at the deploy dims."""
+    g = torch.Generator(device='cuda').manual_seed(N + 1)
+    K1, P, X = 896, 256, 2048
+    x896 = torch.relu(torch.randn(N, K1, device='cuda', generator=g))
+    wpre = torch.randn(P, K1, device='cuda', generator=g) * K1 ** -0.5
+    b = torch.randn(P, device='cuda', generator=g) * 0.1
+    wih = torch.randn(X, P, device='cuda', generator=g) * P ** -0.5
+    w1h, w1l = gpu_ops.split_bf16x2(wpre, True)
+    w2h, w2l = gpu_ops.split_bf16x2(wih, True)
+    x, xp = gpu_ops.pre_rnn_chain(x896, w1h, w1l, b, w2h, w2l)
+    torch.cuda.synchronize()
+    ref_x = torch.relu(x896.double() @ wpre.double().t() + b.double())
+    ref_xp = ref_x @ wih.double().t()
+    for got, ref in ((x, ref_x), (xp, ref_xp)):
+        err = (got.double() - ref).abs().max() / ref.abs().max()
+        assert err < 3e-5, float(err)
+    assert bool((x >= 0).all())
