@@ -322,17 +322,24 @@ class Fp8ActorPolicy(GpuActorPolicy):
     Compact staging: unit features cross PCIe as fp16 and unit handles as int32 (3.3 + 0.7 MB per 4096-slot step
     instead of 6.6 + 1.3 MB — the copies were 57 % of the bf16 step), widened on the GPU inside the captured graph.
     The host-side buffers keep the :class:`GpuActorPolicy` API (``h_units`` / ``h_handles`` numpy views assign with
-    a cast). 1v1 LSTM policies with hidden 512 / pre-RNN 256 (the kernel's shape)."""
+    a cast). ``compact=False`` keeps fp32 / int64 host buffers (the native VecEnv writes those in place: VecActor).
+    1v1 LSTM policies with hidden 512 / pre-RNN 256 (the kernel's shape)."""
 
-    def __init__(self, policy: Policy, n_slots: int, device='cuda', **kw):
+    def __init__(self, policy: Policy, n_slots: int, device='cuda', compact: bool = True, **kw):
         cfg = policy.config
         if cfg.rnn != 'lstm' or cfg.hidden != 512 or cfg.pre_rnn_dim != 256 or cfg.entity_attention:
             raise ValueError('Fp8ActorPolicy: 1v1 LSTM policy with hidden 512, pre-RNN 256')
+        self.compact = bool(compact)
         super().__init__(policy, n_slots, device=device, **kw)
 
     def _alloc(self, inputs_from=None):
         super()._alloc(inputs_from)
         n, U, dev = self.n, self.U, self.device
+        self.z = torch.zeros(n, LDZ, device=dev)
+        if not self.compact:
+            if inputs_from is not None and inputs_from.h_units.dtype != torch.float32:
+                raise ValueError('Fp8ActorPolicy(compact=False): inputs_from must stage fp32 features')
+            return
         if inputs_from is None:
             self.h_units = torch.zeros(n, U, 10, dtype=torch.float16, pin_memory=True)
             self.h_handles = torch.full((n, U), -1, dtype=torch.int32, pin_memory=True)
@@ -340,7 +347,6 @@ class Fp8ActorPolicy(GpuActorPolicy):
             raise ValueError('Fp8ActorPolicy: inputs_from must be another Fp8ActorPolicy (compact staging)')
         self.d_units16 = torch.zeros(n, U, 10, dtype=torch.float16, device=dev)
         self.d_handles32 = torch.full((n, U), -1, dtype=torch.int32, device=dev)
-        self.z = torch.zeros(n, LDZ, device=dev)
 
     def _weight_dict(self, sd):
         w = super()._weight_dict(sd)
@@ -359,6 +365,8 @@ class Fp8ActorPolicy(GpuActorPolicy):
         return w
 
     def _h2d(self):
+        if not self.compact:
+            return super()._h2d()
         self.d_env.copy_(self.h_env, non_blocking=True)
         self.d_units16.copy_(self.h_units, non_blocking=True)
         self.d_handles32.copy_(self.h_handles, non_blocking=True)
@@ -454,6 +462,8 @@ def make_slot_policy(policy: Policy, n_slots: int, device='cuda', precision: str
     cfg = policy.config
     if precision == 'fp8':
         return Fp8ActorPolicy(policy, n_slots, device=dev, **kw)
+    if precision != 'bf16':
+        raise ValueError(f'actor precision must be bf16 or fp8, got {precision!r}')
     if dev.type == 'cuda' and cfg.unit_dim == 128 and cfg.env_dim == 128 and (
             not cfg.entity_attention or (cfg.layout.max_units == 64 and cfg.attention_heads == 4)):
         return GpuActorPolicy(policy, n_slots, device=dev, **kw)

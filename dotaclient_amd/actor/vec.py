@@ -54,7 +54,9 @@ class _Group:
                                    tag=f'{a.tag}{index}', stagger=a.stagger, wire=a.wire)
         self.S = self.ve.slots
         self.ppg = self.ve.players_per_game
-        self.gp = make_slot_policy(a.policy, self.S, device=a.device, seed=seed)
+        # (fp8: fp32 host staging, the native engine writes the buffers in place)
+        fp8 = {'precision': 'fp8', 'compact': False} if a.precision == 'fp8' else {}
+        self.gp = make_slot_policy(a.policy, self.S, device=a.device, seed=seed, **fp8)
         self.env = self.gp.h_env.numpy()
         self.units = self.gp.h_units.numpy()
         self.handles = self.gp.h_handles.numpy()
@@ -80,7 +82,8 @@ class VecActor:
                  mode: str = '1v1', seed: int = 0, rollout_size: int = 10 ** 9, max_dota_time: float = 600.0,
                  latest_weights_prob: float = 1.0, hidden_stride: int = 256, threads: int = 8, groups: int = 2,
                  league=None, opponent_refresh: int = 64, start_time: float = -10.0,
-                 fog: bool = True, tag: str = 'vec', stagger: bool = False, wire: bool = False):
+                 fog: bool = True, tag: str = 'vec', stagger: bool = False, wire: bool = False,
+                 precision: str = 'bf16'):
         from .. import native
         if not native.AVAILABLE:
             raise RuntimeError('VecActor needs the native module (python -m dotaclient_amd.native.build)')
@@ -110,6 +113,10 @@ class VecActor:
         # observations as serialised CMsgBotWorldState protobufs through the native wire decoder + featurizer, and
         # orders as Actions protobufs (the reference actor's observe / act path, agent.py:805-825)
         self.wire = bool(wire)
+        # policy-step precision: bf16 (GpuActorPolicy) or fp8 (Fp8ActorPolicy, BASELINE config 5)
+        if precision not in ('bf16', 'fp8'):
+            raise ValueError(f'precision must be bf16 or fp8, got {precision!r}')
+        self.precision = precision
         groups = max(1, min(int(groups), n_games))
         sizes = [n_games // groups + (1 if i < n_games % groups else 0) for i in range(groups)]
         self.groups = [_Group(self, i, sizes[i], seed * 7919 + i) for i in range(groups)]
@@ -142,8 +149,9 @@ class VecActor:
 
     def _opponent(self, g: _Group, k: int) -> _Opponent:
         while len(g.opp) <= k:
+            fp8 = {'precision': 'fp8', 'compact': False} if self.precision == 'fp8' else {}
             gp = make_slot_policy(self.policy, g.S, device=self.device, seed=g.seed + 104729 * (len(g.opp) + 1),
-                                  inputs_from=g.gp)
+                                  inputs_from=g.gp, **fp8)
             g.opp.append(_Opponent(gp))
         return g.opp[k]
 
@@ -280,7 +288,7 @@ class VecActor:
 
 def measure_vec_actor(policy, device='cuda', n_games: int = 2048, steps: int = 100, warmup: int = 10,
                       threads: int = 8, groups: int = 2, hidden_stride: int = 1400, rollout_size: int = 9999,
-                      max_dota_time: float = 600.0, wire: bool = False) -> Dict[str, float]:
+                      max_dota_time: float = 600.0, wire: bool = False, precision: str = 'bf16') -> Dict[str, float]:
     """Whole-runtime actor throughput: player-steps/s of :class:`VecActor` self-play (engine + featurize + reward +
     GPU policy + trajectory recording + rollout encoding), rollouts counted (published into a sink). Deploy shape
     (params.libsonnet:16-19): whole-game rollouts (``rollout_size`` 9999) of 600 s games, with staggered first
@@ -291,7 +299,7 @@ def measure_vec_actor(policy, device='cuda', n_games: int = 2048, steps: int = 1
     sink = []
     va = VecActor(ws, n_games, lambda b: sink.append(len(b)), device=device, seed=1, threads=threads,
                   groups=groups, hidden_stride=hidden_stride, rollout_size=rollout_size,
-                  max_dota_time=max_dota_time, stagger=True, wire=wire)
+                  max_dota_time=max_dota_time, stagger=True, wire=wire, precision=precision)
     sync = (lambda: torch.cuda.synchronize(va.device)) if va.device.type == 'cuda' else (lambda: None)
     for _ in range(warmup):
         va.step()
@@ -306,4 +314,5 @@ def measure_vec_actor(policy, device='cuda', n_games: int = 2048, steps: int = 1
     return {'steps_per_s': n / dt, 'ms_per_step': dt / steps * 1e3, 'games': n_games,
             'player_steps': n, 'rollouts_per_s': (va.rollouts_sent - r0) / dt,
             'rollout_mb_per_s': sum(sink[k0:]) / dt / 1e6, 'threads': threads, 'groups': groups,
-            'rollout_size': rollout_size, 'wire': wire, 'protobuf_mb_per_s': (va.wire_bytes - w0) / dt / 1e6}
+            'rollout_size': rollout_size, 'wire': wire, 'protobuf_mb_per_s': (va.wire_bytes - w0) / dt / 1e6,
+            'precision': precision}

@@ -55,6 +55,8 @@ def build_parser():
                     help='vec: native vectorised self-play (actor/vec.py, synthetic env only); service: the '
                          'protobuf Actor over DotaService games; auto: vec for synthetic self-play')
     ap.add_argument('--threads', type=int, default=8, help='host threads of the vec runtime')
+    ap.add_argument('--actor-precision', type=str, default='bf16', choices=['bf16', 'fp8'],
+                    help='vec runtime policy step: bf16, or fp8 (e4m3 MFMA kernel; 1v1 LSTM-512 policies)')
     ap.add_argument('--league', type=str, default='oldest', choices=['oldest', 'uniform', 'recent', 'pfsp'],
                     help='opponent sampling over the weight history when not playing the latest weights')
     return ap
@@ -155,7 +157,8 @@ def _run_vec(args, ws, broker, league, device, seed, cfg):
     va = VecActor(ws, args.games, broker.publish_experience, device=device,
                   mode='5v5' if cfg.layout.counts[0] > 1 else '1v1', seed=seed, rollout_size=args.rollout_size,
                   max_dota_time=args.max_dota_time, latest_weights_prob=args.use_latest_weights_prob,
-                  hidden_stride=args.hidden_stride, threads=args.threads, league=league, stagger=True)
+                  hidden_stride=args.hidden_stride, threads=args.threads, league=league, stagger=True,
+                  precision=args.actor_precision)
     try:
         va.run(n_games=args.n_games)
     except Exception:

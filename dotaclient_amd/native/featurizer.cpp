@@ -297,6 +297,17 @@ uint32_t crc32c(py::bytes b) {
   return crc32c_raw((const uint8_t*)buf, (size_t)len);
 }
 
+// CRC-32C of the first n bytes (n < 0: all) of any contiguous buffer (bytes, memoryview, numpy), GIL released —
+// the DCX2 experience-message check on the learner's stager thread runs beside the training thread
+uint32_t crc32c_buf(py::buffer b, py::ssize_t n) {
+  py::buffer_info info = b.request();
+  const py::ssize_t total = info.size * info.itemsize;
+  if (n < 0 || n > total) n = total;
+  const uint8_t* p = static_cast<const uint8_t*>(info.ptr);
+  py::gil_scoped_release nogil;
+  return crc32c_raw(p, (size_t)n);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_native, m) {
@@ -305,6 +316,8 @@ PYBIND11_MODULE(_native, m) {
         py::arg("counts"), py::arg("threads") = 4,
         "Decode CMsgBotWorldState bytes and featurize for (player, team): returns env, units, handles, n_allied_creep");
   m.def("crc32c", &crc32c);
+  m.def("crc32c_buf", &crc32c_buf, py::arg("buf"), py::arg("n") = -1,
+        "CRC-32C of the first n bytes of a contiguous buffer (GIL released)");
   py::class_<PyVecEnv>(m, "VecEnv")
       .def(py::init<int, int, uint64_t, double, long, int, int, std::vector<int>, int, double, bool, bool, double,
                     std::string, bool, bool>(),

@@ -13,8 +13,8 @@ preset                 BASELINE.json config
 ``lstm512-1gpu``       2 — 1v1-mid LSTM-512, batched actor inference + PPO on 1 MI355X
 ``lstm512-8gpu``       3 — 1v1-mid LSTM-512, 8×MI355X data-parallel optimizer (RCCL over xGMI)
 ``5v5-8gpu``           4 — 5v5 entity-attention policy (per-unit embed + max-pool), 8×MI355X DP
-``league-replay``      5 — self-play league (PFSP) + 200 GB on-HBM replay per GPU (fp8 policy GEMMs measured and
-                       dropped: see README)
+``league-replay``      5 — self-play league (PFSP) + 200 GB on-HBM replay per GPU, fp8 actor policy step
+                       (``--actor-precision fp8``: actor/batched.py Fp8ActorPolicy, ops/csrc/actor_fp8.hip)
 =====================  =======================================================================================
 """
 from __future__ import annotations
@@ -67,7 +67,7 @@ PRESETS: Dict[str, RunPreset] = {p.name: p for p in [
     RunPreset('league-replay', 'Self-play league (PFSP opponents) + 200 GB on-HBM replay buffer', 1,
               optimizer=dict(model_preset='lstm512', precision='fp32', replay_gb=200.0, **_DEPLOY),
               agent=dict(model_preset='lstm512', device='cuda', games=1024, runtime='vec', rollout_size=9999,
-                         max_dota_time=600, league='pfsp', use_latest_weights_prob=0.8),
+                         max_dota_time=600, league='pfsp', use_latest_weights_prob=0.8, actor_precision='fp8'),
               bench=dict(model='lstm512', batch_size=8, seq_len=1400, precision='fp32', replay=16384),
               launch=dict(model_preset='lstm512', actors=1, games_per_actor=1024, actor_device='cuda',
                           optimizers=1)),

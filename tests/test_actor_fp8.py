@@ -102,3 +102,18 @@ def test_fp8_policy_enum_agreement_with_bf16(gpu_ops):
         moves.append(float((o16['idx'][:, 0] == 1).mean()))
     print('fp8 vs bf16 enum agreement per step', agree, 'move share', moves)
     assert min(agree) >= 0.99, agree
+
+
+@pytest.mark.gpu
+def test_vec_actor_runs_fp8_policy(gpu_ops):
+    """The self-play runtime on the fp8 step (fp32 host staging written in place by the native engine): rollouts
+    flow, like the bf16 runtime."""
+    from dotaclient_amd import native
+    if not native.AVAILABLE:
+        pytest.skip('native module not built')
+    from dotaclient_amd.actor.vec import measure_vec_actor
+    torch.manual_seed(0)
+    pol = Policy(get_config('lstm512'))
+    r = measure_vec_actor(pol, 'cuda', n_games=64, steps=40, warmup=4, threads=4, rollout_size=16,
+                          max_dota_time=30.0, precision='fp8')
+    assert r['precision'] == 'fp8' and r['steps_per_s'] > 0 and r['rollouts_per_s'] > 0, r
