@@ -306,9 +306,15 @@ class Learner:
         """One DP optimizer step on a minibatch sampled from an on-device replay (``learner.replay.HbmReplay``).
         On the direct fused path the gather itself is part of the captured graph (only the sampled indices are
         copied in)."""
-        idx = replay.sample_indices(B, recent)
+        return self.train_step_indices(replay, replay.sample_indices(B, recent))
+
+    def train_step_indices(self, replay, idx: torch.Tensor) -> Dict[str, torch.Tensor]:
+        """One DP optimizer step on the pool sequences ``idx`` (device int64) of ``replay`` — any object with
+        ``data`` (field → (capacity, S, …) device tensors at fixed addresses), ``S`` and ``gather(idx)``: the HBM
+        replay, or the optimizer's per-iteration pool (epoch permutations over the iteration's sequences)."""
         if not self.direct():
             return self.train_step(replay.gather(idx))
+        B = idx.numel()
         S = replay.S
         if self._graph_ready():
             key = ('replay', id(replay), B, S)

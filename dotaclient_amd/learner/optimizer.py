@@ -106,6 +106,18 @@ class Sequence:
         self.valid = valid
 
 
+class _IterationPool:
+    """Per-iteration sequence pool of the GPU learner (see :meth:`DotaOptimizer._iteration_pool`)."""
+
+    def __init__(self, like: Dict[str, torch.Tensor], capacity: int, S: int):
+        self.capacity, self.S = int(capacity), int(S)
+        self.data = {k: torch.zeros((self.capacity,) + tuple(v.shape[1:]), dtype=v.dtype, device=v.device)
+                     for k, v in like.items()}
+
+    def gather(self, idx: torch.Tensor) -> Dict[str, torch.Tensor]:
+        return {k: v.index_select(0, idx) for k, v in self.data.items()}
+
+
 class DotaOptimizer:
     SPEED_KEY = 'steps per s'
     MAX_TEAMS = 16
@@ -397,6 +409,20 @@ class DotaOptimizer:
                                             pin_memory=pin)
         return buf[:n].view(shape)
 
+    def _iteration_pool(self, data: Dict[str, torch.Tensor], n: int):
+        """The iteration's sequences copied once into a persistent device pool (fixed addresses, so the graph-captured
+        step replays with its gather inside) instead of an ``index_select`` of every field per minibatch followed by
+        the step's own batch-major → time-major copies."""
+        pool = getattr(self, '_pool', None)
+        fields = [k for k in Learner.STEP_FIELDS + ('h0', 'c0') if k in data]
+        if pool is None or pool.capacity < n or set(pool.data) != set(fields) or any(
+                pool.data[k].shape[1:] != data[k].shape[1:] or pool.data[k].dtype != data[k].dtype for k in fields):
+            pool = self._pool = _IterationPool({k: data[k] for k in fields}, max(n, 2 * self.cfg.seq_per_epoch),
+                                               self.cfg.seq_len)
+        for k in fields:
+            pool.data[k][:n].copy_(data[k][:n])
+        return pool
+
     def _sync_running(self):
         """Mirror the device EMA state into the host RunningMeanStd (metrics + checkpoint)."""
         e = self.ema.cpu()
@@ -519,12 +545,17 @@ class DotaOptimizer:
                 losses.append(m['loss'])
                 for k, v in m.items():
                     metrics_acc.setdefault(k, []).append(v)
+        pool = self._iteration_pool(data, n) if (self.replay is None and self.learner.direct()) else None
         for ep in range(cfg.epochs if self.replay is None else 0):
             perm = torch.randperm(n, generator=g)
             for b0 in range(0, n, cfg.batch_size):
                 idx = perm[b0:b0 + cfg.batch_size].to(self.device)
-                batch = {k: v.index_select(0, idx) for k, v in data.items()}
-                m = self.learner.train_step(batch)
+                if pool is not None:
+                    # the captured step gathers its minibatch time-major from the pool itself (replay_gather)
+                    m = self.learner.train_step_indices(pool, idx)
+                else:
+                    batch = {k: v.index_select(0, idx) for k, v in data.items()}
+                    m = self.learner.train_step(batch)
                 losses.append(m['loss'])
                 for k, v in m.items():
                     metrics_acc.setdefault(k, []).append(v)
