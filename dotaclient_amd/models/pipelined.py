@@ -52,6 +52,12 @@ def _addmm(bias, a, b):
     return torch.addmm(bias, a, b) if a.dtype == torch.float32 else torch.addmm(bias, a, b, out_dtype=torch.float32)
 
 
+def _frag_order(w: torch.Tensor) -> torch.Tensor:
+    """(R, K) bf16 → MFMA fragment order [R/16][K/32][lane = 16·(k%32 // 8) + r%16][8] (ops/csrc/attn_block.hip)."""
+    R, K = w.shape
+    return w.view(R // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+
+
 def _acc(a, b):
     """Accumulate a per-chunk gradient: the first chunk's tensor is used as is (no zero fill + add)."""
     return b if a is None else a.add_(b)
@@ -358,8 +364,8 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         if _ATTN_FUSED:
             # one kernel per step; E0' stays untouched (the LayerNorm backward's input), E1 is a new tensor
             E0p = emb.view(N * U, 128)
-            wq = C.split_bf16x2(P['entity_attn.qkv.weight'].detach())
-            wo = C.split_bf16x2(P['entity_attn.out.weight'].detach())
+            wq = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.qkv.weight'].detach())]
+            wo = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.out.weight'].detach())]
             arg = torch.empty(N, 6, 128, dtype=torch.uint8, device=dev)
             Xn, ln_mu, ln_rs, QKV, Oat, lse, E1 = C.attn_block_fwd(
                 E0p, W['bout'], P['entity_attn.ln.weight'].detach(), P['entity_attn.ln.bias'].detach(), wq[0], wq[1],

@@ -15,9 +15,15 @@
 //   D  E1 = E0' + O·W_outᵀ (16x16x32, wave w: output columns 32w … 32w+31) → HBM (the heads' pointer keys) and LDS
 //   E  max-pool + first argmax per unit type over E1 → x896[:, 128:896], arg (compat: enemy towers pool the enemy
 //      non-heroes, reference policy.py:127)
-// The per-step weights arrive as bf16 hi / lo row-major images (x = hi + lo, split once per step); products are
+// The per-step weights arrive as bf16 hi / lo images in MFMA fragment order (x = hi + lo, split once per step); products are
 // hi·hi + lo·hi + hi·lo with fp32 accumulation (≈2⁻¹⁶ relative per product), softmax / LN / residual in fp32.
+// Every workgroup re-reads W_qkv / W_out (256 KB of hi / lo fragments) from L2 for its row — ≈2.9 GB of L2 traffic per
+// step, what bounds it (1.02 ms). Not kept: a weight-stationary persistent form (one workgroup per CU holding its
+// W_qkv / W_out fragments in registers across rows) needs 256 resident registers per lane next to the QKV
+// accumulators and spilled ≈450 registers at the 512-register (one wave per SIMD) budget; at two waves per SIMD the
+// resident set cannot fit at all.
 #include "common.h"
+#include <cstdlib>
 
 namespace {
 
@@ -73,8 +79,10 @@ __device__ __forceinline__ f32x4 mfma3k16(const bf16x4v& ah, const bf16x4v& al, 
 __device__ __forceinline__ bf16x8 frag(const short* img, int pitch, int m0, int k0, int lane) {
   return *reinterpret_cast<const bf16x8*>(img + (m0 + (lane & 15)) * pitch + k0 + 8 * (lane >> 4));
 }
-__device__ __forceinline__ bf16x8 gfrag(const short* __restrict__ w, int m0, int k0, int lane) {   // (·, 128) rows
-  return *reinterpret_cast<const bf16x8*>(w + (size_t)(m0 + (lane & 15)) * kD + k0 + 8 * (lane >> 4));
+// weight fragment of rows m0 … m0+15, k-step k0/32 from a FRAGMENT-ORDERED image [row tile][k-step][lane][8] (one
+// coalesced 1 KB load per wave; the row-major image cost 16 separate 64-B segments per load instruction)
+__device__ __forceinline__ bf16x8 gfrag(const short* __restrict__ w, int m0, int k0, int lane) {
+  return *reinterpret_cast<const bf16x8*>(w + ((size_t)((m0 >> 4) * (kD / 32) + (k0 >> 5)) * 64 + lane) * 8);
 }
 
 __global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P) {
@@ -329,6 +337,7 @@ __global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P)
     }
   }
 }
+
 
 }  // namespace
 

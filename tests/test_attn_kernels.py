@@ -264,8 +264,9 @@ def test_attn_block_fwd_f32_matches_fp64(gpu_ops, compat):
     wo = torch.randn(D, D, device='cuda', generator=g) * D ** -0.5
     x896 = torch.zeros(N, 896, device='cuda')
     arg = torch.empty(N, 6, 128, dtype=torch.uint8, device='cuda')
-    qh, ql = gpu_ops.split_bf16x2(wq)
-    oh, ol = gpu_ops.split_bf16x2(wo)
+    from dotaclient_amd.models.pipelined import _frag_order
+    qh, ql = (_frag_order(t) for t in gpu_ops.split_bf16x2(wq))
+    oh, ol = (_frag_order(t) for t in gpu_ops.split_bf16x2(wo))
     xn, mu, rs, qkv, o, lse, e1 = gpu_ops.attn_block_fwd(e0, bout, gamma, beta, qh, ql, bq, oh, ol, TYPE_OFF, x896,
                                                          arg, compat, 1e-5)
     torch.cuda.synchronize()
