@@ -146,6 +146,12 @@ class WeightImages:
             if wpre_i.shape[1] % 128 == 0 and wih_i.shape[0] % 128 == 0:
                 partsS = {'pre_s': slab(wpre_i), 'ih_s': slab(wih_i), 'dx1_s': slab(wih_i.t()),
                           'dx2_s': slab(wpre_i.t())}
+            if H % 128 == 0:
+                # heads GEMM and its ∂X product on the chain kernel's stages: W_cat zero-padded to 256 rows
+                wcat_p = torch.cat([wcat, neg(256 - LDZ, H)], 0)
+                partsS['wcat_s'] = slab(wcat_p)
+                partsS['wcatT_s'] = slab(wcat_p.t())
+                parts32['bcat256'] = (torch.cat([bcat, neg(256 - LDZ)]), None)
         self.shapes16 = {k: tuple(v.shape) for k, v in parts16.items()}
         self.shapes32 = {k: tuple(v[0].shape) for k, v in parts32.items()}
         m16 = torch.cat([v.reshape(-1) for v in parts16.values()]) if parts16 else torch.zeros(0, dtype=torch.int64)
@@ -207,6 +213,9 @@ _ATTN_FUSED = os.environ.get('DCA_ATTN_FUSED', '1') != '0'
 # fp32 learner: the forward chain x = relu(x896·W_preᵀ + b), xp = x·W_ihᵀ as ONE hand-written kernel (the ∂X
 # kernel's forward twin, ops/csrc/dx_chain.hip) instead of two hipBLASLt GEMMs (DCA_FWD_CHAIN=0)
 _FWD_CHAIN = os.environ.get('DCA_FWD_CHAIN', '1') != '0'
+# fp32 learner: the heads GEMM z = h·W_catᵀ + b and ∂h = ∂z·W_cat on the chain kernel's stages (W_cat padded to 256
+# rows, z / ∂z carried 256 wide) instead of hipBLASLt (DCA_HEADS_ROWMM=0)
+_HEADS_ROWMM = os.environ.get('DCA_HEADS_ROWMM', '1') != '0'
 
 
 def fused_step_tm(fp, *args, **kw):
@@ -445,11 +454,15 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             dx_w = tuple(W['dx1_s']) + tuple(W['dx2_s'])
         else:
             dx_w = tuple(C.split_bf16x2(W['wihT16'], True)) + tuple(C.split_bf16x2(W['wpreT'], True))
+    rowmm = one and f32 and not exact and _HEADS_ROWMM and 'wcat_s' in W
     for (t0, t1), done in zip(spans, fwd_done):
         main.wait_event(done)
         r0, r1 = t0 * B, t1 * B
         xh = hs16[t0:t1].view(-1, H)
-        zc = _addmm(bcat, xh, wcat16.t())     # bias in the GEMM epilogue
+        if rowmm:
+            zc = C.rowmm_out256(xh, W['wcat_s'][0], W['wcat_s'][1], W['bcat256'])   # (n, 256), padding columns 0
+        else:
+            zc = _addmm(bcat, xh, wcat16.t())     # bias in the GEMM epilogue
         # ∂L/∂z straight in the GEMM operand dtype: only the backward GEMMs read it
         dz16, dtl_c, part, lp = C.heads_loss(zc, emb[r0:r1], act_t[r0:r1], msk_t[r0:r1], adv_t[r0:r1],
                                              ret_t[r0:r1], lpo_t[r0:r1], nret_t[r0:r1], norms, algo, False,
@@ -459,16 +472,20 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         first = dWcat is None
         if first:
             dbcat = torch.empty(LDZ, device=dev)
+        dzw = dz16[:, :LDZ] if rowmm else dz16           # (the heads' columns of the 256-wide ∂z)
         if one and _WG_OVERLAP:
             # single chunk: the heads' weight gradient waits on the recurrence stream behind the backward
             # recurrence (off the path between the two recurrences; joined with the other weight gradients)
             dWcat = torch.empty(LDZ, H, device=dev)
-            heads_wg = (dz16, xh)
+            heads_wg = (dzw, xh)
         else:
-            dWcat = gemm_tn(dz16, xh, out=dWcat, accumulate=not first, colsum=dbcat)
+            dWcat = gemm_tn(dzw, xh, out=dWcat, accumulate=not first, colsum=dbcat)
         if one:
             z, dtl, logp = zc, dtl_c, lp
-            dxh = _mm(dz16, wcat16).view(S, B, H)
+            if rowmm:
+                dxh = C.rowmm_in256(dz16, W['wcatT_s'][0], W['wcatT_s'][1]).view(S, B, H)
+            else:
+                dxh = _mm(dz16, wcat16).view(S, B, H)
         else:
             z[r0:r1].copy_(zc)
             dtl[r0:r1].copy_(dtl_c)

@@ -716,6 +716,38 @@ std::vector<torch::Tensor> dpre_dx(torch::Tensor dG, torch::Tensor w1h, torch::T
   return {dpre, dx};
 }
 
+// The chain kernel's stages alone (dx_chain.hip, bf16x3, slab-major bf16 hi / lo weight images):
+// rowmm_out256: C (N, 256) = A (N, K) · Wᵀ + b with W (256, K) → images (K/32, 256, 32) — stage 1, bias epilogue;
+// rowmm_in256:  C (N, X) = A (N, 256) · Wᵀ with W (X, 256) → images (8, X, 32) — stage 2 on A read from HBM.
+// The 1v1 heads GEMM (W_cat zero-padded to 256 rows) and its ∂X product.
+torch::Tensor rowmm_out256(torch::Tensor A, torch::Tensor wh, torch::Tensor wl, torch::Tensor bias) {
+  CHECK_F32(A); CHECK_F32(bias); CHECK_BF16(wh); CHECK_BF16(wl);
+  const int N = A.size(0), K = A.size(1);
+  TORCH_CHECK(A.dim() == 2 && K % 128 == 0 && bias.numel() == 256, "rowmm_out256: A (N, K % 128 == 0), bias (256)");
+  TORCH_CHECK(wh.dim() == 3 && wh.size(0) * 32 == K && wh.size(1) == 256 && wh.size(2) == 32 && wl.sizes() == wh.sizes(),
+              "rowmm_out256: slab-major images (K/32, 256, 32)");
+  TORCH_CHECK((long long)N * K * 4 <= 0x7fff0000LL, "rowmm_out256: A too large for one launch");
+  auto out = torch::empty({N, 256}, A.options());
+  hip_check(dca_dpre_dx(ptr<float>(A), wh.data_ptr(), wl.data_ptr(), ptr<float>(bias), nullptr, nullptr,
+                        ptr<float>(out), nullptr, N, K, 0, 0, 2, cur_stream()),
+            "dca_dpre_dx(stage 1)");
+  return out;
+}
+
+torch::Tensor rowmm_in256(torch::Tensor A, torch::Tensor wh, torch::Tensor wl) {
+  CHECK_F32(A); CHECK_BF16(wh); CHECK_BF16(wl);
+  const int N = A.size(0);
+  TORCH_CHECK(A.dim() == 2 && A.size(1) == 256, "rowmm_in256: A (N, 256)");
+  TORCH_CHECK(wh.dim() == 3 && wh.size(0) == 8 && wh.size(2) == 32 && wl.sizes() == wh.sizes() && wh.size(1) % 128 == 0,
+              "rowmm_in256: slab-major images (8, X, 32), X % 128 == 0");
+  const int X = wh.size(1);
+  auto out = torch::empty({N, X}, A.options());
+  hip_check(dca_dpre_dx(ptr<float>(A), nullptr, nullptr, nullptr, wh.data_ptr(), wl.data_ptr(), nullptr,
+                        ptr<float>(out), N, 0, X, 0, 0, cur_stream()),
+            "dca_dpre_dx(stage 2)");
+  return out;
+}
+
 // The forward twin of dpre_dx (same kernel, bias + ReLU epilogue): x = relu(x896·W_preᵀ + b) (N, 256) and
 // xp = x·W_ihᵀ (N, X) in one launch, bf16x3 with slab-major hi / lo weight images (split_bf16x2(w, True) of W_pre
 // (256, K1) and of W_ih (X, 256)).
@@ -982,6 +1014,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x"), py::arg("w2h"), py::arg("w2l"));
   m.def("pre_rnn_chain", &pre_rnn_chain, "fused forward chain x = relu(x896·W_pre^T + b), xp = x·W_ih^T (bf16x3)",
         py::arg("x896"), py::arg("w1h"), py::arg("w1l"), py::arg("bias"), py::arg("w2h"), py::arg("w2l"));
+  m.def("rowmm_out256", &rowmm_out256, "C (N,256) = A (N,K)·W^T + b on the chain kernel's stage 1 (bf16x3)",
+        py::arg("A"), py::arg("wh"), py::arg("wl"), py::arg("bias"));
+  m.def("rowmm_in256", &rowmm_in256, "C (N,X) = A (N,256)·W^T on the chain kernel's stage 2 (bf16x3)", py::arg("A"),
+        py::arg("wh"), py::arg("wl"));
   m.def("split_bf16x2", &split_bf16x2, "fp32 -> (hi, lo) bf16 images with x = hi + lo (slab_major: (R,K) -> "
         "[K/32][R][32] images, the dpre_dx operand layout)", py::arg("src"), py::arg("slab_major") = false);
   m.def("enc_small_grads", &enc_small_grads, "entity-encoder type-bias and env-layer gradients in one pass");

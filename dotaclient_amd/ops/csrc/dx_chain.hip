@@ -130,7 +130,8 @@ __device__ __forceinline__ void mma_tiles(const Frag (&fa)[NI], const Frag (&fb)
 }
 
 // EPI 0: the ∂X chain's ReLU backward (v = [x > 0]·acc, x the layer's output); EPI 1: the forward chain's bias + ReLU
-// (v = max(acc + b, 0), `x` = the bias (P)) — pre-RNN layer then input projection, x896 → x → x·W_ihᵀ
+// (v = max(acc + b, 0), `x` = the bias (P)) — pre-RNN layer then input projection, x896 → x → x·W_ihᵀ; EPI 2: bias
+// only (the heads GEMM, stage 1 alone). K1 = 0 runs stage 2 alone on A = dG (N, P) (the heads' ∂X product).
 template <bool EXACT, int EPI>
 __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict__ dG, const void* __restrict__ w1h,
                                                         const void* __restrict__ w1l, const float* __restrict__ x,
@@ -148,6 +149,9 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
   const __amdgpu_buffer_rsrc_t rW2h = rsrc(w2h, (long long)X * P * ES);
   const __amdgpu_buffer_rsrc_t rW2l = rsrc(EXACT ? w2h : w2l, (long long)X * P * ES);
 
+  char* dimg = lds;                               // the dpre image aliases the stage-1 buffers
+  constexpr int DIMG = (P / BK) * L::A1;          // one image (hi, or fp32) of the dpre tile
+  if (K1 > 0) {
   // ================= stage 1: C1 (64 × P) = dG[r0:r0+64] · W_ih =================
   const int ar = tid >> 3, ak = (tid & 7) * 4;              // dG slab: one fp32 quad per thread
   const int arow = r0 + ar;
@@ -229,8 +233,7 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
 
   // ================= ReLU mask, dpre → HBM and → LDS (stage-2 A operand, 8 slabs in the A layout) =============
   // accumulator layout: acc[i][j][e] = C[row 32·wr + 16·i + 4·q + e][col 64·wc + 16·j + r16]
-  char* dimg = lds;                               // aliases the stage-1 buffers (all reads done: barrier above)
-  constexpr int DIMG = (P / BK) * L::A1;          // one image (hi, or fp32) of the dpre tile
+  // (the dpre image aliases the stage-1 buffers: all their reads are done, barrier above)
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -242,7 +245,8 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
         float v = 0.f;
         if (grow < N) {
           if constexpr (EPI == 0) v = x[(size_t)grow * P + col] > 0.f ? acc[i][j][e] : 0.f;
-          else v = fmaxf(acc[i][j][e] + x[col], 0.f);
+          else if constexpr (EPI == 1) v = fmaxf(acc[i][j][e] + x[col], 0.f);
+          else v = acc[i][j][e] + x[col];
           dpre[(size_t)grow * P + col] = v;
         }
         const int kk = col & (BK - 1);
@@ -257,8 +261,25 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
         }
       }
 
+  } else if constexpr (!EXACT) {
+    // stage-2-only launch (K1 = 0): the A operand is dG itself, (N, P) fp32 rows, split into the dpre image
+    for (int i = tid; i < BM * P / 4; i += NT) {
+      const int row = i / (P / 4), c4 = (i % (P / 4)) * 4;
+      const int grow = r0 + row;
+      const float4 v = grow < N ? *reinterpret_cast<const float4*>(dG + (size_t)grow * P + c4)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+      uint2 hi, lo;
+      split4(v, hi, lo);
+      const int kk = c4 & (BK - 1);
+      char* slab = dimg + (c4 / BK) * L::A1;
+      const int o = coff<false>(row, kk >> 3) + 2 * (kk & 7);
+      *reinterpret_cast<uint2*>(slab + o) = hi;
+      *reinterpret_cast<uint2*>(slab + DIMG + o) = lo;
+    }
+  }
+
   // ================= stage 2: dx (64 × X) = dpre · W_pre, 128-column chunks =================
-  if (dbg & 4) return;
+  if ((dbg & 4) || X == 0) return;                // (stage-1-only launch: X = 0)
   char* s2 = lds + L::D;
   constexpr int nk2 = P / BK;
   const int nchunk = X / XC, total = nchunk * nk2;   // multiple of RD (nk2 = 8)
@@ -372,7 +393,9 @@ extern "C" hipError_t dca_split_bf16x2(const float* src, short* hi, short* lo, l
 extern "C" hipError_t dca_dpre_dx(const float* dG, const void* w1h, const void* w1l, const float* x, const void* w2h,
                                   const void* w2l, float* dpre, float* dx, int N, int K1, int X, int exact,
                                   int epi, hipStream_t stream) {
-  if (N < 1 || K1 < RD * BK || K1 % (RD * BK) != 0 || X < XC || X % XC != 0 || ((X / XC) * (P / BK)) % RD != 0)
+  // K1 = 0: stage 2 only (A = dG (N, P)); X = 0: stage 1 only
+  if (N < 1 || (K1 == 0 && X == 0) || K1 < 0 || K1 % (RD * BK) != 0 || X < 0 || X % XC != 0 ||
+      ((X / XC) * (P / BK)) % RD != 0 || (K1 == 0 && exact))
     return hipErrorInvalidValue;
   if ((long long)N * K1 * 4 > 0x7fff0000LL) return hipErrorInvalidValue;      // buffer-resource range
   const int grid = (N + BM - 1) / BM;
@@ -387,6 +410,9 @@ extern "C" hipError_t dca_dpre_dx(const float* dG, const void* w1h, const void* 
                        N, K1, X, dbg);
   } else if (epi == 0) {
     hipLaunchKernelGGL((dpre_dx_kernel<false, 0>), dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre,
+                       dx, N, K1, X, dbg);
+  } else if (epi == 2) {
+    hipLaunchKernelGGL((dpre_dx_kernel<false, 2>), dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre,
                        dx, N, K1, X, dbg);
   } else {
     hipLaunchKernelGGL((dpre_dx_kernel<false, 1>), dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre,

@@ -167,7 +167,8 @@ __global__ __launch_bounds__(256) void weight_prep_kernel(const float* __restric
   const int stride = gridDim.x * blockDim.x;
   // bf16x3 operand images: x = hi + lo (the slab-major weight images of the fp32 learner's hand-written chains)
   for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < ns; i += stride) {
-    const float v = src[maps[i]];
+    const int m = maps[i];
+    const float v = m >= 0 ? src[m] : 0.f;          // (-1: zero padding rows)
     const short h = dca::f2bf(v);
     dsth[i] = h;
     dstl[i] = dca::f2bf(v - dca::bf2f(h));

@@ -213,7 +213,7 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
       }
     }
     if (lane == 0) put_dz(P, (size_t)n * P.ldz + kQ + 21, dV);
-    if (lane < P.ldz - kQ - 22) put_dz(P, (size_t)n * P.ldz + kQ + 22 + lane, 0.f);
+    for (int c = kQ + 22 + lane; c < P.ldz; c += 64) put_dz(P, (size_t)n * P.ldz + c, 0.f);   // padding columns
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     // ---- dq = Σ_u dtl[u] · emb[u]

@@ -58,3 +58,26 @@ def test_pre_rnn_chain_matches_fp64(gpu_ops, N):
         err = (got.double() - ref).abs().max() / ref.abs().max()
         assert err < 3e-5, float(err)
     assert bool((x >= 0).all())
+
+
+@pytest.mark.parametrize('N', [11200, 1000])
+def test_rowmm_stages_match_fp64(gpu_ops, N):
+    """The chain kernel's stages alone: C = A·Wᵀ + b (N, 256) and C = A·Wᵀ (N, X) from A (N, 256) — the heads GEMM
+    (W_cat zero-padded to 256 rows) and its ∂X product."""
+    g = torch.Generator(device='cuda').manual_seed(N + 2)
+    K, X = 512, 512
+    a = torch.randn(N, K, device='cuda', generator=g)
+    w = torch.randn(256, K, device='cuda', generator=g) * K ** -0.5
+    w[160:] = 0.0
+    b = torch.randn(256, device='cuda', generator=g)
+    b[160:] = 0.0
+    z = gpu_ops.rowmm_out256(a, *gpu_ops.split_bf16x2(w, True), b)
+    dz = torch.randn(N, 256, device='cuda', generator=g)
+    dx = gpu_ops.rowmm_in256(dz, *gpu_ops.split_bf16x2(w.t().contiguous(), True))
+    torch.cuda.synchronize()
+    ref_z = a.double() @ w.double().t() + b.double()
+    ref_dx = dz.double() @ w.double()
+    for got, ref in ((z, ref_z), (dx, ref_dx)):
+        err = (got.double() - ref).abs().max() / ref.abs().max()
+        assert err < 3e-5, float(err)
+    assert bool((z[:, 160:] == 0).all())
