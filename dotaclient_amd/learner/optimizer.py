@@ -472,7 +472,16 @@ class DotaOptimizer:
 
     def flush_checkpoints(self):
         """Wait for the background publishes / checkpoint writes (``async_checkpoint``); re-raises the first failure
-        on this thread, as the synchronous path would have."""
+        on this thread, as the synchronous path would have. A publish coalesced away at the end of the run (the
+        writer was busy) is made here, so the last iteration's model and trainer state always reach the actors and
+        the disk."""
+        skipped = getattr(self, '_pub_skipped', None)
+        if skipped is not None:
+            f = getattr(self, '_pub_future', None)
+            if f is not None:
+                f.result()
+            self._pub_skipped = None
+            self._upload_model_async(skipped)
         self._check_background(wait=True)
 
     def _check_background(self, wait: bool = False):
@@ -489,7 +498,9 @@ class DotaOptimizer:
 
     def _submit_background(self, fn, *args):
         self._check_background()
-        self.__dict__.setdefault('_bg_futures', []).append(self._ckpt_pool_get().submit(fn, *args))
+        f = self._ckpt_pool_get().submit(fn, *args)
+        self.__dict__.setdefault('_bg_futures', []).append(f)
+        return f
 
     def _pipelined(self) -> bool:
         return self.ingest == 'device' and self.device.type == 'cuda' and self.cfg.prefetch_rollouts > 0
@@ -687,6 +698,16 @@ class DotaOptimizer:
         plus an event, no per-tensor launches, no host sync; host copies on a stream of the writer's own,
         state-dict assembly, serialisation, the model publish and the files run on the ordered background writer,
         overlapping the next iteration's ingest and training."""
+        # coalescing: while the writer is still busy with the previous publish, this version is skipped (the next
+        # iteration's publishes newer weights anyway). Without it a learner iterating faster than one serialise +
+        # publish + checkpoint write (≈20 ms iterations vs ≈88 MB of files each) queued snapshots without bound —
+        # device memory and weight age growing for the whole run
+        f = getattr(self, '_pub_future', None)
+        if f is not None and not f.done():
+            self.n_publish_coalesced = getattr(self, 'n_publish_coalesced', 0) + 1
+            self._pub_skipped = version
+            return
+        self._pub_skipped = None
         fl, opt = self.learner.flat, self.learner.opt
         snap = {'flat': fl.flat.detach().clone(), 'exp_avg': opt.exp_avg.clone(), 'exp_avg_sq': opt.exp_avg_sq.clone(),
                 'steps': opt.steps.clone()}
@@ -695,7 +716,7 @@ class DotaOptimizer:
                 'layout': opt.layout()}
         ev = torch.cuda.Event()
         ev.record()
-        self._submit_background(self._publish_snapshot, snap, meta, ev, version)
+        self._pub_future = self._submit_background(self._publish_snapshot, snap, meta, ev, version)
 
     def _publish_snapshot(self, snap, meta, ev, version: int):
         import io
