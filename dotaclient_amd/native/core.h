@@ -451,11 +451,66 @@ class RingCore {
 };
 
 // ============================================================================================================
-inline uint32_t crc32c_raw(const uint8_t* p, size_t n) {
+inline uint32_t crc32c_serial(const uint8_t* p, size_t n) {
   uint64_t crc = 0xFFFFFFFFu;
   while (n >= 8) { uint64_t v; std::memcpy(&v, p, 8); crc = _mm_crc32_u64(crc, v); p += 8; n -= 8; }
   while (n--) crc = _mm_crc32_u8((uint32_t)crc, *p++);
   return (uint32_t)crc ^ 0xFFFFFFFFu;
+}
+
+// crc(A ‖ B) from crc(A), crc(B) and |B| (zlib's crc32_combine: GF(2) 32×32 operator for "append |B| zero bytes",
+// squared log₂|B| times), Castagnoli polynomial (reflected 0x82F63B78)
+inline uint32_t gf2_times(const uint32_t* mat, uint32_t vec) {
+  uint32_t sum = 0;
+  for (int i = 0; vec; vec >>= 1, ++i)
+    if (vec & 1) sum ^= mat[i];
+  return sum;
+}
+inline void gf2_square(uint32_t* sq, const uint32_t* mat) {
+  for (int n = 0; n < 32; ++n) sq[n] = gf2_times(mat, mat[n]);
+}
+inline uint32_t crc32c_combine(uint32_t crc1, uint32_t crc2, size_t len2) {
+  if (len2 == 0) return crc1;
+  uint32_t even[32], odd[32];
+  odd[0] = 0x82F63B78u;                  // operator for one zero bit
+  uint32_t row = 1;
+  for (int n = 1; n < 32; ++n) { odd[n] = row; row <<= 1; }
+  gf2_square(even, odd);                 // two zero bits
+  gf2_square(odd, even);                 // four zero bits
+  do {                                   // apply len2 zero bytes to crc1
+    gf2_square(even, odd);
+    if (len2 & 1) crc1 = gf2_times(even, crc1);
+    len2 >>= 1;
+    if (len2 == 0) break;
+    gf2_square(odd, even);
+    if (len2 & 1) crc1 = gf2_times(odd, crc1);
+    len2 >>= 1;
+  } while (len2 != 0);
+  return crc1 ^ crc2;
+}
+
+// CRC-32C: three independent crc32 chains over thirds of the buffer (the instruction's 3-cycle latency otherwise
+// caps one chain at a third of its throughput), joined by crc32c_combine
+inline uint32_t crc32c_raw(const uint8_t* p, size_t n) {
+  if (n < (size_t)3 << 16) return crc32c_serial(p, n);
+  const size_t third = (n / 3) & ~(size_t)7;
+  const uint8_t *a = p, *b = p + third, *c = p + 2 * third;
+  uint64_t ca = 0xFFFFFFFFu, cb = 0xFFFFFFFFu, cc = 0xFFFFFFFFu;
+  for (size_t i = 0; i < third; i += 8) {
+    uint64_t va, vb, vc;
+    std::memcpy(&va, a + i, 8);
+    std::memcpy(&vb, b + i, 8);
+    std::memcpy(&vc, c + i, 8);
+    ca = _mm_crc32_u64(ca, va);
+    cb = _mm_crc32_u64(cb, vb);
+    cc = _mm_crc32_u64(cc, vc);
+  }
+  const size_t rest = n - 3 * third;     // tail of the last part
+  const uint8_t* t = c + third;
+  for (size_t i = 0; i + 8 <= rest; i += 8) { uint64_t v; std::memcpy(&v, t + i, 8); cc = _mm_crc32_u64(cc, v); }
+  for (size_t i = rest & ~(size_t)7; i < rest; ++i) cc = _mm_crc32_u8((uint32_t)cc, t[i]);
+  const uint32_t fa = (uint32_t)ca ^ 0xFFFFFFFFu, fb = (uint32_t)cb ^ 0xFFFFFFFFu, fc = (uint32_t)cc ^ 0xFFFFFFFFu;
+  return crc32c_combine(crc32c_combine(fa, fb, third), fc, third + rest);
 }
 
 }  // namespace dca_native
