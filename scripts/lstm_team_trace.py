@@ -75,11 +75,14 @@ def bwd(B=8, H=512, S=200):
     o['step_ns'] = med(np.diff(w[..., 0], axis=2))
     o['gather_ns'] = med(w[..., 1] - w[..., 0])
     o['barrier1_ns'] = med(w[..., 2] - w[..., 1])
-    o['elementwise_ns'] = med(w[..., 3] - w[..., 2])
+    # kernel events (lstm_team_bwd_body): 0 step start, 1 dG_{t+1} gathered, 2 after barrier, 3 partial recurrent
+    # product done, 4 after the reduction barrier, 6 gate gradients computed + dG_t published + ∂gates stored
+    # (event 5 is not stamped: reading it gave the round-2 trace's garbage ±1e15 values)
+    o['recurrent_dot_ns'] = med(w[..., 3] - w[..., 2])
     o['barrier2_ns'] = med(w[..., 4] - w[..., 3])
-    o['mfma_stage_ns'] = med(w[..., 5] - w[..., 4])
-    o['stores_ns'] = med(w[..., 6] - w[..., 5])
+    o['gates_publish_ns'] = med(w[..., 6] - w[..., 4])
     last_pub = w[..., 6].max(axis=(0, 1))
+    o['publish_skew_ns'] = med(last_pub - w[..., 6].min(axis=(0, 1)))
     o['publish_to_first_gather_ns'] = med(w[..., 1].min(axis=(0, 1))[1:] - last_pub[:-1])
     o['publish_to_last_gather_ns'] = med(w[..., 1].max(axis=(0, 1))[1:] - last_pub[:-1])
     o['err'] = int(err.item())
