@@ -98,6 +98,10 @@ __device__ __forceinline__ void st_rel(unsigned* p, unsigned v) {
 __device__ __forceinline__ unsigned add_agent(unsigned* p, unsigned v) {
   return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// explicit global (not flat) stores for the per-lane-address merged stores: a flat store would also count in lgkmcnt,
+// which the LDS barriers wait on
+template <typename T>
+__device__ __forceinline__ void gstore(T* p, T v) { *(__attribute__((address_space(1))) T*)p = v; }
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // 8 consecutive fp32 values → hi / lo bf16 fragments (x = hi + lo up to ≈2⁻¹⁷ relative)
@@ -379,6 +383,14 @@ __device__ __forceinline__ void lstm_team_fwd_body(
   const dca::f32x4 bv = (bias4 && mfma_wave) ? *reinterpret_cast<const dca::f32x4*>(bias4 + eunit * 4)
                                              : dca::f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // V1/V2 merged outputs: every lane of a unit's LPU-lane group carries row 0's state (the dot products are summed
+  // into all of them anyway), so c and h leave in ONE store instruction — slice-0 lanes write c, slice-1 lanes h — and
+  // a step queues two output stores (c|h, gates) behind its publish instead of three (cs, hsf, gates): the stores
+  // ahead of the next poll are what the step pays for (see the notes at the top). Measured (scripts/team_store_ab.py,
+  // bench A/B on one box): 1.420 vs 1.447 µs per standalone forward step, 4.874 vs 4.945 ms per learner step.
+  // Knob bit 14: the three-store form.
+  const bool merged = V1 && !((knobs >> 14) & 1);
+  const int slice = V1 ? lane % LPU : 0;
   unsigned spins = 0;
   for (unsigned iter = 0;; ++iter) {
     const int chain = next_chain(ctl, team, m, iter, nch, &sh_int);
@@ -389,7 +401,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
     float creg[MT], hreg[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const int b = mt * 16 + erow;
+      const int b = merged ? 0 : mt * 16 + erow;
       creg[mt] = (mfma_wave && b < B) ? c0[(size_t)(b0 + b) * H + eunit] : 0.f;
       hreg[mt] = 0.f;
     }
@@ -404,7 +416,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
       if (mfma_wave) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          const int b = mt * 16 + erow;
+          const int b = merged ? 0 : mt * 16 + erow;     // (merged: the group's lanes load the same 16 B, one request)
           const size_t tx = ((knobs >> 10) & 1) ? 0 : (size_t)t;   // knob: every step reads step 0 (L2-resident)
           xv[mt] = (b < B) ? *reinterpret_cast<const dca::f32x4*>(xp4 + (((size_t)(b0 + b) * sb + tx * st) * H + eunit) * 4)
                            : dca::f32x4{0.f, 0.f, 0.f, 0.f};
@@ -550,7 +562,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           const float ig = sigm<PREC>(pi), fg = sigm<PREC>(pf), gg = tanh_<PREC>(pg), og = sigm<PREC>(po);
           const float c = fg * creg[mt] + ig * gg;
           const float hv = og * tanh_<PREC>(c);
-          if (b < B) { creg[mt] = c; hreg[mt] = hv; }
+          if (merged ? 0 < B : b < B) { creg[mt] = c; hreg[mt] = hv; }
           TSTAMP(3);
           if constexpr (F32) {
             // ---- publish h_t: granule {f32 h(u), tag} by every lane of a live row
@@ -572,7 +584,14 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           }
           TSTAMP(4);
           // ---- outputs
-          if (b < B && !((knobs >> 8) & 1)) {
+          if (merged) {
+            if (slice < 2 && 0 < B && !((knobs >> 8) & 1)) {
+              const size_t o = ((size_t)b0 * sb + (size_t)t * st) * H + eunit;
+              float* dst = slice == 0 ? cs + o : hsf + o;        // one store instruction: c (slice 0), h (slice 1)
+              gstore(dst, slice == 0 ? c : hv);
+              if (slice == 0) *reinterpret_cast<dca::f32x4*>(gates4 + o * 4) = dca::f32x4{ig, fg, gg, og};
+            }
+          } else if (b < B && !((knobs >> 8) & 1)) {
             const size_t bt = (size_t)(b0 + b) * sb + (size_t)t * st;
             if (hs) hs[bt * H + eunit] = dca::f2bf(hv);
             if (hsf) hsf[bt * H + eunit] = hv;
@@ -699,6 +718,9 @@ __device__ __forceinline__ void lstm_team_bwd_body(
     if constexpr (F32 && !V1) wfl[ks] = vl;
   }
 
+  // (Tried: one 16-B store instruction for the two hand-off chunks and the ∂gates record — lanes 16·r + u of wave 0
+  // computing unit u redundantly, role r picking the record — the forward's merged-store idea applied here: 1.578 vs
+  // 1.535 µs per step, slower; the three stores of the 16 unit lanes stay.)
   unsigned spins = 0;
   for (unsigned iter = 0;; ++iter) {
     const int chain = next_chain(ctl, team, m, iter, nch, &sh_int);
@@ -939,7 +961,7 @@ __global__ __launch_bounds__((VAR & 3) == 2 ? 512 : kThreads, 1) void lstm_team_
 }
 
 // DCA_TEAM_KNOBS = pre_sleep | skip_outputs << 8 | probe_first << 9 | xp_step0 << 10 | spin count reset per step << 12
-// | no poll back-off sleep << 13 (latency experiments only);
+// | no poll back-off sleep << 13 | three-store forward outputs << 14 (latency experiments only);
 // DCA_TEAM_FAIL=1 sets bit 11: no workgroup joins a team (fault injection: every chain left unprocessed → err 3)
 inline int team_knobs() {
   const char* e = getenv("DCA_TEAM_KNOBS");
