@@ -585,6 +585,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           TSTAMP(4);
           // ---- outputs
           if (merged) {
+            // (one b32 store for everything — slices 0-3 the gates, 4 c, 5 h — measured slower: 1.476 vs 1.410 µs)
             if (slice < 2 && 0 < B && !((knobs >> 8) & 1)) {
               const size_t o = ((size_t)b0 * sb + (size_t)t * st) * H + eunit;
               float* dst = slice == 0 ? cs + o : hsf + o;        // one store instruction: c (slice 0), h (slice 1)

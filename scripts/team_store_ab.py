@@ -42,19 +42,20 @@ def main():
     b4 = torch.randn(4 * H, device=dev) * 0.1
     dh = torch.randn(S, B, H, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
-    res = {0: ([], []), 1 << 14: ([], [])}
+    KN = [int(x) for x in (sys.argv[1:] or ["0", str(1 << 14)])]
+    res = {k: ([], []) for k in KN}
     outs = {}
     for rnd in range(6):
-        for k in (0, 1 << 14):
+        for k in KN:
             os.environ['DCA_TEAM_KNOBS'] = str(k)
             f, b, tf, tb = run(C, xp, whh, h0, c0, err, b4, dh, 3)
             if rnd > 0:
                 res[k][0].append(tf * 1e3 / S)
                 res[k][1].append(tb * 1e3 / S)
             outs[k] = [t.clone() for t in list(f) + list(b) if t is not None and t.numel() > 0]
-    same = all(torch.equal(a, b) for a, b in zip(outs[0], outs[1 << 14]))
+    same = all(torch.equal(a, b) for a, b in zip(outs[0], outs[KN[-1]]))
     for k, (f, b) in res.items():
-        print(json.dumps({'form': 'merged' if k == 0 else 'three-store', 'fwd_us_per_step_median': float(np.median(f)),
+        print(json.dumps({'knobs': k, 'fwd_us_per_step_median': float(np.median(f)),
                           'bwd_us_per_step_median': float(np.median(b)), 'fwd_min': min(f), 'bwd_min': min(b)}),
               flush=True)
     print(json.dumps({'bitwise_equal': bool(same), 'err': int(err.item())}), flush=True)
