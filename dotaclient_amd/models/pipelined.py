@@ -58,6 +58,13 @@ def _frag_order(w: torch.Tensor) -> torch.Tensor:
     return w.view(R // 16, 16, K // 32, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
 
 
+def _k16_order(w: torch.Tensor) -> torch.Tensor:
+    """(R, K) bf16 → 16x16x16 B-fragment order [R/16][K/16][lane = 16·(r%16 // 4) + k%16][4]: element j of lane l is
+    w[16·rt + 4·(l>>4) + j][16·ct + (l&15)] (ops/csrc/attn_block.hip gfrag4)."""
+    R, K = w.shape
+    return w.view(R // 16, 4, 4, K // 16, 16).permute(0, 3, 1, 4, 2).contiguous()
+
+
 def _acc(a, b):
     """Accumulate a per-chunk gradient: the first chunk's tensor is used as is (no zero fill + add)."""
     return b if a is None else a.add_(b)
@@ -210,6 +217,11 @@ _DX_FUSED = os.environ.get('DCA_DX_FUSED', '1') != '0'
 # fp32 5v5: the entity-attention block forward (LN, QKV, attention, out-projection + residual, pools) as ONE kernel
 # (ops/csrc/attn_block.hip) instead of ln_fwd + hipBLASLt + attn_fwd + hipBLASLt + pool (DCA_ATTN_FUSED=0)
 _ATTN_FUSED = os.environ.get('DCA_ATTN_FUSED', '1') != '0'
+# fp32 5v5: the block BACKWARD (∂E1 routing, ∂O, attention backward, ∂Xn, LayerNorm backward) as ONE kernel
+# (ops/csrc/attn_block.hip) instead of demb + hipBLASLt + attn_bwd + hipBLASLt + ln_bwd. Opt-in (DCA_ATTN_BWD_FUSED=1):
+# measured 1936 µs per step against 1858 µs for the five launches it replaces — one 135 KB / 405-register workgroup
+# per CU leaves every phase's memory round trips exposed (see the kernel's notes)
+_ATTN_BWD_FUSED = os.environ.get('DCA_ATTN_BWD_FUSED', '0') == '1'
 # fp32 learner: the forward chain x = relu(x896·W_preᵀ + b), xp = x·W_ihᵀ as ONE hand-written kernel (the ∂X
 # kernel's forward twin, ops/csrc/dx_chain.hip) instead of two hipBLASLt GEMMs (DCA_FWD_CHAIN=0)
 _FWD_CHAIN = os.environ.get('DCA_FWD_CHAIN', '1') != '0'
@@ -582,14 +594,45 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             split()
             split = None
         demb_in = None
-        if attn32:
+        if attn32 and _ATTN_BWD_FUSED:
+            # one kernel from ∂x896 / the pointer gradient to ∂E0; the two weight-gradient GEMMs over the N·U unit
+            # rows (∂W_out = ∂E1ᵀ·O, ∂W_qkv = ∂QKVᵀ·Xn, with their bias column sums) go to the recurrence stream
+            wot = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.out.weight'].detach().t().contiguous())]
+            wq4 = [_k16_order(t) for t in C.split_bf16x2(P['entity_attn.qkv.weight'].detach())]
+            dE1, dQKV, demb_in, lnsum = C.attn_block_bwd(
+                dtl, z, dx896, arg, toff, bool(cfg.compat_bugs), Oat, QKV, bqkv, lse, E0p, W['bout'], ln_mu, ln_rs,
+                P['entity_attn.ln.weight'].detach(), wot[0], wot[1], wq4[0], wq4[1])
+            dgam, dbet, dbt_attn = lnsum[:128], lnsum[128:256], lnsum[256:].view(6, 128)
+            dbout = torch.empty(128, device=dev)
+            dbqkv = torch.empty(384, device=dev)
+            if wg_side:
+                sL.wait_stream(main)
+            with torch.cuda.stream(sL if wg_side else main):
+                dWout = gemm_tn(dE1, Oat, colsum=dbout)
+                dWqkv = gemm_tn(dQKV, Xn, colsum=dbqkv)
+                if wg_side:
+                    wg_done = torch.cuda.Event()
+                    wg_done.record(sL)
+        elif attn32:
+            # the two weight-gradient GEMMs over the N·U unit rows (∂W_out = ∂E1ᵀ·O, ∂W_qkv = ∂QKVᵀ·Xn, with their
+            # bias column sums) run on the recurrence stream, off the ∂E1 → ∂O → attention → ∂Xn → LN → encoder
+            # chain (measured: 596 µs of the 5v5 step's critical path when they ran in line)
             dE1 = C.attn_demb(dtl, z, dx896, arg, toff, bool(cfg.compat_bugs), True)
             dbout = torch.empty(128, device=dev)
-            dWout = gemm_tn(dE1, Oat, colsum=dbout)
+            dbqkv = torch.empty(384, device=dev)
+            if wg_side:
+                sL.wait_stream(main)
+            with torch.cuda.stream(sL if wg_side else main):
+                dWout = gemm_tn(dE1, Oat, colsum=dbout)
             dO = dE1 @ P['entity_attn.out.weight']
             dQKV = C.attn_bwd(QKV, Oat, dO, lse, bqkv)
-            dbqkv = torch.empty(384, device=dev)
-            dWqkv = gemm_tn(dQKV, Xn, colsum=dbqkv)
+            if wg_side:
+                sL.wait_stream(main)
+            with torch.cuda.stream(sL if wg_side else main):
+                dWqkv = gemm_tn(dQKV, Xn, colsum=dbqkv)
+                if wg_side:
+                    wg_done = torch.cuda.Event()
+                    wg_done.record(sL)
             dXn = dQKV @ P['entity_attn.qkv.weight']
             demb_in, dgam, dbet, dbt_attn = C.ln_bwd(dXn, E0p, W['bout'], P['entity_attn.ln.weight'], ln_mu,
                                                      ln_rs, dE1, fp.unit_types(dev))

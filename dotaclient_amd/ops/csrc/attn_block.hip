@@ -338,6 +338,440 @@ __global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P)
   }
 }
 
+// =============================================================================================================
+// Fused fp32 entity-attention block BACKWARD (gfx950, bf16x3 MFMA): ONE launch per step instead of demb + ∂O GEMM +
+// attention backward + ∂Xn GEMM + LayerNorm backward (attn.hip / hipBLASLt: ≈1.86 ms of the 5v5 step's critical path
+// at N = 11 200 rows). One 256-thread workgroup (4 waves) per timestep row n (64 unit slots × 128):
+//   0  ∂E1 = dtl⊗q + ∂pool routed to the argmax unit (demb semantics; compat: the enemy-tower pool's gradient goes to
+//      the enemy-non-hero argmax) → HBM (the out-projection's weight gradient) and an fp32 LDS image
+//   1  ∂O = ∂E1·W_out, wave h: head h's 32 columns (16x16x32, A split from the LDS image, B = W_outᵀ fragment images)
+//   2  attention backward of head h on registers: D = rowsum(∂O∘O) and LSE per query in the accumulator lane layout
+//      (DPP row sums, no LDS), S = Q·Kᵀ and dP = ∂O·Vᵀ i-major (∂O row fragments from a per-wave transposed LDS
+//      image), P = exp(scale·S − LSE), ∂S = scale·P∘(dP − D); then the TRANSPOSED gradients
+//        ∂Vᵀ = ∂Oᵀ·P,  ∂Kᵀ = Qᵀ·∂S  (16x16x16: ∂O's and P / ∂S's accumulators ARE the operands),
+//        ∂Qᵀ = Kᵀ·∂Sᵀ  (16x16x32, ∂Sᵀ from a per-wave hi / lo LDS image by transposed reads)
+//      whose accumulator lanes (d = 4kg + r, unit = lane&15) are exactly 16x16x16 A fragments over d → ∂QKV to HBM
+//      (16-B stores, the QKV weight gradient's operand)
+//   3  ∂Xn partial of head h = Σ_{x ∈ q,k,v} ∂Xᵀ_h·W_x[head rows] (16x16x16, B = W_qkv k16-fragment images) → the
+//      wave's own fp32 LDS slot; the four slots are summed in a fixed order (deterministic)
+//   4  LayerNorm backward + residual: ∂E0 = ∂E1 + rstd·(g − mean(g) − x̂·mean(g∘x̂)), g = ∂Xn∘γ → HBM (the encoder
+//      backward's input); the row's [∂γ | ∂β | ∂b_τ per type] partial (1024 floats) → HBM, summed by
+//      colsum_rows_kernel in a fixed order.
+// LDS: 4 slots of a 64 × 132 fp32 image (135 KB) — phase 0/1 slot 0 = ∂E1, phase 2 slot h = wave h's ∂Oᵀ and ∂Sᵀ
+// images, phase 3 slot h = wave h's ∂Xn partial, phase 4 slots 0-2 = the partial sums — one workgroup per CU.
+// Measured at N = 11 200 (5v5 learner step): 1936 µs, against 1858 µs for the five launches it replaces, so the
+// learner keeps those (models/pipelined.py, opt-in DCA_ATTN_BWD_FUSED=1). 405 registers (no spills) and 135 KB of
+// LDS leave one wave per SIMD and one row in flight per CU: ≈44 µs per row, the sum of each phase's exposed memory
+// round trips (∂E1 inputs, W_out fragments, O / LSE / QKV rows, W_qkv fragments, E0' rows). Making it pay needs
+// rows in flight per CU — a persistent form prefetching row n+1's operands during row n, or two waves per head.
+constexpr int kPT = 132;                    // fp32 pitch of a 64 × 128 slot image
+constexpr int kSlot = kU * kPT;             // floats per slot
+constexpr int kPS = 72;                     // bf16 pitch of the per-wave ∂Oᵀ (32 × 64) and ∂Sᵀ (64 × 64) images
+constexpr int kLnW = 8 * kD;                // per-row LayerNorm partial: ∂γ | ∂β | ∂b_τ (6 types)
+
+struct BwdArgs {
+  const float* dtl; const float* q; const float* dx; const unsigned char* arg;   // demb inputs (q row stride ldq)
+  const float* o; const float* qkv; const float* bq; const float* lse;           // saved by the forward
+  const float* e0; const float* bout; const float* mu; const float* rs; const float* gamma;
+  const short* woth; const short* wotl;     // W_outᵀ (d, c) in 16x16x32 fragment order, bf16 hi / lo
+  const short* wq4h; const short* wq4l;     // W_qkv (384, 128) in 16x16x16 B-fragment order, bf16 hi / lo
+  float* de1; float* dqkv; float* de0; float* part;
+  int off[7];
+  int ldq, compat;
+  float scale;
+};
+
+// 16x16x16 B fragment (rows 16·rt + 4·kg + j, column 16·ct + lane&15) of a k16-fragment-ordered (R, 128) image
+// [R/16][8][lane][4]: one coalesced 512-B load per wave
+__device__ __forceinline__ bf16x4v gfrag4(const short* __restrict__ w, int rt, int ct, int lane) {
+  return *reinterpret_cast<const bf16x4v*>(w + ((size_t)(rt * 8 + ct) * 64 + lane) * 4);
+}
+// Σ over the 16 lanes of this lane's DPP row (xor 1, 2 by quad_perm, half-row and row mirrors), in every lane
+__device__ __forceinline__ float row_sum16(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x140, 0xF, 0xF, false));
+  return v;
+}
+// element jj of lane l = img[k0 + 8(l>>4) + jj][c0 + (l&15)] of a bf16 image [.][kPS] (two transposed reads)
+__device__ __forceinline__ bf16x8 frag_tr(const short* img, int k0, int c0, int lane) {
+  typedef __attribute__((address_space(3))) bf16x4v lds_v4;
+  const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+  const short* a = img + (k0 + 8 * g + q) * kPS + c0 + 4 * p;
+  const bf16x4v lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)a);
+  const bf16x4v hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(a + 4 * kPS));
+  bf16x8 f;
+  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+  return f;
+}
+__device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+__global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
+  __shared__ __attribute__((aligned(16))) float sm[4 * kSlot];
+  __shared__ float sd[kU];
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, kg = lane >> 4, li = lane & 15;
+  const int n = blockIdx.x;
+  const size_t rbase = (size_t)n * kU;
+
+  // ---- 0: ∂E1 (thread: column c, units 32·(tid>>7) … +31)
+  if (tid < kU) sd[tid] = P.dtl[(size_t)n * kU + tid];
+  __syncthreads();
+  {
+    const int c = tid & 127, uh = tid >> 7;
+    const float qc = P.q[(size_t)n * P.ldq + c];
+    int au[6];
+    float dp[6];
+#pragma unroll
+    for (int t = 0; t < 6; ++t) {
+      const int src = (P.compat && t == 5) ? 3 : t;
+      au[t] = P.off[src] + P.arg[((size_t)n * 6 + t) * kD + c];
+      dp[t] = P.dx[(size_t)n * 896 + kD + t * kD + c];
+    }
+#pragma unroll 4
+    for (int i = 0; i < 32; ++i) {
+      const int u = uh * 32 + i;
+      float v = sd[u] * qc;
+#pragma unroll
+      for (int t = 0; t < 6; ++t) v += (au[t] == u) ? dp[t] : 0.f;
+      P.de1[(rbase + u) * kD + c] = v;
+      sm[u * kPT + c] = v;
+    }
+  }
+  __syncthreads();
+
+  // ---- 1: ∂O of head h = w: dO[a][t] lane (unit i = 16a + 4kg + r, d = 16t + li within the head)
+  const int h = w;
+  f32x4 dO[4][2];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) dO[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    bf16x8 bh[2], bl[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      bh[t] = gfrag(P.woth, kHd * h + 16 * t, 32 * ks, lane);
+      bl[t] = gfrag(P.wotl, kHd * h + 16 * t, 32 * ks, lane);
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      bf16x8 ah, al;
+      split8v(&sm[(16 * a + li) * kPT + 32 * ks + 8 * kg], ah, al);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) dO[a][t] = mfma3(ah, al, bh[t], bl[t], dO[a][t]);
+    }
+  }
+  __syncthreads();                                        // slot 0 (∂E1 image) is wave 0's from here on
+
+  // ---- 2: attention backward of head h
+  short* const dTh = reinterpret_cast<short*>(sm + h * kSlot);        // ∂Oᵀ [32 d][kPS] hi / lo
+  short* const dTl = dTh + 32 * kPS;
+  short* const STh = dTh + 64 * kPS;                                  // (scale·∂S)ᵀ [64 j][kPS] hi / lo
+  short* const STl = STh + 64 * kPS;
+  const float* const base = P.qkv + rbase * 384 + kHd * h;
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      bf16x4v hi, lo;
+      split4v(dO[a][t], hi, lo);
+      *reinterpret_cast<bf16x4v*>(dTh + (16 * t + li) * kPS + 16 * a + 4 * kg) = hi;
+      *reinterpret_cast<bf16x4v*>(dTl + (16 * t + li) * kPS + 16 * a + 4 * kg) = lo;
+    }
+  // D_i = Σ_d ∂O[i][d]·O[i][d] and LSE_i for i = 16a + 4kg + r (the lane's query rows in the S layout below)
+  float Dr[4][4], Lr[4][4];
+  {
+    const float* ob = P.o + rbase * kD + kHd * h;
+    const float* lb = P.lse + ((size_t)n * 4 + h) * kU;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * a + 4 * kg + r;
+        const float v = dO[a][0][r] * ob[(size_t)i * kD + li] + dO[a][1][r] * ob[(size_t)i * kD + 16 + li];
+        Dr[a][r] = row_sum16(v);
+        Lr[a][r] = lb[i];
+      }
+  }
+  lds_wait();
+  // S = Q·Kᵀ and dP = ∂O·Vᵀ, i-major: p[a][b] lane (query i = 16a + 4kg + r, key j = 16b + li)
+  f32x4 p[4][4], dp[4][4];
+  {
+    float qb[8], kb8[8], vb8[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      qb[j] = P.bq[kHd * h + 8 * kg + j];
+      kb8[j] = P.bq[128 + kHd * h + 8 * kg + j];
+      vb8[j] = P.bq[256 + kHd * h + 8 * kg + j];
+    }
+    bf16x8 qh[4], ql[4], dh[4], dl[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      float v[8];
+      const float4 x0 = *reinterpret_cast<const float4*>(base + (size_t)(16 * a + li) * 384 + 8 * kg);
+      const float4 x1 = *reinterpret_cast<const float4*>(base + (size_t)(16 * a + li) * 384 + 8 * kg + 4);
+      v[0] = x0.x + qb[0]; v[1] = x0.y + qb[1]; v[2] = x0.z + qb[2]; v[3] = x0.w + qb[3];
+      v[4] = x1.x + qb[4]; v[5] = x1.y + qb[5]; v[6] = x1.z + qb[6]; v[7] = x1.w + qb[7];
+      split8v(v, qh[a], ql[a]);
+      dh[a] = frag_tr(dTh, 0, 16 * a, lane);
+      dl[a] = frag_tr(dTl, 0, 16 * a, lane);
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      float kv[8], vv8[8];
+      const float* kr = base + 128 + (size_t)(16 * b + li) * 384 + 8 * kg;
+      const float* vr = base + 256 + (size_t)(16 * b + li) * 384 + 8 * kg;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        kv[j] = kr[j] + kb8[j];
+        vv8[j] = vr[j] + vb8[j];
+      }
+      bf16x8 kh, kl, vh, vl;
+      split8v(kv, kh, kl);
+      split8v(vv8, vh, vl);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        p[a][b] = mfma3(qh[a], ql[a], kh, kl, f32x4{0.f, 0.f, 0.f, 0.f});
+        dp[a][b] = mfma3(dh[a], dl[a], vh, vl, f32x4{0.f, 0.f, 0.f, 0.f});
+      }
+    }
+  }
+  // P = exp(scale·S − LSE); dp ← scale·P∘(dP − D) = ∂L/∂(Q·Kᵀ); its transpose to the hi / lo images for ∂Qᵀ
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const float pr = __expf(p[a][b][r] * P.scale - Lr[a][r]);
+        p[a][b][r] = pr;
+        dp[a][b][r] = P.scale * pr * (dp[a][b][r] - Dr[a][r]);
+      }
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      bf16x4v sh, sl;
+      split4v(dp[a][b], sh, sl);
+      *reinterpret_cast<bf16x4v*>(STh + (16 * b + li) * kPS + 16 * a + 4 * kg) = sh;
+      *reinterpret_cast<bf16x4v*>(STl + (16 * b + li) * kPS + 16 * a + 4 * kg) = sl;
+    }
+  // ∂Vᵀ[t][b] = Σ_a ∂Oᵀ(t, a)·P(a, b) and ∂Kᵀ[t][b] = Σ_a Qᵀ(t, a)·∂S(a, b): lanes (d = 16t + 4kg + r, j = 16b + li)
+  f32x4 gV[2][4], gK[2][4], gQ[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const float bqc = P.bq[kHd * h + 16 * t + li];
+    bf16x4v oh[4], ol[4], qh[4], ql[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      split4v(dO[a][t], oh[a], ol[a]);
+      f32x4 qv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) qv[r] = base[(size_t)(16 * a + 4 * kg + r) * 384 + 16 * t + li] + bqc;
+      split4v(qv, qh[a], ql[a]);
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      f32x4 av = {0.f, 0.f, 0.f, 0.f}, ak = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        bf16x4v ph, pl, sh, sl;
+        split4v(p[a][b], ph, pl);
+        split4v(dp[a][b], sh, sl);
+        av = mfma3k16(oh[a], ol[a], ph, pl, av);
+        ak = mfma3k16(qh[a], ql[a], sh, sl, ak);
+      }
+      gV[t][b] = av;
+      gK[t][b] = ak;
+    }
+  }
+  lds_wait();
+  // ∂Qᵀ[t][a] = Σ_ks Kᵀ(t, ks)·∂Sᵀ(ks, a): lanes (d = 16t + 4kg + r, i = 16a + li)
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const float kbc = P.bq[128 + kHd * h + 16 * t + li];
+    bf16x8 kh[2], kl[2];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      float kv[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) kv[jj] = base[(size_t)(32 * ks + 8 * kg + jj) * 384 + 128 + 16 * t + li] + kbc;
+      split8v(kv, kh[ks], kl[ks]);
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      f32x4 aq = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        aq = mfma3(kh[ks], kl[ks], frag_tr(STh, 32 * ks, 16 * a, lane), frag_tr(STl, 32 * ks, 16 * a, lane), aq);
+      gQ[t][a] = aq;
+    }
+  }
+  // ∂QKV → HBM (no bias: the bias gradient is the column sum), 4 consecutive d per lane = one 16-B store
+  {
+    float* ob = P.dqkv + rbase * 384 + kHd * h;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u4 = 0; u4 < 4; ++u4) {
+        float* rowp = ob + (size_t)(16 * u4 + li) * 384 + 16 * t + 4 * kg;
+        *reinterpret_cast<f32x4*>(rowp) = gQ[t][u4];
+        *reinterpret_cast<f32x4*>(rowp + 128) = gK[t][u4];
+        *reinterpret_cast<f32x4*>(rowp + 256) = gV[t][u4];
+      }
+  }
+
+  // ---- 3: ∂Xn partial of head h: A = ∂Xᵀ accumulators (m = unit, k = d), B = W_qkv rows 128x + 32h + 16t + …
+  {
+    bf16x4v ah[3][2][4], al[3][2][4];
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u4 = 0; u4 < 4; ++u4) {
+        split4v(gQ[t][u4], ah[0][t][u4], al[0][t][u4]);
+        split4v(gK[t][u4], ah[1][t][u4], al[1][t][u4]);
+        split4v(gV[t][u4], ah[2][t][u4], al[2][t][u4]);
+      }
+    float* slot = sm + h * kSlot;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      f32x4 acc[4][4];
+#pragma unroll
+      for (int u4 = 0; u4 < 4; ++u4)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[u4][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int x = 0; x < 3; ++x)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const int rt = 8 * x + 2 * h + t;
+          bf16x4v bh[4], bl[4];
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            bh[c] = gfrag4(P.wq4h, rt, 4 * half + c, lane);
+            bl[c] = gfrag4(P.wq4l, rt, 4 * half + c, lane);
+          }
+#pragma unroll
+          for (int u4 = 0; u4 < 4; ++u4)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) acc[u4][c] = mfma3k16(ah[x][t][u4], al[x][t][u4], bh[c], bl[c], acc[u4][c]);
+        }
+      // (the wave's own slot: its ∂Oᵀ / ∂Sᵀ images are dead)
+#pragma unroll
+      for (int u4 = 0; u4 < 4; ++u4)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) slot[(16 * u4 + 4 * kg + r) * kPT + 64 * half + 16 * c + li] = acc[u4][c][r];
+    }
+  }
+  __syncthreads();
+
+  // ---- 4: LayerNorm backward + residual, 4 threads per unit row (32 columns each)
+  {
+    const int u = tid >> 2, c0 = 32 * (tid & 3);
+    const size_t row = rbase + u;
+    const float mu = P.mu[row], rs = P.rs[row];
+    float dxn[32], xh[32];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int j4 = 0; j4 < 8; ++j4) {
+      const int c = c0 + 4 * j4;
+      const float4 p0 = *reinterpret_cast<const float4*>(&sm[0 * kSlot + u * kPT + c]);
+      const float4 p1 = *reinterpret_cast<const float4*>(&sm[1 * kSlot + u * kPT + c]);
+      const float4 p2 = *reinterpret_cast<const float4*>(&sm[2 * kSlot + u * kPT + c]);
+      const float4 p3 = *reinterpret_cast<const float4*>(&sm[3 * kSlot + u * kPT + c]);
+      const float4 e = *reinterpret_cast<const float4*>(P.e0 + row * kD + c);
+      const float pv[4][4] = {{p0.x, p0.y, p0.z, p0.w}, {p1.x, p1.y, p1.z, p1.w}, {p2.x, p2.y, p2.z, p2.w},
+                              {p3.x, p3.y, p3.z, p3.w}};
+      const float ev[4] = {e.x, e.y, e.z, e.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float d = ((pv[0][q] + pv[1][q]) + pv[2][q]) + pv[3][q];
+        const float x = (ev[q] - P.bout[c + q] - mu) * rs;
+        dxn[4 * j4 + q] = d;
+        xh[4 * j4 + q] = x;
+        const float g = d * P.gamma[c + q];
+        s1 += g;
+        s2 += g * x;
+      }
+    }
+    s1 += __shfl_xor(s1, 1, 64);
+    s1 += __shfl_xor(s1, 2, 64);
+    s2 += __shfl_xor(s2, 1, 64);
+    s2 += __shfl_xor(s2, 2, 64);
+    s1 *= (1.f / kD);
+    s2 *= (1.f / kD);
+    float de0v[32];
+#pragma unroll
+    for (int j4 = 0; j4 < 8; ++j4) {
+      const int c = c0 + 4 * j4;
+      const float4 r1 = *reinterpret_cast<const float4*>(P.de1 + row * kD + c);
+      const float rv[4] = {r1.x, r1.y, r1.z, r1.w};
+      float o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int j = 4 * j4 + q;
+        const float g = dxn[j] * P.gamma[c + q];
+        o[q] = rv[q] + rs * (g - s1 - xh[j] * s2);
+        de0v[j] = o[q];
+      }
+      *reinterpret_cast<float4*>(P.de0 + row * kD + c) = make_float4(o[0], o[1], o[2], o[3]);
+    }
+    __syncthreads();                                      // every thread has read the ∂Xn partial slots
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      sm[0 * kSlot + u * kPT + c0 + j] = dxn[j] * xh[j];
+      sm[1 * kSlot + u * kPT + c0 + j] = dxn[j];
+      sm[2 * kSlot + u * kPT + c0 + j] = de0v[j];
+    }
+  }
+  __syncthreads();
+  // the row's partial [∂γ | ∂β | ∂b_τ]: fixed-order sums over its units (∂b_τ over the units of type τ)
+  for (int e = tid; e < kLnW; e += 256) {
+    int sl, c, u0, u1;
+    if (e < 2 * kD) {
+      sl = e >> 7; c = e & 127; u0 = 0; u1 = kU;
+    } else {
+      const int t = (e - 2 * kD) >> 7;
+      sl = 2; c = e & 127; u0 = P.off[t]; u1 = P.off[t + 1];
+    }
+    float v = 0.f;
+    for (int u = u0; u < u1; ++u) v += sm[sl * kSlot + u * kPT + c];
+    P.part[(size_t)n * kLnW + e] = v;
+  }
+}
+
+// out[g][c] = Σ rows [g·per, min(R, (g+1)·per)) of part (R, W), fixed order: 64 columns × 4 row phases per block,
+// grid (W/64, G). Two launches (G groups, then 1) sum the N per-row LayerNorm partials with thousands of threads in
+// flight instead of one latency-bound chain per column.
+__global__ __launch_bounds__(256) void colsum_rows_kernel(const float* __restrict__ part, int R, int W, int per,
+                                                          float* __restrict__ out) {
+  const int c = blockIdx.x * 64 + (threadIdx.x & 63), ph = threadIdx.x >> 6, g = blockIdx.y;
+  const int r0 = g * per, r1 = min(R, r0 + per);
+  float s = 0.f;
+  if (c < W) {
+    int r = r0 + ph;
+    for (; r + 12 < r1; r += 16) {
+      const float v0 = part[(size_t)r * W + c], v1 = part[(size_t)(r + 4) * W + c];
+      const float v2 = part[(size_t)(r + 8) * W + c], v3 = part[(size_t)(r + 12) * W + c];
+      s += v0;
+      s += v1;
+      s += v2;
+      s += v3;
+    }
+    for (; r < r1; r += 4) s += part[(size_t)r * W + c];
+  }
+  __shared__ float red[4][64];
+  red[ph][threadIdx.x & 63] = s;
+  __syncthreads();
+  if (ph == 0 && c < W)
+    out[(size_t)g * W + c] = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
+}
+
 
 }  // namespace
 
@@ -352,5 +786,30 @@ extern "C" hipError_t dca_attn_block_fwd_f32(const float* e0, const float* bout,
   for (int i = 0; i < 7; ++i) a.off[i] = off[i];
   if (a.off[6] != kU) return hipErrorInvalidValue;
   hipLaunchKernelGGL(attn_block_fwd_f32_kernel, dim3(N), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
+extern "C" int dca_attn_block_bwd_groups(int N) { return N < 64 ? 1 : 64; }
+
+// part: (N, 1024) per-row partials; tmp: (groups, 1024); sums: (1024) = [∂γ | ∂β | ∂b_τ (6×128)]
+extern "C" hipError_t dca_attn_block_bwd_f32(const float* dtl, const float* q, int ldq, const float* dx,
+                                             const unsigned char* arg, const int* off, int compat, const float* o,
+                                             const float* qkv, const float* bq, const float* lse, const float* e0,
+                                             const float* bout, const float* mu, const float* rs, const float* gamma,
+                                             const short* woth, const short* wotl, const short* wq4h,
+                                             const short* wq4l, float* de1, float* dqkv, float* de0, float* part,
+                                             float* tmp, float* sums, int N, hipStream_t stream) {
+  if (N < 1) return hipSuccess;
+  BwdArgs a{dtl, q, dx, arg, o, qkv, bq, lse, e0, bout, mu, rs, gamma, woth, wotl, wq4h, wq4l, de1, dqkv, de0, part,
+            {0}, ldq, compat, 0.17677669529663687f /* 1/sqrt(32) */};
+  for (int i = 0; i < 7; ++i) a.off[i] = off[i];
+  if (a.off[6] != kU) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(attn_block_bwd_f32_kernel, dim3(N), dim3(256), 0, stream, a);
+  DCA_CHECK_LAUNCH();
+  const int G = dca_attn_block_bwd_groups(N);
+  const int per = (N + G - 1) / G;
+  hipLaunchKernelGGL(colsum_rows_kernel, dim3(kLnW / 64, G), dim3(256), 0, stream, part, N, kLnW, per, tmp);
+  DCA_CHECK_LAUNCH();
+  hipLaunchKernelGGL(colsum_rows_kernel, dim3(kLnW / 64, 1), dim3(256), 0, stream, tmp, G, kLnW, G, sums);
   return hipGetLastError();
 }

@@ -464,6 +464,52 @@ std::vector<torch::Tensor> attn_block_fwd(torch::Tensor e0, torch::Tensor bout, 
   return {xn, mu, rs, qkv, o, lse, e1};
 }
 
+static void check_type_off(const std::vector<int64_t>& t);
+
+// Fused fp32 entity-attention block backward (attn_block.hip). q = the heads' z rows (row stride q.stride(0)), dx =
+// ∂x896; o / qkv / lse / mu / rs from attn_block_fwd, e0 = E0' (N·64, 128); W_outᵀ images in 16x16x32 fragment
+// order, W_qkv images in 16x16x16 B-fragment order (bf16 hi / lo). Returns (∂E1, ∂QKV (no bias), ∂E0,
+// [∂γ | ∂β | ∂b_τ (6×128)] (1024)).
+std::vector<torch::Tensor> attn_block_bwd(torch::Tensor dtl, torch::Tensor q, torch::Tensor dx, torch::Tensor arg,
+                                          std::vector<int64_t> type_off, bool compat, torch::Tensor o,
+                                          torch::Tensor qkv, torch::Tensor bq, torch::Tensor lse, torch::Tensor e0,
+                                          torch::Tensor bout, torch::Tensor mu, torch::Tensor rs, torch::Tensor gamma,
+                                          torch::Tensor woth, torch::Tensor wotl, torch::Tensor wq4h,
+                                          torch::Tensor wq4l) {
+  CHECK_F32(dtl); CHECK_DEV(q); CHECK_DT(q, at::kFloat); CHECK_F32(dx); CHECK_U8(arg); CHECK_F32(o); CHECK_F32(qkv);
+  CHECK_F32(bq); CHECK_F32(lse); CHECK_F32(e0); CHECK_F32(bout); CHECK_F32(mu); CHECK_F32(rs); CHECK_F32(gamma);
+  CHECK_BF16(woth); CHECK_BF16(wotl); CHECK_BF16(wq4h); CHECK_BF16(wq4l);
+  check_type_off(type_off);
+  const int64_t N = dtl.size(0);
+  TORCH_CHECK(dtl.dim() == 2 && dtl.size(1) == 64, "attn_block_bwd: dtl (N, 64)");
+  TORCH_CHECK(q.dim() == 2 && q.size(0) == N && q.size(1) >= 128 && q.stride(1) == 1, "attn_block_bwd: q (N, >=128)");
+  TORCH_CHECK(dx.dim() == 2 && dx.size(0) == N && dx.size(1) == 896, "attn_block_bwd: dx (N, 896)");
+  TORCH_CHECK(arg.numel() == N * 6 * 128, "attn_block_bwd: arg (N, 6, 128)");
+  TORCH_CHECK(o.numel() == N * 64 * 128 && e0.numel() == N * 64 * 128 && qkv.numel() == N * 64 * 384 &&
+              lse.numel() == N * 4 * 64 && mu.numel() == N * 64 && rs.numel() == N * 64, "attn_block_bwd: saved shapes");
+  TORCH_CHECK(bq.numel() == 384 && bout.numel() == 128 && gamma.numel() == 128 && woth.numel() == 128 * 128 &&
+              wotl.numel() == 128 * 128 && wq4h.numel() == 384 * 128 && wq4l.numel() == 384 * 128,
+              "attn_block_bwd: weight shapes");
+  int off[7];
+  for (int i = 0; i < 7; ++i) off[i] = (int)type_off[i];
+  auto o32 = e0.options();
+  auto de1 = torch::empty({N * 64, 128}, o32);
+  auto dqkv = torch::empty({N * 64, 384}, o32);
+  auto de0 = torch::empty({N * 64, 128}, o32);
+  auto part = torch::empty({N, 1024}, o32);
+  auto tmp = torch::empty({(int64_t)dca_attn_block_bwd_groups((int)N), 1024}, o32);
+  auto sums = torch::empty({1024}, o32);
+  hip_check(dca_attn_block_bwd_f32(ptr<float>(dtl), ptr<float>(q), (int)q.stride(0), ptr<float>(dx),
+                                   ptr<unsigned char>(arg), off, compat ? 1 : 0, ptr<float>(o), ptr<float>(qkv),
+                                   ptr<float>(bq), ptr<float>(lse), ptr<float>(e0), ptr<float>(bout), ptr<float>(mu),
+                                   ptr<float>(rs), ptr<float>(gamma), ptr<short>(woth), ptr<short>(wotl),
+                                   ptr<short>(wq4h), ptr<short>(wq4l), ptr<float>(de1), ptr<float>(dqkv),
+                                   ptr<float>(de0), ptr<float>(part), ptr<float>(tmp), ptr<float>(sums), (int)N,
+                                   cur_stream()),
+            "dca_attn_block_bwd_f32");
+  return {de1, dqkv, de0, sums};
+}
+
 // Returns / advantages over concatenated padded rollouts. rew (L,K) f32 and val (L) f32 (GAE; ignored for mode 0)
 // live on the GPU; the per-segment metadata is host data — off (nseg+1) i32 row offsets, seglen (nseg) i32 valid
 // steps, keys (nseg) i32 team key, boot (nseg) f32 bootstrap values, done (nseg) u8 — validated here and uploaded in
@@ -1000,6 +1046,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("active") = py::none());
   m.def("attn_block_fwd", &attn_block_fwd, "fused fp32 entity-attention block forward: LN + QKV + attention + "
         "out-projection + residual + pools (-> xn, mean, rstd, qkv, o, lse, e1)");
+  m.def("attn_block_bwd", &attn_block_bwd, "fused fp32 entity-attention block backward: demb + dO + attention "
+        "backward + dXn + LayerNorm backward (-> de1, dqkv, de0, [dgamma | dbeta | dbt])");
   m.def("loss_prep", &loss_prep, "loss normalisers from one-hot action rows (graph-replayable)");
   m.def("loss_prep_ws_elems", &loss_prep_ws_elems, "int32 workspace elements of loss_prep");
   m.def("loss_assemble", &loss_assemble, "loss scalar + metrics from heads/loss partials");

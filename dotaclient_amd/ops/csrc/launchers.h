@@ -13,6 +13,13 @@ hipError_t dca_attn_block_fwd_f32(const float* e0, const float* bout, const floa
                                   const short* wol, float* xn, float* mu, float* rs, float* qkv, float* o, float* lse,
                                   float* e1, float* x896, unsigned char* arg, const int* off, int compat, int N,
                                   float eps, hipStream_t stream);
+int dca_attn_block_bwd_groups(int N);
+hipError_t dca_attn_block_bwd_f32(const float* dtl, const float* q, int ldq, const float* dx, const unsigned char* arg,
+                                  const int* off, int compat, const float* o, const float* qkv, const float* bq,
+                                  const float* lse, const float* e0, const float* bout, const float* mu,
+                                  const float* rs, const float* gamma, const short* woth, const short* wotl,
+                                  const short* wq4h, const short* wq4l, float* de1, float* dqkv, float* de0,
+                                  float* part, float* tmp, float* sums, int N, hipStream_t stream);
 // actor_fp8.hip
 hipError_t dca_actor_fp8(const short* x896, const void* wpre, const float* spre, const float* bpre, const void* wg,
                          const float* sg, const float* bg, const void* wh, const float* sh, const float* bh, float* h,

@@ -294,3 +294,60 @@ def test_attn_block_fwd_f32_matches_fp64(gpu_ops, compat):
         torch.testing.assert_close(x896[:, D + t * D:D + (t + 1) * D].double(), mx, rtol=1e-4, atol=1e-4)
         got = e1.view(N, U, D)[:, TYPE_OFF[src]:TYPE_OFF[src + 1]].gather(1, arg[:, t].long().unsqueeze(1)).squeeze(1)
         torch.testing.assert_close(got, x896[:, D + t * D:D + (t + 1) * D], rtol=0, atol=0)   # arg = the kernel's max
+
+
+@pytest.mark.parametrize('compat', [False, True])
+def test_attn_block_bwd_f32_matches_fp64(gpu_ops, compat):
+    """Fused fp32 block backward (ops/csrc/attn_block.hip: ∂E1 routing → ∂O → attention backward → ∂Xn → LayerNorm
+    backward + residual) against float64 autograd through the same block: ∂E1, ∂QKV (pre-bias), ∂E0 and the
+    [∂γ | ∂β | per-type ∂b_τ] sums, on the forward kernel's own saved tensors."""
+    from dotaclient_amd.models.pipelined import _frag_order, _k16_order
+    g = _g(7)
+    e0 = torch.randn(N * U, D, device='cuda', generator=g) * 1.5 + 0.3
+    bout = torch.randn(D, device='cuda', generator=g) * 0.1
+    gamma = 1 + 0.1 * torch.randn(D, device='cuda', generator=g)
+    beta = 0.1 * torch.randn(D, device='cuda', generator=g)
+    wq = torch.randn(3 * D, D, device='cuda', generator=g) * D ** -0.5
+    bq = torch.randn(3 * D, device='cuda', generator=g) * 0.2
+    wo = torch.randn(D, D, device='cuda', generator=g) * D ** -0.5
+    x896 = torch.zeros(N, 896, device='cuda')
+    arg = torch.empty(N, 6, 128, dtype=torch.uint8, device='cuda')
+    qh, ql = (_frag_order(t) for t in gpu_ops.split_bf16x2(wq))
+    oh, ol = (_frag_order(t) for t in gpu_ops.split_bf16x2(wo))
+    xn, mu, rs, qkv, o, lse, e1 = gpu_ops.attn_block_fwd(e0, bout, gamma, beta, qh, ql, bq, oh, ol, TYPE_OFF, x896,
+                                                         arg, compat, 1e-5)
+    dtl = torch.randn(N, U, device='cuda', generator=g)
+    z = torch.randn(N, 256, device='cuda', generator=g)          # the heads' 256-wide rows; q = z[:, :128]
+    dx = torch.randn(N, 896, device='cuda', generator=g)
+    toh, tol = (_frag_order(t) for t in gpu_ops.split_bf16x2(wo.t().contiguous()))
+    w4h, w4l = (_k16_order(t) for t in gpu_ops.split_bf16x2(wq))
+    de1, dqkv, de0, sums = gpu_ops.attn_block_bwd(dtl, z, dx, arg, TYPE_OFF, compat, o, qkv, bq, lse, e0, bout, mu, rs,
+                                                  gamma, toh, tol, w4h, w4l)
+    torch.cuda.synchronize()
+    d = lambda t: t.double()   # noqa: E731
+    rel = lambda a, b: float((a.double() - b).norm() / b.norm())   # noqa: E731
+    # ∂E1 (demb semantics, routed to the forward kernel's argmax)
+    de1_r = d(dtl).unsqueeze(-1) * d(z)[:, None, :D]
+    for t in range(6):
+        src = 3 if (compat and t == 5) else t
+        u = TYPE_OFF[src] + arg[:, t].long()
+        de1_r.scatter_add_(1, u.unsqueeze(1), d(dx)[:, D + t * D:D + (t + 1) * D].unsqueeze(1))
+    de1_r = de1_r.view(N * U, D)
+    assert rel(de1, de1_r) < 1e-6
+    E0 = d(e0).requires_grad_(True)
+    gm, bt = d(gamma).requires_grad_(True), d(beta).requires_grad_(True)
+    xr = F.layer_norm(E0 - d(bout), (D,), gm, bt, 1e-5)
+    qkv_r = xr @ d(wq).t()
+    qkv_r.retain_grad()
+    q, k, v = (qkv_r + d(bq)).view(N, U, 3, NH, HD).unbind(2)
+    q, k, v = (t.transpose(1, 2) for t in (q, k, v))
+    s = q @ k.transpose(-1, -2) / HD ** 0.5
+    o_r = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(N * U, D)
+    e1_r = E0 + o_r @ d(wo).t()
+    e1_r.backward(de1_r)
+    assert rel(dqkv, qkv_r.grad) < 5e-5
+    assert rel(de0, E0.grad) < 5e-5
+    assert rel(sums[:D], gm.grad) < 5e-5
+    assert rel(sums[D:2 * D], bt.grad) < 5e-5
+    dbt_r = torch.stack([E0.grad.view(N, U, D)[:, TYPE_OFF[t]:TYPE_OFF[t + 1]].sum((0, 1)) for t in range(6)])
+    assert rel(sums[2 * D:].view(6, D), dbt_r) < 5e-5
