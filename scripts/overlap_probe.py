@@ -17,20 +17,27 @@ def main():
     dev = 'cuda'
     B, S, H = 8, 1400, 512
     torch.manual_seed(0)
-    whh = (torch.randn(4 * H, H, device=dev) * 0.05).to(torch.bfloat16)
+    f32 = 'f32' in sys.argv          # the fp32 learner's recurrence (exact-fp32 VALU V1 forward / V2 backward)
+    whh = torch.randn(4 * H, H, device=dev) * 0.05
+    if not f32:
+        whh = whh.to(torch.bfloat16)
     h0 = torch.zeros(B, H, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     dh = torch.randn(B, S, H, device=dev)
     xp = torch.randn(B, S, H, 4, device=dev) * 0.5
-    out = C.lstm_team_fwd(xp, whh, h0, h0, err, team_ctl(), True)
-    fwd = lambda: C.lstm_team_fwd(xp, whh, h0, h0, err, team_ctl(), True)  # noqa: E731
+    out = C.lstm_team_fwd(xp, whh, h0, h0, err, team_ctl(), not f32)
+    fwd = lambda: C.lstm_team_fwd(xp, whh, h0, h0, err, team_ctl(), not f32)  # noqa: E731
     bwd = lambda: C.lstm_team_bwd(dh, out[3], out[2], h0, None, None, whh, err, team_ctl())  # noqa: E731
     a = torch.randn(89600, 512, device=dev).to(torch.bfloat16)
     w = torch.randn(512, 2048, device=dev).to(torch.bfloat16)
     big = torch.empty(256 << 20, dtype=torch.uint8, device=dev)
     big2 = torch.empty_like(big)
+    from dotaclient_amd.ops.gemm import gemm_tn
+    dg = torch.randn(11200, 2048, device=dev)
+    hs = torch.randn(11200, 512, device=dev)
     loads = {
         'none': None,
+        'gemm_tn_f32': lambda: gemm_tn(dg, hs),
         'gemm': lambda: torch.mm(a, w),
         'copy': lambda: big2.copy_(big),
         'small_gemm': lambda: torch.mm(a[:11200], w),
