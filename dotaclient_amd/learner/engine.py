@@ -22,6 +22,7 @@ Batches are dicts of device tensors (see :func:`dotaclient_amd.learner.synthetic
 from __future__ import annotations
 
 import contextlib
+import threading
 from dataclasses import dataclass
 from typing import Dict, Optional
 
@@ -31,6 +32,12 @@ from ..models.policy import Policy
 from ..parallel.dp import DataParallel, FlatParams
 from .losses import ppo_loss, split_heads, vpg_loss
 from .optim import FlatAdam
+
+
+# Held while the learner captures a step graph: background threads of the learner process (the ingest stager's
+# rare buffer growth) take it around their pinned / device allocations, so no allocation from another thread lands
+# inside a capture window (HIP invalidates a capture on some cross-thread API calls even in thread-local mode).
+CAPTURE_LOCK = threading.RLock()
 
 
 @dataclass
@@ -241,7 +248,7 @@ class Learner:
                 switched.append(True)
 
             torch.cuda.synchronize(self.device)
-            with torch.cuda.stream(s):
+            with CAPTURE_LOCK, torch.cuda.stream(s):
                 g1.capture_begin(capture_error_mode=mode)
                 out = body(switch)
                 if not switched:
@@ -271,7 +278,7 @@ class Learner:
                 body()
             cur.wait_stream(s)
             g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g, stream=s, capture_error_mode=self._capture_mode()):
+            with CAPTURE_LOCK, torch.cuda.graph(g, stream=s, capture_error_mode=self._capture_mode()):
                 out = body()
             graphs[key] = (g, out)
             self.graph = g

@@ -161,14 +161,21 @@ class IngestPipeline:
             slot.uploaded.synchronize()               # the slot's previous upload has left the pinned buffer
         if slot.host is None or slot.host.numel() < nbytes:
             cap = max(nbytes, 2 * (slot.host.numel() if slot.host is not None else 0), 1 << 20)
-            if slot.dev is not None and self.cuda:
-                torch.cuda.synchronize(self.device)   # (rare) growth: nothing may still read the old buffers
-            slot.host = torch.empty(cap, dtype=torch.uint8, pin_memory=self.cuda)
-            if self.cuda:
-                with torch.cuda.stream(self.copy_stream):
-                    slot.dev = torch.empty(cap, dtype=torch.uint8, device=self.device)
-            else:
-                slot.dev = slot.host
+            if slot.consumed is not None:
+                # (rare) growth: the learner has expanded this slot's last contents (its upload was waited for
+                # above), so nothing reads the old buffers any more. An event wait, not a device synchronise: the
+                # learner may be capturing its step graph right now, and a device-wide sync from this thread would
+                # invalidate that capture
+                slot.consumed.synchronize()
+            # pinned / device allocations are serialised against the learner's graph captures (learner/engine.py)
+            from .engine import CAPTURE_LOCK
+            with CAPTURE_LOCK:
+                slot.host = torch.empty(cap, dtype=torch.uint8, pin_memory=self.cuda)
+                if self.cuda:
+                    with torch.cuda.stream(self.copy_stream):
+                        slot.dev = torch.empty(cap, dtype=torch.uint8, device=self.device)
+                else:
+                    slot.dev = slot.host
             slot.consumed = None
         hb = slot.host.numpy()
 

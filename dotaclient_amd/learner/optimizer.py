@@ -720,12 +720,15 @@ class DotaOptimizer:
 
     def _publish_snapshot(self, snap, meta, ev, version: int):
         import io
-        st = getattr(self, '_pub_stream', None)
-        if st is None:
-            st = self._pub_stream = torch.cuda.Stream(device=self.device)
-        with torch.cuda.stream(st):
-            st.wait_event(ev)
-            snap = _to_cpu(snap)
+        from .engine import CAPTURE_LOCK
+        # the device → host copies (and the release of the device snapshot) stay out of a step-graph capture window
+        with CAPTURE_LOCK:
+            st = getattr(self, '_pub_stream', None)
+            if st is None:
+                st = self._pub_stream = torch.cuda.Stream(device=self.device)
+            with torch.cuda.stream(st):
+                st.wait_event(ev)
+                snap = _to_cpu(snap)
         fl = self.learner.flat
         flat = snap['flat']
         # own storage per tensor: the message / checkpoint holds exactly the reference's 30 state_dict tensors
