@@ -72,7 +72,10 @@ def parse():
                     help='host threads of the native actor runtime per GPU (16-CPU share per GPU)')
     ap.add_argument('--e2e', type=float, default=20.0,
                     help='seconds of the end-to-end actors→queue→learners loop on every rank (0 = off)')
-    ap.add_argument('--e2e-games', type=int, default=1024)
+    # node-loop actor shape (scripts/e2e_ab.py on one MI355X, 15 s each: 2048 games × 12 threads 1.40 M steps/s
+    # (527 k valid), 1024 × 14 1.23 M (508 k): the learner process's stager / decode threads share the host cores)
+    ap.add_argument('--e2e-games', type=int, default=2048)
+    ap.add_argument('--e2e-threads', type=int, default=12, help='actor host threads of the node loop')
     ap.add_argument('--e2e-mode', default='process', choices=['process', 'thread'],
                     help='e2e actors as one spawned process per rank over the node broker (deploy split) or as a '
                          'thread (1 GPU only)')
@@ -280,7 +283,7 @@ def main():
         try:
             from dotaclient_amd.learner.e2e import measure_e2e, measure_e2e_node
             kw = dict(model=args.model, device=device, duration=args.e2e, games=args.e2e_games,
-                      threads=args.actor_threads, seq_len=args.seq_len, precision=args.precision)
+                      threads=args.e2e_threads, seq_len=args.seq_len, precision=args.precision)
             progress('e2e start')
             if args.e2e_mode == 'process':
                 e2e = measure_e2e_node(transport=args.e2e_transport, progress=progress, idle_probe=args.e2e_probe,
