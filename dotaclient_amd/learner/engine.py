@@ -313,12 +313,20 @@ class Learner:
         """One DP optimizer step on a minibatch sampled from an on-device replay (``learner.replay.HbmReplay``).
         On the direct fused path the gather itself is part of the captured graph (only the sampled indices are
         copied in)."""
+        if self.direct() and self._graph_ready() and getattr(replay, 'host_sampling', False):
+            key = ('replay', id(replay), B, replay.S)
+            if key in self.__dict__.get('_graphs', {}) and self._static_idx.numel() == B:
+                # captured step: the sampled positions go straight into the graph's index buffer (one copy)
+                replay.sample_into(self._static_idx, recent)
+                return self.train_step_indices(replay, None)
         return self.train_step_indices(replay, replay.sample_indices(B, recent))
 
     def train_step_indices(self, replay, idx: torch.Tensor) -> Dict[str, torch.Tensor]:
         """One DP optimizer step on the pool sequences ``idx`` (device int64) of ``replay`` — any object with
         ``data`` (field → (capacity, S, …) device tensors at fixed addresses), ``S`` and ``gather(idx)``: the HBM
         replay, or the optimizer's per-iteration pool (epoch permutations over the iteration's sequences)."""
+        if idx is None:                                 # already written into the captured graph's index buffer
+            idx = self._static_idx
         if not self.direct():
             return self.train_step(replay.gather(idx))
         B = idx.numel()
@@ -327,7 +335,7 @@ class Learner:
             key = ('replay', id(replay), B, S)
             if key not in self.__dict__.get('_graphs', {}):
                 self._static_idx = idx.clone()
-            else:
+            elif idx is not self._static_idx:
                 self._static_idx.copy_(idx)
             if self._split_mode():
                 vec = self._replay_split(key, lambda hook: self._direct_body(

@@ -122,6 +122,7 @@ class DeviceReplay:
                  chunk: int = 16):
         from .replay import HbmReplay
         self.buf = HbmReplay(n_seq, S, layout, hidden, device, seed=seed)
+        self.buf.host_sampling = True
         for i in range(0, n_seq, chunk):
             self.buf.add(make_batch(min(chunk, n_seq - i), S, layout, hidden, device=device, seed=seed + i))
         self.data = self.buf.data

@@ -738,7 +738,13 @@ def train_direct(fp, batch_tm: Dict[str, torch.Tensor], B: int, S: int) -> torch
     N = B * S
     dev = batch_tm['units'].device
     norms = fp.scratch('norms', (8,), torch.float32, dev)
-    C.loss_prep(batch_tm['actions'], fp.loss_prep_ws(dev), norms)
+    # the loss normalisers only feed the heads/loss kernel (after the forward recurrence, which runs on the side
+    # stream and is waited for by the main stream): computed on that stream, beside the encoder and pre-RNN chain
+    main = torch.cuda.current_stream(dev)
+    sL = fp.side_stream()
+    sL.wait_stream(main)
+    with torch.cuda.stream(sL):
+        C.loss_prep(batch_tm['actions'], fp.loss_prep_ws(dev), norms)
     W = fp.weight_images().refresh(C)
     P = dict(zip(fp.param_names, fp.params))
     H = fp.cfg.hidden

@@ -120,3 +120,22 @@ def test_replay_200gb_on_hbm_accounting_and_training(gpu_ops):
     torch.cuda.synchronize()
     assert torch.isfinite(m['loss'])
     del r
+
+
+@pytest.mark.gpu
+def test_sample_into_host_ring(gpu_ops):
+    """sample_into: host-sampled positions written into a device index buffer by one pinned copy per call (the
+    captured learner step's index buffer), newest-first window like sample_indices, ring slots reused safely."""
+    rep = HbmReplay(10, 8, LAYOUT_1V1, 32, 'cuda', seed=3)
+    rep.add(make_batch(7, 8, LAYOUT_1V1, 32, device='cuda', seed=1))
+    out = torch.empty(5, dtype=torch.long, device='cuda')
+    seen = set()
+    for _ in range(12):                                  # > ring size: slots are recycled behind their copies
+        rep.sample_into(out, recent=3)
+        v = out.cpu().tolist()
+        assert all(i in (4, 5, 6) for i in v), v          # the 3 newest of the 7 written positions
+        seen.update(v)
+    assert seen == {4, 5, 6}
+    rep.add(make_batch(6, 8, LAYOUT_1V1, 32, device='cuda', seed=2))   # wraps: newest are 12 mod 10 = 2 … back
+    rep.sample_into(out)
+    assert all(0 <= i < 10 for i in out.cpu().tolist())
