@@ -469,7 +469,9 @@ __global__ __launch_bounds__(256) void colsum_kernel(const float* __restrict__ p
 // ∂V = Pᵀ∂O and ∂K = ∂Sᵀ Q, and passes ∂S through LDS (hi / lo images, transposed reads) only for ∂Q = ∂S K.
 // Measured and not kept: a backward processed per 16-key block that recomputes S and dP in both layouts (no LDS,
 // ∂Q accumulated from the j-major tiles) to reach two waves per SIMD — 1392 vs 890 µs at 11 200 rows: the doubled
-// MFMA/exp work and 25 spilled registers cost more than the occupancy gains.
+// MFMA/exp work and 25 spilled registers cost more than the occupancy gains. Nor a backward over two query halves
+// of 32 (∂V / ∂K accumulated across the halves, nothing recomputed) bounded to two waves per SIMD (256 registers,
+// 8 spilled): 949 vs 868 µs — the re-read operand rows and the spills outweigh the second wave.
 __device__ __forceinline__ void split8(const float* __restrict__ p, bf16x8& hi, bf16x8& lo,
                                        const float* bias8 = nullptr) {
   const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
