@@ -222,6 +222,10 @@ _ATTN_FUSED = os.environ.get('DCA_ATTN_FUSED', '1') != '0'
 # measured 1936 µs per step against 1858 µs for the five launches it replaces — one 135 KB / 405-register workgroup
 # per CU leaves every phase's memory round trips exposed (see the kernel's notes)
 _ATTN_BWD_FUSED = os.environ.get('DCA_ATTN_BWD_FUSED', '0') == '1'
+# fp32 5v5 (unfused backward): ∂Xn = ∂QKV·W_qkv with the LayerNorm backward as its epilogue, one hand-written kernel
+# instead of a hipBLASLt GEMM + ln_bwd. Opt-in (DCA_DXN_LN_FUSED=1): measured 1033 µs per step against 631 µs for
+# hipBLASLt (350) + ln_bwd (281) — one timestep row per workgroup leaves too few bytes in flight per CU
+_DXN_LN_FUSED = os.environ.get('DCA_DXN_LN_FUSED', '0') == '1'
 # fp32 learner: the forward chain x = relu(x896·W_preᵀ + b), xp = x·W_ihᵀ as ONE hand-written kernel (the ∂X
 # kernel's forward twin, ops/csrc/dx_chain.hip) instead of two hipBLASLt GEMMs (DCA_FWD_CHAIN=0)
 _FWD_CHAIN = os.environ.get('DCA_FWD_CHAIN', '1') != '0'
@@ -401,6 +405,10 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             E1 = E0b.addmm_(Oat, P['entity_attn.out.weight'].detach().t())     # residual + out-projection, in place
             arg = C.attn_pool(E1, toff, x896, bool(cfg.compat_bugs))            # pools of the attended embeddings
         emb = E1.view(N, U, 128)
+        if _DXN_LN_FUSED and not _ATTN_BWD_FUSED:
+            # W_qkv as 16x16x16 B-fragment hi / lo images for the backward's ∂Xn + LayerNorm kernel (built here, off
+            # the backward's critical path)
+            wq4 = [_k16_order(t) for t in C.split_bf16x2(P['entity_attn.qkv.weight'].detach())]
     elif attn:
         # 5v5 entity attention (ops/csrc/attn.hip): emb = E0 + b_out here (bias folded into bt)
         toff = fp.type_offset_list()
@@ -633,9 +641,15 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
                 if wg_side:
                     wg_done = torch.cuda.Event()
                     wg_done.record(sL)
-            dXn = dQKV @ P['entity_attn.qkv.weight']
-            demb_in, dgam, dbet, dbt_attn = C.ln_bwd(dXn, E0p, W['bout'], P['entity_attn.ln.weight'], ln_mu,
-                                                     ln_rs, dE1, fp.unit_types(dev))
+            if _DXN_LN_FUSED:
+                # ∂Xn = ∂QKV·W_qkv and the LayerNorm backward in one launch (∂Xn never goes to HBM)
+                demb_in, lnsum = C.attn_dxn_ln_bwd(dQKV, wq4[0], wq4[1], E0p, W['bout'], ln_mu, ln_rs,
+                                                   P['entity_attn.ln.weight'].detach(), dE1, toff)
+                dgam, dbet, dbt_attn = lnsum[:128], lnsum[128:256], lnsum[256:].view(6, 128)
+            else:
+                dXn = dQKV @ P['entity_attn.qkv.weight']
+                demb_in, dgam, dbet, dbt_attn = C.ln_bwd(dXn, E0p, W['bout'], P['entity_attn.ln.weight'], ln_mu,
+                                                         ln_rs, dE1, fp.unit_types(dev))
         elif attn:
             # attention block backward over this chunk's rows (unit rows r0·U … r1·U)
             a0, a1 = r0 * U, r1 * U
