@@ -159,6 +159,11 @@ class WeightImages:
                 partsS['wcat_s'] = slab(wcat_p)
                 partsS['wcatT_s'] = slab(wcat_p.t())
                 parts32['bcat256'] = (torch.cat([bcat, neg(256 - LDZ)]), None)
+            if cfg.entity_attention:
+                # the fused attention block's W_qkv / W_out hi / lo images in MFMA fragment order (attn_block.hip),
+                # from this same gather instead of two split + two permute-copy launches before the block
+                partsS['wq_f'] = _frag_order(idx('entity_attn.qkv.weight'))
+                partsS['wo_f'] = _frag_order(idx('entity_attn.out.weight'))
         self.shapes16 = {k: tuple(v.shape) for k, v in parts16.items()}
         self.shapes32 = {k: tuple(v[0].shape) for k, v in parts32.items()}
         m16 = torch.cat([v.reshape(-1) for v in parts16.values()]) if parts16 else torch.zeros(0, dtype=torch.int64)
@@ -389,8 +394,11 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         if _ATTN_FUSED:
             # one kernel per step; E0' stays untouched (the LayerNorm backward's input), E1 is a new tensor
             E0p = emb.view(N * U, 128)
-            wq = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.qkv.weight'].detach())]
-            wo = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.out.weight'].detach())]
+            if 'wq_f' in W:                    # hi / lo fragment images from the step's weight_prep launch
+                wq, wo = W['wq_f'], W['wo_f']
+            else:
+                wq = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.qkv.weight'].detach())]
+                wo = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.out.weight'].detach())]
             arg = torch.empty(N, 6, 128, dtype=torch.uint8, device=dev)
             Xn, ln_mu, ln_rs, QKV, Oat, lse, E1 = C.attn_block_fwd(
                 E0p, W['bout'], P['entity_attn.ln.weight'].detach(), P['entity_attn.ln.bias'].detach(), wq[0], wq[1],
