@@ -602,8 +602,8 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             # DP split point: every gradient of the recurrence, pre-RNN and heads is final here (the big ones are
             # already in the flat buffer); apply the small ones and let the learner all-reduce those buckets while
             # the encoder backward below runs (see Learner._replay_split)
-            grads['rnn.bias_ih_l0'] = db[fp.gate_inv(H, dev)]
-            grads['rnn.bias_hh_l0'] = grads['rnn.bias_ih_l0']
+            grads['rnn.bias_ih_l0'] = db             # (gate-major already: the kernel writes PyTorch's order)
+            grads['rnn.bias_hh_l0'] = db
             early = [grads.pop(nm, None) if nm in early_names else None for nm in fp.param_names]
             fp.apply_direct_grads(early, None, set_mask=False)    # the final call records the full mask
             fp.early_applied = early_names
@@ -698,15 +698,14 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         dbe = _acc(dbe, dbe_c)
     if wg_done is not None:
         main.wait_event(wg_done)
-    inv = fp.gate_inv(H, dev)
     if not direct:
         grads['rnn.weight_hh_l0'] = dWhh
         grads['rnn.weight_ih_l0'] = dWih
         grads['affine_pre_rnn.weight'] = dWpre
         grads['affine_pre_rnn.bias'] = dbpre
     if 'rnn.bias_ih_l0' not in fp.early_applied:
-        grads['rnn.bias_ih_l0'] = db[inv]
-        grads['rnn.bias_hh_l0'] = grads['rnn.bias_ih_l0']
+        grads['rnn.bias_ih_l0'] = db
+        grads['rnn.bias_hh_l0'] = db
     grads['affine_unit_basic_stats.weight'] = dw1
     grads['affine_unit_basic_stats.bias'] = db1
     for t, s in enumerate(TYPE_SUFFIX):

@@ -929,7 +929,8 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       for (int o = tid; o < U * 4; o += NT) {
         float acc = 0.f;
         for (int b = 0; b < B; ++b) acc += dbs[b * U * 4 + o];
-        dbpart[(size_t)chain * 4 * H + 4 * j0 + o] = acc;
+        // PyTorch's gate-major order (gate q of unit j at q·H + j): the partials' chain sum IS ∂b_ih = ∂b_hh
+        dbpart[(size_t)chain * 4 * H + (o & 3) * H + j0 + (o >> 2)] = acc;
       }
     }
     __syncthreads();

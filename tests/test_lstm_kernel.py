@@ -107,4 +107,5 @@ def test_team_folded_bias_bf16_dgates_and_bias_grad(gpu_ops, B, S, H, tm):
     assert g16[0].dtype == torch.bfloat16
     torch.testing.assert_close(g16[0].float(), g32[0].to(torch.bfloat16).float(), atol=1e-6, rtol=0)
     torch.testing.assert_close(g16[1], g32[1], atol=1e-6, rtol=1e-6)
-    torch.testing.assert_close(g16[3], g32[0].sum((0, 1)).reshape(-1), atol=1e-3, rtol=1e-4)
+    # the bias gradient comes in PyTorch's gate-major order (unit-major ∂gates summed, then (H, 4) → (4, H))
+    torch.testing.assert_close(g16[3], g32[0].sum((0, 1)).t().reshape(-1), atol=1e-3, rtol=1e-4)
