@@ -617,7 +617,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             wq4 = [_k16_order(t) for t in C.split_bf16x2(P['entity_attn.qkv.weight'].detach())]
             dE1, dQKV, demb_in, lnsum = C.attn_block_bwd(
                 dtl, z, dx896, arg, toff, bool(cfg.compat_bugs), Oat, QKV, bqkv, lse, E0p, W['bout'], ln_mu, ln_rs,
-                P['entity_attn.ln.weight'].detach(), wot[0], wot[1], wq4[0], wq4[1])
+                P['entity_attn.ln.weight'].detach(), wot[0], wot[1], wq4[0], wq4[1], None)
             dgam, dbet, dbt_attn = lnsum[:128], lnsum[128:256], lnsum[256:].view(6, 128)
             dbout = torch.empty(128, device=dev)
             dbqkv = torch.empty(384, device=dev)

@@ -376,6 +376,7 @@ struct BwdArgs {
   const short* woth; const short* wotl;     // W_outᵀ (d, c) in 16x16x32 fragment order, bf16 hi / lo
   const short* wq4h; const short* wq4l;     // W_qkv (384, 128) in 16x16x16 B-fragment order, bf16 hi / lo
   float* de1; float* dqkv; float* de0; float* part;
+  unsigned long long* trace;                // optional phase timestamps (s_memrealtime) of rows < 64: [row][wave][8]
   int off[7];
   int ldq, compat;
   float scale;
@@ -415,6 +416,9 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
   const int n = blockIdx.x;
   const size_t rbase = (size_t)n * kU;
 
+#define PSTAMP(ev)                                                                                        \
+  if (P.trace && n < 64 && lane == 0) P.trace[((size_t)n * 4 + w) * 8 + (ev)] = __builtin_amdgcn_s_memrealtime()
+  PSTAMP(0);
   // ---- 0: ∂E1 (thread: column c, units 32·(tid>>7) … +31)
   if (tid < kU) sd[tid] = P.dtl[(size_t)n * kU + tid];
   __syncthreads();
@@ -441,6 +445,7 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
   }
   __syncthreads();
 
+  PSTAMP(1);
   // ---- 1: ∂O of head h = w: dO[a][t] lane (unit i = 16a + 4kg + r, d = 16t + li within the head)
   const int h = w;
   f32x4 dO[4][2];
@@ -466,6 +471,7 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
   }
   __syncthreads();                                        // slot 0 (∂E1 image) is wave 0's from here on
 
+  PSTAMP(2);
   // ---- 2: attention backward of head h
   short* const dTh = reinterpret_cast<short*>(sm + h * kSlot);        // ∂Oᵀ [32 d][kPS] hi / lo
   short* const dTl = dTh + 32 * kPS;
@@ -624,6 +630,7 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
       }
   }
 
+  PSTAMP(3);
   // ---- 3: ∂Xn partial of head h: A = ∂Xᵀ accumulators (m = unit, k = d), B = W_qkv rows 128x + 32h + 16t + …
   {
     bf16x4v ah[3][2][4], al[3][2][4];
@@ -670,6 +677,7 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
   }
   __syncthreads();
 
+  PSTAMP(4);
   // ---- 4: LayerNorm backward + residual, 4 threads per unit row (32 columns each)
   {
     const int u = tid >> 2, c0 = 32 * (tid & 3);
@@ -730,6 +738,7 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
     }
   }
   __syncthreads();
+  PSTAMP(5);
   // the row's partial [∂γ | ∂β | ∂b_τ]: fixed-order sums over its units (∂b_τ over the units of type τ)
   for (int e = tid; e < kLnW; e += 256) {
     int sl, c, u0, u1;
@@ -743,6 +752,8 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
     for (int u = u0; u < u1; ++u) v += sm[sl * kSlot + u * kPT + c];
     P.part[(size_t)n * kLnW + e] = v;
   }
+  PSTAMP(6);
+#undef PSTAMP
 }
 
 // out[g][c] = Σ rows [g·per, min(R, (g+1)·per)) of part (R, W), fixed order: 64 columns × 4 row phases per block,
@@ -945,10 +956,11 @@ extern "C" hipError_t dca_attn_block_bwd_f32(const float* dtl, const float* q, i
                                              const float* bout, const float* mu, const float* rs, const float* gamma,
                                              const short* woth, const short* wotl, const short* wq4h,
                                              const short* wq4l, float* de1, float* dqkv, float* de0, float* part,
-                                             float* tmp, float* sums, int N, hipStream_t stream) {
+                                             float* tmp, float* sums, int N, hipStream_t stream,
+                                             unsigned long long* trace) {
   if (N < 1) return hipSuccess;
   BwdArgs a{dtl, q, dx, arg, o, qkv, bq, lse, e0, bout, mu, rs, gamma, woth, wotl, wq4h, wq4l, de1, dqkv, de0, part,
-            {0}, ldq, compat, 0.17677669529663687f /* 1/sqrt(32) */};
+            trace, {0}, ldq, compat, 0.17677669529663687f /* 1/sqrt(32) */};
   for (int i = 0; i < 7; ++i) a.off[i] = off[i];
   if (a.off[6] != kU) return hipErrorInvalidValue;
   hipLaunchKernelGGL(attn_block_bwd_f32_kernel, dim3(N), dim3(256), 0, stream, a);

@@ -475,7 +475,7 @@ std::vector<torch::Tensor> attn_block_bwd(torch::Tensor dtl, torch::Tensor q, to
                                           torch::Tensor qkv, torch::Tensor bq, torch::Tensor lse, torch::Tensor e0,
                                           torch::Tensor bout, torch::Tensor mu, torch::Tensor rs, torch::Tensor gamma,
                                           torch::Tensor woth, torch::Tensor wotl, torch::Tensor wq4h,
-                                          torch::Tensor wq4l) {
+                                          torch::Tensor wq4l, c10::optional<torch::Tensor> trace) {
   CHECK_F32(dtl); CHECK_DEV(q); CHECK_DT(q, at::kFloat); CHECK_F32(dx); CHECK_U8(arg); CHECK_F32(o); CHECK_F32(qkv);
   CHECK_F32(bq); CHECK_F32(lse); CHECK_F32(e0); CHECK_F32(bout); CHECK_F32(mu); CHECK_F32(rs); CHECK_F32(gamma);
   CHECK_BF16(woth); CHECK_BF16(wotl); CHECK_BF16(wq4h); CHECK_BF16(wq4l);
@@ -505,7 +505,8 @@ std::vector<torch::Tensor> attn_block_bwd(torch::Tensor dtl, torch::Tensor q, to
                                    ptr<float>(rs), ptr<float>(gamma), ptr<short>(woth), ptr<short>(wotl),
                                    ptr<short>(wq4h), ptr<short>(wq4l), ptr<float>(de1), ptr<float>(dqkv),
                                    ptr<float>(de0), ptr<float>(part), ptr<float>(tmp), ptr<float>(sums), (int)N,
-                                   cur_stream()),
+                                   cur_stream(),
+                                   (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr),
             "dca_attn_block_bwd_f32");
   return {de1, dqkv, de0, sums};
 }

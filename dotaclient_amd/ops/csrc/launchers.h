@@ -23,7 +23,8 @@ hipError_t dca_attn_block_bwd_f32(const float* dtl, const float* q, int ldq, con
                                   const float* lse, const float* e0, const float* bout, const float* mu,
                                   const float* rs, const float* gamma, const short* woth, const short* wotl,
                                   const short* wq4h, const short* wq4l, float* de1, float* dqkv, float* de0,
-                                  float* part, float* tmp, float* sums, int N, hipStream_t stream);
+                                  float* part, float* tmp, float* sums, int N, hipStream_t stream,
+                                  unsigned long long* trace);
 // actor_fp8.hip
 hipError_t dca_actor_fp8(const short* x896, const void* wpre, const float* spre, const float* bpre, const void* wg,
                          const float* sg, const float* bg, const void* wh, const float* sh, const float* bh, float* h,

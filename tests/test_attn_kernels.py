@@ -322,7 +322,7 @@ def test_attn_block_bwd_f32_matches_fp64(gpu_ops, compat):
     toh, tol = (_frag_order(t) for t in gpu_ops.split_bf16x2(wo.t().contiguous()))
     w4h, w4l = (_k16_order(t) for t in gpu_ops.split_bf16x2(wq))
     de1, dqkv, de0, sums = gpu_ops.attn_block_bwd(dtl, z, dx, arg, TYPE_OFF, compat, o, qkv, bq, lse, e0, bout, mu, rs,
-                                                  gamma, toh, tol, w4h, w4l)
+                                                  gamma, toh, tol, w4h, w4l, None)
     torch.cuda.synchronize()
     d = lambda t: t.double()   # noqa: E731
     rel = lambda a, b: float((a.double() - b).norm() / b.norm())   # noqa: E731
