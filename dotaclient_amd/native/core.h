@@ -231,8 +231,10 @@ void unit_rows(const std::vector<const Unit*>& list, const Unit& hero, bool only
     r[2] = (float)((double)u.y / kMapHalf);
     r[3] = (float)((double)u.z / 512.0 - 0.5);
     r[4] = (float)(dist / kMapHalf - 0.5);
-    r[5] = (float)std::sin((double)u.facing * tau / 360.0);
-    r[6] = (float)std::cos((double)u.facing * tau / 360.0);
+    double sf, cf;
+    sincos((double)u.facing * tau / 360.0, &sf, &cf);      // one argument reduction for both (same values)
+    r[5] = (float)sf;
+    r[6] = (float)cf;
     r[7] = (dist <= (double)hero.attack_range ? 1.f : 0.f) - 0.5f;
     r[8] = attacking(u, hero) - 0.5f;
     r[9] = attacking(hero, u) - 0.5f;
