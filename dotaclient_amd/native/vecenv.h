@@ -587,13 +587,23 @@ class SimGame {
   // CMsgBotWorldState(team) as the featurizer sees it after the protobuf round trip
   void world(int team, World& w) const {
     w.dota_time = (float)dota_time;
+    // the team's living units' positions, compacted once (the fog test below scans them per enemy unit)
+    thread_local std::vector<double> ax, ay;
+    if (fog) {
+      ax.clear();
+      ay.clear();
+      for (const SUnit& a : units)
+        if (a.team == team && a.alive) {
+          ax.push_back(a.x);
+          ay.push_back(a.y);
+        }
+    }
     size_t k = 0;                   // overwrite w's units in place: their attack_casters keep their capacity
     for (const SUnit& u : units) {
       if (fog && u.team != team && u.unit_type != TOWER) {
         bool seen = false;
-        for (const SUnit& a : units) {
-          if (a.team != team || !a.alive) continue;
-          const double dx = a.x - u.x, dy = a.y - u.y, d2 = dx * dx + dy * dy;
+        for (size_t j = 0; j < ax.size(); ++j) {
+          const double dx = ax[j] - u.x, dy = ay[j] - u.y, d2 = dx * dx + dy * dy;
           if (d2 > kVision * kVision * (1.0 + 1e-14)) continue;       // sqrt(d2) > kVision for sure
           if (std::sqrt(d2) <= kVision) { seen = true; break; }
         }
