@@ -87,6 +87,10 @@ class OptimizerConfig:
                                        #     the next iteration's decode with this one's training); 0: inline
     record_consumed: int = 0           # keep the keys (game, team, player, version, length) of the last N rollouts
                                        #     consumed (competing-consumer tests; 0 = off)
+    lookahead_ingest: bool = os.environ.get('DCA_LOOKAHEAD', '1') != '0'
+                                       # pipelined GPU ingest: take and expand the NEXT iteration's staged rollouts
+                                       #     while this iteration's steps run on the GPU (its host work then overlaps
+                                       #     the training instead of leaving the GPU idle between iterations)
 
 
 class Sequence:
@@ -423,9 +427,9 @@ class DotaOptimizer:
             pool.data[k][:n].copy_(data[k][:n])
         return pool
 
-    def _sync_running(self):
-        """Mirror the device EMA state into the host RunningMeanStd (metrics + checkpoint)."""
-        e = self.ema.cpu()
+    def _sync_running(self, ema: Optional[torch.Tensor] = None):
+        """Mirror the device EMA state (or a snapshot of it) into the host RunningMeanStd (metrics + checkpoint)."""
+        e = (self.ema if ema is None else ema).cpu()
         for team, k in self.team_keys.items():
             if e[k, 2] != 0:
                 self.running.mean[team] = float(e[k, 0])
@@ -462,6 +466,7 @@ class DotaOptimizer:
         end = self.iteration_start + iterations if iterations is not None else cfg.iterations
         try:
             for it in range(self.iteration_start, end):
+                self._last_iteration = it == end - 1      # no look-ahead: nothing would train on it
                 self.run_iteration(it)
         finally:
             self.close()
@@ -512,7 +517,12 @@ class DotaOptimizer:
         rollouts: List[Rollout] = []
         n_seq = 0
         staged = None
-        if self._pipelined():
+        ahead = getattr(self, '_lookahead', None)
+        self._lookahead = None
+        if ahead is not None:
+            # taken and expanded on the device by the previous iteration, behind its training steps
+            rollouts, n_seq, n_ahead, data_ahead = ahead
+        elif self._pipelined():
             # staged (decoded, packed, uploaded) by the stager thread while the previous iteration trained
             staged = self._ingest_pipeline(thread=True).get()
             rollouts, n_seq = staged.rollouts, staged.n_seq
@@ -537,13 +547,16 @@ class DotaOptimizer:
         self.timer.stop('ingest')
         # all sequences of this iteration go to the device once; minibatches are gathered on-device
         self.timer.start('h2d')
-        n = self._agree_steps(n_seq - n_seq % cfg.batch_size)
-        if staged is not None:
-            data = self._finish_ingest(staged, n)
-        elif self.ingest == 'device':
-            data = self._ingest_device(rollouts, n)
+        if ahead is not None:
+            n, data = n_ahead, data_ahead
         else:
-            data = self._to_device(experiences[:n])
+            n = self._agree_steps(n_seq - n_seq % cfg.batch_size)
+            if staged is not None:
+                data = self._finish_ingest(staged, n)
+            elif self.ingest == 'device':
+                data = self._ingest_device(rollouts, n)
+            else:
+                data = self._to_device(experiences[:n])
         self.timer.stop('h2d')
         self.timer.start('train')
         losses, metrics_acc = [], {}
@@ -570,6 +583,22 @@ class DotaOptimizer:
                 losses.append(m['loss'])
                 for k, v in m.items():
                     metrics_acc.setdefault(k, []).append(v)
+        ema_snap = None
+        if self._pipelined() and cfg.lookahead_ingest and not getattr(self, '_last_iteration', False):
+            # the next iteration's rollouts: staged data taken now and expanded + scanned on the device behind this
+            # iteration's steps (the pool / replay copy above already holds this iteration's rows); the EMA state
+            # this iteration reports is snapshotted first (the look-ahead scan advances it)
+            ema_snap = self.ema.clone() if self.ingest == 'device' else None
+            self.timer.stop('train')
+            self.timer.start('lookahead')
+            st2 = self._ingest_pipeline(thread=True).get()
+            if self.consumed is not None:
+                self.consumed.extend((r.game_id, int(r.team_id), int(r.player_id), int(r.weight_version), r.length)
+                                     for r in st2.rollouts)
+            n2 = self._agree_steps(st2.n_seq - st2.n_seq % cfg.batch_size)
+            self._lookahead = (st2.rollouts, st2.n_seq, n2, self._finish_ingest(st2, n2))
+            self.timer.stop('lookahead')
+            self.timer.start('train')
         if self.device.type == 'cuda':
             # a blocking-sync event: the host thread sleeps until the GPU is done instead of spinning a core that
             # the node's actor threads (same CPU share) can use
@@ -585,7 +614,7 @@ class DotaOptimizer:
         self.learner.check_error()
         n_steps = n_seq * cfg.seq_len
         if self.ingest == 'device':
-            self._sync_running()
+            self._sync_running(ema_snap)
         now = time.time()
         steps_per_s = n_steps / max(now - self.time_last_step, 1e-9)
         self.time_last_step = now
