@@ -120,7 +120,7 @@ def _learner_loop(opt, duration, warmup_iterations, max_iterations, counters, ch
         rows.append((m[DotaOptimizer.SPEED_KEY], m['avg_weight_age'], m['avg_rollout_len'],
                      m.get('time/train', float('nan')), m.get('time/ingest', float('nan')), m['experience_steps'],
                      m.get('time/h2d', float('nan')), m.get('time/log', float('nan')),
-                     m.get('time/publish', float('nan'))))
+                     m.get('time/publish', float('nan')), m.get('time/lookahead', 0.0)))
         e = check()
         if e:
             raise e
@@ -148,6 +148,8 @@ def _summary(rows, wall, actor_steps, dropped, games, config):
         'h2d_ms_per_iteration': 1e3 * float(a[:, 6].mean()) if n_it else float('nan'),
         'log_ms_per_iteration': 1e3 * float(a[:, 7].mean()) if n_it else float('nan'),
         'publish_ms_per_iteration': 1e3 * float(a[:, 8].mean()) if n_it else float('nan'),
+        # taking + expanding the next iteration's rollouts while this one's steps run (look-ahead ingest)
+        'lookahead_ms_per_iteration': 1e3 * float(a[:, 9].mean()) if n_it else float('nan'),
         'actor_steps_per_s': actor_steps / wall,
         'queue_dropped': int(dropped), 'games': games, 'config': config,
     }
