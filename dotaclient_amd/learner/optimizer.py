@@ -259,13 +259,15 @@ class DotaOptimizer:
         are dropped and counted in ``prefetch_dropped``."""
         pf = getattr(self, '_prefetcher', None)
         pl = getattr(self, '_pipeline', None)
-        if pl is not None:
-            self.prefetch_dropped = pl.close()
+        dropped = 0
+        if pl is not None:                   # the stager first: its fetch returns None once it is stopping
+            dropped += pl.close()
             self._pipeline = None
         if pf is not None or pl is not None:
             if pf is not None:
-                self.prefetch_dropped = pf.close()
+                dropped += pf.close()
                 self._prefetcher = None
+            self.prefetch_dropped = dropped
             xb = getattr(self, '_xp_broker', None)
             if xb is not None and xb is not self.broker and hasattr(xb, 'close'):
                 xb.close()
@@ -362,13 +364,18 @@ class DotaOptimizer:
         if pl is None:
             from .ingest import IngestPipeline
             H = self.policy_cfg.hidden if self.policy.is_recurrent else 0
+            fetch = None
             if thread:
                 # a blocking client of its own when the broker has one (TCP): the main thread's broker calls
                 # (queue size, model publish) must not wait behind the stager's long polls
                 mk = getattr(self.broker, 'consumer', None)
                 self._xp_broker = mk() if mk is not None else self.broker
-            pl = self._pipeline = IngestPipeline(self._consume_decode if thread else None, self.cfg.seq_len,
-                                                 self.cfg.seq_per_epoch, self.cfg.algo, H, self.device)
+                # consume + decode (CRC with the GIL released) on a thread of their own, so the stager packs and
+                # uploads iteration k+1 while the rollouts of k+2 are being decoded
+                pf = self._prefetcher = _RolloutPrefetcher(self._consume_decode, self.cfg.prefetch_rollouts)
+                fetch = pf.get_until
+            pl = self._pipeline = IngestPipeline(fetch, self.cfg.seq_len, self.cfg.seq_per_epoch, self.cfg.algo, H,
+                                                 self.device)
         return pl
 
     def _finish_ingest(self, st, n_keep: int) -> Dict[str, torch.Tensor]:
@@ -828,6 +835,18 @@ class _RolloutPrefetcher:
                     raise self.err
                 if not self.th.is_alive():
                     raise RuntimeError('experience prefetch thread exited')
+
+    def get_until(self, stop) -> Optional[Rollout]:
+        """:meth:`get` for a consumer thread of its own (the ingest stager): None once ``stop`` is set."""
+        while not stop.is_set():
+            try:
+                return self.q.get(timeout=0.05)
+            except self._queue_mod.Empty:
+                if self.err is not None:
+                    raise self.err
+                if not self.th.is_alive():
+                    raise RuntimeError('experience prefetch thread exited')
+        return None
 
     def close(self) -> int:
         """Stop and join the thread (it polls the queue in bounded slices); returns the decoded rollouts dropped."""
