@@ -45,12 +45,12 @@ def main(N=11200):
     torch.cuda.synchronize()
     C.attn_block_bwd(*args, tr)
     torch.cuda.synchronize()
-    t = tr.view(64, 4, 8).cpu().numpy().astype(np.float64) * 10.0
+    t = tr.view(64, 4, 8).cpu().numpy().astype(np.float64) * 10.0          # ns (100 MHz counter)
     out = {'N': N, 'kernel_ms': ev[0].elapsed_time(ev[1]) / 5}
     names = ['demb', 'dO_gemm', 'attention', 'dxn_partials', 'ln_bwd', 'ln_partials']
     for k, nm in enumerate(names):
-        out[nm + '_us'] = float(np.median(t[:, :, k + 1] - t[:, :, k]))
-    out['row_us'] = float(np.median(t[:, :, 6] - t[:, :, 0]))
+        out[nm + '_us'] = float(np.median(t[:, :, k + 1] - t[:, :, k])) / 1e3
+    out['row_us'] = float(np.median(t[:, :, 6] - t[:, :, 0])) / 1e3
     print(json.dumps(out), flush=True)
 
 
