@@ -631,6 +631,21 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
   }
 
   PSTAMP(3);
+  // the LayerNorm phase's operands — this thread's 32 columns of E0' (HBM), ∂E1 (written in phase 0, L2), μ, rstd
+  // — requested now, so their round trips overlap the ∂Xn products (they were two exposed trips of a 9.6 µs phase)
+  const int lu = tid >> 2, lc0 = 32 * (tid & 3);
+  f32x4 e0pre[8], de1pre[8];
+  float mu_pre, rs_pre;
+  {
+    const size_t row = rbase + lu;
+#pragma unroll
+    for (int j4 = 0; j4 < 8; ++j4) {
+      e0pre[j4] = *reinterpret_cast<const f32x4*>(P.e0 + row * kD + lc0 + 4 * j4);
+      de1pre[j4] = *reinterpret_cast<const f32x4*>(P.de1 + row * kD + lc0 + 4 * j4);
+    }
+    mu_pre = P.mu[row];
+    rs_pre = P.rs[row];
+  }
   // ---- 3: ∂Xn partial of head h: A = ∂Xᵀ accumulators (m = unit, k = d), B = W_qkv rows 128x + 32h + 16t + …
   {
     bf16x4v ah[3][2][4], al[3][2][4];
@@ -680,9 +695,9 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
   PSTAMP(4);
   // ---- 4: LayerNorm backward + residual, 4 threads per unit row (32 columns each)
   {
-    const int u = tid >> 2, c0 = 32 * (tid & 3);
+    const int u = lu, c0 = lc0;
     const size_t row = rbase + u;
-    const float mu = P.mu[row], rs = P.rs[row];
+    const float mu = mu_pre, rs = rs_pre;
     float dxn[32], xh[32];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -692,10 +707,9 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
       const float4 p1 = *reinterpret_cast<const float4*>(&sm[1 * kSlot + u * kPT + c]);
       const float4 p2 = *reinterpret_cast<const float4*>(&sm[2 * kSlot + u * kPT + c]);
       const float4 p3 = *reinterpret_cast<const float4*>(&sm[3 * kSlot + u * kPT + c]);
-      const float4 e = *reinterpret_cast<const float4*>(P.e0 + row * kD + c);
       const float pv[4][4] = {{p0.x, p0.y, p0.z, p0.w}, {p1.x, p1.y, p1.z, p1.w}, {p2.x, p2.y, p2.z, p2.w},
                               {p3.x, p3.y, p3.z, p3.w}};
-      const float ev[4] = {e.x, e.y, e.z, e.w};
+      const float ev[4] = {e0pre[j4][0], e0pre[j4][1], e0pre[j4][2], e0pre[j4][3]};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float d = ((pv[0][q] + pv[1][q]) + pv[2][q]) + pv[3][q];
@@ -717,8 +731,7 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
 #pragma unroll
     for (int j4 = 0; j4 < 8; ++j4) {
       const int c = c0 + 4 * j4;
-      const float4 r1 = *reinterpret_cast<const float4*>(P.de1 + row * kD + c);
-      const float rv[4] = {r1.x, r1.y, r1.z, r1.w};
+      const float rv[4] = {de1pre[j4][0], de1pre[j4][1], de1pre[j4][2], de1pre[j4][3]};
       float o[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
