@@ -99,6 +99,8 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     use_cuda = torch.cuda.is_available()
     shared = os.environ.get('DCA_SHARED_GPU') == '1'          # rehearsal: every rank on GPU 0
+    if shared:      # the ranks' persistent recurrence kernels contend for CUs: the longer hand-off timeout
+        os.environ.setdefault('DCA_TEAM_PATIENT', '1')
     device = torch.device(f'cuda:{0 if shared else local}' if use_cuda else 'cpu')
     if use_cuda:
         torch.cuda.set_device(device)

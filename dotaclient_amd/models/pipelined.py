@@ -223,10 +223,10 @@ _DX_FUSED = os.environ.get('DCA_DX_FUSED', '1') != '0'
 # (ops/csrc/attn_block.hip) instead of ln_fwd + hipBLASLt + attn_fwd + hipBLASLt + pool (DCA_ATTN_FUSED=0)
 _ATTN_FUSED = os.environ.get('DCA_ATTN_FUSED', '1') != '0'
 # fp32 5v5: the block BACKWARD (∂E1 routing, ∂O, attention backward, ∂Xn, LayerNorm backward) as ONE kernel
-# (ops/csrc/attn_block.hip) instead of demb + hipBLASLt + attn_bwd + hipBLASLt + ln_bwd. Opt-in (DCA_ATTN_BWD_FUSED=1):
-# measured 1936 µs per step against 1858 µs for the five launches it replaces — one 135 KB / 405-register workgroup
-# per CU leaves every phase's memory round trips exposed (see the kernel's notes)
-_ATTN_BWD_FUSED = os.environ.get('DCA_ATTN_BWD_FUSED', '0') == '1'
+# (ops/csrc/attn_block.hip) instead of demb + hipBLASLt + attn_bwd + hipBLASLt + ln_bwd (DCA_ATTN_BWD_FUSED=0).
+# Measured 1843 µs per step against 1858 µs for the five launches it replaces once the LayerNorm operands are
+# prefetched during the ∂Xn products (profiles/r3_5v5_backward_fusions.md)
+_ATTN_BWD_FUSED = os.environ.get('DCA_ATTN_BWD_FUSED', '1') != '0'
 # fp32 5v5 (unfused backward): ∂Xn = ∂QKV·W_qkv with the LayerNorm backward as its epilogue, one hand-written kernel
 # instead of a hipBLASLt GEMM + ln_bwd. Opt-in (DCA_DXN_LN_FUSED=1): measured 1033 µs per step against 631 µs for
 # hipBLASLt (350) + ln_bwd (281) — one timestep row per workgroup leaves too few bytes in flight per CU

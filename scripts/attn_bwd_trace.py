@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Phase timestamps (s_memrealtime, 10 ns) of the fused fp32 5v5 block backward (ops/csrc/attn_block.hip,
-opt-in DCA_ATTN_BWD_FUSED=1) at the learner shape N = 11 200 rows: per-phase µs of rows 0-63 (median over rows and
+the 5v5 fp32 default; DCA_ATTN_BWD_FUSED=0 selects the chain) at the learner shape N = 11 200 rows: per-phase µs of rows 0-63 (median over rows and
 waves) and the kernel time. Phases: 0 ∂E1, 1 ∂O GEMM, 2 attention backward (+ ∂QKV store), 3 ∂Xn partials,
 4 LayerNorm backward, 5 the row's LN partial sums."""
 import json
