@@ -744,10 +744,12 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
     }
     __syncthreads();                                      // every thread has read the ∂Xn partial slots
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
-      sm[0 * kSlot + u * kPT + c0 + j] = dxn[j] * xh[j];
-      sm[1 * kSlot + u * kPT + c0 + j] = dxn[j];
-      sm[2 * kSlot + u * kPT + c0 + j] = de0v[j];
+    for (int j = 0; j < 32; j += 4) {                     // 16-byte LDS stores (kPT and c0 are multiples of 4)
+      float* s0 = &sm[0 * kSlot + u * kPT + c0 + j];
+      *reinterpret_cast<float4*>(s0) =
+          make_float4(dxn[j] * xh[j], dxn[j + 1] * xh[j + 1], dxn[j + 2] * xh[j + 2], dxn[j + 3] * xh[j + 3]);
+      *reinterpret_cast<float4*>(s0 + kSlot) = make_float4(dxn[j], dxn[j + 1], dxn[j + 2], dxn[j + 3]);
+      *reinterpret_cast<float4*>(s0 + 2 * kSlot) = make_float4(de0v[j], de0v[j + 1], de0v[j + 2], de0v[j + 3]);
     }
   }
   __syncthreads();
@@ -761,9 +763,19 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
       const int t = (e - 2 * kD) >> 7;
       sl = 2; c = e & 127; u0 = P.off[t]; u1 = P.off[t + 1];
     }
-    float v = 0.f;
-    for (int u = u0; u < u1; ++u) v += sm[sl * kSlot + u * kPT + c];
-    P.part[(size_t)n * kLnW + e] = v;
+    // four interleaved accumulators (fixed order): the serial LDS-load → add chain was the phase's latency
+    const float* col = sm + sl * kSlot + c;
+    float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f;
+    int u = u0;
+#pragma unroll 2
+    for (; u + 4 <= u1; u += 4) {
+      a0 += col[u * kPT];
+      a1 += col[(u + 1) * kPT];
+      a2 += col[(u + 2) * kPT];
+      a3 += col[(u + 3) * kPT];
+    }
+    for (; u < u1; ++u) a0 += col[u * kPT];
+    P.part[(size_t)n * kLnW + e] = (a0 + a1) + (a2 + a3);
   }
   PSTAMP(6);
 #undef PSTAMP
