@@ -634,7 +634,7 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
   // the LayerNorm phase's operands — this thread's 32 columns of E0' (HBM), ∂E1 (written in phase 0, L2), μ, rstd
   // — requested now, so their round trips overlap the ∂Xn products (they were two exposed trips of a 9.6 µs phase)
   const int lu = tid >> 2, lc0 = 32 * (tid & 3);
-  f32x4 e0pre[8], de1pre[8];
+  f32x4 e0pre[8], de1pre[8], gpre[8], bpre[8];
   float mu_pre, rs_pre;
   {
     const size_t row = rbase + lu;
@@ -642,6 +642,8 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
     for (int j4 = 0; j4 < 8; ++j4) {
       e0pre[j4] = *reinterpret_cast<const f32x4*>(P.e0 + row * kD + lc0 + 4 * j4);
       de1pre[j4] = *reinterpret_cast<const f32x4*>(P.de1 + row * kD + lc0 + 4 * j4);
+      gpre[j4] = *reinterpret_cast<const f32x4*>(P.gamma + lc0 + 4 * j4);
+      bpre[j4] = *reinterpret_cast<const f32x4*>(P.bout + lc0 + 4 * j4);
     }
     mu_pre = P.mu[row];
     rs_pre = P.rs[row];
@@ -713,10 +715,10 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const float d = ((pv[0][q] + pv[1][q]) + pv[2][q]) + pv[3][q];
-        const float x = (ev[q] - P.bout[c + q] - mu) * rs;
+        const float x = (ev[q] - bpre[j4][q] - mu) * rs;
         dxn[4 * j4 + q] = d;
         xh[4 * j4 + q] = x;
-        const float g = d * P.gamma[c + q];
+        const float g = d * gpre[j4][q];
         s1 += g;
         s2 += g * x;
       }
@@ -736,7 +738,7 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int j = 4 * j4 + q;
-        const float g = dxn[j] * P.gamma[c + q];
+        const float g = dxn[j] * gpre[j4][q];
         o[q] = rv[q] + rs * (g - s1 - xh[j] * s2);
         de0v[j] = o[q];
       }
