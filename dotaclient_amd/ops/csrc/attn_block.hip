@@ -419,6 +419,15 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
 #define PSTAMP(ev)                                                                                        \
   if (P.trace && n < 64 && lane == 0) P.trace[((size_t)n * 4 + w) * 8 + (ev)] = __builtin_amdgcn_s_memrealtime()
   PSTAMP(0);
+  // phase 1's W_outᵀ fragments (head w) requested first: their round trip runs alongside phase 0's
+  bf16x8 wfh[4][2], wfl[4][2];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      wfh[ks][t] = gfrag(P.woth, kHd * w + 16 * t, 32 * ks, lane);
+      wfl[ks][t] = gfrag(P.wotl, kHd * w + 16 * t, 32 * ks, lane);
+    }
   // ---- 0: ∂E1 (thread: column c, units 32·(tid>>7) … +31)
   if (tid < kU) sd[tid] = P.dtl[(size_t)n * kU + tid];
   __syncthreads();
@@ -455,18 +464,12 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
     for (int t = 0; t < 2; ++t) dO[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
-    bf16x8 bh[2], bl[2];
-#pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      bh[t] = gfrag(P.woth, kHd * h + 16 * t, 32 * ks, lane);
-      bl[t] = gfrag(P.wotl, kHd * h + 16 * t, 32 * ks, lane);
-    }
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       bf16x8 ah, al;
       split8v(&sm[(16 * a + li) * kPT + 32 * ks + 8 * kg], ah, al);
 #pragma unroll
-      for (int t = 0; t < 2; ++t) dO[a][t] = mfma3(ah, al, bh[t], bl[t], dO[a][t]);
+      for (int t = 0; t < 2; ++t) dO[a][t] = mfma3(ah, al, wfh[ks][t], wfl[ks][t], dO[a][t]);
     }
   }
   __syncthreads();                                        // slot 0 (∂E1 image) is wave 0's from here on
