@@ -224,7 +224,7 @@ _DX_FUSED = os.environ.get('DCA_DX_FUSED', '1') != '0'
 _ATTN_FUSED = os.environ.get('DCA_ATTN_FUSED', '1') != '0'
 # fp32 5v5: the block BACKWARD (∂E1 routing, ∂O, attention backward, ∂Xn, LayerNorm backward) as ONE kernel
 # (ops/csrc/attn_block.hip) instead of demb + hipBLASLt + attn_bwd + hipBLASLt + ln_bwd (DCA_ATTN_BWD_FUSED=0).
-# Measured 1720 µs per step against 1858 µs for the five launches it replaces (5v5 step 8.24 vs 8.39 ms, same box;
+# Measured 1660 µs per step against 1858 µs for the five launches it replaces (5v5 step 8.11 vs 8.33 ms, same box;
 # profiles/r3_5v5_backward_fusions.md)
 _ATTN_BWD_FUSED = os.environ.get('DCA_ATTN_BWD_FUSED', '1') != '0'
 # fp32 5v5 (unfused backward): ∂Xn = ∂QKV·W_qkv with the LayerNorm backward as its epilogue, one hand-written kernel

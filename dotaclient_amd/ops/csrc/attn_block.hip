@@ -457,6 +457,22 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
   PSTAMP(1);
   // ---- 1: ∂O of head h = w: dO[a][t] lane (unit i = 16a + 4kg + r, d = 16t + li within the head)
   const int h = w;
+  // phase 2's O and LSE operands for D_i (query rows 16a + 4kg + r, this lane's two d columns), requested before the
+  // ∂O products so their round trips overlap them
+  float opre[4][4][2], Lr[4][4];
+  {
+    const float* ob = P.o + rbase * kD + kHd * h;
+    const float* lb = P.lse + ((size_t)n * 4 + h) * kU;
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = 16 * a + 4 * kg + r;
+        opre[a][r][0] = ob[(size_t)i * kD + li];
+        opre[a][r][1] = ob[(size_t)i * kD + 16 + li];
+        Lr[a][r] = lb[i];
+      }
+  }
   f32x4 dO[4][2];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
@@ -491,20 +507,11 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
       *reinterpret_cast<bf16x4v*>(dTl + (16 * t + li) * kPS + 16 * a + 4 * kg) = lo;
     }
   // D_i = Σ_d ∂O[i][d]·O[i][d] and LSE_i for i = 16a + 4kg + r (the lane's query rows in the S layout below)
-  float Dr[4][4], Lr[4][4];
-  {
-    const float* ob = P.o + rbase * kD + kHd * h;
-    const float* lb = P.lse + ((size_t)n * 4 + h) * kU;
+  float Dr[4][4];
 #pragma unroll
-    for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < 4; ++a)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int i = 16 * a + 4 * kg + r;
-        const float v = dO[a][0][r] * ob[(size_t)i * kD + li] + dO[a][1][r] * ob[(size_t)i * kD + 16 + li];
-        Dr[a][r] = row_sum16(v);
-        Lr[a][r] = lb[i];
-      }
-  }
+    for (int r = 0; r < 4; ++r) Dr[a][r] = row_sum16(dO[a][0][r] * opre[a][r][0] + dO[a][1][r] * opre[a][r][1]);
   lds_wait();
   // S = Q·Kᵀ and dP = ∂O·Vᵀ, i-major: p[a][b] lane (query i = 16a + 4kg + r, key j = 16b + li)
   f32x4 p[4][4], dp[4][4];
