@@ -430,8 +430,8 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
     }
   // ---- 0: ∂E1 (thread: column c, units 32·(tid>>7) … +31)
   if (tid < kU) sd[tid] = P.dtl[(size_t)n * kU + tid];
-  __syncthreads();
   {
+    // this thread's column operands are requested before the barrier, alongside the ∂logit load
     const int c = tid & 127, uh = tid >> 7;
     const float qc = P.q[(size_t)n * P.ldq + c];
     int au[6];
@@ -442,6 +442,7 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
       au[t] = P.off[src] + P.arg[((size_t)n * 6 + t) * kD + c];
       dp[t] = P.dx[(size_t)n * 896 + kD + t * kD + c];
     }
+    __syncthreads();
 #pragma unroll 4
     for (int i = 0; i < 32; ++i) {
       const int u = uh * 32 + i;
