@@ -56,7 +56,7 @@ def parse():
     ap.add_argument('--model', default='lstm512')
     ap.add_argument('--backend', default='auto', choices=['auto', 'fused', 'torch'])
     ap.add_argument('--algo', default='ppo', choices=['ppo', 'vpg'])
-    ap.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'],
+    ap.add_argument('--precision', default='fp32', choices=['fp32', 'fp32-exact', 'bf16'],
                     help='fp32 = the reference\'s training precision (headline); bf16 = bf16 GEMM operands')
     ap.add_argument('--bf16-extra', type=int, default=1,
                     help='also time the bf16 learner (reported as an extra field, not the headline)')

@@ -150,10 +150,18 @@ class WeightImages:
                 return t.reshape(t.shape[0], t.shape[1] // 32, 32).permute(1, 0, 2).contiguous()
             wpre_i = idx('affine_pre_rnn.weight')
             wih_i = idx('rnn.weight_ih_l0')[perm]
-            if wpre_i.shape[1] % 128 == 0 and wih_i.shape[0] % 128 == 0:
+            if getattr(fp, 'exact', False):
+                # IEEE-fp32 learner: the chain kernels take fp32 weights as they are (no hi / lo images); the heads
+                # GEMM's W_cat zero-padded to 256 rows and its transpose (the ∂h product's operand)
+                if H % 128 == 0:
+                    wcat_p = torch.cat([wcat, neg(256 - LDZ, H)], 0)
+                    parts32['wcat256'] = (wcat_p, None)
+                    parts32['wcatT256'] = (wcat_p.t().contiguous(), None)
+                    parts32['bcat256'] = (torch.cat([bcat, neg(256 - LDZ)]), None)
+            elif wpre_i.shape[1] % 128 == 0 and wih_i.shape[0] % 128 == 0:
                 partsS = {'pre_s': slab(wpre_i), 'ih_s': slab(wih_i), 'dx1_s': slab(wih_i.t()),
                           'dx2_s': slab(wpre_i.t())}
-            if H % 128 == 0:
+            if H % 128 == 0 and not getattr(fp, 'exact', False):
                 # heads GEMM and its ∂X product on the chain kernel's stages: W_cat zero-padded to 256 rows
                 wcat_p = torch.cat([wcat, neg(256 - LDZ, H)], 0)
                 partsS['wcat_s'] = slab(wcat_p)
@@ -237,6 +245,9 @@ _FWD_CHAIN = os.environ.get('DCA_FWD_CHAIN', '1') != '0'
 # fp32 learner: the heads GEMM z = h·W_catᵀ + b and ∂h = ∂z·W_cat on the chain kernel's stages (W_cat padded to 256
 # rows, z / ∂z carried 256 wide) instead of hipBLASLt (DCA_HEADS_ROWMM=0)
 _HEADS_ROWMM = os.environ.get('DCA_HEADS_ROWMM', '1') != '0'
+# IEEE-fp32 learner: the recurrence's gate activations through libm expf / tanhf and an IEEE division
+# (DCA_EXACT_ACT=libm) or through the hardware exp / reciprocal (≈1-2 ulp; 'fast')
+_EXACT_LIBM_ACT = os.environ.get('DCA_EXACT_ACT', 'libm') == 'libm'
 
 
 def fused_step_tm(fp, *args, **kw):
@@ -251,100 +262,6 @@ def fused_step_tm(fp, *args, **kw):
         torch.backends.cuda.matmul.allow_tf32 = prev
 
 
-def _gemm_tn_exact(a, b, out=None, perm=None, accumulate=False, b0=None, colsum=None):
-    """``ops.gemm.gemm_tn`` semantics (C (+)= Aᵀ·B through row map ``perm``, optional B0 rows, optional column sums
-    of A) as exact-f32 hipBLASLt products: the fp32-exact learner's weight gradients.
-
-    Split-K: the K = B·S rows run as ≤ 256-row batched products whose partials are summed afterwards. One long
-    product let the library accumulate each output over all 11 200 rows in one chain — measured 1.8e-5 relative error
-    on the enum head's ∂W (three outputs per row, heavy cancellation) against 9e-8 for the same operands summed in
-    float64 (scripts/exact_stage_diag.py)."""
-    if b0 is not None:
-        b = torch.cat([b0, b])
-    K = a.shape[0]
-    kc = 256
-    nk = (K + kc - 1) // kc
-    if nk > 1:
-        pad = nk * kc - K
-        ap = torch.nn.functional.pad(a, (0, 0, 0, pad)) if pad else a
-        bp = torch.nn.functional.pad(b, (0, 0, 0, pad)) if pad else b
-        c = torch.bmm(ap.reshape(nk, kc, -1).transpose(1, 2), bp.reshape(nk, kc, -1)).sum(0)
-    else:
-        c = a.t() @ b
-    cs = a.sum(0) if colsum is not None else None
-    if perm is not None:
-        idx = perm.long()
-        if out is None:
-            out = torch.zeros(int(perm.numel()), c.shape[1], device=c.device)
-        (out.index_add_ if accumulate else out.index_copy_)(0, idx, c)
-    elif out is None:
-        out = c
-    elif accumulate:
-        out.add_(c)
-    else:
-        out.copy_(c)
-    if cs is not None:
-        colsum.copy_(cs)
-    return out
-
-
-def _encoder_exact(fp, P, units_t, env_t):
-    """The entity encoder (policy.py:97-132 / Policy.encode up to the pre-RNN layer) as exact-f32 torch ops — plain
-    ops, no autograd graph, so the step stays capturable in a hipGraph; pools remember their argmax unit (torch
-    ``max``, the reference's op) for :func:`_encoder_exact_bwd`. Returns x896 (N, 896), emb (N, U, 128), saved."""
-    from ..constants import UNIT_KEYS
-    cfg = fp.cfg
-    sl = cfg.layout.slices()
-    g = lambda n: P[n].detach()    # noqa: E731
-    N, U = units_t.shape[:2]
-    env_e = torch.relu(torch.addmm(g('affine_env.bias'), env_t, g('affine_env.weight').t()))
-    basic = torch.relu(torch.addmm(g('affine_unit_basic_stats.bias'), units_t.reshape(N * U, 10),
-                                   g('affine_unit_basic_stats.weight').t())).view(N, U, -1)
-    emb = torch.empty(N, U, cfg.unit_dim, device=units_t.device, dtype=units_t.dtype)
-    for key, s_ in zip(UNIT_KEYS, TYPE_SUFFIX):
-        a = sl[key]
-        n_u = a.stop - a.start
-        emb[:, a] = torch.addmm(g(f'affine_unit_{s_}.bias'), basic[:, a].reshape(N * n_u, -1),
-                                g(f'affine_unit_{s_}.weight').t()).view(N, n_u, -1)
-    pools, idx = [], []
-    for key in UNIT_KEYS:
-        k = 'enemy_nonheroes' if (cfg.compat_bugs and key == 'enemy_towers') else key
-        m = emb[:, sl[k]].max(dim=1)
-        pools.append(m.values)
-        idx.append((sl[k].start, m.indices))
-    x896 = torch.cat([env_e] + pools, 1)
-    return x896, emb, (env_e, basic, emb, idx, units_t, env_t)
-
-
-def _encoder_exact_bwd(fp, P, saved, dx896, dtl, z):
-    """Encoder parameter gradients (exact-f32 torch ops) from ∂x896 and the pointer head's ∂emb = dtl ⊗ q
-    (q = z[:, :128]); each pooled column routes its gradient to its argmax unit. Returns (dWt (6,128,128),
-    dw1, db1, (dbt (6,128), dWe, dbe))."""
-    from ..constants import UNIT_KEYS
-    env_e, basic, emb, idx, units_t, env_t = saved
-    cfg = fp.cfg
-    sl = cfg.layout.slices()
-    D = emb.shape[2]
-    N, U = units_t.shape[:2]
-    demb = dtl.unsqueeze(2) * z[:, None, :D]
-    for t, (start, ind) in enumerate(idx):
-        dpool = dx896[:, 128 + D * t:128 + D * (t + 1)]
-        demb.scatter_add_(1, (ind + start).unsqueeze(1), dpool.unsqueeze(1))
-    dWt, dbt, dbasic = [], [], torch.empty_like(basic)
-    for key, s_ in zip(UNIT_KEYS, TYPE_SUFFIX):
-        a = sl[key]
-        n_u = a.stop - a.start
-        de = demb[:, a].reshape(N * n_u, D)
-        dWt.append(de.t() @ basic[:, a].reshape(N * n_u, -1))
-        dbt.append(de.sum(0))
-        dbasic[:, a] = (de @ P[f'affine_unit_{s_}.weight'].detach()).view(N, n_u, -1)
-    dpre1 = (dbasic * (basic > 0)).view(N * U, -1)
-    dw1 = dpre1.t() @ units_t.reshape(N * U, 10)
-    db1 = dpre1.sum(0)
-    de_env = dx896[:, :128] * (env_e > 0)
-    return torch.stack(dWt), dw1, db1, (torch.stack(dbt), de_env.t() @ env_t, de_env.sum(0))
-
-
 def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], units_t, env_t, act_t, msk_t, adv_t,
                    ret_t, lpo_t, nret_t, norms, h0, c0, B: int, S: int, gout: Optional[Dict[str, torch.Tensor]] = None):
     """Loss partials and all parameter gradients of one minibatch, from TIME-MAJOR rows (row = t·B + b).
@@ -353,10 +270,12 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     ``gout`` (direct mode): parameter name → gradient tensor (a view of the flat gradient buffer); the big
     weight-gradient GEMMs (W_hh, W_ih, pre-RNN) ACCUMULATE straight into those and are left out of ``grads``.
     Returns (partials (R,16) f32, logp (N) f32 time-major, grads {param name → tensor})."""
-    from ..ops.gemm import gemm_tn
+    from ..ops.gemm import gemm_tn as _gemm_tn
     exact = bool(getattr(fp, 'exact', False))
-    if exact:
-        gemm_tn = _gemm_tn_exact          # noqa: F811 — exact-f32 weight gradients
+
+    def gemm_tn(*a, **k):
+        # weight gradients: split-K MFMA; IEEE-fp32 learner: exact v_mfma_f32_16x16x4_f32 (ops/csrc/gemm_tn.hip)
+        return _gemm_tn(*a, exact=exact, **k)
     C = fp.C
     cfg, lc = fp.cfg, fp.loss_cfg
     N = B * S
@@ -376,12 +295,8 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     f32 = bool(getattr(fp, 'fp32', False))    # fp32-accurate learner: fp32 activations, bf16x3 MFMA, exact-f32 GEMMs
     adt = torch.float32 if f32 else torch.bfloat16
     # (x896 / emb come back in the weights' dtype: bf16, or fp32 from the bf16x3 encoder)
-    enc_graph = None
-    if exact:
-        x896, emb, enc_graph = _encoder_exact(fp, P, units_t, env_t)
-        arg = None
-    else:
-        x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs))
+    # (exact: the IEEE-fp32 variant, ops/csrc/encoder.hip encoder_fwd_x_kernel)
+    x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs), exact=exact)
     attn32 = attn and f32
     if attn32:
         # 5v5 entity attention at fp32 (ops/csrc/attn.hip fp32 kernels: LayerNorm, bf16x3 attention core, pools; the
@@ -427,11 +342,16 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         E1 = torch.addmm(E0p, Oat, W['wout16'].t())                 # residual + out-projection, bf16
         arg = C.attn_pool(E1, toff, x896, bool(cfg.compat_bugs))    # pools of the attended embeddings
         emb = E1.view(N, U, 128)
-    elif cfg.compat_bugs and not exact:   # reference policy.py:127: enemy-tower pool = enemy-nonhero pool
+    elif cfg.compat_bugs:   # reference policy.py:127: enemy-tower pool = enemy-nonhero pool
         x896[:, 768:896] = x896[:, 512:640]
         arg[:, 5] = arg[:, 3]
     # relu(x896·W_preᵀ + b) as ONE hipBLASLt GEMM with a bias+ReLU epilogue, bf16 (fp32) out (x16 > 0 ⟺ x > 0)
-    if f32 and not exact and _FWD_CHAIN:
+    if exact:
+        # IEEE-fp32 forward chain: the same kernel on v_mfma_f32_16x16x4_f32 with the fp32 weights as they are
+        nil = wpre16.new_empty(0)
+        x16, xp = C.pre_rnn_chain(x896, wpre16, nil, W['bpre16'], wih16, nil)
+        xp4 = xp.view(S, B, H, 4)
+    elif f32 and _FWD_CHAIN:
         if 'pre_s' in W:                 # hi / lo images from the step's weight_prep launch
             fw1, fw2 = W['pre_s'], W['ih_s']
         else:
@@ -467,7 +387,8 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     with torch.cuda.stream(sL):
         for t0, t1 in spans:
             o = team_fwd(C, xp4[t0:t1], whh16, h_c, c_c, fp.err, False, time_major=True,
-                         hs_out=hs16[t0:t1], cs_out=cs[t0:t1], gates_out=gates4[t0:t1], bias4=bias_p, precise=exact)
+                         hs_out=hs16[t0:t1], cs_out=cs[t0:t1], gates_out=gates4[t0:t1], bias4=bias_p,
+                         precise=exact and _EXACT_LIBM_ACT)
             h_c, c_c = o[4], o[5]
             e = torch.cuda.Event()
             e.record(sL)
@@ -482,13 +403,21 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             dx_w = tuple(W['dx1_s']) + tuple(W['dx2_s'])
         else:
             dx_w = tuple(C.split_bf16x2(W['wihT16'], True)) + tuple(C.split_bf16x2(W['wpreT'], True))
-    rowmm = one and f32 and not exact and _HEADS_ROWMM and 'wcat_s' in W
+    # heads GEMM + its ∂X product on the chain kernel's stages (bf16x3 images, or exact: fp32 W_cat padded to 256)
+    if exact and 'wcat256' in W:
+        nil = W['wcat256'].new_empty(0)
+        hw = ((W['wcat256'], nil), (W['wcatT256'], nil), W['bcat256'])
+    elif 'wcat_s' in W:
+        hw = (W['wcat_s'], W['wcatT_s'], W['bcat256'])
+    else:
+        hw = None
+    rowmm = one and f32 and _HEADS_ROWMM and hw is not None
     for (t0, t1), done in zip(spans, fwd_done):
         main.wait_event(done)
         r0, r1 = t0 * B, t1 * B
         xh = hs16[t0:t1].view(-1, H)
         if rowmm:
-            zc = C.rowmm_out256(xh, W['wcat_s'][0], W['wcat_s'][1], W['bcat256'])   # (n, 256), padding columns 0
+            zc = C.rowmm_out256(xh, hw[0][0], hw[0][1], hw[2])   # (n, 256), padding columns 0
         else:
             zc = _addmm(bcat, xh, wcat16.t())     # bias in the GEMM epilogue
         # ∂L/∂z straight in the GEMM operand dtype: only the backward GEMMs read it
@@ -511,7 +440,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         if one:
             z, dtl, logp = zc, dtl_c, lp
             if rowmm:
-                dxh = C.rowmm_in256(dz16, W['wcatT_s'][0], W['wcatT_s'][1]).view(S, B, H)
+                dxh = C.rowmm_in256(dz16, hw[1][0], hw[1][1]).view(S, B, H)
             else:
                 dxh = _mm(dz16, wcat16).view(S, B, H)
         else:
@@ -554,7 +483,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             cinit = c0.contiguous() if t0 == 0 else cs[t0 - 1]
             o = team_bwd(C, dxh[t0:t1], gates4[t0:t1], cs[t0:t1], cinit, dh_n, dc_n, whh16, fp.err,
                          time_major=True, dg_out=dgates16[t0:t1], dg_bf16=not f32,
-                         want_dbias=True, precise=exact)
+                         want_dbias=True, precise=exact and _EXACT_LIBM_ACT)
             dh_n, dc_n = o[1], o[2]
             db = _acc(db, o[3])
             e = torch.cuda.Event()
@@ -678,17 +607,15 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             return C.enc_small_grads(z[r0:r1], dtl[r0:r1], fp.type_offsets(dev), dx896, env_t[r0:r1], we, be,
                                      bool(cfg.compat_bugs))
         small = None
-        if exact:
-            dwt_c, dw1_c, db1_c, small = _encoder_exact_bwd(fp, P, enc_graph, dx896, dtl[r0:r1], z[r0:r1])
-        elif wg_side:
+        if wg_side:
             sL.wait_stream(main)
             with torch.cuda.stream(sL):
                 small = small_grads()
                 wg_done = torch.cuda.Event()
                 wg_done.record(sL)
-        if not exact:
-            dwt_c, dw1_c, db1_c = C.encoder_bwd(units_t[r0:r1], w1, b1, wtT16, dtl[r0:r1], z[r0:r1],
-                                                dx896, arg[r0:r1], counts, bool(cfg.compat_bugs), demb_in=demb_in)
+        dwt_c, dw1_c, db1_c = C.encoder_bwd(units_t[r0:r1], w1, b1, wtT16, dtl[r0:r1], z[r0:r1],
+                                            dx896, arg[r0:r1], counts, bool(cfg.compat_bugs), demb_in=demb_in,
+                                            exact=exact)
         dw1 = _acc(dw1, dw1_c)
         db1 = _acc(db1, db1_c)
         dWt = _acc(dWt, dwt_c)

@@ -283,11 +283,12 @@ std::vector<torch::Tensor> heads_loss(torch::Tensor z, torch::Tensor emb, torch:
 // (N,6,128)); x896 / emb have wt's dtype (f32: the fp32-accurate bf16x3 variant).
 std::vector<torch::Tensor> encoder_fwd(torch::Tensor units, torch::Tensor env, torch::Tensor w1, torch::Tensor b1,
                                        torch::Tensor wt, torch::Tensor bt, torch::Tensor we, torch::Tensor be,
-                                       std::vector<int64_t> counts, bool compat) {
+                                       std::vector<int64_t> counts, bool compat, bool exact) {
   CHECK_F32(units); CHECK_F32(env); CHECK_F32(w1); CHECK_F32(b1); CHECK_DEV(wt); CHECK_CONTIG(wt); CHECK_F32(bt);
   CHECK_F32(we); CHECK_F32(be);
   const bool f32w = wt.scalar_type() == at::kFloat;
   TORCH_CHECK(f32w || wt.scalar_type() == at::kBFloat16, "wt must be bf16 or f32");
+  TORCH_CHECK(!exact || f32w, "encoder_fwd: exact mode needs fp32 weights");
   TORCH_CHECK(units.dim() == 3 && units.size(2) == 10, "units must be (N,U,10)");
   const int N = units.size(0), U = units.size(1);
   TORCH_CHECK(env.size(0) == N && env.size(1) == 3, "env must be (N,3)");
@@ -305,7 +306,7 @@ std::vector<torch::Tensor> encoder_fwd(torch::Tensor units, torch::Tensor env, t
   auto arg = torch::empty({N, 6, 128}, o.dtype(at::kByte));
   hip_check(dca_encoder_fwd(ptr<float>(units), ptr<float>(env), ptr<float>(w1), ptr<float>(b1), wt.data_ptr(),
                             ptr<float>(bt), ptr<float>(we), ptr<float>(be), x896.data_ptr(), emb.data_ptr(),
-                            ptr<unsigned char>(arg), N, U, c, compat ? 1 : 0, cur_stream(), f32w ? 1 : 0),
+                            ptr<unsigned char>(arg), N, U, c, compat ? 1 : 0, cur_stream(), exact ? 2 : (f32w ? 1 : 0)),
             "dca_encoder_fwd");
   return {x896, emb, arg};
 }
@@ -314,11 +315,13 @@ std::vector<torch::Tensor> encoder_fwd(torch::Tensor units, torch::Tensor env, t
 std::vector<torch::Tensor> encoder_bwd(torch::Tensor units, torch::Tensor w1, torch::Tensor b1, torch::Tensor wtT,
                                        torch::Tensor dtl, torch::Tensor q, torch::Tensor dx, torch::Tensor arg,
                                        std::vector<int64_t> counts, bool compat,
-                                       c10::optional<torch::Tensor> demb_in) {
+                                       c10::optional<torch::Tensor> demb_in, bool exact) {
   CHECK_F32(units); CHECK_F32(w1); CHECK_F32(b1); CHECK_DEV(wtT); CHECK_CONTIG(wtT); CHECK_F32(dtl); CHECK_F32(dx);
   CHECK_U8(arg); CHECK_DEV(q); CHECK_DT(q, at::kFloat);
   const bool f32w = wtT.scalar_type() == at::kFloat;
   TORCH_CHECK(f32w || wtT.scalar_type() == at::kBFloat16, "wtT must be bf16 or f32");
+  TORCH_CHECK(!exact || f32w, "encoder_bwd: exact mode needs fp32 weights");
+  TORCH_CHECK(!exact || !(demb_in && demb_in->defined()), "encoder_bwd: exact mode covers the 1v1 encoder (no demb_in)");
   const int N = units.size(0), U = units.size(1);
   TORCH_CHECK(q.dim() == 2 && q.size(0) == N && q.size(1) >= 128 && q.stride(1) == 1 && q.stride(0) % 4 == 0,
               "q must be (N, >=128) with unit column stride and 16-B aligned rows");
@@ -345,7 +348,7 @@ std::vector<torch::Tensor> encoder_bwd(torch::Tensor units, torch::Tensor w1, to
   hip_check(dca_encoder_bwd(ptr<float>(units), ptr<float>(w1), ptr<float>(b1), wtT.data_ptr(), ptr<float>(dtl),
                             ptr<float>(q), (int)q.stride(0), ptr<float>(dx), ptr<unsigned char>(arg), ptr<float>(dwt),
                             ptr<float>(dw1), ptr<float>(db1), ws.data_ptr(), wsb, N, U, c, compat ? 1 : 0,
-                            cur_stream(), dein, f32w ? 1 : 0),
+                            cur_stream(), dein, exact ? 2 : (f32w ? 1 : 0)),
             "dca_encoder_bwd");
   return {dwt, dw1, db1};
 }
@@ -654,7 +657,7 @@ void weight_prep(torch::Tensor src, torch::Tensor map16, torch::Tensor dst16, to
 // accuracy); optional B0 (split_rows,N) supplies rows k < split_rows of the B operand. C (M',N) f32 with unit column
 // stride; optional perm (M) i32 maps result row m → C row perm[m].
 void gemm_tn(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<torch::Tensor> perm, bool accumulate,
-             c10::optional<torch::Tensor> B0, c10::optional<torch::Tensor> colsum) {
+             c10::optional<torch::Tensor> B0, c10::optional<torch::Tensor> colsum, bool exact) {
   CHECK_DEV(A); CHECK_DEV(B); CHECK_DEV(C);
   const bool f32 = A.scalar_type() == at::kFloat;
   TORCH_CHECK((A.scalar_type() == at::kBFloat16 || f32) && B.scalar_type() == A.scalar_type() &&
@@ -700,12 +703,14 @@ void gemm_tn(torch::Tensor A, torch::Tensor B, torch::Tensor C, c10::optional<to
     return;
   }
   int splits, kc, tiles;
-  dca_gemm_tn_plan(M, N, K, &splits, &kc, &tiles, f32 ? 1 : 0);
+  TORCH_CHECK(!exact || f32, "gemm_tn: exact mode needs fp32 operands");
+  const int mode = exact ? 2 : (f32 ? 1 : 0);
+  dca_gemm_tn_plan(M, N, K, &splits, &kc, &tiles, mode);
   torch::Tensor slab;
   if (splits > 1) slab = torch::empty({(int64_t)splits * M * N + (csp ? (int64_t)splits * M : 0)}, C.options());
   hip_check(dca_gemm_tn(A.data_ptr(), (int)A.stride(0), B.data_ptr(), (int)B.stride(0), b0, split_rows,
                         ptr<float>(C), (int)C.stride(0), pp, accumulate ? 1 : 0, M, N, K,
-                        splits > 1 ? ptr<float>(slab) : nullptr, csp, cur_stream(), f32 ? 1 : 0),
+                        splits > 1 ? ptr<float>(slab) : nullptr, csp, cur_stream(), mode),
             "dca_gemm_tn");
 }
 
@@ -792,58 +797,91 @@ std::vector<torch::Tensor> dpre_dx(torch::Tensor dG, torch::Tensor w1h, torch::T
   return {dpre, dx};
 }
 
-// The chain kernel's stages alone (dx_chain.hip, bf16x3, slab-major bf16 hi / lo weight images):
+// The chain kernel's stages alone (dx_chain.hip). bf16x3: slab-major bf16 hi / lo weight images; exact (IEEE fp32
+// products, v_mfma_f32_16x16x4_f32): the fp32 weight itself with wl empty.
 // rowmm_out256: C (N, 256) = A (N, K) · Wᵀ + b with W (256, K) → images (K/32, 256, 32) — stage 1, bias epilogue;
 // rowmm_in256:  C (N, X) = A (N, 256) · Wᵀ with W (X, 256) → images (8, X, 32) — stage 2 on A read from HBM.
 // The 1v1 heads GEMM (W_cat zero-padded to 256 rows) and its ∂X product.
+static bool chain_exact(const torch::Tensor& wh, const torch::Tensor& wl, const char* what) {
+  CHECK_DEV(wh); CHECK_CONTIG(wh);
+  if (wh.scalar_type() == at::kFloat) {
+    TORCH_CHECK(wh.dim() == 2 && wl.numel() == 0, what, ": exact weights are 2-D fp32 with an empty lo image");
+    return true;
+  }
+  CHECK_BF16(wh); CHECK_BF16(wl);
+  TORCH_CHECK(wl.sizes() == wh.sizes(), what, ": hi / lo image shapes");
+  return false;
+}
+
 torch::Tensor rowmm_out256(torch::Tensor A, torch::Tensor wh, torch::Tensor wl, torch::Tensor bias) {
-  CHECK_F32(A); CHECK_F32(bias); CHECK_BF16(wh); CHECK_BF16(wl);
+  CHECK_F32(A); CHECK_F32(bias);
+  const bool exact = chain_exact(wh, wl, "rowmm_out256");
   const int N = A.size(0), K = A.size(1);
   TORCH_CHECK(A.dim() == 2 && K % 128 == 0 && bias.numel() == 256, "rowmm_out256: A (N, K % 128 == 0), bias (256)");
-  TORCH_CHECK(wh.dim() == 3 && wh.size(0) * 32 == K && wh.size(1) == 256 && wh.size(2) == 32 && wl.sizes() == wh.sizes(),
-              "rowmm_out256: slab-major images (K/32, 256, 32)");
+  if (exact) {
+    TORCH_CHECK(wh.size(0) == 256 && wh.size(1) == K, "rowmm_out256: exact W (256, K)");
+  } else {
+    TORCH_CHECK(wh.dim() == 3 && wh.size(0) * 32 == K && wh.size(1) == 256 && wh.size(2) == 32,
+                "rowmm_out256: slab-major images (K/32, 256, 32)");
+  }
   TORCH_CHECK((long long)N * K * 4 <= 0x7fff0000LL, "rowmm_out256: A too large for one launch");
   auto out = torch::empty({N, 256}, A.options());
-  hip_check(dca_dpre_dx(ptr<float>(A), wh.data_ptr(), wl.data_ptr(), ptr<float>(bias), nullptr, nullptr,
-                        ptr<float>(out), nullptr, N, K, 0, 0, 2, cur_stream()),
+  hip_check(dca_dpre_dx(ptr<float>(A), wh.data_ptr(), exact ? nullptr : wl.data_ptr(), ptr<float>(bias), nullptr,
+                        nullptr, ptr<float>(out), nullptr, N, K, 0, exact ? 1 : 0, 2, cur_stream()),
             "dca_dpre_dx(stage 1)");
   return out;
 }
 
 torch::Tensor rowmm_in256(torch::Tensor A, torch::Tensor wh, torch::Tensor wl) {
-  CHECK_F32(A); CHECK_BF16(wh); CHECK_BF16(wl);
+  CHECK_F32(A);
+  const bool exact = chain_exact(wh, wl, "rowmm_in256");
   const int N = A.size(0);
   TORCH_CHECK(A.dim() == 2 && A.size(1) == 256, "rowmm_in256: A (N, 256)");
-  TORCH_CHECK(wh.dim() == 3 && wh.size(0) == 8 && wh.size(2) == 32 && wl.sizes() == wh.sizes() && wh.size(1) % 128 == 0,
-              "rowmm_in256: slab-major images (8, X, 32), X % 128 == 0");
-  const int X = wh.size(1);
+  int X;
+  if (exact) {
+    TORCH_CHECK(wh.size(1) == 256 && wh.size(0) % 128 == 0, "rowmm_in256: exact W (X, 256), X % 128 == 0");
+    X = wh.size(0);
+  } else {
+    TORCH_CHECK(wh.dim() == 3 && wh.size(0) == 8 && wh.size(2) == 32 && wh.size(1) % 128 == 0,
+                "rowmm_in256: slab-major images (8, X, 32), X % 128 == 0");
+    X = wh.size(1);
+  }
   auto out = torch::empty({N, X}, A.options());
-  hip_check(dca_dpre_dx(ptr<float>(A), nullptr, nullptr, nullptr, wh.data_ptr(), wl.data_ptr(), nullptr,
-                        ptr<float>(out), N, 0, X, 0, 0, cur_stream()),
+  hip_check(dca_dpre_dx(ptr<float>(A), nullptr, nullptr, nullptr, wh.data_ptr(), exact ? nullptr : wl.data_ptr(),
+                        nullptr, ptr<float>(out), N, 0, X, exact ? 1 : 0, 0, cur_stream()),
             "dca_dpre_dx(stage 2)");
   return out;
 }
 
 // The forward twin of dpre_dx (same kernel, bias + ReLU epilogue): x = relu(x896·W_preᵀ + b) (N, 256) and
-// xp = x·W_ihᵀ (N, X) in one launch, bf16x3 with slab-major hi / lo weight images (split_bf16x2(w, True) of W_pre
-// (256, K1) and of W_ih (X, 256)).
+// xp = x·W_ihᵀ (N, X) in one launch. bf16x3: slab-major hi / lo weight images (split_bf16x2(w, True) of W_pre
+// (256, K1) and of W_ih (X, 256)); exact: W_pre (256, K1) and W_ih (X, 256) fp32 with empty lo images.
 std::vector<torch::Tensor> pre_rnn_chain(torch::Tensor x896, torch::Tensor w1h, torch::Tensor w1l, torch::Tensor bias,
                                          torch::Tensor w2h, torch::Tensor w2l) {
   CHECK_F32(x896); CHECK_F32(bias);
-  CHECK_BF16(w1h); CHECK_BF16(w1l); CHECK_BF16(w2h); CHECK_BF16(w2l);
+  const bool exact = chain_exact(w1h, w1l, "pre_rnn_chain");
+  TORCH_CHECK(chain_exact(w2h, w2l, "pre_rnn_chain") == exact, "pre_rnn_chain: both weights exact or both bf16x3");
   const int N = x896.size(0), K1 = x896.size(1);
   TORCH_CHECK(x896.dim() == 2 && bias.numel() == 256, "pre_rnn_chain: x896 (N, K1), bias (256)");
-  TORCH_CHECK(w1h.dim() == 3 && w1h.size(0) * 32 == K1 && w1h.size(1) == 256 && w1h.size(2) == 32 &&
-              w1l.sizes() == w1h.sizes() && w2h.dim() == 3 && w2h.size(0) == 8 && w2h.size(2) == 32 &&
-              w2l.sizes() == w2h.sizes(), "pre_rnn_chain: slab-major images (K1/32,256,32) and (8,X,32)");
-  const int X = w2h.size(1);
+  int X;
+  if (exact) {
+    TORCH_CHECK(w1h.size(0) == 256 && w1h.size(1) == K1 && w2h.size(1) == 256, "pre_rnn_chain: exact W_pre (256, K1), "
+                "W_ih (X, 256)");
+    X = w2h.size(0);
+  } else {
+    TORCH_CHECK(w1h.dim() == 3 && w1h.size(0) * 32 == K1 && w1h.size(1) == 256 && w1h.size(2) == 32 &&
+                w2h.dim() == 3 && w2h.size(0) == 8 && w2h.size(2) == 32,
+                "pre_rnn_chain: slab-major images (K1/32,256,32) and (8,X,32)");
+    X = w2h.size(1);
+  }
   TORCH_CHECK(K1 % 128 == 0 && X % 128 == 0, "pre_rnn_chain: K1 % 128 == 0 and X % 128 == 0");
   TORCH_CHECK((long long)N * K1 * 4 <= 0x7fff0000LL, "pre_rnn_chain: x896 too large for one launch");
   auto o = x896.options();
   auto x = torch::empty({N, 256}, o);
   auto xp = torch::empty({N, X}, o);
-  hip_check(dca_dpre_dx(ptr<float>(x896), w1h.data_ptr(), w1l.data_ptr(), ptr<float>(bias), w2h.data_ptr(),
-                        w2l.data_ptr(), ptr<float>(x), ptr<float>(xp), N, K1, X, 0, 1, cur_stream()),
+  hip_check(dca_dpre_dx(ptr<float>(x896), w1h.data_ptr(), exact ? nullptr : w1l.data_ptr(), ptr<float>(bias),
+                        w2h.data_ptr(), exact ? nullptr : w2l.data_ptr(), ptr<float>(x), ptr<float>(xp), N, K1, X,
+                        exact ? 1 : 0, 1, cur_stream()),
             "dca_dpre_dx(forward)");
   return {x, xp};
 }
@@ -1049,10 +1087,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("logp_old"), py::arg("nret"), py::arg("norms"), py::arg("algo"), py::arg("compat_value_bug"),
         py::arg("S_bug"), py::arg("B_bug"), py::arg("clip_eps"), py::arg("ent_coef"), py::arg("vf_coef"),
         py::arg("dz_bf16") = false, py::arg("precise") = false);
-  m.def("encoder_fwd", &encoder_fwd, "fused entity encoder forward (unit MLP, per-type GEMM, max-pool+argmax)");
+  m.def("encoder_fwd", &encoder_fwd, "fused entity encoder forward (unit MLP, per-type GEMM, max-pool+argmax)",
+        py::arg("units"), py::arg("env"), py::arg("w1"), py::arg("b1"), py::arg("wt"), py::arg("bt"), py::arg("we"),
+        py::arg("be"), py::arg("counts"), py::arg("compat"), py::arg("exact") = false);
   m.def("encoder_bwd", &encoder_bwd, "fused entity encoder backward: dW_type (K-blocked split-K MFMA GEMM), dW1, db1",
         py::arg("units"), py::arg("w1"), py::arg("b1"), py::arg("wtT"), py::arg("dtl"), py::arg("q"), py::arg("dx"),
-        py::arg("arg"), py::arg("counts"), py::arg("compat"), py::arg("demb_in") = py::none());
+        py::arg("arg"), py::arg("counts"), py::arg("compat"), py::arg("demb_in") = py::none(),
+        py::arg("exact") = false);
   m.def("lstm_bwd", &lstm_bwd, "persistent LSTM backward recurrence (granule reduce-scatter)", py::arg("dhs"),
         py::arg("gates"), py::arg("cs"), py::arg("c0"), py::arg("dhn"), py::arg("dcn"), py::arg("whh"), py::arg("err"),
         py::arg("trace") = py::none());
@@ -1088,7 +1129,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("maps") = py::none(), py::arg("dsth") = py::none(), py::arg("dstl") = py::none());
   m.def("gemm_tn", &gemm_tn, "C (+)= A^T B for K-outer bf16 or fp32 (bf16x3) operands (split-K MFMA, LDS transposed reads)",
         py::arg("A"), py::arg("B"), py::arg("C"), py::arg("perm") = py::none(), py::arg("accumulate") = false,
-        py::arg("B0") = py::none(), py::arg("colsum") = py::none());
+        py::arg("B0") = py::none(), py::arg("colsum") = py::none(), py::arg("exact") = false);
   m.def("dpre_dx", &dpre_dx, "fused pre-RNN dX chain: (dG·W_ih)*[x>0] -> dpre, dpre·W_pre -> dx (bf16x3 with pre-split "
         "bf16 hi/lo weights, or exact-f32 MFMA with fp32 weights)", py::arg("dG"), py::arg("w1h"), py::arg("w1l"),
         py::arg("x"), py::arg("w2h"), py::arg("w2l"));

@@ -27,7 +27,8 @@
 // 5 VALU per MFMA and 205 µs at the deploy shape).
 // EXACT = true: exact fp32 on v_mfma_f32_16x16x4_f32 — a 16x16x32 fragment's 8 k values per lane feed 8 chained
 // 16x16x4 MFMAs (call j takes element j: lane l contributes k = 8·(l/16) + j, so the 8 calls cover all 32 k);
-// fp32 LDS rows (144-B pitch), fp32 weights.
+// fp32 LDS rows (144-B pitch), fp32 weights; every launch form (∂X chain, forward chain, heads GEMM + its ∂X
+// product) has an exact instance: the IEEE-fp32 learner.
 #include "common.h"
 #include <cstdlib>
 
@@ -261,7 +262,17 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
         }
       }
 
-  } else if constexpr (!EXACT) {
+  } else if constexpr (EXACT) {
+    // stage-2-only launch (K1 = 0), exact: dG (N, P) fp32 rows straight into the fp32 dpre image (8 slabs)
+    for (int i = tid; i < BM * P / 4; i += NT) {
+      const int row = i / (P / 4), c4 = (i % (P / 4)) * 4;
+      const int grow = r0 + row;
+      const float4 v = grow < N ? *reinterpret_cast<const float4*>(dG + (size_t)grow * P + c4)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int kk = c4 & (BK - 1);
+      *reinterpret_cast<float4*>(dimg + (c4 / BK) * L::A1 + coff<true>(row, kk >> 2)) = v;
+    }
+  } else {
     // stage-2-only launch (K1 = 0): the A operand is dG itself, (N, P) fp32 rows, split into the dpre image
     for (int i = tid; i < BM * P / 4; i += NT) {
       const int row = i / (P / 4), c4 = (i % (P / 4)) * 4;
@@ -395,28 +406,25 @@ extern "C" hipError_t dca_dpre_dx(const float* dG, const void* w1h, const void* 
                                   int epi, hipStream_t stream) {
   // K1 = 0: stage 2 only (A = dG (N, P)); X = 0: stage 1 only
   if (N < 1 || (K1 == 0 && X == 0) || K1 < 0 || K1 % (RD * BK) != 0 || X < 0 || X % XC != 0 ||
-      ((X / XC) * (P / BK)) % RD != 0 || (K1 == 0 && exact))
+      ((X / XC) * (P / BK)) % RD != 0 || epi < 0 || epi > 2)
     return hipErrorInvalidValue;
   if ((long long)N * K1 * 4 > 0x7fff0000LL) return hipErrorInvalidValue;      // buffer-resource range
   const int grid = (N + BM - 1) / BM;
   // DCA_DX_DBG (microbenchmark knob, scripts/dx_bench.py): bit 0 no global loads past the prologue, bit 1 no MFMA,
   // bit 2 stage 1 only, bit 3 no dG loads, bit 4 no weight loads (stage 1)
   static const int dbg = [] { const char* e = getenv("DCA_DX_DBG"); return e ? atoi(e) : 0; }();
-  if (exact && epi == 0) {
-    hipLaunchKernelGGL((dpre_dx_kernel<true, 0>), dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre, dx,
-                       N, K1, X, dbg);
-  } else if (exact) {
-    hipLaunchKernelGGL((dpre_dx_kernel<true, 1>), dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre, dx,
-                       N, K1, X, dbg);
-  } else if (epi == 0) {
-    hipLaunchKernelGGL((dpre_dx_kernel<false, 0>), dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre,
-                       dx, N, K1, X, dbg);
-  } else if (epi == 2) {
-    hipLaunchKernelGGL((dpre_dx_kernel<false, 2>), dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre,
-                       dx, N, K1, X, dbg);
+#define DCA_DX_LAUNCH(EX, EP)                                                                                    \
+  hipLaunchKernelGGL((dpre_dx_kernel<EX, EP>), dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre, dx, \
+                     N, K1, X, dbg)
+  if (exact) {
+    if (epi == 0) DCA_DX_LAUNCH(true, 0);
+    else if (epi == 1) DCA_DX_LAUNCH(true, 1);
+    else DCA_DX_LAUNCH(true, 2);
   } else {
-    hipLaunchKernelGGL((dpre_dx_kernel<false, 1>), dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre,
-                       dx, N, K1, X, dbg);
+    if (epi == 0) DCA_DX_LAUNCH(false, 0);
+    else if (epi == 1) DCA_DX_LAUNCH(false, 1);
+    else DCA_DX_LAUNCH(false, 2);
   }
+#undef DCA_DX_LAUNCH
   return hipGetLastError();
 }

@@ -982,6 +982,286 @@ __global__ __launch_bounds__(512, 1) void encoder_fwd_f32_items_kernel(FfParams 
   }
 }
 
+// ============================================================================================================
+// EXACT variants (the IEEE-fp32 learner, precision='fp32-exact'): the same item-range organisation as the F32 kernels
+// above, but every product is an IEEE fp32 fma on v_mfma_f32_16x16x4_f32 (bit-for-bit a k-ordered fmaf chain) —
+// no bf16 split anywhere. A 16x16x4 f32 fragment is ONE float per lane, A[m = l&15][k = l>>4] / B[k = l>>4][n = l&15],
+// so:
+//   * layer 1 (K = 10 features + bias) is 3 calls, call c taking feature 4c + (l>>4) (slot 10 = the bias against a
+//     1.0 operand, slot 11 = 0);
+//   * layer 2 (K = 128) is 32 calls: call (s, jj) takes k = 32s + 8·(l>>4) + jj, so the A operand of a lane is 8
+//     consecutive floats of ONE basic row per s — two ds_read_b128 from a row-major fp32 tile image — and the weight
+//     operand is 32 floats per lane held in VGPRs for the whole job (the bf16x3 kernels' hi + lo images: same 32 VGPRs);
+//   * the C-layout tiles (column on the lane, rows 4(l>>4) … +3 in the registers) are directly the A / B operands of
+//     the row-reduction products (∂W_τᵀ = basicᵀ·∂emb, ∂W1 = ∂basicᵀ·units): call r takes row 4(l>>4) + r.
+// Weight-gradient sums are two-level: each item's 16-row product starts from zero and is added into the job's running
+// sum (a 16-long fma chain per item, then one add per item), then the per-job partials go through the fixed-order
+// reduces shared with the F32 kernels. MFMA work per item is 5.3x the bf16x3 kernels' (the f32 MFMA rate is 1/16 of
+// bf16), so these are MFMA-bound where the bf16x3 ones are latency-bound.
+constexpr int kXP = 132;                     // row pitch (floats) of the row-major fp32 tile image [16 rows][128]
+constexpr int kXT = 20;                      // row pitch (floats) of the transposed image [128 columns][16 rows]
+
+// layer 1 of the staged item for basic tile wv (exact): 3 f32 MFMAs, C layout (rows 4kg + r, column 16wv + i)
+__device__ __forceinline__ f32x4 x_layer1(const float* sl, const float (&w1x)[3], int i, int kg) {
+  f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int cc = 0; cc < 3; ++cc) {
+    const int f = 4 * cc + kg;
+    const float a = f < kF ? sl[i * kF + f] : (f == kF ? 1.f : 0.f);
+    c = __builtin_amdgcn_mfma_f32_16x16x4f32(a, w1x[cc], c, 0, 0, 0);
+  }
+  return c;
+}
+
+__device__ __forceinline__ void x_load_w1(const float* w1, const float* b1, int col, int kg, float (&w1x)[3]) {
+#pragma unroll
+  for (int cc = 0; cc < 3; ++cc) {
+    const int f = 4 * cc + kg;
+    w1x[cc] = f < kF ? w1[col * kF + f] : (f == kF ? b1[col] : 0.f);
+  }
+}
+
+// A operand of a 16×128 row-major fp32 image for 32 calls: lane (row i, kg) gets columns 32s + 8kg … +7 per s
+__device__ __forceinline__ void x_afrags(const float* img, int i, int kg, float (&a)[32]) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const float4 p = *reinterpret_cast<const float4*>(img + i * kXP + 32 * s + 8 * kg);
+    const float4 q = *reinterpret_cast<const float4*>(img + i * kXP + 32 * s + 8 * kg + 4);
+    a[8 * s + 0] = p.x; a[8 * s + 1] = p.y; a[8 * s + 2] = p.z; a[8 * s + 3] = p.w;
+    a[8 * s + 4] = q.x; a[8 * s + 5] = q.y; a[8 * s + 6] = q.z; a[8 * s + 7] = q.w;
+  }
+}
+
+// 16 × 128 product over K = 128 against the weight fragments: two interleaved accumulators (the f32 MFMA's
+// dependent latency is 40 cycles against a 32-cycle issue), summed at the end
+__device__ __forceinline__ f32x4 x_mma_k128(const float (&a)[32], const float (&w)[32]) {
+  f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < 32; k += 2) {
+    c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[k], w[k], c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[k + 1], w[k + 1], c1, 0, 0, 0);
+  }
+  return c0 + c1;
+}
+
+// C-layout fragment (rows 4kg + r, column 16n + i) → row-major image (4 dword stores)
+__device__ __forceinline__ void x_put(float* img, int n, const f32x4& v, int i, int kg) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) img[(4 * kg + r) * kXP + 16 * n + i] = v[r];
+}
+
+__global__ __launch_bounds__(512, 1) void encoder_fwd_x_kernel(FfParams P) {
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int i = lane & 15, kg = lane >> 4;
+  const int job = blockIdx.x, N = P.N, U = P.L.U;
+  for (int rbase = 32 * job; rbase < N; rbase += 32 * (int)gridDim.x) {     // env embedding (fp32 VALU)
+    const int row = rbase + (tid >> 4), c0 = (tid & 15) * 8;
+    if (row < N) {
+      const float e0 = P.env[row * 3], e1 = P.env[row * 3 + 1], e2 = P.env[row * 3 + 2];
+#pragma unroll
+      for (int c = c0; c < c0 + 8; ++c)
+        P.x896[(size_t)row * 896 + c] = fmaxf(P.be[c] + P.we[c * 3] * e0 + P.we[c * 3 + 1] * e1 + P.we[c * 3 + 2] * e2, 0.f);
+    }
+  }
+  int tau = 0;
+#pragma unroll
+  for (int t = 1; t < 6; ++t) tau += job >= P.jbase[t] ? 1 : 0;
+  if (job >= P.jbase[6]) return;
+  const int cnt = P.L.cnt[tau], uoff = P.L.off[tau];
+  const int NB = (N + 15) >> 4;
+  const int g0 = (job - P.jbase[tau]) * P.gpj[tau], g1 = min(g0 + P.gpj[tau], NB);
+  const int k0 = g0 * cnt, k1 = g1 * cnt, kl = k1 - 1;
+  __shared__ __attribute__((aligned(16))) float img[2][16 * kXP];
+  __shared__ __attribute__((aligned(16))) float stg[3][kStg];
+
+  const int col = 16 * wv + i;
+  float wx[32], w1x[3];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {   // B[k = j][n = out] = W_τ[out][j], k = 32s + 8kg + jj
+    const float* p = P.wt + ((size_t)tau * kD + col) * kD + 32 * s + 8 * kg;
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    wx[8 * s + 0] = a.x; wx[8 * s + 1] = a.y; wx[8 * s + 2] = a.z; wx[8 * s + 3] = a.w;
+    wx[8 * s + 4] = b.x; wx[8 * s + 5] = b.y; wx[8 * s + 6] = b.z; wx[8 * s + 7] = b.w;
+  }
+  x_load_w1(P.w1, P.b1, col, kg, w1x);
+  const float btv = P.bt[tau * kD + col];
+  const __amdgpu_buffer_rsrc_t Ru = uniform_rsrc(P.units, N * U * kF * 4),
+                               Re = uniform_rsrc(P.emb, N * U * kD * 4);
+  f32x4 pmax = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+  int parg[4] = {0, 0, 0, 0};
+
+  float pre = 0.f;
+  if (wv < 3) {
+    stg[k0 % 3][64 * wv + lane] = ff_stage_load(P, Ru, k0, cnt, uoff, wv, lane);
+    stg[(k0 + 1) % 3][64 * wv + lane] = ff_stage_load(P, Ru, min(k0 + 1, kl), cnt, uoff, wv, lane);
+    pre = ff_stage_load(P, Ru, min(k0 + 2, kl), cnt, uoff, wv, lane);
+  }
+  lds_barrier();
+  {
+    f32x4 b = x_layer1(stg[k0 % 3], w1x, i, kg);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) b[r] = fmaxf(b[r], 0.f);
+    x_put(img[0], wv, b, i, kg);
+  }
+  int buf = 0;
+  for (int k = k0; k < k1; ++k) {
+    lds_barrier();   // image k complete; staging slot of k + 1 written
+    if (wv < 3) {
+      stg[(k + 2) % 3][64 * wv + lane] = pre;
+      pre = ff_stage_load(P, Ru, min(k + 3, kl), cnt, uoff, wv, lane);
+    }
+    const int rb = k / cnt, u = k - rb * cnt, row0 = 16 * rb;
+    float a[32];
+    x_afrags(img[buf], i, kg, a);
+    const f32x4 c = x_mma_k128(a, wx);
+    {   // next item's basic tile into the other image (past the range's end: a rewrite nobody reads)
+      f32x4 b = x_layer1(stg[(k + 1) % 3], w1x, i, kg);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) b[r] = fmaxf(b[r], 0.f);
+      x_put(img[buf ^ 1], wv, b, i, kg);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float v = c[r] + btv;
+      if (v > pmax[r]) { pmax[r] = v; parg[r] = u; }
+      const int row = row0 + 4 * kg + r;
+      __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), Re, ((row * U + uoff + u) * kD + col) * 4,
+                                            0, 0);
+    }
+    if (u == cnt - 1) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = row0 + 4 * kg + r;
+        if (row < N) {
+          P.x896[(size_t)row * 896 + kD + tau * kD + col] = pmax[r];
+          P.arg[((size_t)row * 6 + tau) * kD + col] = (unsigned char)parg[r];
+        }
+        pmax[r] = -INFINITY;
+        parg[r] = 0;
+      }
+    }
+    buf ^= 1;
+  }
+}
+
+// ∂emb e-tile wv of item k (C layout) → row-major image (∂basic's A operand) and transposed image (the ∂W_τ
+// products' B operand: one b128 of rows 4kg … 4kg+3 per lane and tile)
+__device__ __forceinline__ void xb_build(const FbBuild& b, const float* slot, int u, float* im, float* it, int wv,
+                                         int lane) {
+  const int i = lane & 15, kg = lane >> 4;
+  const f32x4 d4 = *reinterpret_cast<const f32x4*>(slot + 16 * kF + 4 * kg);
+  f32x4 v;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) v[r] = d4[r] * b.q[r] + (b.ab[r] == (unsigned)u ? b.ds[r] : 0.f);
+  x_put(im, wv, v, i, kg);
+  *reinterpret_cast<f32x4*>(it + (16 * wv + i) * kXT + 4 * kg) = v;
+}
+
+template <bool COMPAT>
+__global__ __launch_bounds__(512, 1) void encoder_bwd_x_kernel(FbParams P) {
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int i = lane & 15, kg = lane >> 4;
+  const int job = blockIdx.x;
+  int tau = 0;
+#pragma unroll
+  for (int t = 1; t < 6; ++t) tau += job >= P.jbase[t] ? 1 : 0;
+  const int cnt = P.L.cnt[tau], uoff = P.L.off[tau], N = P.N, U = P.L.U;
+  const int NB = (N + 15) >> 4;
+  const int k0 = (job - P.jbase[tau]) * P.items, k1 = min(k0 + P.items, cnt * NB);
+  __shared__ __attribute__((aligned(16))) float img[2][16 * kXP];
+  __shared__ __attribute__((aligned(16))) float imt[2][128 * kXT];
+  __shared__ __attribute__((aligned(16))) float stg[3][kStg];
+  FbRsrc R;
+  R.q = uniform_rsrc(P.q, N * P.ldq * 4);
+  R.x = uniform_rsrc(P.dx, N * 896 * 4);
+  R.a = uniform_rsrc(P.arg, N * 6 * kD);
+
+  // this wave's basic-column tile: B[k = e][n = j] = W_τ[e][j] = W_τᵀ[j][e], k = 32s + 8kg + jj; layer-1 row of W1
+  const int col = 16 * wv + i;
+  float wx[32], w1x[3];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    const float* p = P.wtT + ((size_t)tau * kD + col) * kD + 32 * s + 8 * kg;
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    wx[8 * s + 0] = a.x; wx[8 * s + 1] = a.y; wx[8 * s + 2] = a.z; wx[8 * s + 3] = a.w;
+    wx[8 * s + 4] = b.x; wx[8 * s + 5] = b.y; wx[8 * s + 6] = b.z; wx[8 * s + 7] = b.w;
+  }
+  x_load_w1(P.w1, P.b1, col, kg, w1x);
+  f32x4 acc[8], dw1acc = {0.f, 0.f, 0.f, 0.f};
+  float db1acc = 0.f;
+#pragma unroll
+  for (int et = 0; et < 8; ++et) acc[et] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  FbBuild bn;
+  const int kl = max(k1 - 1, 0);
+  float pre = 0.f;
+  if (wv < 3) {
+    stg[k0 % 3][64 * wv + lane] = fb_stage_load(P, min(k0, kl), cnt, uoff, wv, lane);
+    stg[(k0 + 1) % 3][64 * wv + lane] = fb_stage_load(P, min(k0 + 1, kl), cnt, uoff, wv, lane);
+    pre = fb_stage_load(P, min(k0 + 2, kl), cnt, uoff, wv, lane);
+  }
+  fb_load_build<false, COMPAT>(bn, R, P.ldq, min(k0, kl), true, cnt, uoff, U, tau, wv, i, kg);
+  lds_barrier();
+  xb_build(bn, stg[k0 % 3], k0 % cnt, img[0], imt[0], wv, lane);
+  fb_load_build<false, COMPAT>(bn, R, P.ldq, min(k0 + 1, kl), min(k0 + 1, kl) % cnt == 0, cnt, uoff, U, tau, wv, i, kg);
+  int buf = 0;
+  for (int k = k0; k < k1; ++k) {
+    lds_barrier();
+    if (wv < 3) {
+      stg[(k + 2) % 3][64 * wv + lane] = pre;
+      pre = fb_stage_load(P, min(k + 3, kl), cnt, uoff, wv, lane);
+    }
+    const float* sl = stg[k % 3];
+    float a[32];
+    x_afrags(img[buf], i, kg, a);                 // ∂emb[row i][e], e = 32s + 8kg + jj
+    f32x4 et4[8];
+#pragma unroll
+    for (int et = 0; et < 8; ++et) et4[et] = *reinterpret_cast<const f32x4*>(imt[buf] + (16 * et + i) * kXT + 4 * kg);
+    float ub[4];                                  // units[row 4kg + r][f = i] (f ≥ 10: 0)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ub[r] = i < kF ? sl[(4 * kg + r) * kF + i] : 0.f;
+    f32x4 bas = x_layer1(sl, w1x, i, kg);
+    f32x4 c = x_mma_k128(a, wx);                  // ∂basic[row][j] (before ReLU')
+    // item k + 1's ∂emb into the other images (every wave has passed this item's barrier)
+    xb_build(bn, stg[(k + 1) % 3], min(k + 1, kl) % cnt, img[buf ^ 1], imt[buf ^ 1], wv, lane);
+    fb_load_build<false, COMPAT>(bn, R, P.ldq, min(k + 2, kl), k + 2 <= kl && (k + 2) % cnt == 0, cnt, uoff, U, tau,
+                                 wv, i, kg);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) bas[r] = fmaxf(bas[r], 0.f);
+    // ∂W_τᵀ[j][e] += Σ_rows basic[row][j] · ∂emb[row][e] (this item's 16 rows from zero, then added)
+#pragma unroll
+    for (int et = 0; et < 8; ++et) {
+      f32x4 p = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) p = __builtin_amdgcn_mfma_f32_16x16x4f32(bas[r], et4[et][r], p, 0, 0, 0);
+      acc[et] += p;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      c[r] = bas[r] > 0.f ? c[r] : 0.f;
+      db1acc += c[r];
+    }
+    // ∂W1[j][f] += Σ_rows ∂basic[row][j] · units[row][f]
+    f32x4 p1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) p1 = __builtin_amdgcn_mfma_f32_16x16x4f32(c[r], ub[r], p1, 0, 0, 0);
+    dw1acc += p1;
+    buf ^= 1;
+  }
+  float* dst = P.dwtpart + (size_t)job * (kD * kD);
+#pragma unroll
+  for (int et = 0; et < 8; ++et) *reinterpret_cast<f32x4*>(dst + ((8 * wv + et) * 64 + lane) * 4) = acc[et];
+  float* wp = P.w1part + (size_t)job * kW1;
+  if (i < kF) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) wp[(16 * wv + 4 * kg + r) * kF + i] = dw1acc[r];
+  }
+  float s = db1acc;
+  s += __shfl_xor(s, 16, 64);
+  s += __shfl_xor(s, 32, 64);
+  if (kg == 0) wp[kD * kF + 16 * wv + i] = s;
+}
+
 // Fixed-order sum of a type's fused-backward partials (tile-linear → ∂W_τ[e][j]); 4 job phases per block as dwt_reduce.
 __global__ __launch_bounds__(256) void fb_dwt_reduce(const float* __restrict__ part, FbParams P, float* __restrict__ dwt) {
   __shared__ float red[4][64];
@@ -1105,7 +1385,7 @@ __global__ __launch_bounds__(256) void dwt_reduce(const float* __restrict__ part
 
 }  // namespace
 
-// f32 = 1: wt fp32, x896 / emb fp32 (bf16x3 layer 2); f32 = 0: wt, x896, emb bf16
+// f32 = 1: wt fp32, x896 / emb fp32 (bf16x3 layer 2); f32 = 2: the same, exact fp32 MFMA; f32 = 0: wt, x896, emb bf16
 extern "C" hipError_t dca_encoder_fwd(const float* units, const float* env, const float* w1, const float* b1,
                                       const void* wt, const float* bt, const float* we, const float* be, void* x896,
                                       void* emb, unsigned char* arg, int N, int U, const int* counts, int compat,
@@ -1132,7 +1412,8 @@ extern "C" hipError_t dca_encoder_fwd(const float* units, const float* env, cons
     }
     F.jbase[6] = jobs;
     // every launch also covers the env embedding (32-row blocks strided over the grid)
-    encoder_fwd_f32_items_kernel<<<std::max(jobs, 1), 512, 0, st>>>(F);
+    if (f32 == 2) encoder_fwd_x_kernel<<<std::max(jobs, 1), 512, 0, st>>>(F);
+    else encoder_fwd_f32_items_kernel<<<std::max(jobs, 1), 512, 0, st>>>(F);
     return hipGetLastError();
   }
   const dim3 grid((N + kRows - 1) / kRows, kJobs);
@@ -1205,7 +1486,11 @@ extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const
     const int jobs = F.jbase[6];
     F.w1part = static_cast<float*>(ws);
     F.dwtpart = F.w1part + (size_t)jobs * kW1;
-    if (jobs > 0) {
+    if (f32 == 2 && demb_in) return hipErrorInvalidValue;      // the exact kernels cover the 1v1 encoder
+    if (jobs > 0 && f32 == 2) {
+      if (compat) encoder_bwd_x_kernel<true><<<jobs, 512, 0, st>>>(F);
+      else encoder_bwd_x_kernel<false><<<jobs, 512, 0, st>>>(F);
+    } else if (jobs > 0) {
       if (demb_in) encoder_bwd_f32_fused_kernel<true, false><<<jobs, 512, 0, st>>>(F);
       else if (compat) encoder_bwd_f32_fused_kernel<false, true><<<jobs, 512, 0, st>>>(F);
       else encoder_bwd_f32_fused_kernel<false, false><<<jobs, 512, 0, st>>>(F);

@@ -373,6 +373,164 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_kernel(Args a) {
 #undef SF
 }
 
+// ---- exact fp32 (the IEEE-fp32 learner): v_mfma_f32_16x16x4_f32, one f32 per operand per lane, no split -------
+// Same 128×128 tile / split-K / reduce organisation as above, 32-row K slabs staged as fp32 [k][m] images (row pitch
+// 144 floats: the two 16-lane halves of a ds_read_b32 group read rows k and k+1 → banks 0-15 / 16-31, conflict-free).
+// The 16x16x4 A fragment is A[m = l&15][k = l>>4] and B[k = l>>4][n = l&15]: with K-outer [k][m] images that is one
+// plain dword read per lane, no transpose. Call c of a slab takes rows 4c … 4c+3.
+// Two-level summation: every 32-row slab is accumulated from zero on the MFMA (a 32-long fma chain), then added into
+// the running sum on the VALU — a split's outputs are sums of ≤ kc/32 slab partials instead of one kc-long chain
+// (the round-off of a 1 400-long chain measured 1.8e-5 relative on the enum head's ∂W against float64; the split-K
+// partials then go through the fixed-order reduce as before).
+constexpr int kXP = 144;                          // fp32 image row pitch (floats)
+constexpr int kXImg = 32 * kXP * 4;               // one 32-row operand image (bytes)
+
+struct XStage {
+  float4 a[4], b[4];                              // rows (t>>5) + 8i, columns 4·(t&31) … +3
+};
+
+template <bool WITH_B0>
+__device__ __forceinline__ void load_stage_x(const Args& a, const Rsrc& R, int kbase, int kend, int m_base, int n_base,
+                                             XStage& r) {
+  const int t = threadIdx.x, c4 = 4 * (t & 31);
+  const int m = m_base + c4, n = n_base + c4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int k = kbase + (t >> 5) + 8 * i;
+    const bool kin = k < kend;
+    r.a[i] = __builtin_bit_cast(float4, bload16(R.A, kin && m < a.M ? (k * a.lda + m) * 4 : kOob));
+    r.b[i] = __builtin_bit_cast(float4, bload16(R.B, kin && n < a.N && k >= a.split ? ((k - a.split) * a.ldb + n) * 4
+                                                                                    : kOob));
+  }
+  if (WITH_B0 && kbase < a.split) {               // prologue only (host keeps split ≤ 32 = one slab)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int k = kbase + (t >> 5) + 8 * i;
+      const float4 p = __builtin_bit_cast(float4, bload16(R.B0, k < kend && n < a.N && k < a.split ? (k * a.ldb + n) * 4
+                                                                                                  : kOob));
+      r.b[i] = make_float4(r.b[i].x + p.x, r.b[i].y + p.y, r.b[i].z + p.z, r.b[i].w + p.w);
+    }
+  }
+}
+
+__device__ __forceinline__ void store_stage_x(char* S, const XStage& r) {
+  const int t = threadIdx.x, c4 = 4 * (t & 31);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (t >> 5) + 8 * i;
+    *reinterpret_cast<float4*>(S + (row * kXP + c4) * 4) = r.a[i];
+    *reinterpret_cast<float4*>(S + kXImg + (row * kXP + c4) * 4) = r.b[i];
+  }
+}
+
+__global__ __launch_bounds__(kThreads, 2) void gemm_tn_exact_kernel(Args a) {
+  __shared__ __attribute__((aligned(16))) char smem[4 * kXImg];   // [stage][A image | B image], 72 KB
+  const int tile = blockIdx.x, split = blockIdx.y;
+  const int tm = tile / a.tiles_n, tn = tile % a.tiles_n;
+  const int m_base = tm * BM, n_base = tn * BN;
+  const int k_lo = split * a.kc, k_hi = min(a.K, k_lo + a.kc);
+  const int w = threadIdx.x >> 6, wm = w & 1, wn = w >> 1, l = threadIdx.x & 63;
+  const int fr = l >> 4, fc = l & 15;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float cs[4] = {0.f, 0.f, 0.f, 0.f};
+  const bool do_cs = a.colsum != nullptr && tn == 0;
+  const Rsrc R = make_rsrc(a, 4);
+  XStage st;
+  int buf = 0;
+  if (k_lo < k_hi) {
+    load_stage_x<true>(a, R, k_lo, k_hi, m_base, n_base, st);
+    store_stage_x(smem, st);
+    if (do_cs)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) { cs[0] += st.a[i].x; cs[1] += st.a[i].y; cs[2] += st.a[i].z; cs[3] += st.a[i].w; }
+  }
+  __syncthreads();
+  for (int kb = k_lo; kb < k_hi; kb += 32) {
+    const bool more = kb + 32 < k_hi;
+    if (more) load_stage_x<false>(a, R, kb + 32, k_hi, m_base, n_base, st);   // in flight during the MFMAs
+    const float* As = reinterpret_cast<const float*>(smem + buf * 2 * kXImg);
+    const float* Bs = As + kXImg / 4;
+    f32x4 part[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) part[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const int row = 4 * c + fr;
+      float fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = As[row * kXP + wm * 64 + 16 * i + fc];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = Bs[row * kXP + wn * 64 + 16 * j + fc];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) part[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i], fb[j], part[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] += part[i][j];
+    if (more) {
+      store_stage_x(smem + (buf ^ 1) * 2 * kXImg, st);
+      if (do_cs)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) { cs[0] += st.a[i].x; cs[1] += st.a[i].y; cs[2] += st.a[i].z; cs[3] += st.a[i].w; }
+    }
+    __syncthreads();
+    buf ^= 1;
+  }
+  if (do_cs) {       // 8 row phases share each column quad: fixed-order LDS fold, one value per column
+    float* red = reinterpret_cast<float*>(smem);       // [8][128] (the images are dead after the barrier)
+    const int t = threadIdx.x, c4 = 4 * (t & 31), rg = t >> 5;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[rg * 128 + c4 + j] = cs[j];
+    __syncthreads();
+    if (t < 128) {
+      float v = 0.f;
+      for (int g = 0; g < 8; ++g) v += red[g * 128 + t];
+      const int m = m_base + t;
+      if (m < a.M) {
+        if (a.splits == 1) {
+          float* cp = a.colsum + (a.perm ? a.perm[m] : m);
+          *cp = a.accumulate ? *cp + v : v;
+        } else {
+          a.slab[(size_t)a.splits * a.M * a.N + (size_t)split * a.M + m] = v;
+        }
+      }
+    }
+  }
+  // accumulator element (i, j, e): row m = wm*64 + 16i + 4(l>>4) + e, column n = wn*64 + 16j + (l&15)
+  float* slab = a.slab + (size_t)split * a.M * a.N;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int m = m_base + wm * 64 + 16 * i + 4 * fr + e;
+      if (m >= a.M) continue;
+      if (a.splits == 1) {
+        float* crow = a.C + (size_t)(a.perm ? a.perm[m] : m) * a.ldc;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = n_base + wn * 64 + 16 * j + fc;
+          if (n < a.N) crow[n] = a.accumulate ? crow[n] + acc[i][j][e] : acc[i][j][e];
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = n_base + wn * 64 + 16 * j + fc;
+          if (n < a.N) slab[(size_t)m * a.N + n] = acc[i][j][e];
+        }
+      }
+    }
+}
+
 // Fixed-order (deterministic) sum of the split-K slabs, optional row map / accumulate. A block of 256 threads owns
 // 256/P float4 outputs × P split phases (P = power of two ≤ min(16, splits)): thread (phase p, output o) sums splits
 // p, p+P, … with 4 loads in flight, then a fixed LDS fold over the phases — a long split list (K = 716 800 unit rows
@@ -453,11 +611,14 @@ __global__ __launch_bounds__(256) void gemm_tn_reduce(const float* __restrict__ 
 
 }  // namespace
 
+// f32: 0 bf16, 1 fp32 bf16x3, 2 exact fp32
 extern "C" void dca_gemm_tn_plan(int M, int N, int K, int* splits, int* kc, int* tiles, int f32) {
   const int bk = f32 ? 32 : BK;
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   const int t = tm * tn;
-  int s = (384 + t - 1) / t;                              // aim at ≈1.5 workgroups per CU
+  // ≈1.5 workgroups per CU; exact: ≈2 (MFMA-bound at 1/16 of the bf16 rate, two 64 KB workgroups fit a CU)
+  const int target = f32 == 2 ? 512 : 384;
+  int s = (target + t - 1) / t;
   const int kmax = (K + bk - 1) / bk;                     // at least one K slab per split
   if (s > kmax) s = kmax;
   if (s < 1) s = 1;
@@ -469,7 +630,7 @@ extern "C" void dca_gemm_tn_plan(int M, int N, int K, int* splits, int* kc, int*
   *tiles = t;
 }
 
-// f32 = 0: A, B, B0 bf16; f32 = 1: fp32 operands (bf16x3 split MFMA)
+// f32 = 0: A, B, B0 bf16; f32 = 1: fp32 operands (bf16x3 split MFMA); f32 = 2: fp32 operands, exact fp32 MFMA
 extern "C" hipError_t dca_gemm_tn(const void* A, int lda, const void* B, int ldb, const void* B0, int split_rows,
                                   float* C, int ldc, const int* perm, int accumulate, int M, int N, int K, float* slab,
                                   float* colsum, hipStream_t st, int f32) {
@@ -478,7 +639,8 @@ extern "C" hipError_t dca_gemm_tn(const void* A, int lda, const void* B, int ldb
   dca_gemm_tn_plan(M, N, K, &splits, &kc, &tiles, f32);
   Args a{A, lda, B, ldb, B0 ? B0 : B, B0 ? split_rows : 0, C, ldc, perm, slab, colsum, M, N, K, kc, splits,
          (N + BN - 1) / BN, accumulate};
-  if (f32) hipLaunchKernelGGL(gemm_tn_kernel<true>, dim3(tiles, splits), dim3(kThreads), 8 * kImgF32, st, a);
+  if (f32 == 2) hipLaunchKernelGGL(gemm_tn_exact_kernel, dim3(tiles, splits), dim3(kThreads), 0, st, a);
+  else if (f32) hipLaunchKernelGGL(gemm_tn_kernel<true>, dim3(tiles, splits), dim3(kThreads), 8 * kImgF32, st, a);
   else hipLaunchKernelGGL(gemm_tn_kernel<false>, dim3(tiles, splits), dim3(kThreads), 4 * kTileBytes, st, a);
   DCA_CHECK_LAUNCH();
   if (splits > 1) {

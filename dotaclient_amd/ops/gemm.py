@@ -10,11 +10,12 @@ from . import require
 
 def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None, perm: Optional[torch.Tensor] = None,
             accumulate: bool = False, b0: Optional[torch.Tensor] = None,
-            colsum: Optional[torch.Tensor] = None) -> torch.Tensor:
+            colsum: Optional[torch.Tensor] = None, exact: bool = False) -> torch.Tensor:
     """``a`` (K, M), ``b`` (K - b0_rows, N) — both bf16, or both fp32 (bf16x3 split MFMA: ≈2⁻¹⁶ relative per
     product, fp32 accumulation) — (``b0`` supplies the first rows of the B operand), result
     (M, N) f32 written to ``out`` (through row map ``perm`` if given; added to it if ``accumulate``). ``colsum``
-    (M,) f32, if given, receives Σ_k a[k, m] the same way (a bias gradient, from the staged A tiles)."""
+    (M,) f32, if given, receives Σ_k a[k, m] the same way (a bias gradient, from the staged A tiles). ``exact``
+    (fp32 operands): IEEE fp32 products on v_mfma_f32_16x16x4_f32 instead of the bf16x3 split."""
     C = require()
     M, N = a.shape[1], b.shape[1]
     if out is None:
@@ -22,7 +23,7 @@ def gemm_tn(a: torch.Tensor, b: torch.Tensor, out: Optional[torch.Tensor] = None
     if b0 is not None and b0.shape[0] > _B0_MAX_ROWS:
         # the kernel reads b0 only in a split-K chunk's first K slab (32 rows at fp32); deeper b0: concatenate
         b, b0 = torch.cat([b0, b]), None
-    C.gemm_tn(a, b, out, perm, bool(accumulate), b0, colsum)
+    C.gemm_tn(a, b, out, perm, bool(accumulate), b0, colsum, bool(exact))
     return out
 
 
