@@ -56,14 +56,15 @@ def parse():
     ap.add_argument('--model', default='lstm512')
     ap.add_argument('--backend', default='auto', choices=['auto', 'fused', 'torch'])
     ap.add_argument('--algo', default='ppo', choices=['ppo', 'vpg'])
-    ap.add_argument('--precision', default='fp32', choices=['fp32', 'fp32-exact', 'bf16'],
-                    help='fp32 = the reference\'s training precision (headline); bf16 = bf16 GEMM operands')
-    ap.add_argument('--bf16-extra', type=int, default=1,
-                    help='also time the bf16 learner (reported as an extra field, not the headline)')
+    ap.add_argument('--precision', default='fp32-exact', choices=['fp32-exact', 'fp32', 'bf16'],
+                    help="fp32-exact = IEEE fp32 products everywhere, the reference's training precision (headline); "
+                         'fp32 = fp32 activations with bf16x3-split MFMA operands (~2^-16 per product); bf16 = bf16 '
+                         'GEMM operands')
+    ap.add_argument('--bf16x3-extra', type=int, default=1,
+                    help='also time the bf16x3-operand fp32 learner (extra field fp32_bf16x3_learner, not the headline)')
     ap.add_argument('--model-5v5-extra', type=int, default=1,
-                    help='also time the 5v5 entity-attention policy (BASELINE config 4) at the same B, S, precision')
-    ap.add_argument('--exact-extra', type=int, default=1,
-                    help='also time the fp32-exact learner (IEEE fp32 products, no bf16x3 split; extra field)')
+                    help='also time the 5v5 entity-attention policy (BASELINE config 4) at the same B, S (bf16x3 '
+                         'operands: the attention kernels have no exact-fp32 variant)')
     ap.add_argument('--replay', type=int, default=0, help='sequences in the on-HBM replay pool (0 = 4x batch)')
     ap.add_argument('--graph', type=int, default=-1, help='capture the step in a hipGraph (-1 = auto)')
     ap.add_argument('--actor', type=int, default=1, help='also measure actor steps/s (untimed region)')
@@ -114,6 +115,9 @@ def main():
 
     cfg = get_config(args.model)
     trace = os.environ.get('DCA_BENCH_TRACE') == '1'
+    if cfg.entity_attention and args.precision == 'fp32-exact':
+        progress('5v5 entity attention has no exact-fp32 kernels: timing it at fp32 with bf16x3 operands')
+        args.precision = 'fp32'
 
     def run(precision, cfg=cfg):
         """Build a learner of this precision and time ``args.steps`` DP PPO steps after ``args.warmup``; returns
@@ -181,32 +185,29 @@ def main():
     samples = args.batch_size * args.seq_len * world * args.steps
     value = samples / elapsed
     ms_per_step = elapsed / args.steps * 1e3
-    extra = None
-    if args.bf16_extra and args.precision == 'fp32' and use_cuda:
-        learner = None
-        e16, _, _, _, _ = run('bf16')
-        progress(f'learner bf16 done: {e16 / args.steps * 1e3:.3f} ms/step')
-        extra = {'precision': 'bf16', 'value': samples / e16, 'ms_per_step': e16 / args.steps * 1e3}
-    exact = None
-    if args.exact_extra and args.precision == 'fp32' and use_cuda and not cfg.entity_attention:
+    bf16x3 = None
+    if args.bf16x3_extra and args.precision == 'fp32-exact' and use_cuda:
         learner = None
         try:
-            ex, lx0, lx1, _, _ = run('fp32-exact')
-            progress(f'learner fp32-exact done: {ex / args.steps * 1e3:.3f} ms/step')
-            exact = {'precision': 'fp32-exact (IEEE fp32 products: exact-f32 MFMA / VALU / hipBLASLt)',
-                     'value': samples / ex, 'ms_per_step': ex / args.steps * 1e3, 'loss_first': lx0, 'loss_last': lx1}
+            e3, l30, l31, _, _ = run('fp32')
+            progress(f'learner fp32 (bf16x3 operands) done: {e3 / args.steps * 1e3:.3f} ms/step')
+            bf16x3 = {'precision': 'fp32 activations / bf16x3-split MFMA operands (~2^-16 relative per product)',
+                      'value': samples / e3, 'ms_per_step': e3 / args.steps * 1e3, 'loss_first': l30,
+                      'loss_last': l31}
         except Exception as e:
-            exact = {'error': repr(e)}
+            bf16x3 = {'error': repr(e)}
 
     model_5v5 = None
     if args.model_5v5_extra and use_cuda and not cfg.entity_attention:
         # BASELINE config 4: the 5v5 policy (64 unit slots, pre-LN entity self-attention) through the same fused
         # learner step, same B, S, precision and DP layout
         learner = None
+        p5 = 'fp32' if args.precision == 'fp32-exact' else args.precision
         try:
-            e5, l50, l51, _, _ = run(args.precision, get_config('5v5'))
+            e5, l50, l51, _, _ = run(p5, get_config('5v5'))
             progress(f'learner 5v5 done: {e5 / args.steps * 1e3:.3f} ms/step')
-            model_5v5 = {'model': '5v5', 'precision': args.precision, 'value': samples / e5,
+            model_5v5 = {'model': '5v5', 'precision': p5 + (' (bf16x3 operands)' if p5 == 'fp32' else ''),
+                         'value': samples / e5,
                          'ms_per_step': e5 / args.steps * 1e3, 'loss_first': l50, 'loss_last': l51}
         except Exception as e:
             model_5v5 = {'error': repr(e)}
@@ -314,12 +315,15 @@ def main():
             'vs_baseline': value / BASELINE_STEPS_PER_S,
             'vs_baseline_e2e': (e2e['steps_per_s'] / BASELINE_STEPS_PER_S
                                 if e2e and 'steps_per_s' in e2e else None),
-            'dtype': 'fp32 (bf16x3 MFMA operands)' if args.precision == 'fp32' else args.precision,
-            'precision_note': ('fp32 activations, gradients, accumulation and optimizer; GEMM operands bf16x3-split '
-                               '(x = hi + lo, ~2^-16 relative per product) in the hand-written MFMA kernels and '
-                               "hipBLASLt's fast fp32 mode; the LSTM recurrence and heads/loss are exact fp32 VALU. "
-                               'exact_fp32_learner = the same step with IEEE fp32 products everywhere') if args.precision == 'fp32' else
-                              'bf16 GEMM operands and saved activations, fp32 accumulation / recurrence / optimizer',
+            'dtype': {'fp32-exact': 'fp32', 'fp32': 'fp32 (bf16x3 MFMA operands)'}.get(args.precision, args.precision),
+            'precision_note': {
+                'fp32-exact': 'IEEE fp32 end to end like the reference (torch fp32 nn.Linear + Adam): every GEMM product '
+                              'an fp32 fma on v_mfma_f32_16x16x4_f32 or fp32 VALU in hand-written kernels, fp32 '
+                              'activations, gradients, accumulation and optimizer; no vendor GEMM',
+                'fp32': 'fp32 activations / gradients / optimizer, GEMM operands bf16x3-split (~2^-16 relative per '
+                        'product)',
+            }.get(args.precision, 'bf16 GEMM operands and saved activations, fp32 accumulation / recurrence / '
+                                  'optimizer'),
             'data': 'synthetic (on-HBM replay of synthetic 1v1-mid experience, random-init weights)',
             'config': {'model': f'{args.model} ({cfg.rnn}-{cfg.hidden}, '
                                 f'{"5v5 entity-attention" if cfg.entity_attention else "1v1-mid entity"} encoder, '
@@ -327,8 +331,7 @@ def main():
                        'global_batch': args.batch_size * world, 'seq_len': args.seq_len,
                        'parallelism': f'dp{world}', 'algo': args.algo, 'backend': backend, 'step': step_mode},
             'loss_first': loss_val, 'loss_last': final_loss,
-            'bf16_learner': extra,
-            'exact_fp32_learner': exact,
+            'fp32_bf16x3_learner': bf16x3,
             'model_5v5': model_5v5,
             'dp_replicas_identical': len(set(shas)) == 1,
             'weights_sha16_per_rank': shas,

@@ -120,7 +120,8 @@ def _learner_loop(opt, duration, warmup_iterations, max_iterations, counters, ch
         rows.append((m[DotaOptimizer.SPEED_KEY], m['avg_weight_age'], m['avg_rollout_len'],
                      m.get('time/train', float('nan')), m.get('time/ingest', float('nan')), m['experience_steps'],
                      m.get('time/h2d', float('nan')), m.get('time/log', float('nan')),
-                     m.get('time/publish', float('nan')), m.get('time/lookahead', 0.0)))
+                     m.get('time/publish', float('nan')), m.get('time/lookahead', 0.0),
+                     m.get('time/gpu_train_ms_per_step', float('nan'))))
         e = check()
         if e:
             raise e
@@ -128,6 +129,7 @@ def _learner_loop(opt, duration, warmup_iterations, max_iterations, counters, ch
         torch.cuda.synchronize(opt.device)
     wall = time.perf_counter() - t0
     c1 = counters()
+    opt.flush_metrics()            # the last iteration's deferred metrics / logs (outside the timed window)
     return rows, wall, (c1[0] - c0[0], c1[1] - c0[1])
 
 
@@ -150,6 +152,9 @@ def _summary(rows, wall, actor_steps, dropped, games, config):
         'publish_ms_per_iteration': 1e3 * float(a[:, 8].mean()) if n_it else float('nan'),
         # taking + expanding the next iteration's rollouts while this one's steps run (look-ahead ingest)
         'lookahead_ms_per_iteration': 1e3 * float(a[:, 9].mean()) if n_it else float('nan'),
+        # GPU time from the first to the last training step of an iteration, per step, INSIDE the node loop (actor
+        # graph replays and host enqueue gaps included) — compare with the learner-alone ms_per_step
+        'learner_gpu_ms_per_step': float(np.nanmean(a[:, 10])) if n_it and np.isfinite(a[:, 10]).any() else float('nan'),
         'actor_steps_per_s': actor_steps / wall,
         'queue_dropped': int(dropped), 'games': games, 'config': config,
     }

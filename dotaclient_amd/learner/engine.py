@@ -22,6 +22,7 @@ Batches are dicts of device tensors (see :func:`dotaclient_amd.learner.synthetic
 from __future__ import annotations
 
 import contextlib
+import itertools
 import threading
 from dataclasses import dataclass
 from typing import Dict, Optional
@@ -38,6 +39,9 @@ from .optim import FlatAdam
 # rare buffer growth) take it around their pinned / device allocations, so no allocation from another thread lands
 # inside a capture window (HIP invalidates a capture on some cross-thread API calls even in thread-local mode).
 CAPTURE_LOCK = threading.RLock()
+
+
+_GRAPH_TOKENS = itertools.count(1)   # replay-graph cache tokens (Learner._replay_key)
 
 
 @dataclass
@@ -78,6 +82,7 @@ class Learner:
         self.counts = self.policy.layout.action_counts()
         self.n_steps = 0
         self.graph = None                 # captured forward+backward (see enable_graph)
+        self._static_idx: Dict[tuple, torch.Tensor] = {}    # per replay-graph key: its captured index buffer
         self._graph_warmup = 0
 
     def enable_graph(self, warmup: int = 2):
@@ -309,42 +314,66 @@ class Learner:
             return self._direct_body(bt, B_, S_)
         return self._replay_graph(key, body)
 
+    @staticmethod
+    def _replay_key(replay, B: int, S: int):
+        """Graph-cache key of a replay source. A token unique for the object's lifetime, never ``id()``: a later pool
+        allocated at a freed pool's address must not find (and replay) a graph wired to the freed storage."""
+        tok = replay.__dict__.get('_dca_graph_token')
+        if tok is None:
+            tok = replay.__dict__['_dca_graph_token'] = next(_GRAPH_TOKENS)
+        return ('replay', tok, B, S)
+
+    def release_graphs(self, replay) -> int:
+        """Drop every captured step (and its private memory pool + static index buffer) bound to ``replay`` — call
+        before its storage is reallocated or freed. Returns the number of graphs released."""
+        tok = replay.__dict__.get('_dca_graph_token')
+        if tok is None:
+            return 0
+        graphs = self.__dict__.get('_graphs', {})
+        dead = [k for k in graphs if k[0] == 'replay' and k[1] == tok]
+        for k in dead:
+            g = graphs.pop(k)[0]
+            if self.graph is g or (isinstance(g, tuple) and self.graph in g):
+                self.graph = None
+            self._static_idx.pop(k, None)
+        return len(dead)
+
     def train_step_replay(self, replay, B: int, recent: Optional[int] = None) -> Dict[str, torch.Tensor]:
         """One DP optimizer step on a minibatch sampled from an on-device replay (``learner.replay.HbmReplay``).
         On the direct fused path the gather itself is part of the captured graph (only the sampled indices are
         copied in)."""
         if self.direct() and self._graph_ready() and getattr(replay, 'host_sampling', False):
-            key = ('replay', id(replay), B, replay.S)
-            if key in self.__dict__.get('_graphs', {}) and self._static_idx.numel() == B:
-                # captured step: the sampled positions go straight into the graph's index buffer (one copy)
-                replay.sample_into(self._static_idx, recent)
-                return self.train_step_indices(replay, None)
+            key = self._replay_key(replay, B, replay.S)
+            if key in self.__dict__.get('_graphs', {}):
+                # captured step: the sampled positions go straight into the graph's own index buffer (one copy)
+                replay.sample_into(self._static_idx[key], recent)
+                return self._step_replay_key(replay, key, None)
         return self.train_step_indices(replay, replay.sample_indices(B, recent))
 
     def train_step_indices(self, replay, idx: torch.Tensor) -> Dict[str, torch.Tensor]:
         """One DP optimizer step on the pool sequences ``idx`` (device int64) of ``replay`` — any object with
         ``data`` (field → (capacity, S, …) device tensors at fixed addresses), ``S`` and ``gather(idx)``: the HBM
         replay, or the optimizer's per-iteration pool (epoch permutations over the iteration's sequences)."""
-        if idx is None:                                 # already written into the captured graph's index buffer
-            idx = self._static_idx
         if not self.direct():
             return self.train_step(replay.gather(idx))
-        B = idx.numel()
-        S = replay.S
         if self._graph_ready():
-            key = ('replay', id(replay), B, S)
-            if key not in self.__dict__.get('_graphs', {}):
-                self._static_idx = idx.clone()
-            elif idx is not self._static_idx:
-                self._static_idx.copy_(idx)
-            if self._split_mode():
-                vec = self._replay_split(key, lambda hook: self._direct_body(
-                    self.gather_time_major(replay, self._static_idx, S), B, S, hook=hook))
-            else:
-                vec = self._replay_graph(key, lambda: self._direct_body(
-                    self.gather_time_major(replay, self._static_idx, S), B, S))
+            return self._step_replay_key(replay, self._replay_key(replay, idx.numel(), replay.S), idx)
+        return self._finish(self._direct_body(self.gather_time_major(replay, idx, replay.S), idx.numel(), replay.S))
+
+    def _step_replay_key(self, replay, key, idx: Optional[torch.Tensor]) -> Dict[str, torch.Tensor]:
+        """Captured replay step of graph ``key``; every key owns its static index buffer (``idx`` None: already
+        written into it)."""
+        B, S = key[2], key[3]
+        if key not in self.__dict__.get('_graphs', {}):
+            self._static_idx[key] = idx.clone()
+        elif idx is not None:
+            self._static_idx[key].copy_(idx)
+        sidx = self._static_idx[key]
+        if self._split_mode():
+            vec = self._replay_split(key, lambda hook: self._direct_body(
+                self.gather_time_major(replay, sidx, S), B, S, hook=hook))
         else:
-            vec = self._direct_body(self.gather_time_major(replay, idx, S), B, S)
+            vec = self._replay_graph(key, lambda: self._direct_body(self.gather_time_major(replay, sidx, S), B, S))
         return self._finish(vec)
 
     def _sync_and_step(self):

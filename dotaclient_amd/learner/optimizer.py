@@ -88,6 +88,9 @@ class OptimizerConfig:
     record_consumed: int = 0           # keep the keys (game, team, player, version, length) of the last N rollouts
                                        #     consumed (competing-consumer tests; 0 = off)
     lookahead_ingest: bool = os.environ.get('DCA_LOOKAHEAD', '1') != '0'
+    # pipelined GPU learner with async_checkpoint: publish each iteration's weights right after its steps are queued
+    # and finalise its metrics (the one device→host sync) during the NEXT iteration — no blocking sync per iteration
+    defer_metrics: bool = os.environ.get('DCA_DEFER_METRICS', '1') != '0'
                                        # pipelined GPU ingest: take and expand the NEXT iteration's staged rollouts
                                        #     while this iteration's steps run on the GPU (its host work then overlaps
                                        #     the training instead of leaving the GPU idle between iterations)
@@ -260,14 +263,19 @@ class DotaOptimizer:
         pf = getattr(self, '_prefetcher', None)
         pl = getattr(self, '_pipeline', None)
         dropped = 0
+        ahead = getattr(self, '_lookahead', None)
+        if ahead is not None:
+            # taken off the queue (and logged as consumed) for an iteration that will never run
+            dropped += len(ahead[0])
+            self._lookahead = None
         if pl is not None:                   # the stager first: its fetch returns None once it is stopping
             dropped += pl.close()
             self._pipeline = None
-        if pf is not None or pl is not None:
+        if pf is not None or pl is not None or dropped:
             if pf is not None:
                 dropped += pf.close()
                 self._prefetcher = None
-            self.prefetch_dropped = dropped
+            self.prefetch_dropped = getattr(self, 'prefetch_dropped', 0) + dropped
             xb = getattr(self, '_xp_broker', None)
             if xb is not None and xb is not self.broker and hasattr(xb, 'close'):
                 xb.close()
@@ -428,8 +436,13 @@ class DotaOptimizer:
         fields = [k for k in Learner.STEP_FIELDS + ('h0', 'c0') if k in data]
         if pool is None or pool.capacity < n or set(pool.data) != set(fields) or any(
                 pool.data[k].shape[1:] != data[k].shape[1:] or pool.data[k].dtype != data[k].dtype for k in fields):
-            pool = self._pool = _IterationPool({k: data[k] for k in fields}, max(n, 2 * self.cfg.seq_per_epoch),
-                                               self.cfg.seq_len)
+            cap = max(n, 2 * self.cfg.seq_per_epoch)
+            if pool is not None:
+                # geometric growth (a slowly rising n reallocates O(log n) times, not once per new maximum), and
+                # the captured steps bound to the old storage are released before it is freed
+                cap = max(cap, 2 * pool.capacity)
+                self.learner.release_graphs(pool)
+            pool = self._pool = _IterationPool({k: data[k] for k in fields}, cap, self.cfg.seq_len)
         for k in fields:
             pool.data[k][:n].copy_(data[k][:n])
         return pool
@@ -475,7 +488,9 @@ class DotaOptimizer:
             for it in range(self.iteration_start, end):
                 self._last_iteration = it == end - 1      # no look-ahead: nothing would train on it
                 self.run_iteration(it)
+            self.flush_metrics()
         finally:
+            self._last_iteration = False
             self.close()
             self.flush_checkpoints()
             if self.uploader is not None:
@@ -568,6 +583,13 @@ class DotaOptimizer:
         self.timer.start('train')
         losses, metrics_acc = [], {}
         g = torch.Generator().manual_seed(cfg.seed * 1000003 + it)
+        cuda = self.device.type == 'cuda'
+        ev_t0 = ev_t1 = None
+        if cuda:
+            # in-loop GPU time of this iteration's steps (e2e.learner_gpu_ms_per_step): actor graph replays on the same
+            # device, host enqueue gaps and all
+            ev_t0 = torch.cuda.Event(enable_timing=True)
+            ev_t0.record()
         if self.replay is not None:
             # fresh sequences go into the on-HBM ring; minibatches are sampled from it on-device
             self.replay.add(data, version=it)
@@ -590,12 +612,26 @@ class DotaOptimizer:
                 losses.append(m['loss'])
                 for k, v in m.items():
                     metrics_acc.setdefault(k, []).append(v)
-        ema_snap = None
+        if cuda:
+            ev_t1 = torch.cuda.Event(enable_timing=True)
+            ev_t1.record()
+        defer = self._defer_metrics()
+        published = False
+        if defer and self.checkpoint:
+            # publish BEFORE the look-ahead: the device snapshot of this iteration's weights is queued behind its
+            # steps now, so actors get them one iteration sooner than after the next iteration's data arrived
+            # (a non-finite step never reaches the weights: the fused Adam skips it on the device)
+            self.timer.stop('train')
+            self.timer.start('publish')
+            self.upload_model(version=it)
+            self.timer.stop('publish')
+            self.timer.start('train')
+            published = True
+        ema_snap = self.ema.clone() if (self.ingest == 'device' and (defer or cfg.lookahead_ingest)) else None
         if self._pipelined() and cfg.lookahead_ingest and not getattr(self, '_last_iteration', False):
             # the next iteration's rollouts: staged data taken now and expanded + scanned on the device behind this
             # iteration's steps (the pool / replay copy above already holds this iteration's rows); the EMA state
-            # this iteration reports is snapshotted first (the look-ahead scan advances it)
-            ema_snap = self.ema.clone() if self.ingest == 'device' else None
+            # this iteration reports is the snapshot above (the look-ahead scan advances it)
             self.timer.stop('train')
             self.timer.start('lookahead')
             st2 = self._ingest_pipeline(thread=True).get()
@@ -606,32 +642,63 @@ class DotaOptimizer:
             self._lookahead = (st2.rollouts, st2.n_seq, n2, self._finish_ingest(st2, n2))
             self.timer.stop('lookahead')
             self.timer.start('train')
-        if self.device.type == 'cuda':
+        done = None
+        if cuda:
             # a blocking-sync event: the host thread sleeps until the GPU is done instead of spinning a core that
             # the node's actor threads (same CPU share) can use
-            ev = torch.cuda.Event(blocking=True)
-            ev.record()
-            ev.synchronize()
+            done = torch.cuda.Event(blocking=True)
+            done.record()
+        pending = dict(it=it, losses=losses, metrics_acc=metrics_acc, ema_snap=ema_snap, n_seq=n_seq,
+                       subrewards=subrewards, rollout_lens=rollout_lens, weight_ages=weight_ages, canvas=canvas,
+                       done=done, ev=(ev_t0, ev_t1), n_train=len(losses), published=published)
         self.timer.stop('train')
-        loss_t = torch.stack(losses).float().cpu()
+        if defer:
+            # one-iteration-deferred metrics: this iteration's steps stay queued on the GPU while the host finalises
+            # the PREVIOUS iteration (its event has long completed) and returns to ingest the next one
+            prev, self._pending_metrics = getattr(self, '_pending_metrics', None), pending
+            if prev is not None:
+                self._finalize_iteration(prev)
+        else:
+            self._finalize_iteration(pending)
+
+    def _defer_metrics(self) -> bool:
+        return self._pipelined() and self.cfg.defer_metrics and self.cfg.async_checkpoint
+
+    def flush_metrics(self):
+        """Finalise the iteration whose metrics are still pending (deferred mode): the last one of a run."""
+        prev = getattr(self, '_pending_metrics', None)
+        self._pending_metrics = None
+        if prev is not None:
+            self._finalize_iteration(prev)
+
+    def _finalize_iteration(self, p):
+        """Metrics, NaN / kernel-error checks, logs and (unless already done) the model publish of iteration
+        ``p['it']`` — the reference's end of iteration (optimizer.py:476-563)."""
+        cfg = self.cfg
+        it = p['it']
+        if p['done'] is not None:
+            p['done'].synchronize()
+        loss_t = torch.stack(p['losses']).float().cpu()
         if faults().nan_loss(it):
             loss_t[0] = float('nan')
         if torch.isnan(loss_t).any():
             raise ValueError(f'NaN loss at iteration {it}: {loss_t.tolist()}')
         self.learner.check_error()
-        n_steps = n_seq * cfg.seq_len
+        n_steps = p['n_seq'] * cfg.seq_len
         if self.ingest == 'device':
-            self._sync_running(ema_snap)
+            self._sync_running(p['ema_snap'])
         now = time.time()
         steps_per_s = n_steps / max(now - self.time_last_step, 1e-9)
         self.time_last_step = now
-        sub = np.stack(subrewards) / n_steps * OBSERVATIONS_PER_SECOND
+        sub = np.stack(p['subrewards']) / n_steps * OBSERVATIONS_PER_SECOND
         rollout_rewards = sub.sum(axis=1)
         reward_dict = dict(zip(REWARD_KEYS, sub.sum(axis=0)))
         # every metric's iteration mean in ONE device→host copy (not one synchronising .item() per metric)
+        metrics_acc = p['metrics_acc']
         keys = list(metrics_acc)
         means = torch.stack([torch.stack(metrics_acc[k]).float().mean() for k in keys]).cpu().tolist()
         mean = dict(zip(keys, means))
+        rollout_lens, weight_ages = p['rollout_lens'], p['weight_ages']
         metrics = {
             self.SPEED_KEY: steps_per_s,
             'samples per s per gpu': steps_per_s * cfg.epochs,
@@ -642,6 +709,9 @@ class DotaOptimizer:
             'experience_steps': float(np.sum(rollout_lens)),
             'grad_norm': mean['grad_norm'],
         }
+        e0, e1 = p['ev']
+        if e0 is not None and p['n_train']:
+            metrics['time/gpu_train_ms_per_step'] = e0.elapsed_time(e1) / p['n_train']
         for k in ('approx_kl', 'clipfrac'):
             if k in mean:
                 metrics[k] = mean[k]
@@ -664,18 +734,19 @@ class DotaOptimizer:
             self.timer.start('log')
             hist = None
             if it % cfg.histogram_freq == 1:
-                hist = {name: p.detach().float().cpu().numpy() for name, p in self.policy.named_parameters()}
+                hist = {name: p_.detach().float().cpu().numpy() for name, p_ in self.policy.named_parameters()}
             qs = getattr(self.broker, 'xp_queue_size', None)
             job = (self._write_logs, it, metrics, loss_t.numpy(), np.asarray(rollout_lens), np.asarray(weight_ages),
-                   rollout_rewards, hist, canvas, qs)
+                   rollout_rewards, hist, p['canvas'], qs)
             if cfg.async_checkpoint and self.device.type == 'cuda':
                 self._submit_background(*job)         # tensorboard events + their upload on the ordered writer
             else:
                 job[0](*job[1:])
             self.timer.stop('log')
-            self.timer.start('publish')
-            self.upload_model(version=it)
-            self.timer.stop('publish')
+            if not p['published']:
+                self.timer.start('publish')
+                self.upload_model(version=it)
+                self.timer.stop('publish')
 
     def _write_logs(self, it, metrics, losses, rollout_lens, weight_ages, rollout_rewards, hist, canvas, qs):
         """The reference's tensorboard scalars / histograms / canvas image (optimizer.py:500-561) and the events
@@ -747,6 +818,10 @@ class DotaOptimizer:
         fl, opt = self.learner.flat, self.learner.opt
         snap = {'flat': fl.flat.detach().clone(), 'exp_avg': opt.exp_avg.clone(), 'exp_avg_sq': opt.exp_avg_sq.clone(),
                 'steps': opt.steps.clone()}
+        if self.ingest == 'device':
+            # the reward-normalisation EMA as of these weights (the host mirror may still be an iteration behind
+            # when metrics are deferred): copied with the snapshot, folded into the trainer state by the writer
+            snap['ema'] = self.ema.clone()
         meta = {'n_steps': self.learner.n_steps, 'running': copy.deepcopy(self.running.state_dict()),
                 'hparams': {'lr': opt.lr, 'betas': opt.betas, 'eps': opt.eps, 'max_grad_norm': opt.max_grad_norm},
                 'layout': opt.layout()}
@@ -767,6 +842,13 @@ class DotaOptimizer:
                 snap = _to_cpu(snap)
         fl = self.learner.flat
         flat = snap['flat']
+        if 'ema' in snap:
+            e = snap.pop('ema')
+            run = meta['running']
+            for team, k in self.team_keys.items():
+                if e[k, 2] != 0:
+                    run['mean'][team] = float(e[k, 0])
+                    run['std'][team] = float(e[k, 1])
         # own storage per tensor: the message / checkpoint holds exactly the reference's 30 state_dict tensors
         params = {n: flat[o:o + k].view(p.shape).clone() for n, p, o, k in zip(fl.names, fl.params, fl.offsets,
                                                                                fl.numel)}

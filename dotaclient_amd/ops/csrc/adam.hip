@@ -62,6 +62,7 @@ __global__ __launch_bounds__(kThreads) void adam_update_kernel(
     float b1, float b2, float eps, float max_norm, int divide, const float* __restrict__ skip) {
   __shared__ float red[kThreads / dca::kWave];
   __shared__ float s_coef;
+  __shared__ bool s_bad;
   float acc = 0.f;
   for (int i = threadIdx.x; i < nparts; i += kThreads) acc += partials[i];
   acc = dca::wave_sum(acc);
@@ -75,10 +76,15 @@ __global__ __launch_bounds__(kThreads) void adam_update_kernel(
     float coef = 1.f;
     if (max_norm > 0.f) coef = fminf(1.f, max_norm / (norm + 1e-6f));
     s_coef = coef;
+    // a non-finite gradient (NaN / Inf loss) never reaches the weights: the reference raises before
+    // optimizer.step() (optimizer.py:674-676); the learner raises when it reads the loss, which with deferred
+    // metrics is an iteration later — the weights published meanwhile stay the last finite ones
+    s_bad = !__builtin_isfinite(norm);
     if (blockIdx.x == 0) *norm_out = norm;
   }
   __syncthreads();
   if (skip && *skip != 0.f) return;          // failed step: the norm is reported, nothing is applied
+  if (s_bad) return;
   const float coef = s_coef;
   for (int i = blockIdx.x * kThreads + threadIdx.x; i < n4; i += gridDim.x * kThreads) {
     const int s = seg[i * 4];

@@ -502,6 +502,12 @@ std::vector<torch::Tensor> attn_block_bwd(torch::Tensor dtl, torch::Tensor q, to
   auto part = torch::empty({N, 1024}, o32);
   auto tmp = torch::empty({(int64_t)dca_attn_block_bwd_groups((int)N), 1024}, o32);
   auto sums = torch::empty({1024}, o32);
+  if (trace.has_value() && trace->defined()) {
+    // the kernel writes trace[(n·4 + w)·8 + ev] for rows n < 64 (4 waves, 8 events): 2048 u64 values
+    CHECK_DEV(*trace); CHECK_CONTIG(*trace);
+    TORCH_CHECK(trace->scalar_type() == at::kLong && trace->numel() >= 64 * 4 * 8,
+                "attn_block_bwd: trace must be a contiguous int64 GPU tensor with >= 2048 elements");
+  }
   hip_check(dca_attn_block_bwd_f32(ptr<float>(dtl), ptr<float>(q), (int)q.stride(0), ptr<float>(dx),
                                    ptr<unsigned char>(arg), off, compat ? 1 : 0, ptr<float>(o), ptr<float>(qkv),
                                    ptr<float>(bq), ptr<float>(lse), ptr<float>(e0), ptr<float>(bout), ptr<float>(mu),

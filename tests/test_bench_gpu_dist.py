@@ -30,7 +30,7 @@ def test_bench_two_ranks_on_one_gpu_deploy_shape():
     env = dict(os.environ, PYTHONPATH=ROOT, DCA_SHARED_GPU='1', DCA_DIST_BACKEND='gloo', OMP_NUM_THREADS='4')
     cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node=2',
            '--master-addr', '127.0.0.1', '--master-port', str(_port()), 'bench.py', '--gpus', '2', '--steps', '3',
-           '--warmup', '2', '--bf16-extra', '0', '--actor-games', '256', '--actor-threads', '4', '--e2e', '6',
+           '--warmup', '2', '--bf16x3-extra', '0', '--actor-games', '256', '--actor-threads', '4', '--e2e', '6',
            '--e2e-games', '128', '--e2e-probe', '1']
     # the ranks' progress goes to a file under gpurun_out/ as it happens (a long run stays visibly alive)
     os.makedirs(os.path.join(ROOT, 'gpurun_out'), exist_ok=True)

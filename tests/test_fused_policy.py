@@ -260,3 +260,39 @@ def test_team_formation_failure_never_reaches_the_weights(gpu_ops, monkeypatch, 
     assert torch.equal(L.opt.steps, before[2])
     with pytest.raises(RuntimeError, match='error code 3'):
         L.model.check_error()
+
+
+def test_iteration_pool_growth_releases_captured_graphs(gpu_ops):
+    """The optimizer's per-iteration pool grows twice with graph capture on: each growth releases the graphs bound to
+    the old storage (no stale graph can be replayed at a reused address), every graph key has its own static index
+    buffer, and the captured steps on the new pools match eager steps on the same minibatches."""
+    from dotaclient_amd.learner.optimizer import _IterationPool
+    torch.manual_seed(0)
+    cfg = get_config('lstm128')
+    pol = Policy(cfg)
+    ref = copy.deepcopy(pol)
+    lc = LossConfig(algo='ppo')
+    a = Learner(pol, lc, device='cuda', backend='fused', dp=False)
+    b = Learner(ref, lc, device='cuda', backend='fused', dp=False)
+    assert b.direct() and b.enable_graph(warmup=0)
+    S = 24
+    pool = None
+    for cap, seed in ((4, 1), (8, 2), (16, 3)):
+        data = make_batch(cap, S, cfg.layout, cfg.hidden, device='cuda', seed=seed)
+        fields = {k: v for k, v in data.items() if k in Learner.STEP_FIELDS + ('h0', 'c0')}
+        if pool is not None:
+            n_before = len(b._graphs)
+            assert b.release_graphs(pool) >= 1
+            assert len(b._graphs) < n_before
+        pool = _IterationPool(fields, cap, S)
+        for k in fields:
+            pool.data[k].copy_(fields[k])
+        for step in range(3):
+            idx = torch.randperm(cap, device='cuda')[:4]
+            ma = a.train_step_indices(pool, idx)      # eager (a has no graph)
+            mb = b.train_step_indices(pool, idx)      # captured from its second call on
+            torch.cuda.synchronize()
+            torch.testing.assert_close(mb['loss'], ma['loss'], rtol=1e-5, atol=1e-7, msg=f'cap {cap} step {step}')
+        torch.testing.assert_close(b.flat.flat, a.flat.flat, rtol=1e-5, atol=1e-6)
+    keys = [k for k in b._graphs if k[0] == 'replay']
+    assert len(keys) == 1 and set(b._static_idx) == set(keys)

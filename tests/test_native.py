@@ -77,6 +77,23 @@ def test_crc32c():
     assert native.crc32c(data) == crc ^ 0xFFFFFFFF
 
 
+def _crc_table(data: bytes) -> int:
+    from dotaclient_amd.utils.tfevents import _TABLE
+    crc = 0xFFFFFFFF
+    for x in data:
+        crc = _TABLE[(crc ^ x) & 0xFF] ^ (crc >> 8)
+    return crc ^ 0xFFFFFFFF
+
+
+@pytest.mark.parametrize('n', [(3 << 16) - 1, 3 << 16, (3 << 16) + 1, (3 << 16) + 7, (3 << 16) + 8, (3 << 16) + 13,
+                               400_003, 3 * 131_072 + 5])
+def test_crc32c_three_chain_path_known_answer(n):
+    """Buffers of ≥ 192 KiB take the native three-chain CRC-32C with crc32c_combine (native/core.h): pinned against
+    the table-driven reference at and around the threshold, lengths that are not multiples of 8 or of 3."""
+    data = os.urandom(n)
+    assert native.crc32c(data) == _crc_table(data)
+
+
 def _producer(name, n, k):
     r = native.ShmRing(name, 1 << 16, False)
     for i in range(n):
