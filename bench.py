@@ -69,14 +69,18 @@ def parse():
     ap.add_argument('--graph', type=int, default=-1, help='capture the step in a hipGraph (-1 = auto)')
     ap.add_argument('--actor', type=int, default=1, help='also measure actor steps/s (untimed region)')
     ap.add_argument('--actor-games', type=int, default=2048, help='concurrent 1v1 games of the actor runtime')
-    ap.add_argument('--actor-threads', type=int, default=14,
-                    help='host threads of the native actor runtime per GPU (16-CPU share per GPU)')
+    ap.add_argument('--actor-threads', type=int, default=0,
+                    help='host threads of the native actor runtime per GPU (0 = from this rank\'s CPU share: '
+                         'parallel/placement.py, clamped to [2, 14])')
+    ap.add_argument('--pin', type=int, default=1,
+                    help='pin this rank (learner threads + its actor process) to its GPU-local CPU share')
     ap.add_argument('--e2e', type=float, default=20.0,
                     help='seconds of the end-to-end actors→queue→learners loop on every rank (0 = off)')
     # node-loop actor shape (scripts/e2e_ab.py on one MI355X, 15 s each: 2048 games × 12 threads 1.40 M steps/s
     # (527 k valid), 1024 × 14 1.23 M (508 k): the learner process's stager / decode threads share the host cores)
     ap.add_argument('--e2e-games', type=int, default=2048)
-    ap.add_argument('--e2e-threads', type=int, default=12, help='actor host threads of the node loop')
+    ap.add_argument('--e2e-threads', type=int, default=0,
+                    help='actor host threads of the node loop (0 = from the CPU share, clamped to [2, 12])')
     ap.add_argument('--e2e-mode', default='process', choices=['process', 'thread'],
                     help='e2e actors as one spawned process per rank over the node broker (deploy split) or as a '
                          'thread (1 GPU only)')
@@ -105,6 +109,14 @@ def main():
     device = torch.device(f'cuda:{0 if shared else local}' if use_cuda else 'cpu')
     if use_cuda:
         torch.cuda.set_device(device)
+    # host placement before any worker thread / actor process starts (they inherit the mask)
+    from dotaclient_amd.parallel.placement import for_this_rank
+    place = for_this_rank(pin=bool(args.pin))
+    if not args.actor_threads:
+        args.actor_threads = min(14, place.threads(reserve=2, minimum=2))
+    if not args.e2e_threads:
+        args.e2e_threads = min(12, place.threads(reserve=4, minimum=2))
+    host = dict(place.describe(), actor_threads=args.actor_threads, e2e_threads=args.e2e_threads)
     if world > 1:
         from dotaclient_amd.parallel.dist import init_distribution
         init_distribution(backend=os.environ.get('DCA_DIST_BACKEND') or None, device=device)
@@ -301,6 +313,7 @@ def main():
             e2e = {'error': f'failed on rank(s) {[i for i, x in enumerate(errs) if x]}'}
 
     shas = gather(weights_sha)
+    hosts = gather(host)
     if rank == 0:
         out = {
             'metric': 'PPO optimizer samples/sec (whole node) + actor steps/sec, 1v1-mid LSTM policy',
@@ -337,6 +350,7 @@ def main():
             'weights_sha16_per_rank': shas,
             'actor': actor,
             'e2e': e2e,
+            'host_placement': hosts,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

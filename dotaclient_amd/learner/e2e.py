@@ -121,7 +121,7 @@ def _learner_loop(opt, duration, warmup_iterations, max_iterations, counters, ch
                      m.get('time/train', float('nan')), m.get('time/ingest', float('nan')), m['experience_steps'],
                      m.get('time/h2d', float('nan')), m.get('time/log', float('nan')),
                      m.get('time/publish', float('nan')), m.get('time/lookahead', 0.0),
-                     m.get('time/gpu_train_ms_per_step', float('nan'))))
+                     m.get('time/gpu_train_ms_per_step', float('nan')), m.get('rollouts_consumed', float('nan'))))
         e = check()
         if e:
             raise e
@@ -155,6 +155,7 @@ def _summary(rows, wall, actor_steps, dropped, games, config):
         # GPU time from the first to the last training step of an iteration, per step, INSIDE the node loop (actor
         # graph replays and host enqueue gaps included) — compare with the learner-alone ms_per_step
         'learner_gpu_ms_per_step': float(np.nanmean(a[:, 10])) if n_it and np.isfinite(a[:, 10]).any() else float('nan'),
+        'rollouts_consumed': int(np.nansum(a[:, 11])) if n_it else 0,
         'actor_steps_per_s': actor_steps / wall,
         'queue_dropped': int(dropped), 'games': games, 'config': config,
     }
@@ -367,6 +368,11 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
         out[k] = float(sum(r[k] for r in per_rank))
         out[k + '_per_rank'] = [r[k] for r in per_rank]
     out['queue_dropped'] = int(per_rank[0]['queue_dropped'])
+    # competing consumers on one queue: how evenly the node's rollouts reached the ranks (max / min per rank)
+    cons = [int(r.get('rollouts_consumed', 0)) for r in per_rank]
+    out['rollouts_consumed_per_rank'] = cons
+    out['consumption_skew'] = (max(cons) / max(1, min(cons))) if cons else float('nan')
+    out['learner_gpu_ms_per_step_per_rank'] = [r.get('learner_gpu_ms_per_step') for r in per_rank]
     reports = [r.pop('report') for r in per_rank]
     out.pop('report', None)
     if report is not None:

@@ -650,7 +650,8 @@ class DotaOptimizer:
             done.record()
         pending = dict(it=it, losses=losses, metrics_acc=metrics_acc, ema_snap=ema_snap, n_seq=n_seq,
                        subrewards=subrewards, rollout_lens=rollout_lens, weight_ages=weight_ages, canvas=canvas,
-                       done=done, ev=(ev_t0, ev_t1), n_train=len(losses), published=published)
+                       done=done, ev=(ev_t0, ev_t1), n_train=len(losses), published=published,
+                       n_rollouts=len(rollouts))
         self.timer.stop('train')
         if defer:
             # one-iteration-deferred metrics: this iteration's steps stay queued on the GPU while the host finalises
@@ -707,6 +708,7 @@ class DotaOptimizer:
             'loss/advantage': mean['advantage_loss'], 'entropy': mean['entropy'], 'advantage': mean['advantage'],
             'avg_rollout_len': float(np.mean(rollout_lens)), 'avg_weight_age': float(np.mean(weight_ages)),
             'experience_steps': float(np.sum(rollout_lens)),
+            'rollouts_consumed': float(p['n_rollouts']),
             'grad_norm': mean['grad_norm'],
         }
         e0, e1 = p['ev']

@@ -41,3 +41,8 @@ def test_bench_json_contract_cpu(world):
     assert abs(r['value'] - 2 * world * 16 * 2 / (r['ms_per_step'] * 2 / 1e3)) / r['value'] < 1e-6
     assert r['vs_baseline'] == pytest.approx(r['value'] / 1000.0)
     assert r['dp_replicas_identical'] is True and len(r['weights_sha16_per_rank']) == world
+    # every rank reports the host placement it ran with (CPU share, GPU-local NUMA node, derived thread counts)
+    hp = r['host_placement']
+    assert len(hp) == world and all(h['n_cpus'] >= 1 and h['actor_threads'] >= 2 and h['e2e_threads'] >= 2
+                                    for h in hp)
+    assert [h['local_rank'] for h in hp] == list(range(world))

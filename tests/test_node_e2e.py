@@ -53,7 +53,7 @@ def _worker(rank, world, port, transport, q):
 
 
 @pytest.mark.skipif(not native.AVAILABLE, reason='native module not built')
-@pytest.mark.parametrize('world,transport', [(2, 'shm'), (2, 'tcp'), (4, 'shm'), (4, 'tcp')])
+@pytest.mark.parametrize('world,transport', [(2, 'shm'), (2, 'tcp'), (4, 'shm'), (4, 'tcp'), (8, 'shm'), (8, 'tcp')])
 def test_learner_ranks_share_one_experience_queue(world, transport):
     import glob
     ctx = mp.get_context('spawn')
@@ -91,3 +91,7 @@ def test_learner_ranks_share_one_experience_queue(world, transport):
     assert out['steps_per_s'] > 0 and len(out['steps_per_s_per_rank']) == world
     assert out['actor_steps_per_s'] > 0 and out['queue_dropped'] >= 0
     assert glob.glob(f'/dev/shm/dca_e2e_{ps[0].pid}_*') == []      # rank 0 removed the node's ring + model slot
+    # per-rank consumption counts and their skew (max / min rollouts per rank over the window)
+    cons = out['rollouts_consumed_per_rank']
+    assert len(cons) == world and all(c > 0 for c in cons)
+    assert out['consumption_skew'] == max(cons) / min(cons)
