@@ -86,6 +86,9 @@ def parse():
                          'thread (1 GPU only)')
     ap.add_argument('--e2e-probe', type=float, default=3.0,
                     help='seconds of each actor probe before the e2e window (learner idle / GPU-only learner)')
+    ap.add_argument('--e2e-pack', type=int, default=1,
+                    help='pack whole episodes into the learner sequences (episode-start resets in the recurrence) '
+                         'instead of padding every rollout to seq_len (the reference layout: --e2e-pack 0)')
     ap.add_argument('--e2e-transport', default='auto', choices=['auto', 'shm', 'tcp'],
                     help='node experience queue: shared-memory ring (auto on one node) or a TCP broker on rank 0')
     from dotaclient_amd.presets import parse_with_preset
@@ -298,7 +301,8 @@ def main():
         try:
             from dotaclient_amd.learner.e2e import measure_e2e, measure_e2e_node
             kw = dict(model=args.model, device=device, duration=args.e2e, games=args.e2e_games,
-                      threads=args.e2e_threads, seq_len=args.seq_len, precision=args.precision)
+                      threads=args.e2e_threads, seq_len=args.seq_len, precision=args.precision,
+                      pack=bool(args.e2e_pack))
             progress('e2e start')
             if args.e2e_mode == 'process':
                 e2e = measure_e2e_node(transport=args.e2e_transport, progress=progress, idle_probe=args.e2e_probe,

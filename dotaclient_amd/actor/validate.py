@@ -1,0 +1,69 @@
+"""Validation against the scripted default bot on the native vectorised engine — the reference's only quality signal.
+
+The reference runs a separate validation agent (``--validation``, /root/reference/agent.py:905-927): its hero plays
+the Dota default bot (``HERO_CONTROL_MODE_DEFAULT``) with the latest weights, sends no experience, and writes
+``game/rewards_sum`` / ``game/rewards_<key>`` (and the canvas) to tensorboard per game (agent.py:415-434). Here the
+same evaluation runs many games at once: :class:`~dotaclient_amd.actor.vec.VecActor` in ``vs_default_bot`` mode (the
+controlled side alternates between Radiant and Dire with the game serial; the bot is ``native/vecenv.h``
+``default_bot``, bit-identical to ``env/synthetic.py:256-276``), every finished game's trajectory is decoded from its
+rollout message and reduced to the reference's metrics plus the win rate (end-state reward +1 win / −1 loss / −0.25
+time limit, agent.py:325-337).
+"""
+from __future__ import annotations
+
+import time
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from ..constants import REWARD_KEYS
+
+
+def evaluate_vs_default_bot(policy, n_games: int = 128, device='cuda', seed: int = 12345,
+                            max_dota_time: float = 600.0, threads: int = 8, timeout: float = 600.0,
+                            precision: str = 'bf16') -> Dict[str, float]:
+    """Play ``n_games`` games of ``policy`` (a :class:`~dotaclient_amd.models.policy.Policy`) against the default bot
+    and return the reference's validation metrics averaged over the games: ``game/rewards_sum``,
+    ``game/rewards_<key>`` for every reward key, ``game/win_rate`` (wins / games), ``game/loss_rate``,
+    ``game/steps`` (mean game length) and ``games``. A fixed ``seed`` gives the same games for every policy."""
+    from ..transport.codec import decode
+    from .vec import VecActor
+    from .weights import WeightStore
+
+    ws = WeightStore(policy.config, device='cpu')
+    ws.add(0, {k: v.detach().cpu() for k, v in policy.state_dict().items()})
+    msgs: List[bytes] = []
+    va = VecActor(ws, n_games, msgs.append, device=device, mode='vs_default_bot', seed=seed,
+                  rollout_size=10 ** 9, max_dota_time=max_dota_time, threads=threads, groups=1, stagger=False,
+                  tag=f'val{seed}', precision=precision)
+    t0 = time.time()
+    try:
+        while va.games_finished < n_games:
+            va.step()
+            if time.time() - t0 > timeout:
+                raise TimeoutError(f'validation: {va.games_finished}/{n_games} games after {timeout:.0f} s')
+    finally:
+        va.close()
+    per_game: Dict[str, List[float]] = {}
+    for body in msgs:
+        r = decode(body)
+        rew = np.asarray(r.rewards, np.float64)
+        per_game.setdefault(r.game_id, [])
+        sums = rew.sum(axis=0)
+        row = {'sum': float(sums.sum()), 'steps': float(rew.shape[0]), 'win': float(rew[-1, 1] > 0.5),
+               'loss': float(rew[-1, 1] < -0.5)}
+        row.update({k: float(v) for k, v in zip(REWARD_KEYS, sums)})
+        per_game[r.game_id].append(row)
+    games = [rows[0] for rows in list(per_game.values())[:n_games]]    # one controlled player per game
+    out: Dict[str, float] = {'games': float(len(games))}
+    if not games:
+        return out
+    mean = lambda k: float(np.mean([g[k] for g in games]))             # noqa: E731
+    out['game/rewards_sum'] = mean('sum')
+    out['game/win_rate'] = mean('win')
+    out['game/loss_rate'] = mean('loss')
+    out['game/steps'] = mean('steps')
+    for k in REWARD_KEYS:
+        out[f'game/rewards_{k}'] = mean(k)
+    return out
+

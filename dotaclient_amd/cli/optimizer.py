@@ -3,7 +3,7 @@
 Reference-compatible flags: ``--log-dir --ip --port --epochs --seq-per-epoch --batch-size --seq-len --learning-rate
 --entropy-coef --vf-coef --pretrained-model --mq-prefetch-count -l/--log --run-local``. Additional: ``--broker``,
 ``--algo`` (ppo | vpg), ``--model-preset``, ``--iterations``, ``--device``, ``--backend`` (fused | torch),
-``--precision`` (fp32 | bf16),
+``--precision`` (fp32-exact | fp32 | bf16), ``--pack-sequences``,
 ``--gamma --gae-lambda --clip-eps --max-grad-norm --compat-value-bug --checkpoint-keep``.
 
 Data parallel: launch one process per GPU with ``torch.distributed.run`` (RCCL over xGMI); every rank consumes
@@ -56,8 +56,13 @@ def build_parser():
     ap.add_argument('--graph', type=int, default=1, help='capture the fused train step in a hipGraph')
     ap.add_argument('--async-checkpoint', type=int, default=1,
                     help='publish the model first, write checkpoint files on a background thread')
-    ap.add_argument('--precision', type=str, default='fp32', choices=['fp32', 'bf16'],
-                    help='fp32 = reference training precision (bf16x3 split-MFMA kernels); bf16 = bf16 GEMM operands')
+    ap.add_argument('--precision', type=str, default='fp32-exact', choices=['fp32-exact', 'fp32', 'bf16'],
+                    help='fp32-exact = the reference training precision (IEEE fp32 products on f32 MFMA / VALU); '
+                         'fp32 = fp32 activations with bf16x3-split MFMA operands; bf16 = bf16 GEMM operands '
+                         '(the 5v5 entity-attention policy runs fp32 or bf16)')
+    ap.add_argument('--pack-sequences', type=str2bool, default=False,
+                    help='pack whole episodes into the seq_len sequences with episode-start resets instead of '
+                         'padding every rollout (non-reference layout; GPU device ingest)')
     ap.add_argument('--gamma', type=float, default=0.98)
     ap.add_argument('--gae-lambda', type=float, default=0.95)
     ap.add_argument('--clip-eps', type=float, default=0.1)
@@ -101,7 +106,7 @@ def main(argv=None):
                           checkpoint_keep=args.checkpoint_keep, replay_gb=args.replay_gb,
                           replay_capacity=args.replay_capacity, replay_recent=args.replay_recent,
                           allow_pickle_experience=args.allow_pickle_experience,
-                          prefetch_rollouts=args.prefetch_rollouts)
+                          prefetch_rollouts=args.prefetch_rollouts, pack_sequences=args.pack_sequences)
     broker = make_broker(args.broker or f'tcp://{args.ip}:{args.port}')
     try:
         DotaOptimizer(cfg, broker).run()

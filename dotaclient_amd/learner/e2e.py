@@ -39,7 +39,7 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
                 threads: int = 14, seq_len: int = 1400, batch_size: int = 8, seq_per_epoch: int = 16,
                 epochs: int = 1, precision: str = 'fp32', max_dota_time: float = 600.0, rollout_size: int = 9999,
                 queue_size: int = 64, warmup_iterations: int = 2, max_iterations: Optional[int] = None,
-                log_dir: Optional[str] = None, prefetch: int = 32) -> Dict[str, float]:
+                log_dir: Optional[str] = None, prefetch: int = 32, pack: bool = False) -> Dict[str, float]:
     from ..actor.vec import VecActor
     from ..actor.weights import WeightStore
     from ..transport.broker import InProcBroker
@@ -50,7 +50,7 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
     cfg = OptimizerConfig(log_dir=tmp, epochs=epochs, seq_per_epoch=seq_per_epoch, batch_size=batch_size,
                           seq_len=seq_len, model=model, precision=precision, device=str(device), checkpoint_keep=2,
                           run_local=True, xp_timeout=300.0, histogram_freq=10 ** 9, async_checkpoint=True,
-                          prefetch_rollouts=prefetch)
+                          prefetch_rollouts=prefetch, pack_sequences=pack)
     opt = DotaOptimizer(cfg, broker)                       # publishes model version 0
     ws = WeightStore(model, device='cpu')
     from concurrent.futures import ThreadPoolExecutor
@@ -216,7 +216,7 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                      rollout_size: int = 9999, warmup_iterations: int = 2, max_iterations: Optional[int] = None,
                      log_dir: Optional[str] = None, prefetch: int = 32, ring_bytes: int = 1 << 26,
                      transport: str = 'auto', backend: str = 'auto', idle_probe: float = 3.0,
-                     report=None, record_consumed: int = 0, progress=None) -> Dict[str, float]:
+                     report=None, record_consumed: int = 0, progress=None, pack: bool = False) -> Dict[str, float]:
     """The reference's node topology end to end (optimizer.py:144-150, 274-287; ks-app/components/optimizer.jsonnet:
     79-174): ONE experience queue per node fed by actor processes, ``WORLD_SIZE`` learner ranks (one per GPU, DDP
     over RCCL) consuming disjoint rollouts from it as competing consumers, and rank 0 alone checkpointing and
@@ -288,7 +288,7 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                               seq_len=seq_len, model=model, precision=precision, device=str(device),
                               backend=backend, checkpoint_keep=2, run_local=True, xp_timeout=120.0,
                               histogram_freq=10 ** 9, async_checkpoint=dev.type == 'cuda',
-                              prefetch_rollouts=prefetch, record_consumed=record_consumed)
+                              prefetch_rollouts=prefetch, record_consumed=record_consumed, pack_sequences=pack)
         opt = DotaOptimizer(cfg, broker, checkpoint=rank == 0)     # rank 0 publishes model version 0
         say(f'e2e: learner ready ({transport} broker {addr}); waiting for the actor process')
         if not ready.wait(timeout=900) or failed.is_set():
@@ -382,7 +382,7 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
     out['ranks'] = world
     out['config'] = dict(batch_size=batch_size, seq_len=seq_len, seq_per_epoch=seq_per_epoch, epochs=epochs,
                          rollout_size=rollout_size, max_dota_time=max_dota_time, precision=precision,
-                         prefetch_rollouts=prefetch, games_per_rank=games,
+                         prefetch_rollouts=prefetch, games_per_rank=games, pack_sequences=pack,
                          actor=f'one process per rank over the node {transport} broker', learners=world)
     return out
 

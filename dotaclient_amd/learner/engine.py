@@ -117,7 +117,8 @@ class Learner:
         if self.backend == 'fused':
             return self.model.loss(batch, cfg)
         with self._autocast():
-            logits, values, _ = self.model.forward_packed(batch['env'], batch['units'], self.hidden_from_batch(batch))
+            logits, values, _ = self.model.forward_packed(batch['env'], batch['units'], self.hidden_from_batch(batch),
+                                                          reset=batch.get('reset'))
         logits = {k: v.float() for k, v in logits.items()}
         values = values.float()
         actions = split_heads(batch['actions'], self.counts)
@@ -155,6 +156,8 @@ class Learner:
             if v is None:
                 v = torch.zeros(B, S, device=batch['env'].device)
             out[k] = v.transpose(0, 1).reshape(S * B, *v.shape[2:]).contiguous()
+        if 'reset' in batch:                # sequence packing: episode-start flags (B,S) u8 → time-major rows
+            out['reset'] = batch['reset'].transpose(0, 1).reshape(S * B).contiguous()
         for k in ('h0', 'c0'):
             if k in batch:
                 out[k] = batch[k].contiguous()
@@ -164,19 +167,20 @@ class Learner:
         """Minibatch of replay rows ``idx`` gathered straight into time-major rows: one index_select per field
         over the pool viewed as (capacity·S, …) — no batch-major copy, no transpose."""
         B = idx.numel()
+        fields = self.STEP_FIELDS + (('reset',) if 'reset' in replay.data else ())
         if idx.is_cuda:                 # one HIP launch for every field (ops/csrc/glue.hip replay_gather)
             from .. import ops
             seq = [k for k in ('h0', 'c0') if k in replay.data]
-            outs = ops.require().replay_gather([replay.data[k] for k in self.STEP_FIELDS] +
-                                               [replay.data[k] for k in seq], len(self.STEP_FIELDS),
+            outs = ops.require().replay_gather([replay.data[k] for k in fields] +
+                                               [replay.data[k] for k in seq], len(fields),
                                                idx.contiguous())
-            return dict(zip(list(self.STEP_FIELDS) + seq, outs))
+            return dict(zip(list(fields) + seq, outs))
         ar = getattr(self, '_arange', None)
         if ar is None or ar.numel() < S or ar.device != idx.device:
             ar = self._arange = torch.arange(max(S, 1), device=idx.device, dtype=torch.long)
         rows = (idx.view(1, B) * S + ar[:S].view(S, 1)).reshape(-1)
         out = {}
-        for k in self.STEP_FIELDS:
+        for k in fields:
             pool = replay.data[k]
             out[k] = pool.view(-1, *pool.shape[2:]).index_select(0, rows)
         for k in ('h0', 'c0'):

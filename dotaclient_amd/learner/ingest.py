@@ -15,6 +15,15 @@ training of every iteration (decode → pad into pinned buffers → H2D of the p
 
 Slot reuse is event-ordered: the host waits for a slot's previous upload to finish before repacking it, and the copy
 stream waits for the learner stream's "consumed" event before overwriting the slot's device bytes.
+
+Sequence packing (``pack=True``, non-compat): instead of padding every rollout to a multiple of ``seq_len`` (the
+reference, optimizer.py:355-378 — with ≈560-step games in 1400-step sequences 60 % of the trained rows are padding),
+whole rollouts that start from a zero recurrent state are placed first-fit into the free tail of an open sequence.
+The row where such a rollout starts carries a ``reset`` flag: the recurrence treats h, c as zero before that step
+(forward and backward, ops/csrc/lstm_team.hip), so each episode sees exactly the state it would have seen at the start
+of its own padded sequence. Rollouts longer than a sequence, or starting from a stored non-zero state, keep the
+padded layout (aligned at a sequence start, the stored chunk states as h0 / c0); their last sequence's free tail is
+packed like any other. The return / GAE scan segments are the rollouts in row order.
 """
 from __future__ import annotations
 
@@ -38,6 +47,51 @@ def _round(n: int) -> int:
 
 class _Stopped(Exception):
     pass
+
+
+def _zero_start(r: Rollout) -> bool:
+    """A rollout whose recurrent state at its first step is zero (a game start): it may begin mid-sequence."""
+    h = r.hiddens
+    return h is None or len(h) == 0 or not np.any(np.asarray(h[0]))
+
+
+class SequencePacker:
+    """First-fit placement of rollouts into ``S``-row sequences (see the module docstring). ``add`` places one
+    rollout; ``fits`` tells whether it would go into an open sequence without opening a new one."""
+
+    def __init__(self, S: int, pack: bool = True):
+        self.S, self.pack = int(S), bool(pack)
+        self.n_seq = 0
+        self.open: List[List[int]] = []          # [sequence index, rows used] of sequences with a free tail
+        self.starts: List[int] = []              # first padded row of every added rollout
+        self.seq_src: List[Optional[tuple]] = []  # per sequence: (rollout index, chunk) starting at its row 0
+        self.resets: List[int] = []              # rows where a packed rollout starts mid-sequence
+
+    def fits(self, r: Rollout) -> bool:
+        T = r.length
+        return self.pack and T <= self.S and _zero_start(r) and any(self.S - u >= T for _, u in self.open)
+
+    def add(self, r: Rollout) -> int:
+        S, T, i = self.S, r.length, len(self.starts)
+        if self.pack and T <= S and _zero_start(r):
+            for slot in self.open:
+                if S - slot[1] >= T:
+                    start = slot[0] * S + slot[1]
+                    slot[1] += T
+                    self.starts.append(start)
+                    if start % S:
+                        self.resets.append(start)
+                    return start
+        k = -(-T // S)
+        start = self.n_seq * S
+        for c in range(k):
+            self.seq_src.append((i, c))
+        tail = T - (k - 1) * S
+        if self.pack and tail < S:
+            self.open.append([self.n_seq + k - 1, tail])
+        self.n_seq += k
+        self.starts.append(start)
+        return start
 
 
 @dataclass
@@ -68,9 +122,11 @@ class IngestPipeline:
     """Stager thread + double-buffered pinned/device slots (see module docstring)."""
 
     def __init__(self, fetch: Optional[Callable], seq_len: int, seq_per_epoch: int, algo: str, hidden: int, device,
-                 depth: int = 1):
+                 depth: int = 1, pack: bool = False):
         """``fetch=None``: no stager thread — the learner calls :meth:`stage` and :meth:`expand` inline."""
         self.fetch = fetch                      # fetch(stop_event) -> Rollout | None
+        self.pack = bool(pack)
+        self._carry: Optional[Rollout] = None   # packing: fetched rollout that did not fit the previous iteration
         self.S = int(seq_len)
         self.need = int(seq_per_epoch)
         self.algo = algo
@@ -91,15 +147,33 @@ class IngestPipeline:
 
     # ---- stager thread -----------------------------------------------------------------------------
     def _gather(self) -> Optional[List[Rollout]]:
-        rollouts, n_seq = [], 0
-        while n_seq < self.need:
-            r = self.fetch(self.stop)
+        if not self.pack:
+            rollouts, n_seq = [], 0
+            while n_seq < self.need:
+                r = self.fetch(self.stop)
+                if r is None:
+                    self.lost += len(rollouts)
+                    return None
+                rollouts.append(r)
+                n_seq += -(-r.length // self.S)
+            return rollouts
+        # packing: at least ``need`` sequences, then keep filling their free tails until a rollout does not fit
+        # (it is carried over to the next iteration) or every open tail is nearly full
+        pk, rollouts = SequencePacker(self.S), []
+        while True:
+            r, self._carry = self._carry, None
+            if r is None:
+                r = self.fetch(self.stop)
             if r is None:
                 self.lost += len(rollouts)
                 return None
+            if pk.n_seq >= self.need and not pk.fits(r):
+                self._carry = r
+                return rollouts
+            pk.add(r)
             rollouts.append(r)
-            n_seq += -(-r.length // self.S)
-        return rollouts
+            if pk.n_seq >= self.need and all(self.S - u < 32 for _, u in pk.open):
+                return rollouts
 
     def _run(self):
         import contextlib
@@ -129,11 +203,21 @@ class IngestPipeline:
         """Pack the valid rows of every field into the next pinned slot and issue its upload (any thread)."""
         t0 = time.perf_counter()
         S = self.S
+        pk = SequencePacker(S, self.pack)
+        for r in rollouts:
+            pk.add(r)
+        # rollouts in row order: the scan's segments are [start_s, start_{s+1}) (a rollout plus the free tail that
+        # follows it in its sequence)
+        order = sorted(range(len(rollouts)), key=lambda i: pk.starts[i])
+        rank = {i: k for k, i in enumerate(order)}
+        seq_src = [None if src is None else (rank[src[0]], src[1]) for src in pk.seq_src]
+        rollouts = [rollouts[i] for i in order]
+        starts = [pk.starts[i] for i in order]
         lens = [r.length for r in rollouts]
-        seqs = [-(-T // S) for T in lens]
-        off = np.zeros(len(rollouts) + 1, np.int64)
-        off[1:] = np.cumsum([n * S for n in seqs])
-        L, Lv, n_seq = int(off[-1]), int(sum(lens)), int(sum(seqs))
+        n_seq = pk.n_seq
+        L, Lv = n_seq * S, int(sum(lens))
+        off = np.asarray(starts + [L], np.int64)
+        resets = np.asarray(pk.resets, np.int64)
         r0 = rollouts[0]
         U, A, K = r0.units.shape[1], r0.actions.shape[1], r0.rewards.shape[1]
         gae_mode = self.algo == 'ppo' and all(r.values is not None for r in rollouts)
@@ -151,6 +235,10 @@ class IngestPipeline:
         if self.H:
             hid_off = nbytes
             nbytes += _round(n_seq * 2 * self.H * 4)
+        rst_off = None
+        if self.pack:
+            rst_off = nbytes                     # (L,) u8 episode-start flags in the padded layout
+            nbytes += _round(L)
         slot_i = self._k % 2
         slot = self.slots[slot_i]
         while not slot.free.acquire(timeout=0.1):      # the learner has not expanded this slot's last contents yet
@@ -201,16 +289,20 @@ class IngestPipeline:
             pos += T
         if self.H:
             hid = hview(hid_off, n_seq * 2 * self.H * 4, 'float32', (n_seq, 2, self.H))
-            i = 0
-            for r, T in zip(rollouts, lens):
-                for s in range(-(-T // S)):
-                    a = s * S
+            for i, src in enumerate(seq_src):
+                # the state at the sequence's first row: the stored state of the rollout chunk that starts there
+                # (zero for a game start, and for packed sequences — their rollouts start from zero)
+                hid[i] = 0.0
+                if src is not None:
+                    r = rollouts[src[0]]
+                    a = src[1] * S
                     if r.hiddens is not None and r.hidden_stride and a % r.hidden_stride == 0 \
                             and a // r.hidden_stride < len(r.hiddens):
                         hid[i] = r.hiddens[a // r.hidden_stride]
-                    else:
-                        hid[i] = 0.0
-                    i += 1
+        if self.pack:
+            rv = hview(rst_off, L, 'uint8', (L,))
+            rv[:] = 0
+            rv[resets] = 1
         ev = None
         if self.cuda:
             ev = torch.cuda.Event()
@@ -226,6 +318,8 @@ class IngestPipeline:
         if self.H:
             views['hid'] = slot.dev[hid_off:hid_off + n_seq * 2 * self.H * 4].view(torch.float32).view(n_seq, 2,
                                                                                                        self.H)
+        if self.pack:
+            views['reset'] = slot.dev[rst_off:rst_off + L]
         return StagedIteration(rollouts=rollouts, lens=lens, off=off, n_seq=n_seq, L=L, Lv=Lv, gae_mode=gae_mode,
                                views=views, ready=ev, slot=slot_i, stage_s=time.perf_counter() - t0)
 
@@ -270,6 +364,8 @@ class IngestPipeline:
         out['valid'] = vb
         if 'hid' in v:
             out['hid'] = v['hid'].clone()
+        if 'reset' in v:
+            out['reset'] = v['reset'].clone()
         slot = self.slots[st.slot]
         if cur is not None:
             ev = torch.cuda.Event()
@@ -286,7 +382,8 @@ class IngestPipeline:
         self.th.join(timeout=30.0)
         if self.th.is_alive():
             raise RuntimeError('experience stager thread did not stop')
-        dropped = self.lost
+        dropped = self.lost + (1 if self._carry is not None else 0)
+        self._carry = None
         while True:
             try:
                 dropped += len(self.q.get_nowait().rollouts)

@@ -70,7 +70,7 @@ class OptimizerConfig:
     normalize_advantages: bool = True
     device: str = 'auto'
     backend: str = 'auto'
-    precision: str = 'fp32'            # 'fp32' (reference precision) | 'bf16' (bf16 GEMM operands, fp32 accumulation)
+    precision: str = 'fp32-exact'      # 'fp32-exact' (reference precision, IEEE fp32 products) | 'fp32' (bf16x3 operands) | 'bf16'
     checkpoint_keep: int = 0
     histogram_freq: int = 128          # optimizer.py:214
     xp_timeout: Optional[float] = None
@@ -88,6 +88,9 @@ class OptimizerConfig:
     record_consumed: int = 0           # keep the keys (game, team, player, version, length) of the last N rollouts
                                        #     consumed (competing-consumer tests; 0 = off)
     lookahead_ingest: bool = os.environ.get('DCA_LOOKAHEAD', '1') != '0'
+    # non-compat: pack whole zero-state rollouts first-fit into the free tails of the iteration's sequences (episode
+    # starts flagged, the recurrence resets h, c there) instead of padding each rollout to seq_len (learner/ingest.py)
+    pack_sequences: bool = False
     # pipelined GPU learner with async_checkpoint: publish each iteration's weights right after its steps are queued
     # and finalise its metrics (the one device→host sync) during the NEXT iteration — no blocking sync per iteration
     defer_metrics: bool = os.environ.get('DCA_DEFER_METRICS', '1') != '0'
@@ -172,13 +175,19 @@ class DotaOptimizer:
         lc = LossConfig(algo=cfg.algo, learning_rate=cfg.learning_rate, entropy_coef=cfg.entropy_coef,
                         vf_coef=cfg.vf_coef, clip_eps=cfg.clip_eps, gamma=cfg.gamma, gae_lambda=cfg.gae_lambda,
                         max_grad_norm=cfg.max_grad_norm, compat_value_bug=cfg.compat_value_bug)
-        self.learner = Learner(self.policy, lc, device=self.device, backend=cfg.backend, precision=cfg.precision)
+        prec = cfg.precision
+        if prec == 'fp32-exact' and self.policy_cfg.entity_attention:
+            logger.info('5v5 entity attention has no exact-fp32 kernels: training at fp32 with bf16x3 operands')
+            prec = 'fp32'
+        self.learner = Learner(self.policy, lc, device=self.device, backend=cfg.backend, precision=prec)
         if cfg.graph:
             self.learner.enable_graph(warmup=1)
         if trainer_state is not None:
             self.learner.load_state_dict(trainer_state['learner'])
             self.running.load_state_dict(trainer_state['running'])
         self.ingest = cfg.ingest if cfg.ingest != 'auto' else ('device' if self.device.type == 'cuda' else 'host')
+        if cfg.pack_sequences and self.ingest != 'device':
+            raise ValueError('pack_sequences needs the device ingest (ingest="device")')
         # per-team EMA(0.99) reward statistics as device state (mean, std, initialised) for the device ingest path
         self.ema = torch.zeros(self.MAX_TEAMS, 3, device=self.device)
         for team in self.running.mean:
@@ -383,7 +392,7 @@ class DotaOptimizer:
                 pf = self._prefetcher = _RolloutPrefetcher(self._consume_decode, self.cfg.prefetch_rollouts)
                 fetch = pf.get_until
             pl = self._pipeline = IngestPipeline(fetch, self.cfg.seq_len, self.cfg.seq_per_epoch, self.cfg.algo, H,
-                                                 self.device)
+                                                 self.device, pack=self.cfg.pack_sequences)
         return pl
 
     def _finish_ingest(self, st, n_keep: int) -> Dict[str, torch.Tensor]:
@@ -411,6 +420,8 @@ class DotaOptimizer:
         if self.policy.is_recurrent:
             h = x['hid'][:n_keep]
             d['h0'], d['c0'] = h[:, 0].contiguous(), h[:, 1].contiguous()
+            if 'reset' in x:
+                d['reset'] = x['reset'][:n_rows].view(n_keep, S)
         self._normalize_advantages(d)
         return d
 
@@ -433,7 +444,7 @@ class DotaOptimizer:
         step replays with its gather inside) instead of an ``index_select`` of every field per minibatch followed by
         the step's own batch-major → time-major copies."""
         pool = getattr(self, '_pool', None)
-        fields = [k for k in Learner.STEP_FIELDS + ('h0', 'c0') if k in data]
+        fields = [k for k in Learner.STEP_FIELDS + ('h0', 'c0', 'reset') if k in data]
         if pool is None or pool.capacity < n or set(pool.data) != set(fields) or any(
                 pool.data[k].shape[1:] != data[k].shape[1:] or pool.data[k].dtype != data[k].dtype for k in fields):
             cap = max(n, 2 * self.cfg.seq_per_epoch)

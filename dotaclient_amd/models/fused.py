@@ -466,7 +466,9 @@ class FusedPolicy:
         adv = batch['adv'].reshape(N).contiguous() if 'adv' in batch else zeros
         lpo = batch['logp_old'].reshape(N).contiguous() if 'logp_old' in batch else zeros
         nret = batch['norm_ret'].reshape(N).contiguous() if 'norm_ret' in batch else zeros
+        rst = batch.get('reset')
         if not self.fully_fused and not self.use_pipeline():
+            assert rst is None or not bool(rst.any()), 'packed sequences need the pipelined LSTM step'
             xh, emb, _, _ = self.trunk(batch['env'], batch['units'], batch.get('h0'), batch.get('c0'))
             w, b = self.head_cat(dict(zip(self.param_names, self.params)), differentiable=True)
             U = emb.shape[2]
@@ -478,12 +480,15 @@ class FusedPolicy:
             h0 = torch.zeros(B, H, device=dev)
             c0 = torch.zeros(B, H, device=dev)
         self.refresh()
-        fn = _PolicyLoss
         if self.use_pipeline():
             from .pipelined import PipelinedPolicyLoss
-            fn = PipelinedPolicyLoss
-        part, logp = fn.apply(self, batch['units'].contiguous(), batch['env'].contiguous(), actions, masks,
-                              adv, ret, lpo, nret, norms, h0.contiguous(), c0.contiguous(), *self.params)
+            part, logp = PipelinedPolicyLoss.apply(self, batch['units'].contiguous(), batch['env'].contiguous(), actions,
+                                                   masks, adv, ret, lpo, nret, norms, h0.contiguous(), c0.contiguous(),
+                                                   rst, *self.params)
+        else:
+            assert rst is None or not bool(rst.any()), 'packed sequences need the pipelined LSTM step'
+            part, logp = _PolicyLoss.apply(self, batch['units'].contiguous(), batch['env'].contiguous(), actions, masks,
+                                           adv, ret, lpo, nret, norms, h0.contiguous(), c0.contiguous(), *self.params)
         loss, metrics = assemble_loss(part, norms, cfg, ret, N, S)
         return loss, metrics
 

@@ -263,7 +263,8 @@ def fused_step_tm(fp, *args, **kw):
 
 
 def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], units_t, env_t, act_t, msk_t, adv_t,
-                   ret_t, lpo_t, nret_t, norms, h0, c0, B: int, S: int, gout: Optional[Dict[str, torch.Tensor]] = None):
+                   ret_t, lpo_t, nret_t, norms, h0, c0, B: int, S: int, gout: Optional[Dict[str, torch.Tensor]] = None,
+                   reset_t: Optional[torch.Tensor] = None):
     """Loss partials and all parameter gradients of one minibatch, from TIME-MAJOR rows (row = t·B + b).
 
     ``W`` = :class:`WeightImages` views, ``P`` = fp32 parameters (for the small fp32 weights used directly).
@@ -366,6 +367,10 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     gates4 = torch.empty(S, B, H, 4, device=dev)
     spans = chunk_bounds(S, fp.chunks)
     one = len(spans) == 1            # single chunk: outputs are used as produced (no staging copies)
+    # sequence packing (learner/ingest.py): per-(step, row) episode-start flags, time-major (S, B) u8 — the team
+    # recurrence zeroes h, c before a flagged step (forward) and stops the gradient there (backward)
+    rst = reset_t.reshape(S, B) if reset_t is not None else None
+    assert rst is None or one, 'packed sequences run as one time chunk'
     assert one or not attn32, "the fp32 entity-attention step runs as one time chunk"
     if not one:
         dxh = torch.empty(S, B, H, device=dev)
@@ -388,7 +393,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         for t0, t1 in spans:
             o = team_fwd(C, xp4[t0:t1], whh16, h_c, c_c, fp.err, False, time_major=True,
                          hs_out=hs16[t0:t1], cs_out=cs[t0:t1], gates_out=gates4[t0:t1], bias4=bias_p,
-                         precise=exact and _EXACT_LIBM_ACT)
+                         precise=exact and _EXACT_LIBM_ACT, reset=rst)
             h_c, c_c = o[4], o[5]
             e = torch.cuda.Event()
             e.record(sL)
@@ -483,7 +488,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             cinit = c0.contiguous() if t0 == 0 else cs[t0 - 1]
             o = team_bwd(C, dxh[t0:t1], gates4[t0:t1], cs[t0:t1], cinit, dh_n, dc_n, whh16, fp.err,
                          time_major=True, dg_out=dgates16[t0:t1], dg_bf16=not f32,
-                         want_dbias=True, precise=exact and _EXACT_LIBM_ACT)
+                         want_dbias=True, precise=exact and _EXACT_LIBM_ACT, reset=rst)
             dh_n, dc_n = o[1], o[2]
             db = _acc(db, o[3])
             e = torch.cuda.Event()
@@ -502,7 +507,11 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         n = r1 - r0
         dG16 = dgates16[t0:t1].view(n, 4 * H)
         with torch.cuda.stream(sL if wg_side else main):
-            if t0 > 0:
+            if rst is not None:
+                # packed: the h_{t-1} operand is zero where an episode starts at t (the forward never used it)
+                hprev = torch.cat([h016.unsqueeze(0), hs16[:S - 1]], 0).masked_fill_(rst.bool().unsqueeze(2), 0.0)
+                gemm_tn(dG16, hprev.view(n, H), out=dWhh, perm=gperm, accumulate=True)
+            elif t0 > 0:
                 gemm_tn(dG16, hs16[t0 - 1:t1 - 1].view(n, H), out=dWhh, perm=gperm, accumulate=True)
             else:       # h_{t-1} rows: h0 for t = 0, then hs[0 : t1-1] — no concatenation materialised
                 gemm_tn(dG16, hs16[0:t1 - 1].view(n - B, H), out=dWhh, perm=gperm, accumulate=True, b0=h016)
@@ -653,7 +662,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
 
 class PipelinedPolicyLoss(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, fp, units, env, actions, masks, adv, ret, logp_old, nret, norms, h0, c0, *params):
+    def forward(ctx, fp, units, env, actions, masks, adv, ret, logp_old, nret, norms, h0, c0, reset, *params):
         P = dict(zip(fp.param_names, params))
         B, S, U, _ = units.shape
         N = B * S
@@ -661,8 +670,9 @@ class PipelinedPolicyLoss(torch.autograd.Function):
         units_t = units.transpose(0, 1).reshape(N, U, 10).contiguous()
         env_t = env.transpose(0, 1).reshape(N, 3).contiguous()
         W = fp.weight_images().refresh(fp.C)
+        rst_t = reset.reshape(B, S).transpose(0, 1).reshape(N).contiguous() if reset is not None else None
         part, logp, grads = fused_step_tm(fp, W, P, units_t, env_t, tm(actions), tm(masks), tm(adv), tm(ret),
-                                          tm(logp_old), tm(nret), norms, h0, c0, B, S)
+                                          tm(logp_old), tm(nret), norms, h0, c0, B, S, reset_t=rst_t)
         ctx.grads = [grads.get(nm) for nm in fp.param_names]
         ctx.fp = fp
         logp_b = logp.view(S, B).t().reshape(N)        # back to batch-major (B·S) row order
@@ -673,7 +683,7 @@ class PipelinedPolicyLoss(torch.autograd.Function):
     def backward(ctx, gpart, _glogp):
         ctx.fp.apply_direct_grads(ctx.grads, gpart[15])
         ctx.grads = None
-        return (None,) * (12 + len(ctx.fp.param_names))
+        return (None,) * (13 + len(ctx.fp.param_names))
 
 
 def train_direct(fp, batch_tm: Dict[str, torch.Tensor], B: int, S: int) -> torch.Tensor:
@@ -704,7 +714,8 @@ def train_direct(fp, batch_tm: Dict[str, torch.Tensor], B: int, S: int) -> torch
     gout = {nm: P[nm].grad for nm in DIRECT_GEMM_GRADS}
     part, _, grads = fused_step_tm(fp, W, P, batch_tm['units'], batch_tm['env'], batch_tm['actions'],
                                    batch_tm['masks'], batch_tm['adv'], batch_tm['ret'], batch_tm['logp_old'],
-                                   batch_tm['norm_ret'], norms, h0, c0, B, S, gout=gout)
+                                   batch_tm['norm_ret'], norms, h0, c0, B, S, gout=gout,
+                                   reset_t=batch_tm.get('reset'))
     fp.apply_direct_grads([grads.get(nm) for nm in fp.param_names], None,
                           written=set(DIRECT_GEMM_GRADS) | set(fp.early_applied))
     out = torch.empty(16, device=dev)

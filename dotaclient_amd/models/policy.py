@@ -218,13 +218,31 @@ class Policy(nn.Module):
         x = F.relu(self.affine_pre_rnn(x))
         return x, unit_embedding
 
-    def recurrent(self, x: torch.Tensor, hidden=None):
+    def recurrent(self, x: torch.Tensor, hidden=None, reset: Optional[torch.Tensor] = None):
+        """``reset`` (B, S) bool/u8, sequence packing: an episode starts at step t of row b — its h, c are zero
+        before that step (the oracle of the fused recurrence's reset flags, ops/csrc/lstm_team.hip)."""
         if self.config.rnn == 'linear':
             return self.fake_rnn(x), hidden
         if hidden is None:
             hidden = self.initial_hidden(x.shape[0], device=x.device, dtype=x.dtype)
+        if reset is not None and bool(reset.any()):
+            return self._lstm_with_resets(x, hidden, reset.bool())
         out, hidden = self.rnn(x, hidden)
         return out, hidden
+
+    def _lstm_with_resets(self, x, hidden, reset):
+        r = self.rnn
+        h, c = hidden[0][0], hidden[1][0]
+        xp = F.linear(x, r.weight_ih_l0, r.bias_ih_l0 + r.bias_hh_l0)
+        outs = []
+        for t in range(x.shape[1]):
+            keep = (~reset[:, t]).to(x.dtype).unsqueeze(1)
+            h, c = h * keep, c * keep
+            i, f, g, o = (xp[:, t] + F.linear(h, r.weight_hh_l0)).chunk(4, 1)
+            c = torch.sigmoid(f) * c + torch.sigmoid(i) * torch.tanh(g)
+            h = torch.sigmoid(o) * torch.tanh(c)
+            outs.append(h)
+        return torch.stack(outs, 1), (h.unsqueeze(0), c.unsqueeze(0))
 
     def heads(self, x: torch.Tensor, unit_embedding: torch.Tensor):
         q = self.affine_unit_attention(x)                                        # (B,S,unit_dim)
@@ -237,9 +255,9 @@ class Policy(nn.Module):
         }
         return d, self.affine_value(x)
 
-    def forward_packed(self, env: torch.Tensor, units: torch.Tensor, hidden=None):
+    def forward_packed(self, env: torch.Tensor, units: torch.Tensor, hidden=None, reset=None):
         x, unit_embedding = self.encode(env, units)
-        x, hidden = self.recurrent(x, hidden)
+        x, hidden = self.recurrent(x, hidden, reset)
         logits, value = self.heads(x, unit_embedding)
         return logits, value, hidden
 

@@ -150,6 +150,14 @@ inline torch::Tensor out_or_new(const c10::optional<torch::Tensor>& o, at::IntAr
 }
 }  // namespace
 
+// sequence-packing reset flags: (S, B) time-major or (B, S) u8, 1 where an episode starts (h, c := 0 before that step)
+inline const unsigned char* reset_ptr(const c10::optional<torch::Tensor>& r, int B, int S) {
+  if (!r.has_value() || !r->defined()) return nullptr;
+  CHECK_DEV(*r); CHECK_CONTIG(*r);
+  TORCH_CHECK(r->scalar_type() == at::kByte && r->numel() == (int64_t)B * S, "reset must be B*S uint8 flags");
+  return r->data_ptr<unsigned char>();
+}
+
 inline void check_ctl(const torch::Tensor& ctl) {
   CHECK_DEV(ctl); CHECK_CONTIG(ctl);
   TORCH_CHECK(ctl.numel() * ctl.element_size() >= (int64_t)dca_lstm_team_ctl_bytes(),
@@ -161,7 +169,8 @@ std::vector<torch::Tensor> lstm_team_fwd(torch::Tensor xp4, torch::Tensor whh, t
                                          c10::optional<torch::Tensor> trace,
                                          bool time_major, c10::optional<torch::Tensor> hs_out,
                                          c10::optional<torch::Tensor> cs_out, c10::optional<torch::Tensor> gates_out,
-                                         c10::optional<torch::Tensor> bias4, bool precise) {
+                                         c10::optional<torch::Tensor> bias4, bool precise,
+                                         c10::optional<torch::Tensor> reset) {
   CHECK_F32(xp4); CHECK_DEV(whh); CHECK_CONTIG(whh); CHECK_F32(h0); CHECK_F32(c0); CHECK_I32(err); check_ctl(ctl);
   const bool f32w = whh.scalar_type() == at::kFloat;
   TORCH_CHECK(f32w || whh.scalar_type() == at::kBFloat16, "whh must be bf16 or f32");
@@ -193,7 +202,7 @@ std::vector<torch::Tensor> lstm_team_fwd(torch::Tensor xp4, torch::Tensor whh, t
                               ptr<float>(gates4), ptr<float>(hn), ptr<float>(cn), ctl.data_ptr(), ws.data_ptr(), wsb,
                               ptr<unsigned>(err), B, S, H, time_major ? 1 : 0, cur_stream(),
                               (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr,
-                              bias_p, f32w ? 1 : 0, precise ? 1 : 0),
+                              bias_p, f32w ? 1 : 0, precise ? 1 : 0, reset_ptr(reset, B, S)),
             "dca_lstm_team_fwd");
   if (f32w) return {hs, hs, cs, gates4, hn, cn};
   return {hs, want_f32_h ? hsf : hs, cs, gates4, hn, cn};
@@ -204,7 +213,7 @@ std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4
                                          c10::optional<torch::Tensor> dcn, torch::Tensor whh, torch::Tensor err,
                                          torch::Tensor ctl, c10::optional<torch::Tensor> trace, bool time_major,
                                          c10::optional<torch::Tensor> dg_out, bool dg_bf16, bool want_dbias,
-                                         bool precise) {
+                                         bool precise, c10::optional<torch::Tensor> reset) {
   CHECK_F32(dhs); CHECK_F32(gates4); CHECK_F32(cs); CHECK_F32(c0); CHECK_DEV(whh); CHECK_CONTIG(whh); CHECK_I32(err);
   check_ctl(ctl);
   const bool f32w = whh.scalar_type() == at::kFloat;
@@ -238,7 +247,7 @@ std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4
                               time_major ? 1 : 0, cur_stream(),
                               (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr,
                               dg_bf16 ? ptr<short>(dgates4) : nullptr, want_dbias ? ptr<float>(dbp) : nullptr,
-                              f32w ? 1 : 0, precise ? 1 : 0),
+                              f32w ? 1 : 0, precise ? 1 : 0, reset_ptr(reset, B, S)),
             "dca_lstm_team_bwd");
   if (want_dbias) return {dgates4, dh0, dc0, dbp.sum(0)};
   return {dgates4, dh0, dc0};
@@ -1107,12 +1116,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("xp4"), py::arg("whh"), py::arg("h0"), py::arg("c0"), py::arg("err"), py::arg("ctl"),
         py::arg("want_f32_h"), py::arg("trace") = py::none(), py::arg("time_major") = false, py::arg("hs_out") = py::none(),
         py::arg("cs_out") = py::none(), py::arg("gates_out") = py::none(), py::arg("bias4") = py::none(),
-        py::arg("precise") = false);
+        py::arg("precise") = false, py::arg("reset") = py::none());
   m.def("lstm_team_bwd", &lstm_team_bwd, "XCD-team persistent LSTM backward (L2-local reduce-scatter)",
         py::arg("dhs"), py::arg("gates4"), py::arg("cs"), py::arg("c0"), py::arg("dhn"), py::arg("dcn"),
         py::arg("whh"), py::arg("err"), py::arg("ctl"), py::arg("trace") = py::none(),
         py::arg("time_major") = false, py::arg("dg_out") = py::none(), py::arg("dg_bf16") = false,
-        py::arg("want_dbias") = false, py::arg("precise") = false);
+        py::arg("want_dbias") = false, py::arg("precise") = false, py::arg("reset") = py::none());
   m.def("sample_actions", &sample_actions, "fused masked hierarchical Gumbel-max action sampling (actor)");
   m.def("actor_state_prep", &actor_state_prep, "actor step: state resets + [x | bf16(h)] gate-GEMM operand");
   m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)", py::arg("gates"),

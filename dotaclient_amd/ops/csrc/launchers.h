@@ -72,13 +72,14 @@ size_t dca_lstm_team_workspace(int B, int H, int backward, int f32);
 hipError_t dca_lstm_team_fwd(const float* xp4, const void* whh, const float* h0, const float* c0, short* hs,
                              float* hsf, float* cs, float* gates4, float* hn, float* cn, void* ctl, void* ws,
                              size_t ws_bytes, unsigned* err, int B, int S, int H, int time_major, hipStream_t st,
-                             unsigned long long* trace, const float* bias4, int f32, int precise = 0);
+                             unsigned long long* trace, const float* bias4, int f32, int precise = 0,
+                             const unsigned char* rst = nullptr);
 int dca_lstm_team_chains(int B, int f32);
 hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, const float* cs, const float* c0,
                              const float* dhn, const float* dcn, const void* whh, float* dgates4, float* dh0,
                              float* dc0, void* ctl, void* ws, size_t ws_bytes, unsigned* err, int B, int S, int H,
                              int time_major, hipStream_t st, unsigned long long* trace, short* dg16, float* dbpart,
-                             int f32, int precise = 0);
+                             int f32, int precise = 0, const unsigned char* rst = nullptr);
 
 hipError_t dca_sample_actions(const float* z, int ldz, const short* emb, const long long* handles, int N, int U,
                               unsigned long long seed, const long long* ctr, int* idx, unsigned char* act,

@@ -299,7 +299,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
     const float* __restrict__ c0, short* __restrict__ hs, float* __restrict__ hsf, float* __restrict__ cs,
     float* __restrict__ gates4, float* __restrict__ hn, float* __restrict__ cn, unsigned long long* xg_all,
     TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st, unsigned long long* trace,
-    int knobs, const float* __restrict__ bias4) {
+    int knobs, const float* __restrict__ bias4, const unsigned char* __restrict__ rst) {
   constexpr int H = 128 * KS;
   constexpr int U = H / kT;             // units per workgroup (4·KS)
   constexpr int NTILE = U / 4;          // 16-column MFMA tiles per workgroup (= KS)
@@ -413,6 +413,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
       // ---- prefetch this step's input projection (one 16-B vector per owned (row, unit)). Loading it one step
       // ahead instead measured slower (2.11 vs 1.94 µs per step at B=8, H=512).
       dca::f32x4 xv[MT];
+      bool rz[MT];                                    // sequence packing: an episode starts at step t (h, c := 0)
       if (mfma_wave) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
@@ -420,6 +421,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           const size_t tx = ((knobs >> 10) & 1) ? 0 : (size_t)t;   // knob: every step reads step 0 (L2-resident)
           xv[mt] = (b < B) ? *reinterpret_cast<const dca::f32x4*>(xp4 + (((size_t)(b0 + b) * sb + tx * st) * H + eunit) * 4)
                            : dca::f32x4{0.f, 0.f, 0.f, 0.f};
+          rz[mt] = rst != nullptr && b < B && rst[(size_t)(b0 + b) * sb + (size_t)t * st] != 0;
         }
       }
       // ---- gather h_{t-1} into hl[par]
@@ -559,11 +561,12 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           }
           }   // !V1
           const int b = mt * 16 + erow;
+          if (rz[mt]) { gq0 = 0.f; gq1 = 0.f; gq2 = 0.f; gq3 = 0.f; }   // episode start: no recurrent term
           // (bias added here, at the use: an add right after the prefetch would wait out the load before the gather)
           const float pi = gq0 + (xv[mt][0] + bv[0]), pf = gq1 + (xv[mt][1] + bv[1]), pg = gq2 + (xv[mt][2] + bv[2]),
                       po = gq3 + (xv[mt][3] + bv[3]);
           const float ig = sigm<PREC>(pi), fg = sigm<PREC>(pf), gg = tanh_<PREC>(pg), og = sigm<PREC>(po);
-          const float c = fg * creg[mt] + ig * gg;
+          const float c = fg * (rz[mt] ? 0.f : creg[mt]) + ig * gg;
           const float hv = og * tanh_<PREC>(c);
           if (merged ? 0 < B : b < B) { creg[mt] = c; hreg[mt] = hv; }
           TSTAMP(3);
@@ -641,7 +644,8 @@ __device__ __forceinline__ void lstm_team_bwd_body(
     const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
     const void* __restrict__ whh_, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
     i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
-    unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart, int knobs) {
+    unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart, int knobs,
+    const unsigned char* __restrict__ rst) {
   constexpr int H = 128 * KS;
   constexpr int U = H / kT;             // 4·KS units per workgroup (MFMA N, zero-padded to 16)
   constexpr int VV = VAR & 3;
@@ -749,10 +753,12 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       // ---- prefetch the saved activations of step t for the owned pairs
       dca::f32x4 gv[NPAIR];
       float cv[NPAIR], cpv[NPAIR], dv[NPAIR];
+      bool rcur[NPAIR], rnext[NPAIR];     // packing: episode starts at t (c_{t-1} unused) / at t+1 (h_t unused by t+1)
       if (t >= 0) {
 #pragma unroll
         for (int i = 0; i < NPAIR; ++i) {
           const int pi = tid + NT * i;
+          rcur[i] = rnext[i] = false;
           if (pi < B * U) {
             const int b = pi / U, u = pi % U;
             const size_t bt = (size_t)(b0 + b) * sb + (size_t)t * st;
@@ -760,6 +766,10 @@ __device__ __forceinline__ void lstm_team_bwd_body(
             cv[i] = cs[bt * H + j0 + u];
             cpv[i] = t > 0 ? cs[(bt - st) * H + j0 + u] : c0[(size_t)(b0 + b) * H + j0 + u];
             dv[i] = dhs[bt * H + j0 + u];
+            if (rst != nullptr) {
+              rcur[i] = rst[bt] != 0;
+              rnext[i] = t + 1 < S && rst[bt + st] != 0;
+            }
           }
         }
       }
@@ -868,7 +878,8 @@ __device__ __forceinline__ void lstm_team_bwd_body(
           float acc = 0.f;
 #pragma unroll
           for (int w = 0; w < NW; ++w) acc += red[w][b][u];
-          dh0[(size_t)(b0 + b) * H + j0 + u] = acc;
+          // an episode starting at step 0 never read h0
+          dh0[(size_t)(b0 + b) * H + j0 + u] = (rst != nullptr && rst[(size_t)(b0 + b) * sb] != 0) ? 0.f : acc;
         }
         break;
       }
@@ -883,7 +894,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
           float rec = 0.f;
           if (k == 0) {
             rec = dhn ? dhn[(size_t)(b0 + b) * H + j0 + u] : 0.f;
-          } else {
+          } else if (!rnext[i]) {
 #pragma unroll
             for (int w = 0; w < NW; ++w) rec += red[w][b][u];
           }
@@ -892,10 +903,10 @@ __device__ __forceinline__ void lstm_team_bwd_body(
           const float tc = tanh_<PREC>(cv[i]);
           const float dc = dcarry[i] + dht * og * (1.f - tc * tc);
           const float d_i = dc * gg * ig * (1.f - ig);
-          const float d_f = dc * cpv[i] * fg * (1.f - fg);
+          const float d_f = rcur[i] ? 0.f : dc * cpv[i] * fg * (1.f - fg);
           const float d_g = dc * ig * (1.f - gg * gg);
           const float d_o = dht * tc * og * (1.f - og);
-          dcarry[i] = dc * fg;
+          dcarry[i] = rcur[i] ? 0.f : dc * fg;
           const size_t bt = (size_t)(b0 + b) * sb + (size_t)t * st;
           if constexpr (F32) {
             const int o = (b * H + j0 + u) * 2 * 16;
@@ -945,10 +956,10 @@ __global__ __launch_bounds__((VAR & 3) == 2 ? 512 : kThreads, 1) void lstm_team_
     const float* __restrict__ c0, short* __restrict__ hs, float* __restrict__ hsf, float* __restrict__ cs,
     float* __restrict__ gates4, float* __restrict__ hn, float* __restrict__ cn, unsigned long long* xg_all,
     TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st, unsigned long long* trace,
-    int knobs, const float* __restrict__ bias4) {
+    int knobs, const float* __restrict__ bias4, const unsigned char* __restrict__ rst) {
   __builtin_amdgcn_s_setprio(3);   // issue priority over co-resident waves of kernels overlapped on other streams
   lstm_team_fwd_body<MT, KS, F32, VAR>(xp4, whh, h0, c0, hs, hsf, cs, gates4, hn, cn, xg_all, ctl, err, Btot, Bc, nch, S, sb,
-                             st, trace, knobs, bias4);
+                             st, trace, knobs, bias4, rst);
   team_exit(ctl, err, nch);
 }
 
@@ -958,10 +969,11 @@ __global__ __launch_bounds__((VAR & 3) == 2 ? 512 : kThreads, 1) void lstm_team_
     const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
     const void* __restrict__ whh, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
     i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
-    unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart, int knobs) {
+    unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart, int knobs,
+    const unsigned char* __restrict__ rst) {
   __builtin_amdgcn_s_setprio(3);
   lstm_team_bwd_body<MT, KS, F32, VAR>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, dh0, dc0, xg_all, ctl, err, Btot, Bc, nch,
-                             S, sb, st, trace, dg16, dbpart, knobs);
+                             S, sb, st, trace, dg16, dbpart, knobs, rst);
   team_exit(ctl, err, nch);
 }
 
@@ -1045,7 +1057,7 @@ extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const void* whh, const
                                         short* hs, float* hsf, float* cs, float* gates4, float* hn, float* cn,
                                         void* ctl_mem, void* ws, size_t ws_bytes, unsigned* err, int B, int S, int H,
                                         int time_major, hipStream_t stream, unsigned long long* trace,
-                                        const float* bias4, int f32, int precise) {
+                                        const float* bias4, int f32, int precise, const unsigned char* rst) {
   if (B < 1 || S < 1 || S >= 65535 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
   if (ws_bytes < dca_lstm_team_workspace(B, H, 0, f32) || ctl_mem == nullptr) return hipErrorInvalidValue;
   if (f32 && hsf == nullptr) return hipErrorInvalidValue;
@@ -1059,7 +1071,7 @@ extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const void* whh, const
 #define DCA_F(mt, ks, f, v)                                                                                     \
   (lstm_team_fwd_kernel<mt, ks, f, v><<<kMaxTeams * kT, team_threads(v), 0, stream>>>(xp4, whh, h0, c0, hs, hsf, cs, gates4, \
                                                                           hn, cn, xg, ctl, err, B, Bc, nch, S, sb, \
-                                                                          st, trace, team_knobs(), bias4),         \
+                                                                          st, trace, team_knobs(), bias4, rst),    \
    hipGetLastError())
   DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc, H, 0, precise), DCA_F)
 #undef DCA_F
@@ -1069,7 +1081,8 @@ extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, c
                                         const float* dhn, const float* dcn, const void* whh, float* dgates4,
                                         float* dh0, float* dc0, void* ctl_mem, void* ws, size_t ws_bytes,
                                         unsigned* err, int B, int S, int H, int time_major, hipStream_t stream,
-                                        unsigned long long* trace, short* dg16, float* dbpart, int f32, int precise) {
+                                        unsigned long long* trace, short* dg16, float* dbpart, int f32, int precise,
+                                        const unsigned char* rst) {
   if (B < 1 || S < 1 || S >= 65534 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
   if (dgates4 == nullptr && dg16 == nullptr) return hipErrorInvalidValue;
   if (f32 && dgates4 == nullptr) return hipErrorInvalidValue;
@@ -1084,7 +1097,7 @@ extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, c
   (lstm_team_bwd_kernel<mt, ks, f, v><<<kMaxTeams * kT, team_threads(v), 0, stream>>>(dhs, gates4, cs, c0, dhn, dcn, whh,      \
                                                                           dgates4, dh0, dc0, xb, ctl, err, B, Bc,  \
                                                                           nch, S, sb, st, trace, dg16, dbpart,      \
-                                                                          team_knobs()),                           \
+                                                                          team_knobs(), rst),                      \
    hipGetLastError())
   DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc, H, 1, precise), DCA_B)
 #undef DCA_B

@@ -45,17 +45,17 @@ PRESETS: Dict[str, RunPreset] = {p.name: p for p in [
               bench=dict(model='lstm128', batch_size=4, seq_len=256),
               launch=dict(model_preset='lstm128', actors=1, games_per_actor=1, actor_device='cpu', optimizers=1)),
     RunPreset('lstm512-1gpu', '1v1-mid LSTM-512 policy, batched actor inference + PPO on 1 MI355X', 1,
-              optimizer=dict(model_preset='lstm512', precision='fp32', **_DEPLOY),
+              optimizer=dict(model_preset='lstm512', precision='fp32-exact', **_DEPLOY),
               agent=dict(model_preset='lstm512', device='cuda', games=1024, runtime='vec', rollout_size=9999,
                          max_dota_time=600),
-              bench=dict(model='lstm512', batch_size=8, seq_len=1400, precision='fp32'),
+              bench=dict(model='lstm512', batch_size=8, seq_len=1400, precision='fp32-exact'),
               launch=dict(model_preset='lstm512', actors=1, games_per_actor=1024, actor_device='cuda',
                           optimizers=1)),
     RunPreset('lstm512-8gpu', '1v1-mid LSTM-512, 8xMI355X data-parallel optimizer with RCCL all-reduce over xGMI', 8,
-              optimizer=dict(model_preset='lstm512', precision='fp32', **_DEPLOY),
+              optimizer=dict(model_preset='lstm512', precision='fp32-exact', **_DEPLOY),
               agent=dict(model_preset='lstm512', device='cuda', games=1024, runtime='vec', rollout_size=9999,
                          max_dota_time=600),
-              bench=dict(model='lstm512', batch_size=8, seq_len=1400, precision='fp32'),
+              bench=dict(model='lstm512', batch_size=8, seq_len=1400, precision='fp32-exact'),
               launch=dict(model_preset='lstm512', actors=8, games_per_actor=1024, actor_device='cuda',
                           optimizers=8)),
     RunPreset('5v5-8gpu', '5v5 entity-attention policy (per-unit embed + max-pool), 8xMI355X DP', 8,
@@ -65,10 +65,10 @@ PRESETS: Dict[str, RunPreset] = {p.name: p for p in [
               bench=dict(model='5v5', batch_size=8, seq_len=1400, precision='fp32'),
               launch=dict(model_preset='5v5', actors=8, games_per_actor=256, actor_device='cuda', optimizers=8)),
     RunPreset('league-replay', 'Self-play league (PFSP opponents) + 200 GB on-HBM replay buffer', 1,
-              optimizer=dict(model_preset='lstm512', precision='fp32', replay_gb=200.0, **_DEPLOY),
+              optimizer=dict(model_preset='lstm512', precision='fp32-exact', replay_gb=200.0, **_DEPLOY),
               agent=dict(model_preset='lstm512', device='cuda', games=1024, runtime='vec', rollout_size=9999,
                          max_dota_time=600, league='pfsp', use_latest_weights_prob=0.8, actor_precision='fp8'),
-              bench=dict(model='lstm512', batch_size=8, seq_len=1400, precision='fp32', replay=16384),
+              bench=dict(model='lstm512', batch_size=8, seq_len=1400, precision='fp32-exact', replay=16384),
               launch=dict(model_preset='lstm512', actors=1, games_per_actor=1024, actor_device='cuda',
                           optimizers=1)),
 ]}

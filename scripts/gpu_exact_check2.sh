@@ -6,3 +6,4 @@ DCA_EXACT_ACT=fast timeout -k 10 300 python -u -m pytest -x -s --timeout 300 --t
 DCA_EXACT_ACT=libm timeout -k 10 300 python -u -m pytest -x -s --timeout 300 --timeout-method thread tests/test_exact_mode.py -k deploy > gpurun_out/exact_libm_act.log 2>&1 ; \
 DCA_EXACT_ACT=fast timeout -k 10 300 python -u bench.py --precision fp32-exact --steps 20 --warmup 5 --actor 0 --e2e 0 --bf16x3-extra 0 --model-5v5-extra 0 > gpurun_out/exact_fast_bench.log 2>&1
 timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_fused_policy.py tests/test_learner_async.py tests/test_optim.py -m gpu > gpurun_out/fused_tests.log 2>&1
+timeout -k 10 300 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_packing.py tests/test_lstm_kernel.py -m gpu > gpurun_out/packing_tests.log 2>&1

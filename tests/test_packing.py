@@ -1,0 +1,145 @@
+"""Sequence packing (learner/ingest.py SequencePacker, ``OptimizerConfig.pack_sequences``): several episodes per
+``seq_len`` sequence with episode-start reset flags instead of padding every rollout (the reference pads,
+/root/reference/optimizer.py:355-378).
+
+* the packer's placement: first fit into free tails, long / stored-state rollouts aligned, reset rows, h0 sources;
+* the CPU oracle (torch LSTM with resets, models/policy.py) — a packed sequence [A | B] gives the same PPO loss and
+  parameter gradients as the padded sequences [A], [B];
+* GPU: the fused learner step with the team recurrence's reset flags (ops/csrc/lstm_team.hip) against the same
+  padded evaluation, fp32 (bf16x3) and IEEE fp32."""
+import copy
+
+import numpy as np
+import pytest
+import torch
+
+from dotaclient_amd.learner.engine import Learner, LossConfig
+from dotaclient_amd.learner.ingest import IngestPipeline, SequencePacker
+from dotaclient_amd.learner.synthetic import make_batch
+from dotaclient_amd.models.policy import Policy, get_config
+from dotaclient_amd.transport.codec import Rollout
+
+
+def _rollout(T, seed, hidden=None, stride=0):
+    rng = np.random.default_rng(seed)
+    U = 40
+    A = 21 + U
+    act = np.zeros((T, A), np.uint8)
+    act[np.arange(T), rng.integers(0, 3, T)] = 1
+    return Rollout(game_id=f'g{seed}', team_id=2, player_id=0, env=rng.standard_normal((T, 3)).astype(np.float32),
+                   units=rng.standard_normal((T, U, 10)).astype(np.float32), actions=act, masks=act.copy(),
+                   rewards=rng.standard_normal((T, 9)), weight_version=0, logp=np.zeros(T, np.float32),
+                   values=np.zeros(T, np.float32), hiddens=hidden, hidden_stride=stride)
+
+
+def test_packer_first_fit_and_resets():
+    S = 10
+    pk = SequencePacker(S)
+    starts = [pk.add(_rollout(T, i)) for i, T in enumerate([4, 3, 12, 2, 9, 5])]
+    # 4 → seq 0 [0,4); 3 → seq 0 [4,7) reset; 12 → seqs 1-2 aligned, tail 2 in seq 2; 2 → seq 0 [7,9) reset;
+    # 9 → new seq 3; 5 → seq 2 tail [22, 27) reset
+    assert starts == [0, 4, 10, 7, 30, 22]
+    assert pk.n_seq == 4
+    assert sorted(pk.resets) == [4, 7, 22]
+    assert pk.seq_src == [(0, 0), (2, 0), (2, 1), (4, 0)]
+    # a rollout that starts from a stored non-zero state is never placed mid-sequence
+    h = np.ones((1, 2, 8), np.float32)
+    r = _rollout(1, 9, hidden=h, stride=S)
+    assert not pk.fits(r) and pk.add(r) == 40 and pk.n_seq == 5
+    # padding mode: the reference layout (every rollout at a sequence start)
+    pp = SequencePacker(S, pack=False)
+    assert [pp.add(_rollout(T, i)) for i, T in enumerate([4, 3, 12])] == [0, 10, 20] and pp.resets == []
+
+
+def test_ingest_stage_packs_rows_in_row_order():
+    S = 16
+    pl = IngestPipeline(None, S, 2, 'ppo', 8, 'cpu', pack=True)
+    rs = [_rollout(5, 1), _rollout(20, 2), _rollout(7, 3)]
+    st = pl.stage(rs)
+    # 5 → [0,5); 20 → [16,36) (seqs 1-2, tail 4 rows); 7 → seq 0 [5,12) reset
+    assert st.n_seq == 3 and st.L == 48 and st.Lv == 32
+    assert list(st.off) == [0, 5, 16, 48] and st.lens == [5, 7, 20]
+    x = pl.expand(st, {})
+    rst = x['reset'].numpy()
+    assert rst.sum() == 1 and rst[5] == 1
+    v = x['valid'].numpy()
+    assert v[:12].all() and not v[12:16].any() and v[16:36].all() and not v[36:].any()
+    np.testing.assert_array_equal(x['env'][5:12].numpy(), rs[2].env)
+
+
+def _ppo_grads(pol, batch):
+    lrn = Learner(pol, LossConfig(algo='ppo', vf_coef=0.5, entropy_coef=0.01), device='cpu', backend='torch', dp=False)
+    pol.zero_grad()
+    loss, _ = lrn.loss(batch)
+    loss.backward()
+    return float(loss.detach()), {n: p.grad.clone() for n, p in pol.named_parameters() if p.grad is not None}
+
+
+def _packed_and_padded(cfg, S, la, lb, device='cpu', seed=3):
+    """Padded: two sequences [A | pad], [B | pad]; packed: one sequence [A | B | pad] with a reset at |A|."""
+    src = make_batch(2, S, cfg.layout, cfg.hidden, device='cpu', seed=seed, pad_frac=0.0)
+    pad = {k: v.clone() for k, v in src.items()}
+    for k, v in pad.items():
+        if v.dim() >= 2 and v.shape[1] == S:
+            v[0, la:] = 0
+            v[1, lb:] = 0
+    pad['h0'].zero_()
+    pad['c0'].zero_()
+    packed = {}
+    for k, v in pad.items():
+        if v.dim() >= 2 and v.shape[1] == S:
+            p = torch.zeros_like(v[:1])
+            p[0, :la] = v[0, :la]
+            p[0, la:la + lb] = v[1, :lb]
+            packed[k] = p
+        else:
+            packed[k] = v[:1].clone()
+    rst = torch.zeros(1, S, dtype=torch.uint8)
+    rst[0, la] = 1
+    packed['reset'] = rst
+    mv = lambda d: {k: v.to(device) for k, v in d.items()}     # noqa: E731
+    return mv(pad), mv(packed)
+
+
+def test_packed_sequence_matches_padded_sequences_cpu():
+    torch.manual_seed(0)
+    cfg = get_config('lstm128')
+    pol = Policy(cfg)
+    pad, packed = _packed_and_padded(cfg, 24, 9, 11)
+    l_pad, g_pad = _ppo_grads(copy.deepcopy(pol), pad)
+    l_pack, g_pack = _ppo_grads(copy.deepcopy(pol), packed)
+    assert abs(l_pad - l_pack) < 1e-5, (l_pad, l_pack)
+    assert set(g_pad) == set(g_pack)
+    for n in g_pad:
+        torch.testing.assert_close(g_pack[n], g_pad[n], rtol=1e-4, atol=1e-6, msg=n)
+    # without the reset the packed sequence would carry A's state into B: the loss differs
+    no_reset = dict(packed, reset=torch.zeros_like(packed['reset']))
+    assert abs(_ppo_grads(copy.deepcopy(pol), no_reset)[0] - l_pack) > 1e-7
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('precision', ['fp32', 'fp32-exact'])
+def test_fused_packed_sequence_matches_padded_on_gpu(gpu_ops, precision):
+    """The fused step (team recurrence with reset flags, masked h_{t-1} operand of ∂W_hh) on [A | B] against the
+    padded [A], [B] — loss and every parameter gradient."""
+    torch.manual_seed(0)
+    cfg = get_config('lstm512')
+    pol = Policy(cfg)
+    S = 64
+    pad, packed = _packed_and_padded(cfg, S, 23, 37, device='cuda')
+
+    def run(batch):
+        p = copy.deepcopy(pol)
+        lrn = Learner(p, LossConfig(algo='ppo', vf_coef=0.5, entropy_coef=0.01), device='cuda', backend='fused',
+                      dp=False, precision=precision)
+        lrn.dp.zero_grad()
+        loss, _ = lrn.loss(batch)
+        loss.backward()
+        torch.cuda.synchronize()
+        return float(loss), {n: q.grad.detach().clone() for n, q in p.named_parameters() if q.grad is not None}
+    l_pad, g_pad = run(pad)
+    l_pack, g_pack = run(packed)
+    assert abs(l_pad - l_pack) <= 1e-5 * max(1.0, abs(l_pad)), (l_pad, l_pack)
+    for n, g in g_pad.items():
+        rel = ((g_pack[n] - g).norm() / g.norm().clamp_min(1e-12)).item()
+        assert rel < (1e-5 if precision == 'fp32-exact' else 1e-3), (n, rel)

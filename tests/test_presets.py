@@ -42,4 +42,4 @@ def test_bench_parser_accepts_presets(monkeypatch):
     assert (a.model, a.batch_size, a.seq_len) == ('lstm128', 4, 256)
     monkeypatch.setattr(sys, 'argv', ['bench.py', '--preset', 'lstm512-8gpu', '--steps', '3'])
     a = bench.parse()
-    assert (a.model, a.batch_size, a.seq_len, a.steps, a.precision) == ('lstm512', 8, 1400, 3, 'fp32')
+    assert (a.model, a.batch_size, a.seq_len, a.steps, a.precision) == ('lstm512', 8, 1400, 3, 'fp32-exact')
