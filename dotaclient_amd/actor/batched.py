@@ -31,6 +31,32 @@ from ..models.policy import TYPE_SUFFIX, Policy
 LDZ = 160
 
 
+class _Pack:
+    """Named regions of ONE pinned host buffer and ONE device buffer with the same byte layout (256-B aligned
+    regions in declaration order), so any contiguous run of regions moves in a single copy."""
+
+    def __init__(self, fields, device):
+        self.off, self.size, off = {}, {}, 0
+        for name, shape, dt in fields:
+            nb = int(np.prod(shape)) * torch.empty((), dtype=dt).element_size()
+            self.off[name], self.size[name] = off, nb
+            off = (off + nb + 255) // 256 * 256
+        self.host_bytes = torch.zeros(off, dtype=torch.uint8, pin_memory=True)
+        self.dev_bytes = torch.zeros(off, dtype=torch.uint8, device=device)
+        self.host, self.dev = {}, {}
+        for name, shape, dt in fields:
+            o, nb = self.off[name], self.size[name]
+            self.host[name] = self.host_bytes[o:o + nb].view(dt).view(shape)
+            self.dev[name] = self.dev_bytes[o:o + nb].view(dt).view(shape)
+
+    def copy_range(self, first: str, last: str, to_host: bool = False):
+        a, b = self.off[first], self.off[last] + self.size[last]
+        if to_host:
+            self.host_bytes[a:b].copy_(self.dev_bytes[a:b], non_blocking=True)
+        else:
+            self.dev_bytes[a:b].copy_(self.host_bytes[a:b], non_blocking=True)
+
+
 class GpuActorPolicy:
     """Fixed-slot batched policy step on one GPU: LSTM / linear-RNN policies, 1v1 or 5v5 (entity attention)."""
 
@@ -59,42 +85,55 @@ class GpuActorPolicy:
         self.graph: Optional[torch.cuda.CUDAGraph] = None
 
     # ------------------------------------------------------------------------------------------------
+    # staged input dtypes (Fp8ActorPolicy stages compact fp16 features / int32 handles)
+    UNITS_DTYPE, HANDLES_DTYPE = torch.float32, torch.long
+
     def _alloc(self, inputs_from=None):
         n, U, A, dev = self.n, self.U, self.A, self.device
         H = self.cfg.hidden
         pin = dict(pin_memory=True)
+        ud, hd = self.UNITS_DTYPE, self.HANDLES_DTYPE
+        # ONE packed pinned staging buffer and ONE device mirror per direction: a step's inputs cross PCIe in one copy
+        # and its outputs come back in one (each separate copy was a DMA dispatch of its own inside the graph)
+        self.in_pack = _Pack([('env', (n, 3), torch.float32), ('units', (n, U, 10), ud), ('handles', (n, U), hd),
+                              ('keep', (n, 1), torch.float32), ('active', (n,), torch.float32)], dev)
         if inputs_from is not None:
             # a second policy over the same observations (league opponents): share the staged inputs; keep/active
-            # stay per policy
+            # stay per policy (its own pack's env / units / handles regions are unused)
             if (inputs_from.n, inputs_from.U) != (n, U):
                 raise ValueError('inputs_from: slot count / layout mismatch')
             self.h_env, self.h_units, self.h_handles = inputs_from.h_env, inputs_from.h_units, inputs_from.h_handles
         else:
-            self.h_env = torch.zeros(n, 3, **pin)
-            self.h_units = torch.zeros(n, U, 10, **pin)
-            self.h_handles = torch.full((n, U), -1, dtype=torch.long, **pin)
-        self.h_keep = torch.ones(n, 1, **pin)
-        self.h_active = torch.ones(n, **pin)
-        self.d_env = torch.zeros(n, 3, device=dev)
-        self.d_units = torch.zeros(n, U, 10, device=dev)
-        self.d_handles = torch.full((n, U), -1, dtype=torch.long, device=dev)
-        self.d_keep = torch.ones(n, 1, device=dev)
-        self.d_active = torch.ones(n, device=dev)     # 0 → slot not stepped: LSTM state left untouched
+            self.h_env, self.h_units, self.h_handles = (self.in_pack.host[k] for k in ('env', 'units', 'handles'))
+            self.h_handles.fill_(-1)
+        self._shared_inputs = inputs_from is not None
+        self.h_keep, self.h_active = self.in_pack.host['keep'], self.in_pack.host['active']
+        self.h_keep.fill_(1.0)
+        self.h_active.fill_(1.0)
+        self.d_env = self.in_pack.dev['env']
+        self.d_keep = self.in_pack.dev['keep']
+        self.d_active = self.in_pack.dev['active']     # 0 → slot not stepped: LSTM state left untouched
+        if ud == torch.float32:
+            self.d_units = self.in_pack.dev['units']
+        else:
+            self.d_units = torch.zeros(n, U, 10, device=dev)
+        if hd == torch.long:
+            self.d_handles = self.in_pack.dev['handles']
+        else:
+            self.d_handles = torch.full((n, U), -1, dtype=torch.long, device=dev)
         self.h = torch.zeros(n, H, device=dev)
         self.c = torch.zeros(n, H, device=dev)
         self.h16 = torch.zeros(n, H, dtype=torch.bfloat16, device=dev)
         self.xh = torch.zeros(n, self.cfg.pre_rnn_dim + H, dtype=torch.bfloat16, device=dev)   # [x | bf16(h)]
         self.ctr = torch.zeros(1, dtype=torch.long, device=dev)
-        self.idx = torch.zeros(n, 4, dtype=torch.int32, device=dev)
-        self.act = torch.zeros(n, A, dtype=torch.uint8, device=dev)
-        self.msk = torch.zeros(n, A, dtype=torch.uint8, device=dev)
-        self.logp = torch.zeros(n, device=dev)
-        self.value = torch.zeros(n, device=dev)
-        self.o_idx = torch.zeros(n, 4, dtype=torch.int32, **pin)
-        self.o_logp = torch.zeros(n, **pin)
-        self.o_value = torch.zeros(n, **pin)
-        self.o_act = torch.zeros(n, A, dtype=torch.uint8, **pin)
-        self.o_msk = torch.zeros(n, A, dtype=torch.uint8, **pin)
+        # outputs: [idx | logp | value] first (the part every step returns), then [act | msk] (recorded steps)
+        self.out_pack = _Pack([('idx', (n, 4), torch.int32), ('logp', (n,), torch.float32),
+                               ('value', (n,), torch.float32), ('act', (n, A), torch.uint8),
+                               ('msk', (n, A), torch.uint8)], dev)
+        d, o = self.out_pack.dev, self.out_pack.host
+        self.idx, self.logp, self.value, self.act, self.msk = d['idx'], d['logp'], d['value'], d['act'], d['msk']
+        self.o_idx, self.o_logp, self.o_value, self.o_act, self.o_msk = (o['idx'], o['logp'], o['value'], o['act'],
+                                                                         o['msk'])
         # LSTM state snapshots (h, c before the step, after resets) of selected rows — trajectory hidden states
         self.h_rows = torch.zeros(n, dtype=torch.long, **pin)
         self.d_rows = torch.zeros(n, dtype=torch.long, device=dev)
@@ -197,19 +236,22 @@ class GpuActorPolicy:
         self.ctr.add_(1)
 
     def _h2d(self):
-        self.d_env.copy_(self.h_env, non_blocking=True)
-        self.d_units.copy_(self.h_units, non_blocking=True)
-        self.d_handles.copy_(self.h_handles, non_blocking=True)
-        self.d_keep.copy_(self.h_keep, non_blocking=True)
-        self.d_active.copy_(self.h_active, non_blocking=True)
+        if self._shared_inputs:
+            # observations staged by the policy this one shares them with: its pinned views, our device regions
+            ip = self.in_pack.dev
+            ip['env'].copy_(self.h_env, non_blocking=True)
+            ip['units'].copy_(self.h_units, non_blocking=True)
+            ip['handles'].copy_(self.h_handles, non_blocking=True)
+            self.in_pack.copy_range('keep', 'active')
+        else:
+            self.in_pack.copy_range('env', 'active')          # one H2D copy of the whole staged step
+        self._widen()
+
+    def _widen(self):
+        """Compact staging (fp16 features / int32 handles): widen into the encoder's / sampler's operands."""
 
     def _d2h(self):
-        self.o_idx.copy_(self.idx, non_blocking=True)
-        self.o_logp.copy_(self.logp, non_blocking=True)
-        self.o_value.copy_(self.value, non_blocking=True)
-        if self.record:
-            self.o_act.copy_(self.act, non_blocking=True)
-            self.o_msk.copy_(self.msk, non_blocking=True)
+        self.out_pack.copy_range('idx', 'msk' if self.record else 'value', to_host=True)
 
     def capture(self):
         """Warm up (hipBLASLt heuristics, allocator) on a side stream and capture the WHOLE step — input copies from
@@ -305,15 +347,15 @@ class GpuActorPolicy:
 def fp8_weight(w: torch.Tensor):
     """(N, K) fp32 weight → (e4m3fn bytes in MFMA fragment order, (N,) fp32 per-channel dequant scales) for
     ops/csrc/actor_fp8.hip: each output channel's max |w| maps to 448 (the largest finite e4m3fn); byte order
-    [N/16 column tile][K/64 k-step pair][lane = 16·(k%32 // 8) + n%16][k-step of the pair][k % 8] — one tile's two
-    k-steps are one coalesced 1 KB load of a wave."""
+    [N/16 column tile][K/128 k-step][lane = 16·(k%128 // 32) + n%16][k % 32] — the 32-byte operand of a lane of the
+    16x16x128 f8f6f4 MFMA; one tile's k-step is one coalesced 2 KB load of a wave."""
     N, K = w.shape
-    if N % 16 or K % 64:
-        raise ValueError(f'fp8_weight: ({N}, {K}) must be multiples of (16, 64)')
+    if N % 16 or K % 128:
+        raise ValueError(f'fp8_weight: ({N}, {K}) must be multiples of (16, 128)')
     amax = w.abs().amax(1)
     s = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
     q = (w / s[:, None]).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).view(torch.uint8)
-    frag = q.view(N // 16, 16, K // 64, 2, 4, 8).permute(0, 2, 4, 1, 3, 5).contiguous()
+    frag = q.view(N // 16, 16, K // 128, 4, 32).permute(0, 2, 3, 1, 4).contiguous()
     return frag.view(-1), s.float().contiguous()
 
 
@@ -337,20 +379,12 @@ class Fp8ActorPolicy(GpuActorPolicy):
         super().__init__(policy, n_slots, device=device, **kw)
 
     def _alloc(self, inputs_from=None):
+        if self.compact:
+            self.UNITS_DTYPE, self.HANDLES_DTYPE = torch.float16, torch.int32
         super()._alloc(inputs_from)
-        n, U, dev = self.n, self.U, self.device
-        self.z = torch.zeros(n, LDZ, device=dev)
-        if not self.compact:
-            if inputs_from is not None and inputs_from.h_units.dtype != torch.float32:
-                raise ValueError('Fp8ActorPolicy(compact=False): inputs_from must stage fp32 features')
-            return
-        if inputs_from is None:
-            self.h_units = torch.zeros(n, U, 10, dtype=torch.float16, pin_memory=True)
-            self.h_handles = torch.full((n, U), -1, dtype=torch.int32, pin_memory=True)
-        elif self.h_units.dtype != torch.float16:
-            raise ValueError('Fp8ActorPolicy: inputs_from must be another Fp8ActorPolicy (compact staging)')
-        self.d_units16 = torch.zeros(n, U, 10, dtype=torch.float16, device=dev)
-        self.d_handles32 = torch.full((n, U), -1, dtype=torch.int32, device=dev)
+        self.z = torch.zeros(self.n, LDZ, device=self.device)
+        if inputs_from is not None and inputs_from.h_units.dtype != self.UNITS_DTYPE:
+            raise ValueError('Fp8ActorPolicy: inputs_from must stage the same feature dtype')
 
     def _weight_dict(self, sd):
         w = super()._weight_dict(sd)
@@ -368,16 +402,9 @@ class Fp8ActorPolicy(GpuActorPolicy):
             w.pop(k, None)
         return w
 
-    def _h2d(self):
-        if not self.compact:
-            return super()._h2d()
-        self.d_env.copy_(self.h_env, non_blocking=True)
-        self.d_units16.copy_(self.h_units, non_blocking=True)
-        self.d_handles32.copy_(self.h_handles, non_blocking=True)
-        self.d_keep.copy_(self.h_keep, non_blocking=True)
-        self.d_active.copy_(self.h_active, non_blocking=True)
-        self.d_units.copy_(self.d_units16)          # widen on the GPU (one elementwise pass each)
-        self.d_handles.copy_(self.d_handles32)
+    def _widen(self):
+        if self.compact:   # fp16 features → fp32, int32 handles → int64 in ONE hand-written launch (ops/csrc/actor.hip)
+            self.C.actor_widen(self.in_pack.dev['units'], self.d_units, self.in_pack.dev['handles'], self.d_handles)
 
     def _forward(self):
         """Captured body, 4 launches: encoder → fp8 core (pre-RNN, gates + cell, heads) → sampling → RNG counter."""

@@ -11,6 +11,7 @@
 //   * hierarchical selection, joint log-prob of the sampled action, one-hot actions and selected-heads masks
 //     (the experience record), and V(s).
 #include "common.h"
+#include <hip/hip_fp16.h>
 
 namespace {
 
@@ -175,7 +176,32 @@ __global__ __launch_bounds__(256) void actor_state_prep_kernel(const short* __re
   }
 }
 
+// Compact actor staging widened in one launch: fp16 unit features → fp32 (n4 groups of 4) and int32 unit handles →
+// int64 (m of them); the encoder and the sampling kernel then read their usual operands.
+__global__ __launch_bounds__(256) void actor_widen_kernel(const uint2* __restrict__ u16, float4* __restrict__ u32, int n4,
+                                                          const int* __restrict__ h32, long long* __restrict__ h64,
+                                                          int m) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n4) {
+    const uint2 v = u16[i];
+    const __half2 a = __builtin_bit_cast(__half2, v.x), b = __builtin_bit_cast(__half2, v.y);
+    u32[i] = make_float4(__low2float(a), __high2float(a), __low2float(b), __high2float(b));
+  }
+  if (i < m) h64[i] = h32[i];
+}
+
 }  // namespace
+
+extern "C" hipError_t dca_actor_widen(const void* u16, float* u32, long long n_units, const int* h32, long long* h64,
+                                      long long n_handles, hipStream_t st) {
+  if (n_units % 4) return hipErrorInvalidValue;
+  const long long n4 = n_units / 4, work = n4 > n_handles ? n4 : n_handles;
+  if (work == 0) return hipSuccess;
+  actor_widen_kernel<<<(unsigned)((work + 255) / 256), 256, 0, st>>>(reinterpret_cast<const uint2*>(u16),
+                                                                      reinterpret_cast<float4*>(u32), (int)n4, h32, h64,
+                                                                      (int)n_handles);
+  return hipGetLastError();
+}
 
 extern "C" hipError_t dca_actor_state_prep(const short* pre, float* h, float* c, const float* keep, short* xh, int N,
                                            int P, int H, hipStream_t st) {

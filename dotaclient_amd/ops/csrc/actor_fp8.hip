@@ -9,12 +9,13 @@
 //
 // Quantisation. Weights: per output channel, scaled at hot-swap time (actor/batched.py Fp8ActorPolicy) so the
 // channel's max |w| maps to 448, converted by torch to float8_e4m3fn and laid out in MFMA FRAGMENT ORDER
-// [col tile][k-step pair][lane][16 B]: a wave reads one tile's two k-steps as one coalesced 1 KB load and the
+// [col tile][128-deep k-step][lane][32 B]: a wave reads one tile's k-step as one coalesced 2 KB load and the
 // weights stream from L2 straight into registers (no LDS staging, no reuse inside a workgroup to stage for).
 // Activations: per row, inside the kernel — the row's max |v| over the GEMM's whole K maps to 448 (x896 for the
 // pre-RNN layer; [pre | h] jointly for the gates, fp8 keeps 3 mantissa bits at every exponent so the smaller h
 // values do not need a scale of their own; h for the heads), converted by v_cvt_pk_fp8_f32 (RNE) into an LDS A
-// image. Products run on v_mfma_f32_16x16x32_fp8_fp8 (fp32 accumulation); the epilogue applies
+// image. Products run on v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 operands, unit block scales, fp32 accumulation;
+// twice the rate of the 16x16x32 fp8 form); the epilogue applies
 // scale_row · scale_col + bias. The cell's four gates of a (row, unit) sit in four adjacent lanes of the C layout
 // (unit-major columns); a quad transpose by DPP broadcasts hands each lane one (row, unit).
 //
@@ -34,7 +35,7 @@ constexpr int XD = 896, PD = 256, HD = 512, GD = 4 * HD, KG = PD + HD, ZD = 160;
 constexpr int LDX = XD + 16, LDG = KG + 16, LDF = PD + 4, LDH = HD + 4;   // LDS row pitches (bytes / floats)
 constexpr float kQmax = 448.f;                                          // largest finite e4m3fn
 
-// 8 fp32 → 8 e4m3fn bytes (round to nearest even), element j in byte j: one 16x16x32 fp8 MFMA operand
+// 8 fp32 → 8 e4m3fn bytes (round to nearest even), element j in byte j
 __device__ __forceinline__ long long pack8(const float* v) {
   int lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[0], v[1], 0, false);
   lo = __builtin_amdgcn_cvt_pk_fp8_f32(v[2], v[3], lo, true);
@@ -43,55 +44,60 @@ __device__ __forceinline__ long long pack8(const float* v) {
   return (long long)(unsigned)lo | ((long long)(unsigned)hi << 32);
 }
 
-__device__ __forceinline__ f32x4 mma8(long long a, long long b, f32x4 c) {
-  return __builtin_amdgcn_mfma_f32_16x16x32_fp8_fp8(a, b, c, 0, 0, 0);
+typedef int i32x8 __attribute__((ext_vector_type(8)));
+
+// One K = 128 step on gfx950's block-scaled f8f6f4 MFMA with e4m3 A and B (format 0) and unit block scales
+// (E8M0 127 = 2^0): twice the cycles of the 16x16x32 fp8 form for 4x the K, i.e. twice its rate — the per-row /
+// per-channel dequantisation stays in the epilogue. Lane l's 32 operand bytes are k = 128u + 32(l>>4) + j (A rows /
+// B columns l & 15); A and B use the same lane → k map, so the product is the sum over k whatever order the
+// hardware takes the 32 bytes in.
+__device__ __forceinline__ f32x4 mma128(const i32x8& a, const i32x8& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, c, 0, 0, 0, 127, 0, 127);
 }
 
-// A fragment of k-step s from a row-major fp8 LDS image: lane l holds A[row l&15][k = 32s + 8(l>>4) + j]
-__device__ __forceinline__ long long afrag(const unsigned char* img, int ld, int s, int lane) {
-  return *reinterpret_cast<const long long*>(img + (lane & 15) * ld + 32 * s + 8 * (lane >> 4));
+// A fragment of k-step u (128 deep) from a row-major fp8 LDS image: lane l holds A[row l&15][128u + 32(l>>4) + j]
+__device__ __forceinline__ i32x8 afrag128(const unsigned char* img, int ld, int u, int lane) {
+  const uint4* p = reinterpret_cast<const uint4*>(img + (lane & 15) * ld + 128 * u + 32 * (lane >> 4));
+  const uint4 x = p[0], y = p[1];
+  return i32x8{(int)x.x, (int)x.y, (int)x.z, (int)x.w, (int)y.x, (int)y.y, (int)y.z, (int)y.w};
 }
 
-// one fragment-ordered weight pair (k-steps 2p, 2p+1) of column tile `tile`: 16 B per lane
-__device__ __forceinline__ uint4 bpair(const uint4* __restrict__ w, int ksteps, int tile, int p, int lane) {
-  return w[((size_t)tile * (ksteps / 2) + p) * 64 + lane];
+// one fragment-ordered weight k-step (128 deep) of column tile `tile`: 32 B per lane, a wave's load is 2 KB contiguous
+__device__ __forceinline__ i32x8 wfrag128(const i32x8* __restrict__ w, int ku, int tile, int u, int lane) {
+  return w[((size_t)tile * ku + u) * 64 + lane];
 }
-__device__ __forceinline__ long long lo64(uint4 v) { return (long long)v.x | ((long long)v.y << 32); }
-__device__ __forceinline__ long long hi64(uint4 v) { return (long long)v.z | ((long long)v.w << 32); }
 
-// Streamed weight GEMM: NCH chunks of NTL column tiles (tile of chunk ch, slot i = tile0 + NTL·ch + i, or tile0 +
-// i + 4·ch... via `tile(ch, i)`), each over K = 64·KP (KP k-step pairs). The (chunk, pair) sequence is ONE stream
-// with a D-deep register ring of weight pairs, so the loads of the next chunk are in flight during the epilogue of
-// the current one; the epilogue `epi(ch, acc)` runs after a chunk's last pair (it must not touch global memory:
-// every vector memory op counts in the same in-order vmcnt as the ring's loads).
-template <int NTL, int KP, int NCH, int D, class TileFn, class Epi>
-__device__ __forceinline__ void stream_gemm(const unsigned char* aimg, int lda, const uint4* __restrict__ w,
+// Streamed weight GEMM: NCH chunks of NTL column tiles (`tile(ch, i)`), each over K = 128·KU. The (chunk, k-step)
+// sequence is ONE stream with a D-deep register ring of weight fragments, so the loads of the next chunk are in
+// flight during the epilogue of the current one; the epilogue `epi(ch, acc)` runs after a chunk's last k-step (it
+// must not touch global memory: every vector memory op counts in the same in-order vmcnt as the ring's loads).
+template <int NTL, int KU, int NCH, int D, class TileFn, class Epi>
+__device__ __forceinline__ void stream_gemm(const unsigned char* aimg, int lda, const i32x8* __restrict__ w,
                                             TileFn tile, int lane, Epi epi) {
-  static_assert((NCH * KP) % D == 0, "stream length must be a multiple of the ring depth");
-  constexpr int T = NCH * KP;
-  uint4 ring[D][NTL];
+  constexpr int T = NCH * KU;
+  i32x8 ring[D][NTL];
   f32x4 acc[NTL];
 #pragma unroll
   for (int i = 0; i < NTL; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto issue = [&](int slot, int t) {
-    t = t < T ? t : T - 1;                         // past the end: reload the last pair (never consumed)
-    const int ch = t / KP, p = t - ch * KP;
+    t = t < T ? t : T - 1;                         // past the end: reload the last step (never consumed)
+    const int ch = t / KU, u = t - ch * KU;
 #pragma unroll
-    for (int i = 0; i < NTL; ++i) ring[slot][i] = bpair(w, 2 * KP, tile(ch, i), p, lane);
+    for (int i = 0; i < NTL; ++i) ring[slot][i] = wfrag128(w, KU, tile(ch, i), u, lane);
   };
 #pragma unroll
   for (int d = 0; d < D; ++d) issue(d, d);
   for (int t0 = 0; t0 < T; t0 += D) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      const int t = t0 + d, ch = t / KP, p = t - ch * KP;
-      const long long a0 = afrag(aimg, lda, 2 * p, lane), a1 = afrag(aimg, lda, 2 * p + 1, lane);
+      const int t = t0 + d;
+      if (t >= T) break;                           // (T need not be a multiple of D; wave-uniform)
+      const int ch = t / KU, u = t - ch * KU;
+      const i32x8 a = afrag128(aimg, lda, u, lane);
 #pragma unroll
-      for (int i = 0; i < NTL; ++i) acc[i] = mma8(a0, lo64(ring[d][i]), acc[i]);
-#pragma unroll
-      for (int i = 0; i < NTL; ++i) acc[i] = mma8(a1, hi64(ring[d][i]), acc[i]);
+      for (int i = 0; i < NTL; ++i) acc[i] = mma128(a, ring[d][i], acc[i]);
       issue(d, t + D);
-      if (p == KP - 1) {
+      if (u == KU - 1) {
         epi(ch, acc);
 #pragma unroll
         for (int i = 0; i < NTL; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -111,9 +117,9 @@ __device__ __forceinline__ float dpp_quad_bcast(float v, int k) {   // lane (lan
 
 struct Fp8Args {
   const short* x896;                     // (n, 896) bf16
-  const uint4* wpre; const float* spre; const float* bpre;     // 256 × 896, fragment order
-  const uint4* wg; const float* sg; const float* bg;           // 2048 × 768 unit-major rows ([W_ih | W_hh])
-  const uint4* wh; const float* sh; const float* bh;           // 160 × 512 heads
+  const i32x8* wpre; const float* spre; const float* bpre;     // 256 × 896, fragment order
+  const i32x8* wg; const float* sg; const float* bg;           // 2048 × 768 unit-major rows ([W_ih | W_hh])
+  const i32x8* wh; const float* sh; const float* bh;           // 160 × 512 heads
   float* h; float* c;                    // (n, 512) fp32 state, in place
   const float* keep; const float* active;
   float* z;                              // (n, 160) fp32
@@ -178,7 +184,7 @@ __global__ __launch_bounds__(NT) void actor_fp8_kernel(Fp8Args A) {
   __syncthreads();
 
   // ---- stage 1: pre = relu(x·W_preᵀ·scales + b): wave w owns column tiles 2w, 2w+1
-  stream_gemm<2, XD / 64, 1, 2>(
+  stream_gemm<2, XD / 128, 1, 2>(
       a8x, LDX, A.wpre, [&](int, int i) { return 2 * w + i; }, lane, [&](int, const f32x4 (&acc)[2]) {
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -242,7 +248,7 @@ __global__ __launch_bounds__(NT) void actor_fp8_kernel(Fp8Args A) {
   __syncthreads();
 
   // ---- stage 3: gates (wave w: units 64w … 64w+63 = tiles 16w … 16w+15, 4 chunks of 4) + LSTM cell in LDS
-  stream_gemm<4, KG / 64, 4, 4>(
+  stream_gemm<4, KG / 128, 4, 2>(
       a8g, LDG, A.wg, [&](int ch, int i) { return 16 * w + 4 * ch + i; }, lane,
       [&](int ch, const f32x4 (&acc)[4]) {
 #pragma unroll
@@ -328,7 +334,7 @@ __global__ __launch_bounds__(NT) void actor_fp8_kernel(Fp8Args A) {
 
   // ---- stage 5: heads z = h·W_headsᵀ·scales + b (10 column tiles: wave w takes w and w + 8 — waves 2-7 a
   //      duplicate of their first tile as the second, whose result is dropped)
-  stream_gemm<2, HD / 64, 1, 4>(
+  stream_gemm<2, HD / 128, 1, 2>(
       a8x, LDX, A.wh, [&](int, int i) { return min(w + NW * i, ZD / 16 - 1); }, lane,
       [&](int, const f32x4 (&acc)[2]) {
 #pragma unroll
@@ -355,8 +361,8 @@ extern "C" hipError_t dca_actor_fp8(const short* x896, const void* wpre, const f
                                     const float* bh, float* h, float* c, const float* keep, const float* active,
                                     float* z, int n, hipStream_t stream) {
   if (n < 1) return hipSuccess;
-  Fp8Args a{x896, reinterpret_cast<const uint4*>(wpre), spre, bpre, reinterpret_cast<const uint4*>(wg), sg, bg,
-            reinterpret_cast<const uint4*>(wh), sh, bh, h, c, keep, active, z, n};
+  Fp8Args a{x896, reinterpret_cast<const i32x8*>(wpre), spre, bpre, reinterpret_cast<const i32x8*>(wg), sg, bg,
+            reinterpret_cast<const i32x8*>(wh), sh, bh, h, c, keep, active, z, n};
   hipLaunchKernelGGL(actor_fp8_kernel, dim3((n + BM - 1) / BM), dim3(NT), 0, stream, a);
   return hipGetLastError();
 }

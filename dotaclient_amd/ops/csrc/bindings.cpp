@@ -393,6 +393,19 @@ void actor_state_prep(torch::Tensor pre, torch::Tensor h, torch::Tensor c, torch
                                  H, cur_stream()), "dca_actor_state_prep");
 }
 
+// Compact actor staging → the step's operands in one launch: units16 (…) fp16 → units (same shape) fp32, handles32
+// int32 → handles int64.
+void actor_widen(torch::Tensor units16, torch::Tensor units, torch::Tensor handles32, torch::Tensor handles) {
+  CHECK_DEV(units16); CHECK_CONTIG(units16); CHECK_DT(units16, at::kHalf); CHECK_F32(units);
+  CHECK_DEV(handles32); CHECK_CONTIG(handles32); CHECK_DT(handles32, at::kInt);
+  CHECK_DEV(handles); CHECK_CONTIG(handles); CHECK_DT(handles, at::kLong);
+  TORCH_CHECK(units16.numel() == units.numel() && units.numel() % 4 == 0 && handles32.numel() == handles.numel(),
+              "actor_widen shapes");
+  hip_check(dca_actor_widen(units16.data_ptr(), ptr<float>(units), units.numel(), ptr<int>(handles32),
+                            reinterpret_cast<long long*>(handles.data_ptr()), handles.numel(), cur_stream()),
+            "dca_actor_widen");
+}
+
 // LSTM cell from fp32 pre-activation gates (N,4H): updates h, c (N,H) f32 in place, writes h16 (N,H) bf16.
 // Optional ``active`` (N) f32: rows with active == 0 keep their h / c / h16 (slots not stepped this call).
 void lstm_cell(torch::Tensor gates, torch::Tensor h, torch::Tensor c, torch::Tensor h16,
@@ -1123,6 +1136,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("time_major") = false, py::arg("dg_out") = py::none(), py::arg("dg_bf16") = false,
         py::arg("want_dbias") = false, py::arg("precise") = false, py::arg("reset") = py::none());
   m.def("sample_actions", &sample_actions, "fused masked hierarchical Gumbel-max action sampling (actor)");
+  m.def("actor_widen", &actor_widen, "compact actor staging: fp16 features -> fp32, int32 handles -> int64 (one launch)");
   m.def("actor_state_prep", &actor_state_prep, "actor step: state resets + [x | bf16(h)] gate-GEMM operand");
   m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)", py::arg("gates"),
         py::arg("h"), py::arg("c"), py::arg("h16"), py::arg("active") = py::none());

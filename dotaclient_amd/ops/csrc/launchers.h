@@ -84,6 +84,8 @@ hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, const float*
 hipError_t dca_sample_actions(const float* z, int ldz, const short* emb, const long long* handles, int N, int U,
                               unsigned long long seed, const long long* ctr, int* idx, unsigned char* act,
                               unsigned char* msk, float* logp, float* value, hipStream_t st);
+hipError_t dca_actor_widen(const void* u16, float* u32, long long n_units, const int* h32, long long* h64,
+                           long long n_handles, hipStream_t st);
 hipError_t dca_actor_state_prep(const short* pre, float* h, float* c, const float* keep, short* xh, int N, int P,
                                 int H, hipStream_t st);
 hipError_t dca_lstm_cell(const float* gates, float* h, float* c, short* h16, const float* active, int N, int H,

@@ -16,20 +16,21 @@ from dotaclient_amd.models.policy import Policy, get_config
 
 
 def _unfrag(f, s, N, K):
-    q = f.view(N // 16, K // 64, 4, 16, 2, 8).permute(0, 3, 1, 4, 2, 5).reshape(N, K)
+    # [N/16][K/128][lane = 16·(k%128 // 32) + n%16][k % 32] (the 16x16x128 f8f6f4 operand order)
+    q = f.view(N // 16, K // 128, 4, 16, 32).permute(0, 3, 1, 2, 4).reshape(N, K)
     return q.view(torch.float8_e4m3fn).float() * s[:, None]
 
 
 def test_fp8_weight_fragment_order_roundtrip():
     torch.manual_seed(0)
-    w = torch.randn(48, 192)
+    w = torch.randn(48, 256)
     f, s = fp8_weight(w)
-    back = _unfrag(f, s, 48, 192)
+    back = _unfrag(f, s, 48, 256)
     assert float((back - w).abs().max() / w.abs().max()) < 0.07         # e4m3: 3 mantissa bits
     # exact for values that are e4m3 numbers times the channel scale
-    w2 = torch.tensor([[1.0, -2.0, 0.5, 448.0] * 16] * 16)
+    w2 = torch.tensor([[1.0, -2.0, 0.5, 448.0] * 32] * 16)
     f2, s2 = fp8_weight(w2)
-    torch.testing.assert_close(_unfrag(f2, s2, 16, 64), w2, rtol=0, atol=0)
+    torch.testing.assert_close(_unfrag(f2, s2, 16, 128), w2, rtol=0, atol=0)
 
 
 def _qrows(x):
