@@ -50,9 +50,9 @@ def evaluate_vs_default_bot(policy, n_games: int = 128, device='cuda', seed: int
         rew = np.asarray(r.rewards, np.float64)
         per_game.setdefault(r.game_id, [])
         sums = rew.sum(axis=0)
-        row = {'sum': float(sums.sum()), 'steps': float(rew.shape[0]), 'win': float(rew[-1, 1] > 0.5),
-               'loss': float(rew[-1, 1] < -0.5)}
-        row.update({k: float(v) for k, v in zip(REWARD_KEYS, sums)})
+        row = {k: float(v) for k, v in zip(REWARD_KEYS, sums)}
+        row.update({'sum': float(sums.sum()), 'steps': float(rew.shape[0]), 'won': float(rew[-1, 1] > 0.5),
+                    'lost': float(rew[-1, 1] < -0.5)})
         per_game[r.game_id].append(row)
     games = [rows[0] for rows in list(per_game.values())[:n_games]]    # one controlled player per game
     out: Dict[str, float] = {'games': float(len(games))}
@@ -60,8 +60,8 @@ def evaluate_vs_default_bot(policy, n_games: int = 128, device='cuda', seed: int
         return out
     mean = lambda k: float(np.mean([g[k] for g in games]))             # noqa: E731
     out['game/rewards_sum'] = mean('sum')
-    out['game/win_rate'] = mean('win')
-    out['game/loss_rate'] = mean('loss')
+    out['game/win_rate'] = mean('won')
+    out['game/loss_rate'] = mean('lost')
     out['game/steps'] = mean('steps')
     for k in REWARD_KEYS:
         out[f'game/rewards_{k}'] = mean(k)
