@@ -1,0 +1,113 @@
+"""Learning curve of the node loop against the scripted default bot — the reference's only quality signal.
+
+The actor (VecActor, native engine, self-play on the latest weights) feeds an in-process DotaOptimizer (the fused
+IEEE-fp32 learner by default, lstm512, the reference deploy shape 8 × 1400); every ``eval_every`` seconds of training
+the learner's current weights play ``eval_games`` games against the default bot (actor/validate.py — the reference's
+validation agent, /root/reference/agent.py:905-927 / 415-434) and one row is emitted: training wall time, iterations,
+learner samples, actor steps, ``game/rewards_sum``, ``game/win_rate`` and the per-key rewards. Evaluation games use a
+fixed seed, so every row plays the same opening positions; evaluation time is excluded from ``t_train``.
+
+Used by ``scripts/learning_curve.py`` (profiles/r4_learning_curve.jsonl) and tests/test_learning.py.
+"""
+from __future__ import annotations
+
+import tempfile
+import threading
+import time
+from concurrent.futures import ThreadPoolExecutor
+from typing import Callable, Dict, List, Optional
+
+
+def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_games: int = 128,
+                       model: str = 'lstm512', precision: str = 'fp32-exact', backend: str = 'auto',
+                       games: int = 1024, threads: int = 12, seq_len: int = 1400, batch_size: int = 8,
+                       seq_per_epoch: int = 16, lr: float = 1e-4, entropy_coef: float = 0.01,
+                       max_dota_time: float = 600.0, pack: bool = True, seed: int = 7, device: str = 'cuda',
+                       eval_seed: int = 4242, on_row: Optional[Callable[[Dict], None]] = None) -> List[Dict]:
+    """Train for ``budget`` seconds (evaluations excluded) and return the evaluation rows (the first one before
+    any training). ``on_row`` is called with every row as it is produced."""
+    import torch
+    from ..actor.validate import evaluate_vs_default_bot
+    from ..actor.vec import VecActor
+    from ..actor.weights import WeightStore
+    from ..transport.broker import InProcBroker
+    from .optimizer import DotaOptimizer, OptimizerConfig
+
+    torch.manual_seed(seed)
+    tmp = tempfile.mkdtemp(prefix='dca_curve_')
+    broker = InProcBroker(maxsize=256, drop_oldest=True)
+    cfg = OptimizerConfig(log_dir=tmp, epochs=1, seq_per_epoch=seq_per_epoch, batch_size=batch_size,
+                          seq_len=seq_len, model=model, precision=precision, device=device, backend=backend,
+                          learning_rate=lr, entropy_coef=entropy_coef, checkpoint_keep=2, run_local=True,
+                          xp_timeout=300.0, histogram_freq=10 ** 9, async_checkpoint=True, prefetch_rollouts=64,
+                          pack_sequences=bool(pack), seed=seed)
+    opt = DotaOptimizer(cfg, broker)
+    ws = WeightStore(model, device='cpu')
+    loader = ThreadPoolExecutor(1, thread_name_prefix='weights')
+    broker.subscribe_model(lambda v, b: loader.submit(ws.add_bytes, v, b))
+    loader.submit(lambda: None).result()
+    va = VecActor(ws, games, broker.publish_experience, device=device, seed=seed, rollout_size=9999,
+                  max_dota_time=max_dota_time, hidden_stride=seq_len, threads=threads, stagger=True)
+    stop, pause, paused, err = threading.Event(), threading.Event(), threading.Event(), []
+    rows: List[Dict] = []
+    sync = torch.cuda.synchronize if str(device).startswith('cuda') else (lambda: None)
+
+    def actor_loop():
+        try:
+            while not stop.is_set():
+                if pause.is_set():
+                    paused.set()
+                    time.sleep(0.005)
+                    continue
+                paused.clear()
+                va.step()
+        except BaseException as e:       # surfaced by the training loop
+            err.append(e)
+            paused.set()
+
+    def evaluate(row):
+        pause.set()
+        if th.is_alive():
+            paused.wait(timeout=60)
+        opt.flush_metrics()
+        sync()
+        t0 = time.time()
+        row.update(evaluate_vs_default_bot(opt.policy, n_games=eval_games, device=device, seed=eval_seed,
+                                           max_dota_time=max_dota_time, threads=threads))
+        row['eval_s'] = round(time.time() - t0, 3)
+        pause.clear()
+        rows.append(row)
+        if on_row is not None:
+            on_row(row)
+
+    th = threading.Thread(target=actor_loop, daemon=True)
+    trained, samples, it = 0.0, 0, opt.iteration_start
+    try:
+        evaluate({'t_train': 0.0, 'iteration': 0, 'samples': 0, 'actor_steps': 0, 'model': model,
+                  'precision': precision, 'backend': backend, 'pack': bool(pack)})
+        th.start()
+        next_eval = eval_every
+        while trained < budget:
+            t0 = time.time()
+            opt.run_iteration(it)
+            it += 1
+            samples += seq_per_epoch * seq_len
+            trained += time.time() - t0
+            if err:
+                raise err[0]
+            if trained >= next_eval or trained >= budget:
+                m = getattr(opt, 'last_metrics', {}) or {}
+                evaluate({'t_train': round(trained, 1), 'iteration': it - opt.iteration_start, 'samples': samples,
+                          'actor_steps': va.steps_taken, 'loss': m.get('loss/sum'), 'entropy': m.get('entropy'),
+                          'train_reward_per_sec': m.get('reward_per_sec/sum'),
+                          'avg_weight_age': m.get('avg_weight_age')})
+                next_eval += eval_every
+    finally:
+        stop.set()
+        if th.is_alive():
+            th.join(timeout=60)
+        opt.close()
+        va.close()
+        opt.flush_checkpoints()
+        loader.shutdown(wait=True)
+    return rows

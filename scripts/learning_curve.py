@@ -1,21 +1,12 @@
-"""Learning curve of the fused learner in the node loop, measured the reference's way: against the scripted default bot.
+"""Learning curve of the fused learner in the node loop against the scripted default bot (one JSONL row per
+evaluation; see dotaclient_amd/learner/curve.py).
 
-The actor (VecActor, native engine, self-play, latest weights) feeds an in-process DotaOptimizer (fused IEEE-fp32
-learner by default, lstm512, the reference deploy shape 8 × 1400, 16 sequences per iteration); every
-``--eval-every`` seconds of training the learner's current weights play ``--eval-games`` games against the default
-bot (actor/validate.py — the reference's validation agent, agent.py:905-927 / 415-434) and one JSONL row is written:
-wall time, iterations, learner samples, actor steps, ``game/rewards_sum``, ``game/win_rate`` and the per-key rewards.
-The evaluation games use a fixed seed, so every row plays the same opening positions.
-
-    python scripts/learning_curve.py --budget 150 --out profiles/r4_learning_curve.jsonl
+    python scripts/learning_curve.py --budget 600 --eval-every 30 --out profiles/r4_learning_curve.jsonl
 """
 import argparse
 import json
 import os
 import sys
-import tempfile
-import threading
-import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
@@ -41,90 +32,18 @@ def main(argv=None):
     ap.add_argument('--out', default='gpurun_out/learning_curve.jsonl')
     ap.add_argument('--device', default='cuda')
     a = ap.parse_args(argv)
-
-    import torch
-    from dotaclient_amd.actor.validate import evaluate_vs_default_bot
-    from dotaclient_amd.actor.vec import VecActor
-    from dotaclient_amd.actor.weights import WeightStore
-    from dotaclient_amd.learner.optimizer import DotaOptimizer, OptimizerConfig
-    from dotaclient_amd.transport.broker import InProcBroker
-
-    torch.manual_seed(a.seed)
-    tmp = tempfile.mkdtemp(prefix='dca_curve_')
-    broker = InProcBroker(maxsize=256, drop_oldest=True)
-    cfg = OptimizerConfig(log_dir=tmp, epochs=1, seq_per_epoch=a.seq_per_epoch, batch_size=a.batch_size,
-                          seq_len=a.seq_len, model=a.model, precision=a.precision, device=a.device,
-                          backend=a.backend, learning_rate=a.lr, entropy_coef=a.entropy_coef, checkpoint_keep=2,
-                          run_local=True, xp_timeout=300.0, histogram_freq=10 ** 9, async_checkpoint=True,
-                          prefetch_rollouts=64, pack_sequences=bool(a.pack), seed=a.seed)
-    opt = DotaOptimizer(cfg, broker)
-    ws = WeightStore(a.model, device='cpu')
-    from concurrent.futures import ThreadPoolExecutor
-    loader = ThreadPoolExecutor(1, thread_name_prefix='weights')
-    broker.subscribe_model(lambda v, b: loader.submit(ws.add_bytes, v, b))
-    loader.submit(lambda: None).result()
-    va = VecActor(ws, a.games, broker.publish_experience, device=a.device, seed=a.seed, rollout_size=9999,
-                  max_dota_time=a.max_dota_time, hidden_stride=a.seq_len, threads=a.threads, stagger=True)
-    stop, pause, err = threading.Event(), threading.Event(), []
-
-    def actor_loop():
-        try:
-            while not stop.is_set():
-                if pause.is_set():
-                    time.sleep(0.01)
-                    continue
-                va.step()
-        except BaseException as e:
-            err.append(e)
-
-    def evaluate(row):
-        pause.set()
-        opt.flush_metrics()
-        torch.cuda.synchronize()
-        t0 = time.time()
-        m = evaluate_vs_default_bot(opt.policy, n_games=a.eval_games, device=a.device, seed=4242,
-                                    max_dota_time=a.max_dota_time, threads=a.threads)
-        row.update(m)
-        row['eval_s'] = time.time() - t0
-        pause.clear()
-        print(json.dumps(row), flush=True)
-        fh.write(json.dumps(row) + '\n')
-        fh.flush()
-
+    from dotaclient_amd.learner.curve import run_learning_curve
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
-    fh = open(a.out, 'w')
-    th = threading.Thread(target=actor_loop, daemon=True)
-    trained = 0.0
-    it = opt.iteration_start
-    samples = 0
-    evaluate({'t_train': 0.0, 'iteration': 0, 'samples': 0, 'actor_steps': 0, 'model': a.model,
-              'precision': a.precision, 'pack': bool(a.pack)})
-    th.start()
-    try:
-        next_eval = a.eval_every
-        while trained < a.budget:
-            t0 = time.time()
-            opt.run_iteration(it)
-            it += 1
-            samples += a.seq_per_epoch * a.seq_len
-            trained += time.time() - t0
-            if err:
-                raise err[0]
-            if trained >= next_eval or trained >= a.budget:
-                m = getattr(opt, 'last_metrics', {}) or {}
-                evaluate({'t_train': round(trained, 1), 'iteration': it - opt.iteration_start, 'samples': samples,
-                          'actor_steps': va.steps_taken, 'loss': m.get('loss/sum'), 'entropy': m.get('entropy'),
-                          'train_reward_per_sec': m.get('reward_per_sec/sum'),
-                          'avg_weight_age': m.get('avg_weight_age')})
-                next_eval += a.eval_every
-    finally:
-        stop.set()
-        th.join(timeout=60)
-        opt.close()
-        va.close()
-        opt.flush_checkpoints()
-        loader.shutdown(wait=True)
-        fh.close()
+    with open(a.out, 'w') as fh:
+        def emit(row):
+            print(json.dumps(row), flush=True)
+            fh.write(json.dumps(row) + '\n')
+            fh.flush()
+        run_learning_curve(budget=a.budget, eval_every=a.eval_every, eval_games=a.eval_games, model=a.model,
+                           precision=a.precision, backend=a.backend, games=a.games, threads=a.threads,
+                           seq_len=a.seq_len, batch_size=a.batch_size, seq_per_epoch=a.seq_per_epoch, lr=a.lr,
+                           entropy_coef=a.entropy_coef, max_dota_time=a.max_dota_time, pack=bool(a.pack),
+                           seed=a.seed, device=a.device, on_row=emit)
 
 
 if __name__ == '__main__':
