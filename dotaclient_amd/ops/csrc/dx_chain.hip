@@ -8,14 +8,14 @@
 // Reference: policy.py:135-138 (affine_pre_rnn + ReLU) feeding the recurrent layer (policy.py:143-145; the LSTM of
 // the north star). N = B·S rows (11 200 at the deploy shape), 4H = 2048, P = 256, X = 896.
 //
-// One 512-thread workgroup (8 waves) per 64-row tile; the 64 × P dpre tile never leaves the workgroup between the
+// One 512-thread workgroup (8 waves) per BM-row tile (BM = 48); the BM × P dpre tile never leaves the workgroup between the
 // two products (it is written once to HBM for the pre-RNN weight gradient, and kept in LDS as the second product's
 // A operand):
 // * stage 1, K = 4H in 32-deep slabs, double-buffered through LDS, loads issued RD slabs ahead into a register ring
 //   (one slab of lead left every LDS store waiting out a full memory round trip), one barrier per slab; waves as
-//   2 (32 rows) × 4 (64 columns), each 2 × 4 v_mfma_f32_16x16x32_bf16 tiles;
+//   1 (48 rows) × 8 (32 columns), each 3 × 2 v_mfma_f32_16x16x32_bf16 tiles;
 // * ReLU mask + dpre store in the accumulator layout, dpre written into LDS in the stage-1 A layout (8 slabs);
-// * stage 2, X in 128-column chunks × K = P in 32-deep slabs (same pipeline), waves as 4 (16 rows) × 2 (64 columns).
+// * stage 2, X in 128-column chunks × K = P in 32-deep slabs (same pipeline), waves as 1 (48 rows) × 8 (16 columns).
 // Both weight operands come K-contiguous per output column (W_ihᵀ image (P × 4H), W_preᵀ image (X × P)).
 //
 // EXACT = false: bf16x3 — x = hi + lo (two bf16), products hi·hi + lo·hi + hi·lo on the bf16 MFMA (≈2⁻¹⁶ relative per
@@ -37,7 +37,10 @@ namespace {
 using dca::bf16x8;
 using dca::f32x4;
 
-constexpr int BM = 64, BK = 32, NT = 512, P = 256, XC = 128, RD = 4;
+// BM = 48 rows per workgroup: 234 workgroups at the deploy shape (N = 11 200) on the 256 CUs (one per CU: LDS- and
+// VGPR-bound). BM = 64 left 81 CUs idle (175 workgroups): measured 271 µs for the exact ∂X chain.
+constexpr int BM = 48, BK = 32, NT = 512, P = 256, XC = 128, RD = 4;
+constexpr int NI1 = BM / 16;                      // 16-row tiles per wave (every wave spans all BM rows)
 
 template <bool EXACT>
 struct Lay {
@@ -154,9 +157,9 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
   constexpr int DIMG = (P / BK) * L::A1;          // one image (hi, or fp32) of the dpre tile
   if (K1 > 0) {
   // ================= stage 1: C1 (64 × P) = dG[r0:r0+64] · W_ih =================
-  const int ar = tid >> 3, ak = (tid & 7) * 4;              // dG slab: one fp32 quad per thread
+  const int ar = tid >> 3, ak = (tid & 7) * 4;              // dG slab: one fp32 quad per thread (threads ≥ 8·BM idle)
   const int arow = r0 + ar;
-  const int a_off0 = arow < N ? (arow * K1 + ak) * 4 : kOob;
+  const int a_off0 = (ar < BM && arow < N) ? (arow * K1 + ak) * 4 : kOob;
   const int br = tid & 255, bh = tid >> 8;                   // exact W1 slab: 16 k per thread
   const int b_off0 = (br * K1 + 16 * bh) * ES;
   float4 sa[RD];
@@ -185,15 +188,17 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
     char* base = lds + buf * L::S1;
     char* bb = base + L::IMG * L::A1;
     if constexpr (EXACT) {
-      *reinterpret_cast<float4*>(base + ar * L::RP + ak * 4) = sa[slot];
+      if (ar < BM) *reinterpret_cast<float4*>(base + ar * L::RP + ak * 4) = sa[slot];
 #pragma unroll
       for (int i = 0; i < 4; ++i) *reinterpret_cast<uint4*>(bb + br * L::RP + (16 * bh + 4 * i) * 4) = sb[slot][i];
     } else {
       uint2 hi, lo;
       split4(sa[slot], hi, lo);
       const int o = coff<false>(ar, ak >> 3) + 8 * ((ak >> 2) & 1);
-      *reinterpret_cast<uint2*>(base + o) = hi;
-      *reinterpret_cast<uint2*>(base + L::A1 + o) = lo;
+      if (ar < BM) {
+        *reinterpret_cast<uint2*>(base + o) = hi;
+        *reinterpret_cast<uint2*>(base + L::A1 + o) = lo;
+      }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {              // 16-B chunk tid & 3 of rows tid / 4 and 128 + tid / 4
         const int ob = coff<false>(128 * j + (tid >> 2), tid & 3);
@@ -202,12 +207,12 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
       }
     }
   };
-  const int wr = w >> 2, wc = w & 3;             // 2 × 4 waves: rows 32·wr, cols 64·wc
-  f32x4 acc[2][4];
+  const int wc = w;                              // 1 × 8 waves: all BM rows, cols 32·wc
+  f32x4 acc[NI1][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < NI1; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int nk = K1 / BK;                         // multiple of RD (host check)
 #pragma unroll
   for (int d = 0; d < RD; ++d) load1(d, d * BK);
@@ -219,12 +224,12 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
       const int ks = ks0 + d;
       const char* base = lds + (d & 1) * L::S1;   // (RD even: slab ks sits in buffer ks & 1 = d & 1)
       const char* bb = base + L::IMG * L::A1;
-      Frag fa[2], fb[4];
+      Frag fa[NI1], fb[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) get_frag<EXACT>(base, L::A1, wr * 32 + i * 16 + r16, q, fa[i]);
+      for (int i = 0; i < NI1; ++i) get_frag<EXACT>(base, L::A1, i * 16 + r16, q, fa[i]);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) get_frag<EXACT>(bb, L::B1, wc * 64 + j * 16 + r16, q, fb[j]);
-      if (!(dbg & 2)) mma_tiles<EXACT, 2, 4>(fa, fb, acc);
+      for (int j = 0; j < 2; ++j) get_frag<EXACT>(bb, L::B1, wc * 32 + j * 16 + r16, q, fb[j]);
+      if (!(dbg & 2)) mma_tiles<EXACT, NI1, 2>(fa, fb, acc);
       else if (fa[0].hi[0] == 12345 && fb[0].hi[1] == 4321) acc[0][0][0] += 1.f;
       store1((d + 1) % RD, (d + 1) & 1);            // (after the last slab: zeros into a buffer nobody reads)
       if (!(dbg & 1)) load1(d, (ks + RD) * BK);    // slot d held slab ks, stored at the previous iteration
@@ -233,34 +238,58 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
   }
 
   // ================= ReLU mask, dpre → HBM and → LDS (stage-2 A operand, 8 slabs in the A layout) =============
-  // accumulator layout: acc[i][j][e] = C[row 32·wr + 16·i + 4·q + e][col 64·wc + 16·j + r16]
-  // (the dpre image aliases the stage-1 buffers: all their reads are done, barrier above)
+  // accumulator layout: acc[i][j][e] = C[row 16·i + 4·q + e][col 32·wc + 16·j + r16]
+  // (the dpre image aliases the stage-1 buffers: all their reads are done, barrier above). The ReLU-mask / bias
+  // operands are loaded for the whole tile first (buffer loads, rows past N read 0): loads issued between the dpre
+  // stores made every element one exposed round trip (load → wait → store, 32 in a row).
+  {
+    const __amdgpu_buffer_rsrc_t rX = rsrc(x, EPI == 0 ? (long long)N * P * 4 : (long long)P * 4);
+    float xv[NI1][2][4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < NI1; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int row = wr * 32 + i * 16 + 4 * q + e, col = wc * 64 + j * 16 + r16;
-        const int grow = r0 + row;
-        float v = 0.f;
-        if (grow < N) {
-          if constexpr (EPI == 0) v = x[(size_t)grow * P + col] > 0.f ? acc[i][j][e] : 0.f;
-          else if constexpr (EPI == 1) v = fmaxf(acc[i][j][e] + x[col], 0.f);
-          else v = acc[i][j][e] + x[col];
-          dpre[(size_t)grow * P + col] = v;
+        for (int e = 0; e < 4; ++e) {
+          const int row = i * 16 + 4 * q + e, col = wc * 32 + j * 16 + r16;
+          const int grow = r0 + row;
+          if constexpr (EPI == 0) {
+            xv[i][j][e] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                              rX, grow < N ? (grow * P + col) * 4 : kOob, 0, 0));
+          } else {
+            xv[i][j][e] = e == 0 && i == 0 ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                                                           rX, col * 4, 0, 0))
+                                           : 0.f;
+          }
         }
-        const int kk = col & (BK - 1);
-        char* slab = dimg + (col / BK) * L::A1;
-        if constexpr (EXACT) {
-          *reinterpret_cast<float*>(slab + coff<true>(row, kk >> 2) + 4 * (kk & 3)) = v;
-        } else {
-          const int o = coff<false>(row, kk >> 3) + 2 * (kk & 7);
-          const short h = dca::f2bf(v);
-          *reinterpret_cast<short*>(slab + o) = h;
-          *reinterpret_cast<short*>(slab + DIMG + o) = dca::f2bf(v - dca::bf2f(h));
+    const __amdgpu_buffer_rsrc_t rD = rsrc(dpre, (long long)N * P * 4);
+#pragma unroll
+    for (int i = 0; i < NI1; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int row = i * 16 + 4 * q + e, col = wc * 32 + j * 16 + r16;
+          const int grow = r0 + row;
+          float v;
+          if constexpr (EPI == 0) v = xv[i][j][e] > 0.f ? acc[i][j][e] : 0.f;
+          else if constexpr (EPI == 1) v = fmaxf(acc[i][j][e] + xv[0][j][0], 0.f);
+          else v = acc[i][j][e] + xv[0][j][0];
+          if (grow >= N) v = 0.f;
+          __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rD,
+                                                grow < N ? (grow * P + col) * 4 : kOob, 0, 0);
+          const int kk = col & (BK - 1);
+          char* slab = dimg + (col / BK) * L::A1;
+          if constexpr (EXACT) {
+            *reinterpret_cast<float*>(slab + coff<true>(row, kk >> 2) + 4 * (kk & 3)) = v;
+          } else {
+            const int o = coff<false>(row, kk >> 3) + 2 * (kk & 7);
+            const short h = dca::f2bf(v);
+            *reinterpret_cast<short*>(slab + o) = h;
+            *reinterpret_cast<short*>(slab + DIMG + o) = dca::f2bf(v - dca::bf2f(h));
+          }
         }
-      }
+  }
 
   } else if constexpr (EXACT) {
     // stage-2-only launch (K1 = 0), exact: dG (N, P) fp32 rows straight into the fp32 dpre image (8 slabs)
@@ -319,10 +348,11 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
       *reinterpret_cast<uint4*>(bb + L::B2 + o) = sw[slot][1];
     }
   };
-  const int vr = w >> 1, vc = w & 1;             // 4 × 2 waves: rows 16·vr, cols 64·vc of the chunk
-  f32x4 acc2[1][4];
+  const int vc = w;                              // 1 × 8 waves: all BM rows, cols 16·vc of the chunk
+  f32x4 acc2[NI1][1];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) acc2[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < NI1; ++i) acc2[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const __amdgpu_buffer_rsrc_t rDx = rsrc(dx, (long long)N * X * 4);
 #pragma unroll
   for (int d = 0; d < RD; ++d) load2(d, d);
   store2(0, 0);
@@ -333,22 +363,25 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
       const int it = it0 + d;
       const int chunk = it / nk2, ks = it % nk2;
       const char* bb = s2 + (d & 1) * L::S2;
-      Frag fa[1], fb[4];
-      get_frag<EXACT>(dimg + ks * L::A1, DIMG, vr * 16 + r16, q, fa[0]);
+      Frag fa[NI1], fb[1];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) get_frag<EXACT>(bb, L::B2, vc * 64 + j * 16 + r16, q, fb[j]);
-      mma_tiles<EXACT, 1, 4>(fa, fb, acc2);
+      for (int i = 0; i < NI1; ++i) get_frag<EXACT>(dimg + ks * L::A1, DIMG, i * 16 + r16, q, fa[i]);
+      get_frag<EXACT>(bb, L::B2, vc * 16 + r16, q, fb[0]);
+      mma_tiles<EXACT, NI1, 1>(fa, fb, acc2);
       store2((d + 1) % RD, (d + 1) & 1);
       load2(d, it + RD);
-      if (ks == nk2 - 1) {                        // chunk done: store its 64 × 128 output tile
+      if (ks == nk2 - 1) {                        // chunk done: store its BM × 128 output tile (rows past N dropped)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int i = 0; i < NI1; ++i) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            const int grow = r0 + vr * 16 + 4 * q + e;
-            if (grow < N) dx[(size_t)grow * X + chunk * XC + vc * 64 + j * 16 + r16] = acc2[0][j][e];
+            const int grow = r0 + i * 16 + 4 * q + e;
+            // (through a scalar: __builtin_bit_cast of the vector element itself compiled to element 0 for every e)
+            const float v = acc2[i][0][e];
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, v), rDx,
+                                                  grow < N ? (grow * X + chunk * XC + vc * 16 + r16) * 4 : kOob, 0, 0);
           }
-          acc2[0][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          acc2[i][0] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
       __syncthreads();

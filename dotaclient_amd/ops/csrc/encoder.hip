@@ -1103,17 +1103,20 @@ __global__ __launch_bounds__(512, 1) void encoder_fwd_x_kernel(FfParams P) {
     for (int r = 0; r < 4; ++r) b[r] = fmaxf(b[r], 0.f);
     x_put(img[0], wv, b, i, kg);
   }
+  // the weight / bias loads have landed: no first-iteration wait left inside the loop (where it would stay as a
+  // vmcnt(0) before the emb stores of every item, waiting out the previous item's stores)
+  __builtin_amdgcn_s_waitcnt(0);
   int buf = 0;
   for (int k = k0; k < k1; ++k) {
     lds_barrier();   // image k complete; staging slot of k + 1 written
-    if (wv < 3) {
-      stg[(k + 2) % 3][64 * wv + lane] = pre;
-      pre = ff_stage_load(P, Ru, min(k + 3, kl), cnt, uoff, wv, lane);
-    }
     const int rb = k / cnt, u = k - rb * cnt, row0 = 16 * rb;
     float a[32];
     x_afrags(img[buf], i, kg, a);
     const f32x4 c = x_mma_k128(a, wx);
+    // staging of item k + 2 (slot (k - 1) % 3, free in this iteration), loaded at the end of the previous iteration
+    // AFTER its emb stores: waiting for it does not wait for stores issued later (vmcnt also counts stores on
+    // gfx950), and the next load is issued after this item's stores for the same reason
+    if (wv < 3) stg[(k + 2) % 3][64 * wv + lane] = pre;
     {   // next item's basic tile into the other image (past the range's end: a rewrite nobody reads)
       f32x4 b = x_layer1(stg[(k + 1) % 3], w1x, i, kg);
 #pragma unroll
@@ -1140,6 +1143,7 @@ __global__ __launch_bounds__(512, 1) void encoder_fwd_x_kernel(FfParams P) {
         parg[r] = 0;
       }
     }
+    if (wv < 3) pre = ff_stage_load(P, Ru, min(k + 3, kl), cnt, uoff, wv, lane);
     buf ^= 1;
   }
 }
@@ -1207,10 +1211,6 @@ __global__ __launch_bounds__(512, 1) void encoder_bwd_x_kernel(FbParams P) {
   int buf = 0;
   for (int k = k0; k < k1; ++k) {
     lds_barrier();
-    if (wv < 3) {
-      stg[(k + 2) % 3][64 * wv + lane] = pre;
-      pre = fb_stage_load(P, min(k + 3, kl), cnt, uoff, wv, lane);
-    }
     const float* sl = stg[k % 3];
     float a[32];
     x_afrags(img[buf], i, kg, a);                 // ∂emb[row i][e], e = 32s + 8kg + jj
@@ -1222,8 +1222,14 @@ __global__ __launch_bounds__(512, 1) void encoder_bwd_x_kernel(FbParams P) {
     for (int r = 0; r < 4; ++r) ub[r] = i < kF ? sl[(4 * kg + r) * kF + i] : 0.f;
     f32x4 bas = x_layer1(sl, w1x, i, kg);
     f32x4 c = x_mma_k128(a, wx);                  // ∂basic[row][j] (before ReLU')
+    // The global loads consumed here (staging of item k + 2, build data of item k + 1) were issued one iteration
+    // ago, and nothing was issued after them: the vmcnt(0) the compiler puts before their first use waits out no
+    // fresh round trip. (Issued at the top of the iteration instead, as before, that wait covered a load issued
+    // ~40 MFMAs earlier: one exposed HBM/L2 round trip per item.)
+    if (wv < 3) stg[(k + 2) % 3][64 * wv + lane] = pre;   // slot (k - 1) % 3: nobody reads it in this iteration
     // item k + 1's ∂emb into the other images (every wave has passed this item's barrier)
     xb_build(bn, stg[(k + 1) % 3], min(k + 1, kl) % cnt, img[buf ^ 1], imt[buf ^ 1], wv, lane);
+    if (wv < 3) pre = fb_stage_load(P, min(k + 3, kl), cnt, uoff, wv, lane);
     fb_load_build<false, COMPAT>(bn, R, P.ldq, min(k + 2, kl), k + 2 <= kl && (k + 2) % cnt == 0, cnt, uoff, U, tau,
                                  wv, i, kg);
 #pragma unroll
