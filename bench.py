@@ -24,7 +24,10 @@ EVERY rank (one actor runtime per GPU), and reported as node aggregates (sums ov
   per node fed by one actor process per GPU, WORLD_SIZE learner ranks consuming disjoint rollouts (DDP over RCCL),
   rank 0 alone publishing the model. ``e2e.steps_per_s`` is the reference's own metric (optimizer.py:485-486, padded
   sequence steps incl. the wait for experience) summed over ranks; ``vs_baseline_e2e`` compares THAT with the
-  reference's ≈1000 steps/s, the like-for-like node-level comparison (``vs_baseline`` is the compute-only learner).
+  reference's ≈1000 steps/s, the like-for-like node-level comparison (``vs_baseline`` is the compute-only learner);
+* ``league_replay`` — BASELINE config 5 through the same node loop: PFSP self-play league (80 % of games on the
+  latest weights), the fp8 actor policy step, and learners sampling every minibatch from an on-HBM replay of
+  ``--league-replay-gb`` GB per GPU (``config.replay_capacity`` sequences).
 
 Knobs for rehearsing the multi-rank path on one GPU: ``DCA_DIST_BACKEND=gloo`` and ``DCA_SHARED_GPU=1`` (every rank
 on cuda:0).
@@ -89,6 +92,11 @@ def parse():
     ap.add_argument('--e2e-pack', type=int, default=1,
                     help='pack whole episodes into the learner sequences (episode-start resets in the recurrence) '
                          'instead of padding every rollout to seq_len (the reference layout: --e2e-pack 0)')
+    ap.add_argument('--league-replay-extra', type=float, default=15.0,
+                    help='seconds of the BASELINE config-5 node loop (extra field league_replay, 0 = off): PFSP '
+                         'self-play league on the fp8 actor policy step, learners sampling an on-HBM replay of '
+                         '--league-replay-gb GB per GPU')
+    ap.add_argument('--league-replay-gb', type=float, default=100.0)
     ap.add_argument('--e2e-transport', default='auto', choices=['auto', 'shm', 'tcp'],
                     help='node experience queue: shared-memory ring (auto on one node) or a TCP broker on rank 0')
     from dotaclient_amd.presets import parse_with_preset
@@ -316,6 +324,26 @@ def main():
         if any(errs) and 'error' not in e2e:
             e2e = {'error': f'failed on rank(s) {[i for i, x in enumerate(errs) if x]}'}
 
+    league_replay = None
+    if args.league_replay_extra > 0 and use_cuda and args.e2e_mode == 'process' and cfg.rnn == 'lstm':
+        # BASELINE config 5 (presets.py league-replay): the same node loop with a PFSP league of past versions
+        # (80 % of games on the latest weights), the fp8 actor policy step (actor/batched.py Fp8ActorPolicy) and an
+        # on-HBM replay of --league-replay-gb GB per learner (learner/replay.py) that every minibatch is sampled from
+        try:
+            from dotaclient_amd.learner.e2e import measure_e2e_node
+            progress('league-replay start')
+            league_replay = measure_e2e_node(
+                model=args.model, device=device, duration=args.league_replay_extra, games=args.e2e_games,
+                threads=args.e2e_threads, seq_len=args.seq_len, precision=args.precision, pack=bool(args.e2e_pack),
+                transport=args.e2e_transport, progress=progress, idle_probe=0.0, league='pfsp',
+                latest_weights_prob=0.8, actor_precision='fp8', replay_gb=args.league_replay_gb)
+        except Exception as e:
+            league_replay = {'error': repr(e)}
+        progress(f'league-replay done: {league_replay.get("error", "ok")}')
+        errs = gather('error' in league_replay)
+        if any(errs) and 'error' not in league_replay:
+            league_replay = {'error': f'failed on rank(s) {[i for i, x in enumerate(errs) if x]}'}
+
     shas = gather(weights_sha)
     hosts = gather(host)
     if rank == 0:
@@ -354,6 +382,7 @@ def main():
             'weights_sha16_per_rank': shas,
             'actor': actor,
             'e2e': e2e,
+            'league_replay': league_replay,
             'host_placement': hosts,
         }
         print(json.dumps(out), flush=True)

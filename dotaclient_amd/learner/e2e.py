@@ -172,7 +172,9 @@ def open_node_broker(addr: str, drop_oldest: bool = True):
 
 
 def _actor_process_main(addr: str, model: str, games: int, threads: int, seq_len: int, rollout_size: int,
-                        max_dota_time: float, device: str, seed: int, stop, ready, steps, failed, tag: str = 'a0'):
+                        max_dota_time: float, device: str, seed: int, stop, ready, steps, failed, tag: str = 'a0',
+                        league: Optional[str] = None, latest_weights_prob: float = 1.0,
+                        precision: str = 'bf16'):
     """Actor role of :func:`measure_e2e_node`: a process of its own (own interpreter and GIL) that plays ``games``
     VecActor games on its GPU, pushes whole-game rollouts into the node's experience queue and hot-swaps every model
     the learner's rank 0 publishes (reference agent.py:855-902 with the model subscription of 198-223). It tears its
@@ -190,9 +192,16 @@ def _actor_process_main(addr: str, model: str, games: int, threads: int, seq_len
             raise TimeoutError('no model published by the learner')
         ws.add_bytes(*m)
         br.subscribe_model(lambda v, b: ws.add_bytes(v, b), poll=0.005 if addr.startswith('shm://') else 0.25)
+        lg = None
+        if league:
+            # self-play league (reference agent.py:760-765 mini-league; PFSP opponents by default): the latest
+            # weights play the sampled opponent version with probability 1 - latest_weights_prob
+            from ..actor.league import League
+            lg = League(ws, mode=league)
         va = VecActor(ws, games, br.publish_experience, device=device, seed=seed, rollout_size=rollout_size,
                       max_dota_time=max_dota_time, hidden_stride=seq_len, threads=threads, stagger=True,
-                      tag=f'{tag}.vec')         # game ids unique across the node's actor processes
+                      tag=f'{tag}.vec', league=lg, latest_weights_prob=latest_weights_prob,
+                      precision=precision)      # (game ids unique across the node's actor processes)
         for _ in range(3):
             va.step()
         ready.set()
@@ -216,7 +225,9 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                      rollout_size: int = 9999, warmup_iterations: int = 2, max_iterations: Optional[int] = None,
                      log_dir: Optional[str] = None, prefetch: int = 32, ring_bytes: int = 1 << 26,
                      transport: str = 'auto', backend: str = 'auto', idle_probe: float = 3.0,
-                     report=None, record_consumed: int = 0, progress=None, pack: bool = False) -> Dict[str, float]:
+                     report=None, record_consumed: int = 0, progress=None, pack: bool = False,
+                     league: Optional[str] = None, latest_weights_prob: float = 1.0, actor_precision: str = 'bf16',
+                     replay_gb: float = 0.0) -> Dict[str, float]:
     """The reference's node topology end to end (optimizer.py:144-150, 274-287; ks-app/components/optimizer.jsonnet:
     79-174): ONE experience queue per node fed by actor processes, ``WORLD_SIZE`` learner ranks (one per GPU, DDP
     over RCCL) consuming disjoint rollouts from it as competing consumers, and rank 0 alone checkpointing and
@@ -231,7 +242,11 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
     Returns, on every rank, the node aggregate: ``steps_per_s`` (the reference's ``steps per s``, padded, summed
     over ranks), ``valid_steps_per_s``, ``actor_steps_per_s`` (sum), their per-rank lists, ``queue_dropped`` (ring
     drops during the window) and the per-rank stage times. ``report(opt) -> dict`` (tests) runs on every rank after
-    the window; the results are returned in rank order under ``reports``."""
+    the window; the results are returned in rank order under ``reports``.
+
+    BASELINE config 5 (``league='pfsp'``, ``actor_precision='fp8'``, ``replay_gb`` > 0): the actors play a PFSP
+    self-play league on the fp8 policy step and every learner trains from an on-HBM replay of ``replay_gb`` GB
+    (learner/replay.py) instead of the iteration's fresh rollouts only."""
     import multiprocessing as mp
     import os
     import torch.distributed as tdist
@@ -282,13 +297,15 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
         # waits for rank 0's model version 0
         proc = ctx.Process(target=_actor_process_main, name=f'e2e-actor-{rank}', daemon=True,
                            args=(addr, model, games, threads, seq_len, rollout_size, max_dota_time, str(device),
-                                 11 + 7919 * rank, stop, ready, steps, failed, f'a{rank}'))
+                                 11 + 7919 * rank, stop, ready, steps, failed, f'a{rank}', league,
+                                 latest_weights_prob, actor_precision))
         proc.start()
         cfg = OptimizerConfig(log_dir=tmp, epochs=epochs, seq_per_epoch=seq_per_epoch, batch_size=batch_size,
                               seq_len=seq_len, model=model, precision=precision, device=str(device),
                               backend=backend, checkpoint_keep=2, run_local=True, xp_timeout=120.0,
                               histogram_freq=10 ** 9, async_checkpoint=dev.type == 'cuda',
-                              prefetch_rollouts=prefetch, record_consumed=record_consumed, pack_sequences=pack)
+                              prefetch_rollouts=prefetch, record_consumed=record_consumed, pack_sequences=pack,
+                              replay_gb=replay_gb)
         opt = DotaOptimizer(cfg, broker, checkpoint=rank == 0)     # rank 0 publishes model version 0
         say(f'e2e: learner ready ({transport} broker {addr}); waiting for the actor process')
         if not ready.wait(timeout=900) or failed.is_set():
@@ -383,7 +400,11 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
     out['config'] = dict(batch_size=batch_size, seq_len=seq_len, seq_per_epoch=seq_per_epoch, epochs=epochs,
                          rollout_size=rollout_size, max_dota_time=max_dota_time, precision=precision,
                          prefetch_rollouts=prefetch, games_per_rank=games, pack_sequences=pack,
-                         actor=f'one process per rank over the node {transport} broker', learners=world)
+                         actor=f'one process per rank over the node {transport} broker', learners=world,
+                         league=league, latest_weights_prob=latest_weights_prob, actor_precision=actor_precision,
+                         replay_gb=replay_gb,
+                         replay_sequences=(len(opt.replay) if opt is not None and opt.replay is not None else 0),
+                         replay_capacity=(opt.replay.capacity if opt is not None and opt.replay is not None else 0))
     return out
 
 

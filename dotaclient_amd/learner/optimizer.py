@@ -213,9 +213,11 @@ class DotaOptimizer:
         if cfg.replay_capacity or cfg.replay_gb:
             from .replay import HbmReplay
             hid = self.policy_cfg.hidden if self.policy.is_recurrent else None
+            pk = bool(cfg.pack_sequences)             # packed sequences keep their episode-start flags in the ring
             cap = cfg.replay_capacity or HbmReplay.capacity_for_bytes(cfg.replay_gb * 1e9, cfg.seq_len,
-                                                                       self.policy_cfg.layout, hid)
-            self.replay = HbmReplay(cap, cfg.seq_len, self.policy_cfg.layout, hid, self.device, seed=cfg.seed)
+                                                                       self.policy_cfg.layout, hid, pk)
+            self.replay = HbmReplay(cap, cfg.seq_len, self.policy_cfg.layout, hid, self.device, seed=cfg.seed,
+                                    reset=pk)
             logger.info('on-device replay: %d sequences, %.2f GB', cap, self.replay.nbytes / 1e9)
         self.time_last_step = time.time()
         if self.iteration_start == 1:

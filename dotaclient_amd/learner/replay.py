@@ -25,7 +25,7 @@ from ..constants import UnitLayout
 _F32 = torch.float32
 
 
-def field_specs(S: int, layout: UnitLayout, hidden: Optional[int]):
+def field_specs(S: int, layout: UnitLayout, hidden: Optional[int], reset: bool = False):
     U = layout.max_units
     A = 21 + U
     spec = {
@@ -33,15 +33,17 @@ def field_specs(S: int, layout: UnitLayout, hidden: Optional[int]):
         'masks': ((S, A), torch.uint8), 'ret': ((S,), _F32), 'norm_ret': ((S,), _F32), 'adv': ((S,), _F32),
         'logp_old': ((S,), _F32), 'valid': ((S,), _F32),
     }
+    if reset:                       # sequence packing: episode-start flags (learner/ingest.py SequencePacker)
+        spec['reset'] = ((S,), torch.uint8)
     if hidden:
         spec['h0'] = ((hidden,), _F32)
         spec['c0'] = ((hidden,), _F32)
     return spec
 
 
-def bytes_per_sequence(S: int, layout: UnitLayout, hidden: Optional[int]) -> int:
+def bytes_per_sequence(S: int, layout: UnitLayout, hidden: Optional[int], reset: bool = False) -> int:
     n = 0
-    for shape, dt in field_specs(S, layout, hidden).values():
+    for shape, dt in field_specs(S, layout, hidden, reset).values():
         k = 1
         for d in shape:
             k *= d
@@ -50,13 +52,14 @@ def bytes_per_sequence(S: int, layout: UnitLayout, hidden: Optional[int]) -> int
 
 
 class HbmReplay:
-    def __init__(self, capacity: int, S: int, layout: UnitLayout, hidden: Optional[int], device, seed: int = 0):
+    def __init__(self, capacity: int, S: int, layout: UnitLayout, hidden: Optional[int], device, seed: int = 0,
+                 reset: bool = False):
         if capacity < 1:
             raise ValueError('replay capacity must be >= 1')
         self.capacity = int(capacity)
         self.S = S
         self.device = torch.device(device)
-        self.specs = field_specs(S, layout, hidden)
+        self.specs = field_specs(S, layout, hidden, reset)
         self.data = {k: torch.zeros((self.capacity,) + shape, dtype=dt, device=self.device)
                      for k, (shape, dt) in self.specs.items()}
         self.version = torch.full((self.capacity,), -1, dtype=torch.long, device=self.device)
@@ -70,8 +73,8 @@ class HbmReplay:
         self.host_sampling = False
 
     @staticmethod
-    def capacity_for_bytes(budget: float, S: int, layout: UnitLayout, hidden: Optional[int]) -> int:
-        return max(1, int(budget // bytes_per_sequence(S, layout, hidden)))
+    def capacity_for_bytes(budget: float, S: int, layout: UnitLayout, hidden: Optional[int], reset: bool = False) -> int:
+        return max(1, int(budget // bytes_per_sequence(S, layout, hidden, reset)))
 
     @property
     def nbytes(self) -> int:
@@ -92,6 +95,11 @@ class HbmReplay:
         if first < n:
             spans.append((0, first, n - first))
         for k, dst in self.data.items():
+            src = batch.get(k)
+            if src is None and k == 'reset':        # unpacked sequences: no episode starts inside
+                for d0, _, cnt in spans:
+                    dst[d0:d0 + cnt].zero_()
+                continue
             src = batch[k]
             if src.device.type == 'cpu' and self.device.type == 'cuda' and not src.is_pinned():
                 src = src.pin_memory()

@@ -469,6 +469,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     db = dw1 = db1 = dWt = dbt = dWe = dbe = None
     dgam = dbet = None
     first_attn = True
+    side_after: List = []                # side-stream work enqueued after the encoder backward (5v5 fused path)
     if attn:
         dWout = torch.empty(128, 128, device=dev)
         dbout = torch.empty(128, device=dev)
@@ -563,13 +564,14 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             dbout = torch.empty(128, device=dev)
             dbqkv = torch.empty(384, device=dev)
             if wg_side:
+                # enqueued AFTER the encoder backward below (side_after): issued here, the graph ran the two GEMMs
+                # (156 + 401 µs) and then the encoder backward strictly one after the other
                 sL.wait_stream(main)
-            with torch.cuda.stream(sL if wg_side else main):
+                side_after.append(lambda: (gemm_tn(dE1, Oat, out=dWout, colsum=dbout),
+                                           gemm_tn(dQKV, Xn, out=dWqkv, colsum=dbqkv)))
+            else:
                 dWout = gemm_tn(dE1, Oat, colsum=dbout)
                 dWqkv = gemm_tn(dQKV, Xn, colsum=dbqkv)
-                if wg_side:
-                    wg_done = torch.cuda.Event()
-                    wg_done.record(sL)
         elif attn32:
             # the two weight-gradient GEMMs over the N·U unit rows (∂W_out = ∂E1ᵀ·O, ∂W_qkv = ∂QKVᵀ·Xn, with their
             # bias column sums) run on the recurrence stream, off the ∂E1 → ∂O → attention → ∂Xn → LN → encoder
@@ -619,7 +621,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             return C.enc_small_grads(z[r0:r1], dtl[r0:r1], fp.type_offsets(dev), dx896, env_t[r0:r1], we, be,
                                      bool(cfg.compat_bugs))
         small = None
-        if wg_side:
+        if wg_side and not side_after:
             sL.wait_stream(main)
             with torch.cuda.stream(sL):
                 small = small_grads()
@@ -628,6 +630,15 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         dwt_c, dw1_c, db1_c = C.encoder_bwd(units_t[r0:r1], w1, b1, wtT16, dtl[r0:r1], z[r0:r1],
                                             dx896, arg[r0:r1], counts, bool(cfg.compat_bugs), demb_in=demb_in,
                                             exact=exact)
+        if side_after:
+            # the side stream already waits on the attention backward (not on the encoder backward just issued)
+            with torch.cuda.stream(sL):
+                for fn in side_after:
+                    fn()
+                small = small_grads()
+                wg_done = torch.cuda.Event()
+                wg_done.record(sL)
+            side_after.clear()
         dw1 = _acc(dw1, dw1_c)
         db1 = _acc(db1, db1_c)
         dWt = _acc(dWt, dwt_c)

@@ -45,6 +45,26 @@ def test_capacity_for_bytes_matches_allocation():
     assert r.nbytes == 3 * bytes_per_sequence(16, LAYOUT_1V1, 64)
 
 
+def test_replay_keeps_packed_episode_starts():
+    """Packed sequences (learner/ingest.py SequencePacker) keep their episode-start flags in the ring; unpacked
+    batches added to a packing ring get none; the time-major gather hands them to the step."""
+    from dotaclient_amd.learner.engine import Learner
+    S = 6
+    r = HbmReplay(4, S, LAYOUT_1V1, 64, 'cpu', reset=True)
+    assert r.nbytes == 4 * bytes_per_sequence(S, LAYOUT_1V1, 64, reset=True)
+    b = _batch(2, S, 1, hidden=64)
+    b['reset'] = torch.zeros(2, S, dtype=torch.uint8)
+    b['reset'][1, 3] = 1
+    r.add(b)
+    r.add(_batch(1, S, 2, hidden=64))                  # no flags: zero-filled
+    assert r.data['reset'][:3].sum().item() == 1 and r.data['reset'][1, 3].item() == 1
+    import types
+    out = Learner.gather_time_major(types.SimpleNamespace(STEP_FIELDS=Learner.STEP_FIELDS), r, torch.tensor([1, 2]), S)
+    rst = out['reset'].view(S, 2)                      # time-major rows t·B + b
+    assert rst[3, 0].item() == 1 and rst.sum().item() == 1
+    assert 'reset' not in HbmReplay(2, S, LAYOUT_1V1, 64, 'cpu').data
+
+
 def test_optimizer_trains_from_replay(tmp_path):
     import numpy as np
     from dotaclient_amd.learner.optimizer import DotaOptimizer, OptimizerConfig
