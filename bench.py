@@ -25,6 +25,8 @@ EVERY rank (one actor runtime per GPU), and reported as node aggregates (sums ov
   rank 0 alone publishing the model. ``e2e.steps_per_s`` is the reference's own metric (optimizer.py:485-486, padded
   sequence steps incl. the wait for experience) summed over ranks; ``vs_baseline_e2e`` compares THAT with the
   reference's ≈1000 steps/s, the like-for-like node-level comparison (``vs_baseline`` is the compute-only learner);
+* ``bptt350_learner`` — truncated BPTT: each sequence trained as ``seq_len / 350`` chains of 350 steps from
+  actor-stored (h, c) (bf16x3 operands — the exact recurrence takes ≤ 8 sequences per step; not the headline);
 * ``league_replay`` — BASELINE config 5 through the same node loop: PFSP self-play league (80 % of games on the
   latest weights), the fp8 actor policy step, and learners sampling every minibatch from an on-HBM replay of
   ``--league-replay-gb`` GB per GPU (``config.replay_capacity`` sequences).
@@ -68,6 +70,9 @@ def parse():
     ap.add_argument('--model-5v5-extra', type=int, default=1,
                     help='also time the 5v5 entity-attention policy (BASELINE config 4) at the same B, S (bf16x3 '
                          'operands: the attention kernels have no exact-fp32 variant)')
+    ap.add_argument('--bptt350-extra', type=int, default=1,
+                    help='also time truncated BPTT: each sequence as seq_len/350 chains of 350 steps from stored '
+                         '(h, c) (extra field bptt350_learner, bf16x3 operands; not the headline)')
     ap.add_argument('--replay', type=int, default=0, help='sequences in the on-HBM replay pool (0 = 4x batch)')
     ap.add_argument('--graph', type=int, default=-1, help='capture the step in a hipGraph (-1 = auto)')
     ap.add_argument('--actor', type=int, default=1, help='also measure actor steps/s (untimed region)')
@@ -142,9 +147,12 @@ def main():
         progress('5v5 entity attention has no exact-fp32 kernels: timing it at fp32 with bf16x3 operands')
         args.precision = 'fp32'
 
-    def run(precision, cfg=cfg):
-        """Build a learner of this precision and time ``args.steps`` DP PPO steps after ``args.warmup``; returns
-        (elapsed s (max over ranks), loss_first, loss_last, learner, policy)."""
+    def run(precision, cfg=cfg, B=None, S=None):
+        """Build a learner of this precision and time ``args.steps`` DP PPO steps (``B`` sequences of ``S`` steps,
+        default the command line's) after ``args.warmup``; returns (elapsed s (max over ranks), loss_first,
+        loss_last, learner, policy)."""
+        B = B or args.batch_size
+        S = S or args.seq_len
         torch.manual_seed(7 + rank)
         policy = Policy(cfg)
         backend = args.backend
@@ -153,14 +161,14 @@ def main():
         learner = Learner(policy, LossConfig(algo=args.algo), device=device, backend=backend, precision=precision)
         if args.graph == 1 or (args.graph == -1 and learner.backend == 'fused'):
             learner.enable_graph(warmup=1)
-        n_pool = args.replay or 4 * args.batch_size
-        replay = DeviceReplay(n_pool, args.seq_len, cfg.layout, cfg.hidden if cfg.rnn == 'lstm' else None, device,
+        n_pool = args.replay or 4 * B
+        replay = DeviceReplay(n_pool, S, cfg.layout, cfg.hidden if cfg.rnn == 'lstm' else None, device,
                               seed=1000 * rank)
 
         def step():
             t = time.perf_counter()
             # on-device minibatch gather from the HBM replay pool (part of the captured step on the fused path)
-            out = learner.train_step_replay(replay.buf, args.batch_size)
+            out = learner.train_step_replay(replay.buf, B)
             if trace:
                 torch.cuda.synchronize()
                 print(f'[bench] {precision} step {learner.n_steps} {1e3 * (time.perf_counter() - t):.2f} ms loss '
@@ -234,6 +242,24 @@ def main():
                          'ms_per_step': e5 / args.steps * 1e3, 'loss_first': l50, 'loss_last': l51}
         except Exception as e:
             model_5v5 = {'error': repr(e)}
+
+    bptt = None
+    if (args.bptt350_extra and use_cuda and cfg.rnn == 'lstm' and not cfg.entity_attention
+            and args.seq_len % 350 == 0 and args.seq_len > 350):
+        # truncated BPTT (SURVEY §5 long-context row): every seq_len-step sequence trained as seq_len/350
+        # independent 350-step chains that start from the (h, c) the actor stored every 350 steps (replay h0 / c0),
+        # 4x fewer serial recurrence steps. More than 8 sequences per step run on the bf16x3 team kernel (several rows
+        # per chain), so this extra is fp32 with bf16x3 operands — never the headline
+        learner = None
+        k = args.seq_len // 350
+        try:
+            eb, lb0, lb1, _, _ = run('fp32', B=args.batch_size * k, S=350)
+            progress(f'learner bptt350 done: {eb / args.steps * 1e3:.3f} ms/step')
+            bptt = {'precision': 'fp32 activations / bf16x3-split MFMA operands', 'chains_per_sequence': k,
+                    'batch': args.batch_size * k, 'seq_len': 350, 'value': samples / eb,
+                    'ms_per_step': eb / args.steps * 1e3, 'loss_first': lb0, 'loss_last': lb1}
+        except Exception as e:
+            bptt = {'error': repr(e)}
 
     def gather(x):
         """Every rank's value of ``x`` on every rank (rank order)."""
@@ -378,6 +404,7 @@ def main():
             'loss_first': loss_val, 'loss_last': final_loss,
             'fp32_bf16x3_learner': bf16x3,
             'model_5v5': model_5v5,
+            'bptt350_learner': bptt,
             'dp_replicas_identical': len(set(shas)) == 1,
             'weights_sha16_per_rank': shas,
             'actor': actor,

@@ -360,10 +360,11 @@ def fp8_weight(w: torch.Tensor):
 
 
 class Fp8ActorPolicy(GpuActorPolicy):
-    """:class:`GpuActorPolicy` with the pre-RNN layer, the LSTM step and the heads as ONE hand-written e4m3 MFMA
-    kernel (ops/csrc/actor_fp8.hip; BASELINE config 5, fp8 actor inference): weights quantised per output channel
-    at (hot-)load time, activations per row inside the kernel. The entity encoder (bf16 MFMA kernel) and the
-    sampling kernel are shared with the bf16 step.
+    """:class:`GpuActorPolicy` with the policy's GEMMs on hand-written e4m3 MFMA kernels (ops/csrc/actor_fp8.hip;
+    BASELINE config 5, fp8 actor inference): the entity encoder's unit-type GEMMs (``encoder_fp8``, one 16x16x128
+    f8f6f4 MFMA per output tile) and, in one more launch, the pre-RNN layer, the LSTM step and the heads
+    (``actor_fp8``). Weights are quantised per output channel at (hot-)load time, activations per row (per (row, unit)
+    in the encoder) inside the kernels. The sampling kernel is shared with the bf16 step.
 
     Compact staging: unit features cross PCIe as fp16 and unit handles as int32 (3.3 + 0.7 MB per 4096-slot step
     instead of 6.6 + 1.3 MB — the copies were 57 % of the bf16 step), widened on the GPU inside the captured graph.
@@ -398,19 +399,33 @@ class Fp8ActorPolicy(GpuActorPolicy):
         w['wg8'], w['sg'] = fp8_weight(wcat.contiguous())
         w['bg'] = (g('rnn.bias_ih_l0') + g('rnn.bias_hh_l0'))[perm].contiguous()
         w['wh8'], w['sh8'] = fp8_weight(w['wh32'])
-        for k in ('wcatT', 'brnn', 'whT', 'wpreT', 'bpre16'):   # the bf16 step's operands are not used here
+        # the encoder's six unit-type weights (128 out × 128 in each), per-channel e4m3 in fragment order
+        wt = [fp8_weight(g(f'affine_unit_{s}.weight')) for s in TYPE_SUFFIX]
+        w['wt8'] = torch.cat([q for q, _ in wt]).contiguous()
+        w['st8'] = torch.stack([s_ for _, s_ in wt]).contiguous()
+        for k in ('wcatT', 'brnn', 'whT', 'wpreT', 'bpre16', 'wt16'):   # the bf16 step's operands are not used here
             w.pop(k, None)
         return w
 
     def _widen(self):
-        if self.compact:   # fp16 features → fp32, int32 handles → int64 in ONE hand-written launch (ops/csrc/actor.hip)
-            self.C.actor_widen(self.in_pack.dev['units'], self.d_units, self.in_pack.dev['handles'], self.d_handles)
+        if self.compact:   # int32 handles → int64 for the sampler (the fp8 encoder reads the fp16 features as they are)
+            e = self._no_units
+            self.C.actor_widen(e[0], e[1], self.in_pack.dev['handles'], self.d_handles)
+
+    @property
+    def _no_units(self):
+        e = self.__dict__.get('_empty_units')
+        if e is None:
+            e = self._empty_units = (torch.empty(0, dtype=torch.float16, device=self.device),
+                                     torch.empty(0, dtype=torch.float32, device=self.device))
+        return e
 
     def _forward(self):
-        """Captured body, 4 launches: encoder → fp8 core (pre-RNN, gates + cell, heads) → sampling → RNG counter."""
+        """Captured body, 4 launches: fp8 encoder → fp8 core (pre-RNN, gates + cell, heads) → sampling → RNG counter."""
         C, w, cfg = self.C, self.w, self.cfg
-        x896, emb, _ = C.encoder_fwd(self.d_units, self.d_env, w['w1'], w['b1'], w['wt16'], w['bt'], w['we'],
-                                     w['be'], list(cfg.layout.counts), bool(cfg.compat_bugs))
+        units = self.in_pack.dev['units'] if self.compact else self.d_units    # fp16 staging read directly
+        x896, emb = C.encoder_fp8(units, self.d_env, w['w1'], w['b1'], w['wt8'], w['st8'], w['bt'], w['we'],
+                                  w['be'], list(cfg.layout.counts))
         if cfg.compat_bugs:
             x896[:, 768:896] = x896[:, 512:640]
         C.actor_fp8(x896, w['wpre8'], w['spre'], w['bpre32'], w['wg8'], w['sg'], w['bg'], w['wh8'], w['sh8'],

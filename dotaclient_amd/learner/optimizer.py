@@ -179,6 +179,12 @@ class DotaOptimizer:
         if prec == 'fp32-exact' and self.policy_cfg.entity_attention:
             logger.info('5v5 entity attention has no exact-fp32 kernels: training at fp32 with bf16x3 operands')
             prec = 'fp32'
+        if prec == 'fp32-exact' and self.device.type == 'cuda' and cfg.batch_size > 8:
+            # the exact VALU recurrence runs one sequence per XCD team (8 teams); larger minibatches pack several
+            # rows per chain on the bf16x3 MFMA team kernel
+            logger.info('fp32-exact takes at most 8 sequences per minibatch and GPU: training at fp32 with bf16x3 '
+                        'operands (batch_size %d)', cfg.batch_size)
+            prec = 'fp32'
         self.learner = Learner(self.policy, lc, device=self.device, backend=cfg.backend, precision=prec)
         if cfg.graph:
             self.learner.enable_graph(warmup=1)

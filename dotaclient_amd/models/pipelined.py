@@ -276,6 +276,10 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     Returns (partials (R,16) f32, logp (N) f32 time-major, grads {param name → tensor})."""
     from ..ops.gemm import gemm_tn as _gemm_tn
     exact = bool(getattr(fp, 'exact', False))
+    if exact and B > 8:
+        # lstm_team.hip plan(): up to 8 sequences run as one-row chains (one XCD team each) on the exact fp32 VALU
+        # recurrence; more pack several rows per chain on the bf16x3 MFMA team kernel — not IEEE fp32
+        raise ValueError(f'fp32-exact: at most 8 sequences per step and GPU (got {B}); use precision fp32')
 
     def gemm_tn(*a, **k):
         # weight gradients: split-K MFMA; IEEE-fp32 learner: exact v_mfma_f32_16x16x4_f32 (ops/csrc/gemm_tn.hip)

@@ -25,6 +25,7 @@
 // the stream was latency-bound); the LSTM cell works on c staged in LDS so no global access sits inside the
 // stream, and h / c leave in one coalesced pass.
 #include "common.h"
+#include <hip/hip_fp16.h>
 
 namespace {
 
@@ -351,6 +352,213 @@ __global__ __launch_bounds__(NT) void actor_fp8_kernel(Fp8Args A) {
       });
 }
 
+
+// =============================================================================================================
+// fp8 entity encoder of the actor step (BASELINE config 5: the unit-type GEMMs, ≈63 % of the policy's FLOPs, on e4m3
+// MFMA). Per slot row and unit u of type τ:
+//   basic = relu(W1·u + b1)                 (128, fp32 VALU; K = 10 — W1 rows of the thread's 8 outputs in VGPRs)
+//   emb   = (q(basic)·q(W_τ)ᵀ)·s_row·s_col + b_τ   (one v_mfma_scale_f32_16x16x128_f8f6f4 per 16×16 tile: K = 128
+//                                                    is exactly one MFMA step) → bf16 (the sampling kernel's input)
+//   x896[:, 128 + 128τ + j] = max over the type's units of emb[:, u, j]       (pools, bf16: the fp8 core's input)
+//   x896[:, 0:128] = relu(W_env·env + b_env)
+// Quantisation as in the core: basic per (row, unit) — its max maps to 448 —, W_τ per output channel at hot-swap
+// time (fragment order, actor/batched.py fp8_weight). One 256-thread workgroup per 16 slots: the 16 rows' unit
+// features (contiguous, fp16 from the compact staging or fp32) land in LDS once; per unit, every thread computes 8
+// basic values of one row and quantises them into a double-buffered fp8 A image (one barrier per unit), then wave w
+// runs the MFMAs of output tiles 2w, 2w+1 and keeps the running pool maxima in registers. Replaces the widen kernel
+// (fp16 units are read as they are) and the bf16 encoder.
+// buffer resource over [p, p + bytes) (wave-uniform; out-of-range accesses read 0 / are dropped)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, long long bytes) {
+  const unsigned long long ad = (unsigned long long)p;
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)ad);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(ad >> 32));
+  const int nb = (int)(bytes > 0x7fff0000LL ? 0x7fff0000LL : bytes);
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((unsigned long long)hi << 32) | lo), (short)0,
+                                           __builtin_amdgcn_readfirstlane(nb), 0x00020000);
+}
+
+struct EncFp8Args {
+  const void* units;                     // (N, U, 10) fp16 or fp32
+  const float* env;                      // (N, 3)
+  const float* w1; const float* b1;      // (128, 10), (128)
+  const i32x8* wt; const float* st; const float* bt;   // (6, 128, 128) e4m3 fragment order, (6, 128), (6, 128)
+  const float* we; const float* be;      // (128, 3), (128)
+  short* x896;                           // (N, 896) bf16
+  short* emb;                            // (N, U, 128) bf16
+  int N, U;
+  int off[7];                            // type τ owns units off[τ] .. off[τ+1]-1
+  int njob;                              // unit jobs per row block (blockIdx.y): whole types, balanced by units
+  int nu[3];                             // units of job j, in increasing order (a type's units stay contiguous)
+  unsigned char ul[3][64];
+};
+constexpr int EBR = 16, ENT = 256, EMAXU = 64;
+
+// max over the 16 lanes of a DPP row (row_ror 8, 4, 2, 1: register-to-register, no LDS round trip)
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x128, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x122, 0xF, 0xF, false)));
+  v = fmaxf(v, __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x121, 0xF, 0xF, false)));
+  return v;
+}
+
+template <bool F16>
+__global__ __launch_bounds__(ENT) void encoder_fp8_kernel(EncFp8Args a) {
+  __shared__ __attribute__((aligned(16))) unsigned us[EBR * EMAXU * 10];   // the 16 rows' unit features, raw bytes
+  __shared__ __attribute__((aligned(16))) unsigned char aimg[2][EBR * 128];  // fp8 basic tile, double-buffered
+  __shared__ float rsc[2][EBR];                                             // its row scales
+  constexpr int EP = 128 + 8;                                               // emb tile pitch (bf16)
+  __shared__ __attribute__((aligned(16))) short etile[2][EBR * EP];          // a unit's emb tile, bf16
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r0 = blockIdx.x * EBR, N = a.N, U = a.U, job = blockIdx.y;
+  const int nrows = min(EBR, N - r0);
+  {   // unit features → LDS as they are (fp16 / fp32 bytes) by LDS-DMA: every load in flight at once, one drain
+      // (a convert-per-element loop waited out one memory round trip per element: most of a first version's time).
+      // Rows past N read the last valid dword; their outputs are never stored.
+    typedef __attribute__((address_space(1))) void gvoid;
+    typedef __attribute__((address_space(3))) void lvoid;
+    constexpr int ES = F16 ? 2 : 4;
+    const int nd = nrows * U * 10 * ES / 4, total = EBR * U * 10 * ES / 4;    // dwords (U·10 is even)
+    const unsigned* src = reinterpret_cast<const unsigned*>(static_cast<const char*>(a.units) +
+                                                            (size_t)r0 * U * 10 * ES);
+    for (int q0 = 64 * w; q0 < total; q0 += ENT)
+      __builtin_amdgcn_global_load_lds((gvoid*)(src + min(q0 + lane, nd - 1)), (lvoid*)(us + q0), 4, 0, 0);
+  }
+  const int m = tid >> 4, kc = tid & 15;          // phase 1: row m, outputs 8kc … 8kc+7
+  if (job == 0) {   // env embedding (job 0 of the row block): row m, 8 columns
+    const int row = r0 + m;
+    if (row < N) {
+      const float e0 = a.env[row * 3], e1 = a.env[row * 3 + 1], e2 = a.env[row * 3 + 2];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = 8 * kc + j;
+        a.x896[(size_t)row * 896 + c] = dca::f2bf(fmaxf(a.be[c] + a.we[c * 3] * e0 + a.we[c * 3 + 1] * e1 +
+                                                        a.we[c * 3 + 2] * e2, 0.f));
+      }
+    }
+  }
+  float w1r[8][10], b1r[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    b1r[j] = a.b1[8 * kc + j];
+#pragma unroll
+    for (int f = 0; f < 10; ++f) w1r[j][f] = a.w1[(8 * kc + j) * 10 + f];
+  }
+  f32x4 pm[2];
+  // this wave's two weight fragments of the NEXT unit's type, loaded one unit ahead (an L2 round trip per unit
+  // right before its MFMAs was most of the kernel's time: 69 µs for 4096 slots)
+  auto type_of = [&](int uu) {
+    int t = 0;
+#pragma unroll
+    for (int k = 1; k < 6; ++k) t += uu >= a.off[k] ? 1 : 0;
+    return t;
+  };
+  // Per unit, this wave's two weight fragments of the unit's type (and the lane's columns' dequant scales / biases)
+  // are loaded ONE UNIT AHEAD into the other of two register sets (the loop is unrolled by two, so the sets
+  // alternate without a copy; an L2 round trip right before each unit's MFMAs was most of a first version's time,
+  // 69 µs for 4096 slots).
+  struct WSet {
+    i32x8 w[2];
+    float sw[2], bb[2];
+  };
+  auto fetch = [&](WSet& S, int tn) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int tile = 2 * w + t, col = 16 * tile + (lane & 15);
+      S.w[t] = a.wt[((size_t)tn * 8 + tile) * 64 + lane];
+      S.sw[t] = a.st[tn * 128 + col];
+      S.bb[t] = a.bt[tn * 128 + col];
+    }
+  };
+  // a unit's 16 × 128 bf16 emb tile leaves through LDS as 16-byte stores (one per thread) after the NEXT unit's
+  // barrier — 2-byte C-layout stores straight from the MFMA epilogue were most of the kernel's time (53 µs)
+  const int srow = tid >> 4, sch = tid & 15;      // store phase: row, 16-byte chunk (8 columns)
+  auto flush = [&](int u, int buf) {
+    if (r0 + srow < N)
+      *reinterpret_cast<uint4*>(a.emb + ((size_t)(r0 + srow) * U + u) * 128 + 8 * sch) =
+          *reinterpret_cast<const uint4*>(etile[buf] + srow * EP + 8 * sch);
+  };
+  int prev_u = -1;
+  auto unit = [&](int u, int buf, const WSet& S) {
+    {   // ---- phase 1: basic of (row m, unit u), 8 outputs → e4m3 with the row's scale
+      float x[10];
+      if constexpr (F16) {
+        const __half2* xp = reinterpret_cast<const __half2*>(us) + (m * U + u) * 5;
+#pragma unroll
+        for (int f = 0; f < 5; ++f) {
+          const float2 t2 = __half22float2(xp[f]);
+          x[2 * f] = t2.x;
+          x[2 * f + 1] = t2.y;
+        }
+      } else {
+        const float* xp = reinterpret_cast<const float*>(us) + (m * U + u) * 10;
+#pragma unroll
+        for (int f = 0; f < 10; ++f) x[f] = xp[f];
+      }
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        float sacc = b1r[j];
+#pragma unroll
+        for (int f = 0; f < 10; ++f) sacc = fmaf(w1r[j][f], x[f], sacc);
+        v[j] = fmaxf(sacc, 0.f);
+      }
+      float am = fmaxf(fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])), fmaxf(fmaxf(v[4], v[5]), fmaxf(v[6], v[7])));
+      am = row16_max(am);                        // the row's 16 threads (one DPP row)
+      const float sc = am > 0.f ? am / kQmax : 1.f, inv = am > 0.f ? kQmax / am : 1.f;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] *= inv;
+      *reinterpret_cast<long long*>(aimg[buf] + m * 128 + 8 * kc) = pack8(v);
+      if (kc == 0) rsc[buf][m] = sc;
+    }
+    __syncthreads();   // A image of unit u complete (and every wave is past unit u-1's reads of the other buffer)
+    if (prev_u >= 0) flush(prev_u, buf ^ 1);       // the previous unit's emb tile (written before this barrier)
+    prev_u = u;
+    {   // ---- phase 2: wave w → output tiles 2w, 2w + 1
+      const int tau = type_of(u);
+      const bool first = u == a.off[tau], last = u == a.off[tau + 1] - 1;
+      const i32x8 af = afrag128(aimg[buf], 128, 0, lane);
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const int tile = 2 * w + t, col = 16 * tile + (lane & 15);
+        const f32x4 c = mma128(af, S.w[t], f32x4{0.f, 0.f, 0.f, 0.f});
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = 4 * (lane >> 4) + r;
+          const float e = c[r] * rsc[buf][row] * S.sw[t] + S.bb[t];
+          pm[t][r] = first ? e : fmaxf(pm[t][r], e);
+          etile[buf][row * EP + col] = dca::f2bf(e);
+        }
+        if (last) {                                // (uniform) the type's pool → x896
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int row = 4 * (lane >> 4) + r;
+            if (r0 + row < N) a.x896[(size_t)(r0 + row) * 896 + 128 + 128 * tau + col] = dca::f2bf(pm[t][r]);
+          }
+        }
+      }
+    }
+  };
+  // this workgroup's units: the whole types of job `job` (several workgroups per row block shorten the serial
+  // per-unit chain and let 2-3 workgroups share a CU; one type's units keep their order for the running pool)
+  const int nu = a.nu[job];
+  const unsigned char* ul = a.ul[job];
+  WSet A, B;
+  fetch(A, type_of(ul[0]));
+  __builtin_amdgcn_s_waitcnt(0);                  // W1 / first fragments landed: no first-iteration waits in the loop
+  __syncthreads();                                // unit features staged
+  for (int i = 0; i < nu; i += 2) {
+    fetch(B, type_of(ul[min(i + 1, nu - 1)]));
+    unit(ul[i], i & 1, A);
+    if (i + 1 < nu) {                             // (uniform)
+      fetch(A, type_of(ul[min(i + 2, nu - 1)]));
+      unit(ul[i + 1], (i + 1) & 1, B);
+    }
+  }
+  __syncthreads();
+  flush(prev_u, (nu - 1) & 1);                    // the last unit's tile
+}
+
 }  // namespace
 
 // x896 (n,896) bf16; weights fragment-ordered fp8 (see actor/batched.py fp8_weight) with fp32 per-channel scales and
@@ -364,5 +572,48 @@ extern "C" hipError_t dca_actor_fp8(const short* x896, const void* wpre, const f
   Fp8Args a{x896, reinterpret_cast<const i32x8*>(wpre), spre, bpre, reinterpret_cast<const i32x8*>(wg), sg, bg,
             reinterpret_cast<const i32x8*>(wh), sh, bh, h, c, keep, active, z, n};
   hipLaunchKernelGGL(actor_fp8_kernel, dim3((n + BM - 1) / BM), dim3(NT), 0, stream, a);
+  return hipGetLastError();
+}
+
+// fp8 entity encoder (actor step): units (N, U, 10) fp16 (f16 = 1) or fp32, env (N, 3); W1 (128, 10), b1; W_τ as
+// (6, 128, 128) e4m3 fragment-ordered bytes with per-channel scales st (6, 128) and biases bt (6, 128); W_env (128, 3),
+// b_env. Writes x896 (N, 896) bf16 (env embedding + the six pools) and emb (N, U, 128) bf16. counts: units per type.
+extern "C" hipError_t dca_encoder_fp8(const void* units, int f16, const float* env, const float* w1, const float* b1,
+                                      const void* wt, const float* st, const float* bt, const float* we,
+                                      const float* be, short* x896, short* emb, int N, int U, const int* counts,
+                                      hipStream_t stream) {
+  if (N < 1) return hipSuccess;
+  if (U < 1 || U > EMAXU) return hipErrorInvalidValue;
+  EncFp8Args a{units, env, w1, b1, reinterpret_cast<const i32x8*>(wt), st, bt, we, be, x896, emb, N, U, {}};
+  int acc = 0;
+  for (int t = 0; t < 6; ++t) {
+    a.off[t] = acc;
+    acc += counts[t];
+    if (counts[t] < 1) return hipErrorInvalidValue;   // every type owns ≥ 1 unit slot (pools have no empty case)
+  }
+  a.off[6] = acc;
+  if (acc != U) return hipErrorInvalidValue;
+  // types → 3 jobs, largest first into the lightest job (1v1: {16}, {16}, {1, 5, 1, 1})
+  int order[6] = {0, 1, 2, 3, 4, 5};
+  for (int i = 0; i < 6; ++i)
+    for (int j = i + 1; j < 6; ++j)
+      if (counts[order[j]] > counts[order[i]]) { const int t = order[i]; order[i] = order[j]; order[j] = t; }
+  int load[3] = {0, 0, 0}, owner[6];
+  for (int i = 0; i < 6; ++i) {
+    int b = 0;
+    for (int j = 1; j < 3; ++j) if (load[j] < load[b]) b = j;
+    owner[order[i]] = b;
+    load[b] += counts[order[i]];
+  }
+  a.njob = 0;
+  int remap[3] = {-1, -1, -1};
+  for (int t = 0; t < 6; ++t) {                   // job ids in order of their first type; units in increasing order
+    int& jb = remap[owner[t]];
+    if (jb < 0) { jb = a.njob++; a.nu[jb] = 0; }
+    for (int u = a.off[t]; u < a.off[t + 1]; ++u) a.ul[jb][a.nu[jb]++] = (unsigned char)u;
+  }
+  const dim3 grid((N + EBR - 1) / EBR, a.njob);
+  if (f16) hipLaunchKernelGGL(encoder_fp8_kernel<true>, grid, dim3(ENT), 0, stream, a);
+  else hipLaunchKernelGGL(encoder_fp8_kernel<false>, grid, dim3(ENT), 0, stream, a);
   return hipGetLastError();
 }

@@ -453,6 +453,38 @@ void actor_fp8(torch::Tensor x896, torch::Tensor wpre, torch::Tensor spre, torch
             "dca_actor_fp8");
 }
 
+// fp8 entity encoder of the actor step (actor_fp8.hip): units (N, U, 10) fp16 or fp32, env (N, 3) → x896 (N, 896) bf16
+// (env embedding + pools) and emb (N, U, 128) bf16. W_τ: (6 × 128 × 128) e4m3 bytes in fragment order (fp8_weight per
+// type) with per-channel scales st (6, 128); bt (6, 128).
+std::vector<torch::Tensor> encoder_fp8(torch::Tensor units, torch::Tensor env, torch::Tensor w1, torch::Tensor b1,
+                                       torch::Tensor wt, torch::Tensor st, torch::Tensor bt, torch::Tensor we,
+                                       torch::Tensor be, std::vector<int64_t> counts) {
+  CHECK_DEV(units); CHECK_CONTIG(units); CHECK_F32(env); CHECK_F32(w1); CHECK_F32(b1); CHECK_U8(wt);
+  CHECK_F32(st); CHECK_F32(bt); CHECK_F32(we); CHECK_F32(be);
+  const bool f16 = units.scalar_type() == at::kHalf;
+  TORCH_CHECK(f16 || units.scalar_type() == at::kFloat, "encoder_fp8: units fp16 or fp32");
+  TORCH_CHECK(units.dim() == 3 && units.size(2) == 10, "encoder_fp8: units (N, U, 10)");
+  const int N = units.size(0), U = units.size(1);
+  TORCH_CHECK(env.dim() == 2 && env.size(0) == N && env.size(1) == 3, "encoder_fp8: env (N, 3)");
+  TORCH_CHECK(w1.numel() == 128 * 10 && b1.numel() == 128 && we.numel() == 128 * 3 && be.numel() == 128,
+              "encoder_fp8: W1 (128, 10), W_env (128, 3)");
+  TORCH_CHECK(wt.numel() == 6 * 128 * 128 && st.numel() == 6 * 128 && bt.numel() == 6 * 128,
+              "encoder_fp8: W_τ (6, 128, 128) e4m3, scales / biases (6, 128)");
+  TORCH_CHECK(counts.size() == 6, "encoder_fp8: six unit counts");
+  int c[6];
+  int64_t tot = 0;
+  for (int i = 0; i < 6; ++i) { c[i] = (int)counts[i]; tot += counts[i]; }
+  TORCH_CHECK(tot == U && U <= 64, "encoder_fp8: counts must sum to U <= 64");
+  auto o = env.options();
+  auto x896 = torch::empty({N, 896}, o.dtype(at::kBFloat16));
+  auto emb = torch::empty({N, U, 128}, o.dtype(at::kBFloat16));
+  hip_check(dca_encoder_fp8(units.data_ptr(), f16 ? 1 : 0, ptr<float>(env), ptr<float>(w1), ptr<float>(b1),
+                            wt.data_ptr(), ptr<float>(st), ptr<float>(bt), ptr<float>(we), ptr<float>(be),
+                            ptr<short>(x896), ptr<short>(emb), N, U, c, cur_stream()),
+            "dca_encoder_fp8");
+  return {x896, emb};
+}
+
 // Fused fp32 entity-attention block forward (attn_block.hip): e0 = E0' (N·64, 128) → xn, mean, rstd, qkv (no bias), o,
 // lse, e1 (all for the backward / heads), and the pools into x896[:, 128:896] + arg (N, 6, 128). Weights: bf16 hi / lo
 // images of W_qkv (384, 128) and W_out (128, 128) (split_bf16x2), bq (384).
@@ -1140,6 +1172,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("actor_state_prep", &actor_state_prep, "actor step: state resets + [x | bf16(h)] gate-GEMM operand");
   m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)", py::arg("gates"),
         py::arg("h"), py::arg("c"), py::arg("h16"), py::arg("active") = py::none());
+  m.def("encoder_fp8", &encoder_fp8, "fp8 (e4m3) entity encoder of the actor step: unit MLP, per-type GEMMs, pools");
   m.def("actor_fp8", &actor_fp8, "fp8 (e4m3) actor policy core: pre-RNN + LSTM step + heads from x896",
         py::arg("x896"), py::arg("wpre"), py::arg("spre"), py::arg("bpre"), py::arg("wg"), py::arg("sg"), py::arg("bg"),
         py::arg("wh"), py::arg("sh"), py::arg("bh"), py::arg("h"), py::arg("c"), py::arg("keep"), py::arg("z"),

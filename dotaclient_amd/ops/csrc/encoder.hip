@@ -647,9 +647,15 @@ __device__ __forceinline__ float fb_stage_load(const FbParams& P, int k, int cnt
   const int U = P.L.U, N = P.N;
   const int rb = k / cnt, u = k - rb * cnt, row0 = 16 * rb;
   const int idx = 64 * min(wv, 2) + lane;
-  if (idx < 16 * kF) return P.units[((size_t)min(row0 + idx / kF, N - 1) * U + uoff + u) * kF + idx % kF];
-  const int row = min(row0 + min(idx - 16 * kF, 15), N - 1);
-  return P.dtl ? P.dtl[(size_t)row * U + uoff + u] : 0.f;
+  // one load per lane, address selected (two loads under divergent branches wrote the same register: the second
+  // had to wait for the first, a full memory round trip in the item loop)
+  const bool isu = idx < 16 * kF;
+  const int row = isu ? min(row0 + idx / kF, N - 1) : min(row0 + min(idx - 16 * kF, 15), N - 1);
+  // (no dtl — the given-∂emb variant, which never reads the dtl slots: any valid address; no select on the loaded
+  // value either, which would make the wave wait for the load right here)
+  const float* src = isu ? P.units + ((size_t)row * U + uoff + u) * kF + idx % kF
+                         : (P.dtl ? P.dtl + (size_t)row * U + uoff + u : P.units);
+  return *src;
 }
 
 // ∂emb e-tile wv of item k (C layout) → hi / lo image
@@ -1208,20 +1214,33 @@ __global__ __launch_bounds__(512, 1) void encoder_bwd_x_kernel(FbParams P) {
   lds_barrier();
   xb_build(bn, stg[k0 % 3], k0 % cnt, img[0], imt[0], wv, lane);
   fb_load_build<false, COMPAT>(bn, R, P.ldq, min(k0 + 1, kl), min(k0 + 1, kl) % cnt == 0, cnt, uoff, U, tau, wv, i, kg);
+  // layer-1 operands of the next item (units[row i][4cc + kg] incl. the bias slot, and units[row 4kg + r][f = i]
+  // for ∂W1) are read from the staging slot one iteration ahead into registers: the item's first MFMAs then wait
+  // on no LDS read (read after the A fragments, they made the wave wait for ALL of the item's LDS reads first)
+  float l1n[3], ubn[4];
+  auto l1_read = [&](const float* sl) {
+#pragma unroll
+    for (int cc = 0; cc < 3; ++cc) {
+      const int f = 4 * cc + kg;
+      l1n[cc] = f < kF ? sl[i * kF + f] : (f == kF ? 1.f : 0.f);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ubn[r] = i < kF ? sl[(4 * kg + r) * kF + i] : 0.f;
+  };
+  l1_read(stg[k0 % 3]);
   int buf = 0;
   for (int k = k0; k < k1; ++k) {
     lds_barrier();
-    const float* sl = stg[k % 3];
     float a[32];
     x_afrags(img[buf], i, kg, a);                 // ∂emb[row i][e], e = 32s + 8kg + jj
+    const float ub[4] = {ubn[0], ubn[1], ubn[2], ubn[3]};   // units[row 4kg + r][f = i] (f ≥ 10: 0)
+    f32x4 bas = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int cc = 0; cc < 3; ++cc) bas = __builtin_amdgcn_mfma_f32_16x16x4f32(l1n[cc], w1x[cc], bas, 0, 0, 0);
+    f32x4 c = x_mma_k128(a, wx);                  // ∂basic[row][j] (before ReLU')
     f32x4 et4[8];
 #pragma unroll
     for (int et = 0; et < 8; ++et) et4[et] = *reinterpret_cast<const f32x4*>(imt[buf] + (16 * et + i) * kXT + 4 * kg);
-    float ub[4];                                  // units[row 4kg + r][f = i] (f ≥ 10: 0)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) ub[r] = i < kF ? sl[(4 * kg + r) * kF + i] : 0.f;
-    f32x4 bas = x_layer1(sl, w1x, i, kg);
-    f32x4 c = x_mma_k128(a, wx);                  // ∂basic[row][j] (before ReLU')
     // The global loads consumed here (staging of item k + 2, build data of item k + 1) were issued one iteration
     // ago, and nothing was issued after them: the vmcnt(0) the compiler puts before their first use waits out no
     // fresh round trip. (Issued at the top of the iteration instead, as before, that wait covered a load issued
@@ -1229,18 +1248,24 @@ __global__ __launch_bounds__(512, 1) void encoder_bwd_x_kernel(FbParams P) {
     if (wv < 3) stg[(k + 2) % 3][64 * wv + lane] = pre;   // slot (k - 1) % 3: nobody reads it in this iteration
     // item k + 1's ∂emb into the other images (every wave has passed this item's barrier)
     xb_build(bn, stg[(k + 1) % 3], min(k + 1, kl) % cnt, img[buf ^ 1], imt[buf ^ 1], wv, lane);
-    if (wv < 3) pre = fb_stage_load(P, min(k + 3, kl), cnt, uoff, wv, lane);
+    l1_read(stg[(k + 1) % 3]);                    // (written before barrier k)
     fb_load_build<false, COMPAT>(bn, R, P.ldq, min(k + 2, kl), k + 2 <= kl && (k + 2) % cnt == 0, cnt, uoff, U, tau,
                                  wv, i, kg);
+    if (wv < 3) pre = fb_stage_load(P, min(k + 3, kl), cnt, uoff, wv, lane);
 #pragma unroll
     for (int r = 0; r < 4; ++r) bas[r] = fmaxf(bas[r], 0.f);
-    // ∂W_τᵀ[j][e] += Σ_rows basic[row][j] · ∂emb[row][e] (this item's 16 rows from zero, then added)
+    // ∂W_τᵀ[j][e] += Σ_rows basic[row][j] · ∂emb[row][e] (this item's 16 rows from zero, then added): the 8
+    // e-tiles' chains interleaved (r outer), so no MFMA waits out its predecessor's 40-cycle latency
+    {
+      f32x4 p[8];
 #pragma unroll
-    for (int et = 0; et < 8; ++et) {
-      f32x4 p = {0.f, 0.f, 0.f, 0.f};
+      for (int et = 0; et < 8; ++et) p[et] = __builtin_amdgcn_mfma_f32_16x16x4f32(bas[0], et4[et][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) p = __builtin_amdgcn_mfma_f32_16x16x4f32(bas[r], et4[et][r], p, 0, 0, 0);
-      acc[et] += p;
+      for (int r = 1; r < 4; ++r)
+#pragma unroll
+        for (int et = 0; et < 8; ++et) p[et] = __builtin_amdgcn_mfma_f32_16x16x4f32(bas[r], et4[et][r], p[et], 0, 0, 0);
+#pragma unroll
+      for (int et = 0; et < 8; ++et) acc[et] += p[et];
     }
 #pragma unroll
     for (int r = 0; r < 4; ++r) {

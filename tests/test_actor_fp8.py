@@ -4,6 +4,7 @@
   activation scales, fp8 round trip) in fp32 — a wrong fragment map or quad transpose shows as O(1) errors, the
   tolerance only covers accumulation order and an occasional rounding tie of an intermediate;
 * resets (keep = 0) and inactive slots (state untouched) like the bf16 step;
+* the fp8 entity encoder (unit-type GEMMs on 16x16x128 f8f6f4) against the same emulation;
 * enum-action agreement of the whole graph-captured fp8 step with the bf16 step on the same observations and
   sampling noise ≥ 99 %.
 The fragment-order weight layout round-trips on the CPU."""
@@ -80,6 +81,53 @@ def test_fp8_core_matches_quantised_emulation(gpu_ops):
     off = ~on
     torch.testing.assert_close(h1[off], hk[off], rtol=0, atol=0)
     torch.testing.assert_close(c1[off], ck[off], rtol=0, atol=0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype,n', [(torch.float16, 100), (torch.float32, 4096)])
+def test_fp8_encoder_matches_quantised_emulation(gpu_ops, dtype, n):
+    """The fp8 entity encoder (ops/csrc/actor_fp8.hip encoder_fp8_kernel) against a torch emulation of the same
+    quantisation: basic per (row, unit) and W_τ per output channel in e4m3, fp32 products, bf16 outputs. Pools are
+    the max over the type's units of the emitted emb (bitwise: bf16 rounding is monotone)."""
+    from dotaclient_amd.actor.batched import fp8_weight
+    from dotaclient_amd.models.policy import TYPE_SUFFIX
+    torch.manual_seed(0)
+    pol = Policy(get_config('lstm512')).cuda()
+    cfg = pol.config
+    U = cfg.layout.max_units
+    counts = list(cfg.layout.counts)
+    g = torch.Generator(device='cuda').manual_seed(3)
+    units = torch.randn(n, U, 10, device='cuda', generator=g).to(dtype)
+    env = torch.randn(n, 3, device='cuda', generator=g)
+    P = {k: v.detach().float() for k, v in pol.state_dict().items()}
+    wts = [fp8_weight(P[f'affine_unit_{s}.weight']) for s in TYPE_SUFFIX]
+    wt8 = torch.cat([q for q, _ in wts]).contiguous()
+    st8 = torch.stack([s_ for _, s_ in wts]).contiguous()
+    bt = torch.stack([P[f'affine_unit_{s}.bias'] for s in TYPE_SUFFIX]).contiguous()
+    x896, emb = gpu_ops.encoder_fp8(units, env, P['affine_unit_basic_stats.weight'].contiguous(),
+                                    P['affine_unit_basic_stats.bias'], wt8, st8, bt,
+                                    P['affine_env.weight'].contiguous(), P['affine_env.bias'], counts)
+    torch.cuda.synchronize()
+    # emulation
+    basic = torch.relu(units.float() @ P['affine_unit_basic_stats.weight'].t() + P['affine_unit_basic_stats.bias'])
+    amax = basic.amax(-1, keepdim=True)
+    sc = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+    qb = (basic / sc).to(torch.float8_e4m3fn).float() * sc
+    ref = torch.empty(n, U, 128, device='cuda')
+    o = 0
+    for t, (q, s_) in enumerate(wts):
+        W = _unfrag(q, s_, 128, 128)
+        ref[:, o:o + counts[t]] = qb[:, o:o + counts[t]] @ W.t() + bt[t]
+        o += counts[t]
+    rel = lambda a_, b_: float((a_.float() - b_).norm() / b_.norm())   # noqa: E731
+    assert rel(emb, ref) < 1e-2, rel(emb, ref)
+    env_ref = torch.relu(env @ P['affine_env.weight'].t() + P['affine_env.bias'])
+    assert rel(x896[:, :128], env_ref) < 1e-2
+    o = 0
+    for t in range(6):
+        pool = emb[:, o:o + counts[t]].float().amax(1)
+        torch.testing.assert_close(x896[:, 128 + 128 * t:256 + 128 * t].float(), pool, rtol=0, atol=0)
+        o += counts[t]
 
 
 @pytest.mark.gpu
