@@ -25,6 +25,8 @@ EVERY rank (one actor runtime per GPU), and reported as node aggregates (sums ov
   rank 0 alone publishing the model. ``e2e.steps_per_s`` is the reference's own metric (optimizer.py:485-486, padded
   sequence steps incl. the wait for experience) summed over ranks; ``vs_baseline_e2e`` compares THAT with the
   reference's ≈1000 steps/s, the like-for-like node-level comparison (``vs_baseline`` is the compute-only learner);
+* ``model_5v5_exact`` — the 5v5 policy at IEEE fp32 (BASELINE config 4 at the reference precision): the torch backend,
+  since the fused attention-block kernels are bf16x3 only (``model_5v5`` is the fused bf16x3 number);
 * ``bptt350_learner`` — truncated BPTT: each sequence trained as ``seq_len / 350`` chains of 350 steps from
   actor-stored (h, c) (bf16x3 operands — the exact recurrence takes ≤ 8 sequences per step; not the headline);
 * ``league_replay`` — BASELINE config 5 through the same node loop: PFSP self-play league (80 % of games on the
@@ -70,6 +72,8 @@ def parse():
     ap.add_argument('--model-5v5-extra', type=int, default=1,
                     help='also time the 5v5 entity-attention policy (BASELINE config 4) at the same B, S (bf16x3 '
                          'operands: the attention kernels have no exact-fp32 variant)')
+    ap.add_argument('--model-5v5-exact-extra', type=int, default=1,
+                    help='also time the 5v5 policy at IEEE fp32 on the torch backend (extra field model_5v5_exact)')
     ap.add_argument('--bptt350-extra', type=int, default=1,
                     help='also time truncated BPTT: each sequence as seq_len/350 chains of 350 steps from stored '
                          '(h, c) (extra field bptt350_learner, bf16x3 operands; not the headline)')
@@ -147,15 +151,17 @@ def main():
         progress('5v5 entity attention has no exact-fp32 kernels: timing it at fp32 with bf16x3 operands')
         args.precision = 'fp32'
 
-    def run(precision, cfg=cfg, B=None, S=None):
+    def run(precision, cfg=cfg, B=None, S=None, backend=None, steps=None, warmup=None):
         """Build a learner of this precision and time ``args.steps`` DP PPO steps (``B`` sequences of ``S`` steps,
         default the command line's) after ``args.warmup``; returns (elapsed s (max over ranks), loss_first,
         loss_last, learner, policy)."""
         B = B or args.batch_size
         S = S or args.seq_len
+        n_steps = steps or args.steps
+        n_warm = args.warmup if warmup is None else warmup
         torch.manual_seed(7 + rank)
         policy = Policy(cfg)
-        backend = args.backend
+        backend = backend or args.backend
         if backend == 'auto':
             backend = 'fused' if use_cuda else 'torch'
         learner = Learner(policy, LossConfig(algo=args.algo), device=device, backend=backend, precision=precision)
@@ -180,7 +186,7 @@ def main():
             return out
 
         m = None
-        for _ in range(args.warmup):
+        for _ in range(n_warm):
             m = step()
         if use_cuda:
             torch.cuda.synchronize()
@@ -190,7 +196,7 @@ def main():
         if use_cuda:
             torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(args.steps):
+        for _ in range(n_steps):
             m = step()
         if use_cuda:
             torch.cuda.synchronize()
@@ -242,6 +248,26 @@ def main():
                          'ms_per_step': e5 / args.steps * 1e3, 'loss_first': l50, 'loss_last': l51}
         except Exception as e:
             model_5v5 = {'error': repr(e)}
+
+    model_5v5_exact = None
+    if args.model_5v5_exact_extra and use_cuda and not cfg.entity_attention:
+        # the 5v5 policy at the reference's precision: the fused kernels have no exact-fp32 attention block yet, so
+        # this is the torch backend (autograd, fp32 torch ops with TF32 off — the reference's own execution model)
+        learner = None
+        try:
+            n5 = max(1, min(args.steps, 5))
+            prev_tf32 = torch.backends.cuda.matmul.allow_tf32
+            torch.backends.cuda.matmul.allow_tf32 = False
+            try:
+                e5x, l0, l1, _, _ = run('fp32', get_config('5v5'), backend='torch', steps=n5, warmup=1)
+            finally:
+                torch.backends.cuda.matmul.allow_tf32 = prev_tf32
+            progress(f'learner 5v5 exact (torch) done: {e5x / n5 * 1e3:.3f} ms/step')
+            model_5v5_exact = {'model': '5v5', 'precision': 'IEEE fp32 (torch backend: autograd, fp32 ops, TF32 off)',
+                               'value': args.batch_size * args.seq_len * world * n5 / e5x,
+                               'ms_per_step': e5x / n5 * 1e3, 'steps': n5, 'loss_first': l0, 'loss_last': l1}
+        except Exception as e:
+            model_5v5_exact = {'error': repr(e)}
 
     bptt = None
     if (args.bptt350_extra and use_cuda and cfg.rnn == 'lstm' and not cfg.entity_attention
@@ -404,6 +430,7 @@ def main():
             'loss_first': loss_val, 'loss_last': final_loss,
             'fp32_bf16x3_learner': bf16x3,
             'model_5v5': model_5v5,
+            'model_5v5_exact': model_5v5_exact,
             'bptt350_learner': bptt,
             'dp_replicas_identical': len(set(shas)) == 1,
             'weights_sha16_per_rank': shas,
