@@ -1293,6 +1293,171 @@ __global__ __launch_bounds__(512, 1) void encoder_bwd_x_kernel(FbParams P) {
   if (kg == 0) wp[kD * kF + 16 * wv + i] = s;
 }
 
+// 4-wave form of encoder_bwd_x_kernel (two workgroups per CU): wave w owns basic-column tiles 2w, 2w+1 and builds
+// e-tiles 2w, 2w+1 of the item's ∂emb images. The item's A fragments (∂emb rows) and transposed ∂emb tiles are read
+// once per wave for two column tiles (half the LDS traffic per MFMA), and the two resident workgroups work on
+// different items, so one's barrier / staging phases overlap the other's MFMAs (the 8-wave form keeps both waves of
+// a SIMD in lockstep: ≈55 % MFMA busy). Same products, same per-item two-level sums, same partial layouts.
+template <bool COMPAT>
+__global__ __launch_bounds__(256, 2) void encoder_bwd_x2_kernel(FbParams P) {
+  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  const int i = lane & 15, kg = lane >> 4;
+  const int job = blockIdx.x;
+  int tau = 0;
+#pragma unroll
+  for (int t = 1; t < 6; ++t) tau += job >= P.jbase[t] ? 1 : 0;
+  const int cnt = P.L.cnt[tau], uoff = P.L.off[tau], N = P.N, U = P.L.U;
+  const int NB = (N + 15) >> 4;
+  const int k0 = (job - P.jbase[tau]) * P.items, k1 = min(k0 + P.items, cnt * NB);
+  __shared__ __attribute__((aligned(16))) float img[2][16 * kXP];
+  __shared__ __attribute__((aligned(16))) float imt[2][128 * kXT];
+  __shared__ __attribute__((aligned(16))) float stg[3][kStg];
+  FbRsrc R;
+  R.q = uniform_rsrc(P.q, N * P.ldq * 4);
+  R.x = uniform_rsrc(P.dx, N * 896 * 4);
+  R.a = uniform_rsrc(P.arg, N * 6 * kD);
+
+  float wx[2][32], w1x[2][3];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int col = 16 * (2 * w + t) + i;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float* p = P.wtT + ((size_t)tau * kD + col) * kD + 32 * s + 8 * kg;
+      const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+      wx[t][8 * s + 0] = a.x; wx[t][8 * s + 1] = a.y; wx[t][8 * s + 2] = a.z; wx[t][8 * s + 3] = a.w;
+      wx[t][8 * s + 4] = b.x; wx[t][8 * s + 5] = b.y; wx[t][8 * s + 6] = b.z; wx[t][8 * s + 7] = b.w;
+    }
+    x_load_w1(P.w1, P.b1, col, kg, w1x[t]);
+  }
+  f32x4 acc[2][8], dw1acc[2] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+  float db1acc[2] = {0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int et = 0; et < 8; ++et) acc[t][et] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  FbBuild bn[2];
+  const int kl = max(k1 - 1, 0);
+  float pre = 0.f;
+  if (w < 3) {
+    stg[k0 % 3][64 * w + lane] = fb_stage_load(P, min(k0, kl), cnt, uoff, w, lane);
+    stg[(k0 + 1) % 3][64 * w + lane] = fb_stage_load(P, min(k0 + 1, kl), cnt, uoff, w, lane);
+    pre = fb_stage_load(P, min(k0 + 2, kl), cnt, uoff, w, lane);
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+    fb_load_build<false, COMPAT>(bn[t], R, P.ldq, min(k0, kl), true, cnt, uoff, U, tau, 2 * w + t, i, kg);
+  lds_barrier();
+#pragma unroll
+  for (int t = 0; t < 2; ++t) xb_build(bn[t], stg[k0 % 3], k0 % cnt, img[0], imt[0], 2 * w + t, lane);
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+    fb_load_build<false, COMPAT>(bn[t], R, P.ldq, min(k0 + 1, kl), min(k0 + 1, kl) % cnt == 0, cnt, uoff, U, tau,
+                                 2 * w + t, i, kg);
+  float l1n[3], ubn[4];
+  auto l1_read = [&](const float* sl) {
+#pragma unroll
+    for (int cc = 0; cc < 3; ++cc) {
+      const int f = 4 * cc + kg;
+      l1n[cc] = f < kF ? sl[i * kF + f] : (f == kF ? 1.f : 0.f);
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ubn[r] = i < kF ? sl[(4 * kg + r) * kF + i] : 0.f;
+  };
+  l1_read(stg[k0 % 3]);
+  int buf = 0;
+  for (int k = k0; k < k1; ++k) {
+    lds_barrier();
+    float a[32];
+    x_afrags(img[buf], i, kg, a);                 // ∂emb[row i][e], e = 32s + 8kg + jj (both column tiles)
+    const float ub[4] = {ubn[0], ubn[1], ubn[2], ubn[3]};
+    f32x4 bas[2], c[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      bas[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int cc = 0; cc < 3; ++cc) bas[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(l1n[cc], w1x[t][cc], bas[t], 0, 0, 0);
+    }
+    {   // ∂basic (before ReLU') of both tiles: the two tiles' chains interleaved (even / odd k summed at the end, as
+        // the 8-wave form does)
+      f32x4 c0 = {0.f, 0.f, 0.f, 0.f}, c1 = c0, d0 = c0, d1 = c0;
+#pragma unroll
+      for (int kk = 0; kk < 32; kk += 2) {
+        c0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kk], wx[0][kk], c0, 0, 0, 0);
+        d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kk], wx[1][kk], d0, 0, 0, 0);
+      }
+#pragma unroll
+      for (int kk = 1; kk < 32; kk += 2) {
+        c1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kk], wx[0][kk], c1, 0, 0, 0);
+        d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(a[kk], wx[1][kk], d1, 0, 0, 0);
+      }
+      c[0] = c0 + c1;
+      c[1] = d0 + d1;
+    }
+    f32x4 et4[8];
+#pragma unroll
+    for (int et = 0; et < 8; ++et) et4[et] = *reinterpret_cast<const f32x4*>(imt[buf] + (16 * et + i) * kXT + 4 * kg);
+    if (w < 3) stg[(k + 2) % 3][64 * w + lane] = pre;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      xb_build(bn[t], stg[(k + 1) % 3], min(k + 1, kl) % cnt, img[buf ^ 1], imt[buf ^ 1], 2 * w + t, lane);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+      fb_load_build<false, COMPAT>(bn[t], R, P.ldq, min(k + 2, kl), k + 2 <= kl && (k + 2) % cnt == 0, cnt, uoff, U,
+                                   tau, 2 * w + t, i, kg);
+    l1_read(stg[(k + 1) % 3]);
+    if (w < 3) pre = fb_stage_load(P, min(k + 3, kl), cnt, uoff, w, lane);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bas[t][r] = fmaxf(bas[t][r], 0.f);
+    // ∂W_τᵀ[j][e] += Σ_rows basic[row][j]·∂emb[row][e], per item from zero then added; the two tiles' chains of an
+    // e-tile interleaved
+#pragma unroll
+    for (int et = 0; et < 8; ++et) {
+      f32x4 p0 = __builtin_amdgcn_mfma_f32_16x16x4f32(bas[0][0], et4[et][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+      f32x4 p1 = __builtin_amdgcn_mfma_f32_16x16x4f32(bas[1][0], et4[et][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+#pragma unroll
+      for (int r = 1; r < 4; ++r) {
+        p0 = __builtin_amdgcn_mfma_f32_16x16x4f32(bas[0][r], et4[et][r], p0, 0, 0, 0);
+        p1 = __builtin_amdgcn_mfma_f32_16x16x4f32(bas[1][r], et4[et][r], p1, 0, 0, 0);
+      }
+      acc[0][et] += p0;
+      acc[1][et] += p1;
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        c[t][r] = bas[t][r] > 0.f ? c[t][r] : 0.f;
+        db1acc[t] += c[t][r];
+      }
+      f32x4 p1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) p1 = __builtin_amdgcn_mfma_f32_16x16x4f32(c[t][r], ub[r], p1, 0, 0, 0);
+      dw1acc[t] += p1;
+    }
+    buf ^= 1;
+  }
+  float* dst = P.dwtpart + (size_t)job * (kD * kD);
+  float* wp = P.w1part + (size_t)job * kW1;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int jt = 2 * w + t;
+#pragma unroll
+    for (int et = 0; et < 8; ++et) *reinterpret_cast<f32x4*>(dst + ((8 * jt + et) * 64 + lane) * 4) = acc[t][et];
+    if (i < kF) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) wp[(16 * jt + 4 * kg + r) * kF + i] = dw1acc[t][r];
+    }
+    float s = db1acc[t];
+    s += __shfl_xor(s, 16, 64);
+    s += __shfl_xor(s, 32, 64);
+    if (kg == 0) wp[kD * kF + 16 * jt + i] = s;
+  }
+}
+
 // Fixed-order sum of a type's fused-backward partials (tile-linear → ∂W_τ[e][j]); 4 job phases per block as dwt_reduce.
 __global__ __launch_bounds__(256) void fb_dwt_reduce(const float* __restrict__ part, FbParams P, float* __restrict__ dwt) {
   __shared__ float red[4][64];
@@ -1519,7 +1684,12 @@ extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const
     F.dwtpart = F.w1part + (size_t)jobs * kW1;
     if (f32 == 2 && demb_in) return hipErrorInvalidValue;      // the exact kernels cover the 1v1 encoder
     if (jobs > 0 && f32 == 2) {
-      if (compat) encoder_bwd_x_kernel<true><<<jobs, 512, 0, st>>>(F);
+      // DCA_ENC_BWD_X2=0: the 8-wave one-workgroup-per-CU form (A/B)
+      static const bool x2 = [] { const char* e = getenv("DCA_ENC_BWD_X2"); return !(e && e[0] == '0'); }();
+      if (x2) {
+        if (compat) encoder_bwd_x2_kernel<true><<<jobs, 256, 0, st>>>(F);
+        else encoder_bwd_x2_kernel<false><<<jobs, 256, 0, st>>>(F);
+      } else if (compat) encoder_bwd_x_kernel<true><<<jobs, 512, 0, st>>>(F);
       else encoder_bwd_x_kernel<false><<<jobs, 512, 0, st>>>(F);
     } else if (jobs > 0) {
       if (demb_in) encoder_bwd_f32_fused_kernel<true, false><<<jobs, 512, 0, st>>>(F);
