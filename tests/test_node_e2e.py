@@ -95,3 +95,23 @@ def test_learner_ranks_share_one_experience_queue(world, transport):
     cons = out['rollouts_consumed_per_rank']
     assert len(cons) == world and all(c > 0 for c in cons)
     assert out['consumption_skew'] == max(cons) / min(cons)
+
+
+@pytest.mark.skipif(not native.AVAILABLE, reason='native module not built')
+def test_config5_node_loop_league_and_replay_cpu():
+    """BASELINE config 5 through the node loop (bench.py league_replay): a PFSP league of published versions on the
+    actor side and learners sampling every minibatch from the on-device replay ring (the fp8 actor step is the GPU
+    part, tests/test_actor_fp8.py)."""
+    from dotaclient_amd.learner.e2e import measure_e2e_node
+
+    def report(opt):
+        return {'replay': len(opt.replay), 'inserted': opt.replay.inserted, 'capacity': opt.replay.capacity,
+                'n_steps': opt.learner.n_steps}
+    r = measure_e2e_node(model='lstm128', device='cpu', backend='torch', duration=120.0, max_iterations=3,
+                         warmup_iterations=1, games=6, threads=1, seq_len=16, batch_size=2, seq_per_epoch=4,
+                         max_dota_time=12.0, prefetch=2, transport='shm', idle_probe=0.0, report=report,
+                         league='pfsp', latest_weights_prob=0.5, replay_gb=0.002)
+    rep = r['reports'][0]
+    assert r['config']['league'] == 'pfsp' and r['config']['replay_gb'] == 0.002
+    assert rep['capacity'] > 4 and rep['inserted'] >= 4 and rep['n_steps'] > 0
+    assert r['steps_per_s'] > 0 and r['actor_steps_per_s'] > 0
