@@ -113,14 +113,9 @@ class GpuActorPolicy:
         self.d_env = self.in_pack.dev['env']
         self.d_keep = self.in_pack.dev['keep']
         self.d_active = self.in_pack.dev['active']     # 0 → slot not stepped: LSTM state left untouched
-        if ud == torch.float32:
-            self.d_units = self.in_pack.dev['units']
-        else:
-            self.d_units = torch.zeros(n, U, 10, device=dev)
-        if hd == torch.long:
-            self.d_handles = self.in_pack.dev['handles']
-        else:
-            self.d_handles = torch.full((n, U), -1, dtype=torch.long, device=dev)
+        # the kernels read the staged dtypes as they are (fp8 step: fp16 features, int32 handles)
+        self.d_units = self.in_pack.dev['units']
+        self.d_handles = self.in_pack.dev['handles']
         self.h = torch.zeros(n, H, device=dev)
         self.c = torch.zeros(n, H, device=dev)
         self.h16 = torch.zeros(n, H, dtype=torch.bfloat16, device=dev)
@@ -204,9 +199,9 @@ class GpuActorPolicy:
     def _forward(self):
         """The captured body: reads d_* / h / c, writes idx/act/msk/logp/value and the new h / c.
 
-        bf16 path, 8 launches: encoder kernel → pre-RNN GEMM (bias + ReLU epilogue, bf16 out) → ``actor_state_prep``
-        (episode resets + the [x | bf16(h)] operand) → ONE gate GEMM (K = P + H, bias epilogue) → LSTM cell → heads
-        GEMM (bias epilogue) → sampling kernel → RNG counter."""
+        bf16 path, 7 launches: encoder kernel → pre-RNN GEMM (bias + ReLU epilogue, bf16 out) → ``actor_state_prep``
+        (episode resets + the [x | bf16(h)] operand + the sampler's RNG counter bump) → ONE gate GEMM (K = P + H, bias
+        epilogue) → LSTM cell → heads GEMM (bias epilogue) → sampling kernel."""
         C, w, cfg = self.C, self.w, self.cfg
         x896, emb, _ = C.encoder_fwd(self.d_units, self.d_env, w['w1'], w['b1'], w['wt16'], w['bt'], w['we'],
                                      w['be'], list(cfg.layout.counts), bool(cfg.compat_bugs))
@@ -223,7 +218,7 @@ class GpuActorPolicy:
             x896[:, 768:896] = x896[:, 512:640]
         x = torch._addmm_activation(w['bpre16'], x896, w['wpreT'])
         if cfg.rnn == 'lstm':
-            C.actor_state_prep(x, self.h, self.c, self.d_keep.view(-1), self.xh)
+            C.actor_state_prep(x, self.h, self.c, self.d_keep.view(-1), self.xh, self.ctr)
             gates = torch.addmm(w['brnn'], self.xh, w['wcatT'], out_dtype=torch.float32)
             C.lstm_cell(gates, self.h, self.c, self.h16, self.d_active)
             xh = self.h16
@@ -231,9 +226,10 @@ class GpuActorPolicy:
             self.h.copy_(torch.addmm(w['bf'], x, w['wfT'], out_dtype=torch.float32))
             xh = self.h.to(torch.bfloat16)
         z = torch.addmm(w['bh'], xh, w['whT'], out_dtype=torch.float32)
+        if cfg.rnn != 'lstm':
+            self.ctr.add_(1)
         C.sample_actions(z, emb, self.d_handles, self.seed, self.ctr, self.idx, self.act, self.msk, self.logp,
                          self.value)
-        self.ctr.add_(1)
 
     def _h2d(self):
         if self._shared_inputs:
@@ -245,10 +241,6 @@ class GpuActorPolicy:
             self.in_pack.copy_range('keep', 'active')
         else:
             self.in_pack.copy_range('env', 'active')          # one H2D copy of the whole staged step
-        self._widen()
-
-    def _widen(self):
-        """Compact staging (fp16 features / int32 handles): widen into the encoder's / sampler's operands."""
 
     def _d2h(self):
         self.out_pack.copy_range('idx', 'msk' if self.record else 'value', to_host=True)
@@ -367,7 +359,8 @@ class Fp8ActorPolicy(GpuActorPolicy):
     in the encoder) inside the kernels. The sampling kernel is shared with the bf16 step.
 
     Compact staging: unit features cross PCIe as fp16 and unit handles as int32 (3.3 + 0.7 MB per 4096-slot step
-    instead of 6.6 + 1.3 MB — the copies were 57 % of the bf16 step), widened on the GPU inside the captured graph.
+    instead of 6.6 + 1.3 MB — the copies were 57 % of the bf16 step), read by the kernels as they are (the encoder
+    converts the fp16 features in LDS, the sampler tests int32 handles).
     The host-side buffers keep the :class:`GpuActorPolicy` API (``h_units`` / ``h_handles`` numpy views assign with
     a cast). ``compact=False`` keeps fp32 / int64 host buffers (the native VecEnv writes those in place: VecActor).
     1v1 LSTM policies with hidden 512 / pre-RNN 256 (the kernel's shape)."""
@@ -407,32 +400,18 @@ class Fp8ActorPolicy(GpuActorPolicy):
             w.pop(k, None)
         return w
 
-    def _widen(self):
-        if self.compact:   # int32 handles → int64 for the sampler (the fp8 encoder reads the fp16 features as they are)
-            e = self._no_units
-            self.C.actor_widen(e[0], e[1], self.in_pack.dev['handles'], self.d_handles)
-
-    @property
-    def _no_units(self):
-        e = self.__dict__.get('_empty_units')
-        if e is None:
-            e = self._empty_units = (torch.empty(0, dtype=torch.float16, device=self.device),
-                                     torch.empty(0, dtype=torch.float32, device=self.device))
-        return e
-
     def _forward(self):
-        """Captured body, 4 launches: fp8 encoder → fp8 core (pre-RNN, gates + cell, heads) → sampling → RNG counter."""
+        """Captured body, 3 launches: fp8 encoder → fp8 core (pre-RNN, gates + cell, heads; bumps the sampler's RNG
+        counter) → sampling."""
         C, w, cfg = self.C, self.w, self.cfg
-        units = self.in_pack.dev['units'] if self.compact else self.d_units    # fp16 staging read directly
-        x896, emb = C.encoder_fp8(units, self.d_env, w['w1'], w['b1'], w['wt8'], w['st8'], w['bt'], w['we'],
+        x896, emb = C.encoder_fp8(self.d_units, self.d_env, w['w1'], w['b1'], w['wt8'], w['st8'], w['bt'], w['we'],
                                   w['be'], list(cfg.layout.counts))
         if cfg.compat_bugs:
             x896[:, 768:896] = x896[:, 512:640]
         C.actor_fp8(x896, w['wpre8'], w['spre'], w['bpre32'], w['wg8'], w['sg'], w['bg'], w['wh8'], w['sh8'],
-                    w['bh'], self.h, self.c, self.d_keep.view(-1), self.z, self.d_active)
+                    w['bh'], self.h, self.c, self.d_keep.view(-1), self.z, self.d_active, self.ctr)
         C.sample_actions(self.z, emb, self.d_handles, self.seed, self.ctr, self.idx, self.act, self.msk, self.logp,
                          self.value)
-        self.ctr.add_(1)
 
 
 class TorchSlotPolicy:

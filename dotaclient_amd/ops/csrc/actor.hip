@@ -11,7 +11,6 @@
 //   * hierarchical selection, joint log-prob of the sampled action, one-hot actions and selected-heads masks
 //     (the experience record), and V(s).
 #include "common.h"
-#include <hip/hip_fp16.h>
 
 namespace {
 
@@ -43,9 +42,10 @@ __device__ __forceinline__ int wave_argmax(float v, int lane) {
   return idx;
 }
 
+template <typename HT>   // unit handles: int64 (the reference's layout) or int32 (the fp8 step's compact staging)
 __global__ __launch_bounds__(256) void sample_kernel(const float* __restrict__ z, int ldz,
                                                      const short* __restrict__ emb,
-                                                     const long long* __restrict__ handles, int N, int U,
+                                                     const HT* __restrict__ handles, int N, int U,
                                                      unsigned long long seed, const long long* __restrict__ ctr,
                                                      int* __restrict__ idx_out, unsigned char* __restrict__ act_out,
                                                      unsigned char* __restrict__ msk_out, float* __restrict__ logp_out,
@@ -153,9 +153,12 @@ __global__ __launch_bounds__(256) void lstm_cell_kernel(const float* __restrict_
 // activations (N, P) bf16 (hipBLASLt ReLU epilogue). Replaces three elementwise passes, a cast and two GEMM-output adds.
 __global__ __launch_bounds__(256) void actor_state_prep_kernel(const short* __restrict__ pre, float* __restrict__ h,
                                                                float* __restrict__ c, const float* __restrict__ keep,
-                                                               short* __restrict__ xh, int N, int P, int H) {
+                                                               short* __restrict__ xh, int N, int P, int H,
+                                                               long long* __restrict__ bump) {
   const int per = (P > H ? P : H) / 4;            // one 4-column quad of the row per thread
   const int i = blockIdx.x * 256 + threadIdx.x;
+  // the sampling kernel (later in the step) reads the counter: bumping it here saves a one-element launch
+  if (bump && i == 0) bump[0] += 1;
   if (i >= N * per) return;
   const int n = i / per, j = (i % per) * 4;
   short* xr = xh + (size_t)n * (P + H);
@@ -176,47 +179,27 @@ __global__ __launch_bounds__(256) void actor_state_prep_kernel(const short* __re
   }
 }
 
-// Compact actor staging widened in one launch: fp16 unit features → fp32 (n4 groups of 4) and int32 unit handles →
-// int64 (m of them); the encoder and the sampling kernel then read their usual operands.
-__global__ __launch_bounds__(256) void actor_widen_kernel(const uint2* __restrict__ u16, float4* __restrict__ u32, int n4,
-                                                          const int* __restrict__ h32, long long* __restrict__ h64,
-                                                          int m) {
-  const int i = blockIdx.x * 256 + threadIdx.x;
-  if (i < n4) {
-    const uint2 v = u16[i];
-    const __half2 a = __builtin_bit_cast(__half2, v.x), b = __builtin_bit_cast(__half2, v.y);
-    u32[i] = make_float4(__low2float(a), __high2float(a), __low2float(b), __high2float(b));
-  }
-  if (i < m) h64[i] = h32[i];
-}
-
 }  // namespace
 
-extern "C" hipError_t dca_actor_widen(const void* u16, float* u32, long long n_units, const int* h32, long long* h64,
-                                      long long n_handles, hipStream_t st) {
-  if (n_units % 4) return hipErrorInvalidValue;
-  const long long n4 = n_units / 4, work = n4 > n_handles ? n4 : n_handles;
-  if (work == 0) return hipSuccess;
-  actor_widen_kernel<<<(unsigned)((work + 255) / 256), 256, 0, st>>>(reinterpret_cast<const uint2*>(u16),
-                                                                      reinterpret_cast<float4*>(u32), (int)n4, h32, h64,
-                                                                      (int)n_handles);
-  return hipGetLastError();
-}
-
 extern "C" hipError_t dca_actor_state_prep(const short* pre, float* h, float* c, const float* keep, short* xh, int N,
-                                           int P, int H, hipStream_t st) {
+                                           int P, int H, long long* bump, hipStream_t st) {
   if (H % 4 || P % 4) return hipErrorInvalidValue;
   const int per = (P > H ? P : H) / 4;
-  actor_state_prep_kernel<<<(N * per + 255) / 256, 256, 0, st>>>(pre, h, c, keep, xh, N, P, H);
+  actor_state_prep_kernel<<<(N * per + 255) / 256, 256, 0, st>>>(pre, h, c, keep, xh, N, P, H, bump);
   return hipGetLastError();
 }
 
-extern "C" hipError_t dca_sample_actions(const float* z, int ldz, const short* emb, const long long* handles, int N,
-                                         int U, unsigned long long seed, const long long* ctr, int* idx,
+extern "C" hipError_t dca_sample_actions(const float* z, int ldz, const short* emb, const void* handles, int h32,
+                                         int N, int U, unsigned long long seed, const long long* ctr, int* idx,
                                          unsigned char* act, unsigned char* msk, float* logp, float* value,
                                          hipStream_t st) {
   if (U < 1 || U > 64 || ldz < kQ + 22) return hipErrorInvalidValue;
-  sample_kernel<<<(N + 3) / 4, 256, 0, st>>>(z, ldz, emb, handles, N, U, seed, ctr, idx, act, msk, logp, value);
+  if (h32)
+    sample_kernel<int><<<(N + 3) / 4, 256, 0, st>>>(z, ldz, emb, static_cast<const int*>(handles), N, U, seed, ctr,
+                                                    idx, act, msk, logp, value);
+  else
+    sample_kernel<long long><<<(N + 3) / 4, 256, 0, st>>>(z, ldz, emb, static_cast<const long long*>(handles), N, U,
+                                                          seed, ctr, idx, act, msk, logp, value);
   return hipGetLastError();
 }
 

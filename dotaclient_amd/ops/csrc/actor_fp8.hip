@@ -125,6 +125,7 @@ struct Fp8Args {
   const float* keep; const float* active;
   float* z;                              // (n, 160) fp32
   int n;
+  long long* bump;                       // the sampler's step counter, += 1 here (null: the caller bumps it)
 };
 
 __global__ __launch_bounds__(NT) void actor_fp8_kernel(Fp8Args A) {
@@ -138,6 +139,8 @@ __global__ __launch_bounds__(NT) void actor_fp8_kernel(Fp8Args A) {
   // per-column dequant scales and biases (read in the streamed GEMMs' epilogues, which must stay off global memory)
   __shared__ float col_s[PD + GD + ZD], col_b[PD + GD + ZD];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
+  // the sampling kernel (next launch) reads the counter: bumping it here saves a one-element launch per step
+  if (A.bump && blockIdx.x == 0 && tid == 0) A.bump[0] += 1;
   const int q = lane >> 4, cl = lane & 15;
   const int row0 = blockIdx.x * BM;
   const int n = A.n;
@@ -365,8 +368,8 @@ __global__ __launch_bounds__(NT) void actor_fp8_kernel(Fp8Args A) {
 // time (fragment order, actor/batched.py fp8_weight). One 256-thread workgroup per 16 slots: the 16 rows' unit
 // features (contiguous, fp16 from the compact staging or fp32) land in LDS once; per unit, every thread computes 8
 // basic values of one row and quantises them into a double-buffered fp8 A image (one barrier per unit), then wave w
-// runs the MFMAs of output tiles 2w, 2w+1 and keeps the running pool maxima in registers. Replaces the widen kernel
-// (fp16 units are read as they are) and the bf16 encoder.
+// runs the MFMAs of output tiles 2w, 2w+1 and keeps the running pool maxima in registers. Replaces the bf16 encoder
+// (fp16 units are read as they are).
 // buffer resource over [p, p + bytes) (wave-uniform; out-of-range accesses read 0 / are dropped)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, long long bytes) {
   const unsigned long long ad = (unsigned long long)p;
@@ -389,7 +392,8 @@ struct EncFp8Args {
   int off[7];                            // type τ owns units off[τ] .. off[τ+1]-1
   int njob;                              // unit jobs per row block (blockIdx.y): whole types, balanced by units
   int nu[3];                             // units of job j, in increasing order (a type's units stay contiguous)
-  unsigned char ul[3][64];
+  int ul[3][64];                         // (dwords: wave-uniform scalar loads — byte entries were vector loads, and
+                                         // their vmcnt(0) drained every in-flight fetch / store once per unit)
 };
 constexpr int EBR = 16, ENT = 256, EMAXU = 64;
 
@@ -404,7 +408,10 @@ __device__ __forceinline__ float row16_max(float v) {
 
 template <bool F16>
 __global__ __launch_bounds__(ENT) void encoder_fp8_kernel(EncFp8Args a) {
-  __shared__ __attribute__((aligned(16))) unsigned us[EBR * EMAXU * 10];   // the 16 rows' unit features, raw bytes
+  extern __shared__ __attribute__((aligned(16))) unsigned us[];             // the 16 rows' unit features, raw bytes
+  // W1ᵀ (10 × 128) and b1 in LDS (feature-major: a thread's 8 outputs of feature f are one 32-byte run). In VGPRs
+  // they took 88 of the kernel's 187 registers — 2 workgroups per CU, so 768 of them ran in 1.5 rounds.
+  __shared__ __attribute__((aligned(16))) float w1s[11 * 128];
   __shared__ __attribute__((aligned(16))) unsigned char aimg[2][EBR * 128];  // fp8 basic tile, double-buffered
   __shared__ float rsc[2][EBR];                                             // its row scales
   constexpr int EP = 128 + 8;                                               // emb tile pitch (bf16)
@@ -437,12 +444,9 @@ __global__ __launch_bounds__(ENT) void encoder_fp8_kernel(EncFp8Args a) {
       }
     }
   }
-  float w1r[8][10], b1r[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    b1r[j] = a.b1[8 * kc + j];
-#pragma unroll
-    for (int f = 0; f < 10; ++f) w1r[j][f] = a.w1[(8 * kc + j) * 10 + f];
+  for (int i = tid; i < 11 * 128; i += ENT) {
+    const int f = i >> 7, c = i & 127;
+    w1s[i] = f < 10 ? a.w1[c * 10 + f] : a.b1[c];
   }
   f32x4 pm[2];
   // this wave's two weight fragments of the NEXT unit's type, loaded one unit ahead (an L2 round trip per unit
@@ -496,12 +500,20 @@ __global__ __launch_bounds__(ENT) void encoder_fp8_kernel(EncFp8Args a) {
         for (int f = 0; f < 10; ++f) x[f] = xp[f];
       }
       float v[8];
+      {
+        const float4* wp = reinterpret_cast<const float4*>(w1s + 8 * kc);
+        const float4 b0 = wp[10 * 32], b1 = wp[10 * 32 + 1];
+        v[0] = b0.x; v[1] = b0.y; v[2] = b0.z; v[3] = b0.w; v[4] = b1.x; v[5] = b1.y; v[6] = b1.z; v[7] = b1.w;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        float sacc = b1r[j];
+        for (int f = 0; f < 10; ++f) {
+          const float4 p0 = wp[f * 32], p1 = wp[f * 32 + 1];
+          v[0] = fmaf(p0.x, x[f], v[0]); v[1] = fmaf(p0.y, x[f], v[1]);
+          v[2] = fmaf(p0.z, x[f], v[2]); v[3] = fmaf(p0.w, x[f], v[3]);
+          v[4] = fmaf(p1.x, x[f], v[4]); v[5] = fmaf(p1.y, x[f], v[5]);
+          v[6] = fmaf(p1.z, x[f], v[6]); v[7] = fmaf(p1.w, x[f], v[7]);
+        }
 #pragma unroll
-        for (int f = 0; f < 10; ++f) sacc = fmaf(w1r[j][f], x[f], sacc);
-        v[j] = fmaxf(sacc, 0.f);
+        for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.f);
       }
       float am = fmaxf(fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3])), fmaxf(fmaxf(v[4], v[5]), fmaxf(v[6], v[7])));
       am = row16_max(am);                        // the row's 16 threads (one DPP row)
@@ -542,10 +554,10 @@ __global__ __launch_bounds__(ENT) void encoder_fp8_kernel(EncFp8Args a) {
   // this workgroup's units: the whole types of job `job` (several workgroups per row block shorten the serial
   // per-unit chain and let 2-3 workgroups share a CU; one type's units keep their order for the running pool)
   const int nu = a.nu[job];
-  const unsigned char* ul = a.ul[job];
+  const int* ul = a.ul[job];
   WSet A, B;
   fetch(A, type_of(ul[0]));
-  __builtin_amdgcn_s_waitcnt(0);                  // W1 / first fragments landed: no first-iteration waits in the loop
+  __builtin_amdgcn_s_waitcnt(0);                  // first fragments landed: no first-iteration waits in the loop
   __syncthreads();                                // unit features staged
   for (int i = 0; i < nu; i += 2) {
     fetch(B, type_of(ul[min(i + 1, nu - 1)]));
@@ -567,10 +579,10 @@ __global__ __launch_bounds__(ENT) void encoder_fp8_kernel(EncFp8Args a) {
 extern "C" hipError_t dca_actor_fp8(const short* x896, const void* wpre, const float* spre, const float* bpre,
                                     const void* wg, const float* sg, const float* bg, const void* wh, const float* sh,
                                     const float* bh, float* h, float* c, const float* keep, const float* active,
-                                    float* z, int n, hipStream_t stream) {
+                                    float* z, int n, long long* bump, hipStream_t stream) {
   if (n < 1) return hipSuccess;
   Fp8Args a{x896, reinterpret_cast<const i32x8*>(wpre), spre, bpre, reinterpret_cast<const i32x8*>(wg), sg, bg,
-            reinterpret_cast<const i32x8*>(wh), sh, bh, h, c, keep, active, z, n};
+            reinterpret_cast<const i32x8*>(wh), sh, bh, h, c, keep, active, z, n, bump};
   hipLaunchKernelGGL(actor_fp8_kernel, dim3((n + BM - 1) / BM), dim3(NT), 0, stream, a);
   return hipGetLastError();
 }
@@ -610,10 +622,11 @@ extern "C" hipError_t dca_encoder_fp8(const void* units, int f16, const float* e
   for (int t = 0; t < 6; ++t) {                   // job ids in order of their first type; units in increasing order
     int& jb = remap[owner[t]];
     if (jb < 0) { jb = a.njob++; a.nu[jb] = 0; }
-    for (int u = a.off[t]; u < a.off[t + 1]; ++u) a.ul[jb][a.nu[jb]++] = (unsigned char)u;
+    for (int u = a.off[t]; u < a.off[t + 1]; ++u) a.ul[jb][a.nu[jb]++] = u;
   }
   const dim3 grid((N + EBR - 1) / EBR, a.njob);
-  if (f16) hipLaunchKernelGGL(encoder_fp8_kernel<true>, grid, dim3(ENT), 0, stream, a);
-  else hipLaunchKernelGGL(encoder_fp8_kernel<false>, grid, dim3(ENT), 0, stream, a);
+  const size_t lds = ((size_t)EBR * U * 10 * (f16 ? 2 : 4) + 15) / 16 * 16;   // the staged unit features
+  if (f16) hipLaunchKernelGGL(encoder_fp8_kernel<true>, grid, dim3(ENT), lds, stream, a);
+  else hipLaunchKernelGGL(encoder_fp8_kernel<false>, grid, dim3(ENT), lds, stream, a);
   return hipGetLastError();
 }

@@ -368,7 +368,9 @@ std::vector<torch::Tensor> encoder_bwd(torch::Tensor units, torch::Tensor w1, to
 // logp (N) f32, value (N) f32 (all preallocated so the op is hipGraph-capturable).
 void sample_actions(torch::Tensor z, torch::Tensor emb, torch::Tensor handles, int64_t seed, torch::Tensor ctr,
                     torch::Tensor idx, torch::Tensor act, torch::Tensor msk, torch::Tensor logp, torch::Tensor value) {
-  CHECK_F32(z); CHECK_BF16(emb); CHECK_DEV(handles); CHECK_CONTIG(handles); CHECK_DT(handles, at::kLong);
+  CHECK_F32(z); CHECK_BF16(emb); CHECK_DEV(handles); CHECK_CONTIG(handles);
+  const bool h32 = handles.scalar_type() == at::kInt;
+  TORCH_CHECK(h32 || handles.scalar_type() == at::kLong, "sample_actions: handles int64 or int32");
   CHECK_DEV(ctr); CHECK_DT(ctr, at::kLong); CHECK_I32(idx); CHECK_U8(act); CHECK_U8(msk); CHECK_F32(logp);
   CHECK_F32(value);
   TORCH_CHECK(z.dim() == 2 && emb.dim() == 3 && emb.size(2) == 128, "z (N,ldz), emb (N,U,128)");
@@ -377,33 +379,28 @@ void sample_actions(torch::Tensor z, torch::Tensor emb, torch::Tensor handles, i
   TORCH_CHECK(idx.size(0) == N && idx.size(1) == 4 && logp.numel() == N && value.numel() == N, "output shapes");
   TORCH_CHECK(act.size(0) == N && act.size(1) == 21 + U && msk.sizes() == act.sizes(), "act/msk (N,21+U)");
   TORCH_CHECK(U <= 64 && ldz >= 150, "U <= 64, ldz >= 150");
-  hip_check(dca_sample_actions(ptr<float>(z), ldz, ptr<short>(emb), ptr<long long>(handles), N, U,
+  hip_check(dca_sample_actions(ptr<float>(z), ldz, ptr<short>(emb), handles.data_ptr(), h32 ? 1 : 0, N, U,
                                (unsigned long long)seed, ptr<long long>(ctr), ptr<int>(idx), ptr<unsigned char>(act),
                                ptr<unsigned char>(msk), ptr<float>(logp), ptr<float>(value), cur_stream()),
             "dca_sample_actions");
 }
 
 // Actor step staging: h, c *= keep (N) in place; xh (N, P + H) bf16 = [pre | bf16(h)] for the one-GEMM gates.
-void actor_state_prep(torch::Tensor pre, torch::Tensor h, torch::Tensor c, torch::Tensor keep, torch::Tensor xh) {
+static long long* bump_ptr(const c10::optional<torch::Tensor>& bump) {   // optional (1) int64 device counter
+  if (!bump || !bump->defined()) return nullptr;
+  CHECK_DEV(*bump); CHECK_DT(*bump, at::kLong);
+  TORCH_CHECK(bump->numel() >= 1, "bump: (1) int64 counter");
+  return ptr<long long>(*bump);
+}
+
+void actor_state_prep(torch::Tensor pre, torch::Tensor h, torch::Tensor c, torch::Tensor keep, torch::Tensor xh,
+                      c10::optional<torch::Tensor> bump) {
   CHECK_BF16(pre); CHECK_F32(h); CHECK_F32(c); CHECK_F32(keep); CHECK_BF16(xh);
   const int N = h.size(0), H = h.size(1), P = pre.size(1);
   TORCH_CHECK(pre.dim() == 2 && pre.size(0) == N && c.sizes() == h.sizes() && keep.numel() == N && xh.dim() == 2 &&
               xh.size(0) == N && xh.size(1) == P + H && H % 4 == 0 && P % 4 == 0, "actor_state_prep shapes");
   hip_check(dca_actor_state_prep(ptr<short>(pre), ptr<float>(h), ptr<float>(c), ptr<float>(keep), ptr<short>(xh), N, P,
-                                 H, cur_stream()), "dca_actor_state_prep");
-}
-
-// Compact actor staging → the step's operands in one launch: units16 (…) fp16 → units (same shape) fp32, handles32
-// int32 → handles int64.
-void actor_widen(torch::Tensor units16, torch::Tensor units, torch::Tensor handles32, torch::Tensor handles) {
-  CHECK_DEV(units16); CHECK_CONTIG(units16); CHECK_DT(units16, at::kHalf); CHECK_F32(units);
-  CHECK_DEV(handles32); CHECK_CONTIG(handles32); CHECK_DT(handles32, at::kInt);
-  CHECK_DEV(handles); CHECK_CONTIG(handles); CHECK_DT(handles, at::kLong);
-  TORCH_CHECK(units16.numel() == units.numel() && units.numel() % 4 == 0 && handles32.numel() == handles.numel(),
-              "actor_widen shapes");
-  hip_check(dca_actor_widen(units16.data_ptr(), ptr<float>(units), units.numel(), ptr<int>(handles32),
-                            reinterpret_cast<long long*>(handles.data_ptr()), handles.numel(), cur_stream()),
-            "dca_actor_widen");
+                                 H, bump_ptr(bump), cur_stream()), "dca_actor_state_prep");
 }
 
 // LSTM cell from fp32 pre-activation gates (N,4H): updates h, c (N,H) f32 in place, writes h16 (N,H) bf16.
@@ -429,7 +426,7 @@ void lstm_cell(torch::Tensor gates, torch::Tensor h, torch::Tensor c, torch::Ten
 void actor_fp8(torch::Tensor x896, torch::Tensor wpre, torch::Tensor spre, torch::Tensor bpre, torch::Tensor wg,
                torch::Tensor sg, torch::Tensor bg, torch::Tensor wh, torch::Tensor sh, torch::Tensor bh,
                torch::Tensor h, torch::Tensor c, torch::Tensor keep, torch::Tensor z,
-               c10::optional<torch::Tensor> active) {
+               c10::optional<torch::Tensor> active, c10::optional<torch::Tensor> bump) {
   CHECK_BF16(x896); CHECK_U8(wpre); CHECK_U8(wg); CHECK_U8(wh);
   CHECK_F32(spre); CHECK_F32(bpre); CHECK_F32(sg); CHECK_F32(bg); CHECK_F32(sh); CHECK_F32(bh);
   CHECK_F32(h); CHECK_F32(c); CHECK_F32(keep); CHECK_F32(z);
@@ -449,7 +446,7 @@ void actor_fp8(torch::Tensor x896, torch::Tensor wpre, torch::Tensor spre, torch
   }
   hip_check(dca_actor_fp8(ptr<short>(x896), wpre.data_ptr(), ptr<float>(spre), ptr<float>(bpre), wg.data_ptr(),
                           ptr<float>(sg), ptr<float>(bg), wh.data_ptr(), ptr<float>(sh), ptr<float>(bh), ptr<float>(h),
-                          ptr<float>(c), ptr<float>(keep), act, ptr<float>(z), n, cur_stream()),
+                          ptr<float>(c), ptr<float>(keep), act, ptr<float>(z), n, bump_ptr(bump), cur_stream()),
             "dca_actor_fp8");
 }
 
@@ -1168,15 +1165,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("time_major") = false, py::arg("dg_out") = py::none(), py::arg("dg_bf16") = false,
         py::arg("want_dbias") = false, py::arg("precise") = false, py::arg("reset") = py::none());
   m.def("sample_actions", &sample_actions, "fused masked hierarchical Gumbel-max action sampling (actor)");
-  m.def("actor_widen", &actor_widen, "compact actor staging: fp16 features -> fp32, int32 handles -> int64 (one launch)");
-  m.def("actor_state_prep", &actor_state_prep, "actor step: state resets + [x | bf16(h)] gate-GEMM operand");
+  m.def("actor_state_prep", &actor_state_prep, "actor step: state resets + [x | bf16(h)] gate-GEMM operand",
+        py::arg("pre"), py::arg("h"), py::arg("c"), py::arg("keep"), py::arg("xh"), py::arg("bump") = py::none());
   m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)", py::arg("gates"),
         py::arg("h"), py::arg("c"), py::arg("h16"), py::arg("active") = py::none());
   m.def("encoder_fp8", &encoder_fp8, "fp8 (e4m3) entity encoder of the actor step: unit MLP, per-type GEMMs, pools");
   m.def("actor_fp8", &actor_fp8, "fp8 (e4m3) actor policy core: pre-RNN + LSTM step + heads from x896",
         py::arg("x896"), py::arg("wpre"), py::arg("spre"), py::arg("bpre"), py::arg("wg"), py::arg("sg"), py::arg("bg"),
         py::arg("wh"), py::arg("sh"), py::arg("bh"), py::arg("h"), py::arg("c"), py::arg("keep"), py::arg("z"),
-        py::arg("active") = py::none());
+        py::arg("active") = py::none(), py::arg("bump") = py::none());
   m.def("attn_block_fwd", &attn_block_fwd, "fused fp32 entity-attention block forward: LN + QKV + attention + "
         "out-projection + residual + pools (-> xn, mean, rstd, qkv, o, lse, e1)");
   m.def("attn_block_bwd", &attn_block_bwd, "fused fp32 entity-attention block backward: demb + dO + attention "

@@ -28,7 +28,8 @@ hipError_t dca_attn_block_bwd_f32(const float* dtl, const float* q, int ldq, con
 // actor_fp8.hip
 hipError_t dca_actor_fp8(const short* x896, const void* wpre, const float* spre, const float* bpre, const void* wg,
                          const float* sg, const float* bg, const void* wh, const float* sh, const float* bh, float* h,
-                         float* c, const float* keep, const float* active, float* z, int n, hipStream_t stream);
+                         float* c, const float* keep, const float* active, float* z, int n, long long* bump,
+                         hipStream_t stream);
 hipError_t dca_encoder_fp8(const void* units, int f16, const float* env, const float* w1, const float* b1,
                            const void* wt, const float* st, const float* bt, const float* we, const float* be,
                            short* x896, short* emb, int N, int U, const int* counts, hipStream_t stream);
@@ -84,13 +85,11 @@ hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, const float*
                              int time_major, hipStream_t st, unsigned long long* trace, short* dg16, float* dbpart,
                              int f32, int precise = 0, const unsigned char* rst = nullptr);
 
-hipError_t dca_sample_actions(const float* z, int ldz, const short* emb, const long long* handles, int N, int U,
+hipError_t dca_sample_actions(const float* z, int ldz, const short* emb, const void* handles, int h32, int N, int U,
                               unsigned long long seed, const long long* ctr, int* idx, unsigned char* act,
                               unsigned char* msk, float* logp, float* value, hipStream_t st);
-hipError_t dca_actor_widen(const void* u16, float* u32, long long n_units, const int* h32, long long* h64,
-                           long long n_handles, hipStream_t st);
 hipError_t dca_actor_state_prep(const short* pre, float* h, float* c, const float* keep, short* xh, int N, int P,
-                                int H, hipStream_t st);
+                                int H, long long* bump, hipStream_t st);
 hipError_t dca_lstm_cell(const float* gates, float* h, float* c, short* h16, const float* active, int N, int H,
                          hipStream_t st);
 
