@@ -336,6 +336,10 @@ class GpuActorPolicy:
         return self.h, self.c
 
 
+# fp8 encoder form of the actor step: the per-unit workgroup kernel (True) or the wave-parallel one (False)
+_FP8_ENC_PER_UNIT = os.environ.get('DCA_FP8_ENC_PER_UNIT', '0') == '1'
+
+
 def fp8_weight(w: torch.Tensor):
     """(N, K) fp32 weight → (e4m3fn bytes in MFMA fragment order, (N,) fp32 per-channel dequant scales) for
     ops/csrc/actor_fp8.hip: each output channel's max |w| maps to 448 (the largest finite e4m3fn); byte order
@@ -405,7 +409,7 @@ class Fp8ActorPolicy(GpuActorPolicy):
         counter) → sampling."""
         C, w, cfg = self.C, self.w, self.cfg
         x896, emb = C.encoder_fp8(self.d_units, self.d_env, w['w1'], w['b1'], w['wt8'], w['st8'], w['bt'], w['we'],
-                                  w['be'], list(cfg.layout.counts))
+                                  w['be'], list(cfg.layout.counts), per_unit=_FP8_ENC_PER_UNIT)
         if cfg.compat_bugs:
             x896[:, 768:896] = x896[:, 512:640]
         C.actor_fp8(x896, w['wpre8'], w['spre'], w['bpre32'], w['wg8'], w['sg'], w['bg'], w['wh8'], w['sh8'],

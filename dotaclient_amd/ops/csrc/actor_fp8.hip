@@ -571,6 +571,198 @@ __global__ __launch_bounds__(ENT) void encoder_fp8_kernel(EncFp8Args a) {
   flush(prev_u, (nu - 1) & 1);                    // the last unit's tile
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Wave-parallel form of the fp8 encoder (the default): one 512-thread workgroup (8 waves) per 16 slot rows and ALL
+// unit types. The row block's U units, in type order, are dealt to the 8 waves as contiguous segments (U/8 units each,
+// ≤ 3 same-type runs per segment: 1v1 {1, 5, 16, 16, 1, 1} → 5 units per wave), so every wave works through its own
+// units with NO per-unit workgroup barrier:
+//   basic  lane l computes the 32 outputs 32(l>>4) … +31 of row l&15 (K = 10, W1ᵀ from LDS), the row's max over
+//          its 4 lanes (two shuffles), e4m3 — and those 32 bytes ARE the lane's A operand of the 16x16x128 f8f6f4
+//          MFMA (A[row l&15][k = 32(l>>4) + j]): no A image, no LDS round trip;
+//   GEMM   8 MFMAs (the 128 output columns) against the run's type weights, held in one of two register sets (the
+//          next run's set loads while the current run computes);
+//   emb    dequantised in the accumulator layout, staged through the wave's own LDS tile, 16-byte row stores;
+//   pools  every unit's values folded into the type's LDS pool by integer max on order-preserving keys (exact and
+//          order independent across the waves sharing a type; running maxima in registers spilled), written once at
+//          the end as 16-byte bf16 stores.
+// The per-unit-barrier form above (one unit at a time over the whole workgroup) stays as the fallback for layouts
+// whose segments would need more than 3 runs.
+struct EncW8Args {
+  const void* units; const float* env; const float* w1; const float* b1;
+  const i32x8* wt; const float* st; const float* bt; const float* we; const float* be;
+  short* x896; short* emb;
+  int N, U;
+  int nrun[8];                           // same-type runs of wave w's unit segment (≤ 3)
+  int rt[8][3], rb[8][3], re[8][3];      // run k: type, first unit, one past the last unit
+};
+constexpr int EWT = 512, EWP = 136;      // threads; bf16 pitch of a wave's 16 × 128 emb tile
+
+__device__ __forceinline__ int ord_key(float f) {     // float order as signed-int order (an involution)
+  const int b = __float_as_int(f);
+  return b < 0 ? b ^ 0x7fffffff : b;
+}
+
+template <bool F16>
+__global__ __launch_bounds__(EWT, 1) void encoder_fp8w_kernel(EncW8Args a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned us[];          // the 16 rows' unit features, raw bytes
+  __shared__ __attribute__((aligned(16))) float w1s[11 * 128];            // W1ᵀ (feature-major), then b1
+  __shared__ float cscale[6 * 128], cbias[6 * 128];                       // W_τ dequant scales, b_τ
+  __shared__ __attribute__((aligned(16))) short et[8][EBR * EWP];         // each wave's emb tile
+  __shared__ __attribute__((aligned(16))) int pool[6 * EBR * 128];        // pool keys [type][row][column]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r0 = blockIdx.x * EBR, N = a.N, U = a.U;
+  const int nrows = min(EBR, N - r0);
+  {   // unit features → LDS by LDS-DMA (rows past N read the last valid dword; their outputs are never stored)
+    typedef __attribute__((address_space(1))) void gvoid;
+    typedef __attribute__((address_space(3))) void lvoid;
+    constexpr int ES = F16 ? 2 : 4;
+    const int nd = nrows * U * 10 * ES / 4, total = EBR * U * 10 * ES / 4;
+    const unsigned* src = reinterpret_cast<const unsigned*>(static_cast<const char*>(a.units) +
+                                                            (size_t)r0 * U * 10 * ES);
+    for (int q0 = 64 * w; q0 < total; q0 += EWT)
+      __builtin_amdgcn_global_load_lds((gvoid*)(src + min(q0 + lane, nd - 1)), (lvoid*)(us + q0), 4, 0, 0);
+  }
+  for (int i = tid; i < 11 * 128; i += EWT) {
+    const int f = i >> 7, c = i & 127;
+    w1s[i] = f < 10 ? a.w1[c * 10 + f] : a.b1[c];
+  }
+  for (int i = tid; i < 6 * 128; i += EWT) {
+    cscale[i] = a.st[i];
+    cbias[i] = a.bt[i];
+  }
+  for (int i = tid; i < 6 * EBR * 128; i += EWT) pool[i] = (int)0x80000000;
+  {   // env embedding: row tid>>5, columns 4(tid&31) … +3
+    const int row = r0 + (tid >> 5), c0 = 4 * (tid & 31);
+    if (row < N) {
+      const float e0 = a.env[row * 3], e1 = a.env[row * 3 + 1], e2 = a.env[row * 3 + 2];
+      short o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = c0 + j;
+        o[j] = dca::f2bf(fmaxf(a.be[c] + a.we[c * 3] * e0 + a.we[c * 3 + 1] * e1 + a.we[c * 3 + 2] * e2, 0.f));
+      }
+      *reinterpret_cast<uint2*>(a.x896 + (size_t)row * 896 + c0) =
+          make_uint2((unsigned)(unsigned short)o[0] | ((unsigned)(unsigned short)o[1] << 16),
+                     (unsigned)(unsigned short)o[2] | ((unsigned)(unsigned short)o[3] << 16));
+    }
+  }
+  const int nr = a.nrun[w];
+  i32x8 WA[8], WB[8];
+  auto load = [&](i32x8 (&W)[8], int tau) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) W[t] = a.wt[((size_t)tau * 8 + t) * 64 + lane];
+  };
+  if (nr > 0) load(WA, a.rt[w][0]);
+  if (nr > 1) load(WB, a.rt[w][1]);
+  __builtin_amdgcn_s_waitcnt(0);                  // features (LDS-DMA) and the first weight sets landed
+  __syncthreads();
+
+  const int m = lane & 15, kc = lane >> 4;        // basic: row m, outputs 32kc … 32kc+31
+  short* const tile = et[w];
+  auto unit = [&](int u, const i32x8 (&W)[8], int tau) {
+    float x[10];
+    if constexpr (F16) {
+      const __half2* xp = reinterpret_cast<const __half2*>(us) + (m * U + u) * 5;
+#pragma unroll
+      for (int f = 0; f < 5; ++f) {
+        const float2 t2 = __half22float2(xp[f]);
+        x[2 * f] = t2.x;
+        x[2 * f + 1] = t2.y;
+      }
+    } else {
+      const float* xp = reinterpret_cast<const float*>(us) + (m * U + u) * 10;
+#pragma unroll
+      for (int f = 0; f < 10; ++f) x[f] = xp[f];
+    }
+    const float4* wp = reinterpret_cast<const float4*>(w1s) + 8 * kc;
+    float v[32];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const float4 b = wp[10 * 32 + i];
+      v[4 * i] = b.x; v[4 * i + 1] = b.y; v[4 * i + 2] = b.z; v[4 * i + 3] = b.w;
+    }
+#pragma unroll
+    for (int f = 0; f < 10; ++f)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float4 p = wp[f * 32 + i];
+        v[4 * i] = fmaf(p.x, x[f], v[4 * i]);
+        v[4 * i + 1] = fmaf(p.y, x[f], v[4 * i + 1]);
+        v[4 * i + 2] = fmaf(p.z, x[f], v[4 * i + 2]);
+        v[4 * i + 3] = fmaf(p.w, x[f], v[4 * i + 3]);
+      }
+    float am = 0.f;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      v[j] = fmaxf(v[j], 0.f);
+      am = fmaxf(am, v[j]);
+    }
+    am = fmaxf(am, __shfl_xor(am, 16, 64));
+    am = fmaxf(am, __shfl_xor(am, 32, 64));
+    const float sc = am > 0.f ? am / kQmax : 1.f, inv = am > 0.f ? kQmax / am : 1.f;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) v[j] *= inv;
+    i32x8 af;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const long long p = pack8(v + 8 * q);
+      af[2 * q] = (int)(unsigned)p;
+      af[2 * q + 1] = (int)(unsigned)(p >> 32);
+    }
+    float rs[4];                                  // scales of the accumulator rows 4kc + r (lane 4kc + r has them)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) rs[r] = __shfl(sc, 4 * kc + r, 64);
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const f32x4 c = mma128(af, W[t], f32x4{0.f, 0.f, 0.f, 0.f});
+      const int col = 16 * t + m;
+      const float sw = cscale[tau * 128 + col], bb = cbias[tau * 128 + col];
+      int* pk = pool + tau * EBR * 128 + col;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float e = c[r] * rs[r] * sw + bb;
+        atomicMax(pk + (4 * kc + r) * 128, ord_key(e));
+        tile[(4 * kc + r) * EWP + col] = dca::f2bf(e);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the wave's tile is complete (cross-lane read below)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = 4 * i + kc;
+      if (r0 + row < N)
+        *reinterpret_cast<uint4*>(a.emb + ((size_t)(r0 + row) * U + u) * 128 + 8 * m) =
+            *reinterpret_cast<const uint4*>(tile + row * EWP + 8 * m);
+    }
+  };
+  for (int k = 0; k < nr; ++k) {                  // (wave-uniform)
+    const int tau = a.rt[w][k], ub = a.rb[w][k], ue = a.re[w][k];
+    if ((k & 1) == 0) {
+      for (int u = ub; u < ue; ++u) unit(u, WA, tau);
+      if (k + 2 < nr) load(WA, a.rt[w][k + 2]);
+    } else {
+      for (int u = ub; u < ue; ++u) unit(u, WB, tau);
+      if (k + 2 < nr) load(WB, a.rt[w][k + 2]);
+    }
+  }
+  __syncthreads();
+  // pools → x896[:, 128 + 128τ + c], 8 columns (16 B) per store
+  for (int i = tid; i < 6 * EBR * 16; i += EWT) {
+    const int tau = i / (EBR * 16), rem = i - tau * EBR * 16, row = rem >> 4, ch = rem & 15;
+    if (r0 + row >= N) continue;
+    const int* pk = pool + (tau * EBR + row) * 128 + 8 * ch;
+    unsigned o[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float lo = __int_as_float(ord_key(__int_as_float(pk[2 * j])));
+      const float hi = __int_as_float(ord_key(__int_as_float(pk[2 * j + 1])));
+      o[j] = (unsigned)(unsigned short)dca::f2bf(lo) | ((unsigned)(unsigned short)dca::f2bf(hi) << 16);
+    }
+    *reinterpret_cast<uint4*>(a.x896 + (size_t)(r0 + row) * 896 + 128 + 128 * tau + 8 * ch) =
+        make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 }  // namespace
 
 // x896 (n,896) bf16; weights fragment-ordered fp8 (see actor/batched.py fp8_weight) with fp32 per-channel scales and
@@ -593,9 +785,39 @@ extern "C" hipError_t dca_actor_fp8(const short* x896, const void* wpre, const f
 extern "C" hipError_t dca_encoder_fp8(const void* units, int f16, const float* env, const float* w1, const float* b1,
                                       const void* wt, const float* st, const float* bt, const float* we,
                                       const float* be, short* x896, short* emb, int N, int U, const int* counts,
-                                      hipStream_t stream) {
+                                      int per_unit, hipStream_t stream) {
   if (N < 1) return hipSuccess;
   if (U < 1 || U > EMAXU) return hipErrorInvalidValue;
+  if (!per_unit) {   // wave-parallel form: U units in type order as 8 contiguous segments of ≤ 3 same-type runs
+    EncW8Args b{units, env, w1, b1, reinterpret_cast<const i32x8*>(wt), st, bt, we, be, x896, emb, N, U, {}, {}, {}, {}};
+    int tof[EMAXU], acc = 0;
+    bool ok = true;
+    for (int t = 0; t < 6; ++t) {
+      if (counts[t] < 1) return hipErrorInvalidValue;
+      for (int j = 0; j < counts[t] && acc < EMAXU; ++j) tof[acc++] = t;
+    }
+    if (acc != U) return hipErrorInvalidValue;
+    for (int w = 0; w < 8 && ok; ++w) {
+      const int lo = w * U / 8, hi = (w + 1) * U / 8;
+      b.nrun[w] = 0;
+      for (int u = lo; u < hi; ++u) {
+        if (u == lo || tof[u] != tof[u - 1]) {
+          if (b.nrun[w] == 3) { ok = false; break; }
+          const int k = b.nrun[w]++;
+          b.rt[w][k] = tof[u];
+          b.rb[w][k] = u;
+        }
+        b.re[w][b.nrun[w] - 1] = u + 1;
+      }
+    }
+    if (ok) {
+      const size_t lds = ((size_t)EBR * U * 10 * (f16 ? 2 : 4) + 15) / 16 * 16;
+      const dim3 grid((N + EBR - 1) / EBR);
+      if (f16) hipLaunchKernelGGL(encoder_fp8w_kernel<true>, grid, dim3(EWT), lds, stream, b);
+      else hipLaunchKernelGGL(encoder_fp8w_kernel<false>, grid, dim3(EWT), lds, stream, b);
+      return hipGetLastError();
+    }
+  }
   EncFp8Args a{units, env, w1, b1, reinterpret_cast<const i32x8*>(wt), st, bt, we, be, x896, emb, N, U, {}};
   int acc = 0;
   for (int t = 0; t < 6; ++t) {

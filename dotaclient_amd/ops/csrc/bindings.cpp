@@ -455,7 +455,7 @@ void actor_fp8(torch::Tensor x896, torch::Tensor wpre, torch::Tensor spre, torch
 // type) with per-channel scales st (6, 128); bt (6, 128).
 std::vector<torch::Tensor> encoder_fp8(torch::Tensor units, torch::Tensor env, torch::Tensor w1, torch::Tensor b1,
                                        torch::Tensor wt, torch::Tensor st, torch::Tensor bt, torch::Tensor we,
-                                       torch::Tensor be, std::vector<int64_t> counts) {
+                                       torch::Tensor be, std::vector<int64_t> counts, bool per_unit) {
   CHECK_DEV(units); CHECK_CONTIG(units); CHECK_F32(env); CHECK_F32(w1); CHECK_F32(b1); CHECK_U8(wt);
   CHECK_F32(st); CHECK_F32(bt); CHECK_F32(we); CHECK_F32(be);
   const bool f16 = units.scalar_type() == at::kHalf;
@@ -477,7 +477,7 @@ std::vector<torch::Tensor> encoder_fp8(torch::Tensor units, torch::Tensor env, t
   auto emb = torch::empty({N, U, 128}, o.dtype(at::kBFloat16));
   hip_check(dca_encoder_fp8(units.data_ptr(), f16 ? 1 : 0, ptr<float>(env), ptr<float>(w1), ptr<float>(b1),
                             wt.data_ptr(), ptr<float>(st), ptr<float>(bt), ptr<float>(we), ptr<float>(be),
-                            ptr<short>(x896), ptr<short>(emb), N, U, c, cur_stream()),
+                            ptr<short>(x896), ptr<short>(emb), N, U, c, per_unit ? 1 : 0, cur_stream()),
             "dca_encoder_fp8");
   return {x896, emb};
 }
@@ -1169,7 +1169,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pre"), py::arg("h"), py::arg("c"), py::arg("keep"), py::arg("xh"), py::arg("bump") = py::none());
   m.def("lstm_cell", &lstm_cell, "LSTM cell nonlinearity from fp32 gates (actor single step)", py::arg("gates"),
         py::arg("h"), py::arg("c"), py::arg("h16"), py::arg("active") = py::none());
-  m.def("encoder_fp8", &encoder_fp8, "fp8 (e4m3) entity encoder of the actor step: unit MLP, per-type GEMMs, pools");
+  m.def("encoder_fp8", &encoder_fp8, "fp8 (e4m3) entity encoder of the actor step: unit MLP, per-type GEMMs, pools "
+        "(per_unit: the one-unit-at-a-time workgroup form instead of the wave-parallel one)", py::arg("units"),
+        py::arg("env"), py::arg("w1"), py::arg("b1"), py::arg("wt"), py::arg("st"), py::arg("bt"), py::arg("we"),
+        py::arg("be"), py::arg("counts"), py::arg("per_unit") = false);
   m.def("actor_fp8", &actor_fp8, "fp8 (e4m3) actor policy core: pre-RNN + LSTM step + heads from x896",
         py::arg("x896"), py::arg("wpre"), py::arg("spre"), py::arg("bpre"), py::arg("wg"), py::arg("sg"), py::arg("bg"),
         py::arg("wh"), py::arg("sh"), py::arg("bh"), py::arg("h"), py::arg("c"), py::arg("keep"), py::arg("z"),

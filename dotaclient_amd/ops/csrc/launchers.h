@@ -32,7 +32,8 @@ hipError_t dca_actor_fp8(const short* x896, const void* wpre, const float* spre,
                          hipStream_t stream);
 hipError_t dca_encoder_fp8(const void* units, int f16, const float* env, const float* w1, const float* b1,
                            const void* wt, const float* st, const float* bt, const float* we, const float* be,
-                           short* x896, short* emb, int N, int U, const int* counts, hipStream_t stream);
+                           short* x896, short* emb, int N, int U, const int* counts, int per_unit,
+                           hipStream_t stream);
 
 hipError_t dca_dpre_dx(const float* dG, const void* w1h, const void* w1l, const float* x, const void* w2h,
                        const void* w2l, float* dpre, float* dx, int N, int K1, int X, int exact, int epi, hipStream_t stream);

@@ -84,11 +84,13 @@ def test_fp8_core_matches_quantised_emulation(gpu_ops):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('dtype,n', [(torch.float16, 100), (torch.float32, 4096)])
-def test_fp8_encoder_matches_quantised_emulation(gpu_ops, dtype, n):
-    """The fp8 entity encoder (ops/csrc/actor_fp8.hip encoder_fp8_kernel) against a torch emulation of the same
-    quantisation: basic per (row, unit) and W_τ per output channel in e4m3, fp32 products, bf16 outputs. Pools are
-    the max over the type's units of the emitted emb (bitwise: bf16 rounding is monotone)."""
+@pytest.mark.parametrize('dtype,n,per_unit', [(torch.float16, 100, False), (torch.float32, 4096, False),
+                                              (torch.float16, 100, True), (torch.float32, 4096, True)])
+def test_fp8_encoder_matches_quantised_emulation(gpu_ops, dtype, n, per_unit):
+    """The fp8 entity encoder (ops/csrc/actor_fp8.hip: the wave-parallel encoder_fp8w_kernel and the per-unit
+    encoder_fp8_kernel) against a torch emulation of the same quantisation: basic per (row, unit) and W_τ per output
+    channel in e4m3, fp32 products, bf16 outputs. Pools are the max over the type's units of the emitted emb
+    (bitwise: bf16 rounding is monotone)."""
     from dotaclient_amd.actor.batched import fp8_weight
     from dotaclient_amd.models.policy import TYPE_SUFFIX
     torch.manual_seed(0)
@@ -106,7 +108,8 @@ def test_fp8_encoder_matches_quantised_emulation(gpu_ops, dtype, n):
     bt = torch.stack([P[f'affine_unit_{s}.bias'] for s in TYPE_SUFFIX]).contiguous()
     x896, emb = gpu_ops.encoder_fp8(units, env, P['affine_unit_basic_stats.weight'].contiguous(),
                                     P['affine_unit_basic_stats.bias'], wt8, st8, bt,
-                                    P['affine_env.weight'].contiguous(), P['affine_env.bias'], counts)
+                                    P['affine_env.weight'].contiguous(), P['affine_env.bias'], counts,
+                                    per_unit=per_unit)
     torch.cuda.synchronize()
     # emulation
     basic = torch.relu(units.float() @ P['affine_unit_basic_stats.weight'].t() + P['affine_unit_basic_stats.bias'])
