@@ -149,6 +149,33 @@ class GpuActorPolicy:
                 return self._load_weights(policy_or_state)
         return self._load_weights(policy_or_state)
 
+    @torch.no_grad()
+    def weight_dict(self, policy_or_state):
+        """(operand set, ready event): the kernels' operands of these weights (casts, fragment images, fp8
+        quantisation), built on the step stream — for :meth:`load_weight_dict` of other policies of the same shape
+        (one build per weight version instead of one per policy)."""
+        sd = policy_or_state.state_dict() if isinstance(policy_or_state, torch.nn.Module) else policy_or_state
+        with torch.cuda.stream(self.stream):
+            w = self._weight_dict(sd)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        return w, ev
+
+    @torch.no_grad()
+    def load_weight_dict(self, w: Dict[str, torch.Tensor], ready: Optional[torch.cuda.Event] = None,
+                         producer: Optional[torch.cuda.Stream] = None):
+        """Copy a :meth:`weight_dict` operand set (built on ``producer``, complete at ``ready``) into this policy's
+        buffers, ordered on its step stream."""
+        other = producer is not None and producer != self.stream
+        with torch.cuda.stream(self.stream):
+            if ready is not None:
+                self.stream.wait_event(ready)
+            for k, v in w.items():
+                if isinstance(v, torch.Tensor):
+                    if other:
+                        v.record_stream(self.stream)   # the producer's allocator must not reuse it before this copy
+                    self.w[k].copy_(v)
+
     def _load_weights(self, policy_or_state):
         sd = policy_or_state.state_dict() if isinstance(policy_or_state, torch.nn.Module) else policy_or_state
         w = self._weight_dict(sd)

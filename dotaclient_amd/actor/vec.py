@@ -124,23 +124,42 @@ class VecActor:
         self.games_finished = 0
         self.rollouts_sent = 0
         self._primed = False      # group 0 has a step in flight
+        self._wcache = None       # (version, kernel operands, ready event, stream built on): shared by the groups
 
     # ------------------------------------------------------------------------------------------------
     def _version(self) -> int:
         return int(getattr(self.policy, 'weight_version', -1))
 
     def _sync_weights(self, g: _Group):
+        """Hot-swap the latest weights into the group's captured policy step. The kernels' operand set of a version
+        (H2D of the state dict, casts, fragment images / fp8 quantisation: tens of launches) is built ONCE per version
+        and copied into every group's buffers — the learner publishes every iteration, and building it per group was
+        host time taken from the host-bound actor loop."""
         v = self._version()
         if g.version == v:
             return
-        lock = getattr(self.store, '_lock', None)
-        if lock is not None:
-            with lock:
+        if not hasattr(g.gp, 'load_weight_dict'):
+            lock = getattr(self.store, '_lock', None)
+            if lock is not None:
+                with lock:
+                    g.gp.load_weights(self.policy)
+                    v = self._version()
+            else:
                 g.gp.load_weights(self.policy)
-                v = self._version()
-        else:
-            g.gp.load_weights(self.policy)
-        g.version = v
+            g.version = v
+            return
+        c = self._wcache
+        if c is None or c[0] != v:
+            lock = getattr(self.store, '_lock', None)
+            if lock is not None:
+                with lock:
+                    w, ev = g.gp.weight_dict(self.policy)
+                    v = self._version()
+            else:
+                w, ev = g.gp.weight_dict(self.policy)
+            c = self._wcache = (v, w, ev, g.gp.stream)
+        g.gp.load_weight_dict(c[1], ready=c[2], producer=c[3])
+        g.version = c[0]
 
     def _sample_opponent(self):
         if self.league is not None:
