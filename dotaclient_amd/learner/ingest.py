@@ -305,7 +305,9 @@ class IngestPipeline:
             rv[resets] = 1
         ev = None
         if self.cuda:
-            ev = torch.cuda.Event()
+            # blocking events: the stager waits on them (slot reuse) for up to an iteration, and a spinning wait
+            # burned a host core that the node's actor process needs
+            ev = torch.cuda.Event(blocking=True)
             with torch.cuda.stream(self.copy_stream):
                 if slot.consumed is not None:
                     self.copy_stream.wait_event(slot.consumed)    # the learner has expanded the slot's last contents
@@ -368,7 +370,7 @@ class IngestPipeline:
             out['reset'] = v['reset'].clone()
         slot = self.slots[st.slot]
         if cur is not None:
-            ev = torch.cuda.Event()
+            ev = torch.cuda.Event(blocking=True)
             ev.record(cur)
             slot.consumed = ev
         slot.free.release()
