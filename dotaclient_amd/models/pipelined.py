@@ -251,6 +251,10 @@ _HEADS_ROWMM = os.environ.get('DCA_HEADS_ROWMM', '1') != '0'
 # 2.50e-6, VPG 1.264e-5 vs 1.265e-5 where torch-fp32 itself is at 1.24e-5) and the fast form is 0.5 ms per step
 # faster (5.70 vs 6.20 ms)
 _EXACT_LIBM_ACT = os.environ.get('DCA_EXACT_ACT', 'fast') == 'libm'
+# exact learner, opt-in (DCA_FUSED_DW=1): ∂W_hh accumulated inside the backward recurrence instead of the gemm_tn
+# after it. Measured (profiles/r4_fused_dw_probe.md): the tail loses 330 µs but the recurrence gains 1.66 ms — the
+# 128 accumulators per lane live in AGPRs on the 4-wave form and their updates sit on every step's critical path
+_FUSED_DW = os.environ.get('DCA_FUSED_DW', '0') == '1'
 
 
 def fused_step_tm(fp, *args, **kw):
@@ -491,12 +495,20 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     sL.wait_event(heads_done)
     dh_n = dc_n = None
     bwd_done = []
+    # exact one-chunk step: the backward recurrence accumulates ∂W_hh itself (ops/csrc/lstm_team.hip, V1 + DW: per
+    # chain partials in PyTorch row order, summed below) instead of a gemm_tn over the B·S rows after it
+    fused_dw = (exact and one and _FUSED_DW
+                and C.lstm_team_bwd_fuses_dw(B, H, True, bool(exact and _EXACT_LIBM_ACT)))
+    dwp = None
     with torch.cuda.stream(sL):
+        if fused_dw:
+            dwp = torch.empty(C.lstm_team_chains(B, True), 4 * H, H, device=dev)
         for t0, t1 in reversed(spans):
             cinit = c0.contiguous() if t0 == 0 else cs[t0 - 1]
+            dwk = dict(hs_f32=hs16, h0=h016, dw_out=dwp) if fused_dw else {}
             o = team_bwd(C, dxh[t0:t1], gates4[t0:t1], cs[t0:t1], cinit, dh_n, dc_n, whh16, fp.err,
                          time_major=True, dg_out=dgates16[t0:t1], dg_bf16=not f32,
-                         want_dbias=True, precise=exact and _EXACT_LIBM_ACT, reset=rst)
+                         want_dbias=True, precise=exact and _EXACT_LIBM_ACT, reset=rst, **dwk)
             dh_n, dc_n = o[1], o[2]
             db = _acc(db, o[3])
             e = torch.cuda.Event()
@@ -515,7 +527,11 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         n = r1 - r0
         dG16 = dgates16[t0:t1].view(n, 4 * H)
         with torch.cuda.stream(sL if wg_side else main):
-            if rst is not None:
+            if fused_dw:
+                dWhh.add_(dwp.sum(0))                # the chains' ∂W_hh partials (fixed order: chain index)
+                if not wg_side:
+                    dwp.record_stream(main)
+            elif rst is not None:
                 # packed: the h_{t-1} operand is zero where an episode starts at t (the forward never used it)
                 hprev = torch.cat([h016.unsqueeze(0), hs16[:S - 1]], 0).masked_fill_(rst.bool().unsqueeze(2), 0.0)
                 gemm_tn(dG16, hprev.view(n, H), out=dWhh, perm=gperm, accumulate=True)

@@ -213,7 +213,9 @@ std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4
                                          c10::optional<torch::Tensor> dcn, torch::Tensor whh, torch::Tensor err,
                                          torch::Tensor ctl, c10::optional<torch::Tensor> trace, bool time_major,
                                          c10::optional<torch::Tensor> dg_out, bool dg_bf16, bool want_dbias,
-                                         bool precise, c10::optional<torch::Tensor> reset) {
+                                         bool precise, c10::optional<torch::Tensor> reset,
+                                         c10::optional<torch::Tensor> hs_f32, c10::optional<torch::Tensor> h0,
+                                         c10::optional<torch::Tensor> dw_out) {
   CHECK_F32(dhs); CHECK_F32(gates4); CHECK_F32(cs); CHECK_F32(c0); CHECK_DEV(whh); CHECK_CONTIG(whh); CHECK_I32(err);
   check_ctl(ctl);
   const bool f32w = whh.scalar_type() == at::kFloat;
@@ -241,13 +243,31 @@ std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4
   torch::Tensor dbp = want_dbias ? torch::empty({dca_lstm_team_chains(B, f32w ? 1 : 0), 4 * H}, f32) : torch::Tensor();
   const size_t wsb = dca_lstm_team_workspace(B, H, 1, f32w ? 1 : 0);
   auto ws = torch::empty({(int64_t)wsb}, f32.dtype(at::kByte));
+  // fused ∂W_hh (V2 variant): per-chain partials (chains, 4H, H) in PyTorch row order, summed by the caller
+  const float* hsf_p = nullptr;
+  const float* h0_p = nullptr;
+  float* dw_p = nullptr;
+  if (dw_out.has_value() && dw_out->defined()) {
+    TORCH_CHECK(hs_f32.has_value() && hs_f32->defined() && h0.has_value() && h0->defined(),
+                "lstm_team_bwd: dw_out needs hs_f32 and h0");
+    CHECK_F32((*dw_out)); CHECK_F32((*hs_f32)); CHECK_F32((*h0));
+    TORCH_CHECK(hs_f32->sizes() == dhs.sizes(), "lstm_team_bwd: hs_f32 must match dhs");
+    TORCH_CHECK(h0->size(0) == B && h0->size(1) == H, "lstm_team_bwd: h0 must be (B,H)");
+    TORCH_CHECK(dw_out->numel() == (int64_t)dca_lstm_team_chains(B, f32w ? 1 : 0) * 4 * H * H,
+                "lstm_team_bwd: dw_out must hold (chains, 4H, H)");
+    TORCH_CHECK(dca_lstm_team_bwd_fuses_dw(B, H, f32w ? 1 : 0, precise ? 1 : 0),
+                "lstm_team_bwd: this shape / precision does not take the fused-dW variant");
+    hsf_p = ptr<float>(*hs_f32);
+    h0_p = ptr<float>(*h0);
+    dw_p = ptr<float>(*dw_out);
+  }
   hip_check(dca_lstm_team_bwd(ptr<float>(dhs), ptr<float>(gates4), ptr<float>(cs), ptr<float>(c0), dhn_p, dcn_p,
                               whh.data_ptr(), dg_bf16 ? nullptr : ptr<float>(dgates4), ptr<float>(dh0),
                               ptr<float>(dc0), ctl.data_ptr(), ws.data_ptr(), wsb, ptr<unsigned>(err), B, S, H,
                               time_major ? 1 : 0, cur_stream(),
                               (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr,
                               dg_bf16 ? ptr<short>(dgates4) : nullptr, want_dbias ? ptr<float>(dbp) : nullptr,
-                              f32w ? 1 : 0, precise ? 1 : 0, reset_ptr(reset, B, S)),
+                              f32w ? 1 : 0, precise ? 1 : 0, reset_ptr(reset, B, S), hsf_p, h0_p, dw_p),
             "dca_lstm_team_bwd");
   if (want_dbias) return {dgates4, dh0, dc0, dbp.sum(0)};
   return {dgates4, dh0, dc0};
@@ -1163,7 +1183,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dhs"), py::arg("gates4"), py::arg("cs"), py::arg("c0"), py::arg("dhn"), py::arg("dcn"),
         py::arg("whh"), py::arg("err"), py::arg("ctl"), py::arg("trace") = py::none(),
         py::arg("time_major") = false, py::arg("dg_out") = py::none(), py::arg("dg_bf16") = false,
-        py::arg("want_dbias") = false, py::arg("precise") = false, py::arg("reset") = py::none());
+        py::arg("want_dbias") = false, py::arg("precise") = false, py::arg("reset") = py::none(),
+        py::arg("hs_f32") = py::none(), py::arg("h0") = py::none(), py::arg("dw_out") = py::none());
+  m.def("lstm_team_bwd_fuses_dw", [](int64_t B, int64_t H, bool f32, bool precise) {
+          return dca_lstm_team_bwd_fuses_dw((int)B, (int)H, f32 ? 1 : 0, precise ? 1 : 0) != 0;
+        }, "whether lstm_team_bwd of (B, H) runs the variant that accumulates dW_hh itself (dw_out)",
+        py::arg("B"), py::arg("H"), py::arg("f32"), py::arg("precise") = false);
+  m.def("lstm_team_chains", [](int64_t B, bool f32) { return dca_lstm_team_chains((int)B, f32 ? 1 : 0); },
+        "sequence chains of a team-recurrence launch of B sequences", py::arg("B"), py::arg("f32"));
   m.def("sample_actions", &sample_actions, "fused masked hierarchical Gumbel-max action sampling (actor)");
   m.def("actor_state_prep", &actor_state_prep, "actor step: state resets + [x | bf16(h)] gate-GEMM operand",
         py::arg("pre"), py::arg("h"), py::arg("c"), py::arg("keep"), py::arg("xh"), py::arg("bump") = py::none());

@@ -84,7 +84,9 @@ hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, const float*
                              const float* dhn, const float* dcn, const void* whh, float* dgates4, float* dh0,
                              float* dc0, void* ctl, void* ws, size_t ws_bytes, unsigned* err, int B, int S, int H,
                              int time_major, hipStream_t st, unsigned long long* trace, short* dg16, float* dbpart,
-                             int f32, int precise = 0, const unsigned char* rst = nullptr);
+                             int f32, int precise = 0, const unsigned char* rst = nullptr, const float* hsf = nullptr,
+                             const float* h0 = nullptr, float* dwpart = nullptr);
+int dca_lstm_team_bwd_fuses_dw(int B, int H, int f32, int precise);
 
 hipError_t dca_sample_actions(const float* z, int ldz, const short* emb, const void* handles, int h32, int N, int U,
                               unsigned long long seed, const long long* ctr, int* idx, unsigned char* act,

@@ -141,6 +141,35 @@ __device__ __forceinline__ void pk_dot4(const float* wq, const float* x, float& 
   const f32x2 a01 = a01e + a01o, a23 = a23e + a23o;
   o0 = a01.x; o1 = a01.y; o2 = a23.x; o3 = a23.y;
 }
+// pk_dot4 plus the ∂W_hh update of the same slice: dw[j] += x[j]·(h0, h1), dw[KSL + j] += x[j]·(h2, h3) (h = 0
+// leaves dw unchanged; unit pairs in register pairs for v_pk_fma_f32) — the slice values feed both as they arrive
+// from LDS, so the update needs no registers beyond its accumulators
+template <int KSL>
+__device__ __forceinline__ void pk_dot4_dw(const float* wq, const float* x, const float4 h, f32x2* dw, float& o0,
+                                           float& o1, float& o2, float& o3) {
+  f32x2 a01e = {0.f, 0.f}, a01o = {0.f, 0.f}, a23e = {0.f, 0.f}, a23o = {0.f, 0.f};
+  const f32x2 h01 = {h.x, h.y}, h23 = {h.z, h.w};
+#pragma unroll
+  for (int j = 0; j < KSL; j += 4) {
+    const float4 v = *reinterpret_cast<const float4*>(x + j);
+    a01e = __builtin_elementwise_fma(f32x2{wq[j], wq[KSL + j]}, f32x2{v.x, v.x}, a01e);
+    a23e = __builtin_elementwise_fma(f32x2{wq[2 * KSL + j], wq[3 * KSL + j]}, f32x2{v.x, v.x}, a23e);
+    a01o = __builtin_elementwise_fma(f32x2{wq[j + 1], wq[KSL + j + 1]}, f32x2{v.y, v.y}, a01o);
+    a23o = __builtin_elementwise_fma(f32x2{wq[2 * KSL + j + 1], wq[3 * KSL + j + 1]}, f32x2{v.y, v.y}, a23o);
+    a01e = __builtin_elementwise_fma(f32x2{wq[j + 2], wq[KSL + j + 2]}, f32x2{v.z, v.z}, a01e);
+    a23e = __builtin_elementwise_fma(f32x2{wq[2 * KSL + j + 2], wq[3 * KSL + j + 2]}, f32x2{v.z, v.z}, a23e);
+    a01o = __builtin_elementwise_fma(f32x2{wq[j + 3], wq[KSL + j + 3]}, f32x2{v.w, v.w}, a01o);
+    a23o = __builtin_elementwise_fma(f32x2{wq[2 * KSL + j + 3], wq[3 * KSL + j + 3]}, f32x2{v.w, v.w}, a23o);
+    const float xv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      dw[j + q] = __builtin_elementwise_fma(f32x2{xv[q], xv[q]}, h01, dw[j + q]);
+      dw[KSL + j + q] = __builtin_elementwise_fma(f32x2{xv[q], xv[q]}, h23, dw[KSL + j + q]);
+    }
+  }
+  const f32x2 a01 = a01e + a01o, a23 = a23e + a23o;
+  o0 = a01.x; o1 = a01.y; o2 = a23.x; o3 = a23.y;
+}
 // Σ over the 16 lanes of this lane's DPP row, result in every lane: xor 1, xor 2 (quad_perm), half-row and row mirrors
 __device__ __forceinline__ float row_sum16(float v) {
   v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
@@ -645,7 +674,8 @@ __device__ __forceinline__ void lstm_team_bwd_body(
     const void* __restrict__ whh_, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
     i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
     unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart, int knobs,
-    const unsigned char* __restrict__ rst) {
+    const unsigned char* __restrict__ rst, const float* __restrict__ hsf, const float* __restrict__ h0,
+    float* __restrict__ dwpart) {
   constexpr int H = 128 * KS;
   constexpr int U = H / kT;             // 4·KS units per workgroup (MFMA N, zero-padded to 16)
   constexpr int VV = VAR & 3;
@@ -661,6 +691,16 @@ __device__ __forceinline__ void lstm_team_bwd_body(
   constexpr int KSL = KW / 16;          // V1: K slice per lane of a wave's K part
   static_assert(!V1 || (F32 && MT == 1), "V1 is the fp32 one-row variant");
   static_assert(VV != 2 || H == 512, "V2 is the H = 512 variant");
+  // V1 + DW: ∂W_hh fused into the recurrence. Lane (wv, u-group, slice) owns ∂W_hhᵀ for exactly the (gate column, unit)
+  // pairs whose W_hhᵀ it holds in wq: Σ_t dG_{t+1}[gc]·h_t[j0 + unit] accumulated in fp32 FMAs (descending t) in the
+  // dot phase, from the same LDS reads as the partial recurrent gradient. It runs on the 4-wave V1 form: one wave per
+  // SIMD has 512 registers for wq + the 128 accumulators (on the 8-wave V2, 256 per wave, even a bare 64-accumulator
+  // loop spilled 33 registers). MEASURED SLOWER, opt-in only (models/pipelined.py DCA_FUSED_DW=1): 3755 vs 2091 µs
+  // for the backward at B = 8, S = 1400 (the accumulators land in AGPRs: copies + FMAs on every step's critical
+  // path), against 330 µs saved in the tail — 7.03 vs 5.59 ms per step. Per chain the slice goes to
+  // dwpart[chain] (PyTorch row order); the caller sums the chains. It replaces the ∂W_hh GEMM after the recurrence
+  // (gemm_tn over B·S rows: 220 µs alone, ≈400 µs beside the tail's other kernels).
+  constexpr bool DW = VV == 1 && (VAR & 8) != 0;   // (a template variant: the plain variants keep their registers)
   __shared__ short dgl[V1 ? 1 : RB][V1 ? 1 : GP];
   __shared__ short dglo[F32 && !V1 ? RB : 1][F32 && !V1 ? GP : 1];   // F32: lo bf16 half of the gathered dG
   // V1: dG_{t+1} of row 0, fp32, as 64 K slices each padded by 4 floats (bank spread, as forward)
@@ -746,10 +786,22 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       dcarry[i] = (pi < B * U && dcn) ? dcn[(size_t)(b0 + pi / U) * H + j0 + pi % U] : 0.f;
     }
     bool dead = false;
+    // ∂W_hhᵀ[gc_j][j0 + 4·(lane>>4) + uu]: units (0, 1) at dwq[j], units (2, 3) at dwq[KSL + j]
+    f32x2 dwq[DW ? 2 * KSL : 1];
+#pragma unroll
+    for (int i = 0; i < (DW ? 2 * KSL : 1); ++i) dwq[i] = f32x2{0.f, 0.f};
     for (int k = 0; k <= S; ++k) {
       const int t = S - 1 - k;          // step whose gate gradients are produced this iteration (-1: final)
       if ((knobs >> 12) & 1) spins = 0;
       TSTAMPB(0);
+      // ∂W_hh operand of this iteration: h_t of the lane's 4 units (h0 for t = -1); an episode starting at t+1 never
+      // read h_t, so its term is skipped (the recurrent gradient skips it the same way)
+      float4 hq = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (DW && k > 0) {
+        const size_t hr = t >= 0 ? ((size_t)b0 * sb + (size_t)t * st) * H : (size_t)b0 * H;
+        hq = *reinterpret_cast<const float4*>((t >= 0 ? hsf : h0) + hr + j0 + 4 * (lane >> 4));
+        if (rst != nullptr && rst[(size_t)b0 * sb + (size_t)(t + 1) * st] != 0) hq = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
       // ---- prefetch the saved activations of step t for the owned pairs
       dca::f32x4 gv[NPAIR];
       float cv[NPAIR], cpv[NPAIR], dv[NPAIR];
@@ -830,7 +882,8 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       // ---- partial recurrent gradient over this wave's K quarter → red[wv]
       if (V1 && k > 0) {
         float o0, o1, o2, o3;
-        pk_dot4<KSL>(wq, &dgf[(wv * 16 + (lane & 15)) * SP], o0, o1, o2, o3);
+        if constexpr (DW) pk_dot4_dw<KSL>(wq, &dgf[(wv * 16 + (lane & 15)) * SP], hq, dwq, o0, o1, o2, o3);
+        else pk_dot4<KSL>(wq, &dgf[(wv * 16 + (lane & 15)) * SP], o0, o1, o2, o3);
         o0 = row_sum16(o0);
         o1 = row_sum16(o1);
         o2 = row_sum16(o2);
@@ -929,6 +982,15 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       TSTAMPB(6);
     }
     if (sh_int == -2) return;
+    if constexpr (DW) {
+      // this chain's ∂W_hh slice → dwpart[chain] in PyTorch's gate-major rows (gate q of unit i at row q·H + i)
+#pragma unroll
+      for (int j = 0; j < KSL; ++j) {
+        const int gc = wv * KW + (lane & 15) * KSL + j;
+        *reinterpret_cast<float4*>(dwpart + ((size_t)chain * 4 * H + (size_t)((gc & 3) * H + (gc >> 2))) * H + j0 +
+                                   4 * (lane >> 4)) = make_float4(dwq[j].x, dwq[j].y, dwq[KSL + j].x, dwq[KSL + j].y);
+      }
+    }
     if (dbpart) {
       // bias gradient of this chain for the owned units: Σ over rows (fixed order) of the per-pair sums
 #pragma unroll
@@ -970,10 +1032,11 @@ __global__ __launch_bounds__((VAR & 3) == 2 ? 512 : kThreads, 1) void lstm_team_
     const void* __restrict__ whh, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
     i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
     unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart, int knobs,
-    const unsigned char* __restrict__ rst) {
+    const unsigned char* __restrict__ rst, const float* __restrict__ hsf, const float* __restrict__ h0,
+    float* __restrict__ dwpart) {
   __builtin_amdgcn_s_setprio(3);
   lstm_team_bwd_body<MT, KS, F32, VAR>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, dh0, dc0, xg_all, ctl, err, Btot, Bc, nch,
-                             S, sb, st, trace, dg16, dbpart, knobs, rst);
+                             S, sb, st, trace, dg16, dbpart, knobs, rst, hsf, h0, dwpart);
   team_exit(ctl, err, nch);
 }
 
@@ -1034,6 +1097,15 @@ inline int use_v1(int f32, int Bc, int H, int backward, int precise) {
 }
 inline int team_threads(int var) { return (var & 3) == 2 ? 512 : kThreads; }
 
+// 1 when a backward launch of (B, H) can accumulate ∂W_hh itself (dwpart / hsf / h0): one-row exact fp32 chains
+// at H = 512, on the 4-wave V1 form (DCA_TEAM_FUSED_DW=0 keeps the weight-gradient GEMM)
+extern "C" int dca_lstm_team_bwd_fuses_dw(int B, int H, int f32, int precise) {
+  static const bool off = [] { const char* e = getenv("DCA_TEAM_FUSED_DW"); return e && e[0] == '0'; }();
+  int nch, Bc, MT;
+  plan(B, nch, Bc, MT, f32);
+  return !off && H == 512 && (use_v1(f32, Bc, H, 1, precise) & 3) != 0 ? 1 : 0;
+}
+
 // Workspace bytes (control block + per-team exchange buffers) for a launch of (B, H).
 extern "C" size_t dca_lstm_team_ctl_bytes() { return 256; }
 
@@ -1082,8 +1154,10 @@ extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, c
                                         float* dh0, float* dc0, void* ctl_mem, void* ws, size_t ws_bytes,
                                         unsigned* err, int B, int S, int H, int time_major, hipStream_t stream,
                                         unsigned long long* trace, short* dg16, float* dbpart, int f32, int precise,
-                                        const unsigned char* rst) {
+                                        const unsigned char* rst, const float* hsf, const float* h0, float* dwpart) {
   if (B < 1 || S < 1 || S >= 65534 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
+  if (dwpart != nullptr && (hsf == nullptr || h0 == nullptr || !dca_lstm_team_bwd_fuses_dw(B, H, f32, precise)))
+    return hipErrorInvalidValue;
   if (dgates4 == nullptr && dg16 == nullptr) return hipErrorInvalidValue;
   if (f32 && dgates4 == nullptr) return hipErrorInvalidValue;
   if (ws_bytes < dca_lstm_team_workspace(B, H, 1, f32) || ctl_mem == nullptr) return hipErrorInvalidValue;
@@ -1097,8 +1171,12 @@ extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, c
   (lstm_team_bwd_kernel<mt, ks, f, v><<<kMaxTeams * kT, team_threads(v), 0, stream>>>(dhs, gates4, cs, c0, dhn, dcn, whh,      \
                                                                           dgates4, dh0, dc0, xb, ctl, err, B, Bc,  \
                                                                           nch, S, sb, st, trace, dg16, dbpart,      \
-                                                                          team_knobs(), rst),                      \
+                                                                          team_knobs(), rst, hsf, h0, dwpart),     \
    hipGetLastError())
+  if (dwpart != nullptr) {   // the fused-∂W_hh V1 instances (checked above: H = 512, one-row fp32 chains)
+    if (precise) return DCA_B(1, 4, true, 13);
+    return DCA_B(1, 4, true, 9);
+  }
   DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc, H, 1, precise), DCA_B)
 #undef DCA_B
 }
