@@ -88,11 +88,11 @@ def parse():
                     help='pin this rank (learner threads + its actor process) to its GPU-local CPU share')
     ap.add_argument('--e2e', type=float, default=20.0,
                     help='seconds of the end-to-end actors→queue→learners loop on every rank (0 = off)')
-    # node-loop actor shape (scripts/e2e_ab.py on one MI355X, 15 s each: 2048 games × 12 threads 1.40 M steps/s
-    # (527 k valid), 1024 × 14 1.23 M (508 k): the learner process's stager / decode threads share the host cores)
+    # node-loop actor shape (scripts/e2e_ab.py on one MI355X, 15 s each, after the round-4 host-loop fixes: 2048 games
+    # × 14 threads 1.04 M steps/s (0.89 M valid), × 12 threads 0.91 M, 1024 × 12 0.84 M — same box, same minute)
     ap.add_argument('--e2e-games', type=int, default=2048)
     ap.add_argument('--e2e-threads', type=int, default=0,
-                    help='actor host threads of the node loop (0 = from the CPU share, clamped to [2, 12])')
+                    help='actor host threads of the node loop (0 = from the CPU share, clamped to [2, 14])')
     ap.add_argument('--e2e-mode', default='process', choices=['process', 'thread'],
                     help='e2e actors as one spawned process per rank over the node broker (deploy split) or as a '
                          'thread (1 GPU only)')
@@ -135,7 +135,7 @@ def main():
     if not args.actor_threads:
         args.actor_threads = min(14, place.threads(reserve=2, minimum=2))
     if not args.e2e_threads:
-        args.e2e_threads = min(12, place.threads(reserve=4, minimum=2))
+        args.e2e_threads = min(14, place.threads(reserve=2, minimum=2))
     host = dict(place.describe(), actor_threads=args.actor_threads, e2e_threads=args.e2e_threads)
     if world > 1:
         from dotaclient_amd.parallel.dist import init_distribution
