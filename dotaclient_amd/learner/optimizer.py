@@ -620,8 +620,14 @@ class DotaOptimizer:
         pool = self._iteration_pool(data, n) if (self.replay is None and self.learner.direct()) else None
         for ep in range(cfg.epochs if self.replay is None else 0):
             perm = torch.randperm(n, generator=g)
+            if cuda:
+                # one pinned, non-blocking upload per epoch: a pageable .to(device) per minibatch made the host wait
+                # for the GPU to drain every previous step before it could enqueue the next (a bubble per step)
+                perm = perm.pin_memory().to(self.device, non_blocking=True)
             for b0 in range(0, n, cfg.batch_size):
-                idx = perm[b0:b0 + cfg.batch_size].to(self.device)
+                idx = perm[b0:b0 + cfg.batch_size]
+                if not cuda:
+                    idx = idx.to(self.device)
                 if pool is not None:
                     # the captured step gathers its minibatch time-major from the pool itself (replay_gather)
                     m = self.learner.train_step_indices(pool, idx)
