@@ -6,4 +6,4 @@ export TMPDIR=/tmp
 timeout -k 10 700 python -u -m pytest tests -m gpu -x -q --timeout 250 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1 && \
 timeout -k 10 240 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 && \
 timeout -k 10 400 python -u bench.py > gpurun_out/bench_final.log 2> gpurun_out/bench_final.err && \
-bash scripts/prof_1v1.sh && bash scripts/prof_5v5.sh
+bash scripts/prof_exact.sh profx && bash scripts/prof_1v1.sh && bash scripts/prof_5v5.sh
