@@ -93,6 +93,8 @@ def parse():
     ap.add_argument('--e2e-games', type=int, default=2048)
     ap.add_argument('--e2e-threads', type=int, default=0,
                     help='actor host threads of the node loop (0 = from the CPU share, clamped to [2, 14])')
+    ap.add_argument('--e2e-actor-procs', type=int, default=1,
+                    help='actor processes per rank in the node loop (games and threads split over them)')
     ap.add_argument('--e2e-mode', default='process', choices=['process', 'thread'],
                     help='e2e actors as one spawned process per rank over the node broker (deploy split) or as a '
                          'thread (1 GPU only)')
@@ -366,7 +368,7 @@ def main():
             progress('e2e start')
             if args.e2e_mode == 'process':
                 e2e = measure_e2e_node(transport=args.e2e_transport, progress=progress, idle_probe=args.e2e_probe,
-                                       **kw)
+                                       actor_procs=args.e2e_actor_procs, **kw)
             else:
                 e2e = measure_e2e(**kw)
         except Exception as e:

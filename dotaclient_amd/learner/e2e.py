@@ -227,7 +227,7 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                      transport: str = 'auto', backend: str = 'auto', idle_probe: float = 3.0,
                      report=None, record_consumed: int = 0, progress=None, pack: bool = False,
                      league: Optional[str] = None, latest_weights_prob: float = 1.0, actor_precision: str = 'bf16',
-                     replay_gb: float = 0.0) -> Dict[str, float]:
+                     replay_gb: float = 0.0, actor_procs: int = 1) -> Dict[str, float]:
     """The reference's node topology end to end (optimizer.py:144-150, 274-287; ks-app/components/optimizer.jsonnet:
     79-174): ONE experience queue per node fed by actor processes, ``WORLD_SIZE`` learner ranks (one per GPU, DDP
     over RCCL) consuming disjoint rollouts from it as competing consumers, and rank 0 alone checkpointing and
@@ -246,7 +246,11 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
 
     BASELINE config 5 (``league='pfsp'``, ``actor_precision='fp8'``, ``replay_gb`` > 0): the actors play a PFSP
     self-play league on the fp8 policy step and every learner trains from an on-HBM replay of ``replay_gb`` GB
-    (learner/replay.py) instead of the iteration's fresh rollouts only."""
+    (learner/replay.py) instead of the iteration's fresh rollouts only.
+
+    ``actor_procs`` > 1 splits each rank's ``games`` and ``threads`` over that many actor processes (each with its own
+    interpreter, GIL and graphs on the rank's GPU): the actor loop's Python between its native parallel regions is
+    serial per process."""
     import multiprocessing as mp
     import os
     import torch.distributed as tdist
@@ -288,8 +292,17 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
 
     tmp = log_dir or tempfile.mkdtemp(prefix='dca_e2e_')
     ctx = mp.get_context('spawn')
-    stop, ready, failed = ctx.Event(), ctx.Event(), ctx.Event()
-    steps = ctx.Value('q', 0)
+    stop, failed = ctx.Event(), ctx.Event()
+    K = max(1, int(actor_procs))
+    readies = [ctx.Event() for _ in range(K)]
+    counters = [ctx.Value('q', 0) for _ in range(K)]
+
+    class _Sum:                     # the actor processes' step counters as one (the probes read ``.value``)
+        @property
+        def value(self):
+            return sum(c.value for c in counters)
+    steps = _Sum()
+    procs = []
     proc = opt = None
     rows, wall, actor_steps, idle, gpu_busy = [], 0.0, 0, float('nan'), float('nan')
     err = None
@@ -300,11 +313,16 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
     try:
         # the actor starts first (interpreter + engine + graph capture overlap the learner's construction) and
         # waits for rank 0's model version 0
-        proc = ctx.Process(target=_actor_process_main, name=f'e2e-actor-{rank}', daemon=True,
-                           args=(addr, model, games, threads, seq_len, rollout_size, max_dota_time, str(device),
-                                 11 + 7919 * rank, stop, ready, steps, failed, f'a{rank}', league,
-                                 latest_weights_prob, actor_precision))
-        proc.start()
+        for k in range(K):
+            g_k = games // K + (1 if k < games % K else 0)
+            t_k = max(1, threads // K)
+            proc = ctx.Process(target=_actor_process_main, name=f'e2e-actor-{rank}-{k}', daemon=True,
+                               args=(addr, model, g_k, t_k, seq_len, rollout_size, max_dota_time, str(device),
+                                     11 + 7919 * rank + 104729 * k, stop, readies[k], counters[k], failed,
+                                     f'a{rank}' if K == 1 else f'a{rank}_{k}', league, latest_weights_prob,
+                                     actor_precision))
+            proc.start()
+            procs.append(proc)
         cfg = OptimizerConfig(log_dir=tmp, epochs=epochs, seq_per_epoch=seq_per_epoch, batch_size=batch_size,
                               seq_len=seq_len, model=model, precision=precision, device=str(device),
                               backend=backend, checkpoint_keep=2, run_local=True, xp_timeout=120.0,
@@ -313,7 +331,8 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                               replay_gb=replay_gb)
         opt = DotaOptimizer(cfg, broker, checkpoint=rank == 0)     # rank 0 publishes model version 0
         say(f'e2e: learner ready ({transport} broker {addr}); waiting for the actor process')
-        if not ready.wait(timeout=900) or failed.is_set():
+        t_ready = time.time() + 900
+        if not all(r.wait(timeout=max(1.0, t_ready - time.time())) for r in readies) or failed.is_set():
             raise RuntimeError('e2e actor process failed to start')
         if pdist.is_distributed():
             tdist.barrier()
@@ -335,8 +354,9 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                 say(f'e2e: busy-GPU actor probe {gpu_busy:.0f} player-steps/s')
 
         def check():
-            if failed.is_set() or not proc.is_alive():
-                return RuntimeError(f'e2e actor process died (exit code {proc.exitcode})')
+            for p in procs:
+                if failed.is_set() or not p.is_alive():
+                    return RuntimeError(f'e2e actor process died (exit code {p.exitcode})')
             return None
 
         d0 = dropped_total()
@@ -354,15 +374,15 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
         raise
     finally:
         stop.set()
-        if proc is not None:
-            proc.join(timeout=120)
-            if proc.is_alive():
-                proc.kill()
-                proc.join(timeout=10)
+        for p in procs:
+            p.join(timeout=120)
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
                 if err is None:
                     err = RuntimeError('e2e actor process did not exit')
-            elif proc.exitcode != 0 and err is None:
-                err = RuntimeError(f'e2e actor process exited with status {proc.exitcode}')
+            elif p.exitcode != 0 and err is None:
+                err = RuntimeError(f'e2e actor process exited with status {p.exitcode}')
         if broker is not owner and hasattr(broker, 'close'):
             broker.close()
         if pdist.is_distributed() and err is None:
@@ -405,7 +425,8 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
     out['config'] = dict(batch_size=batch_size, seq_len=seq_len, seq_per_epoch=seq_per_epoch, epochs=epochs,
                          rollout_size=rollout_size, max_dota_time=max_dota_time, precision=precision,
                          prefetch_rollouts=prefetch, games_per_rank=games, pack_sequences=pack,
-                         actor=f'one process per rank over the node {transport} broker', learners=world,
+                         actor=(f'one process per rank over the node {transport} broker' if K == 1 else
+                                f'{K} processes per rank over the node {transport} broker'), learners=world,
                          league=league, latest_weights_prob=latest_weights_prob, actor_precision=actor_precision,
                          replay_gb=replay_gb,
                          replay_sequences=(len(opt.replay) if opt is not None and opt.replay is not None else 0),
