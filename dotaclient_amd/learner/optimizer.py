@@ -303,10 +303,11 @@ class DotaOptimizer:
         in bounded slices so that :meth:`close` ends the thread promptly instead of leaving it blocked inside the
         broker; returns None once ``stop`` is set."""
         broker = getattr(self, '_xp_broker', None) or self.broker
+        consume = getattr(broker, 'consume_experience_view', None) or broker.consume_experience
         total = self.cfg.xp_timeout
         while True:
             if stop is None:
-                body = broker.consume_experience(timeout=total)
+                body = consume(timeout=total)
             else:
                 t0 = time.monotonic()
                 body = None
@@ -314,7 +315,7 @@ class DotaOptimizer:
                     left = None if total is None else total - (time.monotonic() - t0)
                     if left is not None and left <= 0:
                         break
-                    body = broker.consume_experience(timeout=0.25 if left is None else min(0.25, left))
+                    body = consume(timeout=0.25 if left is None else min(0.25, left))
                 if body is None and stop.is_set():
                     return None
             if body is None:

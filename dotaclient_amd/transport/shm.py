@@ -36,6 +36,11 @@ class ShmBroker:
     def consume_experience(self, timeout: Optional[float] = None) -> Optional[bytes]:
         return self.ring.pop(-1.0 if timeout is None else float(timeout))
 
+    def consume_experience_view(self, timeout: Optional[float] = None):
+        """:meth:`consume_experience` as a uint8 numpy array owning the message (no bytes copy under the GIL);
+        the learner's decode thread takes this form when the broker offers it."""
+        return self.ring.pop_view(-1.0 if timeout is None else float(timeout))
+
     @property
     def xp_queue_size(self) -> int:
         return int(self.ring.size())
