@@ -93,6 +93,9 @@ def parse():
     ap.add_argument('--e2e-games', type=int, default=2048)
     ap.add_argument('--e2e-threads', type=int, default=0,
                     help='actor host threads of the node loop (0 = from the CPU share, clamped to [2, 14])')
+    ap.add_argument('--e2e-actor-precision', default='bf16', choices=['bf16', 'fp8'],
+                    help='policy step of the node loop\'s actors (fp8: the BASELINE config-5 step; the loop measured '
+                         '1.15-1.20 vs ≈1.0 M steps/s, its kernels co-run better beside the learner\'s recurrence)')
     ap.add_argument('--e2e-actor-procs', type=int, default=1,
                     help='actor processes per rank in the node loop (games and threads split over them)')
     ap.add_argument('--e2e-mode', default='process', choices=['process', 'thread'],
@@ -368,7 +371,8 @@ def main():
             progress('e2e start')
             if args.e2e_mode == 'process':
                 e2e = measure_e2e_node(transport=args.e2e_transport, progress=progress, idle_probe=args.e2e_probe,
-                                       actor_procs=args.e2e_actor_procs, **kw)
+                                       actor_procs=args.e2e_actor_procs, actor_precision=args.e2e_actor_precision,
+                                       **kw)
             else:
                 e2e = measure_e2e(**kw)
         except Exception as e:
