@@ -85,7 +85,11 @@ __device__ __forceinline__ bf16x8 gfrag(const short* __restrict__ w, int m0, int
   return *reinterpret_cast<const bf16x8*>(w + ((size_t)((m0 >> 4) * (kD / 32) + (k0 >> 5)) * 64 + lane) * 8);
 }
 
-__global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P) {
+// MINB: workgroups per CU the register budget is cut for (2: 256 VGPRs; 1: 512, one row in flight per CU with the
+// phase-B weight fragments double-buffered one k-step ahead — DCA_ATTN_FWD_1WG=1, an A/B knob). Measured slower:
+// 5v5 step 8.45 vs 8.15 ms (two rows in flight per CU hide more than the prefetch does).
+template <int MINB>
+__global__ __launch_bounds__(256, MINB) void attn_block_fwd_f32_kernel(BlockArgs P) {
   __shared__ __attribute__((aligned(16))) short img_h[kU * kPX], img_l[kU * kPX];   // Xn, then O (hi / lo)
   __shared__ __attribute__((aligned(16))) float e1s[kU * kPE];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, kg = lane >> 4, li = lane & 15;
@@ -152,6 +156,43 @@ __global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P)
       kt[c][a] = f32x4{0.f, 0.f, 0.f, 0.f};
       vv[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+  if constexpr (MINB == 1) {
+    // one workgroup per CU: the 12 weight fragments of k-step ks+1 load while ks computes (double-buffered)
+    bf16x8 wb[2][2][6];
+    auto wload = [&](bf16x8 (&w)[2][6], int ks) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int rq = kHd * h + 16 * c;
+        w[c][0] = gfrag(P.wqh, rq, 32 * ks, lane);
+        w[c][1] = gfrag(P.wql, rq, 32 * ks, lane);
+        w[c][2] = gfrag(P.wqh, 128 + rq, 32 * ks, lane);
+        w[c][3] = gfrag(P.wql, 128 + rq, 32 * ks, lane);
+        w[c][4] = gfrag(P.wqh, 256 + rq, 32 * ks, lane);
+        w[c][5] = gfrag(P.wql, 256 + rq, 32 * ks, lane);
+      }
+    };
+    wload(wb[0], 0);
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      if (ks + 1 < 4) wload(wb[(ks + 1) & 1], ks + 1);
+      bf16x8 xh[4], xl[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        xh[a] = frag(img_h, kPX, 16 * a, 32 * ks, lane);
+        xl[a] = frag(img_l, kPX, 16 * a, 32 * ks, lane);
+      }
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const bf16x8(&w)[6] = wb[ks & 1][c];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) {
+          qt[c][a] = mfma3(w[0], w[1], xh[a], xl[a], qt[c][a]);
+          kt[c][a] = mfma3(w[2], w[3], xh[a], xl[a], kt[c][a]);
+          vv[a][c] = mfma3(xh[a], xl[a], w[4], w[5], vv[a][c]);
+        }
+      }
+    }
+  } else {
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     bf16x8 xh[4], xl[4];
@@ -173,6 +214,7 @@ __global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P)
         vv[a][c] = mfma3(xh[a], xl[a], vwh, vwl, vv[a][c]);    // m = unit, n = d
       }
     }
+  }
   }
   // QKV → HBM (no bias): Qᵀ / Kᵀ lanes hold 4 consecutive d of one unit (one 16-B store), V one element
   {
@@ -985,7 +1027,9 @@ extern "C" hipError_t dca_attn_block_fwd_f32(const float* e0, const float* bout,
               0.17677669529663687f /* 1/sqrt(32) */, eps};
   for (int i = 0; i < 7; ++i) a.off[i] = off[i];
   if (a.off[6] != kU) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(attn_block_fwd_f32_kernel, dim3(N), dim3(256), 0, stream, a);
+  static const bool one = [] { const char* e = getenv("DCA_ATTN_FWD_1WG"); return e && e[0] == '1'; }();
+  if (one) hipLaunchKernelGGL(attn_block_fwd_f32_kernel<1>, dim3(N), dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL(attn_block_fwd_f32_kernel<2>, dim3(N), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 
