@@ -32,6 +32,8 @@ EVERY rank (one actor runtime per GPU), and reported as node aggregates (sums ov
 * ``league_replay`` — BASELINE config 5 through the same node loop: PFSP self-play league (80 % of games on the
   latest weights), the fp8 actor policy step, and learners sampling every minibatch from an on-HBM replay of
   ``--league-replay-gb`` GB per GPU (``config.replay_capacity`` sequences).
+* ``e2e_5v5`` — BASELINE config 4 end to end: the same node loop on the 5v5 entity-attention model (5v5 self-play
+  actors, 10 players per game; the learner at bf16x3 operands, which the attention kernels need).
 
 Knobs for rehearsing the multi-rank path on one GPU: ``DCA_DIST_BACKEND=gloo`` and ``DCA_SHARED_GPU=1`` (every rank
 on cuda:0).
@@ -111,6 +113,9 @@ def parse():
                          'self-play league on the fp8 actor policy step, learners sampling an on-HBM replay of '
                          '--league-replay-gb GB per GPU')
     ap.add_argument('--league-replay-gb', type=float, default=100.0)
+    ap.add_argument('--e2e-5v5-extra', type=float, default=15.0,
+                    help='seconds of the node loop on the 5v5 entity-attention model (extra field e2e_5v5, BASELINE '
+                         'config 4 end to end: 5v5 self-play actors, 10 players per game; 0 = off)')
     ap.add_argument('--e2e-transport', default='auto', choices=['auto', 'shm', 'tcp'],
                     help='node experience queue: shared-memory ring (auto on one node) or a TCP broker on rank 0')
     from dotaclient_amd.presets import parse_with_preset
@@ -402,6 +407,24 @@ def main():
         if any(errs) and 'error' not in league_replay:
             league_replay = {'error': f'failed on rank(s) {[i for i, x in enumerate(errs) if x]}'}
 
+    e2e_5v5 = None
+    if args.e2e_5v5_extra > 0 and use_cuda and args.e2e_mode == 'process' and args.model != '5v5':
+        # BASELINE config 4 end to end: the same node loop on the 5v5 model (entity attention, bf16x3 learner — it has
+        # no exact-fp32 kernels), 5v5 self-play games on the VecActor (410 games = 4 100 player slots)
+        try:
+            from dotaclient_amd.learner.e2e import measure_e2e_node
+            progress('e2e-5v5 start')
+            e2e_5v5 = measure_e2e_node(
+                model='5v5', device=device, duration=args.e2e_5v5_extra, games=max(1, args.e2e_games // 5),
+                threads=args.e2e_threads, seq_len=args.seq_len, precision=args.precision, pack=bool(args.e2e_pack),
+                transport=args.e2e_transport, progress=progress, idle_probe=0.0)
+        except Exception as e:
+            e2e_5v5 = {'error': repr(e)}
+        progress(f'e2e-5v5 done: {e2e_5v5.get("error", "ok")}')
+        errs = gather('error' in e2e_5v5)
+        if any(errs) and 'error' not in e2e_5v5:
+            e2e_5v5 = {'error': f'failed on rank(s) {[i for i, x in enumerate(errs) if x]}'}
+
     shas = gather(weights_sha)
     hosts = gather(host)
     if rank == 0:
@@ -443,6 +466,7 @@ def main():
             'actor': actor,
             'e2e': e2e,
             'league_replay': league_replay,
+            'e2e_5v5': e2e_5v5,
             'host_placement': hosts,
         }
         print(json.dumps(out), flush=True)

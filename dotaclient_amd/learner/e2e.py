@@ -209,9 +209,11 @@ def _actor_process_main(addr: str, model: str, games: int, threads: int, seq_len
             # weights play the sampled opponent version with probability 1 - latest_weights_prob
             from ..actor.league import League
             lg = League(ws, mode=league)
-        va = VecActor(ws, games, br.publish_experience, device=device, seed=seed, rollout_size=rollout_size,
-                      max_dota_time=max_dota_time, hidden_stride=seq_len, threads=threads, stagger=True,
-                      tag=f'{tag}.vec', league=lg, latest_weights_prob=latest_weights_prob,
+        from ..models.policy import get_config
+        mode = '5v5' if get_config(model).layout.counts[0] > 1 else '1v1'   # (BASELINE config 4: 5v5 self-play)
+        va = VecActor(ws, games, br.publish_experience, device=device, mode=mode, seed=seed,
+                      rollout_size=rollout_size, max_dota_time=max_dota_time, hidden_stride=seq_len, threads=threads,
+                      stagger=True, tag=f'{tag}.vec', league=lg, latest_weights_prob=latest_weights_prob,
                       precision=precision)      # (game ids unique across the node's actor processes)
         for _ in range(3):
             va.step()
