@@ -113,9 +113,10 @@ def parse():
                          'self-play league on the fp8 actor policy step, learners sampling an on-HBM replay of '
                          '--league-replay-gb GB per GPU')
     ap.add_argument('--league-replay-gb', type=float, default=100.0)
-    ap.add_argument('--e2e-5v5-extra', type=float, default=15.0,
+    ap.add_argument('--e2e-5v5-extra', type=float, default=-1.0,
                     help='seconds of the node loop on the 5v5 entity-attention model (extra field e2e_5v5, BASELINE '
-                         'config 4 end to end: 5v5 self-play actors, 10 players per game; 0 = off)')
+                         'config 4 end to end: 5v5 self-play actors, 10 players per game; 0 = off; default: 15 s on '
+                         'a one-GPU run, off on multi-GPU scaling runs)')
     ap.add_argument('--e2e-transport', default='auto', choices=['auto', 'shm', 'tcp'],
                     help='node experience queue: shared-memory ring (auto on one node) or a TCP broker on rank 0')
     from dotaclient_amd.presets import parse_with_preset
@@ -408,6 +409,8 @@ def main():
             league_replay = {'error': f'failed on rank(s) {[i for i, x in enumerate(errs) if x]}'}
 
     e2e_5v5 = None
+    if args.e2e_5v5_extra < 0:
+        args.e2e_5v5_extra = 15.0 if world == 1 else 0.0
     if args.e2e_5v5_extra > 0 and use_cuda and args.e2e_mode == 'process' and args.model != '5v5':
         # BASELINE config 4 end to end: the same node loop on the 5v5 model (entity attention, bf16x3 learner — it has
         # no exact-fp32 kernels), 5v5 self-play games on the VecActor (410 games = 4 100 player slots)
