@@ -224,6 +224,12 @@ _F32_GEMM_FAST = os.environ.get('DCA_F32_GEMM', 'fast') != 'exact'
 # weight-gradient GEMMs of the recurrence and pre-RNN layer on the (then idle) recurrence stream, overlapped with the
 # ∂X chain of the main stream (DCA_WG_OVERLAP=0: everything on the main stream)
 _WG_OVERLAP = os.environ.get('DCA_WG_OVERLAP', '1') != '0'
+# single-graph step: the pre-RNN weight gradient (∂W_pre, ∂b_pre) on the main stream after the encoder backward
+# instead of queued behind ∂W_hh / ∂W_ih on the recurrence stream, whose exact GEMMs made the side stream the tail's
+# critical path. Measured (scripts/gpu_premain.sh, two same-box pairs): exact 5.560 / 5.573 → 5.514 / 5.530 ms;
+# bf16x3 4.896 / 4.892 → 4.921 / 4.911 ms (slower), so the default ('exact') applies it to the exact learner only.
+# DCA_PRE_ON_MAIN = 0 / 1 / exact.
+_PRE_ON_MAIN = os.environ.get('DCA_PRE_ON_MAIN', 'exact')
 # fp32 learner: the ∂X chain ∂pre = (∂G·W_ih)⊙[x>0], ∂x896 = ∂pre·W_pre as ONE hand-written MFMA kernel
 # (ops/csrc/dx_chain.hip) instead of two hipBLASLt GEMMs + a threshold_backward (DCA_DX_FUSED=0: the library path)
 _DX_FUSED = os.environ.get('DCA_DX_FUSED', '1') != '0'
@@ -478,6 +484,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     dgam = dbet = None
     first_attn = True
     side_after: List = []                # side-stream work enqueued after the encoder backward (5v5 fused path)
+    after_enc: List = []                 # main-stream work enqueued after the encoder backward (DCA_PRE_ON_MAIN)
     if attn:
         dWout = torch.empty(128, 128, device=dev)
         dbout = torch.empty(128, device=dev)
@@ -547,7 +554,14 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         else:
             # ∂pre-activation of the pre-RNN layer: one GEMM (bf16 or exact f32), ReLU mask in one threshold_backward
             dpre16 = torch.ops.aten.threshold_backward(torch.mm(dG16, W['wihT16'].t()), x16[r0:r1], 0)
-        if wg_side:
+        pre_main = wg_side and split is None and (_PRE_ON_MAIN == '1' or (_PRE_ON_MAIN == 'exact' and exact))
+        if pre_main:
+            with torch.cuda.stream(sL):       # the side stream ends with ∂W_ih
+                wg_done = torch.cuda.Event()
+                wg_done.record(sL)
+            after_enc.append(lambda d=dpre16, xr=x896[r0:r1]: gemm_tn(d, xr, out=dWpre, accumulate=True,
+                                                                      colsum=dbpre))
+        elif wg_side:
             sL.wait_stream(main)
             with torch.cuda.stream(sL):
                 gemm_tn(dpre16, x896[r0:r1], out=dWpre, accumulate=True, colsum=dbpre)
@@ -650,6 +664,9 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         dwt_c, dw1_c, db1_c = C.encoder_bwd(units_t[r0:r1], w1, b1, wtT16, dtl[r0:r1], z[r0:r1],
                                             dx896, arg[r0:r1], counts, bool(cfg.compat_bugs), demb_in=demb_in,
                                             exact=exact)
+        for fn in after_enc:
+            fn()
+        after_enc.clear()
         if side_after:
             # the side stream already waits on the attention backward (not on the encoder backward just issued)
             with torch.cuda.stream(sL):
