@@ -230,6 +230,9 @@ _WG_OVERLAP = os.environ.get('DCA_WG_OVERLAP', '1') != '0'
 # bf16x3 4.896 / 4.892 → 4.921 / 4.911 ms (slower), so the default ('exact') applies it to the exact learner only.
 # DCA_PRE_ON_MAIN = 0 / 1 / exact.
 _PRE_ON_MAIN = os.environ.get('DCA_PRE_ON_MAIN', 'exact')
+# 5v5 fused path: ∂W_out on the main stream after the encoder backward (A/B knob DCA_WOUT_MAIN=1; measured slower:
+# 8.138 / 8.127 vs 8.098 / 8.102 ms, scripts/gpu_woutmain.sh)
+_WOUT_MAIN = os.environ.get('DCA_WOUT_MAIN', '0') == '1'
 # fp32 learner: the ∂X chain ∂pre = (∂G·W_ih)⊙[x>0], ∂x896 = ∂pre·W_pre as ONE hand-written MFMA kernel
 # (ops/csrc/dx_chain.hip) instead of two hipBLASLt GEMMs + a threshold_backward (DCA_DX_FUSED=0: the library path)
 _DX_FUSED = os.environ.get('DCA_DX_FUSED', '1') != '0'
@@ -601,8 +604,13 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
                 # enqueued AFTER the encoder backward below (side_after): issued here, the graph ran the two GEMMs
                 # (156 + 401 µs) and then the encoder backward strictly one after the other
                 sL.wait_stream(main)
-                side_after.append(lambda: (gemm_tn(dE1, Oat, out=dWout, colsum=dbout),
-                                           gemm_tn(dQKV, Xn, out=dWqkv, colsum=dbqkv)))
+                if _WOUT_MAIN:
+                    # ∂W_out on the main stream after the encoder backward, ∂W_qkv beside it (balances the streams)
+                    side_after.append(lambda: gemm_tn(dQKV, Xn, out=dWqkv, colsum=dbqkv))
+                    after_enc.append(lambda: gemm_tn(dE1, Oat, out=dWout, colsum=dbout))
+                else:
+                    side_after.append(lambda: (gemm_tn(dE1, Oat, out=dWout, colsum=dbout),
+                                               gemm_tn(dQKV, Xn, out=dWqkv, colsum=dbqkv)))
             else:
                 dWout = gemm_tn(dE1, Oat, colsum=dbout)
                 dWqkv = gemm_tn(dQKV, Xn, colsum=dbqkv)
