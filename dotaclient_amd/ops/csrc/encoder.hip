@@ -1684,8 +1684,10 @@ extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const
     F.dwtpart = F.w1part + (size_t)jobs * kW1;
     if (f32 == 2 && demb_in) return hipErrorInvalidValue;      // the exact kernels cover the 1v1 encoder
     if (jobs > 0 && f32 == 2) {
-      // DCA_ENC_BWD_X2=1: the 4-wave two-workgroups-per-CU form (A/B; default the 8-wave form)
-      static const bool x2 = [] { const char* e = getenv("DCA_ENC_BWD_X2"); return e && e[0] == '1'; }();
+      // the 4-wave two-workgroups-per-CU form by default: 369.7 vs 373.6 µs alone, and in the exact learner step
+      // 5.498 / 5.483 vs 5.518 / 5.513 ms (two same-box pairs, scripts/gpu_x2ab.sh) — beside the side stream's
+      // weight-gradient GEMMs two smaller workgroups per CU schedule better. DCA_ENC_BWD_X2=0: the 8-wave form.
+      static const bool x2 = [] { const char* e = getenv("DCA_ENC_BWD_X2"); return !(e && e[0] == '0'); }();
       if (x2) {
         if (compat) encoder_bwd_x2_kernel<true><<<jobs, 256, 0, st>>>(F);
         else encoder_bwd_x2_kernel<false><<<jobs, 256, 0, st>>>(F);
