@@ -91,8 +91,10 @@ def parse():
     ap.add_argument('--e2e', type=float, default=20.0,
                     help='seconds of the end-to-end actors→queue→learners loop on every rank (0 = off)')
     # node-loop actor shape (scripts/e2e_ab.py on one MI355X, 15 s each, after the round-4 host-loop fixes: 2048 games
-    # × 14 threads 1.04 M steps/s (0.89 M valid), × 12 threads 0.91 M, 1024 × 12 0.84 M — same box, same minute)
-    ap.add_argument('--e2e-games', type=int, default=2048)
+    # × 14 threads 1.04 M steps/s (0.89 M valid), × 12 threads 0.91 M, 1024 × 12 0.84 M — same box, same minute; then
+    # 4096 / 3072 / 2048 / 3072 games × 14: 1.11 / 1.08 / 0.94 / 1.00 M, weight age 5.0 / 4.4 / 3.3 / 4.0 versions —
+    # bigger policy steps hold up better beside the learner's recurrence; 3072 trades a version of policy lag for it)
+    ap.add_argument('--e2e-games', type=int, default=3072)
     ap.add_argument('--e2e-threads', type=int, default=0,
                     help='actor host threads of the node loop (0 = from the CPU share, clamped to [2, 14])')
     ap.add_argument('--e2e-actor-precision', default='bf16', choices=['bf16', 'fp8'],
