@@ -137,3 +137,34 @@ def test_shm_broker_roundtrip():
         assert b.latest_model(newer_than=4) is None
     finally:
         b.close(unlink=True)
+
+
+def test_shm_broker_view_decodes_rollout():
+    """``consume_experience_view`` (ShmRing.pop_view, native/featurizer.cpp) hands the learner's decode thread a
+    uint8 array owning the message: same bytes as ``consume_experience``, and the codec decodes it in place."""
+    from dotaclient_amd.transport.codec import Rollout, decode_any, encode
+    from dotaclient_amd.transport.shm import ShmBroker
+    rng = np.random.RandomState(0)
+    T, U = 12, 20
+    r = Rollout(game_id='g', team_id=2, player_id=0, env=rng.randn(T, 3).astype(np.float32),
+                units=rng.randn(T, U, 10).astype(np.float32), actions=(rng.rand(T, 21 + U) > 0.9).astype(np.uint8),
+                masks=(rng.rand(T, 21 + U) > 0.5).astype(np.uint8), rewards=rng.randn(T, 9), weight_version=3,
+                canvas=np.zeros((8, 8, 3), np.uint8), logp=rng.randn(T).astype(np.float32),
+                values=rng.randn(T).astype(np.float32), hiddens=rng.randn(2, 2, 16).astype(np.float32),
+                hidden_stride=16, bootstrap_value=0.25, done=True)
+    body = encode(r)
+    b = ShmBroker(f'dca_v_{uuid.uuid4().hex[:8]}', capacity=1 << 20, create=True)
+    try:
+        assert b.consume_experience_view(0.0) is None
+        b.publish_experience(body)
+        b.publish_experience(body)
+        v = b.consume_experience_view(1.0)
+        assert isinstance(v, np.ndarray) and v.dtype == np.uint8 and v.tobytes() == body
+        assert b.consume_experience(1.0) == body
+        d = decode_any(v)
+        del v                                          # the decoded arrays must not depend on the view staying alive
+        for k in ['env', 'units', 'actions', 'masks', 'rewards', 'logp', 'values', 'hiddens']:
+            np.testing.assert_array_equal(getattr(d, k), getattr(r, k))
+        assert (d.weight_version, d.bootstrap_value, d.done) == (3, 0.25, True)
+    finally:
+        b.close(unlink=True)
