@@ -78,6 +78,23 @@ void multi_axpy(std::vector<torch::Tensor> dst, std::vector<torch::Tensor> src, 
 }
 
 // ------------------------------------------------------------------------------------------------------------
+// Optional in-kernel timestamp buffers: checked contiguous int64 GPU tensors of at least `need` values (the kernels
+// write without bounds checks). Plain LSTM: its workgroups (chains × H/8, lstm.hip plan_chains) × 8 waves × 64 steps
+// × 8 events; team LSTM: 32 members × 4 waves × 64 steps × 8 events.
+inline int64_t lstm_trace_elems(int B, int H) {
+  const int nwg = H / 8, max_ch = 256 / nwg;
+  const int nch = std::min((B + 31) / 32, max_ch);
+  return (int64_t)nch * nwg * 8 * 64 * 8;
+}
+constexpr int64_t kTeamTraceElems = 32LL * 4 * 64 * 8;
+inline unsigned long long* trace_ptr(const c10::optional<torch::Tensor>& t, int64_t need, const char* name) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  CHECK_DEV(*t); CHECK_CONTIG(*t);
+  TORCH_CHECK(t->scalar_type() == at::kLong && t->numel() >= need, name,
+              ": trace must be a contiguous int64 GPU tensor with >= ", need, " elements");
+  return ptr<unsigned long long>(*t);
+}
+
 // Persistent LSTM recurrence. xp (B,S,4H) f32, whh (4H,H) bf16, h0/c0 (B,H) f32, err (1) int32 device flag.
 std::vector<torch::Tensor> lstm_fwd(torch::Tensor xp, torch::Tensor whh, torch::Tensor h0, torch::Tensor c0,
                                     torch::Tensor err, bool want_f32_h, c10::optional<torch::Tensor> trace) {
@@ -99,7 +116,7 @@ std::vector<torch::Tensor> lstm_fwd(torch::Tensor xp, torch::Tensor whh, torch::
   hip_check(dca_lstm_fwd(ptr<float>(xp), ptr<short>(whh), ptr<float>(h0), ptr<float>(c0), ptr<short>(hs),
                          want_f32_h ? ptr<float>(hsf) : nullptr, ptr<float>(cs), ptr<float>(gates), ptr<float>(hn),
                          ptr<float>(cn), ptr<unsigned long long>(ring), ptr<unsigned>(err), B, S, H, cur_stream(),
-                         (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr),
+                         trace_ptr(trace, lstm_trace_elems(B, H), "lstm_fwd")),
             "dca_lstm_fwd");
   return {hs, want_f32_h ? hsf : hs, cs, gates, hn, cn};
 }
@@ -126,7 +143,7 @@ std::vector<torch::Tensor> lstm_bwd(torch::Tensor dhs, torch::Tensor gates, torc
   hip_check(dca_lstm_bwd(ptr<float>(dhs), ptr<float>(gates), ptr<float>(cs), ptr<float>(c0), dhn_p, dcn_p,
                          ptr<short>(whh), ptr<float>(dgates), ptr<float>(dh0), ptr<float>(dc0),
                          ptr<unsigned long long>(ring), ptr<unsigned>(err), B, S, H, cur_stream(),
-                         (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr),
+                         trace_ptr(trace, lstm_trace_elems(B, H), "lstm_bwd")),
             "dca_lstm_bwd");
   return {dgates, dh0, dc0};
 }
@@ -201,7 +218,7 @@ std::vector<torch::Tensor> lstm_team_fwd(torch::Tensor xp4, torch::Tensor whh, t
                               f32w ? ptr<float>(hs) : (want_f32_h ? ptr<float>(hsf) : nullptr), ptr<float>(cs),
                               ptr<float>(gates4), ptr<float>(hn), ptr<float>(cn), ctl.data_ptr(), ws.data_ptr(), wsb,
                               ptr<unsigned>(err), B, S, H, time_major ? 1 : 0, cur_stream(),
-                              (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr,
+                              trace_ptr(trace, kTeamTraceElems, "lstm_team_fwd"),
                               bias_p, f32w ? 1 : 0, precise ? 1 : 0, reset_ptr(reset, B, S)),
             "dca_lstm_team_fwd");
   if (f32w) return {hs, hs, cs, gates4, hn, cn};
@@ -265,7 +282,7 @@ std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4
                               whh.data_ptr(), dg_bf16 ? nullptr : ptr<float>(dgates4), ptr<float>(dh0),
                               ptr<float>(dc0), ctl.data_ptr(), ws.data_ptr(), wsb, ptr<unsigned>(err), B, S, H,
                               time_major ? 1 : 0, cur_stream(),
-                              (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr,
+                              trace_ptr(trace, kTeamTraceElems, "lstm_team_bwd"),
                               dg_bf16 ? ptr<short>(dgates4) : nullptr, want_dbias ? ptr<float>(dbp) : nullptr,
                               f32w ? 1 : 0, precise ? 1 : 0, reset_ptr(reset, B, S), hsf_p, h0_p, dw_p),
             "dca_lstm_team_bwd");

@@ -109,3 +109,27 @@ def test_team_folded_bias_bf16_dgates_and_bias_grad(gpu_ops, B, S, H, tm):
     torch.testing.assert_close(g16[1], g32[1], atol=1e-6, rtol=1e-6)
     # the bias gradient comes in PyTorch's gate-major order (unit-major ∂gates summed, then (H, 4) → (4, H))
     torch.testing.assert_close(g16[3], g32[0].sum((0, 1)).t().reshape(-1), atol=1e-3, rtol=1e-4)
+
+
+def test_trace_buffers_are_checked_before_launch(gpu_ops):
+    """The recurrence kernels stamp timestamps into the optional trace buffer without bounds checks, so the
+    bindings reject an undersized or wrong-dtype buffer before launching (bindings.cpp trace_ptr)."""
+    from dotaclient_amd import ops
+    from dotaclient_amd.ops.lstm import team_ctl
+    C = ops.require()
+    B, S, H = 8, 4, 128
+    err = torch.zeros(1, dtype=torch.int32, device='cuda')
+    h0 = torch.zeros(B, H, device='cuda')
+    xp4 = torch.randn(B, S, H, 4, device='cuda')
+    whh = (torch.randn(4 * H, H, device='cuda') * 0.05).to(torch.bfloat16)
+    for bad in [torch.zeros(32 * 4 * 64 * 8 - 1, dtype=torch.int64, device='cuda'),
+                torch.zeros(32 * 4 * 64 * 8, dtype=torch.int32, device='cuda')]:
+        with pytest.raises(RuntimeError, match='trace'):
+            C.lstm_team_fwd(xp4, whh, h0, h0, err, team_ctl(), False, bad)
+    xp = torch.randn(B, S, 4 * H, device='cuda')
+    with pytest.raises(RuntimeError, match='trace'):
+        C.lstm_fwd(xp, whh, h0, h0, err, False, torch.zeros(16, dtype=torch.int64, device='cuda'))
+    tr = torch.zeros(32 * 4 * 64 * 8, dtype=torch.int64, device='cuda')
+    C.lstm_team_fwd(xp4, whh, h0, h0, err, team_ctl(), False, tr)
+    torch.cuda.synchronize()
+    assert int(err.item()) == 0 and int((tr != 0).sum().item()) > 0
