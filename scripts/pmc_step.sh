@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc_step
 mkdir -p $OUT
-CMD="python3 bench.py --steps 2 --warmup 2 --actor 0 --e2e 0 --bf16x3-extra 0 --graph 0"
+CMD="python3 bench.py --steps 2 --warmup 2 --actor 0 --e2e 0 --e2e-5v5-extra 0 --bf16x3-extra 0 --graph 0"
 timeout -s KILL 60 rocprofv3 -L > $OUT/counters.txt 2>&1 || true
 timeout -s KILL 150 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU_MFMA_MOPS_BF16 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE -d $OUT/sq -o run -- $CMD > $OUT/sq.log 2>&1
 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run -- $CMD > $OUT/fetch.log 2>&1
