@@ -23,6 +23,7 @@ from __future__ import annotations
 
 import contextlib
 import itertools
+import os
 import threading
 from dataclasses import dataclass
 from typing import Dict, Optional
@@ -44,7 +45,14 @@ CAPTURE_LOCK = threading.RLock()
 _GRAPH_TOKENS = itertools.count(1)   # replay-graph cache tokens (Learner._replay_key)
 
 
+def _capture_stream(device):
+    """The graph-capture stream (DCA_MAIN_PRIORITY=1: high priority, an A/B knob for the step's critical path)."""
+    pr = -1 if os.environ.get('DCA_MAIN_PRIORITY', '0') == '1' else 0
+    return torch.cuda.Stream(device=device, priority=pr)
+
+
 @dataclass
+
 class LossConfig:
     algo: str = 'ppo'                 # 'ppo' (north star) | 'vpg' (reference objective)
     learning_rate: float = 1e-4       # optimizer.py:778
@@ -240,7 +248,7 @@ class Learner:
         graphs = self.__dict__.setdefault('_graphs', {})
         if key not in graphs:
             if getattr(self, '_graph_stream', None) is None:
-                self._graph_stream = torch.cuda.Stream(device=self.device)
+                self._graph_stream = _capture_stream(self.device)
             s = self._graph_stream
             cur = torch.cuda.current_stream(self.device)
             s.wait_stream(cur)
@@ -279,7 +287,7 @@ class Learner:
             # the capture stream must outlive the graph: hipBLASLt's per-stream workspace that the captured GEMM
             # nodes point at belongs to it
             if getattr(self, '_graph_stream', None) is None:
-                self._graph_stream = torch.cuda.Stream(device=self.device)
+                self._graph_stream = _capture_stream(self.device)
             s = self._graph_stream
             cur = torch.cuda.current_stream(self.device)
             s.wait_stream(cur)

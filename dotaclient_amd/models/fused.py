@@ -332,7 +332,10 @@ class FusedPolicy:
 
     def side_stream(self):
         if getattr(self, '_side', None) is None:
-            self._side = torch.cuda.Stream(device=self.err.device)
+            import os
+            # DCA_SIDE_PRIORITY=1: the recurrence / weight-gradient side stream at high priority (A/B knob)
+            pr = -1 if os.environ.get('DCA_SIDE_PRIORITY', '0') == '1' else 0
+            self._side = torch.cuda.Stream(device=self.err.device, priority=pr)
         return self._side
 
     def use_pipeline(self) -> bool:
