@@ -12,6 +12,7 @@ loss → backward → RCCL all-reduce of the flat gradient → fused clip + Adam
 each rank trains on ``--batch-size`` sequences of ``--seq-len`` steps.
 
     python bench.py                                   # 1 GPU
+    python bench.py --gpus 8                          # 8 rank processes started by bench.py itself
     python -m torch.distributed.run --nproc-per-node 8 ... bench.py --gpus 8
 
 Rank 0 prints ONE JSON line. The actor and end-to-end numbers are measured *outside* the timed learner region, on
@@ -85,7 +86,7 @@ def parse():
     ap.add_argument('--actor-games', type=int, default=2048, help='concurrent 1v1 games of the actor runtime')
     ap.add_argument('--actor-threads', type=int, default=0,
                     help='host threads of the native actor runtime per GPU (0 = from this rank\'s CPU share: '
-                         'parallel/placement.py, clamped to [2, 14])')
+                         'parallel/placement.py Placement.actor_threads, in [1, 14])')
     ap.add_argument('--pin', type=int, default=1,
                     help='pin this rank (learner threads + its actor process) to its GPU-local CPU share')
     ap.add_argument('--e2e', type=float, default=20.0,
@@ -96,7 +97,7 @@ def parse():
     # bigger policy steps hold up better beside the learner's recurrence; 3072 trades a version of policy lag for it)
     ap.add_argument('--e2e-games', type=int, default=3072)
     ap.add_argument('--e2e-threads', type=int, default=0,
-                    help='actor host threads of the node loop (0 = from the CPU share, clamped to [2, 14])')
+                    help='actor host threads of the node loop (0 = from the CPU share, in [1, 14])')
     ap.add_argument('--e2e-actor-precision', default='bf16', choices=['bf16', 'fp8'],
                     help='policy step of the node loop\'s actors (fp8: the BASELINE config-5 step; the loop measured '
                          '1.15-1.20 vs ≈1.0 M steps/s, its kernels co-run better beside the learner\'s recurrence)')
@@ -130,8 +131,63 @@ def progress(msg: str):
     print(f'[bench r{os.environ.get("RANK", "0")} {time.strftime("%H:%M:%S")}] {msg}', file=sys.stderr, flush=True)
 
 
+def _free_port() -> int:
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n: int) -> int:
+    """``python bench.py --gpus N`` without a launcher: start N fresh rank processes of this script (one per GPU,
+    env:// rendezvous on 127.0.0.1), forward rank 0's stdout (the JSON line) and every rank's stderr, and return the
+    first non-zero exit status (the other ranks are then stopped by PID). The caller has touched no GPU: the parent
+    only parses arguments, and a HIP-initialised parent must never exec or fork a GPU program."""
+    import signal
+    import subprocess
+    port = os.environ.get('MASTER_PORT') or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK='0', NODE_RANK='0', MASTER_ADDR=os.environ.get('MASTER_ADDR', '127.0.0.1'),
+                   MASTER_PORT=port, DCA_BENCH_LAUNCHED='1')
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else sys.stderr.fileno()))
+    progress(f'launched {n} ranks: pids {[p.pid for p in procs]} (master 127.0.0.1:{port})')
+    status = 0
+    live = list(procs)
+    kill_at = None
+    while live:
+        if kill_at is not None and time.time() > kill_at:
+            for q in live:
+                q.kill()
+            kill_at = float('inf')
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                progress(f'rank pid {p.pid} exited with {rc}: stopping the other ranks')
+                for q in live:
+                    q.send_signal(signal.SIGTERM)
+                kill_at = time.time() + 30.0
+        time.sleep(0.2)
+    return status
+
+
 def main():
     args = parse()
+    env_world = os.environ.get('WORLD_SIZE')
+    if env_world is None and args.gpus > 1:
+        # self-launch BEFORE anything touches the GPU (no torch.cuda call has been made in this process)
+        sys.exit(launch_ranks(args.gpus))
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f'bench.py: --gpus {args.gpus} but WORLD_SIZE={env_world} (launcher and flag disagree)', file=sys.stderr)
+        sys.exit(2)
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
@@ -146,9 +202,9 @@ def main():
     from dotaclient_amd.parallel.placement import for_this_rank
     place = for_this_rank(pin=bool(args.pin))
     if not args.actor_threads:
-        args.actor_threads = min(14, place.threads(reserve=2, minimum=2))
+        args.actor_threads = place.actor_threads()
     if not args.e2e_threads:
-        args.e2e_threads = min(14, place.threads(reserve=2, minimum=2))
+        args.e2e_threads = place.actor_threads()
     host = dict(place.describe(), actor_threads=args.actor_threads, e2e_threads=args.e2e_threads)
     if world > 1:
         from dotaclient_amd.parallel.dist import init_distribution

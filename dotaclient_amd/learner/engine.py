@@ -410,6 +410,7 @@ class Learner:
     def check_error(self):
         """Raise (on every DP rank alike) if a persistent kernel failed on any rank since the last call; host sync,
         call at iteration boundaries."""
+        self.opt.check_nonfinite()
         if self.backend != 'fused':
             return
         sticky = getattr(self, '_err_any', None)
@@ -422,7 +423,9 @@ class Learner:
 
     def _finish(self, vec):
         metrics = self._metrics_from_vec(vec.clone())
-        metrics['grad_norm'] = self._sync_and_step()
+        # a copy: the optimizer's norm is ONE persistent tensor rewritten by every step, and with deferred metrics the
+        # iteration's list is read only after the next iteration's steps were queued
+        metrics['grad_norm'] = self._sync_and_step().clone()
         self.n_steps += 1
         return metrics
 
@@ -431,7 +434,7 @@ class Learner:
         if self.direct():
             return self._finish(self._step_direct_batch(batch))
         metrics = self._fwd_bwd(batch)
-        metrics['grad_norm'] = self._sync_and_step()
+        metrics['grad_norm'] = self._sync_and_step().clone()
         self.n_steps += 1
         return metrics
 

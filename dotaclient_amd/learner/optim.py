@@ -32,6 +32,8 @@ class FlatAdam:
         self.exp_avg_sq = torch.zeros_like(flat.flat)
         self.steps = torch.zeros(len(flat.params), device=dev, dtype=torch.float32)
         self.last_grad_norm = torch.zeros((), device=dev, dtype=torch.float32)
+        # sticky device flag: a step was dropped because its gradient norm was not finite (check_nonfinite raises)
+        self.nonfinite = torch.zeros(1, device=dev, dtype=torch.float32)
         if use_kernels is None:
             use_kernels = dev.type == 'cuda'
         self.use_kernels = use_kernels
@@ -57,8 +59,16 @@ class FlatAdam:
         self._ops.adam_step(self.flat.flat, self.flat.grad, self.exp_avg, self.exp_avg_sq, self.flat.segment_ids,
                             counts, self.steps, self.last_grad_norm, float(self.lr), float(b1), float(b2),
                             float(self.eps), float(max_norm), divide=bool(divide), header=int(self.flat.header),
-                            skip=skip)
+                            skip=skip, nonfinite=self.nonfinite)
         return self.last_grad_norm
+
+    def check_nonfinite(self):
+        """Raise if a step since the last call was dropped for a non-finite gradient (host sync: call at iteration
+        boundaries). The reference raises on a NaN loss before optimizer.step() (optimizer.py:674-676); a finite loss
+        with Inf / NaN gradients is caught here instead of training on with silently skipped steps."""
+        if float(self.nonfinite.item()) != 0.0:
+            self.nonfinite.zero_()
+            raise FloatingPointError('non-finite gradient norm: the optimizer step was skipped')
 
     @torch.no_grad()
     def step_reference(self, counts, divide=False, skip=None):
@@ -71,6 +81,9 @@ class FlatAdam:
         norm = torch.linalg.vector_norm(g)
         self.last_grad_norm.copy_(norm)
         if skip is not None and float(skip.reshape(-1)[0]) != 0.0:
+            return norm
+        if not bool(torch.isfinite(norm)):
+            self.nonfinite.fill_(1.0)       # same as the kernels: nothing applied, step counters unchanged
             return norm
         if self.max_grad_norm is not None:
             coef = (self.max_grad_norm / (norm + 1e-6)).clamp(max=1.0)

@@ -461,6 +461,14 @@ class DotaOptimizer:
                 # geometric growth (a slowly rising n reallocates O(log n) times, not once per new maximum), and
                 # the captured steps bound to the old storage are released before it is freed
                 cap = max(cap, 2 * pool.capacity)
+                # with deferred metrics the previous iteration's replays (reading the old pool, running in the
+                # graphs' private memory pools) may still be in flight: wait for them before the graphs and the
+                # storage go
+                prev = getattr(self, '_pending_metrics', None)
+                if prev is not None and prev.get('done') is not None:
+                    prev['done'].synchronize()
+                if self.device.type == 'cuda':
+                    torch.cuda.current_stream(self.device).synchronize()
                 self.learner.release_graphs(pool)
             pool = self._pool = _IterationPool({k: data[k] for k in fields}, cap, self.cfg.seq_len)
         for k in fields:

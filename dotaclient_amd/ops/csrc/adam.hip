@@ -3,15 +3,20 @@
 // Replaces clip_grad_norm_(0.5) + torch.optim.Adam (reference optimizer.py:281, 680-681) with two launches over the
 // flat buffers of dotaclient_amd.parallel.dp.FlatParams:
 //   1. adam_norm_kernel   : per-block partial sums of g^2 (float4 loads, grid-stride), written to partials[blk];
-//                           block 0 also advances the per-parameter step counters for parameters with count > 0.
+//                           block 0 also snapshots the per-parameter step counters into partials[kMaxBlocks + p].
 //   2. adam_update_kernel : every block re-reduces the (<=1024) partials itself — no third launch, no cross-block
-//                           hand-off — then applies clip + Adam to its float4 groups. Parameters with DP has-grad
-//                           count 0 are skipped (sparse-param semantics, reference distributed.py:40-42).
+//                           hand-off — then applies clip + Adam to its float4 groups with t = snapshot + 1. Parameters
+//                           with DP has-grad count 0 are skipped (sparse-param semantics, reference
+//                           distributed.py:40-42). Block 0 advances the step counters (from the snapshot, so no block
+//                           reads a counter another block is writing) only when the step is APPLIED: a skipped or
+//                           non-finite step leaves Adam's bias correction where it was.
 // Memory-bound: ~28 B/element moved. Offsets are 64-element aligned so a float4 group never straddles parameters.
 // The first h4 float4 groups are the flat buffer's header (has-grad counts + the kernel-error flag, see
 // parallel/dp.py), never part of the gradient norm. `skip` (optional, device): when *skip != 0 — a persistent
 // recurrence kernel failed on some rank this step — neither the step counters nor any parameter / moment changes
 // (the reference raises before optimizer.step(), optimizer.py:674-676; here the decision stays on the device).
+// `nonfinite` (optional, device, sticky): set to 1 when a step is dropped because its gradient norm is not finite, so
+// the learner raises at the iteration boundary like the reference's NaN check instead of training on silently.
 #include "common.h"
 
 namespace {
@@ -31,8 +36,7 @@ __global__ __launch_bounds__(kThreads) void adam_norm_kernel(const float4* __res
                                                              float* __restrict__ partials,
                                                              const float* __restrict__ counts,
                                                              float* __restrict__ steps, int n_params,
-                                                             const int* __restrict__ seg, int divide, int h4,
-                                                             const float* __restrict__ skip) {
+                                                             const int* __restrict__ seg, int divide, int h4) {
   float acc = 0.f;
   for (int i = h4 + blockIdx.x * kThreads + threadIdx.x; i < n4; i += gridDim.x * kThreads) {
     float4 v = g[i];
@@ -49,17 +53,16 @@ __global__ __launch_bounds__(kThreads) void adam_norm_kernel(const float4* __res
     for (int w = 0; w < kThreads / dca::kWave; ++w) s += red[w];
     partials[blockIdx.x] = s;
   }
-  if (blockIdx.x == 0 && !(skip && *skip != 0.f)) {
-    for (int p = threadIdx.x; p < n_params; p += kThreads)
-      if (counts[p] > 0.f) steps[p] += 1.f;
-  }
+  if (blockIdx.x == 0)
+    for (int p = threadIdx.x; p < n_params; p += kThreads) partials[kMaxBlocks + p] = steps[p];
 }
 
 __global__ __launch_bounds__(kThreads) void adam_update_kernel(
     float4* __restrict__ param, const float4* __restrict__ grad, float4* __restrict__ m, float4* __restrict__ v,
     const int* __restrict__ seg, int n4, const float* __restrict__ partials, int nparts,
-    const float* __restrict__ counts, const float* __restrict__ steps, float* __restrict__ norm_out, float lr,
-    float b1, float b2, float eps, float max_norm, int divide, const float* __restrict__ skip) {
+    const float* __restrict__ counts, float* __restrict__ steps, int n_params, float* __restrict__ norm_out,
+    float lr, float b1, float b2, float eps, float max_norm, int divide, const float* __restrict__ skip,
+    float* __restrict__ nonfinite) {
   __shared__ float red[kThreads / dca::kWave];
   __shared__ float s_coef;
   __shared__ bool s_bad;
@@ -84,13 +87,20 @@ __global__ __launch_bounds__(kThreads) void adam_update_kernel(
   }
   __syncthreads();
   if (skip && *skip != 0.f) return;          // failed step: the norm is reported, nothing is applied
-  if (s_bad) return;
+  if (s_bad) {
+    if (blockIdx.x == 0 && threadIdx.x == 0 && nonfinite) *nonfinite = 1.f;
+    return;
+  }
+  const float* snap = partials + kMaxBlocks;
+  if (blockIdx.x == 0)
+    for (int p = threadIdx.x; p < n_params; p += kThreads)
+      if (counts[p] > 0.f) steps[p] = snap[p] + 1.f;
   const float coef = s_coef;
   for (int i = blockIdx.x * kThreads + threadIdx.x; i < n4; i += gridDim.x * kThreads) {
     const int s = seg[i * 4];
     if (s < 0) continue;
     if (!(counts[s] > 0.f)) continue;
-    const float t = steps[s];
+    const float t = snap[s] + 1.f;
     const float gcoef = divide ? coef / counts[s] : coef;
     const float bc1 = 1.f - powf(b1, t);
     const float bc2s = sqrtf(1.f - powf(b2, t));
@@ -113,22 +123,26 @@ __global__ __launch_bounds__(kThreads) void adam_update_kernel(
 
 }  // namespace
 
-// n must be a multiple of 4 (FlatParams pads every parameter to 64 elements). `partials` holds >= kMaxBlocks floats.
+// n must be a multiple of 4 (FlatParams pads every parameter to 64 elements). `partials` holds
+// >= kMaxBlocks + n_params floats (dca_adam_partials_len).
+extern "C" int dca_adam_partials_len(int n_params) { return kMaxBlocks + n_params; }
+
 extern "C" hipError_t dca_adam_step(float* param, const float* grad, float* m, float* v, const int* seg, int64_t n,
                                     const float* counts, float* steps, int n_params, float* partials,
                                     float* norm_out, float lr, float b1, float b2, float eps, float max_norm,
-                                    hipStream_t stream, int divide, int64_t header, const float* skip) {
+                                    hipStream_t stream, int divide, int64_t header, const float* skip,
+                                    float* nonfinite) {
   if (header < 0 || header % 4 != 0 || header > n) return hipErrorInvalidValue;
   const int n4 = (int)(n / 4);
   int blocks = (n4 + kThreads - 1) / kThreads;
   blocks = blocks < 1 ? 1 : (blocks > kMaxBlocks ? kMaxBlocks : blocks);
   adam_norm_kernel<<<blocks, kThreads, 0, stream>>>(reinterpret_cast<const float4*>(grad), n4, partials, counts,
-                                                    steps, n_params, seg, divide, (int)(header / 4), skip);
+                                                    steps, n_params, seg, divide, (int)(header / 4));
   DCA_CHECK_LAUNCH();
   adam_update_kernel<<<blocks, kThreads, 0, stream>>>(
       reinterpret_cast<float4*>(param), reinterpret_cast<const float4*>(grad), reinterpret_cast<float4*>(m),
-      reinterpret_cast<float4*>(v), seg, n4, partials, blocks, counts, steps, norm_out, lr, b1, b2, eps, max_norm,
-      divide, skip);
+      reinterpret_cast<float4*>(v), seg, n4, partials, blocks, counts, steps, n_params, norm_out, lr, b1, b2, eps,
+      max_norm, divide, skip, nonfinite);
   DCA_CHECK_LAUNCH();
   return hipSuccess;
 }

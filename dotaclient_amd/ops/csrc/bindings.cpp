@@ -36,7 +36,8 @@ inline T* ptr(const torch::Tensor& t) { return reinterpret_cast<T*>(t.data_ptr()
 // 1-element f32 device flag — nonzero → the step changes nothing (failed recurrence on some DP rank).
 void adam_step(torch::Tensor param, torch::Tensor grad, torch::Tensor m, torch::Tensor v, torch::Tensor seg,
                torch::Tensor counts, torch::Tensor steps, torch::Tensor norm_out, double lr, double b1, double b2,
-               double eps, double max_norm, bool divide, int64_t header, c10::optional<torch::Tensor> skip) {
+               double eps, double max_norm, bool divide, int64_t header, c10::optional<torch::Tensor> skip,
+               c10::optional<torch::Tensor> nonfinite) {
   CHECK_F32(param); CHECK_F32(grad); CHECK_F32(m); CHECK_F32(v); CHECK_I32(seg); CHECK_F32(counts);
   CHECK_F32(steps); CHECK_F32(norm_out);
   const int64_t n = param.numel();
@@ -49,11 +50,17 @@ void adam_step(torch::Tensor param, torch::Tensor grad, torch::Tensor m, torch::
     TORCH_CHECK(skip->numel() >= 1, "adam_step: skip must hold one float");
     sk = ptr<float>(*skip);
   }
-  auto partials = torch::empty({1024}, param.options());
+  float* nf = nullptr;
+  if (nonfinite.has_value() && nonfinite->defined()) {
+    CHECK_F32((*nonfinite));
+    TORCH_CHECK(nonfinite->numel() >= 1, "adam_step: nonfinite must hold one float");
+    nf = ptr<float>(*nonfinite);
+  }
+  auto partials = torch::empty({dca_adam_partials_len((int)counts.numel())}, param.options());
   hip_check(dca_adam_step(ptr<float>(param), ptr<float>(grad), ptr<float>(m), ptr<float>(v), ptr<int>(seg), n,
                           ptr<float>(counts), ptr<float>(steps), (int)counts.numel(), ptr<float>(partials),
                           ptr<float>(norm_out), (float)lr, (float)b1, (float)b2, (float)eps, (float)max_norm,
-                          cur_stream(), divide ? 1 : 0, header, sk),
+                          cur_stream(), divide ? 1 : 0, header, sk, nf),
             "dca_adam_step");
 }
 
@@ -1168,7 +1175,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "averaged by the has-grad counts in-kernel)", py::arg("param"), py::arg("grad"), py::arg("m"), py::arg("v"),
         py::arg("seg"), py::arg("counts"), py::arg("steps"), py::arg("norm_out"), py::arg("lr"), py::arg("b1"),
         py::arg("b2"), py::arg("eps"), py::arg("max_norm"), py::arg("divide") = false, py::arg("header") = 0,
-        py::arg("skip") = py::none());
+        py::arg("skip") = py::none(), py::arg("nonfinite") = py::none());
   m.def("multi_axpy", &multi_axpy, "dst_i += scale * src_i for a list of fp32 tensors (one graph-safe launch)",
         py::arg("dst"), py::arg("src"), py::arg("scale") = py::none());
   m.def("lstm_team_ctl_bytes", &dca_lstm_team_ctl_bytes, "bytes of a persistent team-LSTM control block");

@@ -41,7 +41,8 @@ hipError_t dca_dpre_dx(const float* dG, const void* w1h, const void* w1l, const 
 hipError_t dca_adam_step(float* param, const float* grad, float* m, float* v, const int* seg, int64_t n,
                          const float* counts, float* steps, int n_params, float* partials, float* norm_out, float lr,
                          float b1, float b2, float eps, float max_norm, hipStream_t st, int divide, int64_t header,
-                         const float* skip);
+                         const float* skip, float* nonfinite);
+int dca_adam_partials_len(int n_params);
 
 hipError_t dca_multi_axpy(float* const* dst, const float* const* src, const long long* numel, int n,
                           const float* scale, hipStream_t st);

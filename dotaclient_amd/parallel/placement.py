@@ -39,6 +39,15 @@ class Placement:
         """Worker threads that fit the share after ``reserve`` CPUs for the learner's main / stager / decode threads."""
         return max(minimum, min(len(self.cpus), self.share or len(self.cpus)) - reserve)
 
+    def actor_threads(self, cap: int = 14, floor: int = 1) -> int:
+        """Host threads of the rank's actor runtime: the share minus the learner's main / stager / decode threads
+        (2 CPUs kept from a share of ≥ 6, 1 from a share of 2-5), at least ``floor``, at most ``cap`` (beyond 14 the
+        one-GPU node loop stopped gaining, profiles/r4_e2e_threads_ab.jsonl). 8 ranks on a 16-CPU quota get 1 thread
+        each, not the 2 that the old fixed floor gave (which oversubscribed the quota 1.5×)."""
+        share = min(len(self.cpus), self.share or len(self.cpus))
+        reserve = 2 if share >= 6 else 1 if share >= 2 else 0
+        return max(floor, min(cap, share - reserve))
+
     def describe(self) -> Dict[str, object]:
         d = asdict(self)
         d['cpus'] = cpulist_str(self.cpus)

@@ -89,3 +89,38 @@ def test_pipelined_ingest_matches_inline_on_gpu(tmp_path):
         outs.append((opt.learner.flat.flat.detach().cpu().clone(), opt.ema.detach().cpu().clone()))
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1], outs[1][1])
+
+
+def test_deferred_metrics_pool_growth_and_grad_norm(tmp_path):
+    """with deferred metrics (the previous iteration's replays may still run when the next iteration
+    starts) the per-iteration pool grows (a 10-sequence rollout after 4-sequence iterations): the growth waits for the
+    pending replays before it frees their graphs and storage, and the run trains exactly like the non-deferred one.
+    Every step's grad_norm is its own tensor (not the optimizer's one persistent norm), so the iteration mean is the
+    mean over that iteration's steps."""
+    from dotaclient_amd.learner.optimizer import DotaOptimizer, OptimizerConfig
+    outs, norms = [], []
+    for defer in (False, True):
+        br = InProcBroker()
+        lens = [48] * 8 + [480] + [48] * 16
+        for i, T in enumerate(lens):
+            br.publish_experience(encode(_rollout(i, T=T)))
+        cfg = OptimizerConfig(log_dir=str(tmp_path / f'd{int(defer)}'), model='lstm128', epochs=1, seq_per_epoch=4,
+                              batch_size=2, seq_len=48, device='cuda', xp_timeout=30, prefetch_rollouts=4,
+                              async_checkpoint=True, defer_metrics=defer, graph=True)
+        opt = DotaOptimizer(cfg, br)
+        assert opt._defer_metrics() == defer
+        seen = []
+        fin = opt._finalize_iteration
+
+        def spy(p, fin=fin, seen=seen):
+            g = p['metrics_acc']['grad_norm']
+            seen.append(([t.data_ptr() for t in g], [float(t) for t in g]))
+            return fin(p)
+        opt._finalize_iteration = spy
+        opt.run(iterations=4)
+        outs.append(opt.learner.flat.flat.detach().cpu().clone())
+        norms.append([v for _, v in seen])
+        for ptrs, _ in seen:
+            assert len(set(ptrs)) == len(ptrs)
+    assert torch.equal(outs[0], outs[1])
+    assert norms[0] == norms[1]

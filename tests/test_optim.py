@@ -122,3 +122,52 @@ def test_adam_state_remaps_across_flat_layouts():
     unversioned = {k: v for k, v in legacy.items() if k != 'layout'}
     with pytest.raises(ValueError, match='older layout'):
         opt2.load_state_dict(unversioned)
+
+
+def _nonfinite_case(device, kernels):
+    torch.manual_seed(0)
+    model = Policy('compat').to(device)
+    flat = FlatParams(model, device=device)
+    opt = FlatAdam(flat, lr=1e-3, max_grad_norm=0.5, use_kernels=kernels)
+    counts = torch.ones(len(flat.params), device=device)
+    for p in flat.params:
+        p.grad.normal_()
+    opt.step(counts)
+    opt.check_nonfinite()
+    before = (flat.flat.clone(), opt.exp_avg.clone(), opt.steps.clone())
+    flat.params[3].grad[0] = float('inf')
+    opt.step(counts)
+    assert not bool(torch.isfinite(opt.last_grad_norm))
+    # nothing applied and Adam's bias-correction clock did not move
+    assert torch.equal(flat.flat, before[0]) and torch.equal(opt.exp_avg, before[1])
+    assert torch.equal(opt.steps, before[2])
+    with pytest.raises(FloatingPointError):
+        opt.check_nonfinite()
+    opt.check_nonfinite()                      # the flag was cleared by the raise
+    flat.params[3].grad[0] = 0.0
+    opt.step(counts)
+    assert torch.equal(opt.steps, before[2] + 1)
+
+
+def test_nonfinite_step_is_skipped_and_raises_cpu():
+    _nonfinite_case('cpu', False)
+
+
+@pytest.mark.gpu
+def test_nonfinite_step_is_skipped_and_raises_gpu(gpu_ops):
+    _nonfinite_case('cuda', True)
+
+
+def test_learner_grad_norm_is_per_step():
+    """Every step's returned grad_norm is its own tensor (the optimizer's norm buffer is rewritten by the
+    next step, so a list of references would hold only the last value)."""
+    from dotaclient_amd.learner.engine import Learner, LossConfig
+    from dotaclient_amd.learner.synthetic import make_batch
+    from dotaclient_amd.models.policy import get_config
+    cfg = get_config('lstm128')
+    torch.manual_seed(0)
+    L = Learner(Policy(cfg), LossConfig(algo='ppo'), device='cpu', backend='torch')
+    ms = [L.train_step(make_batch(2, 8, cfg.layout, cfg.hidden, device='cpu', seed=s)) for s in range(3)]
+    vals = [float(m['grad_norm']) for m in ms]
+    assert len({m['grad_norm'].data_ptr() for m in ms}) == 3
+    assert float(L.opt.last_grad_norm) == vals[-1] and len(set(vals)) == 3

@@ -34,6 +34,24 @@ def test_quota_caps_the_thread_budget_not_the_mask():
     assert min(14, p.threads(reserve=2)) == 14
 
 
+def test_eight_rank_thread_sizing_under_quota():
+    """The thread counts bench.py / the node loop use for 8 ranks: a 16-CPU quota leaves 1 actor thread per rank
+    (the learner keeps the other CPU of its 2-CPU share), a 128-CPU quota the 14-thread cap."""
+    nodes = [0, 0, 0, 0, 1, 1, 1, 1]
+    node_cpus = {0: list(range(0, 64)) + list(range(128, 192)), 1: list(range(64, 128)) + list(range(192, 256))}
+    for quota, expect in ((16, 1), (128, 14), (32, 3), (8, 1)):
+        plans = [P.plan(r, 8, affinity=range(256), quota=quota, gpu_nodes=nodes, node_cpus=node_cpus)
+                 for r in range(8)]
+        assert all(p.share == max(1, quota // 8) for p in plans)
+        assert [p.actor_threads() for p in plans] == [expect] * 8
+        # the node's actor threads plus one learner CPU per rank never exceed the quota once it is ≥ 2 per rank
+        if quota >= 16:
+            assert sum(p.actor_threads() + 1 for p in plans) <= quota
+    # one rank with the whole 16-CPU box share: the measured 14-thread point
+    p = P.plan(0, 1, affinity=range(256), quota=16, gpu_nodes=[0], node_cpus=node_cpus)
+    assert p.actor_threads() == 14
+
+
 def test_even_split_without_topology():
     plans = [P.plan(r, 4, affinity=range(8), quota=None, gpu_nodes=None, node_cpus={}) for r in range(4)]
     assert all(p.source == 'even-split' for p in plans)
