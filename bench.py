@@ -29,7 +29,9 @@ EVERY rank (one actor runtime per GPU), and reported as node aggregates (sums ov
 * ``model_5v5_exact`` — the 5v5 policy at IEEE fp32 (BASELINE config 4 at the reference precision): the torch backend,
   since the fused attention-block kernels are bf16x3 only (``model_5v5`` is the fused bf16x3 number);
 * ``bptt350_learner`` — truncated BPTT: each sequence trained as ``seq_len / 350`` chains of 350 steps from
-  actor-stored (h, c) (bf16x3 operands — the exact recurrence takes ≤ 8 sequences per step; not the headline);
+  actor-stored (h, c) (32 sequences of 350 steps per step, at the headline's precision; not the headline);
+* ``learner_b16`` / ``learner_b32`` — the same learner at 16 / 32 sequences per GPU per step (the exact recurrence
+  packs 2 / 4 rows per XCD chain; the reference's ``--batch-size`` is free, optimizer.py:776; not the headline);
 * ``league_replay`` — BASELINE config 5 through the same node loop: PFSP self-play league (80 % of games on the
   latest weights), the fp8 actor policy step, and learners sampling every minibatch from an on-HBM replay of
   ``--league-replay-gb`` GB per GPU (``config.replay_capacity`` sequences).
@@ -79,7 +81,9 @@ def parse():
                     help='also time the 5v5 policy at IEEE fp32 on the torch backend (extra field model_5v5_exact)')
     ap.add_argument('--bptt350-extra', type=int, default=1,
                     help='also time truncated BPTT: each sequence as seq_len/350 chains of 350 steps from stored '
-                         '(h, c) (extra field bptt350_learner, bf16x3 operands; not the headline)')
+                         '(h, c) (extra field bptt350_learner, headline precision; not the headline)')
+    ap.add_argument('--big-batch-extra', type=int, default=1,
+                    help='also time 16 and 32 sequences per GPU per step (extra fields learner_b16 / learner_b32)')
     ap.add_argument('--replay', type=int, default=0, help='sequences in the on-HBM replay pool (0 = 4x batch)')
     ap.add_argument('--graph', type=int, default=-1, help='capture the step in a hipGraph (-1 = auto)')
     ap.add_argument('--actor', type=int, default=1, help='also measure actor steps/s (untimed region)')
@@ -98,7 +102,7 @@ def parse():
     ap.add_argument('--e2e-games', type=int, default=3072)
     ap.add_argument('--e2e-threads', type=int, default=0,
                     help='actor host threads of the node loop (0 = from the CPU share, in [1, 14])')
-    ap.add_argument('--e2e-actor-precision', default='bf16', choices=['bf16', 'fp8'],
+    ap.add_argument('--e2e-actor-precision', default='bf16', choices=['bf16', 'fp32', 'fp8'],
                     help='policy step of the node loop\'s actors (fp8: the BASELINE config-5 step; the loop measured '
                          '1.15-1.20 vs ≈1.0 M steps/s, its kernels co-run better beside the learner\'s recurrence)')
     ap.add_argument('--e2e-actor-procs', type=int, default=1,
@@ -343,18 +347,32 @@ def main():
             and args.seq_len % 350 == 0 and args.seq_len > 350):
         # truncated BPTT (SURVEY §5 long-context row): every seq_len-step sequence trained as seq_len/350
         # independent 350-step chains that start from the (h, c) the actor stored every 350 steps (replay h0 / c0),
-        # 4x fewer serial recurrence steps. More than 8 sequences per step run on the bf16x3 team kernel (several rows
-        # per chain), so this extra is fp32 with bf16x3 operands — never the headline
+        # 4x fewer serial recurrence steps; 32 chains per step run as 8 XCD chains of 4 rows (exact VALU recurrence)
         learner = None
         k = args.seq_len // 350
         try:
-            eb, lb0, lb1, _, _ = run('fp32', B=args.batch_size * k, S=350)
+            eb, lb0, lb1, _, _ = run(args.precision, B=args.batch_size * k, S=350)
             progress(f'learner bptt350 done: {eb / args.steps * 1e3:.3f} ms/step')
-            bptt = {'precision': 'fp32 activations / bf16x3-split MFMA operands', 'chains_per_sequence': k,
+            bptt = {'precision': args.precision, 'chains_per_sequence': k,
                     'batch': args.batch_size * k, 'seq_len': 350, 'value': samples / eb,
                     'ms_per_step': eb / args.steps * 1e3, 'loss_first': lb0, 'loss_last': lb1}
         except Exception as e:
             bptt = {'error': repr(e)}
+
+    big = {}
+    if args.big_batch_extra and use_cuda and cfg.rnn == 'lstm' and not cfg.entity_attention:
+        # the same learner at 16 / 32 sequences per GPU (2 / 4 rows per XCD chain of the exact recurrence): the
+        # recurrence is latency-bound, so samples per step grow faster than its time
+        learner = None
+        for bb in (16, 32):
+            try:
+                ebb, l0, l1, _, _ = run(args.precision, B=bb)
+                progress(f'learner B={bb} done: {ebb / args.steps * 1e3:.3f} ms/step')
+                big[f'learner_b{bb}'] = {'precision': args.precision, 'batch': bb, 'seq_len': args.seq_len,
+                                         'value': bb * args.seq_len * world * args.steps / ebb,
+                                         'ms_per_step': ebb / args.steps * 1e3, 'loss_first': l0, 'loss_last': l1}
+            except Exception as e:
+                big[f'learner_b{bb}'] = {'error': repr(e)}
 
     def gather(x):
         """Every rank's value of ``x`` on every rank (rank order)."""
@@ -522,6 +540,8 @@ def main():
             'model_5v5': model_5v5,
             'model_5v5_exact': model_5v5_exact,
             'bptt350_learner': bptt,
+            'learner_b16': big.get('learner_b16'),
+            'learner_b32': big.get('learner_b32'),
             'dp_replicas_identical': len(set(shas)) == 1,
             'weights_sha16_per_rank': shas,
             'actor': actor,

@@ -5,13 +5,17 @@ The reference actor runs one player per process on the CPU: featurize → ``poli
 h/c) lives on the GPU in fixed slots and one step of *all* slots is a captured graph:
 
     H2D(env, units, handles, keep)           pinned → static device buffers (one copy each)
-    h, c *= keep                             episode resets without host round trips
     encoder_fwd                              fused entity encoder kernel (shared with the learner)
-    relu(x896·W_preᵀ + b)                    hipBLASLt
-    gates = [x | h]·[W_ih | W_hh]ᵀ + b        ONE hipBLASLt GEMM (fp32 out) → lstm_cell kernel (or fake_rnn Linear)
-    z = h·W_headsᵀ + b                       one GEMM for all 5 heads (q | enum | x | y | value)
+    [5v5: attn_block_fwd                     LayerNorm + QKV + attention + out-projection + pools, one kernel]
+    actor_core                               ONE kernel (ops/csrc/actor_core.hip): episode resets (h, c *= keep),
+                                             relu(x896·W_preᵀ + b), gates = [x | h]·[W_ih | W_hh]ᵀ + b + LSTM cell
+                                             (or the fake_rnn Linear), z = h·W_headsᵀ + b for all 5 heads
     sample_actions                           fused masked log-softmax + Gumbel-max + hierarchical selection
     D2H(idx, logp, value[, act, msk])
+
+No vendor GEMM in any actor step: bf16 operands (:class:`GpuActorPolicy`, the default), IEEE fp32 on the f32 MFMA
+(:class:`F32ActorPolicy` — the reference actor's precision, agent.py:641-660 → policy.py:80-84) or e4m3
+(:class:`Fp8ActorPolicy`).
 
 so the host only featurizes (native C++, :mod:`dotaclient_amd.native`) and turns indices into protobuf actions.
 Sampling uses a counter-based hash RNG (seed, step counter, row, head, entry) kept in device memory, so replays
@@ -57,8 +61,23 @@ class _Pack:
             self.dev_bytes[a:b].copy_(self.host_bytes[a:b], non_blocking=True)
 
 
+def frag_weight(w: torch.Tensor, mode: int) -> torch.Tensor:
+    """(N, K) fp32 weight → the MFMA fragment order of ops/csrc/actor_core.hip: mode 0 (fp32) [N/16][K/16][lane][4]
+    with element j of lane l = w[16·t + (l & 15)][16·g + 4·(l >> 4) + j]; mode 1 (bf16) [N/16][K/32][lane][8] with
+    w[16·t + (l & 15)][32·g + 8·(l >> 4) + j]. One wave's k-group load is 1 KB contiguous."""
+    N, K = w.shape
+    kg, e = (16, 4) if mode == 0 else (32, 8)
+    if N % 16 or K % kg:
+        raise ValueError(f'frag_weight: ({N}, {K}) must be multiples of (16, {kg})')
+    src = w.float() if mode == 0 else w.to(torch.bfloat16)
+    return src.reshape(N // 16, 16, K // kg, 4, e).permute(0, 2, 3, 1, 4).contiguous().view(-1)
+
+
 class GpuActorPolicy:
-    """Fixed-slot batched policy step on one GPU: LSTM / linear-RNN policies, 1v1 or 5v5 (entity attention)."""
+    """Fixed-slot batched policy step on one GPU: LSTM / linear-RNN policies, 1v1 or 5v5 (entity attention), bf16
+    operands on hand-written MFMA kernels (``CORE_MODE`` 1; :class:`F32ActorPolicy` is the IEEE-fp32 twin)."""
+
+    CORE_MODE = 1        # ops/csrc/actor_core.hip: 0 = IEEE fp32 (f32 MFMA), 1 = bf16 operands
 
     def __init__(self, policy: Policy, n_slots: int, device='cuda', seed: int = 0, use_graph: bool = True,
                  record: bool = True, inputs_from: Optional['GpuActorPolicy'] = None):
@@ -118,8 +137,7 @@ class GpuActorPolicy:
         self.d_handles = self.in_pack.dev['handles']
         self.h = torch.zeros(n, H, device=dev)
         self.c = torch.zeros(n, H, device=dev)
-        self.h16 = torch.zeros(n, H, dtype=torch.bfloat16, device=dev)
-        self.xh = torch.zeros(n, self.cfg.pre_rnn_dim + H, dtype=torch.bfloat16, device=dev)   # [x | bf16(h)]
+        self.z = torch.zeros(n, LDZ, device=dev)                 # head logits [q | enum | x | y | value | pad]
         self.ctr = torch.zeros(1, dtype=torch.long, device=dev)
         # outputs: [idx | logp | value] first (the part every step returns), then [act | msk] (recorded steps)
         self.out_pack = _Pack([('idx', (n, 4), torch.int32), ('logp', (n,), torch.float32),
@@ -187,37 +205,44 @@ class GpuActorPolicy:
                     self.w[k].copy_(v)
 
     def _weight_dict(self, sd) -> Dict[str, torch.Tensor]:
-        dev = self.device
+        dev, mode, cfg = self.device, self.CORE_MODE, self.cfg
         g = (lambda k: sd[k].detach().to(dev, torch.float32))
         bf = (lambda k: sd[k].detach().to(dev, torch.bfloat16))
+        attn32 = cfg.entity_attention or mode == 0       # fp32 encoder output (bf16x3 / exact encoder variants)
+        wt = torch.stack([g(f'affine_unit_{s}.weight') for s in TYPE_SUFFIX]).contiguous()
         w = {
             'w1': g('affine_unit_basic_stats.weight').contiguous(), 'b1': g('affine_unit_basic_stats.bias'),
             # (entity attention: the encoder adds b_τ + b_out — the residual's bias folded into E0, as the learner)
-            'wt16': torch.stack([bf(f'affine_unit_{s}.weight') for s in TYPE_SUFFIX]).contiguous(),
+            'wt': wt if attn32 else wt.to(torch.bfloat16),
             'bt': torch.stack([g(f'affine_unit_{s}.bias') for s in TYPE_SUFFIX]).contiguous(),
             'we': g('affine_env.weight').contiguous(), 'be': g('affine_env.bias'),
-            'wpreT': bf('affine_pre_rnn.weight').t().contiguous(), 'bpre': g('affine_pre_rnn.bias'),
-            'bpre16': bf('affine_pre_rnn.bias').contiguous(),
+            'cpre': frag_weight(g('affine_pre_rnn.weight'), mode), 'bpre': g('affine_pre_rnn.bias').contiguous(),
         }
-        if self.cfg.entity_attention:
+        if cfg.entity_attention:
+            from ..models.pipelined import _frag_order
             w['bt'] = (w['bt'] + g('entity_attn.out.bias')[None]).contiguous()
             w['bout'] = g('entity_attn.out.bias').contiguous()
             w['ln_g'] = g('entity_attn.ln.weight').contiguous()
             w['ln_b'] = g('entity_attn.ln.bias').contiguous()
-            w['wqkv16'] = bf('entity_attn.qkv.weight').contiguous()
-            w['bqkv16'] = bf('entity_attn.qkv.bias').contiguous()
-            w['wout16'] = bf('entity_attn.out.weight').contiguous()
-        H = self.cfg.hidden
-        if self.cfg.rnn == 'lstm':
-            w['wcatT'] = torch.cat([bf('rnn.weight_ih_l0'), bf('rnn.weight_hh_l0')], 1).t().contiguous()
-            w['brnn'] = g('rnn.bias_ih_l0') + g('rnn.bias_hh_l0')
+            w['bqkv'] = g('entity_attn.qkv.bias').contiguous()
+            # W_qkv / W_out hi / lo bf16 images in MFMA fragment order (ops/csrc/attn_block.hip, as the learner)
+            for key, name in (('wq', 'entity_attn.qkv.weight'), ('wo', 'entity_attn.out.weight')):
+                hi, lo = self.C.split_bf16x2(g(name).contiguous())
+                w[key + '_h'], w[key + '_l'] = _frag_order(hi), _frag_order(lo)
+        H = cfg.hidden
+        if cfg.rnn == 'lstm':
+            from ..ops.lstm import gate_perm
+            perm = gate_perm(H, dev)                   # unit-major gate rows: a unit's i, f, g, o in 4 columns
+            wcat = torch.cat([g('rnn.weight_ih_l0'), g('rnn.weight_hh_l0')], 1)[perm]
+            w['cg'] = frag_weight(wcat.contiguous(), mode)
+            w['bg'] = (g('rnn.bias_ih_l0') + g('rnn.bias_hh_l0'))[perm].contiguous()
         else:
-            w['wfT'] = bf('fake_rnn.weight').t().contiguous()
-            w['bf'] = g('fake_rnn.bias')
+            w['cg'] = frag_weight(g('fake_rnn.weight'), mode)
+            w['bg'] = g('fake_rnn.bias').contiguous()
         heads = ['affine_unit_attention', 'affine_head_enum', 'affine_move_x', 'affine_move_y', 'affine_value']
         wh = torch.cat([g(f'{k}.weight') for k in heads] + [torch.zeros(LDZ - 150, H, device=dev)], 0)
         bh = torch.cat([g(f'{k}.bias') for k in heads] + [torch.zeros(LDZ - 150, device=dev)], 0)
-        w['whT'] = wh.to(torch.bfloat16).t().contiguous()
+        w['ch'] = frag_weight(wh, mode)
         w['bh'] = bh.contiguous()
         w['wh32'] = wh.contiguous()
         return w
@@ -226,36 +251,26 @@ class GpuActorPolicy:
     def _forward(self):
         """The captured body: reads d_* / h / c, writes idx/act/msk/logp/value and the new h / c.
 
-        bf16 path, 7 launches: encoder kernel → pre-RNN GEMM (bias + ReLU epilogue, bf16 out) → ``actor_state_prep``
-        (episode resets + the [x | bf16(h)] operand + the sampler's RNG counter bump) → ONE gate GEMM (K = P + H, bias
-        epilogue) → LSTM cell → heads GEMM (bias epilogue) → sampling kernel."""
+        3 launches (5v5: 4), none a vendor GEMM: encoder kernel [→ attention block] → ``actor_core`` (episode
+        resets, pre-RNN layer, gates + LSTM cell or the linear layer, heads; bumps the sampler's RNG counter) →
+        sampling kernel."""
         C, w, cfg = self.C, self.w, self.cfg
-        x896, emb, _ = C.encoder_fwd(self.d_units, self.d_env, w['w1'], w['b1'], w['wt16'], w['bt'], w['we'],
-                                     w['be'], list(cfg.layout.counts), bool(cfg.compat_bugs))
+        x896, emb, arg = C.encoder_fwd(self.d_units, self.d_env, w['w1'], w['b1'], w['wt'], w['bt'], w['we'],
+                                       w['be'], list(cfg.layout.counts), bool(cfg.compat_bugs),
+                                       exact=self.CORE_MODE == 0)
         if cfg.entity_attention:
-            # 5v5 pre-LN self-attention over the 64 unit slots (ops/csrc/attn.hip), pools of the attended embeddings
-            E0p = emb.view(self.n * self.U, 128)
-            Xn, _, _ = C.ln_fwd(E0p, w['bout'], w['ln_g'], w['ln_b'], 1e-5)
-            QKV = torch.addmm(w['bqkv16'], Xn, w['wqkv16'].t())
-            Oat, _ = C.attn_fwd(QKV)
-            E1 = torch.addmm(E0p, Oat, w['wout16'].t())                # residual + out-projection
-            C.attn_pool(E1, self.toff, x896, bool(cfg.compat_bugs))
-            emb = E1.view(self.n, self.U, 128)
+            # 5v5 pre-LN self-attention over the 64 unit slots + pools of the attended embeddings, ONE kernel
+            # (ops/csrc/attn_block.hip, the learner's forward); E1 is the pointer head's unit embedding
+            out = C.attn_block_fwd(emb.view(self.n * self.U, 128), w['bout'], w['ln_g'], w['ln_b'], w['wq_h'],
+                                   w['wq_l'], w['bqkv'], w['wo_h'], w['wo_l'], self.toff, x896, arg,
+                                   bool(cfg.compat_bugs), 1e-5)
+            emb = out[6].view(self.n, self.U, 128)
         elif cfg.compat_bugs:
             x896[:, 768:896] = x896[:, 512:640]
-        x = torch._addmm_activation(w['bpre16'], x896, w['wpreT'])
-        if cfg.rnn == 'lstm':
-            C.actor_state_prep(x, self.h, self.c, self.d_keep.view(-1), self.xh, self.ctr)
-            gates = torch.addmm(w['brnn'], self.xh, w['wcatT'], out_dtype=torch.float32)
-            C.lstm_cell(gates, self.h, self.c, self.h16, self.d_active)
-            xh = self.h16
-        else:
-            self.h.copy_(torch.addmm(w['bf'], x, w['wfT'], out_dtype=torch.float32))
-            xh = self.h.to(torch.bfloat16)
-        z = torch.addmm(w['bh'], xh, w['whT'], out_dtype=torch.float32)
-        if cfg.rnn != 'lstm':
-            self.ctr.add_(1)
-        C.sample_actions(z, emb, self.d_handles, self.seed, self.ctr, self.idx, self.act, self.msk, self.logp,
+        C.actor_core(x896, w['cpre'], w['bpre'], w['cg'], w['bg'], w['ch'], w['bh'], self.h, self.c,
+                     self.d_keep.view(-1), self.z, self.CORE_MODE, cfg.rnn != 'lstm', active=self.d_active,
+                     bump=self.ctr)
+        C.sample_actions(self.z, emb, self.d_handles, self.seed, self.ctr, self.idx, self.act, self.msk, self.logp,
                          self.value)
 
     def _h2d(self):
@@ -363,6 +378,20 @@ class GpuActorPolicy:
         return self.h, self.c
 
 
+class F32ActorPolicy(GpuActorPolicy):
+    """:class:`GpuActorPolicy` at the reference actor's precision (agent.py:641-660 → policy.py:80-84, torch fp32):
+    the IEEE-fp32 entity encoder (``encoder_fwd`` exact: the learner's ``encoder_fwd_x_kernel``) and the fp32
+    ``actor_core`` (every product an fp32 FMA on ``v_mfma_f32_16x16x4_f32``), fp32 unit embeddings into the sampler.
+    1v1 policies (LSTM-128 / LSTM-512, or the compat linear layer); the 5v5 attention block has no exact variant."""
+
+    CORE_MODE = 0
+
+    def __init__(self, policy: Policy, n_slots: int, device='cuda', **kw):
+        if policy.config.entity_attention:
+            raise ValueError('F32ActorPolicy: 1v1 policies (the attention block has no IEEE-fp32 kernel)')
+        super().__init__(policy, n_slots, device=device, **kw)
+
+
 # fp8 encoder form of the actor step: the per-unit workgroup kernel (True) or the wave-parallel one (False)
 _FP8_ENC_PER_UNIT = os.environ.get('DCA_FP8_ENC_PER_UNIT', '0') == '1'
 
@@ -407,7 +436,6 @@ class Fp8ActorPolicy(GpuActorPolicy):
         if self.compact:
             self.UNITS_DTYPE, self.HANDLES_DTYPE = torch.float16, torch.int32
         super()._alloc(inputs_from)
-        self.z = torch.zeros(self.n, LDZ, device=self.device)
         if inputs_from is not None and inputs_from.h_units.dtype != self.UNITS_DTYPE:
             raise ValueError('Fp8ActorPolicy: inputs_from must stage the same feature dtype')
 
@@ -427,7 +455,7 @@ class Fp8ActorPolicy(GpuActorPolicy):
         wt = [fp8_weight(g(f'affine_unit_{s}.weight')) for s in TYPE_SUFFIX]
         w['wt8'] = torch.cat([q for q, _ in wt]).contiguous()
         w['st8'] = torch.stack([s_ for _, s_ in wt]).contiguous()
-        for k in ('wcatT', 'brnn', 'whT', 'wpreT', 'bpre16', 'wt16'):   # the bf16 step's operands are not used here
+        for k in ('cpre', 'cg', 'ch', 'wt'):       # the bf16 core's operands are not used here
             w.pop(k, None)
         return w
 
@@ -511,15 +539,20 @@ class TorchSlotPolicy:
         return self._out
 
 
+ACTOR_PRECISIONS = ('bf16', 'fp32', 'fp8')
+
+
 def make_slot_policy(policy: Policy, n_slots: int, device='cuda', precision: str = 'bf16', **kw):
-    """The fused graph-captured :class:`GpuActorPolicy` where it applies (``precision='fp8'``:
-    :class:`Fp8ActorPolicy`), else :class:`TorchSlotPolicy`."""
+    """The fused graph-captured :class:`GpuActorPolicy` where it applies (``precision='fp32'``:
+    :class:`F32ActorPolicy`, ``'fp8'``: :class:`Fp8ActorPolicy`), else :class:`TorchSlotPolicy`."""
     dev = torch.device(device)
     cfg = policy.config
+    if precision not in ACTOR_PRECISIONS:
+        raise ValueError(f'actor precision must be one of {ACTOR_PRECISIONS}, got {precision!r}')
     if precision == 'fp8':
         return Fp8ActorPolicy(policy, n_slots, device=dev, **kw)
-    if precision != 'bf16':
-        raise ValueError(f'actor precision must be bf16 or fp8, got {precision!r}')
+    if precision == 'fp32' and dev.type == 'cuda' and not cfg.entity_attention:
+        return F32ActorPolicy(policy, n_slots, device=dev, **kw)
     if dev.type == 'cuda' and cfg.unit_dim == 128 and cfg.env_dim == 128 and (
             not cfg.entity_attention or (cfg.layout.max_units == 64 and cfg.attention_heads == 4)):
         return GpuActorPolicy(policy, n_slots, device=dev, **kw)
@@ -564,13 +597,14 @@ def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048,
     ``n_games`` 1v1 games = 2·n_games player slots stepped per launch. With ``featurize`` the host side decodes
     and featurizes serialized world states through the native featurizer every step (the reference actor's
     per-step work, agent.py:611-660) overlapped with the previous GPU step; otherwise only the GPU step + copies
-    are timed. ``precision='fp8'``: :class:`Fp8ActorPolicy`. Returns ``{'steps_per_s', 'gpu_steps_per_s',
+    are timed. ``precision='fp8'``: :class:`Fp8ActorPolicy`, ``'fp32'``: :class:`F32ActorPolicy`. Returns ``{'steps_per_s', 'gpu_steps_per_s',
     'ms_per_step', 'slots'}``.
     """
     n = 2 * n_games
     dev = torch.device(device)
     layout = policy.config.layout
-    gp = (Fp8ActorPolicy if precision == 'fp8' else GpuActorPolicy)(policy, n, device=dev, seed=1234, record=True)
+    cls = {'fp8': Fp8ActorPolicy, 'fp32': F32ActorPolicy}.get(precision, GpuActorPolicy)
+    gp = cls(policy, n, device=dev, seed=1234, record=True)
     feat = None
     if featurize:
         from .. import native

@@ -21,11 +21,14 @@ from ..constants import REWARD_KEYS
 
 def evaluate_vs_default_bot(policy, n_games: int = 128, device='cuda', seed: int = 12345,
                             max_dota_time: float = 600.0, threads: int = 8, timeout: float = 600.0,
-                            precision: str = 'bf16') -> Dict[str, float]:
+                            precision: str = 'fp32') -> Dict[str, float]:
     """Play ``n_games`` games of ``policy`` (a :class:`~dotaclient_amd.models.policy.Policy`) against the default bot
     and return the reference's validation metrics averaged over the games: ``game/rewards_sum``,
     ``game/rewards_<key>`` for every reward key, ``game/win_rate`` (wins / games), ``game/loss_rate``,
-    ``game/steps`` (mean game length) and ``games``. A fixed ``seed`` gives the same games for every policy."""
+    ``game/steps`` (mean game length) and ``games``. A fixed ``seed`` gives the same games for every policy.
+    ``precision``: the policy step the games are played with — by default the IEEE-fp32 actor
+    (:class:`~dotaclient_amd.actor.batched.F32ActorPolicy`, the weights as the learner trained them; the reference's
+    validation agent runs the fp32 policy); 5v5 policies fall back to bf16 operands."""
     from ..transport.codec import decode
     from .vec import VecActor
     from .weights import WeightStore
@@ -33,7 +36,8 @@ def evaluate_vs_default_bot(policy, n_games: int = 128, device='cuda', seed: int
     ws = WeightStore(policy.config, device='cpu')
     ws.add(0, {k: v.detach().cpu() for k, v in policy.state_dict().items()})
     msgs: List[bytes] = []
-    va = VecActor(ws, n_games, msgs.append, device=device, mode='vs_default_bot', seed=seed,
+    mode = 'vs_default_bot_5v5' if policy.config.layout.counts[0] > 1 else 'vs_default_bot'   # 5 heroes a side
+    va = VecActor(ws, n_games, msgs.append, device=device, mode=mode, seed=seed,
                   rollout_size=10 ** 9, max_dota_time=max_dota_time, threads=threads, groups=1, stagger=False,
                   tag=f'val{seed}', precision=precision)
     t0 = time.time()
@@ -54,7 +58,8 @@ def evaluate_vs_default_bot(policy, n_games: int = 128, device='cuda', seed: int
         row.update({'sum': float(sums.sum()), 'steps': float(rew.shape[0]), 'won': float(rew[-1, 1] > 0.5),
                     'lost': float(rew[-1, 1] < -0.5)})
         per_game[r.game_id].append(row)
-    games = [rows[0] for rows in list(per_game.values())[:n_games]]    # one controlled player per game
+    # one controlled player per game (5v5: the team's rewards are per player; the end state is shared)
+    games = [rows[0] for rows in list(per_game.values())[:n_games]]
     out: Dict[str, float] = {'games': float(len(games))}
     if not games:
         return out

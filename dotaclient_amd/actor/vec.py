@@ -34,7 +34,7 @@ from .batched import make_slot_policy
 
 logger = logging.getLogger(__name__)
 
-MODES = {'1v1': 0, '5v5': 1, 'vs_default_bot': 2}
+MODES = {'1v1': 0, '5v5': 1, 'vs_default_bot': 2, 'vs_default_bot_5v5': 3}
 
 
 class _Opponent:
@@ -55,7 +55,8 @@ class _Group:
         self.S = self.ve.slots
         self.ppg = self.ve.players_per_game
         # (fp8: fp32 host staging, the native engine writes the buffers in place)
-        fp8 = {'precision': 'fp8', 'compact': False} if a.precision == 'fp8' else {}
+        fp8 = ({'precision': 'fp8', 'compact': False} if a.precision == 'fp8' else
+               {'precision': a.precision})
         self.gp = make_slot_policy(a.policy, self.S, device=a.device, seed=seed, **fp8)
         self.env = self.gp.h_env.numpy()
         self.units = self.gp.h_units.numpy()
@@ -93,7 +94,7 @@ class VecActor:
         self.store = weight_store
         self.policy = weight_store.latest_policy
         self.cfg = self.policy.config
-        if (mode == '5v5') != (self.cfg.layout.counts[0] > 1):
+        if (mode in ('5v5', 'vs_default_bot_5v5')) != (self.cfg.layout.counts[0] > 1):
             raise ValueError(f'mode {mode!r} does not match the policy layout {self.cfg.layout.counts}')
         self.publish = publish
         self.device = torch.device(device)
@@ -113,9 +114,11 @@ class VecActor:
         # observations as serialised CMsgBotWorldState protobufs through the native wire decoder + featurizer, and
         # orders as Actions protobufs (the reference actor's observe / act path, agent.py:805-825)
         self.wire = bool(wire)
-        # policy-step precision: bf16 (GpuActorPolicy) or fp8 (Fp8ActorPolicy, BASELINE config 5)
-        if precision not in ('bf16', 'fp8'):
-            raise ValueError(f'precision must be bf16 or fp8, got {precision!r}')
+        # policy-step precision: bf16 (GpuActorPolicy), fp32 (F32ActorPolicy, the reference actor's precision) or fp8
+        # (Fp8ActorPolicy, BASELINE config 5)
+        from .batched import ACTOR_PRECISIONS
+        if precision not in ACTOR_PRECISIONS:
+            raise ValueError(f'precision must be one of {ACTOR_PRECISIONS}, got {precision!r}')
         self.precision = precision
         groups = max(1, min(int(groups), n_games))
         sizes = [n_games // groups + (1 if i < n_games % groups else 0) for i in range(groups)]
@@ -168,7 +171,8 @@ class VecActor:
 
     def _opponent(self, g: _Group, k: int) -> _Opponent:
         while len(g.opp) <= k:
-            fp8 = {'precision': 'fp8', 'compact': False} if self.precision == 'fp8' else {}
+            fp8 = ({'precision': 'fp8', 'compact': False} if self.precision == 'fp8' else
+                   {'precision': self.precision})
             gp = make_slot_policy(self.policy, g.S, device=self.device, seed=g.seed + 104729 * (len(g.opp) + 1),
                                   inputs_from=g.gp, **fp8)
             g.opp.append(_Opponent(gp))

@@ -55,8 +55,9 @@ def build_parser():
                     help='vec: native vectorised self-play (actor/vec.py, synthetic env only); service: the '
                          'protobuf Actor over DotaService games; auto: vec for synthetic self-play')
     ap.add_argument('--threads', type=int, default=8, help='host threads of the vec runtime')
-    ap.add_argument('--actor-precision', type=str, default='bf16', choices=['bf16', 'fp8'],
-                    help='vec runtime policy step: bf16, or fp8 (e4m3 MFMA kernel; 1v1 LSTM-512 policies)')
+    ap.add_argument('--actor-precision', type=str, default='bf16', choices=['bf16', 'fp32', 'fp8'],
+                    help='vec runtime policy step: bf16, fp32 (IEEE fp32, the reference actor\'s precision; 1v1) or '
+                         'fp8 (e4m3 MFMA kernel; 1v1 LSTM-512 policies)')
     ap.add_argument('--league', type=str, default='oldest', choices=['oldest', 'uniform', 'recent', 'pfsp'],
                     help='opponent sampling over the weight history when not playing the latest weights')
     return ap

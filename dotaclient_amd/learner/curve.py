@@ -23,9 +23,12 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
                        games: int = 1024, threads: int = 12, seq_len: int = 1400, batch_size: int = 8,
                        seq_per_epoch: int = 16, lr: float = 1e-4, entropy_coef: float = 0.01,
                        max_dota_time: float = 600.0, pack: bool = True, seed: int = 7, device: str = 'cuda',
-                       eval_seed: int = 4242, on_row: Optional[Callable[[Dict], None]] = None) -> List[Dict]:
+                       eval_seed: int = 4242, on_row: Optional[Callable[[Dict], None]] = None,
+                       save_model: Optional[str] = None, eval_precision: str = 'fp32',
+                       mode: str = '1v1') -> List[Dict]:
     """Train for ``budget`` seconds (evaluations excluded) and return the evaluation rows (the first one before
-    any training). ``on_row`` is called with every row as it is produced."""
+    any training). ``on_row`` is called with every row as it is produced; ``save_model``: path that receives the
+    final weights (a reference-format state_dict file). ``eval_precision``: the validation games' policy step."""
     import torch
     from ..actor.validate import evaluate_vs_default_bot
     from ..actor.vec import VecActor
@@ -47,7 +50,7 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
     broker.subscribe_model(lambda v, b: loader.submit(ws.add_bytes, v, b))
     loader.submit(lambda: None).result()
     va = VecActor(ws, games, broker.publish_experience, device=device, seed=seed, rollout_size=9999,
-                  max_dota_time=max_dota_time, hidden_stride=seq_len, threads=threads, stagger=True)
+                  max_dota_time=max_dota_time, hidden_stride=seq_len, threads=threads, stagger=True, mode=mode)
     stop, pause, paused, err = threading.Event(), threading.Event(), threading.Event(), []
     rows: List[Dict] = []
     sync = torch.cuda.synchronize if str(device).startswith('cuda') else (lambda: None)
@@ -73,7 +76,7 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
         sync()
         t0 = time.time()
         row.update(evaluate_vs_default_bot(opt.policy, n_games=eval_games, device=device, seed=eval_seed,
-                                           max_dota_time=max_dota_time, threads=threads))
+                                           max_dota_time=max_dota_time, threads=threads, precision=eval_precision))
         row['eval_s'] = round(time.time() - t0, 3)
         pause.clear()
         rows.append(row)
@@ -102,6 +105,10 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
                           'train_reward_per_sec': m.get('reward_per_sec/sum'),
                           'avg_weight_age': m.get('avg_weight_age')})
                 next_eval += eval_every
+        if save_model:
+            opt.flush_metrics()
+            sync()
+            torch.save({k: v.detach().cpu() for k, v in opt.policy.state_dict().items()}, save_model)
     finally:
         stop.set()
         if th.is_alive():

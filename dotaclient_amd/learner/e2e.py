@@ -273,11 +273,9 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
 
     world, rank = pdist.get_world_size(), pdist.get_rank()
     local_world = int(os.environ.get('LOCAL_WORLD_SIZE', world))
-    # the learner's persistent recurrence shares this GPU with the actor process (graph replays, context start-up,
-    # the fp8 / league actors' weight swaps): a team member's CU can be held past the exclusive-GPU hand-off limit
-    # (≈1 s of polling; seen once in the config-5 loop: backward timeout, code 2) — use the patient limit (≈1 min;
-    # a real lost hand-off still ends in the error)
-    os.environ.setdefault('DCA_TEAM_PATIENT', '1')
+    # (the recurrence's hand-off timeout is wall-clock per wait — ops/csrc/lstm_team.hip spin_fail — so the actor
+    # process's kernels slowing it down beside the learner no longer accumulate towards it; the one config-5 timeout
+    # of round 4 was that cumulative poll count, not a lost hand-off)
     if transport == 'auto':
         from .. import native
         transport = 'shm' if (local_world == world and native.AVAILABLE) else 'tcp'

@@ -74,7 +74,8 @@ class Learner:
         self.cfg = loss_cfg
         self.precision = precision
         self.policy = policy.to(self.device)
-        if backend == 'auto':
+        auto = backend == 'auto'
+        if auto:
             backend = 'fused' if self.device.type == 'cuda' else 'torch'
         self.backend = backend
         self.flat = FlatParams(self.policy, device=self.device)
@@ -85,8 +86,14 @@ class Learner:
         self.model = self.policy
         if backend == 'fused':
             from ..models.fused import FusedPolicy
-            self.model = FusedPolicy(self.policy, loss_cfg, precision=precision)
-            self.model.attach_flat(self.flat.flat)
+            fused = FusedPolicy(self.policy, loss_cfg, precision=precision)
+            if fused.use_pipeline():
+                self.model = fused
+                self.model.attach_flat(self.flat.flat)
+            elif auto:
+                self.backend = backend = 'torch'     # a configuration the kernels do not cover
+            else:
+                raise ValueError(f'backend fused: no kernel path for {self.policy.config} at {precision}')
         self.counts = self.policy.layout.action_counts()
         self.n_steps = 0
         self.graph = None                 # captured forward+backward (see enable_graph)

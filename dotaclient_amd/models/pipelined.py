@@ -100,19 +100,23 @@ class WeightImages:
             assert 0 <= off and off + p.numel() <= flat.numel(), f'{name} is not a view of the flat buffer'
             return torch.arange(p.numel(), dtype=torch.int64).view(p.shape) + off
 
-        perm = fp.gate_perm(H, 'cpu')
+        lstm = cfg.rnn == 'lstm'
+        perm = fp.gate_perm(H, 'cpu') if lstm else None
         neg = lambda *shape: torch.full(shape, -1, dtype=torch.int64)  # noqa: E731
+        # the recurrent layer's input weight — W_ih (rows in unit-major gate order) or the reference's linear fake_rnn
+        # W_f (policy.py:67-68, 143-145) — keeps the keys wih16 / wihT16 / ih_s / dx1_s for both
+        w_in = idx('rnn.weight_ih_l0')[perm] if lstm else idx('fake_rnn.weight')
         wt = torch.stack([idx(f'affine_unit_{s}.weight') for s in TYPE_SUFFIX])
         head_rows = [idx('affine_unit_attention.weight'), idx('affine_head_enum.weight'),
                      idx('affine_move_x.weight'), idx('affine_move_y.weight'),
                      idx('affine_value.weight') if with_value else neg(1, H)]
         wcat = torch.cat(head_rows + [neg(LDZ - 150, H)], 0)
         parts16 = {'wt16': wt, 'wtT16': wt.transpose(1, 2).contiguous(), 'wpre16': idx('affine_pre_rnn.weight'),
-                   'bpre16': idx('affine_pre_rnn.bias'),
-                   'wih16': idx('rnn.weight_ih_l0')[perm], 'whh16': idx('rnn.weight_hh_l0'), 'wcat16': wcat,
-                   # (in, 4H) copy for ∂pre = ∂G·W_ih: hipBLASLt is 1.7x faster with this operand K-contiguous
-                   # (85 vs 141 µs at 11200×2048×256, fast fp32)
-                   'wihT16': idx('rnn.weight_ih_l0')[perm].t().contiguous()}
+                   'bpre16': idx('affine_pre_rnn.bias'), 'wih16': w_in, 'wcat16': wcat,
+                   # (in, 4H) copy for ∂pre = ∂G·W_ih: the ∂X chain's operand K-contiguous per column
+                   'wihT16': w_in.t().contiguous()}
+        if lstm:
+            parts16['whh16'] = idx('rnn.weight_hh_l0')
         if getattr(fp, 'fp32', False):
             # (out, in)-transposed pre-RNN weight: the fused ∂X chain's second operand, K-contiguous per column
             parts16['wpreT'] = idx('affine_pre_rnn.weight').t().contiguous()
@@ -120,7 +124,8 @@ class WeightImages:
                   idx('affine_move_y.bias'), idx('affine_value.bias') if with_value else neg(1)]
         bcat = torch.cat(head_b + [neg(LDZ - 150)])
         parts32 = {'bt': (torch.stack([idx(f'affine_unit_{s}.bias') for s in TYPE_SUFFIX]), None),
-                   'bias4': (idx('rnn.bias_ih_l0')[perm], idx('rnn.bias_hh_l0')[perm]),
+                   'bias4': ((idx('rnn.bias_ih_l0')[perm], idx('rnn.bias_hh_l0')[perm]) if lstm
+                             else (idx('fake_rnn.bias'), None)),
                    'bcat': (bcat, None)}
         if cfg.entity_attention and getattr(fp, 'fp32', False):
             # fp32 5v5: the encoder adds b_τ + b_out as well (E0' = E0 + b_out; LayerNorm subtracts it again and the
@@ -149,7 +154,7 @@ class WeightImages:
             def slab(t):
                 return t.reshape(t.shape[0], t.shape[1] // 32, 32).permute(1, 0, 2).contiguous()
             wpre_i = idx('affine_pre_rnn.weight')
-            wih_i = idx('rnn.weight_ih_l0')[perm]
+            wih_i = w_in
             if getattr(fp, 'exact', False):
                 # IEEE-fp32 learner: the chain kernels take fp32 weights as they are (no hi / lo images); the heads
                 # GEMM's W_cat zero-padded to 256 rows and its transpose (the ∂h product's operand)
@@ -260,10 +265,6 @@ _HEADS_ROWMM = os.environ.get('DCA_HEADS_ROWMM', '1') != '0'
 # 2.50e-6, VPG 1.264e-5 vs 1.265e-5 where torch-fp32 itself is at 1.24e-5) and the fast form is 0.5 ms per step
 # faster (5.70 vs 6.20 ms)
 _EXACT_LIBM_ACT = os.environ.get('DCA_EXACT_ACT', 'fast') == 'libm'
-# exact learner, opt-in (DCA_FUSED_DW=1): ∂W_hh accumulated inside the backward recurrence instead of the gemm_tn
-# after it. Measured (profiles/r4_fused_dw_probe.md): the tail loses 330 µs but the recurrence gains 1.66 ms — the
-# 128 accumulators per lane live in AGPRs on the 4-wave form and their updates sit on every step's critical path
-_FUSED_DW = os.environ.get('DCA_FUSED_DW', '0') == '1'
 
 
 def fused_step_tm(fp, *args, **kw):
@@ -289,10 +290,11 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     Returns (partials (R,16) f32, logp (N) f32 time-major, grads {param name → tensor})."""
     from ..ops.gemm import gemm_tn as _gemm_tn
     exact = bool(getattr(fp, 'exact', False))
-    if exact and B > 8:
-        # lstm_team.hip plan(): up to 8 sequences run as one-row chains (one XCD team each) on the exact fp32 VALU
-        # recurrence; more pack several rows per chain on the bf16x3 MFMA team kernel — not IEEE fp32
-        raise ValueError(f'fp32-exact: at most 8 sequences per step and GPU (got {B}); use precision fp32')
+    lin = fp.cfg.rnn != 'lstm'          # the reference's linear fake_rnn layer (compat preset): no recurrence
+    if exact and B > 32 and not lin:
+        # lstm_team.hip plan(): the sequences run as chains of ≤ 4 rows (one XCD team each) on the exact fp32 VALU
+        # recurrence; more than 4 rows per chain take the bf16x3 MFMA team kernel — not IEEE fp32
+        raise ValueError(f'fp32-exact: at most 32 sequences per step and GPU (got {B}); use precision fp32')
 
     def gemm_tn(*a, **k):
         # weight gradients: split-K MFMA; IEEE-fp32 learner: exact v_mfma_f32_16x16x4_f32 (ops/csrc/gemm_tn.hip)
@@ -309,7 +311,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     w1, b1 = P['affine_unit_basic_stats.weight'].detach(), P['affine_unit_basic_stats.bias'].detach()
     we, be = P['affine_env.weight'].detach(), P['affine_env.bias'].detach()
     wt16, wtT16, wpre16 = W['wt16'], W['wtT16'], W['wpre16']
-    wih16, whh16, wcat16 = W['wih16'], W['whh16'], W['wcat16']
+    wih16, whh16, wcat16 = W['wih16'], W.get('whh16'), W['wcat16']
     bt, bias_p, bcat = W['bt'], W['bias4'], W['bcat']
     # ---- encoder, pre-RNN, input projection over all rows (row-parallel, fast)
     attn = cfg.entity_attention
@@ -371,21 +373,27 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         # IEEE-fp32 forward chain: the same kernel on v_mfma_f32_16x16x4_f32 with the fp32 weights as they are
         nil = wpre16.new_empty(0)
         x16, xp = C.pre_rnn_chain(x896, wpre16, nil, W['bpre16'], wih16, nil)
-        xp4 = xp.view(S, B, H, 4)
+        xp4 = xp.view(S, B, H, 4) if not lin else None
     elif f32 and _FWD_CHAIN:
         if 'pre_s' in W:                 # hi / lo images from the step's weight_prep launch
             fw1, fw2 = W['pre_s'], W['ih_s']
         else:
             fw1, fw2 = C.split_bf16x2(wpre16, True), C.split_bf16x2(wih16, True)   # slab-major bf16 hi / lo images
         x16, xp = C.pre_rnn_chain(x896, fw1[0], fw1[1], W['bpre16'], fw2[0], fw2[1])
-        xp4 = xp.view(S, B, H, 4)
+        xp4 = xp.view(S, B, H, 4) if not lin else None
     else:
+        assert not lin, 'the linear recurrent layer runs on the fp32 chain kernels'
         x16 = torch._addmm_activation(W['bpre16'], x896, wpre16.t())
         xp4 = _mm(x16, wih16.t()).view(S, B, H, 4)      # the recurrence kernel adds the bias (bias4)
-    hs16 = torch.empty(S, B, H, dtype=adt, device=dev)
-    cs = torch.empty(S, B, H, device=dev)
-    gates4 = torch.empty(S, B, H, 4, device=dev)
-    spans = chunk_bounds(S, fp.chunks)
+    if lin:
+        # fake_rnn: h = pre·W_fᵀ + b_f (the chain kernel's second product) — no activation, no recurrence
+        hs16 = xp.add_(bias_p).view(S, B, H)
+        cs = gates4 = None
+    else:
+        hs16 = torch.empty(S, B, H, dtype=adt, device=dev)
+        cs = torch.empty(S, B, H, device=dev)
+        gates4 = torch.empty(S, B, H, 4, device=dev)
+    spans = chunk_bounds(S, 1 if lin else fp.chunks)
     one = len(spans) == 1            # single chunk: outputs are used as produced (no staging copies)
     # sequence packing (learner/ingest.py): per-(step, row) episode-start flags, time-major (S, B) u8 — the team
     # recurrence zeroes h, c before a flagged step (forward) and stops the gradient there (backward)
@@ -410,7 +418,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     h_c, c_c = h0.contiguous(), c0.contiguous()
     fwd_done = []
     with torch.cuda.stream(sL):
-        for t0, t1 in spans:
+        for t0, t1 in ([] if lin else spans):
             o = team_fwd(C, xp4[t0:t1], whh16, h_c, c_c, fp.err, False, time_major=True,
                          hs_out=hs16[t0:t1], cs_out=cs[t0:t1], gates_out=gates4[t0:t1], bias4=bias_p,
                          precise=exact and _EXACT_LIBM_ACT, reset=rst)
@@ -418,6 +426,8 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             e = torch.cuda.Event()
             e.record(sL)
             fwd_done.append(e)
+    if lin:
+        fwd_done.append(ready)
     dx_w = None
     if f32 and _DX_FUSED and 'wpreT' in W:
         # weight operands of the fused ∂X kernel, split once per step into bf16 hi/lo images (exact: fp32 as is);
@@ -447,9 +457,10 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             zc = _addmm(bcat, xh, wcat16.t())     # bias in the GEMM epilogue
         # ∂L/∂z straight in the GEMM operand dtype: only the backward GEMMs read it
         dz16, dtl_c, part, lp = C.heads_loss(zc, emb[r0:r1], act_t[r0:r1], msk_t[r0:r1], adv_t[r0:r1],
-                                             ret_t[r0:r1], lpo_t[r0:r1], nret_t[r0:r1], norms, algo, False,
-                                             S, B, float(lc.clip_eps), float(lc.entropy_coef), float(lc.vf_coef),
-                                             dz_bf16=not f32, precise=exact)
+                                             ret_t[r0:r1], lpo_t[r0:r1], nret_t[r0:r1], norms, algo,
+                                             bool(lc.compat_value_bug), S, B, float(lc.clip_eps),
+                                             float(lc.entropy_coef), float(lc.vf_coef), dz_bf16=not f32,
+                                             precise=exact)
         parts.append(part)
         first = dWcat is None
         if first:
@@ -482,7 +493,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     split = fp.split_hook if (gout is not None and one) else None
     early_names = fp.early_param_names() if split is not None else frozenset()
     fp.early_applied = frozenset()
-    dgates16 = torch.empty(S, B, H, 4, dtype=adt, device=dev)   # ∂gates straight from the kernel
+    dgates16 = None if lin else torch.empty(S, B, H, 4, dtype=adt, device=dev)   # ∂gates straight from the kernel
     db = dw1 = db1 = dWt = dbt = dWe = dbe = None
     dgam = dbet = None
     first_attn = True
@@ -497,33 +508,32 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     # weight-gradient GEMMs: split-K MFMA over the B·S rows (ops/csrc/gemm_tn.hip), written in PyTorch's gate-major
     # row order through the gate permutation; in direct mode accumulated straight into the flat gradient buffer
     direct = gout is not None
-    dWhh = gout['rnn.weight_hh_l0'] if direct else torch.zeros(4 * H, H, device=dev)
-    dWih = gout['rnn.weight_ih_l0'] if direct else torch.zeros(4 * H, x16.shape[1], device=dev)
+    if lin:
+        dWhh = None
+        dWih = grads['fake_rnn.weight'] = torch.empty(H, x16.shape[1], device=dev)
+        dbf = grads['fake_rnn.bias'] = torch.empty(H, device=dev)
+    else:
+        dWhh = gout['rnn.weight_hh_l0'] if direct else torch.zeros(4 * H, H, device=dev)
+        dWih = gout['rnn.weight_ih_l0'] if direct else torch.zeros(4 * H, x16.shape[1], device=dev)
     dWpre = gout['affine_pre_rnn.weight'] if direct else torch.zeros(wpre16.shape[0], wpre16.shape[1], device=dev)
     dbpre = gout['affine_pre_rnn.bias'] if direct else torch.zeros(wpre16.shape[0], device=dev)
     h016 = h0.to(adt).contiguous()
     sL.wait_event(heads_done)
     dh_n = dc_n = None
     bwd_done = []
-    # exact one-chunk step: the backward recurrence accumulates ∂W_hh itself (ops/csrc/lstm_team.hip, V1 + DW: per
-    # chain partials in PyTorch row order, summed below) instead of a gemm_tn over the B·S rows after it
-    fused_dw = (exact and one and _FUSED_DW
-                and C.lstm_team_bwd_fuses_dw(B, H, True, bool(exact and _EXACT_LIBM_ACT)))
-    dwp = None
     with torch.cuda.stream(sL):
-        if fused_dw:
-            dwp = torch.empty(C.lstm_team_chains(B, True), 4 * H, H, device=dev)
-        for t0, t1 in reversed(spans):
+        for t0, t1 in ([] if lin else reversed(spans)):
             cinit = c0.contiguous() if t0 == 0 else cs[t0 - 1]
-            dwk = dict(hs_f32=hs16, h0=h016, dw_out=dwp) if fused_dw else {}
             o = team_bwd(C, dxh[t0:t1], gates4[t0:t1], cs[t0:t1], cinit, dh_n, dc_n, whh16, fp.err,
                          time_major=True, dg_out=dgates16[t0:t1], dg_bf16=not f32,
-                         want_dbias=True, precise=exact and _EXACT_LIBM_ACT, reset=rst, **dwk)
+                         want_dbias=True, precise=exact and _EXACT_LIBM_ACT, reset=rst)
             dh_n, dc_n = o[1], o[2]
             db = _acc(db, o[3])
             e = torch.cuda.Event()
             e.record(sL)
             bwd_done.append(e)
+        if lin:
+            bwd_done.append(heads_done)
         if heads_wg is not None:
             gemm_tn(heads_wg[0], heads_wg[1], out=dWcat, colsum=dbcat)
     # single chunk: the recurrence stream (idle once the backward recurrence is done) takes the weight-gradient GEMMs
@@ -535,12 +545,10 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         main.wait_event(done)
         r0, r1 = t0 * B, t1 * B
         n = r1 - r0
-        dG16 = dgates16[t0:t1].view(n, 4 * H)
+        dG16 = dxh.view(n, H) if lin else dgates16[t0:t1].view(n, 4 * H)
         with torch.cuda.stream(sL if wg_side else main):
-            if fused_dw:
-                dWhh.add_(dwp.sum(0))                # the chains' ∂W_hh partials (fixed order: chain index)
-                if not wg_side:
-                    dwp.record_stream(main)
+            if lin:
+                pass                                   # ∂W_f, ∂b_f: below (no recurrent weight)
             elif rst is not None:
                 # packed: the h_{t-1} operand is zero where an episode starts at t (the forward never used it)
                 hprev = torch.cat([h016.unsqueeze(0), hs16[:S - 1]], 0).masked_fill_(rst.bool().unsqueeze(2), 0.0)
@@ -549,7 +557,10 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
                 gemm_tn(dG16, hs16[t0 - 1:t1 - 1].view(n, H), out=dWhh, perm=gperm, accumulate=True)
             else:       # h_{t-1} rows: h0 for t = 0, then hs[0 : t1-1] — no concatenation materialised
                 gemm_tn(dG16, hs16[0:t1 - 1].view(n - B, H), out=dWhh, perm=gperm, accumulate=True, b0=h016)
-            gemm_tn(dG16, x16[r0:r1], out=dWih, perm=gperm, accumulate=True)
+            if lin:
+                gemm_tn(dG16, x16[r0:r1], out=dWih, colsum=dbf)
+            else:
+                gemm_tn(dG16, x16[r0:r1], out=dWih, perm=gperm, accumulate=True)
         fused_dx = dx_w is not None
         if fused_dx:
             # ∂pre = (∂G·W_ih)⊙[x16 > 0] and ∂x896 = ∂pre·W_pre in one launch (the ∂pre tile stays in LDS)
@@ -581,8 +592,9 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             # DP split point: every gradient of the recurrence, pre-RNN and heads is final here (the big ones are
             # already in the flat buffer); apply the small ones and let the learner all-reduce those buckets while
             # the encoder backward below runs (see Learner._replay_split)
-            grads['rnn.bias_ih_l0'] = db             # (gate-major already: the kernel writes PyTorch's order)
-            grads['rnn.bias_hh_l0'] = db
+            if not lin:
+                grads['rnn.bias_ih_l0'] = db         # (gate-major already: the kernel writes PyTorch's order)
+                grads['rnn.bias_hh_l0'] = db
             early = [grads.pop(nm, None) if nm in early_names else None for nm in fp.param_names]
             fp.apply_direct_grads(early, None, set_mask=False)    # the final call records the full mask
             fp.early_applied = early_names
@@ -694,11 +706,12 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     if wg_done is not None:
         main.wait_event(wg_done)
     if not direct:
-        grads['rnn.weight_hh_l0'] = dWhh
-        grads['rnn.weight_ih_l0'] = dWih
+        if not lin:
+            grads['rnn.weight_hh_l0'] = dWhh
+            grads['rnn.weight_ih_l0'] = dWih
         grads['affine_pre_rnn.weight'] = dWpre
         grads['affine_pre_rnn.bias'] = dbpre
-    if 'rnn.bias_ih_l0' not in fp.early_applied:
+    if not lin and 'rnn.bias_ih_l0' not in fp.early_applied:
         grads['rnn.bias_ih_l0'] = db
         grads['rnn.bias_hh_l0'] = db
     grads['affine_unit_basic_stats.weight'] = dw1
@@ -762,6 +775,11 @@ def train_direct(fp, batch_tm: Dict[str, torch.Tensor], B: int, S: int) -> torch
     sL.wait_stream(main)
     with torch.cuda.stream(sL):
         C.loss_prep(batch_tm['actions'], fp.loss_prep_ws(dev), norms)
+        if lc.compat_value_bug and lc.vf_coef > 0:
+            # the reference's value target is the LAST sequence's returns broadcast over the batch (optimizer.py:603,
+            # SURVEY §2.10-2): Σ G_last and Σ G_last² of row b = B-1 for the heads kernel and the loss assembly
+            g_last = batch_tm['ret'].view(S, B)[:, B - 1]
+            norms[6:8] = torch.stack([g_last.sum(), (g_last * g_last).sum()])
     W = fp.weight_images().refresh(C)
     P = dict(zip(fp.param_names, fp.params))
     H = fp.cfg.hidden
@@ -770,13 +788,14 @@ def train_direct(fp, batch_tm: Dict[str, torch.Tensor], B: int, S: int) -> torch
     if h0 is None:
         h0 = torch.zeros(B, H, device=dev)
         c0 = torch.zeros(B, H, device=dev)
-    gout = {nm: P[nm].grad for nm in DIRECT_GEMM_GRADS}
+    gout = {nm: P[nm].grad for nm in DIRECT_GEMM_GRADS if nm in P}
     part, _, grads = fused_step_tm(fp, W, P, batch_tm['units'], batch_tm['env'], batch_tm['actions'],
                                    batch_tm['masks'], batch_tm['adv'], batch_tm['ret'], batch_tm['logp_old'],
                                    batch_tm['norm_ret'], norms, h0, c0, B, S, gout=gout,
                                    reset_t=batch_tm.get('reset'))
     fp.apply_direct_grads([grads.get(nm) for nm in fp.param_names], None,
-                          written=set(DIRECT_GEMM_GRADS) | set(fp.early_applied))
+                          written=set(gout) | set(fp.early_applied))
     out = torch.empty(16, device=dev)
-    C.loss_assemble(part, norms, N, 0 if lc.algo == 'ppo' else 1, float(lc.entropy_coef), float(lc.vf_coef), out)
+    C.loss_assemble(part, norms, N, 0 if lc.algo == 'ppo' else 1, float(lc.entropy_coef), float(lc.vf_coef), out,
+                    S=S, compat_value_bug=bool(lc.compat_value_bug))
     return out

@@ -220,7 +220,7 @@ class PyVecEnv {
                         int hidden_stride, int hidden_size, const std::vector<int>& counts, int threads,
                         double latest_weights_prob, bool validation, bool fog, double start_time,
                         const std::string& tag, bool stagger, bool wire) {
-    if (n_games < 1 || mode < 0 || mode > 2 || counts.size() != 6 || rollout_size < 1 || hidden_size < 0)
+    if (n_games < 1 || mode < 0 || mode > 3 || counts.size() != 6 || rollout_size < 1 || hidden_size < 0)
       throw std::invalid_argument("VecEnv: bad configuration");
     VecConfig c;
     c.n_games = n_games;

@@ -838,7 +838,7 @@ class Pool {
 // ============================================================================================================
 struct VecConfig {
   int n_games = 1;
-  int mode = 0;                  // 0 1v1 self-play, 1 5v5 self-play, 2 1v1 controlled vs the default bot
+  int mode = 0;                  // 0 1v1 self-play, 1 5v5 self-play, 2 1v1 controlled vs the default bot, 3 5v5 vs it
   uint64_t seed = 0;
   double start_time = -10.0, max_dota_time = 600.0, dt = 0.5;
   bool fog = true;
@@ -905,7 +905,7 @@ class VecEnv {
     U_ = 0;
     for (int i = 0; i < 6; ++i) U_ += cfg_.counts[i];
     A_ = 21 + U_;
-    per_game_ = cfg_.mode == 1 ? 10 : (cfg_.mode == 2 ? 1 : 2);
+    per_game_ = cfg_.mode == 1 ? 10 : (cfg_.mode == 2 ? 1 : (cfg_.mode == 3 ? 5 : 2));
     games_.resize(cfg_.n_games);
     rng_.seed(cfg_.seed ^ 0x9e3779b97f4a7c15ULL);
   }
@@ -993,10 +993,11 @@ class VecEnv {
     if (cfg_.mode == 1) {
       team(TEAM_R, CTRL_CONTROLLED, 5);
       team(TEAM_D, CTRL_CONTROLLED, 5);
-    } else if (cfg_.mode == 2) {   // controlled vs the default bot, sides alternate with the game serial
-      const bool r_ctrl = (s & 1) == 0;
-      team(TEAM_R, r_ctrl ? CTRL_CONTROLLED : CTRL_DEFAULT, 1);
-      team(TEAM_D, r_ctrl ? CTRL_DEFAULT : CTRL_CONTROLLED, 1);
+    } else if (cfg_.mode == 2 || cfg_.mode == 3) {   // controlled vs the default bot (1v1 / 5v5), sides alternate
+      const bool r_ctrl = (s & 1) == 0;             // with the game serial
+      const int nh = cfg_.mode == 3 ? 5 : 1;
+      team(TEAM_R, r_ctrl ? CTRL_CONTROLLED : CTRL_DEFAULT, nh);
+      team(TEAM_D, r_ctrl ? CTRL_DEFAULT : CTRL_CONTROLLED, nh);
     } else {
       team(TEAM_R, CTRL_CONTROLLED, 1);
       team(TEAM_D, CTRL_CONTROLLED, 1);

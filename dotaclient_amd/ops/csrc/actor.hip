@@ -42,9 +42,21 @@ __device__ __forceinline__ int wave_argmax(float v, int lane) {
   return idx;
 }
 
-template <typename HT>   // unit handles: int64 (the reference's layout) or int32 (the fp8 step's compact staging)
+__device__ __forceinline__ void load8(const short* p, float* v) {
+  const dca::bf16x8 b = *reinterpret_cast<const dca::bf16x8*>(p);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = dca::bf2f(b[j]);
+}
+__device__ __forceinline__ void load8(const float* p, float* v) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// HT: unit handles int64 (the reference's layout) or int32 (the fp8 step's compact staging); ET: the unit embeddings
+// bf16 (short) or fp32 (the IEEE-fp32 actor step and the 5v5 attention block's output)
+template <typename HT, typename ET>
 __global__ __launch_bounds__(256) void sample_kernel(const float* __restrict__ z, int ldz,
-                                                     const short* __restrict__ emb,
+                                                     const ET* __restrict__ emb,
                                                      const HT* __restrict__ handles, int N, int U,
                                                      unsigned long long seed, const long long* __restrict__ ctr,
                                                      int* __restrict__ idx_out, unsigned char* __restrict__ act_out,
@@ -65,9 +77,10 @@ __global__ __launch_bounds__(256) void sample_kernel(const float* __restrict__ z
     const int u = it * 4 + ug;
     float d = 0.f;
     if (u < U) {
-      const dca::bf16x8 v = *reinterpret_cast<const dca::bf16x8*>(emb + ((size_t)n * U + u) * kQ + 8 * ks);
+      float v[8];
+      load8(emb + ((size_t)n * U + u) * kQ + 8 * ks, v);
 #pragma unroll
-      for (int j = 0; j < 8; ++j) d += q8[j] * dca::bf2f(v[j]);
+      for (int j = 0; j < 8; ++j) d += q8[j] * v[j];
     }
     d = dca::group_sum<16>(d);
     // lane (16·g) holds unit it*4+g; move it to lane u
@@ -189,17 +202,21 @@ extern "C" hipError_t dca_actor_state_prep(const short* pre, float* h, float* c,
   return hipGetLastError();
 }
 
-extern "C" hipError_t dca_sample_actions(const float* z, int ldz, const short* emb, const void* handles, int h32,
-                                         int N, int U, unsigned long long seed, const long long* ctr, int* idx,
-                                         unsigned char* act, unsigned char* msk, float* logp, float* value,
+extern "C" hipError_t dca_sample_actions(const float* z, int ldz, const void* emb, int emb_f32, const void* handles,
+                                         int h32, int N, int U, unsigned long long seed, const long long* ctr,
+                                         int* idx, unsigned char* act, unsigned char* msk, float* logp, float* value,
                                          hipStream_t st) {
   if (U < 1 || U > 64 || ldz < kQ + 22) return hipErrorInvalidValue;
-  if (h32)
-    sample_kernel<int><<<(N + 3) / 4, 256, 0, st>>>(z, ldz, emb, static_cast<const int*>(handles), N, U, seed, ctr,
-                                                    idx, act, msk, logp, value);
-  else
-    sample_kernel<long long><<<(N + 3) / 4, 256, 0, st>>>(z, ldz, emb, static_cast<const long long*>(handles), N, U,
-                                                          seed, ctr, idx, act, msk, logp, value);
+  const dim3 grid((N + 3) / 4), block(256);
+#define DCA_SAMPLE(HT, ET)                                                                                   \
+  hipLaunchKernelGGL((sample_kernel<HT, ET>), grid, block, 0, st, z, ldz, static_cast<const ET*>(emb),    \
+                     static_cast<const HT*>(handles), N, U, seed, ctr, idx, act, msk, logp, value)
+  if (h32) {
+    if (emb_f32) DCA_SAMPLE(int, float); else DCA_SAMPLE(int, short);
+  } else {
+    if (emb_f32) DCA_SAMPLE(long long, float); else DCA_SAMPLE(long long, short);
+  }
+#undef DCA_SAMPLE
   return hipGetLastError();
 }
 

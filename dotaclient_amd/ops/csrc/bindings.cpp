@@ -86,13 +86,7 @@ void multi_axpy(std::vector<torch::Tensor> dst, std::vector<torch::Tensor> src, 
 
 // ------------------------------------------------------------------------------------------------------------
 // Optional in-kernel timestamp buffers: checked contiguous int64 GPU tensors of at least `need` values (the kernels
-// write without bounds checks). Plain LSTM: its workgroups (chains × H/8, lstm.hip plan_chains) × 8 waves × 64 steps
-// × 8 events; team LSTM: 32 members × 4 waves × 64 steps × 8 events.
-inline int64_t lstm_trace_elems(int B, int H) {
-  const int nwg = H / 8, max_ch = 256 / nwg;
-  const int nch = std::min((B + 31) / 32, max_ch);
-  return (int64_t)nch * nwg * 8 * 64 * 8;
-}
+// write without bounds checks). Team LSTM: 32 members × 4 waves × 64 steps × 8 events.
 constexpr int64_t kTeamTraceElems = 32LL * 4 * 64 * 8;
 inline unsigned long long* trace_ptr(const c10::optional<torch::Tensor>& t, int64_t need, const char* name) {
   if (!t.has_value() || !t->defined()) return nullptr;
@@ -102,58 +96,6 @@ inline unsigned long long* trace_ptr(const c10::optional<torch::Tensor>& t, int6
   return ptr<unsigned long long>(*t);
 }
 
-// Persistent LSTM recurrence. xp (B,S,4H) f32, whh (4H,H) bf16, h0/c0 (B,H) f32, err (1) int32 device flag.
-std::vector<torch::Tensor> lstm_fwd(torch::Tensor xp, torch::Tensor whh, torch::Tensor h0, torch::Tensor c0,
-                                    torch::Tensor err, bool want_f32_h, c10::optional<torch::Tensor> trace) {
-  CHECK_F32(xp); CHECK_BF16(whh); CHECK_F32(h0); CHECK_F32(c0); CHECK_I32(err);
-  TORCH_CHECK(xp.dim() == 3, "xp must be (B,S,4H)");
-  const int B = xp.size(0), S = xp.size(1), G4 = xp.size(2), H = G4 / 4;
-  TORCH_CHECK(whh.size(0) == G4 && whh.size(1) == H, "whh must be (4H,H)");
-  TORCH_CHECK(h0.size(0) == B && h0.size(1) == H && c0.size(0) == B && c0.size(1) == H, "h0/c0 must be (B,H)");
-  TORCH_CHECK(H == 128 || H == 256 || H == 512, "lstm_fwd: H in {128,256,512}");
-  TORCH_CHECK(B >= 1 && B <= dca_lstm_max_batch(H), "lstm_fwd: batch exceeds the per-launch maximum");
-  auto f32 = xp.options();
-  auto hs = torch::empty({B, S, H}, f32.dtype(at::kBFloat16));
-  torch::Tensor hsf = want_f32_h ? torch::empty({B, S, H}, f32) : torch::Tensor();
-  auto cs = torch::empty({B, S, H}, f32);
-  auto gates = torch::empty({B, S, G4}, f32);
-  auto hn = torch::empty({B, H}, f32);
-  auto cn = torch::empty({B, H}, f32);
-  auto ring = torch::empty({(int64_t)dca_lstm_ring_elems(B, H, 0)}, f32.dtype(at::kLong));
-  hip_check(dca_lstm_fwd(ptr<float>(xp), ptr<short>(whh), ptr<float>(h0), ptr<float>(c0), ptr<short>(hs),
-                         want_f32_h ? ptr<float>(hsf) : nullptr, ptr<float>(cs), ptr<float>(gates), ptr<float>(hn),
-                         ptr<float>(cn), ptr<unsigned long long>(ring), ptr<unsigned>(err), B, S, H, cur_stream(),
-                         trace_ptr(trace, lstm_trace_elems(B, H), "lstm_fwd")),
-            "dca_lstm_fwd");
-  return {hs, want_f32_h ? hsf : hs, cs, gates, hn, cn};
-}
-
-std::vector<torch::Tensor> lstm_bwd(torch::Tensor dhs, torch::Tensor gates, torch::Tensor cs, torch::Tensor c0,
-                                    c10::optional<torch::Tensor> dhn, c10::optional<torch::Tensor> dcn,
-                                    torch::Tensor whh, torch::Tensor err, c10::optional<torch::Tensor> trace) {
-  CHECK_F32(dhs); CHECK_F32(gates); CHECK_F32(cs); CHECK_F32(c0); CHECK_BF16(whh); CHECK_I32(err);
-  const int B = dhs.size(0), S = dhs.size(1), H = dhs.size(2);
-  TORCH_CHECK(gates.size(0) == B && gates.size(1) == S && gates.size(2) == 4 * H, "gates must be (B,S,4H)");
-  TORCH_CHECK(cs.sizes() == dhs.sizes(), "cs must be (B,S,H)");
-  TORCH_CHECK(whh.size(0) == 4 * H && whh.size(1) == H, "whh must be (4H,H)");
-  TORCH_CHECK(H == 128 || H == 256 || H == 512, "lstm_bwd: H in {128,256,512}");
-  TORCH_CHECK(B >= 1 && B <= dca_lstm_max_batch(H), "lstm_bwd: batch exceeds the per-launch maximum");
-  const float* dhn_p = nullptr;
-  const float* dcn_p = nullptr;
-  if (dhn.has_value() && dhn->defined()) { CHECK_F32((*dhn)); dhn_p = ptr<float>(*dhn); }
-  if (dcn.has_value() && dcn->defined()) { CHECK_F32((*dcn)); dcn_p = ptr<float>(*dcn); }
-  auto f32 = dhs.options();
-  auto dgates = torch::empty({B, S, 4 * H}, f32);
-  auto dh0 = torch::empty({B, H}, f32);
-  auto dc0 = torch::empty({B, H}, f32);
-  auto ring = torch::empty({(int64_t)dca_lstm_ring_elems(B, H, 1)}, f32.dtype(at::kLong));
-  hip_check(dca_lstm_bwd(ptr<float>(dhs), ptr<float>(gates), ptr<float>(cs), ptr<float>(c0), dhn_p, dcn_p,
-                         ptr<short>(whh), ptr<float>(dgates), ptr<float>(dh0), ptr<float>(dc0),
-                         ptr<unsigned long long>(ring), ptr<unsigned>(err), B, S, H, cur_stream(),
-                         trace_ptr(trace, lstm_trace_elems(B, H), "lstm_bwd")),
-            "dca_lstm_bwd");
-  return {dgates, dh0, dc0};
-}
 
 // ------------------------------------------------------------------------------------------------------------
 // XCD-team LSTM recurrence (lstm_team.hip). Gates in unit-major (·,·,H,4) layout; see the kernel header.
@@ -237,9 +179,7 @@ std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4
                                          c10::optional<torch::Tensor> dcn, torch::Tensor whh, torch::Tensor err,
                                          torch::Tensor ctl, c10::optional<torch::Tensor> trace, bool time_major,
                                          c10::optional<torch::Tensor> dg_out, bool dg_bf16, bool want_dbias,
-                                         bool precise, c10::optional<torch::Tensor> reset,
-                                         c10::optional<torch::Tensor> hs_f32, c10::optional<torch::Tensor> h0,
-                                         c10::optional<torch::Tensor> dw_out) {
+                                         bool precise, c10::optional<torch::Tensor> reset) {
   CHECK_F32(dhs); CHECK_F32(gates4); CHECK_F32(cs); CHECK_F32(c0); CHECK_DEV(whh); CHECK_CONTIG(whh); CHECK_I32(err);
   check_ctl(ctl);
   const bool f32w = whh.scalar_type() == at::kFloat;
@@ -267,31 +207,13 @@ std::vector<torch::Tensor> lstm_team_bwd(torch::Tensor dhs, torch::Tensor gates4
   torch::Tensor dbp = want_dbias ? torch::empty({dca_lstm_team_chains(B, f32w ? 1 : 0), 4 * H}, f32) : torch::Tensor();
   const size_t wsb = dca_lstm_team_workspace(B, H, 1, f32w ? 1 : 0);
   auto ws = torch::empty({(int64_t)wsb}, f32.dtype(at::kByte));
-  // fused ∂W_hh (V2 variant): per-chain partials (chains, 4H, H) in PyTorch row order, summed by the caller
-  const float* hsf_p = nullptr;
-  const float* h0_p = nullptr;
-  float* dw_p = nullptr;
-  if (dw_out.has_value() && dw_out->defined()) {
-    TORCH_CHECK(hs_f32.has_value() && hs_f32->defined() && h0.has_value() && h0->defined(),
-                "lstm_team_bwd: dw_out needs hs_f32 and h0");
-    CHECK_F32((*dw_out)); CHECK_F32((*hs_f32)); CHECK_F32((*h0));
-    TORCH_CHECK(hs_f32->sizes() == dhs.sizes(), "lstm_team_bwd: hs_f32 must match dhs");
-    TORCH_CHECK(h0->size(0) == B && h0->size(1) == H, "lstm_team_bwd: h0 must be (B,H)");
-    TORCH_CHECK(dw_out->numel() == (int64_t)dca_lstm_team_chains(B, f32w ? 1 : 0) * 4 * H * H,
-                "lstm_team_bwd: dw_out must hold (chains, 4H, H)");
-    TORCH_CHECK(dca_lstm_team_bwd_fuses_dw(B, H, f32w ? 1 : 0, precise ? 1 : 0),
-                "lstm_team_bwd: this shape / precision does not take the fused-dW variant");
-    hsf_p = ptr<float>(*hs_f32);
-    h0_p = ptr<float>(*h0);
-    dw_p = ptr<float>(*dw_out);
-  }
   hip_check(dca_lstm_team_bwd(ptr<float>(dhs), ptr<float>(gates4), ptr<float>(cs), ptr<float>(c0), dhn_p, dcn_p,
                               whh.data_ptr(), dg_bf16 ? nullptr : ptr<float>(dgates4), ptr<float>(dh0),
                               ptr<float>(dc0), ctl.data_ptr(), ws.data_ptr(), wsb, ptr<unsigned>(err), B, S, H,
                               time_major ? 1 : 0, cur_stream(),
                               trace_ptr(trace, kTeamTraceElems, "lstm_team_bwd"),
                               dg_bf16 ? ptr<short>(dgates4) : nullptr, want_dbias ? ptr<float>(dbp) : nullptr,
-                              f32w ? 1 : 0, precise ? 1 : 0, reset_ptr(reset, B, S), hsf_p, h0_p, dw_p),
+                              f32w ? 1 : 0, precise ? 1 : 0, reset_ptr(reset, B, S)),
             "dca_lstm_team_bwd");
   if (want_dbias) return {dgates4, dh0, dc0, dbp.sum(0)};
   return {dgates4, dh0, dc0};
@@ -412,7 +334,9 @@ std::vector<torch::Tensor> encoder_bwd(torch::Tensor units, torch::Tensor w1, to
 // logp (N) f32, value (N) f32 (all preallocated so the op is hipGraph-capturable).
 void sample_actions(torch::Tensor z, torch::Tensor emb, torch::Tensor handles, int64_t seed, torch::Tensor ctr,
                     torch::Tensor idx, torch::Tensor act, torch::Tensor msk, torch::Tensor logp, torch::Tensor value) {
-  CHECK_F32(z); CHECK_BF16(emb); CHECK_DEV(handles); CHECK_CONTIG(handles);
+  CHECK_F32(z); CHECK_DEV(emb); CHECK_CONTIG(emb); CHECK_DEV(handles); CHECK_CONTIG(handles);
+  const bool e32 = emb.scalar_type() == at::kFloat;
+  TORCH_CHECK(e32 || emb.scalar_type() == at::kBFloat16, "sample_actions: emb bf16 or fp32");
   const bool h32 = handles.scalar_type() == at::kInt;
   TORCH_CHECK(h32 || handles.scalar_type() == at::kLong, "sample_actions: handles int64 or int32");
   CHECK_DEV(ctr); CHECK_DT(ctr, at::kLong); CHECK_I32(idx); CHECK_U8(act); CHECK_U8(msk); CHECK_F32(logp);
@@ -423,9 +347,10 @@ void sample_actions(torch::Tensor z, torch::Tensor emb, torch::Tensor handles, i
   TORCH_CHECK(idx.size(0) == N && idx.size(1) == 4 && logp.numel() == N && value.numel() == N, "output shapes");
   TORCH_CHECK(act.size(0) == N && act.size(1) == 21 + U && msk.sizes() == act.sizes(), "act/msk (N,21+U)");
   TORCH_CHECK(U <= 64 && ldz >= 150, "U <= 64, ldz >= 150");
-  hip_check(dca_sample_actions(ptr<float>(z), ldz, ptr<short>(emb), handles.data_ptr(), h32 ? 1 : 0, N, U,
-                               (unsigned long long)seed, ptr<long long>(ctr), ptr<int>(idx), ptr<unsigned char>(act),
-                               ptr<unsigned char>(msk), ptr<float>(logp), ptr<float>(value), cur_stream()),
+  hip_check(dca_sample_actions(ptr<float>(z), ldz, emb.data_ptr(), e32 ? 1 : 0, handles.data_ptr(), h32 ? 1 : 0, N,
+                               U, (unsigned long long)seed, ptr<long long>(ctr), ptr<int>(idx),
+                               ptr<unsigned char>(act), ptr<unsigned char>(msk), ptr<float>(logp), ptr<float>(value),
+                               cur_stream()),
             "dca_sample_actions");
 }
 
@@ -492,6 +417,45 @@ void actor_fp8(torch::Tensor x896, torch::Tensor wpre, torch::Tensor spre, torch
                           ptr<float>(sg), ptr<float>(bg), wh.data_ptr(), ptr<float>(sh), ptr<float>(bh), ptr<float>(h),
                           ptr<float>(c), ptr<float>(keep), act, ptr<float>(z), n, bump_ptr(bump), cur_stream()),
             "dca_actor_fp8");
+}
+
+// fp32 / bf16 actor policy core (actor_core.hip): x896 (n,896) f32 or bf16 → pre-RNN → LSTM step (h, c in place) or
+// the linear fake_rnn layer → z (n,160). Weights in fragment order (actor/batched.py frag_weight): fp32 (mode 0, IEEE
+// fp32 on the f32 MFMA) or bf16 (mode 1); wg = [W_ih | W_hh] rows in unit-major gate order (LSTM) or W_f (linear).
+void actor_core(torch::Tensor x896, torch::Tensor wpre, torch::Tensor bpre, torch::Tensor wg, torch::Tensor bg,
+                torch::Tensor wh, torch::Tensor bh, torch::Tensor h, torch::Tensor c, torch::Tensor keep,
+                torch::Tensor z, int64_t mode, bool linear, c10::optional<torch::Tensor> active,
+                c10::optional<torch::Tensor> bump) {
+  CHECK_DEV(x896); CHECK_CONTIG(x896); CHECK_DEV(wpre); CHECK_CONTIG(wpre); CHECK_DEV(wg); CHECK_CONTIG(wg);
+  CHECK_DEV(wh); CHECK_CONTIG(wh); CHECK_F32(bpre); CHECK_F32(bg); CHECK_F32(bh); CHECK_F32(h); CHECK_F32(c);
+  CHECK_F32(keep); CHECK_F32(z);
+  TORCH_CHECK(mode == 0 || mode == 1, "actor_core: mode 0 (fp32) or 1 (bf16)");
+  const auto wdt = mode == 0 ? at::kFloat : at::kBFloat16;
+  TORCH_CHECK(wpre.scalar_type() == wdt && wg.scalar_type() == wdt && wh.scalar_type() == wdt,
+              "actor_core: weights must be fp32 (mode 0) or bf16 (mode 1)");
+  const bool x32 = x896.scalar_type() == at::kFloat;
+  TORCH_CHECK(x32 || (x896.scalar_type() == at::kBFloat16 && mode == 1), "actor_core: x896 fp32 (or bf16, mode 1)");
+  const int n = x896.size(0), H = h.size(1);
+  TORCH_CHECK(x896.dim() == 2 && x896.size(1) == 896, "actor_core: x896 (n, 896)");
+  TORCH_CHECK(linear ? H == 256 : (H == 512 || H == 128), "actor_core: hidden 512 / 128 (LSTM) or 256 (linear)");
+  const int64_t gn = linear ? H : 4 * H, gk = linear ? 256 : 256 + H;
+  TORCH_CHECK(wpre.numel() == 256 * 896 && bpre.numel() == 256, "actor_core: pre-RNN 256x896");
+  TORCH_CHECK(wg.numel() == gn * gk && bg.numel() == gn, "actor_core: recurrent weights");
+  TORCH_CHECK(wh.numel() == 160 * H && bh.numel() == 160, "actor_core: heads 160 x hidden");
+  TORCH_CHECK(h.dim() == 2 && h.size(0) == n && c.sizes() == h.sizes() && keep.numel() == n,
+              "actor_core: h, c (n, hidden), keep (n)");
+  TORCH_CHECK(z.dim() == 2 && z.size(0) == n && z.size(1) == 160, "actor_core: z (n, 160)");
+  const float* act = nullptr;
+  if (active && active->defined()) {
+    CHECK_F32(*active);
+    TORCH_CHECK(active->numel() == n, "actor_core: active (n)");
+    act = ptr<float>(*active);
+  }
+  hip_check(dca_actor_core(x896.data_ptr(), x32 ? 1 : 0, wpre.data_ptr(), ptr<float>(bpre), wg.data_ptr(),
+                           ptr<float>(bg), wh.data_ptr(), ptr<float>(bh), ptr<float>(h), ptr<float>(c),
+                           ptr<float>(keep), act, ptr<float>(z), n, H, linear ? 1 : 0, (int)mode, bump_ptr(bump),
+                           cur_stream()),
+            "dca_actor_core");
 }
 
 // fp8 entity encoder of the actor step (actor_fp8.hip): units (N, U, 10) fp16 or fp32, env (N, 3) → x896 (N, 896) bf16
@@ -723,12 +687,13 @@ int64_t loss_prep_ws_elems() { return 5 * dca_loss_prep_blocks() + 1; }
 
 // Loss scalar + metrics (out (16) f32) from the heads/loss partials part (R,16).
 void loss_assemble(torch::Tensor part, torch::Tensor norms, int64_t N, int64_t algo, double ent_coef, double vf_coef,
-                   torch::Tensor out) {
+                   torch::Tensor out, int64_t S, bool compat_value_bug) {
   CHECK_F32(part); CHECK_F32(norms); CHECK_F32(out);
   TORCH_CHECK(part.dim() == 2 && part.size(1) == 16 && out.numel() >= 16 && norms.numel() >= 8,
               "loss_assemble shapes");
   hip_check(dca_loss_assemble(ptr<float>(part), (int)part.size(0), ptr<float>(norms), (int)N, (int)algo,
-                              (float)ent_coef, (float)vf_coef, ptr<float>(out), cur_stream()),
+                              (float)ent_coef, (float)vf_coef, ptr<float>(out), (int)S, compat_value_bug ? 1 : 0,
+                              cur_stream()),
             "dca_loss_assemble");
 }
 
@@ -1179,10 +1144,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("multi_axpy", &multi_axpy, "dst_i += scale * src_i for a list of fp32 tensors (one graph-safe launch)",
         py::arg("dst"), py::arg("src"), py::arg("scale") = py::none());
   m.def("lstm_team_ctl_bytes", &dca_lstm_team_ctl_bytes, "bytes of a persistent team-LSTM control block");
-  m.def("lstm_max_batch", &dca_lstm_max_batch, "max sequences per persistent LSTM launch for hidden size H");
-  m.def("lstm_fwd", &lstm_fwd, "persistent LSTM forward recurrence (granule all-gather)", py::arg("xp"),
-        py::arg("whh"), py::arg("h0"), py::arg("c0"), py::arg("err"), py::arg("want_f32_h"),
-        py::arg("trace") = py::none());
   m.def("heads_loss", &heads_loss, "fused heads + pointer + masked log-softmax + PPO/VPG loss + gradients",
         py::arg("z"), py::arg("emb"), py::arg("act"), py::arg("msk"), py::arg("adv"), py::arg("ret"),
         py::arg("logp_old"), py::arg("nret"), py::arg("norms"), py::arg("algo"), py::arg("compat_value_bug"),
@@ -1195,9 +1156,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("units"), py::arg("w1"), py::arg("b1"), py::arg("wtT"), py::arg("dtl"), py::arg("q"), py::arg("dx"),
         py::arg("arg"), py::arg("counts"), py::arg("compat"), py::arg("demb_in") = py::none(),
         py::arg("exact") = false);
-  m.def("lstm_bwd", &lstm_bwd, "persistent LSTM backward recurrence (granule reduce-scatter)", py::arg("dhs"),
-        py::arg("gates"), py::arg("cs"), py::arg("c0"), py::arg("dhn"), py::arg("dcn"), py::arg("whh"), py::arg("err"),
-        py::arg("trace") = py::none());
   m.def("lstm_team_fwd", &lstm_team_fwd, "XCD-team persistent LSTM forward (L2-local hand-off), unit-major gates",
         py::arg("xp4"), py::arg("whh"), py::arg("h0"), py::arg("c0"), py::arg("err"), py::arg("ctl"),
         py::arg("want_f32_h"), py::arg("trace") = py::none(), py::arg("time_major") = false, py::arg("hs_out") = py::none(),
@@ -1207,12 +1165,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dhs"), py::arg("gates4"), py::arg("cs"), py::arg("c0"), py::arg("dhn"), py::arg("dcn"),
         py::arg("whh"), py::arg("err"), py::arg("ctl"), py::arg("trace") = py::none(),
         py::arg("time_major") = false, py::arg("dg_out") = py::none(), py::arg("dg_bf16") = false,
-        py::arg("want_dbias") = false, py::arg("precise") = false, py::arg("reset") = py::none(),
-        py::arg("hs_f32") = py::none(), py::arg("h0") = py::none(), py::arg("dw_out") = py::none());
-  m.def("lstm_team_bwd_fuses_dw", [](int64_t B, int64_t H, bool f32, bool precise) {
-          return dca_lstm_team_bwd_fuses_dw((int)B, (int)H, f32 ? 1 : 0, precise ? 1 : 0) != 0;
-        }, "whether lstm_team_bwd of (B, H) runs the variant that accumulates dW_hh itself (dw_out)",
-        py::arg("B"), py::arg("H"), py::arg("f32"), py::arg("precise") = false);
+        py::arg("want_dbias") = false, py::arg("precise") = false, py::arg("reset") = py::none());
   m.def("lstm_team_chains", [](int64_t B, bool f32) { return dca_lstm_team_chains((int)B, f32 ? 1 : 0); },
         "sequence chains of a team-recurrence launch of B sequences", py::arg("B"), py::arg("f32"));
   m.def("sample_actions", &sample_actions, "fused masked hierarchical Gumbel-max action sampling (actor)");
@@ -1224,6 +1177,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "(per_unit: the one-unit-at-a-time workgroup form instead of the wave-parallel one)", py::arg("units"),
         py::arg("env"), py::arg("w1"), py::arg("b1"), py::arg("wt"), py::arg("st"), py::arg("bt"), py::arg("we"),
         py::arg("be"), py::arg("counts"), py::arg("per_unit") = false);
+  m.def("actor_core", &actor_core, "fp32 / bf16 actor policy core: pre-RNN + LSTM step (or linear layer) + heads",
+        py::arg("x896"), py::arg("wpre"), py::arg("bpre"), py::arg("wg"), py::arg("bg"), py::arg("wh"), py::arg("bh"),
+        py::arg("h"), py::arg("c"), py::arg("keep"), py::arg("z"), py::arg("mode"), py::arg("linear") = false,
+        py::arg("active") = py::none(), py::arg("bump") = py::none());
   m.def("actor_fp8", &actor_fp8, "fp8 (e4m3) actor policy core: pre-RNN + LSTM step + heads from x896",
         py::arg("x896"), py::arg("wpre"), py::arg("spre"), py::arg("bpre"), py::arg("wg"), py::arg("sg"), py::arg("bg"),
         py::arg("wh"), py::arg("sh"), py::arg("bh"), py::arg("h"), py::arg("c"), py::arg("keep"), py::arg("z"),
@@ -1236,7 +1193,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "[dgamma | dbeta | dbt])");
   m.def("loss_prep", &loss_prep, "loss normalisers from one-hot action rows (graph-replayable)");
   m.def("loss_prep_ws_elems", &loss_prep_ws_elems, "int32 workspace elements of loss_prep");
-  m.def("loss_assemble", &loss_assemble, "loss scalar + metrics from heads/loss partials");
+  m.def("loss_assemble", &loss_assemble, "loss scalar + metrics from heads/loss partials", py::arg("part"),
+        py::arg("norms"), py::arg("N"), py::arg("algo"), py::arg("ent_coef"), py::arg("vf_coef"), py::arg("out"),
+        py::arg("S") = 0, py::arg("compat_value_bug") = false);
   m.def("weight_prep", &weight_prep, "gather the flat fp32 params into bf16 / fp32 working weight images (+ bf16 "
         "hi / lo split images)", py::arg("src"), py::arg("map16"), py::arg("dst16"), py::arg("map32"), py::arg("dst32"),
         py::arg("maps") = py::none(), py::arg("dsth") = py::none(), py::arg("dstl") = py::none());

@@ -105,7 +105,7 @@ constexpr int kAsmThreads = 1024;
 __global__ __launch_bounds__(kAsmThreads) void loss_assemble_kernel(const float* __restrict__ part, int nrows,
                                                                     const float* __restrict__ norms, int N, int algo,
                                                                     float ent_coef, float vf_coef,
-                                                                    float* __restrict__ out) {
+                                                                    float* __restrict__ out, int S, int vbug) {
   const int t = threadIdx.x, col = t & 15, rg = t >> 4;
   float s = 0.f;
   int r = rg;
@@ -146,6 +146,13 @@ __global__ __launch_bounds__(kAsmThreads) void loss_assemble_kernel(const float*
     entl = ent_coef > 0.f ? -ent_coef * ent : 0.f;
     val = vf_coef > 0.f ? vf_coef * p[1] * invN : 0.f;
     adv = p[8] * invN;
+    if (vbug && vf_coef > 0.f && S > 0) {
+      // the reference's value bug (optimizer.py:603): mean over (B, S, S) of (V[b,s] − G_last[s'])², from ΣV (p[9]),
+      // ΣV² (p[10]) and ΣG_last / ΣG_last² (norms[6], norms[7]) — ops/heads.py assemble_loss
+      const float Sf = (float)S, Bf = (float)(N / S);
+      val = vf_coef * (Sf * p[10] - 2.f * p[9] * norms[6] + (float)N * norms[7]) / (Bf * Sf * Sf);
+      adv = p[9] * invN - norms[6] / Sf;
+    }
   }
   out[0] = pol + val + entl;
   out[1] = pol;
@@ -379,9 +386,9 @@ extern "C" hipError_t dca_loss_prep(const unsigned char* act, int N, int A, int*
 }
 
 extern "C" hipError_t dca_loss_assemble(const float* part, int nrows, const float* norms, int N, int algo,
-                                        float ent_coef, float vf_coef, float* out, hipStream_t st) {
+                                        float ent_coef, float vf_coef, float* out, int S, int vbug, hipStream_t st) {
   hipLaunchKernelGGL(loss_assemble_kernel, dim3(1), dim3(kAsmThreads), 0, st, part, nrows, norms, N, algo, ent_coef, vf_coef,
-                     out);
+                     out, S, vbug);
   DCA_CHECK_LAUNCH();
   return hipSuccess;
 }

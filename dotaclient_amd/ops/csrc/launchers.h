@@ -47,16 +47,6 @@ int dca_adam_partials_len(int n_params);
 hipError_t dca_multi_axpy(float* const* dst, const float* const* src, const long long* numel, int n,
                           const float* scale, hipStream_t st);
 
-size_t dca_lstm_ring_elems(int B, int H, int backward);
-int dca_lstm_max_batch(int H);
-hipError_t dca_lstm_fwd(const float* xp, const short* whh, const float* h0, const float* c0, short* hs, float* hsf,
-                        float* cs, float* gates, float* hn, float* cn, unsigned long long* ring, unsigned* err, int B,
-                        int S, int H, hipStream_t st, unsigned long long* trace = nullptr);
-hipError_t dca_lstm_bwd(const float* dhs, const float* gates, const float* cs, const float* c0, const float* dhn,
-                        const float* dcn, const short* whh, float* dgates, float* dh0, float* dc0,
-                        unsigned long long* ring, unsigned* err, int B, int S, int H, hipStream_t st,
-                        unsigned long long* trace = nullptr);
-
 int dca_heads_loss_nblocks(int N);
 hipError_t dca_heads_loss(const float* z, int ldz, const void* emb, const unsigned char* act, const unsigned char* msk,
                           int A, const float* adv, const float* ret, const float* logp_old, const float* nret,
@@ -85,13 +75,15 @@ hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, const float*
                              const float* dhn, const float* dcn, const void* whh, float* dgates4, float* dh0,
                              float* dc0, void* ctl, void* ws, size_t ws_bytes, unsigned* err, int B, int S, int H,
                              int time_major, hipStream_t st, unsigned long long* trace, short* dg16, float* dbpart,
-                             int f32, int precise = 0, const unsigned char* rst = nullptr, const float* hsf = nullptr,
-                             const float* h0 = nullptr, float* dwpart = nullptr);
-int dca_lstm_team_bwd_fuses_dw(int B, int H, int f32, int precise);
+                             int f32, int precise = 0, const unsigned char* rst = nullptr);
 
-hipError_t dca_sample_actions(const float* z, int ldz, const short* emb, const void* handles, int h32, int N, int U,
-                              unsigned long long seed, const long long* ctr, int* idx, unsigned char* act,
-                              unsigned char* msk, float* logp, float* value, hipStream_t st);
+hipError_t dca_sample_actions(const float* z, int ldz, const void* emb, int emb_f32, const void* handles, int h32,
+                              int N, int U, unsigned long long seed, const long long* ctr, int* idx,
+                              unsigned char* act, unsigned char* msk, float* logp, float* value, hipStream_t st);
+hipError_t dca_actor_core(const void* x896, int x_f32, const void* wpre, const float* bpre, const void* wg,
+                          const float* bg, const void* wh, const float* bh, float* h, float* c, const float* keep,
+                          const float* active, float* z, int n, int hidden, int linear, int mode, long long* bump,
+                          hipStream_t st);
 hipError_t dca_actor_state_prep(const short* pre, float* h, float* c, const float* keep, short* xh, int N, int P,
                                 int H, long long* bump, hipStream_t st);
 hipError_t dca_lstm_cell(const float* gates, float* h, float* c, short* h16, const float* active, int N, int H,
@@ -106,7 +98,7 @@ int dca_loss_prep_blocks();
 hipError_t dca_loss_prep(const unsigned char* act, int N, int A, int* partial, unsigned* counter, float* norms,
                          hipStream_t st);
 hipError_t dca_loss_assemble(const float* part, int nrows, const float* norms, int N, int algo, float ent_coef,
-                             float vf_coef, float* out, hipStream_t st);
+                             float vf_coef, float* out, int S, int vbug, hipStream_t st);
 hipError_t dca_weight_prep(const float* src, const int* map16, short* dst16, int n16, const int* map32, float* dst32,
                            int n32, const int* maps, short* dsth, short* dstl, int ns, hipStream_t st);
 

@@ -65,7 +65,7 @@ using dca::bf16x8;
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
 
-constexpr int kT = 32;                  // workgroups per team (CUs per XCD)
+constexpr int kT = 32;                  // workgroups per team (CUs per XCD); VAR bit 4: half teams (16, see below)
 constexpr int kMaxTeams = 8;
 constexpr int kThreads = 256;
 constexpr int kSc1 = 16;                // buffer cache policy: sc1 (bypass the CU's L1, served by the XCD L2)
@@ -141,35 +141,6 @@ __device__ __forceinline__ void pk_dot4(const float* wq, const float* x, float& 
   const f32x2 a01 = a01e + a01o, a23 = a23e + a23o;
   o0 = a01.x; o1 = a01.y; o2 = a23.x; o3 = a23.y;
 }
-// pk_dot4 plus the ∂W_hh update of the same slice: dw[j] += x[j]·(h0, h1), dw[KSL + j] += x[j]·(h2, h3) (h = 0
-// leaves dw unchanged; unit pairs in register pairs for v_pk_fma_f32) — the slice values feed both as they arrive
-// from LDS, so the update needs no registers beyond its accumulators
-template <int KSL>
-__device__ __forceinline__ void pk_dot4_dw(const float* wq, const float* x, const float4 h, f32x2* dw, float& o0,
-                                           float& o1, float& o2, float& o3) {
-  f32x2 a01e = {0.f, 0.f}, a01o = {0.f, 0.f}, a23e = {0.f, 0.f}, a23o = {0.f, 0.f};
-  const f32x2 h01 = {h.x, h.y}, h23 = {h.z, h.w};
-#pragma unroll
-  for (int j = 0; j < KSL; j += 4) {
-    const float4 v = *reinterpret_cast<const float4*>(x + j);
-    a01e = __builtin_elementwise_fma(f32x2{wq[j], wq[KSL + j]}, f32x2{v.x, v.x}, a01e);
-    a23e = __builtin_elementwise_fma(f32x2{wq[2 * KSL + j], wq[3 * KSL + j]}, f32x2{v.x, v.x}, a23e);
-    a01o = __builtin_elementwise_fma(f32x2{wq[j + 1], wq[KSL + j + 1]}, f32x2{v.y, v.y}, a01o);
-    a23o = __builtin_elementwise_fma(f32x2{wq[2 * KSL + j + 1], wq[3 * KSL + j + 1]}, f32x2{v.y, v.y}, a23o);
-    a01e = __builtin_elementwise_fma(f32x2{wq[j + 2], wq[KSL + j + 2]}, f32x2{v.z, v.z}, a01e);
-    a23e = __builtin_elementwise_fma(f32x2{wq[2 * KSL + j + 2], wq[3 * KSL + j + 2]}, f32x2{v.z, v.z}, a23e);
-    a01o = __builtin_elementwise_fma(f32x2{wq[j + 3], wq[KSL + j + 3]}, f32x2{v.w, v.w}, a01o);
-    a23o = __builtin_elementwise_fma(f32x2{wq[2 * KSL + j + 3], wq[3 * KSL + j + 3]}, f32x2{v.w, v.w}, a23o);
-    const float xv[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      dw[j + q] = __builtin_elementwise_fma(f32x2{xv[q], xv[q]}, h01, dw[j + q]);
-      dw[KSL + j + q] = __builtin_elementwise_fma(f32x2{xv[q], xv[q]}, h23, dw[KSL + j + q]);
-    }
-  }
-  const f32x2 a01 = a01e + a01o, a23 = a23e + a23o;
-  o0 = a01.x; o1 = a01.y; o2 = a23.x; o3 = a23.y;
-}
 // Σ over the 16 lanes of this lane's DPP row, result in every lane: xor 1, xor 2 (quad_perm), half-row and row mirrors
 __device__ __forceinline__ float row_sum16(float v) {
   v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
@@ -201,13 +172,20 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, in
                                            __builtin_amdgcn_readfirstlane(bytes), 0x00020000);
 }
 
-// Bounded spin bookkeeping; true when this wave must give up (timeout or another workgroup raised an error).
-__device__ __forceinline__ bool spin_fail(unsigned& spins, TeamCtl* ctl, unsigned* err, unsigned code, int knobs) {
+// Bounded spin bookkeeping; true when this wave must give up (timeout or another workgroup raised an error). The
+// limit is WALL-CLOCK per wait (s_memrealtime, 100 MHz): ≈2 s without one hand-off arriving (DCA_TEAM_PATIENT: ≈60 s,
+// for runs that share the GPU with another process's kernels). It used to count polls over the whole launch, so a
+// recurrence slowed by co-resident kernels (the node loop's actor graph replays) could trip it with no hand-off ever
+// lost — the cumulative count grows with every step's extra polls (the config-5 loop's one backward timeout, code 2).
+// `spins` restarts at every step (the back-off sleep after 32 polls: within ±0.01 µs of never sleeping).
+__device__ __forceinline__ bool spin_fail(unsigned& spins, unsigned long long& since, TeamCtl* ctl, unsigned* err,
+                                          unsigned code, int knobs) {
   asm volatile("" ::: "memory");        // compiler barrier: re-issue the poll loads every round
-  ++spins;
+  if (spins++ == 0) since = __builtin_amdgcn_s_memrealtime();
   if ((spins & 255u) == 0) {
     if (ld_acq(&ctl->abort) != 0) return true;
-    if (spins > (((knobs >> 15) & 1) ? (kSpinLimit << 6) : kSpinLimit)) {
+    const unsigned long long limit = ((knobs >> 15) & 1) ? 6000000000ull : 200000000ull;
+    if (__builtin_amdgcn_s_memrealtime() - since > limit) {
       st_rel(err, code);
       st_rel(&ctl->abort, 1u);
       return true;
@@ -219,20 +197,20 @@ __device__ __forceinline__ bool spin_fail(unsigned& spins, TeamCtl* ctl, unsigne
 
 // Team formation + chain queue. Returns the team id (≥ 0) or -1 if this workgroup must exit. Called by all
 // threads; thread 0 does the global traffic, the result is broadcast through LDS.
-__device__ int join_team(TeamCtl* ctl, unsigned* err, int* sh, unsigned* sh_epoch, bool refuse = false) {
+__device__ int join_team(TeamCtl* ctl, unsigned* err, int* sh, unsigned* sh_epoch, int ts, bool refuse = false) {
   if (threadIdx.x == 0) {
     *sh_epoch = ld_acq(&ctl->epoch);
     int res = -1;
     const unsigned x = xcc_id();
     if (x < kMaxTeams && !refuse) {
       const unsigned r = add_agent(&ctl->xcnt[x], 1u);
-      if (r < (unsigned)kT) {
+      if (r < (unsigned)ts) {
         res = (int)x * 64 + (int)r;        // team x, member r
         unsigned spins = 0;
         if (r == 0) {
           bool ok = false;
           while (true) {
-            if (ld_acq(&ctl->xcnt[x]) >= (unsigned)kT) { ok = true; break; }
+            if (ld_acq(&ctl->xcnt[x]) >= (unsigned)ts) { ok = true; break; }
             if (++spins > (1u << 16)) break;
             __builtin_amdgcn_s_sleep(2);
           }
@@ -255,13 +233,13 @@ __device__ int join_team(TeamCtl* ctl, unsigned* err, int* sh, unsigned* sh_epoc
 }
 
 // Next chain for this team (all members agree). Returns chain id or -1 when the queue is drained / aborted.
-__device__ int next_chain(TeamCtl* ctl, int team, int member, unsigned iter, int nch, int* sh) {
+__device__ int next_chain(TeamCtl* ctl, int team, int member, unsigned iter, int nch, int* sh, int ts) {
   if (threadIdx.x == 0) {
     int res = -1;
     unsigned spins = 0;
     if (member == 0) {
       // every member finished the previous chain (its exchange buffers are free again)
-      while (ld_acq(&ctl->done[team]) < (unsigned)kT * iter) {
+      while (ld_acq(&ctl->done[team]) < (unsigned)ts * iter) {
         if (ld_acq(&ctl->abort) || ++spins > (1u << 24)) { spins = ~0u; break; }
         __builtin_amdgcn_s_sleep(1);
       }
@@ -330,7 +308,8 @@ __device__ __forceinline__ void lstm_team_fwd_body(
     TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st, unsigned long long* trace,
     int knobs, const float* __restrict__ bias4, const unsigned char* __restrict__ rst) {
   constexpr int H = 128 * KS;
-  constexpr int U = H / kT;             // units per workgroup (4·KS)
+  constexpr int TS = (VAR & 16) ? 16 : kT;   // workgroups per team
+  constexpr int U = H / TS;             // units per workgroup (4·KS; half teams 8·KS)
   constexpr int NTILE = U / 4;          // 16-column MFMA tiles per workgroup (= KS)
   constexpr int KSTEP = H / 32;         // k-steps of the full K
   constexpr int HP = H + 8;             // LDS row pitch (bf16)
@@ -338,23 +317,27 @@ __device__ __forceinline__ void lstm_team_fwd_body(
   constexpr int VV = VAR & 3;                     // variant; VAR & 4: precise (libm-class) activations
   constexpr bool PREC = (VAR & 4) != 0;
   constexpr bool V1 = VV >= 1;
-  constexpr int NT = VV == 2 ? 512 : kThreads;    // threads per workgroup
+  constexpr int NT = (VV == 2 || TS == 16) ? 512 : kThreads;    // threads per workgroup (half teams: 8 waves)
   constexpr int LPU = VV == 2 ? 32 : 16;          // V1/V2: lanes (K slices) per unit
   constexpr int UPW = 64 / LPU;                   // V1/V2: units per wave
   constexpr int KSL = H / LPU;                    // V1/V2: K slice per lane
-  static_assert(!V1 || (F32 && MT == 1), "V1 is the fp32 one-row variant");
+  constexpr int R = V1 ? (1 << ((VAR >> 5) & 3)) : 1;   // V1: rows per chain (VAR bits 5-6: 1, 2, 4)
+  constexpr int NR = V1 ? R : MT;                 // per-lane row registers (V1: every row; MFMA: one per tile)
+  static_assert(!V1 || (F32 && MT == 1), "V1 is the fp32 exact VALU variant");
   static_assert(VV != 2 || H == 512, "V2 maps 8 waves x 2 units onto the 16 units of H = 512");
+  static_assert(TS == kT || (VV == 1 && H == 512), "half teams: the V1 form at H = 512 (8 waves x 4 units)");
   __shared__ short hl[V1 ? 1 : 2][V1 ? 1 : RB][V1 ? 1 : HP];
   __shared__ short hlo[F32 && !V1 ? 2 : 1][F32 && !V1 ? RB : 1][F32 && !V1 ? HP : 1];   // F32: lo bf16 half of h
-  // V1: h_{t-1} of row 0 as 16 K slices, each padded by 4 floats (the 16 lanes of a row read 16 different slices
+  // V1: h_{t-1} of each row as 16 K slices, each padded by 4 floats (the 16 lanes of a row read 16 different slices
   // with one ds_read_b128: unpadded 128-B strides would put pairs of lanes on the same banks)
   constexpr int SP = KSL + 4;
-  __shared__ __attribute__((aligned(16))) float hf[V1 ? 2 : 1][V1 ? LPU * SP : 4];
+  constexpr int ROWF = LPU * SP;                  // V1: floats per row image
+  __shared__ __attribute__((aligned(16))) float hf[V1 ? 2 : 1][V1 ? R * ROWF : 4];
   __shared__ int sh_int;
   __shared__ unsigned sh_epoch;
 
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-  const int me = join_team(ctl, err, &sh_int, &sh_epoch, (knobs >> 11) & 1);
+  const int me = join_team(ctl, err, &sh_int, &sh_epoch, TS, (knobs >> 11) & 1);
   const unsigned epoch = sh_epoch;
   if (me < 0) return;
   const int team = me >> 6, m = me & 63;
@@ -412,45 +395,45 @@ __device__ __forceinline__ void lstm_team_fwd_body(
   const dca::f32x4 bv = (bias4 && mfma_wave) ? *reinterpret_cast<const dca::f32x4*>(bias4 + eunit * 4)
                                              : dca::f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // V1/V2 merged outputs: every lane of a unit's LPU-lane group carries row 0's state (the dot products are summed
-  // into all of them anyway), so c and h leave in ONE store instruction — slice-0 lanes write c, slice-1 lanes h — and
-  // a step queues two output stores (c|h, gates) behind its publish instead of three (cs, hsf, gates): the stores
-  // ahead of the next poll are what the step pays for (see the notes at the top). Measured (scripts/team_store_ab.py,
-  // bench A/B on one box): 1.420 vs 1.447 µs per standalone forward step, 4.874 vs 4.945 ms per learner step.
-  // Knob bit 14: the three-store form.
-  const bool merged = V1 && !((knobs >> 14) & 1);
+  // V1/V2 merged outputs: every lane of a unit's LPU-lane group carries every row's state (the dot products are
+  // summed into all of them anyway), so c and h leave in ONE store instruction — slice-2r lanes write row r's c,
+  // slice-(2r+1) lanes its h — and a step queues two output stores (c|h, gates) behind its publish instead of three
+  // (cs, hsf, gates): the stores ahead of the next poll are what the step pays for (see the notes at the top).
+  // Measured (scripts/team_store_ab.py, bench A/B on one box): 1.420 vs 1.447 µs per standalone forward step,
+  // 4.874 vs 4.945 ms per learner step.
   const int slice = V1 ? lane % LPU : 0;
   unsigned spins = 0;
+  unsigned long long since = 0;
   for (unsigned iter = 0;; ++iter) {
-    const int chain = next_chain(ctl, team, m, iter, nch, &sh_int);
+    const int chain = next_chain(ctl, team, m, iter, nch, &sh_int, TS);
     if (chain < 0) break;
     const int b0 = chain * Bc;
     const int B = min(Bc, Btot - b0);
     const unsigned tagbase = make_tagbase(epoch, iter);
-    float creg[MT], hreg[MT];
+    float creg[NR], hreg[NR];
 #pragma unroll
-    for (int mt = 0; mt < MT; ++mt) {
-      const int b = merged ? 0 : mt * 16 + erow;
-      creg[mt] = (mfma_wave && b < B) ? c0[(size_t)(b0 + b) * H + eunit] : 0.f;
-      hreg[mt] = 0.f;
+    for (int i = 0; i < NR; ++i) {
+      const int b = V1 ? i : i * 16 + erow;
+      creg[i] = (mfma_wave && b < B) ? c0[(size_t)(b0 + b) * H + eunit] : 0.f;
+      hreg[i] = 0.f;
     }
     bool dead = false;
     for (int t = 0; t < S; ++t) {
       const int par = t & 1;
-      if ((knobs >> 12) & 1) spins = 0;
+      spins = 0;
       TSTAMP(0);
       // ---- prefetch this step's input projection (one 16-B vector per owned (row, unit)). Loading it one step
       // ahead instead measured slower (2.11 vs 1.94 µs per step at B=8, H=512).
-      dca::f32x4 xv[MT];
-      bool rz[MT];                                    // sequence packing: an episode starts at step t (h, c := 0)
+      dca::f32x4 xv[NR];
+      bool rz[NR];                                    // sequence packing: an episode starts at step t (h, c := 0)
       if (mfma_wave) {
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const int b = merged ? 0 : mt * 16 + erow;     // (merged: the group's lanes load the same 16 B, one request)
+        for (int i = 0; i < NR; ++i) {
+          const int b = V1 ? i : i * 16 + erow;         // (V1: the group's lanes load the same 16 B, one request)
           const size_t tx = ((knobs >> 10) & 1) ? 0 : (size_t)t;   // knob: every step reads step 0 (L2-resident)
-          xv[mt] = (b < B) ? *reinterpret_cast<const dca::f32x4*>(xp4 + (((size_t)(b0 + b) * sb + tx * st) * H + eunit) * 4)
-                           : dca::f32x4{0.f, 0.f, 0.f, 0.f};
-          rz[mt] = rst != nullptr && b < B && rst[(size_t)(b0 + b) * sb + (size_t)t * st] != 0;
+          xv[i] = (b < B) ? *reinterpret_cast<const dca::f32x4*>(xp4 + (((size_t)(b0 + b) * sb + tx * st) * H + eunit) * 4)
+                          : dca::f32x4{0.f, 0.f, 0.f, 0.f};
+          rz[i] = rst != nullptr && b < B && rst[(size_t)(b0 + b) * sb + (size_t)t * st] != 0;
         }
       }
       // ---- gather h_{t-1} into hl[par]
@@ -459,7 +442,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           const int b = i / H, k = i % H;
           const float v = h0[(size_t)(b0 + b) * H + k];
           if constexpr (V1) {
-            hf[par][(k / KSL) * SP + k % KSL] = v;
+            hf[par][b * ROWF + (k / KSL) * SP + k % KSL] = v;
           } else {
             hl[par][b][k] = dca::f2bf(v);
             if constexpr (F32) hlo[par][b][k] = dca::f2bf(v - dca::bf2f(dca::f2bf(v)));
@@ -469,7 +452,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
         const unsigned tag = tagbase | (unsigned)t;          // h_{t-1} carries tag t
         const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(xg + (size_t)((t - 1) & 1) * Bc * GPR, Bc * GPR * 8);
         constexpr int CPR = F32 ? H / 2 : H / 4;              // 16-B chunks (2 f32 / 4 bf16 h values) per row
-        constexpr int NL = ((V1 ? 1 : RB) * CPR + NT - 1) / NT;   // (V1: one row)
+        constexpr int NL = ((V1 ? R : RB) * CPR + NT - 1) / NT;   // (V1: R rows)
         // every chunk is re-polled only until it has arrived, so later rounds move only the missing bytes
         i32x4 g[NL];
         bool okc[NL];
@@ -481,7 +464,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
             g[0] = __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16, 0, kSc1);
             okc[0] = ((unsigned)g[0].y == tag) & ((unsigned)g[0].w == tag);
             if (__all(okc[0])) break;
-            if (spin_fail(spins, ctl, err, 1u, knobs)) { dead = true; break; }
+            if (spin_fail(spins, since, ctl, err, 1u, knobs)) { dead = true; break; }
           }
         }
         while (!dead) {
@@ -495,15 +478,15 @@ __device__ __forceinline__ void lstm_team_fwd_body(
             ok &= okc[i];
           }
           if (__all(ok)) break;
-          if (spin_fail(spins, ctl, err, 1u, knobs)) { dead = true; break; }
+          if (spin_fail(spins, since, ctl, err, 1u, knobs)) { dead = true; break; }
         }
 #pragma unroll
         for (int i = 0; i < NL; ++i) {
           const int ci = tid + NT * i;
           if (ci < B * CPR) {
             if constexpr (V1) {
-              const int k = 2 * ci;
-              *reinterpret_cast<float2*>(&hf[par][(k / KSL) * SP + k % KSL]) =
+              const int b = ci / CPR, k = 2 * (ci % CPR);
+              *reinterpret_cast<float2*>(&hf[par][b * ROWF + (k / KSL) * SP + k % KSL]) =
                   make_float2(__int_as_float(g[i].x), __int_as_float(g[i].z));
             } else if constexpr (F32) {
               const int b = ci / CPR, k = (ci % CPR) * 2;
@@ -525,29 +508,66 @@ __device__ __forceinline__ void lstm_team_fwd_body(
       lds_barrier();
       if (sh_int == -2) break;
       TSTAMP(2);
-      if (mfma_wave) {
+      if constexpr (V1) {
+        // ---- exact fp32 VALU, R rows: the 4 gates of this lane's unit over its K slice for every row (W_hh slice in
+        // VGPRs reused across the rows), summed over the unit's LPU slices — every lane of the group holds every row
+        float g[R][4];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if (r < B) {                                        // (B is uniform)
+            pk_dot4<KSL>(wq, &hf[par][r * ROWF + slice * SP], g[r][0], g[r][1], g[r][2], g[r][3]);
+            // (Tried, one row: a reduce-SCATTER over the 16 slices — xor 1 / xor 2 quad swaps then row_ror 4 / 8, 4
+            // DPP moves instead of 16 — with one activation per lane and a quad broadcast of the four gates: 1.500 vs
+            // 1.481 µs per standalone step, no gain in the learner step; the plain row sums stay.)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) g[r][q] = LPU == 32 ? row_sum32(g[r][q]) : row_sum16(g[r][q]);
+          }
+        }
+        float act[R][4], cr[R], hr[R], hpub = 0.f;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          cr[r] = hr[r] = 0.f;
+          act[r][0] = act[r][1] = act[r][2] = act[r][3] = 0.f;
+          if (r < B) {
+            if (rz[r]) { g[r][0] = 0.f; g[r][1] = 0.f; g[r][2] = 0.f; g[r][3] = 0.f; }   // episode start
+            const float pi = g[r][0] + (xv[r][0] + bv[0]), pf = g[r][1] + (xv[r][1] + bv[1]),
+                        pg = g[r][2] + (xv[r][2] + bv[2]), po = g[r][3] + (xv[r][3] + bv[3]);
+            const float ig = sigm<PREC>(pi), fg = sigm<PREC>(pf), gg = tanh_<PREC>(pg), og = sigm<PREC>(po);
+            const float c = fg * (rz[r] ? 0.f : creg[r]) + ig * gg;
+            const float hv = og * tanh_<PREC>(c);
+            creg[r] = c; hreg[r] = hv; cr[r] = c; hr[r] = hv;
+            act[r][0] = ig; act[r][1] = fg; act[r][2] = gg; act[r][3] = og;
+            if (slice == r) hpub = hv;
+          }
+        }
+        TSTAMP(3);
+        // ---- publish h_t: the slice-r lane of every unit group publishes row r's granule {f32 h(u), tag}
+        if (slice < B) {
+          const u32x2 gv = {(unsigned)__float_as_int(hpub), tagbase | (unsigned)(t + 1)};
+          const __amdgpu_buffer_rsrc_t ws = uniform_rsrc(xg + (size_t)par * Bc * GPR, Bc * GPR * 8);
+          __builtin_amdgcn_raw_buffer_store_b64(gv, ws, (slice * H + eunit) * 8, 0, kPlain);
+        }
+        TSTAMP(4);
+        // ---- outputs, one store instruction per lane: slice 2r → row r's c (+ its gates), slice 2r+1 → row r's h
+        // (one b32 store for everything — slices 0-3 the gates, 4 c, 5 h — measured slower: 1.476 vs 1.410 µs)
+        const int orow = slice >> 1;
+        if (orow < B && orow < R && !((knobs >> 8) & 1)) {
+          float cv = 0.f, hv = 0.f;
+          dca::f32x4 av = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int r = 0; r < R; ++r)
+            if (orow == r) { cv = cr[r]; hv = hr[r]; av = dca::f32x4{act[r][0], act[r][1], act[r][2], act[r][3]}; }
+          const size_t o = ((size_t)(b0 + orow) * sb + (size_t)t * st) * H + eunit;
+          gstore((slice & 1) ? hsf + o : cs + o, (slice & 1) ? hv : cv);
+          if (!(slice & 1)) *reinterpret_cast<dca::f32x4*>(gates4 + o * 4) = av;
+        }
+        TSTAMP(5);
+      } else if (mfma_wave) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           if (mt * 16 >= B) break;                            // wave-uniform
           float gq0 = 0.f, gq1 = 0.f, gq2 = 0.f, gq3 = 0.f;
-          if constexpr (V1) {
-            // ---- exact fp32: 4 gates of this lane's unit over its K slice, summed over the unit's LPU slices
-            pk_dot4<KSL>(wq, &hf[par][(lane % LPU) * SP], gq0, gq1, gq2, gq3);
-            if constexpr (LPU == 32) {
-              gq0 = row_sum32(gq0);
-              gq1 = row_sum32(gq1);
-              gq2 = row_sum32(gq2);
-              gq3 = row_sum32(gq3);
-            } else {
-              // (Tried: a reduce-SCATTER over the 16 slices — xor 1 / xor 2 quad swaps then row_ror 4 / 8, 4 DPP
-              // moves instead of 16 — with one activation per lane and a quad broadcast of the four gates: 1.500 vs
-              // 1.481 µs per standalone step, no gain in the learner step; the plain row sums stay.)
-              gq0 = row_sum16(gq0);
-              gq1 = row_sum16(gq1);
-              gq2 = row_sum16(gq2);
-              gq3 = row_sum16(gq3);
-            }
-          } else {
+          {
           // ---- gates pre-activation tile: rows = batch, columns = (unit, gate)
           dca::f32x4 acc = {0.f, 0.f, 0.f, 0.f};
           if constexpr (F32) {
@@ -588,7 +608,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
             gq2 = qs == 2 ? got : gq2;
             gq3 = qs == 3 ? got : gq3;
           }
-          }   // !V1
+          }
           const int b = mt * 16 + erow;
           if (rz[mt]) { gq0 = 0.f; gq1 = 0.f; gq2 = 0.f; gq3 = 0.f; }   // episode start: no recurrent term
           // (bias added here, at the use: an add right after the prefetch would wait out the load before the gather)
@@ -597,7 +617,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           const float ig = sigm<PREC>(pi), fg = sigm<PREC>(pf), gg = tanh_<PREC>(pg), og = sigm<PREC>(po);
           const float c = fg * (rz[mt] ? 0.f : creg[mt]) + ig * gg;
           const float hv = og * tanh_<PREC>(c);
-          if (merged ? 0 < B : b < B) { creg[mt] = c; hreg[mt] = hv; }
+          if (b < B) { creg[mt] = c; hreg[mt] = hv; }
           TSTAMP(3);
           if constexpr (F32) {
             // ---- publish h_t: granule {f32 h(u), tag} by every lane of a live row
@@ -619,15 +639,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           }
           TSTAMP(4);
           // ---- outputs
-          if (merged) {
-            // (one b32 store for everything — slices 0-3 the gates, 4 c, 5 h — measured slower: 1.476 vs 1.410 µs)
-            if (slice < 2 && 0 < B && !((knobs >> 8) & 1)) {
-              const size_t o = ((size_t)b0 * sb + (size_t)t * st) * H + eunit;
-              float* dst = slice == 0 ? cs + o : hsf + o;        // one store instruction: c (slice 0), h (slice 1)
-              gstore(dst, slice == 0 ? c : hv);
-              if (slice == 0) *reinterpret_cast<dca::f32x4*>(gates4 + o * 4) = dca::f32x4{ig, fg, gg, og};
-            }
-          } else if (b < B && !((knobs >> 8) & 1)) {
+          if (b < B && !((knobs >> 8) & 1)) {
             const size_t bt = (size_t)(b0 + b) * sb + (size_t)t * st;
             if (hs) hs[bt * H + eunit] = dca::f2bf(hv);
             if (hsf) hsf[bt * H + eunit] = hv;
@@ -642,11 +654,11 @@ __device__ __forceinline__ void lstm_team_fwd_body(
     if (sh_int == -2) return;
     if (mfma_wave) {
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) {
-        const int b = mt * 16 + erow;
-        if (b < B) {
-          hn[(size_t)(b0 + b) * H + eunit] = hreg[mt];
-          cn[(size_t)(b0 + b) * H + eunit] = creg[mt];
+      for (int i = 0; i < NR; ++i) {
+        const int b = V1 ? i : i * 16 + erow;
+        if (b < B && (!V1 || slice == i)) {
+          hn[(size_t)(b0 + b) * H + eunit] = hreg[i];
+          cn[(size_t)(b0 + b) * H + eunit] = creg[i];
         }
       }
     }
@@ -674,45 +686,42 @@ __device__ __forceinline__ void lstm_team_bwd_body(
     const void* __restrict__ whh_, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
     i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
     unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart, int knobs,
-    const unsigned char* __restrict__ rst, const float* __restrict__ hsf, const float* __restrict__ h0,
-    float* __restrict__ dwpart) {
+    const unsigned char* __restrict__ rst) {
   constexpr int H = 128 * KS;
-  constexpr int U = H / kT;             // 4·KS units per workgroup (MFMA N, zero-padded to 16)
+  constexpr int TS = (VAR & 16) ? 16 : kT;   // workgroups per team
+  constexpr int U = H / TS;             // 4·KS units per workgroup (MFMA N, zero-padded to 16; half teams 8·KS)
   constexpr int VV = VAR & 3;
   constexpr bool PREC = (VAR & 4) != 0;
   constexpr bool V1 = VV >= 1;
-  constexpr int NW = VV == 2 ? 8 : 4;   // waves (K parts)
+  constexpr int NWK = VV == 2 ? 8 : 4;  // K parts (waves per 16-unit group)
+  constexpr int UH = V1 && U > 16 ? U / 16 : 1;   // V1 16-unit groups (half teams: 2)
+  constexpr int NW = NWK * UH;          // waves
   constexpr int NT = 64 * NW;
-  constexpr int KW = 4 * H / NW;        // K (= 4H gate columns) per wave
+  constexpr int KW = 4 * H / NWK;       // K (= 4H gate columns) per wave
   constexpr int KSTEP = KW / 32;
   constexpr int RB = MT * 16;
   constexpr int GP = 4 * H + 8;         // LDS pitch (bf16) of the gathered dG rows
-  constexpr int NPAIR = (RB * U + NT - 1) / NT;
   constexpr int KSL = KW / 16;          // V1: K slice per lane of a wave's K part
-  static_assert(!V1 || (F32 && MT == 1), "V1 is the fp32 one-row variant");
+  constexpr int R = V1 ? (1 << ((VAR >> 5) & 3)) : 1;   // V1: rows per chain (VAR bits 5-6: 1, 2, 4)
+  constexpr int NPAIR = ((V1 ? R : RB) * U + NT - 1) / NT;
+  static_assert(!V1 || (F32 && MT == 1), "V1 is the fp32 exact VALU variant");
   static_assert(VV != 2 || H == 512, "V2 is the H = 512 variant");
-  // V1 + DW: ∂W_hh fused into the recurrence. Lane (wv, u-group, slice) owns ∂W_hhᵀ for exactly the (gate column, unit)
-  // pairs whose W_hhᵀ it holds in wq: Σ_t dG_{t+1}[gc]·h_t[j0 + unit] accumulated in fp32 FMAs (descending t) in the
-  // dot phase, from the same LDS reads as the partial recurrent gradient. It runs on the 4-wave V1 form: one wave per
-  // SIMD has 512 registers for wq + the 128 accumulators (on the 8-wave V2, 256 per wave, even a bare 64-accumulator
-  // loop spilled 33 registers). MEASURED SLOWER, opt-in only (models/pipelined.py DCA_FUSED_DW=1): 3755 vs 2091 µs
-  // for the backward at B = 8, S = 1400 (the accumulators land in AGPRs: copies + FMAs on every step's critical
-  // path), against 330 µs saved in the tail — 7.03 vs 5.59 ms per step. Per chain the slice goes to
-  // dwpart[chain] (PyTorch row order); the caller sums the chains. It replaces the ∂W_hh GEMM after the recurrence
-  // (gemm_tn over B·S rows: 220 µs alone, ≈400 µs beside the tail's other kernels).
-  constexpr bool DW = VV == 1 && (VAR & 8) != 0;   // (a template variant: the plain variants keep their registers)
+  static_assert(TS == kT || (VV == 1 && H == 512), "half teams: the V1 form at H = 512 (2 unit groups x 4 K parts)");
+  // (Measured and removed in round 5: ∂W_hh accumulated inside this recurrence — 128 accumulators per lane on every
+  // step's critical path, 3755 vs 2091 µs for the backward, 7.03 vs 5.59 ms per learner step.)
   __shared__ short dgl[V1 ? 1 : RB][V1 ? 1 : GP];
   __shared__ short dglo[F32 && !V1 ? RB : 1][F32 && !V1 ? GP : 1];   // F32: lo bf16 half of the gathered dG
   // V1: dG_{t+1} of row 0, fp32, as 64 K slices each padded by 4 floats (bank spread, as forward)
   constexpr int SP = KSL + 4;
-  __shared__ __attribute__((aligned(16))) float dgf[V1 ? (4 * H / KSL) * SP : 4];
-  __shared__ float red[NW][RB][17];
+  constexpr int DROW = (4 * H / KSL) * SP;   // V1: floats per row image of dG_{t+1}
+  __shared__ __attribute__((aligned(16))) float dgf[V1 ? R * DROW : 4];
+  __shared__ float red[NWK][RB][(U > 16 ? U : 16) + 1];
   __shared__ float dbs[RB * U * 4];     // per-(row, unit, gate) bias-gradient sums of a chain
   __shared__ int sh_int;
   __shared__ unsigned sh_epoch;
 
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-  const int me = join_team(ctl, err, &sh_int, &sh_epoch);
+  const int me = join_team(ctl, err, &sh_int, &sh_epoch, TS);
   const unsigned epoch = sh_epoch;
   if (me < 0) return;
   const int team = me >> 6, m = me & 63;
@@ -738,10 +747,10 @@ __device__ __forceinline__ void lstm_team_bwd_body(
     // lane (ug = lane/16, slice = lane%16): W_hhᵀ of units j0 + 4·ug + uu (uu < 4) over the slice's gate columns
 #pragma unroll
     for (int uu = 0; uu < 4; ++uu) {
-      const int unit = 4 * (lane >> 4) + uu;
+      const int unit = 16 * (wv / NWK) + 4 * (lane >> 4) + uu;
 #pragma unroll
       for (int j = 0; j < KSL; ++j) {
-        const int gc = wv * KW + (lane & 15) * KSL + j;
+        const int gc = (wv % NWK) * KW + (lane & 15) * KSL + j;
         wq[uu * KSL + j] =
             (unit < U) ? static_cast<const float*>(whh_)[(size_t)((gc & 3) * H + (gc >> 2)) * H + j0 + unit] : 0.f;
       }
@@ -770,8 +779,9 @@ __device__ __forceinline__ void lstm_team_bwd_body(
   // computing unit u redundantly, role r picking the record — the forward's merged-store idea applied here: 1.578 vs
   // 1.535 µs per step, slower; the three stores of the 16 unit lanes stay.)
   unsigned spins = 0;
+  unsigned long long since = 0;
   for (unsigned iter = 0;; ++iter) {
-    const int chain = next_chain(ctl, team, m, iter, nch, &sh_int);
+    const int chain = next_chain(ctl, team, m, iter, nch, &sh_int, TS);
     if (chain < 0) break;
     const int b0 = chain * Bc;
     const int B = min(Bc, Btot - b0);
@@ -786,22 +796,10 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       dcarry[i] = (pi < B * U && dcn) ? dcn[(size_t)(b0 + pi / U) * H + j0 + pi % U] : 0.f;
     }
     bool dead = false;
-    // ∂W_hhᵀ[gc_j][j0 + 4·(lane>>4) + uu]: units (0, 1) at dwq[j], units (2, 3) at dwq[KSL + j]
-    f32x2 dwq[DW ? 2 * KSL : 1];
-#pragma unroll
-    for (int i = 0; i < (DW ? 2 * KSL : 1); ++i) dwq[i] = f32x2{0.f, 0.f};
     for (int k = 0; k <= S; ++k) {
       const int t = S - 1 - k;          // step whose gate gradients are produced this iteration (-1: final)
-      if ((knobs >> 12) & 1) spins = 0;
+      spins = 0;
       TSTAMPB(0);
-      // ∂W_hh operand of this iteration: h_t of the lane's 4 units (h0 for t = -1); an episode starting at t+1 never
-      // read h_t, so its term is skipped (the recurrent gradient skips it the same way)
-      float4 hq = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (DW && k > 0) {
-        const size_t hr = t >= 0 ? ((size_t)b0 * sb + (size_t)t * st) * H : (size_t)b0 * H;
-        hq = *reinterpret_cast<const float4*>((t >= 0 ? hsf : h0) + hr + j0 + 4 * (lane >> 4));
-        if (rst != nullptr && rst[(size_t)b0 * sb + (size_t)(t + 1) * st] != 0) hq = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
       // ---- prefetch the saved activations of step t for the owned pairs
       dca::f32x4 gv[NPAIR];
       float cv[NPAIR], cpv[NPAIR], dv[NPAIR];
@@ -829,7 +827,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       if (k > 0) {
         const unsigned tag = tagbase | (unsigned)(t + 2);
         const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(xg + (size_t)((t + 1) & 1) * Bc * H * CPU_, Bc * H * CPU_ * 16);
-        constexpr int RG = V1 ? 1 : (F32 ? 4 : 8);         // rows per gather group
+        constexpr int RG = V1 ? R : (F32 ? 4 : 8);         // rows per gather group
         constexpr int NL = RG * H * CPU_ / NT;             // chunks per thread per group
         for (int g0 = 0; g0 < B && !dead; g0 += RG) {
           const int nck = min(RG, B - g0) * H * CPU_;
@@ -848,15 +846,15 @@ __device__ __forceinline__ void lstm_team_bwd_body(
               ok &= okc[i];
             }
             if (__all(ok)) break;
-            if (spin_fail(spins, ctl, err, 2u, knobs)) { dead = true; break; }
+            if (spin_fail(spins, since, ctl, err, 2u, knobs)) { dead = true; break; }
           }
 #pragma unroll
           for (int i = 0; i < NL; ++i) {
             const int ci = tid + NT * i;
             if (ci < nck) {
               if constexpr (V1) {
-                const int gc = 4 * (ci >> 1) + 2 * (ci & 1);
-                *reinterpret_cast<float2*>(&dgf[(gc / KSL) * SP + gc % KSL]) =
+                const int b = ci / (H * CPU_), r = ci % (H * CPU_), gc = 4 * (r >> 1) + 2 * (r & 1);
+                *reinterpret_cast<float2*>(&dgf[b * DROW + (gc / KSL) * SP + gc % KSL]) =
                     make_float2(__int_as_float(g[i].x), __int_as_float(g[i].z));
               } else if constexpr (F32) {
                 const int b = g0 + ci / (2 * H), r = ci % (2 * H), gc = 4 * (r >> 1) + 2 * (r & 1);
@@ -881,19 +879,24 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       TSTAMPB(2);
       // ---- partial recurrent gradient over this wave's K quarter → red[wv]
       if (V1 && k > 0) {
-        float o0, o1, o2, o3;
-        if constexpr (DW) pk_dot4_dw<KSL>(wq, &dgf[(wv * 16 + (lane & 15)) * SP], hq, dwq, o0, o1, o2, o3);
-        else pk_dot4<KSL>(wq, &dgf[(wv * 16 + (lane & 15)) * SP], o0, o1, o2, o3);
-        o0 = row_sum16(o0);
-        o1 = row_sum16(o1);
-        o2 = row_sum16(o2);
-        o3 = row_sum16(o3);
-        const int u0 = 4 * (lane >> 4);
-        if ((lane & 15) == 0 && u0 < U) {
-          red[wv][0][u0] = o0;
-          red[wv][0][u0 + 1] = o1;
-          red[wv][0][u0 + 2] = o2;
-          red[wv][0][u0 + 3] = o3;
+        const int wk = wv % NWK;
+        const int u0 = 16 * (wv / NWK) + 4 * (lane >> 4);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          if (r >= B) break;                                  // (B is uniform)
+          float o0, o1, o2, o3;
+          const float* x = &dgf[r * DROW + (wk * 16 + (lane & 15)) * SP];
+          pk_dot4<KSL>(wq, x, o0, o1, o2, o3);
+          o0 = row_sum16(o0);
+          o1 = row_sum16(o1);
+          o2 = row_sum16(o2);
+          o3 = row_sum16(o3);
+          if ((lane & 15) == 0 && u0 < U) {
+            red[wk][r][u0] = o0;
+            red[wk][r][u0 + 1] = o1;
+            red[wk][r][u0 + 2] = o2;
+            red[wk][r][u0 + 3] = o3;
+          }
         }
       } else if (k > 0) {
 #pragma unroll
@@ -930,7 +933,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
           const int b = i / U, u = i % U;
           float acc = 0.f;
 #pragma unroll
-          for (int w = 0; w < NW; ++w) acc += red[w][b][u];
+          for (int w = 0; w < NWK; ++w) acc += red[w][b][u];
           // an episode starting at step 0 never read h0
           dh0[(size_t)(b0 + b) * H + j0 + u] = (rst != nullptr && rst[(size_t)(b0 + b) * sb] != 0) ? 0.f : acc;
         }
@@ -949,7 +952,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
             rec = dhn ? dhn[(size_t)(b0 + b) * H + j0 + u] : 0.f;
           } else if (!rnext[i]) {
 #pragma unroll
-            for (int w = 0; w < NW; ++w) rec += red[w][b][u];
+            for (int w = 0; w < NWK; ++w) rec += red[w][b][u];
           }
           const float ig = gv[i][0], fg = gv[i][1], gg = gv[i][2], og = gv[i][3];
           const float dht = dv[i] + rec;
@@ -982,15 +985,6 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       TSTAMPB(6);
     }
     if (sh_int == -2) return;
-    if constexpr (DW) {
-      // this chain's ∂W_hh slice → dwpart[chain] in PyTorch's gate-major rows (gate q of unit i at row q·H + i)
-#pragma unroll
-      for (int j = 0; j < KSL; ++j) {
-        const int gc = wv * KW + (lane & 15) * KSL + j;
-        *reinterpret_cast<float4*>(dwpart + ((size_t)chain * 4 * H + (size_t)((gc & 3) * H + (gc >> 2))) * H + j0 +
-                                   4 * (lane >> 4)) = make_float4(dwq[j].x, dwq[j].y, dwq[KSL + j].x, dwq[KSL + j].y);
-      }
-    }
     if (dbpart) {
       // bias gradient of this chain for the owned units: Σ over rows (fixed order) of the per-pair sums
 #pragma unroll
@@ -1012,41 +1006,60 @@ __device__ __forceinline__ void lstm_team_bwd_body(
 #undef TSTAMPB
 }
 
+// Half teams (VAR bit 4): 16 workgroups of 512 threads per team, made CU-EXCLUSIVE by LDS — each workgroup holds
+// ≥ 159 KB of the CU's 160 KB, so no workgroup of another kernel that uses LDS (every GEMM / encoder / chain kernel
+// of the step) can land on a recurrence CU; the other 16 CUs of every XCD stay free for the step's other kernels
+// (which would otherwise co-reside and lengthen every hand-off, profiles/r4_chunk_overlap_probe.md).
+template <int VAR, int PAD>
+__device__ __forceinline__ void claim_cu(int knobs) {
+  if constexpr ((VAR & 16) != 0) {
+    __shared__ char pad[PAD];
+    if (knobs == 0x7fffffff) reinterpret_cast<volatile char*>(pad)[threadIdx.x] = 0;   // (never: keeps the LDS)
+  }
+}
+// pads up to ≈159.5 KB per workgroup: the variants' own LDS (measured from the compiled kernels: forward 4 616 B +
+// 4 608 per extra row, backward 25 864 B + 9 216 per extra row) subtracted from the target
+constexpr int kHalfLds = 163328;
+constexpr int pad_fwd(int var) { return kHalfLds - (4616 + ((1 << ((var >> 5) & 3)) - 1) * 4608); }
+constexpr int pad_bwd(int var) { return kHalfLds - (25864 + ((1 << ((var >> 5) & 3)) - 1) * 9216); }
+inline int team_threads(int var) { return ((var & 3) == 2 || (var & 16)) ? 512 : kThreads; }
+inline int team_size(int var) { return (var & 16) ? 16 : kT; }
+
 template <int MT, int KS, bool F32, int VAR>
-__global__ __launch_bounds__((VAR & 3) == 2 ? 512 : kThreads, 1) void lstm_team_fwd_kernel(
+__global__ __launch_bounds__(((VAR & 3) == 2 || (VAR & 16)) ? 512 : kThreads, 1) void lstm_team_fwd_kernel(
     const float* __restrict__ xp4, const void* __restrict__ whh, const float* __restrict__ h0,
     const float* __restrict__ c0, short* __restrict__ hs, float* __restrict__ hsf, float* __restrict__ cs,
     float* __restrict__ gates4, float* __restrict__ hn, float* __restrict__ cn, unsigned long long* xg_all,
     TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st, unsigned long long* trace,
     int knobs, const float* __restrict__ bias4, const unsigned char* __restrict__ rst) {
   __builtin_amdgcn_s_setprio(3);   // issue priority over co-resident waves of kernels overlapped on other streams
+  claim_cu<VAR, pad_fwd(VAR)>(knobs);
   lstm_team_fwd_body<MT, KS, F32, VAR>(xp4, whh, h0, c0, hs, hsf, cs, gates4, hn, cn, xg_all, ctl, err, Btot, Bc, nch, S, sb,
                              st, trace, knobs, bias4, rst);
   team_exit(ctl, err, nch);
 }
 
 template <int MT, int KS, bool F32, int VAR>
-__global__ __launch_bounds__((VAR & 3) == 2 ? 512 : kThreads, 1) void lstm_team_bwd_kernel(
+__global__ __launch_bounds__(((VAR & 3) == 2 || (VAR & 16)) ? 512 : kThreads, 1) void lstm_team_bwd_kernel(
     const float* __restrict__ dhs, const float* __restrict__ gates4, const float* __restrict__ cs,
     const float* __restrict__ c0, const float* __restrict__ dhn, const float* __restrict__ dcn,
     const void* __restrict__ whh, float* __restrict__ dgates4, float* __restrict__ dh0, float* __restrict__ dc0,
     i32x4* xg_all, TeamCtl* ctl, unsigned* err, int Btot, int Bc, int nch, int S, int sb, int st,
     unsigned long long* trace, short* __restrict__ dg16, float* __restrict__ dbpart, int knobs,
-    const unsigned char* __restrict__ rst, const float* __restrict__ hsf, const float* __restrict__ h0,
-    float* __restrict__ dwpart) {
+    const unsigned char* __restrict__ rst) {
   __builtin_amdgcn_s_setprio(3);
+  claim_cu<VAR, pad_bwd(VAR)>(knobs);
   lstm_team_bwd_body<MT, KS, F32, VAR>(dhs, gates4, cs, c0, dhn, dcn, whh, dgates4, dh0, dc0, xg_all, ctl, err, Btot, Bc, nch,
-                             S, sb, st, trace, dg16, dbpart, knobs, rst, hsf, h0, dwpart);
+                             S, sb, st, trace, dg16, dbpart, knobs, rst);
   team_exit(ctl, err, nch);
 }
 
-// DCA_TEAM_KNOBS = pre_sleep | skip_outputs << 8 | probe_first << 9 | xp_step0 << 10 | spin count reset per step << 12
-// | no poll back-off sleep << 13 | three-store forward outputs << 14 (latency experiments only);
+// DCA_TEAM_KNOBS = pre_sleep | skip_outputs << 8 | probe_first << 9 | xp_step0 << 10 | no poll back-off sleep << 13
+// | three-store forward outputs << 14 (latency experiments only);
 // DCA_TEAM_FAIL=1 sets bit 11: no workgroup joins a team (fault injection: every chain left unprocessed → err 3);
-// DCA_TEAM_PATIENT=1 sets bit 15: a 64× longer hand-off timeout (≈1 min instead of ≈1 s of polling) for runs that
-// share the GPU with another process (bench.py DCA_SHARED_GPU rehearsals), where the other process's kernels can
-// hold a team member's CU long enough to trip the exclusive-GPU limit (seen once: backward timeout, code 2, two
-// ranks on one MI355X); a real lost hand-off still ends in the error, just later
+// DCA_TEAM_PATIENT=1 sets bit 15: a 60 s instead of 2 s wall-clock hand-off timeout (spin_fail) for runs that share
+// the GPU with another process's persistent kernels (bench.py DCA_SHARED_GPU rehearsals: two ranks' recurrences on
+// one MI355X); a real lost hand-off still ends in the error, just later
 inline int team_knobs() {
   const char* e = getenv("DCA_TEAM_KNOBS");
   const char* f = getenv("DCA_TEAM_FAIL");
@@ -1073,7 +1086,7 @@ inline void plan(int B, int& nch, int& Bc, int& MT, int f32 = 0) {
 
 // (F32_, V1_) = (0, 0) bf16 MFMA, (1, 0) bf16x3 MFMA, (1, 1) exact-fp32 VALU for one-row chains
 #define DCA_TEAM_DISPATCH(MT_, KS_, F32_, V1_, ...)                                                        \
-  switch (((V1_) << 12) | ((F32_) << 8) | ((MT_) << 4) | (KS_)) {                                          \
+  switch (((V1_) << 12) | ((F32_) << 8) | ((MT_) << 4) | (KS_)) {   /* V1_ bit 4 (half teams) → 0x10000 */                                          \
     case 0x0011: return __VA_ARGS__(1, 1, false, 0); case 0x0012: return __VA_ARGS__(1, 2, false, 0); \
     case 0x0014: return __VA_ARGS__(1, 4, false, 0); case 0x0021: return __VA_ARGS__(2, 1, false, 0); \
     case 0x0022: return __VA_ARGS__(2, 2, false, 0); case 0x0024: return __VA_ARGS__(2, 4, false, 0); \
@@ -1083,27 +1096,29 @@ inline void plan(int B, int& nch, int& Bc, int& MT, int f32 = 0) {
     case 0x1114: return __VA_ARGS__(1, 4, true, 1);      case 0x2114: return __VA_ARGS__(1, 4, true, 2);      \
     case 0x5111: return __VA_ARGS__(1, 1, true, 5);      case 0x5112: return __VA_ARGS__(1, 2, true, 5);      \
     case 0x5114: return __VA_ARGS__(1, 4, true, 5);      case 0x6114: return __VA_ARGS__(1, 4, true, 6);      \
+    case 0x11114: return __VA_ARGS__(1, 4, true, 17);                                                       \
+    case 0x21111: return __VA_ARGS__(1, 1, true, 33);    case 0x21112: return __VA_ARGS__(1, 2, true, 33);   \
+    case 0x21114: return __VA_ARGS__(1, 4, true, 33);    case 0x22114: return __VA_ARGS__(1, 4, true, 34);   \
+    case 0x31114: return __VA_ARGS__(1, 4, true, 49);                                                       \
+    case 0x41111: return __VA_ARGS__(1, 1, true, 65);    case 0x41112: return __VA_ARGS__(1, 2, true, 65);   \
+    case 0x41114: return __VA_ARGS__(1, 4, true, 65);    case 0x42114: return __VA_ARGS__(1, 4, true, 66);   \
+    case 0x51114: return __VA_ARGS__(1, 4, true, 81);                                                       \
     default: return hipErrorInvalidValue;                                                                    \
   }
 
 // one-row fp32 chains take the exact VALU variant (DCA_TEAM_V1=0 forces the bf16x3 MFMA one, for comparison); at
 // H = 512 the backward takes its 8-wave form V2 (measured B=8, S=1400: backward 2069 vs 2137 µs, while the 8-wave
 // forward was SLOWER, 2056 vs 1778 µs). DCA_TEAM_V2 = 0 (neither), 1 (both directions), default: backward only.
-inline int use_v1(int f32, int Bc, int H, int backward, int precise) {
+// half: the CU-exclusive 16-workgroup teams (V1 form in both directions, H = 512, fast activations).
+inline int use_v1(int f32, int Bc, int H, int backward, int precise, int half = -1) {
   static const int off = [] { const char* e = getenv("DCA_TEAM_V1"); return e && e[0] == '0'; }();
+  static const int half_env = [] { const char* e = getenv("DCA_TEAM_HALF"); return e && e[0] == '1'; }();
+  if (half < 0) half = half_env;
   static const int v2 = [] { const char* e = getenv("DCA_TEAM_V2"); return e ? (e[0] == '0' ? 0 : 3) : 2; }();
-  if (!(f32 && Bc == 1 && !off)) return 0;
-  return ((H == 512 && (v2 & (backward ? 2 : 1))) ? 2 : 1) | (precise ? 4 : 0);
-}
-inline int team_threads(int var) { return (var & 3) == 2 ? 512 : kThreads; }
-
-// 1 when a backward launch of (B, H) can accumulate ∂W_hh itself (dwpart / hsf / h0): one-row exact fp32 chains
-// at H = 512, on the 4-wave V1 form (DCA_TEAM_FUSED_DW=0 keeps the weight-gradient GEMM)
-extern "C" int dca_lstm_team_bwd_fuses_dw(int B, int H, int f32, int precise) {
-  static const bool off = [] { const char* e = getenv("DCA_TEAM_FUSED_DW"); return e && e[0] == '0'; }();
-  int nch, Bc, MT;
-  plan(B, nch, Bc, MT, f32);
-  return !off && H == 512 && (use_v1(f32, Bc, H, 1, precise) & 3) != 0 ? 1 : 0;
+  if (!(f32 && Bc <= 4 && !off)) return 0;
+  const int rows = Bc == 1 ? 0 : (Bc == 2 ? 32 : 64);         // VAR bits 5-6: 2 or 4 rows per chain
+  if (half && H == 512 && !precise) return 1 | 16 | rows;
+  return ((H == 512 && (v2 & (backward ? 2 : 1))) ? 2 : 1) | (precise ? 4 : 0) | rows;
 }
 
 // Workspace bytes (control block + per-team exchange buffers) for a launch of (B, H).
@@ -1141,7 +1156,7 @@ extern "C" hipError_t dca_lstm_team_fwd(const float* xp4, const void* whh, const
   unsigned long long* xg = reinterpret_cast<unsigned long long*>(ws);
   const int KS = H / 128;
 #define DCA_F(mt, ks, f, v)                                                                                     \
-  (lstm_team_fwd_kernel<mt, ks, f, v><<<kMaxTeams * kT, team_threads(v), 0, stream>>>(xp4, whh, h0, c0, hs, hsf, cs, gates4, \
+  (lstm_team_fwd_kernel<mt, ks, f, v><<<kMaxTeams * team_size(v), team_threads(v), 0, stream>>>(xp4, whh, h0, c0, hs, hsf, cs, gates4, \
                                                                           hn, cn, xg, ctl, err, B, Bc, nch, S, sb, \
                                                                           st, trace, team_knobs(), bias4, rst),    \
    hipGetLastError())
@@ -1154,10 +1169,8 @@ extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, c
                                         float* dh0, float* dc0, void* ctl_mem, void* ws, size_t ws_bytes,
                                         unsigned* err, int B, int S, int H, int time_major, hipStream_t stream,
                                         unsigned long long* trace, short* dg16, float* dbpart, int f32, int precise,
-                                        const unsigned char* rst, const float* hsf, const float* h0, float* dwpart) {
+                                        const unsigned char* rst) {
   if (B < 1 || S < 1 || S >= 65534 || (H != 128 && H != 256 && H != 512)) return hipErrorInvalidValue;
-  if (dwpart != nullptr && (hsf == nullptr || h0 == nullptr || !dca_lstm_team_bwd_fuses_dw(B, H, f32, precise)))
-    return hipErrorInvalidValue;
   if (dgates4 == nullptr && dg16 == nullptr) return hipErrorInvalidValue;
   if (f32 && dgates4 == nullptr) return hipErrorInvalidValue;
   if (ws_bytes < dca_lstm_team_workspace(B, H, 1, f32) || ctl_mem == nullptr) return hipErrorInvalidValue;
@@ -1168,15 +1181,11 @@ extern "C" hipError_t dca_lstm_team_bwd(const float* dhs, const float* gates4, c
   i32x4* xb = reinterpret_cast<i32x4*>(ws);
   const int KS = H / 128;
 #define DCA_B(mt, ks, f, v)                                                                                        \
-  (lstm_team_bwd_kernel<mt, ks, f, v><<<kMaxTeams * kT, team_threads(v), 0, stream>>>(dhs, gates4, cs, c0, dhn, dcn, whh,      \
+  (lstm_team_bwd_kernel<mt, ks, f, v><<<kMaxTeams * team_size(v), team_threads(v), 0, stream>>>(dhs, gates4, cs, c0, dhn, dcn, whh,      \
                                                                           dgates4, dh0, dc0, xb, ctl, err, B, Bc,  \
                                                                           nch, S, sb, st, trace, dg16, dbpart,      \
-                                                                          team_knobs(), rst, hsf, h0, dwpart),     \
+                                                                          team_knobs(), rst),                      \
    hipGetLastError())
-  if (dwpart != nullptr) {   // the fused-∂W_hh V1 instances (checked above: H = 512, one-row fp32 chains)
-    if (precise) return DCA_B(1, 4, true, 13);
-    return DCA_B(1, 4, true, 9);
-  }
   DCA_TEAM_DISPATCH(MT, KS, f32 ? 1 : 0, use_v1(f32, Bc, H, 1, precise), DCA_B)
 #undef DCA_B
 }

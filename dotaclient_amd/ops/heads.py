@@ -1,20 +1,14 @@
-"""Autograd wrapper for the fused heads + loss kernel (ops/csrc/heads_loss.hip).
-
-``heads_loss(xh, wcat, bcat, emb, batch, cfg, ...)`` computes, for N = B·S rows,
-``z = xh·Wcatᵀ + bcat`` (ONE bf16 GEMM with fp32 output for all five heads: pointer query, enum, x, y, value), then the
-fused kernel evaluates the masked log-softmaxes, the PPO (or reference VPG) objective, entropies and the value loss
-and writes ∂L/∂z and ∂L/∂(pointer logits) in the same pass. Backward is two GEMMs plus the rank-1 pointer-key
-gradient ∂L/∂emb[n,u] = dtl[n,u]·q[n].
+"""Host-side companions of the fused heads + loss kernel (ops/csrc/heads_loss.hip): the experience-only loss
+normalisers (:func:`batch_norms`) and the loss / metrics assembly from the kernel's partial sums
+(:func:`assemble_loss`; the learner's direct step does the same on the device, glue.hip loss_assemble). The kernel
+evaluates the masked log-softmaxes, the PPO (or reference VPG) objective, entropies and the value loss for N = B·S rows
+of head logits ``z = h·Wcatᵀ + bcat`` and writes ∂L/∂z and ∂L/∂(pointer logits) in the same pass.
 
 Column layout of z / Wcat (``LDZ`` = 160): ``[q 0:128 | enum 128:131 | x 131:140 | y 140:149 | value 149 | pad]``.
 """
 from __future__ import annotations
 
-from typing import Dict
-
 import torch
-
-from . import require
 
 LDZ = 160
 Q = 128
@@ -74,54 +68,3 @@ def assemble_loss(part: torch.Tensor, norms: torch.Tensor, cfg, ret: torch.Tenso
     for k, e in zip(['enum', 'x', 'y', 'target_unit'], ent_h):
         metrics[f'entropy/{k}'] = e.detach()
     return loss, metrics
-
-
-class _HeadsLoss(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, xh, wcat, bcat, emb, actions, masks, adv, ret, logp_old, nret, norms, algo, compat_value_bug,
-                S, B, clip_eps, ent_coef, vf_coef):
-        C = require()
-        N = xh.shape[0]
-        x16 = xh.to(torch.bfloat16)
-        w16 = wcat.detach().to(torch.bfloat16)
-        z = torch.mm(x16, w16.t(), out_dtype=torch.float32) + bcat.detach()
-        dz, dtl, part, logp = C.heads_loss(z, emb.contiguous(), actions, masks, adv, ret, logp_old, nret, norms,
-                                           algo, compat_value_bug, S, B, clip_eps, ent_coef, vf_coef)
-        ctx.save_for_backward(dz, dtl, z, x16, w16)
-        ctx.mark_non_differentiable(part, logp, z)
-        return part.sum(0), logp, z
-
-    @staticmethod
-    def backward(ctx, gpart, _glogp, _gz):
-        dz, dtl, z, x16, w16 = ctx.saved_tensors
-        # The loss is a fixed linear functional of `part` assembled by the caller, which passes its weight
-        # through gpart[15] (an unused slot) — see heads_loss(): loss = Σ part·coef, coef[15] = 1 marks it.
-        g = gpart[15]
-        dZ = dz * g
-        d16 = dZ.to(torch.bfloat16)
-        dxh = torch.mm(d16, w16, out_dtype=torch.float32)
-        dw = torch.mm(d16.t(), x16, out_dtype=torch.float32)
-        db = dZ.sum(0)
-        demb = ((dtl * g).unsqueeze(-1) * z[:, :Q].unsqueeze(1)).to(torch.bfloat16)
-        return (dxh, dw, db, demb) + (None,) * 14
-
-
-def heads_loss(xh: torch.Tensor, wcat: torch.Tensor, bcat: torch.Tensor, emb: torch.Tensor,
-               batch: Dict[str, torch.Tensor], cfg, S: int):
-    """Returns (loss scalar, metrics dict of device scalars, per-row joint logp)."""
-    N = xh.shape[0]
-    actions = batch['actions'].reshape(N, -1).contiguous()
-    masks = batch['masks'].reshape(N, -1).contiguous()
-    algo = 0 if cfg.algo == 'ppo' else 1
-    ret = batch['ret'].reshape(N).float().contiguous()
-    norms = batch_norms(actions, ret, cfg.compat_value_bug and algo == 1, S)
-    zeros = torch.zeros(N, device=xh.device)
-    adv = batch['adv'].reshape(N).contiguous() if 'adv' in batch else zeros
-    lpo = batch['logp_old'].reshape(N).contiguous() if 'logp_old' in batch else zeros
-    nret = batch['norm_ret'].reshape(N).contiguous() if 'norm_ret' in batch else zeros
-    B = N // S
-    part, logp, z = _HeadsLoss.apply(xh, wcat, bcat, emb, actions, masks, adv, ret, lpo, nret, norms, algo,
-                                     bool(cfg.compat_value_bug), S, B, float(cfg.clip_eps), float(cfg.entropy_coef),
-                                     float(cfg.vf_coef))
-    loss, metrics = assemble_loss(part, norms, cfg, ret, N, S)
-    return loss, metrics, logp

@@ -1,34 +1,22 @@
-"""Autograd wrapper around the persistent LSTM recurrence kernels (ops/csrc/lstm.hip).
+"""Autograd wrapper around the XCD-team persistent LSTM recurrence kernels (ops/csrc/lstm_team.hip).
 
 ``lstm_sequence(x, w_ih, w_hh, b_ih, b_hh, h0, c0)`` is a drop-in for a single-layer ``nn.LSTM`` (batch_first,
 PyTorch gate order i, f, g, o) returning ``(out (B,S,H) f32, h_n, c_n)``:
 
 * the input projection ``x·W_ihᵀ + b_ih + b_hh`` for all timesteps is one bf16 GEMM with fp32 output (hipBLASLt);
-* the recurrence runs in ONE persistent launch per ≤64-sequence chunk (``_C.lstm_fwd``), saving the activated gates
-  and cell states for backward;
-* backward runs the reverse recurrence in one launch (``_C.lstm_bwd``) producing ∂L/∂gates for every step, then the
-  weight gradients are plain GEMMs over all B·S rows: dW_ih = dGᵀx, dW_hh = dGᵀh_{t-1}, db = ΣdG, dx = dG·W_ih.
-
-Two kernel families implement the recurrence (``impl()``, env ``DCA_LSTM_IMPL``):
-
-* ``team`` (default, ops/csrc/lstm_team.hip): 32 workgroups of ONE XCD per sequence chain, exchanging the step
-  state through that XCD's L2; gates in unit-major (B,S,H,4) layout;
-* ``ring`` (ops/csrc/lstm.hip): 64+ workgroups across all XCDs, cross-fabric granule hand-off (fallback).
+* the recurrence runs in ONE persistent launch (``_C.lstm_team_fwd``): 32 workgroups of ONE XCD per sequence chain,
+  exchanging the step state through that XCD's L2, gates in unit-major (B,S,H,4) layout; it saves the activated
+  gates and cell states for backward;
+* backward runs the reverse recurrence in one launch (``_C.lstm_team_bwd``) producing ∂L/∂gates for every step, then
+  the weight gradients are plain GEMMs over all B·S rows: dW_ih = dGᵀx, dW_hh = dGᵀh_{t-1}, db = ΣdG, dx = dG·W_ih.
+(A cross-XCD "ring" recurrence — every hand-off over the Infinity Fabric — measured 2.5-3 µs per step against the
+team kernel's ≈1.3-1.5 µs and was removed in round 5.)
 """
 from __future__ import annotations
-
-import os
 
 import torch
 
 from . import require
-
-
-def impl() -> str:
-    v = os.environ.get('DCA_LSTM_IMPL', 'team')
-    if v not in ('team', 'ring'):
-        raise ValueError(f'DCA_LSTM_IMPL must be team or ring, got {v!r}')
-    return v
 
 
 def gate_perm(H: int, device) -> torch.Tensor:
@@ -77,24 +65,10 @@ class _Recurrence(torch.autograd.Function):
         whh16 = w_hh.detach().to(torch.bfloat16).contiguous()
         B, S, G4 = xp.shape
         H = G4 // 4
-        ctx.team = impl() == 'team'
         ctx.err = err
-        if ctx.team:
-            xp4 = xp.view(B, S, 4, H).transpose(2, 3).contiguous()
-            hs16, hsf, cs, gates4, hn, cn = team_fwd(C, xp4, whh16, h0, c0, err, True)
-            ctx.save_for_backward(gates4, cs, c0, whh16, hs16, h0)
-            ctx.mark_non_differentiable(hs16)
-            return hsf, hn, cn, hs16
-        MAX_B = C.lstm_max_batch(w_hh.shape[1])
-        outs = []
-        for s in range(0, B, MAX_B):
-            e = min(B, s + MAX_B)
-            outs.append(C.lstm_fwd(xp[s:e].contiguous(), whh16, h0[s:e].contiguous(), c0[s:e].contiguous(), err,
-                                   True))
-        hs16, hsf, cs, gates, hn, cn = (torch.cat([o[i] for o in outs]) if len(outs) > 1 else outs[0][i]
-                                        for i in range(6))
-        ctx.save_for_backward(gates, cs, c0, whh16, hs16, h0)
-        ctx.err = err
+        xp4 = xp.view(B, S, 4, H).transpose(2, 3).contiguous()
+        hs16, hsf, cs, gates4, hn, cn = team_fwd(C, xp4, whh16, h0, c0, err, True)
+        ctx.save_for_backward(gates4, cs, c0, whh16, hs16, h0)
         ctx.mark_non_differentiable(hs16)
         return hsf, hn, cn, hs16
 
@@ -106,25 +80,10 @@ class _Recurrence(torch.autograd.Function):
         dhs = dhs.contiguous() if dhs is not None else torch.zeros_like(cs)
         dhn = None if dhn is None else dhn.contiguous()
         dcn = None if dcn is None else dcn.contiguous()
-        if ctx.team:
-            dg4, dh0, dc0 = team_bwd(C, dhs, gates, cs, c0, dhn, dcn, whh16, ctx.err)
-            dgates = dg4.permute(0, 1, 3, 2).reshape(B, S, 4 * H)
-            hprev = torch.cat([h0.to(torch.bfloat16).unsqueeze(1), hs16[:, :-1]], dim=1).reshape(B * S, H)
-            dw_hh = _mm_f32(dgates.reshape(B * S, 4 * H).t(), hprev)
-            return dgates, dw_hh, dh0, dc0, None
-        MAX_B = C.lstm_max_batch(H)
-        outs = []
-        for s in range(0, B, MAX_B):
-            e = min(B, s + MAX_B)
-            outs.append(C.lstm_bwd(dhs[s:e], gates[s:e], cs[s:e], c0[s:e].contiguous(),
-                                   None if dhn is None else dhn[s:e].contiguous(),
-                                   None if dcn is None else dcn[s:e].contiguous(), whh16, ctx.err))
-        dgates, dh0, dc0 = (torch.cat([o[i] for o in outs]) if len(outs) > 1 else outs[0][i] for i in range(3))
-        # dW_hh = Σ_t dG_tᵀ h_{t-1}
+        dg4, dh0, dc0 = team_bwd(C, dhs, gates, cs, c0, dhn, dcn, whh16, ctx.err)
+        dgates = dg4.permute(0, 1, 3, 2).reshape(B, S, 4 * H)
         hprev = torch.cat([h0.to(torch.bfloat16).unsqueeze(1), hs16[:, :-1]], dim=1).reshape(B * S, H)
-        dg2 = dgates.reshape(B * S, 4 * H)
-        dw_hh = _mm_f32(dg2.t(), hprev)
-        ctx.dgates = None
+        dw_hh = _mm_f32(dgates.reshape(B * S, 4 * H).t(), hprev)
         return dgates, dw_hh, dh0, dc0, None
 
 

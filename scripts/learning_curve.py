@@ -30,6 +30,9 @@ def main(argv=None):
     ap.add_argument('--pack', type=int, default=1)
     ap.add_argument('--seed', type=int, default=7)
     ap.add_argument('--out', default='gpurun_out/learning_curve.jsonl')
+    ap.add_argument('--save-model', default=None, help='write the final weights here (state_dict file)')
+    ap.add_argument('--eval-precision', default='fp32', choices=['fp32', 'bf16', 'fp8'])
+    ap.add_argument('--mode', default='1v1', choices=['1v1', '5v5'])
     ap.add_argument('--device', default='cuda')
     a = ap.parse_args(argv)
     from dotaclient_amd.learner.curve import run_learning_curve
@@ -43,7 +46,8 @@ def main(argv=None):
                            precision=a.precision, backend=a.backend, games=a.games, threads=a.threads,
                            seq_len=a.seq_len, batch_size=a.batch_size, seq_per_epoch=a.seq_per_epoch, lr=a.lr,
                            entropy_coef=a.entropy_coef, max_dota_time=a.max_dota_time, pack=bool(a.pack),
-                           seed=a.seed, device=a.device, on_row=emit)
+                           seed=a.seed, device=a.device, on_row=emit, save_model=a.save_model,
+                           eval_precision=a.eval_precision, mode=a.mode)
 
 
 if __name__ == '__main__':

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-timestep latency of the persistent LSTM recurrence kernels (forward / backward) on one GPU, for both kernel
-families (team = XCD-local, ring = cross-XCD). Prints one JSON line per configuration."""
+family (the XCD-local team kernels). Prints one JSON line per configuration."""
 import json
 import sys
 import time
@@ -30,22 +30,16 @@ def bench(B, S, H, reps=5, impl='team'):
     h0 = torch.zeros(B, H, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
     dh = torch.randn(B, S, H, device=dev)
-    if impl == 'team':
-        xp = torch.randn(B, S, H, 4, device=dev) * 0.5
-        out = C.lstm_team_fwd(xp, whh, h0, h0, err, team_ctl(), True)
-        tf = _time(lambda: C.lstm_team_fwd(xp, whh, h0, h0, err, team_ctl(), True), reps)
-        tb = _time(lambda: C.lstm_team_bwd(dh, out[3], out[2], h0, None, None, whh, err, team_ctl()), reps)
-    else:
-        xp = torch.randn(B, S, 4 * H, device=dev) * 0.5
-        out = C.lstm_fwd(xp, whh, h0, h0, err, True)
-        tf = _time(lambda: C.lstm_fwd(xp, whh, h0, h0, err, True), reps)
-        tb = _time(lambda: C.lstm_bwd(dh, out[3], out[2], h0, None, None, whh, err), reps)
+    xp = torch.randn(B, S, H, 4, device=dev) * 0.5
+    out = C.lstm_team_fwd(xp, whh, h0, h0, err, team_ctl(), True)
+    tf = _time(lambda: C.lstm_team_fwd(xp, whh, h0, h0, err, team_ctl(), True), reps)
+    tb = _time(lambda: C.lstm_team_bwd(dh, out[3], out[2], h0, None, None, whh, err, team_ctl()), reps)
     return {'impl': impl, 'B': B, 'S': S, 'H': H, 'fwd_us_per_step': tf / S * 1e6, 'bwd_us_per_step': tb / S * 1e6,
             'err': int(err.item())}
 
 
 if __name__ == '__main__':
-    impls = sys.argv[1:] or ['team', 'ring']
+    impls = sys.argv[1:] or ['team']
     for impl in impls:
         for H in (512, 128):
             for B in (8, 16, 32, 64, 128, 256):

@@ -169,3 +169,21 @@ def test_vec_actor_runs_fp8_policy(gpu_ops):
     r = measure_vec_actor(pol, 'cuda', n_games=64, steps=40, warmup=4, threads=4, rollout_size=16,
                           max_dota_time=30.0, precision='fp8')
     assert r['precision'] == 'fp8' and r['steps_per_s'] > 0 and r['rollouts_per_s'] > 0, r
+
+
+@pytest.mark.parametrize('mode', [0, 1])
+def test_core_weight_fragment_order(mode):
+    """actor_core.hip fragment order (actor/batched.py frag_weight): element j of lane l in k-group g of column tile
+    t is w[16t + (l & 15)][KG·g + (KG/4)·(l >> 4) + j] (KG = 16 fp32 / 32 bf16)."""
+    from dotaclient_amd.actor.batched import frag_weight
+    torch.manual_seed(0)
+    N, K = 48, 64
+    w = torch.randn(N, K)
+    f = frag_weight(w, mode)
+    kg, e = (16, 4) if mode == 0 else (32, 8)
+    ref = w if mode == 0 else w.to(torch.bfloat16)
+    f = f.view(N // 16, K // kg, 64, e)
+    for t, g, l, j in ((0, 0, 0, 0), (1, 2, 37, 3), (2, 1, 63, e - 1), (2, K // kg - 1, 17, 1)):
+        g = min(g, K // kg - 1)
+        assert f[t, g, l, j] == ref[16 * t + (l & 15), kg * g + (kg // 4) * (l >> 4) + j]
+    assert torch.equal(f.flatten().sort().values, ref.flatten().sort().values)

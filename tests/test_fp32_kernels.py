@@ -221,7 +221,7 @@ def _fp64_grads(pol, batch, lc):
     return float(loss), dict(zip(names, gs))
 
 
-def _step_grads(precision, preset, algo, B, S, seed=3, fp64=False):
+def _step_grads(precision, preset, algo, B, S, seed=3, fp64=False, vbug=False):
     from dotaclient_amd.learner.engine import Learner, LossConfig
     from dotaclient_amd.learner.synthetic import make_batch
     from dotaclient_amd.models.policy import Policy, get_config
@@ -230,7 +230,7 @@ def _step_grads(precision, preset, algo, B, S, seed=3, fp64=False):
     pol = Policy(cfg)
     ref = copy.deepcopy(pol)
     p0 = copy.deepcopy(pol) if fp64 else None
-    lc = LossConfig(algo=algo, vf_coef=0.5, entropy_coef=0.01)
+    lc = LossConfig(algo=algo, vf_coef=0.5, entropy_coef=0.01, compat_value_bug=vbug)
     fused = Learner(pol, lc, device='cuda', backend='fused', dp=False, precision=precision)
     oracle = Learner(ref, lc, device='cuda', backend='torch', dp=False, precision='fp32')
     batch = make_batch(B, S, cfg.layout, cfg.hidden if cfg.rnn == 'lstm' else None, device='cuda', seed=seed)

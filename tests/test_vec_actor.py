@@ -148,3 +148,16 @@ def test_vec_actor_gpu_graph_policy_replay_consistent(preset, mode):
         np.testing.assert_allclose(hs, r.hiddens, atol=5e-2 if mode == '1v1' else 1e-1)
         np.testing.assert_allclose(vals, r.values, atol=5e-2)
         np.testing.assert_allclose(lps, r.logp, atol=1e-1)
+
+
+def test_validation_vs_default_bot_5v5_cpu():
+    """The reference's validation agent (agent.py:905-927) for the 5v5 policy: five controlled heroes against five
+    default-bot heroes (native engine mode 3, sides alternating with the game serial), the reference's metrics."""
+    from dotaclient_amd.actor.validate import evaluate_vs_default_bot
+    from dotaclient_amd.models.policy import Policy, get_config
+    torch.manual_seed(0)
+    out = evaluate_vs_default_bot(Policy(get_config('5v5')), n_games=4, device='cpu', seed=3, max_dota_time=20.0,
+                                  threads=2, timeout=300)
+    assert out['games'] == 4
+    assert 0.0 <= out['game/win_rate'] <= 1.0 and out['game/steps'] > 10
+    assert 'game/rewards_sum' in out and 'game/rewards_lh' in out
