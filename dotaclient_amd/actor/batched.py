@@ -153,10 +153,10 @@ class GpuActorPolicy:
         self.d_snap = torch.zeros(n, 2, H, device=dev)
         self.o_snap = torch.zeros(n, 2, H, **pin)
         self._snap_n = 0
-        # the actor's step stream at high priority (DCA_ACTOR_STREAM_PRIORITY, torch convention: lower = higher): its
-        # short policy-step graphs are dispatched ahead of a learner training on the same GPU (one-GPU node loop,
-        # scripts/e2e_ab.py 15 1024,14: 1.276 / 1.305 M vs 1.242 / 1.259 M steps/s at the default priority)
-        self.stream = torch.cuda.Stream(device=dev, priority=int(os.environ.get('DCA_ACTOR_STREAM_PRIORITY', '-1')))
+        # the actor's step stream at high priority (torch convention: lower = higher): its short policy-step graphs are
+        # dispatched ahead of a learner training on the same GPU (one-GPU node loop, scripts/e2e_ab.py 15 1024,14:
+        # 1.276 / 1.305 M vs 1.242 / 1.259 M steps/s at the default priority)
+        self.stream = torch.cuda.Stream(device=dev, priority=-1)
 
     @torch.no_grad()
     def load_weights(self, policy_or_state):
@@ -392,8 +392,6 @@ class F32ActorPolicy(GpuActorPolicy):
         super().__init__(policy, n_slots, device=device, **kw)
 
 
-# fp8 encoder form of the actor step: the per-unit workgroup kernel (True) or the wave-parallel one (False)
-_FP8_ENC_PER_UNIT = os.environ.get('DCA_FP8_ENC_PER_UNIT', '0') == '1'
 
 
 def fp8_weight(w: torch.Tensor):
@@ -464,7 +462,7 @@ class Fp8ActorPolicy(GpuActorPolicy):
         counter) → sampling."""
         C, w, cfg = self.C, self.w, self.cfg
         x896, emb = C.encoder_fp8(self.d_units, self.d_env, w['w1'], w['b1'], w['wt8'], w['st8'], w['bt'], w['we'],
-                                  w['be'], list(cfg.layout.counts), per_unit=_FP8_ENC_PER_UNIT)
+                                  w['be'], list(cfg.layout.counts))
         if cfg.compat_bugs:
             x896[:, 768:896] = x896[:, 512:640]
         C.actor_fp8(x896, w['wpre8'], w['spre'], w['bpre32'], w['wg8'], w['sg'], w['bg'], w['wh8'], w['sh8'],

@@ -181,17 +181,15 @@ def _actor_process_main(addr: str, model: str, games: int, threads: int, seq_len
     the learner's rank 0 publishes (reference agent.py:855-902 with the model subscription of 198-223). It tears its
     threads down before returning, so the process exits with status 0.
 
-    The process runs at a lower CPU priority (``DCA_ACTOR_NICE``, default 5): actor and learner share the rank's
+    The process runs at a lower CPU priority (nice 5): actor and learner share the rank's
     CPU share, and when the learner's decode / stager threads lose the CPU to the actor's workers the queue
     overflows (drops) while the learner waits for its next staged iteration — actor work that is thrown away."""
     br = None
     try:
-        nice = int(os.environ.get('DCA_ACTOR_NICE', '5'))
-        if nice > 0:
-            try:
-                os.nice(nice)
-            except OSError:
-                pass
+        try:
+            os.nice(5)
+        except OSError:
+            pass
         from ..actor.vec import VecActor
         from ..actor.weights import WeightStore
         if device.startswith('cuda') and torch.device(device).index is not None:

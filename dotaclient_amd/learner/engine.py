@@ -46,9 +46,8 @@ _GRAPH_TOKENS = itertools.count(1)   # replay-graph cache tokens (Learner._repla
 
 
 def _capture_stream(device):
-    """The graph-capture stream (DCA_MAIN_PRIORITY=1: high priority, an A/B knob for the step's critical path)."""
-    pr = -1 if os.environ.get('DCA_MAIN_PRIORITY', '0') == '1' else 0
-    return torch.cuda.Stream(device=device, priority=pr)
+    """The graph-capture stream (default priority: high priority measured slower, profiles/r4_stream_priority_ab.txt)."""
+    return torch.cuda.Stream(device=device)
 
 
 @dataclass

@@ -87,13 +87,13 @@ class OptimizerConfig:
                                        #     the next iteration's decode with this one's training); 0: inline
     record_consumed: int = 0           # keep the keys (game, team, player, version, length) of the last N rollouts
                                        #     consumed (competing-consumer tests; 0 = off)
-    lookahead_ingest: bool = os.environ.get('DCA_LOOKAHEAD', '1') != '0'
+    lookahead_ingest: bool = True
     # non-compat: pack whole zero-state rollouts first-fit into the free tails of the iteration's sequences (episode
     # starts flagged, the recurrence resets h, c there) instead of padding each rollout to seq_len (learner/ingest.py)
     pack_sequences: bool = False
     # pipelined GPU learner with async_checkpoint: publish each iteration's weights right after its steps are queued
     # and finalise its metrics (the one device→host sync) during the NEXT iteration — no blocking sync per iteration
-    defer_metrics: bool = os.environ.get('DCA_DEFER_METRICS', '1') != '0'
+    defer_metrics: bool = True
                                        # pipelined GPU ingest: take and expand the NEXT iteration's staged rollouts
                                        #     while this iteration's steps run on the GPU (its host work then overlaps
                                        #     the training instead of leaving the GPU idle between iterations)

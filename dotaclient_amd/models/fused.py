@@ -136,10 +136,9 @@ class FusedPolicy:
 
     def side_stream(self):
         if getattr(self, '_side', None) is None:
-            import os
-            # DCA_SIDE_PRIORITY=1: the recurrence / weight-gradient side stream at high priority (A/B knob)
-            pr = -1 if os.environ.get('DCA_SIDE_PRIORITY', '0') == '1' else 0
-            self._side = torch.cuda.Stream(device=self.err.device, priority=pr)
+            # (default priority: either stream at high priority measured 0.7 ms per step slower under graph replay,
+            # profiles/r4_stream_priority_ab.txt)
+            self._side = torch.cuda.Stream(device=self.err.device)
         return self._side
 
     def use_pipeline(self) -> bool:

@@ -44,7 +44,7 @@ METRIC_NAMES = ['loss', 'policy_loss', 'entropy_loss', 'advantage_loss', 'entrop
 
 def _mm(a, b):
     """GEMM with fp32 output: bf16 operands on hipBLASLt's bf16 path, fp32 operands on its fp32 path (fast bf16x3-class
-    mode inside :func:`fused_step_tm` unless DCA_F32_GEMM=exact)."""
+    mode inside :func:`fused_step_tm` for the fp32 learner, exact for fp32-exact)."""
     return a @ b if a.dtype == torch.float32 else torch.mm(a, b, out_dtype=torch.float32)
 
 
@@ -221,55 +221,23 @@ class WeightImages:
         return self.views
 
 
-# fp32 learner: hipBLASLt's plain GEMMs (pre-RNN, input projection, heads, the ∂X products) in its fast fp32 mode
-# (``allow_tf32``; on gfx950 a bf16x3-class split product: 4.4e-6 relative error on an 11200×256×2048 product vs
-# 2.9e-7 exact, 58 vs 127 µs), the same accuracy class as the hand-written bf16x3 kernels. DCA_F32_GEMM=exact keeps
-# hipBLASLt's exact-f32 path.
-_F32_GEMM_FAST = os.environ.get('DCA_F32_GEMM', 'fast') != 'exact'
-# weight-gradient GEMMs of the recurrence and pre-RNN layer on the (then idle) recurrence stream, overlapped with the
-# ∂X chain of the main stream (DCA_WG_OVERLAP=0: everything on the main stream)
-_WG_OVERLAP = os.environ.get('DCA_WG_OVERLAP', '1') != '0'
-# single-graph step: the pre-RNN weight gradient (∂W_pre, ∂b_pre) on the main stream after the encoder backward
-# instead of queued behind ∂W_hh / ∂W_ih on the recurrence stream, whose exact GEMMs made the side stream the tail's
-# critical path. Measured (scripts/gpu_premain.sh, two same-box pairs): exact 5.560 / 5.573 → 5.514 / 5.530 ms;
-# bf16x3 4.896 / 4.892 → 4.921 / 4.911 ms (slower), so the default ('exact') applies it to the exact learner only.
-# DCA_PRE_ON_MAIN = 0 / 1 / exact.
-_PRE_ON_MAIN = os.environ.get('DCA_PRE_ON_MAIN', 'exact')
-# 5v5 fused path: ∂W_out on the main stream after the encoder backward (A/B knob DCA_WOUT_MAIN=1; measured slower:
-# 8.138 / 8.127 vs 8.098 / 8.102 ms, scripts/gpu_woutmain.sh)
-_WOUT_MAIN = os.environ.get('DCA_WOUT_MAIN', '0') == '1'
-# fp32 learner: the ∂X chain ∂pre = (∂G·W_ih)⊙[x>0], ∂x896 = ∂pre·W_pre as ONE hand-written MFMA kernel
-# (ops/csrc/dx_chain.hip) instead of two hipBLASLt GEMMs + a threshold_backward (DCA_DX_FUSED=0: the library path)
-_DX_FUSED = os.environ.get('DCA_DX_FUSED', '1') != '0'
-# fp32 5v5: the entity-attention block forward (LN, QKV, attention, out-projection + residual, pools) as ONE kernel
-# (ops/csrc/attn_block.hip) instead of ln_fwd + hipBLASLt + attn_fwd + hipBLASLt + pool (DCA_ATTN_FUSED=0)
-_ATTN_FUSED = os.environ.get('DCA_ATTN_FUSED', '1') != '0'
-# fp32 5v5: the block BACKWARD (∂E1 routing, ∂O, attention backward, ∂Xn, LayerNorm backward) as ONE kernel
-# (ops/csrc/attn_block.hip) instead of demb + hipBLASLt + attn_bwd + hipBLASLt + ln_bwd (DCA_ATTN_BWD_FUSED=0).
-# Measured 1660 µs per step against 1858 µs for the five launches it replaces (5v5 step 8.11 vs 8.33 ms, same box;
-# profiles/r3_5v5_backward_fusions.md)
-_ATTN_BWD_FUSED = os.environ.get('DCA_ATTN_BWD_FUSED', '1') != '0'
-# fp32 5v5 (unfused backward): ∂Xn = ∂QKV·W_qkv with the LayerNorm backward as its epilogue, one hand-written kernel
-# instead of a hipBLASLt GEMM + ln_bwd. Opt-in (DCA_DXN_LN_FUSED=1): measured 1033 µs per step against 631 µs for
-# hipBLASLt (350) + ln_bwd (281) — one timestep row per workgroup leaves too few bytes in flight per CU
-_DXN_LN_FUSED = os.environ.get('DCA_DXN_LN_FUSED', '0') == '1'
-# fp32 learner: the forward chain x = relu(x896·W_preᵀ + b), xp = x·W_ihᵀ as ONE hand-written kernel (the ∂X
-# kernel's forward twin, ops/csrc/dx_chain.hip) instead of two hipBLASLt GEMMs (DCA_FWD_CHAIN=0)
-_FWD_CHAIN = os.environ.get('DCA_FWD_CHAIN', '1') != '0'
-# fp32 learner: the heads GEMM z = h·W_catᵀ + b and ∂h = ∂z·W_cat on the chain kernel's stages (W_cat padded to 256
-# rows, z / ∂z carried 256 wide) instead of hipBLASLt (DCA_HEADS_ROWMM=0)
-_HEADS_ROWMM = os.environ.get('DCA_HEADS_ROWMM', '1') != '0'
-# IEEE-fp32 learner: the recurrence's gate activations through the hardware exp / reciprocal (v_exp_f32 /
-# v_rcp_f32, ≈1-2 ulp; default) or libm expf / tanhf with an IEEE division (DCA_EXACT_ACT=libm). Both are products-
-# exact; measured at the deploy shape against float64 the two give the same worst tensor errors (PPO 2.50e-6 vs
-# 2.50e-6, VPG 1.264e-5 vs 1.265e-5 where torch-fp32 itself is at 1.24e-5) and the fast form is 0.5 ms per step
-# faster (5.70 vs 6.20 ms)
-_EXACT_LIBM_ACT = os.environ.get('DCA_EXACT_ACT', 'fast') == 'libm'
+# Fixed choices of the step, each measured against its alternative in earlier rounds (the alternatives were removed):
+# * the weight-gradient GEMMs of the recurrence and pre-RNN layer run on the (then idle) recurrence stream, beside the
+#   ∂X chain of the main stream; in the exact learner ∂W_pre / ∂b_pre go to the main stream after the encoder
+#   backward instead (5.514 vs 5.560 ms per step; the bf16x3 learner keeps them on the side stream: 4.911 vs 4.921);
+# * the fp32 forward chain relu(x896·W_preᵀ + b)·W_ihᵀ, the heads GEMM and its ∂X product, and the ∂X chain
+#   (∂G·W_ih)⊙[x>0]·W_pre are hand-written kernels (ops/csrc/dx_chain.hip), not vendor GEMMs;
+# * the fp32 5v5 attention block forward and backward are one kernel each (ops/csrc/attn_block.hip; the five-launch
+#   backward took 1858 vs 1660 µs), ∂W_out / ∂W_qkv on the side stream after the encoder backward (8.10 vs 8.13 ms);
+# * the exact recurrence's gate activations use the hardware exp / reciprocal: products-exact, the same worst
+#   tensor errors against float64 as libm expf / tanhf (PPO 2.50e-6 both), 0.5 ms per step faster.
 
 
 def fused_step_tm(fp, *args, **kw):
+    """:func:`_fused_step_tm` with torch's fp32 matmul mode pinned: exact in the IEEE-fp32 learner, the fast (bf16x3-
+    class) mode in the fp32 learner for the few torch GEMMs left (the multi-chunk heads products)."""
     exact = getattr(fp, 'exact', False)
-    if not (getattr(fp, 'fp32', False) and (exact or _F32_GEMM_FAST)):
+    if not getattr(fp, 'fp32', False):
         return _fused_step_tm(fp, *args, **kw)
     prev = torch.backends.cuda.matmul.allow_tf32
     torch.backends.cuda.matmul.allow_tf32 = not exact
@@ -329,32 +297,18 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         # 213 + 480 µs instead of 359 + 116 (copy, GEMM, bias pass) + 795 µs at N·U = 716 800 rows
         toff = fp.type_offset_list()
         bqkv = P['entity_attn.qkv.bias'].detach()
-        if _ATTN_FUSED:
-            # one kernel per step; E0' stays untouched (the LayerNorm backward's input), E1 is a new tensor
-            E0p = emb.view(N * U, 128)
-            if 'wq_f' in W:                    # hi / lo fragment images from the step's weight_prep launch
-                wq, wo = W['wq_f'], W['wo_f']
-            else:
-                wq = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.qkv.weight'].detach())]
-                wo = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.out.weight'].detach())]
-            arg = torch.empty(N, 6, 128, dtype=torch.uint8, device=dev)
-            Xn, ln_mu, ln_rs, QKV, Oat, lse, E1 = C.attn_block_fwd(
-                E0p, W['bout'], P['entity_attn.ln.weight'].detach(), P['entity_attn.ln.bias'].detach(), wq[0], wq[1],
-                bqkv, wo[0], wo[1], toff, x896, arg, bool(cfg.compat_bugs), 1e-5)
+        # one kernel per step; E0' stays untouched (the LayerNorm backward's input), E1 is a new tensor
+        E0p = emb.view(N * U, 128)
+        if 'wq_f' in W:                    # hi / lo fragment images from the step's weight_prep launch
+            wq, wo = W['wq_f'], W['wo_f']
         else:
-            E0b = emb.view(N * U, 128)
-            E0p = torch.empty_like(E0b)
-            Xn, ln_mu, ln_rs = C.ln_fwd(E0b, W['bout'], P['entity_attn.ln.weight'], P['entity_attn.ln.bias'], 1e-5,
-                                        e0_copy=E0p)
-            QKV = torch.mm(Xn, P['entity_attn.qkv.weight'].detach().t())
-            Oat, lse = C.attn_fwd(QKV, bqkv)
-            E1 = E0b.addmm_(Oat, P['entity_attn.out.weight'].detach().t())     # residual + out-projection, in place
-            arg = C.attn_pool(E1, toff, x896, bool(cfg.compat_bugs))            # pools of the attended embeddings
+            wq = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.qkv.weight'].detach())]
+            wo = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.out.weight'].detach())]
+        arg = torch.empty(N, 6, 128, dtype=torch.uint8, device=dev)
+        Xn, ln_mu, ln_rs, QKV, Oat, lse, E1 = C.attn_block_fwd(
+            E0p, W['bout'], P['entity_attn.ln.weight'].detach(), P['entity_attn.ln.bias'].detach(), wq[0], wq[1],
+            bqkv, wo[0], wo[1], toff, x896, arg, bool(cfg.compat_bugs), 1e-5)
         emb = E1.view(N, U, 128)
-        if _DXN_LN_FUSED and not _ATTN_BWD_FUSED:
-            # W_qkv as 16x16x16 B-fragment hi / lo images for the backward's ∂Xn + LayerNorm kernel (built here, off
-            # the backward's critical path)
-            wq4 = [_k16_order(t) for t in C.split_bf16x2(P['entity_attn.qkv.weight'].detach())]
     elif attn:
         # 5v5 entity attention (ops/csrc/attn.hip): emb = E0 + b_out here (bias folded into bt)
         toff = fp.type_offset_list()
@@ -374,7 +328,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         nil = wpre16.new_empty(0)
         x16, xp = C.pre_rnn_chain(x896, wpre16, nil, W['bpre16'], wih16, nil)
         xp4 = xp.view(S, B, H, 4) if not lin else None
-    elif f32 and _FWD_CHAIN:
+    elif f32:
         if 'pre_s' in W:                 # hi / lo images from the step's weight_prep launch
             fw1, fw2 = W['pre_s'], W['ih_s']
         else:
@@ -421,7 +375,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         for t0, t1 in ([] if lin else spans):
             o = team_fwd(C, xp4[t0:t1], whh16, h_c, c_c, fp.err, False, time_major=True,
                          hs_out=hs16[t0:t1], cs_out=cs[t0:t1], gates_out=gates4[t0:t1], bias4=bias_p,
-                         precise=exact and _EXACT_LIBM_ACT, reset=rst)
+                         reset=rst)
             h_c, c_c = o[4], o[5]
             e = torch.cuda.Event()
             e.record(sL)
@@ -429,7 +383,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     if lin:
         fwd_done.append(ready)
     dx_w = None
-    if f32 and _DX_FUSED and 'wpreT' in W:
+    if f32 and 'wpreT' in W:
         # weight operands of the fused ∂X kernel, split once per step into bf16 hi/lo images (exact: fp32 as is);
         # enqueued before the main stream waits on the forward recurrence, so they run beside it
         if exact:
@@ -446,7 +400,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         hw = (W['wcat_s'], W['wcatT_s'], W['bcat256'])
     else:
         hw = None
-    rowmm = one and f32 and _HEADS_ROWMM and hw is not None
+    rowmm = one and f32 and hw is not None
     for (t0, t1), done in zip(spans, fwd_done):
         main.wait_event(done)
         r0, r1 = t0 * B, t1 * B
@@ -466,7 +420,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         if first:
             dbcat = torch.empty(LDZ, device=dev)
         dzw = dz16[:, :LDZ] if rowmm else dz16           # (the heads' columns of the 256-wide ∂z)
-        if one and _WG_OVERLAP:
+        if one:
             # single chunk: the heads' weight gradient waits on the recurrence stream behind the backward
             # recurrence (off the path between the two recurrences; joined with the other weight gradients)
             dWcat = torch.empty(LDZ, H, device=dev)
@@ -498,7 +452,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     dgam = dbet = None
     first_attn = True
     side_after: List = []                # side-stream work enqueued after the encoder backward (5v5 fused path)
-    after_enc: List = []                 # main-stream work enqueued after the encoder backward (DCA_PRE_ON_MAIN)
+    after_enc: List = []                 # main-stream work enqueued after the encoder backward (exact ∂W_pre)
     if attn:
         dWout = torch.empty(128, 128, device=dev)
         dbout = torch.empty(128, device=dev)
@@ -526,7 +480,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             cinit = c0.contiguous() if t0 == 0 else cs[t0 - 1]
             o = team_bwd(C, dxh[t0:t1], gates4[t0:t1], cs[t0:t1], cinit, dh_n, dc_n, whh16, fp.err,
                          time_major=True, dg_out=dgates16[t0:t1], dg_bf16=not f32,
-                         want_dbias=True, precise=exact and _EXACT_LIBM_ACT, reset=rst)
+                         want_dbias=True, reset=rst)
             dh_n, dc_n = o[1], o[2]
             db = _acc(db, o[3])
             e = torch.cuda.Event()
@@ -539,7 +493,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     # single chunk: the recurrence stream (idle once the backward recurrence is done) takes the weight-gradient GEMMs
     # of W_hh, W_ih and the pre-RNN layer, off the critical ∂X chain (∂pre → ∂x896 → encoder backward) on the main
     # stream; the main stream joins it before the DP split point and before returning
-    wg_side = one and _WG_OVERLAP
+    wg_side = one
     wg_done = None
     for (t0, t1), done in zip(reversed(spans), bwd_done):
         main.wait_event(done)
@@ -568,7 +522,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         else:
             # ∂pre-activation of the pre-RNN layer: one GEMM (bf16 or exact f32), ReLU mask in one threshold_backward
             dpre16 = torch.ops.aten.threshold_backward(torch.mm(dG16, W['wihT16'].t()), x16[r0:r1], 0)
-        pre_main = wg_side and split is None and (_PRE_ON_MAIN == '1' or (_PRE_ON_MAIN == 'exact' and exact))
+        pre_main = wg_side and split is None and exact
         if pre_main:
             with torch.cuda.stream(sL):       # the side stream ends with ∂W_ih
                 wg_done = torch.cuda.Event()
@@ -601,7 +555,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             split()
             split = None
         demb_in = None
-        if attn32 and _ATTN_BWD_FUSED:
+        if attn32:
             # one kernel from ∂x896 / the pointer gradient to ∂E0; the two weight-gradient GEMMs over the N·U unit
             # rows (∂W_out = ∂E1ᵀ·O, ∂W_qkv = ∂QKVᵀ·Xn, with their bias column sums) go to the recurrence stream
             wot = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.out.weight'].detach().t().contiguous())]
@@ -616,45 +570,11 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
                 # enqueued AFTER the encoder backward below (side_after): issued here, the graph ran the two GEMMs
                 # (156 + 401 µs) and then the encoder backward strictly one after the other
                 sL.wait_stream(main)
-                if _WOUT_MAIN:
-                    # ∂W_out on the main stream after the encoder backward, ∂W_qkv beside it (balances the streams)
-                    side_after.append(lambda: gemm_tn(dQKV, Xn, out=dWqkv, colsum=dbqkv))
-                    after_enc.append(lambda: gemm_tn(dE1, Oat, out=dWout, colsum=dbout))
-                else:
-                    side_after.append(lambda: (gemm_tn(dE1, Oat, out=dWout, colsum=dbout),
-                                               gemm_tn(dQKV, Xn, out=dWqkv, colsum=dbqkv)))
+                side_after.append(lambda: (gemm_tn(dE1, Oat, out=dWout, colsum=dbout),
+                                           gemm_tn(dQKV, Xn, out=dWqkv, colsum=dbqkv)))
             else:
                 dWout = gemm_tn(dE1, Oat, colsum=dbout)
                 dWqkv = gemm_tn(dQKV, Xn, colsum=dbqkv)
-        elif attn32:
-            # the two weight-gradient GEMMs over the N·U unit rows (∂W_out = ∂E1ᵀ·O, ∂W_qkv = ∂QKVᵀ·Xn, with their
-            # bias column sums) run on the recurrence stream, off the ∂E1 → ∂O → attention → ∂Xn → LN → encoder
-            # chain (measured: 596 µs of the 5v5 step's critical path when they ran in line)
-            dE1 = C.attn_demb(dtl, z, dx896, arg, toff, bool(cfg.compat_bugs), True)
-            dbout = torch.empty(128, device=dev)
-            dbqkv = torch.empty(384, device=dev)
-            if wg_side:
-                sL.wait_stream(main)
-            with torch.cuda.stream(sL if wg_side else main):
-                dWout = gemm_tn(dE1, Oat, colsum=dbout)
-            dO = dE1 @ P['entity_attn.out.weight']
-            dQKV = C.attn_bwd(QKV, Oat, dO, lse, bqkv)
-            if wg_side:
-                sL.wait_stream(main)
-            with torch.cuda.stream(sL if wg_side else main):
-                dWqkv = gemm_tn(dQKV, Xn, colsum=dbqkv)
-                if wg_side:
-                    wg_done = torch.cuda.Event()
-                    wg_done.record(sL)
-            if _DXN_LN_FUSED:
-                # ∂Xn = ∂QKV·W_qkv and the LayerNorm backward in one launch (∂Xn never goes to HBM)
-                demb_in, lnsum = C.attn_dxn_ln_bwd(dQKV, wq4[0], wq4[1], E0p, W['bout'], ln_mu, ln_rs,
-                                                   P['entity_attn.ln.weight'].detach(), dE1, toff)
-                dgam, dbet, dbt_attn = lnsum[:128], lnsum[128:256], lnsum[256:].view(6, 128)
-            else:
-                dXn = dQKV @ P['entity_attn.qkv.weight']
-                demb_in, dgam, dbet, dbt_attn = C.ln_bwd(dXn, E0p, W['bout'], P['entity_attn.ln.weight'], ln_mu,
-                                                         ln_rs, dE1, fp.unit_types(dev))
         elif attn:
             # attention block backward over this chunk's rows (unit rows r0·U … r1·U)
             a0, a1 = r0 * U, r1 * U

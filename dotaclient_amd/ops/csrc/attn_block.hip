@@ -85,11 +85,9 @@ __device__ __forceinline__ bf16x8 gfrag(const short* __restrict__ w, int m0, int
   return *reinterpret_cast<const bf16x8*>(w + ((size_t)((m0 >> 4) * (kD / 32) + (k0 >> 5)) * 64 + lane) * 8);
 }
 
-// MINB: workgroups per CU the register budget is cut for (2: 256 VGPRs; 1: 512, one row in flight per CU with the
-// phase-B weight fragments double-buffered one k-step ahead — DCA_ATTN_FWD_1WG=1, an A/B knob). Measured slower:
-// 5v5 step 8.45 vs 8.15 ms (two rows in flight per CU hide more than the prefetch does).
-template <int MINB>
-__global__ __launch_bounds__(256, MINB) void attn_block_fwd_f32_kernel(BlockArgs P) {
+// Two rows in flight per CU (256 VGPRs). (Measured slower and removed: one row per CU with the phase-B weight
+// fragments double-buffered one k-step ahead — 5v5 step 8.45 vs 8.15 ms.)
+__global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P) {
   __shared__ __attribute__((aligned(16))) short img_h[kU * kPX], img_l[kU * kPX];   // Xn, then O (hi / lo)
   __shared__ __attribute__((aligned(16))) float e1s[kU * kPE];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, kg = lane >> 4, li = lane & 15;
@@ -156,43 +154,7 @@ __global__ __launch_bounds__(256, MINB) void attn_block_fwd_f32_kernel(BlockArgs
       kt[c][a] = f32x4{0.f, 0.f, 0.f, 0.f};
       vv[a][c] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-  if constexpr (MINB == 1) {
-    // one workgroup per CU: the 12 weight fragments of k-step ks+1 load while ks computes (double-buffered)
-    bf16x8 wb[2][2][6];
-    auto wload = [&](bf16x8 (&w)[2][6], int ks) {
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const int rq = kHd * h + 16 * c;
-        w[c][0] = gfrag(P.wqh, rq, 32 * ks, lane);
-        w[c][1] = gfrag(P.wql, rq, 32 * ks, lane);
-        w[c][2] = gfrag(P.wqh, 128 + rq, 32 * ks, lane);
-        w[c][3] = gfrag(P.wql, 128 + rq, 32 * ks, lane);
-        w[c][4] = gfrag(P.wqh, 256 + rq, 32 * ks, lane);
-        w[c][5] = gfrag(P.wql, 256 + rq, 32 * ks, lane);
-      }
-    };
-    wload(wb[0], 0);
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      if (ks + 1 < 4) wload(wb[(ks + 1) & 1], ks + 1);
-      bf16x8 xh[4], xl[4];
-#pragma unroll
-      for (int a = 0; a < 4; ++a) {
-        xh[a] = frag(img_h, kPX, 16 * a, 32 * ks, lane);
-        xl[a] = frag(img_l, kPX, 16 * a, 32 * ks, lane);
-      }
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        const bf16x8(&w)[6] = wb[ks & 1][c];
-#pragma unroll
-        for (int a = 0; a < 4; ++a) {
-          qt[c][a] = mfma3(w[0], w[1], xh[a], xl[a], qt[c][a]);
-          kt[c][a] = mfma3(w[2], w[3], xh[a], xl[a], kt[c][a]);
-          vv[a][c] = mfma3(xh[a], xl[a], w[4], w[5], vv[a][c]);
-        }
-      }
-    }
-  } else {
+  {
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
     bf16x8 xh[4], xl[4];
@@ -401,8 +363,8 @@ __global__ __launch_bounds__(256, MINB) void attn_block_fwd_f32_kernel(BlockArgs
 //      colsum_rows_kernel in a fixed order.
 // LDS: 4 slots of a 64 × 132 fp32 image (135 KB) — phase 0/1 slot 0 = ∂E1, phase 2 slot h = wave h's ∂Oᵀ and ∂Sᵀ
 // images, phase 3 slot h = wave h's ∂Xn partial, phase 4 slots 0-2 = the partial sums — one workgroup per CU.
-// Measured at N = 11 200 (5v5 learner step): 1936 µs, against 1858 µs for the five launches it replaces, so the
-// learner keeps those (models/pipelined.py, opt-in DCA_ATTN_BWD_FUSED=1). 405 registers (no spills) and 135 KB of
+// Measured at N = 11 200 (5v5 learner step): first 1936 µs against 1858 µs for the five launches it replaced; after
+// the round-3 operand prefetch and interleaved partial sums 1647 µs, the learner's path since. 405 registers (no spills) and 135 KB of
 // LDS leave one wave per SIMD and one row in flight per CU: ≈44 µs per row, the sum of each phase's exposed memory
 // round trips (∂E1 inputs, W_out fragments, O / LSE / QKV rows, W_qkv fragments, E0' rows). Making it pay needs
 // rows in flight per CU — a persistent form prefetching row n+1's operands during row n, or two waves per head.
@@ -867,152 +829,8 @@ __global__ __launch_bounds__(256) void colsum_rows_kernel(const float* __restric
     out[(size_t)g * W + c] = ((red[0][threadIdx.x] + red[1][threadIdx.x]) + red[2][threadIdx.x]) + red[3][threadIdx.x];
 }
 
-// =============================================================================================================
-// ∂Xn GEMM + LayerNorm backward of the fp32 5v5 block in ONE launch (the learner's unfused backward chain: demb →
-// ∂O GEMM → attn_bwd → THIS): ∂Xn = ∂QKV·W_qkv (16x16x16 bf16x3, K = 384) never goes to HBM; the epilogue is the
-// LayerNorm backward + residual of ln_bwd_kernel, ∂E0 = ∂E1 + rstd·(g − mean(g) − x̂·mean(g∘x̂)), g = ∂Xn∘γ, and the
-// row's [∂γ | ∂β | ∂b_τ] partial. Replaces a hipBLASLt GEMM (reads ∂QKV, writes ∂Xn) and ln_bwd (reads ∂Xn again).
-// One 256-thread workgroup per timestep row: wave h takes head h's 96 ∂QKV columns (all 24 of its A-fragment loads in
-// flight at once; no ∂QKV byte read twice) and computes that head's partial ∂Xn over all 128 columns; the four
-// partials are added into one 64 × 132 fp32 LDS image in a fixed wave order (deterministic), which then serves the
-// row-wise LayerNorm reductions (34 KB of LDS, two waves per SIMD). (A first form — wave w owning 32 output columns
-// over the full K, so each ∂QKV row was read by all four waves in 64-B pieces — measured 1579 µs.) Measured 1033 µs
-// at N = 11 200 against 631 µs for hipBLASLt's ∂Xn GEMM (350, big row tiles) + ln_bwd (281): opt-in in the learner
-// (DCA_DXN_LN_FUSED=1) — like the fused block backward, a row per workgroup keeps too few bytes in flight per CU.
-struct DxnArgs {
-  const float* dqkv; const short* wq4h; const short* wq4l;       // (N·64, 384), W_qkv k16-fragment images
-  const float* e0; const float* bout; const float* mu; const float* rs; const float* gamma; const float* de1;
-  float* de0; float* part;
-  int off[7];
-};
-
-__global__ __launch_bounds__(256, 2) void attn_dxn_ln_bwd_f32_kernel(DxnArgs P) {
-  __shared__ __attribute__((aligned(16))) float sm[kSlot];
-  const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, kg = lane >> 4, li = lane & 15;
-  const int n = blockIdx.x;
-  const size_t rbase = (size_t)n * kU;
-  {
-    // wave h: the head's 96 ∂QKV columns (q, k, v slices) as 16x16x16 A fragments, all 24 loads in flight at once
-    const int h = w;
-    bf16x4v ah[3][2][4], al[3][2][4];
-    {
-      f32x4 av[3][2][4];
-#pragma unroll
-      for (int x = 0; x < 3; ++x)
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int u4 = 0; u4 < 4; ++u4)
-            av[x][t][u4] = *reinterpret_cast<const f32x4*>(P.dqkv + (rbase + 16 * u4 + li) * 384 + 128 * x + kHd * h +
-                                                           16 * t + 4 * kg);
-#pragma unroll
-      for (int x = 0; x < 3; ++x)
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-          for (int u4 = 0; u4 < 4; ++u4) split4v(av[x][t][u4], ah[x][t][u4], al[x][t][u4]);
-    }
-    // partial ∂Xn of the head in two column halves; the four waves add theirs into the image in a fixed order
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      f32x4 acc[4][4];
-#pragma unroll
-      for (int u4 = 0; u4 < 4; ++u4)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[u4][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int x = 0; x < 3; ++x)
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const int rt = 8 * x + 2 * h + t;
-          bf16x4v bh[4], bl[4];
-#pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            bh[c] = gfrag4(P.wq4h, rt, 4 * half + c, lane);
-            bl[c] = gfrag4(P.wq4l, rt, 4 * half + c, lane);
-          }
-#pragma unroll
-          for (int u4 = 0; u4 < 4; ++u4)
-#pragma unroll
-            for (int c = 0; c < 4; ++c) acc[u4][c] = mfma3k16(ah[x][t][u4], al[x][t][u4], bh[c], bl[c], acc[u4][c]);
-        }
-#pragma unroll
-      for (int ww = 0; ww < 4; ++ww) {
-        if (w == ww) {
-#pragma unroll
-          for (int u4 = 0; u4 < 4; ++u4)
-#pragma unroll
-            for (int c = 0; c < 4; ++c)
-#pragma unroll
-              for (int r = 0; r < 4; ++r) {
-                float* d = &sm[(16 * u4 + 4 * kg + r) * kPT + 64 * half + 16 * c + li];
-                *d = ww == 0 ? acc[u4][c][r] : *d + acc[u4][c][r];
-              }
-        }
-        __syncthreads();
-      }
-    }
-  }
-  // LayerNorm backward + residual, 4 threads per unit row (32 columns each)
-  const int u = tid >> 2, c0 = 32 * (tid & 3);
-  const size_t row = rbase + u;
-  const float mu = P.mu[row], rs = P.rs[row];
-  float dxn[32], xh[32], de0v[32];
-  float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-  for (int j4 = 0; j4 < 8; ++j4) {
-    const int c = c0 + 4 * j4;
-    const float4 d4 = *reinterpret_cast<const float4*>(&sm[u * kPT + c]);
-    const float4 e = *reinterpret_cast<const float4*>(P.e0 + row * kD + c);
-    const float dv[4] = {d4.x, d4.y, d4.z, d4.w}, ev[4] = {e.x, e.y, e.z, e.w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const float x = (ev[q] - P.bout[c + q] - mu) * rs;
-      dxn[4 * j4 + q] = dv[q];
-      xh[4 * j4 + q] = x;
-      const float g = dv[q] * P.gamma[c + q];
-      s1 += g;
-      s2 += g * x;
-    }
-  }
-  s1 += __shfl_xor(s1, 1, 64);
-  s1 += __shfl_xor(s1, 2, 64);
-  s2 += __shfl_xor(s2, 1, 64);
-  s2 += __shfl_xor(s2, 2, 64);
-  s1 *= (1.f / kD);
-  s2 *= (1.f / kD);
-#pragma unroll
-  for (int j4 = 0; j4 < 8; ++j4) {
-    const int c = c0 + 4 * j4;
-    const float4 r1 = *reinterpret_cast<const float4*>(P.de1 + row * kD + c);
-    const float rv[4] = {r1.x, r1.y, r1.z, r1.w};
-    float o[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int j = 4 * j4 + q;
-      o[q] = rv[q] + rs * (dxn[j] * P.gamma[c + q] - s1 - xh[j] * s2);
-      de0v[j] = o[q];
-    }
-    *reinterpret_cast<float4*>(P.de0 + row * kD + c) = make_float4(o[0], o[1], o[2], o[3]);
-  }
-  // the row's partial [∂γ | ∂β | ∂b_τ]: three passes through the one image, fixed-order sums over the units
-#pragma unroll
-  for (int pass = 0; pass < 3; ++pass) {
-    __syncthreads();                                      // every thread is done with the image's last contents
-#pragma unroll
-    for (int j = 0; j < 32; ++j) sm[u * kPT + c0 + j] = pass == 0 ? dxn[j] * xh[j] : pass == 1 ? dxn[j] : de0v[j];
-    __syncthreads();
-    const int np = pass < 2 ? kD : 6 * kD;
-    for (int e = tid; e < np; e += 256) {
-      const int c = e & 127;
-      int u0 = 0, u1 = kU;
-      if (pass == 2) { u0 = P.off[e >> 7]; u1 = P.off[(e >> 7) + 1]; }
-      float v = 0.f;
-      for (int uu = u0; uu < u1; ++uu) v += sm[uu * kPT + c];
-      P.part[(size_t)n * kLnW + pass * kD + e] = v;
-    }
-  }
-}
+// (A fused ∂Xn GEMM + LayerNorm backward kernel for the unfused block backward measured 1033 vs 631 µs for the
+// two launches it replaced and was removed in round 5, with that backward chain.)
 
 
 }  // namespace
@@ -1027,9 +845,7 @@ extern "C" hipError_t dca_attn_block_fwd_f32(const float* e0, const float* bout,
               0.17677669529663687f /* 1/sqrt(32) */, eps};
   for (int i = 0; i < 7; ++i) a.off[i] = off[i];
   if (a.off[6] != kU) return hipErrorInvalidValue;
-  static const bool one = [] { const char* e = getenv("DCA_ATTN_FWD_1WG"); return e && e[0] == '1'; }();
-  if (one) hipLaunchKernelGGL(attn_block_fwd_f32_kernel<1>, dim3(N), dim3(256), 0, stream, a);
-  else hipLaunchKernelGGL(attn_block_fwd_f32_kernel<2>, dim3(N), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(attn_block_fwd_f32_kernel, dim3(N), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 
@@ -1059,22 +875,3 @@ extern "C" hipError_t dca_attn_block_bwd_f32(const float* dtl, const float* q, i
   return hipGetLastError();
 }
 
-// ∂Xn GEMM + LayerNorm backward (fp32 5v5 learner, unfused chain): part (N, 1024) / tmp (groups, 1024) workspaces,
-// sums (1024) = [∂γ | ∂β | ∂b_τ (6×128)]
-extern "C" hipError_t dca_attn_dxn_ln_bwd_f32(const float* dqkv, const short* wq4h, const short* wq4l, const float* e0,
-                                              const float* bout, const float* mu, const float* rs,
-                                              const float* gamma, const float* de1, const int* off, float* de0,
-                                              float* part, float* tmp, float* sums, int N, hipStream_t stream) {
-  if (N < 1) return hipSuccess;
-  DxnArgs a{dqkv, wq4h, wq4l, e0, bout, mu, rs, gamma, de1, de0, part, {0}};
-  for (int i = 0; i < 7; ++i) a.off[i] = off[i];
-  if (a.off[6] != kU) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(attn_dxn_ln_bwd_f32_kernel, dim3(N), dim3(256), 0, stream, a);
-  DCA_CHECK_LAUNCH();
-  const int G = dca_attn_block_bwd_groups(N);
-  const int per = (N + G - 1) / G;
-  hipLaunchKernelGGL(colsum_rows_kernel, dim3(kLnW / 64, G), dim3(256), 0, stream, part, N, kLnW, per, tmp);
-  DCA_CHECK_LAUNCH();
-  hipLaunchKernelGGL(colsum_rows_kernel, dim3(kLnW / 64, 1), dim3(256), 0, stream, tmp, G, kLnW, G, sums);
-  return hipGetLastError();
-}

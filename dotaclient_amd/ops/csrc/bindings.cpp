@@ -579,34 +579,6 @@ std::vector<torch::Tensor> attn_block_bwd(torch::Tensor dtl, torch::Tensor q, to
   return {de1, dqkv, de0, sums};
 }
 
-// ∂Xn = ∂QKV·W_qkv + LayerNorm backward in one launch (attn_block.hip). dqkv (N·64, 384) f32, W_qkv images in
-// 16x16x16 B-fragment order (bf16 hi / lo), e0 = E0', de1 = ∂E1. Returns (∂E0 (N·64, 128), [∂γ | ∂β | ∂b_τ] (1024)).
-std::vector<torch::Tensor> attn_dxn_ln_bwd(torch::Tensor dqkv, torch::Tensor wq4h, torch::Tensor wq4l,
-                                           torch::Tensor e0, torch::Tensor bout, torch::Tensor mu, torch::Tensor rs,
-                                           torch::Tensor gamma, torch::Tensor de1, std::vector<int64_t> type_off) {
-  CHECK_F32(dqkv); CHECK_BF16(wq4h); CHECK_BF16(wq4l); CHECK_F32(e0); CHECK_F32(bout); CHECK_F32(mu); CHECK_F32(rs);
-  CHECK_F32(gamma); CHECK_F32(de1);
-  check_type_off(type_off);
-  TORCH_CHECK(e0.numel() % (64 * 128) == 0, "attn_dxn_ln_bwd: e0 (N·64, 128)");
-  const int64_t N = e0.numel() / (64 * 128);
-  TORCH_CHECK(dqkv.numel() == N * 64 * 384 && de1.numel() == N * 64 * 128 && mu.numel() == N * 64 &&
-              rs.numel() == N * 64, "attn_dxn_ln_bwd: row shapes");
-  TORCH_CHECK(wq4h.numel() == 384 * 128 && wq4l.numel() == 384 * 128 && bout.numel() == 128 && gamma.numel() == 128,
-              "attn_dxn_ln_bwd: weight shapes");
-  int off[7];
-  for (int i = 0; i < 7; ++i) off[i] = (int)type_off[i];
-  auto o32 = e0.options();
-  auto de0 = torch::empty({N * 64, 128}, o32);
-  auto part = torch::empty({N, 1024}, o32);
-  auto tmp = torch::empty({(int64_t)dca_attn_block_bwd_groups((int)N), 1024}, o32);
-  auto sums = torch::empty({1024}, o32);
-  hip_check(dca_attn_dxn_ln_bwd_f32(ptr<float>(dqkv), ptr<short>(wq4h), ptr<short>(wq4l), ptr<float>(e0),
-                                    ptr<float>(bout), ptr<float>(mu), ptr<float>(rs), ptr<float>(gamma),
-                                    ptr<float>(de1), off, ptr<float>(de0), ptr<float>(part), ptr<float>(tmp),
-                                    ptr<float>(sums), (int)N, cur_stream()),
-            "dca_attn_dxn_ln_bwd_f32");
-  return {de0, sums};
-}
 
 // Returns / advantages over concatenated padded rollouts. rew (L,K) f32 and val (L) f32 (GAE; ignored for mode 0)
 // live on the GPU; the per-segment metadata is host data — off (nseg+1) i32 row offsets, seglen (nseg) i32 valid
@@ -1189,9 +1161,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "out-projection + residual + pools (-> xn, mean, rstd, qkv, o, lse, e1)");
   m.def("attn_block_bwd", &attn_block_bwd, "fused fp32 entity-attention block backward: demb + dO + attention "
         "backward + dXn + LayerNorm backward (-> de1, dqkv, de0, [dgamma | dbeta | dbt])");
-  m.def("attn_dxn_ln_bwd", &attn_dxn_ln_bwd, "fused fp32 dXn = dQKV·W_qkv + LayerNorm backward (-> de0, "
-        "[dgamma | dbeta | dbt])");
-  m.def("loss_prep", &loss_prep, "loss normalisers from one-hot action rows (graph-replayable)");
+    m.def("loss_prep", &loss_prep, "loss normalisers from one-hot action rows (graph-replayable)");
   m.def("loss_prep_ws_elems", &loss_prep_ws_elems, "int32 workspace elements of loss_prep");
   m.def("loss_assemble", &loss_assemble, "loss scalar + metrics from heads/loss partials", py::arg("part"),
         py::arg("norms"), py::arg("N"), py::arg("algo"), py::arg("ent_coef"), py::arg("vf_coef"), py::arg("out"),

@@ -141,7 +141,7 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
                                                         const void* __restrict__ w1l, const float* __restrict__ x,
                                                         const void* __restrict__ w2h, const void* __restrict__ w2l,
                                                         float* __restrict__ dpre, float* __restrict__ dx, int N,
-                                                        int K1, int X, int dbg) {
+                                                        int K1, int X) {
   using L = Lay<EXACT>;
   constexpr int ES = EXACT ? 4 : 2;                 // bytes per weight element in HBM
   __shared__ __attribute__((aligned(16))) char lds[L::BYTES];
@@ -169,8 +169,7 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
   // slab's loads), which serialised the ring
   auto load1 = [&](int slot, int k0) {
     const bool in = k0 < K1;
-    if (!(dbg & 8)) sa[slot] = __builtin_bit_cast(float4, ld16(rA, (in && a_off0 != kOob) ? a_off0 + k0 * 4 : kOob));
-    if (dbg & 16) return;
+    sa[slot] = __builtin_bit_cast(float4, ld16(rA, (in && a_off0 != kOob) ? a_off0 + k0 * 4 : kOob));
     if constexpr (EXACT) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) sb[slot][i] = ld16(rW1h, in ? b_off0 + (k0 + 4 * i) * 4 : kOob);
@@ -229,10 +228,9 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
       for (int i = 0; i < NI1; ++i) get_frag<EXACT>(base, L::A1, i * 16 + r16, q, fa[i]);
 #pragma unroll
       for (int j = 0; j < 2; ++j) get_frag<EXACT>(bb, L::B1, wc * 32 + j * 16 + r16, q, fb[j]);
-      if (!(dbg & 2)) mma_tiles<EXACT, NI1, 2>(fa, fb, acc);
-      else if (fa[0].hi[0] == 12345 && fb[0].hi[1] == 4321) acc[0][0][0] += 1.f;
+      mma_tiles<EXACT, NI1, 2>(fa, fb, acc);
       store1((d + 1) % RD, (d + 1) & 1);            // (after the last slab: zeros into a buffer nobody reads)
-      if (!(dbg & 1)) load1(d, (ks + RD) * BK);    // slot d held slab ks, stored at the previous iteration
+      load1(d, (ks + RD) * BK);                  // slot d held slab ks, stored at the previous iteration
       __syncthreads();
     }
   }
@@ -319,7 +317,7 @@ __global__ __launch_bounds__(NT, 1) void dpre_dx_kernel(const float* __restrict_
   }
 
   // ================= stage 2: dx (64 × X) = dpre · W_pre, 128-column chunks =================
-  if ((dbg & 4) || X == 0) return;                // (stage-1-only launch: X = 0)
+  if (X == 0) return;                             // (stage-1-only launch: X = 0)
   char* s2 = lds + L::D;
   constexpr int nk2 = P / BK;
   const int nchunk = X / XC, total = nchunk * nk2;   // multiple of RD (nk2 = 8)
@@ -443,12 +441,9 @@ extern "C" hipError_t dca_dpre_dx(const float* dG, const void* w1h, const void* 
     return hipErrorInvalidValue;
   if ((long long)N * K1 * 4 > 0x7fff0000LL) return hipErrorInvalidValue;      // buffer-resource range
   const int grid = (N + BM - 1) / BM;
-  // DCA_DX_DBG (microbenchmark knob, scripts/dx_bench.py): bit 0 no global loads past the prologue, bit 1 no MFMA,
-  // bit 2 stage 1 only, bit 3 no dG loads, bit 4 no weight loads (stage 1)
-  static const int dbg = [] { const char* e = getenv("DCA_DX_DBG"); return e ? atoi(e) : 0; }();
 #define DCA_DX_LAUNCH(EX, EP)                                                                                    \
   hipLaunchKernelGGL((dpre_dx_kernel<EX, EP>), dim3(grid), dim3(NT), 0, stream, dG, w1h, w1l, x, w2h, w2l, dpre, dx, \
-                     N, K1, X, dbg)
+                     N, K1, X)
   if (exact) {
     if (epi == 0) DCA_DX_LAUNCH(true, 0);
     else if (epi == 1) DCA_DX_LAUNCH(true, 1);

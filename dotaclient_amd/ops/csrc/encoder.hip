@@ -1167,133 +1167,8 @@ __device__ __forceinline__ void xb_build(const FbBuild& b, const float* slot, in
   *reinterpret_cast<f32x4*>(it + (16 * wv + i) * kXT + 4 * kg) = v;
 }
 
-template <bool COMPAT>
-__global__ __launch_bounds__(512, 1) void encoder_bwd_x_kernel(FbParams P) {
-  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-  const int i = lane & 15, kg = lane >> 4;
-  const int job = blockIdx.x;
-  int tau = 0;
-#pragma unroll
-  for (int t = 1; t < 6; ++t) tau += job >= P.jbase[t] ? 1 : 0;
-  const int cnt = P.L.cnt[tau], uoff = P.L.off[tau], N = P.N, U = P.L.U;
-  const int NB = (N + 15) >> 4;
-  const int k0 = (job - P.jbase[tau]) * P.items, k1 = min(k0 + P.items, cnt * NB);
-  __shared__ __attribute__((aligned(16))) float img[2][16 * kXP];
-  __shared__ __attribute__((aligned(16))) float imt[2][128 * kXT];
-  __shared__ __attribute__((aligned(16))) float stg[3][kStg];
-  FbRsrc R;
-  R.q = uniform_rsrc(P.q, N * P.ldq * 4);
-  R.x = uniform_rsrc(P.dx, N * 896 * 4);
-  R.a = uniform_rsrc(P.arg, N * 6 * kD);
-
-  // this wave's basic-column tile: B[k = e][n = j] = W_τ[e][j] = W_τᵀ[j][e], k = 32s + 8kg + jj; layer-1 row of W1
-  const int col = 16 * wv + i;
-  float wx[32], w1x[3];
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    const float* p = P.wtT + ((size_t)tau * kD + col) * kD + 32 * s + 8 * kg;
-    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
-    wx[8 * s + 0] = a.x; wx[8 * s + 1] = a.y; wx[8 * s + 2] = a.z; wx[8 * s + 3] = a.w;
-    wx[8 * s + 4] = b.x; wx[8 * s + 5] = b.y; wx[8 * s + 6] = b.z; wx[8 * s + 7] = b.w;
-  }
-  x_load_w1(P.w1, P.b1, col, kg, w1x);
-  f32x4 acc[8], dw1acc = {0.f, 0.f, 0.f, 0.f};
-  float db1acc = 0.f;
-#pragma unroll
-  for (int et = 0; et < 8; ++et) acc[et] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  FbBuild bn;
-  const int kl = max(k1 - 1, 0);
-  float pre = 0.f;
-  if (wv < 3) {
-    stg[k0 % 3][64 * wv + lane] = fb_stage_load(P, min(k0, kl), cnt, uoff, wv, lane);
-    stg[(k0 + 1) % 3][64 * wv + lane] = fb_stage_load(P, min(k0 + 1, kl), cnt, uoff, wv, lane);
-    pre = fb_stage_load(P, min(k0 + 2, kl), cnt, uoff, wv, lane);
-  }
-  fb_load_build<false, COMPAT>(bn, R, P.ldq, min(k0, kl), true, cnt, uoff, U, tau, wv, i, kg);
-  lds_barrier();
-  xb_build(bn, stg[k0 % 3], k0 % cnt, img[0], imt[0], wv, lane);
-  fb_load_build<false, COMPAT>(bn, R, P.ldq, min(k0 + 1, kl), min(k0 + 1, kl) % cnt == 0, cnt, uoff, U, tau, wv, i, kg);
-  // layer-1 operands of the next item (units[row i][4cc + kg] incl. the bias slot, and units[row 4kg + r][f = i]
-  // for ∂W1) are read from the staging slot one iteration ahead into registers: the item's first MFMAs then wait
-  // on no LDS read (read after the A fragments, they made the wave wait for ALL of the item's LDS reads first)
-  float l1n[3], ubn[4];
-  auto l1_read = [&](const float* sl) {
-#pragma unroll
-    for (int cc = 0; cc < 3; ++cc) {
-      const int f = 4 * cc + kg;
-      l1n[cc] = f < kF ? sl[i * kF + f] : (f == kF ? 1.f : 0.f);
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) ubn[r] = i < kF ? sl[(4 * kg + r) * kF + i] : 0.f;
-  };
-  l1_read(stg[k0 % 3]);
-  int buf = 0;
-  for (int k = k0; k < k1; ++k) {
-    lds_barrier();
-    float a[32];
-    x_afrags(img[buf], i, kg, a);                 // ∂emb[row i][e], e = 32s + 8kg + jj
-    const float ub[4] = {ubn[0], ubn[1], ubn[2], ubn[3]};   // units[row 4kg + r][f = i] (f ≥ 10: 0)
-    f32x4 bas = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int cc = 0; cc < 3; ++cc) bas = __builtin_amdgcn_mfma_f32_16x16x4f32(l1n[cc], w1x[cc], bas, 0, 0, 0);
-    f32x4 c = x_mma_k128(a, wx);                  // ∂basic[row][j] (before ReLU')
-    f32x4 et4[8];
-#pragma unroll
-    for (int et = 0; et < 8; ++et) et4[et] = *reinterpret_cast<const f32x4*>(imt[buf] + (16 * et + i) * kXT + 4 * kg);
-    // The global loads consumed here (staging of item k + 2, build data of item k + 1) were issued one iteration
-    // ago, and nothing was issued after them: the vmcnt(0) the compiler puts before their first use waits out no
-    // fresh round trip. (Issued at the top of the iteration instead, as before, that wait covered a load issued
-    // ~40 MFMAs earlier: one exposed HBM/L2 round trip per item.)
-    if (wv < 3) stg[(k + 2) % 3][64 * wv + lane] = pre;   // slot (k - 1) % 3: nobody reads it in this iteration
-    // item k + 1's ∂emb into the other images (every wave has passed this item's barrier)
-    xb_build(bn, stg[(k + 1) % 3], min(k + 1, kl) % cnt, img[buf ^ 1], imt[buf ^ 1], wv, lane);
-    l1_read(stg[(k + 1) % 3]);                    // (written before barrier k)
-    fb_load_build<false, COMPAT>(bn, R, P.ldq, min(k + 2, kl), k + 2 <= kl && (k + 2) % cnt == 0, cnt, uoff, U, tau,
-                                 wv, i, kg);
-    if (wv < 3) pre = fb_stage_load(P, min(k + 3, kl), cnt, uoff, wv, lane);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) bas[r] = fmaxf(bas[r], 0.f);
-    // ∂W_τᵀ[j][e] += Σ_rows basic[row][j] · ∂emb[row][e] (this item's 16 rows from zero, then added): the 8
-    // e-tiles' chains interleaved (r outer), so no MFMA waits out its predecessor's 40-cycle latency
-    {
-      f32x4 p[8];
-#pragma unroll
-      for (int et = 0; et < 8; ++et) p[et] = __builtin_amdgcn_mfma_f32_16x16x4f32(bas[0], et4[et][0], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-#pragma unroll
-      for (int r = 1; r < 4; ++r)
-#pragma unroll
-        for (int et = 0; et < 8; ++et) p[et] = __builtin_amdgcn_mfma_f32_16x16x4f32(bas[r], et4[et][r], p[et], 0, 0, 0);
-#pragma unroll
-      for (int et = 0; et < 8; ++et) acc[et] += p[et];
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      c[r] = bas[r] > 0.f ? c[r] : 0.f;
-      db1acc += c[r];
-    }
-    // ∂W1[j][f] += Σ_rows ∂basic[row][j] · units[row][f]
-    f32x4 p1 = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) p1 = __builtin_amdgcn_mfma_f32_16x16x4f32(c[r], ub[r], p1, 0, 0, 0);
-    dw1acc += p1;
-    buf ^= 1;
-  }
-  float* dst = P.dwtpart + (size_t)job * (kD * kD);
-#pragma unroll
-  for (int et = 0; et < 8; ++et) *reinterpret_cast<f32x4*>(dst + ((8 * wv + et) * 64 + lane) * 4) = acc[et];
-  float* wp = P.w1part + (size_t)job * kW1;
-  if (i < kF) {
-#pragma unroll
-    for (int r = 0; r < 4; ++r) wp[(16 * wv + 4 * kg + r) * kF + i] = dw1acc[r];
-  }
-  float s = db1acc;
-  s += __shfl_xor(s, 16, 64);
-  s += __shfl_xor(s, 32, 64);
-  if (kg == 0) wp[kD * kF + 16 * wv + i] = s;
-}
-
-// 4-wave form of encoder_bwd_x_kernel (two workgroups per CU): wave w owns basic-column tiles 2w, 2w+1 and builds
+// Exact encoder backward, 4-wave form (two workgroups per CU; an 8-wave one-per-CU form measured slower and was
+// removed in round 5): wave w owns basic-column tiles 2w, 2w+1 and builds
 // e-tiles 2w, 2w+1 of the item's ∂emb images. The item's A fragments (∂emb rows) and transposed ∂emb tiles are read
 // once per wave for two column tiles (half the LDS traffic per MFMA), and the two resident workgroups work on
 // different items, so one's barrier / staging phases overlap the other's MFMAs (the 8-wave form keeps both waves of
@@ -1684,15 +1559,11 @@ extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const
     F.dwtpart = F.w1part + (size_t)jobs * kW1;
     if (f32 == 2 && demb_in) return hipErrorInvalidValue;      // the exact kernels cover the 1v1 encoder
     if (jobs > 0 && f32 == 2) {
-      // the 4-wave two-workgroups-per-CU form by default: 369.7 vs 373.6 µs alone, and in the exact learner step
-      // 5.498 / 5.483 vs 5.518 / 5.513 ms (two same-box pairs, scripts/gpu_x2ab.sh) — beside the side stream's
-      // weight-gradient GEMMs two smaller workgroups per CU schedule better. DCA_ENC_BWD_X2=0: the 8-wave form.
-      static const bool x2 = [] { const char* e = getenv("DCA_ENC_BWD_X2"); return !(e && e[0] == '0'); }();
-      if (x2) {
-        if (compat) encoder_bwd_x2_kernel<true><<<jobs, 256, 0, st>>>(F);
-        else encoder_bwd_x2_kernel<false><<<jobs, 256, 0, st>>>(F);
-      } else if (compat) encoder_bwd_x_kernel<true><<<jobs, 512, 0, st>>>(F);
-      else encoder_bwd_x_kernel<false><<<jobs, 512, 0, st>>>(F);
+      // the 4-wave two-workgroups-per-CU form: 369.7 vs 373.6 µs alone for the 8-wave form, and in the exact learner
+      // step 5.498 / 5.483 vs 5.518 / 5.513 ms (two same-box pairs) — beside the side stream's weight-gradient GEMMs
+      // two smaller workgroups per CU schedule better
+      if (compat) encoder_bwd_x2_kernel<true><<<jobs, 256, 0, st>>>(F);
+      else encoder_bwd_x2_kernel<false><<<jobs, 256, 0, st>>>(F);
     } else if (jobs > 0) {
       if (demb_in) encoder_bwd_f32_fused_kernel<true, false><<<jobs, 512, 0, st>>>(F);
       else if (compat) encoder_bwd_f32_fused_kernel<false, true><<<jobs, 512, 0, st>>>(F);

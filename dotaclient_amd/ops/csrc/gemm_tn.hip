@@ -618,10 +618,9 @@ extern "C" void dca_gemm_tn_plan(int M, int N, int K, int* splits, int* kc, int*
   const int tm = (M + BM - 1) / BM, tn = (N + BN - 1) / BN;
   const int t = tm * tn;
   // ≈1.5 workgroups per CU; exact: ≈2 (MFMA-bound at 1/16 of the bf16 rate, two 64 KB workgroups fit a CU)
-  // (DCA_GEMM_TN_TARGET overrides the workgroup target: an A/B knob. Exact learner step, two passes each:
-  // 256 → 5.55, 512 → 5.48, 768 → 5.53, 1024 → 5.59 ms; profiles/r4_gemm_tn_target_sweep.txt)
-  static const int tgt_env = [] { const char* e = getenv("DCA_GEMM_TN_TARGET"); return e ? atoi(e) : 0; }();
-  const int target = tgt_env > 0 ? tgt_env : (f32 == 2 ? 512 : 384);
+  // (exact workgroup target swept in round 4, learner step, two passes each: 256 → 5.55, 512 → 5.48, 768 → 5.53,
+  // 1024 → 5.59 ms; profiles/r4_gemm_tn_target_sweep.txt)
+  const int target = f32 == 2 ? 512 : 384;
   int s = (target + t - 1) / t;
   const int kmax = (K + bk - 1) / bk;                     // at least one K slab per split
   if (s > kmax) s = kmax;

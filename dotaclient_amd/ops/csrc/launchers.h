@@ -14,10 +14,6 @@ hipError_t dca_attn_block_fwd_f32(const float* e0, const float* bout, const floa
                                   float* e1, float* x896, unsigned char* arg, const int* off, int compat, int N,
                                   float eps, hipStream_t stream);
 int dca_attn_block_bwd_groups(int N);
-hipError_t dca_attn_dxn_ln_bwd_f32(const float* dqkv, const short* wq4h, const short* wq4l, const float* e0,
-                                   const float* bout, const float* mu, const float* rs, const float* gamma,
-                                   const float* de1, const int* off, float* de0, float* part, float* tmp,
-                                   float* sums, int N, hipStream_t stream);
 hipError_t dca_attn_block_bwd_f32(const float* dtl, const float* q, int ldq, const float* dx, const unsigned char* arg,
                                   const int* off, int compat, const float* o, const float* qkv, const float* bq,
                                   const float* lse, const float* e0, const float* bout, const float* mu,

@@ -1073,9 +1073,6 @@ inline void plan(int B, int& nch, int& Bc, int& MT, int f32 = 0) {
   // 1 chain × 8 rows 2.21/2.82, 2 × 4 2.09/2.57, 4 × 2 2.08/2.41, 8 × 1 2.08/2.26. Chains hold ≤ 32 rows; beyond
   // 8·32 sequences further chains queue behind the running ones.
   nch = B <= kMaxTeams * 32 ? (B < kMaxTeams ? B : kMaxTeams) : (B + 31) / 32;
-  // DCA_TEAM_ROWS = sequences per chain (latency experiments: e.g. 1 → B independent chains on B teams)
-  static const int forced = [] { const char* e = getenv("DCA_TEAM_ROWS"); return e ? atoi(e) : 0; }();
-  if (forced > 0 && forced <= 32) nch = (B + forced - 1) / forced;
   // F32 chains hold ≤ 16 rows (the backward's hi + lo gate-gradient images of 16 rows take 132 KB of LDS)
   if (f32 && (B + nch - 1) / nch > 16) nch = (B + 15) / 16;
   Bc = (B + nch - 1) / nch;
@@ -1106,19 +1103,16 @@ inline void plan(int B, int& nch, int& Bc, int& MT, int f32 = 0) {
     default: return hipErrorInvalidValue;                                                                    \
   }
 
-// one-row fp32 chains take the exact VALU variant (DCA_TEAM_V1=0 forces the bf16x3 MFMA one, for comparison); at
-// H = 512 the backward takes its 8-wave form V2 (measured B=8, S=1400: backward 2069 vs 2137 µs, while the 8-wave
-// forward was SLOWER, 2056 vs 1778 µs). DCA_TEAM_V2 = 0 (neither), 1 (both directions), default: backward only.
+// fp32 chains of ≤ 4 rows take the exact VALU variant; at H = 512 the backward takes its 8-wave form V2 (measured
+// B=8, S=1400: backward 2069 vs 2137 µs, while the 8-wave forward was SLOWER, 2056 vs 1778 µs).
 // half: the CU-exclusive 16-workgroup teams (V1 form in both directions, H = 512, fast activations).
 inline int use_v1(int f32, int Bc, int H, int backward, int precise, int half = -1) {
-  static const int off = [] { const char* e = getenv("DCA_TEAM_V1"); return e && e[0] == '0'; }();
   static const int half_env = [] { const char* e = getenv("DCA_TEAM_HALF"); return e && e[0] == '1'; }();
   if (half < 0) half = half_env;
-  static const int v2 = [] { const char* e = getenv("DCA_TEAM_V2"); return e ? (e[0] == '0' ? 0 : 3) : 2; }();
-  if (!(f32 && Bc <= 4 && !off)) return 0;
+  if (!(f32 && Bc <= 4)) return 0;
   const int rows = Bc == 1 ? 0 : (Bc == 2 ? 32 : 64);         // VAR bits 5-6: 2 or 4 rows per chain
   if (half && H == 512 && !precise) return 1 | 16 | rows;
-  return ((H == 512 && (v2 & (backward ? 2 : 1))) ? 2 : 1) | (precise ? 4 : 0) | rows;
+  return ((H == 512 && backward) ? 2 : 1) | (precise ? 4 : 0) | rows;
 }
 
 // Workspace bytes (control block + per-team exchange buffers) for a launch of (B, H).
