@@ -287,58 +287,87 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     adt = torch.float32 if f32 else torch.bfloat16
     # (x896 / emb come back in the weights' dtype: bf16, or fp32 from the bf16x3 encoder)
     # (exact: the IEEE-fp32 variant, ops/csrc/encoder.hip encoder_fwd_x_kernel)
-    x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs), exact=exact)
+    # time chunks with the 1v1 fp32 policies: the encoder and the forward chain run chunk by chunk, each chunk's
+    # recurrence launched as soon as its input projection is ready (the next chunk's encoder runs beside it)
+    front = len(chunk_bounds(S, fp.chunks)) > 1 and f32 and not attn and not lin and reset_t is None
+    enc_done: List[torch.cuda.Event] = []
     attn32 = attn and f32
-    if attn32:
-        # 5v5 entity attention at fp32 (ops/csrc/attn.hip fp32 kernels: LayerNorm, bf16x3 attention core, pools; the
-        # QKV / out-projection GEMMs on hipBLASLt fp32). emb = E0' = E0 + b_out (bias folded into bt); the LayerNorm
-        # kernel also writes the copy of E0' its backward needs, so the out-projection accumulates onto emb in place
-        # (E1 = E0' + O·W_outᵀ) and the QKV GEMM runs without its bias epilogue (added by the attention kernels):
-        # 213 + 480 µs instead of 359 + 116 (copy, GEMM, bias pass) + 795 µs at N·U = 716 800 rows
-        toff = fp.type_offset_list()
-        bqkv = P['entity_attn.qkv.bias'].detach()
-        # one kernel per step; E0' stays untouched (the LayerNorm backward's input), E1 is a new tensor
-        E0p = emb.view(N * U, 128)
-        if 'wq_f' in W:                    # hi / lo fragment images from the step's weight_prep launch
-            wq, wo = W['wq_f'], W['wo_f']
-        else:
-            wq = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.qkv.weight'].detach())]
-            wo = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.out.weight'].detach())]
+    if front:
+        x896 = torch.empty(N, 896, device=dev)
+        emb = torch.empty(N, U, 128, device=dev)
         arg = torch.empty(N, 6, 128, dtype=torch.uint8, device=dev)
-        Xn, ln_mu, ln_rs, QKV, Oat, lse, E1 = C.attn_block_fwd(
-            E0p, W['bout'], P['entity_attn.ln.weight'].detach(), P['entity_attn.ln.bias'].detach(), wq[0], wq[1],
-            bqkv, wo[0], wo[1], toff, x896, arg, bool(cfg.compat_bugs), 1e-5)
-        emb = E1.view(N, U, 128)
-    elif attn:
-        # 5v5 entity attention (ops/csrc/attn.hip): emb = E0 + b_out here (bias folded into bt)
-        toff = fp.type_offset_list()
-        E0p = emb.view(N * U, 128)
-        Xn, ln_mu, ln_rs = C.ln_fwd(E0p, W['bout'], W['ln_g'], W['ln_b'], 1e-5)
-        QKV = torch.addmm(W['bqkv16'], Xn, W['wqkv16'].t())
-        Oat, lse = C.attn_fwd(QKV)
-        E1 = torch.addmm(E0p, Oat, W['wout16'].t())                 # residual + out-projection, bf16
-        arg = C.attn_pool(E1, toff, x896, bool(cfg.compat_bugs))    # pools of the attended embeddings
-        emb = E1.view(N, U, 128)
-    elif cfg.compat_bugs:   # reference policy.py:127: enemy-tower pool = enemy-nonhero pool
-        x896[:, 768:896] = x896[:, 512:640]
-        arg[:, 5] = arg[:, 3]
-    # relu(x896·W_preᵀ + b) as ONE hipBLASLt GEMM with a bias+ReLU epilogue, bf16 (fp32) out (x16 > 0 ⟺ x > 0)
-    if exact:
-        # IEEE-fp32 forward chain: the same kernel on v_mfma_f32_16x16x4_f32 with the fp32 weights as they are
-        nil = wpre16.new_empty(0)
-        x16, xp = C.pre_rnn_chain(x896, wpre16, nil, W['bpre16'], wih16, nil)
-        xp4 = xp.view(S, B, H, 4) if not lin else None
-    elif f32:
-        if 'pre_s' in W:                 # hi / lo images from the step's weight_prep launch
-            fw1, fw2 = W['pre_s'], W['ih_s']
+        x16 = torch.empty(N, 256, device=dev)
+        xp = torch.empty(N, 4 * H, device=dev)
+        if exact:
+            nil = wpre16.new_empty(0)
+            cw = (wpre16, nil, wih16, nil)
         else:
-            fw1, fw2 = C.split_bf16x2(wpre16, True), C.split_bf16x2(wih16, True)   # slab-major bf16 hi / lo images
-        x16, xp = C.pre_rnn_chain(x896, fw1[0], fw1[1], W['bpre16'], fw2[0], fw2[1])
-        xp4 = xp.view(S, B, H, 4) if not lin else None
+            cw = (W['pre_s'][0], W['pre_s'][1], W['ih_s'][0], W['ih_s'][1])
+        for t0, t1 in chunk_bounds(S, fp.chunks):
+            r0, r1 = t0 * B, t1 * B
+            C.encoder_fwd(units_t[r0:r1], env_t[r0:r1], w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs),
+                          exact=exact, x896_out=x896[r0:r1], emb_out=emb[r0:r1], arg_out=arg[r0:r1])
+            if cfg.compat_bugs:   # reference policy.py:127: enemy-tower pool = enemy-nonhero pool
+                x896[r0:r1, 768:896] = x896[r0:r1, 512:640]
+                arg[r0:r1, 5] = arg[r0:r1, 3]
+            C.pre_rnn_chain(x896[r0:r1], cw[0], cw[1], W['bpre16'], cw[2], cw[3], x_out=x16[r0:r1],
+                            xp_out=xp[r0:r1])
+            e = torch.cuda.Event()
+            e.record(main)
+            enc_done.append(e)
+        xp4 = xp.view(S, B, H, 4)
     else:
-        assert not lin, 'the linear recurrent layer runs on the fp32 chain kernels'
-        x16 = torch._addmm_activation(W['bpre16'], x896, wpre16.t())
-        xp4 = _mm(x16, wih16.t()).view(S, B, H, 4)      # the recurrence kernel adds the bias (bias4)
+        x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs), exact=exact)
+        if attn32:
+            # 5v5 entity attention at fp32 (ops/csrc/attn.hip fp32 kernels: LayerNorm, bf16x3 attention core, pools; the
+            # QKV / out-projection GEMMs on hipBLASLt fp32). emb = E0' = E0 + b_out (bias folded into bt); the LayerNorm
+            # kernel also writes the copy of E0' its backward needs, so the out-projection accumulates onto emb in place
+            # (E1 = E0' + O·W_outᵀ) and the QKV GEMM runs without its bias epilogue (added by the attention kernels):
+            # 213 + 480 µs instead of 359 + 116 (copy, GEMM, bias pass) + 795 µs at N·U = 716 800 rows
+            toff = fp.type_offset_list()
+            bqkv = P['entity_attn.qkv.bias'].detach()
+            # one kernel per step; E0' stays untouched (the LayerNorm backward's input), E1 is a new tensor
+            E0p = emb.view(N * U, 128)
+            if 'wq_f' in W:                    # hi / lo fragment images from the step's weight_prep launch
+                wq, wo = W['wq_f'], W['wo_f']
+            else:
+                wq = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.qkv.weight'].detach())]
+                wo = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.out.weight'].detach())]
+            arg = torch.empty(N, 6, 128, dtype=torch.uint8, device=dev)
+            Xn, ln_mu, ln_rs, QKV, Oat, lse, E1 = C.attn_block_fwd(
+                E0p, W['bout'], P['entity_attn.ln.weight'].detach(), P['entity_attn.ln.bias'].detach(), wq[0], wq[1],
+                bqkv, wo[0], wo[1], toff, x896, arg, bool(cfg.compat_bugs), 1e-5)
+            emb = E1.view(N, U, 128)
+        elif attn:
+            # 5v5 entity attention (ops/csrc/attn.hip): emb = E0 + b_out here (bias folded into bt)
+            toff = fp.type_offset_list()
+            E0p = emb.view(N * U, 128)
+            Xn, ln_mu, ln_rs = C.ln_fwd(E0p, W['bout'], W['ln_g'], W['ln_b'], 1e-5)
+            QKV = torch.addmm(W['bqkv16'], Xn, W['wqkv16'].t())
+            Oat, lse = C.attn_fwd(QKV)
+            E1 = torch.addmm(E0p, Oat, W['wout16'].t())                 # residual + out-projection, bf16
+            arg = C.attn_pool(E1, toff, x896, bool(cfg.compat_bugs))    # pools of the attended embeddings
+            emb = E1.view(N, U, 128)
+        elif cfg.compat_bugs:   # reference policy.py:127: enemy-tower pool = enemy-nonhero pool
+            x896[:, 768:896] = x896[:, 512:640]
+            arg[:, 5] = arg[:, 3]
+        # relu(x896·W_preᵀ + b) as ONE hipBLASLt GEMM with a bias+ReLU epilogue, bf16 (fp32) out (x16 > 0 ⟺ x > 0)
+        if exact:
+            # IEEE-fp32 forward chain: the same kernel on v_mfma_f32_16x16x4_f32 with the fp32 weights as they are
+            nil = wpre16.new_empty(0)
+            x16, xp = C.pre_rnn_chain(x896, wpre16, nil, W['bpre16'], wih16, nil)
+            xp4 = xp.view(S, B, H, 4) if not lin else None
+        elif f32:
+            if 'pre_s' in W:                 # hi / lo images from the step's weight_prep launch
+                fw1, fw2 = W['pre_s'], W['ih_s']
+            else:
+                fw1, fw2 = C.split_bf16x2(wpre16, True), C.split_bf16x2(wih16, True)   # slab-major bf16 hi / lo images
+            x16, xp = C.pre_rnn_chain(x896, fw1[0], fw1[1], W['bpre16'], fw2[0], fw2[1])
+            xp4 = xp.view(S, B, H, 4) if not lin else None
+        else:
+            assert not lin, 'the linear recurrent layer runs on the fp32 chain kernels'
+            x16 = torch._addmm_activation(W['bpre16'], x896, wpre16.t())
+            xp4 = _mm(x16, wih16.t()).view(S, B, H, 4)      # the recurrence kernel adds the bias (bias4)
     if lin:
         # fake_rnn: h = pre·W_fᵀ + b_f (the chain kernel's second product) — no activation, no recurrence
         hs16 = xp.add_(bias_p).view(S, B, H)
@@ -366,13 +395,16 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     # ---- forward recurrence on stream L, heads (+ heads backward) per chunk on the main stream
     ready = torch.cuda.Event()
     ready.record(main)
-    sL.wait_event(ready)
+    if not front:
+        sL.wait_event(ready)
     # every recurrence chunk is enqueued up front (the host must never hold the recurrence stream back while it
     # is busy launching the per-chunk work of the main stream)
     h_c, c_c = h0.contiguous(), c0.contiguous()
     fwd_done = []
     with torch.cuda.stream(sL):
-        for t0, t1 in ([] if lin else spans):
+        for i, (t0, t1) in enumerate([] if lin else spans):
+            if front:
+                sL.wait_event(enc_done[i])
             o = team_fwd(C, xp4[t0:t1], whh16, h_c, c_c, fp.err, False, time_major=True,
                          hs_out=hs16[t0:t1], cs_out=cs[t0:t1], gates_out=gates4[t0:t1], bias4=bias_p,
                          reset=rst)

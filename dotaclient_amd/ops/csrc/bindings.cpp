@@ -258,7 +258,9 @@ std::vector<torch::Tensor> heads_loss(torch::Tensor z, torch::Tensor emb, torch:
 // (N,6,128)); x896 / emb have wt's dtype (f32: the fp32-accurate bf16x3 variant).
 std::vector<torch::Tensor> encoder_fwd(torch::Tensor units, torch::Tensor env, torch::Tensor w1, torch::Tensor b1,
                                        torch::Tensor wt, torch::Tensor bt, torch::Tensor we, torch::Tensor be,
-                                       std::vector<int64_t> counts, bool compat, bool exact) {
+                                       std::vector<int64_t> counts, bool compat, bool exact,
+                                       c10::optional<torch::Tensor> x896_out, c10::optional<torch::Tensor> emb_out,
+                                       c10::optional<torch::Tensor> arg_out) {
   CHECK_F32(units); CHECK_F32(env); CHECK_F32(w1); CHECK_F32(b1); CHECK_DEV(wt); CHECK_CONTIG(wt); CHECK_F32(bt);
   CHECK_F32(we); CHECK_F32(be);
   const bool f32w = wt.scalar_type() == at::kFloat;
@@ -276,9 +278,9 @@ std::vector<torch::Tensor> encoder_fwd(torch::Tensor units, torch::Tensor env, t
   TORCH_CHECK(tot == U && U <= 64, "counts must sum to U <= 64");
   auto o = units.options();
   const auto adt = f32w ? at::kFloat : at::kBFloat16;
-  auto x896 = torch::empty({N, 896}, o.dtype(adt));
-  auto emb = torch::empty({N, U, 128}, o.dtype(adt));
-  auto arg = torch::empty({N, 6, 128}, o.dtype(at::kByte));
+  auto x896 = out_or_new(x896_out, {N, 896}, o.dtype(adt), "x896_out");
+  auto emb = out_or_new(emb_out, {N, U, 128}, o.dtype(adt), "emb_out");
+  auto arg = out_or_new(arg_out, {N, 6, 128}, o.dtype(at::kByte), "arg_out");
   hip_check(dca_encoder_fwd(ptr<float>(units), ptr<float>(env), ptr<float>(w1), ptr<float>(b1), wt.data_ptr(),
                             ptr<float>(bt), ptr<float>(we), ptr<float>(be), x896.data_ptr(), emb.data_ptr(),
                             ptr<unsigned char>(arg), N, U, c, compat ? 1 : 0, cur_stream(), exact ? 2 : (f32w ? 1 : 0)),
@@ -895,7 +897,8 @@ torch::Tensor rowmm_in256(torch::Tensor A, torch::Tensor wh, torch::Tensor wl) {
 // xp = x·W_ihᵀ (N, X) in one launch. bf16x3: slab-major hi / lo weight images (split_bf16x2(w, True) of W_pre
 // (256, K1) and of W_ih (X, 256)); exact: W_pre (256, K1) and W_ih (X, 256) fp32 with empty lo images.
 std::vector<torch::Tensor> pre_rnn_chain(torch::Tensor x896, torch::Tensor w1h, torch::Tensor w1l, torch::Tensor bias,
-                                         torch::Tensor w2h, torch::Tensor w2l) {
+                                         torch::Tensor w2h, torch::Tensor w2l, c10::optional<torch::Tensor> x_out,
+                                         c10::optional<torch::Tensor> xp_out) {
   CHECK_F32(x896); CHECK_F32(bias);
   const bool exact = chain_exact(w1h, w1l, "pre_rnn_chain");
   TORCH_CHECK(chain_exact(w2h, w2l, "pre_rnn_chain") == exact, "pre_rnn_chain: both weights exact or both bf16x3");
@@ -915,8 +918,8 @@ std::vector<torch::Tensor> pre_rnn_chain(torch::Tensor x896, torch::Tensor w1h, 
   TORCH_CHECK(K1 % 128 == 0 && X % 128 == 0, "pre_rnn_chain: K1 % 128 == 0 and X % 128 == 0");
   TORCH_CHECK((long long)N * K1 * 4 <= 0x7fff0000LL, "pre_rnn_chain: x896 too large for one launch");
   auto o = x896.options();
-  auto x = torch::empty({N, 256}, o);
-  auto xp = torch::empty({N, X}, o);
+  auto x = out_or_new(x_out, {N, 256}, o, "x_out");
+  auto xp = out_or_new(xp_out, {N, X}, o, "xp_out");
   hip_check(dca_dpre_dx(ptr<float>(x896), w1h.data_ptr(), exact ? nullptr : w1l.data_ptr(), ptr<float>(bias),
                         w2h.data_ptr(), exact ? nullptr : w2l.data_ptr(), ptr<float>(x), ptr<float>(xp), N, K1, X,
                         exact ? 1 : 0, 1, cur_stream()),
@@ -1123,7 +1126,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dz_bf16") = false, py::arg("precise") = false);
   m.def("encoder_fwd", &encoder_fwd, "fused entity encoder forward (unit MLP, per-type GEMM, max-pool+argmax)",
         py::arg("units"), py::arg("env"), py::arg("w1"), py::arg("b1"), py::arg("wt"), py::arg("bt"), py::arg("we"),
-        py::arg("be"), py::arg("counts"), py::arg("compat"), py::arg("exact") = false);
+        py::arg("be"), py::arg("counts"), py::arg("compat"), py::arg("exact") = false,
+        py::arg("x896_out") = py::none(), py::arg("emb_out") = py::none(), py::arg("arg_out") = py::none());
   m.def("encoder_bwd", &encoder_bwd, "fused entity encoder backward: dW_type (K-blocked split-K MFMA GEMM), dW1, db1",
         py::arg("units"), py::arg("w1"), py::arg("b1"), py::arg("wtT"), py::arg("dtl"), py::arg("q"), py::arg("dx"),
         py::arg("arg"), py::arg("counts"), py::arg("compat"), py::arg("demb_in") = py::none(),
@@ -1176,7 +1180,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "bf16 hi/lo weights, or exact-f32 MFMA with fp32 weights)", py::arg("dG"), py::arg("w1h"), py::arg("w1l"),
         py::arg("x"), py::arg("w2h"), py::arg("w2l"));
   m.def("pre_rnn_chain", &pre_rnn_chain, "fused forward chain x = relu(x896·W_pre^T + b), xp = x·W_ih^T (bf16x3)",
-        py::arg("x896"), py::arg("w1h"), py::arg("w1l"), py::arg("bias"), py::arg("w2h"), py::arg("w2l"));
+        py::arg("x896"), py::arg("w1h"), py::arg("w1l"), py::arg("bias"), py::arg("w2h"), py::arg("w2l"),
+        py::arg("x_out") = py::none(), py::arg("xp_out") = py::none());
   m.def("rowmm_out256", &rowmm_out256, "C (N,256) = A (N,K)·W^T + b on the chain kernel's stage 1 (bf16x3)",
         py::arg("A"), py::arg("wh"), py::arg("wl"), py::arg("bias"));
   m.def("rowmm_in256", &rowmm_in256, "C (N,X) = A (N,256)·W^T on the chain kernel's stage 2 (bf16x3)", py::arg("A"),

@@ -1107,8 +1107,10 @@ inline void plan(int B, int& nch, int& Bc, int& MT, int f32 = 0) {
 // B=8, S=1400: backward 2069 vs 2137 µs, while the 8-wave forward was SLOWER, 2056 vs 1778 µs).
 // half: the CU-exclusive 16-workgroup teams (V1 form in both directions, H = 512, fast activations).
 inline int use_v1(int f32, int Bc, int H, int backward, int precise, int half = -1) {
-  static const int half_env = [] { const char* e = getenv("DCA_TEAM_HALF"); return e && e[0] == '1'; }();
-  if (half < 0) half = half_env;
+  if (half < 0) {                        // read per launch (two launches per learner step): tests flip it
+    const char* e = getenv("DCA_TEAM_HALF");
+    half = e && e[0] == '1';
+  }
   if (!(f32 && Bc <= 4)) return 0;
   const int rows = Bc == 1 ? 0 : (Bc == 2 ? 32 : 64);         // VAR bits 5-6: 2 or 4 rows per chain
   if (half && H == 512 && !precise) return 1 | 16 | rows;

@@ -140,3 +140,36 @@ def test_exact_compat_network_matches_fp64(gpu_ops, vbug):
     m = L.train_step(batch)
     torch.cuda.synchronize()
     assert abs(float(m['loss']) - l64) <= 1e-5 * max(1e-2, abs(l64)), (float(m['loss']), l64)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('half', ['0', '1'])
+def test_exact_chunked_step_matches_one_chunk(gpu_ops, monkeypatch, half):
+    """Time chunks (DCA_PIPELINE_CHUNKS=4: encoder + forward chain per chunk ahead of each recurrence chunk, heads and
+    weight gradients per chunk beside the recurrence) and the CU-exclusive half teams (DCA_TEAM_HALF=1) give the
+    one-chunk step's loss and gradients up to the fp32 summation order of the chunked weight-gradient sums."""
+    import copy
+    from dotaclient_amd.learner.engine import Learner, LossConfig
+    from dotaclient_amd.learner.synthetic import make_batch
+    monkeypatch.setenv('DCA_TEAM_HALF', half)
+    torch.manual_seed(0)
+    cfg = get_config('lstm512')
+    pol = Policy(cfg)
+    lc = LossConfig(algo='ppo', vf_coef=0.5, entropy_coef=0.01)
+    batch = make_batch(8, 280, cfg.layout, cfg.hidden, device='cuda', seed=5)
+    out = []
+    for chunks in ('1', '4'):
+        monkeypatch.setenv('DCA_PIPELINE_CHUNKS', chunks)
+        L = Learner(copy.deepcopy(pol), lc, device='cuda', backend='fused', dp=False, precision='fp32-exact')
+        L.dp.zero_grad()
+        loss, _ = L.loss(batch)
+        loss.backward()
+        torch.cuda.synchronize()
+        L.model.check_error()
+        out.append((float(loss), {n: p.grad.detach().clone() for n, p in zip(L.flat.names, L.flat.params)
+                                  if p.grad is not None}))
+    (l1, g1), (l4, g4) = out
+    assert abs(l1 - l4) <= 1e-6 * max(1.0, abs(l1)), (l1, l4)
+    for n in g1:
+        d = float((g4[n] - g1[n]).norm() / g1[n].norm().clamp_min(1e-30))
+        assert d < 2e-6, (n, d)

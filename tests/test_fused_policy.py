@@ -65,7 +65,7 @@ def test_fused_train_step_decreases_loss(gpu_ops, precision):
     assert losses[-1] < losses[0]
 
 
-@pytest.mark.parametrize('chunks,precision', [('1', 'fp32'), ('3', 'fp32'), ('1', 'bf16')])
+@pytest.mark.parametrize('chunks,precision', [('1', 'fp32'), ('3', 'fp32'), ('1', 'bf16'), ('3', 'fp32-exact')])
 def test_graph_captured_step_matches_eager(gpu_ops, monkeypatch, chunks, precision):
     """hipGraph-captured forward+backward (Learner.enable_graph) gives the same parameters as eager steps, also
     across host synchronisations between replays (a stale host-staged buffer in the graph would show up there)."""
