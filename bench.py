@@ -120,6 +120,10 @@ def parse():
                          'self-play league on the fp8 actor policy step, learners sampling an on-HBM replay of '
                          '--league-replay-gb GB per GPU')
     ap.add_argument('--league-replay-gb', type=float, default=100.0)
+    ap.add_argument('--league-replay-prefill', type=int, default=1,
+                    help='fill the replay ring to capacity from the first ingest (copies of the fresh sequences, '
+                         'version -1) so every timed minibatch gathers from the whole pool; 0 = fills from the '
+                         'actors only (league_replay.config.replay_fill reports the fraction either way)')
     ap.add_argument('--e2e-5v5-extra', type=float, default=-1.0,
                     help='seconds of the node loop on the 5v5 entity-attention model (extra field e2e_5v5, BASELINE '
                          'config 4 end to end: 5v5 self-play actors, 10 players per game; 0 = off; default: 15 s on '
@@ -427,12 +431,23 @@ def main():
                 mine['fp8_vs_bf16_policy_step'] = mb['gpu_steps_per_s'] / mine['policy_step_per_s']
         except Exception as e:
             mine['policy_step_fp8_error'] = repr(e)
+        if not cfg.entity_attention:
+            try:
+                # the reference actor's precision: the IEEE-fp32 policy step (ops/csrc/actor_core.hip MODE 0,
+                # v_mfma_f32_16x16x4_f32, no vendor GEMM)
+                mb = measure_actor_throughput(policy, device, n_games=args.actor_games, threads=args.actor_threads,
+                                              precision='fp32')
+                mine['policy_step_fp32_per_s'] = mb['gpu_steps_per_s']
+                mine['policy_step_fp32_protobuf_featurize_per_s'] = mb['steps_per_s']
+            except Exception as e:
+                mine['policy_step_fp32_error'] = repr(e)
         ranks = gather(mine)
         progress('actor measurements done')
         actor = dict(ranks[0])
         for k in ('steps_per_s', 'protobuf_runtime_steps_per_s', 'policy_step_per_s',
                   'policy_step_protobuf_featurize_per_s', 'policy_step_fp8_per_s',
-                  'policy_step_fp8_protobuf_featurize_per_s'):
+                  'policy_step_fp8_protobuf_featurize_per_s', 'policy_step_fp32_per_s',
+                  'policy_step_fp32_protobuf_featurize_per_s'):
             vals = [r.get(k) for r in ranks]
             if all(v is not None for v in vals):
                 actor[k] = float(sum(vals))
@@ -476,7 +491,8 @@ def main():
                 model=args.model, device=device, duration=args.league_replay_extra, games=args.e2e_games,
                 threads=args.e2e_threads, seq_len=args.seq_len, precision=args.precision, pack=bool(args.e2e_pack),
                 transport=args.e2e_transport, progress=progress, idle_probe=0.0, league='pfsp',
-                latest_weights_prob=0.8, actor_precision='fp8', replay_gb=args.league_replay_gb)
+                latest_weights_prob=0.8, actor_precision='fp8', replay_gb=args.league_replay_gb,
+                replay_prefill=bool(args.league_replay_prefill))
         except Exception as e:
             league_replay = {'error': repr(e)}
         progress(f'league-replay done: {league_replay.get("error", "ok")}')
@@ -520,6 +536,9 @@ def main():
             'vs_baseline': value / BASELINE_STEPS_PER_S,
             'vs_baseline_e2e': (e2e['steps_per_s'] / BASELINE_STEPS_PER_S
                                 if e2e and 'steps_per_s' in e2e else None),
+            'e2e_layout': ('packed: whole episodes packed into the seq_len sequences with episode-start resets '
+                           '(--e2e-pack 1; steps_per_s counts padded steps, valid_steps_per_s real ones)'
+                           if args.e2e_pack else 'reference layout: every rollout padded to seq_len (--e2e-pack 0)'),
             'dtype': {'fp32-exact': 'fp32', 'fp32': 'fp32 (bf16x3 MFMA operands)'}.get(args.precision, args.precision),
             'precision_note': {
                 'fp32-exact': 'IEEE fp32 end to end like the reference (torch fp32 nn.Linear + Adam): every GEMM product '

@@ -307,7 +307,7 @@ class GpuActorPolicy:
         torch.cuda.synchronize(self.device)
         # warm-up steps advanced the recurrent state and the RNG counter: start from a clean slate
         self.ctr.copy_(ctr0)
-        self.h.zero_(); self.c.zero_(); self.h16.zero_()
+        self.h.zero_(); self.c.zero_()
         self.graph = g
 
     # ------------------------------------------------------------------------------------------------

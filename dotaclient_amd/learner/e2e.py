@@ -238,7 +238,7 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                      transport: str = 'auto', backend: str = 'auto', idle_probe: float = 3.0,
                      report=None, record_consumed: int = 0, progress=None, pack: bool = False,
                      league: Optional[str] = None, latest_weights_prob: float = 1.0, actor_precision: str = 'bf16',
-                     replay_gb: float = 0.0, actor_procs: int = 1) -> Dict[str, float]:
+                     replay_gb: float = 0.0, actor_procs: int = 1, replay_prefill: bool = False) -> Dict[str, float]:
     """The reference's node topology end to end (optimizer.py:144-150, 274-287; ks-app/components/optimizer.jsonnet:
     79-174): ONE experience queue per node fed by actor processes, ``WORLD_SIZE`` learner ranks (one per GPU, DDP
     over RCCL) consuming disjoint rollouts from it as competing consumers, and rank 0 alone checkpointing and
@@ -337,7 +337,7 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                               backend=backend, checkpoint_keep=2, run_local=True, xp_timeout=120.0,
                               histogram_freq=10 ** 9, async_checkpoint=dev.type == 'cuda',
                               prefetch_rollouts=prefetch, record_consumed=record_consumed, pack_sequences=pack,
-                              replay_gb=replay_gb)
+                              replay_gb=replay_gb, replay_prefill=replay_prefill)
         opt = DotaOptimizer(cfg, broker, checkpoint=rank == 0)     # rank 0 publishes model version 0
         say(f'e2e: learner ready ({transport} broker {addr}); waiting for the actor process')
         t_ready = time.time() + 900
@@ -439,7 +439,9 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                          league=league, latest_weights_prob=latest_weights_prob, actor_precision=actor_precision,
                          replay_gb=replay_gb,
                          replay_sequences=(len(opt.replay) if opt is not None and opt.replay is not None else 0),
-                         replay_capacity=(opt.replay.capacity if opt is not None and opt.replay is not None else 0))
+                         replay_capacity=(opt.replay.capacity if opt is not None and opt.replay is not None else 0),
+                         replay_fill=(opt.replay.fill_fraction if opt is not None and opt.replay is not None else 0.),
+                         replay_prefill=replay_prefill)
     return out
 
 

@@ -78,6 +78,7 @@ class OptimizerConfig:
     replay_gb: float = 0.0             # on-HBM replay budget (GB); 0 with replay_capacity 0 = reference behaviour
     replay_capacity: int = 0           # sequences (overrides replay_gb)
     replay_recent: int = 0             # sample from the newest N sequences (0 = whole buffer)
+    replay_prefill: bool = False       # fill the ring to capacity from the first ingest (benchmarks, HbmReplay.prefill)
     ingest: str = 'auto'               # 'device' (HIP return/GAE scan over the uploaded rollouts) | 'host' | 'auto'
     artifact_url: Optional[str] = None  # off-node mirror of checkpoints + events (reference: GCS bucket, §utils.artifacts)
     allow_pickle_experience: bool = False  # accept reference-agent pickles (restricted unpickler); off: DCX1 only
@@ -621,6 +622,8 @@ class DotaOptimizer:
         if self.replay is not None:
             # fresh sequences go into the on-HBM ring; minibatches are sampled from it on-device
             self.replay.add(data, version=it)
+            if cfg.replay_prefill and self.replay.fill_fraction < 1.0:
+                self.replay.prefill()
             for _ in range(cfg.epochs * (n // cfg.batch_size)):
                 m = self.learner.train_step_replay(self.replay, cfg.batch_size, cfg.replay_recent or None)
                 losses.append(m['loss'])

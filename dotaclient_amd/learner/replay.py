@@ -112,6 +112,32 @@ class HbmReplay:
         self.inserted += n
         return n
 
+    def prefill(self) -> int:
+        """Fill the rest of the ring with copies of the sequences it already holds (device-to-device, doubling
+        spans: ≈2 bytes moved per byte filled, so 100 GB takes tens of ms at HBM rate) and mark the copies as
+        version -1. Benchmarks use it so a minibatch gathers from the whole ``capacity``-sized pool — the TLB and
+        HBM-page spread of a full 100-200 GB replay — from the first timed step, not from a few GB of fresh data.
+        New sequences keep landing at the cursor and overwrite the copies oldest-first. Returns the rows written."""
+        if self.size == 0:
+            raise RuntimeError('prefill needs at least one added sequence')
+        if self.size >= self.capacity:
+            return 0
+        # the held sequences are the ring's first `size` rows (the cursor has not wrapped yet)
+        have, wrote = self.size, 0
+        while have < self.capacity:
+            n = min(have, self.capacity - have)
+            for v in self.data.values():
+                v[have:have + n].copy_(v[:n])
+            self.version[have:have + n] = -1
+            have += n
+            wrote += n
+        self.size = self.capacity
+        return wrote
+
+    @property
+    def fill_fraction(self) -> float:
+        return self.size / self.capacity
+
     def _window(self, recent: Optional[int]):
         m = self.size if not recent else min(self.size, int(recent))
         return m

@@ -98,17 +98,18 @@ def test_exact_encoder_kernels_match_autograd_fp64(gpu_ops, preset, N):
 @pytest.mark.parametrize('algo,B', [('ppo', 8), ('vpg', 8), ('ppo', 16), ('ppo', 32)])
 def test_exact_fused_step_deploy_shape_matches_fp64(gpu_ops, algo, B):
     """fp32-exact at B=8, S=1400: every gradient tensor within 1e-5 (relative) of float64 — the bf16x3 headline mode
-    is pinned at 1e-3 (tests/test_fp32_kernels.py). VPG's ∂b1 / ∂W1 of the unit encoder sit at ≈1.2e-5 for the plain
-    torch-fp32 evaluation itself (the conditioning of that sum, not the kernels): there a tensor may reach 1.5× the
-    torch-fp32 error instead (measured: fused 1.01e-5 vs torch 1.22e-5). B = 16 / 32: the exact recurrence with 2 / 4
-    rows per XCD chain (lstm_team.hip V1 rows)."""
+    is pinned at 1e-3 (tests/test_fp32_kernels.py). The unit encoder's ∂W1 sits at ≈1.0-1.3e-5 for the plain torch-fp32
+    evaluation itself under VPG and at B = 16 / 32 (the conditioning of that 11 200 × 8-row sum, not the kernels):
+    there a tensor may reach 1.5× the torch-fp32 error instead (measured: fused 1.01e-5 vs torch 1.22e-5 VPG B=8,
+    1.03e-5 vs 1.05e-5 PPO B=16, 1.09e-5 vs 1.26e-5 PPO B=32). B = 16 / 32: the exact recurrence with 2 / 4 rows per
+    XCD chain (lstm_team.hip V1 rows)."""
     from tests.test_fp32_kernels import _rel, _step_grads
     (lf, _, gf), (lo, _, go), (l64, g64) = _step_grads('fp32-exact', 'lstm512', algo, B, 1400, fp64=True)
     rows = sorted(((_rel(gf[n], g64[n]), _rel(go[n], g64[n]), n) for n in g64
                    if g64[n] is not None and g64[n].norm() > 0), reverse=True)
     print(f'fp32-exact {algo} B={B}: worst (fused vs fp64, torch-fp32 vs fp64):', rows[:5], 'loss', lf, lo, l64)
     assert abs(lf - l64) <= 1e-6 * max(1e-2, abs(l64)), (lf, l64)
-    bad = [r for r in rows if r[0] >= max(1e-5, 1.5 * r[1] if algo == 'vpg' else 0.0)]
+    bad = [r for r in rows if r[0] >= max(1e-5, 1.5 * r[1])]
     assert not bad, bad[:5]
 
 

@@ -24,6 +24,20 @@ def test_ring_wraps_and_keeps_newest():
     assert r.version.tolist().count(2) == 2
 
 
+def test_prefill_replicates_to_capacity_and_new_rows_overwrite_copies():
+    r = HbmReplay(11, 4, LAYOUT_1V1, 32, 'cpu')
+    r.add(_batch(3, 4, 7, hidden=32), version=5)
+    assert r.fill_fraction == pytest.approx(3 / 11)
+    assert r.prefill() == 8 and len(r) == 11 and r.fill_fraction == 1.0
+    for k, v in r.data.items():                        # every row is a copy of one of the 3 added sequences
+        for i in range(11):
+            assert torch.equal(v[i], v[i % 3]), k
+    assert r.version.tolist() == [5, 5, 5] + [-1] * 8
+    r.add(_batch(2, 4, 9, hidden=32), version=6)        # lands at the cursor, over the oldest copies
+    assert r.cursor == 5 and r.version.tolist()[3:5] == [6, 6] and len(r) == 11
+    assert r.prefill() == 0
+
+
 def test_recent_window_sampling_only_returns_newest():
     r = HbmReplay(16, 4, LAYOUT_1V1, None, 'cpu', seed=1)
     for seed in range(8):
