@@ -26,8 +26,8 @@ EVERY rank (one actor runtime per GPU), and reported as node aggregates (sums ov
   rank 0 alone publishing the model. ``e2e.steps_per_s`` is the reference's own metric (optimizer.py:485-486, padded
   sequence steps incl. the wait for experience) summed over ranks; ``vs_baseline_e2e`` compares THAT with the
   reference's ≈1000 steps/s, the like-for-like node-level comparison (``vs_baseline`` is the compute-only learner);
-* ``model_5v5_exact`` — the 5v5 policy at IEEE fp32 (BASELINE config 4 at the reference precision): the torch backend,
-  since the fused attention-block kernels are bf16x3 only (``model_5v5`` is the fused bf16x3 number);
+* ``model_5v5_exact`` — the 5v5 policy at IEEE fp32 (BASELINE config 4 at the reference precision) on the fused
+  kernels (the attention block's exact-fp32 twins); ``model_5v5`` is the same step with bf16x3 operands;
 * ``bptt350_learner`` — truncated BPTT: each sequence trained as ``seq_len / 350`` chains of 350 steps from
   actor-stored (h, c) (32 sequences of 350 steps per step, at the headline's precision; not the headline);
 * ``learner_b16`` / ``learner_b32`` — the same learner at 16 / 32 sequences per GPU per step (the exact recurrence
@@ -36,7 +36,7 @@ EVERY rank (one actor runtime per GPU), and reported as node aggregates (sums ov
   latest weights), the fp8 actor policy step, and learners sampling every minibatch from an on-HBM replay of
   ``--league-replay-gb`` GB per GPU (``config.replay_capacity`` sequences).
 * ``e2e_5v5`` — BASELINE config 4 end to end: the same node loop on the 5v5 entity-attention model (5v5 self-play
-  actors, 10 players per game; the learner at bf16x3 operands, which the attention kernels need).
+  actors, 10 players per game; the learner at the headline precision — fp32-exact by default).
 
 Knobs for rehearsing the multi-rank path on one GPU: ``DCA_DIST_BACKEND=gloo`` and ``DCA_SHARED_GPU=1`` (every rank
 on cuda:0).
@@ -75,10 +75,10 @@ def parse():
     ap.add_argument('--bf16x3-extra', type=int, default=1,
                     help='also time the bf16x3-operand fp32 learner (extra field fp32_bf16x3_learner, not the headline)')
     ap.add_argument('--model-5v5-extra', type=int, default=1,
-                    help='also time the 5v5 entity-attention policy (BASELINE config 4) at the same B, S (bf16x3 '
-                         'operands: the attention kernels have no exact-fp32 variant)')
+                    help='also time the 5v5 entity-attention policy (BASELINE config 4) at the same B, S with bf16x3 '
+                         'operands (extra field model_5v5; model_5v5_exact is the fp32-exact number)')
     ap.add_argument('--model-5v5-exact-extra', type=int, default=1,
-                    help='also time the 5v5 policy at IEEE fp32 on the torch backend (extra field model_5v5_exact)')
+                    help='also time the 5v5 policy at fp32-exact on the fused kernels (extra field model_5v5_exact)')
     ap.add_argument('--bptt350-extra', type=int, default=1,
                     help='also time truncated BPTT: each sequence as seq_len/350 chains of 350 steps from stored '
                          '(h, c) (extra field bptt350_learner, headline precision; not the headline)')
@@ -224,9 +224,6 @@ def main():
 
     cfg = get_config(args.model)
     trace = os.environ.get('DCA_BENCH_TRACE') == '1'
-    if cfg.entity_attention and args.precision == 'fp32-exact':
-        progress('5v5 entity attention has no exact-fp32 kernels: timing it at fp32 with bf16x3 operands')
-        args.precision = 'fp32'
 
     def run(precision, cfg=cfg, B=None, S=None, backend=None, steps=None, warmup=None):
         """Build a learner of this precision and time ``args.steps`` DP PPO steps (``B`` sequences of ``S`` steps,
@@ -328,21 +325,15 @@ def main():
 
     model_5v5_exact = None
     if args.model_5v5_exact_extra and use_cuda and not cfg.entity_attention:
-        # the 5v5 policy at the reference's precision: the fused kernels have no exact-fp32 attention block yet, so
-        # this is the torch backend (autograd, fp32 torch ops with TF32 off — the reference's own execution model)
+        # the 5v5 policy at the reference's precision on the fused kernels: the IEEE-fp32 twins of the attention block
+        # (ops/csrc/attn_block.hip EX), the exact encoder / recurrence / heads kernels, exact split-K ∂W GEMMs
         learner = None
         try:
-            n5 = max(1, min(args.steps, 5))
-            prev_tf32 = torch.backends.cuda.matmul.allow_tf32
-            torch.backends.cuda.matmul.allow_tf32 = False
-            try:
-                e5x, l0, l1, _, _ = run('fp32', get_config('5v5'), backend='torch', steps=n5, warmup=1)
-            finally:
-                torch.backends.cuda.matmul.allow_tf32 = prev_tf32
-            progress(f'learner 5v5 exact (torch) done: {e5x / n5 * 1e3:.3f} ms/step')
-            model_5v5_exact = {'model': '5v5', 'precision': 'IEEE fp32 (torch backend: autograd, fp32 ops, TF32 off)',
-                               'value': args.batch_size * args.seq_len * world * n5 / e5x,
-                               'ms_per_step': e5x / n5 * 1e3, 'steps': n5, 'loss_first': l0, 'loss_last': l1}
+            e5x, l0, l1, _, _ = run('fp32-exact', get_config('5v5'))
+            progress(f'learner 5v5 fp32-exact done: {e5x / args.steps * 1e3:.3f} ms/step')
+            model_5v5_exact = {'model': '5v5', 'precision': 'fp32-exact (IEEE fp32 products, hand-written kernels)',
+                               'value': samples / e5x, 'ms_per_step': e5x / args.steps * 1e3, 'loss_first': l0,
+                               'loss_last': l1}
         except Exception as e:
             model_5v5_exact = {'error': repr(e)}
 
@@ -504,8 +495,8 @@ def main():
     if args.e2e_5v5_extra < 0:
         args.e2e_5v5_extra = 15.0 if world == 1 else 0.0
     if args.e2e_5v5_extra > 0 and use_cuda and args.e2e_mode == 'process' and args.model != '5v5':
-        # BASELINE config 4 end to end: the same node loop on the 5v5 model (entity attention, bf16x3 learner — it has
-        # no exact-fp32 kernels), 5v5 self-play games on the VecActor (410 games = 4 100 player slots)
+        # BASELINE config 4 end to end: the same node loop on the 5v5 model (entity attention, the learner at the
+        # headline precision), 5v5 self-play games on the VecActor (e2e_games / 5 games, 10 player slots each)
         try:
             from dotaclient_amd.learner.e2e import measure_e2e_node
             progress('e2e-5v5 start')

@@ -25,10 +25,17 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
                        max_dota_time: float = 600.0, pack: bool = True, seed: int = 7, device: str = 'cuda',
                        eval_seed: int = 4242, on_row: Optional[Callable[[Dict], None]] = None,
                        save_model: Optional[str] = None, eval_precision: str = 'fp32',
-                       mode: str = '1v1') -> List[Dict]:
+                       mode: str = '1v1', log_dir: Optional[str] = None) -> List[Dict]:
     """Train for ``budget`` seconds (evaluations excluded) and return the evaluation rows (the first one before
     any training). ``on_row`` is called with every row as it is produced; ``save_model``: path that receives the
-    final weights (a reference-format state_dict file). ``eval_precision``: the validation games' policy step."""
+    final weights (a reference-format state_dict file). ``eval_precision``: the validation games' policy step.
+
+    ``log_dir``: keep the optimizer's checkpoints there (the latest one only) and resume from them — model, Adam
+    state and return normalisers (DotaOptimizer's resume) plus the curve's own counters (``curve_state.json``), so a
+    long curve runs as several shorter jobs; ``budget`` is then the total, counted from the first job."""
+    import json
+    import os
+
     import torch
     from ..actor.validate import evaluate_vs_default_bot
     from ..actor.vec import VecActor
@@ -37,11 +44,18 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
     from .optimizer import DotaOptimizer, OptimizerConfig
 
     torch.manual_seed(seed)
-    tmp = tempfile.mkdtemp(prefix='dca_curve_')
+    tmp = log_dir or tempfile.mkdtemp(prefix='dca_curve_')
+    os.makedirs(tmp, exist_ok=True)
+    state_path = os.path.join(tmp, 'curve_state.json')
+    resumed = {}
+    if log_dir and os.path.exists(state_path):
+        with open(state_path) as fh:
+            resumed = json.load(fh)
     broker = InProcBroker(maxsize=256, drop_oldest=True)
     cfg = OptimizerConfig(log_dir=tmp, epochs=1, seq_per_epoch=seq_per_epoch, batch_size=batch_size,
                           seq_len=seq_len, model=model, precision=precision, device=device, backend=backend,
-                          learning_rate=lr, entropy_coef=entropy_coef, checkpoint_keep=2, run_local=True,
+                          learning_rate=lr, entropy_coef=entropy_coef, checkpoint_keep=1 if log_dir else 2,
+                          run_local=True,
                           xp_timeout=300.0, histogram_freq=10 ** 9, async_checkpoint=True, prefetch_rollouts=64,
                           pack_sequences=bool(pack), seed=seed)
     opt = DotaOptimizer(cfg, broker)
@@ -84,12 +98,22 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
             on_row(row)
 
     th = threading.Thread(target=actor_loop, daemon=True)
-    trained, samples, it = 0.0, 0, opt.iteration_start
+    trained, samples, it = float(resumed.get('t_train', 0.0)), int(resumed.get('samples', 0)), opt.iteration_start
+    steps0 = int(resumed.get('actor_steps', 0))
+    if resumed and it - 1 != resumed.get('iteration'):
+        raise RuntimeError(f'curve state at iteration {resumed.get("iteration")} but the checkpoint is {it - 1}')
+
+    def save_state():
+        if log_dir:
+            with open(state_path, 'w') as fh:
+                json.dump({'t_train': trained, 'samples': samples, 'actor_steps': steps0 + va.steps_taken,
+                           'iteration': it - 1}, fh)
     try:
-        evaluate({'t_train': 0.0, 'iteration': 0, 'samples': 0, 'actor_steps': 0, 'model': model,
-                  'precision': precision, 'backend': backend, 'pack': bool(pack)})
+        if not resumed:
+            evaluate({'t_train': 0.0, 'iteration': 0, 'samples': 0, 'actor_steps': 0, 'model': model,
+                      'precision': precision, 'backend': backend, 'pack': bool(pack)})
         th.start()
-        next_eval = eval_every
+        next_eval = (int(trained // eval_every) + 1) * eval_every
         while trained < budget:
             t0 = time.time()
             opt.run_iteration(it)
@@ -100,8 +124,8 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
                 raise err[0]
             if trained >= next_eval or trained >= budget:
                 m = getattr(opt, 'last_metrics', {}) or {}
-                evaluate({'t_train': round(trained, 1), 'iteration': it - opt.iteration_start, 'samples': samples,
-                          'actor_steps': va.steps_taken, 'loss': m.get('loss/sum'), 'entropy': m.get('entropy'),
+                evaluate({'t_train': round(trained, 1), 'iteration': it - 1, 'samples': samples,
+                          'actor_steps': steps0 + va.steps_taken, 'resumed': bool(resumed), 'loss': m.get('loss/sum'), 'entropy': m.get('entropy'),
                           'train_reward_per_sec': m.get('reward_per_sec/sum'),
                           'avg_weight_age': m.get('avg_weight_age')})
                 next_eval += eval_every
@@ -116,5 +140,6 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
         opt.close()
         va.close()
         opt.flush_checkpoints()
+        save_state()
         loader.shutdown(wait=True)
     return rows

@@ -177,13 +177,9 @@ class DotaOptimizer:
                         vf_coef=cfg.vf_coef, clip_eps=cfg.clip_eps, gamma=cfg.gamma, gae_lambda=cfg.gae_lambda,
                         max_grad_norm=cfg.max_grad_norm, compat_value_bug=cfg.compat_value_bug)
         prec = cfg.precision
-        if prec == 'fp32-exact' and self.policy_cfg.entity_attention:
-            logger.info('5v5 entity attention has no exact-fp32 kernels: training at fp32 with bf16x3 operands')
-            prec = 'fp32'
-        if prec == 'fp32-exact' and self.device.type == 'cuda' and cfg.batch_size > 8:
-            # the exact VALU recurrence runs one sequence per XCD team (8 teams); larger minibatches pack several
-            # rows per chain on the bf16x3 MFMA team kernel
-            logger.info('fp32-exact takes at most 8 sequences per minibatch and GPU: training at fp32 with bf16x3 '
+        if prec == 'fp32-exact' and self.device.type == 'cuda' and cfg.batch_size > 32:
+            # the exact VALU recurrence runs 1 / 2 / 4 sequences per XCD chain (8 teams): at most 32 per minibatch
+            logger.info('fp32-exact takes at most 32 sequences per minibatch and GPU: training at fp32 with bf16x3 '
                         'operands (batch_size %d)', cfg.batch_size)
             prec = 'fp32'
         self.learner = Learner(self.policy, lc, device=self.device, backend=cfg.backend, precision=prec)

@@ -29,7 +29,8 @@ Precision (``FusedPolicy(precision=...)``):
 * ``'bf16'``: bf16 GEMM operands / saved activations, fp32 accumulation, recurrence state and optimizer.
 
 The 5v5 entity-attention block runs on its bf16 kernels (ops/csrc/attn.hip) in the bf16 learner and on the fp32
-(bf16x3) block kernels (ops/csrc/attn_block.hip) in the fp32 learner. Configurations the kernels do not cover (unit /
+block kernels (ops/csrc/attn_block.hip) in the fp32 learners: bf16x3 products at ``'fp32'``, their IEEE-fp32 twins
+(``v_mfma_f32_16x16x4_f32``) at ``'fp32-exact'``. Configurations the kernels do not cover (unit /
 env widths other than 128, the linear layer below fp32) run on the torch backend (learner/engine.py).
 """
 from __future__ import annotations
@@ -57,8 +58,6 @@ class FusedPolicy:
         # 'fp32-exact': IEEE fp32 products everywhere (no bf16x3 split): the exact-f32 MFMA / VALU twins of every
         # kernel of the step (models/pipelined.py)
         self.exact = precision == 'fp32-exact'
-        if self.exact and policy.config.entity_attention:
-            raise ValueError('fp32-exact covers the 1v1 policies (the entity-attention kernels are bf16x3 only)')
         dev = next(policy.parameters()).device
         self.err = torch.zeros(1, dtype=torch.int32, device=dev)
         self.param_names: List[str] = [n for n, _ in policy.named_parameters()]

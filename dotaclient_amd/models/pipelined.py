@@ -172,7 +172,15 @@ class WeightImages:
                 partsS['wcat_s'] = slab(wcat_p)
                 partsS['wcatT_s'] = slab(wcat_p.t())
                 parts32['bcat256'] = (torch.cat([bcat, neg(256 - LDZ)]), None)
-            if cfg.entity_attention:
+            if cfg.entity_attention and getattr(fp, 'exact', False):
+                # the IEEE-fp32 attention block's fp32 weight images, in the fragment orders of its forward (W_qkv,
+                # W_out) and backward (W_outᵀ, W_qkv k16) — gathered here, no per-step split or permute launches
+                wq_i, wo_i = idx('entity_attn.qkv.weight'), idx('entity_attn.out.weight')
+                parts32['wq_x'] = (_frag_order(wq_i), None)
+                parts32['wo_x'] = (_frag_order(wo_i), None)
+                parts32['wot_x'] = (_frag_order(wo_i.t().contiguous()), None)
+                parts32['wq4_x'] = (_k16_order(wq_i), None)
+            elif cfg.entity_attention:
                 # the fused attention block's W_qkv / W_out hi / lo images in MFMA fragment order (attn_block.hip),
                 # from this same gather instead of two split + two permute-copy launches before the block
                 partsS['wq_f'] = _frag_order(idx('entity_attn.qkv.weight'))
@@ -229,6 +237,7 @@ class WeightImages:
 #   (∂G·W_ih)⊙[x>0]·W_pre are hand-written kernels (ops/csrc/dx_chain.hip), not vendor GEMMs;
 # * the fp32 5v5 attention block forward and backward are one kernel each (ops/csrc/attn_block.hip; the five-launch
 #   backward took 1858 vs 1660 µs), ∂W_out / ∂W_qkv on the side stream after the encoder backward (8.10 vs 8.13 ms);
+#   fp32-exact runs their IEEE-fp32 twins (the same kernels templated on the operand precision);
 # * the exact recurrence's gate activations use the hardware exp / reciprocal: products-exact, the same worst
 #   tensor errors against float64 as libm expf / tanhf (PPO 2.50e-6 both), 0.5 ms per step faster.
 
@@ -328,7 +337,10 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             bqkv = P['entity_attn.qkv.bias'].detach()
             # one kernel per step; E0' stays untouched (the LayerNorm backward's input), E1 is a new tensor
             E0p = emb.view(N * U, 128)
-            if 'wq_f' in W:                    # hi / lo fragment images from the step's weight_prep launch
+            if exact:                          # fp32 fragment images: the IEEE-fp32 block kernel
+                nil = E0p.new_empty(0)
+                wq, wo = (W['wq_x'], nil), (W['wo_x'], nil)
+            elif 'wq_f' in W:                  # hi / lo fragment images from the step's weight_prep launch
                 wq, wo = W['wq_f'], W['wo_f']
             else:
                 wq = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.qkv.weight'].detach())]
@@ -590,8 +602,12 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         if attn32:
             # one kernel from ∂x896 / the pointer gradient to ∂E0; the two weight-gradient GEMMs over the N·U unit
             # rows (∂W_out = ∂E1ᵀ·O, ∂W_qkv = ∂QKVᵀ·Xn, with their bias column sums) go to the recurrence stream
-            wot = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.out.weight'].detach().t().contiguous())]
-            wq4 = [_k16_order(t) for t in C.split_bf16x2(P['entity_attn.qkv.weight'].detach())]
+            if exact:
+                nil = E0p.new_empty(0)
+                wot, wq4 = (W['wot_x'], nil), (W['wq4_x'], nil)
+            else:
+                wot = [_frag_order(t) for t in C.split_bf16x2(P['entity_attn.out.weight'].detach().t().contiguous())]
+                wq4 = [_k16_order(t) for t in C.split_bf16x2(P['entity_attn.qkv.weight'].detach())]
             dE1, dQKV, demb_in, lnsum = C.attn_block_bwd(
                 dtl, z, dx896, arg, toff, bool(cfg.compat_bugs), Oat, QKV, bqkv, lse, E0p, W['bout'], ln_mu, ln_rs,
                 P['entity_attn.ln.weight'].detach(), wot[0], wot[1], wq4[0], wq4[1], None)

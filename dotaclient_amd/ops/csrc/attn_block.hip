@@ -38,8 +38,8 @@ constexpr int kPE = 132;            // fp32 pitch of the E1 image
 struct BlockArgs {
   const float* e0;                  // (N·64, 128) E0' = E0 + b_out
   const float* bout; const float* gamma; const float* beta;
-  const short* wqh; const short* wql; const float* bq;     // (384, 128) bf16 hi / lo, bias (384)
-  const short* woh; const short* wol;                      // (128, 128)
+  const void* wqh; const void* wql; const float* bq;       // (384, 128) bf16 hi / lo (EX: fp32, wql unused), bias
+  const void* woh; const void* wol;                        // (128, 128)
   float* xn; float* mu; float* rs;                         // (N·64, 128), (N·64), (N·64)
   float* qkv; float* o; float* lse;                        // (N·64, 384) without bias, (N·64, 128), (N, 4, 64)
   float* e1;                                               // (N·64, 128)
@@ -85,10 +85,120 @@ __device__ __forceinline__ bf16x8 gfrag(const short* __restrict__ w, int m0, int
   return *reinterpret_cast<const bf16x8*>(w + ((size_t)((m0 >> 4) * (kD / 32) + (k0 >> 5)) * 64 + lane) * 8);
 }
 
+// Operand abstraction of the two precisions. EX = false: bf16x3 — an operand is a (hi, lo) bf16 pair, a product three
+// bf16 MFMAs (hi·hi + lo·hi + hi·lo). EX = true: IEEE fp32 — the operand is the fp32 values themselves and a K = 32
+// (K = 16) step is 8 (4) v_mfma_f32_16x16x4_f32 calls: sub-step j takes k = 8·(lane>>4) + j (4·(lane>>4) + j) of
+// the lane's k-group, i.e. exactly the elements the bf16 lane layout holds, so every fragment load, accumulator
+// layout and LDS image of the bf16x3 form carries over with fp32 in place of the (hi, lo) pair — and the same
+// register count (8 floats = a bf16x8 hi + lo pair). Every product is then an fp32 fma (the fp32-exact learner).
+template <bool EX> struct F8;
+template <> struct F8<false> { bf16x8 h, l; };
+template <> struct F8<true> { float v[8]; };
+template <bool EX> struct F4;
+template <> struct F4<false> { bf16x4v h, l; };
+template <> struct F4<true> { f32x4 v; };
+
+template <bool EX>
+__device__ __forceinline__ F8<EX> mk8(const float* v) {
+  F8<EX> f;
+  if constexpr (EX) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) f.v[j] = v[j];
+  } else {
+    split8v(v, f.h, f.l);
+  }
+  return f;
+}
+template <bool EX>
+__device__ __forceinline__ F4<EX> mk4(const f32x4 v) {
+  F4<EX> f;
+  if constexpr (EX) f.v = v;
+  else split4v(v, f.h, f.l);
+  return f;
+}
+template <bool EX>
+__device__ __forceinline__ f32x4 mma8(const F8<EX>& a, const F8<EX>& b, f32x4 c) {
+  if constexpr (EX) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[j], b.v[j], c, 0, 0, 0);
+    return c;
+  } else {
+    return mfma3(a.h, a.l, b.h, b.l, c);
+  }
+}
+template <bool EX>
+__device__ __forceinline__ f32x4 mma4(const F4<EX>& a, const F4<EX>& b, f32x4 c) {
+  if constexpr (EX) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) c = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[j], b.v[j], c, 0, 0, 0);
+    return c;
+  } else {
+    return mfma3k16(a.h, a.l, b.h, b.l, c);
+  }
+}
+__device__ __forceinline__ void ld8(const float* p, float (&v)[8]) {
+  const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+// weight fragment (gfrag's order) of either precision: EX reads the fp32 image [row tile][k-step][lane][8] from wh
+template <bool EX>
+__device__ __forceinline__ F8<EX> wfrag8(const void* wh, const void* wl, int m0, int k0, int lane) {
+  F8<EX> f;
+  if constexpr (EX) {
+    ld8(static_cast<const float*>(wh) + ((size_t)((m0 >> 4) * (kD / 32) + (k0 >> 5)) * 64 + lane) * 8, f.v);
+  } else {
+    f.h = gfrag(static_cast<const short*>(wh), m0, k0, lane);
+    f.l = gfrag(static_cast<const short*>(wl), m0, k0, lane);
+  }
+  return f;
+}
+// the fwd kernel's Xn / O image: bf16 hi ‖ lo [64][kPX] (EX = false) or fp32 [64][kPE] (EX = true), same footprint
+constexpr int kImgBytes = 2 * kU * kPX * 2;
+static_assert(kU * kPE * 4 <= kImgBytes, "fp32 image must fit the bf16 pair");
+template <bool EX>
+__device__ __forceinline__ F8<EX> ifrag(const char* img, int m0, int k0, int lane) {
+  F8<EX> f;
+  if constexpr (EX) {
+    ld8(reinterpret_cast<const float*>(img) + (m0 + (lane & 15)) * kPE + k0 + 8 * (lane >> 4), f.v);
+  } else {
+    const short* h = reinterpret_cast<const short*>(img);
+    f.h = frag(h, kPX, m0, k0, lane);
+    f.l = frag(h + kU * kPX, kPX, m0, k0, lane);
+  }
+  return f;
+}
+// 8 consecutive values of row u from column c into the image
+template <bool EX>
+__device__ __forceinline__ void iput8(char* img, int u, int c, const float* x) {
+  if constexpr (EX) {
+    float* d = reinterpret_cast<float*>(img) + u * kPE + c;
+    *reinterpret_cast<float4*>(d) = make_float4(x[0], x[1], x[2], x[3]);
+    *reinterpret_cast<float4*>(d + 4) = make_float4(x[4], x[5], x[6], x[7]);
+  } else {
+    bf16x8 hi, lo;
+    split8v(x, hi, lo);
+    short* h = reinterpret_cast<short*>(img);
+    *reinterpret_cast<bf16x8*>(h + u * kPX + c) = hi;
+    *reinterpret_cast<bf16x8*>(h + kU * kPX + u * kPX + c) = lo;
+  }
+}
+template <bool EX>
+__device__ __forceinline__ void iput1(char* img, int i, int col, float v) {
+  if constexpr (EX) {
+    reinterpret_cast<float*>(img)[i * kPE + col] = v;
+  } else {
+    short* h = reinterpret_cast<short*>(img);
+    const short hi = dca::f2bf(v);
+    h[i * kPX + col] = hi;
+    h[kU * kPX + i * kPX + col] = dca::f2bf(v - dca::bf2f(hi));
+  }
+}
+
 // Two rows in flight per CU (256 VGPRs). (Measured slower and removed: one row per CU with the phase-B weight
-// fragments double-buffered one k-step ahead — 5v5 step 8.45 vs 8.15 ms.)
+// fragments double-buffered one k-step ahead — 5v5 step 8.45 vs 8.15 ms.) EX: the IEEE-fp32 twin (F8 / F4 above).
+template <bool EX>
 __global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P) {
-  __shared__ __attribute__((aligned(16))) short img_h[kU * kPX], img_l[kU * kPX];   // Xn, then O (hi / lo)
+  __shared__ __attribute__((aligned(16))) char img[kImgBytes];                   // Xn, then O
   __shared__ __attribute__((aligned(16))) float e1s[kU * kPE];
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63, kg = lane >> 4, li = lane & 15;
   const int n = blockIdx.x;
@@ -129,12 +239,7 @@ __global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P)
     for (int i = 0; i < 8; ++i)
       *reinterpret_cast<float4*>(dst + 4 * i) = make_float4(x[4 * i], x[4 * i + 1], x[4 * i + 2], x[4 * i + 3]);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      bf16x8 hi, lo;
-      split8v(x + 8 * i, hi, lo);
-      *reinterpret_cast<bf16x8*>(img_h + u * kPX + 32 * p + 8 * i) = hi;
-      *reinterpret_cast<bf16x8*>(img_l + u * kPX + 32 * p + 8 * i) = lo;
-    }
+    for (int i = 0; i < 4; ++i) iput8<EX>(img, u, 32 * p + 8 * i, x + 8 * i);
     if (p == 0) {
       P.mu[rbase + u] = mu;
       P.rs[rbase + u] = rs;
@@ -157,23 +262,20 @@ __global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P)
   {
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks) {
-    bf16x8 xh[4], xl[4];
+    F8<EX> xf[4];
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      xh[a] = frag(img_h, kPX, 16 * a, 32 * ks, lane);
-      xl[a] = frag(img_l, kPX, 16 * a, 32 * ks, lane);
-    }
+    for (int a = 0; a < 4; ++a) xf[a] = ifrag<EX>(img, 16 * a, 32 * ks, lane);
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const int rq = kHd * h + 16 * c;
-      const bf16x8 qwh = gfrag(P.wqh, rq, 32 * ks, lane), qwl = gfrag(P.wql, rq, 32 * ks, lane);
-      const bf16x8 kwh = gfrag(P.wqh, 128 + rq, 32 * ks, lane), kwl = gfrag(P.wql, 128 + rq, 32 * ks, lane);
-      const bf16x8 vwh = gfrag(P.wqh, 256 + rq, 32 * ks, lane), vwl = gfrag(P.wql, 256 + rq, 32 * ks, lane);
+      const F8<EX> qw = wfrag8<EX>(P.wqh, P.wql, rq, 32 * ks, lane);
+      const F8<EX> kw = wfrag8<EX>(P.wqh, P.wql, 128 + rq, 32 * ks, lane);
+      const F8<EX> vw = wfrag8<EX>(P.wqh, P.wql, 256 + rq, 32 * ks, lane);
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
-        qt[c][a] = mfma3(qwh, qwl, xh[a], xl[a], qt[c][a]);    // m = d (weight row), n = unit
-        kt[c][a] = mfma3(kwh, kwl, xh[a], xl[a], kt[c][a]);
-        vv[a][c] = mfma3(xh[a], xl[a], vwh, vwl, vv[a][c]);    // m = unit, n = d
+        qt[c][a] = mma8<EX>(qw, xf[a], qt[c][a]);    // m = d (weight row), n = unit
+        kt[c][a] = mma8<EX>(kw, xf[a], kt[c][a]);
+        vv[a][c] = mma8<EX>(xf[a], vw, vv[a][c]);    // m = unit, n = d
       }
     }
   }
@@ -196,7 +298,7 @@ __global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P)
 
   // ---- C: attention of head h. Biases first (q / k: per (c, r) row of the lane, v: per column li)
   {
-    bf16x4v qh[2][4], ql[2][4], khv[2][4], klv[2][4];
+    F4<EX> qf[2][4], kf[2][4];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       f32x4 bqv, bkv;
@@ -207,8 +309,8 @@ __global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P)
       }
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
-        split4v(qt[c][a] + bqv, qh[c][a], ql[c][a]);
-        split4v(kt[c][a] + bkv, khv[c][a], klv[c][a]);
+        qf[c][a] = mk4<EX>(qt[c][a] + bqv);
+        kf[c][a] = mk4<EX>(kt[c][a] + bkv);
       }
     }
     // Sᵀ[b][a]: lane (key j = 16b + 4kg + r, query i = 16a + li)
@@ -219,7 +321,7 @@ __global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P)
       for (int a = 0; a < 4; ++a) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int c = 0; c < 2; ++c) acc = mfma3k16(khv[c][b], klv[c][b], qh[c][a], ql[c][a], acc);
+        for (int c = 0; c < 2; ++c) acc = mma4<EX>(kf[c][b], qf[c][a], acc);
         s[b][a] = acc;
       }
     float* lse = P.lse + ((size_t)n * 4 + h) * kU;
@@ -250,32 +352,30 @@ __global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P)
       if (kg == 0) lse[16 * a + li] = m + __logf(sum);
     }
     // O = P·V: A[m = i][k = j] = s[b][a], B[k = j][n = d] = v[b][c] (+ bias of column d)
-    bf16x4v vh[4][2], vl[4][2];
+    F4<EX> vf[4][2];
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       const float bv = P.bq[256 + kHd * h + 16 * c + li];
 #pragma unroll
-      for (int b = 0; b < 4; ++b) split4v(vv[b][c] + bv, vh[b][c], vl[b][c]);
+      for (int b = 0; b < 4; ++b) vf[b][c] = mk4<EX>(vv[b][c] + bv);
     }
     float* ob = P.o + rbase * kD;
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
-      bf16x4v ph[4], pl[4];
+      F4<EX> pf[4];
 #pragma unroll
-      for (int b = 0; b < 4; ++b) split4v(s[b][a], ph[b], pl[b]);
+      for (int b = 0; b < 4; ++b) pf[b] = mk4<EX>(s[b][a]);
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int b = 0; b < 4; ++b) acc = mfma3k16(ph[b], pl[b], vh[b][c], vl[b][c], acc);
+        for (int b = 0; b < 4; ++b) acc = mma4<EX>(pf[b], vf[b][c], acc);
         const int col = kHd * h + 16 * c + li;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int i = 16 * a + 4 * kg + r;
           ob[(size_t)i * kD + col] = acc[r];
-          const short hi = dca::f2bf(acc[r]);
-          img_h[i * kPX + col] = hi;
-          img_l[i * kPX + col] = dca::f2bf(acc[r] - dca::bf2f(hi));
+          iput1<EX>(img, i, col, acc[r]);
         }
       }
     }
@@ -291,17 +391,14 @@ __global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P)
       for (int t = 0; t < 2; ++t) acc[a][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      bf16x8 wh[2], wl[2];
+      F8<EX> wf[2];
 #pragma unroll
-      for (int t = 0; t < 2; ++t) {
-        wh[t] = gfrag(P.woh, 16 * (2 * w + t), 32 * ks, lane);
-        wl[t] = gfrag(P.wol, 16 * (2 * w + t), 32 * ks, lane);
-      }
+      for (int t = 0; t < 2; ++t) wf[t] = wfrag8<EX>(P.woh, P.wol, 16 * (2 * w + t), 32 * ks, lane);
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
-        const bf16x8 oh = frag(img_h, kPX, 16 * a, 32 * ks, lane), ol = frag(img_l, kPX, 16 * a, 32 * ks, lane);
+        const F8<EX> of = ifrag<EX>(img, 16 * a, 32 * ks, lane);
 #pragma unroll
-        for (int t = 0; t < 2; ++t) acc[a][t] = mfma3(oh, ol, wh[t], wl[t], acc[a][t]);
+        for (int t = 0; t < 2; ++t) acc[a][t] = mma8<EX>(of, wf[t], acc[a][t]);
       }
     }
 #pragma unroll
@@ -377,8 +474,8 @@ struct BwdArgs {
   const float* dtl; const float* q; const float* dx; const unsigned char* arg;   // demb inputs (q row stride ldq)
   const float* o; const float* qkv; const float* bq; const float* lse;           // saved by the forward
   const float* e0; const float* bout; const float* mu; const float* rs; const float* gamma;
-  const short* woth; const short* wotl;     // W_outᵀ (d, c) in 16x16x32 fragment order, bf16 hi / lo
-  const short* wq4h; const short* wq4l;     // W_qkv (384, 128) in 16x16x16 B-fragment order, bf16 hi / lo
+  const void* woth; const void* wotl;       // W_outᵀ (d, c) in 16x16x32 fragment order, bf16 hi / lo (EX: fp32)
+  const void* wq4h; const void* wq4l;       // W_qkv (384, 128) in 16x16x16 B-fragment order, bf16 hi / lo (EX: fp32)
   float* de1; float* dqkv; float* de0; float* part;
   unsigned long long* trace;                // optional phase timestamps (s_memrealtime) of rows < 64: [row][wave][8]
   int off[7];
@@ -413,6 +510,51 @@ __device__ __forceinline__ bf16x8 frag_tr(const short* img, int k0, int c0, int 
 }
 __device__ __forceinline__ void lds_wait() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
+// EX helpers of the backward: the 16x16x16 weight fragment (gfrag4's order) and the per-wave transposed images —
+// fp32 [rows][kPF] instead of the bf16 hi / lo pair [rows][kPS] (26 KB of a 33 KB slot), read transposed by scalar
+// LDS reads (element jj of lane l = img[k0 + 8(l>>4) + jj][c0 + (l&15)], as frag_tr)
+constexpr int kPF = 68;
+static_assert(96 * kPF <= kSlot, "fp32 transposed images must fit a slot");
+template <bool EX>
+__device__ __forceinline__ F4<EX> wfrag4(const void* wh, const void* wl, int rt, int ct, int lane) {
+  F4<EX> f;
+  if constexpr (EX) {
+    f.v = *reinterpret_cast<const f32x4*>(static_cast<const float*>(wh) + ((size_t)(rt * 8 + ct) * 64 + lane) * 4);
+  } else {
+    f.h = gfrag4(static_cast<const short*>(wh), rt, ct, lane);
+    f.l = gfrag4(static_cast<const short*>(wl), rt, ct, lane);
+  }
+  return f;
+}
+// one C-layout accumulator (rows 4kg + r of column li at (row0, col0)) transposed into the image: element r goes to
+// img[col0 + li][row0 + 4kg + r] — a 16-B store (EX) or two 8-B stores (hi, lo)
+template <bool EX>
+__device__ __forceinline__ void tput(void* ih, void* il, int col0, int row0, const f32x4& v, int lane) {
+  const int li = lane & 15, kg = lane >> 4;
+  if constexpr (EX) {
+    *reinterpret_cast<f32x4*>(static_cast<float*>(ih) + (col0 + li) * kPF + row0 + 4 * kg) = v;
+  } else {
+    bf16x4v hi, lo;
+    split4v(v, hi, lo);
+    *reinterpret_cast<bf16x4v*>(static_cast<short*>(ih) + (col0 + li) * kPS + row0 + 4 * kg) = hi;
+    *reinterpret_cast<bf16x4v*>(static_cast<short*>(il) + (col0 + li) * kPS + row0 + 4 * kg) = lo;
+  }
+}
+template <bool EX>
+__device__ __forceinline__ F8<EX> tfrag2(const void* ih, const void* il, int k0, int c0, int lane) {
+  F8<EX> f;
+  if constexpr (EX) {
+    const float* b = static_cast<const float*>(ih) + (k0 + 8 * (lane >> 4)) * kPF + c0 + (lane & 15);
+#pragma unroll
+    for (int jj = 0; jj < 8; ++jj) f.v[jj] = b[jj * kPF];
+  } else {
+    f.h = frag_tr(static_cast<const short*>(ih), k0, c0, lane);
+    f.l = frag_tr(static_cast<const short*>(il), k0, c0, lane);
+  }
+  return f;
+}
+
+template <bool EX>
 __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
   __shared__ __attribute__((aligned(16))) float sm[4 * kSlot];
   __shared__ float sd[kU];
@@ -424,14 +566,11 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
   if (P.trace && n < 64 && lane == 0) P.trace[((size_t)n * 4 + w) * 8 + (ev)] = __builtin_amdgcn_s_memrealtime()
   PSTAMP(0);
   // phase 1's W_outᵀ fragments (head w) requested first: their round trip runs alongside phase 0's
-  bf16x8 wfh[4][2], wfl[4][2];
+  F8<EX> wf[4][2];
 #pragma unroll
   for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      wfh[ks][t] = gfrag(P.woth, kHd * w + 16 * t, 32 * ks, lane);
-      wfl[ks][t] = gfrag(P.wotl, kHd * w + 16 * t, 32 * ks, lane);
-    }
+    for (int t = 0; t < 2; ++t) wf[ks][t] = wfrag8<EX>(P.woth, P.wotl, kHd * w + 16 * t, 32 * ks, lane);
   // ---- 0: ∂E1 (thread: column c, units 32·(tid>>7) … +31)
   if (tid < kU) sd[tid] = P.dtl[(size_t)n * kU + tid];
   {
@@ -489,30 +628,32 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
   for (int ks = 0; ks < 4; ++ks) {
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
-      bf16x8 ah, al;
-      split8v(&sm[(16 * a + li) * kPT + 32 * ks + 8 * kg], ah, al);
+      const F8<EX> af = mk8<EX>(&sm[(16 * a + li) * kPT + 32 * ks + 8 * kg]);
 #pragma unroll
-      for (int t = 0; t < 2; ++t) dO[a][t] = mfma3(ah, al, wfh[ks][t], wfl[ks][t], dO[a][t]);
+      for (int t = 0; t < 2; ++t) dO[a][t] = mma8<EX>(af, wf[ks][t], dO[a][t]);
     }
   }
   __syncthreads();                                        // slot 0 (∂E1 image) is wave 0's from here on
 
   PSTAMP(2);
-  // ---- 2: attention backward of head h
-  short* const dTh = reinterpret_cast<short*>(sm + h * kSlot);        // ∂Oᵀ [32 d][kPS] hi / lo
-  short* const dTl = dTh + 32 * kPS;
-  short* const STh = dTh + 64 * kPS;                                  // (scale·∂S)ᵀ [64 j][kPS] hi / lo
-  short* const STl = STh + 64 * kPS;
+  // ---- 2: attention backward of head h. Per-wave images in slot h: ∂Oᵀ [32 d] and (scale·∂S)ᵀ [64 j] — bf16 hi / lo
+  //      pairs of pitch kPS, or (EX) fp32 of pitch kPF
+  void *dTh, *dTl, *STh, *STl;
+  if constexpr (EX) {
+    dTh = dTl = sm + h * kSlot;
+    STh = STl = sm + h * kSlot + 32 * kPF;
+  } else {
+    short* b = reinterpret_cast<short*>(sm + h * kSlot);
+    dTh = b;
+    dTl = b + 32 * kPS;
+    STh = b + 64 * kPS;
+    STl = b + 128 * kPS;
+  }
   const float* const base = P.qkv + rbase * 384 + kHd * h;
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
-      bf16x4v hi, lo;
-      split4v(dO[a][t], hi, lo);
-      *reinterpret_cast<bf16x4v*>(dTh + (16 * t + li) * kPS + 16 * a + 4 * kg) = hi;
-      *reinterpret_cast<bf16x4v*>(dTl + (16 * t + li) * kPS + 16 * a + 4 * kg) = lo;
-    }
+    for (int t = 0; t < 2; ++t) tput<EX>(dTh, dTl, 16 * t, 16 * a, dO[a][t], lane);
   // D_i = Σ_d ∂O[i][d]·O[i][d] and LSE_i for i = 16a + 4kg + r (the lane's query rows in the S layout below)
   float Dr[4][4];
 #pragma unroll
@@ -530,7 +671,7 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
       kb8[j] = P.bq[128 + kHd * h + 8 * kg + j];
       vb8[j] = P.bq[256 + kHd * h + 8 * kg + j];
     }
-    bf16x8 qh[4], ql[4], dh[4], dl[4];
+    F8<EX> qf[4], df[4];
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       float v[8];
@@ -538,9 +679,8 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
       const float4 x1 = *reinterpret_cast<const float4*>(base + (size_t)(16 * a + li) * 384 + 8 * kg + 4);
       v[0] = x0.x + qb[0]; v[1] = x0.y + qb[1]; v[2] = x0.z + qb[2]; v[3] = x0.w + qb[3];
       v[4] = x1.x + qb[4]; v[5] = x1.y + qb[5]; v[6] = x1.z + qb[6]; v[7] = x1.w + qb[7];
-      split8v(v, qh[a], ql[a]);
-      dh[a] = frag_tr(dTh, 0, 16 * a, lane);
-      dl[a] = frag_tr(dTl, 0, 16 * a, lane);
+      qf[a] = mk8<EX>(v);
+      df[a] = tfrag2<EX>(dTh, dTl, 0, 16 * a, lane);
     }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
@@ -552,17 +692,15 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
         kv[j] = kr[j] + kb8[j];
         vv8[j] = vr[j] + vb8[j];
       }
-      bf16x8 kh, kl, vh, vl;
-      split8v(kv, kh, kl);
-      split8v(vv8, vh, vl);
+      const F8<EX> kf = mk8<EX>(kv), vf = mk8<EX>(vv8);
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
-        p[a][b] = mfma3(qh[a], ql[a], kh, kl, f32x4{0.f, 0.f, 0.f, 0.f});
-        dp[a][b] = mfma3(dh[a], dl[a], vh, vl, f32x4{0.f, 0.f, 0.f, 0.f});
+        p[a][b] = mma8<EX>(qf[a], kf, f32x4{0.f, 0.f, 0.f, 0.f});
+        dp[a][b] = mma8<EX>(df[a], vf, f32x4{0.f, 0.f, 0.f, 0.f});
       }
     }
   }
-  // P = exp(scale·S − LSE); dp ← scale·P∘(dP − D) = ∂L/∂(Q·Kᵀ); its transpose to the hi / lo images for ∂Qᵀ
+  // P = exp(scale·S − LSE); dp ← scale·P∘(dP − D) = ∂L/∂(Q·Kᵀ); its transpose to the images for ∂Qᵀ
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
@@ -576,36 +714,28 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      bf16x4v sh, sl;
-      split4v(dp[a][b], sh, sl);
-      *reinterpret_cast<bf16x4v*>(STh + (16 * b + li) * kPS + 16 * a + 4 * kg) = sh;
-      *reinterpret_cast<bf16x4v*>(STl + (16 * b + li) * kPS + 16 * a + 4 * kg) = sl;
-    }
+    for (int b = 0; b < 4; ++b) tput<EX>(STh, STl, 16 * b, 16 * a, dp[a][b], lane);
   // ∂Vᵀ[t][b] = Σ_a ∂Oᵀ(t, a)·P(a, b) and ∂Kᵀ[t][b] = Σ_a Qᵀ(t, a)·∂S(a, b): lanes (d = 16t + 4kg + r, j = 16b + li)
   f32x4 gV[2][4], gK[2][4], gQ[2][4];
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const float bqc = P.bq[kHd * h + 16 * t + li];
-    bf16x4v oh[4], ol[4], qh[4], ql[4];
+    F4<EX> of[4], qf[4];
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
-      split4v(dO[a][t], oh[a], ol[a]);
+      of[a] = mk4<EX>(dO[a][t]);
       f32x4 qv;
 #pragma unroll
       for (int r = 0; r < 4; ++r) qv[r] = base[(size_t)(16 * a + 4 * kg + r) * 384 + 16 * t + li] + bqc;
-      split4v(qv, qh[a], ql[a]);
+      qf[a] = mk4<EX>(qv);
     }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       f32x4 av = {0.f, 0.f, 0.f, 0.f}, ak = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
-        bf16x4v ph, pl, sh, sl;
-        split4v(p[a][b], ph, pl);
-        split4v(dp[a][b], sh, sl);
-        av = mfma3k16(oh[a], ol[a], ph, pl, av);
-        ak = mfma3k16(qh[a], ql[a], sh, sl, ak);
+        av = mma4<EX>(of[a], mk4<EX>(p[a][b]), av);
+        ak = mma4<EX>(qf[a], mk4<EX>(dp[a][b]), ak);
       }
       gV[t][b] = av;
       gK[t][b] = ak;
@@ -616,20 +746,19 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
 #pragma unroll
   for (int t = 0; t < 2; ++t) {
     const float kbc = P.bq[128 + kHd * h + 16 * t + li];
-    bf16x8 kh[2], kl[2];
+    F8<EX> kf[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       float kv[8];
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) kv[jj] = base[(size_t)(32 * ks + 8 * kg + jj) * 384 + 128 + 16 * t + li] + kbc;
-      split8v(kv, kh[ks], kl[ks]);
+      kf[ks] = mk8<EX>(kv);
     }
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       f32x4 aq = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-        aq = mfma3(kh[ks], kl[ks], frag_tr(STh, 32 * ks, 16 * a, lane), frag_tr(STl, 32 * ks, 16 * a, lane), aq);
+      for (int ks = 0; ks < 2; ++ks) aq = mma8<EX>(kf[ks], tfrag2<EX>(STh, STl, 32 * ks, 16 * a, lane), aq);
       gQ[t][a] = aq;
     }
   }
@@ -669,14 +798,14 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
   }
   // ---- 3: ∂Xn partial of head h: A = ∂Xᵀ accumulators (m = unit, k = d), B = W_qkv rows 128x + 32h + 16t + …
   {
-    bf16x4v ah[3][2][4], al[3][2][4];
+    F4<EX> af[3][2][4];
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
       for (int u4 = 0; u4 < 4; ++u4) {
-        split4v(gQ[t][u4], ah[0][t][u4], al[0][t][u4]);
-        split4v(gK[t][u4], ah[1][t][u4], al[1][t][u4]);
-        split4v(gV[t][u4], ah[2][t][u4], al[2][t][u4]);
+        af[0][t][u4] = mk4<EX>(gQ[t][u4]);
+        af[1][t][u4] = mk4<EX>(gK[t][u4]);
+        af[2][t][u4] = mk4<EX>(gV[t][u4]);
       }
     float* slot = sm + h * kSlot;
 #pragma unroll
@@ -691,16 +820,13 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
           const int rt = 8 * x + 2 * h + t;
-          bf16x4v bh[4], bl[4];
+          F4<EX> bf[4];
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            bh[c] = gfrag4(P.wq4h, rt, 4 * half + c, lane);
-            bl[c] = gfrag4(P.wq4l, rt, 4 * half + c, lane);
-          }
+          for (int c = 0; c < 4; ++c) bf[c] = wfrag4<EX>(P.wq4h, P.wq4l, rt, 4 * half + c, lane);
 #pragma unroll
           for (int u4 = 0; u4 < 4; ++u4)
 #pragma unroll
-            for (int c = 0; c < 4; ++c) acc[u4][c] = mfma3k16(ah[x][t][u4], al[x][t][u4], bh[c], bl[c], acc[u4][c]);
+            for (int c = 0; c < 4; ++c) acc[u4][c] = mma4<EX>(af[x][t][u4], bf[c], acc[u4][c]);
         }
       // (the wave's own slot: its ∂Oᵀ / ∂Sᵀ images are dead)
 #pragma unroll
@@ -835,17 +961,19 @@ __global__ __launch_bounds__(256) void colsum_rows_kernel(const float* __restric
 
 }  // namespace
 
+// exact = 0: bf16 hi / lo weight images (bf16x3); exact = 1: fp32 images in wqh / woh (wql / wol unused)
 extern "C" hipError_t dca_attn_block_fwd_f32(const float* e0, const float* bout, const float* gamma, const float* beta,
-                                             const short* wqh, const short* wql, const float* bq, const short* woh,
-                                             const short* wol, float* xn, float* mu, float* rs, float* qkv, float* o,
+                                             const void* wqh, const void* wql, const float* bq, const void* woh,
+                                             const void* wol, float* xn, float* mu, float* rs, float* qkv, float* o,
                                              float* lse, float* e1, float* x896, unsigned char* arg, const int* off,
-                                             int compat, int N, float eps, hipStream_t stream) {
+                                             int compat, int N, float eps, hipStream_t stream, int exact) {
   if (N < 1) return hipSuccess;
   BlockArgs a{e0, bout, gamma, beta, wqh, wql, bq, woh, wol, xn, mu, rs, qkv, o, lse, e1, x896, arg, {0}, compat,
               0.17677669529663687f /* 1/sqrt(32) */, eps};
   for (int i = 0; i < 7; ++i) a.off[i] = off[i];
   if (a.off[6] != kU) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(attn_block_fwd_f32_kernel, dim3(N), dim3(256), 0, stream, a);
+  if (exact) hipLaunchKernelGGL(attn_block_fwd_f32_kernel<true>, dim3(N), dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL(attn_block_fwd_f32_kernel<false>, dim3(N), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 
@@ -856,16 +984,17 @@ extern "C" hipError_t dca_attn_block_bwd_f32(const float* dtl, const float* q, i
                                              const unsigned char* arg, const int* off, int compat, const float* o,
                                              const float* qkv, const float* bq, const float* lse, const float* e0,
                                              const float* bout, const float* mu, const float* rs, const float* gamma,
-                                             const short* woth, const short* wotl, const short* wq4h,
-                                             const short* wq4l, float* de1, float* dqkv, float* de0, float* part,
+                                             const void* woth, const void* wotl, const void* wq4h,
+                                             const void* wq4l, float* de1, float* dqkv, float* de0, float* part,
                                              float* tmp, float* sums, int N, hipStream_t stream,
-                                             unsigned long long* trace) {
+                                             unsigned long long* trace, int exact) {
   if (N < 1) return hipSuccess;
   BwdArgs a{dtl, q, dx, arg, o, qkv, bq, lse, e0, bout, mu, rs, gamma, woth, wotl, wq4h, wq4l, de1, dqkv, de0, part,
             trace, {0}, ldq, compat, 0.17677669529663687f /* 1/sqrt(32) */};
   for (int i = 0; i < 7; ++i) a.off[i] = off[i];
   if (a.off[6] != kU) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(attn_block_bwd_f32_kernel, dim3(N), dim3(256), 0, stream, a);
+  if (exact) hipLaunchKernelGGL(attn_block_bwd_f32_kernel<true>, dim3(N), dim3(256), 0, stream, a);
+  else hipLaunchKernelGGL(attn_block_bwd_f32_kernel<false>, dim3(N), dim3(256), 0, stream, a);
   DCA_CHECK_LAUNCH();
   const int G = dca_attn_block_bwd_groups(N);
   const int per = (N + G - 1) / G;

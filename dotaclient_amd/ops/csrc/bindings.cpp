@@ -298,7 +298,6 @@ std::vector<torch::Tensor> encoder_bwd(torch::Tensor units, torch::Tensor w1, to
   const bool f32w = wtT.scalar_type() == at::kFloat;
   TORCH_CHECK(f32w || wtT.scalar_type() == at::kBFloat16, "wtT must be bf16 or f32");
   TORCH_CHECK(!exact || f32w, "encoder_bwd: exact mode needs fp32 weights");
-  TORCH_CHECK(!exact || !(demb_in && demb_in->defined()), "encoder_bwd: exact mode covers the 1v1 encoder (no demb_in)");
   const int N = units.size(0), U = units.size(1);
   TORCH_CHECK(q.dim() == 2 && q.size(0) == N && q.size(1) >= 128 && q.stride(1) == 1 && q.stride(0) % 4 == 0,
               "q must be (N, >=128) with unit column stride and 16-B aligned rows");
@@ -500,11 +499,18 @@ std::vector<torch::Tensor> attn_block_fwd(torch::Tensor e0, torch::Tensor bout, 
                                           torch::Tensor wol, std::vector<int64_t> type_off, torch::Tensor x896,
                                           torch::Tensor arg, bool compat, double eps) {
   CHECK_F32(e0); CHECK_F32(bout); CHECK_F32(gamma); CHECK_F32(beta); CHECK_F32(bq); CHECK_F32(x896); CHECK_U8(arg);
-  CHECK_BF16(wqh); CHECK_BF16(wql); CHECK_BF16(woh); CHECK_BF16(wol);
+  // fp32 weight images (wql / wol ignored): the IEEE-fp32 kernel; bf16 hi / lo images: bf16x3
+  const bool exact = wqh.scalar_type() == at::kFloat;
+  CHECK_DEV(wqh); CHECK_CONTIG(wqh); CHECK_DEV(woh); CHECK_CONTIG(woh);
+  if (exact) {
+    CHECK_F32(woh);
+  } else {
+    CHECK_BF16(wqh); CHECK_BF16(wql); CHECK_BF16(woh); CHECK_BF16(wol);
+  }
   TORCH_CHECK(e0.numel() % (64 * 128) == 0 && e0.size(-1) == 128, "attn_block_fwd: e0 (N·64, 128)");
   const int64_t N = e0.numel() / (64 * 128);
-  TORCH_CHECK(wqh.numel() == 384 * 128 && wql.numel() == 384 * 128 && woh.numel() == 128 * 128 &&
-              wol.numel() == 128 * 128 && bq.numel() == 384 && bout.numel() == 128 && gamma.numel() == 128 &&
+  TORCH_CHECK(wqh.numel() == 384 * 128 && (exact || wql.numel() == 384 * 128) && woh.numel() == 128 * 128 &&
+              (exact || wol.numel() == 128 * 128) && bq.numel() == 384 && bout.numel() == 128 && gamma.numel() == 128 &&
               beta.numel() == 128, "attn_block_fwd: weight shapes");
   TORCH_CHECK(x896.dim() == 2 && x896.size(0) == N && x896.size(1) == 896, "attn_block_fwd: x896 (N, 896)");
   TORCH_CHECK(arg.numel() == N * 6 * 128, "attn_block_fwd: arg (N, 6, 128)");
@@ -520,10 +526,11 @@ std::vector<torch::Tensor> attn_block_fwd(torch::Tensor e0, torch::Tensor bout, 
   auto lse = torch::empty({N, 4, 64}, o32);
   auto e1 = torch::empty({N * 64, 128}, o32);
   hip_check(dca_attn_block_fwd_f32(ptr<float>(e0), ptr<float>(bout), ptr<float>(gamma), ptr<float>(beta),
-                                   ptr<short>(wqh), ptr<short>(wql), ptr<float>(bq), ptr<short>(woh), ptr<short>(wol),
-                                   ptr<float>(xn), ptr<float>(mu), ptr<float>(rs), ptr<float>(qkv), ptr<float>(o),
-                                   ptr<float>(lse), ptr<float>(e1), ptr<float>(x896), ptr<unsigned char>(arg), off,
-                                   compat ? 1 : 0, (int)N, (float)eps, cur_stream()),
+                                   wqh.data_ptr(), exact ? nullptr : wql.data_ptr(), ptr<float>(bq), woh.data_ptr(),
+                                   exact ? nullptr : wol.data_ptr(), ptr<float>(xn), ptr<float>(mu), ptr<float>(rs),
+                                   ptr<float>(qkv), ptr<float>(o), ptr<float>(lse), ptr<float>(e1), ptr<float>(x896),
+                                   ptr<unsigned char>(arg), off, compat ? 1 : 0, (int)N, (float)eps, cur_stream(),
+                                   exact ? 1 : 0),
             "dca_attn_block_fwd_f32");
   return {xn, mu, rs, qkv, o, lse, e1};
 }
@@ -542,7 +549,13 @@ std::vector<torch::Tensor> attn_block_bwd(torch::Tensor dtl, torch::Tensor q, to
                                           torch::Tensor wq4l, c10::optional<torch::Tensor> trace) {
   CHECK_F32(dtl); CHECK_DEV(q); CHECK_DT(q, at::kFloat); CHECK_F32(dx); CHECK_U8(arg); CHECK_F32(o); CHECK_F32(qkv);
   CHECK_F32(bq); CHECK_F32(lse); CHECK_F32(e0); CHECK_F32(bout); CHECK_F32(mu); CHECK_F32(rs); CHECK_F32(gamma);
-  CHECK_BF16(woth); CHECK_BF16(wotl); CHECK_BF16(wq4h); CHECK_BF16(wq4l);
+  const bool exact = woth.scalar_type() == at::kFloat;     // fp32 images: the IEEE-fp32 kernel
+  CHECK_DEV(woth); CHECK_CONTIG(woth); CHECK_DEV(wq4h); CHECK_CONTIG(wq4h);
+  if (exact) {
+    CHECK_F32(wq4h);
+  } else {
+    CHECK_BF16(woth); CHECK_BF16(wotl); CHECK_BF16(wq4h); CHECK_BF16(wq4l);
+  }
   check_type_off(type_off);
   const int64_t N = dtl.size(0);
   TORCH_CHECK(dtl.dim() == 2 && dtl.size(1) == 64, "attn_block_bwd: dtl (N, 64)");
@@ -552,8 +565,8 @@ std::vector<torch::Tensor> attn_block_bwd(torch::Tensor dtl, torch::Tensor q, to
   TORCH_CHECK(o.numel() == N * 64 * 128 && e0.numel() == N * 64 * 128 && qkv.numel() == N * 64 * 384 &&
               lse.numel() == N * 4 * 64 && mu.numel() == N * 64 && rs.numel() == N * 64, "attn_block_bwd: saved shapes");
   TORCH_CHECK(bq.numel() == 384 && bout.numel() == 128 && gamma.numel() == 128 && woth.numel() == 128 * 128 &&
-              wotl.numel() == 128 * 128 && wq4h.numel() == 384 * 128 && wq4l.numel() == 384 * 128,
-              "attn_block_bwd: weight shapes");
+              (exact || wotl.numel() == 128 * 128) && wq4h.numel() == 384 * 128 &&
+              (exact || wq4l.numel() == 384 * 128), "attn_block_bwd: weight shapes");
   int off[7];
   for (int i = 0; i < 7; ++i) off[i] = (int)type_off[i];
   auto o32 = e0.options();
@@ -572,11 +585,13 @@ std::vector<torch::Tensor> attn_block_bwd(torch::Tensor dtl, torch::Tensor q, to
   hip_check(dca_attn_block_bwd_f32(ptr<float>(dtl), ptr<float>(q), (int)q.stride(0), ptr<float>(dx),
                                    ptr<unsigned char>(arg), off, compat ? 1 : 0, ptr<float>(o), ptr<float>(qkv),
                                    ptr<float>(bq), ptr<float>(lse), ptr<float>(e0), ptr<float>(bout), ptr<float>(mu),
-                                   ptr<float>(rs), ptr<float>(gamma), ptr<short>(woth), ptr<short>(wotl),
-                                   ptr<short>(wq4h), ptr<short>(wq4l), ptr<float>(de1), ptr<float>(dqkv),
+                                   ptr<float>(rs), ptr<float>(gamma), woth.data_ptr(),
+                                   exact ? nullptr : wotl.data_ptr(), wq4h.data_ptr(),
+                                   exact ? nullptr : wq4l.data_ptr(), ptr<float>(de1), ptr<float>(dqkv),
                                    ptr<float>(de0), ptr<float>(part), ptr<float>(tmp), ptr<float>(sums), (int)N,
                                    cur_stream(),
-                                   (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr),
+                                   (trace.has_value() && trace->defined()) ? ptr<unsigned long long>(*trace) : nullptr,
+                                   exact ? 1 : 0),
             "dca_attn_block_bwd_f32");
   return {de1, dqkv, de0, sums};
 }

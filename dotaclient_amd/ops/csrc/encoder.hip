@@ -1155,14 +1155,21 @@ __global__ __launch_bounds__(512, 1) void encoder_fwd_x_kernel(FfParams P) {
 }
 
 // ∂emb e-tile wv of item k (C layout) → row-major image (∂basic's A operand) and transposed image (the ∂W_τ
-// products' B operand: one b128 of rows 4kg … 4kg+3 per lane and tile)
+// products' B operand: one b128 of rows 4kg … 4kg+3 per lane and tile). GIVEN: the item's ∂emb as loaded (the
+// entity-attention path hands the encoder ∂E0 instead of the pointer / pool gradients)
+template <bool GIVEN>
 __device__ __forceinline__ void xb_build(const FbBuild& b, const float* slot, int u, float* im, float* it, int wv,
                                          int lane) {
   const int i = lane & 15, kg = lane >> 4;
-  const f32x4 d4 = *reinterpret_cast<const f32x4*>(slot + 16 * kF + 4 * kg);
   f32x4 v;
+  if constexpr (GIVEN) {
 #pragma unroll
-  for (int r = 0; r < 4; ++r) v[r] = d4[r] * b.q[r] + (b.ab[r] == (unsigned)u ? b.ds[r] : 0.f);
+    for (int r = 0; r < 4; ++r) v[r] = b.q[r];
+  } else {
+    const f32x4 d4 = *reinterpret_cast<const f32x4*>(slot + 16 * kF + 4 * kg);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = d4[r] * b.q[r] + (b.ab[r] == (unsigned)u ? b.ds[r] : 0.f);
+  }
   x_put(im, wv, v, i, kg);
   *reinterpret_cast<f32x4*>(it + (16 * wv + i) * kXT + 4 * kg) = v;
 }
@@ -1173,7 +1180,9 @@ __device__ __forceinline__ void xb_build(const FbBuild& b, const float* slot, in
 // once per wave for two column tiles (half the LDS traffic per MFMA), and the two resident workgroups work on
 // different items, so one's barrier / staging phases overlap the other's MFMAs (the 8-wave form keeps both waves of
 // a SIMD in lockstep: ≈55 % MFMA busy). Same products, same per-item two-level sums, same partial layouts.
-template <bool COMPAT>
+// GIVEN: ∂emb read from P.demb_in (the 5v5 entity-attention step, ∂E0 of the attention block) instead of built from
+// the pointer / pool gradients.
+template <bool GIVEN, bool COMPAT>
 __global__ __launch_bounds__(256, 2) void encoder_bwd_x2_kernel(FbParams P) {
   const int tid = threadIdx.x, w = tid >> 6, lane = tid & 63;
   const int i = lane & 15, kg = lane >> 4;
@@ -1188,9 +1197,13 @@ __global__ __launch_bounds__(256, 2) void encoder_bwd_x2_kernel(FbParams P) {
   __shared__ __attribute__((aligned(16))) float imt[2][128 * kXT];
   __shared__ __attribute__((aligned(16))) float stg[3][kStg];
   FbRsrc R;
-  R.q = uniform_rsrc(P.q, N * P.ldq * 4);
-  R.x = uniform_rsrc(P.dx, N * 896 * 4);
-  R.a = uniform_rsrc(P.arg, N * 6 * kD);
+  if constexpr (GIVEN) {
+    R.g = uniform_rsrc(P.demb_in, N * U * kD * 4);
+  } else {
+    R.q = uniform_rsrc(P.q, N * P.ldq * 4);
+    R.x = uniform_rsrc(P.dx, N * 896 * 4);
+    R.a = uniform_rsrc(P.arg, N * 6 * kD);
+  }
 
   float wx[2][32], w1x[2][3];
 #pragma unroll
@@ -1222,13 +1235,13 @@ __global__ __launch_bounds__(256, 2) void encoder_bwd_x2_kernel(FbParams P) {
   }
 #pragma unroll
   for (int t = 0; t < 2; ++t)
-    fb_load_build<false, COMPAT>(bn[t], R, P.ldq, min(k0, kl), true, cnt, uoff, U, tau, 2 * w + t, i, kg);
+    fb_load_build<GIVEN, COMPAT>(bn[t], R, P.ldq, min(k0, kl), true, cnt, uoff, U, tau, 2 * w + t, i, kg);
   lds_barrier();
 #pragma unroll
-  for (int t = 0; t < 2; ++t) xb_build(bn[t], stg[k0 % 3], k0 % cnt, img[0], imt[0], 2 * w + t, lane);
+  for (int t = 0; t < 2; ++t) xb_build<GIVEN>(bn[t], stg[k0 % 3], k0 % cnt, img[0], imt[0], 2 * w + t, lane);
 #pragma unroll
   for (int t = 0; t < 2; ++t)
-    fb_load_build<false, COMPAT>(bn[t], R, P.ldq, min(k0 + 1, kl), min(k0 + 1, kl) % cnt == 0, cnt, uoff, U, tau,
+    fb_load_build<GIVEN, COMPAT>(bn[t], R, P.ldq, min(k0 + 1, kl), min(k0 + 1, kl) % cnt == 0, cnt, uoff, U, tau,
                                  2 * w + t, i, kg);
   float l1n[3], ubn[4];
   auto l1_read = [&](const float* sl) {
@@ -1276,10 +1289,10 @@ __global__ __launch_bounds__(256, 2) void encoder_bwd_x2_kernel(FbParams P) {
     if (w < 3) stg[(k + 2) % 3][64 * w + lane] = pre;
 #pragma unroll
     for (int t = 0; t < 2; ++t)
-      xb_build(bn[t], stg[(k + 1) % 3], min(k + 1, kl) % cnt, img[buf ^ 1], imt[buf ^ 1], 2 * w + t, lane);
+      xb_build<GIVEN>(bn[t], stg[(k + 1) % 3], min(k + 1, kl) % cnt, img[buf ^ 1], imt[buf ^ 1], 2 * w + t, lane);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
-      fb_load_build<false, COMPAT>(bn[t], R, P.ldq, min(k + 2, kl), k + 2 <= kl && (k + 2) % cnt == 0, cnt, uoff, U,
+      fb_load_build<GIVEN, COMPAT>(bn[t], R, P.ldq, min(k + 2, kl), k + 2 <= kl && (k + 2) % cnt == 0, cnt, uoff, U,
                                    tau, 2 * w + t, i, kg);
     l1_read(stg[(k + 1) % 3]);
     if (w < 3) pre = fb_stage_load(P, min(k + 3, kl), cnt, uoff, w, lane);
@@ -1557,13 +1570,13 @@ extern "C" hipError_t dca_encoder_bwd(const float* units, const float* w1, const
     const int jobs = F.jbase[6];
     F.w1part = static_cast<float*>(ws);
     F.dwtpart = F.w1part + (size_t)jobs * kW1;
-    if (f32 == 2 && demb_in) return hipErrorInvalidValue;      // the exact kernels cover the 1v1 encoder
     if (jobs > 0 && f32 == 2) {
       // the 4-wave two-workgroups-per-CU form: 369.7 vs 373.6 µs alone for the 8-wave form, and in the exact learner
       // step 5.498 / 5.483 vs 5.518 / 5.513 ms (two same-box pairs) — beside the side stream's weight-gradient GEMMs
       // two smaller workgroups per CU schedule better
-      if (compat) encoder_bwd_x2_kernel<true><<<jobs, 256, 0, st>>>(F);
-      else encoder_bwd_x2_kernel<false><<<jobs, 256, 0, st>>>(F);
+      if (demb_in) encoder_bwd_x2_kernel<true, false><<<jobs, 256, 0, st>>>(F);
+      else if (compat) encoder_bwd_x2_kernel<false, true><<<jobs, 256, 0, st>>>(F);
+      else encoder_bwd_x2_kernel<false, false><<<jobs, 256, 0, st>>>(F);
     } else if (jobs > 0) {
       if (demb_in) encoder_bwd_f32_fused_kernel<true, false><<<jobs, 512, 0, st>>>(F);
       else if (compat) encoder_bwd_f32_fused_kernel<false, true><<<jobs, 512, 0, st>>>(F);

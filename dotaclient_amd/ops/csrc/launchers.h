@@ -9,18 +9,18 @@ hipError_t dca_split_bf16x2(const float* src, short* hi, short* lo, long long n,
 hipError_t dca_split_bf16x2_blk(const float* src, short* hi, short* lo, int R, int K, hipStream_t stream);
 // attn_block.hip
 hipError_t dca_attn_block_fwd_f32(const float* e0, const float* bout, const float* gamma, const float* beta,
-                                  const short* wqh, const short* wql, const float* bq, const short* woh,
-                                  const short* wol, float* xn, float* mu, float* rs, float* qkv, float* o, float* lse,
+                                  const void* wqh, const void* wql, const float* bq, const void* woh,
+                                  const void* wol, float* xn, float* mu, float* rs, float* qkv, float* o, float* lse,
                                   float* e1, float* x896, unsigned char* arg, const int* off, int compat, int N,
-                                  float eps, hipStream_t stream);
+                                  float eps, hipStream_t stream, int exact);
 int dca_attn_block_bwd_groups(int N);
 hipError_t dca_attn_block_bwd_f32(const float* dtl, const float* q, int ldq, const float* dx, const unsigned char* arg,
                                   const int* off, int compat, const float* o, const float* qkv, const float* bq,
                                   const float* lse, const float* e0, const float* bout, const float* mu,
-                                  const float* rs, const float* gamma, const short* woth, const short* wotl,
-                                  const short* wq4h, const short* wq4l, float* de1, float* dqkv, float* de0,
+                                  const float* rs, const float* gamma, const void* woth, const void* wotl,
+                                  const void* wq4h, const void* wq4l, float* de1, float* dqkv, float* de0,
                                   float* part, float* tmp, float* sums, int N, hipStream_t stream,
-                                  unsigned long long* trace);
+                                  unsigned long long* trace, int exact);
 // actor_fp8.hip
 hipError_t dca_actor_fp8(const short* x896, const void* wpre, const float* spre, const float* bpre, const void* wg,
                          const float* sg, const float* bg, const void* wh, const float* sh, const float* bh, float* h,

@@ -1,4 +1,4 @@
-"""Batched GPU actor throughput alone (for rocprofv3): python3 scripts/actor_bench.py [n_games] [bf16|fp8]"""
+"""Batched GPU actor throughput alone (for rocprofv3): python3 scripts/actor_bench.py [n_games] [bf16|fp32|fp8]"""
 import json
 import os
 import sys

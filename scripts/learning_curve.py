@@ -34,10 +34,13 @@ def main(argv=None):
     ap.add_argument('--eval-precision', default='fp32', choices=['fp32', 'bf16', 'fp8'])
     ap.add_argument('--mode', default='1v1', choices=['1v1', '5v5'])
     ap.add_argument('--device', default='cuda')
+    ap.add_argument('--log-dir', default=None,
+                    help='checkpoint directory: resume the curve from it (model, Adam, normalisers, counters) and '
+                         'append to --out; --budget is the total over all resumed jobs')
     a = ap.parse_args(argv)
     from dotaclient_amd.learner.curve import run_learning_curve
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
-    with open(a.out, 'w') as fh:
+    with open(a.out, 'a' if a.log_dir else 'w') as fh:
         def emit(row):
             print(json.dumps(row), flush=True)
             fh.write(json.dumps(row) + '\n')
@@ -47,7 +50,8 @@ def main(argv=None):
                            seq_len=a.seq_len, batch_size=a.batch_size, seq_per_epoch=a.seq_per_epoch, lr=a.lr,
                            entropy_coef=a.entropy_coef, max_dota_time=a.max_dota_time, pack=bool(a.pack),
                            seed=a.seed, device=a.device, on_row=emit, save_model=a.save_model,
-                           eval_precision=a.eval_precision, mode=a.mode)
+                           eval_precision=a.eval_precision, mode=a.mode,
+                           log_dir=a.log_dir)
 
 
 if __name__ == '__main__':

@@ -144,6 +144,22 @@ def test_exact_compat_network_matches_fp64(gpu_ops, vbug):
 
 
 @pytest.mark.gpu
+def test_exact_5v5_step_matches_fp64(gpu_ops):
+    """The 5v5 entity-attention learner at fp32-exact (BASELINE config 4 at the reference precision) on the IEEE-fp32
+    twins of the attention block kernels (ops/csrc/attn_block.hip EX = true), the exact encoder backward with the
+    block's ∂E0 as its input, exact ∂W_qkv / ∂W_out GEMMs — deploy shape B=8, S=1400: every gradient tensor within
+    1e-5 of float64, or 1.5× the torch-fp32 error where that is larger."""
+    from tests.test_fp32_kernels import _rel, _step_grads
+    (lf, _, gf), (lo, _, go), (l64, g64) = _step_grads('fp32-exact', '5v5', 'ppo', 8, 1400, fp64=True)
+    rows = sorted(((_rel(gf[n], g64[n]), _rel(go[n], g64[n]), n) for n in g64
+                   if g64[n] is not None and g64[n].norm() > 0), reverse=True)
+    print('5v5 fp32-exact: worst (fused vs fp64, torch-fp32 vs fp64):', rows[:6], 'loss', lf, lo, l64)
+    assert abs(lf - l64) <= 1e-6 * max(1e-2, abs(l64)), (lf, l64)
+    bad = [r for r in rows if r[0] >= max(1e-5, 1.5 * r[1])]
+    assert not bad, bad[:5]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('half', ['0', '1'])
 def test_exact_chunked_step_matches_one_chunk(gpu_ops, monkeypatch, half):
     """Time chunks (DCA_PIPELINE_CHUNKS=4: encoder + forward chain per chunk ahead of each recurrence chunk, heads and

@@ -34,6 +34,18 @@ def test_learning_curve_loop_cpu():
     assert rows[0]['t_train'] == 0.0 and rows[-1]['t_train'] >= 3
 
 
+def test_learning_curve_resumes_from_log_dir_cpu(tmp_path):
+    """A long curve as several jobs: the second job resumes the checkpointed learner and the curve's counters."""
+    kw = dict(eval_every=1.0, eval_games=4, model='lstm128', precision='fp32', games=8, threads=2, seq_len=16,
+              batch_size=2, seq_per_epoch=2, max_dota_time=10.0, device='cpu', pack=False, log_dir=str(tmp_path))
+    first = run_learning_curve(budget=1.5, **kw)
+    second = run_learning_curve(budget=3.0, **kw)
+    assert first[0]['t_train'] == 0.0 and second[0].get('resumed')
+    assert second[0]['iteration'] > first[-1]['iteration'] and second[0]['t_train'] > first[-1]['t_train']
+    assert second[-1]['samples'] > first[-1]['samples'] and second[-1]['t_train'] >= 3.0
+    assert second[-1]['actor_steps'] > first[-1]['actor_steps']
+
+
 @pytest.mark.gpu
 def test_short_training_beats_the_untrained_policy_vs_default_bot(gpu_ops):
     """30 s of fused fp32-exact training in the node loop, evaluated with the fp32 actor against the default bot:
