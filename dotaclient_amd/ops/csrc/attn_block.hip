@@ -90,7 +90,8 @@ __device__ __forceinline__ bf16x8 gfrag(const short* __restrict__ w, int m0, int
 // (K = 16) step is 8 (4) v_mfma_f32_16x16x4_f32 calls: sub-step j takes k = 8·(lane>>4) + j (4·(lane>>4) + j) of
 // the lane's k-group, i.e. exactly the elements the bf16 lane layout holds, so every fragment load, accumulator
 // layout and LDS image of the bf16x3 form carries over with fp32 in place of the (hi, lo) pair — and the same
-// register count (8 floats = a bf16x8 hi + lo pair). Every product is then an fp32 fma (the fp32-exact learner).
+// register count (8 floats = a bf16x8 hi + lo pair). Every product is then an fp32 fma (the fp32-exact learner), and
+// the softmax takes libm expf / logf instead of the hardware approximations.
 template <bool EX> struct F8;
 template <> struct F8<false> { bf16x8 h, l; };
 template <> struct F8<true> { float v[8]; };
@@ -340,7 +341,7 @@ __global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P)
       for (int b = 0; b < 4; ++b)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float e = __expf(s[b][a][r] * P.scale - m);
+          const float e = EX ? expf(s[b][a][r] * P.scale - m) : __expf(s[b][a][r] * P.scale - m);
           s[b][a][r] = e;
           sum += e;
         }
@@ -349,7 +350,7 @@ __global__ __launch_bounds__(256, 2) void attn_block_fwd_f32_kernel(BlockArgs P)
       const float inv = 1.f / sum;
 #pragma unroll
       for (int b = 0; b < 4; ++b) s[b][a] *= inv;
-      if (kg == 0) lse[16 * a + li] = m + __logf(sum);
+      if (kg == 0) lse[16 * a + li] = m + (EX ? logf(sum) : __logf(sum));
     }
     // O = P·V: A[m = i][k = j] = s[b][a], B[k = j][n = d] = v[b][c] (+ bias of column d)
     F4<EX> vf[4][2];
@@ -707,7 +708,7 @@ __global__ __launch_bounds__(256, 1) void attn_block_bwd_f32_kernel(BwdArgs P) {
     for (int r = 0; r < 4; ++r)
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
-        const float pr = __expf(p[a][b][r] * P.scale - Lr[a][r]);
+        const float pr = EX ? expf(p[a][b][r] * P.scale - Lr[a][r]) : __expf(p[a][b][r] * P.scale - Lr[a][r]);
         p[a][b][r] = pr;
         dp[a][b][r] = P.scale * pr * (dp[a][b][r] - Dr[a][r]);
       }

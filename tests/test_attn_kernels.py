@@ -215,7 +215,8 @@ def test_encoder_bwd_with_given_demb(gpu_ops):
 
 def test_exact_encoder_bwd_with_given_demb_matches_fp64(gpu_ops):
     """encoder_bwd(demb_in=∂E0, exact=True) — the 5v5 fp32-exact step's encoder backward (encoder_bwd_x2_kernel
-    GIVEN): ∂W_τ, ∂W1, ∂b1 against float64 autograd, ≤ 1e-6 relative."""
+    GIVEN): ∂W_τ, ∂W1, ∂b1 against float64 autograd, within max(2e-6, 2× the torch-fp32 evaluation's own error)
+    (∂W1 / ∂b1 sum through the ReLU mask, whose rare near-zero pre-activations both fp32 evaluations may flip)."""
     g = _g(4)
     Nr = 1111
     units = torch.randn(Nr, U, 10, device='cuda', generator=g)
@@ -229,14 +230,24 @@ def test_exact_encoder_bwd_with_given_demb_matches_fp64(gpu_ops):
                                         torch.zeros(Nr, 896, device='cuda'),
                                         torch.zeros(Nr, 6, 128, dtype=torch.uint8, device='cuda'), counts, False,
                                         demb_in=demb, exact=True)
-    d = lambda t: t.double().requires_grad_(True)   # noqa: E731
-    W1, B1, WT = d(w1), d(b1), d(wt)
-    basic = F.relu(units.double() @ W1.t() + B1)
-    torch.cat([basic[:, TYPE_OFF[t]:TYPE_OFF[t + 1]] @ WT[t].t() for t in range(6)], 1).backward(demb.double())
+
+    def ref(dt):
+        W1, B1, WT = (t.to(dt).requires_grad_(True) for t in (w1, b1, wt))
+        basic = F.relu(units.to(dt) @ W1.t() + B1)
+        torch.cat([basic[:, TYPE_OFF[t]:TYPE_OFF[t + 1]] @ WT[t].t() for t in range(6)], 1).backward(demb.to(dt))
+        return {'dwt': WT.grad, 'dw1': W1.grad, 'db1': B1.grad}
+    prev = torch.backends.cuda.matmul.allow_tf32
+    torch.backends.cuda.matmul.allow_tf32 = False
+    try:
+        r64, r32 = ref(torch.float64), ref(torch.float32)
+    finally:
+        torch.backends.cuda.matmul.allow_tf32 = prev
     rel = lambda a, b: float((a.double() - b).norm() / b.norm())   # noqa: E731
-    errs = {'dwt': rel(dwt, WT.grad), 'dw1': rel(dw1, W1.grad), 'db1': rel(db1, B1.grad)}
-    print('exact encoder bwd (given demb):', errs)
-    assert max(errs.values()) < 1e-6, errs
+    got = {'dwt': dwt, 'dw1': dw1, 'db1': db1}
+    errs = {k: (rel(got[k], r64[k]), rel(r32[k], r64[k])) for k in got}
+    print('exact encoder bwd (given demb), (fused, torch-fp32) vs fp64:', errs)
+    for k, (e, e32) in errs.items():
+        assert e <= max(2e-6, 2 * e32), (k, e, e32)
 
 
 @pytest.mark.parametrize('layout', ['1v1', '5v5'])
