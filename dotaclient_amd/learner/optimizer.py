@@ -300,7 +300,8 @@ class DotaOptimizer:
         in bounded slices so that :meth:`close` ends the thread promptly instead of leaving it blocked inside the
         broker; returns None once ``stop`` is set."""
         broker = getattr(self, '_xp_broker', None) or self.broker
-        consume = getattr(broker, 'consume_experience_view', None) or broker.consume_experience
+        checked = getattr(broker, 'consume_experience_checked', None)    # shm ring: CRC verified during the copy
+        consume = checked or getattr(broker, 'consume_experience_view', None) or broker.consume_experience
         total = self.cfg.xp_timeout
         while True:
             if stop is None:
@@ -317,8 +318,13 @@ class DotaOptimizer:
                     return None
             if body is None:
                 raise TimeoutError('no experience received')
+            ok = None
+            if checked is not None:
+                body, ok = body
             try:
-                return decode_any(body, allow_pickle=self.cfg.allow_pickle_experience)
+                if ok is False:
+                    raise CorruptMessage('experience message CRC mismatch (corrupted or truncated)')
+                return decode_any(body, allow_pickle=self.cfg.allow_pickle_experience, crc_checked=ok is True)
             except CorruptMessage as e:       # drop it, like a lost message; the actors keep producing
                 self.corrupt_rollouts += 1
                 logger.warning('dropping corrupted experience message (%s); %d so far', e, self.corrupt_rollouts)

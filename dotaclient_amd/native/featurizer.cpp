@@ -114,6 +114,44 @@ class ShmRing {
     return py::array_t<uint8_t>({(py::ssize_t)out->size()}, {(py::ssize_t)1},
                                 reinterpret_cast<const uint8_t*>(out->data()), owner);
   }
+  // pop_view + the DCX2 trailer check in the same pass: the payload is copied out in 64 KB blocks and each block's
+  // CRC-32C is taken while it is still in cache (combined per block), instead of a second full read of the message
+  // by the decoder. Returns (array, ok): ok = True (DCX2, CRC matches), False (DCX2, mismatch — corrupted), None
+  // (another format: the decoder checks it).
+  py::object pop_checked(double timeout) {
+    uint8_t* buf = nullptr;
+    uint64_t n = 0;
+    int ok = -1;
+    bool got;
+    {
+      py::gil_scoped_release rel;
+      got = r_.pop_with([&](const uint8_t* src, uint64_t len) {
+        buf = static_cast<uint8_t*>(std::malloc(len ? len : 1));
+        n = len;
+        const bool dcx2 = len >= 12 && std::memcmp(src, "DCX2", 4) == 0;
+        const uint64_t body = dcx2 ? len - 4 : len;
+        uint32_t crc = 0;
+        constexpr uint64_t kBlk = 64 << 10;
+        for (uint64_t o = 0; o < len; o += kBlk) {
+          const uint64_t b = std::min(kBlk, len - o);
+          std::memcpy(buf + o, src + o, b);
+          if (dcx2 && o < body) {
+            const uint64_t c = std::min(b, body - o);
+            crc = o == 0 ? crc32c_raw(buf, c) : crc32c_combine(crc, crc32c_raw(buf + o, c), c);
+          }
+        }
+        if (dcx2) {
+          uint32_t want;
+          std::memcpy(&want, buf + body, 4);
+          ok = crc == want ? 1 : 0;
+        }
+      }, timeout);
+    }
+    if (!got) return py::none();
+    py::capsule owner(buf, [](void* p) { std::free(p); });
+    py::array_t<uint8_t> arr({(py::ssize_t)n}, {(py::ssize_t)1}, buf, owner);
+    return py::make_tuple(arr, ok < 0 ? py::object(py::none()) : py::object(py::bool_(ok == 1)));
+  }
   uint64_t size() { return r_.size(); }
   uint64_t dropped() { return r_.dropped(); }
   static void unlink(const std::string& name) { RingCore::unlink(name); }
@@ -392,6 +430,7 @@ PYBIND11_MODULE(_native, m) {
       .def("push", &ShmRing::push, py::arg("msg"), py::arg("timeout") = -1.0, py::arg("drop_oldest") = false)
       .def("pop", &ShmRing::pop, py::arg("timeout") = -1.0)
       .def("pop_view", &ShmRing::pop_view, py::arg("timeout") = -1.0)
+      .def("pop_checked", &ShmRing::pop_checked, py::arg("timeout") = -1.0)
       .def("size", &ShmRing::size)
       .def("dropped", &ShmRing::dropped)
       .def_static("unlink", &ShmRing::unlink);

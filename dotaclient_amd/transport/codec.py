@@ -158,17 +158,20 @@ def encode(r: Rollout) -> bytes:
     return body + struct.pack('<I', crc)
 
 
-def decode(buf: bytes) -> Rollout:
+def decode(buf: bytes, crc_checked: bool = False) -> Rollout:
+    """``crc_checked``: the trailer was verified while the message was copied out of the ring
+    (``ShmBroker.consume_experience_checked``) — skip the second pass over it."""
     magic = bytes(buf[:4])
     if magic not in MAGICS:
         raise ValueError('not a DCX1 / DCX2 experience message')
     if len(buf) < 12:
         raise CorruptMessage('truncated experience message')
-    (crc,) = struct.unpack_from('<I', buf, len(buf) - 4)
-    n = len(buf) - 4
-    got = _crc32c_prefix(buf, n) if magic == MAGIC2 else zlib.crc32(memoryview(buf)[:n])
-    if got != crc:
-        raise CorruptMessage('experience message CRC mismatch (corrupted or truncated)')
+    if not (crc_checked and magic == MAGIC2):
+        (crc,) = struct.unpack_from('<I', buf, len(buf) - 4)
+        n = len(buf) - 4
+        got = _crc32c_prefix(buf, n) if magic == MAGIC2 else zlib.crc32(memoryview(buf)[:n])
+        if got != crc:
+            raise CorruptMessage('experience message CRC mismatch (corrupted or truncated)')
     (hl,) = struct.unpack_from('<I', buf, 4)
     header = json.loads(bytes(buf[8:8 + hl]))
     base = 8 + hl
@@ -229,12 +232,13 @@ class _ArrayUnpickler(pickle.Unpickler):
         raise pickle.UnpicklingError(f'global {module}.{name} is not allowed in an experience message')
 
 
-def decode_any(buf: bytes, allow_pickle: bool = False) -> Rollout:
+def decode_any(buf: bytes, allow_pickle: bool = False, crc_checked: bool = False) -> Rollout:
     """DCX1 binary, or (``allow_pickle``) a reference agent's pickled dict through :class:`_ArrayUnpickler`. Every
-    decode failure surfaces as :class:`CorruptMessage` (the learner drops the message and carries on)."""
+    decode failure surfaces as :class:`CorruptMessage` (the learner drops the message and carries on).
+    ``crc_checked``: a DCX2 trailer already verified by the ring (:func:`decode`)."""
     try:
         if bytes(buf[:4]) in MAGICS:
-            return decode(buf)
+            return decode(buf, crc_checked=crc_checked)
         if not allow_pickle:
             raise CorruptMessage('not a DCX1 / DCX2 message (reference pickles need allow_pickle / '
                                  '--allow-pickle-experience)')

@@ -41,6 +41,12 @@ class ShmBroker:
         the learner's decode thread takes this form when the broker offers it."""
         return self.ring.pop_view(-1.0 if timeout is None else float(timeout))
 
+    def consume_experience_checked(self, timeout: Optional[float] = None):
+        """:meth:`consume_experience_view` with the DCX2 CRC-32C trailer verified in the same pass as the copy out
+        of the ring (``ShmRing.pop_checked``): ``(array, ok)`` with ok True / False for DCX2 messages and None for
+        other formats (the decoder then checks them), or None when nothing arrived."""
+        return self.ring.pop_checked(-1.0 if timeout is None else float(timeout))
+
     @property
     def xp_queue_size(self) -> int:
         return int(self.ring.size())

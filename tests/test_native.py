@@ -125,6 +125,54 @@ def test_shm_ring_mpmc():
         native.ShmRing.unlink(name)
 
 
+def test_shm_ring_copies_outside_lock_exactly_once():
+    """Producers copy into reserved regions and consumers copy out of claimed ones outside the ring's lock
+    (native/core.h RingCore): under 3 producer and 3 consumer threads with messages of up to a quarter of the ring
+    (wrap-arounds, space held by in-flight copies), every message arrives exactly once and intact; drop_oldest on a
+    full ring drops committed messages only and counts them."""
+    import hashlib
+    import threading
+    name = f'/dca_test_{uuid.uuid4().hex[:8]}'
+    ring = native.ShmRing(name, 1 << 20, True)
+    try:
+        per, got, lock = 300, [], threading.Lock()
+
+        def prod(k):
+            rng = np.random.RandomState(k)
+            for i in range(per):
+                body = rng.bytes(int(rng.randint(1, 1 << 18)))
+                assert ring.push(f'{k}:{i}:'.encode() + hashlib.sha1(body).hexdigest().encode() + b':' + body, 30.0,
+                                 False)
+
+        def cons():
+            while True:
+                m = ring.pop(5.0)
+                if m is None:
+                    return
+                with lock:
+                    got.append(m)
+        ts = [threading.Thread(target=prod, args=(k,)) for k in range(3)] + \
+             [threading.Thread(target=cons) for _ in range(3)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=120)
+        seen = set()
+        for m in got:
+            k, i, h, body = m.split(b':', 3)
+            assert hashlib.sha1(body).hexdigest().encode() == h
+            seen.add((int(k), int(i)))
+        assert len(got) == 3 * per and len(seen) == 3 * per and ring.size() == 0
+        # drop_oldest: a full ring makes room by discarding its oldest committed messages
+        for i in range(40):
+            assert ring.push(bytes([i]) * 60000, 0.0, True)
+        assert ring.dropped() > 0
+        first = ring.pop(0.0)
+        assert first is not None and first[0] == 40 - ring.size() - 1
+    finally:
+        native.ShmRing.unlink(name)
+
+
 def test_shm_broker_roundtrip():
     from dotaclient_amd.transport.shm import ShmBroker
     name = f'dca_b_{uuid.uuid4().hex[:8]}'
@@ -166,5 +214,21 @@ def test_shm_broker_view_decodes_rollout():
         for k in ['env', 'units', 'actions', 'masks', 'rewards', 'logp', 'values', 'hiddens']:
             np.testing.assert_array_equal(getattr(d, k), getattr(r, k))
         assert (d.weight_version, d.bootstrap_value, d.done) == (3, 0.25, True)
+        # the CRC-checked pop: the trailer verified while copying out (64 KB blocks, combined CRCs)
+        big = encode(Rollout(**{**r.__dict__, 'units': rng.randn(400, U, 10).astype(np.float32),
+                                'env': rng.randn(400, 3).astype(np.float32),
+                                'actions': np.zeros((400, 21 + U), np.uint8), 'masks': np.ones((400, 21 + U), np.uint8),
+                                'rewards': rng.randn(400, 9), 'logp': rng.randn(400).astype(np.float32),
+                                'values': rng.randn(400).astype(np.float32)}))
+        assert len(big) > 3 * (64 << 10)
+        bad = bytearray(big)
+        bad[len(bad) // 2] ^= 0x10
+        for msg, want in ((big, True), (bytes(bad), False), (b'not a dcx2 message', None)):
+            b.publish_experience(msg)
+            arr, ok = b.consume_experience_checked(1.0)
+            assert ok is want and arr.tobytes() == msg
+        assert b.consume_experience_checked(0.0) is None
+        d2 = decode_any(np.frombuffer(big, np.uint8), crc_checked=True)
+        assert d2.units.shape == (400, U, 10)
     finally:
         b.close(unlink=True)
