@@ -234,7 +234,7 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                      threads: int = 14, seq_len: int = 1400, batch_size: int = 8, seq_per_epoch: int = 16,
                      epochs: int = 1, precision: str = 'fp32', max_dota_time: float = 600.0,
                      rollout_size: int = 9999, warmup_iterations: int = 2, max_iterations: Optional[int] = None,
-                     log_dir: Optional[str] = None, prefetch: int = 32, ring_bytes: int = 1 << 26,
+                     log_dir: Optional[str] = None, prefetch: int = 32, ring_bytes: int = 1 << 29,
                      transport: str = 'auto', backend: str = 'auto', idle_probe: float = 3.0,
                      report=None, record_consumed: int = 0, progress=None, pack: bool = False,
                      league: Optional[str] = None, latest_weights_prob: float = 1.0, actor_precision: str = 'bf16',

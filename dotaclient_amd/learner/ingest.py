@@ -45,6 +45,15 @@ def _round(n: int) -> int:
     return (n + _ALIGN - 1) // _ALIGN * _ALIGN
 
 
+def _release_all(rollouts):
+    """Give the ring regions of dropped ring-resident rollouts back (learner/optimizer.py zero-copy consumption)."""
+    for r in rollouts:
+        rel = getattr(r, 'release', None)
+        if rel is not None:
+            r.release = None
+            rel()
+
+
 class _Stopped(Exception):
     pass
 
@@ -153,6 +162,7 @@ class IngestPipeline:
                 r = self.fetch(self.stop)
                 if r is None:
                     self.lost += len(rollouts)
+                    _release_all(rollouts)
                     return None
                 rollouts.append(r)
                 n_seq += -(-r.length // self.S)
@@ -166,6 +176,7 @@ class IngestPipeline:
                 r = self.fetch(self.stop)
             if r is None:
                 self.lost += len(rollouts)
+                _release_all(rollouts)
                 return None
             if pk.n_seq >= self.need and not pk.fits(r):
                 self._carry = r
@@ -187,6 +198,7 @@ class IngestPipeline:
                         st = self.stage(rollouts)
                     except _Stopped:
                         self.lost += len(rollouts)
+                        _release_all(rollouts)
                         break
                     while True:
                         try:
@@ -303,6 +315,10 @@ class IngestPipeline:
             rv = hview(rst_off, L, 'uint8', (L,))
             rv[:] = 0
             rv[resets] = 1
+        # ring-resident rollouts (zero-copy consumption, learner/optimizer.py): everything the upload needs is in the
+        # pinned slot now — give their ring regions back (the canvas of the last one is kept for the logs)
+        for i, r in enumerate(rollouts):
+            r.detach_shared(keep_canvas=i == len(rollouts) - 1)
         ev = None
         if self.cuda:
             # blocking events: the stager waits on them (slot reuse) for up to an iteration, and a spinning wait
@@ -385,6 +401,8 @@ class IngestPipeline:
         if self.th.is_alive():
             raise RuntimeError('experience stager thread did not stop')
         dropped = self.lost + (1 if self._carry is not None else 0)
+        if self._carry is not None:
+            _release_all([self._carry])
         self._carry = None
         while True:
             try:

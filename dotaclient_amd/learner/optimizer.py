@@ -266,7 +266,8 @@ class DotaOptimizer:
                 # (queue size, model publish) must not wait behind the thread's long polls
                 mk = getattr(self.broker, 'consumer', None)
                 self._xp_broker = mk() if mk is not None else self.broker
-                pf = self._prefetcher = _RolloutPrefetcher(self._consume_decode, self.cfg.prefetch_rollouts)
+                pf = self._prefetcher = _RolloutPrefetcher(lambda stop: self._consume_decode(stop, claim=True),
+                                                           self.cfg.prefetch_rollouts)
                 self.prefetch_dropped = 0
             return pf.get()
         return self._consume_decode()
@@ -295,11 +296,46 @@ class DotaOptimizer:
                 xb.close()
             self._xp_broker = None
 
-    def _consume_decode(self, stop=None) -> Rollout:
+    def _consume_decode(self, stop=None, claim: bool = False) -> Rollout:
         """Next decodable rollout from the queue. With ``stop`` (the decode-ahead thread's event) the queue is polled
         in bounded slices so that :meth:`close` ends the thread promptly instead of leaving it blocked inside the
-        broker; returns None once ``stop`` is set."""
+        broker; returns None once ``stop`` is set.
+
+        ``claim`` (the GPU learner's stager pipeline on the node's shared-memory ring): the rollout's arrays VIEW the
+        message inside the ring — no copy out of it; the stager copies the fields straight into its pinned upload slot
+        and gives the region back (:meth:`Rollout.detach_shared`). One host copy per message instead of two (ring →
+        heap → pinned). Claims are budgeted to half the ring, beyond that the copying path is taken, so held claims
+        can never starve the producers."""
         broker = getattr(self, '_xp_broker', None) or self.broker
+        if claim and stop is not None and hasattr(broker, 'claim_experience'):
+            cb = self.__dict__.setdefault('_claim_budget', _ClaimBudget(getattr(broker, 'capacity', 0) // 2))
+            t0 = time.monotonic()
+            while cb.available():
+                got = None
+                while got is None:
+                    if stop.is_set():
+                        return None
+                    if self.cfg.xp_timeout is not None and time.monotonic() - t0 > self.cfg.xp_timeout:
+                        raise TimeoutError('no experience received')
+                    got = broker.claim_experience(timeout=0.25)
+                view, token = got
+                n = cb.take(view.nbytes)
+                released = [False]
+
+                def rel(token=token, n=n, released=released):
+                    if not released[0]:
+                        released[0] = True
+                        broker.release_experience(token)
+                        cb.give(n)
+                try:
+                    r = decode_any(view, allow_pickle=self.cfg.allow_pickle_experience)
+                except CorruptMessage as e:
+                    rel()
+                    self.corrupt_rollouts += 1
+                    logger.warning('dropping corrupted experience message (%s); %d so far', e, self.corrupt_rollouts)
+                    continue
+                r.release = rel
+                return r
         checked = getattr(broker, 'consume_experience_checked', None)    # shm ring: CRC verified during the copy
         consume = checked or getattr(broker, 'consume_experience_view', None) or broker.consume_experience
         total = self.cfg.xp_timeout
@@ -915,6 +951,29 @@ class DotaOptimizer:
         ckpt.prune(self.cfg.log_dir, self.cfg.checkpoint_keep)
 
 
+class _ClaimBudget:
+    """Bytes of ring-resident (claimed, not yet released) messages the learner may hold at once."""
+
+    def __init__(self, limit: int):
+        import threading
+        self.limit = int(limit)
+        self.held = 0
+        self.lock = threading.Lock()
+
+    def available(self) -> bool:
+        with self.lock:
+            return self.held < self.limit
+
+    def take(self, n: int) -> int:
+        with self.lock:
+            self.held += n
+        return n
+
+    def give(self, n: int):
+        with self.lock:
+            self.held -= n
+
+
 class _RolloutPrefetcher:
     """Background consume + decode of experience messages into a bounded queue. The learner's main thread then only
     waits when the actors are behind; DCX1 decode (CRC, array views) and broker waits overlap the GPU training of the
@@ -945,6 +1004,7 @@ class _RolloutPrefetcher:
                     except self._queue_mod.Full:
                         if self.stop.is_set():
                             self.lost += 1
+                            _release(r)
                             return
         except BaseException as e:       # surfaced on the consumer's thread
             self.err = e
@@ -977,7 +1037,22 @@ class _RolloutPrefetcher:
         self.th.join(timeout=30.0)
         if self.th.is_alive():
             raise RuntimeError('experience prefetch thread did not stop')
-        return self.lost + self.q.qsize()
+        n = self.lost
+        while True:
+            try:
+                _release(self.q.get_nowait())
+            except self._queue_mod.Empty:
+                break
+            n += 1
+        return n
+
+
+def _release(r):
+    """Give a ring-resident rollout's region back (a dropped one: nothing of it is read any more)."""
+    rel = getattr(r, 'release', None)
+    if rel is not None:
+        r.release = None
+        rel()
 
 
 def _to_cpu(x):

@@ -429,6 +429,27 @@ class RingCore {
   // pop the oldest committed message, handing (payload, length) to fn OUTSIDE the lock (fn copies it out)
   template <class F>
   bool pop_with(F&& fn, double timeout) {
+    uint64_t pos, len;
+    if (!claim(&pos, &len, timeout)) return false;
+    fn(data_ + pos + 8, len);
+    release(pos);
+    return true;
+  }
+
+  // zero-copy consumption: claim the oldest committed message (its region stays reserved, readable at
+  // payload(pos), until release(pos)); releases may come in any order, space is reclaimed oldest-first
+  const uint8_t* payload(uint64_t pos) const { return data_ + pos + 8; }
+  void release(uint64_t pos) {
+    lock();
+    const uint64_t w = word_at(pos);
+    if ((w >> 56) == kReading) {
+      set_word(pos, (kDone << 56) | (w & kLenMask));
+      reclaim_locked();
+      pthread_cond_broadcast(&hdr_->not_full);
+    }
+    unlock();
+  }
+  bool claim(uint64_t* pos_out, uint64_t* len_out, double timeout) {
     timespec ts;
     if (timeout > 0) deadline_in(timeout, ts);
     uint64_t stuck_at = ~0ull;          // head offset seen in the writing state, and since when
@@ -445,12 +466,8 @@ class RingCore {
           hdr_->head = off + padded(len);
           hdr_->count -= 1;
           unlock();
-          fn(data_ + pos + 8, len);     // outside the lock
-          lock();
-          set_word(pos, (kDone << 56) | len);
-          reclaim_locked();
-          pthread_cond_broadcast(&hdr_->not_full);
-          unlock();
+          *pos_out = pos;
+          *len_out = len;
           return true;
         }
         // the oldest message is still being written: wait for its commit; a producer that never commits (it died

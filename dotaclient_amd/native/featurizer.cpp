@@ -152,6 +152,23 @@ class ShmRing {
     py::array_t<uint8_t> arr({(py::ssize_t)n}, {(py::ssize_t)1}, buf, owner);
     return py::make_tuple(arr, ok < 0 ? py::object(py::none()) : py::object(py::bool_(ok == 1)));
   }
+  // zero-copy: (uint8 array viewing the message IN the shared ring, token) — the region stays reserved until
+  // release(token); the array must not be read after that. The array keeps this ring object alive.
+  py::object claim(py::object self, double timeout) {
+    uint64_t pos, len;
+    bool got;
+    {
+      py::gil_scoped_release rel;
+      got = r_.claim(&pos, &len, timeout);
+    }
+    if (!got) return py::none();
+    py::array_t<uint8_t> arr({(py::ssize_t)len}, {(py::ssize_t)1}, r_.payload(pos), self);
+    return py::make_tuple(arr, pos);
+  }
+  void release(uint64_t token) {
+    py::gil_scoped_release rel;
+    r_.release(token);
+  }
   uint64_t size() { return r_.size(); }
   uint64_t dropped() { return r_.dropped(); }
   static void unlink(const std::string& name) { RingCore::unlink(name); }
@@ -431,6 +448,9 @@ PYBIND11_MODULE(_native, m) {
       .def("pop", &ShmRing::pop, py::arg("timeout") = -1.0)
       .def("pop_view", &ShmRing::pop_view, py::arg("timeout") = -1.0)
       .def("pop_checked", &ShmRing::pop_checked, py::arg("timeout") = -1.0)
+      .def("claim", [](py::object self, double timeout) { return self.cast<ShmRing&>().claim(self, timeout); },
+           py::arg("timeout") = -1.0)
+      .def("release", &ShmRing::release, py::arg("token"))
       .def("size", &ShmRing::size)
       .def("dropped", &ShmRing::dropped)
       .def_static("unlink", &ShmRing::unlink);

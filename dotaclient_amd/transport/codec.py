@@ -89,10 +89,25 @@ class Rollout:
     bootstrap_value: float = 0.0
     done: bool = True
     layout: Tuple[int, ...] = field(default_factory=lambda: LAYOUT_1V1.counts)
+    # zero-copy consumption (ShmBroker.claim_experience): the arrays view the message inside the shared ring, and this
+    # callable gives its region back; see :meth:`detach_shared`
+    release: Optional[object] = field(default=None, repr=False, compare=False)
 
     @property
     def length(self) -> int:
         return int(self.rewards.shape[0])
+
+    def detach_shared(self, keep_canvas: bool = False):
+        """Once a ring-resident rollout has been staged (learner/ingest.py): keep private copies of what the learner
+        still reads afterwards (rewards for the per-key logs, optionally the canvas), drop the views of the bulk
+        arrays — any later read fails loudly instead of reading a recycled ring region — and release the region."""
+        if self.release is None:
+            return
+        self.rewards = np.array(self.rewards)
+        self.canvas = np.array(self.canvas) if (keep_canvas and self.canvas is not None) else None
+        self.env = self.units = self.actions = self.masks = self.logp = self.values = self.hiddens = None
+        rel, self.release = self.release, None
+        rel()
 
     def unit_layout(self) -> UnitLayout:
         return UnitLayout(*self.layout)

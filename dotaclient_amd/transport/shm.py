@@ -22,6 +22,7 @@ class ShmBroker:
         if create is None:
             create = not os.path.exists(path)
         self.ring = native.ShmRing(f'/{self.name}_xp', capacity, create)
+        self._capacity = os.path.getsize(path)       # (+ the ring header: close enough for claim budgeting)
         self.model_path = f'/dev/shm/{self.name}_model'
         self.drop_oldest = drop_oldest
         self._subs = []
@@ -46,6 +47,18 @@ class ShmBroker:
         of the ring (``ShmRing.pop_checked``): ``(array, ok)`` with ok True / False for DCX2 messages and None for
         other formats (the decoder then checks them), or None when nothing arrived."""
         return self.ring.pop_checked(-1.0 if timeout is None else float(timeout))
+
+    def claim_experience(self, timeout: Optional[float] = None):
+        """Zero-copy consumption: ``(array, token)`` with the array viewing the message inside the ring (its region
+        stays reserved) until :meth:`release_experience` ``(token)`` — exactly once; None when nothing arrived."""
+        return self.ring.claim(-1.0 if timeout is None else float(timeout))
+
+    def release_experience(self, token: int):
+        self.ring.release(int(token))
+
+    @property
+    def capacity(self) -> int:
+        return int(self._capacity)
 
     @property
     def xp_queue_size(self) -> int:

@@ -67,6 +67,49 @@ def test_ingest_stage_packs_rows_in_row_order():
     np.testing.assert_array_equal(x['env'][5:12].numpy(), rs[2].env)
 
 
+def test_stager_stages_ring_resident_rollouts_and_releases_them():
+    """Zero-copy consumption (learner/optimizer.py ``_consume_decode(claim=True)``): the stager thread receives
+    rollouts whose arrays view their messages inside the shared-memory ring, copies every field straight into its
+    upload slot, and gives the regions back (Rollout.detach_shared) — the staged rows equal the rollouts, the bulk
+    arrays are dropped afterwards, the last canvas is kept, and the ring has its space back."""
+    import threading
+    import uuid
+    from dotaclient_amd import native
+    from dotaclient_amd.learner.optimizer import DotaOptimizer, OptimizerConfig
+    from dotaclient_amd.transport.codec import encode
+    from dotaclient_amd.transport.shm import ShmBroker
+    if not native.AVAILABLE:
+        pytest.skip('native module not built')
+    S = 16
+    b = ShmBroker(f'dca_zc_{uuid.uuid4().hex[:8]}', capacity=1 << 24, create=True)
+    try:
+        cfg = OptimizerConfig(log_dir='', model='lstm128', seq_len=S, seq_per_epoch=2, batch_size=2,
+                              pack_sequences=True, run_local=True)
+        opt = DotaOptimizer.__new__(DotaOptimizer)      # only the consumption path: no learner, no GPU
+        opt.cfg, opt.broker, opt.corrupt_rollouts = cfg, b, 0
+        rs = [_rollout(5, 1), _rollout(20, 2), _rollout(7, 3)]
+        for r in rs:
+            r.canvas = np.full((4, 4, 3), r.length, np.uint8)
+            b.publish_experience(encode(r))
+        stop = threading.Event()
+        got = [opt._consume_decode(stop, claim=True) for _ in rs]
+        assert all(g.release is not None for g in got) and opt._claim_budget.held > 0
+        pl = IngestPipeline(None, S, 2, 'ppo', 8, 'cpu', pack=True)
+        st = pl.stage(got)
+        assert opt._claim_budget.held == 0 and all(g.release is None and g.units is None for g in got)
+        assert st.rollouts[-1].canvas is not None and all(g.canvas is None for g in st.rollouts[:-1])
+        x = pl.expand(st, {})
+        np.testing.assert_array_equal(x['env'][5:12].numpy(), rs[2].env)
+        np.testing.assert_array_equal(x['units'][16:36].numpy(), rs[1].units)
+        assert [g.length for g in st.rollouts] == [5, 7, 20]
+        # the ring is empty and its space reusable: a half-ring message goes through (wherever the cursor stands)
+        big = b'x' * ((1 << 23) - 4096)
+        b.publish_experience(big, timeout=5.0)
+        assert b.consume_experience(1.0) == big
+    finally:
+        b.close(unlink=True)
+
+
 def _ppo_grads(pol, batch):
     lrn = Learner(pol, LossConfig(algo='ppo', vf_coef=0.5, entropy_coef=0.01), device='cpu', backend='torch', dp=False)
     pol.zero_grad()
