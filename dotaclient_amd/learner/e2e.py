@@ -209,10 +209,12 @@ def _actor_process_main(addr: str, model: str, games: int, threads: int, seq_len
             lg = League(ws, mode=league)
         from ..models.policy import get_config
         mode = '5v5' if get_config(model).layout.counts[0] > 1 else '1v1'   # (BASELINE config 4: 5v5 self-play)
+        # on the node's shared-memory ring the engine encodes finished rollouts straight into it (VecActor ring_sink)
+        sink = br if hasattr(br, 'ring') else None
         va = VecActor(ws, games, br.publish_experience, device=device, mode=mode, seed=seed,
                       rollout_size=rollout_size, max_dota_time=max_dota_time, hidden_stride=seq_len, threads=threads,
                       stagger=True, tag=f'{tag}.vec', league=lg, latest_weights_prob=latest_weights_prob,
-                      precision=precision)      # (game ids unique across the node's actor processes)
+                      precision=precision, ring_sink=sink)   # (game ids unique across the node's actor processes)
         for _ in range(3):
             va.step()
         ready.set()

@@ -380,6 +380,17 @@ class RingCore {
   void unlock() { pthread_mutex_unlock(&hdr_->mu); }
 
   bool push(const char* msg_data, size_t msg_size, double timeout, bool drop_oldest) {
+    uint64_t pos;
+    if (!reserve(msg_size, timeout, drop_oldest, &pos)) return false;
+    std::memcpy(data_ + pos + 8, msg_data, msg_size);     // outside the lock
+    return commit(pos, msg_size);
+  }
+
+  // producer side in two steps: reserve a region for msg_size bytes (writable at wpayload(pos) without the lock),
+  // then commit it. False from reserve: no space within the timeout; false from commit: the region was given up as
+  // abandoned (kAbandonS) and the message is lost.
+  uint8_t* wpayload(uint64_t pos) { return data_ + pos + 8; }
+  bool reserve(size_t msg_size, double timeout, bool drop_oldest, uint64_t* pos_out) {
     const uint64_t need = padded(msg_size);
     if (need + 8 > hdr_->capacity || msg_size > kLenMask) throw std::invalid_argument("message larger than ring");
     timespec ts;
@@ -397,19 +408,12 @@ class RingCore {
           hdr_->tail += to_end;
         }
         const uint64_t p = hdr_->tail % cap;
-        const uint64_t w = (kWriting << 56) | (uint64_t)msg_size;
-        set_word(p, w);
+        set_word(p, (kWriting << 56) | (uint64_t)msg_size);
         hdr_->tail += need;
         hdr_->count += 1;
         unlock();
-        std::memcpy(data_ + p + 8, msg_data, msg_size);     // outside the lock
-        lock();
-        const bool ok = word_at(p) == w;                     // (else a consumer gave the region up as abandoned)
-        if (ok) set_word(p, (kReady << 56) | (uint64_t)msg_size);
-        pthread_cond_broadcast(&hdr_->not_empty);
-        pthread_cond_broadcast(&hdr_->not_full);   // a drop_oldest producer may be waiting for this commit
-        unlock();
-        return ok;
+        *pos_out = p;
+        return true;
       }
       if (drop_oldest && drop_head_locked()) continue;
       if (timeout == 0.0) { unlock(); return false; }
@@ -420,6 +424,15 @@ class RingCore {
         return false;
       }
     }
+  }
+  bool commit(uint64_t pos, size_t msg_size) {
+    lock();
+    const bool ok = word_at(pos) == ((kWriting << 56) | (uint64_t)msg_size);   // (else given up as abandoned)
+    if (ok) set_word(pos, (kReady << 56) | (uint64_t)msg_size);
+    pthread_cond_broadcast(&hdr_->not_empty);
+    pthread_cond_broadcast(&hdr_->not_full);   // a drop_oldest producer may be waiting for this commit
+    unlock();
+    return ok;
   }
 
   bool pop(std::string* out, double timeout) {

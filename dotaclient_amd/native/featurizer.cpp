@@ -169,6 +169,7 @@ class ShmRing {
     py::gil_scoped_release rel;
     r_.release(token);
   }
+  RingCore* core() { return &r_; }
   uint64_t size() { return r_.size(); }
   uint64_t dropped() { return r_.dropped(); }
   static void unlink(const std::string& name) { RingCore::unlink(name); }
@@ -266,6 +267,13 @@ class PyVecEnv {
   long games_finished() const { return env_.games_finished(); }
   long steps_taken() const { return env_.steps_taken(); }
   long rollouts_sent() const { return env_.rollouts_sent(); }
+  long sink_lost() const { return env_.sink_lost(); }
+  // finished rollouts go straight into this ring (encoded in place by the worker threads); the ring object is kept
+  // alive by this env
+  void set_ring_sink(py::object ring, double timeout, bool drop_oldest) {
+    ring_ref_ = ring;
+    env_.set_sink(ring.cast<ShmRing&>().core(), timeout, drop_oldest);
+  }
   long wire_bytes() const { return env_.wire_bytes(); }
   double dota_time(int g) const { return env_.dota_time(g); }
   int status(int g) const { return env_.status(g); }
@@ -296,6 +304,7 @@ class PyVecEnv {
     c.wire = wire;
     return c;
   }
+  py::object ring_ref_;     // (declared before env_: destroyed after it)
   VecEnv env_;
   int S_ = 0, U_ = 0, H_ = 0;
 };
@@ -428,6 +437,9 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("games_finished", &PyVecEnv::games_finished)
       .def_property_readonly("steps_taken", &PyVecEnv::steps_taken)
       .def_property_readonly("rollouts_sent", &PyVecEnv::rollouts_sent)
+      .def_property_readonly("sink_lost", &PyVecEnv::sink_lost)
+      .def("set_ring_sink", &PyVecEnv::set_ring_sink, py::arg("ring"), py::arg("timeout") = -1.0,
+           py::arg("drop_oldest") = true)
       .def_property_readonly("wire_bytes", &PyVecEnv::wire_bytes)
       .def("dota_time", &PyVecEnv::dota_time)
       .def("status", &PyVecEnv::status);

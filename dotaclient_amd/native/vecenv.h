@@ -733,9 +733,10 @@ inline std::string json_escape(const std::string& s) {
   return o;
 }
 
-inline std::string encode_dcx1(const std::string& game_id, int team_id, int player_id, long weight_version,
+// DCX2 header JSON of a message (transport/codec.py encode); *arrays_bytes = Σ array payload bytes
+inline std::string dcx2_header(const std::string& game_id, int team_id, int player_id, long weight_version,
                                double bootstrap, bool done, int hidden_stride, const int* layout,
-                               const std::vector<ArrayRef>& arrays) {
+                               const std::vector<ArrayRef>& arrays, size_t* arrays_bytes) {
   std::string h = "{\"game_id\":\"" + json_escape(game_id) + "\",\"team_id\":" + std::to_string(team_id) +
                   ",\"player_id\":" + std::to_string(player_id) + ",\"weight_version\":" +
                   std::to_string(weight_version) + ",\"bootstrap_value\":";
@@ -755,15 +756,43 @@ inline std::string encode_dcx1(const std::string& game_id, int team_id, int play
     off += a.bytes;
   }
   h += "]}";
-  std::string out;
-  out.reserve(8 + h.size() + off + 4);
-  out.append("DCX2", 4);
+  *arrays_bytes = off;
+  return h;
+}
+inline size_t dcx2_size(const std::string& h, size_t arrays_bytes) { return 8 + h.size() + arrays_bytes + 4; }
+
+// write a DCX2 message (dcx2_size bytes) into dst: magic, header length, header, arrays, CRC-32C trailer. Each piece
+// is copied in 64 KB blocks and CRC'd right after, while the block is in cache (per-block CRCs combined), instead of a
+// second full pass over the message.
+inline void dcx2_write(uint8_t* dst, const std::string& h, const std::vector<ArrayRef>& arrays) {
+  uint32_t crc = 0;
+  size_t at = 0;
+  auto put = [&](const void* src, size_t n) {
+    constexpr size_t kBlk = 64 << 10;
+    for (size_t o = 0; o < n; o += kBlk) {
+      const size_t b = std::min(kBlk, n - o);
+      std::memcpy(dst + at, static_cast<const uint8_t*>(src) + o, b);
+      const uint32_t c = crc32c_raw(dst + at, b);
+      crc = at == 0 ? c : crc32c_combine(crc, c, b);
+      at += b;
+    }
+  };
   const uint32_t hl = (uint32_t)h.size();
-  out.append((const char*)&hl, 4);
-  out.append(h);
-  for (const ArrayRef& a : arrays) out.append((const char*)a.data, a.bytes);
-  const uint32_t crc = crc32c_raw((const uint8_t*)out.data(), out.size());
-  out.append((const char*)&crc, 4);
+  put("DCX2", 4);
+  put(&hl, 4);
+  put(h.data(), h.size());
+  for (const ArrayRef& a : arrays) put(a.data, a.bytes);
+  std::memcpy(dst + at, &crc, 4);
+}
+
+inline std::string encode_dcx1(const std::string& game_id, int team_id, int player_id, long weight_version,
+                               double bootstrap, bool done, int hidden_stride, const int* layout,
+                               const std::vector<ArrayRef>& arrays) {
+  size_t ab;
+  const std::string h = dcx2_header(game_id, team_id, player_id, weight_version, bootstrap, done, hidden_stride,
+                                    layout, arrays, &ab);
+  std::string out(dcx2_size(h, ab), '\0');
+  dcx2_write(reinterpret_cast<uint8_t*>(&out[0]), h, arrays);
   return out;
 }
 
@@ -970,6 +999,13 @@ class VecEnv {
   long games_finished() const { return games_finished_; }
   long steps_taken() const { return steps_taken_.load(); }
   long rollouts_sent() const { return rollouts_sent_.load(); }
+  long sink_lost() const { return sink_lost_.load(); }
+  // publish finished rollouts straight into a shared-memory ring (the caller keeps it alive) instead of out_
+  void set_sink(RingCore* ring, double timeout, bool drop_oldest) {
+    sink_ = ring;
+    sink_timeout_ = timeout;
+    sink_drop_ = drop_oldest;
+  }
   long wire_bytes() const { return wire_bytes_.load(); }
   double dota_time(int gi) const { return games_[gi].sim.dota_time; }
   int status(int gi) const { return games_[gi].sim.status; }
@@ -1121,6 +1157,26 @@ class VecEnv {
     if (!t.hiddens.empty()) {
       const long K = (long)(t.hiddens.size() / (2 * (size_t)cfg_.hidden_size));
       arr.push_back({"hiddens", "<f4", {K, 2, cfg_.hidden_size}, t.hiddens.data(), t.hiddens.size() * 4});
+    }
+    if (sink_ != nullptr) {
+      // encoded straight into a reserved region of the node's experience ring (no intermediate string, no Python
+      // bytes object, no second copy by a publish call) from this worker thread
+      size_t ab;
+      const std::string h = dcx2_header(g.game_id, p.team, p.player_id, version, bootstrap, done,
+                                        t.hiddens.empty() ? 0 : cfg_.hidden_stride, cfg_.counts, arr, &ab);
+      const size_t n = dcx2_size(h, ab);
+      uint64_t pos;
+      if (!sink_->reserve(n, sink_timeout_, sink_drop_, &pos)) {
+        sink_lost_ += 1;
+        return;
+      }
+      dcx2_write(sink_->wpayload(pos), h, arr);
+      if (!sink_->commit(pos, n)) {
+        sink_lost_ += 1;
+        return;
+      }
+      rollouts_sent_ += 1;
+      return;
     }
     std::string b = encode_dcx1(g.game_id, p.team, p.player_id, version, bootstrap, done,
                                 t.hiddens.empty() ? 0 : cfg_.hidden_stride, cfg_.counts, arr);
@@ -1318,7 +1374,10 @@ class VecEnv {
   PyRandom rng_;
   uint64_t started_ = 0;
   long games_finished_ = 0;
-  std::atomic<long> steps_taken_{0}, rollouts_sent_{0}, wire_bytes_{0};
+  std::atomic<long> steps_taken_{0}, rollouts_sent_{0}, wire_bytes_{0}, sink_lost_{0};
+  RingCore* sink_ = nullptr;
+  double sink_timeout_ = -1.0;
+  bool sink_drop_ = true;
   std::mutex out_m_;
   std::vector<std::string> out_;
   std::vector<std::array<int, 3>> results_;

@@ -81,6 +81,43 @@ def test_vec_actor_rollouts_replay_consistent(groups):
     assert va.steps_taken >= sum(r.length for r in rs)
 
 
+def test_vec_actor_ring_sink_encodes_into_the_ring():
+    """VecActor(ring_sink=ShmBroker): the engine's worker threads encode finished rollouts straight into reserved ring
+    regions (native/vecenv.h dcx2_write, per-block CRC) — the same messages the publish path produces: they decode
+    with a valid CRC-32C, replay-consistent, counted in rollouts_sent, none through ``publish``."""
+    import uuid
+    from dotaclient_amd.actor.vec import VecActor
+    from dotaclient_amd.transport.shm import ShmBroker
+    cfg = get_config('lstm128')
+    ws = _store(cfg)
+    b = ShmBroker(f'dca_sink_{uuid.uuid4().hex[:8]}', capacity=1 << 26, create=True, drop_oldest=True)
+    try:
+        sent = []
+        stride = 8
+        va = VecActor(ws, 3, sent.append, device='cpu', seed=5, rollout_size=24, max_dota_time=25.0,
+                      hidden_stride=stride, threads=2, groups=2, ring_sink=b)
+        while va.games_finished < 4:
+            va.step()
+        assert not sent and va.rollouts_sent > 0 and va.sink_lost == 0
+        rs = []
+        while True:
+            got = b.consume_experience_checked(0.0)
+            if got is None:
+                break
+            arr, ok = got
+            assert ok is True
+            rs.append(decode(arr.tobytes()))
+        assert len(rs) == va.rollouts_sent
+        pol = ws.policy_for(ws.latest_weights())
+        for r in rs[:6]:
+            hs, vals, lps = _replay(pol, r, stride)
+            np.testing.assert_allclose(hs, r.hiddens, atol=2e-5)
+            np.testing.assert_allclose(vals, r.values, atol=2e-5)
+            np.testing.assert_allclose(lps, r.logp, atol=5e-4)
+    finally:
+        b.close(unlink=True)
+
+
 def test_vec_actor_league_opponents_and_hot_swap():
     from dotaclient_amd.actor.league import League
     from dotaclient_amd.actor.vec import VecActor
