@@ -509,6 +509,9 @@ __device__ __forceinline__ void lstm_team_fwd_body(
       if (sh_int == -2) break;
       TSTAMP(2);
       if constexpr (V1) {
+       // (only the waves that own units: at H < 512 a workgroup's U = H/32 units take U/4 of its 4 waves — the
+       // others have no W_hh slice and would publish / store other workgroups' units)
+       if (mfma_wave) {
         // ---- exact fp32 VALU, R rows: the 4 gates of this lane's unit over its K slice for every row (W_hh slice in
         // VGPRs reused across the rows), summed over the unit's LPU slices — every lane of the group holds every row
         float g[R][4];
@@ -562,6 +565,7 @@ __device__ __forceinline__ void lstm_team_fwd_body(
           if (!(slice & 1)) *reinterpret_cast<dca::f32x4*>(gates4 + o * 4) = av;
         }
         TSTAMP(5);
+       }
       } else if (mfma_wave) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
