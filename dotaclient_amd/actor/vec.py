@@ -328,31 +328,61 @@ class VecActor:
 
 def measure_vec_actor(policy, device='cuda', n_games: int = 2048, steps: int = 100, warmup: int = 10,
                       threads: int = 8, groups: int = 2, hidden_stride: int = 1400, rollout_size: int = 9999,
-                      max_dota_time: float = 600.0, wire: bool = False, precision: str = 'bf16') -> Dict[str, float]:
+                      max_dota_time: float = 600.0, wire: bool = False, precision: str = 'bf16',
+                      ring: bool = True) -> Dict[str, float]:
     """Whole-runtime actor throughput: player-steps/s of :class:`VecActor` self-play (engine + featurize + reward +
-    GPU policy + trajectory recording + rollout encoding), rollouts counted (published into a sink). Deploy shape
-    (params.libsonnet:16-19): whole-game rollouts (``rollout_size`` 9999) of 600 s games, with staggered first
-    games so the measured window sees the steady-state rate of finished games (and their DCX1 encoding)."""
+    GPU policy + trajectory recording + rollout encoding), rollouts counted. Deploy shape (params.libsonnet:16-19):
+    whole-game rollouts (``rollout_size`` 9999) of 600 s games, with staggered first games so the measured window sees
+    the steady-state rate of finished games (and their encoding). ``ring`` (default): rollouts are encoded into a
+    shared-memory experience ring as in the node loop (VecActor ring_sink), drained by a thread that claims and
+    releases them without copying (the learner's consumption cost belongs to the learner process); otherwise they are
+    published as Python bytes into a list."""
+    import threading
+    import uuid
     from .weights import WeightStore
     ws = WeightStore(policy.config, device='cpu')
     ws.add(0, {k: v.detach().cpu() for k, v in policy.state_dict().items()})
     sink = []
-    va = VecActor(ws, n_games, lambda b: sink.append(len(b)), device=device, seed=1, threads=threads,
-                  groups=groups, hidden_stride=hidden_stride, rollout_size=rollout_size,
-                  max_dota_time=max_dota_time, stagger=True, wire=wire, precision=precision)
-    sync = (lambda: torch.cuda.synchronize(va.device)) if va.device.type == 'cuda' else (lambda: None)
-    for _ in range(warmup):
-        va.step()
-    sync()
-    s0, r0, k0, w0 = va.steps_taken, va.rollouts_sent, len(sink), va.wire_bytes
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        va.step()
-    sync()
-    dt = time.perf_counter() - t0
-    n = va.steps_taken - s0
-    return {'steps_per_s': n / dt, 'ms_per_step': dt / steps * 1e3, 'games': n_games,
-            'player_steps': n, 'rollouts_per_s': (va.rollouts_sent - r0) / dt,
-            'rollout_mb_per_s': sum(sink[k0:]) / dt / 1e6, 'threads': threads, 'groups': groups,
-            'rollout_size': rollout_size, 'wire': wire, 'protobuf_mb_per_s': (va.wire_bytes - w0) / dt / 1e6,
-            'precision': precision}
+    br = drain = None
+    stop = threading.Event()
+    drained = [0, 0]
+    if ring:
+        from ..transport.shm import ShmBroker
+        br = ShmBroker(f'dca_actor_{uuid.uuid4().hex[:10]}', capacity=1 << 28, create=True, drop_oldest=True)
+
+        def run():
+            while not stop.is_set():
+                got = br.claim_experience(0.05)
+                if got is not None:
+                    drained[0] += 1
+                    drained[1] += int(got[0].nbytes)
+                    br.release_experience(got[1])
+        drain = threading.Thread(target=run, name='actor-bench-drain', daemon=True)
+        drain.start()
+    try:
+        va = VecActor(ws, n_games, lambda b: sink.append(len(b)), device=device, seed=1, threads=threads,
+                      groups=groups, hidden_stride=hidden_stride, rollout_size=rollout_size,
+                      max_dota_time=max_dota_time, stagger=True, wire=wire, precision=precision, ring_sink=br)
+        sync = (lambda: torch.cuda.synchronize(va.device)) if va.device.type == 'cuda' else (lambda: None)
+        for _ in range(warmup):
+            va.step()
+        sync()
+        s0, r0, k0, w0, b0 = va.steps_taken, va.rollouts_sent, len(sink), va.wire_bytes, drained[1]
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            va.step()
+        sync()
+        dt = time.perf_counter() - t0
+        n = va.steps_taken - s0
+        mb = (drained[1] - b0) if ring else sum(sink[k0:])
+        return {'steps_per_s': n / dt, 'ms_per_step': dt / steps * 1e3, 'games': n_games,
+                'player_steps': n, 'rollouts_per_s': (va.rollouts_sent - r0) / dt,
+                'rollout_mb_per_s': mb / dt / 1e6, 'threads': threads, 'groups': groups,
+                'rollout_size': rollout_size, 'wire': wire, 'protobuf_mb_per_s': (va.wire_bytes - w0) / dt / 1e6,
+                'precision': precision, 'publish': 'shm ring (in-place encode)' if ring else 'python bytes'}
+    finally:
+        stop.set()
+        if drain is not None:
+            drain.join(timeout=10)
+        if br is not None:
+            br.close(unlink=True)

@@ -57,6 +57,17 @@ def hook_q(m, i, o):
 
 
 pol64 = pol64.double()
+_heads = pol64.heads
+
+
+def heads_hook(x, ue):
+    d, v = _heads(x, ue)
+    d['target_unit'].retain_grad()
+    cap['tl'] = d['target_unit']
+    return d, v
+
+
+pol64.heads = heads_hook
 pol64.entity_attn.register_forward_hook(lambda m, i, o: hook_e1(m, i, o))
 pol64.affine_unit_attention.register_forward_hook(lambda m, i, o: hook_q(m, i, o))
 b = {k: (v.double() if v.is_floating_point() else v) for k, v in batch.items()}
@@ -87,3 +98,17 @@ print('att bias grad rel', rel(g_f['affine_unit_attention.bias'], g64['affine_un
 dq_own = torch.einsum('nu,nud->nd', rec['dtl'].double(), rec['emb'].view(S * B, -1, 128).double())
 print('dq accumulation rel (kernel vs fp64 of its own dtl, E1)', rel(rec['dz'][:, :128], dq_own))
 print('dq from kernel dtl and fp64 E1 vs fp64 dq', rel(torch.einsum('nu,nud->nd', rec['dtl'].double(), E1_64), dq64))
+
+dtl64 = tm(cap['tl'].grad.detach())
+dtlk = rec['dtl'].double()
+E1k = rec['emb'].view(S * B, -1, 128).double()
+print('dtl rel per row', rel(dtlk, dtl64))
+lk = torch.einsum('nd,nud->nu', rec['z'][:, :128].double(), E1k)
+print('pointer logits rel (kernel q, E1 in fp64 vs fp64)', rel(lk, tm(cap['tl'].detach())))
+dq64s = dq64.double().sum(0)
+for name, dt, e in (('kernel dtl, kernel E1', dtlk, E1k), ('fp64 dtl, kernel E1', dtl64, E1k),
+                    ('kernel dtl, fp64 E1', dtlk, E1_64.double()), ('fp64 dtl, fp64 E1', dtl64, E1_64.double())):
+    print(f'Σ_n dq ({name}) rel', rel(torch.einsum('nu,nud->d', dt, e), dq64s))
+print('cancellation Σ|dq| / |Σ dq|', float(dq64.double().abs().sum(0).norm() / dq64s.norm()))
+err = rec['dz'][:, :128].double() - dq64
+print('error coherence |Σ err| / Σ|err|', float(err.sum(0).norm() / err.abs().sum(0).norm()))
