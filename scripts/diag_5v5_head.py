@@ -15,6 +15,12 @@ from dotaclient_amd.models.policy import Policy, get_config  # noqa: E402
 from dotaclient_amd.learner.losses import ppo_loss, split_heads  # noqa: E402
 
 B, S = 8, int(sys.argv[1]) if len(sys.argv) > 1 else 1400
+if len(sys.argv) > 2 and sys.argv[2] == 'precise':       # the recurrence with libm-class activations
+    import dotaclient_amd.models.pipelined as pl
+    _tf, _tb = pl.team_fwd, pl.team_bwd
+    pl.team_fwd = lambda *a, **k: _tf(*a, precise=True, **k)
+    pl.team_bwd = lambda *a, **k: _tb(*a, precise=True, **k)
+    print('recurrence: precise activations')
 torch.manual_seed(0)
 cfg = get_config('5v5')
 pol = Policy(cfg)
@@ -112,3 +118,13 @@ for name, dt, e in (('kernel dtl, kernel E1', dtlk, E1k), ('fp64 dtl, kernel E1'
 print('cancellation Σ|dq| / |Σ dq|', float(dq64.double().abs().sum(0).norm() / dq64s.norm()))
 err = rec['dz'][:, :128].double() - dq64
 print('error coherence |Σ err| / Σ|err|', float(err.sum(0).norm() / err.abs().sum(0).norm()))
+# dtl of the float64 loss evaluated AT the kernel's pointer logits: logits error vs heads_loss arithmetic
+lg = {k: v.detach() for k, v in logits.items()}
+lkb = lk.view(S, B, -1).transpose(0, 1).contiguous().requires_grad_(True)
+lg['target_unit'] = lkb
+lm, _ = ppo_loss(lg, values.detach(), split_heads(b['actions'], counts), split_heads(b['masks'], counts), b['adv'],
+                 b['ret'], b['logp_old'], lc.clip_eps, lc.entropy_coef, lc.vf_coef, stable=True)
+lm.backward()
+dtl_mixed = tm(lkb.grad.detach())
+print('dtl_mixed (fp64 loss at kernel logits) vs fp64 dtl', rel(dtl_mixed, dtl64), '; vs kernel dtl', rel(dtlk, dtl_mixed))
+print('Σ_n dq (dtl_mixed, fp64 E1) rel', rel(torch.einsum('nu,nud->d', dtl_mixed, E1_64.double()), dq64s))
