@@ -122,7 +122,8 @@ def _learner_loop(opt, duration, warmup_iterations, max_iterations, counters, ch
                      m.get('time/train', float('nan')), m.get('time/ingest', float('nan')), m['experience_steps'],
                      m.get('time/h2d', float('nan')), m.get('time/log', float('nan')),
                      m.get('time/publish', float('nan')), m.get('time/lookahead', 0.0),
-                     m.get('time/gpu_train_ms_per_step', float('nan')), m.get('rollouts_consumed', float('nan'))))
+                     m.get('time/gpu_train_ms_per_step', float('nan')), m.get('rollouts_consumed', float('nan')),
+                     m.get('time/stage', float('nan')), m.get('time/gather', float('nan'))))
         e = check()
         if e:
             raise e
@@ -157,6 +158,9 @@ def _summary(rows, wall, actor_steps, dropped, games, config):
         # graph replays and host enqueue gaps included) — compare with the learner-alone ms_per_step
         'learner_gpu_ms_per_step': float(np.nanmean(a[:, 10])) if n_it and np.isfinite(a[:, 10]).any() else float('nan'),
         'rollouts_consumed': int(np.nansum(a[:, 11])) if n_it else 0,
+        # the stager thread per iteration: packing + upload issue, and waiting for the decoded rollouts
+        'stage_ms_per_iteration': 1e3 * float(np.nanmean(a[:, 12])) if n_it and np.isfinite(a[:, 12]).any() else float('nan'),
+        'gather_ms_per_iteration': 1e3 * float(np.nanmean(a[:, 13])) if n_it and np.isfinite(a[:, 13]).any() else float('nan'),
         'actor_steps_per_s': actor_steps / wall,
         'queue_dropped': int(dropped), 'games': games, 'config': config,
     }

@@ -710,6 +710,8 @@ class DotaOptimizer:
             self.timer.stop('train')
             self.timer.start('lookahead')
             st2 = self._ingest_pipeline(thread=True).get()
+            self.timer.add('stage', st2.stage_s)
+            self.timer.add('gather', st2.gather_s)
             if self.consumed is not None:
                 self.consumed.extend((r.game_id, int(r.team_id), int(r.player_id), int(r.weight_version), r.length)
                                      for r in st2.rollouts)

@@ -392,6 +392,34 @@ uint32_t crc32c_buf(py::buffer b, py::ssize_t n) {
   return crc32c_raw(p, (size_t)n);
 }
 
+// Parallel memcpy of a job list (n, 3) int64 = (dst address, src address, bytes), GIL released: the learner's ingest
+// stager packs an iteration's rollout fields (≈40 MB for 16 sequences of 1400 steps) into its pinned upload slot with
+// `threads` threads instead of one numpy copy after another. Jobs are split into ≤ 1 MB pieces and dealt round-robin.
+void copy_jobs(py::array_t<int64_t, py::array::c_style> jobs, int threads) {
+  if (jobs.ndim() != 2 || jobs.shape(1) != 3) throw std::invalid_argument("jobs must be (n, 3) int64");
+  const int64_t* j = jobs.data();
+  const py::ssize_t n = jobs.shape(0);
+  struct Piece { uint8_t* d; const uint8_t* s; size_t b; };
+  std::vector<Piece> pcs;
+  constexpr size_t kPiece = 1 << 20;
+  for (py::ssize_t i = 0; i < n; ++i) {
+    if (j[3 * i + 2] < 0) throw std::invalid_argument("negative byte count");
+    uint8_t* d = reinterpret_cast<uint8_t*>(j[3 * i]);
+    const uint8_t* s = reinterpret_cast<const uint8_t*>(j[3 * i + 1]);
+    const size_t b = (size_t)j[3 * i + 2];
+    for (size_t o = 0; o < b; o += kPiece) pcs.push_back({d + o, s + o, std::min(kPiece, b - o)});
+  }
+  py::gil_scoped_release rel;
+  const int T = std::max(1, std::min<int>(threads, (int)pcs.size()));
+  auto work = [&](int t) {
+    for (size_t k = t; k < pcs.size(); k += T) std::memcpy(pcs[k].d, pcs[k].s, pcs[k].b);
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < T; ++t) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+}
+
 }  // namespace
 
 // glibc malloc for the actor runtime's allocation pattern: every step appends to per-player trajectories (≈2 MB
@@ -414,6 +442,8 @@ PYBIND11_MODULE(_native, m) {
         py::arg("counts"), py::arg("threads") = 4,
         "Decode CMsgBotWorldState bytes and featurize for (player, team): returns env, units, handles, n_allied_creep");
   m.def("crc32c", &crc32c);
+  m.def("copy_jobs", &copy_jobs, py::arg("jobs"), py::arg("threads") = 4,
+        "memcpy a (n, 3) int64 job list of (dst address, src address, bytes) on `threads` threads (GIL released)");
   m.def("crc32c_buf", &crc32c_buf, py::arg("buf"), py::arg("n") = -1,
         "CRC-32C of the first n bytes of a contiguous buffer (GIL released)");
   py::class_<PyVecEnv>(m, "VecEnv")

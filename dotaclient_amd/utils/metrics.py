@@ -95,6 +95,10 @@ class StageTimer:
     def stop(self, name):
         self.t[name] = self.t.get(name, 0.0) + time.perf_counter() - self._t0.pop(name)
 
+    def add(self, name, seconds: float):
+        """Time measured elsewhere (another thread's stage) reported with this iteration's timers."""
+        self.t[name] = self.t.get(name, 0.0) + float(seconds)
+
     def pop(self) -> Dict[str, float]:
         out = {f'time/{k}': v for k, v in self.t.items()}
         self.t = {}
