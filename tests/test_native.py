@@ -232,3 +232,17 @@ def test_shm_broker_view_decodes_rollout():
         assert d2.units.shape == (400, U, 10)
     finally:
         b.close(unlink=True)
+
+
+def test_copy_jobs_parallel_memcpy():
+    """native copy_jobs (the ingest stager's parallel field copy): every job lands, pieces > 1 MB split correctly."""
+    rng = np.random.default_rng(0)
+    srcs = [rng.integers(0, 255, n, dtype=np.uint8) for n in (1, 17, 1 << 20, (3 << 20) + 5, 4096)]
+    dst = np.zeros(sum(s.nbytes for s in srcs) + 64, np.uint8)
+    jobs, o = [], 0
+    for s in srcs:
+        jobs.append((dst.ctypes.data + o, s.ctypes.data, s.nbytes))
+        o += s.nbytes
+    native.copy_jobs(np.asarray(jobs, np.int64), 3)
+    np.testing.assert_array_equal(dst[:o], np.concatenate(srcs))
+    assert not dst[o:].any()
