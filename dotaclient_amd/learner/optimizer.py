@@ -266,8 +266,9 @@ class DotaOptimizer:
                 # (queue size, model publish) must not wait behind the thread's long polls
                 mk = getattr(self.broker, 'consumer', None)
                 self._xp_broker = mk() if mk is not None else self.broker
+                zc = hasattr(self._xp_broker, 'claim_experience')       # the node's shm ring: zero-copy, parallel CRC
                 pf = self._prefetcher = _RolloutPrefetcher(lambda stop: self._consume_decode(stop, claim=True),
-                                                           self.cfg.prefetch_rollouts)
+                                                           self.cfg.prefetch_rollouts, threads=3 if zc else 1)
                 self.prefetch_dropped = 0
             return pf.get()
         return self._consume_decode()
@@ -308,7 +309,9 @@ class DotaOptimizer:
         can never starve the producers."""
         broker = getattr(self, '_xp_broker', None) or self.broker
         if claim and stop is not None and hasattr(broker, 'claim_experience'):
-            cb = self.__dict__.setdefault('_claim_budget', _ClaimBudget(getattr(broker, 'capacity', 0) // 2))
+            cb = self.__dict__.get('_claim_budget')
+            if cb is None:
+                cb = self.__dict__.setdefault('_claim_budget', _ClaimBudget(getattr(broker, 'capacity', 0) // 2))
             t0 = time.monotonic()
             while cb.available():
                 got = None
@@ -979,9 +982,14 @@ class _ClaimBudget:
 class _RolloutPrefetcher:
     """Background consume + decode of experience messages into a bounded queue. The learner's main thread then only
     waits when the actors are behind; DCX1 decode (CRC, array views) and broker waits overlap the GPU training of the
-    previous iteration. An exception in the thread (e.g. the experience timeout) is re-raised by :meth:`get`."""
+    previous iteration. An exception in the thread (e.g. the experience timeout) is re-raised by :meth:`get`.
 
-    def __init__(self, fetch, depth: int):
+    ``threads`` > 1 (the zero-copy shm path, whose per-message CRC runs with the GIL released): several decode threads
+    feed the queue — one thread's CRC pass over ≈1.35 MB per whole-game rollout capped the node loop at ≈2 000
+    rollouts/s (the stager waited 15 ms per iteration for them). Arrival order is then not the queue's order, as with
+    competing consumers anyway; the in-process broker keeps one thread (a deterministic order)."""
+
+    def __init__(self, fetch, depth: int, threads: int = 1):
         import queue
         import threading
         self._queue_mod = queue
@@ -989,9 +997,13 @@ class _RolloutPrefetcher:
         self.fetch = fetch
         self.err: Optional[BaseException] = None
         self.lost = 0
+        self._lost_lock = threading.Lock()
         self.stop = threading.Event()
-        self.th = threading.Thread(target=self._run, name='xp-prefetch', daemon=True)
-        self.th.start()
+        self.threads = [threading.Thread(target=self._run, name=f'xp-prefetch-{i}', daemon=True)
+                        for i in range(max(1, int(threads)))]
+        self.th = self.threads[0]
+        for t in self.threads:
+            t.start()
 
     def _run(self):
         try:
@@ -1005,7 +1017,8 @@ class _RolloutPrefetcher:
                         break
                     except self._queue_mod.Full:
                         if self.stop.is_set():
-                            self.lost += 1
+                            with self._lost_lock:
+                                self.lost += 1
                             _release(r)
                             return
         except BaseException as e:       # surfaced on the consumer's thread
@@ -1018,7 +1031,7 @@ class _RolloutPrefetcher:
             except self._queue_mod.Empty:
                 if self.err is not None:
                     raise self.err
-                if not self.th.is_alive():
+                if not any(t.is_alive() for t in self.threads):
                     raise RuntimeError('experience prefetch thread exited')
 
     def get_until(self, stop) -> Optional[Rollout]:
@@ -1029,15 +1042,16 @@ class _RolloutPrefetcher:
             except self._queue_mod.Empty:
                 if self.err is not None:
                     raise self.err
-                if not self.th.is_alive():
+                if not any(t.is_alive() for t in self.threads):
                     raise RuntimeError('experience prefetch thread exited')
         return None
 
     def close(self) -> int:
         """Stop and join the thread (it polls the queue in bounded slices); returns the decoded rollouts dropped."""
         self.stop.set()
-        self.th.join(timeout=30.0)
-        if self.th.is_alive():
+        for t in self.threads:
+            t.join(timeout=30.0)
+        if any(t.is_alive() for t in self.threads):
             raise RuntimeError('experience prefetch thread did not stop')
         n = self.lost
         while True:

@@ -59,7 +59,10 @@ __device__ __forceinline__ void head_lsm(float logit, bool m, int lane, int W, f
   float s = dca::wave_sum(e);
   if (!(s > 0.f)) s = 1.f;
   logp = logit - mx - xlog<PRECISE>(s);
-  p = (in && m) ? xexp<PRECISE>(logp) : 0.f;
+  // PRECISE: p = e / s (each entry's own rounding) instead of exp(logp), which carries the rounding of log(s) into
+  // every entry of the row alike — a row-coherent error that the pointer head's ∂q sums (Σ_u ∂t_u · E1_u over 64
+  // units, then over 11 200 rows that cancel ≈20×) turned into 1e-5 on its bias gradient (scripts/diag_5v5_head.py)
+  p = (in && m) ? (PRECISE ? e / s : xexp<PRECISE>(logp)) : 0.f;
 }
 
 template <bool F32, bool PRECISE>
