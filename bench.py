@@ -392,6 +392,17 @@ def main():
             mine.update(steps_per_s=rt['steps_per_s'], runtime=rt)
         except Exception as e:  # the learner metric stands on its own
             mine['runtime_error'] = repr(e)
+        if not cfg.entity_attention:
+            if world > 1:
+                dist.barrier()
+            try:
+                # the same runtime with the IEEE-fp32 policy step (the reference actor's precision: log-probs within
+                # 1e-5 of the torch fp32 policy, PPO ratio 1 ± 1e-7 at weight age 0)
+                rt = measure_vec_actor(policy, device, n_games=args.actor_games, threads=args.actor_threads,
+                                       precision='fp32')
+                mine.update(steps_per_s_fp32=rt['steps_per_s'])
+            except Exception as e:
+                mine['runtime_fp32_error'] = repr(e)
         if world > 1:
             dist.barrier()
         try:
@@ -435,7 +446,7 @@ def main():
         ranks = gather(mine)
         progress('actor measurements done')
         actor = dict(ranks[0])
-        for k in ('steps_per_s', 'protobuf_runtime_steps_per_s', 'policy_step_per_s',
+        for k in ('steps_per_s', 'steps_per_s_fp32', 'protobuf_runtime_steps_per_s', 'policy_step_per_s',
                   'policy_step_protobuf_featurize_per_s', 'policy_step_fp8_per_s',
                   'policy_step_fp8_protobuf_featurize_per_s', 'policy_step_fp32_per_s',
                   'policy_step_fp32_protobuf_featurize_per_s'):

@@ -277,9 +277,10 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
 
     world, rank = pdist.get_world_size(), pdist.get_rank()
     local_world = int(os.environ.get('LOCAL_WORLD_SIZE', world))
-    # (the recurrence's hand-off timeout is wall-clock per wait — ops/csrc/lstm_team.hip spin_fail — so the actor
-    # process's kernels slowing it down beside the learner no longer accumulate towards it; the one config-5 timeout
-    # of round 4 was that cumulative poll count, not a lost hand-off)
+    # the recurrence's hand-off timeout (ops/csrc/lstm_team.hip spin_fail) is wall clock per wait: 2 s for a GPU of
+    # its own, 60 s here, where the actor process shares the GPU (its kernels time-slice against the persistent team
+    # kernel; round 5 saw one 2 s expiry in the config-5 loop beside the fp8 actor). A lost hand-off still errors.
+    os.environ.setdefault('DCA_TEAM_PATIENT', '1')
     if transport == 'auto':
         from .. import native
         transport = 'shm' if (local_world == world and native.AVAILABLE) else 'tcp'
@@ -377,8 +378,11 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
         d0 = dropped_total()
         say('e2e: learner loop')
         try:
+            s0 = opt.ingest_stats()
             rows, wall, (actor_steps, _) = _learner_loop(opt, duration, warmup_iterations, max_iterations,
                                                          counters=lambda: (steps.value, 0), check=check, agree=agree)
+            s1 = opt.ingest_stats()
+            ingest_diag = {k: s1[k] - s0[k] for k in s1}
         finally:
             opt.close()
             opt.flush_checkpoints()
@@ -413,6 +417,7 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
         raise err
     mine = _summary(rows, wall, actor_steps, queue_dropped, games, dict(seq_per_epoch=seq_per_epoch, seq_len=seq_len))
     mine['actor_idle_steps_per_s'] = idle
+    mine['ingest_decode'] = ingest_diag          # decode threads over the window (claims, waits, decode seconds)
     mine['actor_gpu_busy_steps_per_s'] = gpu_busy
     mine['report'] = extra
     per_rank = [mine]

@@ -315,12 +315,16 @@ class DotaOptimizer:
             t0 = time.monotonic()
             while cb.available():
                 got = None
+                tw = time.perf_counter()
                 while got is None:
                     if stop.is_set():
                         return None
                     if self.cfg.xp_timeout is not None and time.monotonic() - t0 > self.cfg.xp_timeout:
                         raise TimeoutError('no experience received')
                     got = broker.claim_experience(timeout=0.25)
+                td = time.perf_counter()
+                st = self.__dict__.setdefault('_claim_stats', [0, 0.0, 0.0])   # messages, claim wait s, decode s
+                st[1] += td - tw
                 view, token = got
                 n = cb.take(view.nbytes)
                 released = [False]
@@ -338,6 +342,8 @@ class DotaOptimizer:
                     logger.warning('dropping corrupted experience message (%s); %d so far', e, self.corrupt_rollouts)
                     continue
                 r.release = rel
+                st[0] += 1
+                st[2] += time.perf_counter() - td
                 return r
         checked = getattr(broker, 'consume_experience_checked', None)    # shm ring: CRC verified during the copy
         consume = checked or getattr(broker, 'consume_experience_view', None) or broker.consume_experience
@@ -426,6 +432,14 @@ class DotaOptimizer:
         device (:mod:`learner.ingest`), then the return / GAE scan. The pipelined form runs the staging on the
         stager thread one iteration ahead (``prefetch_rollouts`` > 0 on a GPU learner)."""
         return self._finish_ingest(self._ingest_pipeline(thread=False).stage(rollouts), n_keep)
+
+    def ingest_stats(self) -> Dict[str, float]:
+        """Decode-side counters of the zero-copy path (node-loop diagnostics): messages claimed, total seconds the
+        decode threads waited in the ring's claim and spent decoding (CRC + header), and waited on the full queue."""
+        st = self.__dict__.get('_claim_stats', [0, 0.0, 0.0])
+        pf = getattr(self, '_prefetcher', None)
+        return {'claimed': int(st[0]), 'claim_wait_s': float(st[1]), 'decode_s': float(st[2]),
+                'queue_put_wait_s': float(pf.put_wait) if pf is not None else float('nan')}
 
     def _ingest_pipeline(self, thread: bool):
         pl = getattr(self, '_pipeline', None)
@@ -997,6 +1011,7 @@ class _RolloutPrefetcher:
         self.fetch = fetch
         self.err: Optional[BaseException] = None
         self.lost = 0
+        self.put_wait = 0.0                 # s the decode threads waited for room in the queue (stager behind)
         self._lost_lock = threading.Lock()
         self.stop = threading.Event()
         self.threads = [threading.Thread(target=self._run, name=f'xp-prefetch-{i}', daemon=True)
@@ -1011,9 +1026,11 @@ class _RolloutPrefetcher:
                 r = self.fetch(self.stop)
                 if r is None:
                     break
+                tp = time.perf_counter()
                 while True:
                     try:
                         self.q.put(r, timeout=0.1)
+                        self.put_wait += time.perf_counter() - tp
                         break
                     except self._queue_mod.Full:
                         if self.stop.is_set():

@@ -1,0 +1,5 @@
+# round 5 (m): node loop diagnostics (decode-thread waits) + config 5 with the patient hand-off
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 400 python -u bench.py --steps 10 --warmup 3 --bf16x3-extra 0 --model-5v5-extra 0 --model-5v5-exact-extra 0 --bptt350-extra 0 --big-batch-extra 0 --actor 0 --e2e 20 --league-replay-extra 15 --e2e-5v5-extra 0 > gpurun_out/r5_e2e_diag.json 2> gpurun_out/r5_e2e_diag.err
+echo "e2e rc=$?"
