@@ -266,9 +266,8 @@ class DotaOptimizer:
                 # (queue size, model publish) must not wait behind the thread's long polls
                 mk = getattr(self.broker, 'consumer', None)
                 self._xp_broker = mk() if mk is not None else self.broker
-                zc = hasattr(self._xp_broker, 'claim_experience')       # the node's shm ring: zero-copy, parallel CRC
-                pf = self._prefetcher = _RolloutPrefetcher(lambda stop: self._consume_decode(stop, claim=True),
-                                                           self.cfg.prefetch_rollouts, threads=3 if zc else 1)
+                # (copying consumption here: nothing stages these rollouts, so ring claims would never be released)
+                pf = self._prefetcher = _RolloutPrefetcher(self._consume_decode, self.cfg.prefetch_rollouts)
                 self.prefetch_dropped = 0
             return pf.get()
         return self._consume_decode()
@@ -453,8 +452,11 @@ class DotaOptimizer:
                 mk = getattr(self.broker, 'consumer', None)
                 self._xp_broker = mk() if mk is not None else self.broker
                 # consume + decode (CRC with the GIL released) on a thread of their own, so the stager packs and
-                # uploads iteration k+1 while the rollouts of k+2 are being decoded
-                pf = self._prefetcher = _RolloutPrefetcher(self._consume_decode, self.cfg.prefetch_rollouts)
+                # uploads iteration k+1 while the rollouts of k+2 are being decoded; on the node's shm ring zero-copy
+                # (claimed regions, released once staged — IngestPipeline.stage) with three decode threads
+                zc = hasattr(self._xp_broker, 'claim_experience')
+                pf = self._prefetcher = _RolloutPrefetcher(lambda stop: self._consume_decode(stop, claim=zc),
+                                                           self.cfg.prefetch_rollouts, threads=3 if zc else 1)
                 fetch = pf.get_until
             pl = self._pipeline = IngestPipeline(fetch, self.cfg.seq_len, self.cfg.seq_per_epoch, self.cfg.algo, H,
                                                  self.device, pack=self.cfg.pack_sequences)
