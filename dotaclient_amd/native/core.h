@@ -301,7 +301,7 @@ int featurize_one(const World& w, int player_id, int team_id, const int* counts,
 // second each way the lock was held most of the time, and two dedicated threads moved 2 850 messages/s.) Each message
 // is a u64 word + the payload padded to 8 bytes; the word holds the state in its top byte and the length below
 // (~0 marks "wrap to the start"). Regions are reclaimed oldest-first once their consumer is done (free_off), so
-// the producers' space limit is free_off, not head.
+// the producers' space limit is free_off, not head; drop_oldest drops only what it can reclaim.
 // ============================================================================================================
 struct RingHeader {
   uint64_t magic;
@@ -559,9 +559,14 @@ class RingCore {
       hdr_->free_off += padded(w & kLenMask);
     }
   }
-  // drop_oldest: discard the oldest committed message (not one still being written)
+  // drop_oldest: discard the oldest committed message (not one still being written) — only when that frees space:
+  // with an older message still claimed (zero-copy consumers hold regions for a whole staging pass) the dropped
+  // region could not be reclaimed, and a full ring would drop every new message while the consumer, short of one
+  // more rollout to finish its batch, waits forever. The producer then waits for the release instead.
   bool drop_head_locked() {
     if (hdr_->count == 0) return false;
+    reclaim_locked();
+    if (hdr_->free_off != hdr_->head) return false;
     uint64_t off = hdr_->head;
     const uint64_t pos = resolve(off);
     const uint64_t w = word_at(pos);

@@ -186,3 +186,61 @@ def test_fused_packed_sequence_matches_padded_on_gpu(gpu_ops, precision):
     for n, g in g_pad.items():
         rel = ((g_pack[n] - g).norm() / g.norm().clamp_min(1e-12)).item()
         assert rel < (1e-5 if precision == 'fp32-exact' else 1e-3), (n, rel)
+
+
+def test_zero_copy_stager_keeps_up_with_a_faster_drop_oldest_producer():
+    """The node loop's consumption under overload: a producer publishing into the drop_oldest ring faster than the
+    stager takes rollouts, three claiming decode threads, packed staging. A consumer that holds claimed regions for a
+    whole gather pins the ring's reclaim point; the ring used to keep dropping every new message behind it (space it
+    could never reclaim) until the stager, one rollout short of its batch, waited forever (native/core.h
+    drop_head_locked now drops only what it can reclaim and otherwise lets the producer wait)."""
+    import threading
+    import time
+    import uuid
+    from dotaclient_amd import native
+    from dotaclient_amd.learner.optimizer import DotaOptimizer, OptimizerConfig, _RolloutPrefetcher
+    from dotaclient_amd.transport.codec import encode
+    from dotaclient_amd.transport.shm import ShmBroker
+    if not native.AVAILABLE:
+        pytest.skip('native module not built')
+    S = 256
+    rng = np.random.default_rng(0)
+    msgs = [encode(_rollout(int(T), i)) for i, T in enumerate(rng.integers(50, 400, 32))]
+    b = ShmBroker(f'dca_zf_{uuid.uuid4().hex[:8]}', capacity=1 << 26, create=True, drop_oldest=True)
+    stop = threading.Event()
+    err = []
+
+    def produce():
+        i = 0
+        try:
+            while not stop.is_set():
+                b.publish_experience(msgs[i % len(msgs)], timeout=5.0)
+                i += 1
+        except BaseException as e:
+            if not stop.is_set():       # (at the end: the closed consumer no longer releases space)
+                err.append(e)
+    th = threading.Thread(target=produce, daemon=True)
+    th.start()
+    cfg = OptimizerConfig(log_dir='', model='lstm128', seq_len=S, seq_per_epoch=8, batch_size=8,
+                          pack_sequences=True, run_local=True)
+    opt = DotaOptimizer.__new__(DotaOptimizer)
+    opt.cfg, opt.broker, opt.corrupt_rollouts, opt._xp_broker = cfg, b, 0, b
+    pf = _RolloutPrefetcher(lambda s: opt._consume_decode(s, claim=True), 32, threads=3)
+    pl = IngestPipeline(pf.get_until, S, 8, 'ppo', 128, 'cpu', pack=True)
+    n, t0 = 0, time.monotonic()
+    try:
+        while n < 150 and time.monotonic() - t0 < 30.0:
+            st = pl.get()
+            pl.expand(st, {})
+            n += 1
+    finally:
+        stop.set()
+        th.join(10.0)
+        pl.close()
+        pf.close()
+    try:
+        assert not err, err
+        assert n == 150
+        assert opt._claim_budget.held == 0 and opt.ingest_stats()['claimed'] > 0
+    finally:
+        b.close(unlink=True)
