@@ -123,7 +123,9 @@ def _learner_loop(opt, duration, warmup_iterations, max_iterations, counters, ch
                      m.get('time/h2d', float('nan')), m.get('time/log', float('nan')),
                      m.get('time/publish', float('nan')), m.get('time/lookahead', 0.0),
                      m.get('time/gpu_train_ms_per_step', float('nan')), m.get('rollouts_consumed', float('nan')),
-                     m.get('time/stage', float('nan')), m.get('time/gather', float('nan'))))
+                     m.get('time/stage', float('nan')), m.get('time/gather', float('nan')),
+                     m.get('time/stage_wait', float('nan')), m.get('time/stage_copy', float('nan')),
+                     m.get('time/stage_release', float('nan'))))
         e = check()
         if e:
             raise e
@@ -161,6 +163,10 @@ def _summary(rows, wall, actor_steps, dropped, games, config):
         # the stager thread per iteration: packing + upload issue, and waiting for the decoded rollouts
         'stage_ms_per_iteration': 1e3 * float(np.nanmean(a[:, 12])) if n_it and np.isfinite(a[:, 12]).any() else float('nan'),
         'gather_ms_per_iteration': 1e3 * float(np.nanmean(a[:, 13])) if n_it and np.isfinite(a[:, 13]).any() else float('nan'),
+        # part of stage_ms spent waiting for a free upload slot (the stager ahead of the learner)
+        'stage_wait_ms_per_iteration': 1e3 * float(np.nanmean(a[:, 14])) if n_it and np.isfinite(a[:, 14]).any() else float('nan'),
+        'stage_copy_ms_per_iteration': 1e3 * float(np.nanmean(a[:, 15])) if n_it and np.isfinite(a[:, 15]).any() else float('nan'),
+        'stage_release_ms_per_iteration': 1e3 * float(np.nanmean(a[:, 16])) if n_it and np.isfinite(a[:, 16]).any() else float('nan'),
         'actor_steps_per_s': actor_steps / wall,
         'queue_dropped': int(dropped), 'games': games, 'config': config,
     }
@@ -281,6 +287,10 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
     # its own, 60 s here, where the actor process shares the GPU (its kernels time-slice against the persistent team
     # kernel; round 5 saw one 2 s expiry in the config-5 loop beside the fp8 actor). A lost hand-off still errors.
     os.environ.setdefault('DCA_TEAM_PATIENT', '1')
+    if os.environ.get('DCA_SWITCH_INTERVAL'):
+        # the learner process's GIL hand-off interval (the stager, decode and main threads share one interpreter)
+        import sys
+        sys.setswitchinterval(float(os.environ['DCA_SWITCH_INTERVAL']))
     if transport == 'auto':
         from .. import native
         transport = 'shm' if (local_world == world and native.AVAILABLE) else 'tcp'

@@ -26,7 +26,7 @@ import itertools
 import os
 import threading
 from dataclasses import dataclass
-from typing import Dict, Optional
+from typing import Dict, List, Optional
 
 import torch
 
@@ -426,6 +426,18 @@ class Learner:
             raise RuntimeError(f'persistent kernel error on a data-parallel rank (own code {own}): the step was '
                                'skipped by every rank\'s Adam')
         self.model.check_error()
+
+    def error_flags(self) -> List[torch.Tensor]:
+        """The device flags :meth:`check_error` reads (non-finite step, sticky DP error, recurrence error), for a
+        caller that snapshots them asynchronously with its other per-iteration values: when the snapshot shows one
+        non-zero it calls :meth:`check_error`, whose host syncs then only happen on the failure path."""
+        flags = [self.opt.nonfinite]
+        if self.backend == 'fused':
+            sticky = getattr(self, '_err_any', None)
+            if sticky is not None:
+                flags.append(sticky)
+            flags.append(self.model.err)
+        return flags
 
     def _finish(self, vec):
         metrics = self._metrics_from_vec(vec.clone())

@@ -128,6 +128,9 @@ class StagedIteration:
     slot: int = 0
     stage_s: float = 0.0                    # host packing + upload issue time (stager thread)
     gather_s: float = 0.0                   # stager time waiting for the iteration's decoded rollouts
+    wait_s: float = 0.0                     # part of stage_s spent waiting for a free slot (the learner behind)
+    copy_s: float = 0.0                     # part of stage_s in the field copies into the pinned slot
+    release_s: float = 0.0                  # part of stage_s giving ring-resident rollouts back
 
 
 class _Slot:
@@ -268,12 +271,14 @@ class IngestPipeline:
             nbytes += _round(L)
         slot_i = self._k % 2
         slot = self.slots[slot_i]
+        tw = time.perf_counter()
         while not slot.free.acquire(timeout=0.1):      # the learner has not expanded this slot's last contents yet
             if self.stop.is_set():
                 raise _Stopped()
         self._k += 1
         if slot.uploaded is not None:
             slot.uploaded.synchronize()               # the slot's previous upload has left the pinned buffer
+        tw = time.perf_counter() - tw
         if slot.host is None or slot.host.numel() < nbytes:
             cap = max(nbytes, 2 * (slot.host.numel() if slot.host is not None else 0), 1 << 20)
             if slot.consumed is not None:
@@ -317,8 +322,10 @@ class IngestPipeline:
                     dst[...] = src
             np.copyto(views_h['rewards'][sl], r.rewards, casting='same_kind')
             pos += T
+        tc = time.perf_counter()
         if jobs:
             _native_copy(np.asarray(jobs, dtype=np.int64), 4)
+        tc = time.perf_counter() - tc
         if self.H:
             hid = hview(hid_off, n_seq * 2 * self.H * 4, 'float32', (n_seq, 2, self.H))
             for i, src in enumerate(seq_src):
@@ -337,8 +344,10 @@ class IngestPipeline:
             rv[resets] = 1
         # ring-resident rollouts (zero-copy consumption, learner/optimizer.py): everything the upload needs is in the
         # pinned slot now — give their ring regions back (the canvas of the last one is kept for the logs)
+        tr = time.perf_counter()
         for i, r in enumerate(rollouts):
             r.detach_shared(keep_canvas=i == len(rollouts) - 1)
+        tr = time.perf_counter() - tr
         ev = None
         if self.cuda:
             # blocking events: the stager waits on them (slot reuse) for up to an iteration, and a spinning wait
@@ -359,7 +368,8 @@ class IngestPipeline:
         if self.pack:
             views['reset'] = slot.dev[rst_off:rst_off + L]
         return StagedIteration(rollouts=rollouts, lens=lens, off=off, n_seq=n_seq, L=L, Lv=Lv, gae_mode=gae_mode,
-                               views=views, ready=ev, slot=slot_i, stage_s=time.perf_counter() - t0)
+                               views=views, ready=ev, slot=slot_i, stage_s=time.perf_counter() - t0, wait_s=tw,
+                               copy_s=tc, release_s=tr)
 
     # ---- learner thread ----------------------------------------------------------------------------
     def get(self) -> StagedIteration:

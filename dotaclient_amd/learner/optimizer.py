@@ -455,8 +455,9 @@ class DotaOptimizer:
                 # uploads iteration k+1 while the rollouts of k+2 are being decoded; on the node's shm ring zero-copy
                 # (claimed regions, released once staged — IngestPipeline.stage) with three decode threads
                 zc = hasattr(self._xp_broker, 'claim_experience')
+                nth = int(os.environ.get('DCA_DECODE_THREADS', '0')) or 1
                 pf = self._prefetcher = _RolloutPrefetcher(lambda stop: self._consume_decode(stop, claim=zc),
-                                                           self.cfg.prefetch_rollouts, threads=3 if zc else 1)
+                                                           self.cfg.prefetch_rollouts, threads=nth if zc else 1)
                 fetch = pf.get_until
             pl = self._pipeline = IngestPipeline(fetch, self.cfg.seq_len, self.cfg.seq_per_epoch, self.cfg.algo, H,
                                                  self.device, pack=self.cfg.pack_sequences)
@@ -731,6 +732,9 @@ class DotaOptimizer:
             st2 = self._ingest_pipeline(thread=True).get()
             self.timer.add('stage', st2.stage_s)
             self.timer.add('gather', st2.gather_s)
+            self.timer.add('stage_wait', st2.wait_s)
+            self.timer.add('stage_copy', st2.copy_s)
+            self.timer.add('stage_release', st2.release_s)
             if self.consumed is not None:
                 self.consumed.extend((r.game_id, int(r.team_id), int(r.player_id), int(r.weight_version), r.length)
                                      for r in st2.rollouts)
@@ -739,7 +743,9 @@ class DotaOptimizer:
             self.timer.stop('lookahead')
             self.timer.start('train')
         done = None
+        host = None
         if cuda:
+            host = self._host_snapshot(losses, metrics_acc, ema_snap) if defer else None
             # a blocking-sync event: the host thread sleeps until the GPU is done instead of spinning a core that
             # the node's actor threads (same CPU share) can use
             done = torch.cuda.Event(blocking=True)
@@ -747,7 +753,7 @@ class DotaOptimizer:
         pending = dict(it=it, losses=losses, metrics_acc=metrics_acc, ema_snap=ema_snap, n_seq=n_seq,
                        subrewards=subrewards, rollout_lens=rollout_lens, weight_ages=weight_ages, canvas=canvas,
                        done=done, ev=(ev_t0, ev_t1), n_train=len(losses), published=published,
-                       n_rollouts=len(rollouts))
+                       n_rollouts=len(rollouts), host=host)
         self.timer.stop('train')
         if defer:
             # one-iteration-deferred metrics: this iteration's steps stay queued on the GPU while the host finalises
@@ -757,6 +763,37 @@ class DotaOptimizer:
                 self._finalize_iteration(prev)
         else:
             self._finalize_iteration(pending)
+
+    def _host_snapshot(self, losses, metrics_acc, ema_snap):
+        """Everything :meth:`_finalize_iteration` reads from the device — the losses, every metric's iteration mean, the
+        reward-EMA snapshot and the learner's error flags — packed into ONE vector and copied into pinned host memory
+        behind this iteration's steps (no host sync). Finalising the previous iteration with ``.cpu()`` / ``.item()``
+        reads instead queued those copies behind the CURRENT iteration's steps and made the host wait for the GPU to
+        drain before it could enqueue the next iteration: a GPU bubble of host time per iteration in the node loop."""
+        if not losses or not all(torch.is_tensor(x) and x.is_cuda for x in losses):
+            return None
+        keys = list(metrics_acc)
+        parts = [torch.stack(losses).float().reshape(-1),
+                 torch.stack([torch.stack(metrics_acc[k]).float().mean() for k in keys])]
+        n_ema = 0
+        if ema_snap is not None:
+            parts.append(ema_snap.float().reshape(-1))
+            n_ema = ema_snap.numel()
+        flags = [f.float().reshape(-1)[:1] for f in self.learner.error_flags()]
+        parts += flags
+        vec = torch.cat(parts)
+        buf = self.__dict__.setdefault('_host_bufs', [])
+        # two pinned buffers alternate (the previous iteration's is read while this one's copy is in flight)
+        while len(buf) < 2:
+            buf.append(torch.empty(0, dtype=torch.float32).pin_memory())
+        i = self.__dict__.get('_host_buf_i', 0)
+        self._host_buf_i = 1 - i
+        if buf[i].numel() < vec.numel():
+            buf[i] = torch.empty(max(vec.numel(), 2 * buf[i].numel()), dtype=torch.float32).pin_memory()
+        h = buf[i][:vec.numel()]
+        h.copy_(vec, non_blocking=True)
+        return dict(vec=h, n_loss=len(losses), keys=keys, n_ema=n_ema,
+                    ema_shape=tuple(ema_snap.shape) if ema_snap is not None else None, n_flags=len(flags))
 
     def _defer_metrics(self) -> bool:
         return self._pipelined() and self.cfg.defer_metrics and self.cfg.async_checkpoint
@@ -775,15 +812,26 @@ class DotaOptimizer:
         it = p['it']
         if p['done'] is not None:
             p['done'].synchronize()
-        loss_t = torch.stack(p['losses']).float().cpu()
+        hs = p.get('host')
+        if hs is not None:
+            # the pinned snapshot of the device values (_host_snapshot): complete once ``done`` is, no further syncs
+            v = hs['vec'].clone()
+            nl, nk, ne = hs['n_loss'], len(hs['keys']), hs['n_ema']
+            loss_t = v[:nl]
+            means = v[nl:nl + nk].tolist()
+            ema_host = v[nl + nk:nl + nk + ne].view(hs['ema_shape']) if ne else None
+            flags = v[nl + nk + ne:]
+        else:
+            loss_t = torch.stack(p['losses']).float().cpu()
         if faults().nan_loss(it):
             loss_t[0] = float('nan')
         if torch.isnan(loss_t).any():
             raise ValueError(f'NaN loss at iteration {it}: {loss_t.tolist()}')
-        self.learner.check_error()
+        if hs is None or bool((flags != 0).any()):
+            self.learner.check_error()          # (the snapshot path: host syncs only when a flag is up)
         n_steps = p['n_seq'] * cfg.seq_len
         if self.ingest == 'device':
-            self._sync_running(p['ema_snap'])
+            self._sync_running(ema_host if (hs is not None and ema_host is not None) else p['ema_snap'])
         now = time.time()
         steps_per_s = n_steps / max(now - self.time_last_step, 1e-9)
         self.time_last_step = now
@@ -792,8 +840,11 @@ class DotaOptimizer:
         reward_dict = dict(zip(REWARD_KEYS, sub.sum(axis=0)))
         # every metric's iteration mean in ONE device→host copy (not one synchronising .item() per metric)
         metrics_acc = p['metrics_acc']
-        keys = list(metrics_acc)
-        means = torch.stack([torch.stack(metrics_acc[k]).float().mean() for k in keys]).cpu().tolist()
+        if hs is not None:
+            keys = hs['keys']
+        else:
+            keys = list(metrics_acc)
+            means = torch.stack([torch.stack(metrics_acc[k]).float().mean() for k in keys]).cpu().tolist()
         mean = dict(zip(keys, means))
         rollout_lens, weight_ages = p['rollout_lens'], p['weight_ages']
         metrics = {
