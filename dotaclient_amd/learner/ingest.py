@@ -27,6 +27,7 @@ packed like any other. The return / GAE scan segments are the rollouts in row or
 """
 from __future__ import annotations
 
+import os
 import queue
 import threading
 import time
@@ -39,6 +40,9 @@ import torch
 from ..transport.codec import Rollout
 
 _ALIGN = 64
+
+
+_STAGE_PROF = os.environ.get('DCA_STAGE_PROF') == '1'
 
 
 def _round(n: int) -> int:
@@ -54,6 +58,17 @@ def _load_native_copy():
 
 
 _native_copy = _load_native_copy()
+
+
+def _load_native_pack():
+    try:
+        from ..native import _native
+        return _native.pack_rows
+    except (ImportError, AttributeError):
+        return None
+
+
+_native_pack = _load_native_pack()
 
 
 def _release_all(rollouts):
@@ -233,6 +248,11 @@ class IngestPipeline:
         """Pack the valid rows of every field into the next pinned slot and issue its upload (any thread)."""
         t0 = time.perf_counter()
         S = self.S
+        marks = self._marks = [('start', t0, time.thread_time())] if _STAGE_PROF else None
+
+        def mk(label):
+            if marks is not None:
+                marks.append((label, time.perf_counter(), time.thread_time()))
         pk = SequencePacker(S, self.pack)
         for r in rollouts:
             pk.add(r)
@@ -269,6 +289,7 @@ class IngestPipeline:
         if self.pack:
             rst_off = nbytes                     # (L,) u8 episode-start flags in the padded layout
             nbytes += _round(L)
+        mk('pack')
         slot_i = self._k % 2
         slot = self.slots[slot_i]
         tw = time.perf_counter()
@@ -298,17 +319,36 @@ class IngestPipeline:
                     slot.dev = slot.host
             slot.consumed = None
         hb = slot.host.numpy()
+        mk('slot')
 
         def hview(o, n, dt, shape):
             return hb[o:o + n].view(np.dtype(str(dt).replace('torch.', ''))).reshape(shape)
         views_h = {name: hview(o, n, dt, (Lv,) + tail) for name, dt, tail, o, n in layout}
         pos = 0
         rows = views_h['rows']
-        # the same-dtype fields (≈97 % of the bytes: units, env, actions, masks, logp, values) go to the native
-        # parallel copy as one job list, GIL released; rows, the f64 → f32 rewards and missing fields stay numpy
         jobs = []
         direct = ('env', 'units', 'actions', 'masks', 'logp') + (('values',) if gae_mode else ())
-        for r, T, a in zip(rollouts, lens, off[:-1]):
+        tc = 0.0
+        if _native_pack is not None:
+            # every field of every rollout in ONE native call (memcpy / f64 → f32 rewards / zero fill, GIL released);
+            # the rows (padded-layout index of every valid row) vectorised
+            vpos = np.zeros(len(rollouts) + 1, np.int64)
+            np.cumsum(lens, out=vpos[1:])
+            rows[:] = np.arange(Lv, dtype=np.int64) + np.repeat(off[:-1] - vpos[:-1], lens)
+            mk('loop')
+            tc = time.perf_counter()
+            try:
+                _native_pack([(views_h[name], [getattr(r, name) for r in rollouts])
+                              for name in direct + ('rewards',)], vpos, 4)
+                rollouts_loop = ()
+            except ValueError:          # a field of another dtype (e.g. a reference agent's pickle): numpy converts
+                rollouts_loop = zip(rollouts, lens, off[:-1])
+            tc = time.perf_counter() - tc
+        else:
+            rollouts_loop = zip(rollouts, lens, off[:-1])
+        # fallback without the native module: the same-dtype fields go to the native parallel copy as one job list
+        # when that exists, rows, the f64 → f32 rewards and missing fields stay numpy
+        for r, T, a in rollouts_loop:
             sl = slice(pos, pos + T)
             rows[sl] = np.arange(a, a + T)
             for name in direct:
@@ -322,10 +362,12 @@ class IngestPipeline:
                     dst[...] = src
             np.copyto(views_h['rewards'][sl], r.rewards, casting='same_kind')
             pos += T
-        tc = time.perf_counter()
         if jobs:
+            mk('loop')
+            tc = time.perf_counter()
             _native_copy(np.asarray(jobs, dtype=np.int64), 4)
-        tc = time.perf_counter() - tc
+            tc = time.perf_counter() - tc
+        mk('copy')
         if self.H:
             hid = hview(hid_off, n_seq * 2 * self.H * 4, 'float32', (n_seq, 2, self.H))
             for i, src in enumerate(seq_src):
@@ -344,10 +386,12 @@ class IngestPipeline:
             rv[resets] = 1
         # ring-resident rollouts (zero-copy consumption, learner/optimizer.py): everything the upload needs is in the
         # pinned slot now — give their ring regions back (the canvas of the last one is kept for the logs)
+        mk('hid+reset')
         tr = time.perf_counter()
         for i, r in enumerate(rollouts):
             r.detach_shared(keep_canvas=i == len(rollouts) - 1)
         tr = time.perf_counter() - tr
+        mk('release')
         ev = None
         if self.cuda:
             # blocking events: the stager waits on them (slot reuse) for up to an iteration, and a spinning wait
@@ -359,6 +403,7 @@ class IngestPipeline:
                 slot.dev[:nbytes].copy_(slot.host[:nbytes], non_blocking=True)
                 ev.record(self.copy_stream)
         slot.uploaded = ev
+        mk('upload')
         views = {}
         for name, dt, tail, o, n in layout:
             views[name] = slot.dev[o:o + n].view(dt).view((Lv,) + tail)
@@ -367,9 +412,28 @@ class IngestPipeline:
                                                                                                        self.H)
         if self.pack:
             views['reset'] = slot.dev[rst_off:rst_off + L]
+        mk('views')
+        self._prof_done()
         return StagedIteration(rollouts=rollouts, lens=lens, off=off, n_seq=n_seq, L=L, Lv=Lv, gae_mode=gae_mode,
                                views=views, ready=ev, slot=slot_i, stage_s=time.perf_counter() - t0, wait_s=tw,
                                copy_s=tc, release_s=tr)
+
+    def _prof_done(self):
+        """DCA_STAGE_PROF=1: accumulate the stage() sections and print their means every 200 iterations (stderr)."""
+        m = getattr(self, '_marks', None)
+        if not m:
+            return
+        acc = self.__dict__.setdefault('_prof', {})
+        for (_, a, ca), (lab, b, cb) in zip(m, m[1:]):
+            w, c = acc.get(lab, (0.0, 0.0))
+            acc[lab] = (w + (b - a), c + (cb - ca))
+        self._prof_n = getattr(self, '_prof_n', 0) + 1
+        if self._prof_n % 100 == 0:
+            import sys
+            n = self._prof_n
+            print('[stage prof] ms/iteration wall/cpu ' + ' '.join(f'{k}={1e3 * w / n:.2f}/{1e3 * c / n:.2f}'
+                                                                for k, (w, c) in acc.items()),
+                  file=sys.stderr, flush=True)
 
     # ---- learner thread ----------------------------------------------------------------------------
     def get(self) -> StagedIteration:

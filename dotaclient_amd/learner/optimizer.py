@@ -887,7 +887,9 @@ class DotaOptimizer:
             qs = getattr(self.broker, 'xp_queue_size', None)
             job = (self._write_logs, it, metrics, loss_t.numpy(), np.asarray(rollout_lens), np.asarray(weight_ages),
                    rollout_rewards, hist, p['canvas'], qs)
-            if cfg.async_checkpoint and self.device.type == 'cuda':
+            if os.environ.get('DCA_DIAG_SKIP_FILES') == '1':
+                pass                                  # (diagnostics: no event files — isolates the writer's GIL use)
+            elif cfg.async_checkpoint and self.device.type == 'cuda':
                 self._submit_background(*job)         # tensorboard events + their upload on the ordered writer
             else:
                 job[0](*job[1:])
@@ -1014,6 +1016,8 @@ class DotaOptimizer:
         self._write_checkpoint(data, trainer, version)
 
     def _write_checkpoint(self, data: bytes, trainer, version: int):
+        if os.environ.get('DCA_DIAG_SKIP_FILES') == '1':
+            return
         path = ckpt.write_model_bytes(data, self.cfg.log_dir, version)
         spath = ckpt.save_trainer_state(trainer, self.cfg.log_dir, version)
         if self.uploader is not None:   # reference optimizer.py:713-715 (GCS upload of the model file)

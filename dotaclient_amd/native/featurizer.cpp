@@ -420,6 +420,80 @@ void copy_jobs(py::array_t<int64_t, py::array::c_style> jobs, int threads) {
   for (auto& th : pool) th.join();
 }
 
+// The stager's whole field packing in one call: for every field (dst (Lv, ...) contiguous, [src_i or None]) the
+// rollouts' rows go to dst[pos[i]:pos[i+1]] — same-dtype memcpy, f64 → f32 conversion (rewards) or zero fill
+// (missing field) — split into ≤ 1 MB pieces over `threads` threads with the GIL released. Replaces a Python loop
+// over rollouts × fields (≈8 ms per 16 × 1400-step iteration on the node's busy CPU, most of it waiting for the GIL
+// the decode, writer and main threads also need).
+void pack_rows(py::list fields, py::array_t<int64_t, py::array::c_style> pos, int threads) {
+  const int64_t* p = pos.data();
+  const py::ssize_t n = pos.size() - 1;
+  if (n < 0) throw std::invalid_argument("pos must hold n + 1 offsets");
+  struct Piece { uint8_t* d; const uint8_t* s; size_t count; int kind; };   // kind 0 memcpy, 1 f64→f32, 2 zero
+  std::vector<Piece> pcs;
+  constexpr size_t kPiece = 1 << 20;
+  for (py::handle fh : fields) {
+    py::tuple f = py::reinterpret_borrow<py::tuple>(fh);
+    if (f.size() != 2) throw std::invalid_argument("fields are (dst, [src...]) pairs");
+    py::array dst = py::reinterpret_borrow<py::array>(f[0]);
+    py::list srcs = py::reinterpret_borrow<py::list>(f[1]);
+    if (!(dst.flags() & py::array::c_style) || !dst.writeable()) throw std::invalid_argument("dst must be contiguous");
+    if ((py::ssize_t)srcs.size() != n) throw std::invalid_argument("one source per rollout");
+    const py::ssize_t rows = dst.ndim() ? dst.shape(0) : 0;
+    if (rows < p[n]) throw std::invalid_argument("dst has fewer rows than the rollouts");
+    const size_t row_bytes = rows ? (size_t)dst.nbytes() / (size_t)rows : 0;
+    const size_t isz = (size_t)dst.itemsize();
+    uint8_t* dbase = static_cast<uint8_t*>(dst.mutable_data());
+    const char dk = dst.dtype().kind();
+    for (py::ssize_t i = 0; i < n; ++i) {
+      const int64_t r0 = p[i], r1 = p[i + 1];
+      if (r1 < r0 || r0 < 0) throw std::invalid_argument("pos must be non-decreasing");
+      uint8_t* d = dbase + (size_t)r0 * row_bytes;
+      const size_t bytes = (size_t)(r1 - r0) * row_bytes;
+      py::handle sh = srcs[i];
+      if (sh.is_none()) {
+        for (size_t o = 0; o < bytes; o += kPiece) pcs.push_back({d + o, nullptr, std::min(kPiece, bytes - o), 2});
+        continue;
+      }
+      py::array s = py::reinterpret_borrow<py::array>(sh);
+      if (!(s.flags() & py::array::c_style)) throw std::invalid_argument("source arrays must be C-contiguous");
+      if (s.ndim() == 0 || s.shape(0) != r1 - r0) throw std::invalid_argument("source rows != pos range");
+      const char sk = s.dtype().kind();
+      const size_t ssz = (size_t)s.itemsize();
+      const uint8_t* sp = static_cast<const uint8_t*>(s.data());
+      if (sk == dk && ssz == isz && (size_t)s.nbytes() == bytes) {
+        for (size_t o = 0; o < bytes; o += kPiece) pcs.push_back({d + o, sp + o, std::min(kPiece, bytes - o), 0});
+      } else if (dk == 'f' && isz == 4 && sk == 'f' && ssz == 8 && (size_t)s.nbytes() == 2 * bytes) {
+        const size_t elems = bytes / 4, step = kPiece / 8;
+        for (size_t e = 0; e < elems; e += step)
+          pcs.push_back({d + 4 * e, sp + 8 * e, std::min(step, elems - e), 1});
+      } else {
+        throw std::invalid_argument("source dtype / size does not match its destination field");
+      }
+    }
+  }
+  py::gil_scoped_release rel;
+  const int T = std::max(1, std::min<int>(threads, (int)pcs.size()));
+  auto work = [&](int t) {
+    for (size_t k = t; k < pcs.size(); k += T) {
+      const Piece& q = pcs[k];
+      if (q.kind == 0) {
+        std::memcpy(q.d, q.s, q.count);
+      } else if (q.kind == 2) {
+        std::memset(q.d, 0, q.count);
+      } else {
+        const double* s = reinterpret_cast<const double*>(q.s);
+        float* d = reinterpret_cast<float*>(q.d);
+        for (size_t e = 0; e < q.count; ++e) d[e] = (float)s[e];
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (int t = 1; t < T; ++t) pool.emplace_back(work, t);
+  work(0);
+  for (auto& th : pool) th.join();
+}
+
 }  // namespace
 
 // glibc malloc for the actor runtime's allocation pattern: every step appends to per-player trajectories (≈2 MB
@@ -444,6 +518,9 @@ PYBIND11_MODULE(_native, m) {
   m.def("crc32c", &crc32c);
   m.def("copy_jobs", &copy_jobs, py::arg("jobs"), py::arg("threads") = 4,
         "memcpy a (n, 3) int64 job list of (dst address, src address, bytes) on `threads` threads (GIL released)");
+  m.def("pack_rows", &pack_rows, py::arg("fields"), py::arg("pos"), py::arg("threads") = 4,
+        "pack per-rollout rows of every (dst, [src or None]) field into dst[pos[i]:pos[i+1]] (memcpy, f64->f32, "
+        "zero fill) on `threads` threads, GIL released");
   m.def("crc32c_buf", &crc32c_buf, py::arg("buf"), py::arg("n") = -1,
         "CRC-32C of the first n bytes of a contiguous buffer (GIL released)");
   py::class_<PyVecEnv>(m, "VecEnv")

@@ -246,3 +246,33 @@ def test_copy_jobs_parallel_memcpy():
     native.copy_jobs(np.asarray(jobs, np.int64), 3)
     np.testing.assert_array_equal(dst[:o], np.concatenate(srcs))
     assert not dst[o:].any()
+
+
+def test_pack_rows_copies_converts_and_zero_fills():
+    """native.pack_rows (the ingest stager's field packing): per-rollout rows land at their valid-row offsets,
+    f64 sources convert to f32, a missing field zero-fills, mismatched sources raise."""
+    from dotaclient_amd import native
+    if not native.AVAILABLE:
+        pytest.skip('native module not built')
+    rng = np.random.default_rng(0)
+    lens = [3, 0, 5, 2]
+    pos = np.zeros(len(lens) + 1, np.int64)
+    np.cumsum(lens, out=pos[1:])
+    units = [rng.standard_normal((T, 7, 10)).astype(np.float32) for T in lens]
+    rew = [rng.standard_normal((T, 9)) for T in lens]
+    acts = [rng.integers(0, 255, (T, 61)).astype(np.uint8) for T in lens]
+    du = np.full((12, 7, 10), 7.0, np.float32)
+    dr = np.full((12, 9), 7.0, np.float32)
+    da = np.full((12, 61), 7, np.uint8)
+    dv = np.full(12, 7.0, np.float32)
+    native.pack_rows([(du, units), (dr, rew), (da, acts), (dv, [None] * 4)], pos, 3)
+    np.testing.assert_array_equal(du[:10], np.concatenate(units))
+    np.testing.assert_array_equal(dr[:10], np.concatenate(rew).astype(np.float32))
+    np.testing.assert_array_equal(da[:10], np.concatenate(acts))
+    assert not dv[:10].any() and (du[10:] == 7).all() and (dv[10:] == 7).all()
+    with pytest.raises(ValueError):
+        native.pack_rows([(du, [u[:, :5] .copy() for u in units])], pos, 2)        # wrong row width
+    with pytest.raises(ValueError):
+        native.pack_rows([(da, [a.astype(np.int64) for a in acts])], pos, 2)      # another dtype
+    with pytest.raises(ValueError):
+        native.pack_rows([(du, units[:3])], pos, 2)                               # one source short
