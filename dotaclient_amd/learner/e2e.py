@@ -387,12 +387,19 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
 
         d0 = dropped_total()
         say('e2e: learner loop')
+        probe = None
+        if os.environ.get('DCA_GIL_PROBE') == '1':
+            from ..utils.gilprobe import GilProbe
+            probe = GilProbe()
         try:
             s0 = opt.ingest_stats()
             rows, wall, (actor_steps, _) = _learner_loop(opt, duration, warmup_iterations, max_iterations,
                                                          counters=lambda: (steps.value, 0), check=check, agree=agree)
             s1 = opt.ingest_stats()
             ingest_diag = {k: s1[k] - s0[k] for k in s1}
+            if probe is not None:
+                import sys
+                print(probe.report(), file=sys.stderr, flush=True)
         finally:
             opt.close()
             opt.flush_checkpoints()

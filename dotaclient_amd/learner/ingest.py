@@ -388,8 +388,15 @@ class IngestPipeline:
         # pinned slot now — give their ring regions back (the canvas of the last one is kept for the logs)
         mk('hid+reset')
         tr = time.perf_counter()
-        for i, r in enumerate(rollouts):
-            r.detach_shared(keep_canvas=i == len(rollouts) - 1)
+        rels = [rel for i, r in enumerate(rollouts)
+                if (rel := r.detach_shared(keep_canvas=i == len(rollouts) - 1, release=False)) is not None]
+        if rels:
+            batch = getattr(type(rels[0]), 'release_all', None)      # (learner/optimizer.py _RingClaim: one lock)
+            if batch is not None:
+                batch(rels)
+            else:
+                for rel in rels:
+                    rel()
         tr = time.perf_counter() - tr
         mk('release')
         ev = None

@@ -325,14 +325,7 @@ class DotaOptimizer:
                 st = self.__dict__.setdefault('_claim_stats', [0, 0.0, 0.0])   # messages, claim wait s, decode s
                 st[1] += td - tw
                 view, token = got
-                n = cb.take(view.nbytes)
-                released = [False]
-
-                def rel(token=token, n=n, released=released):
-                    if not released[0]:
-                        released[0] = True
-                        broker.release_experience(token)
-                        cb.give(n)
+                rel = _RingClaim(broker, token, cb.take(view.nbytes), cb)
                 try:
                     r = decode_any(view, allow_pickle=self.cfg.allow_pickle_experience)
                 except CorruptMessage as e:
@@ -887,9 +880,7 @@ class DotaOptimizer:
             qs = getattr(self.broker, 'xp_queue_size', None)
             job = (self._write_logs, it, metrics, loss_t.numpy(), np.asarray(rollout_lens), np.asarray(weight_ages),
                    rollout_rewards, hist, p['canvas'], qs)
-            if os.environ.get('DCA_DIAG_SKIP_FILES') == '1':
-                pass                                  # (diagnostics: no event files — isolates the writer's GIL use)
-            elif cfg.async_checkpoint and self.device.type == 'cuda':
+            if cfg.async_checkpoint and self.device.type == 'cuda':
                 self._submit_background(*job)         # tensorboard events + their upload on the ordered writer
             else:
                 job[0](*job[1:])
@@ -1016,8 +1007,6 @@ class DotaOptimizer:
         self._write_checkpoint(data, trainer, version)
 
     def _write_checkpoint(self, data: bytes, trainer, version: int):
-        if os.environ.get('DCA_DIAG_SKIP_FILES') == '1':
-            return
         path = ckpt.write_model_bytes(data, self.cfg.log_dir, version)
         spath = ckpt.save_trainer_state(trainer, self.cfg.log_dir, version)
         if self.uploader is not None:   # reference optimizer.py:713-715 (GCS upload of the model file)
@@ -1025,6 +1014,39 @@ class DotaOptimizer:
             self.uploader.submit(spath, f'{self.store_prefix}/{os.path.basename(spath)}')
             self.uploader.flush()       # a pruned file must not vanish before its upload
         ckpt.prune(self.cfg.log_dir, self.cfg.checkpoint_keep)
+
+
+class _RingClaim:
+    """The release of one claimed ring message (Rollout.release): exactly once, budget given back. ``release_all``
+    gives a batch back under one ring lock per broker (the stager releases an iteration's rollouts together)."""
+    __slots__ = ('broker', 'token', 'n', 'cb', 'done')
+
+    def __init__(self, broker, token, n, cb):
+        self.broker, self.token, self.n, self.cb, self.done = broker, token, n, cb, False
+
+    def __call__(self):
+        if not self.done:
+            self.done = True
+            self.broker.release_experience(self.token)
+            self.cb.give(self.n)
+
+    @staticmethod
+    def release_all(claims):
+        groups = {}
+        for c in claims:
+            if not c.done:
+                c.done = True
+                groups.setdefault(id(c.broker), []).append(c)
+        for cs in groups.values():
+            b = cs[0].broker
+            many = getattr(b, 'release_experience_many', None)
+            if many is not None:
+                many([c.token for c in cs])
+            else:
+                for c in cs:
+                    b.release_experience(c.token)
+            for c in cs:
+                c.cb.give(c.n)
 
 
 class _ClaimBudget:

@@ -462,6 +462,23 @@ class RingCore {
     }
     unlock();
   }
+  // several claimed regions given back under ONE lock acquisition and one wake-up of the producers
+  void release_many(const uint64_t* pos, size_t n) {
+    lock();
+    bool any = false;
+    for (size_t i = 0; i < n; ++i) {
+      const uint64_t w = word_at(pos[i]);
+      if ((w >> 56) == kReading) {
+        set_word(pos[i], (kDone << 56) | (w & kLenMask));
+        any = true;
+      }
+    }
+    if (any) {
+      reclaim_locked();
+      pthread_cond_broadcast(&hdr_->not_full);
+    }
+    unlock();
+  }
   bool claim(uint64_t* pos_out, uint64_t* len_out, double timeout) {
     timespec ts;
     if (timeout > 0) deadline_in(timeout, ts);

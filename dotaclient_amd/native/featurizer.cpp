@@ -169,6 +169,10 @@ class ShmRing {
     py::gil_scoped_release rel;
     r_.release(token);
   }
+  void release_many(std::vector<uint64_t> tokens) {
+    py::gil_scoped_release rel;
+    r_.release_many(tokens.data(), tokens.size());
+  }
   RingCore* core() { return &r_; }
   uint64_t size() { return r_.size(); }
   uint64_t dropped() { return r_.dropped(); }
@@ -570,6 +574,7 @@ PYBIND11_MODULE(_native, m) {
       .def("claim", [](py::object self, double timeout) { return self.cast<ShmRing&>().claim(self, timeout); },
            py::arg("timeout") = -1.0)
       .def("release", &ShmRing::release, py::arg("token"))
+      .def("release_many", &ShmRing::release_many, py::arg("tokens"))
       .def("size", &ShmRing::size)
       .def("dropped", &ShmRing::dropped)
       .def_static("unlink", &ShmRing::unlink);

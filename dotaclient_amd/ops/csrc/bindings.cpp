@@ -638,15 +638,18 @@ void returns_scan(torch::Tensor rew, torch::Tensor val, torch::Tensor off, torch
     TORCH_CHECK(k[i] >= 0 && k[i] < ema.size(0), "returns_scan: key out of range at segment ", i);
     max_len = std::max(max_len, o[i + 1] - o[i]);
   }
-  // one upload of the packed metadata: [off | seglen | keys | boot | done]
-  auto meta = torch::empty({(int64_t)(4 * nseg + 1 + (nseg + 3) / 4)}, torch::dtype(at::kInt));
+  // one upload of the packed metadata: [off | seglen | keys | boot | done] — from pinned memory, non-blocking. (A
+  // pageable upload is a synchronous copy that waits for everything already queued on the stream: in the node loop's
+  // look-ahead ingest that was the whole iteration's training steps, with the GIL held by this call, so the stager
+  // and decode threads stalled behind it. The caching host allocator keeps the pinned block until the copy is done.)
+  auto meta = torch::empty({(int64_t)(4 * nseg + 1 + (nseg + 3) / 4)}, torch::dtype(at::kInt).pinned_memory(true));
   int* mp = meta.data_ptr<int>();
   std::memcpy(mp, o, sizeof(int) * (nseg + 1));
   std::memcpy(mp + nseg + 1, seglen.data_ptr<int>(), sizeof(int) * nseg);
   std::memcpy(mp + 2 * nseg + 1, k, sizeof(int) * nseg);
   std::memcpy(mp + 3 * nseg + 1, boot.data_ptr<float>(), sizeof(float) * nseg);
   std::memcpy(mp + 4 * nseg + 1, done.data_ptr<uint8_t>(), nseg);
-  auto md = meta.to(rew.device());
+  auto md = meta.to(rew.device(), /*non_blocking=*/true);
   int* d = md.data_ptr<int>();
   auto ema_out = ema.clone();
   hip_check(dca_returns(ptr<float>(rew), (int)rew.size(1), vp, d, d + nseg + 1, reinterpret_cast<float*>(d + 3 * nseg + 1),

@@ -97,17 +97,21 @@ class Rollout:
     def length(self) -> int:
         return int(self.rewards.shape[0])
 
-    def detach_shared(self, keep_canvas: bool = False):
+    def detach_shared(self, keep_canvas: bool = False, release: bool = True):
         """Once a ring-resident rollout has been staged (learner/ingest.py): keep private copies of what the learner
         still reads afterwards (rewards for the per-key logs, optionally the canvas), drop the views of the bulk
-        arrays — any later read fails loudly instead of reading a recycled ring region — and release the region."""
+        arrays — any later read fails loudly instead of reading a recycled ring region — and release the region
+        (``release=False``: return the release callable instead, for a caller that releases several at once)."""
         if self.release is None:
-            return
+            return None
         self.rewards = np.array(self.rewards)
         self.canvas = np.array(self.canvas) if (keep_canvas and self.canvas is not None) else None
         self.env = self.units = self.actions = self.masks = self.logp = self.values = self.hiddens = None
         rel, self.release = self.release, None
+        if not release:
+            return rel
         rel()
+        return None
 
     def unit_layout(self) -> UnitLayout:
         return UnitLayout(*self.layout)

@@ -56,6 +56,10 @@ class ShmBroker:
     def release_experience(self, token: int):
         self.ring.release(int(token))
 
+    def release_experience_many(self, tokens):
+        """Several claims given back under one ring lock (the stager releases an iteration's rollouts at once)."""
+        self.ring.release_many([int(t) for t in tokens])
+
     @property
     def capacity(self) -> int:
         return int(self._capacity)
