@@ -283,10 +283,9 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
 
     world, rank = pdist.get_world_size(), pdist.get_rank()
     local_world = int(os.environ.get('LOCAL_WORLD_SIZE', world))
-    # the recurrence's hand-off timeout (ops/csrc/lstm_team.hip spin_fail) is wall clock per wait: 2 s for a GPU of
-    # its own, 60 s here, where the actor process shares the GPU (its kernels time-slice against the persistent team
-    # kernel; round 5 saw one 2 s expiry in the config-5 loop beside the fp8 actor). A lost hand-off still errors.
-    os.environ.setdefault('DCA_TEAM_PATIENT', '1')
+    # (the recurrence keeps its default 2 s hand-off timeout beside the actor process: the config-5 loop's one expiry
+    # and its stall in round 5 came with ring claims leaked by the host ingest path — fixed; e2e, config 5 and config
+    # 4 loops then ran clean at 2 s, profiles/r5_default_timeout_loops.json)
     if os.environ.get('DCA_SWITCH_INTERVAL'):
         # the learner process's GIL hand-off interval (the stager, decode and main threads share one interpreter)
         import sys
