@@ -283,9 +283,10 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
 
     world, rank = pdist.get_world_size(), pdist.get_rank()
     local_world = int(os.environ.get('LOCAL_WORLD_SIZE', world))
-    # (the recurrence keeps its default 2 s hand-off timeout beside the actor process: the config-5 loop's one expiry
-    # and its stall in round 5 came with ring claims leaked by the host ingest path — fixed; e2e, config 5 and config
-    # 4 loops then ran clean at 2 s, profiles/r5_default_timeout_loops.json)
+    # (the recurrence keeps its default 2 s hand-off timeout beside the actor process. Round 5 saw one expiry in the
+    # config-5 loop, in the same build whose host ingest path leaked ring claims and stalled that loop; with the leak
+    # and the ingest's GIL-held stream wait fixed, the e2e, config-5 and config-4 loops run clean at 2 s —
+    # profiles/r5_default_timeout_loops.json. A lost hand-off errors within 2 s again.)
     if os.environ.get('DCA_SWITCH_INTERVAL'):
         # the learner process's GIL hand-off interval (the stager, decode and main threads share one interpreter)
         import sys
