@@ -287,10 +287,6 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
     # config-5 loop, in the same build whose host ingest path leaked ring claims and stalled that loop; with the leak
     # and the ingest's GIL-held stream wait fixed, the e2e, config-5 and config-4 loops run clean at 2 s —
     # profiles/r5_default_timeout_loops.json. A lost hand-off errors within 2 s again.)
-    if os.environ.get('DCA_SWITCH_INTERVAL'):
-        # the learner process's GIL hand-off interval (the stager, decode and main threads share one interpreter)
-        import sys
-        sys.setswitchinterval(float(os.environ['DCA_SWITCH_INTERVAL']))
     if transport == 'auto':
         from .. import native
         transport = 'shm' if (local_world == world and native.AVAILABLE) else 'tcp'

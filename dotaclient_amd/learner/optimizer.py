@@ -446,11 +446,12 @@ class DotaOptimizer:
                 self._xp_broker = mk() if mk is not None else self.broker
                 # consume + decode (CRC with the GIL released) on a thread of their own, so the stager packs and
                 # uploads iteration k+1 while the rollouts of k+2 are being decoded; on the node's shm ring zero-copy
-                # (claimed regions, released once staged — IngestPipeline.stage) with three decode threads
+                # (claimed regions, released once staged — IngestPipeline.stage)
+                # (one decode thread: with zero-copy its CRC pass is ≈30 % of a core at the loop's 2 000 rollouts/s;
+                # three measured no faster, round 5)
                 zc = hasattr(self._xp_broker, 'claim_experience')
-                nth = int(os.environ.get('DCA_DECODE_THREADS', '0')) or 1
                 pf = self._prefetcher = _RolloutPrefetcher(lambda stop: self._consume_decode(stop, claim=zc),
-                                                           self.cfg.prefetch_rollouts, threads=nth if zc else 1)
+                                                           self.cfg.prefetch_rollouts)
                 fetch = pf.get_until
             pl = self._pipeline = IngestPipeline(fetch, self.cfg.seq_len, self.cfg.seq_per_epoch, self.cfg.algo, H,
                                                  self.device, pack=self.cfg.pack_sequences)
@@ -1077,10 +1078,9 @@ class _RolloutPrefetcher:
     waits when the actors are behind; DCX1 decode (CRC, array views) and broker waits overlap the GPU training of the
     previous iteration. An exception in the thread (e.g. the experience timeout) is re-raised by :meth:`get`.
 
-    ``threads`` > 1 (the zero-copy shm path, whose per-message CRC runs with the GIL released): several decode threads
-    feed the queue — one thread's CRC pass over ≈1.35 MB per whole-game rollout capped the node loop at ≈2 000
-    rollouts/s (the stager waited 15 ms per iteration for them). Arrival order is then not the queue's order, as with
-    competing consumers anyway; the in-process broker keeps one thread (a deterministic order)."""
+    ``threads`` > 1: several decode threads feed the queue (arrival order is then not the queue's order, as with
+    competing consumers anyway). The node loop uses one: its 2 000 rollouts/s once looked decode-bound at ≈15 ms of
+    stager wait per iteration, which was the look-ahead ingest's GIL-held stream wait (returns scan), not the CRC."""
 
     def __init__(self, fetch, depth: int, threads: int = 1):
         import queue
