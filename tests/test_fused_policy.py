@@ -30,7 +30,9 @@ def test_fused_loss_and_grads_match_reference(gpu_ops, monkeypatch, pipeline, pr
     pol = Policy(cfg)
     ref = copy.deepcopy(pol)
     lc = LossConfig(algo=algo, vf_coef=0.5, entropy_coef=0.01)
-    fused = Learner(pol, lc, device='cuda', backend='fused', dp=False, precision='bf16')
+    # the reference-compat model (rnn 'linear') has kernels at fp32 / fp32-exact only: it is checked at fp32 here
+    fused = Learner(pol, lc, device='cuda', backend='fused', dp=False,
+                    precision='fp32' if preset == 'compat' else 'bf16')
     torch_l = Learner(ref, lc, device='cuda', backend='torch', dp=False, precision='fp32')   # fp32 oracle
     batch = make_batch(B, S, cfg.layout, cfg.hidden if cfg.rnn == 'lstm' else None, device='cuda', seed=3)
     for L in (fused, torch_l):
