@@ -74,7 +74,6 @@ class GpuRunner:
             torch.cuda.synchronize(self.device)
             gp.h[:old.n].copy_(old.h)
             gp.c[:old.n].copy_(old.c)
-            gp.h16[:old.n].copy_(old.h16)
             gp.ctr.copy_(old.ctr)
             self.free = list(range(cap - 1, old.n - 1, -1)) + self.free
         else:
