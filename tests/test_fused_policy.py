@@ -88,12 +88,20 @@ def test_graph_captured_step_matches_eager(gpu_ops, monkeypatch, chunks, precisi
         torch.cuda.synchronize()
         torch.testing.assert_close(mb['grad_norm'], ma['grad_norm'], rtol=1e-4, atol=1e-7)
     assert b.graph is not None
+    if chunks == '1':
+        torch.testing.assert_close(b.flat.flat, a.flat.flat, rtol=1e-5, atol=1e-6)
+        torch.testing.assert_close(mb['loss'], ma['loss'], rtol=1e-5, atol=1e-6)
+        return
     # the chunked two-stream fp32 step is not bitwise reproducible run to run (two EAGER learners differed by 4e-8 in
-    # a parameter at step 4 on MI355X; cause not isolated — the chunked mode is off by default); Adam's m/√v turns
-    # that into ≈5e-6 on near-zero-gradient elements. A stale graph buffer shows up as O(1e-2+) errors.
-    rtol, atol = (1e-3, 1e-5) if chunks != '1' else (1e-5, 1e-6)
-    torch.testing.assert_close(b.flat.flat, a.flat.flat, rtol=rtol, atol=atol)
-    torch.testing.assert_close(mb['loss'], ma['loss'], rtol=rtol, atol=atol)
+    # a parameter at step 4; the chunked mode is off by default). Adam's m/√v amplifies such a rounding difference on
+    # a near-zero-gradient element to up to lr per step (seen: 4.7e-5 after 4 steps), and bounds ANY gradient error
+    # the same way — so the parameters are only held to 4 steps × lr, and the decisive check is the last step's
+    # whole gradient: a stale graph buffer is an O(1) relative error there, rounding ≈1e-6
+    torch.testing.assert_close(b.flat.flat, a.flat.flat, rtol=0, atol=4 * lc.learning_rate)
+    assert a.flat.grad.norm() > 0
+    rel = ((b.flat.grad - a.flat.grad).norm() / a.flat.grad.norm()).item()
+    assert rel < 1e-3, rel
+    torch.testing.assert_close(mb['loss'], ma['loss'], rtol=1e-3, atol=1e-5)
 
 
 @pytest.mark.parametrize('precision', ['fp32', 'bf16'])
