@@ -159,6 +159,8 @@ def _summary(rows, wall, actor_steps, dropped, games, config):
         # GPU time from the first to the last training step of an iteration, per step, INSIDE the node loop (actor
         # graph replays and host enqueue gaps included) — compare with the learner-alone ms_per_step
         'learner_gpu_ms_per_step': float(np.nanmean(a[:, 10])) if n_it and np.isfinite(a[:, 10]).any() else float('nan'),
+        # the slowest iteration's steps (a device-wide stall — queue preemption, memory eviction — shows here)
+        'learner_gpu_ms_per_step_max': float(np.nanmax(a[:, 10])) if n_it and np.isfinite(a[:, 10]).any() else float('nan'),
         'rollouts_consumed': int(np.nansum(a[:, 11])) if n_it else 0,
         # the stager thread per iteration: packing + upload issue, and waiting for the decoded rollouts
         'stage_ms_per_iteration': 1e3 * float(np.nanmean(a[:, 12])) if n_it and np.isfinite(a[:, 12]).any() else float('nan'),
