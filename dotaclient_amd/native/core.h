@@ -311,11 +311,13 @@ struct RingHeader {
   uint64_t count;      // messages between head and tail (being written or ready)
   uint64_t dropped;
   uint64_t free_off;   // oldest byte still in use; [free_off, head) holds messages being read or done
+  uint64_t stuck_off;  // a claimed region seen blocking the reclaim at free_off, and since when (CLOCK_MONOTONIC ns)
+  uint64_t stuck_ns;
   pthread_mutex_t mu;
   pthread_cond_t not_empty;
   pthread_cond_t not_full;
 };
-constexpr uint64_t kMagic = 0x444341524e473032ull;   // "DCARNG02"
+constexpr uint64_t kMagic = 0x444341524e473033ull;   // "DCARNG03"
 
 void deadline_in(double seconds, timespec& ts) {
   clock_gettime(CLOCK_REALTIME, &ts);
@@ -334,6 +336,11 @@ class RingCore {
   static constexpr uint64_t kWrap = ~0ull;
   // a producer that reserved a region and never committed it (it died mid-copy) is skipped after this long
   static constexpr double kAbandonS = 30.0;
+  // a claimed region that blocks the reclaim (its consumer died, or holds it) is given up after this long when a
+  // producer needs the space (set_claim_abandon: tests); its late release is then ignored (claim tokens are
+  // monotonic offsets, below free_off once reclaimed)
+  double claim_abandon_s_ = 60.0;
+  void set_claim_abandon(double s) { claim_abandon_s_ = s; }
 
   RingCore(const std::string& name, uint64_t capacity, bool create) : name_(name) {
     const int flags = create ? (O_CREAT | O_RDWR) : O_RDWR;
@@ -416,12 +423,19 @@ class RingCore {
         return true;
       }
       if (drop_oldest && drop_head_locked()) continue;
+      if (abandon_stuck_claim_locked()) continue;
       if (timeout == 0.0) { unlock(); return false; }
-      if (timeout < 0) {
-        pthread_cond_wait(&hdr_->not_full, &hdr_->mu);
-      } else if (pthread_cond_timedwait(&hdr_->not_full, &hdr_->mu, &ts) == ETIMEDOUT) {
-        unlock();
-        return false;
+      // bounded waits (≤ 1 s) so a claim abandoned meanwhile is noticed without a wake-up
+      timespec wt;
+      deadline_in(1.0, wt);
+      if (timeout > 0 && (ts.tv_sec < wt.tv_sec || (ts.tv_sec == wt.tv_sec && ts.tv_nsec < wt.tv_nsec))) wt = ts;
+      if (pthread_cond_timedwait(&hdr_->not_full, &hdr_->mu, &wt) == ETIMEDOUT && timeout > 0) {
+        timespec now;
+        clock_gettime(CLOCK_REALTIME, &now);
+        if (now.tv_sec > ts.tv_sec || (now.tv_sec == ts.tv_sec && now.tv_nsec >= ts.tv_nsec)) {
+          unlock();
+          return false;
+        }
       }
     }
   }
@@ -442,34 +456,30 @@ class RingCore {
   // pop the oldest committed message, handing (payload, length) to fn OUTSIDE the lock (fn copies it out)
   template <class F>
   bool pop_with(F&& fn, double timeout) {
-    uint64_t pos, len;
-    if (!claim(&pos, &len, timeout)) return false;
+    uint64_t pos, len, tok;
+    if (!claim(&pos, &len, timeout, &tok)) return false;
     fn(data_ + pos + 8, len);
-    release(pos);
+    release(tok);
     return true;
   }
 
   // zero-copy consumption: claim the oldest committed message (its region stays reserved, readable at
-  // payload(pos), until release(pos)); releases may come in any order, space is reclaimed oldest-first
+  // payload(pos), until release(token)); releases may come in any order, space is reclaimed oldest-first. The token
+  // is the message's monotonic offset: a release that arrives after its region was abandoned and reclaimed
+  // (token < free_off) is ignored instead of touching whatever message occupies that position now.
   const uint8_t* payload(uint64_t pos) const { return data_ + pos + 8; }
-  void release(uint64_t pos) {
-    lock();
-    const uint64_t w = word_at(pos);
-    if ((w >> 56) == kReading) {
-      set_word(pos, (kDone << 56) | (w & kLenMask));
-      reclaim_locked();
-      pthread_cond_broadcast(&hdr_->not_full);
-    }
-    unlock();
-  }
+  void release(uint64_t token) { release_many(&token, 1); }
   // several claimed regions given back under ONE lock acquisition and one wake-up of the producers
-  void release_many(const uint64_t* pos, size_t n) {
+  void release_many(const uint64_t* tokens, size_t n) {
     lock();
     bool any = false;
     for (size_t i = 0; i < n; ++i) {
-      const uint64_t w = word_at(pos[i]);
+      uint64_t off = tokens[i];
+      if (off < hdr_->free_off || off >= hdr_->head) continue;     // reclaimed (abandoned) or never claimed
+      const uint64_t pos = resolve(off);
+      const uint64_t w = word_at(pos);
       if ((w >> 56) == kReading) {
-        set_word(pos[i], (kDone << 56) | (w & kLenMask));
+        set_word(pos, (kDone << 56) | (w & kLenMask));
         any = true;
       }
     }
@@ -479,7 +489,7 @@ class RingCore {
     }
     unlock();
   }
-  bool claim(uint64_t* pos_out, uint64_t* len_out, double timeout) {
+  bool claim(uint64_t* pos_out, uint64_t* len_out, double timeout, uint64_t* token_out = nullptr) {
     timespec ts;
     if (timeout > 0) deadline_in(timeout, ts);
     uint64_t stuck_at = ~0ull;          // head offset seen in the writing state, and since when
@@ -498,6 +508,7 @@ class RingCore {
           unlock();
           *pos_out = pos;
           *len_out = len;
+          if (token_out) *token_out = off;
           return true;
         }
         // the oldest message is still being written: wait for its commit; a producer that never commits (it died
@@ -563,6 +574,30 @@ class RingCore {
       return 0;
     }
     return pos;
+  }
+  // a claimed region at free_off that has blocked the reclaim for claim_abandon_s_ (the same region, seen by the
+  // producers waiting for space): given up — marked done and counted as dropped — so a consumer that died holding
+  // claims cannot stop the node's actors for good
+  bool abandon_stuck_claim_locked() {
+    if (hdr_->free_off >= hdr_->head) return false;
+    uint64_t off = hdr_->free_off;
+    const uint64_t pos = resolve(off);
+    const uint64_t w = word_at(pos);
+    if ((w >> 56) != kReading) return false;
+    timespec now;
+    clock_gettime(CLOCK_MONOTONIC, &now);
+    const uint64_t ns = (uint64_t)now.tv_sec * 1000000000ull + (uint64_t)now.tv_nsec;
+    if (hdr_->stuck_off != off || hdr_->stuck_ns == 0) {
+      hdr_->stuck_off = off;
+      hdr_->stuck_ns = ns;
+      return false;
+    }
+    if ((double)(ns - hdr_->stuck_ns) * 1e-9 < claim_abandon_s_) return false;
+    set_word(pos, (kDone << 56) | (w & kLenMask));
+    hdr_->dropped += 1;
+    hdr_->stuck_ns = 0;
+    reclaim_locked();
+    return true;
   }
   // reclaim the finished regions at the old end: [free_off, head) holds messages being read or done
   void reclaim_locked() {

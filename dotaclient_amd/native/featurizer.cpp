@@ -155,16 +155,17 @@ class ShmRing {
   // zero-copy: (uint8 array viewing the message IN the shared ring, token) — the region stays reserved until
   // release(token); the array must not be read after that. The array keeps this ring object alive.
   py::object claim(py::object self, double timeout) {
-    uint64_t pos, len;
+    uint64_t pos, len, token;
     bool got;
     {
       py::gil_scoped_release rel;
-      got = r_.claim(&pos, &len, timeout);
+      got = r_.claim(&pos, &len, timeout, &token);
     }
     if (!got) return py::none();
     py::array_t<uint8_t> arr({(py::ssize_t)len}, {(py::ssize_t)1}, r_.payload(pos), self);
-    return py::make_tuple(arr, pos);
+    return py::make_tuple(arr, token);
   }
+  void set_claim_abandon(double seconds) { r_.set_claim_abandon(seconds); }
   void release(uint64_t token) {
     py::gil_scoped_release rel;
     r_.release(token);
@@ -575,6 +576,7 @@ PYBIND11_MODULE(_native, m) {
            py::arg("timeout") = -1.0)
       .def("release", &ShmRing::release, py::arg("token"))
       .def("release_many", &ShmRing::release_many, py::arg("tokens"))
+      .def("set_claim_abandon", &ShmRing::set_claim_abandon, py::arg("seconds"))
       .def("size", &ShmRing::size)
       .def("dropped", &ShmRing::dropped)
       .def_static("unlink", &ShmRing::unlink);

@@ -276,3 +276,48 @@ def test_pack_rows_copies_converts_and_zero_fills():
         native.pack_rows([(da, [a.astype(np.int64) for a in acts])], pos, 2)      # another dtype
     with pytest.raises(ValueError):
         native.pack_rows([(du, units[:3])], pos, 2)                               # one source short
+
+
+def test_shm_ring_abandons_a_claim_that_pins_it():
+    """A consumer that dies holding a claimed message must not stop the producers for good: once the claimed region
+    at the reclaim point has blocked a producer for the abandonment time (60 s by default; 0.5 s here) it is given up
+    and counted as dropped, the producer's message goes in, and the late release of the old token is ignored."""
+    import time
+    import uuid
+    from dotaclient_amd import native
+    from dotaclient_amd.transport.shm import ShmBroker
+    if not native.AVAILABLE:
+        pytest.skip('native module not built')
+    b = ShmBroker(f'dca_ab_{uuid.uuid4().hex[:8]}', capacity=1 << 20, create=True, drop_oldest=True)
+    try:
+        b.ring.set_claim_abandon(0.5)
+        msg = b'm' * (200 << 10)
+        b.publish_experience(msg, timeout=1.0)
+        view, token = b.claim_experience(1.0)          # held, never released by this "dead" consumer
+        assert bytes(view[:4]) == b'mmmm'
+        while True:                                     # fill the ring behind the claim (no blocking)
+            try:
+                b.publish_experience(msg, timeout=0.0)
+            except TimeoutError:
+                break
+        d0 = b.ring.dropped()
+        t0 = time.monotonic()
+        # the ring is full and pinned by the claim (drop_oldest cannot reclaim behind it): the producer waits for the
+        # claim's abandonment
+        b.publish_experience(b'n' * (200 << 10), timeout=5.0)
+        waited = time.monotonic() - t0
+        assert 0.3 < waited < 4.0, waited
+        assert b.ring.dropped() > d0
+        b.release_experience(token)                     # late: ignored, the region was reclaimed
+        got = []
+        while True:
+            m = b.consume_experience(0.0)
+            if m is None:
+                break
+            got.append(bytes(m[:1]))
+        assert got and got[-1] == b'n'
+        # and the ring still works end to end
+        b.publish_experience(msg, timeout=1.0)
+        assert b.consume_experience(1.0) == msg
+    finally:
+        b.close(unlink=True)
