@@ -304,13 +304,16 @@ class DotaOptimizer:
         ``claim`` (the GPU learner's stager pipeline on the node's shared-memory ring): the rollout's arrays VIEW the
         message inside the ring — no copy out of it; the stager copies the fields straight into its pinned upload slot
         and gives the region back (:meth:`Rollout.detach_shared`). One host copy per message instead of two (ring →
-        heap → pinned). Claims are budgeted to half the ring, beyond that the copying path is taken, so held claims
-        can never starve the producers."""
+        heap → pinned). Claims are budgeted to half the ring (split over the node's learner ranks), beyond that the
+        copying path is taken, so held claims can never starve the producers."""
         broker = getattr(self, '_xp_broker', None) or self.broker
         if claim and stop is not None and hasattr(broker, 'claim_experience'):
             cb = self.__dict__.get('_claim_budget')
             if cb is None:
-                cb = self.__dict__.setdefault('_claim_budget', _ClaimBudget(getattr(broker, 'capacity', 0) // 2))
+                # half the ring, shared by the node's learner ranks (competing consumers of the one ring)
+                ranks = max(1, int(os.environ.get('LOCAL_WORLD_SIZE', os.environ.get('WORLD_SIZE', '1')) or 1))
+                cb = self.__dict__.setdefault('_claim_budget',
+                                              _ClaimBudget(getattr(broker, 'capacity', 0) // (2 * ranks)))
             t0 = time.monotonic()
             while cb.available():
                 got = None
