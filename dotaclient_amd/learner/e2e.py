@@ -304,8 +304,16 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
     if rank == 0:
         if transport == 'shm':
             from ..transport.shm import ShmBroker
+            from ..transport.shm import shm_free_bytes
             name = f'dca_e2e_{os.getpid()}_{int(time.time() * 1e3) % 10 ** 9}'
-            owner = ShmBroker(name, capacity=ring_bytes * world, create=True, drop_oldest=True)
+            cap = ring_bytes * world
+            free = shm_free_bytes()
+            if free is not None and cap > free // 2:
+                # a small /dev/shm (container default 64 MB, or a node with little RAM): the ring takes at most half
+                # of it, at least 64 MB (whole-game rollouts are ≈1.35 MB)
+                cap = max(64 << 20, free // 2)
+                say(f'e2e: /dev/shm has {free >> 20} MiB free: experience ring clamped to {cap >> 20} MiB')
+            owner = ShmBroker(name, capacity=cap, create=True, drop_oldest=True)
             addr = f'shm://{name}'
         else:
             from ..transport.broker import TcpBrokerServer

@@ -13,6 +13,15 @@ from typing import Callable, Optional
 from .. import native
 
 
+def shm_free_bytes() -> Optional[int]:
+    """Free bytes of /dev/shm (None where it cannot be read)."""
+    try:
+        import shutil
+        return int(shutil.disk_usage('/dev/shm').free)
+    except OSError:
+        return None
+
+
 class ShmBroker:
     def __init__(self, name: str, capacity: int = 1 << 28, create: Optional[bool] = None, drop_oldest: bool = False):
         if not native.AVAILABLE:
@@ -21,6 +30,13 @@ class ShmBroker:
         path = f'/dev/shm/{self.name}_xp'
         if create is None:
             create = not os.path.exists(path)
+        if create:
+            # tmpfs backs the ring lazily: a ring larger than /dev/shm's free space would be created fine and then
+            # SIGBUS its producers mid-write once the pages run out — refuse it here instead
+            free = shm_free_bytes()
+            if free is not None and capacity + (64 << 20) > free:
+                raise MemoryError(f'/dev/shm has {free >> 20} MiB free, the experience ring needs {capacity >> 20} MiB '
+                                  f'(+ the model file): pass a smaller capacity')
         self.ring = native.ShmRing(f'/{self.name}_xp', capacity, create)
         self._capacity = os.path.getsize(path)       # (+ the ring header: close enough for claim budgeting)
         self.model_path = f'/dev/shm/{self.name}_model'
