@@ -527,8 +527,14 @@ class DotaOptimizer:
                     torch.cuda.current_stream(self.device).synchronize()
                 self.learner.release_graphs(pool)
             pool = self._pool = _IterationPool({k: data[k] for k in fields}, cap, self.cfg.seq_len)
-        for k in fields:
-            pool.data[k][:n].copy_(data[k][:n])
+        dst = [pool.data[k][:n] for k in fields]
+        src = [data[k][:n] for k in fields]
+        if self.device.type == 'cuda' and all(t.is_contiguous() and t.data_ptr() % 16 == 0 for t in dst + src):
+            from ..ops import require
+            require().multi_copy(dst, src)            # one launch for every field (was one copy launch each)
+        else:
+            for d, t in zip(dst, src):
+                d.copy_(t)
         return pool
 
     def _sync_running(self, ema: Optional[torch.Tensor] = None):
@@ -770,8 +776,14 @@ class DotaOptimizer:
         if not losses or not all(torch.is_tensor(x) and x.is_cuda for x in losses):
             return None
         keys = list(metrics_acc)
-        parts = [torch.stack(losses).float().reshape(-1),
-                 torch.stack([torch.stack(metrics_acc[k]).float().mean() for k in keys])]
+        # every per-step value flat in ONE concatenation (the per-key means are taken on the host): a stack + mean
+        # per metric key was ≈40 small launches per iteration on the learner's stream
+        parts = [x.reshape(-1).float() for x in losses]
+        seg = []
+        for k in keys:
+            vs = [v.reshape(-1).float() for v in metrics_acc[k]]
+            seg.append(sum(v.numel() for v in vs))
+            parts += vs
         n_ema = 0
         if ema_snap is not None:
             parts.append(ema_snap.float().reshape(-1))
@@ -789,7 +801,7 @@ class DotaOptimizer:
             buf[i] = torch.empty(max(vec.numel(), 2 * buf[i].numel()), dtype=torch.float32).pin_memory()
         h = buf[i][:vec.numel()]
         h.copy_(vec, non_blocking=True)
-        return dict(vec=h, n_loss=len(losses), keys=keys, n_ema=n_ema,
+        return dict(vec=h, n_loss=sum(x.numel() for x in losses), keys=keys, seg=seg, n_ema=n_ema,
                     ema_shape=tuple(ema_snap.shape) if ema_snap is not None else None, n_flags=len(flags))
 
     def _defer_metrics(self) -> bool:
@@ -813,11 +825,14 @@ class DotaOptimizer:
         if hs is not None:
             # the pinned snapshot of the device values (_host_snapshot): complete once ``done`` is, no further syncs
             v = hs['vec'].clone()
-            nl, nk, ne = hs['n_loss'], len(hs['keys']), hs['n_ema']
+            nl, ne = hs['n_loss'], hs['n_ema']
             loss_t = v[:nl]
-            means = v[nl:nl + nk].tolist()
-            ema_host = v[nl + nk:nl + nk + ne].view(hs['ema_shape']) if ne else None
-            flags = v[nl + nk + ne:]
+            means, o = [], nl
+            for c in hs['seg']:
+                means.append(float(v[o:o + c].double().mean()) if c else float('nan'))
+                o += c
+            ema_host = v[o:o + ne].view(hs['ema_shape']) if ne else None
+            flags = v[o + ne:]
         else:
             loss_t = torch.stack(p['losses']).float().cpu()
         if faults().nan_loss(it):

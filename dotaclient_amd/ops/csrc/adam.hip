@@ -193,3 +193,60 @@ extern "C" hipError_t dca_multi_axpy(float* const* dst, const float* const* src,
   multi_axpy_kernel<<<blocks, 256, 0, st>>>(tab, scale);
   return hipGetLastError();
 }
+
+// ------------------------------------------------------------------------------------------------------------
+// Multi-tensor copy: up to kMaxCopy (dst, src, bytes) segments in ONE launch (16-byte chunks, byte tail), table by
+// value in the kernel arguments. The learner's per-iteration pool fill was a dozen separate copy launches.
+namespace {
+constexpr int kMaxCopy = 64;
+struct CopyTable {
+  unsigned char* dst[kMaxCopy];
+  const unsigned char* src[kMaxCopy];
+  long long bytes[kMaxCopy];
+  long long start[kMaxCopy + 1];   // prefix sum of 16-byte chunk counts
+  int n;
+};
+
+__global__ __launch_bounds__(256) void multi_copy_kernel(CopyTable tab) {
+  const long long total = tab.start[tab.n];
+  for (long long e = (long long)blockIdx.x * 256 + threadIdx.x; e < total; e += (long long)gridDim.x * 256) {
+    int lo = 0, hi = tab.n - 1;
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tab.start[mid] <= e) lo = mid; else hi = mid - 1;
+    }
+    const long long off = (e - tab.start[lo]) * 16;
+    const long long nb = tab.bytes[lo];
+    if (off + 16 <= nb) {
+      *reinterpret_cast<uint4*>(tab.dst[lo] + off) = *reinterpret_cast<const uint4*>(tab.src[lo] + off);
+    } else {
+      for (long long b = off; b < nb; ++b) tab.dst[lo][b] = tab.src[lo][b];
+    }
+  }
+}
+}  // namespace
+
+extern "C" hipError_t dca_multi_copy(void* const* dst, const void* const* src, const long long* bytes, int n,
+                                     hipStream_t st) {
+  if (n < 0 || n > kMaxCopy) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  CopyTable tab;
+  tab.n = n;
+  tab.start[0] = 0;
+  for (int i = 0; i < n; ++i) {
+    // 16-byte chunks need 16-byte aligned segments (torch allocations and their leading slices are)
+    if ((reinterpret_cast<unsigned long long>(dst[i]) | reinterpret_cast<unsigned long long>(src[i])) & 15ull)
+      return hipErrorInvalidValue;
+    tab.dst[i] = static_cast<unsigned char*>(dst[i]);
+    tab.src[i] = static_cast<const unsigned char*>(src[i]);
+    tab.bytes[i] = bytes[i];
+    tab.start[i + 1] = tab.start[i] + (bytes[i] + 15) / 16;
+  }
+  const long long total = tab.start[n];
+  long long blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks < 1) blocks = 1;
+  multi_copy_kernel<<<(int)blocks, 256, 0, st>>>(tab);
+  return hipGetLastError();
+}
+

@@ -66,6 +66,22 @@ void adam_step(torch::Tensor param, torch::Tensor grad, torch::Tensor m, torch::
 
 // dst_i += scale · src_i over a list of fp32 tensors in one graph-capturable launch (scale: 1-element device
 // tensor or None = 1).
+void multi_copy(std::vector<torch::Tensor> dst, std::vector<torch::Tensor> src) {
+  TORCH_CHECK(dst.size() == src.size(), "multi_copy: list length mismatch");
+  TORCH_CHECK(dst.size() <= 64, "multi_copy: at most 64 tensors");
+  std::vector<void*> d;
+  std::vector<const void*> s;
+  std::vector<long long> n;
+  for (size_t i = 0; i < dst.size(); ++i) {
+    CHECK_DEV(dst[i]); CHECK_DEV(src[i]); CHECK_CONTIG(dst[i]); CHECK_CONTIG(src[i]);
+    TORCH_CHECK(dst[i].nbytes() == src[i].nbytes(), "multi_copy: byte size mismatch at ", i);
+    d.push_back(dst[i].data_ptr());
+    s.push_back(src[i].data_ptr());
+    n.push_back((long long)dst[i].nbytes());
+  }
+  hip_check(dca_multi_copy(d.data(), s.data(), n.data(), (int)d.size(), cur_stream()), "dca_multi_copy");
+}
+
 void multi_axpy(std::vector<torch::Tensor> dst, std::vector<torch::Tensor> src, c10::optional<torch::Tensor> scale) {
   TORCH_CHECK(dst.size() == src.size(), "multi_axpy: list length mismatch");
   TORCH_CHECK(dst.size() <= 64, "multi_axpy: at most 64 tensors");
@@ -1134,6 +1150,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("seg"), py::arg("counts"), py::arg("steps"), py::arg("norm_out"), py::arg("lr"), py::arg("b1"),
         py::arg("b2"), py::arg("eps"), py::arg("max_norm"), py::arg("divide") = false, py::arg("header") = 0,
         py::arg("skip") = py::none(), py::arg("nonfinite") = py::none());
+  m.def("multi_copy", &multi_copy, "dst_i <- src_i (same byte sizes, contiguous, 16-B aligned) in one launch");
   m.def("multi_axpy", &multi_axpy, "dst_i += scale * src_i for a list of fp32 tensors (one graph-safe launch)",
         py::arg("dst"), py::arg("src"), py::arg("scale") = py::none());
   m.def("lstm_team_ctl_bytes", &dca_lstm_team_ctl_bytes, "bytes of a persistent team-LSTM control block");

@@ -121,3 +121,19 @@ def test_scan_kernel_matches_reference(gpu_ops, mode):
     for k in ('ret', 'adv', 'norm', 'stats'):
         torch.testing.assert_close(got[k].cpu(), ref[k], rtol=2e-4, atol=2e-4, msg=k)
     torch.testing.assert_close(ema_g.cpu(), ema_c, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_multi_copy_matches_per_tensor_copies(gpu_ops):
+    """ops multi_copy (the learner's one-launch pool fill): every segment byte-exact, including byte tails of
+    uint8 fields whose sizes are not multiples of 16."""
+    g = torch.Generator(device='cuda').manual_seed(0)
+    srcs = [torch.randn(1000, 7, device='cuda', generator=g), torch.randint(0, 255, (333, 61), device='cuda',
+                                                                             dtype=torch.uint8, generator=g),
+            torch.randn(5, device='cuda', generator=g), torch.randint(0, 2, (1401,), device='cuda', dtype=torch.uint8,
+                                                                      generator=g)]
+    dsts = [torch.full_like(t, 7) for t in srcs]
+    gpu_ops.multi_copy(dsts, srcs)
+    torch.cuda.synchronize()
+    for d, s in zip(dsts, srcs):
+        assert torch.equal(d, s)
