@@ -476,6 +476,9 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                                 f'{K} processes per rank over the node {transport} broker'), learners=world,
                          league=league, latest_weights_prob=latest_weights_prob, actor_precision=actor_precision,
                          replay_gb=replay_gb,
+                         # what was allocated (≤ replay_gb: the learner keeps the replay within the free HBM)
+                         replay_gb_allocated=(opt.replay.nbytes / 1e9 if opt is not None and opt.replay is not None
+                                              else 0.),
                          replay_sequences=(len(opt.replay) if opt is not None and opt.replay is not None else 0),
                          replay_capacity=(opt.replay.capacity if opt is not None and opt.replay is not None else 0),
                          replay_fill=(opt.replay.fill_fraction if opt is not None and opt.replay is not None else 0.),

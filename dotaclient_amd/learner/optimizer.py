@@ -217,7 +217,18 @@ class DotaOptimizer:
             from .replay import HbmReplay
             hid = self.policy_cfg.hidden if self.policy.is_recurrent else None
             pk = bool(cfg.pack_sequences)             # packed sequences keep their episode-start flags in the ring
-            cap = cfg.replay_capacity or HbmReplay.capacity_for_bytes(cfg.replay_gb * 1e9, cfg.seq_len,
+            gb = cfg.replay_gb
+            if not cfg.replay_capacity and self.device.type == 'cuda':
+                # never more than the GPU can hold beside this learner, the node loop's actor process and whatever
+                # else is resident: a replay that oversubscribes HBM turns into device-wide stalls of many seconds per
+                # step (round 5: a box with 262 GB already in use). Keep 24 GB of headroom.
+                free = torch.cuda.mem_get_info(self.device)[0] / 1e9
+                if gb > free - 24.0:
+                    fit = max(1.0, free - 24.0)
+                    logger.warning('replay_gb %.0f > %.0f GB free on %s: the replay takes %.0f GB', gb, free,
+                                   self.device, fit)
+                    gb = fit
+            cap = cfg.replay_capacity or HbmReplay.capacity_for_bytes(gb * 1e9, cfg.seq_len,
                                                                        self.policy_cfg.layout, hid, pk)
             self.replay = HbmReplay(cap, cfg.seq_len, self.policy_cfg.layout, hid, self.device, seed=cfg.seed,
                                     reset=pk)
