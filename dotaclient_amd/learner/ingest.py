@@ -60,6 +60,12 @@ def _load_native_copy():
 _native_copy = _load_native_copy()
 
 
+def _ops():
+    """The HIP extension (raises when it is not built: a GPU learner never falls back silently)."""
+    from .. import ops
+    return ops.require()
+
+
 def _load_native_pack():
     try:
         from ..native import _native
@@ -289,6 +295,8 @@ class IngestPipeline:
         if self.pack:
             rst_off = nbytes                     # (L,) u8 episode-start flags in the padded layout
             nbytes += _round(L)
+        inv_off = nbytes                         # (L,) i32: the valid row each padded row takes, −1 for padding
+        nbytes += _round(4 * L)
         mk('pack')
         slot_i = self._k % 2
         slot = self.slots[slot_i]
@@ -380,6 +388,9 @@ class IngestPipeline:
                     if r.hiddens is not None and r.hidden_stride and a % r.hidden_stride == 0 \
                             and a // r.hidden_stride < len(r.hiddens):
                         hid[i] = r.hiddens[a // r.hidden_stride]
+        iv = hview(inv_off, 4 * L, 'int32', (L,))
+        iv[:] = -1
+        iv[rows] = np.arange(Lv, dtype=np.int32)
         if self.pack:
             rv = hview(rst_off, L, 'uint8', (L,))
             rv[:] = 0
@@ -419,6 +430,7 @@ class IngestPipeline:
                                                                                                        self.H)
         if self.pack:
             views['reset'] = slot.dev[rst_off:rst_off + L]
+        views['inv'] = slot.dev[inv_off:inv_off + 4 * L].view(torch.int32)
         mk('views')
         self._prof_done()
         return StagedIteration(rollouts=rollouts, lens=lens, off=off, n_seq=n_seq, L=L, Lv=Lv, gae_mode=gae_mode,
@@ -462,24 +474,29 @@ class IngestPipeline:
         v = st.views
         rows = v['rows']
         out = {}
-        for name in ('env', 'units', 'actions', 'masks', 'logp', 'rewards') + (('values',) if st.gae_mode else ()):
+        names = ('env', 'units', 'actions', 'masks', 'logp', 'rewards') + (('values',) if st.gae_mode else ())
+        for name in names:
             src = v[name]
-            shape = (st.L,) + tuple(src.shape[1:])
             buf = pad.get(name)
             if buf is None or buf.dtype != src.dtype or buf.shape[1:] != src.shape[1:] or buf.shape[0] < st.L:
                 buf = pad[name] = torch.empty((max(st.L, 2 * (buf.shape[0] if buf is not None else 0)),) +
                                               tuple(src.shape[1:]), dtype=src.dtype, device=self.device)
-            b = buf[:st.L]
-            b.zero_()
-            b.index_copy_(0, rows, src)
-            out[name] = b.view(shape)
+            out[name] = buf[:st.L]
         valid = pad.get('valid')
         if valid is None or valid.shape[0] < st.L:
             valid = pad['valid'] = torch.empty(max(st.L, 2 * (valid.shape[0] if valid is not None else 0)),
                                                device=self.device)
         vb = valid[:st.L]
-        vb.zero_()
-        vb.index_fill_(0, rows, 1.0)
+        C = _ops() if self.cuda else None
+        if C is not None and 'inv' in v:
+            # every field's padded rows and the validity mask in one launch (ops/csrc/ingest.hip)
+            C.ingest_scatter([out[n] for n in names], [v[n] for n in names], v['inv'], vb)
+        else:
+            for name in names:
+                out[name].zero_()
+                out[name].index_copy_(0, rows, v[name])
+            vb.zero_()
+            vb.index_fill_(0, rows, 1.0)
         out['valid'] = vb
         if 'hid' in v:
             out['hid'] = v['hid'].clone()

@@ -558,6 +558,14 @@ class DotaOptimizer:
 
     def _normalize_advantages(self, d):
         if self.cfg.algo == 'ppo' and self.cfg.normalize_advantages:
+            a, v = d['adv'], d['valid']
+            if a.is_cuda and a.is_contiguous() and v.is_contiguous() and a.dtype == v.dtype == torch.float32:
+                # one single-workgroup kernel (ops/csrc/ingest.hip) instead of ≈10 small launches
+                from ..ops import require
+                out = torch.empty_like(a)
+                require().adv_normalize(a, v, out, float(EPS))
+                d['adv'] = out
+                return
             v = d['valid']
             n = v.sum().clamp_min(1.0)
             mu = (d['adv'] * v).sum() / n

@@ -66,6 +66,44 @@ void adam_step(torch::Tensor param, torch::Tensor grad, torch::Tensor m, torch::
 
 // dst_i += scale · src_i over a list of fp32 tensors in one graph-capturable launch (scale: 1-element device
 // tensor or None = 1).
+// the look-ahead ingest's expand (learner/ingest.py): padded row r of every field takes packed valid row inv[r]
+// (zeros when inv[r] < 0); valid[r] = inv[r] >= 0
+void ingest_scatter(std::vector<torch::Tensor> dst, std::vector<torch::Tensor> src, torch::Tensor inv,
+                    torch::Tensor valid) {
+  TORCH_CHECK(dst.size() == src.size() && dst.size() <= 16, "ingest_scatter: at most 16 (dst, src) pairs");
+  CHECK_DEV(inv); CHECK_CONTIG(inv); CHECK_DT(inv, at::kInt);
+  CHECK_F32(valid);
+  const int64_t L = inv.numel();
+  TORCH_CHECK(valid.numel() == L, "ingest_scatter: valid must have one entry per padded row");
+  std::vector<void*> d;
+  std::vector<const void*> s;
+  std::vector<int> rb;
+  int64_t nsrc = INT32_MAX;
+  for (size_t i = 0; i < dst.size(); ++i) {
+    CHECK_DEV(dst[i]); CHECK_DEV(src[i]); CHECK_CONTIG(dst[i]); CHECK_CONTIG(src[i]);
+    TORCH_CHECK(dst[i].scalar_type() == src[i].scalar_type(), "ingest_scatter: dtype mismatch at ", i);
+    nsrc = std::min<int64_t>(nsrc, src[i].size(0));
+    TORCH_CHECK(dst[i].dim() >= 1 && dst[i].size(0) == L, "ingest_scatter: dst ", i, " must have L rows");
+    const int64_t row = dst[i].numel() / std::max<int64_t>(1, L) * dst[i].element_size();
+    TORCH_CHECK(src[i].dim() >= 1 && src[i].numel() / std::max<int64_t>(1, src[i].size(0)) * src[i].element_size() == row,
+                "ingest_scatter: row size mismatch at ", i);
+    d.push_back(dst[i].data_ptr());
+    s.push_back(src[i].data_ptr());
+    rb.push_back((int)row);
+  }
+  // inv entries beyond the shortest source read nothing (the kernel zero-fills those rows): no out-of-range reads
+  if (d.empty()) nsrc = 0;
+  hip_check(dca_ingest_scatter(d.data(), s.data(), rb.data(), (int)d.size(), ptr<int>(inv), (int)L, (int)nsrc,
+                               ptr<float>(valid), cur_stream()), "dca_ingest_scatter");
+}
+
+void adv_normalize(torch::Tensor adv, torch::Tensor valid, torch::Tensor out, double eps) {
+  CHECK_F32(adv); CHECK_F32(valid); CHECK_F32(out);
+  TORCH_CHECK(adv.numel() == valid.numel() && out.numel() == adv.numel(), "adv_normalize: size mismatch");
+  hip_check(dca_adv_normalize(ptr<float>(adv), ptr<float>(valid), ptr<float>(out), (int)adv.numel(), (float)eps,
+                              cur_stream()), "dca_adv_normalize");
+}
+
 void multi_copy(std::vector<torch::Tensor> dst, std::vector<torch::Tensor> src) {
   TORCH_CHECK(dst.size() == src.size(), "multi_copy: list length mismatch");
   TORCH_CHECK(dst.size() <= 64, "multi_copy: at most 64 tensors");
@@ -1150,6 +1188,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("seg"), py::arg("counts"), py::arg("steps"), py::arg("norm_out"), py::arg("lr"), py::arg("b1"),
         py::arg("b2"), py::arg("eps"), py::arg("max_norm"), py::arg("divide") = false, py::arg("header") = 0,
         py::arg("skip") = py::none(), py::arg("nonfinite") = py::none());
+  m.def("ingest_scatter", &ingest_scatter, "packed valid rows -> zero-padded rows of every field + validity mask");
+  m.def("adv_normalize", &adv_normalize, "PPO advantage normalisation over the valid rows (one workgroup)");
   m.def("multi_copy", &multi_copy, "dst_i <- src_i (same byte sizes, contiguous, 16-B aligned) in one launch");
   m.def("multi_axpy", &multi_axpy, "dst_i += scale * src_i for a list of fp32 tensors (one graph-safe launch)",
         py::arg("dst"), py::arg("src"), py::arg("scale") = py::none());

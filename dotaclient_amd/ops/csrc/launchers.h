@@ -40,6 +40,9 @@ hipError_t dca_adam_step(float* param, const float* grad, float* m, float* v, co
                          const float* skip, float* nonfinite);
 int dca_adam_partials_len(int n_params);
 
+hipError_t dca_ingest_scatter(void* const* dst, const void* const* src, const int* row_bytes, int n, const int* inv,
+                              int L, int nsrc, float* valid, hipStream_t st);
+hipError_t dca_adv_normalize(const float* adv, const float* valid, float* out, int L, float eps, hipStream_t st);
 hipError_t dca_multi_copy(void* const* dst, const void* const* src, const long long* bytes, int n, hipStream_t st);
 hipError_t dca_multi_axpy(float* const* dst, const float* const* src, const long long* numel, int n,
                           const float* scale, hipStream_t st);

@@ -137,3 +137,37 @@ def test_multi_copy_matches_per_tensor_copies(gpu_ops):
     torch.cuda.synchronize()
     for d, s in zip(dsts, srcs):
         assert torch.equal(d, s)
+
+
+@pytest.mark.gpu
+def test_ingest_scatter_and_adv_normalize_match_torch(gpu_ops):
+    """ops ingest_scatter (the look-ahead expand's one launch) against zero_() + index_copy_() per field, incl. byte
+    rows (uint8, 61 B) and out-of-range inv entries (zeros, never read); adv_normalize against the torch expression."""
+    g = torch.Generator(device='cuda').manual_seed(1)
+    L, Lv = 500, 321
+    rows = torch.randperm(L, device='cuda', generator=g)[:Lv].sort().values
+    inv = torch.full((L,), -1, dtype=torch.int32, device='cuda')
+    inv[rows] = torch.arange(Lv, dtype=torch.int32, device='cuda')
+    inv[rows[-1]] = Lv + 5                                   # out of range: must come out as a padding row
+    srcs = [torch.randn(Lv, 40, 10, device='cuda', generator=g),
+            torch.randint(0, 255, (Lv, 61), dtype=torch.uint8, device='cuda', generator=g),
+            torch.randn(Lv, device='cuda', generator=g), torch.randn(Lv, 9, device='cuda', generator=g)]
+    dsts = [torch.full((L,) + tuple(t.shape[1:]), 7, dtype=t.dtype, device='cuda') for t in srcs]
+    valid = torch.full((L,), 7.0, device='cuda')
+    gpu_ops.ingest_scatter(dsts, srcs, inv, valid)
+    keep = rows[:-1]
+    for d, s in zip(dsts, srcs):
+        ref = torch.zeros_like(d)
+        ref.index_copy_(0, keep, s[:Lv - 1])
+        assert torch.equal(d, ref)
+    vref = torch.zeros(L, device='cuda')
+    vref[keep] = 1.0
+    assert torch.equal(valid, vref)
+    adv = torch.randn(8, 64, device='cuda', generator=g) * 3 + 1
+    v = (torch.rand(8, 64, device='cuda', generator=g) > 0.3).float()
+    out = torch.empty_like(adv)
+    gpu_ops.adv_normalize(adv, v, out, 1e-8)
+    n = v.sum().clamp_min(1.0)
+    mu = (adv * v).sum() / n
+    sd = (((adv - mu) ** 2 * v).sum() / n).sqrt()
+    torch.testing.assert_close(out, ((adv - mu) / (sd + 1e-8)) * v, rtol=1e-5, atol=1e-6)
