@@ -25,14 +25,21 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
                        max_dota_time: float = 600.0, pack: bool = True, seed: int = 7, device: str = 'cuda',
                        eval_seed: int = 4242, on_row: Optional[Callable[[Dict], None]] = None,
                        save_model: Optional[str] = None, eval_precision: str = 'fp32',
-                       mode: str = '1v1', log_dir: Optional[str] = None) -> List[Dict]:
+                       mode: str = '1v1', log_dir: Optional[str] = None, league: Optional[str] = None,
+                       latest_weights_prob: float = 0.8, actor_precision: str = 'bf16',
+                       replay_gb: float = 0.0) -> List[Dict]:
     """Train for ``budget`` seconds (evaluations excluded) and return the evaluation rows (the first one before
     any training). ``on_row`` is called with every row as it is produced; ``save_model``: path that receives the
     final weights (a reference-format state_dict file). ``eval_precision``: the validation games' policy step.
 
     ``log_dir``: keep the optimizer's checkpoints there (the latest one only) and resume from them — model, Adam
     state and return normalisers (DotaOptimizer's resume) plus the curve's own counters (``curve_state.json``), so a
-    long curve runs as several shorter jobs; ``budget`` is then the total, counted from the first job."""
+    long curve runs as several shorter jobs; ``budget`` is then the total, counted from the first job.
+
+    BASELINE config 5 as a curve: ``league`` ('pfsp' / 'uniform', actor/league.py) makes the actors play the latest
+    weights against sampled past versions (``latest_weights_prob`` of the games self-play the latest), the actor's
+    policy step runs at ``actor_precision`` ('fp8' for config 5), and ``replay_gb`` > 0 trains every minibatch from
+    an on-HBM replay of that size (learner/replay.py) instead of the iteration's fresh rollouts."""
     import json
     import os
 
@@ -57,14 +64,20 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
                           learning_rate=lr, entropy_coef=entropy_coef, checkpoint_keep=1 if log_dir else 2,
                           run_local=True,
                           xp_timeout=300.0, histogram_freq=10 ** 9, async_checkpoint=True, prefetch_rollouts=64,
-                          pack_sequences=bool(pack), seed=seed)
+                          pack_sequences=bool(pack), seed=seed, replay_gb=replay_gb)
     opt = DotaOptimizer(cfg, broker)
     ws = WeightStore(model, device='cpu')
     loader = ThreadPoolExecutor(1, thread_name_prefix='weights')
     broker.subscribe_model(lambda v, b: loader.submit(ws.add_bytes, v, b))
     loader.submit(lambda: None).result()
+    lg = None
+    if league:
+        from ..actor.league import League
+        lg = League(ws, mode=league)
     va = VecActor(ws, games, broker.publish_experience, device=device, seed=seed, rollout_size=9999,
-                  max_dota_time=max_dota_time, hidden_stride=seq_len, threads=threads, stagger=True, mode=mode)
+                  max_dota_time=max_dota_time, hidden_stride=seq_len, threads=threads, stagger=True, mode=mode,
+                  league=lg, latest_weights_prob=latest_weights_prob if lg is not None else 1.0,
+                  precision=actor_precision)
     stop, pause, paused, err = threading.Event(), threading.Event(), threading.Event(), []
     rows: List[Dict] = []
     sync = torch.cuda.synchronize if str(device).startswith('cuda') else (lambda: None)

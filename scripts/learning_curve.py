@@ -33,6 +33,11 @@ def main(argv=None):
     ap.add_argument('--save-model', default=None, help='write the final weights here (state_dict file)')
     ap.add_argument('--eval-precision', default='fp32', choices=['fp32', 'bf16', 'fp8'])
     ap.add_argument('--mode', default='1v1', choices=['1v1', '5v5'])
+    ap.add_argument('--league', default=None, choices=[None, 'pfsp', 'uniform'],
+                    help='self-play league opponents (BASELINE config 5)')
+    ap.add_argument('--latest-weights-prob', type=float, default=0.8)
+    ap.add_argument('--actor-precision', default='bf16', choices=['fp32', 'bf16', 'fp8'])
+    ap.add_argument('--replay-gb', type=float, default=0.0, help='on-HBM replay the learner samples from')
     ap.add_argument('--device', default='cuda')
     ap.add_argument('--log-dir', default=None,
                     help='checkpoint directory: resume the curve from it (model, Adam, normalisers, counters) and '
@@ -51,7 +56,8 @@ def main(argv=None):
                            entropy_coef=a.entropy_coef, max_dota_time=a.max_dota_time, pack=bool(a.pack),
                            seed=a.seed, device=a.device, on_row=emit, save_model=a.save_model,
                            eval_precision=a.eval_precision, mode=a.mode,
-                           log_dir=a.log_dir)
+                           log_dir=a.log_dir, league=a.league, latest_weights_prob=a.latest_weights_prob,
+                           actor_precision=a.actor_precision, replay_gb=a.replay_gb)
 
 
 if __name__ == '__main__':
