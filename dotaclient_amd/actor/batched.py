@@ -153,10 +153,11 @@ class GpuActorPolicy:
         self.d_snap = torch.zeros(n, 2, H, device=dev)
         self.o_snap = torch.zeros(n, 2, H, **pin)
         self._snap_n = 0
-        # the actor's step stream at high priority (torch convention: lower = higher): its short policy-step graphs are
-        # dispatched ahead of a learner training on the same GPU (one-GPU node loop, scripts/e2e_ab.py 15 1024,14:
-        # 1.276 / 1.305 M vs 1.242 / 1.259 M steps/s at the default priority)
-        self.stream = torch.cuda.Stream(device=dev, priority=-1)
+        # the actor's step stream at the DEFAULT priority. (High priority, round 4: +2-3 % in the then actor-bound node
+        # loop; round 5: no difference in the GPU-bound loop, scripts/gpu_r5_ff.sh — and with a league's opponent
+        # policies adding more high-priority work beside the learner's persistent recurrence, the recurrence stalled
+        # for seconds: profiles/r5_replay_timeout.md, scripts/gpu_r5_bisect.sh.)
+        self.stream = torch.cuda.Stream(device=dev)
 
     @torch.no_grad()
     def load_weights(self, policy_or_state):
