@@ -201,10 +201,10 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     use_cuda = torch.cuda.is_available()
     shared = os.environ.get('DCA_SHARED_GPU') == '1'          # rehearsal: every rank on GPU 0
-    # the recurrence's hand-off timeout at 60 s instead of 2 s for every section: the same kernels (only the error
-    # deadline of a spin differs), but a transient device-wide stall — measured 1.5-26 s in round 5 on boxes that had
-    # just released a 100 GB replay, profiles/r5_replay_timeout.md — slows one step instead of failing the bench; a
-    # lost hand-off still errors, after 60 s
+    # the recurrence's hand-off deadline at 60 s instead of 2 s for every section: the same kernels (only the error
+    # deadline of a spin differs), so a transient device-wide stall on a shared box slows one step instead of failing
+    # the measurement (round 5's config-5 stalls had a cause in this code — high-priority actor streams — fixed, see
+    # profiles/r5_replay_timeout.md); a lost hand-off still errors, after 60 s
     os.environ.setdefault('DCA_TEAM_PATIENT', '1')
     device = torch.device(f'cuda:{0 if shared else local}' if use_cuda else 'cpu')
     if use_cuda:

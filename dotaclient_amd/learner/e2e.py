@@ -285,14 +285,10 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
 
     world, rank = pdist.get_world_size(), pdist.get_rank()
     local_world = int(os.environ.get('LOCAL_WORLD_SIZE', world))
-    # the recurrence's hand-off timeout (ops/csrc/lstm_team.hip spin_fail) is wall clock per wait: 2 s on a GPU of its
-    # own, 60 s here, where another process (the actor) allocates and launches on the same GPU. Measured round 5
-    # (profiles/r5_replay_timeout.md): config 5 with a 150 or 200 GB replay trips the 2 s limit within seconds of the
-    # loop's start (VRAM nearly full: the box showed 63 GB in use before the run), while the same 200 GB run under the
-    # 60 s limit completes with its slowest steady-state step at 26 ms — a transient device-wide stall of the
-    # memory-pressure kind (queue preemption while buffers move), not a lost hand-off. At 100 GB both limits pass.
-    # A real lost hand-off still errors, after 60 s.
-    os.environ.setdefault('DCA_TEAM_PATIENT', '1')
+    # (the recurrence keeps its default 2 s hand-off deadline beside the actor process: the multi-second stalls of
+    # round 5's config-5 loops came from the actor's HIGH-PRIORITY step streams — a league's opponent policies keep them
+    # busy and the persistent team kernel lost its CUs for seconds; with default-priority actor streams the e2e,
+    # config-5 and config-4 loops run clean at 2 s, profiles/r5_replay_timeout.md)
     if transport == 'auto':
         from .. import native
         transport = 'shm' if (local_world == world and native.AVAILABLE) else 'tcp'
