@@ -201,11 +201,10 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', '0'))
     use_cuda = torch.cuda.is_available()
     shared = os.environ.get('DCA_SHARED_GPU') == '1'          # rehearsal: every rank on GPU 0
-    # the recurrence's hand-off deadline at 60 s instead of 2 s for every section: the same kernels (only the error
-    # deadline of a spin differs), so a transient device-wide stall on a shared box slows one step instead of failing
-    # the measurement (round 5's config-5 stalls had a cause in this code — high-priority actor streams — fixed, see
-    # profiles/r5_replay_timeout.md); a lost hand-off still errors, after 60 s
-    os.environ.setdefault('DCA_TEAM_PATIENT', '1')
+    # the recurrence's hand-off deadline stays at its default 2 s (DCA_TEAM_PATIENT unset): round 5's multi-second
+    # device stalls had a cause in this code — the league's high-priority actor streams preempting the persistent
+    # recurrence, fixed (profiles/r5_replay_timeout.md) — so a stall now fails the section loudly instead of deflating
+    # its number; every node-loop section reports its slowest in-loop learner step (learner_gpu_ms_per_step_max)
     device = torch.device(f'cuda:{0 if shared else local}' if use_cuda else 'cpu')
     if use_cuda:
         torch.cuda.set_device(device)

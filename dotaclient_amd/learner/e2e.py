@@ -299,15 +299,14 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
     addr = None
     if rank == 0:
         if transport == 'shm':
-            from ..transport.shm import ShmBroker
-            from ..transport.shm import shm_free_bytes
+            from ..transport.shm import ShmBroker, ring_capacity_for, shm_free_bytes
             name = f'dca_e2e_{os.getpid()}_{int(time.time() * 1e3) % 10 ** 9}'
-            cap = ring_bytes * world
+            want = ring_bytes * world
             free = shm_free_bytes()
-            if free is not None and cap > free // 2:
-                # a small /dev/shm (container default 64 MB, or a node with little RAM): the ring takes at most half
-                # of it, at least 64 MB (whole-game rollouts are ≈1.35 MB)
-                cap = max(64 << 20, free // 2)
+            # a small /dev/shm (container default 64 MB, or a node with little RAM): the ring takes at most half of
+            # it and leaves the broker's headroom (one rule with ShmBroker's own check); too small fails here, clearly
+            cap = ring_capacity_for(want, free)
+            if cap < want:
                 say(f'e2e: /dev/shm has {free >> 20} MiB free: experience ring clamped to {cap >> 20} MiB')
             owner = ShmBroker(name, capacity=cap, create=True, drop_oldest=True)
             addr = f'shm://{name}'

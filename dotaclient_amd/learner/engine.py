@@ -6,14 +6,16 @@ optimizer is one fused HIP kernel pair.
 
 Backends for the model math:
 
-* ``'fused'`` (default on GPU): :class:`~dotaclient_amd.models.fused.FusedPolicy` — hand-written gfx950 HIP kernels
-  for the entity encoder, LSTM recurrence and heads+loss; plain GEMMs through hipBLASLt.
-* ``'torch'``: the eager reference model (``models.policy.Policy``): fp32, or under bf16 autocast on GPU with
-  ``precision='bf16'``.
+* ``'fused'`` (default on GPU): :class:`~dotaclient_amd.models.fused.FusedPolicy` — every product of the step in a
+  hand-written gfx950 HIP kernel (entity encoder, attention block, forward / ∂X chains, recurrence, heads + loss,
+  split-K weight-gradient GEMMs, clip + Adam); no vendor GEMM.
+* ``'torch'``: the eager reference model (``models.policy.Policy``, the oracle): fp32, or under bf16 autocast on GPU
+  with ``precision='bf16'`` (the only way a bf16 learner runs: the fused step has no bf16 branch).
 
-``precision`` (default ``'fp32'``, the reference's training precision — optimizer.py:281 trains the fp32 module):
-``'fp32'`` keeps activations, gradients and accumulation in fp32 (the fused kernels run bf16x3 split MFMA, see
-``models/fused.py``); ``'bf16'`` uses bf16 GEMM operands / saved activations with fp32 accumulation and optimizer.
+``precision``: ``'fp32-exact'`` — the reference's training precision (optimizer.py:281 trains the fp32 module) with
+every product an IEEE fp32 FMA; the default of the CLI, the presets and ``bench.py`` (``OptimizerConfig.precision``).
+``'fp32'`` (this class's default, kept for the many short-horizon tests) keeps activations, gradients and
+accumulation in fp32 with bf16x3-split MFMA operands (``models/fused.py``); ``'bf16'`` = torch backend under autocast.
 
 Batches are dicts of device tensors (see :func:`dotaclient_amd.learner.synthetic.make_batch` for the schema):
 ``env (B,S,3) f32``, ``units (B,S,U,10) f32``, ``actions``/``masks (B,S,A) u8`` (flat ``enum|x|y|target_unit``),

@@ -90,6 +90,17 @@ class _Stopped(Exception):
     pass
 
 
+class _ClaimsAbandoned(Exception):
+    """stage(): a ring-resident rollout's claim was abandoned by the ring while it was being copied."""
+
+
+def _claim_ok(r: Rollout) -> bool:
+    """Whether a rollout's bytes are still its own: True for heap rollouts, else the ring's verdict on its claim."""
+    rel = getattr(r, 'release', None)
+    valid = getattr(rel, 'valid', None)
+    return True if valid is None else bool(valid())
+
+
 def _zero_start(r: Rollout) -> bool:
     """A rollout whose recurrent state at its first step is zero (a game start): it may begin mid-sequence."""
     h = r.hiddens
@@ -184,6 +195,7 @@ class IngestPipeline:
         self.err: Optional[BaseException] = None
         self.stop = threading.Event()
         self.lost = 0
+        self.abandoned_iterations = 0          # iterations dropped because a zero-copy claim was abandoned mid-copy
         self._k = 0
         self.th = None
         if fetch is not None:
@@ -235,6 +247,11 @@ class IngestPipeline:
                     try:
                         st = self.stage(rollouts)
                         st.gather_s = tg
+                    except _ClaimsAbandoned:
+                        # (stage() gave every region back): the iteration is dropped, the stager gathers anew
+                        self.lost += len(rollouts)
+                        self.abandoned_iterations += 1
+                        continue
                     except _Stopped:
                         self.lost += len(rollouts)
                         _release_all(rollouts)
@@ -399,6 +416,15 @@ class IngestPipeline:
         # pinned slot now — give their ring regions back (the canvas of the last one is kept for the logs)
         mk('hid+reset')
         tr = time.perf_counter()
+        # a zero-copy claim held past the ring's abandonment deadline (native/core.h claim_abandon_s_, 60 s: a learner
+        # stalled that long while producers needed the space) may have been reclaimed and overwritten WHILE it was
+        # copied above — its CRC was checked at claim time, so nothing else would notice: drop the whole iteration
+        gone = sum(1 for r in rollouts if not _claim_ok(r))
+        if gone:
+            _release_all(rollouts)              # (the abandoned tokens' releases are ignored by the ring)
+            self._k -= 1                        # the slot was not used: the next stage takes it again
+            slot.free.release()
+            raise _ClaimsAbandoned(gone)
         rels = [rel for i, r in enumerate(rollouts)
                 if (rel := r.detach_shared(keep_canvas=i == len(rollouts) - 1, release=False)) is not None]
         if rels:

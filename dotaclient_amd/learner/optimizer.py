@@ -1068,6 +1068,11 @@ class _RingClaim:
             self.broker.release_experience(self.token)
             self.cb.give(self.n)
 
+    def valid(self) -> bool:
+        """Whether the claim still owns its ring region (False once the ring abandoned and reclaimed it)."""
+        f = getattr(self.broker, 'claim_valid', None)
+        return True if (f is None or self.done) else f(self.token)
+
     @staticmethod
     def release_all(claims):
         groups = {}

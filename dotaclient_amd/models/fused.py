@@ -26,12 +26,12 @@ Precision (``FusedPolicy(precision=...)``):
   product an IEEE fp32 FMA (``v_mfma_f32_16x16x4_f32`` / fp32 VALU), fp32 activations, gradients and accumulation.
 * ``'fp32'``: fp32 activations; the hand-written MFMA kernels split each fp32 operand into a hi and a lo bf16 and
   sum hi·hi + lo·hi + hi·lo (≈2⁻¹⁶ relative per product, "bf16x3").
-* ``'bf16'``: bf16 GEMM operands / saved activations, fp32 accumulation, recurrence state and optimizer.
+* ``'bf16'`` has no kernel path (:meth:`use_pipeline` is False): the learner runs it on the torch backend under bf16
+  autocast (learner/engine.py). The fused step has no vendor-GEMM branch.
 
-The 5v5 entity-attention block runs on its bf16 kernels (ops/csrc/attn.hip) in the bf16 learner and on the fp32
-block kernels (ops/csrc/attn_block.hip) in the fp32 learners: bf16x3 products at ``'fp32'``, their IEEE-fp32 twins
-(``v_mfma_f32_16x16x4_f32``) at ``'fp32-exact'``. Configurations the kernels do not cover (unit /
-env widths other than 128, the linear layer below fp32) run on the torch backend (learner/engine.py).
+The 5v5 entity-attention block runs on the fused block kernels (ops/csrc/attn_block.hip): bf16x3 products at
+``'fp32'``, their IEEE-fp32 twins (``v_mfma_f32_16x16x4_f32``) at ``'fp32-exact'``. Configurations the kernels do not
+cover (unit / env widths other than 128, bf16) run on the torch backend (learner/engine.py).
 """
 from __future__ import annotations
 
@@ -141,13 +141,13 @@ class FusedPolicy:
         return self._side
 
     def use_pipeline(self) -> bool:
-        """Whether the kernels cover this configuration (models/pipelined.py): the LSTM policies, or — at fp32 /
-        fp32-exact — the reference's linear fake_rnn layer with its VPG value quirk (the compat preset)."""
-        if not (self.fully_fused or self.attention_fused):
+        """Whether the kernels cover this configuration (models/pipelined.py): fp32 / fp32-exact, the LSTM policies or
+        the reference's linear fake_rnn layer with its VPG value quirk (the compat preset)."""
+        if not (self.fully_fused or self.attention_fused) or not self.fp32:
             return False
         if self.cfg.rnn == 'lstm':
-            return True
-        return self.fp32 and self.cfg.hidden % 128 == 0 and self.cfg.pre_rnn_dim == 256
+            return self.cfg.hidden % 128 == 0
+        return self.cfg.hidden % 128 == 0 and self.cfg.pre_rnn_dim == 256
 
     # Data-parallel split of the direct step (learner/engine.py): the learner sets ``split_hook`` to a callable
     # that the step calls once, at the point where every gradient of :meth:`early_param_names` is final.
@@ -164,8 +164,9 @@ class FusedPolicy:
     @property
     def chunks(self) -> int:
         import os
-        # 1 = no time-chunk overlap: measured on MI355X, GEMMs running concurrently on the other XCDs slow the
-        # L2-bound team recurrence by more than they save (bench 10.25 / 10.6 / 11.0 ms at 1 / 2 / 4 chunks)
+        # 1 = no time-chunk overlap: measured on MI355X, work running concurrently on the other XCDs slows the
+        # L2-bound team recurrence by more than it saves (profiles/r5_half_team.md: 5.45 ms at one chunk, 6.2-6.9 ms
+        # chunked)
         return int(os.environ.get('DCA_PIPELINE_CHUNKS', '1'))
 
     def gate_perm(self, H, device):

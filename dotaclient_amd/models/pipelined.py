@@ -19,9 +19,14 @@ Time chunks (``DCA_PIPELINE_CHUNKS`` > 1) software-pipeline the step over two st
     stream A (everything):     H0 H1 H2 H3            G3 G2 G1 G0
 
 ``F_c``/``B_c`` = team-LSTM forward/backward over chunk c, ``H_c`` = heads GEMM + heads/loss kernel + heads backward
-of chunk c, ``G_c`` = the weight gradients that depend on chunk c. Measured on MI355X it does not pay (GEMMs on the
-other XCDs slow the L2-bound recurrence more than they save: 10.25 / 10.6 / 11.0 ms per bench step at 1 / 2 / 4
-chunks), so the default is one chunk.
+of chunk c, ``G_c`` = the weight gradients that depend on chunk c. Measured on MI355X it does not pay: work on the
+other XCDs slows the L2-bound recurrence more than it saves (round 2: +3.5 % / +7 % per step at 2 / 4 chunks; round 5
+with CU-exclusive half teams: 5.45 ms at one chunk against 6.2-6.9 ms chunked, profiles/r5_half_team.md), so the
+default is one chunk.
+
+Precisions: ``fp32-exact`` (IEEE fp32 products) and ``fp32`` (fp32 activations, bf16x3-split MFMA operands). Every
+product of the step runs in a hand-written kernel — there is no vendor-GEMM branch; a bf16 learner runs on the torch
+backend (learner/engine.py).
 """
 from __future__ import annotations
 
@@ -40,16 +45,6 @@ DIRECT_GEMM_GRADS = ('rnn.weight_hh_l0', 'rnn.weight_ih_l0', 'affine_pre_rnn.wei
 
 METRIC_NAMES = ['loss', 'policy_loss', 'entropy_loss', 'advantage_loss', 'entropy', 'advantage', 'approx_kl',
                 'clipfrac', 'entropy/enum', 'entropy/x', 'entropy/y', 'entropy/target_unit']
-
-
-def _mm(a, b):
-    """GEMM with fp32 output: bf16 operands on hipBLASLt's bf16 path, fp32 operands on its fp32 path (fast bf16x3-class
-    mode inside :func:`fused_step_tm` for the fp32 learner, exact for fp32-exact)."""
-    return a @ b if a.dtype == torch.float32 else torch.mm(a, b, out_dtype=torch.float32)
-
-
-def _addmm(bias, a, b):
-    return torch.addmm(bias, a, b) if a.dtype == torch.float32 else torch.addmm(bias, a, b, out_dtype=torch.float32)
 
 
 def _frag_order(w: torch.Tensor) -> torch.Tensor:
@@ -80,7 +75,7 @@ class WeightImages:
     """Per-step working copies of the weights, produced by ONE ``weight_prep`` gather launch from the flat fp32
     parameter buffer (instead of ≈25 cast / stack / permute / cat launches):
 
-    GEMM operands (bf16 in the bf16 learner, fp32 in the fp32 learner — same keys): ``wt16`` (6,128,128) type
+    GEMM operands (fp32; the historical ``16`` suffix of the keys is kept): ``wt16`` (6,128,128) type
     weights, ``wtT16`` their transposes, ``wpre16`` (256,896) + ``bpre16``, ``wih16`` (4H,256) rows in unit-major
     gate order, ``whh16`` (4H,H), ``wcat16`` (LDZ,H) = [attention|enum|x|y|value|0-pad];
     always fp32: ``bt`` (6,128), ``bias4`` (4H) = (b_ih + b_hh) in unit-major gate order, ``bcat`` (LDZ).
@@ -133,20 +128,10 @@ class WeightImages:
             bo = idx('entity_attn.out.bias')
             parts32['bt'] = (parts32['bt'][0], bo.unsqueeze(0).expand(6, -1))
             parts32['bout'] = (bo, None)
-        if cfg.entity_attention and not getattr(fp, 'fp32', False):
-            # 5v5 attention block; the encoder adds b_τ + b_out (residual bias folded into E0, see attn.hip)
-            parts16['wqkv16'] = idx('entity_attn.qkv.weight')
-            parts16['bqkv16'] = idx('entity_attn.qkv.bias')
-            parts16['wout16'] = idx('entity_attn.out.weight')
-            bo = idx('entity_attn.out.bias')
-            parts32['bt'] = (parts32['bt'][0], bo.unsqueeze(0).expand(6, -1))
-            parts32['bout'] = (bo, None)
-            parts32['ln_g'] = (idx('entity_attn.ln.weight'), None)
-            parts32['ln_b'] = (idx('entity_attn.ln.bias'), None)
         partsS = {}
         if getattr(fp, 'fp32', False):
             # fp32 learner: the GEMM operand images are fp32 gathers too (the HIP kernels split them into bf16 hi/lo
-            # pairs themselves, hipBLASLt runs exact f32)
+            # pairs themselves)
             parts32.update({k: (v, None) for k, v in parts16.items()})
             parts16 = {}
             # bf16 hi / lo SLAB-MAJOR images [K/32][rows][32] of the chain kernels' weights (ops/csrc/dx_chain.hip):
@@ -243,17 +228,8 @@ class WeightImages:
 
 
 def fused_step_tm(fp, *args, **kw):
-    """:func:`_fused_step_tm` with torch's fp32 matmul mode pinned: exact in the IEEE-fp32 learner, the fast (bf16x3-
-    class) mode in the fp32 learner for the few torch GEMMs left (the multi-chunk heads products)."""
-    exact = getattr(fp, 'exact', False)
-    if not getattr(fp, 'fp32', False):
-        return _fused_step_tm(fp, *args, **kw)
-    prev = torch.backends.cuda.matmul.allow_tf32
-    torch.backends.cuda.matmul.allow_tf32 = not exact
-    try:
-        return _fused_step_tm(fp, *args, **kw)
-    finally:
-        torch.backends.cuda.matmul.allow_tf32 = prev
+    """:func:`_fused_step_tm`: every product on a hand-written kernel (no torch GEMM, so no matmul mode to pin)."""
+    return _fused_step_tm(fp, *args, **kw)
 
 
 def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], units_t, env_t, act_t, msk_t, adv_t,
@@ -288,19 +264,17 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     w1, b1 = P['affine_unit_basic_stats.weight'].detach(), P['affine_unit_basic_stats.bias'].detach()
     we, be = P['affine_env.weight'].detach(), P['affine_env.bias'].detach()
     wt16, wtT16, wpre16 = W['wt16'], W['wtT16'], W['wpre16']
-    wih16, whh16, wcat16 = W['wih16'], W.get('whh16'), W['wcat16']
-    bt, bias_p, bcat = W['bt'], W['bias4'], W['bcat']
+    wih16, whh16 = W['wih16'], W.get('whh16')
+    bt, bias_p = W['bt'], W['bias4']
     # ---- encoder, pre-RNN, input projection over all rows (row-parallel, fast)
     attn = cfg.entity_attention
-    f32 = bool(getattr(fp, 'fp32', False))    # fp32-accurate learner: fp32 activations, bf16x3 MFMA, exact-f32 GEMMs
-    adt = torch.float32 if f32 else torch.bfloat16
-    # (x896 / emb come back in the weights' dtype: bf16, or fp32 from the bf16x3 encoder)
-    # (exact: the IEEE-fp32 variant, ops/csrc/encoder.hip encoder_fwd_x_kernel)
+    assert getattr(fp, 'fp32', False), 'the fused step runs at fp32 / fp32-exact (bf16: torch backend)'
+    adt = torch.float32         # fp32 activations; bf16x3 MFMA operands (fp32) or IEEE-fp32 products (fp32-exact)
+    # (exact: the IEEE-fp32 encoder variant, ops/csrc/encoder.hip encoder_fwd_x_kernel)
     # time chunks with the 1v1 fp32 policies: the encoder and the forward chain run chunk by chunk, each chunk's
     # recurrence launched as soon as its input projection is ready (the next chunk's encoder runs beside it)
-    front = len(chunk_bounds(S, fp.chunks)) > 1 and f32 and not attn and not lin and reset_t is None
+    front = len(chunk_bounds(S, fp.chunks)) > 1 and not attn and not lin and reset_t is None
     enc_done: List[torch.cuda.Event] = []
-    attn32 = attn and f32
     if front:
         x896 = torch.empty(N, 896, device=dev)
         emb = torch.empty(N, U, 128, device=dev)
@@ -327,12 +301,10 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         xp4 = xp.view(S, B, H, 4)
     else:
         x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, wt16, bt, we, be, counts, bool(cfg.compat_bugs), exact=exact)
-        if attn32:
-            # 5v5 entity attention at fp32 (ops/csrc/attn.hip fp32 kernels: LayerNorm, bf16x3 attention core, pools; the
-            # QKV / out-projection GEMMs on hipBLASLt fp32). emb = E0' = E0 + b_out (bias folded into bt); the LayerNorm
-            # kernel also writes the copy of E0' its backward needs, so the out-projection accumulates onto emb in place
-            # (E1 = E0' + O·W_outᵀ) and the QKV GEMM runs without its bias epilogue (added by the attention kernels):
-            # 213 + 480 µs instead of 359 + 116 (copy, GEMM, bias pass) + 795 µs at N·U = 716 800 rows
+        if attn:
+            # 5v5 entity attention, ONE kernel (ops/csrc/attn_block.hip attn_block_fwd_f32_kernel): LayerNorm → QKV
+            # (bias added in the kernel) → 4-head self-attention → out-projection onto E0' = E0 + b_out (bias folded into
+            # bt) → pools / argmax of the attended embeddings; bf16x3 operands, or the IEEE-fp32 twin at fp32-exact
             toff = fp.type_offset_list()
             bqkv = P['entity_attn.qkv.bias'].detach()
             # one kernel per step; E0' stays untouched (the LayerNorm backward's input), E1 is a new tensor
@@ -350,36 +322,22 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
                 E0p, W['bout'], P['entity_attn.ln.weight'].detach(), P['entity_attn.ln.bias'].detach(), wq[0], wq[1],
                 bqkv, wo[0], wo[1], toff, x896, arg, bool(cfg.compat_bugs), 1e-5)
             emb = E1.view(N, U, 128)
-        elif attn:
-            # 5v5 entity attention (ops/csrc/attn.hip): emb = E0 + b_out here (bias folded into bt)
-            toff = fp.type_offset_list()
-            E0p = emb.view(N * U, 128)
-            Xn, ln_mu, ln_rs = C.ln_fwd(E0p, W['bout'], W['ln_g'], W['ln_b'], 1e-5)
-            QKV = torch.addmm(W['bqkv16'], Xn, W['wqkv16'].t())
-            Oat, lse = C.attn_fwd(QKV)
-            E1 = torch.addmm(E0p, Oat, W['wout16'].t())                 # residual + out-projection, bf16
-            arg = C.attn_pool(E1, toff, x896, bool(cfg.compat_bugs))    # pools of the attended embeddings
-            emb = E1.view(N, U, 128)
         elif cfg.compat_bugs:   # reference policy.py:127: enemy-tower pool = enemy-nonhero pool
             x896[:, 768:896] = x896[:, 512:640]
             arg[:, 5] = arg[:, 3]
-        # relu(x896·W_preᵀ + b) as ONE hipBLASLt GEMM with a bias+ReLU epilogue, bf16 (fp32) out (x16 > 0 ⟺ x > 0)
+        # the forward chain relu(x896·W_preᵀ + b)·W_ihᵀ in ONE kernel (ops/csrc/dx_chain.hip; x16 > 0 ⟺ x > 0)
         if exact:
             # IEEE-fp32 forward chain: the same kernel on v_mfma_f32_16x16x4_f32 with the fp32 weights as they are
             nil = wpre16.new_empty(0)
             x16, xp = C.pre_rnn_chain(x896, wpre16, nil, W['bpre16'], wih16, nil)
             xp4 = xp.view(S, B, H, 4) if not lin else None
-        elif f32:
+        else:
             if 'pre_s' in W:                 # hi / lo images from the step's weight_prep launch
                 fw1, fw2 = W['pre_s'], W['ih_s']
             else:
                 fw1, fw2 = C.split_bf16x2(wpre16, True), C.split_bf16x2(wih16, True)   # slab-major bf16 hi / lo images
             x16, xp = C.pre_rnn_chain(x896, fw1[0], fw1[1], W['bpre16'], fw2[0], fw2[1])
             xp4 = xp.view(S, B, H, 4) if not lin else None
-        else:
-            assert not lin, 'the linear recurrent layer runs on the fp32 chain kernels'
-            x16 = torch._addmm_activation(W['bpre16'], x896, wpre16.t())
-            xp4 = _mm(x16, wih16.t()).view(S, B, H, 4)      # the recurrence kernel adds the bias (bias4)
     if lin:
         # fake_rnn: h = pre·W_fᵀ + b_f (the chain kernel's second product) — no activation, no recurrence
         hs16 = xp.add_(bias_p).view(S, B, H)
@@ -394,10 +352,10 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     # recurrence zeroes h, c before a flagged step (forward) and stops the gradient there (backward)
     rst = reset_t.reshape(S, B) if reset_t is not None else None
     assert rst is None or one, 'packed sequences run as one time chunk'
-    assert one or not attn32, "the fp32 entity-attention step runs as one time chunk"
+    assert one or not attn, "the entity-attention step runs as one time chunk"
     if not one:
         dxh = torch.empty(S, B, H, device=dev)
-        z = torch.empty(N, LDZ, device=dev)
+        z = torch.empty(N, 256, device=dev)
         dtl = torch.empty(N, U, device=dev)
         logp = torch.empty(N, device=dev)
     dWcat = dbcat = None
@@ -426,44 +384,34 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             fwd_done.append(e)
     if lin:
         fwd_done.append(ready)
-    dx_w = None
-    if f32 and 'wpreT' in W:
-        # weight operands of the fused ∂X kernel, split once per step into bf16 hi/lo images (exact: fp32 as is);
-        # enqueued before the main stream waits on the forward recurrence, so they run beside it
-        if exact:
-            dx_w = (W['wihT16'], W['wihT16'].new_empty(0), W['wpreT'], W['wpreT'].new_empty(0))
-        elif 'dx1_s' in W:
-            dx_w = tuple(W['dx1_s']) + tuple(W['dx2_s'])
-        else:
-            dx_w = tuple(C.split_bf16x2(W['wihT16'], True)) + tuple(C.split_bf16x2(W['wpreT'], True))
+    # weight operands of the fused ∂X kernel: bf16 hi/lo images from the step's weight_prep (exact: fp32 as is)
+    if exact:
+        dx_w = (W['wihT16'], W['wihT16'].new_empty(0), W['wpreT'], W['wpreT'].new_empty(0))
+    elif 'dx1_s' in W:
+        dx_w = tuple(W['dx1_s']) + tuple(W['dx2_s'])
+    else:
+        dx_w = tuple(C.split_bf16x2(W['wihT16'], True)) + tuple(C.split_bf16x2(W['wpreT'], True))
     # heads GEMM + its ∂X product on the chain kernel's stages (bf16x3 images, or exact: fp32 W_cat padded to 256)
-    if exact and 'wcat256' in W:
+    if exact:
         nil = W['wcat256'].new_empty(0)
         hw = ((W['wcat256'], nil), (W['wcatT256'], nil), W['bcat256'])
-    elif 'wcat_s' in W:
-        hw = (W['wcat_s'], W['wcatT_s'], W['bcat256'])
     else:
-        hw = None
-    rowmm = one and f32 and hw is not None
+        hw = (W['wcat_s'], W['wcatT_s'], W['bcat256'])
     for (t0, t1), done in zip(spans, fwd_done):
         main.wait_event(done)
         r0, r1 = t0 * B, t1 * B
         xh = hs16[t0:t1].view(-1, H)
-        if rowmm:
-            zc = C.rowmm_out256(xh, hw[0][0], hw[0][1], hw[2])   # (n, 256), padding columns 0
-        else:
-            zc = _addmm(bcat, xh, wcat16.t())     # bias in the GEMM epilogue
-        # ∂L/∂z straight in the GEMM operand dtype: only the backward GEMMs read it
+        zc = C.rowmm_out256(xh, hw[0][0], hw[0][1], hw[2])   # (n, 256), padding columns 0
         dz16, dtl_c, part, lp = C.heads_loss(zc, emb[r0:r1], act_t[r0:r1], msk_t[r0:r1], adv_t[r0:r1],
                                              ret_t[r0:r1], lpo_t[r0:r1], nret_t[r0:r1], norms, algo,
                                              bool(lc.compat_value_bug), S, B, float(lc.clip_eps),
-                                             float(lc.entropy_coef), float(lc.vf_coef), dz_bf16=not f32,
+                                             float(lc.entropy_coef), float(lc.vf_coef), dz_bf16=False,
                                              precise=exact)
         parts.append(part)
         first = dWcat is None
         if first:
             dbcat = torch.empty(LDZ, device=dev)
-        dzw = dz16[:, :LDZ] if rowmm else dz16           # (the heads' columns of the 256-wide ∂z)
+        dzw = dz16[:, :LDZ]                              # (the heads' columns of the 256-wide ∂z)
         if one:
             # single chunk: the heads' weight gradient waits on the recurrence stream behind the backward
             # recurrence (off the path between the two recurrences; joined with the other weight gradients)
@@ -473,15 +421,12 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             dWcat = gemm_tn(dzw, xh, out=dWcat, accumulate=not first, colsum=dbcat)
         if one:
             z, dtl, logp = zc, dtl_c, lp
-            if rowmm:
-                dxh = C.rowmm_in256(dz16, hw[1][0], hw[1][1]).view(S, B, H)
-            else:
-                dxh = _mm(dz16, wcat16).view(S, B, H)
+            dxh = C.rowmm_in256(dz16, hw[1][0], hw[1][1]).view(S, B, H)
         else:
             z[r0:r1].copy_(zc)
             dtl[r0:r1].copy_(dtl_c)
             logp[r0:r1].copy_(lp)
-            dxh[t0:t1].copy_(_mm(dz16, wcat16).view(t1 - t0, B, H))
+            dxh[t0:t1].copy_(C.rowmm_in256(dz16, hw[1][0], hw[1][1]).view(t1 - t0, B, H))
     heads_done = torch.cuda.Event()
     heads_done.record(main)
     # ---- backward recurrence on stream L (reverse chunks), weight gradients per chunk on the main stream
@@ -494,7 +439,6 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     dgates16 = None if lin else torch.empty(S, B, H, 4, dtype=adt, device=dev)   # ∂gates straight from the kernel
     db = dw1 = db1 = dWt = dbt = dWe = dbe = None
     dgam = dbet = None
-    first_attn = True
     side_after: List = []                # side-stream work enqueued after the encoder backward (5v5 fused path)
     after_enc: List = []                 # main-stream work enqueued after the encoder backward (exact ∂W_pre)
     if attn:
@@ -523,7 +467,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         for t0, t1 in ([] if lin else reversed(spans)):
             cinit = c0.contiguous() if t0 == 0 else cs[t0 - 1]
             o = team_bwd(C, dxh[t0:t1], gates4[t0:t1], cs[t0:t1], cinit, dh_n, dc_n, whh16, fp.err,
-                         time_major=True, dg_out=dgates16[t0:t1], dg_bf16=not f32,
+                         time_major=True, dg_out=dgates16[t0:t1], dg_bf16=False,
                          want_dbias=True, reset=rst)
             dh_n, dc_n = o[1], o[2]
             db = _acc(db, o[3])
@@ -559,13 +503,8 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
                 gemm_tn(dG16, x16[r0:r1], out=dWih, colsum=dbf)
             else:
                 gemm_tn(dG16, x16[r0:r1], out=dWih, perm=gperm, accumulate=True)
-        fused_dx = dx_w is not None
-        if fused_dx:
-            # ∂pre = (∂G·W_ih)⊙[x16 > 0] and ∂x896 = ∂pre·W_pre in one launch (the ∂pre tile stays in LDS)
-            dpre16, dx896 = C.dpre_dx(dG16, dx_w[0], dx_w[1], x16[r0:r1], dx_w[2], dx_w[3])
-        else:
-            # ∂pre-activation of the pre-RNN layer: one GEMM (bf16 or exact f32), ReLU mask in one threshold_backward
-            dpre16 = torch.ops.aten.threshold_backward(torch.mm(dG16, W['wihT16'].t()), x16[r0:r1], 0)
+        # ∂pre = (∂G·W_ih)⊙[x16 > 0] and ∂x896 = ∂pre·W_pre in one launch (the ∂pre tile stays in LDS)
+        dpre16, dx896 = C.dpre_dx(dG16, dx_w[0], dx_w[1], x16[r0:r1], dx_w[2], dx_w[3])
         pre_main = wg_side and split is None and exact
         if pre_main:
             with torch.cuda.stream(sL):       # the side stream ends with ∂W_ih
@@ -581,8 +520,6 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
                 wg_done.record(sL)
         else:
             gemm_tn(dpre16, x896[r0:r1], out=dWpre, accumulate=True, colsum=dbpre)
-        if not fused_dx:
-            dx896 = _mm(dpre16, wpre16)
         if split is not None:
             if wg_done is not None:
                 main.wait_event(wg_done)
@@ -599,7 +536,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             split()
             split = None
         demb_in = None
-        if attn32:
+        if attn:
             # one kernel from ∂x896 / the pointer gradient to ∂E0; the two weight-gradient GEMMs over the N·U unit
             # rows (∂W_out = ∂E1ᵀ·O, ∂W_qkv = ∂QKVᵀ·Xn, with their bias column sums) go to the recurrence stream
             if exact:
@@ -623,20 +560,6 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             else:
                 dWout = gemm_tn(dE1, Oat, colsum=dbout)
                 dWqkv = gemm_tn(dQKV, Xn, colsum=dbqkv)
-        elif attn:
-            # attention block backward over this chunk's rows (unit rows r0·U … r1·U)
-            a0, a1 = r0 * U, r1 * U
-            dE1 = C.attn_demb(dtl[r0:r1], z[r0:r1], dx896, arg[r0:r1], toff, bool(cfg.compat_bugs), False)
-            gemm_tn(dE1, Oat[a0:a1], out=dWout, accumulate=not first_attn, colsum=dbout)
-            dO = torch.mm(dE1, W['wout16'])
-            dQKV = C.attn_bwd(QKV[a0:a1], Oat[a0:a1], dO, lse[r0:r1])
-            gemm_tn(dQKV, Xn[a0:a1], out=dWqkv, accumulate=not first_attn, colsum=dbqkv)
-            dXn = torch.mm(dQKV, W['wqkv16'])
-            demb_in, dg_c, dbe_c_, dbt_attn = C.ln_bwd(dXn, E0p[a0:a1], W['bout'], W['ln_g'], ln_mu[a0:a1],
-                                                       ln_rs[a0:a1], dE1, fp.unit_types(dev))
-            dgam = _acc(dgam, dg_c)
-            dbet = _acc(dbet, dbe_c_)
-            first_attn = False
         # ∂b_τ, ∂W_env, ∂b_env: one pass over the rows (ops/csrc/glue.hip enc_small_grads); single chunk: on the
         # recurrence stream, concurrent with the encoder backward
         def small_grads():

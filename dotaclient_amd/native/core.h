@@ -313,11 +313,13 @@ struct RingHeader {
   uint64_t free_off;   // oldest byte still in use; [free_off, head) holds messages being read or done
   uint64_t stuck_off;  // a claimed region seen blocking the reclaim at free_off, and since when (CLOCK_MONOTONIC ns)
   uint64_t stuck_ns;
+  uint64_t wstuck_off; // the message at head seen still being written, and since when (CLOCK_MONOTONIC ns): shared by
+  uint64_t wstuck_ns;  // every consumer call, so short polling claims add up to the writer-abandonment time
   pthread_mutex_t mu;
   pthread_cond_t not_empty;
   pthread_cond_t not_full;
 };
-constexpr uint64_t kMagic = 0x444341524e473033ull;   // "DCARNG03"
+constexpr uint64_t kMagic = 0x444341524e473034ull;   // "DCARNG04"
 
 void deadline_in(double seconds, timespec& ts) {
   clock_gettime(CLOCK_REALTIME, &ts);
@@ -335,7 +337,9 @@ class RingCore {
   static constexpr uint64_t kLenMask = (1ull << 56) - 1;
   static constexpr uint64_t kWrap = ~0ull;
   // a producer that reserved a region and never committed it (it died mid-copy) is skipped after this long
-  static constexpr double kAbandonS = 30.0;
+  // (set_writer_abandon: tests)
+  double writer_abandon_s_ = 30.0;
+  void set_writer_abandon(double s) { writer_abandon_s_ = s; }
   // a claimed region that blocks the reclaim (its consumer died, or holds it) is given up after this long when a
   // producer needs the space (set_claim_abandon: tests); its late release is then ignored (claim tokens are
   // monotonic offsets, below free_off once reclaimed)
@@ -387,17 +391,21 @@ class RingCore {
   void unlock() { pthread_mutex_unlock(&hdr_->mu); }
 
   bool push(const char* msg_data, size_t msg_size, double timeout, bool drop_oldest) {
-    uint64_t pos;
-    if (!reserve(msg_size, timeout, drop_oldest, &pos)) return false;
+    uint64_t pos, tok;
+    if (!reserve(msg_size, timeout, drop_oldest, &pos, &tok)) return false;
     std::memcpy(data_ + pos + 8, msg_data, msg_size);     // outside the lock
-    return commit(pos, msg_size);
+    return commit(pos, msg_size, tok);
   }
 
   // producer side in two steps: reserve a region for msg_size bytes (writable at wpayload(pos) without the lock),
-  // then commit it. False from reserve: no space within the timeout; false from commit: the region was given up as
-  // abandoned (kAbandonS) and the message is lost.
+  // then commit it with the reservation's token (the message's monotonic offset). False from reserve: no space
+  // within the timeout; false from commit: the region was given up as abandoned (writer_abandon_s_) and the message
+  // is lost.
   uint8_t* wpayload(uint64_t pos) { return data_ + pos + 8; }
-  bool reserve(size_t msg_size, double timeout, bool drop_oldest, uint64_t* pos_out) {
+  // true when msg_size bytes can never fit (reserve would throw): callers on worker threads count such a message as
+  // lost instead of letting the exception escape the thread
+  bool too_large(size_t msg_size) const { return padded(msg_size) + 8 > hdr_->capacity || msg_size > kLenMask; }
+  bool reserve(size_t msg_size, double timeout, bool drop_oldest, uint64_t* pos_out, uint64_t* token_out) {
     const uint64_t need = padded(msg_size);
     if (need + 8 > hdr_->capacity || msg_size > kLenMask) throw std::invalid_argument("message larger than ring");
     timespec ts;
@@ -416,6 +424,7 @@ class RingCore {
         }
         const uint64_t p = hdr_->tail % cap;
         set_word(p, (kWriting << 56) | (uint64_t)msg_size);
+        *token_out = hdr_->tail;
         hdr_->tail += need;
         hdr_->count += 1;
         unlock();
@@ -439,9 +448,14 @@ class RingCore {
       }
     }
   }
-  bool commit(uint64_t pos, size_t msg_size) {
+  // The token, not the ring position, identifies the message: a writer skipped as abandoned (writer_abandon_s_) has
+  // its region reclaimed, and a NEW producer may reserve the same position with the same size — the old writer's late
+  // commit must not mark that half-written region ready. A skipped message lies below head (consumers moved past
+  // it); a live one never does.
+  bool commit(uint64_t pos, size_t msg_size, uint64_t token) {
     lock();
-    const bool ok = word_at(pos) == ((kWriting << 56) | (uint64_t)msg_size);   // (else given up as abandoned)
+    const bool ok = token >= hdr_->head && token % hdr_->capacity == pos &&
+                    word_at(pos) == ((kWriting << 56) | (uint64_t)msg_size);   // (else given up as abandoned)
     if (ok) set_word(pos, (kReady << 56) | (uint64_t)msg_size);
     pthread_cond_broadcast(&hdr_->not_empty);
     pthread_cond_broadcast(&hdr_->not_full);   // a drop_oldest producer may be waiting for this commit
@@ -468,6 +482,20 @@ class RingCore {
   // is the message's monotonic offset: a release that arrives after its region was abandoned and reclaimed
   // (token < free_off) is ignored instead of touching whatever message occupies that position now.
   const uint8_t* payload(uint64_t pos) const { return data_ + pos + 8; }
+  // whether the claim `token` still owns its region: false once it was abandoned (claim_abandon_s_) and reclaimed —
+  // a producer may then have overwritten the bytes. A zero-copy consumer checks this AFTER copying a claimed message
+  // out (the CRC was checked at claim time) and drops what it copied when the claim is gone.
+  bool claim_valid(uint64_t token) {
+    lock();
+    bool ok = token >= hdr_->free_off && token < hdr_->head;
+    if (ok) {
+      uint64_t off = token;
+      const uint64_t pos = resolve(off);
+      ok = off == token && (word_at(pos) >> 56) == kReading;
+    }
+    unlock();
+    return ok;
+  }
   void release(uint64_t token) { release_many(&token, 1); }
   // several claimed regions given back under ONE lock acquisition and one wake-up of the producers
   void release_many(const uint64_t* tokens, size_t n) {
@@ -492,8 +520,6 @@ class RingCore {
   bool claim(uint64_t* pos_out, uint64_t* len_out, double timeout, uint64_t* token_out = nullptr) {
     timespec ts;
     if (timeout > 0) deadline_in(timeout, ts);
-    uint64_t stuck_at = ~0ull;          // head offset seen in the writing state, and since when
-    timespec stuck_since{};
     lock();
     while (true) {
       if (hdr_->count > 0) {
@@ -512,17 +538,14 @@ class RingCore {
           return true;
         }
         // the oldest message is still being written: wait for its commit; a producer that never commits (it died
-        // mid-copy) is skipped after kAbandonS (its late commit then fails, push() returns false)
-        timespec now;
-        clock_gettime(CLOCK_MONOTONIC, &now);
-        if (stuck_at != off) {
-          stuck_at = off;
-          stuck_since = now;
-        } else if ((now.tv_sec - stuck_since.tv_sec) + 1e-9 * (now.tv_nsec - stuck_since.tv_nsec) > kAbandonS) {
+        // mid-copy) is skipped after writer_abandon_s_ — measured across calls (the header's wstuck clock), since
+        // consumers poll in short claims — and its late commit then fails (commit checks the token against head)
+        if (writer_stuck_locked(off)) {
           set_word(pos, (kDone << 56) | len);
           hdr_->head = off + padded(len);
           hdr_->count -= 1;
           hdr_->dropped += 1;
+          hdr_->wstuck_ns = 0;
           reclaim_locked();
           pthread_cond_broadcast(&hdr_->not_full);
           continue;
@@ -532,7 +555,7 @@ class RingCore {
       // bounded waits while a writer is mid-copy, so the abandonment clock above is re-checked
       timespec wt;
       if (hdr_->count > 0) {
-        deadline_in(1.0, wt);
+        deadline_in(std::min(1.0, std::max(0.01, writer_abandon_s_)), wt);
         if (timeout > 0 && (ts.tv_sec < wt.tv_sec || (ts.tv_sec == wt.tv_sec && ts.tv_nsec < wt.tv_nsec))) wt = ts;
       } else if (timeout > 0) {
         wt = ts;
@@ -544,11 +567,12 @@ class RingCore {
         timespec now;
         clock_gettime(CLOCK_REALTIME, &now);
         if (now.tv_sec > ts.tv_sec || (now.tv_sec == ts.tv_sec && now.tv_nsec >= ts.tv_nsec)) {
-          // one last look (a commit may have landed with the timeout)
+          // one last look (a commit may have landed with the timeout, or the writer's time ran out)
           if (hdr_->count > 0) {
             uint64_t off = hdr_->head;
             const uint64_t pos = resolve(off);
-            if ((word_at(pos) >> 56) == kReady) continue;
+            const uint64_t st = word_at(pos) >> 56;
+            if (st == kReady || (st == kWriting && writer_stuck_locked(off, false))) continue;
           }
           break;
         }
@@ -574,6 +598,21 @@ class RingCore {
       return 0;
     }
     return pos;
+  }
+  // whether the message being written at monotonic offset `off` (the head) has been for writer_abandon_s_; starts
+  // its clock on first sight (`arm`)
+  bool writer_stuck_locked(uint64_t off, bool arm = true) {
+    timespec now;
+    clock_gettime(CLOCK_MONOTONIC, &now);
+    const uint64_t ns = (uint64_t)now.tv_sec * 1000000000ull + (uint64_t)now.tv_nsec;
+    if (hdr_->wstuck_off != off || hdr_->wstuck_ns == 0) {
+      if (arm) {
+        hdr_->wstuck_off = off;
+        hdr_->wstuck_ns = ns;
+      }
+      return false;
+    }
+    return (double)(ns - hdr_->wstuck_ns) * 1e-9 > writer_abandon_s_;
   }
   // a claimed region at free_off that has blocked the reclaim for claim_abandon_s_ (the same region, seen by the
   // producers waiting for space): given up — marked done and counted as dropped — so a consumer that died holding

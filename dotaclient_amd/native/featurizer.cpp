@@ -166,6 +166,10 @@ class ShmRing {
     return py::make_tuple(arr, token);
   }
   void set_claim_abandon(double seconds) { r_.set_claim_abandon(seconds); }
+  bool claim_valid(uint64_t token) {
+    py::gil_scoped_release rel;
+    return r_.claim_valid(token);
+  }
   void release(uint64_t token) {
     py::gil_scoped_release rel;
     r_.release(token);
@@ -577,6 +581,8 @@ PYBIND11_MODULE(_native, m) {
       .def("release", &ShmRing::release, py::arg("token"))
       .def("release_many", &ShmRing::release_many, py::arg("tokens"))
       .def("set_claim_abandon", &ShmRing::set_claim_abandon, py::arg("seconds"))
+      .def("claim_valid", &ShmRing::claim_valid, py::arg("token"),
+           "whether a zero-copy claim still owns its region (False once abandoned and reclaimed)")
       .def("size", &ShmRing::size)
       .def("dropped", &ShmRing::dropped)
       .def_static("unlink", &ShmRing::unlink);

@@ -162,6 +162,38 @@ static int check_ring() {
   return 0;
 }
 
+// A writer skipped as abandoned must not be able to commit into the region a NEW producer reserved at the same ring
+// position with the same size (commit checks the reservation's monotonic token, not the position + size word).
+static int check_stale_commit() {
+  const std::string name = "/dca_sanitize_sc_" + std::to_string((long)getpid());
+  RingCore::unlink(name);
+  {
+    RingCore ring(name, 224, true);       // two 112-byte slots (8-byte word + 104-byte padded payload of 100 bytes)
+    ring.set_writer_abandon(0.05);
+    const std::string a(100, 'a'), b(100, 'b'), c(100, 'c');
+    uint64_t pa, ta, pos, len, tok;
+    if (!ring.reserve(100, 1.0, false, &pa, &ta)) return fail("stale-commit: reserve A");
+    // writer A stalls; the consumer skips its region after the abandonment time (nothing else to claim)
+    if (ring.claim(&pos, &len, 0.3, &tok)) return fail("stale-commit: claimed an uncommitted message");
+    // B1 fills the second slot and is consumed; B2 wraps to A's position with A's size
+    if (!ring.push(b.data(), b.size(), 1.0, false)) return fail("stale-commit: push B1");
+    std::string m;
+    if (!ring.pop(&m, 1.0) || m != b) return fail("stale-commit: pop B1");
+    uint64_t p2, t2;
+    if (!ring.reserve(100, 1.0, false, &p2, &t2)) return fail("stale-commit: reserve B2");
+    if (p2 != pa || t2 == ta) return fail("stale-commit: B2 did not reuse A's position");
+    std::memcpy(ring.wpayload(pa), a.data(), a.size());   // A's late copy ...
+    if (ring.commit(pa, 100, ta)) return fail("stale-commit: A's late commit was accepted");
+    if (ring.claim(&pos, &len, 0.0, &tok)) return fail("stale-commit: B2's half-written region became ready");
+    std::memcpy(ring.wpayload(p2), c.data(), c.size());
+    if (!ring.commit(p2, 100, t2)) return fail("stale-commit: B2's commit refused");
+    if (!ring.pop(&m, 1.0) || m != c) return fail("stale-commit: B2's message");
+  }
+  RingCore::unlink(name);
+  std::printf("ring: stale commit of a skipped writer refused\n");
+  return 0;
+}
+
 int main(int argc, char** argv) {
   if (argc < 2) return fail("usage: sanitize <seed_file> [iterations]");
   const int iters = argc > 2 ? std::atoi(argv[2]) : 20000;
@@ -169,6 +201,7 @@ int main(int argc, char** argv) {
   if (seeds.empty()) return fail("no seeds");
   if (check_decoder(seeds, iters)) return 1;
   if (check_ring()) return 1;
+  if (check_stale_commit()) return 1;
   const char* kat = "123456789";
   if (crc32c_raw((const uint8_t*)kat, 9) != 0xE3069283u) return fail("crc32c known answer");
   std::printf("crc32c ok\nall sanitizer checks passed\n");

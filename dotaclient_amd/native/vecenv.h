@@ -1165,13 +1165,14 @@ class VecEnv {
       const std::string h = dcx2_header(g.game_id, p.team, p.player_id, version, bootstrap, done,
                                         t.hiddens.empty() ? 0 : cfg_.hidden_stride, cfg_.counts, arr, &ab);
       const size_t n = dcx2_size(h, ab);
-      uint64_t pos;
-      if (!sink_->reserve(n, sink_timeout_, sink_drop_, &pos)) {
+      uint64_t pos, tok;
+      // (a rollout larger than the whole ring is lost, not thrown: this runs on a Pool worker thread)
+      if (sink_->too_large(n) || !sink_->reserve(n, sink_timeout_, sink_drop_, &pos, &tok)) {
         sink_lost_ += 1;
         return;
       }
       dcx2_write(sink_->wpayload(pos), h, arr);
-      if (!sink_->commit(pos, n)) {
+      if (!sink_->commit(pos, n, tok)) {
         sink_lost_ += 1;
         return;
       }

@@ -589,7 +589,10 @@ std::vector<torch::Tensor> attn_block_fwd(torch::Tensor e0, torch::Tensor bout, 
   return {xn, mu, rs, qkv, o, lse, e1};
 }
 
-static void check_type_off(const std::vector<int64_t>& t);
+static void check_type_off(const std::vector<int64_t>& t) {
+  TORCH_CHECK(t.size() == 7 && t[0] == 0 && t[6] == 64, "type offsets must be 7 values from 0 to 64");
+  for (int i = 0; i < 6; ++i) TORCH_CHECK(t[i + 1] >= t[i], "type offsets must be non-decreasing");
+}
 
 // Fused fp32 entity-attention block backward (attn_block.hip). q = the heads' z rows (row stride q.stride(0)), dx =
 // ∂x896; o / qkv / lse / mu / rs from attn_block_fwd, e0 = E0' (N·64, 128); W_outᵀ images in 16x16x32 fragment
@@ -660,7 +663,7 @@ std::vector<torch::Tensor> attn_block_bwd(torch::Tensor dtl, torch::Tensor q, to
 void returns_scan(torch::Tensor rew, torch::Tensor val, torch::Tensor off, torch::Tensor seglen, torch::Tensor boot,
                   torch::Tensor done, torch::Tensor keys, torch::Tensor ema, torch::Tensor ret, torch::Tensor adv,
                   torch::Tensor norm, torch::Tensor stats, int64_t mode, bool normalize, double gamma, double lam,
-                  double factor, double eps) {
+                  double factor, double eps, c10::optional<torch::Tensor> lr, double rho_bar, double c_bar) {
   CHECK_F32(rew); CHECK_F32(ema); CHECK_F32(ret); CHECK_F32(adv); CHECK_F32(norm); CHECK_F32(stats);
   TORCH_CHECK(rew.dim() == 2, "rew must be (L, K)");
   const int64_t L = rew.size(0);
@@ -674,13 +677,20 @@ void returns_scan(torch::Tensor rew, torch::Tensor val, torch::Tensor off, torch
   TORCH_CHECK(ret.numel() == L && adv.numel() == L && norm.numel() == L && stats.numel() == 2 * nseg,
               "returns_scan: output lengths");
   TORCH_CHECK(ema.dim() == 2 && ema.size(1) == 3, "ema must be (n_keys, 3)");
-  TORCH_CHECK(mode == 0 || mode == 1, "mode must be 0 (discount) or 1 (gae)");
+  TORCH_CHECK(mode == 0 || mode == 1 || mode == 2, "mode must be 0 (discount), 1 (gae) or 2 (v-trace gae)");
   TORCH_CHECK(rew.size(1) <= 64, "returns_scan: at most 64 sub-rewards");
   const float* vp = nullptr;
-  if (mode == 1) {
+  const float* lp = nullptr;
+  if (mode >= 1) {
     CHECK_F32(val);
     TORCH_CHECK(val.numel() == L, "returns_scan: values must have one entry per row");
     vp = ptr<float>(val);
+  }
+  if (mode == 2) {
+    TORCH_CHECK(lr.has_value() && lr->defined(), "returns_scan: v-trace needs the per-row log ratios");
+    CHECK_F32((*lr));
+    TORCH_CHECK(lr->numel() == L, "returns_scan: log ratios must have one entry per row");
+    lp = ptr<float>(*lr);
   }
   if (nseg == 0) return;
   const int* o = off.data_ptr<int>();
@@ -706,11 +716,12 @@ void returns_scan(torch::Tensor rew, torch::Tensor val, torch::Tensor off, torch
   auto md = meta.to(rew.device(), /*non_blocking=*/true);
   int* d = md.data_ptr<int>();
   auto ema_out = ema.clone();
-  hip_check(dca_returns(ptr<float>(rew), (int)rew.size(1), vp, d, d + nseg + 1, reinterpret_cast<float*>(d + 3 * nseg + 1),
-                        reinterpret_cast<unsigned char*>(d + 4 * nseg + 1), d + 2 * nseg + 1, nseg, max_len,
-                        ptr<float>(ret), ptr<float>(adv), ptr<float>(norm), ptr<float>(stats), ptr<float>(ema),
-                        ptr<float>(ema_out), (int)mode, normalize ? 1 : 0, (float)gamma, (float)lam, (float)factor,
-                        (float)eps, cur_stream()),
+  hip_check(dca_returns(ptr<float>(rew), (int)rew.size(1), vp, lp, d, d + nseg + 1,
+                        reinterpret_cast<float*>(d + 3 * nseg + 1), reinterpret_cast<unsigned char*>(d + 4 * nseg + 1),
+                        d + 2 * nseg + 1, nseg, max_len, ptr<float>(ret), ptr<float>(adv), ptr<float>(norm),
+                        ptr<float>(stats), ptr<float>(ema), ptr<float>(ema_out), (int)mode, normalize ? 1 : 0,
+                        (float)gamma, (float)lam, (float)rho_bar, (float)c_bar, (float)factor, (float)eps,
+                        cur_stream()),
             "dca_returns");
   ema.copy_(ema_out);
 }
@@ -999,145 +1010,6 @@ std::vector<torch::Tensor> pre_rnn_chain(torch::Tensor x896, torch::Tensor w1h, 
   return {x, xp};
 }
 
-// ---- 5v5 entity-attention block (ops/csrc/attn.hip); 64 unit slots, width 128, 4 heads × 32 -------------------
-std::vector<torch::Tensor> ln_fwd(torch::Tensor e0, torch::Tensor bsub, torch::Tensor gamma, torch::Tensor beta,
-                                  double eps, c10::optional<torch::Tensor> e0_copy) {
-  // bf16 learner: bf16 E0' with b_sub; fp32 learner: fp32 E0, b_sub an empty tensor (no subtraction)
-  const bool f32 = e0.scalar_type() == at::kFloat;
-  if (f32) { CHECK_F32(e0); } else { CHECK_BF16(e0); }
-  CHECK_F32(gamma); CHECK_F32(beta);
-  if (bsub.numel()) { CHECK_F32(bsub); }
-  TORCH_CHECK(e0.size(-1) == 128 && (bsub.numel() == 128 || (f32 && bsub.numel() == 0)) && gamma.numel() == 128 &&
-              beta.numel() == 128, "ln_fwd");
-  const int64_t R = e0.numel() / 128;
-  auto xn = torch::empty({R, 128}, e0.options());
-  auto mean = torch::empty({R}, gamma.options());
-  auto rstd = torch::empty({R}, gamma.options());
-  void* cp = nullptr;
-  if (e0_copy.has_value() && e0_copy->defined()) {
-    TORCH_CHECK(e0_copy->scalar_type() == e0.scalar_type() && e0_copy->is_contiguous() && e0_copy->numel() == R * 128,
-                "e0_copy must be a contiguous tensor like e0");
-    cp = e0_copy->data_ptr();
-  }
-  hip_check(dca_ln_fwd(e0.data_ptr(), bsub.numel() ? ptr<float>(bsub) : nullptr, ptr<float>(gamma), ptr<float>(beta),
-                       xn.data_ptr(), ptr<float>(mean), ptr<float>(rstd), (int)R, (float)eps, f32 ? 1 : 0, cp,
-                       cur_stream()),
-            "dca_ln_fwd");
-  return {xn, mean, rstd};
-}
-
-// fp32 variants: qkv WITHOUT its bias (the kernels add bqkv on load; zeros when absent)
-static torch::Tensor qkv_bias(const torch::Tensor& qkv, const c10::optional<torch::Tensor>& bqkv) {
-  if (bqkv.has_value() && bqkv->defined()) {
-    CHECK_F32((*bqkv));
-    TORCH_CHECK(bqkv->numel() == 384, "bqkv must hold 384 floats");
-    return *bqkv;
-  }
-  return torch::zeros({384}, qkv.options().dtype(at::kFloat));
-}
-
-std::vector<torch::Tensor> attn_fwd(torch::Tensor qkv, c10::optional<torch::Tensor> bqkv) {
-  TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) == 384 && qkv.size(0) % 64 == 0, "qkv must be (N*64, 384)");
-  const int N = qkv.size(0) / 64;
-  auto o = torch::empty({(int64_t)N * 64, 128}, qkv.options());
-  auto lse = torch::empty({(int64_t)N, 4, 64}, qkv.options().dtype(at::kFloat));
-  if (qkv.scalar_type() == at::kFloat) {   // fp32 learner: bf16x3 split-MFMA kernel
-    CHECK_F32(qkv);
-    auto b = qkv_bias(qkv, bqkv);
-    hip_check(dca_attn_fwd_f32(ptr<float>(qkv), ptr<float>(b), ptr<float>(o), ptr<float>(lse), N, 1.f / sqrtf(32.f),
-                               cur_stream()),
-              "dca_attn_fwd_f32");
-    return {o, lse};
-  }
-  TORCH_CHECK(!(bqkv.has_value() && bqkv->defined()), "attn_fwd: the bf16 kernel takes qkv with its bias");
-  CHECK_BF16(qkv);
-  hip_check(dca_attn_fwd(ptr<short>(qkv), ptr<short>(o), ptr<float>(lse), N, 1.f / sqrtf(32.f), cur_stream()),
-            "dca_attn_fwd");
-  return {o, lse};
-}
-
-torch::Tensor attn_bwd(torch::Tensor qkv, torch::Tensor o, torch::Tensor dout, torch::Tensor lse,
-                       c10::optional<torch::Tensor> bqkv) {
-  CHECK_F32(lse);
-  TORCH_CHECK(qkv.dim() == 2 && qkv.size(1) == 384 && qkv.size(0) % 64 == 0, "qkv must be (N*64, 384)");
-  const int N = qkv.size(0) / 64;
-  TORCH_CHECK(o.numel() == (int64_t)N * 64 * 128 && dout.numel() == o.numel() && lse.numel() == (int64_t)N * 256,
-              "attn_bwd shapes");
-  auto dqkv = torch::empty_like(qkv);
-  if (qkv.scalar_type() == at::kFloat) {
-    CHECK_F32(qkv); CHECK_F32(o); CHECK_F32(dout);
-    auto b = qkv_bias(qkv, bqkv);
-    hip_check(dca_attn_bwd_f32(ptr<float>(qkv), ptr<float>(b), ptr<float>(o), ptr<float>(dout), ptr<float>(lse),
-                               ptr<float>(dqkv), N, 1.f / sqrtf(32.f), cur_stream()),
-              "dca_attn_bwd_f32");
-    return dqkv;
-  }
-  CHECK_BF16(qkv); CHECK_BF16(o); CHECK_BF16(dout);
-  hip_check(dca_attn_bwd(ptr<short>(qkv), ptr<short>(o), ptr<short>(dout), ptr<float>(lse), ptr<short>(dqkv), N,
-                         1.f / sqrtf(32.f), cur_stream()),
-            "dca_attn_bwd");
-  return dqkv;
-}
-
-static void check_type_off(const std::vector<int64_t>& t) {
-  TORCH_CHECK(t.size() == 7 && t[0] == 0 && t[6] == 64, "type offsets must be 7 values from 0 to 64");
-  for (int i = 0; i < 6; ++i) TORCH_CHECK(t[i + 1] >= t[i], "type offsets must be non-decreasing");
-}
-
-// pools of E1 (N*64,128) bf16 into x896[:, 128:] (bf16, in place) and arg (N,6,128) u8 (returned)
-torch::Tensor attn_pool(torch::Tensor e1, std::vector<int64_t> type_off, torch::Tensor x896, bool compat) {
-  const bool f32 = e1.scalar_type() == at::kFloat;
-  if (f32) { CHECK_F32(e1); CHECK_F32(x896); } else { CHECK_BF16(e1); CHECK_BF16(x896); }
-  check_type_off(type_off);
-  const int N = e1.numel() / (64 * 128);
-  TORCH_CHECK(x896.numel() == (int64_t)N * 896, "x896 must be (N, 896)");
-  auto arg = torch::empty({(int64_t)N, 6, 128}, e1.options().dtype(at::kByte));
-  int off[7];
-  for (int i = 0; i < 7; ++i) off[i] = (int)type_off[i];
-  hip_check(dca_attn_pool(e1.data_ptr(), off, x896.data_ptr(), ptr<unsigned char>(arg), N, compat ? 1 : 0,
-                          f32 ? 1 : 0, cur_stream()),
-            "dca_attn_pool");
-  return arg;
-}
-
-torch::Tensor attn_demb(torch::Tensor dtl, torch::Tensor q, torch::Tensor dx, torch::Tensor arg,
-                        std::vector<int64_t> type_off, bool compat, bool f32) {
-  CHECK_F32(dtl); CHECK_DEV(q); CHECK_DT(q, at::kFloat); CHECK_F32(dx); CHECK_U8(arg);
-  check_type_off(type_off);
-  const int N = dtl.size(0);
-  TORCH_CHECK(dtl.size(1) == 64 && q.size(0) == N && q.stride(1) == 1 && dx.size(0) == N && dx.size(1) == 896 &&
-              arg.numel() == (int64_t)N * 6 * 128, "attn_demb shapes");
-  auto de1 = torch::empty({(int64_t)N * 64, 128}, dx.options().dtype(f32 ? at::kFloat : at::kBFloat16));
-  int off[7];
-  for (int i = 0; i < 7; ++i) off[i] = (int)type_off[i];
-  hip_check(dca_attn_demb(ptr<float>(dtl), ptr<float>(q), (int)q.stride(0), ptr<float>(dx), ptr<unsigned char>(arg),
-                          off, de1.data_ptr(), N, compat ? 1 : 0, f32 ? 1 : 0, cur_stream()),
-            "dca_attn_demb");
-  return de1;
-}
-
-// returns (dE0 bf16 (R,128), dgamma (128), dbeta (128), dbt (6,128)); type_of: (64) u8 device, unit slot → type
-std::vector<torch::Tensor> ln_bwd(torch::Tensor dxn, torch::Tensor e0, torch::Tensor bsub, torch::Tensor gamma,
-                                  torch::Tensor mean, torch::Tensor rstd, torch::Tensor de1, torch::Tensor type_of) {
-  const bool f32 = e0.scalar_type() == at::kFloat;
-  if (f32) { CHECK_F32(dxn); CHECK_F32(e0); CHECK_F32(de1); } else { CHECK_BF16(dxn); CHECK_BF16(e0); CHECK_BF16(de1); }
-  CHECK_F32(gamma); CHECK_F32(mean); CHECK_F32(rstd); CHECK_U8(type_of);
-  if (bsub.numel()) { CHECK_F32(bsub); }
-  TORCH_CHECK(bsub.numel() == 128 || (f32 && bsub.numel() == 0), "ln_bwd: b_sub must be (128) (or empty in fp32)");
-  const int64_t R = e0.numel() / 128;
-  TORCH_CHECK(dxn.numel() == R * 128 && de1.numel() == R * 128 && mean.numel() == R && rstd.numel() == R &&
-              type_of.numel() == 64 && R % 64 == 0, "ln_bwd shapes");
-  auto de0 = torch::empty({R, 128}, e0.options());
-  const int W = dca_ln_part_width();
-  const int nblk = (int)std::min<int64_t>(1024, (R + 15) / 16);
-  auto part = torch::empty({(int64_t)nblk * W}, gamma.options());
-  auto out = torch::empty({W}, gamma.options());
-  hip_check(dca_ln_bwd(dxn.data_ptr(), e0.data_ptr(), bsub.numel() ? ptr<float>(bsub) : nullptr, ptr<float>(gamma),
-                       ptr<float>(mean), ptr<float>(rstd), de1.data_ptr(), ptr<unsigned char>(type_of),
-                       de0.data_ptr(), ptr<float>(part), nblk, ptr<float>(out), (int)R, f32 ? 1 : 0, cur_stream()),
-            "dca_ln_bwd");
-  return {de0, out.narrow(0, 0, 128), out.narrow(0, 128, 128), out.narrow(0, 256, 768).view({6, 128})};
-}
 
 // Minibatch gather from an HBM replay pool into time-major rows (one launch for all fields). pools: per-step
 // fields (capacity, S, …) then per-sequence fields (capacity, …) (n_step of them are per-step); idx (B) int64 device.
@@ -1264,16 +1136,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("split_bf16x2", &split_bf16x2, "fp32 -> (hi, lo) bf16 images with x = hi + lo (slab_major: (R,K) -> "
         "[K/32][R][32] images, the dpre_dx operand layout)", py::arg("src"), py::arg("slab_major") = false);
   m.def("enc_small_grads", &enc_small_grads, "entity-encoder type-bias and env-layer gradients in one pass");
-  m.def("ln_fwd", &ln_fwd, "LayerNorm(E0 - bsub) -> (xn, mean, rstd); bf16, or fp32 (bsub may be empty); optional copy of E0",
-        py::arg("e0"), py::arg("bsub"), py::arg("gamma"), py::arg("beta"), py::arg("eps"),
-        py::arg("e0_copy") = py::none());
-  m.def("attn_fwd", &attn_fwd, "entity self-attention per (row, head): (o, lse); bf16, or fp32 (bf16x3 MFMA, qkv bias "
-        "added on load)", py::arg("qkv"), py::arg("bqkv") = py::none());
-  m.def("attn_bwd", &attn_bwd, "entity self-attention backward: dqkv", py::arg("qkv"), py::arg("o"), py::arg("dout"),
-        py::arg("lse"), py::arg("bqkv") = py::none());
-  m.def("attn_pool", &attn_pool, "per-type max-pool + argmax of attended embeddings into x896");
-  m.def("attn_demb", &attn_demb, "dE1 = dtl*q + pool gradient at the argmax unit (bf16 or f32 out)");
-  m.def("ln_bwd", &ln_bwd, "LayerNorm backward + residual: (dE0, dgamma, dbeta, dbt)");
   m.def("replay_gather", &replay_gather, "minibatch gather from an HBM replay pool into time-major rows (one launch)");
-  m.def("returns_scan", &returns_scan, "segmented reverse scan: discounted returns / GAE + per-team EMA normalisation");
+  m.def("returns_scan", &returns_scan, "segmented reverse scan: discounted returns / GAE / V-trace GAE + per-team EMA "
+        "normalisation (positional: ..., factor, eps, lr or None, rho_bar, c_bar)");
 }

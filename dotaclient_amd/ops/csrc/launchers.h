@@ -89,10 +89,11 @@ hipError_t dca_actor_state_prep(const short* pre, float* h, float* c, const floa
 hipError_t dca_lstm_cell(const float* gates, float* h, float* c, short* h16, const float* active, int N, int H,
                          hipStream_t st);
 
-hipError_t dca_returns(const float* rew, int K, const float* val, const int* off, const int* seglen,
+hipError_t dca_returns(const float* rew, int K, const float* val, const float* lr, const int* off, const int* seglen,
                        const float* boot, const unsigned char* done, const int* keys, int nseg, int max_len,
                        float* ret, float* adv, float* norm, float* stats, const float* ema_in, float* ema_out,
-                       int mode, int normalize, float gamma, float lam, float factor, float eps, hipStream_t st);
+                       int mode, int normalize, float gamma, float lam, float rho_bar, float c_bar, float factor,
+                       float eps, hipStream_t st);
 
 int dca_loss_prep_blocks();
 hipError_t dca_loss_prep(const unsigned char* act, int N, int A, int* partial, unsigned* counter, float* norms,
@@ -112,23 +113,6 @@ int dca_enc_small_blocks();
 hipError_t dca_enc_small_grads(const float* z, int ldz, const float* dtl, int U, const int* type_off, const float* dx,
                                const float* env, const float* we, const float* be, int N, int compat, float* part,
                                float* out, hipStream_t st);
-
-int dca_ln_part_width();
-hipError_t dca_ln_fwd(const void* e0, const float* bsub, const float* gamma, const float* beta, void* xn, float* mean,
-                      float* rstd, int R, float eps, int f32, void* e0_copy, hipStream_t st);
-hipError_t dca_attn_fwd(const short* qkv, short* o, float* lse, int N, float scale, hipStream_t st);
-hipError_t dca_attn_fwd_f32(const float* qkv, const float* bq, float* o, float* lse, int N, float scale, hipStream_t st);
-hipError_t dca_attn_bwd_f32(const float* qkv, const float* bq, const float* o, const float* dout, const float* lse,
-                            float* dqkv, int N, float scale, hipStream_t st);
-hipError_t dca_attn_bwd(const short* qkv, const short* o, const short* dout, const float* lse, short* dqkv, int N,
-                        float scale, hipStream_t st);
-hipError_t dca_attn_pool(const void* e1, const int* type_off, void* x896, unsigned char* arg, int N, int compat,
-                         int f32, hipStream_t st);
-hipError_t dca_attn_demb(const float* dtl, const float* q, int ldq, const float* dx, const unsigned char* arg,
-                         const int* type_off, void* de1, int N, int compat, int f32, hipStream_t st);
-hipError_t dca_ln_bwd(const void* dxn, const void* e0, const float* bsub, const float* gamma, const float* mean,
-                      const float* rstd, const void* de1, const unsigned char* type_of, void* de0, float* part,
-                      int nblk, float* out, int R, int f32, hipStream_t st);
 
 hipError_t dca_replay_gather(const void* const* src, void* const* dst, const long long* row_bytes, const int* per_step,
                              int nf, const long long* idx, int S, int B, hipStream_t st);

@@ -8,6 +8,11 @@
 //     normalised return (G − μ)/(σ + eps) (optimizer.py:335-343, 185-186);
 //   * the PPO path (north star): GAE(γ, λ) over the valid prefix, A_t = δ_t + γλ·A_{t+1},
 //     δ_t = r_t + γ·V_{t+1} − V_t (bootstrapped with the actor's V at the cut, 0 at a terminal), returns = A + V.
+//   * mode 2, V-trace GAE (off-policy experience; Espeholt et al. 2018): the values are the LEARNER's (its forward at
+//     the iteration's weights) and lr_t = log π(a_t) − log μ(a_t) against the actor's behaviour log-prob;
+//     ρ_t = min(ρ̄, e^{lr_t}), c_t = λ·min(c̄, e^{lr_t}), A_t = ρ_t·δ_t + γ·c_t·A_{t+1} (so the value target
+//     v_t = V_t + A_t is the V-trace target), and the policy advantage ρ_t·(r_t + γ·v_{t+1} − V_t) =
+//     ρ_t·δ_t + ρ_t·γ·A_{t+1}. At π = μ (weight age 0) this is mode 1 exactly.
 //
 // Layout: all rollouts of an iteration are concatenated, each padded to a multiple of seq_len (segment s spans
 // [off[s], off[s+1]) with T_s valid steps), so the learner's sequences are a plain reshape of the outputs.
@@ -33,32 +38,48 @@ __device__ __forceinline__ float forcing(const float* __restrict__ rew, int K, c
   const float* rr = rew + row * K;
   float r = 0.f;
   for (int k = 0; k < K; ++k) r += rr[k];
-  if (mode == 1) {
+  if (mode >= 1) {
     const float vn = (t + 1 < T) ? val[row + 1] : vboot;
     return r + gamma * vn - val[row];
   }
   return r;
 }
 
+// V-trace truncated importance weights of row i (mode 2): ρ = min(ρ̄, e^{lr}), the trace coefficient min(c̄, e^{lr})
+__device__ __forceinline__ void vtrace_w(const float* __restrict__ lr, size_t i, float rho_bar, float c_bar,
+                                         float& rho, float& cw) {
+  const float r = __expf(fminf(lr[i], 30.f));
+  rho = fminf(rho_bar, r);
+  cw = fminf(c_bar, r);
+}
+
 __global__ __launch_bounds__(kT) void returns_scan_kernel(
-    const float* __restrict__ rew, int K, const float* __restrict__ val, const int* __restrict__ off,
-    const int* __restrict__ seglen, const float* __restrict__ boot, const unsigned char* __restrict__ done,
-    float* __restrict__ ret, float* __restrict__ adv, float* __restrict__ stats, int mode, float gamma, float lam) {
+    const float* __restrict__ rew, int K, const float* __restrict__ val, const float* __restrict__ lr,
+    const int* __restrict__ off, const int* __restrict__ seglen, const float* __restrict__ boot,
+    const unsigned char* __restrict__ done, float* __restrict__ ret, float* __restrict__ adv,
+    float* __restrict__ stats, int mode, float gamma, float lam, float rho_bar, float c_bar) {
   const int s = blockIdx.x;
   const int base = off[s];
   const int P = off[s + 1] - base;
   const int T = min(seglen[s], P);
-  const int n = (mode == 1) ? T : P;                 // GAE: the padded tail is zero
-  const float c = (mode == 1) ? gamma * lam : gamma;
-  const float vboot = (mode == 1 && !done[s]) ? boot[s] : 0.f;
-  float* acc_out = (mode == 1) ? adv : ret;          // the scanned quantity
+  const int n = (mode >= 1) ? T : P;                 // GAE: the padded tail is zero
+  const float c0 = (mode >= 1) ? gamma * lam : gamma;
+  const float vboot = (mode >= 1 && !done[s]) ? boot[s] : 0.f;
+  float* acc_out = (mode >= 1) ? adv : ret;          // the scanned quantity
   const int per = (n + kT - 1) / kT;
   const int lo = min((int)threadIdx.x * per, n), hi = min(lo + per, n);
 
   // pass 1: forcing terms (parked in acc_out) and this chunk's map y -> X + p*y
   float X = 0.f, p = 1.f;
   for (int t = hi - 1; t >= lo; --t) {
-    const float d = forcing(rew, K, val, (size_t)base + t, t, T, vboot, gamma, mode);
+    float d = forcing(rew, K, val, (size_t)base + t, t, T, vboot, gamma, mode);
+    float c = c0;
+    if (mode == 2) {
+      float rho, cw;
+      vtrace_w(lr, (size_t)base + t, rho_bar, c_bar, rho, cw);
+      d *= rho;
+      c = c0 * cw;
+    }
     acc_out[base + t] = d;
     X = d + c * X;
     p *= c;
@@ -89,16 +110,25 @@ __global__ __launch_bounds__(kT) void returns_scan_kernel(
   float sum = 0.f;
   for (int t = hi - 1; t >= lo; --t) {
     const size_t i = (size_t)base + t;
-    carry = acc_out[i] + c * carry;
-    acc_out[i] = carry;
+    const float d = acc_out[i];
+    if (mode == 2) {
+      float rho, cw;
+      vtrace_w(lr, i, rho_bar, c_bar, rho, cw);
+      const float next = carry;                       // A_{t+1} (0 past the last step: the bootstrap is in δ)
+      carry = d + c0 * cw * carry;
+      acc_out[i] = d + rho * gamma * next;            // policy advantage ρ_t·(r_t + γ·v_{t+1} − V_t)
+    } else {
+      carry = d + c0 * carry;
+      acc_out[i] = carry;
+    }
     float g = carry;
-    if (mode == 1) {
+    if (mode >= 1) {
       g = carry + val[i];
       ret[i] = g;
     }
     sum += g;
   }
-  if (mode == 1) {                                    // zero tail of a GAE segment
+  if (mode >= 1) {                                    // zero tail of a GAE segment
     for (int t = T + threadIdx.x; t < P; t += kT) {
       ret[base + t] = 0.f;
       adv[base + t] = 0.f;
@@ -172,14 +202,14 @@ __global__ __launch_bounds__(kT) void ema_normalize_kernel(
 
 }  // namespace
 
-extern "C" hipError_t dca_returns(const float* rew, int K, const float* val, const int* off, const int* seglen,
-                                  const float* boot, const unsigned char* done, const int* keys, int nseg, int max_len,
-                                  float* ret, float* adv, float* norm, float* stats, const float* ema_in,
-                                  float* ema_out, int mode, int normalize, float gamma, float lam, float factor,
-                                  float eps, hipStream_t st) {
+extern "C" hipError_t dca_returns(const float* rew, int K, const float* val, const float* lr, const int* off,
+                                  const int* seglen, const float* boot, const unsigned char* done, const int* keys,
+                                  int nseg, int max_len, float* ret, float* adv, float* norm, float* stats,
+                                  const float* ema_in, float* ema_out, int mode, int normalize, float gamma, float lam,
+                                  float rho_bar, float c_bar, float factor, float eps, hipStream_t st) {
   if (nseg <= 0) return hipSuccess;
-  hipLaunchKernelGGL(returns_scan_kernel, dim3(nseg), dim3(kT), 0, st, rew, K, val, off, seglen, boot, done, ret, adv,
-                     stats, mode, gamma, lam);
+  hipLaunchKernelGGL(returns_scan_kernel, dim3(nseg), dim3(kT), 0, st, rew, K, val, lr, off, seglen, boot, done, ret,
+                     adv, stats, mode, gamma, lam, rho_bar, c_bar);
   DCA_CHECK_LAUNCH();
   const int by = normalize ? max(1, min(64, (max_len + 4 * kT - 1) / (4 * kT))) : 1;
   hipLaunchKernelGGL(ema_normalize_kernel, dim3(nseg, by), dim3(kT), 0, st, ret, off, keys, stats, nseg, ema_in,

@@ -1,22 +1,19 @@
-"""Autograd wrapper around the XCD-team persistent LSTM recurrence kernels (ops/csrc/lstm_team.hip).
+"""Launch helpers of the XCD-team persistent LSTM recurrence kernels (ops/csrc/lstm_team.hip).
 
-``lstm_sequence(x, w_ih, w_hh, b_ih, b_hh, h0, c0)`` is a drop-in for a single-layer ``nn.LSTM`` (batch_first,
-PyTorch gate order i, f, g, o) returning ``(out (B,S,H) f32, h_n, c_n)``:
+* ``team_fwd`` — the recurrence in ONE persistent launch (``_C.lstm_team_fwd``): 32 workgroups of ONE XCD per
+  sequence chain, exchanging the step state through that XCD's L2, gates in unit-major (…, H, 4) layout; it saves the
+  activated gates and cell states for the backward;
+* ``team_bwd`` — the reverse recurrence in one launch (``_C.lstm_team_bwd``) producing ∂L/∂gates for every step (the
+  weight gradients are the learner's split-K GEMMs, ops/csrc/gemm_tn.hip);
+* ``gate_perm`` / ``team_ctl`` — the gate-major → unit-major row permutation and the per-stream control block.
 
-* the input projection ``x·W_ihᵀ + b_ih + b_hh`` for all timesteps is one bf16 GEMM with fp32 output (hipBLASLt);
-* the recurrence runs in ONE persistent launch (``_C.lstm_team_fwd``): 32 workgroups of ONE XCD per sequence chain,
-  exchanging the step state through that XCD's L2, gates in unit-major (B,S,H,4) layout; it saves the activated
-  gates and cell states for backward;
-* backward runs the reverse recurrence in one launch (``_C.lstm_team_bwd``) producing ∂L/∂gates for every step, then
-  the weight gradients are plain GEMMs over all B·S rows: dW_ih = dGᵀx, dW_hh = dGᵀh_{t-1}, db = ΣdG, dx = dG·W_ih.
 (A cross-XCD "ring" recurrence — every hand-off over the Infinity Fabric — measured 2.5-3 µs per step against the
-team kernel's ≈1.3-1.5 µs and was removed in round 5.)
+team kernel's ≈1.3-1.5 µs and was removed in round 5. The ``nn.LSTM``-shaped autograd wrapper that tests the
+kernels against torch lives in tests/test_lstm_kernel.py.)
 """
 from __future__ import annotations
 
 import torch
-
-from . import require
 
 
 def gate_perm(H: int, device) -> torch.Tensor:
@@ -52,67 +49,3 @@ def team_bwd(C, dhs, gates4, cs, c0, dhn, dcn, whh16, err, **kw):
     return C.lstm_team_bwd(dhs, gates4, cs, c0.contiguous(), dhn, dcn, whh16, err, team_ctl(dhs.device), **kw)
 
 
-
-def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
-    """bf16 × bf16 → fp32 GEMM (hipBLASLt) — fp32 accumulation and output."""
-    return torch.mm(a.to(torch.bfloat16), b.to(torch.bfloat16), out_dtype=torch.float32)
-
-
-class _Recurrence(torch.autograd.Function):
-    @staticmethod
-    def forward(ctx, xp, w_hh, h0, c0, err):
-        C = require()
-        whh16 = w_hh.detach().to(torch.bfloat16).contiguous()
-        B, S, G4 = xp.shape
-        H = G4 // 4
-        ctx.err = err
-        xp4 = xp.view(B, S, 4, H).transpose(2, 3).contiguous()
-        hs16, hsf, cs, gates4, hn, cn = team_fwd(C, xp4, whh16, h0, c0, err, True)
-        ctx.save_for_backward(gates4, cs, c0, whh16, hs16, h0)
-        ctx.mark_non_differentiable(hs16)
-        return hsf, hn, cn, hs16
-
-    @staticmethod
-    def backward(ctx, dhs, dhn, dcn, _dhs16):
-        C = require()
-        gates, cs, c0, whh16, hs16, h0 = ctx.saved_tensors
-        B, S, H = cs.shape
-        dhs = dhs.contiguous() if dhs is not None else torch.zeros_like(cs)
-        dhn = None if dhn is None else dhn.contiguous()
-        dcn = None if dcn is None else dcn.contiguous()
-        dg4, dh0, dc0 = team_bwd(C, dhs, gates, cs, c0, dhn, dcn, whh16, ctx.err)
-        dgates = dg4.permute(0, 1, 3, 2).reshape(B, S, 4 * H)
-        hprev = torch.cat([h0.to(torch.bfloat16).unsqueeze(1), hs16[:, :-1]], dim=1).reshape(B * S, H)
-        dw_hh = _mm_f32(dgates.reshape(B * S, 4 * H).t(), hprev)
-        return dgates, dw_hh, dh0, dc0, None
-
-
-class _InputProjection(torch.autograd.Function):
-    """xp = x·W_ihᵀ + b_ih + b_hh as one bf16 GEMM with fp32 output."""
-
-    @staticmethod
-    def forward(ctx, x, w_ih, b_ih, b_hh):
-        B, S, I = x.shape
-        x2 = x.reshape(B * S, I).to(torch.bfloat16)
-        w16 = w_ih.detach().to(torch.bfloat16)
-        xp = _mm_f32(x2, w16.t()) + (b_ih + b_hh)
-        ctx.save_for_backward(x2, w16)
-        ctx.shape = (B, S, I)
-        return xp.view(B, S, -1)
-
-    @staticmethod
-    def backward(ctx, dxp):
-        x2, w16 = ctx.saved_tensors
-        B, S, I = ctx.shape
-        g2 = dxp.reshape(B * S, -1)
-        g16 = g2.to(torch.bfloat16)
-        dx = torch.mm(g16, w16, out_dtype=torch.float32).view(B, S, I)
-        dw = torch.mm(g16.t(), x2, out_dtype=torch.float32)
-        db = g2.sum(0)
-        return dx, dw, db, db
-
-
-def lstm_sequence(x, w_ih, w_hh, b_ih, b_hh, h0, c0, err):
-    """Returns (out f32 (B,S,H), h_n (B,H), c_n (B,H), out_bf16 (B,S,H))."""
-    xp = _InputProjection.apply(x, w_ih, b_ih, b_hh)
-    return _Recurrence.apply(xp, w_hh, h0, c0, err)

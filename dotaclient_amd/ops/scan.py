@@ -10,6 +10,10 @@ per-team EMA state ``ema`` (``(n_keys, 3)`` = mean, std, initialised) in rollout
   return ``(G − μ)/(σ + eps)`` (optimizer.py:185-186) in ``norm`` (= ``adv``).
 * ``mode='gae'`` — PPO path: GAE(γ, λ) over the valid prefix, ``ret = adv + V``, zeros in the padded tail; the EMA is
   updated with the statistics of ``ret[:T]`` (metrics only); ``norm`` = ``adv``.
+* ``mode='vtrace'`` — off-policy PPO path (Espeholt et al. 2018, V-trace): ``val`` are the LEARNER's values (its
+  forward at the iteration's weights), ``lr`` = log π − log μ per row (learner vs behaviour log-prob of the sampled
+  action); ρ_t = min(ρ̄, e^lr), c_t = λ·min(c̄, e^lr), A_t = ρ_t·δ_t + γ·c_t·A_{t+1}; ``ret = A + V`` is the V-trace
+  value target and ``adv`` the policy advantage ρ_t·(r_t + γ·v_{t+1} − V_t). Equal to ``gae`` at lr = 0.
 
 On a GPU tensor the HIP kernel runs (and the extension is required); on CPU the torch reference below runs — it is
 also the oracle of the GPU tests.
@@ -22,13 +26,15 @@ import torch
 
 from ..constants import EPS
 
-MODES = {'discount': 0, 'gae': 1}
+MODES = {'discount': 0, 'gae': 1, 'vtrace': 2}
 
 
-def _reference(rew, val, off, seglen, boot, done, keys, ema, mode, gamma, lam, factor, eps, normalize):
+def _reference(rew, val, off, seglen, boot, done, keys, ema, mode, gamma, lam, factor, eps, normalize, lr=None,
+               rho_bar=1.0, c_bar=1.0):
     L = rew.shape[0]
     r = rew.double().sum(1)
-    v = val.double() if mode == 1 else None
+    v = val.double() if mode >= 1 else None
+    w = torch.exp(lr.double().clamp(max=30.0)) if mode == 2 else None
     ret = torch.zeros(L, dtype=torch.float64)
     adv = torch.zeros(L, dtype=torch.float64)
     nseg = seglen.numel()
@@ -45,6 +51,16 @@ def _reference(rew, val, off, seglen, boot, done, keys, ema, mode, gamma, lam, f
                 nv = float(v[a + t])
             ret[a:a + T] = adv[a:a + T] + v[a:a + T]
             seg = ret[a:a + T]
+        elif mode == 2:
+            acc, nv = 0.0, (0.0 if bool(done[s]) else float(boot[s]))
+            for t in range(T - 1, -1, -1):
+                rho, cw = min(rho_bar, float(w[a + t])), min(c_bar, float(w[a + t]))
+                delta = float(r[a + t]) + gamma * nv - float(v[a + t])
+                adv[a + t] = rho * (delta + gamma * acc)          # ρ_t·(r_t + γ·v_{t+1} − V_t)
+                acc = rho * delta + gamma * lam * cw * acc        # v_t − V_t
+                ret[a + t] = acc + float(v[a + t])
+                nv = float(v[a + t])
+            seg = ret[a:a + T]
         else:
             acc = 0.0
             for t in range(b - a - 1, -1, -1):
@@ -55,7 +71,7 @@ def _reference(rew, val, off, seglen, boot, done, keys, ema, mode, gamma, lam, f
             stats[s, 0] = seg.mean()
             stats[s, 1] = seg.std(unbiased=False)
     ema_new = ema.clone().double()
-    norm = adv.clone() if mode == 1 else torch.zeros(L, dtype=torch.float64)
+    norm = adv.clone() if mode >= 1 else torch.zeros(L, dtype=torch.float64)
     for s in range(nseg):
         k = int(keys[s])
         if ema_new[k, 2] == 0:
@@ -75,31 +91,36 @@ def _reference(rew, val, off, seglen, boot, done, keys, ema, mode, gamma, lam, f
 
 def compute_returns(rew: torch.Tensor, val, off, seglen, boot, done, keys, ema: torch.Tensor, mode: str = 'gae',
                     gamma: float = 0.98, lam: float = 0.95, factor: float = 0.99, eps: float = EPS,
-                    normalize: bool = True) -> Dict[str, torch.Tensor]:
+                    normalize: bool = True, lr=None, rho_bar: float = 1.0,
+                    c_bar: float = 1.0) -> Dict[str, torch.Tensor]:
     """``rew`` (L, K) f32 sub-rewards (summed per row), ``val`` (L,) f32 or None; per-segment metadata as host
     int32/float32/uint8 tensors or sequences; ``ema`` (n_keys, 3) f32 on the same device as ``rew`` (updated in
-    place)."""
+    place); ``lr`` (L,) f32 log ratios for ``mode='vtrace'``."""
     m = MODES[mode]
     off = torch.as_tensor(off, dtype=torch.int32).contiguous()
     seglen = torch.as_tensor(seglen, dtype=torch.int32).contiguous()
     keys = torch.as_tensor(keys, dtype=torch.int32).contiguous()
     boot = torch.as_tensor(boot, dtype=torch.float32).contiguous()
     done = torch.as_tensor(done, dtype=torch.uint8).contiguous()
-    if m == 1 and val is None:
+    if m >= 1 and val is None:
         raise ValueError('gae needs values')
+    if m == 2 and lr is None:
+        raise ValueError('vtrace needs the per-row log ratios')
     if rew.device.type != 'cuda':
-        return _reference(rew, val, off, seglen, boot, done, keys, ema, m, gamma, lam, factor, eps, normalize)
+        return _reference(rew, val, off, seglen, boot, done, keys, ema, m, gamma, lam, factor, eps, normalize, lr,
+                          rho_bar, c_bar)
     from . import require
     C = require()
     L = rew.shape[0]
     rew = rew.float().contiguous()
-    v = val.float().contiguous() if m == 1 else rew.new_empty(0)
+    v = val.float().contiguous() if m >= 1 else rew.new_empty(0)
     ret = torch.empty(L, device=rew.device)
-    adv = torch.empty(L, device=rew.device) if m == 1 else ret.new_empty(L)
+    adv = torch.empty(L, device=rew.device) if m >= 1 else ret.new_empty(L)
     norm = torch.empty(L, device=rew.device) if m == 0 else adv
     stats = torch.empty(seglen.numel(), 2, device=rew.device)
     C.returns_scan(rew, v, off, seglen, boot, done, keys, ema, ret, adv, norm, stats, m, bool(normalize and m == 0),
-                   float(gamma), float(lam), float(factor), float(eps))
+                   float(gamma), float(lam), float(factor), float(eps),
+                   lr.float().contiguous() if m == 2 else None, float(rho_bar), float(c_bar))
     if m == 0:
         adv = norm if normalize else ret
     return {'ret': ret, 'adv': adv, 'norm': norm, 'stats': stats}

@@ -13,6 +13,23 @@ from typing import Callable, Optional
 from .. import native
 
 
+SHM_HEADROOM = 64 << 20      # /dev/shm bytes a ring leaves free (the model file, ≈8-90 MB, lives there too)
+MIN_RING = 16 << 20          # smallest useful experience ring (whole-game rollouts are ≈1.35 MB)
+
+
+def ring_capacity_for(want: int, free: Optional[int]) -> int:
+    """The ring size to create on a /dev/shm with ``free`` bytes: ``want``, clamped to half the free space and to
+    what leaves :data:`SHM_HEADROOM` (the same rule :class:`ShmBroker` enforces); MemoryError when even
+    :data:`MIN_RING` does not fit."""
+    if free is None:
+        return int(want)
+    cap = min(int(want), free // 2, free - SHM_HEADROOM)
+    if cap < MIN_RING:
+        raise MemoryError(f'/dev/shm has {free >> 20} MiB free: not even a {MIN_RING >> 20} MiB experience ring fits '
+                          f'beside {SHM_HEADROOM >> 20} MiB of headroom (enlarge /dev/shm, e.g. docker --shm-size)')
+    return cap
+
+
 def shm_free_bytes() -> Optional[int]:
     """Free bytes of /dev/shm (None where it cannot be read)."""
     try:
@@ -34,7 +51,7 @@ class ShmBroker:
             # tmpfs backs the ring lazily: a ring larger than /dev/shm's free space would be created fine and then
             # SIGBUS its producers mid-write once the pages run out — refuse it here instead
             free = shm_free_bytes()
-            if free is not None and capacity + (64 << 20) > free:
+            if free is not None and capacity + SHM_HEADROOM > free:
                 raise MemoryError(f'/dev/shm has {free >> 20} MiB free, the experience ring needs {capacity >> 20} MiB '
                                   f'(+ the model file): pass a smaller capacity')
         self.ring = native.ShmRing(f'/{self.name}_xp', capacity, create)
@@ -68,6 +85,11 @@ class ShmBroker:
         """Zero-copy consumption: ``(array, token)`` with the array viewing the message inside the ring (its region
         stays reserved) until :meth:`release_experience` ``(token)`` — exactly once; None when nothing arrived."""
         return self.ring.claim(-1.0 if timeout is None else float(timeout))
+
+    def claim_valid(self, token: int) -> bool:
+        """Whether a zero-copy claim still owns its ring region: False once the ring abandoned it (a claim held past
+        the abandonment deadline while producers needed the space) — its bytes may have been overwritten since."""
+        return bool(self.ring.claim_valid(int(token)))
 
     def release_experience(self, token: int):
         self.ring.release(int(token))

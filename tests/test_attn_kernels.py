@@ -1,4 +1,5 @@
-"""5v5 entity-attention block kernels (ops/csrc/attn.hip) vs plain PyTorch fp32 references of the same ops."""
+"""5v5 entity-attention kernels — the fused block forward / backward (ops/csrc/attn_block.hip) and the encoder with a
+given ∂E0 (ops/csrc/encoder.hip) — vs plain PyTorch fp32 / float64 references of the same ops."""
 import pytest
 import torch
 import torch.nn.functional as F
@@ -16,176 +17,6 @@ def _bf(t):
 
 def _g(seed):
     return torch.Generator(device='cuda').manual_seed(seed)
-
-
-def test_ln_fwd(gpu_ops):
-    g = _g(0)
-    e0 = _bf(torch.randn(N * U, D, device='cuda', generator=g) * 2 + 0.5)
-    bsub = torch.randn(D, device='cuda', generator=g) * 0.1
-    gamma = 1 + 0.1 * torch.randn(D, device='cuda', generator=g)
-    beta = 0.1 * torch.randn(D, device='cuda', generator=g)
-    xn, mean, rstd = gpu_ops.ln_fwd(e0, bsub, gamma, beta, 1e-5)
-    x = e0.float() - bsub
-    ref = F.layer_norm(x, (D,), gamma, beta, 1e-5)
-    torch.testing.assert_close(xn.float(), ref, rtol=2e-2, atol=2e-2)
-    torch.testing.assert_close(mean, x.mean(-1), rtol=1e-4, atol=1e-4)
-    torch.testing.assert_close(rstd, 1 / torch.sqrt(x.var(-1, unbiased=False) + 1e-5), rtol=1e-3, atol=1e-3)
-
-
-def _attn_ref(qkv):
-    q, k, v = qkv.float().view(N, U, 3, NH, HD).unbind(2)
-    q, k, v = (t.transpose(1, 2) for t in (q, k, v))            # (N, h, U, d)
-    s = q @ k.transpose(-1, -2) / HD ** 0.5
-    o = torch.softmax(s, -1) @ v
-    return o.transpose(1, 2).reshape(N * U, D), torch.logsumexp(s, -1)
-
-
-def test_attn_fwd_bwd(gpu_ops):
-    g = _g(1)
-    qkv = _bf(torch.randn(N * U, 3 * D, device='cuda', generator=g))
-    o, lse = gpu_ops.attn_fwd(qkv)
-    o_ref, lse_ref = _attn_ref(qkv)
-    torch.testing.assert_close(o.float(), o_ref, rtol=3e-2, atol=3e-2)
-    torch.testing.assert_close(lse, lse_ref, rtol=1e-3, atol=1e-3)
-    dout = _bf(torch.randn(N * U, D, device='cuda', generator=g))
-    dqkv = gpu_ops.attn_bwd(qkv, o, dout, lse)
-    x = qkv.float().requires_grad_(True)
-    _attn_ref(x)[0].backward(dout.float())
-    ref = x.grad
-    err = (dqkv.float() - ref).norm() / ref.norm()
-    assert err < 2e-2, float(err)
-    for part in range(3):   # q, k, v blocks each
-        a, b = dqkv.float()[:, part * D:(part + 1) * D], ref[:, part * D:(part + 1) * D]
-        assert (a - b).norm() / b.norm() < 3e-2, part
-
-
-def test_attn_fwd_bwd_f32(gpu_ops):
-    """fp32 attention core (bf16x3 split MFMA, fp32 softmax) vs an fp64 reference: fp32-class accuracy."""
-    g = _g(2)
-    qkv = torch.randn(N * U, 3 * D, device='cuda', generator=g) * 1.5       # peaky rows as well as flat ones
-    bq = torch.randn(3 * D, device='cuda', generator=g) * 0.5                # added by the kernels on load
-    o, lse = gpu_ops.attn_fwd(qkv, bq)
-    assert o.dtype == torch.float32
-    x = (qkv + bq).double().requires_grad_(True)
-    q, k, v = x.view(N, U, 3, NH, HD).unbind(2)
-    q, k, v = (t.transpose(1, 2) for t in (q, k, v))
-    s = q @ k.transpose(-1, -2) / HD ** 0.5
-    o_ref = (torch.softmax(s, -1) @ v).transpose(1, 2).reshape(N * U, D)
-    rel = lambda a, b: float((a.double() - b).norm() / b.norm())   # noqa: E731
-    assert rel(o, o_ref.detach()) < 2e-5
-    torch.testing.assert_close(lse.double(), torch.logsumexp(s, -1).detach(), rtol=1e-5, atol=1e-5)
-    dout = torch.randn(N * U, D, device='cuda', generator=g)
-    dqkv = gpu_ops.attn_bwd(qkv, o, dout, lse, bq)
-    o_ref.backward(dout.double())
-    for part in range(3):   # q, k, v blocks each
-        a, b = dqkv[:, part * D:(part + 1) * D], x.grad[:, part * D:(part + 1) * D]
-        assert rel(a, b) < 5e-5, (part, rel(a, b))
-
-
-@pytest.mark.parametrize('compat', [False, True])
-def test_pool_and_demb(gpu_ops, compat):
-    g = _g(2)
-    e1 = _bf(torch.randn(N * U, D, device='cuda', generator=g))
-    x896 = torch.zeros(N, 896, device='cuda', dtype=torch.bfloat16)
-    arg = gpu_ops.attn_pool(e1, TYPE_OFF, x896, compat)
-    e = e1.float().view(N, U, D)
-    for t in range(6):
-        src = 3 if (compat and t == 5) else t
-        seg = e[:, TYPE_OFF[src]:TYPE_OFF[src + 1]]
-        mx, am = seg.max(1)
-        torch.testing.assert_close(x896[:, D + t * D:D + (t + 1) * D].float(), mx)
-        got = seg.gather(1, arg[:, t].long().unsqueeze(1)).squeeze(1)
-        torch.testing.assert_close(got, mx)
-    # ∂E1 = dtl ⊗ q + pool gradient routed to the argmax unit
-    dtl = torch.randn(N, U, device='cuda', generator=g)
-    z = torch.randn(N, 160, device='cuda', generator=g)
-    dx = torch.randn(N, 896, device='cuda', generator=g)
-    de1 = gpu_ops.attn_demb(dtl, z, dx, arg, TYPE_OFF, compat, False)
-    ref = dtl.unsqueeze(-1) * z[:, None, :D]
-    for t in range(6):
-        src = 3 if (compat and t == 5) else t
-        u = TYPE_OFF[src] + arg[:, t].long()                    # (N, D)
-        ref.scatter_add_(1, u.unsqueeze(1), dx[:, D + t * D:D + (t + 1) * D].unsqueeze(1))
-    torch.testing.assert_close(de1.float().view(N, U, D), ref, rtol=1e-2, atol=2e-2)
-
-
-def test_ln_bwd(gpu_ops):
-    g = _g(3)
-    R = N * U
-    e0 = _bf(torch.randn(R, D, device='cuda', generator=g))
-    bsub = torch.randn(D, device='cuda', generator=g) * 0.1
-    gamma = 1 + 0.1 * torch.randn(D, device='cuda', generator=g)
-    beta = 0.1 * torch.randn(D, device='cuda', generator=g)
-    _, mean, rstd = gpu_ops.ln_fwd(e0, bsub, gamma, beta, 1e-5)
-    dxn = _bf(torch.randn(R, D, device='cuda', generator=g))
-    de1 = _bf(torch.randn(R, D, device='cuda', generator=g))
-    type_of = torch.tensor(sum([[t] * (TYPE_OFF[t + 1] - TYPE_OFF[t]) for t in range(6)], []), dtype=torch.uint8,
-                           device='cuda')
-    de0, dgam, dbet, dbt = gpu_ops.ln_bwd(dxn, e0, bsub, gamma, mean, rstd, de1, type_of)
-    x = (e0.float() - bsub).requires_grad_(True)
-    gm, bt = gamma.clone().requires_grad_(True), beta.clone().requires_grad_(True)
-    F.layer_norm(x, (D,), gm, bt, 1e-5).backward(dxn.float())
-    ref_de0 = x.grad + de1.float()
-    torch.testing.assert_close(de0.float(), ref_de0, rtol=2e-2, atol=3e-2)
-    torch.testing.assert_close(dgam, gm.grad, rtol=1e-3, atol=1e-2)
-    torch.testing.assert_close(dbet, bt.grad, rtol=1e-3, atol=1e-2)
-    ref_dbt = torch.stack([ref_de0.view(N, U, D)[:, TYPE_OFF[t]:TYPE_OFF[t + 1]].sum((0, 1)) for t in range(6)])
-    torch.testing.assert_close(dbt, ref_dbt, rtol=2e-2, atol=0.5)
-
-
-@pytest.mark.parametrize('compat', [False, True])
-def test_block_kernels_f32(gpu_ops, compat):
-    """fp32 learner's block kernels: LayerNorm fwd/bwd without b_sub (+ residual, ∂γ, ∂β, per-type ∂b_τ), pools and
-    ∂E1 routing, against float64 references."""
-    g = _g(5)
-    R = N * U
-    rel = lambda a, b: float((a.double() - b).norm() / b.norm())   # noqa: E731
-    e0 = torch.randn(R, D, device='cuda', generator=g) * 2 + 0.5
-    gamma = 1 + 0.1 * torch.randn(D, device='cuda', generator=g)
-    beta = 0.1 * torch.randn(D, device='cuda', generator=g)
-    nob = torch.empty(0, device='cuda')
-    cp = torch.empty_like(e0)
-    xn, mean, rstd = gpu_ops.ln_fwd(e0, nob, gamma, beta, 1e-5, e0_copy=cp)
-    assert xn.dtype == torch.float32 and torch.equal(cp, e0)
-    bsub = torch.randn(D, device='cuda', generator=g) * 0.1               # b_sub path: LN(e0 + b − b) == LN(e0)
-    xn2, mean2, rstd2 = gpu_ops.ln_fwd(e0 + bsub, bsub, gamma, beta, 1e-5)
-    torch.testing.assert_close(xn2, xn, rtol=1e-5, atol=1e-5)
-    x = e0.double().requires_grad_(True)
-    gm, bt = gamma.double().requires_grad_(True), beta.double().requires_grad_(True)
-    y = F.layer_norm(x, (D,), gm, bt, 1e-5)
-    assert rel(xn, y.detach()) < 1e-6
-    dxn = torch.randn(R, D, device='cuda', generator=g)
-    de1 = torch.randn(R, D, device='cuda', generator=g)
-    type_of = torch.tensor(sum([[t] * (TYPE_OFF[t + 1] - TYPE_OFF[t]) for t in range(6)], []), dtype=torch.uint8,
-                           device='cuda')
-    de0, dgam, dbet, dbt = gpu_ops.ln_bwd(dxn, e0, nob, gamma, mean, rstd, de1, type_of)
-    y.backward(dxn.double())
-    ref_de0 = x.grad + de1.double()
-    assert rel(de0, ref_de0) < 1e-5
-    assert rel(dgam, gm.grad) < 1e-5 and rel(dbet, bt.grad) < 1e-5
-    ref_dbt = torch.stack([ref_de0.view(N, U, D)[:, TYPE_OFF[t]:TYPE_OFF[t + 1]].sum((0, 1)) for t in range(6)])
-    assert rel(dbt, ref_dbt) < 1e-5
-    # pools (exact: max is a selection) and the routed ∂E1
-    x896 = torch.zeros(N, 896, device='cuda')
-    arg = gpu_ops.attn_pool(e0, TYPE_OFF, x896, compat)
-    e = e0.view(N, U, D)
-    for t in range(6):
-        src = 3 if (compat and t == 5) else t
-        seg = e[:, TYPE_OFF[src]:TYPE_OFF[src + 1]]
-        mx, am = seg.max(1)
-        assert torch.equal(x896[:, D + t * D:D + (t + 1) * D], mx)
-        assert torch.equal(seg.gather(1, arg[:, t].long().unsqueeze(1)).squeeze(1), mx)
-    dtl = torch.randn(N, U, device='cuda', generator=g)
-    z = torch.randn(N, 160, device='cuda', generator=g)
-    dx = torch.randn(N, 896, device='cuda', generator=g)
-    got = gpu_ops.attn_demb(dtl, z, dx, arg, TYPE_OFF, compat, True)
-    assert got.dtype == torch.float32
-    ref = dtl.double().unsqueeze(-1) * z.double()[:, None, :D]
-    for t in range(6):
-        src = 3 if (compat and t == 5) else t
-        u = TYPE_OFF[src] + arg[:, t].long()
-        ref.scatter_add_(1, u.unsqueeze(1), dx.double()[:, D + t * D:D + (t + 1) * D].unsqueeze(1))
-    assert rel(got.view(N, U, D), ref) < 1e-6
 
 
 def test_encoder_bwd_with_given_demb(gpu_ops):

@@ -55,7 +55,7 @@ def _worker(rank, world, port, precision, q):
         q.put((rank, repr(e), None, None, None))
 
 
-@pytest.mark.parametrize('world,precision', [(2, 'fp32'), (4, 'fp32'), (2, 'bf16')])
+@pytest.mark.parametrize('world,precision', [(2, 'fp32'), (4, 'fp32'), (2, 'fp32-exact')])
 def test_fused_dp_split_graph_step_multi_rank(gpu_ops, world, precision):
     import torch.multiprocessing as mp
     from dotaclient_amd.learner.engine import Learner, LossConfig

@@ -250,13 +250,12 @@ def _step_grads(precision, preset, algo, B, S, seed=3, fp64=False, vbug=False):
     return out
 
 
-# per-tensor relative gradient error allowed at B=8, S=1400 (lstm512): fp32 is the acceptance bound; the bf16 bound
-# pins what bf16 GEMM operands + bf16 saved activations cost over 1400 recurrent steps
-# (measured on MI355X: fp32 worst 3.9e-4 — affine_unit_basic_stats.weight —, bf16 worst 7.8e-3)
-TOL = {'fp32': 1e-3, 'bf16': 2e-2}
+# per-tensor relative gradient error allowed at B=8, S=1400 (lstm512) for the bf16x3 learner
+# (measured on MI355X: worst 3.9e-4 — affine_unit_basic_stats.weight)
+TOL = {'fp32': 1e-3}
 
 
-@pytest.mark.parametrize('precision', ['fp32', 'bf16'])
+@pytest.mark.parametrize('precision', ['fp32'])
 def test_fused_step_deploy_shape_matches_fp32_oracle(gpu_ops, precision):
     res = _step_grads(precision, 'lstm512', 'ppo', 8, 1400, fp64=precision == 'fp32')
     (lf, mf, gf), (lr_, mr, gr) = res[:2]

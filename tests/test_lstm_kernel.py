@@ -2,7 +2,81 @@
 import pytest
 import torch
 
+from dotaclient_amd.ops.lstm import team_bwd, team_fwd
+
 pytestmark = pytest.mark.gpu
+
+
+def gpu_C():
+    from dotaclient_amd.ops import require
+    return require()
+
+# --- test glue: an nn.LSTM-shaped autograd wrapper around the team kernels (input projection and the weight
+# gradients as torch GEMMs, the recurrence forward / backward on lstm_team.hip)
+def _mm_f32(a: torch.Tensor, b: torch.Tensor) -> torch.Tensor:
+    """bf16 × bf16 → fp32 GEMM (torch, test glue only) — fp32 accumulation and output."""
+    return torch.mm(a.to(torch.bfloat16), b.to(torch.bfloat16), out_dtype=torch.float32)
+
+
+class _Recurrence(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, xp, w_hh, h0, c0, err):
+        C = gpu_C()
+        whh16 = w_hh.detach().to(torch.bfloat16).contiguous()
+        B, S, G4 = xp.shape
+        H = G4 // 4
+        ctx.err = err
+        xp4 = xp.view(B, S, 4, H).transpose(2, 3).contiguous()
+        hs16, hsf, cs, gates4, hn, cn = team_fwd(C, xp4, whh16, h0, c0, err, True)
+        ctx.save_for_backward(gates4, cs, c0, whh16, hs16, h0)
+        ctx.mark_non_differentiable(hs16)
+        return hsf, hn, cn, hs16
+
+    @staticmethod
+    def backward(ctx, dhs, dhn, dcn, _dhs16):
+        C = gpu_C()
+        gates, cs, c0, whh16, hs16, h0 = ctx.saved_tensors
+        B, S, H = cs.shape
+        dhs = dhs.contiguous() if dhs is not None else torch.zeros_like(cs)
+        dhn = None if dhn is None else dhn.contiguous()
+        dcn = None if dcn is None else dcn.contiguous()
+        dg4, dh0, dc0 = team_bwd(C, dhs, gates, cs, c0, dhn, dcn, whh16, ctx.err)
+        dgates = dg4.permute(0, 1, 3, 2).reshape(B, S, 4 * H)
+        hprev = torch.cat([h0.to(torch.bfloat16).unsqueeze(1), hs16[:, :-1]], dim=1).reshape(B * S, H)
+        dw_hh = _mm_f32(dgates.reshape(B * S, 4 * H).t(), hprev)
+        return dgates, dw_hh, dh0, dc0, None
+
+
+class _InputProjection(torch.autograd.Function):
+    """xp = x·W_ihᵀ + b_ih + b_hh as one bf16 GEMM with fp32 output."""
+
+    @staticmethod
+    def forward(ctx, x, w_ih, b_ih, b_hh):
+        B, S, I = x.shape
+        x2 = x.reshape(B * S, I).to(torch.bfloat16)
+        w16 = w_ih.detach().to(torch.bfloat16)
+        xp = _mm_f32(x2, w16.t()) + (b_ih + b_hh)
+        ctx.save_for_backward(x2, w16)
+        ctx.shape = (B, S, I)
+        return xp.view(B, S, -1)
+
+    @staticmethod
+    def backward(ctx, dxp):
+        x2, w16 = ctx.saved_tensors
+        B, S, I = ctx.shape
+        g2 = dxp.reshape(B * S, -1)
+        g16 = g2.to(torch.bfloat16)
+        dx = torch.mm(g16, w16, out_dtype=torch.float32).view(B, S, I)
+        dw = torch.mm(g16.t(), x2, out_dtype=torch.float32)
+        db = g2.sum(0)
+        return dx, dw, db, db
+
+
+def lstm_sequence(x, w_ih, w_hh, b_ih, b_hh, h0, c0, err):
+    """Returns (out f32 (B,S,H), h_n (B,H), c_n (B,H), out_bf16 (B,S,H))."""
+    xp = _InputProjection.apply(x, w_ih, b_ih, b_hh)
+    return _Recurrence.apply(xp, w_hh, h0, c0, err)
+
 
 
 def _rel(a, b):
@@ -11,7 +85,6 @@ def _rel(a, b):
 
 @pytest.mark.parametrize('B,S,H', [(5, 37, 128), (8, 64, 512), (24, 20, 256), (40, 16, 512), (64, 8, 128), (100, 9, 512), (300, 5, 128)])
 def test_lstm_fwd_bwd_matches_torch(gpu_ops, B, S, H):
-    from dotaclient_amd.ops.lstm import lstm_sequence
     torch.manual_seed(B * 1000 + S)
     dev = 'cuda'
     I = 96
@@ -42,7 +115,6 @@ def test_lstm_fwd_bwd_matches_torch(gpu_ops, B, S, H):
 
 def test_lstm_repeat_launch_consistent(gpu_ops):
     """Exchange-buffer re-initialisation: back-to-back launches on the same stream give identical results."""
-    from dotaclient_amd.ops.lstm import lstm_sequence
     torch.manual_seed(0)
     B, S, H = 8, 100, 512
     w_ih = torch.randn(4 * H, 256, device='cuda') * 0.05
@@ -59,7 +131,6 @@ def test_lstm_repeat_launch_consistent(gpu_ops):
 
 def test_team_many_chains_queue(gpu_ops):
     """More chains than XCD teams (B=600 → 19 chains of 32): teams pull chains from the queue; result == torch."""
-    from dotaclient_amd.ops.lstm import lstm_sequence
     torch.manual_seed(1)
     B, S, H, I = 600, 12, 128, 64
     ref = torch.nn.LSTM(I, H, batch_first=True).cuda()
@@ -78,7 +149,6 @@ def test_team_many_chains_queue(gpu_ops):
 def test_team_folded_bias_bf16_dgates_and_bias_grad(gpu_ops, B, S, H, tm):
     """Folded bias (bias4) == bias added to xp4; bf16 ∂gates == f32 ∂gates rounded; the in-kernel bias gradient
     == Σ over rows and steps of the f32 ∂gates."""
-    from dotaclient_amd.ops.lstm import team_bwd, team_fwd
     C = gpu_ops
     torch.manual_seed(7)
     shp = (S, B, H, 4) if tm else (B, S, H, 4)

@@ -321,3 +321,17 @@ def test_shm_ring_abandons_a_claim_that_pins_it():
         assert b.consume_experience(1.0) == msg
     finally:
         b.close(unlink=True)
+
+
+def test_ring_capacity_clamp_matches_the_broker_rule():
+    """learner/e2e.py sizes the node ring with transport.shm.ring_capacity_for: whatever it returns for a given free
+    /dev/shm size, ShmBroker's own headroom check accepts; too small a /dev/shm fails early with a clear message
+    (the old clamp, max(64 MiB, free/2), ended in MemoryError below 128 MiB free)."""
+    from dotaclient_amd.transport.shm import MIN_RING, SHM_HEADROOM, ring_capacity_for
+    for free in (100 << 20, 128 << 20, 200 << 20, 1 << 30, 64 << 30):
+        cap = ring_capacity_for(1 << 32, free)
+        assert MIN_RING <= cap <= free // 2 and cap + SHM_HEADROOM <= free
+    assert ring_capacity_for(32 << 20, 64 << 30) == 32 << 20
+    assert ring_capacity_for(1 << 30, None) == 1 << 30
+    with pytest.raises(MemoryError, match='shm-size'):
+        ring_capacity_for(1 << 30, 64 << 20)        # the container default /dev/shm

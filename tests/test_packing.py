@@ -246,3 +246,67 @@ def test_zero_copy_stager_keeps_up_with_a_faster_drop_oldest_producer():
         assert opt._claim_budget.held == 0 and opt.ingest_stats()['claimed'] > 0
     finally:
         b.close(unlink=True)
+
+
+def test_stager_rejects_an_iteration_whose_claim_was_abandoned():
+    """Zero-copy staging vs the ring's claim abandonment (native/core.h claim_abandon_s_): a learner that holds claimed
+    rollouts past the deadline while producers need the space loses them to the producers — the ring reclaims the
+    regions and new messages overwrite the bytes. The stager checks every claim after copying and drops the iteration
+    instead of training on the overwritten rows; releases of the abandoned tokens are ignored; the next iteration is
+    staged normally."""
+    import threading
+    import time
+    import uuid
+    from dotaclient_amd import native
+    from dotaclient_amd.learner.ingest import _ClaimsAbandoned
+    from dotaclient_amd.learner.optimizer import DotaOptimizer, OptimizerConfig
+    from dotaclient_amd.transport.codec import encode
+    from dotaclient_amd.transport.shm import ShmBroker
+    if not native.AVAILABLE:
+        pytest.skip('native module not built')
+    S = 64
+    msgs = [encode(_rollout(60, i)) for i in range(3)]
+    b = ShmBroker(f'dca_ca_{uuid.uuid4().hex[:8]}', capacity=4 * len(msgs[0]) + 4096, create=True, drop_oldest=True)
+    try:
+        cfg = OptimizerConfig(log_dir='', model='lstm128', seq_len=S, seq_per_epoch=2, batch_size=2, run_local=True)
+        opt = DotaOptimizer.__new__(DotaOptimizer)
+        opt.cfg, opt.broker, opt.corrupt_rollouts, opt._xp_broker = cfg, b, 0, b
+        stop = threading.Event()
+        pl = IngestPipeline(None, S, 2, 'ppo', 128, 'cpu')
+        # control: claimed, staged, released — accepted
+        for m in msgs[:2]:
+            b.publish_experience(m, timeout=1.0)
+        rs = [opt._consume_decode(stop, claim=True) for _ in range(2)]
+        assert all(getattr(r, 'release', None) is not None for r in rs)
+        st = pl.stage(rs)
+        assert st.n_seq == 2
+        pl.expand(st, {})
+        assert opt._claim_budget.held == 0
+        # now hold two claims while a producer fills the ring and waits for space: after 0.3 s the claim at the
+        # reclaim point is abandoned and overwritten
+        b.ring.set_claim_abandon(0.3)
+        for m in msgs[:2]:
+            b.publish_experience(m, timeout=1.0)
+        rs = [opt._consume_decode(stop, claim=True) for _ in range(2)]
+        d0 = b.ring.dropped()
+        t0 = time.monotonic()
+        for i in range(6):                  # more than fits behind the held claims: the last ones wait for abandonment
+            b.publish_experience(msgs[2], timeout=5.0)
+        assert time.monotonic() - t0 > 0.2 and b.ring.dropped() > d0
+        assert not all(r.release.valid() for r in rs)
+        with pytest.raises(_ClaimsAbandoned):
+            pl.stage(rs)
+        assert all(getattr(r, 'release', None) is None for r in rs)     # every claim given back (late: ignored)
+        assert opt._claim_budget.held == 0
+        # the ring and the stager still work: drain, then one more accepted iteration
+        b.ring.set_claim_abandon(60.0)
+        while b.consume_experience(0.0) is not None:
+            pass
+        for m in msgs[:2]:
+            b.publish_experience(m, timeout=1.0)
+        rs = [opt._consume_decode(stop, claim=True) for _ in range(2)]
+        st = pl.stage(rs)
+        pl.expand(st, {})
+        assert st.n_seq == 2 and opt._claim_budget.held == 0
+    finally:
+        b.close(unlink=True)

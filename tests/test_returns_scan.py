@@ -101,8 +101,59 @@ def test_device_ingest_equals_host_ingest(tmp_path, algo):
             assert dev.running.std[team] == pytest.approx(host.running.std[team], rel=1e-5, abs=1e-6)
 
 
+def _vtrace_np(r, v, lr, boot, gamma, lam, rho_bar=1.0, c_bar=1.0):
+    """V-trace (Espeholt et al. 2018, eq. 1) written out as the explicit sum, independently of the recursion:
+    v_s = V_s + Σ_{t≥s} γ^{t−s} (Π_{i=s}^{t−1} c_i) ρ_t δ_t, c_i = λ·min(c̄, w_i), ρ_t = min(ρ̄, w_t)."""
+    T = len(r)
+    w = np.exp(lr)
+    vn = np.append(v[1:], boot)
+    delta = r + gamma * vn - v
+    rho, c = np.minimum(rho_bar, w), lam * np.minimum(c_bar, w)
+    vs = np.zeros(T)
+    for s_ in range(T):
+        acc, prod = 0.0, 1.0
+        for t in range(s_, T):
+            acc += gamma ** (t - s_) * prod * rho[t] * delta[t]
+            prod *= c[t]
+        vs[s_] = v[s_] + acc
+    vs_next = np.append(vs[1:], boot)
+    pg = rho * (r + gamma * vs_next - v)
+    return vs, pg
+
+
+def test_vtrace_reference_matches_explicit_sum_and_equals_gae_on_policy():
+    rng = np.random.RandomState(5)
+    S = 32
+    lens = [30, 32, 70, 5]
+    keys = [0, 1, 0, 1]
+    boot = rng.randn(len(lens)).astype(np.float32)
+    done = [False, True, False, False]
+    off, rew, val = _segments(rng, lens, S)
+    lr = (rng.randn(int(off[-1])) * 0.7).astype(np.float32)
+    out = compute_returns(torch.from_numpy(rew), torch.from_numpy(val), off, lens, boot, done, keys, torch.zeros(2, 3),
+                          'vtrace', lr=torch.from_numpy(lr))
+    for i, (T, a, b) in enumerate(zip(lens, off[:-1], off[1:])):
+        r = rew[a:a + T].astype(np.float64).sum(1)
+        vs, pg = _vtrace_np(r, val[a:a + T].astype(np.float64), lr[a:a + T].astype(np.float64),
+                            0.0 if done[i] else float(boot[i]), 0.98, 0.95)
+        np.testing.assert_allclose(out['ret'][a:a + T].numpy(), vs, rtol=1e-5, atol=1e-5)
+        np.testing.assert_allclose(out['adv'][a:a + T].numpy(), pg, rtol=1e-5, atol=1e-5)
+        assert (out['ret'][a + T:b] == 0).all() and (out['adv'][a + T:b] == 0).all()
+    # on-policy (π = μ): V-trace's value target is GAE's return; its policy advantage ρ(r + γv' − V) = δ + γ·A'
+    gae_out = compute_returns(torch.from_numpy(rew), torch.from_numpy(val), off, lens, boot, done, keys,
+                              torch.zeros(2, 3), 'gae')
+    on = compute_returns(torch.from_numpy(rew), torch.from_numpy(val), off, lens, boot, done, keys, torch.zeros(2, 3),
+                         'vtrace', lr=torch.zeros(int(off[-1])))
+    torch.testing.assert_close(on['ret'], gae_out['ret'], rtol=1e-5, atol=1e-5)
+    a_gae = gae_out['adv']
+    for T, a in zip(lens, off[:-1]):
+        nxt = torch.cat([a_gae[a + 1:a + T], torch.zeros(1)])
+        lam_part = 0.98 * (1 - 0.95) * nxt          # δ + γA' = A + γ(1−λ)A'
+        torch.testing.assert_close(on['adv'][a:a + T], a_gae[a:a + T] + lam_part, rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize('mode', ['discount', 'gae'])
+@pytest.mark.parametrize('mode', ['discount', 'gae', 'vtrace'])
 def test_scan_kernel_matches_reference(gpu_ops, mode):
     rng = np.random.RandomState(11)
     S = 1400
@@ -114,9 +165,10 @@ def test_scan_kernel_matches_reference(gpu_ops, mode):
     ema_c = torch.zeros(3, 3)
     ema_c[1] = torch.tensor([0.3, 1.5, 1.0])            # a resumed team state
     ema_g = ema_c.clone().cuda()
-    ref = compute_returns(torch.from_numpy(rew), torch.from_numpy(val), off, lens, boot, done, keys, ema_c, mode)
+    lr = torch.from_numpy((rng.randn(int(off[-1])) * 0.5).astype(np.float32))
+    ref = compute_returns(torch.from_numpy(rew), torch.from_numpy(val), off, lens, boot, done, keys, ema_c, mode, lr=lr)
     got = compute_returns(torch.from_numpy(rew).cuda(), torch.from_numpy(val).cuda(), off, lens, boot, done, keys,
-                          ema_g, mode)
+                          ema_g, mode, lr=lr.cuda())
     torch.cuda.synchronize()
     for k in ('ret', 'adv', 'norm', 'stats'):
         torch.testing.assert_close(got[k].cpu(), ref[k], rtol=2e-4, atol=2e-4, msg=k)
