@@ -226,10 +226,15 @@ class GpuActorPolicy:
             w['ln_g'] = g('entity_attn.ln.weight').contiguous()
             w['ln_b'] = g('entity_attn.ln.bias').contiguous()
             w['bqkv'] = g('entity_attn.qkv.bias').contiguous()
-            # W_qkv / W_out hi / lo bf16 images in MFMA fragment order (ops/csrc/attn_block.hip, as the learner)
+            # W_qkv / W_out in MFMA fragment order (ops/csrc/attn_block.hip, as the learner): hi / lo bf16 images
+            # (bf16x3 block), or — the IEEE-fp32 actor, mode 0 — the fp32 image and an empty lo (the exact block
+            # kernel attn_block_fwd_f32_kernel<true>, the fp32-exact learner's forward)
             for key, name in (('wq', 'entity_attn.qkv.weight'), ('wo', 'entity_attn.out.weight')):
-                hi, lo = self.C.split_bf16x2(g(name).contiguous())
-                w[key + '_h'], w[key + '_l'] = _frag_order(hi), _frag_order(lo)
+                if mode == 0:
+                    w[key + '_h'], w[key + '_l'] = _frag_order(g(name).contiguous()), g(name).new_empty(0)
+                else:
+                    hi, lo = self.C.split_bf16x2(g(name).contiguous())
+                    w[key + '_h'], w[key + '_l'] = _frag_order(hi), _frag_order(lo)
         H = cfg.hidden
         if cfg.rnn == 'lstm':
             from ..ops.lstm import gate_perm
@@ -288,9 +293,16 @@ class GpuActorPolicy:
     def _d2h(self):
         self.out_pack.copy_range('idx', 'msk' if self.record else 'value', to_host=True)
 
+    # The step's input / output copies run OUTSIDE the captured graph, as plain async copies on the step stream: from
+    # pinned memory those go to the SDMA copy engines. Captured, they became blit kernels (__amd_rocclr_copyBuffer) on
+    # the shader cores — 155 µs of CU time per 4 096-slot step, 36-58 % of the actor step, running beside the
+    # learner's latency-bound recurrence in the node loop (profiles/r5_actor_*_summary.md). DCA_ACTOR_GRAPH_COPIES=1
+    # captures them again (A/B).
+    GRAPH_COPIES = os.environ.get('DCA_ACTOR_GRAPH_COPIES', '0') == '1'
+
     def capture(self):
-        """Warm up (hipBLASLt heuristics, allocator) on a side stream and capture the WHOLE step — input copies from
-        the pinned staging buffers, the policy step, output copies back — in one hipGraph: a step is one launch."""
+        """Warm up (allocator) on a side stream and capture the policy step in one hipGraph: a step is one launch
+        (plus the two SDMA copies around it, or — ``GRAPH_COPIES`` — with the copies inside the graph)."""
         s = self.stream
         s.wait_stream(torch.cuda.current_stream(self.device))
         ctr0 = self.ctr.clone()
@@ -302,9 +314,11 @@ class GpuActorPolicy:
         torch.cuda.current_stream(self.device).wait_stream(s)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, stream=s, capture_error_mode='thread_local'):
-            self._h2d()
+            if self.GRAPH_COPIES:
+                self._h2d()
             self._forward()
-            self._d2h()
+            if self.GRAPH_COPIES:
+                self._d2h()
         torch.cuda.synchronize(self.device)
         # warm-up steps advanced the recurrent state and the RNG counter: start from a clean slate
         self.ctr.copy_(ctr0)
@@ -336,7 +350,11 @@ class GpuActorPolicy:
             if snapshot_rows is not None and len(snapshot_rows) and self.cfg.rnn == 'lstm':
                 self._snapshot(np.asarray(snapshot_rows))
             if self.graph is not None:
+                if not self.GRAPH_COPIES:
+                    self._h2d()
                 self.graph.replay()
+                if not self.GRAPH_COPIES:
+                    self._d2h()
             else:
                 self._h2d()
                 self._forward()
@@ -381,16 +399,12 @@ class GpuActorPolicy:
 
 class F32ActorPolicy(GpuActorPolicy):
     """:class:`GpuActorPolicy` at the reference actor's precision (agent.py:641-660 → policy.py:80-84, torch fp32):
-    the IEEE-fp32 entity encoder (``encoder_fwd`` exact: the learner's ``encoder_fwd_x_kernel``) and the fp32
-    ``actor_core`` (every product an fp32 FMA on ``v_mfma_f32_16x16x4_f32``), fp32 unit embeddings into the sampler.
-    1v1 policies (LSTM-128 / LSTM-512, or the compat linear layer); the 5v5 attention block has no exact variant."""
+    the IEEE-fp32 entity encoder (``encoder_fwd`` exact: the learner's ``encoder_fwd_x_kernel``), for the 5v5 policy
+    the IEEE-fp32 attention block (``attn_block_fwd`` with fp32 fragment images: the fp32-exact learner's block
+    forward), and the fp32 ``actor_core`` (every product an fp32 FMA on ``v_mfma_f32_16x16x4_f32``), fp32 unit
+    embeddings into the sampler. LSTM-128 / LSTM-512 / 5v5, or the compat linear layer."""
 
     CORE_MODE = 0
-
-    def __init__(self, policy: Policy, n_slots: int, device='cuda', **kw):
-        if policy.config.entity_attention:
-            raise ValueError('F32ActorPolicy: 1v1 policies (the attention block has no IEEE-fp32 kernel)')
-        super().__init__(policy, n_slots, device=device, **kw)
 
 
 
@@ -550,7 +564,8 @@ def make_slot_policy(policy: Policy, n_slots: int, device='cuda', precision: str
         raise ValueError(f'actor precision must be one of {ACTOR_PRECISIONS}, got {precision!r}')
     if precision == 'fp8':
         return Fp8ActorPolicy(policy, n_slots, device=dev, **kw)
-    if precision == 'fp32' and dev.type == 'cuda' and not cfg.entity_attention:
+    if precision == 'fp32' and dev.type == 'cuda' and cfg.unit_dim == 128 and cfg.env_dim == 128 and (
+            not cfg.entity_attention or (cfg.layout.max_units == 64 and cfg.attention_heads == 4)):
         return F32ActorPolicy(policy, n_slots, device=dev, **kw)
     if dev.type == 'cuda' and cfg.unit_dim == 128 and cfg.env_dim == 128 and (
             not cfg.entity_attention or (cfg.layout.max_units == 64 and cfg.attention_heads == 4)):

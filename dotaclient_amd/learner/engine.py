@@ -64,6 +64,10 @@ class LossConfig:
     gae_lambda: float = 0.95
     max_grad_norm: float = 0.5        # optimizer.py:215
     compat_value_bug: bool = False    # optimizer.py:603 broadcast quirk
+    # PPO policy term: 'clip' = the clipped surrogate against logp_old (fresh experience: logp_old is the learner's own
+    # log-prob at the iteration's weights, learner/optimizer.py old_logp='learner'); 'tis' = off-policy policy
+    # gradient with the truncated importance weight min(1, π/π_old) (replayed experience, V-trace style)
+    offpolicy: str = 'clip'
 
 
 class Learner:
@@ -141,7 +145,7 @@ class Learner:
         masks = split_heads(batch['masks'], self.counts)
         if cfg.algo == 'ppo':
             return ppo_loss(logits, values, actions, masks, batch['adv'], batch['ret'], batch['logp_old'],
-                            cfg.clip_eps, cfg.entropy_coef, cfg.vf_coef, stable=stable)
+                            cfg.clip_eps, cfg.entropy_coef, cfg.vf_coef, stable=stable, offpolicy=cfg.offpolicy)
         return vpg_loss(logits, values, actions, masks, batch['norm_ret'], batch['ret'], cfg.entropy_coef,
                         cfg.vf_coef, compat_value_bug=cfg.compat_value_bug, stable=stable)
 
@@ -459,6 +463,44 @@ class Learner:
         return metrics
 
     # ------------------------------------------------------------------------------------------------
+    @torch.no_grad()
+    def evaluate_sequences(self, data: Dict[str, torch.Tensor], n: int, chunk: int = 32):
+        """Log-prob of the sampled actions and value of every step of sequences ``0..n-1`` of ``data`` (batch-major
+        ``(≥n, S, …)`` fields ``units``, ``env``, ``actions``, ``masks`` (+ ``h0``/``c0``, ``reset``)) at the
+        CURRENT weights, in stream order: the learner-side ``policy_old`` of the reference (optimizer.py:279, 474) —
+        the PPO ratio's denominator and the GAE / V-trace values of the iteration's experience. Returns (logp (n, S),
+        value (n, S)) f32 on the learner's device. The fused path runs the step's forward kernels (fp32-exact: IEEE
+        fp32, ``chunk`` ≤ 32 sequences per launch — the exact recurrence's 4 rows per XCD chain); the torch path the
+        eager module."""
+        S = data['units'].shape[1]
+        if self.direct():
+            from .. import ops
+            C = ops.require()
+            fields = ('units', 'env', 'actions', 'masks') + (('reset',) if 'reset' in data else ())
+            seq = [k for k in ('h0', 'c0') if k in data]
+            lps, vals = [], []
+            for i0 in range(0, n, chunk):
+                i1 = min(n, i0 + chunk)
+                idx = torch.arange(i0, i1, device=self.device, dtype=torch.int64)
+                outs = C.replay_gather([data[k] for k in fields] + [data[k] for k in seq], len(fields), idx)
+                bt = dict(zip(list(fields) + seq, outs))
+                lp, v = self.model.forward_logp_value(bt, i1 - i0, S)
+                lps.append(lp.view(S, i1 - i0).t())
+                vals.append(v.view(S, i1 - i0).t())
+            return torch.cat(lps, 0).contiguous(), torch.cat(vals, 0).contiguous()
+        from .losses import sampled_logp
+        hidden = None
+        if self.policy.is_recurrent and 'h0' in data:
+            hidden = (data['h0'][:n].unsqueeze(0).contiguous(), data['c0'][:n].unsqueeze(0).contiguous())
+        with self._autocast():
+            logits, values, _ = self.model.forward_packed(data['env'][:n], data['units'][:n], hidden,
+                                                          reset=data['reset'][:n] if 'reset' in data else None)
+        logits = {k: v.float() for k, v in logits.items()}
+        lp = sampled_logp(logits, split_heads(data['actions'][:n], self.counts), split_heads(data['masks'][:n],
+                                                                                             self.counts),
+                          stable=not self.policy.config.compat_bugs)
+        return lp.float(), values.float().reshape(n, S)
+
     def state_dict(self):
         return {'optimizer': self.opt.state_dict(), 'n_steps': self.n_steps}
 

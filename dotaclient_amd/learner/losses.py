@@ -82,17 +82,26 @@ def vpg_loss(logits: Dict[str, torch.Tensor], values: torch.Tensor, actions: Dic
 
 def ppo_loss(logits: Dict[str, torch.Tensor], values: torch.Tensor, actions: Dict[str, torch.Tensor],
              masks: Dict[str, torch.Tensor], advantages: torch.Tensor, returns: torch.Tensor,
-             logp_old: torch.Tensor, clip_eps: float, entropy_coef: float, vf_coef: float, stable: bool = True):
-    """Clipped-surrogate PPO on the joint (summed over sampled heads) log-probability. All per-step tensors (B,S)."""
+             logp_old: torch.Tensor, clip_eps: float, entropy_coef: float, vf_coef: float, stable: bool = True,
+             offpolicy: str = 'clip'):
+    """Clipped-surrogate PPO on the joint (summed over sampled heads) log-probability. All per-step tensors (B,S).
+
+    ``offpolicy='tis'``: the policy term is the off-policy policy gradient with the truncated importance weight
+    w = min(1, π/π_old) held constant (V-trace style, for replayed experience): value −mean(w·A), gradient
+    −mean(w·A·∇log π); ``clipfrac`` then counts the truncated rows (π > π_old)."""
     terms = head_terms(logits, actions, masks, stable=stable)
     logp = sum(t[1] for t in terms.values())
     valid = sum(actions[k].sum(-1) for k in actions).gt(0).to(logp.dtype)   # padded steps select nothing
     n_valid = valid.sum().clamp_min(1.0)
     log_ratio = logp - logp_old
     ratio = torch.exp(log_ratio)
-    surr1 = ratio * advantages
-    surr2 = torch.clamp(ratio, 1.0 - clip_eps, 1.0 + clip_eps) * advantages
-    policy_loss = -(torch.minimum(surr1, surr2) * valid).sum() / n_valid
+    if offpolicy == 'tis':
+        w = ratio.detach().clamp(max=1.0)
+        policy_loss = -(w * advantages * (1.0 + logp - logp.detach()) * valid).sum() / n_valid
+    else:
+        surr1 = ratio * advantages
+        surr2 = torch.clamp(ratio, 1.0 - clip_eps, 1.0 + clip_eps) * advantages
+        policy_loss = -(torch.minimum(surr1, surr2) * valid).sum() / n_valid
     v = values.squeeze(-1)
     if vf_coef > 0:
         value_loss = vf_coef * ((v - returns).pow(2) * valid).sum() / n_valid
@@ -104,7 +113,8 @@ def ppo_loss(logits: Dict[str, torch.Tensor], values: torch.Tensor, actions: Dic
     loss = policy_loss + value_loss + entropy_loss
     with torch.no_grad():
         approx_kl = ((-log_ratio) * valid).sum() / n_valid
-        clipfrac = (((ratio - 1.0).abs() > clip_eps).to(logp.dtype) * valid).sum() / n_valid
+        hit = (ratio > 1.0) if offpolicy == 'tis' else ((ratio - 1.0).abs() > clip_eps)
+        clipfrac = (hit.to(logp.dtype) * valid).sum() / n_valid
     metrics = {'loss': loss, 'policy_loss': policy_loss, 'entropy_loss': entropy_loss, 'advantage_loss': value_loss,
                'advantage': (advantages * valid).sum() / n_valid, 'entropy': entropy, 'approx_kl': approx_kl,
                'clipfrac': clipfrac}

@@ -92,6 +92,17 @@ class OptimizerConfig:
     # non-compat: pack whole zero-state rollouts first-fit into the free tails of the iteration's sequences (episode
     # starts flagged, the recurrence resets h, c there) instead of padding each rollout to seq_len (learner/ingest.py)
     pack_sequences: bool = False
+    # PPO's old log-probs and GAE values: 'learner' = the reference's policy_old (optimizer.py:279, 474) — once per
+    # iteration, before its minibatches, the learner evaluates the iteration's experience at the iteration's starting
+    # weights (Learner.evaluate_sequences, the step's forward kernels) and computes V-trace GAE (ops/scan.py 'vtrace':
+    # truncated importance weights against the actor's behaviour log-prob) from its own values; 'actor' = the
+    # actor's log-probs / values from collection time (on-policy only at weight age 0). Device ingest only.
+    old_logp: str = 'learner'
+    vtrace_rho_bar: float = 1.0
+    vtrace_c_bar: float = 1.0
+    # policy term on replayed experience (replay_gb / replay_capacity): 'tis' = truncated importance weight
+    # min(1, π/π_old) (never zero on many-versions-old samples), 'clip' = PPO's clipped surrogate
+    replay_offpolicy: str = 'tis'
     # pipelined GPU learner with async_checkpoint: publish each iteration's weights right after its steps are queued
     # and finalise its metrics (the one device→host sync) during the NEXT iteration — no blocking sync per iteration
     defer_metrics: bool = True
@@ -173,9 +184,11 @@ class DotaOptimizer:
             trainer_state = ckpt.load_trainer_state(cfg.log_dir, self.iteration_start - 1)
         if pretrained is not None:
             self.policy.load_state_dict(ckpt.load_model_file(pretrained), strict=False)
+        replay_on = bool(cfg.replay_capacity or cfg.replay_gb)
         lc = LossConfig(algo=cfg.algo, learning_rate=cfg.learning_rate, entropy_coef=cfg.entropy_coef,
                         vf_coef=cfg.vf_coef, clip_eps=cfg.clip_eps, gamma=cfg.gamma, gae_lambda=cfg.gae_lambda,
-                        max_grad_norm=cfg.max_grad_norm, compat_value_bug=cfg.compat_value_bug)
+                        max_grad_norm=cfg.max_grad_norm, compat_value_bug=cfg.compat_value_bug,
+                        offpolicy=cfg.replay_offpolicy if replay_on else 'clip')
         prec = cfg.precision
         if prec == 'fp32-exact' and self.device.type == 'cuda' and cfg.batch_size > 32:
             # the exact VALU recurrence runs 1 / 2 / 4 sequences per XCD chain (8 teams): at most 32 per minibatch
@@ -191,6 +204,10 @@ class DotaOptimizer:
         self.ingest = cfg.ingest if cfg.ingest != 'auto' else ('device' if self.device.type == 'cuda' else 'host')
         if cfg.pack_sequences and self.ingest != 'device':
             raise ValueError('pack_sequences needs the device ingest (ingest="device")')
+        if cfg.old_logp not in ('learner', 'actor'):
+            raise ValueError(f'old_logp must be learner or actor, got {cfg.old_logp!r}')
+        if cfg.old_logp == 'learner' and self.ingest != 'device' and cfg.algo == 'ppo':
+            logger.warning('old_logp=learner needs the device ingest: the host ingest keeps the actor\'s log-probs')
         # per-team EMA(0.99) reward statistics as device state (mean, std, initialised) for the device ingest path
         self.ema = torch.zeros(self.MAX_TEAMS, 3, device=self.device)
         for team in self.running.mean:
@@ -485,10 +502,22 @@ class DotaOptimizer:
              'logp_old': x['logp'], 'valid': x['valid']}
         rollouts = st.rollouts
         keys = [self._team_key(r.team_id) for r in rollouts]
-        out = compute_returns(x['rewards'], x.get('values') if st.gae_mode else None, st.off.astype(np.int32),
+        values, mode, lr = (x.get('values'), 'gae', None) if st.gae_mode else (None, 'discount', None)
+        prox = None
+        if st.gae_mode and cfg.old_logp == 'learner':
+            # the reference's policy_old, refreshed every iteration (optimizer.py:279, 474): the iteration's
+            # sequences evaluated at the weights its first minibatch will see (this is enqueued behind the previous
+            # iteration's steps in stream order — the look-ahead — so those ARE the weights it reads), its log-probs
+            # the PPO ratio's denominator, its values the V-trace GAE baseline with truncated importance weights
+            # against the actor's behaviour log-probs (stale experience: the actor played version − weight age)
+            lp, values, prox = self._evaluate_iteration(x, st.n_seq)
+            lr = lp - x['logp']
+            d['logp_old'] = lp
+            mode = 'vtrace'
+        out = compute_returns(x['rewards'], values, st.off.astype(np.int32),
                               st.lens, [r.bootstrap_value for r in rollouts], [bool(r.done) for r in rollouts], keys,
-                              self.ema, 'gae' if st.gae_mode else 'discount', gamma=cfg.gamma, lam=cfg.gae_lambda,
-                              factor=self.running.factor)
+                              self.ema, mode, gamma=cfg.gamma, lam=cfg.gae_lambda,
+                              factor=self.running.factor, lr=lr, rho_bar=cfg.vtrace_rho_bar, c_bar=cfg.vtrace_c_bar)
         d['ret'], d['adv'] = out['ret'], out['adv']
         d['norm_ret'] = out['norm'] if not st.gae_mode else out['adv']
         n_rows = n_keep * S
@@ -499,7 +528,34 @@ class DotaOptimizer:
             if 'reset' in x:
                 d['reset'] = x['reset'][:n_rows].view(n_keep, S)
         self._normalize_advantages(d)
+        if prox is not None:
+            d['_prox'] = prox          # (metrics; popped by run_iteration before the data is used)
         return d
+
+    def _evaluate_iteration(self, x: Dict[str, torch.Tensor], n_seq: int):
+        """Learner-side log-probs and values of the expanded iteration ``x`` (padded layout, ``n_seq`` sequences of
+        ``seq_len`` rows) at the current weights, plus device metrics of how far the behaviour policy was:
+        ``offpolicy/behaviour_kl`` (mean log μ − log π over valid rows), ``offpolicy/rho_mean`` (mean truncated
+        importance weight), ``offpolicy/rho_truncated`` (fraction of rows with π > μ) and
+        ``offpolicy/max_abs_logratio``. Returns (logp (L,), value (L,), metrics)."""
+        S = self.cfg.seq_len
+        L = n_seq * S
+        view = {k: x[k][:L].reshape((n_seq, S) + tuple(x[k].shape[1:])) for k in ('units', 'env', 'actions', 'masks')}
+        if 'hid' in x:
+            view['h0'], view['c0'] = x['hid'][:, 0].contiguous(), x['hid'][:, 1].contiguous()
+        if 'reset' in x:
+            view['reset'] = x['reset'][:L].reshape(n_seq, S)
+        lp, v = self.learner.evaluate_sequences(view, n_seq)
+        lp, v = lp.reshape(L), v.reshape(L)
+        valid = x['valid'][:L]
+        nv = valid.sum().clamp_min(1.0)
+        dlt = (lp - x['logp'][:L]) * valid
+        w = torch.exp(dlt.clamp(max=30.0))
+        m = {'offpolicy/behaviour_kl': -dlt.sum() / nv,
+             'offpolicy/rho_mean': (w.clamp(max=self.cfg.vtrace_rho_bar) * valid).sum() / nv,
+             'offpolicy/rho_truncated': ((w > self.cfg.vtrace_rho_bar).float() * valid).sum() / nv,
+             'offpolicy/max_abs_logratio': dlt.abs().max()}
+        return lp, v, m
 
     def _staging(self, name: str, shape, dtype, pin: bool) -> torch.Tensor:
         """Host staging buffer for one ingest field (contents undefined: the caller writes every row), reused across
@@ -691,6 +747,10 @@ class DotaOptimizer:
         self.timer.stop('h2d')
         self.timer.start('train')
         losses, metrics_acc = [], {}
+        prox = data.pop('_prox', None) if isinstance(data, dict) else None
+        if prox:
+            for k, v in prox.items():
+                metrics_acc[k] = [v]
         g = torch.Generator().manual_seed(cfg.seed * 1000003 + it)
         cuda = self.device.type == 'cuda'
         ev_t0 = ev_t1 = None
@@ -894,6 +954,9 @@ class DotaOptimizer:
             metrics['time/gpu_train_ms_per_step'] = e0.elapsed_time(e1) / p['n_train']
         for k in ('approx_kl', 'clipfrac'):
             if k in mean:
+                metrics[k] = mean[k]
+        for k in mean:
+            if k.startswith('offpolicy/'):
                 metrics[k] = mean[k]
         if self.replay is not None:
             metrics['replay/size'] = float(len(self.replay))

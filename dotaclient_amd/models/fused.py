@@ -133,6 +133,19 @@ class FusedPolicy:
         self.direct_used = False
         return train_direct(self, batch_tm, B, S)
 
+    def forward_logp_value(self, batch_tm, B: int, S: int):
+        """(logp, value) per time-major row at the current weights: the forward half of the step, no backward
+        (models/pipelined.py :func:`forward_logp_value`)."""
+        from .pipelined import forward_logp_value
+        self.refresh()
+        H = self.cfg.hidden
+        dev = batch_tm['units'].device
+        h0, c0 = batch_tm.get('h0'), batch_tm.get('c0')
+        if h0 is None:
+            h0 = c0 = torch.zeros(B, H, device=dev)
+        return forward_logp_value(self, batch_tm['units'], batch_tm['env'], batch_tm['actions'], batch_tm['masks'],
+                                  h0, c0, B, S, reset_t=batch_tm.get('reset'))
+
     def side_stream(self):
         if getattr(self, '_side', None) is None:
             # (default priority: either stream at high priority measured 0.7 ms per step slower under graph replay,

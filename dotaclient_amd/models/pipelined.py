@@ -361,7 +361,8 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     dWcat = dbcat = None
     heads_wg = None
     parts: List[torch.Tensor] = []
-    algo = 0 if lc.algo == 'ppo' else 1
+    # heads_loss algo: 0 = PPO clipped surrogate, 1 = VPG (reference), 2 = PPO's truncated-IS off-policy term
+    algo = (2 if getattr(lc, 'offpolicy', 'clip') == 'tis' else 0) if lc.algo == 'ppo' else 1
     # ---- forward recurrence on stream L, heads (+ heads backward) per chunk on the main stream
     ready = torch.cuda.Event()
     ready.record(main)
@@ -690,3 +691,64 @@ def train_direct(fp, batch_tm: Dict[str, torch.Tensor], B: int, S: int) -> torch
     C.loss_assemble(part, norms, N, 0 if lc.algo == 'ppo' else 1, float(lc.entropy_coef), float(lc.vf_coef), out,
                     S=S, compat_value_bug=bool(lc.compat_value_bug))
     return out
+
+
+def forward_logp_value(fp, units_t, env_t, act_t, msk_t, h0, c0, B: int, S: int,
+                       reset_t: Optional[torch.Tensor] = None):
+    """The policy's log-prob of the sampled actions and its value, per time-major row (row = t·B + b), at the weights
+    in the flat buffer NOW (in stream order) — the forward half of :func:`fused_step_tm` on the same kernels and at
+    the same precision (entity encoder [+ attention block] → forward chain → recurrence → heads GEMM → heads kernel),
+    no backward. The learner's ``policy_old`` (reference optimizer.py:279, 474): once per iteration, before its
+    minibatches, the iteration's experience is evaluated at the iteration's starting weights
+    (learner/optimizer.py ``old_logp='learner'``). Returns (logp (N,) f32, value (N,) f32)."""
+    C = fp.C
+    cfg = fp.cfg
+    exact = bool(getattr(fp, 'exact', False))
+    lin = cfg.rnn != 'lstm'
+    N = B * S
+    U = units_t.shape[1]
+    H = cfg.hidden
+    dev = units_t.device
+    W = fp.weight_images().refresh(C)
+    P = dict(zip(fp.param_names, fp.params))
+    w1, b1 = P['affine_unit_basic_stats.weight'].detach(), P['affine_unit_basic_stats.bias'].detach()
+    we, be = P['affine_env.weight'].detach(), P['affine_env.bias'].detach()
+    x896, emb, arg = C.encoder_fwd(units_t, env_t, w1, b1, W['wt16'], W['bt'], we, be, list(cfg.layout.counts),
+                                   bool(cfg.compat_bugs), exact=exact)
+    if cfg.entity_attention:
+        E0p = emb.view(N * U, 128)
+        if exact:
+            nil = E0p.new_empty(0)
+            wq, wo = (W['wq_x'], nil), (W['wo_x'], nil)
+        else:
+            wq, wo = W['wq_f'], W['wo_f']
+        arg = torch.empty(N, 6, 128, dtype=torch.uint8, device=dev)
+        out = C.attn_block_fwd(E0p, W['bout'], P['entity_attn.ln.weight'].detach(), P['entity_attn.ln.bias'].detach(),
+                               wq[0], wq[1], P['entity_attn.qkv.bias'].detach(), wo[0], wo[1],
+                               fp.type_offset_list(), x896, arg, bool(cfg.compat_bugs), 1e-5)
+        emb = out[6].view(N, U, 128)
+    elif cfg.compat_bugs:   # reference policy.py:127: enemy-tower pool = enemy-nonhero pool
+        x896[:, 768:896] = x896[:, 512:640]
+    if exact:
+        nil = W['wpre16'].new_empty(0)
+        x16, xp = C.pre_rnn_chain(x896, W['wpre16'], nil, W['bpre16'], W['wih16'], nil)
+        hw = ((W['wcat256'], nil), W['bcat256'])
+    else:
+        x16, xp = C.pre_rnn_chain(x896, W['pre_s'][0], W['pre_s'][1], W['bpre16'], W['ih_s'][0], W['ih_s'][1])
+        hw = (W['wcat_s'], W['bcat256'])
+    if lin:
+        hs = xp.add_(W['bias4']).view(S, B, H)
+    else:
+        rst = reset_t.reshape(S, B) if reset_t is not None else None
+        hs = torch.empty(S, B, H, device=dev)
+        o = team_fwd(C, xp.view(S, B, H, 4), W['whh16'], h0.contiguous(), c0.contiguous(), fp.err, False,
+                     time_major=True, hs_out=hs, cs_out=torch.empty(S, B, H, device=dev),
+                     gates_out=torch.empty(S, B, H, 4, device=dev), bias4=W['bias4'], reset=rst)
+        hs = o[0]
+    z = C.rowmm_out256(hs.reshape(N, H), hw[0][0], hw[0][1], hw[1])          # (N, 256): heads logits | value
+    zero = fp.scratch('fwd_zero', (N,), torch.float32, dev)
+    norms = fp.scratch('fwd_norms', (8,), torch.float32, dev)
+    # the heads kernel's selected-action log-prob (its loss partials / gradients are not used here)
+    _, _, _, lp = C.heads_loss(z, emb, act_t, msk_t, zero, zero, zero, zero, norms, 0, False, S, B, 0.1, 0.0, 0.0,
+                               dz_bf16=False, precise=exact)
+    return lp, z[:, 149].contiguous()

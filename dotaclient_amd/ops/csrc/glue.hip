@@ -134,7 +134,7 @@ __global__ __launch_bounds__(kAsmThreads) void loss_assemble_kernel(const float*
   }
   float pol, val, entl, adv, kl = 0.f, cf = 0.f;
   const float invN = 1.f / (float)(N > 0 ? N : 1);
-  if (algo == 0) {
+  if (algo != 1) {   // PPO clipped surrogate (0) or truncated-IS off-policy PG (2)
     pol = -p[0] * norms[0];
     val = vf_coef * p[1] * norms[0];
     entl = -ent_coef * ent;

@@ -178,6 +178,20 @@ __global__ __launch_bounds__(256) void heads_loss_kernel(Params P) {
       acc[6] += valid * (-lr);
       acc[7] += valid * (fabsf(r - 1.f) > P.clip_eps ? 1.f : 0.f);
       acc[8] += valid * A;
+    } else if (P.algo == 2) {   // off-policy PG with a truncated importance weight (replayed experience, V-trace style)
+      // w = min(1, π/π_old) is a constant of the gradient: ∂/∂logπ of −w·A·logπ is −w·A (never zero, unlike the
+      // clipped surrogate on experience many versions old); acc[7] counts the truncated rows
+      const float A = A_n;
+      const float lr = sel - lpo_n;
+      const float r = xexp<PRECISE>(lr);
+      const float w = fminf(r, 1.f);
+      acc[0] += valid * w * A;
+      g_sel = -valid * A * w * nm[0];
+      acc[1] += valid * (V - R) * (V - R);
+      dV = P.vf_coef * 2.f * (V - R) * valid * nm[0];
+      acc[6] += valid * (-lr);
+      acc[7] += valid * (r > 1.f ? 1.f : 0.f);
+      acc[8] += valid * A;
     } else {             // VPG (reference objective)
       const float nr = nret_n;
       acc[0] += -sel * nr;

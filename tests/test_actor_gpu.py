@@ -113,7 +113,7 @@ TOL = {'bf16': dict(logp=5e-2, value=2e-2, h=2e-2), 'fp32': dict(logp=1e-5, valu
 
 @pytest.mark.parametrize('preset,precision', [('lstm512', 'bf16'), ('lstm128', 'bf16'), ('compat', 'bf16'),
                                               ('5v5', 'bf16'), ('lstm512', 'fp32'), ('lstm128', 'fp32'),
-                                              ('compat', 'fp32')])
+                                              ('compat', 'fp32'), ('5v5', 'fp32')])
 @pytest.mark.parametrize('graph', [True, False])
 def test_gpu_actor_matches_policy(gpu_ops, preset, precision, graph):
     """Graph-captured batched actor (hand-written kernels only: encoder → [attention block] → actor_core →
