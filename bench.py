@@ -241,6 +241,7 @@ def main():
         if backend == 'auto':
             backend = 'fused' if use_cuda else 'torch'
         learner = Learner(policy, LossConfig(algo=args.algo), device=device, backend=backend, precision=precision)
+        learner.dp.timing = world > 1       # per-step all-reduce timing events (DataParallel.comm_stats)
         if args.graph == 1 or (args.graph == -1 and learner.backend == 'fused'):
             learner.enable_graph(warmup=1)
         n_pool = args.replay or 4 * B
@@ -291,6 +292,12 @@ def main():
     elapsed, loss_val, final_loss, learner, policy = run(args.precision)
     progress(f'learner {args.precision} done: {elapsed / args.steps * 1e3:.3f} ms/step')
     backend = learner.backend
+    # per-rank all-reduce wall time, the share of the early buckets' all-reduce hidden behind the step's second
+    # compute phase, the exposed comm time, the bucket layout (the first 8-GPU driver run must be diagnosable)
+    comm = learner.dp.comm_stats() if world > 1 else None
+    if comm is not None:
+        comm['dist_backend'] = dist.get_backend()
+        comm['rank'] = rank
     step_mode = {'hipgraph': learner.graph is not None, 'dp_split_overlap': bool(getattr(learner, '_split', False)),
                  'dist_backend': dist.get_backend() if world > 1 else None}
     # DP replicas must hold bit-identical weights after the timed steps (checked across ranks below)
@@ -526,6 +533,7 @@ def main():
 
     shas = gather(weights_sha)
     hosts = gather(host)
+    comms = gather(comm)
     if rank == 0:
         out = {
             'metric': 'PPO optimizer samples/sec (whole node) + actor steps/sec, 1v1-mid LSTM policy',
@@ -566,6 +574,10 @@ def main():
             'learner_b16': big.get('learner_b16'),
             'learner_b32': big.get('learner_b32'),
             'dp_replicas_identical': len(set(shas)) == 1,
+            'dp_comm': ({'dist_backend': step_mode['dist_backend'], 'per_rank': comms,
+                         'allreduce_ms_max': max((c or {}).get('allreduce_ms', 0.0) for c in comms),
+                         'exposed_ms_max': max((c or {}).get('exposed_ms', 0.0) for c in comms)}
+                        if world > 1 else None),
             'weights_sha16_per_rank': shas,
             'actor': actor,
             'e2e': e2e,

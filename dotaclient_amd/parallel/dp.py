@@ -23,6 +23,8 @@ Re-designed for MI355X / RCCL over xGMI rather than translated:
 """
 from __future__ import annotations
 
+import time
+
 from typing import Dict, List, Optional, Sequence
 
 import torch
@@ -116,6 +118,12 @@ class DataParallel:
         self._pending: Dict[int, int] = {}
         self._next = 0
         self._hooks = []
+        # per-step communication timing (enable_timing): the early buckets' all-reduce on the comm stream against the
+        # step's second compute phase (graph 2), and the count-carrying last bucket after it — a ring of the last
+        # records, read without a host sync by comm_stats() (only completed records count)
+        self.timing = False
+        self._trec: List[dict] = []
+        self._cur: Optional[dict] = None
         for i, p in enumerate(self.flat.params):
             self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(i)))
         if broadcast and self.enabled:
@@ -184,13 +192,34 @@ class DataParallel:
         self._extend_last()
         return True
 
+    def _mark(self, name: str, stream=None):
+        """Timing mark of the current step's record: a timing event on ``stream`` (GPU) or the wall clock (CPU)."""
+        if not self.timing:
+            return
+        if self._cur is None:
+            self._cur = {}
+        if self.overlap:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(stream)
+            self._cur[name] = ev
+        else:
+            self._cur[name] = time.perf_counter()
+
     def launch_early(self):
         """All-reduce every bucket but the last (the early-phase gradients) now, asynchronously on the comm
         stream, overlapping whatever the current stream runs next; :meth:`sync` finishes the step."""
         if not self.enabled:
             return
+        if self.timing and self._next < len(self.buckets) - 1:
+            cur = torch.cuda.current_stream(self.flat.grad.device) if self.overlap else None
+            self._mark('phase2_start', cur)                     # graph 2 starts behind this point
+            if self.overlap:
+                self._comm_stream.wait_stream(cur)
+            self._mark('early_start', self._comm_stream)
         for b in range(self._next, len(self.buckets) - 1):
             self._launch(b)
+        if self.timing and 'early_start' in (self._cur or {}):
+            self._mark('early_end', self._comm_stream)
         self._next = len(self.buckets) - 1
 
     def _make_hook(self, i: int):
@@ -234,21 +263,39 @@ class DataParallel:
         if not self.enabled:                  # counts IS has_grad (same header view)
             return
         # Launch whatever the hooks did not (params without grad on this rank, the count-carrying last bucket).
-        for b in range(self._next, len(self.buckets) - 1):
+        rest = range(self._next, len(self.buckets) - 1)
+        if self.timing and len(rest) and 'early_start' not in (self._cur or {}):
+            cur = torch.cuda.current_stream(self.flat.grad.device) if self.overlap else None
+            if self.overlap:
+                self._comm_stream.wait_stream(cur)
+            self._mark('early_start', self._comm_stream if self.overlap else None)
+        for b in rest:
             self._launch(b)
+        if self.timing and len(rest) and 'early_end' not in (self._cur or {}):
+            self._mark('early_end', self._comm_stream if self.overlap else None)
         # The last bucket starts at 0: header (has-grad flags, error flag) + the first parameters, one view.
         lo, hi = self.bucket_ranges[-1]
         last = self.flat.grad[lo:hi]
         if self.overlap:
             cur = torch.cuda.current_stream(last.device)
+            self._mark('compute_end', cur)                      # the step's compute is queued up to here
             self._comm_stream.wait_stream(cur)
+            self._mark('late_start', self._comm_stream)
             with torch.cuda.stream(self._comm_stream):
                 dist.all_reduce(last, op=dist.ReduceOp.SUM, group=self.group)
+            self._mark('late_end', self._comm_stream)
             for w in self._works:
                 w.wait()
             cur.wait_stream(self._comm_stream)
         else:
+            self._mark('compute_end')
+            self._mark('late_start')
             dist.all_reduce(last, op=dist.ReduceOp.SUM, group=self.group)
+            self._mark('late_end')
+        if self.timing and self._cur is not None:
+            self._trec.append(self._cur)
+            del self._trec[:-64]
+        self._cur = None
         self._works = []
         self._pending = {}
         self._next = 0
@@ -260,6 +307,44 @@ class DataParallel:
         seg = self.flat.segment_ids[h:]
         scale = torch.where(seg >= 0, inv[seg.clamp_min(0).long()], torch.zeros_like(self.flat.grad[h:]))
         self.flat.grad[h:].mul_(scale)
+
+    def comm_stats(self) -> Optional[Dict[str, float]]:
+        """Mean per-step communication timing over the recorded steps (``timing`` on), None without records:
+        ``allreduce_ms`` (early + last bucket on the comm stream), ``early_ms`` / ``late_ms``, ``overlap_frac`` — the
+        share of the early buckets' all-reduce that ran while the step's second compute phase (graph 2: the encoder
+        backward) was still running — and ``exposed_ms``, the comm time after the compute ended (the step waits for
+        it). GPU records are timing events read once complete (``query()``, no host sync); CPU (gloo) records the
+        wall clock of the synchronous calls (no overlap)."""
+        recs = []
+        for r in self._trec:
+            if 'late_end' not in r:
+                continue
+            if self.overlap:
+                if not all(e.query() for e in r.values()):
+                    continue
+                t = lambda a, b: r[a].elapsed_time(r[b])  # noqa: E731
+            else:
+                t = lambda a, b: 1e3 * (r[b] - r[a])       # noqa: E731
+            late = t('late_start', 'late_end')
+            early = ov = 0.0
+            if 'early_end' in r:
+                early = t('early_start', 'early_end')
+                if 'phase2_start' in r:
+                    # [early_start, early_end] ∩ [phase2_start, compute_end] on the comm / compute timelines
+                    ov = max(0.0, min(early, t('early_start', 'compute_end')) -
+                             max(0.0, t('early_start', 'phase2_start')))
+            exposed = max(0.0, t('compute_end', 'late_end'))
+            recs.append((early + late, early, late, ov / early if early > 0 else 0.0, exposed))
+        if not recs:
+            return None
+        n = len(recs)
+        keys = ('allreduce_ms', 'early_ms', 'late_ms', 'overlap_frac', 'exposed_ms')
+        out = {k: sum(r[i] for r in recs) / n for i, k in enumerate(keys)}
+        out['steps'] = n
+        out['buckets'] = len(self.buckets)
+        out['bucket_mb'] = [round((hi - lo) * self.flat.grad.element_size() / 2 ** 20, 3)
+                            for lo, hi in self.bucket_ranges]
+        return out
 
     def remove_hooks(self):
         for h in self._hooks:

@@ -46,6 +46,18 @@ def test_bench_json_contract_cpu(world):
     assert len(hp) == world and all(h['n_cpus'] >= 1 and h['actor_threads'] >= 1 and h['e2e_threads'] >= 1
                                     for h in hp)
     assert [h['local_rank'] for h in hp] == list(range(world))
+    # per-rank all-reduce timing of the timed steps (DataParallel.comm_stats): the first multi-GPU driver run reports
+    # where its step time went
+    dc = r['dp_comm']
+    if world == 1:
+        assert dc is None
+        return
+    assert dc['dist_backend'] == 'gloo' and len(dc['per_rank']) == world
+    for i, c in enumerate(dc['per_rank']):
+        assert c['rank'] == i and c['dist_backend'] == 'gloo' and c['steps'] >= 1
+        assert c['allreduce_ms'] > 0 and 0.0 <= c['overlap_frac'] <= 1.0 and c['exposed_ms'] >= 0
+        assert len(c['bucket_mb']) == c['buckets'] >= 1
+    assert dc['allreduce_ms_max'] == max(c['allreduce_ms'] for c in dc['per_rank'])
 
 
 def test_bench_self_launches_ranks_for_gpus_flag():
