@@ -34,6 +34,7 @@ class League:
         self.rng = rng or random.Random()
         self.wins: Dict[int, float] = {}
         self.games: Dict[int, float] = {}
+        self.results: Dict[int, list] = {}     # per opponent version: every game's result (1 / 0 / 0.5), in order
         self._cache: 'OrderedDict[int, object]' = OrderedDict()
         self.cache_size = cache_size
 
@@ -82,6 +83,7 @@ class League:
         v = int(opponent_version)
         self.wins[v] = self.wins.get(v, 0.0) + float(learner_result)
         self.games[v] = self.games.get(v, 0.0) + 1.0
+        self.results.setdefault(v, []).append(float(learner_result))
 
     def win_rate(self, version: int) -> float:
         v = int(version)

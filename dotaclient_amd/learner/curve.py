@@ -7,6 +7,13 @@ validation agent, /root/reference/agent.py:905-927 / 415-434) and one row is emi
 learner samples, actor steps, ``game/rewards_sum``, ``game/win_rate`` and the per-key rewards. Evaluation games use a
 fixed seed, so every row plays the same opening positions; evaluation time is excluded from ``t_train``.
 
+Beyond the reference (round 6): the default-bot win rate saturates (5v5 ends games in ≈130 steps at 100 % wins), so
+every row also plays the current weights head-to-head against frozen snapshots of itself from ``snapshot_lags``
+seconds of training earlier (``snap/win_rate_vs_<lag>``, actor/validate.py ``evaluate_vs_snapshot``), and a league
+curve logs the training league's score against its pool (``league/score``, ``league/pool``). Every row carries the
+learner's ``approx_kl`` / ``clipfrac`` / ``avg_weight_age`` and the off-policy diagnostics of the learner-side
+policy_old pass (``offpolicy/*``).
+
 Used by ``scripts/learning_curve.py`` (profiles/r4_learning_curve.jsonl) and tests/test_learning.py.
 """
 from __future__ import annotations
@@ -27,7 +34,8 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
                        save_model: Optional[str] = None, eval_precision: str = 'fp32',
                        mode: str = '1v1', log_dir: Optional[str] = None, league: Optional[str] = None,
                        latest_weights_prob: float = 0.8, actor_precision: str = 'bf16',
-                       replay_gb: float = 0.0) -> List[Dict]:
+                       replay_gb: float = 0.0, snapshot_lags=(120.0, 300.0, 600.0), snapshot_games: int = 64,
+                       old_logp: str = 'learner', league_matrix_n: int = 0) -> List[Dict]:
     """Train for ``budget`` seconds (evaluations excluded) and return the evaluation rows (the first one before
     any training). ``on_row`` is called with every row as it is produced; ``save_model``: path that receives the
     final weights (a reference-format state_dict file). ``eval_precision``: the validation games' policy step.
@@ -44,7 +52,7 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
     import os
 
     import torch
-    from ..actor.validate import evaluate_vs_default_bot
+    from ..actor.validate import evaluate_vs_default_bot, evaluate_vs_snapshot
     from ..actor.vec import VecActor
     from ..actor.weights import WeightStore
     from ..transport.broker import InProcBroker
@@ -64,7 +72,7 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
                           learning_rate=lr, entropy_coef=entropy_coef, checkpoint_keep=1 if log_dir else 2,
                           run_local=True,
                           xp_timeout=300.0, histogram_freq=10 ** 9, async_checkpoint=True, prefetch_rollouts=64,
-                          pack_sequences=bool(pack), seed=seed, replay_gb=replay_gb)
+                          pack_sequences=bool(pack), seed=seed, replay_gb=replay_gb, old_logp=old_logp)
     opt = DotaOptimizer(cfg, broker)
     ws = WeightStore(model, device='cpu')
     loader = ThreadPoolExecutor(1, thread_name_prefix='weights')
@@ -95,6 +103,8 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
             err.append(e)
             paused.set()
 
+    snaps: List = []                   # (t_train, cpu state_dict) at every evaluation: the snapshot pool
+
     def evaluate(row):
         pause.set()
         if th.is_alive():
@@ -104,6 +114,23 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
         t0 = time.time()
         row.update(evaluate_vs_default_bot(opt.policy, n_games=eval_games, device=device, seed=eval_seed,
                                            max_dota_time=max_dota_time, threads=threads, precision=eval_precision))
+        t_now = float(row.get('t_train', 0.0))
+        for lag in snapshot_lags or ():
+            past = [sn for sn in snaps if sn[0] <= t_now - lag + 1e-6]
+            if not past:
+                continue
+            r = evaluate_vs_snapshot(opt.policy, past[-1][1], n_games=snapshot_games, device=device,
+                                     seed=eval_seed + int(lag), max_dota_time=max_dota_time, threads=threads,
+                                     precision=eval_precision)
+            tag = f'{int(lag) // 60}min' if lag >= 60 else f'{int(lag)}s'
+            row[f'snap/win_rate_vs_{tag}'] = r['win_rate']
+            row[f'snap/age_s_vs_{tag}'] = round(t_now - past[-1][0], 1)
+        snaps.append((t_now, {k: v.detach().cpu().clone() for k, v in opt.policy.state_dict().items()}))
+        if lg is not None:
+            g = sum(lg.games.values())
+            row['league/pool'] = len(ws.weights)
+            row['league/score'] = sum(lg.wins.values()) / g if g else None
+            row['league/games'] = g
         row['eval_s'] = round(time.time() - t0, 3)
         pause.clear()
         rows.append(row)
@@ -140,8 +167,25 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
                 evaluate({'t_train': round(trained, 1), 'iteration': it - 1, 'samples': samples,
                           'actor_steps': steps0 + va.steps_taken, 'resumed': bool(resumed), 'loss': m.get('loss/sum'), 'entropy': m.get('entropy'),
                           'train_reward_per_sec': m.get('reward_per_sec/sum'),
-                          'avg_weight_age': m.get('avg_weight_age')})
+                          'avg_weight_age': m.get('avg_weight_age'), 'approx_kl': m.get('approx_kl'),
+                          'clipfrac': m.get('clipfrac'),
+                          **{k: v for k, v in m.items() if k.startswith('offpolicy/')}})
                 next_eval += eval_every
+        if league_matrix_n and len(snaps) >= 2:
+            # the pool's pairwise win rates: snapshots spread evenly over the run, oldest first
+            from ..actor.validate import league_matrix
+            pause.set()
+            if th.is_alive():
+                paused.wait(timeout=60)
+            k = min(league_matrix_n, len(snaps))
+            pick = [snaps[round(i * (len(snaps) - 1) / (k - 1))] for i in range(k)]
+            lm = league_matrix([(f't{int(t)}s', sd) for t, sd in pick], opt.policy.config,
+                               n_games=snapshot_games, device=device, max_dota_time=max_dota_time, threads=threads,
+                               precision=eval_precision)
+            row = {'league_matrix': lm, 't_train': round(trained, 1)}
+            rows.append(row)
+            if on_row is not None:
+                on_row(row)
         if save_model:
             opt.flush_metrics()
             sync()

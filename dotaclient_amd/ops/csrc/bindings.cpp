@@ -743,6 +743,16 @@ void loss_prep(torch::Tensor act, torch::Tensor ws, torch::Tensor norms) {
 int64_t loss_prep_ws_elems() { return 5 * dca_loss_prep_blocks() + 1; }
 
 // Loss scalar + metrics (out (16) f32) from the heads/loss partials part (R,16).
+// Test utility (glue.hip): hold `blocks`·(1/8) CUs of XCD `xcd` for `seconds` on the current stream; returns the
+// per-workgroup placement record (XCC id + 1 where it held a CU, 0 elsewhere).
+torch::Tensor occupy_xcd(int64_t xcd, int64_t blocks, double seconds, torch::Tensor like) {
+  TORCH_CHECK(xcd >= 0 && xcd < 8 && blocks >= 1 && blocks <= 4096 && seconds > 0.0 && seconds <= 10.0,
+              "occupy_xcd: xcd in [0, 8), 1..4096 blocks, 0 < seconds <= 10");
+  auto seen = torch::zeros({blocks}, like.options().dtype(at::kInt));
+  hip_check(dca_occupy_xcd((int)xcd, (int)blocks, seconds, ptr<int>(seen), cur_stream()), "dca_occupy_xcd");
+  return seen;
+}
+
 void loss_assemble(torch::Tensor part, torch::Tensor norms, int64_t N, int64_t algo, double ent_coef, double vf_coef,
                    torch::Tensor out, int64_t S, bool compat_value_bug) {
   CHECK_F32(part); CHECK_F32(norms); CHECK_F32(out);
@@ -1137,6 +1147,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "[K/32][R][32] images, the dpre_dx operand layout)", py::arg("src"), py::arg("slab_major") = false);
   m.def("enc_small_grads", &enc_small_grads, "entity-encoder type-bias and env-layer gradients in one pass");
   m.def("replay_gather", &replay_gather, "minibatch gather from an HBM replay pool into time-major rows (one launch)");
+  m.def("occupy_xcd", &occupy_xcd, "test utility: hold CUs of one XCD for a while (160 KB LDS per workgroup)",
+        py::arg("xcd"), py::arg("blocks"), py::arg("seconds"), py::arg("like"));
   m.def("returns_scan", &returns_scan, "segmented reverse scan: discounted returns / GAE / V-trace GAE + per-team EMA "
         "normalisation (positional: ..., factor, eps, lr or None, rho_bar, c_bar)");
 }

@@ -406,3 +406,40 @@ extern "C" hipError_t dca_weight_prep(const float* src, const int* map16, short*
   DCA_CHECK_LAUNCH();
   return hipSuccess;
 }
+
+// ---- test utility: occupy CUs of ONE XCD -------------------------------------------------------------------------
+// Workgroups that land on XCD `xcd` (HW_REG_XCC_ID) hold their CU for `ticks` of the 100 MHz s_memrealtime clock
+// with a 160 KB LDS allocation (no other LDS-using workgroup can share the CU); every other workgroup exits at once.
+// Every wave ends when its own deadline passes (no flag to wait for), and writes one vector store of where it ran
+// (`seen[blockIdx.x]` = XCC id + 1 on the target XCD, 0 elsewhere). Used by tests/test_team_residency.py to check
+// that the XCD-team recurrence forms its teams on the remaining XCDs when part of one XCD is already occupied.
+namespace {
+constexpr int kOccupyLds = 160 * 1024;
+__global__ __launch_bounds__(64) void occupy_xcd_kernel(int xcd, unsigned long long ticks, int* seen) {
+  extern __shared__ __attribute__((aligned(16))) float occ_lds[];
+  const unsigned x = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 0xf;
+  if ((int)x != xcd) {
+    if (threadIdx.x == 0) seen[blockIdx.x] = 0;
+    return;
+  }
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  occ_lds[threadIdx.x] = 0.f;                                  // touch the allocation
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+  if (threadIdx.x == 0) seen[blockIdx.x] = (int)x + 1 + (int)occ_lds[threadIdx.x];
+}
+}  // namespace
+
+extern "C" hipError_t dca_occupy_xcd(int xcd, int blocks, double seconds, int* seen, hipStream_t st) {
+  if (blocks < 1 || blocks > 4096 || seconds <= 0.0 || seconds > 10.0) return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(occupy_xcd_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, kOccupyLds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const unsigned long long ticks = (unsigned long long)(seconds * 1e8);
+  hipLaunchKernelGGL(occupy_xcd_kernel, dim3(blocks), dim3(64), kOccupyLds, st, xcd, ticks, seen);
+  DCA_CHECK_LAUNCH();
+  return hipSuccess;
+}

@@ -98,6 +98,7 @@ hipError_t dca_returns(const float* rew, int K, const float* val, const float* l
 int dca_loss_prep_blocks();
 hipError_t dca_loss_prep(const unsigned char* act, int N, int A, int* partial, unsigned* counter, float* norms,
                          hipStream_t st);
+hipError_t dca_occupy_xcd(int xcd, int blocks, double seconds, int* seen, hipStream_t st);
 hipError_t dca_loss_assemble(const float* part, int nrows, const float* norms, int N, int algo, float ent_coef,
                              float vf_coef, float* out, int S, int vbug, hipStream_t st);
 hipError_t dca_weight_prep(const float* src, const int* map16, short* dst16, int n16, const int* map32, float* dst32,

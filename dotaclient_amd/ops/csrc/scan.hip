@@ -10,9 +10,9 @@
 //     δ_t = r_t + γ·V_{t+1} − V_t (bootstrapped with the actor's V at the cut, 0 at a terminal), returns = A + V.
 //   * mode 2, V-trace GAE (off-policy experience; Espeholt et al. 2018): the values are the LEARNER's (its forward at
 //     the iteration's weights) and lr_t = log π(a_t) − log μ(a_t) against the actor's behaviour log-prob;
-//     ρ_t = min(ρ̄, e^{lr_t}), c_t = λ·min(c̄, e^{lr_t}), A_t = ρ_t·δ_t + γ·c_t·A_{t+1} (so the value target
-//     v_t = V_t + A_t is the V-trace target), and the policy advantage ρ_t·(r_t + γ·v_{t+1} − V_t) =
-//     ρ_t·δ_t + ρ_t·γ·A_{t+1}. At π = μ (weight age 0) this is mode 1 exactly.
+//     ρ_t = min(ρ̄, e^{lr_t}), c_t = λ·min(c̄, e^{lr_t}), A_t = ρ_t·δ_t + γ·c_t·A_{t+1}: the value target
+//     v_t = V_t + A_t is the V-trace target and A_t the advantage (the off-policy-corrected GAE — at π = μ, weight
+//     age 0, exactly mode 1's GAE(γ, λ)).
 //
 // Layout: all rollouts of an iteration are concatenated, each padded to a multiple of seq_len (segment s spans
 // [off[s], off[s+1]) with T_s valid steps), so the learner's sequences are a plain reshape of the outputs.
@@ -114,9 +114,8 @@ __global__ __launch_bounds__(kT) void returns_scan_kernel(
     if (mode == 2) {
       float rho, cw;
       vtrace_w(lr, i, rho_bar, c_bar, rho, cw);
-      const float next = carry;                       // A_{t+1} (0 past the last step: the bootstrap is in δ)
-      carry = d + c0 * cw * carry;
-      acc_out[i] = d + rho * gamma * next;            // policy advantage ρ_t·(r_t + γ·v_{t+1} − V_t)
+      carry = d + c0 * cw * carry;                    // A_t = ρ_t·δ_t + γλ·min(c̄, w_t)·A_{t+1}
+      acc_out[i] = carry;
     } else {
       carry = d + c0 * carry;
       acc_out[i] = carry;

@@ -13,7 +13,7 @@ per-team EMA state ``ema`` (``(n_keys, 3)`` = mean, std, initialised) in rollout
 * ``mode='vtrace'`` — off-policy PPO path (Espeholt et al. 2018, V-trace): ``val`` are the LEARNER's values (its
   forward at the iteration's weights), ``lr`` = log π − log μ per row (learner vs behaviour log-prob of the sampled
   action); ρ_t = min(ρ̄, e^lr), c_t = λ·min(c̄, e^lr), A_t = ρ_t·δ_t + γ·c_t·A_{t+1}; ``ret = A + V`` is the V-trace
-  value target and ``adv`` the policy advantage ρ_t·(r_t + γ·v_{t+1} − V_t). Equal to ``gae`` at lr = 0.
+  value target and ``adv`` = A the off-policy-corrected GAE. Equal to ``gae`` at lr = 0.
 
 On a GPU tensor the HIP kernel runs (and the extension is required); on CPU the torch reference below runs — it is
 also the oracle of the GPU tests.
@@ -56,8 +56,8 @@ def _reference(rew, val, off, seglen, boot, done, keys, ema, mode, gamma, lam, f
             for t in range(T - 1, -1, -1):
                 rho, cw = min(rho_bar, float(w[a + t])), min(c_bar, float(w[a + t]))
                 delta = float(r[a + t]) + gamma * nv - float(v[a + t])
-                adv[a + t] = rho * (delta + gamma * acc)          # ρ_t·(r_t + γ·v_{t+1} − V_t)
-                acc = rho * delta + gamma * lam * cw * acc        # v_t − V_t
+                acc = rho * delta + gamma * lam * cw * acc        # A_t = v_t − V_t
+                adv[a + t] = acc
                 ret[a + t] = acc + float(v[a + t])
                 nv = float(v[a + t])
             seg = ret[a:a + T]

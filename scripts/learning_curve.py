@@ -39,6 +39,13 @@ def main(argv=None):
     ap.add_argument('--actor-precision', default='bf16', choices=['fp32', 'bf16', 'fp8'])
     ap.add_argument('--replay-gb', type=float, default=0.0, help='on-HBM replay the learner samples from')
     ap.add_argument('--device', default='cuda')
+    ap.add_argument('--snapshot-lags', default='120,300,600',
+                    help='seconds of training: every row also plays the weights from that long ago (comma list, '
+                         'empty = off)')
+    ap.add_argument('--snapshot-games', type=int, default=64)
+    ap.add_argument('--old-logp', default='learner', choices=['learner', 'actor'])
+    ap.add_argument('--league-matrix', type=int, default=0,
+                    help='after the curve: pairwise win rates of this many snapshots spread over the run')
     ap.add_argument('--log-dir', default=None,
                     help='checkpoint directory: resume the curve from it (model, Adam, normalisers, counters) and '
                          'append to --out; --budget is the total over all resumed jobs')
@@ -57,7 +64,10 @@ def main(argv=None):
                            seed=a.seed, device=a.device, on_row=emit, save_model=a.save_model,
                            eval_precision=a.eval_precision, mode=a.mode,
                            log_dir=a.log_dir, league=a.league, latest_weights_prob=a.latest_weights_prob,
-                           actor_precision=a.actor_precision, replay_gb=a.replay_gb)
+                           actor_precision=a.actor_precision, replay_gb=a.replay_gb,
+                           snapshot_lags=tuple(float(x) for x in a.snapshot_lags.split(',') if x.strip()),
+                           snapshot_games=a.snapshot_games, old_logp=a.old_logp,
+                           league_matrix_n=a.league_matrix)
 
 
 if __name__ == '__main__':

@@ -144,3 +144,20 @@ def test_fused_truncated_is_step_matches_torch(gpu_ops):
         assert abs(float(mf[k]) - float(mr[k])) <= 1e-4 * max(1.0, abs(float(mr[k]))), (k, float(mf[k]), float(mr[k]))
     rel = ((fused.flat.grad - oracle.flat.grad).norm() / oracle.flat.grad.norm()).item()
     assert rel < 1e-4, rel
+
+
+@pytest.mark.skipif(not native.AVAILABLE, reason='native module not built')
+def test_snapshot_evaluation_and_league_matrix_cpu():
+    """Head-to-head evaluation against frozen snapshots (actor/validate.py): every game a league game of the current
+    weights against the snapshot; results counted per game; the league matrix is antisymmetric around ½."""
+    from dotaclient_amd.actor.validate import evaluate_vs_snapshot, league_matrix
+    cfg = get_config('lstm128')
+    torch.manual_seed(1)
+    a, b = Policy(cfg), Policy(cfg)
+    r = evaluate_vs_snapshot(a, b.state_dict(), n_games=6, device='cpu', seed=3, max_dota_time=12.0, threads=2)
+    assert r['games'] >= 6 and 0.0 <= r['win_rate'] <= 1.0
+    assert r['wins'] + r['losses'] + r['draws'] == r['games']
+    m = league_matrix([('v0', a.state_dict()), ('v1', b.state_dict())], cfg, n_games=4, device='cpu',
+                      max_dota_time=12.0, threads=2)
+    w = m['win_rate']
+    assert m['labels'] == ['v0', 'v1'] and w[0][0] == 0.5 and abs(w[0][1] + w[1][0] - 1.0) < 1e-9
