@@ -102,9 +102,15 @@ def parse():
     ap.add_argument('--e2e-games', type=int, default=3072)
     ap.add_argument('--e2e-threads', type=int, default=0,
                     help='actor host threads of the node loop (0 = from the CPU share, in [1, 14])')
-    ap.add_argument('--e2e-actor-precision', default='bf16', choices=['bf16', 'fp32', 'fp8'],
-                    help='policy step of the node loop\'s actors (fp8: the BASELINE config-5 step; the loop measured '
-                         '1.15-1.20 vs ≈1.0 M steps/s, its kernels co-run better beside the learner\'s recurrence)')
+    ap.add_argument('--e2e-actor-precision', default='fp32', choices=['bf16', 'fp32', 'fp8'],
+                    help='policy step of the node loop\'s actors: fp32 = the reference actor\'s precision (IEEE fp32 '
+                         'products, F32ActorPolicy; the credited e2e number); bf16 / fp8 as extras (--e2e-extra)')
+    ap.add_argument('--e2e-extra', type=float, default=10.0,
+                    help='seconds of the same node loop with the bf16 actor policy step (extra field e2e_bf16; 0 = off)')
+    ap.add_argument('--e2e-old-logp', default='learner', choices=['learner', 'actor'],
+                    help="PPO's old log-probs and GAE values in the node loops: the learner's per-iteration policy_old "
+                         "forward (reference optimizer.py:279, 474; V-trace against the actor's log-probs) or the "
+                         "actor's from collection time")
     ap.add_argument('--e2e-actor-procs', type=int, default=1,
                     help='actor processes per rank in the node loop (games and threads split over them)')
     ap.add_argument('--e2e-mode', default='process', choices=['process', 'thread'],
@@ -475,7 +481,7 @@ def main():
             from dotaclient_amd.learner.e2e import measure_e2e, measure_e2e_node
             kw = dict(model=args.model, device=device, duration=args.e2e, games=args.e2e_games,
                       threads=args.e2e_threads, seq_len=args.seq_len, precision=args.precision,
-                      pack=bool(args.e2e_pack))
+                      pack=bool(args.e2e_pack), old_logp=args.e2e_old_logp)
             progress('e2e start')
             if args.e2e_mode == 'process':
                 e2e = measure_e2e_node(transport=args.e2e_transport, progress=progress, idle_probe=args.e2e_probe,
@@ -490,6 +496,25 @@ def main():
         if any(errs) and 'error' not in e2e:
             e2e = {'error': f'failed on rank(s) {[i for i, x in enumerate(errs) if x]}'}
 
+    e2e_bf16 = None
+    if (args.e2e > 0 and args.e2e_extra > 0 and use_cuda and args.e2e_mode == 'process'
+            and args.e2e_actor_precision != 'bf16'):
+        # the same node loop with the bf16 actor policy step (extra; the credited e2e runs the reference precision)
+        try:
+            from dotaclient_amd.learner.e2e import measure_e2e_node
+            progress('e2e-bf16 start')
+            e2e_bf16 = measure_e2e_node(
+                model=args.model, device=device, duration=args.e2e_extra, games=args.e2e_games,
+                threads=args.e2e_threads, seq_len=args.seq_len, precision=args.precision, pack=bool(args.e2e_pack),
+                transport=args.e2e_transport, progress=progress, idle_probe=0.0, actor_precision='bf16',
+                old_logp=args.e2e_old_logp)
+        except Exception as e:
+            e2e_bf16 = {'error': repr(e)}
+        progress(f'e2e-bf16 done: {e2e_bf16.get("error", "ok")}')
+        errs = gather('error' in e2e_bf16)
+        if any(errs) and 'error' not in e2e_bf16:
+            e2e_bf16 = {'error': f'failed on rank(s) {[i for i, x in enumerate(errs) if x]}'}
+
     league_replay = None
     if args.league_replay_extra > 0 and use_cuda and args.e2e_mode == 'process' and cfg.rnn == 'lstm':
         # BASELINE config 5 (presets.py league-replay): the same node loop with a PFSP league of past versions
@@ -503,7 +528,7 @@ def main():
                 threads=args.e2e_threads, seq_len=args.seq_len, precision=args.precision, pack=bool(args.e2e_pack),
                 transport=args.e2e_transport, progress=progress, idle_probe=0.0, league='pfsp',
                 latest_weights_prob=0.8, actor_precision='fp8', replay_gb=args.league_replay_gb,
-                replay_prefill=bool(args.league_replay_prefill))
+                replay_prefill=bool(args.league_replay_prefill), old_logp=args.e2e_old_logp)
         except Exception as e:
             league_replay = {'error': repr(e)}
         progress(f'league-replay done: {league_replay.get("error", "ok")}')
@@ -523,7 +548,8 @@ def main():
             e2e_5v5 = measure_e2e_node(
                 model='5v5', device=device, duration=args.e2e_5v5_extra, games=max(1, args.e2e_games // 5),
                 threads=args.e2e_threads, seq_len=args.seq_len, precision=args.precision, pack=bool(args.e2e_pack),
-                transport=args.e2e_transport, progress=progress, idle_probe=0.0)
+                transport=args.e2e_transport, progress=progress, idle_probe=0.0,
+                actor_precision=args.e2e_actor_precision, old_logp=args.e2e_old_logp)
         except Exception as e:
             e2e_5v5 = {'error': repr(e)}
         progress(f'e2e-5v5 done: {e2e_5v5.get("error", "ok")}')
@@ -581,6 +607,7 @@ def main():
             'weights_sha16_per_rank': shas,
             'actor': actor,
             'e2e': e2e,
+            'e2e_bf16': e2e_bf16,
             'league_replay': league_replay,
             'e2e_5v5': e2e_5v5,
             'host_placement': hosts,

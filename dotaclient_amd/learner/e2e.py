@@ -40,7 +40,8 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
                 threads: int = 14, seq_len: int = 1400, batch_size: int = 8, seq_per_epoch: int = 16,
                 epochs: int = 1, precision: str = 'fp32', max_dota_time: float = 600.0, rollout_size: int = 9999,
                 queue_size: int = 64, warmup_iterations: int = 2, max_iterations: Optional[int] = None,
-                log_dir: Optional[str] = None, prefetch: int = 32, pack: bool = False) -> Dict[str, float]:
+                log_dir: Optional[str] = None, prefetch: int = 32, pack: bool = False,
+                old_logp: str = 'learner') -> Dict[str, float]:
     from ..actor.vec import VecActor
     from ..actor.weights import WeightStore
     from ..transport.broker import InProcBroker
@@ -51,7 +52,7 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
     cfg = OptimizerConfig(log_dir=tmp, epochs=epochs, seq_per_epoch=seq_per_epoch, batch_size=batch_size,
                           seq_len=seq_len, model=model, precision=precision, device=str(device), checkpoint_keep=2,
                           run_local=True, xp_timeout=300.0, histogram_freq=10 ** 9, async_checkpoint=True,
-                          prefetch_rollouts=prefetch, pack_sequences=pack)
+                          prefetch_rollouts=prefetch, pack_sequences=pack, old_logp=old_logp)
     opt = DotaOptimizer(cfg, broker)                       # publishes model version 0
     ws = WeightStore(model, device='cpu')
     from concurrent.futures import ThreadPoolExecutor
@@ -99,6 +100,7 @@ def _learner_loop(opt, duration, warmup_iterations, max_iterations, counters, ch
     makes data-parallel ranks stop on the same iteration (every rank runs the same number of DP steps)."""
     from .optimizer import DotaOptimizer
     rows = []
+    _learner_loop.metrics = {}
     it = opt.iteration_start
     for _ in range(warmup_iterations):
         opt.run_iteration(it)
@@ -126,6 +128,11 @@ def _learner_loop(opt, duration, warmup_iterations, max_iterations, counters, ch
                      m.get('time/stage', float('nan')), m.get('time/gather', float('nan')),
                      m.get('time/stage_wait', float('nan')), m.get('time/stage_copy', float('nan')),
                      m.get('time/stage_release', float('nan'))))
+        for k, v in m.items():      # PPO / off-policy diagnostics of the window (means, _learner_loop.metrics)
+            if k in ('approx_kl', 'clipfrac', 'avg_weight_age') or k.startswith('offpolicy/'):
+                acc = _learner_loop.metrics.setdefault(k, [0.0, 0])
+                acc[0] += float(v)
+                acc[1] += 1
         e = check()
         if e:
             raise e
@@ -252,7 +259,8 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                      transport: str = 'auto', backend: str = 'auto', idle_probe: float = 3.0,
                      report=None, record_consumed: int = 0, progress=None, pack: bool = False,
                      league: Optional[str] = None, latest_weights_prob: float = 1.0, actor_precision: str = 'bf16',
-                     replay_gb: float = 0.0, actor_procs: int = 1, replay_prefill: bool = False) -> Dict[str, float]:
+                     replay_gb: float = 0.0, actor_procs: int = 1, replay_prefill: bool = False,
+                     old_logp: str = 'learner') -> Dict[str, float]:
     """The reference's node topology end to end (optimizer.py:144-150, 274-287; ks-app/components/optimizer.jsonnet:
     79-174): ONE experience queue per node fed by actor processes, ``WORLD_SIZE`` learner ranks (one per GPU, DDP
     over RCCL) consuming disjoint rollouts from it as competing consumers, and rank 0 alone checkpointing and
@@ -359,7 +367,7 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                               backend=backend, checkpoint_keep=2, run_local=True, xp_timeout=120.0,
                               histogram_freq=10 ** 9, async_checkpoint=dev.type == 'cuda',
                               prefetch_rollouts=prefetch, record_consumed=record_consumed, pack_sequences=pack,
-                              replay_gb=replay_gb, replay_prefill=replay_prefill)
+                              replay_gb=replay_gb, replay_prefill=replay_prefill, old_logp=old_logp)
         opt = DotaOptimizer(cfg, broker, checkpoint=rank == 0)     # rank 0 publishes model version 0
         say(f'e2e: learner ready ({transport} broker {addr}); waiting for the actor process')
         t_ready = time.time() + 900
@@ -441,6 +449,7 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
     mine['actor_idle_steps_per_s'] = idle
     mine['ingest_decode'] = ingest_diag          # decode threads over the window (claims, waits, decode seconds)
     mine['actor_gpu_busy_steps_per_s'] = gpu_busy
+    mine['learner_metrics'] = {k: a / max(n, 1) for k, (a, n) in getattr(_learner_loop, 'metrics', {}).items()}
     mine['report'] = extra
     per_rank = [mine]
     if pdist.is_distributed():
@@ -477,7 +486,10 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                          replay_sequences=(len(opt.replay) if opt is not None and opt.replay is not None else 0),
                          replay_capacity=(opt.replay.capacity if opt is not None and opt.replay is not None else 0),
                          replay_fill=(opt.replay.fill_fraction if opt is not None and opt.replay is not None else 0.),
-                         replay_prefill=replay_prefill)
+                         replay_prefill=replay_prefill,
+                         # PPO's old log-probs / GAE values: the learner's per-iteration policy_old forward (included
+                         # in every rate above) or the actor's from collection time
+                         old_logp=old_logp)
     return out
 
 

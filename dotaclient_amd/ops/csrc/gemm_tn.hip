@@ -69,6 +69,8 @@ struct Args {
   float* slab;          // [splits][M][N] fp32 partials (splits > 1), then [splits][M] column-sum partials
   float* colsum;        // optional: colsum[m] (+)= Σ_k A[k][m] (a bias gradient), computed by the tn == 0 tiles
   int M, N, K, kc, splits, tiles_n, accumulate;
+  unsigned* tickets;    // exact kernel, splits > 1: per-tile arrival counters (self-cleaning) — the last workgroup of a
+                        // tile sums its slabs in split order (no separate reduce launch); nullptr: gemm_tn_reduce
 };
 
 struct Rsrc {
@@ -542,6 +544,57 @@ __global__ __launch_bounds__(kThreads, 2) void gemm_tn_exact_kernel(Args a) {
         }
       }
     }
+  if (a.splits == 1 || a.tickets == nullptr) return;
+  // ---- split-K fold: the LAST workgroup of this tile to finish sums the tile's slabs in split order (deterministic
+  // whichever workgroup arrives last) and writes C (and the column sums). Release: this workgroup's slab stores are
+  // made visible device-wide (cross-XCD: the L2s are per XCD) before it takes its ticket; acquire before the reads.
+  __shared__ unsigned s_last;
+  __threadfence();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(a.tickets + tile, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    s_last = prev == (unsigned)(a.splits - 1) ? 1u : 0u;
+  }
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  const size_t plane = (size_t)a.M * a.N;
+  const int n4t = BN / 4;                                   // float4 columns of a full tile
+  for (int q = threadIdx.x; q < BM * n4t; q += kThreads) {
+    const int m = m_base + q / n4t, n = n_base + 4 * (q % n4t);
+    if (m >= a.M || n >= a.N) continue;                     // (N % 4 == 0: checked by the host)
+    const f32x4* src = reinterpret_cast<const f32x4*>(a.slab + (size_t)m * a.N + n);
+    const size_t pl4 = plane / 4;
+    f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+    int sp = 0;
+    for (; sp + 3 < a.splits; sp += 4) {                    // 4 loads in flight, summed in split order
+      const f32x4 v0 = __builtin_nontemporal_load(src + (size_t)(sp + 0) * pl4);
+      const f32x4 v1 = __builtin_nontemporal_load(src + (size_t)(sp + 1) * pl4);
+      const f32x4 v2 = __builtin_nontemporal_load(src + (size_t)(sp + 2) * pl4);
+      const f32x4 v3 = __builtin_nontemporal_load(src + (size_t)(sp + 3) * pl4);
+      sum += v0;
+      sum += v1;
+      sum += v2;
+      sum += v3;
+    }
+    for (; sp < a.splits; ++sp) sum += __builtin_nontemporal_load(src + (size_t)sp * pl4);
+    float* cp = a.C + (size_t)(a.perm ? a.perm[m] : m) * a.ldc + n;
+    if (a.accumulate) {
+      sum[0] += cp[0]; sum[1] += cp[1]; sum[2] += cp[2]; sum[3] += cp[3];
+    }
+    cp[0] = sum[0]; cp[1] = sum[1]; cp[2] = sum[2]; cp[3] = sum[3];
+  }
+  if (do_cs && threadIdx.x < BM) {
+    const int m = m_base + threadIdx.x;
+    if (m < a.M) {
+      const float* cs_part = a.slab + (size_t)a.splits * plane + m;
+      float v = 0.f;
+      for (int sp = 0; sp < a.splits; ++sp) v += cs_part[(size_t)sp * a.M];
+      float* cp = a.colsum + (a.perm ? a.perm[m] : m);
+      *cp = a.accumulate ? *cp + v : v;
+    }
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(a.tickets + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Fixed-order (deterministic) sum of the split-K slabs, optional row map / accumulate. A block of 256 threads owns
@@ -645,6 +698,25 @@ extern "C" void dca_gemm_tn_plan(int M, int N, int K, int* splits, int* kc, int*
   *tiles = t;
 }
 
+// Split-K fold tickets: one persistent, zero-initialised pool of per-tile counters; every launch takes the next
+// region round-robin (each tile's last workgroup resets its counter, so a region is clean again when its kernel ends).
+// Regions are baked into captured graphs: 1 M counters are ≈ 5 000 step captures before a region is handed out again,
+// and only kernels running at the same time could collide.
+constexpr int kFoldMaxSplits = 64;
+constexpr size_t kTicketPool = 1u << 20;
+static unsigned* fold_tickets(int tiles) {
+  static unsigned* pool = nullptr;
+  static size_t next = 0;
+  if (pool == nullptr) {
+    if (hipMalloc(reinterpret_cast<void**>(&pool), kTicketPool * sizeof(unsigned)) != hipSuccess) return nullptr;
+    if (hipMemset(pool, 0, kTicketPool * sizeof(unsigned)) != hipSuccess) return nullptr;
+  }
+  if (next + (size_t)tiles > kTicketPool) next = 0;
+  unsigned* r = pool + next;
+  next += (size_t)(tiles + 63) / 64 * 64;
+  return r;
+}
+
 // f32 = 0: A, B, B0 bf16; f32 = 1: fp32 operands (bf16x3 split MFMA); f32 = 2: fp32 operands, exact fp32 MFMA
 extern "C" hipError_t dca_gemm_tn(const void* A, int lda, const void* B, int ldb, const void* B0, int split_rows,
                                   float* C, int ldc, const int* perm, int accumulate, int M, int N, int K, float* slab,
@@ -652,13 +724,22 @@ extern "C" hipError_t dca_gemm_tn(const void* A, int lda, const void* B, int ldb
   if (B0 && split_rows > (f32 ? 32 : BK)) return hipErrorInvalidValue;   // B0 is read by a chunk's first slab only
   int splits, kc, tiles;
   dca_gemm_tn_plan(M, N, K, &splits, &kc, &tiles, f32);
+  // exact kernel: the slabs are folded by each tile's last workgroup (no reduce launch, no second pass over the
+  // slabs by another kernel) when the split list is short — a long one (the 5v5 ∂W_qkv over 716 800 unit rows: ≈170
+  // splits of 3 tiles) keeps the many-workgroup reduce kernel. DCA_GEMM_FOLD=0: always the reduce kernel (A/B)
+  static const bool fold_on = [] { const char* e = getenv("DCA_GEMM_FOLD"); return !(e && e[0] == '0'); }();
+  unsigned* tickets = nullptr;
+  if (f32 == 2 && splits > 1 && splits <= kFoldMaxSplits && (N % 4) == 0 && fold_on) {
+    tickets = fold_tickets(tiles);
+    if (tickets == nullptr) return hipErrorOutOfMemory;
+  }
   Args a{A, lda, B, ldb, B0 ? B0 : B, B0 ? split_rows : 0, C, ldc, perm, slab, colsum, M, N, K, kc, splits,
-         (N + BN - 1) / BN, accumulate};
+         (N + BN - 1) / BN, accumulate, tickets};
   if (f32 == 2) hipLaunchKernelGGL(gemm_tn_exact_kernel, dim3(tiles, splits), dim3(kThreads), 0, st, a);
   else if (f32) hipLaunchKernelGGL(gemm_tn_kernel<true>, dim3(tiles, splits), dim3(kThreads), 8 * kImgF32, st, a);
   else hipLaunchKernelGGL(gemm_tn_kernel<false>, dim3(tiles, splits), dim3(kThreads), 4 * kTileBytes, st, a);
   DCA_CHECK_LAUNCH();
-  if (splits > 1) {
+  if (splits > 1 && tickets == nullptr) {
     int lp = 0;
     while (lp < 4 && (2 << lp) <= splits) ++lp;            // P = 2^lp ≤ min(16, splits)
     const int n = M * (N / 4), opb = 256 >> lp;
