@@ -549,12 +549,20 @@ class DotaOptimizer:
         lp, v = lp.reshape(L), v.reshape(L)
         valid = x['valid'][:L]
         nv = valid.sum().clamp_min(1.0)
+        # a row whose recorded action the learner gives no probability (−inf: a mask that excludes it) or a padding
+        # row keeps the actor's log-prob: a −inf denominator would make the PPO ratio NaN
+        ok = torch.isfinite(lp) & (valid > 0)
+        bad = ((~torch.isfinite(lp)).float() * valid).sum()
+        lp = torch.where(ok, lp, x['logp'][:L])
+        v = torch.where(torch.isfinite(v), v, torch.zeros_like(v))
         dlt = (lp - x['logp'][:L]) * valid
         w = torch.exp(dlt.clamp(max=30.0))
         m = {'offpolicy/behaviour_kl': -dlt.sum() / nv,
              'offpolicy/rho_mean': (w.clamp(max=self.cfg.vtrace_rho_bar) * valid).sum() / nv,
              'offpolicy/rho_truncated': ((w > self.cfg.vtrace_rho_bar).float() * valid).sum() / nv,
-             'offpolicy/max_abs_logratio': dlt.abs().max()}
+             'offpolicy/max_abs_logratio': dlt.abs().max(),
+             'offpolicy/logratio_gt1_frac': ((dlt.abs() > 1.0).float() * valid).sum() / nv,
+             'offpolicy/nonfinite_rows': bad}
         return lp, v, m
 
     def _staging(self, name: str, shape, dtype, pin: bool) -> torch.Tensor:

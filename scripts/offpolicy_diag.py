@@ -27,8 +27,12 @@ def main(precision='fp32', steps=6, pack=True):
     va = VecActor(ws, 256, sent.append, device='cuda', seed=5, rollout_size=9999, max_dota_time=600.0,
                   hidden_stride=1400, threads=8, stagger=True, precision=precision)
     t0 = time.time()
-    while len(sent) < 48 and time.time() - t0 < 120:
+    total, seen = 0, 0
+    while time.time() - t0 < 180 and total < 26 * 1400:
         va.step()
+        for b in sent[seen:]:
+            total += decode(b).length
+        seen = len(sent)
     va.close()
     rs = [decode(b) for b in sent]
     cfg = OptimizerConfig(log_dir='/tmp/dca_offdiag', batch_size=8, seq_len=1400, seq_per_epoch=16, epochs=1,
@@ -36,14 +40,11 @@ def main(precision='fp32', steps=6, pack=True):
     opt = DotaOptimizer(cfg, InProcBroker())
     opt.policy.load_state_dict(ws.latest_weights()[1])
     opt.learner.after_load_weights()
-    n_seq = 0
-    use = []
-    for r in rs:
-        use.append(r)
-        n_seq = -(-sum(x.length for x in use) // 1400) if pack else sum(-(-x.length // 1400) for x in use)
-        if n_seq >= 24:
-            break
-    d = opt._ingest_device(use, 16)
+    st = opt._ingest_pipeline(thread=False).stage(rs)
+    n = min(16, st.n_seq - st.n_seq % 8)
+    assert n >= 16, (st.n_seq, len(rs))
+    d = opt._finish_ingest(st, n)
+    use = rs
     prox = {k: float(v) for k, v in d.pop('_prox').items()}
     out = {'actor_precision': precision, 'rollouts': len(use), 'prox': prox}
     pool = opt._iteration_pool(d, 16)
