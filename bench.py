@@ -107,10 +107,13 @@ def parse():
                          'products, F32ActorPolicy; the credited e2e number); bf16 / fp8 as extras (--e2e-extra)')
     ap.add_argument('--e2e-extra', type=float, default=10.0,
                     help='seconds of the same node loop with the bf16 actor policy step (extra field e2e_bf16; 0 = off)')
-    ap.add_argument('--e2e-old-logp', default='learner', choices=['learner', 'actor'],
-                    help="PPO's old log-probs and GAE values in the node loops: the learner's per-iteration policy_old "
-                         "forward (reference optimizer.py:279, 474; V-trace against the actor's log-probs) or the "
-                         "actor's from collection time")
+    ap.add_argument('--e2e-advantages', default='vtrace-step', choices=['vtrace-step', 'vtrace-iteration', 'gae'],
+                    help="PPO advantages of the node loops' stale experience: V-trace inside every learner step from "
+                         "the step's own values (default), the per-iteration policy_old forward (reference "
+                         "optimizer.py:279, 474) + V-trace, or GAE from the actor's values")
+    ap.add_argument('--e2e-old-logp', default='actor', choices=['learner', 'actor'],
+                    help="the PPO ratio's denominator: the actor's behaviour log-prob, or the learner's policy_old "
+                         "(needs --e2e-advantages vtrace-iteration)")
     ap.add_argument('--e2e-actor-procs', type=int, default=1,
                     help='actor processes per rank in the node loop (games and threads split over them)')
     ap.add_argument('--e2e-mode', default='process', choices=['process', 'thread'],
@@ -481,7 +484,7 @@ def main():
             from dotaclient_amd.learner.e2e import measure_e2e, measure_e2e_node
             kw = dict(model=args.model, device=device, duration=args.e2e, games=args.e2e_games,
                       threads=args.e2e_threads, seq_len=args.seq_len, precision=args.precision,
-                      pack=bool(args.e2e_pack), old_logp=args.e2e_old_logp)
+                      pack=bool(args.e2e_pack), old_logp=args.e2e_old_logp, advantages=args.e2e_advantages)
             progress('e2e start')
             if args.e2e_mode == 'process':
                 e2e = measure_e2e_node(transport=args.e2e_transport, progress=progress, idle_probe=args.e2e_probe,
@@ -507,7 +510,7 @@ def main():
                 model=args.model, device=device, duration=args.e2e_extra, games=args.e2e_games,
                 threads=args.e2e_threads, seq_len=args.seq_len, precision=args.precision, pack=bool(args.e2e_pack),
                 transport=args.e2e_transport, progress=progress, idle_probe=0.0, actor_precision='bf16',
-                old_logp=args.e2e_old_logp)
+                old_logp=args.e2e_old_logp, advantages=args.e2e_advantages)
         except Exception as e:
             e2e_bf16 = {'error': repr(e)}
         progress(f'e2e-bf16 done: {e2e_bf16.get("error", "ok")}')
@@ -528,7 +531,7 @@ def main():
                 threads=args.e2e_threads, seq_len=args.seq_len, precision=args.precision, pack=bool(args.e2e_pack),
                 transport=args.e2e_transport, progress=progress, idle_probe=0.0, league='pfsp',
                 latest_weights_prob=0.8, actor_precision='fp8', replay_gb=args.league_replay_gb,
-                replay_prefill=bool(args.league_replay_prefill), old_logp=args.e2e_old_logp)
+                replay_prefill=bool(args.league_replay_prefill), old_logp=args.e2e_old_logp, advantages=args.e2e_advantages)
         except Exception as e:
             league_replay = {'error': repr(e)}
         progress(f'league-replay done: {league_replay.get("error", "ok")}')
@@ -549,7 +552,7 @@ def main():
                 model='5v5', device=device, duration=args.e2e_5v5_extra, games=max(1, args.e2e_games // 5),
                 threads=args.e2e_threads, seq_len=args.seq_len, precision=args.precision, pack=bool(args.e2e_pack),
                 transport=args.e2e_transport, progress=progress, idle_probe=0.0,
-                actor_precision=args.e2e_actor_precision, old_logp=args.e2e_old_logp)
+                actor_precision=args.e2e_actor_precision, old_logp=args.e2e_old_logp, advantages=args.e2e_advantages)
         except Exception as e:
             e2e_5v5 = {'error': repr(e)}
         progress(f'e2e-5v5 done: {e2e_5v5.get("error", "ok")}')

@@ -63,6 +63,12 @@ def build_parser():
     ap.add_argument('--pack-sequences', type=str2bool, default=False,
                     help='pack whole episodes into the seq_len sequences with episode-start resets instead of '
                          'padding every rollout (non-reference layout; GPU device ingest)')
+    ap.add_argument('--advantages', type=str, default='vtrace-step',
+                    choices=['vtrace-step', 'vtrace-iteration', 'gae'],
+                    help='PPO advantages of stale / replayed experience: V-trace inside every learner step (default), '
+                         'the per-iteration policy_old forward + V-trace, or GAE from the actor values')
+    ap.add_argument('--old-logp', type=str, default='actor', choices=['actor', 'learner'],
+                    help="PPO ratio denominator: the actor's behaviour log-prob or the learner's policy_old")
     ap.add_argument('--gamma', type=float, default=0.98)
     ap.add_argument('--gae-lambda', type=float, default=0.95)
     ap.add_argument('--clip-eps', type=float, default=0.1)
@@ -101,6 +107,7 @@ def main(argv=None):
                           artifact_url=args.artifact_url,
                           iterations=args.iterations, algo=args.algo, model=args.model_preset, gamma=args.gamma,
                           gae_lambda=args.gae_lambda, clip_eps=args.clip_eps, max_grad_norm=args.max_grad_norm,
+                          advantages=args.advantages, old_logp=args.old_logp,
                           compat_value_bug=args.compat_value_bug, device=device, backend=args.backend,
                           precision=args.precision, graph=bool(args.graph), async_checkpoint=bool(args.async_checkpoint),
                           checkpoint_keep=args.checkpoint_keep, replay_gb=args.replay_gb,

@@ -35,7 +35,8 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
                        mode: str = '1v1', log_dir: Optional[str] = None, league: Optional[str] = None,
                        latest_weights_prob: float = 0.8, actor_precision: str = 'bf16',
                        replay_gb: float = 0.0, snapshot_lags=(120.0, 300.0, 600.0), snapshot_games: int = 64,
-                       old_logp: str = 'learner', league_matrix_n: int = 0) -> List[Dict]:
+                       old_logp: str = 'actor', league_matrix_n: int = 0,
+                       advantages: str = 'vtrace-step') -> List[Dict]:
     """Train for ``budget`` seconds (evaluations excluded) and return the evaluation rows (the first one before
     any training). ``on_row`` is called with every row as it is produced; ``save_model``: path that receives the
     final weights (a reference-format state_dict file). ``eval_precision``: the validation games' policy step.
@@ -72,7 +73,8 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
                           learning_rate=lr, entropy_coef=entropy_coef, checkpoint_keep=1 if log_dir else 2,
                           run_local=True,
                           xp_timeout=300.0, histogram_freq=10 ** 9, async_checkpoint=True, prefetch_rollouts=64,
-                          pack_sequences=bool(pack), seed=seed, replay_gb=replay_gb, old_logp=old_logp)
+                          pack_sequences=bool(pack), seed=seed, replay_gb=replay_gb, old_logp=old_logp,
+                          advantages=advantages)
     opt = DotaOptimizer(cfg, broker)
     ws = WeightStore(model, device='cpu')
     loader = ThreadPoolExecutor(1, thread_name_prefix='weights')

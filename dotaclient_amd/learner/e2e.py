@@ -41,7 +41,7 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
                 epochs: int = 1, precision: str = 'fp32', max_dota_time: float = 600.0, rollout_size: int = 9999,
                 queue_size: int = 64, warmup_iterations: int = 2, max_iterations: Optional[int] = None,
                 log_dir: Optional[str] = None, prefetch: int = 32, pack: bool = False,
-                old_logp: str = 'learner') -> Dict[str, float]:
+                old_logp: str = 'actor', advantages: str = 'vtrace-step') -> Dict[str, float]:
     from ..actor.vec import VecActor
     from ..actor.weights import WeightStore
     from ..transport.broker import InProcBroker
@@ -52,7 +52,8 @@ def measure_e2e(model: str = 'lstm512', device='cuda', duration: float = 20.0, g
     cfg = OptimizerConfig(log_dir=tmp, epochs=epochs, seq_per_epoch=seq_per_epoch, batch_size=batch_size,
                           seq_len=seq_len, model=model, precision=precision, device=str(device), checkpoint_keep=2,
                           run_local=True, xp_timeout=300.0, histogram_freq=10 ** 9, async_checkpoint=True,
-                          prefetch_rollouts=prefetch, pack_sequences=pack, old_logp=old_logp)
+                          prefetch_rollouts=prefetch, pack_sequences=pack, old_logp=old_logp,
+                          advantages=advantages)
     opt = DotaOptimizer(cfg, broker)                       # publishes model version 0
     ws = WeightStore(model, device='cpu')
     from concurrent.futures import ThreadPoolExecutor
@@ -260,7 +261,7 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                      report=None, record_consumed: int = 0, progress=None, pack: bool = False,
                      league: Optional[str] = None, latest_weights_prob: float = 1.0, actor_precision: str = 'bf16',
                      replay_gb: float = 0.0, actor_procs: int = 1, replay_prefill: bool = False,
-                     old_logp: str = 'learner') -> Dict[str, float]:
+                     old_logp: str = 'actor', advantages: str = 'vtrace-step') -> Dict[str, float]:
     """The reference's node topology end to end (optimizer.py:144-150, 274-287; ks-app/components/optimizer.jsonnet:
     79-174): ONE experience queue per node fed by actor processes, ``WORLD_SIZE`` learner ranks (one per GPU, DDP
     over RCCL) consuming disjoint rollouts from it as competing consumers, and rank 0 alone checkpointing and
@@ -367,7 +368,8 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                               backend=backend, checkpoint_keep=2, run_local=True, xp_timeout=120.0,
                               histogram_freq=10 ** 9, async_checkpoint=dev.type == 'cuda',
                               prefetch_rollouts=prefetch, record_consumed=record_consumed, pack_sequences=pack,
-                              replay_gb=replay_gb, replay_prefill=replay_prefill, old_logp=old_logp)
+                              replay_gb=replay_gb, replay_prefill=replay_prefill, old_logp=old_logp,
+                              advantages=advantages)
         opt = DotaOptimizer(cfg, broker, checkpoint=rank == 0)     # rank 0 publishes model version 0
         say(f'e2e: learner ready ({transport} broker {addr}); waiting for the actor process')
         t_ready = time.time() + 900
@@ -487,9 +489,9 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
                          replay_capacity=(opt.replay.capacity if opt is not None and opt.replay is not None else 0),
                          replay_fill=(opt.replay.fill_fraction if opt is not None and opt.replay is not None else 0.),
                          replay_prefill=replay_prefill,
-                         # PPO's old log-probs / GAE values: the learner's per-iteration policy_old forward (included
-                         # in every rate above) or the actor's from collection time
-                         old_logp=old_logp)
+                         # PPO advantages (in-step V-trace / per-iteration policy_old forward / actor GAE — whatever
+                         # they cost is inside every rate above) and the PPO ratio's denominator
+                         advantages=advantages, old_logp=old_logp)
     return out
 
 

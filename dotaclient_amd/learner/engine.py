@@ -68,6 +68,12 @@ class LossConfig:
     # log-prob at the iteration's weights, learner/optimizer.py old_logp='learner'); 'tis' = off-policy policy
     # gradient with the truncated importance weight min(1, π/π_old) (replayed experience, V-trace style)
     offpolicy: str = 'clip'
+    # V-trace inside the step: the advantages and value targets of every minibatch recomputed from the step's own
+    # values and log-probs against the actor's behaviour log-prob (``logp_old``) — batches carry the per-row ``vt``
+    # field {reward, bootstrap, valid, last} (learner/optimizer.py advantages='vtrace-step'); ``adv`` / ``ret`` unused
+    vtrace: bool = False
+    vtrace_rho_bar: float = 1.0
+    vtrace_c_bar: float = 1.0
 
 
 class Learner:
@@ -144,10 +150,45 @@ class Learner:
         actions = split_heads(batch['actions'], self.counts)
         masks = split_heads(batch['masks'], self.counts)
         if cfg.algo == 'ppo':
-            return ppo_loss(logits, values, actions, masks, batch['adv'], batch['ret'], batch['logp_old'],
-                            cfg.clip_eps, cfg.entropy_coef, cfg.vf_coef, stable=stable, offpolicy=cfg.offpolicy)
+            adv, ret, extra = batch['adv'], batch['ret'], {}
+            if cfg.vtrace:
+                adv, ret, extra = self._vtrace_torch(batch, logits, values, masks, actions)
+            loss, metrics = ppo_loss(logits, values, actions, masks, adv, ret, batch['logp_old'],
+                                     cfg.clip_eps, cfg.entropy_coef, cfg.vf_coef, stable=stable,
+                                     offpolicy=cfg.offpolicy)
+            metrics.update(extra)
+            return loss, metrics
         return vpg_loss(logits, values, actions, masks, batch['norm_ret'], batch['ret'], cfg.entropy_coef,
                         cfg.vf_coef, compat_value_bug=cfg.compat_value_bug, stable=stable)
+
+    def _vtrace_torch(self, batch, logits, values, masks, actions):
+        """The torch oracle of the fused step's in-step V-trace (ops/scan.py vtrace_step over time-major rows): the
+        step's own (detached) values and log-probs of the recorded actions against ``logp_old``; advantages
+        normalised over the valid rows. Returns (adv (B,S), ret (B,S), off-policy metrics)."""
+        from ..constants import EPS
+        from ..ops.scan import vtrace_step
+        from .losses import sampled_logp
+        cfg = self.cfg
+        B, S = batch['env'].shape[:2]
+        tm = (lambda x: x.detach().float().reshape(B, S, *x.shape[2:]).transpose(0, 1).reshape(B * S, *x.shape[2:]))
+        with torch.no_grad():
+            lp = sampled_logp(logits, actions, masks, stable=not self.policy.config.compat_bugs)
+            adv, ret, st = vtrace_step(tm(values.squeeze(-1)).cpu(), tm(lp).cpu(), tm(batch['logp_old']).cpu(),
+                                       tm(batch['vt']).cpu(), B, S, cfg.gamma, cfg.gae_lambda, cfg.vtrace_rho_bar,
+                                       cfg.vtrace_c_bar)
+            dev = batch['env'].device
+            back = (lambda x: x.reshape(S, B).t().contiguous().to(dev))
+            adv, ret = back(adv), back(ret)
+            v = batch['vt'][..., 2].float()
+            n = v.sum().clamp_min(1.0)
+            mu = (adv * v).sum() / n
+            sd = (((adv - mu) ** 2 * v).sum() / n).sqrt()
+            adv = ((adv - mu) / (sd + EPS)) * v
+            s = st.sum(0)
+            extra = {'offpolicy/rho_mean': (s[0] / s[3].clamp_min(1)).to(dev),
+                     'offpolicy/rho_truncated': (s[1] / s[3].clamp_min(1)).to(dev),
+                     'offpolicy/behaviour_kl': (s[2] / s[3].clamp_min(1)).to(dev)}
+        return adv, ret, extra
 
     def _fwd_bwd(self, batch):
         self.dp.zero_grad()
@@ -178,6 +219,8 @@ class Learner:
             out[k] = v.transpose(0, 1).reshape(S * B, *v.shape[2:]).contiguous()
         if 'reset' in batch:                # sequence packing: episode-start flags (B,S) u8 → time-major rows
             out['reset'] = batch['reset'].transpose(0, 1).reshape(S * B).contiguous()
+        if 'vt' in batch:                   # in-step V-trace rows {reward, bootstrap, valid, last} (B,S,4)
+            out['vt'] = batch['vt'].transpose(0, 1).reshape(S * B, 4).contiguous()
         for k in ('h0', 'c0'):
             if k in batch:
                 out[k] = batch[k].contiguous()
@@ -187,7 +230,7 @@ class Learner:
         """Minibatch of replay rows ``idx`` gathered straight into time-major rows: one index_select per field
         over the pool viewed as (capacity·S, …) — no batch-major copy, no transpose."""
         B = idx.numel()
-        fields = self.STEP_FIELDS + (('reset',) if 'reset' in replay.data else ())
+        fields = self.STEP_FIELDS + tuple(k for k in ('reset', 'vt') if k in replay.data)
         if idx.is_cuda:                 # one HIP launch for every field (ops/csrc/glue.hip replay_gather)
             from .. import ops
             seq = [k for k in ('h0', 'c0') if k in replay.data]
@@ -239,8 +282,8 @@ class Learner:
 
     def _metrics_from_vec(self, vec):
         from ..models.pipelined import METRIC_NAMES
-        names = METRIC_NAMES if self.cfg.algo == 'ppo' else [n for n in METRIC_NAMES
-                                                              if n not in ('approx_kl', 'clipfrac')]
+        names = [n for n in METRIC_NAMES if (self.cfg.algo == 'ppo' or n not in ('approx_kl', 'clipfrac'))
+                 and (self.cfg.vtrace or not n.startswith('offpolicy/'))]
         return {n: vec[METRIC_NAMES.index(n)] for n in names}
 
     def _graph_ready(self) -> bool:

@@ -92,12 +92,21 @@ class OptimizerConfig:
     # non-compat: pack whole zero-state rollouts first-fit into the free tails of the iteration's sequences (episode
     # starts flagged, the recurrence resets h, c there) instead of padding each rollout to seq_len (learner/ingest.py)
     pack_sequences: bool = False
-    # PPO's old log-probs and GAE values: 'learner' = the reference's policy_old (optimizer.py:279, 474) — once per
-    # iteration, before its minibatches, the learner evaluates the iteration's experience at the iteration's starting
-    # weights (Learner.evaluate_sequences, the step's forward kernels) and computes V-trace GAE (ops/scan.py 'vtrace':
-    # truncated importance weights against the actor's behaviour log-prob) from its own values; 'actor' = the
-    # actor's log-probs / values from collection time (on-policy only at weight age 0). Device ingest only.
-    old_logp: str = 'learner'
+    # PPO advantages / value targets of stale experience (PPO + device ingest):
+    # * 'vtrace-step' (default): V-trace INSIDE every learner step — the minibatch's advantages and value targets from
+    #   the step's own values and log-probs (the weights being trained) with truncated importance weights against the
+    #   actor's behaviour log-probs (LossConfig.vtrace, ops/csrc/scan.hip vtrace_step_kernel): correct for fresh and
+    #   for replayed experience alike, ≈0.1 ms per step;
+    # * 'vtrace-iteration': the reference's policy_old (optimizer.py:279, 474) — once per iteration, before its
+    #   minibatches, the iteration's experience is evaluated at the iteration's starting weights (Learner.
+    #   evaluate_sequences, the step's forward kernels) and V-trace GAE computed from those values (a whole extra
+    #   forward per iteration: ≈30 % of the node loop's rate);
+    # * 'gae': the actor's values from collection time (on-policy only at weight age 0; rounds 1-5).
+    advantages: str = 'vtrace-step'
+    # the PPO ratio's denominator: 'actor' = the behaviour log-prob (the clip is a trust region around what the actors
+    # played — measured stable at weight age 18); 'learner' = the iteration's starting policy (with 'vtrace-iteration';
+    # decoupled PPO: measured to drift and collapse at weight age ≥ 6, profiles/r6_*)
+    old_logp: str = 'actor'
     vtrace_rho_bar: float = 1.0
     vtrace_c_bar: float = 1.0
     # policy term on replayed experience (replay_gb / replay_capacity): 'tis' = truncated importance weight
@@ -185,10 +194,20 @@ class DotaOptimizer:
         if pretrained is not None:
             self.policy.load_state_dict(ckpt.load_model_file(pretrained), strict=False)
         replay_on = bool(cfg.replay_capacity or cfg.replay_gb)
+        if cfg.advantages not in ('vtrace-step', 'vtrace-iteration', 'gae'):
+            raise ValueError(f'advantages must be vtrace-step, vtrace-iteration or gae, got {cfg.advantages!r}')
+        dev_ingest = (cfg.ingest if cfg.ingest != 'auto' else
+                      ('device' if (cfg.device == 'auto' and torch.cuda.is_available()) or
+                       str(cfg.device).startswith('cuda') else 'host'))
+        self.vtrace_step = cfg.advantages == 'vtrace-step' and cfg.algo == 'ppo' and dev_ingest == 'device'
         lc = LossConfig(algo=cfg.algo, learning_rate=cfg.learning_rate, entropy_coef=cfg.entropy_coef,
                         vf_coef=cfg.vf_coef, clip_eps=cfg.clip_eps, gamma=cfg.gamma, gae_lambda=cfg.gae_lambda,
                         max_grad_norm=cfg.max_grad_norm, compat_value_bug=cfg.compat_value_bug,
-                        offpolicy=cfg.replay_offpolicy if replay_on else 'clip')
+                        # (in-step V-trace: the advantages already carry the truncated IS weight; the policy term
+                        # stays PPO's clip around the behaviour policy, the trust region measured stable at high lag)
+                        offpolicy=cfg.replay_offpolicy if (replay_on and not self.vtrace_step) else 'clip',
+                        vtrace=self.vtrace_step,
+                        vtrace_rho_bar=cfg.vtrace_rho_bar, vtrace_c_bar=cfg.vtrace_c_bar)
         prec = cfg.precision
         if prec == 'fp32-exact' and self.device.type == 'cuda' and cfg.batch_size > 32:
             # the exact VALU recurrence runs 1 / 2 / 4 sequences per XCD chain (8 teams): at most 32 per minibatch
@@ -206,8 +225,11 @@ class DotaOptimizer:
             raise ValueError('pack_sequences needs the device ingest (ingest="device")')
         if cfg.old_logp not in ('learner', 'actor'):
             raise ValueError(f'old_logp must be learner or actor, got {cfg.old_logp!r}')
-        if cfg.old_logp == 'learner' and self.ingest != 'device' and cfg.algo == 'ppo':
-            logger.warning('old_logp=learner needs the device ingest: the host ingest keeps the actor\'s log-probs')
+        if cfg.old_logp == 'learner' and cfg.advantages != 'vtrace-iteration':
+            raise ValueError("old_logp='learner' needs advantages='vtrace-iteration' (the per-iteration policy_old pass)")
+        if cfg.advantages != 'gae' and self.ingest != 'device' and cfg.algo == 'ppo':
+            logger.warning('advantages=%s needs the device ingest: the host ingest computes GAE from the actor\'s '
+                           'values', cfg.advantages)
         # per-team EMA(0.99) reward statistics as device state (mean, std, initialised) for the device ingest path
         self.ema = torch.zeros(self.MAX_TEAMS, 3, device=self.device)
         for team in self.running.mean:
@@ -246,9 +268,10 @@ class DotaOptimizer:
                                    self.device, fit)
                     gb = fit
             cap = cfg.replay_capacity or HbmReplay.capacity_for_bytes(gb * 1e9, cfg.seq_len,
-                                                                       self.policy_cfg.layout, hid, pk)
+                                                                       self.policy_cfg.layout, hid, pk,
+                                                                       vtrace=self.vtrace_step)
             self.replay = HbmReplay(cap, cfg.seq_len, self.policy_cfg.layout, hid, self.device, seed=cfg.seed,
-                                    reset=pk)
+                                    reset=pk, vtrace=self.vtrace_step)
             logger.info('on-device replay: %d sequences, %.2f GB', cap, self.replay.nbytes / 1e9)
         self.time_last_step = time.time()
         if self.iteration_start == 1:
@@ -504,7 +527,7 @@ class DotaOptimizer:
         keys = [self._team_key(r.team_id) for r in rollouts]
         values, mode, lr = (x.get('values'), 'gae', None) if st.gae_mode else (None, 'discount', None)
         prox = None
-        if st.gae_mode and cfg.old_logp == 'learner':
+        if st.gae_mode and cfg.advantages == 'vtrace-iteration':
             # the reference's policy_old, refreshed every iteration (optimizer.py:279, 474): the iteration's
             # sequences evaluated at the weights its first minibatch will see (this is enqueued behind the previous
             # iteration's steps in stream order — the look-ahead — so those ARE the weights it reads), its log-probs
@@ -512,7 +535,8 @@ class DotaOptimizer:
             # against the actor's behaviour log-probs (stale experience: the actor played version − weight age)
             lp, values, prox = self._evaluate_iteration(x, st.n_seq)
             lr = lp - x['logp']
-            d['logp_old'] = lp
+            if cfg.old_logp == 'learner':
+                d['logp_old'] = lp
             mode = 'vtrace'
         out = compute_returns(x['rewards'], values, st.off.astype(np.int32),
                               st.lens, [r.bootstrap_value for r in rollouts], [bool(r.done) for r in rollouts], keys,
@@ -520,6 +544,8 @@ class DotaOptimizer:
                               factor=self.running.factor, lr=lr, rho_bar=cfg.vtrace_rho_bar, c_bar=cfg.vtrace_c_bar)
         d['ret'], d['adv'] = out['ret'], out['adv']
         d['norm_ret'] = out['norm'] if not st.gae_mode else out['adv']
+        if self.vtrace_step and st.gae_mode:
+            d['vt'] = self._vtrace_rows(x, st)
         n_rows = n_keep * S
         d = {k: v[:n_rows].reshape((n_keep, S) + tuple(v.shape[1:])) for k, v in d.items()}
         if self.policy.is_recurrent:
@@ -531,6 +557,37 @@ class DotaOptimizer:
         if prox is not None:
             d['_prox'] = prox          # (metrics; popped by run_iteration before the data is used)
         return d
+
+    def _vtrace_rows(self, x: Dict[str, torch.Tensor], st) -> torch.Tensor:
+        """Per-row inputs of the in-step V-trace (LossConfig.vtrace) in the padded layout: (L, 4) = {summed reward,
+        bootstrap, valid, last}. ``last`` marks where an episode segment ends inside its sequence: the rollout's last
+        row (bootstrap 0 at a terminal, else the actor's bootstrap value) and every sequence boundary the rollout
+        runs past (bootstrap: the actor's value of the next row, the first row of the next sequence)."""
+        S = self.cfg.seq_len
+        L = st.L
+        dev = x['rewards'].device
+        vt = torch.zeros(L, 4, device=dev)
+        vt[:, 0] = x['rewards'][:L].float().sum(1)
+        vt[:, 2] = x['valid'][:L]
+        starts = np.asarray(st.off[:-1], np.int64)
+        lens = np.asarray(st.lens, np.int64)
+        ends = starts + lens - 1
+        boot = np.asarray([0.0 if r.done else float(r.bootstrap_value) for r in st.rollouts], np.float32)
+        bnd = [np.arange((a // S + 1) * S - 1, a + T - 1, S, dtype=np.int64) for a, T in zip(starts, lens)]
+        bnd = np.concatenate(bnd) if bnd else np.zeros(0, np.int64)
+        cuda = dev.type == 'cuda'
+
+        def up(a):      # small host arrays: pinned (the caching host allocator keeps a block until its copy ran)
+            t = torch.from_numpy(a)
+            return t.pin_memory().to(dev, non_blocking=True) if cuda else t
+        e_d, b_d = up(ends), up(boot)
+        vt[:, 3].index_fill_(0, e_d, 1.0)
+        vt[:, 1].index_copy_(0, e_d, b_d)
+        if len(bnd):
+            n_d = up(bnd)
+            vt[:, 3].index_fill_(0, n_d, 1.0)
+            vt[:, 1].index_copy_(0, n_d, x['values'][:L].float().index_select(0, n_d + 1))
+        return vt
 
     def _evaluate_iteration(self, x: Dict[str, torch.Tensor], n_seq: int):
         """Learner-side log-probs and values of the expanded iteration ``x`` (padded layout, ``n_seq`` sequences of
@@ -584,7 +641,7 @@ class DotaOptimizer:
         step replays with its gather inside) instead of an ``index_select`` of every field per minibatch followed by
         the step's own batch-major → time-major copies."""
         pool = getattr(self, '_pool', None)
-        fields = [k for k in Learner.STEP_FIELDS + ('h0', 'c0', 'reset') if k in data]
+        fields = [k for k in Learner.STEP_FIELDS + ('h0', 'c0', 'reset', 'vt') if k in data]
         if pool is None or pool.capacity < n or set(pool.data) != set(fields) or any(
                 pool.data[k].shape[1:] != data[k].shape[1:] or pool.data[k].dtype != data[k].dtype for k in fields):
             cap = max(n, 2 * self.cfg.seq_per_epoch)

@@ -10,8 +10,10 @@ per field on the GPU (``(capacity, seq_len, …)``), so
 * capacity is chosen from a byte budget (``capacity_for_bytes``): one LSTM-512 1v1 sequence of 1400 steps is
   ≈2.4 MB, so 200 GB holds ≈80k sequences (≈115 M timesteps).
 
-Sampling is uniform over the filled part, optionally restricted to the ``recent`` newest sequences (on-policy-ish
-PPO typically samples the newest window; off-policy correction is the PPO ratio against the stored ``logp_old``).
+Sampling is uniform over the filled part, optionally restricted to the ``recent`` newest sequences. Off-policy
+correction: the PPO ratio against the stored behaviour ``logp_old``, and — with the in-step V-trace (``vtrace``,
+learner/optimizer.py advantages='vtrace-step') — every sampled sequence's advantages and value targets recomputed
+at the weights being trained, with truncated importance weights against that behaviour log-prob.
 """
 from __future__ import annotations
 
@@ -25,7 +27,7 @@ from ..constants import UnitLayout
 _F32 = torch.float32
 
 
-def field_specs(S: int, layout: UnitLayout, hidden: Optional[int], reset: bool = False):
+def field_specs(S: int, layout: UnitLayout, hidden: Optional[int], reset: bool = False, vtrace: bool = False):
     U = layout.max_units
     A = 21 + U
     spec = {
@@ -35,15 +37,18 @@ def field_specs(S: int, layout: UnitLayout, hidden: Optional[int], reset: bool =
     }
     if reset:                       # sequence packing: episode-start flags (learner/ingest.py SequencePacker)
         spec['reset'] = ((S,), torch.uint8)
+    if vtrace:                      # in-step V-trace rows {reward, bootstrap, valid, last}: replayed sequences get
+        spec['vt'] = ((S, 4), _F32)  # their advantages recomputed at every sampling, from the weights being trained
     if hidden:
         spec['h0'] = ((hidden,), _F32)
         spec['c0'] = ((hidden,), _F32)
     return spec
 
 
-def bytes_per_sequence(S: int, layout: UnitLayout, hidden: Optional[int], reset: bool = False) -> int:
+def bytes_per_sequence(S: int, layout: UnitLayout, hidden: Optional[int], reset: bool = False,
+                       vtrace: bool = False) -> int:
     n = 0
-    for shape, dt in field_specs(S, layout, hidden, reset).values():
+    for shape, dt in field_specs(S, layout, hidden, reset, vtrace).values():
         k = 1
         for d in shape:
             k *= d
@@ -53,13 +58,13 @@ def bytes_per_sequence(S: int, layout: UnitLayout, hidden: Optional[int], reset:
 
 class HbmReplay:
     def __init__(self, capacity: int, S: int, layout: UnitLayout, hidden: Optional[int], device, seed: int = 0,
-                 reset: bool = False):
+                 reset: bool = False, vtrace: bool = False):
         if capacity < 1:
             raise ValueError('replay capacity must be >= 1')
         self.capacity = int(capacity)
         self.S = S
         self.device = torch.device(device)
-        self.specs = field_specs(S, layout, hidden, reset)
+        self.specs = field_specs(S, layout, hidden, reset, vtrace)
         self.data = {k: torch.zeros((self.capacity,) + shape, dtype=dt, device=self.device)
                      for k, (shape, dt) in self.specs.items()}
         self.version = torch.full((self.capacity,), -1, dtype=torch.long, device=self.device)
@@ -73,8 +78,9 @@ class HbmReplay:
         self.host_sampling = False
 
     @staticmethod
-    def capacity_for_bytes(budget: float, S: int, layout: UnitLayout, hidden: Optional[int], reset: bool = False) -> int:
-        return max(1, int(budget // bytes_per_sequence(S, layout, hidden, reset)))
+    def capacity_for_bytes(budget: float, S: int, layout: UnitLayout, hidden: Optional[int], reset: bool = False,
+                           vtrace: bool = False) -> int:
+        return max(1, int(budget // bytes_per_sequence(S, layout, hidden, reset, vtrace)))
 
     @property
     def nbytes(self) -> int:

@@ -299,10 +299,15 @@ class FusedPolicy:
             h0 = torch.zeros(B, H, device=dev)
             c0 = torch.zeros(B, H, device=dev)
         self.refresh()
+        vt = batch.get('vt') if getattr(cfg, 'vtrace', False) else None
         part, logp = PipelinedPolicyLoss.apply(self, batch['units'].contiguous(), batch['env'].contiguous(), actions,
                                                masks, adv, ret, lpo, nret, norms, h0.contiguous(), c0.contiguous(),
-                                               rst, *self.params)
+                                               rst, vt, *self.params)
         loss, metrics = assemble_loss(part, norms, cfg, ret, N, S)
+        if getattr(self, 'vtrace_stats', None) is not None:
+            st = self.vtrace_stats.sum(0)
+            for i, k in enumerate(('offpolicy/rho_mean', 'offpolicy/rho_truncated', 'offpolicy/behaviour_kl')):
+                metrics[k] = st[i] / st[3].clamp_min(1.0)
         return loss, metrics
 
     def check_error(self):

@@ -44,7 +44,10 @@ LDZ = 160
 DIRECT_GEMM_GRADS = ('rnn.weight_hh_l0', 'rnn.weight_ih_l0', 'affine_pre_rnn.weight', 'affine_pre_rnn.bias')
 
 METRIC_NAMES = ['loss', 'policy_loss', 'entropy_loss', 'advantage_loss', 'entropy', 'advantage', 'approx_kl',
-                'clipfrac', 'entropy/enum', 'entropy/x', 'entropy/y', 'entropy/target_unit']
+                'clipfrac', 'entropy/enum', 'entropy/x', 'entropy/y', 'entropy/target_unit',
+                # in-step V-trace (LossConfig.vtrace): mean truncated importance weight, fraction truncated, and the
+                # behaviour KL estimate mean(log μ − log π) of the minibatch
+                'offpolicy/rho_mean', 'offpolicy/rho_truncated', 'offpolicy/behaviour_kl']
 
 
 def _frag_order(w: torch.Tensor) -> torch.Tensor:
@@ -234,7 +237,7 @@ def fused_step_tm(fp, *args, **kw):
 
 def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], units_t, env_t, act_t, msk_t, adv_t,
                    ret_t, lpo_t, nret_t, norms, h0, c0, B: int, S: int, gout: Optional[Dict[str, torch.Tensor]] = None,
-                   reset_t: Optional[torch.Tensor] = None):
+                   reset_t: Optional[torch.Tensor] = None, vt_t: Optional[torch.Tensor] = None):
     """Loss partials and all parameter gradients of one minibatch, from TIME-MAJOR rows (row = t·B + b).
 
     ``W`` = :class:`WeightImages` views, ``P`` = fp32 parameters (for the small fp32 weights used directly).
@@ -398,11 +401,29 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         hw = ((W['wcat256'], nil), (W['wcatT256'], nil), W['bcat256'])
     else:
         hw = (W['wcat_s'], W['wcatT_s'], W['bcat256'])
+    fp.vtrace_stats = None
     for (t0, t1), done in zip(spans, fwd_done):
         main.wait_event(done)
         r0, r1 = t0 * B, t1 * B
         xh = hs16[t0:t1].view(-1, H)
         zc = C.rowmm_out256(xh, hw[0][0], hw[0][1], hw[2])   # (n, 256), padding columns 0
+        if vt_t is not None:
+            # V-trace INSIDE the step (LossConfig.vtrace): this step's own values (z column 149) and log-probs of the
+            # recorded actions (a first, forward-only pass of the heads kernel) against the actor's behaviour
+            # log-probs (lpo_t) give the advantages and value targets — for fresh and replayed experience alike,
+            # at the weights being trained (ops/csrc/scan.hip vtrace_step_kernel), then normalised over the valid rows
+            from ..constants import EPS
+            from ..ops.scan import vtrace_step
+            assert one, 'in-step V-trace runs as one time chunk'
+            zero = fp.scratch('vt_zero', (N,), torch.float32, dev)
+            _, _, _, lp_a = C.heads_loss(zc, emb, act_t, msk_t, zero, zero, zero, zero, norms, 0, False, S, B,
+                                         float(lc.clip_eps), 0.0, 0.0, dz_bf16=False, precise=exact)
+            adv_v, ret_t, vstats = vtrace_step(None, lp_a, lpo_t, vt_t, B, S, lc.gamma, lc.gae_lambda,
+                                               getattr(lc, 'vtrace_rho_bar', 1.0), getattr(lc, 'vtrace_c_bar', 1.0),
+                                               z=zc, vcol=149)
+            adv_t = torch.empty_like(adv_v)
+            C.adv_normalize(adv_v, vt_t[:, 2].contiguous(), adv_t, float(EPS))
+            fp.vtrace_stats = vstats
         dz16, dtl_c, part, lp = C.heads_loss(zc, emb[r0:r1], act_t[r0:r1], msk_t[r0:r1], adv_t[r0:r1],
                                              ret_t[r0:r1], lpo_t[r0:r1], nret_t[r0:r1], norms, algo,
                                              bool(lc.compat_value_bug), S, B, float(lc.clip_eps),
@@ -626,7 +647,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
 
 class PipelinedPolicyLoss(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, fp, units, env, actions, masks, adv, ret, logp_old, nret, norms, h0, c0, reset, *params):
+    def forward(ctx, fp, units, env, actions, masks, adv, ret, logp_old, nret, norms, h0, c0, reset, vt, *params):
         P = dict(zip(fp.param_names, params))
         B, S, U, _ = units.shape
         N = B * S
@@ -636,7 +657,8 @@ class PipelinedPolicyLoss(torch.autograd.Function):
         W = fp.weight_images().refresh(fp.C)
         rst_t = reset.reshape(B, S).transpose(0, 1).reshape(N).contiguous() if reset is not None else None
         part, logp, grads = fused_step_tm(fp, W, P, units_t, env_t, tm(actions), tm(masks), tm(adv), tm(ret),
-                                          tm(logp_old), tm(nret), norms, h0, c0, B, S, reset_t=rst_t)
+                                          tm(logp_old), tm(nret), norms, h0, c0, B, S, reset_t=rst_t,
+                                          vt_t=tm(vt.reshape(N, 4)) if vt is not None else None)
         ctx.grads = [grads.get(nm) for nm in fp.param_names]
         ctx.fp = fp
         logp_b = logp.view(S, B).t().reshape(N)        # back to batch-major (B·S) row order
@@ -647,7 +669,7 @@ class PipelinedPolicyLoss(torch.autograd.Function):
     def backward(ctx, gpart, _glogp):
         ctx.fp.apply_direct_grads(ctx.grads, gpart[15])
         ctx.grads = None
-        return (None,) * (13 + len(ctx.fp.param_names))
+        return (None,) * (14 + len(ctx.fp.param_names))
 
 
 def train_direct(fp, batch_tm: Dict[str, torch.Tensor], B: int, S: int) -> torch.Tensor:
@@ -681,15 +703,21 @@ def train_direct(fp, batch_tm: Dict[str, torch.Tensor], B: int, S: int) -> torch
         h0 = torch.zeros(B, H, device=dev)
         c0 = torch.zeros(B, H, device=dev)
     gout = {nm: P[nm].grad for nm in DIRECT_GEMM_GRADS if nm in P}
+    vt = batch_tm.get('vt') if getattr(lc, 'vtrace', False) else None
+    if getattr(lc, 'vtrace', False) and vt is None:
+        raise ValueError('LossConfig.vtrace needs the per-row vt field (learner/optimizer.py advantages="vtrace-step")')
     part, _, grads = fused_step_tm(fp, W, P, batch_tm['units'], batch_tm['env'], batch_tm['actions'],
                                    batch_tm['masks'], batch_tm['adv'], batch_tm['ret'], batch_tm['logp_old'],
                                    batch_tm['norm_ret'], norms, h0, c0, B, S, gout=gout,
-                                   reset_t=batch_tm.get('reset'))
+                                   reset_t=batch_tm.get('reset'), vt_t=vt)
     fp.apply_direct_grads([grads.get(nm) for nm in fp.param_names], None,
                           written=set(gout) | set(fp.early_applied))
     out = torch.empty(16, device=dev)
     C.loss_assemble(part, norms, N, 0 if lc.algo == 'ppo' else 1, float(lc.entropy_coef), float(lc.vf_coef), out,
                     S=S, compat_value_bug=bool(lc.compat_value_bug))
+    if fp.vtrace_stats is not None:
+        st = fp.vtrace_stats.sum(0)
+        out[12:15] = st[:3] / st[3].clamp_min(1.0)
     return out
 
 

@@ -743,6 +743,27 @@ void loss_prep(torch::Tensor act, torch::Tensor ws, torch::Tensor norms) {
 int64_t loss_prep_ws_elems() { return 5 * dca_loss_prep_blocks() + 1; }
 
 // Loss scalar + metrics (out (16) f32) from the heads/loss partials part (R,16).
+// V-trace inside the learner step (scan.hip vtrace_step_kernel): z (N, ldz) heads logits with the value in column
+// vcol, lp / mu (N) the step's and the behaviour log-probs, vt (N, 4) {reward, bootstrap, valid, last}, time-major rows
+// of B sequences × S steps. Returns (adv (N), ret (N), stats (B, 4) = Σ valid {ρ, truncated, mu − lp, 1}).
+std::vector<torch::Tensor> vtrace_step(torch::Tensor z, int64_t vcol, torch::Tensor lp, torch::Tensor mu,
+                                       torch::Tensor vt, int64_t B, int64_t S, double gamma, double lam,
+                                       double rho_bar, double c_bar) {
+  CHECK_DEV(z); CHECK_DT(z, at::kFloat); CHECK_F32(lp); CHECK_F32(mu); CHECK_F32(vt);
+  const int64_t N = B * S;
+  TORCH_CHECK(z.dim() == 2 && z.size(0) == N && z.stride(1) == 1 && vcol >= 0 && vcol < z.size(1),
+              "vtrace_step: z (B·S, ldz) with the value column inside");
+  TORCH_CHECK(lp.numel() == N && mu.numel() == N && vt.numel() == 4 * N, "vtrace_step: per-row inputs");
+  auto adv = torch::empty({N}, z.options());
+  auto ret = torch::empty({N}, z.options());
+  auto stats = torch::empty({B, 4}, z.options());
+  hip_check(dca_vtrace_step(ptr<float>(z), (int)z.stride(0), (int)vcol, ptr<float>(lp), ptr<float>(mu),
+                            ptr<float>(vt), ptr<float>(adv), ptr<float>(ret), ptr<float>(stats), (int)B, (int)S,
+                            (float)gamma, (float)lam, (float)rho_bar, (float)c_bar, cur_stream()),
+            "dca_vtrace_step");
+  return {adv, ret, stats};
+}
+
 // Test utility (glue.hip): hold `blocks`·(1/8) CUs of XCD `xcd` for `seconds` on the current stream; returns the
 // per-workgroup placement record (XCC id + 1 where it held a CU, 0 elsewhere).
 torch::Tensor occupy_xcd(int64_t xcd, int64_t blocks, double seconds, torch::Tensor like) {
@@ -1147,6 +1168,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "[K/32][R][32] images, the dpre_dx operand layout)", py::arg("src"), py::arg("slab_major") = false);
   m.def("enc_small_grads", &enc_small_grads, "entity-encoder type-bias and env-layer gradients in one pass");
   m.def("replay_gather", &replay_gather, "minibatch gather from an HBM replay pool into time-major rows (one launch)");
+  m.def("vtrace_step", &vtrace_step, "V-trace advantages / value targets of a minibatch from the step's own values",
+        py::arg("z"), py::arg("vcol"), py::arg("lp"), py::arg("mu"), py::arg("vt"), py::arg("B"), py::arg("S"),
+        py::arg("gamma"), py::arg("lam"), py::arg("rho_bar") = 1.0, py::arg("c_bar") = 1.0);
   m.def("occupy_xcd", &occupy_xcd, "test utility: hold CUs of one XCD for a while (160 KB LDS per workgroup)",
         py::arg("xcd"), py::arg("blocks"), py::arg("seconds"), py::arg("like"));
   m.def("returns_scan", &returns_scan, "segmented reverse scan: discounted returns / GAE / V-trace GAE + per-team EMA "

@@ -89,6 +89,9 @@ hipError_t dca_actor_state_prep(const short* pre, float* h, float* c, const floa
 hipError_t dca_lstm_cell(const float* gates, float* h, float* c, short* h16, const float* active, int N, int H,
                          hipStream_t st);
 
+hipError_t dca_vtrace_step(const float* z, int ldz, int vcol, const float* lp, const float* mu, const float* vt,
+                           float* adv, float* ret, float* stats, int B, int S, float gamma, float lam, float rho_bar,
+                           float c_bar, hipStream_t st);
 hipError_t dca_returns(const float* rew, int K, const float* val, const float* lr, const int* off, const int* seglen,
                        const float* boot, const unsigned char* done, const int* keys, int nseg, int max_len,
                        float* ret, float* adv, float* norm, float* stats, const float* ema_in, float* ema_out,

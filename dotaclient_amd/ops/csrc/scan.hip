@@ -199,6 +199,92 @@ __global__ __launch_bounds__(kT) void ema_normalize_kernel(
   for (int t = blockIdx.y * kT + threadIdx.x; t < P; t += gridDim.y * kT) norm[base + t] = (ret[base + t] - m) * inv;
 }
 
+
+// ---- V-trace inside the learner step (time-major rows r = t·B + b of one minibatch) ------------------------------
+// The advantages and value targets of a minibatch from the step's OWN forward: V_t = z[r][vcol] (the heads GEMM's
+// value column) and log π(a_t) = lp[r] (the heads kernel's selected-action log-prob) at the weights of this very
+// step, against the actor's behaviour log-prob mu[r]. vt[r] = {reward, bootstrap, valid, last}: `last` marks the last
+// row of an episode segment inside its sequence (the episode's end — bootstrap 0 if done, else the actor's
+// bootstrap value — or a sequence boundary the rollout continues past — bootstrap the actor's value of the next
+// row). ρ_t = min(ρ̄, w_t), w_t = e^{lp − mu}; A_t = ρ_t·δ_t + γλ·min(c̄, w_t)·A_{t+1} (A_{t+1} = 0 at `last`);
+// adv = A, ret = A + V (V-trace target; GAE(γ, λ) exactly when π = μ). One workgroup per sequence: each thread owns
+// a chunk of steps, the chunks' affine maps are composed by a wave suffix scan + an LDS pass over the 4 waves.
+// stats[b] = Σ over valid rows of {ρ, [w > ρ̄], mu − lp, 1}.
+__global__ __launch_bounds__(kT) void vtrace_step_kernel(
+    const float* __restrict__ z, int ldz, int vcol, const float* __restrict__ lp, const float* __restrict__ mu,
+    const float* __restrict__ vt, float* __restrict__ adv, float* __restrict__ ret, float* __restrict__ stats, int B,
+    int S, float gamma, float lam, float rho_bar, float c_bar) {
+  const int b = blockIdx.x;
+  const int per = (S + kT - 1) / kT;
+  const int lo = min((int)threadIdx.x * per, S), hi = min(lo + per, S);
+  float X = 0.f, p = 1.f;
+  float s_rho = 0.f, s_tr = 0.f, s_kl = 0.f, s_n = 0.f;
+  for (int t = hi - 1; t >= lo; --t) {
+    const size_t r = (size_t)t * B + b;
+    const float4 v4 = *reinterpret_cast<const float4*>(vt + 4 * r);       // reward, bootstrap, valid, last
+    const bool valid = v4.z > 0.f, last = v4.w > 0.f || t == S - 1;
+    const float V = z[r * ldz + vcol];
+    const float nextV = last ? v4.y : z[(r + B) * ldz + vcol];
+    const float dl = lp[r] - mu[r];
+    const float w = __expf(fminf(dl, 30.f));
+    const float rho = fminf(rho_bar, w), cw = fminf(c_bar, w);
+    const float d = valid ? rho * (v4.x + gamma * nextV - V) : 0.f;
+    const float k = (valid && !last) ? gamma * lam * cw : 0.f;
+    adv[r] = d;                                       // parked: the forcing term and the coefficient
+    ret[r] = k;
+    X = d + k * X;
+    p *= k;
+    if (valid) {
+      s_rho += rho;
+      s_tr += w > rho_bar * (1.f + 1e-6f) ? 1.f : 0.f;
+      s_kl += -dl;
+      s_n += 1.f;
+    }
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float xo = __shfl_down(X, o, 64), po = __shfl_down(p, o, 64);
+    if (lane + o < 64) {
+      X = X + p * xo;
+      p = p * po;
+    }
+  }
+  __shared__ float wx[kWaves], wp[kWaves], red[4][kWaves];
+  if (lane == 0) {
+    wx[w] = X;
+    wp[w] = p;
+  }
+  __syncthreads();
+  float y = 0.f;
+  for (int k = kWaves - 1; k > w; --k) y = wx[k] + wp[k] * y;
+  const float x1 = __shfl_down(X, 1, 64), p1 = __shfl_down(p, 1, 64);
+  float carry = (lane == 63) ? y : x1 + p1 * y;
+  for (int t = hi - 1; t >= lo; --t) {
+    const size_t r = (size_t)t * B + b;
+    const float d = adv[r], k = ret[r];
+    carry = d + k * carry;
+    adv[r] = carry;
+    ret[r] = vt[4 * r + 2] > 0.f ? carry + z[r * ldz + vcol] : 0.f;
+  }
+  s_rho = dca::wave_sum(s_rho);
+  s_tr = dca::wave_sum(s_tr);
+  s_kl = dca::wave_sum(s_kl);
+  s_n = dca::wave_sum(s_n);
+  if (lane == 0) {
+    red[0][w] = s_rho;
+    red[1][w] = s_tr;
+    red[2][w] = s_kl;
+    red[3][w] = s_n;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    float v = 0.f;
+#pragma unroll
+    for (int k = 0; k < kWaves; ++k) v += red[threadIdx.x][k];
+    stats[4 * b + threadIdx.x] = v;
+  }
+}
 }  // namespace
 
 extern "C" hipError_t dca_returns(const float* rew, int K, const float* val, const float* lr, const int* off,
@@ -213,6 +299,16 @@ extern "C" hipError_t dca_returns(const float* rew, int K, const float* val, con
   const int by = normalize ? max(1, min(64, (max_len + 4 * kT - 1) / (4 * kT))) : 1;
   hipLaunchKernelGGL(ema_normalize_kernel, dim3(nseg, by), dim3(kT), 0, st, ret, off, keys, stats, nseg, ema_in,
                      ema_out, norm, normalize, factor, eps);
+  DCA_CHECK_LAUNCH();
+  return hipSuccess;
+}
+
+extern "C" hipError_t dca_vtrace_step(const float* z, int ldz, int vcol, const float* lp, const float* mu,
+                                      const float* vt, float* adv, float* ret, float* stats, int B, int S,
+                                      float gamma, float lam, float rho_bar, float c_bar, hipStream_t st) {
+  if (B <= 0 || S <= 0) return hipSuccess;
+  hipLaunchKernelGGL(vtrace_step_kernel, dim3(B), dim3(kT), 0, st, z, ldz, vcol, lp, mu, vt, adv, ret, stats, B, S,
+                     gamma, lam, rho_bar, c_bar);
   DCA_CHECK_LAUNCH();
   return hipSuccess;
 }

@@ -124,3 +124,42 @@ def compute_returns(rew: torch.Tensor, val, off, seglen, boot, done, keys, ema: 
     if m == 0:
         adv = norm if normalize else ret
     return {'ret': ret, 'adv': adv, 'norm': norm, 'stats': stats}
+
+
+def vtrace_step(values: torch.Tensor, lp: torch.Tensor, mu: torch.Tensor, vt: torch.Tensor, B: int, S: int,
+                gamma: float = 0.98, lam: float = 0.95, rho_bar: float = 1.0, c_bar: float = 1.0, z=None,
+                vcol: int = 149):
+    """V-trace inside the learner step over a minibatch's TIME-MAJOR rows (r = t·B + b): ``values`` (N,) the step's
+    own values, ``lp`` (N,) its log-probs of the recorded actions, ``mu`` (N,) the actor's behaviour log-probs, ``vt``
+    (N, 4) = {reward, bootstrap, valid, last} (``last``: the episode segment ends at this row inside its sequence; its
+    successor value is ``bootstrap``). ρ_t = min(ρ̄, e^{lp − mu}), A_t = ρ_t·δ_t + γλ·min(c̄, e^{lp − mu})·A_{t+1};
+    returns (adv = A, ret = A + V on valid rows, stats (B, 4) = Σ valid {ρ, [w > ρ̄], mu − lp, 1}). GPU with ``z``
+    (the heads logits, value in column ``vcol``): the HIP kernel (ops/csrc/scan.hip vtrace_step_kernel); otherwise
+    this torch reference (its oracle)."""
+    if z is not None and z.is_cuda:
+        from . import require
+        return tuple(require().vtrace_step(z, vcol, lp.contiguous(), mu.contiguous(), vt.contiguous(), B, S,
+                                           float(gamma), float(lam), float(rho_bar), float(c_bar)))
+    V = values.reshape(S, B).double()
+    dl = (lp - mu).reshape(S, B).double()
+    v4 = vt.reshape(S, B, 4).double()
+    w = torch.exp(dl.clamp(max=30.0))
+    rho, cw = w.clamp(max=rho_bar), w.clamp(max=c_bar)
+    valid = v4[..., 2] > 0
+    last = v4[..., 3] > 0
+    last[S - 1] = True
+    nextV = torch.cat([V[1:], torch.zeros(1, B, dtype=V.dtype)], 0)
+    nextV = torch.where(last, v4[..., 1], nextV)
+    d = torch.where(valid, rho * (v4[..., 0] + gamma * nextV - V), torch.zeros_like(V))
+    k = torch.where(valid & ~last, gamma * lam * cw, torch.zeros_like(V))
+    A = torch.zeros(S, B, dtype=torch.float64)
+    acc = torch.zeros(B, dtype=torch.float64)
+    for t in range(S - 1, -1, -1):
+        acc = d[t] + k[t] * acc
+        A[t] = acc
+    ret = torch.where(valid, A + V, torch.zeros_like(V))
+    vf = valid.double()
+    stats = torch.stack([(rho * vf).sum(0), ((w > rho_bar * (1 + 1e-6)).double() * vf).sum(0), (-dl * vf).sum(0),
+                         vf.sum(0)], 1)
+    f = torch.float32
+    return A.reshape(-1).to(f), ret.reshape(-1).to(f), stats.to(f)

@@ -43,7 +43,8 @@ def main(argv=None):
                     help='seconds of training: every row also plays the weights from that long ago (comma list, '
                          'empty = off)')
     ap.add_argument('--snapshot-games', type=int, default=64)
-    ap.add_argument('--old-logp', default='learner', choices=['learner', 'actor'])
+    ap.add_argument('--old-logp', default='actor', choices=['learner', 'actor'])
+    ap.add_argument('--advantages', default='vtrace-step', choices=['vtrace-step', 'vtrace-iteration', 'gae'])
     ap.add_argument('--league-matrix', type=int, default=0,
                     help='after the curve: pairwise win rates of this many snapshots spread over the run')
     ap.add_argument('--log-dir', default=None,
@@ -66,7 +67,7 @@ def main(argv=None):
                            log_dir=a.log_dir, league=a.league, latest_weights_prob=a.latest_weights_prob,
                            actor_precision=a.actor_precision, replay_gb=a.replay_gb,
                            snapshot_lags=tuple(float(x) for x in a.snapshot_lags.split(',') if x.strip()),
-                           snapshot_games=a.snapshot_games, old_logp=a.old_logp,
+                           snapshot_games=a.snapshot_games, old_logp=a.old_logp, advantages=a.advantages,
                            league_matrix_n=a.league_matrix)
 
 

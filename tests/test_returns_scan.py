@@ -81,7 +81,7 @@ def test_device_ingest_equals_host_ingest(tmp_path, algo):
     def make(ingest, sub):
         cfg = OptimizerConfig(log_dir=str(tmp_path / sub), batch_size=2, seq_len=32, seq_per_epoch=8, epochs=1,
                               algo=algo, model='lstm128', device='cpu', backend='torch', ingest=ingest,
-                              old_logp='actor')     # (the host ingest keeps the actor's log-probs / values)
+                              advantages='gae')     # (the host ingest: GAE from the actor's values)
         return DotaOptimizer(cfg, InProcBroker())
     host, dev = make('host', 'h'), make('device', 'd')
     for it in range(2):                                  # two rounds: the EMA state carries over
