@@ -506,7 +506,7 @@ def _gpu_busy_probe(opt, steps, seconds: float, batch_size: int, seq_len: int, a
         return float('nan')
     cfg = opt.policy_cfg
     rep = DeviceReplay(2 * batch_size, seq_len, cfg.layout, cfg.hidden if cfg.rnn == 'lstm' else None, opt.device,
-                       seed=5)
+                       seed=5, vtrace=bool(getattr(lrn.cfg, 'vtrace', False)))
     saved = [t.clone() for t in (lrn.flat.flat, lrn.opt.exp_avg, lrn.opt.exp_avg_sq, lrn.opt.steps)]
     n_steps = lrn.n_steps
     lrn.train_step_replay(rep.buf, batch_size)

@@ -106,8 +106,14 @@ def make_batch(B: int, S: int, layout: UnitLayout, hidden: Optional[int], device
     adv = (adv - adv[pv].mean()) / (adv[pv].std() + 1e-8) * step_valid
     n_sel = actions.sum(-1).float()
     logp_old = -(rnd(B, S) * 2.0 + 0.5) * (n_sel > 0)
+    # in-step V-trace rows {reward, bootstrap, valid, last}: each sequence one episode ending at its last valid row
+    # (a terminal: bootstrap 0)
+    last = torch.zeros(B, S)
+    n_valid = step_valid.sum(1).long()
+    last[torch.arange(B), (n_valid - 1).clamp(min=0)] = 1.0
+    vt = torch.stack([rew, torch.zeros(B, S), step_valid, last], -1)
     out = {'env': env, 'units': units, 'actions': actions, 'masks': masks, 'adv': adv, 'ret': ret,
-           'logp_old': logp_old, 'norm_ret': adv.clone(), 'valid': step_valid}
+           'logp_old': logp_old, 'norm_ret': adv.clone(), 'valid': step_valid, 'vt': vt}
     if hidden:
         out['h0'] = torch.randn(B, hidden, generator=g) * 0.1
         out['c0'] = torch.randn(B, hidden, generator=g) * 0.1
@@ -119,9 +125,9 @@ class DeviceReplay:
     :func:`make_batch` data); :meth:`sample` gathers a minibatch on-device — the bench's on-HBM replay source."""
 
     def __init__(self, n_seq: int, S: int, layout: UnitLayout, hidden: Optional[int], device, seed: int = 0,
-                 chunk: int = 16):
+                 chunk: int = 16, vtrace: bool = False):
         from .replay import HbmReplay
-        self.buf = HbmReplay(n_seq, S, layout, hidden, device, seed=seed)
+        self.buf = HbmReplay(n_seq, S, layout, hidden, device, seed=seed, vtrace=vtrace)
         self.buf.host_sampling = True
         for i in range(0, n_seq, chunk):
             self.buf.add(make_batch(min(chunk, n_seq - i), S, layout, hidden, device=device, seed=seed + i))
