@@ -36,7 +36,7 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
                        latest_weights_prob: float = 0.8, actor_precision: str = 'bf16',
                        replay_gb: float = 0.0, snapshot_lags=(120.0, 300.0, 600.0), snapshot_games: int = 64,
                        old_logp: str = 'actor', league_matrix_n: int = 0,
-                       advantages: str = 'vtrace-step') -> List[Dict]:
+                       advantages: str = 'vtrace-step', weight_lag: int = 0) -> List[Dict]:
     """Train for ``budget`` seconds (evaluations excluded) and return the evaluation rows (the first one before
     any training). ``on_row`` is called with every row as it is produced; ``save_model``: path that receives the
     final weights (a reference-format state_dict file). ``eval_precision``: the validation games' policy step.
@@ -78,7 +78,19 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
     opt = DotaOptimizer(cfg, broker)
     ws = WeightStore(model, device='cpu')
     loader = ThreadPoolExecutor(1, thread_name_prefix='weights')
-    broker.subscribe_model(lambda v, b: loader.submit(ws.add_bytes, v, b))
+    if weight_lag > 0:
+        # staleness on demand: the actors get version v only once `weight_lag` newer versions were published (the node
+        # loop's process-mode actors run ≈12-22 versions behind; the in-process actor here ≈2-4)
+        import collections
+        held = collections.deque()
+
+        def delayed(v, b):
+            held.append((v, b))
+            if v == 0 or len(held) > weight_lag:
+                loader.submit(ws.add_bytes, *held.popleft())
+        broker.subscribe_model(delayed)
+    else:
+        broker.subscribe_model(lambda v, b: loader.submit(ws.add_bytes, v, b))
     loader.submit(lambda: None).result()
     lg = None
     if league:

@@ -724,10 +724,12 @@ extern "C" hipError_t dca_gemm_tn(const void* A, int lda, const void* B, int ldb
   if (B0 && split_rows > (f32 ? 32 : BK)) return hipErrorInvalidValue;   // B0 is read by a chunk's first slab only
   int splits, kc, tiles;
   dca_gemm_tn_plan(M, N, K, &splits, &kc, &tiles, f32);
-  // exact kernel: the slabs are folded by each tile's last workgroup (no reduce launch, no second pass over the
-  // slabs by another kernel) when the split list is short — a long one (the 5v5 ∂W_qkv over 716 800 unit rows: ≈170
-  // splits of 3 tiles) keeps the many-workgroup reduce kernel. DCA_GEMM_FOLD=0: always the reduce kernel (A/B)
-  static const bool fold_on = [] { const char* e = getenv("DCA_GEMM_FOLD"); return !(e && e[0] == '0'); }();
+  // exact kernel, DCA_GEMM_FOLD=1: the slabs are folded by each tile's last workgroup (no reduce launch) when the
+  // split list is short. Measured SLOWER and therefore off by default (round 6, same box: learner step 5.88 vs 5.55 ms,
+  // 5v5 exact 10.94 vs 10.63 ms — every workgroup's release fence writes its XCD's dirty L2 lines back before taking
+  // a ticket, and the last workgroup's serial pass over the slabs lands on the step's tail; the separate reduce kernel
+  // overlaps the encoder backward instead; profiles/r6_split_k_fold.md)
+  static const bool fold_on = [] { const char* e = getenv("DCA_GEMM_FOLD"); return e && e[0] == '1'; }();
   unsigned* tickets = nullptr;
   if (f32 == 2 && splits > 1 && splits <= kFoldMaxSplits && (N % 4) == 0 && fold_on) {
     tickets = fold_tickets(tiles);

@@ -45,6 +45,9 @@ def main(argv=None):
     ap.add_argument('--snapshot-games', type=int, default=64)
     ap.add_argument('--old-logp', default='actor', choices=['learner', 'actor'])
     ap.add_argument('--advantages', default='vtrace-step', choices=['vtrace-step', 'vtrace-iteration', 'gae'])
+    ap.add_argument('--weight-lag', type=int, default=0,
+                    help='hold every published version back from the actors until this many newer ones exist '
+                         '(staleness on demand: weight age ≈ lag + the loop\'s own)')
     ap.add_argument('--league-matrix', type=int, default=0,
                     help='after the curve: pairwise win rates of this many snapshots spread over the run')
     ap.add_argument('--log-dir', default=None,
@@ -68,6 +71,7 @@ def main(argv=None):
                            actor_precision=a.actor_precision, replay_gb=a.replay_gb,
                            snapshot_lags=tuple(float(x) for x in a.snapshot_lags.split(',') if x.strip()),
                            snapshot_games=a.snapshot_games, old_logp=a.old_logp, advantages=a.advantages,
+                           weight_lag=a.weight_lag,
                            league_matrix_n=a.league_matrix)
 
 
