@@ -436,6 +436,7 @@ def main():
             from dotaclient_amd.actor.batched import measure_actor_throughput
             mb = measure_actor_throughput(policy, device, n_games=args.actor_games, threads=args.actor_threads)
             mine['policy_step_per_s'] = mb['gpu_steps_per_s']
+            mine['policy_step_pipelined_per_s'] = mb['gpu_pipelined_steps_per_s']
             mine['policy_step_protobuf_featurize_per_s'] = mb['steps_per_s']
         except Exception as e:
             mine['policy_step_error'] = repr(e)
@@ -446,9 +447,13 @@ def main():
             mb = measure_actor_throughput(policy, device, n_games=args.actor_games, threads=args.actor_threads,
                                           precision='fp8')
             mine['policy_step_fp8_per_s'] = mb['gpu_steps_per_s']
+            mine['policy_step_fp8_pipelined_per_s'] = mb['gpu_pipelined_steps_per_s']
             mine['policy_step_fp8_protobuf_featurize_per_s'] = mb['steps_per_s']
             if mine.get('policy_step_per_s'):
                 mine['fp8_vs_bf16_policy_step'] = mb['gpu_steps_per_s'] / mine['policy_step_per_s']
+            if mine.get('policy_step_pipelined_per_s'):
+                mine['fp8_vs_bf16_policy_step_pipelined'] = (mb['gpu_pipelined_steps_per_s']
+                                                             / mine['policy_step_pipelined_per_s'])
         except Exception as e:
             mine['policy_step_fp8_error'] = repr(e)
         if not cfg.entity_attention:
@@ -458,6 +463,7 @@ def main():
                 mb = measure_actor_throughput(policy, device, n_games=args.actor_games, threads=args.actor_threads,
                                               precision='fp32')
                 mine['policy_step_fp32_per_s'] = mb['gpu_steps_per_s']
+                mine['policy_step_fp32_pipelined_per_s'] = mb['gpu_pipelined_steps_per_s']
                 mine['policy_step_fp32_protobuf_featurize_per_s'] = mb['steps_per_s']
             except Exception as e:
                 mine['policy_step_fp32_error'] = repr(e)
@@ -465,6 +471,7 @@ def main():
         progress('actor measurements done')
         actor = dict(ranks[0])
         for k in ('steps_per_s', 'steps_per_s_fp32', 'protobuf_runtime_steps_per_s', 'policy_step_per_s',
+                  'policy_step_pipelined_per_s', 'policy_step_fp8_pipelined_per_s', 'policy_step_fp32_pipelined_per_s',
                   'policy_step_protobuf_featurize_per_s', 'policy_step_fp8_per_s',
                   'policy_step_fp8_protobuf_featurize_per_s', 'policy_step_fp32_per_s',
                   'policy_step_fp32_protobuf_featurize_per_s'):

@@ -80,9 +80,13 @@ class GpuActorPolicy:
     CORE_MODE = 1        # ops/csrc/actor_core.hip: 0 = IEEE fp32 (f32 MFMA), 1 = bf16 operands
 
     def __init__(self, policy: Policy, n_slots: int, device='cuda', seed: int = 0, use_graph: bool = True,
-                 record: bool = True, inputs_from: Optional['GpuActorPolicy'] = None):
+                 record: bool = True, inputs_from: Optional['GpuActorPolicy'] = None, raw: bool = False):
         from .. import ops
         self.C = ops.require()
+        # raw: observations staged as compact raw unit records (features/raw.py, 32 B per unit slot + a 16 B hero
+        # record per slot instead of 40 B of features + an 8 B handle) and featurized by the step's first kernel
+        # (ops/csrc/featurize.hip); the host's native engine then skips the per-unit feature arithmetic
+        self.raw = bool(raw)
         cfg = policy.config
         if cfg.unit_dim != 128 or cfg.env_dim != 128:
             raise ValueError('GpuActorPolicy needs 128-wide unit / env embeddings (the fused encoder kernel)')
@@ -108,9 +112,38 @@ class GpuActorPolicy:
     UNITS_DTYPE, HANDLES_DTYPE = torch.float32, torch.long
 
     def _alloc(self, inputs_from=None):
-        n, U, A, dev = self.n, self.U, self.A, self.device
-        H = self.cfg.hidden
-        pin = dict(pin_memory=True)
+        if self.raw:
+            self._alloc_raw(inputs_from)
+        else:
+            self._alloc_features(inputs_from)
+        self.h_keep, self.h_active = self.in_pack.host['keep'], self.in_pack.host['active']
+        self.h_keep.fill_(1.0)
+        self.h_active.fill_(1.0)
+        self.d_env = self.in_pack.dev['env']
+        self.d_keep = self.in_pack.dev['keep']
+        self.d_active = self.in_pack.dev['active']     # 0 → slot not stepped: LSTM state left untouched
+        self._alloc_state()
+
+    def _alloc_raw(self, inputs_from):
+        n, U, dev = self.n, self.U, self.device
+        self.in_pack = _Pack([('env', (n, 3), torch.float32), ('hero', (n, 4), torch.float32),
+                              ('raw', (n, U, 8), torch.int32), ('keep', (n, 1), torch.float32),
+                              ('active', (n,), torch.float32)], dev)
+        if inputs_from is not None:
+            if (inputs_from.n, inputs_from.U) != (n, U) or not inputs_from.raw:
+                raise ValueError('inputs_from: slot count / layout / staging mismatch')
+            self.h_env, self.h_hero, self.h_raw = inputs_from.h_env, inputs_from.h_hero, inputs_from.h_raw
+        else:
+            self.h_env, self.h_hero, self.h_raw = (self.in_pack.host[k] for k in ('env', 'hero', 'raw'))
+        self._shared_inputs = inputs_from is not None
+        self.h_units = self.h_handles = None
+        self.d_hero, self.d_raw = self.in_pack.dev['hero'], self.in_pack.dev['raw']
+        # the featurize kernel's outputs: device-only, in the dtypes the step's kernels read
+        self.d_units = torch.zeros(n, U, 10, dtype=self.UNITS_DTYPE, device=dev)
+        self.d_handles = torch.full((n, U), -1, dtype=self.HANDLES_DTYPE, device=dev)
+
+    def _alloc_features(self, inputs_from):
+        n, U, dev = self.n, self.U, self.device
         ud, hd = self.UNITS_DTYPE, self.HANDLES_DTYPE
         # ONE packed pinned staging buffer and ONE device mirror per direction: a step's inputs cross PCIe in one copy
         # and its outputs come back in one (each separate copy was a DMA dispatch of its own inside the graph)
@@ -126,15 +159,14 @@ class GpuActorPolicy:
             self.h_env, self.h_units, self.h_handles = (self.in_pack.host[k] for k in ('env', 'units', 'handles'))
             self.h_handles.fill_(-1)
         self._shared_inputs = inputs_from is not None
-        self.h_keep, self.h_active = self.in_pack.host['keep'], self.in_pack.host['active']
-        self.h_keep.fill_(1.0)
-        self.h_active.fill_(1.0)
-        self.d_env = self.in_pack.dev['env']
-        self.d_keep = self.in_pack.dev['keep']
-        self.d_active = self.in_pack.dev['active']     # 0 → slot not stepped: LSTM state left untouched
         # the kernels read the staged dtypes as they are (fp8 step: fp16 features, int32 handles)
         self.d_units = self.in_pack.dev['units']
         self.d_handles = self.in_pack.dev['handles']
+
+    def _alloc_state(self):
+        n, A, dev = self.n, self.A, self.device
+        H = self.cfg.hidden
+        pin = dict(pin_memory=True)
         self.h = torch.zeros(n, H, device=dev)
         self.c = torch.zeros(n, H, device=dev)
         self.z = torch.zeros(n, LDZ, device=dev)                 # head logits [q | enum | x | y | value | pad]
@@ -261,6 +293,8 @@ class GpuActorPolicy:
         resets, pre-RNN layer, gates + LSTM cell or the linear layer, heads; bumps the sampler's RNG counter) →
         sampling kernel."""
         C, w, cfg = self.C, self.w, self.cfg
+        if self.raw:
+            C.featurize_raw(self.d_raw, self.d_hero, self.d_units, self.d_handles)
         x896, emb, arg = C.encoder_fwd(self.d_units, self.d_env, w['w1'], w['b1'], w['wt'], w['bt'], w['we'],
                                        w['be'], list(cfg.layout.counts), bool(cfg.compat_bugs),
                                        exact=self.CORE_MODE == 0)
@@ -284,8 +318,12 @@ class GpuActorPolicy:
             # observations staged by the policy this one shares them with: its pinned views, our device regions
             ip = self.in_pack.dev
             ip['env'].copy_(self.h_env, non_blocking=True)
-            ip['units'].copy_(self.h_units, non_blocking=True)
-            ip['handles'].copy_(self.h_handles, non_blocking=True)
+            if self.raw:
+                ip['hero'].copy_(self.h_hero, non_blocking=True)
+                ip['raw'].copy_(self.h_raw, non_blocking=True)
+            else:
+                ip['units'].copy_(self.h_units, non_blocking=True)
+                ip['handles'].copy_(self.h_handles, non_blocking=True)
             self.in_pack.copy_range('keep', 'active')
         else:
             self.in_pack.copy_range('env', 'active')          # one H2D copy of the whole staged step
@@ -386,12 +424,32 @@ class GpuActorPolicy:
         self.step_async()
         return self.wait()
 
+    def step_raw(self, env: np.ndarray, hero: np.ndarray, raw: np.ndarray, reset: Optional[np.ndarray] = None,
+                 active: Optional[np.ndarray] = None):
+        """:meth:`step` from raw unit records (a ``raw=True`` policy): (n,3) env, (n,4) hero, (n,U,8) int32 raw."""
+        self.stage_raw(env, hero, raw)
+        if reset is not None:
+            self.h_keep.numpy()[:, 0] = 1.0 - np.asarray(reset, dtype=np.float32)
+        self.h_active.numpy()[:] = 1.0 if active is None else np.asarray(active, dtype=np.float32)
+        self.step_async()
+        return self.wait()
+
     def stage(self, env: np.ndarray, units: np.ndarray, handles: np.ndarray):
         """Copy (n,3), (n,U,10), (n,U) host arrays into the pinned staging buffers (torch's vectorised casts: the
         fp8 step stages fp16 / int32, and numpy's fp32→fp16 cast is several times slower)."""
+        if self.raw:
+            raise RuntimeError('stage: this policy stages raw unit records (stage_raw)')
         self.h_env.copy_(torch.from_numpy(np.ascontiguousarray(env)))
         self.h_units.copy_(torch.from_numpy(np.ascontiguousarray(units)))
         self.h_handles.copy_(torch.from_numpy(np.ascontiguousarray(handles)))
+
+    def stage_raw(self, env: np.ndarray, hero: np.ndarray, raw: np.ndarray):
+        """Copy (n,3) env, (n,4) hero and (n,U,8) int32 raw unit records (features/raw.py) into the staging buffers."""
+        if not self.raw:
+            raise RuntimeError('stage_raw: this policy stages features (stage)')
+        self.h_env.copy_(torch.from_numpy(np.ascontiguousarray(env)))
+        self.h_hero.copy_(torch.from_numpy(np.ascontiguousarray(hero)))
+        self.h_raw.copy_(torch.from_numpy(np.ascontiguousarray(raw)))
 
     def hidden(self):
         return self.h, self.c
@@ -446,10 +504,10 @@ class Fp8ActorPolicy(GpuActorPolicy):
         super().__init__(policy, n_slots, device=device, **kw)
 
     def _alloc(self, inputs_from=None):
-        if self.compact:
+        if self.compact or self.raw:
             self.UNITS_DTYPE, self.HANDLES_DTYPE = torch.float16, torch.int32
         super()._alloc(inputs_from)
-        if inputs_from is not None and inputs_from.h_units.dtype != self.UNITS_DTYPE:
+        if inputs_from is not None and not self.raw and inputs_from.h_units.dtype != self.UNITS_DTYPE:
             raise ValueError('Fp8ActorPolicy: inputs_from must stage the same feature dtype')
 
     def _weight_dict(self, sd):
@@ -476,6 +534,8 @@ class Fp8ActorPolicy(GpuActorPolicy):
         """Captured body, 3 launches: fp8 encoder → fp8 core (pre-RNN, gates + cell, heads; bumps the sampler's RNG
         counter) → sampling."""
         C, w, cfg = self.C, self.w, self.cfg
+        if self.raw:
+            C.featurize_raw(self.d_raw, self.d_hero, self.d_units, self.d_handles)
         x896, emb = C.encoder_fp8(self.d_units, self.d_env, w['w1'], w['b1'], w['wt8'], w['st8'], w['bt'], w['we'],
                                   w['be'], list(cfg.layout.counts))
         if cfg.compat_bugs:
@@ -555,23 +615,31 @@ class TorchSlotPolicy:
 ACTOR_PRECISIONS = ('bf16', 'fp32', 'fp8')
 
 
-def make_slot_policy(policy: Policy, n_slots: int, device='cuda', precision: str = 'bf16', **kw):
-    """The fused graph-captured :class:`GpuActorPolicy` where it applies (``precision='fp32'``:
-    :class:`F32ActorPolicy`, ``'fp8'``: :class:`Fp8ActorPolicy`), else :class:`TorchSlotPolicy`."""
+def slot_policy_class(policy: Policy, device='cuda', precision: str = 'bf16'):
+    """The class :func:`make_slot_policy` builds: the fused graph-captured :class:`GpuActorPolicy` where it applies
+    (``precision='fp32'``: :class:`F32ActorPolicy`, ``'fp8'``: :class:`Fp8ActorPolicy`), else :class:`TorchSlotPolicy`."""
     dev = torch.device(device)
     cfg = policy.config
     if precision not in ACTOR_PRECISIONS:
         raise ValueError(f'actor precision must be one of {ACTOR_PRECISIONS}, got {precision!r}')
     if precision == 'fp8':
-        return Fp8ActorPolicy(policy, n_slots, device=dev, **kw)
-    if precision == 'fp32' and dev.type == 'cuda' and cfg.unit_dim == 128 and cfg.env_dim == 128 and (
-            not cfg.entity_attention or (cfg.layout.max_units == 64 and cfg.attention_heads == 4)):
-        return F32ActorPolicy(policy, n_slots, device=dev, **kw)
-    if dev.type == 'cuda' and cfg.unit_dim == 128 and cfg.env_dim == 128 and (
-            not cfg.entity_attention or (cfg.layout.max_units == 64 and cfg.attention_heads == 4)):
-        return GpuActorPolicy(policy, n_slots, device=dev, **kw)
-    kw.pop('use_graph', None)
-    return TorchSlotPolicy(policy, n_slots, device=dev, **kw)
+        return Fp8ActorPolicy
+    fused = dev.type == 'cuda' and cfg.unit_dim == 128 and cfg.env_dim == 128 and (
+        not cfg.entity_attention or (cfg.layout.max_units == 64 and cfg.attention_heads == 4))
+    if fused:
+        return F32ActorPolicy if precision == 'fp32' else GpuActorPolicy
+    return TorchSlotPolicy
+
+
+def make_slot_policy(policy: Policy, n_slots: int, device='cuda', precision: str = 'bf16', **kw):
+    """A :func:`slot_policy_class` policy over ``n_slots`` slots (``raw=True``: raw unit-record staging with the
+    features computed on the GPU — the fused policies only)."""
+    cls = slot_policy_class(policy, device, precision)
+    if cls is TorchSlotPolicy:
+        if kw.pop('raw', False):
+            raise ValueError('raw unit-record staging needs a fused GPU actor policy')
+        kw.pop('use_graph', None)
+    return cls(policy, n_slots, device=torch.device(device), **kw)
 
 
 # ----------------------------------------------------------------------------------------------------
@@ -612,7 +680,8 @@ def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048,
     and featurizes serialized world states through the native featurizer every step (the reference actor's
     per-step work, agent.py:611-660) overlapped with the previous GPU step; otherwise only the GPU step + copies
     are timed. ``precision='fp8'``: :class:`Fp8ActorPolicy`, ``'fp32'``: :class:`F32ActorPolicy`. Returns ``{'steps_per_s', 'gpu_steps_per_s',
-    'ms_per_step', 'slots'}``.
+    'gpu_pipelined_steps_per_s', 'ms_per_step', 'slots'}`` (``gpu_steps_per_s``: one policy, copy → step → copy
+    serially; ``gpu_pipelined_steps_per_s``: two policies alternating as the runtime's two groups do).
     """
     n = 2 * n_games
     dev = torch.device(device)
@@ -668,4 +737,19 @@ def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048,
         gp.wait()
         fill(f)
     dt = (time.perf_counter() - t0) / steps
-    return {'steps_per_s': n / dt, 'gpu_steps_per_s': n / gpu_dt, 'ms_per_step': dt * 1e3, 'slots': n}
+    # two policies of n slots on their own step streams, launched back to back (VecActor's two software-pipelined
+    # groups): one step's SDMA input / output copies run beside the other's kernels, so the rate is set by the larger
+    # of copy and compute rather than their sum
+    gp2 = cls(policy, n, device=dev, seed=4321, record=True)
+    gp2.stage(gp.h_env.numpy(), gp.h_units.numpy(), gp.h_handles.numpy())
+    gp2.step_async(); gp2.wait()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        gp.step_async()
+        gp2.step_async()
+        gp.wait()
+        gp2.wait()
+    pipe_dt = (time.perf_counter() - t0) / steps
+    return {'steps_per_s': n / dt, 'gpu_steps_per_s': n / gpu_dt, 'gpu_pipelined_steps_per_s': 2 * n / pipe_dt,
+            'ms_per_step': dt * 1e3, 'slots': n}

@@ -47,22 +47,26 @@ class _Opponent:
 class _Group:
     def __init__(self, actor: 'VecActor', index: int, n_games: int, seed: int):
         a = actor
+        self.raw = a.raw
         self.ve = a._native.VecEnv(n_games, mode=MODES[a.mode], seed=seed, max_dota_time=a.max_dota_time,
                                    rollout_size=a.rollout_size, hidden_stride=a.hidden_stride if a.H else 0,
                                    hidden_size=a.H, counts=list(a.cfg.layout.counts), threads=a.threads,
                                    latest_weights_prob=a.latest_weights_prob, start_time=a.start_time, fog=a.fog,
-                                   tag=f'{a.tag}{index}', stagger=a.stagger, wire=a.wire)
+                                   tag=f'{a.tag}{index}', stagger=a.stagger, wire=a.wire, raw=self.raw)
         if a.ring_sink is not None:
             self.ve.set_ring_sink(a.ring_sink.ring, -1.0, bool(a.ring_sink.drop_oldest))
         self.S = self.ve.slots
         self.ppg = self.ve.players_per_game
-        # (fp8: fp32 host staging, the native engine writes the buffers in place)
-        fp8 = ({'precision': 'fp8', 'compact': False} if a.precision == 'fp8' else
-               {'precision': a.precision})
-        self.gp = make_slot_policy(a.policy, self.S, device=a.device, seed=seed, **fp8)
+        self.gp = make_slot_policy(a.policy, self.S, device=a.device, seed=seed, **a._policy_kw())
         self.env = self.gp.h_env.numpy()
-        self.units = self.gp.h_units.numpy()
-        self.handles = self.gp.h_handles.numpy()
+        if self.raw:
+            # raw unit records staged for the GPU featurizer; the host keeps only the handles (action targets)
+            self.hero = self.gp.h_hero.numpy()
+            self.rawbuf = self.gp.h_raw.numpy()
+            self.handles = np.full((self.S, a.cfg.layout.max_units), -1, np.int64)
+        else:
+            self.units = self.gp.h_units.numpy()
+            self.handles = self.gp.h_handles.numpy()
         self.active = np.zeros(self.S, np.uint8)
         self.opp: List[_Opponent] = []
         self.cur_opp = 0
@@ -90,7 +94,7 @@ class VecActor:
                  latest_weights_prob: float = 1.0, hidden_stride: int = 256, threads: int = 8, groups: int = 2,
                  league=None, opponent_refresh: int = 64, start_time: float = -10.0,
                  fog: bool = True, tag: str = 'vec', stagger: bool = False, wire: bool = False,
-                 precision: str = 'bf16', ring_sink=None):
+                 precision: str = 'bf16', ring_sink=None, raw: Optional[bool] = None):
         from .. import native
         if not native.AVAILABLE:
             raise RuntimeError('VecActor needs the native module (python -m dotaclient_amd.native.build)')
@@ -127,6 +131,14 @@ class VecActor:
         if precision not in ACTOR_PRECISIONS:
             raise ValueError(f'precision must be one of {ACTOR_PRECISIONS}, got {precision!r}')
         self.precision = precision
+        # GPU featurization (features/raw.py, ops/csrc/featurize.hip): the engine stages raw unit records and ships
+        # them in the rollouts; the step's first kernel featurizes them. Default: on wherever the policy step is a
+        # fused GPU policy (the eager CPU / torch policy consumes host features)
+        from .batched import TorchSlotPolicy, slot_policy_class
+        fused = slot_policy_class(self.policy, self.device, precision) is not TorchSlotPolicy
+        if raw and not fused:
+            raise ValueError('raw observation staging needs a fused GPU actor policy')
+        self.raw = fused if raw is None else bool(raw)
         groups = max(1, min(int(groups), n_games))
         sizes = [n_games // groups + (1 if i < n_games % groups else 0) for i in range(groups)]
         self.groups = [_Group(self, i, sizes[i], seed * 7919 + i) for i in range(groups)]
@@ -171,6 +183,14 @@ class VecActor:
         g.gp.load_weight_dict(c[1], ready=c[2], producer=c[3])
         g.version = c[0]
 
+    def _policy_kw(self) -> dict:
+        kw = {'precision': self.precision}
+        if self.precision == 'fp8':
+            kw['compact'] = False          # (feature staging: the native VecEnv writes the fp32 buffers in place)
+        if self.raw:
+            kw['raw'] = True
+        return kw
+
     def _sample_opponent(self):
         if self.league is not None:
             return self.league.sample()
@@ -178,10 +198,8 @@ class VecActor:
 
     def _opponent(self, g: _Group, k: int) -> _Opponent:
         while len(g.opp) <= k:
-            fp8 = ({'precision': 'fp8', 'compact': False} if self.precision == 'fp8' else
-                   {'precision': self.precision})
             gp = make_slot_policy(self.policy, g.S, device=self.device, seed=g.seed + 104729 * (len(g.opp) + 1),
-                                  inputs_from=g.gp, **fp8)
+                                  inputs_from=g.gp, **self._policy_kw())
             g.opp.append(_Opponent(gp))
         return g.opp[k]
 
@@ -231,7 +249,10 @@ class VecActor:
     def _observe_and_launch(self, g: _Group):
         reset = g.ve.begin_step()
         self._assign_opponents(g, reset)
-        need = g.ve.observe(g.env, g.units, g.handles, g.active)
+        if g.raw:
+            need = g.ve.observe_raw(g.env, g.hero, g.rawbuf, g.handles, g.active)
+        else:
+            need = g.ve.observe(g.env, g.units, g.handles, g.active)
         g.gp.h_keep.numpy()[reset, 0] = 0.0
         self._sync_weights(g)
         act = g.active.astype(np.float32)

@@ -163,6 +163,7 @@ class StagedIteration:
     wait_s: float = 0.0                     # part of stage_s spent waiting for a free slot (the learner behind)
     copy_s: float = 0.0                     # part of stage_s in the field copies into the pinned slot
     release_s: float = 0.0                  # part of stage_s giving ring-resident rollouts back
+    raw: bool = False                       # units staged as raw records (featurized on the device in expand)
 
 
 class _Slot:
@@ -292,9 +293,19 @@ class IngestPipeline:
         off = np.asarray(starts + [L], np.int64)
         resets = np.asarray(pk.resets, np.int64)
         r0 = rollouts[0]
-        U, A, K = r0.units.shape[1], r0.actions.shape[1], r0.rewards.shape[1]
+        # raw rollouts (an actor with GPU featurization, features/raw.py): the compact unit records are uploaded and
+        # featurized on the device in expand(); an iteration that mixes them with featurized rollouts converts the
+        # raw ones on the host (exact: the numpy oracle of the kernel)
+        raw = all(r.units is None and r.units_raw is not None for r in rollouts)
+        if not raw:
+            for r in rollouts:
+                r.ensure_units()
+        U = (r0.units_raw if raw else r0.units).shape[1]
+        A, K = r0.actions.shape[1], r0.rewards.shape[1]
         gae_mode = self.algo == 'ppo' and all(r.values is not None for r in rollouts)
-        fields = [('rows', torch.int64, ()), ('env', torch.float32, (3,)), ('units', torch.float32, (U, 10)),
+        unit_fields = ([('units_raw', torch.int32, (U, 8)), ('hero', torch.float32, (4,))] if raw else
+                       [('units', torch.float32, (U, 10))])
+        fields = [('rows', torch.int64, ()), ('env', torch.float32, (3,))] + unit_fields + [
                   ('actions', torch.uint8, (A,)), ('masks', torch.uint8, (A,)), ('logp', torch.float32, ()),
                   ('rewards', torch.float32, (K,))]
         if gae_mode:
@@ -352,7 +363,8 @@ class IngestPipeline:
         pos = 0
         rows = views_h['rows']
         jobs = []
-        direct = ('env', 'units', 'actions', 'masks', 'logp') + (('values',) if gae_mode else ())
+        direct = (('env',) + tuple(f[0] for f in unit_fields) + ('actions', 'masks', 'logp')
+                  + (('values',) if gae_mode else ()))
         tc = 0.0
         if _native_pack is not None:
             # every field of every rollout in ONE native call (memcpy / f64 → f32 rewards / zero fill, GIL released);
@@ -461,7 +473,7 @@ class IngestPipeline:
         self._prof_done()
         return StagedIteration(rollouts=rollouts, lens=lens, off=off, n_seq=n_seq, L=L, Lv=Lv, gae_mode=gae_mode,
                                views=views, ready=ev, slot=slot_i, stage_s=time.perf_counter() - t0, wait_s=tw,
-                               copy_s=tc, release_s=tr)
+                               copy_s=tc, release_s=tr, raw=raw)
 
     def _prof_done(self):
         """DCA_STAGE_PROF=1: accumulate the stage() sections and print their means every 200 iterations (stderr)."""
@@ -500,7 +512,8 @@ class IngestPipeline:
         v = st.views
         rows = v['rows']
         out = {}
-        names = ('env', 'units', 'actions', 'masks', 'logp', 'rewards') + (('values',) if st.gae_mode else ())
+        units = ('units_raw', 'hero') if st.raw else ('units',)
+        names = ('env',) + units + ('actions', 'masks', 'logp', 'rewards') + (('values',) if st.gae_mode else ())
         for name in names:
             src = v[name]
             buf = pad.get(name)
@@ -524,6 +537,21 @@ class IngestPipeline:
             vb.zero_()
             vb.index_fill_(0, rows, 1.0)
         out['valid'] = vb
+        if st.raw:
+            # GPU featurization of the padded rows (ops/csrc/featurize.hip; padding rows are empty records → zero
+            # features, as the featurized path's zero fill)
+            raw_t, hero_t = out.pop('units_raw'), out.pop('hero')
+            buf = pad.get('units')
+            shape = tuple(raw_t.shape[1:2]) + (10,)
+            if buf is None or buf.shape[1:] != shape or buf.shape[0] < st.L:
+                buf = pad['units'] = torch.empty((max(st.L, 2 * (buf.shape[0] if buf is not None else 0)),) + shape,
+                                                 dtype=torch.float32, device=self.device)
+            out['units'] = buf[:st.L]
+            if C is not None:
+                C.featurize_raw(raw_t, hero_t, out['units'])
+            else:
+                from ..features.raw import featurize_raw_np
+                out['units'].copy_(torch.from_numpy(featurize_raw_np(raw_t.numpy(), hero_t.numpy())[0]))
         if 'hid' in v:
             out['hid'] = v['hid'].clone()
         if 'reset' in v:

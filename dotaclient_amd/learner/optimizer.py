@@ -448,7 +448,7 @@ class DotaOptimizer:
             adv = norm
             values = np.zeros(T + pad, np.float32)
         logp = padt(r.logp.astype(np.float32)) if r.logp is not None else np.zeros(T + pad, np.float32)
-        env, units = padt(r.env), padt(r.units)
+        env, units = padt(r.env), padt(r.ensure_units().units)      # (a raw rollout: host features, exact)
         actions, masks = padt(r.actions), padt(r.masks)
         seqs = []
         H = self.policy_cfg.hidden

@@ -2,8 +2,8 @@
 from __future__ import annotations
 
 try:
-    from ._native import ShmRing, copy_jobs, crc32c, featurize_batch, pack_rows  # noqa: F401
+    from ._native import ShmRing, copy_jobs, crc32c, featurize_batch, featurize_batch_raw, pack_rows  # noqa: F401
     AVAILABLE = True
 except ImportError:  # pragma: no cover - not built yet
     AVAILABLE = False
-    ShmRing = copy_jobs = crc32c = featurize_batch = pack_rows = None
+    ShmRing = copy_jobs = crc32c = featurize_batch = featurize_batch_raw = pack_rows = None

@@ -248,16 +248,14 @@ void unit_rows(const std::vector<const Unit*>& list, const Unit& hero, bool only
   }
 }
 
-// returns number of allied lane creeps (for the creep-spawn sanity check), or -1 when the hero is missing
-int featurize_one(const World& w, int player_id, int team_id, const int* counts, int U, float* env, float* units,
-                  int64_t* handles) {
-  const Unit* hero = nullptr;
+// the observing hero and its six unit blocks in slot order (agent.py:456-493, 575-611); returns the number of allied
+// lane creeps (for the creep-spawn sanity check), or -1 when the hero is missing. The lists are per-thread scratch.
+int separate(const World& w, int player_id, const int* counts, const Unit*& hero,
+             const std::vector<const Unit*>* (&lists)[6]) {
+  hero = nullptr;
   for (const Unit& u : w.units)
     if (u.unit_type == HERO && u.player_id == player_id) { hero = &u; break; }
   if (!hero) return -1;
-  env[0] = (float)((double)w.dota_time / 1200.0);
-  env[1] = (float)std::sin((double)w.dota_time * (2.0 * 3.14159265358979323846) / 60.0);
-  env[2] = team_id == 3 ? -0.2f : 0.2f;
   // per-thread scratch lists (capacity reused across calls: no allocation per observation)
   thread_local std::vector<const Unit*> ah, eh, anhc, enhc, ac, ec, at, et, s5;
   ah.clear(); eh.clear(); anhc.clear(); enhc.clear(); ac.clear(); ec.clear(); at.clear(); et.clear();
@@ -282,14 +280,90 @@ int featurize_one(const World& w, int player_id, int team_id, const int* counts,
       if (u->player_id != player_id) s5.push_back(u);
     ah.swap(s5);
   }
-  const std::vector<const Unit*>* lists[6] = {&ah, &eh, &anhc, &enhc, &at, &et};
+  lists[0] = &ah; lists[1] = &eh; lists[2] = &anhc; lists[3] = &enhc; lists[4] = &at; lists[5] = &et;
+  return (int)ac.size();
+}
+
+void env_row(const World& w, int team_id, float* env) {
+  env[0] = (float)((double)w.dota_time / 1200.0);
+  env[1] = (float)std::sin((double)w.dota_time * (2.0 * 3.14159265358979323846) / 60.0);
+  env[2] = team_id == 3 ? -0.2f : 0.2f;
+}
+
+// returns number of allied lane creeps (for the creep-spawn sanity check), or -1 when the hero is missing
+int featurize_one(const World& w, int player_id, int team_id, const int* counts, int U, float* env, float* units,
+                  int64_t* handles) {
+  const Unit* hero;
+  const std::vector<const Unit*>* lists[6];
+  const int nc = separate(w, player_id, counts, hero, lists);
+  if (nc < 0) return -1;
+  env_row(w, team_id, env);
   int off = 0;
   for (int t = 0; t < 6; ++t) {
     unit_rows(*lists[t], *hero, t == 0 && counts[0] == 1, counts[t], units + off * 10, handles + off);
     off += counts[t];
   }
   (void)U;
-  return (int)ac.size();
+  return nc;
+}
+
+// ---- raw unit records for GPU featurization (ops/csrc/featurize.hip, features/raw.py): 8 words per slot —
+// x, y, z, facing (f32) | 1 − health / health_max (f32, double then rounded once), handle (−1: not targetable), flags
+// (bit 0 present, 1 attacks the hero, 2 the hero attacks it), 0 — and a hero record (x, y, attack range, 0). The
+// slot selection, validity rules and attack cross-references are unit_rows'; the distance / sincos / range arithmetic
+// is left to the device. (Handles are stored as int32: the engines' handles are far below 2^31.)
+constexpr int kRawWords = 8;
+
+void unit_rows_raw(const std::vector<const Unit*>& list, const Unit& hero, bool only_self, int max_units, int32_t* r,
+                   int64_t* handles) {
+  std::memset(r, 0, sizeof(int32_t) * kRawWords * (size_t)max_units);
+  for (int i = 0; i < max_units; ++i) handles[i] = -1;
+  int i = 0;
+  const uint32_t opp = hero.team_id == 2 ? 3 : (hero.team_id == 3 ? 2 : 0);
+  for (const Unit* up : list) {
+    const Unit& u = *up;
+    if (!u.is_alive) continue;
+    if (only_self && u.handle != hero.handle) continue;
+    if (i >= max_units) break;
+    const double hp = u.health_max ? (double)u.health / (double)u.health_max : 0.0;
+    int32_t* w = r + i * kRawWords;
+    const float rel = (float)(1.0 - hp);
+    std::memcpy(w + 0, &u.x, 4);
+    std::memcpy(w + 1, &u.y, 4);
+    std::memcpy(w + 2, &u.z, 4);
+    std::memcpy(w + 3, &u.facing, 4);
+    std::memcpy(w + 4, &rel, 4);
+    int64_t h = (int64_t)u.handle;
+    if (u.invuln || u.attack_immune) h = -1;
+    else if (u.team_id == opp && u.unit_type == TOWER && u.anim == 1500) h = -1;
+    else if (u.team_id == hero.team_id && u.unit_type == TOWER) h = -1;
+    else if (u.team_id == hero.team_id && hp > 0.5) h = -1;
+    w[5] = (int32_t)h;
+    w[6] = 1 | (attacking(u, hero) != 0.f ? 2 : 0) | (attacking(hero, u) != 0.f ? 4 : 0);
+    handles[i] = h;
+    ++i;
+  }
+}
+
+// raw form of featurize_one: env (3), hero (4), raw (U, 8) and the host's handles (U) (the action decoder's targets)
+int featurize_one_raw(const World& w, int player_id, int team_id, const int* counts, float* env, float* hero4,
+                      int32_t* raw, int64_t* handles) {
+  const Unit* hero;
+  const std::vector<const Unit*>* lists[6];
+  const int nc = separate(w, player_id, counts, hero, lists);
+  if (nc < 0) return -1;
+  env_row(w, team_id, env);
+  hero4[0] = hero->x;
+  hero4[1] = hero->y;
+  hero4[2] = (float)hero->attack_range;
+  hero4[3] = 0.f;
+  int off = 0;
+  for (int t = 0; t < 6; ++t) {
+    unit_rows_raw(*lists[t], *hero, t == 0 && counts[0] == 1, counts[t], raw + (size_t)off * kRawWords,
+                  handles + off);
+    off += counts[t];
+  }
+  return nc;
 }
 
 // ============================================================================================================

@@ -76,6 +76,59 @@ py::tuple featurize_batch(const std::vector<py::bytes>& states, const std::vecto
   return py::make_tuple(env, units, handles, n_creep);
 }
 
+// raw form (GPU featurization, ops/csrc/featurize.hip): → (env (N,3), hero (N,4), raw (N,U,8) int32, handles (N,U),
+// n_allied_creep)
+py::tuple featurize_batch_raw(const std::vector<py::bytes>& states, const std::vector<int>& player_ids,
+                              const std::vector<int>& team_ids, const std::vector<int>& counts, int threads) {
+  const size_t N = states.size();
+  if (player_ids.size() != N || team_ids.size() != N) throw std::invalid_argument("length mismatch");
+  if (counts.size() != 6) throw std::invalid_argument("counts must have 6 entries");
+  int U = 0;
+  for (int c : counts) U += c;
+  py::array_t<float> env({(py::ssize_t)N, (py::ssize_t)3});
+  py::array_t<float> hero({(py::ssize_t)N, (py::ssize_t)4});
+  py::array_t<int32_t> raw({(py::ssize_t)N, (py::ssize_t)U, (py::ssize_t)kRawWords});
+  py::array_t<int64_t> handles({(py::ssize_t)N, (py::ssize_t)U});
+  py::array_t<int32_t> n_creep({(py::ssize_t)N});
+  std::vector<std::string_view> views(N);
+  for (size_t i = 0; i < N; ++i) {
+    char* buf;
+    py::ssize_t len;
+    PYBIND11_BYTES_AS_STRING_AND_SIZE(states[i].ptr(), &buf, &len);
+    views[i] = std::string_view(buf, (size_t)len);
+  }
+  float* envp = env.mutable_data();
+  float* herop = hero.mutable_data();
+  int32_t* rp = raw.mutable_data();
+  int64_t* hp = handles.mutable_data();
+  int32_t* cp = n_creep.mutable_data();
+  std::vector<std::string> errors(N);
+  {
+    py::gil_scoped_release rel;
+    const int T = std::max(1, std::min<int>(threads, (int)N));
+    std::atomic<size_t> next{0};
+    auto work = [&]() {
+      for (size_t i; (i = next.fetch_add(1)) < N;) {
+        try {
+          World w;
+          parse_world((const uint8_t*)views[i].data(), views[i].size(), w);
+          cp[i] = featurize_one_raw(w, player_ids[i], team_ids[i], counts.data(), envp + 3 * i, herop + 4 * i,
+                                    rp + i * (size_t)U * kRawWords, hp + (size_t)i * U);
+        } catch (const std::exception& e) {
+          errors[i] = e.what();
+        }
+      }
+    };
+    std::vector<std::thread> pool;
+    for (int t = 1; t < T; ++t) pool.emplace_back(work);
+    work();
+    for (auto& th : pool) th.join();
+  }
+  for (size_t i = 0; i < N; ++i)
+    if (!errors[i].empty()) throw std::runtime_error("observation " + std::to_string(i) + ": " + errors[i]);
+  return py::make_tuple(env, hero, raw, handles, n_creep);
+}
+
 // pybind face of the ring: the GIL is released around every blocking call
 class ShmRing {
  public:
@@ -203,9 +256,9 @@ class PyVecEnv {
  public:
   PyVecEnv(int n_games, int mode, uint64_t seed, double max_dota_time, long rollout_size, int hidden_stride,
            int hidden_size, std::vector<int> counts, int threads, double latest_weights_prob, bool validation,
-           bool fog, double start_time, std::string tag, bool stagger, bool wire)
+           bool fog, double start_time, std::string tag, bool stagger, bool wire, bool raw)
       : env_(make(n_games, mode, seed, max_dota_time, rollout_size, hidden_stride, hidden_size, counts, threads,
-                  latest_weights_prob, validation, fog, start_time, tag, stagger, wire)) {
+                  latest_weights_prob, validation, fog, start_time, tag, stagger, wire, raw)) {
     S_ = env_.slots();
     U_ = env_.units();
     H_ = hidden_size;
@@ -218,7 +271,23 @@ class PyVecEnv {
     }
     return py::array_t<int32_t>((py::ssize_t)r.size(), r.data());
   }
+  py::array_t<int32_t> observe_raw(py::array env, py::array hero, py::array raw, py::array handles,
+                                   py::array active) {
+    if (!env_.raw()) throw std::invalid_argument("observe_raw: the VecEnv was not created with raw=True");
+    float* e = checked<float>(env, {S_, 3}, "env", true);
+    float* hr = checked<float>(hero, {S_, 4}, "hero", true);
+    int32_t* r = checked<int32_t>(raw, {S_, U_, kRawWords}, "raw", true);
+    int64_t* h = checked<int64_t>(handles, {S_, U_}, "handles", true);
+    uint8_t* a = checked<uint8_t>(active, {S_}, "active", true);
+    std::vector<int> need;
+    {
+      py::gil_scoped_release rel;
+      need = env_.observe_raw(e, hr, r, h, a);
+    }
+    return py::array_t<int32_t>((py::ssize_t)need.size(), need.data());
+  }
   py::array_t<int32_t> observe(py::array env, py::array units, py::array handles, py::array active) {
+    if (env_.raw()) throw std::invalid_argument("observe: the VecEnv was created with raw=True (use observe_raw)");
     float* e = checked<float>(env, {S_, 3}, "env", true);
     float* u = checked<float>(units, {S_, U_, 10}, "units", true);
     int64_t* h = checked<int64_t>(handles, {S_, U_}, "handles", true);
@@ -272,6 +341,7 @@ class PyVecEnv {
     return py::array_t<int32_t>((py::ssize_t)s.size(), s.data());
   }
   int slots() const { return S_; }
+  bool raw() const { return env_.raw(); }
   int players_per_game() const { return env_.players_per_game(); }
   long games_finished() const { return env_.games_finished(); }
   long steps_taken() const { return env_.steps_taken(); }
@@ -291,7 +361,7 @@ class PyVecEnv {
   static VecConfig make(int n_games, int mode, uint64_t seed, double max_dota_time, long rollout_size,
                         int hidden_stride, int hidden_size, const std::vector<int>& counts, int threads,
                         double latest_weights_prob, bool validation, bool fog, double start_time,
-                        const std::string& tag, bool stagger, bool wire) {
+                        const std::string& tag, bool stagger, bool wire, bool raw) {
     if (n_games < 1 || mode < 0 || mode > 3 || counts.size() != 6 || rollout_size < 1 || hidden_size < 0)
       throw std::invalid_argument("VecEnv: bad configuration");
     VecConfig c;
@@ -311,6 +381,7 @@ class PyVecEnv {
     c.tag = tag;
     c.stagger = stagger;
     c.wire = wire;
+    c.raw = raw;
     return c;
   }
   py::object ring_ref_;     // (declared before env_: destroyed after it)
@@ -356,6 +427,19 @@ class PySimGame {
     featurize_one(w, player_id, team, counts.data(), U, env.mutable_data(), units.mutable_data(),
                   handles.mutable_data());
     return py::make_tuple(env, units, handles);
+  }
+  py::tuple featurize_raw(int team, int player_id, std::vector<int> counts) {
+    World w;
+    g_.world(team, w);
+    int U = 0;
+    for (int c : counts) U += c;
+    py::array_t<float> env({(py::ssize_t)3});
+    py::array_t<float> hero({(py::ssize_t)4});
+    py::array_t<int32_t> raw({(py::ssize_t)U, (py::ssize_t)kRawWords});
+    py::array_t<int64_t> handles({(py::ssize_t)U});
+    featurize_one_raw(w, player_id, team, counts.data(), env.mutable_data(), hero.mutable_data(), raw.mutable_data(),
+                      handles.mutable_data());
+    return py::make_tuple(env, hero, raw, handles);
   }
   py::array_t<double> reward(int player_id, int team) {   // reward vs the previous call's view
     RewardView cur = reward_view(g_, player_id, team);
@@ -524,6 +608,11 @@ PYBIND11_MODULE(_native, m) {
   m.def("featurize_batch", &featurize_batch, py::arg("states"), py::arg("player_ids"), py::arg("team_ids"),
         py::arg("counts"), py::arg("threads") = 4,
         "Decode CMsgBotWorldState bytes and featurize for (player, team): returns env, units, handles, n_allied_creep");
+  m.def("featurize_batch_raw", &featurize_batch_raw, py::arg("states"), py::arg("player_ids"), py::arg("team_ids"),
+        py::arg("counts"), py::arg("threads") = 4,
+        "featurize_batch's raw form for GPU featurization: returns env, hero, raw (N,U,8) int32, handles, "
+        "n_allied_creep");
+  m.attr("RAW_WORDS") = kRawWords;
   m.def("crc32c", &crc32c);
   m.def("copy_jobs", &copy_jobs, py::arg("jobs"), py::arg("threads") = 4,
         "memcpy a (n, 3) int64 job list of (dst address, src address, bytes) on `threads` threads (GIL released)");
@@ -534,15 +623,18 @@ PYBIND11_MODULE(_native, m) {
         "CRC-32C of the first n bytes of a contiguous buffer (GIL released)");
   py::class_<PyVecEnv>(m, "VecEnv")
       .def(py::init<int, int, uint64_t, double, long, int, int, std::vector<int>, int, double, bool, bool, double,
-                    std::string, bool, bool>(),
+                    std::string, bool, bool, bool>(),
            py::arg("n_games"), py::arg("mode") = 0, py::arg("seed") = 0, py::arg("max_dota_time") = 600.0,
            py::arg("rollout_size") = (long)1 << 40, py::arg("hidden_stride") = 0, py::arg("hidden_size") = 0,
            py::arg("counts") = std::vector<int>{1, 5, 16, 16, 1, 1}, py::arg("threads") = 8,
            py::arg("latest_weights_prob") = 1.0, py::arg("validation") = false, py::arg("fog") = true,
            py::arg("start_time") = -10.0, py::arg("tag") = std::string("vec"), py::arg("stagger") = false,
-           py::arg("wire") = false)
+           py::arg("wire") = false, py::arg("raw") = false)
       .def("begin_step", &PyVecEnv::begin_step)
       .def("observe", &PyVecEnv::observe, py::arg("env"), py::arg("units"), py::arg("handles"), py::arg("active"))
+      .def("observe_raw", &PyVecEnv::observe_raw, py::arg("env"), py::arg("hero"), py::arg("raw"), py::arg("handles"),
+           py::arg("active"))
+      .def_property_readonly("raw", [](const PyVecEnv& e) { return e.raw(); })
       .def("act", &PyVecEnv::act, py::arg("idx"), py::arg("act"), py::arg("msk"), py::arg("logp"), py::arg("value"),
            py::arg("hidden"), py::arg("hidden_slots"), py::arg("handles"), py::arg("weight_version"))
       .def("pop_rollouts", &PyVecEnv::pop_rollouts)
@@ -564,6 +656,7 @@ PYBIND11_MODULE(_native, m) {
            py::arg("seed"), py::arg("start_time") = -10.0, py::arg("fog") = true, py::arg("dt") = 0.5)
       .def("step", &PySimGame::step)
       .def("featurize", &PySimGame::featurize)
+      .def("featurize_raw", &PySimGame::featurize_raw)
       .def("world_bytes", &PySimGame::world_bytes)
       .def("reward", &PySimGame::reward)
       .def("units", &PySimGame::units)

@@ -884,16 +884,21 @@ struct VecConfig {
   // observations as serialised CMsgBotWorldState protobufs decoded by the wire featurizer (the reference actor's
   // observe → featurize path) instead of straight from the engine's state
   bool wire = false;
+  // observations as compact raw unit records (native/core.h featurize_one_raw) for GPU featurization
+  // (ops/csrc/featurize.hip): observe_raw() fills the staging buffers, the trajectories keep the records and the
+  // rollouts carry them ('units_raw' (T, U, 8) int32 + 'hero' (T, 4) fp32) instead of 'units' (T, U, 10)
+  bool raw = false;
 };
 
 struct Traj {
-  std::vector<float> env, units, logp, values, hiddens;
+  std::vector<float> env, units, logp, values, hiddens;   // (raw mode: units holds the raw records' 32-bit words)
+  std::vector<float> hero;                                  // raw mode: the observing hero record, 4 per step
   std::vector<uint8_t> actions, masks;
   std::vector<double> rewards;
   std::vector<uint8_t> canvas;   // snapshot taken when a truncated rollout is cut (published one step later)
   long n = 0;
   void clear() {
-    env.clear(); units.clear(); logp.clear(); values.clear(); hiddens.clear(); actions.clear(); masks.clear();
+    env.clear(); units.clear(); hero.clear(); logp.clear(); values.clear(); hiddens.clear(); actions.clear(); masks.clear();
     rewards.clear(); canvas.clear();
     n = 0;
   }
@@ -958,11 +963,20 @@ class VecEnv {
   // returns the slots whose trajectory records an LSTM state this step (hidden_stride)
   std::vector<int> observe(float* env, float* units, int64_t* handles, uint8_t* active) {
     std::vector<std::vector<int>> need(cfg_.n_games);
-    pool_.run(cfg_.n_games, [&](int gi) { observe_game(gi, env, units, handles, active, need[gi]); });
+    pool_.run(cfg_.n_games, [&](int gi) { observe_game(gi, env, units, nullptr, nullptr, handles, active, need[gi]); });
     std::vector<int> out;
     for (auto& v : need) out.insert(out.end(), v.begin(), v.end());
     return out;
   }
+  // raw mode: env (slots, 3), hero (slots, 4), raw (slots, U, 8) and the host's handles (slots, U) (action targets)
+  std::vector<int> observe_raw(float* env, float* hero, int32_t* raw, int64_t* handles, uint8_t* active) {
+    std::vector<std::vector<int>> need(cfg_.n_games);
+    pool_.run(cfg_.n_games, [&](int gi) { observe_game(gi, env, nullptr, hero, raw, handles, active, need[gi]); });
+    std::vector<int> out;
+    for (auto& v : need) out.insert(out.end(), v.begin(), v.end());
+    return out;
+  }
+  bool raw() const { return cfg_.raw; }
 
   // record the policy outputs, decode orders, advance the engines, rollout bookkeeping
   // (handles: the (slots, U) unit handles of the observe() these outputs answer — attack targets)
@@ -1075,7 +1089,8 @@ class VecEnv {
     }
   }
 
-  void observe_game(int gi, float* env, float* units, int64_t* handles, uint8_t* active, std::vector<int>& need) {
+  void observe_game(int gi, float* env, float* units, float* hero, int32_t* raw, int64_t* handles, uint8_t* active,
+                    std::vector<int>& need) {
     VGame& g = games_[gi];
     for (VPlayer& p : g.players) {
       active[p.slot] = 0;
@@ -1126,15 +1141,24 @@ class VecEnv {
       p.prev = cur;
       p.rewarded = true;
       const int slot = p.slot;
-      const int nc = featurize_one(w[ti], p.player_id, p.team, cfg_.counts, U_, env + 3 * (size_t)slot,
-                                   units + (size_t)slot * U_ * 10, handles + (size_t)slot * U_);
-      (void)nc;
+      if (cfg_.raw) {
+        int32_t* rr = raw + (size_t)slot * U_ * kRawWords;
+        featurize_one_raw(w[ti], p.player_id, p.team, cfg_.counts, env + 3 * (size_t)slot, hero + 4 * (size_t)slot,
+                          rr, handles + (size_t)slot * U_);
+        // keep the raw records for the trajectory (their 32-bit words; the learner featurizes them on the GPU)
+        const float* rf = reinterpret_cast<const float*>(rr);
+        p.traj.units.insert(p.traj.units.end(), rf, rf + (size_t)U_ * kRawWords);
+        p.traj.hero.insert(p.traj.hero.end(), hero + 4 * (size_t)slot, hero + 4 * (size_t)slot + 4);
+      } else {
+        featurize_one(w[ti], p.player_id, p.team, cfg_.counts, U_, env + 3 * (size_t)slot,
+                      units + (size_t)slot * U_ * 10, handles + (size_t)slot * U_);
+        // keep the features for the trajectory
+        p.traj.units.insert(p.traj.units.end(), units + (size_t)slot * U_ * 10, units + (size_t)(slot + 1) * U_ * 10);
+      }
       active[slot] = 1;
       p.stepped = true;
       if (cfg_.hidden_size && cfg_.hidden_stride && p.traj.n % cfg_.hidden_stride == 0) need.push_back(slot);
-      // keep the features for the trajectory
       p.traj.env.insert(p.traj.env.end(), env + 3 * (size_t)slot, env + 3 * (size_t)slot + 3);
-      p.traj.units.insert(p.traj.units.end(), units + (size_t)slot * U_ * 10, units + (size_t)(slot + 1) * U_ * 10);
     }
     g.last_reward_sum[0] = reward_sum[0];
     g.last_reward_sum[1] = reward_sum[1];
@@ -1146,7 +1170,12 @@ class VecEnv {
     const long T = t.n;
     std::vector<ArrayRef> arr;
     arr.push_back({"env", "<f4", {T, 3}, t.env.data(), t.env.size() * 4});
-    arr.push_back({"units", "<f4", {T, U_, 10}, t.units.data(), t.units.size() * 4});
+    if (cfg_.raw) {
+      arr.push_back({"units_raw", "<i4", {T, U_, kRawWords}, t.units.data(), t.units.size() * 4});
+      arr.push_back({"hero", "<f4", {T, 4}, t.hero.data(), t.hero.size() * 4});
+    } else {
+      arr.push_back({"units", "<f4", {T, U_, 10}, t.units.data(), t.units.size() * 4});
+    }
     arr.push_back({"actions", "|u1", {T, A_}, t.actions.data(), t.actions.size()});
     arr.push_back({"masks", "|u1", {T, A_}, t.masks.data(), t.masks.size()});
     arr.push_back({"rewards", "<f8", {T, 9}, t.rewards.data(), t.rewards.size() * 8});

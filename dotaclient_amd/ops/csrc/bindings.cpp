@@ -764,6 +764,32 @@ std::vector<torch::Tensor> vtrace_step(torch::Tensor z, int64_t vcol, torch::Ten
   return {adv, ret, stats};
 }
 
+// GPU unit featurization (featurize.hip): raw records (rows, U, 8) int32 + hero (rows, 4) fp32 → features (rows, U, 10)
+// fp32 + handles (rows, U) int64, or fp16 + int32 (the fp8 actor's staged dtypes); handles optional
+void featurize_raw(torch::Tensor raw, torch::Tensor hero, torch::Tensor units, c10::optional<torch::Tensor> handles) {
+  CHECK_DEV(raw); CHECK_CONTIG(raw); CHECK_DT(raw, at::kInt);
+  CHECK_F32(hero);
+  CHECK_DEV(units); CHECK_CONTIG(units);
+  TORCH_CHECK(raw.dim() == 3 && raw.size(2) == 8, "featurize_raw: raw must be (rows, U, 8) int32");
+  const int64_t rows = raw.size(0), U = raw.size(1);
+  TORCH_CHECK(hero.numel() == rows * 4, "featurize_raw: hero must be (rows, 4)");
+  TORCH_CHECK(units.numel() == rows * U * 10, "featurize_raw: units must be (rows, U, 10)");
+  const bool half = units.scalar_type() == at::kHalf;
+  TORCH_CHECK(half || units.scalar_type() == at::kFloat, "featurize_raw: units fp32 or fp16");
+  void* hp = nullptr;
+  if (handles.has_value() && handles->defined()) {
+    CHECK_DEV(*handles); CHECK_CONTIG(*handles);
+    TORCH_CHECK(handles->numel() == rows * U, "featurize_raw: handles must be (rows, U)");
+    TORCH_CHECK(handles->scalar_type() == (half ? at::kInt : at::kLong),
+                "featurize_raw: handles int64 with fp32 features, int32 with fp16");
+    hp = handles->data_ptr();
+  }
+  TORCH_CHECK(rows * U < (int64_t)1 << 31, "featurize_raw: too many unit slots");
+  hip_check(dca_featurize_raw(raw.data_ptr(), ptr<float>(hero), units.data_ptr(), hp, (int)rows, (int)U, half ? 1 : 0,
+                              cur_stream()),
+            "dca_featurize_raw");
+}
+
 // Test utility (glue.hip): hold `blocks`·(1/8) CUs of XCD `xcd` for `seconds` on the current stream; returns the
 // per-workgroup placement record (XCC id + 1 where it held a CU, 0 elsewhere).
 torch::Tensor occupy_xcd(int64_t xcd, int64_t blocks, double seconds, torch::Tensor like) {
@@ -1171,6 +1197,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("vtrace_step", &vtrace_step, "V-trace advantages / value targets of a minibatch from the step's own values",
         py::arg("z"), py::arg("vcol"), py::arg("lp"), py::arg("mu"), py::arg("vt"), py::arg("B"), py::arg("S"),
         py::arg("gamma"), py::arg("lam"), py::arg("rho_bar") = 1.0, py::arg("c_bar") = 1.0);
+  m.def("featurize_raw", &featurize_raw, "GPU unit featurization from raw unit records (featurize.hip)",
+        py::arg("raw"), py::arg("hero"), py::arg("units"), py::arg("handles") = py::none());
   m.def("occupy_xcd", &occupy_xcd, "test utility: hold CUs of one XCD for a while (160 KB LDS per workgroup)",
         py::arg("xcd"), py::arg("blocks"), py::arg("seconds"), py::arg("like"));
   m.def("returns_scan", &returns_scan, "segmented reverse scan: discounted returns / GAE / V-trace GAE + per-team EMA "

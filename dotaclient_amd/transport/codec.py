@@ -76,7 +76,7 @@ class Rollout:
     team_id: int
     player_id: int
     env: np.ndarray                      # (T, 3) f32
-    units: np.ndarray                    # (T, U, 10) f32
+    units: Optional[np.ndarray]          # (T, U, 10) f32 (None in a raw rollout: see units_raw)
     actions: np.ndarray                  # (T, 21+U) u8 one-hot per sampled head
     masks: np.ndarray                    # (T, 21+U) u8 selected-heads mask
     rewards: np.ndarray                  # (T, 9) f64 in REWARD_KEYS order
@@ -89,6 +89,11 @@ class Rollout:
     bootstrap_value: float = 0.0
     done: bool = True
     layout: Tuple[int, ...] = field(default_factory=lambda: LAYOUT_1V1.counts)
+    # GPU featurization (features/raw.py, ops/csrc/featurize.hip): a VecEnv(raw=True) actor ships the compact raw unit
+    # records (T, U, 8) int32 and the observing hero (T, 4) f32 instead of units; the learner featurizes them on the
+    # device at ingest, host consumers through :meth:`ensure_units`
+    units_raw: Optional[np.ndarray] = None
+    hero: Optional[np.ndarray] = None
     # zero-copy consumption (ShmBroker.claim_experience): the arrays view the message inside the shared ring, and this
     # callable gives its region back; see :meth:`detach_shared`
     release: Optional[object] = field(default=None, repr=False, compare=False)
@@ -96,6 +101,13 @@ class Rollout:
     @property
     def length(self) -> int:
         return int(self.rewards.shape[0])
+
+    def ensure_units(self) -> 'Rollout':
+        """Host features of a raw rollout (the numpy oracle of the device kernel; exact): fills ``units``."""
+        if self.units is None and self.units_raw is not None:
+            from ..features.raw import featurize_raw_np
+            self.units = featurize_raw_np(self.units_raw, self.hero)[0]
+        return self
 
     def detach_shared(self, keep_canvas: bool = False, release: bool = True):
         """Once a ring-resident rollout has been staged (learner/ingest.py): keep private copies of what the learner
@@ -107,6 +119,7 @@ class Rollout:
         self.rewards = np.array(self.rewards)
         self.canvas = np.array(self.canvas) if (keep_canvas and self.canvas is not None) else None
         self.env = self.units = self.actions = self.masks = self.logp = self.values = self.hiddens = None
+        self.units_raw = self.hero = None
         rel, self.release = self.release, None
         if not release:
             return rel
@@ -121,6 +134,7 @@ class Rollout:
         """Reference message layout (agent.py:397-407), torch tensors as the reference's pickles carry."""
         import torch
         lay = self.unit_layout()
+        self.ensure_units()
         states = {'env': torch.from_numpy(np.ascontiguousarray(self.env))}
         for k, sl in lay.slices().items():
             states[k] = torch.from_numpy(np.ascontiguousarray(self.units[:, sl]))
@@ -152,7 +166,7 @@ class Rollout:
                    layout=counts)
 
 
-_ARRAYS = ['env', 'units', 'actions', 'masks', 'rewards', 'canvas', 'logp', 'values', 'hiddens']
+_ARRAYS = ['env', 'units', 'actions', 'masks', 'rewards', 'canvas', 'logp', 'values', 'hiddens', 'units_raw', 'hero']
 
 
 def encode(r: Rollout) -> bytes:

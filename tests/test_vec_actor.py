@@ -28,7 +28,9 @@ def _store(cfg, versions=(0,), seed=0):
 
 
 def _replay(policy, r, stride):
-    """Re-run a rollout; returns (hidden states at the stride points, values, logp of the recorded actions)."""
+    """Re-run a rollout; returns (hidden states at the stride points, values, logp of the recorded actions).
+    (A GPU actor's rollouts carry raw unit records: featurized here by the kernel's numpy oracle.)"""
+    r.ensure_units()
     U = r.units.shape[1]
     heads = HEADS + [('target_unit', 21, U)]
     h = (torch.from_numpy(r.hiddens[0, 0].copy())[None, None], torch.from_numpy(r.hiddens[0, 1].copy())[None, None])
@@ -180,6 +182,8 @@ def test_vec_actor_gpu_graph_policy_replay_consistent(preset, mode):
     pol = ws.policy_for(ws.latest_weights())
     rs = [decode(b) for b in sent]
     assert len(rs) > 16
+    # GPU featurization: the rollouts carry raw unit records (features/raw.py), not host features
+    assert all(r.units is None and r.units_raw is not None and r.hero is not None for r in rs)
     for r in rs[:60]:
         hs, vals, lps = _replay(pol, r, 16)
         np.testing.assert_allclose(hs, r.hiddens, atol=5e-2 if mode == '1v1' else 1e-1)
