@@ -673,7 +673,7 @@ def _synthetic_states(n_states: int, seed: int = 0):
 
 def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048, steps: int = 50,
                              warmup: int = 5, featurize: bool = True, threads: int = 8,
-                             precision: str = 'bf16') -> Dict[str, float]:
+                             precision: str = 'bf16', raw: bool = True) -> Dict[str, float]:
     """Actor steps/s (player-observations → sampled actions per second) of one GPU-resident batched actor.
 
     ``n_games`` 1v1 games = 2·n_games player slots stepped per launch. With ``featurize`` the host side decodes
@@ -681,13 +681,15 @@ def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048,
     per-step work, agent.py:611-660) overlapped with the previous GPU step; otherwise only the GPU step + copies
     are timed. ``precision='fp8'``: :class:`Fp8ActorPolicy`, ``'fp32'``: :class:`F32ActorPolicy`. Returns ``{'steps_per_s', 'gpu_steps_per_s',
     'gpu_pipelined_steps_per_s', 'ms_per_step', 'slots'}`` (``gpu_steps_per_s``: one policy, copy → step → copy
-    serially; ``gpu_pipelined_steps_per_s``: two policies alternating as the runtime's two groups do).
+    serially; ``gpu_pipelined_steps_per_s``: two policies alternating as the runtime's two groups do). ``raw``
+    (default, the runtime's path): raw unit records staged and featurized on the GPU (ops/csrc/featurize.hip);
+    otherwise host features.
     """
     n = 2 * n_games
     dev = torch.device(device)
     layout = policy.config.layout
     cls = {'fp8': Fp8ActorPolicy, 'fp32': F32ActorPolicy}.get(precision, GpuActorPolicy)
-    gp = cls(policy, n, device=dev, seed=1234, record=True)
+    gp = cls(policy, n, device=dev, seed=1234, record=True, raw=raw)
     feat = None
     if featurize:
         from .. import native
@@ -701,6 +703,8 @@ def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048,
             counts = list(layout.counts)
 
             def feat():
+                if raw:
+                    return native.featurize_batch_raw(batch, pids, teams, counts, threads)[:3]
                 return native.featurize_batch(batch, pids, teams, counts, threads)
     if not featurize:
         rng = np.random.default_rng(0)
@@ -709,11 +713,24 @@ def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048,
         handles = np.where(rng.random((n, layout.max_units)) < 0.5, rng.integers(1, 1000, (n, layout.max_units)),
                            -1).astype(np.int64)
 
+        if raw:
+            from ..features.raw import F_PRESENT
+            hero = np.zeros((n, 4), np.float32)
+            hero[:, :2] = rng.uniform(-7000, 7000, (n, 2))
+            hero[:, 2] = 600.0
+            rawb = np.zeros((n, layout.max_units, 8), np.int32)
+            rawb.view(np.float32)[..., :5] = rng.uniform(-1000, 1000, (n, layout.max_units, 5))
+            rawb[..., 5] = handles
+            rawb[..., 6] = np.where(rng.random((n, layout.max_units)) < 0.6, F_PRESENT, 0)
+
         def feat():
-            return env, units, handles, None
+            return (env, hero, rawb) if raw else (env, units, handles, None)
 
     def fill(f):
-        gp.stage(f[0], f[1], f[2])
+        if raw:
+            gp.stage_raw(f[0], f[1], f[2])
+        else:
+            gp.stage(f[0], f[1], f[2])
 
     fill(feat())
     gp.step_async(); gp.wait()
@@ -740,8 +757,11 @@ def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048,
     # two policies of n slots on their own step streams, launched back to back (VecActor's two software-pipelined
     # groups): one step's SDMA input / output copies run beside the other's kernels, so the rate is set by the larger
     # of copy and compute rather than their sum
-    gp2 = cls(policy, n, device=dev, seed=4321, record=True)
-    gp2.stage(gp.h_env.numpy(), gp.h_units.numpy(), gp.h_handles.numpy())
+    gp2 = cls(policy, n, device=dev, seed=4321, record=True, raw=raw)
+    if raw:
+        gp2.stage_raw(gp.h_env.numpy(), gp.h_hero.numpy(), gp.h_raw.numpy())
+    else:
+        gp2.stage(gp.h_env.numpy(), gp.h_units.numpy(), gp.h_handles.numpy())
     gp2.step_async(); gp2.wait()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
