@@ -73,8 +73,8 @@ def parse():
     ap.add_argument('--algo', default='ppo', choices=['ppo', 'vpg'])
     ap.add_argument('--precision', default='fp32-exact', choices=['fp32-exact', 'fp32', 'bf16'],
                     help="fp32-exact = IEEE fp32 products everywhere, the reference's training precision (headline); "
-                         'fp32 = fp32 activations with bf16x3-split MFMA operands (~2^-16 per product); bf16 = bf16 '
-                         'GEMM operands')
+                         'fp32 = fp32 activations with bf16x3-split MFMA operands (~2^-16 per product); bf16 = the '
+                         'torch backend under bf16 autocast (no kernel path)')
     ap.add_argument('--bf16x3-extra', type=int, default=1,
                     help='also time the bf16x3-operand fp32 learner (extra field fp32_bf16x3_learner, not the headline)')
     ap.add_argument('--model-5v5-extra', type=int, default=1,

@@ -71,6 +71,7 @@ struct Args {
   int M, N, K, kc, splits, tiles_n, accumulate;
   unsigned* tickets;    // exact kernel, splits > 1: per-tile arrival counters (self-cleaning) — the last workgroup of a
                         // tile sums its slabs in split order (no separate reduce launch); nullptr: gemm_tn_reduce
+  int xcd_remap;        // tile_split(): XCD-aware id map (default; DCA_GEMM_XCD=0: the plain map, A/B)
 };
 
 struct Rsrc {
@@ -225,6 +226,20 @@ __device__ __forceinline__ bf16x8 frag_tr(const char* img, int k0, int c0) {
   return f;
 }
 
+// XCD-aware (tile, split) of this workgroup (1-D grid of tiles × splits). Workgroups are dispatched round-robin over
+// the 8 XCDs (each with its own L2): with the plain id → (tile, split) map the M-tiles of one K split — which read the
+// SAME B rows (the 5v5 ∂W_qkv: 3 M-tiles over 716 800 × 128 fp32 Xn rows) and, for wide outputs, the same A rows —
+// land on different XCDs and each fetch them from HBM. The bijective remap (q = n/8, r = n%8) gives every XCD a
+// contiguous id range, so a split's tiles run side by side on one XCD and share its L2.
+__device__ __forceinline__ void tile_split(const Args& a, int& tile, int& split) {
+  const int tiles = ((a.M + BM - 1) / BM) * a.tiles_n;
+  const int n = gridDim.x, orig = blockIdx.x;
+  const int q = n >> 3, r = n & 7, x = orig & 7;
+  const int id = a.xcd_remap ? (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (orig >> 3) : orig;
+  tile = id % tiles;
+  split = id / tiles;
+}
+
 template <bool F32>
 __global__ __launch_bounds__(kThreads) void gemm_tn_kernel(Args a) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -233,7 +248,8 @@ __global__ __launch_bounds__(kThreads) void gemm_tn_kernel(Args a) {
 #define AS(b) (smem + (b) * kTileBytes)
 #define BS(b) (smem + (2 + (b)) * kTileBytes)
 #define SF(b) (smem + (b) * 4 * kImgF32)
-  const int tile = blockIdx.x, split = blockIdx.y;
+  int tile, split;
+  tile_split(a, tile, split);
   const int tm = tile / a.tiles_n, tn = tile % a.tiles_n;
   const int m_base = tm * BM, n_base = tn * BN;
   const int k_lo = split * a.kc, k_hi = min(a.K, k_lo + a.kc);
@@ -444,7 +460,8 @@ __device__ __forceinline__ void add_slab_colsum(float (&cs)[4], float (&cc)[4], 
 
 __global__ __launch_bounds__(kThreads, 2) void gemm_tn_exact_kernel(Args a) {
   __shared__ __attribute__((aligned(16))) char smem[4 * kXImg];   // [stage][A image | B image], 72 KB
-  const int tile = blockIdx.x, split = blockIdx.y;
+  int tile, split;
+  tile_split(a, tile, split);
   const int tm = tile / a.tiles_n, tn = tile % a.tiles_n;
   const int m_base = tm * BM, n_base = tn * BN;
   const int k_lo = split * a.kc, k_hi = min(a.K, k_lo + a.kc);
@@ -735,11 +752,13 @@ extern "C" hipError_t dca_gemm_tn(const void* A, int lda, const void* B, int ldb
     tickets = fold_tickets(tiles);
     if (tickets == nullptr) return hipErrorOutOfMemory;
   }
+  static const int xcd_remap = [] { const char* e = getenv("DCA_GEMM_XCD"); return (e && e[0] == '0') ? 0 : 1; }();
   Args a{A, lda, B, ldb, B0 ? B0 : B, B0 ? split_rows : 0, C, ldc, perm, slab, colsum, M, N, K, kc, splits,
-         (N + BN - 1) / BN, accumulate, tickets};
-  if (f32 == 2) hipLaunchKernelGGL(gemm_tn_exact_kernel, dim3(tiles, splits), dim3(kThreads), 0, st, a);
-  else if (f32) hipLaunchKernelGGL(gemm_tn_kernel<true>, dim3(tiles, splits), dim3(kThreads), 8 * kImgF32, st, a);
-  else hipLaunchKernelGGL(gemm_tn_kernel<false>, dim3(tiles, splits), dim3(kThreads), 4 * kTileBytes, st, a);
+         (N + BN - 1) / BN, accumulate, tickets, xcd_remap};
+  const dim3 grid(tiles * splits);                          // 1-D: tile_split() maps it XCD-aware
+  if (f32 == 2) hipLaunchKernelGGL(gemm_tn_exact_kernel, grid, dim3(kThreads), 0, st, a);
+  else if (f32) hipLaunchKernelGGL(gemm_tn_kernel<true>, grid, dim3(kThreads), 8 * kImgF32, st, a);
+  else hipLaunchKernelGGL(gemm_tn_kernel<false>, grid, dim3(kThreads), 4 * kTileBytes, st, a);
   DCA_CHECK_LAUNCH();
   if (splits > 1 && tickets == nullptr) {
     int lp = 0;

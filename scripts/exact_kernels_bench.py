@@ -1,5 +1,6 @@
 """Standalone timings of the IEEE-fp32 learner's MFMA kernels at the deploy shape (lstm512, B·S = 11 200 rows):
-encoder forward / backward (exact), forward chain, ∂X chain, heads stages, and the four weight-gradient TN GEMMs.
+encoder forward / backward (exact), forward chain, ∂X chain, heads stages, the four weight-gradient TN GEMMs and the
+5v5 attention block's two (K = 716 800).
 python scripts/exact_kernels_bench.py [iters]"""
 import sys
 
@@ -62,3 +63,10 @@ for nm, (a, b) in {'dW_hh (2048x512)': (dG, hs), 'dW_ih (2048x256)': (dG, x), 'd
     out = torch.empty(a.shape[1], b.shape[1], device=dev)
     timeit(f'gemm_tn exact {nm}', lambda: gemm_tn(a, b, out=out, exact=True), 2 * N * a.shape[1] * b.shape[1])
     timeit(f'gemm_tn bf16x3 {nm}', lambda: gemm_tn(a, b, out=out))
+# the 5v5 attention weight gradients: K = 716 800 unit rows (11 200 timesteps × 64 slots), skinny outputs
+R5 = N * 64
+dqkv, xn, o5, de1 = r(R5, 384), r(R5, 128), r(R5, 128), r(R5, 128)
+for nm, (a, b) in {'dW_qkv 5v5 (384x128, K=716800)': (dqkv, xn), 'dW_out 5v5 (128x128, K=716800)': (de1, o5)}.items():
+    out = torch.empty(a.shape[1], b.shape[1], device=dev)
+    timeit(f'gemm_tn exact {nm}', lambda: gemm_tn(a, b, out=out, exact=True), 2 * R5 * a.shape[1] * b.shape[1])
+    timeit(f'gemm_tn bf16x3 {nm}', lambda: gemm_tn(a, b, out=out), 2 * R5 * a.shape[1] * b.shape[1])
