@@ -2,7 +2,7 @@
 # of the bench, plain map (DCA_GEMM_XCD=0) vs remap on the same box; the GEMM / exact-mode GPU tests
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread -m gpu tests/test_exact_mode.py \
+timeout -k 10 300 python -u -m pytest -x -v -s --timeout 240 --timeout-method thread -m gpu tests/test_exact_mode.py \
   tests/test_fp32_kernels.py > gpurun_out/r6h_gpu_tests.log 2>&1 || exit $?
 DCA_GEMM_XCD=0 timeout -k 10 300 python -u scripts/exact_kernels_bench.py 10 > gpurun_out/r6h_kernels_plain.txt 2>&1 || exit $?
 timeout -k 10 300 python -u scripts/exact_kernels_bench.py 10 > gpurun_out/r6h_kernels_xcd.txt 2>&1 || exit $?
