@@ -230,6 +230,11 @@ class WeightImages:
 #   tensor errors against float64 as libm expf / tanhf (PPO 2.50e-6 both), 0.5 ms per step faster.
 
 
+# 5v5: ∂W_out on the main stream after the encoder backward, ∂W_qkv alone on the recurrence stream (A/B knob, round 6:
+# both GEMMs serial on the recurrence stream left ∂W_qkv exposed at the step's end, profiles/r5_5v5_exact_timeline.txt)
+_WG_BALANCE = os.environ.get('DCA_5V5_WG_BALANCE', '1') == '1'
+
+
 def fused_step_tm(fp, *args, **kw):
     """:func:`_fused_step_tm`: every product on a hand-written kernel (no torch GEMM, so no matmul mode to pin)."""
     return _fused_step_tm(fp, *args, **kw)
@@ -573,7 +578,13 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             dgam, dbet, dbt_attn = lnsum[:128], lnsum[128:256], lnsum[256:].view(6, 128)
             dbout = torch.empty(128, device=dev)
             dbqkv = torch.empty(384, device=dev)
-            if wg_side:
+            if wg_side and _WG_BALANCE:
+                # ∂W_qkv (the larger: 384 × 128 over the N·U rows) alone on the recurrence stream from the attention
+                # backward on; ∂W_out on the main stream after the encoder backward — the two streams' tails balance
+                sL.wait_stream(main)
+                side_after.append(lambda: gemm_tn(dQKV, Xn, out=dWqkv, colsum=dbqkv))
+                after_enc.append(lambda: gemm_tn(dE1, Oat, out=dWout, colsum=dbout))
+            elif wg_side:
                 # enqueued AFTER the encoder backward below (side_after): issued here, the graph ran the two GEMMs
                 # (156 + 401 µs) and then the encoder backward strictly one after the other
                 sL.wait_stream(main)

@@ -1,5 +1,6 @@
-# round 6 (h): XCD-aware (tile, split) map in the split-K TN GEMM — standalone kernel timings and the learner sections
-# of the bench, plain map (DCA_GEMM_XCD=0) vs remap on the same box; the GEMM / exact-mode GPU tests
+# round 6 (h): XCD-aware (tile, split) map in the split-K TN GEMM (DCA_GEMM_XCD) and the balanced 5v5 weight-gradient
+# streams (DCA_5V5_WG_BALANCE) — standalone kernel timings and the learner sections of the bench, on one box,
+# baseline (both off) first and last; the GEMM / exact-mode GPU tests (with the 5v5 worst-tensor print)
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -v -s --timeout 240 --timeout-method thread -m gpu tests/test_exact_mode.py \
@@ -7,8 +8,8 @@ timeout -k 10 300 python -u -m pytest -x -v -s --timeout 240 --timeout-method th
 DCA_GEMM_XCD=0 timeout -k 10 300 python -u scripts/exact_kernels_bench.py 10 > gpurun_out/r6h_kernels_plain.txt 2>&1 || exit $?
 timeout -k 10 300 python -u scripts/exact_kernels_bench.py 10 > gpurun_out/r6h_kernels_xcd.txt 2>&1 || exit $?
 B="--actor 0 --e2e 0 --league-replay-extra 0 --e2e-5v5-extra 0"
-DCA_GEMM_XCD=0 timeout -k 10 400 python -u bench.py $B > gpurun_out/r6h_bench_plain.json 2> gpurun_out/r6h_bench_plain.err || exit $?
-timeout -k 10 400 python -u bench.py $B > gpurun_out/r6h_bench_xcd.json 2> gpurun_out/r6h_bench_xcd.err || exit $?
-DCA_GEMM_XCD=0 timeout -k 10 400 python -u bench.py $B > gpurun_out/r6h_bench_plain2.json 2> gpurun_out/r6h_bench_plain2.err || exit $?
-timeout -k 10 400 python -u bench.py $B > gpurun_out/r6h_bench_xcd2.json 2> gpurun_out/r6h_bench_xcd2.err || exit $?
+run() {  # name xcd balance
+  DCA_GEMM_XCD=$2 DCA_5V5_WG_BALANCE=$3 timeout -k 10 400 python -u bench.py $B > gpurun_out/r6h_bench_$1.json 2> gpurun_out/r6h_bench_$1.err
+}
+run base 0 0 && run xcd 1 0 && run both 1 1 && run bal 0 1 && run base2 0 0 && run both2 1 1 || exit $?
 echo done
