@@ -108,8 +108,10 @@ class GpuActorPolicy:
         self.graph: Optional[torch.cuda.CUDAGraph] = None
 
     # ------------------------------------------------------------------------------------------------
-    # staged input dtypes (Fp8ActorPolicy stages compact fp16 features / int32 handles)
+    # staged input dtypes (Fp8ActorPolicy stages compact fp16 features / int32 handles); words per staged raw record
+    # (Fp8ActorPolicy: the 16-byte form, features/raw.py pack_raw16)
     UNITS_DTYPE, HANDLES_DTYPE = torch.float32, torch.long
+    RAW_WORDS = 8
 
     def _alloc(self, inputs_from=None):
         if self.raw:
@@ -127,7 +129,7 @@ class GpuActorPolicy:
     def _alloc_raw(self, inputs_from):
         n, U, dev = self.n, self.U, self.device
         self.in_pack = _Pack([('env', (n, 3), torch.float32), ('hero', (n, 4), torch.float32),
-                              ('raw', (n, U, 8), torch.int32), ('keep', (n, 1), torch.float32),
+                              ('raw', (n, U, self.RAW_WORDS), torch.int32), ('keep', (n, 1), torch.float32),
                               ('active', (n,), torch.float32)], dev)
         if inputs_from is not None:
             if (inputs_from.n, inputs_from.U) != (n, U) or not inputs_from.raw:
@@ -444,9 +446,13 @@ class GpuActorPolicy:
         self.h_handles.copy_(torch.from_numpy(np.ascontiguousarray(handles)))
 
     def stage_raw(self, env: np.ndarray, hero: np.ndarray, raw: np.ndarray):
-        """Copy (n,3) env, (n,4) hero and (n,U,8) int32 raw unit records (features/raw.py) into the staging buffers."""
+        """Copy (n,3) env, (n,4) hero and (n,U,8) int32 raw unit records (features/raw.py) into the staging buffers
+        (a 16-byte-record policy also takes (n,U,4) records as they are)."""
         if not self.raw:
             raise RuntimeError('stage_raw: this policy stages features (stage)')
+        if self.RAW_WORDS == 4 and raw.shape[-1] == 8:
+            from ..features.raw import pack_raw16
+            raw = pack_raw16(raw)
         self.h_env.copy_(torch.from_numpy(np.ascontiguousarray(env)))
         self.h_hero.copy_(torch.from_numpy(np.ascontiguousarray(hero)))
         self.h_raw.copy_(torch.from_numpy(np.ascontiguousarray(raw)))
@@ -493,7 +499,10 @@ class Fp8ActorPolicy(GpuActorPolicy):
     instead of 6.6 + 1.3 MB — the copies were 57 % of the bf16 step), read by the kernels as they are (the encoder
     converts the fp16 features in LDS, the sampler tests int32 handles).
     The host-side buffers keep the :class:`GpuActorPolicy` API (``h_units`` / ``h_handles`` numpy views assign with
-    a cast). ``compact=False`` keeps fp32 / int64 host buffers (the native VecEnv writes those in place: VecActor).
+    a cast). ``compact=False`` keeps fp32 / int64 host buffers. ``raw=True`` (VecActor's default): 16-byte raw unit
+    records — position, height, facing and the health ratio as binary16, flags, handle; 16 B per unit slot against
+    32 B for the fp32 / bf16 steps' records — featurized to fp16 by the step's first kernel (``featurize_raw16_kernel``);
+    the engine keeps the full records for the learner.
     1v1 LSTM policies with hidden 512 / pre-RNN 256 (the kernel's shape)."""
 
     def __init__(self, policy: Policy, n_slots: int, device='cuda', compact: bool = True, **kw):
@@ -502,6 +511,8 @@ class Fp8ActorPolicy(GpuActorPolicy):
             raise ValueError('Fp8ActorPolicy: 1v1 LSTM policy with hidden 512, pre-RNN 256')
         self.compact = bool(compact)
         super().__init__(policy, n_slots, device=device, **kw)
+
+    RAW_WORDS = 4            # raw staging: the 16-byte records (binary16 fields; the step's features are fp16)
 
     def _alloc(self, inputs_from=None):
         if self.compact or self.raw:

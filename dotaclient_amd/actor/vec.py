@@ -249,7 +249,9 @@ class VecActor:
     def _observe_and_launch(self, g: _Group):
         reset = g.ve.begin_step()
         self._assign_opponents(g, reset)
-        if g.raw:
+        if g.raw and g.gp.RAW_WORDS == 4:        # fp8 step: the 16-byte records staged, the full ones kept
+            need = g.ve.observe_raw16(g.env, g.hero, g.rawbuf, g.handles, g.active)
+        elif g.raw:
             need = g.ve.observe_raw(g.env, g.hero, g.rawbuf, g.handles, g.active)
         else:
             need = g.ve.observe(g.env, g.units, g.handles, g.active)

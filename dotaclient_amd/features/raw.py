@@ -113,3 +113,44 @@ def featurize_raw_np(raw: np.ndarray, hero: np.ndarray) -> Tuple[np.ndarray, np.
     units[~present] = 0.0
     handles = np.where(present, raw[..., 5].astype(np.int64), -1)
     return units, handles
+
+
+# ---- the 16-byte record of the fp8 policy step (its features are fp16): x | y, z | facing, (1 − hp) | flags as
+# binary16 pairs, then the handle (native/core.h raw_to_raw16, ops/csrc/featurize.hip featurize_raw16_kernel)
+RAW16_WORDS = 4
+
+
+def pack_raw16(raw: np.ndarray) -> np.ndarray:
+    """(…, U, 8) int32 raw records → (…, U, 4) int32 16-byte records (float → binary16 round to nearest even)."""
+    raw = np.ascontiguousarray(raw, dtype=np.int32)
+    f16 = raw.view(np.float32)[..., :5].astype(np.float16).view(np.uint16).astype(np.uint32)
+    out = np.empty(raw.shape[:-1] + (RAW16_WORDS,), np.uint32)
+    out[..., 0] = f16[..., 0] | (f16[..., 1] << 16)
+    out[..., 1] = f16[..., 2] | (f16[..., 3] << 16)
+    out[..., 2] = f16[..., 4] | ((raw[..., 6].astype(np.uint32) & 0xFFFF) << 16)
+    out[..., 3] = raw[..., 5].view(np.uint32)
+    return out.view(np.int32)
+
+
+def featurize_raw16_np(raw16: np.ndarray, hero: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """Numpy oracle of ``featurize_raw16_kernel`` (fp32 arithmetic, one fp16 rounding per feature): → units (…, U, 10)
+    fp16, handles (…, U) int32."""
+    w = np.asarray(raw16).view(np.uint32)
+    half = lambda v: v.astype(np.uint16).view(np.float16).astype(np.float32)   # noqa: E731
+    x, y = half(w[..., 0] & 0xFFFF), half(w[..., 0] >> 16)
+    z, facing = half(w[..., 1] & 0xFFFF), half(w[..., 1] >> 16)
+    rel, flags = half(w[..., 2] & 0xFFFF), (w[..., 2] >> 16).astype(np.int32)
+    hero = np.asarray(hero, np.float32)[..., None, :]
+    dx, dy = hero[..., 0] - x, hero[..., 1] - y
+    dist = np.sqrt(dx * dx + dy * dy)
+    ang = facing * np.float32(2.0 * 3.14159265358979) / np.float32(360.0)
+    one, h = np.float32(1.0), np.float32(0.5)
+    units = np.stack([rel, x / np.float32(7000.0), y / np.float32(7000.0), z / np.float32(512.0) - h,
+                      dist / np.float32(7000.0) - h, np.sin(ang), np.cos(ang),
+                      np.where(dist <= hero[..., 2], one, np.float32(0.0)) - h,
+                      np.where(flags & F_ATTACKS_ME, one, np.float32(0.0)) - h,
+                      np.where(flags & F_ME_ATTACKING, one, np.float32(0.0)) - h], -1).astype(np.float16)
+    present = (flags & F_PRESENT) != 0
+    units[~present] = 0
+    handles = np.where(present, w[..., 3].view(np.int32), -1).astype(np.int32)
+    return units, handles

@@ -345,6 +345,44 @@ void unit_rows_raw(const std::vector<const Unit*>& list, const Unit& hero, bool 
   }
 }
 
+// IEEE binary16 of a float, round to nearest even (the F16C / numpy astype(float16) result; no F16C dependency)
+inline uint16_t f32_to_f16(float f) {
+  uint32_t x;
+  std::memcpy(&x, &f, 4);
+  const uint32_t sign = (x >> 16) & 0x8000u;
+  const uint32_t ax = x & 0x7fffffffu;
+  if (ax >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (ax > 0x7f800000u ? 0x200u : 0u));   // inf / nan
+  if (ax >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);                                       // overflow → inf
+  if (ax < 0x38800000u) {                                                                          // subnormal / 0
+    if (ax < 0x33000000u) return (uint16_t)sign;
+    const uint32_t m = (ax & 0x7fffffu) | 0x800000u;
+    const int e = (int)(ax >> 23);
+    const int shift = 126 - e;                      // 14..24
+    uint32_t h = m >> (shift);
+    const uint32_t rem = m & ((1u << shift) - 1u), half = 1u << (shift - 1);
+    if (rem > half || (rem == half && (h & 1u))) ++h;
+    return (uint16_t)(sign | h);
+  }
+  uint32_t h = ((ax - 0x38000000u) >> 13);
+  const uint32_t rem = ax & 0x1fffu;
+  if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;
+  return (uint16_t)(sign | h);
+}
+
+// 16-byte form of a raw record for the fp8 policy step (its features are fp16 anyway): x | y, z | facing, 1 − hp |
+// flags as binary16 pairs, then the handle (ops/csrc/featurize.hip featurize_raw16_kernel, features/raw.py pack_raw16)
+constexpr int kRaw16Words = 4;
+inline void raw_to_raw16(const int32_t* r, int U, int32_t* o) {
+  for (int u = 0; u < U; ++u, r += kRawWords, o += kRaw16Words) {
+    float f[5];
+    std::memcpy(f, r, sizeof(f));
+    o[0] = (int32_t)((uint32_t)f32_to_f16(f[0]) | ((uint32_t)f32_to_f16(f[1]) << 16));
+    o[1] = (int32_t)((uint32_t)f32_to_f16(f[2]) | ((uint32_t)f32_to_f16(f[3]) << 16));
+    o[2] = (int32_t)((uint32_t)f32_to_f16(f[4]) | ((uint32_t)(r[6] & 0xffff) << 16));
+    o[3] = r[5];
+  }
+}
+
 // raw form of featurize_one: env (3), hero (4), raw (U, 8) and the host's handles (U) (the action decoder's targets)
 int featurize_one_raw(const World& w, int player_id, int team_id, const int* counts, float* env, float* hero4,
                       int32_t* raw, int64_t* handles) {

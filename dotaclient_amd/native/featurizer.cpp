@@ -286,6 +286,21 @@ class PyVecEnv {
     }
     return py::array_t<int32_t>((py::ssize_t)need.size(), need.data());
   }
+  py::array_t<int32_t> observe_raw16(py::array env, py::array hero, py::array raw16, py::array handles,
+                                     py::array active) {
+    if (!env_.raw()) throw std::invalid_argument("observe_raw16: the VecEnv was not created with raw=True");
+    float* e = checked<float>(env, {S_, 3}, "env", true);
+    float* hr = checked<float>(hero, {S_, 4}, "hero", true);
+    int32_t* r = checked<int32_t>(raw16, {S_, U_, kRaw16Words}, "raw16", true);
+    int64_t* h = checked<int64_t>(handles, {S_, U_}, "handles", true);
+    uint8_t* a = checked<uint8_t>(active, {S_}, "active", true);
+    std::vector<int> need;
+    {
+      py::gil_scoped_release rel;
+      need = env_.observe_raw16(e, hr, r, h, a);
+    }
+    return py::array_t<int32_t>((py::ssize_t)need.size(), need.data());
+  }
   py::array_t<int32_t> observe(py::array env, py::array units, py::array handles, py::array active) {
     if (env_.raw()) throw std::invalid_argument("observe: the VecEnv was created with raw=True (use observe_raw)");
     float* e = checked<float>(env, {S_, 3}, "env", true);
@@ -613,6 +628,15 @@ PYBIND11_MODULE(_native, m) {
         "featurize_batch's raw form for GPU featurization: returns env, hero, raw (N,U,8) int32, handles, "
         "n_allied_creep");
   m.attr("RAW_WORDS") = kRawWords;
+  m.def("pack_raw16", [](py::array_t<int32_t, py::array::c_style> raw) {
+    if (raw.ndim() < 1 || raw.shape(raw.ndim() - 1) != kRawWords) throw std::invalid_argument("pack_raw16: (..., 8)");
+    std::vector<py::ssize_t> shape(raw.shape(), raw.shape() + raw.ndim());
+    shape.back() = kRaw16Words;
+    py::array_t<int32_t> out(shape);
+    const py::ssize_t n = raw.size() / kRawWords;
+    raw_to_raw16(raw.data(), (int)n, out.mutable_data());
+    return out;
+  }, py::arg("raw"), "the 16-byte (binary16) form of raw unit records (fp8 policy step staging)");
   m.def("crc32c", &crc32c);
   m.def("copy_jobs", &copy_jobs, py::arg("jobs"), py::arg("threads") = 4,
         "memcpy a (n, 3) int64 job list of (dst address, src address, bytes) on `threads` threads (GIL released)");
@@ -634,6 +658,8 @@ PYBIND11_MODULE(_native, m) {
       .def("observe", &PyVecEnv::observe, py::arg("env"), py::arg("units"), py::arg("handles"), py::arg("active"))
       .def("observe_raw", &PyVecEnv::observe_raw, py::arg("env"), py::arg("hero"), py::arg("raw"), py::arg("handles"),
            py::arg("active"))
+      .def("observe_raw16", &PyVecEnv::observe_raw16, py::arg("env"), py::arg("hero"), py::arg("raw16"),
+           py::arg("handles"), py::arg("active"))
       .def_property_readonly("raw", [](const PyVecEnv& e) { return e.raw(); })
       .def("act", &PyVecEnv::act, py::arg("idx"), py::arg("act"), py::arg("msk"), py::arg("logp"), py::arg("value"),
            py::arg("hidden"), py::arg("hidden_slots"), py::arg("handles"), py::arg("weight_version"))

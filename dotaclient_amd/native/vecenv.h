@@ -963,7 +963,8 @@ class VecEnv {
   // returns the slots whose trajectory records an LSTM state this step (hidden_stride)
   std::vector<int> observe(float* env, float* units, int64_t* handles, uint8_t* active) {
     std::vector<std::vector<int>> need(cfg_.n_games);
-    pool_.run(cfg_.n_games, [&](int gi) { observe_game(gi, env, units, nullptr, nullptr, handles, active, need[gi]); });
+    pool_.run(cfg_.n_games,
+              [&](int gi) { observe_game(gi, env, units, nullptr, nullptr, nullptr, handles, active, need[gi]); });
     std::vector<int> out;
     for (auto& v : need) out.insert(out.end(), v.begin(), v.end());
     return out;
@@ -971,7 +972,18 @@ class VecEnv {
   // raw mode: env (slots, 3), hero (slots, 4), raw (slots, U, 8) and the host's handles (slots, U) (action targets)
   std::vector<int> observe_raw(float* env, float* hero, int32_t* raw, int64_t* handles, uint8_t* active) {
     std::vector<std::vector<int>> need(cfg_.n_games);
-    pool_.run(cfg_.n_games, [&](int gi) { observe_game(gi, env, nullptr, hero, raw, handles, active, need[gi]); });
+    pool_.run(cfg_.n_games,
+              [&](int gi) { observe_game(gi, env, nullptr, hero, raw, nullptr, handles, active, need[gi]); });
+    std::vector<int> out;
+    for (auto& v : need) out.insert(out.end(), v.begin(), v.end());
+    return out;
+  }
+  // raw mode, fp8 policy step: the staged records in their 16-byte form (raw16 (slots, U, 4)); the trajectories keep
+  // the full records (the learner's exact features)
+  std::vector<int> observe_raw16(float* env, float* hero, int32_t* raw16, int64_t* handles, uint8_t* active) {
+    std::vector<std::vector<int>> need(cfg_.n_games);
+    pool_.run(cfg_.n_games,
+              [&](int gi) { observe_game(gi, env, nullptr, hero, nullptr, raw16, handles, active, need[gi]); });
     std::vector<int> out;
     for (auto& v : need) out.insert(out.end(), v.begin(), v.end());
     return out;
@@ -1089,8 +1101,8 @@ class VecEnv {
     }
   }
 
-  void observe_game(int gi, float* env, float* units, float* hero, int32_t* raw, int64_t* handles, uint8_t* active,
-                    std::vector<int>& need) {
+  void observe_game(int gi, float* env, float* units, float* hero, int32_t* raw, int32_t* raw16, int64_t* handles,
+                    uint8_t* active, std::vector<int>& need) {
     VGame& g = games_[gi];
     for (VPlayer& p : g.players) {
       active[p.slot] = 0;
@@ -1142,9 +1154,17 @@ class VecEnv {
       p.rewarded = true;
       const int slot = p.slot;
       if (cfg_.raw) {
-        int32_t* rr = raw + (size_t)slot * U_ * kRawWords;
+        thread_local std::vector<int32_t> scratch;
+        int32_t* rr;
+        if (raw16) {
+          scratch.resize((size_t)U_ * kRawWords);
+          rr = scratch.data();
+        } else {
+          rr = raw + (size_t)slot * U_ * kRawWords;
+        }
         featurize_one_raw(w[ti], p.player_id, p.team, cfg_.counts, env + 3 * (size_t)slot, hero + 4 * (size_t)slot,
                           rr, handles + (size_t)slot * U_);
+        if (raw16) raw_to_raw16(rr, U_, raw16 + (size_t)slot * U_ * kRaw16Words);
         // keep the raw records for the trajectory (their 32-bit words; the learner featurizes them on the GPU)
         const float* rf = reinterpret_cast<const float*>(rr);
         p.traj.units.insert(p.traj.units.end(), rf, rf + (size_t)U_ * kRawWords);

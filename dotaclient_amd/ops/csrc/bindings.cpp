@@ -770,7 +770,8 @@ void featurize_raw(torch::Tensor raw, torch::Tensor hero, torch::Tensor units, c
   CHECK_DEV(raw); CHECK_CONTIG(raw); CHECK_DT(raw, at::kInt);
   CHECK_F32(hero);
   CHECK_DEV(units); CHECK_CONTIG(units);
-  TORCH_CHECK(raw.dim() == 3 && raw.size(2) == 8, "featurize_raw: raw must be (rows, U, 8) int32");
+  TORCH_CHECK(raw.dim() == 3 && (raw.size(2) == 8 || raw.size(2) == 4),
+              "featurize_raw: raw must be (rows, U, 8) int32, or (rows, U, 4) — the 16-byte records (fp16 out)");
   const int64_t rows = raw.size(0), U = raw.size(1);
   TORCH_CHECK(hero.numel() == rows * 4, "featurize_raw: hero must be (rows, 4)");
   TORCH_CHECK(units.numel() == rows * U * 10, "featurize_raw: units must be (rows, U, 10)");
@@ -785,6 +786,13 @@ void featurize_raw(torch::Tensor raw, torch::Tensor hero, torch::Tensor units, c
     hp = handles->data_ptr();
   }
   TORCH_CHECK(rows * U < (int64_t)1 << 31, "featurize_raw: too many unit slots");
+  if (raw.size(2) == 4) {
+    TORCH_CHECK(half, "featurize_raw: 16-byte records featurize to fp16 (+ int32 handles)");
+    hip_check(dca_featurize_raw16(raw.data_ptr(), ptr<float>(hero), units.data_ptr(), hp, (int)rows, (int)U,
+                                  cur_stream()),
+              "dca_featurize_raw16");
+    return;
+  }
   hip_check(dca_featurize_raw(raw.data_ptr(), ptr<float>(hero), units.data_ptr(), hp, (int)rows, (int)U, half ? 1 : 0,
                               cur_stream()),
             "dca_featurize_raw");

@@ -79,9 +79,54 @@ __global__ __launch_bounds__(256) void featurize_raw_kernel(const int4* __restri
   if (handles) handles[i] = (HT)b.y;
 }
 
+// fp8 policy step (its features are fp16): the 16-byte record — x | y, z | facing, (1 − hp) | flags as binary16 pairs,
+// then the handle — featurized in fp32 arithmetic (hero record fp32) and rounded to fp16 once per feature.
+__global__ __launch_bounds__(256) void featurize_raw16_kernel(const int4* __restrict__ raw, const float4* __restrict__ hero,
+                                                             __half* __restrict__ units, int32_t* __restrict__ handles,
+                                                             int rows, int U) {
+#pragma clang fp contract(off)
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)rows * U) return;
+  const int4 r = raw[i];
+  const int flags = (int)((unsigned)r.z >> 16);
+  __half* o = units + i * 10;
+  if (!(flags & 1)) {
+#pragma unroll
+    for (int k = 0; k < 10; ++k) o[k] = __float2half_rn(0.f);
+    if (handles) handles[i] = -1;
+    return;
+  }
+  auto lo = [](int w) { return __half2float(__ushort_as_half((unsigned short)((unsigned)w & 0xffffu))); };
+  auto hi = [](int w) { return __half2float(__ushort_as_half((unsigned short)((unsigned)w >> 16))); };
+  const float4 h = hero[i / U];
+  const float x = lo(r.x), y = hi(r.x), z = lo(r.y), facing = hi(r.y);
+  const float dx = h.x - x, dy = h.y - y;
+  const float dist = sqrtf(dx * dx + dy * dy);
+  float sf, cf;
+  sincosf(facing * (2.f * 3.14159265358979f) / 360.f, &sf, &cf);
+  const float f[10] = {lo(r.z), x / 7000.f, y / 7000.f, z / 512.f - 0.5f, dist / 7000.f - 0.5f, sf, cf,
+                       (dist <= h.z ? 1.f : 0.f) - 0.5f, ((flags >> 1) & 1 ? 1.f : 0.f) - 0.5f,
+                       ((flags >> 2) & 1 ? 1.f : 0.f) - 0.5f};
+#pragma unroll
+  for (int k = 0; k < 10; ++k) o[k] = __float2half_rn(f[k]);
+  if (handles) handles[i] = r.w;
+}
+
 }  // namespace
 
 // half_out: fp16 features + int32 handles; else fp32 features + int64 handles
+// 16-byte records (rows, U, 4) → fp16 features + int32 handles (may be null)
+extern "C" hipError_t dca_featurize_raw16(const void* raw16, const float* hero, void* units, void* handles, int rows,
+                                          int U, hipStream_t st) {
+  const long n = (long)rows * U;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(featurize_raw16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     static_cast<const int4*>(raw16), reinterpret_cast<const float4*>(hero),
+                     static_cast<__half*>(units), static_cast<int32_t*>(handles), rows, U);
+  DCA_CHECK_LAUNCH();
+  return hipSuccess;
+}
+
 extern "C" hipError_t dca_featurize_raw(const void* raw, const float* hero, void* units, void* handles, int rows, int U,
                                         int half_out, hipStream_t st) {
   const long n = (long)rows * U;

@@ -106,6 +106,8 @@ hipError_t dca_occupy_xcd(int xcd, int blocks, double seconds, int* seen, hipStr
 // half_out: fp16 features / int32 handles, else fp32 / int64 (featurize.hip)
 hipError_t dca_featurize_raw(const void* raw, const float* hero, void* units, void* handles, int rows, int U,
                              int half_out, hipStream_t st);
+hipError_t dca_featurize_raw16(const void* raw16, const float* hero, void* units, void* handles, int rows, int U,
+                               hipStream_t st);
 hipError_t dca_loss_assemble(const float* part, int nrows, const float* norms, int N, int algo, float ent_coef,
                              float vf_coef, float* out, int S, int vbug, hipStream_t st);
 hipError_t dca_weight_prep(const float* src, const int* map16, short* dst16, int n16, const int* map32, float* dst32,

@@ -5,6 +5,11 @@ set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest -x -v -s --timeout 240 --timeout-method thread -m gpu tests/test_exact_mode.py \
   tests/test_fp32_kernels.py > gpurun_out/r6h_gpu_tests.log 2>&1 || exit $?
+timeout -k 10 300 python -u -m pytest -x -v --timeout 240 --timeout-method thread -m gpu tests/test_gpu_featurize.py \
+  tests/test_vec_actor.py > gpurun_out/r6h_gpu_tests_featurize.log 2>&1 || exit $?
+for P in bf16 fp8; do
+  timeout -k 10 300 python -u scripts/actor_bench.py 2048 $P > gpurun_out/r6h_actor_$P.json 2>&1 || exit $?
+done
 DCA_GEMM_XCD=0 timeout -k 10 300 python -u scripts/exact_kernels_bench.py 10 > gpurun_out/r6h_kernels_plain.txt 2>&1 || exit $?
 timeout -k 10 300 python -u scripts/exact_kernels_bench.py 10 > gpurun_out/r6h_kernels_xcd.txt 2>&1 || exit $?
 B="--actor 0 --e2e 0 --league-replay-extra 0 --e2e-5v5-extra 0"

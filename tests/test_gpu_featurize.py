@@ -243,7 +243,8 @@ def test_ingest_featurizes_raw_rollouts_on_gpu(gpu_ops):
 def test_raw_staged_actor_step_equals_feature_staged(gpu_ops, preset, precision):
     """The actor step fed raw unit records (featurized by the step's first kernel) returns exactly what the step fed
     the host featurizer's features returns — sampled actions, log-probs, values, recurrent state — so the IEEE-fp32
-    actor's log-probs keep their 1e-5 bound against torch fp32 (tests/test_actor_gpu.py) on GPU features."""
+    actor's log-probs keep their 1e-5 bound against torch fp32 (tests/test_actor_gpu.py) on GPU features. (fp8: the
+    16-byte records, within the fp16 features' quantisation.)"""
     from dotaclient_amd.actor.batched import _synthetic_states, make_slot_policy
     from dotaclient_amd.models.policy import Policy, get_config
     torch.manual_seed(3)
@@ -276,6 +277,83 @@ def test_raw_staged_actor_step_equals_feature_staged(gpu_ops, preset, precision)
             reset[::3] = True
         oa = a.step(env, units, handles, reset=reset)
         ob = b.step_raw(env, hero, raw, reset=reset)
+        if precision == 'fp8':
+            # the fp8 step stages the 16-byte records (binary16 fields, fp32 arithmetic): features within its fp16
+            # quantisation of the exact ones, so the same actions nearly everywhere and log-probs at fp8 tolerance
+            same = (ob['idx'] == oa['idx']).all(1)
+            assert same.mean() >= 0.9, (step, same.mean())
+            assert np.abs(ob['logp'][same] - oa['logp'][same]).mean() < 2e-2
+            continue
         for k in ('idx', 'logp', 'value', 'actions', 'masks'):
             np.testing.assert_array_equal(ob[k], oa[k], err_msg=f'{k} step {step}')
         assert torch.equal(a.hidden()[0], b.hidden()[0])
+
+
+def test_pack_raw16_native_equals_numpy():
+    from dotaclient_amd.features.raw import pack_raw16
+    from dotaclient_amd.native import _native as N
+    blobs, pids, tids = _batch(get_1v1_selfplay_config, {TEAM_RADIANT: [0], TEAM_DIRE: [5]})
+    _, hero, raw, _, _ = native.featurize_batch_raw(blobs, pids, tids, list(LAYOUT_1V1.counts), 4)
+    a, b = N.pack_raw16(raw), pack_raw16(raw)
+    np.testing.assert_array_equal(a, b)
+    f = np.random.default_rng(0).standard_normal((4096, 8)).astype(np.float32) * np.float32(3e4)
+    f[:8] = [[0.0, -0.0, 6e-8, 1e-5, 65504.0, 65520.0, np.inf, 1.0]] * 8    # subnormal / overflow edges
+    r = f.view(np.int32)
+    np.testing.assert_array_equal(N.pack_raw16(r), pack_raw16(r))
+
+
+def test_vecenv_raw16_staging_matches_raw_records():
+    """observe_raw16 stages the 16-byte form of exactly the records observe_raw writes, and keeps the full records in
+    the trajectories (the learner's exact features): the published rollouts are identical."""
+    from dotaclient_amd.features.raw import pack_raw16
+    from dotaclient_amd.native import _native as N
+    from dotaclient_amd.transport.codec import decode
+    U = LAYOUT_1V1.max_units
+    out = {}
+    for mode in ('raw', 'raw16'):
+        ve = N.VecEnv(4, mode=0, seed=5, max_dota_time=30.0, rollout_size=25, counts=list(LAYOUT_1V1.counts),
+                      threads=2, raw=True)
+        S, A = ve.slots, 21 + U
+        env, hero = np.zeros((S, 3), np.float32), np.zeros((S, 4), np.float32)
+        buf = np.zeros((S, U, 8 if mode == 'raw' else 4), np.int32)
+        handles, active = np.full((S, U), -1, np.int64), np.zeros(S, np.uint8)
+        rng = np.random.default_rng(5)
+        staged, rolls = [], []
+        for _ in range(80):
+            ve.begin_step()
+            getattr(ve, 'observe_' + mode)(env, hero, buf, handles, active)
+            staged.append(buf.copy())
+            idx = np.zeros((S, 4), np.int32)
+            idx[:, 0] = rng.integers(0, 2, S)
+            idx[:, 1:3] = rng.integers(0, 9, (S, 2))
+            ve.act(idx, np.zeros((S, A), np.uint8), np.ones((S, A), np.uint8), np.zeros(S, np.float32),
+                   np.zeros(S, np.float32), None, None, handles, 0)
+            rolls += [decode(b) for b in ve.pop_rollouts()]
+        rolls.sort(key=lambda r: (r.game_id, r.team_id, r.player_id))
+        out[mode] = staged, rolls
+    for a, b in zip(out['raw'][0], out['raw16'][0]):
+        np.testing.assert_array_equal(pack_raw16(a), b)
+    assert len(out['raw'][1]) == len(out['raw16'][1]) > 4
+    for a, b in zip(out['raw'][1], out['raw16'][1]):
+        np.testing.assert_array_equal(a.units_raw, b.units_raw)
+
+
+@pytest.mark.gpu
+def test_featurize_raw16_kernel_matches_numpy(gpu_ops):
+    from dotaclient_amd.features.raw import featurize_raw16_np, pack_raw16
+    blobs, pids, tids = _batch(get_1v1_selfplay_config, {TEAM_RADIANT: [0], TEAM_DIRE: [5]})
+    env, hero, raw, handles, _ = native.featurize_batch_raw(blobs, pids, tids, list(LAYOUT_1V1.counts), 4)
+    r16 = pack_raw16(raw)
+    want_u, want_h = featurize_raw16_np(r16, hero)
+    u = torch.empty(raw.shape[:2] + (10,), dtype=torch.float16, device='cuda')
+    h = torch.empty(raw.shape[:2], dtype=torch.int32, device='cuda')
+    gpu_ops.featurize_raw(torch.from_numpy(r16).cuda(), torch.from_numpy(hero).cuda(), u, h)
+    got = u.cpu().numpy()
+    np.testing.assert_array_equal(h.cpu().numpy(), want_h)
+    np.testing.assert_array_equal(want_h, handles.astype(np.int32))
+    # fp32 sinf / cosf may differ from numpy's by an ulp: at most one fp16 step on a handful of entries
+    d = np.abs(got.astype(np.float32) - want_u.astype(np.float32))
+    assert d.max() <= 2e-3 and (d > 0).mean() < 1e-3, (d.max(), (d > 0).mean())
+    # against the exact features: the fp16 path's quantisation only
+    exact, _ = featurize_raw_np(raw, hero)
+    assert np.abs(got.astype(np.float32) - exact).max() < 1e-2
