@@ -702,8 +702,11 @@ extern "C" void dca_gemm_tn_plan(int M, int N, int K, int* splits, int* kc, int*
   // ≈1.5 workgroups per CU; exact: ≈2 (MFMA-bound at 1/16 of the bf16 rate, two 64 KB workgroups fit a CU)
   // (exact workgroup target swept in round 4, learner step, two passes each: 256 → 5.55, 512 → 5.48, 768 → 5.53,
   // 1024 → 5.59 ms; profiles/r4_gemm_tn_target_sweep.txt)
+  // (round 6: the split count is rounded DOWN — t·s never exceeds the target: with 2 workgroups per CU the exact
+  // kernel's 512 slots hold the whole grid, where ceil(512 / t) left a straggler round for a handful of workgroups,
+  // e.g. the 5v5 ∂W_qkv at t = 3 → 513 workgroups took 984 µs, twice its per-workgroup time; 1v1 ∂W_pre t = 14 → 518)
   const int target = f32 == 2 ? 512 : 384;
-  int s = (target + t - 1) / t;
+  int s = t >= target ? 1 : target / t;
   const int kmax = (K + bk - 1) / bk;                     // at least one K slab per split
   if (s > kmax) s = kmax;
   if (s < 1) s = 1;
