@@ -9,5 +9,5 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 240 --timeout-method threa
 timeout -k 10 300 python -u scripts/exact_kernels_bench.py 10 > gpurun_out/r6g_kernels.txt 2>&1 || exit $?
 timeout -k 10 1000 python -u scripts/learning_curve.py --model 5v5 --mode 5v5 --eval-precision fp32 --actor-precision fp32 \
   --games 400 --budget 720 --eval-every 90 --eval-games 128 --snapshot-lags 120,300,600 --snapshot-games 64 \
-  --log-dir gpurun_out/r6_curve5v5_ckpt --out gpurun_out/r6_curve_5v5.jsonl > gpurun_out/r6_curve_5v5.log 2>&1
+  --log-dir /tmp/r6_curve5v5_ckpt --out gpurun_out/r6_curve_5v5.jsonl > gpurun_out/r6_curve_5v5.log 2>&1
 echo "curve rc=$?"
