@@ -212,6 +212,14 @@ def decode(buf: bytes, crc_checked: bool = False) -> Rollout:
     mv = memoryview(buf)
     for name, dt, shape, off, n in header['arrays']:
         arrays[name] = np.frombuffer(mv[base + off: base + off + n], dtype=np.dtype(dt)).reshape(shape)
+    if arrays.get('units') is None:
+        # a raw rollout (GPU featurization): the records and the hero rows must both be there, in their layout
+        ur, hr = arrays.get('units_raw'), arrays.get('hero')
+        if ur is None or hr is None:
+            raise CorruptMessage('experience message without units (or units_raw + hero)')
+        if (ur.dtype != np.int32 or ur.ndim != 3 or ur.shape[2] != 8 or hr.dtype != np.float32
+                or hr.shape != (ur.shape[0], 4)):
+            raise CorruptMessage(f'bad raw unit records {ur.dtype}{ur.shape} / hero {hr.dtype}{hr.shape}')
     return Rollout(game_id=header['game_id'], team_id=header['team_id'], player_id=header['player_id'],
                    weight_version=header['weight_version'], bootstrap_value=header['bootstrap_value'],
                    hidden_stride=header.get('hidden_stride', 0),

@@ -357,3 +357,18 @@ def test_featurize_raw16_kernel_matches_numpy(gpu_ops):
     # against the exact features: the fp16 path's quantisation only
     exact, _ = featurize_raw_np(raw, hero)
     assert np.abs(got.astype(np.float32) - exact).max() < 1e-2
+
+
+def test_decode_rejects_incomplete_raw_rollouts():
+    from dotaclient_amd.transport.codec import CorruptMessage, decode, encode
+    r = _raw_rollout(6, 11)
+    back = decode(encode(r))
+    np.testing.assert_array_equal(back.units_raw, r.units_raw)
+    np.testing.assert_array_equal(back.hero, r.hero)
+    r.hero = None
+    with pytest.raises(CorruptMessage):
+        decode(encode(r))
+    r = _raw_rollout(6, 11)
+    r.units_raw = r.units_raw[:, :, :6].copy()
+    with pytest.raises(CorruptMessage):
+        decode(encode(r))
