@@ -20,10 +20,9 @@ EVERY rank (one actor runtime per GPU), and reported as node aggregates (sums ov
 
 * ``actor.steps_per_s`` — player-steps/s of the whole self-play runtime (actor/vec.py), ``actor.policy_step_per_s``
   the batched GPU policy step alone (raw unit records staged and featurized on the GPU, the runtime's path;
-  ``policy_step_host_features_per_s``: fed host features instead), one policy stepped copy → kernels → copy, and
-  ``policy_step_pipelined_per_s`` two policies alternating (the runtime's two groups: one's SDMA copies beside the
-  other's kernels); ``actor.policy_step_fp8_per_s`` the same step on the e4m3 MFMA kernel (BASELINE config 5,
-  actor/batched.py Fp8ActorPolicy) and ``actor.fp8_vs_bf16_policy_step`` (``_pipelined``) their ratio;
+  ``policy_step_host_features_per_s``: fed host features instead), copy → kernels → copy one step at a time;
+  ``actor.policy_step_fp8_per_s`` the same step on the e4m3 MFMA kernel (BASELINE config 5, actor/batched.py
+  Fp8ActorPolicy, 16-byte raw records) and ``actor.fp8_vs_bf16_policy_step`` their ratio;
 * ``e2e`` — the reference's node topology run for real (learner/e2e.py ``measure_e2e_node``): one experience queue
   per node fed by one actor process per GPU, WORLD_SIZE learner ranks consuming disjoint rollouts (DDP over RCCL),
   rank 0 alone publishing the model. ``e2e.steps_per_s`` is the reference's own metric (optimizer.py:485-486, padded
@@ -439,7 +438,6 @@ def main():
             from dotaclient_amd.actor.batched import measure_actor_throughput
             mb = measure_actor_throughput(policy, device, n_games=args.actor_games, threads=args.actor_threads)
             mine['policy_step_per_s'] = mb['gpu_steps_per_s']
-            mine['policy_step_pipelined_per_s'] = mb['gpu_pipelined_steps_per_s']
             mine['policy_step_protobuf_featurize_per_s'] = mb['steps_per_s']
             # the same step fed host features (40 B fp32 + an 8 B handle per unit slot) instead of raw unit records
             # (32 B) featurized on the GPU (ops/csrc/featurize.hip) — the pre-round-6 staging
@@ -456,13 +454,9 @@ def main():
             mb = measure_actor_throughput(policy, device, n_games=args.actor_games, threads=args.actor_threads,
                                           precision='fp8')
             mine['policy_step_fp8_per_s'] = mb['gpu_steps_per_s']
-            mine['policy_step_fp8_pipelined_per_s'] = mb['gpu_pipelined_steps_per_s']
             mine['policy_step_fp8_protobuf_featurize_per_s'] = mb['steps_per_s']
             if mine.get('policy_step_per_s'):
                 mine['fp8_vs_bf16_policy_step'] = mb['gpu_steps_per_s'] / mine['policy_step_per_s']
-            if mine.get('policy_step_pipelined_per_s'):
-                mine['fp8_vs_bf16_policy_step_pipelined'] = (mb['gpu_pipelined_steps_per_s']
-                                                             / mine['policy_step_pipelined_per_s'])
         except Exception as e:
             mine['policy_step_fp8_error'] = repr(e)
         if not cfg.entity_attention:
@@ -472,7 +466,6 @@ def main():
                 mb = measure_actor_throughput(policy, device, n_games=args.actor_games, threads=args.actor_threads,
                                               precision='fp32')
                 mine['policy_step_fp32_per_s'] = mb['gpu_steps_per_s']
-                mine['policy_step_fp32_pipelined_per_s'] = mb['gpu_pipelined_steps_per_s']
                 mine['policy_step_fp32_protobuf_featurize_per_s'] = mb['steps_per_s']
             except Exception as e:
                 mine['policy_step_fp32_error'] = repr(e)
@@ -480,7 +473,6 @@ def main():
         progress('actor measurements done')
         actor = dict(ranks[0])
         for k in ('steps_per_s', 'steps_per_s_fp32', 'protobuf_runtime_steps_per_s', 'policy_step_per_s',
-                  'policy_step_pipelined_per_s', 'policy_step_fp8_pipelined_per_s', 'policy_step_fp32_pipelined_per_s',
                   'policy_step_host_features_per_s', 'policy_step_host_features_protobuf_featurize_per_s',
                   'policy_step_protobuf_featurize_per_s', 'policy_step_fp8_per_s',
                   'policy_step_fp8_protobuf_featurize_per_s', 'policy_step_fp32_per_s',

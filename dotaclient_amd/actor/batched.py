@@ -691,8 +691,7 @@ def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048,
     and featurizes serialized world states through the native featurizer every step (the reference actor's
     per-step work, agent.py:611-660) overlapped with the previous GPU step; otherwise only the GPU step + copies
     are timed. ``precision='fp8'``: :class:`Fp8ActorPolicy`, ``'fp32'``: :class:`F32ActorPolicy`. Returns ``{'steps_per_s', 'gpu_steps_per_s',
-    'gpu_pipelined_steps_per_s', 'ms_per_step', 'slots'}`` (``gpu_steps_per_s``: one policy, copy → step → copy
-    serially; ``gpu_pipelined_steps_per_s``: two policies alternating as the runtime's two groups do). ``raw``
+    'ms_per_step', 'slots'}`` (``gpu_steps_per_s``: copy → step → copy, one step at a time). ``raw``
     (default, the runtime's path): raw unit records staged and featurized on the GPU (ops/csrc/featurize.hip);
     otherwise host features.
     """
@@ -765,22 +764,4 @@ def measure_actor_throughput(policy: Policy, device='cuda', n_games: int = 2048,
         gp.wait()
         fill(f)
     dt = (time.perf_counter() - t0) / steps
-    # two policies of n slots on their own step streams, launched back to back (VecActor's two software-pipelined
-    # groups): one step's SDMA input / output copies run beside the other's kernels, so the rate is set by the larger
-    # of copy and compute rather than their sum
-    gp2 = cls(policy, n, device=dev, seed=4321, record=True, raw=raw)
-    if raw:
-        gp2.stage_raw(gp.h_env.numpy(), gp.h_hero.numpy(), gp.h_raw.numpy())
-    else:
-        gp2.stage(gp.h_env.numpy(), gp.h_units.numpy(), gp.h_handles.numpy())
-    gp2.step_async(); gp2.wait()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        gp.step_async()
-        gp2.step_async()
-        gp.wait()
-        gp2.wait()
-    pipe_dt = (time.perf_counter() - t0) / steps
-    return {'steps_per_s': n / dt, 'gpu_steps_per_s': n / gpu_dt, 'gpu_pipelined_steps_per_s': 2 * n / pipe_dt,
-            'ms_per_step': dt * 1e3, 'slots': n}
+    return {'steps_per_s': n / dt, 'gpu_steps_per_s': n / gpu_dt, 'ms_per_step': dt * 1e3, 'slots': n}

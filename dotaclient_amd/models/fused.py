@@ -153,11 +153,6 @@ class FusedPolicy:
             self._side = torch.cuda.Stream(device=self.err.device)
         return self._side
 
-    def third_stream(self):
-        if getattr(self, '_third', None) is None:
-            self._third = torch.cuda.Stream(device=self.err.device)
-        return self._third
-
     def use_pipeline(self) -> bool:
         """Whether the kernels cover this configuration (models/pipelined.py): fp32 / fp32-exact, the LSTM policies or
         the reference's linear fake_rnn layer with its VPG value quirk (the compat preset)."""

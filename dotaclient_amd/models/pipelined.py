@@ -232,7 +232,7 @@ class WeightImages:
 
 # 5v5: ∂W_out on the main stream after the encoder backward, ∂W_qkv alone on the recurrence stream (A/B knob, round 6:
 # both GEMMs serial on the recurrence stream left ∂W_qkv exposed at the step's end, profiles/r5_5v5_exact_timeline.txt)
-# ('2': ∂W_out on a third stream instead, concurrent with both)
+# (A third stream for ∂W_out, concurrent with both, measured 0.27 ms slower: profiles/r6_gemm_map_and_5v5_streams.md.)
 _WG_BALANCE = os.environ.get('DCA_5V5_WG_BALANCE', '1')
 
 
@@ -468,8 +468,6 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
     db = dw1 = db1 = dWt = dbt = dWe = dbe = None
     dgam = dbet = None
     side_after: List = []                # side-stream work enqueued after the encoder backward (5v5 fused path)
-    third_after: List = []               # (DCA_5V5_WG_BALANCE=2: third-stream work, likewise)
-    third_done = None
     after_enc: List = []                 # main-stream work enqueued after the encoder backward (exact ∂W_pre)
     if attn:
         dWout = torch.empty(128, 128, device=dev)
@@ -581,13 +579,7 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
             dgam, dbet, dbt_attn = lnsum[:128], lnsum[128:256], lnsum[256:].view(6, 128)
             dbout = torch.empty(128, device=dev)
             dbqkv = torch.empty(384, device=dev)
-            if wg_side and _WG_BALANCE == '2':
-                sL.wait_stream(main)
-                s3 = fp.third_stream()
-                s3.wait_stream(main)
-                side_after.append(lambda: gemm_tn(dQKV, Xn, out=dWqkv, colsum=dbqkv))
-                third_after.append(lambda: gemm_tn(dE1, Oat, out=dWout, colsum=dbout))
-            elif wg_side and _WG_BALANCE == '1':
+            if wg_side and _WG_BALANCE == '1':
                 # ∂W_qkv (the larger: 384 × 128 over the N·U rows) alone on the recurrence stream from the attention
                 # backward on; ∂W_out on the main stream after the encoder backward — the two streams' tails balance
                 sL.wait_stream(main)
@@ -617,14 +609,6 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         dwt_c, dw1_c, db1_c = C.encoder_bwd(units_t[r0:r1], w1, b1, wtT16, dtl[r0:r1], z[r0:r1],
                                             dx896, arg[r0:r1], counts, bool(cfg.compat_bugs), demb_in=demb_in,
                                             exact=exact)
-        if third_after:
-            s3 = fp.third_stream()
-            with torch.cuda.stream(s3):
-                for fn in third_after:
-                    fn()
-                third_done = torch.cuda.Event()
-                third_done.record(s3)
-            third_after.clear()
         for fn in after_enc:
             fn()
         after_enc.clear()
@@ -646,8 +630,6 @@ def _fused_step_tm(fp, W: Dict[str, torch.Tensor], P: Dict[str, torch.Tensor], u
         dbe = _acc(dbe, dbe_c)
     if wg_done is not None:
         main.wait_event(wg_done)
-    if third_done is not None:
-        main.wait_event(third_done)
     if not direct:
         if not lin:
             grads['rnn.weight_hh_l0'] = dWhh
