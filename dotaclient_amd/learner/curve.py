@@ -36,7 +36,8 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
                        latest_weights_prob: float = 0.8, actor_precision: str = 'bf16',
                        replay_gb: float = 0.0, snapshot_lags=(120.0, 300.0, 600.0), snapshot_games: int = 64,
                        old_logp: str = 'actor', league_matrix_n: int = 0,
-                       advantages: str = 'vtrace-step', weight_lag: int = 0) -> List[Dict]:
+                       advantages: str = 'vtrace-step', weight_lag: int = 0,
+                       replay_recent: int = 0) -> List[Dict]:
     """Train for ``budget`` seconds (evaluations excluded) and return the evaluation rows (the first one before
     any training). ``on_row`` is called with every row as it is produced; ``save_model``: path that receives the
     final weights (a reference-format state_dict file). ``eval_precision``: the validation games' policy step.
@@ -48,7 +49,8 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
     BASELINE config 5 as a curve: ``league`` ('pfsp' / 'uniform', actor/league.py) makes the actors play the latest
     weights against sampled past versions (``latest_weights_prob`` of the games self-play the latest), the actor's
     policy step runs at ``actor_precision`` ('fp8' for config 5), and ``replay_gb`` > 0 trains every minibatch from
-    an on-HBM replay of that size (learner/replay.py) instead of the iteration's fresh rollouts."""
+    an on-HBM replay of that size (learner/replay.py) instead of the iteration's fresh rollouts — uniformly over the
+    whole buffer, or over its ``replay_recent`` newest sequences."""
     import json
     import os
 
@@ -74,6 +76,7 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
                           run_local=True,
                           xp_timeout=300.0, histogram_freq=10 ** 9, async_checkpoint=True, prefetch_rollouts=64,
                           pack_sequences=bool(pack), seed=seed, replay_gb=replay_gb, old_logp=old_logp,
+                          replay_recent=int(replay_recent),
                           advantages=advantages)
     opt = DotaOptimizer(cfg, broker)
     ws = WeightStore(model, device='cpu')
@@ -165,7 +168,9 @@ def run_learning_curve(budget: float = 150.0, eval_every: float = 25.0, eval_gam
     try:
         if not resumed:
             evaluate({'t_train': 0.0, 'iteration': 0, 'samples': 0, 'actor_steps': 0, 'model': model,
-                      'precision': precision, 'backend': backend, 'pack': bool(pack)})
+                      'precision': precision, 'backend': backend, 'pack': bool(pack), 'league': league,
+                      'actor_precision': actor_precision, 'replay_gb': replay_gb, 'replay_recent': int(replay_recent),
+                      'advantages': advantages, 'old_logp': old_logp, 'weight_lag': int(weight_lag)})
         th.start()
         next_eval = (int(trained // eval_every) + 1) * eval_every
         while trained < budget:

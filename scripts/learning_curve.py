@@ -38,6 +38,8 @@ def main(argv=None):
     ap.add_argument('--latest-weights-prob', type=float, default=0.8)
     ap.add_argument('--actor-precision', default='bf16', choices=['fp32', 'bf16', 'fp8'])
     ap.add_argument('--replay-gb', type=float, default=0.0, help='on-HBM replay the learner samples from')
+    ap.add_argument('--replay-recent', type=int, default=0,
+                    help='sample the replay\'s newest N sequences only (0 = the whole buffer)')
     ap.add_argument('--device', default='cuda')
     ap.add_argument('--snapshot-lags', default='120,300,600',
                     help='seconds of training: every row also plays the weights from that long ago (comma list, '
@@ -71,7 +73,7 @@ def main(argv=None):
                            actor_precision=a.actor_precision, replay_gb=a.replay_gb,
                            snapshot_lags=tuple(float(x) for x in a.snapshot_lags.split(',') if x.strip()),
                            snapshot_games=a.snapshot_games, old_logp=a.old_logp, advantages=a.advantages,
-                           weight_lag=a.weight_lag,
+                           weight_lag=a.weight_lag, replay_recent=a.replay_recent,
                            league_matrix_n=a.league_matrix)
 
 
