@@ -3,7 +3,7 @@
 # over all experience so far learns the default-bot game slowly)
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 1150 python -u scripts/learning_curve.py --budget 600 --eval-every 75 --eval-games 256 \
+timeout -k 10 900 python -u scripts/learning_curve.py --budget 600 --eval-every 75 --eval-games 256 \
   --league pfsp --latest-weights-prob 0.8 --actor-precision fp8 --replay-gb 100 --replay-recent 4096 \
   --snapshot-lags 120,300,600 --snapshot-games 64 --league-matrix 4 --out gpurun_out/r6_curve_league_recent.jsonl \
   > gpurun_out/r6_curve_league_recent.log 2>&1
