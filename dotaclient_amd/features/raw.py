@@ -121,8 +121,18 @@ RAW16_WORDS = 4
 
 
 def pack_raw16(raw: np.ndarray) -> np.ndarray:
-    """(…, U, 8) int32 raw records → (…, U, 4) int32 16-byte records (float → binary16 round to nearest even)."""
+    """(…, U, 8) int32 raw records → (…, U, 4) int32 16-byte records (float → binary16 round to nearest even; the
+    native converter when built, this numpy form otherwise — equal, tests/test_gpu_featurize.py)."""
     raw = np.ascontiguousarray(raw, dtype=np.int32)
+    try:
+        from ..native import _native
+        return _native.pack_raw16(raw)
+    except (ImportError, AttributeError):
+        pass
+    return _pack_raw16_np(raw)
+
+
+def _pack_raw16_np(raw: np.ndarray) -> np.ndarray:
     f16 = raw.view(np.float32)[..., :5].astype(np.float16).view(np.uint16).astype(np.uint32)
     out = np.empty(raw.shape[:-1] + (RAW16_WORDS,), np.uint32)
     out[..., 0] = f16[..., 0] | (f16[..., 1] << 16)

@@ -290,7 +290,7 @@ def test_raw_staged_actor_step_equals_feature_staged(gpu_ops, preset, precision)
 
 
 def test_pack_raw16_native_equals_numpy():
-    from dotaclient_amd.features.raw import pack_raw16
+    from dotaclient_amd.features.raw import _pack_raw16_np as pack_raw16
     from dotaclient_amd.native import _native as N
     blobs, pids, tids = _batch(get_1v1_selfplay_config, {TEAM_RADIANT: [0], TEAM_DIRE: [5]})
     _, hero, raw, _, _ = native.featurize_batch_raw(blobs, pids, tids, list(LAYOUT_1V1.counts), 4)
