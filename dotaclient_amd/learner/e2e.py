@@ -353,16 +353,29 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
     try:
         # the actor starts first (interpreter + engine + graph capture overlap the learner's construction) and
         # waits for rank 0's model version 0
-        for k in range(K):
-            g_k = games // K + (1 if k < games % K else 0)
-            t_k = max(1, threads // K)
-            proc = ctx.Process(target=_actor_process_main, name=f'e2e-actor-{rank}-{k}', daemon=True,
-                               args=(addr, model, g_k, t_k, seq_len, rollout_size, max_dota_time, str(device),
-                                     11 + 7919 * rank + 104729 * k, stop, readies[k], counters[k], failed,
-                                     f'a{rank}' if K == 1 else f'a{rank}_{k}', league, latest_weights_prob,
-                                     actor_precision))
-            proc.start()
-            procs.append(proc)
+        # DCA_E2E_ACTOR_HW_QUEUES: hardware queues of the actor process only (HIP's GPU_MAX_HW_QUEUES, read by the
+        # spawned interpreter at its runtime init) — fewer queues beside the learner's persistent recurrence (A/B)
+        hwq = os.environ.get('DCA_E2E_ACTOR_HW_QUEUES')
+        saved_hwq = os.environ.get('GPU_MAX_HW_QUEUES')
+        if hwq and 1 <= int(hwq) <= 32:
+            os.environ['GPU_MAX_HW_QUEUES'] = str(int(hwq))
+        try:
+            for k in range(K):
+                g_k = games // K + (1 if k < games % K else 0)
+                t_k = max(1, threads // K)
+                proc = ctx.Process(target=_actor_process_main, name=f'e2e-actor-{rank}-{k}', daemon=True,
+                                   args=(addr, model, g_k, t_k, seq_len, rollout_size, max_dota_time, str(device),
+                                         11 + 7919 * rank + 104729 * k, stop, readies[k], counters[k], failed,
+                                         f'a{rank}' if K == 1 else f'a{rank}_{k}', league, latest_weights_prob,
+                                         actor_precision))
+                proc.start()
+                procs.append(proc)
+        finally:
+            if hwq:
+                if saved_hwq is None:
+                    os.environ.pop('GPU_MAX_HW_QUEUES', None)
+                else:
+                    os.environ['GPU_MAX_HW_QUEUES'] = saved_hwq
         cfg = OptimizerConfig(log_dir=tmp, epochs=epochs, seq_per_epoch=seq_per_epoch, batch_size=batch_size,
                               seq_len=seq_len, model=model, precision=precision, device=str(device),
                               backend=backend, checkpoint_keep=2, run_local=True, xp_timeout=120.0,
