@@ -65,7 +65,11 @@ PRESETS: Dict[str, RunPreset] = {p.name: p for p in [
               bench=dict(model='5v5', batch_size=8, seq_len=1400, precision='fp32'),
               launch=dict(model_preset='5v5', actors=8, games_per_actor=256, actor_device='cuda', optimizers=8)),
     RunPreset('league-replay', 'Self-play league (PFSP opponents) + 200 GB on-HBM replay buffer', 1,
-              optimizer=dict(model_preset='lstm512', precision='fp32-exact', replay_gb=200.0, **_DEPLOY),
+              # (the learner samples the replay's 4 096 newest sequences: uniform sampling over the whole buffer
+              # trained mostly on old games and learned the default-bot game several times slower,
+              # profiles/r6_curve_league{,_recent}.jsonl)
+              optimizer=dict(model_preset='lstm512', precision='fp32-exact', replay_gb=200.0, replay_recent=4096,
+                             **_DEPLOY),
               agent=dict(model_preset='lstm512', device='cuda', games=1024, runtime='vec', rollout_size=9999,
                          max_dota_time=600, league='pfsp', use_latest_weights_prob=0.8, actor_precision='fp8'),
               bench=dict(model='lstm512', batch_size=8, seq_len=1400, precision='fp32-exact', replay=16384),
