@@ -87,6 +87,10 @@ class VecActor:
     every finished rollout straight into a reserved region of that node ring instead (``publish`` is then unused):
     no intermediate string, no Python bytes object built under the GIL, no second copy by a publish call — ≈0.5 ms
     of this process's main thread per whole-game rollout.
+    ``raw`` (default: on with a fused GPU policy step): the engine stages compact raw unit records instead of
+    features (features/raw.py; the fp8 step their 16-byte form), the step's first kernel featurizes them
+    (ops/csrc/featurize.hip), and the rollouts carry the records (``units_raw`` / ``hero``) for the learner's device
+    featurization.
     """
 
     def __init__(self, weight_store, n_games: int, publish: Optional[Callable[[bytes], None]], device='cuda',
