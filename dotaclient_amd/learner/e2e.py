@@ -231,10 +231,12 @@ def _actor_process_main(addr: str, model: str, games: int, threads: int, seq_len
         mode = '5v5' if get_config(model).layout.counts[0] > 1 else '1v1'   # (BASELINE config 4: 5v5 self-play)
         # on the node's shared-memory ring the engine encodes finished rollouts straight into it (VecActor ring_sink)
         sink = br if hasattr(br, 'ring') else None
+        # (DCA_E2E_ACTOR_GROUPS: software-pipelined game groups of the actor, default 2 — A/B of the launch shape)
+        groups = int(os.environ.get('DCA_E2E_ACTOR_GROUPS', '2'))
         va = VecActor(ws, games, br.publish_experience, device=device, mode=mode, seed=seed,
                       rollout_size=rollout_size, max_dota_time=max_dota_time, hidden_stride=seq_len, threads=threads,
                       stagger=True, tag=f'{tag}.vec', league=lg, latest_weights_prob=latest_weights_prob,
-                      precision=precision, ring_sink=sink)   # (game ids unique across the node's actor processes)
+                      precision=precision, ring_sink=sink, groups=groups)   # (game ids unique across the node)
         for _ in range(3):
             va.step()
         ready.set()
