@@ -30,6 +30,8 @@ EVERY rank (one actor runtime per GPU), and reported as node aggregates (sums ov
   reference's ≈1000 steps/s, the like-for-like node-level comparison (``vs_baseline`` is the compute-only learner);
 * ``model_5v5_exact`` — the 5v5 policy at IEEE fp32 (BASELINE config 4 at the reference precision) on the fused
   kernels (the attention block's exact-fp32 twins); ``model_5v5`` is the same step with bf16x3 operands;
+* ``learner_vtrace`` — the headline step with the in-step V-trace (the node loop's default advantages, learner
+  /engine.py); the node loop's learner runs this step;
 * ``bptt350_learner`` — truncated BPTT: each sequence trained as ``seq_len / 350`` chains of 350 steps from
   actor-stored (h, c) (32 sequences of 350 steps per step, at the headline's precision; not the headline);
 * ``learner_b16`` / ``learner_b32`` — the same learner at 16 / 32 sequences per GPU per step (the exact recurrence
@@ -74,6 +76,8 @@ def parse():
                     help="fp32-exact = IEEE fp32 products everywhere, the reference's training precision (headline); "
                          'fp32 = fp32 activations with bf16x3-split MFMA operands (~2^-16 per product); bf16 = the '
                          'torch backend under bf16 autocast (no kernel path)')
+    ap.add_argument('--vtrace-extra', type=int, default=1,
+                    help='also time the headline step with the in-step V-trace (extra field learner_vtrace)')
     ap.add_argument('--bf16x3-extra', type=int, default=1,
                     help='also time the bf16x3-operand fp32 learner (extra field fp32_bf16x3_learner, not the headline)')
     ap.add_argument('--model-5v5-extra', type=int, default=1,
@@ -238,7 +242,7 @@ def main():
     cfg = get_config(args.model)
     trace = os.environ.get('DCA_BENCH_TRACE') == '1'
 
-    def run(precision, cfg=cfg, B=None, S=None, backend=None, steps=None, warmup=None):
+    def run(precision, cfg=cfg, B=None, S=None, backend=None, steps=None, warmup=None, vtrace=False):
         """Build a learner of this precision and time ``args.steps`` DP PPO steps (``B`` sequences of ``S`` steps,
         default the command line's) after ``args.warmup``; returns (elapsed s (max over ranks), loss_first,
         loss_last, learner, policy)."""
@@ -251,13 +255,14 @@ def main():
         backend = backend or args.backend
         if backend == 'auto':
             backend = 'fused' if use_cuda else 'torch'
-        learner = Learner(policy, LossConfig(algo=args.algo), device=device, backend=backend, precision=precision)
+        lc = LossConfig(algo=args.algo, vtrace=True) if vtrace else LossConfig(algo=args.algo)
+        learner = Learner(policy, lc, device=device, backend=backend, precision=precision)
         learner.dp.timing = world > 1       # per-step all-reduce timing events (DataParallel.comm_stats)
         if args.graph == 1 or (args.graph == -1 and learner.backend == 'fused'):
             learner.enable_graph(warmup=1)
         n_pool = args.replay or 4 * B
         replay = DeviceReplay(n_pool, S, cfg.layout, cfg.hidden if cfg.rnn == 'lstm' else None, device,
-                              seed=1000 * rank)
+                              seed=1000 * rank, vtrace=vtrace)
 
         def step():
             t = time.perf_counter()
@@ -316,6 +321,18 @@ def main():
     samples = args.batch_size * args.seq_len * world * args.steps
     value = samples / elapsed
     ms_per_step = elapsed / args.steps * 1e3
+    vtr = None
+    if args.vtrace_extra and args.algo == 'ppo' and use_cuda:
+        # the same step with the in-step V-trace (the node loop's default advantages: every minibatch's advantages and
+        # value targets recomputed from the step's own values / log-probs against the behaviour log-prob)
+        learner = None
+        try:
+            ev, lv0, lv1, _, _ = run(args.precision, vtrace=True)
+            progress(f'learner {args.precision} + in-step V-trace done: {ev / args.steps * 1e3:.3f} ms/step')
+            vtr = {'precision': args.precision, 'advantages': 'vtrace-step', 'value': samples / ev,
+                   'ms_per_step': ev / args.steps * 1e3, 'loss_first': lv0, 'loss_last': lv1}
+        except Exception as e:
+            vtr = {'error': repr(e)}
     bf16x3 = None
     if args.bf16x3_extra and args.precision == 'fp32-exact' and use_cuda:
         learner = None
@@ -609,6 +626,7 @@ def main():
             'model_5v5': model_5v5,
             'model_5v5_exact': model_5v5_exact,
             'bptt350_learner': bptt,
+            'learner_vtrace': vtr,
             'learner_b16': big.get('learner_b16'),
             'learner_b32': big.get('learner_b32'),
             'dp_replicas_identical': len(set(shas)) == 1,
