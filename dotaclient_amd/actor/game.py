@@ -18,7 +18,6 @@ from __future__ import annotations
 
 import logging
 import random
-import time
 import uuid
 from collections import Counter
 from datetime import datetime
@@ -26,7 +25,7 @@ from typing import Callable, Dict, List, NamedTuple, Optional
 
 import numpy as np
 
-from ..constants import (LAYOUT_1V1, OPPOSITE_TEAM, REWARD_KEYS, UnitLayout)
+from ..constants import (LAYOUT_1V1, OPPOSITE_TEAM, UnitLayout)
 from ..features.actions import action_to_pb
 from ..features.featurizer import featurize, get_unit
 from ..features.reward import end_state_reward, get_reward, pack_rewards

@@ -12,7 +12,7 @@ time limit, agent.py:325-337).
 from __future__ import annotations
 
 import time
-from typing import Dict, List, Optional
+from typing import Dict, List
 
 import numpy as np
 

@@ -10,7 +10,6 @@
 """
 from __future__ import annotations
 
-import copy
 import threading
 from collections import deque
 from typing import Optional

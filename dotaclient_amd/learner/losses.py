@@ -17,7 +17,7 @@ functions are its oracle.
 """
 from __future__ import annotations
 
-from typing import Dict, Tuple
+from typing import Dict
 
 import torch
 

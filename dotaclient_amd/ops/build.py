@@ -17,7 +17,6 @@ import glob
 import os
 import shutil
 import subprocess
-import sys
 import sysconfig
 
 HERE = os.path.dirname(os.path.abspath(__file__))

@@ -38,7 +38,7 @@ from typing import Dict, Optional, Tuple
 
 import numpy as np
 
-from ..constants import INPUT_KEYS, LAYOUT_1V1, N_MOVE_ENUMS, REWARD_KEYS, UNIT_KEYS, UnitLayout
+from ..constants import LAYOUT_1V1, UNIT_KEYS, UnitLayout
 
 MAGIC1 = b'DCX1'           # zlib CRC-32 trailer (decode only)
 MAGIC2 = b'DCX2'           # CRC-32C trailer
