@@ -372,3 +372,29 @@ def test_decode_rejects_incomplete_raw_rollouts():
     r.units_raw = r.units_raw[:, :, :6].copy()
     with pytest.raises(CorruptMessage):
         decode(encode(r))
+
+
+def test_optimizer_trains_raw_rollouts_like_featurized_ones(tmp_path):
+    """DotaOptimizer on CPU: an iteration fed raw rollouts (featurized by the learner) ends on exactly the weights of
+    the same iteration fed the host features."""
+    from dotaclient_amd.learner.optimizer import DotaOptimizer, OptimizerConfig
+    from dotaclient_amd.transport.broker import InProcBroker
+    from dotaclient_amd.transport.codec import encode
+    outs = []
+    for raw in (True, False):
+        br = InProcBroker()
+        for i in range(8):
+            r = _raw_rollout(24, 100 + i)
+            r.actions[:] = 0
+            r.actions[:, 0] = 1
+            r.masks[:] = 0
+            r.masks[:, :3] = 1
+            br.publish_experience(encode(r if raw else _featurized(r)))
+        cfg = OptimizerConfig(log_dir=str(tmp_path / f'r{int(raw)}'), model='lstm128', epochs=1, seq_per_epoch=4,
+                              batch_size=2, seq_len=24, device='cpu', xp_timeout=30, seed=3)
+        torch.manual_seed(0)
+        opt = DotaOptimizer(cfg, br)
+        opt.run(iterations=2)
+        outs.append({k: v.detach().clone() for k, v in opt.policy.state_dict().items()})
+    for k in outs[0]:
+        assert torch.equal(outs[0][k], outs[1][k]), k
