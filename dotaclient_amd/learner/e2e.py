@@ -254,6 +254,59 @@ def _actor_process_main(addr: str, model: str, games: int, threads: int, seq_len
             br.close()                  # joins the model subscriber thread
 
 
+def _feeder_process_main(addr: str, model: str, seq_len: int, stop, ready, steps, failed, seed: int = 0):
+    """Diagnostic stand-in for the actor process (DCA_E2E_FEEDER=1): republishes a fixed set of synthetic raw
+    rollouts (random records, whole games of 300-900 steps) into the node's experience queue as fast as the ring takes
+    them, with no GPU work at all — the learner's in-loop step without the actor's kernels beside it."""
+    br = None
+    try:
+        import numpy as np
+        from ..models.policy import get_config
+        from ..transport.codec import Rollout, encode
+        br = open_node_broker(addr, drop_oldest=True)
+        U = get_config(model).layout.max_units
+        A = 21 + U
+        rng = np.random.default_rng(seed)
+        msgs = []
+        for i in range(48):
+            T = int(rng.integers(300, 900))
+            raw = np.zeros((T, U, 8), np.int32)
+            f = raw.view(np.float32)
+            f[..., :2] = rng.uniform(-7000, 7000, (T, U, 2))
+            f[..., 2] = 128.0
+            f[..., 3] = rng.uniform(0, 360, (T, U))
+            f[..., 4] = rng.uniform(0, 1, (T, U))
+            raw[..., 5] = rng.integers(1, 5000, (T, U))
+            raw[..., 6] = np.where(rng.random((T, U)) < 0.4, 1, 0)
+            hero = np.zeros((T, 4), np.float32)
+            hero[:, :2] = rng.uniform(-7000, 7000, (T, 2))
+            hero[:, 2] = 600.0
+            act = np.zeros((T, A), np.uint8)
+            act[np.arange(T), rng.integers(0, 3, T)] = 1
+            msk = np.zeros((T, A), np.uint8)
+            msk[:, :3] = 1
+            r = Rollout(game_id=f'feed{seed}_{i}', team_id=2 + i % 2, player_id=0, weight_version=0,
+                        env=rng.standard_normal((T, 3)).astype(np.float32), units=None, units_raw=raw, hero=hero,
+                        actions=act, masks=msk, rewards=rng.standard_normal((T, 9)) * 0.1,
+                        logp=np.full(T, -1.1, np.float32), values=np.zeros(T, np.float32), done=True)
+            msgs.append((encode(r), T))
+        ready.set()
+        k = 0
+        while not stop.is_set():
+            b, T = msgs[k % len(msgs)]
+            br.publish_experience(b)
+            steps.value += T
+            k += 1
+    except BaseException:
+        import traceback
+        traceback.print_exc()
+        failed.set()
+        ready.set()
+    finally:
+        if br is not None:
+            br.close()
+
+
 def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20.0, games: int = 1024,
                      threads: int = 14, seq_len: int = 1400, batch_size: int = 8, seq_per_epoch: int = 16,
                      epochs: int = 1, precision: str = 'fp32', max_dota_time: float = 600.0,
@@ -362,9 +415,17 @@ def measure_e2e_node(model: str = 'lstm512', device='cuda', duration: float = 20
         if hwq and 1 <= int(hwq) <= 32:
             os.environ['GPU_MAX_HW_QUEUES'] = str(int(hwq))
         try:
+            feeder = os.environ.get('DCA_E2E_FEEDER') == '1'
             for k in range(K):
                 g_k = games // K + (1 if k < games % K else 0)
                 t_k = max(1, threads // K)
+                if feeder:
+                    proc = ctx.Process(target=_feeder_process_main, name=f'e2e-feeder-{rank}-{k}', daemon=True,
+                                       args=(addr, model, seq_len, stop, readies[k], counters[k], failed,
+                                             11 + 7919 * rank + 104729 * k))
+                    proc.start()
+                    procs.append(proc)
+                    continue
                 proc = ctx.Process(target=_actor_process_main, name=f'e2e-actor-{rank}-{k}', daemon=True,
                                    args=(addr, model, g_k, t_k, seq_len, rollout_size, max_dota_time, str(device),
                                          11 + 7919 * rank + 104729 * k, stop, readies[k], counters[k], failed,
