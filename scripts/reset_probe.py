@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Cost of sequence packing inside the exact-fp32 team recurrence: forward / backward per-call time at B = 8, S = 1400,
 H = 512 with no reset tensor, an all-zero one, and the packed node loop's density (≈2 episode starts per row).
-python scripts/reset_probe.py [reps]"""
+python scripts/reset_probe.py [reps] [path/to/_C.so — A/B against another build of the extension]"""
 import json
 import sys
 import time
@@ -26,6 +26,11 @@ def _time(fn, reps):
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     C = ops.require()
+    if len(sys.argv) > 2:
+        import importlib.util
+        spec = importlib.util.spec_from_file_location('dotaclient_amd.ops._C', sys.argv[2])
+        C = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(C)
     dev = 'cuda'
     B, S, H = 8, 1400, 512
     torch.manual_seed(0)
