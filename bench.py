@@ -220,6 +220,11 @@ def main():
     # device stalls had a cause in this code — the league's high-priority actor streams preempting the persistent
     # recurrence, fixed (profiles/r5_replay_timeout.md) — so a stall now fails the section loudly instead of deflating
     # its number; every node-loop section reports its slowest in-loop learner step (learner_gpu_ms_per_step_max)
+    if shared:
+        # (rehearsal only: every rank's processes time-slice one device, so a rank's recurrence can be switched out
+        # for longer than the 2 s hand-off deadline — measured: a two-rank shared run failing with a backward hand-off
+        # timeout — the 60 s deadline applies; the driver's one-rank-per-GPU runs keep 2 s)
+        os.environ.setdefault('DCA_TEAM_PATIENT', '1')
     device = torch.device(f'cuda:{0 if shared else local}' if use_cuda else 'cpu')
     if use_cuda:
         torch.cuda.set_device(device)
