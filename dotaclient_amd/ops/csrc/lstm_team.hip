@@ -812,14 +812,12 @@ __device__ __forceinline__ void lstm_team_bwd_body(
       // ---- prefetch the saved activations of step t for the owned pairs
       dca::f32x4 gv[NPAIR];
       float cv[NPAIR], cpv[NPAIR], dv[NPAIR];
-      // packing: episode starts at t (c_{t-1} unused) / at t+1 (h_t unused by t+1). Raw flag bytes, compared at
-      // their use after the gather (see the forward: a compare here waits out the load before the gather).
-      int rcur[NPAIR], rnext[NPAIR];
+      bool rcur[NPAIR], rnext[NPAIR];     // packing: episode starts at t (c_{t-1} unused) / at t+1 (h_t unused by t+1)
       if (t >= 0) {
 #pragma unroll
         for (int i = 0; i < NPAIR; ++i) {
           const int pi = tid + NT * i;
-          rcur[i] = rnext[i] = 0;
+          rcur[i] = rnext[i] = false;
           if (pi < B * U) {
             const int b = pi / U, u = pi % U;
             const size_t bt = (size_t)(b0 + b) * sb + (size_t)t * st;
@@ -828,8 +826,8 @@ __device__ __forceinline__ void lstm_team_bwd_body(
             cpv[i] = t > 0 ? cs[(bt - st) * H + j0 + u] : c0[(size_t)(b0 + b) * H + j0 + u];
             dv[i] = dhs[bt * H + j0 + u];
             if (rst != nullptr) {
-              rcur[i] = rst[bt];
-              if (t + 1 < S) rnext[i] = rst[bt + st];
+              rcur[i] = rst[bt] != 0;
+              rnext[i] = t + 1 < S && rst[bt + st] != 0;
             }
           }
         }
