@@ -728,6 +728,13 @@ __device__ __forceinline__ void lstm_team_bwd_body(
   __shared__ float dbs[RB * U * 4];     // per-(row, unit, gate) bias-gradient sums of a chain
   __shared__ int sh_int;
   __shared__ unsigned sh_epoch;
+  // packing: the chain's episode-start flags as a bit image (row b, step t → bit t of rbits[b·wpr + t/32]), built
+  // once per chain. Byte loads of the flags at every step — two per owned pair, compared where they were issued —
+  // measured +0.32 ms per B = 8, S = 1400 backward call on some boxes (1921 → 2244 µs, scripts/reset_probe.py);
+  // chains with more than kRstWords·32 (row, step) flags read them from global memory as before (so do the half-team
+  // variants, whose LDS is full).
+  constexpr int kRstWords = (VAR & 16) ? 1 : 2048;
+  __shared__ unsigned rbits[kRstWords];
 
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int me = join_team(ctl, err, &sh_int, &sh_epoch, TS);
@@ -735,6 +742,7 @@ __device__ __forceinline__ void lstm_team_bwd_body(
   if (me < 0) return;
   const int team = me >> 6, m = me & 63;
   const int j0 = m * U;
+  const int wpr = (S + 31) >> 5;        // flag words per row
   // 16-B chunks per (row, unit): bf16 {d_i,d_f | tag | d_g,d_o | tag}; F32 {d_i, tag, d_f, tag} {d_g, tag, d_o, tag}
   constexpr int CPU_ = F32 ? 2 : 1;
   i32x4* xg = xg_all + (size_t)team * 2 * Bc * H * CPU_;
@@ -795,6 +803,19 @@ __device__ __forceinline__ void lstm_team_bwd_body(
     const int b0 = chain * Bc;
     const int B = min(Bc, Btot - b0);
     const unsigned tagbase = make_tagbase(epoch, iter);
+    const bool rl = rst != nullptr && B * wpr <= kRstWords;    // flags from the LDS bit image
+    if (rl) {
+      for (int w = tid; w < B * wpr; w += NT) {
+        const int b = w / wpr, tb = (w - b * wpr) * 32;
+        const unsigned char* fr = rst + (size_t)(b0 + b) * sb;
+        unsigned v = 0;
+#pragma unroll
+        for (int j = 0; j < 32; ++j)
+          if (tb + j < S) v |= (fr[(size_t)(tb + j) * st] != 0 ? 1u : 0u) << j;
+        rbits[w] = v;
+      }
+      lds_barrier();
+    }
     float dcarry[NPAIR];
     dca::f32x4 dsum[NPAIR];               // Σ_t ∂gates of the owned pairs (bias gradient)
 #pragma unroll
@@ -825,7 +846,11 @@ __device__ __forceinline__ void lstm_team_bwd_body(
             cv[i] = cs[bt * H + j0 + u];
             cpv[i] = t > 0 ? cs[(bt - st) * H + j0 + u] : c0[(size_t)(b0 + b) * H + j0 + u];
             dv[i] = dhs[bt * H + j0 + u];
-            if (rst != nullptr) {
+            if (rl) {
+              const unsigned* rw = rbits + b * wpr;
+              rcur[i] = (rw[t >> 5] >> (t & 31)) & 1u;
+              rnext[i] = t + 1 < S && ((rw[(t + 1) >> 5] >> ((t + 1) & 31)) & 1u);
+            } else if (rst != nullptr) {
               rcur[i] = rst[bt] != 0;
               rnext[i] = t + 1 < S && rst[bt + st] != 0;
             }
